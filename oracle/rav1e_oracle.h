@@ -1,0 +1,119 @@
+/*
+ * rav1e_oracle.h -- CPU restatement of the rav1e encode hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the parity checker for the
+ * MI355X product path (rav1e_amd/, include/rav1e_hip.h).  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it; the
+ * product never links, calls or falls back to it.
+ *
+ * Every function restates a reference function of geobacter-rs/rav1e
+ * (/root/reference); the file:line each one follows is cited next to its
+ * definition.  Parity pins ("Oracle"):
+ *   - SAD / SATD: the 88 known-answer values of src/dist.rs:379-460;
+ *   - 1-D and 2-D transforms: golden vectors produced by evaluating the
+ *     reference's own transform source (tools/refeval/, tests/golden/);
+ *   - MC put/prep/avg: restated from src/mc.rs:213-408 (no KATs exist in
+ *     the reference: "parity unpinned" beyond the restatement itself).
+ *
+ * Conventions: pixel buffers are `const void*` + stride in ELEMENTS + an
+ * `hbd` flag (0 = u8, 1 = u16), mirroring the generated-kernel ABI of the
+ * reference (build/kernel/gen/dist.rs:132-139).  All i32 arithmetic wraps
+ * (Rust release semantics).
+ */
+#ifndef RAV1E_ORACLE_H
+#define RAV1E_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- distortion (src/dist.rs, src/rdo.rs) ---------------------------- */
+uint32_t orc_get_sad(const void *org, ptrdiff_t org_stride, const void *ref,
+                     ptrdiff_t ref_stride, int w, int h, int hbd);
+/* emulate_gen: 0 = get_satd_ref (src/dist.rs:197-328);
+ *              1 = generated i16-lane kernel (build/kernel/gen/dist.rs:173-357) */
+uint32_t orc_get_satd(const void *org, ptrdiff_t org_stride, const void *ref,
+                      ptrdiff_t ref_stride, int w, int h, int hbd,
+                      int emulate_gen);
+/* sse_wxh raw partials (src/rdo.rs:286-335): one u64 per importance
+ * sub-block, raster order, (w/bw)*(h/bh) values, bw = min(8,w)>>xdec. */
+int orc_sse_wxh(const void *a, ptrdiff_t sa, const void *b, ptrdiff_t sb,
+                int w, int h, int xdec, int ydec, int hbd, uint64_t *out);
+/* cdef_dist_wxh_8x8 integer moments (src/rdo.rs:219-253):
+ * out[0]=sum_s out[1]=sum_d out[2]=sum_s2 out[3]=sum_d2 out[4]=sum_sd */
+void orc_cdef_moments_8x8(const void *a, ptrdiff_t sa, const void *b,
+                          ptrdiff_t sb, int hbd, int64_t out[5]);
+/* f64 tail of cdef_dist_wxh_8x8 (src/rdo.rs:242-252) */
+uint64_t orc_cdef_dist_from_moments(const int64_t m[5], int bit_depth);
+
+/* ---- motion compensation (src/mc.rs) ---------------------------------- */
+/* src points at the block's integer position; reads rows -3..h+4 and
+ * columns -3..w+4 around it (src/mc.rs:232, 251, 273).
+ * emulate_gen: 1 = generated u8 kernels' missing upper clamp
+ * (build/kernel/gen/mc.rs:253-261, 281-290, 337-344). */
+void orc_put_8tap(void *dst, ptrdiff_t dst_stride, const void *src,
+                  ptrdiff_t src_stride, int w, int h, int col_frac,
+                  int row_frac, int mode_x, int mode_y, int bit_depth,
+                  int hbd, int emulate_gen);
+void orc_prep_8tap(int16_t *tmp, const void *src, ptrdiff_t src_stride, int w,
+                   int h, int col_frac, int row_frac, int mode_x, int mode_y,
+                   int bit_depth, int hbd);
+void orc_mc_avg(void *dst, ptrdiff_t dst_stride, const int16_t *tmp1,
+                const int16_t *tmp2, int w, int h, int bit_depth, int hbd,
+                int emulate_gen);
+/* SUBPEL_FILTERS + get_filter (src/mc.rs:70-179, 201-210) */
+const int32_t *orc_get_filter(int mode, int frac, int length);
+
+/* ---- transforms (src/transform/) -------------------------------------- */
+/* 1-D kernel ids: 0 = Id, 1 = Dct, 2 = Adst, 3 = FlipAdst (TBL_IDX order,
+ * src/transform/mod.rs:158-173). Return 0 on success, -1 if the reference
+ * leaves the (kind, n) pair unimplemented. */
+int orc_fwd_txfm1d(int kind, int n, const int32_t *in, int32_t *out);
+int orc_inv_txfm1d(int kind, int n, const int32_t *in, int32_t *out,
+                   int range);
+/* tx_size: TxSize enum order (src/transform/mod.rs:225-247);
+ * tx_type: TxType enum order (src/transform/mod.rs:123-140).
+ * forward: FwdTxfm2D::fht (src/transform/forward.rs:1804-1899); output is a
+ * W-stride raster of W*H i32. */
+int orc_fwd_txfm2d(const int16_t *residual, int32_t *coeffs, int tx_size,
+                   int tx_type, int bit_depth);
+/* inverse + add: NativeInvTxfm2D (src/transform/inverse.rs:1939-2114);
+ * coeffs are min(W,32)*min(H,32) i32, row stride min(W,32). */
+int orc_inv_txfm2d_add(const int32_t *coeffs, void *dst, ptrdiff_t dst_stride,
+                       int tx_size, int tx_type, int bit_depth, int hbd);
+/* diff (src/encoder.rs:1044-1058) */
+void orc_diff(int16_t *dst, const void *a, ptrdiff_t sa, const void *b,
+              ptrdiff_t sb, int w, int h, int hbd);
+
+/* ---- motion search (src/me.rs) ---------------------------------------- */
+typedef struct { int16_t row, col; } orc_mv;
+uint32_t orc_get_mv_rate(orc_mv a, orc_mv b, int allow_hp);
+/* full_search (src/me.rs:943-990). org/ref point at plane (0,0) (the data
+ * origin); x/y in pixels relative to it; may be negative (padding). */
+void orc_full_search(const void *org, ptrdiff_t org_stride, const void *ref,
+                     ptrdiff_t ref_stride, int hbd, int po_x, int po_y,
+                     int x_lo, int x_hi, int y_lo, int y_hi, int blk_w,
+                     int blk_h, int step, uint32_t lambda, orc_mv pmv0,
+                     orc_mv pmv1, int allow_hp, orc_mv *best_mv,
+                     uint64_t *lowest_cost);
+
+/* ---- frame layout (src/frame/) --------------------------------------- */
+/* Plane::new geometry (src/frame/plane.rs:215-244). Writes
+ * {stride, alloc_height, xorigin, yorigin}. */
+void orc_plane_geometry(int width, int height, int xpad, int ypad, int hbd,
+                        int out[4]);
+/* Plane::pad (src/frame/plane.rs:269-314) on a buffer of stride*alloc_h */
+void orc_plane_pad(void *data, int stride, int alloc_height, int xorigin,
+                   int yorigin, int xdec, int ydec, int w, int h, int hbd);
+/* Plane::downsample_from (src/frame/plane.rs:399-423); both pointers at
+ * their plane's data origin. */
+void orc_downsample(void *dst, ptrdiff_t dst_stride, int dst_w, int dst_h,
+                    const void *src, ptrdiff_t src_stride, int hbd);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

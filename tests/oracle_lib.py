@@ -1,0 +1,178 @@
+"""ctypes binding of the CPU oracle (oracle/), for tests only.
+
+The oracle is the parity checker; nothing in the product imports this.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+_LIB = os.path.join(ROOT, "oracle", "build", "librav1e_oracle.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = C.CDLL(_LIB)
+        vp, sz, i32 = C.c_void_p, C.c_ssize_t, C.c_int
+        L.orc_get_sad.restype = C.c_uint32
+        L.orc_get_sad.argtypes = [vp, sz, vp, sz, i32, i32, i32]
+        L.orc_get_satd.restype = C.c_uint32
+        L.orc_get_satd.argtypes = [vp, sz, vp, sz, i32, i32, i32, i32]
+        L.orc_sse_wxh.restype = i32
+        L.orc_sse_wxh.argtypes = [vp, sz, vp, sz, i32, i32, i32, i32, i32, vp]
+        L.orc_cdef_moments_8x8.argtypes = [vp, sz, vp, sz, i32, vp]
+        L.orc_cdef_dist_from_moments.restype = C.c_uint64
+        L.orc_cdef_dist_from_moments.argtypes = [vp, i32]
+        L.orc_put_8tap.argtypes = [vp, sz, vp, sz] + [i32] * 9
+        L.orc_prep_8tap.argtypes = [vp, vp, sz] + [i32] * 8
+        L.orc_mc_avg.argtypes = [vp, sz, vp, vp] + [i32] * 5
+        L.orc_fwd_txfm1d.restype = i32
+        L.orc_fwd_txfm1d.argtypes = [i32, i32, vp, vp]
+        L.orc_inv_txfm1d.restype = i32
+        L.orc_inv_txfm1d.argtypes = [i32, i32, vp, vp, i32]
+        L.orc_fwd_txfm2d.restype = i32
+        L.orc_fwd_txfm2d.argtypes = [vp, vp, i32, i32, i32]
+        L.orc_inv_txfm2d_add.restype = i32
+        L.orc_inv_txfm2d_add.argtypes = [vp, vp, sz, i32, i32, i32, i32]
+        L.orc_diff.argtypes = [vp, vp, sz, vp, sz, i32, i32, i32]
+        L.orc_plane_geometry.argtypes = [i32] * 5 + [vp]
+        L.orc_plane_pad.argtypes = [vp] + [i32] * 9
+        L.orc_downsample.argtypes = [vp, sz, i32, i32, vp, sz, i32]
+        L.orc_get_mv_rate.restype = C.c_uint32
+        _lib = L
+    return _lib
+
+
+def ptr(a, offset=0):
+    """Pointer to element `offset` (flat, in elements) of a numpy array."""
+    return C.c_void_p(a.ctypes.data + offset * a.itemsize)
+
+
+def hbd_of(a):
+    return 1 if a.dtype == np.uint16 else 0
+
+
+# ---- thin wrappers (arrays are 2-D numpy, regions addressed by (y, x)) ----
+def get_sad(org, oy, ox, ref, ry, rx, w, h):
+    L = lib()
+    return L.orc_get_sad(ptr(org, oy * org.shape[1] + ox), org.shape[1],
+                         ptr(ref, ry * ref.shape[1] + rx), ref.shape[1], w, h, hbd_of(org))
+
+
+def get_satd(org, oy, ox, ref, ry, rx, w, h, emulate_gen=0):
+    L = lib()
+    return L.orc_get_satd(ptr(org, oy * org.shape[1] + ox), org.shape[1],
+                          ptr(ref, ry * ref.shape[1] + rx), ref.shape[1], w, h,
+                          hbd_of(org), emulate_gen)
+
+
+def put_8tap(src, sy, sx, w, h, col_frac, row_frac, mode_x=0, mode_y=0, bd=8, emulate_gen=0):
+    dst = np.zeros((h, w), dtype=src.dtype)
+    lib().orc_put_8tap(ptr(dst), w, ptr(src, sy * src.shape[1] + sx), src.shape[1], w, h,
+                       col_frac, row_frac, mode_x, mode_y, bd, hbd_of(src), emulate_gen)
+    return dst
+
+
+def prep_8tap(src, sy, sx, w, h, col_frac, row_frac, mode_x=0, mode_y=0, bd=8):
+    tmp = np.zeros((h, w), dtype=np.int16)
+    lib().orc_prep_8tap(ptr(tmp), ptr(src, sy * src.shape[1] + sx), src.shape[1], w, h,
+                        col_frac, row_frac, mode_x, mode_y, bd, hbd_of(src))
+    return tmp
+
+
+def mc_avg(t1, t2, bd=8, hbd=0, emulate_gen=0):
+    h, w = t1.shape
+    dst = np.zeros((h, w), dtype=np.uint16 if hbd else np.uint8)
+    lib().orc_mc_avg(ptr(dst), w, ptr(np.ascontiguousarray(t1)), ptr(np.ascontiguousarray(t2)),
+                     w, h, bd, hbd, emulate_gen)
+    return dst
+
+
+def fwd_txfm1d(kind, vec):
+    v = np.ascontiguousarray(vec, dtype=np.int32)
+    out = np.zeros_like(v)
+    rc = lib().orc_fwd_txfm1d(kind, v.size, ptr(v), ptr(out))
+    return None if rc else out
+
+
+def inv_txfm1d(kind, vec, rng):
+    v = np.ascontiguousarray(vec, dtype=np.int32)
+    out = np.zeros_like(v)
+    rc = lib().orc_inv_txfm1d(kind, v.size, ptr(v), ptr(out), rng)
+    return None if rc else out
+
+
+def fwd_txfm2d(residual, tx_size, tx_type, bd):
+    r = np.ascontiguousarray(residual, dtype=np.int16).ravel()
+    out = np.zeros(r.size, dtype=np.int32)
+    rc = lib().orc_fwd_txfm2d(ptr(r), ptr(out), tx_size, tx_type, bd)
+    return None if rc else out
+
+
+def inv_txfm2d_add(coeffs, dst, tx_size, tx_type, bd):
+    c = np.ascontiguousarray(coeffs, dtype=np.int32).ravel()
+    d = np.array(dst, copy=True)
+    rc = lib().orc_inv_txfm2d_add(ptr(c), ptr(d), d.shape[1], tx_size, tx_type, bd, hbd_of(d))
+    return None if rc else d
+
+
+def sse_wxh(a, b, w, h, xdec=0, ydec=0):
+    out = np.zeros(256, dtype=np.uint64)
+    n = lib().orc_sse_wxh(ptr(a), a.shape[1], ptr(b), b.shape[1], w, h, xdec, ydec,
+                          hbd_of(a), ptr(out))
+    return out[:n]
+
+
+def cdef_moments(a, b):
+    out = np.zeros(5, dtype=np.int64)
+    lib().orc_cdef_moments_8x8(ptr(a), a.shape[1], ptr(b), b.shape[1], hbd_of(a), ptr(out))
+    return out
+
+
+def cdef_dist(moments, bd):
+    m = np.ascontiguousarray(moments, dtype=np.int64)
+    return lib().orc_cdef_dist_from_moments(ptr(m), bd)
+
+
+def plane_geometry(width, height, xpad, ypad, hbd):
+    out = np.zeros(4, dtype=np.int32)
+    lib().orc_plane_geometry(width, height, xpad, ypad, hbd, ptr(out))
+    return tuple(int(x) for x in out)  # stride, alloc_height, xorigin, yorigin
+
+
+TX_W_LOG2 = [2, 3, 4, 5, 6, 2, 3, 3, 4, 4, 5, 5, 6, 2, 4, 3, 5, 4, 6]
+TX_H_LOG2 = [2, 3, 4, 5, 6, 3, 2, 4, 3, 5, 4, 6, 5, 4, 2, 5, 3, 6, 4]
+TX_NAMES = ["4x4", "8x8", "16x16", "32x32", "64x64", "4x8", "8x4", "8x16", "16x8",
+            "16x32", "32x16", "32x64", "64x32", "4x16", "16x4", "8x32", "32x8",
+            "16x64", "64x16"]
+TX_TYPES = ["DCT_DCT", "ADST_DCT", "DCT_ADST", "ADST_ADST", "FLIPADST_DCT",
+            "DCT_FLIPADST", "FLIPADST_FLIPADST", "ADST_FLIPADST", "FLIPADST_ADST",
+            "IDTX", "V_DCT", "H_DCT", "V_ADST", "H_ADST", "V_FLIPADST", "H_FLIPADST"]
+BLOCKS = ["4x4", "4x8", "8x4", "8x8", "8x16", "16x8", "16x16", "16x32", "32x16",
+          "32x32", "32x64", "64x32", "64x64", "64x128", "128x64", "128x128",
+          "4x16", "16x4", "8x32", "32x8", "16x64", "64x16"]
+
+
+def block_wh(name):
+    w, h = name.split("x")
+    return int(w), int(h)
+
+
+def dist_kat_planes(dtype):
+    """setup_planes of src/dist.rs:342-375, in the reference's exact layout."""
+    hbd = 1 if dtype == np.uint16 else 0
+    planes = []
+    for pad, pattern in ((128 + 8, "sum"), (2 * 128 + 8, "diff")):
+        stride, alloc_h, xorigin, yorigin = plane_geometry(640, 480, pad, pad, hbd)
+        xpad_off = (xorigin - pad) - 8
+        i = np.arange(alloc_h)[:, None]
+        j = np.arange(stride)[None, :]
+        v = ((j + i) - xpad_off) & 255 if pattern == "sum" else (j - i - xpad_off) & 255
+        planes.append((v.astype(dtype), xorigin, yorigin))
+    return planes
