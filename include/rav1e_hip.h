@@ -1,0 +1,395 @@
+/*
+ * rav1e_hip.h -- C ABI of the MI355X (gfx950) encode hot path for rav1e.
+ *
+ * Two layers, both plain C (no torch / HIP types in any signature; a
+ * stream is an opaque `void *` that is a hipStream_t, NULL = the library's
+ * per-thread default stream):
+ *
+ *  1. Drop-in "asm backend" entry points, one symbol per (kernel, block
+ *     size, pixel type), with exactly the signatures rav1e's x86 FFI binds
+ *     (byte strides, `isize`, `i32`), so a src/asm/hip/{dist,mc}.rs table can
+ *     point at them the way src/asm/x86/{dist,mc}.rs point at NASM.  They
+ *     take HOST pointers, stage the block through the device and block
+ *     until the result is back: correct, reentrant, latency bound.  They
+ *     exist for drop-in parity (the reference's `check_asm` pattern); the
+ *     production path is layer 2.
+ *
+ *  2. Batched entry points (`rv_*_batch`): one launch per tile-step over
+ *     all candidate blocks, device-resident planes (`rv_plane`) and job
+ *     arrays, results left in device memory, asynchronous on `stream`.
+ *
+ * Semantics follow the reference's declared ground truth (the `*_ref`
+ * functions that `feature = "check_asm"` cross-checks against) bit for bit;
+ * each entry point cites the reference function it replaces.
+ * Reference = geobacter-rs/rav1e; paths below are relative to its root.
+ *
+ * Errors: batched entry points return 0 on success, RV_EINVAL for
+ * arguments the reference's safe wrappers would `assert!` on, RV_EHIP for
+ * a HIP runtime failure (rv_last_error() has the text).  The asm-shaped
+ * entry points have no error channel (neither has NASM): on a HIP failure
+ * they print the error and abort(), they never return a wrong value.
+ */
+#ifndef RAV1E_HIP_H
+#define RAV1E_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RV_OK 0
+#define RV_EINVAL (-1)
+#define RV_EHIP (-2)
+#define RV_ENOTSUP (-3)
+
+/* ---------------------------------------------------------------------
+ * Dispatch level.  Mirrors CpuFeatureLevel (src/cpu_features/x86.rs:13-61)
+ * with one more level, HIP, selected like the others through
+ * RAV1E_CPU_TARGET (src/cpu_features/x86.rs:44-59): RAV1E_CPU_TARGET=hip.
+ * ------------------------------------------------------------------- */
+typedef enum rv_cpu_feature_level {
+  RV_CPU_NATIVE = 0,
+  RV_CPU_SSE2 = 1,
+  RV_CPU_SSSE3 = 2,
+  RV_CPU_AVX2 = 3,
+  RV_CPU_HIP = 4,
+  RV_CPU_LEVELS = 5
+} rv_cpu_feature_level;
+
+/* CpuFeatureLevel::default() + the RAV1E_CPU_TARGET override
+ * (src/cpu_features/x86.rs:34-61); "hip" selects RV_CPU_HIP. */
+int rv_cpu_feature_level_default(void);
+/* CpuFeatureLevel::as_index (src/cpu_features/x86.rs:26-30) */
+int rv_cpu_feature_level_index(int level);
+
+/* ---------------------------------------------------------------------
+ * Runtime
+ * ------------------------------------------------------------------- */
+/* Number of visible gfx950 devices (0 if none; never aborts). */
+int rv_device_count(void);
+/* Select the device for the calling thread (hipSetDevice). */
+int rv_set_device(int device);
+const char *rv_last_error(void);
+/* Library build string, e.g. "rav1e_hip gfx950 <date>". */
+const char *rv_version(void);
+
+void *rv_malloc(size_t bytes);            /* device memory, NULL on error */
+void rv_free(void *p);
+void *rv_host_alloc(size_t bytes);        /* pinned host memory */
+void rv_host_free(void *p);
+int rv_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream);
+int rv_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);
+int rv_memcpy_d2d(void *dst, const void *src, size_t bytes, void *stream);
+int rv_memset(void *dst, int value, size_t bytes, void *stream);
+void *rv_stream_create(void);
+int rv_stream_destroy(void *stream);
+int rv_stream_sync(void *stream);
+int rv_device_sync(void);
+void *rv_event_create(void);
+int rv_event_destroy(void *ev);
+int rv_event_record(void *ev, void *stream);
+int rv_event_sync(void *ev);
+/* milliseconds between two recorded events (hipEventElapsedTime) */
+float rv_event_elapsed_ms(void *start, void *stop);
+
+/* ---------------------------------------------------------------------
+ * Data model: a padded plane in device memory.  Reproduces PlaneConfig
+ * (src/frame/plane.rs:22-47, geometry Plane::new :215-244): pixel (x, y)
+ * of the visible area lives at data[(yorigin + y) * stride + xorigin + x];
+ * x, y may be negative down to -xorigin / -yorigin (the padding).
+ * ------------------------------------------------------------------- */
+typedef struct rv_plane {
+  void *data;         /* device pointer to element 0 of the allocation */
+  int32_t stride;     /* in elements */
+  int32_t alloc_height;
+  int32_t width;      /* visible width / height */
+  int32_t height;
+  int32_t xorigin;
+  int32_t yorigin;
+  int32_t xdec;
+  int32_t ydec;
+  int32_t hbd;        /* 0: u8 pixels, 1: u16 pixels */
+  int32_t reserved;
+} rv_plane;
+
+/* Plane::new geometry (src/frame/plane.rs:215-244): fills stride,
+ * alloc_height, xorigin, yorigin, width, height, xdec, ydec, hbd; data is
+ * left NULL.  Returns the allocation size in bytes. */
+size_t rv_plane_geometry(rv_plane *p, int width, int height, int xdec,
+                         int ydec, int xpad, int ypad, int hbd);
+/* Plane::pad (src/frame/plane.rs:269-314): replicate edges into padding. */
+int rv_plane_pad(const rv_plane *p, void *stream);
+/* Plane::downsample_from (src/frame/plane.rs:399-423): 2x2 box filter
+ * (s + 2) >> 2 of src's visible area into dst (dst->width x dst->height),
+ * followed by dst padding like Frame::new's callers do. */
+int rv_plane_downsample(const rv_plane *dst, const rv_plane *src,
+                        void *stream);
+
+/* ---------------------------------------------------------------------
+ * Batched distortion.  All jobs of one call share (w, h).
+ * Block positions are in the plane's visible coordinates.
+ * ------------------------------------------------------------------- */
+typedef struct rv_dist_job {
+  int32_t org_x, org_y; /* block in `org` */
+  int32_t ref_x, ref_y; /* block in `ref` */
+} rv_dist_job;
+
+/* get_sad (src/dist.rs:48-111) == get_sad_ref (src/dist.rs:25-46):
+ * out[i] = sum |org - ref| over the w x h block of job i. */
+int rv_sad_batch(const rv_plane *org, const rv_plane *ref,
+                 const rv_dist_job *d_jobs, int n, int w, int h,
+                 uint32_t *d_out, void *stream);
+/* get_satd (src/dist.rs:121-193) == get_satd_ref (src/dist.rs:197-328):
+ * 4x4 (min(w,h) == 4) or 8x8 Hadamard, sum |.| then
+ * (sum + (1 << ln >> 1)) >> ln, ln = msb(min(w, h, 8)). */
+int rv_satd_batch(const rv_plane *org, const rv_plane *ref,
+                  const rv_dist_job *d_jobs, int n, int w, int h,
+                  uint32_t *d_out, void *stream);
+/* sse_wxh raw partials (src/rdo.rs:286-335): per job, one u64 per
+ * importance sub-block (bw x bh = (min(w,8) >> xdec) x (min(h,8) >> ydec),
+ * xdec/ydec taken from `org`), raster order: d_out[i * nsub + k],
+ * nsub = (w / bw) * (h / bh).  The f64 bias stays with the caller
+ * (src/rdo.rs:325-331). */
+int rv_sse_batch(const rv_plane *org, const rv_plane *ref,
+                 const rv_dist_job *d_jobs, int n, int w, int h,
+                 uint64_t *d_out, void *stream);
+/* cdef_dist_wxh_8x8 integer moments (src/rdo.rs:219-241) for every 8x8 of
+ * a w x h block (w, h multiples of 8): d_out[(i * nsub + k) * 5 + m],
+ * m = {sum_s, sum_d, sum_s2, sum_d2, sum_sd}, nsub = (w/8) * (h/8). */
+int rv_cdef_moments_batch(const rv_plane *org, const rv_plane *ref,
+                          const rv_dist_job *d_jobs, int n, int w, int h,
+                          int64_t *d_out, void *stream);
+
+/* ---------------------------------------------------------------------
+ * Batched motion compensation.  FilterMode (src/mc.rs:58-66):
+ * 0 REGULAR, 1 SMOOTH, 2 SHARP, 3 BILINEAR.  Fracs are 1/16 pel (0..15).
+ * The source block's integer position is (src_x, src_y); the filters read
+ * rows -3..h+4 and columns -3..w+4 around it (src/mc.rs:232-273), which
+ * must lie inside the padded allocation (PlaneSlice::clamp,
+ * src/frame/plane.rs:521-533, is the caller's job as in predict_inter).
+ * ------------------------------------------------------------------- */
+typedef struct rv_mc_job {
+  int32_t src_x, src_y;   /* integer source position in `src` */
+  int32_t dst_x, dst_y;   /* destination block in `dst` (put/avg) */
+  int32_t col_frac, row_frac;
+} rv_mc_job;
+
+/* put_8tap (src/mc.rs:410-519) == put_8tap_ref (src/mc.rs:213-307). */
+int rv_put_8tap_batch(const rv_plane *dst, const rv_plane *src,
+                      const rv_mc_job *d_jobs, int n, int w, int h,
+                      int mode_x, int mode_y, int bit_depth, void *stream);
+/* prep_8tap (src/mc.rs:520-616) == prep_8tap_ref (src/mc.rs:310-387):
+ * d_tmp[i * w * h + r * w + c], i16. */
+int rv_prep_8tap_batch(int16_t *d_tmp, const rv_plane *src,
+                       const rv_mc_job *d_jobs, int n, int w, int h,
+                       int mode_x, int mode_y, int bit_depth, void *stream);
+/* mc_avg (src/mc.rs:617-706) == mc_avg_ref (src/mc.rs:389-408) of the
+ * i-th w*h tiles of tmp1 / tmp2 into dst at (dst_x, dst_y) of job i. */
+int rv_mc_avg_batch(const rv_plane *dst, const int16_t *d_tmp1,
+                    const int16_t *d_tmp2, const rv_mc_job *d_jobs, int n,
+                    int w, int h, int bit_depth, void *stream);
+
+/* Fused sub-pel candidate evaluation: predict_inter's put_8tap into
+ * on-chip memory, then get_sad / get_satd against org -- the pair
+ * compute_mv_rd_cost runs per sub-pel candidate (src/me.rs:811-838).
+ * job.dst_x/dst_y = the org block; out[i] = SAD (metric 0) or SATD (1). */
+int rv_mc_dist_batch(const rv_plane *org, const rv_plane *ref,
+                     const rv_mc_job *d_jobs, int n, int w, int h,
+                     int mode_x, int mode_y, int bit_depth, int metric,
+                     uint32_t *d_out, void *stream);
+
+/* ---------------------------------------------------------------------
+ * Batched transforms.  TxSize order = src/transform/mod.rs:225-247
+ * (0 TX_4X4 ... 18 TX_64X16); TxType order = src/transform/mod.rs:123-140
+ * (0 DCT_DCT ... 15 H_FLIPADST).
+ * ------------------------------------------------------------------- */
+/* forward_transform (src/transform/mod.rs:556-566) = FwdTxfm2D::fht
+ * (src/transform/forward.rs:1804-1899): residual [n][W*H] i16 ->
+ * coeffs [n][W*H] i32 (W-stride raster, full W x H also for 64-point
+ * sizes, forward.rs:1885-1889).  RV_ENOTSUP for (size, type) pairs the
+ * reference leaves unimplemented. */
+int rv_fwd_txfm_batch(const int16_t *d_residual, int32_t *d_coeffs, int n,
+                      int tx_size, int tx_type, int bit_depth, void *stream);
+typedef struct rv_tx_job {
+  int32_t src_x, src_y;   /* source block (org) */
+  int32_t pred_x, pred_y; /* prediction block */
+} rv_tx_job;
+/* diff (src/encoder.rs:1044-1058) fused with forward_transform: the
+ * residual src - pred never leaves the chip.  coeffs as above. */
+int rv_diff_fwd_txfm_batch(const rv_plane *src, const rv_plane *pred,
+                           const rv_tx_job *d_jobs, int n, int tx_size,
+                           int tx_type, int bit_depth, int32_t *d_coeffs,
+                           void *stream);
+/* inverse_transform_add (src/transform/mod.rs:568-580) =
+ * NativeInvTxfm2D::inv_txfm2d_add (src/transform/inverse.rs:1939-2114):
+ * coeffs [n][min(W,32)*min(H,32)] (row stride min(W,32)) added into dst
+ * at (pred_x, pred_y) of job i with clip to [0, 2^bd - 1]. */
+int rv_inv_txfm_add_batch(const int32_t *d_coeffs, const rv_plane *dst,
+                          const rv_tx_job *d_jobs, int n, int tx_size,
+                          int tx_type, int bit_depth, void *stream);
+
+/* ---------------------------------------------------------------------
+ * Motion search
+ * ------------------------------------------------------------------- */
+typedef struct rv_mv {
+  int16_t row, col; /* 1/8 pel (MotionVector, src/mc.rs:28-31) */
+} rv_mv;
+typedef struct rv_fs_job {
+  int32_t po_x, po_y;            /* block origin in org (plane coords) */
+  int32_t x_lo, x_hi, y_lo, y_hi; /* inclusive candidate window in ref */
+  rv_mv pmv[2];
+  uint32_t lambda;
+  int32_t reserved;
+} rv_fs_job;
+typedef struct rv_fs_result {
+  rv_mv best_mv;
+  uint32_t reserved;
+  uint64_t cost;
+} rv_fs_result;
+/* full_search (src/me.rs:943-990): every candidate (x, y), y outer,
+ * x inner, step `step`: cost = 256 * SAD + rate * lambda,
+ * rate = min(rate(mv - pmv0), rate(mv - pmv1) + 1) (get_mv_rate,
+ * src/me.rs:1006-1021); strict-< argmin in raster order. */
+int rv_full_search_batch(const rv_plane *org, const rv_plane *ref,
+                         const rv_fs_job *d_jobs, int n, int blk_w,
+                         int blk_h, int step, int allow_hp,
+                         rv_fs_result *d_out, void *stream);
+
+/* ---------------------------------------------------------------------
+ * Hot-path replay driver (see DESIGN.md "Replay driver"): reproduces the
+ * per-frame call structure of a speed-10 encode for the accelerated
+ * stages, frames resident in HBM.
+ * ------------------------------------------------------------------- */
+typedef struct rv_replay_cfg {
+  int32_t width, height;      /* luma, visible */
+  int32_t xdec, ydec;         /* chroma subsampling (1,1 = 4:2:0) */
+  int32_t bit_depth;          /* 8 or 10 */
+  int32_t tile_x0, tile_y0;   /* tile rectangle in 64x64 superblocks */
+  int32_t tile_w, tile_h;     /* (a whole frame: 0, 0, sb_cols, sb_rows) */
+  int32_t n_refs;             /* reference frames searched per frame */
+  int32_t rdo_candidates;     /* inter candidates per superblock */
+  int32_t flags;              /* reserved, 0 */
+} rv_replay_cfg;
+typedef struct rv_replay rv_replay;
+/* Allocate device state for one tile; frames are uploaded with
+ * rv_replay_set_frame.  NULL on failure. */
+rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream);
+void rv_replay_destroy(rv_replay *r);
+/* Upload a source picture (planar, tightly packed: Y w*h, then the two
+ * chroma planes) into slot `slot` (0 .. n_refs) and pad it. */
+int rv_replay_set_frame(rv_replay *r, int slot, const void *host_yuv);
+/* Run the hot path for one frame: input = slot 0, references =
+ * slots 1..n_refs; me_range_scale as src/encoder.rs:838.  Asynchronous. */
+int rv_replay_frame(rv_replay *r, int me_range_scale);
+/* Copy the frame's results to host: per-superblock best MVs and costs,
+ * checksums of coefficients / reconstruction / distortion.  Layout in
+ * DESIGN.md; returns number of u64 written (<= cap). */
+int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
+/* Kernel-time breakdown of the last frame (ms per stage, HIP events). */
+int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
+
+/* ---------------------------------------------------------------------
+ * Layer 1: drop-in asm-shaped entry points.  Signatures = the reference's
+ * FFI declarations; strides in BYTES (T::to_asm_stride,
+ * src/util/mod.rs:185-187).  Host pointers.
+ * ------------------------------------------------------------------- */
+#define RV_DIST_SIZES(X) \
+  X(4, 4) X(4, 8) X(8, 4) X(8, 8) X(8, 16) X(16, 8) X(16, 16) X(16, 32) \
+  X(32, 16) X(32, 32) X(32, 64) X(64, 32) X(64, 64) X(64, 128) X(128, 64) \
+  X(128, 128) X(4, 16) X(16, 4) X(8, 32) X(32, 8) X(16, 64) X(64, 16)
+
+/* SadFn / SadHBDFn / SatdFn (src/asm/x86/dist.rs:16-32, externs :34-98):
+ *   rav1e_sad{W}x{H}_hip, rav1e_sad{W}x{H}_hbd_hip,
+ *   rav1e_satd_{W}x{H}_hip, rav1e_satd_{W}x{H}_hbd_hip */
+#define RV_DECL_DIST(W, H)                                                   \
+  uint32_t rav1e_sad##W##x##H##_hip(const uint8_t *src, ptrdiff_t src_stride, \
+                                    const uint8_t *dst, ptrdiff_t dst_stride); \
+  uint32_t rav1e_sad##W##x##H##_hbd_hip(const uint16_t *src,                  \
+                                        ptrdiff_t src_stride,                 \
+                                        const uint16_t *dst,                  \
+                                        ptrdiff_t dst_stride);                \
+  uint32_t rav1e_satd_##W##x##H##_hip(const uint8_t *src,                     \
+                                      ptrdiff_t src_stride,                   \
+                                      const uint8_t *dst,                     \
+                                      ptrdiff_t dst_stride);                  \
+  uint32_t rav1e_satd_##W##x##H##_hbd_hip(const uint16_t *src,                \
+                                          ptrdiff_t src_stride,               \
+                                          const uint16_t *dst,                \
+                                          ptrdiff_t dst_stride);
+RV_DIST_SIZES(RV_DECL_DIST)
+#undef RV_DECL_DIST
+
+/* PutFn / PutHBDFn / PrepFn / PrepHBDFn / AvgFn / AvgHBDFn
+ * (src/asm/x86/mc.rs:17-78; tables :300-439, index mode_x + 4 * mode_y,
+ * get_2d_mode_idx :81-83):
+ *   rav1e_put_8tap_{mx}_{my}_hip  (u8)   rav1e_put_8tap_{mx}_{my}_16bpc_hip
+ *   rav1e_prep_8tap_{mx}_{my}_hip (u8)   rav1e_prep_8tap_{mx}_{my}_16bpc_hip
+ *   rav1e_avg_hip / rav1e_avg_16bpc_hip
+ * with {mx},{my} in regular, smooth, sharp, bilinear. */
+#define RV_FILTER_PAIRS(X)                                                  \
+  X(regular, regular, 0, 0) X(smooth, regular, 1, 0)                       \
+  X(sharp, regular, 2, 0) X(bilinear, regular, 3, 0)                       \
+  X(regular, smooth, 0, 1) X(smooth, smooth, 1, 1) X(sharp, smooth, 2, 1)  \
+  X(bilinear, smooth, 3, 1) X(regular, sharp, 0, 2) X(smooth, sharp, 1, 2) \
+  X(sharp, sharp, 2, 2) X(bilinear, sharp, 3, 2)                           \
+  X(regular, bilinear, 0, 3) X(smooth, bilinear, 1, 3)                     \
+  X(sharp, bilinear, 2, 3) X(bilinear, bilinear, 3, 3)
+
+#define RV_DECL_MC(NX, NY, MX, MY)                                            \
+  void rav1e_put_8tap_##NX##_##NY##_hip(                                      \
+      uint8_t *dst, ptrdiff_t dst_stride, const uint8_t *src,                 \
+      ptrdiff_t src_stride, int32_t w, int32_t h, int32_t mx, int32_t my);    \
+  void rav1e_put_8tap_##NX##_##NY##_16bpc_hip(                                \
+      uint16_t *dst, ptrdiff_t dst_stride, const uint16_t *src,               \
+      ptrdiff_t src_stride, int32_t w, int32_t h, int32_t mx, int32_t my,     \
+      int32_t bit_depth);                                                     \
+  void rav1e_prep_8tap_##NX##_##NY##_hip(int16_t *tmp, const uint8_t *src,    \
+                                         ptrdiff_t src_stride, int32_t w,     \
+                                         int32_t h, int32_t mx, int32_t my);  \
+  void rav1e_prep_8tap_##NX##_##NY##_16bpc_hip(                               \
+      int16_t *tmp, const uint16_t *src, ptrdiff_t src_stride, int32_t w,     \
+      int32_t h, int32_t mx, int32_t my, int32_t bit_depth);
+RV_FILTER_PAIRS(RV_DECL_MC)
+#undef RV_DECL_MC
+
+void rav1e_avg_hip(uint8_t *dst, ptrdiff_t dst_stride, const int16_t *tmp1,
+                   const int16_t *tmp2, int32_t w, int32_t h);
+void rav1e_avg_16bpc_hip(uint16_t *dst, ptrdiff_t dst_stride,
+                         const int16_t *tmp1, const int16_t *tmp2, int32_t w,
+                         int32_t h, int32_t bit_depth);
+
+/* Transforms.  The reference has no asm/generated forward transform
+ * (src/encoder.rs:1166-1168 calls the generic Rust), so the HIP level adds
+ * the table FWD_TX[TxSize][TxType]:
+ *   void rav1e_fwd_txfm_hip(const int16_t *residual, int32_t *coeffs,
+ *                           int32_t tx_size, int32_t tx_type, int32_t bd)
+ * and replaces InvTxAddF (build/kernel/gen/tx.rs:1365-1370) with
+ *   rav1e_inv_txfm_add_hip(coeffs, dst, byte stride, size, type, bd)
+ * which covers every pair the native fallback covers (incl. 64-point).
+ * Return 0 or RV_ENOTSUP. */
+int rav1e_fwd_txfm_hip(const int16_t *residual, int32_t *coeffs,
+                       int32_t tx_size, int32_t tx_type, int32_t bit_depth);
+int rav1e_inv_txfm_add_hip(const int32_t *coeffs, void *dst,
+                           ptrdiff_t dst_stride, int32_t tx_size,
+                           int32_t tx_type, int32_t bit_depth);
+
+/* Dispatch tables in the reference's shape (SAD_FNS / SATD_FNS,
+ * src/asm/x86/dist.rs:193-327, indexed [cpu][bsize & 31]; PUT_FNS /
+ * PREP_FNS, src/asm/x86/mc.rs:300-439, indexed [cpu][mode_x + 4*mode_y]).
+ * Entries for levels other than RV_CPU_HIP are NULL (= "use native").
+ * BlockSize order: src/partition.rs:116-140. */
+typedef uint32_t (*rv_dist_fn)(const void *src, ptrdiff_t src_stride,
+                               const void *dst, ptrdiff_t dst_stride);
+rv_dist_fn rv_sad_fn(int cpu_level, int bsize, int hbd);
+rv_dist_fn rv_satd_fn(int cpu_level, int bsize, int hbd);
+typedef void (*rv_put_fn)(void *dst, ptrdiff_t dst_stride, const void *src,
+                          ptrdiff_t src_stride, int32_t w, int32_t h,
+                          int32_t mx, int32_t my);
+rv_put_fn rv_put_fn_get(int cpu_level, int mode_x, int mode_y);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAV1E_HIP_H */

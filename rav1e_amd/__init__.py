@@ -1,0 +1,643 @@
+"""rav1e_amd -- MI355X (gfx950) encode hot path for rav1e, host side.
+
+Python mirror of the reference's dispatch interface for the hot path
+(geobacter-rs/rav1e): ``CpuFeatureLevel`` with a ``HIP`` level, the
+``get_sad`` / ``get_satd`` / ``put_8tap`` / ``prep_8tap`` / ``mc_avg`` /
+``forward_transform`` / ``inverse_transform_add`` / ``sse_wxh`` /
+``cdef_dist_wxh`` entry points, plus the batched forms that are the
+production path.  Everything runs through the C ABI of
+``rav1e_amd/lib/librav1e_hip.so`` (``include/rav1e_hip.h``); there is no
+CPU fallback: without the library this module raises on import of any
+entry point, and the HIP level requires a gfx950 device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+import os
+
+import numpy as np
+
+_ROOT = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_ROOT, "lib", "librav1e_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_ROOT), "include", "rav1e_hip.h")
+
+RV_OK, RV_EINVAL, RV_EHIP, RV_ENOTSUP = 0, -1, -2, -3
+
+
+class Rav1eHipError(RuntimeError):
+    pass
+
+
+# ---- C structs (include/rav1e_hip.h) -----------------------------------
+class RvPlane(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("stride", C.c_int32),
+                ("alloc_height", C.c_int32), ("width", C.c_int32),
+                ("height", C.c_int32), ("xorigin", C.c_int32),
+                ("yorigin", C.c_int32), ("xdec", C.c_int32),
+                ("ydec", C.c_int32), ("hbd", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+class RvMv(C.Structure):
+    _fields_ = [("row", C.c_int16), ("col", C.c_int16)]
+
+
+class RvFsResult(C.Structure):
+    _fields_ = [("best_mv", RvMv), ("reserved", C.c_uint32), ("cost", C.c_uint64)]
+
+
+# job layouts as numpy dtypes (arrays of these go to the device verbatim)
+DIST_JOB = np.dtype([("org_x", "<i4"), ("org_y", "<i4"), ("ref_x", "<i4"), ("ref_y", "<i4")])
+MC_JOB = np.dtype([("src_x", "<i4"), ("src_y", "<i4"), ("dst_x", "<i4"), ("dst_y", "<i4"),
+                   ("col_frac", "<i4"), ("row_frac", "<i4")])
+TX_JOB = np.dtype([("src_x", "<i4"), ("src_y", "<i4"), ("pred_x", "<i4"), ("pred_y", "<i4")])
+FS_JOB = np.dtype([("po_x", "<i4"), ("po_y", "<i4"), ("x_lo", "<i4"), ("x_hi", "<i4"),
+                   ("y_lo", "<i4"), ("y_hi", "<i4"), ("pmv0_row", "<i2"), ("pmv0_col", "<i2"),
+                   ("pmv1_row", "<i2"), ("pmv1_col", "<i2"), ("lambda_", "<u4"),
+                   ("reserved", "<i4")])
+FS_RESULT = np.dtype([("mv_row", "<i2"), ("mv_col", "<i2"), ("reserved", "<u4"),
+                      ("cost", "<u8")])
+REPLAY_CFG_FIELDS = ["width", "height", "xdec", "ydec", "bit_depth", "tile_x0", "tile_y0",
+                     "tile_w", "tile_h", "n_refs", "rdo_candidates", "flags"]
+
+
+class RvReplayCfg(C.Structure):
+    _fields_ = [(f, C.c_int32) for f in REPLAY_CFG_FIELDS]
+
+
+# ---- reference enums ----------------------------------------------------
+class CpuFeatureLevel(enum.IntEnum):
+    """src/cpu_features/x86.rs:13-19 plus the HIP level."""
+    NATIVE = 0
+    SSE2 = 1
+    SSSE3 = 2
+    AVX2 = 3
+    HIP = 4
+
+    @staticmethod
+    def default() -> "CpuFeatureLevel":
+        """CpuFeatureLevel::default() with RAV1E_CPU_TARGET (x86.rs:34-61)."""
+        return CpuFeatureLevel(lib().rv_cpu_feature_level_default())
+
+    def as_index(self) -> int:
+        return int(self)
+
+
+class BlockSize(enum.IntEnum):
+    """src/partition.rs:116-140 (order = table index)."""
+    BLOCK_4X4 = 0
+    BLOCK_4X8 = 1
+    BLOCK_8X4 = 2
+    BLOCK_8X8 = 3
+    BLOCK_8X16 = 4
+    BLOCK_16X8 = 5
+    BLOCK_16X16 = 6
+    BLOCK_16X32 = 7
+    BLOCK_32X16 = 8
+    BLOCK_32X32 = 9
+    BLOCK_32X64 = 10
+    BLOCK_64X32 = 11
+    BLOCK_64X64 = 12
+    BLOCK_64X128 = 13
+    BLOCK_128X64 = 14
+    BLOCK_128X128 = 15
+    BLOCK_4X16 = 16
+    BLOCK_16X4 = 17
+    BLOCK_8X32 = 18
+    BLOCK_32X8 = 19
+    BLOCK_16X64 = 20
+    BLOCK_64X16 = 21
+
+    def width(self) -> int:
+        return int(self.name.split("_")[1].split("X")[0])
+
+    def height(self) -> int:
+        return int(self.name.split("X")[-1])
+
+    @staticmethod
+    def from_width_and_height(w: int, h: int) -> "BlockSize":
+        return BlockSize[f"BLOCK_{w}X{h}"]
+
+
+class TxSize(enum.IntEnum):
+    """src/transform/mod.rs:225-247."""
+    TX_4X4 = 0
+    TX_8X8 = 1
+    TX_16X16 = 2
+    TX_32X32 = 3
+    TX_64X64 = 4
+    TX_4X8 = 5
+    TX_8X4 = 6
+    TX_8X16 = 7
+    TX_16X8 = 8
+    TX_16X32 = 9
+    TX_32X16 = 10
+    TX_32X64 = 11
+    TX_64X32 = 12
+    TX_4X16 = 13
+    TX_16X4 = 14
+    TX_8X32 = 15
+    TX_32X8 = 16
+    TX_16X64 = 17
+    TX_64X16 = 18
+
+    def width(self) -> int:
+        return int(self.name.split("_")[1].split("X")[0])
+
+    def height(self) -> int:
+        return int(self.name.split("X")[-1])
+
+
+class TxType(enum.IntEnum):
+    """src/transform/mod.rs:123-140."""
+    DCT_DCT = 0
+    ADST_DCT = 1
+    DCT_ADST = 2
+    ADST_ADST = 3
+    FLIPADST_DCT = 4
+    DCT_FLIPADST = 5
+    FLIPADST_FLIPADST = 6
+    ADST_FLIPADST = 7
+    FLIPADST_ADST = 8
+    IDTX = 9
+    V_DCT = 10
+    H_DCT = 11
+    V_ADST = 12
+    H_ADST = 13
+    V_FLIPADST = 14
+    H_FLIPADST = 15
+
+
+class FilterMode(enum.IntEnum):
+    """src/mc.rs:58-66."""
+    REGULAR = 0
+    SMOOTH = 1
+    SHARP = 2
+    BILINEAR = 3
+
+
+# ---- library loading ------------------------------------------------------
+_lib = None
+
+
+def _declare(L):
+    vp, i32, sz = C.c_void_p, C.c_int, C.c_size_t
+    P = C.POINTER(RvPlane)
+    sig = {
+        "rv_cpu_feature_level_default": (i32, []),
+        "rv_cpu_feature_level_index": (i32, [i32]),
+        "rv_device_count": (i32, []),
+        "rv_set_device": (i32, [i32]),
+        "rv_last_error": (C.c_char_p, []),
+        "rv_version": (C.c_char_p, []),
+        "rv_malloc": (vp, [sz]),
+        "rv_free": (None, [vp]),
+        "rv_host_alloc": (vp, [sz]),
+        "rv_host_free": (None, [vp]),
+        "rv_memcpy_h2d": (i32, [vp, vp, sz, vp]),
+        "rv_memcpy_d2h": (i32, [vp, vp, sz, vp]),
+        "rv_memcpy_d2d": (i32, [vp, vp, sz, vp]),
+        "rv_memset": (i32, [vp, i32, sz, vp]),
+        "rv_stream_create": (vp, []),
+        "rv_stream_destroy": (i32, [vp]),
+        "rv_stream_sync": (i32, [vp]),
+        "rv_device_sync": (i32, []),
+        "rv_event_create": (vp, []),
+        "rv_event_destroy": (i32, [vp]),
+        "rv_event_record": (i32, [vp, vp]),
+        "rv_event_sync": (i32, [vp]),
+        "rv_event_elapsed_ms": (C.c_float, [vp, vp]),
+        "rv_plane_geometry": (sz, [P, i32, i32, i32, i32, i32, i32, i32]),
+        "rv_plane_pad": (i32, [P, vp]),
+        "rv_plane_downsample": (i32, [P, P, vp]),
+        "rv_sad_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
+        "rv_satd_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
+        "rv_sse_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
+        "rv_cdef_moments_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
+        "rv_put_8tap_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, i32, vp]),
+        "rv_prep_8tap_batch": (i32, [vp, P, vp, i32, i32, i32, i32, i32, i32, vp]),
+        "rv_mc_avg_batch": (i32, [P, vp, vp, vp, i32, i32, i32, i32, vp]),
+        "rv_mc_dist_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
+        "rv_fwd_txfm_batch": (i32, [vp, vp, i32, i32, i32, i32, vp]),
+        "rv_diff_fwd_txfm_batch": (i32, [P, P, vp, i32, i32, i32, i32, vp, vp]),
+        "rv_inv_txfm_add_batch": (i32, [vp, P, vp, i32, i32, i32, i32, vp]),
+        "rv_full_search_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, vp, vp]),
+        "rv_replay_create": (vp, [C.POINTER(RvReplayCfg), vp]),
+        "rv_replay_destroy": (None, [vp]),
+        "rv_replay_set_frame": (i32, [vp, i32, vp]),
+        "rv_replay_frame": (i32, [vp, i32]),
+        "rv_replay_results": (i32, [vp, vp, i32]),
+        "rv_replay_stage_times": (i32, [vp, vp, i32]),
+        "rav1e_fwd_txfm_hip": (i32, [vp, vp, i32, i32, i32]),
+        "rav1e_inv_txfm_add_hip": (i32, [vp, vp, C.c_ssize_t, i32, i32, i32]),
+        "rv_sad_fn": (vp, [i32, i32, i32]),
+        "rv_satd_fn": (vp, [i32, i32, i32]),
+        "rv_put_fn_get": (vp, [i32, i32, i32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+
+
+def lib():
+    """Load the HIP library; raises if it was not built (no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise Rav1eHipError(
+                f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != RV_OK:
+        raise Rav1eHipError(f"{what} failed ({rc}): {lib().rv_last_error().decode()}")
+
+
+def require_device(device: int = 0):
+    """Fail loudly unless a gfx950 device is visible."""
+    L = lib()
+    if L.rv_device_count() <= device:
+        raise Rav1eHipError("no HIP device visible: the HIP level needs a gfx950 GPU")
+    _check(L.rv_set_device(device), "rv_set_device")
+
+
+# ---- device memory --------------------------------------------------------
+class DeviceBuffer:
+    """Device allocation owned by Python (rv_malloc / rv_free)."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        self.ptr = lib().rv_malloc(max(1, self.nbytes))
+        if not self.ptr:
+            raise Rav1eHipError(f"rv_malloc({nbytes}): {lib().rv_last_error().decode()}")
+
+    @classmethod
+    def from_array(cls, a: np.ndarray) -> "DeviceBuffer":
+        a = np.ascontiguousarray(a)
+        b = cls(a.nbytes)
+        b.upload(a)
+        return b
+
+    def upload(self, a: np.ndarray, stream=None):
+        a = np.ascontiguousarray(a)
+        assert a.nbytes <= self.nbytes
+        if a.nbytes:
+            _check(lib().rv_memcpy_h2d(self.ptr, a.ctypes.data, a.nbytes, stream), "rv_memcpy_h2d")
+
+    def download(self, dtype, count=None, stream=None) -> np.ndarray:
+        dt = np.dtype(dtype)
+        n = self.nbytes // dt.itemsize if count is None else int(count)
+        out = np.empty(n, dtype=dt)
+        if out.nbytes:
+            _check(lib().rv_memcpy_d2h(out.ctypes.data, self.ptr, out.nbytes, stream),
+                   "rv_memcpy_d2h")
+        return out
+
+    def zero(self, stream=None):
+        _check(lib().rv_memset(self.ptr, 0, self.nbytes, stream), "rv_memset")
+        _check(lib().rv_stream_sync(stream), "rv_stream_sync")
+
+    def free(self):
+        if self.ptr:
+            lib().rv_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class DevicePlane:
+    """A padded plane in HBM with the reference's PlaneConfig geometry
+    (Plane::new, src/frame/plane.rs:215-244)."""
+
+    def __init__(self, width, height, xdec=0, ydec=0, xpad=0, ypad=0, hbd=False):
+        self.desc = RvPlane()
+        nbytes = lib().rv_plane_geometry(C.byref(self.desc), width, height, xdec, ydec,
+                                         xpad, ypad, 1 if hbd else 0)
+        self.buf = DeviceBuffer(nbytes)
+        self.desc.data = self.buf.ptr
+        self.dtype = np.uint16 if hbd else np.uint8
+
+    @classmethod
+    def from_array(cls, a: np.ndarray, xpad=0, ypad=0, xdec=0, ydec=0, pad=True):
+        p = cls(a.shape[1], a.shape[0], xdec, ydec, xpad, ypad, a.dtype == np.uint16)
+        p.upload_visible(a, pad=pad)
+        return p
+
+    @classmethod
+    def from_full(cls, full: np.ndarray, xorigin, yorigin, width, height):
+        """Wrap a whole padded allocation (stride = full.shape[1])."""
+        p = cls.__new__(cls)
+        p.desc = RvPlane()
+        p.desc.stride, p.desc.alloc_height = full.shape[1], full.shape[0]
+        p.desc.width, p.desc.height = width, height
+        p.desc.xorigin, p.desc.yorigin = xorigin, yorigin
+        p.desc.hbd = 1 if full.dtype == np.uint16 else 0
+        p.buf = DeviceBuffer.from_array(full)
+        p.desc.data = p.buf.ptr
+        p.dtype = full.dtype
+        return p
+
+    @property
+    def shape_full(self):
+        return (self.desc.alloc_height, self.desc.stride)
+
+    def upload_visible(self, a: np.ndarray, pad=True):
+        full = np.zeros(self.shape_full, dtype=self.dtype)
+        d = self.desc
+        full[d.yorigin:d.yorigin + d.height, d.xorigin:d.xorigin + d.width] = a
+        self.buf.upload(full)
+        if pad:
+            _check(lib().rv_plane_pad(C.byref(self.desc), None), "rv_plane_pad")
+            _check(lib().rv_stream_sync(None), "rv_stream_sync")
+
+    def download_full(self) -> np.ndarray:
+        return self.buf.download(self.dtype).reshape(self.shape_full)
+
+    def download_visible(self) -> np.ndarray:
+        d = self.desc
+        return self.download_full()[d.yorigin:d.yorigin + d.height,
+                                    d.xorigin:d.xorigin + d.width].copy()
+
+
+def _sync(stream=None):
+    _check(lib().rv_stream_sync(stream), "rv_stream_sync")
+
+
+# ---- batched entry points (production path) -------------------------------
+def sad_batch(org: DevicePlane, ref: DevicePlane, jobs: np.ndarray, w: int, h: int,
+              satd: bool = False) -> np.ndarray:
+    jobs = np.ascontiguousarray(jobs, dtype=DIST_JOB)
+    dj = DeviceBuffer.from_array(jobs)
+    out = DeviceBuffer(4 * len(jobs))
+    f = lib().rv_satd_batch if satd else lib().rv_sad_batch
+    _check(f(C.byref(org.desc), C.byref(ref.desc), dj.ptr, len(jobs), w, h, out.ptr, None),
+           "rv_satd_batch" if satd else "rv_sad_batch")
+    _sync()
+    return out.download(np.uint32)
+
+
+def satd_batch(org, ref, jobs, w, h) -> np.ndarray:
+    return sad_batch(org, ref, jobs, w, h, satd=True)
+
+
+def sse_batch(org, ref, jobs, w, h) -> np.ndarray:
+    jobs = np.ascontiguousarray(jobs, dtype=DIST_JOB)
+    bw = min(w, 8) >> org.desc.xdec
+    bh = min(h, 8) >> org.desc.ydec
+    nsub = (w // bw) * (h // bh)
+    dj = DeviceBuffer.from_array(jobs)
+    out = DeviceBuffer(8 * nsub * max(1, len(jobs)))
+    _check(lib().rv_sse_batch(C.byref(org.desc), C.byref(ref.desc), dj.ptr, len(jobs), w, h,
+                              out.ptr, None), "rv_sse_batch")
+    _sync()
+    return out.download(np.uint64, nsub * len(jobs)).reshape(len(jobs), nsub)
+
+
+def cdef_moments_batch(org, ref, jobs, w, h) -> np.ndarray:
+    jobs = np.ascontiguousarray(jobs, dtype=DIST_JOB)
+    nsub = (w // 8) * (h // 8)
+    dj = DeviceBuffer.from_array(jobs)
+    out = DeviceBuffer(40 * nsub * max(1, len(jobs)))
+    _check(lib().rv_cdef_moments_batch(C.byref(org.desc), C.byref(ref.desc), dj.ptr, len(jobs),
+                                       w, h, out.ptr, None), "rv_cdef_moments_batch")
+    _sync()
+    return out.download(np.int64, 5 * nsub * len(jobs)).reshape(len(jobs), nsub, 5)
+
+
+def put_8tap_batch(dst: DevicePlane, src: DevicePlane, jobs, w, h, mode_x=0, mode_y=0,
+                   bit_depth=8):
+    jobs = np.ascontiguousarray(jobs, dtype=MC_JOB)
+    dj = DeviceBuffer.from_array(jobs)
+    _check(lib().rv_put_8tap_batch(C.byref(dst.desc), C.byref(src.desc), dj.ptr, len(jobs), w, h,
+                                   mode_x, mode_y, bit_depth, None), "rv_put_8tap_batch")
+    _sync()
+
+
+def prep_8tap_batch(src: DevicePlane, jobs, w, h, mode_x=0, mode_y=0, bit_depth=8):
+    jobs = np.ascontiguousarray(jobs, dtype=MC_JOB)
+    dj = DeviceBuffer.from_array(jobs)
+    out = DeviceBuffer(2 * w * h * max(1, len(jobs)))
+    _check(lib().rv_prep_8tap_batch(out.ptr, C.byref(src.desc), dj.ptr, len(jobs), w, h,
+                                    mode_x, mode_y, bit_depth, None), "rv_prep_8tap_batch")
+    _sync()
+    return out.download(np.int16, w * h * len(jobs)).reshape(len(jobs), h, w)
+
+
+def mc_avg_batch(dst: DevicePlane, tmp1: np.ndarray, tmp2: np.ndarray, jobs, w, h,
+                 bit_depth=8):
+    jobs = np.ascontiguousarray(jobs, dtype=MC_JOB)
+    dj = DeviceBuffer.from_array(jobs)
+    t1 = DeviceBuffer.from_array(np.ascontiguousarray(tmp1, dtype=np.int16))
+    t2 = DeviceBuffer.from_array(np.ascontiguousarray(tmp2, dtype=np.int16))
+    _check(lib().rv_mc_avg_batch(C.byref(dst.desc), t1.ptr, t2.ptr, dj.ptr, len(jobs), w, h,
+                                 bit_depth, None), "rv_mc_avg_batch")
+    _sync()
+
+
+def mc_dist_batch(org: DevicePlane, ref: DevicePlane, jobs, w, h, mode_x=0, mode_y=0,
+                  bit_depth=8, metric=0) -> np.ndarray:
+    jobs = np.ascontiguousarray(jobs, dtype=MC_JOB)
+    dj = DeviceBuffer.from_array(jobs)
+    out = DeviceBuffer(4 * max(1, len(jobs)))
+    _check(lib().rv_mc_dist_batch(C.byref(org.desc), C.byref(ref.desc), dj.ptr, len(jobs), w, h,
+                                  mode_x, mode_y, bit_depth, metric, out.ptr, None),
+           "rv_mc_dist_batch")
+    _sync()
+    return out.download(np.uint32, len(jobs))
+
+
+def fwd_txfm_batch(residual: np.ndarray, tx_size, tx_type, bit_depth=8) -> np.ndarray:
+    """residual: [n, H, W] int16 -> coeffs [n, H*W] int32 (W-stride raster)."""
+    r = np.ascontiguousarray(residual, dtype=np.int16)
+    n = r.shape[0]
+    w, h = TxSize(tx_size).width(), TxSize(tx_size).height()
+    dr = DeviceBuffer.from_array(r)
+    out = DeviceBuffer(4 * w * h * max(1, n))
+    _check(lib().rv_fwd_txfm_batch(dr.ptr, out.ptr, n, int(tx_size), int(tx_type), bit_depth,
+                                   None), "rv_fwd_txfm_batch")
+    _sync()
+    return out.download(np.int32, w * h * n).reshape(n, w * h)
+
+
+def diff_fwd_txfm_batch(src: DevicePlane, pred: DevicePlane, jobs, tx_size, tx_type,
+                        bit_depth=8) -> np.ndarray:
+    jobs = np.ascontiguousarray(jobs, dtype=TX_JOB)
+    w, h = TxSize(tx_size).width(), TxSize(tx_size).height()
+    dj = DeviceBuffer.from_array(jobs)
+    out = DeviceBuffer(4 * w * h * max(1, len(jobs)))
+    _check(lib().rv_diff_fwd_txfm_batch(C.byref(src.desc), C.byref(pred.desc), dj.ptr, len(jobs),
+                                        int(tx_size), int(tx_type), bit_depth, out.ptr, None),
+           "rv_diff_fwd_txfm_batch")
+    _sync()
+    return out.download(np.int32, w * h * len(jobs)).reshape(len(jobs), w * h)
+
+
+def inv_txfm_add_batch(coeffs: np.ndarray, dst: DevicePlane, jobs, tx_size, tx_type,
+                       bit_depth=8):
+    """coeffs: [n, min(H,32)*min(W,32)] int32, added into dst in place."""
+    jobs = np.ascontiguousarray(jobs, dtype=TX_JOB)
+    dc = DeviceBuffer.from_array(np.ascontiguousarray(coeffs, dtype=np.int32))
+    dj = DeviceBuffer.from_array(jobs)
+    _check(lib().rv_inv_txfm_add_batch(dc.ptr, C.byref(dst.desc), dj.ptr, len(jobs),
+                                       int(tx_size), int(tx_type), bit_depth, None),
+           "rv_inv_txfm_add_batch")
+    _sync()
+
+
+def full_search_batch(org: DevicePlane, ref: DevicePlane, jobs, blk_w, blk_h, step=1,
+                      allow_hp=False) -> np.ndarray:
+    jobs = np.ascontiguousarray(jobs, dtype=FS_JOB)
+    dj = DeviceBuffer.from_array(jobs)
+    out = DeviceBuffer(16 * max(1, len(jobs)))
+    _check(lib().rv_full_search_batch(C.byref(org.desc), C.byref(ref.desc), dj.ptr, len(jobs),
+                                      blk_w, blk_h, step, 1 if allow_hp else 0, out.ptr, None),
+           "rv_full_search_batch")
+    _sync()
+    return out.download(FS_RESULT, len(jobs))
+
+
+# ---- reference-shaped single-call entry points ----------------------------
+class PlaneRegion:
+    """A block position inside a DevicePlane (PlaneRegion,
+    src/tiling/plane_region.rs:110-152)."""
+
+    def __init__(self, plane: DevicePlane, x: int, y: int):
+        self.plane, self.x, self.y = plane, x, y
+
+
+def _require_hip(cpu):
+    if CpuFeatureLevel(cpu) != CpuFeatureLevel.HIP:
+        raise Rav1eHipError(f"{CpuFeatureLevel(cpu).name}: only the HIP level is built here")
+
+
+def get_sad(org: PlaneRegion, ref: PlaneRegion, bsize: BlockSize, bit_depth: int,
+            cpu=CpuFeatureLevel.HIP) -> int:
+    """get_sad (src/dist.rs:48-111)."""
+    _require_hip(cpu)
+    bs = BlockSize(bsize)
+    job = np.array([(org.x, org.y, ref.x, ref.y)], dtype=DIST_JOB)
+    return int(sad_batch(org.plane, ref.plane, job, bs.width(), bs.height())[0])
+
+
+def get_satd(org: PlaneRegion, ref: PlaneRegion, bsize: BlockSize, bit_depth: int,
+             cpu=CpuFeatureLevel.HIP) -> int:
+    """get_satd (src/dist.rs:121-193)."""
+    _require_hip(cpu)
+    bs = BlockSize(bsize)
+    job = np.array([(org.x, org.y, ref.x, ref.y)], dtype=DIST_JOB)
+    return int(satd_batch(org.plane, ref.plane, job, bs.width(), bs.height())[0])
+
+
+def put_8tap(dst: PlaneRegion, src: PlaneRegion, width, height, col_frac, row_frac,
+             mode_x=FilterMode.REGULAR, mode_y=FilterMode.REGULAR, bit_depth=8,
+             cpu=CpuFeatureLevel.HIP):
+    """put_8tap (src/mc.rs:410-519): src = the block's integer position."""
+    _require_hip(cpu)
+    job = np.array([(src.x, src.y, dst.x, dst.y, col_frac, row_frac)], dtype=MC_JOB)
+    put_8tap_batch(dst.plane, src.plane, job, width, height, int(mode_x), int(mode_y), bit_depth)
+
+
+def prep_8tap(src: PlaneRegion, width, height, col_frac, row_frac,
+              mode_x=FilterMode.REGULAR, mode_y=FilterMode.REGULAR, bit_depth=8,
+              cpu=CpuFeatureLevel.HIP) -> np.ndarray:
+    """prep_8tap (src/mc.rs:520-616): returns the i16 tmp[h][w]."""
+    _require_hip(cpu)
+    job = np.array([(src.x, src.y, 0, 0, col_frac, row_frac)], dtype=MC_JOB)
+    return prep_8tap_batch(src.plane, job, width, height, int(mode_x), int(mode_y), bit_depth)[0]
+
+
+def mc_avg(dst: PlaneRegion, tmp1, tmp2, width, height, bit_depth=8, cpu=CpuFeatureLevel.HIP):
+    """mc_avg (src/mc.rs:617-706)."""
+    _require_hip(cpu)
+    job = np.array([(0, 0, dst.x, dst.y, 0, 0)], dtype=MC_JOB)
+    mc_avg_batch(dst.plane, np.asarray(tmp1)[None], np.asarray(tmp2)[None], job, width, height,
+                 bit_depth)
+
+
+def forward_transform(residual: np.ndarray, tx_size: TxSize, tx_type: TxType, bit_depth=8,
+                      cpu=CpuFeatureLevel.HIP) -> np.ndarray:
+    """forward_transform (src/transform/mod.rs:556-566)."""
+    _require_hip(cpu)
+    return fwd_txfm_batch(np.asarray(residual)[None], tx_size, tx_type, bit_depth)[0]
+
+
+def inverse_transform_add(coeffs: np.ndarray, dst: PlaneRegion, tx_size: TxSize,
+                          tx_type: TxType, bit_depth=8, cpu=CpuFeatureLevel.HIP):
+    """inverse_transform_add (src/transform/mod.rs:568-580)."""
+    _require_hip(cpu)
+    job = np.array([(0, 0, dst.x, dst.y)], dtype=TX_JOB)
+    inv_txfm_add_batch(np.asarray(coeffs)[None], dst.plane, job, tx_size, tx_type, bit_depth)
+
+
+def sse_wxh(src1: PlaneRegion, src2: PlaneRegion, w, h, compute_bias=None) -> float:
+    """sse_wxh (src/rdo.rs:286-335): integer partials on the device, the
+    f64 bias (compute_bias(x, y) per importance sub-block) on the host."""
+    job = np.array([(src1.x, src1.y, src2.x, src2.y)], dtype=DIST_JOB)
+    parts = sse_batch(src1.plane, src2.plane, job, w, h)[0]
+    if compute_bias is None:
+        return int(parts.sum())
+    bw = min(w, 8) >> src1.plane.desc.xdec
+    bh = min(h, 8) >> src1.plane.desc.ydec
+    sx = w // bw
+    total = 0.0
+    for k, v in enumerate(parts):
+        total += float(int(v)) * compute_bias((k % sx) * bw, (k // sx) * bh)
+    return total
+
+
+def cdef_dist_from_moments(m, bit_depth: int) -> int:
+    """f64 tail of cdef_dist_wxh_8x8 (src/rdo.rs:242-252), on the host."""
+    import math
+    cs = bit_depth - 8
+    sum_s, sum_d, s2, d2, sd = (int(v) for v in m)
+    svar = float(s2 - ((sum_s * sum_s + 32) >> 6))
+    dvar = float(d2 - ((sum_d * sum_d + 32) >> 6))
+    sse = float(d2 + s2 - 2 * sd)
+    boost = (4033.0 / 16384.0) * (svar + dvar + float(16384 << (2 * cs))) / math.sqrt(
+        float(16265089 << (4 * cs)) + svar * dvar)
+    v = sse * boost + 0.5
+    return int(v) if v > 0 else 0
+
+
+def cdef_dist_wxh(src1: PlaneRegion, src2: PlaneRegion, w, h, bit_depth=8,
+                  compute_bias=None) -> float:
+    """cdef_dist_wxh (src/rdo.rs:256-283)."""
+    job = np.array([(src1.x, src1.y, src2.x, src2.y)], dtype=DIST_JOB)
+    mom = cdef_moments_batch(src1.plane, src2.plane, job, w, h)[0]
+    sx = w // 8
+    total = 0.0
+    for k, m in enumerate(mom):
+        d = cdef_dist_from_moments(m, bit_depth)
+        total += d * (compute_bias((k % sx) * 8, (k // sx) * 8) if compute_bias else 1.0)
+    return total
+
+
+def exported_symbols_from_header(path: str = HEADER_PATH):
+    """Every function name include/rav1e_hip.h declares (macros expanded)."""
+    import re
+    text = open(path).read()
+    names = set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(rv_\w+|rav1e_\w+)\s*\(", text, re.M))
+    names = {n for n in names if not n.startswith("rv_dist_fn") and n not in ("rv_put_fn",)}
+    sizes = re.findall(r"X\((\d+), (\d+)\)", text.split("#define RV_DIST_SIZES")[1].split(
+        "/*")[0])
+    for w, h in sizes:
+        names |= {f"rav1e_sad{w}x{h}_hip", f"rav1e_sad{w}x{h}_hbd_hip",
+                  f"rav1e_satd_{w}x{h}_hip", f"rav1e_satd_{w}x{h}_hbd_hip"}
+    pairs = re.findall(r"X\((\w+), (\w+), \d, \d\)", text.split("#define RV_FILTER_PAIRS")[1]
+                       .split("#define RV_DECL_MC")[0])
+    for nx, ny in pairs:
+        names |= {f"rav1e_put_8tap_{nx}_{ny}_hip", f"rav1e_put_8tap_{nx}_{ny}_16bpc_hip",
+                  f"rav1e_prep_8tap_{nx}_{ny}_hip", f"rav1e_prep_8tap_{nx}_{ny}_16bpc_hip"}
+    return sorted(n for n in names if "##" not in n and not n.endswith("_hip_") and
+                  n not in ("rav1e_sad", "rav1e_satd_", "rav1e_put_8tap_",
+                            "rav1e_prep_8tap_"))

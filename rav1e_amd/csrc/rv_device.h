@@ -1,0 +1,101 @@
+// rv_device.h -- device-side primitives shared by the gfx950 kernels.
+//
+// Integer semantics follow the reference's Rust release build: i32
+// arithmetic wraps (done through u32 here to stay clear of C++ UB), `>>` on
+// signed values is arithmetic.  Citations: geobacter-rs/rav1e.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rav1e_hip.h"
+
+#define RV_WAVE 64
+
+namespace rv {
+
+__device__ __forceinline__ int32_t wadd(int32_t a, int32_t b) {
+  return (int32_t)((uint32_t)a + (uint32_t)b);
+}
+__device__ __forceinline__ int32_t wsub(int32_t a, int32_t b) {
+  return (int32_t)((uint32_t)a - (uint32_t)b);
+}
+__device__ __forceinline__ int32_t wmul(int32_t a, int32_t b) {
+  return (int32_t)((uint32_t)a * (uint32_t)b);
+}
+// round_shift (src/util/mod.rs:241-243); ISimd::round_shift is identical
+// (src/util/simd.rs:98-100).  Wrapping add, arithmetic shift.
+__device__ __forceinline__ int32_t round_shift(int32_t v, int bit) {
+  return wadd(v, (1 << bit) >> 1) >> bit;
+}
+__device__ __forceinline__ int32_t clampi(int32_t v, int32_t lo, int32_t hi) {
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+// msb (src/util/mod.rs:235-238)
+__device__ __forceinline__ int msb(int32_t x) {
+  return 31 - __builtin_clz((uint32_t)x);
+}
+
+// Plane addressing (PlaneConfig, src/frame/plane.rs:22-47).
+struct PlaneView {
+  uint8_t *data;
+  int32_t stride;
+  int32_t hbd;
+  __device__ __forceinline__ int64_t idx(int32_t x, int32_t y) const {
+    return (int64_t)y * stride + x;
+  }
+};
+
+__host__ __device__ __forceinline__ int64_t plane_origin_index(
+    const rv_plane &p) {
+  return (int64_t)p.yorigin * p.stride + p.xorigin;
+}
+
+template <typename Px>
+__device__ __forceinline__ const Px *plane_ptr(const rv_plane &p, int32_t x,
+                                               int32_t y) {
+  return reinterpret_cast<const Px *>(p.data) + plane_origin_index(p) +
+         (int64_t)y * p.stride + x;
+}
+template <typename Px>
+__device__ __forceinline__ Px *plane_ptr_mut(const rv_plane &p, int32_t x,
+                                             int32_t y) {
+  return reinterpret_cast<Px *>(p.data) + plane_origin_index(p) +
+         (int64_t)y * p.stride + x;
+}
+
+// Wave-level reductions over aligned sub-groups of G lanes (G power of 2,
+// <= 64): every lane of the group ends up with the group's total.
+template <int G, typename T>
+__device__ __forceinline__ T group_sum(T v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, RV_WAVE);
+  return v;
+}
+
+// Unaligned 4-byte load of u8 pixels (the compiler picks byte loads if the
+// target cannot do it in one access).
+__device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t *p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+}
+
+// |a - b| summed over the 4 bytes of a and b, plus acc (v_sad_u8).
+__device__ __forceinline__ uint32_t sad_u8x4(uint32_t a, uint32_t b,
+                                             uint32_t acc) {
+  return __builtin_amdgcn_sad_u8(a, b, acc);
+}
+
+}  // namespace rv
+
+#define RV_HIP_CHECK_LAUNCH()                                   \
+  do {                                                          \
+    hipError_t e_ = hipGetLastError();                          \
+    if (e_ != hipSuccess) return rv_set_hip_error(e_, __func__); \
+  } while (0)
+
+// Host-side helpers implemented in rv_runtime.cpp.
+extern "C++" int rv_set_hip_error(hipError_t e, const char *where);
+extern "C++" int rv_set_error(int code, const char *msg);
+extern "C++" hipStream_t rv_resolve_stream(void *stream);

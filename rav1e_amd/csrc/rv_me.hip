@@ -1,0 +1,278 @@
+// rv_me.hip -- batched exhaustive motion search (gfx950).
+//
+// full_search (src/me.rs:943-990) for many blocks in one launch: one
+// workgroup per block.  The reference evaluates every candidate window in
+// raster order (y outer, x inner) and keeps the first strict minimum of
+// cost = 256 * SAD + rate * lambda; here every lane evaluates a tile of
+// candidates and the workgroup reduces (cost, raster index)
+// lexicographically, which selects the same candidate.
+//
+// Fast path (u8, 16x16 block, step 1 -- the quarter-resolution search of
+// every 64x64 superblock, estimate_motion_ss4 src/me.rs:1023-1075): the
+// search window is staged in LDS in bands, the 16x16 source block lives in
+// 64 VGPRs, and each lane computes a 4-wide x 8-tall candidate tile with
+// v_sad_u8 on packed dwords (v_alignbyte for the 3 unaligned shifts), so a
+// reference row is read from LDS once per 32 candidates.  The search is
+// VALU-bound (~256 |a-b| per candidate), not HBM-bound.
+#include "rv_device.h"
+
+namespace rv {
+
+constexpr int kFsThreads = 256;
+
+// get_mv_rate / diff_to_rate (src/me.rs:1006-1021)
+__device__ __forceinline__ uint32_t diff_to_rate(int16_t diff, int hp) {
+  int16_t d = hp ? diff : (int16_t)(diff >> 1);
+  if (d == 0) return 0;
+  uint32_t a = (uint16_t)(d < 0 ? -d : d);
+  return 2u * (16u - (uint32_t)(__builtin_clz(a) - 16));
+}
+__device__ __forceinline__ uint32_t mv_rate(int16_t row, int16_t col,
+                                            rv_mv p, int hp) {
+  return diff_to_rate((int16_t)(row - p.row), hp) +
+         diff_to_rate((int16_t)(col - p.col), hp);
+}
+
+struct Best {
+  uint64_t cost;
+  uint32_t idx;
+};
+__device__ __forceinline__ bool better(uint64_t c, uint32_t i, const Best &b) {
+  return c < b.cost || (c == b.cost && i < b.idx);
+}
+
+__device__ __forceinline__ uint64_t cand_cost(uint32_t sad, int x, int y,
+                                              const rv_fs_job &jb, int hp) {
+  const int16_t row = (int16_t)(8 * (y - jb.po_y));
+  const int16_t col = (int16_t)(8 * (x - jb.po_x));
+  const uint32_t r1 = mv_rate(row, col, jb.pmv[0], hp);
+  const uint32_t r2 = mv_rate(row, col, jb.pmv[1], hp);
+  const uint32_t rate = r1 < r2 + 1 ? r1 : r2 + 1;
+  return 256ull * sad + (uint64_t)rate * jb.lambda;
+}
+
+// Workgroup argmin over (cost, idx); lane 0 of wave 0 holds the result.
+__device__ __forceinline__ Best block_best(Best b) {
+  __shared__ uint64_t sc[kFsThreads / 64];
+  __shared__ uint32_t si[kFsThreads / 64];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    uint64_t c = __shfl_xor(b.cost, o, 64);
+    uint32_t i = __shfl_xor(b.idx, o, 64);
+    if (better(c, i, b)) b = Best{c, i};
+  }
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sc[wid] = b.cost;
+    si[wid] = b.idx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int k = 1; k < (int)(blockDim.x >> 6); k++)
+      if (better(sc[k], si[k], b)) b = Best{sc[k], si[k]};
+  return b;
+}
+
+__device__ __forceinline__ void write_result(const rv_fs_job &jb, Best b,
+                                             int nx, int step,
+                                             rv_fs_result *out) {
+  rv_fs_result r;
+  r.reserved = 0;
+  if (b.cost == ~0ull && b.idx == 0xffffffffu) {
+    r.best_mv = rv_mv{0, 0};  // MotionVector::default(), cost u64::MAX
+    r.cost = ~0ull;
+  } else {
+    const int iy = b.idx / nx, ix = b.idx - iy * nx;
+    const int x = jb.x_lo + ix * step, y = jb.y_lo + iy * step;
+    r.best_mv = rv_mv{(int16_t)(8 * (y - jb.po_y)), (int16_t)(8 * (x - jb.po_x))};
+    r.cost = b.cost;
+  }
+  *out = r;
+}
+
+// ---- generic path: one lane per candidate --------------------------------
+template <typename Px>
+__device__ void fs_generic_body(const rv_plane &org, const rv_plane &ref,
+                                const rv_fs_job &jb, int bw, int bh,
+                                int step, int hp, rv_fs_result *out) {
+  const int nx = jb.x_hi >= jb.x_lo ? (jb.x_hi - jb.x_lo) / step + 1 : 0;
+  const int ny = jb.y_hi >= jb.y_lo ? (jb.y_hi - jb.y_lo) / step + 1 : 0;
+  const Px *o = plane_ptr<Px>(org, jb.po_x, jb.po_y);
+  Best b{~0ull, 0xffffffffu};
+  for (int c = threadIdx.x; c < nx * ny; c += blockDim.x) {
+    const int iy = c / nx, ix = c - iy * nx;
+    const int x = jb.x_lo + ix * step, y = jb.y_lo + iy * step;
+    const Px *r = plane_ptr<Px>(ref, x, y);
+    uint32_t sad = 0;
+    for (int rr = 0; rr < bh; rr++) {
+      const Px *po = o + (int64_t)rr * org.stride;
+      const Px *pr = r + (int64_t)rr * ref.stride;
+      if constexpr (sizeof(Px) == 1) {
+        for (int cc = 0; cc < bw; cc += 4)
+          sad = sad_u8x4(load_u32_unaligned(po + cc),
+                         load_u32_unaligned(pr + cc), sad);
+      } else {
+        for (int cc = 0; cc < bw; cc++) {
+          int d = (int)po[cc] - (int)pr[cc];
+          sad += (uint32_t)(d < 0 ? -d : d);
+        }
+      }
+    }
+    const uint64_t cost = cand_cost(sad, x, y, jb, hp);
+    if (better(cost, (uint32_t)c, b)) b = Best{cost, (uint32_t)c};
+  }
+  b = block_best(b);
+  if (threadIdx.x == 0) write_result(jb, b, nx > 0 ? nx : 1, step, out);
+}
+
+template <typename Px>
+__global__ __launch_bounds__(kFsThreads) void fs_generic_kernel(
+    rv_plane org, rv_plane ref, const rv_fs_job *__restrict__ jobs, int n,
+    int bw, int bh, int step, int hp, rv_fs_result *__restrict__ out) {
+  const int job = blockIdx.x;
+  if (job >= n) return;
+  const rv_fs_job jb = jobs[job];
+  fs_generic_body<Px>(org, ref, jb, bw, bh, step, hp, out + job);
+}
+
+// ---- fast path: u8, 16x16, step 1 ---------------------------------------
+constexpr int kTileRows = 8;          // candidate rows per lane
+constexpr int kLdsWords = 14 * 1024;  // 56 KiB search band
+
+__global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(
+    rv_plane org, rv_plane ref, const rv_fs_job *__restrict__ jobs, int n,
+    int hp, rv_fs_result *__restrict__ out) {
+  __shared__ uint32_t band[kLdsWords];
+  const int job = blockIdx.x;
+  if (job >= n) return;
+  const rv_fs_job jb = jobs[job];
+  const int nx = jb.x_hi >= jb.x_lo ? jb.x_hi - jb.x_lo + 1 : 0;
+  const int ny = jb.y_hi >= jb.y_lo ? jb.y_hi - jb.y_lo + 1 : 0;
+  const int tid = threadIdx.x;
+
+  // 16x16 source block -> 64 packed dwords in VGPRs (same in every lane)
+  uint32_t ow[16][4];
+  {
+    const uint8_t *o = plane_ptr<uint8_t>(org, jb.po_x, jb.po_y);
+#pragma unroll
+    for (int r = 0; r < 16; r++)
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        ow[r][i] = load_u32_unaligned(o + (int64_t)r * org.stride + 4 * i);
+  }
+
+  const int tx_n = (nx + 3) >> 2;       // 4-wide candidate columns
+  const int rw = tx_n + 4;              // band row length in dwords
+  if (rw * (2 * kTileRows + 15) > kLdsWords) {  // window too wide for a band
+    fs_generic_body<uint8_t>(org, ref, jb, 16, 16, 1, hp, out + job);
+    return;
+  }
+  const int vis_w = nx + 15;            // bytes of a ref row that exist
+  int pb = kLdsWords / rw - (kTileRows + 15);  // candidate rows per band
+  pb = (pb / kTileRows) * kTileRows;
+
+  Best b{~0ull, 0xffffffffu};
+  const uint8_t *rbase = plane_ptr<uint8_t>(ref, jb.x_lo, jb.y_lo);
+  for (int y0 = 0; y0 < ny; y0 += pb) {
+    const int rows = ny - y0 < pb ? ny - y0 : pb;
+    const int lrows = rows + 15;  // ref rows with data
+    const int ty_n = (rows + kTileRows - 1) / kTileRows;
+    const int brows = ty_n * kTileRows + 15;  // rows the tiles touch
+    __syncthreads();
+    for (int i = tid; i < brows * rw; i += blockDim.x) {
+      const int r = i / rw, wd = i - r * rw;
+      const int c = 4 * wd;
+      uint32_t v = 0;
+      if (r < lrows) {
+        const uint8_t *p = rbase + (int64_t)(y0 + r) * ref.stride + c;
+        if (c + 3 < vis_w) {
+          v = load_u32_unaligned(p);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if (c + k < vis_w) v |= (uint32_t)p[k] << (8 * k);
+        }
+      }
+      band[i] = v;
+    }
+    __syncthreads();
+    const int tasks = tx_n * ty_n;
+    for (int t = tid; t < tasks; t += blockDim.x) {
+      const int tcy = t / tx_n, tcx = t - tcy * tx_n;
+      const int cy0 = tcy * kTileRows;
+      uint32_t acc[kTileRows][4];
+#pragma unroll
+      for (int c = 0; c < kTileRows; c++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[c][j] = 0;
+      const uint32_t *bp = band + cy0 * rw + tcx;
+#pragma unroll
+      for (int yy = 0; yy < kTileRows + 15; yy++) {
+        uint32_t wv[5];
+#pragma unroll
+        for (int i = 0; i < 5; i++) wv[i] = bp[yy * rw + i];
+        uint32_t sh[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          sh[0][i] = wv[i];
+          sh[1][i] = __builtin_amdgcn_alignbyte(wv[i + 1], wv[i], 1);
+          sh[2][i] = __builtin_amdgcn_alignbyte(wv[i + 1], wv[i], 2);
+          sh[3][i] = __builtin_amdgcn_alignbyte(wv[i + 1], wv[i], 3);
+        }
+#pragma unroll
+        for (int c = 0; c < kTileRows; c++) {
+          const int r = yy - c;
+          if (r >= 0 && r < 16) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+#pragma unroll
+              for (int i = 0; i < 4; i++)
+                acc[c][j] = sad_u8x4(ow[r][i], sh[j][i], acc[c][j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < kTileRows; c++) {
+        const int iy = y0 + cy0 + c;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int ix = 4 * tcx + j;
+          if (ix < nx && cy0 + c < rows) {
+            const uint64_t cost =
+                cand_cost(acc[c][j], jb.x_lo + ix, jb.y_lo + iy, jb, hp);
+            const uint32_t idx = (uint32_t)(iy * nx + ix);
+            if (better(cost, idx, b)) b = Best{cost, idx};
+          }
+        }
+      }
+    }
+  }
+  b = block_best(b);
+  if (tid == 0) write_result(jb, b, nx > 0 ? nx : 1, 1, out + job);
+}
+
+}  // namespace rv
+
+using namespace rv;
+
+extern "C" int rv_full_search_batch(const rv_plane *org, const rv_plane *ref,
+                                    const rv_fs_job *d_jobs, int n, int blk_w,
+                                    int blk_h, int step, int allow_hp,
+                                    rv_fs_result *d_out, void *stream) {
+  if (!org || !ref || n < 0 || blk_w < 4 || blk_h < 4 || blk_w > 128 ||
+      blk_h > 128 || (blk_w & 3) || step < 1 || org->hbd != ref->hbd)
+    return rv_set_error(RV_EINVAL, "rv_full_search_batch: bad arguments");
+  if (n == 0) return RV_OK;
+  hipStream_t s = rv_resolve_stream(stream);
+  if (!org->hbd && blk_w == 16 && blk_h == 16 && step == 1)
+    fs16_u8_kernel<<<n, kFsThreads, 0, s>>>(*org, *ref, d_jobs, n,
+                                            allow_hp ? 1 : 0, d_out);
+  else if (org->hbd)
+    fs_generic_kernel<uint16_t><<<n, kFsThreads, 0, s>>>(
+        *org, *ref, d_jobs, n, blk_w, blk_h, step, allow_hp ? 1 : 0, d_out);
+  else
+    fs_generic_kernel<uint8_t><<<n, kFsThreads, 0, s>>>(
+        *org, *ref, d_jobs, n, blk_w, blk_h, step, allow_hp ? 1 : 0, d_out);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}

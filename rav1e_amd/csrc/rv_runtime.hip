@@ -1,0 +1,194 @@
+// rv_runtime.hip -- runtime plumbing of the C ABI (include/rav1e_hip.h):
+// errors, device memory, streams, events, plane geometry, dispatch level.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <strings.h>
+
+#include <string>
+
+#include "rv_device.h"
+
+static thread_local std::string g_last_error;
+
+int rv_set_hip_error(hipError_t e, const char *where) {
+  g_last_error = std::string(where) + ": " + hipGetErrorString(e);
+  return RV_EHIP;
+}
+int rv_set_error(int code, const char *msg) {
+  g_last_error = msg;
+  return code;
+}
+hipStream_t rv_resolve_stream(void *stream) {
+  return stream ? reinterpret_cast<hipStream_t>(stream) : hipStreamPerThread;
+}
+
+#define RV_TRY(expr)                                       \
+  do {                                                     \
+    hipError_t e_ = (expr);                                \
+    if (e_ != hipSuccess) return rv_set_hip_error(e_, #expr); \
+  } while (0)
+
+extern "C" {
+
+const char *rv_last_error(void) { return g_last_error.c_str(); }
+
+const char *rv_version(void) {
+  return "rav1e_hip gfx950 " __DATE__ " " __TIME__;
+}
+
+// CpuFeatureLevel::default() with the RAV1E_CPU_TARGET override
+// (src/cpu_features/x86.rs:34-61).  Without the override the HIP level is
+// chosen when a device is present, as the reference picks the best ISA the
+// machine has; an unknown value falls back like the reference does.
+int rv_cpu_feature_level_default(void) {
+  const char *env = getenv("RAV1E_CPU_TARGET");
+  if (env) {
+    if (!strcasecmp(env, "rust") || !strcasecmp(env, "native"))
+      return RV_CPU_NATIVE;
+    if (!strcasecmp(env, "sse2")) return RV_CPU_SSE2;
+    if (!strcasecmp(env, "ssse3")) return RV_CPU_SSSE3;
+    if (!strcasecmp(env, "avx2")) return RV_CPU_AVX2;
+    if (!strcasecmp(env, "hip")) return RV_CPU_HIP;
+  }
+  return rv_device_count() > 0 ? RV_CPU_HIP : RV_CPU_NATIVE;
+}
+
+int rv_cpu_feature_level_index(int level) {
+  return (level >= 0 && level < RV_CPU_LEVELS) ? level : 0;
+}
+
+int rv_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+int rv_set_device(int device) {
+  RV_TRY(hipSetDevice(device));
+  return RV_OK;
+}
+
+void *rv_malloc(size_t bytes) {
+  void *p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
+  if (e != hipSuccess) {
+    rv_set_hip_error(e, "hipMalloc");
+    return nullptr;
+  }
+  return p;
+}
+void rv_free(void *p) {
+  if (p) (void)hipFree(p);
+}
+void *rv_host_alloc(size_t bytes) {
+  void *p = nullptr;
+  hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    rv_set_hip_error(e, "hipHostMalloc");
+    return nullptr;
+  }
+  return p;
+}
+void rv_host_free(void *p) {
+  if (p) (void)hipHostFree(p);
+}
+int rv_memcpy_h2d(void *dst, const void *src, size_t bytes, void *stream) {
+  RV_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice,
+                        rv_resolve_stream(stream)));
+  RV_TRY(hipStreamSynchronize(rv_resolve_stream(stream)));
+  return RV_OK;
+}
+int rv_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream) {
+  RV_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost,
+                        rv_resolve_stream(stream)));
+  RV_TRY(hipStreamSynchronize(rv_resolve_stream(stream)));
+  return RV_OK;
+}
+int rv_memcpy_d2d(void *dst, const void *src, size_t bytes, void *stream) {
+  RV_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice,
+                        rv_resolve_stream(stream)));
+  return RV_OK;
+}
+int rv_memset(void *dst, int value, size_t bytes, void *stream) {
+  RV_TRY(hipMemsetAsync(dst, value, bytes, rv_resolve_stream(stream)));
+  return RV_OK;
+}
+void *rv_stream_create(void) {
+  hipStream_t s = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    rv_set_hip_error(e, "hipStreamCreate");
+    return nullptr;
+  }
+  return s;
+}
+int rv_stream_destroy(void *stream) {
+  if (stream) RV_TRY(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)));
+  return RV_OK;
+}
+int rv_stream_sync(void *stream) {
+  RV_TRY(hipStreamSynchronize(rv_resolve_stream(stream)));
+  return RV_OK;
+}
+int rv_device_sync(void) {
+  RV_TRY(hipDeviceSynchronize());
+  return RV_OK;
+}
+void *rv_event_create(void) {
+  hipEvent_t ev = nullptr;
+  hipError_t e = hipEventCreate(&ev);
+  if (e != hipSuccess) {
+    rv_set_hip_error(e, "hipEventCreate");
+    return nullptr;
+  }
+  return ev;
+}
+int rv_event_destroy(void *ev) {
+  if (ev) RV_TRY(hipEventDestroy(reinterpret_cast<hipEvent_t>(ev)));
+  return RV_OK;
+}
+int rv_event_record(void *ev, void *stream) {
+  RV_TRY(hipEventRecord(reinterpret_cast<hipEvent_t>(ev),
+                        rv_resolve_stream(stream)));
+  return RV_OK;
+}
+int rv_event_sync(void *ev) {
+  RV_TRY(hipEventSynchronize(reinterpret_cast<hipEvent_t>(ev)));
+  return RV_OK;
+}
+float rv_event_elapsed_ms(void *start, void *stop) {
+  float ms = -1.0f;
+  hipError_t e = hipEventElapsedTime(&ms, reinterpret_cast<hipEvent_t>(start),
+                                     reinterpret_cast<hipEvent_t>(stop));
+  if (e != hipSuccess) {
+    rv_set_hip_error(e, "hipEventElapsedTime");
+    return -1.0f;
+  }
+  return ms;
+}
+
+// Plane::new (src/frame/plane.rs:215-244): STRIDE_ALIGNMENT_LOG2 = 5, so
+// xorigin and stride are rounded up to 32 bytes (2^(5+1-sizeof(T)) pixels).
+size_t rv_plane_geometry(rv_plane *p, int width, int height, int xdec,
+                         int ydec, int xpad, int ypad, int hbd) {
+  int al = 5 + 1 - (hbd ? 2 : 1);
+  int m = (1 << al) - 1;
+  memset(p, 0, sizeof(*p));
+  p->width = width;
+  p->height = height;
+  p->xdec = xdec;
+  p->ydec = ydec;
+  p->hbd = hbd ? 1 : 0;
+  p->xorigin = (xpad + m) & ~m;
+  p->yorigin = ypad;
+  p->stride = (p->xorigin + width + xpad + m) & ~m;
+  p->alloc_height = p->yorigin + height + ypad;
+  return (size_t)p->stride * p->alloc_height * (hbd ? 2 : 1);
+}
+
+}  // extern "C"

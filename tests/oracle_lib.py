@@ -176,3 +176,28 @@ def dist_kat_planes(dtype):
         v = ((j + i) - xpad_off) & 255 if pattern == "sum" else (j - i - xpad_off) & 255
         planes.append((v.astype(dtype), xorigin, yorigin))
     return planes
+
+
+class _Mv(C.Structure):
+    _fields_ = [("row", C.c_int16), ("col", C.c_int16)]
+
+
+def full_search(org_full, ref_full, xorigin, yorigin, job, blk_w, blk_h, step, allow_hp):
+    """orc_full_search on full padded arrays; job = one FS_JOB record
+    (coordinates relative to the plane origin).  Returns ((row, col), cost)."""
+    L = lib()
+    L.orc_full_search.argtypes = [C.c_void_p, C.c_ssize_t, C.c_void_p, C.c_ssize_t, C.c_int,
+                                  C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  C.c_int, C.c_int, C.c_int, C.c_uint32, _Mv, _Mv, C.c_int,
+                                  C.POINTER(_Mv), C.POINTER(C.c_uint64)]
+    o = ptr(org_full, yorigin * org_full.shape[1] + xorigin)
+    r = ptr(ref_full, yorigin * ref_full.shape[1] + xorigin)
+    best = _Mv(0, 0)
+    cost = C.c_uint64(2 ** 64 - 1)
+    L.orc_full_search(o, org_full.shape[1], r, ref_full.shape[1], hbd_of(org_full),
+                      int(job["po_x"]), int(job["po_y"]), int(job["x_lo"]), int(job["x_hi"]),
+                      int(job["y_lo"]), int(job["y_hi"]), blk_w, blk_h, step,
+                      int(job["lambda_"]), _Mv(int(job["pmv0_row"]), int(job["pmv0_col"])),
+                      _Mv(int(job["pmv1_row"]), int(job["pmv1_col"])), allow_hp,
+                      C.byref(best), C.byref(cost))
+    return (best.row, best.col), cost.value
