@@ -51,7 +51,7 @@ def lib():
 
 def ptr(a, offset=0):
     """Pointer to element `offset` (flat, in elements) of a numpy array."""
-    return C.c_void_p(a.ctypes.data + offset * a.itemsize)
+    return C.c_void_p(int(a.ctypes.data) + int(offset) * a.itemsize)
 
 
 def hbd_of(a):
@@ -123,7 +123,7 @@ def inv_txfm2d_add(coeffs, dst, tx_size, tx_type, bd):
 
 
 def sse_wxh(a, b, w, h, xdec=0, ydec=0):
-    out = np.zeros(256, dtype=np.uint64)
+    out = np.zeros(w * h, dtype=np.uint64)  # >= sub-block count
     n = lib().orc_sse_wxh(ptr(a), a.shape[1], ptr(b), b.shape[1], w, h, xdec, ydec,
                           hbd_of(a), ptr(out))
     return out[:n]
