@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""bench.py -- encode hot-path replay throughput on MI355X.
+
+Metric (BASELINE.json): encoded frames/sec (+ Mpixels/sec) of the speed-10
+hot path, frames resident in HBM, vs the host CPU running the same schedule.
+A "step" = one frame of the replay driver (DESIGN.md "Replay driver"):
+F0 downsample, F1 1/4-res full search, F2 1/2-res diamond, F3 full-res
+diamond + sub-pel, F4 RDO candidates (MC, diff+fwd DCT, coefficient
+stand-in, inverse DCT + add, distortion), F5 8x8 importance SATD.
+Frames cycle through the reorder pyramid's me_range_scale (4, 2, 1, 1).
+
+N = 1: configs[1] of BASELINE.json (1080p 8-bit 4:2:0, one tile, 1 GPU).
+N > 1 (torch.distributed.run, one process per GPU): every rank runs its own
+1080p tile stream -- tiles are independent units in the replay, so there is
+no data-path collective; `value` = frames of all ranks / max-over-ranks
+time ("scaling": "weak").  torch.distributed (gloo) carries only the
+barrier and the max-time reduction.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {  # name: (width, height, xdec, ydec, bit_depth)
+    "360p": (640, 360, 1, 1, 8),
+    "1080p": (1920, 1080, 1, 1, 8),
+    "2160p": (3840, 2160, 1, 1, 8),
+    "2160p10": (3840, 2160, 1, 1, 10),
+    "2160p444": (3840, 2160, 0, 0, 8),
+}
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
+SAD_PEAK_PX = 256 * 4 * 32 * 2.4e9 * 4  # v_sad_u8: 4 |a-b| per lane-op, 128 lanes/clk/CU
+
+
+def coarse_windows(W, H, R, scale, tile=(0, 0, 0, 0)):
+    """(nx, ny) of every F1 job: estimate_motion_ss4's window
+    (src/me.rs:1023-1075), as the replay builds it."""
+    w_in_b, h_in_b = 2 * ((W + 7) >> 3), 2 * ((H + 7) >> 3)
+    sbc, sbr = (W + 63) // 64, (H + 63) // 64
+    tx0, ty0, tw, th = tile
+    tw, th = tw or sbc - tx0, th or sbr - ty0
+    vis_w = min(W - tx0 * 64, tw * 64)
+    vis_h = min(H - ty0 * 64, th * 64)
+    mi_w, mi_h = vis_w >> 2, vis_h >> 2
+
+    def tdiv8(v):
+        return int(v / 8)
+    out = []
+    for sb in range(tw * th):
+        bx, by = (sb % tw) * 16, (sb // tw) * 16
+        bx, by = max(min(bx, mi_w - 16), 0), max(min(by, mi_h - 16), 0)
+        fbx, fby = bx + tx0 * 16, by + ty0 * 16
+        mr = [-fbx * 32 - 640, (w_in_b - fbx - 16) * 32 + 640,
+              -fby * 32 - 640, (h_in_b - fby - 16) * 32 + 640]
+        rx, ry = 192 * scale, 64 * scale
+        x_lo = fbx + (max(-rx, tdiv8(mr[0])) >> 2)
+        x_hi = fbx + (min(rx, tdiv8(mr[1])) >> 2)
+        y_lo = fby + (max(-ry, tdiv8(mr[2])) >> 2)
+        y_hi = fby + (min(ry, tdiv8(mr[3])) >> 2)
+        out.append((max(0, x_hi - x_lo + 1), max(0, y_hi - y_lo + 1)))
+    return out * R
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--config", default="1080p", choices=sorted(CONFIGS))
+    ap.add_argument("--refs", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", rank))
+
+    import rav1e_amd as R  # load the HIP library before anything else
+    from rav1e_amd import replay as RP
+    R.lib()
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo", rank=rank, world_size=world)
+        dist = (torch, tdist)
+    R.require_device(local % max(1, R.lib().rv_device_count()))
+
+    W, H, xdec, ydec, bd = CONFIGS[args.config]
+    nref = args.refs
+    t_off = 1000 * rank  # every rank its own tile stream
+    frames = [RP.synth_frame(W, H, t_off + t, xdec, ydec, bd) for t in range(nref + 1)]
+    hip = RP.HipReplay(W, H, xdec, ydec, bd, nref)
+    for s, f in enumerate(frames):
+        hip.set_frame(s, f)
+
+    scales = RP.GOP_SCALES
+    for i in range(args.warmup):
+        hip.frame(scales[i % 4])
+    hip.results()  # drains the stream
+
+    def barrier():
+        if dist:
+            dist[1].barrier()
+    barrier()
+    R._sync(None)
+    ev0 = R.lib().rv_event_create()
+    ev1 = R.lib().rv_event_create()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        hip.frame(scales[(args.warmup + i) % 4])
+    words = hip.results()  # blocks until the last frame is done
+    t1 = time.perf_counter()
+    barrier()
+    dt = t1 - t0
+    if dist:
+        torch, tdist = dist
+        tt = torch.tensor([dt], dtype=torch.float64)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        dt = float(tt[0])
+
+    # per-kernel times over the timed frames (HIP events on the replay stream)
+    k = min(args.steps, 64)
+    ms = hip.stage_ms_sum(k) / k  # per frame
+    evals = hip.counters()
+    nsb = ((W + 63) // 64) * ((H + 63) // 64)
+    px = 2 if bd > 8 else 1
+    # algorithmic bytes per frame of each kernel class
+    fs_bytes = sum(sum((nx + 15) * (ny + 15) * px + 256 * px + 40
+                       for nx, ny in coarse_windows(W, H, nref, s)) for s in scales) / 4.0
+    fs_ops = sum(sum(nx * ny * 256 for nx, ny in coarse_windows(W, H, nref, s))
+                 for s in scales) / 4.0
+    total_frames = args.warmup + args.steps
+    nctx = nsb * 2 * nref
+    kernels = {
+        "full_search": dict(ms=float(ms[1]), launches=nref, bytes=fs_bytes, sad_px=fs_ops),
+        "diamond_f3": dict(ms=float(ms[3]), launches=2 * nref,
+                           bytes=float(evals[0] * 2 * 64 * 64 * px +
+                                       evals[1] * (71 * 71 * px + 64 * 64 * px)) / total_frames),
+        "put_luma": dict(ms=float(ms[6]), launches=nref,
+                         bytes=float(nctx * (71 * 71 * px + 64 * 64 * px))),
+        "diff_fwd_64": dict(ms=float(ms[7]), launches=1,
+                            bytes=float(nctx * (2 * 64 * 64 * px + 4 * 64 * 64))),
+        "inv_add_64": dict(ms=float(ms[8]), launches=1,
+                           bytes=float(nctx * (4 * 32 * 32 + 2 * 64 * 64 * px))),
+        "cdef_moments": dict(ms=float(ms[9]), launches=1,
+                             bytes=float(nctx * (2 * 64 * 64 * px + 64 * 40))),
+    }
+    dom = max(kernels, key=lambda n: kernels[n]["ms"])
+    kd = kernels[dom]
+    launch_s = kd["ms"] / 1e3 / kd["launches"]
+    ach = kd["bytes"] / kd["launches"] / launch_s / 1e9
+    roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+            "avg_launch_ms": round(kd["ms"] / kd["launches"], 5)}
+    if dom == "full_search":
+        achv = kd["sad_px"] / (kd["ms"] / 1e3) / 1e12
+        roof["valu"] = {"achieved": round(achv, 3), "peak": round(SAD_PEAK_PX / 1e12, 1),
+                        "unit": "T |a-b|/s (v_sad_u8)", "frac": round(achv * 1e12 / SAD_PEAK_PX, 4)}
+    fps = world * args.steps / dt
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from tests import oracle_lib as O  # the checker / CPU baseline only
+        threads = min(16, os.cpu_count() or 1)
+        c = O.CpuReplay(W, H, xdec, ydec, bd, nref, threads=threads)
+        for s, f in enumerate(frames):
+            c.set_frame(s, f)
+        n, tc0 = 0, time.perf_counter()
+        while n < 4 or (time.perf_counter() - tc0 < args.cpu_seconds and n < 16):
+            c.frame(scales[n % 4])
+            n += 1
+        tc = time.perf_counter() - tc0
+        cpu = {"value": round(n / tc, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+               "sample": f"{n} full {args.config} frames (scales {list(scales)}) of the same "
+                         f"replay schedule, oracle/orc_replay.c -O3 on {threads} host threads",
+               "mpix_per_s": round(n / tc * W * H / 1e6, 3)}
+        c.close()
+
+    if rank == 0:
+        line = {
+            "metric": "encoded frames/sec + Mpixels/sec, 4K 8-bit speed=10, 1/2/4/8 GPU vs host CPU",
+            "value": round(fps, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u16" if bd > 8 else "u8", "data": "synthetic",
+            "config": {"workload": f"{args.config} {bd}-bit "
+                                   f"{'4:2:0' if xdec else '4:4:4'} speed=10 hot-path replay, "
+                                   f"1 tile per GPU, {nref} refs, GOP scales (4,2,1,1)",
+                       "width": W, "height": H, "refs": nref, "parallelism": f"tiles{world}"},
+            "mpix_per_s": round(fps * W * H / 1e6, 3),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "gpu_vs_cpu": round(fps / cpu["value"], 2) if cpu else None,
+            "stage_ms": {n: round(float(v), 4) for n, v in
+                         zip(["F0_downsample", "F1_full_search", "F2_diamond_half",
+                              "F3_diamond_full_subpel", "F4_rdo", "F5_importance_satd"], ms[:6])},
+            "kernels_ms": {n: round(v["ms"], 4) for n, v in kernels.items()},
+            "checksum": int(words[-3]) & 0xFFFFFFFF,
+        }
+        print(json.dumps(line), flush=True)
+    hip.close()
+    if dist:
+        dist[1].destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

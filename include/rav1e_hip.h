@@ -257,6 +257,31 @@ int rv_full_search_batch(const rv_plane *org, const rv_plane *ref,
                          int blk_h, int step, int allow_hp,
                          rv_fs_result *d_out, void *stream);
 
+/* diamond_me_search (src/me.rs:693-785) with get_best_predictor
+ * (:655-691), get_mv_rd_cost (:787-838), compute_mv_rd_cost (:840-856):
+ * one persistent workgroup per job runs the whole data-dependent search.
+ * Full-pel (subpixel = 0): radius 16 -> 8 (1/8 pel units), candidates are
+ * the reference region at po + mv / 8.  Sub-pel (subpixel = 1): radius
+ * 4 -> 2 (1 with allow_hp), candidates are predict_inter (REGULAR 8-tap,
+ * src/predict.rs:255-338, PlaneSlice::clamp included) into on-chip memory.
+ * Distortion: SAD (use_satd = 0) or SATD; cost = 256 * dist + rate *
+ * lambda; candidates outside [mv*_min, mv*_max] cost u64::MAX. */
+#define RV_DS_MAX_PRED 8
+typedef struct rv_ds_job {
+  int32_t po_x, po_y;                 /* block origin (plane coords) */
+  int32_t mvx_min, mvx_max;           /* get_mv_range, 1/8 pel */
+  int32_t mvy_min, mvy_max;
+  rv_mv pmv[2];                       /* rate predictors */
+  uint32_t lambda;
+  int32_t n_pred;                     /* predictors used (<= 8) */
+  rv_mv pred[RV_DS_MAX_PRED];         /* search start candidates */
+} rv_ds_job;
+int rv_diamond_search_batch(const rv_plane *org, const rv_plane *ref,
+                            const rv_ds_job *d_jobs, int n, int blk_w,
+                            int blk_h, int subpixel, int use_satd,
+                            int allow_hp, int bit_depth,
+                            rv_fs_result *d_out, void *stream);
+
 /* ---------------------------------------------------------------------
  * Hot-path replay driver (see DESIGN.md "Replay driver"): reproduces the
  * per-frame call structure of a speed-10 encode for the accelerated
@@ -287,8 +312,17 @@ int rv_replay_frame(rv_replay *r, int me_range_scale);
  * checksums of coefficients / reconstruction / distortion.  Layout in
  * DESIGN.md; returns number of u64 written (<= cap). */
 int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
-/* Kernel-time breakdown of the last frame (ms per stage, HIP events). */
+/* Kernel-time breakdown of the last frame (HIP events on the replay
+ * stream), ms: [0..5] stages F0..F5 (F1 = the full-search launches),
+ * [6] luma put_8tap, [7] luma diff + forward TX_64X64, [8] luma inverse
+ * TX_64X64 + add, [9] luma cdef moments.  Returns the count written. */
 int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
+/* Same breakdown summed over the last `last_frames` frames (<= 64). */
+int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,
+                              int cap);
+/* Cumulative diamond-search candidate evaluations since creation:
+ * out[0] full-pel 64x64 (F3), out[1] sub-pel 64x64 (F3). */
+int rv_replay_counters(rv_replay *r, uint64_t *out, int cap);
 
 /* ---------------------------------------------------------------------
  * Layer 1: drop-in asm-shaped entry points.  Signatures = the reference's

@@ -40,3 +40,88 @@ void orc_full_search(const void *org, ptrdiff_t org_stride, const void *ref,
       }
     }
 }
+
+/* get_mv_rd_cost + compute_mv_rd_cost, src/me.rs:787-856. */
+static uint64_t mv_rd_cost(const orc_ds_ctx *c, orc_mv mv) {
+  if (mv.col < c->mvx_min || mv.col > c->mvx_max || mv.row < c->mvy_min ||
+      mv.row > c->mvy_max)
+    return UINT64_MAX;
+  size_t px = c->hbd ? 2 : 1;
+  const char *o = (const char *)c->org +
+                  ((ptrdiff_t)c->po_y * c->org_stride + c->po_x) * (ptrdiff_t)px;
+  uint32_t dist;
+  if (!c->subpel) {
+    /* Rust i16 `/` truncates toward zero, as C does */
+    const char *r = (const char *)c->ref +
+                    ((ptrdiff_t)(c->po_y + mv.row / 8) * c->ref_stride +
+                     (c->po_x + mv.col / 8)) * (ptrdiff_t)px;
+    dist = c->satd ? orc_get_satd(o, c->org_stride, r, c->ref_stride, c->w,
+                                  c->h, c->hbd, 0)
+                   : orc_get_sad(o, c->org_stride, r, c->ref_stride, c->w,
+                                 c->h, c->hbd);
+  } else {
+    /* predict_inter / get_params, src/predict.rs:267-283 (luma: dec 0) */
+    int ys = 3 + c->ref_ydec, xs = 3 + c->ref_xdec;
+    int roff = (int)mv.row >> ys, coff = (int)mv.col >> xs;
+    int rf = ((int)mv.row - (roff << ys)) << (4 - ys);
+    int cf = ((int)mv.col - (coff << xs)) << (4 - xs);
+    /* PlaneSlice::clamp, src/frame/plane.rs:521-533 */
+    int qx = c->po_x + coff - 3, qy = c->po_y + roff - 3;
+    if (qx > c->ref_width) qx = c->ref_width;
+    if (qx < -c->ref_xorigin) qx = -c->ref_xorigin;
+    if (qy > c->ref_height) qy = c->ref_height;
+    if (qy < -c->ref_yorigin) qy = -c->ref_yorigin;
+    const char *s = (const char *)c->ref +
+                    ((ptrdiff_t)(qy + 3) * c->ref_stride + (qx + 3)) * (ptrdiff_t)px;
+    uint16_t tmp[128 * 128];
+    orc_put_8tap(tmp, c->w, s, c->ref_stride, c->w, c->h, cf, rf, 0, 0,
+                 c->bit_depth, c->hbd, 0);
+    dist = c->satd ? orc_get_satd(o, c->org_stride, tmp, c->w, c->w, c->h,
+                                  c->hbd, 0)
+                   : orc_get_sad(o, c->org_stride, tmp, c->w, c->w, c->h,
+                                 c->hbd);
+  }
+  uint32_t r1 = orc_get_mv_rate(mv, c->pmv[0], c->allow_hp);
+  uint32_t r2 = orc_get_mv_rate(mv, c->pmv[1], c->allow_hp);
+  uint32_t rate = r1 < r2 + 1 ? r1 : r2 + 1;
+  return 256ull * dist + (uint64_t)rate * c->lambda;
+}
+
+/* diamond_me_search + get_best_predictor, src/me.rs:655-785. */
+void orc_diamond_search(const orc_ds_ctx *c, const orc_mv *pred, int n_pred,
+                        orc_mv *best_mv, uint64_t *best_cost) {
+  orc_mv center = {0, 0};
+  uint64_t center_cost = UINT64_MAX;
+  for (int p = 0; p < n_pred; p++) {
+    uint64_t cost = mv_rd_cost(c, pred[p]);
+    if (cost < center_cost) {
+      center = pred[p];
+      center_cost = cost;
+    }
+  }
+  static const int16_t pat[4][2] = {{1, 0}, {0, 1}, {-1, 0}, {0, -1}};
+  int16_t radius = c->subpel ? 4 : 16;
+  int16_t radius_end = c->subpel ? (c->allow_hp ? 1 : 2) : 8;
+  for (;;) {
+    uint64_t best = UINT64_MAX;
+    orc_mv bmv = {0, 0};
+    for (int p = 0; p < 4; p++) {
+      orc_mv cand = {(int16_t)(center.row + radius * pat[p][0]),
+                     (int16_t)(center.col + radius * pat[p][1])};
+      uint64_t cost = mv_rd_cost(c, cand);
+      if (cost < best) {
+        best = cost;
+        bmv = cand;
+      }
+    }
+    if (center_cost <= best) {
+      if (radius == radius_end) break;
+      radius /= 2;
+    } else {
+      center = bmv;
+      center_cost = best;
+    }
+  }
+  *best_mv = center;
+  *best_cost = center_cost;
+}

@@ -100,6 +100,25 @@ void orc_full_search(const void *org, ptrdiff_t org_stride, const void *ref,
                      orc_mv pmv1, int allow_hp, orc_mv *best_mv,
                      uint64_t *lowest_cost);
 
+/* diamond_me_search (src/me.rs:655-856).  org / ref point at their
+ * plane's data origin (visible (0,0)); the ref geometry feeds
+ * PlaneSlice::clamp for sub-pel prediction. */
+typedef struct {
+  const void *org;
+  ptrdiff_t org_stride;
+  const void *ref;
+  ptrdiff_t ref_stride;
+  int ref_width, ref_height, ref_xorigin, ref_yorigin, ref_xdec, ref_ydec;
+  int hbd, bit_depth;
+  int po_x, po_y, w, h;
+  int mvx_min, mvx_max, mvy_min, mvy_max;
+  orc_mv pmv[2];
+  uint32_t lambda;
+  int subpel, satd, allow_hp;
+} orc_ds_ctx;
+void orc_diamond_search(const orc_ds_ctx *c, const orc_mv *pred, int n_pred,
+                        orc_mv *best_mv, uint64_t *best_cost);
+
 /* ---- frame layout (src/frame/) --------------------------------------- */
 /* Plane::new geometry (src/frame/plane.rs:215-244). Writes
  * {stride, alloc_height, xorigin, yorigin}. */

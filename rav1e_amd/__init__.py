@@ -229,6 +229,9 @@ def _declare(L):
         "rv_replay_frame": (i32, [vp, i32]),
         "rv_replay_results": (i32, [vp, vp, i32]),
         "rv_replay_stage_times": (i32, [vp, vp, i32]),
+        "rv_replay_stage_times_sum": (i32, [vp, i32, vp, i32]),
+        "rv_replay_counters": (i32, [vp, vp, i32]),
+        "rv_diamond_search_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
         "rav1e_fwd_txfm_hip": (i32, [vp, vp, i32, i32, i32]),
         "rav1e_inv_txfm_add_hip": (i32, [vp, vp, C.c_ssize_t, i32, i32, i32]),
         "rv_sad_fn": (vp, [i32, i32, i32]),

@@ -1,19 +1,756 @@
-// rv_replay.hip -- hot-path replay driver (placeholder until the schedule
-// lands; see DESIGN.md "Replay driver").
+// rv_replay.hip -- hot-path replay driver: the per-frame call structure of
+// a speed-10 encode of one tile, for the stages this library accelerates,
+// with every frame resident in HBM.  Schedule (DESIGN.md "Replay driver"):
+//
+//   F0  hres / qres of the input (encode_frame, src/encoder.rs:3382-3385)
+//   F1  coarse ME: full_search at 1/4 res, 16x16 per 64x64 superblock and
+//       reference (estimate_motion_ss4, src/me.rs:1023-1075)
+//   F2  half-res diamond, 32x32 (estimate_motion_ss2 / me_ss2,
+//       src/me.rs:287-519)
+//   F3  full-res full-pel diamond then sub-pel diamond, 64x64
+//       (motion_estimation, src/me.rs:193-285)
+//   F4  RDO candidates per superblock: {sub-pel MV, zero MV} x reference:
+//       put_8tap luma + chroma, diff + forward DCT (TX_64X64 luma,
+//       TX_32X32 chroma), coefficient stand-in for quantize/dequantize,
+//       inverse transform + add, cdef-moment luma / SSE chroma distortion,
+//       argmin (encode_tx_block src/encoder.rs:1077-1237,
+//       compute_distortion src/rdo.rs:338-411)
+//   F5  8x8 importance SATD against reference 1 (compute_block_importances,
+//       src/api/internal.rs:823-1010)
+//
+// Every stage is one batched launch over all superblocks of the tile; the
+// glue between dependent stages (job lists built from the previous
+// stage's results) runs on the device, so a frame is a single stream of
+// launches with no host round trip.  The CPU baseline (oracle/orc_replay.c)
+// runs the same schedule and must produce the same result words.
+#include <string.h>
+
+#include <vector>
+
 #include "rv_device.h"
 
-struct rv_replay {
-  int dummy;
+// rv_me_diamond.hip: the public batch entry plus an evaluation counter
+int rv_diamond_search_batch_counted(const rv_plane *org, const rv_plane *ref,
+                                    const rv_ds_job *d_jobs, int n, int blk_w, int blk_h,
+                                    int subpixel, int use_satd, int allow_hp, int bit_depth,
+                                    rv_fs_result *d_out, unsigned long long *evals,
+                                    void *stream);
+
+namespace rv {
+
+constexpr int kSb = 64;
+constexpr int kQstep = 8;  // quantize/dequantize stand-in
+
+struct Geo {
+  int W, H, xdec, ydec, bd, hbd;
+  int w_in_b, h_in_b;       // MiCols / MiRows (src/encoder.rs:580-581)
+  int tx0, ty0, tw, th;     // tile rect in superblocks
+  int mi_w, mi_h;           // tile size in 4x4 units (tile_state.rs:93)
+  int nsb, R, C, nctx;      // superblocks, references, candidates, nsb * C
+  int cw, ch;               // chroma block of a superblock
 };
 
+__host__ __device__ inline int div_trunc8(int v) { return v / 8; }
+
+// get_mv_range (src/me.rs:64-80); bo in 4x4 units (frame).  Rust usize
+// arithmetic wraps and is cast back to isize, i.e. signed here.
+__host__ __device__ inline void mv_range(const Geo &g, int bx, int by, int bw,
+                                         int bh, int r[4]) {
+  const int border_w = 128 + bw * 8, border_h = 128 + bh * 8;
+  r[0] = -bx * 32 - border_w;
+  r[1] = (g.w_in_b - bx - bw / 4) * 32 + border_w;
+  r[2] = -by * 32 - border_h;
+  r[3] = (g.h_in_b - by - bh / 4) * 32 + border_h;
+}
+// adjust_bo (src/me.rs:993-1004) on tile-relative 4x4 offsets
+__host__ __device__ inline void adjust_bo(const Geo &g, int &bx, int &by,
+                                          int bw, int bh) {
+  int x = bx < g.mi_w - bw / 4 ? bx : g.mi_w - bw / 4;
+  int y = by < g.mi_h - bh / 4 ? by : g.mi_h - bh / 4;
+  bx = x > 0 ? x : 0;
+  by = y > 0 ? y : 0;
+}
+__host__ __device__ inline uint32_t pack_mv(rv_mv m) {
+  return ((uint32_t)(uint16_t)m.row << 16) | (uint16_t)m.col;
+}
+__host__ __device__ inline rv_mv qfull(rv_mv m) {  // quantize_to_fullpel
+  return rv_mv{(int16_t)((m.row / 8) * 8), (int16_t)((m.col / 8) * 8)};
+}
+
+// ---- device glue -----------------------------------------------------------
+// F2 jobs from F1 results: one thread per (superblock, reference)
+__global__ void make_ss2_jobs(Geo g, const rv_fs_result *coarse, uint32_t lambda,
+                              rv_ds_job *jobs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // r * nsb + sb
+  if (i >= g.nsb * g.R) return;
+  const int sb = i % g.nsb;
+  int bx = (sb % g.tw) * 16, by = (sb / g.tw) * 16;
+  adjust_bo(g, bx, by, 64, 64);
+  const int fbx = bx + g.tx0 * 16, fby = by + g.ty0 * 16;
+  int r[4];
+  mv_range(g, fbx, fby, 64, 64, r);
+  rv_ds_job j;
+  memset(&j, 0, sizeof(j));
+  j.po_x = fbx * 2;  // (bo << BLOCK_TO_PLANE_SHIFT) >> 1
+  j.po_y = fby * 2;
+  j.mvx_min = r[0] >> 1;
+  j.mvx_max = r[1] >> 1;
+  j.mvy_min = r[2] >> 1;
+  j.mvy_max = r[3] >> 1;
+  j.lambda = lambda;
+  j.n_pred = 1 + g.R;  // zero + the coarse MVs of every reference
+  j.pred[0] = rv_mv{0, 0};
+  for (int k = 0; k < g.R; k++) {
+    const rv_mv c = coarse[k * g.nsb + sb].best_mv;
+    const rv_mv cm{(int16_t)(c.row * 4), (int16_t)(c.col * 4)};
+    const rv_mv q = qfull(cm);
+    j.pred[1 + k] = rv_mv{(int16_t)(q.row >> 1), (int16_t)(q.col >> 1)};
+  }
+  jobs[i] = j;
+}
+
+// F3 full-pel jobs from F2 results
+__global__ void make_full_jobs(Geo g, const rv_fs_result *half, uint32_t lambda,
+                               rv_ds_job *jobs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // r * nsb + sb
+  if (i >= g.nsb * g.R) return;
+  const int sb = i % g.nsb;
+  const int fbx = (sb % g.tw + g.tx0) * 16, fby = (sb / g.tw + g.ty0) * 16;
+  int r[4];
+  mv_range(g, fbx, fby, 64, 64, r);
+  rv_ds_job j;
+  memset(&j, 0, sizeof(j));
+  j.po_x = fbx * 4;
+  j.po_y = fby * 4;
+  j.mvx_min = r[0];
+  j.mvx_max = r[1];
+  j.mvy_min = r[2];
+  j.mvy_max = r[3];
+  j.lambda = lambda;
+  const rv_mv h = half[i].best_mv;
+  j.n_pred = 2;
+  j.pred[0] = rv_mv{0, 0};
+  j.pred[1] = qfull(rv_mv{(int16_t)(h.row * 2), (int16_t)(h.col * 2)});
+  jobs[i] = j;
+}
+
+// F3 sub-pel jobs: same block, the full-pel winner as the only predictor
+__global__ void make_subpel_jobs(int n, const rv_fs_result *full, rv_ds_job *jobs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  rv_ds_job j = jobs[i];
+  j.n_pred = 1;
+  j.pred[0] = full[i].best_mv;
+  jobs[i] = j;
+}
+
+// predict_inter / get_params (src/predict.rs:267-283) for plane geometry p
+__device__ inline rv_mc_job mc_job_for(const rv_plane &p, int po_x, int po_y,
+                                       rv_mv mv, int dst_x, int dst_y) {
+  const int ys = 3 + p.ydec, xs = 3 + p.xdec;
+  const int roff = (int)mv.row >> ys, coff = (int)mv.col >> xs;
+  rv_mc_job m;
+  m.row_frac = ((int)mv.row - (roff << ys)) << (4 - ys);
+  m.col_frac = ((int)mv.col - (coff << xs)) << (4 - xs);
+  m.src_x = clampi(po_x + coff - 3, -p.xorigin, p.width) + 3;
+  m.src_y = clampi(po_y + roff - 3, -p.yorigin, p.height) + 3;
+  m.dst_x = dst_x;
+  m.dst_y = dst_y;
+  return m;
+}
+
+// F4 MC jobs: candidate c = 2 * ref + k (k 0: sub-pel MV, 1: zero MV).
+// Candidate c of superblock (sx, sy) predicts into the tall scratch plane
+// at (sx * bw, (c * th + sy) * bh).  One array per reference and plane.
+__global__ void make_mc_jobs(Geo g, const rv_fs_result *sub, rv_plane luma,
+                             rv_plane chroma, rv_mc_job *ljobs, rv_mc_job *cjobs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over nsb * C
+  if (i >= g.nsb * g.C) return;
+  const int c = i / g.nsb, sb = i - c * g.nsb;
+  const int r = c >> 1, k = c & 1;
+  const int sx = sb % g.tw, sy = sb / g.tw;
+  const rv_mv mv = k ? rv_mv{0, 0} : sub[r * g.nsb + sb].best_mv;
+  const int px = (sx + g.tx0) * kSb, py = (sy + g.ty0) * kSb;
+  // job arrays are grouped by reference: [r][k][sb]
+  const int o = (r * 2 + k) * g.nsb + sb;
+  ljobs[o] = mc_job_for(luma, px, py, mv, sx * kSb, (c * g.th + sy) * kSb);
+  cjobs[o] = mc_job_for(chroma, px >> chroma.xdec, py >> chroma.ydec, mv, sx * g.cw,
+                        (c * g.th + sy) * g.ch);
+}
+
+// quantize/dequantize stand-in + coefficient compaction: the top-left
+// min(W,32) x min(H,32) of each W-stride raster, each value replaced by
+// (v / kQstep) * kQstep (truncating), packed with row stride min(W,32).
+// Also folds a position-weighted checksum of the packed coefficients.
+__global__ void pack_coeffs(const int32_t *raster, int n, int tw, int th,
+                            int32_t *packed, unsigned long long *csum) {
+  const int cw = tw < 32 ? tw : 32, ch = th < 32 ? th : 32;
+  const int64_t total = (int64_t)n * cw * ch;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t s = 0;
+  if (i < total) {
+    const int64_t b = i / (cw * ch);
+    const int e = (int)(i - b * cw * ch);
+    const int r = e / cw, c = e - r * cw;
+    const int32_t v = raster[b * tw * th + r * tw + c];
+    const int32_t q = (v / kQstep) * kQstep;
+    packed[i] = q;
+    s = (uint64_t)(int64_t)q * (uint64_t)(e + 1);
+  }
+  s = group_sum<64>(s);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(csum, (unsigned long long)s);
+}
+
+// Candidate score = luma SSE (from the cdef moments) + chroma SSE, then the
+// per-superblock argmin (first minimum) and result words.
+__global__ void score_candidates(Geo g, const int64_t *lmom, const uint64_t *usse,
+                                 const uint64_t *vsse, int lsub, int csub,
+                                 const rv_fs_result *coarse, const rv_fs_result *half,
+                                 const rv_fs_result *full, const rv_fs_result *sub,
+                                 uint64_t *words) {
+  const int sb = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sb >= g.nsb) return;
+  uint64_t best = ~0ull;
+  int best_c = 0;
+  for (int c = 0; c < g.C; c++) {
+    const int o = c * g.nsb + sb;  // candidate-major, like the MC jobs
+    uint64_t s = 0;
+    for (int k = 0; k < lsub; k++) {
+      const int64_t *m = lmom + ((int64_t)o * lsub + k) * 5;
+      s += (uint64_t)(m[3] + m[2] - 2 * m[4]);
+    }
+    for (int k = 0; k < csub; k++) s += usse[(int64_t)o * csub + k] + vsse[(int64_t)o * csub + k];
+    if (s < best) {
+      best = s;
+      best_c = c;
+    }
+  }
+  uint64_t *w = words + (int64_t)sb * (8 * g.R + 2);
+  for (int r = 0; r < g.R; r++) {
+    const int i = r * g.nsb + sb;
+    w[8 * r + 0] = pack_mv(coarse[i].best_mv);
+    w[8 * r + 1] = coarse[i].cost;
+    w[8 * r + 2] = pack_mv(half[i].best_mv);
+    w[8 * r + 3] = half[i].cost;
+    w[8 * r + 4] = pack_mv(full[i].best_mv);
+    w[8 * r + 5] = full[i].cost;
+    w[8 * r + 6] = pack_mv(sub[i].best_mv);
+    w[8 * r + 7] = sub[i].cost;
+  }
+  w[8 * g.R] = (uint64_t)best_c;
+  w[8 * g.R + 1] = best;
+}
+
+// F5 jobs: every 8x8 luma block of the tile inside the frame, against
+// reference 1 at the full-pel part of its superblock's sub-pel MV.
+__global__ void make_imp_jobs(Geo g, const rv_fs_result *sub, rv_dist_job *jobs,
+                              int nbx, int nby) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nbx * nby) return;
+  const int bx = i % nbx, by = i / nbx;
+  const int sb = (by / 8) * g.tw + (bx / 8);
+  const rv_mv mv = sub[sb].best_mv;  // reference 1 (ref-major index 0)
+  const int x = g.tx0 * kSb + bx * 8, y = g.ty0 * kSb + by * 8;
+  rv_dist_job j;
+  j.org_x = x;
+  j.org_y = y;
+  j.ref_x = x + ((int)mv.col >> 3);
+  j.ref_y = y + ((int)mv.row >> 3);
+  jobs[i] = j;
+}
+
+__global__ void sum_u32(const uint32_t *v, int n, unsigned long long *out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t s = i < n ? v[i] : 0;
+  s = group_sum<64>(s);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, (unsigned long long)s);
+}
+
+// Sum of the reconstructed pixels of a plane region (all candidates).
+template <typename Px>
+__global__ void sum_plane(rv_plane p, int w, int h, unsigned long long *out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t s = 0;
+  if (i < (int64_t)w * h) {
+    const int y = (int)(i / w), x = (int)(i - (int64_t)y * w);
+    s = *plane_ptr<Px>(p, x, y);
+  }
+  s = group_sum<64>(s);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, (unsigned long long)s);
+}
+
+}  // namespace rv
+
+using namespace rv;
+
+struct RvFrameSlot {
+  rv_plane y, u, v, hres, qres;
+  void *mem = nullptr;
+};
+
+struct rv_replay {
+  rv_replay_cfg cfg;
+  Geo g;
+  hipStream_t stream;
+  bool own_stream;
+  double me_lambda;
+  std::vector<RvFrameSlot> slots;  // 0 = input, 1..R = references
+  // scratch
+  rv_plane tall_y, tall_u, tall_v;
+  void *tall_mem = nullptr;
+  std::vector<void *> allocs;
+  rv_fs_job *fs_jobs[3] = {nullptr, nullptr, nullptr};  // per scale 1, 2, 4
+  rv_fs_result *coarse, *half, *full, *sub;
+  rv_ds_job *ds_jobs;
+  rv_mc_job *l_mc, *c_mc;
+  rv_tx_job *l_tx, *c_tx;
+  rv_dist_job *l_dist, *c_dist, *imp_jobs;
+  int32_t *l_raster, *c_raster, *l_packed, *c_packed;
+  int64_t *l_mom;
+  uint64_t *u_sse, *v_sse, *words;
+  uint32_t *imp_satd;
+  unsigned long long *tail;  // [coeff csum, recon csum, imp satd sum]
+  int n_ctx, n_imp, imp_bx, imp_by, lsub, csub;
+  // Event ring: frame f records into set f % kRing (0..6 stage bounds,
+  // 7..14 kernel brackets), so per-kernel times can be summed over a whole
+  // timed run without a host sync per frame.
+  static constexpr int kRing = 64;
+  hipEvent_t evs[kRing][16];
+  hipEvent_t *ev;
+  long frames = 0;
+  unsigned long long *ds_evals;  // diamond candidate evaluations [full, sub]
+};
+
+namespace {
+
+void *dalloc(rv_replay *r, size_t bytes) {
+  void *p = nullptr;
+  if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
+  r->allocs.push_back(p);
+  return p;
+}
+
+bool alloc_slot(rv_replay *r, RvFrameSlot &s) {
+  const Geo &g = r->g;
+  // Frame::new (src/frame/mod.rs:55-90): luma pad 64 + 24, chroma >> dec
+  const int pad = 88;
+  const int cw = (g.W + g.xdec) >> g.xdec, ch = (g.H + g.ydec) >> g.ydec;
+  size_t by = rv_plane_geometry(&s.y, g.W, g.H, 0, 0, pad, pad, g.hbd);
+  size_t bu = rv_plane_geometry(&s.u, cw, ch, g.xdec, g.ydec, pad >> g.xdec, pad >> g.ydec, g.hbd);
+  size_t bv = rv_plane_geometry(&s.v, cw, ch, g.xdec, g.ydec, pad >> g.xdec, pad >> g.ydec, g.hbd);
+  // input_hres / input_qres (src/encoder.rs:362-377)
+  size_t bh = rv_plane_geometry(&s.hres, g.W / 2, g.H / 2, 1, 1, pad / 2, pad / 2, g.hbd);
+  size_t bq = rv_plane_geometry(&s.qres, g.W / 4, g.H / 4, 2, 2, pad / 4, pad / 4, g.hbd);
+  const size_t al = 256;
+  auto up = [&](size_t v) { return (v + al - 1) / al * al; };
+  size_t total = up(by) + up(bu) + up(bv) + up(bh) + up(bq);
+  uint8_t *m = (uint8_t *)dalloc(r, total);
+  if (!m) return false;
+  s.mem = m;
+  s.y.data = m;
+  m += up(by);
+  s.u.data = m;
+  m += up(bu);
+  s.v.data = m;
+  m += up(bv);
+  s.hres.data = m;
+  m += up(bh);
+  s.qres.data = m;
+  return hipMemsetAsync(s.mem, 0, total, r->stream) == hipSuccess;
+}
+
+int build_static_jobs(rv_replay *r) {
+  const Geo &g = r->g;
+  // F1 coarse jobs for me_range_scale 1, 2, 4 (estimate_motion_ss4)
+  const uint32_t lambda4 = (uint32_t)(r->me_lambda * 256.0 / 16.0 * 0.125);
+  for (int si = 0; si < 3; si++) {
+    const int s = 1 << si;
+    std::vector<rv_fs_job> jobs(g.nsb * g.R);
+    for (int sb = 0; sb < g.nsb; sb++) {
+      int bx = (sb % g.tw) * 16, by = (sb / g.tw) * 16;
+      adjust_bo(g, bx, by, 64, 64);
+      const int fbx = bx + g.tx0 * 16, fby = by + g.ty0 * 16;
+      const int pox = fbx, poy = fby;  // (bo << 2) >> 2
+      const int range_x = 192 * s, range_y = 64 * s;
+      int mr[4];
+      mv_range(g, fbx, fby, 64, 64, mr);
+      auto mx = [](int a, int b) { return a > b ? a : b; };
+      auto mn = [](int a, int b) { return a < b ? a : b; };
+      rv_fs_job j;
+      memset(&j, 0, sizeof(j));
+      j.po_x = pox;
+      j.po_y = poy;
+      j.x_lo = pox + (mx(-range_x, div_trunc8(mr[0])) >> 2);
+      j.x_hi = pox + (mn(range_x, div_trunc8(mr[1])) >> 2);
+      j.y_lo = poy + (mx(-range_y, div_trunc8(mr[2])) >> 2);
+      j.y_hi = poy + (mn(range_y, div_trunc8(mr[3])) >> 2);
+      j.lambda = lambda4;
+      for (int k = 0; k < g.R; k++) jobs[k * g.nsb + sb] = j;  // ref-major
+    }
+    r->fs_jobs[si] = (rv_fs_job *)dalloc(r, jobs.size() * sizeof(rv_fs_job));
+    if (!r->fs_jobs[si]) return RV_EHIP;
+    if (hipMemcpy(r->fs_jobs[si], jobs.data(), jobs.size() * sizeof(rv_fs_job),
+                  hipMemcpyHostToDevice) != hipSuccess)
+      return RV_EHIP;
+  }
+  // F4 transform / distortion jobs (static: positions only)
+  const int ntx_c = (g.cw / 32) * (g.ch / 32);  // 32x32 chroma tx per plane
+  std::vector<rv_tx_job> ltx(g.nctx), ctx_(g.nctx * ntx_c);
+  std::vector<rv_dist_job> ld(g.nctx), cd(g.nctx);
+  for (int c = 0; c < g.C; c++)
+    for (int sb = 0; sb < g.nsb; sb++) {
+      const int o = c * g.nsb + sb;
+      const int sx = sb % g.tw, sy = sb / g.tw;
+      const int px = (sx + g.tx0) * kSb, py = (sy + g.ty0) * kSb;
+      const int tx = sx * kSb, ty = (c * g.th + sy) * kSb;
+      ltx[o] = rv_tx_job{px, py, tx, ty};
+      ld[o] = rv_dist_job{px, py, tx, ty};
+      const int cpx = px >> g.xdec, cpy = py >> g.ydec;
+      const int ctx0 = sx * g.cw, cty0 = (c * g.th + sy) * g.ch;
+      cd[o] = rv_dist_job{cpx, cpy, ctx0, cty0};
+      for (int t = 0; t < ntx_c; t++) {
+        const int ox = (t % (g.cw / 32)) * 32, oy = (t / (g.cw / 32)) * 32;
+        ctx_[o * ntx_c + t] = rv_tx_job{cpx + ox, cpy + oy, ctx0 + ox, cty0 + oy};
+      }
+    }
+  auto upload = [&](auto &vec, auto *&dst) -> int {
+    dst = (std::remove_reference_t<decltype(dst)>)dalloc(r, vec.size() * sizeof(vec[0]));
+    if (!dst) return RV_EHIP;
+    return hipMemcpy(dst, vec.data(), vec.size() * sizeof(vec[0]), hipMemcpyHostToDevice) ==
+                   hipSuccess
+               ? RV_OK
+               : RV_EHIP;
+  };
+  int e;
+  if ((e = upload(ltx, r->l_tx)) || (e = upload(ctx_, r->c_tx)) || (e = upload(ld, r->l_dist)) ||
+      (e = upload(cd, r->c_dist)))
+    return e;
+  return RV_OK;
+}
+
+}  // namespace
+
+#define RV_R(expr)                                        \
+  do {                                                    \
+    int e_ = (expr);                                      \
+    if (e_ != RV_OK) return e_;                           \
+  } while (0)
+#define RV_H(expr)                                                   \
+  do {                                                               \
+    hipError_t e_ = (expr);                                          \
+    if (e_ != hipSuccess) return rv_set_hip_error(e_, #expr);        \
+  } while (0)
+
 extern "C" {
-rv_replay *rv_replay_create(const rv_replay_cfg *, void *) {
-  rv_set_error(RV_ENOTSUP, "rv_replay_create: not built yet");
-  return nullptr;
+
+void rv_replay_destroy(rv_replay *r) {
+  if (!r) return;
+  for (void *p : r->allocs) (void)hipFree(p);
+  for (int f = 0; f < rv_replay::kRing; f++)
+    for (int i = 0; i < 16; i++)
+      if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
+  if (r->own_stream && r->stream) (void)hipStreamDestroy(r->stream);
+  delete r;
 }
-void rv_replay_destroy(rv_replay *) {}
-int rv_replay_set_frame(rv_replay *, int, const void *) { return RV_ENOTSUP; }
-int rv_replay_frame(rv_replay *, int) { return RV_ENOTSUP; }
-int rv_replay_results(rv_replay *, uint64_t *, int) { return RV_ENOTSUP; }
-int rv_replay_stage_times(rv_replay *, float *, int) { return RV_ENOTSUP; }
+
+rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
+  if (!cfg || cfg->width <= 0 || cfg->height <= 0 || (cfg->width & 7) ||
+      (cfg->height & 7) || (cfg->bit_depth != 8 && cfg->bit_depth != 10) ||
+      cfg->xdec < 0 || cfg->xdec > 1 || cfg->ydec < 0 || cfg->ydec > 1 ||
+      cfg->n_refs < 1 || cfg->n_refs > RV_DS_MAX_PRED - 1) {
+    rv_set_error(RV_EINVAL, "rv_replay_create: bad config");
+    return nullptr;
+  }
+  rv_replay *r = new rv_replay();
+  memset(r->evs, 0, sizeof(r->evs));
+  r->ev = r->evs[0];
+  r->cfg = *cfg;
+  Geo &g = r->g;
+  g.W = cfg->width;
+  g.H = cfg->height;
+  g.xdec = cfg->xdec;
+  g.ydec = cfg->ydec;
+  g.bd = cfg->bit_depth;
+  g.hbd = cfg->bit_depth > 8;
+  g.w_in_b = 2 * ((g.W + 7) >> 3);
+  g.h_in_b = 2 * ((g.H + 7) >> 3);
+  const int sbc = (g.W + kSb - 1) / kSb, sbr = (g.H + kSb - 1) / kSb;
+  g.tx0 = cfg->tile_x0;
+  g.ty0 = cfg->tile_y0;
+  g.tw = cfg->tile_w > 0 ? cfg->tile_w : sbc - g.tx0;
+  g.th = cfg->tile_h > 0 ? cfg->tile_h : sbr - g.ty0;
+  if (g.tx0 < 0 || g.ty0 < 0 || g.tw <= 0 || g.th <= 0 || g.tx0 + g.tw > sbc ||
+      g.ty0 + g.th > sbr) {
+    rv_set_error(RV_EINVAL, "rv_replay_create: bad tile");
+    delete r;
+    return nullptr;
+  }
+  const int vis_w = (g.W - g.tx0 * kSb) < g.tw * kSb ? g.W - g.tx0 * kSb : g.tw * kSb;
+  const int vis_h = (g.H - g.ty0 * kSb) < g.th * kSb ? g.H - g.ty0 * kSb : g.th * kSb;
+  g.mi_w = vis_w >> 2;
+  g.mi_h = vis_h >> 2;
+  g.nsb = g.tw * g.th;
+  g.R = cfg->n_refs;
+  g.C = 2 * g.R;
+  g.nctx = g.nsb * g.C;
+  g.cw = kSb >> g.xdec;
+  g.ch = kSb >> g.ydec;
+  // me_lambda = sqrt(lambda), lambda scaled by 1 << 2 (bd - 8)
+  // (src/encoder.rs:876-878); the replay fixes the 8-bit value.
+  r->me_lambda = 24.0 * (double)(1 << (g.bd - 8));
+  if (stream) {
+    r->stream = (hipStream_t)stream;
+    r->own_stream = false;
+  } else {
+    r->own_stream = true;
+    if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess) {
+      rv_set_error(RV_EHIP, "rv_replay_create: stream");
+      delete r;
+      return nullptr;
+    }
+  }
+  bool ok = true;
+  r->slots.resize(g.R + 1);
+  for (auto &s : r->slots) ok = ok && alloc_slot(r, s);
+  // tall scratch planes: candidate c of superblock (sx, sy) at
+  // (sx * bw, (c * th + sy) * bh)
+  size_t by = rv_plane_geometry(&r->tall_y, g.tw * kSb, g.C * g.th * kSb, 0, 0, 0, 0, g.hbd);
+  size_t bu = rv_plane_geometry(&r->tall_u, g.tw * g.cw, g.C * g.th * g.ch, g.xdec, g.ydec, 0, 0,
+                                g.hbd);
+  r->tall_v = r->tall_u;
+  r->tall_y.data = dalloc(r, by);
+  r->tall_u.data = dalloc(r, bu);
+  r->tall_v.data = dalloc(r, bu);
+  const int ntx_c = (g.cw / 32) * (g.ch / 32);
+  const int nr = g.nsb * g.R;
+  r->coarse = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
+  r->half = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
+  r->full = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
+  r->sub = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
+  r->ds_jobs = (rv_ds_job *)dalloc(r, nr * sizeof(rv_ds_job));
+  r->l_mc = (rv_mc_job *)dalloc(r, g.nctx * sizeof(rv_mc_job));
+  r->c_mc = (rv_mc_job *)dalloc(r, g.nctx * sizeof(rv_mc_job));
+  r->l_raster = (int32_t *)dalloc(r, (size_t)g.nctx * 4096 * 4);
+  r->c_raster = (int32_t *)dalloc(r, (size_t)g.nctx * ntx_c * 1024 * 4 * 2);
+  r->l_packed = (int32_t *)dalloc(r, (size_t)g.nctx * 1024 * 4);
+  r->c_packed = (int32_t *)dalloc(r, (size_t)g.nctx * ntx_c * 1024 * 4 * 2);
+  r->lsub = (kSb / 8) * (kSb / 8);
+  {
+    const int bw = (g.cw < 8 ? g.cw : 8) >> g.xdec, bh = (g.ch < 8 ? g.ch : 8) >> g.ydec;
+    r->csub = (g.cw / bw) * (g.ch / bh);
+  }
+  r->l_mom = (int64_t *)dalloc(r, (size_t)g.nctx * r->lsub * 5 * 8);
+  r->u_sse = (uint64_t *)dalloc(r, (size_t)g.nctx * r->csub * 8);
+  r->v_sse = (uint64_t *)dalloc(r, (size_t)g.nctx * r->csub * 8);
+  r->words = (uint64_t *)dalloc(r, (size_t)g.nsb * (8 * g.R + 2) * 8);
+  r->imp_bx = vis_w / 8;
+  r->imp_by = vis_h / 8;
+  r->n_imp = r->imp_bx * r->imp_by;
+  r->imp_jobs = (rv_dist_job *)dalloc(r, (size_t)r->n_imp * sizeof(rv_dist_job));
+  r->imp_satd = (uint32_t *)dalloc(r, (size_t)r->n_imp * 4);
+  r->tail = (unsigned long long *)dalloc(r, 4 * 8);
+  for (int f = 0; f < rv_replay::kRing; f++)
+    for (int i = 0; i < 16; i++) ok = ok && hipEventCreate(&r->evs[f][i]) == hipSuccess;
+  r->ds_evals = (unsigned long long *)dalloc(r, 4 * 8);
+  ok = ok && r->ds_evals && hipMemsetAsync(r->ds_evals, 0, 4 * 8, r->stream) == hipSuccess;
+  ok = ok && r->tall_y.data && r->tall_u.data && r->tall_v.data && r->tail;
+  if (!ok || build_static_jobs(r) != RV_OK) {
+    rv_set_error(RV_EHIP, "rv_replay_create: device allocation failed");
+    rv_replay_destroy(r);
+    return nullptr;
+  }
+  if (hipStreamSynchronize(r->stream) != hipSuccess) {
+    rv_replay_destroy(r);
+    return nullptr;
+  }
+  return r;
 }
+
+static int upload_plane(rv_replay *r, const rv_plane &p, const uint8_t *src) {
+  const int px = p.hbd ? 2 : 1;
+  uint8_t *dst = (uint8_t *)p.data + ((size_t)p.yorigin * p.stride + p.xorigin) * px;
+  RV_H(hipMemcpy2DAsync(dst, (size_t)p.stride * px, src, (size_t)p.width * px,
+                        (size_t)p.width * px, p.height, hipMemcpyHostToDevice, r->stream));
+  return rv_plane_pad(&p, r->stream);
+}
+
+int rv_replay_set_frame(rv_replay *r, int slot, const void *host_yuv) {
+  if (!r || !host_yuv || slot < 0 || slot > r->g.R)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_frame: bad slot");
+  RvFrameSlot &s = r->slots[slot];
+  const int px = r->g.hbd ? 2 : 1;
+  const uint8_t *p = (const uint8_t *)host_yuv;
+  RV_R(upload_plane(r, s.y, p));
+  p += (size_t)s.y.width * s.y.height * px;
+  RV_R(upload_plane(r, s.u, p));
+  p += (size_t)s.u.width * s.u.height * px;
+  RV_R(upload_plane(r, s.v, p));
+  RV_R(rv_plane_downsample(&s.hres, &s.y, r->stream));
+  RV_R(rv_plane_downsample(&s.qres, &s.hres, r->stream));
+  RV_H(hipStreamSynchronize(r->stream));
+  return RV_OK;
+}
+
+int rv_replay_frame(rv_replay *r, int me_range_scale) {
+  if (!r || (me_range_scale != 1 && me_range_scale != 2 && me_range_scale != 4))
+    return rv_set_error(RV_EINVAL, "rv_replay_frame: bad me_range_scale");
+  const Geo &g = r->g;
+  hipStream_t st = r->stream;
+  RvFrameSlot &cur = r->slots[0];
+  const int nr = g.nsb;  // jobs per reference
+  const int T = 256;
+  auto blocks = [](int64_t n) { return (unsigned)((n + 255) / 256); };
+  const int si = me_range_scale == 1 ? 0 : me_range_scale == 2 ? 1 : 2;
+  const uint32_t lambda2 = (uint32_t)(r->me_lambda * 256.0 / 4.0 * 0.125);
+  const uint32_t lambda1 = (uint32_t)(r->me_lambda * 256.0 * 0.5);
+
+  r->ev = r->evs[r->frames % rv_replay::kRing];
+  r->frames++;
+  RV_H(hipEventRecord(r->ev[0], st));
+  RV_H(hipMemsetAsync(r->tail, 0, 4 * 8, st));
+  // F0 (encode_frame, src/encoder.rs:3382-3385)
+  RV_R(rv_plane_downsample(&cur.hres, &cur.y, st));
+  RV_R(rv_plane_downsample(&cur.qres, &cur.hres, st));
+  RV_H(hipEventRecord(r->ev[1], st));
+  // F1 coarse full search per reference
+  for (int k = 0; k < g.R; k++)
+    RV_R(rv_full_search_batch(&cur.qres, &r->slots[1 + k].qres, r->fs_jobs[si] + k * nr, nr, 16,
+                              16, 1, 0, r->coarse + k * nr, st));
+  RV_H(hipEventRecord(r->ev[2], st));  // = the full-search kernel bracket
+  // F2 half-res diamond
+  make_ss2_jobs<<<blocks(nr * g.R), T, 0, st>>>(g, r->coarse, lambda2, r->ds_jobs);
+  for (int k = 0; k < g.R; k++)
+    RV_R(rv_diamond_search_batch(&cur.hres, &r->slots[1 + k].hres, r->ds_jobs + k * nr, nr, 32,
+                                 32, 0, 0, 0, g.bd, r->half + k * nr, st));
+  RV_H(hipEventRecord(r->ev[3], st));
+  // F3 full-res full-pel + sub-pel diamond (speed 10: SAD, no hp)
+  make_full_jobs<<<blocks(nr * g.R), T, 0, st>>>(g, r->half, lambda1, r->ds_jobs);
+  for (int k = 0; k < g.R; k++)
+    RV_R(rv_diamond_search_batch_counted(&cur.y, &r->slots[1 + k].y, r->ds_jobs + k * nr, nr, 64,
+                                         64, 0, 0, 0, g.bd, r->full + k * nr, r->ds_evals, st));
+  make_subpel_jobs<<<blocks(nr * g.R), T, 0, st>>>(nr * g.R, r->full, r->ds_jobs);
+  for (int k = 0; k < g.R; k++)
+    RV_R(rv_diamond_search_batch_counted(&cur.y, &r->slots[1 + k].y, r->ds_jobs + k * nr, nr, 64,
+                                         64, 1, 0, 0, g.bd, r->sub + k * nr, r->ds_evals + 1,
+                                         st));
+  RV_H(hipEventRecord(r->ev[4], st));
+  // F4 RDO candidates
+  make_mc_jobs<<<blocks(g.nctx), T, 0, st>>>(g, r->sub, cur.y, cur.u, r->l_mc, r->c_mc);
+  RV_H(hipEventRecord(r->ev[7], st));
+  for (int k = 0; k < g.R; k++) {  // luma put_8tap: kernel bracket 7..8
+    const int o = k * 2 * nr;        // both candidates of reference k
+    RV_R(rv_put_8tap_batch(&r->tall_y, &r->slots[1 + k].y, r->l_mc + o, 2 * nr, kSb, kSb, 0, 0,
+                           g.bd, st));
+  }
+  RV_H(hipEventRecord(r->ev[8], st));
+  for (int k = 0; k < g.R; k++) {
+    const RvFrameSlot &ref = r->slots[1 + k];
+    const int o = k * 2 * nr;
+    RV_R(rv_put_8tap_batch(&r->tall_u, &ref.u, r->c_mc + o, 2 * nr, g.cw, g.ch, 0, 0, g.bd, st));
+    RV_R(rv_put_8tap_batch(&r->tall_v, &ref.v, r->c_mc + o, 2 * nr, g.cw, g.ch, 0, 0, g.bd, st));
+  }
+  const int ntx_c = (g.cw / 32) * (g.ch / 32);
+  const int nct = g.nctx * ntx_c;
+  int32_t *u_raster = r->c_raster, *v_raster = r->c_raster + (size_t)nct * 1024;
+  int32_t *u_packed = r->c_packed, *v_packed = r->c_packed + (size_t)nct * 1024;
+  RV_H(hipEventRecord(r->ev[9], st));  // luma diff + fwd TX_64X64: 9..10
+  RV_R(rv_diff_fwd_txfm_batch(&cur.y, &r->tall_y, r->l_tx, g.nctx, 4, 0, g.bd, r->l_raster, st));
+  RV_H(hipEventRecord(r->ev[10], st));
+  RV_R(rv_diff_fwd_txfm_batch(&cur.u, &r->tall_u, r->c_tx, nct, 3, 0, g.bd, u_raster, st));
+  RV_R(rv_diff_fwd_txfm_batch(&cur.v, &r->tall_v, r->c_tx, nct, 3, 0, g.bd, v_raster, st));
+  pack_coeffs<<<blocks((int64_t)g.nctx * 1024), T, 0, st>>>(r->l_raster, g.nctx, 64, 64,
+                                                             r->l_packed, r->tail);
+  pack_coeffs<<<blocks((int64_t)nct * 1024), T, 0, st>>>(u_raster, nct, 32, 32, u_packed,
+                                                         r->tail);
+  pack_coeffs<<<blocks((int64_t)nct * 1024), T, 0, st>>>(v_raster, nct, 32, 32, v_packed,
+                                                         r->tail);
+  RV_H(hipEventRecord(r->ev[11], st));  // luma inverse TX_64X64 + add: 11..12
+  RV_R(rv_inv_txfm_add_batch(r->l_packed, &r->tall_y, r->l_tx, g.nctx, 4, 0, g.bd, st));
+  RV_H(hipEventRecord(r->ev[12], st));
+  RV_R(rv_inv_txfm_add_batch(u_packed, &r->tall_u, r->c_tx, nct, 3, 0, g.bd, st));
+  RV_R(rv_inv_txfm_add_batch(v_packed, &r->tall_v, r->c_tx, nct, 3, 0, g.bd, st));
+  RV_H(hipEventRecord(r->ev[13], st));  // luma cdef moments: 13..14
+  RV_R(rv_cdef_moments_batch(&cur.y, &r->tall_y, r->l_dist, g.nctx, kSb, kSb, r->l_mom, st));
+  RV_H(hipEventRecord(r->ev[14], st));
+  RV_R(rv_sse_batch(&cur.u, &r->tall_u, r->c_dist, g.nctx, g.cw, g.ch, r->u_sse, st));
+  RV_R(rv_sse_batch(&cur.v, &r->tall_v, r->c_dist, g.nctx, g.cw, g.ch, r->v_sse, st));
+  score_candidates<<<blocks(g.nsb), T, 0, st>>>(g, r->l_mom, r->u_sse, r->v_sse, r->lsub, r->csub,
+                                                r->coarse, r->half, r->full, r->sub, r->words);
+  if (g.hbd) {
+    sum_plane<uint16_t><<<blocks((int64_t)r->tall_y.width * r->tall_y.height), T, 0, st>>>(
+        r->tall_y, r->tall_y.width, r->tall_y.height, r->tail + 1);
+    sum_plane<uint16_t><<<blocks((int64_t)r->tall_u.width * r->tall_u.height), T, 0, st>>>(
+        r->tall_u, r->tall_u.width, r->tall_u.height, r->tail + 1);
+    sum_plane<uint16_t><<<blocks((int64_t)r->tall_v.width * r->tall_v.height), T, 0, st>>>(
+        r->tall_v, r->tall_v.width, r->tall_v.height, r->tail + 1);
+  } else {
+    sum_plane<uint8_t><<<blocks((int64_t)r->tall_y.width * r->tall_y.height), T, 0, st>>>(
+        r->tall_y, r->tall_y.width, r->tall_y.height, r->tail + 1);
+    sum_plane<uint8_t><<<blocks((int64_t)r->tall_u.width * r->tall_u.height), T, 0, st>>>(
+        r->tall_u, r->tall_u.width, r->tall_u.height, r->tail + 1);
+    sum_plane<uint8_t><<<blocks((int64_t)r->tall_v.width * r->tall_v.height), T, 0, st>>>(
+        r->tall_v, r->tall_v.width, r->tall_v.height, r->tail + 1);
+  }
+  RV_H(hipEventRecord(r->ev[5], st));
+  // F5 importance SATD against reference 1
+  make_imp_jobs<<<blocks(r->n_imp), T, 0, st>>>(g, r->sub, r->imp_jobs, r->imp_bx, r->imp_by);
+  RV_R(rv_satd_batch(&cur.y, &r->slots[1].y, r->imp_jobs, r->n_imp, 8, 8, r->imp_satd, st));
+  sum_u32<<<blocks(r->n_imp), T, 0, st>>>(r->imp_satd, r->n_imp, r->tail + 2);
+  RV_H(hipEventRecord(r->ev[6], st));
+  RV_H(hipGetLastError());
+  return RV_OK;
+}
+
+int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap) {
+  if (!r || !host_out) return rv_set_error(RV_EINVAL, "rv_replay_results: null");
+  const Geo &g = r->g;
+  const int nw = g.nsb * (8 * g.R + 2);
+  const int total = nw + 4;
+  if (cap < total) return rv_set_error(RV_EINVAL, "rv_replay_results: cap too small");
+  RV_H(hipMemcpyAsync(host_out, r->words, (size_t)nw * 8, hipMemcpyDeviceToHost, r->stream));
+  RV_H(hipMemcpyAsync(host_out + nw, r->tail, 3 * 8, hipMemcpyDeviceToHost, r->stream));
+  RV_H(hipStreamSynchronize(r->stream));
+  host_out[nw + 3] = (uint64_t)r->n_imp;
+  return total;
+}
+
+static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
+  if (!r || !ms_out) return rv_set_error(RV_EINVAL, "rv_replay_stage_times: null");
+  if (r->frames == 0) return rv_set_error(RV_EINVAL, "rv_replay_stage_times: no frame");
+  if (last < 1) last = 1;
+  if (last > rv_replay::kRing) last = rv_replay::kRing;
+  if (last > r->frames) last = (int)r->frames;
+  for (int i = 0; i < cap && i < 10; i++) ms_out[i] = 0.f;
+  int n = 0;
+  for (int f = 0; f < last; f++) {
+    hipEvent_t *e = r->evs[(r->frames - 1 - f) % rv_replay::kRing];
+    RV_H(hipEventSynchronize(e[6]));
+    n = 0;
+    for (int i = 0; i < 6 && n < cap; i++) {  // stages F0..F5
+      float ms = 0.f;
+      RV_H(hipEventElapsedTime(&ms, e[i], e[i + 1]));
+      ms_out[n++] += ms;
+    }
+    for (int i = 7; i < 15 && n < cap; i += 2) {  // luma put, fwd, inv, cdef
+      float ms = 0.f;
+      RV_H(hipEventElapsedTime(&ms, e[i], e[i + 1]));
+      ms_out[n++] += ms;
+    }
+  }
+  return n;
+}
+
+int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap) {
+  return stage_times(r, ms_out, cap, 1);
+}
+int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out, int cap) {
+  return stage_times(r, ms_out, cap, last_frames);
+}
+int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
+  if (!r || !out || cap < 2) return rv_set_error(RV_EINVAL, "rv_replay_counters");
+  RV_H(hipStreamSynchronize(r->stream));
+  RV_H(hipMemcpy(out, r->ds_evals, 2 * 8, hipMemcpyDeviceToHost));
+  return 2;
+}
+
+}  // extern "C"

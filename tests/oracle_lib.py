@@ -201,3 +201,44 @@ def full_search(org_full, ref_full, xorigin, yorigin, job, blk_w, blk_h, step, a
                       _Mv(int(job["pmv1_row"]), int(job["pmv1_col"])), allow_hp,
                       C.byref(best), C.byref(cost))
     return (best.row, best.col), cost.value
+
+
+class CpuReplay:
+    """orc_replay_* (oracle/orc_replay.c): the replay schedule on the CPU."""
+
+    def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, tile=None,
+                 threads=1):
+        L = lib()
+        L.orc_replay_create.restype = C.c_void_p
+        L.orc_replay_create.argtypes = [C.c_int] * 11
+        L.orc_replay_destroy.argtypes = [C.c_void_p]
+        L.orc_replay_set_frame.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.orc_replay_frame.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.orc_replay_results.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        tx0, ty0, tw, th = tile or (0, 0, 0, 0)
+        self.h = L.orc_replay_create(width, height, xdec, ydec, bit_depth, tx0, ty0, tw, th,
+                                     n_refs, threads)
+        assert self.h, "orc_replay_create failed"
+        sbc, sbr = (width + 63) // 64, (height + 63) // 64
+        self.n_words = (tw or sbc - tx0) * (th or sbr - ty0) * (8 * n_refs + 2) + 4
+
+    def set_frame(self, slot, yuv):
+        yuv = np.ascontiguousarray(yuv)
+        assert lib().orc_replay_set_frame(self.h, slot, yuv.ctypes.data) == 0
+
+    def frame(self, scale, sb_limit=0):
+        assert lib().orc_replay_frame(self.h, scale, sb_limit) == 0
+
+    def results(self):
+        out = np.zeros(self.n_words, dtype=np.uint64)
+        n = lib().orc_replay_results(self.h, out.ctypes.data, out.size)
+        assert n == out.size
+        return out
+
+    def close(self):
+        if self.h:
+            lib().orc_replay_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
