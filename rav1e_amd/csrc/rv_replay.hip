@@ -181,24 +181,42 @@ __global__ void make_mc_jobs(Geo g, const rv_fs_result *sub, rv_plane luma,
 // quantize/dequantize stand-in + coefficient compaction: the top-left
 // min(W,32) x min(H,32) of each W-stride raster, each value replaced by
 // (v / kQstep) * kQstep (truncating), packed with row stride min(W,32).
-// Also folds a position-weighted checksum of the packed coefficients.
 __global__ void pack_coeffs(const int32_t *raster, int n, int tw, int th,
-                            int32_t *packed, unsigned long long *csum) {
+                            int32_t *packed) {
   const int cw = tw < 32 ? tw : 32, ch = th < 32 ? th : 32;
   const int64_t total = (int64_t)n * cw * ch;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t s = 0;
-  if (i < total) {
-    const int64_t b = i / (cw * ch);
-    const int e = (int)(i - b * cw * ch);
-    const int r = e / cw, c = e - r * cw;
-    const int32_t v = raster[b * tw * th + r * tw + c];
-    const int32_t q = (v / kQstep) * kQstep;
-    packed[i] = q;
-    s = (uint64_t)(int64_t)q * (uint64_t)(e + 1);
-  }
+  if (i >= total) return;
+  const int64_t b = i / (cw * ch);
+  const int e = (int)(i - b * cw * ch);
+  const int r = e / cw, c = e - r * cw;
+  const int32_t v = raster[b * tw * th + r * tw + c];
+  packed[i] = (v / kQstep) * kQstep;
+}
+
+// Block-level reduction helper: one atomic per workgroup (never one per
+// wavefront: same-address atomics serialise, MI355X_MICROARCH.md).
+__device__ inline void block_atomic_add(uint64_t s, unsigned long long *out) {
+  __shared__ uint64_t red[4];
   s = group_sum<64>(s);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(csum, (unsigned long long)s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); i++) t += red[i];
+    if (t) atomicAdd(out, (unsigned long long)t);
+  }
+}
+
+// Verification checksum of packed coefficients (results time, not per
+// frame): sum of q * (position in block + 1), wrapping u64.
+__global__ void coeff_checksum(const int32_t *packed, int64_t total, int per_block,
+                               unsigned long long *out) {
+  uint64_t s = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x)
+    s += (uint64_t)(int64_t)packed[i] * (uint64_t)(i % per_block + 1);
+  block_atomic_add(s, out);
 }
 
 // Candidate score = luma SSE (from the cdef moments) + chroma SSE, then the
@@ -260,23 +278,22 @@ __global__ void make_imp_jobs(Geo g, const rv_fs_result *sub, rv_dist_job *jobs,
 }
 
 __global__ void sum_u32(const uint32_t *v, int n, unsigned long long *out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t s = i < n ? v[i] : 0;
-  s = group_sum<64>(s);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, (unsigned long long)s);
+  uint64_t s = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    s += v[i];
+  block_atomic_add(s, out);
 }
 
-// Sum of the reconstructed pixels of a plane region (all candidates).
+// Sum of the reconstructed pixels of a plane (all candidates; results time).
 template <typename Px>
 __global__ void sum_plane(rv_plane p, int w, int h, unsigned long long *out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t s = 0;
-  if (i < (int64_t)w * h) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)w * h;
+       i += (int64_t)gridDim.x * blockDim.x) {
     const int y = (int)(i / w), x = (int)(i - (int64_t)y * w);
-    s = *plane_ptr<Px>(p, x, y);
+    s += *plane_ptr<Px>(p, x, y);
   }
-  s = group_sum<64>(s);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(out, (unsigned long long)s);
+  block_atomic_add(s, out);
 }
 
 }  // namespace rv
@@ -607,7 +624,7 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   r->ev = r->evs[r->frames % rv_replay::kRing];
   r->frames++;
   RV_H(hipEventRecord(r->ev[0], st));
-  RV_H(hipMemsetAsync(r->tail, 0, 4 * 8, st));
+  RV_H(hipMemsetAsync(r->tail + 2, 0, 8, st));
   // F0 (encode_frame, src/encoder.rs:3382-3385)
   RV_R(rv_plane_downsample(&cur.hres, &cur.y, st));
   RV_R(rv_plane_downsample(&cur.qres, &cur.hres, st));
@@ -659,11 +676,9 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   RV_R(rv_diff_fwd_txfm_batch(&cur.u, &r->tall_u, r->c_tx, nct, 3, 0, g.bd, u_raster, st));
   RV_R(rv_diff_fwd_txfm_batch(&cur.v, &r->tall_v, r->c_tx, nct, 3, 0, g.bd, v_raster, st));
   pack_coeffs<<<blocks((int64_t)g.nctx * 1024), T, 0, st>>>(r->l_raster, g.nctx, 64, 64,
-                                                             r->l_packed, r->tail);
-  pack_coeffs<<<blocks((int64_t)nct * 1024), T, 0, st>>>(u_raster, nct, 32, 32, u_packed,
-                                                         r->tail);
-  pack_coeffs<<<blocks((int64_t)nct * 1024), T, 0, st>>>(v_raster, nct, 32, 32, v_packed,
-                                                         r->tail);
+                                                             r->l_packed);
+  pack_coeffs<<<blocks((int64_t)nct * 1024), T, 0, st>>>(u_raster, nct, 32, 32, u_packed);
+  pack_coeffs<<<blocks((int64_t)nct * 1024), T, 0, st>>>(v_raster, nct, 32, 32, v_packed);
   RV_H(hipEventRecord(r->ev[11], st));  // luma inverse TX_64X64 + add: 11..12
   RV_R(rv_inv_txfm_add_batch(r->l_packed, &r->tall_y, r->l_tx, g.nctx, 4, 0, g.bd, st));
   RV_H(hipEventRecord(r->ev[12], st));
@@ -676,26 +691,11 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   RV_R(rv_sse_batch(&cur.v, &r->tall_v, r->c_dist, g.nctx, g.cw, g.ch, r->v_sse, st));
   score_candidates<<<blocks(g.nsb), T, 0, st>>>(g, r->l_mom, r->u_sse, r->v_sse, r->lsub, r->csub,
                                                 r->coarse, r->half, r->full, r->sub, r->words);
-  if (g.hbd) {
-    sum_plane<uint16_t><<<blocks((int64_t)r->tall_y.width * r->tall_y.height), T, 0, st>>>(
-        r->tall_y, r->tall_y.width, r->tall_y.height, r->tail + 1);
-    sum_plane<uint16_t><<<blocks((int64_t)r->tall_u.width * r->tall_u.height), T, 0, st>>>(
-        r->tall_u, r->tall_u.width, r->tall_u.height, r->tail + 1);
-    sum_plane<uint16_t><<<blocks((int64_t)r->tall_v.width * r->tall_v.height), T, 0, st>>>(
-        r->tall_v, r->tall_v.width, r->tall_v.height, r->tail + 1);
-  } else {
-    sum_plane<uint8_t><<<blocks((int64_t)r->tall_y.width * r->tall_y.height), T, 0, st>>>(
-        r->tall_y, r->tall_y.width, r->tall_y.height, r->tail + 1);
-    sum_plane<uint8_t><<<blocks((int64_t)r->tall_u.width * r->tall_u.height), T, 0, st>>>(
-        r->tall_u, r->tall_u.width, r->tall_u.height, r->tail + 1);
-    sum_plane<uint8_t><<<blocks((int64_t)r->tall_v.width * r->tall_v.height), T, 0, st>>>(
-        r->tall_v, r->tall_v.width, r->tall_v.height, r->tail + 1);
-  }
   RV_H(hipEventRecord(r->ev[5], st));
   // F5 importance SATD against reference 1
   make_imp_jobs<<<blocks(r->n_imp), T, 0, st>>>(g, r->sub, r->imp_jobs, r->imp_bx, r->imp_by);
   RV_R(rv_satd_batch(&cur.y, &r->slots[1].y, r->imp_jobs, r->n_imp, 8, 8, r->imp_satd, st));
-  sum_u32<<<blocks(r->n_imp), T, 0, st>>>(r->imp_satd, r->n_imp, r->tail + 2);
+  sum_u32<<<256, T, 0, st>>>(r->imp_satd, r->n_imp, r->tail + 2);
   RV_H(hipEventRecord(r->ev[6], st));
   RV_H(hipGetLastError());
   return RV_OK;
@@ -707,6 +707,21 @@ int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap) {
   const int nw = g.nsb * (8 * g.R + 2);
   const int total = nw + 4;
   if (cap < total) return rv_set_error(RV_EINVAL, "rv_replay_results: cap too small");
+  // verification checksums of the last frame (outside the per-frame work)
+  hipStream_t st = r->stream;
+  const int ntx_c = (g.cw / 32) * (g.ch / 32);
+  const int64_t nl = (int64_t)g.nctx * 1024, nc = (int64_t)g.nctx * ntx_c * 1024;
+  RV_H(hipMemsetAsync(r->tail, 0, 2 * 8, st));
+  coeff_checksum<<<1024, 256, 0, st>>>(r->l_packed, nl, 1024, r->tail);
+  coeff_checksum<<<1024, 256, 0, st>>>(r->c_packed, 2 * nc, 1024, r->tail);
+  const rv_plane *tp[3] = {&r->tall_y, &r->tall_u, &r->tall_v};
+  for (int i = 0; i < 3; i++) {
+    if (g.hbd)
+      sum_plane<uint16_t><<<1024, 256, 0, st>>>(*tp[i], tp[i]->width, tp[i]->height, r->tail + 1);
+    else
+      sum_plane<uint8_t><<<1024, 256, 0, st>>>(*tp[i], tp[i]->width, tp[i]->height, r->tail + 1);
+  }
+  RV_H(hipGetLastError());
   RV_H(hipMemcpyAsync(host_out, r->words, (size_t)nw * 8, hipMemcpyDeviceToHost, r->stream));
   RV_H(hipMemcpyAsync(host_out + nw, r->tail, 3 * 8, hipMemcpyDeviceToHost, r->stream));
   RV_H(hipStreamSynchronize(r->stream));
