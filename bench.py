@@ -11,10 +11,10 @@ Frames cycle through the reorder pyramid's me_range_scale (4, 2, 1, 1).
 
 N = 1: configs[1] of BASELINE.json (1080p 8-bit 4:2:0, one tile, 1 GPU).
 N > 1 (torch.distributed.run, one process per GPU): every rank runs its own
-1080p tile stream -- tiles are independent units in the replay, so there is
-no data-path collective; `value` = frames of all ranks / max-over-ranks
-time ("scaling": "weak").  torch.distributed (gloo) carries only the
-barrier and the max-time reduction.
+1080p tile stream (rav1e_amd/ranks.py) -- tiles are independent units in
+the replay, so there is no data-path collective; `value` = frames of all
+ranks / max-over-ranks time ("scaling": "weak").  torch.distributed (gloo)
+carries only the barrier and the max-time reduction.
 """
 import argparse
 import json
@@ -67,6 +67,31 @@ def coarse_windows(W, H, R, scale, tile=(0, 0, 0, 0)):
     return out * R
 
 
+def timed_run(engine, group, steps, warmup, scales=None, sync=None):
+    """W untimed frames, then exactly K timed frames bracketed by a barrier
+    and a device sync on both sides; returns (max-over-ranks seconds, result
+    words of the last frame).  `engine` is a HipReplay (the product) or, in
+    the multi-rank CPU tests, the oracle's CpuReplay."""
+    from rav1e_amd import replay as RP
+    scales = scales or RP.GOP_SCALES
+    for i in range(warmup):
+        engine.frame(scales[i % len(scales)])
+    if warmup:
+        engine.results()  # drains the stream
+    group.barrier()
+    if sync:
+        sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        engine.frame(scales[(warmup + i) % len(scales)])
+    words = engine.results()  # blocks until the last frame is done
+    if sync:
+        sync()
+    t1 = time.perf_counter()
+    group.barrier()
+    return group.max(t1 - t0), words
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,80 +103,54 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", rank))
-
     import rav1e_amd as R  # load the HIP library before anything else
     from rav1e_amd import replay as RP
+    from rav1e_amd.ranks import RankGroup, rank_info
     R.lib()
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-        tdist.init_process_group("gloo", rank=rank, world_size=world)
-        dist = (torch, tdist)
-    R.require_device(local % max(1, R.lib().rv_device_count()))
+    info = rank_info()
+    rank, world = info.rank, info.world
+    group = RankGroup(info)
+    R.require_device(info.local_rank % max(1, R.lib().rv_device_count()))
 
     W, H, xdec, ydec, bd = CONFIGS[args.config]
     nref = args.refs
-    t_off = 1000 * rank  # every rank its own tile stream
-    frames = [RP.synth_frame(W, H, t_off + t, xdec, ydec, bd) for t in range(nref + 1)]
+    frames = [RP.synth_frame(W, H, info.frame_offset + t, xdec, ydec, bd) for t in range(nref + 1)]
     hip = RP.HipReplay(W, H, xdec, ydec, bd, nref)
     for s, f in enumerate(frames):
         hip.set_frame(s, f)
-
     scales = RP.GOP_SCALES
-    for i in range(args.warmup):
-        hip.frame(scales[i % 4])
-    hip.results()  # drains the stream
-
-    def barrier():
-        if dist:
-            dist[1].barrier()
-    barrier()
-    R._sync(None)
-    ev0 = R.lib().rv_event_create()
-    ev1 = R.lib().rv_event_create()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        hip.frame(scales[(args.warmup + i) % 4])
-    words = hip.results()  # blocks until the last frame is done
-    t1 = time.perf_counter()
-    barrier()
-    dt = t1 - t0
-    if dist:
-        torch, tdist = dist
-        tt = torch.tensor([dt], dtype=torch.float64)
-        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-        dt = float(tt[0])
+    dt, words = timed_run(hip, group, args.steps, args.warmup, scales, sync=lambda: R._sync(None))
 
     # per-kernel times over the timed frames (HIP events on the replay stream)
     k = min(args.steps, 64)
     ms = hip.stage_ms_sum(k) / k  # per frame
-    evals = hip.counters()
+    ev_full, ev_sub, ev_frames = (int(v) for v in hip.counters())
+    ev_frames = max(1, ev_frames)
     nsb = ((W + 63) // 64) * ((H + 63) // 64)
     px = 2 if bd > 8 else 1
-    # algorithmic bytes per frame of each kernel class (SURVEY.md §8d)
-    fs_bytes = sum(sum((nx + 15) * (ny + 15) * px + 256 * px + 40
+    # algorithmic bytes per frame of each kernel class (DESIGN.md §5)
+    fs_bytes = sum(sum((nx + 15) * (ny + 15) * px + 256 * px + 56
                        for nx, ny in coarse_windows(W, H, nref, s)) for s in scales) / 4.0
     fs_ops = sum(sum(nx * ny * 256 for nx, ny in coarse_windows(W, H, nref, s))
                  for s in scales) / 4.0
-    total_frames = args.warmup + args.steps
+    nj = nsb * nref
     nctx = nsb * 2 * nref
     kernels = {
         "full_search": dict(ms=float(ms[1]), launches=nref, bytes=fs_bytes, sad_px=fs_ops),
-        "diamond_f3": dict(ms=float(ms[3]), launches=2 * nref,
-                           bytes=float(evals[0] * 2 * 64 * 64 * px +
-                                       evals[1] * (71 * 71 * px + 64 * 64 * px)) / total_frames),
-        "put_luma": dict(ms=float(ms[6]), launches=nref,
-                         bytes=float(nctx * (71 * 71 * px + 64 * 64 * px))),
-        "diff_fwd_64": dict(ms=float(ms[7]), launches=1,
+        "diamond_fullpel_64": dict(ms=float(ms[6]), launches=1,
+                                   bytes=nj * (64 * 64 * px + 80) +
+                                   ev_full / ev_frames * 64 * 64 * px),
+        "diamond_subpel_64": dict(ms=float(ms[7]), launches=1,
+                                  bytes=nj * (64 * 64 * px + 80) +
+                                  ev_sub / ev_frames * 71 * 71 * px),
+        "put_luma_64": dict(ms=float(ms[8]), launches=nref,
+                            bytes=float(nctx * (71 * 71 * px + 64 * 64 * px))),
+        "diff_fwd_64": dict(ms=float(ms[9]), launches=1,
                             bytes=float(nctx * (2 * 64 * 64 * px + 4 * 64 * 64))),
-        "inv_add_64": dict(ms=float(ms[8]), launches=1,
+        "inv_add_64": dict(ms=float(ms[10]), launches=1,
                            bytes=float(nctx * (4 * 32 * 32 + 2 * 64 * 64 * px))),
-        "cdef_moments": dict(ms=float(ms[9]), launches=1,
-                             bytes=float(nctx * (2 * 64 * 64 * px + 64 * 40))),
+        "cdef_moments_64": dict(ms=float(ms[11]), launches=1,
+                                bytes=float(nctx * (2 * 64 * 64 * px + 64 * 40))),
     }
     dom = max(kernels, key=lambda n: kernels[n]["ms"])
     kd = kernels[dom]
@@ -203,12 +202,13 @@ def main():
                          zip(["F0_downsample", "F1_full_search", "F2_diamond_half",
                               "F3_diamond_full_subpel", "F4_rdo", "F5_importance_satd"], ms[:6])},
             "kernels_ms": {n: round(v["ms"], 4) for n, v in kernels.items()},
+            "diamond_evals_per_frame": [round(ev_full / ev_frames, 1),
+                                        round(ev_sub / ev_frames, 1)],
             "checksum": int(words[-3]) & 0xFFFFFFFF,
         }
         print(json.dumps(line), flush=True)
     hip.close()
-    if dist:
-        dist[1].destroy_process_group()
+    group.close()
 
 
 if __name__ == "__main__":

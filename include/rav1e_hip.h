@@ -313,15 +313,17 @@ int rv_replay_frame(rv_replay *r, int me_range_scale);
  * DESIGN.md; returns number of u64 written (<= cap). */
 int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
 /* Kernel-time breakdown of the last frame (HIP events on the replay
- * stream), ms: [0..5] stages F0..F5 (F1 = the full-search launches),
- * [6] luma put_8tap, [7] luma diff + forward TX_64X64, [8] luma inverse
- * TX_64X64 + add, [9] luma cdef moments.  Returns the count written. */
+ * stream), ms: [0..5] stages F0..F5 (F1 = exactly the full-search
+ * launches), then kernel brackets [6] F3 full-pel diamond, [7] F3 sub-pel
+ * diamond, [8] luma put_8tap, [9] luma diff + forward TX_64X64, [10] luma
+ * inverse TX_64X64 + add, [11] luma cdef moments.  Returns the count. */
 int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
 /* Same breakdown summed over the last `last_frames` frames (<= 64). */
 int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,
                               int cap);
-/* Cumulative diamond-search candidate evaluations since creation:
- * out[0] full-pel 64x64 (F3), out[1] sub-pel 64x64 (F3). */
+/* Diamond-search candidate evaluations summed over the last min(frames, 64)
+ * frames: out[0] F3 full-pel 64x64, out[1] F3 sub-pel 64x64, out[2] = the
+ * number of frames summed (cap >= 3). */
 int rv_replay_counters(rv_replay *r, uint64_t *out, int cap);
 
 /* ---------------------------------------------------------------------

@@ -56,6 +56,10 @@ FS_JOB = np.dtype([("po_x", "<i4"), ("po_y", "<i4"), ("x_lo", "<i4"), ("x_hi", "
                    ("y_lo", "<i4"), ("y_hi", "<i4"), ("pmv0_row", "<i2"), ("pmv0_col", "<i2"),
                    ("pmv1_row", "<i2"), ("pmv1_col", "<i2"), ("lambda_", "<u4"),
                    ("reserved", "<i4")])
+DS_JOB = np.dtype([("po_x", "<i4"), ("po_y", "<i4"), ("mvx_min", "<i4"), ("mvx_max", "<i4"),
+                   ("mvy_min", "<i4"), ("mvy_max", "<i4"), ("pmv0_row", "<i2"),
+                   ("pmv0_col", "<i2"), ("pmv1_row", "<i2"), ("pmv1_col", "<i2"),
+                   ("lambda_", "<u4"), ("n_pred", "<i4"), ("pred", "<i2", (8, 2))])
 FS_RESULT = np.dtype([("mv_row", "<i2"), ("mv_col", "<i2"), ("reserved", "<u4"),
                       ("cost", "<u8")])
 REPLAY_CFG_FIELDS = ["width", "height", "xdec", "ydec", "bit_depth", "tile_x0", "tile_y0",
@@ -505,6 +509,21 @@ def full_search_batch(org: DevicePlane, ref: DevicePlane, jobs, blk_w, blk_h, st
     _check(lib().rv_full_search_batch(C.byref(org.desc), C.byref(ref.desc), dj.ptr, len(jobs),
                                       blk_w, blk_h, step, 1 if allow_hp else 0, out.ptr, None),
            "rv_full_search_batch")
+    _sync()
+    return out.download(FS_RESULT, len(jobs))
+
+
+def diamond_search_batch(org: DevicePlane, ref: DevicePlane, jobs, blk_w, blk_h,
+                         subpixel=False, use_satd=False, allow_hp=False,
+                         bit_depth=8) -> np.ndarray:
+    """diamond_me_search (src/me.rs:693-785) for every job in one launch."""
+    jobs = np.ascontiguousarray(jobs, dtype=DS_JOB)
+    dj = DeviceBuffer.from_array(jobs)
+    out = DeviceBuffer(16 * max(1, len(jobs)))
+    _check(lib().rv_diamond_search_batch(C.byref(org.desc), C.byref(ref.desc), dj.ptr,
+                                         len(jobs), blk_w, blk_h, int(subpixel), int(use_satd),
+                                         int(allow_hp), bit_depth, out.ptr, None),
+           "rv_diamond_search_batch")
     _sync()
     return out.download(FS_RESULT, len(jobs))
 

@@ -1,19 +1,35 @@
-// rv_me_diamond.hip -- batched diamond motion search, one persistent
-// workgroup per (block, reference) (gfx950).
+// rv_me_diamond.hip -- batched diamond motion search (gfx950).
 //
 // diamond_me_search (src/me.rs:693-785) with get_best_predictor
 // (:655-691), get_mv_rd_cost (:787-838) and compute_mv_rd_cost (:840-856):
-// the whole data-dependent search loop of a block runs inside one
-// workgroup, so a tile's blocks advance in parallel without a host round
-// trip per diamond step.  Full-pel candidates read the reference region
-// straight from HBM; sub-pel candidates run predict_inter's put_8tap
-// (src/predict.rs:255-338, REGULAR filters) into LDS first.  Every block
-// evaluation is a workgroup-wide SAD / SATD reduced through LDS.
+// the whole data-dependent search of a block runs inside one workgroup, so
+// a tile's blocks advance in parallel with no host round trip per step.
+//
+// Fast path (SAD, u8/u16, block widths 16/32/64): a workgroup is 4
+// wavefronts and every wavefront evaluates one candidate on its own, so the
+// 4 points of a diamond step (and up to 4 predictors) run concurrently;
+// the step's winner is chosen from LDS in pattern order with the
+// reference's strict `<` (first minimum), exactly as the sequential loop.
+//  * full-pel: the source block lives in VGPRs (16-byte row chunks); a
+//    candidate is 16-byte unaligned loads of the reference block + v_sad_u8
+//    / v_sad_u16 + one wave reduction.
+//  * sub-pel: predict_inter's put_8tap (src/predict.rs:255-338, REGULAR,
+//    PlaneSlice::clamp) runs per wavefront: the (h+7) x (w+7) window is
+//    staged in a wave-private LDS slab, lane = output column; the
+//    horizontal 8-tap is two v_dot4_i32_i8 (u8, pixels biased by -128) or
+//    four v_dot2_i32_i16 (u16), the vertical 8-tap a register ring of the
+//    i16 intermediates, and |org - pred| accumulates in registers -- the
+//    prediction never leaves the wavefront.
+// Anything else (SATD, other sizes) takes the generic workgroup-per-
+// candidate kernel.
+#include <string.h>
+
 #include "rv_device.h"
 
 namespace rv {
 
 constexpr int kDsThreads = 256;
+constexpr int kDsWaves = kDsThreads / 64;
 
 // SUBPEL_FILTERS REGULAR sets (src/mc.rs:70-179): index 0 = 8-tap
 // REGULAR, 1 = 4-tap REGULAR (get_filter for length <= 4, src/mc.rs:201-210)
@@ -35,6 +51,7 @@ __constant__ int8_t kReg[2][16][8] = {
      {0, 0, -8, 38, 110, -12, 0, 0}, {0, 0, -6, 28, 116, -10, 0, 0},
      {0, 0, -4, 18, 122, -8, 0, 0}, {0, 0, -2, 8, 126, -4, 0, 0}}};
 
+// get_mv_rate's diff_to_rate (src/me.rs:1006-1021)
 __device__ __forceinline__ uint32_t ds_diff_to_rate(int16_t diff, int hp) {
   int16_t d = hp ? diff : (int16_t)(diff >> 1);
   if (d == 0) return 0;
@@ -42,28 +59,358 @@ __device__ __forceinline__ uint32_t ds_diff_to_rate(int16_t diff, int hp) {
   return 2u * (16u - (uint32_t)(__builtin_clz(a) - 16));
 }
 
+// compute_mv_rd_cost (src/me.rs:840-856) given the distortion
+__device__ __forceinline__ uint64_t ds_cost(uint32_t dist, rv_mv mv, const rv_ds_job &jb,
+                                            int hp) {
+  const uint32_t r1 = ds_diff_to_rate((int16_t)(mv.row - jb.pmv[0].row), hp) +
+                      ds_diff_to_rate((int16_t)(mv.col - jb.pmv[0].col), hp);
+  const uint32_t r2 = ds_diff_to_rate((int16_t)(mv.row - jb.pmv[1].row), hp) +
+                      ds_diff_to_rate((int16_t)(mv.col - jb.pmv[1].col), hp);
+  const uint32_t rate = r1 < r2 + 1 ? r1 : r2 + 1;
+  return 256ull * dist + (uint64_t)rate * jb.lambda;
+}
+
+__device__ __forceinline__ bool ds_in_range(rv_mv mv, const rv_ds_job &jb) {
+  return !(mv.col < jb.mvx_min || mv.col > jb.mvx_max || mv.row < jb.mvy_min ||
+           mv.row > jb.mvy_max);
+}
+
+// blockIdx -> job with consecutive jobs on one XCD (blocks are dealt to
+// the 8 XCDs round-robin): neighbouring superblocks share reference rows
+// in that XCD's L2.  The grid is rounded up to a multiple of 8.
+__device__ __forceinline__ int xcd_job(int n) {
+  const int per = (int)gridDim.x >> 3;
+  return ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+}
+
+struct DsArgs {
+  rv_plane org;
+  rv_plane ref[RV_DS_MAX_PRED];  // reference of job i = ref[i / n_per_ref]
+  const rv_ds_job *jobs;
+  rv_fs_result *out;
+  int n, n_per_ref, w, h, subpel, satd, hp, bd;
+  uint32_t *evals;  // optional: in-range candidate evaluations per job
+};
+
+__device__ __forceinline__ void ds_write(const DsArgs &a, int job, rv_mv center,
+                                         uint64_t cost) {
+  rv_fs_result r;
+  r.best_mv = center;
+  r.reserved = 0;
+  r.cost = cost;
+  a.out[job] = r;
+}
+
+// ============================ fast path ====================================
+// 16-byte chunk helpers: 16 u8 or 8 u16 pixels
+__device__ __forceinline__ uint4 ld16(const void *p) {
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);  // unaligned global_load_dwordx4
+  return v;
+}
+template <typename Px>
+__device__ __forceinline__ uint32_t sad16(uint4 a, uint4 b, uint32_t acc) {
+  if constexpr (sizeof(Px) == 1) {
+    acc = __builtin_amdgcn_sad_u8(a.x, b.x, acc);
+    acc = __builtin_amdgcn_sad_u8(a.y, b.y, acc);
+    acc = __builtin_amdgcn_sad_u8(a.z, b.z, acc);
+    return __builtin_amdgcn_sad_u8(a.w, b.w, acc);
+  } else {
+    acc = __builtin_amdgcn_sad_u16(a.x, b.x, acc);
+    acc = __builtin_amdgcn_sad_u16(a.y, b.y, acc);
+    acc = __builtin_amdgcn_sad_u16(a.z, b.z, acc);
+    return __builtin_amdgcn_sad_u16(a.w, b.w, acc);
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return group_sum<64>(v); }
+
+// Full-pel layout: K 16-byte chunks per block row, R rows per wave
+// instruction, I instructions per block.
+template <typename Px, int W, int H>
+struct FullGeo {
+  static constexpr int K = W * (int)sizeof(Px) / 16;
+  static constexpr int R = 64 / K;
+  static constexpr int I = (H + R - 1) / R;
+  static constexpr bool kPartial = (R * I != H);
+};
+
+// Sub-pel layout: lane = column c (lane % W), row group g = lane / W of
+// RG = H / (64 / W) output rows; the wave-private LDS window is (H + 7)
+// rows x P bytes.
+template <typename Px, int W, int H>
+struct SubGeo {
+  static constexpr int G = 64 / W;
+  static constexpr int RG = H / G;
+  static constexpr int P = sizeof(Px) == 1 ? ((W + 8 + 15) / 16) * 16
+                                           : ((2 * (W + 8) + 15) / 16) * 16;
+  static constexpr int kWinDwords = (H + 7) * P / 4;
+  static constexpr int kOrgDwords = RG * (int)sizeof(Px) / 4;
+};
+
+template <typename Px, int W, int H, bool SUB>
+struct DsFast {
+  using F = FullGeo<Px, W, H>;
+  using S = SubGeo<Px, W, H>;
+  static constexpr int kOrgRegs = SUB ? S::kOrgDwords : 4 * F::I;
+};
+
+template <typename Px, int W, int H, bool SUB>
+__global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
+  using F = FullGeo<Px, W, H>;
+  using S = SubGeo<Px, W, H>;
+  constexpr int B = (int)sizeof(Px);
+  __shared__ uint64_t pcost[RV_DS_MAX_PRED];
+  __shared__ uint64_t scost[2][kDsWaves];
+  __shared__ uint32_t wevals[kDsWaves];
+  __shared__ uint32_t win_all[SUB ? kDsWaves * S::kWinDwords : 1];
+
+  const int job = xcd_job(a.n);
+  if (job >= a.n) return;  // whole workgroup, uniformly
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const rv_ds_job *jp = a.jobs + job;  // pred[] read through the pointer
+  const rv_ds_job jb = *jp;
+  const rv_plane &ref = a.ref[job / a.n_per_ref];
+  const int ib = a.bd == 12 ? 2 : 4;
+  const int maxv = (1 << a.bd) - 1;
+
+  // ---- the source block, in registers ------------------------------------
+  uint32_t org[DsFast<Px, W, H, SUB>::kOrgRegs];
+  const int col = lane % W, grp = lane / W;  // sub-pel lane mapping
+  const int frow = lane / F::K, fchunk = lane % F::K;  // full-pel
+  if constexpr (SUB) {
+    const Px *o = plane_ptr<Px>(a.org, jb.po_x + col, jb.po_y + grp * S::RG);
+#pragma unroll
+    for (int i = 0; i < S::kOrgDwords; i++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int k = 0; k < 4 / B; k++)
+        v |= (uint32_t)o[(int64_t)(i * (4 / B) + k) * a.org.stride] << (8 * B * k);
+      org[i] = v;
+    }
+  } else {
+    const uint8_t *o = (const uint8_t *)plane_ptr<Px>(a.org, jb.po_x, jb.po_y);
+    const int64_t os = (int64_t)a.org.stride * B;
+#pragma unroll
+    for (int i = 0; i < F::I; i++) {
+      const int r = i * F::R + frow;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (!F::kPartial || r < H) v = ld16(o + r * os + fchunk * 16);
+      org[4 * i + 0] = v.x;
+      org[4 * i + 1] = v.y;
+      org[4 * i + 2] = v.z;
+      org[4 * i + 3] = v.w;
+    }
+  }
+  uint32_t *win = win_all + (SUB ? wave * S::kWinDwords : 0);
+  uint32_t evals = 0;
+
+  // ---- one candidate, evaluated by this wavefront ----------------------
+  auto eval = [&](rv_mv mv) -> uint64_t {
+    if (!ds_in_range(mv, jb)) return ~0ull;
+    evals++;
+    uint32_t acc = 0;
+    if constexpr (!SUB) {
+      // region at po + mv / 8 (Rust `/` truncates toward zero)
+      const uint8_t *r = (const uint8_t *)plane_ptr<Px>(ref, jb.po_x + mv.col / 8,
+                                                        jb.po_y + mv.row / 8);
+      const int64_t rs = (int64_t)ref.stride * B;
+#pragma unroll
+      for (int i = 0; i < F::I; i++) {
+        const int rr = i * F::R + frow;
+        if (!F::kPartial || rr < H) {
+          const uint4 v = ld16(r + rr * rs + fchunk * 16);
+          acc = sad16<Px>(make_uint4(org[4 * i], org[4 * i + 1], org[4 * i + 2], org[4 * i + 3]),
+                          v, acc);
+        }
+      }
+    } else {
+      // predict_inter / get_params (src/predict.rs:267-283), luma plane
+      const int xs = 3 + ref.xdec, ys = 3 + ref.ydec;
+      const int roff = (int)mv.row >> ys, coff = (int)mv.col >> xs;
+      const int rf = ((int)mv.row - (roff << ys)) << (4 - ys);
+      const int cf = ((int)mv.col - (coff << xs)) << (4 - xs);
+      // PlaneSlice::clamp (src/frame/plane.rs:521-533) of the -3 origin
+      const int qx = clampi(jb.po_x + coff - 3, -ref.xorigin, ref.width);
+      const int qy = clampi(jb.po_y + roff - 3, -ref.yorigin, ref.height);
+      const uint8_t *sp = (const uint8_t *)plane_ptr<Px>(ref, qx, qy);
+      const int64_t rs = (int64_t)ref.stride * B;
+      // stage the window: (H + 7) rows of ceil((W + 7) * B / 4) dwords
+      constexpr int kRowDw = ((W + 7) * B + 3) / 4;
+      constexpr int kTot = (H + 7) * kRowDw;
+      __builtin_amdgcn_wave_barrier();  // previous candidate done with LDS
+#pragma unroll 4
+      for (int i = lane; i < kTot; i += 64) {
+        const int r = i / kRowDw, d = i - r * kRowDw;
+        uint32_t v;
+        __builtin_memcpy(&v, sp + r * rs + 4 * d, 4);
+        win[r * (S::P / 4) + d] = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // filters (wave-uniform): packed taps
+      const int8_t *xf = kReg[W <= 4][cf];
+      const int8_t *yf = kReg[H <= 4][rf];
+      int yt[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) yt[k] = yf[k];
+      uint32_t xp[4];  // u8: 2 x i8x4 (xp[0..1]); u16: 4 x i16x2
+      int xsum = 0;
+      if constexpr (B == 1) {
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+          xp[h] = (uint32_t)(uint8_t)xf[4 * h] | ((uint32_t)(uint8_t)xf[4 * h + 1] << 8) |
+                  ((uint32_t)(uint8_t)xf[4 * h + 2] << 16) |
+                  ((uint32_t)(uint8_t)xf[4 * h + 3] << 24);
+#pragma unroll
+        for (int k = 0; k < 8; k++) xsum += xf[k];
+        xp[2] = xp[3] = 0;
+      } else {
+#pragma unroll
+        for (int h = 0; h < 4; h++)
+          xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h] |
+                  ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] << 16);
+      }
+      const int vshift = cf ? 7 + ib : 7;
+      // horizontal value of window row t (group-relative) for column col
+      auto hval = [&](int t) -> int32_t {
+        const uint32_t *row = win + (grp * S::RG + t) * (S::P / 4);
+        if constexpr (B == 1) {
+          const int d0 = col >> 2, sh = col & 3;
+          const uint32_t w0 = row[d0], w1 = row[d0 + 1], w2 = row[d0 + 2];
+          const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+          const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+          if (!cf) return (int32_t)(lo >> 24);
+          int32_t s = __builtin_amdgcn_sdot4((int)(lo ^ 0x80808080u), (int)xp[0], 128 * xsum,
+                                             false);
+          s = __builtin_amdgcn_sdot4((int)(hi ^ 0x80808080u), (int)xp[1], s, false);
+          return (int32_t)(int16_t)round_shift(s, 7 - ib);
+        } else {
+          typedef short s2 __attribute__((ext_vector_type(2)));
+          const int d0 = col >> 1, sh = (col & 1) * 2;
+          uint32_t w[5];
+#pragma unroll
+          for (int k = 0; k < 5; k++) w[k] = row[d0 + k];
+          uint32_t p[4];
+#pragma unroll
+          for (int k = 0; k < 4; k++) p[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+          if (!cf) return (int32_t)(p[1] >> 16);
+          int32_t s = 0;
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            s = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, p[k]), __builtin_bit_cast(s2, xp[k]),
+                                       s, false);
+          return (int32_t)(int16_t)round_shift(s, 7 - ib);
+        }
+      };
+      int32_t ring[8];
+#pragma unroll
+      for (int t = 0; t < 7; t++) ring[t] = hval(t);
+      ring[7] = 0;
+#pragma clang loop unroll(full)
+      for (int r = 0; r < S::RG; r++) {
+        ring[(r + 7) & 7] = hval(r + 7);
+        int32_t v;
+        if (rf) {
+          int32_t s = 0;
+#pragma unroll
+          for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(r + k) & 7]);
+          v = round_shift(s, vshift);
+        } else {
+          v = cf ? round_shift(ring[(r + 3) & 7], ib) : ring[(r + 3) & 7];
+        }
+        v = clampi(v, 0, maxv);
+        const int o = (int)((org[r * B / 4] >> (8 * B * (r % (4 / B)))) & (B == 1 ? 0xffu : 0xffffu));
+        const int d = o - v;
+        acc += (uint32_t)(d < 0 ? -d : d);
+      }
+    }
+    return ds_cost(wave_sum(acc), mv, jb, a.hp);
+  };
+
+  // ---- get_best_predictor: predictors evaluated 4 at a time ------------
+  const int np = jb.n_pred < RV_DS_MAX_PRED ? jb.n_pred : RV_DS_MAX_PRED;
+  for (int p0 = 0; p0 < np; p0 += kDsWaves) {
+    const int p = p0 + wave;
+    if (p < np) {
+      const uint64_t c = eval(jp->pred[p]);
+      if (lane == 0) pcost[p] = c;
+    }
+  }
+  __syncthreads();
+  rv_mv center{0, 0};
+  uint64_t center_cost = ~0ull;
+  for (int p = 0; p < np; p++) {
+    const uint64_t c = pcost[p];
+    if (c < center_cost) {
+      center = jp->pred[p];
+      center_cost = c;
+    }
+  }
+  // ---- diamond steps: the 4 pattern points in parallel -----------------
+  int16_t radius = a.subpel ? 4 : 16;
+  const int16_t radius_end = a.subpel ? (a.hp ? 1 : 2) : 8;
+  const int pr = wave == 0 ? 1 : wave == 2 ? -1 : 0;  // diamond_pattern
+  const int pc = wave == 1 ? 1 : wave == 3 ? -1 : 0;
+  // Every move strictly lowers center_cost, so the loop ends; the bound
+  // only guarantees the grid drains whatever the inputs.
+  for (int iter = 0; iter < 4096; iter++) {
+    const rv_mv cand{(int16_t)(center.row + radius * pr), (int16_t)(center.col + radius * pc)};
+    const uint64_t c = eval(cand);
+    if (lane == 0) scost[iter & 1][wave] = c;
+    __syncthreads();
+    uint64_t best = ~0ull;
+    int bp = 0;
+#pragma unroll
+    for (int p = 0; p < kDsWaves; p++) {
+      const uint64_t v = scost[iter & 1][p];
+      if (v < best) {
+        best = v;
+        bp = p;
+      }
+    }
+    if (center_cost <= best) {
+      if (radius == radius_end) break;
+      radius /= 2;
+    } else {
+      const int br = bp == 0 ? 1 : bp == 2 ? -1 : 0, bc = bp == 1 ? 1 : bp == 3 ? -1 : 0;
+      center = rv_mv{(int16_t)(center.row + radius * br), (int16_t)(center.col + radius * bc)};
+      center_cost = best;
+    }
+  }
+  if (a.evals) {
+    if (lane == 0) wevals[wave] = evals;
+    __syncthreads();
+    if (threadIdx.x == 0) a.evals[job] = wevals[0] + wevals[1] + wevals[2] + wevals[3];
+  }
+  if (threadIdx.x == 0) ds_write(a, job, center, center_cost);
+}
+
+// ============================ generic path =================================
 template <int N>
 __device__ __forceinline__ void ds_had(int32_t *v, int s) {
 #pragma unroll
   for (int k = 0; k < N; k += 2) {
-    int32_t a = v[k * s], b = v[(k + 1) * s];
-    v[k * s] = a + b;
-    v[(k + 1) * s] = a - b;
+    int32_t x = v[k * s], y = v[(k + 1) * s];
+    v[k * s] = x + y;
+    v[(k + 1) * s] = x - y;
   }
 #pragma unroll
   for (int g = 0; g < N; g += 4)
 #pragma unroll
     for (int k = 0; k < 2; k++) {
-      int32_t a = v[(g + k) * s], b = v[(g + k + 2) * s];
-      v[(g + k) * s] = a + b;
-      v[(g + k + 2) * s] = a - b;
+      int32_t x = v[(g + k) * s], y = v[(g + k + 2) * s];
+      v[(g + k) * s] = x + y;
+      v[(g + k + 2) * s] = x - y;
     }
   if constexpr (N == 8) {
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      int32_t a = v[k * s], b = v[(k + 4) * s];
-      v[k * s] = a + b;
-      v[(k + 4) * s] = a - b;
+      int32_t x = v[k * s], y = v[(k + 4) * s];
+      v[k * s] = x + y;
+      v[(k + 4) * s] = x - y;
     }
   }
 }
@@ -75,15 +422,34 @@ __device__ __forceinline__ uint64_t wg_sum(uint64_t v, uint64_t *red) {
   __syncthreads();
   uint64_t t = 0;
 #pragma unroll
-  for (int i = 0; i < kDsThreads / 64; i++) t += red[i];
+  for (int i = 0; i < kDsWaves; i++) t += red[i];
   return t;
+}
+
+// Chunked Hadamard of one N x N difference block (get_satd_ref's butterfly
+// order, src/dist.rs:208-272); diff(r, c) supplies org - pred.
+template <int N, typename Diff>
+__device__ __forceinline__ uint32_t had_abs_sum(Diff diff) {
+  int32_t d[N * N];
+#pragma unroll
+  for (int r = 0; r < N; r++)
+#pragma unroll
+    for (int c = 0; c < N; c++) d[r * N + c] = diff(r, c);
+#pragma unroll
+  for (int c = 0; c < N; c++) ds_had<N>(d + c, N);
+#pragma unroll
+  for (int r = 0; r < N; r++) ds_had<N>(d + r * N, 1);
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < N * N; i++) acc += (uint32_t)(d[i] < 0 ? -d[i] : d[i]);
+  return acc;
 }
 
 // SAD or SATD (get_sad / get_satd semantics) of org vs pred(r, c),
 // evaluated by the whole workgroup; all threads get the result.
 template <typename Px, typename Pred>
-__device__ uint32_t wg_dist(const Px *o, int ostride, int w, int h, int satd,
-                            Pred pred, uint64_t *red) {
+__device__ uint32_t wg_dist(const Px *o, int ostride, int w, int h, int satd, Pred pred,
+                            uint64_t *red) {
   uint64_t acc = 0;
   if (!satd) {
     for (int i = threadIdx.x; i < w * h; i += kDsThreads) {
@@ -97,91 +463,56 @@ __device__ uint32_t wg_dist(const Px *o, int ostride, int w, int h, int satd,
   const int N = n8 ? 8 : 4, cw = w / N, chunks = cw * (h / N);
   for (int ci = threadIdx.x; ci < chunks; ci += kDsThreads) {
     const int cy = (ci / cw) * N, cx = (ci % cw) * N;
-    if (n8) {
-      int32_t d[64];
-#pragma unroll
-      for (int r = 0; r < 8; r++)
-#pragma unroll
-        for (int c = 0; c < 8; c++)
-          d[r * 8 + c] = (int)o[(int64_t)(cy + r) * ostride + cx + c] - pred(cy + r, cx + c);
-#pragma unroll
-      for (int c = 0; c < 8; c++) ds_had<8>(d + c, 8);
-#pragma unroll
-      for (int r = 0; r < 8; r++) ds_had<8>(d + r * 8, 1);
-#pragma unroll
-      for (int i = 0; i < 64; i++) acc += (uint32_t)(d[i] < 0 ? -d[i] : d[i]);
-    } else {
-      int32_t d[16];
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-          d[r * 4 + c] = (int)o[(int64_t)(cy + r) * ostride + cx + c] - pred(cy + r, cx + c);
-#pragma unroll
-      for (int c = 0; c < 4; c++) ds_had<4>(d + c, 4);
-#pragma unroll
-      for (int r = 0; r < 4; r++) ds_had<4>(d + r * 4, 1);
-#pragma unroll
-      for (int i = 0; i < 16; i++) acc += (uint32_t)(d[i] < 0 ? -d[i] : d[i]);
-    }
+    auto diff = [&](int r, int c) {
+      return (int)o[(int64_t)(cy + r) * ostride + cx + c] - pred(cy + r, cx + c);
+    };
+    acc += n8 ? had_abs_sum<8>(diff) : had_abs_sum<4>(diff);
   }
   const uint64_t s = wg_sum(acc, red);
   const int ln = n8 ? 3 : 2;
   return (uint32_t)((s + ((1ull << ln) >> 1)) >> ln);
 }
 
-struct DsArgs {
-  rv_plane org, ref;
-  const rv_ds_job *jobs;
-  rv_fs_result *out;
-  int n, w, h, subpel, satd, hp, bd;
-  unsigned long long *evals;  // optional: candidate evaluations (a counter)
-};
-
 template <typename Px>
 __global__ __launch_bounds__(kDsThreads) void diamond_kernel(DsArgs a) {
   extern __shared__ __align__(16) int16_t lds[];
-  __shared__ uint64_t red[kDsThreads / 64];
+  __shared__ uint64_t red[kDsWaves];
   const int job = blockIdx.x;
   if (job >= a.n) return;
   const rv_ds_job jb = a.jobs[job];
+  const rv_plane &ref = a.ref[job / a.n_per_ref];
   const int w = a.w, h = a.h;
   const Px *o = plane_ptr<Px>(a.org, jb.po_x, jb.po_y);
   const int ib = a.bd == 12 ? 2 : 4;
   const int maxv = (1 << a.bd) - 1;
   const int sw = w + 7, shh = h + 7;
-  int16_t *win = lds;               // [h+7][w+7]
-  int16_t *mid = lds + sw * shh;    // [h+7][w]
-  int16_t *pred = mid + shh * w;    // [h][w]
+  int16_t *win = lds;             // [h+7][w+7]
+  int16_t *mid = lds + sw * shh;  // [h+7][w]
+  int16_t *pred = mid + shh * w;  // [h][w]
 
   // get_mv_rd_cost: range check, prediction, distortion, rate
-  unsigned evals = 0;
+  uint32_t evals = 0;
   auto rd_cost = [&](rv_mv mv) -> uint64_t {
-    if (mv.col < jb.mvx_min || mv.col > jb.mvx_max || mv.row < jb.mvy_min ||
-        mv.row > jb.mvy_max)
-      return ~0ull;
+    if (!ds_in_range(mv, jb)) return ~0ull;
     evals++;
     uint32_t dist;
     if (!a.subpel) {
-      // region at po + mv / 8 (Rust `/` truncates toward zero)
-      const Px *r = plane_ptr<Px>(a.ref, jb.po_x + mv.col / 8, jb.po_y + mv.row / 8);
-      const int rs = a.ref.stride;
+      const Px *r = plane_ptr<Px>(ref, jb.po_x + mv.col / 8, jb.po_y + mv.row / 8);
+      const int rs = ref.stride;
       dist = wg_dist<Px>(o, a.org.stride, w, h, a.satd,
                          [&](int rr, int cc) { return (int)r[(int64_t)rr * rs + cc]; }, red);
     } else {
-      // predict_inter / get_params (src/predict.rs:267-283), luma plane
-      const int xs = 3 + a.ref.xdec, ys = 3 + a.ref.ydec;
+      const int xs = 3 + ref.xdec, ys = 3 + ref.ydec;
       const int roff = (int)mv.row >> ys, coff = (int)mv.col >> xs;
       const int rf = ((int)mv.row - (roff << ys)) << (4 - ys);
       const int cf = ((int)mv.col - (coff << xs)) << (4 - xs);
-      // PlaneSlice::clamp (src/frame/plane.rs:521-533) of the -3 origin
-      const int qx = clampi(jb.po_x + coff - 3, -a.ref.xorigin, a.ref.width);
-      const int qy = clampi(jb.po_y + roff - 3, -a.ref.yorigin, a.ref.height);
-      const Px *sp = plane_ptr<Px>(a.ref, qx, qy);  // window origin (-3, -3)
+      const int qx = clampi(jb.po_x + coff - 3, -ref.xorigin, ref.width);
+      const int qy = clampi(jb.po_y + roff - 3, -ref.yorigin, ref.height);
+      const Px *sp = plane_ptr<Px>(ref, qx, qy);  // window origin (-3, -3)
       __syncthreads();  // previous candidate done with LDS
       for (int i = threadIdx.x; i < sw * shh; i += kDsThreads) {
         const int r = i / sw, c = i - r * sw;
-        win[i] = (int16_t)sp[(int64_t)r * a.ref.stride + c];
+        win[i] = (int16_t)sp[(int64_t)r * ref.stride + c];
       }
       __syncthreads();
       const int8_t *xf = kReg[w <= 4][cf];
@@ -223,12 +554,7 @@ __global__ __launch_bounds__(kDsThreads) void diamond_kernel(DsArgs a) {
       dist = wg_dist<Px>(o, a.org.stride, w, h, a.satd,
                          [&](int rr, int cc) { return (int)pred[rr * w + cc]; }, red);
     }
-    const uint32_t r1 = ds_diff_to_rate((int16_t)(mv.row - jb.pmv[0].row), a.hp) +
-                        ds_diff_to_rate((int16_t)(mv.col - jb.pmv[0].col), a.hp);
-    const uint32_t r2 = ds_diff_to_rate((int16_t)(mv.row - jb.pmv[1].row), a.hp) +
-                        ds_diff_to_rate((int16_t)(mv.col - jb.pmv[1].col), a.hp);
-    const uint32_t rate = r1 < r2 + 1 ? r1 : r2 + 1;
-    return 256ull * dist + (uint64_t)rate * jb.lambda;
+    return ds_cost(dist, mv, jb, a.hp);
   };
 
   // get_best_predictor
@@ -245,8 +571,6 @@ __global__ __launch_bounds__(kDsThreads) void diamond_kernel(DsArgs a) {
   int16_t radius = a.subpel ? 4 : 16;
   const int16_t radius_end = a.subpel ? (a.hp ? 1 : 2) : 8;
   const int16_t pat[4][2] = {{1, 0}, {0, 1}, {-1, 0}, {0, -1}};
-  // Every move strictly lowers center_cost, so the loop ends; the bound
-  // only guarantees the grid drains whatever the inputs.
   for (int iter = 0; iter < 4096; iter++) {
     uint64_t best = ~0ull;
     rv_mv best_mv{0, 0};
@@ -268,41 +592,85 @@ __global__ __launch_bounds__(kDsThreads) void diamond_kernel(DsArgs a) {
     }
   }
   if (threadIdx.x == 0) {
-    if (a.evals) atomicAdd(a.evals, (unsigned long long)evals);
-    rv_fs_result r;
-    r.best_mv = center;
-    r.reserved = 0;
-    r.cost = center_cost;
-    a.out[job] = r;
+    if (a.evals) a.evals[job] = evals;
+    ds_write(a, job, center, center_cost);
   }
+}
+
+template <typename Px, int W, int H, bool SUB>
+void launch_fast(const DsArgs &a, hipStream_t s) {
+  const unsigned grid = (unsigned)((a.n + 7) / 8 * 8);
+  ds_fast_kernel<Px, W, H, SUB><<<grid, kDsThreads, 0, s>>>(a);
+}
+
+template <typename Px>
+bool try_fast(const DsArgs &a, hipStream_t s) {
+  if (a.satd) return false;
+#define RV_DS_CASE(W, H)                                        \
+  if (a.w == W && a.h == H) {                                   \
+    if (a.subpel)                                               \
+      launch_fast<Px, W, H, true>(a, s);                        \
+    else                                                        \
+      launch_fast<Px, W, H, false>(a, s);                       \
+    return true;                                                \
+  }
+  RV_DS_CASE(64, 64)
+  RV_DS_CASE(32, 32)
+  RV_DS_CASE(64, 32)
+  RV_DS_CASE(32, 64)
+  RV_DS_CASE(16, 32)
+  RV_DS_CASE(16, 64)
+#undef RV_DS_CASE
+  return false;
 }
 
 }  // namespace rv
 
 using namespace rv;
 
-int rv_diamond_search_batch_counted(const rv_plane *org, const rv_plane *ref,
-                                    const rv_ds_job *d_jobs, int n, int blk_w, int blk_h,
-                                    int subpixel, int use_satd, int allow_hp, int bit_depth,
-                                    rv_fs_result *d_out, unsigned long long *evals,
-                                    void *stream) {
+// Multi-reference form used by the replay driver: jobs [n_refs][n_per_ref],
+// job i searches refs[i / n_per_ref]; evals (optional) receives the
+// in-range candidate evaluations per job.
+int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
+                            const rv_ds_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
+                            int subpixel, int use_satd, int allow_hp, int bit_depth,
+                            rv_fs_result *d_out, uint32_t *d_evals, void *stream) {
   auto p2 = [](int v) { return v >= 4 && v <= 128 && (v & (v - 1)) == 0; };
-  if (!org || !ref || n < 0 || !p2(blk_w) || !p2(blk_h) ||
-      org->hbd != ref->hbd ||
-      (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
+  if (!org || !refs || n_refs < 1 || n_refs > RV_DS_MAX_PRED || n_per_ref < 0 || !p2(blk_w) ||
+      !p2(blk_h) || (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
       (!org->hbd && bit_depth != 8))
     return rv_set_error(RV_EINVAL, "rv_diamond_search_batch: bad arguments");
+  for (int k = 0; k < n_refs; k++)
+    if (refs[k].hbd != org->hbd)
+      return rv_set_error(RV_EINVAL, "rv_diamond_search_batch: pixel type mismatch");
+  const int n = n_refs * n_per_ref;
   if (n == 0) return RV_OK;
-  DsArgs a{*org, *ref, d_jobs, d_out, n, blk_w, blk_h, subpixel ? 1 : 0,
-           use_satd ? 1 : 0, allow_hp ? 1 : 0, bit_depth, evals};
-  const size_t lds = subpixel ? (size_t)((blk_w + 7) * (blk_h + 7) + (blk_h + 7) * blk_w +
-                                         blk_w * blk_h) * sizeof(int16_t)
-                              : 0;
+  DsArgs a;
+  memset(&a, 0, sizeof(a));
+  a.org = *org;
+  for (int k = 0; k < n_refs; k++) a.ref[k] = refs[k];
+  a.jobs = d_jobs;
+  a.out = d_out;
+  a.n = n;
+  a.n_per_ref = n_per_ref;
+  a.w = blk_w;
+  a.h = blk_h;
+  a.subpel = subpixel ? 1 : 0;
+  a.satd = use_satd ? 1 : 0;
+  a.hp = allow_hp ? 1 : 0;
+  a.bd = bit_depth;
+  a.evals = d_evals;
   hipStream_t s = rv_resolve_stream(stream);
-  if (org->hbd)
-    diamond_kernel<uint16_t><<<n, kDsThreads, lds, s>>>(a);
-  else
-    diamond_kernel<uint8_t><<<n, kDsThreads, lds, s>>>(a);
+  const bool fast = org->hbd ? try_fast<uint16_t>(a, s) : try_fast<uint8_t>(a, s);
+  if (!fast) {
+    const size_t lds = subpixel ? (size_t)((blk_w + 7) * (blk_h + 7) + (blk_h + 7) * blk_w +
+                                           blk_w * blk_h) * sizeof(int16_t)
+                                : 0;
+    if (org->hbd)
+      diamond_kernel<uint16_t><<<n, kDsThreads, lds, s>>>(a);
+    else
+      diamond_kernel<uint8_t><<<n, kDsThreads, lds, s>>>(a);
+  }
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }
@@ -312,7 +680,7 @@ extern "C" int rv_diamond_search_batch(const rv_plane *org, const rv_plane *ref,
                                        int blk_h, int subpixel, int use_satd,
                                        int allow_hp, int bit_depth,
                                        rv_fs_result *d_out, void *stream) {
-  return rv_diamond_search_batch_counted(org, ref, d_jobs, n, blk_w, blk_h, subpixel,
-                                         use_satd, allow_hp, bit_depth, d_out, nullptr,
-                                         stream);
+  if (!ref) return rv_set_error(RV_EINVAL, "rv_diamond_search_batch: null ref");
+  return rv_diamond_search_multi(org, ref, 1, d_jobs, n, blk_w, blk_h, subpixel, use_satd,
+                                 allow_hp, bit_depth, d_out, nullptr, stream);
 }

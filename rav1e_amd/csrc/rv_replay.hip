@@ -29,12 +29,12 @@
 
 #include "rv_device.h"
 
-// rv_me_diamond.hip: the public batch entry plus an evaluation counter
-int rv_diamond_search_batch_counted(const rv_plane *org, const rv_plane *ref,
-                                    const rv_ds_job *d_jobs, int n, int blk_w, int blk_h,
-                                    int subpixel, int use_satd, int allow_hp, int bit_depth,
-                                    rv_fs_result *d_out, unsigned long long *evals,
-                                    void *stream);
+// rv_me_diamond.hip: every reference in one launch + per-job evaluation
+// counts
+int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
+                            const rv_ds_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
+                            int subpixel, int use_satd, int allow_hp, int bit_depth,
+                            rv_fs_result *d_out, uint32_t *d_evals, void *stream);
 
 namespace rv {
 
@@ -220,43 +220,41 @@ __global__ void coeff_checksum(const int32_t *packed, int64_t total, int per_blo
 }
 
 // Candidate score = luma SSE (from the cdef moments) + chroma SSE, then the
-// per-superblock argmin (first minimum) and result words.
-__global__ void score_candidates(Geo g, const int64_t *lmom, const uint64_t *usse,
-                                 const uint64_t *vsse, int lsub, int csub,
-                                 const rv_fs_result *coarse, const rv_fs_result *half,
-                                 const rv_fs_result *full, const rv_fs_result *sub,
-                                 uint64_t *words) {
-  const int sb = blockIdx.x * blockDim.x + threadIdx.x;
-  if (sb >= g.nsb) return;
+// per-superblock argmin (first minimum) and result words.  One wavefront
+// per superblock: lanes stride over the sub-blocks of a candidate.
+__global__ __launch_bounds__(64) void score_candidates(
+    Geo g, const int64_t *lmom, const uint64_t *usse, const uint64_t *vsse, int lsub, int csub,
+    const rv_fs_result *coarse, const rv_fs_result *half, const rv_fs_result *full,
+    const rv_fs_result *sub, uint64_t *words) {
+  const int sb = blockIdx.x;
+  const int lane = threadIdx.x;
   uint64_t best = ~0ull;
   int best_c = 0;
   for (int c = 0; c < g.C; c++) {
-    const int o = c * g.nsb + sb;  // candidate-major, like the MC jobs
+    const int64_t o = (int64_t)c * g.nsb + sb;  // candidate-major, like the MC jobs
     uint64_t s = 0;
-    for (int k = 0; k < lsub; k++) {
-      const int64_t *m = lmom + ((int64_t)o * lsub + k) * 5;
+    for (int k = lane; k < lsub; k += 64) {
+      const int64_t *m = lmom + (o * lsub + k) * 5;
       s += (uint64_t)(m[3] + m[2] - 2 * m[4]);
     }
-    for (int k = 0; k < csub; k++) s += usse[(int64_t)o * csub + k] + vsse[(int64_t)o * csub + k];
+    for (int k = lane; k < csub; k += 64) s += usse[o * csub + k] + vsse[o * csub + k];
+    s = group_sum<64>(s);
     if (s < best) {
       best = s;
       best_c = c;
     }
   }
   uint64_t *w = words + (int64_t)sb * (8 * g.R + 2);
-  for (int r = 0; r < g.R; r++) {
-    const int i = r * g.nsb + sb;
-    w[8 * r + 0] = pack_mv(coarse[i].best_mv);
-    w[8 * r + 1] = coarse[i].cost;
-    w[8 * r + 2] = pack_mv(half[i].best_mv);
-    w[8 * r + 3] = half[i].cost;
-    w[8 * r + 4] = pack_mv(full[i].best_mv);
-    w[8 * r + 5] = full[i].cost;
-    w[8 * r + 6] = pack_mv(sub[i].best_mv);
-    w[8 * r + 7] = sub[i].cost;
+  for (int i = lane; i < 8 * g.R; i += 64) {
+    const int r = i >> 3, f = i & 7;
+    const rv_fs_result *src = (f >> 1) == 0 ? coarse : (f >> 1) == 1 ? half : (f >> 1) == 2 ? full : sub;
+    const rv_fs_result v = src[r * g.nsb + sb];
+    w[i] = (f & 1) ? v.cost : pack_mv(v.best_mv);
   }
-  w[8 * g.R] = (uint64_t)best_c;
-  w[8 * g.R + 1] = best;
+  if (lane == 0) {
+    w[8 * g.R] = (uint64_t)best_c;
+    w[8 * g.R + 1] = best;
+  }
 }
 
 // F5 jobs: every 8x8 luma block of the tile inside the frame, against
@@ -332,10 +330,13 @@ struct rv_replay {
   // 7..14 kernel brackets), so per-kernel times can be summed over a whole
   // timed run without a host sync per frame.
   static constexpr int kRing = 64;
-  hipEvent_t evs[kRing][16];
+  static constexpr int kEv = 20;
+  hipEvent_t evs[kRing][kEv];
   hipEvent_t *ev;
   long frames = 0;
-  unsigned long long *ds_evals;  // diamond candidate evaluations [full, sub]
+  // diamond candidate evaluations per job, per ring slot: [kRing][2][nsb*R]
+  // (F3 full-pel, F3 sub-pel)
+  uint32_t *ds_evals;
 };
 
 namespace {
@@ -464,7 +465,7 @@ void rv_replay_destroy(rv_replay *r) {
   if (!r) return;
   for (void *p : r->allocs) (void)hipFree(p);
   for (int f = 0; f < rv_replay::kRing; f++)
-    for (int i = 0; i < 16; i++)
+    for (int i = 0; i < rv_replay::kEv; i++)
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
   if (r->own_stream && r->stream) (void)hipStreamDestroy(r->stream);
   delete r;
@@ -567,9 +568,10 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->imp_satd = (uint32_t *)dalloc(r, (size_t)r->n_imp * 4);
   r->tail = (unsigned long long *)dalloc(r, 4 * 8);
   for (int f = 0; f < rv_replay::kRing; f++)
-    for (int i = 0; i < 16; i++) ok = ok && hipEventCreate(&r->evs[f][i]) == hipSuccess;
-  r->ds_evals = (unsigned long long *)dalloc(r, 4 * 8);
-  ok = ok && r->ds_evals && hipMemsetAsync(r->ds_evals, 0, 4 * 8, r->stream) == hipSuccess;
+    for (int i = 0; i < rv_replay::kEv; i++) ok = ok && hipEventCreate(&r->evs[f][i]) == hipSuccess;
+  const size_t ev_bytes = (size_t)rv_replay::kRing * 2 * nr * 4;
+  r->ds_evals = (uint32_t *)dalloc(r, ev_bytes);
+  ok = ok && r->ds_evals && hipMemsetAsync(r->ds_evals, 0, ev_bytes, r->stream) == hipSuccess;
   ok = ok && r->tall_y.data && r->tall_u.data && r->tall_v.data && r->tail;
   if (!ok || build_static_jobs(r) != RV_OK) {
     rv_set_error(RV_EHIP, "rv_replay_create: device allocation failed");
@@ -608,6 +610,11 @@ int rv_replay_set_frame(rv_replay *r, int slot, const void *host_yuv) {
   return RV_OK;
 }
 
+// Event layout per frame (ring slot): 0..6 stage bounds F0..F5; then
+// kernel brackets [7,8] F3 full-pel diamond, [9,10] F3 sub-pel diamond,
+// [11,12] luma put_8tap, [13,14] luma diff + fwd TX_64X64, [15,16] luma
+// inverse TX_64X64 + add, [17,18] luma cdef moments.  F1 ([1,2]) holds only
+// the full-search launches.
 int rv_replay_frame(rv_replay *r, int me_range_scale) {
   if (!r || (me_range_scale != 1 && me_range_scale != 2 && me_range_scale != 4))
     return rv_set_error(RV_EINVAL, "rv_replay_frame: bad me_range_scale");
@@ -620,8 +627,16 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   const int si = me_range_scale == 1 ? 0 : me_range_scale == 2 ? 1 : 2;
   const uint32_t lambda2 = (uint32_t)(r->me_lambda * 256.0 / 4.0 * 0.125);
   const uint32_t lambda1 = (uint32_t)(r->me_lambda * 256.0 * 0.5);
+  rv_plane refs_y[RV_DS_MAX_PRED], refs_h[RV_DS_MAX_PRED];
+  for (int k = 0; k < g.R; k++) {
+    refs_y[k] = r->slots[1 + k].y;
+    refs_h[k] = r->slots[1 + k].hres;
+  }
+  const int slot = (int)(r->frames % rv_replay::kRing);
+  uint32_t *ev_full = r->ds_evals + (size_t)slot * 2 * nr * g.R;
+  uint32_t *ev_sub = ev_full + (size_t)nr * g.R;
 
-  r->ev = r->evs[r->frames % rv_replay::kRing];
+  r->ev = r->evs[slot];
   r->frames++;
   RV_H(hipEventRecord(r->ev[0], st));
   RV_H(hipMemsetAsync(r->tail + 2, 0, 8, st));
@@ -634,32 +649,32 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
     RV_R(rv_full_search_batch(&cur.qres, &r->slots[1 + k].qres, r->fs_jobs[si] + k * nr, nr, 16,
                               16, 1, 0, r->coarse + k * nr, st));
   RV_H(hipEventRecord(r->ev[2], st));  // = the full-search kernel bracket
-  // F2 half-res diamond
+  // F2 half-res diamond, every reference in one launch
   make_ss2_jobs<<<blocks(nr * g.R), T, 0, st>>>(g, r->coarse, lambda2, r->ds_jobs);
-  for (int k = 0; k < g.R; k++)
-    RV_R(rv_diamond_search_batch(&cur.hres, &r->slots[1 + k].hres, r->ds_jobs + k * nr, nr, 32,
-                                 32, 0, 0, 0, g.bd, r->half + k * nr, st));
+  RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->ds_jobs, nr, 32, 32, 0, 0, 0, g.bd,
+                               r->half, nullptr, st));
   RV_H(hipEventRecord(r->ev[3], st));
   // F3 full-res full-pel + sub-pel diamond (speed 10: SAD, no hp)
   make_full_jobs<<<blocks(nr * g.R), T, 0, st>>>(g, r->half, lambda1, r->ds_jobs);
-  for (int k = 0; k < g.R; k++)
-    RV_R(rv_diamond_search_batch_counted(&cur.y, &r->slots[1 + k].y, r->ds_jobs + k * nr, nr, 64,
-                                         64, 0, 0, 0, g.bd, r->full + k * nr, r->ds_evals, st));
+  RV_H(hipEventRecord(r->ev[7], st));
+  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->ds_jobs, nr, 64, 64, 0, 0, 0, g.bd,
+                               r->full, ev_full, st));
+  RV_H(hipEventRecord(r->ev[8], st));
   make_subpel_jobs<<<blocks(nr * g.R), T, 0, st>>>(nr * g.R, r->full, r->ds_jobs);
-  for (int k = 0; k < g.R; k++)
-    RV_R(rv_diamond_search_batch_counted(&cur.y, &r->slots[1 + k].y, r->ds_jobs + k * nr, nr, 64,
-                                         64, 1, 0, 0, g.bd, r->sub + k * nr, r->ds_evals + 1,
-                                         st));
+  RV_H(hipEventRecord(r->ev[9], st));
+  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->ds_jobs, nr, 64, 64, 1, 0, 0, g.bd,
+                               r->sub, ev_sub, st));
+  RV_H(hipEventRecord(r->ev[10], st));
   RV_H(hipEventRecord(r->ev[4], st));
   // F4 RDO candidates
   make_mc_jobs<<<blocks(g.nctx), T, 0, st>>>(g, r->sub, cur.y, cur.u, r->l_mc, r->c_mc);
-  RV_H(hipEventRecord(r->ev[7], st));
-  for (int k = 0; k < g.R; k++) {  // luma put_8tap: kernel bracket 7..8
+  RV_H(hipEventRecord(r->ev[11], st));
+  for (int k = 0; k < g.R; k++) {  // luma put_8tap
     const int o = k * 2 * nr;        // both candidates of reference k
     RV_R(rv_put_8tap_batch(&r->tall_y, &r->slots[1 + k].y, r->l_mc + o, 2 * nr, kSb, kSb, 0, 0,
                            g.bd, st));
   }
-  RV_H(hipEventRecord(r->ev[8], st));
+  RV_H(hipEventRecord(r->ev[12], st));
   for (int k = 0; k < g.R; k++) {
     const RvFrameSlot &ref = r->slots[1 + k];
     const int o = k * 2 * nr;
@@ -670,27 +685,27 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   const int nct = g.nctx * ntx_c;
   int32_t *u_raster = r->c_raster, *v_raster = r->c_raster + (size_t)nct * 1024;
   int32_t *u_packed = r->c_packed, *v_packed = r->c_packed + (size_t)nct * 1024;
-  RV_H(hipEventRecord(r->ev[9], st));  // luma diff + fwd TX_64X64: 9..10
+  RV_H(hipEventRecord(r->ev[13], st));
   RV_R(rv_diff_fwd_txfm_batch(&cur.y, &r->tall_y, r->l_tx, g.nctx, 4, 0, g.bd, r->l_raster, st));
-  RV_H(hipEventRecord(r->ev[10], st));
+  RV_H(hipEventRecord(r->ev[14], st));
   RV_R(rv_diff_fwd_txfm_batch(&cur.u, &r->tall_u, r->c_tx, nct, 3, 0, g.bd, u_raster, st));
   RV_R(rv_diff_fwd_txfm_batch(&cur.v, &r->tall_v, r->c_tx, nct, 3, 0, g.bd, v_raster, st));
   pack_coeffs<<<blocks((int64_t)g.nctx * 1024), T, 0, st>>>(r->l_raster, g.nctx, 64, 64,
                                                              r->l_packed);
   pack_coeffs<<<blocks((int64_t)nct * 1024), T, 0, st>>>(u_raster, nct, 32, 32, u_packed);
   pack_coeffs<<<blocks((int64_t)nct * 1024), T, 0, st>>>(v_raster, nct, 32, 32, v_packed);
-  RV_H(hipEventRecord(r->ev[11], st));  // luma inverse TX_64X64 + add: 11..12
+  RV_H(hipEventRecord(r->ev[15], st));
   RV_R(rv_inv_txfm_add_batch(r->l_packed, &r->tall_y, r->l_tx, g.nctx, 4, 0, g.bd, st));
-  RV_H(hipEventRecord(r->ev[12], st));
+  RV_H(hipEventRecord(r->ev[16], st));
   RV_R(rv_inv_txfm_add_batch(u_packed, &r->tall_u, r->c_tx, nct, 3, 0, g.bd, st));
   RV_R(rv_inv_txfm_add_batch(v_packed, &r->tall_v, r->c_tx, nct, 3, 0, g.bd, st));
-  RV_H(hipEventRecord(r->ev[13], st));  // luma cdef moments: 13..14
+  RV_H(hipEventRecord(r->ev[17], st));
   RV_R(rv_cdef_moments_batch(&cur.y, &r->tall_y, r->l_dist, g.nctx, kSb, kSb, r->l_mom, st));
-  RV_H(hipEventRecord(r->ev[14], st));
+  RV_H(hipEventRecord(r->ev[18], st));
   RV_R(rv_sse_batch(&cur.u, &r->tall_u, r->c_dist, g.nctx, g.cw, g.ch, r->u_sse, st));
   RV_R(rv_sse_batch(&cur.v, &r->tall_v, r->c_dist, g.nctx, g.cw, g.ch, r->v_sse, st));
-  score_candidates<<<blocks(g.nsb), T, 0, st>>>(g, r->l_mom, r->u_sse, r->v_sse, r->lsub, r->csub,
-                                                r->coarse, r->half, r->full, r->sub, r->words);
+  score_candidates<<<g.nsb, 64, 0, st>>>(g, r->l_mom, r->u_sse, r->v_sse, r->lsub, r->csub,
+                                         r->coarse, r->half, r->full, r->sub, r->words);
   RV_H(hipEventRecord(r->ev[5], st));
   // F5 importance SATD against reference 1
   make_imp_jobs<<<blocks(r->n_imp), T, 0, st>>>(g, r->sub, r->imp_jobs, r->imp_bx, r->imp_by);
@@ -735,7 +750,7 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
   if (last < 1) last = 1;
   if (last > rv_replay::kRing) last = rv_replay::kRing;
   if (last > r->frames) last = (int)r->frames;
-  for (int i = 0; i < cap && i < 10; i++) ms_out[i] = 0.f;
+  for (int i = 0; i < cap && i < 12; i++) ms_out[i] = 0.f;
   int n = 0;
   for (int f = 0; f < last; f++) {
     hipEvent_t *e = r->evs[(r->frames - 1 - f) % rv_replay::kRing];
@@ -746,7 +761,7 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
       RV_H(hipEventElapsedTime(&ms, e[i], e[i + 1]));
       ms_out[n++] += ms;
     }
-    for (int i = 7; i < 15 && n < cap; i += 2) {  // luma put, fwd, inv, cdef
+    for (int i = 7; i < 19 && n < cap; i += 2) {  // kernel brackets
       float ms = 0.f;
       RV_H(hipEventElapsedTime(&ms, e[i], e[i + 1]));
       ms_out[n++] += ms;
@@ -761,11 +776,22 @@ int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap) {
 int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out, int cap) {
   return stage_times(r, ms_out, cap, last_frames);
 }
+// Diamond-search candidate evaluations summed over the last min(frames, 64)
+// frames: out[0] F3 full-pel, out[1] F3 sub-pel, out[2] frames summed.
 int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
-  if (!r || !out || cap < 2) return rv_set_error(RV_EINVAL, "rv_replay_counters");
+  if (!r || !out || cap < 3) return rv_set_error(RV_EINVAL, "rv_replay_counters");
+  const Geo &g = r->g;
+  const int nj = g.nsb * g.R;
+  const int nf = r->frames < rv_replay::kRing ? (int)r->frames : rv_replay::kRing;
   RV_H(hipStreamSynchronize(r->stream));
-  RV_H(hipMemcpy(out, r->ds_evals, 2 * 8, hipMemcpyDeviceToHost));
-  return 2;
+  std::vector<uint32_t> h((size_t)nf * 2 * nj);
+  if (nf) RV_H(hipMemcpy(h.data(), r->ds_evals, h.size() * 4, hipMemcpyDeviceToHost));
+  out[0] = out[1] = 0;
+  for (int f = 0; f < nf; f++)
+    for (int k = 0; k < 2; k++)
+      for (int j = 0; j < nj; j++) out[k] += h[((size_t)f * 2 + k) * nj + j];
+  out[2] = (uint64_t)nf;
+  return 3;
 }
 
 }  // extern "C"

@@ -100,22 +100,23 @@ class HipReplay:
         return out[:n]
 
     def stage_ms(self) -> np.ndarray:
-        out = np.zeros(10, dtype=np.float32)
-        n = lib().rv_replay_stage_times(self.h, out.ctypes.data, 10)
+        out = np.zeros(12, dtype=np.float32)
+        n = lib().rv_replay_stage_times(self.h, out.ctypes.data, 12)
         if n < 0:
             _check(n, "rv_replay_stage_times")
         return out[:n]
 
     def stage_ms_sum(self, last_frames: int) -> np.ndarray:
-        out = np.zeros(10, dtype=np.float32)
-        n = lib().rv_replay_stage_times_sum(self.h, last_frames, out.ctypes.data, 10)
+        out = np.zeros(12, dtype=np.float32)
+        n = lib().rv_replay_stage_times_sum(self.h, last_frames, out.ctypes.data, 12)
         if n < 0:
             _check(n, "rv_replay_stage_times_sum")
         return out[:n]
 
     def counters(self) -> np.ndarray:
-        out = np.zeros(2, dtype=np.uint64)
-        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 2) - 2, "rv_replay_counters")
+        """[F3 full-pel evals, F3 sub-pel evals, frames] over the last <= 64 frames."""
+        out = np.zeros(3, dtype=np.uint64)
+        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 3) - 3, "rv_replay_counters")
         return out
 
     def close(self):

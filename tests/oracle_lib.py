@@ -203,6 +203,47 @@ def full_search(org_full, ref_full, xorigin, yorigin, job, blk_w, blk_h, step, a
     return (best.row, best.col), cost.value
 
 
+class _DsCtx(C.Structure):
+    _fields_ = [("org", C.c_void_p), ("org_stride", C.c_ssize_t), ("ref", C.c_void_p),
+                ("ref_stride", C.c_ssize_t)] + [(f, C.c_int) for f in (
+                    "ref_width", "ref_height", "ref_xorigin", "ref_yorigin", "ref_xdec",
+                    "ref_ydec", "hbd", "bit_depth", "po_x", "po_y", "w", "h", "mvx_min",
+                    "mvx_max", "mvy_min", "mvy_max")] + [
+                ("pmv", _Mv * 2), ("lambda_", C.c_uint32), ("subpel", C.c_int),
+                ("satd", C.c_int), ("allow_hp", C.c_int)]
+
+
+def diamond_search(org_full, ref_full, xorigin, yorigin, width, height, job, w, h, subpel,
+                   satd, allow_hp, bd):
+    """orc_diamond_search for one DS_JOB record on full padded arrays (both
+    planes share the geometry).  Returns ((row, col), cost)."""
+    L = lib()
+    L.orc_diamond_search.argtypes = [C.POINTER(_DsCtx), C.POINTER(_Mv), C.c_int,
+                                     C.POINTER(_Mv), C.POINTER(C.c_uint64)]
+    c = _DsCtx()
+    c.org = ptr(org_full, yorigin * org_full.shape[1] + xorigin)
+    c.org_stride = org_full.shape[1]
+    c.ref = ptr(ref_full, yorigin * ref_full.shape[1] + xorigin)
+    c.ref_stride = ref_full.shape[1]
+    c.ref_width, c.ref_height, c.ref_xorigin, c.ref_yorigin = width, height, xorigin, yorigin
+    c.ref_xdec = c.ref_ydec = 0
+    c.hbd, c.bit_depth = hbd_of(org_full), bd
+    c.po_x, c.po_y, c.w, c.h = int(job["po_x"]), int(job["po_y"]), w, h
+    c.mvx_min, c.mvx_max = int(job["mvx_min"]), int(job["mvx_max"])
+    c.mvy_min, c.mvy_max = int(job["mvy_min"]), int(job["mvy_max"])
+    c.pmv[0] = _Mv(int(job["pmv0_row"]), int(job["pmv0_col"]))
+    c.pmv[1] = _Mv(int(job["pmv1_row"]), int(job["pmv1_col"]))
+    c.lambda_ = int(job["lambda_"])
+    c.subpel, c.satd, c.allow_hp = int(subpel), int(satd), int(allow_hp)
+    n = int(job["n_pred"])
+    preds = (_Mv * max(1, n))(*[_Mv(int(job["pred"][k][0]), int(job["pred"][k][1]))
+                                for k in range(n)])
+    best = _Mv(0, 0)
+    cost = C.c_uint64(0)
+    L.orc_diamond_search(C.byref(c), preds, n, C.byref(best), C.byref(cost))
+    return (best.row, best.col), cost.value
+
+
 class CpuReplay:
     """orc_replay_* (oracle/orc_replay.c): the replay schedule on the CPU."""
 

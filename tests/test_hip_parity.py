@@ -353,6 +353,70 @@ def test_full_search_empty_window():
     assert got[0]["cost"] == 2 ** 64 - 1 and got[0]["mv_row"] == 0 and got[0]["mv_col"] == 0
 
 
+def _ds_case(rng, bd, w, h, nj, subpel, edge=False):
+    H, W = 200, 280
+    org = rand_plane(rng, H, W, bd) if not edge else np.zeros((H, W), np.uint16 if bd > 8
+                                                             else np.uint8)
+    # reference = org moved by a sub-pel-ish amount plus noise, so the search has a trend
+    ref = np.roll(org, (2, -3), (0, 1))
+    if not edge:
+        noise = rng.integers(-3, 4, ref.shape)
+        ref = np.clip(ref.astype(np.int32) + noise, 0, (1 << bd) - 1).astype(org.dtype)
+    else:  # 0 / max step edges: the MC overshoot cases
+        ref[:, ::2] = (1 << bd) - 1
+    po_ = R.DevicePlane.from_array(org, xpad=88, ypad=88)
+    pr_ = R.DevicePlane.from_array(ref, xpad=88, ypad=88)
+    fo, fr = po_.download_full(), pr_.download_full()
+    jobs = np.zeros(nj, dtype=R.DS_JOB)
+    for k in range(nj):
+        px = int(rng.integers(-8, W - w + 8)) if k % 3 else 0
+        py = int(rng.integers(-8, H - h + 8)) if k % 3 else H - h
+        span = 8 * int(rng.integers(2, 24))
+        jobs[k]["po_x"], jobs[k]["po_y"] = px, py
+        jobs[k]["mvx_min"], jobs[k]["mvx_max"] = -span, span
+        jobs[k]["mvy_min"], jobs[k]["mvy_max"] = -span // 2, span // 2
+        jobs[k]["pmv0_row"], jobs[k]["pmv0_col"] = rng.integers(-40, 40, 2)
+        jobs[k]["lambda_"] = int(rng.integers(0, 4000))
+        n = int(rng.integers(1, 9))
+        jobs[k]["n_pred"] = n
+        step = 1 if subpel else 8
+        jobs[k]["pred"][:n] = rng.integers(-12, 12, (n, 2)) * step
+        if k % 4 == 1:  # a predictor out of range
+            jobs[k]["pred"][0] = (span + 8, 0)
+    return po_, pr_, fo, fr, jobs, W, H
+
+
+@pytest.mark.parametrize("bd,w,h,subpel,satd", [
+    (8, 64, 64, False, False), (8, 64, 64, True, False), (8, 32, 32, False, False),
+    (8, 32, 32, True, False), (8, 16, 32, True, False), (8, 64, 32, True, False),
+    (10, 64, 64, False, False), (10, 64, 64, True, False), (10, 32, 32, True, False),
+    (8, 8, 8, True, False), (8, 16, 16, True, True), (10, 32, 32, False, True),
+])
+def test_diamond_search_vs_oracle(bd, w, h, subpel, satd):
+    """Fast (wavefront-per-candidate) and generic paths vs orc_diamond_search."""
+    rng = np.random.default_rng(1100 + w + 7 * h + bd + subpel)
+    po_, pr_, fo, fr, jobs, W, H = _ds_case(rng, bd, w, h, 24, subpel)
+    xo, yo = po_.desc.xorigin, po_.desc.yorigin
+    for hp in (False, True) if subpel else (False,):
+        got = R.diamond_search_batch(po_, pr_, jobs, w, h, subpel, satd, hp, bd)
+        for k, j in enumerate(jobs):
+            mv, cost = O.diamond_search(fo, fr, xo, yo, W, H, j, w, h, subpel, satd, hp, bd)
+            assert (got[k]["mv_row"], got[k]["mv_col"], got[k]["cost"]) == (mv[0], mv[1], cost), \
+                (k, hp, got[k], mv, cost)
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_diamond_subpel_edges_vs_oracle(bd):
+    """0/max column stripes (8-tap overshoot) and blocks clamped at the frame edge."""
+    rng = np.random.default_rng(1200 + bd)
+    po_, pr_, fo, fr, jobs, W, H = _ds_case(rng, bd, 64, 64, 16, True, edge=True)
+    xo, yo = po_.desc.xorigin, po_.desc.yorigin
+    got = R.diamond_search_batch(po_, pr_, jobs, 64, 64, True, False, False, bd)
+    for k, j in enumerate(jobs):
+        mv, cost = O.diamond_search(fo, fr, xo, yo, W, H, j, 64, 64, True, False, False, bd)
+        assert (got[k]["mv_row"], got[k]["mv_col"], got[k]["cost"]) == (mv[0], mv[1], cost), k
+
+
 # ---- frame layout -----------------------------------------------------------
 @pytest.mark.parametrize("hbd", [False, True])
 def test_pad_and_downsample_vs_oracle(hbd):
