@@ -135,6 +135,9 @@ def main():
                  for s in scales) / 4.0
     nj = nsb * nref
     nctx = nsb * 2 * nref
+    cw, ch = 64 >> xdec, 64 >> ydec
+    ntx_c = (cw // 32) * (ch // 32)
+    csub = (cw // (min(cw, 8) >> xdec)) * (ch // (min(ch, 8) >> ydec))
     kernels = {
         "full_search": dict(ms=float(ms[1]), launches=nref, bytes=fs_bytes, sad_px=fs_ops),
         "diamond_fullpel_64": dict(ms=float(ms[6]), launches=1,
@@ -143,14 +146,13 @@ def main():
         "diamond_subpel_64": dict(ms=float(ms[7]), launches=1,
                                   bytes=nj * (64 * 64 * px + 80) +
                                   ev_sub / ev_frames * 71 * 71 * px),
-        "put_luma_64": dict(ms=float(ms[8]), launches=nref,
-                            bytes=float(nctx * (71 * 71 * px + 64 * 64 * px))),
-        "diff_fwd_64": dict(ms=float(ms[9]), launches=1,
-                            bytes=float(nctx * (2 * 64 * 64 * px + 4 * 64 * 64))),
-        "inv_add_64": dict(ms=float(ms[10]), launches=1,
-                           bytes=float(nctx * (4 * 32 * 32 + 2 * 64 * 64 * px))),
-        "cdef_moments_64": dict(ms=float(ms[11]), launches=1,
-                                bytes=float(nctx * (2 * 64 * 64 * px + 64 * 40))),
+        "rdo_luma_64": dict(ms=float(ms[8]), launches=1,
+                            bytes=float(nctx * (71 * 71 * px + 64 * 64 * px + 4 * 32 * 32 +
+                                                64 * 64 * px + 64 * 40 + 16 + 24))),
+        "rdo_chroma": dict(ms=float(ms[9]), launches=1,
+                           bytes=float(2 * nctx * ((cw + 7) * (ch + 7) * px + 2 * cw * ch * px +
+                                                   4 * ntx_c * 32 * 32 + 8 * csub + 16 +
+                                                   24 * ntx_c))),
     }
     dom = max(kernels, key=lambda n: kernels[n]["ms"])
     kd = kernels[dom]

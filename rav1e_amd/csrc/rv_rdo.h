@@ -1,0 +1,34 @@
+// rv_rdo.h -- the fused RDO inter-candidate launch (rv_rdo.hip), used by the
+// replay driver's stage F4.
+#pragma once
+
+#include "rv_device.h"
+
+namespace rv {
+
+struct RdoPlane {
+  rv_plane org;                  // source plane
+  rv_plane ref[RV_DS_MAX_PRED];  // reference planes of this plane type
+  rv_plane dst;                  // tall prediction / reconstruction plane
+  const rv_mc_job *mc;           // per candidate
+  const rv_tx_job *tx;           // per (candidate, transform block)
+  int32_t *packed;               // per transform block: min(N,32)^2 i32
+  void *dist;                    // luma: i64 x 5 per 8x8; chroma: u64 per sub-block
+};
+
+struct RdoArgs {
+  RdoPlane p[2];      // blockIdx.y selects the plane (chroma: U, V)
+  int n_tx;           // transform blocks per plane
+  int ntx_per_cand;   // transform blocks per candidate
+  int cands_per_ref;  // candidates of one reference (job arrays are ref-major)
+  int bd;
+  int mb_w, mb_h;     // MC block size (filter choice, distortion grid)
+  int sub_w, sub_h;   // distortion sub-block (SSE); moments use 8x8
+};
+
+}  // namespace rv
+
+// n = transform size (64 luma / 32 chroma); moments: cdef moments (luma)
+// else SSE partials.
+int rv_rdo_candidates(const rv::RdoArgs &a, int nplanes, int n, int moments, int hbd,
+                      hipStream_t s);

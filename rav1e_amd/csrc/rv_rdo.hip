@@ -1,0 +1,346 @@
+// rv_rdo.hip -- fused RDO inter-candidate evaluation (replay stage F4).
+//
+// One wavefront per (candidate, transform block) runs the whole per-
+// candidate chain of encode_tx_block (src/encoder.rs:1077-1237) for the
+// pixel-domain distortion of the default tune (src/rdo.rs:338-411):
+//
+//   predict_inter's put_8tap (src/mc.rs:213-307, REGULAR, via
+//   src/predict.rs:255-338)            -> prediction in LDS
+//   diff (src/encoder.rs:1044-1058) + FwdTxfm2D::fht DCT_DCT
+//   (src/transform/forward.rs:1804-1899) -> coefficients in LDS
+//   quantize/dequantize stand-in (v / 8 * 8 on the top-left
+//   min(W,32) x min(H,32), the packed layout inverse_transform_add reads)
+//                                      -> packed coefficients to HBM
+//   inv_txfm2d_add (src/transform/inverse.rs:1939-2114)
+//                                      -> reconstruction in LDS + HBM
+//   cdef_dist_wxh_8x8 moments (src/rdo.rs:219-241, luma) or sse_wxh
+//   partials (src/rdo.rs:286-335, chroma) -> HBM
+//
+// Every intermediate (prediction, residual, 64x64 i32 coefficient block,
+// reconstruction) stays in the wavefront's LDS slab; HBM sees the reference
+// window, the source block, and the results the encoder keeps.  The
+// standalone batched kernels (rv_put_8tap_batch, rv_diff_fwd_txfm_batch,
+// rv_inv_txfm_add_batch, rv_cdef_moments_batch, rv_sse_batch) compute the
+// same values one stage per launch; the replay parity test pins the fused
+// kernel to the CPU replay, which chains the oracle's restatements of them.
+#include <string.h>
+
+#include "rv_rdo.h"
+#include "rv_tx.h"
+
+namespace rv {
+
+constexpr int kQstep = 8;  // quantize/dequantize stand-in
+
+// SUBPEL_FILTERS REGULAR (src/mc.rs:70-179): [0] 8-tap, [1] 4-tap (get_filter
+// for length <= 4, src/mc.rs:201-210).  Frac 0 is never filtered.
+__constant__ int8_t kRdoReg[2][16][8] = {
+    {{0, 0, 0, 127, 0, 0, 0, 0}, {0, 2, -6, 126, 8, -2, 0, 0},
+     {0, 2, -10, 122, 18, -4, 0, 0}, {0, 2, -12, 116, 28, -8, 2, 0},
+     {0, 2, -14, 110, 38, -10, 2, 0}, {0, 2, -14, 102, 48, -12, 2, 0},
+     {0, 2, -16, 94, 58, -12, 2, 0}, {0, 2, -14, 84, 66, -12, 2, 0},
+     {0, 2, -14, 76, 76, -14, 2, 0}, {0, 2, -12, 66, 84, -14, 2, 0},
+     {0, 2, -12, 58, 94, -16, 2, 0}, {0, 2, -12, 48, 102, -14, 2, 0},
+     {0, 2, -10, 38, 110, -14, 2, 0}, {0, 2, -8, 28, 116, -12, 2, 0},
+     {0, 0, -4, 18, 122, -10, 2, 0}, {0, 0, -2, 8, 126, -6, 2, 0}},
+    {{0, 0, 0, 127, 0, 0, 0, 0}, {0, 0, -4, 126, 8, -2, 0, 0},
+     {0, 0, -8, 122, 18, -4, 0, 0}, {0, 0, -10, 116, 28, -6, 0, 0},
+     {0, 0, -12, 110, 38, -8, 0, 0}, {0, 0, -12, 102, 48, -10, 0, 0},
+     {0, 0, -14, 94, 58, -10, 0, 0}, {0, 0, -12, 84, 66, -10, 0, 0},
+     {0, 0, -12, 76, 76, -12, 0, 0}, {0, 0, -10, 66, 84, -12, 0, 0},
+     {0, 0, -10, 58, 94, -14, 0, 0}, {0, 0, -10, 48, 102, -12, 0, 0},
+     {0, 0, -8, 38, 110, -12, 0, 0}, {0, 0, -6, 28, 116, -10, 0, 0},
+     {0, 0, -4, 18, 122, -8, 0, 0}, {0, 0, -2, 8, 126, -4, 0, 0}}};
+
+// FWD_SHIFT_32X32 / FWD_SHIFT_64X64 (forward.rs:22-40) by shift_idx, and
+// InvBlock::INTERMEDIATE_SHIFT (inverse.rs:1643-1666) = 2 for both.
+template <int N>
+__device__ __forceinline__ void fwd_shifts(int idx, int &s0, int &s1, int &s2) {
+  constexpr int8_t k32[3][3] = {{4, -2, 0}, {2, 0, 0}, {0, 0, 2}};
+  constexpr int8_t k64[3][3] = {{4, -1, -2}, {2, 0, -1}, {0, 0, 1}};
+  const int8_t *k = N == 64 ? k64[idx] : k32[idx];
+  s0 = k[0];
+  s1 = k[1];
+  s2 = k[2];
+}
+
+// round_shift_array (src/transform/mod.rs:499-521)
+__device__ __forceinline__ int32_t rdo_rsa(int32_t v, int bit) {
+  if (bit > 0) return round_shift(v, bit);
+  if (bit < 0) return (int32_t)((uint32_t)v << -bit);
+  return v;
+}
+
+template <typename Px, int N, bool MOMENTS>
+__global__ __launch_bounds__(64) void rdo_cand_kernel(RdoArgs a) {
+  constexpr int B = (int)sizeof(Px);
+  constexpr int S = N + 1;                       // padded LDS row (i32)
+  constexpr int G = 64 / N, RG = N / G;          // MC lane groups
+  constexpr int P = B == 1 ? ((N + 8 + 15) / 16) * 16 : ((2 * (N + 8) + 15) / 16) * 16;
+  constexpr int C32 = N < 32 ? N : 32;           // coded coefficient extent
+  static_assert((N + 7) * P <= N * S * 4, "window must fit the coefficient slab");
+  __shared__ int32_t buf[N * S];
+  __shared__ Px pred[N * N];
+
+  const int t = blockIdx.x;
+  if (t >= a.n_tx) return;
+  const RdoPlane &pl = a.p[blockIdx.y];
+  const int lane = threadIdx.x;
+  const int cand = t / a.ntx_per_cand;
+  const rv_mc_job mj = pl.mc[cand];
+  const rv_tx_job tj = pl.tx[t];
+  const rv_plane &ref = pl.ref[cand / a.cands_per_ref];
+  const int ox = tj.pred_x - mj.dst_x, oy = tj.pred_y - mj.dst_y;  // in the MC block
+  const int bd = a.bd, ib = bd == 12 ? 2 : 4, maxv = (1 << bd) - 1;
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+
+  // ---- A. put_8tap into LDS ------------------------------------------------
+  {
+    uint32_t *win = reinterpret_cast<uint32_t *>(buf);
+    const uint8_t *sp = (const uint8_t *)plane_ptr<Px>(ref, mj.src_x + ox - 3, mj.src_y + oy - 3);
+    const int64_t rs = (int64_t)ref.stride * B;
+    constexpr int kRowDw = ((N + 7) * B + 3) / 4;
+    constexpr int kTot = (N + 7) * kRowDw;
+#pragma unroll 4
+    for (int i = lane; i < kTot; i += 64) {
+      const int r = i / kRowDw, d = i - r * kRowDw;
+      uint32_t v;
+      __builtin_memcpy(&v, sp + r * rs + 4 * d, 4);
+      win[r * (P / 4) + d] = v;
+    }
+    wave_sync();
+    const int cf = mj.col_frac, rf = mj.row_frac;
+    const int8_t *xf = kRdoReg[a.mb_w <= 4][cf];
+    const int8_t *yf = kRdoReg[a.mb_h <= 4][rf];
+    int yt[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) yt[k] = yf[k];
+    uint32_t xp[4];
+    int xsum = 0;
+    if constexpr (B == 1) {
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+        xp[h] = (uint32_t)(uint8_t)xf[4 * h] | ((uint32_t)(uint8_t)xf[4 * h + 1] << 8) |
+                ((uint32_t)(uint8_t)xf[4 * h + 2] << 16) | ((uint32_t)(uint8_t)xf[4 * h + 3] << 24);
+#pragma unroll
+      for (int k = 0; k < 8; k++) xsum += xf[k];
+      xp[2] = xp[3] = 0;
+    } else {
+#pragma unroll
+      for (int h = 0; h < 4; h++)
+        xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h] |
+                ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] << 16);
+    }
+    const int col = lane % N, grp = lane / N;
+    auto hval = [&](int tr) -> int32_t {
+      const uint32_t *row = win + (grp * RG + tr) * (P / 4);
+      if constexpr (B == 1) {
+        const int d0 = col >> 2, sh = col & 3;
+        const uint32_t w0 = row[d0], w1 = row[d0 + 1], w2 = row[d0 + 2];
+        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        if (!cf) return (int32_t)(lo >> 24);
+        int32_t s = __builtin_amdgcn_sdot4((int)(lo ^ 0x80808080u), (int)xp[0], 128 * xsum, false);
+        s = __builtin_amdgcn_sdot4((int)(hi ^ 0x80808080u), (int)xp[1], s, false);
+        return (int32_t)(int16_t)round_shift(s, 7 - ib);
+      } else {
+        typedef short s2 __attribute__((ext_vector_type(2)));
+        const int d0 = col >> 1, sh = (col & 1) * 2;
+        uint32_t w[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) w[k] = row[d0 + k];
+        uint32_t pp[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) pp[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+        if (!cf) return (int32_t)(pp[1] >> 16);
+        int32_t s = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          s = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, pp[k]), __builtin_bit_cast(s2, xp[k]), s,
+                                     false);
+        return (int32_t)(int16_t)round_shift(s, 7 - ib);
+      }
+    };
+    const int vshift = cf ? 7 + ib : 7;
+    int32_t ring[8];
+#pragma unroll
+    for (int k = 0; k < 7; k++) ring[k] = hval(k);
+    ring[7] = 0;
+#pragma clang loop unroll(full)
+    for (int r = 0; r < RG; r++) {
+      ring[(r + 7) & 7] = hval(r + 7);
+      int32_t v;
+      if (rf) {
+        int32_t s = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(r + k) & 7]);
+        v = round_shift(s, vshift);
+      } else {
+        v = cf ? round_shift(ring[(r + 3) & 7], ib) : ring[(r + 3) & 7];
+      }
+      pred[(grp * RG + r) * N + col] = (Px)clampi(v, 0, maxv);
+    }
+    wave_sync();  // window reads done (buf is reused), prediction visible
+  }
+
+  int s0, s1, s2;
+  fwd_shifts<N>((bd - 8) / 2, s0, s1, s2);
+  // ---- B. residual = org - pred, << -shift[0] ------------------------------
+  {
+    constexpr int PPD = 4 / B;                 // pixels per dword
+    constexpr int DPR = N / PPD;               // dwords per row
+    const uint8_t *op = (const uint8_t *)plane_ptr<Px>(pl.org, tj.src_x, tj.src_y);
+    const int64_t os = (int64_t)pl.org.stride * B;
+#pragma unroll 8
+    for (int i = lane; i < N * DPR; i += 64) {
+      const int r = i / DPR, c = (i - r * DPR) * PPD;
+      uint32_t ov, pv;
+      __builtin_memcpy(&ov, op + r * os + c * B, 4);
+      __builtin_memcpy(&pv, pred + r * N + c, 4);
+#pragma unroll
+      for (int k = 0; k < PPD; k++) {
+        const int sh = 8 * B * k, m = B == 1 ? 0xff : 0xffff;
+        const int16_t d = (int16_t)((int16_t)((ov >> sh) & m) - (int16_t)((pv >> sh) & m));
+        buf[r * S + c + k] = rdo_rsa((int32_t)d, -s0);
+      }
+    }
+    wave_sync();
+  }
+  // ---- C. forward DCT_DCT: column pass, then the coded rows ---------------
+  if (lane < N) {
+    int32_t v[N];
+#pragma unroll
+    for (int r = 0; r < N; r++) v[r] = buf[r * S + lane];
+    tx::fwd1d<1, N>(v, v);
+#pragma unroll
+    for (int r = 0; r < N; r++) buf[r * S + lane] = rdo_rsa(v[r], -s1);
+  }
+  wave_sync();
+  if (lane < C32) {
+    int32_t v[N];
+#pragma unroll
+    for (int c = 0; c < N; c++) v[c] = buf[lane * S + c];
+    tx::fwd1d<1, N>(v, v);
+#pragma unroll
+    for (int c = 0; c < C32; c++) buf[lane * S + c] = (rdo_rsa(v[c], -s2) / kQstep) * kQstep;
+  }
+  wave_sync();
+  // packed coefficients (row stride min(W,32)), coalesced
+  {
+    int32_t *pk = pl.packed + (int64_t)t * C32 * C32;
+#pragma unroll 4
+    for (int i = lane; i < C32 * C32; i += 64) pk[i] = buf[(i / C32) * S + (i % C32)];
+  }
+  // ---- D. inverse: rows of the coded coefficients, then columns + add ------
+  const int range = bd + 8;
+  if (lane < C32) {
+    int32_t v[N];
+#pragma unroll
+    for (int c = 0; c < N; c++) v[c] = c < C32 ? tx::clampv(buf[lane * S + c], range) : 0;
+    tx::inv1d<1, N>(v, range);
+#pragma unroll
+    for (int c = 0; c < N; c++) buf[lane * S + c] = v[c];
+  }
+  wave_sync();
+  if (lane < N) {
+    const int crange = bd + 6 > 16 ? bd + 6 : 16;
+    int32_t v[N];
+#pragma unroll
+    for (int r = 0; r < N; r++)
+      v[r] = r < C32 ? tx::clampv(round_shift(buf[r * S + lane], 2), crange) : 0;
+    tx::inv1d<1, N>(v, crange);
+#pragma unroll
+    for (int r = 0; r < N; r++) {
+      Px *q = pred + r * N + lane;
+      *q = (Px)clampi(wadd((int32_t)*q, round_shift(v[r], 4)), 0, maxv);
+    }
+  }
+  wave_sync();
+  // reconstruction -> the tall plane, coalesced dwords
+  {
+    constexpr int PPD = 4 / B, DPR = N / PPD;
+    uint8_t *dp = (uint8_t *)plane_ptr_mut<Px>(pl.dst, tj.pred_x, tj.pred_y);
+    const int64_t ds = (int64_t)pl.dst.stride * B;
+#pragma unroll 8
+    for (int i = lane; i < N * DPR; i += 64) {
+      const int r = i / DPR, c = (i - r * DPR) * PPD;
+      uint32_t v;
+      __builtin_memcpy(&v, pred + r * N + c, 4);
+      __builtin_memcpy(dp + r * ds + c * B, &v, 4);
+    }
+  }
+  // ---- E. distortion partials of org vs reconstruction ---------------------
+  const Px *o = plane_ptr<Px>(pl.org, tj.src_x, tj.src_y);
+  if constexpr (MOMENTS) {
+    constexpr int NB = N / 8;  // 8x8 blocks per row of this transform block
+    const int sub_x = a.mb_w / 8, nsub = sub_x * (a.mb_h / 8);
+    for (int k = lane; k < NB * NB; k += 64) {
+      const int by = k / NB, bx = k - by * NB;
+      int32_t ss = 0, sd = 0;
+      int64_t ss2 = 0, sd2 = 0, ssd = 0;
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const int32_t s = o[(int64_t)(by * 8 + j) * pl.org.stride + bx * 8 + i];
+          const int32_t d = pred[(by * 8 + j) * N + bx * 8 + i];
+          ss += s;
+          sd += d;
+          ss2 += (int64_t)wmul(s, s);
+          sd2 += (int64_t)wmul(d, d);
+          ssd += (int64_t)wmul(s, d);
+        }
+      const int kk = ((oy >> 3) + by) * sub_x + (ox >> 3) + bx;
+      int64_t *m = (int64_t *)pl.dist + ((int64_t)cand * nsub + kk) * 5;
+      m[0] = ss;
+      m[1] = sd;
+      m[2] = ss2;
+      m[3] = sd2;
+      m[4] = ssd;
+    }
+  } else {
+    const int bw = a.sub_w, bh = a.sub_h;
+    const int nbx = N / bw, nby = N / bh;
+    const int sub_x = a.mb_w / bw, nsub = sub_x * (a.mb_h / bh);
+    for (int k = lane; k < nbx * nby; k += 64) {
+      const int by = k / nbx, bx = k - by * nbx;
+      uint64_t value = 0;
+      for (int j = 0; j < bh; j++) {
+        uint32_t row = 0;
+        for (int i = 0; i < bw; i++) {
+          const int32_t c = (int32_t)(int16_t)o[(int64_t)(by * bh + j) * pl.org.stride + bx * bw + i] -
+                            (int32_t)(int16_t)pred[(by * bh + j) * N + bx * bw + i];
+          row += (uint32_t)wmul(c, c);
+        }
+        value += row;
+      }
+      const int kk = (oy / bh + by) * sub_x + ox / bw + bx;
+      ((uint64_t *)pl.dist)[(int64_t)cand * nsub + kk] = value;
+    }
+  }
+}
+
+}  // namespace rv
+
+using namespace rv;
+
+// Replay-internal entry (rv_replay.hip).  Luma: one plane, N = 64, cdef
+// moments; chroma: planes U and V in one launch (blockIdx.y), N = 32, SSE.
+int rv_rdo_candidates(const RdoArgs &a, int nplanes, int n, int moments, int hbd,
+                      hipStream_t s) {
+  if (a.n_tx == 0) return RV_OK;
+  dim3 grid((unsigned)a.n_tx, (unsigned)nplanes);
+#define RV_RDO(PX, NN, MOM) rdo_cand_kernel<PX, NN, MOM><<<grid, 64, 0, s>>>(a)
+  if (n == 64 && moments && !hbd) RV_RDO(uint8_t, 64, true);
+  else if (n == 64 && moments && hbd) RV_RDO(uint16_t, 64, true);
+  else if (n == 32 && !moments && !hbd) RV_RDO(uint8_t, 32, false);
+  else if (n == 32 && !moments && hbd) RV_RDO(uint16_t, 32, false);
+  else return rv_set_error(RV_ENOTSUP, "rv_rdo_candidates: unsupported shape");
+#undef RV_RDO
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "rv_device.h"
+#include "rv_rdo.h"
 
 // rv_me_diamond.hip: every reference in one launch + per-job evaluation
 // counts
@@ -39,7 +40,6 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
 namespace rv {
 
 constexpr int kSb = 64;
-constexpr int kQstep = 8;  // quantize/dequantize stand-in
 
 struct Geo {
   int W, H, xdec, ydec, bd, hbd;
@@ -178,22 +178,6 @@ __global__ void make_mc_jobs(Geo g, const rv_fs_result *sub, rv_plane luma,
                         (c * g.th + sy) * g.ch);
 }
 
-// quantize/dequantize stand-in + coefficient compaction: the top-left
-// min(W,32) x min(H,32) of each W-stride raster, each value replaced by
-// (v / kQstep) * kQstep (truncating), packed with row stride min(W,32).
-__global__ void pack_coeffs(const int32_t *raster, int n, int tw, int th,
-                            int32_t *packed) {
-  const int cw = tw < 32 ? tw : 32, ch = th < 32 ? th : 32;
-  const int64_t total = (int64_t)n * cw * ch;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int64_t b = i / (cw * ch);
-  const int e = (int)(i - b * cw * ch);
-  const int r = e / cw, c = e - r * cw;
-  const int32_t v = raster[b * tw * th + r * tw + c];
-  packed[i] = (v / kQstep) * kQstep;
-}
-
 // Block-level reduction helper: one atomic per workgroup (never one per
 // wavefront: same-address atomics serialise, MI355X_MICROARCH.md).
 __device__ inline void block_atomic_add(uint64_t s, unsigned long long *out) {
@@ -320,7 +304,7 @@ struct rv_replay {
   rv_mc_job *l_mc, *c_mc;
   rv_tx_job *l_tx, *c_tx;
   rv_dist_job *l_dist, *c_dist, *imp_jobs;
-  int32_t *l_raster, *c_raster, *l_packed, *c_packed;
+  int32_t *l_packed, *c_packed;
   int64_t *l_mom;
   uint64_t *u_sse, *v_sse, *words;
   uint32_t *imp_satd;
@@ -548,8 +532,6 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->ds_jobs = (rv_ds_job *)dalloc(r, nr * sizeof(rv_ds_job));
   r->l_mc = (rv_mc_job *)dalloc(r, g.nctx * sizeof(rv_mc_job));
   r->c_mc = (rv_mc_job *)dalloc(r, g.nctx * sizeof(rv_mc_job));
-  r->l_raster = (int32_t *)dalloc(r, (size_t)g.nctx * 4096 * 4);
-  r->c_raster = (int32_t *)dalloc(r, (size_t)g.nctx * ntx_c * 1024 * 4 * 2);
   r->l_packed = (int32_t *)dalloc(r, (size_t)g.nctx * 1024 * 4);
   r->c_packed = (int32_t *)dalloc(r, (size_t)g.nctx * ntx_c * 1024 * 4 * 2);
   r->lsub = (kSb / 8) * (kSb / 8);
@@ -612,9 +594,8 @@ int rv_replay_set_frame(rv_replay *r, int slot, const void *host_yuv) {
 
 // Event layout per frame (ring slot): 0..6 stage bounds F0..F5; then
 // kernel brackets [7,8] F3 full-pel diamond, [9,10] F3 sub-pel diamond,
-// [11,12] luma put_8tap, [13,14] luma diff + fwd TX_64X64, [15,16] luma
-// inverse TX_64X64 + add, [17,18] luma cdef moments.  F1 ([1,2]) holds only
-// the full-search launches.
+// [11,12] F4 fused luma candidates, [13,14] F4 fused chroma candidates.
+// F1 ([1,2]) holds only the full-search launches.
 int rv_replay_frame(rv_replay *r, int me_range_scale) {
   if (!r || (me_range_scale != 1 && me_range_scale != 2 && me_range_scale != 4))
     return rv_set_error(RV_EINVAL, "rv_replay_frame: bad me_range_scale");
@@ -666,44 +647,52 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
                                r->sub, ev_sub, st));
   RV_H(hipEventRecord(r->ev[10], st));
   RV_H(hipEventRecord(r->ev[4], st));
-  // F4 RDO candidates
+  // F4 RDO candidates: one fused launch for luma, one for both chroma planes
   make_mc_jobs<<<blocks(g.nctx), T, 0, st>>>(g, r->sub, cur.y, cur.u, r->l_mc, r->c_mc);
-  RV_H(hipEventRecord(r->ev[11], st));
-  for (int k = 0; k < g.R; k++) {  // luma put_8tap
-    const int o = k * 2 * nr;        // both candidates of reference k
-    RV_R(rv_put_8tap_batch(&r->tall_y, &r->slots[1 + k].y, r->l_mc + o, 2 * nr, kSb, kSb, 0, 0,
-                           g.bd, st));
-  }
-  RV_H(hipEventRecord(r->ev[12], st));
-  for (int k = 0; k < g.R; k++) {
-    const RvFrameSlot &ref = r->slots[1 + k];
-    const int o = k * 2 * nr;
-    RV_R(rv_put_8tap_batch(&r->tall_u, &ref.u, r->c_mc + o, 2 * nr, g.cw, g.ch, 0, 0, g.bd, st));
-    RV_R(rv_put_8tap_batch(&r->tall_v, &ref.v, r->c_mc + o, 2 * nr, g.cw, g.ch, 0, 0, g.bd, st));
-  }
   const int ntx_c = (g.cw / 32) * (g.ch / 32);
   const int nct = g.nctx * ntx_c;
-  int32_t *u_raster = r->c_raster, *v_raster = r->c_raster + (size_t)nct * 1024;
-  int32_t *u_packed = r->c_packed, *v_packed = r->c_packed + (size_t)nct * 1024;
-  RV_H(hipEventRecord(r->ev[13], st));
-  RV_R(rv_diff_fwd_txfm_batch(&cur.y, &r->tall_y, r->l_tx, g.nctx, 4, 0, g.bd, r->l_raster, st));
-  RV_H(hipEventRecord(r->ev[14], st));
-  RV_R(rv_diff_fwd_txfm_batch(&cur.u, &r->tall_u, r->c_tx, nct, 3, 0, g.bd, u_raster, st));
-  RV_R(rv_diff_fwd_txfm_batch(&cur.v, &r->tall_v, r->c_tx, nct, 3, 0, g.bd, v_raster, st));
-  pack_coeffs<<<blocks((int64_t)g.nctx * 1024), T, 0, st>>>(r->l_raster, g.nctx, 64, 64,
-                                                             r->l_packed);
-  pack_coeffs<<<blocks((int64_t)nct * 1024), T, 0, st>>>(u_raster, nct, 32, 32, u_packed);
-  pack_coeffs<<<blocks((int64_t)nct * 1024), T, 0, st>>>(v_raster, nct, 32, 32, v_packed);
-  RV_H(hipEventRecord(r->ev[15], st));
-  RV_R(rv_inv_txfm_add_batch(r->l_packed, &r->tall_y, r->l_tx, g.nctx, 4, 0, g.bd, st));
-  RV_H(hipEventRecord(r->ev[16], st));
-  RV_R(rv_inv_txfm_add_batch(u_packed, &r->tall_u, r->c_tx, nct, 3, 0, g.bd, st));
-  RV_R(rv_inv_txfm_add_batch(v_packed, &r->tall_v, r->c_tx, nct, 3, 0, g.bd, st));
-  RV_H(hipEventRecord(r->ev[17], st));
-  RV_R(rv_cdef_moments_batch(&cur.y, &r->tall_y, r->l_dist, g.nctx, kSb, kSb, r->l_mom, st));
-  RV_H(hipEventRecord(r->ev[18], st));
-  RV_R(rv_sse_batch(&cur.u, &r->tall_u, r->c_dist, g.nctx, g.cw, g.ch, r->u_sse, st));
-  RV_R(rv_sse_batch(&cur.v, &r->tall_v, r->c_dist, g.nctx, g.cw, g.ch, r->v_sse, st));
+  {
+    RdoArgs la;
+    memset(&la, 0, sizeof(la));
+    la.p[0].org = cur.y;
+    for (int k = 0; k < g.R; k++) la.p[0].ref[k] = r->slots[1 + k].y;
+    la.p[0].dst = r->tall_y;
+    la.p[0].mc = r->l_mc;
+    la.p[0].tx = r->l_tx;
+    la.p[0].packed = r->l_packed;
+    la.p[0].dist = r->l_mom;
+    la.n_tx = g.nctx;
+    la.ntx_per_cand = 1;
+    la.cands_per_ref = 2 * nr;
+    la.bd = g.bd;
+    la.mb_w = la.mb_h = kSb;
+    la.sub_w = la.sub_h = 8;
+    RV_H(hipEventRecord(r->ev[11], st));
+    RV_R(rv_rdo_candidates(la, 1, 64, 1, g.hbd, st));
+    RV_H(hipEventRecord(r->ev[12], st));
+    RdoArgs ca = la;
+    const rv_plane *cp[2] = {&cur.u, &cur.v};
+    const rv_plane *tp[2] = {&r->tall_u, &r->tall_v};
+    uint64_t *cs[2] = {r->u_sse, r->v_sse};
+    for (int p = 0; p < 2; p++) {
+      ca.p[p].org = *cp[p];
+      for (int k = 0; k < g.R; k++) ca.p[p].ref[k] = p ? r->slots[1 + k].v : r->slots[1 + k].u;
+      ca.p[p].dst = *tp[p];
+      ca.p[p].mc = r->c_mc;
+      ca.p[p].tx = r->c_tx;
+      ca.p[p].packed = r->c_packed + (size_t)p * nct * 1024;
+      ca.p[p].dist = cs[p];
+    }
+    ca.n_tx = nct;
+    ca.ntx_per_cand = ntx_c;
+    ca.mb_w = g.cw;
+    ca.mb_h = g.ch;
+    ca.sub_w = (g.cw < 8 ? g.cw : 8) >> g.xdec;
+    ca.sub_h = (g.ch < 8 ? g.ch : 8) >> g.ydec;
+    RV_H(hipEventRecord(r->ev[13], st));
+    RV_R(rv_rdo_candidates(ca, 2, 32, 0, g.hbd, st));
+    RV_H(hipEventRecord(r->ev[14], st));
+  }
   score_candidates<<<g.nsb, 64, 0, st>>>(g, r->l_mom, r->u_sse, r->v_sse, r->lsub, r->csub,
                                          r->coarse, r->half, r->full, r->sub, r->words);
   RV_H(hipEventRecord(r->ev[5], st));
@@ -750,7 +739,7 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
   if (last < 1) last = 1;
   if (last > rv_replay::kRing) last = rv_replay::kRing;
   if (last > r->frames) last = (int)r->frames;
-  for (int i = 0; i < cap && i < 12; i++) ms_out[i] = 0.f;
+  for (int i = 0; i < cap && i < 10; i++) ms_out[i] = 0.f;
   int n = 0;
   for (int f = 0; f < last; f++) {
     hipEvent_t *e = r->evs[(r->frames - 1 - f) % rv_replay::kRing];
@@ -761,7 +750,7 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
       RV_H(hipEventElapsedTime(&ms, e[i], e[i + 1]));
       ms_out[n++] += ms;
     }
-    for (int i = 7; i < 19 && n < cap; i += 2) {  // kernel brackets
+    for (int i = 7; i < 15 && n < cap; i += 2) {  // kernel brackets
       float ms = 0.f;
       RV_H(hipEventElapsedTime(&ms, e[i], e[i + 1]));
       ms_out[n++] += ms;
