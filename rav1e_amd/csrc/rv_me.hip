@@ -14,6 +14,8 @@
 // v_sad_u8 on packed dwords (v_alignbyte for the 3 unaligned shifts), so a
 // reference row is read from LDS once per 32 candidates.  The search is
 // VALU-bound (~256 |a-b| per candidate), not HBM-bound.
+#include <string.h>
+
 #include "rv_device.h"
 
 namespace rv {
@@ -136,35 +138,43 @@ __global__ __launch_bounds__(kFsThreads) void fs_generic_kernel(
 }
 
 // ---- fast path: u8, 16x16, step 1 ---------------------------------------
-constexpr int kTileRows = 8;          // candidate rows per lane
-constexpr int kLdsWords = 14 * 1024;  // 56 KiB search band
+constexpr int kTileRows = 8;         // candidate rows per lane
+constexpr int kLdsWords = 7 * 1024;  // 28 KiB search band: 5 workgroups per CU
 
-__global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(
-    rv_plane org, rv_plane ref, const rv_fs_job *__restrict__ jobs, int n,
-    int hp, rv_fs_result *__restrict__ out) {
+struct FsArgs {
+  rv_plane org;
+  rv_plane ref[RV_DS_MAX_PRED];  // job i searches ref[i / n_per_ref]
+  const rv_fs_job *jobs;
+  rv_fs_result *out;
+  int n, n_per_ref, hp;
+};
+
+__global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(FsArgs a) {
   __shared__ uint32_t band[kLdsWords];
-  const int job = blockIdx.x;
-  if (job >= n) return;
-  const rv_fs_job jb = jobs[job];
+  // consecutive jobs on one XCD (blocks are dealt round-robin to the 8 XCDs;
+  // neighbouring superblocks share reference rows in that XCD's L2)
+  const int per = (int)gridDim.x >> 3;
+  const int job = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+  if (job >= a.n) return;
+  const rv_fs_job jb = a.jobs[job];
+  const rv_plane &ref = a.ref[job / a.n_per_ref];
   const int nx = jb.x_hi >= jb.x_lo ? jb.x_hi - jb.x_lo + 1 : 0;
   const int ny = jb.y_hi >= jb.y_lo ? jb.y_hi - jb.y_lo + 1 : 0;
   const int tid = threadIdx.x;
 
-  // 16x16 source block -> 64 packed dwords in VGPRs (same in every lane)
-  uint32_t ow[16][4];
-  {
-    const uint8_t *o = plane_ptr<uint8_t>(org, jb.po_x, jb.po_y);
-#pragma unroll
-    for (int r = 0; r < 16; r++)
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-        ow[r][i] = load_u32_unaligned(o + (int64_t)r * org.stride + 4 * i);
+  // 16x16 source block -> LDS (64 dwords); every lane reads the same row,
+  // so the reads are broadcasts and the VGPRs stay with the accumulators
+  __shared__ uint4 orgs[16];
+  if (tid < 64) {
+    const uint8_t *o = plane_ptr<uint8_t>(a.org, jb.po_x, jb.po_y);
+    reinterpret_cast<uint32_t *>(orgs)[tid] =
+        load_u32_unaligned(o + (int64_t)(tid >> 2) * a.org.stride + 4 * (tid & 3));
   }
 
   const int tx_n = (nx + 3) >> 2;       // 4-wide candidate columns
   const int rw = tx_n + 4;              // band row length in dwords
   if (rw * (2 * kTileRows + 15) > kLdsWords) {  // window too wide for a band
-    fs_generic_body<uint8_t>(org, ref, jb, 16, 16, 1, hp, out + job);
+    fs_generic_body<uint8_t>(a.org, ref, jb, 16, 16, 1, a.hp, a.out + job);
     return;
   }
   const int vis_w = nx + 15;            // bytes of a ref row that exist
@@ -178,22 +188,32 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(
     const int lrows = rows + 15;  // ref rows with data
     const int ty_n = (rows + kTileRows - 1) / kTileRows;
     const int brows = ty_n * kTileRows + 15;  // rows the tiles touch
+    const int total = brows * rw;
     __syncthreads();
-    for (int i = tid; i < brows * rw; i += blockDim.x) {
-      const int r = i / rw, wd = i - r * rw;
-      const int c = 4 * wd;
-      uint32_t v = 0;
-      if (r < lrows) {
-        const uint8_t *p = rbase + (int64_t)(y0 + r) * ref.stride + c;
-        if (c + 3 < vis_w) {
-          v = load_u32_unaligned(p);
-        } else {
+    // band fill: 8 independent loads in flight per thread before the LDS
+    // stores, so the fill costs ~one memory round trip, not eight
+    for (int i0 = tid; i0 < total; i0 += 8 * kFsThreads) {
+      uint32_t v[8];
 #pragma unroll
-          for (int k = 0; k < 4; k++)
-            if (c + k < vis_w) v |= (uint32_t)p[k] << (8 * k);
+      for (int u = 0; u < 8; u++) {
+        const int i = i0 + u * kFsThreads;
+        const int r = i / rw, c = 4 * (i - r * rw);
+        uint32_t x = 0;
+        if (i < total && r < lrows) {
+          const uint8_t *p = rbase + (int64_t)(y0 + r) * ref.stride + c;
+          if (c + 3 < vis_w) {
+            x = load_u32_unaligned(p);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+              if (c + k < vis_w) x |= (uint32_t)p[k] << (8 * k);
+          }
         }
+        v[u] = x;
       }
-      band[i] = v;
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (i0 + u * kFsThreads < total) band[i0 + u * kFsThreads] = v[u];
     }
     __syncthreads();
     const int tasks = tx_n * ty_n;
@@ -206,7 +226,7 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(
 #pragma unroll
         for (int j = 0; j < 4; j++) acc[c][j] = 0;
       const uint32_t *bp = band + cy0 * rw + tcx;
-#pragma unroll
+#pragma unroll 1
       for (int yy = 0; yy < kTileRows + 15; yy++) {
         uint32_t wv[5];
 #pragma unroll
@@ -221,13 +241,14 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(
         }
 #pragma unroll
         for (int c = 0; c < kTileRows; c++) {
-          const int r = yy - c;
+          const int r = yy - c;  // source row against candidate row c
           if (r >= 0 && r < 16) {
+            const uint4 o4 = orgs[r];
+            const uint32_t ov[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
             for (int j = 0; j < 4; j++)
 #pragma unroll
-              for (int i = 0; i < 4; i++)
-                acc[c][j] = sad_u8x4(ow[r][i], sh[j][i], acc[c][j]);
+              for (int i = 0; i < 4; i++) acc[c][j] = sad_u8x4(ov[i], sh[j][i], acc[c][j]);
           }
         }
       }
@@ -239,7 +260,7 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(
           const int ix = 4 * tcx + j;
           if (ix < nx && cy0 + c < rows) {
             const uint64_t cost =
-                cand_cost(acc[c][j], jb.x_lo + ix, jb.y_lo + iy, jb, hp);
+                cand_cost(acc[c][j], jb.x_lo + ix, jb.y_lo + iy, jb, a.hp);
             const uint32_t idx = (uint32_t)(iy * nx + ix);
             if (better(cost, idx, b)) b = Best{cost, idx};
           }
@@ -248,31 +269,60 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(
     }
   }
   b = block_best(b);
-  if (tid == 0) write_result(jb, b, nx > 0 ? nx : 1, 1, out + job);
+  if (tid == 0) write_result(jb, b, nx > 0 ? nx : 1, 1, a.out + job);
 }
 
 }  // namespace rv
 
 using namespace rv;
 
+// Multi-reference form used by the replay driver: jobs [n_refs][n_per_ref],
+// job i searches refs[i / n_per_ref], all in one launch.
+int rv_full_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
+                         const rv_fs_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
+                         int step, int allow_hp, rv_fs_result *d_out, void *stream) {
+  if (!org || !refs || n_refs < 1 || n_refs > RV_DS_MAX_PRED || n_per_ref < 0 || blk_w < 4 ||
+      blk_h < 4 || blk_w > 128 || blk_h > 128 || (blk_w & 3) || step < 1)
+    return rv_set_error(RV_EINVAL, "rv_full_search_batch: bad arguments");
+  for (int k = 0; k < n_refs; k++)
+    if (refs[k].hbd != org->hbd)
+      return rv_set_error(RV_EINVAL, "rv_full_search_batch: pixel type mismatch");
+  const int n = n_refs * n_per_ref;
+  if (n == 0) return RV_OK;
+  hipStream_t s = rv_resolve_stream(stream);
+  if (!org->hbd && blk_w == 16 && blk_h == 16 && step == 1) {
+    FsArgs a;
+    memset(&a, 0, sizeof(a));
+    a.org = *org;
+    for (int k = 0; k < n_refs; k++) a.ref[k] = refs[k];
+    a.jobs = d_jobs;
+    a.out = d_out;
+    a.n = n;
+    a.n_per_ref = n_per_ref;
+    a.hp = allow_hp ? 1 : 0;
+    fs16_u8_kernel<<<(unsigned)((n + 7) / 8 * 8), kFsThreads, 0, s>>>(a);
+  } else {
+    for (int k = 0; k < n_refs; k++) {
+      const rv_fs_job *j = d_jobs + (size_t)k * n_per_ref;
+      rv_fs_result *o = d_out + (size_t)k * n_per_ref;
+      if (n_per_ref == 0) continue;
+      if (org->hbd)
+        fs_generic_kernel<uint16_t><<<n_per_ref, kFsThreads, 0, s>>>(
+            *org, refs[k], j, n_per_ref, blk_w, blk_h, step, allow_hp ? 1 : 0, o);
+      else
+        fs_generic_kernel<uint8_t><<<n_per_ref, kFsThreads, 0, s>>>(
+            *org, refs[k], j, n_per_ref, blk_w, blk_h, step, allow_hp ? 1 : 0, o);
+    }
+  }
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
 extern "C" int rv_full_search_batch(const rv_plane *org, const rv_plane *ref,
                                     const rv_fs_job *d_jobs, int n, int blk_w,
                                     int blk_h, int step, int allow_hp,
                                     rv_fs_result *d_out, void *stream) {
-  if (!org || !ref || n < 0 || blk_w < 4 || blk_h < 4 || blk_w > 128 ||
-      blk_h > 128 || (blk_w & 3) || step < 1 || org->hbd != ref->hbd)
-    return rv_set_error(RV_EINVAL, "rv_full_search_batch: bad arguments");
-  if (n == 0) return RV_OK;
-  hipStream_t s = rv_resolve_stream(stream);
-  if (!org->hbd && blk_w == 16 && blk_h == 16 && step == 1)
-    fs16_u8_kernel<<<n, kFsThreads, 0, s>>>(*org, *ref, d_jobs, n,
-                                            allow_hp ? 1 : 0, d_out);
-  else if (org->hbd)
-    fs_generic_kernel<uint16_t><<<n, kFsThreads, 0, s>>>(
-        *org, *ref, d_jobs, n, blk_w, blk_h, step, allow_hp ? 1 : 0, d_out);
-  else
-    fs_generic_kernel<uint8_t><<<n, kFsThreads, 0, s>>>(
-        *org, *ref, d_jobs, n, blk_w, blk_h, step, allow_hp ? 1 : 0, d_out);
-  RV_HIP_CHECK_LAUNCH();
-  return RV_OK;
+  if (!ref) return rv_set_error(RV_EINVAL, "rv_full_search_batch: null ref");
+  return rv_full_search_multi(org, ref, 1, d_jobs, n, blk_w, blk_h, step, allow_hp, d_out,
+                              stream);
 }

@@ -152,7 +152,7 @@ template <typename Px, int W, int H, bool SUB>
 struct DsFast {
   using F = FullGeo<Px, W, H>;
   using S = SubGeo<Px, W, H>;
-  static constexpr int kOrgRegs = SUB ? S::kOrgDwords : 4 * F::I;
+  static constexpr int kOrgRegs = SUB ? 1 : 4 * F::I;
 };
 
 template <typename Px, int W, int H, bool SUB>
@@ -160,10 +160,12 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
   using F = FullGeo<Px, W, H>;
   using S = SubGeo<Px, W, H>;
   constexpr int B = (int)sizeof(Px);
+  static_assert(!SUB || S::RG % 8 == 0, "sub-pel row groups are unrolled by 8");
   __shared__ uint64_t pcost[RV_DS_MAX_PRED];
   __shared__ uint64_t scost[2][kDsWaves];
   __shared__ uint32_t wevals[kDsWaves];
   __shared__ uint32_t win_all[SUB ? kDsWaves * S::kWinDwords : 1];
+  __shared__ Px org_lds[SUB ? W * H : 1];  // sub-pel: the source block, shared by all waves
 
   const int job = xcd_job(a.n);
   if (job >= a.n) return;  // whole workgroup, uniformly
@@ -180,15 +182,11 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
   const int col = lane % W, grp = lane / W;  // sub-pel lane mapping
   const int frow = lane / F::K, fchunk = lane % F::K;  // full-pel
   if constexpr (SUB) {
-    const Px *o = plane_ptr<Px>(a.org, jb.po_x + col, jb.po_y + grp * S::RG);
-#pragma unroll
-    for (int i = 0; i < S::kOrgDwords; i++) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int k = 0; k < 4 / B; k++)
-        v |= (uint32_t)o[(int64_t)(i * (4 / B) + k) * a.org.stride] << (8 * B * k);
-      org[i] = v;
-    }
+    org[0] = 0;
+    const Px *o = plane_ptr<Px>(a.org, jb.po_x, jb.po_y);
+    for (int i = threadIdx.x; i < W * H; i += kDsThreads)
+      org_lds[i] = o[(int64_t)(i / W) * a.org.stride + (i % W)];
+    __syncthreads();
   } else {
     const uint8_t *o = (const uint8_t *)plane_ptr<Px>(a.org, jb.po_x, jb.po_y);
     const int64_t os = (int64_t)a.org.stride * B;
@@ -305,26 +303,33 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
           return (int32_t)(int16_t)round_shift(s, 7 - ib);
         }
       };
+      // vertical pass: register ring of 8 horizontal values; the row loop is
+      // unrolled by 8 only, so the ring indices stay compile-time constants
+      // without the whole block's LDS reads being hoisted into VGPRs
       int32_t ring[8];
 #pragma unroll
       for (int t = 0; t < 7; t++) ring[t] = hval(t);
       ring[7] = 0;
-#pragma clang loop unroll(full)
-      for (int r = 0; r < S::RG; r++) {
-        ring[(r + 7) & 7] = hval(r + 7);
-        int32_t v;
-        if (rf) {
-          int32_t s = 0;
+      const Px *ocol = org_lds + grp * S::RG * W + col;
+#pragma unroll 1
+      for (int r0 = 0; r0 < S::RG; r0 += 8) {
 #pragma unroll
-          for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(r + k) & 7]);
-          v = round_shift(s, vshift);
-        } else {
-          v = cf ? round_shift(ring[(r + 3) & 7], ib) : ring[(r + 3) & 7];
+        for (int u = 0; u < 8; u++) {
+          const int r = r0 + u;
+          ring[(u + 7) & 7] = hval(r + 7);
+          int32_t v;
+          if (rf) {
+            int32_t s = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(u + k) & 7]);
+            v = round_shift(s, vshift);
+          } else {
+            v = cf ? round_shift(ring[(u + 3) & 7], ib) : ring[(u + 3) & 7];
+          }
+          v = clampi(v, 0, maxv);
+          const int d = (int)ocol[r * W] - v;
+          acc += (uint32_t)(d < 0 ? -d : d);
         }
-        v = clampi(v, 0, maxv);
-        const int o = (int)((org[r * B / 4] >> (8 * B * (r % (4 / B)))) & (B == 1 ? 0xffu : 0xffffu));
-        const int d = o - v;
-        acc += (uint32_t)(d < 0 ? -d : d);
       }
     }
     return ds_cost(wave_sum(acc), mv, jb, a.hp);

@@ -30,6 +30,10 @@
 #include "rv_device.h"
 #include "rv_rdo.h"
 
+// rv_me.hip: every reference in one launch
+int rv_full_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
+                         const rv_fs_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
+                         int step, int allow_hp, rv_fs_result *d_out, void *stream);
 // rv_me_diamond.hip: every reference in one launch + per-job evaluation
 // counts
 int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
@@ -625,10 +629,11 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   RV_R(rv_plane_downsample(&cur.hres, &cur.y, st));
   RV_R(rv_plane_downsample(&cur.qres, &cur.hres, st));
   RV_H(hipEventRecord(r->ev[1], st));
-  // F1 coarse full search per reference
-  for (int k = 0; k < g.R; k++)
-    RV_R(rv_full_search_batch(&cur.qres, &r->slots[1 + k].qres, r->fs_jobs[si] + k * nr, nr, 16,
-                              16, 1, 0, r->coarse + k * nr, st));
+  // F1 coarse full search, every reference in one launch
+  rv_plane refs_q[RV_DS_MAX_PRED];
+  for (int k = 0; k < g.R; k++) refs_q[k] = r->slots[1 + k].qres;
+  RV_R(rv_full_search_multi(&cur.qres, refs_q, g.R, r->fs_jobs[si], nr, 16, 16, 1, 0, r->coarse,
+                            st));
   RV_H(hipEventRecord(r->ev[2], st));  // = the full-search kernel bracket
   // F2 half-res diamond, every reference in one launch
   make_ss2_jobs<<<blocks(nr * g.R), T, 0, st>>>(g, r->coarse, lambda2, r->ds_jobs);
