@@ -146,13 +146,12 @@ def main():
         "diamond_subpel_64": dict(ms=float(ms[7]), launches=1,
                                   bytes=nj * (64 * 64 * px + 80) +
                                   ev_sub / ev_frames * 71 * 71 * px),
-        "rdo_luma_64": dict(ms=float(ms[8]), launches=1,
-                            bytes=float(nctx * (71 * 71 * px + 64 * 64 * px + 4 * 32 * 32 +
-                                                64 * 64 * px + 64 * 40 + 16 + 24))),
-        "rdo_chroma": dict(ms=float(ms[9]), launches=1,
-                           bytes=float(2 * nctx * ((cw + 7) * (ch + 7) * px + 2 * cw * ch * px +
-                                                   4 * ntx_c * 32 * 32 + 8 * csub + 16 +
-                                                   24 * ntx_c))),
+        "rdo_candidates": dict(ms=float(ms[8]), launches=1,
+                               bytes=float(nctx * (71 * 71 * px + 64 * 64 * px + 4 * 32 * 32 +
+                                                   64 * 64 * px + 64 * 40 + 16 + 24) +
+                                           2 * nctx * ((cw + 7) * (ch + 7) * px +
+                                                       2 * cw * ch * px + 4 * ntx_c * 32 * 32 +
+                                                       8 * csub + 16 + 24 * ntx_c))),
     }
     dom = max(kernels, key=lambda n: kernels[n]["ms"])
     kd = kernels[dom]

@@ -146,6 +146,11 @@ struct SubGeo {
                                            : ((2 * (W + 8) + 15) / 16) * 16;
   static constexpr int kWinDwords = (H + 7) * P / 4;
   static constexpr int kOrgDwords = RG * (int)sizeof(Px) / 4;
+  // union window of one diamond round: D px of slack in each direction,
+  // pitch UP bytes (+3 px for the dword over-read of the horizontal pass)
+  static constexpr int D = 4;
+  static constexpr int UP = (((W + 7 + D + 4) * (int)sizeof(Px)) + 15) / 16 * 16;
+  static constexpr int kUnionDwords = (H + 7 + D) * UP / 4;
 };
 
 template <typename Px, int W, int H, bool SUB>
@@ -164,7 +169,7 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
   __shared__ uint64_t pcost[RV_DS_MAX_PRED];
   __shared__ uint64_t scost[2][kDsWaves];
   __shared__ uint32_t wevals[kDsWaves];
-  __shared__ uint32_t win_all[SUB ? kDsWaves * S::kWinDwords : 1];
+  __shared__ uint32_t win_all[SUB ? S::kUnionDwords : 1];
   __shared__ Px org_lds[SUB ? W * H : 1];  // sub-pel: the source block, shared by all waves
 
   const int job = xcd_job(a.n);
@@ -201,146 +206,228 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
       org[4 * i + 3] = v.w;
     }
   }
-  uint32_t *win = win_all + (SUB ? wave * S::kWinDwords : 0);
   uint32_t evals = 0;
 
-  // ---- one candidate, evaluated by this wavefront ----------------------
-  auto eval = [&](rv_mv mv) -> uint64_t {
+  // ---- full-pel: one candidate, evaluated by this wavefront -------------
+  auto eval_full = [&](rv_mv mv) -> uint64_t {
     if (!ds_in_range(mv, jb)) return ~0ull;
     evals++;
     uint32_t acc = 0;
-    if constexpr (!SUB) {
-      // region at po + mv / 8 (Rust `/` truncates toward zero)
-      const uint8_t *r = (const uint8_t *)plane_ptr<Px>(ref, jb.po_x + mv.col / 8,
-                                                        jb.po_y + mv.row / 8);
-      const int64_t rs = (int64_t)ref.stride * B;
+    // region at po + mv / 8 (Rust `/` truncates toward zero)
+    const uint8_t *r =
+        (const uint8_t *)plane_ptr<Px>(ref, jb.po_x + mv.col / 8, jb.po_y + mv.row / 8);
+    const int64_t rs = (int64_t)ref.stride * B;
 #pragma unroll
-      for (int i = 0; i < F::I; i++) {
-        const int rr = i * F::R + frow;
-        if (!F::kPartial || rr < H) {
-          const uint4 v = ld16(r + rr * rs + fchunk * 16);
-          acc = sad16<Px>(make_uint4(org[4 * i], org[4 * i + 1], org[4 * i + 2], org[4 * i + 3]),
-                          v, acc);
-        }
-      }
-    } else {
-      // predict_inter / get_params (src/predict.rs:267-283), luma plane
-      const int xs = 3 + ref.xdec, ys = 3 + ref.ydec;
-      const int roff = (int)mv.row >> ys, coff = (int)mv.col >> xs;
-      const int rf = ((int)mv.row - (roff << ys)) << (4 - ys);
-      const int cf = ((int)mv.col - (coff << xs)) << (4 - xs);
-      // PlaneSlice::clamp (src/frame/plane.rs:521-533) of the -3 origin
-      const int qx = clampi(jb.po_x + coff - 3, -ref.xorigin, ref.width);
-      const int qy = clampi(jb.po_y + roff - 3, -ref.yorigin, ref.height);
-      const uint8_t *sp = (const uint8_t *)plane_ptr<Px>(ref, qx, qy);
-      const int64_t rs = (int64_t)ref.stride * B;
-      // stage the window: (H + 7) rows of ceil((W + 7) * B / 4) dwords
-      constexpr int kRowDw = ((W + 7) * B + 3) / 4;
-      constexpr int kTot = (H + 7) * kRowDw;
-      __builtin_amdgcn_wave_barrier();  // previous candidate done with LDS
-#pragma unroll 4
-      for (int i = lane; i < kTot; i += 64) {
-        const int r = i / kRowDw, d = i - r * kRowDw;
-        uint32_t v;
-        __builtin_memcpy(&v, sp + r * rs + 4 * d, 4);
-        win[r * (S::P / 4) + d] = v;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // filters (wave-uniform): packed taps
-      const int8_t *xf = kReg[W <= 4][cf];
-      const int8_t *yf = kReg[H <= 4][rf];
-      int yt[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) yt[k] = yf[k];
-      uint32_t xp[4];  // u8: 2 x i8x4 (xp[0..1]); u16: 4 x i16x2
-      int xsum = 0;
-      if constexpr (B == 1) {
-#pragma unroll
-        for (int h = 0; h < 2; h++)
-          xp[h] = (uint32_t)(uint8_t)xf[4 * h] | ((uint32_t)(uint8_t)xf[4 * h + 1] << 8) |
-                  ((uint32_t)(uint8_t)xf[4 * h + 2] << 16) |
-                  ((uint32_t)(uint8_t)xf[4 * h + 3] << 24);
-#pragma unroll
-        for (int k = 0; k < 8; k++) xsum += xf[k];
-        xp[2] = xp[3] = 0;
-      } else {
-#pragma unroll
-        for (int h = 0; h < 4; h++)
-          xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h] |
-                  ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] << 16);
-      }
-      const int vshift = cf ? 7 + ib : 7;
-      // horizontal value of window row t (group-relative) for column col
-      auto hval = [&](int t) -> int32_t {
-        const uint32_t *row = win + (grp * S::RG + t) * (S::P / 4);
-        if constexpr (B == 1) {
-          const int d0 = col >> 2, sh = col & 3;
-          const uint32_t w0 = row[d0], w1 = row[d0 + 1], w2 = row[d0 + 2];
-          const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
-          const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-          if (!cf) return (int32_t)(lo >> 24);
-          int32_t s = __builtin_amdgcn_sdot4((int)(lo ^ 0x80808080u), (int)xp[0], 128 * xsum,
-                                             false);
-          s = __builtin_amdgcn_sdot4((int)(hi ^ 0x80808080u), (int)xp[1], s, false);
-          return (int32_t)(int16_t)round_shift(s, 7 - ib);
-        } else {
-          typedef short s2 __attribute__((ext_vector_type(2)));
-          const int d0 = col >> 1, sh = (col & 1) * 2;
-          uint32_t w[5];
-#pragma unroll
-          for (int k = 0; k < 5; k++) w[k] = row[d0 + k];
-          uint32_t p[4];
-#pragma unroll
-          for (int k = 0; k < 4; k++) p[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-          if (!cf) return (int32_t)(p[1] >> 16);
-          int32_t s = 0;
-#pragma unroll
-          for (int k = 0; k < 4; k++)
-            s = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, p[k]), __builtin_bit_cast(s2, xp[k]),
-                                       s, false);
-          return (int32_t)(int16_t)round_shift(s, 7 - ib);
-        }
-      };
-      // vertical pass: register ring of 8 horizontal values; the row loop is
-      // unrolled by 8 only, so the ring indices stay compile-time constants
-      // without the whole block's LDS reads being hoisted into VGPRs
-      int32_t ring[8];
-#pragma unroll
-      for (int t = 0; t < 7; t++) ring[t] = hval(t);
-      ring[7] = 0;
-      const Px *ocol = org_lds + grp * S::RG * W + col;
-#pragma unroll 1
-      for (int r0 = 0; r0 < S::RG; r0 += 8) {
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const int r = r0 + u;
-          ring[(u + 7) & 7] = hval(r + 7);
-          int32_t v;
-          if (rf) {
-            int32_t s = 0;
-#pragma unroll
-            for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(u + k) & 7]);
-            v = round_shift(s, vshift);
-          } else {
-            v = cf ? round_shift(ring[(u + 3) & 7], ib) : ring[(u + 3) & 7];
-          }
-          v = clampi(v, 0, maxv);
-          const int d = (int)ocol[r * W] - v;
-          acc += (uint32_t)(d < 0 ? -d : d);
-        }
+    for (int i = 0; i < F::I; i++) {
+      const int rr = i * F::R + frow;
+      if (!F::kPartial || rr < H) {
+        const uint4 v = ld16(r + rr * rs + fchunk * 16);
+        acc = sad16<Px>(make_uint4(org[4 * i], org[4 * i + 1], org[4 * i + 2], org[4 * i + 3]), v,
+                        acc);
       }
     }
     return ds_cost(wave_sum(acc), mv, jb, a.hp);
+  };
+
+  // ---- sub-pel: a round of up to 4 candidates (one per wavefront) ------
+  // predict_inter / get_params (src/predict.rs:267-283): integer source
+  // origin (PlaneSlice::clamp of the -3 origin, src/frame/plane.rs:521-533)
+  // and 1/16 fracs.  The candidates of a diamond step lie within 1 px of
+  // each other, so the workgroup stages ONE window covering all of them
+  // (cooperative, 256 threads) and every wavefront filters its candidate
+  // out of it at its own offset.
+  struct SubPos {
+    int qx, qy, cf, rf, ok;
+  };
+  auto sub_pos = [&](rv_mv mv) -> SubPos {
+    SubPos q;
+    q.ok = ds_in_range(mv, jb);
+    const int xs = 3 + ref.xdec, ys = 3 + ref.ydec;
+    const int roff = (int)mv.row >> ys, coff = (int)mv.col >> xs;
+    q.rf = ((int)mv.row - (roff << ys)) << (4 - ys);
+    q.cf = ((int)mv.col - (coff << xs)) << (4 - xs);
+    q.qx = clampi(jb.po_x + coff - 3, -ref.xorigin, ref.width);
+    q.qy = clampi(jb.po_y + roff - 3, -ref.yorigin, ref.height);
+    return q;
+  };
+  // stage the box at (bx, by) of rows x cols pixels into uwin (pitch UP bytes)
+  auto load_box = [&](int bx, int by, int rows, int cols) {
+    const uint8_t *sp = (const uint8_t *)plane_ptr<Px>(ref, bx, by);
+    const int64_t rs = (int64_t)ref.stride * B;
+    const int rdw = (cols * B + 3) >> 2, tot = rows * rdw;
+    for (int i0 = threadIdx.x; i0 < tot; i0 += 4 * kDsThreads) {
+      uint32_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int i = i0 + u * kDsThreads;
+        v[u] = 0;
+        if (i < tot) {
+          const int r = i / rdw, d = i - r * rdw;
+          __builtin_memcpy(&v[u], sp + r * rs + 4 * d, 4);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int i = i0 + u * kDsThreads;
+        if (i < tot) {
+          const int r = i / rdw, d = i - r * rdw;
+          win_all[r * (S::UP / 4) + d] = v[u];
+        }
+      }
+    }
+  };
+  // SAD of this wavefront's candidate from the staged window, the window
+  // pixel (dx, dy) being the candidate's (-3, -3) origin
+  auto sub_sad = [&](int cf, int rf, int dx, int dy) -> uint32_t {
+    const int8_t *xf = kReg[W <= 4][cf];
+    const int8_t *yf = kReg[H <= 4][rf];
+    int yt[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) yt[k] = yf[k];
+    uint32_t xp[4];  // u8: 2 x i8x4 (xp[0..1]); u16: 4 x i16x2
+    int xsum = 0;
+    if constexpr (B == 1) {
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+        xp[h] = (uint32_t)(uint8_t)xf[4 * h] | ((uint32_t)(uint8_t)xf[4 * h + 1] << 8) |
+                ((uint32_t)(uint8_t)xf[4 * h + 2] << 16) | ((uint32_t)(uint8_t)xf[4 * h + 3] << 24);
+#pragma unroll
+      for (int k = 0; k < 8; k++) xsum += xf[k];
+      xp[2] = xp[3] = 0;
+    } else {
+#pragma unroll
+      for (int h = 0; h < 4; h++)
+        xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h] |
+                ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] << 16);
+    }
+    const int ib2 = ib;
+    const int cx = col + dx;  // window column of this lane's output
+    // horizontal value of window row t (group-relative) for column col
+    auto hval = [&](int t) -> int32_t {
+      const uint32_t *row = win_all + (dy + grp * S::RG + t) * (S::UP / 4);
+      if constexpr (B == 1) {
+        const int d0 = cx >> 2, sh = cx & 3;
+        const uint32_t w0 = row[d0], w1 = row[d0 + 1], w2 = row[d0 + 2];
+        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        if (!cf) return (int32_t)(lo >> 24);
+        int32_t s = __builtin_amdgcn_sdot4((int)(lo ^ 0x80808080u), (int)xp[0], 128 * xsum, false);
+        s = __builtin_amdgcn_sdot4((int)(hi ^ 0x80808080u), (int)xp[1], s, false);
+        return (int32_t)(int16_t)round_shift(s, 7 - ib2);
+      } else {
+        typedef short s2 __attribute__((ext_vector_type(2)));
+        const int d0 = cx >> 1, sh = (cx & 1) * 2;
+        uint32_t w[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) w[k] = row[d0 + k];
+        uint32_t p[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) p[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+        if (!cf) return (int32_t)(p[1] >> 16);
+        int32_t s = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          s = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, p[k]), __builtin_bit_cast(s2, xp[k]), s,
+                                     false);
+        return (int32_t)(int16_t)round_shift(s, 7 - ib2);
+      }
+    };
+    const int vshift = cf ? 7 + ib : 7;
+    // vertical pass: register ring of 8 horizontal values; the row loop is
+    // unrolled by 8 only, so the ring indices stay compile-time constants
+    // without the whole block's LDS reads being hoisted into VGPRs
+    uint32_t acc = 0;
+    int32_t ring[8];
+#pragma unroll
+    for (int t = 0; t < 7; t++) ring[t] = hval(t);
+    ring[7] = 0;
+    const Px *ocol = org_lds + grp * S::RG * W + col;
+#pragma unroll 1
+    for (int r0 = 0; r0 < S::RG; r0 += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int r = r0 + u;
+        ring[(u + 7) & 7] = hval(r + 7);
+        int32_t v;
+        if (rf) {
+          int32_t s = 0;
+#pragma unroll
+          for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(u + k) & 7]);
+          v = round_shift(s, vshift);
+        } else {
+          v = cf ? round_shift(ring[(u + 3) & 7], ib) : ring[(u + 3) & 7];
+        }
+        v = clampi(v, 0, maxv);
+        const int d = (int)ocol[r * W] - v;
+        acc += (uint32_t)(d < 0 ? -d : d);
+      }
+    }
+    return wave_sum(acc);
+  };
+  // Called by every thread.  Wave w evaluates cands[w] (w < n); returns its
+  // cost (u64::MAX when out of range or w >= n).  No trailing barrier: the
+  // caller's cost exchange barrier orders the next round's window writes.
+  auto sub_round = [&](const rv_mv *cands, int n) -> uint64_t {
+    SubPos q[kDsWaves];
+    int ux = 1 << 30, uy = 1 << 30, ux2 = -(1 << 30), uy2 = -(1 << 30), any = 0;
+#pragma unroll
+    for (int k = 0; k < kDsWaves; k++) {
+      q[k] = sub_pos(cands[k < n ? k : 0]);
+      q[k].ok = q[k].ok && k < n;
+      if (q[k].ok) {
+        any = 1;
+        ux = q[k].qx < ux ? q[k].qx : ux;
+        uy = q[k].qy < uy ? q[k].qy : uy;
+        ux2 = q[k].qx > ux2 ? q[k].qx : ux2;
+        uy2 = q[k].qy > uy2 ? q[k].qy : uy2;
+      }
+    }
+    uint64_t mine = ~0ull;
+    if (!any) return mine;
+    SubPos me = q[0];
+    rv_mv me_mv = cands[0];
+#pragma unroll
+    for (int k = 1; k < kDsWaves; k++)
+      if (wave == k) {
+        me = q[k];
+        me_mv = cands[k < n ? k : 0];
+      }
+    if (ux2 - ux <= S::D && uy2 - uy <= S::D) {
+      load_box(ux, uy, (uy2 - uy) + H + 7, (ux2 - ux) + W + 7);
+      __syncthreads();
+      if (me.ok) {
+        evals++;
+        mine = ds_cost(sub_sad(me.cf, me.rf, me.qx - ux, me.qy - uy), me_mv, jb, a.hp);
+      }
+    } else {  // far-apart predictors: one window at a time
+#pragma unroll
+      for (int k = 0; k < kDsWaves; k++) {
+        if (!q[k].ok) continue;
+        __syncthreads();  // previous window consumed
+        load_box(q[k].qx, q[k].qy, H + 7, W + 7);
+        __syncthreads();
+        if (wave == k) {
+          evals++;
+          mine = ds_cost(sub_sad(q[k].cf, q[k].rf, 0, 0), cands[k], jb, a.hp);
+        }
+      }
+    }
+    return mine;
   };
 
   // ---- get_best_predictor: predictors evaluated 4 at a time ------------
   const int np = jb.n_pred < RV_DS_MAX_PRED ? jb.n_pred : RV_DS_MAX_PRED;
   for (int p0 = 0; p0 < np; p0 += kDsWaves) {
     const int p = p0 + wave;
-    if (p < np) {
-      const uint64_t c = eval(jp->pred[p]);
+    if constexpr (SUB) {
+      rv_mv c4[kDsWaves];
+#pragma unroll
+      for (int k = 0; k < kDsWaves; k++) c4[k] = jp->pred[p0 + k < np ? p0 + k : p0];
+      const uint64_t c = sub_round(c4, np - p0 < kDsWaves ? np - p0 : kDsWaves);
+      if (lane == 0 && p < np) pcost[p] = c;
+      __syncthreads();  // window consumed before the next round
+    } else if (p < np) {
+      const uint64_t c = eval_full(jp->pred[p]);
       if (lane == 0) pcost[p] = c;
     }
   }
@@ -362,8 +449,17 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
   // Every move strictly lowers center_cost, so the loop ends; the bound
   // only guarantees the grid drains whatever the inputs.
   for (int iter = 0; iter < 4096; iter++) {
-    const rv_mv cand{(int16_t)(center.row + radius * pr), (int16_t)(center.col + radius * pc)};
-    const uint64_t c = eval(cand);
+    uint64_t c;
+    if constexpr (SUB) {
+      const rv_mv c4[kDsWaves] = {
+          rv_mv{(int16_t)(center.row + radius), center.col},
+          rv_mv{center.row, (int16_t)(center.col + radius)},
+          rv_mv{(int16_t)(center.row - radius), center.col},
+          rv_mv{center.row, (int16_t)(center.col - radius)}};
+      c = sub_round(c4, kDsWaves);
+    } else {
+      c = eval_full(rv_mv{(int16_t)(center.row + radius * pr), (int16_t)(center.col + radius * pc)});
+    }
     if (lane == 0) scost[iter & 1][wave] = c;
     __syncthreads();
     uint64_t best = ~0ull;

@@ -28,7 +28,7 @@ struct RdoArgs {
 
 }  // namespace rv
 
-// n = transform size (64 luma / 32 chroma); moments: cdef moments (luma)
-// else SSE partials.
-int rv_rdo_candidates(const rv::RdoArgs &a, int nplanes, int n, int moments, int hbd,
+// Luma candidates (64x64 transform, cdef moments) and the chroma transform
+// blocks of planes U and V (32x32, SSE partials) in one launch.
+int rv_rdo_candidates(const rv::RdoArgs &luma, const rv::RdoArgs &chroma, int hbd,
                       hipStream_t s);

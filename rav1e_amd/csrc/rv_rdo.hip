@@ -72,19 +72,14 @@ __device__ __forceinline__ int32_t rdo_rsa(int32_t v, int bit) {
 }
 
 template <typename Px, int N, bool MOMENTS>
-__global__ __launch_bounds__(64) void rdo_cand_kernel(RdoArgs a) {
+__device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &pl, int t,
+                                              int32_t *buf, Px *pred) {
   constexpr int B = (int)sizeof(Px);
   constexpr int S = N + 1;                       // padded LDS row (i32)
   constexpr int G = 64 / N, RG = N / G;          // MC lane groups
   constexpr int P = B == 1 ? ((N + 8 + 15) / 16) * 16 : ((2 * (N + 8) + 15) / 16) * 16;
   constexpr int C32 = N < 32 ? N : 32;           // coded coefficient extent
   static_assert((N + 7) * P <= N * S * 4, "window must fit the coefficient slab");
-  __shared__ int32_t buf[N * S];
-  __shared__ Px pred[N * N];
-
-  const int t = blockIdx.x;
-  if (t >= a.n_tx) return;
-  const RdoPlane &pl = a.p[blockIdx.y];
   const int lane = threadIdx.x;
   const int cand = t / a.ntx_per_cand;
   const rv_mc_job mj = pl.mc[cand];
@@ -324,23 +319,36 @@ __global__ __launch_bounds__(64) void rdo_cand_kernel(RdoArgs a) {
   }
 }
 
+// One launch per frame: blocks [0, luma.n_tx) are the luma candidates
+// (N = 64, cdef moments), the rest the chroma transform blocks of planes U
+// then V (N = 32, SSE).  Luma first: the long tasks start first.
+template <typename Px>
+__global__ __launch_bounds__(64) void rdo_frame_kernel(RdoArgs luma, RdoArgs chroma) {
+  __shared__ int32_t buf[64 * 65];
+  __shared__ Px pred[64 * 64];
+  int b = blockIdx.x;
+  if (b < luma.n_tx) {
+    rdo_cand_body<Px, 64, true>(luma, luma.p[0], b, buf, pred);
+  } else {
+    b -= luma.n_tx;
+    const int plane = b / chroma.n_tx;
+    rdo_cand_body<Px, 32, false>(chroma, chroma.p[plane], b - plane * chroma.n_tx, buf, pred);
+  }
+}
+
 }  // namespace rv
 
 using namespace rv;
 
-// Replay-internal entry (rv_replay.hip).  Luma: one plane, N = 64, cdef
-// moments; chroma: planes U and V in one launch (blockIdx.y), N = 32, SSE.
-int rv_rdo_candidates(const RdoArgs &a, int nplanes, int n, int moments, int hbd,
-                      hipStream_t s) {
-  if (a.n_tx == 0) return RV_OK;
-  dim3 grid((unsigned)a.n_tx, (unsigned)nplanes);
-#define RV_RDO(PX, NN, MOM) rdo_cand_kernel<PX, NN, MOM><<<grid, 64, 0, s>>>(a)
-  if (n == 64 && moments && !hbd) RV_RDO(uint8_t, 64, true);
-  else if (n == 64 && moments && hbd) RV_RDO(uint16_t, 64, true);
-  else if (n == 32 && !moments && !hbd) RV_RDO(uint8_t, 32, false);
-  else if (n == 32 && !moments && hbd) RV_RDO(uint16_t, 32, false);
-  else return rv_set_error(RV_ENOTSUP, "rv_rdo_candidates: unsupported shape");
-#undef RV_RDO
+// Replay-internal entry (rv_replay.hip): luma (N = 64, moments) and both
+// chroma planes (N = 32, SSE) of every candidate in one launch.
+int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s) {
+  const unsigned grid = (unsigned)(luma.n_tx + 2 * chroma.n_tx);
+  if (grid == 0) return RV_OK;
+  if (hbd)
+    rdo_frame_kernel<uint16_t><<<grid, 64, 0, s>>>(luma, chroma);
+  else
+    rdo_frame_kernel<uint8_t><<<grid, 64, 0, s>>>(luma, chroma);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

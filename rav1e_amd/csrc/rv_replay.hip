@@ -598,7 +598,7 @@ int rv_replay_set_frame(rv_replay *r, int slot, const void *host_yuv) {
 
 // Event layout per frame (ring slot): 0..6 stage bounds F0..F5; then
 // kernel brackets [7,8] F3 full-pel diamond, [9,10] F3 sub-pel diamond,
-// [11,12] F4 fused luma candidates, [13,14] F4 fused chroma candidates.
+// [11,12] F4 fused candidates (luma + chroma, one launch).
 // F1 ([1,2]) holds only the full-search launches.
 int rv_replay_frame(rv_replay *r, int me_range_scale) {
   if (!r || (me_range_scale != 1 && me_range_scale != 2 && me_range_scale != 4))
@@ -672,9 +672,6 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
     la.bd = g.bd;
     la.mb_w = la.mb_h = kSb;
     la.sub_w = la.sub_h = 8;
-    RV_H(hipEventRecord(r->ev[11], st));
-    RV_R(rv_rdo_candidates(la, 1, 64, 1, g.hbd, st));
-    RV_H(hipEventRecord(r->ev[12], st));
     RdoArgs ca = la;
     const rv_plane *cp[2] = {&cur.u, &cur.v};
     const rv_plane *tp[2] = {&r->tall_u, &r->tall_v};
@@ -694,9 +691,9 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
     ca.mb_h = g.ch;
     ca.sub_w = (g.cw < 8 ? g.cw : 8) >> g.xdec;
     ca.sub_h = (g.ch < 8 ? g.ch : 8) >> g.ydec;
-    RV_H(hipEventRecord(r->ev[13], st));
-    RV_R(rv_rdo_candidates(ca, 2, 32, 0, g.hbd, st));
-    RV_H(hipEventRecord(r->ev[14], st));
+    RV_H(hipEventRecord(r->ev[11], st));
+    RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
+    RV_H(hipEventRecord(r->ev[12], st));
   }
   score_candidates<<<g.nsb, 64, 0, st>>>(g, r->l_mom, r->u_sse, r->v_sse, r->lsub, r->csub,
                                          r->coarse, r->half, r->full, r->sub, r->words);
@@ -744,7 +741,7 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
   if (last < 1) last = 1;
   if (last > rv_replay::kRing) last = rv_replay::kRing;
   if (last > r->frames) last = (int)r->frames;
-  for (int i = 0; i < cap && i < 10; i++) ms_out[i] = 0.f;
+  for (int i = 0; i < cap && i < 9; i++) ms_out[i] = 0.f;
   int n = 0;
   for (int f = 0; f < last; f++) {
     hipEvent_t *e = r->evs[(r->frames - 1 - f) % rv_replay::kRing];
@@ -755,7 +752,7 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
       RV_H(hipEventElapsedTime(&ms, e[i], e[i + 1]));
       ms_out[n++] += ms;
     }
-    for (int i = 7; i < 15 && n < cap; i += 2) {  // kernel brackets
+    for (int i = 7; i < 13 && n < cap; i += 2) {  // kernel brackets
       float ms = 0.f;
       RV_H(hipEventElapsedTime(&ms, e[i], e[i + 1]));
       ms_out[n++] += ms;
