@@ -153,6 +153,110 @@ struct SubGeo {
   static constexpr int kUnionDwords = (H + 7 + D) * UP / 4;
 };
 
+// |org - put_8tap| of one lane's column over RG output rows, read from a
+// staged window (pitch UP bytes, `win` = the candidate's row -3, `cx` = the
+// lane's window column of its output's -3 tap).  HF / VF: horizontal /
+// vertical filtering active (frac != 0), fixed per candidate so the row loop
+// carries no per-row branches (src/mc.rs:232-307 cases (x,y), (x,0), (0,y),
+// (0,0)).
+template <typename Px, int W, int RG, int UP, bool HF, bool VF>
+__device__ __forceinline__ uint32_t sub_sad_rows(const uint32_t *win, const Px *ocol, int cx,
+                                                 int grp, const int8_t *xf, const int8_t *yf,
+                                                 int ib, int maxv) {
+  constexpr int B = (int)sizeof(Px);
+  constexpr int PD = UP / 4;  // window pitch in dwords
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  uint32_t xp[4] = {0, 0, 0, 0};  // u8: 2 x i8x4; u16: 4 x i16x2
+  int xsum = 0;
+  if constexpr (HF) {
+    if constexpr (B == 1) {
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+        xp[h] = (uint32_t)(uint8_t)xf[4 * h] | ((uint32_t)(uint8_t)xf[4 * h + 1] << 8) |
+                ((uint32_t)(uint8_t)xf[4 * h + 2] << 16) | ((uint32_t)(uint8_t)xf[4 * h + 3] << 24);
+#pragma unroll
+      for (int k = 0; k < 8; k++) xsum += xf[k];
+    } else {
+#pragma unroll
+      for (int h = 0; h < 4; h++)
+        xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h] |
+                ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] << 16);
+    }
+  }
+  int yt[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) yt[k] = VF ? yf[k] : 0;
+  const uint32_t *base = win + grp * RG * PD;
+  // horizontal value of window row t at this lane's column: the 8-tap sum
+  // rounded to the i16 intermediate (HF), or the pixel under tap 3
+  auto hval = [&](int t) __attribute__((always_inline)) -> int32_t {
+    const uint32_t *row = base + t * PD;
+    if constexpr (B == 1) {
+      if constexpr (!HF) {
+        return (int32_t)reinterpret_cast<const uint8_t *>(row)[cx + 3];
+      } else {
+        const int d0 = cx >> 2, sh = cx & 3;
+        const uint32_t w0 = row[d0], w1 = row[d0 + 1], w2 = row[d0 + 2];
+        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        int32_t s = __builtin_amdgcn_sdot4((int)(lo ^ 0x80808080u), (int)xp[0], 128 * xsum, false);
+        s = __builtin_amdgcn_sdot4((int)(hi ^ 0x80808080u), (int)xp[1], s, false);
+        return (int32_t)(int16_t)round_shift(s, 7 - ib);
+      }
+    } else {
+      if constexpr (!HF) {
+        return (int32_t)reinterpret_cast<const uint16_t *>(row)[cx + 3];
+      } else {
+        const int d0 = cx >> 1, sh = (cx & 1) * 2;
+        uint32_t w[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) w[k] = row[d0 + k];
+        int32_t s = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          s = __builtin_amdgcn_sdot2(
+              __builtin_bit_cast(s2, __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh)),
+              __builtin_bit_cast(s2, xp[k]), s, false);
+        return (int32_t)(int16_t)round_shift(s, 7 - ib);
+      }
+    }
+  };
+  uint32_t acc = 0;
+  if constexpr (!VF) {
+    // (x,0): round_shift(intermediate, ib); (0,0): the pixel itself
+#pragma unroll 8
+    for (int r = 0; r < RG; r++) {
+      int32_t v = hval(r + 3);
+      if constexpr (HF) v = clampi(round_shift(v, ib), 0, maxv);
+      const int d = (int)ocol[r * W] - v;
+      acc += (uint32_t)(d < 0 ? -d : d);
+    }
+  } else {
+    // vertical 8-tap over a register ring of horizontal values; unrolled by
+    // 8 so the ring indices are compile-time constants
+    const int vshift = HF ? 7 + ib : 7;
+    int32_t ring[8];
+#pragma unroll
+    for (int t = 0; t < 7; t++) ring[t] = hval(t);
+    ring[7] = 0;
+#pragma unroll 1
+    for (int r0 = 0; r0 < RG; r0 += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int r = r0 + u;
+        ring[(u + 7) & 7] = hval(r + 7);
+        int32_t s = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(u + k) & 7]);
+        const int v = clampi(round_shift(s, vshift), 0, maxv);
+        const int d = (int)ocol[r * W] - v;
+        acc += (uint32_t)(d < 0 ? -d : d);
+      }
+    }
+  }
+  return acc;
+}
+
 template <typename Px, int W, int H, bool SUB>
 struct DsFast {
   using F = FullGeo<Px, W, H>;
@@ -166,7 +270,6 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
   using S = SubGeo<Px, W, H>;
   constexpr int B = (int)sizeof(Px);
   static_assert(!SUB || S::RG % 8 == 0, "sub-pel row groups are unrolled by 8");
-  __shared__ uint64_t pcost[RV_DS_MAX_PRED];
   __shared__ uint64_t scost[2][kDsWaves];
   __shared__ uint32_t wevals[kDsWaves];
   __shared__ uint32_t win_all[SUB ? S::kUnionDwords : 1];
@@ -209,7 +312,7 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
   uint32_t evals = 0;
 
   // ---- full-pel: one candidate, evaluated by this wavefront -------------
-  auto eval_full = [&](rv_mv mv) -> uint64_t {
+  auto eval_full = [&](rv_mv mv) __attribute__((always_inline)) -> uint64_t {
     if (!ds_in_range(mv, jb)) return ~0ull;
     evals++;
     uint32_t acc = 0;
@@ -239,7 +342,7 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
   struct SubPos {
     int qx, qy, cf, rf, ok;
   };
-  auto sub_pos = [&](rv_mv mv) -> SubPos {
+  auto sub_pos = [&](rv_mv mv) __attribute__((always_inline)) -> SubPos {
     SubPos q;
     q.ok = ds_in_range(mv, jb);
     const int xs = 3 + ref.xdec, ys = 3 + ref.ydec;
@@ -251,7 +354,7 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
     return q;
   };
   // stage the box at (bx, by) of rows x cols pixels into uwin (pitch UP bytes)
-  auto load_box = [&](int bx, int by, int rows, int cols) {
+  auto load_box = [&](int bx, int by, int rows, int cols) __attribute__((always_inline)) {
     const uint8_t *sp = (const uint8_t *)plane_ptr<Px>(ref, bx, by);
     const int64_t rs = (int64_t)ref.stride * B;
     const int rdw = (cols * B + 3) >> 2, tot = rows * rdw;
@@ -277,97 +380,28 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
     }
   };
   // SAD of this wavefront's candidate from the staged window, the window
-  // pixel (dx, dy) being the candidate's (-3, -3) origin
-  auto sub_sad = [&](int cf, int rf, int dx, int dy) -> uint32_t {
+  // pixel (dx, dy) being the candidate's (-3, -3) origin; the filter case
+  // (horizontal / vertical / both / copy) is resolved once per candidate
+  auto sub_sad = [&](int cf, int rf, int dx, int dy) __attribute__((always_inline)) -> uint32_t {
+    const uint32_t *w0 = win_all + dy * (S::UP / 4);
+    const Px *ocol = org_lds + grp * S::RG * W + col;
     const int8_t *xf = kReg[W <= 4][cf];
     const int8_t *yf = kReg[H <= 4][rf];
-    int yt[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) yt[k] = yf[k];
-    uint32_t xp[4];  // u8: 2 x i8x4 (xp[0..1]); u16: 4 x i16x2
-    int xsum = 0;
-    if constexpr (B == 1) {
-#pragma unroll
-      for (int h = 0; h < 2; h++)
-        xp[h] = (uint32_t)(uint8_t)xf[4 * h] | ((uint32_t)(uint8_t)xf[4 * h + 1] << 8) |
-                ((uint32_t)(uint8_t)xf[4 * h + 2] << 16) | ((uint32_t)(uint8_t)xf[4 * h + 3] << 24);
-#pragma unroll
-      for (int k = 0; k < 8; k++) xsum += xf[k];
-      xp[2] = xp[3] = 0;
-    } else {
-#pragma unroll
-      for (int h = 0; h < 4; h++)
-        xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h] |
-                ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] << 16);
-    }
-    const int ib2 = ib;
-    const int cx = col + dx;  // window column of this lane's output
-    // horizontal value of window row t (group-relative) for column col
-    auto hval = [&](int t) -> int32_t {
-      const uint32_t *row = win_all + (dy + grp * S::RG + t) * (S::UP / 4);
-      if constexpr (B == 1) {
-        const int d0 = cx >> 2, sh = cx & 3;
-        const uint32_t w0 = row[d0], w1 = row[d0 + 1], w2 = row[d0 + 2];
-        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-        if (!cf) return (int32_t)(lo >> 24);
-        int32_t s = __builtin_amdgcn_sdot4((int)(lo ^ 0x80808080u), (int)xp[0], 128 * xsum, false);
-        s = __builtin_amdgcn_sdot4((int)(hi ^ 0x80808080u), (int)xp[1], s, false);
-        return (int32_t)(int16_t)round_shift(s, 7 - ib2);
-      } else {
-        typedef short s2 __attribute__((ext_vector_type(2)));
-        const int d0 = cx >> 1, sh = (cx & 1) * 2;
-        uint32_t w[5];
-#pragma unroll
-        for (int k = 0; k < 5; k++) w[k] = row[d0 + k];
-        uint32_t p[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) p[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-        if (!cf) return (int32_t)(p[1] >> 16);
-        int32_t s = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          s = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, p[k]), __builtin_bit_cast(s2, xp[k]), s,
-                                     false);
-        return (int32_t)(int16_t)round_shift(s, 7 - ib2);
-      }
-    };
-    const int vshift = cf ? 7 + ib : 7;
-    // vertical pass: register ring of 8 horizontal values; the row loop is
-    // unrolled by 8 only, so the ring indices stay compile-time constants
-    // without the whole block's LDS reads being hoisted into VGPRs
-    uint32_t acc = 0;
-    int32_t ring[8];
-#pragma unroll
-    for (int t = 0; t < 7; t++) ring[t] = hval(t);
-    ring[7] = 0;
-    const Px *ocol = org_lds + grp * S::RG * W + col;
-#pragma unroll 1
-    for (int r0 = 0; r0 < S::RG; r0 += 8) {
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int r = r0 + u;
-        ring[(u + 7) & 7] = hval(r + 7);
-        int32_t v;
-        if (rf) {
-          int32_t s = 0;
-#pragma unroll
-          for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(u + k) & 7]);
-          v = round_shift(s, vshift);
-        } else {
-          v = cf ? round_shift(ring[(u + 3) & 7], ib) : ring[(u + 3) & 7];
-        }
-        v = clampi(v, 0, maxv);
-        const int d = (int)ocol[r * W] - v;
-        acc += (uint32_t)(d < 0 ? -d : d);
-      }
-    }
+    uint32_t acc;
+    if (cf && rf)
+      acc = sub_sad_rows<Px, W, S::RG, S::UP, true, true>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
+    else if (cf)
+      acc = sub_sad_rows<Px, W, S::RG, S::UP, true, false>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
+    else if (rf)
+      acc = sub_sad_rows<Px, W, S::RG, S::UP, false, true>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
+    else
+      acc = sub_sad_rows<Px, W, S::RG, S::UP, false, false>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
     return wave_sum(acc);
   };
   // Called by every thread.  Wave w evaluates cands[w] (w < n); returns its
   // cost (u64::MAX when out of range or w >= n).  No trailing barrier: the
   // caller's cost exchange barrier orders the next round's window writes.
-  auto sub_round = [&](const rv_mv *cands, int n) -> uint64_t {
+  auto sub_round = [&](const rv_mv *cands, int n) __attribute__((always_inline)) -> uint64_t {
     SubPos q[kDsWaves];
     int ux = 1 << 30, uy = 1 << 30, ux2 = -(1 << 30), uy2 = -(1 << 30), any = 0;
 #pragma unroll
@@ -400,84 +434,91 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
         mine = ds_cost(sub_sad(me.cf, me.rf, me.qx - ux, me.qy - uy), me_mv, jb, a.hp);
       }
     } else {  // far-apart predictors: one window at a time
+#pragma unroll 1
+      for (int k = 0; k < n; k++) {
+        rv_mv ck = cands[0];  // static indices only (no scratch)
 #pragma unroll
-      for (int k = 0; k < kDsWaves; k++) {
-        if (!q[k].ok) continue;
+        for (int j = 1; j < kDsWaves; j++)
+          if (k == j) ck = cands[j];
+        const SubPos qk = sub_pos(ck);
         __syncthreads();  // previous window consumed
-        load_box(q[k].qx, q[k].qy, H + 7, W + 7);
+        if (qk.ok) load_box(qk.qx, qk.qy, H + 7, W + 7);
         __syncthreads();
-        if (wave == k) {
+        if (qk.ok && wave == k) {
           evals++;
-          mine = ds_cost(sub_sad(q[k].cf, q[k].rf, 0, 0), cands[k], jb, a.hp);
+          mine = ds_cost(sub_sad(qk.cf, qk.rf, 0, 0), ck, jb, a.hp);
         }
       }
     }
     return mine;
   };
 
-  // ---- get_best_predictor: predictors evaluated 4 at a time ------------
+  // ---- get_best_predictor, then diamond steps: one round loop -----------
+  // A round evaluates up to 4 candidates, one per wavefront: first the
+  // predictors in groups of 4 (the sequential strict-< scan of
+  // get_best_predictor, applied group by group in order, is the same
+  // first minimum), then the 4 pattern points of each diamond step.  One
+  // call site keeps a single inlined copy of the candidate code.
   const int np = jb.n_pred < RV_DS_MAX_PRED ? jb.n_pred : RV_DS_MAX_PRED;
-  for (int p0 = 0; p0 < np; p0 += kDsWaves) {
-    const int p = p0 + wave;
-    if constexpr (SUB) {
-      rv_mv c4[kDsWaves];
-#pragma unroll
-      for (int k = 0; k < kDsWaves; k++) c4[k] = jp->pred[p0 + k < np ? p0 + k : p0];
-      const uint64_t c = sub_round(c4, np - p0 < kDsWaves ? np - p0 : kDsWaves);
-      if (lane == 0 && p < np) pcost[p] = c;
-      __syncthreads();  // window consumed before the next round
-    } else if (p < np) {
-      const uint64_t c = eval_full(jp->pred[p]);
-      if (lane == 0) pcost[p] = c;
-    }
-  }
-  __syncthreads();
   rv_mv center{0, 0};
   uint64_t center_cost = ~0ull;
-  for (int p = 0; p < np; p++) {
-    const uint64_t c = pcost[p];
-    if (c < center_cost) {
-      center = jp->pred[p];
-      center_cost = c;
-    }
-  }
-  // ---- diamond steps: the 4 pattern points in parallel -----------------
   int16_t radius = a.subpel ? 4 : 16;
   const int16_t radius_end = a.subpel ? (a.hp ? 1 : 2) : 8;
-  const int pr = wave == 0 ? 1 : wave == 2 ? -1 : 0;  // diamond_pattern
-  const int pc = wave == 1 ? 1 : wave == 3 ? -1 : 0;
-  // Every move strictly lowers center_cost, so the loop ends; the bound
-  // only guarantees the grid drains whatever the inputs.
-  for (int iter = 0; iter < 4096; iter++) {
+  int p0 = 0;  // next predictor group; >= np once the diamond phase runs
+  // Every diamond move strictly lowers center_cost, so the loop ends; the
+  // bound only guarantees the grid drains whatever the inputs.
+  for (int iter = 0; iter < 4096 + RV_DS_MAX_PRED; iter++) {
+    const bool pred_phase = p0 < np;
+    rv_mv c4[kDsWaves];
+    int n;
+    if (pred_phase) {
+      n = np - p0 < kDsWaves ? np - p0 : kDsWaves;
+#pragma unroll
+      for (int k = 0; k < kDsWaves; k++) c4[k] = jp->pred[p0 + (k < n ? k : 0)];
+    } else {
+      n = kDsWaves;
+      c4[0] = rv_mv{(int16_t)(center.row + radius), center.col};  // diamond_pattern
+      c4[1] = rv_mv{center.row, (int16_t)(center.col + radius)};
+      c4[2] = rv_mv{(int16_t)(center.row - radius), center.col};
+      c4[3] = rv_mv{center.row, (int16_t)(center.col - radius)};
+    }
     uint64_t c;
     if constexpr (SUB) {
-      const rv_mv c4[kDsWaves] = {
-          rv_mv{(int16_t)(center.row + radius), center.col},
-          rv_mv{center.row, (int16_t)(center.col + radius)},
-          rv_mv{(int16_t)(center.row - radius), center.col},
-          rv_mv{center.row, (int16_t)(center.col - radius)}};
-      c = sub_round(c4, kDsWaves);
+      c = sub_round(c4, n);
     } else {
-      c = eval_full(rv_mv{(int16_t)(center.row + radius * pr), (int16_t)(center.col + radius * pc)});
+      rv_mv mine = c4[0];
+#pragma unroll
+      for (int k = 1; k < kDsWaves; k++)
+        if (wave == k) mine = c4[k];
+      c = wave < n ? eval_full(mine) : ~0ull;
     }
     if (lane == 0) scost[iter & 1][wave] = c;
     __syncthreads();
     uint64_t best = ~0ull;
     int bp = 0;
 #pragma unroll
-    for (int p = 0; p < kDsWaves; p++) {
-      const uint64_t v = scost[iter & 1][p];
-      if (v < best) {
+    for (int k = 0; k < kDsWaves; k++) {
+      const uint64_t v = scost[iter & 1][k];
+      if (k < n && v < best) {
         best = v;
-        bp = p;
+        bp = k;
       }
     }
-    if (center_cost <= best) {
+    rv_mv bmv = c4[0];
+#pragma unroll
+    for (int k = 1; k < kDsWaves; k++)
+      if (bp == k) bmv = c4[k];
+    if (pred_phase) {
+      if (best < center_cost) {
+        center = bmv;
+        center_cost = best;
+      }
+      p0 += kDsWaves;
+    } else if (center_cost <= best) {
       if (radius == radius_end) break;
       radius /= 2;
     } else {
-      const int br = bp == 0 ? 1 : bp == 2 ? -1 : 0, bc = bp == 1 ? 1 : bp == 3 ? -1 : 0;
-      center = rv_mv{(int16_t)(center.row + radius * br), (int16_t)(center.col + radius * bc)};
+      center = bmv;
       center_cost = best;
     }
   }
