@@ -155,10 +155,14 @@ struct SubGeo {
 
 // |org - put_8tap| of one lane's column over RG output rows, read from a
 // staged window (pitch UP bytes, `win` = the candidate's row -3, `cx` = the
-// lane's window column of its output's -3 tap).  HF / VF: horizontal /
-// vertical filtering active (frac != 0), fixed per candidate so the row loop
-// carries no per-row branches (src/mc.rs:232-307 cases (x,y), (x,0), (0,y),
-// (0,0)).
+// lane's window column of its output's -3 tap; u8 windows are stored with
+// every byte XOR 0x80, i.e. as i8 = pixel - 128, for v_dot4_i32_i8).
+// HF / VF: horizontal / vertical filtering active (frac != 0), fixed per
+// candidate so the row loop carries no per-row branches (src/mc.rs:232-307
+// cases (x,y), (x,0), (0,y), (0,0)).  The vertical 8-tap runs as four
+// v_dot2_i32_i16 over a ring of packed (m[j], m[j+1]) intermediate pairs.
+// Range: every intermediate fits i16 for REGULAR taps at 8/10/12 bits
+// (max 4095 * 136 >> 5), so the reference's `as i16` is the identity here.
 template <typename Px, int W, int RG, int UP, bool HF, bool VF>
 __device__ __forceinline__ uint32_t sub_sad_rows(const uint32_t *win, const Px *ocol, int cx,
                                                  int grp, const int8_t *xf, const int8_t *yf,
@@ -183,25 +187,31 @@ __device__ __forceinline__ uint32_t sub_sad_rows(const uint32_t *win, const Px *
                 ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] << 16);
     }
   }
-  int yt[8];
+  uint32_t tp[4] = {0, 0, 0, 0};  // vertical taps as i16 pairs
+  if constexpr (VF) {
 #pragma unroll
-  for (int k = 0; k < 8; k++) yt[k] = VF ? yf[k] : 0;
+    for (int h = 0; h < 4; h++)
+      tp[h] = (uint32_t)(uint16_t)(int16_t)yf[2 * h] |
+              ((uint32_t)(uint16_t)(int16_t)yf[2 * h + 1] << 16);
+  }
+  const int hbias = 128 * xsum;
+  const int hround = (1 << (7 - ib)) >> 1, hsh = 7 - ib;
   const uint32_t *base = win + grp * RG * PD;
   // horizontal value of window row t at this lane's column: the 8-tap sum
-  // rounded to the i16 intermediate (HF), or the pixel under tap 3
+  // rounded to the intermediate (HF), or the pixel under tap 3
   auto hval = [&](int t) __attribute__((always_inline)) -> int32_t {
     const uint32_t *row = base + t * PD;
     if constexpr (B == 1) {
       if constexpr (!HF) {
-        return (int32_t)reinterpret_cast<const uint8_t *>(row)[cx + 3];
+        return (int32_t)(reinterpret_cast<const uint8_t *>(row)[cx + 3] ^ 0x80u);
       } else {
         const int d0 = cx >> 2, sh = cx & 3;
         const uint32_t w0 = row[d0], w1 = row[d0 + 1], w2 = row[d0 + 2];
-        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-        int32_t s = __builtin_amdgcn_sdot4((int)(lo ^ 0x80808080u), (int)xp[0], 128 * xsum, false);
-        s = __builtin_amdgcn_sdot4((int)(hi ^ 0x80808080u), (int)xp[1], s, false);
-        return (int32_t)(int16_t)round_shift(s, 7 - ib);
+        int32_t s = __builtin_amdgcn_sdot4((int)__builtin_amdgcn_alignbyte(w1, w0, sh), (int)xp[0],
+                                           hbias + hround, false);
+        s = __builtin_amdgcn_sdot4((int)__builtin_amdgcn_alignbyte(w2, w1, sh), (int)xp[1], s,
+                                   false);
+        return s >> hsh;
       }
     } else {
       if constexpr (!HF) {
@@ -211,15 +221,18 @@ __device__ __forceinline__ uint32_t sub_sad_rows(const uint32_t *win, const Px *
         uint32_t w[5];
 #pragma unroll
         for (int k = 0; k < 5; k++) w[k] = row[d0 + k];
-        int32_t s = 0;
+        int32_t s = hround;
 #pragma unroll
         for (int k = 0; k < 4; k++)
           s = __builtin_amdgcn_sdot2(
               __builtin_bit_cast(s2, __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh)),
               __builtin_bit_cast(s2, xp[k]), s, false);
-        return (int32_t)(int16_t)round_shift(s, 7 - ib);
+        return s >> hsh;
       }
     }
+  };
+  auto absdiff_acc = [](uint32_t a, uint32_t b, uint32_t acc) __attribute__((always_inline)) {
+    return (a > b ? a - b : b - a) + acc;  // v_sad_u32
   };
   uint32_t acc = 0;
   if constexpr (!VF) {
@@ -228,29 +241,38 @@ __device__ __forceinline__ uint32_t sub_sad_rows(const uint32_t *win, const Px *
     for (int r = 0; r < RG; r++) {
       int32_t v = hval(r + 3);
       if constexpr (HF) v = clampi(round_shift(v, ib), 0, maxv);
-      const int d = (int)ocol[r * W] - v;
-      acc += (uint32_t)(d < 0 ? -d : d);
+      acc = absdiff_acc((uint32_t)ocol[r * W], (uint32_t)v, acc);
     }
   } else {
-    // vertical 8-tap over a register ring of horizontal values; unrolled by
-    // 8 so the ring indices are compile-time constants
     const int vshift = HF ? 7 + ib : 7;
-    int32_t ring[8];
+    const int vround = (1 << vshift) >> 1;
+    auto pack = [](int32_t lo, int32_t hi) __attribute__((always_inline)) {
+      return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
+    };
+    uint32_t pr[8];  // pr[j & 7] = (m[j], m[j + 1])
+    int32_t prev = hval(0);
 #pragma unroll
-    for (int t = 0; t < 7; t++) ring[t] = hval(t);
-    ring[7] = 0;
+    for (int t = 1; t < 7; t++) {
+      const int32_t m = hval(t);
+      pr[t - 1] = pack(prev, m);
+      prev = m;
+    }
+    pr[6] = pr[7] = 0;
 #pragma unroll 1
     for (int r0 = 0; r0 < RG; r0 += 8) {
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int r = r0 + u;
-        ring[(u + 7) & 7] = hval(r + 7);
-        int32_t s = 0;
+        const int32_t m = hval(r + 7);
+        pr[(u + 6) & 7] = pack(prev, m);
+        prev = m;
+        int32_t s = vround;
 #pragma unroll
-        for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(u + k) & 7]);
-        const int v = clampi(round_shift(s, vshift), 0, maxv);
-        const int d = (int)ocol[r * W] - v;
-        acc += (uint32_t)(d < 0 ? -d : d);
+        for (int k = 0; k < 4; k++)
+          s = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, pr[(u + 2 * k) & 7]),
+                                     __builtin_bit_cast(s2, tp[k]), s, false);
+        const int v = clampi(s >> vshift, 0, maxv);
+        acc = absdiff_acc((uint32_t)ocol[r * W], (uint32_t)v, acc);
       }
     }
   }
@@ -374,7 +396,8 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
         const int i = i0 + u * kDsThreads;
         if (i < tot) {
           const int r = i / rdw, d = i - r * rdw;
-          win_all[r * (S::UP / 4) + d] = v[u];
+          // u8: stored as i8 = pixel - 128 (the horizontal v_dot4_i32_i8)
+          win_all[r * (S::UP / 4) + d] = B == 1 ? v[u] ^ 0x80808080u : v[u];
         }
       }
     }
