@@ -28,7 +28,7 @@ __device__ __forceinline__ int32_t wmul(int32_t a, int32_t b) {
 __device__ __forceinline__ int32_t round_shift(int32_t v, int bit) {
   return wadd(v, (1 << bit) >> 1) >> bit;
 }
-__device__ __forceinline__ int32_t clampi(int32_t v, int32_t lo, int32_t hi) {
+__host__ __device__ __forceinline__ int32_t clampi(int32_t v, int32_t lo, int32_t hi) {
   return v < lo ? lo : (v > hi ? hi : v);
 }
 // msb (src/util/mod.rs:235-238)
@@ -85,6 +85,49 @@ __device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t *p) {
 __device__ __forceinline__ uint32_t sad_u8x4(uint32_t a, uint32_t b,
                                              uint32_t acc) {
   return __builtin_amdgcn_sad_u8(a, b, acc);
+}
+
+// ---- SATD chunk: get_satd_ref (src/dist.rs:197-328) ------------------------
+// The butterfly network is exact integer arithmetic whose outputs are a
+// signed permutation of the Walsh-Hadamard transform, so sum |.| does not
+// depend on butterfly order; the network below is the reference's
+// (hadamard4_1d / hadamard8_1d, src/dist.rs:208-256).
+template <int N>
+__device__ __forceinline__ void had1d(int32_t *v, int s) {
+#pragma unroll
+  for (int k = 0; k < N; k += 2) {
+    int32_t a = v[k * s], b = v[(k + 1) * s];
+    v[k * s] = a + b;
+    v[(k + 1) * s] = a - b;
+  }
+#pragma unroll
+  for (int g = 0; g < N; g += 4)
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      int32_t a = v[(g + k) * s], b = v[(g + k + 2) * s];
+      v[(g + k) * s] = a + b;
+      v[(g + k + 2) * s] = a - b;
+    }
+  if constexpr (N == 8) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int32_t a = v[k * s], b = v[(k + 4) * s];
+      v[k * s] = a + b;
+      v[(k + 4) * s] = a - b;
+    }
+  }
+}
+
+template <int N>
+__device__ __forceinline__ uint64_t satd_chunk(int32_t *d) {
+#pragma unroll
+  for (int c = 0; c < N; c++) had1d<N>(d + c, N);  // vertical
+#pragma unroll
+  for (int r = 0; r < N; r++) had1d<N>(d + r * N, 1);  // horizontal
+  uint32_t s = 0;  // <= 64 * 64 * 4095 per 8x8 chunk: fits u32
+#pragma unroll
+  for (int i = 0; i < N * N; i++) s += (uint32_t)(d[i] < 0 ? -d[i] : d[i]);
+  return s;
 }
 
 }  // namespace rv

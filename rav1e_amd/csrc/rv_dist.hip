@@ -55,49 +55,8 @@ __global__ __launch_bounds__(kBlock) void sad_kernel(
   if (live && t == 0) out[job] = acc;
 }
 
-// ---- SATD: get_satd_ref (src/dist.rs:197-328) -----------------------------
-// The butterfly network is exact integer arithmetic whose outputs are a
-// signed permutation of the Walsh-Hadamard transform, so sum |.| does not
-// depend on butterfly order; the network below is the reference's
-// (hadamard4_1d / hadamard8_1d, src/dist.rs:208-256).
-template <int N>
-__device__ __forceinline__ void had1d(int32_t *v, int s) {
-#pragma unroll
-  for (int k = 0; k < N; k += 2) {
-    int32_t a = v[k * s], b = v[(k + 1) * s];
-    v[k * s] = a + b;
-    v[(k + 1) * s] = a - b;
-  }
-#pragma unroll
-  for (int g = 0; g < N; g += 4)
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      int32_t a = v[(g + k) * s], b = v[(g + k + 2) * s];
-      v[(g + k) * s] = a + b;
-      v[(g + k + 2) * s] = a - b;
-    }
-  if constexpr (N == 8) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      int32_t a = v[k * s], b = v[(k + 4) * s];
-      v[k * s] = a + b;
-      v[(k + 4) * s] = a - b;
-    }
-  }
-}
-
-template <int N>
-__device__ __forceinline__ uint64_t satd_chunk(int32_t *d) {
-#pragma unroll
-  for (int c = 0; c < N; c++) had1d<N>(d + c, N);  // vertical
-#pragma unroll
-  for (int r = 0; r < N; r++) had1d<N>(d + r * N, 1);  // horizontal
-  uint32_t s = 0;  // <= 64 * 64 * 4095 per 8x8 chunk: fits u32
-#pragma unroll
-  for (int i = 0; i < N * N; i++) s += (uint32_t)(d[i] < 0 ? -d[i] : d[i]);
-  return s;
-}
-
+// ---- SATD: get_satd_ref (src/dist.rs:197-328); had1d / satd_chunk live in
+// rv_device.h (the replay's importance kernel uses them too)
 template <typename Px, int N, int LG>
 __global__ __launch_bounds__(kBlock) void satd_kernel(
     rv_plane org, rv_plane ref, const rv_dist_job *__restrict__ jobs, int n,

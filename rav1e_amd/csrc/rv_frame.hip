@@ -36,9 +36,53 @@ __global__ __launch_bounds__(256) void downsample_kernel(rv_plane dst,
   *plane_ptr_mut<Px>(dst, c, r) = (Px)((sum + 2) >> 2);
 }
 
+// The replay's per-frame F0 in one launch: input_hres and input_qres
+// (src/encoder.rs:3382-3385: downsample_from twice, each followed by pad)
+// computed straight from the full-resolution plane.  Every allocation pixel
+// of hres (blockIdx.y = 0) / qres (1) is the downsampled value at the
+// clamped visible coordinate -- exactly what downsample + pad leave there;
+// qres pixels recompute their four hres parents with the same rounding.
+template <typename Px>
+__device__ __forceinline__ uint32_t ds2x2(const Px *s, int stride) {
+  return ((uint32_t)s[0] + (uint32_t)s[1] + (uint32_t)s[stride] + (uint32_t)s[stride + 1] + 2) >> 2;
+}
+template <typename Px>
+__global__ __launch_bounds__(256) void pyramid_kernel(rv_plane y, rv_plane h, rv_plane q) {
+  const rv_plane &d = blockIdx.y ? q : h;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)d.stride * d.alloc_height) return;
+  const int ay = (int)(i / d.stride), ax = (int)(i - (int64_t)ay * d.stride);
+  const int c = clampi(ax - d.xorigin, 0, d.width - 1), r = clampi(ay - d.yorigin, 0, d.height - 1);
+  uint32_t v;
+  if (blockIdx.y == 0) {
+    v = ds2x2(plane_ptr<Px>(y, 2 * c, 2 * r), y.stride);
+  } else {
+    const Px *s = plane_ptr<Px>(y, 4 * c, 4 * r);
+    const int st = y.stride;
+    v = (ds2x2(s, st) + ds2x2(s + 2, st) + ds2x2(s + 2 * st, st) + ds2x2(s + 2 * st + 2, st) + 2) >> 2;
+  }
+  reinterpret_cast<Px *>(d.data)[i] = (Px)v;
+}
+
 }  // namespace rv
 
 using namespace rv;
+
+// hres = downsample(y) + pad, qres = downsample(hres) + pad, one launch.
+int rv_plane_pyramid(const rv_plane *y, const rv_plane *h, const rv_plane *q, void *stream) {
+  if (!y || !h || !q || y->hbd != h->hbd || h->hbd != q->hbd || h->width * 2 != y->width ||
+      h->height * 2 != y->height || q->width * 2 != h->width || q->height * 2 != h->height)
+    return rv_set_error(RV_EINVAL, "rv_plane_pyramid: size mismatch");
+  const int64_t th = (int64_t)h->stride * h->alloc_height;
+  dim3 grid((unsigned)((th + 255) / 256), 2);
+  hipStream_t s = rv_resolve_stream(stream);
+  if (y->hbd)
+    pyramid_kernel<uint16_t><<<grid, 256, 0, s>>>(*y, *h, *q);
+  else
+    pyramid_kernel<uint8_t><<<grid, 256, 0, s>>>(*y, *h, *q);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
 
 extern "C" {
 

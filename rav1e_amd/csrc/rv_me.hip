@@ -16,6 +16,7 @@
 // VALU-bound (~256 |a-b| per candidate), not HBM-bound.
 #include <string.h>
 
+#include "rv_chain.h"
 #include "rv_device.h"
 
 namespace rv {
@@ -75,7 +76,7 @@ __device__ __forceinline__ Best block_best(Best b) {
   return b;
 }
 
-__device__ __forceinline__ void write_result(const rv_fs_job &jb, Best b,
+__device__ __forceinline__ rv_fs_result write_result(const rv_fs_job &jb, Best b,
                                              int nx, int step,
                                              rv_fs_result *out) {
   rv_fs_result r;
@@ -90,13 +91,32 @@ __device__ __forceinline__ void write_result(const rv_fs_job &jb, Best b,
     r.cost = b.cost;
   }
   *out = r;
+  return r;
+}
+
+struct FsArgs {
+  rv_plane org;
+  rv_plane ref[RV_DS_MAX_PRED];  // job i searches ref[i / n_per_ref]
+  const rv_fs_job *jobs;
+  rv_fs_result *out;
+  int n, n_per_ref, hp, bw, bh, step;
+  ChainNext next;  // replay: feed the winner into the next stage's jobs
+};
+
+// blockIdx -> job with consecutive jobs on one XCD (blocks are dealt
+// round-robin to the 8 XCDs; neighbouring superblocks share reference rows
+// in that XCD's L2).  The grid is a multiple of 8.
+__device__ __forceinline__ int fs_job_index() {
+  const int per = (int)gridDim.x >> 3;
+  return ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
 }
 
 // ---- generic path: one lane per candidate --------------------------------
+// The result is valid in thread 0.
 template <typename Px>
-__device__ void fs_generic_body(const rv_plane &org, const rv_plane &ref,
-                                const rv_fs_job &jb, int bw, int bh,
-                                int step, int hp, rv_fs_result *out) {
+__device__ rv_fs_result fs_generic_body(const rv_plane &org, const rv_plane &ref,
+                                        const rv_fs_job &jb, int bw, int bh,
+                                        int step, int hp, rv_fs_result *out) {
   const int nx = jb.x_hi >= jb.x_lo ? (jb.x_hi - jb.x_lo) / step + 1 : 0;
   const int ny = jb.y_hi >= jb.y_lo ? (jb.y_hi - jb.y_lo) / step + 1 : 0;
   const Px *o = plane_ptr<Px>(org, jb.po_x, jb.po_y);
@@ -124,37 +144,28 @@ __device__ void fs_generic_body(const rv_plane &org, const rv_plane &ref,
     if (better(cost, (uint32_t)c, b)) b = Best{cost, (uint32_t)c};
   }
   b = block_best(b);
-  if (threadIdx.x == 0) write_result(jb, b, nx > 0 ? nx : 1, step, out);
+  rv_fs_result res{};
+  if (threadIdx.x == 0) res = write_result(jb, b, nx > 0 ? nx : 1, step, out);
+  return res;
 }
 
 template <typename Px>
-__global__ __launch_bounds__(kFsThreads) void fs_generic_kernel(
-    rv_plane org, rv_plane ref, const rv_fs_job *__restrict__ jobs, int n,
-    int bw, int bh, int step, int hp, rv_fs_result *__restrict__ out) {
-  const int job = blockIdx.x;
-  if (job >= n) return;
-  const rv_fs_job jb = jobs[job];
-  fs_generic_body<Px>(org, ref, jb, bw, bh, step, hp, out + job);
+__global__ __launch_bounds__(kFsThreads) void fs_generic_kernel(FsArgs a) {
+  const int job = fs_job_index();
+  if (job >= a.n) return;
+  const rv_fs_job jb = a.jobs[job];
+  const rv_fs_result res = fs_generic_body<Px>(a.org, a.ref[job / a.n_per_ref], jb, a.bw, a.bh,
+                                               a.step, a.hp, a.out + job);
+  if (threadIdx.x == 0) chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, res.best_mv);
 }
 
 // ---- fast path: u8, 16x16, step 1 ---------------------------------------
 constexpr int kTileRows = 8;         // candidate rows per lane
 constexpr int kLdsWords = 7 * 1024;  // 28 KiB search band: 5 workgroups per CU
 
-struct FsArgs {
-  rv_plane org;
-  rv_plane ref[RV_DS_MAX_PRED];  // job i searches ref[i / n_per_ref]
-  const rv_fs_job *jobs;
-  rv_fs_result *out;
-  int n, n_per_ref, hp;
-};
-
 __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(FsArgs a) {
   __shared__ uint32_t band[kLdsWords];
-  // consecutive jobs on one XCD (blocks are dealt round-robin to the 8 XCDs;
-  // neighbouring superblocks share reference rows in that XCD's L2)
-  const int per = (int)gridDim.x >> 3;
-  const int job = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+  const int job = fs_job_index();
   if (job >= a.n) return;
   const rv_fs_job jb = a.jobs[job];
   const rv_plane &ref = a.ref[job / a.n_per_ref];
@@ -174,7 +185,8 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(FsArgs a) {
   const int tx_n = (nx + 3) >> 2;       // 4-wide candidate columns
   const int rw = tx_n + 4;              // band row length in dwords
   if (rw * (2 * kTileRows + 15) > kLdsWords) {  // window too wide for a band
-    fs_generic_body<uint8_t>(a.org, ref, jb, 16, 16, 1, a.hp, a.out + job);
+    const rv_fs_result res = fs_generic_body<uint8_t>(a.org, ref, jb, 16, 16, 1, a.hp, a.out + job);
+    if (tid == 0) chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, res.best_mv);
     return;
   }
   const int vis_w = nx + 15;            // bytes of a ref row that exist
@@ -269,7 +281,10 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(FsArgs a) {
     }
   }
   b = block_best(b);
-  if (tid == 0) write_result(jb, b, nx > 0 ? nx : 1, 1, a.out + job);
+  if (tid == 0) {
+    const rv_fs_result res = write_result(jb, b, nx > 0 ? nx : 1, 1, a.out + job);
+    chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, res.best_mv);
+  }
 }
 
 }  // namespace rv
@@ -277,10 +292,12 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(FsArgs a) {
 using namespace rv;
 
 // Multi-reference form used by the replay driver: jobs [n_refs][n_per_ref],
-// job i searches refs[i / n_per_ref], all in one launch.
+// job i searches refs[i / n_per_ref], all in one launch; `next` (may be
+// null) chains each winner into the next stage's jobs.
 int rv_full_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
                          const rv_fs_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
-                         int step, int allow_hp, rv_fs_result *d_out, void *stream) {
+                         int step, int allow_hp, rv_fs_result *d_out, const ChainNext *next,
+                         void *stream) {
   if (!org || !refs || n_refs < 1 || n_refs > RV_DS_MAX_PRED || n_per_ref < 0 || blk_w < 4 ||
       blk_h < 4 || blk_w > 128 || blk_h > 128 || (blk_w & 3) || step < 1)
     return rv_set_error(RV_EINVAL, "rv_full_search_batch: bad arguments");
@@ -290,30 +307,26 @@ int rv_full_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
   const int n = n_refs * n_per_ref;
   if (n == 0) return RV_OK;
   hipStream_t s = rv_resolve_stream(stream);
-  if (!org->hbd && blk_w == 16 && blk_h == 16 && step == 1) {
-    FsArgs a;
-    memset(&a, 0, sizeof(a));
-    a.org = *org;
-    for (int k = 0; k < n_refs; k++) a.ref[k] = refs[k];
-    a.jobs = d_jobs;
-    a.out = d_out;
-    a.n = n;
-    a.n_per_ref = n_per_ref;
-    a.hp = allow_hp ? 1 : 0;
-    fs16_u8_kernel<<<(unsigned)((n + 7) / 8 * 8), kFsThreads, 0, s>>>(a);
-  } else {
-    for (int k = 0; k < n_refs; k++) {
-      const rv_fs_job *j = d_jobs + (size_t)k * n_per_ref;
-      rv_fs_result *o = d_out + (size_t)k * n_per_ref;
-      if (n_per_ref == 0) continue;
-      if (org->hbd)
-        fs_generic_kernel<uint16_t><<<n_per_ref, kFsThreads, 0, s>>>(
-            *org, refs[k], j, n_per_ref, blk_w, blk_h, step, allow_hp ? 1 : 0, o);
-      else
-        fs_generic_kernel<uint8_t><<<n_per_ref, kFsThreads, 0, s>>>(
-            *org, refs[k], j, n_per_ref, blk_w, blk_h, step, allow_hp ? 1 : 0, o);
-    }
-  }
+  FsArgs a;
+  memset(&a, 0, sizeof(a));
+  a.org = *org;
+  for (int k = 0; k < n_refs; k++) a.ref[k] = refs[k];
+  a.jobs = d_jobs;
+  a.out = d_out;
+  a.n = n;
+  a.n_per_ref = n_per_ref;
+  a.hp = allow_hp ? 1 : 0;
+  a.bw = blk_w;
+  a.bh = blk_h;
+  a.step = step;
+  if (next) a.next = *next;
+  const unsigned grid = (unsigned)((n + 7) / 8 * 8);
+  if (!org->hbd && blk_w == 16 && blk_h == 16 && step == 1)
+    fs16_u8_kernel<<<grid, kFsThreads, 0, s>>>(a);
+  else if (org->hbd)
+    fs_generic_kernel<uint16_t><<<grid, kFsThreads, 0, s>>>(a);
+  else
+    fs_generic_kernel<uint8_t><<<grid, kFsThreads, 0, s>>>(a);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }
@@ -324,5 +337,5 @@ extern "C" int rv_full_search_batch(const rv_plane *org, const rv_plane *ref,
                                     rv_fs_result *d_out, void *stream) {
   if (!ref) return rv_set_error(RV_EINVAL, "rv_full_search_batch: null ref");
   return rv_full_search_multi(org, ref, 1, d_jobs, n, blk_w, blk_h, step, allow_hp, d_out,
-                              stream);
+                              nullptr, stream);
 }

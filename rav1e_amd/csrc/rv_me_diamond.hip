@@ -24,6 +24,7 @@
 // candidate kernel.
 #include <string.h>
 
+#include "rv_chain.h"
 #include "rv_device.h"
 
 namespace rv {
@@ -90,6 +91,7 @@ struct DsArgs {
   rv_fs_result *out;
   int n, n_per_ref, w, h, subpel, satd, hp, bd;
   uint32_t *evals;  // optional: in-range candidate evaluations per job
+  ChainNext next;   // replay: feed the winner into the next stage's jobs
 };
 
 __device__ __forceinline__ void ds_write(const DsArgs &a, int job, rv_mv center,
@@ -550,7 +552,10 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) a.evals[job] = wevals[0] + wevals[1] + wevals[2] + wevals[3];
   }
-  if (threadIdx.x == 0) ds_write(a, job, center, center_cost);
+  if (threadIdx.x == 0) {
+    ds_write(a, job, center, center_cost);
+    chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, center);
+  }
 }
 
 // ============================ generic path =================================
@@ -759,6 +764,7 @@ __global__ __launch_bounds__(kDsThreads) void diamond_kernel(DsArgs a) {
   if (threadIdx.x == 0) {
     if (a.evals) a.evals[job] = evals;
     ds_write(a, job, center, center_cost);
+    chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, center);
   }
 }
 
@@ -799,7 +805,8 @@ using namespace rv;
 int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
                             const rv_ds_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
                             int subpixel, int use_satd, int allow_hp, int bit_depth,
-                            rv_fs_result *d_out, uint32_t *d_evals, void *stream) {
+                            rv_fs_result *d_out, uint32_t *d_evals, const ChainNext *next,
+                            void *stream) {
   auto p2 = [](int v) { return v >= 4 && v <= 128 && (v & (v - 1)) == 0; };
   if (!org || !refs || n_refs < 1 || n_refs > RV_DS_MAX_PRED || n_per_ref < 0 || !p2(blk_w) ||
       !p2(blk_h) || (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
@@ -825,6 +832,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
   a.hp = allow_hp ? 1 : 0;
   a.bd = bit_depth;
   a.evals = d_evals;
+  if (next) a.next = *next;
   hipStream_t s = rv_resolve_stream(stream);
   const bool fast = org->hbd ? try_fast<uint16_t>(a, s) : try_fast<uint8_t>(a, s);
   if (!fast) {
@@ -847,5 +855,5 @@ extern "C" int rv_diamond_search_batch(const rv_plane *org, const rv_plane *ref,
                                        rv_fs_result *d_out, void *stream) {
   if (!ref) return rv_set_error(RV_EINVAL, "rv_diamond_search_batch: null ref");
   return rv_diamond_search_multi(org, ref, 1, d_jobs, n, blk_w, blk_h, subpixel, use_satd,
-                                 allow_hp, bit_depth, d_out, nullptr, stream);
+                                 allow_hp, bit_depth, d_out, nullptr, nullptr, stream);
 }

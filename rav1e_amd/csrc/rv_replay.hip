@@ -18,28 +18,34 @@
 //   F5  8x8 importance SATD against reference 1 (compute_block_importances,
 //       src/api/internal.rs:823-1010)
 //
-// Every stage is one batched launch over all superblocks of the tile; the
-// glue between dependent stages (job lists built from the previous
-// stage's results) runs on the device, so a frame is a single stream of
-// launches with no host round trip.  The CPU baseline (oracle/orc_replay.c)
-// runs the same schedule and must produce the same result words.
+// Every stage is one batched launch over all superblocks of the tile.  The
+// glue between dependent stages is chained on the device (rv_chain.h): the
+// workgroup finishing a search writes its winner into the next stage's job
+// records, whose static fields are built once at creation.  A frame is 8
+// launches on one stream with no host round trip.  The CPU baseline
+// (oracle/orc_replay.c) runs the same schedule and must produce the same
+// result words.
 #include <string.h>
 
 #include <vector>
 
+#include "rv_chain.h"
 #include "rv_device.h"
 #include "rv_rdo.h"
 
-// rv_me.hip: every reference in one launch
+// rv_me.hip / rv_me_diamond.hip: every reference in one launch, per-job
+// evaluation counts, winners chained into the next stage's jobs
 int rv_full_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
                          const rv_fs_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
-                         int step, int allow_hp, rv_fs_result *d_out, void *stream);
-// rv_me_diamond.hip: every reference in one launch + per-job evaluation
-// counts
+                         int step, int allow_hp, rv_fs_result *d_out, const rv::ChainNext *next,
+                         void *stream);
 int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
                             const rv_ds_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
                             int subpixel, int use_satd, int allow_hp, int bit_depth,
-                            rv_fs_result *d_out, uint32_t *d_evals, void *stream);
+                            rv_fs_result *d_out, uint32_t *d_evals, const rv::ChainNext *next,
+                            void *stream);
+// rv_frame.hip: hres + qres (+ padding) in one launch
+int rv_plane_pyramid(const rv_plane *y, const rv_plane *h, const rv_plane *q, void *stream);
 
 namespace rv {
 
@@ -77,111 +83,6 @@ __host__ __device__ inline void adjust_bo(const Geo &g, int &bx, int &by,
 __host__ __device__ inline uint32_t pack_mv(rv_mv m) {
   return ((uint32_t)(uint16_t)m.row << 16) | (uint16_t)m.col;
 }
-__host__ __device__ inline rv_mv qfull(rv_mv m) {  // quantize_to_fullpel
-  return rv_mv{(int16_t)((m.row / 8) * 8), (int16_t)((m.col / 8) * 8)};
-}
-
-// ---- device glue -----------------------------------------------------------
-// F2 jobs from F1 results: one thread per (superblock, reference)
-__global__ void make_ss2_jobs(Geo g, const rv_fs_result *coarse, uint32_t lambda,
-                              rv_ds_job *jobs) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // r * nsb + sb
-  if (i >= g.nsb * g.R) return;
-  const int sb = i % g.nsb;
-  int bx = (sb % g.tw) * 16, by = (sb / g.tw) * 16;
-  adjust_bo(g, bx, by, 64, 64);
-  const int fbx = bx + g.tx0 * 16, fby = by + g.ty0 * 16;
-  int r[4];
-  mv_range(g, fbx, fby, 64, 64, r);
-  rv_ds_job j;
-  memset(&j, 0, sizeof(j));
-  j.po_x = fbx * 2;  // (bo << BLOCK_TO_PLANE_SHIFT) >> 1
-  j.po_y = fby * 2;
-  j.mvx_min = r[0] >> 1;
-  j.mvx_max = r[1] >> 1;
-  j.mvy_min = r[2] >> 1;
-  j.mvy_max = r[3] >> 1;
-  j.lambda = lambda;
-  j.n_pred = 1 + g.R;  // zero + the coarse MVs of every reference
-  j.pred[0] = rv_mv{0, 0};
-  for (int k = 0; k < g.R; k++) {
-    const rv_mv c = coarse[k * g.nsb + sb].best_mv;
-    const rv_mv cm{(int16_t)(c.row * 4), (int16_t)(c.col * 4)};
-    const rv_mv q = qfull(cm);
-    j.pred[1 + k] = rv_mv{(int16_t)(q.row >> 1), (int16_t)(q.col >> 1)};
-  }
-  jobs[i] = j;
-}
-
-// F3 full-pel jobs from F2 results
-__global__ void make_full_jobs(Geo g, const rv_fs_result *half, uint32_t lambda,
-                               rv_ds_job *jobs) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // r * nsb + sb
-  if (i >= g.nsb * g.R) return;
-  const int sb = i % g.nsb;
-  const int fbx = (sb % g.tw + g.tx0) * 16, fby = (sb / g.tw + g.ty0) * 16;
-  int r[4];
-  mv_range(g, fbx, fby, 64, 64, r);
-  rv_ds_job j;
-  memset(&j, 0, sizeof(j));
-  j.po_x = fbx * 4;
-  j.po_y = fby * 4;
-  j.mvx_min = r[0];
-  j.mvx_max = r[1];
-  j.mvy_min = r[2];
-  j.mvy_max = r[3];
-  j.lambda = lambda;
-  const rv_mv h = half[i].best_mv;
-  j.n_pred = 2;
-  j.pred[0] = rv_mv{0, 0};
-  j.pred[1] = qfull(rv_mv{(int16_t)(h.row * 2), (int16_t)(h.col * 2)});
-  jobs[i] = j;
-}
-
-// F3 sub-pel jobs: same block, the full-pel winner as the only predictor
-__global__ void make_subpel_jobs(int n, const rv_fs_result *full, rv_ds_job *jobs) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  rv_ds_job j = jobs[i];
-  j.n_pred = 1;
-  j.pred[0] = full[i].best_mv;
-  jobs[i] = j;
-}
-
-// predict_inter / get_params (src/predict.rs:267-283) for plane geometry p
-__device__ inline rv_mc_job mc_job_for(const rv_plane &p, int po_x, int po_y,
-                                       rv_mv mv, int dst_x, int dst_y) {
-  const int ys = 3 + p.ydec, xs = 3 + p.xdec;
-  const int roff = (int)mv.row >> ys, coff = (int)mv.col >> xs;
-  rv_mc_job m;
-  m.row_frac = ((int)mv.row - (roff << ys)) << (4 - ys);
-  m.col_frac = ((int)mv.col - (coff << xs)) << (4 - xs);
-  m.src_x = clampi(po_x + coff - 3, -p.xorigin, p.width) + 3;
-  m.src_y = clampi(po_y + roff - 3, -p.yorigin, p.height) + 3;
-  m.dst_x = dst_x;
-  m.dst_y = dst_y;
-  return m;
-}
-
-// F4 MC jobs: candidate c = 2 * ref + k (k 0: sub-pel MV, 1: zero MV).
-// Candidate c of superblock (sx, sy) predicts into the tall scratch plane
-// at (sx * bw, (c * th + sy) * bh).  One array per reference and plane.
-__global__ void make_mc_jobs(Geo g, const rv_fs_result *sub, rv_plane luma,
-                             rv_plane chroma, rv_mc_job *ljobs, rv_mc_job *cjobs) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over nsb * C
-  if (i >= g.nsb * g.C) return;
-  const int c = i / g.nsb, sb = i - c * g.nsb;
-  const int r = c >> 1, k = c & 1;
-  const int sx = sb % g.tw, sy = sb / g.tw;
-  const rv_mv mv = k ? rv_mv{0, 0} : sub[r * g.nsb + sb].best_mv;
-  const int px = (sx + g.tx0) * kSb, py = (sy + g.ty0) * kSb;
-  // job arrays are grouped by reference: [r][k][sb]
-  const int o = (r * 2 + k) * g.nsb + sb;
-  ljobs[o] = mc_job_for(luma, px, py, mv, sx * kSb, (c * g.th + sy) * kSb);
-  cjobs[o] = mc_job_for(chroma, px >> chroma.xdec, py >> chroma.ydec, mv, sx * g.cw,
-                        (c * g.th + sy) * g.ch);
-}
-
 // Block-level reduction helper: one atomic per workgroup (never one per
 // wavefront: same-address atomics serialise, MI355X_MICROARCH.md).
 __device__ inline void block_atomic_add(uint64_t s, unsigned long long *out) {
@@ -213,9 +114,10 @@ __global__ void coeff_checksum(const int32_t *packed, int64_t total, int per_blo
 __global__ __launch_bounds__(64) void score_candidates(
     Geo g, const int64_t *lmom, const uint64_t *usse, const uint64_t *vsse, int lsub, int csub,
     const rv_fs_result *coarse, const rv_fs_result *half, const rv_fs_result *full,
-    const rv_fs_result *sub, uint64_t *words) {
+    const rv_fs_result *sub, uint64_t *words, unsigned long long *imp_sum) {
   const int sb = blockIdx.x;
   const int lane = threadIdx.x;
+  if (sb == 0 && lane == 0) *imp_sum = 0;  // F5 accumulates after this launch
   uint64_t best = ~0ull;
   int best_c = 0;
   for (int c = 0; c < g.C; c++) {
@@ -245,29 +147,32 @@ __global__ __launch_bounds__(64) void score_candidates(
   }
 }
 
-// F5 jobs: every 8x8 luma block of the tile inside the frame, against
-// reference 1 at the full-pel part of its superblock's sub-pel MV.
-__global__ void make_imp_jobs(Geo g, const rv_fs_result *sub, rv_dist_job *jobs,
-                              int nbx, int nby) {
+// F5: get_satd of every 8x8 luma block of the tile inside the frame against
+// reference 1 at the full-pel part of its superblock's sub-pel MV
+// (compute_block_importances, src/api/internal.rs:823-1010), summed.  One
+// lane per block; the job is computed in place.
+template <typename Px>
+__global__ __launch_bounds__(256) void importance_kernel(Geo g, rv_plane org, rv_plane ref,
+                                                          const rv_fs_result *sub, int nbx,
+                                                          int nby, unsigned long long *sum) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nbx * nby) return;
-  const int bx = i % nbx, by = i / nbx;
-  const int sb = (by / 8) * g.tw + (bx / 8);
-  const rv_mv mv = sub[sb].best_mv;  // reference 1 (ref-major index 0)
-  const int x = g.tx0 * kSb + bx * 8, y = g.ty0 * kSb + by * 8;
-  rv_dist_job j;
-  j.org_x = x;
-  j.org_y = y;
-  j.ref_x = x + ((int)mv.col >> 3);
-  j.ref_y = y + ((int)mv.row >> 3);
-  jobs[i] = j;
-}
-
-__global__ void sum_u32(const uint32_t *v, int n, unsigned long long *out) {
-  uint64_t s = 0;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    s += v[i];
-  block_atomic_add(s, out);
+  uint64_t v = 0;
+  if (i < nbx * nby) {
+    const int bx = i % nbx, by = i / nbx;
+    const rv_mv mv = sub[(by / 8) * g.tw + (bx / 8)].best_mv;  // reference 1
+    const int x = g.tx0 * kSb + bx * 8, y = g.ty0 * kSb + by * 8;
+    const Px *o = plane_ptr<Px>(org, x, y);
+    const Px *r = plane_ptr<Px>(ref, x + ((int)mv.col >> 3), y + ((int)mv.row >> 3));
+    int32_t d[64];
+#pragma unroll
+    for (int rr = 0; rr < 8; rr++)
+#pragma unroll
+      for (int cc = 0; cc < 8; cc++)
+        d[rr * 8 + cc] = (int32_t)o[(int64_t)rr * org.stride + cc] -
+                         (int32_t)r[(int64_t)rr * ref.stride + cc];
+    v = (satd_chunk<8>(d) + 4) >> 3;  // (sum + (1 << ln >> 1)) >> ln, ln = 3
+  }
+  block_atomic_add(v, sum);
 }
 
 // Sum of the reconstructed pixels of a plane (all candidates; results time).
@@ -304,21 +209,21 @@ struct rv_replay {
   std::vector<void *> allocs;
   rv_fs_job *fs_jobs[3] = {nullptr, nullptr, nullptr};  // per scale 1, 2, 4
   rv_fs_result *coarse, *half, *full, *sub;
-  rv_ds_job *ds_jobs;
+  // chained search jobs (static fields built at creation, predictors
+  // written by the previous stage, rv_chain.h)
+  rv_ds_job *jobs_half, *jobs_full, *jobs_sub;
   rv_mc_job *l_mc, *c_mc;
   rv_tx_job *l_tx, *c_tx;
-  rv_dist_job *l_dist, *c_dist, *imp_jobs;
   int32_t *l_packed, *c_packed;
   int64_t *l_mom;
   uint64_t *u_sse, *v_sse, *words;
-  uint32_t *imp_satd;
   unsigned long long *tail;  // [coeff csum, recon csum, imp satd sum]
-  int n_ctx, n_imp, imp_bx, imp_by, lsub, csub;
-  // Event ring: frame f records into set f % kRing (0..6 stage bounds,
-  // 7..14 kernel brackets), so per-kernel times can be summed over a whole
-  // timed run without a host sync per frame.
+  int n_imp, imp_bx, imp_by, lsub, csub;
+  // Event ring: frame f records into set f % kRing (stage bounds and
+  // kernel brackets, see rv_replay_frame), so per-kernel times can be
+  // summed over a whole timed run without a host sync per frame.
   static constexpr int kRing = 64;
-  static constexpr int kEv = 20;
+  static constexpr int kEv = 9;
   hipEvent_t evs[kRing][kEv];
   hipEvent_t *ev;
   long frames = 0;
@@ -399,10 +304,64 @@ int build_static_jobs(rv_replay *r) {
                   hipMemcpyHostToDevice) != hipSuccess)
       return RV_EHIP;
   }
-  // F4 transform / distortion jobs (static: positions only)
+  // F2 / F3 diamond jobs: static fields (positions, MV ranges, lambdas);
+  // the predictors are chained in by the previous stage each frame
+  const uint32_t lambda2 = (uint32_t)(r->me_lambda * 256.0 / 4.0 * 0.125);
+  const uint32_t lambda1 = (uint32_t)(r->me_lambda * 256.0 * 0.5);
+  std::vector<rv_ds_job> jh(g.nsb * g.R), jf(g.nsb * g.R), js(g.nsb * g.R);
+  for (int k = 0; k < g.R; k++)
+    for (int sb = 0; sb < g.nsb; sb++) {
+      const int i = k * g.nsb + sb;
+      // me_ss2 (src/me.rs:470-519): adjusted 64x64 origin at 1/2 res
+      int bx = (sb % g.tw) * 16, by = (sb / g.tw) * 16;
+      adjust_bo(g, bx, by, 64, 64);
+      int fbx = bx + g.tx0 * 16, fby = by + g.ty0 * 16;
+      int mr[4];
+      mv_range(g, fbx, fby, 64, 64, mr);
+      rv_ds_job j;
+      memset(&j, 0, sizeof(j));
+      j.po_x = fbx * 2;  // (bo << BLOCK_TO_PLANE_SHIFT) >> 1
+      j.po_y = fby * 2;
+      j.mvx_min = mr[0] >> 1;
+      j.mvx_max = mr[1] >> 1;
+      j.mvy_min = mr[2] >> 1;
+      j.mvy_max = mr[3] >> 1;
+      j.lambda = lambda2;
+      j.n_pred = 1 + g.R;  // zero + the coarse MV of every reference
+      jh[i] = j;
+      // full resolution (motion_estimation, src/me.rs:193-285)
+      fbx = (sb % g.tw + g.tx0) * 16;
+      fby = (sb / g.tw + g.ty0) * 16;
+      mv_range(g, fbx, fby, 64, 64, mr);
+      memset(&j, 0, sizeof(j));
+      j.po_x = fbx * 4;
+      j.po_y = fby * 4;
+      j.mvx_min = mr[0];
+      j.mvx_max = mr[1];
+      j.mvy_min = mr[2];
+      j.mvy_max = mr[3];
+      j.lambda = lambda1;
+      j.n_pred = 2;  // zero + the half-res winner
+      jf[i] = j;
+      j.n_pred = 1;  // the full-pel winner
+      js[i] = j;
+    }
+  // F4 MC jobs of the zero-MV candidates (k = 1); the sub-pel MV ones
+  // (k = 0) are chained in by the sub-pel search
+  RvFrameSlot &cur = r->slots[0];
+  std::vector<rv_mc_job> lmc(g.nctx), cmc(g.nctx);
+  for (int c = 0; c < g.C; c++)
+    for (int sb = 0; sb < g.nsb; sb++) {
+      const int o = c * g.nsb + sb;
+      const int sx = sb % g.tw, sy = sb / g.tw;
+      const int px = (sx + g.tx0) * kSb, py = (sy + g.ty0) * kSb;
+      lmc[o] = mc_job_for(cur.y, px, py, rv_mv{0, 0}, sx * kSb, (c * g.th + sy) * kSb);
+      cmc[o] = mc_job_for(cur.u, px >> g.xdec, py >> g.ydec, rv_mv{0, 0}, sx * g.cw,
+                          (c * g.th + sy) * g.ch);
+    }
+  // F4 transform jobs (static: positions only)
   const int ntx_c = (g.cw / 32) * (g.ch / 32);  // 32x32 chroma tx per plane
   std::vector<rv_tx_job> ltx(g.nctx), ctx_(g.nctx * ntx_c);
-  std::vector<rv_dist_job> ld(g.nctx), cd(g.nctx);
   for (int c = 0; c < g.C; c++)
     for (int sb = 0; sb < g.nsb; sb++) {
       const int o = c * g.nsb + sb;
@@ -410,10 +369,8 @@ int build_static_jobs(rv_replay *r) {
       const int px = (sx + g.tx0) * kSb, py = (sy + g.ty0) * kSb;
       const int tx = sx * kSb, ty = (c * g.th + sy) * kSb;
       ltx[o] = rv_tx_job{px, py, tx, ty};
-      ld[o] = rv_dist_job{px, py, tx, ty};
       const int cpx = px >> g.xdec, cpy = py >> g.ydec;
       const int ctx0 = sx * g.cw, cty0 = (c * g.th + sy) * g.ch;
-      cd[o] = rv_dist_job{cpx, cpy, ctx0, cty0};
       for (int t = 0; t < ntx_c; t++) {
         const int ox = (t % (g.cw / 32)) * 32, oy = (t / (g.cw / 32)) * 32;
         ctx_[o * ntx_c + t] = rv_tx_job{cpx + ox, cpy + oy, ctx0 + ox, cty0 + oy};
@@ -428,8 +385,9 @@ int build_static_jobs(rv_replay *r) {
                : RV_EHIP;
   };
   int e;
-  if ((e = upload(ltx, r->l_tx)) || (e = upload(ctx_, r->c_tx)) || (e = upload(ld, r->l_dist)) ||
-      (e = upload(cd, r->c_dist)))
+  if ((e = upload(ltx, r->l_tx)) || (e = upload(ctx_, r->c_tx)) || (e = upload(jh, r->jobs_half)) ||
+      (e = upload(jf, r->jobs_full)) || (e = upload(js, r->jobs_sub)) || (e = upload(lmc, r->l_mc)) ||
+      (e = upload(cmc, r->c_mc)))
     return e;
   return RV_OK;
 }
@@ -533,9 +491,6 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->half = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
   r->full = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
   r->sub = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
-  r->ds_jobs = (rv_ds_job *)dalloc(r, nr * sizeof(rv_ds_job));
-  r->l_mc = (rv_mc_job *)dalloc(r, g.nctx * sizeof(rv_mc_job));
-  r->c_mc = (rv_mc_job *)dalloc(r, g.nctx * sizeof(rv_mc_job));
   r->l_packed = (int32_t *)dalloc(r, (size_t)g.nctx * 1024 * 4);
   r->c_packed = (int32_t *)dalloc(r, (size_t)g.nctx * ntx_c * 1024 * 4 * 2);
   r->lsub = (kSb / 8) * (kSb / 8);
@@ -550,11 +505,9 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->imp_bx = vis_w / 8;
   r->imp_by = vis_h / 8;
   r->n_imp = r->imp_bx * r->imp_by;
-  r->imp_jobs = (rv_dist_job *)dalloc(r, (size_t)r->n_imp * sizeof(rv_dist_job));
-  r->imp_satd = (uint32_t *)dalloc(r, (size_t)r->n_imp * 4);
   r->tail = (unsigned long long *)dalloc(r, 4 * 8);
   for (int f = 0; f < rv_replay::kRing; f++)
-    for (int i = 0; i < rv_replay::kEv; i++) ok = ok && hipEventCreate(&r->evs[f][i]) == hipSuccess;
+    for (int i = 0; i < rv_replay::kEv; i++) ok = ok && hipEventCreateWithFlags(&r->evs[f][i], hipEventDisableSystemFence) == hipSuccess;
   const size_t ev_bytes = (size_t)rv_replay::kRing * 2 * nr * 4;
   r->ds_evals = (uint32_t *)dalloc(r, ev_bytes);
   ok = ok && r->ds_evals && hipMemsetAsync(r->ds_evals, 0, ev_bytes, r->stream) == hipSuccess;
@@ -590,16 +543,17 @@ int rv_replay_set_frame(rv_replay *r, int slot, const void *host_yuv) {
   RV_R(upload_plane(r, s.u, p));
   p += (size_t)s.u.width * s.u.height * px;
   RV_R(upload_plane(r, s.v, p));
-  RV_R(rv_plane_downsample(&s.hres, &s.y, r->stream));
-  RV_R(rv_plane_downsample(&s.qres, &s.hres, r->stream));
+  RV_R(rv_plane_pyramid(&s.y, &s.hres, &s.qres, r->stream));
   RV_H(hipStreamSynchronize(r->stream));
   return RV_OK;
 }
 
-// Event layout per frame (ring slot): 0..6 stage bounds F0..F5; then
-// kernel brackets [7,8] F3 full-pel diamond, [9,10] F3 sub-pel diamond,
-// [11,12] F4 fused candidates (luma + chroma, one launch).
-// F1 ([1,2]) holds only the full-search launches.
+// Event layout per frame (ring slot): e[0..6] = stage bounds F0..F5 end;
+// e[7] splits F3 between the full-pel and the sub-pel diamond launch, e[8]
+// splits F4 between the fused candidate launch and the scoring launch.
+// Every stage is one launch except those two, so the stage bounds are also
+// the kernel brackets.  The events are created without the system-scope
+// fence (they only time).
 int rv_replay_frame(rv_replay *r, int me_range_scale) {
   if (!r || (me_range_scale != 1 && me_range_scale != 2 && me_range_scale != 4))
     return rv_set_error(RV_EINVAL, "rv_replay_frame: bad me_range_scale");
@@ -607,53 +561,59 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   hipStream_t st = r->stream;
   RvFrameSlot &cur = r->slots[0];
   const int nr = g.nsb;  // jobs per reference
-  const int T = 256;
-  auto blocks = [](int64_t n) { return (unsigned)((n + 255) / 256); };
   const int si = me_range_scale == 1 ? 0 : me_range_scale == 2 ? 1 : 2;
-  const uint32_t lambda2 = (uint32_t)(r->me_lambda * 256.0 / 4.0 * 0.125);
-  const uint32_t lambda1 = (uint32_t)(r->me_lambda * 256.0 * 0.5);
-  rv_plane refs_y[RV_DS_MAX_PRED], refs_h[RV_DS_MAX_PRED];
+  rv_plane refs_y[RV_DS_MAX_PRED], refs_h[RV_DS_MAX_PRED], refs_q[RV_DS_MAX_PRED];
   for (int k = 0; k < g.R; k++) {
     refs_y[k] = r->slots[1 + k].y;
     refs_h[k] = r->slots[1 + k].hres;
+    refs_q[k] = r->slots[1 + k].qres;
   }
   const int slot = (int)(r->frames % rv_replay::kRing);
   uint32_t *ev_full = r->ds_evals + (size_t)slot * 2 * nr * g.R;
   uint32_t *ev_sub = ev_full + (size_t)nr * g.R;
+  ChainNext to_half{}, to_full{}, to_sub{}, to_mc{};
+  to_half.mode = kChainCoarseToHalf;
+  to_half.jobs = r->jobs_half;
+  to_full.mode = kChainHalfToFull;
+  to_full.jobs = r->jobs_full;
+  to_sub.mode = kChainFullToSub;
+  to_sub.jobs = r->jobs_sub;
+  to_mc.mode = kChainSubToMc;
+  to_mc.l_mc = r->l_mc;
+  to_mc.c_mc = r->c_mc;
+  to_mc.luma = cur.y;
+  to_mc.chroma = cur.u;
+  to_mc.tw = g.tw;
+  to_mc.th = g.th;
+  to_mc.tx0 = g.tx0;
+  to_mc.ty0 = g.ty0;
+  to_mc.cw = g.cw;
+  to_mc.ch = g.ch;
 
-  r->ev = r->evs[slot];
+  hipEvent_t *e = r->evs[slot];
+  r->ev = e;
   r->frames++;
-  RV_H(hipEventRecord(r->ev[0], st));
-  RV_H(hipMemsetAsync(r->tail + 2, 0, 8, st));
-  // F0 (encode_frame, src/encoder.rs:3382-3385)
-  RV_R(rv_plane_downsample(&cur.hres, &cur.y, st));
-  RV_R(rv_plane_downsample(&cur.qres, &cur.hres, st));
-  RV_H(hipEventRecord(r->ev[1], st));
-  // F1 coarse full search, every reference in one launch
-  rv_plane refs_q[RV_DS_MAX_PRED];
-  for (int k = 0; k < g.R; k++) refs_q[k] = r->slots[1 + k].qres;
+  RV_H(hipEventRecord(e[0], st));
+  // F0 hres + qres of the input (encode_frame, src/encoder.rs:3382-3385)
+  RV_R(rv_plane_pyramid(&cur.y, &cur.hres, &cur.qres, st));
+  RV_H(hipEventRecord(e[1], st));
+  // F1 coarse full search, every reference in one launch -> F2 predictors
   RV_R(rv_full_search_multi(&cur.qres, refs_q, g.R, r->fs_jobs[si], nr, 16, 16, 1, 0, r->coarse,
-                            st));
-  RV_H(hipEventRecord(r->ev[2], st));  // = the full-search kernel bracket
-  // F2 half-res diamond, every reference in one launch
-  make_ss2_jobs<<<blocks(nr * g.R), T, 0, st>>>(g, r->coarse, lambda2, r->ds_jobs);
-  RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->ds_jobs, nr, 32, 32, 0, 0, 0, g.bd,
-                               r->half, nullptr, st));
-  RV_H(hipEventRecord(r->ev[3], st));
-  // F3 full-res full-pel + sub-pel diamond (speed 10: SAD, no hp)
-  make_full_jobs<<<blocks(nr * g.R), T, 0, st>>>(g, r->half, lambda1, r->ds_jobs);
-  RV_H(hipEventRecord(r->ev[7], st));
-  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->ds_jobs, nr, 64, 64, 0, 0, 0, g.bd,
-                               r->full, ev_full, st));
-  RV_H(hipEventRecord(r->ev[8], st));
-  make_subpel_jobs<<<blocks(nr * g.R), T, 0, st>>>(nr * g.R, r->full, r->ds_jobs);
-  RV_H(hipEventRecord(r->ev[9], st));
-  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->ds_jobs, nr, 64, 64, 1, 0, 0, g.bd,
-                               r->sub, ev_sub, st));
-  RV_H(hipEventRecord(r->ev[10], st));
-  RV_H(hipEventRecord(r->ev[4], st));
-  // F4 RDO candidates: one fused launch for luma, one for both chroma planes
-  make_mc_jobs<<<blocks(g.nctx), T, 0, st>>>(g, r->sub, cur.y, cur.u, r->l_mc, r->c_mc);
+                            &to_half, st));
+  RV_H(hipEventRecord(e[2], st));
+  // F2 half-res diamond -> F3 full-pel predictors
+  RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half, nr, 32, 32, 0, 0, 0, g.bd,
+                               r->half, nullptr, &to_full, st));
+  RV_H(hipEventRecord(e[3], st));
+  // F3 full-res full-pel diamond -> sub-pel predictor; sub-pel diamond
+  // (speed 10: SAD, no hp) -> the F4 MC jobs of the sub-pel candidates
+  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full, nr, 64, 64, 0, 0, 0, g.bd,
+                               r->full, ev_full, &to_sub, st));
+  RV_H(hipEventRecord(e[7], st));
+  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub, nr, 64, 64, 1, 0, 0, g.bd,
+                               r->sub, ev_sub, &to_mc, st));
+  RV_H(hipEventRecord(e[4], st));
+  // F4 RDO candidates: luma + both chroma planes in one fused launch
   const int ntx_c = (g.cw / 32) * (g.ch / 32);
   const int nct = g.nctx * ntx_c;
   {
@@ -691,18 +651,24 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
     ca.mb_h = g.ch;
     ca.sub_w = (g.cw < 8 ? g.cw : 8) >> g.xdec;
     ca.sub_h = (g.ch < 8 ? g.ch : 8) >> g.ydec;
-    RV_H(hipEventRecord(r->ev[11], st));
     RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
-    RV_H(hipEventRecord(r->ev[12], st));
   }
+  RV_H(hipEventRecord(e[8], st));
   score_candidates<<<g.nsb, 64, 0, st>>>(g, r->l_mom, r->u_sse, r->v_sse, r->lsub, r->csub,
-                                         r->coarse, r->half, r->full, r->sub, r->words);
-  RV_H(hipEventRecord(r->ev[5], st));
+                                         r->coarse, r->half, r->full, r->sub, r->words,
+                                         r->tail + 2);
+  RV_H(hipEventRecord(e[5], st));
   // F5 importance SATD against reference 1
-  make_imp_jobs<<<blocks(r->n_imp), T, 0, st>>>(g, r->sub, r->imp_jobs, r->imp_bx, r->imp_by);
-  RV_R(rv_satd_batch(&cur.y, &r->slots[1].y, r->imp_jobs, r->n_imp, 8, 8, r->imp_satd, st));
-  sum_u32<<<256, T, 0, st>>>(r->imp_satd, r->n_imp, r->tail + 2);
-  RV_H(hipEventRecord(r->ev[6], st));
+  {
+    const unsigned nb = (unsigned)((r->n_imp + 255) / 256);
+    if (g.hbd)
+      importance_kernel<uint16_t><<<nb, 256, 0, st>>>(g, cur.y, r->slots[1].y, r->sub, r->imp_bx,
+                                                      r->imp_by, r->tail + 2);
+    else
+      importance_kernel<uint8_t><<<nb, 256, 0, st>>>(g, cur.y, r->slots[1].y, r->sub, r->imp_bx,
+                                                     r->imp_by, r->tail + 2);
+  }
+  RV_H(hipEventRecord(e[6], st));
   RV_H(hipGetLastError());
   return RV_OK;
 }
@@ -752,9 +718,12 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
       RV_H(hipEventElapsedTime(&ms, e[i], e[i + 1]));
       ms_out[n++] += ms;
     }
-    for (int i = 7; i < 13 && n < cap; i += 2) {  // kernel brackets
+    // kernel brackets: F3 full-pel diamond, F3 sub-pel diamond, F4 fused
+    // candidate launch
+    const int br[3][2] = {{3, 7}, {7, 4}, {4, 8}};
+    for (int i = 0; i < 3 && n < cap; i++) {
       float ms = 0.f;
-      RV_H(hipEventElapsedTime(&ms, e[i], e[i + 1]));
+      RV_H(hipEventElapsedTime(&ms, e[br[i][0]], e[br[i][1]]));
       ms_out[n++] += ms;
     }
   }
