@@ -194,6 +194,8 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(FsArgs a) {
   pb = (pb / kTileRows) * kTileRows;
 
   Best b{~0ull, 0xffffffffu};
+  uint64_t bkey = ~0ull;  // (u32 cost << 32 | index) while costs fit u32
+  const bool small_cost = jb.lambda < (1u << 25);
   const uint8_t *rbase = plane_ptr<uint8_t>(ref, jb.x_lo, jb.y_lo);
   for (int y0 = 0; y0 < ny; y0 += pb) {
     const int rows = ny - y0 < pb ? ny - y0 : pb;
@@ -264,6 +266,25 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(FsArgs a) {
           }
         }
       }
+      // cost = 256 * sad + rate * lambda (get_mv_rate, src/me.rs:1006-1021):
+      // the rate splits into a row part per tile row and a column part per
+      // tile column, so a tile needs 24 diff_to_rate instead of 128.  For a
+      // 16x16 u8 block 256 * sad < 2^24, so with lambda < 2^25 the cost
+      // fits u32 and (cost, raster index) packs into one u64 key whose
+      // minimum is the reference's first strict minimum.
+      int rr0[kTileRows], rr1[kTileRows], rc0[4], rc1[4];
+#pragma unroll
+      for (int c = 0; c < kTileRows; c++) {
+        const int16_t row = (int16_t)(8 * (jb.y_lo + y0 + cy0 + c - jb.po_y));
+        rr0[c] = diff_to_rate((int16_t)(row - jb.pmv[0].row), a.hp);
+        rr1[c] = diff_to_rate((int16_t)(row - jb.pmv[1].row), a.hp);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int16_t col = (int16_t)(8 * (jb.x_lo + 4 * tcx + j - jb.po_x));
+        rc0[j] = diff_to_rate((int16_t)(col - jb.pmv[0].col), a.hp);
+        rc1[j] = diff_to_rate((int16_t)(col - jb.pmv[1].col), a.hp);
+      }
 #pragma unroll
       for (int c = 0; c < kTileRows; c++) {
         const int iy = y0 + cy0 + c;
@@ -271,15 +292,23 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(FsArgs a) {
         for (int j = 0; j < 4; j++) {
           const int ix = 4 * tcx + j;
           if (ix < nx && cy0 + c < rows) {
-            const uint64_t cost =
-                cand_cost(acc[c][j], jb.x_lo + ix, jb.y_lo + iy, jb, a.hp);
+            const uint32_t r1 = rr0[c] + rc0[j], r2 = rr1[c] + rc1[j];
+            const uint32_t rate = r1 < r2 + 1 ? r1 : r2 + 1;
             const uint32_t idx = (uint32_t)(iy * nx + ix);
-            if (better(cost, idx, b)) b = Best{cost, idx};
+            if (small_cost) {
+              const uint64_t key =
+                  ((uint64_t)((acc[c][j] << 8) + rate * jb.lambda) << 32) | idx;
+              bkey = key < bkey ? key : bkey;
+            } else {
+              const uint64_t cost = 256ull * acc[c][j] + (uint64_t)rate * jb.lambda;
+              if (better(cost, idx, b)) b = Best{cost, idx};
+            }
           }
         }
       }
     }
   }
+  if (bkey != ~0ull && better(bkey >> 32, (uint32_t)bkey, b)) b = Best{bkey >> 32, (uint32_t)bkey};
   b = block_best(b);
   if (tid == 0) {
     const rv_fs_result res = write_result(jb, b, nx > 0 ? nx : 1, 1, a.out + job);
