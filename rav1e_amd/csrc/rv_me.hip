@@ -7,7 +7,7 @@
 // candidates and the workgroup reduces (cost, raster index)
 // lexicographically, which selects the same candidate.
 //
-// Fast path (u8, 16x16 block, step 1 -- the quarter-resolution search of
+// Fast path (16x16 block, step 1, u8 and u16 -- the quarter-resolution search of
 // every 64x64 superblock, estimate_motion_ss4 src/me.rs:1023-1075): the
 // search window is staged in LDS in bands, the 16x16 source block lives in
 // 64 VGPRs, and each lane computes a 4-wide x 8-tall candidate tile with
@@ -159,12 +159,32 @@ __global__ __launch_bounds__(kFsThreads) void fs_generic_kernel(FsArgs a) {
   if (threadIdx.x == 0) chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, res.best_mv);
 }
 
-// ---- fast path: u8, 16x16, step 1 ---------------------------------------
-constexpr int kTileRows = 8;         // candidate rows per lane
-constexpr int kLdsWords = 7 * 1024;  // 28 KiB search band: 5 workgroups per CU
+// ---- fast path: 16x16, step 1 (u8 and u16) --------------------------------
+constexpr int kTileRows = 8;  // candidate rows per lane
 
-__global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(FsArgs a) {
-  __shared__ uint32_t band[kLdsWords];
+template <typename Px>
+struct Fs16 {
+  static constexpr int B = (int)sizeof(Px);
+  static constexpr int ODW = 16 * B / 4;        // source dwords per row
+  static constexpr int WV = (4 + 16) * B / 4;   // band dwords a 4-wide tile row touches
+  // LDS search band: 28 KiB for u8 (5 workgroups per CU), 56 KiB for u16
+  // (its rows are twice as long; keeps ~40 candidate rows per band)
+  static constexpr int kLdsWords = B == 1 ? 7 * 1024 : 14 * 1024;
+};
+
+template <typename Px>
+__device__ __forceinline__ uint32_t sad_px(uint32_t a, uint32_t b, uint32_t acc) {
+  if constexpr (sizeof(Px) == 1)
+    return __builtin_amdgcn_sad_u8(a, b, acc);
+  else
+    return __builtin_amdgcn_sad_u16(a, b, acc);
+}
+
+template <typename Px>
+__global__ __launch_bounds__(kFsThreads) void fs16_kernel(FsArgs a) {
+  using G = Fs16<Px>;
+  constexpr int B = G::B, ODW = G::ODW, WV = G::WV;
+  __shared__ uint32_t band[G::kLdsWords];
   const int job = fs_job_index();
   if (job >= a.n) return;
   const rv_fs_job jb = a.jobs[job];
@@ -173,30 +193,30 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(FsArgs a) {
   const int ny = jb.y_hi >= jb.y_lo ? jb.y_hi - jb.y_lo + 1 : 0;
   const int tid = threadIdx.x;
 
-  // 16x16 source block -> LDS (64 dwords); every lane reads the same row,
-  // so the reads are broadcasts and the VGPRs stay with the accumulators
-  __shared__ uint4 orgs[16];
-  if (tid < 64) {
-    const uint8_t *o = plane_ptr<uint8_t>(a.org, jb.po_x, jb.po_y);
-    reinterpret_cast<uint32_t *>(orgs)[tid] =
-        load_u32_unaligned(o + (int64_t)(tid >> 2) * a.org.stride + 4 * (tid & 3));
+  // 16x16 source block -> LDS; every lane reads the same row, so the reads
+  // are broadcasts and the VGPRs stay with the accumulators
+  __shared__ uint32_t orgs[16 * ODW];
+  if (tid < 16 * ODW) {
+    const uint8_t *o = (const uint8_t *)plane_ptr<Px>(a.org, jb.po_x, jb.po_y);
+    orgs[tid] = load_u32_unaligned(o + (int64_t)(tid / ODW) * a.org.stride * B + 4 * (tid % ODW));
   }
 
-  const int tx_n = (nx + 3) >> 2;       // 4-wide candidate columns
-  const int rw = tx_n + 4;              // band row length in dwords
-  if (rw * (2 * kTileRows + 15) > kLdsWords) {  // window too wide for a band
-    const rv_fs_result res = fs_generic_body<uint8_t>(a.org, ref, jb, 16, 16, 1, a.hp, a.out + job);
+  const int tx_n = (nx + 3) >> 2;        // 4-wide candidate columns
+  const int rw = tx_n * B + WV - B;      // band row length in dwords
+  if (rw * (2 * kTileRows + 15) > G::kLdsWords) {  // window too wide for a band
+    const rv_fs_result res = fs_generic_body<Px>(a.org, ref, jb, 16, 16, 1, a.hp, a.out + job);
     if (tid == 0) chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, res.best_mv);
     return;
   }
-  const int vis_w = nx + 15;            // bytes of a ref row that exist
-  int pb = kLdsWords / rw - (kTileRows + 15);  // candidate rows per band
+  const int vis_w = (nx + 15) * B;       // bytes of a ref row that exist
+  int pb = G::kLdsWords / rw - (kTileRows + 15);  // candidate rows per band
   pb = (pb / kTileRows) * kTileRows;
 
   Best b{~0ull, 0xffffffffu};
   uint64_t bkey = ~0ull;  // (u32 cost << 32 | index) while costs fit u32
   const bool small_cost = jb.lambda < (1u << 25);
-  const uint8_t *rbase = plane_ptr<uint8_t>(ref, jb.x_lo, jb.y_lo);
+  const uint8_t *rbase = (const uint8_t *)plane_ptr<Px>(ref, jb.x_lo, jb.y_lo);
+  const int64_t rstride = (int64_t)ref.stride * B;
   for (int y0 = 0; y0 < ny; y0 += pb) {
     const int rows = ny - y0 < pb ? ny - y0 : pb;
     const int lrows = rows + 15;  // ref rows with data
@@ -214,7 +234,7 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(FsArgs a) {
         const int r = i / rw, c = 4 * (i - r * rw);
         uint32_t x = 0;
         if (i < total && r < lrows) {
-          const uint8_t *p = rbase + (int64_t)(y0 + r) * ref.stride + c;
+          const uint8_t *p = rbase + (int64_t)(y0 + r) * rstride + c;
           if (c + 3 < vis_w) {
             x = load_u32_unaligned(p);
           } else {
@@ -239,38 +259,54 @@ __global__ __launch_bounds__(kFsThreads) void fs16_u8_kernel(FsArgs a) {
       for (int c = 0; c < kTileRows; c++)
 #pragma unroll
         for (int j = 0; j < 4; j++) acc[c][j] = 0;
-      const uint32_t *bp = band + cy0 * rw + tcx;
+      const uint32_t *bp = band + cy0 * rw + tcx * B;
 #pragma unroll 1
       for (int yy = 0; yy < kTileRows + 15; yy++) {
-        uint32_t wv[5];
+        uint32_t wv[WV];
 #pragma unroll
-        for (int i = 0; i < 5; i++) wv[i] = bp[yy * rw + i];
-        uint32_t sh[4][4];
+        for (int i = 0; i < WV; i++) wv[i] = bp[yy * rw + i];
+        // sh[j][i]: reference dword under source dword i for candidate
+        // column j (u8: byte shift j; u16: dword j/2, half-word shift j&1)
+        uint32_t sh[4][ODW];
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          sh[0][i] = wv[i];
-          sh[1][i] = __builtin_amdgcn_alignbyte(wv[i + 1], wv[i], 1);
-          sh[2][i] = __builtin_amdgcn_alignbyte(wv[i + 1], wv[i], 2);
-          sh[3][i] = __builtin_amdgcn_alignbyte(wv[i + 1], wv[i], 3);
+        for (int i = 0; i < ODW; i++) {
+          if constexpr (B == 1) {
+            sh[0][i] = wv[i];
+            sh[1][i] = __builtin_amdgcn_alignbyte(wv[i + 1], wv[i], 1);
+            sh[2][i] = __builtin_amdgcn_alignbyte(wv[i + 1], wv[i], 2);
+            sh[3][i] = __builtin_amdgcn_alignbyte(wv[i + 1], wv[i], 3);
+          } else {
+            sh[0][i] = wv[i];
+            sh[1][i] = __builtin_amdgcn_alignbyte(wv[i + 1], wv[i], 2);
+            sh[2][i] = wv[i + 1];
+            sh[3][i] = __builtin_amdgcn_alignbyte(wv[i + 2], wv[i + 1], 2);
+          }
         }
 #pragma unroll
         for (int c = 0; c < kTileRows; c++) {
           const int r = yy - c;  // source row against candidate row c
           if (r >= 0 && r < 16) {
-            const uint4 o4 = orgs[r];
-            const uint32_t ov[4] = {o4.x, o4.y, o4.z, o4.w};
+            uint32_t ov[ODW];
+#pragma unroll
+            for (int i = 0; i < ODW; i += 4) {
+              const uint4 o4 = *reinterpret_cast<const uint4 *>(orgs + r * ODW + i);
+              ov[i] = o4.x;
+              ov[i + 1] = o4.y;
+              ov[i + 2] = o4.z;
+              ov[i + 3] = o4.w;
+            }
 #pragma unroll
             for (int j = 0; j < 4; j++)
 #pragma unroll
-              for (int i = 0; i < 4; i++) acc[c][j] = sad_u8x4(ov[i], sh[j][i], acc[c][j]);
+              for (int i = 0; i < ODW; i++) acc[c][j] = sad_px<Px>(ov[i], sh[j][i], acc[c][j]);
           }
         }
       }
       // cost = 256 * sad + rate * lambda (get_mv_rate, src/me.rs:1006-1021):
       // the rate splits into a row part per tile row and a column part per
       // tile column, so a tile needs 24 diff_to_rate instead of 128.  For a
-      // 16x16 u8 block 256 * sad < 2^24, so with lambda < 2^25 the cost
-      // fits u32 and (cost, raster index) packs into one u64 key whose
+      // 16x16 block 256 * sad < 2^28 (12-bit), so with lambda < 2^25 the
+      // cost fits u32 and (cost, raster index) packs into one u64 key whose
       // minimum is the reference's first strict minimum.
       int rr0[kTileRows], rr1[kTileRows], rc0[4], rc1[4];
 #pragma unroll
@@ -350,8 +386,10 @@ int rv_full_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
   a.step = step;
   if (next) a.next = *next;
   const unsigned grid = (unsigned)((n + 7) / 8 * 8);
-  if (!org->hbd && blk_w == 16 && blk_h == 16 && step == 1)
-    fs16_u8_kernel<<<grid, kFsThreads, 0, s>>>(a);
+  if (blk_w == 16 && blk_h == 16 && step == 1 && org->hbd)
+    fs16_kernel<uint16_t><<<grid, kFsThreads, 0, s>>>(a);
+  else if (blk_w == 16 && blk_h == 16 && step == 1)
+    fs16_kernel<uint8_t><<<grid, kFsThreads, 0, s>>>(a);
   else if (org->hbd)
     fs_generic_kernel<uint16_t><<<grid, kFsThreads, 0, s>>>(a);
   else
