@@ -67,6 +67,33 @@ def coarse_windows(W, H, R, scale, tile=(0, 0, 0, 0)):
     return out * R
 
 
+# rocprofv3 kernel names of the bench's kernel classes (u8 / u16 builds)
+ROCPROF_NAMES = {
+    "full_search": "fs16_kernel<{px}>",
+    "diamond_fullpel_64": "ds_fast_kernel<{px}, 64, 64, false>",
+    "diamond_subpel_64": "ds_fast_kernel<{px}, 64, 64, true>",
+    "rdo_candidates": "rdo_frame_kernel<{px}>",
+}
+
+
+def measured_traffic(args, kernel, bd):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    passes (profiles/traffic_1080p.json: 2 x FETCH_SIZE + WRITE_SIZE, see
+    tools/prof_summary.py), for the default workload it was measured on;
+    None otherwise."""
+    path = os.path.join(ROOT, "profiles", "traffic_1080p.json")
+    if args.config != "1080p" or args.refs != 2 or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        tj = json.load(f)
+    want = ROCPROF_NAMES.get(kernel, "?").format(px="unsigned short" if bd > 8 else "unsigned char")
+    for name, v in tj["kernels"].items():
+        if want in name:
+            return {"bytes_per_launch": round(v["hbm_bytes"]), "source": tj["source"],
+                    "git": tj["git"]}
+    return None
+
+
 def timed_run(engine, group, steps, warmup, scales=None, sync=None):
     """W untimed frames, then exactly K timed frames bracketed by a barrier
     and a device sync on both sides; returns (max-over-ranks seconds, result
@@ -158,8 +185,10 @@ def main():
     launch_s = kd["ms"] / 1e3 / kd["launches"]
     ach = kd["bytes"] / kd["launches"] / launch_s / 1e9
     roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
-            "avg_launch_ms": round(kd["ms"] / kd["launches"], 5)}
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
+            "traffic": measured_traffic(args, dom, bd),
+            "avg_launch_ms": round(kd["ms"] / kd["launches"], 5),
+            "algorithmic_bytes_per_launch": round(kd["bytes"] / kd["launches"])}
     if dom == "full_search":
         achv = kd["sad_px"] / (kd["ms"] / 1e3) / 1e12
         roof["valu"] = {"achieved": round(achv, 3), "peak": round(SAD_PEAK_PX / 1e12, 1),

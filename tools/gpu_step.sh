@@ -7,6 +7,7 @@ mkdir -p gpurun_out
 for step in "$@"; do
   secs=${step%% *}; rest=${step#* }; log=${rest%% *}; cmd=${rest#* }
   echo "== [$secs s] $cmd" | tee -a gpurun_out/steps.log
+  mkdir -p "$(dirname "gpurun_out/$log")"
   timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$log" 2>&1
   rc=$?
   echo "   rc=$rc" | tee -a gpurun_out/steps.log

@@ -46,6 +46,8 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--bench")
     ap.add_argument("--title", default="")
+    ap.add_argument("--traffic-json", help="also write per-kernel HBM bytes per launch "
+                    "(FETCH_SIZE x2 + WRITE_SIZE, bytes) for bench.py's roofline.traffic")
     a = ap.parse_args()
     tk = top_kernels(os.path.join(a.prof_dir, "trace", "run_results.db"))
     fe = pmc(os.path.join(a.prof_dir, "fetch", "run_results.db"))
@@ -71,8 +73,25 @@ def main():
         ws = f"{w[1]:.1f}" if w else "-"
         lines.append(f"| `{short(name)}` | {calls} | {avg:.2f} | {tot:.1f} | "
                      f"{pct:.1f} | {fs} | {f2} | {ws} |")
+    lines += ["", "Calibration (tools/ubench/pmc_cal.hip, 1 GiB streams on this pool): FETCH_SIZE "
+              "reports 1/2 of the bytes read at byte, dword and dwordx4 widths alike; WRITE_SIZE "
+              "reports the bytes written exactly. So HBM bytes = 2 x FETCH + WRITE."]
     with open(a.out, "w") as f:
         f.write("\n".join(lines) + "\n")
+    if a.traffic_json:
+        import subprocess
+        rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True,
+                             text=True).stdout.strip()
+        tj = {"source": os.path.basename(a.out), "git": rev, "unit": "bytes per launch",
+              "kernels": {}}
+        for name, calls, tot, avg, pct in tk:
+            f_, w_ = fe.get(name), wr.get(name)
+            if f_ and w_:
+                tj["kernels"][name] = {"fetch": 2 * f_[1] * 1024, "write": w_[1] * 1024,
+                                       "hbm_bytes": 2 * f_[1] * 1024 + w_[1] * 1024,
+                                       "avg_us": avg}
+        with open(a.traffic_json, "w") as f:
+            json.dump(tj, f, indent=1)
     print("\n".join(lines))
 
 
