@@ -73,6 +73,7 @@ ROCPROF_NAMES = {
     "diamond_fullpel_64": "ds_fast_kernel<{px}, 64, 64, false>",
     "diamond_subpel_64": "ds_fast_kernel<{px}, 64, 64, true>",
     "rdo_candidates": "rdo_frame_kernel<{px}>",
+    "rdo_candidates_zero_mv": "rdo_frame_kernel<{px}>",
 }
 
 
@@ -165,6 +166,10 @@ def main():
     cw, ch = 64 >> xdec, 64 >> ydec
     ntx_c = (cw // 32) * (ch // 32)
     csub = (cw // (min(cw, 8) >> xdec)) * (ch // (min(ch, 8) >> ydec))
+    rdo_bytes = float(nctx * (71 * 71 * px + 64 * 64 * px + 4 * 32 * 32 + 64 * 64 * px +
+                              64 * 40 + 16 + 24) +
+                      2 * nctx * ((cw + 7) * (ch + 7) * px + 2 * cw * ch * px +
+                                  4 * ntx_c * 32 * 32 + 8 * csub + 16 + 24 * ntx_c))
     kernels = {
         "full_search": dict(ms=float(ms[1]), launches=nref, bytes=fs_bytes, sad_px=fs_ops),
         "diamond_fullpel_64": dict(ms=float(ms[6]), launches=1,
@@ -173,12 +178,11 @@ def main():
         "diamond_subpel_64": dict(ms=float(ms[7]), launches=1,
                                   bytes=nj * (64 * 64 * px + 80) +
                                   ev_sub / ev_frames * 71 * 71 * px),
-        "rdo_candidates": dict(ms=float(ms[8]), launches=1,
-                               bytes=float(nctx * (71 * 71 * px + 64 * 64 * px + 4 * 32 * 32 +
-                                                   64 * 64 * px + 64 * 40 + 16 + 24) +
-                                           2 * nctx * ((cw + 7) * (ch + 7) * px +
-                                                       2 * cw * ch * px + 4 * ntx_c * 32 * 32 +
-                                                       8 * csub + 16 + 24 * ntx_c))),
+        # F4 is two launches of the same kernel: the sub-pel-MV candidates on
+        # the replay stream and the zero-MV candidates on a second stream
+        # (concurrent with F0-F3); each covers half of the candidates
+        "rdo_candidates": dict(ms=float(ms[8]), launches=1, bytes=rdo_bytes / 2),
+        "rdo_candidates_zero_mv": dict(ms=float(ms[9]), launches=1, bytes=rdo_bytes / 2),
     }
     dom = max(kernels, key=lambda n: kernels[n]["ms"])
     kd = kernels[dom]

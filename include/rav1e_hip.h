@@ -315,9 +315,11 @@ int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
 /* Kernel-time breakdown of the last frame (HIP events on the replay
  * stream), ms: [0..5] stages F0..F5 (F1 = exactly the full-search
  * launches), then kernel brackets [6] F3 full-pel diamond, [7] F3 sub-pel
- * diamond, [8] F4 fused candidate launch (luma: MC + diff + fwd TX_64X64 +
- * coefficient stand-in + inverse + add + cdef moments; chroma U and V: the
- * same with TX_32X32 and SSE).  Returns the count written (<= 9). */
+ * diamond, [8] F4 fused launch of the sub-pel-MV candidates (luma: MC +
+ * diff + fwd TX_64X64 + coefficient stand-in + inverse + add + cdef
+ * moments; chroma U and V: the same with TX_32X32 and SSE), [9] F4 fused
+ * launch of the zero-MV candidates, which runs on a second stream
+ * concurrently with F0-F3.  Returns the count written (<= 10). */
 int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
 /* Same breakdown summed over the last `last_frames` frames (<= 64). */
 int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,

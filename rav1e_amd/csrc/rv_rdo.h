@@ -18,7 +18,9 @@ struct RdoPlane {
 
 struct RdoArgs {
   RdoPlane p[2];      // blockIdx.y selects the plane (chroma: U, V)
-  int n_tx;           // transform blocks per plane
+  int n_tx;           // transform blocks per plane in this launch
+  int k_sel;          // -1: every candidate; 0 / 1: only candidates 2r + k_sel
+  int nsb;            // superblocks (candidate c of SB sb = c * nsb + sb)
   int ntx_per_cand;   // transform blocks per candidate
   int cands_per_ref;  // candidates of one reference (job arrays are ref-major)
   int bd;

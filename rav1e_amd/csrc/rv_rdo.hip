@@ -322,17 +322,29 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
 // One launch per frame: blocks [0, luma.n_tx) are the luma candidates
 // (N = 64, cdef moments), the rest the chroma transform blocks of planes U
 // then V (N = 32, SSE).  Luma first: the long tasks start first.
+// Task i of a launch -> transform block index t (candidate-major).  With
+// k_sel >= 0 the launch covers only candidates 2r + k_sel (the replay runs
+// the zero-MV candidates, which need no motion search, concurrently with
+// the searches on a second stream).
+__device__ __forceinline__ int rdo_task(const RdoArgs &a, int i) {
+  if (a.k_sel < 0) return i;
+  const int cl = i / a.ntx_per_cand, sub = i - cl * a.ntx_per_cand;
+  const int r = cl / a.nsb, sb = cl - r * a.nsb;
+  return ((2 * r + a.k_sel) * a.nsb + sb) * a.ntx_per_cand + sub;
+}
+
 template <typename Px>
 __global__ __launch_bounds__(64) void rdo_frame_kernel(RdoArgs luma, RdoArgs chroma) {
   __shared__ int32_t buf[64 * 65];
   __shared__ Px pred[64 * 64];
   int b = blockIdx.x;
   if (b < luma.n_tx) {
-    rdo_cand_body<Px, 64, true>(luma, luma.p[0], b, buf, pred);
+    rdo_cand_body<Px, 64, true>(luma, luma.p[0], rdo_task(luma, b), buf, pred);
   } else {
     b -= luma.n_tx;
     const int plane = b / chroma.n_tx;
-    rdo_cand_body<Px, 32, false>(chroma, chroma.p[plane], b - plane * chroma.n_tx, buf, pred);
+    rdo_cand_body<Px, 32, false>(chroma, chroma.p[plane],
+                                 rdo_task(chroma, b - plane * chroma.n_tx), buf, pred);
   }
 }
 

@@ -200,6 +200,7 @@ struct rv_replay {
   rv_replay_cfg cfg;
   Geo g;
   hipStream_t stream;
+  hipStream_t side;  // zero-MV RDO candidates, concurrent with the searches
   bool own_stream;
   double me_lambda;
   std::vector<RvFrameSlot> slots;  // 0 = input, 1..R = references
@@ -223,8 +224,9 @@ struct rv_replay {
   // kernel brackets, see rv_replay_frame), so per-kernel times can be
   // summed over a whole timed run without a host sync per frame.
   static constexpr int kRing = 64;
-  static constexpr int kEv = 9;
+  static constexpr int kEv = 11;  // + [9,10]: side-stream RDO bracket
   hipEvent_t evs[kRing][kEv];
+  hipEvent_t fork[kRing], join[kRing];  // cross-stream ordering only
   hipEvent_t *ev;
   long frames = 0;
   // diamond candidate evaluations per job, per ring slot: [kRing][2][nsb*R]
@@ -410,9 +412,13 @@ extern "C" {
 void rv_replay_destroy(rv_replay *r) {
   if (!r) return;
   for (void *p : r->allocs) (void)hipFree(p);
-  for (int f = 0; f < rv_replay::kRing; f++)
+  for (int f = 0; f < rv_replay::kRing; f++) {
     for (int i = 0; i < rv_replay::kEv; i++)
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
+    if (r->fork[f]) (void)hipEventDestroy(r->fork[f]);
+    if (r->join[f]) (void)hipEventDestroy(r->join[f]);
+  }
+  if (r->side) (void)hipStreamDestroy(r->side);
   if (r->own_stream && r->stream) (void)hipStreamDestroy(r->stream);
   delete r;
 }
@@ -427,6 +433,9 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   }
   rv_replay *r = new rv_replay();
   memset(r->evs, 0, sizeof(r->evs));
+  memset(r->fork, 0, sizeof(r->fork));
+  memset(r->join, 0, sizeof(r->join));
+  r->side = nullptr;
   r->ev = r->evs[0];
   r->cfg = *cfg;
   Geo &g = r->g;
@@ -506,8 +515,13 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->imp_by = vis_h / 8;
   r->n_imp = r->imp_bx * r->imp_by;
   r->tail = (unsigned long long *)dalloc(r, 4 * 8);
-  for (int f = 0; f < rv_replay::kRing; f++)
-    for (int i = 0; i < rv_replay::kEv; i++) ok = ok && hipEventCreateWithFlags(&r->evs[f][i], hipEventDisableSystemFence) == hipSuccess;
+  for (int f = 0; f < rv_replay::kRing; f++) {
+    for (int i = 0; i < rv_replay::kEv; i++)
+      ok = ok && hipEventCreateWithFlags(&r->evs[f][i], hipEventDisableSystemFence) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&r->fork[f], hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&r->join[f], hipEventDisableTiming) == hipSuccess;
+  }
+  ok = ok && hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking) == hipSuccess;
   const size_t ev_bytes = (size_t)rv_replay::kRing * 2 * nr * 4;
   r->ds_evals = (uint32_t *)dalloc(r, ev_bytes);
   ok = ok && r->ds_evals && hipMemsetAsync(r->ds_evals, 0, ev_bytes, r->stream) == hipSuccess;
@@ -594,6 +608,55 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   r->ev = e;
   r->frames++;
   RV_H(hipEventRecord(e[0], st));
+  // F4 zero-MV candidates need no motion search: they run on the side
+  // stream concurrently with F0-F3 (rav1e evaluates them in the same RDO
+  // loop, src/rdo.rs:949-1006; only the order of independent work changes)
+  const int ntx_c = (g.cw / 32) * (g.ch / 32);
+  const int nct = g.nctx * ntx_c;
+  RdoArgs la, ca;
+  {
+    memset(&la, 0, sizeof(la));
+    la.p[0].org = cur.y;
+    for (int k = 0; k < g.R; k++) la.p[0].ref[k] = r->slots[1 + k].y;
+    la.p[0].dst = r->tall_y;
+    la.p[0].mc = r->l_mc;
+    la.p[0].tx = r->l_tx;
+    la.p[0].packed = r->l_packed;
+    la.p[0].dist = r->l_mom;
+    la.n_tx = g.nctx / 2;  // one candidate kind per launch
+    la.ntx_per_cand = 1;
+    la.cands_per_ref = 2 * nr;
+    la.nsb = nr;
+    la.bd = g.bd;
+    la.mb_w = la.mb_h = kSb;
+    la.sub_w = la.sub_h = 8;
+    ca = la;
+    const rv_plane *cp[2] = {&cur.u, &cur.v};
+    const rv_plane *tp[2] = {&r->tall_u, &r->tall_v};
+    uint64_t *cs[2] = {r->u_sse, r->v_sse};
+    for (int p = 0; p < 2; p++) {
+      ca.p[p].org = *cp[p];
+      for (int k = 0; k < g.R; k++) ca.p[p].ref[k] = p ? r->slots[1 + k].v : r->slots[1 + k].u;
+      ca.p[p].dst = *tp[p];
+      ca.p[p].mc = r->c_mc;
+      ca.p[p].tx = r->c_tx;
+      ca.p[p].packed = r->c_packed + (size_t)p * nct * 1024;
+      ca.p[p].dist = cs[p];
+    }
+    ca.n_tx = nct / 2;
+    ca.ntx_per_cand = ntx_c;
+    ca.mb_w = g.cw;
+    ca.mb_h = g.ch;
+    ca.sub_w = (g.cw < 8 ? g.cw : 8) >> g.xdec;
+    ca.sub_h = (g.ch < 8 ? g.ch : 8) >> g.ydec;
+  }
+  RV_H(hipEventRecord(r->fork[slot], st));
+  RV_H(hipStreamWaitEvent(r->side, r->fork[slot], 0));
+  la.k_sel = ca.k_sel = 1;
+  RV_H(hipEventRecord(e[9], r->side));
+  RV_R(rv_rdo_candidates(la, ca, g.hbd, r->side));
+  RV_H(hipEventRecord(e[10], r->side));
+  RV_H(hipEventRecord(r->join[slot], r->side));
   // F0 hres + qres of the input (encode_frame, src/encoder.rs:3382-3385)
   RV_R(rv_plane_pyramid(&cur.y, &cur.hres, &cur.qres, st));
   RV_H(hipEventRecord(e[1], st));
@@ -613,47 +676,11 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub, nr, 64, 64, 1, 0, 0, g.bd,
                                r->sub, ev_sub, &to_mc, st));
   RV_H(hipEventRecord(e[4], st));
-  // F4 RDO candidates: luma + both chroma planes in one fused launch
-  const int ntx_c = (g.cw / 32) * (g.ch / 32);
-  const int nct = g.nctx * ntx_c;
-  {
-    RdoArgs la;
-    memset(&la, 0, sizeof(la));
-    la.p[0].org = cur.y;
-    for (int k = 0; k < g.R; k++) la.p[0].ref[k] = r->slots[1 + k].y;
-    la.p[0].dst = r->tall_y;
-    la.p[0].mc = r->l_mc;
-    la.p[0].tx = r->l_tx;
-    la.p[0].packed = r->l_packed;
-    la.p[0].dist = r->l_mom;
-    la.n_tx = g.nctx;
-    la.ntx_per_cand = 1;
-    la.cands_per_ref = 2 * nr;
-    la.bd = g.bd;
-    la.mb_w = la.mb_h = kSb;
-    la.sub_w = la.sub_h = 8;
-    RdoArgs ca = la;
-    const rv_plane *cp[2] = {&cur.u, &cur.v};
-    const rv_plane *tp[2] = {&r->tall_u, &r->tall_v};
-    uint64_t *cs[2] = {r->u_sse, r->v_sse};
-    for (int p = 0; p < 2; p++) {
-      ca.p[p].org = *cp[p];
-      for (int k = 0; k < g.R; k++) ca.p[p].ref[k] = p ? r->slots[1 + k].v : r->slots[1 + k].u;
-      ca.p[p].dst = *tp[p];
-      ca.p[p].mc = r->c_mc;
-      ca.p[p].tx = r->c_tx;
-      ca.p[p].packed = r->c_packed + (size_t)p * nct * 1024;
-      ca.p[p].dist = cs[p];
-    }
-    ca.n_tx = nct;
-    ca.ntx_per_cand = ntx_c;
-    ca.mb_w = g.cw;
-    ca.mb_h = g.ch;
-    ca.sub_w = (g.cw < 8 ? g.cw : 8) >> g.xdec;
-    ca.sub_h = (g.ch < 8 ? g.ch : 8) >> g.ydec;
-    RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
-  }
+  // F4 sub-pel MV candidates: luma + both chroma planes in one fused launch
+  la.k_sel = ca.k_sel = 0;
+  RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
   RV_H(hipEventRecord(e[8], st));
+  RV_H(hipStreamWaitEvent(st, r->join[slot], 0));
   score_candidates<<<g.nsb, 64, 0, st>>>(g, r->l_mom, r->u_sse, r->v_sse, r->lsub, r->csub,
                                          r->coarse, r->half, r->full, r->sub, r->words,
                                          r->tail + 2);
@@ -707,7 +734,7 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
   if (last < 1) last = 1;
   if (last > rv_replay::kRing) last = rv_replay::kRing;
   if (last > r->frames) last = (int)r->frames;
-  for (int i = 0; i < cap && i < 9; i++) ms_out[i] = 0.f;
+  for (int i = 0; i < cap && i < 10; i++) ms_out[i] = 0.f;
   int n = 0;
   for (int f = 0; f < last; f++) {
     hipEvent_t *e = r->evs[(r->frames - 1 - f) % rv_replay::kRing];
@@ -719,9 +746,10 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
       ms_out[n++] += ms;
     }
     // kernel brackets: F3 full-pel diamond, F3 sub-pel diamond, F4 fused
-    // candidate launch
-    const int br[3][2] = {{3, 7}, {7, 4}, {4, 8}};
-    for (int i = 0; i < 3 && n < cap; i++) {
+    // sub-pel MV candidates (main stream), F4 fused zero-MV candidates
+    // (side stream, concurrent with F0-F3)
+    const int br[4][2] = {{3, 7}, {7, 4}, {4, 8}, {9, 10}};
+    for (int i = 0; i < 4 && n < cap; i++) {
       float ms = 0.f;
       RV_H(hipEventElapsedTime(&ms, e[br[i][0]], e[br[i][1]]));
       ms_out[n++] += ms;

@@ -100,15 +100,15 @@ class HipReplay:
         return out[:n]
 
     def stage_ms(self) -> np.ndarray:
-        out = np.zeros(9, dtype=np.float32)
-        n = lib().rv_replay_stage_times(self.h, out.ctypes.data, 9)
+        out = np.zeros(10, dtype=np.float32)
+        n = lib().rv_replay_stage_times(self.h, out.ctypes.data, 10)
         if n < 0:
             _check(n, "rv_replay_stage_times")
         return out[:n]
 
     def stage_ms_sum(self, last_frames: int) -> np.ndarray:
-        out = np.zeros(9, dtype=np.float32)
-        n = lib().rv_replay_stage_times_sum(self.h, last_frames, out.ctypes.data, 9)
+        out = np.zeros(10, dtype=np.float32)
+        n = lib().rv_replay_stage_times_sum(self.h, last_frames, out.ctypes.data, 10)
         if n < 0:
             _check(n, "rv_replay_stage_times_sum")
         return out[:n]

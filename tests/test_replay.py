@@ -68,4 +68,4 @@ def test_gpu_replay_matches_cpu_replay(w, h, xdec, ydec, bd, refs, tile):
         gw, cw = g.results(), c.results()
         bad = np.nonzero(gw != cw)[0]
         assert bad.size == 0, (scale, bad[:10], gw[bad[:10]], cw[bad[:10]])
-    assert len(g.stage_ms()) == 9
+    assert len(g.stage_ms()) == 10
