@@ -162,6 +162,16 @@ int rv_cdef_moments_batch(const rv_plane *org, const rv_plane *ref,
                           const rv_dist_job *d_jobs, int n, int w, int h,
                           int64_t *d_out, void *stream);
 
+/* Transform-domain distortion of encode_tx_block (src/encoder.rs:1210-1224,
+ * tune = Psnr): per block, sum over the coded area (min(W,32) *
+ * min(H,32)) of ((c - rc) * (c - rc)) as u64 -- i32 wrapping square,
+ * sign-extended -- then (d + (1 << (s - 1))) >> s, s = 2 * (3 -
+ * get_log_tx_scale(tx_size)) (src/quantize.rs:34-39).  coeffs: block i at
+ * d_coeffs + i * coeff_stride (the fht raster); rcoeffs: [n][coded area]. */
+int rv_tx_dist_batch(const int32_t *d_coeffs, int coeff_stride,
+                     const int32_t *d_rcoeffs, int n, int tx_size,
+                     uint64_t *d_out, void *stream);
+
 /* ---------------------------------------------------------------------
  * Batched motion compensation.  FilterMode (src/mc.rs:58-66):
  * 0 REGULAR, 1 SMOOTH, 2 SHARP, 3 BILINEAR.  Fracs are 1/16 pel (0..15).
@@ -281,6 +291,18 @@ int rv_diamond_search_batch(const rv_plane *org, const rv_plane *ref,
                             int blk_h, int subpixel, int use_satd,
                             int allow_hp, int bit_depth,
                             rv_fs_result *d_out, void *stream);
+
+/* telescopic_subpel_search (src/me.rs:858-941, the FullSearch sub-pel
+ * stage): 3x3 grids around the running best at steps 8, 4, 2 (and 1 with
+ * allow_hp), REGULAR 8-tap prediction, SAD or SATD; start[i] = the full-pel
+ * (best_mv, lowest_cost) the search refines, out[i] = the result.  Job
+ * fields used: po, MV range, pmv, lambda. */
+int rv_telescopic_subpel_batch(const rv_plane *org, const rv_plane *ref,
+                               const rv_ds_job *d_jobs,
+                               const rv_fs_result *d_start, int n, int blk_w,
+                               int blk_h, int use_satd, int allow_hp,
+                               int bit_depth, rv_fs_result *d_out,
+                               void *stream);
 
 /* ---------------------------------------------------------------------
  * Hot-path replay driver (see DESIGN.md "Replay driver"): reproduces the

@@ -125,3 +125,44 @@ void orc_diamond_search(const orc_ds_ctx *c, const orc_mv *pred, int n_pred,
   *best_mv = center;
   *best_cost = center_cost;
 }
+
+/* telescopic_subpel_search (src/me.rs:858-941): 3x3 grids around the
+ * running best at steps 8, 4, 2 (and 1 with allow_hp); the grid centre
+ * of a step is fixed, every candidate in (i, j) raster order updates the
+ * best on a strict '<'. */
+void orc_telescopic_subpel(const orc_ds_ctx *c, orc_mv *best_mv, uint64_t *lowest_cost) {
+  const int nsteps = c->allow_hp ? 4 : 3;
+  for (int st = 0; st < nsteps; st++) {
+    const int16_t step = (int16_t)(8 >> st);
+    const orc_mv center = *best_mv;
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        if (i == 1 && j == 1) continue;
+        orc_mv cand = {(int16_t)(center.row + step * (i - 1)), (int16_t)(center.col + step * (j - 1))};
+        /* out-of-range candidates are skipped (mv_rd_cost returns MAX) */
+        uint64_t cost = mv_rd_cost(c, cand);
+        if (cost < *lowest_cost) {
+          *lowest_cost = cost;
+          *best_mv = cand;
+        }
+      }
+  }
+}
+
+/* tx-domain distortion of encode_tx_block (src/encoder.rs:1210-1224):
+ * sum over the coded area of ((c - rc) * (c - rc)) as u64 -- i32 wrapping
+ * square, sign-extended -- then rounded by 2 * (3 - get_log_tx_scale)
+ * (src/quantize.rs:34-39) bits. */
+uint64_t orc_tx_dist(const int32_t *coeffs, const int32_t *rcoeffs, int coded_area,
+                     int tx_w, int tx_h) {
+  uint64_t d = 0;
+  for (int i = 0; i < coded_area; i++) {
+    int32_t e = (int32_t)((uint32_t)coeffs[i] - (uint32_t)rcoeffs[i]);
+    int32_t sq = (int32_t)((uint32_t)e * (uint32_t)e);
+    d += (uint64_t)(int64_t)sq;
+  }
+  const int area = tx_w * tx_h;
+  const int log_scale = (area > 256) + (area > 1024);
+  const int bits = 2 * (3 - log_scale);
+  return (d + (1ull << (bits - 1))) >> bits;
+}

@@ -311,8 +311,11 @@ static void run_sb(orc_replay *r, int sb, uint64_t tail[3]) {
     /* luma TX_64X64 DCT_DCT */
     orc_diff(res, at(&cur->y, hbd, px, py), cur->y.stride, ly, SB, SB, SB, hbd);
     orc_fwd_txfm2d(res, co, 4, 0, r->bd);
+    /* coefficient stand-in over the first coded_tx_area (1024) entries of
+     * the W-stride raster: what quantize and the tx-domain zip consume
+     * (src/encoder.rs:1152-1156, 1210-1219; SURVEY.md §0.6 fork quirk) */
     for (int i = 0; i < 32 * 32; i++) {
-      int32_t q = (co[(i / 32) * 64 + (i % 32)] / QSTEP) * QSTEP;
+      int32_t q = (co[i] / QSTEP) * QSTEP;
       pk[i] = q;
       tail[0] += (uint64_t)(int64_t)q * (uint64_t)(i + 1);
     }

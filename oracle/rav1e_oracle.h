@@ -118,6 +118,12 @@ typedef struct {
 } orc_ds_ctx;
 void orc_diamond_search(const orc_ds_ctx *c, const orc_mv *pred, int n_pred,
                         orc_mv *best_mv, uint64_t *best_cost);
+/* telescopic_subpel_search (src/me.rs:858-941): best_mv / lowest_cost are
+ * the search's start (in) and result (out). */
+void orc_telescopic_subpel(const orc_ds_ctx *c, orc_mv *best_mv, uint64_t *lowest_cost);
+/* tx-domain distortion (src/encoder.rs:1210-1224). */
+uint64_t orc_tx_dist(const int32_t *coeffs, const int32_t *rcoeffs, int coded_area,
+                     int tx_w, int tx_h);
 
 /* ---- frame layout (src/frame/) --------------------------------------- */
 /* Plane::new geometry (src/frame/plane.rs:215-244). Writes

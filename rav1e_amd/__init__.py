@@ -236,6 +236,8 @@ def _declare(L):
         "rv_replay_stage_times_sum": (i32, [vp, i32, vp, i32]),
         "rv_replay_counters": (i32, [vp, vp, i32]),
         "rv_diamond_search_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
+        "rv_telescopic_subpel_batch": (i32, [P, P, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp]),
+        "rv_tx_dist_batch": (i32, [vp, i32, vp, i32, i32, vp, vp]),
         "rav1e_fwd_txfm_hip": (i32, [vp, vp, i32, i32, i32]),
         "rav1e_inv_txfm_add_hip": (i32, [vp, vp, C.c_ssize_t, i32, i32, i32]),
         "rv_sad_fn": (vp, [i32, i32, i32]),
@@ -526,6 +528,37 @@ def diamond_search_batch(org: DevicePlane, ref: DevicePlane, jobs, blk_w, blk_h,
            "rv_diamond_search_batch")
     _sync()
     return out.download(FS_RESULT, len(jobs))
+
+
+def telescopic_subpel_batch(org: DevicePlane, ref: DevicePlane, jobs, start, blk_w, blk_h,
+                            use_satd=False, allow_hp=False, bit_depth=8) -> np.ndarray:
+    """telescopic_subpel_search (src/me.rs:858-941); start = FS_RESULT records
+    (the full-pel best_mv / lowest_cost each search refines)."""
+    jobs = np.ascontiguousarray(jobs, dtype=DS_JOB)
+    start = np.ascontiguousarray(start, dtype=FS_RESULT)
+    assert len(start) == len(jobs)
+    dj, ds = DeviceBuffer.from_array(jobs), DeviceBuffer.from_array(start)
+    out = DeviceBuffer(16 * max(1, len(jobs)))
+    _check(lib().rv_telescopic_subpel_batch(C.byref(org.desc), C.byref(ref.desc), dj.ptr, ds.ptr,
+                                            len(jobs), blk_w, blk_h, int(use_satd), int(allow_hp),
+                                            bit_depth, out.ptr, None),
+           "rv_telescopic_subpel_batch")
+    _sync()
+    return out.download(FS_RESULT, len(jobs))
+
+
+def tx_dist_batch(coeffs: np.ndarray, rcoeffs: np.ndarray, tx_size) -> np.ndarray:
+    """Transform-domain distortion (src/encoder.rs:1210-1224): coeffs [n][W*H]
+    rasters, rcoeffs [n][coded area]."""
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.int32)
+    rcoeffs = np.ascontiguousarray(rcoeffs, dtype=np.int32)
+    n = coeffs.shape[0]
+    dc, dr = DeviceBuffer.from_array(coeffs), DeviceBuffer.from_array(rcoeffs)
+    out = DeviceBuffer(8 * max(1, n))
+    _check(lib().rv_tx_dist_batch(dc.ptr, coeffs.shape[1], dr.ptr, n, int(tx_size), out.ptr, None),
+           "rv_tx_dist_batch")
+    _sync()
+    return out.download(np.uint64, n)
 
 
 # ---- reference-shaped single-call entry points ----------------------------

@@ -7,6 +7,7 @@
 // units).  Groups reduce with xor-shuffles (no LDS, no atomics), so small
 // blocks pack 64 / G jobs per wavefront and large blocks use whole waves.
 #include "rv_device.h"
+#include "rv_tx.h"
 
 namespace rv {
 
@@ -162,6 +163,28 @@ __global__ __launch_bounds__(kBlock) void cdef_moments_kernel(
   }
 }
 
+// ---- tx-domain distortion (src/encoder.rs:1210-1224) ------------------------
+// One wavefront per transform block: sum over the coded area of
+// ((c - rc) * (c - rc)) as u64 (i32 wrapping square, sign-extended), then
+// (d + (1 << (bits - 1))) >> bits, bits = 2 * (3 - get_log_tx_scale).
+__global__ __launch_bounds__(kBlock) void tx_dist_kernel(const int32_t *__restrict__ coeffs,
+                                                         int cstride,
+                                                         const int32_t *__restrict__ rcoeffs,
+                                                         int n, int area, int bits,
+                                                         uint64_t *__restrict__ out) {
+  const int blk = (int)((blockIdx.x * kBlock + threadIdx.x) >> 6), lane = threadIdx.x & 63;
+  if (blk >= n) return;  // whole wavefront
+  const int32_t *c = coeffs + (int64_t)blk * cstride;
+  const int32_t *rc = rcoeffs + (int64_t)blk * area;
+  uint64_t d = 0;
+  for (int i = lane; i < area; i += 64) {
+    const int32_t e = wsub(c[i], rc[i]);
+    d += (uint64_t)(int64_t)wmul(e, e);
+  }
+  d = group_sum<64>(d);
+  if (lane == 0) out[blk] = (d + (1ull << (bits - 1))) >> bits;
+}
+
 // ---- launch helpers -------------------------------------------------------
 static bool valid_block(int w, int h) {
   auto p2 = [](int v) { return v >= 4 && v <= 128 && (v & (v - 1)) == 0; };
@@ -290,6 +313,25 @@ int rv_cdef_moments_batch(const rv_plane *org, const rv_plane *ref,
   else
     cdef_moments_kernel<uint8_t><<<grid, kBlock, 0, s>>>(*org, *ref, d_jobs, n,
                                                          sub_x, nsub, d_out);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+// tx-domain distortion of a batch of transform blocks: coeffs [n] at
+// coeff_stride (e.g. the W*H raster of rv_fwd_txfm_batch), rcoeffs [n][coded
+// area] (the packed dequantized coefficients).
+int rv_tx_dist_batch(const int32_t *d_coeffs, int coeff_stride, const int32_t *d_rcoeffs, int n,
+                     int tx_size, uint64_t *d_out, void *stream) {
+  if (!d_coeffs || !d_rcoeffs || !d_out || n < 0 || tx_size < 0 || tx_size > 18)
+    return rv_set_error(RV_EINVAL, "rv_tx_dist_batch: bad arguments");
+  const int w = 1 << tx_w_log2(tx_size), h = 1 << tx_h_log2(tx_size);
+  const int area = (w < 32 ? w : 32) * (h < 32 ? h : 32);  // coded_tx_area
+  if (coeff_stride < area) return rv_set_error(RV_EINVAL, "rv_tx_dist_batch: stride < coded area");
+  const int log_scale = (w * h > 256) + (w * h > 1024);  // get_log_tx_scale
+  if (n == 0) return RV_OK;
+  const unsigned grid = (unsigned)((n + 3) / 4);
+  tx_dist_kernel<<<grid, kBlock, 0, rv_resolve_stream(stream)>>>(
+      d_coeffs, coeff_stride, d_rcoeffs, n, area, 2 * (3 - log_scale), d_out);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

@@ -92,6 +92,8 @@ struct DsArgs {
   int n, n_per_ref, w, h, subpel, satd, hp, bd;
   uint32_t *evals;  // optional: in-range candidate evaluations per job
   ChainNext next;   // replay: feed the winner into the next stage's jobs
+  int tele;         // 1: telescopic_subpel_search instead of the diamond
+  const rv_fs_result *start;  // tele: the search's start (best_mv, lowest_cost)
 };
 
 __device__ __forceinline__ void ds_write(const DsArgs &a, int job, rv_mv center,
@@ -478,73 +480,126 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
     return mine;
   };
 
-  // ---- get_best_predictor, then diamond steps: one round loop -----------
-  // A round evaluates up to 4 candidates, one per wavefront: first the
-  // predictors in groups of 4 (the sequential strict-< scan of
-  // get_best_predictor, applied group by group in order, is the same
-  // first minimum), then the 4 pattern points of each diamond step.  One
-  // call site keeps a single inlined copy of the candidate code.
-  const int np = jb.n_pred < RV_DS_MAX_PRED ? jb.n_pred : RV_DS_MAX_PRED;
   rv_mv center{0, 0};
   uint64_t center_cost = ~0ull;
-  int16_t radius = a.subpel ? 4 : 16;
-  const int16_t radius_end = a.subpel ? (a.hp ? 1 : 2) : 8;
-  int p0 = 0;  // next predictor group; >= np once the diamond phase runs
-  // Every diamond move strictly lowers center_cost, so the loop ends; the
-  // bound only guarantees the grid drains whatever the inputs.
-  for (int iter = 0; iter < 4096 + RV_DS_MAX_PRED; iter++) {
-    const bool pred_phase = p0 < np;
-    rv_mv c4[kDsWaves];
-    int n;
-    if (pred_phase) {
-      n = np - p0 < kDsWaves ? np - p0 : kDsWaves;
+  // ---- telescopic_subpel_search (src/me.rs:858-941) ---------------------
+  // 3x3 grid around the running best at steps 8, 4, 2 (and 1 with hp); the
+  // 8 grid points of a step are two rounds of 4; the reference's in-order
+  // strict-< updates against a fixed grid centre equal the first minimum
+  // of the step compared with the running cost.
+  if (a.tele) {
+    rv_mv best = a.start[job].best_mv;
+    uint64_t lowest = a.start[job].cost;
+    int round = 0;
+    const int nsteps = a.hp ? 4 : 3;
+    for (int st = 0; st < nsteps; st++) {
+      const int16_t step = (int16_t)(8 >> st);
+      const rv_mv ctr = best;
+      uint64_t bc = ~0ull;
+      rv_mv bm = ctr;
+      for (int half = 0; half < 2; half++, round++) {
+        rv_mv c4[kDsWaves];
 #pragma unroll
-      for (int k = 0; k < kDsWaves; k++) c4[k] = jp->pred[p0 + (k < n ? k : 0)];
-    } else {
-      n = kDsWaves;
-      c4[0] = rv_mv{(int16_t)(center.row + radius), center.col};  // diamond_pattern
-      c4[1] = rv_mv{center.row, (int16_t)(center.col + radius)};
-      c4[2] = rv_mv{(int16_t)(center.row - radius), center.col};
-      c4[3] = rv_mv{center.row, (int16_t)(center.col - radius)};
-    }
-    uint64_t c;
-    if constexpr (SUB) {
-      c = sub_round(c4, n);
-    } else {
-      rv_mv mine = c4[0];
+        for (int k = 0; k < kDsWaves; k++) {
+          const int gi = half * 4 + k < 4 ? half * 4 + k : half * 4 + k + 1;  // skip the centre
+          c4[k] = rv_mv{(int16_t)(ctr.row + step * (gi / 3 - 1)),
+                        (int16_t)(ctr.col + step * (gi % 3 - 1))};
+        }
+        uint64_t c;
+        if constexpr (SUB) {
+          c = sub_round(c4, kDsWaves);
+        } else {
+          rv_mv mine = c4[0];
 #pragma unroll
-      for (int k = 1; k < kDsWaves; k++)
-        if (wave == k) mine = c4[k];
-      c = wave < n ? eval_full(mine) : ~0ull;
-    }
-    if (lane == 0) scost[iter & 1][wave] = c;
-    __syncthreads();
-    uint64_t best = ~0ull;
-    int bp = 0;
+          for (int k = 1; k < kDsWaves; k++)
+            if (wave == k) mine = c4[k];
+          c = eval_full(mine);
+        }
+        if (lane == 0) scost[round & 1][wave] = c;
+        __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kDsWaves; k++) {
-      const uint64_t v = scost[iter & 1][k];
-      if (k < n && v < best) {
-        best = v;
-        bp = k;
+        for (int k = 0; k < kDsWaves; k++) {
+          const uint64_t v = scost[round & 1][k];
+          if (v < bc) {
+            bc = v;
+            bm = c4[k];
+          }
+        }
+      }
+      if (bc < lowest) {
+        lowest = bc;
+        best = bm;
       }
     }
-    rv_mv bmv = c4[0];
-#pragma unroll
-    for (int k = 1; k < kDsWaves; k++)
-      if (bp == k) bmv = c4[k];
-    if (pred_phase) {
-      if (best < center_cost) {
+    center = best;
+    center_cost = lowest;
+  } else {
+    // ---- get_best_predictor, then diamond steps: one round loop -----------
+    // A round evaluates up to 4 candidates, one per wavefront: first the
+    // predictors in groups of 4 (the sequential strict-< scan of
+    // get_best_predictor, applied group by group in order, is the same
+    // first minimum), then the 4 pattern points of each diamond step.  One
+    // call site keeps a single inlined copy of the candidate code.
+    const int np = jb.n_pred < RV_DS_MAX_PRED ? jb.n_pred : RV_DS_MAX_PRED;
+    int16_t radius = a.subpel ? 4 : 16;
+    const int16_t radius_end = a.subpel ? (a.hp ? 1 : 2) : 8;
+    int p0 = 0;  // next predictor group; >= np once the diamond phase runs
+    // Every diamond move strictly lowers center_cost, so the loop ends; the
+    // bound only guarantees the grid drains whatever the inputs.
+    for (int iter = 0; iter < 4096 + RV_DS_MAX_PRED; iter++) {
+      const bool pred_phase = p0 < np;
+      rv_mv c4[kDsWaves];
+      int n;
+      if (pred_phase) {
+        n = np - p0 < kDsWaves ? np - p0 : kDsWaves;
+  #pragma unroll
+        for (int k = 0; k < kDsWaves; k++) c4[k] = jp->pred[p0 + (k < n ? k : 0)];
+      } else {
+        n = kDsWaves;
+        c4[0] = rv_mv{(int16_t)(center.row + radius), center.col};  // diamond_pattern
+        c4[1] = rv_mv{center.row, (int16_t)(center.col + radius)};
+        c4[2] = rv_mv{(int16_t)(center.row - radius), center.col};
+        c4[3] = rv_mv{center.row, (int16_t)(center.col - radius)};
+      }
+      uint64_t c;
+      if constexpr (SUB) {
+        c = sub_round(c4, n);
+      } else {
+        rv_mv mine = c4[0];
+  #pragma unroll
+        for (int k = 1; k < kDsWaves; k++)
+          if (wave == k) mine = c4[k];
+        c = wave < n ? eval_full(mine) : ~0ull;
+      }
+      if (lane == 0) scost[iter & 1][wave] = c;
+      __syncthreads();
+      uint64_t best = ~0ull;
+      int bp = 0;
+  #pragma unroll
+      for (int k = 0; k < kDsWaves; k++) {
+        const uint64_t v = scost[iter & 1][k];
+        if (k < n && v < best) {
+          best = v;
+          bp = k;
+        }
+      }
+      rv_mv bmv = c4[0];
+  #pragma unroll
+      for (int k = 1; k < kDsWaves; k++)
+        if (bp == k) bmv = c4[k];
+      if (pred_phase) {
+        if (best < center_cost) {
+          center = bmv;
+          center_cost = best;
+        }
+        p0 += kDsWaves;
+      } else if (center_cost <= best) {
+        if (radius == radius_end) break;
+        radius /= 2;
+      } else {
         center = bmv;
         center_cost = best;
       }
-      p0 += kDsWaves;
-    } else if (center_cost <= best) {
-      if (radius == radius_end) break;
-      radius /= 2;
-    } else {
-      center = bmv;
-      center_cost = best;
     }
   }
   if (a.evals) {
@@ -727,38 +782,58 @@ __global__ __launch_bounds__(kDsThreads) void diamond_kernel(DsArgs a) {
     return ds_cost(dist, mv, jb, a.hp);
   };
 
-  // get_best_predictor
   rv_mv center{0, 0};
   uint64_t center_cost = ~0ull;
-  const int np = jb.n_pred < RV_DS_MAX_PRED ? jb.n_pred : RV_DS_MAX_PRED;
-  for (int p = 0; p < np; p++) {
-    const uint64_t c = rd_cost(jb.pred[p]);
-    if (c < center_cost) {
-      center = jb.pred[p];
-      center_cost = c;
+  if (a.tele) {  // telescopic_subpel_search (src/me.rs:858-941)
+    center = a.start[job].best_mv;
+    center_cost = a.start[job].cost;
+    const int nsteps = a.hp ? 4 : 3;
+    for (int st = 0; st < nsteps; st++) {
+      const int16_t step = (int16_t)(8 >> st);
+      const rv_mv ctr = center;
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+          if (i == 1 && j == 1) continue;
+          const rv_mv cand{(int16_t)(ctr.row + step * (i - 1)), (int16_t)(ctr.col + step * (j - 1))};
+          const uint64_t c = rd_cost(cand);
+          if (c < center_cost) {
+            center_cost = c;
+            center = cand;
+          }
+        }
     }
-  }
-  int16_t radius = a.subpel ? 4 : 16;
-  const int16_t radius_end = a.subpel ? (a.hp ? 1 : 2) : 8;
-  const int16_t pat[4][2] = {{1, 0}, {0, 1}, {-1, 0}, {0, -1}};
-  for (int iter = 0; iter < 4096; iter++) {
-    uint64_t best = ~0ull;
-    rv_mv best_mv{0, 0};
-    for (int p = 0; p < 4; p++) {
-      const rv_mv cand{(int16_t)(center.row + radius * pat[p][0]),
-                       (int16_t)(center.col + radius * pat[p][1])};
-      const uint64_t c = rd_cost(cand);
-      if (c < best) {
-        best = c;
-        best_mv = cand;
+  } else {
+    // get_best_predictor
+    const int np = jb.n_pred < RV_DS_MAX_PRED ? jb.n_pred : RV_DS_MAX_PRED;
+    for (int p = 0; p < np; p++) {
+      const uint64_t c = rd_cost(jb.pred[p]);
+      if (c < center_cost) {
+        center = jb.pred[p];
+        center_cost = c;
       }
     }
-    if (center_cost <= best) {
-      if (radius == radius_end) break;
-      radius /= 2;
-    } else {
-      center = best_mv;
-      center_cost = best;
+    int16_t radius = a.subpel ? 4 : 16;
+    const int16_t radius_end = a.subpel ? (a.hp ? 1 : 2) : 8;
+    const int16_t pat[4][2] = {{1, 0}, {0, 1}, {-1, 0}, {0, -1}};
+    for (int iter = 0; iter < 4096; iter++) {
+      uint64_t best = ~0ull;
+      rv_mv best_mv{0, 0};
+      for (int p = 0; p < 4; p++) {
+        const rv_mv cand{(int16_t)(center.row + radius * pat[p][0]),
+                         (int16_t)(center.col + radius * pat[p][1])};
+        const uint64_t c = rd_cost(cand);
+        if (c < best) {
+          best = c;
+          best_mv = cand;
+        }
+      }
+      if (center_cost <= best) {
+        if (radius == radius_end) break;
+        radius /= 2;
+      } else {
+        center = best_mv;
+        center_cost = best;
+      }
     }
   }
   if (threadIdx.x == 0) {
@@ -802,6 +877,8 @@ using namespace rv;
 // Multi-reference form used by the replay driver: jobs [n_refs][n_per_ref],
 // job i searches refs[i / n_per_ref]; evals (optional) receives the
 // in-range candidate evaluations per job.
+static int ds_dispatch(DsArgs &a, void *stream);
+
 int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
                             const rv_ds_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
                             int subpixel, int use_satd, int allow_hp, int bit_depth,
@@ -833,6 +910,14 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
   a.bd = bit_depth;
   a.evals = d_evals;
   if (next) a.next = *next;
+  return ds_dispatch(a, stream);
+}
+
+// Launch a filled DsArgs: the wavefront-per-candidate fast path where it
+// applies (SAD, W,H in {16,32,64}), else the workgroup-per-candidate kernel.
+static int ds_dispatch(DsArgs &a, void *stream) {
+  const int n = a.n, blk_w = a.w, blk_h = a.h, subpixel = a.subpel;
+  const rv_plane *org = &a.org;
   hipStream_t s = rv_resolve_stream(stream);
   const bool fast = org->hbd ? try_fast<uint16_t>(a, s) : try_fast<uint8_t>(a, s);
   if (!fast) {
@@ -856,4 +941,36 @@ extern "C" int rv_diamond_search_batch(const rv_plane *org, const rv_plane *ref,
   if (!ref) return rv_set_error(RV_EINVAL, "rv_diamond_search_batch: null ref");
   return rv_diamond_search_multi(org, ref, 1, d_jobs, n, blk_w, blk_h, subpixel, use_satd,
                                  allow_hp, bit_depth, d_out, nullptr, nullptr, stream);
+}
+
+// telescopic_subpel_search (src/me.rs:858-941) for every job in one launch:
+// start[i] = (best_mv, lowest_cost) from the full-pel search (or the
+// use_satd recomputation, src/me.rs:232-253); out[i] = the result.
+extern "C" int rv_telescopic_subpel_batch(const rv_plane *org, const rv_plane *ref,
+                                          const rv_ds_job *d_jobs, const rv_fs_result *d_start,
+                                          int n, int blk_w, int blk_h, int use_satd,
+                                          int allow_hp, int bit_depth, rv_fs_result *d_out,
+                                          void *stream) {
+  auto p2 = [](int v) { return v >= 4 && v <= 128 && (v & (v - 1)) == 0; };
+  if (!org || !ref || !d_start || n < 0 || !p2(blk_w) || !p2(blk_h) || ref->hbd != org->hbd ||
+      (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) || (!org->hbd && bit_depth != 8))
+    return rv_set_error(RV_EINVAL, "rv_telescopic_subpel_batch: bad arguments");
+  if (n == 0) return RV_OK;
+  DsArgs a;
+  memset(&a, 0, sizeof(a));
+  a.org = *org;
+  a.ref[0] = *ref;
+  a.jobs = d_jobs;
+  a.out = d_out;
+  a.n = n;
+  a.n_per_ref = n;
+  a.w = blk_w;
+  a.h = blk_h;
+  a.subpel = 1;
+  a.satd = use_satd ? 1 : 0;
+  a.hp = allow_hp ? 1 : 0;
+  a.bd = bit_depth;
+  a.tele = 1;
+  a.start = d_start;
+  return ds_dispatch(a, stream);
 }

@@ -8,8 +8,8 @@
 //   src/predict.rs:255-338)            -> prediction in LDS
 //   diff (src/encoder.rs:1044-1058) + FwdTxfm2D::fht DCT_DCT
 //   (src/transform/forward.rs:1804-1899) -> coefficients in LDS
-//   quantize/dequantize stand-in (v / 8 * 8 on the top-left
-//   min(W,32) x min(H,32), the packed layout inverse_transform_add reads)
+//   quantize/dequantize stand-in (v / 8 * 8 on the first
+//   coded_tx_area entries of the W-stride raster, the slice quantize reads)
 //                                      -> packed coefficients to HBM
 //   inv_txfm2d_add (src/transform/inverse.rs:1939-2114)
 //                                      -> reconstruction in LDS + HBM
@@ -215,30 +215,46 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     for (int r = 0; r < N; r++) buf[r * S + lane] = rdo_rsa(v[r], -s1);
   }
   wave_sync();
-  if (lane < C32) {
+  // The stand-in consumes the first coded_tx_area = C32 * C32 entries of
+  // the W-stride raster -- what quantize and the tx-domain zip read
+  // (src/encoder.rs:1152-1156, 1210-1219): for 64x64 that is raster rows
+  // 0..15, so only those rows need the row pass.
+  constexpr int CA = C32 * C32, RR = CA / N;  // coded area, raster rows it spans
+  if (lane < RR) {
     int32_t v[N];
 #pragma unroll
     for (int c = 0; c < N; c++) v[c] = buf[lane * S + c];
     tx::fwd1d<1, N>(v, v);
 #pragma unroll
-    for (int c = 0; c < C32; c++) buf[lane * S + c] = (rdo_rsa(v[c], -s2) / kQstep) * kQstep;
+    for (int c = 0; c < N; c++) buf[lane * S + c] = (rdo_rsa(v[c], -s2) / kQstep) * kQstep;
   }
   wave_sync();
-  // packed coefficients (row stride min(W,32)), coalesced
+  // packed coefficients = raster entries 0..CA-1 (row stride min(W,32) for
+  // inverse_transform_add), coalesced
   {
-    int32_t *pk = pl.packed + (int64_t)t * C32 * C32;
+    int32_t *pk = pl.packed + (int64_t)t * CA;
 #pragma unroll 4
-    for (int i = lane; i < C32 * C32; i += 64) pk[i] = buf[(i / C32) * S + (i % C32)];
+    for (int i = lane; i < CA; i += 64) pk[i] = buf[(i / N) * S + (i % N)];
   }
   // ---- D. inverse: rows of the coded coefficients, then columns + add ------
+  // input row rr of the C32 x C32 block = packed[rr * C32 ..] = raster
+  // entries rr * C32 ..; all reads precede the in-place row writes
   const int range = bd + 8;
-  if (lane < C32) {
+  {
     int32_t v[N];
+    if (lane < C32) {
 #pragma unroll
-    for (int c = 0; c < N; c++) v[c] = c < C32 ? tx::clampv(buf[lane * S + c], range) : 0;
-    tx::inv1d<1, N>(v, range);
+      for (int c = 0; c < N; c++) {
+        const int i = lane * C32 + c;
+        v[c] = c < C32 ? tx::clampv(buf[(i / N) * S + (i % N)], range) : 0;
+      }
+    }
+    wave_sync();
+    if (lane < C32) {
+      tx::inv1d<1, N>(v, range);
 #pragma unroll
-    for (int c = 0; c < N; c++) buf[lane * S + c] = v[c];
+      for (int c = 0; c < N; c++) buf[lane * S + c] = v[c];
+    }
   }
   wave_sync();
   if (lane < N) {

@@ -213,13 +213,8 @@ class _DsCtx(C.Structure):
                 ("satd", C.c_int), ("allow_hp", C.c_int)]
 
 
-def diamond_search(org_full, ref_full, xorigin, yorigin, width, height, job, w, h, subpel,
-                   satd, allow_hp, bd):
-    """orc_diamond_search for one DS_JOB record on full padded arrays (both
-    planes share the geometry).  Returns ((row, col), cost)."""
-    L = lib()
-    L.orc_diamond_search.argtypes = [C.POINTER(_DsCtx), C.POINTER(_Mv), C.c_int,
-                                     C.POINTER(_Mv), C.POINTER(C.c_uint64)]
+def _ds_ctx(org_full, ref_full, xorigin, yorigin, width, height, job, w, h, subpel, satd,
+            allow_hp, bd):
     c = _DsCtx()
     c.org = ptr(org_full, yorigin * org_full.shape[1] + xorigin)
     c.org_stride = org_full.shape[1]
@@ -235,6 +230,18 @@ def diamond_search(org_full, ref_full, xorigin, yorigin, width, height, job, w, 
     c.pmv[1] = _Mv(int(job["pmv1_row"]), int(job["pmv1_col"]))
     c.lambda_ = int(job["lambda_"])
     c.subpel, c.satd, c.allow_hp = int(subpel), int(satd), int(allow_hp)
+    return c
+
+
+def diamond_search(org_full, ref_full, xorigin, yorigin, width, height, job, w, h, subpel,
+                   satd, allow_hp, bd):
+    """orc_diamond_search for one DS_JOB record on full padded arrays (both
+    planes share the geometry).  Returns ((row, col), cost)."""
+    L = lib()
+    L.orc_diamond_search.argtypes = [C.POINTER(_DsCtx), C.POINTER(_Mv), C.c_int,
+                                     C.POINTER(_Mv), C.POINTER(C.c_uint64)]
+    c = _ds_ctx(org_full, ref_full, xorigin, yorigin, width, height, job, w, h, subpel, satd,
+                allow_hp, bd)
     n = int(job["n_pred"])
     preds = (_Mv * max(1, n))(*[_Mv(int(job["pred"][k][0]), int(job["pred"][k][1]))
                                 for k in range(n)])
@@ -242,6 +249,28 @@ def diamond_search(org_full, ref_full, xorigin, yorigin, width, height, job, w, 
     cost = C.c_uint64(0)
     L.orc_diamond_search(C.byref(c), preds, n, C.byref(best), C.byref(cost))
     return (best.row, best.col), cost.value
+
+
+def telescopic_subpel(org_full, ref_full, xorigin, yorigin, width, height, job, w, h, satd,
+                      allow_hp, bd, start_mv, start_cost):
+    """orc_telescopic_subpel for one DS_JOB record; returns ((row, col), cost)."""
+    L = lib()
+    L.orc_telescopic_subpel.argtypes = [C.POINTER(_DsCtx), C.POINTER(_Mv), C.POINTER(C.c_uint64)]
+    c = _ds_ctx(org_full, ref_full, xorigin, yorigin, width, height, job, w, h, True, satd,
+                allow_hp, bd)
+    best = _Mv(int(start_mv[0]), int(start_mv[1]))
+    cost = C.c_uint64(int(start_cost))
+    L.orc_telescopic_subpel(C.byref(c), C.byref(best), C.byref(cost))
+    return (best.row, best.col), cost.value
+
+
+def tx_dist(coeffs, rcoeffs, tx_w, tx_h):
+    L = lib()
+    L.orc_tx_dist.restype = C.c_uint64
+    L.orc_tx_dist.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.int32)
+    rcoeffs = np.ascontiguousarray(rcoeffs, dtype=np.int32)
+    return int(L.orc_tx_dist(coeffs.ctypes.data, rcoeffs.ctypes.data, rcoeffs.size, tx_w, tx_h))
 
 
 class CpuReplay:

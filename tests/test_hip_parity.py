@@ -417,6 +417,45 @@ def test_diamond_subpel_edges_vs_oracle(bd):
         assert (got[k]["mv_row"], got[k]["mv_col"], got[k]["cost"]) == (mv[0], mv[1], cost), k
 
 
+@pytest.mark.parametrize("bd,w,h,satd", [
+    (8, 64, 64, False), (8, 32, 32, False), (10, 64, 64, False), (8, 16, 32, False),
+    (8, 16, 16, True), (10, 8, 8, True), (8, 8, 16, False),
+])
+def test_telescopic_subpel_vs_oracle(bd, w, h, satd):
+    """telescopic_subpel_search (src/me.rs:858-941): fast and generic paths."""
+    rng = np.random.default_rng(1300 + w + 3 * h + bd + satd)
+    po_, pr_, fo, fr, jobs, W, H = _ds_case(rng, bd, w, h, 20, False)
+    xo, yo = po_.desc.xorigin, po_.desc.yorigin
+    start = np.zeros(len(jobs), dtype=R.FS_RESULT)
+    for k in range(len(jobs)):  # full-pel starting points, some out of range
+        start[k]["mv_row"], start[k]["mv_col"] = 8 * rng.integers(-3, 4), 8 * rng.integers(-3, 4)
+        start[k]["cost"] = int(rng.integers(0, 1 << 22)) if k % 5 else 2 ** 64 - 1
+    for hp in (False, True):
+        got = R.telescopic_subpel_batch(po_, pr_, jobs, start, w, h, satd, hp, bd)
+        for k, j in enumerate(jobs):
+            mv, cost = O.telescopic_subpel(fo, fr, xo, yo, W, H, j, w, h, satd, hp, bd,
+                                           (start[k]["mv_row"], start[k]["mv_col"]),
+                                           start[k]["cost"])
+            assert (got[k]["mv_row"], got[k]["mv_col"], got[k]["cost"]) == (mv[0], mv[1], cost), \
+                (k, hp, got[k], mv, cost)
+
+
+@pytest.mark.parametrize("tx_size", [0, 1, 2, 3, 4, 9, 12, 17])
+def test_tx_dist_vs_oracle(tx_size):
+    """tx-domain distortion (src/encoder.rs:1210-1224), incl. i32-wrapping squares."""
+    rng = np.random.default_rng(1400 + tx_size)
+    tw, th = R.TxSize(tx_size).width, R.TxSize(tx_size).height
+    area = min(tw, 32) * min(th, 32)
+    n = 9
+    co = rng.integers(-40000, 40000, (n, tw * th)).astype(np.int32)
+    rc = (co[:, :area] // 8 * 8 + rng.integers(-3, 4, (n, area))).astype(np.int32)
+    co[0, :4] = [2 ** 31 - 1, -2 ** 31, 70000, -70000]  # wrapping squares
+    rc[0, :4] = [-2 ** 31, 2 ** 31 - 1, 0, 0]
+    got = R.tx_dist_batch(co, rc, tx_size)
+    for b in range(n):
+        assert int(got[b]) == O.tx_dist(co[b, :area], rc[b], tw, th), b
+
+
 # ---- frame layout -----------------------------------------------------------
 @pytest.mark.parametrize("hbd", [False, True])
 def test_pad_and_downsample_vs_oracle(hbd):

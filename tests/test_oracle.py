@@ -235,3 +235,20 @@ def test_cdef_dist_and_sse():
     diff = (big_a.astype(np.int64) - big_b) ** 2
     assert int(parts.sum()) == int(diff.sum())
     assert int(parts[0]) == int(diff[:4, :4].sum())
+
+
+def test_tx_dist_oracle_matches_restatement():
+    """orc_tx_dist vs a numpy restatement of src/encoder.rs:1210-1224 with
+    get_log_tx_scale (src/quantize.rs:34-39), incl. the i32 wrapping square
+    sign-extended to u64."""
+    rng = np.random.default_rng(77)
+    for tw, th in ((4, 4), (16, 16), (32, 32), (64, 64), (16, 64)):
+        area = min(tw, 32) * min(th, 32)
+        co = rng.integers(-60000, 60000, area).astype(np.int64)
+        rc = rng.integers(-60000, 60000, area).astype(np.int64)
+        e = ((co - rc + 2 ** 31) % 2 ** 32) - 2 ** 31
+        sq = ((e * e + 2 ** 31) % 2 ** 32) - 2 ** 31          # i32 wrap
+        d = sum(int(v) % 2 ** 64 for v in sq) % 2 ** 64  # `as u64` sign-extends
+        bits = 2 * (3 - ((tw * th > 256) + (tw * th > 1024)))
+        want = ((d + (1 << (bits - 1))) % 2 ** 64) >> bits
+        assert O.tx_dist(co.astype(np.int32), rc.astype(np.int32), tw, th) == want
