@@ -444,7 +444,7 @@ def test_telescopic_subpel_vs_oracle(bd, w, h, satd):
 def test_tx_dist_vs_oracle(tx_size):
     """tx-domain distortion (src/encoder.rs:1210-1224), incl. i32-wrapping squares."""
     rng = np.random.default_rng(1400 + tx_size)
-    tw, th = R.TxSize(tx_size).width, R.TxSize(tx_size).height
+    tw, th = R.TxSize(tx_size).width(), R.TxSize(tx_size).height()
     area = min(tw, 32) * min(th, 32)
     n = 9
     co = rng.integers(-40000, 40000, (n, tw * th)).astype(np.int32)
