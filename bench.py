@@ -35,7 +35,10 @@ CONFIGS = {  # name: (width, height, xdec, ydec, bit_depth)
     "2160p444": (3840, 2160, 0, 0, 8),
 }
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
-SAD_PEAK_PX = 256 * 4 * 32 * 2.4e9 * 4  # v_sad_u8: 4 |a-b| per lane-op, 128 lanes/clk/CU
+# v_sad_u8 issue peak: a wave64 VALU op takes 4 cycles on a SIMD (64 lanes
+# per CU-cycle over 4 SIMDs; tools/ubench/valu_rates.hip measures 0.87 of
+# it), 4 |a-b| per lane-op for u8, 2 for v_sad_u16
+SAD_PEAK_PX = 256 * 64 * 2.4e9 * 4
 
 
 def coarse_windows(W, H, R, scale, tile=(0, 0, 0, 0)):
@@ -129,6 +132,8 @@ def main():
     ap.add_argument("--refs", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--side-rdo", action="store_true",
+                    help="zero-MV RDO candidates on a second stream, concurrent with F0-F3")
     args = ap.parse_args()
 
     import rav1e_amd as R  # load the HIP library before anything else
@@ -143,7 +148,8 @@ def main():
     W, H, xdec, ydec, bd = CONFIGS[args.config]
     nref = args.refs
     frames = [RP.synth_frame(W, H, info.frame_offset + t, xdec, ydec, bd) for t in range(nref + 1)]
-    hip = RP.HipReplay(W, H, xdec, ydec, bd, nref)
+    hip = RP.HipReplay(W, H, xdec, ydec, bd, nref,
+                       flags=RP.RV_REPLAY_SIDE_RDO if args.side_rdo else 0)
     for s, f in enumerate(frames):
         hip.set_frame(s, f)
     scales = RP.GOP_SCALES
@@ -171,19 +177,21 @@ def main():
                       2 * nctx * ((cw + 7) * (ch + 7) * px + 2 * cw * ch * px +
                                   4 * ntx_c * 32 * 32 + 8 * csub + 16 + 24 * ntx_c))
     kernels = {
-        "full_search": dict(ms=float(ms[1]), launches=nref, bytes=fs_bytes, sad_px=fs_ops),
+        "full_search": dict(ms=float(ms[1]), launches=1, bytes=fs_bytes, sad_px=fs_ops),
         "diamond_fullpel_64": dict(ms=float(ms[6]), launches=1,
                                    bytes=nj * (64 * 64 * px + 80) +
                                    ev_full / ev_frames * 64 * 64 * px),
         "diamond_subpel_64": dict(ms=float(ms[7]), launches=1,
                                   bytes=nj * (64 * 64 * px + 80) +
                                   ev_sub / ev_frames * 71 * 71 * px),
-        # F4 is two launches of the same kernel: the sub-pel-MV candidates on
-        # the replay stream and the zero-MV candidates on a second stream
-        # (concurrent with F0-F3); each covers half of the candidates
-        "rdo_candidates": dict(ms=float(ms[8]), launches=1, bytes=rdo_bytes / 2),
-        "rdo_candidates_zero_mv": dict(ms=float(ms[9]), launches=1, bytes=rdo_bytes / 2),
+        # F4: one fused launch over every candidate; with --side-rdo two launches
+        # (sub-pel-MV candidates on the replay stream, zero-MV candidates on a
+        # second stream concurrent with F0-F3), each half of the candidates
+        "rdo_candidates": dict(ms=float(ms[8]), launches=1,
+                               bytes=rdo_bytes / 2 if args.side_rdo else rdo_bytes),
     }
+    if args.side_rdo:
+        kernels["rdo_candidates_zero_mv"] = dict(ms=float(ms[9]), launches=1, bytes=rdo_bytes / 2)
     dom = max(kernels, key=lambda n: kernels[n]["ms"])
     kd = kernels[dom]
     launch_s = kd["ms"] / 1e3 / kd["launches"]
@@ -195,8 +203,10 @@ def main():
             "algorithmic_bytes_per_launch": round(kd["bytes"] / kd["launches"])}
     if dom == "full_search":
         achv = kd["sad_px"] / (kd["ms"] / 1e3) / 1e12
-        roof["valu"] = {"achieved": round(achv, 3), "peak": round(SAD_PEAK_PX / 1e12, 1),
-                        "unit": "T |a-b|/s (v_sad_u8)", "frac": round(achv * 1e12 / SAD_PEAK_PX, 4)}
+        peak = SAD_PEAK_PX / (2 if bd > 8 else 1)
+        roof["valu"] = {"achieved": round(achv, 3), "peak": round(peak / 1e12, 1),
+                        "unit": "T |a-b|/s (v_sad_u8 / v_sad_u16)",
+                        "frac": round(achv * 1e12 / peak, 4)}
     fps = world * args.steps / dt
 
     cpu = None

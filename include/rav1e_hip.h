@@ -317,8 +317,13 @@ typedef struct rv_replay_cfg {
   int32_t tile_w, tile_h;     /* (a whole frame: 0, 0, sb_cols, sb_rows) */
   int32_t n_refs;             /* reference frames searched per frame */
   int32_t rdo_candidates;     /* inter candidates per superblock */
-  int32_t flags;              /* reserved, 0 */
+  int32_t flags;              /* RV_REPLAY_* bits, 0 = default */
 } rv_replay_cfg;
+/* flags: run the zero-MV RDO candidates (which need no motion search) on a
+ * second stream concurrently with F0-F3 instead of in the main stream's F4
+ * launch.  Measured neutral at 1080p and -2% at 4K on MI355X, so off by
+ * default. */
+#define RV_REPLAY_SIDE_RDO 1
 typedef struct rv_replay rv_replay;
 /* Allocate device state for one tile; frames are uploaded with
  * rv_replay_set_frame.  NULL on failure. */

@@ -650,13 +650,16 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
     ca.sub_w = (g.cw < 8 ? g.cw : 8) >> g.xdec;
     ca.sub_h = (g.ch < 8 ? g.ch : 8) >> g.ydec;
   }
+  const bool serial = (r->cfg.flags & RV_REPLAY_SIDE_RDO) == 0;
   RV_H(hipEventRecord(r->fork[slot], st));
-  RV_H(hipStreamWaitEvent(r->side, r->fork[slot], 0));
-  la.k_sel = ca.k_sel = 1;
-  RV_H(hipEventRecord(e[9], r->side));
-  RV_R(rv_rdo_candidates(la, ca, g.hbd, r->side));
-  RV_H(hipEventRecord(e[10], r->side));
-  RV_H(hipEventRecord(r->join[slot], r->side));
+  if (!serial) {
+    RV_H(hipStreamWaitEvent(r->side, r->fork[slot], 0));
+    la.k_sel = ca.k_sel = 1;
+    RV_H(hipEventRecord(e[9], r->side));
+    RV_R(rv_rdo_candidates(la, ca, g.hbd, r->side));
+    RV_H(hipEventRecord(e[10], r->side));
+    RV_H(hipEventRecord(r->join[slot], r->side));
+  }
   // F0 hres + qres of the input (encode_frame, src/encoder.rs:3382-3385)
   RV_R(rv_plane_pyramid(&cur.y, &cur.hres, &cur.qres, st));
   RV_H(hipEventRecord(e[1], st));
@@ -676,11 +679,23 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub, nr, 64, 64, 1, 0, 0, g.bd,
                                r->sub, ev_sub, &to_mc, st));
   RV_H(hipEventRecord(e[4], st));
-  // F4 sub-pel MV candidates: luma + both chroma planes in one fused launch
-  la.k_sel = ca.k_sel = 0;
+  // F4 sub-pel MV candidates (all candidates when serial): luma + both
+  // chroma planes in one fused launch
+  if (serial) {
+    la.k_sel = ca.k_sel = -1;
+    la.n_tx *= 2;
+    ca.n_tx *= 2;
+  } else {
+    la.k_sel = ca.k_sel = 0;
+  }
   RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
   RV_H(hipEventRecord(e[8], st));
-  RV_H(hipStreamWaitEvent(st, r->join[slot], 0));
+  if (serial) {  // empty side bracket
+    RV_H(hipEventRecord(e[9], st));
+    RV_H(hipEventRecord(e[10], st));
+  } else {
+    RV_H(hipStreamWaitEvent(st, r->join[slot], 0));
+  }
   score_candidates<<<g.nsb, 64, 0, st>>>(g, r->l_mom, r->u_sse, r->v_sse, r->lsub, r->csub,
                                          r->coarse, r->half, r->full, r->sub, r->words,
                                          r->tail + 2);

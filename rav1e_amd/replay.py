@@ -14,6 +14,8 @@ import numpy as np
 
 from . import RvReplayCfg, _check, lib
 
+RV_REPLAY_SIDE_RDO = 1  # include/rav1e_hip.h
+
 # GOP of the reference's reorder pyramid (src/api/internal.rs:61-95):
 # group_input_len 4, levels 0,1,2,2 -> me_range_scale = 4 >> level
 # (src/encoder.rs:838).
@@ -72,10 +74,11 @@ class HipReplay:
     """The GPU replay of one tile (rv_replay_create ... rv_replay_destroy)."""
 
     def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, tile=None,
-                 stream=None):
+                 stream=None, flags=0):
         cfg = RvReplayCfg()
         cfg.width, cfg.height, cfg.xdec, cfg.ydec = width, height, xdec, ydec
         cfg.bit_depth, cfg.n_refs, cfg.rdo_candidates = bit_depth, n_refs, 2 * n_refs
+        cfg.flags = flags
         if tile:
             cfg.tile_x0, cfg.tile_y0, cfg.tile_w, cfg.tile_h = tile
         self.cfg = cfg

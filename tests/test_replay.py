@@ -53,11 +53,12 @@ def test_cpu_replay_thread_invariant():
     (256, 128, 1, 1, 10, 2, None),
     (384, 192, 1, 1, 8, 2, (2, 0, 4, 3)),
 ])
-def test_gpu_replay_matches_cpu_replay(w, h, xdec, ydec, bd, refs, tile):
+@pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_SIDE_RDO])
+def test_gpu_replay_matches_cpu_replay(w, h, xdec, ydec, bd, refs, tile, flags):
     import rav1e_amd as R
     R.require_device(0)
     fr = _frames(w, h, xdec, ydec, bd, refs + 1)
-    g = RP.HipReplay(w, h, xdec, ydec, bd, refs, tile=tile)
+    g = RP.HipReplay(w, h, xdec, ydec, bd, refs, tile=tile, flags=flags)
     c = O.CpuReplay(w, h, xdec, ydec, bd, refs, tile=tile, threads=4)
     for s, f in enumerate(fr):
         g.set_frame(s, f)
