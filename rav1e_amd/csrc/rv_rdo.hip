@@ -71,16 +71,20 @@ __device__ __forceinline__ int32_t rdo_rsa(int32_t v, int bit) {
   return v;
 }
 
-template <typename Px, int N, bool MOMENTS>
+// LPB = lanes per transform block: 64 (luma, N = 64) or 32 (chroma, N = 32:
+// a wavefront carries two chroma blocks, one per half, so every phase keeps
+// all 64 lanes busy).  `valid` = false for a second half without a block:
+// it recomputes its partner's block and stores nothing.
+template <typename Px, int N, bool MOMENTS, int LPB>
 __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &pl, int t,
-                                              int32_t *buf, Px *pred) {
+                                              bool valid, int32_t *buf, Px *pred) {
   constexpr int B = (int)sizeof(Px);
   constexpr int S = N + 1;                       // padded LDS row (i32)
-  constexpr int G = 64 / N, RG = N / G;          // MC lane groups
+  constexpr int G = LPB / N, RG = N / G;         // MC lane groups
   constexpr int P = B == 1 ? ((N + 8 + 15) / 16) * 16 : ((2 * (N + 8) + 15) / 16) * 16;
   constexpr int C32 = N < 32 ? N : 32;           // coded coefficient extent
   static_assert((N + 7) * P <= N * S * 4, "window must fit the coefficient slab");
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (LPB - 1);
   const int cand = t / a.ntx_per_cand;
   const rv_mc_job mj = pl.mc[cand];
   const rv_tx_job tj = pl.tx[t];
@@ -101,7 +105,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     constexpr int kRowDw = ((N + 7) * B + 3) / 4;
     constexpr int kTot = (N + 7) * kRowDw;
 #pragma unroll 4
-    for (int i = lane; i < kTot; i += 64) {
+    for (int i = lane; i < kTot; i += LPB) {
       const int r = i / kRowDw, d = i - r * kRowDw;
       uint32_t v;
       __builtin_memcpy(&v, sp + r * rs + 4 * d, 4);
@@ -191,7 +195,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     const uint8_t *op = (const uint8_t *)plane_ptr<Px>(pl.org, tj.src_x, tj.src_y);
     const int64_t os = (int64_t)pl.org.stride * B;
 #pragma unroll 8
-    for (int i = lane; i < N * DPR; i += 64) {
+    for (int i = lane; i < N * DPR; i += LPB) {
       const int r = i / DPR, c = (i - r * DPR) * PPD;
       uint32_t ov, pv;
       __builtin_memcpy(&ov, op + r * os + c * B, 4);
@@ -233,8 +237,9 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   // inverse_transform_add), coalesced
   {
     int32_t *pk = pl.packed + (int64_t)t * CA;
+    if (valid)
 #pragma unroll 4
-    for (int i = lane; i < CA; i += 64) pk[i] = buf[(i / N) * S + (i % N)];
+      for (int i = lane; i < CA; i += LPB) pk[i] = buf[(i / N) * S + (i % N)];
   }
   // ---- D. inverse: rows of the coded coefficients, then columns + add ------
   // input row rr of the C32 x C32 block = packed[rr * C32 ..] = raster
@@ -277,11 +282,11 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     uint8_t *dp = (uint8_t *)plane_ptr_mut<Px>(pl.dst, tj.pred_x, tj.pred_y);
     const int64_t ds = (int64_t)pl.dst.stride * B;
 #pragma unroll 8
-    for (int i = lane; i < N * DPR; i += 64) {
+    for (int i = lane; i < N * DPR; i += LPB) {
       const int r = i / DPR, c = (i - r * DPR) * PPD;
       uint32_t v;
       __builtin_memcpy(&v, pred + r * N + c, 4);
-      __builtin_memcpy(dp + r * ds + c * B, &v, 4);
+      if (valid) __builtin_memcpy(dp + r * ds + c * B, &v, 4);
     }
   }
   // ---- E. distortion partials of org vs reconstruction ---------------------
@@ -289,7 +294,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   if constexpr (MOMENTS) {
     constexpr int NB = N / 8;  // 8x8 blocks per row of this transform block
     const int sub_x = a.mb_w / 8, nsub = sub_x * (a.mb_h / 8);
-    for (int k = lane; k < NB * NB; k += 64) {
+    for (int k = lane; k < NB * NB; k += LPB) {
       const int by = k / NB, bx = k - by * NB;
       int32_t ss = 0, sd = 0;
       int64_t ss2 = 0, sd2 = 0, ssd = 0;
@@ -307,6 +312,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
         }
       const int kk = ((oy >> 3) + by) * sub_x + (ox >> 3) + bx;
       int64_t *m = (int64_t *)pl.dist + ((int64_t)cand * nsub + kk) * 5;
+      if (!valid) continue;
       m[0] = ss;
       m[1] = sd;
       m[2] = ss2;
@@ -317,7 +323,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     const int bw = a.sub_w, bh = a.sub_h;
     const int nbx = N / bw, nby = N / bh;
     const int sub_x = a.mb_w / bw, nsub = sub_x * (a.mb_h / bh);
-    for (int k = lane; k < nbx * nby; k += 64) {
+    for (int k = lane; k < nbx * nby; k += LPB) {
       const int by = k / nbx, bx = k - by * nbx;
       uint64_t value = 0;
       for (int j = 0; j < bh; j++) {
@@ -330,7 +336,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
         value += row;
       }
       const int kk = (oy / bh + by) * sub_x + ox / bw + bx;
-      ((uint64_t *)pl.dist)[(int64_t)cand * nsub + kk] = value;
+      if (valid) ((uint64_t *)pl.dist)[(int64_t)cand * nsub + kk] = value;
     }
   }
 }
@@ -349,18 +355,25 @@ __device__ __forceinline__ int rdo_task(const RdoArgs &a, int i) {
   return ((2 * r + a.k_sel) * a.nsb + sb) * a.ntx_per_cand + sub;
 }
 
+// Blocks [0, luma.n_tx) are luma candidates (one per wavefront); the rest
+// carry chroma transform blocks two per wavefront, plane U then V.
 template <typename Px>
 __global__ __launch_bounds__(64) void rdo_frame_kernel(RdoArgs luma, RdoArgs chroma) {
   __shared__ int32_t buf[64 * 65];
   __shared__ Px pred[64 * 64];
   int b = blockIdx.x;
   if (b < luma.n_tx) {
-    rdo_cand_body<Px, 64, true>(luma, luma.p[0], rdo_task(luma, b), buf, pred);
+    rdo_cand_body<Px, 64, true, 64>(luma, luma.p[0], rdo_task(luma, b), true, buf, pred);
   } else {
     b -= luma.n_tx;
-    const int plane = b / chroma.n_tx;
-    rdo_cand_body<Px, 32, false>(chroma, chroma.p[plane],
-                                 rdo_task(chroma, b - plane * chroma.n_tx), buf, pred);
+    const int pairs = (chroma.n_tx + 1) / 2;
+    const int plane = b / pairs;
+    const int half = threadIdx.x >> 5;
+    int i = 2 * (b - plane * pairs) + half;
+    const bool valid = i < chroma.n_tx;
+    if (!valid) i -= 1;
+    rdo_cand_body<Px, 32, false, 32>(chroma, chroma.p[plane], rdo_task(chroma, i), valid,
+                                     buf + half * 32 * 33, pred + half * 32 * 32);
   }
 }
 
@@ -371,7 +384,7 @@ using namespace rv;
 // Replay-internal entry (rv_replay.hip): luma (N = 64, moments) and both
 // chroma planes (N = 32, SSE) of every candidate in one launch.
 int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s) {
-  const unsigned grid = (unsigned)(luma.n_tx + 2 * chroma.n_tx);
+  const unsigned grid = (unsigned)(luma.n_tx + 2 * ((chroma.n_tx + 1) / 2));
   if (grid == 0) return RV_OK;
   if (hbd)
     rdo_frame_kernel<uint16_t><<<grid, 64, 0, s>>>(luma, chroma);
