@@ -132,6 +132,8 @@ def main():
     ap.add_argument("--refs", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--split-rdo", action="store_true",
+                    help="F4 luma and chroma candidate kernels on two concurrent streams")
     ap.add_argument("--side-rdo", action="store_true",
                     help="zero-MV RDO candidates on a second stream, concurrent with F0-F3")
     args = ap.parse_args()
@@ -149,7 +151,8 @@ def main():
     nref = args.refs
     frames = [RP.synth_frame(W, H, info.frame_offset + t, xdec, ydec, bd) for t in range(nref + 1)]
     hip = RP.HipReplay(W, H, xdec, ydec, bd, nref,
-                       flags=RP.RV_REPLAY_SIDE_RDO if args.side_rdo else 0)
+                       flags=(RP.RV_REPLAY_SIDE_RDO if args.side_rdo else 0) |
+                       (RP.RV_REPLAY_SPLIT_RDO if args.split_rdo else 0))
     for s, f in enumerate(frames):
         hip.set_frame(s, f)
     scales = RP.GOP_SCALES

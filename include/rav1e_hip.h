@@ -324,6 +324,9 @@ typedef struct rv_replay_cfg {
  * launch.  Measured neutral at 1080p and -2% at 4K on MI355X, so off by
  * default. */
 #define RV_REPLAY_SIDE_RDO 1
+/* flags: F4 luma candidates on the replay stream and the chroma transform
+ * blocks concurrently on a second stream (separate, smaller-LDS kernel). */
+#define RV_REPLAY_SPLIT_RDO 2
 typedef struct rv_replay rv_replay;
 /* Allocate device state for one tile; frames are uploaded with
  * rv_replay_set_frame.  NULL on failure. */

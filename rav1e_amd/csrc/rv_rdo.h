@@ -33,4 +33,4 @@ struct RdoArgs {
 // Luma candidates (64x64 transform, cdef moments) and the chroma transform
 // blocks of planes U and V (32x32, SSE partials) in one launch.
 int rv_rdo_candidates(const rv::RdoArgs &luma, const rv::RdoArgs &chroma, int hbd,
-                      hipStream_t s);
+                      hipStream_t s, hipStream_t chroma_stream = nullptr);

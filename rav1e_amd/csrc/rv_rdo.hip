@@ -358,23 +358,36 @@ __device__ __forceinline__ int rdo_task(const RdoArgs &a, int i) {
 // Blocks [0, luma.n_tx) are luma candidates (one per wavefront); the rest
 // carry chroma transform blocks two per wavefront, plane U then V.
 template <typename Px>
+__device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, int32_t *buf,
+                                                Px *pred) {
+  const int pairs = (chroma.n_tx + 1) / 2;
+  const int plane = b / pairs;
+  const int half = threadIdx.x >> 5;
+  int i = 2 * (b - plane * pairs) + half;
+  const bool valid = i < chroma.n_tx;
+  if (!valid) i -= 1;
+  rdo_cand_body<Px, 32, false, 32>(chroma, chroma.p[plane], rdo_task(chroma, i), valid,
+                                   buf + half * 32 * 33, pred + half * 32 * 32);
+}
+
+template <typename Px>
 __global__ __launch_bounds__(64) void rdo_frame_kernel(RdoArgs luma, RdoArgs chroma) {
   __shared__ int32_t buf[64 * 65];
   __shared__ Px pred[64 * 64];
-  int b = blockIdx.x;
-  if (b < luma.n_tx) {
+  const int b = blockIdx.x;
+  if (b < luma.n_tx)
     rdo_cand_body<Px, 64, true, 64>(luma, luma.p[0], rdo_task(luma, b), true, buf, pred);
-  } else {
-    b -= luma.n_tx;
-    const int pairs = (chroma.n_tx + 1) / 2;
-    const int plane = b / pairs;
-    const int half = threadIdx.x >> 5;
-    int i = 2 * (b - plane * pairs) + half;
-    const bool valid = i < chroma.n_tx;
-    if (!valid) i -= 1;
-    rdo_cand_body<Px, 32, false, 32>(chroma, chroma.p[plane], rdo_task(chroma, i), valid,
-                                     buf + half * 32 * 33, pred + half * 32 * 32);
-  }
+  else
+    rdo_chroma_pair<Px>(chroma, b - luma.n_tx, buf, pred);
+}
+
+// Chroma pairs alone (10.5 KiB of LDS instead of the luma slab's 20.7 KiB,
+// so about twice the resident wavefronts), for a second stream.
+template <typename Px>
+__global__ __launch_bounds__(64) void rdo_chroma_kernel(RdoArgs chroma) {
+  __shared__ int32_t buf[2 * 32 * 33];
+  __shared__ Px pred[2 * 32 * 32];
+  rdo_chroma_pair<Px>(chroma, blockIdx.x, buf, pred);
 }
 
 }  // namespace rv
@@ -382,9 +395,29 @@ __global__ __launch_bounds__(64) void rdo_frame_kernel(RdoArgs luma, RdoArgs chr
 using namespace rv;
 
 // Replay-internal entry (rv_replay.hip): luma (N = 64, moments) and both
-// chroma planes (N = 32, SSE) of every candidate in one launch.
-int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s) {
-  const unsigned grid = (unsigned)(luma.n_tx + 2 * ((chroma.n_tx + 1) / 2));
+// chroma planes (N = 32, SSE) of every candidate.  One launch on `s`, or,
+// with a second stream `cs`, the luma candidates on `s` and the chroma
+// pairs concurrently on `cs` (the caller orders `cs` after the MC jobs).
+int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s,
+                      hipStream_t cs) {
+  const unsigned cpairs = (unsigned)(2 * ((chroma.n_tx + 1) / 2));
+  if (cs) {
+    RdoArgs l = luma, c = chroma;
+    l.n_tx = luma.n_tx;
+    if (luma.n_tx) {
+      RdoArgs none = chroma;
+      none.n_tx = 0;
+      if (hbd) rdo_frame_kernel<uint16_t><<<luma.n_tx, 64, 0, s>>>(l, none);
+      else rdo_frame_kernel<uint8_t><<<luma.n_tx, 64, 0, s>>>(l, none);
+    }
+    if (cpairs) {
+      if (hbd) rdo_chroma_kernel<uint16_t><<<cpairs, 64, 0, cs>>>(c);
+      else rdo_chroma_kernel<uint8_t><<<cpairs, 64, 0, cs>>>(c);
+    }
+    RV_HIP_CHECK_LAUNCH();
+    return RV_OK;
+  }
+  const unsigned grid = (unsigned)luma.n_tx + cpairs;
   if (grid == 0) return RV_OK;
   if (hbd)
     rdo_frame_kernel<uint16_t><<<grid, 64, 0, s>>>(luma, chroma);

@@ -226,7 +226,7 @@ struct rv_replay {
   static constexpr int kRing = 64;
   static constexpr int kEv = 11;  // + [9,10]: side-stream RDO bracket
   hipEvent_t evs[kRing][kEv];
-  hipEvent_t fork[kRing], join[kRing];  // cross-stream ordering only
+  hipEvent_t fork[kRing], join[kRing], fork2[kRing], join2[kRing];  // cross-stream ordering
   hipEvent_t *ev;
   long frames = 0;
   // diamond candidate evaluations per job, per ring slot: [kRing][2][nsb*R]
@@ -417,6 +417,8 @@ void rv_replay_destroy(rv_replay *r) {
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
     if (r->fork[f]) (void)hipEventDestroy(r->fork[f]);
     if (r->join[f]) (void)hipEventDestroy(r->join[f]);
+    if (r->fork2[f]) (void)hipEventDestroy(r->fork2[f]);
+    if (r->join2[f]) (void)hipEventDestroy(r->join2[f]);
   }
   if (r->side) (void)hipStreamDestroy(r->side);
   if (r->own_stream && r->stream) (void)hipStreamDestroy(r->stream);
@@ -435,6 +437,8 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   memset(r->evs, 0, sizeof(r->evs));
   memset(r->fork, 0, sizeof(r->fork));
   memset(r->join, 0, sizeof(r->join));
+  memset(r->fork2, 0, sizeof(r->fork2));
+  memset(r->join2, 0, sizeof(r->join2));
   r->side = nullptr;
   r->ev = r->evs[0];
   r->cfg = *cfg;
@@ -520,6 +524,8 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
       ok = ok && hipEventCreateWithFlags(&r->evs[f][i], hipEventDisableSystemFence) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&r->fork[f], hipEventDisableTiming) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&r->join[f], hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&r->fork2[f], hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&r->join2[f], hipEventDisableTiming) == hipSuccess;
   }
   ok = ok && hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking) == hipSuccess;
   const size_t ev_bytes = (size_t)rv_replay::kRing * 2 * nr * 4;
@@ -688,7 +694,16 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   } else {
     la.k_sel = ca.k_sel = 0;
   }
-  RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
+  const bool split = serial && (r->cfg.flags & RV_REPLAY_SPLIT_RDO) != 0;
+  if (split) {  // luma here, chroma pairs concurrently on the side stream
+    RV_H(hipEventRecord(r->fork2[slot], st));
+    RV_H(hipStreamWaitEvent(r->side, r->fork2[slot], 0));
+    RV_R(rv_rdo_candidates(la, ca, g.hbd, st, r->side));
+    RV_H(hipEventRecord(r->join2[slot], r->side));
+    RV_H(hipStreamWaitEvent(st, r->join2[slot], 0));
+  } else {
+    RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
+  }
   RV_H(hipEventRecord(e[8], st));
   if (serial) {  // empty side bracket
     RV_H(hipEventRecord(e[9], st));

@@ -15,6 +15,7 @@ import numpy as np
 from . import RvReplayCfg, _check, lib
 
 RV_REPLAY_SIDE_RDO = 1  # include/rav1e_hip.h
+RV_REPLAY_SPLIT_RDO = 2
 
 # GOP of the reference's reorder pyramid (src/api/internal.rs:61-95):
 # group_input_len 4, levels 0,1,2,2 -> me_range_scale = 4 >> level
