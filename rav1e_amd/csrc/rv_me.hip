@@ -14,6 +14,7 @@
 // v_sad_u8 on packed dwords (v_alignbyte for the 3 unaligned shifts), so a
 // reference row is read from LDS once per 32 candidates.  The search is
 // VALU-bound (~256 |a-b| per candidate), not HBM-bound.
+#include <stdlib.h>
 #include <string.h>
 
 #include "rv_chain.h"
@@ -34,6 +35,15 @@ __device__ __forceinline__ uint32_t mv_rate(int16_t row, int16_t col,
                                             rv_mv p, int hp) {
   return diff_to_rate((int16_t)(row - p.row), hp) +
          diff_to_rate((int16_t)(col - p.col), hp);
+}
+
+__device__ __forceinline__ uint64_t group_min_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t w = __shfl_xor(v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
 }
 
 struct Best {
@@ -352,9 +362,267 @@ __global__ __launch_bounds__(kFsThreads) void fs16_kernel(FsArgs a) {
   }
 }
 
+// ---- exact successive-elimination path: u8, 16x16, step 1 ----------------
+// The triangle inequality bounds every candidate from below:
+//   SAD(org, cand) >= sum over the four 8x8 quadrants q of |S_org,q - S_cand,q|
+// (S = pixel sum), so cost >= LB = 256 * that + rate * lambda.  A candidate
+// whose LB exceeds an achieved cost UB cannot be the strict first minimum,
+// so skipping it leaves the result of full_search (src/me.rs:943-990)
+// unchanged bit for bit.  Per band: (A) the 8x8 box sums S8 of every
+// candidate position go to LDS (horizontal 8-sums by v_sad_u8 against zero,
+// vertical by a sliding register ring); (B) every lane takes the
+// minimum-LB candidate of its tiles and evaluates it exactly -> UB (carried
+// across bands); (C) the candidates with LB <= UB are compacted and
+// evaluated exactly, spread over all lanes.
+constexpr int kSeaLdsBytes = 48 * 1024;
+constexpr int kSeaMaxTiles = 512;
+
+__device__ __forceinline__ uint32_t sum8_u8(const uint32_t *row, int x) {
+  const int d = x >> 2, sh = x & 3;
+  const uint32_t w0 = row[d], w1 = row[d + 1], w2 = row[d + 2];
+  return __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, sh), 0u,
+                                 __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w2, w1, sh), 0u, 0u));
+}
+
+__global__ __launch_bounds__(kFsThreads) void fs16_sea_kernel(FsArgs a) {
+  extern __shared__ __align__(16) uint32_t sea_lds[];
+  __shared__ uint4 orgs[16];
+  __shared__ uint32_t so[4];
+  __shared__ uint32_t tmin[kSeaMaxTiles];
+  __shared__ uint32_t lmask[kSeaMaxTiles], ltile[kSeaMaxTiles], lpre[kSeaMaxTiles + 1];
+  __shared__ uint32_t cnt, ub_s;
+  const int job = fs_job_index();
+  if (job >= a.n) return;
+  const rv_fs_job jb = a.jobs[job];
+  const rv_plane &ref = a.ref[job / a.n_per_ref];
+  const int nx = jb.x_hi >= jb.x_lo ? jb.x_hi - jb.x_lo + 1 : 0;
+  const int ny = jb.y_hi >= jb.y_lo ? jb.y_hi - jb.y_lo + 1 : 0;
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    const uint8_t *o = plane_ptr<uint8_t>(a.org, jb.po_x, jb.po_y);
+    reinterpret_cast<uint32_t *>(orgs)[tid] =
+        load_u32_unaligned(o + (int64_t)(tid >> 2) * a.org.stride + 4 * (tid & 3));
+  }
+  if (tid == 0) ub_s = 0xffffffffu;
+  __syncthreads();
+  if (tid < 4) {  // quadrant sums of the source block
+    const uint32_t *ow = reinterpret_cast<const uint32_t *>(orgs);
+    uint32_t t = 0;
+    for (int r = 0; r < 8; r++)
+      for (int i = 0; i < 2; i++)
+        t = __builtin_amdgcn_sad_u8(ow[(8 * (tid >> 1) + r) * 4 + 2 * (tid & 1) + i], 0u, t);
+    so[tid] = t;
+  }
+  const int tx_n = (nx + 3) >> 2;
+  const int rw = tx_n + 4;             // band row length in dwords (pixels)
+  const int sw = 4 * tx_n + 8;         // S8 row length in u16 (candidate cols + 8)
+  const int vis_w = nx + 15;
+  // band rows: pixels (pb + 15) * rw * 4 + S8 (pb + 8) * sw * 2 <= budget
+  int pb = (kSeaLdsBytes - 4 - 15 * rw * 4 - 8 * sw * 2) / (rw * 4 + sw * 2);
+  pb = (pb / kTileRows) * kTileRows;
+  pb = pb > kSeaMaxTiles / tx_n * kTileRows ? kSeaMaxTiles / tx_n * kTileRows : pb;
+  // window too wide for the SEA band, or costs that may not fit u32
+  // (256 * sad < 2^24 needs lambda < 2^25): exhaustive path
+  if (pb < kTileRows || jb.lambda >= (1u << 25)) {
+    const rv_fs_result res = fs_generic_body<uint8_t>(a.org, ref, jb, 16, 16, 1, a.hp, a.out + job);
+    if (tid == 0) chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, res.best_mv);
+    return;
+  }
+  uint32_t *band = sea_lds;
+  // S8 rows are read as 8-byte uint2: start the table on an 8-byte boundary
+  uint16_t *s8 = reinterpret_cast<uint16_t *>(sea_lds + (((pb + 15) * rw + 1) & ~1));
+  uint64_t bkey = ~0ull;  // (u32 cost << 32 | raster index)
+  const uint8_t *rbase = plane_ptr<uint8_t>(ref, jb.x_lo, jb.y_lo);
+  auto rate_of = [&](int iy, int ix) -> uint32_t {
+    const int16_t row = (int16_t)(8 * (jb.y_lo + iy - jb.po_y));
+    const int16_t col = (int16_t)(8 * (jb.x_lo + ix - jb.po_x));
+    const uint32_t r1 = diff_to_rate((int16_t)(row - jb.pmv[0].row), a.hp) +
+                        diff_to_rate((int16_t)(col - jb.pmv[0].col), a.hp);
+    const uint32_t r2 = diff_to_rate((int16_t)(row - jb.pmv[1].row), a.hp) +
+                        diff_to_rate((int16_t)(col - jb.pmv[1].col), a.hp);
+    return r1 < r2 + 1 ? r1 : r2 + 1;
+  };
+  // exact cost key of the candidate at band row y, column x (raster iy, ix)
+  auto exact_key = [&](int y, int x, int iy, int ix) -> uint64_t {
+    uint32_t sad = 0;
+    const int d = x >> 2, sh = x & 3;
+#pragma unroll 4
+    for (int r = 0; r < 16; r++) {
+      const uint32_t *row = band + (y + r) * rw + d;
+      uint32_t w[5];
+#pragma unroll
+      for (int i = 0; i < 5; i++) w[i] = row[i];
+      const uint4 o4 = orgs[r];
+      sad = __builtin_amdgcn_sad_u8(o4.x, __builtin_amdgcn_alignbyte(w[1], w[0], sh), sad);
+      sad = __builtin_amdgcn_sad_u8(o4.y, __builtin_amdgcn_alignbyte(w[2], w[1], sh), sad);
+      sad = __builtin_amdgcn_sad_u8(o4.z, __builtin_amdgcn_alignbyte(w[3], w[2], sh), sad);
+      sad = __builtin_amdgcn_sad_u8(o4.w, __builtin_amdgcn_alignbyte(w[4], w[3], sh), sad);
+    }
+    const uint32_t cost = (sad << 8) + rate_of(iy, ix) * jb.lambda;
+    return ((uint64_t)cost << 32) | (uint32_t)(iy * nx + ix);
+  };
+
+  for (int y0 = 0; y0 < ny; y0 += pb) {
+    const int rows = ny - y0 < pb ? ny - y0 : pb;
+    const int lrows = rows + 15;
+    const int ty_n = (rows + kTileRows - 1) / kTileRows;
+    const int brows = ty_n * kTileRows + 15;
+    const int total = brows * rw;
+    __syncthreads();
+    for (int i0 = tid; i0 < total; i0 += 8 * kFsThreads) {  // band fill
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int i = i0 + u * kFsThreads;
+        const int r = i / rw, c = 4 * (i - r * rw);
+        uint32_t x = 0;
+        if (i < total && r < lrows) {
+          const uint8_t *p = rbase + (int64_t)(y0 + r) * ref.stride + c;
+          if (c + 3 < vis_w) {
+            x = load_u32_unaligned(p);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+              if (c + k < vis_w) x |= (uint32_t)p[k] << (8 * k);
+          }
+        }
+        v[u] = x;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (i0 + u * kFsThreads < total) band[i0 + u * kFsThreads] = v[u];
+    }
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    // (A) S8[y][x] = sum of the 8x8 block at band (y, x), y < ty_n*8 + 8
+    const int s8rows = ty_n * kTileRows + 8;
+    for (int x = tid; x < sw; x += kFsThreads) {
+      uint32_t ring[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) ring[k] = sum8_u8(band + k * rw, x);
+      uint32_t acc = ring[0] + ring[1] + ring[2] + ring[3] + ring[4] + ring[5] + ring[6] + ring[7];
+#pragma unroll 1
+      for (int y = 0; y < s8rows; y += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          s8[(y + u) * sw + x] = (uint16_t)acc;
+          const uint32_t nxt = y + u + 8 < brows ? sum8_u8(band + (y + u + 8) * rw, x) : 0u;
+          acc += nxt - ring[u];
+          ring[u] = nxt;
+        }
+      }
+    }
+    __syncthreads();
+    // (B) tile lower bounds; each lane's minimum-LB candidate
+    const uint32_t so0 = so[0], so1 = so[1], so2 = so[2], so3 = so[3];
+    const int tasks = tx_n * ty_n;
+    uint64_t lbest = ~0ull;  // (LB << 32 | band-local candidate index)
+    auto lb_tile = [&](int t, uint32_t thr, uint32_t *mask) -> uint32_t {
+      const int tcy = t / tx_n, tcx = t - tcy * tx_n;
+      uint32_t tm = 0xffffffffu, m = 0;
+#pragma unroll
+      for (int c = 0; c < kTileRows; c++) {
+        const int y = tcy * kTileRows + c;
+        const uint2 t0 = *reinterpret_cast<const uint2 *>(s8 + y * sw + 4 * tcx);
+        const uint2 t1 = *reinterpret_cast<const uint2 *>(s8 + y * sw + 4 * tcx + 8);
+        const uint2 b0 = *reinterpret_cast<const uint2 *>(s8 + (y + 8) * sw + 4 * tcx);
+        const uint2 b1 = *reinterpret_cast<const uint2 *>(s8 + (y + 8) * sw + 4 * tcx + 8);
+        const uint32_t tl[4] = {t0.x & 0xffff, t0.x >> 16, t0.y & 0xffff, t0.y >> 16};
+        const uint32_t tr[4] = {t1.x & 0xffff, t1.x >> 16, t1.y & 0xffff, t1.y >> 16};
+        const uint32_t bl[4] = {b0.x & 0xffff, b0.x >> 16, b0.y & 0xffff, b0.y >> 16};
+        const uint32_t br[4] = {b1.x & 0xffff, b1.x >> 16, b1.y & 0xffff, b1.y >> 16};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int ix = 4 * tcx + j;
+          if (ix >= nx || y >= rows) continue;
+          uint32_t l = so0 > tl[j] ? so0 - tl[j] : tl[j] - so0;
+          l += so1 > tr[j] ? so1 - tr[j] : tr[j] - so1;
+          l += so2 > bl[j] ? so2 - bl[j] : bl[j] - so2;
+          l += so3 > br[j] ? so3 - br[j] : br[j] - so3;
+          const uint32_t lb = (l << 8) + rate_of(y0 + y, ix) * jb.lambda;
+          tm = lb < tm ? lb : tm;
+          if (mask) {
+            if (lb <= thr) m |= 1u << (c * 4 + j);
+          } else {
+            const uint64_t k = ((uint64_t)lb << 32) | (uint32_t)(y * nx + ix);
+            lbest = k < lbest ? k : lbest;
+          }
+        }
+      }
+      if (mask) *mask = m;
+      return tm;
+    };
+    for (int t = tid; t < tasks; t += kFsThreads) tmin[t] = lb_tile(t, 0, nullptr);
+    if (lbest != ~0ull) {  // evaluate the lane's most promising candidate
+      const uint32_t li = (uint32_t)lbest;
+      const int y = (int)(li / nx), x = (int)(li - (uint32_t)y * nx);
+      const uint64_t k = exact_key(y, x, y0 + y, x);
+      bkey = k < bkey ? k : bkey;
+      atomicMin(&ub_s, (uint32_t)(k >> 32));
+    }
+    __syncthreads();
+    const uint32_t ub = ub_s;
+    // (C) compact the surviving candidates (LB <= UB) and evaluate them
+    for (int t = tid; t < tasks; t += kFsThreads) {
+      if (tmin[t] > ub) continue;
+      uint32_t m;
+      lb_tile(t, ub, &m);
+      if (m) {
+        const uint32_t slot = atomicAdd(&cnt, 1u);
+        ltile[slot] = (uint32_t)t;
+        lmask[slot] = m;
+      }
+    }
+    __syncthreads();
+    const int ns = (int)cnt;
+    if (tid == 0) {  // serial prefix over <= kSeaMaxTiles popcounts
+      uint32_t acc = 0;
+      for (int i = 0; i < ns; i++) {
+        lpre[i] = acc;
+        acc += __builtin_popcount(lmask[i]);
+      }
+      lpre[ns] = acc;
+    }
+    __syncthreads();
+    const int nsurv = (int)lpre[ns];
+    for (int k = tid; k < nsurv; k += kFsThreads) {
+      int lo = 0, hi = ns - 1;  // entry e with lpre[e] <= k < lpre[e + 1]
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (lpre[mid] <= (uint32_t)k) lo = mid;
+        else hi = mid - 1;
+      }
+      uint32_t m = lmask[lo];
+      for (uint32_t r = (uint32_t)k - lpre[lo]; r; r--) m &= m - 1;  // r-th set bit
+      const int bit = __builtin_ctz(m);
+      const int t = (int)ltile[lo], tcy = t / tx_n, tcx = t - tcy * tx_n;
+      const int y = tcy * kTileRows + (bit >> 2), x = 4 * tcx + (bit & 3);
+      const uint64_t key = exact_key(y, x, y0 + y, x);
+      bkey = key < bkey ? key : bkey;
+    }
+    if (tid < 64) atomicMin(&ub_s, (uint32_t)(group_min_u64(bkey) >> 32));
+  }
+  Best b{~0ull, 0xffffffffu};
+  if (bkey != ~0ull) b = Best{bkey >> 32, (uint32_t)bkey};
+  b = block_best(b);
+  if (tid == 0) {
+    const rv_fs_result res = write_result(jb, b, nx > 0 ? nx : 1, 1, a.out + job);
+    chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, res.best_mv);
+  }
+}
+
 }  // namespace rv
 
 using namespace rv;
+
+// RAV1E_HIP_FS_SEA=0 selects the exhaustive u8 path (A/B and tests).
+static bool sea_enabled() {
+  static const int v = [] {
+    const char *e = getenv("RAV1E_HIP_FS_SEA");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return v != 0;
+}
 
 // Multi-reference form used by the replay driver: jobs [n_refs][n_per_ref],
 // job i searches refs[i / n_per_ref], all in one launch; `next` (may be
@@ -386,7 +654,9 @@ int rv_full_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
   a.step = step;
   if (next) a.next = *next;
   const unsigned grid = (unsigned)((n + 7) / 8 * 8);
-  if (blk_w == 16 && blk_h == 16 && step == 1 && org->hbd)
+  if (blk_w == 16 && blk_h == 16 && step == 1 && !org->hbd && sea_enabled())
+    fs16_sea_kernel<<<grid, kFsThreads, kSeaLdsBytes, s>>>(a);
+  else if (blk_w == 16 && blk_h == 16 && step == 1 && org->hbd)
     fs16_kernel<uint16_t><<<grid, kFsThreads, 0, s>>>(a);
   else if (blk_w == 16 && blk_h == 16 && step == 1)
     fs16_kernel<uint8_t><<<grid, kFsThreads, 0, s>>>(a);

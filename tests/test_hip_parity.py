@@ -332,6 +332,39 @@ def test_full_search_vs_oracle(hbd, blk, step):
         assert (got[k]["mv_row"], got[k]["mv_col"], got[k]["cost"]) == (mv[0], mv[1], cost), k
 
 
+@pytest.mark.parametrize("scale", [4, 2, 1])
+def test_full_search_replay_windows_vs_oracle(scale):
+    """The quarter-res coarse search of the replay (estimate_motion_ss4
+    windows at me_range_scale 4/2/1, natural-ish content): the exact
+    successive-elimination path must return the oracle's exhaustive
+    argmin (cost and first raster index)."""
+    from rav1e_amd import replay as RP
+    W, H = 640, 384
+    q = []
+    for t in (0, 1):
+        y = RP.synth_frame(W, H, t)[:W * H].reshape(H, W).astype(np.int32)
+        for _ in range(2):
+            y = (y[0::2, 0::2] + y[1::2, 0::2] + y[0::2, 1::2] + y[1::2, 1::2] + 2) >> 2
+        q.append(y.astype(np.uint8))
+    po_, pr_ = R.DevicePlane.from_array(q[0], xpad=22, ypad=22), R.DevicePlane.from_array(
+        q[1], xpad=22, ypad=22)
+    fo, fr = po_.download_full(), pr_.download_full()
+    xo, yo = po_.desc.xorigin, po_.desc.yorigin
+    qw, qh = W // 4, H // 4
+    jobs = np.zeros(12, dtype=R.FS_JOB)
+    rng = np.random.default_rng(1500 + scale)
+    for k in range(len(jobs)):
+        px, py = 16 * int(rng.integers(0, qw // 16)), 16 * int(rng.integers(0, qh // 16))
+        rx, ry = 48 * scale, 16 * scale
+        jobs[k] = (px, py, max(px - rx, -20), min(px + rx, qw - 16 + 20), max(py - ry, -20),
+                   min(py + ry, qh - 16 + 20), int(rng.integers(-40, 40)),
+                   int(rng.integers(-40, 40)), 0, 0, int(rng.integers(0, 200)), 0)
+    got = R.full_search_batch(po_, pr_, jobs, 16, 16, 1)
+    for k, j in enumerate(jobs):
+        mv, cost = O.full_search(fo, fr, xo, yo, j, 16, 16, 1, 0)
+        assert (got[k]["mv_row"], got[k]["mv_col"], got[k]["cost"]) == (mv[0], mv[1], cost), k
+
+
 def test_full_search_ties_keep_first_raster_candidate():
     rng = np.random.default_rng(900)
     po_, pr_, fo, fr, xo, yo, jobs = _fs_case(rng, False, 16, 6, flat=True)
