@@ -323,7 +323,13 @@ def _fs_case(rng, hbd, blk, nj, flat=False):
 
 @pytest.mark.parametrize("hbd,blk,step", [(False, 16, 1), (False, 32, 1), (True, 16, 1),
                                           (False, 8, 2), (False, 16, 3)])
-def test_full_search_vs_oracle(hbd, blk, step):
+@pytest.mark.parametrize("sea", ["0", "1"])
+def test_full_search_vs_oracle(hbd, blk, step, sea, monkeypatch):
+    monkeypatch.setenv("RAV1E_HIP_FS_SEA", sea)
+    _full_search_vs_oracle(hbd, blk, step)
+
+
+def _full_search_vs_oracle(hbd, blk, step):
     rng = np.random.default_rng(800 + blk + step)
     po_, pr_, fo, fr, xo, yo, jobs = _fs_case(rng, hbd, blk, 12)
     got = R.full_search_batch(po_, pr_, jobs, blk, blk, step, allow_hp=False)
@@ -332,13 +338,15 @@ def test_full_search_vs_oracle(hbd, blk, step):
         assert (got[k]["mv_row"], got[k]["mv_col"], got[k]["cost"]) == (mv[0], mv[1], cost), k
 
 
+@pytest.mark.parametrize("sea", ["0", "1"])
 @pytest.mark.parametrize("scale", [4, 2, 1])
-def test_full_search_replay_windows_vs_oracle(scale):
+def test_full_search_replay_windows_vs_oracle(scale, sea, monkeypatch):
     """The quarter-res coarse search of the replay (estimate_motion_ss4
     windows at me_range_scale 4/2/1, natural-ish content): the exact
     successive-elimination path must return the oracle's exhaustive
     argmin (cost and first raster index)."""
     from rav1e_amd import replay as RP
+    monkeypatch.setenv("RAV1E_HIP_FS_SEA", sea)
     W, H = 640, 384
     q = []
     for t in (0, 1):
