@@ -342,7 +342,12 @@ int rv_replay_frame(rv_replay *r, int me_range_scale);
  * checksums of coefficients / reconstruction / distortion.  Layout in
  * DESIGN.md; returns number of u64 written (<= cap). */
 int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
-/* Kernel-time breakdown of the last frame (HIP events on the replay
+/* Record the timing events on every `stride`-th frame only (1 = every
+ * frame, the default; 0 = never).  Each event record leaves the GPU idle
+ * for a few microseconds between kernels, so timed runs instrument a
+ * sample of frames. */
+int rv_replay_set_timing(rv_replay *r, int stride);
+/* Kernel-time breakdown of the last instrumented frame (HIP events on the replay
  * stream), ms: [0..5] stages F0..F5 (F1 = exactly the full-search
  * launches), then kernel brackets [6] F3 full-pel diamond, [7] F3 sub-pel
  * diamond, [8] F4 fused launch of the sub-pel-MV candidates (luma: MC +
@@ -351,7 +356,8 @@ int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
  * launch of the zero-MV candidates, which runs on a second stream
  * concurrently with F0-F3.  Returns the count written (<= 10). */
 int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
-/* Same breakdown summed over the last `last_frames` frames (<= 64). */
+/* Same breakdown summed over the last `last_frames` instrumented frames
+ * (<= 64). */
 int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,
                               int cap);
 /* Diamond-search candidate evaluations summed over the last min(frames, 64)

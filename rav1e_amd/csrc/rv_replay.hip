@@ -229,6 +229,12 @@ struct rv_replay {
   hipEvent_t fork[kRing], join[kRing], fork2[kRing], join2[kRing];  // cross-stream ordering
   hipEvent_t *ev;
   long frames = 0;
+  // Every `timing_stride`-th frame records the timing events (each record
+  // costs ~4.4 us of idle GPU between kernels on MI355X); `timed` counts
+  // the instrumented frames, which own the event ring slots.
+  int timing_stride = 1;
+  long timed = 0;
+  bool ev_side[kRing];
   // diamond candidate evaluations per job, per ring slot: [kRing][2][nsb*R]
   // (F3 full-pel, F3 sub-pel)
   uint32_t *ds_evals;
@@ -610,10 +616,17 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   to_mc.cw = g.cw;
   to_mc.ch = g.ch;
 
-  hipEvent_t *e = r->evs[slot];
+  const bool tm = r->timing_stride > 0 && r->frames % r->timing_stride == 0;
+  const int tslot = (int)(r->timed % rv_replay::kRing);
+  hipEvent_t *e = r->evs[tslot];
   r->ev = e;
   r->frames++;
-  RV_H(hipEventRecord(e[0], st));
+  if (tm) r->timed++;
+#define RV_EV(i, stream)                                 \
+  do {                                                   \
+    if (tm) RV_H(hipEventRecord(e[i], (stream)));        \
+  } while (0)
+  RV_EV(0, st);
   // F4 zero-MV candidates need no motion search: they run on the side
   // stream concurrently with F0-F3 (rav1e evaluates them in the same RDO
   // loop, src/rdo.rs:949-1006; only the order of independent work changes)
@@ -657,34 +670,34 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
     ca.sub_h = (g.ch < 8 ? g.ch : 8) >> g.ydec;
   }
   const bool serial = (r->cfg.flags & RV_REPLAY_SIDE_RDO) == 0;
-  RV_H(hipEventRecord(r->fork[slot], st));
   if (!serial) {
+    RV_H(hipEventRecord(r->fork[slot], st));
     RV_H(hipStreamWaitEvent(r->side, r->fork[slot], 0));
     la.k_sel = ca.k_sel = 1;
-    RV_H(hipEventRecord(e[9], r->side));
+    RV_EV(9, r->side);
     RV_R(rv_rdo_candidates(la, ca, g.hbd, r->side));
-    RV_H(hipEventRecord(e[10], r->side));
+    RV_EV(10, r->side);
     RV_H(hipEventRecord(r->join[slot], r->side));
   }
   // F0 hres + qres of the input (encode_frame, src/encoder.rs:3382-3385)
   RV_R(rv_plane_pyramid(&cur.y, &cur.hres, &cur.qres, st));
-  RV_H(hipEventRecord(e[1], st));
+  RV_EV(1, st);
   // F1 coarse full search, every reference in one launch -> F2 predictors
   RV_R(rv_full_search_multi(&cur.qres, refs_q, g.R, r->fs_jobs[si], nr, 16, 16, 1, 0, r->coarse,
                             &to_half, st));
-  RV_H(hipEventRecord(e[2], st));
+  RV_EV(2, st);
   // F2 half-res diamond -> F3 full-pel predictors
   RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half, nr, 32, 32, 0, 0, 0, g.bd,
                                r->half, nullptr, &to_full, st));
-  RV_H(hipEventRecord(e[3], st));
+  RV_EV(3, st);
   // F3 full-res full-pel diamond -> sub-pel predictor; sub-pel diamond
   // (speed 10: SAD, no hp) -> the F4 MC jobs of the sub-pel candidates
   RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full, nr, 64, 64, 0, 0, 0, g.bd,
                                r->full, ev_full, &to_sub, st));
-  RV_H(hipEventRecord(e[7], st));
+  RV_EV(7, st);
   RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub, nr, 64, 64, 1, 0, 0, g.bd,
                                r->sub, ev_sub, &to_mc, st));
-  RV_H(hipEventRecord(e[4], st));
+  RV_EV(4, st);
   // F4 sub-pel MV candidates (all candidates when serial): luma + both
   // chroma planes in one fused launch
   if (serial) {
@@ -704,17 +717,16 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   } else {
     RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
   }
-  RV_H(hipEventRecord(e[8], st));
-  if (serial) {  // empty side bracket
-    RV_H(hipEventRecord(e[9], st));
-    RV_H(hipEventRecord(e[10], st));
+  RV_EV(8, st);
+  if (tm) r->ev_side[tslot] = !serial;
+  if (serial) {
   } else {
     RV_H(hipStreamWaitEvent(st, r->join[slot], 0));
   }
   score_candidates<<<g.nsb, 64, 0, st>>>(g, r->l_mom, r->u_sse, r->v_sse, r->lsub, r->csub,
                                          r->coarse, r->half, r->full, r->sub, r->words,
                                          r->tail + 2);
-  RV_H(hipEventRecord(e[5], st));
+  RV_EV(5, st);
   // F5 importance SATD against reference 1
   {
     const unsigned nb = (unsigned)((r->n_imp + 255) / 256);
@@ -725,7 +737,8 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
       importance_kernel<uint8_t><<<nb, 256, 0, st>>>(g, cur.y, r->slots[1].y, r->sub, r->imp_bx,
                                                      r->imp_by, r->tail + 2);
   }
-  RV_H(hipEventRecord(e[6], st));
+  RV_EV(6, st);
+#undef RV_EV
   RV_H(hipGetLastError());
   return RV_OK;
 }
@@ -760,14 +773,15 @@ int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap) {
 
 static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
   if (!r || !ms_out) return rv_set_error(RV_EINVAL, "rv_replay_stage_times: null");
-  if (r->frames == 0) return rv_set_error(RV_EINVAL, "rv_replay_stage_times: no frame");
+  if (r->timed == 0) return rv_set_error(RV_EINVAL, "rv_replay_stage_times: no timed frame");
   if (last < 1) last = 1;
   if (last > rv_replay::kRing) last = rv_replay::kRing;
-  if (last > r->frames) last = (int)r->frames;
+  if (last > r->timed) last = (int)r->timed;
   for (int i = 0; i < cap && i < 10; i++) ms_out[i] = 0.f;
   int n = 0;
   for (int f = 0; f < last; f++) {
-    hipEvent_t *e = r->evs[(r->frames - 1 - f) % rv_replay::kRing];
+    const int ts = (int)((r->timed - 1 - f) % rv_replay::kRing);
+    hipEvent_t *e = r->evs[ts];
     RV_H(hipEventSynchronize(e[6]));
     n = 0;
     for (int i = 0; i < 6 && n < cap; i++) {  // stages F0..F5
@@ -781,11 +795,17 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
     const int br[4][2] = {{3, 7}, {7, 4}, {4, 8}, {9, 10}};
     for (int i = 0; i < 4 && n < cap; i++) {
       float ms = 0.f;
-      RV_H(hipEventElapsedTime(&ms, e[br[i][0]], e[br[i][1]]));
+      if (i < 3 || r->ev_side[ts]) RV_H(hipEventElapsedTime(&ms, e[br[i][0]], e[br[i][1]]));
       ms_out[n++] += ms;
     }
   }
   return n;
+}
+
+int rv_replay_set_timing(rv_replay *r, int stride) {
+  if (!r || stride < 0) return rv_set_error(RV_EINVAL, "rv_replay_set_timing: bad stride");
+  r->timing_stride = stride;
+  return RV_OK;
 }
 
 int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap) {

@@ -103,6 +103,10 @@ class HipReplay:
             _check(n, "rv_replay_results")
         return out[:n]
 
+    def set_timing(self, stride: int):
+        """Record the timing events on every stride-th frame (rv_replay_set_timing)."""
+        _check(lib().rv_replay_set_timing(self.h, stride), "rv_replay_set_timing")
+
     def stage_ms(self) -> np.ndarray:
         out = np.zeros(10, dtype=np.float32)
         n = lib().rv_replay_stage_times(self.h, out.ctypes.data, 10)
