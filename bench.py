@@ -34,7 +34,7 @@ CONFIGS = {  # name: (width, height, xdec, ydec, bit_depth)
     "2160p10": (3840, 2160, 1, 1, 10),
     "2160p444": (3840, 2160, 0, 0, 8),
 }
-TIMING_STRIDE = 5
+TIMING_STRIDE = 4  # in GOPs
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
 # v_sad_u8 issue peak: a wave64 VALU op takes 4 cycles on a SIMD (64 lanes
 # per CU-cycle over 4 SIMDs; tools/ubench/valu_rates.hip measures 0.87 of
@@ -157,14 +157,15 @@ def main():
     for s, f in enumerate(frames):
         hip.set_frame(s, f)
     scales = RP.GOP_SCALES
-    # HIP events on a sample of frames: every TIMING_STRIDE-th frame records
-    # them (coprime with the 4-frame GOP, so every me_range_scale is sampled)
-    hip.set_timing(TIMING_STRIDE)
+    # HIP events on a sample of frames: every TIMING_STRIDE-th GOP records
+    # them (whole GOPs, so every me_range_scale is equally represented)
+    gop = len(scales)
+    hip.set_timing(TIMING_STRIDE, gop)
     dt, words = timed_run(hip, group, args.steps, args.warmup, scales, sync=lambda: R._sync(None))
 
     # per-kernel times over the instrumented frames of the timed region
-    k = min(sum(1 for f in range(args.warmup, args.warmup + args.steps) if f % TIMING_STRIDE == 0),
-            64)
+    k = min(sum(1 for f in range(args.warmup, args.warmup + args.steps)
+                if (f // gop) % TIMING_STRIDE == 0), 64)
     k = max(k, 1)
     ms = hip.stage_ms_sum(k) / k  # per frame
     ev_full, ev_sub, ev_frames = (int(v) for v in hip.counters())

@@ -342,11 +342,12 @@ int rv_replay_frame(rv_replay *r, int me_range_scale);
  * checksums of coefficients / reconstruction / distortion.  Layout in
  * DESIGN.md; returns number of u64 written (<= cap). */
 int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
-/* Record the timing events on every `stride`-th frame only (1 = every
- * frame, the default; 0 = never).  Each event record leaves the GPU idle
- * for a few microseconds between kernels, so timed runs instrument a
- * sample of frames. */
-int rv_replay_set_timing(rv_replay *r, int stride);
+/* Record the timing events only on frames f with (f / block) % stride == 0
+ * (stride 1 = every frame, the default; 0 = never).  Each event record
+ * leaves the GPU idle for a few microseconds between kernels, so timed runs
+ * instrument a sample: block = the GOP length keeps every me_range_scale
+ * equally represented. */
+int rv_replay_set_timing(rv_replay *r, int stride, int block);
 /* Kernel-time breakdown of the last instrumented frame (HIP events on the replay
  * stream), ms: [0..5] stages F0..F5 (F1 = exactly the full-search
  * launches), then kernel brackets [6] F3 full-pel diamond, [7] F3 sub-pel

@@ -232,7 +232,7 @@ struct rv_replay {
   // Every `timing_stride`-th frame records the timing events (each record
   // costs ~4.4 us of idle GPU between kernels on MI355X); `timed` counts
   // the instrumented frames, which own the event ring slots.
-  int timing_stride = 1;
+  int timing_stride = 1, timing_block = 1;
   long timed = 0;
   bool ev_side[kRing];
   // diamond candidate evaluations per job, per ring slot: [kRing][2][nsb*R]
@@ -616,7 +616,7 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   to_mc.cw = g.cw;
   to_mc.ch = g.ch;
 
-  const bool tm = r->timing_stride > 0 && r->frames % r->timing_stride == 0;
+  const bool tm = r->timing_stride > 0 && (r->frames / r->timing_block) % r->timing_stride == 0;
   const int tslot = (int)(r->timed % rv_replay::kRing);
   hipEvent_t *e = r->evs[tslot];
   r->ev = e;
@@ -802,9 +802,11 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
   return n;
 }
 
-int rv_replay_set_timing(rv_replay *r, int stride) {
-  if (!r || stride < 0) return rv_set_error(RV_EINVAL, "rv_replay_set_timing: bad stride");
+int rv_replay_set_timing(rv_replay *r, int stride, int block) {
+  if (!r || stride < 0 || block < 1)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_timing: bad stride / block");
   r->timing_stride = stride;
+  r->timing_block = block;
   return RV_OK;
 }
 

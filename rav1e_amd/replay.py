@@ -103,9 +103,10 @@ class HipReplay:
             _check(n, "rv_replay_results")
         return out[:n]
 
-    def set_timing(self, stride: int):
-        """Record the timing events on every stride-th frame (rv_replay_set_timing)."""
-        _check(lib().rv_replay_set_timing(self.h, stride), "rv_replay_set_timing")
+    def set_timing(self, stride: int, block: int = 1):
+        """Record the timing events on frames f with (f // block) % stride == 0
+        (rv_replay_set_timing)."""
+        _check(lib().rv_replay_set_timing(self.h, stride, block), "rv_replay_set_timing")
 
     def stage_ms(self) -> np.ndarray:
         out = np.zeros(10, dtype=np.float32)
