@@ -73,7 +73,8 @@ def coarse_windows(W, H, R, scale, tile=(0, 0, 0, 0)):
 
 # rocprofv3 kernel names of the bench's kernel classes (u8 / u16 builds)
 ROCPROF_NAMES = {
-    "full_search": "fs16_kernel<{px}>",
+    "full_search": "fs16_sea_kernel_{pxs}",
+    "full_search_exhaustive": "fs16_kernel<{px}>",
     "diamond_fullpel_64": "ds_fast_kernel<{px}, 64, 64, false>",
     "diamond_subpel_64": "ds_fast_kernel<{px}, 64, 64, true>",
     "rdo_candidates": "rdo_frame_kernel<{px}>",
@@ -91,7 +92,10 @@ def measured_traffic(args, kernel, bd):
         return None
     with open(path) as f:
         tj = json.load(f)
-    want = ROCPROF_NAMES.get(kernel, "?").format(px="unsigned short" if bd > 8 else "unsigned char")
+    if kernel == "full_search" and args.exhaustive_fs:
+        kernel = "full_search_exhaustive"
+    want = ROCPROF_NAMES.get(kernel, "?").format(px="unsigned short" if bd > 8 else "unsigned char",
+                                                 pxs="u16" if bd > 8 else "u8")
     for name, v in tj["kernels"].items():
         if want in name:
             return {"bytes_per_launch": round(v["hbm_bytes"]), "source": tj["source"],
@@ -137,6 +141,8 @@ def main():
                     help="F4 luma and chroma candidate kernels on two concurrent streams")
     ap.add_argument("--side-rdo", action="store_true",
                     help="zero-MV RDO candidates on a second stream, concurrent with F0-F3")
+    ap.add_argument("--exhaustive-fs", action="store_true",
+                    help="F1 coarse search without successive elimination (same results)")
     args = ap.parse_args()
 
     import rav1e_amd as R  # load the HIP library before anything else
@@ -153,7 +159,9 @@ def main():
     frames = [RP.synth_frame(W, H, info.frame_offset + t, xdec, ydec, bd) for t in range(nref + 1)]
     hip = RP.HipReplay(W, H, xdec, ydec, bd, nref,
                        flags=(RP.RV_REPLAY_SIDE_RDO if args.side_rdo else 0) |
-                       (RP.RV_REPLAY_SPLIT_RDO if args.split_rdo else 0))
+                       (RP.RV_REPLAY_SPLIT_RDO if args.split_rdo else 0) |
+                       (RP.RV_REPLAY_EXHAUSTIVE_FS if args.exhaustive_fs else 0))
+    sea = bd <= 10 and not args.exhaustive_fs  # the replay's F1 path
     for s, f in enumerate(frames):
         hip.set_frame(s, f)
     scales = RP.GOP_SCALES
@@ -172,8 +180,10 @@ def main():
     ev_frames = max(1, ev_frames)
     nsb = ((W + 63) // 64) * ((H + 63) // 64)
     px = 2 if bd > 8 else 1
-    # algorithmic bytes per frame of each kernel class
-    fs_bytes = sum(sum((nx + 15) * (ny + 15) * px + 256 * px + 56
+    # algorithmic bytes per frame of each kernel class; the
+    # SEA search also reads the window's 8x8 box-sum table (u16)
+    fs_bytes = sum(sum((nx + 15) * (ny + 15) * px + 256 * px + 56 +
+                       ((nx + 11) * (ny + 15) * 2 if sea else 0)
                        for nx, ny in coarse_windows(W, H, nref, s)) for s in scales) / 4.0
     fs_ops = sum(sum(nx * ny * 256 for nx, ny in coarse_windows(W, H, nref, s))
                  for s in scales) / 4.0
@@ -211,7 +221,7 @@ def main():
             "traffic": measured_traffic(args, dom, bd),
             "avg_launch_ms": round(kd["ms"] / kd["launches"], 5),
             "algorithmic_bytes_per_launch": round(kd["bytes"] / kd["launches"])}
-    if dom == "full_search":
+    if dom == "full_search" and not sea:
         achv = kd["sad_px"] / (kd["ms"] / 1e3) / 1e12
         peak = SAD_PEAK_PX / (2 if bd > 8 else 1)
         roof["valu"] = {"achieved": round(achv, 3), "peak": round(peak / 1e12, 1),
@@ -256,6 +266,7 @@ def main():
                          zip(["F0_downsample", "F1_full_search", "F2_diamond_half",
                               "F3_diamond_full_subpel", "F4_rdo", "F5_importance_satd"], ms[:6])},
             "kernels_ms": {n: round(v["ms"], 4) for n, v in kernels.items()},
+            "full_search_path": "successive elimination" if sea else "exhaustive",
             "diamond_evals_per_frame": [round(ev_full / ev_frames, 1),
                                         round(ev_sub / ev_frames, 1)],
             "checksum": int(words[-3]) & 0xFFFFFFFF,

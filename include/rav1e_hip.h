@@ -267,6 +267,29 @@ int rv_full_search_batch(const rv_plane *org, const rv_plane *ref,
                          int blk_h, int step, int allow_hp,
                          rv_fs_result *d_out, void *stream);
 
+/* Paired box sums of a plane (bit depth <= 10, so every sum fits 16
+ * bits), for the successive-elimination search below.  d_box (16-byte
+ * aligned) holds two tables with the plane's geometry, n = stride *
+ * alloc_height u32 each: entry (ax, ay) of the allocation in [0, n) is
+ * S8(ax, ay) | S8(ax + 8, ay) << 16, in [n, 2n) S4(ax, ay) | S4(ax + 4, ay)
+ * << 16, SK = the sum of the K x K pixels whose top-left corner is there (0
+ * where that block would leave the allocation).  A reference frame needs
+ * them once (rav1e searches each input_qres as a reference for several
+ * frames). */
+int rv_plane_box_sums(const rv_plane *p, uint32_t *d_box, void *stream);
+
+/* rv_full_search_batch for 16x16 blocks, step 1 (estimate_motion_ss4's
+ * quarter-resolution search, src/me.rs:1023-1075) with exact successive
+ * elimination: SAD >= sum over the four 8x8 quadrants (and over the
+ * sixteen 4x4 blocks) of |S_org - S_ref|, so every candidate whose lower
+ * bound exceeds an achieved cost is skipped.  Results are identical to
+ * rv_full_search_batch (same cost, same first raster minimum).
+ * d_ref_box = rv_plane_box_sums of ref. */
+int rv_full_search_sea_batch(const rv_plane *org, const rv_plane *ref,
+                             const uint32_t *d_ref_box, const rv_fs_job *d_jobs,
+                             int n, int allow_hp, rv_fs_result *d_out,
+                             void *stream);
+
 /* diamond_me_search (src/me.rs:693-785) with get_best_predictor
  * (:655-691), get_mv_rd_cost (:787-838), compute_mv_rd_cost (:840-856):
  * one persistent workgroup per job runs the whole data-dependent search.
@@ -327,6 +350,10 @@ typedef struct rv_replay_cfg {
 /* flags: F4 luma candidates on the replay stream and the chroma transform
  * blocks concurrently on a second stream (separate, smaller-LDS kernel). */
 #define RV_REPLAY_SPLIT_RDO 2
+/* flags: F1 coarse search exhaustively (rv_full_search_batch) instead of
+ * by successive elimination over box-sum tables (rv_full_search_sea_batch;
+ * same results, the default for bit depth <= 10). */
+#define RV_REPLAY_EXHAUSTIVE_FS 4
 typedef struct rv_replay rv_replay;
 /* Allocate device state for one tile; frames are uploaded with
  * rv_replay_set_frame.  NULL on failure. */

@@ -227,6 +227,8 @@ def _declare(L):
         "rv_diff_fwd_txfm_batch": (i32, [P, P, vp, i32, i32, i32, i32, vp, vp]),
         "rv_inv_txfm_add_batch": (i32, [vp, P, vp, i32, i32, i32, i32, vp]),
         "rv_full_search_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, vp, vp]),
+        "rv_full_search_sea_batch": (i32, [P, P, vp, vp, i32, i32, vp, vp]),
+        "rv_plane_box_sums": (i32, [P, vp, vp]),
         "rv_replay_create": (vp, [C.POINTER(RvReplayCfg), vp]),
         "rv_replay_destroy": (None, [vp]),
         "rv_replay_set_frame": (i32, [vp, i32, vp]),
@@ -512,6 +514,33 @@ def full_search_batch(org: DevicePlane, ref: DevicePlane, jobs, blk_w, blk_h, st
     _check(lib().rv_full_search_batch(C.byref(org.desc), C.byref(ref.desc), dj.ptr, len(jobs),
                                       blk_w, blk_h, step, 1 if allow_hp else 0, out.ptr, None),
            "rv_full_search_batch")
+    _sync()
+    return out.download(FS_RESULT, len(jobs))
+
+
+def plane_box_sums(plane: DevicePlane) -> DeviceBuffer:
+    """rv_plane_box_sums: paired 8x8 then paired 4x4 box sums over the whole
+    allocation (u32 S8(x, y) | S8(x + 8, y) << 16, then S4(x, y) |
+    S4(x + 4, y) << 16, each in the plane's stride x alloc_height layout)."""
+    d = plane.desc
+    out = DeviceBuffer(8 * d.stride * d.alloc_height)
+    _check(lib().rv_plane_box_sums(C.byref(d), out.ptr, None), "rv_plane_box_sums")
+    _sync()
+    return out
+
+
+def full_search_sea_batch(org: DevicePlane, ref: DevicePlane, jobs, allow_hp=False,
+                          s8: "DeviceBuffer | None" = None) -> np.ndarray:
+    """rv_full_search_sea_batch (16x16, step 1): same results as
+    full_search_batch by successive elimination over ref's box sums."""
+    jobs = np.ascontiguousarray(jobs, dtype=FS_JOB)
+    if s8 is None:
+        s8 = plane_box_sums(ref)
+    dj = DeviceBuffer.from_array(jobs)
+    out = DeviceBuffer(16 * max(1, len(jobs)))
+    _check(lib().rv_full_search_sea_batch(C.byref(org.desc), C.byref(ref.desc), s8.ptr, dj.ptr,
+                                          len(jobs), 1 if allow_hp else 0, out.ptr, None),
+           "rv_full_search_sea_batch")
     _sync()
     return out.download(FS_RESULT, len(jobs))
 

@@ -111,6 +111,7 @@ struct FsArgs {
   rv_fs_result *out;
   int n, n_per_ref, hp, bw, bh, step;
   ChainNext next;  // replay: feed the winner into the next stage's jobs
+  const uint32_t *box[RV_DS_MAX_PRED];  // rv_plane_box_sums of each ref (SEA path)
 };
 
 // blockIdx -> job with consecutive jobs on one XCD (blocks are dealt
@@ -362,275 +363,298 @@ __global__ __launch_bounds__(kFsThreads) void fs16_kernel(FsArgs a) {
   }
 }
 
-// ---- exact successive-elimination path: u8, 16x16, step 1 ----------------
+// ---- exact successive-elimination path: 16x16, step 1 ---------------------
 // The triangle inequality bounds every candidate from below:
 //   SAD(org, cand) >= sum over the four 8x8 quadrants q of |S_org,q - S_cand,q|
 // (S = pixel sum), so cost >= LB = 256 * that + rate * lambda.  A candidate
 // whose LB exceeds an achieved cost UB cannot be the strict first minimum,
 // so skipping it leaves the result of full_search (src/me.rs:943-990)
-// unchanged bit for bit.  Per band: (A) the 8x8 box sums S8 of every
-// candidate position go to LDS (horizontal 8-sums by v_sad_u8 against zero,
-// vertical by a sliding register ring); (B) every lane takes the
-// minimum-LB candidate of its tiles and evaluates it exactly -> UB (carried
-// across bands); (C) the candidates with LB <= UB are compacted and
-// evaluated exactly, spread over all lanes.
-constexpr int kSeaLdsBytes = 48 * 1024;
-constexpr int kSeaMaxTiles = 512;
+// unchanged bit for bit.  The reference's box sums come from tables built
+// once per reference frame (rv_plane_box_sums; every superblock of several
+// frames searches the same reference), stored as horizontal pairs
+// (S8(x, y) | S8(x + 8, y) << 16 and S4(x, y) | S4(x + 4, y) << 16), so one
+// v_sad_u16 against the packed source sums gives two block terms: the 8x8
+// bound of a candidate is 2 v_sad_u16 + 1 add from two aligned dwords, the
+// sharper 4x4 bound (16 blocks) 8 v_sad_u16.  Per job:
+//   (1) the 16x16 neighbourhood of mv 0 (where natural motion puts the
+//       minimum) is evaluated exactly -> UB;
+//   (2) one pass over 4-wide x 8-tall candidate tiles computes every LB
+//       (16 dwordx4 table rows per tile, L2-resident), keeps each tile's
+//       minimum in LDS, and every lane evaluates the minimum-LB candidate of
+//       its best tile exactly -> UB (now the cost of some valid candidate);
+//   (3) tiles whose minimum is <= UB are revisited with the sharper 4x4
+//       bound (on the replay's content it keeps ~1 in 40 of the 8x8
+//       survivors); its survivors are compacted and evaluated exactly,
+//       spread over all lanes.
+// Out-of-window candidates of edge tiles get a bound >= 2^30, above every
+// real cost (lambda < 2^23 here; larger lambdas take the exhaustive path).
+constexpr int kSeaMaxTiles = 1664;  // 97 x 17: the me_range_scale 4 window
+constexpr uint32_t kSeaOut = 1u << 30;
 
-__device__ __forceinline__ uint32_t sum8_u8(const uint32_t *row, int x) {
-  const int d = x >> 2, sh = x & 3;
-  const uint32_t w0 = row[d], w1 = row[d + 1], w2 = row[d + 2];
-  return __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, sh), 0u,
-                                 __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w2, w1, sh), 0u, 0u));
+// Reference rows are read with dword-aligned loads and realigned in
+// registers (v_alignbyte): lane addresses that are not 4-byte aligned make a
+// multi-dword global load ~3x slower (tools/ubench/load_align.hip).  The
+// extra trailing dword is only read when the row is misaligned; it then
+// holds needed bytes, so no read leaves a dword-aligned allocation.
+
+// Exact SAD of the 16x16 source block (LDS, 4 * B dwords per row) against
+// the reference block at p (global memory, rs bytes per row, rs % 4 == 0).
+template <typename Px>
+__device__ __forceinline__ uint32_t sad16_global(const uint32_t *orgs, const uint8_t *p,
+                                                 int64_t rs) {
+  constexpr int B = (int)sizeof(Px);
+  const int sh = (int)((uintptr_t)p & 3);
+  const uint8_t *pa = p - sh;
+  uint32_t sad = 0;
+#pragma unroll 8
+  for (int r = 0; r < 16; r++) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(pa + r * rs);
+    uint32_t v[4 * B + 1];
+#pragma unroll
+    for (int h = 0; h < B; h++) {
+      const uint4 x = *reinterpret_cast<const uint4 *>(w + 4 * h);
+      v[4 * h] = x.x;
+      v[4 * h + 1] = x.y;
+      v[4 * h + 2] = x.z;
+      v[4 * h + 3] = x.w;
+    }
+    v[4 * B] = sh ? w[4 * B] : 0u;
+#pragma unroll
+    for (int h = 0; h < B; h++) {
+      const uint4 o = *reinterpret_cast<const uint4 *>(orgs + r * 4 * B + 4 * h);
+      sad = sad_px<Px>(o.x, __builtin_amdgcn_alignbyte(v[4 * h + 1], v[4 * h], sh), sad);
+      sad = sad_px<Px>(o.y, __builtin_amdgcn_alignbyte(v[4 * h + 2], v[4 * h + 1], sh), sad);
+      sad = sad_px<Px>(o.z, __builtin_amdgcn_alignbyte(v[4 * h + 3], v[4 * h + 2], sh), sad);
+      sad = sad_px<Px>(o.w, __builtin_amdgcn_alignbyte(v[4 * h + 4], v[4 * h + 3], sh), sad);
+    }
+  }
+  return sad;
 }
 
-__global__ __launch_bounds__(kFsThreads) void fs16_sea_kernel(FsArgs a) {
-  extern __shared__ __align__(16) uint32_t sea_lds[];
-  __shared__ uint4 orgs[16];
-  __shared__ uint32_t so[4];
-  __shared__ uint32_t tmin[kSeaMaxTiles];
-  __shared__ uint32_t lmask[kSeaMaxTiles], ltile[kSeaMaxTiles], lpre[kSeaMaxTiles + 1];
-  __shared__ uint32_t cnt, ub_s;
-  const int job = fs_job_index();
-  if (job >= a.n) return;
-  const rv_fs_job jb = a.jobs[job];
-  const rv_plane &ref = a.ref[job / a.n_per_ref];
-  const int nx = jb.x_hi >= jb.x_lo ? jb.x_hi - jb.x_lo + 1 : 0;
-  const int ny = jb.y_hi >= jb.y_lo ? jb.y_hi - jb.y_lo + 1 : 0;
+struct SeaCtx {
+  const uint32_t *box;   // paired 8x8 table at window position (0, 0)
+  const uint32_t *box4;  // paired 4x4 table at window position (0, 0)
+  int stride;            // table row pitch (elements)
+  int nx, ny, tx_n;
+  uint32_t so01, so23;   // packed source 8x8 quadrant sums
+  const uint32_t *s4;    // LDS: packed source 4x4 sums, row i: [2i] = cols 0|1, [2i+1] = cols 2|3
+};
+
+// rate * lambda of the tile's candidates (get_mv_rate, src/me.rs:1006-1021)
+// as row terms rr and column terms rc; candidates outside the window get
+// kSeaOut from both.  SAME: pmv[0] == pmv[1], so min(r0, r1 + 1) is r0 and
+// the product splits: rr0 / rc0 already hold rate * lambda.
+template <bool SAME>
+struct SeaRates {
+  uint32_t rr0[kTileRows], rr1[kTileRows], rc0[4], rc1[4];
+  __device__ __forceinline__ SeaRates(const SeaCtx &c, const rv_fs_job &jb, int hp, int cy0,
+                                      int tcx) {
+#pragma unroll
+    for (int k = 0; k < kTileRows; k++) {
+      const int16_t rw = (int16_t)(8 * (jb.y_lo + cy0 + k - jb.po_y));
+      const bool in = cy0 + k < c.ny;
+      rr0[k] = in ? diff_to_rate((int16_t)(rw - jb.pmv[0].row), hp) : kSeaOut;
+      rr1[k] = SAME ? 0u : (in ? diff_to_rate((int16_t)(rw - jb.pmv[1].row), hp) : kSeaOut);
+      if (SAME && in) rr0[k] *= jb.lambda;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int16_t cl = (int16_t)(8 * (jb.x_lo + 4 * tcx + j - jb.po_x));
+      const bool in = 4 * tcx + j < c.nx;
+      rc0[j] = in ? diff_to_rate((int16_t)(cl - jb.pmv[0].col), hp) : kSeaOut;
+      rc1[j] = SAME ? 0u : (in ? diff_to_rate((int16_t)(cl - jb.pmv[1].col), hp) : kSeaOut);
+      if (SAME && in) rc0[j] *= jb.lambda;
+    }
+  }
+  __device__ __forceinline__ uint32_t rl(int k, int j, uint32_t lambda) const {
+    if (SAME) return rr0[k] + rc0[j];
+    const uint32_t r1 = rr0[k] + rc0[j], r2 = rr1[k] + rc1[j] + 1;
+    const uint32_t r = r1 < r2 ? r1 : r2;
+    return r >= kSeaOut ? kSeaOut : r * lambda;
+  }
+};
+
+// 8x8 lower bounds of the 32 candidates of tile t: returns the tile
+// minimum; ARG: also the raster index of its first minimum (*arg).
+template <bool ARG, bool SAME>
+__device__ __forceinline__ uint32_t sea_tile(const SeaCtx &c, const rv_fs_job &jb, int hp,
+                                             int t, uint32_t *arg) {
+  const int tcy = t / c.tx_n, tcx = t - tcy * c.tx_n;
+  const int cy0 = tcy * kTileRows;
+  uint4 row[kTileRows + 8];
+  const uint32_t *bp = c.box + (int64_t)cy0 * c.stride + 4 * tcx;
+#pragma unroll
+  for (int r = 0; r < kTileRows + 8; r++)
+    row[r] = *reinterpret_cast<const uint4 *>(bp + (int64_t)r * c.stride);
+  const SeaRates<SAME> rt(c, jb, hp, cy0, tcx);
+  uint32_t tm = 0xffffffffu, am = 0;
+#pragma unroll
+  for (int k = 0; k < kTileRows; k++) {
+    const uint32_t top[4] = {row[k].x, row[k].y, row[k].z, row[k].w};
+    const uint32_t bot[4] = {row[k + 8].x, row[k + 8].y, row[k + 8].z, row[k + 8].w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t l = __builtin_amdgcn_sad_u16(bot[j], c.so23, __builtin_amdgcn_sad_u16(top[j], c.so01, 0u));
+      const uint32_t lb = (l << 8) + rt.rl(k, j, jb.lambda);
+      if (ARG && lb < tm) am = (uint32_t)(k * 4 + j);
+      tm = lb < tm ? lb : tm;
+    }
+  }
+  if (ARG) *arg = (uint32_t)((cy0 + (int)(am >> 2)) * c.nx + 4 * tcx + (int)(am & 3));
+  return tm;
+}
+
+// 4x4 lower bounds (sixteen block terms, >= the 8x8 bound) of the 32
+// candidates of tile t: the mask of those <= thr.  Four passes over the
+// block rows i, each loading 8 table rows x 2 dwordx4.
+template <bool SAME>
+__device__ __forceinline__ uint32_t sea_tile4(const SeaCtx &c, const rv_fs_job &jb, int hp,
+                                              int t, uint32_t thr) {
+  const int tcy = t / c.tx_n, tcx = t - tcy * c.tx_n;
+  const int cy0 = tcy * kTileRows;
+  uint32_t acc[kTileRows][4];
+#pragma unroll
+  for (int k = 0; k < kTileRows; k++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc[k][j] = 0;
+#pragma unroll 1
+  for (int i = 0; i < 4; i++) {  // rolled: 16 loads in flight, not 64
+    const uint32_t s4a = c.s4[2 * i], s4b = c.s4[2 * i + 1];
+    const uint32_t *bp = c.box4 + (int64_t)(cy0 + 4 * i) * c.stride + 4 * tcx;
+    uint4 lo[kTileRows], hi[kTileRows];
+#pragma unroll
+    for (int r = 0; r < kTileRows; r++) {
+      lo[r] = *reinterpret_cast<const uint4 *>(bp + (int64_t)r * c.stride);
+      hi[r] = *reinterpret_cast<const uint4 *>(bp + (int64_t)r * c.stride + 8);
+    }
+#pragma unroll
+    for (int k = 0; k < kTileRows; k++) {
+      const uint32_t l4[4] = {lo[k].x, lo[k].y, lo[k].z, lo[k].w};
+      const uint32_t h4[4] = {hi[k].x, hi[k].y, hi[k].z, hi[k].w};
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        acc[k][j] = __builtin_amdgcn_sad_u16(h4[j], s4b, __builtin_amdgcn_sad_u16(l4[j], s4a, acc[k][j]));
+    }
+  }
+  const SeaRates<SAME> rt(c, jb, hp, cy0, tcx);
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < kTileRows; k++)
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if ((acc[k][j] << 8) + rt.rl(k, j, jb.lambda) <= thr) m |= 1u << (k * 4 + j);
+  return m;
+}
+
+template <typename Px, bool SAME>
+__device__ __forceinline__ void sea_search(const FsArgs &a, const rv_fs_job &jb, int job,
+                                           const rv_plane &ref, const SeaCtx &c,
+                                           const uint32_t *orgs, uint32_t *tmin, uint32_t *lmask,
+                                           uint32_t *ltile, uint32_t *lpre, uint32_t &cnt,
+                                           uint32_t &ub_s) {
+  constexpr int B = (int)sizeof(Px);
   const int tid = threadIdx.x;
-  if (tid < 64) {
-    const uint8_t *o = plane_ptr<uint8_t>(a.org, jb.po_x, jb.po_y);
-    reinterpret_cast<uint32_t *>(orgs)[tid] =
-        load_u32_unaligned(o + (int64_t)(tid >> 2) * a.org.stride + 4 * (tid & 3));
-  }
-  if (tid == 0) ub_s = 0xffffffffu;
-  __syncthreads();
-  if (tid < 4) {  // quadrant sums of the source block
-    const uint32_t *ow = reinterpret_cast<const uint32_t *>(orgs);
-    uint32_t t = 0;
-    for (int r = 0; r < 8; r++)
-      for (int i = 0; i < 2; i++)
-        t = __builtin_amdgcn_sad_u8(ow[(8 * (tid >> 1) + r) * 4 + 2 * (tid & 1) + i], 0u, t);
-    so[tid] = t;
-  }
-  const int tx_n = (nx + 3) >> 2;
-  const int rw = tx_n + 4;             // band row length in dwords (pixels)
-  const int sw = 4 * tx_n + 8;         // S8 row length in u16 (candidate cols + 8)
-  const int vis_w = nx + 15;
-  // band rows: pixels (pb + 15) * rw * 4 + S8 (pb + 8) * sw * 2 <= budget
-  int pb = (kSeaLdsBytes - 4 - 15 * rw * 4 - 8 * sw * 2) / (rw * 4 + sw * 2);
-  pb = (pb / kTileRows) * kTileRows;
-  pb = pb > kSeaMaxTiles / tx_n * kTileRows ? kSeaMaxTiles / tx_n * kTileRows : pb;
-  // window too wide for the SEA band, or costs that may not fit u32
-  // (256 * sad < 2^24 needs lambda < 2^25): exhaustive path
-  if (pb < kTileRows || jb.lambda >= (1u << 25)) {
-    const rv_fs_result res = fs_generic_body<uint8_t>(a.org, ref, jb, 16, 16, 1, a.hp, a.out + job);
-    if (tid == 0) chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, res.best_mv);
-    return;
-  }
-  uint32_t *band = sea_lds;
-  // S8 rows are read as 8-byte uint2: start the table on an 8-byte boundary
-  uint16_t *s8 = reinterpret_cast<uint16_t *>(sea_lds + (((pb + 15) * rw + 1) & ~1));
-  uint64_t bkey = ~0ull;  // (u32 cost << 32 | raster index)
-  const uint8_t *rbase = plane_ptr<uint8_t>(ref, jb.x_lo, jb.y_lo);
-  auto rate_of = [&](int iy, int ix) -> uint32_t {
+  const int nx = c.nx, ny = c.ny, tasks = c.tx_n * ((ny + kTileRows - 1) / kTileRows);
+  const uint8_t *rbase = (const uint8_t *)plane_ptr<Px>(ref, jb.x_lo, jb.y_lo);
+  const int64_t rs = (int64_t)ref.stride * B;
+  // exact (u32 cost << 32 | raster index) of candidate (iy, ix)
+  auto exact_key = [&](int iy, int ix) __attribute__((always_inline)) -> uint64_t {
+    const uint32_t sad = sad16_global<Px>(orgs, rbase + iy * rs + ix * B, rs);
     const int16_t row = (int16_t)(8 * (jb.y_lo + iy - jb.po_y));
     const int16_t col = (int16_t)(8 * (jb.x_lo + ix - jb.po_x));
     const uint32_t r1 = diff_to_rate((int16_t)(row - jb.pmv[0].row), a.hp) +
                         diff_to_rate((int16_t)(col - jb.pmv[0].col), a.hp);
     const uint32_t r2 = diff_to_rate((int16_t)(row - jb.pmv[1].row), a.hp) +
                         diff_to_rate((int16_t)(col - jb.pmv[1].col), a.hp);
-    return r1 < r2 + 1 ? r1 : r2 + 1;
-  };
-  // exact cost key of the candidate at band row y, column x (raster iy, ix)
-  auto exact_key = [&](int y, int x, int iy, int ix) -> uint64_t {
-    uint32_t sad = 0;
-    const int d = x >> 2, sh = x & 3;
-#pragma unroll 4
-    for (int r = 0; r < 16; r++) {
-      const uint32_t *row = band + (y + r) * rw + d;
-      uint32_t w[5];
-#pragma unroll
-      for (int i = 0; i < 5; i++) w[i] = row[i];
-      const uint4 o4 = orgs[r];
-      sad = __builtin_amdgcn_sad_u8(o4.x, __builtin_amdgcn_alignbyte(w[1], w[0], sh), sad);
-      sad = __builtin_amdgcn_sad_u8(o4.y, __builtin_amdgcn_alignbyte(w[2], w[1], sh), sad);
-      sad = __builtin_amdgcn_sad_u8(o4.z, __builtin_amdgcn_alignbyte(w[3], w[2], sh), sad);
-      sad = __builtin_amdgcn_sad_u8(o4.w, __builtin_amdgcn_alignbyte(w[4], w[3], sh), sad);
-    }
-    const uint32_t cost = (sad << 8) + rate_of(iy, ix) * jb.lambda;
+    const uint32_t cost = (sad << 8) + (r1 < r2 + 1 ? r1 : r2 + 1) * jb.lambda;
     return ((uint64_t)cost << 32) | (uint32_t)(iy * nx + ix);
   };
 
-  for (int y0 = 0; y0 < ny; y0 += pb) {
-    const int rows = ny - y0 < pb ? ny - y0 : pb;
-    const int lrows = rows + 15;
-    const int ty_n = (rows + kTileRows - 1) / kTileRows;
-    const int brows = ty_n * kTileRows + 15;
-    const int total = brows * rw;
-    __syncthreads();
-    for (int i0 = tid; i0 < total; i0 += 8 * kFsThreads) {  // band fill
-      uint32_t v[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const int i = i0 + u * kFsThreads;
-        const int r = i / rw, c = 4 * (i - r * rw);
-        uint32_t x = 0;
-        if (i < total && r < lrows) {
-          const uint8_t *p = rbase + (int64_t)(y0 + r) * ref.stride + c;
-          if (c + 3 < vis_w) {
-            x = load_u32_unaligned(p);
-          } else {
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-              if (c + k < vis_w) x |= (uint32_t)p[k] << (8 * k);
-          }
-        }
-        v[u] = x;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; u++)
-        if (i0 + u * kFsThreads < total) band[i0 + u * kFsThreads] = v[u];
+  // (1) the 16x16 candidates around mv 0
+  uint64_t bkey = ~0ull;
+  {
+    const int ix = jb.po_x - jb.x_lo - 8 + (tid & 15), iy = jb.po_y - jb.y_lo - 8 + (tid >> 4);
+    if (ix >= 0 && ix < nx && iy >= 0 && iy < ny) {
+      bkey = exact_key(iy, ix);
+      atomicMin(&ub_s, (uint32_t)(bkey >> 32));
     }
-    if (tid == 0) cnt = 0;
-    __syncthreads();
-    // (A) S8[y][x] = sum of the 8x8 block at band (y, x), y < ty_n*8 + 8
-    const int s8rows = ty_n * kTileRows + 8;
-    for (int x = tid; x < sw; x += kFsThreads) {
-      uint32_t ring[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) ring[k] = sum8_u8(band + k * rw, x);
-      uint32_t acc = ring[0] + ring[1] + ring[2] + ring[3] + ring[4] + ring[5] + ring[6] + ring[7];
-#pragma unroll 1
-      for (int y = 0; y < s8rows; y += 8) {
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          s8[(y + u) * sw + x] = (uint16_t)acc;
-          const uint32_t nxt = y + u + 8 < brows ? sum8_u8(band + (y + u + 8) * rw, x) : 0u;
-          acc += nxt - ring[u];
-          ring[u] = nxt;
-        }
-      }
+  }
+  // (2) tile minima; each lane's best tile
+  uint32_t lt_min = 0xffffffffu;
+  int lt = -1;
+  for (int t = tid; t < tasks; t += kFsThreads) {
+    const uint32_t tm = sea_tile<false, SAME>(c, jb, a.hp, t, nullptr);
+    tmin[t] = tm;
+    if (tm < lt_min) {
+      lt_min = tm;
+      lt = t;
     }
-    __syncthreads();
-    // (B) tile lower bounds; each lane's minimum-LB candidate
-    const uint32_t so0 = so[0], so1 = so[1], so2 = so[2], so3 = so[3];
-    const int tasks = tx_n * ty_n;
-    uint64_t lbest = ~0ull;  // (LB << 32 | band-local candidate index)
-    auto lb_tile = [&](int t, uint32_t thr, uint32_t *mask) -> uint32_t {
-      const int tcy = t / tx_n, tcx = t - tcy * tx_n;
-      // separable rate terms (get_mv_rate): 24 diff_to_rate per 32 candidates
-      uint32_t rr0[kTileRows], rr1[kTileRows], rc0[4], rc1[4];
-#pragma unroll
-      for (int c = 0; c < kTileRows; c++) {
-        const int16_t row = (int16_t)(8 * (jb.y_lo + y0 + tcy * kTileRows + c - jb.po_y));
-        rr0[c] = diff_to_rate((int16_t)(row - jb.pmv[0].row), a.hp);
-        rr1[c] = diff_to_rate((int16_t)(row - jb.pmv[1].row), a.hp);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int16_t col = (int16_t)(8 * (jb.x_lo + 4 * tcx + j - jb.po_x));
-        rc0[j] = diff_to_rate((int16_t)(col - jb.pmv[0].col), a.hp);
-        rc1[j] = diff_to_rate((int16_t)(col - jb.pmv[1].col), a.hp);
-      }
-      uint32_t tm = 0xffffffffu, m = 0;
-#pragma unroll
-      for (int c = 0; c < kTileRows; c++) {
-        const int y = tcy * kTileRows + c;
-        const uint2 t0 = *reinterpret_cast<const uint2 *>(s8 + y * sw + 4 * tcx);
-        const uint2 t1 = *reinterpret_cast<const uint2 *>(s8 + y * sw + 4 * tcx + 8);
-        const uint2 b0 = *reinterpret_cast<const uint2 *>(s8 + (y + 8) * sw + 4 * tcx);
-        const uint2 b1 = *reinterpret_cast<const uint2 *>(s8 + (y + 8) * sw + 4 * tcx + 8);
-        const uint32_t tl[4] = {t0.x & 0xffff, t0.x >> 16, t0.y & 0xffff, t0.y >> 16};
-        const uint32_t tr[4] = {t1.x & 0xffff, t1.x >> 16, t1.y & 0xffff, t1.y >> 16};
-        const uint32_t bl[4] = {b0.x & 0xffff, b0.x >> 16, b0.y & 0xffff, b0.y >> 16};
-        const uint32_t br[4] = {b1.x & 0xffff, b1.x >> 16, b1.y & 0xffff, b1.y >> 16};
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int ix = 4 * tcx + j;
-          if (ix >= nx || y >= rows) continue;
-          uint32_t l = so0 > tl[j] ? so0 - tl[j] : tl[j] - so0;
-          l += so1 > tr[j] ? so1 - tr[j] : tr[j] - so1;
-          l += so2 > bl[j] ? so2 - bl[j] : bl[j] - so2;
-          l += so3 > br[j] ? so3 - br[j] : br[j] - so3;
-          const uint32_t r1 = rr0[c] + rc0[j], r2 = rr1[c] + rc1[j];
-          const uint32_t lb = (l << 8) + (r1 < r2 + 1 ? r1 : r2 + 1) * jb.lambda;
-          tm = lb < tm ? lb : tm;
-          if (mask) {
-            if (lb <= thr) m |= 1u << (c * 4 + j);
-          } else {
-            const uint64_t k = ((uint64_t)lb << 32) | (uint32_t)(y * nx + ix);
-            lbest = k < lbest ? k : lbest;
-          }
-        }
-      }
-      if (mask) *mask = m;
-      return tm;
-    };
-    for (int t = tid; t < tasks; t += kFsThreads) tmin[t] = lb_tile(t, 0, nullptr);
-    if (lbest != ~0ull) {  // evaluate the lane's most promising candidate
-      const uint32_t li = (uint32_t)lbest;
-      const int y = (int)(li / nx), x = (int)(li - (uint32_t)y * nx);
-      const uint64_t k = exact_key(y, x, y0 + y, x);
-      bkey = k < bkey ? k : bkey;
-      atomicMin(&ub_s, (uint32_t)(k >> 32));
+  }
+  if (lt >= 0 && lt_min < *(volatile uint32_t *)&ub_s) {
+    // the plain read of ub_s only filters: any achieved cost is a bound
+    uint32_t li;
+    sea_tile<true, SAME>(c, jb, a.hp, lt, &li);
+    const int iy = (int)(li / (uint32_t)nx), ix = (int)(li - (uint32_t)iy * nx);
+    const uint64_t k = exact_key(iy, ix);
+    bkey = k < bkey ? k : bkey;
+    atomicMin(&ub_s, (uint32_t)(k >> 32));
+  }
+  __syncthreads();
+  const uint32_t ub = ub_s;
+  // (3) compact the surviving candidates (LB <= UB) and evaluate them
+  for (int t = tid; t < tasks; t += kFsThreads) {
+    if (tmin[t] > ub) continue;
+    const uint32_t m = sea_tile4<SAME>(c, jb, a.hp, t, ub);
+    if (m) {
+      const uint32_t slot = atomicAdd(&cnt, 1u);
+      ltile[slot] = (uint32_t)t;
+      lmask[slot] = m;
     }
-    __syncthreads();
-    const uint32_t ub = ub_s;
-    // (C) compact the surviving candidates (LB <= UB) and evaluate them
-    for (int t = tid; t < tasks; t += kFsThreads) {
-      if (tmin[t] > ub) continue;
-      uint32_t m;
-      lb_tile(t, ub, &m);
-      if (m) {
-        const uint32_t slot = atomicAdd(&cnt, 1u);
-        ltile[slot] = (uint32_t)t;
-        lmask[slot] = m;
-      }
-    }
-    __syncthreads();
-    const int ns = (int)cnt;
-    {  // exclusive prefix of the survivors' popcounts: 2 entries per thread,
-       // wave scans by shuffles, wave totals through LDS
-      __shared__ uint32_t wsum[kFsThreads / 64];
-      const int e0 = 2 * tid;
-      const uint32_t p0 = e0 < ns ? __builtin_popcount(lmask[e0]) : 0u;
-      const uint32_t p1 = e0 + 1 < ns ? __builtin_popcount(lmask[e0 + 1]) : 0u;
-      uint32_t v = p0 + p1, inc = v;
-      const int lane = tid & 63;
+  }
+  __syncthreads();
+  const int ns = (int)cnt;
+  // exclusive prefix of the survivors' popcounts: wave scans by shuffles,
+  // wave totals through LDS, entries strided over the workgroup
+  __shared__ uint32_t wsum[kFsThreads / 64];
+  uint32_t carry = 0;
+  for (int e0 = 0; e0 < ns; e0 += kFsThreads) {
+    const int e = e0 + tid;
+    const uint32_t v = e < ns ? __builtin_popcount(lmask[e]) : 0u;
+    uint32_t inc = v;
+    const int lane = tid & 63;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += u;
-      }
-      if (lane == 63) wsum[tid >> 6] = inc;
-      __syncthreads();
-      uint32_t base = 0;
-      for (int w = 0; w < (tid >> 6); w++) base += wsum[w];
-      const uint32_t ex = base + inc - v;
-      if (e0 < ns) lpre[e0] = ex;
-      if (e0 + 1 < ns) lpre[e0 + 1] = ex + p0;
-      if (tid == kFsThreads - 1) lpre[ns] = base + inc;
-      if (ns == 0 && tid == 0) lpre[0] = 0;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
     }
+    if (lane == 63) wsum[tid >> 6] = inc;
     __syncthreads();
-    const int nsurv = (int)lpre[ns];
-    for (int k = tid; k < nsurv; k += kFsThreads) {
-      int lo = 0, hi = ns - 1;  // entry e with lpre[e] <= k < lpre[e + 1]
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (lpre[mid] <= (uint32_t)k) lo = mid;
-        else hi = mid - 1;
-      }
-      uint32_t m = lmask[lo];
-      for (uint32_t r = (uint32_t)k - lpre[lo]; r; r--) m &= m - 1;  // r-th set bit
-      const int bit = __builtin_ctz(m);
-      const int t = (int)ltile[lo], tcy = t / tx_n, tcx = t - tcy * tx_n;
-      const int y = tcy * kTileRows + (bit >> 2), x = 4 * tcx + (bit & 3);
-      const uint64_t key = exact_key(y, x, y0 + y, x);
-      bkey = key < bkey ? key : bkey;
+    uint32_t base = carry, tot = 0;
+    for (int w = 0; w < kFsThreads / 64; w++) {
+      if (w < (tid >> 6)) base += wsum[w];
+      tot += wsum[w];
     }
-    if (tid < 64) atomicMin(&ub_s, (uint32_t)(group_min_u64(bkey) >> 32));
+    if (e < ns) lpre[e] = base + inc - v;
+    carry += tot;
+    __syncthreads();  // wsum reuse
+  }
+  if (tid == 0) lpre[ns] = carry;
+  __syncthreads();
+  const int nsurv = (int)lpre[ns];
+  for (int k = tid; k < nsurv; k += kFsThreads) {
+    int lo = 0, hi = ns - 1;  // entry e with lpre[e] <= k < lpre[e + 1]
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (lpre[mid] <= (uint32_t)k) lo = mid;
+      else hi = mid - 1;
+    }
+    uint32_t m = lmask[lo];
+    for (uint32_t r = (uint32_t)k - lpre[lo]; r; r--) m &= m - 1;  // r-th set bit
+    const int bit = __builtin_ctz(m);
+    const int t = (int)ltile[lo], tcy = t / c.tx_n, tcx = t - tcy * c.tx_n;
+    const int iy = tcy * kTileRows + (bit >> 2), ix = 4 * tcx + (bit & 3);
+    const uint64_t key = exact_key(iy, ix);
+    bkey = key < bkey ? key : bkey;
   }
   Best b{~0ull, 0xffffffffu};
   if (bkey != ~0ull) b = Best{bkey >> 32, (uint32_t)bkey};
@@ -641,20 +665,163 @@ __global__ __launch_bounds__(kFsThreads) void fs16_sea_kernel(FsArgs a) {
   }
 }
 
+template <typename Px>
+__device__ __forceinline__ void fs16_sea_body(const FsArgs &a) {
+  constexpr int B = (int)sizeof(Px), ODW = 4 * B;
+  __shared__ uint32_t orgs[16 * ODW];
+  __shared__ uint32_t so[4], so4[16], s4p[8];
+  __shared__ uint32_t tmin[kSeaMaxTiles];
+  __shared__ uint32_t lmask[kSeaMaxTiles], ltile[kSeaMaxTiles], lpre[kSeaMaxTiles + 1];
+  __shared__ uint32_t cnt, ub_s;
+  const int job = fs_job_index();
+  if (job >= a.n) return;
+  const rv_fs_job jb = a.jobs[job];
+  const int r_idx = job / a.n_per_ref;
+  const rv_plane &ref = a.ref[r_idx];
+  SeaCtx c;
+  c.nx = jb.x_hi >= jb.x_lo ? jb.x_hi - jb.x_lo + 1 : 0;
+  c.ny = jb.y_hi >= jb.y_lo ? jb.y_hi - jb.y_lo + 1 : 0;
+  c.tx_n = (c.nx + 3) >> 2;
+  const int tasks = c.tx_n * ((c.ny + kTileRows - 1) / kTileRows);
+  // window larger than the tile lists, or lambdas whose costs could reach
+  // the out-of-window marker: exhaustive path
+  if (tasks > kSeaMaxTiles || jb.lambda >= (1u << 23)) {
+    const rv_fs_result res = fs_generic_body<Px>(a.org, ref, jb, 16, 16, 1, a.hp, a.out + job);
+    if (threadIdx.x == 0) chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, res.best_mv);
+    return;
+  }
+  const int tid = threadIdx.x;
+  if (tid < 16 * ODW) {
+    const uint8_t *o = (const uint8_t *)plane_ptr<Px>(a.org, jb.po_x, jb.po_y);
+    orgs[tid] = load_u32_unaligned(o + (int64_t)(tid / ODW) * a.org.stride * B + 4 * (tid % ODW));
+  }
+  if (tid == 0) {
+    ub_s = 0xffffffffu;
+    cnt = 0;
+  }
+  __syncthreads();
+  if (tid < 16) {  // 4x4 block sums of the source block (row-major blocks)
+    uint32_t t = 0;
+    for (int r = 0; r < 4; r++)
+      for (int i = 0; i < B; i++)
+        t = sad_px<Px>(orgs[(4 * (tid >> 2) + r) * ODW + B * (tid & 3) + i], 0u, t);
+    so4[tid] = t;
+  }
+  __syncthreads();
+  if (tid < 4) {  // 8x8 quadrants
+    const int b0 = 8 * (tid >> 1) + 2 * (tid & 1);
+    so[tid] = so4[b0] + so4[b0 + 1] + so4[b0 + 4] + so4[b0 + 5];
+  }
+  if (tid < 8) s4p[tid] = so4[2 * tid] | (so4[2 * tid + 1] << 16);
+  __syncthreads();
+  c.so01 = so[0] | (so[1] << 16);
+  c.so23 = so[2] | (so[3] << 16);
+  c.s4 = s4p;
+  c.stride = ref.stride;
+  const int64_t wo = plane_origin_index(ref) + (int64_t)jb.y_lo * ref.stride + jb.x_lo;
+  c.box = a.box[r_idx] + wo;
+  c.box4 = a.box[r_idx] + (int64_t)ref.stride * ref.alloc_height + wo;
+  if (jb.pmv[0].row == jb.pmv[1].row && jb.pmv[0].col == jb.pmv[1].col)
+    sea_search<Px, true>(a, jb, job, ref, c, orgs, tmin, lmask, ltile, lpre, cnt, ub_s);
+  else
+    sea_search<Px, false>(a, jb, job, ref, c, orgs, tmin, lmask, ltile, lpre, cnt, ub_s);
+}
+
+// u8: capped at 128 VGPRs (4 waves per SIMD) without spilling; u16 keeps
+// its registers (the cap would spill).
+__global__ __launch_bounds__(kFsThreads) __attribute__((amdgpu_waves_per_eu(4))) void
+fs16_sea_kernel_u8(FsArgs a) {
+  fs16_sea_body<uint8_t>(a);
+}
+__global__ __launch_bounds__(kFsThreads) void fs16_sea_kernel_u16(FsArgs a) {
+  fs16_sea_body<uint16_t>(a);
+}
+
+// Paired box sums (rv_plane_box_sums).  blockIdx.z = 0: S8 pairs, 1: S4
+// pairs.  A thread computes 4 adjacent positions x 8 rows, for x and x + D
+// (D = 8 or 4), from dword-aligned loads (the pixels under positions
+// ax .. ax + 3 + D + K - 1 lie in 5 aligned dwords for u8, 10 for u16),
+// sliding the vertical K-row sums over 7 + K rows of horizontal K-sums; one
+// 16-byte store per row.  Stride is a multiple of 32 bytes (Plane::new).
+template <typename Px, int K>
+__device__ __forceinline__ void box_rows(const rv_plane &p, uint32_t *box, int ax, int ay0) {
+  constexpr int B = (int)sizeof(Px);
+  constexpr int NDW = 5 * B;
+  constexpr int NR = 7 + K;  // rows of horizontal sums
+  const uint32_t *base =
+      reinterpret_cast<const uint32_t *>((const uint8_t *)p.data + ((int64_t)ay0 * p.stride + ax) * B);
+  const int rdw = p.stride * B / 4;          // dwords per row
+  const int ndw = (p.stride - ax) * B / 4;   // dwords left in the row
+  uint32_t h[NR][8];  // horizontal K-sums at ax + j (j < 4) and ax + K + (j - 4)
+#pragma unroll
+  for (int k = 0; k < NR; k++) {
+    uint32_t w[NDW + 1];
+#pragma unroll
+    for (int i = 0; i <= NDW; i++)
+      w[i] = (ay0 + k < p.alloc_height && i < ndw) ? base[(int64_t)k * rdw + i] : 0u;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int x = j < 4 ? j : j - 4 + K;  // pixel offset of the position
+      uint32_t t = 0;
+#pragma unroll
+      for (int g = 0; g < K; g += 4) {  // 4-pixel groups
+        if constexpr (B == 1) {
+          const int d = (x + g) >> 2, sh = (x + g) & 3;
+          t = __builtin_amdgcn_sad_u8(sh ? __builtin_amdgcn_alignbyte(w[d + 1], w[d], sh) : w[d], 0u, t);
+        } else {  // u16: dword (x + g) / 2, half-word (x + g) & 1
+          const int d = (x + g) >> 1;
+#pragma unroll
+          for (int i = 0; i < 2; i++)
+            t = __builtin_amdgcn_sad_u16(((x + g) & 1) ? __builtin_amdgcn_alignbyte(w[d + i + 1], w[d + i], 2)
+                                                       : w[d + i],
+                                         0u, t);
+        }
+      }
+      h[k][j] = t;
+    }
+  }
+  uint32_t acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    acc[j] = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) acc[j] += h[k][j];
+  }
+#pragma unroll
+  for (int u = 0; u < 8; u++) {
+    const int ay = ay0 + u;
+    if (ay < p.alloc_height) {
+      // a half whose block leaves the allocation is 0
+      const bool vy = ay + K <= p.alloc_height;
+      uint32_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t lo = vy && ax + j + K <= p.stride ? acc[j] : 0u;
+        const uint32_t hi = vy && ax + j + 2 * K <= p.stride ? acc[j + 4] : 0u;
+        v[j] = lo | (hi << 16);
+      }
+      *reinterpret_cast<uint4 *>(box + (int64_t)ay * p.stride + ax) = uint4{v[0], v[1], v[2], v[3]};
+    }
+    if (u < 7)
+#pragma unroll
+      for (int j = 0; j < 8; j++) acc[j] += h[u + K][j] - h[u][j];
+  }
+}
+
+template <typename Px>
+__global__ __launch_bounds__(64) void box_sums_kernel(rv_plane p, uint32_t *box) {
+  const int ax = ((int)blockIdx.x * 64 + (int)threadIdx.x) * 4;
+  const int ay0 = (int)blockIdx.y * 8;
+  if (ax >= p.stride || ay0 >= p.alloc_height) return;
+  if (blockIdx.z == 0)
+    box_rows<Px, 8>(p, box, ax, ay0);
+  else
+    box_rows<Px, 4>(p, box + (int64_t)p.stride * p.alloc_height, ax, ay0);
+}
+
 }  // namespace rv
 
 using namespace rv;
-
-// RAV1E_HIP_FS_SEA=1 selects the successive-elimination u8 path (read per
-// launch).  Off by default: measured 2.2x slower than the exhaustive tile
-// kernel on the 1080p replay -- the first band's upper bound is loose
-// (the window centre, where the best usually is, sits in a middle band)
-// and the phase barriers at 2 workgroups per CU cost more than the pruned
-// SADs save.  Kept, exact and tested, as the base for a centre-first probe.
-static bool sea_enabled() {
-  const char *e = getenv("RAV1E_HIP_FS_SEA");
-  return e && e[0] == '1';
-}
 
 // Multi-reference form used by the replay driver: jobs [n_refs][n_per_ref],
 // job i searches refs[i / n_per_ref], all in one launch; `next` (may be
@@ -662,7 +829,7 @@ static bool sea_enabled() {
 int rv_full_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
                          const rv_fs_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
                          int step, int allow_hp, rv_fs_result *d_out, const ChainNext *next,
-                         void *stream) {
+                         const uint32_t *const *box, void *stream) {
   if (!org || !refs || n_refs < 1 || n_refs > RV_DS_MAX_PRED || n_per_ref < 0 || blk_w < 4 ||
       blk_h < 4 || blk_w > 128 || blk_h > 128 || (blk_w & 3) || step < 1)
     return rv_set_error(RV_EINVAL, "rv_full_search_batch: bad arguments");
@@ -685,9 +852,20 @@ int rv_full_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
   a.bh = blk_h;
   a.step = step;
   if (next) a.next = *next;
+  const bool sea = box && blk_w == 16 && blk_h == 16 && step == 1;
+  if (sea)
+    for (int k = 0; k < n_refs; k++) {
+      if (!box[k] || ((uintptr_t)box[k] & 15))
+        return rv_set_error(RV_EINVAL, "rv_full_search_sea_batch: box-sum table null or unaligned");
+      if (refs[k].stride % 4)
+        return rv_set_error(RV_EINVAL, "rv_full_search_sea_batch: ref stride not Plane::new's");
+      a.box[k] = box[k];
+    }
   const unsigned grid = (unsigned)((n + 7) / 8 * 8);
-  if (blk_w == 16 && blk_h == 16 && step == 1 && !org->hbd && sea_enabled())
-    fs16_sea_kernel<<<grid, kFsThreads, kSeaLdsBytes, s>>>(a);
+  if (sea && org->hbd)
+    fs16_sea_kernel_u16<<<grid, kFsThreads, 0, s>>>(a);
+  else if (sea)
+    fs16_sea_kernel_u8<<<grid, kFsThreads, 0, s>>>(a);
   else if (blk_w == 16 && blk_h == 16 && step == 1 && org->hbd)
     fs16_kernel<uint16_t><<<grid, kFsThreads, 0, s>>>(a);
   else if (blk_w == 16 && blk_h == 16 && step == 1)
@@ -706,5 +884,29 @@ extern "C" int rv_full_search_batch(const rv_plane *org, const rv_plane *ref,
                                     rv_fs_result *d_out, void *stream) {
   if (!ref) return rv_set_error(RV_EINVAL, "rv_full_search_batch: null ref");
   return rv_full_search_multi(org, ref, 1, d_jobs, n, blk_w, blk_h, step, allow_hp, d_out,
-                              nullptr, stream);
+                              nullptr, nullptr, stream);
+}
+
+extern "C" int rv_full_search_sea_batch(const rv_plane *org, const rv_plane *ref,
+                                        const uint32_t *d_ref_box, const rv_fs_job *d_jobs, int n,
+                                        int allow_hp, rv_fs_result *d_out, void *stream) {
+  if (!ref || !d_ref_box)
+    return rv_set_error(RV_EINVAL, "rv_full_search_sea_batch: null ref or box-sum table");
+  return rv_full_search_multi(org, ref, 1, d_jobs, n, 16, 16, 1, allow_hp, d_out, nullptr,
+                              &d_ref_box, stream);
+}
+
+extern "C" int rv_plane_box_sums(const rv_plane *p, uint32_t *d_box, void *stream) {
+  if (!p || !p->data || !d_box || p->stride < 1 || p->alloc_height < 1)
+    return rv_set_error(RV_EINVAL, "rv_plane_box_sums: bad arguments");
+  hipStream_t s = rv_resolve_stream(stream);
+  if (p->stride % (p->hbd ? 16 : 32) || ((uintptr_t)p->data & 15) || ((uintptr_t)d_box & 15))
+    return rv_set_error(RV_EINVAL, "rv_plane_box_sums: plane stride / alignment not Plane::new's");
+  const dim3 grid((unsigned)((p->stride / 4 + 63) / 64), (unsigned)((p->alloc_height + 7) / 8), 2);
+  if (p->hbd)
+    box_sums_kernel<uint16_t><<<grid, 64, 0, s>>>(*p, d_box);
+  else
+    box_sums_kernel<uint8_t><<<grid, 64, 0, s>>>(*p, d_box);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
 }

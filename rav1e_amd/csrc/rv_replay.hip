@@ -38,7 +38,7 @@
 int rv_full_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
                          const rv_fs_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
                          int step, int allow_hp, rv_fs_result *d_out, const rv::ChainNext *next,
-                         void *stream);
+                         const uint32_t *const *box, void *stream);
 int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
                             const rv_ds_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
                             int subpixel, int use_satd, int allow_hp, int bit_depth,
@@ -193,6 +193,7 @@ using namespace rv;
 
 struct RvFrameSlot {
   rv_plane y, u, v, hres, qres;
+  uint32_t *qres_box = nullptr;  // rv_plane_box_sums of qres (the SEA coarse search)
   void *mem = nullptr;
 };
 
@@ -202,6 +203,7 @@ struct rv_replay {
   hipStream_t stream;
   hipStream_t side;  // zero-MV RDO candidates, concurrent with the searches
   bool own_stream;
+  bool sea;  // successive-elimination coarse search (bit depth <= 10)
   double me_lambda;
   std::vector<RvFrameSlot> slots;  // 0 = input, 1..R = references
   // scratch
@@ -262,7 +264,8 @@ bool alloc_slot(rv_replay *r, RvFrameSlot &s) {
   size_t bq = rv_plane_geometry(&s.qres, g.W / 4, g.H / 4, 2, 2, pad / 4, pad / 4, g.hbd);
   const size_t al = 256;
   auto up = [&](size_t v) { return (v + al - 1) / al * al; };
-  size_t total = up(by) + up(bu) + up(bv) + up(bh) + up(bq);
+  const size_t bs8 = (size_t)s.qres.stride * s.qres.alloc_height * 8;
+  size_t total = up(by) + up(bu) + up(bv) + up(bh) + up(bq) + up(bs8);
   uint8_t *m = (uint8_t *)dalloc(r, total);
   if (!m) return false;
   s.mem = m;
@@ -275,6 +278,8 @@ bool alloc_slot(rv_replay *r, RvFrameSlot &s) {
   s.hres.data = m;
   m += up(bh);
   s.qres.data = m;
+  m += up(bq);
+  s.qres_box = (uint32_t *)m;
   return hipMemsetAsync(s.mem, 0, total, r->stream) == hipSuccess;
 }
 
@@ -481,6 +486,9 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   // me_lambda = sqrt(lambda), lambda scaled by 1 << 2 (bd - 8)
   // (src/encoder.rs:876-878); the replay fixes the 8-bit value.
   r->me_lambda = 24.0 * (double)(1 << (g.bd - 8));
+  // 8x8 sums of 10-bit pixels fit the u16 box-sum table; 12-bit searches
+  // exhaustively
+  r->sea = g.bd <= 10 && (cfg->flags & RV_REPLAY_EXHAUSTIVE_FS) == 0;
   if (stream) {
     r->stream = (hipStream_t)stream;
     r->own_stream = false;
@@ -570,6 +578,7 @@ int rv_replay_set_frame(rv_replay *r, int slot, const void *host_yuv) {
   p += (size_t)s.u.width * s.u.height * px;
   RV_R(upload_plane(r, s.v, p));
   RV_R(rv_plane_pyramid(&s.y, &s.hres, &s.qres, r->stream));
+  if (r->sea) RV_R(rv_plane_box_sums(&s.qres, s.qres_box, r->stream));
   RV_H(hipStreamSynchronize(r->stream));
   return RV_OK;
 }
@@ -681,10 +690,16 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
   }
   // F0 hres + qres of the input (encode_frame, src/encoder.rs:3382-3385)
   RV_R(rv_plane_pyramid(&cur.y, &cur.hres, &cur.qres, st));
+  // box sums of the input's qres: the table this frame's coarse search
+  // needs once it is a reference (one per frame in a real encode; the
+  // replay's references are fixed, so it is computed and not consumed)
+  if (r->sea) RV_R(rv_plane_box_sums(&cur.qres, cur.qres_box, st));
   RV_EV(1, st);
   // F1 coarse full search, every reference in one launch -> F2 predictors
+  const uint32_t *box[RV_DS_MAX_PRED];
+  for (int k = 0; k < g.R; k++) box[k] = r->slots[1 + k].qres_box;
   RV_R(rv_full_search_multi(&cur.qres, refs_q, g.R, r->fs_jobs[si], nr, 16, 16, 1, 0, r->coarse,
-                            &to_half, st));
+                            &to_half, r->sea ? box : nullptr, st));
   RV_EV(2, st);
   // F2 half-res diamond -> F3 full-pel predictors
   RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half, nr, 32, 32, 0, 0, 0, g.bd,

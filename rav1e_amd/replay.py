@@ -16,6 +16,7 @@ from . import RvReplayCfg, _check, lib
 
 RV_REPLAY_SIDE_RDO = 1  # include/rav1e_hip.h
 RV_REPLAY_SPLIT_RDO = 2
+RV_REPLAY_EXHAUSTIVE_FS = 4  # F1 without successive elimination (same results)
 
 # GOP of the reference's reorder pyramid (src/api/internal.rs:61-95):
 # group_input_len 4, levels 0,1,2,2 -> me_range_scale = 4 >> level

@@ -323,30 +323,31 @@ def _fs_case(rng, hbd, blk, nj, flat=False):
 
 @pytest.mark.parametrize("hbd,blk,step", [(False, 16, 1), (False, 32, 1), (True, 16, 1),
                                           (False, 8, 2), (False, 16, 3)])
-@pytest.mark.parametrize("sea", ["0", "1"])
-def test_full_search_vs_oracle(hbd, blk, step, sea, monkeypatch):
-    monkeypatch.setenv("RAV1E_HIP_FS_SEA", sea)
-    _full_search_vs_oracle(hbd, blk, step)
-
-
-def _full_search_vs_oracle(hbd, blk, step):
+@pytest.mark.parametrize("sea", [False, True])
+def test_full_search_vs_oracle(hbd, blk, step, sea):
+    """Exhaustive kernels and (16x16, step 1) the successive-elimination
+    path over box-sum tables vs orc_full_search."""
+    if sea and (blk, step) != (16, 1):
+        pytest.skip("the SEA entry point is 16x16, step 1")
     rng = np.random.default_rng(800 + blk + step)
     po_, pr_, fo, fr, xo, yo, jobs = _fs_case(rng, hbd, blk, 12)
-    got = R.full_search_batch(po_, pr_, jobs, blk, blk, step, allow_hp=False)
+    if sea:
+        got = R.full_search_sea_batch(po_, pr_, jobs)
+    else:
+        got = R.full_search_batch(po_, pr_, jobs, blk, blk, step, allow_hp=False)
     for k, j in enumerate(jobs):
         mv, cost = O.full_search(fo, fr, xo, yo, j, blk, blk, step, 0)
         assert (got[k]["mv_row"], got[k]["mv_col"], got[k]["cost"]) == (mv[0], mv[1], cost), k
 
 
-@pytest.mark.parametrize("sea", ["0", "1"])
+@pytest.mark.parametrize("sea", [False, True])
 @pytest.mark.parametrize("scale", [4, 2, 1])
-def test_full_search_replay_windows_vs_oracle(scale, sea, monkeypatch):
+def test_full_search_replay_windows_vs_oracle(scale, sea):
     """The quarter-res coarse search of the replay (estimate_motion_ss4
     windows at me_range_scale 4/2/1, natural-ish content): the exact
     successive-elimination path must return the oracle's exhaustive
     argmin (cost and first raster index)."""
     from rav1e_amd import replay as RP
-    monkeypatch.setenv("RAV1E_HIP_FS_SEA", sea)
     W, H = 640, 384
     q = []
     for t in (0, 1):
@@ -367,22 +368,79 @@ def test_full_search_replay_windows_vs_oracle(scale, sea, monkeypatch):
         jobs[k] = (px, py, max(px - rx, -20), min(px + rx, qw - 16 + 20), max(py - ry, -20),
                    min(py + ry, qh - 16 + 20), int(rng.integers(-40, 40)),
                    int(rng.integers(-40, 40)), 0, 0, int(rng.integers(0, 200)), 0)
-    got = R.full_search_batch(po_, pr_, jobs, 16, 16, 1)
+    if sea:
+        got = R.full_search_sea_batch(po_, pr_, jobs)
+    else:
+        got = R.full_search_batch(po_, pr_, jobs, 16, 16, 1)
     for k, j in enumerate(jobs):
         mv, cost = O.full_search(fo, fr, xo, yo, j, 16, 16, 1, 0)
         assert (got[k]["mv_row"], got[k]["mv_col"], got[k]["cost"]) == (mv[0], mv[1], cost), k
 
 
-def test_full_search_ties_keep_first_raster_candidate():
+@pytest.mark.parametrize("sea", [False, True])
+def test_full_search_ties_keep_first_raster_candidate(sea):
     rng = np.random.default_rng(900)
     po_, pr_, fo, fr, xo, yo, jobs = _fs_case(rng, False, 16, 6, flat=True)
     jobs["lambda_"] = 0  # every candidate costs 0: the first raster one wins
-    got = R.full_search_batch(po_, pr_, jobs, 16, 16, 1)
+    if sea:
+        got = R.full_search_sea_batch(po_, pr_, jobs)
+    else:
+        got = R.full_search_batch(po_, pr_, jobs, 16, 16, 1)
     for k, j in enumerate(jobs):
         mv, cost = O.full_search(fo, fr, xo, yo, j, 16, 16, 1, 0)
         assert cost == 0
         assert (got[k]["mv_row"], got[k]["mv_col"]) == mv
         assert mv == (8 * (j["y_lo"] - j["po_y"]), 8 * (j["x_lo"] - j["po_x"]))
+
+
+@pytest.mark.parametrize("hbd", [False, True])
+def test_plane_box_sums_vs_numpy(hbd):
+    """rv_plane_box_sums over the whole allocation (padding included) vs an
+    integral-image box sum, paired as SK(x, y) | SK(x + K, y) << 16 for K = 8
+    then K = 4; a half whose block leaves the allocation is 0."""
+    rng = np.random.default_rng(950 + hbd)
+    a = rand_plane(rng, 70, 90, 10 if hbd else 8)
+    p = R.DevicePlane.from_array(a, xpad=12, ypad=12)
+    full = p.download_full().astype(np.int64)
+    got = R.plane_box_sums(p).download(np.uint32).reshape((2,) + full.shape).astype(np.int64)
+    ii = np.zeros((full.shape[0] + 1, full.shape[1] + 1), np.int64)
+    ii[1:, 1:] = full.cumsum(0).cumsum(1)
+    for t, k in enumerate((8, 4)):
+        sk = np.zeros(full.shape, np.int64)
+        sk[:1 - k or None, :1 - k or None] = ii[k:, k:] - ii[:-k, k:] - ii[k:, :-k] + ii[:-k, :-k]
+        hi = np.zeros_like(sk)
+        hi[:, :-k] = sk[:, k:]
+        np.testing.assert_array_equal(got[t] & 0xFFFF, sk, err_msg=f"K={k} low")
+        np.testing.assert_array_equal(got[t] >> 16, hi, err_msg=f"K={k} high")
+
+
+@pytest.mark.parametrize("hbd", [False, True])
+def test_full_search_sea_pruning_edge_cases(hbd):
+    """SEA path: flat + textured mixes, huge lambdas (exhaustive fallback),
+    windows clipped into the padding, the mv-0 probe outside the window."""
+    rng = np.random.default_rng(960 + hbd)
+    bd = 10 if hbd else 8
+    org = rand_plane(rng, 120, 200, bd)
+    org[:, :100] = org[:, :100] // 64 * 64  # quantised half: many LB ties
+    ref = np.roll(org, (2, 7), (0, 1))
+    po_, pr_ = R.DevicePlane.from_array(org, xpad=24, ypad=24), R.DevicePlane.from_array(
+        ref, xpad=24, ypad=24)
+    fo, fr = po_.download_full(), pr_.download_full()
+    xo, yo = po_.desc.xorigin, po_.desc.yorigin
+    jobs = np.zeros(10, dtype=R.FS_JOB)
+    for k in range(len(jobs)):
+        px, py = int(rng.integers(0, 200 - 16)), int(rng.integers(0, 120 - 16))
+        lam = [0, 40, 3000, (1 << 23) - 1, 1 << 23, (1 << 26) + 5][k % 6]
+        if k == 7:  # window far from mv 0: the probe finds nothing
+            jobs[k] = (px, py, -24, -24 + 30, -24, -24 + 9, 0, 0, 0, 0, lam, 0)
+            continue
+        jobs[k] = (px, py, max(px - 40, -24), min(px + 40, 200 - 16 + 24), max(py - 12, -24),
+                   min(py + 12, 120 - 16 + 24), int(rng.integers(-40, 40)),
+                   int(rng.integers(-40, 40)), 0, 0, lam, 0)
+    got = R.full_search_sea_batch(po_, pr_, jobs)
+    for k, j in enumerate(jobs):
+        mv, cost = O.full_search(fo, fr, xo, yo, j, 16, 16, 1, 0)
+        assert (got[k]["mv_row"], got[k]["mv_col"], got[k]["cost"]) == (mv[0], mv[1], cost), k
 
 
 def test_full_search_empty_window():

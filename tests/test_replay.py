@@ -53,7 +53,8 @@ def test_cpu_replay_thread_invariant():
     (256, 128, 1, 1, 10, 2, None),
     (384, 192, 1, 1, 8, 2, (2, 0, 4, 3)),
 ])
-@pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_SIDE_RDO, RP.RV_REPLAY_SPLIT_RDO])
+@pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_SIDE_RDO, RP.RV_REPLAY_SPLIT_RDO,
+                                   RP.RV_REPLAY_EXHAUSTIVE_FS])
 def test_gpu_replay_matches_cpu_replay(w, h, xdec, ydec, bd, refs, tile, flags):
     import rav1e_amd as R
     R.require_device(0)
