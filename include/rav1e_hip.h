@@ -271,18 +271,18 @@ int rv_full_search_batch(const rv_plane *org, const rv_plane *ref,
  * bits), for the successive-elimination search below.  d_box (16-byte
  * aligned) holds two tables with the plane's geometry, n = stride *
  * alloc_height u32 each: entry (ax, ay) of the allocation in [0, n) is
- * S8(ax, ay) | S8(ax + 8, ay) << 16, in [n, 2n) S4(ax, ay) | S4(ax + 4, ay)
- * << 16, SK = the sum of the K x K pixels whose top-left corner is there (0
- * where that block would leave the allocation).  A reference frame needs
+ * S48(ax, ay) | S48(ax + 8, ay) << 16, in [n, 2n) S4(ax, ay) | S4(ax + 4, ay)
+ * << 16; S48 / S4 = the sum of the 4-tall x 8-wide / 4x4 pixels whose
+ * top-left corner is there (0 where that block would leave the allocation).  A reference frame needs
  * them once (rav1e searches each input_qres as a reference for several
  * frames). */
 int rv_plane_box_sums(const rv_plane *p, uint32_t *d_box, void *stream);
 
 /* rv_full_search_batch for 16x16 blocks, step 1 (estimate_motion_ss4's
  * quarter-resolution search, src/me.rs:1023-1075) with exact successive
- * elimination: SAD >= sum over the four 8x8 quadrants (and over the
- * sixteen 4x4 blocks) of |S_org - S_ref|, so every candidate whose lower
- * bound exceeds an achieved cost is skipped.  Results are identical to
+ * elimination: SAD >= sum over the eight 4x8 blocks (and over the sixteen
+ * 4x4 blocks) of |S_org - S_ref|, so every candidate whose lower bound
+ * exceeds an achieved cost is skipped.  Results are identical to
  * rv_full_search_batch (same cost, same first raster minimum).
  * d_ref_box = rv_plane_box_sums of ref. */
 int rv_full_search_sea_batch(const rv_plane *org, const rv_plane *ref,

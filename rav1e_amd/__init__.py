@@ -519,8 +519,8 @@ def full_search_batch(org: DevicePlane, ref: DevicePlane, jobs, blk_w, blk_h, st
 
 
 def plane_box_sums(plane: DevicePlane) -> DeviceBuffer:
-    """rv_plane_box_sums: paired 8x8 then paired 4x4 box sums over the whole
-    allocation (u32 S8(x, y) | S8(x + 8, y) << 16, then S4(x, y) |
+    """rv_plane_box_sums: paired 4-tall x 8-wide then paired 4x4 box sums over
+    the whole allocation (u32 S48(x, y) | S48(x + 8, y) << 16, then S4(x, y) |
     S4(x + 4, y) << 16, each in the plane's stride x alloc_height layout)."""
     d = plane.desc
     out = DeviceBuffer(8 * d.stride * d.alloc_height)

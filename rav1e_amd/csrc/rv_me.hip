@@ -365,30 +365,33 @@ __global__ __launch_bounds__(kFsThreads) void fs16_kernel(FsArgs a) {
 
 // ---- exact successive-elimination path: 16x16, step 1 ---------------------
 // The triangle inequality bounds every candidate from below:
-//   SAD(org, cand) >= sum over the four 8x8 quadrants q of |S_org,q - S_cand,q|
+//   SAD(org, cand) >= sum over any partition into blocks q of |S_org,q - S_cand,q|
 // (S = pixel sum), so cost >= LB = 256 * that + rate * lambda.  A candidate
 // whose LB exceeds an achieved cost UB cannot be the strict first minimum,
 // so skipping it leaves the result of full_search (src/me.rs:943-990)
 // unchanged bit for bit.  The reference's box sums come from tables built
 // once per reference frame (rv_plane_box_sums; every superblock of several
 // frames searches the same reference), stored as horizontal pairs
-// (S8(x, y) | S8(x + 8, y) << 16 and S4(x, y) | S4(x + 4, y) << 16), so one
-// v_sad_u16 against the packed source sums gives two block terms: the 8x8
-// bound of a candidate is 2 v_sad_u16 + 1 add from two aligned dwords, the
-// sharper 4x4 bound (16 blocks) 8 v_sad_u16.  Per job:
-//   (1) the 16x16 neighbourhood of mv 0 (where natural motion puts the
-//       minimum) is evaluated exactly -> UB;
-//   (2) one pass over 4-wide x 8-tall candidate tiles computes every LB
-//       (16 dwordx4 table rows per tile, L2-resident), keeps each tile's
-//       minimum in LDS, and every lane evaluates the minimum-LB candidate of
-//       its best tile exactly -> UB (now the cost of some valid candidate);
-//   (3) tiles whose minimum is <= UB are revisited with the sharper 4x4
-//       bound (on the replay's content it keeps ~1 in 40 of the 8x8
-//       survivors); its survivors are compacted and evaluated exactly,
-//       spread over all lanes.
+// (S48(x, y) | S48(x + 8, y) << 16 for 4-tall x 8-wide blocks and
+// S4(x, y) | S4(x + 4, y) << 16), so one v_sad_u16 against the packed
+// source sums gives two block terms: the 8-block bound of a candidate is 4
+// v_sad_u16 from four aligned dwords, the sharper 16-block 4x4 bound 8.
+// Per job:
+//   (1) the 16x16 neighbourhood of mv 0 (clamped into the window; natural
+//       motion puts the minimum there) is evaluated exactly -> UB;
+//   (2) the window's 4-wide x 8-tall candidate tiles are taken in chunks of
+//       one tile per lane: each lane computes its tile's 8-block bounds (24
+//       dwordx4 table rows, L2-resident) against the live UB and appends the
+//       survivors to an LDS list (on the replay's content ~1 in 150
+//       candidates; 8x8 quadrants would keep ~9x more); then the list is
+//       spread over all lanes, each survivor checked against the 4x4 bound
+//       (which keeps ~1 in 5) and, if it passes, evaluated exactly (which
+//       tightens the UB for the next chunk).
 // Out-of-window candidates of edge tiles get a bound >= 2^30, above every
 // real cost (lambda < 2^23 here; larger lambdas take the exhaustive path).
-constexpr int kSeaMaxTiles = 1664;  // 97 x 17: the me_range_scale 4 window
+// The list holds a chunk's worst case (256 tiles x 32), so it never
+// overflows.
+constexpr int kSeaList = kFsThreads * 32;  // survivors of one chunk, worst case
 constexpr uint32_t kSeaOut = 1u << 30;
 
 // Reference rows are read with dword-aligned loads and realigned in
@@ -436,7 +439,7 @@ struct SeaCtx {
   const uint32_t *box4;  // paired 4x4 table at window position (0, 0)
   int stride;            // table row pitch (elements)
   int nx, ny, tx_n;
-  uint32_t so01, so23;   // packed source 8x8 quadrant sums
+  const uint32_t *s48;   // LDS: packed source 4-tall x 8-wide block sums, block row i: cols 0-7 | 8-15
   const uint32_t *s4;    // LDS: packed source 4x4 sums, row i: [2i] = cols 0|1, [2i+1] = cols 2|3
 };
 
@@ -474,187 +477,140 @@ struct SeaRates {
   }
 };
 
-// 8x8 lower bounds of the 32 candidates of tile t: returns the tile
-// minimum; ARG: also the raster index of its first minimum (*arg).
-template <bool ARG, bool SAME>
-__device__ __forceinline__ uint32_t sea_tile(const SeaCtx &c, const rv_fs_job &jb, int hp,
-                                             int t, uint32_t *arg) {
-  const int tcy = t / c.tx_n, tcx = t - tcy * c.tx_n;
-  const int cy0 = tcy * kTileRows;
-  uint4 row[kTileRows + 8];
-  const uint32_t *bp = c.box + (int64_t)cy0 * c.stride + 4 * tcx;
-#pragma unroll
-  for (int r = 0; r < kTileRows + 8; r++)
-    row[r] = *reinterpret_cast<const uint4 *>(bp + (int64_t)r * c.stride);
-  const SeaRates<SAME> rt(c, jb, hp, cy0, tcx);
-  uint32_t tm = 0xffffffffu, am = 0;
-#pragma unroll
-  for (int k = 0; k < kTileRows; k++) {
-    const uint32_t top[4] = {row[k].x, row[k].y, row[k].z, row[k].w};
-    const uint32_t bot[4] = {row[k + 8].x, row[k + 8].y, row[k + 8].z, row[k + 8].w};
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t l = __builtin_amdgcn_sad_u16(bot[j], c.so23, __builtin_amdgcn_sad_u16(top[j], c.so01, 0u));
-      const uint32_t lb = (l << 8) + rt.rl(k, j, jb.lambda);
-      if (ARG && lb < tm) am = (uint32_t)(k * 4 + j);
-      tm = lb < tm ? lb : tm;
-    }
-  }
-  if (ARG) *arg = (uint32_t)((cy0 + (int)(am >> 2)) * c.nx + 4 * tcx + (int)(am & 3));
-  return tm;
-}
-
-// 4x4 lower bounds (sixteen block terms, >= the 8x8 bound) of the 32
-// candidates of tile t: the mask of those <= thr.  Four passes over the
-// block rows i, each loading 8 table rows x 2 dwordx4.
+// Mask of the candidates of tile t whose 4x8 lower bound (eight 4-tall x
+// 8-wide blocks) is <= ub: 256 * l + rate * lambda <= ub, tested as
+// 256 * l + rc[j] <= ub - rr[k] when SAME.
 template <bool SAME>
-__device__ __forceinline__ uint32_t sea_tile4(const SeaCtx &c, const rv_fs_job &jb, int hp,
-                                              int t, uint32_t thr) {
+__device__ __forceinline__ uint32_t sea_tile(const SeaCtx &c, const rv_fs_job &jb, int hp,
+                                             int t, uint32_t ub) {
   const int tcy = t / c.tx_n, tcx = t - tcy * c.tx_n;
   const int cy0 = tcy * kTileRows;
+  // 8 block terms per candidate: table rows k + 4 i, i = 0..3, in two
+  // halves of 12 rows (block rows 0-1, then 2-3)
   uint32_t acc[kTileRows][4];
 #pragma unroll
   for (int k = 0; k < kTileRows; k++)
 #pragma unroll
     for (int j = 0; j < 4; j++) acc[k][j] = 0;
 #pragma unroll 1
-  for (int i = 0; i < 4; i++) {  // rolled: 16 loads in flight, not 64
-    const uint32_t s4a = c.s4[2 * i], s4b = c.s4[2 * i + 1];
-    const uint32_t *bp = c.box4 + (int64_t)(cy0 + 4 * i) * c.stride + 4 * tcx;
-    uint4 lo[kTileRows], hi[kTileRows];
+  for (int h = 0; h < 2; h++) {  // rolled: 12 loads in flight
+    const uint32_t sa = c.s48[2 * h], sb = c.s48[2 * h + 1];
+    uint4 row[kTileRows + 4];
+    const uint32_t *bp = c.box + (int64_t)(cy0 + 8 * h) * c.stride + 4 * tcx;
 #pragma unroll
-    for (int r = 0; r < kTileRows; r++) {
-      lo[r] = *reinterpret_cast<const uint4 *>(bp + (int64_t)r * c.stride);
-      hi[r] = *reinterpret_cast<const uint4 *>(bp + (int64_t)r * c.stride + 8);
-    }
+    for (int r = 0; r < kTileRows + 4; r++)
+      row[r] = *reinterpret_cast<const uint4 *>(bp + (int64_t)r * c.stride);
 #pragma unroll
     for (int k = 0; k < kTileRows; k++) {
-      const uint32_t l4[4] = {lo[k].x, lo[k].y, lo[k].z, lo[k].w};
-      const uint32_t h4[4] = {hi[k].x, hi[k].y, hi[k].z, hi[k].w};
+      const uint32_t a0[4] = {row[k].x, row[k].y, row[k].z, row[k].w};
+      const uint32_t a1[4] = {row[k + 4].x, row[k + 4].y, row[k + 4].z, row[k + 4].w};
 #pragma unroll
       for (int j = 0; j < 4; j++)
-        acc[k][j] = __builtin_amdgcn_sad_u16(h4[j], s4b, __builtin_amdgcn_sad_u16(l4[j], s4a, acc[k][j]));
+        acc[k][j] = __builtin_amdgcn_sad_u16(a1[j], sb, __builtin_amdgcn_sad_u16(a0[j], sa, acc[k][j]));
     }
   }
   const SeaRates<SAME> rt(c, jb, hp, cy0, tcx);
   uint32_t m = 0;
 #pragma unroll
-  for (int k = 0; k < kTileRows; k++)
+  for (int k = 0; k < kTileRows; k++) {
+    // SAME: the row term moves to the threshold (out-of-window rows carry
+    // kSeaOut > ub and never pass)
+    const uint32_t rk = SAME ? rt.rr0[k] : 0u;
+    const uint32_t thr = ub >= rk ? ub - rk : 0u;
+    const bool row_ok = ub >= rk;
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-      if ((acc[k][j] << 8) + rt.rl(k, j, jb.lambda) <= thr) m |= 1u << (k * 4 + j);
+    for (int j = 0; j < 4; j++) {
+      const uint32_t lb = (acc[k][j] << 8) + (SAME ? rt.rc0[j] : rt.rl(k, j, jb.lambda));
+      if (row_ok && lb <= thr) m |= 1u << (k * 4 + j);
+    }
+  }
   return m;
+}
+
+// 4x4 lower bound (sixteen block terms, >= the 8x8 bound) of candidate
+// (iy, ix): 8 paired table dwords.
+__device__ __forceinline__ uint32_t sea_lb4(const SeaCtx &c, int iy, int ix) {
+  const uint32_t *q = c.box4 + (int64_t)iy * c.stride + ix;
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    w[2 * i] = q[(int64_t)(4 * i) * c.stride];
+    w[2 * i + 1] = q[(int64_t)(4 * i) * c.stride + 8];
+  }
+  uint32_t l = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) l = __builtin_amdgcn_sad_u16(w[i], c.s4[i], l);
+  return l;
 }
 
 template <typename Px, bool SAME>
 __device__ __forceinline__ void sea_search(const FsArgs &a, const rv_fs_job &jb, int job,
                                            const rv_plane &ref, const SeaCtx &c,
-                                           const uint32_t *orgs, uint32_t *tmin, uint32_t *lmask,
-                                           uint32_t *ltile, uint32_t *lpre, uint32_t &cnt,
+                                           const uint32_t *orgs, uint32_t *list, uint32_t *cnt,
                                            uint32_t &ub_s) {
   constexpr int B = (int)sizeof(Px);
   const int tid = threadIdx.x;
   const int nx = c.nx, ny = c.ny, tasks = c.tx_n * ((ny + kTileRows - 1) / kTileRows);
   const uint8_t *rbase = (const uint8_t *)plane_ptr<Px>(ref, jb.x_lo, jb.y_lo);
   const int64_t rs = (int64_t)ref.stride * B;
-  // exact (u32 cost << 32 | raster index) of candidate (iy, ix)
-  auto exact_key = [&](int iy, int ix) __attribute__((always_inline)) -> uint64_t {
-    const uint32_t sad = sad16_global<Px>(orgs, rbase + iy * rs + ix * B, rs);
+  auto rate_l = [&](int iy, int ix) __attribute__((always_inline)) -> uint32_t {
     const int16_t row = (int16_t)(8 * (jb.y_lo + iy - jb.po_y));
     const int16_t col = (int16_t)(8 * (jb.x_lo + ix - jb.po_x));
     const uint32_t r1 = diff_to_rate((int16_t)(row - jb.pmv[0].row), a.hp) +
                         diff_to_rate((int16_t)(col - jb.pmv[0].col), a.hp);
     const uint32_t r2 = diff_to_rate((int16_t)(row - jb.pmv[1].row), a.hp) +
                         diff_to_rate((int16_t)(col - jb.pmv[1].col), a.hp);
-    const uint32_t cost = (sad << 8) + (r1 < r2 + 1 ? r1 : r2 + 1) * jb.lambda;
-    return ((uint64_t)cost << 32) | (uint32_t)(iy * nx + ix);
+    return (r1 < r2 + 1 ? r1 : r2 + 1) * jb.lambda;
+  };
+  // exact (u32 cost << 32 | raster index) of candidate (iy, ix)
+  auto exact_key = [&](int iy, int ix, uint32_t rl) __attribute__((always_inline)) -> uint64_t {
+    const uint32_t sad = sad16_global<Px>(orgs, rbase + iy * rs + ix * B, rs);
+    return ((uint64_t)((sad << 8) + rl) << 32) | (uint32_t)(iy * nx + ix);
   };
 
-  // (1) the 16x16 candidates around mv 0
+  // (1) the 16x16 candidates around mv 0, clamped into the window
   uint64_t bkey = ~0ull;
   {
-    const int ix = jb.po_x - jb.x_lo - 8 + (tid & 15), iy = jb.po_y - jb.y_lo - 8 + (tid >> 4);
+    int cx = jb.po_x - jb.x_lo, cy = jb.po_y - jb.y_lo;
+    cx = cx < 0 ? 0 : cx >= nx ? nx - 1 : cx;
+    cy = cy < 0 ? 0 : cy >= ny ? ny - 1 : cy;
+    const int ix = cx - 8 + (tid & 15), iy = cy - 8 + (tid >> 4);
     if (ix >= 0 && ix < nx && iy >= 0 && iy < ny) {
-      bkey = exact_key(iy, ix);
+      bkey = exact_key(iy, ix, rate_l(iy, ix));
       atomicMin(&ub_s, (uint32_t)(bkey >> 32));
     }
   }
-  // (2) tile minima; each lane's best tile
-  uint32_t lt_min = 0xffffffffu;
-  int lt = -1;
-  for (int t = tid; t < tasks; t += kFsThreads) {
-    const uint32_t tm = sea_tile<false, SAME>(c, jb, a.hp, t, nullptr);
-    tmin[t] = tm;
-    if (tm < lt_min) {
-      lt_min = tm;
-      lt = t;
-    }
-  }
-  if (lt >= 0 && lt_min < *(volatile uint32_t *)&ub_s) {
-    // the plain read of ub_s only filters: any achieved cost is a bound
-    uint32_t li;
-    sea_tile<true, SAME>(c, jb, a.hp, lt, &li);
-    const int iy = (int)(li / (uint32_t)nx), ix = (int)(li - (uint32_t)iy * nx);
-    const uint64_t k = exact_key(iy, ix);
-    bkey = k < bkey ? k : bkey;
-    atomicMin(&ub_s, (uint32_t)(k >> 32));
-  }
   __syncthreads();
-  const uint32_t ub = ub_s;
-  // (3) compact the surviving candidates (LB <= UB) and evaluate them
-  for (int t = tid; t < tasks; t += kFsThreads) {
-    if (tmin[t] > ub) continue;
-    const uint32_t m = sea_tile4<SAME>(c, jb, a.hp, t, ub);
-    if (m) {
-      const uint32_t slot = atomicAdd(&cnt, 1u);
-      ltile[slot] = (uint32_t)t;
-      lmask[slot] = m;
+  // (2) chunks of one tile per lane: 8x8 bounds -> list -> 4x4 bound -> exact
+  int par = 0;
+  for (int base = 0; base < tasks; base += kFsThreads, par ^= 1) {
+    const int t = base + tid;
+    if (t < tasks) {
+      uint32_t m = sea_tile<SAME>(c, jb, a.hp, t, *(volatile uint32_t *)&ub_s);
+      if (m) {
+        const int tcy = t / c.tx_n, tcx = t - tcy * c.tx_n;
+        uint32_t slot = atomicAdd(&cnt[par], (uint32_t)__builtin_popcount(m));
+        while (m) {
+          const int bit = __builtin_ctz(m);
+          m &= m - 1;
+          list[slot++] = ((uint32_t)(tcy * kTileRows + (bit >> 2)) << 16) | (uint32_t)(4 * tcx + (bit & 3));
+        }
+      }
     }
-  }
-  __syncthreads();
-  const int ns = (int)cnt;
-  // exclusive prefix of the survivors' popcounts: wave scans by shuffles,
-  // wave totals through LDS, entries strided over the workgroup
-  __shared__ uint32_t wsum[kFsThreads / 64];
-  uint32_t carry = 0;
-  for (int e0 = 0; e0 < ns; e0 += kFsThreads) {
-    const int e = e0 + tid;
-    const uint32_t v = e < ns ? __builtin_popcount(lmask[e]) : 0u;
-    uint32_t inc = v;
-    const int lane = tid & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += u;
-    }
-    if (lane == 63) wsum[tid >> 6] = inc;
+    if (tid == 0) cnt[par ^ 1] = 0;  // the next chunk's counter
     __syncthreads();
-    uint32_t base = carry, tot = 0;
-    for (int w = 0; w < kFsThreads / 64; w++) {
-      if (w < (tid >> 6)) base += wsum[w];
-      tot += wsum[w];
+    const int n = (int)cnt[par];
+    for (int e = tid; e < n; e += kFsThreads) {
+      const uint32_t v = list[e];
+      const int iy = (int)(v >> 16), ix = (int)(v & 0xffff);
+      const uint32_t rl = rate_l(iy, ix);
+      const uint32_t ub = *(volatile uint32_t *)&ub_s;  // only tightens
+      if ((sea_lb4(c, iy, ix) << 8) + rl > ub) continue;
+      const uint64_t key = exact_key(iy, ix, rl);
+      bkey = key < bkey ? key : bkey;
+      atomicMin(&ub_s, (uint32_t)(key >> 32));
     }
-    if (e < ns) lpre[e] = base + inc - v;
-    carry += tot;
-    __syncthreads();  // wsum reuse
-  }
-  if (tid == 0) lpre[ns] = carry;
-  __syncthreads();
-  const int nsurv = (int)lpre[ns];
-  for (int k = tid; k < nsurv; k += kFsThreads) {
-    int lo = 0, hi = ns - 1;  // entry e with lpre[e] <= k < lpre[e + 1]
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (lpre[mid] <= (uint32_t)k) lo = mid;
-      else hi = mid - 1;
-    }
-    uint32_t m = lmask[lo];
-    for (uint32_t r = (uint32_t)k - lpre[lo]; r; r--) m &= m - 1;  // r-th set bit
-    const int bit = __builtin_ctz(m);
-    const int t = (int)ltile[lo], tcy = t / c.tx_n, tcx = t - tcy * c.tx_n;
-    const int iy = tcy * kTileRows + (bit >> 2), ix = 4 * tcx + (bit & 3);
-    const uint64_t key = exact_key(iy, ix);
-    bkey = key < bkey ? key : bkey;
+    __syncthreads();  // list reuse
   }
   Best b{~0ull, 0xffffffffu};
   if (bkey != ~0ull) b = Best{bkey >> 32, (uint32_t)bkey};
@@ -669,10 +625,9 @@ template <typename Px>
 __device__ __forceinline__ void fs16_sea_body(const FsArgs &a) {
   constexpr int B = (int)sizeof(Px), ODW = 4 * B;
   __shared__ uint32_t orgs[16 * ODW];
-  __shared__ uint32_t so[4], so4[16], s4p[8];
-  __shared__ uint32_t tmin[kSeaMaxTiles];
-  __shared__ uint32_t lmask[kSeaMaxTiles], ltile[kSeaMaxTiles], lpre[kSeaMaxTiles + 1];
-  __shared__ uint32_t cnt, ub_s;
+  __shared__ uint32_t so4[16], s4p[8], s48p[4];
+  __shared__ uint32_t list[kSeaList];
+  __shared__ uint32_t cnt[2], ub_s;
   const int job = fs_job_index();
   if (job >= a.n) return;
   const rv_fs_job jb = a.jobs[job];
@@ -682,10 +637,9 @@ __device__ __forceinline__ void fs16_sea_body(const FsArgs &a) {
   c.nx = jb.x_hi >= jb.x_lo ? jb.x_hi - jb.x_lo + 1 : 0;
   c.ny = jb.y_hi >= jb.y_lo ? jb.y_hi - jb.y_lo + 1 : 0;
   c.tx_n = (c.nx + 3) >> 2;
-  const int tasks = c.tx_n * ((c.ny + kTileRows - 1) / kTileRows);
-  // window larger than the tile lists, or lambdas whose costs could reach
-  // the out-of-window marker: exhaustive path
-  if (tasks > kSeaMaxTiles || jb.lambda >= (1u << 23)) {
+  // lambdas whose costs could reach the out-of-window marker, or windows
+  // wider than the list's 16-bit columns: exhaustive path
+  if (jb.lambda >= (1u << 23) || c.nx > 65535) {
     const rv_fs_result res = fs_generic_body<Px>(a.org, ref, jb, 16, 16, 1, a.hp, a.out + job);
     if (threadIdx.x == 0) chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, res.best_mv);
     return;
@@ -697,7 +651,7 @@ __device__ __forceinline__ void fs16_sea_body(const FsArgs &a) {
   }
   if (tid == 0) {
     ub_s = 0xffffffffu;
-    cnt = 0;
+    cnt[0] = 0;
   }
   __syncthreads();
   if (tid < 16) {  // 4x4 block sums of the source block (row-major blocks)
@@ -708,23 +662,20 @@ __device__ __forceinline__ void fs16_sea_body(const FsArgs &a) {
     so4[tid] = t;
   }
   __syncthreads();
-  if (tid < 4) {  // 8x8 quadrants
-    const int b0 = 8 * (tid >> 1) + 2 * (tid & 1);
-    so[tid] = so4[b0] + so4[b0 + 1] + so4[b0 + 4] + so4[b0 + 5];
-  }
   if (tid < 8) s4p[tid] = so4[2 * tid] | (so4[2 * tid + 1] << 16);
+  if (tid < 4)
+    s48p[tid] = (so4[4 * tid] + so4[4 * tid + 1]) | ((so4[4 * tid + 2] + so4[4 * tid + 3]) << 16);
   __syncthreads();
-  c.so01 = so[0] | (so[1] << 16);
-  c.so23 = so[2] | (so[3] << 16);
   c.s4 = s4p;
+  c.s48 = s48p;
   c.stride = ref.stride;
   const int64_t wo = plane_origin_index(ref) + (int64_t)jb.y_lo * ref.stride + jb.x_lo;
   c.box = a.box[r_idx] + wo;
   c.box4 = a.box[r_idx] + (int64_t)ref.stride * ref.alloc_height + wo;
   if (jb.pmv[0].row == jb.pmv[1].row && jb.pmv[0].col == jb.pmv[1].col)
-    sea_search<Px, true>(a, jb, job, ref, c, orgs, tmin, lmask, ltile, lpre, cnt, ub_s);
+    sea_search<Px, true>(a, jb, job, ref, c, orgs, list, cnt, ub_s);
   else
-    sea_search<Px, false>(a, jb, job, ref, c, orgs, tmin, lmask, ltile, lpre, cnt, ub_s);
+    sea_search<Px, false>(a, jb, job, ref, c, orgs, list, cnt, ub_s);
 }
 
 // u8: capped at 128 VGPRs (4 waves per SIMD) without spilling; u16 keeps
@@ -737,22 +688,22 @@ __global__ __launch_bounds__(kFsThreads) void fs16_sea_kernel_u16(FsArgs a) {
   fs16_sea_body<uint16_t>(a);
 }
 
-// Paired box sums (rv_plane_box_sums).  blockIdx.z = 0: S8 pairs, 1: S4
-// pairs.  A thread computes 4 adjacent positions x 8 rows, for x and x + D
-// (D = 8 or 4), from dword-aligned loads (the pixels under positions
-// ax .. ax + 3 + D + K - 1 lie in 5 aligned dwords for u8, 10 for u16),
-// sliding the vertical K-row sums over 7 + K rows of horizontal K-sums; one
-// 16-byte store per row.  Stride is a multiple of 32 bytes (Plane::new).
-template <typename Px, int K>
+// Paired box sums (rv_plane_box_sums).  blockIdx.z = 0: 4-tall x 8-wide
+// pairs, 1: 4x4 pairs.  A thread computes 4 adjacent positions x 8 rows,
+// for x and x + KW, from dword-aligned loads (the pixels under positions
+// ax .. ax + 3 + 2 KW - 1 lie in 5 aligned dwords for u8, 10 for u16),
+// sliding the vertical KH-row sums over 7 + KH rows of horizontal KW-sums;
+// one 16-byte store per row.  Stride is a multiple of 32 bytes (Plane::new).
+template <typename Px, int KH, int KW>
 __device__ __forceinline__ void box_rows(const rv_plane &p, uint32_t *box, int ax, int ay0) {
   constexpr int B = (int)sizeof(Px);
   constexpr int NDW = 5 * B;
-  constexpr int NR = 7 + K;  // rows of horizontal sums
+  constexpr int NR = 7 + KH;  // rows of horizontal sums
   const uint32_t *base =
       reinterpret_cast<const uint32_t *>((const uint8_t *)p.data + ((int64_t)ay0 * p.stride + ax) * B);
   const int rdw = p.stride * B / 4;          // dwords per row
   const int ndw = (p.stride - ax) * B / 4;   // dwords left in the row
-  uint32_t h[NR][8];  // horizontal K-sums at ax + j (j < 4) and ax + K + (j - 4)
+  uint32_t h[NR][8];  // horizontal KW-sums at ax + j (j < 4) and ax + KW + (j - 4)
 #pragma unroll
   for (int k = 0; k < NR; k++) {
     uint32_t w[NDW + 1];
@@ -761,10 +712,10 @@ __device__ __forceinline__ void box_rows(const rv_plane &p, uint32_t *box, int a
       w[i] = (ay0 + k < p.alloc_height && i < ndw) ? base[(int64_t)k * rdw + i] : 0u;
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      const int x = j < 4 ? j : j - 4 + K;  // pixel offset of the position
+      const int x = j < 4 ? j : j - 4 + KW;  // pixel offset of the position
       uint32_t t = 0;
 #pragma unroll
-      for (int g = 0; g < K; g += 4) {  // 4-pixel groups
+      for (int g = 0; g < KW; g += 4) {  // 4-pixel groups
         if constexpr (B == 1) {
           const int d = (x + g) >> 2, sh = (x + g) & 3;
           t = __builtin_amdgcn_sad_u8(sh ? __builtin_amdgcn_alignbyte(w[d + 1], w[d], sh) : w[d], 0u, t);
@@ -785,26 +736,26 @@ __device__ __forceinline__ void box_rows(const rv_plane &p, uint32_t *box, int a
   for (int j = 0; j < 8; j++) {
     acc[j] = 0;
 #pragma unroll
-    for (int k = 0; k < K; k++) acc[j] += h[k][j];
+    for (int k = 0; k < KH; k++) acc[j] += h[k][j];
   }
 #pragma unroll
   for (int u = 0; u < 8; u++) {
     const int ay = ay0 + u;
     if (ay < p.alloc_height) {
       // a half whose block leaves the allocation is 0
-      const bool vy = ay + K <= p.alloc_height;
+      const bool vy = ay + KH <= p.alloc_height;
       uint32_t v[4];
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        const uint32_t lo = vy && ax + j + K <= p.stride ? acc[j] : 0u;
-        const uint32_t hi = vy && ax + j + 2 * K <= p.stride ? acc[j + 4] : 0u;
+        const uint32_t lo = vy && ax + j + KW <= p.stride ? acc[j] : 0u;
+        const uint32_t hi = vy && ax + j + 2 * KW <= p.stride ? acc[j + 4] : 0u;
         v[j] = lo | (hi << 16);
       }
       *reinterpret_cast<uint4 *>(box + (int64_t)ay * p.stride + ax) = uint4{v[0], v[1], v[2], v[3]};
     }
     if (u < 7)
 #pragma unroll
-      for (int j = 0; j < 8; j++) acc[j] += h[u + K][j] - h[u][j];
+      for (int j = 0; j < 8; j++) acc[j] += h[u + KH][j] - h[u][j];
   }
 }
 
@@ -814,9 +765,9 @@ __global__ __launch_bounds__(64) void box_sums_kernel(rv_plane p, uint32_t *box)
   const int ay0 = (int)blockIdx.y * 8;
   if (ax >= p.stride || ay0 >= p.alloc_height) return;
   if (blockIdx.z == 0)
-    box_rows<Px, 8>(p, box, ax, ay0);
+    box_rows<Px, 4, 8>(p, box, ax, ay0);
   else
-    box_rows<Px, 4>(p, box + (int64_t)p.stride * p.alloc_height, ax, ay0);
+    box_rows<Px, 4, 4>(p, box + (int64_t)p.stride * p.alloc_height, ax, ay0);
 }
 
 }  // namespace rv

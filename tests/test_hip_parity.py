@@ -396,8 +396,9 @@ def test_full_search_ties_keep_first_raster_candidate(sea):
 @pytest.mark.parametrize("hbd", [False, True])
 def test_plane_box_sums_vs_numpy(hbd):
     """rv_plane_box_sums over the whole allocation (padding included) vs an
-    integral-image box sum, paired as SK(x, y) | SK(x + K, y) << 16 for K = 8
-    then K = 4; a half whose block leaves the allocation is 0."""
+    integral-image box sum of 4-tall x KW-wide blocks, paired as
+    S(x, y) | S(x + KW, y) << 16 for KW = 8 then 4; a half whose block
+    leaves the allocation is 0."""
     rng = np.random.default_rng(950 + hbd)
     a = rand_plane(rng, 70, 90, 10 if hbd else 8)
     p = R.DevicePlane.from_array(a, xpad=12, ypad=12)
@@ -405,13 +406,14 @@ def test_plane_box_sums_vs_numpy(hbd):
     got = R.plane_box_sums(p).download(np.uint32).reshape((2,) + full.shape).astype(np.int64)
     ii = np.zeros((full.shape[0] + 1, full.shape[1] + 1), np.int64)
     ii[1:, 1:] = full.cumsum(0).cumsum(1)
-    for t, k in enumerate((8, 4)):
+    kh = 4
+    for t, kw in enumerate((8, 4)):
         sk = np.zeros(full.shape, np.int64)
-        sk[:1 - k or None, :1 - k or None] = ii[k:, k:] - ii[:-k, k:] - ii[k:, :-k] + ii[:-k, :-k]
+        sk[:1 - kh, :1 - kw] = ii[kh:, kw:] - ii[:-kh, kw:] - ii[kh:, :-kw] + ii[:-kh, :-kw]
         hi = np.zeros_like(sk)
-        hi[:, :-k] = sk[:, k:]
-        np.testing.assert_array_equal(got[t] & 0xFFFF, sk, err_msg=f"K={k} low")
-        np.testing.assert_array_equal(got[t] >> 16, hi, err_msg=f"K={k} high")
+        hi[:, :-kw] = sk[:, kw:]
+        np.testing.assert_array_equal(got[t] & 0xFFFF, sk, err_msg=f"KW={kw} low")
+        np.testing.assert_array_equal(got[t] >> 16, hi, err_msg=f"KW={kw} high")
 
 
 @pytest.mark.parametrize("hbd", [False, True])
