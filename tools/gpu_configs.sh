@@ -9,7 +9,7 @@ O="$R/gpurun_out/$TAG"
 mkdir -p "$O"
 cd "$R/gpurun_out" && ln -sfn "$TAG" last && cd "$R"
 bash "$R/tools/gpu_step.sh" \
-  "420 $TAG/pytest_gpu.log python -m pytest $R/tests -x -q -m gpu" \
+  "420 $TAG/pytest_gpu.log python -u -m pytest $R/tests -x -v -m gpu --timeout 120 --timeout-method thread" \
   "300 $TAG/bench_1080p.log python $R/bench.py" \
   "300 $TAG/bench_2160p.log python $R/bench.py --config 2160p --steps 16 --cpu-seconds 15" \
   "300 $TAG/bench_2160p10.log python $R/bench.py --config 2160p10 --steps 16 --cpu-seconds 15" \

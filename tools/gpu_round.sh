@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 P="$R/gpurun_out/prof_$TAG"
 mkdir -p "$P"
 bash "$R/tools/gpu_step.sh" \
-  "420 pytest_gpu.log python -m pytest $R/tests -x -q -m gpu" \
+  "420 pytest_gpu.log python -u -m pytest $R/tests -x -v -m gpu --timeout 120 --timeout-method thread" \
   "420 bench.log python $R/bench.py" \
   "300 prof_trace.log cd /tmp && rocprofv3 --kernel-trace --stats -d $P/trace -o run -- python3 $R/bench.py --no-cpu-baseline --steps 16 --warmup 4" \
   "300 prof_fetch.log cd /tmp && rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o run -- python3 $R/bench.py --no-cpu-baseline --steps 8 --warmup 2" \
