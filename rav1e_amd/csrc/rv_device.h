@@ -23,6 +23,14 @@ __device__ __forceinline__ int32_t wsub(int32_t a, int32_t b) {
 __device__ __forceinline__ int32_t wmul(int32_t a, int32_t b) {
   return (int32_t)((uint32_t)a * (uint32_t)b);
 }
+// Wrapping i32 product of operands that fit signed 24 bits: v_mul_i32_i24
+// returns the low 32 bits of the exact product, i.e. wmul, at full VALU rate
+// (v_mul_lo_u32 is a multi-pass op).  The transforms' data operands stay
+// below 2^21 for every i16 residual / clamped coefficient input at 8-12 bits
+// (tools/txbounds.c measures them over the oracle), the constants below 2^16.
+__device__ __forceinline__ int32_t wmul24(int32_t a, int32_t b) {
+  return __mul24(a, b);
+}
 // round_shift (src/util/mod.rs:241-243); ISimd::round_shift is identical
 // (src/util/simd.rs:98-100).  Wrapping add, arithmetic shift.
 __device__ __forceinline__ int32_t round_shift(int32_t v, int bit) {

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kBlock) void sse_kernel(
       // (i16::cast_from(a) - i16::cast_from(b)) as i32, squared as u32
       int32_t c = (int32_t)(int16_t)pa[(int64_t)j * a.stride + i] -
                   (int32_t)(int16_t)pb[(int64_t)j * b.stride + i];
-      row += (uint32_t)wmul(c, c);
+      row += (uint32_t)wmul24(c, c);
     }
     value += row;
   }
@@ -143,9 +143,9 @@ __global__ __launch_bounds__(kBlock) void cdef_moments_kernel(
       int32_t s = pa[i], d = pb[i];
       ss += s;
       sd += d;
-      ss2 += (int64_t)wmul(s, s);
-      sd2 += (int64_t)wmul(d, d);
-      ssd += (int64_t)wmul(s, d);
+      ss2 += (int64_t)wmul24(s, s);
+      sd2 += (int64_t)wmul24(d, d);
+      ssd += (int64_t)wmul24(s, d);
     }
   }
   ss = group_sum<8>(ss);

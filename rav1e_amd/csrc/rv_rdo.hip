@@ -25,6 +25,8 @@
 // kernel to the CPU replay, which chains the oracle's restatements of them.
 #include <string.h>
 
+#include <type_traits>
+
 #include "rv_rdo.h"
 #include "rv_tx.h"
 
@@ -169,19 +171,24 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
 #pragma unroll
     for (int k = 0; k < 7; k++) ring[k] = hval(k);
     ring[7] = 0;
-#pragma clang loop unroll(full)
-    for (int r = 0; r < RG; r++) {
-      ring[(r + 7) & 7] = hval(r + 7);
-      int32_t v;
-      if (rf) {
-        int32_t s = 0;
+    static_assert(RG % 8 == 0, "MC rows run in groups of 8 (static ring indices)");
+#pragma unroll 1
+    for (int r0 = 0; r0 < RG; r0 += 8) {
 #pragma unroll
-        for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(r + k) & 7]);
-        v = round_shift(s, vshift);
-      } else {
-        v = cf ? round_shift(ring[(r + 3) & 7], ib) : ring[(r + 3) & 7];
+      for (int u = 0; u < 8; u++) {
+        const int r = r0 + u;
+        ring[(u + 7) & 7] = hval(r + 7);
+        int32_t v;
+        if (rf) {
+          int32_t s = 0;
+#pragma unroll
+          for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(u + k) & 7]);
+          v = round_shift(s, vshift);
+        } else {
+          v = cf ? round_shift(ring[(u + 3) & 7], ib) : ring[(u + 3) & 7];
+        }
+        pred[(grp * RG + r) * N + col] = (Px)clampi(v, 0, maxv);
       }
-      pred[(grp * RG + r) * N + col] = (Px)clampi(v, 0, maxv);
     }
     wave_sync();  // window reads done (buf is reused), prediction visible
   }
@@ -296,8 +303,10 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     const int sub_x = a.mb_w / 8, nsub = sub_x * (a.mb_h / 8);
     for (int k = lane; k < NB * NB; k += LPB) {
       const int by = k / NB, bx = k - by * NB;
+      // 64 products of 12-bit pixels stay below 2^30: u32 sums, one
+      // v_mad_u32_u24 per product, widened to the reference's i64 at the end
       int32_t ss = 0, sd = 0;
-      int64_t ss2 = 0, sd2 = 0, ssd = 0;
+      uint32_t ss2 = 0, sd2 = 0, ssd = 0;
 #pragma unroll
       for (int j = 0; j < 8; j++)
 #pragma unroll
@@ -306,18 +315,18 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
           const int32_t d = pred[(by * 8 + j) * N + bx * 8 + i];
           ss += s;
           sd += d;
-          ss2 += (int64_t)wmul(s, s);
-          sd2 += (int64_t)wmul(d, d);
-          ssd += (int64_t)wmul(s, d);
+          ss2 += (uint32_t)wmul24(s, s);
+          sd2 += (uint32_t)wmul24(d, d);
+          ssd += (uint32_t)wmul24(s, d);
         }
       const int kk = ((oy >> 3) + by) * sub_x + (ox >> 3) + bx;
       int64_t *m = (int64_t *)pl.dist + ((int64_t)cand * nsub + kk) * 5;
       if (!valid) continue;
       m[0] = ss;
       m[1] = sd;
-      m[2] = ss2;
-      m[3] = sd2;
-      m[4] = ssd;
+      m[2] = (int64_t)ss2;
+      m[3] = (int64_t)sd2;
+      m[4] = (int64_t)ssd;
     }
   } else {
     const int bw = a.sub_w, bh = a.sub_h;
@@ -331,13 +340,262 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
         for (int i = 0; i < bw; i++) {
           const int32_t c = (int32_t)(int16_t)o[(int64_t)(by * bh + j) * pl.org.stride + bx * bw + i] -
                             (int32_t)(int16_t)pred[(by * bh + j) * N + bx * bw + i];
-          row += (uint32_t)wmul(c, c);
+          row += (uint32_t)wmul24(c, c);
         }
         value += row;
       }
       const int kk = (oy / bh + by) * sub_x + ox / bw + bx;
       if (valid) ((uint64_t *)pl.dist)[(int64_t)cand * nsub + kk] = value;
     }
+  }
+}
+
+// ---- luma candidates: 64x64, one wavefront, ~8 KiB of LDS -------------------
+// The same chain as rdo_cand_body<Px, 64, true, 64> with the 64x64 i32 slab
+// gone, so four wavefronts fit a SIMD instead of two:
+//  * put_8tap in two halves of 32 output rows (39 staged window rows each);
+//  * the residual is formed per column straight from the source plane and
+//    the LDS prediction, and only column-DCT outputs 0..15 are kept: the
+//    stand-in reads raster rows 0..15 of the 64x64 fht output
+//    (src/encoder.rs:1152-1156), and row r of that raster is the row DCT of
+//    column-pass row r, so the compiler drops the other 48 outputs;
+//  * the inverse row pass stores round_shift(., INTERMEDIATE_SHIFT) clamped
+//    to the column range (inverse.rs:2075-2098) -- 16 bits for u8, so i16.
+struct LumaLds {
+  template <typename Px>
+  static constexpr int kWinP = sizeof(Px) == 1 ? 80 : 144;  // window row pitch, bytes
+  template <typename Px>
+  using Mid = typename std::conditional<sizeof(Px) == 1, int16_t, int32_t>::type;
+  template <typename Px>
+  static constexpr int kScr() {  // bytes of the phase-shared scratch
+    constexpr int win = 39 * kWinP<Px>, fwd = 16 * 65 * 4, inv = 32 * 66 * (int)sizeof(Mid<Px>);
+    return win > fwd ? (win > inv ? win : inv) : (fwd > inv ? fwd : inv);
+  }
+  template <typename Px>
+  static constexpr int kBytes = kScr<Px>() + 64 * 64 * (int)sizeof(Px);
+};
+
+template <typename Px>
+__device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &pl, int t,
+                                              uint8_t *scr, Px *pred) {
+  constexpr int N = 64, B = (int)sizeof(Px);
+  constexpr int P = LumaLds::kWinP<Px>;
+  using Mid = LumaLds::Mid<Px>;
+  const int lane = threadIdx.x & 63;
+  const int cand = t / a.ntx_per_cand;
+  const rv_mc_job mj = pl.mc[cand];
+  const rv_tx_job tj = pl.tx[t];
+  const rv_plane &ref = pl.ref[cand / a.cands_per_ref];
+  const int ox = tj.pred_x - mj.dst_x, oy = tj.pred_y - mj.dst_y;
+  const int bd = a.bd, ib = bd == 12 ? 2 : 4, maxv = (1 << bd) - 1;
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+
+  // ---- A. put_8tap (src/mc.rs:213-307) into pred, two halves --------------
+  {
+    uint32_t *win = reinterpret_cast<uint32_t *>(scr);
+    const int cf = mj.col_frac, rf = mj.row_frac;
+    const int8_t *xf = kRdoReg[a.mb_w <= 4][cf];
+    const int8_t *yf = kRdoReg[a.mb_h <= 4][rf];
+    int yt[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) yt[k] = yf[k];
+    uint32_t xp[4];
+    int xsum = 0;
+    if constexpr (B == 1) {
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+        xp[h] = (uint32_t)(uint8_t)xf[4 * h] | ((uint32_t)(uint8_t)xf[4 * h + 1] << 8) |
+                ((uint32_t)(uint8_t)xf[4 * h + 2] << 16) | ((uint32_t)(uint8_t)xf[4 * h + 3] << 24);
+#pragma unroll
+      for (int k = 0; k < 8; k++) xsum += xf[k];
+      xp[2] = xp[3] = 0;
+    } else {
+#pragma unroll
+      for (int h = 0; h < 4; h++)
+        xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h] |
+                ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] << 16);
+    }
+    const int col = lane;
+    auto hval = [&](int tr) __attribute__((always_inline)) -> int32_t {
+      const uint32_t *row = win + tr * (P / 4);
+      if constexpr (B == 1) {
+        const int d0 = col >> 2, sh = col & 3;
+        const uint32_t w0 = row[d0], w1 = row[d0 + 1], w2 = row[d0 + 2];
+        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        if (!cf) return (int32_t)(lo >> 24);
+        int32_t s = __builtin_amdgcn_sdot4((int)(lo ^ 0x80808080u), (int)xp[0], 128 * xsum, false);
+        s = __builtin_amdgcn_sdot4((int)(hi ^ 0x80808080u), (int)xp[1], s, false);
+        return (int32_t)(int16_t)round_shift(s, 7 - ib);
+      } else {
+        typedef short s2 __attribute__((ext_vector_type(2)));
+        const int d0 = col >> 1, sh = (col & 1) * 2;
+        uint32_t w[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) w[k] = row[d0 + k];
+        uint32_t pp[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) pp[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+        if (!cf) return (int32_t)(pp[1] >> 16);
+        int32_t s = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          s = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, pp[k]), __builtin_bit_cast(s2, xp[k]), s,
+                                     false);
+        return (int32_t)(int16_t)round_shift(s, 7 - ib);
+      }
+    };
+    const int vshift = cf ? 7 + ib : 7;
+    constexpr int kRowDw = ((N + 7) * B + 3) / 4;
+    constexpr int kTot = 39 * kRowDw;
+    const int64_t rs = (int64_t)ref.stride * B;
+#pragma unroll 1
+    for (int half = 0; half < 2; half++) {
+      const uint8_t *sp =
+          (const uint8_t *)plane_ptr<Px>(ref, mj.src_x + ox - 3, mj.src_y + oy - 3 + 32 * half);
+      if (half) wave_sync();  // the first half's window reads are done
+#pragma unroll 4
+      for (int i = lane; i < kTot; i += 64) {
+        const int r = i / kRowDw, d = i - r * kRowDw;
+        uint32_t v;
+        __builtin_memcpy(&v, sp + r * rs + 4 * d, 4);
+        win[r * (P / 4) + d] = v;
+      }
+      wave_sync();
+      int32_t ring[8];
+#pragma unroll
+      for (int k = 0; k < 7; k++) ring[k] = hval(k);
+      ring[7] = 0;
+#pragma unroll 1
+      for (int r0 = 0; r0 < 32; r0 += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int r = r0 + u;
+          ring[(u + 7) & 7] = hval(r + 7);
+          int32_t v;
+          if (rf) {
+            int32_t s = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(u + k) & 7]);
+            v = round_shift(s, vshift);
+          } else {
+            v = cf ? round_shift(ring[(u + 3) & 7], ib) : ring[(u + 3) & 7];
+          }
+          pred[(32 * half + r) * N + col] = (Px)clampi(v, 0, maxv);
+        }
+      }
+    }
+    wave_sync();  // window reads done (scr is reused), prediction visible
+  }
+
+  int s0, s1, s2;
+  fwd_shifts<N>((bd - 8) / 2, s0, s1, s2);
+  const Px *o = plane_ptr<Px>(pl.org, tj.src_x, tj.src_y);
+  int32_t *fmid = reinterpret_cast<int32_t *>(scr);  // [16][65]: column-DCT rows 0..15
+  // ---- B + C. residual (src/encoder.rs:1044-1058) and the column DCT -------
+  {
+    int32_t v[N];
+#pragma unroll
+    for (int r = 0; r < N; r++) {
+      const int16_t d = (int16_t)((int16_t)o[(int64_t)r * pl.org.stride + lane] -
+                                  (int16_t)pred[r * N + lane]);
+      v[r] = rdo_rsa((int32_t)d, -s0);
+    }
+    tx::fwd1d<1, N>(v, v);
+#pragma unroll
+    for (int r = 0; r < 16; r++) fmid[r * 65 + lane] = rdo_rsa(v[r], -s1);
+  }
+  wave_sync();
+  // ---- C'. row DCT of raster rows 0..15 + the quantize stand-in ------------
+  if (lane < 16) {
+    int32_t v[N];
+#pragma unroll
+    for (int c = 0; c < N; c++) v[c] = fmid[lane * 65 + c];
+    tx::fwd1d<1, N>(v, v);
+#pragma unroll
+    for (int c = 0; c < N; c++) fmid[lane * 65 + c] = (rdo_rsa(v[c], -s2) / kQstep) * kQstep;
+  }
+  wave_sync();
+  // packed coefficients = raster entries 0..1023 (row stride 32), coalesced
+  {
+    int32_t *pk = pl.packed + (int64_t)t * 1024;
+#pragma unroll 4
+    for (int i = lane; i < 1024; i += 64) pk[i] = fmid[(i >> 6) * 65 + (i & 63)];
+  }
+  // ---- D. inverse rows: input row rr = packed[rr * 32 ..] ------------------
+  const int range = bd + 8;
+  const int crange = bd + 6 > 16 ? bd + 6 : 16;
+  Mid *imid = reinterpret_cast<Mid *>(scr);  // [32][66]
+  {
+    int32_t v[N];
+    if (lane < 32) {
+#pragma unroll
+      for (int c = 0; c < N; c++)
+        v[c] = c < 32 ? tx::clampv(fmid[(lane >> 1) * 65 + (lane & 1) * 32 + c], range) : 0;
+    }
+    wave_sync();  // every read of fmid precedes the imid writes (same bytes)
+    if (lane < 32) {
+      tx::inv1d<1, N>(v, range);
+#pragma unroll
+      for (int c = 0; c < N; c++) imid[lane * 66 + c] = (Mid)tx::clampv(round_shift(v[c], 2), crange);
+    }
+  }
+  wave_sync();
+  // ---- D'. inverse columns + add into pred ---------------------------------
+  {
+    int32_t v[N];
+#pragma unroll
+    for (int r = 0; r < N; r++) v[r] = r < 32 ? (int32_t)imid[r * 66 + lane] : 0;
+    tx::inv1d<1, N>(v, crange);
+#pragma unroll
+    for (int r = 0; r < N; r++) {
+      Px *q = pred + r * N + lane;
+      *q = (Px)clampi(wadd((int32_t)*q, round_shift(v[r], 4)), 0, maxv);
+    }
+  }
+  wave_sync();
+  // reconstruction -> the tall plane, coalesced dwords
+  {
+    constexpr int PPD = 4 / B, DPR = N / PPD;
+    uint8_t *dp = (uint8_t *)plane_ptr_mut<Px>(pl.dst, tj.pred_x, tj.pred_y);
+    const int64_t ds = (int64_t)pl.dst.stride * B;
+#pragma unroll 8
+    for (int i = lane; i < N * DPR; i += 64) {
+      const int r = i / DPR, c = (i - r * DPR) * PPD;
+      uint32_t v;
+      __builtin_memcpy(&v, pred + r * N + c, 4);
+      __builtin_memcpy(dp + r * ds + c * B, &v, 4);
+    }
+  }
+  // ---- E. cdef_dist_wxh_8x8 moments (src/rdo.rs:219-241), one 8x8 per lane
+  {
+    const int by = lane >> 3, bx = lane & 7;
+    const int sub_x = a.mb_w / 8, nsub = sub_x * (a.mb_h / 8);
+    int32_t ss = 0, sd = 0;
+    uint32_t ss2 = 0, sd2 = 0, ssd = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const int32_t s = o[(int64_t)(by * 8 + j) * pl.org.stride + bx * 8 + i];
+        const int32_t d = pred[(by * 8 + j) * N + bx * 8 + i];
+        ss += s;
+        sd += d;
+        ss2 += (uint32_t)wmul24(s, s);
+        sd2 += (uint32_t)wmul24(d, d);
+        ssd += (uint32_t)wmul24(s, d);
+      }
+    const int kk = ((oy >> 3) + by) * sub_x + (ox >> 3) + bx;
+    int64_t *m = (int64_t *)pl.dist + ((int64_t)cand * nsub + kk) * 5;
+    m[0] = ss;
+    m[1] = sd;
+    m[2] = (int64_t)ss2;
+    m[3] = (int64_t)sd2;
+    m[4] = (int64_t)ssd;
   }
 }
 
@@ -370,15 +628,21 @@ __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, in
                                    buf + half * 32 * 33, pred + half * 32 * 32);
 }
 
+// LDS: the larger of the luma layout and the chroma pair (2 x (32 x 33 i32 +
+// 32 x 32 Px)), ~10 KiB for u8.
 template <typename Px>
-__global__ __launch_bounds__(64) void rdo_frame_kernel(RdoArgs luma, RdoArgs chroma) {
-  __shared__ int32_t buf[64 * 65];
-  __shared__ Px pred[64 * 64];
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void rdo_frame_kernel(
+    RdoArgs luma, RdoArgs chroma) {
+  constexpr int kChroma = 2 * 32 * 33 * 4 + 2 * 32 * 32 * (int)sizeof(Px);
+  constexpr int kLuma = LumaLds::kBytes<Px>;
+  __shared__ __align__(16) uint8_t lds[kLuma > kChroma ? kLuma : kChroma];
   const int b = blockIdx.x;
   if (b < luma.n_tx)
-    rdo_cand_body<Px, 64, true, 64>(luma, luma.p[0], rdo_task(luma, b), true, buf, pred);
+    rdo_luma_body<Px>(luma, luma.p[0], rdo_task(luma, b), lds,
+                      reinterpret_cast<Px *>(lds + LumaLds::kScr<Px>()));
   else
-    rdo_chroma_pair<Px>(chroma, b - luma.n_tx, buf, pred);
+    rdo_chroma_pair<Px>(chroma, b - luma.n_tx, reinterpret_cast<int32_t *>(lds),
+                        reinterpret_cast<Px *>(lds + 2 * 32 * 33 * 4));
 }
 
 // Chroma pairs alone (10.5 KiB of LDS instead of the luma slab's 20.7 KiB,

@@ -29,7 +29,7 @@ struct TT {
 #define RV_DI __device__ __forceinline__
 
 // ---- TxOperations for i32 (forward.rs:114-130) ----------------------------
-RV_DI T txmul(T x, int m, int s) { return wadd(wmul(x, m), (1 << s) >> 1) >> s; }
+RV_DI T txmul(T x, int m, int s) { return wadd(wmul24(x, m), (1 << s) >> 1) >> s; }
 RV_DI T rsh1(T x) { return wadd(x, x < 0 ? 1 : 0) >> 1; }
 RV_DI T add_avg(T a, T b) { return wadd(a, b) >> 1; }
 RV_DI T sub_avg(T a, T b) { return wsub(a, b) >> 1; }
@@ -585,13 +585,14 @@ __host__ __device__ constexpr int32_t sin128(int angle) {
   return cos128(angle - 64);
 }
 
+// clamp_value (src/transform/mod.rs:490) for bit <= 31: one v_med3_i32
 RV_DI T clampv(T v, int bit) {
-  const int64_t hi = ((int64_t)1 << (bit - 1)) - 1, lo = -((int64_t)1 << (bit - 1));
-  return v < lo ? (T)lo : (v > hi ? (T)hi : v);
+  const T hi = (T)((1u << (bit - 1)) - 1u), lo = -hi - 1;
+  return __builtin_elementwise_min(__builtin_elementwise_max(v, lo), hi);
 }
 // half_btf (src/transform/mod.rs:476-488)
 RV_DI T half_btf(T w0, T in0, T w1, T in1) {
-  return wadd(wadd(wmul(w0, in0), wmul(w1, in1)), 1 << 11) >> 12;
+  return wadd(wadd(wmul24(w0, in0), wmul24(w1, in1)), 1 << 11) >> 12;
 }
 // B(a, b, angle, flip) and H(a, b, flip) of the spec's butterfly program.
 RV_DI void Bf(T *t, int a, int b, int angle, int flip) {
@@ -765,15 +766,15 @@ RV_DI void idct(T *t, int r) {
 // av1_iadst4 (inverse.rs:63-109): SINPI_INV (inverse.rs:31), no clamps
 RV_DI void iadst4(T *t) {
   const T x0 = t[0], x1 = t[1], x2 = t[2], x3 = t[3];
-  T s0 = wmul(1321, x0), s1 = wmul(2482, x0);
-  T s2 = wmul(3344, x1), s3 = wmul(3803, x2);
-  T s4 = wmul(1321, x2), s5 = wmul(2482, x3);
-  T s6 = wmul(3803, x3);
+  T s0 = wmul24(1321, x0), s1 = wmul24(2482, x0);
+  T s2 = wmul24(3344, x1), s3 = wmul24(3803, x2);
+  T s4 = wmul24(1321, x2), s5 = wmul24(2482, x3);
+  T s6 = wmul24(3803, x3);
   T s7 = wadd(wsub(x0, x2), x3);
   s0 = wadd(s0, s3);
   s1 = wsub(s1, s4);
   s3 = s2;
-  s2 = wmul(3344, s7);
+  s2 = wmul24(3344, s7);
   s0 = wadd(s0, s5);
   s1 = wsub(s1, s6);
   const T y0 = wadd(s0, s3), y1 = wadd(s1, s3), y2 = s2;
@@ -863,9 +864,9 @@ RV_DI void inv1d(T *t, int range) {
   if constexpr (KIND == 0) {  // av1_iidentity4/8/16/32 (inverse.rs:111-854)
 #pragma unroll
     for (int i = 0; i < N; i++) {
-      if constexpr (N == 4) t[i] = round_shift(wmul(5793, t[i]), 12);
+      if constexpr (N == 4) t[i] = round_shift(wmul24(5793, t[i]), 12);
       else if constexpr (N == 8) t[i] = wmul(2, t[i]);
-      else if constexpr (N == 16) t[i] = round_shift(wmul(5793 * 2, t[i]), 12);
+      else if constexpr (N == 16) t[i] = round_shift(wmul24(5793 * 2, t[i]), 12);
       else t[i] = wmul(4, t[i]);
     }
   } else if constexpr (KIND == 1) {
