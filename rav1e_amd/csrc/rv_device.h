@@ -31,6 +31,24 @@ __device__ __forceinline__ int32_t wmul(int32_t a, int32_t b) {
 __device__ __forceinline__ int32_t wmul24(int32_t a, int32_t b) {
   return __mul24(a, b);
 }
+// Signed integer dot products (v_dot4_i32_i8 / v_dot2_i32_i16).  These stay
+// compiler builtins: gfx950 requires wait states between a dot that writes a
+// VGPR and another VALU reading it, which the compiler inserts for the
+// builtins but cannot see inside inline asm (measured: wrong sub-pel SADs).
+__device__ __forceinline__ int32_t dot4_i8(uint32_t a, uint32_t b, int32_t c) {
+  return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
+}
+__device__ __forceinline__ int32_t dot2_i16(uint32_t a, uint32_t b, int32_t c) {
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, a), __builtin_bit_cast(s2, b), c, false);
+}
+// clamp of a signed value into [lo, hi], lo <= hi: one v_med3_i32 (the
+// compiler only forms it when both bounds are constants)
+__device__ __forceinline__ int32_t clamp_med3(int32_t v, int32_t lo, int32_t hi) {
+  int32_t d;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(d) : "v"(v), "v"(lo), "v"(hi));
+  return d;
+}
 // round_shift (src/util/mod.rs:241-243); ISimd::round_shift is identical
 // (src/util/simd.rs:98-100).  Wrapping add, arithmetic shift.
 __device__ __forceinline__ int32_t round_shift(int32_t v, int bit) {

@@ -173,8 +173,7 @@ __device__ __forceinline__ uint32_t sub_sad_rows(const uint32_t *win, const Px *
                                                  int ib, int maxv) {
   constexpr int B = (int)sizeof(Px);
   constexpr int PD = UP / 4;  // window pitch in dwords
-  typedef short s2 __attribute__((ext_vector_type(2)));
-  uint32_t xp[4] = {0, 0, 0, 0};  // u8: 2 x i8x4; u16: 4 x i16x2
+  uint32_t xp[4] = {0, 0, 0, 0};  // u8: 2 x i8x4; u16: 3 x i16x2
   int xsum = 0;
   if constexpr (HF) {
     if constexpr (B == 1) {
@@ -186,17 +185,21 @@ __device__ __forceinline__ uint32_t sub_sad_rows(const uint32_t *win, const Px *
       for (int k = 0; k < 8; k++) xsum += xf[k];
     } else {
 #pragma unroll
-      for (int h = 0; h < 4; h++)
-        xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h] |
-                ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] << 16);
+      for (int h = 0; h < 3; h++)  // taps 1..6 as pairs (taps 0 and 7 are zero)
+        xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] |
+                ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 2] << 16);
     }
   }
-  uint32_t tp[4] = {0, 0, 0, 0};  // vertical taps as i16 pairs
+  // REGULAR taps 0 and 7 are zero for every fraction (src/mc.rs:71-88; the
+  // 4-tap set also zeroes 1 and 6), so the vertical pass is three v_dot2
+  // over the pairs (1,2), (3,4), (5,6) and window rows 0 and h+6 are never
+  // filtered.
+  uint32_t tp[3] = {0, 0, 0};  // vertical taps 1..6 as i16 pairs
   if constexpr (VF) {
 #pragma unroll
-    for (int h = 0; h < 4; h++)
-      tp[h] = (uint32_t)(uint16_t)(int16_t)yf[2 * h] |
-              ((uint32_t)(uint16_t)(int16_t)yf[2 * h + 1] << 16);
+    for (int h = 0; h < 3; h++)
+      tp[h] = (uint32_t)(uint16_t)(int16_t)yf[2 * h + 1] |
+              ((uint32_t)(uint16_t)(int16_t)yf[2 * h + 2] << 16);
   }
   const int hbias = 128 * xsum;
   const int hround = (1 << (7 - ib)) >> 1, hsh = 7 - ib;
@@ -211,26 +214,21 @@ __device__ __forceinline__ uint32_t sub_sad_rows(const uint32_t *win, const Px *
       } else {
         const int d0 = cx >> 2, sh = cx & 3;
         const uint32_t w0 = row[d0], w1 = row[d0 + 1], w2 = row[d0 + 2];
-        int32_t s = __builtin_amdgcn_sdot4((int)__builtin_amdgcn_alignbyte(w1, w0, sh), (int)xp[0],
-                                           hbias + hround, false);
-        s = __builtin_amdgcn_sdot4((int)__builtin_amdgcn_alignbyte(w2, w1, sh), (int)xp[1], s,
-                                   false);
+        int32_t s = dot4_i8(__builtin_amdgcn_alignbyte(w1, w0, sh), xp[0], hbias + hround);
+        s = dot4_i8(__builtin_amdgcn_alignbyte(w2, w1, sh), xp[1], s);
         return s >> hsh;
       }
     } else {
       if constexpr (!HF) {
         return (int32_t)reinterpret_cast<const uint16_t *>(row)[cx + 3];
       } else {
-        const int d0 = cx >> 1, sh = (cx & 1) * 2;
-        uint32_t w[5];
+        const int c1 = cx + 1, d0 = c1 >> 1, sh = (c1 & 1) * 2;  // pixels cx+1 .. cx+6
+        uint32_t w[4];
 #pragma unroll
-        for (int k = 0; k < 5; k++) w[k] = row[d0 + k];
+        for (int k = 0; k < 4; k++) w[k] = row[d0 + k];
         int32_t s = hround;
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-          s = __builtin_amdgcn_sdot2(
-              __builtin_bit_cast(s2, __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh)),
-              __builtin_bit_cast(s2, xp[k]), s, false);
+        for (int k = 0; k < 3; k++) s = dot2_i16(__builtin_amdgcn_alignbyte(w[k + 1], w[k], sh), xp[k], s);
         return s >> hsh;
       }
     }
@@ -244,7 +242,7 @@ __device__ __forceinline__ uint32_t sub_sad_rows(const uint32_t *win, const Px *
 #pragma unroll 8
     for (int r = 0; r < RG; r++) {
       int32_t v = hval(r + 3);
-      if constexpr (HF) v = clampi(round_shift(v, ib), 0, maxv);
+      if constexpr (HF) v = clamp_med3(round_shift(v, ib), 0, maxv);
       acc = absdiff_acc((uint32_t)ocol[r * W], (uint32_t)v, acc);
     }
   } else {
@@ -254,28 +252,26 @@ __device__ __forceinline__ uint32_t sub_sad_rows(const uint32_t *win, const Px *
       return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
     };
     uint32_t pr[8];  // pr[j & 7] = (m[j], m[j + 1])
-    int32_t prev = hval(0);
+    int32_t prev = hval(1);
 #pragma unroll
-    for (int t = 1; t < 7; t++) {
+    for (int t = 2; t < 6; t++) {
       const int32_t m = hval(t);
       pr[t - 1] = pack(prev, m);
       prev = m;
     }
-    pr[6] = pr[7] = 0;
+    pr[0] = pr[5] = pr[6] = pr[7] = 0;
 #pragma unroll 1
     for (int r0 = 0; r0 < RG; r0 += 8) {
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int r = r0 + u;
-        const int32_t m = hval(r + 7);
-        pr[(u + 6) & 7] = pack(prev, m);
+        const int32_t m = hval(r + 6);
+        pr[(u + 5) & 7] = pack(prev, m);
         prev = m;
         int32_t s = vround;
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-          s = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, pr[(u + 2 * k) & 7]),
-                                     __builtin_bit_cast(s2, tp[k]), s, false);
-        const int v = clampi(s >> vshift, 0, maxv);
+        for (int k = 0; k < 3; k++) s = dot2_i16(pr[(u + 2 * k + 1) & 7], tp[k], s);
+        const int v = clamp_med3(s >> vshift, 0, maxv);
         acc = absdiff_acc((uint32_t)ocol[r * W], (uint32_t)v, acc);
       }
     }

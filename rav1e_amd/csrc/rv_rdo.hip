@@ -111,7 +111,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
       const int r = i / kRowDw, d = i - r * kRowDw;
       uint32_t v;
       __builtin_memcpy(&v, sp + r * rs + 4 * d, 4);
-      win[r * (P / 4) + d] = v;
+      win[r * (P / 4) + d] = B == 1 ? v ^ 0x80808080u : v;  // u8: stored as i8 = px - 128
     }
     wave_sync();
     const int cf = mj.col_frac, rf = mj.row_frac;
@@ -132,9 +132,10 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
       xp[2] = xp[3] = 0;
     } else {
 #pragma unroll
-      for (int h = 0; h < 4; h++)
-        xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h] |
-                ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] << 16);
+      for (int h = 0; h < 3; h++)  // taps 1..6 (REGULAR taps 0 and 7 are zero)
+        xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] |
+                ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 2] << 16);
+      xp[3] = 0;
     }
     const int col = lane % N, grp = lane / N;
     auto hval = [&](int tr) -> int32_t {
@@ -144,50 +145,48 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
         const uint32_t w0 = row[d0], w1 = row[d0 + 1], w2 = row[d0 + 2];
         const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
         const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-        if (!cf) return (int32_t)(lo >> 24);
-        int32_t s = __builtin_amdgcn_sdot4((int)(lo ^ 0x80808080u), (int)xp[0], 128 * xsum, false);
-        s = __builtin_amdgcn_sdot4((int)(hi ^ 0x80808080u), (int)xp[1], s, false);
+        if (!cf) return (int32_t)((lo >> 24) ^ 0x80u);
+        int32_t s = dot4_i8(lo, xp[0], 128 * xsum);
+        s = dot4_i8(hi, xp[1], s);
         return (int32_t)(int16_t)round_shift(s, 7 - ib);
       } else {
-        typedef short s2 __attribute__((ext_vector_type(2)));
-        const int d0 = col >> 1, sh = (col & 1) * 2;
-        uint32_t w[5];
+        const int c1 = col + 1, d0 = c1 >> 1, sh = (c1 & 1) * 2;  // pixels col+1 .. col+6
+        uint32_t w[4];
 #pragma unroll
-        for (int k = 0; k < 5; k++) w[k] = row[d0 + k];
-        uint32_t pp[4];
+        for (int k = 0; k < 4; k++) w[k] = row[d0 + k];
+        uint32_t pp[3];
 #pragma unroll
-        for (int k = 0; k < 4; k++) pp[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-        if (!cf) return (int32_t)(pp[1] >> 16);
+        for (int k = 0; k < 3; k++) pp[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+        if (!cf) return (int32_t)(pp[1] & 0xffffu);  // pixel col + 3
         int32_t s = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-          s = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, pp[k]), __builtin_bit_cast(s2, xp[k]), s,
-                                     false);
+        for (int k = 0; k < 3; k++)
+          s = dot2_i16(pp[k], xp[k], s);
         return (int32_t)(int16_t)round_shift(s, 7 - ib);
       }
     };
     const int vshift = cf ? 7 + ib : 7;
-    int32_t ring[8];
+    int32_t ring[8];  // ring[j & 7] = intermediate of window row j
 #pragma unroll
-    for (int k = 0; k < 7; k++) ring[k] = hval(k);
-    ring[7] = 0;
+    for (int k = 1; k < 6; k++) ring[k] = hval(k);
+    ring[0] = ring[6] = ring[7] = 0;
     static_assert(RG % 8 == 0, "MC rows run in groups of 8 (static ring indices)");
 #pragma unroll 1
     for (int r0 = 0; r0 < RG; r0 += 8) {
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         const int r = r0 + u;
-        ring[(u + 7) & 7] = hval(r + 7);
+        ring[(u + 6) & 7] = hval(r + 6);
         int32_t v;
-        if (rf) {
+        if (rf) {  // taps 1..6: REGULAR taps 0 and 7 are zero (src/mc.rs:71-88)
           int32_t s = 0;
 #pragma unroll
-          for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(u + k) & 7]);
+          for (int k = 1; k < 7; k++) s += __mul24(yt[k], ring[(u + k) & 7]);
           v = round_shift(s, vshift);
         } else {
           v = cf ? round_shift(ring[(u + 3) & 7], ib) : ring[(u + 3) & 7];
         }
-        pred[(grp * RG + r) * N + col] = (Px)clampi(v, 0, maxv);
+        pred[(grp * RG + r) * N + col] = (Px)clamp_med3(v, 0, maxv);
       }
     }
     wave_sync();  // window reads done (buf is reused), prediction visible
@@ -279,7 +278,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
 #pragma unroll
     for (int r = 0; r < N; r++) {
       Px *q = pred + r * N + lane;
-      *q = (Px)clampi(wadd((int32_t)*q, round_shift(v[r], 4)), 0, maxv);
+      *q = (Px)clamp_med3(wadd((int32_t)*q, round_shift(v[r], 4)), 0, maxv);
     }
   }
   wave_sync();
@@ -415,9 +414,10 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
       xp[2] = xp[3] = 0;
     } else {
 #pragma unroll
-      for (int h = 0; h < 4; h++)
-        xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h] |
-                ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] << 16);
+      for (int h = 0; h < 3; h++)  // taps 1..6 (REGULAR taps 0 and 7 are zero)
+        xp[h] = (uint32_t)(uint16_t)(int16_t)xf[2 * h + 1] |
+                ((uint32_t)(uint16_t)(int16_t)xf[2 * h + 2] << 16);
+      xp[3] = 0;
     }
     const int col = lane;
     auto hval = [&](int tr) __attribute__((always_inline)) -> int32_t {
@@ -427,25 +427,23 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
         const uint32_t w0 = row[d0], w1 = row[d0 + 1], w2 = row[d0 + 2];
         const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
         const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-        if (!cf) return (int32_t)(lo >> 24);
-        int32_t s = __builtin_amdgcn_sdot4((int)(lo ^ 0x80808080u), (int)xp[0], 128 * xsum, false);
-        s = __builtin_amdgcn_sdot4((int)(hi ^ 0x80808080u), (int)xp[1], s, false);
+        if (!cf) return (int32_t)((lo >> 24) ^ 0x80u);
+        int32_t s = dot4_i8(lo, xp[0], 128 * xsum);
+        s = dot4_i8(hi, xp[1], s);
         return (int32_t)(int16_t)round_shift(s, 7 - ib);
       } else {
-        typedef short s2 __attribute__((ext_vector_type(2)));
-        const int d0 = col >> 1, sh = (col & 1) * 2;
-        uint32_t w[5];
+        const int c1 = col + 1, d0 = c1 >> 1, sh = (c1 & 1) * 2;  // pixels col+1 .. col+6
+        uint32_t w[4];
 #pragma unroll
-        for (int k = 0; k < 5; k++) w[k] = row[d0 + k];
-        uint32_t pp[4];
+        for (int k = 0; k < 4; k++) w[k] = row[d0 + k];
+        uint32_t pp[3];
 #pragma unroll
-        for (int k = 0; k < 4; k++) pp[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-        if (!cf) return (int32_t)(pp[1] >> 16);
+        for (int k = 0; k < 3; k++) pp[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+        if (!cf) return (int32_t)(pp[1] & 0xffffu);  // pixel col + 3
         int32_t s = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-          s = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, pp[k]), __builtin_bit_cast(s2, xp[k]), s,
-                                     false);
+        for (int k = 0; k < 3; k++)
+          s = dot2_i16(pp[k], xp[k], s);
         return (int32_t)(int16_t)round_shift(s, 7 - ib);
       }
     };
@@ -463,29 +461,29 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
         const int r = i / kRowDw, d = i - r * kRowDw;
         uint32_t v;
         __builtin_memcpy(&v, sp + r * rs + 4 * d, 4);
-        win[r * (P / 4) + d] = v;
+        win[r * (P / 4) + d] = B == 1 ? v ^ 0x80808080u : v;  // u8: stored as i8 = px - 128
       }
       wave_sync();
-      int32_t ring[8];
+      int32_t ring[8];  // ring[j & 7] = intermediate of window row j
 #pragma unroll
-      for (int k = 0; k < 7; k++) ring[k] = hval(k);
-      ring[7] = 0;
+      for (int k = 1; k < 6; k++) ring[k] = hval(k);
+      ring[0] = ring[6] = ring[7] = 0;
 #pragma unroll 1
       for (int r0 = 0; r0 < 32; r0 += 8) {
 #pragma unroll
         for (int u = 0; u < 8; u++) {
           const int r = r0 + u;
-          ring[(u + 7) & 7] = hval(r + 7);
+          ring[(u + 6) & 7] = hval(r + 6);
           int32_t v;
-          if (rf) {
+          if (rf) {  // taps 1..6 (REGULAR taps 0 and 7 are zero)
             int32_t s = 0;
 #pragma unroll
-            for (int k = 0; k < 8; k++) s += __mul24(yt[k], ring[(u + k) & 7]);
+            for (int k = 1; k < 7; k++) s += __mul24(yt[k], ring[(u + k) & 7]);
             v = round_shift(s, vshift);
           } else {
             v = cf ? round_shift(ring[(u + 3) & 7], ib) : ring[(u + 3) & 7];
           }
-          pred[(32 * half + r) * N + col] = (Px)clampi(v, 0, maxv);
+          pred[(32 * half + r) * N + col] = (Px)clamp_med3(v, 0, maxv);
         }
       }
     }
@@ -554,7 +552,7 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
 #pragma unroll
     for (int r = 0; r < N; r++) {
       Px *q = pred + r * N + lane;
-      *q = (Px)clampi(wadd((int32_t)*q, round_shift(v[r], 4)), 0, maxv);
+      *q = (Px)clamp_med3(wadd((int32_t)*q, round_shift(v[r], 4)), 0, maxv);
     }
   }
   wave_sync();
