@@ -9,9 +9,11 @@ diamond + sub-pel, F4 RDO candidates (MC, diff+fwd DCT, coefficient
 stand-in, inverse DCT + add, distortion), F5 8x8 importance SATD.
 Frames cycle through the reorder pyramid's me_range_scale (4, 2, 1, 1).
 
-N = 1: configs[1] of BASELINE.json (1080p 8-bit 4:2:0, one tile, 1 GPU).
+N = 1: the configuration BASELINE.json's metric is quoted on -- 4K (2160p)
+8-bit 4:2:0 speed 10, one tile on one GPU (it fits one GPU; --config picks
+the other shapes of `configs`, e.g. 1080p = configs[1]).
 N > 1 (torch.distributed.run, one process per GPU): every rank runs its own
-1080p tile stream (rav1e_amd/ranks.py) -- tiles are independent units in
+2160p tile stream (rav1e_amd/ranks.py) -- tiles are independent units in
 the replay, so there is no data-path collective; `value` = frames of all
 ranks / max-over-ranks time ("scaling": "weak").  torch.distributed (gloo)
 carries only the barrier and the max-time reduction.
@@ -40,6 +42,7 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
 # per CU-cycle over 4 SIMDs; tools/ubench/valu_rates.hip measures 0.87 of
 # it), 4 |a-b| per lane-op for u8, 2 for v_sad_u16
 SAD_PEAK_PX = 256 * 64 * 2.4e9 * 4
+VALU_PEAK_GIPS = 256 * 4 * 2.4 / 4  # G wave64 VALU instructions/s
 
 
 def coarse_windows(W, H, R, scale, tile=(0, 0, 0, 0)):
@@ -84,11 +87,11 @@ ROCPROF_NAMES = {
 
 def measured_traffic(args, kernel, bd):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
-    passes (profiles/traffic_1080p.json: 2 x FETCH_SIZE + WRITE_SIZE, see
-    tools/prof_summary.py), for the default workload it was measured on;
-    None otherwise."""
-    path = os.path.join(ROOT, "profiles", "traffic_1080p.json")
-    if args.config != "1080p" or args.refs != 2 or not os.path.exists(path):
+    passes (profiles/traffic_<config>.json: 2 x FETCH_SIZE + WRITE_SIZE, see
+    tools/prof_summary.py), for the workload it was measured on; None
+    otherwise."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if args.refs != 2 or not os.path.exists(path):
         return None
     with open(path) as f:
         tj = json.load(f)
@@ -100,6 +103,25 @@ def measured_traffic(args, kernel, bd):
         if want in name:
             return {"bytes_per_launch": round(v["hbm_bytes"]), "source": tj["source"],
                     "git": tj["git"]}
+    return None
+
+
+def measured_valu(args, kernel, bd):
+    """Wave64 VALU instructions per launch of `kernel` (SQ_INSTS_VALU) from the
+    committed rocprofv3 SQ counter pass profiles/valu_<config>.json
+    (tools/pmc_json.py); None when the workload has no committed pass."""
+    path = os.path.join(ROOT, "profiles", f"valu_{args.config}.json")
+    if args.refs != 2 or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        tj = json.load(f)
+    if kernel == "full_search" and args.exhaustive_fs:
+        kernel = "full_search_exhaustive"
+    want = ROCPROF_NAMES.get(kernel, "?").format(px="unsigned short" if bd > 8 else "unsigned char",
+                                                 pxs="u16" if bd > 8 else "u8")
+    for name, v in tj["kernels"].items():
+        if want in name:
+            return v["SQ_INSTS_VALU"], tj
     return None
 
 
@@ -133,7 +155,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=4)
-    ap.add_argument("--config", default="1080p", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="2160p", choices=sorted(CONFIGS))
     ap.add_argument("--refs", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -221,6 +243,16 @@ def main():
             "traffic": measured_traffic(args, dom, bd),
             "avg_launch_ms": round(kd["ms"] / kd["launches"], 5),
             "algorithmic_bytes_per_launch": round(kd["bytes"] / kd["launches"])}
+    mv = measured_valu(args, dom, bd)
+    if mv:
+        # VALU issue roofline: one wave64 VALU instruction per 4 cycles per
+        # SIMD (1024 SIMDs at 2.4 GHz); instructions per launch from the
+        # committed SQ_INSTS_VALU pass, time from this run's HIP events
+        achv = mv[0] / launch_s / 1e9
+        roof["valu"] = {"achieved": round(achv, 1), "peak": VALU_PEAK_GIPS,
+                        "unit": "G wave64 VALU instr/s", "frac": round(achv / VALU_PEAK_GIPS, 4),
+                        "insts_per_launch": round(mv[0]), "source": mv[1]["source"],
+                        "git": mv[1]["git"]}
     if dom == "full_search" and not sea:
         achv = kd["sad_px"] / (kd["ms"] / 1e3) / 1e12
         peak = SAD_PEAK_PX / (2 if bd > 8 else 1)
