@@ -421,16 +421,16 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
       acc = sub_sad_rows<Px, W, S::RG, S::UP, false, false>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
     return wave_sum(acc);
   };
-  // Called by every thread.  Wave w evaluates cands[w] (w < n); returns its
-  // cost (u64::MAX when out of range or w >= n).  No trailing barrier: the
+  // Called by every thread.  Wave w evaluates cands[w] (w < n, w != skip);
+  // returns its cost (u64::MAX when out of range, skipped or w >= n).  No trailing barrier: the
   // caller's cost exchange barrier orders the next round's window writes.
-  auto sub_round = [&](const rv_mv *cands, int n) __attribute__((always_inline)) -> uint64_t {
+  auto sub_round = [&](const rv_mv *cands, int n, int skip) __attribute__((always_inline)) -> uint64_t {
     SubPos q[kDsWaves];
     int ux = 1 << 30, uy = 1 << 30, ux2 = -(1 << 30), uy2 = -(1 << 30), any = 0;
 #pragma unroll
     for (int k = 0; k < kDsWaves; k++) {
       q[k] = sub_pos(cands[k < n ? k : 0]);
-      q[k].ok = q[k].ok && k < n;
+      q[k].ok = q[k].ok && k < n && k != skip;
       if (q[k].ok) {
         any = 1;
         ux = q[k].qx < ux ? q[k].qx : ux;
@@ -463,7 +463,8 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
 #pragma unroll
         for (int j = 1; j < kDsWaves; j++)
           if (k == j) ck = cands[j];
-        const SubPos qk = sub_pos(ck);
+        SubPos qk = sub_pos(ck);
+        qk.ok = qk.ok && k != skip;
         __syncthreads();  // previous window consumed
         if (qk.ok) load_box(qk.qx, qk.qy, H + 7, W + 7);
         __syncthreads();
@@ -503,7 +504,7 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
         }
         uint64_t c;
         if constexpr (SUB) {
-          c = sub_round(c4, kDsWaves);
+          c = sub_round(c4, kDsWaves, -1);
         } else {
           rv_mv mine = c4[0];
 #pragma unroll
@@ -540,6 +541,13 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
     int16_t radius = a.subpel ? 4 : 16;
     const int16_t radius_end = a.subpel ? (a.hp ? 1 : 2) : 8;
     int p0 = 0;  // next predictor group; >= np once the diamond phase runs
+    // After a move along pattern p the step at the same radius contains the
+    // previous centre again (pattern (p + 2) & 3).  Its cost is the old
+    // centre cost, which the move strictly undercut, so whatever the other
+    // three give, it cannot move the centre: the step's outcome (move to the
+    // first strict minimum, or halve the radius) is the same without it.
+    // (The oracle, orc_diamond_search, evaluates it like the reference.)
+    int back = -1;
     // Every diamond move strictly lowers center_cost, so the loop ends; the
     // bound only guarantees the grid drains whatever the inputs.
     for (int iter = 0; iter < 4096 + RV_DS_MAX_PRED; iter++) {
@@ -557,15 +565,16 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
         c4[2] = rv_mv{(int16_t)(center.row - radius), center.col};
         c4[3] = rv_mv{center.row, (int16_t)(center.col - radius)};
       }
+      const int skip = pred_phase ? -1 : back;
       uint64_t c;
       if constexpr (SUB) {
-        c = sub_round(c4, n);
+        c = sub_round(c4, n, skip);
       } else {
         rv_mv mine = c4[0];
   #pragma unroll
         for (int k = 1; k < kDsWaves; k++)
           if (wave == k) mine = c4[k];
-        c = wave < n ? eval_full(mine) : ~0ull;
+        c = wave < n && wave != skip ? eval_full(mine) : ~0ull;
       }
       if (lane == 0) scost[iter & 1][wave] = c;
       __syncthreads();
@@ -592,7 +601,11 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
       } else if (center_cost <= best) {
         if (radius == radius_end) break;
         radius /= 2;
+        back = -1;
       } else {
+        // the old centre's cost is genuine unless it is the u64::MAX
+        // placeholder of a search whose predictors were all out of range
+        back = center_cost != ~0ull ? (bp + 2) & 3 : -1;
         center = bmv;
         center_cost = best;
       }
