@@ -150,9 +150,11 @@ struct SubGeo {
                                            : ((2 * (W + 8) + 15) / 16) * 16;
   static constexpr int kWinDwords = (H + 7) * P / 4;
   static constexpr int kOrgDwords = RG * (int)sizeof(Px) / 4;
-  // union window of one diamond round: D px of slack in each direction,
-  // pitch UP bytes (+3 px for the dword over-read of the horizontal pass)
-  static constexpr int D = 4;
+  // staged window: D px of slack in each direction around the candidates'
+  // integer origins, so successive rounds of a search (which stay within a
+  // pixel or two) reuse it; pitch UP bytes (+3 px for the dword over-read of
+  // the horizontal pass)
+  static constexpr int D = 8;
   static constexpr int UP = (((W + 7 + D + 4) * (int)sizeof(Px)) + 15) / 16 * 16;
   static constexpr int kUnionDwords = (H + 7 + D) * UP / 4;
 };
@@ -424,6 +426,10 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
   // Called by every thread.  Wave w evaluates cands[w] (w < n, w != skip);
   // returns its cost (u64::MAX when out of range, skipped or w >= n).  No trailing barrier: the
   // caller's cost exchange barrier orders the next round's window writes.
+  // The window currently staged in win_all: origin (wx, wy), D px of slack;
+  // wvalid = false after a far-apart round overwrote it.
+  int wx = 0, wy = 0;
+  bool wvalid = false;
   auto sub_round = [&](const rv_mv *cands, int n, int skip) __attribute__((always_inline)) -> uint64_t {
     SubPos q[kDsWaves];
     int ux = 1 << 30, uy = 1 << 30, ux2 = -(1 << 30), uy2 = -(1 << 30), any = 0;
@@ -450,13 +456,26 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
         me_mv = cands[k < n ? k : 0];
       }
     if (ux2 - ux <= S::D && uy2 - uy <= S::D) {
-      load_box(ux, uy, (uy2 - uy) + H + 7, (ux2 - ux) + W + 7);
-      __syncthreads();
+      // Re-stage only when a candidate leaves the staged window.  The last
+      // round's cost-exchange barrier follows every read of the old window.
+      // The new origin centres the slack on this round's candidates, kept
+      // within the origins PlaneSlice::clamp can produce (so the reads stay
+      // where a single candidate's window may read).
+      if (!(wvalid && ux >= wx && ux2 <= wx + S::D && uy >= wy && uy2 <= wy + S::D)) {
+        wx = clampi(ux - ((S::D - (ux2 - ux)) >> 1), max(ux2 - S::D, -ref.xorigin),
+                    min(ux, ref.width - S::D));
+        wy = clampi(uy - ((S::D - (uy2 - uy)) >> 1), max(uy2 - S::D, -ref.yorigin),
+                    min(uy, ref.height - S::D));
+        load_box(wx, wy, S::D + H + 7, S::D + W + 7);
+        __syncthreads();
+        wvalid = true;
+      }
       if (me.ok) {
         evals++;
-        mine = ds_cost(sub_sad(me.cf, me.rf, me.qx - ux, me.qy - uy), me_mv, jb, a.hp);
+        mine = ds_cost(sub_sad(me.cf, me.rf, me.qx - wx, me.qy - wy), me_mv, jb, a.hp);
       }
     } else {  // far-apart predictors: one window at a time
+      wvalid = false;
 #pragma unroll 1
       for (int k = 0; k < n; k++) {
         rv_mv ck = cands[0];  // static indices only (no scratch)
