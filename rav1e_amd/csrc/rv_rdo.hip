@@ -349,37 +349,48 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   }
 }
 
-// ---- luma candidates: 64x64, one wavefront, ~8 KiB of LDS -------------------
-// The same chain as rdo_cand_body<Px, 64, true, 64> with the 64x64 i32 slab
-// gone, so four wavefronts fit a SIMD instead of two:
-//  * put_8tap in two halves of 32 output rows (39 staged window rows each);
+// ---- luma candidates: 64x64 --------------------------------------------------
+// The chain of rdo_cand_body<Px, 64, true, 64> without the 64x64 i32 slab:
+//  * put_8tap in NPART bands of 64 / NPART output rows, their window rows
+//    staged in turn;
 //  * the residual is formed per column straight from the source plane and
 //    the LDS prediction, and only column-DCT outputs 0..15 are kept: the
 //    stand-in reads raster rows 0..15 of the 64x64 fht output
 //    (src/encoder.rs:1152-1156), and row r of that raster is the row DCT of
 //    column-pass row r, so the compiler drops the other 48 outputs;
 //  * the inverse row pass stores round_shift(., INTERMEDIATE_SHIFT) clamped
-//    to the column range (inverse.rs:2075-2098) -- 16 bits for u8, so i16.
+//    to the column range max(bd + 6, 16) (inverse.rs:2075-2098): i16 up to
+//    10 bits (Mid), i32 for 12.
+// Phases: luma_front (MC, residual, column DCT -> fmid), luma_fwd_row (row
+// DCT + stand-in of one raster row, one lane per row), luma_inv_row_load /
+// _tx (one lane per coded row), luma_back (inverse columns, reconstruction,
+// cdef moments).
+__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+template <typename Px, typename Mid, int NPART>
 struct LumaLds {
-  template <typename Px>
   static constexpr int kWinP = sizeof(Px) == 1 ? 80 : 144;  // window row pitch, bytes
-  template <typename Px>
-  using Mid = typename std::conditional<sizeof(Px) == 1, int16_t, int32_t>::type;
-  template <typename Px>
-  static constexpr int kScr() {  // bytes of the phase-shared scratch
-    constexpr int win = 39 * kWinP<Px>, fwd = 16 * 65 * 4, inv = 32 * 66 * (int)sizeof(Mid<Px>);
-    return win > fwd ? (win > inv ? win : inv) : (fwd > inv ? fwd : inv);
-  }
-  template <typename Px>
-  static constexpr int kBytes = kScr<Px>() + 64 * 64 * (int)sizeof(Px);
+  static constexpr int kWinRows = 64 / NPART + 7;
+  static constexpr int kScr =  // bytes of the phase-shared scratch
+      cmax(cmax(kWinRows * kWinP, 16 * 65 * 4), 32 * 66 * (int)sizeof(Mid));
+  static constexpr int kSlot = (kScr + 64 * 64 * (int)sizeof(Px) + 15) / 16 * 16;  // + pred
 };
 
-template <typename Px>
-__device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &pl, int t,
-                                              uint8_t *scr, Px *pred) {
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// MC into pred, then residual + column DCT: fmid = scr as i32 [16][65].  No
+// trailing synchronisation (the caller's).
+template <typename Px, int NPART>
+__device__ __forceinline__ void luma_front(const RdoArgs &a, const RdoPlane &pl, int t,
+                                           uint8_t *scr, Px *pred) {
   constexpr int N = 64, B = (int)sizeof(Px);
-  constexpr int P = LumaLds::kWinP<Px>;
-  using Mid = LumaLds::Mid<Px>;
+  constexpr int P = LumaLds<Px, int16_t, NPART>::kWinP;
+  constexpr int RP = N / NPART;  // output rows per band
+  static_assert(RP % 8 == 0, "MC rows run in groups of 8");
   const int lane = threadIdx.x & 63;
   const int cand = t / a.ntx_per_cand;
   const rv_mc_job mj = pl.mc[cand];
@@ -387,13 +398,8 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
   const rv_plane &ref = pl.ref[cand / a.cands_per_ref];
   const int ox = tj.pred_x - mj.dst_x, oy = tj.pred_y - mj.dst_y;
   const int bd = a.bd, ib = bd == 12 ? 2 : 4, maxv = (1 << bd) - 1;
-  auto wave_sync = [] {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
 
-  // ---- A. put_8tap (src/mc.rs:213-307) into pred, two halves --------------
+  // ---- A. put_8tap (src/mc.rs:213-307) into pred, NPART bands --------------
   {
     uint32_t *win = reinterpret_cast<uint32_t *>(scr);
     const int cf = mj.col_frac, rf = mj.row_frac;
@@ -449,13 +455,13 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
     };
     const int vshift = cf ? 7 + ib : 7;
     constexpr int kRowDw = ((N + 7) * B + 3) / 4;
-    constexpr int kTot = 39 * kRowDw;
+    constexpr int kTot = (RP + 7) * kRowDw;
     const int64_t rs = (int64_t)ref.stride * B;
 #pragma unroll 1
-    for (int half = 0; half < 2; half++) {
+    for (int half = 0; half < NPART; half++) {
       const uint8_t *sp =
-          (const uint8_t *)plane_ptr<Px>(ref, mj.src_x + ox - 3, mj.src_y + oy - 3 + 32 * half);
-      if (half) wave_sync();  // the first half's window reads are done
+          (const uint8_t *)plane_ptr<Px>(ref, mj.src_x + ox - 3, mj.src_y + oy - 3 + RP * half);
+      if (half) wave_sync();  // the previous band's window reads are done
 #pragma unroll 4
       for (int i = lane; i < kTot; i += 64) {
         const int r = i / kRowDw, d = i - r * kRowDw;
@@ -469,7 +475,7 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
       for (int k = 1; k < 6; k++) ring[k] = hval(k);
       ring[0] = ring[6] = ring[7] = 0;
 #pragma unroll 1
-      for (int r0 = 0; r0 < 32; r0 += 8) {
+      for (int r0 = 0; r0 < RP; r0 += 8) {
 #pragma unroll
         for (int u = 0; u < 8; u++) {
           const int r = r0 + u;
@@ -483,7 +489,7 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
           } else {
             v = cf ? round_shift(ring[(u + 3) & 7], ib) : ring[(u + 3) & 7];
           }
-          pred[(32 * half + r) * N + col] = (Px)clamp_med3(v, 0, maxv);
+          pred[(RP * half + r) * N + col] = (Px)clamp_med3(v, 0, maxv);
         }
       }
     }
@@ -507,42 +513,57 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
 #pragma unroll
     for (int r = 0; r < 16; r++) fmid[r * 65 + lane] = rdo_rsa(v[r], -s1);
   }
-  wave_sync();
-  // ---- C'. row DCT of raster rows 0..15 + the quantize stand-in ------------
-  if (lane < 16) {
-    int32_t v[N];
+}
+
+// Row DCT + quantize stand-in of one fmid row (raster row r of the 64x64
+// fht output), in place.
+__device__ __forceinline__ void luma_fwd_row(int32_t *row, int bd) {
+  int s0, s1, s2;
+  fwd_shifts<64>((bd - 8) / 2, s0, s1, s2);
+  int32_t v[64];
 #pragma unroll
-    for (int c = 0; c < N; c++) v[c] = fmid[lane * 65 + c];
-    tx::fwd1d<1, N>(v, v);
+  for (int c = 0; c < 64; c++) v[c] = row[c];
+  tx::fwd1d<1, 64>(v, v);
 #pragma unroll
-    for (int c = 0; c < N; c++) fmid[lane * 65 + c] = (rdo_rsa(v[c], -s2) / kQstep) * kQstep;
+  for (int c = 0; c < 64; c++) row[c] = (rdo_rsa(v[c], -s2) / kQstep) * kQstep;
+}
+
+// Inverse row rr (0..31) of the coded 32x32 block: packed[rr * 32 ..] =
+// raster entries of fmid row rr >> 1 from column (rr & 1) * 32.  pk (may be
+// null) receives the 32 raw coefficients (the packed output).
+__device__ __forceinline__ void luma_inv_row_load(const int32_t *fmid, int rr, int32_t *v,
+                                                  int range, int32_t *pk) {
+  const int32_t *src = fmid + (rr >> 1) * 65 + (rr & 1) * 32;
+#pragma unroll
+  for (int c = 0; c < 32; c++) {
+    const int32_t x = src[c];
+    if (pk) pk[c] = x;
+    v[c] = tx::clampv(x, range);
   }
-  wave_sync();
-  // packed coefficients = raster entries 0..1023 (row stride 32), coalesced
-  {
-    int32_t *pk = pl.packed + (int64_t)t * 1024;
-#pragma unroll 4
-    for (int i = lane; i < 1024; i += 64) pk[i] = fmid[(i >> 6) * 65 + (i & 63)];
-  }
-  // ---- D. inverse rows: input row rr = packed[rr * 32 ..] ------------------
-  const int range = bd + 8;
+#pragma unroll
+  for (int c = 32; c < 64; c++) v[c] = 0;
+}
+template <typename Mid>
+__device__ __forceinline__ void luma_inv_row_tx(int32_t *v, Mid *dst, int range, int crange) {
+  tx::inv1d<1, 64>(v, range);
+#pragma unroll
+  for (int c = 0; c < 64; c++) dst[c] = (Mid)tx::clampv(round_shift(v[c], 2), crange);
+}
+
+// Inverse columns + add into pred, reconstruction to the tall plane, cdef
+// moments.  imid = [32][66] row-pass output.
+template <typename Px, typename Mid>
+__device__ __forceinline__ void luma_back(const RdoArgs &a, const RdoPlane &pl, int t,
+                                          const Mid *imid, Px *pred) {
+  constexpr int N = 64, B = (int)sizeof(Px);
+  const int lane = threadIdx.x & 63;
+  const int cand = t / a.ntx_per_cand;
+  const rv_mc_job mj = pl.mc[cand];
+  const rv_tx_job tj = pl.tx[t];
+  const int ox = tj.pred_x - mj.dst_x, oy = tj.pred_y - mj.dst_y;
+  const int bd = a.bd, maxv = (1 << bd) - 1;
   const int crange = bd + 6 > 16 ? bd + 6 : 16;
-  Mid *imid = reinterpret_cast<Mid *>(scr);  // [32][66]
-  {
-    int32_t v[N];
-    if (lane < 32) {
-#pragma unroll
-      for (int c = 0; c < N; c++)
-        v[c] = c < 32 ? tx::clampv(fmid[(lane >> 1) * 65 + (lane & 1) * 32 + c], range) : 0;
-    }
-    wave_sync();  // every read of fmid precedes the imid writes (same bytes)
-    if (lane < 32) {
-      tx::inv1d<1, N>(v, range);
-#pragma unroll
-      for (int c = 0; c < N; c++) imid[lane * 66 + c] = (Mid)tx::clampv(round_shift(v[c], 2), crange);
-    }
-  }
-  wave_sync();
+  const Px *o = plane_ptr<Px>(pl.org, tj.src_x, tj.src_y);
   // ---- D'. inverse columns + add into pred ---------------------------------
   {
     int32_t v[N];
@@ -597,6 +618,34 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
   }
 }
 
+// One luma candidate per wavefront (12-bit, and the split-stream option).
+template <typename Px, typename Mid, int NPART>
+__device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &pl, int t,
+                                              uint8_t *scr, Px *pred) {
+  const int lane = threadIdx.x & 63;
+  luma_front<Px, NPART>(a, pl, t, scr, pred);
+  wave_sync();
+  int32_t *fmid = reinterpret_cast<int32_t *>(scr);
+  if (lane < 16) luma_fwd_row(fmid + lane * 65, a.bd);
+  wave_sync();
+  // packed coefficients = raster entries 0..1023 (row stride 32), coalesced
+  {
+    int32_t *pk = pl.packed + (int64_t)t * 1024;
+#pragma unroll 4
+    for (int i = lane; i < 1024; i += 64) pk[i] = fmid[(i >> 6) * 65 + (i & 63)];
+  }
+  const int range = a.bd + 8, crange = a.bd + 6 > 16 ? a.bd + 6 : 16;
+  Mid *imid = reinterpret_cast<Mid *>(scr);  // [32][66]
+  {
+    int32_t v[64];
+    if (lane < 32) luma_inv_row_load(fmid, lane, v, range, nullptr);
+    wave_sync();  // every read of fmid precedes the imid writes (same bytes)
+    if (lane < 32) luma_inv_row_tx(v, imid + lane * 66, range, crange);
+  }
+  wave_sync();
+  luma_back<Px, Mid>(a, pl, t, imid, pred);
+}
+
 // One launch per frame: blocks [0, luma.n_tx) are the luma candidates
 // (N = 64, cdef moments), the rest the chroma transform blocks of planes U
 // then V (N = 32, SSE).  Luma first: the long tasks start first.
@@ -618,7 +667,7 @@ __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, in
                                                 Px *pred) {
   const int pairs = (chroma.n_tx + 1) / 2;
   const int plane = b / pairs;
-  const int half = threadIdx.x >> 5;
+  const int half = (threadIdx.x & 63) >> 5;
   int i = 2 * (b - plane * pairs) + half;
   const bool valid = i < chroma.n_tx;
   if (!valid) i -= 1;
@@ -626,21 +675,89 @@ __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, in
                                    buf + half * 32 * 33, pred + half * 32 * 32);
 }
 
-// LDS: the larger of the luma layout and the chroma pair (2 x (32 x 33 i32 +
-// 32 x 32 Px)), ~10 KiB for u8.
+// One luma candidate or one chroma pair per 64-thread workgroup: the
+// 12-bit path (its row-pass intermediate needs i32) and the split-stream
+// option.  LDS: the larger of the luma slot and the chroma pair.
+template <typename Px>
+using SingleLds = LumaLds<Px, typename std::conditional<sizeof(Px) == 1, int16_t, int32_t>::type, 2>;
+constexpr int kChromaPair(int pxb) { return 2 * 32 * 33 * 4 + 2 * 32 * 32 * pxb; }
+
 template <typename Px>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void rdo_frame_kernel(
     RdoArgs luma, RdoArgs chroma) {
-  constexpr int kChroma = 2 * 32 * 33 * 4 + 2 * 32 * 32 * (int)sizeof(Px);
-  constexpr int kLuma = LumaLds::kBytes<Px>;
-  __shared__ __align__(16) uint8_t lds[kLuma > kChroma ? kLuma : kChroma];
+  using L = SingleLds<Px>;
+  using Mid = typename std::conditional<sizeof(Px) == 1, int16_t, int32_t>::type;
+  __shared__ __align__(16) uint8_t lds[cmax(L::kSlot, kChromaPair(sizeof(Px)))];
   const int b = blockIdx.x;
   if (b < luma.n_tx)
-    rdo_luma_body<Px>(luma, luma.p[0], rdo_task(luma, b), lds,
-                      reinterpret_cast<Px *>(lds + LumaLds::kScr<Px>()));
+    rdo_luma_body<Px, Mid, 2>(luma, luma.p[0], rdo_task(luma, b), lds,
+                              reinterpret_cast<Px *>(lds + L::kScr));
   else
     rdo_chroma_pair<Px>(chroma, b - luma.n_tx, reinterpret_cast<int32_t *>(lds),
                         reinterpret_cast<Px *>(lds + 2 * 32 * 33 * 4));
+}
+
+// 8- and 10-bit: 256-thread workgroups.  Blocks [0, nquads) carry four luma
+// candidates, one per wavefront, that share the two narrow phases -- the row
+// DCT (16 raster rows per candidate: wavefront 0 runs all 64 rows) and the
+// inverse rows (32 per candidate: wavefronts 0 and 1 run all 128) -- so
+// those phases issue a quarter / half of the instructions of the
+// single-candidate body.  The rest carry chroma pairs, three per workgroup
+// (wavefront 3 leaves at once), inside the same LDS.
+template <typename Px>
+struct QuadLds {
+  using L = LumaLds<Px, int16_t, sizeof(Px) == 1 ? 2 : 4>;
+  static constexpr int kBytes = cmax(4 * L::kSlot, 3 * kChromaPair(sizeof(Px)));
+};
+
+template <typename Px>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_quad_kernel(
+    RdoArgs luma, RdoArgs chroma, int nquads) {
+  using L = typename QuadLds<Px>::L;
+  constexpr int NPART = sizeof(Px) == 1 ? 2 : 4;
+  __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int b = blockIdx.x;
+  if (b >= nquads) {  // chroma pairs: wave-local, no workgroup barriers
+    const int pair = 3 * (b - nquads) + wave;
+    if (wave == 3 || pair >= 2 * ((chroma.n_tx + 1) / 2)) return;
+    uint8_t *w = lds + wave * kChromaPair(sizeof(Px));
+    rdo_chroma_pair<Px>(chroma, pair, reinterpret_cast<int32_t *>(w),
+                        reinterpret_cast<Px *>(w + 2 * 32 * 33 * 4));
+    return;
+  }
+  auto slot = [&](int q) __attribute__((always_inline)) { return lds + q * L::kSlot; };
+  auto fmid = [&](int q) __attribute__((always_inline)) {
+    return reinterpret_cast<int32_t *>(slot(q));
+  };
+  auto imid = [&](int q) __attribute__((always_inline)) {
+    return reinterpret_cast<int16_t *>(slot(q));
+  };
+  auto pred = [&](int q) __attribute__((always_inline)) {
+    return reinterpret_cast<Px *>(slot(q) + L::kScr);
+  };
+  const int t0 = 4 * b;
+  const bool valid = t0 + wave < luma.n_tx;
+  if (valid) luma_front<Px, NPART>(luma, luma.p[0], rdo_task(luma, t0 + wave), slot(wave), pred(wave));
+  __syncthreads();
+  if (wave == 0) {  // row DCT: lane = 16 * candidate + raster row
+    const int q = lane >> 4;
+    if (t0 + q < luma.n_tx) luma_fwd_row(fmid(q) + (lane & 15) * 65, luma.bd);
+  }
+  __syncthreads();
+  if (wave < 2) {  // inverse rows: lane = 32 * (candidate & 1) + coded row
+    const int q = 2 * wave + (lane >> 5), rr = lane & 31;
+    const bool vq = t0 + q < luma.n_tx;
+    const int range = luma.bd + 8, crange = luma.bd + 6 > 16 ? luma.bd + 6 : 16;
+    int32_t v[64];
+    if (vq)
+      luma_inv_row_load(fmid(q), rr, v, range,
+                        luma.p[0].packed + (int64_t)rdo_task(luma, t0 + q) * 1024 + rr * 32);
+    wave_sync();  // the wavefront's fmid reads precede its imid writes (same bytes)
+    if (vq) luma_inv_row_tx(v, imid(q) + rr * 66, range, crange);
+  }
+  __syncthreads();
+  if (valid) luma_back<Px, int16_t>(luma, luma.p[0], rdo_task(luma, t0 + wave), imid(wave), pred(wave));
 }
 
 // Chroma pairs alone (10.5 KiB of LDS instead of the luma slab's 20.7 KiB,
@@ -679,12 +796,20 @@ int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipSt
     RV_HIP_CHECK_LAUNCH();
     return RV_OK;
   }
-  const unsigned grid = (unsigned)luma.n_tx + cpairs;
+  if (luma.bd == 12) {  // i32 row-pass intermediate: one candidate per workgroup
+    const unsigned grid = (unsigned)luma.n_tx + cpairs;
+    if (grid == 0) return RV_OK;
+    rdo_frame_kernel<uint16_t><<<grid, 64, 0, s>>>(luma, chroma);
+    RV_HIP_CHECK_LAUNCH();
+    return RV_OK;
+  }
+  const int nquads = (luma.n_tx + 3) / 4;
+  const unsigned grid = (unsigned)nquads + (cpairs + 2) / 3;
   if (grid == 0) return RV_OK;
   if (hbd)
-    rdo_frame_kernel<uint16_t><<<grid, 64, 0, s>>>(luma, chroma);
+    rdo_quad_kernel<uint16_t><<<grid, 256, 0, s>>>(luma, chroma, nquads);
   else
-    rdo_frame_kernel<uint8_t><<<grid, 64, 0, s>>>(luma, chroma);
+    rdo_quad_kernel<uint8_t><<<grid, 256, 0, s>>>(luma, chroma, nquads);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }
