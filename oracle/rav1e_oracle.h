@@ -84,6 +84,30 @@ int orc_fwd_txfm2d(const int16_t *residual, int32_t *coeffs, int tx_size,
  * coeffs are min(W,32)*min(H,32) i32, row stride min(W,32). */
 int orc_inv_txfm2d_add(const int32_t *coeffs, void *dst, ptrdiff_t dst_stride,
                        int tx_size, int tx_type, int bit_depth, int hbd);
+/* ---- quantize / dequantize (src/quantize.rs) --------------------------- */
+typedef struct {
+  int log_tx_scale;
+  uint32_t dc_quant;
+  int32_t dc_offset;
+  uint32_t dc_mul_add[3];
+  uint32_t ac_quant;
+  int32_t ac_offset_eob, ac_offset0, ac_offset1;
+  uint32_t ac_mul_add[3];
+} orc_qctx; /* QuantizationContext (src/quantize.rs:108-120) */
+int orc_get_log_tx_scale(int tx_size);
+int orc_coded_tx_area(int tx_size);
+int orc_dc_q(int qindex, int delta_q, int bd);
+int orc_ac_q(int qindex, int delta_q, int bd);
+void orc_divu_gen(uint32_t d, uint32_t out[3]);
+int32_t orc_divu_pair(int32_t x, const uint32_t d[3]);
+void orc_qctx_update(orc_qctx *c, int qindex, int tx_size, int is_intra, int bd,
+                     int dc_delta_q, int ac_delta_q);
+/* coeffs indexed by scan position (the forward transform's W-stride raster,
+ * first coded_tx_area entries); returns eob. */
+int orc_quantize(const orc_qctx *c, const int32_t *coeffs, int32_t *qcoeffs, int tx_size,
+                 int tx_type);
+void orc_dequantize(int qindex, const int32_t *coeffs, int32_t *rcoeffs, int tx_size, int bd,
+                    int dc_delta_q, int ac_delta_q);
 /* diff (src/encoder.rs:1044-1058) */
 void orc_diff(int16_t *dst, const void *a, ptrdiff_t sa, const void *b,
               ptrdiff_t sb, int w, int h, int hbd);

@@ -45,6 +45,15 @@ def lib():
         L.orc_plane_pad.argtypes = [vp] + [i32] * 9
         L.orc_downsample.argtypes = [vp, sz, i32, i32, vp, sz, i32]
         L.orc_get_mv_rate.restype = C.c_uint32
+        L.orc_divu_pair.restype = i32
+        L.orc_divu_pair.argtypes = [i32, vp]
+        L.orc_divu_gen.argtypes = [C.c_uint32, vp]
+        L.orc_qctx_update.argtypes = [vp] + [i32] * 6
+        L.orc_quantize.restype = i32
+        L.orc_quantize.argtypes = [vp, vp, vp, i32, i32]
+        L.orc_dequantize.argtypes = [i32, vp, vp, i32, i32, i32, i32]
+        L.orc_coded_tx_area.restype = i32
+        L.orc_get_log_tx_scale.restype = i32
         _lib = L
     return _lib
 
@@ -113,6 +122,39 @@ def fwd_txfm2d(residual, tx_size, tx_type, bd):
     out = np.zeros(r.size, dtype=np.int32)
     rc = lib().orc_fwd_txfm2d(ptr(r), ptr(out), tx_size, tx_type, bd)
     return None if rc else out
+
+
+def divu_gen(d):
+    out = np.zeros(3, dtype=np.uint32)
+    lib().orc_divu_gen(d, ptr(out))
+    return out
+
+
+def divu_pair(x, dgen):
+    return lib().orc_divu_pair(int(x), ptr(dgen))
+
+
+QCTX_BYTES = 64  # >= sizeof(orc_qctx)
+
+
+def quantize(coeffs, tx_size, tx_type, qindex, bd, is_intra=False, dc_delta_q=0,
+             ac_delta_q=0):
+    """QuantizationContext::update + quantize (src/quantize.rs:205-316):
+    (qcoeffs[coded_tx_area], eob)."""
+    ctx = np.zeros(QCTX_BYTES, dtype=np.uint8)
+    lib().orc_qctx_update(ptr(ctx), qindex, tx_size, int(is_intra), bd, dc_delta_q, ac_delta_q)
+    c = np.ascontiguousarray(coeffs, dtype=np.int32).ravel()
+    q = np.zeros(lib().orc_coded_tx_area(tx_size), dtype=np.int32)
+    eob = lib().orc_quantize(ptr(ctx), ptr(c), ptr(q), tx_size, tx_type)
+    return q, eob
+
+
+def dequantize(qcoeffs, tx_size, qindex, bd, dc_delta_q=0, ac_delta_q=0):
+    """dequantize (src/quantize.rs:319-333)"""
+    q = np.ascontiguousarray(qcoeffs, dtype=np.int32).ravel()
+    r = np.zeros(q.size, dtype=np.int32)
+    lib().orc_dequantize(qindex, ptr(q), ptr(r), tx_size, bd, dc_delta_q, ac_delta_q)
+    return r
 
 
 def inv_txfm2d_add(coeffs, dst, tx_size, tx_type, bd):

@@ -252,3 +252,92 @@ def test_tx_dist_oracle_matches_restatement():
         bits = 2 * (3 - ((tw * th > 256) + (tw * th > 1024)))
         want = ((d + (1 << (bits - 1))) % 2 ** 64) >> bits
         assert O.tx_dist(co.astype(np.int32), rc.astype(np.int32), tw, th) == want
+
+
+# ---- quantize / dequantize (src/quantize.rs) ---------------------------------
+def test_divu_pair_reference_test():
+    """test_divu_pair (src/quantize.rs:160-168): divu_pair(x, divu_gen(d)) ==
+    x / d (Rust: truncating) for d in 1..1024, x in -1000..1000."""
+    for d in range(1, 1024):
+        g = O.divu_gen(d)
+        for x in range(-1000, 1000):
+            assert O.divu_pair(x, g) == int(x / d), (d, x)
+
+
+def test_log_tx_scale_reference_test():
+    """test_tx_log_scale (src/quantize.rs:176-202), TxSize enum order."""
+    want = [0, 0, 0, 1, 2, 0, 0, 0, 0, 1, 1, 2, 2, 0, 0, 0, 0, 1, 1]
+    assert [O.lib().orc_get_log_tx_scale(s) for s in range(19)] == want
+
+
+def _py_quantize(coeffs, scan, n, lts, ac_q, dc_q, is_intra):
+    """Independent restatement of QuantizationContext::update + quantize
+    (src/quantize.rs:205-316) with exact integer division for divu_pair."""
+    dc_off = dc_q * (109 if is_intra else 108) // 256
+    off0 = ac_q * (98 if is_intra else 97) // 256
+    off1 = ac_q * (109 if is_intra else 108) // 256
+    off_eob = ac_q * (88 if is_intra else 44) // 256
+    dz = (ac_q - off_eob + (1 << lts) - 1) >> lts
+    div = lambda x, d: -((-x) // d) if x < 0 else x // d  # noqa: E731
+    sg = lambda v: (v > 0) - (v < 0)  # noqa: E731
+    eob = 1
+    for i in range(n - 1, 0, -1):
+        if abs(int(coeffs[scan[i]])) >= dz:
+            eob = i
+            break
+    q = np.zeros(n, np.int64)
+    c0 = int(coeffs[0]) << lts
+    q[0] = div(c0 + sg(c0) * dc_off, dc_q)
+    mode = 1
+    for i in range(1, min(eob, n - 1) + 1):
+        c = int(coeffs[scan[i]]) << lts
+        l0 = div(c, ac_q)
+        v = div(c + sg(c) * (off1 if l0 > 1 - mode else off0), ac_q)
+        q[scan[i]] = v
+        if mode and v == 0:
+            mode = 0
+        elif v > 1:
+            mode = 1
+    return q, eob
+
+
+@pytest.mark.parametrize("tx_size,tx_type", [(3, 0), (4, 0), (1, 0), (0, 3), (2, 9), (9, 0), (12, 0)])
+def test_quantize_matches_restatement(tx_size, tx_type):
+    """orc_quantize / orc_dequantize vs the restatement above, on coefficient
+    magnitudes around the deadzone and large ones, several qindices, 8/10/12
+    bits, intra and inter.  Scan orders: tools/refeval/gen_quant_tables.py
+    (checked against src/scan_order.rs)."""
+    rng = np.random.default_rng(500 + 19 * tx_type + tx_size)
+    n = O.lib().orc_coded_tx_area(tx_size)
+    lts = O.lib().orc_get_log_tx_scale(tx_size)
+    scan = _scan(tx_size, tx_type)
+    for bd in (8, 10, 12):
+        for qi in (1, 60, 100, 200, 255):
+            dcq, acq = O.lib().orc_dc_q(qi, 0, bd), O.lib().orc_ac_q(qi, 0, bd)
+            for is_intra in (False, True):
+                c = rng.integers(-3 * acq, 3 * acq, n)
+                c[rng.random(n) < 0.5] = 0
+                c[: n // 8] *= 7
+                q, eob = O.quantize(c, tx_size, tx_type, qi, bd, is_intra)
+                want, weob = _py_quantize(c, scan, n, lts, acq, dcq, is_intra)
+                assert eob == weob and (q == want).all(), (bd, qi, is_intra)
+                r = O.dequantize(q, tx_size, qi, bd)
+                off = (1 << lts) - 1
+                quant = np.full(n, acq, np.int64)
+                quant[0] = dcq
+                wr = (q.astype(np.int64) * quant + ((q >> 31) & off)) >> lts
+                assert (r == wr).all()
+
+
+def _scan(tx_size, tx_type):
+    """The scan as the oracle's generated table holds it (read back through
+    quantize of one-hot inputs is circular, so parse the header)."""
+    import re
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "oracle", "orc_quant_tables.h")).read()
+    def arr(name):
+        m = re.search(name + r"\[\d+\] = \{(.*?)\};", hdr, re.S)
+        return [int(v) for v in re.findall(r"\d+", m.group(1))]
+    scans, off = arr("ORC_SCANS"), arr("ORC_SCAN_OFF")
+    n = O.lib().orc_coded_tx_area(tx_size)
+    o = off[tx_size * 16 + tx_type]
+    return scans[o:o + n]
