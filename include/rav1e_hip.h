@@ -241,6 +241,29 @@ int rv_inv_txfm_add_batch(const int32_t *d_coeffs, const rv_plane *dst,
                           int tx_type, int bit_depth, void *stream);
 
 /* ---------------------------------------------------------------------
+ * Quantisation, the step of encode_tx_block between the transforms
+ * (src/encoder.rs:1170, 1192).  One wavefront per block.
+ * ------------------------------------------------------------------- */
+/* QuantizationContext::update + quantize (src/quantize.rs:205-316) of n
+ * blocks of one (tx_size, tx_type): block i at d_coeffs + i * coeff_stride,
+ * read at the scan positions of av1_scan_orders[tx_size][tx_type]
+ * (src/scan_order.rs:892) -- i.e. the forward transform's W-stride raster,
+ * first coded_tx_area = min(W,32) * min(H,32) entries, as encode_tx_block
+ * hands it over.  d_qcoeffs: [n][coded area] levels; d_rcoeffs (may be
+ * NULL): the same blocks dequantized (src/quantize.rs:319-333), the
+ * inverse transform's input; d_eob (may be NULL): eob per block as the
+ * reference computes it.  qindex 1..255 (lossless is unsupported, as in
+ * src/encoder.rs:1099). */
+int rv_quantize_batch(const int32_t *d_coeffs, int coeff_stride, int n, int tx_size,
+                      int tx_type, int qindex, int bit_depth, int is_intra,
+                      int dc_delta_q, int ac_delta_q, int32_t *d_qcoeffs,
+                      int32_t *d_rcoeffs, uint32_t *d_eob, void *stream);
+/* dequantize (src/quantize.rs:319-333): [n][coded area] levels -> values. */
+int rv_dequantize_batch(const int32_t *d_qcoeffs, int n, int tx_size, int qindex,
+                        int bit_depth, int dc_delta_q, int ac_delta_q,
+                        int32_t *d_rcoeffs, void *stream);
+
+/* ---------------------------------------------------------------------
  * Motion search
  * ------------------------------------------------------------------- */
 typedef struct rv_mv {

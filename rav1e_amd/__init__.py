@@ -226,6 +226,9 @@ def _declare(L):
         "rv_fwd_txfm_batch": (i32, [vp, vp, i32, i32, i32, i32, vp]),
         "rv_diff_fwd_txfm_batch": (i32, [P, P, vp, i32, i32, i32, i32, vp, vp]),
         "rv_inv_txfm_add_batch": (i32, [vp, P, vp, i32, i32, i32, i32, vp]),
+        "rv_quantize_batch": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp,
+                                    vp]),
+        "rv_dequantize_batch": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp]),
         "rv_full_search_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, vp, vp]),
         "rv_full_search_sea_batch": (i32, [P, P, vp, vp, i32, i32, vp, vp]),
         "rv_plane_box_sums": (i32, [P, vp, vp]),
@@ -492,6 +495,48 @@ def diff_fwd_txfm_batch(src: DevicePlane, pred: DevicePlane, jobs, tx_size, tx_t
            "rv_diff_fwd_txfm_batch")
     _sync()
     return out.download(np.int32, w * h * len(jobs)).reshape(len(jobs), w * h)
+
+
+def coded_tx_area(tx_size) -> int:
+    """av1_get_coded_tx_size(tx_size).area() (src/context.rs:1949-1956)."""
+    t = TxSize(tx_size)
+    return min(t.width(), 32) * min(t.height(), 32)
+
+
+def quantize_batch(coeffs: np.ndarray, tx_size, tx_type, qindex, bit_depth=8, is_intra=False,
+                   dc_delta_q=0, ac_delta_q=0):
+    """QuantizationContext::update + quantize + dequantize (src/quantize.rs:
+    205-333) of coeffs [n, >= coded area] (the forward transform's raster):
+    (qcoeffs [n, coded], rcoeffs [n, coded], eob [n])."""
+    c = np.ascontiguousarray(coeffs, dtype=np.int32)
+    n, stride = c.shape
+    coded = coded_tx_area(tx_size)
+    dc = DeviceBuffer.from_array(c)
+    dq = DeviceBuffer(4 * coded * max(1, n))
+    dr = DeviceBuffer(4 * coded * max(1, n))
+    de = DeviceBuffer(4 * max(1, n))
+    _check(lib().rv_quantize_batch(dc.ptr, stride, n, int(tx_size), int(tx_type), int(qindex),
+                                   bit_depth, int(bool(is_intra)), dc_delta_q, ac_delta_q, dq.ptr,
+                                   dr.ptr, de.ptr, None), "rv_quantize_batch")
+    _sync()
+    return (dq.download(np.int32, coded * n).reshape(n, coded),
+            dr.download(np.int32, coded * n).reshape(n, coded), de.download(np.uint32, n))
+
+
+def dequantize_batch(qcoeffs: np.ndarray, tx_size, qindex, bit_depth=8, dc_delta_q=0,
+                     ac_delta_q=0):
+    """dequantize (src/quantize.rs:319-333) of [n, coded area] levels."""
+    q = np.ascontiguousarray(qcoeffs, dtype=np.int32)
+    n = q.shape[0]
+    coded = coded_tx_area(tx_size)
+    if q.shape[1] != coded:
+        raise Rav1eHipError("dequantize_batch: rows must hold the coded area")
+    dq = DeviceBuffer.from_array(q)
+    dr = DeviceBuffer(4 * coded * max(1, n))
+    _check(lib().rv_dequantize_batch(dq.ptr, n, int(tx_size), int(qindex), bit_depth, dc_delta_q,
+                                     ac_delta_q, dr.ptr, None), "rv_dequantize_batch")
+    _sync()
+    return dr.download(np.int32, coded * n).reshape(n, coded)
 
 
 def inv_txfm_add_batch(coeffs: np.ndarray, dst: DevicePlane, jobs, tx_size, tx_type,

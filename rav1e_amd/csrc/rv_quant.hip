@@ -1,0 +1,86 @@
+// rv_quant.hip -- batched quantize / dequantize (src/quantize.rs), one
+// wavefront per transform block (rv_quant.h has the algorithm).
+#include "rv_quant.h"
+
+namespace rv {
+
+constexpr uint8_t kQTxWLog2[19] = {2, 3, 4, 5, 6, 2, 3, 3, 4, 4, 5, 5, 6, 2, 4, 3, 5, 4, 6};
+constexpr uint8_t kQTxHLog2[19] = {2, 3, 4, 5, 6, 3, 2, 4, 3, 5, 4, 6, 5, 4, 2, 5, 3, 6, 4};
+
+struct QArgs {
+  const int32_t *coeffs;
+  int cstride, n, area, coded, tx_index;  // tx_index = tx_size * 16 + tx_type
+  int qindex, bd, is_intra, dc_delta_q, ac_delta_q;
+  int32_t *qcoeffs, *rcoeffs;
+  uint32_t *eob;
+};
+
+__global__ __launch_bounds__(64) void quantize_kernel(QArgs a) {
+  const int blk = blockIdx.x;
+  if (blk >= a.n) return;
+  const QCtx c = q_ctx(a.qindex, a.area, a.is_intra, a.bd, a.dc_delta_q, a.ac_delta_q);
+  const int32_t *co = a.coeffs + (int64_t)blk * a.cstride;
+  int32_t *q = a.qcoeffs + (int64_t)blk * a.coded;
+  int32_t *r = a.rcoeffs ? a.rcoeffs + (int64_t)blk * a.coded : nullptr;
+  const int eob = quantize_block<64>(
+      c, RV_SCANS + RV_SCAN_OFF[a.tx_index], a.coded, [&](int pos) { return co[pos]; },
+      [&](int pos, int32_t qv, int32_t rv) {
+        q[pos] = qv;
+        if (r) r[pos] = rv;
+      });
+  if (a.eob && threadIdx.x == 0) a.eob[blk] = (uint32_t)eob;
+}
+
+__global__ __launch_bounds__(256) void dequantize_kernel(const int32_t *q, int total, int coded,
+                                                         int lts, int qindex, int bd,
+                                                         int dc_delta_q, int ac_delta_q,
+                                                         int32_t *r) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int32_t v = q[i];
+  const int32_t quant = (i % coded) == 0 ? q_lookup(0, qindex, dc_delta_q, bd)
+                                         : q_lookup(1, qindex, ac_delta_q, bd);
+  r[i] = wadd(wmul(v, quant), (v >> 31) & ((1 << lts) - 1)) >> lts;
+}
+
+}  // namespace rv
+
+using namespace rv;
+
+extern "C" int rv_quantize_batch(const int32_t *d_coeffs, int coeff_stride, int n, int tx_size,
+                                 int tx_type, int qindex, int bit_depth, int is_intra,
+                                 int dc_delta_q, int ac_delta_q, int32_t *d_qcoeffs,
+                                 int32_t *d_rcoeffs, uint32_t *d_eob, void *stream) {
+  if (n < 0 || tx_size < 0 || tx_size > 18 || tx_type < 0 || tx_type > 15 || qindex < 1 ||
+      qindex > 255 || (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
+      (n > 0 && (!d_coeffs || !d_qcoeffs)))
+    return rv_set_error(RV_EINVAL, "rv_quantize_batch: bad arguments");
+  const int w = 1 << kQTxWLog2[tx_size], h = 1 << kQTxHLog2[tx_size];
+  const int coded = (w < 32 ? w : 32) * (h < 32 ? h : 32);
+  if (coeff_stride < coded)
+    return rv_set_error(RV_EINVAL, "rv_quantize_batch: coeff_stride below the coded area");
+  if (n == 0) return RV_OK;
+  QArgs a{d_coeffs, coeff_stride, n, w * h, coded, tx_size * 16 + tx_type, qindex, bit_depth,
+          is_intra ? 1 : 0, dc_delta_q, ac_delta_q, d_qcoeffs, d_rcoeffs, d_eob};
+  quantize_kernel<<<n, 64, 0, rv_resolve_stream(stream)>>>(a);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+extern "C" int rv_dequantize_batch(const int32_t *d_qcoeffs, int n, int tx_size, int qindex,
+                                   int bit_depth, int dc_delta_q, int ac_delta_q,
+                                   int32_t *d_rcoeffs, void *stream) {
+  if (n < 0 || tx_size < 0 || tx_size > 18 || qindex < 1 || qindex > 255 ||
+      (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
+      (n > 0 && (!d_qcoeffs || !d_rcoeffs)))
+    return rv_set_error(RV_EINVAL, "rv_dequantize_batch: bad arguments");
+  if (n == 0) return RV_OK;
+  const int w = 1 << kQTxWLog2[tx_size], h = 1 << kQTxHLog2[tx_size];
+  const int coded = (w < 32 ? w : 32) * (h < 32 ? h : 32);
+  const int total = n * coded;
+  dequantize_kernel<<<(total + 255) / 256, 256, 0, rv_resolve_stream(stream)>>>(
+      d_qcoeffs, total, coded, q_log_tx_scale(w * h), qindex, bit_depth, dc_delta_q, ac_delta_q,
+      d_rcoeffs);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}

@@ -618,3 +618,35 @@ def test_asm_shims_match_oracle():
     want = O.inv_txfm2d_add(co // 8, d, 3, 0, 8)
     assert L.rav1e_inv_txfm_add_hip(O.ptr((co // 8).astype(np.int32)), O.ptr(d), 32, 3, 0, 8) == 0
     np.testing.assert_array_equal(d, want)
+
+
+# ---- quantize / dequantize (src/quantize.rs) ----------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("tx_size,tx_type", [(4, 0), (3, 0), (0, 0), (1, 3), (2, 9), (5, 0),
+                                              (11, 0), (17, 0), (2, 11), (3, 10)])
+def test_quantize_vs_oracle(tx_size, tx_type):
+    """rv_quantize_batch / rv_dequantize_batch vs orc_quantize /
+    orc_dequantize: levels, dequantized values and eob, bit for bit, over
+    8/10/12 bits, several qindices, intra and inter; the input is the
+    forward transform's full W*H raster as encode_tx_block hands it over."""
+    rng = np.random.default_rng(1500 + 16 * tx_size + tx_type)
+    t = R.TxSize(tx_size)
+    area, coded = t.width() * t.height(), R.coded_tx_area(tx_size)
+    for bd in (8, 10, 12):
+        for qi in (1, 40, 120, 255):
+            acq = O.lib().orc_ac_q(qi, 0, bd)
+            for is_intra in (False, True):
+                n = 12
+                c = rng.integers(-4 * acq, 4 * acq, (n, area)).astype(np.int32)
+                c[rng.random((n, area)) < 0.6] = 0
+                c[0] = 0                                    # eob = 1, all zero
+                c[1, :] = 0
+                c[1, 0] = 5 * acq                           # DC only
+                c[2] = rng.integers(-(1 << 18), 1 << 18, area)  # large values
+                q, r, eob = R.quantize_batch(c, tx_size, tx_type, qi, bd, is_intra)
+                for k in range(n):
+                    wq, weob = O.quantize(c[k], tx_size, tx_type, qi, bd, is_intra)
+                    assert int(eob[k]) == weob, (bd, qi, is_intra, k)
+                    np.testing.assert_array_equal(q[k], wq, err_msg=f"{bd} {qi} {is_intra} {k}")
+                    np.testing.assert_array_equal(r[k], O.dequantize(wq, tx_size, qi, bd))
+                np.testing.assert_array_equal(R.dequantize_batch(q, tx_size, qi, bd), r)
