@@ -9,7 +9,7 @@
  *   F1 full_search at 1/4 res (estimate_motion_ss4, src/me.rs:1023-1075)
  *   F2 diamond at 1/2 res (me_ss2, src/me.rs:470-519)
  *   F3 diamond full-pel + sub-pel at full res (src/me.rs:193-285)
- *   F4 put_8tap, diff + fht, coefficient stand-in, inverse + add,
+ *   F4 put_8tap, diff + fht, quantize + dequantize, inverse + add,
  *      cdef moments / sse (src/encoder.rs:1077-1237, src/rdo.rs:219-411)
  *   F5 8x8 SATD importance (src/api/internal.rs:823-1010)
  * It must produce the same result words as the GPU driver.
@@ -21,7 +21,7 @@
 #include "orc_common.h"
 
 #define SB 64
-#define QSTEP 8
+#define QIDX 100 /* kReplayQindex of rv_replay.hip */
 
 typedef struct {
   uint8_t *mem; /* allocation, element 0 */
@@ -36,6 +36,7 @@ typedef struct orc_replay {
   int W, H, xdec, ydec, bd, hbd, R, C;
   int w_in_b, h_in_b, tx0, ty0, tw, th, mi_w, mi_h, nsb, cw, ch, vis_w, vis_h;
   double me_lambda;
+  orc_qctx q_luma, q_chroma; /* TX_64X64 / TX_32X32, inter, qindex QIDX */
   oslot *slots;
   int threads;
   /* per frame */
@@ -123,6 +124,8 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd,
   r->cw = SB >> xdec;
   r->ch = SB >> ydec;
   r->me_lambda = 24.0 * (double)(1 << (bd - 8));
+  orc_qctx_update(&r->q_luma, QIDX, 4, 0, bd, 0, 0);
+  orc_qctx_update(&r->q_chroma, QIDX, 3, 0, bd, 0, 0);
   r->threads = threads > 0 ? threads : 1;
   r->slots = calloc(n_refs + 1, sizeof(oslot));
   int cw = (W + xdec) >> xdec, ch = (H + ydec) >> ydec;
@@ -301,7 +304,7 @@ static void run_sb(orc_replay *r, int sb, uint64_t tail[3]) {
   int best_c = 0;
   uint16_t ly[SB * SB], lu[SB * SB], lv[SB * SB];
   int16_t res[SB * SB];
-  int32_t co[SB * SB], pk[32 * 32];
+  int32_t co[SB * SB], qc[32 * 32], pk[32 * 32];
   for (int c = 0; c < r->C; c++) {
     const oslot *ref = &r->slots[1 + (c >> 1)];
     orc_mv mv = (c & 1) ? zero : smv[c >> 1];
@@ -311,14 +314,13 @@ static void run_sb(orc_replay *r, int sb, uint64_t tail[3]) {
     /* luma TX_64X64 DCT_DCT */
     orc_diff(res, at(&cur->y, hbd, px, py), cur->y.stride, ly, SB, SB, SB, hbd);
     orc_fwd_txfm2d(res, co, 4, 0, r->bd);
-    /* coefficient stand-in over the first coded_tx_area (1024) entries of
-     * the W-stride raster: what quantize and the tx-domain zip consume
-     * (src/encoder.rs:1152-1156, 1210-1219; SURVEY.md §0.6 fork quirk) */
-    for (int i = 0; i < 32 * 32; i++) {
-      int32_t q = (co[i] / QSTEP) * QSTEP;
-      pk[i] = q;
-      tail[0] += (uint64_t)(int64_t)q * (uint64_t)(i + 1);
-    }
+    /* quantize reads the first coded_tx_area (1024) entries of the
+     * W-stride raster (src/encoder.rs:1152-1170; SURVEY.md §0.6 fork
+     * quirk); dequantize feeds the inverse (:1192-1208) */
+    orc_quantize(&r->q_luma, co, qc, 4, 0);
+    for (int i = 0; i < 32 * 32; i++)
+      tail[0] += (uint64_t)(int64_t)qc[i] * (uint64_t)(i + 1);
+    orc_dequantize(QIDX, qc, pk, 4, r->bd, 0, 0);
     orc_inv_txfm2d_add(pk, ly, SB, 4, 0, r->bd, hbd);
     /* chroma TX_32X32 DCT_DCT blocks */
     uint16_t *cp[2] = {lu, lv};
@@ -330,11 +332,10 @@ static void run_sb(orc_replay *r, int sb, uint64_t tail[3]) {
           orc_diff(res, at(cs[pl], hbd, cpx + tx, cpy + ty), cs[pl]->stride, pb,
                    cwid, 32, 32, hbd);
           orc_fwd_txfm2d(res, co, 3, 0, r->bd);
-          for (int i = 0; i < 32 * 32; i++) {
-            int32_t q = (co[i] / QSTEP) * QSTEP;
-            pk[i] = q;
-            tail[0] += (uint64_t)(int64_t)q * (uint64_t)(i + 1);
-          }
+          orc_quantize(&r->q_chroma, co, qc, 3, 0);
+          for (int i = 0; i < 32 * 32; i++)
+            tail[0] += (uint64_t)(int64_t)qc[i] * (uint64_t)(i + 1);
+          orc_dequantize(QIDX, qc, pk, 3, r->bd, 0, 0);
           orc_inv_txfm2d_add(pk, pb, cwid, 3, 0, r->bd, hbd);
         }
     /* distortion: luma cdef moments (SSE part), chroma sse_wxh */

@@ -87,34 +87,52 @@ __device__ __forceinline__ QCtx q_ctx(int qindex, int area, int is_intra, int bd
 
 __device__ __forceinline__ int32_t q_signum(int32_t v) { return (v > 0) - (v < 0); }
 
-// The level of one AC coefficient under level_mode `mode`; *next = the
-// level_mode after it (src/quantize.rs:293-311).
-__device__ __forceinline__ int32_t q_ac_level(const QCtx &c, int32_t raw, int mode, int *next) {
-  const int32_t coeff = (int32_t)((uint32_t)raw << c.log_tx_scale);
-  const int32_t level0 = q_divu(coeff, c.ac_a, c.ac_b, c.ac_s);
-  const int32_t offset = level0 > 1 - mode ? c.ac_offset1 : c.ac_offset0;
-  const int32_t q = q_divu(wadd(coeff, q_signum(coeff) * offset), c.ac_a, c.ac_b, c.ac_s);
-  *next = (mode != 0 && q == 0) ? 0 : (q > 1 ? 1 : mode);
-  return q;
-}
-
-// Quantize + dequantize one block: `co(pos)` reads the forward transform's
-// coefficient at scan position pos (< n = coded_tx_area); `put(pos, q, r)`
-// receives the level (qcoeffs[pos]) and the dequantized value
+// Quantize + dequantize one block of N = coded_tx_area positions: `co(pos)`
+// reads the forward transform's coefficient at scan position pos; `put(pos,
+// q, r)` receives the level (qcoeffs[pos]) and the dequantized value
 // (rcoeffs[pos], src/quantize.rs:319-333).  Every position is written
 // exactly once, by the lane that read it (so `put` may overwrite `co`'s
 // storage in place).  All LPB lanes of the group call it; returns eob.
-template <int LPB, typename Co, typename Put>
-__device__ __forceinline__ int quantize_block(const QCtx &c, const uint16_t *scan, int n, Co co,
+//
+// divu_pair is exact truncating division (its construction, and the
+// reference's own test, src/quantize.rs:160-168), and the coefficient and
+// its rounding offset have the same sign, so with a = |coeff << scale| and
+// the offset o the loop picks (src/quantize.rs:293-311):
+//   level0 > 1 - mode   <=>  coeff > 0 and a >= (mode ? 1 : 2) * ac_quant
+//   level == 0          <=>  a + o < ac_quant
+//   level > 1           <=>  coeff > 0 and a + o >= 2 * ac_quant
+// so the level_mode transitions need comparisons only and each coefficient
+// is divided once, in the final pass.  Valid for |coefficient| < 2^28 (the
+// forward transforms stay below 2^21, tools/txbounds).
+template <int N, int LPB, typename Co, typename Put>
+__device__ __forceinline__ int quantize_block(const QCtx &c, const uint16_t *scan, Co co,
                                               Put put) {
+  constexpr int K = N >= LPB ? N / LPB : 1;  // scan indices per lane
   const int lane = threadIdx.x & (LPB - 1);
-  const int K = (n + LPB - 1) / LPB;  // scan indices per lane (n is a power of 2 >= 16)
-  const int i0 = lane * K, i1 = i0 + K < n ? i0 + K : n;
-  // 1. eob
+  const int i0 = lane * K;
+  const bool live = i0 < N;
+  const int s = c.log_tx_scale;
+  const int32_t acq = c.ac_quant, acq2 = 2 * c.ac_quant;
+  // coefficients << log_tx_scale: held in registers for up to 16 per lane,
+  // re-read from `co` per pass beyond that (register budget of the fused
+  // kernels)
+  constexpr bool kCache = K <= 16;
+  constexpr int kUnroll = kCache ? K : 2;
+  int32_t cf[kCache ? K : 1];
+  if constexpr (kCache) {
+#pragma unroll
+    for (int k = 0; k < K; k++) cf[k] = live ? (int32_t)((uint32_t)co(scan[i0 + k]) << s) : 0;
+  }
+  auto coef = [&](int k) __attribute__((always_inline)) -> int32_t {
+    if constexpr (kCache) return cf[k];
+    return live ? (int32_t)((uint32_t)co(scan[i0 + k]) << s) : 0;
+  };
+  // 1. eob: the deadzone test is on the unscaled magnitude
   int last = 0;
-  for (int i = i0; i < i1; i++) {
-    const int32_t v = co(scan[i]);
-    if (i >= 1 && (v < 0 ? wsub(0, v) : v) >= c.deadzone) last = i;
+#pragma unroll kUnroll
+  for (int k = 0; k < K; k++) {
+    const int32_t v = coef(k) >> s;
+    if (i0 + k >= 1 && (v < 0 ? -v : v) >= c.deadzone) last = i0 + k;
   }
 #pragma unroll
   for (int o = LPB / 2; o > 0; o >>= 1) {
@@ -122,47 +140,55 @@ __device__ __forceinline__ int quantize_block(const QCtx &c, const uint16_t *sca
     last = w > last ? w : last;
   }
   const int eob = last >= 1 ? last : 1;
-  // 2. this lane's transition map over scan indices [max(i0,1), min(i1, eob + 1))
-  int map = 2;  // identity: (f(0), f(1)) = (0, 1), f(s) = (map >> s) & 1
-  for (int i = i0 < 1 ? 1 : i0; i < i1 && i <= eob; i++) {
-    const int32_t raw = co(scan[i]);
-    int n0, n1;
-    q_ac_level(c, raw, 0, &n0);
-    q_ac_level(c, raw, 1, &n1);
-    const int f0 = (map >> 0) & 1, f1 = (map >> 1) & 1;  // compose: T o map
-    map = (f0 ? n1 : n0) | ((f1 ? n1 : n0) << 1);
+  // 2. this lane's transition map over its indices in [1, eob]:
+  // T(0) = [level under mode 0 > 1], T(1) = [level under mode 1 != 0]
+  int map = 2;  // identity; f(st) = (map >> st) & 1
+#pragma unroll kUnroll
+  for (int k = 0; k < K; k++) {
+    const int i = i0 + k;
+    if (i >= 1 && i <= eob) {
+      const int32_t v = coef(k), a = v < 0 ? -v : v;
+      const int32_t o0 = v > 0 && a >= acq2 ? c.ac_offset1 : c.ac_offset0;
+      const int32_t o1 = v > 0 && a >= acq ? c.ac_offset1 : c.ac_offset0;
+      const int t0 = v > 0 && a + o0 >= acq2;
+      const int t1 = a + o1 >= acq;
+      const int f0 = map & 1, f1 = (map >> 1) & 1;
+      map = (f0 ? t1 : t0) | ((f1 ? t1 : t0) << 1);
+    }
   }
-  // 3. inclusive prefix of maps in lane order (P_l = M_l o ... o M_0), then
-  // the state entering this lane's chunk = P_{l-1}(1)
+  // 3. inclusive prefix of the maps in lane order; the state entering this
+  // lane's chunk is P_{l-1}(1) (level_mode starts at 1)
   int pre = map;
 #pragma unroll
   for (int d = 1; d < LPB; d <<= 1) {
     const int other = __shfl_up(pre, d, LPB);
     if (lane >= d) {
-      const int a0 = (other >> 0) & 1, a1 = (other >> 1) & 1;  // pre o other
+      const int a0 = other & 1, a1 = (other >> 1) & 1;  // pre o other
       pre = ((pre >> a0) & 1) | (((pre >> a1) & 1) << 1);
     }
   }
-  int prev = __shfl_up(pre, 1, LPB);
+  const int prev = __shfl_up(pre, 1, LPB);
   int mode = lane == 0 ? 1 : (prev >> 1) & 1;
-  // 4. levels and dequantized values
-  const int32_t roff = (1 << c.log_tx_scale) - 1;
-  for (int i = i0; i < i1; i++) {
-    const int pos = scan[i];
+  // 4. levels (one division each) and dequantized values
+  const int32_t roff = (1 << s) - 1;
+#pragma unroll kUnroll
+  for (int k = 0; k < K; k++) {
+    const int i = i0 + k;
+    if (!live) break;
+    const int32_t v = coef(k);
     int32_t q;
     if (i == 0) {
-      int32_t dc = (int32_t)((uint32_t)co(0) << c.log_tx_scale);
-      dc = wadd(dc, q_signum(dc) * c.dc_offset);
-      q = q_divu(dc, c.dc_a, c.dc_b, c.dc_s);
+      q = q_divu(wadd(v, q_signum(v) * c.dc_offset), c.dc_a, c.dc_b, c.dc_s);
     } else if (i <= eob) {
-      int nx;
-      q = q_ac_level(c, co(pos), mode, &nx);
-      mode = nx;
+      const int32_t a = v < 0 ? -v : v;
+      const int32_t o = v > 0 && a >= (mode ? acq : acq2) ? c.ac_offset1 : c.ac_offset0;
+      q = q_divu(wadd(v, q_signum(v) * o), c.ac_a, c.ac_b, c.ac_s);
+      mode = (mode != 0 && q == 0) ? 0 : (q > 1 ? 1 : mode);
     } else {
       q = 0;
     }
-    const int32_t r = wadd(wmul(q, i == 0 ? c.dc_quant : c.ac_quant), (q >> 31) & roff) >> c.log_tx_scale;
-    put(pos, q, r);
+    const int32_t r = wadd(wmul(q, i == 0 ? c.dc_quant : c.ac_quant), (q >> 31) & roff) >> s;
+    put(scan[i], q, r);
   }
   return eob;
 }

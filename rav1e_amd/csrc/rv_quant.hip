@@ -1,6 +1,7 @@
 // rv_quant.hip -- batched quantize / dequantize (src/quantize.rs), one
 // wavefront per transform block (rv_quant.h has the algorithm).
 #include "rv_quant.h"
+#include "rv_rdo.h"
 
 namespace rv {
 
@@ -15,6 +16,7 @@ struct QArgs {
   uint32_t *eob;
 };
 
+template <int N>
 __global__ __launch_bounds__(64) void quantize_kernel(QArgs a) {
   const int blk = blockIdx.x;
   if (blk >= a.n) return;
@@ -22,8 +24,8 @@ __global__ __launch_bounds__(64) void quantize_kernel(QArgs a) {
   const int32_t *co = a.coeffs + (int64_t)blk * a.cstride;
   int32_t *q = a.qcoeffs + (int64_t)blk * a.coded;
   int32_t *r = a.rcoeffs ? a.rcoeffs + (int64_t)blk * a.coded : nullptr;
-  const int eob = quantize_block<64>(
-      c, RV_SCANS + RV_SCAN_OFF[a.tx_index], a.coded, [&](int pos) { return co[pos]; },
+  const int eob = quantize_block<N, 64>(
+      c, RV_SCANS + RV_SCAN_OFF[a.tx_index], [&](int pos) { return co[pos]; },
       [&](int pos, int32_t qv, int32_t rv) {
         q[pos] = qv;
         if (r) r[pos] = rv;
@@ -43,9 +45,25 @@ __global__ __launch_bounds__(256) void dequantize_kernel(const int32_t *q, int t
   r[i] = wadd(wmul(v, quant), (v >> 31) & ((1 << lts) - 1)) >> lts;
 }
 
+__global__ void q_ctx_kernel(int qindex, int area, int is_intra, int bd, int dc_delta_q,
+                             int ac_delta_q, QCtx *out) {
+  *out = q_ctx(qindex, area, is_intra, bd, dc_delta_q, ac_delta_q);
+}
+
 }  // namespace rv
 
 using namespace rv;
+
+int rv_quant_ctx(int qindex, int tx_area, int is_intra, int bit_depth, int dc_delta_q,
+                 int ac_delta_q, QCtx *out) {
+  QCtx *d = nullptr;
+  if (hipMalloc((void **)&d, sizeof(QCtx)) != hipSuccess)
+    return rv_set_error(RV_EHIP, "rv_quant_ctx: alloc");
+  q_ctx_kernel<<<1, 1>>>(qindex, tx_area, is_intra, bit_depth, dc_delta_q, ac_delta_q, d);
+  const bool ok = hipMemcpy(out, d, sizeof(QCtx), hipMemcpyDeviceToHost) == hipSuccess;
+  hipFree(d);
+  return ok ? RV_OK : rv_set_error(RV_EHIP, "rv_quant_ctx");
+}
 
 extern "C" int rv_quantize_batch(const int32_t *d_coeffs, int coeff_stride, int n, int tx_size,
                                  int tx_type, int qindex, int bit_depth, int is_intra,
@@ -62,7 +80,17 @@ extern "C" int rv_quantize_batch(const int32_t *d_coeffs, int coeff_stride, int 
   if (n == 0) return RV_OK;
   QArgs a{d_coeffs, coeff_stride, n, w * h, coded, tx_size * 16 + tx_type, qindex, bit_depth,
           is_intra ? 1 : 0, dc_delta_q, ac_delta_q, d_qcoeffs, d_rcoeffs, d_eob};
-  quantize_kernel<<<n, 64, 0, rv_resolve_stream(stream)>>>(a);
+  hipStream_t st = rv_resolve_stream(stream);
+  switch (coded) {  // coded areas of the 19 TxSizes: 16 .. 1024
+#define RV_QCASE(N) \
+  case N:           \
+    quantize_kernel<N><<<n, 64, 0, st>>>(a); \
+    break;
+    RV_QCASE(16) RV_QCASE(32) RV_QCASE(64) RV_QCASE(128) RV_QCASE(256) RV_QCASE(512) RV_QCASE(1024)
+#undef RV_QCASE
+    default:
+      return rv_set_error(RV_EINVAL, "rv_quantize_batch: coded area");
+  }
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

@@ -3,6 +3,7 @@
 #pragma once
 
 #include "rv_device.h"
+#include "rv_quant.h"
 
 namespace rv {
 
@@ -26,9 +27,16 @@ struct RdoArgs {
   int bd;
   int mb_w, mb_h;     // MC block size (filter choice, distortion grid)
   int sub_w, sub_h;   // distortion sub-block (SSE); moments use 8x8
+  QCtx q;             // QuantizationContext of this plane type's transform
+  int q_tx_index;     // tx_size * 16 + tx_type: av1_scan_orders entry
 };
 
 }  // namespace rv
+
+// QuantizationContext::update (src/quantize.rs:205-253) evaluated on the
+// device (the lookups live there), for the replay's launch arguments.
+int rv_quant_ctx(int qindex, int tx_area, int is_intra, int bit_depth, int dc_delta_q,
+                 int ac_delta_q, rv::QCtx *out);
 
 // Luma candidates (64x64 transform, cdef moments) and the chroma transform
 // blocks of planes U and V (32x32, SSE partials) in one launch.

@@ -8,9 +8,10 @@
 //   src/predict.rs:255-338)            -> prediction in LDS
 //   diff (src/encoder.rs:1044-1058) + FwdTxfm2D::fht DCT_DCT
 //   (src/transform/forward.rs:1804-1899) -> coefficients in LDS
-//   quantize/dequantize stand-in (v / 8 * 8 on the first
-//   coded_tx_area entries of the W-stride raster, the slice quantize reads)
-//                                      -> packed coefficients to HBM
+//   quantize (src/quantize.rs:255-316, QuantizationContext at the
+//   replay's qindex) on the first coded_tx_area entries of the W-stride
+//   raster, the slice encode_tx_block hands it   -> levels to HBM
+//   dequantize (src/quantize.rs:319-333)      -> the inverse's input in LDS
 //   inv_txfm2d_add (src/transform/inverse.rs:1939-2114)
 //                                      -> reconstruction in LDS + HBM
 //   cdef_dist_wxh_8x8 moments (src/rdo.rs:219-241, luma) or sse_wxh
@@ -32,7 +33,6 @@
 
 namespace rv {
 
-constexpr int kQstep = 8;  // quantize/dequantize stand-in
 
 // SUBPEL_FILTERS REGULAR (src/mc.rs:70-179): [0] 8-tap, [1] 4-tap (get_filter
 // for length <= 4, src/mc.rs:201-210).  Frac 0 is never filtered.
@@ -225,10 +225,9 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     for (int r = 0; r < N; r++) buf[r * S + lane] = rdo_rsa(v[r], -s1);
   }
   wave_sync();
-  // The stand-in consumes the first coded_tx_area = C32 * C32 entries of
-  // the W-stride raster -- what quantize and the tx-domain zip read
-  // (src/encoder.rs:1152-1156, 1210-1219): for 64x64 that is raster rows
-  // 0..15, so only those rows need the row pass.
+  // quantize reads the first coded_tx_area = C32 * C32 entries of the
+  // W-stride raster (src/encoder.rs:1152-1170): for 64x64 that is raster
+  // rows 0..15, so only those rows need the row pass.
   constexpr int CA = C32 * C32, RR = CA / N;  // coded area, raster rows it spans
   if (lane < RR) {
     int32_t v[N];
@@ -236,17 +235,22 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     for (int c = 0; c < N; c++) v[c] = buf[lane * S + c];
     tx::fwd1d<1, N>(v, v);
 #pragma unroll
-    for (int c = 0; c < N; c++) buf[lane * S + c] = (rdo_rsa(v[c], -s2) / kQstep) * kQstep;
+    for (int c = 0; c < N; c++) buf[lane * S + c] = rdo_rsa(v[c], -s2);
   }
   wave_sync();
-  // packed coefficients = raster entries 0..CA-1 (row stride min(W,32) for
-  // inverse_transform_add), coalesced
+  // quantize (levels -> HBM, the entropy coder's input) + dequantize in
+  // place (the inverse transform's input, raster entry i = packed entry i)
   {
     int32_t *pk = pl.packed + (int64_t)t * CA;
-    if (valid)
-#pragma unroll 4
-      for (int i = lane; i < CA; i += LPB) pk[i] = buf[(i / N) * S + (i % N)];
+    quantize_block<CA, LPB>(
+        a.q, RV_SCANS + RV_SCAN_OFF[a.q_tx_index],
+        [&](int pos) { return buf[(pos / N) * S + (pos % N)]; },
+        [&](int pos, int32_t q, int32_t r) {
+          if (valid) pk[pos] = q;
+          buf[(pos / N) * S + (pos % N)] = r;
+        });
   }
+  wave_sync();
   // ---- D. inverse: rows of the coded coefficients, then columns + add ------
   // input row rr of the C32 x C32 block = packed[rr * C32 ..] = raster
   // entries rr * C32 ..; all reads precede the in-place row writes
@@ -355,14 +359,14 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
 //    staged in turn;
 //  * the residual is formed per column straight from the source plane and
 //    the LDS prediction, and only column-DCT outputs 0..15 are kept: the
-//    stand-in reads raster rows 0..15 of the 64x64 fht output
+//    quantizer reads raster rows 0..15 of the 64x64 fht output
 //    (src/encoder.rs:1152-1156), and row r of that raster is the row DCT of
 //    column-pass row r, so the compiler drops the other 48 outputs;
 //  * the inverse row pass stores round_shift(., INTERMEDIATE_SHIFT) clamped
 //    to the column range max(bd + 6, 16) (inverse.rs:2075-2098): i16 up to
 //    10 bits (Mid), i32 for 12.
 // Phases: luma_front (MC, residual, column DCT -> fmid), luma_fwd_row (row
-// DCT + stand-in of one raster row, one lane per row), luma_inv_row_load /
+// DCT of one raster row, one lane per row), luma_quantize, luma_inv_row_load /
 // _tx (one lane per coded row), luma_back (inverse columns, reconstruction,
 // cdef moments).
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
@@ -515,8 +519,7 @@ __device__ __forceinline__ void luma_front(const RdoArgs &a, const RdoPlane &pl,
   }
 }
 
-// Row DCT + quantize stand-in of one fmid row (raster row r of the 64x64
-// fht output), in place.
+// Row DCT of one fmid row (raster row r of the 64x64 fht output), in place.
 __device__ __forceinline__ void luma_fwd_row(int32_t *row, int bd) {
   int s0, s1, s2;
   fwd_shifts<64>((bd - 8) / 2, s0, s1, s2);
@@ -525,7 +528,23 @@ __device__ __forceinline__ void luma_fwd_row(int32_t *row, int bd) {
   for (int c = 0; c < 64; c++) v[c] = row[c];
   tx::fwd1d<1, 64>(v, v);
 #pragma unroll
-  for (int c = 0; c < 64; c++) row[c] = (rdo_rsa(v[c], -s2) / kQstep) * kQstep;
+  for (int c = 0; c < 64; c++) row[c] = rdo_rsa(v[c], -s2);
+}
+
+// quantize + dequantize of the candidate's coded 32x32 area (raster entries
+// 0..1023 of the 64x64 fht output = fmid rows 0..15, src/encoder.rs:1170,
+// 1192): levels -> pl.packed (the entropy coder's input), dequantized
+// values in place (the inverse transform's input).
+__device__ __forceinline__ void luma_quantize(const RdoArgs &a, const RdoPlane &pl, int t,
+                                              int32_t *fmid) {
+  int32_t *pk = pl.packed + (int64_t)t * 1024;
+  quantize_block<1024, 64>(
+      a.q, RV_SCANS + RV_SCAN_OFF[a.q_tx_index],
+      [&](int pos) { return fmid[(pos >> 6) * 65 + (pos & 63)]; },
+      [&](int pos, int32_t q, int32_t r) {
+        pk[pos] = q;
+        fmid[(pos >> 6) * 65 + (pos & 63)] = r;
+      });
 }
 
 // Inverse row rr (0..31) of the coded 32x32 block: packed[rr * 32 ..] =
@@ -628,12 +647,8 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
   int32_t *fmid = reinterpret_cast<int32_t *>(scr);
   if (lane < 16) luma_fwd_row(fmid + lane * 65, a.bd);
   wave_sync();
-  // packed coefficients = raster entries 0..1023 (row stride 32), coalesced
-  {
-    int32_t *pk = pl.packed + (int64_t)t * 1024;
-#pragma unroll 4
-    for (int i = lane; i < 1024; i += 64) pk[i] = fmid[(i >> 6) * 65 + (i & 63)];
-  }
+  luma_quantize(a, pl, t, fmid);
+  wave_sync();
   const int range = a.bd + 8, crange = a.bd + 6 > 16 ? a.bd + 6 : 16;
   Mid *imid = reinterpret_cast<Mid *>(scr);  // [32][66]
   {
@@ -745,14 +760,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     if (t0 + q < luma.n_tx) luma_fwd_row(fmid(q) + (lane & 15) * 65, luma.bd);
   }
   __syncthreads();
+  if (valid) luma_quantize(luma, luma.p[0], rdo_task(luma, t0 + wave), fmid(wave));
+  __syncthreads();
   if (wave < 2) {  // inverse rows: lane = 32 * (candidate & 1) + coded row
     const int q = 2 * wave + (lane >> 5), rr = lane & 31;
     const bool vq = t0 + q < luma.n_tx;
     const int range = luma.bd + 8, crange = luma.bd + 6 > 16 ? luma.bd + 6 : 16;
     int32_t v[64];
-    if (vq)
-      luma_inv_row_load(fmid(q), rr, v, range,
-                        luma.p[0].packed + (int64_t)rdo_task(luma, t0 + q) * 1024 + rr * 32);
+    if (vq) luma_inv_row_load(fmid(q), rr, v, range, nullptr);
     wave_sync();  // the wavefront's fmid reads precede its imid writes (same bytes)
     if (vq) luma_inv_row_tx(v, imid(q) + rr * 66, range, crange);
   }

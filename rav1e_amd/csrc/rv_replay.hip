@@ -11,7 +11,7 @@
 //       (motion_estimation, src/me.rs:193-285)
 //   F4  RDO candidates per superblock: {sub-pel MV, zero MV} x reference:
 //       put_8tap luma + chroma, diff + forward DCT (TX_64X64 luma,
-//       TX_32X32 chroma), coefficient stand-in for quantize/dequantize,
+//       TX_32X32 chroma), quantize + dequantize at qindex kReplayQindex,
 //       inverse transform + add, cdef-moment luma / SSE chroma distortion,
 //       argmin (encode_tx_block src/encoder.rs:1077-1237,
 //       compute_distortion src/rdo.rs:338-411)
@@ -50,6 +50,10 @@ int rv_plane_pyramid(const rv_plane *y, const rv_plane *h, const rv_plane *q, vo
 namespace rv {
 
 constexpr int kSb = 64;
+// base_q_idx of the replay's frames: rav1e's default --quantizer (100) used
+// directly as the qindex; the rate controller that would vary it per frame
+// type is out of scope.  oracle/orc_replay.c uses the same value.
+constexpr int kReplayQindex = 100;
 
 struct Geo {
   int W, H, xdec, ydec, bd, hbd;
@@ -205,6 +209,7 @@ struct rv_replay {
   bool own_stream;
   bool sea;  // successive-elimination coarse search (bit depth <= 10)
   double me_lambda;
+  QCtx q_luma, q_chroma;  // QuantizationContext, TX_64X64 / TX_32X32 inter
   std::vector<RvFrameSlot> slots;  // 0 = input, 1..R = references
   // scratch
   rv_plane tall_y, tall_u, tall_v;
@@ -486,6 +491,14 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   // me_lambda = sqrt(lambda), lambda scaled by 1 << 2 (bd - 8)
   // (src/encoder.rs:876-878); the replay fixes the 8-bit value.
   r->me_lambda = 24.0 * (double)(1 << (g.bd - 8));
+  // quantizer of every RDO candidate: base_q_idx kReplayQindex with no
+  // per-plane deltas, inter (QuantizationContext::update calls of
+  // write_tx_tree, src/encoder.rs:1925-1931, 1987-1994)
+  if (rv_quant_ctx(kReplayQindex, 64 * 64, 0, g.bd, 0, 0, &r->q_luma) != RV_OK ||
+      rv_quant_ctx(kReplayQindex, 32 * 32, 0, g.bd, 0, 0, &r->q_chroma) != RV_OK) {
+    delete r;
+    return nullptr;
+  }
   // 8x8 sums of 10-bit pixels fit the u16 box-sum table; 12-bit searches
   // exhaustively
   r->sea = g.bd <= 10 && (cfg->flags & RV_REPLAY_EXHAUSTIVE_FS) == 0;
@@ -658,7 +671,11 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
     la.bd = g.bd;
     la.mb_w = la.mb_h = kSb;
     la.sub_w = la.sub_h = 8;
+    la.q = r->q_luma;
+    la.q_tx_index = 4 * 16 + 0;  // TX_64X64, DCT_DCT
     ca = la;
+    ca.q = r->q_chroma;
+    ca.q_tx_index = 3 * 16 + 0;  // TX_32X32, DCT_DCT
     const rv_plane *cp[2] = {&cur.u, &cur.v};
     const rv_plane *tp[2] = {&r->tall_u, &r->tall_v};
     uint64_t *cs[2] = {r->u_sse, r->v_sse};
