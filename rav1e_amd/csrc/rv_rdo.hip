@@ -79,7 +79,8 @@ __device__ __forceinline__ int32_t rdo_rsa(int32_t v, int bit) {
 // it recomputes its partner's block and stores nothing.
 template <typename Px, int N, bool MOMENTS, int LPB>
 __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &pl, int t,
-                                              bool valid, int32_t *buf, Px *pred) {
+                                              bool valid, int32_t *buf, Px *pred,
+                                              const uint16_t *scan) {
   constexpr int B = (int)sizeof(Px);
   constexpr int S = N + 1;                       // padded LDS row (i32)
   constexpr int G = LPB / N, RG = N / G;         // MC lane groups
@@ -243,7 +244,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   {
     int32_t *pk = pl.packed + (int64_t)t * CA;
     quantize_block<CA, LPB>(
-        a.q, RV_SCANS + RV_SCAN_OFF[a.q_tx_index],
+        a.q, scan,
         [&](int pos) { return buf[(pos / N) * S + (pos % N)]; },
         [&](int pos, int32_t q, int32_t r) {
           if (valid) pk[pos] = q;
@@ -536,10 +537,10 @@ __device__ __forceinline__ void luma_fwd_row(int32_t *row, int bd) {
 // 1192): levels -> pl.packed (the entropy coder's input), dequantized
 // values in place (the inverse transform's input).
 __device__ __forceinline__ void luma_quantize(const RdoArgs &a, const RdoPlane &pl, int t,
-                                              int32_t *fmid) {
+                                              int32_t *fmid, const uint16_t *scan) {
   int32_t *pk = pl.packed + (int64_t)t * 1024;
   quantize_block<1024, 64>(
-      a.q, RV_SCANS + RV_SCAN_OFF[a.q_tx_index],
+      a.q, scan,
       [&](int pos) { return fmid[(pos >> 6) * 65 + (pos & 63)]; },
       [&](int pos, int32_t q, int32_t r) {
         pk[pos] = q;
@@ -640,14 +641,14 @@ __device__ __forceinline__ void luma_back(const RdoArgs &a, const RdoPlane &pl, 
 // One luma candidate per wavefront (12-bit, and the split-stream option).
 template <typename Px, typename Mid, int NPART>
 __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &pl, int t,
-                                              uint8_t *scr, Px *pred) {
+                                              uint8_t *scr, Px *pred, const uint16_t *scan) {
   const int lane = threadIdx.x & 63;
   luma_front<Px, NPART>(a, pl, t, scr, pred);
   wave_sync();
   int32_t *fmid = reinterpret_cast<int32_t *>(scr);
   if (lane < 16) luma_fwd_row(fmid + lane * 65, a.bd);
   wave_sync();
-  luma_quantize(a, pl, t, fmid);
+  luma_quantize(a, pl, t, fmid, scan);
   wave_sync();
   const int range = a.bd + 8, crange = a.bd + 6 > 16 ? a.bd + 6 : 16;
   Mid *imid = reinterpret_cast<Mid *>(scr);  // [32][66]
@@ -679,7 +680,7 @@ __device__ __forceinline__ int rdo_task(const RdoArgs &a, int i) {
 // carry chroma transform blocks two per wavefront, plane U then V.
 template <typename Px>
 __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, int32_t *buf,
-                                                Px *pred) {
+                                                Px *pred, const uint16_t *scan) {
   const int pairs = (chroma.n_tx + 1) / 2;
   const int plane = b / pairs;
   const int half = (threadIdx.x & 63) >> 5;
@@ -687,7 +688,15 @@ __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, in
   const bool valid = i < chroma.n_tx;
   if (!valid) i -= 1;
   rdo_cand_body<Px, 32, false, 32>(chroma, chroma.p[plane], rdo_task(chroma, i), valid,
-                                   buf + half * 32 * 33, pred + half * 32 * 32);
+                                   buf + half * 32 * 33, pred + half * 32 * 32, scan);
+}
+
+// The quantizer's scan (coded area <= 1024) staged in LDS for the
+// workgroup; ends with a barrier.
+__device__ __forceinline__ void stage_scan(uint16_t *dst, int tx_index) {
+  const uint16_t *src = RV_SCANS + RV_SCAN_OFF[tx_index];
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
 }
 
 // One luma candidate or one chroma pair per 64-thread workgroup: the
@@ -703,13 +712,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void rd
   using L = SingleLds<Px>;
   using Mid = typename std::conditional<sizeof(Px) == 1, int16_t, int32_t>::type;
   __shared__ __align__(16) uint8_t lds[cmax(L::kSlot, kChromaPair(sizeof(Px)))];
+  __shared__ uint16_t scan[1024];
   const int b = blockIdx.x;
+  stage_scan(scan, b < luma.n_tx ? luma.q_tx_index : chroma.q_tx_index);
   if (b < luma.n_tx)
     rdo_luma_body<Px, Mid, 2>(luma, luma.p[0], rdo_task(luma, b), lds,
-                              reinterpret_cast<Px *>(lds + L::kScr));
+                              reinterpret_cast<Px *>(lds + L::kScr), scan);
   else
     rdo_chroma_pair<Px>(chroma, b - luma.n_tx, reinterpret_cast<int32_t *>(lds),
-                        reinterpret_cast<Px *>(lds + 2 * 32 * 33 * 4));
+                        reinterpret_cast<Px *>(lds + 2 * 32 * 33 * 4), scan);
 }
 
 // 8- and 10-bit: 256-thread workgroups.  Blocks [0, nquads) carry four luma
@@ -731,14 +742,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
   using L = typename QuadLds<Px>::L;
   constexpr int NPART = sizeof(Px) == 1 ? 2 : 4;
   __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
+  __shared__ uint16_t scan[1024];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int b = blockIdx.x;
+  stage_scan(scan, b >= nquads ? chroma.q_tx_index : luma.q_tx_index);
   if (b >= nquads) {  // chroma pairs: wave-local, no workgroup barriers
     const int pair = 3 * (b - nquads) + wave;
     if (wave == 3 || pair >= 2 * ((chroma.n_tx + 1) / 2)) return;
     uint8_t *w = lds + wave * kChromaPair(sizeof(Px));
     rdo_chroma_pair<Px>(chroma, pair, reinterpret_cast<int32_t *>(w),
-                        reinterpret_cast<Px *>(w + 2 * 32 * 33 * 4));
+                        reinterpret_cast<Px *>(w + 2 * 32 * 33 * 4), scan);
     return;
   }
   auto slot = [&](int q) __attribute__((always_inline)) { return lds + q * L::kSlot; };
@@ -760,7 +773,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     if (t0 + q < luma.n_tx) luma_fwd_row(fmid(q) + (lane & 15) * 65, luma.bd);
   }
   __syncthreads();
-  if (valid) luma_quantize(luma, luma.p[0], rdo_task(luma, t0 + wave), fmid(wave));
+  if (valid) luma_quantize(luma, luma.p[0], rdo_task(luma, t0 + wave), fmid(wave), scan);
   __syncthreads();
   if (wave < 2) {  // inverse rows: lane = 32 * (candidate & 1) + coded row
     const int q = 2 * wave + (lane >> 5), rr = lane & 31;
@@ -781,7 +794,9 @@ template <typename Px>
 __global__ __launch_bounds__(64) void rdo_chroma_kernel(RdoArgs chroma) {
   __shared__ int32_t buf[2 * 32 * 33];
   __shared__ Px pred[2 * 32 * 32];
-  rdo_chroma_pair<Px>(chroma, blockIdx.x, buf, pred);
+  __shared__ uint16_t scan[1024];
+  stage_scan(scan, chroma.q_tx_index);
+  rdo_chroma_pair<Px>(chroma, blockIdx.x, buf, pred, scan);
 }
 
 }  // namespace rv
