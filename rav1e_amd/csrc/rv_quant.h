@@ -7,16 +7,16 @@
 // loop whose rounding offset depends on a 2-state `level_mode` carried from
 // coefficient to coefficient.  Here every lane takes a contiguous chunk of
 // scan indices:
-//   1. eob = the last scan index >= 1 whose |coeff| reaches the deadzone
-//      (a max over the lanes);
+//   1. eob = the last scan index >= 1 whose |coeff| reaches the deadzone:
+//      the value held by the highest lane with one (a ballot);
 //   2. each lane composes, over its chunk, the state transition the loop
 //      applies from level_mode 0 and from level_mode 1 -- a map {0,1} ->
-//      {0,1} in two bits;
-//   3. an exclusive prefix composition of the lanes' maps (log2(LPB)
-//      shuffle steps, starting from level_mode = 1) gives every lane the
-//      level_mode entering its chunk;
+//      {0,1}, always the identity or a constant;
+//   3. the level_mode entering a lane's chunk is the constant of the last
+//      constant map below it (two ballots), else the initial 1;
 //   4. each lane re-runs its chunk from that state and writes the levels.
 // The result is the reference's sequential loop, position for position.
+// Every lane of the wavefront calls it together (ballots are wave-wide).
 #pragma once
 
 #include "rv_device.h"
@@ -134,15 +134,18 @@ __device__ __forceinline__ int quantize_block(const QCtx &c, const uint16_t *sca
     const int32_t v = coef(k) >> s;
     if (i0 + k >= 1 && (v < 0 ? -v : v) >= c.deadzone) last = i0 + k;
   }
-#pragma unroll
-  for (int o = LPB / 2; o > 0; o >>= 1) {
-    const int w = __shfl_xor(last, o, LPB);
-    last = w > last ? w : last;
-  }
-  const int eob = last >= 1 ? last : 1;
+  // lanes of this group in the wavefront's 64-bit masks
+  const int wl = threadIdx.x & 63;
+  const uint64_t gmask = LPB == 64 ? ~0ull : (0xFFFFFFFFull << (wl & 32));
+  const uint64_t sig = __ballot(last >= 1) & gmask;
+  // chunks ascend with the lane, so the highest lane holding a significant
+  // coefficient holds the eob
+  const int eob = sig ? __shfl(last, 63 - __builtin_clzll(sig), 64) : 1;
   // 2. this lane's transition map over its indices in [1, eob]:
-  // T(0) = [level under mode 0 > 1], T(1) = [level under mode 1 != 0]
-  int map = 2;  // identity; f(st) = (map >> st) & 1
+  // T(0) = [level under mode 0 > 1], T(1) = [level under mode 1 != 0].
+  // T(0) <= T(1) always (mode 1 never picks the smaller offset), so every
+  // map and composition is the identity (2), constant 0 (0) or constant 1 (3).
+  int map = 2;  // f(st) = (map >> st) & 1
 #pragma unroll kUnroll
   for (int k = 0; k < K; k++) {
     const int i = i0 + k;
@@ -156,19 +159,12 @@ __device__ __forceinline__ int quantize_block(const QCtx &c, const uint16_t *sca
       map = (f0 ? t1 : t0) | ((f1 ? t1 : t0) << 1);
     }
   }
-  // 3. inclusive prefix of the maps in lane order; the state entering this
-  // lane's chunk is P_{l-1}(1) (level_mode starts at 1)
-  int pre = map;
-#pragma unroll
-  for (int d = 1; d < LPB; d <<= 1) {
-    const int other = __shfl_up(pre, d, LPB);
-    if (lane >= d) {
-      const int a0 = other & 1, a1 = (other >> 1) & 1;  // pre o other
-      pre = ((pre >> a0) & 1) | (((pre >> a1) & 1) << 1);
-    }
-  }
-  const int prev = __shfl_up(pre, 1, LPB);
-  int mode = lane == 0 ? 1 : (prev >> 1) & 1;
+  // 3. the level_mode entering this lane's chunk: the constant of the last
+  // non-identity map below this lane in the group, else the initial 1
+  const uint64_t nonid = __ballot(map != 2) & gmask;
+  const uint64_t ones = __ballot(map == 3) & gmask;
+  const uint64_t below = nonid & ((1ull << wl) - 1);
+  int mode = below ? (int)((ones >> (63 - __builtin_clzll(below))) & 1) : 1;
   // 4. levels (one division each) and dequantized values
   const int32_t roff = (1 << s) - 1;
 #pragma unroll kUnroll
@@ -191,6 +187,12 @@ __device__ __forceinline__ int quantize_block(const QCtx &c, const uint16_t *sca
     put(scan[i], q, r);
   }
   return eob;
+}
+
+// dequantize (src/quantize.rs:319-333) of the level at raster index i
+__device__ __forceinline__ int32_t q_dequant(const QCtx &c, int32_t q, int i) {
+  return wadd(wmul(q, i == 0 ? c.dc_quant : c.ac_quant), (q >> 31) & ((1 << c.log_tx_scale) - 1)) >>
+         c.log_tx_scale;
 }
 
 }  // namespace rv

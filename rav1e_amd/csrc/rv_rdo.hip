@@ -241,15 +241,21 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   wave_sync();
   // quantize (levels -> HBM, the entropy coder's input) + dequantize in
   // place (the inverse transform's input, raster entry i = packed entry i)
+  // Levels go back in place (scattered LDS writes); then one coalesced
+  // pass stores them to HBM and dequantizes them in place.
+  quantize_block<CA, LPB>(
+      a.q, scan, [&](int pos) { return buf[(pos / N) * S + (pos % N)]; },
+      [&](int pos, int32_t q, int32_t) { buf[(pos / N) * S + (pos % N)] = q; });
+  wave_sync();
   {
     int32_t *pk = pl.packed + (int64_t)t * CA;
-    quantize_block<CA, LPB>(
-        a.q, scan,
-        [&](int pos) { return buf[(pos / N) * S + (pos % N)]; },
-        [&](int pos, int32_t q, int32_t r) {
-          if (valid) pk[pos] = q;
-          buf[(pos / N) * S + (pos % N)] = r;
-        });
+#pragma unroll 4
+    for (int i = lane; i < CA; i += LPB) {
+      int32_t *e = buf + (i / N) * S + (i % N);
+      const int32_t q = *e;
+      if (valid) pk[i] = q;
+      *e = q_dequant(a.q, q, i);
+    }
   }
   wave_sync();
   // ---- D. inverse: rows of the coded coefficients, then columns + add ------
@@ -538,14 +544,20 @@ __device__ __forceinline__ void luma_fwd_row(int32_t *row, int bd) {
 // values in place (the inverse transform's input).
 __device__ __forceinline__ void luma_quantize(const RdoArgs &a, const RdoPlane &pl, int t,
                                               int32_t *fmid, const uint16_t *scan) {
-  int32_t *pk = pl.packed + (int64_t)t * 1024;
   quantize_block<1024, 64>(
-      a.q, scan,
-      [&](int pos) { return fmid[(pos >> 6) * 65 + (pos & 63)]; },
-      [&](int pos, int32_t q, int32_t r) {
-        pk[pos] = q;
-        fmid[(pos >> 6) * 65 + (pos & 63)] = r;
-      });
+      a.q, scan, [&](int pos) { return fmid[(pos >> 6) * 65 + (pos & 63)]; },
+      [&](int pos, int32_t q, int32_t) { fmid[(pos >> 6) * 65 + (pos & 63)] = q; });
+  wave_sync();
+  // levels to HBM (coalesced), dequantized in place
+  int32_t *pk = pl.packed + (int64_t)t * 1024;
+  const int lane = threadIdx.x & 63;
+#pragma unroll 4
+  for (int i = lane; i < 1024; i += 64) {
+    int32_t *e = fmid + (i >> 6) * 65 + (i & 63);
+    const int32_t q = *e;
+    pk[i] = q;
+    *e = q_dequant(a.q, q, i);
+  }
 }
 
 // Inverse row rr (0..31) of the coded 32x32 block: packed[rr * 32 ..] =
