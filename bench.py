@@ -80,8 +80,8 @@ ROCPROF_NAMES = {
     "full_search_exhaustive": "fs16_kernel<{px}>",
     "diamond_fullpel_64": "ds_fast_kernel<{px}, 64, 64, false>",
     "diamond_subpel_64": "ds_fast_kernel<{px}, 64, 64, true>",
-    "rdo_candidates": "rdo_frame_kernel<{px}>",
-    "rdo_candidates_zero_mv": "rdo_frame_kernel<{px}>",
+    "rdo_candidates": "rdo_quad_kernel<{px}>",
+    "rdo_candidates_zero_mv": "rdo_quad_kernel<{px}>",
 }
 
 

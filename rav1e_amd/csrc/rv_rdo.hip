@@ -24,6 +24,7 @@
 // rv_inv_txfm_add_batch, rv_cdef_moments_batch, rv_sse_batch) compute the
 // same values one stage per launch; the replay parity test pins the fused
 // kernel to the CPU replay, which chains the oracle's restatements of them.
+#include <stdlib.h>
 #include <string.h>
 
 #include <type_traits>
@@ -838,7 +839,22 @@ int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipSt
     RV_HIP_CHECK_LAUNCH();
     return RV_OK;
   }
-  if (luma.bd == 12) {  // i32 row-pass intermediate: one candidate per workgroup
+  // RAV1E_HIP_RDO_SINGLE=1: one candidate per workgroup at every bit depth
+  static const bool single = [] {
+    const char *e = getenv("RAV1E_HIP_RDO_SINGLE");
+    return e && e[0] == '1';
+  }();
+  if (luma.bd == 12 || single) {  // 12-bit: i32 row-pass intermediate
+    const unsigned grid = (unsigned)luma.n_tx + cpairs;
+    if (grid == 0) return RV_OK;
+    if (hbd)
+      rdo_frame_kernel<uint16_t><<<grid, 64, 0, s>>>(luma, chroma);
+    else
+      rdo_frame_kernel<uint8_t><<<grid, 64, 0, s>>>(luma, chroma);
+    RV_HIP_CHECK_LAUNCH();
+    return RV_OK;
+  }
+  if (false) {
     const unsigned grid = (unsigned)luma.n_tx + cpairs;
     if (grid == 0) return RV_OK;
     rdo_frame_kernel<uint16_t><<<grid, 64, 0, s>>>(luma, chroma);
