@@ -358,7 +358,7 @@ int rv_telescopic_subpel_batch(const rv_plane *org, const rv_plane *ref,
 typedef struct rv_replay_cfg {
   int32_t width, height;      /* luma, visible */
   int32_t xdec, ydec;         /* chroma subsampling (1,1 = 4:2:0) */
-  int32_t bit_depth;          /* 8 or 10 */
+  int32_t bit_depth;          /* 8, 10 or 12 (12: exhaustive full search) */
   int32_t tile_x0, tile_y0;   /* tile rectangle in 64x64 superblocks */
   int32_t tile_w, tile_h;     /* (a whole frame: 0, 0, sb_cols, sb_rows) */
   int32_t n_refs;             /* reference frames searched per frame */

@@ -98,7 +98,7 @@ static orc_mv qfull(orc_mv m) {
 orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd,
                               int tile_x0, int tile_y0, int tile_w,
                               int tile_h, int n_refs, int threads) {
-  if ((W & 7) || (H & 7) || (bd != 8 && bd != 10) || n_refs < 1 || n_refs > 7)
+  if ((W & 7) || (H & 7) || (bd != 8 && bd != 10 && bd != 12) || n_refs < 1 || n_refs > 7)
     return NULL;
   orc_replay *r = calloc(1, sizeof(*r));
   r->W = W;

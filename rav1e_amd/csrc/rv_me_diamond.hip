@@ -22,6 +22,7 @@
 //    prediction never leaves the wavefront.
 // Anything else (SATD, other sizes) takes the generic workgroup-per-
 // candidate kernel.
+#include <stdlib.h>
 #include <string.h>
 
 #include "rv_chain.h"
@@ -871,10 +872,155 @@ __global__ __launch_bounds__(kDsThreads) void diamond_kernel(DsArgs a) {
   }
 }
 
+// Full-pel diamond, one wavefront per job.  A round's (up to) 4
+// candidates are evaluated together by the one wavefront -- all their row
+// loads in flight at once, then four wave reductions -- so the round's
+// decision needs no LDS exchange or barrier, and a 64x64 job occupies one
+// wave instead of four (the search is a chain of dependent rounds, bound by
+// load latency: more jobs in flight per CU is what shortens it).
+template <typename Px, int W, int H>
+__global__ __launch_bounds__(64) void ds_wave_kernel(DsArgs a) {
+  using F = FullGeo<Px, W, H>;
+  constexpr int B = (int)sizeof(Px);
+  const int job = xcd_job(a.n);
+  if (job >= a.n) return;
+  const int lane = threadIdx.x;
+  const rv_ds_job *jp = a.jobs + job;
+  const rv_ds_job jb = *jp;
+  const rv_plane &ref = a.ref[job / a.n_per_ref];
+  const int frow = lane / F::K, fchunk = lane % F::K;
+  uint32_t org[4 * F::I];
+  {
+    const uint8_t *o = (const uint8_t *)plane_ptr<Px>(a.org, jb.po_x, jb.po_y);
+    const int64_t os = (int64_t)a.org.stride * B;
+#pragma unroll
+    for (int i = 0; i < F::I; i++) {
+      const int r = i * F::R + frow;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (!F::kPartial || r < H) v = ld16(o + r * os + fchunk * 16);
+      org[4 * i + 0] = v.x;
+      org[4 * i + 1] = v.y;
+      org[4 * i + 2] = v.z;
+      org[4 * i + 3] = v.w;
+    }
+  }
+  const int64_t rs = (int64_t)ref.stride * B;
+  uint32_t evals = 0;
+  // costs of cands[k], k < n, k != skip (u64::MAX when out of range,
+  // skipped or k >= n); wave-uniform
+  auto round4 = [&](const rv_mv *cands, int n, int skip, uint64_t *cost)
+      __attribute__((always_inline)) {
+    bool ok[kDsWaves];
+    const uint8_t *rp[kDsWaves];
+#pragma unroll
+    for (int k = 0; k < kDsWaves; k++) {
+      ok[k] = k < n && k != skip && ds_in_range(cands[k], jb);
+      // region at po + mv / 8 (Rust `/` truncates toward zero)
+      rp[k] = (const uint8_t *)plane_ptr<Px>(ref, jb.po_x + (ok[k] ? cands[k].col / 8 : 0),
+                                             jb.po_y + (ok[k] ? cands[k].row / 8 : 0));
+      evals += ok[k];
+    }
+    uint32_t acc[kDsWaves] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < F::I; i++) {
+      const int rr = i * F::R + frow;
+      if (!F::kPartial || rr < H) {
+        uint4 v[kDsWaves];
+#pragma unroll
+        for (int k = 0; k < kDsWaves; k++)
+          v[k] = ok[k] ? ld16(rp[k] + rr * rs + fchunk * 16) : make_uint4(0, 0, 0, 0);
+        const uint4 o = make_uint4(org[4 * i], org[4 * i + 1], org[4 * i + 2], org[4 * i + 3]);
+#pragma unroll
+        for (int k = 0; k < kDsWaves; k++) acc[k] = sad16<Px>(o, v[k], acc[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kDsWaves; k++)
+      cost[k] = ok[k] ? ds_cost(wave_sum(acc[k]), cands[k], jb, a.hp) : ~0ull;
+  };
+
+  // get_best_predictor, then the diamond steps: the round loop of
+  // ds_fast_kernel (its comments give the exactness arguments), decided in
+  // registers.
+  rv_mv center{0, 0};
+  uint64_t center_cost = ~0ull;
+  const int np = jb.n_pred < RV_DS_MAX_PRED ? jb.n_pred : RV_DS_MAX_PRED;
+  int16_t radius = 16;
+  const int16_t radius_end = 8;
+  int p0 = 0;
+  int back = -1;
+  for (int iter = 0; iter < 4096 + RV_DS_MAX_PRED; iter++) {
+    const bool pred_phase = p0 < np;
+    rv_mv c4[kDsWaves];
+    int n;
+    if (pred_phase) {
+      n = np - p0 < kDsWaves ? np - p0 : kDsWaves;
+#pragma unroll
+      for (int k = 0; k < kDsWaves; k++) c4[k] = jp->pred[p0 + (k < n ? k : 0)];
+    } else {
+      n = kDsWaves;
+      c4[0] = rv_mv{(int16_t)(center.row + radius), center.col};  // diamond_pattern
+      c4[1] = rv_mv{center.row, (int16_t)(center.col + radius)};
+      c4[2] = rv_mv{(int16_t)(center.row - radius), center.col};
+      c4[3] = rv_mv{center.row, (int16_t)(center.col - radius)};
+    }
+    uint64_t c[kDsWaves];
+    round4(c4, n, pred_phase ? -1 : back, c);
+    uint64_t best = ~0ull;
+    int bp = 0;
+#pragma unroll
+    for (int k = 0; k < kDsWaves; k++)
+      if (k < n && c[k] < best) {
+        best = c[k];
+        bp = k;
+      }
+    rv_mv bmv = c4[0];
+#pragma unroll
+    for (int k = 1; k < kDsWaves; k++)
+      if (bp == k) bmv = c4[k];
+    if (pred_phase) {
+      if (best < center_cost) {
+        center = bmv;
+        center_cost = best;
+      }
+      p0 += kDsWaves;
+    } else if (center_cost <= best) {
+      if (radius == radius_end) break;
+      radius /= 2;
+      back = -1;
+    } else {
+      back = center_cost != ~0ull ? (bp + 2) & 3 : -1;
+      center = bmv;
+      center_cost = best;
+    }
+  }
+  if (lane == 0) {
+    if (a.evals) a.evals[job] = evals;
+    ds_write(a, job, center, center_cost);
+    chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, center);
+  }
+}
+
+// Blocks up to 32x32 take ds_wave_kernel (2160p F2, 32x32 at half
+// resolution: 0.031 -> 0.023 ms); 64x64 stays on the 4-wavefront kernel
+// (0.035 vs 0.037 ms: 16 row loads per round from one wavefront issue
+// slower than 4 from each of four).  RAV1E_HIP_DS_WG=1: always the
+// 4-wavefront kernel (A/B).
+static bool ds_full_wave() {
+  static const bool on = [] {
+    const char *e = getenv("RAV1E_HIP_DS_WG");
+    return !(e && e[0] == '1');
+  }();
+  return on;
+}
+
 template <typename Px, int W, int H, bool SUB>
 void launch_fast(const DsArgs &a, hipStream_t s) {
   const unsigned grid = (unsigned)((a.n + 7) / 8 * 8);
-  ds_fast_kernel<Px, W, H, SUB><<<grid, kDsThreads, 0, s>>>(a);
+  if (!SUB && !a.tele && W * H <= 32 * 32 && ds_full_wave())
+    ds_wave_kernel<Px, W, H><<<grid, 64, 0, s>>>(a);
+  else
+    ds_fast_kernel<Px, W, H, SUB><<<grid, kDsThreads, 0, s>>>(a);
 }
 
 template <typename Px>

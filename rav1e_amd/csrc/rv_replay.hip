@@ -443,7 +443,7 @@ void rv_replay_destroy(rv_replay *r) {
 
 rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   if (!cfg || cfg->width <= 0 || cfg->height <= 0 || (cfg->width & 7) ||
-      (cfg->height & 7) || (cfg->bit_depth != 8 && cfg->bit_depth != 10) ||
+      (cfg->height & 7) || (cfg->bit_depth != 8 && cfg->bit_depth != 10 && cfg->bit_depth != 12) ||
       cfg->xdec < 0 || cfg->xdec > 1 || cfg->ydec < 0 || cfg->ydec > 1 ||
       cfg->n_refs < 1 || cfg->n_refs > RV_DS_MAX_PRED - 1) {
     rv_set_error(RV_EINVAL, "rv_replay_create: bad config");

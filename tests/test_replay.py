@@ -51,6 +51,7 @@ def test_cpu_replay_thread_invariant():
     (256, 192, 1, 1, 8, 2, None),
     (320, 128, 0, 0, 8, 1, None),
     (256, 128, 1, 1, 10, 2, None),
+    (192, 128, 1, 1, 12, 1, None),  # 12 bits: exhaustive full search, 12-bit RDO kernel
     (384, 192, 1, 1, 8, 2, (2, 0, 4, 3)),
 ])
 @pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_SIDE_RDO, RP.RV_REPLAY_SPLIT_RDO,
