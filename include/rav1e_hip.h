@@ -263,6 +263,13 @@ int rv_dequantize_batch(const int32_t *d_qcoeffs, int n, int tx_size, int qindex
                         int bit_depth, int dc_delta_q, int ac_delta_q,
                         int32_t *d_rcoeffs, void *stream);
 
+/* estimate_rate (src/rdo.rs:204-216) for n blocks of one TxSize: d_rate[i] =
+ * the rate the reference reads off RDO_RATE_TABLE for tx-domain distortion
+ * d_tx_dist[i] (rv_tx_dist_batch's output, src/encoder.rs:1210-1224) at the
+ * frame's base qindex (0..255).  Replaces the call at src/encoder.rs:1231. */
+int rv_estimate_rate_batch(const uint64_t *d_tx_dist, int n, int qindex, int tx_size,
+                           uint64_t *d_rate, void *stream);
+
 /* ---------------------------------------------------------------------
  * Motion search
  * ------------------------------------------------------------------- */

@@ -128,3 +128,23 @@ void orc_dequantize(int qindex, const int32_t *coeffs, int32_t *rcoeffs, int tx_
     rcoeffs[i] = w_add(w_mul(c, i == 0 ? dcq : acq), asr(c, 31) & offset) >> s;
   }
 }
+
+/* estimate_rate (src/rdo.rs:204-216): linear interpolation in the trained
+ * RDO_RATE_TABLE between the two distortion bins around fast_distortion
+ * (the tx-domain distortion of src/encoder.rs:1210-1224), i64 arithmetic. */
+#include "orc_rate_table.h"
+uint64_t orc_estimate_rate(int qindex, int tx_size, uint64_t fast_distortion) {
+  const int q_bin = qindex / RV_RDO_QUANT_DIV;
+  uint64_t down = fast_distortion / RV_RATE_EST_BIN_SIZE;
+  if (down > RV_RDO_NUM_BINS - 2) down = RV_RDO_NUM_BINS - 2;
+  uint64_t up = down + 1;
+  if (up > RV_RDO_NUM_BINS - 1) up = RV_RDO_NUM_BINS - 1;
+  const int64_t x0 = (int64_t)(down * RV_RATE_EST_BIN_SIZE);
+  const int64_t x1 = (int64_t)(up * RV_RATE_EST_BIN_SIZE);
+  const uint32_t *row = RV_RDO_RATE_TABLE + ((size_t)q_bin * 19 + tx_size) * RV_RDO_NUM_BINS;
+  const int64_t y0 = row[down], y1 = row[up];
+  const int64_t slope = (int64_t)((uint64_t)(y1 - y0) << 8) / (x1 - x0); /* truncates */
+  const int64_t d = (int64_t)fast_distortion - x0;
+  const int64_t r = y0 + ((int64_t)((uint64_t)d * (uint64_t)slope) >> 8); /* wrapping mul */
+  return r > 0 ? (uint64_t)r : 0;
+}

@@ -108,6 +108,8 @@ int orc_quantize(const orc_qctx *c, const int32_t *coeffs, int32_t *qcoeffs, int
                  int tx_type);
 void orc_dequantize(int qindex, const int32_t *coeffs, int32_t *rcoeffs, int tx_size, int bd,
                     int dc_delta_q, int ac_delta_q);
+/* estimate_rate (src/rdo.rs:204-216) */
+uint64_t orc_estimate_rate(int qindex, int tx_size, uint64_t fast_distortion);
 /* diff (src/encoder.rs:1044-1058) */
 void orc_diff(int16_t *dst, const void *a, ptrdiff_t sa, const void *b,
               ptrdiff_t sb, int w, int h, int hbd);

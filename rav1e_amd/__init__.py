@@ -229,6 +229,7 @@ def _declare(L):
         "rv_quantize_batch": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp,
                                     vp]),
         "rv_dequantize_batch": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp]),
+        "rv_estimate_rate_batch": (i32, [vp, i32, i32, i32, vp, vp]),
         "rv_full_search_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, vp, vp]),
         "rv_full_search_sea_batch": (i32, [P, P, vp, vp, i32, i32, vp, vp]),
         "rv_plane_box_sums": (i32, [P, vp, vp]),
@@ -537,6 +538,19 @@ def dequantize_batch(qcoeffs: np.ndarray, tx_size, qindex, bit_depth=8, dc_delta
                                      ac_delta_q, dr.ptr, None), "rv_dequantize_batch")
     _sync()
     return dr.download(np.int32, coded * n).reshape(n, coded)
+
+
+def estimate_rate_batch(tx_dist: np.ndarray, tx_size, qindex) -> np.ndarray:
+    """estimate_rate (src/rdo.rs:204-216) of each block's tx-domain
+    distortion (u64) at base qindex: the table-interpolated rate, u64."""
+    d = np.ascontiguousarray(tx_dist, dtype=np.uint64).ravel()
+    n = d.size
+    dd = DeviceBuffer.from_array(d if n else np.zeros(1, np.uint64))
+    dr = DeviceBuffer(8 * max(1, n))
+    _check(lib().rv_estimate_rate_batch(dd.ptr, n, int(qindex), int(tx_size), dr.ptr, None),
+           "rv_estimate_rate_batch")
+    _sync()
+    return dr.download(np.uint64, n)
 
 
 def inv_txfm_add_batch(coeffs: np.ndarray, dst: DevicePlane, jobs, tx_size, tx_type,

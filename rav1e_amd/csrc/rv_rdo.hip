@@ -854,13 +854,6 @@ int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipSt
     RV_HIP_CHECK_LAUNCH();
     return RV_OK;
   }
-  if (false) {
-    const unsigned grid = (unsigned)luma.n_tx + cpairs;
-    if (grid == 0) return RV_OK;
-    rdo_frame_kernel<uint16_t><<<grid, 64, 0, s>>>(luma, chroma);
-    RV_HIP_CHECK_LAUNCH();
-    return RV_OK;
-  }
   const int nquads = (luma.n_tx + 3) / 4;
   const unsigned grid = (unsigned)nquads + (cpairs + 2) / 3;
   if (grid == 0) return RV_OK;

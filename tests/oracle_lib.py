@@ -53,6 +53,8 @@ def lib():
         L.orc_quantize.argtypes = [vp, vp, vp, i32, i32]
         L.orc_dequantize.argtypes = [i32, vp, vp, i32, i32, i32, i32]
         L.orc_coded_tx_area.restype = i32
+        L.orc_estimate_rate.restype = C.c_uint64
+        L.orc_estimate_rate.argtypes = [i32, i32, C.c_uint64]
         L.orc_get_log_tx_scale.restype = i32
         _lib = L
     return _lib
@@ -155,6 +157,11 @@ def dequantize(qcoeffs, tx_size, qindex, bd, dc_delta_q=0, ac_delta_q=0):
     r = np.zeros(q.size, dtype=np.int32)
     lib().orc_dequantize(qindex, ptr(q), ptr(r), tx_size, bd, dc_delta_q, ac_delta_q)
     return r
+
+
+def estimate_rate(qindex, tx_size, fast_distortion):
+    """estimate_rate (src/rdo.rs:204-216)"""
+    return int(lib().orc_estimate_rate(int(qindex), int(tx_size), int(fast_distortion)))
 
 
 def inv_txfm2d_add(coeffs, dst, tx_size, tx_type, bd):

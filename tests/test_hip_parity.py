@@ -622,6 +622,22 @@ def test_asm_shims_match_oracle():
 
 # ---- quantize / dequantize (src/quantize.rs) ----------------------------------
 @pytest.mark.gpu
+def test_estimate_rate_vs_oracle():
+    """rv_estimate_rate_batch vs orc_estimate_rate, every TxSize at several
+    base qindices, over bin edges, the clamped top bins and large values."""
+    rng = np.random.default_rng(1900)
+    fd = np.concatenate([np.array([0, 1, 1999, 2000, 97999, 98000, 99999, 100000, 10 ** 7, 2 ** 40],
+                                  dtype=np.uint64),
+                         rng.integers(0, 120000, 54).astype(np.uint64)])
+    for qi in (0, 60, 100, 255):
+        for ts in range(19):
+            got = R.estimate_rate_batch(fd, ts, qi)
+            want = [O.estimate_rate(qi, ts, int(v)) for v in fd]
+            np.testing.assert_array_equal(got, np.array(want, dtype=np.uint64), err_msg=f"{qi} {ts}")
+    assert R.estimate_rate_batch(np.zeros(0, np.uint64), 0, 0).size == 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("tx_size,tx_type", [(4, 0), (3, 0), (0, 0), (1, 3), (2, 9), (5, 0),
                                               (11, 0), (17, 0), (2, 11), (3, 10)])
 def test_quantize_vs_oracle(tx_size, tx_type):

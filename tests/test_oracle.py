@@ -341,3 +341,48 @@ def _scan(tx_size, tx_type):
     n = O.lib().orc_coded_tx_area(tx_size)
     o = off[tx_size * 16 + tx_type]
     return scans[o:o + n]
+
+
+# ---- estimate_rate (src/rdo.rs:204-216) -------------------------------------
+def _rate_table():
+    """RDO_RATE_TABLE as the generated header holds it: [8][19][50]."""
+    import re
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "oracle", "orc_rate_table.h")).read()
+    m = re.search(r"RV_RDO_RATE_TABLE\[\d+\] = \{(.*?)\};", hdr, re.S)
+    v = [int(x) for x in re.findall(r"\d+", m.group(1))]
+    assert len(v) == 8 * 19 * 50
+    return np.array(v, dtype=np.int64).reshape(8, 19, 50)
+
+
+def _py_estimate_rate(tab, qindex, ts, fd):
+    """Restatement with Rust's i64 semantics: `/` truncates toward zero,
+    `>>` is arithmetic, the product wraps."""
+    down = min(fd // 2000, 48)
+    up = min(down + 1, 49)
+    x0, x1 = down * 2000, up * 2000
+    y0, y1 = int(tab[qindex // 32, ts, down]), int(tab[qindex // 32, ts, up])
+    num = (y1 - y0) << 8
+    slope = abs(num) // (x1 - x0) * (1 if num >= 0 else -1)
+    prod = ((fd - x0) * slope + (1 << 63)) % (1 << 64) - (1 << 63)
+    return max(y0 + (prod >> 8), 0)
+
+
+def test_estimate_rate_reference_test():
+    """estimate_rate_test (src/rdo.rs:2148-2150): distortion 0 at qindex 0,
+    TX_4X4 reads the table's first entry."""
+    tab = _rate_table()
+    assert O.estimate_rate(0, 0, 0) == int(tab[0, 0, 0])
+
+
+def test_estimate_rate_matches_restatement():
+    """The oracle against the Python restatement over every q bin and
+    TxSize: bin edges, interiors, the clamp to the last bins and large
+    distortions."""
+    tab = _rate_table()
+    rng = np.random.default_rng(77)
+    fds = [0, 1, 1999, 2000, 2001, 49999, 96000, 97999, 98000, 99999, 100000, 10 ** 7, 2 ** 40]
+    fds += [int(x) for x in rng.integers(0, 120000, 12)]
+    for q in (0, 31, 32, 100, 255):
+        for ts in range(19):
+            for fd in fds:
+                assert O.estimate_rate(q, ts, fd) == _py_estimate_rate(tab, q, ts, fd), (q, ts, fd)
