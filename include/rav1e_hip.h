@@ -147,6 +147,15 @@ int rv_sad_batch(const rv_plane *org, const rv_plane *ref,
 int rv_satd_batch(const rv_plane *org, const rv_plane *ref,
                   const rv_dist_job *d_jobs, int n, int w, int h,
                   uint32_t *d_out, void *stream);
+/* compute_lookahead_intra_costs (src/api/internal.rs:680-765) of a luma
+ * plane: d_costs[by * ceil(width / 8) + bx] = get_satd of the 8x8 block at
+ * (8 bx, 8 by) against its DC_PRED prediction, which the reference's tile
+ * rect makes pred_dc_128 (the constant 128 << (bit_depth - 8)).  Blocks of
+ * a partial last column / row read the plane's padding, as the reference's
+ * region does. */
+int rv_lookahead_intra_costs(const rv_plane *p, int bit_depth, uint32_t *d_costs,
+                             void *stream);
+
 /* sse_wxh raw partials (src/rdo.rs:286-335): per job, one u64 per
  * importance sub-block (bw x bh = (min(w,8) >> xdec) x (min(h,8) >> ydec),
  * xdec/ydec taken from `org`), raster order: d_out[i * nsub + k],

@@ -211,3 +211,28 @@ uint64_t orc_cdef_dist_from_moments(const int64_t m[5], int bit_depth) {
   if (v >= 18446744073709551615.0) return UINT64_MAX;
   return (uint64_t)v;
 }
+
+/* compute_lookahead_intra_costs (src/api/internal.rs:680-765): per 8x8
+ * importance block (w_in_imp_b = ceil(w / 8), src/encoder.rs:624-625),
+ * PredictionMode::DC_PRED.predict_intra into a copy of the plane with the
+ * tile rect at the block itself, so relative position (0, 0) ->
+ * PredictionVariant::NONE -> pred_dc_128 (src/predict.rs:214-221, 552-557,
+ * 623-633), then get_satd (src/dist.rs:197-328) of source vs prediction.
+ * org: the plane's pixel (0, 0); stride in elements. */
+void orc_lookahead_intra_costs(const void *org, ptrdiff_t stride, int w, int h, int hbd, int bd,
+                               uint32_t *out) {
+  const int nbx = (w + 7) / 8, nby = (h + 7) / 8;
+  uint16_t pred16[64];
+  uint8_t pred8[64];
+  for (int i = 0; i < 64; i++) {  /* pred_dc_128: 128 << (bit_depth - 8) */
+    pred16[i] = (uint16_t)(128u << (bd - 8));
+    pred8[i] = (uint8_t)(128u << (bd - 8));
+  }
+  const size_t px = hbd ? 2 : 1;
+  for (int by = 0; by < nby; by++)
+    for (int bx = 0; bx < nbx; bx++) {
+      const uint8_t *o = (const uint8_t *)org + ((ptrdiff_t)by * 8 * stride + bx * 8) * px;
+      out[by * nbx + bx] =
+          orc_get_satd(o, stride, hbd ? (const void *)pred16 : (const void *)pred8, 8, 8, 8, hbd, 0);
+    }
+}

@@ -38,6 +38,10 @@ uint32_t orc_get_sad(const void *org, ptrdiff_t org_stride, const void *ref,
 uint32_t orc_get_satd(const void *org, ptrdiff_t org_stride, const void *ref,
                       ptrdiff_t ref_stride, int w, int h, int hbd,
                       int emulate_gen);
+/* compute_lookahead_intra_costs (src/api/internal.rs:680-765): ceil(w/8) x
+ * ceil(h/8) costs, org = the plane's pixel (0, 0), stride in elements. */
+void orc_lookahead_intra_costs(const void *org, ptrdiff_t stride, int w, int h, int hbd, int bd,
+                               uint32_t *out);
 /* sse_wxh raw partials (src/rdo.rs:286-335): one u64 per importance
  * sub-block, raster order, (w/bw)*(h/bh) values, bw = min(8,w)>>xdec. */
 int orc_sse_wxh(const void *a, ptrdiff_t sa, const void *b, ptrdiff_t sb,

@@ -218,6 +218,7 @@ def _declare(L):
         "rv_sad_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
         "rv_satd_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
         "rv_sse_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
+        "rv_lookahead_intra_costs": (i32, [P, i32, vp, vp]),
         "rv_cdef_moments_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
         "rv_put_8tap_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, i32, vp]),
         "rv_prep_8tap_batch": (i32, [vp, P, vp, i32, i32, i32, i32, i32, i32, vp]),
@@ -404,6 +405,17 @@ def sad_batch(org: DevicePlane, ref: DevicePlane, jobs: np.ndarray, w: int, h: i
 
 def satd_batch(org, ref, jobs, w, h) -> np.ndarray:
     return sad_batch(org, ref, jobs, w, h, satd=True)
+
+
+def lookahead_intra_costs(plane: DevicePlane, bit_depth: int = 8) -> np.ndarray:
+    """compute_lookahead_intra_costs (src/api/internal.rs:680-765) of a luma
+    plane: u32 [ceil(h / 8), ceil(w / 8)]."""
+    nbx, nby = (plane.desc.width + 7) // 8, (plane.desc.height + 7) // 8
+    out = DeviceBuffer(4 * nbx * nby)
+    _check(lib().rv_lookahead_intra_costs(C.byref(plane.desc), int(bit_depth), out.ptr, None),
+           "rv_lookahead_intra_costs")
+    _sync()
+    return out.download(np.uint32, nbx * nby).reshape(nby, nbx)
 
 
 def sse_batch(org, ref, jobs, w, h) -> np.ndarray:

@@ -230,11 +230,57 @@ static void launch_satd(const rv_plane &o, const rv_plane &r,
   }
 }
 
+// compute_lookahead_intra_costs (src/api/internal.rs:680-765): for every
+// 8x8 importance block, DC_PRED into a copy of the plane, then get_satd of
+// the source block against it.  predict_intra is handed a tile rect that
+// starts at the block itself (:731-736), so its position relative to the
+// "tile" is (0, 0), PredictionVariant::NONE, and DC_PRED becomes pred_dc_128
+// (src/predict.rs:214-221, 552-557, 623-633): the prediction is the constant
+// 128 << (bd - 8) whatever the edges hold.  One thread per block.
+template <typename Px>
+__global__ __launch_bounds__(kBlock) void intra_cost_kernel(rv_plane p, int nbx, int nby,
+                                                            int base, uint32_t *out) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= nbx * nby) return;
+  const int bx = i % nbx, by = i / nbx;
+  const Px *o = plane_ptr<Px>(p, bx * 8, by * 8);
+  int32_t d[64];
+#pragma unroll
+  for (int r = 0; r < 8; r++)
+#pragma unroll
+    for (int c = 0; c < 8; c++) d[r * 8 + c] = (int32_t)o[(int64_t)r * p.stride + c] - base;
+  out[i] = (uint32_t)((satd_chunk<8>(d) + 4) >> 3);  // ln = msb(8)
+}
+
 }  // namespace rv
 
 using namespace rv;
 
 extern "C" {
+
+int rv_lookahead_intra_costs(const rv_plane *p, int bit_depth, uint32_t *d_costs,
+                             void *stream) {
+  if (!p || !d_costs || (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
+      (!p->hbd && bit_depth != 8) || p->width <= 0 || p->height <= 0 || p->xdec || p->ydec)
+    return rv_set_error(RV_EINVAL, "rv_lookahead_intra_costs: bad arguments");
+  // w_in_imp_b = w_in_b / 2 (src/encoder.rs:624-625): ceil(width / 8); the
+  // last column / row of blocks may read the plane's padding, as the
+  // reference's region does
+  const int nbx = (p->width + 7) >> 3, nby = (p->height + 7) >> 3;
+  if (p->xorigin + nbx * 8 > p->stride || p->yorigin + nby * 8 > p->alloc_height)
+    return rv_set_error(RV_EINVAL, "rv_lookahead_intra_costs: blocks leave the allocation");
+  const int n = nbx * nby;
+  hipStream_t s = rv_resolve_stream(stream);
+  const int base = 128 << (bit_depth - 8);
+  if (p->hbd)
+    intra_cost_kernel<uint16_t><<<(n + kBlock - 1) / kBlock, kBlock, 0, s>>>(*p, nbx, nby, base,
+                                                                           d_costs);
+  else
+    intra_cost_kernel<uint8_t><<<(n + kBlock - 1) / kBlock, kBlock, 0, s>>>(*p, nbx, nby, base,
+                                                                          d_costs);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
 
 int rv_sad_batch(const rv_plane *org, const rv_plane *ref,
                  const rv_dist_job *d_jobs, int n, int w, int h,

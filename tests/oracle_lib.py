@@ -54,6 +54,7 @@ def lib():
         L.orc_dequantize.argtypes = [i32, vp, vp, i32, i32, i32, i32]
         L.orc_coded_tx_area.restype = i32
         L.orc_estimate_rate.restype = C.c_uint64
+        L.orc_lookahead_intra_costs.argtypes = [vp, sz, i32, i32, i32, i32, vp]
         L.orc_estimate_rate.argtypes = [i32, i32, C.c_uint64]
         L.orc_get_log_tx_scale.restype = i32
         _lib = L
@@ -157,6 +158,16 @@ def dequantize(qcoeffs, tx_size, qindex, bd, dc_delta_q=0, ac_delta_q=0):
     r = np.zeros(q.size, dtype=np.int32)
     lib().orc_dequantize(qindex, ptr(q), ptr(r), tx_size, bd, dc_delta_q, ac_delta_q)
     return r
+
+
+def lookahead_intra_costs(full, yo, xo, w, h, bd):
+    """compute_lookahead_intra_costs of the plane whose pixel (0, 0) is
+    full[yo, xo] (the padded allocation): u32 [ceil(h / 8), ceil(w / 8)]."""
+    nbx, nby = (w + 7) // 8, (h + 7) // 8
+    out = np.zeros(nbx * nby, dtype=np.uint32)
+    lib().orc_lookahead_intra_costs(ptr(full, yo * full.shape[1] + xo), full.shape[1], w, h,
+                                    hbd_of(full), bd, ptr(out))
+    return out.reshape(nby, nbx)
 
 
 def estimate_rate(qindex, tx_size, fast_distortion):

@@ -622,6 +622,22 @@ def test_asm_shims_match_oracle():
 
 # ---- quantize / dequantize (src/quantize.rs) ----------------------------------
 @pytest.mark.gpu
+@pytest.mark.parametrize("bd", [8, 10, 12])
+def test_lookahead_intra_costs_vs_oracle(bd):
+    """rv_lookahead_intra_costs vs the oracle on the same padded plane, with
+    sizes that leave partial last blocks (read from the padding)."""
+    rng = np.random.default_rng(2000 + bd)
+    dt = np.uint8 if bd == 8 else np.uint16
+    for w, h in ((64, 64), (100, 60), (1920, 1080)):
+        a = rng.integers(0, 1 << bd, (h, w)).astype(dt)
+        p = R.DevicePlane.from_array(a, xpad=16, ypad=16)
+        got = R.lookahead_intra_costs(p, bd)
+        full = p.download_full()
+        want = O.lookahead_intra_costs(full, p.desc.yorigin, p.desc.xorigin, w, h, bd)
+        np.testing.assert_array_equal(got, want, err_msg=f"{bd} {w}x{h}")
+
+
+@pytest.mark.gpu
 def test_estimate_rate_vs_oracle():
     """rv_estimate_rate_batch vs orc_estimate_rate, every TxSize at several
     base qindices, over bin edges, the clamped top bins and large values."""

@@ -386,3 +386,27 @@ def test_estimate_rate_matches_restatement():
         for ts in range(19):
             for fd in fds:
                 assert O.estimate_rate(q, ts, fd) == _py_estimate_rate(tab, q, ts, fd), (q, ts, fd)
+
+
+# ---- lookahead intra costs (src/api/internal.rs:680-765) --------------------
+def test_lookahead_intra_costs_known_answers():
+    """DC_PRED at the block's own tile origin is pred_dc_128, so a constant
+    plane v costs get_satd of a DC-only difference: 64 |v - base| after the
+    8x8 Hadamard, (64 |v - base| + 4) >> 3 = 8 |v - base| per block; a plane
+    at the base value costs nothing; a block costs get_satd against a flat
+    block of the base value."""
+    for bd, dt in ((8, np.uint8), (10, np.uint16), (12, np.uint16)):
+        base = 128 << (bd - 8)
+        for v in (0, base, base + 7, (1 << bd) - 1):
+            full = np.full((40, 56), v, dtype=dt)
+            got = O.lookahead_intra_costs(full, 4, 8, 40, 24, bd)
+            assert got.shape == (3, 5)
+            assert (got == 8 * abs(v - base)).all(), (bd, v)
+    rng = np.random.default_rng(5)
+    full = rng.integers(0, 256, (48, 64)).astype(np.uint8)
+    got = O.lookahead_intra_costs(full, 8, 0, 60, 36, 8)  # partial last column / row
+    flat = np.full((8, 8), 128, dtype=np.uint8)
+    for by in range(5):
+        for bx in range(8):
+            want = O.get_satd(full, 8 + 8 * by, 8 * bx, flat, 0, 0, 8, 8)
+            assert got[by, bx] == want, (by, bx)
