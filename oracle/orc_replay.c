@@ -11,7 +11,8 @@
  *   F3 diamond full-pel + sub-pel at full res (src/me.rs:193-285)
  *   F4 put_8tap, diff + fht, quantize + dequantize, inverse + add,
  *      cdef moments / sse (src/encoder.rs:1077-1237, src/rdo.rs:219-411)
- *   F5 8x8 SATD importance (src/api/internal.rs:823-1010)
+ *   F5 8x8 SATD importance (src/api/internal.rs:823-1010) + lookahead
+ *      intra cost of the same blocks (:680-765, orc_lookahead_intra_costs)
  * It must produce the same result words as the GPU driver.
  */
 #include <pthread.h>
@@ -376,6 +377,9 @@ static void run_sb(orc_replay *r, int sb, uint64_t tail[3]) {
                               at(&r->slots[1].y, hbd, x + ((int)smv[0].col >> 3),
                                  y + ((int)smv[0].row >> 3)),
                               r->slots[1].y.stride, 8, 8, hbd, 0);
+      uint32_t ic;
+      orc_lookahead_intra_costs(at(&cur->y, hbd, x, y), cur->y.stride, 8, 8, hbd, r->bd, &ic);
+      tail[2] += ic;
     }
 }
 

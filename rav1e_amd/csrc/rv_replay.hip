@@ -16,7 +16,9 @@
 //       argmin (encode_tx_block src/encoder.rs:1077-1237,
 //       compute_distortion src/rdo.rs:338-411)
 //   F5  8x8 importance SATD against reference 1 (compute_block_importances,
-//       src/api/internal.rs:823-1010)
+//       src/api/internal.rs:823-1010) and the lookahead intra cost of the
+//       same blocks (compute_lookahead_intra_costs, :680-765: SATD against
+//       pred_dc_128, rv_dist.hip)
 //
 // Every stage is one batched launch over all superblocks of the tile.  The
 // glue between dependent stages is chained on the device (rv_chain.h): the
@@ -153,8 +155,10 @@ __global__ __launch_bounds__(64) void score_candidates(
 
 // F5: get_satd of every 8x8 luma block of the tile inside the frame against
 // reference 1 at the full-pel part of its superblock's sub-pel MV
-// (compute_block_importances, src/api/internal.rs:823-1010), summed.  One
-// lane per block; the job is computed in place.
+// (compute_block_importances, src/api/internal.rs:823-1010) plus its
+// lookahead intra cost (get_satd against pred_dc_128,
+// src/api/internal.rs:680-765), summed.  One lane per block; the job is
+// computed in place, the source block read once for both.
 template <typename Px>
 __global__ __launch_bounds__(256) void importance_kernel(Geo g, rv_plane org, rv_plane ref,
                                                           const rv_fs_result *sub, int nbx,
@@ -167,14 +171,18 @@ __global__ __launch_bounds__(256) void importance_kernel(Geo g, rv_plane org, rv
     const int x = g.tx0 * kSb + bx * 8, y = g.ty0 * kSb + by * 8;
     const Px *o = plane_ptr<Px>(org, x, y);
     const Px *r = plane_ptr<Px>(ref, x + ((int)mv.col >> 3), y + ((int)mv.row >> 3));
-    int32_t d[64];
+    const int32_t base = 128 << (g.bd - 8);
+    int32_t d[64], e[64];
 #pragma unroll
     for (int rr = 0; rr < 8; rr++)
 #pragma unroll
-      for (int cc = 0; cc < 8; cc++)
-        d[rr * 8 + cc] = (int32_t)o[(int64_t)rr * org.stride + cc] -
-                         (int32_t)r[(int64_t)rr * ref.stride + cc];
-    v = (satd_chunk<8>(d) + 4) >> 3;  // (sum + (1 << ln >> 1)) >> ln, ln = 3
+      for (int cc = 0; cc < 8; cc++) {
+        const int32_t ov = (int32_t)o[(int64_t)rr * org.stride + cc];
+        d[rr * 8 + cc] = ov - (int32_t)r[(int64_t)rr * ref.stride + cc];
+        e[rr * 8 + cc] = ov - base;
+      }
+    // (sum + (1 << ln >> 1)) >> ln, ln = 3
+    v = ((satd_chunk<8>(d) + 4) >> 3) + ((satd_chunk<8>(e) + 4) >> 3);
   }
   block_atomic_add(v, sum);
 }
