@@ -144,6 +144,13 @@ __device__ __forceinline__ void had1d(int32_t *v, int s) {
   }
 }
 
+// Order the LDS accesses of one wavefront's lanes (no workgroup barrier).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int N>
 __device__ __forceinline__ uint64_t satd_chunk(int32_t *d) {
 #pragma unroll

@@ -389,8 +389,8 @@ __global__ __launch_bounds__(kFsThreads) void fs16_kernel(FsArgs a) {
 //       tightens the UB for the next chunk).
 // Out-of-window candidates of edge tiles get a bound >= 2^30, above every
 // real cost (lambda < 2^23 here; larger lambdas take the exhaustive path).
-// The list holds a chunk's worst case (256 tiles x 32), so it never
-// overflows.
+// Each wavefront's list holds its 64 tiles' worst case (64 x 32), so it
+// never overflows.
 constexpr int kSeaList = kFsThreads * 32;  // survivors of one chunk, worst case
 constexpr uint32_t kSeaOut = 1u << 30;
 
@@ -581,27 +581,32 @@ __device__ __forceinline__ void sea_search(const FsArgs &a, const rv_fs_job &jb,
     }
   }
   __syncthreads();
-  // (2) chunks of one tile per lane: 8x8 bounds -> list -> 4x4 bound -> exact
-  int par = 0;
-  for (int base = 0; base < tasks; base += kFsThreads, par ^= 1) {
+  // (2) chunks of one tile per lane: 8x8 bounds -> list -> 4x4 bound ->
+  // exact.  Each wavefront keeps its own survivor list and works through
+  // its tiles with wave-local synchronisation only: the wavefronts of a job
+  // run decoupled (one's table loads overlap another's exact evaluations)
+  // and share only the bound, which only tightens.
+  const int lane = tid & 63;
+  uint32_t *wl = list + (tid >> 6) * (kSeaList / (kFsThreads / 64));
+  uint32_t *wc = cnt + (tid >> 6);
+  for (int base = 0; base < tasks; base += kFsThreads) {
     const int t = base + tid;
     if (t < tasks) {
       uint32_t m = sea_tile<SAME>(c, jb, a.hp, t, *(volatile uint32_t *)&ub_s);
       if (m) {
         const int tcy = t / c.tx_n, tcx = t - tcy * c.tx_n;
-        uint32_t slot = atomicAdd(&cnt[par], (uint32_t)__builtin_popcount(m));
+        uint32_t slot = atomicAdd(wc, (uint32_t)__builtin_popcount(m));
         while (m) {
           const int bit = __builtin_ctz(m);
           m &= m - 1;
-          list[slot++] = ((uint32_t)(tcy * kTileRows + (bit >> 2)) << 16) | (uint32_t)(4 * tcx + (bit & 3));
+          wl[slot++] = ((uint32_t)(tcy * kTileRows + (bit >> 2)) << 16) | (uint32_t)(4 * tcx + (bit & 3));
         }
       }
     }
-    if (tid == 0) cnt[par ^ 1] = 0;  // the next chunk's counter
-    __syncthreads();
-    const int n = (int)cnt[par];
-    for (int e = tid; e < n; e += kFsThreads) {
-      const uint32_t v = list[e];
+    wave_sync();
+    const int n = (int)*(volatile uint32_t *)wc;
+    for (int e = lane; e < n; e += 64) {
+      const uint32_t v = wl[e];
       const int iy = (int)(v >> 16), ix = (int)(v & 0xffff);
       const uint32_t rl = rate_l(iy, ix);
       const uint32_t ub = *(volatile uint32_t *)&ub_s;  // only tightens
@@ -610,7 +615,9 @@ __device__ __forceinline__ void sea_search(const FsArgs &a, const rv_fs_job &jb,
       bkey = key < bkey ? key : bkey;
       atomicMin(&ub_s, (uint32_t)(key >> 32));
     }
-    __syncthreads();  // list reuse
+    wave_sync();  // every read of the list and the counter done
+    if (lane == 0) *wc = 0;
+    wave_sync();
   }
   Best b{~0ull, 0xffffffffu};
   if (bkey != ~0ull) b = Best{bkey >> 32, (uint32_t)bkey};
@@ -627,7 +634,7 @@ __device__ __forceinline__ void fs16_sea_body(const FsArgs &a) {
   __shared__ uint32_t orgs[16 * ODW];
   __shared__ uint32_t so4[16], s4p[8], s48p[4];
   __shared__ uint32_t list[kSeaList];
-  __shared__ uint32_t cnt[2], ub_s;
+  __shared__ uint32_t cnt[kFsThreads / 64], ub_s;  // survivors per wavefront
   const int job = fs_job_index();
   if (job >= a.n) return;
   const rv_fs_job jb = a.jobs[job];
@@ -651,7 +658,7 @@ __device__ __forceinline__ void fs16_sea_body(const FsArgs &a) {
   }
   if (tid == 0) {
     ub_s = 0xffffffffu;
-    cnt[0] = 0;
+    for (int w = 0; w < kFsThreads / 64; w++) cnt[w] = 0;
   }
   __syncthreads();
   if (tid < 16) {  // 4x4 block sums of the source block (row-major blocks)

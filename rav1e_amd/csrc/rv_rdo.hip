@@ -388,11 +388,6 @@ struct LumaLds {
   static constexpr int kSlot = (kScr + 64 * 64 * (int)sizeof(Px) + 15) / 16 * 16;  // + pred
 };
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // MC into pred, then residual + column DCT: fmid = scr as i32 [16][65].  No
 // trailing synchronisation (the caller's).
