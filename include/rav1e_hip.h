@@ -297,6 +297,26 @@ typedef struct rv_fs_result {
   uint32_t reserved;
   uint64_t cost;
 } rv_fs_result;
+
+/* The importance propagation of compute_block_importances
+ * (src/api/internal.rs:823-1010) for one (frame, reference) pass, bit-exact
+ * in f32.  org: the frame's luma plane; ref: the reference's; d_mvs,
+ * d_intra_costs, d_importances: the frame's [ceil(h / 8)][ceil(w / 8)]
+ * lookahead MVs (lookahead_mvs sampled at [2y][2x]), intra costs
+ * (rv_lookahead_intra_costs) and block importances; n_unique: the number of
+ * distinct references of the frame (1..3).  Every block adds
+ * amount * overlap fraction to the four blocks of d_ref_importances its
+ * MV-displaced area overlaps, in the reference's order (source raster
+ * order; top-left, top-right, bottom-left, bottom-right), so the float sums
+ * round exactly as the reference's.  A block whose 8x8 reference area
+ * leaves the allocation (where the reference's region panics) contributes
+ * nothing.  d_scratch: device memory of rv_propagate_importances_scratch()
+ * bytes. */
+size_t rv_propagate_importances_scratch(int w_imp, int h_imp);
+int rv_propagate_importances(const rv_plane *org, const rv_plane *ref, const rv_mv *d_mvs,
+                             const uint32_t *d_intra_costs, const float *d_importances,
+                             int n_unique, float *d_ref_importances, void *d_scratch,
+                             size_t scratch_bytes, void *stream);
 /* full_search (src/me.rs:943-990): every candidate (x, y), y outer,
  * x inner, step `step`: cost = 256 * SAD + rate * lambda,
  * rate = min(rate(mv - pmv0), rate(mv - pmv1) + 1) (get_mv_rate,

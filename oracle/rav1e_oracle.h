@@ -120,6 +120,15 @@ void orc_diff(int16_t *dst, const void *a, ptrdiff_t sa, const void *b,
 
 /* ---- motion search (src/me.rs) ---------------------------------------- */
 typedef struct { int16_t row, col; } orc_mv;
+
+/* ---- lookahead (src/api/internal.rs) ------------------------------------ */
+/* compute_block_importances' propagation (:823-1010), one (frame, reference)
+ * pass; see orc_lookahead.c. */
+void orc_propagate_importances(const void *org, ptrdiff_t org_stride, const void *ref,
+                               ptrdiff_t ref_stride, int w_imp, int h_imp, int hbd,
+                               const orc_mv *mvs, const uint32_t *intra_costs,
+                               const float *importances, int n_unique,
+                               float *ref_importances);
 uint32_t orc_get_mv_rate(orc_mv a, orc_mv b, int allow_hp);
 /* full_search (src/me.rs:943-990). org/ref point at plane (0,0) (the data
  * origin); x/y in pixels relative to it; may be negative (padding). */

@@ -51,6 +51,7 @@ class RvFsResult(C.Structure):
 DIST_JOB = np.dtype([("org_x", "<i4"), ("org_y", "<i4"), ("ref_x", "<i4"), ("ref_y", "<i4")])
 MC_JOB = np.dtype([("src_x", "<i4"), ("src_y", "<i4"), ("dst_x", "<i4"), ("dst_y", "<i4"),
                    ("col_frac", "<i4"), ("row_frac", "<i4")])
+MOTION_VECTOR = np.dtype([("row", "<i2"), ("col", "<i2")])  # rv_mv / MotionVector
 TX_JOB = np.dtype([("src_x", "<i4"), ("src_y", "<i4"), ("pred_x", "<i4"), ("pred_y", "<i4")])
 FS_JOB = np.dtype([("po_x", "<i4"), ("po_y", "<i4"), ("x_lo", "<i4"), ("x_hi", "<i4"),
                    ("y_lo", "<i4"), ("y_hi", "<i4"), ("pmv0_row", "<i2"), ("pmv0_col", "<i2"),
@@ -219,6 +220,8 @@ def _declare(L):
         "rv_satd_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
         "rv_sse_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
         "rv_lookahead_intra_costs": (i32, [P, i32, vp, vp]),
+        "rv_propagate_importances_scratch": (sz, [i32, i32]),
+        "rv_propagate_importances": (i32, [P, P, vp, vp, vp, i32, vp, vp, sz, vp]),
         "rv_cdef_moments_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
         "rv_put_8tap_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, i32, vp]),
         "rv_prep_8tap_batch": (i32, [vp, P, vp, i32, i32, i32, i32, i32, i32, vp]),
@@ -416,6 +419,28 @@ def lookahead_intra_costs(plane: DevicePlane, bit_depth: int = 8) -> np.ndarray:
            "rv_lookahead_intra_costs")
     _sync()
     return out.download(np.uint32, nbx * nby).reshape(nby, nbx)
+
+
+def propagate_importances(org: DevicePlane, ref: DevicePlane, mvs: np.ndarray,
+                          intra_costs: np.ndarray, importances: np.ndarray, n_unique: int,
+                          ref_importances: np.ndarray) -> np.ndarray:
+    """compute_block_importances' propagation (src/api/internal.rs:823-1010)
+    for one (frame, reference) pass: mvs [h_imp, w_imp] MOTION_VECTOR,
+    intra_costs u32, importances f32 of the frame; returns the reference's
+    f32 importances after the pass (ref_importances is the value before)."""
+    nbx, nby = (org.desc.width + 7) // 8, (org.desc.height + 7) // 8
+    mv = np.ascontiguousarray(mvs, dtype=MOTION_VECTOR).reshape(nby * nbx)
+    dm = DeviceBuffer.from_array(mv)
+    di = DeviceBuffer.from_array(np.ascontiguousarray(intra_costs, dtype=np.uint32).ravel())
+    dp = DeviceBuffer.from_array(np.ascontiguousarray(importances, dtype=np.float32).ravel())
+    dr = DeviceBuffer.from_array(np.ascontiguousarray(ref_importances, dtype=np.float32).ravel())
+    nbytes = lib().rv_propagate_importances_scratch(nbx, nby)
+    ds = DeviceBuffer(max(1, nbytes))
+    _check(lib().rv_propagate_importances(C.byref(org.desc), C.byref(ref.desc), dm.ptr, di.ptr,
+                                          dp.ptr, int(n_unique), dr.ptr, ds.ptr, nbytes, None),
+           "rv_propagate_importances")
+    _sync()
+    return dr.download(np.float32, nbx * nby).reshape(nby, nbx)
 
 
 def sse_batch(org, ref, jobs, w, h) -> np.ndarray:

@@ -55,6 +55,8 @@ def lib():
         L.orc_coded_tx_area.restype = i32
         L.orc_estimate_rate.restype = C.c_uint64
         L.orc_lookahead_intra_costs.argtypes = [vp, sz, i32, i32, i32, i32, vp]
+        L.orc_propagate_importances.argtypes = [vp, sz, vp, sz, i32, i32, i32, vp, vp, vp, i32,
+                                                vp]
         L.orc_estimate_rate.argtypes = [i32, i32, C.c_uint64]
         L.orc_get_log_tx_scale.restype = i32
         _lib = L
@@ -167,6 +169,25 @@ def lookahead_intra_costs(full, yo, xo, w, h, bd):
     out = np.zeros(nbx * nby, dtype=np.uint32)
     lib().orc_lookahead_intra_costs(ptr(full, yo * full.shape[1] + xo), full.shape[1], w, h,
                                     hbd_of(full), bd, ptr(out))
+    return out.reshape(nby, nbx)
+
+
+def propagate_importances(org_full, oyo, oxo, ref_full, ryo, rxo, w, h, mvs, intra_costs,
+                          importances, n_unique, ref_importances):
+    """compute_block_importances' propagation, one (frame, reference) pass:
+    org_full / ref_full are padded allocations whose pixel (0, 0) is at
+    [yo, xo]; mvs is an int16 [h_imp, w_imp, 2] (row, col) array.  Returns
+    the reference's importances after the pass."""
+    nbx, nby = (w + 7) // 8, (h + 7) // 8
+    mv = np.ascontiguousarray(mvs, dtype=np.int16).reshape(nby * nbx * 2)
+    ic = np.ascontiguousarray(intra_costs, dtype=np.uint32).ravel()
+    imp = np.ascontiguousarray(importances, dtype=np.float32).ravel()
+    out = np.array(ref_importances, dtype=np.float32).ravel().copy()
+    lib().orc_propagate_importances(ptr(org_full, oyo * org_full.shape[1] + oxo),
+                                    org_full.shape[1],
+                                    ptr(ref_full, ryo * ref_full.shape[1] + rxo),
+                                    ref_full.shape[1], nbx, nby, hbd_of(org_full), ptr(mv),
+                                    ptr(ic), ptr(imp), int(n_unique), ptr(out))
     return out.reshape(nby, nbx)
 
 

@@ -638,6 +638,42 @@ def test_lookahead_intra_costs_vs_oracle(bd):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("bd,n_unique", [(8, 1), (8, 2), (10, 3)])
+def test_propagate_importances_vs_oracle(bd, n_unique):
+    """rv_propagate_importances vs the oracle, f32 bit patterns: 1080p-sized
+    importance grid (32400 blocks), sub-pel and negative MVs, zero intra
+    costs, many sources per target (a constant MV field piles four sources
+    onto most targets) -- the sort-and-ordered-sum must reproduce the
+    reference's += sequence exactly."""
+    rng = np.random.default_rng(2100 + bd + n_unique)
+    dt = np.uint8 if bd == 8 else np.uint16
+    w, h = 1920, 1080
+    a = rng.integers(0, 1 << bd, (h, w)).astype(dt)
+    b = np.roll(a, (3, -5), axis=(0, 1)) + rng.integers(0, 4, (h, w)).astype(dt)
+    b = np.minimum(b, (1 << bd) - 1).astype(dt)
+    po = R.DevicePlane.from_array(a, xpad=88, ypad=88)
+    pr = R.DevicePlane.from_array(b, xpad=88, ypad=88)
+    nbx, nby = w // 8, h // 8
+    mvs = np.zeros((nby, nbx), dtype=R.MOTION_VECTOR)
+    mvs["row"] = rng.integers(-512, 513, (nby, nbx))
+    mvs["col"] = rng.integers(-512, 513, (nby, nbx))
+    # the true motion (b is a rolled by (3, -5)) with sub-pel parts: small
+    # inter costs, so these blocks propagate
+    mvs[: nby // 2, : nbx // 2] = (np.int16(3 * 8 + 5), np.int16(-5 * 8 + 3))
+    intra = R.lookahead_intra_costs(po, bd)
+    intra[0, :50] = 0
+    imp = (rng.random((nby, nbx)) * 1000).astype(np.float32)
+    ref0 = (rng.random((nby, nbx)) * 300).astype(np.float32)
+    got = R.propagate_importances(po, pr, mvs, intra, imp, n_unique, ref0)
+    of, rf = po.download_full(), pr.download_full()
+    mv2 = np.stack([mvs["row"], mvs["col"]], axis=-1)
+    want = O.propagate_importances(of, po.desc.yorigin, po.desc.xorigin, rf, pr.desc.yorigin,
+                                   pr.desc.xorigin, w, h, mv2, intra, imp, n_unique, ref0)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert (got != ref0).mean() > 0.2
+
+
+@pytest.mark.gpu
 def test_estimate_rate_vs_oracle():
     """rv_estimate_rate_batch vs orc_estimate_rate, every TxSize at several
     base qindices, over bin edges, the clamped top bins and large values."""

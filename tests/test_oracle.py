@@ -410,3 +410,52 @@ def test_lookahead_intra_costs_known_answers():
         for bx in range(8):
             want = O.get_satd(full, 8 + 8 * by, 8 * bx, flat, 0, 0, 8, 8)
             assert got[by, bx] == want, (by, bx)
+
+
+# ---- importance propagation (src/api/internal.rs:823-1010) ------------------
+def _py_propagate(org, oyo, oxo, ref, ryo, rxo, nbx, nby, mvs, intra, imp, n_unique, out):
+    """Restatement in numpy float32 scalars (IEEE single, no fused ops)."""
+    f32 = np.float32
+    out = out.astype(np.float32).copy()
+    for y in range(nby):
+        for x in range(nbx):
+            row, col = int(mvs[y, x, 0]), int(mvs[y, x, 1])
+            rx, ry = x * 64 + col, y * 64 + row
+            px_x, px_y = int(rx / 8), int(ry / 8)  # toward zero
+            inter = f32(O.get_satd(org, oyo + 8 * y, oxo + 8 * x, ref, ryo + px_y, rxo + px_x, 8, 8))
+            ic = f32(intra[y, x])
+            with np.errstate(divide="ignore", invalid="ignore"):
+                fr = f32(1) - inter / ic
+            fr = f32(0) if np.isnan(fr) or fr < 0 else fr
+            amount = (ic + imp[y, x]) * fr / f32(n_unique)
+            tlx = (rx - (63 if rx < 0 else 0)) // 64 * 64 if rx >= 0 else -((-(rx - 63)) // 64) * 64
+            tly = (ry - (63 if ry < 0 else 0)) // 64 * 64 if ry >= 0 else -((-(ry - 63)) // 64) * 64
+            trx, bly = tlx + 64, tly + 64
+            parts = ((tlx, tly, (trx - rx) * (bly - ry)), (trx, tly, (rx + 64 - trx) * (bly - ry)),
+                     (tlx, bly, (trx - rx) * (ry + 64 - bly)), (trx, bly, (rx + 64 - trx) * (ry + 64 - bly)))
+            for tx, ty, a in parts:
+                bx, by = int(tx / 64), int(ty / 64)
+                if 0 <= bx < nbx and 0 <= by < nby:
+                    out[by, bx] = out[by, bx] + amount * (f32(a) / f32(4096))
+    return out
+
+
+@pytest.mark.parametrize("n_unique", [1, 2, 3])
+def test_propagate_importances_matches_restatement(n_unique):
+    """The oracle's f32 propagation against the numpy restatement, bit for
+    bit: sub-pel and negative MVs (truncating division, floor to the block
+    grid), zero intra costs (inf and NaN fractions), targets off the grid."""
+    rng = np.random.default_rng(300 + n_unique)
+    w, h, pad = 64, 48, 40
+    nbx, nby = 8, 6
+    org = rng.integers(0, 256, (h + 2 * pad, w + 2 * pad)).astype(np.uint8)
+    ref = rng.integers(0, 256, (h + 2 * pad, w + 2 * pad)).astype(np.uint8)
+    mvs = rng.integers(-256, 257, (nby, nbx, 2)).astype(np.int16)
+    intra = rng.integers(0, 3000, (nby, nbx)).astype(np.uint32)
+    intra[0, :3] = 0
+    imp = (rng.random((nby, nbx)) * 500).astype(np.float32)
+    out0 = (rng.random((nby, nbx)) * 100).astype(np.float32)
+    got = O.propagate_importances(org, pad, pad, ref, pad, pad, w, h, mvs, intra, imp, n_unique,
+                                  out0)
+    want = _py_propagate(org, pad, pad, ref, pad, pad, nbx, nby, mvs, intra, imp, n_unique, out0)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
