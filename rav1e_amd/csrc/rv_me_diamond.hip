@@ -290,7 +290,7 @@ struct DsFast {
 };
 
 template <typename Px, int W, int H, bool SUB>
-__global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
+__device__ __forceinline__ void ds_fast_body(const DsArgs &a) {
   using F = FullGeo<Px, W, H>;
   using S = SubGeo<Px, W, H>;
   constexpr int B = (int)sizeof(Px);
@@ -640,6 +640,19 @@ __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel(DsArgs a) {
     ds_write(a, job, center, center_cost);
     chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, center);
   }
+}
+
+// The 4-wavefront search at 5 waves per SIMD (<= 96 VGPRs: the u8 sub-pel
+// search fits without spilling), and at the compiler's choice
+// (RAV1E_HIP_DS_OCC4=1, A/B).
+template <typename Px, int W, int H, bool SUB>
+__global__ __launch_bounds__(kDsThreads) __attribute__((amdgpu_waves_per_eu(5))) void
+ds_fast_kernel(DsArgs a) {
+  ds_fast_body<Px, W, H, SUB>(a);
+}
+template <typename Px, int W, int H, bool SUB>
+__global__ __launch_bounds__(kDsThreads) void ds_fast_kernel_occ4(DsArgs a) {
+  ds_fast_body<Px, W, H, SUB>(a);
 }
 
 // ============================ generic path =================================
@@ -1017,8 +1030,14 @@ static bool ds_full_wave() {
 template <typename Px, int W, int H, bool SUB>
 void launch_fast(const DsArgs &a, hipStream_t s) {
   const unsigned grid = (unsigned)((a.n + 7) / 8 * 8);
+  static const bool occ4 = [] {
+    const char *e = getenv("RAV1E_HIP_DS_OCC4");
+    return e && e[0] == '1';
+  }();
   if (!SUB && !a.tele && W * H <= 32 * 32 && ds_full_wave())
     ds_wave_kernel<Px, W, H><<<grid, 64, 0, s>>>(a);
+  else if (occ4)
+    ds_fast_kernel_occ4<Px, W, H, SUB><<<grid, kDsThreads, 0, s>>>(a);
   else
     ds_fast_kernel<Px, W, H, SUB><<<grid, kDsThreads, 0, s>>>(a);
 }
