@@ -492,21 +492,27 @@ __device__ __forceinline__ uint32_t sea_tile(const SeaCtx &c, const rv_fs_job &j
   for (int k = 0; k < kTileRows; k++)
 #pragma unroll
     for (int j = 0; j < 4; j++) acc[k][j] = 0;
-#pragma unroll 1
-  for (int h = 0; h < 2; h++) {  // rolled: 12 loads in flight
-    const uint32_t sa = c.s48[2 * h], sb = c.s48[2 * h + 1];
-    uint4 row[kTileRows + 4];
-    const uint32_t *bp = c.box + (int64_t)(cy0 + 8 * h) * c.stride + 4 * tcx;
+  // table rows 0..19 in five groups of four, each row loaded once (block
+  // row i of candidate row k is table row k + 4 i)
+  const uint32_t *bp = c.box + (int64_t)cy0 * c.stride + 4 * tcx;
 #pragma unroll
-    for (int r = 0; r < kTileRows + 4; r++)
-      row[r] = *reinterpret_cast<const uint4 *>(bp + (int64_t)r * c.stride);
+  for (int g = 0; g < 5; g++) {
+    uint4 row[4];
 #pragma unroll
-    for (int k = 0; k < kTileRows; k++) {
-      const uint32_t a0[4] = {row[k].x, row[k].y, row[k].z, row[k].w};
-      const uint32_t a1[4] = {row[k + 4].x, row[k + 4].y, row[k + 4].z, row[k + 4].w};
+    for (int u = 0; u < 4; u++)
+      row[u] = *reinterpret_cast<const uint4 *>(bp + (int64_t)(4 * g + u) * c.stride);
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        acc[k][j] = __builtin_amdgcn_sad_u16(a1[j], sb, __builtin_amdgcn_sad_u16(a0[j], sa, acc[k][j]));
+    for (int u = 0; u < 4; u++) {
+      const int r = 4 * g + u;
+      const uint32_t a[4] = {row[u].x, row[u].y, row[u].z, row[u].w};
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int k = r - 4 * i;
+        if (k >= 0 && k < kTileRows) {
+#pragma unroll
+          for (int j = 0; j < 4; j++) acc[k][j] = __builtin_amdgcn_sad_u16(a[j], c.s48[i], acc[k][j]);
+        }
+      }
     }
   }
   const SeaRates<SAME> rt(c, jb, hp, cy0, tcx);
