@@ -377,7 +377,7 @@ __global__ __launch_bounds__(kFsThreads) void fs16_kernel(FsArgs a) {
 // source sums gives two block terms: the 8-block bound of a candidate is 4
 // v_sad_u16 from four aligned dwords, the sharper 16-block 4x4 bound 8.
 // Per job:
-//   (1) the 16x16 neighbourhood of mv 0 (clamped into the window; natural
+//   (1) the kSeaNb x kSeaNb neighbourhood of mv 0 (clamped into the window; natural
 //       motion puts the minimum there) is evaluated exactly -> UB;
 //   (2) the window's 4-wide x 8-tall candidate tiles are taken in chunks of
 //       one tile per lane: each lane computes its tile's 8-block bounds (24
@@ -393,6 +393,7 @@ __global__ __launch_bounds__(kFsThreads) void fs16_kernel(FsArgs a) {
 // never overflows.
 constexpr int kSeaList = kFsThreads * 32;  // survivors of one chunk, worst case
 constexpr uint32_t kSeaOut = 1u << 30;
+constexpr int kSeaNb = 8;  // side of the exactly evaluated neighbourhood of mv 0
 
 // Reference rows are read with dword-aligned loads and realigned in
 // registers (v_alignbyte): lane addresses that are not 4-byte aligned make a
@@ -574,14 +575,14 @@ __device__ __forceinline__ void sea_search(const FsArgs &a, const rv_fs_job &jb,
     return ((uint64_t)((sad << 8) + rl) << 32) | (uint32_t)(iy * nx + ix);
   };
 
-  // (1) the 16x16 candidates around mv 0, clamped into the window
+  // (1) the kSeaNb x kSeaNb candidates around mv 0, clamped into the window
   uint64_t bkey = ~0ull;
   {
     int cx = jb.po_x - jb.x_lo, cy = jb.po_y - jb.y_lo;
     cx = cx < 0 ? 0 : cx >= nx ? nx - 1 : cx;
     cy = cy < 0 ? 0 : cy >= ny ? ny - 1 : cy;
-    const int ix = cx - 8 + (tid & 15), iy = cy - 8 + (tid >> 4);
-    if (ix >= 0 && ix < nx && iy >= 0 && iy < ny) {
+    const int ix = cx - kSeaNb / 2 + tid % kSeaNb, iy = cy - kSeaNb / 2 + tid / kSeaNb;
+    if (tid < kSeaNb * kSeaNb && ix >= 0 && ix < nx && iy >= 0 && iy < ny) {
       bkey = exact_key(iy, ix, rate_l(iy, ix));
       atomicMin(&ub_s, (uint32_t)(bkey >> 32));
     }
