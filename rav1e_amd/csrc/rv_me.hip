@@ -393,7 +393,7 @@ __global__ __launch_bounds__(kFsThreads) void fs16_kernel(FsArgs a) {
 // never overflows.
 constexpr int kSeaList = kFsThreads * 32;  // survivors of one chunk, worst case
 constexpr uint32_t kSeaOut = 1u << 30;
-constexpr int kSeaNb = 8;  // side of the exactly evaluated neighbourhood of mv 0
+constexpr int kSeaNb = 4;  // side of the exactly evaluated neighbourhood of mv 0
 
 // Reference rows are read with dword-aligned loads and realigned in
 // registers (v_alignbyte): lane addresses that are not 4-byte aligned make a
