@@ -151,6 +151,73 @@ def timed_run(engine, group, steps, warmup, scales=None, sync=None):
     return group.max(t1 - t0), words
 
 
+def cpu_baseline_and_parity(args, frames, W, H, xdec, ydec, bd, nref, scales):
+    """The CPU baseline and the full-size parity check, from one CPU run.
+
+    The CPU replay (oracle/orc_replay.c: the same schedule over the oracle's
+    restatements; the build for this host's ISA level) runs frames 0..n-1 of
+    the bench's workload on every host thread this process may use, timed,
+    keeping each frame's result words.  A fresh GPU replay then runs the same
+    n frames and its words must equal the CPU's, frame by frame: the bench's
+    own full-size bit-exactness check.  A bounded 1-thread sample (the first
+    superblocks of one GOP) is timed beside it."""
+    import rav1e_amd as R
+    from rav1e_amd import replay as RP
+    from tests import oracle_lib as O  # the checker / CPU baseline only
+    L, isa = O.baseline_lib()
+    threads = O.cpu_share()
+    c = O.CpuReplay(W, H, xdec, ydec, bd, nref, threads=threads, L=L)
+    for s, f in enumerate(frames):
+        c.set_frame(s, f)
+    cpu_words = []
+    n, tc0 = 0, time.perf_counter()
+    while n < len(scales) or (time.perf_counter() - tc0 < args.cpu_seconds and n < 16):
+        c.frame(scales[n % len(scales)])
+        n += 1
+        cpu_words.append(c.results())  # a memcpy; kept inside the timing
+    tc = time.perf_counter() - tc0
+    c.close()
+    # 1 thread: the first 1/8 of the superblocks of one GOP
+    nsb = ((W + 63) // 64) * ((H + 63) // 64)
+    lim = max(1, nsb // 8)
+    c1 = O.CpuReplay(W, H, xdec, ydec, bd, nref, threads=1, L=L)
+    for s, f in enumerate(frames):
+        c1.set_frame(s, f)
+    t1 = time.perf_counter()
+    for i in range(len(scales)):
+        c1.frame(scales[i], lim)
+    t1 = time.perf_counter() - t1
+    c1.close()
+    fps1 = len(scales) * (lim / nsb) / t1
+    cpu = {"value": round(n / tc, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+           "isa": isa,
+           "sample": f"{n} full {args.config} frames (scales {[scales[i % len(scales)] for i in range(n)]}) "
+                     f"of the same replay schedule, oracle/orc_replay.c -O3 -march={isa} on "
+                     f"{threads} host threads",
+           "mpix_per_s": round(n / tc * W * H / 1e6, 3),
+           "one_thread": {"value": round(fps1, 5), "unit": "frames/s",
+                          "sample": f"first {lim} of {nsb} superblocks of each frame of one GOP "
+                                    f"(scales {list(scales)}), scaled to whole frames"}}
+    # the GPU replay over the same frames, word for word
+    g = RP.HipReplay(W, H, xdec, ydec, bd, nref)
+    for s, f in enumerate(frames):
+        g.set_frame(s, f)
+    bad = []
+    for i in range(n):
+        g.frame(scales[i % len(scales)])
+        gw = g.results()
+        d = np.nonzero(gw != cpu_words[i])[0]
+        if d.size:
+            bad.append({"frame": i, "n_diff": int(d.size), "first": int(d[0])})
+    g.close()
+    R._check(R.lib().rv_device_sync(), "rv_device_sync")
+    parity = {"frames": n, "words": int(sum(w.size for w in cpu_words)),
+              "bit_exact": not bad, "vs": "oracle/orc_replay.c (CPU replay)"}
+    if bad:
+        parity["mismatches"] = bad[:8]
+    return cpu, parity
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -204,9 +271,10 @@ def main():
     nsb = ((W + 63) // 64) * ((H + 63) // 64)
     px = 2 if bd > 8 else 1
     # algorithmic bytes per frame of each kernel class; the
-    # SEA search also reads the window's 8x8 box-sum table (u16)
+    # SEA search also reads the box-sum tables: per 4-wide x 8-tall tile of
+    # candidates, 20 rows of 16 B (paired u32 4x8 sums, rv_me.hip)
     fs_bytes = sum(sum((nx + 15) * (ny + 15) * px + 256 * px + 56 +
-                       ((nx + 11) * (ny + 15) * 2 if sea else 0)
+                       (((nx + 3) // 4) * ((ny + 7) // 8) * 20 * 16 if sea else 0)
                        for nx, ny in coarse_windows(W, H, nref, s)) for s in scales) / 4.0
     fs_ops = sum(sum(nx * ny * 256 for nx, ny in coarse_windows(W, H, nref, s))
                  for s in scales) / 4.0
@@ -262,23 +330,10 @@ def main():
                         "frac": round(achv * 1e12 / peak, 4)}
     fps = world * args.steps / dt
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from tests import oracle_lib as O  # the checker / CPU baseline only
-        threads = min(16, os.cpu_count() or 1)
-        c = O.CpuReplay(W, H, xdec, ydec, bd, nref, threads=threads)
-        for s, f in enumerate(frames):
-            c.set_frame(s, f)
-        n, tc0 = 0, time.perf_counter()
-        while n < 4 or (time.perf_counter() - tc0 < args.cpu_seconds and n < 16):
-            c.frame(scales[n % 4])
-            n += 1
-        tc = time.perf_counter() - tc0
-        cpu = {"value": round(n / tc, 4), "unit": "frames/s", "cores": threads, "kind": "port",
-               "sample": f"{n} full {args.config} frames (scales {list(scales)}) of the same "
-                         f"replay schedule, oracle/orc_replay.c -O3 on {threads} host threads",
-               "mpix_per_s": round(n / tc * W * H / 1e6, 3)}
-        c.close()
+        hip.close()  # the parity pass below builds a fresh GPU replay
+        cpu, parity = cpu_baseline_and_parity(args, frames, W, H, xdec, ydec, bd, nref, scales)
 
     if rank == 0:
         line = {
@@ -294,6 +349,7 @@ def main():
             "mpix_per_s": round(fps * W * H / 1e6, 3),
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity,
             "gpu_vs_cpu": round(fps / cpu["value"], 2) if cpu else None,
             "stage_ms": {n: round(float(v), 4) for n, v in
                          zip(["F0_downsample", "F1_full_search", "F2_diamond_half",

@@ -111,7 +111,10 @@ typedef struct rv_plane {
   int32_t xdec;
   int32_t ydec;
   int32_t hbd;        /* 0: u8 pixels, 1: u16 pixels */
-  int32_t reserved;
+  int32_t bit_depth;  /* 8 / 10 / 12; rv_plane_geometry sets 8 for u8 planes
+                         and 0 ("not stated") for u16 ones.  Entry points
+                         whose exactness depends on the range (the SEA box
+                         sums) require it on u16 planes. */
 } rv_plane;
 
 /* Plane::new geometry (src/frame/plane.rs:215-244): fills stride,
@@ -327,7 +330,7 @@ int rv_full_search_batch(const rv_plane *org, const rv_plane *ref,
                          rv_fs_result *d_out, void *stream);
 
 /* Paired box sums of a plane (bit depth <= 10, so every sum fits 16
- * bits), for the successive-elimination search below.  d_box (16-byte
+ * bits; a u16 plane must state bit_depth 9 or 10, else RV_EINVAL), for the successive-elimination search below.  d_box (16-byte
  * aligned) holds two tables with the plane's geometry, n = stride *
  * alloc_height u32 each: entry (ax, ay) of the allocation in [0, n) is
  * S48(ax, ay) | S48(ax + 8, ay) << 16, in [n, 2n) S4(ax, ay) | S4(ax + 4, ay)
@@ -457,6 +460,17 @@ int rv_replay_counters(rv_replay *r, uint64_t *out, int cap);
  * FFI declarations; strides in BYTES (T::to_asm_stride,
  * src/util/mod.rs:185-187).  Host pointers.
  * ------------------------------------------------------------------- */
+
+/* Each calling thread stages its blocks through its own stream, device
+ * scratch and pinned buffer, created on first use.  They are never freed
+ * from a thread-exit destructor (which may run after the HIP runtime is
+ * gone): rv_shims_release() frees the calling thread's context (call it
+ * from a worker before it exits); rv_shims_shutdown() frees every thread's
+ * context (call it once, while HIP is alive, after all threads have stopped
+ * calling the shims).  Unreleased contexts are left to process teardown. */
+void rv_shims_release(void);
+void rv_shims_shutdown(void);
+
 #define RV_DIST_SIZES(X) \
   X(4, 4) X(4, 8) X(8, 4) X(8, 8) X(8, 16) X(16, 8) X(16, 16) X(16, 32) \
   X(32, 16) X(32, 32) X(32, 64) X(64, 32) X(64, 64) X(64, 128) X(128, 64) \

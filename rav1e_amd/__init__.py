@@ -36,7 +36,7 @@ class RvPlane(C.Structure):
                 ("height", C.c_int32), ("xorigin", C.c_int32),
                 ("yorigin", C.c_int32), ("xdec", C.c_int32),
                 ("ydec", C.c_int32), ("hbd", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("bit_depth", C.c_int32)]
 
 
 class RvMv(C.Structure):
@@ -339,22 +339,27 @@ class DevicePlane:
     """A padded plane in HBM with the reference's PlaneConfig geometry
     (Plane::new, src/frame/plane.rs:215-244)."""
 
-    def __init__(self, width, height, xdec=0, ydec=0, xpad=0, ypad=0, hbd=False):
+    def __init__(self, width, height, xdec=0, ydec=0, xpad=0, ypad=0, hbd=False,
+                 bit_depth=None):
         self.desc = RvPlane()
         nbytes = lib().rv_plane_geometry(C.byref(self.desc), width, height, xdec, ydec,
                                          xpad, ypad, 1 if hbd else 0)
+        if bit_depth is not None:
+            self.desc.bit_depth = int(bit_depth)
         self.buf = DeviceBuffer(nbytes)
         self.desc.data = self.buf.ptr
         self.dtype = np.uint16 if hbd else np.uint8
 
     @classmethod
-    def from_array(cls, a: np.ndarray, xpad=0, ypad=0, xdec=0, ydec=0, pad=True):
-        p = cls(a.shape[1], a.shape[0], xdec, ydec, xpad, ypad, a.dtype == np.uint16)
+    def from_array(cls, a: np.ndarray, xpad=0, ypad=0, xdec=0, ydec=0, pad=True,
+                   bit_depth=None):
+        p = cls(a.shape[1], a.shape[0], xdec, ydec, xpad, ypad, a.dtype == np.uint16,
+                bit_depth)
         p.upload_visible(a, pad=pad)
         return p
 
     @classmethod
-    def from_full(cls, full: np.ndarray, xorigin, yorigin, width, height):
+    def from_full(cls, full: np.ndarray, xorigin, yorigin, width, height, bit_depth=None):
         """Wrap a whole padded allocation (stride = full.shape[1])."""
         p = cls.__new__(cls)
         p.desc = RvPlane()
@@ -362,6 +367,7 @@ class DevicePlane:
         p.desc.width, p.desc.height = width, height
         p.desc.xorigin, p.desc.yorigin = xorigin, yorigin
         p.desc.hbd = 1 if full.dtype == np.uint16 else 0
+        p.desc.bit_depth = bit_depth if bit_depth is not None else (0 if p.desc.hbd else 8)
         p.buf = DeviceBuffer.from_array(full)
         p.desc.data = p.buf.ptr
         p.dtype = full.dtype

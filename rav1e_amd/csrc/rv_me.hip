@@ -377,10 +377,12 @@ __global__ __launch_bounds__(kFsThreads) void fs16_kernel(FsArgs a) {
 // source sums gives two block terms: the 8-block bound of a candidate is 4
 // v_sad_u16 from four aligned dwords, the sharper 16-block 4x4 bound 8.
 // Per job:
-//   (1) the kSeaNb x kSeaNb neighbourhood of mv 0 (clamped into the window; natural
-//       motion puts the minimum there) is evaluated exactly -> UB;
+//   (1) the 4x4 (kSeaNb) neighbourhood of mv 0, clamped into the window
+//       (natural motion puts the minimum there), is evaluated exactly -> UB;
+//       a neighbourhood clamped mostly away (mv 0 on a window corner or
+//       outside the window) just gives a looser first UB;
 //   (2) the window's 4-wide x 8-tall candidate tiles are taken in chunks of
-//       one tile per lane: each lane computes its tile's 8-block bounds (24
+//       one tile per lane: each lane computes its tile's 8-block bounds (20
 //       dwordx4 table rows, L2-resident) against the live UB and appends the
 //       survivors to an LDS list (on the replay's content ~1 in 150
 //       candidates; 8x8 quadrants would keep ~9x more); then the list is
@@ -855,8 +857,15 @@ extern "C" int rv_full_search_batch(const rv_plane *org, const rv_plane *ref,
 extern "C" int rv_full_search_sea_batch(const rv_plane *org, const rv_plane *ref,
                                         const uint32_t *d_ref_box, const rv_fs_job *d_jobs, int n,
                                         int allow_hp, rv_fs_result *d_out, void *stream) {
-  if (!ref || !d_ref_box)
+  if (!ref || !d_ref_box || !org)
     return rv_set_error(RV_EINVAL, "rv_full_search_sea_batch: null ref or box-sum table");
+  // the packed 16-bit box sums (and the source's 4x8 sums) hold only for
+  // pixels <= 10 bits: a u16 plane must say so
+  if ((org->hbd && (org->bit_depth < 9 || org->bit_depth > 10)) ||
+      (ref->hbd && (ref->bit_depth < 9 || ref->bit_depth > 10)))
+    return rv_set_error(RV_EINVAL,
+                        "rv_full_search_sea_batch: u16 planes must state bit_depth 9 or 10 "
+                        "(12-bit sums overflow the packed tables: use rv_full_search_batch)");
   return rv_full_search_multi(org, ref, 1, d_jobs, n, 16, 16, 1, allow_hp, d_out, nullptr,
                               &d_ref_box, stream);
 }
@@ -864,6 +873,10 @@ extern "C" int rv_full_search_sea_batch(const rv_plane *org, const rv_plane *ref
 extern "C" int rv_plane_box_sums(const rv_plane *p, uint32_t *d_box, void *stream) {
   if (!p || !p->data || !d_box || p->stride < 1 || p->alloc_height < 1)
     return rv_set_error(RV_EINVAL, "rv_plane_box_sums: bad arguments");
+  if (p->hbd && (p->bit_depth < 9 || p->bit_depth > 10))
+    return rv_set_error(RV_EINVAL,
+                        "rv_plane_box_sums: a u16 plane must state bit_depth 9 or 10 (4x8 "
+                        "sums of 12-bit pixels overflow 16 bits)");
   hipStream_t s = rv_resolve_stream(stream);
   if (p->stride % (p->hbd ? 16 : 32) || ((uintptr_t)p->data & 15) || ((uintptr_t)d_box & 15))
     return rv_set_error(RV_EINVAL, "rv_plane_box_sums: plane stride / alignment not Plane::new's");

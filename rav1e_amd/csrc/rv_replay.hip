@@ -275,6 +275,7 @@ bool alloc_slot(rv_replay *r, RvFrameSlot &s) {
   // input_hres / input_qres (src/encoder.rs:362-377)
   size_t bh = rv_plane_geometry(&s.hres, g.W / 2, g.H / 2, 1, 1, pad / 2, pad / 2, g.hbd);
   size_t bq = rv_plane_geometry(&s.qres, g.W / 4, g.H / 4, 2, 2, pad / 4, pad / 4, g.hbd);
+  s.y.bit_depth = s.u.bit_depth = s.v.bit_depth = s.hres.bit_depth = s.qres.bit_depth = g.bd;
   const size_t al = 256;
   auto up = [&](size_t v) { return (v + al - 1) / al * al; };
   const size_t bs8 = (size_t)s.qres.stride * s.qres.alloc_height * 8;

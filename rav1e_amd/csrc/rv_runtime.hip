@@ -184,6 +184,7 @@ size_t rv_plane_geometry(rv_plane *p, int width, int height, int xdec,
   p->xdec = xdec;
   p->ydec = ydec;
   p->hbd = hbd ? 1 : 0;
+  p->bit_depth = hbd ? 0 : 8;
   p->xorigin = (xpad + m) & ~m;
   p->yorigin = ypad;
   p->stride = (p->xorigin + width + xpad + m) & ~m;

@@ -12,22 +12,35 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+#include <vector>
+
 #include "rv_device.h"
 
 namespace {
 
+// Per-thread staging context.  It has no destructor on purpose: a
+// thread_local destructor runs at thread / process exit, possibly after the
+// HIP runtime has been torn down (a known crash-at-exit of drop-in asm
+// backends).  Contexts are released explicitly by rv_shims_release() (the
+// calling thread's) or rv_shims_shutdown() (all of them), and are otherwise
+// left to the process teardown.
 struct ShimCtx {
   hipStream_t stream = nullptr;
   uint8_t *dev = nullptr;
   uint8_t *host = nullptr;
   size_t cap = 0;
-  ~ShimCtx() {
-    if (dev) (void)hipFree(dev);
-    if (host) (void)hipHostFree(host);
-    if (stream) (void)hipStreamDestroy(stream);
-  }
 };
-thread_local ShimCtx g_ctx;
+thread_local ShimCtx *g_ctx = nullptr;
+std::mutex g_all_mu;
+std::vector<ShimCtx *> g_all;
+
+void free_ctx(ShimCtx *c) {
+  if (c->dev) (void)hipFree(c->dev);
+  if (c->host) (void)hipHostFree(c->host);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
 
 [[noreturn]] void die(const char *what, const char *detail) {
   fprintf(stderr, "rav1e_hip: %s failed: %s\n", what, detail);
@@ -41,7 +54,12 @@ void check_rv(int rc, const char *what) {
 }
 
 ShimCtx &ctx(size_t bytes) {
-  ShimCtx &c = g_ctx;
+  if (!g_ctx) {
+    g_ctx = new ShimCtx();
+    std::lock_guard<std::mutex> lk(g_all_mu);
+    g_all.push_back(g_ctx);
+  }
+  ShimCtx &c = *g_ctx;
   if (!c.stream) check(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking),
                        "hipStreamCreate");
   if (bytes > c.cap) {
@@ -318,3 +336,24 @@ rv_put_fn rv_put_fn_get(int cpu_level, int mode_x, int mode_y) {
 }
 
 }  // extern "C"
+
+extern "C" void rv_shims_release(void) {
+  if (!g_ctx) return;
+  {
+    std::lock_guard<std::mutex> lk(g_all_mu);
+    for (size_t i = 0; i < g_all.size(); i++)
+      if (g_all[i] == g_ctx) {
+        g_all.erase(g_all.begin() + (long)i);
+        break;
+      }
+  }
+  free_ctx(g_ctx);
+  g_ctx = nullptr;
+}
+
+extern "C" void rv_shims_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_all_mu);
+  for (ShimCtx *c : g_all) free_ctx(c);
+  g_all.clear();
+  g_ctx = nullptr;  // other threads' pointers are stale: they must not call again
+}

@@ -354,12 +354,54 @@ def tx_dist(coeffs, rcoeffs, tx_w, tx_h):
     return int(L.orc_tx_dist(coeffs.ctypes.data, rcoeffs.ctypes.data, rcoeffs.size, tx_w, tx_h))
 
 
+_V4_FLAGS = {"avx512f", "avx512bw", "avx512cd", "avx512dq", "avx512vl"}
+_baseline = None
+
+
+def baseline_lib():
+    """The oracle build for the bench's CPU baseline: x86-64-v4 (AVX-512)
+    when this host has it, else the x86-64-v3 (AVX2) build the tests use --
+    "-march=native" resolved on the host that runs the bench (the GPU box's
+    CPU is not this container's).  Returns (ctypes lib, ISA label)."""
+    global _baseline
+    if _baseline is None:
+        flags = set()
+        try:
+            with open("/proc/cpuinfo") as f:
+                for line in f:
+                    if line.startswith("flags"):
+                        flags = set(line.split(":", 1)[1].split())
+                        break
+        except OSError:
+            pass
+        v4 = os.path.join(ROOT, "oracle", "build", "librav1e_oracle_v4.so")
+        if _V4_FLAGS <= flags and os.path.exists(v4):
+            _baseline = (C.CDLL(v4), "x86-64-v4")
+        else:
+            _baseline = (lib(), "x86-64-v3")
+    return _baseline
+
+
+def cpu_share() -> int:
+    """Host threads this process may use: its affinity mask, capped at 16
+    (the GPU box's per-GPU CPU share; os.cpu_count() there reports the whole
+    machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 class CpuReplay:
-    """orc_replay_* (oracle/orc_replay.c): the replay schedule on the CPU."""
+    """orc_replay_* (oracle/orc_replay.c): the replay schedule on the CPU.
+    `L` selects the oracle build (default: the tests' build; the bench's
+    baseline passes baseline_lib()[0])."""
 
     def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, tile=None,
-                 threads=1):
-        L = lib()
+                 threads=1, L=None):
+        L = L or lib()
+        self.L = L
         L.orc_replay_create.restype = C.c_void_p
         L.orc_replay_create.argtypes = [C.c_int] * 11
         L.orc_replay_destroy.argtypes = [C.c_void_p]
@@ -375,20 +417,20 @@ class CpuReplay:
 
     def set_frame(self, slot, yuv):
         yuv = np.ascontiguousarray(yuv)
-        assert lib().orc_replay_set_frame(self.h, slot, yuv.ctypes.data) == 0
+        assert self.L.orc_replay_set_frame(self.h, slot, yuv.ctypes.data) == 0
 
     def frame(self, scale, sb_limit=0):
-        assert lib().orc_replay_frame(self.h, scale, sb_limit) == 0
+        assert self.L.orc_replay_frame(self.h, scale, sb_limit) == 0
 
     def results(self):
         out = np.zeros(self.n_words, dtype=np.uint64)
-        n = lib().orc_replay_results(self.h, out.ctypes.data, out.size)
+        n = self.L.orc_replay_results(self.h, out.ctypes.data, out.size)
         assert n == out.size
         return out
 
     def close(self):
         if self.h:
-            lib().orc_replay_destroy(self.h)
+            self.L.orc_replay_destroy(self.h)
             self.h = None
 
     def __del__(self):

@@ -306,8 +306,8 @@ def _fs_case(rng, hbd, blk, nj, flat=False):
     ref = np.roll(org, (3, -5), (0, 1)) if not flat else np.full_like(org, 77)
     if flat:
         org[:] = 77
-    po_, pr_ = R.DevicePlane.from_array(org, xpad=40, ypad=40), R.DevicePlane.from_array(
-        ref, xpad=40, ypad=40)
+    po_, pr_ = R.DevicePlane.from_array(org, xpad=40, ypad=40, bit_depth=bd), \
+        R.DevicePlane.from_array(ref, xpad=40, ypad=40, bit_depth=bd)
     fo, fr = po_.download_full(), pr_.download_full()
     xo, yo = po_.desc.xorigin, po_.desc.yorigin
     jobs = np.zeros(nj, dtype=R.FS_JOB)
@@ -401,7 +401,7 @@ def test_plane_box_sums_vs_numpy(hbd):
     leaves the allocation is 0."""
     rng = np.random.default_rng(950 + hbd)
     a = rand_plane(rng, 70, 90, 10 if hbd else 8)
-    p = R.DevicePlane.from_array(a, xpad=12, ypad=12)
+    p = R.DevicePlane.from_array(a, xpad=12, ypad=12, bit_depth=10 if hbd else 8)
     full = p.download_full().astype(np.int64)
     got = R.plane_box_sums(p).download(np.uint32).reshape((2,) + full.shape).astype(np.int64)
     ii = np.zeros((full.shape[0] + 1, full.shape[1] + 1), np.int64)
@@ -425,16 +425,20 @@ def test_full_search_sea_pruning_edge_cases(hbd):
     org = rand_plane(rng, 120, 200, bd)
     org[:, :100] = org[:, :100] // 64 * 64  # quantised half: many LB ties
     ref = np.roll(org, (2, 7), (0, 1))
-    po_, pr_ = R.DevicePlane.from_array(org, xpad=24, ypad=24), R.DevicePlane.from_array(
-        ref, xpad=24, ypad=24)
+    po_, pr_ = R.DevicePlane.from_array(org, xpad=24, ypad=24, bit_depth=bd), \
+        R.DevicePlane.from_array(ref, xpad=24, ypad=24, bit_depth=bd)
     fo, fr = po_.download_full(), pr_.download_full()
     xo, yo = po_.desc.xorigin, po_.desc.yorigin
-    jobs = np.zeros(10, dtype=R.FS_JOB)
+    jobs = np.zeros(12, dtype=R.FS_JOB)
     for k in range(len(jobs)):
         px, py = int(rng.integers(0, 200 - 16)), int(rng.integers(0, 120 - 16))
         lam = [0, 40, 3000, (1 << 23) - 1, 1 << 23, (1 << 26) + 5][k % 6]
         if k == 7:  # window far from mv 0: the probe finds nothing
             jobs[k] = (px, py, -24, -24 + 30, -24, -24 + 9, 0, 0, 0, 0, lam, 0)
+            continue
+        if k in (10, 11):  # mv 0 on a window corner: the 4x4 probe mostly clamped away
+            x_lo, y_lo = (px, py) if k == 10 else (px - 30, py - 9)
+            jobs[k] = (px, py, x_lo, x_lo + 30, y_lo, y_lo + 9, 0, 0, 0, 0, lam, 0)
             continue
         jobs[k] = (px, py, max(px - 40, -24), min(px + 40, 200 - 16 + 24), max(py - 12, -24),
                    min(py + 12, 120 - 16 + 24), int(rng.integers(-40, 40)),
@@ -443,6 +447,21 @@ def test_full_search_sea_pruning_edge_cases(hbd):
     for k, j in enumerate(jobs):
         mv, cost = O.full_search(fo, fr, xo, yo, j, 16, 16, 1, 0)
         assert (got[k]["mv_row"], got[k]["mv_col"], got[k]["cost"]) == (mv[0], mv[1], cost), k
+
+
+def test_full_search_sea_rejects_12bit_and_unstated_depth():
+    """The packed 16-bit box sums overflow for 12-bit pixels: the SEA entry
+    points refuse u16 planes that do not state bit_depth 9 or 10."""
+    a = np.full((64, 64), 4000, np.uint16)
+    for bd in (12, None):
+        p = R.DevicePlane.from_array(a, xpad=16, ypad=16, bit_depth=bd)
+        with pytest.raises(R.Rav1eHipError):
+            R.plane_box_sums(p)
+        jobs = np.zeros(1, dtype=R.FS_JOB)
+        jobs[0] = (0, 0, 0, 4, 0, 4, 0, 0, 0, 0, 1, 0)
+        box = R.DeviceBuffer(8 * p.desc.stride * p.desc.alloc_height)
+        with pytest.raises(R.Rav1eHipError):
+            R.full_search_sea_batch(p, p, jobs, s8=box)
 
 
 def test_full_search_empty_window():

@@ -72,3 +72,28 @@ def test_gpu_replay_matches_cpu_replay(w, h, xdec, ydec, bd, refs, tile, flags):
         bad = np.nonzero(gw != cw)[0]
         assert bad.size == 0, (scale, bad[:10], gw[bad[:10]], cw[bad[:10]])
     assert len(g.stage_ms()) == 10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["1080p", "2160p", "2160p10", "2160p444"])
+def test_gpu_replay_full_size_gop(config):
+    """One GOP (me_range_scale 4, 2, 1, 1) at the BASELINE shapes, GPU words
+    equal to the CPU replay's frame by frame."""
+    import bench
+    import rav1e_amd as R
+    R.require_device(0)
+    w, h, xdec, ydec, bd = bench.CONFIGS[config]
+    fr = _frames(w, h, xdec, ydec, bd, 3)
+    g = RP.HipReplay(w, h, xdec, ydec, bd, 2)
+    c = O.CpuReplay(w, h, xdec, ydec, bd, 2, threads=O.cpu_share())
+    for s, f in enumerate(fr):
+        g.set_frame(s, f)
+        c.set_frame(s, f)
+    for i, scale in enumerate(RP.GOP_SCALES):
+        g.frame(scale)
+        c.frame(scale)
+        gw, cw = g.results(), c.results()
+        bad = np.nonzero(gw != cw)[0]
+        assert bad.size == 0, (config, i, scale, bad[:10], gw[bad[:10]], cw[bad[:10]])
+    g.close()
+    c.close()
