@@ -1,0 +1,310 @@
+"""Parity against vectors produced by RUNNING the reference's own Rust text.
+
+tests/golden/ref_{mc,dist,rdo,me,quant,tx}.npz were written by
+tools/refeval/gen_golden_ref.py, which parses the reference functions
+(src/mc.rs put_8tap_ref/prep_8tap_ref/mc_avg_ref, src/dist.rs get_sad_ref/
+get_satd_ref, src/rdo.rs cdef_dist_wxh(_8x8)/sse_wxh, src/me.rs full_search/
+get_mv_rate, src/quantize.rs QuantizationContext::update/quantize/dequantize/
+divu_*, src/transform/{forward,inverse}.rs fht/inv_txfm2d_add) out of
+/root/reference and evaluates them (tools/refeval/rsinterp.py).  The
+reference itself is not read at test time: the fixtures are data.
+
+Unmarked tests pin the CPU oracle (oracle/) to those vectors; the `gpu`
+tests pin the HIP path (through the C ABI) to the same vectors.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from tests import oracle_lib as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, "ref_%s.npz" % name))
+
+
+def px(a, bd):
+    return a.astype(np.uint8 if bd == 8 else np.uint16)
+
+
+def bias_of(x, y):
+    """The compute_bias closure gen_golden_ref.py passed (src/rdo.rs:525-530
+    applies it as (value as f64 * bias) as u64)."""
+    return 0.65 + ((x * 7 + y * 3) % 11) / 8.0
+
+
+def biased(v, x, y):
+    return int(float(v) * bias_of(x, y))
+
+
+def mc_cases(g, bd):
+    k = "mc_bd%d_" % bd
+    cases = g[k + "cases"]
+    offs = np.concatenate([[0], np.cumsum(cases[:, 0] * cases[:, 1])])
+    return px(g[k + "src"], bd), cases, offs
+
+
+# ---- oracle vs reference-evaluated vectors --------------------------------
+@pytest.mark.parametrize("bd", [8, 10, 12])
+def test_oracle_mc_vs_reference(bd):
+    g = load("mc")
+    src, cases, offs = mc_cases(g, bd)
+    put, prep = g["mc_bd%d_put" % bd], g["mc_bd%d_prep" % bd]
+    for i, (w, h, cf, rf, mx, my, x, y) in enumerate(cases):
+        got = O.put_8tap(src, y, x, w, h, cf, rf, mx, my, bd=bd)
+        np.testing.assert_array_equal(got.ravel(), put[offs[i]:offs[i + 1]], err_msg=str(cases[i]))
+        gp = O.prep_8tap(src, y, x, w, h, cf, rf, mx, my, bd=bd)
+        np.testing.assert_array_equal(gp.ravel(), prep[offs[i]:offs[i + 1]], err_msg=str(cases[i]))
+    avg = g["mc_bd%d_avg" % bd]
+    o = 0
+    for i, j in g["mc_bd%d_avg_cases" % bd]:
+        w, h = cases[i][0], cases[i][1]
+        t1 = prep[offs[i]:offs[i + 1]].reshape(h, w)
+        t2 = prep[offs[j]:offs[j + 1]].reshape(h, w)
+        got = O.mc_avg(t1, t2, bd=bd, hbd=int(bd > 8))
+        np.testing.assert_array_equal(got.ravel(), avg[o:o + w * h])
+        o += w * h
+
+
+@pytest.mark.parametrize("bd", [8, 10, 12])
+def test_oracle_sad_satd_vs_reference(bd):
+    g = load("dist")
+    k = "dist_bd%d_" % bd
+    org, ref = px(g[k + "org"], bd), px(g[k + "ref"], bd)
+    for n, (bs, x, y, rx, ry) in enumerate(g[k + "cases"]):
+        w, h = O.block_wh(O.BLOCKS[bs])
+        assert O.get_sad(org, y, x, ref, ry, rx, w, h) == g[k + "sad"][n], (bs, x, y)
+        assert O.get_satd(org, y, x, ref, ry, rx, w, h) == g[k + "satd"][n], (bs, x, y)
+
+
+@pytest.mark.parametrize("bd", [8, 10, 12])
+def test_oracle_cdef_sse_vs_reference(bd):
+    g = load("rdo")
+    k = "rdo_bd%d_" % bd
+    a, b = px(g[k + "a"], bd), px(g[k + "b"], bd)
+    for (x, y), want in zip(g[k + "c8_cases"], g[k + "c8"]):
+        m = O.cdef_moments(a[y:y + 8, x:x + 8].copy(), b[y:y + 8, x:x + 8].copy())
+        assert O.cdef_dist(m, bd) == want, (x, y)
+    for (w, h, x, y), wc, ws in zip(g[k + "blk_cases"], g[k + "cdef"], g[k + "sse"]):
+        tot = 0
+        for j in range(h // 8):
+            for i in range(w // 8):
+                yy, xx = y + 8 * j, x + 8 * i
+                m = O.cdef_moments(a[yy:yy + 8, xx:xx + 8].copy(), b[yy:yy + 8, xx:xx + 8].copy())
+                tot += biased(O.cdef_dist(m, bd), 8 * i, 8 * j)
+        assert tot == wc, (w, h, x, y)
+        sub = O.sse_wxh(a[y:y + h, x:x + w].copy(), b[y:y + h, x:x + w].copy(), w, h)
+        bw, bh = min(w, 8), min(h, 8)
+        tot = sum(biased(v, (n % (w // bw)) * bw, (n // (w // bw)) * bh) for n, v in enumerate(sub))
+        assert tot == ws, (w, h, x, y)
+    for (xdec, ydec, w, h, x, y), want in zip(g[k + "ch_cases"], g[k + "ch_sse"]):
+        sub = O.sse_wxh(a[y:y + h, x:x + w].copy(), b[y:y + h, x:x + w].copy(), w, h,
+                        xdec, ydec)
+        bw, bh = min(w, 8) >> xdec, min(h, 8) >> ydec
+        nx = w // bw
+        tot = sum(biased(v, (n % nx) * bw, (n // nx) * bh) for n, v in enumerate(sub))
+        assert tot == want, (xdec, ydec, w, h, x, y)
+
+
+def fs_job(c):
+    import rav1e_amd as R
+    blk, step, hp, px_, py, x_lo, x_hi, y_lo, y_hi, p0r, p0c, p1r, p1c, lam = (int(v) for v in c)
+    j = np.zeros(1, dtype=R.FS_JOB)[0]
+    j["po_x"], j["po_y"], j["x_lo"], j["x_hi"], j["y_lo"], j["y_hi"] = px_, py, x_lo, x_hi, y_lo, y_hi
+    j["pmv0_row"], j["pmv0_col"], j["pmv1_row"], j["pmv1_col"], j["lambda_"] = p0r, p0c, p1r, p1c, lam
+    return j, blk, step, hp
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_oracle_full_search_vs_reference(bd):
+    g = load("me")
+    k = "me_bd%d_" % bd
+    fo, fr = px(g[k + "org"], bd), px(g[k + "ref"], bd)
+    xo, yo = int(g[k + "geom"][0]), int(g[k + "geom"][1])
+    for n, c in enumerate(g[k + "cases"]):
+        j, blk, step, hp = fs_job(c)
+        mv, cost = O.full_search(fo, fr, xo, yo, j, blk, blk, step, hp)
+        assert (mv[0], mv[1], cost) == (g[k + "mv"][n][0], g[k + "mv"][n][1], g[k + "cost"][n]), n
+
+
+def test_oracle_mv_rate_vs_reference():
+    """get_mv_rate (src/me.rs:1006-1021) through a 1x1-window full search:
+    cost = 256 * sad + rate * lambda with one candidate."""
+    g = load("me")
+    for hp, dr, dc, rate in g["me_mv_rate"]:
+        if abs(dr) % 8 or abs(dc) % 8:
+            continue  # full-pel candidates only
+        a = np.zeros((80, 80), np.uint8)
+        # pmv0 = -mv so that mv - pmv0 is (dr, dc) for the candidate at offset 0
+        j = np.zeros(1, dtype=__import__("rav1e_amd").FS_JOB)[0]
+        j["po_x"] = j["po_y"] = 40
+        j["x_lo"] = j["x_hi"] = 40
+        j["y_lo"] = j["y_hi"] = 40
+        j["pmv0_row"], j["pmv0_col"] = -dr, -dc
+        j["pmv1_row"], j["pmv1_col"] = -dr, -dc
+        j["lambda_"] = 1
+        _, cost = O.full_search(a, a, 0, 0, j, 8, 8, 1, int(hp))
+        assert cost == min(rate, rate + 1), (hp, dr, dc)
+
+
+def test_oracle_quant_vs_reference():
+    g = load("quant")
+    co, q, dq = g["quant_coeffs"], g["quant_q"], g["quant_dq"]
+    for ts, tt, bd, qi, intra, off in g["quant_cases"]:
+        area = O.lib().orc_coded_tx_area(int(ts))
+        c = co[off:off + area]
+        wq, _ = O.quantize(c, int(ts), int(tt), int(qi), int(bd), bool(intra))
+        np.testing.assert_array_equal(wq, q[off:off + area], err_msg=str((ts, tt, bd, qi, intra)))
+        np.testing.assert_array_equal(O.dequantize(wq, int(ts), int(qi), int(bd)),
+                                      dq[off:off + area])
+    for d, x, want in g["quant_divu"]:
+        assert O.divu_pair(int(x), O.divu_gen(int(d))) == want, (d, x)
+
+
+def test_oracle_tx2d_vs_reference():
+    g = load("tx")
+    fin, fout = g["tx_fwd_in"], g["tx_fwd_out"]
+    for ts, tt, bd, off in g["tx_fwd_cases"]:
+        n = (1 << O.TX_W_LOG2[ts]) * (1 << O.TX_H_LOG2[ts])
+        got = O.fwd_txfm2d(fin[off:off + n], int(ts), int(tt), int(bd))
+        np.testing.assert_array_equal(got, fout[off:off + n], err_msg=str((ts, tt, bd)))
+    co, dst, out = g["tx_inv_coeffs"], g["tx_inv_dst"], g["tx_inv_out"]
+    for ts, tt, bd, coff, doff in g["tx_inv_cases"]:
+        w, h = 1 << O.TX_W_LOG2[ts], 1 << O.TX_H_LOG2[ts]
+        nc = min(w, 32) * min(h, 32)
+        d = px(dst[doff:doff + w * h].reshape(h, w), bd)
+        got = O.inv_txfm2d_add(co[coff:coff + nc], d, int(ts), int(tt), int(bd))
+        np.testing.assert_array_equal(got.ravel(), out[doff:doff + w * h],
+                                      err_msg=str((ts, tt, bd)))
+
+
+# ---- HIP path vs reference-evaluated vectors ------------------------------
+@pytest.fixture
+def R():
+    import rav1e_amd
+    rav1e_amd.require_device(0)
+    return rav1e_amd
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bd", [8, 10, 12])
+def test_hip_mc_vs_reference(R, bd):
+    g = load("mc")
+    src, cases, offs = mc_cases(g, bd)
+    put, prep = g["mc_bd%d_put" % bd], g["mc_bd%d_prep" % bd]
+    ps = R.DevicePlane.from_array(src, xpad=16, ypad=16)
+    for i, (w, h, cf, rf, mx, my, x, y) in enumerate(cases):
+        jobs = np.array([(x, y, 0, 0, cf, rf)], dtype=R.MC_JOB)
+        dst = R.DevicePlane(int(w), int(h), 0, 0, 0, 0, bd > 8)
+        R.put_8tap_batch(dst, ps, jobs, int(w), int(h), int(mx), int(my), bd)
+        np.testing.assert_array_equal(dst.download_visible().ravel(), put[offs[i]:offs[i + 1]],
+                                      err_msg=str(cases[i]))
+        gp = R.prep_8tap_batch(ps, jobs, int(w), int(h), int(mx), int(my), bd)
+        np.testing.assert_array_equal(gp.ravel(), prep[offs[i]:offs[i + 1]], err_msg=str(cases[i]))
+    avg = g["mc_bd%d_avg" % bd]
+    o = 0
+    for i, j in g["mc_bd%d_avg_cases" % bd]:
+        w, h = int(cases[i][0]), int(cases[i][1])
+        t1 = prep[offs[i]:offs[i + 1]].reshape(1, h, w)
+        t2 = prep[offs[j]:offs[j + 1]].reshape(1, h, w)
+        dst = R.DevicePlane(w, h, 0, 0, 0, 0, bd > 8)
+        R.mc_avg_batch(dst, t1, t2, np.zeros(1, dtype=R.MC_JOB), w, h, bd)
+        np.testing.assert_array_equal(dst.download_visible().ravel(), avg[o:o + w * h])
+        o += w * h
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bd", [8, 10, 12])
+def test_hip_sad_satd_vs_reference(R, bd):
+    g = load("dist")
+    k = "dist_bd%d_" % bd
+    org = R.DevicePlane.from_array(px(g[k + "org"], bd), xpad=16, ypad=16)
+    ref = R.DevicePlane.from_array(px(g[k + "ref"], bd), xpad=16, ypad=16)
+    for n, (bs, x, y, rx, ry) in enumerate(g[k + "cases"]):
+        w, h = O.block_wh(O.BLOCKS[bs])
+        jobs = np.array([(x, y, rx, ry)], dtype=R.DIST_JOB)
+        assert R.sad_batch(org, ref, jobs, w, h)[0] == g[k + "sad"][n], (bs, x, y)
+        assert R.satd_batch(org, ref, jobs, w, h)[0] == g[k + "satd"][n], (bs, x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bd", [8, 10, 12])
+def test_hip_cdef_sse_vs_reference(R, bd):
+    g = load("rdo")
+    k = "rdo_bd%d_" % bd
+    a, b = px(g[k + "a"], bd), px(g[k + "b"], bd)
+    pa = R.DevicePlane.from_array(a, xpad=16, ypad=16)
+    pb = R.DevicePlane.from_array(b, xpad=16, ypad=16)
+    for (x, y), want in zip(g[k + "c8_cases"], g[k + "c8"]):
+        m = R.cdef_moments_batch(pa, pb, np.array([(x, y, x, y)], dtype=R.DIST_JOB), 8, 8)
+        assert O.cdef_dist(m[0, 0], bd) == want, (x, y)
+    for (w, h, x, y), wc, ws in zip(g[k + "blk_cases"], g[k + "cdef"], g[k + "sse"]):
+        jobs = np.array([(x, y, x, y)], dtype=R.DIST_JOB)
+        m = R.cdef_moments_batch(pa, pb, jobs, int(w), int(h))[0]
+        nx = w // 8
+        tot = sum(biased(O.cdef_dist(m[n], bd), (n % nx) * 8, (n // nx) * 8) for n in range(len(m)))
+        assert tot == wc, (w, h, x, y)
+        sub = R.sse_batch(pa, pb, jobs, int(w), int(h))[0]
+        tot = sum(biased(v, (n % nx) * 8, (n // nx) * 8) for n, v in enumerate(sub))
+        assert tot == ws, (w, h, x, y)
+    for (xdec, ydec, w, h, x, y), want in zip(g[k + "ch_cases"], g[k + "ch_sse"]):
+        ca = R.DevicePlane.from_array(a, xpad=16, ypad=16, xdec=int(xdec), ydec=int(ydec))
+        cb = R.DevicePlane.from_array(b, xpad=16, ypad=16, xdec=int(xdec), ydec=int(ydec))
+        sub = R.sse_batch(ca, cb, np.array([(x, y, x, y)], dtype=R.DIST_JOB), int(w), int(h))[0]
+        bw, bh = min(w, 8) >> xdec, min(h, 8) >> ydec
+        nx = w // bw
+        tot = sum(biased(v, (n % nx) * bw, (n // nx) * bh) for n, v in enumerate(sub))
+        assert tot == want, (xdec, ydec, w, h, x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bd", [8, 10])
+def test_hip_full_search_vs_reference(R, bd):
+    g = load("me")
+    k = "me_bd%d_" % bd
+    fo, fr = px(g[k + "org"], bd), px(g[k + "ref"], bd)
+    xo, yo, W, H = (int(v) for v in g[k + "geom"])
+    po = R.DevicePlane.from_full(fo, xo, yo, W, H, bit_depth=bd)
+    pr = R.DevicePlane.from_full(fr, xo, yo, W, H, bit_depth=bd)
+    for n, c in enumerate(g[k + "cases"]):
+        j, blk, step, hp = fs_job(c)
+        got = R.full_search_batch(po, pr, np.array([j]), blk, blk, step, allow_hp=bool(hp))[0]
+        want = (g[k + "mv"][n][0], g[k + "mv"][n][1], g[k + "cost"][n])
+        assert (got["mv_row"], got["mv_col"], got["cost"]) == want, n
+        if (blk, step) == (16, 1) and bd <= 10:
+            s = R.full_search_sea_batch(po, pr, np.array([j]), allow_hp=bool(hp))[0]
+            assert (s["mv_row"], s["mv_col"], s["cost"]) == want, ("sea", n)
+
+
+@pytest.mark.gpu
+def test_hip_quant_vs_reference(R):
+    g = load("quant")
+    co, q, dq = g["quant_coeffs"], g["quant_q"], g["quant_dq"]
+    for ts, tt, bd, qi, intra, off in g["quant_cases"]:
+        area = R.coded_tx_area(int(ts))
+        c = co[off:off + area].reshape(1, area)
+        gq, gr, _ = R.quantize_batch(c, int(ts), int(tt), int(qi), int(bd), bool(intra))
+        np.testing.assert_array_equal(gq[0], q[off:off + area], err_msg=str((ts, tt, bd, qi)))
+        np.testing.assert_array_equal(gr[0], dq[off:off + area])
+
+
+@pytest.mark.gpu
+def test_hip_tx2d_vs_reference(R):
+    g = load("tx")
+    fin, fout = g["tx_fwd_in"], g["tx_fwd_out"]
+    for ts, tt, bd, off in g["tx_fwd_cases"]:
+        w, h = 1 << O.TX_W_LOG2[ts], 1 << O.TX_H_LOG2[ts]
+        got = R.fwd_txfm_batch(fin[off:off + w * h].reshape(1, h, w), int(ts), int(tt), int(bd))
+        np.testing.assert_array_equal(got[0], fout[off:off + w * h], err_msg=str((ts, tt, bd)))
+    co, dst, out = g["tx_inv_coeffs"], g["tx_inv_dst"], g["tx_inv_out"]
+    for ts, tt, bd, coff, doff in g["tx_inv_cases"]:
+        w, h = 1 << O.TX_W_LOG2[ts], 1 << O.TX_H_LOG2[ts]
+        nc = min(w, 32) * min(h, 32)
+        pd = R.DevicePlane.from_array(px(dst[doff:doff + w * h].reshape(h, w), bd))
+        R.inv_txfm_add_batch(co[coff:coff + nc].reshape(1, nc), pd,
+                             np.array([(0, 0, 0, 0)], dtype=R.TX_JOB), int(ts), int(tt), int(bd))
+        np.testing.assert_array_equal(pd.download_visible().ravel(), out[doff:doff + w * h],
+                                      err_msg=str((ts, tt, bd)))

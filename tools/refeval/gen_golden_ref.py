@@ -1,0 +1,603 @@
+"""Golden vectors produced by RUNNING the reference's own Rust function text.
+
+Run in the build container (needs /root/reference):
+    python tools/refeval/gen_golden_ref.py [section ...]
+
+`rsinterp.py` parses the named reference functions out of
+/root/reference/src and evaluates them; `rshost.py` supplies rav1e's frame
+types over Python lists.  Only the resulting numbers are written
+(tests/golden/ref_*.npz).  Functions evaluated, by section:
+
+  mc    src/mc.rs:182-408      run_filter, get_filter, put_8tap_ref,
+                               prep_8tap_ref, mc_avg_ref (+ SUBPEL_FILTERS)
+  dist  src/dist.rs:25-46,197-328  get_sad_ref, get_satd_ref (8/10/12-bit,
+                               random and maximum-residual planes)
+  rdo   src/rdo.rs:219-335, 511-560  cdef_dist_wxh_8x8, cdef_dist_wxh,
+                               sse_wxh, RawDistortion/Distortion arithmetic
+  me    src/me.rs:943-1021     full_search, get_mv_rate (get_sad -> get_sad_ref)
+  quant src/quantize.rs:34-160, 205-333  QuantizationContext::update /
+                               quantize, dequantize, divu_gen/divu_pair,
+                               dc_q/ac_q, get_log_tx_scale (+ av1_scan_orders)
+  tx    src/transform/forward.rs:1771-1900 FwdTxfm2D::fht and
+        src/transform/inverse.rs:1939-2114 inv_txfm2d_add / inv_txfm2d, over
+        the reference's 1-D kernels (rs2py.py); round_shift_array,
+        get_rect_tx_log_ratio, clamp_value from src/transform/mod.rs.
+
+SIMD note (tx): fht is written over packed_simd lanes (`S::ColSimd::LANES`);
+every operation on those vectors is lane-wise, so the
+function is evaluated with LANES = 1.
+"""
+import os
+import random
+import re
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(__file__))
+import rs2py  # noqa: E402
+import rshost as H  # noqa: E402
+import rsinterp as RI  # noqa: E402
+
+REF = "/root/reference/src/"
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+OUT = os.path.join(ROOT, "tests", "golden")
+
+TX_W_LOG2 = [2, 3, 4, 5, 6, 2, 3, 3, 4, 4, 5, 5, 6, 2, 4, 3, 5, 4, 6]
+TX_H_LOG2 = [2, 3, 4, 5, 6, 3, 2, 4, 3, 5, 4, 6, 5, 4, 2, 5, 3, 6, 4]
+# TxType -> (column 1-D kind, row 1-D kind): 0 Id, 1 Dct, 2 Adst, 3 FlipAdst
+# (src/transform/mod.rs:123-160 TxType order; tx_2d_types)
+TX_COL = [1, 2, 1, 2, 3, 1, 3, 2, 3, 0, 1, 0, 2, 0, 3, 0]
+TX_ROW = [1, 1, 2, 2, 1, 3, 3, 3, 2, 0, 0, 1, 0, 2, 0, 3]
+KIND = {"Id": 0, "Dct": 1, "Adst": 2, "FlipAdst": 3}
+
+
+class TxSizeV(int):
+    """A TxSize enum value (src/transform/mod.rs:162-247)."""
+
+    def __new__(cls, idx):
+        o = int.__new__(cls, idx)
+        o.w, o.h = 1 << TX_W_LOG2[idx], 1 << TX_H_LOG2[idx]
+        return o
+
+    def width(self):
+        return RI.TInt(self.w, "usize")
+
+    def height(self):
+        return RI.TInt(self.h, "usize")
+
+    def area(self):
+        return RI.TInt(self.w * self.h, "usize")
+
+    def width_log2(self):
+        return RI.TInt(TX_W_LOG2[int(self)], "usize")
+
+    def height_log2(self):
+        return RI.TInt(TX_H_LOG2[int(self)], "usize")
+
+
+class _Mem:
+    @staticmethod
+    def size_of_val(v):
+        v = RI.deref(v)
+        return RI.TInt(RI.INT_BITS[RI.ty_of(v)] // 8, "usize")
+
+
+class Fi:
+    """The FrameInvariants fields full_search reads."""
+
+    def __init__(self, bd):
+        self.sequence = RI.Struct("Sequence", {"bit_depth": RI.TInt(bd, "usize")})
+        self.cpu_feature_level = 0
+
+
+def make_interp():
+    env = H.base_env()
+    env.update({"IMPORTANCE_BLOCK_SIZE": RI.TInt(8, "usize"),  # src/encoder.rs:58
+                "MI_SIZE": RI.TInt(4, "usize"),  # src/context.rs:51
+                "mem": _Mem,
+                "Into": type("Into", (), {"into": staticmethod(
+                    lambda v: RI.TInt(int(RI.deref(v)), "usize"))}),
+                "RawDistortion": RI.StructType("RawDistortion"),
+                "Distortion": RI.StructType("Distortion"),
+                "ScaledDistortion": RI.StructType("ScaledDistortion"),
+                "QuantizationContext": RI.StructType("QuantizationContext"),
+                "SUBPEL_FILTER_SIZE": RI.TInt(8, "usize")})
+    I = RI.Interp(env)
+    I.sources = [RI.Source(REF + p) for p in (
+        "util/mod.rs", "mc.rs", "dist.rs", "rdo.rs", "me.rs", "quantize.rs",
+        "transform/mod.rs", "transform/forward.rs", "transform/inverse.rs", "scan_order.rs")]
+    return I
+
+
+def F(I, name, src=None, after=None):
+    if src is not None:
+        I.define_fn(I.sources[[s.path.endswith(src) for s in I.sources].index(True)]
+                    .fn(name, after))
+    elif name not in I.globals.vars:
+        assert I.resolve(name), name
+    return I.globals.vars[name]
+
+
+def src_of(I, tail):
+    return [s for s in I.sources if s.path.endswith(tail)][0]
+
+
+def region_at(plane, x, y):
+    return plane.region(RI.Struct("Area::StartingAt", {"x": x, "y": y}))
+
+
+def prim(bd):
+    return RI.PrimType("u8" if bd == 8 else "u16")
+
+
+def rand_plane(rng, h, w, bd):
+    return rng.integers(0, 1 << bd, (h, w)).astype(np.int64)
+
+
+# ---------------------------------------------------------------- MC
+MC_SIZES = [(4, 4), (8, 4), (4, 8), (8, 8), (16, 16), (16, 8), (8, 16), (4, 16), (16, 4),
+            (32, 32), (32, 8), (64, 64)]
+
+
+def gen_mc(I, rng, out):
+    put, prep, avg = F(I, "put_8tap_ref"), F(I, "prep_8tap_ref"), F(I, "mc_avg_ref")
+    for bd in (8, 10, 12):
+        H_, W_ = 96, 112
+        src = rand_plane(rng, H_, W_, bd)
+        mx = (1 << bd) - 1
+        src[:, 40:48] = np.array([0, 1, 0, 1, 1, 0, 1, 0]) * mx  # clamp stripes
+        src[60:66, :] = mx
+        plane = H.Plane.from_full(src, 0, 0, W_, H_)
+        cases, puts, preps = [], [], []
+        for (w, h) in MC_SIZES:
+            fr = [(0, 0), (int(rng.integers(1, 16)), 0), (0, int(rng.integers(1, 16))),
+                  (int(rng.integers(1, 16)), int(rng.integers(1, 16))),
+                  (int(rng.integers(1, 16)), int(rng.integers(1, 16)))]
+            modes = [(0, 0), (0, 0), (1, 2), (int(rng.integers(0, 4)), int(rng.integers(0, 4))),
+                     (int(rng.integers(0, 4)), int(rng.integers(0, 4)))]
+            for (cf, rf), (mdx, mdy) in zip(fr, modes):
+                x = int(rng.integers(3, W_ - w - 4))
+                y = int(rng.integers(3, H_ - h - 4))
+                if len(cases) % 3 == 0:
+                    x = 38 - w // 2 if w < 40 else 3  # across the stripes
+                dst = H.Plane.from_full(np.zeros((h, w), np.int64), 0, 0, w, h)
+                put(region_at(dst, 0, 0), plane.slice(RI.Struct("PlaneOffset", {"x": x, "y": y})),
+                    RI.TInt(w, "usize"), RI.TInt(h, "usize"), cf, rf, mdx, mdy,
+                    RI.TInt(bd, "usize"), 0, generics={"T": prim(bd)})
+                tmp = [RI.TInt(0, "i16")] * (w * h)
+                prep(RI.Slice(tmp), plane.slice(RI.Struct("PlaneOffset", {"x": x, "y": y})),
+                     RI.TInt(w, "usize"), RI.TInt(h, "usize"), cf, rf, mdx, mdy,
+                     RI.TInt(bd, "usize"), 0, generics={"T": prim(bd)})
+                cases.append((w, h, cf, rf, mdx, mdy, x, y))
+                puts.extend(dst.data)
+                preps.extend(int(v) for v in tmp)
+        # mc_avg over pairs of prep outputs of equal size
+        offs = np.cumsum([0] + [c[0] * c[1] for c in cases])
+        avg_cases, avgs = [], []
+        for i in range(len(cases)):
+            j = (i + 3) % len(cases)
+            while (cases[j][0], cases[j][1]) != (cases[i][0], cases[i][1]):
+                j = (j + 1) % len(cases)
+            w, h = cases[i][0], cases[i][1]
+            t1 = preps[offs[i]:offs[i + 1]]
+            t2 = preps[offs[j]:offs[j + 1]]
+            dst = H.Plane.from_full(np.zeros((h, w), np.int64), 0, 0, w, h)
+            avg(region_at(dst, 0, 0), RI.Slice([RI.TInt(v, "i16") for v in t1]),
+                RI.Slice([RI.TInt(v, "i16") for v in t2]), RI.TInt(w, "usize"),
+                RI.TInt(h, "usize"), RI.TInt(bd, "usize"), 0, generics={"T": prim(bd)})
+            avg_cases.append((i, j))
+            avgs.extend(dst.data)
+        k = "mc_bd%d_" % bd
+        out[k + "src"] = src.astype(np.uint16)
+        out[k + "cases"] = np.array(cases, np.int32)
+        out[k + "put"] = np.array(puts, np.uint16)
+        out[k + "prep"] = np.array(preps, np.int16)
+        out[k + "avg_cases"] = np.array(avg_cases, np.int32)
+        out[k + "avg"] = np.array(avgs, np.uint16)
+        print("mc bd%d: %d put/prep, %d avg" % (bd, len(cases), len(avg_cases)))
+
+
+# ---------------------------------------------------------------- dist
+def gen_dist(I, rng, out):
+    sad, satd = F(I, "get_sad_ref"), F(I, "get_satd_ref")
+    for bd in (8, 10, 12):
+        mx = (1 << bd) - 1
+        H_, W_ = 200, 200
+        org = rand_plane(rng, H_, W_, bd)
+        ref = rand_plane(rng, H_, W_, bd)
+        # maximum-residual corner: org = max, ref = 0 / checkerboard
+        org[:64, :64] = mx
+        ref[:64, :64] = 0
+        yy, xx = np.mgrid[0:64, 0:64]
+        ref[:64, 64:128] = ((yy + xx) & 1) * mx
+        org[:64, 64:128] = (1 - ((yy + xx) & 1)) * mx
+        po = H.Plane.from_full(org, 0, 0, W_, H_)
+        pr = H.Plane.from_full(ref, 0, 0, W_, H_)
+        cases, sads, satds = [], [], []
+        for bs in range(22):
+            b = H.BlockSize.from_width_and_height(*map(int, H.BLOCK_NAMES[bs].split("X")))
+            w, h = b.w, b.h
+            pos = [(0, 0), (64, 0) if w <= 64 and h <= 64 else (0, 0)]
+            pos.append((int(rng.integers(0, W_ - w + 1)), int(rng.integers(0, H_ - h + 1))))
+            for (x, y) in pos:
+                rx, ry = (x, y) if len(cases) % 2 == 0 else (
+                    int(rng.integers(0, W_ - w + 1)), int(rng.integers(0, H_ - h + 1)))
+                a = region_at(po, x, y)
+                r = region_at(pr, rx, ry)
+                g = {"T": prim(bd)}
+                sads.append(int(sad(a, r, b, RI.TInt(bd, "usize"), 0, generics=g)))
+                satds.append(int(satd(a, r, b, RI.TInt(bd, "usize"), 0, generics=g)))
+                cases.append((bs, x, y, rx, ry))
+        k = "dist_bd%d_" % bd
+        out[k + "org"] = org.astype(np.uint16)
+        out[k + "ref"] = ref.astype(np.uint16)
+        out[k + "cases"] = np.array(cases, np.int32)
+        out[k + "sad"] = np.array(sads, np.uint32)
+        out[k + "satd"] = np.array(satds, np.uint32)
+        print("dist bd%d: %d cases" % (bd, len(cases)))
+
+
+# ---------------------------------------------------------------- rdo distortion
+def bias_of(area):
+    """A deterministic non-trivial compute_bias closure (the device returns
+    raw partials; the f64 bias is host arithmetic, src/rdo.rs:525-530)."""
+    x, y = int(area.x), int(area.y)
+    return 0.65 + ((x * 7 + y * 3) % 11) / 8.0
+
+
+def gen_rdo(I, rng, out):
+    rdo = src_of(I, "rdo.rs")
+    for n in ("RawDistortion", "Distortion", "ScaledDistortion"):
+        fns = []
+        for m in re.finditer(r"\bimpl\b[^{;]*\b%s\s*\{" % n, rdo.src):
+            fns += RI.parse_impl_fns(RI.find_item(rdo.src, "impl", n, m.start()))
+        I.define_impl(n, fns)
+    c8 = F(I, "cdef_dist_wxh_8x8", "rdo.rs")
+    cdef = F(I, "cdef_dist_wxh", "rdo.rs")
+    sse = F(I, "sse_wxh", "rdo.rs")
+    for bd in (8, 10, 12):
+        H_, W_ = 96, 96
+        a = rand_plane(rng, H_, W_, bd)
+        b = np.clip(a + rng.integers(-40, 41, a.shape) * (1 << (bd - 8)), 0, (1 << bd) - 1)
+        b[:16, :16] = rand_plane(rng, 16, 16, bd)  # uncorrelated corner
+        pa = H.Plane.from_full(a, 0, 0, W_, H_)
+        pb = H.Plane.from_full(b, 0, 0, W_, H_)
+        c8_cases, c8_vals = [], []
+        for (x, y) in [(0, 0), (8, 0), (40, 24), (88, 88)] + \
+                [(int(rng.integers(0, 89)), int(rng.integers(0, 89))) for _ in range(8)]:
+            v = c8(region_at(pa, x, y), region_at(pb, x, y), RI.TInt(bd, "usize"),
+                   generics={"T": prim(bd)})
+            c8_cases.append((x, y))
+            c8_vals.append(int(v._f["0"]))
+        blk_cases, cdef_vals, sse_vals = [], [], []
+        for (w, h, x, y) in [(8, 8, 0, 0), (64, 64, 0, 0), (32, 16, 40, 24), (16, 32, 8, 56),
+                             (64, 32, 32, 64)]:
+            bias = (lambda area, bsize: bias_of(area))
+            d = cdef(region_at(pa, x, y), region_at(pb, x, y), RI.TInt(w, "usize"),
+                     RI.TInt(h, "usize"), RI.TInt(bd, "usize"), bias, generics={"T": prim(bd)})
+            s = sse(region_at(pa, x, y), region_at(pb, x, y), RI.TInt(w, "usize"),
+                    RI.TInt(h, "usize"), bias, generics={"T": prim(bd)})
+            blk_cases.append((w, h, x, y))
+            cdef_vals.append(int(d._f["0"]))
+            sse_vals.append(int(s._f["0"]))
+        # chroma planes (4:2:0 and 4:2:2): sse over importance sub-blocks >> dec
+        ch_cases, ch_vals = [], []
+        for xdec, ydec in ((1, 1), (1, 0)):
+            qa = H.Plane.from_full(a, 0, 0, W_, H_, xdec, ydec)
+            qb = H.Plane.from_full(b, 0, 0, W_, H_, xdec, ydec)
+            for (w, h, x, y) in [(32, 32, 0, 0), (16, 16, 12, 20), (8, 8, 40, 4)]:
+                s = sse(region_at(qa, x, y), region_at(qb, x, y), RI.TInt(w, "usize"),
+                        RI.TInt(h, "usize"), lambda area, bsize: bias_of(area),
+                        generics={"T": prim(bd)})
+                ch_cases.append((xdec, ydec, w, h, x, y))
+                ch_vals.append(int(s._f["0"]))
+        k = "rdo_bd%d_" % bd
+        out[k + "a"] = a.astype(np.uint16)
+        out[k + "b"] = b.astype(np.uint16)
+        out[k + "c8_cases"] = np.array(c8_cases, np.int32)
+        out[k + "c8"] = np.array(c8_vals, np.uint64)
+        out[k + "blk_cases"] = np.array(blk_cases, np.int32)
+        out[k + "cdef"] = np.array(cdef_vals, np.uint64)
+        out[k + "sse"] = np.array(sse_vals, np.uint64)
+        out[k + "ch_cases"] = np.array(ch_cases, np.int32)
+        out[k + "ch_sse"] = np.array(ch_vals, np.uint64)
+        print("rdo bd%d" % bd)
+
+
+# ---------------------------------------------------------------- motion search
+def gen_me(I, rng, out):
+    fs = F(I, "full_search", "me.rs")
+    sad_ref = F(I, "get_sad_ref")
+    for bd in (8, 10):
+        pad = 24
+        H_, W_ = 64, 96
+        org = rand_plane(rng, H_, W_, bd)
+        ref = np.roll(org, (3, -5), (0, 1))
+        ref = np.clip(ref + rng.integers(-2, 3, ref.shape), 0, (1 << bd) - 1)
+        ref[40:, 60:] = 77 << (bd - 8)  # flat area: ties resolve to the first raster candidate
+        org[40:, 60:] = 77 << (bd - 8)
+        fo = np.pad(org, pad, mode="edge")
+        fr = np.pad(ref, pad, mode="edge")
+        po = H.Plane.from_full(fo, pad, pad, W_, H_)
+        pr = H.Plane.from_full(fr, pad, pad, W_, H_)
+        I.globals.vars["get_sad"] = (
+            lambda a, b, bs, bd_, cpu, _g={"T": prim(bd)}: sad_ref(a, b, bs, bd_, cpu, generics=_g))
+        cases, res = [], []
+        for k in range(10):
+            blk = [8, 16, 16, 8, 16, 16, 16, 8, 16, 16][k]
+            step = [1, 1, 2, 1, 1, 1, 1, 3, 1, 1][k]
+            if k == 5:
+                px, py = 64, 44  # inside the flat area
+            elif k == 6:
+                px, py = 0, 0  # window crosses the padding
+            else:
+                px, py = int(rng.integers(0, W_ - blk)), int(rng.integers(0, H_ - blk))
+            rx, ry = int(rng.integers(4, 14)), int(rng.integers(3, 9))
+            x_lo, x_hi = max(px - rx, -pad + 4), min(px + rx, W_ - blk + pad - 4)
+            y_lo, y_hi = max(py - ry, -pad + 4), min(py + ry, H_ - blk + pad - 4)
+            pm0 = (int(rng.integers(-40, 40)), int(rng.integers(-40, 40)))
+            pm1 = (int(rng.integers(-40, 40)), int(rng.integers(-40, 40)))
+            lam = int(rng.integers(0, 3000)) if k != 4 else 0
+            hp = k % 2
+            best = [H.motion_vector(0, 0)]
+            cost = [RI.TInt(2 ** 64 - 1, "u64")]
+            best_ref = RI.Ref(lambda: best[0], lambda v: best.__setitem__(0, v))
+            cost_ref = RI.Ref(lambda: cost[0], lambda v: cost.__setitem__(0, v))
+            bsize = H.BlockSize.from_width_and_height(blk, blk)
+            fs(Fi(bd), RI.TInt(x_lo, "isize"), RI.TInt(x_hi, "isize"), RI.TInt(y_lo, "isize"),
+               RI.TInt(y_hi, "isize"), bsize, po, pr, best_ref, cost_ref,
+               RI.Struct("PlaneOffset", {"x": RI.TInt(px, "isize"), "y": RI.TInt(py, "isize")}),
+               RI.TInt(step, "usize"), RI.TInt(lam, "u32"),
+               [H.motion_vector(*pm0), H.motion_vector(*pm1)], bool(hp), generics={"T": prim(bd)})
+            cases.append((blk, step, hp, px, py, x_lo, x_hi, y_lo, y_hi, pm0[0], pm0[1],
+                          pm1[0], pm1[1], lam))
+            res.append((int(best[0].row), int(best[0].col), int(cost[0])))
+        kk = "me_bd%d_" % bd
+        out[kk + "org"] = fo.astype(np.uint16)
+        out[kk + "ref"] = fr.astype(np.uint16)
+        out[kk + "geom"] = np.array([pad, pad, W_, H_], np.int32)
+        out[kk + "cases"] = np.array(cases, np.int64)
+        out[kk + "mv"] = np.array([r[:2] for r in res], np.int16)
+        out[kk + "cost"] = np.array([r[2] for r in res], np.uint64)
+        print("me bd%d: %d searches" % (bd, len(cases)))
+    # get_mv_rate on its own over a grid of differences
+    rate = F(I, "get_mv_rate", "me.rs")
+    g = []
+    for hp in (False, True):
+        for dr in (-300, -17, -8, -1, 0, 1, 2, 3, 7, 8, 255, 4000):
+            for dc in (-9, 0, 5, 64):
+                g.append((int(hp), dr, dc, int(rate(H.motion_vector(dr, dc), H.motion_vector(0, 0),
+                                                    hp))))
+    out["me_mv_rate"] = np.array(g, np.int32)
+
+
+# ---------------------------------------------------------------- quantizer
+def gen_quant(I, rng, out):
+    q = src_of(I, "quantize.rs")
+    I.define_impl("QuantizationContext", q.impl("QuantizationContext", "impl QuantizationContext"))
+    deq = F(I, "dequantize", "quantize.rs")
+    I.globals.vars["TxSize"] = type("TxSizeNS", (), {})
+    cases, qout, dqout, coeffs_all = [], [], [], []
+    for ts in range(19):
+        w, h = 1 << TX_W_LOG2[ts], 1 << TX_H_LOG2[ts]
+        area = min(w, 32) * min(h, 32)
+        types = [0, 9] if max(w, h) <= 16 else [0]
+        if max(w, h) <= 16:
+            types += [int(rng.integers(1, 16))]
+        for tt in types:
+            if max(w, h) == 64 and tt != 0:
+                continue
+            for bd in (8, 10, 12):
+                for qi, intra in ((100, False), (int(rng.integers(1, 256)), True),
+                                  (int(rng.integers(1, 256)), False)):
+                    sc = 1 << (bd - 8)
+                    co = (rng.laplace(0, 40 * sc, area) * np.exp(-np.arange(area) / (area / 4)))
+                    co = co.astype(np.int64)
+                    co[0] = int(rng.integers(-2000 * sc, 2000 * sc))
+                    ctx = RI.Struct("QuantizationContext", {
+                        "log_tx_scale": RI.TInt(0, "usize"), "dc_quant": RI.TInt(0, "u32"),
+                        "dc_offset": RI.TInt(0, "i32"), "dc_mul_add": (0, 0, 0),
+                        "ac_quant": RI.TInt(0, "u32"), "ac_offset_eob": RI.TInt(0, "i32"),
+                        "ac_offset0": RI.TInt(0, "i32"), "ac_offset1": RI.TInt(0, "i32"),
+                        "ac_mul_add": (0, 0, 0)})
+                    upd = I.make_method("QuantizationContext", "update", ctx, I.globals)
+                    upd(RI.TInt(qi, "u8"), TxSizeV(ts), intra, RI.TInt(bd, "usize"),
+                        RI.TInt(0, "i8"), RI.TInt(0, "i8"))
+                    quant = I.make_fn(q.fn("quantize", "impl QuantizationContext"), I.globals)
+                    cin = [RI.TInt(int(v), "i32") for v in co]
+                    qc = [RI.TInt(0, "i32")] * area
+                    quant(ctx, RI.Slice(cin), RI.Slice(qc), TxSizeV(ts), RI.TInt(tt, "usize"),
+                          generics={"T": RI.PrimType("i32")},
+                          bind={"Self": I.globals.vars["QuantizationContext"]})
+                    rc = [RI.TInt(0, "i32")] * area
+                    deq(RI.TInt(qi, "u8"), RI.Slice(list(qc)), RI.Slice(rc), TxSizeV(ts),
+                        RI.TInt(bd, "usize"), RI.TInt(0, "i8"), RI.TInt(0, "i8"))
+                    cases.append((ts, tt, bd, qi, int(intra), len(coeffs_all)))
+                    coeffs_all.extend(int(v) for v in co)
+                    qout.extend(int(v) for v in qc)
+                    dqout.extend(int(v) for v in rc)
+    out["quant_cases"] = np.array(cases, np.int32)
+    out["quant_coeffs"] = np.array(coeffs_all, np.int32)
+    out["quant_q"] = np.array(qout, np.int32)
+    out["quant_dq"] = np.array(dqout, np.int32)
+    divu = []
+    gen, pair = F(I, "divu_gen", "quantize.rs"), F(I, "divu_pair", "quantize.rs")
+    for d in (1, 2, 3, 4, 7, 8, 100, 1000, 1337, 21387, 65535):
+        dg = gen(RI.TInt(d, "u32"))
+        for x in (-70000, -1001, -1, 0, 1, 5, 999, 123456, 2 ** 20 + 3):
+            divu.append((d, x, int(pair(RI.TInt(x, "i32"), dg))))
+    out["quant_divu"] = np.array(divu, np.int64)
+    print("quant: %d blocks" % len(cases))
+
+
+# ---------------------------------------------------------------- transforms
+class Lane1:
+    """packed_simd vector types at LANES = 1 (see module docstring)."""
+    LANES = RI.TInt(1, "usize")
+
+    @staticmethod
+    def load_from_slice(s):
+        return RI.as_slice(s)[0]
+
+    @staticmethod
+    def slice_cast_ref(s):
+        return s
+
+    slice_cast_mut = slice_cast_ref
+
+    @staticmethod
+    def _splat(v):
+        return v
+
+
+class AlignedArray:
+    def __init__(self, arr):
+        self.array = arr
+
+    @staticmethod
+    def uninitialized():
+        return AlignedArray([RI.TInt(0, "i32")] * (64 * 64))
+
+    @staticmethod
+    def new(arr):
+        return AlignedArray(arr)
+
+    def index_range(self, r):
+        return RI.index_get(self.array, r)
+
+    def as_slice(self):
+        return RI.Slice(self.array)
+
+
+def tx_tables(I):
+    fwd = src_of(I, "transform/forward.rs")
+    inv = src_of(I, "transform/inverse.rs")
+    ns = rs2py.load()
+    # 1-D forward kernel per (kind, n): the reference's txfm_types::d! table
+    blk = fwd.raw[fwd.raw.index("pub mod txfm_types"):]
+    f1 = {}
+    for m in re.finditer(r"\((Dct|Adst|FlipAdst|Id),\s*(\d+),\s*(\w+),\s*\)", blk):
+        f1[(KIND[m.group(1)], int(m.group(2)))] = ns[m.group(3)]
+    # inverse 1-D kernel per (kind, n): inverse.rs txfm_types::d! (FlipAdst and
+    # the 32/64-point Adst are `unimplemented!` there, so never reached)
+    iblk = inv.raw[inv.raw.index("mod txfm_types"):]
+    iblk = iblk[:iblk.index("unimplemented inversions")]
+    i1 = {}
+    for m in re.finditer(r"\((Dct|Adst|FlipAdst|Id),\s*(\d+),\s*(\w+),\s*\)", iblk):
+        i1[(KIND[m.group(1)], int(m.group(2)))] = ns[m.group(3)]
+    # InvBlock::INTERMEDIATE_SHIFT from the impl_inv_txs! invocations
+    ish = {}
+    for m in re.finditer(r"impl_inv_txs!\s*\{\s*([^}]*)\}", inv.src):
+        body = m.group(1)
+        if "$" in body:
+            continue
+        sh = int(body.strip().split()[-1])
+        for w, h in re.findall(r"\((\d+),\s*(\d+)\)", body):
+            ish[(int(w), int(h))] = sh
+    return f1, i1, ish
+
+
+class _NS:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def gen_tx(I, rng, out):
+    f1, i1, ish = tx_tables(I)
+    fwd = src_of(I, "transform/forward.rs")
+    inv = src_of(I, "transform/inverse.rs")
+    fht = fwd.fn("fht", "impl<P, S, T> FwdTxfm2D<P> for (S, T)")
+    itx2 = inv.fn("inv_txfm2d", "type ColTxfm = ")
+    itx_add = inv.fn("inv_txfm2d_add", "type ColTxfm = ")
+    I.globals.vars["AlignedArray"] = AlignedArray
+    I.globals.vars["round_shift_array"] = I.make_fn(
+        src_of(I, "transform/mod.rs").fn("round_shift_array"), I.globals)
+    I.globals.vars["PixelType"] = _NS(U8=0, U16=1)
+    nocall = [[None] * 4 for _ in range(4)]
+    I.globals.vars["kernels"] = _NS(U8_INV_TX_ADD_KERNELS=[[nocall] * 22],
+                                    U16_INV_TX_ADD_KERNELS=[[nocall] * 22])
+    cases_f, fin, fout, cases_i, icoef, idst, iout = [], [], [], [], [], [], []
+    for ts in range(19):
+        w, h = 1 << TX_W_LOG2[ts], 1 << TX_H_LOG2[ts]
+        shift = fwd.load_static(I, "FWD_SHIFT_%dX%d" % (w, h))
+        size = _NS(W=RI.TInt(w, "usize"), H=RI.TInt(h, "usize"), WIDTH=RI.TInt(w, "usize"),
+                   HEIGHT=RI.TInt(h, "usize"), AREA=RI.TInt(w * h, "usize"),
+                   ColSimd=Lane1, RowSimd=Lane1, IColSimd=Lane1,
+                   INTERMEDIATE_SHIFT=RI.TInt(ish[(w, h)], "u16"))
+        for tt in range(16):
+            ck, rk = TX_COL[tt], TX_ROW[tt]
+            for bd in (8, 10, 12):
+                if rk != 3 and (ck, h) in f1 and (rk, w) in f1:
+                    ctx = _NS(Size=size, SHIFT=shift,
+                              Col=_NS(FLIPPED=ck == 3), Row=_NS(FLIPPED=rk == 3),
+                              ColTx=_NS(forward=lambda i, o, f=f1[(ck, h)]: f(i, o)),
+                              RowTx=_NS(forward=lambda i, o, f=f1[(rk, w)]: f(i, o)))
+                    amp = (1 << bd) - 1
+                    res = [int(v) for v in rng.integers(-amp, amp + 1, w * h)]
+                    if len(cases_f) % 4 == 0:  # extreme residuals
+                        res = [amp if (k * 7 + k // w) % 3 else -amp for k in range(w * h)]
+                    co = [RI.TInt(0, "i32")] * (w * h)
+                    fn = I.make_fn(fht, I.globals)
+                    fn(RI.Slice([RI.TInt(v, "i16") for v in res]), RI.Slice(co),
+                       RI.TInt(bd, "usize"), bind={"Self": ctx, "S": size})
+                    cases_f.append((ts, tt, bd, len(fin)))
+                    fin.extend(res)
+                    fout.extend(int(v) for v in co)
+                if (ck, h) in i1 and (rk, w) in i1 and bd in (8, 10, 12):
+                    cw, ch = min(w, 32), min(h, 32)
+                    co = [0] * (cw * ch)
+                    for k in range(cw * ch):
+                        if rng.random() < 0.3:
+                            co[k] = int(rng.integers(-(1 << (bd + 3)), 1 << (bd + 3)))
+                    co[0] = int(rng.integers(-(1 << (bd + 6)), 1 << (bd + 6)))
+                    dst = rand_plane(rng, h, w, bd)
+                    pd = H.Plane.from_full(dst.copy(), 0, 0, w, h)
+                    ictx = _NS(Size=size, RowTxfm=_NS(inverse=lambda i, o, r, f=i1[(rk, w)]:
+                                                      f(i, o, r)),
+                               ColTxfm=_NS(inverse=lambda i, o, r, f=i1[(ck, h)]: f(i, o, r)))
+                    tt_ns = _NS(Row=_NS(TBL_IDX=0), Col=_NS(TBL_IDX=0), TX_TYPE=tt)
+                    inner = I.make_fn(itx2, I.globals)
+                    ictx.inv_txfm2d = (lambda *a, _f=inner, _c=ictx, _s=size:
+                                       _f(*a, bind={"Self": _c, "S": _s}))
+                    pt = prim(bd)
+                    pt.type_enum = lambda _b=bd: 0 if _b == 8 else 1
+                    fn = I.make_fn(itx_add, I.globals)
+                    fn(RI.Slice([RI.TInt(v, "i32") for v in co] + [RI.TInt(0, "i32")] * 32),
+                       region_at(pd, 0, 0), RI.TInt(bd, "usize"), H.base_env()["CpuFeatureLevel"],
+                       bind={"Self": ictx, "S": size, "T": tt_ns, "P": pt})
+                    cases_i.append((ts, tt, bd, len(icoef), len(idst)))
+                    icoef.extend(co)
+                    idst.extend(int(v) for v in dst.reshape(-1))
+                    iout.extend(pd.data)
+        print("tx size %d done (%d fwd, %d inv)" % (ts, len(cases_f), len(cases_i)))
+    out["tx_fwd_cases"] = np.array(cases_f, np.int32)
+    out["tx_fwd_in"] = np.array(fin, np.int16)
+    out["tx_fwd_out"] = np.array(fout, np.int32)
+    out["tx_inv_cases"] = np.array(cases_i, np.int32)
+    out["tx_inv_coeffs"] = np.array(icoef, np.int32)
+    out["tx_inv_dst"] = np.array(idst, np.uint16)
+    out["tx_inv_out"] = np.array(iout, np.uint16)
+
+
+SECTIONS = {"mc": gen_mc, "dist": gen_dist, "rdo": gen_rdo, "me": gen_me, "quant": gen_quant,
+            "tx": gen_tx}
+
+
+def main(argv):
+    names = argv or list(SECTIONS)
+    os.makedirs(OUT, exist_ok=True)
+    for n in names:
+        I = make_interp()
+        rng = np.random.default_rng(0x5EED + sorted(SECTIONS).index(n))
+        random.seed(1)
+        out = {}
+        t = time.time()
+        SECTIONS[n](I, rng, out)
+        np.savez_compressed(os.path.join(OUT, "ref_%s.npz" % n), **out)
+        print("%s: %.1f s" % (n, time.time() - t))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -158,7 +158,8 @@ def clamp_value(v, bit):
 
 
 def round_shift(v, bit):
-    return _chk((v + ((1 << bit) >> 1)) >> bit)
+    # src/util/mod.rs:241-243: `value: i32` is already wrapped, and so is the add
+    return _chk(_chk(_chk(v) + ((1 << bit) >> 1)) >> bit)
 
 
 class View:
