@@ -267,8 +267,10 @@ def test_hip_full_search_vs_reference(R, bd):
     k = "me_bd%d_" % bd
     fo, fr = px(g[k + "org"], bd), px(g[k + "ref"], bd)
     xo, yo, W, H = (int(v) for v in g[k + "geom"])
-    po = R.DevicePlane.from_full(fo, xo, yo, W, H, bit_depth=bd)
-    pr = R.DevicePlane.from_full(fr, xo, yo, W, H, bit_depth=bd)
+    # the fixture's padding is edge replication (np.pad "edge"), so Plane::new
+    # geometry with replicated padding holds the same pixels the windows read
+    po = R.DevicePlane.from_array(fo[yo:yo + H, xo:xo + W], xpad=xo, ypad=yo, bit_depth=bd)
+    pr = R.DevicePlane.from_array(fr[yo:yo + H, xo:xo + W], xpad=xo, ypad=yo, bit_depth=bd)
     for n, c in enumerate(g[k + "cases"]):
         j, blk, step, hp = fs_job(c)
         got = R.full_search_batch(po, pr, np.array([j]), blk, blk, step, allow_hp=bool(hp))[0]
@@ -308,3 +310,57 @@ def test_hip_tx2d_vs_reference(R):
                              np.array([(0, 0, 0, 0)], dtype=R.TX_JOB), int(ts), int(tt), int(bd))
         np.testing.assert_array_equal(pd.download_visible().ravel(), out[doff:doff + w * h],
                                       err_msg=str((ts, tt, bd)))
+
+
+# ---- diamond / telescopic sub-pel searches ---------------------------------
+def ds_case(c):
+    import rav1e_amd as R
+    c = [int(v) for v in c]
+    w, h, sub, satd, hp, kind, px_, py = c[:8]
+    j = np.zeros(1, dtype=R.DS_JOB)[0]
+    j["po_x"], j["po_y"] = px_, py
+    j["mvx_min"], j["mvx_max"], j["mvy_min"], j["mvy_max"] = c[8:12]
+    j["pmv0_row"], j["pmv0_col"], j["pmv1_row"], j["pmv1_col"] = c[12:16]
+    j["lambda_"], j["n_pred"] = c[16], c[17]
+    j["pred"][:] = np.array(c[18:34]).reshape(8, 2)
+    start = (c[34], c[35])
+    start_cost = c[36] | (c[37] << 32)
+    return w, h, sub, satd, hp, kind, j, start, start_cost
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_oracle_diamond_subpel_vs_reference(bd):
+    g = load("ds")
+    k = "ds_bd%d_" % bd
+    fo, fr = px(g[k + "org"], bd), px(g[k + "ref"], bd)
+    xo, yo, W, H = (int(v) for v in g[k + "geom"])
+    for n, c in enumerate(g[k + "cases"]):
+        w, h, sub, satd, hp, kind, j, start, sc = ds_case(c)
+        if kind == 0:
+            mv, cost = O.diamond_search(fo, fr, xo, yo, W, H, j, w, h, sub, satd, hp, bd)
+        else:
+            mv, cost = O.telescopic_subpel(fo, fr, xo, yo, W, H, j, w, h, satd, hp, bd, start, sc)
+        want = (g[k + "mv"][n][0], g[k + "mv"][n][1], g[k + "cost"][n])
+        assert (mv[0], mv[1], cost) == want, (n, mv, cost, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bd", [8, 10])
+def test_hip_diamond_subpel_vs_reference(R, bd):
+    g = load("ds")
+    k = "ds_bd%d_" % bd
+    fo, fr = px(g[k + "org"], bd), px(g[k + "ref"], bd)
+    xo, yo, W, H = (int(v) for v in g[k + "geom"])
+    po = R.DevicePlane.from_array(fo[yo:yo + H, xo:xo + W], xpad=xo, ypad=yo, bit_depth=bd)
+    pr = R.DevicePlane.from_array(fr[yo:yo + H, xo:xo + W], xpad=xo, ypad=yo, bit_depth=bd)
+    for n, c in enumerate(g[k + "cases"]):
+        w, h, sub, satd, hp, kind, j, start, sc = ds_case(c)
+        jobs = np.array([j])
+        if kind == 0:
+            got = R.diamond_search_batch(po, pr, jobs, w, h, bool(sub), bool(satd), bool(hp), bd)[0]
+        else:
+            st = np.zeros(1, dtype=R.FS_RESULT)
+            st[0]["mv_row"], st[0]["mv_col"], st[0]["cost"] = start[0], start[1], sc
+            got = R.telescopic_subpel_batch(po, pr, jobs, st, w, h, bool(satd), bool(hp), bd)[0]
+        want = (g[k + "mv"][n][0], g[k + "mv"][n][1], g[k + "cost"][n])
+        assert (got["mv_row"], got["mv_col"], got["cost"]) == want, (n, got, want)

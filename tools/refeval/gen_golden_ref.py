@@ -15,6 +15,11 @@ types over Python lists.  Only the resulting numbers are written
   rdo   src/rdo.rs:219-335, 511-560  cdef_dist_wxh_8x8, cdef_dist_wxh,
                                sse_wxh, RawDistortion/Distortion arithmetic
   me    src/me.rs:943-1021     full_search, get_mv_rate (get_sad -> get_sad_ref)
+  ds    src/me.rs:654-941      get_best_predictor, diamond_me_search,
+                               get_mv_rd_cost, compute_mv_rd_cost,
+                               telescopic_subpel_search; src/predict.rs:255-338
+                               predict_inter (+ get_params); TileRect
+                               (src/tiling/tile.rs); put/prep/avg -> *_ref
   quant src/quantize.rs:34-160, 205-333  QuantizationContext::update /
                                quantize, dequantize, divu_gen/divu_pair,
                                dc_q/ac_q, get_log_tx_scale (+ av1_scan_orders)
@@ -373,6 +378,128 @@ def gen_me(I, rng, out):
     out["me_mv_rate"] = np.array(g, np.int32)
 
 
+# ---------------------------------------------------------------- diamond / sub-pel
+class RefV(int):
+    """RefType (src/frame/mod.rs / context: INTRA_FRAME = 0 .. NONE_FRAME)."""
+
+    def to_index(self):
+        return RI.TInt(int(self) - 1, "usize")
+
+
+class _RefType:
+    INTRA_FRAME, LAST_FRAME, NONE_FRAME = RefV(0), RefV(1), RefV(8)
+
+
+class PredModeV(int):
+    """PredictionMode::NEWMV; is_intra() is `self < NEARESTMV` (predict.rs:243)."""
+    interp = None
+
+    def is_intra(self):
+        return False
+
+    def predict_inter(self, *args):
+        return PredModeV.fn(self, *args, generics={"T": PredModeV.pixel})
+
+
+class DsFi(Fi):
+    """FrameInvariants fields the diamond / sub-pel searches and predict_inter read."""
+
+    def __init__(self, bd, ref_plane, allow_hp):
+        super().__init__(bd)
+        self.allow_high_precision_mv = bool(allow_hp)
+        self.default_filter = RI.TInt(0, "usize")  # REGULAR (src/encoder.rs:705)
+        rec = RI.Struct("ReferenceFrame", {"frame": RI.Struct("Frame", {"planes": [ref_plane]})})
+        self.rec_buffer = RI.Struct("ReferenceFramesSet", {"frames": [rec] * 8})
+        self.ref_frames = [RI.TInt(0, "u8")] * 7
+
+
+def gen_ds(I, rng, out):
+    tile = RI.Source(REF + "tiling/tile.rs")
+    I.define_impl("TileRect", tile.impl("TileRect"))
+    I.globals.vars["TileRect"] = RI.StructType("TileRect")
+    I.globals.vars["RefType"] = _RefType
+    I.globals.vars["NONE_FRAME"] = _RefType.NONE_FRAME
+    I.globals.vars["PredictionMode"] = type("PM", (), {"NEWMV": PredModeV(16)})
+    I.globals.vars["Plane"] = type("PlaneNS", (), {"new": staticmethod(
+        lambda w, h, xd, yd, xp, yp: H.Plane.from_full(np.zeros((int(h), int(w)), np.int64),
+                                                       0, 0, int(w), int(h)))})
+    pred = RI.Source(REF + "predict.rs")
+    PredModeV.fn = I.make_fn(pred.fn("predict_inter"), I.globals)
+    ds = F(I, "diamond_me_search", "me.rs")
+    tel = F(I, "telescopic_subpel_search", "me.rs")
+    sad_ref, satd_ref = F(I, "get_sad_ref"), F(I, "get_satd_ref")
+    put_ref, prep_ref, avg_ref = F(I, "put_8tap_ref"), F(I, "prep_8tap_ref"), F(I, "mc_avg_ref")
+    for bd in (8, 10):
+        g = {"T": prim(bd)}
+        PredModeV.pixel = prim(bd)
+        I.globals.vars["get_sad"] = lambda *a, _g=g: sad_ref(*a, generics=_g)
+        I.globals.vars["get_satd"] = lambda *a, _g=g: satd_ref(*a, generics=_g)
+        I.globals.vars["put_8tap"] = lambda *a, _g=g: put_ref(*a, generics=_g)
+        I.globals.vars["prep_8tap"] = lambda *a, _g=g: prep_ref(*a, generics=_g)
+        I.globals.vars["mc_avg"] = lambda *a, _g=g: avg_ref(*a, generics=_g)
+        pad, H_, W_ = 88, 96, 128
+        org = rand_plane(rng, H_, W_, bd)
+        ref = np.roll(org, (2, -3), (0, 1))
+        ref = np.clip(ref + rng.integers(-3, 4, ref.shape), 0, (1 << bd) - 1)
+        ref[:, 100:128:2] = (1 << bd) - 1  # 0/max stripes near the right edge
+        ref[:, 101:128:2] = 0
+        fo = np.pad(org, pad, mode="edge")
+        fr = np.pad(ref, pad, mode="edge")
+        po = H.Plane.from_full(fo, pad, pad, W_, H_)
+        pr = H.Plane.from_full(fr, pad, pad, W_, H_)
+        cases, res = [], []
+        specs = [  # (w, h, subpel, satd, hp, kind) kind 0 diamond, 1 telescopic
+            (64, 64, 0, 0, 0, 0), (32, 32, 0, 0, 0, 0), (16, 16, 0, 1, 0, 0), (32, 16, 0, 0, 0, 0),
+            (8, 8, 1, 0, 0, 0), (8, 8, 1, 0, 1, 0), (16, 16, 1, 0, 0, 0), (16, 8, 1, 1, 1, 0),
+            (8, 16, 1, 0, 1, 0), (8, 8, 0, 0, 0, 1), (8, 8, 0, 1, 1, 1), (16, 16, 0, 0, 1, 1),
+            (16, 8, 0, 0, 0, 1)]
+        for n, (w, h, sub, satd, hp, kind) in enumerate(specs):
+            px_ = int(rng.integers(-4, W_ - w + 4)) if n % 4 else W_ - w + 2
+            py_ = int(rng.integers(-4, H_ - h + 4)) if n % 4 else 0
+            span = 8 * int(rng.integers(3, 10))
+            rng_ = (-span, span, -span // 2, span // 2)
+            pm0 = [int(v) for v in rng.integers(-40, 40, 2)]
+            pm1 = [int(v) for v in rng.integers(-40, 40, 2)]
+            lam = int(rng.integers(0, 4000))
+            npred = int(rng.integers(1, 6))
+            step = 1 if sub else 8
+            preds = [[int(v) * step for v in rng.integers(-6, 6, 2)] for _ in range(npred)]
+            if n % 5 == 2:
+                preds[0] = [span + 8, 0]  # out of range
+            start = (8 * int(rng.integers(-2, 3)), 8 * int(rng.integers(-2, 3)))
+            start_cost = int(rng.integers(0, 1 << 22)) if n % 3 else 2 ** 64 - 1
+            fi = DsFi(bd, pr, hp)
+            best = [H.motion_vector(*start) if kind else H.motion_vector(0, 0)]
+            cost = [RI.TInt(start_cost if kind else 0, "u64")]
+            bref = RI.Ref(lambda: best[0], lambda v: best.__setitem__(0, v))
+            cref = RI.Ref(lambda: cost[0], lambda v: cost.__setitem__(0, v))
+            po_ = RI.Struct("PlaneOffset", {"x": RI.TInt(px_, "isize"), "y": RI.TInt(py_, "isize")})
+            pmv = [H.motion_vector(*pm0), H.motion_vector(*pm1)]
+            bs = H.BlockSize.from_width_and_height(w, h)
+            lo = [RI.TInt(v, "isize") for v in rng_]
+            if kind == 0:
+                ds(fi, po_, po, pr, [H.motion_vector(*p) for p in preds], RI.TInt(bd, "usize"),
+                   pmv, RI.TInt(lam, "u32"), lo[0], lo[1], lo[2], lo[3], bs, bool(satd), bref,
+                   cref, bool(sub), _RefType.LAST_FRAME, generics=g)
+            else:
+                ts = RI.Struct("TileStateMut", {"input": RI.Struct("Frame", {"planes": [po]})})
+                tel(fi, ts, po_, RI.TInt(lam, "u32"), _RefType.LAST_FRAME, pmv, lo[0], lo[1],
+                    lo[2], lo[3], bs, bool(satd), bref, cref, generics=g)
+            pp = preds + [[0, 0]] * (8 - npred)
+            cases.append([w, h, sub, satd, hp, kind, px_, py_] + list(rng_) + pm0 + pm1 +
+                         [lam, npred] + [v for p in pp for v in p] + list(start) +
+                         [start_cost & 0xFFFFFFFF, start_cost >> 32])
+            res.append((int(best[0].row), int(best[0].col), int(cost[0])))
+            print("  ds bd%d case %d: %s -> %s" % (bd, n, specs[n], res[-1]))
+        kk = "ds_bd%d_" % bd
+        out[kk + "org"] = fo.astype(np.uint16)
+        out[kk + "ref"] = fr.astype(np.uint16)
+        out[kk + "geom"] = np.array([pad, pad, W_, H_], np.int32)
+        out[kk + "cases"] = np.array(cases, np.int64)
+        out[kk + "mv"] = np.array([r[:2] for r in res], np.int16)
+        out[kk + "cost"] = np.array([r[2] for r in res], np.uint64)
+
+
 # ---------------------------------------------------------------- quantizer
 def gen_quant(I, rng, out):
     q = src_of(I, "quantize.rs")
@@ -582,7 +709,7 @@ def gen_tx(I, rng, out):
 
 
 SECTIONS = {"mc": gen_mc, "dist": gen_dist, "rdo": gen_rdo, "me": gen_me, "quant": gen_quant,
-            "tx": gen_tx}
+            "tx": gen_tx, "ds": gen_ds}
 
 
 def main(argv):

@@ -2046,6 +2046,9 @@ class OptSome:
 
 
 def _slice_method(r, name, args, gty, raw):
+    if isinstance(r, list) and name == "push":
+        r.append(args[0])
+        return None
     s = as_slice(r)
     if name == "len":
         return TInt(len(s), "usize")
