@@ -285,6 +285,10 @@ int rv_estimate_rate_batch(const uint64_t *d_tx_dist, int n, int qindex, int tx_
 /* ---------------------------------------------------------------------
  * Motion search
  * ------------------------------------------------------------------- */
+/* dc_q / ac_q lookups (src/quantize.rs:42-62) on the host: ac = 0 for
+ * dc_qlookup*_Q3, 1 for ac_qlookup*_Q3; -1 on bad arguments. */
+int rv_q_lookup(int ac, int qindex, int bit_depth);
+
 typedef struct rv_mv {
   int16_t row, col; /* 1/8 pel (MotionVector, src/mc.rs:28-31) */
 } rv_mv;
@@ -390,46 +394,97 @@ int rv_telescopic_subpel_batch(const rv_plane *org, const rv_plane *ref,
                                void *stream);
 
 /* ---------------------------------------------------------------------
- * Hot-path replay driver (see DESIGN.md "Replay driver"): reproduces the
- * per-frame call structure of a speed-10 encode for the accelerated
- * stages, frames resident in HBM.
+ * Hot-path replay driver (see DESIGN.md "Replay driver"): the per-frame
+ * call structure of a speed-10 encode of a stream for the accelerated
+ * stages -- motion search, every RDO inter candidate (skip / non-skip),
+ * the winners' reconstruction, which becomes the next frames' reference --
+ * in the coding order of rav1e's reorder pyramid, frames resident in HBM.
+ * One instance encodes one tile group (a rectangle of whole AV1 tiles).
  * ------------------------------------------------------------------- */
 typedef struct rv_replay_cfg {
   int32_t width, height;      /* luma, visible */
   int32_t xdec, ydec;         /* chroma subsampling (1,1 = 4:2:0) */
   int32_t bit_depth;          /* 8, 10 or 12 (12: exhaustive full search) */
-  int32_t tile_x0, tile_y0;   /* tile rectangle in 64x64 superblocks */
-  int32_t tile_w, tile_h;     /* (a whole frame: 0, 0, sb_cols, sb_rows) */
-  int32_t n_refs;             /* reference frames searched per frame */
-  int32_t rdo_candidates;     /* inter candidates per superblock */
+  int32_t tile_x0, tile_y0;   /* tile group rectangle in 64x64 superblocks */
+  int32_t tile_w, tile_h;     /* (a whole frame: 0, 0, 0, 0) */
+  int32_t n_refs;             /* reference frames searched per frame: 1 or 2 */
+  int32_t tile_w_sb, tile_h_sb; /* uniform AV1 tile size (TilingInfo::
+                                 * tile_width_sb / tile_height_sb,
+                                 * src/tiling/tiler.rs:49-126); 0 = one tile */
+  int32_t n_inputs;           /* input frames resident in HBM; display d
+                               * reads input d % n_inputs */
   int32_t flags;              /* RV_REPLAY_* bits, 0 = default */
 } rv_replay_cfg;
-/* flags: run the zero-MV RDO candidates (which need no motion search) on a
- * second stream concurrently with F0-F3 instead of in the main stream's F4
- * launch.  Measured neutral at 1080p and -2% at 4K on MI355X, so off by
- * default. */
-#define RV_REPLAY_SIDE_RDO 1
-/* flags: F4 luma candidates on the replay stream and the chroma transform
- * blocks concurrently on a second stream (separate, smaller-LDS kernel). */
-#define RV_REPLAY_SPLIT_RDO 2
 /* flags: F1 coarse search exhaustively (rv_full_search_batch) instead of
  * by successive elimination over box-sum tables (rv_full_search_sea_batch;
  * same results, the default for bit depth <= 10). */
 #define RV_REPLAY_EXHAUSTIVE_FS 4
+typedef struct rv_replay_frame_info {
+  int32_t display;            /* display index of the coded frame */
+  int32_t me_range_scale;     /* 4 >> pyramid level (src/encoder.rs:838) */
+  int32_t level;              /* pyramid level */
+  int32_t is_key;             /* 1: the key frame (input taken as recon) */
+  int32_t ref_display[2];     /* display index of each reference */
+} rv_replay_frame_info;
+/* The frame parameters of one pyramid level (FrameInvariants::
+ * set_quantizers, src/encoder.rs:865-880): base_q_idx, per-plane dc / ac
+ * qindex deltas, lambda (bit-depth scaled), me_lambda = sqrt(lambda),
+ * dist_scale per plane.  rav1e_amd/rate.py computes them for a fixed
+ * --quantizer (src/rate.rs:546-606, 746-775). */
+typedef struct rv_replay_level_params {
+  int32_t base_q_idx;
+  int32_t dc_delta_q[3];
+  int32_t ac_delta_q[3];
+  int32_t reserved;
+  double lambda, me_lambda;
+  double dist_scale[3];
+} rv_replay_level_params;
 typedef struct rv_replay rv_replay;
-/* Allocate device state for one tile; frames are uploaded with
- * rv_replay_set_frame.  NULL on failure. */
+/* Allocate the device state of one tile group: n_inputs input frames, a
+ * 12-frame DPB (reconstruction + input hres / qres + box sums).  NULL on
+ * failure (rv_last_error). */
 rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream);
 void rv_replay_destroy(rv_replay *r);
-/* Upload a source picture (planar, tightly packed: Y w*h, then the two
- * chroma planes) into slot `slot` (0 .. n_refs) and pad it. */
-int rv_replay_set_frame(rv_replay *r, int slot, const void *host_yuv);
-/* Run the hot path for one frame: input = slot 0, references =
- * slots 1..n_refs; me_range_scale as src/encoder.rs:838.  Asynchronous. */
-int rv_replay_frame(rv_replay *r, int me_range_scale);
-/* Copy the frame's results to host: per-superblock best MVs and costs,
- * checksums of coefficients / reconstruction / distortion.  Layout in
- * DESIGN.md; returns number of u64 written (<= cap). */
+/* Set the parameters of pyramid level 0..2 (all three before the first
+ * inter frame). */
+int rv_replay_set_level_params(rv_replay *r, int level, const rv_replay_level_params *p);
+/* Generate input i = synthetic frame t0 + i (integer form;
+ * rav1e_amd/replay.py synth_frame is its bit-exact numpy twin) for every
+ * input slot, in HBM. */
+int rv_replay_synth_inputs(rv_replay *r, int t0);
+/* Upload / download input `idx` (planar, tightly packed: Y w*h, then the two
+ * chroma planes); the upload pads it. */
+int rv_replay_set_input(rv_replay *r, int idx, const void *host_yuv);
+int rv_replay_get_input(rv_replay *r, int idx, void *host_yuv);
+/* The reconstruction of display frame `display` (one of the last 12). */
+int rv_replay_get_recon(rv_replay *r, int display, void *host_yuv);
+/* block_importances (f32, w_imp x h_imp = ceil(w/8) x ceil(h/8)) that bias
+ * the RDO distortion (compute_distortion_bias, src/rdo.rs:476-508); NULL =
+ * all zero (the default). */
+int rv_replay_set_importances(rv_replay *r, const float *host, int n);
+/* Code the next frame of the stream (asynchronous on the replay's stream):
+ * the key frame first, then the pyramid's coding order.  info may be NULL. */
+int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info);
+/* Tile-parallel runs (one instance per rank): every rank's tile-group
+ * rectangle (4 x i32 in superblocks per group, rank order), this instance's
+ * group, and an RCCL communicator from rv_comm_create (or NULL: the caller
+ * all-gathers the packed regions from rv_replay_exchange_buffers' send
+ * buffer into its recv buffer, group k at k * bytes_per_group, and calls
+ * rv_replay_import after every rv_replay_frame). */
+int rv_replay_set_groups(rv_replay *r, int n_groups, const int32_t *rects, int my_group,
+                         void *comm);
+int rv_replay_exchange_buffers(rv_replay *r, void **send, void **recv, size_t *bytes_per_group);
+int rv_replay_import(rv_replay *r);
+/* RCCL (over xGMI) for the per-frame reconstruction all-gather: rank 0 gets
+ * an id (returns its size), every rank creates the communicator with it. */
+int rv_comm_unique_id(uint8_t *out, int cap);
+void *rv_comm_create(const uint8_t *id, int nranks, int rank);
+void rv_comm_destroy(void *comm);
+/* Copy the last coded frame's results to host: per superblock the search
+ * results (8 words per reference) and the RDO winner [candidate, skip,
+ * rd cost bits, distortion]; then [levels checksum, group reconstruction
+ * sum, importance SATD sum, importance blocks, frame reconstruction sum].
+ * Returns the number of u64 written (<= cap). */
 int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
 /* Record the timing events only on frames f with (f / block) % stride == 0
  * (stride 1 = every frame, the default; 0 = never).  Each event record
@@ -437,14 +492,14 @@ int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
  * instrument a sample: block = the GOP length keeps every me_range_scale
  * equally represented. */
 int rv_replay_set_timing(rv_replay *r, int stride, int block);
-/* Kernel-time breakdown of the last instrumented frame (HIP events on the replay
- * stream), ms: [0..5] stages F0..F5 (F1 = exactly the full-search
- * launches), then kernel brackets [6] F3 full-pel diamond, [7] F3 sub-pel
- * diamond, [8] F4 fused launch of the sub-pel-MV candidates (luma: MC +
- * diff + fwd TX_64X64 + coefficient stand-in + inverse + add + cdef
- * moments; chroma U and V: the same with TX_32X32 and SSE), [9] F4 fused
- * launch of the zero-MV candidates, which runs on a second stream
- * concurrently with F0-F3.  Returns the count written (<= 10). */
+/* Kernel-time breakdown of the last instrumented frame (HIP events on the
+ * replay stream), ms: [0] F0 pyramid + box sums, [1] F1 full search, [2] F2
+ * half-res diamond, [3] F3 full-pel diamond, [4] F3 sub-pel diamond, [5] F4
+ * fused candidate launch (luma: MC + skip distortion + diff + fwd TX_64X64
+ * + quantize + estimate_rate + inverse + add + non-skip distortion; chroma
+ * U and V: the same with TX_32X32 and SSE), [6] F4 rd cost + argmin, [7] F6
+ * commit, [8] F5 importance, [9] F7 pad / exchange.  Returns the count
+ * written (<= 10). */
 int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
 /* Same breakdown summed over the last `last_frames` instrumented frames
  * (<= 64). */

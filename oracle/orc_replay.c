@@ -1,18 +1,25 @@
 /* CPU replay of the hot-path schedule (test infrastructure + the
  * bench's cpu_baseline leg only; see DESIGN.md "Replay driver").
  *
- * Runs the same per-frame schedule as rav1e_amd/csrc/rv_replay.hip with the
- * oracle's restatements of the reference functions, one superblock per
- * task on a pthread pool (rav1e runs tiles on rayon, src/encoder.rs:
- * 2772-2781; within one tile the replay's superblocks are independent):
- *   F0 downsample_from (src/frame/plane.rs:399-423)
- *   F1 full_search at 1/4 res (estimate_motion_ss4, src/me.rs:1023-1075)
- *   F2 diamond at 1/2 res (me_ss2, src/me.rs:470-519)
- *   F3 diamond full-pel + sub-pel at full res (src/me.rs:193-285)
- *   F4 put_8tap, diff + fht, quantize + dequantize, inverse + add,
- *      cdef moments / sse (src/encoder.rs:1077-1237, src/rdo.rs:219-411)
- *   F5 8x8 SATD importance (src/api/internal.rs:823-1010) + lookahead
- *      intra cost of the same blocks (:680-765, orc_lookahead_intra_costs)
+ * Runs the same stream schedule as rav1e_amd/csrc/rv_replay.hip with the
+ * oracle's restatements of the reference functions, on a pthread pool over
+ * superblocks (rav1e runs tiles on rayon, src/encoder.rs:2772-2781):
+ *   key frame: its input is its reconstruction
+ *   F0 downsample_from (src/frame/plane.rs:399-423) of the input
+ *   pass A, per superblock:
+ *     F1 full_search at 1/4 res (estimate_motion_ss4, src/me.rs:1023-1075)
+ *     F2 diamond at 1/2 res (me_ss2, src/me.rs:470-519)
+ *     F3 diamond full-pel + sub-pel at full res (src/me.rs:193-285)
+ *   pass B, per superblock (needs the neighbours' NEWMVs):
+ *     F4 every inter candidate of rdo_mode_decision (src/rdo.rs:825-1006),
+ *        skip and non-skip (:649-700): put_8tap, compute_distortion,
+ *        diff + fht, quantize, tx-domain distortion + estimate_rate,
+ *        dequantize, inverse + add (src/encoder.rs:1077-1237,
+ *        src/rdo.rs:204-569); compute_rd_cost and the argmin
+ *     F6 the winner's levels and reconstruction into the frame
+ *     F5 8x8 SATD importance (src/api/internal.rs:823-1010) + lookahead
+ *        intra cost of the same blocks (:680-765)
+ *   F7 pad the reconstruction (or export / import the tile group's region)
  * It must produce the same result words as the GPU driver.
  */
 #include <pthread.h>
@@ -22,7 +29,8 @@
 #include "orc_common.h"
 
 #define SB 64
-#define QIDX 100 /* kReplayQindex of rv_replay.hip */
+#define NSLOT 12
+#define NMODE 4
 
 typedef struct {
   uint8_t *mem; /* allocation, element 0 */
@@ -33,25 +41,44 @@ typedef struct {
   oplane y, u, v, hres, qres;
 } oslot;
 
+typedef struct {
+  oplane y, u, v;
+} oinput;
+
+typedef struct {
+  int display, me_range_scale, level, is_key, ref_display[2];
+} orc_frame_info; /* = rv_replay_frame_info */
+
 typedef struct orc_replay {
   int W, H, xdec, ydec, bd, hbd, R, C;
-  int w_in_b, h_in_b, tx0, ty0, tw, th, mi_w, mi_h, nsb, cw, ch, vis_w, vis_h;
-  double me_lambda;
-  orc_qctx q_luma, q_chroma; /* TX_64X64 / TX_32X32, inter, qindex QIDX */
-  oslot *slots;
+  int w_in_b, h_in_b, w_imp, tx0, ty0, tw, th, tws, ths, nsb, cw, ch, vis_w, vis_h, ntx_c;
+  /* per pyramid level: quantizers (TX_64X64 luma, TX_32X32 chroma, inter)
+   * and lambdas (rv_replay_set_level_params) */
+  struct {
+    int set, qidx, dc[3], ac[3];
+    orc_qctx q[3];
+    double lambda, me_lambda, ds[3];
+  } lv[3];
+  oslot slots[NSLOT];
+  oinput *inputs;
+  int n_inputs;
+  float *imp; /* block_importances, NULL = zero */
   int threads;
+  long coded;
+  orc_frame_info fi;
   /* per frame */
-  int scale;
+  orc_mv *coarse, *half, *full, *sub; /* [R][nsb] */
+  uint64_t *cc, *hc, *fc, *sc;
   uint64_t *words;
-  uint64_t tail[4];
+  int32_t *lev; /* committed levels: per SB luma 1024 + 2 * ntx_c * 1024 */
+  uint64_t tail[5];
   pthread_mutex_t mu;
-  int next_sb;
+  int next_sb, pass, sb_limit;
 } orc_replay;
 
 static size_t px_of(const orc_replay *r) { return r->hbd ? 2 : 1; }
 
-static int plane_init(oplane *p, int w, int h, int xdec, int ydec, int pad,
-                      int hbd) {
+static int plane_init(oplane *p, int w, int h, int xdec, int ydec, int pad, int hbd) {
   int out[4];
   orc_plane_geometry(w, h, pad >> xdec, pad >> ydec, hbd, out);
   p->stride = out[0];
@@ -65,41 +92,87 @@ static int plane_init(oplane *p, int w, int h, int xdec, int ydec, int pad,
   p->mem = calloc((size_t)p->stride * p->alloc_h, hbd ? 2 : 1);
   return p->mem ? 0 : -1;
 }
+static size_t plane_size(const oplane *p, int hbd) {
+  return (size_t)p->stride * p->alloc_h * (hbd ? 2 : 1);
+}
 /* data origin (visible (0,0)) */
 static void *org_of(const oplane *p, int hbd) {
   return p->mem + ((size_t)p->yo * p->stride + p->xo) * (hbd ? 2 : 1);
 }
 static void *at(const oplane *p, int hbd, int x, int y) {
-  return (uint8_t *)org_of(p, hbd) +
-         ((ptrdiff_t)y * p->stride + x) * (ptrdiff_t)(hbd ? 2 : 1);
+  return (uint8_t *)org_of(p, hbd) + ((ptrdiff_t)y * p->stride + x) * (ptrdiff_t)(hbd ? 2 : 1);
 }
 
-static void mv_range(const orc_replay *r, int bx, int by, int bw, int bh,
-                     int m[4]) {
+static void mv_range(const orc_replay *r, int bx, int by, int bw, int bh, int m[4]) {
   int border_w = 128 + bw * 8, border_h = 128 + bh * 8;
   m[0] = -bx * 32 - border_w;
   m[1] = (r->w_in_b - bx - bw / 4) * 32 + border_w;
   m[2] = -by * 32 - border_h;
   m[3] = (r->h_in_b - by - bh / 4) * 32 + border_h;
 }
-static void adjust_bo(const orc_replay *r, int *bx, int *by, int bw, int bh) {
-  int x = *bx < r->mi_w - bw / 4 ? *bx : r->mi_w - bw / 4;
-  int y = *by < r->mi_h - bh / 4 ? *by : r->mi_h - bh / 4;
+/* the tile of group superblock (sx, sy): origin (SBs), visible 4x4 size */
+static void sb_tile(const orc_replay *r, int sx, int sy, int *t0x, int *t0y, int *mi_w,
+                    int *mi_h) {
+  int fx = r->tx0 + sx, fy = r->ty0 + sy;
+  *t0x = fx - fx % r->tws;
+  *t0y = fy - fy % r->ths;
+  int vw = r->W - *t0x * SB < r->tws * SB ? r->W - *t0x * SB : r->tws * SB;
+  int vh = r->H - *t0y * SB < r->ths * SB ? r->H - *t0y * SB : r->ths * SB;
+  *mi_w = vw >> 2;
+  *mi_h = vh >> 2;
+}
+static void adjust_bo(int mi_w, int mi_h, int *bx, int *by, int bw, int bh) {
+  int x = *bx < mi_w - bw / 4 ? *bx : mi_w - bw / 4;
+  int y = *by < mi_h - bh / 4 ? *by : mi_h - bh / 4;
   *bx = x > 0 ? x : 0;
   *by = y > 0 ? y : 0;
 }
-static uint64_t pack_mv(orc_mv m) {
-  return ((uint64_t)(uint16_t)m.row << 16) | (uint16_t)m.col;
-}
+static uint64_t pack_mv(orc_mv m) { return ((uint64_t)(uint16_t)m.row << 16) | (uint16_t)m.col; }
 static orc_mv qfull(orc_mv m) {
   orc_mv q = {(int16_t)((m.row / 8) * 8), (int16_t)((m.col / 8) * 8)};
   return q;
 }
+static int mv_eq(orc_mv a, orc_mv b) { return a.row == b.row && a.col == b.col; }
 
-orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd,
-                              int tile_x0, int tile_y0, int tile_w,
-                              int tile_h, int n_refs, int threads) {
-  if ((W & 7) || (H & 7) || (bd != 8 && bd != 10 && bd != 12) || n_refs < 1 || n_refs > 7)
+/* The MV stack and candidate MVs of rv_chain.h cand_stack / cand_mv: the
+ * row above, then the column to the left (merged if equal), inside the
+ * tile; NEARESTMV, NEAR0MV, GLOBALMV, NEWMV per reference
+ * (src/rdo.rs:880-905). */
+static int cand_mv(const orc_replay *r, int sb, int c, orc_mv *mv) {
+  int k = c / NMODE, m = c % NMODE;
+  int sx = sb % r->tw, sy = sb / r->tw, fx = r->tx0 + sx, fy = r->ty0 + sy;
+  const orc_mv *s = r->sub + (size_t)k * r->nsb;
+  orc_mv st[2], zero = {0, 0};
+  int n = 0;
+  if (fy % r->ths) st[n++] = s[sb - r->tw];
+  if (fx % r->tws) {
+    orc_mv v = s[sb - 1];
+    if (n == 0 || !mv_eq(v, st[0])) st[n++] = v;
+  }
+  switch (m) {
+    case 0:
+      *mv = n >= 1 ? st[0] : zero;
+      return 1;
+    case 1:
+      *mv = n >= 2 ? st[1] : zero;
+      return n >= 1;
+    case 2:
+      *mv = zero;
+      return n >= 2;
+    default: {
+      orc_mv me = s[sb];
+      *mv = me;
+      return !(n >= 1 && mv_eq(st[0], me)) && !(n >= 2 && mv_eq(st[1], me)) &&
+             (me.row != 0 || me.col != 0);
+    }
+  }
+}
+
+orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile_x0, int tile_y0,
+                              int tile_w, int tile_h, int tile_w_sb, int tile_h_sb, int n_refs,
+                              int n_inputs, int threads) {
+  if ((W & 7) || (H & 7) || (bd != 8 && bd != 10 && bd != 12) || n_refs < 1 || n_refs > 2 ||
+      n_inputs < 1)
     return NULL;
   orc_replay *r = calloc(1, sizeof(*r));
   r->W = W;
@@ -109,44 +182,59 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd,
   r->bd = bd;
   r->hbd = bd > 8;
   r->R = n_refs;
-  r->C = 2 * n_refs;
+  r->C = NMODE * n_refs;
   r->w_in_b = 2 * ((W + 7) >> 3);
   r->h_in_b = 2 * ((H + 7) >> 3);
+  r->w_imp = r->w_in_b / 2;
   int sbc = (W + SB - 1) / SB, sbr = (H + SB - 1) / SB;
   r->tx0 = tile_x0;
   r->ty0 = tile_y0;
   r->tw = tile_w > 0 ? tile_w : sbc - tile_x0;
   r->th = tile_h > 0 ? tile_h : sbr - tile_y0;
+  r->tws = tile_w_sb > 0 ? tile_w_sb : sbc;
+  r->ths = tile_h_sb > 0 ? tile_h_sb : sbr;
   r->vis_w = W - r->tx0 * SB < r->tw * SB ? W - r->tx0 * SB : r->tw * SB;
   r->vis_h = H - r->ty0 * SB < r->th * SB ? H - r->ty0 * SB : r->th * SB;
-  r->mi_w = r->vis_w >> 2;
-  r->mi_h = r->vis_h >> 2;
   r->nsb = r->tw * r->th;
   r->cw = SB >> xdec;
   r->ch = SB >> ydec;
-  r->me_lambda = 24.0 * (double)(1 << (bd - 8));
-  orc_qctx_update(&r->q_luma, QIDX, 4, 0, bd, 0, 0);
-  orc_qctx_update(&r->q_chroma, QIDX, 3, 0, bd, 0, 0);
+  r->ntx_c = (r->cw / 32) * (r->ch / 32);
   r->threads = threads > 0 ? threads : 1;
-  r->slots = calloc(n_refs + 1, sizeof(oslot));
   int cw = (W + xdec) >> xdec, ch = (H + ydec) >> ydec;
-  for (int s = 0; s <= n_refs; s++) {
+  for (int s = 0; s < NSLOT; s++) {
     oslot *o = &r->slots[s];
-    if (plane_init(&o->y, W, H, 0, 0, 88, r->hbd) ||
-        plane_init(&o->u, cw, ch, xdec, ydec, 88, r->hbd) ||
+    if (plane_init(&o->y, W, H, 0, 0, 88, r->hbd) || plane_init(&o->u, cw, ch, xdec, ydec, 88, r->hbd) ||
         plane_init(&o->v, cw, ch, xdec, ydec, 88, r->hbd) ||
         plane_init(&o->hres, W / 2, H / 2, 0, 0, 44, r->hbd) ||
         plane_init(&o->qres, W / 4, H / 4, 0, 0, 22, r->hbd))
       return NULL;
   }
-  r->words = calloc((size_t)r->nsb * (8 * r->R + 2), 8);
+  r->n_inputs = n_inputs;
+  r->inputs = calloc(n_inputs, sizeof(oinput));
+  for (int i = 0; i < n_inputs; i++) {
+    oinput *o = &r->inputs[i];
+    if (plane_init(&o->y, W, H, 0, 0, 88, r->hbd) || plane_init(&o->u, cw, ch, xdec, ydec, 88, r->hbd) ||
+        plane_init(&o->v, cw, ch, xdec, ydec, 88, r->hbd))
+      return NULL;
+  }
+  size_t nr = (size_t)r->R * r->nsb;
+  r->coarse = calloc(nr, sizeof(orc_mv));
+  r->half = calloc(nr, sizeof(orc_mv));
+  r->full = calloc(nr, sizeof(orc_mv));
+  r->sub = calloc(nr, sizeof(orc_mv));
+  r->cc = calloc(nr, 8);
+  r->hc = calloc(nr, 8);
+  r->fc = calloc(nr, 8);
+  r->sc = calloc(nr, 8);
+  r->words = calloc((size_t)r->nsb * (8 * r->R + 4), 8);
+  r->lev = calloc((size_t)r->nsb * (1024 + 2 * r->ntx_c * 1024), 4);
   pthread_mutex_init(&r->mu, NULL);
   return r;
 }
 
 void orc_replay_destroy(orc_replay *r) {
   if (!r) return;
-  for (int s = 0; s <= r->R; s++) {
+  for (int s = 0; s < NSLOT; s++) {
     oslot *o = &r->slots[s];
     free(o->y.mem);
     free(o->u.mem);
@@ -154,56 +242,109 @@ void orc_replay_destroy(orc_replay *r) {
     free(o->hres.mem);
     free(o->qres.mem);
   }
-  free(r->slots);
+  for (int i = 0; i < r->n_inputs; i++) {
+    free(r->inputs[i].y.mem);
+    free(r->inputs[i].u.mem);
+    free(r->inputs[i].v.mem);
+  }
+  free(r->inputs);
+  free(r->imp);
+  free(r->coarse);
+  free(r->half);
+  free(r->full);
+  free(r->sub);
+  free(r->cc);
+  free(r->hc);
+  free(r->fc);
+  free(r->sc);
   free(r->words);
+  free(r->lev);
   pthread_mutex_destroy(&r->mu);
   free(r);
 }
 
 static void pad(const orc_replay *r, oplane *p) {
-  orc_plane_pad(p->mem, p->stride, p->alloc_h, p->xo, p->yo, 0, 0, p->w, p->h,
-                r->hbd);
+  orc_plane_pad(p->mem, p->stride, p->alloc_h, p->xo, p->yo, 0, 0, p->w, p->h, r->hbd);
 }
 static void downsample(const orc_replay *r, oplane *dst, const oplane *src) {
-  orc_downsample(org_of(dst, r->hbd), dst->stride, dst->w, dst->h,
-                 org_of(src, r->hbd), src->stride, r->hbd);
+  orc_downsample(org_of(dst, r->hbd), dst->stride, dst->w, dst->h, org_of(src, r->hbd),
+                 src->stride, r->hbd);
   pad(r, dst);
 }
 
-int orc_replay_set_frame(orc_replay *r, int slot, const void *yuv) {
-  if (slot < 0 || slot > r->R) return -1;
-  oslot *o = &r->slots[slot];
+static void copy_planes(orc_replay *r, oplane **pl, void *host, int to_plane) {
   size_t px = px_of(r);
-  const uint8_t *p = yuv;
-  oplane *pl[3] = {&o->y, &o->u, &o->v};
+  uint8_t *p = host;
   for (int k = 0; k < 3; k++) {
-    for (int y = 0; y < pl[k]->h; y++)
-      memcpy(at(pl[k], r->hbd, 0, y), p + (size_t)y * pl[k]->w * px,
-             (size_t)pl[k]->w * px);
+    for (int y = 0; y < pl[k]->h; y++) {
+      if (to_plane)
+        memcpy(at(pl[k], r->hbd, 0, y), p + (size_t)y * pl[k]->w * px, (size_t)pl[k]->w * px);
+      else
+        memcpy(p + (size_t)y * pl[k]->w * px, at(pl[k], r->hbd, 0, y), (size_t)pl[k]->w * px);
+    }
     p += (size_t)pl[k]->w * pl[k]->h * px;
-    pad(r, pl[k]);
+    if (to_plane) pad(r, pl[k]);
   }
-  downsample(r, &o->hres, &o->y);
-  downsample(r, &o->qres, &o->hres);
+}
+
+int orc_replay_set_level_params(orc_replay *r, int level, int base_q_idx, const int32_t dc[3],
+                                const int32_t ac[3], double lambda, double me_lambda,
+                                const double ds[3]) {
+  if (level < 0 || level > 2 || base_q_idx < 1 || base_q_idx > 255) return -1;
+  r->lv[level].qidx = base_q_idx;
+  for (int p = 0; p < 3; p++) {
+    r->lv[level].dc[p] = dc[p];
+    r->lv[level].ac[p] = ac[p];
+    r->lv[level].ds[p] = ds[p];
+    orc_qctx_update(&r->lv[level].q[p], base_q_idx, p ? 3 : 4, 0, r->bd, dc[p], ac[p]);
+  }
+  r->lv[level].lambda = lambda;
+  r->lv[level].me_lambda = me_lambda;
+  r->lv[level].set = 1;
+  return 0;
+}
+
+int orc_replay_set_input(orc_replay *r, int idx, const void *yuv) {
+  if (idx < 0 || idx >= r->n_inputs) return -1;
+  oinput *o = &r->inputs[idx];
+  oplane *pl[3] = {&o->y, &o->u, &o->v};
+  copy_planes(r, pl, (void *)yuv, 1);
+  return 0;
+}
+
+int orc_replay_get_recon(orc_replay *r, int display, void *yuv) {
+  if (display < 0) return -1;
+  oslot *o = &r->slots[display % NSLOT];
+  oplane *pl[3] = {&o->y, &o->u, &o->v};
+  copy_planes(r, pl, yuv, 0);
+  return 0;
+}
+
+int orc_replay_set_importances(orc_replay *r, const float *imp, int n) {
+  free(r->imp);
+  r->imp = NULL;
+  if (!imp) return 0;
+  if (n != r->w_imp * (r->h_in_b / 2)) return -1;
+  r->imp = malloc((size_t)n * 4);
+  memcpy(r->imp, imp, (size_t)n * 4);
   return 0;
 }
 
 /* predict_inter / get_params (src/predict.rs:267-283) + put_8tap */
-static void predict(const orc_replay *r, const oplane *ref, int po_x, int po_y,
-                    orc_mv mv, int w, int h, void *dst, int dst_stride) {
+static void predict(const orc_replay *r, const oplane *ref, int po_x, int po_y, orc_mv mv, int w,
+                    int h, void *dst, int dst_stride) {
   int ys = 3 + ref->ydec, xs = 3 + ref->xdec;
   int roff = (int)mv.row >> ys, coff = (int)mv.col >> xs;
   int rf = ((int)mv.row - (roff << ys)) << (4 - ys);
   int cf = ((int)mv.col - (coff << xs)) << (4 - xs);
   int qx = clamp_i32(po_x + coff - 3, -ref->xo, ref->w) + 3;
   int qy = clamp_i32(po_y + roff - 3, -ref->yo, ref->h) + 3;
-  orc_put_8tap(dst, dst_stride, at(ref, r->hbd, qx, qy), ref->stride, w, h, cf,
-               rf, 0, 0, r->bd, r->hbd, 0);
+  orc_put_8tap(dst, dst_stride, at(ref, r->hbd, qx, qy), ref->stride, w, h, cf, rf, 0, 0, r->bd,
+               r->hbd, 0);
 }
 
-static void ds_ctx(const orc_replay *r, orc_ds_ctx *c, const oplane *org,
-                   const oplane *ref, int po_x, int po_y, int w, int h,
-                   const int m[4], uint32_t lambda, int subpel) {
+static void ds_ctx(const orc_replay *r, orc_ds_ctx *c, const oplane *org, const oplane *ref,
+                   int po_x, int po_y, int w, int h, const int m[4], uint32_t lambda, int subpel) {
   memset(c, 0, sizeof(*c));
   c->org = org_of(org, r->hbd);
   c->org_stride = org->stride;
@@ -229,46 +370,117 @@ static void ds_ctx(const orc_replay *r, orc_ds_ctx *c, const oplane *org,
   c->subpel = subpel;
 }
 
-/* One superblock through F1..F5; returns its tail contributions. */
-static void run_sb(orc_replay *r, int sb, uint64_t tail[3]) {
-  const oslot *cur = &r->slots[0];
+/* compute_distortion_bias (src/rdo.rs:476-508) of the BLOCK_8X8
+ * importance area at 4x4 block (mi_x, mi_y) */
+static double dist_bias(const orc_replay *r, int mi_x, int mi_y) {
+  if (!r->imp) return 0.65;
+  int x2 = mi_x + 2 < r->w_in_b ? mi_x + 2 : r->w_in_b;
+  int y2 = mi_y + 2 < r->h_in_b ? mi_y + 2 : r->h_in_b;
+  float tot = 0.f;
+  for (int y = mi_y; y < y2; y++)
+    for (int x = mi_x; x < x2; x++) tot += r->imp[(y >> 1) * r->w_imp + (x >> 1)];
+  float mean = tot / 4.0f;
+  return (double)(mean / 3.0f) + 0.65;
+}
+static uint64_t biased(uint64_t v, double bias) { return (uint64_t)((double)v * bias); }
+
+/* compute_distortion (src/rdo.rs:338-411) of a 64x64 superblock at luma
+ * (px, py): luma cdef_dist_wxh, chroma sse_wxh, each 8x8 / sub-block biased */
+static uint64_t sb_distortion(const orc_replay *r, const oinput *cur, int px, int py,
+                              const void *ly, const void *lu, const void *lv) {
+  const int hbd = r->hbd;
+  const double *ds = r->lv[r->fi.level].ds;
+  uint64_t d = 0;
+  for (int j = 0; j < SB; j += 8)
+    for (int i = 0; i < SB; i += 8) {
+      int64_t mo[5];
+      orc_cdef_moments_8x8(at(&cur->y, hbd, px + i, py + j), cur->y.stride,
+                           (const uint8_t *)ly + ((size_t)j * SB + i) * px_of(r), SB, hbd, mo);
+      d += biased(orc_cdef_dist_from_moments(mo, r->bd), dist_bias(r, (px + i) >> 2, (py + j) >> 2));
+    }
+  /* Distortion * dist_scale[p] -> ScaledDistortion (src/rdo.rs:375, 406) */
+  d = (uint64_t)((double)d * ds[0]);
+  const int cpx = px >> r->xdec, cpy = py >> r->ydec;
+  const int bw = 8 >> r->xdec, bh = 8 >> r->ydec, nbx = r->cw / bw;
+  uint64_t parts[SB * SB];
+  const oplane *cs[2] = {&cur->u, &cur->v};
+  const void *cp[2] = {lu, lv};
+  for (int pl = 0; pl < 2; pl++) {
+    int n = orc_sse_wxh(at(cs[pl], hbd, cpx, cpy), cs[pl]->stride, cp[pl], r->cw, r->cw, r->ch,
+                        r->xdec, r->ydec, hbd, parts);
+    uint64_t dp = 0;
+    for (int k = 0; k < n; k++) {
+      int bx = k % nbx, by = k / nbx;
+      int x = cpx + bx * bw, y = cpy + by * bh;
+      dp += biased(parts[k], dist_bias(r, (x << r->xdec) >> 2, (y << r->ydec) >> 2));
+    }
+    d += (uint64_t)((double)dp * ds[1 + pl]);
+  }
+  return d;
+}
+
+/* encode_tx_block (src/encoder.rs:1077-1237) of one transform block:
+ * diff + fht + quantize, tx-domain distortion -> estimate_rate,
+ * dequantize, inverse + add into `rec` (stride rs).  Returns the rate. */
+static uint64_t tx_block(const orc_replay *r, const oplane *src, int sx, int sy, void *rec, int rs,
+                         int tx_size, int plane, int32_t *levels_out) {
+  const int lvl = r->fi.level, qidx = r->lv[lvl].qidx;
+  const orc_qctx *q = &r->lv[lvl].q[plane];
+  const int n = 1 << ORC_TX_W_LOG2[tx_size];
+  int16_t res[SB * SB];
+  int32_t co[SB * SB], qc[32 * 32], rc[32 * 32];
+  orc_diff(res, at(src, r->hbd, sx, sy), src->stride, rec, rs, n, n, r->hbd);
+  orc_fwd_txfm2d(res, co, tx_size, 0, r->bd);
+  orc_quantize(q, co, qc, tx_size, 0);
+  orc_dequantize(qidx, qc, rc, tx_size, r->bd, r->lv[lvl].dc[plane], r->lv[lvl].ac[plane]);
+  const int ca = orc_coded_tx_area(tx_size);
+  uint64_t rate = orc_estimate_rate(qidx, tx_size, orc_tx_dist(co, rc, ca, n, n));
+  orc_inv_txfm2d_add(rc, rec, rs, tx_size, 0, r->bd, r->hbd);
+  if (levels_out) memcpy(levels_out, qc, (size_t)ca * 4);
+  return rate;
+}
+
+/* Pass A: F1-F3 for one superblock. */
+static void run_me(orc_replay *r, int sb) {
+  const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
+  const oslot *S = &r->slots[r->fi.display % NSLOT];
   const int R = r->R, hbd = r->hbd;
   const int sx = sb % r->tw, sy = sb / r->tw;
-  uint64_t *w = r->words + (size_t)sb * (8 * R + 2);
-  orc_mv cmv[8], hmv, fmv, smv[8];
   uint64_t cost;
-  /* F1 */
-  int bx = sx * 16, by = sy * 16;
-  adjust_bo(r, &bx, &by, 64, 64);
-  int fbx = bx + r->tx0 * 16, fby = by + r->ty0 * 16;
+  int t0x, t0y, mi_w, mi_h;
+  sb_tile(r, sx, sy, &t0x, &t0y, &mi_w, &mi_h);
+  int bx = (r->tx0 + sx - t0x) * 16, by = (r->ty0 + sy - t0y) * 16;
+  adjust_bo(mi_w, mi_h, &bx, &by, 64, 64);
+  int fbx = bx + t0x * 16, fby = by + t0y * 16;
   int m[4];
   mv_range(r, fbx, fby, 64, 64, m);
-  uint32_t lambda4 = (uint32_t)(r->me_lambda * 256.0 / 16.0 * 0.125);
-  uint32_t lambda2 = (uint32_t)(r->me_lambda * 256.0 / 4.0 * 0.125);
-  uint32_t lambda1 = (uint32_t)(r->me_lambda * 256.0 * 0.5);
-  int rx = 192 * r->scale, ry = 64 * r->scale;
+  const double me_lambda = r->lv[r->fi.level].me_lambda;
+  uint32_t lambda4 = (uint32_t)(me_lambda * 256.0 / 16.0 * 0.125);
+  uint32_t lambda2 = (uint32_t)(me_lambda * 256.0 / 4.0 * 0.125);
+  uint32_t lambda1 = (uint32_t)(me_lambda * 256.0 * 0.5);
+  int scale = r->fi.me_range_scale;
+  int rx = 192 * scale, ry = 64 * scale;
   int x_lo = fbx + ((m[0] / 8 > -rx ? m[0] / 8 : -rx) >> 2);
   int x_hi = fbx + ((m[1] / 8 < rx ? m[1] / 8 : rx) >> 2);
   int y_lo = fby + ((m[2] / 8 > -ry ? m[2] / 8 : -ry) >> 2);
   int y_hi = fby + ((m[3] / 8 < ry ? m[3] / 8 : ry) >> 2);
   orc_mv zero = {0, 0};
+  const oslot *ref[2];
+  for (int k = 0; k < R; k++) ref[k] = &r->slots[r->fi.ref_display[k] % NSLOT];
   for (int k = 0; k < R; k++) {
-    const oslot *ref = &r->slots[1 + k];
     orc_mv best = {0, 0};
     cost = UINT64_MAX;
-    orc_full_search(org_of(&cur->qres, hbd), cur->qres.stride,
-                    org_of(&ref->qres, hbd), ref->qres.stride, hbd, fbx, fby,
-                    x_lo, x_hi, y_lo, y_hi, 16, 16, 1, lambda4, zero, zero, 0,
-                    &best, &cost);
-    cmv[k] = best;
-    w[8 * k + 0] = pack_mv(best);
-    w[8 * k + 1] = cost;
+    orc_full_search(org_of(&S->qres, hbd), S->qres.stride, org_of(&ref[k]->qres, hbd),
+                    ref[k]->qres.stride, hbd, fbx, fby, x_lo, x_hi, y_lo, y_hi, 16, 16, 1, lambda4,
+                    zero, zero, 0, &best, &cost);
+    r->coarse[k * r->nsb + sb] = best;
+    r->cc[k * r->nsb + sb] = cost;
   }
-  /* F2 */
   orc_mv preds[8];
   preds[0] = zero;
   for (int k = 0; k < R; k++) {
-    orc_mv c4 = {(int16_t)(cmv[k].row * 4), (int16_t)(cmv[k].col * 4)};
+    orc_mv c4 = {(int16_t)(r->coarse[k * r->nsb + sb].row * 4),
+                 (int16_t)(r->coarse[k * r->nsb + sb].col * 4)};
     orc_mv q = qfull(c4);
     preds[1 + k].row = (int16_t)(q.row >> 1);
     preds[1 + k].col = (int16_t)(q.col >> 1);
@@ -278,105 +490,128 @@ static void run_sb(orc_replay *r, int sb, uint64_t tail[3]) {
   int mf[4];
   mv_range(r, fbx0, fby0, 64, 64, mf);
   for (int k = 0; k < R; k++) {
-    const oslot *ref = &r->slots[1 + k];
     orc_ds_ctx c;
-    ds_ctx(r, &c, &cur->hres, &ref->hres, fbx * 2, fby * 2, 32, 32, m2, lambda2,
-           0);
+    orc_mv hmv, fmv, smv;
+    ds_ctx(r, &c, &S->hres, &ref[k]->hres, fbx * 2, fby * 2, 32, 32, m2, lambda2, 0);
     orc_diamond_search(&c, preds, 1 + R, &hmv, &cost);
-    w[8 * k + 2] = pack_mv(hmv);
-    w[8 * k + 3] = cost;
-    /* F3 */
-    orc_mv fp[2] = {zero, qfull((orc_mv){(int16_t)(hmv.row * 2),
-                                         (int16_t)(hmv.col * 2)})};
-    ds_ctx(r, &c, &cur->y, &ref->y, fbx0 * 4, fby0 * 4, 64, 64, mf, lambda1, 0);
+    r->half[k * r->nsb + sb] = hmv;
+    r->hc[k * r->nsb + sb] = cost;
+    orc_mv fp[2] = {zero, qfull((orc_mv){(int16_t)(hmv.row * 2), (int16_t)(hmv.col * 2)})};
+    ds_ctx(r, &c, &cur->y, &ref[k]->y, fbx0 * 4, fby0 * 4, 64, 64, mf, lambda1, 0);
     orc_diamond_search(&c, fp, 2, &fmv, &cost);
-    w[8 * k + 4] = pack_mv(fmv);
-    w[8 * k + 5] = cost;
+    r->full[k * r->nsb + sb] = fmv;
+    r->fc[k * r->nsb + sb] = cost;
     c.subpel = 1;
-    orc_diamond_search(&c, &fmv, 1, &smv[k], &cost);
-    w[8 * k + 6] = pack_mv(smv[k]);
-    w[8 * k + 7] = cost;
+    orc_diamond_search(&c, &fmv, 1, &smv, &cost);
+    r->sub[k * r->nsb + sb] = smv;
+    r->sc[k * r->nsb + sb] = cost;
   }
-  /* F4 */
-  const int px = (sx + r->tx0) * SB, py = (sy + r->ty0) * SB;
-  const int cwid = r->cw, chei = r->ch;
-  const int cpx = px >> r->xdec, cpy = py >> r->ydec;
-  uint64_t best_s = UINT64_MAX;
-  int best_c = 0;
+}
+
+/* Pass B: F4 + F6 + F5 for one superblock. */
+static void run_rdo(orc_replay *r, int sb, uint64_t tail[3]) {
+  const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
+  oslot *S = &r->slots[r->fi.display % NSLOT];
+  const int R = r->R, hbd = r->hbd;
+  const size_t px = px_of(r);
+  const int sx = sb % r->tw, sy = sb / r->tw;
+  const oslot *ref[2];
+  for (int k = 0; k < R; k++) ref[k] = &r->slots[r->fi.ref_display[k] % NSLOT];
+  uint64_t *w = r->words + (size_t)sb * (8 * R + 4);
+  for (int k = 0; k < R; k++) {
+    size_t o = (size_t)k * r->nsb + sb;
+    w[8 * k + 0] = pack_mv(r->coarse[o]);
+    w[8 * k + 1] = r->cc[o];
+    w[8 * k + 2] = pack_mv(r->half[o]);
+    w[8 * k + 3] = r->hc[o];
+    w[8 * k + 4] = pack_mv(r->full[o]);
+    w[8 * k + 5] = r->fc[o];
+    w[8 * k + 6] = pack_mv(r->sub[o]);
+    w[8 * k + 7] = r->sc[o];
+  }
+  const int ppx = (sx + r->tx0) * SB, ppy = (sy + r->ty0) * SB;
+  const int cwid = r->cw, chei = r->ch, cpx = ppx >> r->xdec, cpy = ppy >> r->ydec;
+  const int ntx_c = r->ntx_c;
+  /* the best so far: reconstruction and levels */
+  uint16_t by_[SB * SB], bu_[SB * SB], bv_[SB * SB];
+  int32_t *blev = r->lev + (size_t)sb * (1024 + 2 * ntx_c * 1024);
+  int32_t clev[1024 + 2 * 4 * 1024];
   uint16_t ly[SB * SB], lu[SB * SB], lv[SB * SB];
-  int16_t res[SB * SB];
-  int32_t co[SB * SB], qc[32 * 32], pk[32 * 32];
+  double best = 1.7976931348623157e308;
+  int best_c = 0, best_skip = 0;
+  uint64_t best_d = 0;
   for (int c = 0; c < r->C; c++) {
-    const oslot *ref = &r->slots[1 + (c >> 1)];
-    orc_mv mv = (c & 1) ? zero : smv[c >> 1];
-    predict(r, &ref->y, px, py, mv, SB, SB, ly, SB);
-    predict(r, &ref->u, cpx, cpy, mv, cwid, chei, lu, cwid);
-    predict(r, &ref->v, cpx, cpy, mv, cwid, chei, lv, cwid);
-    /* luma TX_64X64 DCT_DCT */
-    orc_diff(res, at(&cur->y, hbd, px, py), cur->y.stride, ly, SB, SB, SB, hbd);
-    orc_fwd_txfm2d(res, co, 4, 0, r->bd);
-    /* quantize reads the first coded_tx_area (1024) entries of the
-     * W-stride raster (src/encoder.rs:1152-1170; SURVEY.md §0.6 fork
-     * quirk); dequantize feeds the inverse (:1192-1208) */
-    orc_quantize(&r->q_luma, co, qc, 4, 0);
-    for (int i = 0; i < 32 * 32; i++)
-      tail[0] += (uint64_t)(int64_t)qc[i] * (uint64_t)(i + 1);
-    orc_dequantize(QIDX, qc, pk, 4, r->bd, 0, 0);
-    orc_inv_txfm2d_add(pk, ly, SB, 4, 0, r->bd, hbd);
-    /* chroma TX_32X32 DCT_DCT blocks */
+    orc_mv mv;
+    if (!cand_mv(r, sb, c, &mv)) continue;
+    const oslot *rf = ref[c / NMODE];
+    predict(r, &rf->y, ppx, ppy, mv, SB, SB, ly, SB);
+    predict(r, &rf->u, cpx, cpy, mv, cwid, chei, lu, cwid);
+    predict(r, &rf->v, cpx, cpy, mv, cwid, chei, lv, cwid);
+    /* skip: the prediction is the reconstruction */
+    uint64_t ds = sb_distortion(r, cur, ppx, ppy, ly, lu, lv);
+    int zero_dist = 0;
+    const double lambda = r->lv[r->fi.level].lambda;
+    double rs = (double)ds + lambda * (0.0 / 8.0);
+    if (rs < best) {
+      best = rs;
+      best_c = c;
+      best_skip = 1;
+      best_d = ds;
+      zero_dist = ds == 0;
+      memcpy(by_, ly, SB * SB * px);
+      memcpy(bu_, lu, (size_t)cwid * chei * px);
+      memcpy(bv_, lv, (size_t)cwid * chei * px);
+    }
+    if (zero_dist) continue;
+    /* non-skip: luma TX_64X64, chroma TX_32X32 blocks */
+    uint32_t rate = (uint32_t)tx_block(r, &cur->y, ppx, ppy, ly, SB, 4, 0, clev);
     uint16_t *cp[2] = {lu, lv};
     const oplane *cs[2] = {&cur->u, &cur->v};
     for (int pl = 0; pl < 2; pl++)
-      for (int ty = 0; ty < chei; ty += 32)
-        for (int tx = 0; tx < cwid; tx += 32) {
-          uint8_t *pb = (uint8_t *)cp[pl] + ((size_t)ty * cwid + tx) * px_of(r);
-          orc_diff(res, at(cs[pl], hbd, cpx + tx, cpy + ty), cs[pl]->stride, pb,
-                   cwid, 32, 32, hbd);
-          orc_fwd_txfm2d(res, co, 3, 0, r->bd);
-          orc_quantize(&r->q_chroma, co, qc, 3, 0);
-          for (int i = 0; i < 32 * 32; i++)
-            tail[0] += (uint64_t)(int64_t)qc[i] * (uint64_t)(i + 1);
-          orc_dequantize(QIDX, qc, pk, 3, r->bd, 0, 0);
-          orc_inv_txfm2d_add(pk, pb, cwid, 3, 0, r->bd, hbd);
-        }
-    /* distortion: luma cdef moments (SSE part), chroma sse_wxh */
-    uint64_t s = 0;
-    for (int j = 0; j < SB; j += 8)
-      for (int i = 0; i < SB; i += 8) {
-        int64_t mo[5];
-        orc_cdef_moments_8x8(at(&cur->y, hbd, px + i, py + j), cur->y.stride,
-                             (uint8_t *)ly + ((size_t)j * SB + i) * px_of(r), SB,
-                             hbd, mo);
-        s += (uint64_t)(mo[3] + mo[2] - 2 * mo[4]);
+      for (int t = 0; t < ntx_c; t++) {
+        int tx = (t % (cwid / 32)) * 32, ty = (t / (cwid / 32)) * 32;
+        uint8_t *pb = (uint8_t *)cp[pl] + ((size_t)ty * cwid + tx) * px;
+        rate += (uint32_t)tx_block(r, cs[pl], cpx + tx, cpy + ty, pb, cwid, 3, 1 + pl,
+                                   clev + 1024 + (pl * ntx_c + t) * 1024);
       }
-    uint64_t parts[SB * SB];
-    for (int pl = 0; pl < 2; pl++) {
-      int n = orc_sse_wxh(at(cs[pl], hbd, cpx, cpy), cs[pl]->stride, cp[pl], cwid,
-                          cwid, chei, r->xdec, r->ydec, hbd, parts);
-      for (int i = 0; i < n; i++) s += parts[i];
-    }
-    if (s < best_s) {
-      best_s = s;
+    uint64_t dn = sb_distortion(r, cur, ppx, ppy, ly, lu, lv);
+    double rn = (double)dn + lambda * ((double)rate / 8.0);
+    if (rn < best) {
+      best = rn;
       best_c = c;
+      best_skip = 0;
+      best_d = dn;
+      memcpy(by_, ly, SB * SB * px);
+      memcpy(bu_, lu, (size_t)cwid * chei * px);
+      memcpy(bv_, lv, (size_t)cwid * chei * px);
+      memcpy(blev, clev, (size_t)(1024 + 2 * ntx_c * 1024) * 4);
     }
-    /* recon checksum over the candidate's blocks */
-    for (int i = 0; i < SB * SB; i++) tail[1] += hbd ? ly[i] : ((uint8_t *)ly)[i];
-    for (int i = 0; i < cwid * chei; i++)
-      tail[1] += hbd ? (uint64_t)lu[i] + lv[i]
-                     : (uint64_t)((uint8_t *)lu)[i] + ((uint8_t *)lv)[i];
   }
-  w[8 * R] = (uint64_t)best_c;
-  w[8 * R + 1] = best_s;
-  /* F5: the 8x8 blocks of this superblock inside the tile's visible area */
+  if (best_skip) memset(blev, 0, (size_t)(1024 + 2 * ntx_c * 1024) * 4);
+  uint64_t cb;
+  memcpy(&cb, &best, 8);
+  w[8 * R + 0] = (uint64_t)best_c;
+  w[8 * R + 1] = (uint64_t)best_skip;
+  w[8 * R + 2] = cb;
+  w[8 * R + 3] = best_d;
+  /* F6: the winner into the frame (whole superblock; past the frame edge
+   * it lands in the padding, which F7 rewrites) */
+  for (int y = 0; y < SB; y++) memcpy(at(&S->y, hbd, ppx, ppy + y), (uint8_t *)by_ + y * SB * px, SB * px);
+  for (int y = 0; y < chei; y++) {
+    memcpy(at(&S->u, hbd, cpx, cpy + y), (uint8_t *)bu_ + (size_t)y * cwid * px, cwid * px);
+    memcpy(at(&S->v, hbd, cpx, cpy + y), (uint8_t *)bv_ + (size_t)y * cwid * px, cwid * px);
+  }
+  /* F5: the 8x8 blocks of this superblock inside the group's visible area */
+  const orc_mv mv0 = r->sub[sb];
+  const oslot *r0 = ref[0];
   for (int j = 0; j < 8; j++)
     for (int i = 0; i < 8; i++) {
       int bxx = sx * 8 + i, byy = sy * 8 + j;
       if (bxx >= r->vis_w / 8 || byy >= r->vis_h / 8) continue;
       int x = r->tx0 * SB + bxx * 8, y = r->ty0 * SB + byy * 8;
       tail[2] += orc_get_satd(at(&cur->y, hbd, x, y), cur->y.stride,
-                              at(&r->slots[1].y, hbd, x + ((int)smv[0].col >> 3),
-                                 y + ((int)smv[0].row >> 3)),
-                              r->slots[1].y.stride, 8, 8, hbd, 0);
+                              at(&r0->y, hbd, x + ((int)mv0.col >> 3), y + ((int)mv0.row >> 3)),
+                              r0->y.stride, 8, 8, hbd, 0);
       uint32_t ic;
       orc_lookahead_intra_costs(at(&cur->y, hbd, x, y), cur->y.stride, 8, 8, hbd, r->bd, &ic);
       tail[2] += ic;
@@ -386,12 +621,16 @@ static void run_sb(orc_replay *r, int sb, uint64_t tail[3]) {
 static void *worker(void *arg) {
   orc_replay *r = arg;
   uint64_t tail[3] = {0, 0, 0};
+  int lim = r->sb_limit > 0 && r->sb_limit < r->nsb ? r->sb_limit : r->nsb;
   for (;;) {
     pthread_mutex_lock(&r->mu);
     int sb = r->next_sb++;
     pthread_mutex_unlock(&r->mu);
-    if (sb >= r->nsb) break;
-    run_sb(r, sb, tail);
+    if (sb >= lim) break;
+    if (r->pass == 0)
+      run_me(r, sb);
+    else
+      run_rdo(r, sb, tail);
   }
   pthread_mutex_lock(&r->mu);
   for (int i = 0; i < 3; i++) r->tail[i] += tail[i];
@@ -399,32 +638,141 @@ static void *worker(void *arg) {
   return NULL;
 }
 
-/* One frame; sb_limit > 0 runs only the first sb_limit superblocks (a
- * bounded sample for timing). */
-int orc_replay_frame(orc_replay *r, int me_range_scale, int sb_limit) {
-  if (me_range_scale != 1 && me_range_scale != 2 && me_range_scale != 4)
-    return -1;
-  oslot *cur = &r->slots[0];
-  downsample(r, &cur->hres, &cur->y);
-  downsample(r, &cur->qres, &cur->hres);
-  r->scale = me_range_scale;
-  memset(r->tail, 0, sizeof(r->tail));
+static void run_pass(orc_replay *r, int pass) {
+  r->pass = pass;
   r->next_sb = 0;
-  int nsb = r->nsb;
-  if (sb_limit > 0 && sb_limit < nsb) r->nsb = sb_limit;
   pthread_t th[256];
   int nt = r->threads < 256 ? r->threads : 256;
   for (int i = 0; i < nt; i++) pthread_create(&th[i], NULL, worker, r);
   for (int i = 0; i < nt; i++) pthread_join(th[i], NULL);
-  r->nsb = nsb;
+}
+
+/* Coding order of the reorder pyramid (rv_replay.hip frame_info). */
+static void frame_info(long n, int R, orc_frame_info *f) {
+  memset(f, 0, sizeof(*f));
+  if (n == 0) {
+    f->is_key = 1;
+    return;
+  }
+  long g = (n - 1) / 4, j = (n - 1) % 4;
+  static const int off[4] = {4, 2, 1, 3}, scale[4] = {4, 2, 1, 1};
+  static const int rf[4][2] = {{0, -4}, {0, 4}, {0, 2}, {2, 4}};
+  f->display = (int)(4 * g + off[j]);
+  f->me_range_scale = scale[j];
+  f->level = j == 0 ? 0 : j == 1 ? 1 : 2;
+  for (int k = 0; k < R; k++) {
+    long d = 4 * g + rf[j][k];
+    f->ref_display[k] = (int)(d < 0 ? 0 : d);
+  }
+}
+
+/* Code the next frame.  sb_limit > 0 runs only the first sb_limit
+ * superblocks of both passes (a bounded sample for timing).  pad_recon = 0
+ * leaves the padding to orc_replay_import (tile groups). */
+int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_recon) {
+  frame_info(r->coded, r->R, &r->fi);
+  if (info) *info = r->fi;
+  if (r->fi.is_key) {
+    oinput *in = &r->inputs[0];
+    oslot *s = &r->slots[0];
+    memcpy(s->y.mem, in->y.mem, plane_size(&in->y, r->hbd));
+    memcpy(s->u.mem, in->u.mem, plane_size(&in->u, r->hbd));
+    memcpy(s->v.mem, in->v.mem, plane_size(&in->v, r->hbd));
+    downsample(r, &s->hres, &in->y);
+    downsample(r, &s->qres, &s->hres);
+    r->coded++;
+    return 0;
+  }
+  if (!r->lv[0].set || !r->lv[1].set || !r->lv[2].set) return -1;
+  oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
+  oslot *S = &r->slots[r->fi.display % NSLOT];
+  downsample(r, &S->hres, &cur->y);
+  downsample(r, &S->qres, &S->hres);
+  memset(r->tail, 0, sizeof(r->tail));
+  r->sb_limit = sb_limit;
+  run_pass(r, 0);
+  run_pass(r, 1);
   r->tail[3] = (uint64_t)(r->vis_w / 8) * (r->vis_h / 8);
+  if (pad_recon) {
+    pad(r, &S->y);
+    pad(r, &S->u);
+    pad(r, &S->v);
+  }
+  r->coded++;
   return 0;
 }
 
+/* The group's visible rectangle of plane p (x0, y0, w, h). */
+static void group_rect(const orc_replay *r, int p, const int32_t *gr, int out[4]) {
+  int xd = p ? r->xdec : 0, yd = p ? r->ydec : 0;
+  int pw = p ? (r->W + r->xdec) >> r->xdec : r->W, ph = p ? (r->H + r->ydec) >> r->ydec : r->H;
+  int x0 = (gr[0] * SB) >> xd, y0 = (gr[1] * SB) >> yd;
+  int x1 = ((gr[0] + gr[2]) * SB) >> xd, y1 = ((gr[1] + gr[3]) * SB) >> yd;
+  out[0] = x0;
+  out[1] = y0;
+  out[2] = (x1 < pw ? x1 : pw) - x0;
+  out[3] = (y1 < ph ? y1 : ph) - y0;
+}
+
+/* Pack (to_buf = 1) or unpack group `gr`'s region of the last coded frame
+ * (Y, U, V rows, tightly packed); returns the bytes. */
+int64_t orc_replay_xcopy(orc_replay *r, const int32_t *gr, void *buf, int to_buf) {
+  oslot *s = &r->slots[r->fi.display % NSLOT];
+  oplane *pl[3] = {&s->y, &s->u, &s->v};
+  size_t px = px_of(r);
+  uint8_t *b = buf;
+  int64_t off = 0;
+  for (int p = 0; p < 3; p++) {
+    int rc[4];
+    group_rect(r, p, gr, rc);
+    for (int y = 0; y < rc[3]; y++) {
+      uint8_t *q = at(pl[p], r->hbd, rc[0], rc[1] + y);
+      if (b) {
+        if (to_buf)
+          memcpy(b + off, q, (size_t)rc[2] * px);
+        else
+          memcpy(q, b + off, (size_t)rc[2] * px);
+      }
+      off += (int64_t)rc[2] * px;
+    }
+  }
+  return off;
+}
+
+/* Pad the last coded frame (after every group's region is in). */
+void orc_replay_pad_recon(orc_replay *r) {
+  oslot *s = &r->slots[r->fi.display % NSLOT];
+  pad(r, &s->y);
+  pad(r, &s->u);
+  pad(r, &s->v);
+}
+
 int orc_replay_results(orc_replay *r, uint64_t *out, int cap) {
-  int nw = r->nsb * (8 * r->R + 2);
-  if (cap < nw + 4) return -1;
+  int nw = r->nsb * (8 * r->R + 4);
+  if (cap < nw + 5) return -1;
   memcpy(out, r->words, (size_t)nw * 8);
-  memcpy(out + nw, r->tail, 4 * 8);
-  return nw + 4;
+  /* levels checksum, recon sums of the group and of the frame */
+  uint64_t lc = 0;
+  size_t per = 1024 + 2 * (size_t)r->ntx_c * 1024;
+  for (int sb = 0; sb < r->nsb; sb++)
+    for (size_t i = 0; i < per; i++)
+      lc += (uint64_t)(int64_t)r->lev[sb * per + i] * (uint64_t)(i % 1024 + 1);
+  oslot *s = &r->slots[r->fi.display % NSLOT];
+  oplane *pl[3] = {&s->y, &s->u, &s->v};
+  int32_t gr[4] = {r->tx0, r->ty0, r->tw, r->th};
+  uint64_t gs = 0, fs = 0;
+  for (int p = 0; p < 3; p++) {
+    int rc[4];
+    group_rect(r, p, gr, rc);
+    for (int y = 0; y < rc[3]; y++)
+      for (int x = 0; x < rc[2]; x++) gs += (uint64_t)orc_px(at(pl[p], r->hbd, rc[0] + x, rc[1] + y), r->hbd, 0);
+    for (int y = 0; y < pl[p]->h; y++)
+      for (int x = 0; x < pl[p]->w; x++) fs += (uint64_t)orc_px(at(pl[p], r->hbd, x, y), r->hbd, 0);
+  }
+  out[nw + 0] = lc;
+  out[nw + 1] = gs;
+  out[nw + 2] = r->tail[2];
+  out[nw + 3] = (uint64_t)(r->vis_w / 8) * (r->vis_h / 8);
+  out[nw + 4] = fs;
+  return nw + 5;
 }

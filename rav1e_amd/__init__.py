@@ -64,11 +64,32 @@ DS_JOB = np.dtype([("po_x", "<i4"), ("po_y", "<i4"), ("mvx_min", "<i4"), ("mvx_m
 FS_RESULT = np.dtype([("mv_row", "<i2"), ("mv_col", "<i2"), ("reserved", "<u4"),
                       ("cost", "<u8")])
 REPLAY_CFG_FIELDS = ["width", "height", "xdec", "ydec", "bit_depth", "tile_x0", "tile_y0",
-                     "tile_w", "tile_h", "n_refs", "rdo_candidates", "flags"]
+                     "tile_w", "tile_h", "n_refs", "tile_w_sb", "tile_h_sb", "n_inputs", "flags"]
 
 
 class RvReplayCfg(C.Structure):
     _fields_ = [(f, C.c_int32) for f in REPLAY_CFG_FIELDS]
+
+
+class RvReplayLevelParams(C.Structure):
+    _fields_ = [("base_q_idx", C.c_int32), ("dc_delta_q", C.c_int32 * 3),
+                ("ac_delta_q", C.c_int32 * 3), ("reserved", C.c_int32), ("lambda_", C.c_double),
+                ("me_lambda", C.c_double), ("dist_scale", C.c_double * 3)]
+
+    @classmethod
+    def from_dict(cls, d):
+        p = cls()
+        p.base_q_idx = d["base_q_idx"]
+        for i in range(3):
+            p.dc_delta_q[i], p.ac_delta_q[i] = d["dc_delta_q"][i], d["ac_delta_q"][i]
+            p.dist_scale[i] = d["dist_scale"][i]
+        p.lambda_, p.me_lambda = d["lambda"], d["me_lambda"]
+        return p
+
+
+class RvReplayFrameInfo(C.Structure):
+    _fields_ = [("display", C.c_int32), ("me_range_scale", C.c_int32), ("level", C.c_int32),
+                ("is_key", C.c_int32), ("ref_display", C.c_int32 * 2)]
 
 
 # ---- reference enums ----------------------------------------------------
@@ -239,8 +260,21 @@ def _declare(L):
         "rv_plane_box_sums": (i32, [P, vp, vp]),
         "rv_replay_create": (vp, [C.POINTER(RvReplayCfg), vp]),
         "rv_replay_destroy": (None, [vp]),
-        "rv_replay_set_frame": (i32, [vp, i32, vp]),
-        "rv_replay_frame": (i32, [vp, i32]),
+        "rv_q_lookup": (i32, [i32, i32, i32]),
+        "rv_replay_synth_inputs": (i32, [vp, i32]),
+        "rv_replay_set_level_params": (i32, [vp, i32, C.POINTER(RvReplayLevelParams)]),
+        "rv_replay_set_input": (i32, [vp, i32, vp]),
+        "rv_replay_get_input": (i32, [vp, i32, vp]),
+        "rv_replay_get_recon": (i32, [vp, i32, vp]),
+        "rv_replay_set_importances": (i32, [vp, vp, i32]),
+        "rv_replay_frame": (i32, [vp, C.POINTER(RvReplayFrameInfo)]),
+        "rv_replay_set_groups": (i32, [vp, i32, vp, i32, vp]),
+        "rv_replay_exchange_buffers": (i32, [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                             C.POINTER(C.c_size_t)]),
+        "rv_replay_import": (i32, [vp]),
+        "rv_comm_unique_id": (i32, [vp, i32]),
+        "rv_comm_create": (vp, [vp, i32, i32]),
+        "rv_comm_destroy": (None, [vp]),
         "rv_replay_results": (i32, [vp, vp, i32]),
         "rv_replay_stage_times": (i32, [vp, vp, i32]),
         "rv_replay_stage_times_sum": (i32, [vp, i32, vp, i32]),

@@ -43,17 +43,11 @@ enum ChainMode {
   kChainCoarseToHalf = 1,  // F1 -> F2: pred[1 + r] of every reference's job
   kChainHalfToFull = 2,    // F2 -> F3 full-pel: pred[1]
   kChainFullToSub = 3,     // F3 full-pel -> F3 sub-pel: pred[0]
-  kChainSubToMc = 4,       // F3 sub-pel -> F4: the sub-pel MV candidate's MC jobs
 };
 
 struct ChainNext {
   int mode;
-  rv_ds_job *jobs;  // modes 1-3
-  // mode 4: candidate c = 2 * ref (sub-pel MV) of superblock sb predicts
-  // into the tall scratch planes at (sx * cw, (c * th + sy) * ch)
-  rv_mc_job *l_mc, *c_mc;
-  rv_plane luma, chroma;
-  int tw, th, tx0, ty0, cw, ch;
+  rv_ds_job *jobs;
 };
 
 // Called by one thread of the workgroup that finished job `job` (= r *
@@ -74,18 +68,80 @@ __device__ inline void chain_emit(const ChainNext &c, int job, int n_per_ref, in
     case kChainFullToSub:
       c.jobs[job].pred[0] = best;
       break;
-    case kChainSubToMc: {
-      const int sx = sb % c.tw, sy = sb / c.tw;
-      const int px = (sx + c.tx0) * 64, py = (sy + c.ty0) * 64;
-      const int cand = 2 * r;  // k = 0: the sub-pel MV
-      const int o = cand * n_per_ref + sb;
-      c.l_mc[o] = mc_job_for(c.luma, px, py, best, sx * 64, (cand * c.th + sy) * 64);
-      c.c_mc[o] = mc_job_for(c.chroma, px >> c.chroma.xdec, py >> c.chroma.ydec, best,
-                             sx * c.cw, (cand * c.th + sy) * c.ch);
-      break;
-    }
     default:
       break;
+  }
+}
+
+// ---- RDO inter candidates (rdo_mode_decision, src/rdo.rs:825-1006) ---------
+// Superblock grid of a replay instance: a rectangle of whole AV1 tiles
+// (uniform tile size tws x ths superblocks, TilingInfo, src/tiling/tiler.rs:
+// 49-126) at superblock (tx0, ty0) of the frame, tw x th superblocks.
+struct CandGeo {
+  int nsb, tw, th, tx0, ty0, tws, ths;
+  int R;  // references searched
+  int M;  // inter modes per reference (kCandModes)
+};
+
+// Per reference, rav1e pushes (src/rdo.rs:880-905, speed 10: no near MVs
+// beyond NEAR0): NEARESTMV, NEAR0MV if the MV stack is non-empty, GLOBALMV
+// if it holds >= 2 entries, NEWMV if the motion-search MV is non-zero and
+// not among the first two stack entries; every mode runs skip, then
+// non-skip unless skip had zero distortion (luma_chroma_mode_rdo, :649-700).
+// GLOBALMV is the zero MV (no global motion).
+enum CandMode { kNearestMv = 0, kNear0Mv = 1, kGlobalMv = 2, kNewMv = 3, kCandModes = 4 };
+
+__host__ __device__ inline bool mv_eq(rv_mv a, rv_mv b) { return a.row == b.row && a.col == b.col; }
+
+// The MV stack of superblock sb for reference k: find_mvrefs scans the row
+// above before the column to the left and merges equal MVs
+// (src/mvref / context.rs add_ref_mv_candidate); neighbours never cross a
+// tile edge.  The replay takes the neighbours' motion-search MVs (their
+// NEWMV) instead of the MVs their RDO chose, so every superblock of a frame
+// stays independent: one batched launch per stage.  Returns the entry
+// count (0..2); s0 / s1 the entries (scalars: no scratch on the device).
+__host__ __device__ inline int cand_stack(const CandGeo &g, const rv_fs_result *sub, int sb,
+                                          int k, rv_mv &s0, rv_mv &s1) {
+  const int sx = sb % g.tw, sy = sb / g.tw;
+  const int fx = g.tx0 + sx, fy = g.ty0 + sy;
+  const bool up = fy % g.ths != 0, left = fx % g.tws != 0;
+  const rv_mv zero{0, 0};
+  const rv_mv a = up ? sub[k * g.nsb + sb - g.tw].best_mv : zero;
+  const rv_mv l = left ? sub[k * g.nsb + sb - 1].best_mv : zero;
+  if (up) {
+    s0 = a;
+    s1 = l;
+    return left && !mv_eq(l, a) ? 2 : 1;
+  }
+  s0 = l;
+  s1 = zero;
+  return left ? 1 : 0;
+}
+
+// MV of candidate c = k * M + m of superblock sb; false if rav1e would not
+// push that mode (rdo_mode_decision's inter_mode_set).
+__host__ __device__ inline bool cand_mv(const CandGeo &g, const rv_fs_result *sub, int sb, int c,
+                                        rv_mv *mv) {
+  const int k = c / g.M, m = c - k * g.M;
+  rv_mv s0, s1;
+  const int n = cand_stack(g, sub, sb, k, s0, s1);
+  const rv_mv zero{0, 0};
+  switch (m) {
+    case kNearestMv:
+      *mv = n >= 1 ? s0 : zero;
+      return true;
+    case kNear0Mv:
+      *mv = n >= 2 ? s1 : zero;
+      return n >= 1;
+    case kGlobalMv:
+      *mv = zero;
+      return n >= 2;
+    default: {  // kNewMv
+      const rv_mv me = sub[k * g.nsb + sb].best_mv;
+      *mv = me;
+      return !(n >= 1 && mv_eq(s0, me)) && !(n >= 2 && mv_eq(s1, me)) &&
+             (me.row != 0 || me.col != 0);
+    }
   }
 }
 

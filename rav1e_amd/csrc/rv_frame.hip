@@ -64,9 +64,74 @@ __global__ __launch_bounds__(256) void pyramid_kernel(rv_plane y, rv_plane h, rv
   reinterpret_cast<Px *>(d.data)[i] = (Px)v;
 }
 
+// ---- synthetic input (integer form) --------------------------
+// The bench's y4m stand-in, generated in HBM (the inputs are resident before
+// the timed region, as an uploaded clip would be).  Pure integer arithmetic,
+// so rav1e_amd/replay.py:synth_frame (numpy) produces the same planes bit
+// for bit: a 2-D wave times a moving value-noise texture plus +-2 noise,
+// moving (1.25, 0.75) luma px per frame (sub-pel motion), per plane p at
+// luma-space quarter-pel coordinates.
+__host__ __device__ inline uint32_t synth_hash(uint32_t x) {  // lowbias32
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// integer parabola standing in for a sine of period P (amplitude 64)
+__host__ __device__ inline int synth_wave(int q, int P) {
+  const int h = P / 2;
+  return q < h ? 256 * q * (h - q) / (h * h) : -(256 * (q - h) * (P - q) / (h * h));
+}
+__host__ __device__ inline int synth_lat(int ix, int iy) {
+  return (int)(synth_hash((uint32_t)ix * 0x9E3779B1u ^ (uint32_t)iy * 0x85EBCA77u ^ 0x5EEDu) & 511) -
+         256;
+}
+template <typename Px>
+__global__ __launch_bounds__(256) void synth_kernel(rv_plane p, int t, int pidx, int bd) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)p.width * p.height) return;
+  const int y = (int)(i / p.width), x = (int)(i - (int64_t)y * p.width);
+  const int X4 = ((4 * x) << p.xdec) - 5 * t + 64 * pidx, Y4 = ((4 * y) << p.ydec) - 3 * t;
+  const int ix = X4 >> 5, fx = X4 & 31, iy = Y4 >> 5, fy = Y4 & 31;
+  const int v = (synth_lat(ix, iy) * (32 - fx) + synth_lat(ix + 1, iy) * fx) * (32 - fy) +
+                (synth_lat(ix, iy + 1) * (32 - fx) + synth_lat(ix + 1, iy + 1) * fx) * fy;
+  const int ta = pidx ? 12 : 24, wa = pidx ? 30 : 60;
+  const int tex = (v * ta) >> 18;
+  const int px = ((X4 % 388) + 388) % 388, py = ((Y4 % 244) + 244) % 244;
+  const int wave = (synth_wave(px, 388) * synth_wave(py, 244) * wa) >> 12;
+  const uint32_t hs = synth_hash((uint32_t)x * 0x27D4EB2Du ^ (uint32_t)y * 0x165667B1u ^
+                                 (uint32_t)t * 0x9E3779B9u ^ (uint32_t)pidx * 0x85EBCA6Bu);
+  const int noise = (int)(hs % 5u) - 2;
+  int v8 = 128 + wave + tex + noise;
+  v8 = v8 < 0 ? 0 : v8 > 255 ? 255 : v8;
+  const int val = (v8 << (bd - 8)) | (int)(synth_hash(hs ^ 0xABCDu) & ((1u << (bd - 8)) - 1));
+  *plane_ptr_mut<Px>(p, x, y) = (Px)val;
+}
+
 }  // namespace rv
 
 using namespace rv;
+
+// One synthetic frame t into planes y, u, v (visible area), then padded.
+int rv_synth_frame(const rv_plane *y, const rv_plane *u, const rv_plane *v, int t, int bit_depth,
+                   void *stream) {
+  const rv_plane *pl[3] = {y, u, v};
+  hipStream_t s = rv_resolve_stream(stream);
+  for (int k = 0; k < 3; k++) {
+    const int64_t n = (int64_t)pl[k]->width * pl[k]->height;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    if (pl[k]->hbd)
+      synth_kernel<uint16_t><<<g, 256, 0, s>>>(*pl[k], t, k, bit_depth);
+    else
+      synth_kernel<uint8_t><<<g, 256, 0, s>>>(*pl[k], t, k, bit_depth);
+    RV_HIP_CHECK_LAUNCH();
+    const int e = rv_plane_pad(pl[k], stream);
+    if (e != RV_OK) return e;
+  }
+  return RV_OK;
+}
 
 // hres = downsample(y) + pad, qres = downsample(hres) + pad, one launch.
 int rv_plane_pyramid(const rv_plane *y, const rv_plane *h, const rv_plane *q, void *stream) {

@@ -21,6 +21,7 @@
 
 #include "rv_device.h"
 #include "rv_quant_tables.h"
+#include "rv_rate_table.h"
 
 namespace rv {
 
@@ -193,6 +194,23 @@ __device__ __forceinline__ int quantize_block(const QCtx &c, const uint16_t *sca
 __device__ __forceinline__ int32_t q_dequant(const QCtx &c, int32_t q, int i) {
   return wadd(wmul(q, i == 0 ? c.dc_quant : c.ac_quant), (q >> 31) & ((1 << c.log_tx_scale) - 1)) >>
          c.log_tx_scale;
+}
+
+// estimate_rate (src/rdo.rs:204-216): the rate read off the trained table,
+// linearly interpolated between the two distortion bins around the block's
+// tx-domain distortion; i64 as in the reference (the bins differ by one, so
+// the divisor is RATE_EST_BIN_SIZE and the division truncates toward zero).
+__device__ __forceinline__ uint64_t q_estimate_rate(int qindex, int tx_size, uint64_t fd) {
+  const uint32_t *row =
+      RV_RDO_RATE_TABLE + ((qindex / RV_RDO_QUANT_DIV) * 19 + tx_size) * RV_RDO_NUM_BINS;
+  uint64_t down = fd / RV_RATE_EST_BIN_SIZE;
+  down = down < RV_RDO_NUM_BINS - 2 ? down : RV_RDO_NUM_BINS - 2;
+  const uint64_t up = down + 1;
+  const int64_t x0 = (int64_t)(down * RV_RATE_EST_BIN_SIZE);
+  const int64_t y0 = row[down], y1 = row[up];
+  const int64_t slope = (int64_t)((uint64_t)(y1 - y0) << 8) / RV_RATE_EST_BIN_SIZE;
+  const int64_t r = y0 + ((int64_t)((uint64_t)((int64_t)fd - x0) * (uint64_t)slope) >> 8);
+  return r > 0 ? (uint64_t)r : 0;
 }
 
 }  // namespace rv

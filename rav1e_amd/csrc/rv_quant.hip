@@ -1,7 +1,6 @@
 // rv_quant.hip -- batched quantize / dequantize (src/quantize.rs), one
 // wavefront per transform block (rv_quant.h has the algorithm).
 #include "rv_quant.h"
-#include "rv_rate_table.h"
 #include "rv_rdo.h"
 
 namespace rv {
@@ -46,26 +45,13 @@ __global__ __launch_bounds__(256) void dequantize_kernel(const int32_t *q, int t
   r[i] = wadd(wmul(v, quant), (v >> 31) & ((1 << lts) - 1)) >> lts;
 }
 
-// estimate_rate (src/rdo.rs:204-216), one block per thread: the rate read
-// off the trained table, linearly interpolated between the two distortion
-// bins around the block's tx-domain distortion; i64 as in the reference
-// (the bins differ by one, so the divisor is RATE_EST_BIN_SIZE and the
-// division truncates toward zero like Rust's).
+// estimate_rate (src/rdo.rs:204-216), one block per thread (q_estimate_rate).
 __global__ __launch_bounds__(256) void estimate_rate_kernel(const uint64_t *dist, int n,
-                                                            int row_off, uint64_t *rate) {
+                                                            int qindex, int tx_size,
+                                                            uint64_t *rate) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const uint32_t *row = RV_RDO_RATE_TABLE + row_off;
-  const uint64_t fd = dist[i];
-  uint64_t down = fd / RV_RATE_EST_BIN_SIZE;
-  down = down < RV_RDO_NUM_BINS - 2 ? down : RV_RDO_NUM_BINS - 2;
-  const uint64_t up = down + 1;
-  const int64_t x0 = (int64_t)(down * RV_RATE_EST_BIN_SIZE);
-  const int64_t y0 = row[down], y1 = row[up];
-  const int64_t slope = (int64_t)((uint64_t)(y1 - y0) << 8) / RV_RATE_EST_BIN_SIZE;
-  const int64_t r =
-      y0 + ((int64_t)((uint64_t)((int64_t)fd - x0) * (uint64_t)slope) >> 8);  // wrapping mul
-  rate[i] = r > 0 ? (uint64_t)r : 0;
+  rate[i] = q_estimate_rate(qindex, tx_size, dist[i]);
 }
 
 __global__ void q_ctx_kernel(int qindex, int area, int is_intra, int bd, int dc_delta_q,
@@ -142,9 +128,18 @@ extern "C" int rv_estimate_rate_batch(const uint64_t *d_tx_dist, int n, int qind
       (n > 0 && (!d_tx_dist || !d_rate)))
     return rv_set_error(RV_EINVAL, "rv_estimate_rate_batch: bad arguments");
   if (n == 0) return RV_OK;
-  const int q_bin = qindex / RV_RDO_QUANT_DIV;
   estimate_rate_kernel<<<(n + 255) / 256, 256, 0, rv_resolve_stream(stream)>>>(
-      d_tx_dist, n, (q_bin * 19 + tx_size) * RV_RDO_NUM_BINS, d_rate);
+      d_tx_dist, n, qindex, tx_size, d_rate);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
+}
+
+// dc_q / ac_q (src/quantize.rs:42-62) on the host: the fixed-quantizer
+// parameters (rav1e_amd/rate.py, src/rate.rs:746-775) select qindices from
+// these lookups.  ac = 0: dc_qlookup*_Q3, 1: ac_qlookup*_Q3; -1 on bad args.
+extern "C" int rv_q_lookup(int ac, int qindex, int bit_depth) {
+  if ((ac != 0 && ac != 1) || qindex < 0 || qindex > 255 ||
+      (bit_depth != 8 && bit_depth != 10 && bit_depth != 12))
+    return -1;
+  return RV_QLOOKUP_HOST[(3 * ac + (bit_depth - 8) / 2) * 256 + qindex];
 }

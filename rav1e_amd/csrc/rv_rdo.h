@@ -1,7 +1,9 @@
-// rv_rdo.h -- the fused RDO inter-candidate launch (rv_rdo.hip), used by the
-// replay driver's stage F4.
+// rv_rdo.h -- the fused RDO inter-candidate launches (rv_rdo.hip) of the
+// replay driver: stage F4 (score every candidate) and F6 (commit the
+// winner of every superblock into the reconstruction).
 #pragma once
 
+#include "rv_chain.h"
 #include "rv_device.h"
 #include "rv_quant.h"
 
@@ -10,25 +12,36 @@ namespace rv {
 struct RdoPlane {
   rv_plane org;                  // source plane
   rv_plane ref[RV_DS_MAX_PRED];  // reference planes of this plane type
-  rv_plane dst;                  // tall prediction / reconstruction plane
-  const rv_mc_job *mc;           // per candidate
-  const rv_tx_job *tx;           // per (candidate, transform block)
-  int32_t *packed;               // per transform block: min(N,32)^2 i32
-  void *dist;                    // luma: i64 x 5 per 8x8; chroma: u64 per sub-block
+  rv_plane dst;                  // commit: the reconstruction plane (frame slot)
+  int32_t *levels;               // commit: CA i32 levels per transform block
+  uint64_t *out;                 // score: [dist skip, dist non-skip, rate] per transform block
+  QCtx q;                        // QuantizationContext of this plane's transform
+};
+
+// The winner of a superblock (score_candidates -> commit).
+struct RdoWinner {
+  int32_t c;     // candidate index (ref * M + mode)
+  int32_t skip;  // 1: the skip variant (no residual)
+  double cost;   // compute_rd_cost
+  uint64_t dist; // its ScaledDistortion
 };
 
 struct RdoArgs {
-  RdoPlane p[2];      // blockIdx.y selects the plane (chroma: U, V)
-  int n_tx;           // transform blocks per plane in this launch
-  int k_sel;          // -1: every candidate; 0 / 1: only candidates 2r + k_sel
-  int nsb;            // superblocks (candidate c of SB sb = c * nsb + sb)
-  int ntx_per_cand;   // transform blocks per candidate
-  int cands_per_ref;  // candidates of one reference (job arrays are ref-major)
+  RdoPlane p[2];       // chroma: U, V (the launch's blocks cover both)
+  CandGeo g;           // superblock grid + candidate MVs (rv_chain.h)
+  const rv_fs_result *sub;  // NEWMV of every (reference, superblock)
+  const RdoWinner *win;     // commit: per superblock
+  const float *imp;         // block_importances (w_imp per row), may be null
+  int w_in_b, h_in_b, w_imp;
+  int n_tx;            // transform blocks per plane in this launch
+  int commit;          // 0: score every candidate, 1: commit the winners
+  int ntx_per_cand;    // transform blocks per candidate
   int bd;
-  int mb_w, mb_h;     // MC block size (filter choice, distortion grid)
-  int sub_w, sub_h;   // distortion sub-block (SSE); moments use 8x8
-  QCtx q;             // QuantizationContext of this plane type's transform
-  int q_tx_index;     // tx_size * 16 + tx_type: av1_scan_orders entry
+  int mb_w, mb_h;      // prediction block (filter choice)
+  int sub_w, sub_h;    // SSE distortion sub-block (chroma)
+  int xdec, ydec;      // this plane type's subsampling
+  int q_tx_index;      // tx_size * 16 + tx_type: av1_scan_orders entry
+  int tx_size, qindex; // estimate_rate
 };
 
 }  // namespace rv
@@ -38,7 +51,7 @@ struct RdoArgs {
 int rv_quant_ctx(int qindex, int tx_area, int is_intra, int bit_depth, int dc_delta_q,
                  int ac_delta_q, rv::QCtx *out);
 
-// Luma candidates (64x64 transform, cdef moments) and the chroma transform
-// blocks of planes U and V (32x32, SSE partials) in one launch.
+// Luma candidates (64x64 transform, cdef distortion) and the chroma
+// transform blocks of planes U and V (32x32, SSE) in one launch.
 int rv_rdo_candidates(const rv::RdoArgs &luma, const rv::RdoArgs &chroma, int hbd,
-                      hipStream_t s, hipStream_t chroma_stream = nullptr);
+                      hipStream_t s);

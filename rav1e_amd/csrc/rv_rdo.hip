@@ -1,25 +1,34 @@
 // rv_rdo.hip -- fused RDO inter-candidate evaluation (replay stage F4).
 //
 // One wavefront per (candidate, transform block) runs the whole per-
-// candidate chain of encode_tx_block (src/encoder.rs:1077-1237) for the
+// candidate chain of luma_chroma_mode_rdo -> encode_block_post_cdef ->
+// encode_tx_block (src/rdo.rs:649-700, src/encoder.rs:1077-1237) for the
 // pixel-domain distortion of the default tune (src/rdo.rs:338-411):
 //
 //   predict_inter's put_8tap (src/mc.rs:213-307, REGULAR, via
 //   src/predict.rs:255-338)            -> prediction in LDS
+//   skip variant: compute_distortion of the prediction (cdef_dist_wxh x
+//   compute_distortion_bias for luma, sse_wxh x bias for chroma,
+//   src/rdo.rs:219-335, 476-508)       -> one u64
 //   diff (src/encoder.rs:1044-1058) + FwdTxfm2D::fht DCT_DCT
 //   (src/transform/forward.rs:1804-1899) -> coefficients in LDS
 //   quantize (src/quantize.rs:255-316, QuantizationContext at the
 //   replay's qindex) on the first coded_tx_area entries of the W-stride
-//   raster, the slice encode_tx_block hands it   -> levels to HBM
+//   raster, the slice encode_tx_block hands it; the tx-domain distortion
+//   of that slice against its dequantized values -> estimate_rate
+//   (src/encoder.rs:1214-1231, src/rdo.rs:204-216)
 //   dequantize (src/quantize.rs:319-333)      -> the inverse's input in LDS
 //   inv_txfm2d_add (src/transform/inverse.rs:1939-2114)
-//                                      -> reconstruction in LDS + HBM
-//   cdef_dist_wxh_8x8 moments (src/rdo.rs:219-241, luma) or sse_wxh
-//   partials (src/rdo.rs:286-335, chroma) -> HBM
+//                                      -> reconstruction in LDS
+//   non-skip variant: compute_distortion of the reconstruction -> one u64
 //
-// Every intermediate (prediction, residual, 64x64 i32 coefficient block,
-// reconstruction) stays in the wavefront's LDS slab; HBM sees the reference
-// window, the source block, and the results the encoder keeps.  The
+// Score launch (F4): every candidate; HBM receives three u64 per candidate
+// transform block [skip distortion, non-skip distortion, rate].  Commit
+// launch (F6): the winner of every superblock runs the same chain (levels
+// forced to zero for a skip winner, which makes the reconstruction the
+// prediction) and stores its levels (the entropy coder's input) and its
+// reconstruction into the frame.  Every intermediate stays in the
+// wavefront's LDS slab.  The
 // standalone batched kernels (rv_put_8tap_batch, rv_diff_fwd_txfm_batch,
 // rv_inv_txfm_add_batch, rv_cdef_moments_batch, rv_sse_batch) compute the
 // same values one stage per launch; the replay parity test pins the fused
@@ -74,11 +83,130 @@ __device__ __forceinline__ int32_t rdo_rsa(int32_t v, int bit) {
   return v;
 }
 
+// The per-task job: candidate (score) or superblock winner (commit) ->
+// prediction block, transform block inside it, MC source and fracs.
+struct RdoJob {
+  int bx, by;        // prediction block origin in the plane
+  int ox, oy;        // transform block offset inside the prediction block
+  int src_x, src_y;  // predict_inter's clamped integer source position
+  int cf, rf;        // 1/16-pel fracs
+  int ref;           // reference index
+  bool zero;         // commit of a skip winner: every level is zero
+};
+
+template <int N>
+__device__ __forceinline__ RdoJob rdo_job(const RdoArgs &a, const RdoPlane &pl, int t) {
+  const int cand = t / a.ntx_per_cand, sub = t - cand * a.ntx_per_cand;
+  int sb, c;
+  RdoJob j;
+  j.zero = false;
+  if (a.commit) {
+    sb = cand;
+    c = a.win[sb].c;
+    j.zero = a.win[sb].skip != 0;
+  } else {
+    c = cand / a.g.nsb;
+    sb = cand - c * a.g.nsb;
+  }
+  rv_mv mv;
+  (void)cand_mv(a.g, a.sub, sb, c, &mv);
+  j.ref = c / a.g.M;
+  const int sx = sb % a.g.tw, sy = sb / a.g.tw;
+  j.bx = ((a.g.tx0 + sx) * 64) >> a.xdec;
+  j.by = ((a.g.ty0 + sy) * 64) >> a.ydec;
+  const int txc = a.mb_w / N;
+  j.ox = (sub % txc) * N;
+  j.oy = (sub / txc) * N;
+  const rv_mc_job m = mc_job_for(pl.ref[j.ref], j.bx, j.by, mv, 0, 0);
+  j.src_x = m.src_x;
+  j.src_y = m.src_y;
+  j.cf = m.col_frac;
+  j.rf = m.row_frac;
+  return j;
+}
+
+// compute_distortion_bias (src/rdo.rs:476-508) of the BLOCK_8X8 importance
+// area at 4x4-block (mi_x, mi_y) of the frame: compute_mean_importance sums
+// the f32 importances of the in-frame 4x4 blocks in y-then-x order and
+// divides by the full area; the bias is (mean / 3) as f64 + 0.65.
+__device__ __forceinline__ double rdo_bias(const RdoArgs &a, int mi_x, int mi_y) {
+  if (!a.imp) return 0.65;  // (0f32 / 3) as f64 + 0.65
+  const int x2 = mi_x + 2 < a.w_in_b ? mi_x + 2 : a.w_in_b;
+  const int y2 = mi_y + 2 < a.h_in_b ? mi_y + 2 : a.h_in_b;
+  float tot = 0.f;
+  for (int y = mi_y; y < y2; y++)
+    for (int x = mi_x; x < x2; x++) tot = __fadd_rn(tot, a.imp[(y >> 1) * a.w_imp + (x >> 1)]);
+  return (double)__fdiv_rn(__fdiv_rn(tot, 4.0f), 3.0f) + 0.65;
+}
+// RawDistortion * bias (src/rdo.rs:539-544): `(value as f64 * bias) as u64`
+__device__ __forceinline__ uint64_t rdo_biased(uint64_t v, double bias) {
+  return (uint64_t)((double)v * bias);
+}
+
+// cdef_dist_wxh_8x8 (src/rdo.rs:219-261) of the 8x8 block at o (plane) vs
+// d (LDS, row pitch dp): i32 / i64 moments (64 products of 12-bit pixels
+// stay below 2^30: u32 sums, one v_mad_u32_u24 per product), then the f64
+// ssim boost; `(sse * ssim_boost + 0.5) as u64`.
+template <typename Px>
+__device__ __forceinline__ uint64_t rdo_cdef_8x8(const Px *o, int64_t os, const Px *d, int dp,
+                                                 int bd) {
+  int32_t ss = 0, sd = 0;
+  uint32_t ss2 = 0, sd2 = 0, ssd = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++)
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int32_t s = o[(int64_t)j * os + i];
+      const int32_t e = d[j * dp + i];
+      ss += s;
+      sd += e;
+      ss2 += (uint32_t)wmul24(s, s);
+      sd2 += (uint32_t)wmul24(e, e);
+      ssd += (uint32_t)wmul24(s, e);
+    }
+  const int cs = bd - 8;
+  const int64_t s2 = (int64_t)ss2, d2 = (int64_t)sd2, sdv = (int64_t)ssd;
+  const double svar = (double)(s2 - (((int64_t)ss * ss + 32) >> 6));
+  const double dvar = (double)(d2 - (((int64_t)sd * sd + 32) >> 6));
+  const double sse = (double)(d2 + s2 - 2 * sdv);
+  const double boost = (4033.0 / 16384.0) * (svar + dvar + (double)(16384ll << (2 * cs))) /
+                       sqrt((double)(16265089ull << (4 * cs)) + svar * dvar);
+  const double v = sse * boost + 0.5;
+  return v > 0.0 ? (uint64_t)v : 0;
+}
+
+// sse_wxh (src/rdo.rs:286-335) over the transform block's sub-blocks (bw x
+// bh chroma pixels = an 8x8 importance block), each biased; lanes of a
+// group of LPB stride over the sub-blocks.  Returns the lane's partial sum.
+template <typename Px, int N, int LPB>
+__device__ __forceinline__ uint64_t rdo_sse_biased(const RdoArgs &a, const RdoJob &j, const Px *o,
+                                                   int64_t os, const Px *d) {
+  const int bw = a.sub_w, bh = a.sub_h, nbx = N / bw, nby = N / bh;
+  const int lane = threadIdx.x & (LPB - 1);
+  uint64_t acc = 0;
+  for (int k = lane; k < nbx * nby; k += LPB) {
+    const int by = k / nbx, bx = k - by * nbx;
+    uint64_t value = 0;
+    for (int jj = 0; jj < bh; jj++) {
+      uint32_t row = 0;
+      for (int i = 0; i < bw; i++) {
+        const int32_t c = (int32_t)(int16_t)o[(int64_t)(by * bh + jj) * os + bx * bw + i] -
+                          (int32_t)(int16_t)d[(by * bh + jj) * N + bx * bw + i];
+        row += (uint32_t)wmul24(c, c);
+      }
+      value += row;
+    }
+    const int px = j.bx + j.ox + bx * bw, py = j.by + j.oy + by * bh;
+    acc += rdo_biased(value, rdo_bias(a, (px << a.xdec) >> 2, (py << a.ydec) >> 2));
+  }
+  return acc;
+}
+
 // LPB = lanes per transform block: 64 (luma, N = 64) or 32 (chroma, N = 32:
 // a wavefront carries two chroma blocks, one per half, so every phase keeps
 // all 64 lanes busy).  `valid` = false for a second half without a block:
 // it recomputes its partner's block and stores nothing.
-template <typename Px, int N, bool MOMENTS, int LPB>
+template <typename Px, int N, int LPB>
 __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &pl, int t,
                                               bool valid, int32_t *buf, Px *pred,
                                               const uint16_t *scan) {
@@ -89,12 +217,11 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   constexpr int C32 = N < 32 ? N : 32;           // coded coefficient extent
   static_assert((N + 7) * P <= N * S * 4, "window must fit the coefficient slab");
   const int lane = threadIdx.x & (LPB - 1);
-  const int cand = t / a.ntx_per_cand;
-  const rv_mc_job mj = pl.mc[cand];
-  const rv_tx_job tj = pl.tx[t];
-  const rv_plane &ref = pl.ref[cand / a.cands_per_ref];
-  const int ox = tj.pred_x - mj.dst_x, oy = tj.pred_y - mj.dst_y;  // in the MC block
+  const RdoJob jb = rdo_job<N>(a, pl, t);
+  const rv_plane &ref = pl.ref[jb.ref];
+  const int ox = jb.ox, oy = jb.oy;  // in the MC block
   const int bd = a.bd, ib = bd == 12 ? 2 : 4, maxv = (1 << bd) - 1;
+  const int sx0 = jb.bx + ox, sy0 = jb.by + oy;  // the transform block in the plane
   auto wave_sync = [] {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -104,7 +231,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   // ---- A. put_8tap into LDS ------------------------------------------------
   {
     uint32_t *win = reinterpret_cast<uint32_t *>(buf);
-    const uint8_t *sp = (const uint8_t *)plane_ptr<Px>(ref, mj.src_x + ox - 3, mj.src_y + oy - 3);
+    const uint8_t *sp = (const uint8_t *)plane_ptr<Px>(ref, jb.src_x + ox - 3, jb.src_y + oy - 3);
     const int64_t rs = (int64_t)ref.stride * B;
     constexpr int kRowDw = ((N + 7) * B + 3) / 4;
     constexpr int kTot = (N + 7) * kRowDw;
@@ -116,7 +243,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
       win[r * (P / 4) + d] = B == 1 ? v ^ 0x80808080u : v;  // u8: stored as i8 = px - 128
     }
     wave_sync();
-    const int cf = mj.col_frac, rf = mj.row_frac;
+    const int cf = jb.cf, rf = jb.rf;
     const int8_t *xf = kRdoReg[a.mb_w <= 4][cf];
     const int8_t *yf = kRdoReg[a.mb_h <= 4][rf];
     int yt[8];
@@ -193,6 +320,13 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     }
     wave_sync();  // window reads done (buf is reused), prediction visible
   }
+  const Px *o = plane_ptr<Px>(pl.org, sx0, sy0);
+  const int64_t ost = pl.org.stride;
+  // ---- skip variant: sse_wxh of the prediction ------------------------------
+  if (!a.commit) {
+    const uint64_t d = group_sum<LPB>(rdo_sse_biased<Px, N, LPB>(a, jb, o, ost, pred));
+    if (valid && lane == 0) pl.out[(int64_t)t * 3 + 0] = d;
+  }
 
   int s0, s1, s2;
   fwd_shifts<N>((bd - 8) / 2, s0, s1, s2);
@@ -200,7 +334,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   {
     constexpr int PPD = 4 / B;                 // pixels per dword
     constexpr int DPR = N / PPD;               // dwords per row
-    const uint8_t *op = (const uint8_t *)plane_ptr<Px>(pl.org, tj.src_x, tj.src_y);
+    const uint8_t *op = (const uint8_t *)o;
     const int64_t os = (int64_t)pl.org.stride * B;
 #pragma unroll 8
     for (int i = lane; i < N * DPR; i += LPB) {
@@ -244,18 +378,33 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   // place (the inverse transform's input, raster entry i = packed entry i)
   // Levels go back in place (scattered LDS writes); then one coalesced
   // pass stores them to HBM and dequantizes them in place.
+  // the tx-domain distortion of the coded slice against its dequantized
+  // values (src/encoder.rs:1214-1224): wrapping i32 square, sign-extended
+  uint64_t txd = 0;
   quantize_block<CA, LPB>(
-      a.q, scan, [&](int pos) { return buf[(pos / N) * S + (pos % N)]; },
-      [&](int pos, int32_t q, int32_t) { buf[(pos / N) * S + (pos % N)] = q; });
+      pl.q, scan, [&](int pos) { return buf[(pos / N) * S + (pos % N)]; },
+      [&](int pos, int32_t q, int32_t r) {
+        int32_t *e = buf + (pos / N) * S + (pos % N);
+        const int32_t dd = wsub(*e, r);
+        txd += (uint64_t)(int64_t)wmul(dd, dd);
+        *e = jb.zero ? 0 : q;
+      });
   wave_sync();
+  if (!a.commit) {
+    txd = group_sum<LPB>(txd);
+    const int bits = 2 * (3 - pl.q.log_tx_scale);
+    if (valid && lane == 0)
+      pl.out[(int64_t)t * 3 + 2] =
+          q_estimate_rate(a.qindex, a.tx_size, (txd + (1ull << (bits - 1))) >> bits);
+  }
   {
-    int32_t *pk = pl.packed + (int64_t)t * CA;
+    int32_t *pk = pl.levels + (int64_t)t * CA;
 #pragma unroll 4
     for (int i = lane; i < CA; i += LPB) {
       int32_t *e = buf + (i / N) * S + (i % N);
       const int32_t q = *e;
-      if (valid) pk[i] = q;
-      *e = q_dequant(a.q, q, i);
+      if (valid && a.commit) pk[i] = q;
+      *e = q_dequant(pl.q, q, i);
     }
   }
   wave_sync();
@@ -294,10 +443,9 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     }
   }
   wave_sync();
-  // reconstruction -> the tall plane, coalesced dwords
-  {
+  if (a.commit) {  // reconstruction -> the frame, coalesced dwords
     constexpr int PPD = 4 / B, DPR = N / PPD;
-    uint8_t *dp = (uint8_t *)plane_ptr_mut<Px>(pl.dst, tj.pred_x, tj.pred_y);
+    uint8_t *dp = (uint8_t *)plane_ptr_mut<Px>(pl.dst, sx0, sy0);
     const int64_t ds = (int64_t)pl.dst.stride * B;
 #pragma unroll 8
     for (int i = lane; i < N * DPR; i += LPB) {
@@ -306,59 +454,11 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
       __builtin_memcpy(&v, pred + r * N + c, 4);
       if (valid) __builtin_memcpy(dp + r * ds + c * B, &v, 4);
     }
+    return;
   }
-  // ---- E. distortion partials of org vs reconstruction ---------------------
-  const Px *o = plane_ptr<Px>(pl.org, tj.src_x, tj.src_y);
-  if constexpr (MOMENTS) {
-    constexpr int NB = N / 8;  // 8x8 blocks per row of this transform block
-    const int sub_x = a.mb_w / 8, nsub = sub_x * (a.mb_h / 8);
-    for (int k = lane; k < NB * NB; k += LPB) {
-      const int by = k / NB, bx = k - by * NB;
-      // 64 products of 12-bit pixels stay below 2^30: u32 sums, one
-      // v_mad_u32_u24 per product, widened to the reference's i64 at the end
-      int32_t ss = 0, sd = 0;
-      uint32_t ss2 = 0, sd2 = 0, ssd = 0;
-#pragma unroll
-      for (int j = 0; j < 8; j++)
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          const int32_t s = o[(int64_t)(by * 8 + j) * pl.org.stride + bx * 8 + i];
-          const int32_t d = pred[(by * 8 + j) * N + bx * 8 + i];
-          ss += s;
-          sd += d;
-          ss2 += (uint32_t)wmul24(s, s);
-          sd2 += (uint32_t)wmul24(d, d);
-          ssd += (uint32_t)wmul24(s, d);
-        }
-      const int kk = ((oy >> 3) + by) * sub_x + (ox >> 3) + bx;
-      int64_t *m = (int64_t *)pl.dist + ((int64_t)cand * nsub + kk) * 5;
-      if (!valid) continue;
-      m[0] = ss;
-      m[1] = sd;
-      m[2] = (int64_t)ss2;
-      m[3] = (int64_t)sd2;
-      m[4] = (int64_t)ssd;
-    }
-  } else {
-    const int bw = a.sub_w, bh = a.sub_h;
-    const int nbx = N / bw, nby = N / bh;
-    const int sub_x = a.mb_w / bw, nsub = sub_x * (a.mb_h / bh);
-    for (int k = lane; k < nbx * nby; k += LPB) {
-      const int by = k / nbx, bx = k - by * nbx;
-      uint64_t value = 0;
-      for (int j = 0; j < bh; j++) {
-        uint32_t row = 0;
-        for (int i = 0; i < bw; i++) {
-          const int32_t c = (int32_t)(int16_t)o[(int64_t)(by * bh + j) * pl.org.stride + bx * bw + i] -
-                            (int32_t)(int16_t)pred[(by * bh + j) * N + bx * bw + i];
-          row += (uint32_t)wmul24(c, c);
-        }
-        value += row;
-      }
-      const int kk = (oy / bh + by) * sub_x + ox / bw + bx;
-      if (valid) ((uint64_t *)pl.dist)[(int64_t)cand * nsub + kk] = value;
-    }
-  }
+  // ---- non-skip variant: sse_wxh of the reconstruction ----------------------
+  const uint64_t d = group_sum<LPB>(rdo_sse_biased<Px, N, LPB>(a, jb, o, ost, pred));
+  if (valid && lane == 0) pl.out[(int64_t)t * 3 + 1] = d;
 }
 
 // ---- luma candidates: 64x64 --------------------------------------------------
@@ -391,25 +491,35 @@ struct LumaLds {
 
 // MC into pred, then residual + column DCT: fmid = scr as i32 [16][65].  No
 // trailing synchronisation (the caller's).
+// The lane's 8x8 block (lane = 8 * row + column) of the 64x64 luma block:
+// cdef_dist_wxh_8x8 x compute_distortion_bias, summed over the wavefront
+// (cdef_dist_wxh, src/rdo.rs:263-283) -- the luma compute_distortion.
+template <typename Px>
+__device__ __forceinline__ uint64_t luma_dist(const RdoArgs &a, const RdoJob &j, const Px *o,
+                                              int64_t os, const Px *pred) {
+  const int lane = threadIdx.x & 63, by = lane >> 3, bx = lane & 7;
+  const uint64_t v =
+      rdo_cdef_8x8<Px>(o + (int64_t)(by * 8) * os + bx * 8, os, pred + by * 8 * 64 + bx * 8, 64, a.bd);
+  const int px = j.bx + bx * 8, py = j.by + by * 8;
+  return group_sum<64>(rdo_biased(v, rdo_bias(a, px >> 2, py >> 2)));
+}
+
 template <typename Px, int NPART>
 __device__ __forceinline__ void luma_front(const RdoArgs &a, const RdoPlane &pl, int t,
-                                           uint8_t *scr, Px *pred) {
+                                           const RdoJob &jb, bool valid, uint8_t *scr, Px *pred) {
   constexpr int N = 64, B = (int)sizeof(Px);
   constexpr int P = LumaLds<Px, int16_t, NPART>::kWinP;
   constexpr int RP = N / NPART;  // output rows per band
   static_assert(RP % 8 == 0, "MC rows run in groups of 8");
   const int lane = threadIdx.x & 63;
-  const int cand = t / a.ntx_per_cand;
-  const rv_mc_job mj = pl.mc[cand];
-  const rv_tx_job tj = pl.tx[t];
-  const rv_plane &ref = pl.ref[cand / a.cands_per_ref];
-  const int ox = tj.pred_x - mj.dst_x, oy = tj.pred_y - mj.dst_y;
+  const rv_plane &ref = pl.ref[jb.ref];
+  const int ox = 0, oy = 0;
   const int bd = a.bd, ib = bd == 12 ? 2 : 4, maxv = (1 << bd) - 1;
 
   // ---- A. put_8tap (src/mc.rs:213-307) into pred, NPART bands --------------
   {
     uint32_t *win = reinterpret_cast<uint32_t *>(scr);
-    const int cf = mj.col_frac, rf = mj.row_frac;
+    const int cf = jb.cf, rf = jb.rf;
     const int8_t *xf = kRdoReg[a.mb_w <= 4][cf];
     const int8_t *yf = kRdoReg[a.mb_h <= 4][rf];
     int yt[8];
@@ -467,7 +577,7 @@ __device__ __forceinline__ void luma_front(const RdoArgs &a, const RdoPlane &pl,
 #pragma unroll 1
     for (int half = 0; half < NPART; half++) {
       const uint8_t *sp =
-          (const uint8_t *)plane_ptr<Px>(ref, mj.src_x + ox - 3, mj.src_y + oy - 3 + RP * half);
+          (const uint8_t *)plane_ptr<Px>(ref, jb.src_x + ox - 3, jb.src_y + oy - 3 + RP * half);
       if (half) wave_sync();  // the previous band's window reads are done
 #pragma unroll 4
       for (int i = lane; i < kTot; i += 64) {
@@ -503,9 +613,14 @@ __device__ __forceinline__ void luma_front(const RdoArgs &a, const RdoPlane &pl,
     wave_sync();  // window reads done (scr is reused), prediction visible
   }
 
+  const Px *o = plane_ptr<Px>(pl.org, jb.bx, jb.by);
+  // ---- skip variant: compute_distortion of the prediction -------------------
+  if (!a.commit) {
+    const uint64_t d = luma_dist<Px>(a, jb, o, pl.org.stride, pred);
+    if (valid && lane == 0) pl.out[(int64_t)t * 3 + 0] = d;
+  }
   int s0, s1, s2;
   fwd_shifts<N>((bd - 8) / 2, s0, s1, s2);
-  const Px *o = plane_ptr<Px>(pl.org, tj.src_x, tj.src_y);
   int32_t *fmid = reinterpret_cast<int32_t *>(scr);  // [16][65]: column-DCT rows 0..15
   // ---- B + C. residual (src/encoder.rs:1044-1058) and the column DCT -------
   {
@@ -536,23 +651,38 @@ __device__ __forceinline__ void luma_fwd_row(int32_t *row, int bd) {
 
 // quantize + dequantize of the candidate's coded 32x32 area (raster entries
 // 0..1023 of the 64x64 fht output = fmid rows 0..15, src/encoder.rs:1170,
-// 1192): levels -> pl.packed (the entropy coder's input), dequantized
-// values in place (the inverse transform's input).
+// 1192), dequantized values in place (the inverse transform's input).
+// Score: the tx-domain distortion of the slice -> estimate_rate -> out[2].
+// Commit: levels -> pl.levels (the entropy coder's input), zero for a skip
+// winner.
 __device__ __forceinline__ void luma_quantize(const RdoArgs &a, const RdoPlane &pl, int t,
-                                              int32_t *fmid, const uint16_t *scan) {
+                                              const RdoJob &jb, bool valid, int32_t *fmid,
+                                              const uint16_t *scan) {
+  uint64_t txd = 0;
   quantize_block<1024, 64>(
-      a.q, scan, [&](int pos) { return fmid[(pos >> 6) * 65 + (pos & 63)]; },
-      [&](int pos, int32_t q, int32_t) { fmid[(pos >> 6) * 65 + (pos & 63)] = q; });
-  wave_sync();
-  // levels to HBM (coalesced), dequantized in place
-  int32_t *pk = pl.packed + (int64_t)t * 1024;
+      pl.q, scan, [&](int pos) { return fmid[(pos >> 6) * 65 + (pos & 63)]; },
+      [&](int pos, int32_t q, int32_t r) {
+        int32_t *e = fmid + (pos >> 6) * 65 + (pos & 63);
+        const int32_t dd = wsub(*e, r);
+        txd += (uint64_t)(int64_t)wmul(dd, dd);
+        *e = jb.zero ? 0 : q;
+      });
   const int lane = threadIdx.x & 63;
+  if (!a.commit) {
+    txd = group_sum<64>(txd);
+    const int bits = 2 * (3 - pl.q.log_tx_scale);
+    if (valid && lane == 0)
+      pl.out[(int64_t)t * 3 + 2] =
+          q_estimate_rate(a.qindex, a.tx_size, (txd + (1ull << (bits - 1))) >> bits);
+  }
+  wave_sync();
+  int32_t *pk = pl.levels + (int64_t)t * 1024;
 #pragma unroll 4
   for (int i = lane; i < 1024; i += 64) {
     int32_t *e = fmid + (i >> 6) * 65 + (i & 63);
     const int32_t q = *e;
-    pk[i] = q;
-    *e = q_dequant(a.q, q, i);
+    if (a.commit) pk[i] = q;
+    *e = q_dequant(pl.q, q, i);
   }
 }
 
@@ -578,20 +708,17 @@ __device__ __forceinline__ void luma_inv_row_tx(int32_t *v, Mid *dst, int range,
   for (int c = 0; c < 64; c++) dst[c] = (Mid)tx::clampv(round_shift(v[c], 2), crange);
 }
 
-// Inverse columns + add into pred, reconstruction to the tall plane, cdef
-// moments.  imid = [32][66] row-pass output.
+// Inverse columns + add into pred; commit: the reconstruction -> the
+// frame; score: the non-skip compute_distortion -> out[1].  imid = [32][66]
+// row-pass output.
 template <typename Px, typename Mid>
 __device__ __forceinline__ void luma_back(const RdoArgs &a, const RdoPlane &pl, int t,
-                                          const Mid *imid, Px *pred) {
+                                          const RdoJob &jb, bool valid, const Mid *imid,
+                                          Px *pred) {
   constexpr int N = 64, B = (int)sizeof(Px);
   const int lane = threadIdx.x & 63;
-  const int cand = t / a.ntx_per_cand;
-  const rv_mc_job mj = pl.mc[cand];
-  const rv_tx_job tj = pl.tx[t];
-  const int ox = tj.pred_x - mj.dst_x, oy = tj.pred_y - mj.dst_y;
   const int bd = a.bd, maxv = (1 << bd) - 1;
   const int crange = bd + 6 > 16 ? bd + 6 : 16;
-  const Px *o = plane_ptr<Px>(pl.org, tj.src_x, tj.src_y);
   // ---- D'. inverse columns + add into pred ---------------------------------
   {
     int32_t v[N];
@@ -605,58 +732,36 @@ __device__ __forceinline__ void luma_back(const RdoArgs &a, const RdoPlane &pl, 
     }
   }
   wave_sync();
-  // reconstruction -> the tall plane, coalesced dwords
-  {
+  if (a.commit) {  // reconstruction -> the frame, coalesced dwords
     constexpr int PPD = 4 / B, DPR = N / PPD;
-    uint8_t *dp = (uint8_t *)plane_ptr_mut<Px>(pl.dst, tj.pred_x, tj.pred_y);
+    uint8_t *dp = (uint8_t *)plane_ptr_mut<Px>(pl.dst, jb.bx, jb.by);
     const int64_t ds = (int64_t)pl.dst.stride * B;
 #pragma unroll 8
     for (int i = lane; i < N * DPR; i += 64) {
       const int r = i / DPR, c = (i - r * DPR) * PPD;
       uint32_t v;
       __builtin_memcpy(&v, pred + r * N + c, 4);
-      __builtin_memcpy(dp + r * ds + c * B, &v, 4);
+      if (valid) __builtin_memcpy(dp + r * ds + c * B, &v, 4);
     }
+    return;
   }
-  // ---- E. cdef_dist_wxh_8x8 moments (src/rdo.rs:219-241), one 8x8 per lane
-  {
-    const int by = lane >> 3, bx = lane & 7;
-    const int sub_x = a.mb_w / 8, nsub = sub_x * (a.mb_h / 8);
-    int32_t ss = 0, sd = 0;
-    uint32_t ss2 = 0, sd2 = 0, ssd = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++)
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const int32_t s = o[(int64_t)(by * 8 + j) * pl.org.stride + bx * 8 + i];
-        const int32_t d = pred[(by * 8 + j) * N + bx * 8 + i];
-        ss += s;
-        sd += d;
-        ss2 += (uint32_t)wmul24(s, s);
-        sd2 += (uint32_t)wmul24(d, d);
-        ssd += (uint32_t)wmul24(s, d);
-      }
-    const int kk = ((oy >> 3) + by) * sub_x + (ox >> 3) + bx;
-    int64_t *m = (int64_t *)pl.dist + ((int64_t)cand * nsub + kk) * 5;
-    m[0] = ss;
-    m[1] = sd;
-    m[2] = (int64_t)ss2;
-    m[3] = (int64_t)sd2;
-    m[4] = (int64_t)ssd;
-  }
+  // ---- E. non-skip variant: compute_distortion of the reconstruction -------
+  const uint64_t d = luma_dist<Px>(a, jb, plane_ptr<Px>(pl.org, jb.bx, jb.by), pl.org.stride, pred);
+  if (valid && lane == 0) pl.out[(int64_t)t * 3 + 1] = d;
 }
 
-// One luma candidate per wavefront (12-bit, and the split-stream option).
+// One luma candidate per wavefront (12-bit).
 template <typename Px, typename Mid, int NPART>
 __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &pl, int t,
                                               uint8_t *scr, Px *pred, const uint16_t *scan) {
   const int lane = threadIdx.x & 63;
-  luma_front<Px, NPART>(a, pl, t, scr, pred);
+  const RdoJob jb = rdo_job<64>(a, pl, t);
+  luma_front<Px, NPART>(a, pl, t, jb, true, scr, pred);
   wave_sync();
   int32_t *fmid = reinterpret_cast<int32_t *>(scr);
   if (lane < 16) luma_fwd_row(fmid + lane * 65, a.bd);
   wave_sync();
-  luma_quantize(a, pl, t, fmid, scan);
+  luma_quantize(a, pl, t, jb, true, fmid, scan);
   wave_sync();
   const int range = a.bd + 8, crange = a.bd + 6 > 16 ? a.bd + 6 : 16;
   Mid *imid = reinterpret_cast<Mid *>(scr);  // [32][66]
@@ -667,25 +772,11 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
     if (lane < 32) luma_inv_row_tx(v, imid + lane * 66, range, crange);
   }
   wave_sync();
-  luma_back<Px, Mid>(a, pl, t, imid, pred);
+  luma_back<Px, Mid>(a, pl, t, jb, true, imid, pred);
 }
 
-// One launch per frame: blocks [0, luma.n_tx) are the luma candidates
-// (N = 64, cdef moments), the rest the chroma transform blocks of planes U
-// then V (N = 32, SSE).  Luma first: the long tasks start first.
-// Task i of a launch -> transform block index t (candidate-major).  With
-// k_sel >= 0 the launch covers only candidates 2r + k_sel (the replay runs
-// the zero-MV candidates, which need no motion search, concurrently with
-// the searches on a second stream).
-__device__ __forceinline__ int rdo_task(const RdoArgs &a, int i) {
-  if (a.k_sel < 0) return i;
-  const int cl = i / a.ntx_per_cand, sub = i - cl * a.ntx_per_cand;
-  const int r = cl / a.nsb, sb = cl - r * a.nsb;
-  return ((2 * r + a.k_sel) * a.nsb + sb) * a.ntx_per_cand + sub;
-}
-
-// Blocks [0, luma.n_tx) are luma candidates (one per wavefront); the rest
-// carry chroma transform blocks two per wavefront, plane U then V.
+// Chroma transform blocks, two per wavefront (one per half), plane U then
+// V: pair b of the launch.
 template <typename Px>
 __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, int32_t *buf,
                                                 Px *pred, const uint16_t *scan) {
@@ -695,8 +786,8 @@ __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, in
   int i = 2 * (b - plane * pairs) + half;
   const bool valid = i < chroma.n_tx;
   if (!valid) i -= 1;
-  rdo_cand_body<Px, 32, false, 32>(chroma, chroma.p[plane], rdo_task(chroma, i), valid,
-                                   buf + half * 32 * 33, pred + half * 32 * 32, scan);
+  rdo_cand_body<Px, 32, 32>(chroma, chroma.p[plane], i, valid, buf + half * 32 * 33,
+                            pred + half * 32 * 32, scan);
 }
 
 // The quantizer's scan (coded area <= 1024) staged in LDS for the
@@ -714,9 +805,10 @@ template <typename Px>
 using SingleLds = LumaLds<Px, typename std::conditional<sizeof(Px) == 1, int16_t, int32_t>::type, 2>;
 constexpr int kChromaPair(int pxb) { return 2 * 32 * 33 * 4 + 2 * 32 * 32 * pxb; }
 
-template <typename Px>
+template <typename Px, bool COMMIT>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void rdo_frame_kernel(
     RdoArgs luma, RdoArgs chroma) {
+  (void)COMMIT;  // separate score / commit instantiations (rocprof names)
   using L = SingleLds<Px>;
   using Mid = typename std::conditional<sizeof(Px) == 1, int16_t, int32_t>::type;
   __shared__ __align__(16) uint8_t lds[cmax(L::kSlot, kChromaPair(sizeof(Px)))];
@@ -724,7 +816,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void rd
   const int b = blockIdx.x;
   stage_scan(scan, b < luma.n_tx ? luma.q_tx_index : chroma.q_tx_index);
   if (b < luma.n_tx)
-    rdo_luma_body<Px, Mid, 2>(luma, luma.p[0], rdo_task(luma, b), lds,
+    rdo_luma_body<Px, Mid, 2>(luma, luma.p[0], b, lds,
                               reinterpret_cast<Px *>(lds + L::kScr), scan);
   else
     rdo_chroma_pair<Px>(chroma, b - luma.n_tx, reinterpret_cast<int32_t *>(lds),
@@ -744,9 +836,10 @@ struct QuadLds {
   static constexpr int kBytes = cmax(4 * L::kSlot, 3 * kChromaPair(sizeof(Px)));
 };
 
-template <typename Px>
+template <typename Px, bool COMMIT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_quad_kernel(
     RdoArgs luma, RdoArgs chroma, int nquads) {
+  (void)COMMIT;  // separate score / commit instantiations (rocprof names)
   using L = typename QuadLds<Px>::L;
   constexpr int NPART = sizeof(Px) == 1 ? 2 : 4;
   __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
@@ -772,16 +865,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
   auto pred = [&](int q) __attribute__((always_inline)) {
     return reinterpret_cast<Px *>(slot(q) + L::kScr);
   };
-  const int t0 = 4 * b;
-  const bool valid = t0 + wave < luma.n_tx;
-  if (valid) luma_front<Px, NPART>(luma, luma.p[0], rdo_task(luma, t0 + wave), slot(wave), pred(wave));
+  const int t0 = 4 * b, t = t0 + wave;
+  const bool valid = t < luma.n_tx;
+  const RdoJob jb = rdo_job<64>(luma, luma.p[0], valid ? t : luma.n_tx - 1);
+  if (valid) luma_front<Px, NPART>(luma, luma.p[0], t, jb, true, slot(wave), pred(wave));
   __syncthreads();
   if (wave == 0) {  // row DCT: lane = 16 * candidate + raster row
     const int q = lane >> 4;
     if (t0 + q < luma.n_tx) luma_fwd_row(fmid(q) + (lane & 15) * 65, luma.bd);
   }
   __syncthreads();
-  if (valid) luma_quantize(luma, luma.p[0], rdo_task(luma, t0 + wave), fmid(wave), scan);
+  if (valid) luma_quantize(luma, luma.p[0], t, jb, true, fmid(wave), scan);
   __syncthreads();
   if (wave < 2) {  // inverse rows: lane = 32 * (candidate & 1) + coded row
     const int q = 2 * wave + (lane >> 5), rr = lane & 31;
@@ -793,47 +887,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     if (vq) luma_inv_row_tx(v, imid(q) + rr * 66, range, crange);
   }
   __syncthreads();
-  if (valid) luma_back<Px, int16_t>(luma, luma.p[0], rdo_task(luma, t0 + wave), imid(wave), pred(wave));
-}
-
-// Chroma pairs alone (10.5 KiB of LDS instead of the luma slab's 20.7 KiB,
-// so about twice the resident wavefronts), for a second stream.
-template <typename Px>
-__global__ __launch_bounds__(64) void rdo_chroma_kernel(RdoArgs chroma) {
-  __shared__ int32_t buf[2 * 32 * 33];
-  __shared__ Px pred[2 * 32 * 32];
-  __shared__ uint16_t scan[1024];
-  stage_scan(scan, chroma.q_tx_index);
-  rdo_chroma_pair<Px>(chroma, blockIdx.x, buf, pred, scan);
+  if (valid) luma_back<Px, int16_t>(luma, luma.p[0], t, jb, true, imid(wave), pred(wave));
 }
 
 }  // namespace rv
 
 using namespace rv;
 
-// Replay-internal entry (rv_replay.hip): luma (N = 64, moments) and both
-// chroma planes (N = 32, SSE) of every candidate.  One launch on `s`, or,
-// with a second stream `cs`, the luma candidates on `s` and the chroma
-// pairs concurrently on `cs` (the caller orders `cs` after the MC jobs).
-int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s,
-                      hipStream_t cs) {
+// Replay-internal entry (rv_replay.hip): luma (N = 64, cdef distortion)
+// and both chroma planes (N = 32, SSE) of every task, one launch on `s`.
+int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s) {
   const unsigned cpairs = (unsigned)(2 * ((chroma.n_tx + 1) / 2));
-  if (cs) {
-    RdoArgs l = luma, c = chroma;
-    l.n_tx = luma.n_tx;
-    if (luma.n_tx) {
-      RdoArgs none = chroma;
-      none.n_tx = 0;
-      if (hbd) rdo_frame_kernel<uint16_t><<<luma.n_tx, 64, 0, s>>>(l, none);
-      else rdo_frame_kernel<uint8_t><<<luma.n_tx, 64, 0, s>>>(l, none);
-    }
-    if (cpairs) {
-      if (hbd) rdo_chroma_kernel<uint16_t><<<cpairs, 64, 0, cs>>>(c);
-      else rdo_chroma_kernel<uint8_t><<<cpairs, 64, 0, cs>>>(c);
-    }
-    RV_HIP_CHECK_LAUNCH();
-    return RV_OK;
-  }
   // RAV1E_HIP_RDO_SINGLE=1: one candidate per workgroup at every bit depth
   static const bool single = [] {
     const char *e = getenv("RAV1E_HIP_RDO_SINGLE");
@@ -842,20 +906,28 @@ int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipSt
   if (luma.bd == 12 || single) {  // 12-bit: i32 row-pass intermediate
     const unsigned grid = (unsigned)luma.n_tx + cpairs;
     if (grid == 0) return RV_OK;
-    if (hbd)
-      rdo_frame_kernel<uint16_t><<<grid, 64, 0, s>>>(luma, chroma);
+    if (hbd && luma.commit)
+      rdo_frame_kernel<uint16_t, true><<<grid, 64, 0, s>>>(luma, chroma);
+    else if (hbd)
+      rdo_frame_kernel<uint16_t, false><<<grid, 64, 0, s>>>(luma, chroma);
+    else if (luma.commit)
+      rdo_frame_kernel<uint8_t, true><<<grid, 64, 0, s>>>(luma, chroma);
     else
-      rdo_frame_kernel<uint8_t><<<grid, 64, 0, s>>>(luma, chroma);
+      rdo_frame_kernel<uint8_t, false><<<grid, 64, 0, s>>>(luma, chroma);
     RV_HIP_CHECK_LAUNCH();
     return RV_OK;
   }
   const int nquads = (luma.n_tx + 3) / 4;
   const unsigned grid = (unsigned)nquads + (cpairs + 2) / 3;
   if (grid == 0) return RV_OK;
-  if (hbd)
-    rdo_quad_kernel<uint16_t><<<grid, 256, 0, s>>>(luma, chroma, nquads);
+  if (hbd && luma.commit)
+    rdo_quad_kernel<uint16_t, true><<<grid, 256, 0, s>>>(luma, chroma, nquads);
+  else if (hbd)
+    rdo_quad_kernel<uint16_t, false><<<grid, 256, 0, s>>>(luma, chroma, nquads);
+  else if (luma.commit)
+    rdo_quad_kernel<uint8_t, true><<<grid, 256, 0, s>>>(luma, chroma, nquads);
   else
-    rdo_quad_kernel<uint8_t><<<grid, 256, 0, s>>>(luma, chroma, nquads);
+    rdo_quad_kernel<uint8_t, false><<<grid, 256, 0, s>>>(luma, chroma, nquads);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

@@ -1,32 +1,35 @@
-// rv_replay.hip -- hot-path replay driver: the per-frame call structure of
-// a speed-10 encode of one tile, for the stages this library accelerates,
-// with every frame resident in HBM.  Schedule (DESIGN.md "Replay driver"):
+// rv_replay.hip -- hot-path replay driver: the per-frame call structure of a
+// speed-10 encode of a stream, for the stages this library accelerates, with
+// every frame resident in HBM.  Per coded frame:
 //
 //   F0  hres / qres of the input (encode_frame, src/encoder.rs:3382-3385)
 //   F1  coarse ME: full_search at 1/4 res, 16x16 per 64x64 superblock and
 //       reference (estimate_motion_ss4, src/me.rs:1023-1075)
-//   F2  half-res diamond, 32x32 (estimate_motion_ss2 / me_ss2,
-//       src/me.rs:287-519)
+//   F2  half-res diamond, 32x32 (me_ss2, src/me.rs:287-519)
 //   F3  full-res full-pel diamond then sub-pel diamond, 64x64
 //       (motion_estimation, src/me.rs:193-285)
-//   F4  RDO candidates per superblock: {sub-pel MV, zero MV} x reference:
-//       put_8tap luma + chroma, diff + forward DCT (TX_64X64 luma,
-//       TX_32X32 chroma), quantize + dequantize at qindex kReplayQindex,
-//       inverse transform + add, cdef-moment luma / SSE chroma distortion,
-//       argmin (encode_tx_block src/encoder.rs:1077-1237,
-//       compute_distortion src/rdo.rs:338-411)
-//   F5  8x8 importance SATD against reference 1 (compute_block_importances,
-//       src/api/internal.rs:823-1010) and the lookahead intra cost of the
-//       same blocks (compute_lookahead_intra_costs, :680-765: SATD against
-//       pred_dc_128, rv_dist.hip)
+//   F4  RDO: every inter candidate of rdo_mode_decision (src/rdo.rs:825-1006:
+//       NEARESTMV / NEAR0MV / GLOBALMV / NEWMV per reference), skip and
+//       non-skip (luma_chroma_mode_rdo, :649-700): put_8tap, diff + fht,
+//       quantize + dequantize, estimate_rate, inverse + add,
+//       compute_distortion (rv_rdo.hip); then compute_rd_cost and the
+//       per-superblock argmin in rav1e's candidate order
+//   F6  commit: the winner of every superblock re-runs its chain and writes
+//       its levels and its reconstruction into the frame
+//   F5  8x8 importance SATD against reference 0 (compute_block_importances,
+//       src/api/internal.rs:823-1010) + lookahead intra cost (:680-765)
+//   F7  the reconstruction becomes a reference: pad (single tile group), or
+//       pack the group's region, all-gather it over RCCL, unpack every other
+//       group's region and pad (tile-parallel multi-GPU, src/encoder.rs:
+//       2772-2781, 3411-3429)
 //
-// Every stage is one batched launch over all superblocks of the tile.  The
-// glue between dependent stages is chained on the device (rv_chain.h): the
-// workgroup finishing a search writes its winner into the next stage's job
-// records, whose static fields are built once at creation.  A frame is 8
-// launches on one stream with no host round trip.  The CPU baseline
-// (oracle/orc_replay.c) runs the same schedule and must produce the same
-// result words.
+// Frames run in the coding order of rav1e's reorder pyramid (src/api/
+// internal.rs:40-95; group_input_len 4): display 4g+4, 4g+2, 4g+1, 4g+3 at
+// me_range_scale 4, 2, 1, 1 (src/encoder.rs:838), each referencing the
+// reconstructions its pyramid level sees.  Display frame 0 is the key frame:
+// intra coding is out of scope, its input is taken as its reconstruction.
+// The CPU replay (oracle/orc_replay.c) runs the same schedule and must
+// produce the same result words.
 #include <string.h>
 
 #include <vector>
@@ -34,6 +37,13 @@
 #include "rv_chain.h"
 #include "rv_device.h"
 #include "rv_rdo.h"
+
+#if __has_include(<rccl/rccl.h>)
+#include <rccl/rccl.h>
+#define RV_HAVE_RCCL 1
+#else
+#define RV_HAVE_RCCL 0
+#endif
 
 // rv_me.hip / rv_me_diamond.hip: every reference in one launch, per-job
 // evaluation counts, winners chained into the next stage's jobs
@@ -46,43 +56,56 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             int subpixel, int use_satd, int allow_hp, int bit_depth,
                             rv_fs_result *d_out, uint32_t *d_evals, const rv::ChainNext *next,
                             void *stream);
-// rv_frame.hip: hres + qres (+ padding) in one launch
+// rv_frame.hip
 int rv_plane_pyramid(const rv_plane *y, const rv_plane *h, const rv_plane *q, void *stream);
+int rv_synth_frame(const rv_plane *y, const rv_plane *u, const rv_plane *v, int t, int bit_depth,
+                   void *stream);
 
 namespace rv {
 
 constexpr int kSb = 64;
-// base_q_idx of the replay's frames: rav1e's default --quantizer (100) used
-// directly as the qindex; the rate controller that would vary it per frame
-// type is out of scope.  oracle/orc_replay.c uses the same value.
-constexpr int kReplayQindex = 100;
+constexpr int kSlots = 12;  // DPB slots, keyed by display index % 12
+constexpr int kMaxGroups = 8;
 
 struct Geo {
   int W, H, xdec, ydec, bd, hbd;
   int w_in_b, h_in_b;       // MiCols / MiRows (src/encoder.rs:580-581)
-  int tx0, ty0, tw, th;     // tile rect in superblocks
-  int mi_w, mi_h;           // tile size in 4x4 units (tile_state.rs:93)
-  int nsb, R, C, nctx;      // superblocks, references, candidates, nsb * C
+  int tx0, ty0, tw, th;     // this instance's tile group, in superblocks
+  int tws, ths;             // uniform tile size in superblocks (TilingInfo)
+  int nsb, R, M, C;         // superblocks, references, modes per ref, candidates
   int cw, ch;               // chroma block of a superblock
+  int w_imp, h_imp;         // importance grid (src/encoder.rs:624-625)
+  int vis_w, vis_h;         // the group's visible size (pixels)
 };
 
 __host__ __device__ inline int div_trunc8(int v) { return v / 8; }
 
 // get_mv_range (src/me.rs:64-80); bo in 4x4 units (frame).  Rust usize
 // arithmetic wraps and is cast back to isize, i.e. signed here.
-__host__ __device__ inline void mv_range(const Geo &g, int bx, int by, int bw,
-                                         int bh, int r[4]) {
+__host__ __device__ inline void mv_range(const Geo &g, int bx, int by, int bw, int bh, int r[4]) {
   const int border_w = 128 + bw * 8, border_h = 128 + bh * 8;
   r[0] = -bx * 32 - border_w;
   r[1] = (g.w_in_b - bx - bw / 4) * 32 + border_w;
   r[2] = -by * 32 - border_h;
   r[3] = (g.h_in_b - by - bh / 4) * 32 + border_h;
 }
+// The tile of superblock (sx, sy) of the group: its origin (superblocks)
+// and visible size in 4x4 units (TileStateMut mi_width / mi_height,
+// src/tiling/tile_state.rs:93).
+__host__ __device__ inline void sb_tile(const Geo &g, int sx, int sy, int &t0x, int &t0y,
+                                        int &mi_w, int &mi_h) {
+  const int fx = g.tx0 + sx, fy = g.ty0 + sy;
+  t0x = fx - fx % g.tws;
+  t0y = fy - fy % g.ths;
+  const int vw = g.W - t0x * kSb < g.tws * kSb ? g.W - t0x * kSb : g.tws * kSb;
+  const int vh = g.H - t0y * kSb < g.ths * kSb ? g.H - t0y * kSb : g.ths * kSb;
+  mi_w = vw >> 2;
+  mi_h = vh >> 2;
+}
 // adjust_bo (src/me.rs:993-1004) on tile-relative 4x4 offsets
-__host__ __device__ inline void adjust_bo(const Geo &g, int &bx, int &by,
-                                          int bw, int bh) {
-  int x = bx < g.mi_w - bw / 4 ? bx : g.mi_w - bw / 4;
-  int y = by < g.mi_h - bh / 4 ? by : g.mi_h - bh / 4;
+__host__ __device__ inline void adjust_bo(int mi_w, int mi_h, int &bx, int &by, int bw, int bh) {
+  int x = bx < mi_w - bw / 4 ? bx : mi_w - bw / 4;
+  int y = by < mi_h - bh / 4 ? by : mi_h - bh / 4;
   bx = x > 0 ? x : 0;
   by = y > 0 ? y : 0;
 }
@@ -103,7 +126,7 @@ __device__ inline void block_atomic_add(uint64_t s, unsigned long long *out) {
   }
 }
 
-// Verification checksum of packed coefficients (results time, not per
+// Verification checksum of the committed levels (results time, not per
 // frame): sum of q * (position in block + 1), wrapping u64.
 __global__ void coeff_checksum(const int32_t *packed, int64_t total, int per_block,
                                unsigned long long *out) {
@@ -114,51 +137,78 @@ __global__ void coeff_checksum(const int32_t *packed, int64_t total, int per_blo
   block_atomic_add(s, out);
 }
 
-// Candidate score = luma SSE (from the cdef moments) + chroma SSE, then the
-// per-superblock argmin (first minimum) and result words.  One wavefront
-// per superblock: lanes stride over the sub-blocks of a candidate.
+// compute_rd_cost + the per-superblock argmin (rdo_mode_decision): the
+// candidates in rav1e's order (reference-major: NEARESTMV, NEAR0MV,
+// GLOBALMV, NEWMV), each skip first, then non-skip unless the skip variant
+// became the best with zero distortion (luma_chroma_mode_rdo,
+// src/rdo.rs:690-700); strict `<`.  ScaledDistortion = luma + U + V
+// (dist_scale 1.0); rate = the estimate_rate bits of every transform block
+// (the rate model of RDOType::TxDistEstRate, src/encoder.rs:1226-1231; the
+// entropy coder's mode and MV bits are out of scope); rd = dist as f64 +
+// lambda * rate / 8 (src/rdo.rs:563-569).  One thread per superblock, which
+// also writes the superblock's result words.
 __global__ __launch_bounds__(64) void score_candidates(
-    Geo g, const int64_t *lmom, const uint64_t *usse, const uint64_t *vsse, int lsub, int csub,
+    Geo g, CandGeo cg, double lambda, double ds_u, double ds_v, const rv_fs_result *sub,
+    const uint64_t *lout,
+    const uint64_t *uout, const uint64_t *vout, int ntx_c, RdoWinner *win,
     const rv_fs_result *coarse, const rv_fs_result *half, const rv_fs_result *full,
-    const rv_fs_result *sub, uint64_t *words, unsigned long long *imp_sum) {
-  const int sb = blockIdx.x;
-  const int lane = threadIdx.x;
-  if (sb == 0 && lane == 0) *imp_sum = 0;  // F5 accumulates after this launch
-  uint64_t best = ~0ull;
-  int best_c = 0;
+    uint64_t *words) {
+  const int sb = blockIdx.x * 64 + threadIdx.x;
+  if (sb >= g.nsb) return;
+  double best = 1.7976931348623157e308;  // f64::MAX
+  RdoWinner w{0, 0, best, 0};
   for (int c = 0; c < g.C; c++) {
-    const int64_t o = (int64_t)c * g.nsb + sb;  // candidate-major, like the MC jobs
-    uint64_t s = 0;
-    for (int k = lane; k < lsub; k += 64) {
-      const int64_t *m = lmom + (o * lsub + k) * 5;
-      s += (uint64_t)(m[3] + m[2] - 2 * m[4]);
+    rv_mv mv;
+    if (!cand_mv(cg, sub, sb, c, &mv)) continue;
+    const int64_t o = (int64_t)c * g.nsb + sb;
+    uint64_t su = 0, sv = 0, nu = 0, nv = 0;
+    uint32_t rate = (uint32_t)lout[o * 3 + 2];
+    for (int j = 0; j < ntx_c; j++) {
+      const int64_t t = (o * ntx_c + j) * 3;
+      su += uout[t];
+      sv += vout[t];
+      nu += uout[t + 1];
+      nv += vout[t + 1];
+      rate += (uint32_t)uout[t + 2] + (uint32_t)vout[t + 2];
     }
-    for (int k = lane; k < csub; k += 64) s += usse[o * csub + k] + vsse[o * csub + k];
-    s = group_sum<64>(s);
-    if (s < best) {
-      best = s;
-      best_c = c;
+    // Distortion * dist_scale[p] -> ScaledDistortion, summed over planes
+    const uint64_t ds = (uint64_t)((double)lout[o * 3 + 0] * 1.0) + (uint64_t)((double)su * ds_u) +
+                        (uint64_t)((double)sv * ds_v);
+    const uint64_t dn = (uint64_t)((double)lout[o * 3 + 1] * 1.0) + (uint64_t)((double)nu * ds_u) +
+                        (uint64_t)((double)nv * ds_v);
+    bool zero_dist = false;
+    const double rs = (double)ds + lambda * (0.0 / 8.0);
+    if (rs < w.cost) {
+      w = RdoWinner{c, 1, rs, ds};
+      zero_dist = ds == 0;
+    }
+    if (!zero_dist) {
+      const double rn = (double)dn + lambda * ((double)rate / 8.0);
+      if (rn < w.cost) w = RdoWinner{c, 0, rn, dn};
     }
   }
-  uint64_t *w = words + (int64_t)sb * (8 * g.R + 2);
-  for (int i = lane; i < 8 * g.R; i += 64) {
+  win[sb] = w;
+  uint64_t *wd = words + (int64_t)sb * (8 * g.R + 4);
+  for (int i = 0; i < 8 * g.R; i++) {
     const int r = i >> 3, f = i & 7;
     const rv_fs_result *src = (f >> 1) == 0 ? coarse : (f >> 1) == 1 ? half : (f >> 1) == 2 ? full : sub;
     const rv_fs_result v = src[r * g.nsb + sb];
-    w[i] = (f & 1) ? v.cost : pack_mv(v.best_mv);
+    wd[i] = (f & 1) ? v.cost : pack_mv(v.best_mv);
   }
-  if (lane == 0) {
-    w[8 * g.R] = (uint64_t)best_c;
-    w[8 * g.R + 1] = best;
-  }
+  uint64_t cb;
+  __builtin_memcpy(&cb, &w.cost, 8);
+  wd[8 * g.R + 0] = (uint64_t)w.c;
+  wd[8 * g.R + 1] = (uint64_t)w.skip;
+  wd[8 * g.R + 2] = cb;
+  wd[8 * g.R + 3] = w.dist;
 }
 
-// F5: get_satd of every 8x8 luma block of the tile inside the frame against
-// reference 1 at the full-pel part of its superblock's sub-pel MV
+// F5: get_satd of every 8x8 luma block of the group inside the frame
+// against reference 0 at the full-pel part of its superblock's NEWMV
 // (compute_block_importances, src/api/internal.rs:823-1010) plus its
 // lookahead intra cost (get_satd against pred_dc_128,
-// src/api/internal.rs:680-765), summed.  One lane per block; the job is
-// computed in place, the source block read once for both.
+// src/api/internal.rs:680-765), summed.  One lane per block; the source
+// block is read once for both.
 template <typename Px>
 __global__ __launch_bounds__(256) void importance_kernel(Geo g, rv_plane org, rv_plane ref,
                                                           const rv_fs_result *sub, int nbx,
@@ -167,7 +217,7 @@ __global__ __launch_bounds__(256) void importance_kernel(Geo g, rv_plane org, rv
   uint64_t v = 0;
   if (i < nbx * nby) {
     const int bx = i % nbx, by = i / nbx;
-    const rv_mv mv = sub[(by / 8) * g.tw + (bx / 8)].best_mv;  // reference 1
+    const rv_mv mv = sub[(by / 8) * g.tw + (bx / 8)].best_mv;  // reference 0
     const int x = g.tx0 * kSb + bx * 8, y = g.ty0 * kSb + by * 8;
     const Px *o = plane_ptr<Px>(org, x, y);
     const Px *r = plane_ptr<Px>(ref, x + ((int)mv.col >> 3), y + ((int)mv.row >> 3));
@@ -187,71 +237,105 @@ __global__ __launch_bounds__(256) void importance_kernel(Geo g, rv_plane org, rv
   block_atomic_add(v, sum);
 }
 
-// Sum of the reconstructed pixels of a plane (all candidates; results time).
+// Sum of the visible pixels of a rectangle of a plane (results time).
 template <typename Px>
-__global__ void sum_plane(rv_plane p, int w, int h, unsigned long long *out) {
+__global__ void sum_rect(rv_plane p, int x0, int y0, int w, int h, unsigned long long *out) {
   uint64_t s = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)w * h;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int y = (int)(i / w), x = (int)(i - (int64_t)y * w);
-    s += *plane_ptr<Px>(p, x, y);
+    s += *plane_ptr<Px>(p, x0 + x, y0 + y);
   }
   block_atomic_add(s, out);
+}
+
+// F7 exchange: copy rectangles between planes and a packed buffer (row-major
+// per rectangle, `off` bytes into it).  blockIdx.y = rectangle.
+struct XRect {
+  int64_t off;
+  int plane, x0, y0, w, h;
+};
+struct XArgs {
+  rv_plane pl[3];
+  XRect rect[3 * kMaxGroups];
+  int n;
+  int to_plane;  // 1: buffer -> planes (unpack), 0: planes -> buffer (pack)
+  uint8_t *buf;
+};
+template <typename Px>
+__global__ __launch_bounds__(256) void xcopy_kernel(XArgs a) {
+  const XRect &r = a.rect[blockIdx.y];
+  const int64_t n = (int64_t)r.w * r.h;
+  Px *b = reinterpret_cast<Px *>(a.buf + r.off);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int y = (int)(i / r.w), x = (int)(i - (int64_t)y * r.w);
+    Px *p = plane_ptr_mut<Px>(a.pl[r.plane], r.x0 + x, r.y0 + y);
+    if (a.to_plane)
+      *p = b[i];
+    else
+      b[i] = *p;
+  }
 }
 
 }  // namespace rv
 
 using namespace rv;
 
-struct RvFrameSlot {
+struct RvSlot {  // one frame of the DPB: reconstruction + input pyramid
   rv_plane y, u, v, hres, qres;
   uint32_t *qres_box = nullptr;  // rv_plane_box_sums of qres (the SEA coarse search)
-  void *mem = nullptr;
+};
+struct RvInput {
+  rv_plane y, u, v;
 };
 
 struct rv_replay {
   rv_replay_cfg cfg;
   Geo g;
+  CandGeo cg;
   hipStream_t stream;
-  hipStream_t side;  // zero-MV RDO candidates, concurrent with the searches
   bool own_stream;
   bool sea;  // successive-elimination coarse search (bit depth <= 10)
-  double me_lambda;
-  QCtx q_luma, q_chroma;  // QuantizationContext, TX_64X64 / TX_32X32 inter
-  std::vector<RvFrameSlot> slots;  // 0 = input, 1..R = references
-  // scratch
-  rv_plane tall_y, tall_u, tall_v;
-  void *tall_mem = nullptr;
+  // per pyramid level: the frame's quantizers (QuantizationContext of
+  // TX_64X64 luma / TX_32X32 chroma, inter) and lambdas
+  struct Level {
+    bool set = false;
+    int qidx;
+    QCtx ql, qu, qv;
+    double lambda, me_lambda, ds[3];
+  } lv[3];
+  bool jobs_built = false;
+  std::vector<RvSlot> slots;
+  std::vector<RvInput> inputs;
   std::vector<void *> allocs;
-  rv_fs_job *fs_jobs[3] = {nullptr, nullptr, nullptr};  // per scale 1, 2, 4
+  rv_fs_job *fs_jobs[3] = {nullptr, nullptr, nullptr};  // per level (scale 4, 2, 1)
   rv_fs_result *coarse, *half, *full, *sub;
-  // chained search jobs (static fields built at creation, predictors
-  // written by the previous stage, rv_chain.h)
-  rv_ds_job *jobs_half, *jobs_full, *jobs_sub;
-  rv_mc_job *l_mc, *c_mc;
-  rv_tx_job *l_tx, *c_tx;
-  int32_t *l_packed, *c_packed;
-  int64_t *l_mom;
-  uint64_t *u_sse, *v_sse, *words;
-  unsigned long long *tail;  // [coeff csum, recon csum, imp satd sum]
-  int n_imp, imp_bx, imp_by, lsub, csub;
-  // Event ring: frame f records into set f % kRing (stage bounds and
-  // kernel brackets, see rv_replay_frame), so per-kernel times can be
-  // summed over a whole timed run without a host sync per frame.
+  rv_ds_job *jobs_half[3], *jobs_full[3], *jobs_sub[3];  // per level
+  uint64_t *l_out, *c_out;  // F4: [skip dist, non-skip dist, rate] per transform block
+  RdoWinner *win;
+  int32_t *l_lev, *c_lev;   // F6: committed levels
+  uint64_t *words;
+  unsigned long long *tail;  // [levels csum, group recon sum, imp satd sum, -, frame recon sum]
+  float *imp = nullptr;      // block_importances (null: all zero)
+  int n_imp, imp_bx, imp_by, ntx_c;
+  long coded = 0;            // frames coded so far (0 = the key frame next)
+  rv_replay_frame_info last{};
+  // tile-group exchange (F7)
+  int n_groups = 1, my_group = 0;
+  int32_t grects[4 * kMaxGroups];
+  size_t xbytes = 0;         // packed bytes per group (the largest group)
+  uint8_t *xsend = nullptr, *xrecv = nullptr;
+  void *comm = nullptr;      // ncclComm_t (rv_comm)
+  // Event ring: instrumented frame k records into set k % kRing, so per-
+  // kernel times can be summed over a timed run without a host sync per
+  // frame.  Every `timing_stride`-th block of frames is instrumented (each
+  // record costs ~4.4 us of idle GPU between kernels on MI355X).
   static constexpr int kRing = 64;
-  static constexpr int kEv = 11;  // + [9,10]: side-stream RDO bracket
+  static constexpr int kEv = 11;
   hipEvent_t evs[kRing][kEv];
-  hipEvent_t fork[kRing], join[kRing], fork2[kRing], join2[kRing];  // cross-stream ordering
-  hipEvent_t *ev;
-  long frames = 0;
-  // Every `timing_stride`-th frame records the timing events (each record
-  // costs ~4.4 us of idle GPU between kernels on MI355X); `timed` counts
-  // the instrumented frames, which own the event ring slots.
   int timing_stride = 1, timing_block = 1;
   long timed = 0;
-  bool ev_side[kRing];
   // diamond candidate evaluations per job, per ring slot: [kRing][2][nsb*R]
-  // (F3 full-pel, F3 sub-pel)
   uint32_t *ds_evals;
 };
 
@@ -264,208 +348,265 @@ void *dalloc(rv_replay *r, size_t bytes) {
   return p;
 }
 
-bool alloc_slot(rv_replay *r, RvFrameSlot &s) {
-  const Geo &g = r->g;
-  // Frame::new (src/frame/mod.rs:55-90): luma pad 64 + 24, chroma >> dec
+// Frame::new (src/frame/mod.rs:55-90): luma pad 64 + 24, chroma >> dec
+size_t frame_planes(const Geo &g, rv_plane &y, rv_plane &u, rv_plane &v) {
   const int pad = 88;
   const int cw = (g.W + g.xdec) >> g.xdec, ch = (g.H + g.ydec) >> g.ydec;
-  size_t by = rv_plane_geometry(&s.y, g.W, g.H, 0, 0, pad, pad, g.hbd);
-  size_t bu = rv_plane_geometry(&s.u, cw, ch, g.xdec, g.ydec, pad >> g.xdec, pad >> g.ydec, g.hbd);
-  size_t bv = rv_plane_geometry(&s.v, cw, ch, g.xdec, g.ydec, pad >> g.xdec, pad >> g.ydec, g.hbd);
+  size_t b = rv_plane_geometry(&y, g.W, g.H, 0, 0, pad, pad, g.hbd);
+  b += rv_plane_geometry(&u, cw, ch, g.xdec, g.ydec, pad >> g.xdec, pad >> g.ydec, g.hbd);
+  rv_plane_geometry(&v, cw, ch, g.xdec, g.ydec, pad >> g.xdec, pad >> g.ydec, g.hbd);
+  y.bit_depth = u.bit_depth = v.bit_depth = g.bd;
+  return b;
+}
+size_t plane_bytes(const rv_plane &p) { return (size_t)p.stride * p.alloc_height * (p.hbd ? 2 : 1); }
+
+bool alloc_input(rv_replay *r, RvInput &in) {
+  frame_planes(r->g, in.y, in.u, in.v);
+  const size_t by = plane_bytes(in.y), bu = plane_bytes(in.u);
+  uint8_t *m = (uint8_t *)dalloc(r, by + 2 * bu);
+  if (!m) return false;
+  in.y.data = m;
+  in.u.data = m + by;
+  in.v.data = m + by + bu;
+  return hipMemsetAsync(m, 0, by + 2 * bu, r->stream) == hipSuccess;
+}
+
+bool alloc_slot(rv_replay *r, RvSlot &s) {
+  const Geo &g = r->g;
+  frame_planes(g, s.y, s.u, s.v);
+  const int pad = 88;
   // input_hres / input_qres (src/encoder.rs:362-377)
-  size_t bh = rv_plane_geometry(&s.hres, g.W / 2, g.H / 2, 1, 1, pad / 2, pad / 2, g.hbd);
-  size_t bq = rv_plane_geometry(&s.qres, g.W / 4, g.H / 4, 2, 2, pad / 4, pad / 4, g.hbd);
-  s.y.bit_depth = s.u.bit_depth = s.v.bit_depth = s.hres.bit_depth = s.qres.bit_depth = g.bd;
+  rv_plane_geometry(&s.hres, g.W / 2, g.H / 2, 1, 1, pad / 2, pad / 2, g.hbd);
+  rv_plane_geometry(&s.qres, g.W / 4, g.H / 4, 2, 2, pad / 4, pad / 4, g.hbd);
+  s.hres.bit_depth = s.qres.bit_depth = g.bd;
   const size_t al = 256;
   auto up = [&](size_t v) { return (v + al - 1) / al * al; };
+  const size_t by = plane_bytes(s.y), bu = plane_bytes(s.u), bh = plane_bytes(s.hres),
+               bq = plane_bytes(s.qres);
   const size_t bs8 = (size_t)s.qres.stride * s.qres.alloc_height * 8;
-  size_t total = up(by) + up(bu) + up(bv) + up(bh) + up(bq) + up(bs8);
+  const size_t total = up(by) + 2 * up(bu) + up(bh) + up(bq) + up(bs8);
   uint8_t *m = (uint8_t *)dalloc(r, total);
   if (!m) return false;
-  s.mem = m;
   s.y.data = m;
   m += up(by);
   s.u.data = m;
   m += up(bu);
   s.v.data = m;
-  m += up(bv);
+  m += up(bu);
   s.hres.data = m;
   m += up(bh);
   s.qres.data = m;
   m += up(bq);
   s.qres_box = (uint32_t *)m;
-  return hipMemsetAsync(s.mem, 0, total, r->stream) == hipSuccess;
+  return hipMemsetAsync(s.y.data, 0, total, r->stream) == hipSuccess;
 }
 
 int build_static_jobs(rv_replay *r) {
   const Geo &g = r->g;
-  // F1 coarse jobs for me_range_scale 1, 2, 4 (estimate_motion_ss4)
-  const uint32_t lambda4 = (uint32_t)(r->me_lambda * 256.0 / 16.0 * 0.125);
-  for (int si = 0; si < 3; si++) {
-    const int s = 1 << si;
-    std::vector<rv_fs_job> jobs(g.nsb * g.R);
-    for (int sb = 0; sb < g.nsb; sb++) {
-      int bx = (sb % g.tw) * 16, by = (sb / g.tw) * 16;
-      adjust_bo(g, bx, by, 64, 64);
-      const int fbx = bx + g.tx0 * 16, fby = by + g.ty0 * 16;
-      const int pox = fbx, poy = fby;  // (bo << 2) >> 2
-      const int range_x = 192 * s, range_y = 64 * s;
-      int mr[4];
-      mv_range(g, fbx, fby, 64, 64, mr);
-      auto mx = [](int a, int b) { return a > b ? a : b; };
-      auto mn = [](int a, int b) { return a < b ? a : b; };
-      rv_fs_job j;
-      memset(&j, 0, sizeof(j));
-      j.po_x = pox;
-      j.po_y = poy;
-      j.x_lo = pox + (mx(-range_x, div_trunc8(mr[0])) >> 2);
-      j.x_hi = pox + (mn(range_x, div_trunc8(mr[1])) >> 2);
-      j.y_lo = poy + (mx(-range_y, div_trunc8(mr[2])) >> 2);
-      j.y_hi = poy + (mn(range_y, div_trunc8(mr[3])) >> 2);
-      j.lambda = lambda4;
-      for (int k = 0; k < g.R; k++) jobs[k * g.nsb + sb] = j;  // ref-major
-    }
-    r->fs_jobs[si] = (rv_fs_job *)dalloc(r, jobs.size() * sizeof(rv_fs_job));
-    if (!r->fs_jobs[si]) return RV_EHIP;
-    if (hipMemcpy(r->fs_jobs[si], jobs.data(), jobs.size() * sizeof(rv_fs_job),
-                  hipMemcpyHostToDevice) != hipSuccess)
-      return RV_EHIP;
-  }
-  // F2 / F3 diamond jobs: static fields (positions, MV ranges, lambdas);
-  // the predictors are chained in by the previous stage each frame
-  const uint32_t lambda2 = (uint32_t)(r->me_lambda * 256.0 / 4.0 * 0.125);
-  const uint32_t lambda1 = (uint32_t)(r->me_lambda * 256.0 * 0.5);
-  std::vector<rv_ds_job> jh(g.nsb * g.R), jf(g.nsb * g.R), js(g.nsb * g.R);
-  for (int k = 0; k < g.R; k++)
-    for (int sb = 0; sb < g.nsb; sb++) {
-      const int i = k * g.nsb + sb;
-      // me_ss2 (src/me.rs:470-519): adjusted 64x64 origin at 1/2 res
-      int bx = (sb % g.tw) * 16, by = (sb / g.tw) * 16;
-      adjust_bo(g, bx, by, 64, 64);
-      int fbx = bx + g.tx0 * 16, fby = by + g.ty0 * 16;
-      int mr[4];
-      mv_range(g, fbx, fby, 64, 64, mr);
-      rv_ds_job j;
-      memset(&j, 0, sizeof(j));
-      j.po_x = fbx * 2;  // (bo << BLOCK_TO_PLANE_SHIFT) >> 1
-      j.po_y = fby * 2;
-      j.mvx_min = mr[0] >> 1;
-      j.mvx_max = mr[1] >> 1;
-      j.mvy_min = mr[2] >> 1;
-      j.mvy_max = mr[3] >> 1;
-      j.lambda = lambda2;
-      j.n_pred = 1 + g.R;  // zero + the coarse MV of every reference
-      jh[i] = j;
-      // full resolution (motion_estimation, src/me.rs:193-285)
-      fbx = (sb % g.tw + g.tx0) * 16;
-      fby = (sb / g.tw + g.ty0) * 16;
-      mv_range(g, fbx, fby, 64, 64, mr);
-      memset(&j, 0, sizeof(j));
-      j.po_x = fbx * 4;
-      j.po_y = fby * 4;
-      j.mvx_min = mr[0];
-      j.mvx_max = mr[1];
-      j.mvy_min = mr[2];
-      j.mvy_max = mr[3];
-      j.lambda = lambda1;
-      j.n_pred = 2;  // zero + the half-res winner
-      jf[i] = j;
-      j.n_pred = 1;  // the full-pel winner
-      js[i] = j;
-    }
-  // F4 MC jobs of the zero-MV candidates (k = 1); the sub-pel MV ones
-  // (k = 0) are chained in by the sub-pel search
-  RvFrameSlot &cur = r->slots[0];
-  std::vector<rv_mc_job> lmc(g.nctx), cmc(g.nctx);
-  for (int c = 0; c < g.C; c++)
-    for (int sb = 0; sb < g.nsb; sb++) {
-      const int o = c * g.nsb + sb;
-      const int sx = sb % g.tw, sy = sb / g.tw;
-      const int px = (sx + g.tx0) * kSb, py = (sy + g.ty0) * kSb;
-      lmc[o] = mc_job_for(cur.y, px, py, rv_mv{0, 0}, sx * kSb, (c * g.th + sy) * kSb);
-      cmc[o] = mc_job_for(cur.u, px >> g.xdec, py >> g.ydec, rv_mv{0, 0}, sx * g.cw,
-                          (c * g.th + sy) * g.ch);
-    }
-  // F4 transform jobs (static: positions only)
-  const int ntx_c = (g.cw / 32) * (g.ch / 32);  // 32x32 chroma tx per plane
-  std::vector<rv_tx_job> ltx(g.nctx), ctx_(g.nctx * ntx_c);
-  for (int c = 0; c < g.C; c++)
-    for (int sb = 0; sb < g.nsb; sb++) {
-      const int o = c * g.nsb + sb;
-      const int sx = sb % g.tw, sy = sb / g.tw;
-      const int px = (sx + g.tx0) * kSb, py = (sy + g.ty0) * kSb;
-      const int tx = sx * kSb, ty = (c * g.th + sy) * kSb;
-      ltx[o] = rv_tx_job{px, py, tx, ty};
-      const int cpx = px >> g.xdec, cpy = py >> g.ydec;
-      const int ctx0 = sx * g.cw, cty0 = (c * g.th + sy) * g.ch;
-      for (int t = 0; t < ntx_c; t++) {
-        const int ox = (t % (g.cw / 32)) * 32, oy = (t / (g.cw / 32)) * 32;
-        ctx_[o * ntx_c + t] = rv_tx_job{cpx + ox, cpy + oy, ctx0 + ox, cty0 + oy};
-      }
-    }
+  auto mx = [](int a, int b) { return a > b ? a : b; };
+  auto mn = [](int a, int b) { return a < b ? a : b; };
   auto upload = [&](auto &vec, auto *&dst) -> int {
-    dst = (std::remove_reference_t<decltype(dst)>)dalloc(r, vec.size() * sizeof(vec[0]));
+    if (!dst) dst = (std::remove_reference_t<decltype(dst)>)dalloc(r, vec.size() * sizeof(vec[0]));
     if (!dst) return RV_EHIP;
     return hipMemcpy(dst, vec.data(), vec.size() * sizeof(vec[0]), hipMemcpyHostToDevice) ==
                    hipSuccess
                ? RV_OK
                : RV_EHIP;
   };
+  for (int lv = 0; lv < 3; lv++) {
+    const double me_lambda = r->lv[lv].me_lambda;
+    // F1 coarse jobs (estimate_motion_ss4) at this level's me_range_scale
+    const int s = 4 >> lv;
+    const uint32_t lambda4 = (uint32_t)(me_lambda * 256.0 / 16.0 * 0.125);
+    std::vector<rv_fs_job> jobs(g.nsb * g.R);
+    for (int sb = 0; sb < g.nsb; sb++) {
+      const int sx = sb % g.tw, sy = sb / g.tw;
+      int t0x, t0y, mi_w, mi_h;
+      sb_tile(g, sx, sy, t0x, t0y, mi_w, mi_h);
+      int bx = (g.tx0 + sx - t0x) * 16, by = (g.ty0 + sy - t0y) * 16;
+      adjust_bo(mi_w, mi_h, bx, by, 64, 64);
+      const int fbx = bx + t0x * 16, fby = by + t0y * 16;
+      const int range_x = 192 * s, range_y = 64 * s;
+      int mr[4];
+      mv_range(g, fbx, fby, 64, 64, mr);
+      rv_fs_job j;
+      memset(&j, 0, sizeof(j));
+      j.po_x = fbx;  // (bo << 2) >> 2
+      j.po_y = fby;
+      j.x_lo = fbx + (mx(-range_x, div_trunc8(mr[0])) >> 2);
+      j.x_hi = fbx + (mn(range_x, div_trunc8(mr[1])) >> 2);
+      j.y_lo = fby + (mx(-range_y, div_trunc8(mr[2])) >> 2);
+      j.y_hi = fby + (mn(range_y, div_trunc8(mr[3])) >> 2);
+      j.lambda = lambda4;
+      for (int k = 0; k < g.R; k++) jobs[k * g.nsb + sb] = j;  // ref-major
+    }
+    int e;
+    if ((e = upload(jobs, r->fs_jobs[lv]))) return e;
+    // F2 / F3 diamond jobs: static fields (positions, MV ranges, lambdas);
+    // the predictors are chained in by the previous stage each frame
+    const uint32_t lambda2 = (uint32_t)(me_lambda * 256.0 / 4.0 * 0.125);
+    const uint32_t lambda1 = (uint32_t)(me_lambda * 256.0 * 0.5);
+    std::vector<rv_ds_job> jh(g.nsb * g.R), jf(g.nsb * g.R), js(g.nsb * g.R);
+    for (int k = 0; k < g.R; k++)
+      for (int sb = 0; sb < g.nsb; sb++) {
+        const int i = k * g.nsb + sb;
+        const int sx = sb % g.tw, sy = sb / g.tw;
+        int t0x, t0y, mi_w, mi_h;
+        sb_tile(g, sx, sy, t0x, t0y, mi_w, mi_h);
+        // me_ss2 (src/me.rs:470-519): adjusted 64x64 origin at 1/2 res
+        int bx = (g.tx0 + sx - t0x) * 16, by = (g.ty0 + sy - t0y) * 16;
+        adjust_bo(mi_w, mi_h, bx, by, 64, 64);
+        int fbx = bx + t0x * 16, fby = by + t0y * 16;
+        int mr[4];
+        mv_range(g, fbx, fby, 64, 64, mr);
+        rv_ds_job j;
+        memset(&j, 0, sizeof(j));
+        j.po_x = fbx * 2;  // (bo << BLOCK_TO_PLANE_SHIFT) >> 1
+        j.po_y = fby * 2;
+        j.mvx_min = mr[0] >> 1;
+        j.mvx_max = mr[1] >> 1;
+        j.mvy_min = mr[2] >> 1;
+        j.mvy_max = mr[3] >> 1;
+        j.lambda = lambda2;
+        j.n_pred = 1 + g.R;  // zero + the coarse MV of every reference
+        jh[i] = j;
+        // full resolution (motion_estimation, src/me.rs:193-285)
+        fbx = (g.tx0 + sx) * 16;
+        fby = (g.ty0 + sy) * 16;
+        mv_range(g, fbx, fby, 64, 64, mr);
+        memset(&j, 0, sizeof(j));
+        j.po_x = fbx * 4;
+        j.po_y = fby * 4;
+        j.mvx_min = mr[0];
+        j.mvx_max = mr[1];
+        j.mvy_min = mr[2];
+        j.mvy_max = mr[3];
+        j.lambda = lambda1;
+        j.n_pred = 2;  // zero + the half-res winner
+        jf[i] = j;
+        j.n_pred = 1;  // the full-pel winner
+        js[i] = j;
+      }
+    if ((e = upload(jh, r->jobs_half[lv])) || (e = upload(jf, r->jobs_full[lv])) ||
+        (e = upload(js, r->jobs_sub[lv])))
+      return e;
+  }
+  r->jobs_built = true;
+  return RV_OK;
+}
+
+// Packed rectangles of group k (its visible Y, U, V region), bytes into the
+// group's slice of the exchange buffer.
+int group_rects(const rv_replay *r, int k, XRect out[3]) {
+  const Geo &g = r->g;
+  const int32_t *gr = r->grects + 4 * k;
+  const int px = g.hbd ? 2 : 1;
+  const int cw = (g.W + g.xdec) >> g.xdec, ch = (g.H + g.ydec) >> g.ydec;
+  int64_t off = 0;
+  for (int p = 0; p < 3; p++) {
+    const int xd = p ? g.xdec : 0, yd = p ? g.ydec : 0;
+    const int pw = p ? cw : g.W, ph = p ? ch : g.H;
+    const int x0 = (gr[0] * kSb) >> xd, y0 = (gr[1] * kSb) >> yd;
+    int x1 = ((gr[0] + gr[2]) * kSb) >> xd, y1 = ((gr[1] + gr[3]) * kSb) >> yd;
+    x1 = x1 < pw ? x1 : pw;
+    y1 = y1 < ph ? y1 : ph;
+    out[p] = XRect{off, p, x0, y0, x1 - x0, y1 - y0};
+    off += (int64_t)(x1 - x0) * (y1 - y0) * px;
+  }
+  return (int)off;
+}
+
+int xcopy(rv_replay *r, const RvSlot &s, const XRect *rects, int n, int to_plane, uint8_t *buf) {
+  if (n == 0) return RV_OK;
+  XArgs a;
+  memset(&a, 0, sizeof(a));
+  a.pl[0] = s.y;
+  a.pl[1] = s.u;
+  a.pl[2] = s.v;
+  int64_t most = 0;
+  for (int i = 0; i < n; i++) {
+    a.rect[i] = rects[i];
+    const int64_t px = (int64_t)rects[i].w * rects[i].h;
+    most = px > most ? px : most;
+  }
+  a.n = n;
+  a.to_plane = to_plane;
+  a.buf = buf;
+  int64_t gx = (most + 255) / 256;
+  gx = gx > 4096 ? 4096 : gx < 1 ? 1 : gx;
+  dim3 grid((unsigned)gx, (unsigned)n);
+  if (r->g.hbd)
+    xcopy_kernel<uint16_t><<<grid, 256, 0, r->stream>>>(a);
+  else
+    xcopy_kernel<uint8_t><<<grid, 256, 0, r->stream>>>(a);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+int pad_slot(rv_replay *r, const RvSlot &s) {
   int e;
-  if ((e = upload(ltx, r->l_tx)) || (e = upload(ctx_, r->c_tx)) || (e = upload(jh, r->jobs_half)) ||
-      (e = upload(jf, r->jobs_full)) || (e = upload(js, r->jobs_sub)) || (e = upload(lmc, r->l_mc)) ||
-      (e = upload(cmc, r->c_mc)))
+  if ((e = rv_plane_pad(&s.y, r->stream)) || (e = rv_plane_pad(&s.u, r->stream)) ||
+      (e = rv_plane_pad(&s.v, r->stream)))
     return e;
   return RV_OK;
 }
 
+// Coding order of the reorder pyramid: coded frame n >= 1 (n = 0 is the
+// key frame, display 0).
+void frame_info(long n, int R, rv_replay_frame_info *f) {
+  memset(f, 0, sizeof(*f));
+  if (n == 0) {
+    f->is_key = 1;
+    return;
+  }
+  const long g = (n - 1) / 4, j = (n - 1) % 4;
+  static const int kOff[4] = {4, 2, 1, 3}, kScale[4] = {4, 2, 1, 1};
+  static const int kRef[4][2] = {{0, -4}, {0, 4}, {0, 2}, {2, 4}};
+  f->display = (int)(4 * g + kOff[j]);
+  f->me_range_scale = kScale[j];
+  f->level = j == 0 ? 0 : j == 1 ? 1 : 2;
+  for (int k = 0; k < R; k++) {
+    long d = 4 * g + kRef[j][k];
+    f->ref_display[k] = (int)(d < 0 ? 0 : d);
+  }
+}
+
 }  // namespace
 
-#define RV_R(expr)                                        \
-  do {                                                    \
-    int e_ = (expr);                                      \
-    if (e_ != RV_OK) return e_;                           \
+#define RV_R(expr)                  \
+  do {                              \
+    int e_ = (expr);                \
+    if (e_ != RV_OK) return e_;     \
   } while (0)
-#define RV_H(expr)                                                   \
-  do {                                                               \
-    hipError_t e_ = (expr);                                          \
-    if (e_ != hipSuccess) return rv_set_hip_error(e_, #expr);        \
+#define RV_H(expr)                                            \
+  do {                                                        \
+    hipError_t e_ = (expr);                                   \
+    if (e_ != hipSuccess) return rv_set_hip_error(e_, #expr); \
   } while (0)
 
 extern "C" {
 
 void rv_replay_destroy(rv_replay *r) {
   if (!r) return;
+  if (r->stream) (void)hipStreamSynchronize(r->stream);
   for (void *p : r->allocs) (void)hipFree(p);
-  for (int f = 0; f < rv_replay::kRing; f++) {
+  for (int f = 0; f < rv_replay::kRing; f++)
     for (int i = 0; i < rv_replay::kEv; i++)
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
-    if (r->fork[f]) (void)hipEventDestroy(r->fork[f]);
-    if (r->join[f]) (void)hipEventDestroy(r->join[f]);
-    if (r->fork2[f]) (void)hipEventDestroy(r->fork2[f]);
-    if (r->join2[f]) (void)hipEventDestroy(r->join2[f]);
-  }
-  if (r->side) (void)hipStreamDestroy(r->side);
   if (r->own_stream && r->stream) (void)hipStreamDestroy(r->stream);
   delete r;
 }
 
 rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
-  if (!cfg || cfg->width <= 0 || cfg->height <= 0 || (cfg->width & 7) ||
-      (cfg->height & 7) || (cfg->bit_depth != 8 && cfg->bit_depth != 10 && cfg->bit_depth != 12) ||
-      cfg->xdec < 0 || cfg->xdec > 1 || cfg->ydec < 0 || cfg->ydec > 1 ||
-      cfg->n_refs < 1 || cfg->n_refs > RV_DS_MAX_PRED - 1) {
+  if (!cfg || cfg->width <= 0 || cfg->height <= 0 || (cfg->width & 7) || (cfg->height & 7) ||
+      (cfg->bit_depth != 8 && cfg->bit_depth != 10 && cfg->bit_depth != 12) || cfg->xdec < 0 ||
+      cfg->xdec > 1 || cfg->ydec < 0 || cfg->ydec > 1 || cfg->n_refs < 1 || cfg->n_refs > 2 ||
+      cfg->n_inputs < 1 || cfg->tile_w_sb < 0 || cfg->tile_h_sb < 0) {
     rv_set_error(RV_EINVAL, "rv_replay_create: bad config");
     return nullptr;
   }
   rv_replay *r = new rv_replay();
   memset(r->evs, 0, sizeof(r->evs));
-  memset(r->fork, 0, sizeof(r->fork));
-  memset(r->join, 0, sizeof(r->join));
-  memset(r->fork2, 0, sizeof(r->fork2));
-  memset(r->join2, 0, sizeof(r->join2));
-  r->side = nullptr;
-  r->ev = r->evs[0];
   r->cfg = *cfg;
   Geo &g = r->g;
   g.W = cfg->width;
@@ -481,33 +622,28 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   g.ty0 = cfg->tile_y0;
   g.tw = cfg->tile_w > 0 ? cfg->tile_w : sbc - g.tx0;
   g.th = cfg->tile_h > 0 ? cfg->tile_h : sbr - g.ty0;
+  g.tws = cfg->tile_w_sb > 0 ? cfg->tile_w_sb : sbc;
+  g.ths = cfg->tile_h_sb > 0 ? cfg->tile_h_sb : sbr;
+  // the group is a rectangle of whole tiles
   if (g.tx0 < 0 || g.ty0 < 0 || g.tw <= 0 || g.th <= 0 || g.tx0 + g.tw > sbc ||
-      g.ty0 + g.th > sbr) {
-    rv_set_error(RV_EINVAL, "rv_replay_create: bad tile");
+      g.ty0 + g.th > sbr || g.tx0 % g.tws || g.ty0 % g.ths ||
+      ((g.tx0 + g.tw) % g.tws && g.tx0 + g.tw != sbc) ||
+      ((g.ty0 + g.th) % g.ths && g.ty0 + g.th != sbr)) {
+    rv_set_error(RV_EINVAL, "rv_replay_create: the tile group is not a rectangle of whole tiles");
     delete r;
     return nullptr;
   }
-  const int vis_w = (g.W - g.tx0 * kSb) < g.tw * kSb ? g.W - g.tx0 * kSb : g.tw * kSb;
-  const int vis_h = (g.H - g.ty0 * kSb) < g.th * kSb ? g.H - g.ty0 * kSb : g.th * kSb;
-  g.mi_w = vis_w >> 2;
-  g.mi_h = vis_h >> 2;
+  g.vis_w = (g.W - g.tx0 * kSb) < g.tw * kSb ? g.W - g.tx0 * kSb : g.tw * kSb;
+  g.vis_h = (g.H - g.ty0 * kSb) < g.th * kSb ? g.H - g.ty0 * kSb : g.th * kSb;
   g.nsb = g.tw * g.th;
   g.R = cfg->n_refs;
-  g.C = 2 * g.R;
-  g.nctx = g.nsb * g.C;
+  g.M = kCandModes;
+  g.C = g.R * g.M;
   g.cw = kSb >> g.xdec;
   g.ch = kSb >> g.ydec;
-  // me_lambda = sqrt(lambda), lambda scaled by 1 << 2 (bd - 8)
-  // (src/encoder.rs:876-878); the replay fixes the 8-bit value.
-  r->me_lambda = 24.0 * (double)(1 << (g.bd - 8));
-  // quantizer of every RDO candidate: base_q_idx kReplayQindex with no
-  // per-plane deltas, inter (QuantizationContext::update calls of
-  // write_tx_tree, src/encoder.rs:1925-1931, 1987-1994)
-  if (rv_quant_ctx(kReplayQindex, 64 * 64, 0, g.bd, 0, 0, &r->q_luma) != RV_OK ||
-      rv_quant_ctx(kReplayQindex, 32 * 32, 0, g.bd, 0, 0, &r->q_chroma) != RV_OK) {
-    delete r;
-    return nullptr;
-  }
+  g.w_imp = g.w_in_b / 2;
+  g.h_imp = g.h_in_b / 2;
+  r->cg = CandGeo{g.nsb, g.tw, g.th, g.tx0, g.ty0, g.tws, g.ths, g.R, g.M};
   // 8x8 sums of 10-bit pixels fit the u16 box-sum table; 12-bit searches
   // exhaustively
   r->sea = g.bd <= 10 && (cfg->flags & RV_REPLAY_EXHAUSTIVE_FS) == 0;
@@ -523,52 +659,48 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
     }
   }
   bool ok = true;
-  r->slots.resize(g.R + 1);
+  r->slots.resize(kSlots);
   for (auto &s : r->slots) ok = ok && alloc_slot(r, s);
-  // tall scratch planes: candidate c of superblock (sx, sy) at
-  // (sx * bw, (c * th + sy) * bh)
-  size_t by = rv_plane_geometry(&r->tall_y, g.tw * kSb, g.C * g.th * kSb, 0, 0, 0, 0, g.hbd);
-  size_t bu = rv_plane_geometry(&r->tall_u, g.tw * g.cw, g.C * g.th * g.ch, g.xdec, g.ydec, 0, 0,
-                                g.hbd);
-  r->tall_v = r->tall_u;
-  r->tall_y.data = dalloc(r, by);
-  r->tall_u.data = dalloc(r, bu);
-  r->tall_v.data = dalloc(r, bu);
-  const int ntx_c = (g.cw / 32) * (g.ch / 32);
+  r->inputs.resize(cfg->n_inputs);
+  for (auto &in : r->inputs) ok = ok && alloc_input(r, in);
+  r->ntx_c = (g.cw / 32) * (g.ch / 32);
   const int nr = g.nsb * g.R;
+  const int64_t nc = (int64_t)g.nsb * g.C;
   r->coarse = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
   r->half = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
   r->full = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
   r->sub = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
-  r->l_packed = (int32_t *)dalloc(r, (size_t)g.nctx * 1024 * 4);
-  r->c_packed = (int32_t *)dalloc(r, (size_t)g.nctx * ntx_c * 1024 * 4 * 2);
-  r->lsub = (kSb / 8) * (kSb / 8);
-  {
-    const int bw = (g.cw < 8 ? g.cw : 8) >> g.xdec, bh = (g.ch < 8 ? g.ch : 8) >> g.ydec;
-    r->csub = (g.cw / bw) * (g.ch / bh);
-  }
-  r->l_mom = (int64_t *)dalloc(r, (size_t)g.nctx * r->lsub * 5 * 8);
-  r->u_sse = (uint64_t *)dalloc(r, (size_t)g.nctx * r->csub * 8);
-  r->v_sse = (uint64_t *)dalloc(r, (size_t)g.nctx * r->csub * 8);
-  r->words = (uint64_t *)dalloc(r, (size_t)g.nsb * (8 * g.R + 2) * 8);
-  r->imp_bx = vis_w / 8;
-  r->imp_by = vis_h / 8;
+  r->l_out = (uint64_t *)dalloc(r, (size_t)nc * 3 * 8);
+  r->c_out = (uint64_t *)dalloc(r, (size_t)nc * r->ntx_c * 3 * 8 * 2);
+  r->win = (RdoWinner *)dalloc(r, (size_t)g.nsb * sizeof(RdoWinner));
+  r->l_lev = (int32_t *)dalloc(r, (size_t)g.nsb * 1024 * 4);
+  r->c_lev = (int32_t *)dalloc(r, (size_t)g.nsb * r->ntx_c * 1024 * 4 * 2);
+  r->words = (uint64_t *)dalloc(r, (size_t)g.nsb * (8 * g.R + 4) * 8);
+  r->imp_bx = g.vis_w / 8;
+  r->imp_by = g.vis_h / 8;
   r->n_imp = r->imp_bx * r->imp_by;
-  r->tail = (unsigned long long *)dalloc(r, 4 * 8);
-  for (int f = 0; f < rv_replay::kRing; f++) {
+  r->tail = (unsigned long long *)dalloc(r, 5 * 8);
+  ok = ok && r->coarse && r->half && r->full && r->sub && r->l_out && r->c_out && r->win &&
+       r->l_lev && r->c_lev && r->words && r->tail;
+  if (ok) {
+    ok = hipMemsetAsync(r->words, 0, (size_t)g.nsb * (8 * g.R + 4) * 8, r->stream) == hipSuccess &&
+         hipMemsetAsync(r->tail, 0, 5 * 8, r->stream) == hipSuccess &&
+         hipMemsetAsync(r->l_lev, 0, (size_t)g.nsb * 1024 * 4, r->stream) == hipSuccess &&
+         hipMemsetAsync(r->c_lev, 0, (size_t)g.nsb * r->ntx_c * 1024 * 4 * 2, r->stream) ==
+             hipSuccess;
+  }
+  for (int f = 0; f < rv_replay::kRing; f++)
     for (int i = 0; i < rv_replay::kEv; i++)
       ok = ok && hipEventCreateWithFlags(&r->evs[f][i], hipEventDisableSystemFence) == hipSuccess;
-    ok = ok && hipEventCreateWithFlags(&r->fork[f], hipEventDisableTiming) == hipSuccess;
-    ok = ok && hipEventCreateWithFlags(&r->join[f], hipEventDisableTiming) == hipSuccess;
-    ok = ok && hipEventCreateWithFlags(&r->fork2[f], hipEventDisableTiming) == hipSuccess;
-    ok = ok && hipEventCreateWithFlags(&r->join2[f], hipEventDisableTiming) == hipSuccess;
-  }
-  ok = ok && hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking) == hipSuccess;
   const size_t ev_bytes = (size_t)rv_replay::kRing * 2 * nr * 4;
   r->ds_evals = (uint32_t *)dalloc(r, ev_bytes);
   ok = ok && r->ds_evals && hipMemsetAsync(r->ds_evals, 0, ev_bytes, r->stream) == hipSuccess;
-  ok = ok && r->tall_y.data && r->tall_u.data && r->tall_v.data && r->tail;
-  if (!ok || build_static_jobs(r) != RV_OK) {
+  r->grects[0] = g.tx0;
+  r->grects[1] = g.ty0;
+  r->grects[2] = g.tw;
+  r->grects[3] = g.th;
+  for (int lv = 0; lv < 3; lv++) r->jobs_half[lv] = r->jobs_full[lv] = r->jobs_sub[lv] = nullptr;
+  if (!ok) {
     rv_set_error(RV_EHIP, "rv_replay_create: device allocation failed");
     rv_replay_destroy(r);
     return nullptr;
@@ -580,206 +712,340 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   return r;
 }
 
-static int upload_plane(rv_replay *r, const rv_plane &p, const uint8_t *src) {
-  const int px = p.hbd ? 2 : 1;
-  uint8_t *dst = (uint8_t *)p.data + ((size_t)p.yorigin * p.stride + p.xorigin) * px;
-  RV_H(hipMemcpy2DAsync(dst, (size_t)p.stride * px, src, (size_t)p.width * px,
-                        (size_t)p.width * px, p.height, hipMemcpyHostToDevice, r->stream));
-  return rv_plane_pad(&p, r->stream);
+// The quantizers and lambdas of the frames of pyramid level `level`
+// (FrameInvariants::set_quantizers, src/encoder.rs:865-880, from
+// QuantizerParameters; the host computes them, rav1e_amd/rate.py).  Every
+// level must be set before the first inter frame.
+int rv_replay_set_level_params(rv_replay *r, int level, const rv_replay_level_params *p) {
+  if (!r || !p || level < 0 || level > 2 || p->base_q_idx < 1 || p->base_q_idx > 255)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_level_params: bad arguments");
+  rv_replay::Level &L = r->lv[level];
+  const int bd = r->g.bd;
+  // QuantizationContext::update of write_tx_tree's inter blocks
+  // (src/encoder.rs:1925-1931, 1987-1994): per plane dc / ac deltas
+  RV_R(rv_quant_ctx(p->base_q_idx, 64 * 64, 0, bd, p->dc_delta_q[0], p->ac_delta_q[0], &L.ql));
+  RV_R(rv_quant_ctx(p->base_q_idx, 32 * 32, 0, bd, p->dc_delta_q[1], p->ac_delta_q[1], &L.qu));
+  RV_R(rv_quant_ctx(p->base_q_idx, 32 * 32, 0, bd, p->dc_delta_q[2], p->ac_delta_q[2], &L.qv));
+  L.qidx = p->base_q_idx;
+  L.lambda = p->lambda;
+  L.me_lambda = p->me_lambda;
+  for (int i = 0; i < 3; i++) L.ds[i] = p->dist_scale[i];
+  L.set = true;
+  r->jobs_built = false;
+  return RV_OK;
 }
 
-int rv_replay_set_frame(rv_replay *r, int slot, const void *host_yuv) {
-  if (!r || !host_yuv || slot < 0 || slot > r->g.R)
-    return rv_set_error(RV_EINVAL, "rv_replay_set_frame: bad slot");
-  RvFrameSlot &s = r->slots[slot];
-  const int px = r->g.hbd ? 2 : 1;
-  const uint8_t *p = (const uint8_t *)host_yuv;
-  RV_R(upload_plane(r, s.y, p));
-  p += (size_t)s.y.width * s.y.height * px;
-  RV_R(upload_plane(r, s.u, p));
-  p += (size_t)s.u.width * s.u.height * px;
-  RV_R(upload_plane(r, s.v, p));
-  RV_R(rv_plane_pyramid(&s.y, &s.hres, &s.qres, r->stream));
-  if (r->sea) RV_R(rv_plane_box_sums(&s.qres, s.qres_box, r->stream));
+int rv_replay_synth_inputs(rv_replay *r, int t0) {
+  if (!r) return rv_set_error(RV_EINVAL, "rv_replay_synth_inputs: null");
+  for (size_t i = 0; i < r->inputs.size(); i++) {
+    const RvInput &in = r->inputs[i];
+    RV_R(rv_synth_frame(&in.y, &in.u, &in.v, t0 + (int)i, r->g.bd, r->stream));
+  }
   RV_H(hipStreamSynchronize(r->stream));
   return RV_OK;
 }
 
-// Event layout per frame (ring slot): e[0..6] = stage bounds F0..F5 end;
-// e[7] splits F3 between the full-pel and the sub-pel diamond launch, e[8]
-// splits F4 between the fused candidate launch and the scoring launch.
-// Every stage is one launch except those two, so the stage bounds are also
-// the kernel brackets.  The events are created without the system-scope
-// fence (they only time).
-int rv_replay_frame(rv_replay *r, int me_range_scale) {
-  if (!r || (me_range_scale != 1 && me_range_scale != 2 && me_range_scale != 4))
-    return rv_set_error(RV_EINVAL, "rv_replay_frame: bad me_range_scale");
+static int copy_plane(rv_replay *r, const rv_plane &p, uint8_t *host, bool to_device) {
+  const int px = p.hbd ? 2 : 1;
+  uint8_t *dev = (uint8_t *)p.data + ((size_t)p.yorigin * p.stride + p.xorigin) * px;
+  if (to_device) {
+    RV_H(hipMemcpy2DAsync(dev, (size_t)p.stride * px, host, (size_t)p.width * px,
+                          (size_t)p.width * px, p.height, hipMemcpyHostToDevice, r->stream));
+    return rv_plane_pad(&p, r->stream);
+  }
+  RV_H(hipMemcpy2DAsync(host, (size_t)p.width * px, dev, (size_t)p.stride * px,
+                        (size_t)p.width * px, p.height, hipMemcpyDeviceToHost, r->stream));
+  return RV_OK;
+}
+
+static int copy_frame(rv_replay *r, const rv_plane *pl, void *host, bool to_device) {
+  const int px = r->g.hbd ? 2 : 1;
+  uint8_t *p = (uint8_t *)host;
+  for (int k = 0; k < 3; k++) {
+    RV_R(copy_plane(r, pl[k], p, to_device));
+    p += (size_t)pl[k].width * pl[k].height * px;
+  }
+  RV_H(hipStreamSynchronize(r->stream));
+  return RV_OK;
+}
+
+int rv_replay_set_input(rv_replay *r, int idx, const void *host_yuv) {
+  if (!r || !host_yuv || idx < 0 || idx >= (int)r->inputs.size())
+    return rv_set_error(RV_EINVAL, "rv_replay_set_input: bad index");
+  const RvInput &in = r->inputs[idx];
+  const rv_plane pl[3] = {in.y, in.u, in.v};
+  return copy_frame(r, pl, const_cast<void *>(host_yuv), true);
+}
+
+int rv_replay_get_input(rv_replay *r, int idx, void *host_yuv) {
+  if (!r || !host_yuv || idx < 0 || idx >= (int)r->inputs.size())
+    return rv_set_error(RV_EINVAL, "rv_replay_get_input: bad index");
+  const RvInput &in = r->inputs[idx];
+  const rv_plane pl[3] = {in.y, in.u, in.v};
+  return copy_frame(r, pl, host_yuv, false);
+}
+
+// The reconstruction of display frame `display` (it must still be in the
+// DPB: the last 12 displays).
+int rv_replay_get_recon(rv_replay *r, int display, void *host_yuv) {
+  if (!r || !host_yuv || display < 0) return rv_set_error(RV_EINVAL, "rv_replay_get_recon");
+  const RvSlot &s = r->slots[display % kSlots];
+  const rv_plane pl[3] = {s.y, s.u, s.v};
+  return copy_frame(r, pl, host_yuv, false);
+}
+
+int rv_replay_set_importances(rv_replay *r, const float *host, int n) {
+  if (!r) return rv_set_error(RV_EINVAL, "rv_replay_set_importances: null");
+  const int need = r->g.w_imp * r->g.h_imp;
+  if (!host) {
+    r->imp = nullptr;
+    return RV_OK;
+  }
+  if (n != need) return rv_set_error(RV_EINVAL, "rv_replay_set_importances: size != w_imp * h_imp");
+  float *d = (float *)dalloc(r, (size_t)need * 4);
+  if (!d) return rv_set_error(RV_EHIP, "rv_replay_set_importances: alloc");
+  RV_H(hipMemcpy(d, host, (size_t)need * 4, hipMemcpyHostToDevice));
+  r->imp = d;
+  return RV_OK;
+}
+
+// Tile groups of all ranks (rects in superblocks, 4 per group), this
+// instance's index among them, and the RCCL communicator (rv_comm_create)
+// that all-gathers the reconstructions; comm may be null: then the caller
+// moves the packed regions itself (rv_replay_exchange_buffers,
+// rv_replay_import).
+int rv_replay_set_groups(rv_replay *r, int n_groups, const int32_t *rects, int my_group,
+                         void *comm) {
+  if (!r || n_groups < 1 || n_groups > kMaxGroups || !rects || my_group < 0 ||
+      my_group >= n_groups)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_groups: bad groups");
+  const Geo &g = r->g;
+  if (rects[4 * my_group] != g.tx0 || rects[4 * my_group + 1] != g.ty0 ||
+      rects[4 * my_group + 2] != g.tw || rects[4 * my_group + 3] != g.th)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_groups: my group != the configured tile group");
+  memcpy(r->grects, rects, (size_t)n_groups * 4 * sizeof(int32_t));
+  r->n_groups = n_groups;
+  r->my_group = my_group;
+  size_t most = 0;
+  for (int k = 0; k < n_groups; k++) {
+    XRect xr[3];
+    const size_t b = (size_t)group_rects(r, k, xr);
+    most = b > most ? b : most;
+  }
+  r->xbytes = (most + 255) / 256 * 256;
+  if (n_groups > 1) {
+    r->xsend = (uint8_t *)dalloc(r, r->xbytes);
+    r->xrecv = (uint8_t *)dalloc(r, r->xbytes * n_groups);
+    if (!r->xsend || !r->xrecv) return rv_set_error(RV_EHIP, "rv_replay_set_groups: alloc");
+  }
+  r->comm = comm;
+  return RV_OK;
+}
+
+int rv_replay_exchange_buffers(rv_replay *r, void **send, void **recv, size_t *bytes_per_group) {
+  if (!r || !send || !recv || !bytes_per_group)
+    return rv_set_error(RV_EINVAL, "rv_replay_exchange_buffers: null");
+  *send = r->xsend;
+  *recv = r->xrecv;
+  *bytes_per_group = r->xbytes;
+  return RV_OK;
+}
+
+// Unpack every other group's region of the last coded frame from the
+// gathered buffer (group k at k * bytes_per_group) and pad: the frame is
+// then a complete reference on this rank (src/encoder.rs:3411-3429).
+int rv_replay_import(rv_replay *r) {
+  if (!r) return rv_set_error(RV_EINVAL, "rv_replay_import: null");
+  if (r->n_groups < 2) return RV_OK;
+  const RvSlot &s = r->slots[r->last.display % kSlots];
+  XRect rects[3 * kMaxGroups];
+  int n = 0;
+  for (int k = 0; k < r->n_groups; k++) {
+    if (k == r->my_group) continue;
+    XRect xr[3];
+    group_rects(r, k, xr);
+    for (int p = 0; p < 3; p++) {
+      xr[p].off += (int64_t)k * (int64_t)r->xbytes;
+      rects[n++] = xr[p];
+    }
+  }
+  RV_R(xcopy(r, s, rects, n, 1, r->xrecv));
+  return pad_slot(r, s);
+}
+
+// Event layout per instrumented frame: e[0] start, e[1..10] after F0, F1,
+// F2, F3 full-pel, F3 sub-pel, F4 score, F4 argmin, F6 commit, F5, F7.
+int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
+  if (!r) return rv_set_error(RV_EINVAL, "rv_replay_frame: null");
   const Geo &g = r->g;
   hipStream_t st = r->stream;
-  RvFrameSlot &cur = r->slots[0];
-  const int nr = g.nsb;  // jobs per reference
-  const int si = me_range_scale == 1 ? 0 : me_range_scale == 2 ? 1 : 2;
-  rv_plane refs_y[RV_DS_MAX_PRED], refs_h[RV_DS_MAX_PRED], refs_q[RV_DS_MAX_PRED];
-  for (int k = 0; k < g.R; k++) {
-    refs_y[k] = r->slots[1 + k].y;
-    refs_h[k] = r->slots[1 + k].hres;
-    refs_q[k] = r->slots[1 + k].qres;
+  rv_replay_frame_info fi;
+  frame_info(r->coded, g.R, &fi);
+  if (fi.is_key) {
+    // the key frame: its input is its reconstruction (intra coding is out
+    // of scope); the pyramid of its input for the searches that reference it
+    const RvInput &in = r->inputs[0];
+    const RvSlot &s = r->slots[0];
+    RV_H(hipMemcpyAsync(s.y.data, in.y.data, plane_bytes(in.y), hipMemcpyDeviceToDevice, st));
+    RV_H(hipMemcpyAsync(s.u.data, in.u.data, plane_bytes(in.u), hipMemcpyDeviceToDevice, st));
+    RV_H(hipMemcpyAsync(s.v.data, in.v.data, plane_bytes(in.v), hipMemcpyDeviceToDevice, st));
+    RV_R(rv_plane_pyramid(&in.y, &s.hres, &s.qres, st));
+    if (r->sea) RV_R(rv_plane_box_sums(&s.qres, s.qres_box, st));
+    r->coded++;
+    r->last = fi;
+    if (info) *info = fi;
+    RV_H(hipGetLastError());
+    return RV_OK;
   }
-  const int slot = (int)(r->frames % rv_replay::kRing);
+  if (!r->lv[0].set || !r->lv[1].set || !r->lv[2].set)
+    return rv_set_error(RV_EINVAL, "rv_replay_frame: level params not set");
+  if (!r->jobs_built) RV_R(build_static_jobs(r));
+  const rv_replay::Level &L = r->lv[fi.level];
+  const int lv = fi.level;
+  const RvInput &cur = r->inputs[fi.display % r->inputs.size()];
+  const RvSlot &S = r->slots[fi.display % kSlots];
+  const RvSlot *ref[2];
+  rv_plane refs_y[RV_DS_MAX_PRED], refs_h[RV_DS_MAX_PRED], refs_q[RV_DS_MAX_PRED];
+  const uint32_t *box[RV_DS_MAX_PRED];
+  for (int k = 0; k < g.R; k++) {
+    ref[k] = &r->slots[fi.ref_display[k] % kSlots];
+    refs_y[k] = ref[k]->y;
+    refs_h[k] = ref[k]->hres;
+    refs_q[k] = ref[k]->qres;
+    box[k] = ref[k]->qres_box;
+  }
+  const int nr = g.nsb;  // jobs per reference
+  const long ncoded = r->coded - 1;  // non-key frames before this one
+  const int slot = (int)(ncoded % rv_replay::kRing);
   uint32_t *ev_full = r->ds_evals + (size_t)slot * 2 * nr * g.R;
   uint32_t *ev_sub = ev_full + (size_t)nr * g.R;
-  ChainNext to_half{}, to_full{}, to_sub{}, to_mc{};
-  to_half.mode = kChainCoarseToHalf;
-  to_half.jobs = r->jobs_half;
-  to_full.mode = kChainHalfToFull;
-  to_full.jobs = r->jobs_full;
-  to_sub.mode = kChainFullToSub;
-  to_sub.jobs = r->jobs_sub;
-  to_mc.mode = kChainSubToMc;
-  to_mc.l_mc = r->l_mc;
-  to_mc.c_mc = r->c_mc;
-  to_mc.luma = cur.y;
-  to_mc.chroma = cur.u;
-  to_mc.tw = g.tw;
-  to_mc.th = g.th;
-  to_mc.tx0 = g.tx0;
-  to_mc.ty0 = g.ty0;
-  to_mc.cw = g.cw;
-  to_mc.ch = g.ch;
+  ChainNext to_half{kChainCoarseToHalf, r->jobs_half[lv]},
+      to_full{kChainHalfToFull, r->jobs_full[lv]}, to_sub{kChainFullToSub, r->jobs_sub[lv]};
 
-  const bool tm = r->timing_stride > 0 && (r->frames / r->timing_block) % r->timing_stride == 0;
-  const int tslot = (int)(r->timed % rv_replay::kRing);
-  hipEvent_t *e = r->evs[tslot];
-  r->ev = e;
-  r->frames++;
+  const bool tm = r->timing_stride > 0 && (ncoded / r->timing_block) % r->timing_stride == 0;
+  hipEvent_t *e = r->evs[r->timed % rv_replay::kRing];
   if (tm) r->timed++;
-#define RV_EV(i, stream)                                 \
-  do {                                                   \
-    if (tm) RV_H(hipEventRecord(e[i], (stream)));        \
+#define RV_EV(i)                                   \
+  do {                                             \
+    if (tm) RV_H(hipEventRecord(e[i], st));        \
   } while (0)
-  RV_EV(0, st);
-  // F4 zero-MV candidates need no motion search: they run on the side
-  // stream concurrently with F0-F3 (rav1e evaluates them in the same RDO
-  // loop, src/rdo.rs:949-1006; only the order of independent work changes)
-  const int ntx_c = (g.cw / 32) * (g.ch / 32);
-  const int nct = g.nctx * ntx_c;
-  RdoArgs la, ca;
-  {
-    memset(&la, 0, sizeof(la));
-    la.p[0].org = cur.y;
-    for (int k = 0; k < g.R; k++) la.p[0].ref[k] = r->slots[1 + k].y;
-    la.p[0].dst = r->tall_y;
-    la.p[0].mc = r->l_mc;
-    la.p[0].tx = r->l_tx;
-    la.p[0].packed = r->l_packed;
-    la.p[0].dist = r->l_mom;
-    la.n_tx = g.nctx / 2;  // one candidate kind per launch
-    la.ntx_per_cand = 1;
-    la.cands_per_ref = 2 * nr;
-    la.nsb = nr;
-    la.bd = g.bd;
-    la.mb_w = la.mb_h = kSb;
-    la.sub_w = la.sub_h = 8;
-    la.q = r->q_luma;
-    la.q_tx_index = 4 * 16 + 0;  // TX_64X64, DCT_DCT
-    ca = la;
-    ca.q = r->q_chroma;
-    ca.q_tx_index = 3 * 16 + 0;  // TX_32X32, DCT_DCT
-    const rv_plane *cp[2] = {&cur.u, &cur.v};
-    const rv_plane *tp[2] = {&r->tall_u, &r->tall_v};
-    uint64_t *cs[2] = {r->u_sse, r->v_sse};
-    for (int p = 0; p < 2; p++) {
-      ca.p[p].org = *cp[p];
-      for (int k = 0; k < g.R; k++) ca.p[p].ref[k] = p ? r->slots[1 + k].v : r->slots[1 + k].u;
-      ca.p[p].dst = *tp[p];
-      ca.p[p].mc = r->c_mc;
-      ca.p[p].tx = r->c_tx;
-      ca.p[p].packed = r->c_packed + (size_t)p * nct * 1024;
-      ca.p[p].dist = cs[p];
-    }
-    ca.n_tx = nct / 2;
-    ca.ntx_per_cand = ntx_c;
-    ca.mb_w = g.cw;
-    ca.mb_h = g.ch;
-    ca.sub_w = (g.cw < 8 ? g.cw : 8) >> g.xdec;
-    ca.sub_h = (g.ch < 8 ? g.ch : 8) >> g.ydec;
-  }
-  const bool serial = (r->cfg.flags & RV_REPLAY_SIDE_RDO) == 0;
-  if (!serial) {
-    RV_H(hipEventRecord(r->fork[slot], st));
-    RV_H(hipStreamWaitEvent(r->side, r->fork[slot], 0));
-    la.k_sel = ca.k_sel = 1;
-    RV_EV(9, r->side);
-    RV_R(rv_rdo_candidates(la, ca, g.hbd, r->side));
-    RV_EV(10, r->side);
-    RV_H(hipEventRecord(r->join[slot], r->side));
-  }
+  RV_EV(0);
   // F0 hres + qres of the input (encode_frame, src/encoder.rs:3382-3385)
-  RV_R(rv_plane_pyramid(&cur.y, &cur.hres, &cur.qres, st));
-  // box sums of the input's qres: the table this frame's coarse search
-  // needs once it is a reference (one per frame in a real encode; the
-  // replay's references are fixed, so it is computed and not consumed)
-  if (r->sea) RV_R(rv_plane_box_sums(&cur.qres, cur.qres_box, st));
-  RV_EV(1, st);
+  // into this frame's DPB slot, and the box sums its later searches need
+  RV_R(rv_plane_pyramid(&cur.y, &S.hres, &S.qres, st));
+  if (r->sea) RV_R(rv_plane_box_sums(&S.qres, S.qres_box, st));
+  RV_EV(1);
   // F1 coarse full search, every reference in one launch -> F2 predictors
-  const uint32_t *box[RV_DS_MAX_PRED];
-  for (int k = 0; k < g.R; k++) box[k] = r->slots[1 + k].qres_box;
-  RV_R(rv_full_search_multi(&cur.qres, refs_q, g.R, r->fs_jobs[si], nr, 16, 16, 1, 0, r->coarse,
+  RV_R(rv_full_search_multi(&S.qres, refs_q, g.R, r->fs_jobs[lv], nr, 16, 16, 1, 0, r->coarse,
                             &to_half, r->sea ? box : nullptr, st));
-  RV_EV(2, st);
+  RV_EV(2);
   // F2 half-res diamond -> F3 full-pel predictors
-  RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half, nr, 32, 32, 0, 0, 0, g.bd,
+  RV_R(rv_diamond_search_multi(&S.hres, refs_h, g.R, r->jobs_half[lv], nr, 32, 32, 0, 0, 0, g.bd,
                                r->half, nullptr, &to_full, st));
-  RV_EV(3, st);
+  RV_EV(3);
   // F3 full-res full-pel diamond -> sub-pel predictor; sub-pel diamond
-  // (speed 10: SAD, no hp) -> the F4 MC jobs of the sub-pel candidates
-  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full, nr, 64, 64, 0, 0, 0, g.bd,
+  // (speed 10: SAD, no hp) -> NEWMV of every superblock and reference
+  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
                                r->full, ev_full, &to_sub, st));
-  RV_EV(7, st);
-  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub, nr, 64, 64, 1, 0, 0, g.bd,
-                               r->sub, ev_sub, &to_mc, st));
-  RV_EV(4, st);
-  // F4 sub-pel MV candidates (all candidates when serial): luma + both
-  // chroma planes in one fused launch
-  if (serial) {
-    la.k_sel = ca.k_sel = -1;
-    la.n_tx *= 2;
-    ca.n_tx *= 2;
-  } else {
-    la.k_sel = ca.k_sel = 0;
+  RV_EV(4);
+  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
+                               r->sub, ev_sub, nullptr, st));
+  RV_EV(5);
+  // F4 every candidate, luma + both chroma planes in one fused launch
+  RdoArgs la, ca;
+  memset(&la, 0, sizeof(la));
+  la.p[0].org = cur.y;
+  for (int k = 0; k < g.R; k++) la.p[0].ref[k] = ref[k]->y;
+  la.p[0].dst = S.y;
+  la.p[0].levels = r->l_lev;
+  la.p[0].out = r->l_out;
+  la.g = r->cg;
+  la.sub = r->sub;
+  la.win = r->win;
+  la.imp = r->imp;
+  la.w_in_b = g.w_in_b;
+  la.h_in_b = g.h_in_b;
+  la.w_imp = g.w_imp;
+  la.n_tx = g.nsb * g.C;
+  la.ntx_per_cand = 1;
+  la.bd = g.bd;
+  la.mb_w = la.mb_h = kSb;
+  la.sub_w = la.sub_h = 8;
+  la.p[0].q = L.ql;
+  la.q_tx_index = 4 * 16 + 0;  // TX_64X64, DCT_DCT
+  la.tx_size = 4;
+  la.qindex = L.qidx;
+  ca = la;
+  const int ntx_c = r->ntx_c;
+  const int64_t nct = (int64_t)g.nsb * g.C * ntx_c;
+  const rv_plane cur_c[2] = {cur.u, cur.v}, s_c[2] = {S.u, S.v};
+  for (int p = 0; p < 2; p++) {
+    ca.p[p].org = cur_c[p];
+    for (int k = 0; k < g.R; k++) ca.p[p].ref[k] = p ? ref[k]->v : ref[k]->u;
+    ca.p[p].dst = s_c[p];
+    ca.p[p].levels = r->c_lev + (size_t)p * g.nsb * ntx_c * 1024;
+    ca.p[p].out = r->c_out + (size_t)p * nct * 3;
+    ca.p[p].q = p ? L.qv : L.qu;
   }
-  const bool split = serial && (r->cfg.flags & RV_REPLAY_SPLIT_RDO) != 0;
-  if (split) {  // luma here, chroma pairs concurrently on the side stream
-    RV_H(hipEventRecord(r->fork2[slot], st));
-    RV_H(hipStreamWaitEvent(r->side, r->fork2[slot], 0));
-    RV_R(rv_rdo_candidates(la, ca, g.hbd, st, r->side));
-    RV_H(hipEventRecord(r->join2[slot], r->side));
-    RV_H(hipStreamWaitEvent(st, r->join2[slot], 0));
-  } else {
-    RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
-  }
-  RV_EV(8, st);
-  if (tm) r->ev_side[tslot] = !serial;
-  if (serial) {
-  } else {
-    RV_H(hipStreamWaitEvent(st, r->join[slot], 0));
-  }
-  score_candidates<<<g.nsb, 64, 0, st>>>(g, r->l_mom, r->u_sse, r->v_sse, r->lsub, r->csub,
-                                         r->coarse, r->half, r->full, r->sub, r->words,
-                                         r->tail + 2);
-  RV_EV(5, st);
-  // F5 importance SATD against reference 1
+  ca.n_tx = (int)nct;
+  ca.ntx_per_cand = ntx_c;
+  ca.mb_w = g.cw;
+  ca.mb_h = g.ch;
+  ca.xdec = g.xdec;
+  ca.ydec = g.ydec;
+  ca.sub_w = (g.cw < 8 ? g.cw : 8) >> g.xdec;
+  ca.sub_h = (g.ch < 8 ? g.ch : 8) >> g.ydec;
+  ca.q_tx_index = 3 * 16 + 0;  // TX_32X32, DCT_DCT
+  ca.tx_size = 3;
+  RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
+  RV_EV(6);
+  score_candidates<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, r->cg, L.lambda, L.ds[1], L.ds[2], r->sub,
+                                                     r->l_out,
+                                                     r->c_out, r->c_out + nct * 3, ntx_c, r->win,
+                                                     r->coarse, r->half, r->full, r->words);
+  RV_EV(7);
+  // F6 commit the winners into the frame
+  la.commit = ca.commit = 1;
+  la.n_tx = g.nsb;
+  ca.n_tx = g.nsb * ntx_c;
+  la.ntx_per_cand = 1;
+  RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
+  RV_EV(8);
+  // F5 importance SATD against reference 0
+  RV_H(hipMemsetAsync(r->tail + 2, 0, 8, st));
   {
     const unsigned nb = (unsigned)((r->n_imp + 255) / 256);
     if (g.hbd)
-      importance_kernel<uint16_t><<<nb, 256, 0, st>>>(g, cur.y, r->slots[1].y, r->sub, r->imp_bx,
+      importance_kernel<uint16_t><<<nb, 256, 0, st>>>(g, cur.y, ref[0]->y, r->sub, r->imp_bx,
                                                       r->imp_by, r->tail + 2);
     else
-      importance_kernel<uint8_t><<<nb, 256, 0, st>>>(g, cur.y, r->slots[1].y, r->sub, r->imp_bx,
+      importance_kernel<uint8_t><<<nb, 256, 0, st>>>(g, cur.y, ref[0]->y, r->sub, r->imp_bx,
                                                      r->imp_by, r->tail + 2);
   }
-  RV_EV(6, st);
+  RV_EV(9);
+  // F7 the reconstruction becomes a reference
+  r->coded++;
+  r->last = fi;
+  if (r->n_groups < 2) {
+    RV_R(pad_slot(r, S));
+  } else {
+    XRect xr[3];
+    group_rects(r, r->my_group, xr);
+    RV_R(xcopy(r, S, xr, 3, 0, r->xsend));
+    if (r->comm) {
+#if RV_HAVE_RCCL
+      if (ncclAllGather(r->xsend, r->xrecv, r->xbytes, ncclUint8, (ncclComm_t)r->comm, st) !=
+          ncclSuccess)
+        return rv_set_error(RV_EHIP, "rv_replay_frame: ncclAllGather");
+      RV_R(rv_replay_import(r));
+#else
+      return rv_set_error(RV_EINVAL, "rv_replay_frame: built without RCCL");
+#endif
+    }
+  }
+  RV_EV(10);
 #undef RV_EV
+  if (info) *info = fi;
   RV_H(hipGetLastError());
   return RV_OK;
 }
@@ -787,27 +1053,38 @@ int rv_replay_frame(rv_replay *r, int me_range_scale) {
 int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap) {
   if (!r || !host_out) return rv_set_error(RV_EINVAL, "rv_replay_results: null");
   const Geo &g = r->g;
-  const int nw = g.nsb * (8 * g.R + 2);
-  const int total = nw + 4;
+  const int nw = g.nsb * (8 * g.R + 4);
+  const int total = nw + 5;
   if (cap < total) return rv_set_error(RV_EINVAL, "rv_replay_results: cap too small");
-  // verification checksums of the last frame (outside the per-frame work)
+  // verification checksums of the last coded frame (outside the per-frame work)
   hipStream_t st = r->stream;
-  const int ntx_c = (g.cw / 32) * (g.ch / 32);
-  const int64_t nl = (int64_t)g.nctx * 1024, nc = (int64_t)g.nctx * ntx_c * 1024;
+  const int64_t nl = (int64_t)g.nsb * 1024, nc = (int64_t)g.nsb * r->ntx_c * 1024;
   RV_H(hipMemsetAsync(r->tail, 0, 2 * 8, st));
-  coeff_checksum<<<1024, 256, 0, st>>>(r->l_packed, nl, 1024, r->tail);
-  coeff_checksum<<<1024, 256, 0, st>>>(r->c_packed, 2 * nc, 1024, r->tail);
-  const rv_plane *tp[3] = {&r->tall_y, &r->tall_u, &r->tall_v};
+  RV_H(hipMemsetAsync(r->tail + 3, 0, 2 * 8, st));
+  coeff_checksum<<<1024, 256, 0, st>>>(r->l_lev, nl, 1024, r->tail);
+  coeff_checksum<<<1024, 256, 0, st>>>(r->c_lev, 2 * nc, 1024, r->tail);
+  const RvSlot &s = r->slots[r->last.display % kSlots];
+  const rv_plane *pl[3] = {&s.y, &s.u, &s.v};
   for (int i = 0; i < 3; i++) {
-    if (g.hbd)
-      sum_plane<uint16_t><<<1024, 256, 0, st>>>(*tp[i], tp[i]->width, tp[i]->height, r->tail + 1);
-    else
-      sum_plane<uint8_t><<<1024, 256, 0, st>>>(*tp[i], tp[i]->width, tp[i]->height, r->tail + 1);
+    const rv_plane &p = *pl[i];
+    const int xd = i ? g.xdec : 0, yd = i ? g.ydec : 0;
+    const int x0 = (g.tx0 * kSb) >> xd, y0 = (g.ty0 * kSb) >> yd;
+    int x1 = ((g.tx0 + g.tw) * kSb) >> xd, y1 = ((g.ty0 + g.th) * kSb) >> yd;
+    x1 = x1 < p.width ? x1 : p.width;
+    y1 = y1 < p.height ? y1 : p.height;
+    // the group's region, and (after the exchange) the whole frame
+    if (g.hbd) {
+      sum_rect<uint16_t><<<1024, 256, 0, st>>>(p, x0, y0, x1 - x0, y1 - y0, r->tail + 1);
+      sum_rect<uint16_t><<<1024, 256, 0, st>>>(p, 0, 0, p.width, p.height, r->tail + 4);
+    } else {
+      sum_rect<uint8_t><<<1024, 256, 0, st>>>(p, x0, y0, x1 - x0, y1 - y0, r->tail + 1);
+      sum_rect<uint8_t><<<1024, 256, 0, st>>>(p, 0, 0, p.width, p.height, r->tail + 4);
+    }
   }
   RV_H(hipGetLastError());
-  RV_H(hipMemcpyAsync(host_out, r->words, (size_t)nw * 8, hipMemcpyDeviceToHost, r->stream));
-  RV_H(hipMemcpyAsync(host_out + nw, r->tail, 3 * 8, hipMemcpyDeviceToHost, r->stream));
-  RV_H(hipStreamSynchronize(r->stream));
+  RV_H(hipMemcpyAsync(host_out, r->words, (size_t)nw * 8, hipMemcpyDeviceToHost, st));
+  RV_H(hipMemcpyAsync(host_out + nw, r->tail, 5 * 8, hipMemcpyDeviceToHost, st));
+  RV_H(hipStreamSynchronize(st));
   host_out[nw + 3] = (uint64_t)r->n_imp;
   return total;
 }
@@ -818,25 +1095,15 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
   if (last < 1) last = 1;
   if (last > rv_replay::kRing) last = rv_replay::kRing;
   if (last > r->timed) last = (int)r->timed;
-  for (int i = 0; i < cap && i < 10; i++) ms_out[i] = 0.f;
+  for (int i = 0; i < cap && i < rv_replay::kEv - 1; i++) ms_out[i] = 0.f;
   int n = 0;
   for (int f = 0; f < last; f++) {
-    const int ts = (int)((r->timed - 1 - f) % rv_replay::kRing);
-    hipEvent_t *e = r->evs[ts];
-    RV_H(hipEventSynchronize(e[6]));
+    hipEvent_t *e = r->evs[(r->timed - 1 - f) % rv_replay::kRing];
+    RV_H(hipEventSynchronize(e[rv_replay::kEv - 1]));
     n = 0;
-    for (int i = 0; i < 6 && n < cap; i++) {  // stages F0..F5
+    for (int i = 0; i < rv_replay::kEv - 1 && n < cap; i++) {
       float ms = 0.f;
       RV_H(hipEventElapsedTime(&ms, e[i], e[i + 1]));
-      ms_out[n++] += ms;
-    }
-    // kernel brackets: F3 full-pel diamond, F3 sub-pel diamond, F4 fused
-    // sub-pel MV candidates (main stream), F4 fused zero-MV candidates
-    // (side stream, concurrent with F0-F3)
-    const int br[4][2] = {{3, 7}, {7, 4}, {4, 8}, {9, 10}};
-    for (int i = 0; i < 4 && n < cap; i++) {
-      float ms = 0.f;
-      if (i < 3 || r->ev_side[ts]) RV_H(hipEventElapsedTime(&ms, e[br[i][0]], e[br[i][1]]));
       ms_out[n++] += ms;
     }
   }
@@ -858,12 +1125,13 @@ int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out, int 
   return stage_times(r, ms_out, cap, last_frames);
 }
 // Diamond-search candidate evaluations summed over the last min(frames, 64)
-// frames: out[0] F3 full-pel, out[1] F3 sub-pel, out[2] frames summed.
+// coded frames: out[0] F3 full-pel, out[1] F3 sub-pel, out[2] frames summed.
 int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
   if (!r || !out || cap < 3) return rv_set_error(RV_EINVAL, "rv_replay_counters");
   const Geo &g = r->g;
   const int nj = g.nsb * g.R;
-  const int nf = r->frames < rv_replay::kRing ? (int)r->frames : rv_replay::kRing;
+  const long nonkey = r->coded > 0 ? r->coded - 1 : 0;
+  const int nf = nonkey < rv_replay::kRing ? (int)nonkey : rv_replay::kRing;
   RV_H(hipStreamSynchronize(r->stream));
   std::vector<uint32_t> h((size_t)nf * 2 * nj);
   if (nf) RV_H(hipMemcpy(h.data(), r->ds_evals, h.size() * 4, hipMemcpyDeviceToHost));
@@ -873,6 +1141,52 @@ int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
       for (int j = 0; j < nj; j++) out[k] += h[((size_t)f * 2 + k) * nj + j];
   out[2] = (uint64_t)nf;
   return 3;
+}
+
+// ---- RCCL communicator for the tile-group exchange ---------------------------
+int rv_comm_unique_id(uint8_t *out, int cap) {
+#if RV_HAVE_RCCL
+  if (!out || cap < (int)sizeof(ncclUniqueId)) return rv_set_error(RV_EINVAL, "rv_comm_unique_id");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return rv_set_error(RV_EHIP, "ncclGetUniqueId");
+  memcpy(out, &id, sizeof(id));
+  return (int)sizeof(id);
+#else
+  (void)out;
+  (void)cap;
+  return rv_set_error(RV_EINVAL, "rv_comm_unique_id: built without RCCL");
+#endif
+}
+
+void *rv_comm_create(const uint8_t *id, int nranks, int rank) {
+#if RV_HAVE_RCCL
+  if (!id || nranks < 1 || rank < 0 || rank >= nranks) {
+    rv_set_error(RV_EINVAL, "rv_comm_create");
+    return nullptr;
+  }
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  ncclComm_t c = nullptr;
+  if (ncclCommInitRank(&c, nranks, u, rank) != ncclSuccess) {
+    rv_set_error(RV_EHIP, "ncclCommInitRank");
+    return nullptr;
+  }
+  return c;
+#else
+  (void)id;
+  (void)nranks;
+  (void)rank;
+  rv_set_error(RV_EINVAL, "rv_comm_create: built without RCCL");
+  return nullptr;
+#endif
+}
+
+void rv_comm_destroy(void *comm) {
+#if RV_HAVE_RCCL
+  if (comm) (void)ncclCommDestroy((ncclComm_t)comm);
+#else
+  (void)comm;
+#endif
 }
 
 }  // extern "C"

@@ -1,16 +1,23 @@
-"""One process per GPU: rank bookkeeping for tile-parallel runs.
+"""One process per GPU: rank bookkeeping and the tile-parallel encode of one
+stream.
 
 rav1e parallelises a frame only across AV1 tiles (rayon `into_par_iter`
 over `TileContextMut`s, src/encoder.rs:2772-2781); tiles share nothing but
-read-only reference frames.  Here every rank (one per GPU, launched by
-torch.distributed.run) owns its own tile stream, so the data path has no
-collective: torch.distributed (gloo) carries only the start barrier and the
-max-over-ranks time.  SURVEY.md §8e, DESIGN.md §6.
+the reference frames.  Here every rank (one per GPU, launched by
+torch.distributed.run) codes one tile group of every frame of the SAME
+stream; after each frame the reconstruction of every group must reach every
+rank before the next frame's motion search (the reference's write-back,
+src/encoder.rs:3411-3429): an all-gather of the packed group regions --
+RCCL over xGMI inside rv_replay_frame on the GPU, gloo in the CPU tests.
+torch.distributed (gloo) also carries the barrier, the max-over-ranks time
+and the RCCL bootstrap.  SURVEY.md §8e, DESIGN.md §6.
 """
 from __future__ import annotations
 
 import os
 from dataclasses import dataclass
+
+import numpy as np
 
 
 @dataclass
@@ -18,12 +25,6 @@ class RankInfo:
     rank: int
     world: int
     local_rank: int
-
-    @property
-    def frame_offset(self) -> int:
-        """Synthetic-input time offset of this rank's tile stream: ranks
-        encode different content (no two ranks redo the same work)."""
-        return 1000 * self.rank
 
 
 def rank_info() -> RankInfo:
@@ -34,8 +35,8 @@ def rank_info() -> RankInfo:
 
 
 class RankGroup:
-    """torch.distributed on gloo (CPU tensors): barrier + reductions of
-    scalars.  A no-op at world size 1."""
+    """torch.distributed on gloo (CPU tensors): barrier, reductions of
+    scalars, byte all-gathers.  A no-op at world size 1."""
 
     def __init__(self, info: RankInfo, backend: str = "gloo"):
         self.info = info
@@ -69,7 +70,57 @@ class RankGroup:
         self.dist.all_gather(out, t)
         return [int(o[0]) for o in out]
 
+    def all_gather_bytes(self, buf: np.ndarray, size: int) -> list[np.ndarray]:
+        """Every rank's byte buffer (padded to `size`), in rank order."""
+        if not self.dist:
+            return [buf]
+        import torch
+        t = torch.zeros(size, dtype=torch.uint8)
+        t[: buf.size] = torch.from_numpy(buf)
+        out = [torch.zeros(size, dtype=torch.uint8) for _ in range(self.info.world)]
+        self.dist.all_gather(out, t)
+        return [o.numpy() for o in out]
+
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
             self.dist = None
+
+
+class TileParallel:
+    """This rank's share of a tile-parallel encode: the engine (HipReplay or
+    the oracle's CpuReplay) codes tile group rects[my] of every frame; frame()
+    also moves every group's reconstruction to every rank.
+
+    * HipReplay with an RCCL communicator: rv_replay_frame packs the group,
+      all-gathers over RCCL on the replay stream, unpacks and pads -- no
+      host round trip (comm from rav1e_amd.replay.RcclComm).
+    * CpuReplay: pack, gloo all-gather, unpack, pad."""
+
+    def __init__(self, engine, rects, my, group: RankGroup, comm=None):
+        self.engine, self.rects, self.my, self.group = engine, list(rects), my, group
+        self.world = len(self.rects)
+        self.host = not hasattr(engine, "set_groups")
+        if self.world > 1 and not self.host:
+            engine.set_groups(self.rects, my, comm.h if comm else None)
+            if comm is None:
+                raise ValueError("a GPU engine in a multi-rank run needs an RCCL communicator")
+        if self.host:
+            self.size = max(engine.region_bytes(r) for r in self.rects)
+
+    def frame(self):
+        if self.world == 1:
+            return self.engine.frame()
+        if not self.host:
+            return self.engine.frame()
+        info = self.engine.frame(pad=False)
+        mine = self.engine.export(self.rects[self.my])
+        bufs = self.group.all_gather_bytes(mine, self.size)
+        for k, (rect, b) in enumerate(zip(self.rects, bufs)):
+            if k != self.my:
+                self.engine.import_(rect, b[: self.engine.region_bytes(rect)])
+        self.engine.pad_recon()
+        return info
+
+    def results(self):
+        return self.engine.results()

@@ -1,10 +1,12 @@
 """Hot-path replay: synthetic input frames and the HIP replay driver
 (rv_replay_* of include/rav1e_hip.h).  See DESIGN.md "Replay driver".
 
-The replay runs, per frame, the accelerated stages of a speed-10 rav1e
-encode of one tile (coarse 1/4-res full search, 1/2-res and full-res
-diamond + sub-pel search, RDO candidate MC / transforms / distortion,
-8x8 importance SATD) with all frames resident in HBM.
+The replay codes a stream in the reorder pyramid's coding order: per frame
+the accelerated stages of a speed-10 rav1e encode of one tile group (coarse
+1/4-res full search, 1/2-res and full-res diamond + sub-pel search, every
+RDO inter candidate skip / non-skip with rav1e's rd cost, the winners'
+reconstruction -- the later frames' reference -- and the 8x8 importance
+SATD), all frames resident in HBM.
 """
 from __future__ import annotations
 
@@ -12,10 +14,11 @@ import ctypes as C
 
 import numpy as np
 
-from . import RvReplayCfg, _check, lib
+from . import RvReplayCfg, RvReplayFrameInfo, RvReplayLevelParams, _check, lib
+from . import rate as _rate
 
-RV_REPLAY_SIDE_RDO = 1  # include/rav1e_hip.h
-RV_REPLAY_SPLIT_RDO = 2
+DEFAULT_QUANTIZER = 100  # rav1e's default --quantizer (src/api/config.rs)
+
 RV_REPLAY_EXHAUSTIVE_FS = 4  # F1 without successive elimination (same results)
 
 # GOP of the reference's reorder pyramid (src/api/internal.rs:61-95):
@@ -23,79 +26,246 @@ RV_REPLAY_EXHAUSTIVE_FS = 4  # F1 without successive elimination (same results)
 # (src/encoder.rs:838).
 GOP_SCALES = (4, 2, 1, 1)
 
-_LATTICE = 8
+def _hash32(x: np.ndarray) -> np.ndarray:
+    """lowbias32 on uint32 arrays (wrapping), = synth_hash in rv_frame.hip."""
+    x = x.astype(np.uint32)
+    x ^= x >> np.uint32(16)
+    x *= np.uint32(0x7FEB352D)
+    x ^= x >> np.uint32(15)
+    x *= np.uint32(0x846CA68B)
+    x ^= x >> np.uint32(16)
+    return x
 
 
-def _value_noise(xs: np.ndarray, ys: np.ndarray) -> np.ndarray:
-    """Bilinear value noise on an 8-px lattice of seeded values (0x5EED)."""
-    rng = np.random.default_rng(0x5EED)
-    lat = rng.random((257, 257)) * 2.0 - 1.0
-    gx, gy = xs / _LATTICE, ys / _LATTICE
-    x0, y0 = np.floor(gx), np.floor(gy)
-    fx, fy = gx - x0, gy - y0
-    x0 = x0.astype(np.int64) % 256
-    y0 = y0.astype(np.int64) % 256
-    v00 = lat[y0, x0]
-    v01 = lat[y0, x0 + 1]
-    v10 = lat[y0 + 1, x0]
-    v11 = lat[y0 + 1, x0 + 1]
-    return (v00 * (1 - fx) + v01 * fx) * (1 - fy) + (v10 * (1 - fx) + v11 * fx) * fy
+def _u32(v) -> np.ndarray:
+    return np.asarray(v, dtype=np.int64).astype(np.uint32)
 
 
-def synth_plane(w, h, t, scale_x=1, scale_y=1, amp=60.0, tex=24.0, phase=0.0, bd=8):
-    x = np.arange(w, dtype=np.float64)[None, :] * scale_x
-    y = np.arange(h, dtype=np.float64)[:, None] * scale_y
-    xm, ym = x - 1.25 * t, y - 0.75 * t
-    base = 128.0 + amp * np.sin(2 * np.pi * xm / 97.0 + phase) * np.cos(2 * np.pi * ym / 61.0)
-    base = base + tex * _value_noise(np.broadcast_to(xm, (h, w)), np.broadcast_to(ym, (h, w)))
-    rng = np.random.default_rng(0x5EED ^ (int(t) * 2654435761 + int(phase * 1000)))
-    base = base + rng.integers(-2, 3, (h, w))
-    y8 = np.clip(np.floor(base + 0.5), 0, 255).astype(np.int64)
-    if bd == 8:
-        return y8.astype(np.uint8)
-    return (y8 * 4 + rng.integers(0, 4, (h, w))).astype(np.uint16)
+def _wave(q: np.ndarray, period: int) -> np.ndarray:
+    h = period // 2
+    return np.where(q < h, 256 * q * (h - q) // (h * h), -(256 * (q - h) * (period - q) // (h * h)))
+
+
+def _lat(ix: np.ndarray, iy: np.ndarray) -> np.ndarray:
+    k = _u32(ix) * np.uint32(0x9E3779B1) ^ _u32(iy) * np.uint32(0x85EBCA77) ^ np.uint32(0x5EED)
+    return (_hash32(k) & np.uint32(511)).astype(np.int64) - 256
+
+
+def synth_plane(w, h, t, xdec=0, ydec=0, pidx=0, bd=8) -> np.ndarray:
+    """Plane pidx of synthetic frame t (integer form):
+    bit-identical to rv_synth_frame (rv_frame.hip synth_kernel).  A 2-D wave
+    times a value-noise texture on an 8-px lattice plus +-2 noise, moving
+    (1.25, 0.75) luma px per frame, in luma-space quarter-pel coordinates."""
+    with np.errstate(over="ignore"):
+        x = np.arange(w, dtype=np.int64)[None, :]
+        y = np.arange(h, dtype=np.int64)[:, None]
+        X4 = ((4 * x) << xdec) - 5 * t + 64 * pidx
+        Y4 = ((4 * y) << ydec) - 3 * t
+        X4, Y4 = np.broadcast_arrays(X4, Y4)
+        ix, fx, iy, fy = X4 >> 5, X4 & 31, Y4 >> 5, Y4 & 31
+        v = ((_lat(ix, iy) * (32 - fx) + _lat(ix + 1, iy) * fx) * (32 - fy) +
+             (_lat(ix, iy + 1) * (32 - fx) + _lat(ix + 1, iy + 1) * fx) * fy)
+        ta, wa = (12, 30) if pidx else (24, 60)
+        tex = (v * ta) >> 18
+        wave = (_wave(X4 % 388, 388) * _wave(Y4 % 244, 244) * wa) >> 12
+        xs, ys = np.broadcast_arrays(x, y)
+        hs = _hash32(_u32(xs) * np.uint32(0x27D4EB2D) ^ _u32(ys) * np.uint32(0x165667B1) ^
+                     _u32(t) * np.uint32(0x9E3779B9) ^ _u32(pidx) * np.uint32(0x85EBCA6B))
+        noise = (hs % np.uint32(5)).astype(np.int64) - 2
+        v8 = np.clip(128 + wave + tex + noise, 0, 255)
+        if bd == 8:
+            return v8.astype(np.uint8)
+        lo = (_hash32(hs ^ np.uint32(0xABCD)) & np.uint32((1 << (bd - 8)) - 1)).astype(np.int64)
+        return ((v8 << (bd - 8)) | lo).astype(np.uint16)
 
 
 def synth_frame(w, h, t, xdec=1, ydec=1, bd=8) -> np.ndarray:
-    """Planar Y, U, V of synthetic frame t, concatenated."""
+    """Planar Y, U, V of synthetic frame t, concatenated (= rv_synth_frame)."""
     cw, ch = (w + xdec) >> xdec, (h + ydec) >> ydec
-    y = synth_plane(w, h, t, bd=bd)
-    u = synth_plane(cw, ch, t, 1 << xdec, 1 << ydec, 30.0, 12.0, 1.3, bd)
-    v = synth_plane(cw, ch, t, 1 << xdec, 1 << ydec, 30.0, 12.0, 2.6, bd)
+    y = synth_plane(w, h, t, 0, 0, 0, bd)
+    u = synth_plane(cw, ch, t, xdec, ydec, 1, bd)
+    v = synth_plane(cw, ch, t, xdec, ydec, 2, bd)
     return np.concatenate([y.ravel(), u.ravel(), v.ravel()])
+
+
+def frame_bytes(width, height, xdec=1, ydec=1, bit_depth=8) -> int:
+    """Bytes of one planar Y, U, V picture (tightly packed)."""
+    cw, ch = (width + xdec) >> xdec, (height + ydec) >> ydec
+    return (width * height + 2 * cw * ch) * (2 if bit_depth > 8 else 1)
+
+
+# ---- tiling (TilingInfo, src/tiling/tiler.rs:18-138) ---------------------
+MAX_TILE_WIDTH, MAX_TILE_AREA = 4096, 4096 * 2304
+MAX_TILE_COLS = MAX_TILE_ROWS = 64
+MAX_TILE_RATE = 4096.0 * 2176.0 * 60.0 * 1.1
+
+
+def tile_log2(blk_size: int, target: int) -> int:
+    """TilingInfo::tile_log2 (src/tiling/tiler.rs:132-138)."""
+    k = 0
+    while (blk_size << k) < target:
+        k += 1
+    return k
+
+
+def tiling_info(width, height, tile_cols_log2=0, tile_rows_log2=0, frame_rate=30.0,
+                sb_size_log2=6) -> dict:
+    """TilingInfo::from_target_tiles (src/tiling/tiler.rs:49-126)."""
+    import math
+    fw, fh = (width + 7) & ~7, (height + 7) & ~7
+
+    def shift(v, n):  # align_power_of_two_and_shift
+        return (v + (1 << n) - 1) >> n
+    sb_cols, sb_rows = shift(fw, sb_size_log2), shift(fh, sb_size_log2)
+    max_tile_width_sb = MAX_TILE_WIDTH >> sb_size_log2
+    max_tile_area_sb = MAX_TILE_AREA >> (2 * sb_size_log2)
+    min_cols_log2 = tile_log2(max_tile_width_sb, sb_cols)
+    max_cols_log2 = tile_log2(1, min(sb_cols, MAX_TILE_COLS))
+    max_rows_log2 = tile_log2(1, min(sb_rows, MAX_TILE_ROWS))
+    min_tiles_log2 = max(min_cols_log2, tile_log2(max_tile_area_sb, sb_cols * sb_rows))
+    rl = math.ceil(math.log2(math.ceil(fw * fh * frame_rate / MAX_TILE_RATE)))
+    min_tiles_rl_log2 = max(min_tiles_log2, int(rl))
+    cols_log2 = min(max(tile_cols_log2, min_cols_log2), max_cols_log2)
+    tile_w = shift(sb_cols, cols_log2)
+    min_rows_log2 = min_tiles_log2 - cols_log2 if min_tiles_log2 > cols_log2 else 0
+    min_rows_rl = min_tiles_rl_log2 - cols_log2 if min_tiles_rl_log2 > cols_log2 else 0
+    rows_log2 = min(max(tile_rows_log2, min_rows_log2, min_rows_rl), max_rows_log2)
+    tile_h = shift(sb_rows, rows_log2)
+    return {"tile_width_sb": tile_w, "tile_height_sb": tile_h,
+            "cols": (sb_cols + tile_w - 1) // tile_w, "rows": (sb_rows + tile_h - 1) // tile_h,
+            "tile_cols_log2": cols_log2, "tile_rows_log2": rows_log2,
+            "max_tile_cols_log2": max_cols_log2, "max_tile_rows_log2": max_rows_log2,
+            "sb_cols": sb_cols, "sb_rows": sb_rows}
+
+
+def tiling_for(width, height, tile_cols=0, tile_rows=0, tiles=0) -> dict:
+    """The encoder's tiling: --tile-cols / --tile-rows, or --tiles via the
+    search loop of src/encoder.rs:583-621."""
+    t = tiling_info(width, height, tile_log2(1, max(tile_cols, 1)), tile_log2(1, max(tile_rows, 1)))
+    if tiles > 0:
+        rl = cl = 0
+        while rl < t["max_tile_rows_log2"] or cl < t["max_tile_cols_log2"]:
+            t = tiling_info(width, height, cl, rl)
+            if t["rows"] * t["cols"] >= tiles:
+                break
+            if (t["tile_height_sb"] >= t["tile_width_sb"] and
+                    t["tile_rows_log2"] < t["max_tile_rows_log2"]) or cl >= t["max_tile_cols_log2"]:
+                rl += 1
+            else:
+                cl += 1
+    return t
+
+
+def tile_groups(tiling: dict, world: int) -> list:
+    """Split the tiles (raster order) into `world` contiguous groups, one per
+    rank; every group must be a rectangle of whole tiles.  Rects are
+    (tx0, ty0, tw, th) in superblocks."""
+    cols, rows = tiling["cols"], tiling["rows"]
+    tws, ths = tiling["tile_width_sb"], tiling["tile_height_sb"]
+    sbc, sbr = tiling["sb_cols"], tiling["sb_rows"]
+    n = cols * rows
+    if world < 1 or world > n:
+        raise ValueError(f"{world} ranks for {n} tiles")
+    out = []
+    for r in range(world):
+        a, b = r * n // world, (r + 1) * n // world
+        tiles = [(i % cols, i // cols) for i in range(a, b)]
+        c0, c1 = min(t[0] for t in tiles), max(t[0] for t in tiles)
+        r0, r1 = min(t[1] for t in tiles), max(t[1] for t in tiles)
+        if len(tiles) != (c1 - c0 + 1) * (r1 - r0 + 1):
+            raise ValueError(f"tiles {a}..{b - 1} of a {cols}x{rows} grid are not a rectangle")
+        x0, y0 = c0 * tws, r0 * ths
+        out.append((x0, y0, min((c1 + 1) * tws, sbc) - x0, min((r1 + 1) * ths, sbr) - y0))
+    return out
 
 
 def result_words(width, height, n_refs, tile_w_sb=0, tile_h_sb=0, tile_x0=0, tile_y0=0):
     sbc, sbr = (width + 63) // 64, (height + 63) // 64
     tw = tile_w_sb or (sbc - tile_x0)
     th = tile_h_sb or (sbr - tile_y0)
-    return tw * th * (8 * n_refs + 2) + 4
+    return tw * th * (8 * n_refs + 4) + 5
 
 
 class HipReplay:
-    """The GPU replay of one tile (rv_replay_create ... rv_replay_destroy)."""
+    """The GPU replay of one tile group (rv_replay_create ... rv_replay_destroy).
 
-    def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, tile=None,
-                 stream=None, flags=0):
+    group = (tx0, ty0, tw, th) superblocks (None: the whole frame);
+    tile_size = (tile_width_sb, tile_height_sb) of the uniform tiling (0: one
+    tile); n_inputs input frames live in HBM (display d reads d % n_inputs)."""
+
+    def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, group=None,
+                 tile_size=(0, 0), n_inputs=8, stream=None, flags=0,
+                 quantizer=DEFAULT_QUANTIZER):
         cfg = RvReplayCfg()
         cfg.width, cfg.height, cfg.xdec, cfg.ydec = width, height, xdec, ydec
-        cfg.bit_depth, cfg.n_refs, cfg.rdo_candidates = bit_depth, n_refs, 2 * n_refs
-        cfg.flags = flags
-        if tile:
-            cfg.tile_x0, cfg.tile_y0, cfg.tile_w, cfg.tile_h = tile
+        cfg.bit_depth, cfg.n_refs, cfg.n_inputs, cfg.flags = bit_depth, n_refs, n_inputs, flags
+        cfg.tile_w_sb, cfg.tile_h_sb = tile_size
+        if group:
+            cfg.tile_x0, cfg.tile_y0, cfg.tile_w, cfg.tile_h = group
         self.cfg = cfg
+        self.geom = (width, height, xdec, ydec, bit_depth)
         self.h = lib().rv_replay_create(C.byref(cfg), stream)
         if not self.h:
             raise RuntimeError(f"rv_replay_create: {lib().rv_last_error().decode()}")
         self.n_words = result_words(width, height, n_refs, cfg.tile_w, cfg.tile_h,
                                     cfg.tile_x0, cfg.tile_y0)
+        self.levels = _rate.level_params(quantizer, bit_depth)
+        for lv, d in enumerate(self.levels):
+            p = RvReplayLevelParams.from_dict(d)
+            _check(lib().rv_replay_set_level_params(self.h, lv, C.byref(p)),
+                   "rv_replay_set_level_params")
 
-    def set_frame(self, slot: int, yuv: np.ndarray):
+    def _frame_array(self):
+        w, h, xd, yd, bd = self.geom
+        n = frame_bytes(w, h, xd, yd, bd) // (2 if bd > 8 else 1)
+        return np.zeros(n, dtype=np.uint16 if bd > 8 else np.uint8)
+
+    def synth_inputs(self, t0: int = 0):
+        _check(lib().rv_replay_synth_inputs(self.h, t0), "rv_replay_synth_inputs")
+
+    def set_input(self, idx: int, yuv: np.ndarray):
         yuv = np.ascontiguousarray(yuv)
-        _check(lib().rv_replay_set_frame(self.h, slot, yuv.ctypes.data), "rv_replay_set_frame")
+        _check(lib().rv_replay_set_input(self.h, idx, yuv.ctypes.data), "rv_replay_set_input")
 
-    def frame(self, me_range_scale: int):
-        _check(lib().rv_replay_frame(self.h, me_range_scale), "rv_replay_frame")
+    def get_input(self, idx: int) -> np.ndarray:
+        out = self._frame_array()
+        _check(lib().rv_replay_get_input(self.h, idx, out.ctypes.data), "rv_replay_get_input")
+        return out
+
+    def get_recon(self, display: int) -> np.ndarray:
+        out = self._frame_array()
+        _check(lib().rv_replay_get_recon(self.h, display, out.ctypes.data), "rv_replay_get_recon")
+        return out
+
+    def set_importances(self, imp):
+        if imp is None:
+            _check(lib().rv_replay_set_importances(self.h, None, 0), "rv_replay_set_importances")
+            return
+        imp = np.ascontiguousarray(imp, dtype=np.float32)
+        _check(lib().rv_replay_set_importances(self.h, imp.ctypes.data, imp.size),
+               "rv_replay_set_importances")
+
+    def frame(self) -> dict:
+        fi = RvReplayFrameInfo()
+        _check(lib().rv_replay_frame(self.h, C.byref(fi)), "rv_replay_frame")
+        return {"display": fi.display, "me_range_scale": fi.me_range_scale, "level": fi.level,
+                "is_key": fi.is_key, "ref_display": list(fi.ref_display)}
+
+    def set_groups(self, rects, my_group, comm=None):
+        arr = np.ascontiguousarray(np.asarray(rects, dtype=np.int32).ravel())
+        _check(lib().rv_replay_set_groups(self.h, len(rects), arr.ctypes.data, my_group, comm),
+               "rv_replay_set_groups")
+
+    def exchange_buffers(self):
+        """(send, recv, bytes_per_group): device pointers of the packed
+        region of this group and of the gathered regions of all groups."""
+        s, r, n = C.c_void_p(), C.c_void_p(), C.c_size_t()
+        _check(lib().rv_replay_exchange_buffers(self.h, C.byref(s), C.byref(r), C.byref(n)),
+               "rv_replay_exchange_buffers")
+        return s.value, r.value, n.value
+
+    def import_(self):
+        _check(lib().rv_replay_import(self.h), "rv_replay_import")
 
     def results(self) -> np.ndarray:
         out = np.zeros(self.n_words, dtype=np.uint64)
@@ -105,8 +275,8 @@ class HipReplay:
         return out[:n]
 
     def set_timing(self, stride: int, block: int = 1):
-        """Record the timing events on frames f with (f // block) % stride == 0
-        (rv_replay_set_timing)."""
+        """Record the timing events on coded frames f with (f // block) %
+        stride == 0 (rv_replay_set_timing)."""
         _check(lib().rv_replay_set_timing(self.h, stride, block), "rv_replay_set_timing")
 
     def stage_ms(self) -> np.ndarray:
@@ -139,3 +309,28 @@ class HipReplay:
             self.close()
         except Exception:
             pass
+
+
+class RcclComm:
+    """An RCCL communicator over all ranks (rv_comm_*), bootstrapped through
+    torch.distributed (gloo): rank 0's unique id is broadcast as bytes."""
+
+    def __init__(self, group):
+        import torch
+        info = group.info
+        idb = np.zeros(256, dtype=np.uint8)
+        if info.rank == 0:
+            n = lib().rv_comm_unique_id(idb.ctypes.data, idb.size)
+            if n < 0:
+                _check(n, "rv_comm_unique_id")
+        t = torch.from_numpy(idb)
+        group.dist.broadcast(t, src=0)
+        idb = t.numpy().copy()
+        self.h = lib().rv_comm_create(idb.ctypes.data, info.world, info.rank)
+        if not self.h:
+            raise RuntimeError(f"rv_comm_create: {lib().rv_last_error().decode()}")
+
+    def close(self):
+        if self.h:
+            lib().rv_comm_destroy(self.h)
+            self.h = None

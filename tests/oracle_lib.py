@@ -393,34 +393,93 @@ def cpu_share() -> int:
     return max(1, min(16, n))
 
 
-class CpuReplay:
-    """orc_replay_* (oracle/orc_replay.c): the replay schedule on the CPU.
-    `L` selects the oracle build (default: the tests' build; the bench's
-    baseline passes baseline_lib()[0])."""
+class OrcFrameInfo(C.Structure):
+    _fields_ = [("display", C.c_int32), ("me_range_scale", C.c_int32), ("level", C.c_int32),
+                ("is_key", C.c_int32), ("ref_display", C.c_int32 * 2)]
 
-    def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, tile=None,
-                 threads=1, L=None):
+
+class CpuReplay:
+    """orc_replay_* (oracle/orc_replay.c): the replay schedule on the CPU,
+    the same API as rav1e_amd.replay.HipReplay.  `L` selects the oracle
+    build (default: the tests' build; the bench's baseline passes
+    baseline_lib()[0])."""
+
+    def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, group=None,
+                 tile_size=(0, 0), n_inputs=8, threads=1, L=None, quantizer=100):
+        from rav1e_amd import rate as RT
         L = L or lib()
         self.L = L
         L.orc_replay_create.restype = C.c_void_p
-        L.orc_replay_create.argtypes = [C.c_int] * 11
+        L.orc_replay_create.argtypes = [C.c_int] * 14
         L.orc_replay_destroy.argtypes = [C.c_void_p]
-        L.orc_replay_set_frame.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
-        L.orc_replay_frame.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        L.orc_replay_set_input.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.orc_replay_get_recon.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.orc_replay_set_importances.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_replay_frame.argtypes = [C.c_void_p, C.POINTER(OrcFrameInfo), C.c_int, C.c_int]
         L.orc_replay_results.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
-        tx0, ty0, tw, th = tile or (0, 0, 0, 0)
+        L.orc_replay_xcopy.restype = C.c_int64
+        L.orc_replay_xcopy.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_replay_pad_recon.argtypes = [C.c_void_p]
+        I3, D3 = C.c_int32 * 3, C.c_double * 3
+        L.orc_replay_set_level_params.argtypes = [C.c_void_p, C.c_int, C.c_int, I3, I3,
+                                                  C.c_double, C.c_double, D3]
+        self.group = tuple(group) if group else None
+        tx0, ty0, tw, th = group or (0, 0, 0, 0)
         self.h = L.orc_replay_create(width, height, xdec, ydec, bit_depth, tx0, ty0, tw, th,
-                                     n_refs, threads)
+                                     tile_size[0], tile_size[1], n_refs, n_inputs, threads)
         assert self.h, "orc_replay_create failed"
         sbc, sbr = (width + 63) // 64, (height + 63) // 64
-        self.n_words = (tw or sbc - tx0) * (th or sbr - ty0) * (8 * n_refs + 2) + 4
+        self.n_words = (tw or sbc - tx0) * (th or sbr - ty0) * (8 * n_refs + 4) + 5
+        self.geom = (width, height, xdec, ydec, bit_depth)
+        self.levels = RT.level_params(quantizer, bit_depth)
+        for lv, d in enumerate(self.levels):
+            assert L.orc_replay_set_level_params(
+                self.h, lv, d["base_q_idx"], I3(*d["dc_delta_q"]), I3(*d["ac_delta_q"]),
+                d["lambda"], d["me_lambda"], D3(*d["dist_scale"])) == 0
 
-    def set_frame(self, slot, yuv):
+    def set_input(self, idx, yuv):
         yuv = np.ascontiguousarray(yuv)
-        assert self.L.orc_replay_set_frame(self.h, slot, yuv.ctypes.data) == 0
+        assert self.L.orc_replay_set_input(self.h, idx, yuv.ctypes.data) == 0
 
-    def frame(self, scale, sb_limit=0):
-        assert self.L.orc_replay_frame(self.h, scale, sb_limit) == 0
+    def set_importances(self, imp):
+        if imp is None:
+            assert self.L.orc_replay_set_importances(self.h, None, 0) == 0
+            return
+        imp = np.ascontiguousarray(imp, dtype=np.float32)
+        assert self.L.orc_replay_set_importances(self.h, imp.ctypes.data, imp.size) == 0
+
+    def frame(self, sb_limit=0, pad=True) -> dict:
+        fi = OrcFrameInfo()
+        assert self.L.orc_replay_frame(self.h, C.byref(fi), sb_limit, 1 if pad else 0) == 0
+        return {"display": fi.display, "me_range_scale": fi.me_range_scale, "level": fi.level,
+                "is_key": fi.is_key, "ref_display": list(fi.ref_display)}
+
+    def region_bytes(self, rect) -> int:
+        r = np.ascontiguousarray(np.asarray(rect, dtype=np.int32))
+        return int(self.L.orc_replay_xcopy(self.h, r.ctypes.data, None, 1))
+
+    def export(self, rect) -> np.ndarray:
+        """The packed reconstruction of tile group `rect` of the last frame."""
+        r = np.ascontiguousarray(np.asarray(rect, dtype=np.int32))
+        out = np.zeros(self.region_bytes(rect), dtype=np.uint8)
+        self.L.orc_replay_xcopy(self.h, r.ctypes.data, out.ctypes.data, 1)
+        return out
+
+    def import_(self, rect, buf: np.ndarray):
+        r = np.ascontiguousarray(np.asarray(rect, dtype=np.int32))
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        self.L.orc_replay_xcopy(self.h, r.ctypes.data, buf.ctypes.data, 0)
+
+    def pad_recon(self):
+        self.L.orc_replay_pad_recon(self.h)
+
+    def get_recon(self, display) -> np.ndarray:
+        from rav1e_amd.replay import frame_bytes
+        w, h, xd, yd, bd = self.geom
+        out = np.zeros(frame_bytes(w, h, xd, yd, bd) // (2 if bd > 8 else 1),
+                       dtype=np.uint16 if bd > 8 else np.uint8)
+        assert self.L.orc_replay_get_recon(self.h, display, out.ctypes.data) == 0
+        return out
 
     def results(self):
         out = np.zeros(self.n_words, dtype=np.uint64)

@@ -1,16 +1,17 @@
-"""N > 1 bench path on the CPU: world_size-2 gloo ranks, each running its own
-tile stream through bench.timed_run (the same loop bench.py times on the
-GPU), with the oracle's CpuReplay standing in for the device engine.
-Checks: no data-path collective is needed (each rank's words equal a
-single-process run of that rank's stream), ranks encode different content,
-and the reported time is the max over ranks."""
+"""N > 1 bench path on the CPU: world_size-2 gloo ranks code the tile groups
+of ONE stream through bench.timed_run and rav1e_amd.ranks.TileParallel
+(the loop bench.py times on the GPU), with the oracle's CpuReplay standing
+in for the device engine and gloo for the RCCL all-gather.  Checks: every
+rank's superblock words equal a single-process run of the whole frame with
+the same tiling, every rank ends with the same (whole) reconstruction, and
+the reported time is the max over ranks."""
 import os
 import socket
 
 import numpy as np
 import torch.multiprocessing as mp
 
-W, H, REFS = 192, 128, 1
+W, H, REFS, NIN = 384, 192, 2, 12
 
 
 def _free_port():
@@ -21,14 +22,21 @@ def _free_port():
     return p
 
 
-def _stream_words(offset, steps=3, warmup=1):
+def _tiling():
+    from rav1e_amd import replay as RP
+    t = RP.tiling_for(W, H, tile_cols=2)
+    return t, (t["tile_width_sb"], t["tile_height_sb"])
+
+
+def _single_words(frames):
     from rav1e_amd import replay as RP
     from tests import oracle_lib as O
-    c = O.CpuReplay(W, H, 1, 1, 8, REFS, threads=2)
-    for s in range(REFS + 1):
-        c.set_frame(s, RP.synth_frame(W, H, offset + s))
-    for i in range(warmup + steps):
-        c.frame(RP.GOP_SCALES[i % 4])
+    _, ts = _tiling()
+    c = O.CpuReplay(W, H, 1, 1, 8, REFS, tile_size=ts, n_inputs=NIN, threads=2)
+    for i in range(NIN):
+        c.set_input(i, RP.synth_frame(W, H, i))
+    for _ in range(frames):
+        c.frame()
     w = c.results()
     c.close()
     return w
@@ -39,29 +47,32 @@ def _rank_main(rank, world, port, q):
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import bench
     from rav1e_amd import replay as RP
-    from rav1e_amd.ranks import RankGroup, rank_info
+    from rav1e_amd.ranks import RankGroup, TileParallel, rank_info
     from tests import oracle_lib as O
     info = rank_info()
     g = RankGroup(info)
-    c = O.CpuReplay(W, H, 1, 1, 8, REFS, threads=2)
-    for s in range(REFS + 1):
-        c.set_frame(s, RP.synth_frame(W, H, info.frame_offset + s))
+    t, ts = _tiling()
+    rects = RP.tile_groups(t, world)
+    c = O.CpuReplay(W, H, 1, 1, 8, REFS, group=rects[rank], tile_size=ts, n_inputs=NIN,
+                    threads=2)
+    for i in range(NIN):
+        c.set_input(i, RP.synth_frame(W, H, i))
     if rank == 1:  # make rank 1 the slow one: the reported time must be its
         import time
         orig = c.frame
 
-        def slow(scale, sb_limit=0):
+        def slow(sb_limit=0, pad=True):
             time.sleep(0.05)
-            orig(scale, sb_limit)
+            return orig(sb_limit, pad)
         c.frame = slow
-    dt, words = bench.timed_run(c, g, steps=3, warmup=1)
-    sums = g.gather_u64(int(np.bitwise_xor.reduce(words)))
-    q.put((rank, dt, words.tolist(), sums))
+    eng = TileParallel(c, rects, rank, g)
+    dt, words = bench.timed_run(eng, g, steps=4, warmup=2)
+    q.put((rank, dt, words.tolist(), rects[rank]))
     c.close()
     g.close()
 
 
-def test_two_rank_gloo_tile_streams():
+def test_two_rank_gloo_tile_parallel_stream():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -70,16 +81,21 @@ def test_two_rank_gloo_tile_streams():
         p.start()
     res = {}
     for _ in range(2):
-        rank, dt, words, sums = q.get(timeout=240)
-        res[rank] = (dt, np.array(words, dtype=np.uint64), sums)
+        rank, dt, words, rect = q.get(timeout=240)
+        res[rank] = (dt, np.array(words, dtype=np.uint64), rect)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # max over ranks: both report the slow rank's time (>= 3 sleeps)
-    assert abs(res[0][0] - res[1][0]) < 1e-9 and res[0][0] >= 0.15
-    # each rank's result = a single-process run of its own stream
+    # max over ranks: both report the slow rank's time (>= 4 sleeps)
+    assert abs(res[0][0] - res[1][0]) < 1e-9 and res[0][0] >= 0.2
+    single = _single_words(6)
+    per = 8 * REFS + 4
+    sbc = (W + 63) // 64
+    sw = single[: len(single) - 5].reshape(-1, per)
     for r in range(2):
-        np.testing.assert_array_equal(res[r][1], _stream_words(1000 * r))
-    # different content per rank, and the gather agrees on every rank
-    assert not np.array_equal(res[0][1], res[1][1])
-    assert res[0][2] == res[1][2]
+        words, (x0, y0, gw, gh) = res[r][1], res[r][2]
+        gsb = words[: gw * gh * per].reshape(-1, per)
+        for sb in range(gw * gh):
+            np.testing.assert_array_equal(gsb[sb], sw[(y0 + sb // gw) * sbc + x0 + sb % gw])
+        assert words[-1] == single[-1]  # the whole reconstruction on every rank
+    assert res[0][2] != res[1][2]

@@ -1,15 +1,24 @@
-"""Replay driver: the HIP schedule (rv_replay_*) must reproduce the CPU
+"""Replay driver: the HIP stream schedule (rv_replay_*) must reproduce the CPU
 replay (oracle/orc_replay.c, the same schedule over the oracle's
-restatements) word for word; CPU-only tests pin the CPU replay itself."""
+restatements) word for word, frame by frame; CPU-only tests pin the CPU
+replay itself, the synthetic input and the host-side frame parameters."""
 import numpy as np
 import pytest
 
+from rav1e_amd import rate as RT
 from rav1e_amd import replay as RP
 from tests import oracle_lib as O
+
+PER_REF = 8
 
 
 def _frames(w, h, xdec, ydec, bd, n):
     return [RP.synth_frame(w, h, t, xdec, ydec, bd) for t in range(n)]
+
+
+def _sb_words(words, nsb, refs):
+    per = PER_REF * refs + 4
+    return words[: nsb * per].reshape(nsb, per)
 
 
 def test_synth_frames_deterministic_and_moving():
@@ -19,81 +28,259 @@ def test_synth_frames_deterministic_and_moving():
     assert a.dtype == np.uint8 and a.size == 128 * 64 * 3 // 2
     np.testing.assert_array_equal(a, b)
     assert (a != c).mean() > 0.5
+    assert 40 < a.mean() < 220 and a.std() > 10
     t10 = RP.synth_frame(128, 64, 3, bd=10)
     assert t10.dtype == np.uint16 and t10.max() <= 1023
     assert np.array_equal(t10[: 128 * 64] >> 2, a[: 128 * 64])
 
 
-def test_cpu_replay_thread_invariant():
-    fr = _frames(192, 128, 1, 1, 8, 3)
+def test_tiling_matches_the_encoders_tiling():
+    """TilingInfo::from_target_tiles / the --tiles loop (src/tiling/
+    tiler.rs:49-126, src/encoder.rs:583-621) at the BASELINE configs."""
+    c = RP.tiling_for(3840, 2160, tile_cols=8)
+    assert (c["tile_width_sb"], c["tile_height_sb"], c["cols"], c["rows"]) == (8, 34, 8, 1)
+    e = RP.tiling_for(3840, 2160, tiles=4)
+    assert (e["tile_width_sb"], e["tile_height_sb"], e["cols"], e["rows"]) == (30, 17, 2, 2)
+    b = RP.tiling_for(1920, 1080)
+    assert (b["cols"], b["rows"]) == (1, 1)
+    assert RP.tile_groups(c, 8)[-1] == (56, 0, 4, 34)
+    assert RP.tile_groups(c, 2) == [(0, 0, 32, 34), (32, 0, 28, 34)]
+    assert RP.tile_groups(e, 4)[3] == (30, 17, 30, 17)
+    with pytest.raises(ValueError):
+        RP.tile_groups(RP.tiling_for(3840, 2160, tile_cols=4, tile_rows=2), 3)
+
+
+def test_fixed_quantizer_frame_params():
+    """select_qi / new_from_log_q (src/rate.rs:570-606, 746-775) for
+    --quantizer 100: the P frame keeps base_q_idx 100, the pyramid's B
+    levels are 15-step coarser, lambda = ln2/6 * q^2 grows with the level;
+    bexp64 / blog64 invert each other (src/rate.rs:108-267)."""
+    for v in (1, 8, 100, 1000, 123456):
+        assert RT.bexp64(RT.blog64(v)) == v
+    assert RT.blog64(8) == RT.q57(3)
+    lv = RT.level_params(100, 8)
+    assert lv[0]["base_q_idx"] == 100
+    assert lv[0]["base_q_idx"] < lv[1]["base_q_idx"] < lv[2]["base_q_idx"]
+    assert 15 < lv[0]["lambda"] < lv[1]["lambda"] < lv[2]["lambda"] < 100
+    assert all(p["dist_scale"][0] == 1.0 and p["dist_scale"][1] > 1 for p in lv)
+    assert abs(lv[0]["me_lambda"] ** 2 - lv[0]["lambda"]) < 1e-9
+    lv10 = RT.level_params(100, 10)
+    assert abs(lv10[0]["lambda"] / lv[0]["lambda"] - 16) < 1.0
+
+
+def test_cpu_replay_stream_and_thread_invariant():
+    w, h = 256, 128
+    fr = _frames(w, h, 1, 1, 8, 12)
     outs = []
     for threads in (1, 3):
-        r = O.CpuReplay(192, 128, 1, 1, 8, 2, threads=threads)
-        for s, f in enumerate(fr):
-            r.set_frame(s, f)
-        r.frame(2)
+        r = O.CpuReplay(w, h, 1, 1, 8, 2, n_inputs=12, threads=threads)
+        for i, f in enumerate(fr):
+            r.set_input(i, f)
+        infos = [r.frame() for _ in range(6)]
         outs.append(r.results())
     np.testing.assert_array_equal(outs[0], outs[1])
-    w = outs[0]
-    nsb = 3 * 2
-    assert w[-1] == (192 // 8) * (128 // 8)  # importance blocks
-    assert w[-2] > 0 and w[-3] > 0  # satd sum, recon checksum
-    # the motion found at full res tracks the synthetic global motion
-    # (1.25, 0.75) px/frame: reference slot 1 is frame t=1, slot 0 is t=0
-    per = 8 * 2 + 2
-    subs = [int(w[sb * per + 6]) for sb in range(nsb)]
-    cols = [((s & 0xFFFF) ^ 0x8000) - 0x8000 for s in subs]
-    assert np.median(cols) > 0
+    assert [i["display"] for i in infos] == [0, 4, 2, 1, 3, 8]
+    assert infos[0]["is_key"] and [i["me_range_scale"] for i in infos[1:]] == [4, 2, 1, 1, 4]
+    assert infos[3]["ref_display"] == [0, 2] and infos[5]["ref_display"] == [4, 0]
+    wd = outs[0]
+    assert wd[-2] == (w // 8) * (h // 8)  # importance blocks
+    assert wd[-1] > 0 and wd[-3] > 0 and wd[-4] == wd[-1]  # one group: group sum = frame sum
+    sb = _sb_words(wd, 8, 2)
+    assert (sb[:, 16] < 8).all() and set(np.unique(sb[:, 17])) <= {0, 1}
+    # the NEWMV of the full-res search tracks the synthetic motion
+    # (1.25 px/frame; display 8 from 4: +5 px, i.e. +40 in 1/8 pel)
+    cols = [((int(s) & 0xFFFF) ^ 0x8000) - 0x8000 for s in sb[:, 6]]
+    assert np.median(cols) < 0
+
+
+def test_cpu_replay_reconstruction_is_the_reference():
+    """The coded frame's reconstruction lands in the DPB: the key frame's
+    reconstruction is its input, an inter frame's differs from its input
+    but stays close (skip / residual coding of a good prediction)."""
+    w, h = 192, 128
+    fr = _frames(w, h, 1, 1, 8, 8)
+    r = O.CpuReplay(w, h, 1, 1, 8, 2, n_inputs=8, threads=2)
+    for i, f in enumerate(fr):
+        r.set_input(i, f)
+    r.frame()
+    np.testing.assert_array_equal(r.get_recon(0), fr[0])
+    r.frame()
+    rec = r.get_recon(4).astype(np.int32)
+    err = np.abs(rec - fr[4].astype(np.int32))
+    assert err.mean() < 6 and (rec != fr[4]).any()
+
+
+def test_cpu_replay_importance_bias():
+    """compute_distortion_bias with block importances: a uniform importance
+    3 gives bias 1.65 instead of 0.65 (src/rdo.rs:495-508): every
+    distortion scales up, the searches do not change."""
+    w, h = 192, 128
+    fr = _frames(w, h, 1, 1, 8, 8)
+    res = []
+    for imp in (None, np.full((h // 8) * (w // 8), 3.0, np.float32)):
+        r = O.CpuReplay(w, h, 1, 1, 8, 1, n_inputs=8, threads=2)
+        for i, f in enumerate(fr):
+            r.set_input(i, f)
+        r.set_importances(imp)
+        r.frame()
+        r.frame()
+        res.append(_sb_words(r.results(), 6, 1))
+    np.testing.assert_array_equal(res[0][:, :8], res[1][:, :8])
+    cost = [np.ascontiguousarray(x[:, 10]).view(np.float64) for x in res]
+    assert (cost[1] >= cost[0]).all() and (cost[1] > cost[0]).any()
+
+
+def test_cpu_tile_groups_equal_the_whole_frame():
+    """Two tile groups coded separately and exchanging their
+    reconstructions reproduce the single-instance run of the same tiling,
+    superblock for superblock (tiles are independent, src/encoder.rs:
+    2772-2781)."""
+    w, h = 384, 192
+    fr = _frames(w, h, 1, 1, 8, 10)
+    t = RP.tiling_for(w, h, tile_cols=2)
+    ts = (t["tile_width_sb"], t["tile_height_sb"])
+    rects = RP.tile_groups(t, 2)
+    single = O.CpuReplay(w, h, n_inputs=10, threads=2, tile_size=ts)
+    gs = [O.CpuReplay(w, h, n_inputs=10, threads=2, group=r, tile_size=ts) for r in rects]
+    for e in [single] + gs:
+        for i, f in enumerate(fr):
+            e.set_input(i, f)
+    sbc = (w + 63) // 64
+    for _ in range(6):
+        single.frame()
+        for g in gs:
+            g.frame(pad=False)
+        bufs = [g.export(r) for g, r in zip(gs, rects)]
+        for k, g in enumerate(gs):
+            for j, r in enumerate(rects):
+                if j != k:
+                    g.import_(r, bufs[j])
+            g.pad_recon()
+        ws = single.results()
+        sw = _sb_words(ws, len(ws) // 20, 2)
+        for g, (x0, y0, gw_, gh_) in zip(gs, rects):
+            wg = g.results()
+            gsb = _sb_words(wg, gw_ * gh_, 2)
+            for sb in range(gw_ * gh_):
+                fsb = (y0 + sb // gw_) * sbc + x0 + sb % gw_
+                np.testing.assert_array_equal(gsb[sb], sw[fsb])
+            assert wg[-1] == ws[-1]  # every rank holds the whole reconstruction
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,h,xdec,ydec,bd,refs,tile", [
-    (256, 192, 1, 1, 8, 2, None),
-    (320, 128, 0, 0, 8, 1, None),
-    (256, 128, 1, 1, 10, 2, None),
-    (192, 128, 1, 1, 12, 1, None),  # 12 bits: exhaustive full search, 12-bit RDO kernel
-    (384, 192, 1, 1, 8, 2, (2, 0, 4, 3)),
-])
-@pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_SIDE_RDO, RP.RV_REPLAY_SPLIT_RDO,
-                                   RP.RV_REPLAY_EXHAUSTIVE_FS])
-def test_gpu_replay_matches_cpu_replay(w, h, xdec, ydec, bd, refs, tile, flags):
+def test_gpu_synth_equals_numpy_twin():
     import rav1e_amd as R
     R.require_device(0)
-    fr = _frames(w, h, xdec, ydec, bd, refs + 1)
-    g = RP.HipReplay(w, h, xdec, ydec, bd, refs, tile=tile, flags=flags)
-    c = O.CpuReplay(w, h, xdec, ydec, bd, refs, tile=tile, threads=4)
-    for s, f in enumerate(fr):
-        g.set_frame(s, f)
-        c.set_frame(s, f)
-    for scale in (1, 2, 4):
-        g.frame(scale)
-        c.frame(scale)
+    for (w, h, xd, yd, bd) in [(200, 120, 1, 1, 8), (136, 72, 0, 0, 10), (64, 48, 1, 1, 12)]:
+        g = RP.HipReplay(w, h, xd, yd, bd, 1, n_inputs=3)
+        g.synth_inputs(5)
+        for i in range(3):
+            np.testing.assert_array_equal(g.get_input(i), RP.synth_frame(w, h, 5 + i, xd, yd, bd))
+        g.close()
+
+
+def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=None, quantizer=100):
+    import rav1e_amd as R
+    R.require_device(0)
+    t = RP.tiling_for(w, h, **(tiling or {}))
+    ts = (t["tile_width_sb"], t["tile_height_sb"])
+    nin = frames + 8
+    g = RP.HipReplay(w, h, xdec, ydec, bd, refs, tile_size=ts, n_inputs=nin, flags=flags,
+                     quantizer=quantizer)
+    g.synth_inputs(0)
+    c = O.CpuReplay(w, h, xdec, ydec, bd, refs, tile_size=ts, n_inputs=nin,
+                    threads=O.cpu_share(), quantizer=quantizer)
+    for i in range(nin):
+        c.set_input(i, g.get_input(i))
+    if imp is not None:
+        g.set_importances(imp)
+        c.set_importances(imp)
+    for n in range(frames):
+        gi, ci = g.frame(), c.frame()
+        assert gi == ci
         gw, cw = g.results(), c.results()
         bad = np.nonzero(gw != cw)[0]
-        assert bad.size == 0, (scale, bad[:10], gw[bad[:10]], cw[bad[:10]])
-    assert len(g.stage_ms()) == 10
+        assert bad.size == 0, (n, gi, bad[:10], gw[bad[:10]], cw[bad[:10]])
+    np.testing.assert_array_equal(g.get_recon(gi["display"]), c.get_recon(ci["display"]))
+    g.close()
+    c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,xdec,ydec,bd,refs,tiling,flags", [
+    (256, 192, 1, 1, 8, 2, None, 0),
+    (320, 128, 0, 0, 8, 1, None, 0),
+    (256, 128, 1, 1, 10, 2, None, 0),
+    (192, 128, 1, 1, 12, 1, None, 0),  # 12 bits: exhaustive full search, 12-bit RDO kernel
+    (384, 192, 1, 1, 8, 2, {"tile_cols": 2}, 0),
+    (384, 256, 0, 0, 8, 2, {"tiles": 4}, 0),
+    (256, 192, 1, 1, 8, 2, None, RP.RV_REPLAY_EXHAUSTIVE_FS),
+])
+def test_gpu_replay_matches_cpu_replay(w, h, xdec, ydec, bd, refs, tiling, flags):
+    _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, 10, tiling, flags)
+
+
+@pytest.mark.gpu
+def test_gpu_replay_importance_bias_and_quantizer():
+    w, h = 256, 192
+    rng = np.random.default_rng(3)
+    imp = rng.random((h // 8) * (w // 8)).astype(np.float32) * 7
+    _gpu_vs_cpu(w, h, 1, 1, 8, 2, 6, imp=imp, quantizer=60)
+
+
+@pytest.mark.gpu
+def test_gpu_tile_groups_exchange():
+    """Two GPU tile groups in one process, exchanging reconstructions
+    through their device exchange buffers (the RCCL all-gather's layout),
+    reproduce the CPU replay of the whole frame."""
+    import ctypes as C
+
+    import rav1e_amd as R
+    R.require_device(0)
+    w, h = 384, 192
+    t = RP.tiling_for(w, h, tile_cols=2)
+    ts = (t["tile_width_sb"], t["tile_height_sb"])
+    rects = RP.tile_groups(t, 2)
+    gs = [RP.HipReplay(w, h, group=r, tile_size=ts, n_inputs=14) for r in rects]
+    for k, g in enumerate(gs):
+        g.synth_inputs(0)
+        g.set_groups(rects, k, None)
+    c = O.CpuReplay(w, h, tile_size=ts, n_inputs=14, threads=4)
+    for i in range(14):
+        c.set_input(i, RP.synth_frame(w, h, i))
+    L = R.lib()
+    bufs = [g.exchange_buffers() for g in gs]
+    nb = bufs[0][2]
+    sbc = (w + 63) // 64
+    for n in range(7):
+        for g in gs:
+            g.frame()
+        c.frame()
+        R._check(L.rv_device_sync(), "sync")  # the packs ran on the replay streams
+        for k in range(2):  # all-gather: group j's send -> slot j of every recv
+            for j in range(2):
+                R._check(L.rv_memcpy_d2d(C.c_void_p(bufs[k][1] + j * nb), C.c_void_p(bufs[j][0]),
+                                         nb, None), "rv_memcpy_d2d")
+        R._check(L.rv_device_sync(), "sync")
+        for g in gs:
+            g.import_()
+        cw = c.results()
+        sw = _sb_words(cw, len(cw) // 20, 2)
+        for g, (x0, y0, gw_, gh_) in zip(gs, rects):
+            wg = g.results()
+            gsb = _sb_words(wg, gw_ * gh_, 2)
+            for sb in range(gw_ * gh_):
+                np.testing.assert_array_equal(gsb[sb], sw[(y0 + sb // gw_) * sbc + x0 + sb % gw_])
+            assert wg[-1] == cw[-1]
+    for g in gs:
+        g.close()
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("config", ["1080p", "2160p", "2160p10", "2160p444"])
 def test_gpu_replay_full_size_gop(config):
-    """One GOP (me_range_scale 4, 2, 1, 1) at the BASELINE shapes, GPU words
-    equal to the CPU replay's frame by frame."""
+    """The key frame and one GOP (me_range_scale 4, 2, 1, 1) at the BASELINE
+    shapes and tilings, GPU words equal to the CPU replay's frame by frame."""
     import bench
-    import rav1e_amd as R
-    R.require_device(0)
-    w, h, xdec, ydec, bd = bench.CONFIGS[config]
-    fr = _frames(w, h, xdec, ydec, bd, 3)
-    g = RP.HipReplay(w, h, xdec, ydec, bd, 2)
-    c = O.CpuReplay(w, h, xdec, ydec, bd, 2, threads=O.cpu_share())
-    for s, f in enumerate(fr):
-        g.set_frame(s, f)
-        c.set_frame(s, f)
-    for i, scale in enumerate(RP.GOP_SCALES):
-        g.frame(scale)
-        c.frame(scale)
-        gw, cw = g.results(), c.results()
-        bad = np.nonzero(gw != cw)[0]
-        assert bad.size == 0, (config, i, scale, bad[:10], gw[bad[:10]], cw[bad[:10]])
-    g.close()
-    c.close()
+    w, h, xdec, ydec, bd, tk, _ = bench.CONFIGS[config]
+    _gpu_vs_cpu(w, h, xdec, ydec, bd, 2, 5, tk)
