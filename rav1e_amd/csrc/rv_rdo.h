@@ -33,7 +33,9 @@ struct RdoArgs {
   const RdoWinner *win;     // commit: per superblock
   const float *imp;         // block_importances (w_imp per row), may be null
   int w_in_b, h_in_b, w_imp;
-  int n_tx;            // transform blocks per plane in this launch
+  int n_tx;            // transform blocks per plane in this launch (the grid's size)
+  const int32_t *list;  // score: the valid candidates (c * nsb + sb), compacted on
+  const int32_t *count; //   the device; the launch covers count * ntx_per_cand blocks
   int commit;          // 0: score every candidate, 1: commit the winners
   int ntx_per_cand;    // transform blocks per candidate
   int bd;

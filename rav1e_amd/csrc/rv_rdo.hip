@@ -92,14 +92,23 @@ struct RdoJob {
   int cf, rf;        // 1/16-pel fracs
   int ref;           // reference index
   bool zero;         // commit of a skip winner: every level is zero
+  int oi;            // output slot: candidate (or superblock) * ntx_per_cand + block
 };
+
+// Transform blocks of this launch: n_tx, or count * ntx_per_cand for a
+// compacted candidate list.
+__device__ __forceinline__ int rdo_ntx(const RdoArgs &a) {
+  return a.count ? __builtin_amdgcn_readfirstlane(*a.count) * a.ntx_per_cand : a.n_tx;
+}
 
 template <int N>
 __device__ __forceinline__ RdoJob rdo_job(const RdoArgs &a, const RdoPlane &pl, int t) {
-  const int cand = t / a.ntx_per_cand, sub = t - cand * a.ntx_per_cand;
+  const int ci = t / a.ntx_per_cand, sub = t - ci * a.ntx_per_cand;
+  const int cand = a.list ? a.list[ci] : ci;
   int sb, c;
   RdoJob j;
   j.zero = false;
+  j.oi = cand * a.ntx_per_cand + sub;
   if (a.commit) {
     sb = cand;
     c = a.win[sb].c;
@@ -325,7 +334,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   // ---- skip variant: sse_wxh of the prediction ------------------------------
   if (!a.commit) {
     const uint64_t d = group_sum<LPB>(rdo_sse_biased<Px, N, LPB>(a, jb, o, ost, pred));
-    if (valid && lane == 0) pl.out[(int64_t)t * 3 + 0] = d;
+    if (valid && lane == 0) pl.out[(int64_t)jb.oi * 3 + 0] = d;
   }
 
   int s0, s1, s2;
@@ -394,11 +403,11 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     txd = group_sum<LPB>(txd);
     const int bits = 2 * (3 - pl.q.log_tx_scale);
     if (valid && lane == 0)
-      pl.out[(int64_t)t * 3 + 2] =
+      pl.out[(int64_t)jb.oi * 3 + 2] =
           q_estimate_rate(a.qindex, a.tx_size, (txd + (1ull << (bits - 1))) >> bits);
   }
   {
-    int32_t *pk = pl.levels + (int64_t)t * CA;
+    int32_t *pk = pl.levels + (int64_t)jb.oi * CA;
 #pragma unroll 4
     for (int i = lane; i < CA; i += LPB) {
       int32_t *e = buf + (i / N) * S + (i % N);
@@ -458,7 +467,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   }
   // ---- non-skip variant: sse_wxh of the reconstruction ----------------------
   const uint64_t d = group_sum<LPB>(rdo_sse_biased<Px, N, LPB>(a, jb, o, ost, pred));
-  if (valid && lane == 0) pl.out[(int64_t)t * 3 + 1] = d;
+  if (valid && lane == 0) pl.out[(int64_t)jb.oi * 3 + 1] = d;
 }
 
 // ---- luma candidates: 64x64 --------------------------------------------------
@@ -617,7 +626,7 @@ __device__ __forceinline__ void luma_front(const RdoArgs &a, const RdoPlane &pl,
   // ---- skip variant: compute_distortion of the prediction -------------------
   if (!a.commit) {
     const uint64_t d = luma_dist<Px>(a, jb, o, pl.org.stride, pred);
-    if (valid && lane == 0) pl.out[(int64_t)t * 3 + 0] = d;
+    if (valid && lane == 0) pl.out[(int64_t)jb.oi * 3 + 0] = d;
   }
   int s0, s1, s2;
   fwd_shifts<N>((bd - 8) / 2, s0, s1, s2);
@@ -672,11 +681,11 @@ __device__ __forceinline__ void luma_quantize(const RdoArgs &a, const RdoPlane &
     txd = group_sum<64>(txd);
     const int bits = 2 * (3 - pl.q.log_tx_scale);
     if (valid && lane == 0)
-      pl.out[(int64_t)t * 3 + 2] =
+      pl.out[(int64_t)jb.oi * 3 + 2] =
           q_estimate_rate(a.qindex, a.tx_size, (txd + (1ull << (bits - 1))) >> bits);
   }
   wave_sync();
-  int32_t *pk = pl.levels + (int64_t)t * 1024;
+  int32_t *pk = pl.levels + (int64_t)jb.oi * 1024;
 #pragma unroll 4
   for (int i = lane; i < 1024; i += 64) {
     int32_t *e = fmid + (i >> 6) * 65 + (i & 63);
@@ -747,7 +756,7 @@ __device__ __forceinline__ void luma_back(const RdoArgs &a, const RdoPlane &pl, 
   }
   // ---- E. non-skip variant: compute_distortion of the reconstruction -------
   const uint64_t d = luma_dist<Px>(a, jb, plane_ptr<Px>(pl.org, jb.bx, jb.by), pl.org.stride, pred);
-  if (valid && lane == 0) pl.out[(int64_t)t * 3 + 1] = d;
+  if (valid && lane == 0) pl.out[(int64_t)jb.oi * 3 + 1] = d;
 }
 
 // One luma candidate per wavefront (12-bit).
@@ -780,11 +789,13 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
 template <typename Px>
 __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, int32_t *buf,
                                                 Px *pred, const uint16_t *scan) {
-  const int pairs = (chroma.n_tx + 1) / 2;
+  const int pairs = (chroma.n_tx + 1) / 2;  // per plane, for the grid's size
   const int plane = b / pairs;
   const int half = (threadIdx.x & 63) >> 5;
+  const int n = rdo_ntx(chroma);
   int i = 2 * (b - plane * pairs) + half;
-  const bool valid = i < chroma.n_tx;
+  if (i - half >= n) return;  // past the compacted list: the whole pair
+  const bool valid = i < n;
   if (!valid) i -= 1;
   rdo_cand_body<Px, 32, 32>(chroma, chroma.p[plane], i, valid, buf + half * 32 * 33,
                             pred + half * 32 * 32, scan);
@@ -815,6 +826,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void rd
   __shared__ uint16_t scan[1024];
   const int b = blockIdx.x;
   stage_scan(scan, b < luma.n_tx ? luma.q_tx_index : chroma.q_tx_index);
+  if (b < luma.n_tx && b >= rdo_ntx(luma)) return;  // past the compacted list
   if (b < luma.n_tx)
     rdo_luma_body<Px, Mid, 2>(luma, luma.p[0], b, lds,
                               reinterpret_cast<Px *>(lds + L::kScr), scan);
@@ -866,20 +878,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     return reinterpret_cast<Px *>(slot(q) + L::kScr);
   };
   const int t0 = 4 * b, t = t0 + wave;
-  const bool valid = t < luma.n_tx;
-  const RdoJob jb = rdo_job<64>(luma, luma.p[0], valid ? t : luma.n_tx - 1);
+  const int n = rdo_ntx(luma);
+  if (t0 >= n) return;  // past the compacted list (uniform over the workgroup)
+  const bool valid = t < n;
+  const RdoJob jb = rdo_job<64>(luma, luma.p[0], valid ? t : n - 1);
   if (valid) luma_front<Px, NPART>(luma, luma.p[0], t, jb, true, slot(wave), pred(wave));
   __syncthreads();
   if (wave == 0) {  // row DCT: lane = 16 * candidate + raster row
     const int q = lane >> 4;
-    if (t0 + q < luma.n_tx) luma_fwd_row(fmid(q) + (lane & 15) * 65, luma.bd);
+    if (t0 + q < n) luma_fwd_row(fmid(q) + (lane & 15) * 65, luma.bd);
   }
   __syncthreads();
   if (valid) luma_quantize(luma, luma.p[0], t, jb, true, fmid(wave), scan);
   __syncthreads();
   if (wave < 2) {  // inverse rows: lane = 32 * (candidate & 1) + coded row
     const int q = 2 * wave + (lane >> 5), rr = lane & 31;
-    const bool vq = t0 + q < luma.n_tx;
+    const bool vq = t0 + q < n;
     const int range = luma.bd + 8, crange = luma.bd + 6 > 16 ? luma.bd + 6 : 16;
     int32_t v[64];
     if (vq) luma_inv_row_load(fmid(q), rr, v, range, nullptr);

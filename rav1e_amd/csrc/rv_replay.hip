@@ -203,6 +203,29 @@ __global__ __launch_bounds__(64) void score_candidates(
   wd[8 * g.R + 3] = w.dist;
 }
 
+// The valid candidates (cand_mv true) of every superblock, compacted for
+// the F4 launch: rav1e evaluates only the modes it pushes (about half of
+// the 4 per reference on smooth motion: NEWMV often repeats a neighbour's
+// MV).  One thread per candidate c * nsb + sb; wave-aggregated appends
+// (the order of the list does not matter: every output is indexed by the
+// candidate).
+__global__ __launch_bounds__(256) void cand_list_kernel(CandGeo cg, const rv_fs_result *sub,
+                                                         int n, int32_t *list, int32_t *count) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  bool v = false;
+  if (i < n) {
+    rv_mv mv;
+    const int c = i / cg.nsb, sb = i - c * cg.nsb;
+    v = cand_mv(cg, sub, sb, c, &mv);
+  }
+  const uint64_t m = __ballot(v);
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == 0 && m) base = atomicAdd(count, (int)__popcll(m));
+  base = __shfl(base, 0, 64);
+  if (v) list[base + __popcll(m & ((1ull << lane) - 1))] = i;
+}
+
 // F5: get_satd of every 8x8 luma block of the group inside the frame
 // against reference 0 at the full-pel part of its superblock's NEWMV
 // (compute_block_importances, src/api/internal.rs:823-1010) plus its
@@ -313,6 +336,7 @@ struct rv_replay {
   rv_ds_job *jobs_half[3], *jobs_full[3], *jobs_sub[3];  // per level
   uint64_t *l_out, *c_out;  // F4: [skip dist, non-skip dist, rate] per transform block
   RdoWinner *win;
+  int32_t *cand_list, *cand_count;  // F4: the valid candidates
   int32_t *l_lev, *c_lev;   // F6: committed levels
   uint64_t *words;
   unsigned long long *tail;  // [levels csum, group recon sum, imp satd sum, -, frame recon sum]
@@ -673,6 +697,8 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->l_out = (uint64_t *)dalloc(r, (size_t)nc * 3 * 8);
   r->c_out = (uint64_t *)dalloc(r, (size_t)nc * r->ntx_c * 3 * 8 * 2);
   r->win = (RdoWinner *)dalloc(r, (size_t)g.nsb * sizeof(RdoWinner));
+  r->cand_list = (int32_t *)dalloc(r, (size_t)nc * 4);
+  r->cand_count = (int32_t *)dalloc(r, 4);
   r->l_lev = (int32_t *)dalloc(r, (size_t)g.nsb * 1024 * 4);
   r->c_lev = (int32_t *)dalloc(r, (size_t)g.nsb * r->ntx_c * 1024 * 4 * 2);
   r->words = (uint64_t *)dalloc(r, (size_t)g.nsb * (8 * g.R + 4) * 8);
@@ -681,6 +707,7 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->n_imp = r->imp_bx * r->imp_by;
   r->tail = (unsigned long long *)dalloc(r, 5 * 8);
   ok = ok && r->coarse && r->half && r->full && r->sub && r->l_out && r->c_out && r->win &&
+       r->cand_list && r->cand_count &&
        r->l_lev && r->c_lev && r->words && r->tail;
   if (ok) {
     ok = hipMemsetAsync(r->words, 0, (size_t)g.nsb * (8 * g.R + 4) * 8, r->stream) == hipSuccess &&
@@ -856,7 +883,8 @@ int rv_replay_exchange_buffers(rv_replay *r, void **send, void **recv, size_t *b
 // then a complete reference on this rank (src/encoder.rs:3411-3429).
 int rv_replay_import(rv_replay *r) {
   if (!r) return rv_set_error(RV_EINVAL, "rv_replay_import: null");
-  if (r->n_groups < 2) return RV_OK;
+  // one group, or the key frame (every rank copied its own input): nothing to move
+  if (r->n_groups < 2 || r->last.is_key) return RV_OK;
   const RvSlot &s = r->slots[r->last.display % kSlots];
   XRect rects[3 * kMaxGroups];
   int n = 0;
@@ -950,8 +978,12 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   RV_EV(4);
   RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
                                r->sub, ev_sub, nullptr, st));
+  // the valid candidates (a few microseconds; bracketed with F3 sub-pel)
+  RV_H(hipMemsetAsync(r->cand_count, 0, 4, st));
+  cand_list_kernel<<<(g.nsb * g.C + 255) / 256, 256, 0, st>>>(r->cg, r->sub, g.nsb * g.C,
+                                                              r->cand_list, r->cand_count);
   RV_EV(5);
-  // F4 every candidate, luma + both chroma planes in one fused launch
+  // F4 every valid candidate, luma + both chroma planes in one fused launch
   RdoArgs la, ca;
   memset(&la, 0, sizeof(la));
   la.p[0].org = cur.y;
@@ -967,6 +999,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   la.h_in_b = g.h_in_b;
   la.w_imp = g.w_imp;
   la.n_tx = g.nsb * g.C;
+  la.list = r->cand_list;
+  la.count = r->cand_count;
   la.ntx_per_cand = 1;
   la.bd = g.bd;
   la.mb_w = la.mb_h = kSb;
@@ -1006,6 +1040,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   RV_EV(7);
   // F6 commit the winners into the frame
   la.commit = ca.commit = 1;
+  la.list = ca.list = nullptr;
+  la.count = ca.count = nullptr;
   la.n_tx = g.nsb;
   ca.n_tx = g.nsb * ntx_c;
   la.ntx_per_cand = 1;
