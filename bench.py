@@ -81,8 +81,9 @@ ROCPROF_NAMES = {
     "full_search": "fs16_sea_kernel_{pxs}",
     "diamond_fullpel_64": "ds_fast_kernel<{px}, 64, 64, false>",
     "diamond_subpel_64": "ds_fast_kernel<{px}, 64, 64, true>",
-    "rdo_candidates": "rdo_quad_kernel<{px}, false>",
-    "rdo_commit": "rdo_quad_kernel<{px}, true>",
+    "rdo_candidates": "rdo_quad_kernel<{px}, 0>",
+    "rdo_compound": "rdo_quad_kernel<{px}, 1>",
+    "rdo_commit": "rdo_quad_kernel<{px}, 2>",
 }
 
 
@@ -245,7 +246,7 @@ def main():
     k = min(sum(1 for f in nonkey if (f // gop) % TIMING_STRIDE == 0), 64)
     k = max(k, 1)
     ms = hip.stage_ms_sum(k) / k  # per frame
-    ev_full, ev_sub, ev_frames = (int(v) for v in hip.counters())
+    ev_full, ev_sub, ev_frames, n_single, n_comp = (int(v) for v in hip.counters())
     ev_frames = max(1, ev_frames)
     gx0, gy0, gw, gh = rects[rank]
     nsb = gw * gh
@@ -258,13 +259,16 @@ def main():
                        for nx, ny in coarse_windows(W, H, nref, s, tiling, rects[rank]))
                    for s in RP.GOP_SCALES) / 4.0
     nj = nsb * nref
-    ncand = nsb * nref * 4  # every candidate of every superblock
     cw, ch = 64 >> xdec, 64 >> ydec
     ntx_c = (cw // 32) * (ch // 32)
-    # per candidate: luma (64+7)^2 window + 64x64 source + 3 result words;
-    # per chroma 32x32 transform block the same at 32 (U and V)
-    rdo_bytes = float(ncand * ((71 * 71 + 64 * 64) * px + 24) +
-                      2 * ncand * ntx_c * ((39 * 39 + 32 * 32) * px + 24))
+    # F4 per evaluated candidate (the measured counts): luma (64+7)^2 window
+    # (two for compound) + 64x64 source + 3 result words; per chroma 32x32
+    # transform block the same at 32 (U and V)
+    ns, nc = n_single / ev_frames, n_comp / ev_frames
+    rdo_bytes = float(ns * ((71 * 71 + 64 * 64) * px + 24) +
+                      nc * ((2 * 71 * 71 + 64 * 64) * px + 24) +
+                      2 * ntx_c * (ns * ((39 * 39 + 32 * 32) * px + 24) +
+                                   nc * ((2 * 39 * 39 + 32 * 32) * px + 24)))
     # commit: one candidate per superblock, + levels and the reconstruction
     commit_bytes = float(nsb * ((71 * 71 + 2 * 64 * 64) * px + 4096 + 16) +
                          2 * nsb * ntx_c * ((39 * 39 + 2 * 32 * 32) * px + 4096))
@@ -324,6 +328,8 @@ def main():
             "full_search_path": "successive elimination" if sea else "exhaustive",
             "diamond_evals_per_frame": [round(ev_full / ev_frames, 1),
                                         round(ev_sub / ev_frames, 1)],
+            "rdo_candidates_per_frame": {"single_ref": round(ns, 1), "compound": round(nc, 1),
+                                         "variants": "skip + non-skip each"},
             "checksum": int(words[-5]) & 0xFFFFFFFF,
         }
         print(json.dumps(line), flush=True)

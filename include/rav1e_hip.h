@@ -425,6 +425,8 @@ typedef struct rv_replay_frame_info {
   int32_t level;              /* pyramid level */
   int32_t is_key;             /* 1: the key frame (input taken as recon) */
   int32_t ref_display[2];     /* display index of each reference */
+  int32_t compound;           /* 1: compound candidates (reference_mode SELECT
+                               * with a forward and a backward reference) */
 } rv_replay_frame_info;
 /* The frame parameters of one pyramid level (FrameInvariants::
  * set_quantizers, src/encoder.rs:865-880): base_q_idx, per-plane dc / ac
@@ -505,9 +507,10 @@ int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
  * (<= 64). */
 int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,
                               int cap);
-/* Diamond-search candidate evaluations summed over the last min(frames, 64)
- * frames: out[0] F3 full-pel 64x64, out[1] F3 sub-pel 64x64, out[2] = the
- * number of frames summed (cap >= 3). */
+/* Candidate evaluations summed over the last min(frames, 64) coded frames:
+ * out[0] F3 full-pel 64x64 diamond, out[1] F3 sub-pel 64x64 diamond, out[2]
+ * = the number of frames summed (cap >= 3); with cap >= 5, out[3] / out[4]
+ * the F4 single-reference / compound RDO candidates.  Returns the count. */
 int rv_replay_counters(rv_replay *r, uint64_t *out, int cap);
 
 /* ---------------------------------------------------------------------

@@ -46,7 +46,7 @@ typedef struct {
 } oinput;
 
 typedef struct {
-  int display, me_range_scale, level, is_key, ref_display[2];
+  int display, me_range_scale, level, is_key, ref_display[2], compound;
 } orc_frame_info; /* = rv_replay_frame_info */
 
 typedef struct orc_replay {
@@ -165,6 +165,42 @@ static int cand_mv(const orc_replay *r, int sb, int c, orc_mv *mv) {
       return !(n >= 1 && mv_eq(st[0], me)) && !(n >= 2 && mv_eq(st[1], me)) &&
              (me.row != 0 || me.col != 0);
     }
+  }
+}
+
+/* rv_chain.h comp_mvs: RAV1E_INTER_COMPOUND_MODES (src/predict.rs:51-58)
+ * GLOBAL_GLOBALMV, NEAREST_NEARESTMV, NEW_NEWMV, NEAREST_NEWMV,
+ * NEW_NEARESTMV, NEAR_NEARMV over the (ref 0, ref 1) stack of the above /
+ * left neighbours' NEWMV pairs, merged if equal (src/rdo.rs:952-992) */
+static void comp_mvs(const orc_replay *r, int sb, int m, orc_mv *mv0, orc_mv *mv1) {
+  int sx = sb % r->tw, sy = sb / r->tw, fx = r->tx0 + sx, fy = r->ty0 + sy;
+  const orc_mv *s0 = r->sub, *s1 = r->sub + r->nsb;
+  orc_mv zero = {0, 0}, e[2][2] = {{zero, zero}, {zero, zero}};
+  int n = 0;
+  if (fy % r->ths) {
+    e[0][0] = s0[sb - r->tw];
+    e[0][1] = s1[sb - r->tw];
+    n = 1;
+  }
+  if (fx % r->tws) {
+    orc_mv l0 = s0[sb - 1], l1 = s1[sb - 1];
+    if (n == 0 || !mv_eq(l0, e[0][0]) || !mv_eq(l1, e[0][1])) {
+      e[n][0] = l0;
+      e[n][1] = l1;
+      n++;
+    }
+  }
+  orc_mv me0 = s0[sb], me1 = s1[sb];
+  switch (m) {
+    case 0: *mv0 = zero; *mv1 = zero; break;
+    case 1: *mv0 = e[0][0]; *mv1 = e[0][1]; break;
+    case 2: *mv0 = me0; *mv1 = me1; break;
+    case 3: *mv0 = e[0][0]; *mv1 = me1; break;
+    case 4: *mv0 = me0; *mv1 = e[0][1]; break;
+    default:
+      *mv0 = n >= 2 ? e[1][0] : zero;
+      *mv1 = n >= 2 ? e[1][1] : zero;
+      break;
   }
 }
 
@@ -341,6 +377,28 @@ static void predict(const orc_replay *r, const oplane *ref, int po_x, int po_y, 
   int qy = clamp_i32(po_y + roff - 3, -ref->yo, ref->h) + 3;
   orc_put_8tap(dst, dst_stride, at(ref, r->hbd, qx, qy), ref->stride, w, h, cf, rf, 0, 0, r->bd,
                r->hbd, 0);
+}
+
+/* compound predict_inter (src/predict.rs:300-338): prep_8tap of both
+ * references, mc_avg */
+static void predict_comp(const orc_replay *r, const oplane *ref0, const oplane *ref1, int po_x,
+                         int po_y, orc_mv mv0, orc_mv mv1, int w, int h, void *dst,
+                         int dst_stride) {
+  int16_t tmp[2][SB * SB];
+  const oplane *rf[2] = {ref0, ref1};
+  orc_mv mv[2] = {mv0, mv1};
+  for (int i = 0; i < 2; i++) {
+    const oplane *ref = rf[i];
+    int ys = 3 + ref->ydec, xs = 3 + ref->xdec;
+    int roff = (int)mv[i].row >> ys, coff = (int)mv[i].col >> xs;
+    int rfr = ((int)mv[i].row - (roff << ys)) << (4 - ys);
+    int cfr = ((int)mv[i].col - (coff << xs)) << (4 - xs);
+    int qx = clamp_i32(po_x + coff - 3, -ref->xo, ref->w) + 3;
+    int qy = clamp_i32(po_y + roff - 3, -ref->yo, ref->h) + 3;
+    orc_prep_8tap(tmp[i], at(ref, r->hbd, qx, qy), ref->stride, w, h, cfr, rfr, 0, 0, r->bd,
+                  r->hbd);
+  }
+  orc_mc_avg(dst, dst_stride, tmp[0], tmp[1], w, h, r->bd, r->hbd, 0);
 }
 
 static void ds_ctx(const orc_replay *r, orc_ds_ctx *c, const oplane *org, const oplane *ref,
@@ -540,13 +598,22 @@ static void run_rdo(orc_replay *r, int sb, uint64_t tail[3]) {
   double best = 1.7976931348623157e308;
   int best_c = 0, best_skip = 0;
   uint64_t best_d = 0;
-  for (int c = 0; c < r->C; c++) {
+  const int ncand = r->C + (r->fi.compound ? 6 : 0);
+  for (int c = 0; c < ncand; c++) {
     orc_mv mv;
-    if (!cand_mv(r, sb, c, &mv)) continue;
-    const oslot *rf = ref[c / NMODE];
-    predict(r, &rf->y, ppx, ppy, mv, SB, SB, ly, SB);
-    predict(r, &rf->u, cpx, cpy, mv, cwid, chei, lu, cwid);
-    predict(r, &rf->v, cpx, cpy, mv, cwid, chei, lv, cwid);
+    if (c < r->C) {
+      if (!cand_mv(r, sb, c, &mv)) continue;
+      const oslot *rf = ref[c / NMODE];
+      predict(r, &rf->y, ppx, ppy, mv, SB, SB, ly, SB);
+      predict(r, &rf->u, cpx, cpy, mv, cwid, chei, lu, cwid);
+      predict(r, &rf->v, cpx, cpy, mv, cwid, chei, lv, cwid);
+    } else {
+      orc_mv m0, m1;
+      comp_mvs(r, sb, c - r->C, &m0, &m1);
+      predict_comp(r, &ref[0]->y, &ref[1]->y, ppx, ppy, m0, m1, SB, SB, ly, SB);
+      predict_comp(r, &ref[0]->u, &ref[1]->u, cpx, cpy, m0, m1, cwid, chei, lu, cwid);
+      predict_comp(r, &ref[0]->v, &ref[1]->v, cpx, cpy, m0, m1, cwid, chei, lv, cwid);
+    }
     /* skip: the prediction is the reconstruction */
     uint64_t ds = sb_distortion(r, cur, ppx, ppy, ly, lu, lv);
     int zero_dist = 0;
@@ -664,6 +731,9 @@ static void frame_info(long n, int R, orc_frame_info *f) {
     long d = 4 * g + rf[j][k];
     f->ref_display[k] = (int)(d < 0 ? 0 : d);
   }
+  /* reference_mode SELECT with a forward and a backward reference
+   * (src/encoder.rs:832-836, src/rdo.rs:914-941) */
+  f->compound = R == 2 && (j == 1 || j == 3);
 }
 
 /* Code the next frame.  sb_limit > 0 runs only the first sb_limit

@@ -89,7 +89,7 @@ class RvReplayLevelParams(C.Structure):
 
 class RvReplayFrameInfo(C.Structure):
     _fields_ = [("display", C.c_int32), ("me_range_scale", C.c_int32), ("level", C.c_int32),
-                ("is_key", C.c_int32), ("ref_display", C.c_int32 * 2)]
+                ("is_key", C.c_int32), ("ref_display", C.c_int32 * 2), ("compound", C.c_int32)]
 
 
 # ---- reference enums ----------------------------------------------------

@@ -79,8 +79,9 @@ __device__ inline void chain_emit(const ChainNext &c, int job, int n_per_ref, in
 // 49-126) at superblock (tx0, ty0) of the frame, tw x th superblocks.
 struct CandGeo {
   int nsb, tw, th, tx0, ty0, tws, ths;
-  int R;  // references searched
-  int M;  // inter modes per reference (kCandModes)
+  int R;     // references searched
+  int M;     // inter modes per reference (kCandModes)
+  int comp;  // compound candidates after the R * M single ones (0 or kCompModes)
 };
 
 // Per reference, rav1e pushes (src/rdo.rs:880-905, speed 10: no near MVs
@@ -90,6 +91,13 @@ struct CandGeo {
 // non-skip unless skip had zero distortion (luma_chroma_mode_rdo, :649-700).
 // GLOBALMV is the zero MV (no global motion).
 enum CandMode { kNearestMv = 0, kNear0Mv = 1, kGlobalMv = 2, kNewMv = 3, kCandModes = 4 };
+// RAV1E_INTER_COMPOUND_MODES (src/predict.rs:51-58), pushed for the
+// (forward, backward) reference pair when the frame's reference_mode is
+// SELECT (src/rdo.rs:914-941, src/encoder.rs:832-836)
+enum CompMode {
+  kGlobalGlobal = 0, kNearestNearest = 1, kNewNew = 2, kNearestNew = 3, kNewNearest = 4,
+  kNearNear = 5, kCompModes = 6
+};
 
 __host__ __device__ inline bool mv_eq(rv_mv a, rv_mv b) { return a.row == b.row && a.col == b.col; }
 
@@ -118,8 +126,74 @@ __host__ __device__ inline int cand_stack(const CandGeo &g, const rv_fs_result *
   return left ? 1 : 0;
 }
 
+// The compound MV stack of (reference 0, reference 1): the above and left
+// neighbours' (NEWMV 0, NEWMV 1) pairs, merged if equal (the same
+// neighbour-NEWMV stand-in as cand_stack).  Entries in scalars (no
+// scratch on the device); returns the count.
+__host__ __device__ inline int comp_stack(const CandGeo &g, const rv_fs_result *sub, int sb,
+                                          rv_mv &e00, rv_mv &e01, rv_mv &e10, rv_mv &e11) {
+  const int sx = sb % g.tw, sy = sb / g.tw;
+  const int fx = g.tx0 + sx, fy = g.ty0 + sy;
+  const bool up = fy % g.ths != 0, left = fx % g.tws != 0;
+  const rv_mv zero{0, 0};
+  const rv_mv a0 = up ? sub[sb - g.tw].best_mv : zero, a1 = up ? sub[g.nsb + sb - g.tw].best_mv : zero;
+  const rv_mv l0 = left ? sub[sb - 1].best_mv : zero, l1 = left ? sub[g.nsb + sb - 1].best_mv : zero;
+  e10 = e11 = zero;
+  if (up) {
+    e00 = a0;
+    e01 = a1;
+    if (left && (!mv_eq(l0, a0) || !mv_eq(l1, a1))) {
+      e10 = l0;
+      e11 = l1;
+      return 2;
+    }
+    return 1;
+  }
+  e00 = l0;
+  e01 = l1;
+  return left ? 1 : 0;
+}
+
+// The two MVs of compound candidate m of superblock sb (rdo_mode_decision's
+// mvs for the compound modes, src/rdo.rs:952-992; an empty stack reads as
+// zero MVs).  Always pushed.
+__host__ __device__ inline void comp_mvs(const CandGeo &g, const rv_fs_result *sub, int sb, int m,
+                                         rv_mv *mv0, rv_mv *mv1) {
+  rv_mv e00, e01, e10, e11;
+  const int n = comp_stack(g, sub, sb, e00, e01, e10, e11);
+  const rv_mv zero{0, 0};
+  const rv_mv me0 = sub[sb].best_mv, me1 = sub[g.nsb + sb].best_mv;
+  const rv_mv n00 = n >= 1 ? e00 : zero, n01 = n >= 1 ? e01 : zero;
+  switch (m) {
+    case kGlobalGlobal:
+      *mv0 = *mv1 = zero;
+      break;
+    case kNearestNearest:
+      *mv0 = n00;
+      *mv1 = n01;
+      break;
+    case kNewNew:
+      *mv0 = me0;
+      *mv1 = me1;
+      break;
+    case kNearestNew:
+      *mv0 = n00;
+      *mv1 = me1;
+      break;
+    case kNewNearest:
+      *mv0 = me0;
+      *mv1 = n01;
+      break;
+    default:  // kNearNear
+      *mv0 = n >= 2 ? e10 : zero;
+      *mv1 = n >= 2 ? e11 : zero;
+      break;
+  }
+}
+
 // MV of candidate c = k * M + m of superblock sb; false if rav1e would not
-// push that mode (rdo_mode_decision's inter_mode_set).
+// push that mode (rdo_mode_decision's inter_mode_set).  Compound
+// candidates (c >= R * M) are handled by comp_mvs.
 __host__ __device__ inline bool cand_mv(const CandGeo &g, const rv_fs_result *sub, int sb, int c,
                                         rv_mv *mv) {
   const int k = c / g.M, m = c - k * g.M;

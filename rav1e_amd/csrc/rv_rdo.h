@@ -34,6 +34,7 @@ struct RdoArgs {
   const float *imp;         // block_importances (w_imp per row), may be null
   int w_in_b, h_in_b, w_imp;
   int n_tx;            // transform blocks per plane in this launch (the grid's size)
+  int cand_base;       // score without a list: candidate = cand_base + task / ntx_per_cand
   const int32_t *list;  // score: the valid candidates (c * nsb + sb), compacted on
   const int32_t *count; //   the device; the launch covers count * ntx_per_cand blocks
   int commit;          // 0: score every candidate, 1: commit the winners
@@ -56,4 +57,4 @@ int rv_quant_ctx(int qindex, int tx_area, int is_intra, int bit_depth, int dc_de
 // Luma candidates (64x64 transform, cdef distortion) and the chroma
 // transform blocks of planes U and V (32x32, SSE) in one launch.
 int rv_rdo_candidates(const rv::RdoArgs &luma, const rv::RdoArgs &chroma, int hbd,
-                      hipStream_t s);
+                      hipStream_t s, bool compound = false);

@@ -91,6 +91,8 @@ struct RdoJob {
   int src_x, src_y;  // predict_inter's clamped integer source position
   int cf, rf;        // 1/16-pel fracs
   int ref;           // reference index
+  bool comp;         // compound: prep_8tap of references 0 and 1, mc_avg
+  int src2_x, src2_y, cf2, rf2;  // compound: reference 1's source and fracs
   bool zero;         // commit of a skip winner: every level is zero
   int oi;            // output slot: candidate (or superblock) * ntx_per_cand + block
 };
@@ -104,7 +106,7 @@ __device__ __forceinline__ int rdo_ntx(const RdoArgs &a) {
 template <int N>
 __device__ __forceinline__ RdoJob rdo_job(const RdoArgs &a, const RdoPlane &pl, int t) {
   const int ci = t / a.ntx_per_cand, sub = t - ci * a.ntx_per_cand;
-  const int cand = a.list ? a.list[ci] : ci;
+  const int cand = a.list ? a.list[ci] : a.cand_base + ci;
   int sb, c;
   RdoJob j;
   j.zero = false;
@@ -117,9 +119,15 @@ __device__ __forceinline__ RdoJob rdo_job(const RdoArgs &a, const RdoPlane &pl, 
     c = cand / a.g.nsb;
     sb = cand - c * a.g.nsb;
   }
-  rv_mv mv;
-  (void)cand_mv(a.g, a.sub, sb, c, &mv);
-  j.ref = c / a.g.M;
+  rv_mv mv, mv1{0, 0};
+  j.comp = c >= a.g.R * a.g.M;
+  if (j.comp) {
+    comp_mvs(a.g, a.sub, sb, c - a.g.R * a.g.M, &mv, &mv1);
+    j.ref = 0;
+  } else {
+    (void)cand_mv(a.g, a.sub, sb, c, &mv);
+    j.ref = c / a.g.M;
+  }
   const int sx = sb % a.g.tw, sy = sb / a.g.tw;
   j.bx = ((a.g.tx0 + sx) * 64) >> a.xdec;
   j.by = ((a.g.ty0 + sy) * 64) >> a.ydec;
@@ -131,7 +139,147 @@ __device__ __forceinline__ RdoJob rdo_job(const RdoArgs &a, const RdoPlane &pl, 
   j.src_y = m.src_y;
   j.cf = m.col_frac;
   j.rf = m.row_frac;
+  j.src2_x = j.src2_y = j.cf2 = j.rf2 = 0;
+  if (j.comp) {
+    const rv_mc_job m1 = mc_job_for(pl.ref[1], j.bx, j.by, mv1, 0, 0);
+    j.src2_x = m1.src_x;
+    j.src2_y = m1.src_y;
+    j.cf2 = m1.col_frac;
+    j.rf2 = m1.row_frac;
+  }
   return j;
+}
+
+// ---- compound prediction: prep_8tap x 2 + mc_avg (src/predict.rs:300-338,
+// src/mc.rs:310-408) ----------------------------------------------------------
+// REGULAR filter setup of one reference: packed horizontal taps (u8: all 8
+// as i8 for two v_dot4; u16: taps 1..6 as i16 pairs), vertical taps.
+struct McF {
+  uint32_t xp[3];
+  int xsum;
+  int yt[8];
+  int cf, rf;
+};
+template <typename Px>
+__device__ __forceinline__ McF mc_setup(int cf, int rf, int w, int h) {
+  McF f;
+  f.cf = cf;
+  f.rf = rf;
+  const int8_t *xf = kRdoReg[w <= 4][cf];
+  const int8_t *yf = kRdoReg[h <= 4][rf];
+#pragma unroll
+  for (int k = 0; k < 8; k++) f.yt[k] = yf[k];
+  f.xsum = 0;
+  if constexpr (sizeof(Px) == 1) {
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+      f.xp[q] = (uint32_t)(uint8_t)xf[4 * q] | ((uint32_t)(uint8_t)xf[4 * q + 1] << 8) |
+                ((uint32_t)(uint8_t)xf[4 * q + 2] << 16) | ((uint32_t)(uint8_t)xf[4 * q + 3] << 24);
+#pragma unroll
+    for (int k = 0; k < 8; k++) f.xsum += xf[k];
+    f.xp[2] = 0;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 3; q++)
+      f.xp[q] = (uint32_t)(uint16_t)(int16_t)xf[2 * q + 1] |
+                ((uint32_t)(uint16_t)(int16_t)xf[2 * q + 2] << 16);
+  }
+  return f;
+}
+// The horizontal pass of window row `row` (staged like the single-reference
+// MC: u8 as i8 = px - 128) at column col: i16 round_shift(sum, 7 - ib), or
+// the pixel when the column frac is 0.
+template <typename Px>
+__device__ __forceinline__ int32_t mc_h(const McF &f, const uint32_t *row, int col, int ib) {
+  if constexpr (sizeof(Px) == 1) {
+    const int d0 = col >> 2, sh = col & 3;
+    const uint32_t w0 = row[d0], w1 = row[d0 + 1], w2 = row[d0 + 2];
+    const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    if (!f.cf) return (int32_t)((lo >> 24) ^ 0x80u);
+    int32_t s = dot4_i8(lo, f.xp[0], 128 * f.xsum);
+    s = dot4_i8(hi, f.xp[1], s);
+    return (int32_t)(int16_t)round_shift(s, 7 - ib);
+  } else {
+    const int c1 = col + 1, d0 = c1 >> 1, sh = (c1 & 1) * 2;  // pixels col+1 .. col+6
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) w[k] = row[d0 + k];
+    uint32_t pp[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) pp[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+    if (!f.cf) return (int32_t)(pp[1] & 0xffffu);  // pixel col + 3
+    int32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) s = dot2_i16(pp[k], f.xp[k], s);
+    return (int32_t)(int16_t)round_shift(s, 7 - ib);
+  }
+}
+// prep_8tap's output for ring position u (ring[j & 7] = h-pass of window
+// row j): (0,0) px << ib; (x,0) the h-pass; (0,y) round_shift(sum, 7 - ib);
+// (x,y) round_shift(sum, 7) -- REGULAR taps 0 and 7 are zero.
+__device__ __forceinline__ int32_t mc_prep_v(const McF &f, const int32_t *ring, int u, int ib) {
+  if (f.rf) {
+    int32_t s = 0;
+#pragma unroll
+    for (int k = 1; k < 7; k++) s += __mul24(f.yt[k], ring[(u + k) & 7]);
+    return round_shift(s, f.cf ? 7 : 7 - ib);
+  }
+  return f.cf ? ring[(u + 3) & 7] : ring[(u + 3) & 7] << ib;
+}
+
+// Compound prediction of an N x N block (lane = column) into pred, in bands
+// of RB rows whose two windows (references 0 and 1) are staged in `win`;
+// mc_avg = clamp(round_shift(t0 + t1, ib + 1)).  Ends with a wave sync.
+template <typename Px, int N, int RB>
+__device__ __forceinline__ void mc_compound(const RdoArgs &a, const RdoPlane &pl, const RdoJob &jb,
+                                            uint32_t *win, Px *pred) {
+  constexpr int B = (int)sizeof(Px);
+  constexpr int P = B == 1 ? ((N + 8 + 15) / 16) * 16 : ((2 * (N + 8) + 15) / 16) * 16;
+  constexpr int kRowDw = ((N + 7) * B + 3) / 4, kTot = (RB + 7) * kRowDw;
+  static_assert(RB % 8 == 0 && N % RB == 0, "bands of whole 8-row groups");
+  const int col = threadIdx.x & (N - 1);
+  const int ib = a.bd == 12 ? 2 : 4, maxv = (1 << a.bd) - 1;
+  const McF f0 = mc_setup<Px>(jb.cf, jb.rf, a.mb_w, a.mb_h);
+  const McF f1 = mc_setup<Px>(jb.cf2, jb.rf2, a.mb_w, a.mb_h);
+  uint32_t *w0 = win, *w1 = win + (RB + 7) * (P / 4);
+  const uint8_t *sp0 = (const uint8_t *)plane_ptr<Px>(pl.ref[0], jb.src_x + jb.ox - 3, jb.src_y + jb.oy - 3);
+  const uint8_t *sp1 =
+      (const uint8_t *)plane_ptr<Px>(pl.ref[1], jb.src2_x + jb.ox - 3, jb.src2_y + jb.oy - 3);
+  const int64_t rs0 = (int64_t)pl.ref[0].stride * B, rs1 = (int64_t)pl.ref[1].stride * B;
+#pragma unroll 1
+  for (int band = 0; band < N / RB; band++) {
+    if (band) wave_sync();  // the previous band's window reads are done
+#pragma unroll 2
+    for (int i = col; i < kTot; i += N) {
+      const int r = i / kRowDw, d = i - r * kRowDw;
+      uint32_t v0, v1;
+      __builtin_memcpy(&v0, sp0 + (band * RB + r) * rs0 + 4 * d, 4);
+      __builtin_memcpy(&v1, sp1 + (band * RB + r) * rs1 + 4 * d, 4);
+      w0[r * (P / 4) + d] = B == 1 ? v0 ^ 0x80808080u : v0;
+      w1[r * (P / 4) + d] = B == 1 ? v1 ^ 0x80808080u : v1;
+    }
+    wave_sync();
+    int32_t g0[8], g1[8];
+#pragma unroll
+    for (int k = 1; k < 6; k++) {
+      g0[k] = mc_h<Px>(f0, w0 + k * (P / 4), col, ib);
+      g1[k] = mc_h<Px>(f1, w1 + k * (P / 4), col, ib);
+    }
+    g0[0] = g0[6] = g0[7] = g1[0] = g1[6] = g1[7] = 0;
+#pragma unroll 1
+    for (int r0 = 0; r0 < RB; r0 += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int r = r0 + u;
+        g0[(u + 6) & 7] = mc_h<Px>(f0, w0 + (r + 6) * (P / 4), col, ib);
+        g1[(u + 6) & 7] = mc_h<Px>(f1, w1 + (r + 6) * (P / 4), col, ib);
+        const int32_t t = mc_prep_v(f0, g0, u, ib) + mc_prep_v(f1, g1, u, ib);
+        pred[(band * RB + r) * N + col] = (Px)clamp_med3(round_shift(t, ib + 1), 0, maxv);
+      }
+    }
+  }
+  wave_sync();  // window reads done, prediction visible
 }
 
 // compute_distortion_bias (src/rdo.rs:476-508) of the BLOCK_8X8 importance
@@ -215,7 +363,9 @@ __device__ __forceinline__ uint64_t rdo_sse_biased(const RdoArgs &a, const RdoJo
 // a wavefront carries two chroma blocks, one per half, so every phase keeps
 // all 64 lanes busy).  `valid` = false for a second half without a block:
 // it recomputes its partner's block and stores nothing.
-template <typename Px, int N, int LPB>
+// MODE: 0 single-reference candidates, 1 compound candidates, 2 either
+// (by the job: the commit launch).
+template <typename Px, int N, int LPB, int MODE>
 __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &pl, int t,
                                               bool valid, int32_t *buf, Px *pred,
                                               const uint16_t *scan) {
@@ -237,7 +387,12 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
-  // ---- A. put_8tap into LDS ------------------------------------------------
+  // ---- A. put_8tap into LDS (compound: prep_8tap x 2 + mc_avg) -------------
+  if (MODE == 1 || (MODE == 2 && jb.comp)) {
+    static_assert(2 * (16 + 7) * (sizeof(Px) == 1 ? 48 : 80) <= N * (N + 1) * 4 || N != 32,
+                  "compound windows must fit the coefficient slab");
+    mc_compound<Px, N, 16>(a, pl, jb, reinterpret_cast<uint32_t *>(buf), pred);
+  } else
   {
     uint32_t *win = reinterpret_cast<uint32_t *>(buf);
     const uint8_t *sp = (const uint8_t *)plane_ptr<Px>(ref, jb.src_x + ox - 3, jb.src_y + oy - 3);
@@ -492,8 +647,10 @@ template <typename Px, typename Mid, int NPART>
 struct LumaLds {
   static constexpr int kWinP = sizeof(Px) == 1 ? 80 : 144;  // window row pitch, bytes
   static constexpr int kWinRows = 64 / NPART + 7;
+  static constexpr int kCompRows = sizeof(Px) == 1 ? 16 : 8;  // compound MC band
   static constexpr int kScr =  // bytes of the phase-shared scratch
-      cmax(cmax(kWinRows * kWinP, 16 * 65 * 4), 32 * 66 * (int)sizeof(Mid));
+      cmax(cmax(cmax(kWinRows * kWinP, 16 * 65 * 4), 32 * 66 * (int)sizeof(Mid)),
+           2 * (kCompRows + 7) * kWinP);
   static constexpr int kSlot = (kScr + 64 * 64 * (int)sizeof(Px) + 15) / 16 * 16;  // + pred
 };
 
@@ -513,7 +670,7 @@ __device__ __forceinline__ uint64_t luma_dist(const RdoArgs &a, const RdoJob &j,
   return group_sum<64>(rdo_biased(v, rdo_bias(a, px >> 2, py >> 2)));
 }
 
-template <typename Px, int NPART>
+template <typename Px, int NPART, int MODE>
 __device__ __forceinline__ void luma_front(const RdoArgs &a, const RdoPlane &pl, int t,
                                            const RdoJob &jb, bool valid, uint8_t *scr, Px *pred) {
   constexpr int N = 64, B = (int)sizeof(Px);
@@ -525,7 +682,12 @@ __device__ __forceinline__ void luma_front(const RdoArgs &a, const RdoPlane &pl,
   const int ox = 0, oy = 0;
   const int bd = a.bd, ib = bd == 12 ? 2 : 4, maxv = (1 << bd) - 1;
 
-  // ---- A. put_8tap (src/mc.rs:213-307) into pred, NPART bands --------------
+  // ---- A. put_8tap (src/mc.rs:213-307) into pred, NPART bands; compound:
+  // prep_8tap x 2 + mc_avg in bands of kCompRows
+  if (MODE == 1 || (MODE == 2 && jb.comp)) {
+    mc_compound<Px, 64, LumaLds<Px, int16_t, NPART>::kCompRows>(
+        a, pl, jb, reinterpret_cast<uint32_t *>(scr), pred);
+  } else
   {
     uint32_t *win = reinterpret_cast<uint32_t *>(scr);
     const int cf = jb.cf, rf = jb.rf;
@@ -760,12 +922,12 @@ __device__ __forceinline__ void luma_back(const RdoArgs &a, const RdoPlane &pl, 
 }
 
 // One luma candidate per wavefront (12-bit).
-template <typename Px, typename Mid, int NPART>
+template <typename Px, typename Mid, int NPART, int MODE>
 __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &pl, int t,
                                               uint8_t *scr, Px *pred, const uint16_t *scan) {
   const int lane = threadIdx.x & 63;
   const RdoJob jb = rdo_job<64>(a, pl, t);
-  luma_front<Px, NPART>(a, pl, t, jb, true, scr, pred);
+  luma_front<Px, NPART, MODE>(a, pl, t, jb, true, scr, pred);
   wave_sync();
   int32_t *fmid = reinterpret_cast<int32_t *>(scr);
   if (lane < 16) luma_fwd_row(fmid + lane * 65, a.bd);
@@ -786,7 +948,7 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
 
 // Chroma transform blocks, two per wavefront (one per half), plane U then
 // V: pair b of the launch.
-template <typename Px>
+template <typename Px, int MODE>
 __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, int32_t *buf,
                                                 Px *pred, const uint16_t *scan) {
   const int pairs = (chroma.n_tx + 1) / 2;  // per plane, for the grid's size
@@ -797,7 +959,7 @@ __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, in
   if (i - half >= n) return;  // past the compacted list: the whole pair
   const bool valid = i < n;
   if (!valid) i -= 1;
-  rdo_cand_body<Px, 32, 32>(chroma, chroma.p[plane], i, valid, buf + half * 32 * 33,
+  rdo_cand_body<Px, 32, 32, MODE>(chroma, chroma.p[plane], i, valid, buf + half * 32 * 33,
                             pred + half * 32 * 32, scan);
 }
 
@@ -816,10 +978,10 @@ template <typename Px>
 using SingleLds = LumaLds<Px, typename std::conditional<sizeof(Px) == 1, int16_t, int32_t>::type, 2>;
 constexpr int kChromaPair(int pxb) { return 2 * 32 * 33 * 4 + 2 * 32 * 32 * pxb; }
 
-template <typename Px, bool COMMIT>
+// MODE 0 / 1: score single-reference / compound candidates; 2: commit
+template <typename Px, int MODE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void rdo_frame_kernel(
     RdoArgs luma, RdoArgs chroma) {
-  (void)COMMIT;  // separate score / commit instantiations (rocprof names)
   using L = SingleLds<Px>;
   using Mid = typename std::conditional<sizeof(Px) == 1, int16_t, int32_t>::type;
   __shared__ __align__(16) uint8_t lds[cmax(L::kSlot, kChromaPair(sizeof(Px)))];
@@ -828,10 +990,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void rd
   stage_scan(scan, b < luma.n_tx ? luma.q_tx_index : chroma.q_tx_index);
   if (b < luma.n_tx && b >= rdo_ntx(luma)) return;  // past the compacted list
   if (b < luma.n_tx)
-    rdo_luma_body<Px, Mid, 2>(luma, luma.p[0], b, lds,
+    rdo_luma_body<Px, Mid, 2, MODE>(luma, luma.p[0], b, lds,
                               reinterpret_cast<Px *>(lds + L::kScr), scan);
   else
-    rdo_chroma_pair<Px>(chroma, b - luma.n_tx, reinterpret_cast<int32_t *>(lds),
+    rdo_chroma_pair<Px, MODE>(chroma, b - luma.n_tx, reinterpret_cast<int32_t *>(lds),
                         reinterpret_cast<Px *>(lds + 2 * 32 * 33 * 4), scan);
 }
 
@@ -848,10 +1010,9 @@ struct QuadLds {
   static constexpr int kBytes = cmax(4 * L::kSlot, 3 * kChromaPair(sizeof(Px)));
 };
 
-template <typename Px, bool COMMIT>
+template <typename Px, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_quad_kernel(
     RdoArgs luma, RdoArgs chroma, int nquads) {
-  (void)COMMIT;  // separate score / commit instantiations (rocprof names)
   using L = typename QuadLds<Px>::L;
   constexpr int NPART = sizeof(Px) == 1 ? 2 : 4;
   __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
@@ -863,7 +1024,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     const int pair = 3 * (b - nquads) + wave;
     if (wave == 3 || pair >= 2 * ((chroma.n_tx + 1) / 2)) return;
     uint8_t *w = lds + wave * kChromaPair(sizeof(Px));
-    rdo_chroma_pair<Px>(chroma, pair, reinterpret_cast<int32_t *>(w),
+    rdo_chroma_pair<Px, MODE>(chroma, pair, reinterpret_cast<int32_t *>(w),
                         reinterpret_cast<Px *>(w + 2 * 32 * 33 * 4), scan);
     return;
   }
@@ -882,7 +1043,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
   if (t0 >= n) return;  // past the compacted list (uniform over the workgroup)
   const bool valid = t < n;
   const RdoJob jb = rdo_job<64>(luma, luma.p[0], valid ? t : n - 1);
-  if (valid) luma_front<Px, NPART>(luma, luma.p[0], t, jb, true, slot(wave), pred(wave));
+  if (valid) luma_front<Px, NPART, MODE>(luma, luma.p[0], t, jb, true, slot(wave), pred(wave));
   __syncthreads();
   if (wave == 0) {  // row DCT: lane = 16 * candidate + raster row
     const int q = lane >> 4;
@@ -910,38 +1071,44 @@ using namespace rv;
 
 // Replay-internal entry (rv_replay.hip): luma (N = 64, cdef distortion)
 // and both chroma planes (N = 32, SSE) of every task, one launch on `s`.
-int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s) {
+template <int MODE>
+static void rdo_launch(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s,
+                       bool single, unsigned cpairs) {
+  if (luma.bd == 12 || single) {  // 12-bit: i32 row-pass intermediate
+    const unsigned grid = (unsigned)luma.n_tx + cpairs;
+    if (grid == 0) return;
+    if (hbd)
+      rdo_frame_kernel<uint16_t, MODE><<<grid, 64, 0, s>>>(luma, chroma);
+    else
+      rdo_frame_kernel<uint8_t, MODE><<<grid, 64, 0, s>>>(luma, chroma);
+    return;
+  }
+  const int nquads = (luma.n_tx + 3) / 4;
+  const unsigned grid = (unsigned)nquads + (cpairs + 2) / 3;
+  if (grid == 0) return;
+  if (hbd)
+    rdo_quad_kernel<uint16_t, MODE><<<grid, 256, 0, s>>>(luma, chroma, nquads);
+  else
+    rdo_quad_kernel<uint8_t, MODE><<<grid, 256, 0, s>>>(luma, chroma, nquads);
+}
+
+// Replay-internal entry (rv_replay.hip): luma (N = 64, cdef distortion)
+// and both chroma planes (N = 32, SSE) of every task, one launch on `s`.
+// compound: the tasks are compound candidates (score launches only).
+int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s,
+                      bool compound) {
   const unsigned cpairs = (unsigned)(2 * ((chroma.n_tx + 1) / 2));
   // RAV1E_HIP_RDO_SINGLE=1: one candidate per workgroup at every bit depth
   static const bool single = [] {
     const char *e = getenv("RAV1E_HIP_RDO_SINGLE");
     return e && e[0] == '1';
   }();
-  if (luma.bd == 12 || single) {  // 12-bit: i32 row-pass intermediate
-    const unsigned grid = (unsigned)luma.n_tx + cpairs;
-    if (grid == 0) return RV_OK;
-    if (hbd && luma.commit)
-      rdo_frame_kernel<uint16_t, true><<<grid, 64, 0, s>>>(luma, chroma);
-    else if (hbd)
-      rdo_frame_kernel<uint16_t, false><<<grid, 64, 0, s>>>(luma, chroma);
-    else if (luma.commit)
-      rdo_frame_kernel<uint8_t, true><<<grid, 64, 0, s>>>(luma, chroma);
-    else
-      rdo_frame_kernel<uint8_t, false><<<grid, 64, 0, s>>>(luma, chroma);
-    RV_HIP_CHECK_LAUNCH();
-    return RV_OK;
-  }
-  const int nquads = (luma.n_tx + 3) / 4;
-  const unsigned grid = (unsigned)nquads + (cpairs + 2) / 3;
-  if (grid == 0) return RV_OK;
-  if (hbd && luma.commit)
-    rdo_quad_kernel<uint16_t, true><<<grid, 256, 0, s>>>(luma, chroma, nquads);
-  else if (hbd)
-    rdo_quad_kernel<uint16_t, false><<<grid, 256, 0, s>>>(luma, chroma, nquads);
-  else if (luma.commit)
-    rdo_quad_kernel<uint8_t, true><<<grid, 256, 0, s>>>(luma, chroma, nquads);
+  if (luma.commit)
+    rdo_launch<2>(luma, chroma, hbd, s, single, cpairs);
+  else if (compound)
+    rdo_launch<1>(luma, chroma, hbd, s, single, cpairs);
   else
-    rdo_quad_kernel<uint8_t, false><<<grid, 256, 0, s>>>(luma, chroma, nquads);
+    rdo_launch<0>(luma, chroma, hbd, s, single, cpairs);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

@@ -152,14 +152,21 @@ __global__ __launch_bounds__(64) void score_candidates(
     const uint64_t *lout,
     const uint64_t *uout, const uint64_t *vout, int ntx_c, RdoWinner *win,
     const rv_fs_result *coarse, const rv_fs_result *half, const rv_fs_result *full,
-    uint64_t *words) {
+    uint64_t *words, int32_t *cand_count, unsigned long long *imp_sum, uint32_t *evals) {
   const int sb = blockIdx.x * 64 + threadIdx.x;
+  if (sb == 0) {  // F4's list is consumed: ready for the next frame; F5 sums next
+    evals[0] = (uint32_t)*cand_count;  // single-reference candidates evaluated
+    evals[1] = (uint32_t)(cg.comp * g.nsb);  // compound ones
+    *cand_count = 0;
+    *imp_sum = 0;
+  }
   if (sb >= g.nsb) return;
   double best = 1.7976931348623157e308;  // f64::MAX
   RdoWinner w{0, 0, best, 0};
-  for (int c = 0; c < g.C; c++) {
+  const int ns = g.R * g.M;  // single-reference candidates; compound ones follow
+  for (int c = 0; c < ns + cg.comp; c++) {
     rv_mv mv;
-    if (!cand_mv(cg, sub, sb, c, &mv)) continue;
+    if (c < ns && !cand_mv(cg, sub, sb, c, &mv)) continue;
     const int64_t o = (int64_t)c * g.nsb + sb;
     uint64_t su = 0, sv = 0, nu = 0, nv = 0;
     uint32_t rate = (uint32_t)lout[o * 3 + 2];
@@ -337,6 +344,7 @@ struct rv_replay {
   uint64_t *l_out, *c_out;  // F4: [skip dist, non-skip dist, rate] per transform block
   RdoWinner *win;
   int32_t *cand_list, *cand_count;  // F4: the valid candidates
+  uint32_t *cand_evals;             // [kRing][2]: F4 candidates per frame (single, compound)
   int32_t *l_lev, *c_lev;   // F6: committed levels
   uint64_t *words;
   unsigned long long *tail;  // [levels csum, group recon sum, imp satd sum, -, frame recon sum]
@@ -593,6 +601,10 @@ void frame_info(long n, int R, rv_replay_frame_info *f) {
     long d = 4 * g + kRef[j][k];
     f->ref_display[k] = (int)(d < 0 ? 0 : d);
   }
+  // reference_mode SELECT unless the frame is the first output of its group
+  // (src/encoder.rs:832-836); compound needs a forward and a backward
+  // reference (src/rdo.rs:914-941): display 4g+2 and 4g+3
+  f->compound = R == 2 && (j == 1 || j == 3);
 }
 
 }  // namespace
@@ -662,12 +674,12 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   g.nsb = g.tw * g.th;
   g.R = cfg->n_refs;
   g.M = kCandModes;
-  g.C = g.R * g.M;
+  g.C = g.R * g.M + (g.R == 2 ? kCompModes : 0);  // the most a frame evaluates
   g.cw = kSb >> g.xdec;
   g.ch = kSb >> g.ydec;
   g.w_imp = g.w_in_b / 2;
   g.h_imp = g.h_in_b / 2;
-  r->cg = CandGeo{g.nsb, g.tw, g.th, g.tx0, g.ty0, g.tws, g.ths, g.R, g.M};
+  r->cg = CandGeo{g.nsb, g.tw, g.th, g.tx0, g.ty0, g.tws, g.ths, g.R, g.M, 0};
   // 8x8 sums of 10-bit pixels fit the u16 box-sum table; 12-bit searches
   // exhaustively
   r->sea = g.bd <= 10 && (cfg->flags & RV_REPLAY_EXHAUSTIVE_FS) == 0;
@@ -699,6 +711,9 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->win = (RdoWinner *)dalloc(r, (size_t)g.nsb * sizeof(RdoWinner));
   r->cand_list = (int32_t *)dalloc(r, (size_t)nc * 4);
   r->cand_count = (int32_t *)dalloc(r, 4);
+  r->cand_evals = (uint32_t *)dalloc(r, rv_replay::kRing * 2 * 4);
+  if (r->cand_evals) (void)hipMemsetAsync(r->cand_evals, 0, rv_replay::kRing * 2 * 4, r->stream);
+  if (r->cand_count) (void)hipMemsetAsync(r->cand_count, 0, 4, r->stream);
   r->l_lev = (int32_t *)dalloc(r, (size_t)g.nsb * 1024 * 4);
   r->c_lev = (int32_t *)dalloc(r, (size_t)g.nsb * r->ntx_c * 1024 * 4 * 2);
   r->words = (uint64_t *)dalloc(r, (size_t)g.nsb * (8 * g.R + 4) * 8);
@@ -707,7 +722,7 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->n_imp = r->imp_bx * r->imp_by;
   r->tail = (unsigned long long *)dalloc(r, 5 * 8);
   ok = ok && r->coarse && r->half && r->full && r->sub && r->l_out && r->c_out && r->win &&
-       r->cand_list && r->cand_count &&
+       r->cand_list && r->cand_count && r->cand_evals &&
        r->l_lev && r->c_lev && r->words && r->tail;
   if (ok) {
     ok = hipMemsetAsync(r->words, 0, (size_t)g.nsb * (8 * g.R + 4) * 8, r->stream) == hipSuccess &&
@@ -930,6 +945,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   if (!r->jobs_built) RV_R(build_static_jobs(r));
   const rv_replay::Level &L = r->lv[fi.level];
   const int lv = fi.level;
+  CandGeo cg = r->cg;
+  cg.comp = fi.compound ? kCompModes : 0;
   const RvInput &cur = r->inputs[fi.display % r->inputs.size()];
   const RvSlot &S = r->slots[fi.display % kSlots];
   const RvSlot *ref[2];
@@ -978,10 +995,11 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   RV_EV(4);
   RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
                                r->sub, ev_sub, nullptr, st));
-  // the valid candidates (a few microseconds; bracketed with F3 sub-pel)
-  RV_H(hipMemsetAsync(r->cand_count, 0, 4, st));
-  cand_list_kernel<<<(g.nsb * g.C + 255) / 256, 256, 0, st>>>(r->cg, r->sub, g.nsb * g.C,
-                                                              r->cand_list, r->cand_count);
+  // the valid candidates (a few microseconds; bracketed with F3 sub-pel;
+  // the count was zeroed by the previous frame's argmin or at creation)
+  const int nsingle = g.nsb * g.R * g.M;
+  cand_list_kernel<<<(nsingle + 255) / 256, 256, 0, st>>>(cg, r->sub, nsingle, r->cand_list,
+                                                          r->cand_count);
   RV_EV(5);
   // F4 every valid candidate, luma + both chroma planes in one fused launch
   RdoArgs la, ca;
@@ -991,14 +1009,14 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   la.p[0].dst = S.y;
   la.p[0].levels = r->l_lev;
   la.p[0].out = r->l_out;
-  la.g = r->cg;
+  la.g = cg;
   la.sub = r->sub;
   la.win = r->win;
   la.imp = r->imp;
   la.w_in_b = g.w_in_b;
   la.h_in_b = g.h_in_b;
   la.w_imp = g.w_imp;
-  la.n_tx = g.nsb * g.C;
+  la.n_tx = nsingle;
   la.list = r->cand_list;
   la.count = r->cand_count;
   la.ntx_per_cand = 1;
@@ -1011,7 +1029,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   la.qindex = L.qidx;
   ca = la;
   const int ntx_c = r->ntx_c;
-  const int64_t nct = (int64_t)g.nsb * g.C * ntx_c;
+  const int64_t nct = (int64_t)g.nsb * g.C * ntx_c;  // output blocks per chroma plane
   const rv_plane cur_c[2] = {cur.u, cur.v}, s_c[2] = {S.u, S.v};
   for (int p = 0; p < 2; p++) {
     ca.p[p].org = cur_c[p];
@@ -1021,7 +1039,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     ca.p[p].out = r->c_out + (size_t)p * nct * 3;
     ca.p[p].q = p ? L.qv : L.qu;
   }
-  ca.n_tx = (int)nct;
+  ca.n_tx = nsingle * ntx_c;
   ca.ntx_per_cand = ntx_c;
   ca.mb_w = g.cw;
   ca.mb_h = g.ch;
@@ -1032,11 +1050,22 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   ca.q_tx_index = 3 * 16 + 0;  // TX_32X32, DCT_DCT
   ca.tx_size = 3;
   RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
+  if (cg.comp) {  // the compound candidates: every one is pushed, no list
+    RdoArgs lc = la, cc = ca;
+    lc.list = cc.list = nullptr;
+    lc.count = cc.count = nullptr;
+    lc.cand_base = cc.cand_base = nsingle;
+    lc.n_tx = g.nsb * cg.comp;
+    cc.n_tx = g.nsb * cg.comp * ntx_c;
+    RV_R(rv_rdo_candidates(lc, cc, g.hbd, st, true));
+  }
   RV_EV(6);
-  score_candidates<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, r->cg, L.lambda, L.ds[1], L.ds[2], r->sub,
+  score_candidates<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, cg, L.lambda, L.ds[1], L.ds[2], r->sub,
                                                      r->l_out,
                                                      r->c_out, r->c_out + nct * 3, ntx_c, r->win,
-                                                     r->coarse, r->half, r->full, r->words);
+                                                     r->coarse, r->half, r->full, r->words,
+                                                     r->cand_count, r->tail + 2,
+                                                     r->cand_evals + 2 * slot);
   RV_EV(7);
   // F6 commit the winners into the frame
   la.commit = ca.commit = 1;
@@ -1047,8 +1076,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   la.ntx_per_cand = 1;
   RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
   RV_EV(8);
-  // F5 importance SATD against reference 0
-  RV_H(hipMemsetAsync(r->tail + 2, 0, 8, st));
+  // F5 importance SATD against reference 0 (the sum was zeroed by the argmin)
   {
     const unsigned nb = (unsigned)((r->n_imp + 255) / 256);
     if (g.hbd)
@@ -1160,8 +1188,10 @@ int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap) {
 int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out, int cap) {
   return stage_times(r, ms_out, cap, last_frames);
 }
-// Diamond-search candidate evaluations summed over the last min(frames, 64)
-// coded frames: out[0] F3 full-pel, out[1] F3 sub-pel, out[2] frames summed.
+// Candidate evaluations summed over the last min(frames, 64) coded frames:
+// out[0] F3 full-pel diamond, out[1] F3 sub-pel diamond, out[2] frames
+// summed, and (cap >= 5) out[3] / out[4] the F4 single-reference / compound
+// RDO candidates.
 int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
   if (!r || !out || cap < 3) return rv_set_error(RV_EINVAL, "rv_replay_counters");
   const Geo &g = r->g;
@@ -1176,7 +1206,15 @@ int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
     for (int k = 0; k < 2; k++)
       for (int j = 0; j < nj; j++) out[k] += h[((size_t)f * 2 + k) * nj + j];
   out[2] = (uint64_t)nf;
-  return 3;
+  if (cap < 5) return 3;
+  std::vector<uint32_t> ce((size_t)nf * 2);
+  if (nf) RV_H(hipMemcpy(ce.data(), r->cand_evals, ce.size() * 4, hipMemcpyDeviceToHost));
+  out[3] = out[4] = 0;
+  for (int f = 0; f < nf; f++) {
+    out[3] += ce[2 * f];
+    out[4] += ce[2 * f + 1];
+  }
+  return 5;
 }
 
 // ---- RCCL communicator for the tile-group exchange ---------------------------

@@ -249,7 +249,8 @@ class HipReplay:
         fi = RvReplayFrameInfo()
         _check(lib().rv_replay_frame(self.h, C.byref(fi)), "rv_replay_frame")
         return {"display": fi.display, "me_range_scale": fi.me_range_scale, "level": fi.level,
-                "is_key": fi.is_key, "ref_display": list(fi.ref_display)}
+                "is_key": fi.is_key, "ref_display": list(fi.ref_display),
+                "compound": fi.compound}
 
     def set_groups(self, rects, my_group, comm=None):
         arr = np.ascontiguousarray(np.asarray(rects, dtype=np.int32).ravel())
@@ -294,9 +295,10 @@ class HipReplay:
         return out[:n]
 
     def counters(self) -> np.ndarray:
-        """[F3 full-pel evals, F3 sub-pel evals, frames] over the last <= 64 frames."""
-        out = np.zeros(3, dtype=np.uint64)
-        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 3) - 3, "rv_replay_counters")
+        """[F3 full-pel evals, F3 sub-pel evals, frames, F4 single-reference
+        candidates, F4 compound candidates] over the last <= 64 frames."""
+        out = np.zeros(5, dtype=np.uint64)
+        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 5) - 5, "rv_replay_counters")
         return out
 
     def close(self):

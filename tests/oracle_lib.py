@@ -395,7 +395,7 @@ def cpu_share() -> int:
 
 class OrcFrameInfo(C.Structure):
     _fields_ = [("display", C.c_int32), ("me_range_scale", C.c_int32), ("level", C.c_int32),
-                ("is_key", C.c_int32), ("ref_display", C.c_int32 * 2)]
+                ("is_key", C.c_int32), ("ref_display", C.c_int32 * 2), ("compound", C.c_int32)]
 
 
 class CpuReplay:
@@ -452,7 +452,8 @@ class CpuReplay:
         fi = OrcFrameInfo()
         assert self.L.orc_replay_frame(self.h, C.byref(fi), sb_limit, 1 if pad else 0) == 0
         return {"display": fi.display, "me_range_scale": fi.me_range_scale, "level": fi.level,
-                "is_key": fi.is_key, "ref_display": list(fi.ref_display)}
+                "is_key": fi.is_key, "ref_display": list(fi.ref_display),
+                "compound": fi.compound}
 
     def region_bytes(self, rect) -> int:
         r = np.ascontiguousarray(np.asarray(rect, dtype=np.int32))
