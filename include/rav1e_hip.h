@@ -285,6 +285,22 @@ int rv_estimate_rate_batch(const uint64_t *d_tx_dist, int n, int qindex, int tx_
 /* ---------------------------------------------------------------------
  * Motion search
  * ------------------------------------------------------------------- */
+/* ---- intra prediction (src/predict.rs:202-241, 538-1035) ---------------
+ * PredictionMode::predict_intra without CfL for every job: mode is the
+ * PredictionMode (0 DC_PRED, 1 V, 2 H, 3 D45, 4 D135, 5 D117, 6 D153,
+ * 7 D207, 8 D63, 9 SMOOTH, 10 SMOOTH_V, 11 SMOOTH_H, 12 PAETH), variant the
+ * PredictionVariant of the block's tile position (0 NONE, 1 LEFT, 2 TOP,
+ * 3 BOTH, src/predict.rs:175-184); the predicted tx_size block is written at
+ * (x, y) of dst.  d_edges: per job rav1e's edge_buf, 4 * 64 + 1 pixels of
+ * dst's pixel type (left bottom-to-top right-aligned in [0, 128), top-left
+ * at 128, above from 129; get_intra_edges, src/recon_intra.rs). */
+typedef struct rv_intra_job {
+  int32_t x, y;
+  int32_t mode, variant;
+} rv_intra_job;
+int rv_predict_intra_batch(const rv_plane *dst, const rv_intra_job *d_jobs, const void *d_edges,
+                           int n, int tx_size, int bit_depth, void *stream);
+
 /* dc_q / ac_q lookups (src/quantize.rs:42-62) on the host: ac = 0 for
  * dc_qlookup*_Q3, 1 for ac_qlookup*_Q3; -1 on bad arguments. */
 int rv_q_lookup(int ac, int qindex, int bit_depth);

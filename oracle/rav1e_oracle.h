@@ -68,6 +68,11 @@ void orc_prep_8tap(int16_t *tmp, const void *src, ptrdiff_t src_stride, int w,
 void orc_mc_avg(void *dst, ptrdiff_t dst_stride, const int16_t *tmp1,
                 const int16_t *tmp2, int w, int h, int bit_depth, int hbd,
                 int emulate_gen);
+/* PredictionMode::predict_intra without CfL (src/predict.rs:202-241, 538-1035):
+ * mode = PredictionMode (0 DC .. 12 PAETH), variant = PredictionVariant,
+ * edge = rav1e's 257-pixel edge_buf. */
+void orc_predict_intra(int mode, int variant, void *dst, ptrdiff_t stride, int w, int h,
+                       int bit_depth, int hbd, const void *edge);
 /* SUBPEL_FILTERS + get_filter (src/mc.rs:70-179, 201-210) */
 const int32_t *orc_get_filter(int mode, int frac, int length);
 

@@ -49,6 +49,7 @@ class RvFsResult(C.Structure):
 
 # job layouts as numpy dtypes (arrays of these go to the device verbatim)
 DIST_JOB = np.dtype([("org_x", "<i4"), ("org_y", "<i4"), ("ref_x", "<i4"), ("ref_y", "<i4")])
+INTRA_JOB = np.dtype([("x", "<i4"), ("y", "<i4"), ("mode", "<i4"), ("variant", "<i4")])
 MC_JOB = np.dtype([("src_x", "<i4"), ("src_y", "<i4"), ("dst_x", "<i4"), ("dst_y", "<i4"),
                    ("col_frac", "<i4"), ("row_frac", "<i4")])
 MOTION_VECTOR = np.dtype([("row", "<i2"), ("col", "<i2")])  # rv_mv / MotionVector
@@ -245,6 +246,7 @@ def _declare(L):
         "rv_propagate_importances": (i32, [P, P, vp, vp, vp, i32, vp, vp, sz, vp]),
         "rv_cdef_moments_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
         "rv_put_8tap_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, i32, vp]),
+        "rv_predict_intra_batch": (i32, [P, vp, vp, i32, i32, i32, vp]),
         "rv_prep_8tap_batch": (i32, [vp, P, vp, i32, i32, i32, i32, i32, i32, vp]),
         "rv_mc_avg_batch": (i32, [P, vp, vp, vp, i32, i32, i32, i32, vp]),
         "rv_mc_dist_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
@@ -513,6 +515,44 @@ def put_8tap_batch(dst: DevicePlane, src: DevicePlane, jobs, w, h, mode_x=0, mod
     dj = DeviceBuffer.from_array(jobs)
     _check(lib().rv_put_8tap_batch(C.byref(dst.desc), C.byref(src.desc), dj.ptr, len(jobs), w, h,
                                    mode_x, mode_y, bit_depth, None), "rv_put_8tap_batch")
+    _sync()
+
+
+class PredictionMode(enum.IntEnum):
+    """src/predict.rs:135-166 (the intra modes)."""
+    DC_PRED = 0
+    V_PRED = 1
+    H_PRED = 2
+    D45_PRED = 3
+    D135_PRED = 4
+    D117_PRED = 5
+    D153_PRED = 6
+    D207_PRED = 7
+    D63_PRED = 8
+    SMOOTH_PRED = 9
+    SMOOTH_V_PRED = 10
+    SMOOTH_H_PRED = 11
+    PAETH_PRED = 12
+
+
+# RAV1E_INTRA_MODES (src/predict.rs:32-46): the screening order
+RAV1E_INTRA_MODES = [0, 2, 1, 9, 11, 10, 12, 3, 4, 5, 6, 7, 8]
+EDGE_PX = 4 * 64 + 1  # edge_buf: 4 * MAX_TX_SIZE + 1
+
+
+def predict_intra_batch(dst: DevicePlane, jobs, edges: np.ndarray, tx_size, bit_depth=8):
+    """PredictionMode::predict_intra (no CfL) of every job into dst; edges
+    (n, 257) in rav1e's edge_buf layout (src/predict.rs:545-551)."""
+    jobs = np.ascontiguousarray(jobs, dtype=INTRA_JOB)
+    edges = np.ascontiguousarray(edges, dtype=np.uint16 if bit_depth > 8 else np.uint8)
+    if edges.shape != (len(jobs), EDGE_PX):
+        raise Rav1eHipError("predict_intra_batch: edges must be (n_jobs, 257)")
+    if not (0 <= jobs["mode"]).all() or not (jobs["mode"] <= 12).all():
+        raise Rav1eHipError("predict_intra_batch: CfL / inter modes are not intra predictions here")
+    dj = DeviceBuffer.from_array(jobs)
+    de = DeviceBuffer.from_array(edges)
+    _check(lib().rv_predict_intra_batch(C.byref(dst.desc), dj.ptr, de.ptr, len(jobs), tx_size,
+                                        bit_depth, None), "rv_predict_intra_batch")
     _sync()
 
 

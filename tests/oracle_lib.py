@@ -30,6 +30,7 @@ def lib():
         L.orc_cdef_dist_from_moments.restype = C.c_uint64
         L.orc_cdef_dist_from_moments.argtypes = [vp, i32]
         L.orc_put_8tap.argtypes = [vp, sz, vp, sz] + [i32] * 9
+        L.orc_predict_intra.argtypes = [i32, i32, vp, sz, i32, i32, i32, i32, vp]
         L.orc_prep_8tap.argtypes = [vp, vp, sz] + [i32] * 8
         L.orc_mc_avg.argtypes = [vp, sz, vp, vp] + [i32] * 5
         L.orc_fwd_txfm1d.restype = i32
@@ -90,6 +91,15 @@ def put_8tap(src, sy, sx, w, h, col_frac, row_frac, mode_x=0, mode_y=0, bd=8, em
     dst = np.zeros((h, w), dtype=src.dtype)
     lib().orc_put_8tap(ptr(dst), w, ptr(src, sy * src.shape[1] + sx), src.shape[1], w, h,
                        col_frac, row_frac, mode_x, mode_y, bd, hbd_of(src), emulate_gen)
+    return dst
+
+
+def predict_intra(mode, variant, w, h, edge, bd=8):
+    """orc_predict_intra: PredictionMode::predict_intra (no CfL) of a w x h
+    block from a 257-pixel edge_buf."""
+    edge = np.ascontiguousarray(edge, dtype=np.uint16 if bd > 8 else np.uint8)
+    dst = np.zeros((h, w), dtype=edge.dtype)
+    lib().orc_predict_intra(mode, variant, ptr(dst), w, w, h, bd, 1 if bd > 8 else 0, ptr(edge))
     return dst
 
 

@@ -737,3 +737,51 @@ def test_quantize_vs_oracle(tx_size, tx_type):
                     np.testing.assert_array_equal(q[k], wq, err_msg=f"{bd} {qi} {is_intra} {k}")
                     np.testing.assert_array_equal(r[k], O.dequantize(wq, tx_size, qi, bd))
                 np.testing.assert_array_equal(R.dequantize_batch(q, tx_size, qi, bd), r)
+
+
+# ---- intra prediction (src/predict.rs:202-241, 538-1035) -------------------
+@pytest.mark.parametrize("bd", [8, 10, 12])
+def test_predict_intra_vs_oracle(bd):
+    """Every intra mode (PAETH through its variant remap) x every
+    PredictionVariant x all 19 TxSizes, random and saturated edge buffers."""
+    rng = np.random.default_rng(900 + bd)
+    dt = np.uint8 if bd == 8 else np.uint16
+    for tx in range(19):
+        w, h = 1 << O.TX_W_LOG2[tx], 1 << O.TX_H_LOG2[tx]
+        combos = [(m, v) for m in range(13) for v in range(4)]
+        edges = rng.integers(0, 1 << bd, (len(combos) + 2, R.EDGE_PX)).astype(dt)
+        edges[-2] = (1 << bd) - 1
+        edges[-1, ::2] = 0
+        edges[-1, 1::2] = (1 << bd) - 1
+        combos += [(9, 3), (5, 3)]
+        jobs = np.zeros(len(combos), dtype=R.INTRA_JOB)
+        for k, (m, v) in enumerate(combos):
+            jobs[k] = (0, k * h, m, v)
+        dst = R.DevicePlane(w, h * len(combos), 0, 0, 0, 0, bd > 8)
+        R.predict_intra_batch(dst, jobs, edges, tx, bd)
+        got = dst.download_visible()
+        for k, (m, v) in enumerate(combos):
+            want = O.predict_intra(m, v, w, h, edges[k], bd)
+            np.testing.assert_array_equal(got[k * h:(k + 1) * h], want, err_msg=str((tx, m, v)))
+
+
+def test_predict_intra_reference_kats():
+    """The reference's own 4x4 known answers (src/predict.rs:1047-1107)
+    through the HIP path."""
+    eb = [max(i + 32 - 64, 0) for i in range(129)]
+    e = np.zeros(R.EDGE_PX, np.uint8)
+    e[124:128], e[128], e[129:133] = eb[60:64], eb[64], eb[65:69]
+    kats = [(0, 3, [32] * 16), (0, 2, [35] * 16), (0, 1, [30] * 16), (0, 0, [128] * 16),
+            (1, 3, [33, 34, 35, 36] * 4), (2, 3, [31] * 4 + [30] * 4 + [29] * 4 + [28] * 4),
+            (12, 3, [32, 34, 35, 36, 30, 32, 32, 36, 29, 32, 32, 32, 28, 28, 32, 32]),
+            (9, 3, [32, 34, 35, 35, 30, 32, 33, 34, 29, 31, 32, 32, 29, 30, 32, 32]),
+            (11, 3, [31, 33, 34, 35, 30, 33, 34, 35, 29, 32, 34, 34, 28, 31, 33, 34]),
+            (10, 3, [33, 34, 35, 36, 31, 31, 32, 33, 30, 30, 30, 31, 29, 30, 30, 30])]
+    jobs = np.zeros(len(kats), dtype=R.INTRA_JOB)
+    for k, (m, v, _) in enumerate(kats):
+        jobs[k] = (0, 4 * k, m, v)
+    dst = R.DevicePlane(4, 4 * len(kats), 0, 0, 0, 0, False)
+    R.predict_intra_batch(dst, jobs, np.tile(e, (len(kats), 1)), 0, 8)
+    got = dst.download_visible()
+    for k, (m, v, want) in enumerate(kats):
+        assert got[4 * k:4 * k + 4].ravel().tolist() == want, (m, v)

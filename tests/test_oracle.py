@@ -459,3 +459,55 @@ def test_propagate_importances_matches_restatement(n_unique):
                                   out0)
     want = _py_propagate(org, pad, pad, ref, pad, pad, nbx, nby, mvs, intra, imp, n_unique, out0)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+# ---- intra prediction: the reference's own known answers -------------------
+def _kat_edge(bd=8, fill=None):
+    """pred_matches_u8's edge_buf (src/predict.rs:1047-1056) mapped into the
+    257-pixel layout: edge_buf[i] = (i + 32).saturating_sub(64); left =
+    edge_buf[60..64] (bottom-to-top), top_left = edge_buf[64], above =
+    edge_buf[65..69]."""
+    e = np.zeros(257, dtype=np.uint16 if bd > 8 else np.uint8)
+    if fill is not None:
+        e[:] = fill
+        return e
+    eb = [max(i + 32 - 64, 0) for i in range(129)]
+    e[124:128] = eb[60:64]
+    e[128] = eb[64]
+    e[129:133] = eb[65:69]
+    return e
+
+
+def test_intra_pred_matches_u8_kats():
+    """src/predict.rs:1047-1107 (mode, PredictionVariant) -> expected 4x4."""
+    e = _kat_edge()
+    kats = [
+        (0, 3, [32] * 16), (0, 2, [35] * 16), (0, 1, [30] * 16), (0, 0, [128] * 16),
+        (1, 3, [33, 34, 35, 36] * 4),
+        (2, 3, [31] * 4 + [30] * 4 + [29] * 4 + [28] * 4),
+        (12, 3, [32, 34, 35, 36, 30, 32, 32, 36, 29, 32, 32, 32, 28, 28, 32, 32]),
+        (9, 3, [32, 34, 35, 35, 30, 32, 33, 34, 29, 31, 32, 32, 29, 30, 32, 32]),
+        (11, 3, [31, 33, 34, 35, 30, 33, 34, 35, 29, 32, 34, 34, 28, 31, 33, 34]),
+        (10, 3, [33, 34, 35, 36, 31, 31, 32, 33, 30, 30, 30, 31, 29, 30, 30, 30]),
+    ]
+    for mode, variant, want in kats:
+        got = O.predict_intra(mode, variant, 4, 4, e, 8)
+        assert got.ravel().tolist() == want, (mode, variant, got.ravel().tolist())
+
+
+def test_intra_pred_max_kats():
+    """src/predict.rs:1109-1170: 12-bit maximum edges predict the maximum."""
+    e = _kat_edge(12, 4095)
+    for mode in (0, 2, 1, 12, 9, 11, 10):
+        assert (O.predict_intra(mode, 3, 4, 4, e, 12) == 4095).all(), mode
+
+
+def test_intra_directional_constant_edges():
+    """A constant edge predicts the constant in every mode and size (the
+    directional interpolation weights sum to 32, the smooth ones to 256)."""
+    for bd, v in ((8, 77), (10, 901), (12, 3000)):
+        e = _kat_edge(bd, v)
+        for tx in (0, 1, 4, 5, 12, 17):
+            w, h = 1 << O.TX_W_LOG2[tx], 1 << O.TX_H_LOG2[tx]
+            for mode in range(13):
+                assert (O.predict_intra(mode, 3, w, h, e, bd) == v).all(), (bd, tx, mode)
