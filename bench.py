@@ -41,9 +41,16 @@ CONFIGS = {
 }
 TIMING_STRIDE = 4  # in GOPs
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
+# VALU issue peaks, G wave64 instructions/s over 256 CUs at 2.4 GHz: the
+# guide's 2 cycles per wave instruction per SIMD (MI355X_MICROARCH.md "Wave
+# scheduling"), and the rate measured for the integer SAD / dot / alignbyte
+# instructions these kernels are built from: ~0.9 wave-instr per CU-cycle
+# at full occupancy (tools/ubench/valu_rates.hip, profiles/valu_rates.txt)
+VALU_PEAK_GUIDE = 256 * 4 * 2.4 / 2
+VALU_PEAK_INT = 256 * 1 * 2.4
 STAGES = ["F0_pyramid", "F1_full_search", "F2_diamond_half", "F3_diamond_fullpel",
-          "F3_diamond_subpel", "F4_rdo_candidates", "F4_rd_cost_argmin", "F6_commit",
-          "F5_importance_satd", "F7_pad_exchange"]
+          "F3_diamond_subpel", "F4_rdo_single_ref", "F4_rdo_compound", "F4_rd_cost_argmin",
+          "F6_commit", "F5_importance_satd", "F7_pad_exchange"]
 
 
 def coarse_windows(W, H, R, scale, tiling, group):
@@ -266,9 +273,9 @@ def main():
     # transform block the same at 32 (U and V)
     ns, nc = n_single / ev_frames, n_comp / ev_frames
     rdo_bytes = float(ns * ((71 * 71 + 64 * 64) * px + 24) +
-                      nc * ((2 * 71 * 71 + 64 * 64) * px + 24) +
-                      2 * ntx_c * (ns * ((39 * 39 + 32 * 32) * px + 24) +
-                                   nc * ((2 * 39 * 39 + 32 * 32) * px + 24)))
+                      2 * ntx_c * ns * ((39 * 39 + 32 * 32) * px + 24))
+    comp_bytes = float(nc * ((2 * 71 * 71 + 64 * 64) * px + 24) +
+                       2 * ntx_c * nc * ((2 * 39 * 39 + 32 * 32) * px + 24))
     # commit: one candidate per superblock, + levels and the reconstruction
     commit_bytes = float(nsb * ((71 * 71 + 2 * 64 * 64) * px + 4096 + 16) +
                          2 * nsb * ntx_c * ((39 * 39 + 2 * 32 * 32) * px + 4096))
@@ -279,7 +286,8 @@ def main():
         "diamond_subpel_64": dict(ms=float(ms[4]),
                                   bytes=nj * (64 * 64 * px + 80) + ev_sub / ev_frames * 71 * 71 * px),
         "rdo_candidates": dict(ms=float(ms[5]), bytes=rdo_bytes),
-        "rdo_commit": dict(ms=float(ms[7]), bytes=commit_bytes),
+        "rdo_compound": dict(ms=float(ms[6]), bytes=comp_bytes),
+        "rdo_commit": dict(ms=float(ms[8]), bytes=commit_bytes),
     }
     dom = max(kernels, key=lambda n: kernels[n]["ms"])
     kd = kernels[dom]
@@ -292,6 +300,17 @@ def main():
                          "git": tr[1]["git"]} if tr else None),
             "avg_launch_ms": round(kd["ms"], 5),
             "algorithmic_bytes_per_launch": round(kd["bytes"])}
+    vp = _profile_entry(args, dom, bd, "valu")
+    if vp:
+        # instructions per launch from the committed SQ pass; time from this run
+        insts = vp[0]["SQ_INSTS_VALU"]
+        achv = insts / launch_s / 1e9
+        roof["valu"] = {"achieved": round(achv, 1), "unit": "G wave64 VALU instr/s",
+                        "peak_guide": VALU_PEAK_GUIDE, "frac_guide": round(achv / VALU_PEAK_GUIDE, 4),
+                        "peak_int_measured": VALU_PEAK_INT,
+                        "frac_int_measured": round(achv / VALU_PEAK_INT, 4),
+                        "insts_per_launch": round(insts), "source": vp[1]["source"],
+                        "git": vp[1]["git"]}
     fps = args.steps / dt  # frames of the one stream
 
     cpu = parity = None

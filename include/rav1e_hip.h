@@ -512,12 +512,13 @@ int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
 int rv_replay_set_timing(rv_replay *r, int stride, int block);
 /* Kernel-time breakdown of the last instrumented frame (HIP events on the
  * replay stream), ms: [0] F0 pyramid + box sums, [1] F1 full search, [2] F2
- * half-res diamond, [3] F3 full-pel diamond, [4] F3 sub-pel diamond, [5] F4
- * fused candidate launch (luma: MC + skip distortion + diff + fwd TX_64X64
- * + quantize + estimate_rate + inverse + add + non-skip distortion; chroma
- * U and V: the same with TX_32X32 and SSE), [6] F4 rd cost + argmin, [7] F6
- * commit, [8] F5 importance, [9] F7 pad / exchange.  Returns the count
- * written (<= 10). */
+ * half-res diamond, [3] F3 full-pel diamond, [4] F3 sub-pel diamond + the
+ * candidate list, [5] F4 fused single-reference candidate launch (luma: MC
+ * + skip distortion + diff + fwd TX_64X64 + quantize + estimate_rate +
+ * inverse + add + non-skip distortion; chroma U and V: the same with
+ * TX_32X32 and SSE), [6] F4 compound candidates, [7] F4 rd cost + argmin,
+ * [8] F6 commit, [9] F5 importance, [10] F7 pad / exchange.  Returns the
+ * count written (<= 11). */
 int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
 /* Same breakdown summed over the last `last_frames` instrumented frames
  * (<= 64). */

@@ -363,7 +363,7 @@ struct rv_replay {
   // frame.  Every `timing_stride`-th block of frames is instrumented (each
   // record costs ~4.4 us of idle GPU between kernels on MI355X).
   static constexpr int kRing = 64;
-  static constexpr int kEv = 11;
+  static constexpr int kEv = 12;
   hipEvent_t evs[kRing][kEv];
   int timing_stride = 1, timing_block = 1;
   long timed = 0;
@@ -916,8 +916,9 @@ int rv_replay_import(rv_replay *r) {
   return pad_slot(r, s);
 }
 
-// Event layout per instrumented frame: e[0] start, e[1..10] after F0, F1,
-// F2, F3 full-pel, F3 sub-pel, F4 score, F4 argmin, F6 commit, F5, F7.
+// Event layout per instrumented frame: e[0] start, e[1..11] after F0, F1,
+// F2, F3 full-pel, F3 sub-pel, F4 single-reference candidates, F4 compound
+// candidates, F4 argmin, F6 commit, F5, F7.
 int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   if (!r) return rv_set_error(RV_EINVAL, "rv_replay_frame: null");
   const Geo &g = r->g;
@@ -1057,16 +1058,19 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     lc.cand_base = cc.cand_base = nsingle;
     lc.n_tx = g.nsb * cg.comp;
     cc.n_tx = g.nsb * cg.comp * ntx_c;
+    RV_EV(6);
     RV_R(rv_rdo_candidates(lc, cc, g.hbd, st, true));
+  } else {
+    RV_EV(6);
   }
-  RV_EV(6);
+  RV_EV(7);
   score_candidates<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, cg, L.lambda, L.ds[1], L.ds[2], r->sub,
                                                      r->l_out,
                                                      r->c_out, r->c_out + nct * 3, ntx_c, r->win,
                                                      r->coarse, r->half, r->full, r->words,
                                                      r->cand_count, r->tail + 2,
                                                      r->cand_evals + 2 * slot);
-  RV_EV(7);
+  RV_EV(8);
   // F6 commit the winners into the frame
   la.commit = ca.commit = 1;
   la.list = ca.list = nullptr;
@@ -1075,7 +1079,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   ca.n_tx = g.nsb * ntx_c;
   la.ntx_per_cand = 1;
   RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
-  RV_EV(8);
+  RV_EV(9);
   // F5 importance SATD against reference 0 (the sum was zeroed by the argmin)
   {
     const unsigned nb = (unsigned)((r->n_imp + 255) / 256);
@@ -1086,7 +1090,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       importance_kernel<uint8_t><<<nb, 256, 0, st>>>(g, cur.y, ref[0]->y, r->sub, r->imp_bx,
                                                      r->imp_by, r->tail + 2);
   }
-  RV_EV(9);
+  RV_EV(10);
   // F7 the reconstruction becomes a reference
   r->coded++;
   r->last = fi;
@@ -1107,7 +1111,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
 #endif
     }
   }
-  RV_EV(10);
+  RV_EV(11);
 #undef RV_EV
   if (info) *info = fi;
   RV_H(hipGetLastError());

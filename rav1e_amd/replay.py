@@ -281,15 +281,15 @@ class HipReplay:
         _check(lib().rv_replay_set_timing(self.h, stride, block), "rv_replay_set_timing")
 
     def stage_ms(self) -> np.ndarray:
-        out = np.zeros(10, dtype=np.float32)
-        n = lib().rv_replay_stage_times(self.h, out.ctypes.data, 10)
+        out = np.zeros(11, dtype=np.float32)
+        n = lib().rv_replay_stage_times(self.h, out.ctypes.data, 11)
         if n < 0:
             _check(n, "rv_replay_stage_times")
         return out[:n]
 
     def stage_ms_sum(self, last_frames: int) -> np.ndarray:
-        out = np.zeros(10, dtype=np.float32)
-        n = lib().rv_replay_stage_times_sum(self.h, last_frames, out.ctypes.data, 10)
+        out = np.zeros(11, dtype=np.float32)
+        n = lib().rv_replay_stage_times_sum(self.h, last_frames, out.ctypes.data, 11)
         if n < 0:
             _check(n, "rv_replay_stage_times_sum")
         return out[:n]

@@ -29,8 +29,10 @@ __global__ __launch_bounds__(256) void k(uint32_t *out, uint32_t seed) {
         typedef short s2 __attribute__((ext_vector_type(2)));
         a[i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(s2, b), __builtin_bit_cast(s2, c + i), (int)a[i], false);
       }
-      if constexpr (OP == 4) a[i] = __mul24((int)b, (int)(c + i)) + a[i];
-      if constexpr (OP == 5) a[i] = a[i] + (b ^ i);
+      // dependent on the accumulator, so the compiler cannot hoist or fold
+      // the loop (8 independent chains per lane, 8 waves per SIMD)
+      if constexpr (OP == 4) a[i] = __mul24((int)a[i], (int)(c + i)) + b;
+      if constexpr (OP == 5) a[i] = (a[i] ^ b) + c;
       if constexpr (OP == 6) a[i] = __builtin_amdgcn_alignbyte(b, a[i], c);
     }
     if constexpr (OP == 7) {
