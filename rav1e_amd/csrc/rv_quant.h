@@ -137,7 +137,7 @@ __device__ __forceinline__ int quantize_block(const QCtx &c, const uint16_t *sca
   }
   // lanes of this group in the wavefront's 64-bit masks
   const int wl = threadIdx.x & 63;
-  const uint64_t gmask = LPB == 64 ? ~0ull : (0xFFFFFFFFull << (wl & 32));
+  const uint64_t gmask = LPB == 64 ? ~0ull : (((1ull << LPB) - 1) << (wl & ~(LPB - 1)));
   const uint64_t sig = __ballot(last >= 1) & gmask;
   // chunks ascend with the lane, so the highest lane holding a significant
   // coefficient holds the eob

@@ -40,6 +40,7 @@ struct RdoArgs {
   int commit;          // 0: score every candidate, 1: commit the winners
   int ntx_per_cand;    // transform blocks per candidate
   int bd;
+  int bsize;           // luma block size of this launch's superblock grid (64 .. 8)
   int mb_w, mb_h;      // prediction block (filter choice)
   int sub_w, sub_h;    // SSE distortion sub-block (chroma)
   int xdec, ydec;      // this plane type's subsampling
@@ -58,3 +59,9 @@ int rv_quant_ctx(int qindex, int tx_area, int is_intra, int bit_depth, int dc_de
 // transform blocks of planes U and V (32x32, SSE) in one launch.
 int rv_rdo_candidates(const rv::RdoArgs &luma, const rv::RdoArgs &chroma, int hbd,
                       hipStream_t s, bool compound = false);
+
+// Blocks below 64x64 (speed 6): one launch over the tasks of a (luma or
+// the two chroma planes) for transform size n_tx_size; mode 0 single,
+// 1 compound (score), 2 commit.
+int rv_rdo_blocks(const rv::RdoArgs &a, bool luma, int nplanes, int n_tx_size, int hbd,
+                  hipStream_t s, int mode);

@@ -129,8 +129,8 @@ __device__ __forceinline__ RdoJob rdo_job(const RdoArgs &a, const RdoPlane &pl, 
     j.ref = c / a.g.M;
   }
   const int sx = sb % a.g.tw, sy = sb / a.g.tw;
-  j.bx = ((a.g.tx0 + sx) * 64) >> a.xdec;
-  j.by = ((a.g.ty0 + sy) * 64) >> a.ydec;
+  j.bx = ((a.g.tx0 + sx) * a.bsize) >> a.xdec;
+  j.by = ((a.g.ty0 + sy) * a.bsize) >> a.ydec;
   const int txc = a.mb_w / N;
   j.ox = (sub % txc) * N;
   j.oy = (sub / txc) * N;
@@ -237,7 +237,8 @@ __device__ __forceinline__ void mc_compound(const RdoArgs &a, const RdoPlane &pl
   constexpr int B = (int)sizeof(Px);
   constexpr int P = B == 1 ? ((N + 8 + 15) / 16) * 16 : ((2 * (N + 8) + 15) / 16) * 16;
   constexpr int kRowDw = ((N + 7) * B + 3) / 4, kTot = (RB + 7) * kRowDw;
-  static_assert(RB % 8 == 0 && N % RB == 0, "bands of whole 8-row groups");
+  static_assert((RB % 8 == 0 || RB < 8) && N % RB == 0, "bands of whole 8-row groups");
+  constexpr int U = RB < 8 ? RB : 8;
   const int col = threadIdx.x & (N - 1);
   const int ib = a.bd == 12 ? 2 : 4, maxv = (1 << a.bd) - 1;
   const McF f0 = mc_setup<Px>(jb.cf, jb.rf, a.mb_w, a.mb_h);
@@ -268,9 +269,9 @@ __device__ __forceinline__ void mc_compound(const RdoArgs &a, const RdoPlane &pl
     }
     g0[0] = g0[6] = g0[7] = g1[0] = g1[6] = g1[7] = 0;
 #pragma unroll 1
-    for (int r0 = 0; r0 < RB; r0 += 8) {
+    for (int r0 = 0; r0 < RB; r0 += U) {
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < U; u++) {
         const int r = r0 + u;
         g0[(u + 6) & 7] = mc_h<Px>(f0, w0 + (r + 6) * (P / 4), col, ib);
         g1[(u + 6) & 7] = mc_h<Px>(f1, w1 + (r + 6) * (P / 4), col, ib);
@@ -359,22 +360,58 @@ __device__ __forceinline__ uint64_t rdo_sse_biased(const RdoArgs &a, const RdoJo
   return acc;
 }
 
+// compute_distortion of one transform block (the lane's partial): luma
+// cdef_dist_wxh_8x8 x bias per 8x8 (src/rdo.rs:263-283), chroma sse_wxh.
+template <typename Px, int N, int LPB, bool LUMA>
+__device__ __forceinline__ uint64_t rdo_dist_biased(const RdoArgs &a, const RdoJob &j, const Px *o,
+                                                    int64_t os, const Px *d) {
+  if constexpr (LUMA) {
+    constexpr int NB = N / 8;
+    const int lane = threadIdx.x & (LPB - 1);
+    uint64_t acc = 0;
+    for (int k = lane; k < NB * NB; k += LPB) {
+      const int by = k / NB, bx = k - by * NB;
+      const uint64_t v = rdo_cdef_8x8<Px>(o + (int64_t)(by * 8) * os + bx * 8, os,
+                                          d + by * 8 * N + bx * 8, N, a.bd);
+      const int px = j.bx + j.ox + bx * 8, py = j.by + j.oy + by * 8;
+      acc += rdo_biased(v, rdo_bias(a, px >> 2, py >> 2));
+    }
+    return acc;
+  } else {
+    return rdo_sse_biased<Px, N, LPB>(a, j, o, os, d);
+  }
+}
+
 // LPB = lanes per transform block: 64 (luma, N = 64) or 32 (chroma, N = 32:
 // a wavefront carries two chroma blocks, one per half, so every phase keeps
 // all 64 lanes busy).  `valid` = false for a second half without a block:
 // it recomputes its partner's block and stores nothing.
+// Bytes of a transform block's LDS slab: the i32 coefficient block, the MC
+// window, or the two compound windows, whichever is largest.
+template <typename Px, int N>
+__host__ __device__ constexpr int rdo_slab_bytes() {
+  constexpr int B = (int)sizeof(Px);
+  constexpr int P = B == 1 ? ((N + 8 + 15) / 16) * 16 : ((2 * (N + 8) + 15) / 16) * 16;
+  constexpr int RB = N < 16 ? N : 16;
+  constexpr int a = N * (N + 1) * 4, b = (N + 7) * P, c = 2 * (RB + 7) * P;
+  return ((a > b ? a : b) > c ? (a > b ? a : b) : c);
+}
+
 // MODE: 0 single-reference candidates, 1 compound candidates, 2 either
-// (by the job: the commit launch).
-template <typename Px, int N, int LPB, int MODE>
+// (by the job: the commit launch).  LUMA: the distortion is cdef_dist_wxh
+// per 8x8 (N >= 8), else sse_wxh per importance sub-block.  `buf` holds
+// rdo_slab_bytes<Px, N>().
+template <typename Px, int N, int LPB, int MODE, bool LUMA = false>
 __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &pl, int t,
                                               bool valid, int32_t *buf, Px *pred,
                                               const uint16_t *scan) {
   constexpr int B = (int)sizeof(Px);
   constexpr int S = N + 1;                       // padded LDS row (i32)
   constexpr int G = LPB / N, RG = N / G;         // MC lane groups
+  constexpr int U = RG < 8 ? RG : 8;             // MC rows per ring step
   constexpr int P = B == 1 ? ((N + 8 + 15) / 16) * 16 : ((2 * (N + 8) + 15) / 16) * 16;
   constexpr int C32 = N < 32 ? N : 32;           // coded coefficient extent
-  static_assert((N + 7) * P <= N * S * 4, "window must fit the coefficient slab");
+  static_assert(!LUMA || N >= 8, "cdef distortion runs on 8x8 blocks");
   const int lane = threadIdx.x & (LPB - 1);
   const RdoJob jb = rdo_job<N>(a, pl, t);
   const rv_plane &ref = pl.ref[jb.ref];
@@ -391,7 +428,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   if (MODE == 1 || (MODE == 2 && jb.comp)) {
     static_assert(2 * (16 + 7) * (sizeof(Px) == 1 ? 48 : 80) <= N * (N + 1) * 4 || N != 32,
                   "compound windows must fit the coefficient slab");
-    mc_compound<Px, N, 16>(a, pl, jb, reinterpret_cast<uint32_t *>(buf), pred);
+    mc_compound<Px, N, (N < 16 ? N : 16)>(a, pl, jb, reinterpret_cast<uint32_t *>(buf), pred);
   } else
   {
     uint32_t *win = reinterpret_cast<uint32_t *>(buf);
@@ -463,11 +500,11 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
 #pragma unroll
     for (int k = 1; k < 6; k++) ring[k] = hval(k);
     ring[0] = ring[6] = ring[7] = 0;
-    static_assert(RG % 8 == 0, "MC rows run in groups of 8 (static ring indices)");
+    static_assert(RG % 8 == 0 || RG < 8, "MC rows run in groups of 8 (static ring indices)");
 #pragma unroll 1
-    for (int r0 = 0; r0 < RG; r0 += 8) {
+    for (int r0 = 0; r0 < RG; r0 += U) {
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < U; u++) {
         const int r = r0 + u;
         ring[(u + 6) & 7] = hval(r + 6);
         int32_t v;
@@ -488,7 +525,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   const int64_t ost = pl.org.stride;
   // ---- skip variant: sse_wxh of the prediction ------------------------------
   if (!a.commit) {
-    const uint64_t d = group_sum<LPB>(rdo_sse_biased<Px, N, LPB>(a, jb, o, ost, pred));
+    const uint64_t d = group_sum<LPB>(rdo_dist_biased<Px, N, LPB, LUMA>(a, jb, o, ost, pred));
     if (valid && lane == 0) pl.out[(int64_t)jb.oi * 3 + 0] = d;
   }
 
@@ -621,7 +658,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     return;
   }
   // ---- non-skip variant: sse_wxh of the reconstruction ----------------------
-  const uint64_t d = group_sum<LPB>(rdo_sse_biased<Px, N, LPB>(a, jb, o, ost, pred));
+  const uint64_t d = group_sum<LPB>(rdo_dist_biased<Px, N, LPB, LUMA>(a, jb, o, ost, pred));
   if (valid && lane == 0) pl.out[(int64_t)jb.oi * 3 + 1] = d;
 }
 
@@ -1071,6 +1108,44 @@ using namespace rv;
 
 // Replay-internal entry (rv_replay.hip): luma (N = 64, cdef distortion)
 // and both chroma planes (N = 32, SSE) of every task, one launch on `s`.
+// Blocks below 64x64 (the speed-6 partition search): N x N transform
+// blocks, N lanes each (64 / N per wavefront, four wavefronts per
+// workgroup); the launch's tasks cover plane p[0] then p[1] (chroma).
+template <typename Px, int N, int MODE, bool LUMA>
+__global__ __launch_bounds__(256) void rdo_small_kernel(RdoArgs a, int nplanes) {
+  constexpr int TPW = 64 / N;
+  constexpr int SLAB = rdo_slab_bytes<Px, N>();
+  constexpr int PER = (SLAB + N * N * (int)sizeof(Px) + 15) / 16 * 16;
+  __shared__ __align__(16) uint8_t lds[4 * TPW * PER];
+  __shared__ uint16_t scan[1024];
+  stage_scan(scan, a.q_tx_index);
+  const int wave = threadIdx.x >> 6, g = (threadIdx.x & 63) / N;
+  const int n = rdo_ntx(a), total = n * nplanes;
+  const int w0 = (blockIdx.x * 4 + wave) * TPW;
+  if (w0 >= total) return;  // the whole wavefront is past the tasks
+  const int i = w0 + g;
+  const bool valid = i < total;
+  const int ii = valid ? i : total - 1;  // recomputed, nothing stored
+  const int plane = ii / n, t = ii - plane * n;
+  uint8_t *mine = lds + (wave * TPW + g) * PER;
+  rdo_cand_body<Px, N, N, MODE, LUMA>(a, a.p[plane], t, valid, reinterpret_cast<int32_t *>(mine),
+                                       reinterpret_cast<Px *>(mine + SLAB), scan);
+}
+
+template <int N, bool LUMA>
+static void rdo_small_launch(const RdoArgs &a, int nplanes, int hbd, hipStream_t s, int mode) {
+  constexpr int TPW = 64 / N;
+  const unsigned grid = (unsigned)((a.n_tx * nplanes + 4 * TPW - 1) / (4 * TPW));
+  if (grid == 0) return;
+#define RV_SMALL(PX, M) rdo_small_kernel<PX, N, M, LUMA><<<grid, 256, 0, s>>>(a, nplanes)
+  if (hbd) {
+    if (mode == 0) RV_SMALL(uint16_t, 0); else if (mode == 1) RV_SMALL(uint16_t, 1); else RV_SMALL(uint16_t, 2);
+  } else {
+    if (mode == 0) RV_SMALL(uint8_t, 0); else if (mode == 1) RV_SMALL(uint8_t, 1); else RV_SMALL(uint8_t, 2);
+  }
+#undef RV_SMALL
+}
+
 template <int MODE>
 static void rdo_launch(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s,
                        bool single, unsigned cpairs) {
@@ -1109,6 +1184,26 @@ int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipSt
     rdo_launch<1>(luma, chroma, hbd, s, single, cpairs);
   else
     rdo_launch<0>(luma, chroma, hbd, s, single, cpairs);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+// The speed-6 levels: luma N x N (N = 32, 16, 8; cdef distortion) or the
+// chroma planes' transform blocks (N = 16, 8, 4 in 4:2:0; SSE) of every task.
+int rv_rdo_blocks(const RdoArgs &a, bool luma, int nplanes, int n_tx_size, int hbd,
+                  hipStream_t s, int mode) {
+  if (luma) {
+    if (n_tx_size == 32) rdo_small_launch<32, true>(a, nplanes, hbd, s, mode);
+    else if (n_tx_size == 16) rdo_small_launch<16, true>(a, nplanes, hbd, s, mode);
+    else if (n_tx_size == 8) rdo_small_launch<8, true>(a, nplanes, hbd, s, mode);
+    else return rv_set_error(RV_EINVAL, "rv_rdo_blocks: luma size");
+  } else {
+    if (n_tx_size == 32) rdo_small_launch<32, false>(a, nplanes, hbd, s, mode);
+    else if (n_tx_size == 16) rdo_small_launch<16, false>(a, nplanes, hbd, s, mode);
+    else if (n_tx_size == 8) rdo_small_launch<8, false>(a, nplanes, hbd, s, mode);
+    else if (n_tx_size == 4) rdo_small_launch<4, false>(a, nplanes, hbd, s, mode);
+    else return rv_set_error(RV_EINVAL, "rv_rdo_blocks: chroma size");
+  }
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

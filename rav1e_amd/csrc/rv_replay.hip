@@ -1022,6 +1022,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   la.count = r->cand_count;
   la.ntx_per_cand = 1;
   la.bd = g.bd;
+  la.bsize = kSb;
   la.mb_w = la.mb_h = kSb;
   la.sub_w = la.sub_h = 8;
   la.p[0].q = L.ql;
