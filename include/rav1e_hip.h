@@ -435,6 +435,18 @@ typedef struct rv_replay_cfg {
  * by successive elimination over box-sum tables (rv_full_search_sea_batch;
  * same results, the default for bit depth <= 10). */
 #define RV_REPLAY_EXHAUSTIVE_FS 4
+/* flags: the speed-6 schedule (config D; SpeedSettings::from_preset(6),
+ * src/api/config.rs:309-460): every inter frame also searches and scores
+ * 32x32, 16x16 and 8x8 blocks (motion_estimation per block, SATD sub-pel),
+ * picks the partition top-down (PARTITION_NONE vs PARTITION_SPLIT,
+ * rdo_partition_decision, src/rdo.rs:1500-1668; must_split past the frame
+ * edge, src/encoder.rs:2392-2470) and commits the leaves.  Needs xdec ==
+ * ydec.  Result words: the 64x64 words, then per 32x32 / 16x16 / 8x8 block
+ * of the group [(full-pel MV, cost, sub-pel MV, cost) per reference,
+ * winner, skip, cost bits, distortion], then one partition mask per
+ * superblock (bit 0: 64x64 split, 1 + q: 32x32 quadrant q split, 5 + 4 *
+ * row + col: 16x16 split), then the 5 tail words. */
+#define RV_REPLAY_SPEED6 8
 typedef struct rv_replay_frame_info {
   int32_t display;            /* display index of the coded frame */
   int32_t me_range_scale;     /* 4 >> pyramid level (src/encoder.rs:838) */

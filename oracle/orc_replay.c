@@ -72,6 +72,20 @@ typedef struct orc_replay {
   uint64_t *words;
   int32_t *lev; /* committed levels: per SB luma 1024 + 2 * ntx_c * 1024 */
   uint64_t tail[5];
+  /* speed 6 (orc_replay_set_speed): the 32x32, 16x16 and 8x8 levels */
+  int s6;
+  struct olevel {
+    int B, n, gw, gh, bc, bch, txl, txc, tx0, ty0, tws, ths;
+    orc_mv *full, *sub; /* [R][n] */
+    uint64_t *fc, *sc;
+    double *cost;       /* the winners' rd cost */
+    int32_t *lev;       /* per block: luma B * B, then U, V bc * bch */
+    uint8_t *leaf;      /* committed by the partition decision */
+    size_t woff;
+  } pl[4];
+  orc_qctx qs[3][4][3];
+  uint8_t *leaf0;
+  size_t nwords, wpart;
   pthread_mutex_t mu;
   int next_sb, pass, sb_limit;
 } orc_replay;
@@ -134,18 +148,24 @@ static orc_mv qfull(orc_mv m) {
 }
 static int mv_eq(orc_mv a, orc_mv b) { return a.row == b.row && a.col == b.col; }
 
+/* A block grid (superblocks, or one speed-6 level): rv_chain.h CandGeo */
+typedef struct {
+  int nsb, tw, tx0, ty0, tws, ths;
+  const orc_mv *sub; /* [R][nsb] sub-pel winners (NEWMV) */
+} cgeo;
+
 /* The MV stack and candidate MVs of rv_chain.h cand_stack / cand_mv: the
  * row above, then the column to the left (merged if equal), inside the
  * tile; NEARESTMV, NEAR0MV, GLOBALMV, NEWMV per reference
  * (src/rdo.rs:880-905). */
-static int cand_mv(const orc_replay *r, int sb, int c, orc_mv *mv) {
+static int cand_mv_g(const cgeo *g, int sb, int c, orc_mv *mv) {
   int k = c / NMODE, m = c % NMODE;
-  int sx = sb % r->tw, sy = sb / r->tw, fx = r->tx0 + sx, fy = r->ty0 + sy;
-  const orc_mv *s = r->sub + (size_t)k * r->nsb;
+  int sx = sb % g->tw, sy = sb / g->tw, fx = g->tx0 + sx, fy = g->ty0 + sy;
+  const orc_mv *s = g->sub + (size_t)k * g->nsb;
   orc_mv st[2], zero = {0, 0};
   int n = 0;
-  if (fy % r->ths) st[n++] = s[sb - r->tw];
-  if (fx % r->tws) {
+  if (fy % g->ths) st[n++] = s[sb - g->tw];
+  if (fx % g->tws) {
     orc_mv v = s[sb - 1];
     if (n == 0 || !mv_eq(v, st[0])) st[n++] = v;
   }
@@ -172,17 +192,17 @@ static int cand_mv(const orc_replay *r, int sb, int c, orc_mv *mv) {
  * GLOBAL_GLOBALMV, NEAREST_NEARESTMV, NEW_NEWMV, NEAREST_NEWMV,
  * NEW_NEARESTMV, NEAR_NEARMV over the (ref 0, ref 1) stack of the above /
  * left neighbours' NEWMV pairs, merged if equal (src/rdo.rs:952-992) */
-static void comp_mvs(const orc_replay *r, int sb, int m, orc_mv *mv0, orc_mv *mv1) {
-  int sx = sb % r->tw, sy = sb / r->tw, fx = r->tx0 + sx, fy = r->ty0 + sy;
-  const orc_mv *s0 = r->sub, *s1 = r->sub + r->nsb;
+static void comp_mvs_g(const cgeo *g, int sb, int m, orc_mv *mv0, orc_mv *mv1) {
+  int sx = sb % g->tw, sy = sb / g->tw, fx = g->tx0 + sx, fy = g->ty0 + sy;
+  const orc_mv *s0 = g->sub, *s1 = g->sub + g->nsb;
   orc_mv zero = {0, 0}, e[2][2] = {{zero, zero}, {zero, zero}};
   int n = 0;
-  if (fy % r->ths) {
-    e[0][0] = s0[sb - r->tw];
-    e[0][1] = s1[sb - r->tw];
+  if (fy % g->ths) {
+    e[0][0] = s0[sb - g->tw];
+    e[0][1] = s1[sb - g->tw];
     n = 1;
   }
-  if (fx % r->tws) {
+  if (fx % g->tws) {
     orc_mv l0 = s0[sb - 1], l1 = s1[sb - 1];
     if (n == 0 || !mv_eq(l0, e[0][0]) || !mv_eq(l1, e[0][1])) {
       e[n][0] = l0;
@@ -202,6 +222,24 @@ static void comp_mvs(const orc_replay *r, int sb, int m, orc_mv *mv0, orc_mv *mv
       *mv1 = n >= 2 ? e[1][1] : zero;
       break;
   }
+}
+
+static cgeo sb_geo(const orc_replay *r) {
+  cgeo g = {r->nsb, r->tw, r->tx0, r->ty0, r->tws, r->ths, r->sub};
+  return g;
+}
+static cgeo level_geo(const orc_replay *r, int l) {
+  const struct olevel *P = &r->pl[l];
+  cgeo g = {P->n, P->gw, P->tx0, P->ty0, P->tws, P->ths, P->sub};
+  return g;
+}
+static int cand_mv(const orc_replay *r, int sb, int c, orc_mv *mv) {
+  cgeo g = sb_geo(r);
+  return cand_mv_g(&g, sb, c, mv);
+}
+static void comp_mvs(const orc_replay *r, int sb, int m, orc_mv *mv0, orc_mv *mv1) {
+  cgeo g = sb_geo(r);
+  comp_mvs_g(&g, sb, m, mv0, mv1);
 }
 
 orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile_x0, int tile_y0,
@@ -262,7 +300,8 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile
   r->hc = calloc(nr, 8);
   r->fc = calloc(nr, 8);
   r->sc = calloc(nr, 8);
-  r->words = calloc((size_t)r->nsb * (8 * r->R + 4), 8);
+  r->nwords = (size_t)r->nsb * (8 * r->R + 4);
+  r->words = calloc(r->nwords, 8);
   r->lev = calloc((size_t)r->nsb * (1024 + 2 * r->ntx_c * 1024), 4);
   pthread_mutex_init(&r->mu, NULL);
   return r;
@@ -295,8 +334,62 @@ void orc_replay_destroy(orc_replay *r) {
   free(r->sc);
   free(r->words);
   free(r->lev);
+  for (int l = 1; l < 4; l++) {
+    struct olevel *P = &r->pl[l];
+    free(P->full);
+    free(P->sub);
+    free(P->fc);
+    free(P->sc);
+    free(P->cost);
+    free(P->lev);
+    free(P->leaf);
+  }
+  free(r->leaf0);
   pthread_mutex_destroy(&r->mu);
   free(r);
+}
+
+/* The speed-6 schedule (RV_REPLAY_SPEED6); call before the level params.
+ * speed 10 is the default. */
+int orc_replay_set_speed(orc_replay *r, int speed) {
+  if (speed != 6 && speed != 10) return -1;
+  if (speed == 10 || r->s6) return 0;
+  if (r->xdec != r->ydec) return -1;
+  r->s6 = 1;
+  r->nwords = (size_t)r->nsb * (8 * r->R + 4);
+  for (int l = 1; l < 4; l++) {
+    struct olevel *P = &r->pl[l];
+    int k = 1 << l;
+    P->B = SB >> l;
+    P->gw = r->tw * k;
+    P->gh = r->th * k;
+    P->n = P->gw * P->gh;
+    P->bc = P->B >> r->xdec;
+    P->bch = P->B >> r->ydec;
+    P->txl = 4 - l;
+    P->txc = P->bc == 32 ? 3 : P->bc == 16 ? 2 : P->bc == 8 ? 1 : 0;
+    P->tx0 = r->tx0 * k;
+    P->ty0 = r->ty0 * k;
+    P->tws = r->tws * k;
+    P->ths = r->ths * k;
+    size_t nr = (size_t)r->R * P->n;
+    P->full = calloc(nr, sizeof(orc_mv));
+    P->sub = calloc(nr, sizeof(orc_mv));
+    P->fc = calloc(nr, 8);
+    P->sc = calloc(nr, 8);
+    P->cost = calloc(P->n, sizeof(double));
+    P->lev = calloc((size_t)P->n * (P->B * P->B + 2 * P->bc * P->bch), 4);
+    P->leaf = calloc(P->n, 1);
+    if (!P->full || !P->sub || !P->fc || !P->sc || !P->cost || !P->lev || !P->leaf) return -1;
+    P->woff = r->nwords;
+    r->nwords += (size_t)P->n * (4 * r->R + 4);
+  }
+  r->wpart = r->nwords;
+  r->nwords += (size_t)r->nsb;
+  r->leaf0 = calloc(r->nsb, 1);
+  free(r->words);
+  r->words = calloc(r->nwords, 8);
+  return r->words && r->leaf0 ? 0 : -1;
 }
 
 static void pad(const orc_replay *r, oplane *p) {
@@ -333,6 +426,9 @@ int orc_replay_set_level_params(orc_replay *r, int level, int base_q_idx, const 
     r->lv[level].ac[p] = ac[p];
     r->lv[level].ds[p] = ds[p];
     orc_qctx_update(&r->lv[level].q[p], base_q_idx, p ? 3 : 4, 0, r->bd, dc[p], ac[p]);
+    for (int l = 1; r->s6 && l < 4; l++)
+      orc_qctx_update(&r->qs[level][l][p], base_q_idx, p ? r->pl[l].txc : r->pl[l].txl, 0, r->bd,
+                      dc[p], ac[p]);
   }
   r->lv[level].lambda = lambda;
   r->lv[level].me_lambda = me_lambda;
@@ -428,62 +524,71 @@ static void ds_ctx(const orc_replay *r, orc_ds_ctx *c, const oplane *org, const 
   c->subpel = subpel;
 }
 
-/* compute_distortion_bias (src/rdo.rs:476-508) of the BLOCK_8X8
- * importance area at 4x4 block (mi_x, mi_y) */
-static double dist_bias(const orc_replay *r, int mi_x, int mi_y) {
+/* compute_distortion_bias (src/rdo.rs:476-508) of the importance area of
+ * m x m 4x4 blocks (BLOCK_8X8: m = 2; BLOCK_4X4 for chroma planes narrower
+ * than 8: m = 1) at 4x4 block (mi_x, mi_y) */
+static double dist_bias(const orc_replay *r, int mi_x, int mi_y, int m) {
   if (!r->imp) return 0.65;
-  int x2 = mi_x + 2 < r->w_in_b ? mi_x + 2 : r->w_in_b;
-  int y2 = mi_y + 2 < r->h_in_b ? mi_y + 2 : r->h_in_b;
+  int x2 = mi_x + m < r->w_in_b ? mi_x + m : r->w_in_b;
+  int y2 = mi_y + m < r->h_in_b ? mi_y + m : r->h_in_b;
   float tot = 0.f;
   for (int y = mi_y; y < y2; y++)
     for (int x = mi_x; x < x2; x++) tot += r->imp[(y >> 1) * r->w_imp + (x >> 1)];
-  float mean = tot / 4.0f;
+  float mean = tot / (float)(m * m);
   return (double)(mean / 3.0f) + 0.65;
 }
 static uint64_t biased(uint64_t v, double bias) { return (uint64_t)((double)v * bias); }
 
-/* compute_distortion (src/rdo.rs:338-411) of a 64x64 superblock at luma
- * (px, py): luma cdef_dist_wxh, chroma sse_wxh, each 8x8 / sub-block biased */
-static uint64_t sb_distortion(const orc_replay *r, const oinput *cur, int px, int py,
-                              const void *ly, const void *lu, const void *lv) {
+/* compute_distortion (src/rdo.rs:338-411) of a B x B block at luma (px,
+ * py) with bc x bch chroma blocks (predictions / reconstructions at pitch B
+ * and bc): luma cdef_dist_wxh, chroma sse_wxh, each 8x8 / importance
+ * sub-block biased */
+static uint64_t blk_distortion(const orc_replay *r, const oinput *cur, int px, int py, int B,
+                               int bc, int bch, const void *ly, const void *lu, const void *lv) {
   const int hbd = r->hbd;
   const double *ds = r->lv[r->fi.level].ds;
   uint64_t d = 0;
-  for (int j = 0; j < SB; j += 8)
-    for (int i = 0; i < SB; i += 8) {
+  for (int j = 0; j < B; j += 8)
+    for (int i = 0; i < B; i += 8) {
       int64_t mo[5];
       orc_cdef_moments_8x8(at(&cur->y, hbd, px + i, py + j), cur->y.stride,
-                           (const uint8_t *)ly + ((size_t)j * SB + i) * px_of(r), SB, hbd, mo);
-      d += biased(orc_cdef_dist_from_moments(mo, r->bd), dist_bias(r, (px + i) >> 2, (py + j) >> 2));
+                           (const uint8_t *)ly + ((size_t)j * B + i) * px_of(r), B, hbd, mo);
+      d += biased(orc_cdef_dist_from_moments(mo, r->bd),
+                  dist_bias(r, (px + i) >> 2, (py + j) >> 2, 2));
     }
   /* Distortion * dist_scale[p] -> ScaledDistortion (src/rdo.rs:375, 406) */
   d = (uint64_t)((double)d * ds[0]);
   const int cpx = px >> r->xdec, cpy = py >> r->ydec;
-  const int bw = 8 >> r->xdec, bh = 8 >> r->ydec, nbx = r->cw / bw;
+  const int iw = bc < 8 ? bc : 8, ih = bch < 8 ? bch : 8;
+  const int bw = iw >> r->xdec, bh = ih >> r->ydec, nbx = bc / bw, m = iw / 4;
   uint64_t parts[SB * SB];
   const oplane *cs[2] = {&cur->u, &cur->v};
   const void *cp[2] = {lu, lv};
   for (int pl = 0; pl < 2; pl++) {
-    int n = orc_sse_wxh(at(cs[pl], hbd, cpx, cpy), cs[pl]->stride, cp[pl], r->cw, r->cw, r->ch,
-                        r->xdec, r->ydec, hbd, parts);
+    int n = orc_sse_wxh(at(cs[pl], hbd, cpx, cpy), cs[pl]->stride, cp[pl], bc, bc, bch, r->xdec,
+                        r->ydec, hbd, parts);
     uint64_t dp = 0;
     for (int k = 0; k < n; k++) {
       int bx = k % nbx, by = k / nbx;
       int x = cpx + bx * bw, y = cpy + by * bh;
-      dp += biased(parts[k], dist_bias(r, (x << r->xdec) >> 2, (y << r->ydec) >> 2));
+      dp += biased(parts[k], dist_bias(r, (x << r->xdec) >> 2, (y << r->ydec) >> 2, m));
     }
     d += (uint64_t)((double)dp * ds[1 + pl]);
   }
   return d;
 }
+static uint64_t sb_distortion(const orc_replay *r, const oinput *cur, int px, int py,
+                              const void *ly, const void *lu, const void *lv) {
+  return blk_distortion(r, cur, px, py, SB, r->cw, r->ch, ly, lu, lv);
+}
 
 /* encode_tx_block (src/encoder.rs:1077-1237) of one transform block:
  * diff + fht + quantize, tx-domain distortion -> estimate_rate,
  * dequantize, inverse + add into `rec` (stride rs).  Returns the rate. */
-static uint64_t tx_block(const orc_replay *r, const oplane *src, int sx, int sy, void *rec, int rs,
-                         int tx_size, int plane, int32_t *levels_out) {
+static uint64_t tx_block_q(const orc_replay *r, const oplane *src, int sx, int sy, void *rec,
+                           int rs, int tx_size, int plane, int32_t *levels_out,
+                           const orc_qctx *q) {
   const int lvl = r->fi.level, qidx = r->lv[lvl].qidx;
-  const orc_qctx *q = &r->lv[lvl].q[plane];
   const int n = 1 << ORC_TX_W_LOG2[tx_size];
   int16_t res[SB * SB];
   int32_t co[SB * SB], qc[32 * 32], rc[32 * 32];
@@ -496,6 +601,11 @@ static uint64_t tx_block(const orc_replay *r, const oplane *src, int sx, int sy,
   orc_inv_txfm2d_add(rc, rec, rs, tx_size, 0, r->bd, r->hbd);
   if (levels_out) memcpy(levels_out, qc, (size_t)ca * 4);
   return rate;
+}
+static uint64_t tx_block(const orc_replay *r, const oplane *src, int sx, int sy, void *rec, int rs,
+                         int tx_size, int plane, int32_t *levels_out) {
+  return tx_block_q(r, src, sx, sy, rec, rs, tx_size, plane, levels_out,
+                    &r->lv[r->fi.level].q[plane]);
 }
 
 /* Pass A: F1-F3 for one superblock. */
@@ -560,10 +670,221 @@ static void run_me(orc_replay *r, int sb) {
     r->full[k * r->nsb + sb] = fmv;
     r->fc[k * r->nsb + sb] = cost;
     c.subpel = 1;
+    c.satd = r->s6; /* use_satd_subpel (speed <= 9) */
     orc_diamond_search(&c, &fmv, 1, &smv, &cost);
     r->sub[k * r->nsb + sb] = smv;
     r->sc[k * r->nsb + sb] = cost;
   }
+  if (!r->s6) return;
+  /* speed 6: motion_estimation of every 32x32, then 16x16 and 8x8 block of
+   * the superblock at its own position (src/me.rs:193-278), seeded with the
+   * enclosing 64x64's (32x32) or 32x32's (16x16, 8x8) sub-pel winner */
+  for (int l = 1; l < 4; l++) {
+    struct olevel *P = &r->pl[l];
+    const int k2 = 1 << l, B = P->B;
+    const struct olevel *U = &r->pl[1];
+    for (int j = 0; j < k2; j++)
+      for (int i = 0; i < k2; i++) {
+        const int bx = sx * k2 + i, by = sy * k2 + j, b = by * P->gw + bx;
+        const int X = (P->tx0 + bx) * B, Y = (P->ty0 + by) * B;
+        int mb[4];
+        mv_range(r, X >> 2, Y >> 2, B, B, mb);
+        for (int k = 0; k < R; k++) {
+          orc_mv par = l == 1 ? r->sub[k * r->nsb + sb]
+                              : U->sub[(size_t)k * U->n + (by >> (l - 1)) * U->gw + (bx >> (l - 1))];
+          orc_mv fp[2] = {zero, qfull(par)}, fmv, smv;
+          orc_ds_ctx c;
+          ds_ctx(r, &c, &cur->y, &ref[k]->y, X, Y, B, B, mb, lambda1, 0);
+          orc_diamond_search(&c, fp, 2, &fmv, &cost);
+          P->full[(size_t)k * P->n + b] = fmv;
+          P->fc[(size_t)k * P->n + b] = cost;
+          c.subpel = 1;
+          c.satd = 1;
+          orc_diamond_search(&c, &fmv, 1, &smv, &cost);
+          P->sub[(size_t)k * P->n + b] = smv;
+          P->sc[(size_t)k * P->n + b] = cost;
+        }
+      }
+  }
+}
+
+/* Speed 6: rdo_mode_decision of block b of level l (B x B luma with one
+ * TX_BxB, bc x bch chroma blocks with one transform each): the winner's
+ * words, levels and rd cost; its reconstruction into oy / ou / ov (pitch
+ * SB and r->cw). */
+static void rdo_level_block(orc_replay *r, int l, int b, const oinput *cur, const oslot **ref,
+                            uint8_t *oy, uint8_t *ou, uint8_t *ov) {
+  struct olevel *P = &r->pl[l];
+  const int R = r->R, B = P->B, bc = P->bc, bch = P->bch;
+  const size_t px = px_of(r);
+  const int X = (P->tx0 + b % P->gw) * B, Y = (P->ty0 + b / P->gw) * B;
+  const int cpx = X >> r->xdec, cpy = Y >> r->ydec;
+  const cgeo g = level_geo(r, l);
+  const int lvl = r->fi.level;
+  const double lambda = r->lv[lvl].lambda;
+  const int per = B * B + 2 * bc * bch;
+  int32_t *blev = P->lev + (size_t)b * per;
+  int32_t clev[32 * 32 * 3];
+  uint16_t ly[32 * 32], lu[32 * 32], lv[32 * 32], by_[32 * 32], bu_[32 * 32], bv_[32 * 32];
+  double best = 1.7976931348623157e308;
+  int best_c = 0, best_skip = 0;
+  uint64_t best_d = 0;
+  const int ncand = r->C + (r->fi.compound ? 6 : 0);
+  for (int c = 0; c < ncand; c++) {
+    if (c < r->C) {
+      orc_mv mv;
+      if (!cand_mv_g(&g, b, c, &mv)) continue;
+      const oslot *rf = ref[c / NMODE];
+      predict(r, &rf->y, X, Y, mv, B, B, ly, B);
+      predict(r, &rf->u, cpx, cpy, mv, bc, bch, lu, bc);
+      predict(r, &rf->v, cpx, cpy, mv, bc, bch, lv, bc);
+    } else {
+      orc_mv m0, m1;
+      comp_mvs_g(&g, b, c - r->C, &m0, &m1);
+      predict_comp(r, &ref[0]->y, &ref[1]->y, X, Y, m0, m1, B, B, ly, B);
+      predict_comp(r, &ref[0]->u, &ref[1]->u, cpx, cpy, m0, m1, bc, bch, lu, bc);
+      predict_comp(r, &ref[0]->v, &ref[1]->v, cpx, cpy, m0, m1, bc, bch, lv, bc);
+    }
+    uint64_t ds = blk_distortion(r, cur, X, Y, B, bc, bch, ly, lu, lv);
+    int zero_dist = 0;
+    double rs = (double)ds + lambda * (0.0 / 8.0);
+    if (rs < best) {
+      best = rs;
+      best_c = c;
+      best_skip = 1;
+      best_d = ds;
+      zero_dist = ds == 0;
+      memcpy(by_, ly, (size_t)B * B * px);
+      memcpy(bu_, lu, (size_t)bc * bch * px);
+      memcpy(bv_, lv, (size_t)bc * bch * px);
+    }
+    if (zero_dist) continue;
+    uint32_t rate = (uint32_t)tx_block_q(r, &cur->y, X, Y, ly, B, P->txl, 0, clev,
+                                          &r->qs[lvl][l][0]);
+    rate += (uint32_t)tx_block_q(r, &cur->u, cpx, cpy, lu, bc, P->txc, 1, clev + B * B,
+                                 &r->qs[lvl][l][1]);
+    rate += (uint32_t)tx_block_q(r, &cur->v, cpx, cpy, lv, bc, P->txc, 2,
+                                 clev + B * B + bc * bch, &r->qs[lvl][l][2]);
+    uint64_t dn = blk_distortion(r, cur, X, Y, B, bc, bch, ly, lu, lv);
+    double rn = (double)dn + lambda * ((double)rate / 8.0);
+    if (rn < best) {
+      best = rn;
+      best_c = c;
+      best_skip = 0;
+      best_d = dn;
+      memcpy(by_, ly, (size_t)B * B * px);
+      memcpy(bu_, lu, (size_t)bc * bch * px);
+      memcpy(bv_, lv, (size_t)bc * bch * px);
+      memcpy(blev, clev, (size_t)per * 4);
+    }
+  }
+  if (best_skip) memset(blev, 0, (size_t)per * 4);
+  P->cost[b] = best;
+  uint64_t *w = r->words + P->woff + (size_t)b * (4 * R + 4);
+  for (int k = 0; k < R; k++) {
+    size_t o = (size_t)k * P->n + b;
+    w[4 * k + 0] = pack_mv(P->full[o]);
+    w[4 * k + 1] = P->fc[o];
+    w[4 * k + 2] = pack_mv(P->sub[o]);
+    w[4 * k + 3] = P->sc[o];
+  }
+  uint64_t cb;
+  memcpy(&cb, &best, 8);
+  w[4 * R + 0] = (uint64_t)best_c;
+  w[4 * R + 1] = (uint64_t)best_skip;
+  w[4 * R + 2] = cb;
+  w[4 * R + 3] = best_d;
+  for (int y = 0; y < B; y++) memcpy(oy + (size_t)y * SB * px, (uint8_t *)by_ + (size_t)y * B * px, B * px);
+  for (int y = 0; y < bch; y++) {
+    memcpy(ou + (size_t)y * r->cw * px, (uint8_t *)bu_ + (size_t)y * bc * px, bc * px);
+    memcpy(ov + (size_t)y * r->cw * px, (uint8_t *)bv_ + (size_t)y * bc * px, bc * px);
+  }
+}
+
+/* encode_partition_topdown (src/encoder.rs:2392-2470) of superblock sb
+ * (rv_replay.hip partition_kernel): a block past the frame edge must split;
+ * a block that fits compares its mode decision's rd cost with the sum of its
+ * four children's (rdo_partition_decision, src/rdo.rs:1500-1668; strict
+ * `<`); 8x8 blocks are leaves.  The leaves' reconstructions (rec[l], the
+ * superblock at pitch SB / cw) go into the frame. */
+static double level_cost(const orc_replay *r, double c0, int l, int x, int y) {
+  if (l == 0) return c0;
+  const struct olevel *P = &r->pl[l];
+  return P->cost[((y / P->B) - P->ty0) * P->gw + (x / P->B) - P->tx0];
+}
+static int split_at(const orc_replay *r, double c0, int l, int x, int y) {
+  const int B = SB >> l;
+  if (x + B > r->W || y + B > r->H) return 1;
+  if (l == 3) return 0;
+  const int h = B / 2;
+  double s = 0.0;
+  s += level_cost(r, c0, l + 1, x, y);
+  s += level_cost(r, c0, l + 1, x + h, y);
+  s += level_cost(r, c0, l + 1, x, y + h);
+  s += level_cost(r, c0, l + 1, x + h, y + h);
+  return 0.0 + s < level_cost(r, c0, l, x, y);
+}
+static void commit_leaf(orc_replay *r, int l, int x, int y, int X, int Y, oslot *S,
+                        uint16_t (*ry)[SB * SB], uint16_t (*ru)[SB * SB],
+                        uint16_t (*rv)[SB * SB]) {
+  const int B = SB >> l, hbd = r->hbd, cw = r->cw;
+  const size_t px = px_of(r);
+  const int bc = B >> r->xdec, bch = B >> r->ydec;
+  const int ox = x - X, oy = y - Y, cox = ox >> r->xdec, coy = oy >> r->ydec;
+  for (int j = 0; j < B; j++)
+    memcpy(at(&S->y, hbd, x, y + j), (uint8_t *)ry[l] + ((size_t)(oy + j) * SB + ox) * px, B * px);
+  for (int j = 0; j < bch; j++) {
+    memcpy(at(&S->u, hbd, x >> r->xdec, (y >> r->ydec) + j),
+           (uint8_t *)ru[l] + ((size_t)(coy + j) * cw + cox) * px, bc * px);
+    memcpy(at(&S->v, hbd, x >> r->xdec, (y >> r->ydec) + j),
+           (uint8_t *)rv[l] + ((size_t)(coy + j) * cw + cox) * px, bc * px);
+  }
+  if (l == 0)
+    r->leaf0[((Y / SB) - r->ty0) * r->tw + (X / SB) - r->tx0] = 1;
+  else {
+    struct olevel *P = &r->pl[l];
+    P->leaf[((y / B) - P->ty0) * P->gw + (x / B) - P->tx0] = 1;
+  }
+}
+static void partition_sb(orc_replay *r, int sb, double c0, oslot *S, uint16_t (*ry)[SB * SB],
+                         uint16_t (*ru)[SB * SB], uint16_t (*rv)[SB * SB]) {
+  const int X = (r->tx0 + sb % r->tw) * SB, Y = (r->ty0 + sb / r->tw) * SB;
+  uint64_t mask = 0;
+  /* clear this superblock's leaf flags */
+  r->leaf0[sb] = 0;
+  for (int l = 1; l < 4; l++) {
+    struct olevel *P = &r->pl[l];
+    const int k2 = 1 << l, bx0 = (sb % r->tw) * k2, by0 = (sb / r->tw) * k2;
+    for (int j = 0; j < k2; j++) memset(P->leaf + (size_t)(by0 + j) * P->gw + bx0, 0, k2);
+  }
+  if (!split_at(r, c0, 0, X, Y)) {
+    commit_leaf(r, 0, X, Y, X, Y, S, ry, ru, rv);
+  } else {
+    mask |= 1;
+    for (int q = 0; q < 4; q++) {
+      const int x1 = X + (q & 1) * 32, y1 = Y + (q >> 1) * 32;
+      if (x1 >= r->W || y1 >= r->H) continue;
+      if (!split_at(r, c0, 1, x1, y1)) {
+        commit_leaf(r, 1, x1, y1, X, Y, S, ry, ru, rv);
+        continue;
+      }
+      mask |= 2u << q;
+      for (int t = 0; t < 4; t++) {
+        const int x2 = x1 + (t & 1) * 16, y2 = y1 + (t >> 1) * 16;
+        if (x2 >= r->W || y2 >= r->H) continue;
+        if (!split_at(r, c0, 2, x2, y2)) {
+          commit_leaf(r, 2, x2, y2, X, Y, S, ry, ru, rv);
+          continue;
+        }
+        mask |= 1u << (5 + ((y2 - Y) / 16) * 4 + (x2 - X) / 16);
+        for (int u = 0; u < 4; u++) {
+          const int x3 = x2 + (u & 1) * 8, y3 = y2 + (u >> 1) * 8;
+          if (x3 < r->W && y3 < r->H) commit_leaf(r, 3, x3, y3, X, Y, S, ry, ru, rv);
+        }
+      }
+    }
+  }
+  r->words[r->wpart + sb] = mask;
 }
 
 /* Pass B: F4 + F6 + F5 for one superblock. */
@@ -661,12 +982,33 @@ static void run_rdo(orc_replay *r, int sb, uint64_t tail[3]) {
   w[8 * R + 1] = (uint64_t)best_skip;
   w[8 * R + 2] = cb;
   w[8 * R + 3] = best_d;
-  /* F6: the winner into the frame (whole superblock; past the frame edge
-   * it lands in the padding, which F7 rewrites) */
-  for (int y = 0; y < SB; y++) memcpy(at(&S->y, hbd, ppx, ppy + y), (uint8_t *)by_ + y * SB * px, SB * px);
-  for (int y = 0; y < chei; y++) {
-    memcpy(at(&S->u, hbd, cpx, cpy + y), (uint8_t *)bu_ + (size_t)y * cwid * px, cwid * px);
-    memcpy(at(&S->v, hbd, cpx, cpy + y), (uint8_t *)bv_ + (size_t)y * cwid * px, cwid * px);
+  if (!r->s6) {
+    /* F6: the winner into the frame (whole superblock; past the frame edge
+     * it lands in the padding, which F7 rewrites) */
+    for (int y = 0; y < SB; y++) memcpy(at(&S->y, hbd, ppx, ppy + y), (uint8_t *)by_ + y * SB * px, SB * px);
+    for (int y = 0; y < chei; y++) {
+      memcpy(at(&S->u, hbd, cpx, cpy + y), (uint8_t *)bu_ + (size_t)y * cwid * px, cwid * px);
+      memcpy(at(&S->v, hbd, cpx, cpy + y), (uint8_t *)bv_ + (size_t)y * cwid * px, cwid * px);
+    }
+  } else {
+    /* speed 6: every 32x32, 16x16 and 8x8 block of the superblock, the
+     * partition decision, the leaves into the frame */
+    static _Thread_local uint16_t ry[4][SB * SB], ru[4][SB * SB], rv[4][SB * SB];
+    memcpy(ry[0], by_, SB * SB * px);
+    memcpy(ru[0], bu_, (size_t)cwid * chei * px);
+    memcpy(rv[0], bv_, (size_t)cwid * chei * px);
+    for (int l = 1; l < 4; l++) {
+      const struct olevel *P = &r->pl[l];
+      const int k2 = 1 << l;
+      for (int j = 0; j < k2; j++)
+        for (int i = 0; i < k2; i++) {
+          const int b = (sy * k2 + j) * P->gw + sx * k2 + i;
+          rdo_level_block(r, l, b, cur, ref, (uint8_t *)ry[l] + ((size_t)j * P->B * SB + i * P->B) * px,
+                          (uint8_t *)ru[l] + ((size_t)j * P->bch * cwid + i * P->bc) * px,
+                          (uint8_t *)rv[l] + ((size_t)j * P->bch * cwid + i * P->bc) * px);
+        }
+    }
+    partition_sb(r, sb, best, S, ry, ru, rv);
   }
   /* F5: the 8x8 blocks of this superblock inside the group's visible area */
   const orc_mv mv0 = r->sub[sb];
@@ -818,15 +1160,29 @@ void orc_replay_pad_recon(orc_replay *r) {
 }
 
 int orc_replay_results(orc_replay *r, uint64_t *out, int cap) {
-  int nw = r->nsb * (8 * r->R + 4);
+  int nw = (int)r->nwords;
   if (cap < nw + 5) return -1;
   memcpy(out, r->words, (size_t)nw * 8);
-  /* levels checksum, recon sums of the group and of the frame */
+  /* levels checksum (speed 6: of the committed blocks), recon sums of the
+   * group and of the frame */
   uint64_t lc = 0;
   size_t per = 1024 + 2 * (size_t)r->ntx_c * 1024;
-  for (int sb = 0; sb < r->nsb; sb++)
+  for (int sb = 0; sb < r->nsb; sb++) {
+    if (r->s6 && !r->leaf0[sb]) continue;
     for (size_t i = 0; i < per; i++)
       lc += (uint64_t)(int64_t)r->lev[sb * per + i] * (uint64_t)(i % 1024 + 1);
+  }
+  for (int l = 1; r->s6 && l < 4; l++) {
+    const struct olevel *P = &r->pl[l];
+    const size_t pl_ = (size_t)P->B * P->B, pc = (size_t)P->bc * P->bch, pb = pl_ + 2 * pc;
+    for (int b = 0; b < P->n; b++) {
+      if (!P->leaf[b]) continue;
+      const int32_t *v = P->lev + (size_t)b * pb;
+      for (size_t i = 0; i < pl_; i++) lc += (uint64_t)(int64_t)v[i] * (uint64_t)(i + 1);
+      for (size_t i = 0; i < 2 * pc; i++)
+        lc += (uint64_t)(int64_t)v[pl_ + i] * (uint64_t)(i % pc + 1);
+    }
+  }
   oslot *s = &r->slots[r->fi.display % NSLOT];
   oplane *pl[3] = {&s->y, &s->u, &s->v};
   int32_t gr[4] = {r->tx0, r->ty0, r->tw, r->th};

@@ -64,16 +64,23 @@ __constant__ int8_t kRdoReg[2][16][8] = {
      {0, 0, -8, 38, 110, -12, 0, 0}, {0, 0, -6, 28, 116, -10, 0, 0},
      {0, 0, -4, 18, 122, -8, 0, 0}, {0, 0, -2, 8, 126, -4, 0, 0}}};
 
-// FWD_SHIFT_32X32 / FWD_SHIFT_64X64 (forward.rs:22-40) by shift_idx, and
-// InvBlock::INTERMEDIATE_SHIFT (inverse.rs:1643-1666) = 2 for both.
+// FWD_SHIFT_{4X4, 8X8, 16X16, 32X32, 64X64} (forward.rs:22-26) by shift_idx
 template <int N>
 __device__ __forceinline__ void fwd_shifts(int idx, int &s0, int &s1, int &s2) {
+  constexpr int8_t k4[3][3] = {{3, 0, 0}, {2, 0, 1}, {0, 0, 3}};
+  constexpr int8_t k8[3][3] = {{4, -1, 0}, {2, 0, 1}, {0, 0, 3}};
   constexpr int8_t k32[3][3] = {{4, -2, 0}, {2, 0, 0}, {0, 0, 2}};
   constexpr int8_t k64[3][3] = {{4, -1, -2}, {2, 0, -1}, {0, 0, 1}};
-  const int8_t *k = N == 64 ? k64[idx] : k32[idx];
+  const int8_t *k = N == 64 ? k64[idx] : N == 32 ? k32[idx] : N == 4 ? k4[idx] : k8[idx];
   s0 = k[0];
   s1 = k[1];
   s2 = k[2];
+}
+// InvBlock::INTERMEDIATE_SHIFT (inverse.rs:1643-1666): 0 for 4x4, 1 for
+// 8x8, 2 from 16x16 up
+template <int N>
+constexpr int inv_mid_shift() {
+  return N == 4 ? 0 : N == 8 ? 1 : 2;
 }
 
 // round_shift_array (src/transform/mod.rs:499-521)
@@ -283,18 +290,20 @@ __device__ __forceinline__ void mc_compound(const RdoArgs &a, const RdoPlane &pl
   wave_sync();  // window reads done, prediction visible
 }
 
-// compute_distortion_bias (src/rdo.rs:476-508) of the BLOCK_8X8 importance
-// area at 4x4-block (mi_x, mi_y) of the frame: compute_mean_importance sums
-// the f32 importances of the in-frame 4x4 blocks in y-then-x order and
-// divides by the full area; the bias is (mean / 3) as f64 + 0.65.
-__device__ __forceinline__ double rdo_bias(const RdoArgs &a, int mi_x, int mi_y) {
+// compute_distortion_bias (src/rdo.rs:476-508) of the importance area of
+// m x m 4x4 blocks (BLOCK_8X8: m = 2; a chroma plane narrower than 8
+// pixels biases BLOCK_4X4 areas, m = 1) at 4x4-block (mi_x, mi_y) of the
+// frame: compute_mean_importance sums the f32 importances of the in-frame
+// 4x4 blocks in y-then-x order and divides by the full area; the bias is
+// (mean / 3) as f64 + 0.65.
+__device__ __forceinline__ double rdo_bias(const RdoArgs &a, int mi_x, int mi_y, int m = 2) {
   if (!a.imp) return 0.65;  // (0f32 / 3) as f64 + 0.65
-  const int x2 = mi_x + 2 < a.w_in_b ? mi_x + 2 : a.w_in_b;
-  const int y2 = mi_y + 2 < a.h_in_b ? mi_y + 2 : a.h_in_b;
+  const int x2 = mi_x + m < a.w_in_b ? mi_x + m : a.w_in_b;
+  const int y2 = mi_y + m < a.h_in_b ? mi_y + m : a.h_in_b;
   float tot = 0.f;
   for (int y = mi_y; y < y2; y++)
     for (int x = mi_x; x < x2; x++) tot = __fadd_rn(tot, a.imp[(y >> 1) * a.w_imp + (x >> 1)]);
-  return (double)__fdiv_rn(__fdiv_rn(tot, 4.0f), 3.0f) + 0.65;
+  return (double)__fdiv_rn(__fdiv_rn(tot, (float)(m * m)), 3.0f) + 0.65;
 }
 // RawDistortion * bias (src/rdo.rs:539-544): `(value as f64 * bias) as u64`
 __device__ __forceinline__ uint64_t rdo_biased(uint64_t v, double bias) {
@@ -355,7 +364,7 @@ __device__ __forceinline__ uint64_t rdo_sse_biased(const RdoArgs &a, const RdoJo
       value += row;
     }
     const int px = j.bx + j.ox + bx * bw, py = j.by + j.oy + by * bh;
-    acc += rdo_biased(value, rdo_bias(a, (px << a.xdec) >> 2, (py << a.ydec) >> 2));
+    acc += rdo_biased(value, rdo_bias(a, (px << a.xdec) >> 2, (py << a.ydec) >> 2, (N < 8 ? N : 8) / 4));
   }
   return acc;
 }
@@ -635,7 +644,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     int32_t v[N];
 #pragma unroll
     for (int r = 0; r < N; r++)
-      v[r] = r < C32 ? tx::clampv(round_shift(buf[r * S + lane], 2), crange) : 0;
+      v[r] = r < C32 ? tx::clampv(round_shift(buf[r * S + lane], inv_mid_shift<N>()), crange) : 0;
     tx::inv1d<1, N>(v, crange);
 #pragma unroll
     for (int r = 0; r < N; r++) {
@@ -1106,8 +1115,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
 
 using namespace rv;
 
-// Replay-internal entry (rv_replay.hip): luma (N = 64, cdef distortion)
-// and both chroma planes (N = 32, SSE) of every task, one launch on `s`.
 // Blocks below 64x64 (the speed-6 partition search): N x N transform
 // blocks, N lanes each (64 / N per wavefront, four wavefronts per
 // workgroup); the launch's tasks cover plane p[0] then p[1] (chroma).

@@ -147,27 +147,17 @@ __global__ void coeff_checksum(const int32_t *packed, int64_t total, int per_blo
 // entropy coder's mode and MV bits are out of scope); rd = dist as f64 +
 // lambda * rate / 8 (src/rdo.rs:563-569).  One thread per superblock, which
 // also writes the superblock's result words.
-__global__ __launch_bounds__(64) void score_candidates(
-    Geo g, CandGeo cg, double lambda, double ds_u, double ds_v, const rv_fs_result *sub,
-    const uint64_t *lout,
-    const uint64_t *uout, const uint64_t *vout, int ntx_c, RdoWinner *win,
-    const rv_fs_result *coarse, const rv_fs_result *half, const rv_fs_result *full,
-    uint64_t *words, int32_t *cand_count, unsigned long long *imp_sum, uint32_t *evals) {
-  const int sb = blockIdx.x * 64 + threadIdx.x;
-  if (sb == 0) {  // F4's list is consumed: ready for the next frame; F5 sums next
-    evals[0] = (uint32_t)*cand_count;  // single-reference candidates evaluated
-    evals[1] = (uint32_t)(cg.comp * g.nsb);  // compound ones
-    *cand_count = 0;
-    *imp_sum = 0;
-  }
-  if (sb >= g.nsb) return;
+__device__ inline RdoWinner block_argmin(const CandGeo &cg, double lambda, double ds_u,
+                                         double ds_v, const rv_fs_result *sub,
+                                         const uint64_t *lout, const uint64_t *uout,
+                                         const uint64_t *vout, int ntx_c, int sb) {
   double best = 1.7976931348623157e308;  // f64::MAX
   RdoWinner w{0, 0, best, 0};
-  const int ns = g.R * g.M;  // single-reference candidates; compound ones follow
+  const int ns = cg.R * cg.M;  // single-reference candidates; compound ones follow
   for (int c = 0; c < ns + cg.comp; c++) {
     rv_mv mv;
     if (c < ns && !cand_mv(cg, sub, sb, c, &mv)) continue;
-    const int64_t o = (int64_t)c * g.nsb + sb;
+    const int64_t o = (int64_t)c * cg.nsb + sb;
     uint64_t su = 0, sv = 0, nu = 0, nv = 0;
     uint32_t rate = (uint32_t)lout[o * 3 + 2];
     for (int j = 0; j < ntx_c; j++) {
@@ -194,6 +184,27 @@ __global__ __launch_bounds__(64) void score_candidates(
       if (rn < w.cost) w = RdoWinner{c, 0, rn, dn};
     }
   }
+  return w;
+}
+
+__global__ __launch_bounds__(64) void score_candidates(
+    Geo g, CandGeo cg, double lambda, double ds_u, double ds_v, const rv_fs_result *sub,
+    const uint64_t *lout,
+    const uint64_t *uout, const uint64_t *vout, int ntx_c, RdoWinner *win,
+    const rv_fs_result *coarse, const rv_fs_result *half, const rv_fs_result *full,
+    uint64_t *words, int32_t *cand_count, unsigned long long *imp_sum, uint32_t *evals,
+    int32_t *leaf_count) {
+  const int sb = blockIdx.x * 64 + threadIdx.x;
+  if (sb == 0) {  // F4's list is consumed: ready for the next frame; F5 sums next
+    evals[0] = (uint32_t)*cand_count;  // single-reference candidates evaluated
+    evals[1] = (uint32_t)(cg.comp * g.nsb);  // compound ones
+    *cand_count = 0;
+    *imp_sum = 0;
+    if (leaf_count)  // speed 6: the partition decision appends next
+      for (int l = 0; l < 4; l++) leaf_count[l] = 0;
+  }
+  if (sb >= g.nsb) return;
+  const RdoWinner w = block_argmin(cg, lambda, ds_u, ds_v, sub, lout, uout, vout, ntx_c, sb);
   win[sb] = w;
   uint64_t *wd = words + (int64_t)sb * (8 * g.R + 4);
   for (int i = 0; i < 8 * g.R; i++) {
@@ -307,6 +318,160 @@ __global__ __launch_bounds__(256) void xcopy_kernel(XArgs a) {
   }
 }
 
+// ---- speed 6 (config D): the partition levels below 64x64 -----------------
+constexpr int kLevels = 4;  // 64x64, 32x32, 16x16, 8x8
+
+// The full-pel jobs of a level take the sub-pel winner of the enclosing
+// block of level `parent` as their coarse predictor, quantize_to_fullpel
+// (get_subset_predictors, src/me.rs:82-96): rdo_mode_decision keeps b_me in
+// pmvs for 64x64 and 32x32 blocks only (src/rdo.rs:866-876), so 32x32
+// blocks start from their 64x64 and 16x16 / 8x8 blocks from their 32x32.
+__global__ void seed_level_kernel(rv_ds_job *jobs, int n, int gw, int R,
+                                  const rv_fs_result *parent, int pn, int pgw, int f) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * R) return;
+  const int k = i / n, b = i - k * n, bx = b % gw, by = b / gw;
+  jobs[i].pred[1] = qfull(parent[k * pn + (by / f) * pgw + bx / f].best_mv);
+}
+
+// rdo_mode_decision's winner of every block of a level + its result words
+// (the level's full-pel / sub-pel searches, winner, skip, cost, distortion).
+__global__ __launch_bounds__(64) void score_level(CandGeo cg, double lambda, double ds_u,
+                                                  double ds_v, const rv_fs_result *full,
+                                                  const rv_fs_result *sub, const uint64_t *lout,
+                                                  const uint64_t *uout, const uint64_t *vout,
+                                                  RdoWinner *win, uint64_t *words,
+                                                  int32_t *cand_count, uint32_t *evals) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b == 0) {
+    atomicAdd((unsigned int *)&evals[0], (unsigned int)*cand_count);
+    atomicAdd((unsigned int *)&evals[1], (unsigned int)(cg.comp * cg.nsb));
+    *cand_count = 0;
+  }
+  if (b >= cg.nsb) return;
+  const RdoWinner w = block_argmin(cg, lambda, ds_u, ds_v, sub, lout, uout, vout, 1, b);
+  win[b] = w;
+  uint64_t *wd = words + (int64_t)b * (4 * cg.R + 4);
+  for (int k = 0; k < cg.R; k++) {
+    const rv_fs_result f = full[k * cg.nsb + b], s = sub[k * cg.nsb + b];
+    wd[4 * k + 0] = pack_mv(f.best_mv);
+    wd[4 * k + 1] = f.cost;
+    wd[4 * k + 2] = pack_mv(s.best_mv);
+    wd[4 * k + 3] = s.cost;
+  }
+  uint64_t cb;
+  __builtin_memcpy(&cb, &w.cost, 8);
+  wd[4 * cg.R + 0] = (uint64_t)w.c;
+  wd[4 * cg.R + 1] = (uint64_t)w.skip;
+  wd[4 * cg.R + 2] = cb;
+  wd[4 * cg.R + 3] = w.dist;
+}
+
+struct PartArgs {
+  const RdoWinner *win[kLevels];
+  int gw[kLevels];          // level grid width (blocks)
+  int32_t *leaf[kLevels];   // the committed blocks of each level
+  int32_t *leaf_count;      // [kLevels], zeroed by score_candidates
+  uint64_t *words;          // one partition mask per superblock
+};
+
+// encode_partition_topdown (src/encoder.rs:2392-2470) over every superblock
+// of the group: a block past the frame edge must split; a block that fits
+// compares PARTITION_NONE (its mode decision's rd cost) with
+// PARTITION_SPLIT (the sum of its four children's, rdo_partition_decision,
+// src/rdo.rs:1500-1668; strict `<`; the partition symbol's rate is not
+// modelled) and recurses into a split; 8x8 blocks are leaves.  One thread
+// per superblock; the leaves go to per-level lists (wave-aggregated
+// appends, order irrelevant: every output is indexed by block).
+__global__ __launch_bounds__(64) void partition_kernel(Geo g, PartArgs p) {
+  const int sb = blockIdx.x * 64 + threadIdx.x;
+  const bool live = sb < g.nsb;
+  const int gx0 = g.tx0 * kSb, gy0 = g.ty0 * kSb;
+  const int X = gx0 + (live ? sb % g.tw : 0) * kSb, Y = gy0 + (live ? sb / g.tw : 0) * kSb;
+  auto idx = [&](int l, int x, int y) {
+    const int B = kSb >> l;
+    return ((y - gy0) / B) * p.gw[l] + (x - gx0) / B;
+  };
+  auto cost = [&](int l, int x, int y) { return p.win[l][idx(l, x, y)].cost; };
+  auto split = [&](int l, int x, int y) -> bool {
+    const int B = kSb >> l;
+    if (x + B > g.W || y + B > g.H) return true;  // must_split
+    if (l == kLevels - 1) return false;
+    const int h = B / 2;
+    double s = 0.0;
+    s += cost(l + 1, x, y);
+    s += cost(l + 1, x + h, y);
+    s += cost(l + 1, x, y + h);
+    s += cost(l + 1, x + h, y + h);
+    return 0.0 + s < cost(l, x, y);
+  };
+  uint32_t mask = 0;
+  auto walk = [&](auto emit) {
+    if (!live) return;
+    if (!split(0, X, Y)) {
+      emit(0, X, Y);
+      return;
+    }
+    mask |= 1u;
+    for (int q = 0; q < 4; q++) {
+      const int x1 = X + (q & 1) * 32, y1 = Y + (q >> 1) * 32;
+      if (x1 >= g.W || y1 >= g.H) continue;
+      if (!split(1, x1, y1)) {
+        emit(1, x1, y1);
+        continue;
+      }
+      mask |= 2u << q;
+      for (int r = 0; r < 4; r++) {
+        const int x2 = x1 + (r & 1) * 16, y2 = y1 + (r >> 1) * 16;
+        if (x2 >= g.W || y2 >= g.H) continue;
+        if (!split(2, x2, y2)) {
+          emit(2, x2, y2);
+          continue;
+        }
+        mask |= 1u << (5 + ((y2 - Y) / 16) * 4 + (x2 - X) / 16);
+        for (int t = 0; t < 4; t++) {
+          const int x3 = x2 + (t & 1) * 8, y3 = y2 + (t >> 1) * 8;
+          if (x3 < g.W && y3 < g.H) emit(3, x3, y3);
+        }
+      }
+    }
+  };
+  int cnt[kLevels] = {0, 0, 0, 0};
+  walk([&](int l, int, int) { cnt[l]++; });
+  const int lane = threadIdx.x & 63;
+  int base[kLevels];
+  for (int l = 0; l < kLevels; l++) {
+    int v = cnt[l];
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(v, o, 64);
+      if (lane >= o) v += t;
+    }
+    const int total = __shfl(v, 63, 64);
+    int b0 = 0;
+    if (lane == 63 && total) b0 = atomicAdd(&p.leaf_count[l], total);
+    b0 = __shfl(b0, 63, 64);
+    base[l] = b0 + v - cnt[l];
+  }
+  walk([&](int l, int x, int y) { p.leaf[l][base[l]++] = idx(l, x, y); });
+  if (live) p.words[sb] = mask;
+}
+
+// Levels checksum over the committed blocks of a list: sum of q *
+// (position in its transform block + 1), wrapping u64.
+__global__ void coeff_checksum_list(const int32_t *packed, const int32_t *list,
+                                    const int32_t *count, int per, int wmod,
+                                    unsigned long long *out) {
+  const int64_t total = (int64_t)*count * per;
+  uint64_t s = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = i / per;
+    const int e = (int)(i - j * per);
+    s += (uint64_t)(int64_t)packed[(int64_t)list[j] * per + e] * (uint64_t)(e % wmod + 1);
+  }
+  block_atomic_add(s, out);
+}
+
 }  // namespace rv
 
 using namespace rv;
@@ -332,8 +497,26 @@ struct rv_replay {
     bool set = false;
     int qidx;
     QCtx ql, qu, qv;
+    QCtx qs[kLevels][3];  // speed 6: luma / U / V of the 32x32 .. 8x8 blocks
     double lambda, me_lambda, ds[3];
   } lv[3];
+  // speed 6: the partition levels below 64x64 (index 0 = the superblocks,
+  // whose arrays are the ones above)
+  struct PLevel {
+    int B, n, gw, gh, bc, bch, txl, txc;
+    CandGeo cg;
+    rv_ds_job *jobs_full[3] = {nullptr, nullptr, nullptr}, *jobs_sub[3] = {nullptr, nullptr, nullptr};
+    rv_fs_result *full = nullptr, *sub = nullptr;
+    uint64_t *l_out = nullptr, *c_out = nullptr;
+    RdoWinner *win = nullptr;
+    int32_t *cand_list = nullptr, *cand_count = nullptr;
+    int32_t *l_lev = nullptr, *c_lev = nullptr;
+    int32_t *leaf = nullptr;
+    size_t woff = 0;  // result words offset
+  } pl[kLevels];
+  bool s6 = false;
+  int32_t *leaf_count = nullptr;  // [kLevels]
+  size_t nwords = 0, wpart = 0;   // result words; offset of the partition masks
   bool jobs_built = false;
   std::vector<RvSlot> slots;
   std::vector<RvInput> inputs;
@@ -522,6 +705,33 @@ int build_static_jobs(rv_replay *r) {
     if ((e = upload(jh, r->jobs_half[lv])) || (e = upload(jf, r->jobs_full[lv])) ||
         (e = upload(js, r->jobs_sub[lv])))
       return e;
+    // speed 6: motion_estimation of every 32x32 / 16x16 / 8x8 block at its
+    // own position (no adjust_bo, src/me.rs:193-278): zero + the seeded
+    // coarse predictor, then the sub-pel search from the full-pel winner
+    for (int l = 1; r->s6 && l < kLevels; l++) {
+      rv_replay::PLevel &P = r->pl[l];
+      std::vector<rv_ds_job> f6((size_t)P.n * g.R), s6((size_t)P.n * g.R);
+      for (int k = 0; k < g.R; k++)
+        for (int b = 0; b < P.n; b++) {
+          const int X = (P.cg.tx0 + b % P.gw) * P.B, Y = (P.cg.ty0 + b / P.gw) * P.B;
+          int mr[4];
+          mv_range(g, X >> 2, Y >> 2, P.B, P.B, mr);
+          rv_ds_job j;
+          memset(&j, 0, sizeof(j));
+          j.po_x = X;
+          j.po_y = Y;
+          j.mvx_min = mr[0];
+          j.mvx_max = mr[1];
+          j.mvy_min = mr[2];
+          j.mvy_max = mr[3];
+          j.lambda = lambda1;
+          j.n_pred = 2;
+          f6[(size_t)k * P.n + b] = j;
+          j.n_pred = 1;
+          s6[(size_t)k * P.n + b] = j;
+        }
+      if ((e = upload(f6, P.jobs_full[lv])) || (e = upload(s6, P.jobs_sub[lv]))) return e;
+    }
   }
   r->jobs_built = true;
   return RV_OK;
@@ -716,7 +926,63 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   if (r->cand_count) (void)hipMemsetAsync(r->cand_count, 0, 4, r->stream);
   r->l_lev = (int32_t *)dalloc(r, (size_t)g.nsb * 1024 * 4);
   r->c_lev = (int32_t *)dalloc(r, (size_t)g.nsb * r->ntx_c * 1024 * 4 * 2);
-  r->words = (uint64_t *)dalloc(r, (size_t)g.nsb * (8 * g.R + 4) * 8);
+  r->nwords = (size_t)g.nsb * (8 * g.R + 4);
+  if (cfg->flags & RV_REPLAY_SPEED6) {
+    if (g.xdec != g.ydec) {
+      rv_set_error(RV_EINVAL, "rv_replay_create: speed 6 needs 4:2:0 or 4:4:4");
+      rv_replay_destroy(r);
+      return nullptr;
+    }
+    r->s6 = true;
+    rv_replay::PLevel &P0 = r->pl[0];
+    P0.B = kSb;
+    P0.n = g.nsb;
+    P0.gw = g.tw;
+    P0.gh = g.th;
+    size_t nleaf = (size_t)g.nsb;
+    for (int l = 1; l < kLevels; l++) {
+      rv_replay::PLevel &P = r->pl[l];
+      const int k = 1 << l;
+      P.B = kSb >> l;
+      P.gw = g.tw * k;
+      P.gh = g.th * k;
+      P.n = P.gw * P.gh;
+      P.bc = P.B >> g.xdec;
+      P.bch = P.B >> g.ydec;
+      P.txl = 4 - l;                                              // TX_32X32 .. TX_8X8
+      P.txc = P.bc == 32 ? 3 : P.bc == 16 ? 2 : P.bc == 8 ? 1 : 0;  // .. TX_4X4
+      P.cg = CandGeo{P.n, P.gw, P.gh, g.tx0 * k, g.ty0 * k, g.tws * k, g.ths * k, g.R, g.M, 0};
+      const int64_t nc = (int64_t)P.n * g.C;
+      P.full = (rv_fs_result *)dalloc(r, (size_t)P.n * g.R * sizeof(rv_fs_result));
+      P.sub = (rv_fs_result *)dalloc(r, (size_t)P.n * g.R * sizeof(rv_fs_result));
+      P.l_out = (uint64_t *)dalloc(r, (size_t)nc * 3 * 8);
+      P.c_out = (uint64_t *)dalloc(r, (size_t)nc * 3 * 8 * 2);
+      P.win = (RdoWinner *)dalloc(r, (size_t)P.n * sizeof(RdoWinner));
+      P.cand_list = (int32_t *)dalloc(r, (size_t)nc * 4);
+      P.cand_count = (int32_t *)dalloc(r, 4);
+      P.l_lev = (int32_t *)dalloc(r, (size_t)P.n * P.B * P.B * 4);
+      P.c_lev = (int32_t *)dalloc(r, (size_t)P.n * P.bc * P.bch * 4 * 2);
+      ok = ok && P.full && P.sub && P.l_out && P.c_out && P.win && P.cand_list && P.cand_count &&
+           P.l_lev && P.c_lev;
+      if (P.cand_count) (void)hipMemsetAsync(P.cand_count, 0, 4, r->stream);
+      if (P.l_lev) (void)hipMemsetAsync(P.l_lev, 0, (size_t)P.n * P.B * P.B * 4, r->stream);
+      if (P.c_lev) (void)hipMemsetAsync(P.c_lev, 0, (size_t)P.n * P.bc * P.bch * 8, r->stream);
+      P.woff = r->nwords;
+      r->nwords += (size_t)P.n * (4 * g.R + 4);
+      nleaf += (size_t)P.n;
+    }
+    r->wpart = r->nwords;
+    r->nwords += (size_t)g.nsb;
+    int32_t *lf = (int32_t *)dalloc(r, nleaf * 4);
+    r->leaf_count = (int32_t *)dalloc(r, kLevels * 4);
+    ok = ok && lf && r->leaf_count;
+    if (r->leaf_count) (void)hipMemsetAsync(r->leaf_count, 0, kLevels * 4, r->stream);
+    for (int l = 0; l < kLevels && lf; l++) {
+      r->pl[l].leaf = lf;
+      lf += r->pl[l].n;
+    }
+  }
+  r->words = (uint64_t *)dalloc(r, r->nwords * 8);
   r->imp_bx = g.vis_w / 8;
   r->imp_by = g.vis_h / 8;
   r->n_imp = r->imp_bx * r->imp_by;
@@ -725,7 +991,7 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
        r->cand_list && r->cand_count && r->cand_evals &&
        r->l_lev && r->c_lev && r->words && r->tail;
   if (ok) {
-    ok = hipMemsetAsync(r->words, 0, (size_t)g.nsb * (8 * g.R + 4) * 8, r->stream) == hipSuccess &&
+    ok = hipMemsetAsync(r->words, 0, r->nwords * 8, r->stream) == hipSuccess &&
          hipMemsetAsync(r->tail, 0, 5 * 8, r->stream) == hipSuccess &&
          hipMemsetAsync(r->l_lev, 0, (size_t)g.nsb * 1024 * 4, r->stream) == hipSuccess &&
          hipMemsetAsync(r->c_lev, 0, (size_t)g.nsb * r->ntx_c * 1024 * 4 * 2, r->stream) ==
@@ -768,6 +1034,13 @@ int rv_replay_set_level_params(rv_replay *r, int level, const rv_replay_level_pa
   RV_R(rv_quant_ctx(p->base_q_idx, 64 * 64, 0, bd, p->dc_delta_q[0], p->ac_delta_q[0], &L.ql));
   RV_R(rv_quant_ctx(p->base_q_idx, 32 * 32, 0, bd, p->dc_delta_q[1], p->ac_delta_q[1], &L.qu));
   RV_R(rv_quant_ctx(p->base_q_idx, 32 * 32, 0, bd, p->dc_delta_q[2], p->ac_delta_q[2], &L.qv));
+  for (int l = 1; r->s6 && l < kLevels; l++) {  // speed 6: the smaller transforms
+    const rv_replay::PLevel &P = r->pl[l];
+    RV_R(rv_quant_ctx(p->base_q_idx, P.B * P.B, 0, bd, p->dc_delta_q[0], p->ac_delta_q[0], &L.qs[l][0]));
+    for (int c = 1; c < 3; c++)
+      RV_R(rv_quant_ctx(p->base_q_idx, P.bc * P.bch, 0, bd, p->dc_delta_q[c], p->ac_delta_q[c],
+                        &L.qs[l][c]));
+  }
   L.qidx = p->base_q_idx;
   L.lambda = p->lambda;
   L.me_lambda = p->me_lambda;
@@ -994,13 +1267,32 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
                                r->full, ev_full, &to_sub, st));
   RV_EV(4);
-  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
-                               r->sub, ev_sub, nullptr, st));
+  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, r->s6 ? 1 : 0,
+                               0, g.bd, r->sub, ev_sub, nullptr, st));
+  // speed 6: the same search for every 32x32, 16x16 and 8x8 block (SATD
+  // sub-pel, use_satd_subpel, src/api/config.rs:429-431)
+  for (int l = 1; r->s6 && l < kLevels; l++) {
+    rv_replay::PLevel &P = r->pl[l];
+    const int up = l == 1 ? 0 : 1;  // the level whose sub-pel winners seed this one
+    const rv_fs_result *parent = up == 0 ? r->sub : r->pl[1].sub;
+    seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, st>>>(
+        P.jobs_full[lv], P.n, P.gw, g.R, parent, r->pl[up].n, r->pl[up].gw, 1 << (l - up));
+    ChainNext to_s{kChainFullToSub, P.jobs_sub[lv]};
+    RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, P.jobs_full[lv], P.n, P.B, P.B, 0, 0, 0,
+                                 g.bd, P.full, nullptr, &to_s, st));
+    RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, P.jobs_sub[lv], P.n, P.B, P.B, 1, 1, 0,
+                                 g.bd, P.sub, nullptr, nullptr, st));
+  }
   // the valid candidates (a few microseconds; bracketed with F3 sub-pel;
   // the count was zeroed by the previous frame's argmin or at creation)
   const int nsingle = g.nsb * g.R * g.M;
   cand_list_kernel<<<(nsingle + 255) / 256, 256, 0, st>>>(cg, r->sub, nsingle, r->cand_list,
                                                           r->cand_count);
+  for (int l = 1; r->s6 && l < kLevels; l++) {
+    rv_replay::PLevel &P = r->pl[l];
+    const int ns = P.n * g.R * g.M;
+    cand_list_kernel<<<(ns + 255) / 256, 256, 0, st>>>(P.cg, P.sub, ns, P.cand_list, P.cand_count);
+  }
   RV_EV(5);
   // F4 every valid candidate, luma + both chroma planes in one fused launch
   RdoArgs la, ca;
@@ -1052,6 +1344,54 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   ca.q_tx_index = 3 * 16 + 0;  // TX_32X32, DCT_DCT
   ca.tx_size = 3;
   RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
+  // speed 6: the candidates of every 32x32 .. 8x8 block, luma (cdef
+  // distortion) and chroma launches per level
+  RdoArgs ll[kLevels], lc6[kLevels];
+  for (int l = 1; r->s6 && l < kLevels; l++) {
+    rv_replay::PLevel &P = r->pl[l];
+    CandGeo cgl = P.cg;
+    cgl.comp = cg.comp;
+    const int ns = P.n * g.R * g.M;
+    RdoArgs a = la;
+    a.p[0].levels = P.l_lev;
+    a.p[0].out = P.l_out;
+    a.p[0].q = L.qs[l][0];
+    a.g = cgl;
+    a.sub = P.sub;
+    a.win = P.win;
+    a.n_tx = ns;
+    a.list = P.cand_list;
+    a.count = P.cand_count;
+    a.ntx_per_cand = 1;
+    a.bsize = P.B;
+    a.mb_w = a.mb_h = P.B;
+    a.q_tx_index = P.txl * 16;  // DCT_DCT
+    a.tx_size = P.txl;
+    RdoArgs c = ca;
+    for (int q = 0; q < 2; q++) {
+      c.p[q].levels = P.c_lev + (size_t)q * P.n * P.bc * P.bch;
+      c.p[q].out = P.c_out + (size_t)q * P.n * g.C * 3;
+      c.p[q].q = L.qs[l][1 + q];
+    }
+    c.g = cgl;
+    c.sub = P.sub;
+    c.win = P.win;
+    c.n_tx = ns;
+    c.list = P.cand_list;
+    c.count = P.cand_count;
+    c.ntx_per_cand = 1;
+    c.bsize = P.B;
+    c.mb_w = P.bc;
+    c.mb_h = P.bch;
+    c.sub_w = (P.bc < 8 ? P.bc : 8) >> g.xdec;   // sse_wxh's importance blocks
+    c.sub_h = (P.bch < 8 ? P.bch : 8) >> g.ydec;
+    c.q_tx_index = P.txc * 16;
+    c.tx_size = P.txc;
+    ll[l] = a;
+    lc6[l] = c;
+    RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, st, 0));
+    RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, st, 0));
+  }
   if (cg.comp) {  // the compound candidates: every one is pushed, no list
     RdoArgs lc = la, cc = ca;
     lc.list = cc.list = nullptr;
@@ -1061,6 +1401,16 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     cc.n_tx = g.nsb * cg.comp * ntx_c;
     RV_EV(6);
     RV_R(rv_rdo_candidates(lc, cc, g.hbd, st, true));
+    for (int l = 1; r->s6 && l < kLevels; l++) {
+      const rv_replay::PLevel &P = r->pl[l];
+      RdoArgs a = ll[l], c = lc6[l];
+      a.list = c.list = nullptr;
+      a.count = c.count = nullptr;
+      a.cand_base = c.cand_base = P.n * g.R * g.M;
+      a.n_tx = c.n_tx = P.n * cg.comp;
+      RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, st, 1));
+      RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, st, 1));
+    }
   } else {
     RV_EV(6);
   }
@@ -1070,16 +1420,47 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                                      r->c_out, r->c_out + nct * 3, ntx_c, r->win,
                                                      r->coarse, r->half, r->full, r->words,
                                                      r->cand_count, r->tail + 2,
-                                                     r->cand_evals + 2 * slot);
+                                                     r->cand_evals + 2 * slot, r->leaf_count);
+  if (r->s6) {
+    PartArgs pa;
+    memset(&pa, 0, sizeof(pa));
+    for (int l = 0; l < kLevels; l++) {
+      rv_replay::PLevel &P = r->pl[l];
+      if (l > 0) {
+        CandGeo cgl = P.cg;
+        cgl.comp = cg.comp;
+        score_level<<<(P.n + 63) / 64, 64, 0, st>>>(cgl, L.lambda, L.ds[1], L.ds[2], P.full, P.sub,
+                                                    P.l_out, P.c_out, P.c_out + (size_t)P.n * g.C * 3,
+                                                    P.win, r->words + P.woff, P.cand_count,
+                                                    r->cand_evals + 2 * slot);
+      }
+      pa.win[l] = l ? P.win : r->win;
+      pa.gw[l] = P.gw;
+      pa.leaf[l] = P.leaf;
+    }
+    pa.leaf_count = r->leaf_count;
+    pa.words = r->words + r->wpart;
+    partition_kernel<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, pa);
+  }
   RV_EV(8);
   // F6 commit the winners into the frame
   la.commit = ca.commit = 1;
-  la.list = ca.list = nullptr;
-  la.count = ca.count = nullptr;
+  la.list = ca.list = r->s6 ? r->pl[0].leaf : nullptr;  // speed 6: the unsplit superblocks
+  la.count = ca.count = r->s6 ? r->leaf_count : nullptr;
   la.n_tx = g.nsb;
   ca.n_tx = g.nsb * ntx_c;
   la.ntx_per_cand = 1;
   RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
+  for (int l = 1; r->s6 && l < kLevels; l++) {  // and the leaves of every level
+    const rv_replay::PLevel &P = r->pl[l];
+    RdoArgs a = ll[l], c = lc6[l];
+    a.commit = c.commit = 1;
+    a.list = c.list = P.leaf;
+    a.count = c.count = r->leaf_count + l;
+    a.n_tx = c.n_tx = P.n;
+    RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, st, 2));
+    RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, st, 2));
+  }
   RV_EV(9);
   // F5 importance SATD against reference 0 (the sum was zeroed by the argmin)
   {
@@ -1122,7 +1503,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
 int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap) {
   if (!r || !host_out) return rv_set_error(RV_EINVAL, "rv_replay_results: null");
   const Geo &g = r->g;
-  const int nw = g.nsb * (8 * g.R + 4);
+  const int nw = (int)r->nwords;
   const int total = nw + 5;
   if (cap < total) return rv_set_error(RV_EINVAL, "rv_replay_results: cap too small");
   // verification checksums of the last coded frame (outside the per-frame work)
@@ -1130,8 +1511,25 @@ int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap) {
   const int64_t nl = (int64_t)g.nsb * 1024, nc = (int64_t)g.nsb * r->ntx_c * 1024;
   RV_H(hipMemsetAsync(r->tail, 0, 2 * 8, st));
   RV_H(hipMemsetAsync(r->tail + 3, 0, 2 * 8, st));
-  coeff_checksum<<<1024, 256, 0, st>>>(r->l_lev, nl, 1024, r->tail);
-  coeff_checksum<<<1024, 256, 0, st>>>(r->c_lev, 2 * nc, 1024, r->tail);
+  if (!r->s6) {
+    coeff_checksum<<<1024, 256, 0, st>>>(r->l_lev, nl, 1024, r->tail);
+    coeff_checksum<<<1024, 256, 0, st>>>(r->c_lev, 2 * nc, 1024, r->tail);
+  } else {  // the committed blocks (leaves) of every level
+    coeff_checksum_list<<<1024, 256, 0, st>>>(r->l_lev, r->pl[0].leaf, r->leaf_count, 1024, 1024,
+                                              r->tail);
+    for (int q = 0; q < 2; q++)
+      coeff_checksum_list<<<1024, 256, 0, st>>>(r->c_lev + q * nc, r->pl[0].leaf, r->leaf_count,
+                                                r->ntx_c * 1024, 1024, r->tail);
+    for (int l = 1; l < kLevels; l++) {
+      const rv_replay::PLevel &P = r->pl[l];
+      const int pl_ = P.B * P.B, pc = P.bc * P.bch;
+      coeff_checksum_list<<<1024, 256, 0, st>>>(P.l_lev, P.leaf, r->leaf_count + l, pl_, pl_,
+                                                r->tail);
+      for (int q = 0; q < 2; q++)
+        coeff_checksum_list<<<1024, 256, 0, st>>>(P.c_lev + (size_t)q * P.n * pc, P.leaf,
+                                                  r->leaf_count + l, pc, pc, r->tail);
+    }
+  }
   const RvSlot &s = r->slots[r->last.display % kSlots];
   const rv_plane *pl[3] = {&s.y, &s.u, &s.v};
   for (int i = 0; i < 3; i++) {

@@ -20,6 +20,7 @@ from . import rate as _rate
 DEFAULT_QUANTIZER = 100  # rav1e's default --quantizer (src/api/config.rs)
 
 RV_REPLAY_EXHAUSTIVE_FS = 4  # F1 without successive elimination (same results)
+RV_REPLAY_SPEED6 = 8  # the speed-6 schedule: partition RDO 64x64 .. 8x8 (config D)
 
 # GOP of the reference's reorder pyramid (src/api/internal.rs:61-95):
 # group_input_len 4, levels 0,1,2,2 -> me_range_scale = 4 >> level
@@ -179,11 +180,35 @@ def tile_groups(tiling: dict, world: int) -> list:
     return out
 
 
-def result_words(width, height, n_refs, tile_w_sb=0, tile_h_sb=0, tile_x0=0, tile_y0=0):
+def result_words(width, height, n_refs, tile_w_sb=0, tile_h_sb=0, tile_x0=0, tile_y0=0,
+                 speed=10):
+    """Result words of a group (rv_replay_results): per superblock 8 * R + 4;
+    speed 6 adds 4 * R + 4 per 32x32, 16x16 and 8x8 block and one partition
+    mask per superblock; then 5 tail words."""
     sbc, sbr = (width + 63) // 64, (height + 63) // 64
     tw = tile_w_sb or (sbc - tile_x0)
     th = tile_h_sb or (sbr - tile_y0)
-    return tw * th * (8 * n_refs + 4) + 5
+    n = tw * th * (8 * n_refs + 4)
+    if speed == 6:
+        n += sum(tw * th * 4 ** l * (4 * n_refs + 4) for l in (1, 2, 3)) + tw * th
+    return n + 5
+
+
+def level_words(width, height, n_refs, words, tile_w_sb=0, tile_h_sb=0, tile_x0=0, tile_y0=0):
+    """Split speed-6 result words: (superblock words [nsb, 8R+4], [level 1..3
+    words [n_l, 4R+4]], partition masks [nsb], tail [5])."""
+    sbc, sbr = (width + 63) // 64, (height + 63) // 64
+    tw = tile_w_sb or (sbc - tile_x0)
+    th = tile_h_sb or (sbr - tile_y0)
+    nsb = tw * th
+    o = nsb * (8 * n_refs + 4)
+    sbw = words[:o].reshape(nsb, 8 * n_refs + 4)
+    lv = []
+    for l in (1, 2, 3):
+        n = nsb * 4 ** l
+        lv.append(words[o:o + n * (4 * n_refs + 4)].reshape(n, 4 * n_refs + 4))
+        o += n * (4 * n_refs + 4)
+    return sbw, lv, words[o:o + nsb], words[o + nsb:]
 
 
 class HipReplay:
@@ -207,8 +232,9 @@ class HipReplay:
         self.h = lib().rv_replay_create(C.byref(cfg), stream)
         if not self.h:
             raise RuntimeError(f"rv_replay_create: {lib().rv_last_error().decode()}")
+        self.speed = 6 if flags & RV_REPLAY_SPEED6 else 10
         self.n_words = result_words(width, height, n_refs, cfg.tile_w, cfg.tile_h,
-                                    cfg.tile_x0, cfg.tile_y0)
+                                    cfg.tile_x0, cfg.tile_y0, self.speed)
         self.levels = _rate.level_params(quantizer, bit_depth)
         for lv, d in enumerate(self.levels):
             p = RvReplayLevelParams.from_dict(d)

@@ -415,7 +415,7 @@ class CpuReplay:
     baseline_lib()[0])."""
 
     def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, group=None,
-                 tile_size=(0, 0), n_inputs=8, threads=1, L=None, quantizer=100):
+                 tile_size=(0, 0), n_inputs=8, threads=1, L=None, quantizer=100, speed=10):
         from rav1e_amd import rate as RT
         L = L or lib()
         self.L = L
@@ -438,8 +438,11 @@ class CpuReplay:
         self.h = L.orc_replay_create(width, height, xdec, ydec, bit_depth, tx0, ty0, tw, th,
                                      tile_size[0], tile_size[1], n_refs, n_inputs, threads)
         assert self.h, "orc_replay_create failed"
-        sbc, sbr = (width + 63) // 64, (height + 63) // 64
-        self.n_words = (tw or sbc - tx0) * (th or sbr - ty0) * (8 * n_refs + 4) + 5
+        from rav1e_amd.replay import result_words
+        L.orc_replay_set_speed.argtypes = [C.c_void_p, C.c_int]
+        assert L.orc_replay_set_speed(self.h, speed) == 0, "orc_replay_set_speed"
+        self.speed = speed
+        self.n_words = result_words(width, height, n_refs, tw, th, tx0, ty0, speed)
         self.geom = (width, height, xdec, ydec, bit_depth)
         self.levels = RT.level_params(quantizer, bit_depth)
         for lv, d in enumerate(self.levels):

@@ -167,6 +167,41 @@ def test_cpu_tile_groups_equal_the_whole_frame():
             assert wg[-1] == ws[-1]  # every rank holds the whole reconstruction
 
 
+def test_cpu_speed6_partition_and_levels():
+    """Speed 6 (config D): thread-invariant words; the 64x64 words keep the
+    speed-10 layout; every superblock's partition mask is a valid tree
+    (a 32x32 split only under a 64x64 split, a 16x16 split only under its
+    32x32's); the bottom superblock row of a 200-row frame (8 visible rows)
+    must split down to its 8x8 blocks."""
+    w, h = 256, 200
+    fr = _frames(w, h, 1, 1, 8, 10)
+    outs = []
+    for threads in (1, 3):
+        r = O.CpuReplay(w, h, 1, 1, 8, 2, n_inputs=10, threads=threads, speed=6, quantizer=60)
+        for i, f in enumerate(fr):
+            r.set_input(i, f)
+        for _ in range(5):
+            r.frame()
+        outs.append(r.results())
+    np.testing.assert_array_equal(outs[0], outs[1])
+    wd = outs[0]
+    assert wd.size == RP.result_words(w, h, 2, speed=6)
+    sbw, lv, part, tail = RP.level_words(w, h, 2, wd)
+    assert [x.shape[0] for x in lv] == [64, 256, 1024]
+    for m in part.astype(np.int64):
+        if not m & 1:
+            assert m == 0
+        for q in range(4):
+            if not m & (2 << q):
+                for t in range(4):  # the 16x16 blocks of quadrant q
+                    assert not m & (1 << (5 + ((q >> 1) * 2 + (t >> 1)) * 4 + (q & 1) * 2 + (t & 1)))
+    # y = 192: the 64x64, its 32x32 and its 16x16 blocks are past the edge
+    for m in part[-4:].astype(np.int64):
+        assert m & 1 and m & 2 and m & 4 and m & (1 << 5) and m & (1 << 6)
+    assert (lv[2][:, 9] <= 1).all() and (lv[2][:, 8] < 14).all()
+    assert tail[0] != 0  # some committed block codes coefficients at quantizer 60
+
+
 @pytest.mark.gpu
 def test_gpu_synth_equals_numpy_twin():
     import rav1e_amd as R
@@ -189,7 +224,8 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
                      quantizer=quantizer)
     g.synth_inputs(0)
     c = O.CpuReplay(w, h, xdec, ydec, bd, refs, tile_size=ts, n_inputs=nin,
-                    threads=O.cpu_share(), quantizer=quantizer)
+                    threads=O.cpu_share(), quantizer=quantizer,
+                    speed=6 if flags & RP.RV_REPLAY_SPEED6 else 10)
     for i in range(nin):
         c.set_input(i, g.get_input(i))
     if imp is not None:
@@ -215,17 +251,21 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
     (384, 192, 1, 1, 8, 2, {"tile_cols": 2}, 0),
     (384, 256, 0, 0, 8, 2, {"tiles": 4}, 0),
     (256, 192, 1, 1, 8, 2, None, RP.RV_REPLAY_EXHAUSTIVE_FS),
+    (256, 200, 1, 1, 8, 2, None, RP.RV_REPLAY_SPEED6),      # speed 6: partition RDO
+    (256, 136, 1, 1, 10, 2, None, RP.RV_REPLAY_SPEED6),
+    (192, 128, 0, 0, 8, 2, {"tile_cols": 2}, RP.RV_REPLAY_SPEED6),
 ])
 def test_gpu_replay_matches_cpu_replay(w, h, xdec, ydec, bd, refs, tiling, flags):
     _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, 10, tiling, flags)
 
 
 @pytest.mark.gpu
-def test_gpu_replay_importance_bias_and_quantizer():
+@pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_SPEED6])
+def test_gpu_replay_importance_bias_and_quantizer(flags):
     w, h = 256, 192
     rng = np.random.default_rng(3)
     imp = rng.random((h // 8) * (w // 8)).astype(np.float32) * 7
-    _gpu_vs_cpu(w, h, 1, 1, 8, 2, 6, imp=imp, quantizer=60)
+    _gpu_vs_cpu(w, h, 1, 1, 8, 2, 6, imp=imp, quantizer=60, flags=flags)
 
 
 @pytest.mark.gpu
