@@ -31,13 +31,13 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# name: (width, height, xdec, ydec, bit_depth, tiling kwargs, BASELINE config)
+# name: (width, height, xdec, ydec, bit_depth, tiling kwargs, BASELINE config, speed)
 CONFIGS = {
-    "360p": (640, 360, 1, 1, 8, {}, "A"),
-    "1080p": (1920, 1080, 1, 1, 8, {}, "B"),
-    "2160p": (3840, 2160, 1, 1, 8, {"tile_cols": 8}, "C"),
-    "2160p10": (3840, 2160, 1, 1, 10, {}, "D (speed-10 schedule)"),
-    "2160p444": (3840, 2160, 0, 0, 8, {"tiles": 4}, "E"),
+    "360p": (640, 360, 1, 1, 8, {}, "A", 10),
+    "1080p": (1920, 1080, 1, 1, 8, {}, "B", 10),
+    "2160p": (3840, 2160, 1, 1, 8, {"tile_cols": 8}, "C", 10),
+    "2160p10": (3840, 2160, 1, 1, 10, {}, "D", 6),
+    "2160p444": (3840, 2160, 0, 0, 8, {"tiles": 4}, "E", 10),
 }
 TIMING_STRIDE = 4  # in GOPs
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -51,6 +51,11 @@ VALU_PEAK_INT = 256 * 1 * 2.4
 STAGES = ["F0_pyramid", "F1_full_search", "F2_diamond_half", "F3_diamond_fullpel",
           "F3_diamond_subpel", "F4_rdo_single_ref", "F4_rdo_compound", "F4_rd_cost_argmin",
           "F6_commit", "F5_importance_satd", "F7_pad_exchange"]
+# speed 6: the 32x32 / 16x16 / 8x8 searches run inside the sub-pel stage,
+# their candidates inside F4, the partition decision with the argmin
+STAGES6 = ["F0_pyramid", "F1_full_search", "F2_diamond_half", "F3_diamond_fullpel",
+           "F3_subpel_and_level_me", "F4_rdo_single_ref_all_levels", "F4_rdo_compound_all_levels",
+           "F4_argmin_partition", "F6_commit_leaves", "F5_importance_satd", "F7_pad_exchange"]
 
 
 def coarse_windows(W, H, R, scale, tiling, group):
@@ -135,7 +140,8 @@ def timed_run(engine, group, steps, warmup, sync=None):
     return group.max(t1 - t0), words
 
 
-def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling, n_inputs):
+def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling, n_inputs,
+                            speed=10):
     """The CPU baseline and the full-size parity check, from one CPU run.
 
     The CPU replay (oracle/orc_replay.c: the same schedule over the oracle's
@@ -153,7 +159,8 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     threads = O.cpu_share()
     ts = (tiling["tile_width_sb"], tiling["tile_height_sb"])
     nin = len(hip_inputs)
-    c = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=threads, L=L)
+    c = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=threads, L=L,
+                    speed=speed)
     for i in range(nin):
         c.set_input(i, hip_inputs[i])
     c.frame()  # the key frame (a copy), untimed
@@ -168,7 +175,8 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     # 1 thread: the first 1/8 of the superblocks of one GOP
     nsb = ((W + 63) // 64) * ((H + 63) // 64)
     lim = max(1, nsb // 8)
-    c1 = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=1, L=L)
+    c1 = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=1, L=L,
+                     speed=speed)
     for i in range(nin):
         c1.set_input(i, hip_inputs[i])
     c1.frame()
@@ -188,7 +196,8 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
                           "sample": f"first {lim} of {nsb} superblocks of each frame of one GOP, "
                                     f"scaled to whole frames"}}
     # the GPU replay over the same frames, word for word
-    g = RP.HipReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=n_inputs)
+    g = RP.HipReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=n_inputs,
+                     flags=RP.RV_REPLAY_SPEED6 if speed == 6 else 0)
     g.synth_inputs(0)
     g.frame()
     bad = []
@@ -216,6 +225,8 @@ def main():
     ap.add_argument("--refs", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--speed", type=int, choices=(6, 10), default=None,
+                    help="schedule (default: the config's BASELINE speed)")
     ap.add_argument("--exhaustive-fs", action="store_true",
                     help="F1 coarse search without successive elimination (same results)")
     args = ap.parse_args()
@@ -229,13 +240,15 @@ def main():
     group = RankGroup(info)
     R.require_device(info.local_rank % max(1, R.lib().rv_device_count()))
 
-    W, H, xdec, ydec, bd, tkw, cfg_name = CONFIGS[args.config]
+    W, H, xdec, ydec, bd, tkw, cfg_name, speed = CONFIGS[args.config]
+    speed = args.speed or speed
     nref = args.refs
     tiling = RP.tiling_for(W, H, **tkw)
     ts = (tiling["tile_width_sb"], tiling["tile_height_sb"])
     rects = RP.tile_groups(tiling, world)
     n_inputs = args.warmup + args.steps + 8  # every display the run codes
-    flags = RP.RV_REPLAY_EXHAUSTIVE_FS if args.exhaustive_fs else 0
+    flags = (RP.RV_REPLAY_EXHAUSTIVE_FS if args.exhaustive_fs else 0) | \
+        (RP.RV_REPLAY_SPEED6 if speed == 6 else 0)
     hip = RP.HipReplay(W, H, xdec, ydec, bd, nref, group=rects[rank], tile_size=ts,
                        n_inputs=n_inputs, flags=flags)
     hip.synth_inputs(0)  # the stream's frames, resident in HBM before the timing
@@ -253,7 +266,8 @@ def main():
     k = min(sum(1 for f in nonkey if (f // gop) % TIMING_STRIDE == 0), 64)
     k = max(k, 1)
     ms = hip.stage_ms_sum(k) / k  # per frame
-    ev_full, ev_sub, ev_frames, n_single, n_comp = (int(v) for v in hip.counters())
+    cnt = [int(v) for v in hip.counters()]
+    ev_full, ev_sub, ev_frames, n_single, n_comp = cnt[:5]
     ev_frames = max(1, ev_frames)
     gx0, gy0, gw, gh = rects[rank]
     nsb = gw * gh
@@ -279,6 +293,19 @@ def main():
     # commit: one candidate per superblock, + levels and the reconstruction
     commit_bytes = float(nsb * ((71 * 71 + 2 * 64 * 64) * px + 4096 + 16) +
                          2 * nsb * ntx_c * ((39 * 39 + 2 * 32 * 32) * px + 4096))
+    level_cands = {}
+    if speed == 6:
+        # the 32x32 / 16x16 / 8x8 candidates: B x B luma ((B+7)^2 window + source),
+        # bc x bc per chroma plane, 3 result words each; compound reads two windows
+        for l in (1, 2, 3):
+            B = 64 >> l
+            bc = B >> xdec
+            s1, c1 = cnt[5 + 2 * (l - 1)] / ev_frames, cnt[6 + 2 * (l - 1)] / ev_frames
+            level_cands[f"{B}x{B}"] = {"single_ref": round(s1, 1), "compound": round(c1, 1)}
+            rdo_bytes += s1 * (((B + 7) ** 2 + B * B) * px + 24 +
+                               2 * (((bc + 7) ** 2 + bc * bc) * px + 24))
+            comp_bytes += c1 * ((2 * (B + 7) ** 2 + B * B) * px + 24 +
+                                2 * ((2 * (bc + 7) ** 2 + bc * bc) * px + 24))
     kernels = {
         "full_search": dict(ms=float(ms[1]), bytes=fs_bytes),
         "diamond_fullpel_64": dict(ms=float(ms[3]),
@@ -319,7 +346,7 @@ def main():
         inputs = [hip.get_input(i) for i in range(min(22, n_inputs))]
         hip.close()  # the parity pass below builds a fresh GPU replay
         cpu, parity = cpu_baseline_and_parity(args, inputs, W, H, xdec, ydec, bd, nref,
-                                              tiling, n_inputs)
+                                              tiling, n_inputs, speed)
 
     if rank == 0:
         line = {
@@ -329,26 +356,29 @@ def main():
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "u16" if bd > 8 else "u8", "data": "synthetic",
             "config": {"workload": f"{args.config} {bd}-bit "
-                                   f"{'4:2:0' if xdec else '4:4:4'} speed=10 hot-path replay of one "
+                                   f"{'4:2:0' if xdec else '4:4:4'} speed={speed} hot-path replay of one "
                                    f"stream (BASELINE config {cfg_name}), "
                                    f"{tiling['cols']}x{tiling['rows']} tiles over {world} GPU(s), "
                                    f"{nref} refs, reorder-pyramid coding order",
-                       "width": W, "height": H, "refs": nref, "speed": 10,
+                       "width": W, "height": H, "refs": nref, "speed": speed,
                        "tiles": [tiling["cols"], tiling["rows"]],
                        "parallelism": f"tile-groups{world}",
-                       "candidates_per_sb": f"{4 * nref} inter modes x (skip, non-skip)"},
+                       "candidates_per_sb": f"{4 * nref} inter modes x (skip, non-skip)",
+                       **({"partition": "64x64 .. 8x8 top-down NONE vs SPLIT, every level "
+                                        "searched and scored"} if speed == 6 else {})},
             "mpix_per_s": round(fps * W * H / 1e6, 3),
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,
             "gpu_vs_cpu": round(fps / cpu["value"], 2) if cpu else None,
-            "stage_ms": {n: round(float(v), 4) for n, v in zip(STAGES, ms)},
+            "stage_ms": {n: round(float(v), 4) for n, v in zip(STAGES6 if speed == 6 else STAGES, ms)},
             "kernels_ms": {n: round(v["ms"], 4) for n, v in kernels.items()},
             "full_search_path": "successive elimination" if sea else "exhaustive",
             "diamond_evals_per_frame": [round(ev_full / ev_frames, 1),
                                         round(ev_sub / ev_frames, 1)],
             "rdo_candidates_per_frame": {"single_ref": round(ns, 1), "compound": round(nc, 1),
-                                         "variants": "skip + non-skip each"},
+                                         "variants": "skip + non-skip each",
+                                         **({"levels": level_cands} if level_cands else {})},
             "checksum": int(words[-5]) & 0xFFFFFFFF,
         }
         print(json.dumps(line), flush=True)

@@ -344,8 +344,8 @@ __global__ __launch_bounds__(64) void score_level(CandGeo cg, double lambda, dou
                                                   int32_t *cand_count, uint32_t *evals) {
   const int b = blockIdx.x * 64 + threadIdx.x;
   if (b == 0) {
-    atomicAdd((unsigned int *)&evals[0], (unsigned int)*cand_count);
-    atomicAdd((unsigned int *)&evals[1], (unsigned int)(cg.comp * cg.nsb));
+    evals[0] = (uint32_t)*cand_count;
+    evals[1] = (uint32_t)(cg.comp * cg.nsb);
     *cand_count = 0;
   }
   if (b >= cg.nsb) return;
@@ -527,7 +527,7 @@ struct rv_replay {
   uint64_t *l_out, *c_out;  // F4: [skip dist, non-skip dist, rate] per transform block
   RdoWinner *win;
   int32_t *cand_list, *cand_count;  // F4: the valid candidates
-  uint32_t *cand_evals;             // [kRing][2]: F4 candidates per frame (single, compound)
+  uint32_t *cand_evals;  // [kRing][2 * kLevels]: F4 candidates per frame and level (single, compound)
   int32_t *l_lev, *c_lev;   // F6: committed levels
   uint64_t *words;
   unsigned long long *tail;  // [levels csum, group recon sum, imp satd sum, -, frame recon sum]
@@ -921,8 +921,9 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->win = (RdoWinner *)dalloc(r, (size_t)g.nsb * sizeof(RdoWinner));
   r->cand_list = (int32_t *)dalloc(r, (size_t)nc * 4);
   r->cand_count = (int32_t *)dalloc(r, 4);
-  r->cand_evals = (uint32_t *)dalloc(r, rv_replay::kRing * 2 * 4);
-  if (r->cand_evals) (void)hipMemsetAsync(r->cand_evals, 0, rv_replay::kRing * 2 * 4, r->stream);
+  r->cand_evals = (uint32_t *)dalloc(r, rv_replay::kRing * 2 * kLevels * 4);
+  if (r->cand_evals)
+    (void)hipMemsetAsync(r->cand_evals, 0, rv_replay::kRing * 2 * kLevels * 4, r->stream);
   if (r->cand_count) (void)hipMemsetAsync(r->cand_count, 0, 4, r->stream);
   r->l_lev = (int32_t *)dalloc(r, (size_t)g.nsb * 1024 * 4);
   r->c_lev = (int32_t *)dalloc(r, (size_t)g.nsb * r->ntx_c * 1024 * 4 * 2);
@@ -1420,7 +1421,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                                      r->c_out, r->c_out + nct * 3, ntx_c, r->win,
                                                      r->coarse, r->half, r->full, r->words,
                                                      r->cand_count, r->tail + 2,
-                                                     r->cand_evals + 2 * slot, r->leaf_count);
+                                                     r->cand_evals + 2 * slot * kLevels,
+                                                     r->leaf_count);
   if (r->s6) {
     PartArgs pa;
     memset(&pa, 0, sizeof(pa));
@@ -1432,7 +1434,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
         score_level<<<(P.n + 63) / 64, 64, 0, st>>>(cgl, L.lambda, L.ds[1], L.ds[2], P.full, P.sub,
                                                     P.l_out, P.c_out, P.c_out + (size_t)P.n * g.C * 3,
                                                     P.win, r->words + P.woff, P.cand_count,
-                                                    r->cand_evals + 2 * slot);
+                                                    r->cand_evals + 2 * (slot * kLevels + l));
       }
       pa.win[l] = l ? P.win : r->win;
       pa.gw[l] = P.gw;
@@ -1592,9 +1594,10 @@ int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out, int 
   return stage_times(r, ms_out, cap, last_frames);
 }
 // Candidate evaluations summed over the last min(frames, 64) coded frames:
-// out[0] F3 full-pel diamond, out[1] F3 sub-pel diamond, out[2] frames
-// summed, and (cap >= 5) out[3] / out[4] the F4 single-reference / compound
-// RDO candidates.
+// out[0] F3 full-pel diamond, out[1] F3 sub-pel diamond (64x64 jobs), out[2]
+// frames summed, (cap >= 5) out[3] / out[4] the F4 single-reference /
+// compound RDO candidates of the 64x64 blocks, (cap >= 11, speed 6) out[5 +
+// 2 (l - 1)] / out[6 + 2 (l - 1)] those of the 32x32, 16x16, 8x8 blocks.
 int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
   if (!r || !out || cap < 3) return rv_set_error(RV_EINVAL, "rv_replay_counters");
   const Geo &g = r->g;
@@ -1610,14 +1613,18 @@ int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
       for (int j = 0; j < nj; j++) out[k] += h[((size_t)f * 2 + k) * nj + j];
   out[2] = (uint64_t)nf;
   if (cap < 5) return 3;
-  std::vector<uint32_t> ce((size_t)nf * 2);
+  const int nl = cap >= 11 ? kLevels : 1;
+  std::vector<uint32_t> ce((size_t)nf * 2 * kLevels);
   if (nf) RV_H(hipMemcpy(ce.data(), r->cand_evals, ce.size() * 4, hipMemcpyDeviceToHost));
-  out[3] = out[4] = 0;
-  for (int f = 0; f < nf; f++) {
-    out[3] += ce[2 * f];
-    out[4] += ce[2 * f + 1];
+  for (int l = 0; l < nl; l++) {
+    uint64_t &a = out[l ? 5 + 2 * (l - 1) : 3], &b = out[l ? 6 + 2 * (l - 1) : 4];
+    a = b = 0;
+    for (int f = 0; f < nf; f++) {
+      a += ce[(size_t)(f * kLevels + l) * 2];
+      b += ce[(size_t)(f * kLevels + l) * 2 + 1];
+    }
   }
-  return 5;
+  return nl == 1 ? 5 : 11;
 }
 
 // ---- RCCL communicator for the tile-group exchange ---------------------------

@@ -322,9 +322,11 @@ class HipReplay:
 
     def counters(self) -> np.ndarray:
         """[F3 full-pel evals, F3 sub-pel evals, frames, F4 single-reference
-        candidates, F4 compound candidates] over the last <= 64 frames."""
-        out = np.zeros(5, dtype=np.uint64)
-        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 5) - 5, "rv_replay_counters")
+        candidates, F4 compound candidates of the 64x64 blocks, then (speed
+        6) single / compound of the 32x32, 16x16 and 8x8 blocks] over the
+        last <= 64 frames."""
+        out = np.zeros(11, dtype=np.uint64)
+        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 11) - 11, "rv_replay_counters")
         return out
 
     def close(self):

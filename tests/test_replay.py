@@ -317,10 +317,12 @@ def test_gpu_tile_groups_exchange():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("config", ["1080p", "2160p", "2160p10", "2160p444"])
-def test_gpu_replay_full_size_gop(config):
+@pytest.mark.parametrize("config,speed", [("1080p", 10), ("2160p", 10), ("2160p10", 10),
+                                          ("2160p10", 6), ("2160p444", 10)])
+def test_gpu_replay_full_size_gop(config, speed):
     """The key frame and one GOP (me_range_scale 4, 2, 1, 1) at the BASELINE
-    shapes and tilings, GPU words equal to the CPU replay's frame by frame."""
+    shapes and tilings (config D also at its speed-6 schedule), GPU words
+    equal to the CPU replay's frame by frame."""
     import bench
-    w, h, xdec, ydec, bd, tk, _ = bench.CONFIGS[config]
-    _gpu_vs_cpu(w, h, xdec, ydec, bd, 2, 5, tk)
+    w, h, xdec, ydec, bd, tk = bench.CONFIGS[config][:6]
+    _gpu_vs_cpu(w, h, xdec, ydec, bd, 2, 5, tk, flags=RP.RV_REPLAY_SPEED6 if speed == 6 else 0)
