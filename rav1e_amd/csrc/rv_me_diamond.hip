@@ -20,8 +20,8 @@
 //    four v_dot2_i32_i16 (u16), the vertical 8-tap a register ring of the
 //    i16 intermediates, and |org - pred| accumulates in registers -- the
 //    prediction never leaves the wavefront.
-// Anything else (SATD, other sizes) takes the generic workgroup-per-
-// candidate kernel.
+// SATD and square blocks of 8 and 16: ds_grp_kernel (lane groups per job).
+// Anything else takes the generic workgroup-per-candidate kernel.
 #include <stdlib.h>
 #include <string.h>
 
@@ -1014,6 +1014,291 @@ __global__ __launch_bounds__(64) void ds_wave_kernel(DsArgs a) {
   }
 }
 
+// Square blocks with SATD (use_satd_subpel, src/me.rs:232-253) and the
+// small full-pel searches of the speed-6 partition levels: one group of
+// L = 4 C lanes per job, 64 / L jobs per wavefront, every round's (up to) 4
+// candidates evaluated at once by the group's four C-lane subgroups.  A
+// lane owns RPL rows x 8 columns of one 8x8 chunk of its candidate (CPL
+// chunks in turn): it forms org - prediction for them (sub-pel: put_8tap
+// of its rows, the horizontal pass streamed row by row into per-row
+// vertical accumulators), then for SATD the 8-point row Hadamards in-lane
+// and the column butterflies in-lane over its rows and across the LPC lanes
+// of the chunk by shuffles (get_satd's 8x8 Hadamard, src/dist.rs:208-272:
+// the sum of |coefficients| does not depend on the butterfly order).  The
+// subgroup's sums meet by shuffles, the four costs by shuffles across the
+// group, so a job's rounds need no LDS and no barrier; groups of one
+// wavefront diverge freely (a shuffle only reads its own group's lanes).
+template <int N>
+struct GrpGeo {
+  static constexpr int C = N == 8 ? 4 : 16;            // lanes per candidate
+  static constexpr int L = 4 * C;                      // lanes per job
+  static constexpr int RPL = N == 64 || N == 32 ? 8 : 2;  // chunk rows per lane
+  static constexpr int LPC = 8 / RPL;                  // lanes per chunk
+  static constexpr int NC = N / 8;                     // chunks per row
+  static constexpr int CPL = NC * NC * LPC / C;        // chunks per lane
+};
+
+template <typename Px, int N, bool SUB, bool SATD>
+__global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
+  using G = GrpGeo<N>;
+  static_assert(G::CPL >= 1 && G::C % G::LPC == 0, "lane layout");
+  const int lane = threadIdx.x & 63;
+  const int gl = lane % G::L, k = gl / G::C, c = gl % G::C;
+  const int gbase = lane - gl;  // the group's first lane
+  const int job = ((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * (64 / G::L) + lane / G::L;
+  if (job - (lane / G::L) >= a.n) return;  // the whole wavefront is past the jobs
+  const bool live = job < a.n;
+  const int jid = live ? job : a.n - 1;
+  const rv_ds_job *jp = a.jobs + jid;
+  const rv_ds_job jb = *jp;
+  const rv_plane &ref = a.ref[jid / a.n_per_ref];
+  const int ib = a.bd == 12 ? 2 : 4, maxv = (1 << a.bd) - 1;
+  const int lic = c % G::LPC;  // lane in chunk
+
+  // distortion of candidate mv for this subgroup (all lanes of the
+  // subgroup return it); ok = false: zero work, the value is unused
+  auto dist = [&](rv_mv mv, bool ok) -> uint32_t {
+    int cf = 0, rf = 0, sx = 0, sy = 0;
+    if (SUB) {
+      const int xs = 3 + ref.xdec, ys = 3 + ref.ydec;
+      const int roff = (int)mv.row >> ys, coff = (int)mv.col >> xs;
+      rf = ((int)mv.row - (roff << ys)) << (4 - ys);
+      cf = ((int)mv.col - (coff << xs)) << (4 - xs);
+      sx = clampi(jb.po_x + coff - 3, -ref.xorigin, ref.width);  // window origin (-3, -3)
+      sy = clampi(jb.po_y + roff - 3, -ref.yorigin, ref.height);
+    } else {
+      sx = jb.po_x + (ok ? mv.col / 8 : 0);
+      sy = jb.po_y + (ok ? mv.row / 8 : 0);
+    }
+    const int8_t *xf = kReg[0][cf];
+    const int8_t *yf = kReg[0][rf];
+    uint32_t acc = 0;
+#pragma unroll 1
+    for (int j = 0; j < G::CPL; j++) {
+      const int q = c / G::LPC + j * (G::C / G::LPC);
+      const int x0 = (q % G::NC) * 8, y0 = (q / G::NC) * 8 + lic * G::RPL;
+      int32_t d[G::RPL][8];
+      if (ok) {
+        if (!SUB) {
+#pragma unroll
+          for (int i = 0; i < G::RPL; i++) {
+            const Px *o = plane_ptr<Px>(a.org, jb.po_x + x0, jb.po_y + y0 + i);
+            const Px *r = plane_ptr<Px>(ref, sx + x0, sy + y0 + i);
+#pragma unroll
+            for (int t = 0; t < 8; t++) d[i][t] = (int32_t)o[t] - (int32_t)r[t];
+          }
+        } else {
+          // output rows y0 .. y0 + RPL - 1 need window rows y0 .. y0 + RPL + 6
+          int32_t v[G::RPL][8];
+#pragma unroll
+          for (int i = 0; i < G::RPL; i++)
+#pragma unroll
+            for (int t = 0; t < 8; t++) v[i][t] = 0;
+#pragma unroll
+          for (int m = 0; m < G::RPL + 7; m++) {
+            if (!rf && (m < 3 || m >= G::RPL + 3)) continue;  // only rows i + 3 are used
+            const Px *w = plane_ptr<Px>(ref, sx + x0, sy + y0 + m);
+            int32_t mid[8];
+            if (cf) {
+              int32_t px[15];
+#pragma unroll
+              for (int t = 0; t < 15; t++) px[t] = w[t];
+#pragma unroll
+              for (int t = 0; t < 8; t++) {
+                int32_t s = 0;
+#pragma unroll
+                for (int u = 0; u < 8; u++) s += __mul24((int32_t)xf[u], px[t + u]);
+                mid[t] = round_shift(s, 7 - ib);
+              }
+            } else {
+#pragma unroll
+              for (int t = 0; t < 8; t++) mid[t] = w[t + 3];
+            }
+            if (rf) {
+#pragma unroll
+              for (int i = 0; i < G::RPL; i++) {
+                const int kk = m - i;
+                if (kk >= 0 && kk < 8) {
+                  const int32_t f = yf[kk];
+#pragma unroll
+                  for (int t = 0; t < 8; t++) v[i][t] += __mul24(f, mid[t]);
+                }
+              }
+            } else {
+#pragma unroll
+              for (int t = 0; t < 8; t++) v[m - 3][t] = cf ? round_shift(mid[t], ib) : mid[t];
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < G::RPL; i++) {
+            const Px *o = plane_ptr<Px>(a.org, jb.po_x + x0, jb.po_y + y0 + i);
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+              int32_t p = v[i][t];
+              if (rf) p = round_shift(p, cf ? 7 + ib : 7);
+              p = clampi(p, 0, maxv);
+              d[i][t] = (int32_t)o[t] - p;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < G::RPL; i++)
+#pragma unroll
+          for (int t = 0; t < 8; t++) d[i][t] = 0;
+      }
+      if (SATD) {
+#pragma unroll
+        for (int i = 0; i < G::RPL; i++) ds_had<8>(&d[i][0], 1);  // rows
+        // columns: row bits inside the lane ...
+#pragma unroll
+        for (int b = 1; b < G::RPL; b <<= 1)
+#pragma unroll
+          for (int i = 0; i < G::RPL; i++)
+            if (!(i & b))
+#pragma unroll
+              for (int t = 0; t < 8; t++) {
+                const int32_t x = d[i][t], y = d[i + b][t];
+                d[i][t] = x + y;
+                d[i + b][t] = x - y;
+              }
+        // ... and across the chunk's lanes
+#pragma unroll
+        for (int b = 1; b < G::LPC; b <<= 1) {
+          const bool up = (lic & b) != 0;
+#pragma unroll
+          for (int i = 0; i < G::RPL; i++)
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+              const int32_t p = __shfl_xor(d[i][t], b, 64);
+              d[i][t] = up ? p - d[i][t] : d[i][t] + p;
+            }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < G::RPL; i++)
+#pragma unroll
+        for (int t = 0; t < 8; t++) acc += (uint32_t)(d[i][t] < 0 ? -d[i][t] : d[i][t]);
+    }
+#pragma unroll
+    for (int m = G::C / 2; m; m >>= 1) acc += __shfl_xor(acc, m, 64);
+    return SATD ? (acc + 4) >> 3 : acc;  // get_satd: (sum + (1 << ln >> 1)) >> ln, ln = 3
+  };
+
+  uint32_t evals = 0;
+  // costs of cands[0..3] (u64::MAX when out of range, skipped or >= n),
+  // uniform over the group
+  auto round4 = [&](const rv_mv *cands, int n, int skip, uint64_t *cost)
+      __attribute__((always_inline)) {
+    bool ok[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++) {
+      ok[kk] = kk < n && kk != skip && ds_in_range(cands[kk], jb);
+      evals += ok[kk];
+    }
+    rv_mv mine = cands[0];
+    bool okm = ok[0];
+#pragma unroll
+    for (int kk = 1; kk < 4; kk++)
+      if (k == kk) {
+        mine = cands[kk];
+        okm = ok[kk];
+      }
+    const uint32_t dv = dist(mine, okm);
+    const uint64_t cm = okm ? ds_cost(dv, mine, jb, a.hp) : ~0ull;
+    const uint32_t lo = (uint32_t)cm, hi = (uint32_t)(cm >> 32);
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++) {
+      const uint32_t l = __shfl(lo, gbase + kk * G::C, 64), h = __shfl(hi, gbase + kk * G::C, 64);
+      cost[kk] = ((uint64_t)h << 32) | l;
+    }
+  };
+
+  rv_mv center{0, 0};
+  uint64_t center_cost = ~0ull;
+  const int np = jb.n_pred < RV_DS_MAX_PRED ? jb.n_pred : RV_DS_MAX_PRED;
+  int16_t radius = SUB ? 4 : 16;
+  const int16_t radius_end = SUB ? (a.hp ? 1 : 2) : 8;
+  int p0 = 0, back = -1;
+  for (int iter = 0; iter < 4096 + RV_DS_MAX_PRED; iter++) {
+    const bool pred_phase = p0 < np;
+    rv_mv c4[4];
+    int n;
+    if (pred_phase) {
+      n = np - p0 < 4 ? np - p0 : 4;
+#pragma unroll
+      for (int kk = 0; kk < 4; kk++) c4[kk] = jp->pred[p0 + (kk < n ? kk : 0)];
+    } else {
+      n = 4;
+      c4[0] = rv_mv{(int16_t)(center.row + radius), center.col};  // diamond_pattern
+      c4[1] = rv_mv{center.row, (int16_t)(center.col + radius)};
+      c4[2] = rv_mv{(int16_t)(center.row - radius), center.col};
+      c4[3] = rv_mv{center.row, (int16_t)(center.col - radius)};
+    }
+    uint64_t cst[4];
+    round4(c4, n, pred_phase ? -1 : back, cst);
+    uint64_t best = ~0ull;
+    int bp = 0;
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++)
+      if (kk < n && cst[kk] < best) {
+        best = cst[kk];
+        bp = kk;
+      }
+    rv_mv bmv = c4[0];
+#pragma unroll
+    for (int kk = 1; kk < 4; kk++)
+      if (bp == kk) bmv = c4[kk];
+    if (pred_phase) {
+      if (best < center_cost) {
+        center = bmv;
+        center_cost = best;
+      }
+      p0 += 4;
+    } else if (center_cost <= best) {
+      if (radius == radius_end) break;
+      radius /= 2;
+      back = -1;
+    } else {
+      back = center_cost != ~0ull ? (bp + 2) & 3 : -1;
+      center = bmv;
+      center_cost = best;
+    }
+  }
+  if (gl == 0 && live) {
+    if (a.evals) a.evals[job] = evals;
+    ds_write(a, job, center, center_cost);
+    chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, center);
+  }
+}
+
+template <typename Px>
+bool try_grp(const DsArgs &a, hipStream_t s) {
+  if (a.tele || a.w != a.h) return false;
+  const int n = a.w;
+  const bool small = n == 8 || n == 16;
+  if (!(small || (a.satd && (n == 32 || n == 64)))) return false;
+  const int jpw = 64 / (n == 8 ? 16 : 64);
+  const unsigned grid = (unsigned)((a.n + 4 * jpw - 1) / (4 * jpw));
+#define RV_GRP(N)                                                                     \
+  if (n == N) {                                                                       \
+    if (a.subpel) {                                                                   \
+      if (a.satd) ds_grp_kernel<Px, N, true, true><<<grid, 256, 0, s>>>(a);           \
+      else ds_grp_kernel<Px, N, true, false><<<grid, 256, 0, s>>>(a);                 \
+    } else {                                                                          \
+      if (a.satd) ds_grp_kernel<Px, N, false, true><<<grid, 256, 0, s>>>(a);          \
+      else ds_grp_kernel<Px, N, false, false><<<grid, 256, 0, s>>>(a);                \
+    }                                                                                 \
+    return true;                                                                      \
+  }
+  RV_GRP(8)
+  RV_GRP(16)
+  RV_GRP(32)
+  RV_GRP(64)
+#undef RV_GRP
+  return false;
+}
+
 // Blocks up to 32x32 take ds_wave_kernel (2160p F2, 32x32 at half
 // resolution: 0.031 -> 0.023 ms); 64x64 stays on the 4-wavefront kernel
 // (0.035 vs 0.037 ms: 16 row loads per round from one wavefront issue
@@ -1112,7 +1397,14 @@ static int ds_dispatch(DsArgs &a, void *stream) {
   const int n = a.n, blk_w = a.w, blk_h = a.h, subpixel = a.subpel;
   const rv_plane *org = &a.org;
   hipStream_t s = rv_resolve_stream(stream);
-  const bool fast = org->hbd ? try_fast<uint16_t>(a, s) : try_fast<uint8_t>(a, s);
+  // RAV1E_HIP_DS_GENERIC=1: the workgroup-per-candidate kernel for SATD and
+  // the small blocks (A/B)
+  static const bool grp_on = [] {
+    const char *e = getenv("RAV1E_HIP_DS_GENERIC");
+    return !(e && e[0] == '1');
+  }();
+  const bool fast = (grp_on && (org->hbd ? try_grp<uint16_t>(a, s) : try_grp<uint8_t>(a, s))) ||
+                    (org->hbd ? try_fast<uint16_t>(a, s) : try_fast<uint8_t>(a, s));
   if (!fast) {
     const size_t lds = subpixel ? (size_t)((blk_w + 7) * (blk_h + 7) + (blk_h + 7) * blk_w +
                                            blk_w * blk_h) * sizeof(int16_t)

@@ -511,6 +511,11 @@ def _ds_case(rng, bd, w, h, nj, subpel, edge=False):
     (8, 32, 32, True, False), (8, 16, 32, True, False), (8, 64, 32, True, False),
     (10, 64, 64, False, False), (10, 64, 64, True, False), (10, 32, 32, True, False),
     (8, 8, 8, True, False), (8, 16, 16, True, True), (10, 32, 32, False, True),
+    # lane-group kernel: SATD sub-pel at every square size, small full-pel
+    (8, 8, 8, True, True), (10, 8, 8, True, True), (12, 16, 16, True, True),
+    (10, 32, 32, True, True), (8, 64, 64, True, True), (10, 64, 64, True, True),
+    (8, 8, 8, False, False), (10, 16, 16, False, False), (12, 8, 8, False, True),
+    (10, 16, 16, True, False),
 ])
 def test_diamond_search_vs_oracle(bd, w, h, subpel, satd):
     """Fast (wavefront-per-candidate) and generic paths vs orc_diamond_search."""
@@ -525,15 +530,16 @@ def test_diamond_search_vs_oracle(bd, w, h, subpel, satd):
                 (k, hp, got[k], mv, cost)
 
 
-@pytest.mark.parametrize("bd", [8, 10])
-def test_diamond_subpel_edges_vs_oracle(bd):
+@pytest.mark.parametrize("bd,n,satd", [(8, 64, False), (10, 64, False), (10, 8, True),
+                                       (12, 32, True)])
+def test_diamond_subpel_edges_vs_oracle(bd, n, satd):
     """0/max column stripes (8-tap overshoot) and blocks clamped at the frame edge."""
-    rng = np.random.default_rng(1200 + bd)
-    po_, pr_, fo, fr, jobs, W, H = _ds_case(rng, bd, 64, 64, 16, True, edge=True)
+    rng = np.random.default_rng(1200 + bd + n)
+    po_, pr_, fo, fr, jobs, W, H = _ds_case(rng, bd, n, n, 16, True, edge=True)
     xo, yo = po_.desc.xorigin, po_.desc.yorigin
-    got = R.diamond_search_batch(po_, pr_, jobs, 64, 64, True, False, False, bd)
+    got = R.diamond_search_batch(po_, pr_, jobs, n, n, True, satd, False, bd)
     for k, j in enumerate(jobs):
-        mv, cost = O.diamond_search(fo, fr, xo, yo, W, H, j, 64, 64, True, False, False, bd)
+        mv, cost = O.diamond_search(fo, fr, xo, yo, W, H, j, n, n, True, satd, False, bd)
         assert (got[k]["mv_row"], got[k]["mv_col"], got[k]["cost"]) == (mv[0], mv[1], cost), k
 
 
