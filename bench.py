@@ -48,14 +48,15 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
 # at full occupancy (tools/ubench/valu_rates.hip, profiles/valu_rates.txt)
 VALU_PEAK_GUIDE = 256 * 4 * 2.4 / 2
 VALU_PEAK_INT = 256 * 1 * 2.4
-STAGES = ["F0_pyramid", "F1_full_search", "F2_diamond_half", "F3_diamond_fullpel",
-          "F3_diamond_subpel", "F4_rdo_single_ref", "F4_rdo_compound", "F4_rd_cost_argmin",
-          "F6_commit", "F5_importance_satd", "F7_pad_exchange"]
+STAGES = ["F0_pyramid", "F1_full_search", "F2_half_res_quadrants", "FL_lookahead_16x16",
+          "F3_diamond_fullpel", "F3_diamond_subpel", "F4_rdo_single_ref", "F4_rdo_compound",
+          "F4_rd_cost_argmin", "F6_commit", "F5_importance_satd", "F7_pad_exchange"]
 # speed 6: the 32x32 / 16x16 / 8x8 searches run inside the sub-pel stage,
 # their candidates inside F4, the partition decision with the argmin
-STAGES6 = ["F0_pyramid", "F1_full_search", "F2_diamond_half", "F3_diamond_fullpel",
-           "F3_subpel_and_level_me", "F4_rdo_single_ref_all_levels", "F4_rdo_compound_all_levels",
-           "F4_argmin_partition", "F6_commit_leaves", "F5_importance_satd", "F7_pad_exchange"]
+STAGES6 = ["F0_pyramid", "F1_full_search", "F2_half_res_quadrants", "FL_lookahead_16x16",
+           "F3_diamond_fullpel", "F3_subpel_and_level_me", "F4_rdo_single_ref_all_levels",
+           "F4_rdo_compound_all_levels", "F4_argmin_partition", "F6_commit_leaves",
+           "F5_importance_satd", "F7_pad_exchange"]
 
 
 def coarse_windows(W, H, R, scale, tiling, group):
@@ -308,13 +309,13 @@ def main():
                                 2 * ((2 * (bc + 7) ** 2 + bc * bc) * px + 24))
     kernels = {
         "full_search": dict(ms=float(ms[1]), bytes=fs_bytes),
-        "diamond_fullpel_64": dict(ms=float(ms[3]),
+        "diamond_fullpel_64": dict(ms=float(ms[4]),
                                    bytes=nj * (64 * 64 * px + 80) + ev_full / ev_frames * 64 * 64 * px),
-        "diamond_subpel_64": dict(ms=float(ms[4]),
+        "diamond_subpel_64": dict(ms=float(ms[5]),
                                   bytes=nj * (64 * 64 * px + 80) + ev_sub / ev_frames * 71 * 71 * px),
-        "rdo_candidates": dict(ms=float(ms[5]), bytes=rdo_bytes),
-        "rdo_compound": dict(ms=float(ms[6]), bytes=comp_bytes),
-        "rdo_commit": dict(ms=float(ms[8]), bytes=commit_bytes),
+        "rdo_candidates": dict(ms=float(ms[6]), bytes=rdo_bytes),
+        "rdo_compound": dict(ms=float(ms[7]), bytes=comp_bytes),
+        "rdo_commit": dict(ms=float(ms[9]), bytes=commit_bytes),
     }
     dom = max(kernels, key=lambda n: kernels[n]["ms"])
     kd = kernels[dom]

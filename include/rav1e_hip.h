@@ -510,10 +510,13 @@ int rv_replay_import(rv_replay *r);
 int rv_comm_unique_id(uint8_t *out, int cap);
 void *rv_comm_create(const uint8_t *id, int nranks, int rank);
 void rv_comm_destroy(void *comm);
-/* Copy the last coded frame's results to host: per superblock the search
- * results (8 words per reference) and the RDO winner [candidate, skip,
- * rd cost bits, distortion]; then [levels checksum, group reconstruction
- * sum, importance SATD sum, importance blocks, frame reconstruction sum].
+/* Copy the last coded frame's results to host: per superblock and
+ * reference the search results as (mv, cost) pairs -- coarse, the four
+ * half-res quadrants, full-pel, sub-pel, the 16 lookahead 16x16 blocks (46
+ * words) -- and the RDO winner [candidate, skip, rd cost bits,
+ * distortion]; (speed 6: the level words and partition masks); then
+ * [levels checksum, group reconstruction sum, importance SATD sum,
+ * importance blocks, frame reconstruction sum].
  * Returns the number of u64 written (<= cap). */
 int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
 /* Record the timing events only on frames f with (f / block) % stride == 0

@@ -31,6 +31,9 @@
 #define SB 64
 #define NSLOT 12
 #define NMODE 4
+/* result words per superblock and reference: coarse (mv, cost), the four
+ * half-res quadrants, full-pel, sub-pel, the 16 lookahead 16x16 blocks */
+#define WPR (2 + 8 + 2 + 2 + 32)
 
 typedef struct {
   uint8_t *mem; /* allocation, element 0 */
@@ -67,8 +70,9 @@ typedef struct orc_replay {
   long coded;
   orc_frame_info fi;
   /* per frame */
-  orc_mv *coarse, *half, *full, *sub; /* [R][nsb] */
-  uint64_t *cc, *hc, *fc, *sc;
+  orc_mv *coarse, *half, *full, *sub; /* [R][nsb] (half: [R][nsb][4]) */
+  orc_mv *look;                        /* lookahead: [R][nsb][16] */
+  uint64_t *cc, *hc, *fc, *sc, *lc;
   uint64_t *words;
   int32_t *lev; /* committed levels: per SB luma 1024 + 2 * ntx_c * 1024 */
   uint64_t tail[5];
@@ -293,14 +297,16 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile
   }
   size_t nr = (size_t)r->R * r->nsb;
   r->coarse = calloc(nr, sizeof(orc_mv));
-  r->half = calloc(nr, sizeof(orc_mv));
+  r->half = calloc(nr * 4, sizeof(orc_mv));
+  r->look = calloc(nr * 16, sizeof(orc_mv));
+  r->lc = calloc(nr * 16, 8);
   r->full = calloc(nr, sizeof(orc_mv));
   r->sub = calloc(nr, sizeof(orc_mv));
   r->cc = calloc(nr, 8);
-  r->hc = calloc(nr, 8);
+  r->hc = calloc(nr * 4, 8);
   r->fc = calloc(nr, 8);
   r->sc = calloc(nr, 8);
-  r->nwords = (size_t)r->nsb * (8 * r->R + 4);
+  r->nwords = (size_t)r->nsb * (WPR * r->R + 4);
   r->words = calloc(r->nwords, 8);
   r->lev = calloc((size_t)r->nsb * (1024 + 2 * r->ntx_c * 1024), 4);
   pthread_mutex_init(&r->mu, NULL);
@@ -326,6 +332,8 @@ void orc_replay_destroy(orc_replay *r) {
   free(r->imp);
   free(r->coarse);
   free(r->half);
+  free(r->look);
+  free(r->lc);
   free(r->full);
   free(r->sub);
   free(r->cc);
@@ -356,7 +364,7 @@ int orc_replay_set_speed(orc_replay *r, int speed) {
   if (speed == 10 || r->s6) return 0;
   if (r->xdec != r->ydec) return -1;
   r->s6 = 1;
-  r->nwords = (size_t)r->nsb * (8 * r->R + 4);
+  r->nwords = (size_t)r->nsb * (WPR * r->R + 4);
   for (int l = 1; l < 4; l++) {
     struct olevel *P = &r->pl[l];
     int k = 1 << l;
@@ -608,24 +616,56 @@ static uint64_t tx_block(const orc_replay *r, const oplane *src, int sx, int sy,
                     &r->lv[r->fi.level].q[plane]);
 }
 
-/* Pass A: F1-F3 for one superblock. */
-static void run_me(orc_replay *r, int sb) {
-  const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
-  const oslot *S = &r->slots[r->fi.display % NSLOT];
-  const int R = r->R, hbd = r->hbd;
+/* Static search geometry of superblock sb: its tile's origin, visible
+ * 4x4 size, the superblock's place in the tile and the tile's size in
+ * superblocks. */
+typedef struct {
+  int t0x, t0y, mi_w, mi_h, tsx, tsy, tsw, tsh;
+} sbgeo;
+static sbgeo sb_geo_of(const orc_replay *r, int sb) {
+  sbgeo g;
   const int sx = sb % r->tw, sy = sb / r->tw;
-  uint64_t cost;
-  int t0x, t0y, mi_w, mi_h;
-  sb_tile(r, sx, sy, &t0x, &t0y, &mi_w, &mi_h);
-  int bx = (r->tx0 + sx - t0x) * 16, by = (r->ty0 + sy - t0y) * 16;
-  adjust_bo(mi_w, mi_h, &bx, &by, 64, 64);
-  int fbx = bx + t0x * 16, fby = by + t0y * 16;
+  sb_tile(r, sx, sy, &g.t0x, &g.t0y, &g.mi_w, &g.mi_h);
+  g.tsx = r->tx0 + sx - g.t0x;
+  g.tsy = r->ty0 + sy - g.t0y;
+  g.tsw = (g.mi_w + 15) / 16;
+  g.tsh = (g.mi_h + 15) / 16;
+  return g;
+}
+/* A diamond search context at tile-relative 4x4 offset (bx, by) of size
+ * bw (adjust_bo'd if adj), on the 1 >> shift resolution planes. */
+static void ds_at(const orc_replay *r, orc_ds_ctx *c, const sbgeo *g, const oplane *org,
+                  const oplane *ref, int bx, int by, int bw, int adj, int shift, uint32_t lambda) {
+  if (adj) adjust_bo(g->mi_w, g->mi_h, &bx, &by, bw, bw);
+  const int fbx = bx + g->t0x * 16, fby = by + g->t0y * 16;
+  int m[4];
+  mv_range(r, fbx, fby, bw, bw, m);
+  int ms[4] = {m[0] >> shift, m[1] >> shift, m[2] >> shift, m[3] >> shift};
+  ds_ctx(r, c, org, ref, (fbx * 4) >> shift, (fby * 4) >> shift, bw >> shift, bw >> shift, ms,
+         lambda, 0);
+}
+/* coarse / half-res MVs in 1/8 pel of full resolution, quantize_to_fullpel */
+static orc_mv coarse_fp(const orc_replay *r, int k, int sb) {
+  orc_mv c = r->coarse[(size_t)k * r->nsb + sb];
+  return qfull((orc_mv){(int16_t)(c.row * 4), (int16_t)(c.col * 4)});
+}
+static orc_mv half_fp(const orc_replay *r, int k, int sb, int q) {
+  orc_mv h = r->half[((size_t)k * r->nsb + sb) * 4 + q];
+  return qfull((orc_mv){(int16_t)(h.row * 2), (int16_t)(h.col * 2)});
+}
+
+/* Pass A1: F1 estimate_motion_ss4 (build_coarse_pmvs) of one superblock. */
+static void run_coarse(orc_replay *r, int sb) {
+  const oslot *S = &r->slots[r->fi.display % NSLOT];
+  const int hbd = r->hbd;
+  const sbgeo g = sb_geo_of(r, sb);
+  int bx = g.tsx * 16, by = g.tsy * 16;
+  adjust_bo(g.mi_w, g.mi_h, &bx, &by, 64, 64);
+  int fbx = bx + g.t0x * 16, fby = by + g.t0y * 16;
   int m[4];
   mv_range(r, fbx, fby, 64, 64, m);
   const double me_lambda = r->lv[r->fi.level].me_lambda;
   uint32_t lambda4 = (uint32_t)(me_lambda * 256.0 / 16.0 * 0.125);
-  uint32_t lambda2 = (uint32_t)(me_lambda * 256.0 / 4.0 * 0.125);
-  uint32_t lambda1 = (uint32_t)(me_lambda * 256.0 * 0.5);
   int scale = r->fi.me_range_scale;
   int rx = 192 * scale, ry = 64 * scale;
   int x_lo = fbx + ((m[0] / 8 > -rx ? m[0] / 8 : -rx) >> 2);
@@ -633,39 +673,114 @@ static void run_me(orc_replay *r, int sb) {
   int y_lo = fby + ((m[2] / 8 > -ry ? m[2] / 8 : -ry) >> 2);
   int y_hi = fby + ((m[3] / 8 < ry ? m[3] / 8 : ry) >> 2);
   orc_mv zero = {0, 0};
-  const oslot *ref[2];
-  for (int k = 0; k < R; k++) ref[k] = &r->slots[r->fi.ref_display[k] % NSLOT];
-  for (int k = 0; k < R; k++) {
+  for (int k = 0; k < r->R; k++) {
+    const oslot *ref = &r->slots[r->fi.ref_display[k] % NSLOT];
     orc_mv best = {0, 0};
-    cost = UINT64_MAX;
-    orc_full_search(org_of(&S->qres, hbd), S->qres.stride, org_of(&ref[k]->qres, hbd),
-                    ref[k]->qres.stride, hbd, fbx, fby, x_lo, x_hi, y_lo, y_hi, 16, 16, 1, lambda4,
+    uint64_t cost = UINT64_MAX;
+    orc_full_search(org_of(&S->qres, hbd), S->qres.stride, org_of(&ref->qres, hbd),
+                    ref->qres.stride, hbd, fbx, fby, x_lo, x_hi, y_lo, y_hi, 16, 16, 1, lambda4,
                     zero, zero, 0, &best, &cost);
     r->coarse[k * r->nsb + sb] = best;
     r->cc[k * r->nsb + sb] = cost;
   }
-  orc_mv preds[8];
-  preds[0] = zero;
-  for (int k = 0; k < R; k++) {
-    orc_mv c4 = {(int16_t)(r->coarse[k * r->nsb + sb].row * 4),
-                 (int16_t)(r->coarse[k * r->nsb + sb].col * 4)};
-    orc_mv q = qfull(c4);
-    preds[1 + k].row = (int16_t)(q.row >> 1);
-    preds[1 + k].col = (int16_t)(q.col >> 1);
+}
+
+/* Pass A2: F2 build_half_res_pmvs (src/encoder.rs:2864-3019): the four
+ * 32x32 quadrants at half resolution (me_ss2, src/me.rs:465-519) from
+ * [zero, the coarse MVs of the superblock, its horizontal and vertical
+ * neighbour in the tile], each halved. */
+static void run_half(orc_replay *r, int sb) {
+  const oslot *S = &r->slots[r->fi.display % NSLOT];
+  const sbgeo g = sb_geo_of(r, sb);
+  const double me_lambda = r->lv[r->fi.level].me_lambda;
+  uint32_t lambda2 = (uint32_t)(me_lambda * 256.0 / 4.0 * 0.125);
+  const int hw = g.tsx > 0, he = g.tsx < g.tsw - 1, hn = g.tsy > 0, hs = g.tsy < g.tsh - 1;
+  for (int k = 0; k < r->R; k++) {
+    const oslot *ref = &r->slots[r->fi.ref_display[k] % NSLOT];
+    for (int q = 0; q < 4; q++) {
+      orc_mv p[4];
+      int n = 0;
+      p[n++] = (orc_mv){0, 0};
+      p[n++] = coarse_fp(r, k, sb);
+      if ((q & 1) ? he : hw) p[n++] = coarse_fp(r, k, (q & 1) ? sb + 1 : sb - 1);
+      if ((q >> 1) ? hs : hn) p[n++] = coarse_fp(r, k, (q >> 1) ? sb + r->tw : sb - r->tw);
+      for (int i = 0; i < n; i++) {
+        p[i].row = (int16_t)(p[i].row >> 1);
+        p[i].col = (int16_t)(p[i].col >> 1);
+      }
+      orc_ds_ctx c;
+      ds_at(r, &c, &g, &S->hres, &ref->hres, g.tsx * 16 + (q & 1) * 8, g.tsy * 16 + (q >> 1) * 8,
+            32, 1, 1, lambda2);
+      orc_mv mv;
+      uint64_t cost;
+      orc_diamond_search(&c, p, n, &mv, &cost);
+      r->half[((size_t)k * r->nsb + sb) * 4 + q] = mv;
+      r->hc[((size_t)k * r->nsb + sb) * 4 + q] = cost;
+    }
   }
-  int m2[4] = {m[0] >> 1, m[1] >> 1, m[2] >> 1, m[3] >> 1};
-  int fbx0 = (sx + r->tx0) * 16, fby0 = (sy + r->ty0) * 16;
-  int mf[4];
-  mv_range(r, fbx0, fby0, 64, 64, mf);
+}
+
+/* Pass A3: the lookahead's build_full_res_pmvs (src/encoder.rs:3021-3166,
+ * 16x16 full-pel vs the references' original frames), F3 motion_estimation
+ * of the 64x64 (src/me.rs:193-278: zero + the coarse MV, then sub-pel) and,
+ * at speed 6, of every 32x32, 16x16 and 8x8 block of the superblock. */
+static void run_me(orc_replay *r, int sb) {
+  const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
+  const int R = r->R;
+  const int sx = sb % r->tw, sy = sb / r->tw;
+  uint64_t cost;
+  const sbgeo g = sb_geo_of(r, sb);
+  const double me_lambda = r->lv[r->fi.level].me_lambda;
+  uint32_t lambda1 = (uint32_t)(me_lambda * 256.0 * 0.5);
+  orc_mv zero = {0, 0};
+  const oslot *ref[2];
+  for (int k = 0; k < R; k++) ref[k] = &r->slots[r->fi.ref_display[k] % NSLOT];
+  const int hw = g.tsx > 0, he = g.tsx < g.tsw - 1, hn = g.tsy > 0, hs = g.tsy < g.tsh - 1;
+  for (int k = 0; k < R; k++) {
+    const oplane *orig = &r->inputs[r->fi.ref_display[k] % r->n_inputs].y;
+    /* pmvs_X[e] of superblock sb + (dx, dy): e = 0 coarse, 1..4 quadrants */
+#define PM(dx, dy, e, out)                                                         \
+  do {                                                                             \
+    const int ok_ = (dx) < 0 ? hw : (dx) > 0 ? he : (dy) < 0 ? hn : (dy) > 0 ? hs : 1; \
+    if (ok_) {                                                                     \
+      const int s2_ = sb + (dx) + (dy) * r->tw;                                    \
+      cand[nc++] = (e) == 0 ? coarse_fp(r, k, s2_) : half_fp(r, k, s2_, (e) - 1);  \
+    }                                                                              \
+  } while (0)
+    for (int y = 0; y < 4; y++)
+      for (int x = 0; x < 4; x++) {
+        orc_mv cand[8];
+        int nc = 0;
+        cand[nc++] = zero;
+        const int L = x <= 1, T = y <= 1;
+        PM(0, 0, 0, _);
+        PM(0, 0, T ? (L ? 1 : 2) : (L ? 3 : 4), _);
+        switch (y) {
+          case 0: PM(0, -1, 0, _); PM(0, -1, L ? 3 : 4, _); break;
+          case 1: PM(0, -1, L ? 3 : 4, _); PM(0, 0, L ? 3 : 4, _); break;
+          case 2: PM(0, 1, L ? 1 : 2, _); PM(0, 0, L ? 1 : 2, _); break;
+          default: PM(0, 1, 0, _); PM(0, 1, L ? 1 : 2, _); break;
+        }
+        switch (x) {
+          case 0: PM(-1, 0, 0, _); PM(-1, 0, T ? 2 : 4, _); break;
+          case 1: PM(-1, 0, T ? 2 : 4, _); PM(0, 0, T ? 2 : 4, _); break;
+          case 2: PM(1, 0, T ? 1 : 3, _); PM(0, 0, T ? 1 : 3, _); break;
+          default: PM(1, 0, 0, _); PM(1, 0, T ? 2 : 4, _); break;
+        }
+        orc_ds_ctx c;
+        ds_at(r, &c, &g, &cur->y, orig, g.tsx * 16 + x * 4, g.tsy * 16 + y * 4, 16, 1, 0, lambda1);
+        orc_mv mv;
+        orc_diamond_search(&c, cand, nc, &mv, &cost);
+        r->look[((size_t)k * r->nsb + sb) * 16 + y * 4 + x] = mv;
+        r->lc[((size_t)k * r->nsb + sb) * 16 + y * 4 + x] = cost;
+      }
+#undef PM
+  }
   for (int k = 0; k < R; k++) {
     orc_ds_ctx c;
-    orc_mv hmv, fmv, smv;
-    ds_ctx(r, &c, &S->hres, &ref[k]->hres, fbx * 2, fby * 2, 32, 32, m2, lambda2, 0);
-    orc_diamond_search(&c, preds, 1 + R, &hmv, &cost);
-    r->half[k * r->nsb + sb] = hmv;
-    r->hc[k * r->nsb + sb] = cost;
-    orc_mv fp[2] = {zero, qfull((orc_mv){(int16_t)(hmv.row * 2), (int16_t)(hmv.col * 2)})};
-    ds_ctx(r, &c, &cur->y, &ref[k]->y, fbx0 * 4, fby0 * 4, 64, 64, mf, lambda1, 0);
+    orc_mv fmv, smv;
+    orc_mv fp[2] = {zero, coarse_fp(r, k, sb)};
+    ds_at(r, &c, &g, &cur->y, &ref[k]->y, g.tsx * 16, g.tsy * 16, 64, 0, 0, lambda1);
     orc_diamond_search(&c, fp, 2, &fmv, &cost);
     r->full[k * r->nsb + sb] = fmv;
     r->fc[k * r->nsb + sb] = cost;
@@ -678,7 +793,8 @@ static void run_me(orc_replay *r, int sb) {
   if (!r->s6) return;
   /* speed 6: motion_estimation of every 32x32, then 16x16 and 8x8 block of
    * the superblock at its own position (src/me.rs:193-278), seeded with the
-   * enclosing 64x64's (32x32) or 32x32's (16x16, 8x8) sub-pel winner */
+   * pmvs entry: a 32x32 its half-res quadrant search, a 16x16 / 8x8 its
+   * 32x32's sub-pel winner */
   for (int l = 1; l < 4; l++) {
     struct olevel *P = &r->pl[l];
     const int k2 = 1 << l, B = P->B;
@@ -690,9 +806,10 @@ static void run_me(orc_replay *r, int sb) {
         int mb[4];
         mv_range(r, X >> 2, Y >> 2, B, B, mb);
         for (int k = 0; k < R; k++) {
-          orc_mv par = l == 1 ? r->sub[k * r->nsb + sb]
-                              : U->sub[(size_t)k * U->n + (by >> (l - 1)) * U->gw + (bx >> (l - 1))];
-          orc_mv fp[2] = {zero, qfull(par)}, fmv, smv;
+          orc_mv par = l == 1 ? half_fp(r, k, sb, j * 2 + i)
+                              : qfull(U->sub[(size_t)k * U->n + (by >> (l - 1)) * U->gw +
+                                             (bx >> (l - 1))]);
+          orc_mv fp[2] = {zero, par}, fmv, smv;
           orc_ds_ctx c;
           ds_ctx(r, &c, &cur->y, &ref[k]->y, X, Y, B, B, mb, lambda1, 0);
           orc_diamond_search(&c, fp, 2, &fmv, &cost);
@@ -896,17 +1013,24 @@ static void run_rdo(orc_replay *r, int sb, uint64_t tail[3]) {
   const int sx = sb % r->tw, sy = sb / r->tw;
   const oslot *ref[2];
   for (int k = 0; k < R; k++) ref[k] = &r->slots[r->fi.ref_display[k] % NSLOT];
-  uint64_t *w = r->words + (size_t)sb * (8 * R + 4);
+  uint64_t *w = r->words + (size_t)sb * (WPR * R + 4);
   for (int k = 0; k < R; k++) {
     size_t o = (size_t)k * r->nsb + sb;
-    w[8 * k + 0] = pack_mv(r->coarse[o]);
-    w[8 * k + 1] = r->cc[o];
-    w[8 * k + 2] = pack_mv(r->half[o]);
-    w[8 * k + 3] = r->hc[o];
-    w[8 * k + 4] = pack_mv(r->full[o]);
-    w[8 * k + 5] = r->fc[o];
-    w[8 * k + 6] = pack_mv(r->sub[o]);
-    w[8 * k + 7] = r->sc[o];
+    uint64_t *wk = w + WPR * k;
+    wk[0] = pack_mv(r->coarse[o]);
+    wk[1] = r->cc[o];
+    for (int q = 0; q < 4; q++) {
+      wk[2 + 2 * q] = pack_mv(r->half[o * 4 + q]);
+      wk[3 + 2 * q] = r->hc[o * 4 + q];
+    }
+    wk[10] = pack_mv(r->full[o]);
+    wk[11] = r->fc[o];
+    wk[12] = pack_mv(r->sub[o]);
+    wk[13] = r->sc[o];
+    for (int q = 0; q < 16; q++) {
+      wk[14 + 2 * q] = pack_mv(r->look[o * 16 + q]);
+      wk[15 + 2 * q] = r->lc[o * 16 + q];
+    }
   }
   const int ppx = (sx + r->tx0) * SB, ppy = (sy + r->ty0) * SB;
   const int cwid = r->cw, chei = r->ch, cpx = ppx >> r->xdec, cpy = ppy >> r->ydec;
@@ -978,10 +1102,10 @@ static void run_rdo(orc_replay *r, int sb, uint64_t tail[3]) {
   if (best_skip) memset(blev, 0, (size_t)(1024 + 2 * ntx_c * 1024) * 4);
   uint64_t cb;
   memcpy(&cb, &best, 8);
-  w[8 * R + 0] = (uint64_t)best_c;
-  w[8 * R + 1] = (uint64_t)best_skip;
-  w[8 * R + 2] = cb;
-  w[8 * R + 3] = best_d;
+  w[WPR * R + 0] = (uint64_t)best_c;
+  w[WPR * R + 1] = (uint64_t)best_skip;
+  w[WPR * R + 2] = cb;
+  w[WPR * R + 3] = best_d;
   if (!r->s6) {
     /* F6: the winner into the frame (whole superblock; past the frame edge
      * it lands in the padding, which F7 rewrites) */
@@ -1010,17 +1134,18 @@ static void run_rdo(orc_replay *r, int sb, uint64_t tail[3]) {
     }
     partition_sb(r, sb, best, S, ry, ru, rv);
   }
-  /* F5: the 8x8 blocks of this superblock inside the group's visible area */
-  const orc_mv mv0 = r->sub[sb];
-  const oslot *r0 = ref[0];
+  /* F5: the 8x8 blocks of this superblock inside the group's visible area,
+   * against reference 0's original frame at the lookahead MV of their 16x16 */
+  const oplane *o0 = &r->inputs[r->fi.ref_display[0] % r->n_inputs].y;
   for (int j = 0; j < 8; j++)
     for (int i = 0; i < 8; i++) {
       int bxx = sx * 8 + i, byy = sy * 8 + j;
       if (bxx >= r->vis_w / 8 || byy >= r->vis_h / 8) continue;
       int x = r->tx0 * SB + bxx * 8, y = r->ty0 * SB + byy * 8;
+      const orc_mv mv0 = r->look[(size_t)sb * 16 + (j / 2) * 4 + i / 2];
       tail[2] += orc_get_satd(at(&cur->y, hbd, x, y), cur->y.stride,
-                              at(&r0->y, hbd, x + ((int)mv0.col >> 3), y + ((int)mv0.row >> 3)),
-                              r0->y.stride, 8, 8, hbd, 0);
+                              at(o0, hbd, x + ((int)mv0.col >> 3), y + ((int)mv0.row >> 3)),
+                              o0->stride, 8, 8, hbd, 0);
       uint32_t ic;
       orc_lookahead_intra_costs(at(&cur->y, hbd, x, y), cur->y.stride, 8, 8, hbd, r->bd, &ic);
       tail[2] += ic;
@@ -1037,6 +1162,10 @@ static void *worker(void *arg) {
     pthread_mutex_unlock(&r->mu);
     if (sb >= lim) break;
     if (r->pass == 0)
+      run_coarse(r, sb);
+    else if (r->pass == 1)
+      run_half(r, sb);
+    else if (r->pass == 2)
       run_me(r, sb);
     else
       run_rdo(r, sb, tail);
@@ -1102,8 +1231,7 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
   downsample(r, &S->qres, &S->hres);
   memset(r->tail, 0, sizeof(r->tail));
   r->sb_limit = sb_limit;
-  run_pass(r, 0);
-  run_pass(r, 1);
+  for (int pass = 0; pass < 4; pass++) run_pass(r, pass);
   r->tail[3] = (uint64_t)(r->vis_w / 8) * (r->vis_h / 8);
   if (pad_recon) {
     pad(r, &S->y);

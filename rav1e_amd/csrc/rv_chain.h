@@ -2,12 +2,12 @@
 // search stages.
 //
 // motion_estimation feeds every stage's winner into the next stage's
-// predictor list (estimate_motion_ss4 -> me_ss2 -> full-pel diamond ->
-// sub-pel diamond -> the RDO candidates, src/me.rs:193-519, 1023-1075;
-// src/rdo.rs:949-1006).  Instead of a job-building launch between stages,
-// the workgroup that finishes a search writes its result straight into the
-// next stage's job records (whose static fields -- positions, MV ranges,
-// lambdas -- are built once when the replay is created).  One writer per
+// predictor list (full-pel diamond -> sub-pel diamond -> the RDO
+// candidates, src/me.rs:193-278; src/rdo.rs:949-1006).  The workgroup that
+// finishes a full-pel search writes its result straight into the sub-pel
+// job record (whose static fields -- positions, MV ranges, lambdas -- are
+// built once when the replay is created); the RDO kernels derive their
+// candidates from the sub-pel results in-kernel.  One writer per
 // destination field, and the consumer runs in a later launch on the same
 // stream, so no synchronisation beyond stream order is needed.
 #pragma once
@@ -40,9 +40,7 @@ __host__ __device__ inline rv_mc_job mc_job_for(const rv_plane &p, int po_x, int
 
 enum ChainMode {
   kChainNone = 0,
-  kChainCoarseToHalf = 1,  // F1 -> F2: pred[1 + r] of every reference's job
-  kChainHalfToFull = 2,    // F2 -> F3 full-pel: pred[1]
-  kChainFullToSub = 3,     // F3 full-pel -> F3 sub-pel: pred[0]
+  kChainFullToSub = 3,  // full-pel -> sub-pel diamond of the same job: pred[0]
 };
 
 struct ChainNext {
@@ -50,27 +48,14 @@ struct ChainNext {
   rv_ds_job *jobs;
 };
 
-// Called by one thread of the workgroup that finished job `job` (= r *
-// n_per_ref + sb, reference-major) with its best MV.
+// Called by one thread of the workgroup that finished job `job` with its
+// best MV.  (The coarse and half-res results feed several later jobs each;
+// fill_preds_kernel in rv_replay.hip gathers those.)
 __device__ inline void chain_emit(const ChainNext &c, int job, int n_per_ref, int n_refs,
                                   rv_mv best) {
-  const int r = job / n_per_ref, sb = job - r * n_per_ref;
-  switch (c.mode) {
-    case kChainCoarseToHalf: {  // me_ss2 predictors (src/me.rs:470-519)
-      const rv_mv q = qfull(rv_mv{(int16_t)(best.row * 4), (int16_t)(best.col * 4)});
-      const rv_mv p{(int16_t)(q.row >> 1), (int16_t)(q.col >> 1)};
-      for (int k = 0; k < n_refs; k++) c.jobs[k * n_per_ref + sb].pred[1 + r] = p;
-      break;
-    }
-    case kChainHalfToFull:
-      c.jobs[job].pred[1] = qfull(rv_mv{(int16_t)(best.row * 2), (int16_t)(best.col * 2)});
-      break;
-    case kChainFullToSub:
-      c.jobs[job].pred[0] = best;
-      break;
-    default:
-      break;
-  }
+  (void)n_per_ref;
+  (void)n_refs;
+  if (c.mode == kChainFullToSub) c.jobs[job].pred[0] = best;
 }
 
 // ---- RDO inter candidates (rdo_mode_decision, src/rdo.rs:825-1006) ---------

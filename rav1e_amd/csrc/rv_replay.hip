@@ -65,6 +65,9 @@ namespace rv {
 
 constexpr int kSb = 64;
 constexpr int kSlots = 12;  // DPB slots, keyed by display index % 12
+// result words per superblock and reference: coarse (mv, cost), the four
+// half-res quadrants, full-pel, sub-pel, the 16 lookahead 16x16 blocks
+constexpr int kWordsPerRef = 2 + 8 + 2 + 2 + 32;
 constexpr int kMaxGroups = 8;
 
 struct Geo {
@@ -192,8 +195,8 @@ __global__ __launch_bounds__(64) void score_candidates(
     const uint64_t *lout,
     const uint64_t *uout, const uint64_t *vout, int ntx_c, RdoWinner *win,
     const rv_fs_result *coarse, const rv_fs_result *half, const rv_fs_result *full,
-    uint64_t *words, int32_t *cand_count, unsigned long long *imp_sum, uint32_t *evals,
-    int32_t *leaf_count) {
+    const rv_fs_result *look, uint64_t *words, int32_t *cand_count,
+    unsigned long long *imp_sum, uint32_t *evals, int32_t *leaf_count) {
   const int sb = blockIdx.x * 64 + threadIdx.x;
   if (sb == 0) {  // F4's list is consumed: ready for the next frame; F5 sums next
     evals[0] = (uint32_t)*cand_count;  // single-reference candidates evaluated
@@ -206,19 +209,45 @@ __global__ __launch_bounds__(64) void score_candidates(
   if (sb >= g.nsb) return;
   const RdoWinner w = block_argmin(cg, lambda, ds_u, ds_v, sub, lout, uout, vout, ntx_c, sb);
   win[sb] = w;
-  uint64_t *wd = words + (int64_t)sb * (8 * g.R + 4);
-  for (int i = 0; i < 8 * g.R; i++) {
-    const int r = i >> 3, f = i & 7;
-    const rv_fs_result *src = (f >> 1) == 0 ? coarse : (f >> 1) == 1 ? half : (f >> 1) == 2 ? full : sub;
-    const rv_fs_result v = src[r * g.nsb + sb];
-    wd[i] = (f & 1) ? v.cost : pack_mv(v.best_mv);
+  uint64_t *wd = words + (int64_t)sb * (kWordsPerRef * g.R + 4);
+  auto put = [&](int i, const rv_fs_result &v) {
+    wd[2 * i] = pack_mv(v.best_mv);
+    wd[2 * i + 1] = v.cost;
+  };
+  for (int r = 0; r < g.R; r++, wd += kWordsPerRef) {
+    const int64_t o = (int64_t)r * g.nsb + sb;
+    put(0, coarse[o]);
+    for (int q = 0; q < 4; q++) put(1 + q, half[o * 4 + q]);
+    put(5, full[o]);
+    put(6, sub[o]);
+    for (int q = 0; q < 16; q++) put(7 + q, look[o * 16 + q]);
   }
   uint64_t cb;
   __builtin_memcpy(&cb, &w.cost, 8);
-  wd[8 * g.R + 0] = (uint64_t)w.c;
-  wd[8 * g.R + 1] = (uint64_t)w.skip;
-  wd[8 * g.R + 2] = cb;
-  wd[8 * g.R + 3] = w.dist;
+  wd[0] = (uint64_t)w.c;
+  wd[1] = (uint64_t)w.skip;
+  wd[2] = cb;
+  wd[3] = w.dist;
+}
+
+// The searches' predictor lists (get_subset_predictors, src/me.rs:82-96:
+// zero, then the coarse MVs quantize_to_fullpel'd): slot p >= 1 of job i
+// takes source src[8 i + p] (-1: none) = 2 * index + kind, kind 0 a coarse
+// result (estimate_motion_ss4's MV * 4), 1 a half-res result
+// (estimate_motion_ss2's MV * 2); `shr`: me_ss2 halves every predictor.
+__global__ void fill_preds_kernel(rv_ds_job *jobs, const int32_t *src, int n,
+                                  const rv_fs_result *coarse, const rv_fs_result *half, int shr) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  for (int p = 1; p < RV_DS_MAX_PRED; p++) {
+    const int v = src[8 * i + p];
+    if (v < 0) break;
+    const rv_mv m = (v & 1) ? half[v >> 1].best_mv : coarse[v >> 1].best_mv;
+    const int sc = (v & 1) ? 2 : 4;
+    rv_mv q = qfull(rv_mv{(int16_t)(m.row * sc), (int16_t)(m.col * sc)});
+    if (shr) q = rv_mv{(int16_t)(q.row >> 1), (int16_t)(q.col >> 1)};
+    jobs[i].pred[p] = q;
+  }
 }
 
 // The valid candidates (cand_mv true) of every superblock, compacted for
@@ -245,20 +274,22 @@ __global__ __launch_bounds__(256) void cand_list_kernel(CandGeo cg, const rv_fs_
 }
 
 // F5: get_satd of every 8x8 luma block of the group inside the frame
-// against reference 0 at the full-pel part of its superblock's NEWMV
-// (compute_block_importances, src/api/internal.rs:823-1010) plus its
+// against reference 0's original frame at the full-pel part of its
+// lookahead MV (the 16x16 block's, fi.lookahead_mvs[y * 2][x * 2];
+// compute_block_importances, src/api/internal.rs:823-1010) plus its
 // lookahead intra cost (get_satd against pred_dc_128,
 // src/api/internal.rs:680-765), summed.  One lane per block; the source
 // block is read once for both.
 template <typename Px>
 __global__ __launch_bounds__(256) void importance_kernel(Geo g, rv_plane org, rv_plane ref,
-                                                          const rv_fs_result *sub, int nbx,
+                                                          const rv_fs_result *look, int nbx,
                                                           int nby, unsigned long long *sum) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t v = 0;
   if (i < nbx * nby) {
     const int bx = i % nbx, by = i / nbx;
-    const rv_mv mv = sub[(by / 8) * g.tw + (bx / 8)].best_mv;  // reference 0
+    const int sb = (by / 8) * g.tw + (bx / 8), q = ((by % 8) / 2) * 4 + (bx % 8) / 2;
+    const rv_mv mv = look[sb * 16 + q].best_mv;  // reference 0
     const int x = g.tx0 * kSb + bx * 8, y = g.ty0 * kSb + by * 8;
     const Px *o = plane_ptr<Px>(org, x, y);
     const Px *r = plane_ptr<Px>(ref, x + ((int)mv.col >> 3), y + ((int)mv.row >> 3));
@@ -321,16 +352,22 @@ __global__ __launch_bounds__(256) void xcopy_kernel(XArgs a) {
 // ---- speed 6 (config D): the partition levels below 64x64 -----------------
 constexpr int kLevels = 4;  // 64x64, 32x32, 16x16, 8x8
 
-// The full-pel jobs of a level take the sub-pel winner of the enclosing
-// block of level `parent` as their coarse predictor, quantize_to_fullpel
-// (get_subset_predictors, src/me.rs:82-96): rdo_mode_decision keeps b_me in
-// pmvs for 64x64 and 32x32 blocks only (src/rdo.rs:866-876), so 32x32
-// blocks start from their 64x64 and 16x16 / 8x8 blocks from their 32x32.
+// The full-pel jobs of a level take their pmvs entry as the coarse
+// predictor, quantize_to_fullpel'd (get_subset_predictors, src/me.rs:82-96):
+// a 32x32 block the half-res search of its quadrant (build_half_res_pmvs),
+// a 16x16 / 8x8 block the sub-pel winner of its 32x32 (rdo_mode_decision
+// stores b_me into pmvs for 32x32 and 64x64 blocks, src/rdo.rs:866-876).
 __global__ void seed_level_kernel(rv_ds_job *jobs, int n, int gw, int R,
                                   const rv_fs_result *parent, int pn, int pgw, int f) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n * R) return;
   const int k = i / n, b = i - k * n, bx = b % gw, by = b / gw;
+  if (pgw == 0) {  // 32x32: the half-res search of its quadrant (pmvs[1..4], MV * 2)
+    const int sb = (by >> 1) * (gw >> 1) + (bx >> 1), q = (by & 1) * 2 + (bx & 1);
+    const rv_mv m = parent[((int64_t)k * pn + sb) * 4 + q].best_mv;
+    jobs[i].pred[1] = qfull(rv_mv{(int16_t)(m.row * 2), (int16_t)(m.col * 2)});
+    return;
+  }
   jobs[i].pred[1] = qfull(parent[k * pn + (by / f) * pgw + bx / f].best_mv);
 }
 
@@ -522,8 +559,10 @@ struct rv_replay {
   std::vector<RvInput> inputs;
   std::vector<void *> allocs;
   rv_fs_job *fs_jobs[3] = {nullptr, nullptr, nullptr};  // per level (scale 4, 2, 1)
-  rv_fs_result *coarse, *half, *full, *sub;
-  rv_ds_job *jobs_half[3], *jobs_full[3], *jobs_sub[3];  // per level
+  rv_fs_result *coarse, *half, *full, *sub;  // half: 4 quadrants per superblock
+  rv_fs_result *look;                         // lookahead: 16 16x16 blocks per superblock
+  rv_ds_job *jobs_half[3], *jobs_full[3], *jobs_sub[3], *jobs_look[3];  // per level
+  int32_t *src_half = nullptr, *src_full = nullptr, *src_look = nullptr;  // predictor sources
   uint64_t *l_out, *c_out;  // F4: [skip dist, non-skip dist, rate] per transform block
   RdoWinner *win;
   int32_t *cand_list, *cand_count;  // F4: the valid candidates
@@ -546,7 +585,7 @@ struct rv_replay {
   // frame.  Every `timing_stride`-th block of frames is instrumented (each
   // record costs ~4.4 us of idle GPU between kernels on MI355X).
   static constexpr int kRing = 64;
-  static constexpr int kEv = 12;
+  static constexpr int kEv = 13;
   hipEvent_t evs[kRing][kEv];
   int timing_stride = 1, timing_block = 1;
   long timed = 0;
@@ -657,53 +696,111 @@ int build_static_jobs(rv_replay *r) {
     }
     int e;
     if ((e = upload(jobs, r->fs_jobs[lv]))) return e;
-    // F2 / F3 diamond jobs: static fields (positions, MV ranges, lambdas);
-    // the predictors are chained in by the previous stage each frame
+    // F2 / F3 / lookahead diamond jobs: static fields (positions, MV ranges,
+    // lambdas, predictor counts); fill_preds_kernel writes the predictors
+    // from the coarse / half-res results every frame
     const uint32_t lambda2 = (uint32_t)(me_lambda * 256.0 / 4.0 * 0.125);
     const uint32_t lambda1 = (uint32_t)(me_lambda * 256.0 * 0.5);
-    std::vector<rv_ds_job> jh(g.nsb * g.R), jf(g.nsb * g.R), js(g.nsb * g.R);
+    const int nsb = g.nsb;
+    std::vector<rv_ds_job> jh((size_t)nsb * g.R * 4), jf(nsb * g.R), js(nsb * g.R),
+        jl((size_t)nsb * g.R * 16);
+    std::vector<int32_t> sh(jh.size() * 8, -1), sf(jf.size() * 8, -1), sl(jl.size() * 8, -1);
     for (int k = 0; k < g.R; k++)
-      for (int sb = 0; sb < g.nsb; sb++) {
-        const int i = k * g.nsb + sb;
+      for (int sb = 0; sb < nsb; sb++) {
+        const int i = k * nsb + sb;
         const int sx = sb % g.tw, sy = sb / g.tw;
         int t0x, t0y, mi_w, mi_h;
         sb_tile(g, sx, sy, t0x, t0y, mi_w, mi_h);
-        // me_ss2 (src/me.rs:470-519): adjusted 64x64 origin at 1/2 res
-        int bx = (g.tx0 + sx - t0x) * 16, by = (g.ty0 + sy - t0y) * 16;
-        adjust_bo(mi_w, mi_h, bx, by, 64, 64);
-        int fbx = bx + t0x * 16, fby = by + t0y * 16;
-        int mr[4];
-        mv_range(g, fbx, fby, 64, 64, mr);
-        rv_ds_job j;
-        memset(&j, 0, sizeof(j));
-        j.po_x = fbx * 2;  // (bo << BLOCK_TO_PLANE_SHIFT) >> 1
-        j.po_y = fby * 2;
-        j.mvx_min = mr[0] >> 1;
-        j.mvx_max = mr[1] >> 1;
-        j.mvy_min = mr[2] >> 1;
-        j.mvy_max = mr[3] >> 1;
-        j.lambda = lambda2;
-        j.n_pred = 1 + g.R;  // zero + the coarse MV of every reference
-        jh[i] = j;
-        // full resolution (motion_estimation, src/me.rs:193-285)
-        fbx = (g.tx0 + sx) * 16;
-        fby = (g.ty0 + sy) * 16;
-        mv_range(g, fbx, fby, 64, 64, mr);
-        memset(&j, 0, sizeof(j));
-        j.po_x = fbx * 4;
-        j.po_y = fby * 4;
-        j.mvx_min = mr[0];
-        j.mvx_max = mr[1];
-        j.mvy_min = mr[2];
-        j.mvy_max = mr[3];
-        j.lambda = lambda1;
-        j.n_pred = 2;  // zero + the half-res winner
-        jf[i] = j;
-        j.n_pred = 1;  // the full-pel winner
-        js[i] = j;
+        // the superblock in its tile, and the tile's size in superblocks
+        const int tsx = g.tx0 + sx - t0x, tsy = g.ty0 + sy - t0y;
+        const int tsw = (mi_w + 15) / 16, tsh = (mi_h + 15) / 16;
+        const bool hw = tsx > 0, he = tsx < tsw - 1, hn = tsy > 0, hs = tsy < tsh - 1;
+        auto coarse_src = [&](int sb2) { return 2 * (k * nsb + sb2); };
+        auto half_src = [&](int sb2, int q) { return 2 * ((k * nsb + sb2) * 4 + q) + 1; };
+        // diamond job at tile-relative 4x4 offset (bx, by), size bw, adjust_bo'd
+        auto make = [&](int bx, int by, int bw, bool adj, int shift, uint32_t lambda) {
+          if (adj) adjust_bo(mi_w, mi_h, bx, by, bw, bw);
+          const int fbx = bx + t0x * 16, fby = by + t0y * 16;
+          int mr[4];
+          mv_range(g, fbx, fby, bw, bw, mr);
+          rv_ds_job j;
+          memset(&j, 0, sizeof(j));
+          j.po_x = (fbx * 4) >> shift;
+          j.po_y = (fby * 4) >> shift;
+          j.mvx_min = mr[0] >> shift;
+          j.mvx_max = mr[1] >> shift;
+          j.mvy_min = mr[2] >> shift;
+          j.mvy_max = mr[3] >> shift;
+          j.lambda = lambda;
+          return j;
+        };
+        // F2: build_half_res_pmvs (src/encoder.rs:2864-3019): the four 32x32
+        // quadrants at half resolution (estimate_motion_ss2 / me_ss2,
+        // src/me.rs:280-327, 465-519) from [the superblock's coarse MV, the
+        // horizontal, the vertical neighbour's] (inside the tile)
+        for (int q = 0; q < 4; q++) {
+          rv_ds_job j = make(tsx * 16 + (q & 1) * 8, tsy * 16 + (q >> 1) * 8, 32, true, 1, lambda2);
+          int32_t *ps = &sh[((size_t)i * 4 + q) * 8];
+          int n = 1;
+          ps[n++] = coarse_src(sb);
+          if ((q & 1) ? he : hw) ps[n++] = coarse_src((q & 1) ? sb + 1 : sb - 1);
+          if ((q >> 1) ? hs : hn) ps[n++] = coarse_src((q >> 1) ? sb + g.tw : sb - g.tw);
+          j.n_pred = n;
+          jh[(size_t)i * 4 + q] = j;
+        }
+        // F3: motion_estimation of the 64x64 (src/me.rs:193-278) from zero and
+        // pmvs[0], the coarse MV; sub-pel from the full-pel winner
+        {
+          rv_ds_job j = make(tsx * 16, tsy * 16, 64, false, 0, lambda1);
+          sf[(size_t)i * 8 + 1] = coarse_src(sb);
+          j.n_pred = 2;
+          jf[i] = j;
+          j.n_pred = 1;
+          js[i] = j;
+        }
+        // lookahead: build_full_res_pmvs (src/encoder.rs:3021-3166), the 16
+        // 16x16 blocks from [the coarse MV, the covering quadrant, two
+        // vertical and two horizontal candidates of this and the adjacent
+        // superblocks] (estimate_motion, src/me.rs:337-390, full-pel)
+        for (int y = 0; y < 4; y++)
+          for (int x = 0; x < 4; x++) {
+            rv_ds_job j = make(tsx * 16 + x * 4, tsy * 16 + y * 4, 16, true, 0, lambda1);
+            // pmvs_X[0] = coarse, [1..4] = quadrants of superblock X; -1 absent
+            auto pm = [&](int dx, int dy, int e) -> int {
+              const bool ok = dx < 0 ? hw : dx > 0 ? he : dy < 0 ? hn : dy > 0 ? hs : true;
+              if (!ok) return -1;
+              const int sb2 = sb + dx + dy * g.tw;
+              return e == 0 ? coarse_src(sb2) : half_src(sb2, e - 1);
+            };
+            const int L = x <= 1, T = y <= 1;
+            const int cover = pm(0, 0, T ? (L ? 1 : 2) : (L ? 3 : 4));
+            int v1, v2, h1, h2;
+            switch (y) {
+              case 0: v1 = pm(0, -1, 0); v2 = pm(0, -1, L ? 3 : 4); break;
+              case 1: v1 = pm(0, -1, L ? 3 : 4); v2 = pm(0, 0, L ? 3 : 4); break;
+              case 2: v1 = pm(0, 1, L ? 1 : 2); v2 = pm(0, 0, L ? 1 : 2); break;
+              default: v1 = pm(0, 1, 0); v2 = pm(0, 1, L ? 1 : 2); break;
+            }
+            switch (x) {
+              case 0: h1 = pm(-1, 0, 0); h2 = pm(-1, 0, T ? 2 : 4); break;
+              case 1: h1 = pm(-1, 0, T ? 2 : 4); h2 = pm(0, 0, T ? 2 : 4); break;
+              case 2: h1 = pm(1, 0, T ? 1 : 3); h2 = pm(0, 0, T ? 1 : 3); break;
+              default: h1 = pm(1, 0, 0); h2 = pm(1, 0, T ? 2 : 4); break;
+            }
+            const int cand[6] = {coarse_src(sb), cover, v1, v2, h1, h2};
+            int32_t *ps = &sl[((size_t)i * 16 + y * 4 + x) * 8];
+            int n = 1;
+            for (int c = 0; c < 6; c++)
+              if (cand[c] >= 0) ps[n++] = cand[c];
+            j.n_pred = n;
+            jl[(size_t)i * 16 + y * 4 + x] = j;
+          }
       }
     if ((e = upload(jh, r->jobs_half[lv])) || (e = upload(jf, r->jobs_full[lv])) ||
-        (e = upload(js, r->jobs_sub[lv])))
+        (e = upload(js, r->jobs_sub[lv])) || (e = upload(jl, r->jobs_look[lv])))
+      return e;
+    if (lv == 0 && ((e = upload(sh, r->src_half)) || (e = upload(sf, r->src_full)) ||
+                    (e = upload(sl, r->src_look))))
       return e;
     // speed 6: motion_estimation of every 32x32 / 16x16 / 8x8 block at its
     // own position (no adjust_bo, src/me.rs:193-278): zero + the seeded
@@ -913,7 +1010,8 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   const int nr = g.nsb * g.R;
   const int64_t nc = (int64_t)g.nsb * g.C;
   r->coarse = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
-  r->half = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
+  r->half = (rv_fs_result *)dalloc(r, nr * 4 * sizeof(rv_fs_result));
+  r->look = (rv_fs_result *)dalloc(r, nr * 16 * sizeof(rv_fs_result));
   r->full = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
   r->sub = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
   r->l_out = (uint64_t *)dalloc(r, (size_t)nc * 3 * 8);
@@ -927,7 +1025,7 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   if (r->cand_count) (void)hipMemsetAsync(r->cand_count, 0, 4, r->stream);
   r->l_lev = (int32_t *)dalloc(r, (size_t)g.nsb * 1024 * 4);
   r->c_lev = (int32_t *)dalloc(r, (size_t)g.nsb * r->ntx_c * 1024 * 4 * 2);
-  r->nwords = (size_t)g.nsb * (8 * g.R + 4);
+  r->nwords = (size_t)g.nsb * (kWordsPerRef * g.R + 4);
   if (cfg->flags & RV_REPLAY_SPEED6) {
     if (g.xdec != g.ydec) {
       rv_set_error(RV_EINVAL, "rv_replay_create: speed 6 needs 4:2:0 or 4:4:4");
@@ -988,7 +1086,7 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->imp_by = g.vis_h / 8;
   r->n_imp = r->imp_bx * r->imp_by;
   r->tail = (unsigned long long *)dalloc(r, 5 * 8);
-  ok = ok && r->coarse && r->half && r->full && r->sub && r->l_out && r->c_out && r->win &&
+  ok = ok && r->coarse && r->half && r->look && r->full && r->sub && r->l_out && r->c_out && r->win &&
        r->cand_list && r->cand_count && r->cand_evals &&
        r->l_lev && r->c_lev && r->words && r->tail;
   if (ok) {
@@ -1008,7 +1106,8 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->grects[1] = g.ty0;
   r->grects[2] = g.tw;
   r->grects[3] = g.th;
-  for (int lv = 0; lv < 3; lv++) r->jobs_half[lv] = r->jobs_full[lv] = r->jobs_sub[lv] = nullptr;
+  for (int lv = 0; lv < 3; lv++)
+    r->jobs_half[lv] = r->jobs_full[lv] = r->jobs_sub[lv] = r->jobs_look[lv] = nullptr;
   if (!ok) {
     rv_set_error(RV_EHIP, "rv_replay_create: device allocation failed");
     rv_replay_destroy(r);
@@ -1190,9 +1289,9 @@ int rv_replay_import(rv_replay *r) {
   return pad_slot(r, s);
 }
 
-// Event layout per instrumented frame: e[0] start, e[1..11] after F0, F1,
-// F2, F3 full-pel, F3 sub-pel, F4 single-reference candidates, F4 compound
-// candidates, F4 argmin, F6 commit, F5, F7.
+// Event layout per instrumented frame: e[0] start, e[1..12] after F0, F1,
+// F2, FL (lookahead), F3 full-pel, F3 sub-pel, F4 single-reference
+// candidates, F4 compound candidates, F4 argmin, F6 commit, F5, F7.
 int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   if (!r) return rv_set_error(RV_EINVAL, "rv_replay_frame: null");
   const Geo &g = r->g;
@@ -1239,8 +1338,10 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   const int slot = (int)(ncoded % rv_replay::kRing);
   uint32_t *ev_full = r->ds_evals + (size_t)slot * 2 * nr * g.R;
   uint32_t *ev_sub = ev_full + (size_t)nr * g.R;
-  ChainNext to_half{kChainCoarseToHalf, r->jobs_half[lv]},
-      to_full{kChainHalfToFull, r->jobs_full[lv]}, to_sub{kChainFullToSub, r->jobs_sub[lv]};
+  ChainNext to_sub{kChainFullToSub, r->jobs_sub[lv]};
+  // the lookahead searches the references' original frames
+  rv_plane refs_o[RV_DS_MAX_PRED];
+  for (int k = 0; k < g.R; k++) refs_o[k] = r->inputs[fi.ref_display[k] % r->inputs.size()].y;
 
   const bool tm = r->timing_stride > 0 && (ncoded / r->timing_block) % r->timing_stride == 0;
   hipEvent_t *e = r->evs[r->timed % rv_replay::kRing];
@@ -1255,29 +1356,53 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   RV_R(rv_plane_pyramid(&cur.y, &S.hres, &S.qres, st));
   if (r->sea) RV_R(rv_plane_box_sums(&S.qres, S.qres_box, st));
   RV_EV(1);
-  // F1 coarse full search, every reference in one launch -> F2 predictors
+  // F1 coarse full search (build_coarse_pmvs), every reference in one launch
   RV_R(rv_full_search_multi(&S.qres, refs_q, g.R, r->fs_jobs[lv], nr, 16, 16, 1, 0, r->coarse,
-                            &to_half, r->sea ? box : nullptr, st));
+                            nullptr, r->sea ? box : nullptr, st));
   RV_EV(2);
-  // F2 half-res diamond -> F3 full-pel predictors
-  RV_R(rv_diamond_search_multi(&S.hres, refs_h, g.R, r->jobs_half[lv], nr, 32, 32, 0, 0, 0, g.bd,
-                               r->half, nullptr, &to_full, st));
+  // F2 build_half_res_pmvs: the four 32x32 quadrants of every superblock at
+  // half resolution, predictors from the coarse MVs; the 64x64 full-pel
+  // predictors (pmvs[0]) too
+  {
+    const int nh = nr * g.R * 4, nf = nr * g.R;
+    fill_preds_kernel<<<(nh + 255) / 256, 256, 0, st>>>(r->jobs_half[lv], r->src_half, nh,
+                                                        r->coarse, r->half, 1);
+    fill_preds_kernel<<<(nf + 255) / 256, 256, 0, st>>>(r->jobs_full[lv], r->src_full, nf,
+                                                        r->coarse, r->half, 0);
+  }
+  RV_R(rv_diamond_search_multi(&S.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
+                               g.bd, r->half, nullptr, nullptr, st));
   RV_EV(3);
+  // FL the lookahead's build_full_res_pmvs (compute_lookahead_motion_vectors,
+  // src/api/internal.rs:514-622): 16x16 full-pel searches against the
+  // references' original frames; its coarse and half-res stages are F1 / F2
+  // (the same inputs).  F5 reads its MVs.
+  {
+    const int nl = nr * g.R * 16;
+    fill_preds_kernel<<<(nl + 255) / 256, 256, 0, st>>>(r->jobs_look[lv], r->src_look, nl,
+                                                        r->coarse, r->half, 0);
+  }
+  RV_R(rv_diamond_search_multi(&cur.y, refs_o, g.R, r->jobs_look[lv], nr * 16, 16, 16, 0, 0, 0,
+                               g.bd, r->look, nullptr, nullptr, st));
+  RV_EV(4);
   // F3 full-res full-pel diamond -> sub-pel predictor; sub-pel diamond
   // (speed 10: SAD, no hp) -> NEWMV of every superblock and reference
   RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
                                r->full, ev_full, &to_sub, st));
-  RV_EV(4);
+  RV_EV(5);
   RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, r->s6 ? 1 : 0,
                                0, g.bd, r->sub, ev_sub, nullptr, st));
   // speed 6: the same search for every 32x32, 16x16 and 8x8 block (SATD
   // sub-pel, use_satd_subpel, src/api/config.rs:429-431)
   for (int l = 1; r->s6 && l < kLevels; l++) {
     rv_replay::PLevel &P = r->pl[l];
-    const int up = l == 1 ? 0 : 1;  // the level whose sub-pel winners seed this one
-    const rv_fs_result *parent = up == 0 ? r->sub : r->pl[1].sub;
-    seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, st>>>(
-        P.jobs_full[lv], P.n, P.gw, g.R, parent, r->pl[up].n, r->pl[up].gw, 1 << (l - up));
+    // 32x32: the half-res quadrant searches; 16x16 / 8x8: the 32x32's sub-pel
+    if (l == 1)
+      seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, st>>>(P.jobs_full[lv], P.n, P.gw, g.R,
+                                                                  r->half, g.nsb, 0, 0);
+    else
+      seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, st>>>(
+          P.jobs_full[lv], P.n, P.gw, g.R, r->pl[1].sub, r->pl[1].n, r->pl[1].gw, 1 << (l - 1));
     ChainNext to_s{kChainFullToSub, P.jobs_sub[lv]};
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, P.jobs_full[lv], P.n, P.B, P.B, 0, 0, 0,
                                  g.bd, P.full, nullptr, &to_s, st));
@@ -1294,7 +1419,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     const int ns = P.n * g.R * g.M;
     cand_list_kernel<<<(ns + 255) / 256, 256, 0, st>>>(P.cg, P.sub, ns, P.cand_list, P.cand_count);
   }
-  RV_EV(5);
+  RV_EV(6);
   // F4 every valid candidate, luma + both chroma planes in one fused launch
   RdoArgs la, ca;
   memset(&la, 0, sizeof(la));
@@ -1400,7 +1525,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     lc.cand_base = cc.cand_base = nsingle;
     lc.n_tx = g.nsb * cg.comp;
     cc.n_tx = g.nsb * cg.comp * ntx_c;
-    RV_EV(6);
+    RV_EV(7);
     RV_R(rv_rdo_candidates(lc, cc, g.hbd, st, true));
     for (int l = 1; r->s6 && l < kLevels; l++) {
       const rv_replay::PLevel &P = r->pl[l];
@@ -1413,13 +1538,14 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, st, 1));
     }
   } else {
-    RV_EV(6);
+    RV_EV(7);
   }
-  RV_EV(7);
+  RV_EV(8);
   score_candidates<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, cg, L.lambda, L.ds[1], L.ds[2], r->sub,
                                                      r->l_out,
                                                      r->c_out, r->c_out + nct * 3, ntx_c, r->win,
-                                                     r->coarse, r->half, r->full, r->words,
+                                                     r->coarse, r->half, r->full, r->look,
+                                                     r->words,
                                                      r->cand_count, r->tail + 2,
                                                      r->cand_evals + 2 * slot * kLevels,
                                                      r->leaf_count);
@@ -1444,7 +1570,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     pa.words = r->words + r->wpart;
     partition_kernel<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, pa);
   }
-  RV_EV(8);
+  RV_EV(9);
   // F6 commit the winners into the frame
   la.commit = ca.commit = 1;
   la.list = ca.list = r->s6 ? r->pl[0].leaf : nullptr;  // speed 6: the unsplit superblocks
@@ -1463,18 +1589,18 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, st, 2));
     RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, st, 2));
   }
-  RV_EV(9);
+  RV_EV(10);
   // F5 importance SATD against reference 0 (the sum was zeroed by the argmin)
   {
     const unsigned nb = (unsigned)((r->n_imp + 255) / 256);
     if (g.hbd)
-      importance_kernel<uint16_t><<<nb, 256, 0, st>>>(g, cur.y, ref[0]->y, r->sub, r->imp_bx,
+      importance_kernel<uint16_t><<<nb, 256, 0, st>>>(g, cur.y, refs_o[0], r->look, r->imp_bx,
                                                       r->imp_by, r->tail + 2);
     else
-      importance_kernel<uint8_t><<<nb, 256, 0, st>>>(g, cur.y, ref[0]->y, r->sub, r->imp_bx,
+      importance_kernel<uint8_t><<<nb, 256, 0, st>>>(g, cur.y, refs_o[0], r->look, r->imp_bx,
                                                      r->imp_by, r->tail + 2);
   }
-  RV_EV(10);
+  RV_EV(11);
   // F7 the reconstruction becomes a reference
   r->coded++;
   r->last = fi;
@@ -1495,7 +1621,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
 #endif
     }
   }
-  RV_EV(11);
+  RV_EV(12);
 #undef RV_EV
   if (info) *info = fi;
   RV_H(hipGetLastError());

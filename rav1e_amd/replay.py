@@ -21,6 +21,9 @@ DEFAULT_QUANTIZER = 100  # rav1e's default --quantizer (src/api/config.rs)
 
 RV_REPLAY_EXHAUSTIVE_FS = 4  # F1 without successive elimination (same results)
 RV_REPLAY_SPEED6 = 8  # the speed-6 schedule: partition RDO 64x64 .. 8x8 (config D)
+# HIP-event stages of a frame: F0, F1, F2, FL (lookahead), F3 full-pel, F3
+# sub-pel, F4 single, F4 compound, F4 argmin, F6 commit, F5, F7
+N_STAGES = 12
 
 # GOP of the reference's reorder pyramid (src/api/internal.rs:61-95):
 # group_input_len 4, levels 0,1,2,2 -> me_range_scale = 4 >> level
@@ -180,29 +183,41 @@ def tile_groups(tiling: dict, world: int) -> list:
     return out
 
 
+# result words per superblock and reference (rv_replay_results): coarse
+# (mv, cost), the four half-res quadrants, full-pel, sub-pel, the 16
+# lookahead 16x16 blocks; then per superblock winner, skip, cost, distortion
+WORDS_PER_REF = 2 + 8 + 2 + 2 + 32
+W_COARSE, W_HALF, W_FULL, W_SUB, W_LOOK = 0, 2, 10, 12, 14
+
+
+def sb_words_per(n_refs):
+    return WORDS_PER_REF * n_refs + 4
+
+
 def result_words(width, height, n_refs, tile_w_sb=0, tile_h_sb=0, tile_x0=0, tile_y0=0,
                  speed=10):
-    """Result words of a group (rv_replay_results): per superblock 8 * R + 4;
+    """Result words of a group (rv_replay_results): per superblock
+    WORDS_PER_REF * R + 4;
     speed 6 adds 4 * R + 4 per 32x32, 16x16 and 8x8 block and one partition
     mask per superblock; then 5 tail words."""
     sbc, sbr = (width + 63) // 64, (height + 63) // 64
     tw = tile_w_sb or (sbc - tile_x0)
     th = tile_h_sb or (sbr - tile_y0)
-    n = tw * th * (8 * n_refs + 4)
+    n = tw * th * sb_words_per(n_refs)
     if speed == 6:
         n += sum(tw * th * 4 ** l * (4 * n_refs + 4) for l in (1, 2, 3)) + tw * th
     return n + 5
 
 
 def level_words(width, height, n_refs, words, tile_w_sb=0, tile_h_sb=0, tile_x0=0, tile_y0=0):
-    """Split speed-6 result words: (superblock words [nsb, 8R+4], [level 1..3
+    """Split speed-6 result words: (superblock words [nsb, 46R+4], [level 1..3
     words [n_l, 4R+4]], partition masks [nsb], tail [5])."""
     sbc, sbr = (width + 63) // 64, (height + 63) // 64
     tw = tile_w_sb or (sbc - tile_x0)
     th = tile_h_sb or (sbr - tile_y0)
     nsb = tw * th
-    o = nsb * (8 * n_refs + 4)
-    sbw = words[:o].reshape(nsb, 8 * n_refs + 4)
+    o = nsb * sb_words_per(n_refs)
+    sbw = words[:o].reshape(nsb, sb_words_per(n_refs))
     lv = []
     for l in (1, 2, 3):
         n = nsb * 4 ** l
@@ -307,15 +322,15 @@ class HipReplay:
         _check(lib().rv_replay_set_timing(self.h, stride, block), "rv_replay_set_timing")
 
     def stage_ms(self) -> np.ndarray:
-        out = np.zeros(11, dtype=np.float32)
-        n = lib().rv_replay_stage_times(self.h, out.ctypes.data, 11)
+        out = np.zeros(N_STAGES, dtype=np.float32)
+        n = lib().rv_replay_stage_times(self.h, out.ctypes.data, N_STAGES)
         if n < 0:
             _check(n, "rv_replay_stage_times")
         return out[:n]
 
     def stage_ms_sum(self, last_frames: int) -> np.ndarray:
-        out = np.zeros(11, dtype=np.float32)
-        n = lib().rv_replay_stage_times_sum(self.h, last_frames, out.ctypes.data, 11)
+        out = np.zeros(N_STAGES, dtype=np.float32)
+        n = lib().rv_replay_stage_times_sum(self.h, last_frames, out.ctypes.data, N_STAGES)
         if n < 0:
             _check(n, "rv_replay_stage_times_sum")
         return out[:n]

@@ -11,6 +11,8 @@ import socket
 import numpy as np
 import torch.multiprocessing as mp
 
+from rav1e_amd import replay as RP
+
 W, H, REFS, NIN = 384, 192, 2, 12
 
 
@@ -89,7 +91,7 @@ def test_two_rank_gloo_tile_parallel_stream():
     # max over ranks: both report the slow rank's time (>= 4 sleeps)
     assert abs(res[0][0] - res[1][0]) < 1e-9 and res[0][0] >= 0.2
     single = _single_words(6)
-    per = 8 * REFS + 4
+    per = RP.sb_words_per(REFS)
     sbc = (W + 63) // 64
     sw = single[: len(single) - 5].reshape(-1, per)
     for r in range(2):

@@ -9,7 +9,7 @@ from rav1e_amd import rate as RT
 from rav1e_amd import replay as RP
 from tests import oracle_lib as O
 
-PER_REF = 8
+PER_REF = RP.WORDS_PER_REF
 
 
 def _frames(w, h, xdec, ydec, bd, n):
@@ -86,11 +86,14 @@ def test_cpu_replay_stream_and_thread_invariant():
     assert wd[-2] == (w // 8) * (h // 8)  # importance blocks
     assert wd[-1] > 0 and wd[-3] > 0 and wd[-4] == wd[-1]  # one group: group sum = frame sum
     sb = _sb_words(wd, 8, 2)
-    assert (sb[:, 16] < 8).all() and set(np.unique(sb[:, 17])) <= {0, 1}
-    # the NEWMV of the full-res search tracks the synthetic motion
-    # (1.25 px/frame; display 8 from 4: +5 px, i.e. +40 in 1/8 pel)
-    cols = [((int(s) & 0xFFFF) ^ 0x8000) - 0x8000 for s in sb[:, 6]]
-    assert np.median(cols) < 0
+    assert (sb[:, 2 * PER_REF] < 8).all() and set(np.unique(sb[:, 2 * PER_REF + 1])) <= {0, 1}
+    # the NEWMV of the full-res search and the lookahead MVs track the
+    # synthetic motion (1.25 px/frame; display 8 from 4: +5 px, i.e. +40 in
+    # 1/8 pel, the source moving right: the reference block sits left)
+    def col(w):
+        return ((int(w) & 0xFFFF) ^ 0x8000) - 0x8000
+    assert np.median([col(s) for s in sb[:, RP.W_SUB]]) < 0
+    assert np.median([col(s) for s in sb[:, RP.W_LOOK:RP.W_LOOK + 32:2].ravel()]) < 0
 
 
 def test_cpu_replay_reconstruction_is_the_reference():
@@ -125,8 +128,8 @@ def test_cpu_replay_importance_bias():
         r.frame()
         r.frame()
         res.append(_sb_words(r.results(), 6, 1))
-    np.testing.assert_array_equal(res[0][:, :8], res[1][:, :8])
-    cost = [np.ascontiguousarray(x[:, 10]).view(np.float64) for x in res]
+    np.testing.assert_array_equal(res[0][:, :PER_REF], res[1][:, :PER_REF])
+    cost = [np.ascontiguousarray(x[:, PER_REF + 2]).view(np.float64) for x in res]
     assert (cost[1] >= cost[0]).all() and (cost[1] > cost[0]).any()
 
 
@@ -157,7 +160,7 @@ def test_cpu_tile_groups_equal_the_whole_frame():
                     g.import_(r, bufs[j])
             g.pad_recon()
         ws = single.results()
-        sw = _sb_words(ws, len(ws) // 20, 2)
+        sw = _sb_words(ws, len(ws) // RP.sb_words_per(2), 2)
         for g, (x0, y0, gw_, gh_) in zip(gs, rects):
             wg = g.results()
             gsb = _sb_words(wg, gw_ * gh_, 2)
@@ -305,7 +308,7 @@ def test_gpu_tile_groups_exchange():
         for g in gs:
             g.import_()
         cw = c.results()
-        sw = _sb_words(cw, len(cw) // 20, 2)
+        sw = _sb_words(cw, len(cw) // RP.sb_words_per(2), 2)
         for g, (x0, y0, gw_, gh_) in zip(gs, rects):
             wg = g.results()
             gsb = _sb_words(wg, gw_ * gh_, 2)
