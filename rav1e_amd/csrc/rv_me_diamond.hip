@@ -1079,7 +1079,24 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
       const int x0 = (q % G::NC) * 8, y0 = (q / G::NC) * 8 + lic * G::RPL;
       int32_t d[G::RPL][8];
       if (ok) {
-        if (!SUB) {
+        if (!SUB && !SATD) {  // 8-pixel row chunks: unaligned vector loads + v_sad
+#pragma unroll
+          for (int i = 0; i < G::RPL; i++) {
+            const Px *o = plane_ptr<Px>(a.org, jb.po_x + x0, jb.po_y + y0 + i);
+            const Px *r = plane_ptr<Px>(ref, sx + x0, sy + y0 + i);
+            if constexpr (sizeof(Px) == 1) {
+              uint2 ov, rv;
+              __builtin_memcpy(&ov, o, 8);
+              __builtin_memcpy(&rv, r, 8);
+              acc = __builtin_amdgcn_sad_u8(ov.x, rv.x, acc);
+              acc = __builtin_amdgcn_sad_u8(ov.y, rv.y, acc);
+            } else {
+              acc = sad16<Px>(ld16(o), ld16(r), acc);
+            }
+#pragma unroll
+            for (int t = 0; t < 8; t++) d[i][t] = 0;
+          }
+        } else if (!SUB) {
 #pragma unroll
           for (int i = 0; i < G::RPL; i++) {
             const Px *o = plane_ptr<Px>(a.org, jb.po_x + x0, jb.po_y + y0 + i);
@@ -1101,8 +1118,17 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
             int32_t mid[8];
             if (cf) {
               int32_t px[15];
+              if constexpr (sizeof(Px) == 1) {  // 16 bytes, one unaligned load
+                const uint4 v = ld16(w);
+                const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-              for (int t = 0; t < 15; t++) px[t] = w[t];
+                for (int t = 0; t < 15; t++) px[t] = (wd[t >> 2] >> (8 * (t & 3))) & 0xff;
+              } else {  // 32 bytes, two
+                const uint4 v0 = ld16(w), v1 = ld16(w + 8);
+                const uint32_t wd[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+                for (int t = 0; t < 15; t++) px[t] = (wd[t >> 1] >> (16 * (t & 1))) & 0xffff;
+              }
 #pragma unroll
               for (int t = 0; t < 8; t++) {
                 int32_t s = 0;
