@@ -1030,7 +1030,9 @@ __global__ __launch_bounds__(64) void ds_wave_kernel(DsArgs a) {
 // wavefront diverge freely (a shuffle only reads its own group's lanes).
 // SAD-only full-pel searches (SADONLY) give each lane a whole 8x8 chunk: a
 // 16x16 job then takes 16 lanes and a wavefront carries 4 jobs, which hides
-// the rounds' load latency better than one job per wavefront.
+// the rounds' load latency better than one job per wavefront (FL, F2:
+// 0.24 -> 0.13 ms at 2160p).  (Sub-pel tried the same, and a window staged
+// in LDS per round: both slower, the sub-pel search is VALU-bound.)
 template <int N, bool SADONLY>
 struct GrpGeo {
   static constexpr int C = N == 8 || (SADONLY && N == 16) ? 4 : 16;  // lanes per candidate
@@ -1057,22 +1059,6 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
   const rv_plane &ref = a.ref[jid / a.n_per_ref];
   const int ib = a.bd == 12 ? 2 : 4, maxv = (1 << a.bd) - 1;
   const int lic = c % G::LPC;  // lane in chunk
-  // sub-pel: the round's candidates lie within one pixel of each other, so
-  // the group stages the union of their (N + 7)^2 windows, (N + 8)^2
-  // pixels, in a job-private LDS slab once per round (coalesced loads by
-  // all L lanes) and the MC reads it from there; a round whose windows
-  // spread wider (arbitrary predictors) reads the plane directly.
-  constexpr int WN = N + 8;
-  constexpr int SLAB = SUB ? (WN * WN * (int)sizeof(Px) + 15) / 16 * 16 : 16;
-  __shared__ __align__(16) uint8_t lds_all[4 * (64 / G::L) * SLAB];
-  Px *slab = reinterpret_cast<Px *>(lds_all + ((threadIdx.x >> 6) * (64 / G::L) + lane / G::L) * SLAB);
-  bool staged = false;
-  int lox = 0, loy = 0;
-  auto origin = [&](rv_mv mv, int &ox, int &oy) {  // predict_inter's clamped window origin
-    const int xs = 3 + ref.xdec, ys = 3 + ref.ydec;
-    ox = clampi(jb.po_x + ((int)mv.col >> xs) - 3, -ref.xorigin, ref.width);
-    oy = clampi(jb.po_y + ((int)mv.row >> ys) - 3, -ref.yorigin, ref.height);
-  };
 
   // distortion of candidate mv for this subgroup (all lanes of the
   // subgroup return it); ok = false: zero work, the value is unused
@@ -1134,14 +1120,10 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
           for (int m = 0; m < G::RPL + 7; m++) {
             if (!rf && (m < 3 || m >= G::RPL + 3)) continue;  // only rows i + 3 are used
             const Px *w = plane_ptr<Px>(ref, sx + x0, sy + y0 + m);
-            const Px *ws = slab + (sy - loy + y0 + m) * WN + (sx - lox + x0);
             int32_t mid[8];
             if (cf) {
               int32_t px[15];
-              if (staged) {
-#pragma unroll
-                for (int t = 0; t < 15; t++) px[t] = ws[t];
-              } else if constexpr (sizeof(Px) == 1) {  // 16 bytes, one unaligned load
+              if constexpr (sizeof(Px) == 1) {  // 16 bytes, one unaligned load
                 const uint4 v = ld16(w);
                 const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -1161,7 +1143,7 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
               }
             } else {
 #pragma unroll
-              for (int t = 0; t < 8; t++) mid[t] = staged ? ws[t + 3] : w[t + 3];
+              for (int t = 0; t < 8; t++) mid[t] = w[t + 3];
             }
             if (rf) {
 #pragma unroll
@@ -1253,40 +1235,6 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
         mine = cands[kk];
         okm = ok[kk];
       }
-    if constexpr (SUB) {
-      int hix = -1 << 30, hiy = -1 << 30;
-      lox = loy = 1 << 30;
-      bool any = false;
-#pragma unroll
-      for (int kk = 0; kk < 4; kk++)
-        if (ok[kk]) {
-          int ox, oy;
-          origin(cands[kk], ox, oy);
-          lox = ox < lox ? ox : lox;
-          loy = oy < loy ? oy : loy;
-          hix = ox > hix ? ox : hix;
-          hiy = oy > hiy ? oy : hiy;
-          any = true;
-        }
-      staged = any && hix - lox <= 1 && hiy - loy <= 1;
-      if (staged) {  // uniform over the group
-        constexpr int B = (int)sizeof(Px), RD = (WN * B) / 4;  // dwords per window row
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();  // the previous round's reads are done
-        const uint8_t *src = (const uint8_t *)plane_ptr<Px>(ref, lox, loy);
-        const int64_t rs = (int64_t)ref.stride * B;
-        uint32_t *dst = reinterpret_cast<uint32_t *>(slab);
-        for (int i2 = gl; i2 < WN * RD; i2 += G::L) {
-          const int rr = i2 / RD, dd = i2 - rr * RD;
-          uint32_t v;
-          __builtin_memcpy(&v, src + rr * rs + 4 * dd, 4);
-          dst[i2] = v;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-    }
     const uint32_t dv = dist(mine, okm);
     const uint64_t cm = okm ? ds_cost(dv, mine, jb, a.hp) : ~0ull;
     const uint32_t lo = (uint32_t)cm, hi = (uint32_t)(cm >> 32);
