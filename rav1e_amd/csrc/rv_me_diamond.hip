@@ -1119,6 +1119,7 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
 #pragma unroll
           for (int m = 0; m < G::RPL + 7; m++) {
             if (!rf && (m < 3 || m >= G::RPL + 3)) continue;  // only rows i + 3 are used
+            if (rf && (m == 0 || m == G::RPL + 6)) continue;    // only by the zero taps 0 / 7
             const Px *w = plane_ptr<Px>(ref, sx + x0, sy + y0 + m);
             int32_t mid[8];
             if (cf) {
@@ -1134,11 +1135,12 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
 #pragma unroll
                 for (int t = 0; t < 15; t++) px[t] = (wd[t >> 1] >> (16 * (t & 1))) & 0xffff;
               }
+              // REGULAR taps 0 and 7 are zero for every fraction (src/mc.rs:71-88)
 #pragma unroll
               for (int t = 0; t < 8; t++) {
                 int32_t s = 0;
 #pragma unroll
-                for (int u = 0; u < 8; u++) s += __mul24((int32_t)xf[u], px[t + u]);
+                for (int u = 1; u < 7; u++) s += __mul24((int32_t)xf[u], px[t + u]);
                 mid[t] = round_shift(s, 7 - ib);
               }
             } else {
@@ -1149,7 +1151,7 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
 #pragma unroll
               for (int i = 0; i < G::RPL; i++) {
                 const int kk = m - i;
-                if (kk >= 0 && kk < 8) {
+                if (kk >= 1 && kk < 7) {  // taps 1..6
                   const int32_t f = yf[kk];
 #pragma unroll
                   for (int t = 0; t < 8; t++) v[i][t] += __mul24(f, mid[t]);

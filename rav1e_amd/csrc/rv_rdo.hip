@@ -314,6 +314,8 @@ __device__ __forceinline__ uint64_t rdo_biased(uint64_t v, double bias) {
 // d (LDS, row pitch dp): i32 / i64 moments (64 products of 12-bit pixels
 // stay below 2^30: u32 sums, one v_mad_u32_u24 per product), then the f64
 // ssim boost; `(sse * ssim_boost + 0.5) as u64`.
+__device__ __forceinline__ uint64_t rdo_cdef_finish(int32_t ss, int32_t sd, uint32_t ss2,
+                                                    uint32_t sd2, uint32_t ssd, int bd);
 template <typename Px>
 __device__ __forceinline__ uint64_t rdo_cdef_8x8(const Px *o, int64_t os, const Px *d, int dp,
                                                  int bd) {
@@ -331,6 +333,10 @@ __device__ __forceinline__ uint64_t rdo_cdef_8x8(const Px *o, int64_t os, const 
       sd2 += (uint32_t)wmul24(e, e);
       ssd += (uint32_t)wmul24(s, e);
     }
+  return rdo_cdef_finish(ss, sd, ss2, sd2, ssd, bd);
+}
+__device__ __forceinline__ uint64_t rdo_cdef_finish(int32_t ss, int32_t sd, uint32_t ss2,
+                                                    uint32_t sd2, uint32_t ssd, int bd) {
   const int cs = bd - 8;
   const int64_t s2 = (int64_t)ss2, d2 = (int64_t)sd2, sdv = (int64_t)ssd;
   const double svar = (double)(s2 - (((int64_t)ss * ss + 32) >> 6));
@@ -375,15 +381,42 @@ template <typename Px, int N, int LPB, bool LUMA>
 __device__ __forceinline__ uint64_t rdo_dist_biased(const RdoArgs &a, const RdoJob &j, const Px *o,
                                                     int64_t os, const Px *d) {
   if constexpr (LUMA) {
-    constexpr int NB = N / 8;
+    // one row of an 8x8 block per lane: row moments, a reduction over the
+    // block's 8 lanes (aligned groups of 8), the f64 tail on its first lane
+    constexpr int NB = N / 8, ROWS = NB * NB * 8;
+    static_assert(LPB % 8 == 0 && ROWS % LPB == 0, "rows of 8x8 blocks over the lanes");
     const int lane = threadIdx.x & (LPB - 1);
     uint64_t acc = 0;
-    for (int k = lane; k < NB * NB; k += LPB) {
-      const int by = k / NB, bx = k - by * NB;
-      const uint64_t v = rdo_cdef_8x8<Px>(o + (int64_t)(by * 8) * os + bx * 8, os,
-                                          d + by * 8 * N + bx * 8, N, a.bd);
-      const int px = j.bx + j.ox + bx * 8, py = j.by + j.oy + by * 8;
-      acc += rdo_biased(v, rdo_bias(a, px >> 2, py >> 2));
+#pragma unroll
+    for (int k0 = 0; k0 < ROWS; k0 += LPB) {
+      const int k = k0 + lane, blk = k >> 3, row = k & 7;
+      const int by = blk / NB, bx = blk - by * NB;
+      const Px *op = o + (int64_t)(by * 8 + row) * os + bx * 8;
+      const Px *dp = d + (by * 8 + row) * N + bx * 8;
+      int32_t ss = 0, sd = 0;
+      uint32_t ss2 = 0, sd2 = 0, ssd = 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const int32_t sv = op[i], e = dp[i];
+        ss += sv;
+        sd += e;
+        ss2 += (uint32_t)wmul24(sv, sv);
+        sd2 += (uint32_t)wmul24(e, e);
+        ssd += (uint32_t)wmul24(sv, e);
+      }
+#pragma unroll
+      for (int m = 1; m < 8; m <<= 1) {
+        ss += __shfl_xor(ss, m, 64);
+        sd += __shfl_xor(sd, m, 64);
+        ss2 += __shfl_xor(ss2, m, 64);
+        sd2 += __shfl_xor(sd2, m, 64);
+        ssd += __shfl_xor(ssd, m, 64);
+      }
+      if (row == 0) {
+        const uint64_t v = rdo_cdef_finish(ss, sd, ss2, sd2, ssd, a.bd);
+        const int px = j.bx + j.ox + bx * 8, py = j.by + j.oy + by * 8;
+        acc += rdo_biased(v, rdo_bias(a, px >> 2, py >> 2));
+      }
     }
     return acc;
   } else {
