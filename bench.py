@@ -2,10 +2,12 @@
 """bench.py -- encode hot-path replay throughput on MI355X.
 
 Metric (BASELINE.json): encoded frames/sec (+ Mpixels/sec) of the speed-10
-hot path of one stream, frames resident in HBM, vs the host CPU running the
-same schedule.  A "step" = one coded frame of the replay driver (DESIGN.md
-§3): F0 pyramid, F1 1/4-res full search, F2 1/2-res diamond, F3 full-res
-diamond + sub-pel, F4 every RDO inter candidate (NEARESTMV / NEAR0MV /
+hot path of one stream (config D: speed 6), frames resident in HBM, vs the
+host CPU running the same schedule.  A "step" = one coded frame of the replay
+driver: F0 pyramid, F1 1/4-res full search, F2 the four
+half-res quadrant searches, FL the lookahead's 16x16 searches, F3 full-res
+diamond + sub-pel (speed 6: also every 32x32, 16x16 and 8x8 block, and the
+partition decision), F4 every RDO inter candidate (NEARESTMV / NEAR0MV /
 GLOBALMV / NEWMV x reference, skip and non-skip: MC, distortion, diff + fwd
 DCT, quantize, estimate_rate, inverse + add) with rav1e's rd cost and
 argmin, F6 the winners' reconstruction, F5 8x8 importance SATD, F7 the

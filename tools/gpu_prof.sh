@@ -18,5 +18,6 @@ bash "$R/tools/gpu_step.sh" \
   "300 prof_$TAG/bench_1080p.log python $R/bench.py --config 1080p" \
   "300 prof_$TAG/bench_2160p444.log python $R/bench.py --config 2160p444" \
   "300 prof_$TAG/bench_2160p10.log python $R/bench.py --config 2160p10" \
+  "300 prof_$TAG/bench_2160p.log python $R/bench.py --config 2160p" \
   "200 prof_$TAG/bench_360p.log python $R/bench.py --config 360p" \
   "400 prof_$TAG/pytest_replay.log python -u -m pytest $R/tests/test_replay.py -x -q -m gpu --timeout 240 --timeout-method thread"
