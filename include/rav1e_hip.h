@@ -301,6 +301,23 @@ typedef struct rv_intra_job {
 int rv_predict_intra_batch(const rv_plane *dst, const rv_intra_job *d_jobs, const void *d_edges,
                            int n, int tx_size, int bit_depth, void *stream);
 
+/* ---- deblocking (src/deblock.rs) ---------------------------------------
+ * deblock_plane (src/deblock.rs:1174-1335, replaces the per-edge loop of
+ * deblock_filter_frame :1410-1416) of plane pli (0 Y, 1 U, 2 V) of a frame
+ * width x height luma pixels, in place: every transform edge of the 4x4
+ * grid, vertical then horizontal, with the 4 / 6 / 8 / 14-tap filters and
+ * their masks.  d_lg / d_skip: per luma 4x4 block (row pitch mi_stride,
+ * device memory) log2 of the square block's width in 4x4 units (1 = 8x8 ..
+ * 4 = 64x64; the transform is the block's size) and its skip flag; every
+ * block inter, loop-filter deltas off.  levels (host) = DeblockState.levels
+ * [Y vertical, Y horizontal, U, V]. */
+int rv_deblock_plane(const rv_plane *plane, int pli, int width, int height, const uint8_t *d_lg,
+                     const uint8_t *d_skip, int mi_stride, const uint8_t *levels, int bit_depth,
+                     void *stream);
+/* deblock_filter_optimize's fast path (src/deblock.rs:1477-1517, speed >= 8):
+ * the level from the frame's ac quantizer (ac_q(base_q_idx, 0, bd)). */
+int rv_deblock_fast_level(int ac_q, int bit_depth, int is_key);
+
 /* dc_q / ac_q lookups (src/quantize.rs:42-62) on the host: ac = 0 for
  * dc_qlookup*_Q3, 1 for ac_qlookup*_Q3; -1 on bad arguments. */
 int rv_q_lookup(int ac, int qindex, int bit_depth);

@@ -73,6 +73,14 @@ void orc_mc_avg(void *dst, ptrdiff_t dst_stride, const int16_t *tmp1,
  * edge = rav1e's 257-pixel edge_buf. */
 void orc_predict_intra(int mode, int variant, void *dst, ptrdiff_t stride, int w, int h,
                        int bit_depth, int hbd, const void *edge);
+/* deblock_plane (src/deblock.rs:1174-1335) of plane pli at origin (visible
+ * (0, 0)); lg / skip per luma 4x4 block (row pitch mi_stride): log2 of the
+ * square block's width in 4x4 units, skip flag; levels = [Y vertical, Y
+ * horizontal, U, V] */
+void orc_deblock_plane(void *origin, ptrdiff_t stride, int hbd, int bd, int width, int height,
+                       int xdec, int ydec, int pli, const uint8_t *lg, const uint8_t *skip,
+                       int mi_stride, const uint8_t levels[4]);
+int orc_deblock_fast_level(int ac_q, int bd, int is_key);
 /* SUBPEL_FILTERS + get_filter (src/mc.rs:70-179, 201-210) */
 const int32_t *orc_get_filter(int mode, int frac, int length);
 

@@ -247,6 +247,8 @@ def _declare(L):
         "rv_cdef_moments_batch": (i32, [P, P, vp, i32, i32, i32, vp, vp]),
         "rv_put_8tap_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, i32, vp]),
         "rv_predict_intra_batch": (i32, [P, vp, vp, i32, i32, i32, vp]),
+        "rv_deblock_plane": (i32, [P, i32, i32, i32, vp, vp, i32, vp, i32, vp]),
+        "rv_deblock_fast_level": (i32, [i32, i32, i32]),
         "rv_prep_8tap_batch": (i32, [vp, P, vp, i32, i32, i32, i32, i32, i32, vp]),
         "rv_mc_avg_batch": (i32, [P, vp, vp, vp, i32, i32, i32, i32, vp]),
         "rv_mc_dist_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
@@ -554,6 +556,29 @@ def predict_intra_batch(dst: DevicePlane, jobs, edges: np.ndarray, tx_size, bit_
     _check(lib().rv_predict_intra_batch(C.byref(dst.desc), dj.ptr, de.ptr, len(jobs), tx_size,
                                         bit_depth, None), "rv_predict_intra_batch")
     _sync()
+
+
+def deblock_plane(plane: DevicePlane, pli, width, height, lg: np.ndarray, skip: np.ndarray,
+                  levels, bit_depth=8):
+    """deblock_plane (src/deblock.rs:1174-1335) of plane pli of a width x
+    height frame, in place.  lg / skip: (rows, cols) per luma 4x4 block
+    (log2 of the square block's width in 4x4 units, skip flag); levels =
+    [Y vertical, Y horizontal, U, V]."""
+    lg = np.ascontiguousarray(lg, dtype=np.uint8)
+    skip = np.ascontiguousarray(skip, dtype=np.uint8)
+    if lg.shape != skip.shape or lg.shape[1] < (width + 3) // 4 or lg.shape[0] < (height + 3) // 4:
+        raise Rav1eHipError("deblock_plane: lg / skip must cover the frame's 4x4 grid")
+    if not ((lg >= 1) & (lg <= 4)).all():
+        raise Rav1eHipError("deblock_plane: block sizes 8x8 .. 64x64 (lg 1 .. 4)")
+    dl, ds = DeviceBuffer.from_array(lg), DeviceBuffer.from_array(skip)
+    lv = np.ascontiguousarray(np.asarray(levels, dtype=np.uint8))
+    _check(lib().rv_deblock_plane(C.byref(plane.desc), pli, width, height, dl.ptr, ds.ptr,
+                                  lg.shape[1], lv.ctypes.data, bit_depth, None), "rv_deblock_plane")
+    _sync()
+
+
+def deblock_fast_level(ac_q, bit_depth, is_key=False):
+    return int(lib().rv_deblock_fast_level(int(ac_q), bit_depth, 1 if is_key else 0))
 
 
 def prep_8tap_batch(src: DevicePlane, jobs, w, h, mode_x=0, mode_y=0, bit_depth=8):

@@ -1,0 +1,242 @@
+// rv_deblock.hip -- the deblocking filter of a reconstructed plane
+// (deblock_plane, src/deblock.rs:1174-1335) on gfx950.
+//
+// One lane per pixel row (vertical edges) or column (horizontal edges) of a
+// 4-pixel edge segment.  Within a pass no filter reads a pixel another one
+// writes (the transform grid keeps edges >= 8 pixels apart and the widest
+// filter writes 6 on a side), so a pass is one launch; rav1e's interleaved
+// order (horizontal edges lagging one 4x4 row and two columns) is
+// equivalent to all vertical edges, then all horizontal ones.  Blocks come
+// as per-4x4 bytes: log2 of the square block's width in 4x4 units and the
+// skip flag (every block inter, loop-filter deltas off).
+#include "rv_device.h"
+
+namespace rv {
+
+struct DbArgs {
+  rv_plane p;
+  const uint8_t *lg, *skip;
+  int mi_stride, cols, rows, xdec, ydec, pli, level, bd, vert;
+};
+
+__device__ __forceinline__ int db_abs(int v) { return v < 0 ? -v : v; }
+__device__ __forceinline__ int db_max(int a, int b) { return a > b ? a : b; }
+__device__ __forceinline__ int lim_lv(int v, int s) { return (v + (1 << s) - 1) >> s; }
+__device__ __forceinline__ int blim_lv(int v, int s) { return (((v + (1 << s) - 1) >> s) - 2) / 3; }
+__device__ __forceinline__ int thr_lv(int v, int s) { return (v + (1 << s) - 1) >> s << 4; }
+
+// filter_narrow2_4 / filter_narrow4_4 (src/deblock.rs:165-240) on p1 p0 q0 q1
+__device__ __forceinline__ void db_narrow(int32_t *v, int s, bool four) {
+  const int lo = -(128 << s), hi = (128 << s) - 1, mx = (256 << s) - 1;
+  const int f0 = four ? 0 : clampi(v[0] - v[3], lo, hi);
+  const int f1 = clampi(f0 + 3 * (v[2] - v[1]) + 4, lo, hi) >> 3;
+  const int f2 = clampi(f0 + 3 * (v[2] - v[1]) + 3, lo, hi) >> 3;
+  if (four) {
+    const int f3 = (f1 + 1) >> 1;
+    v[0] = clampi(v[0] + f3, 0, mx);
+    v[3] = clampi(v[3] - f3, 0, mx);
+  }
+  v[1] = clampi(v[1] + f2, 0, mx);
+  v[2] = clampi(v[2] - f1, 0, mx);
+}
+__device__ __forceinline__ void db_narrow_sel(int32_t *c, int s, int level) {
+  const int nhev = thr_lv(db_max(db_abs(c[0] - c[1]), db_abs(c[3] - c[2])), s);
+  db_narrow(c, s, nhev <= level);
+}
+__device__ __forceinline__ int db_blim(const int32_t *c, int s) {
+  return blim_lv(db_abs(c[1] - c[2]) * 2 + db_abs(c[0] - c[3]) / 2, s);
+}
+
+// deblock_size{4,6,8,14}_inner (:382-995) on N taps across the edge
+template <int N>
+__device__ __forceinline__ void db_filter(int32_t *t, int level, int bd) {
+  const int s = bd - 8, flat = 1 << s;
+  if constexpr (N == 4) {
+    const int m = db_max(lim_lv(db_max(db_abs(t[0] - t[1]), db_abs(t[3] - t[2])), s), db_blim(t, s));
+    if (m <= level) db_narrow_sel(t, s, level);
+  } else if constexpr (N == 6) {
+    const int m = db_max(lim_lv(db_max(db_max(db_abs(t[0] - t[1]), db_abs(t[1] - t[2])),
+                                       db_max(db_abs(t[5] - t[4]), db_abs(t[4] - t[3]))), s),
+                         db_blim(t + 1, s));
+    if (m > level) return;
+    const int f = db_max(db_max(db_abs(t[1] - t[2]), db_abs(t[4] - t[3])),
+                         db_max(db_abs(t[0] - t[2]), db_abs(t[5] - t[3])));
+    if (f <= flat) {  // filter_wide6_4
+      const int p2 = t[0], p1 = t[1], p0 = t[2], q0 = t[3], q1 = t[4], q2 = t[5];
+      t[1] = (p2 * 3 + p1 * 2 + p0 * 2 + q0 + 4) >> 3;
+      t[2] = (p2 + p1 * 2 + p0 * 2 + q0 * 2 + q1 + 4) >> 3;
+      t[3] = (p1 + p0 * 2 + q0 * 2 + q1 * 2 + q2 + 4) >> 3;
+      t[4] = (p0 + q0 * 2 + q1 * 2 + q2 * 3 + 4) >> 3;
+    } else {
+      db_narrow_sel(t + 1, s, level);
+    }
+  } else {
+    int32_t *in = N == 8 ? t : t + 3;  // p3 .. q3
+    const int m = db_max(
+        lim_lv(db_max(db_max(db_max(db_abs(in[0] - in[1]), db_abs(in[1] - in[2])), db_abs(in[2] - in[3])),
+                      db_max(db_max(db_abs(in[7] - in[6]), db_abs(in[6] - in[5])), db_abs(in[5] - in[4]))),
+               s),
+        db_blim(in + 2, s));
+    if (m > level) return;
+    const int f8 = db_max(db_max(db_max(db_abs(in[2] - in[3]), db_abs(in[5] - in[4])),
+                                 db_max(db_abs(in[1] - in[3]), db_abs(in[6] - in[4]))),
+                          db_max(db_abs(in[0] - in[3]), db_abs(in[7] - in[4])));
+    if (f8 > flat) {
+      db_narrow_sel(in + 2, s, level);
+      return;
+    }
+    bool wide14 = false;
+    if constexpr (N == 14) {
+      const int f14 = db_max(db_max(db_max(db_abs(t[2] - t[6]), db_abs(t[11] - t[7])),
+                                    db_max(db_abs(t[1] - t[6]), db_abs(t[12] - t[7]))),
+                             db_max(db_abs(t[0] - t[6]), db_abs(t[13] - t[7])));
+      wide14 = f14 <= flat;
+    }
+    if (wide14) {  // filter_wide14_12
+      const int p6 = t[0], p5 = t[1], p4 = t[2], p3 = t[3], p2 = t[4], p1 = t[5], p0 = t[6];
+      const int q0 = t[7], q1 = t[8], q2 = t[9], q3 = t[10], q4 = t[11], q5 = t[12], q6 = t[13];
+      t[1] = (p6 * 7 + p5 * 2 + p4 * 2 + p3 + p2 + p1 + p0 + q0 + 8) >> 4;
+      t[2] = (p6 * 5 + p5 * 2 + p4 * 2 + p3 * 2 + p2 + p1 + p0 + q0 + q1 + 8) >> 4;
+      t[3] = (p6 * 4 + p5 + p4 * 2 + p3 * 2 + p2 * 2 + p1 + p0 + q0 + q1 + q2 + 8) >> 4;
+      t[4] = (p6 * 3 + p5 + p4 + p3 * 2 + p2 * 2 + p1 * 2 + p0 + q0 + q1 + q2 + q3 + 8) >> 4;
+      t[5] = (p6 * 2 + p5 + p4 + p3 + p2 * 2 + p1 * 2 + p0 * 2 + q0 + q1 + q2 + q3 + q4 + 8) >> 4;
+      t[6] = (p6 + p5 + p4 + p3 + p2 + p1 * 2 + p0 * 2 + q0 * 2 + q1 + q2 + q3 + q4 + q5 + 8) >> 4;
+      t[7] = (p5 + p4 + p3 + p2 + p1 + p0 * 2 + q0 * 2 + q1 * 2 + q2 + q3 + q4 + q5 + q6 + 8) >> 4;
+      t[8] = (p4 + p3 + p2 + p1 + p0 + q0 * 2 + q1 * 2 + q2 * 2 + q3 + q4 + q5 + q6 * 2 + 8) >> 4;
+      t[9] = (p3 + p2 + p1 + p0 + q0 + q1 * 2 + q2 * 2 + q3 * 2 + q4 + q5 + q6 * 3 + 8) >> 4;
+      t[10] = (p2 + p1 + p0 + q0 + q1 + q2 * 2 + q3 * 2 + q4 * 2 + q5 + q6 * 4 + 8) >> 4;
+      t[11] = (p1 + p0 + q0 + q1 + q2 + q3 * 2 + q4 * 2 + q5 * 2 + q6 * 5 + 8) >> 4;
+      t[12] = (p0 + q0 + q1 + q2 + q3 + q4 * 2 + q5 * 2 + q6 * 7 + 8) >> 4;
+    } else {  // filter_wide8_6 on p3 .. q3
+      const int p3 = in[0], p2 = in[1], p1 = in[2], p0 = in[3], q0 = in[4], q1 = in[5], q2 = in[6],
+                q3 = in[7];
+      in[1] = (p3 * 3 + p2 * 2 + p1 + p0 + q0 + 4) >> 3;
+      in[2] = (p3 * 2 + p2 + p1 * 2 + p0 + q0 + q1 + 4) >> 3;
+      in[3] = (p3 + p2 + p1 + p0 * 2 + q0 + q1 + q2 + 4) >> 3;
+      in[4] = (p2 + p1 + p0 + q0 * 2 + q1 + q2 + q3 + 4) >> 3;
+      in[5] = (p1 + p0 + q0 + q1 * 2 + q2 + q3 * 2 + 4) >> 3;
+      in[6] = (p0 + q0 + q1 + q2 * 2 + q3 * 3 + 4) >> 3;
+    }
+  }
+}
+
+// transform width / height in 4x4 units: luma = the block, chroma =
+// largest_chroma_tx_size (coded size <= 32, src/partition.rs:288-297)
+__device__ __forceinline__ int db_tx_mi(int lg, int pli, int dec) {
+  if (pli == 0) return 1 << lg;
+  int px = (4 << lg) >> dec;
+  px = px > 32 ? 32 : px;
+  return px >= 4 ? px >> 2 : 1;
+}
+
+template <typename Px, int N>
+__device__ __forceinline__ void db_apply(const DbArgs &a, int ox, int oy, int k) {
+  const int h = N >> 1;
+  Px *base = a.vert ? plane_ptr_mut<Px>(a.p, ox - h, oy + k) : plane_ptr_mut<Px>(a.p, ox + k, oy - h);
+  const int64_t step = a.vert ? 1 : a.p.stride;
+  int32_t t[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) t[i] = base[i * step];
+  db_filter<N>(t, a.level, a.bd);
+#pragma unroll
+  for (int i = 0; i < N; i++) base[i * step] = (Px)t[i];
+}
+
+// thread = (edge segment, pixel row / column k of its 4)
+template <typename Px>
+__global__ __launch_bounds__(256) void deblock_kernel(DbArgs a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int k = i & 3, seg = i >> 2;
+  const int sx = a.vert ? (a.cols >> a.xdec) - 1 : (a.cols >> a.xdec);  // segments per row
+  const int sy = a.vert ? (a.rows >> a.ydec) : (a.rows >> a.ydec) - 1;
+  if (seg >= sx * sy) return;
+  const int gy = seg / sx, gx = seg - gy * sx;
+  const int x = (gx + (a.vert ? 1 : 0)) << a.xdec, y = (gy + (a.vert ? 0 : 1)) << a.ydec;
+  const int b = y * a.mi_stride + x;
+  const int lgb = a.lg[b], n4 = 1 << lgb;
+  const int pos = a.vert ? x : y, dec = a.vert ? a.xdec : a.ydec;
+  if (((pos >> dec) & (db_tx_mi(lgb, a.pli, dec) - 1)) != 0) return;  // not a transform edge
+  const int px = (x | a.xdec) - (a.vert ? 1 << a.xdec : 0);
+  const int py = (y | a.ydec) - (a.vert ? 0 : 1 << a.ydec);
+  const int pb = py * a.mi_stride + px;
+  const bool block_edge = (pos & (n4 - 1)) == 0;
+  if (!(block_edge || !a.skip[b] || !a.skip[pb])) return;
+  const int tn = db_tx_mi(lgb, a.pli, dec), tp = db_tx_mi(a.lg[pb], a.pli, dec);
+  int size = (tn < tp ? tn : tp) << 2;
+  const int cap = a.pli == 0 ? 14 : 6;
+  size = size < cap ? size : cap;
+  const int ox = (x * 4) >> a.xdec, oy = (y * 4) >> a.ydec;
+  if (size == 4)
+    db_apply<Px, 4>(a, ox, oy, k);
+  else if (size == 6)
+    db_apply<Px, 6>(a, ox, oy, k);
+  else if (size == 8)
+    db_apply<Px, 8>(a, ox, oy, k);
+  else
+    db_apply<Px, 14>(a, ox, oy, k);
+}
+
+}  // namespace rv
+
+using namespace rv;
+
+// The deblocking of one plane (pli 0 = Y, 1 = U, 2 = V) of a frame of
+// width x height luma pixels; lg / skip per luma 4x4 block (row pitch
+// mi_stride >= the frame's 4x4 columns, device memory); levels = the
+// DeblockState levels [Y vertical, Y horizontal, U, V].
+int rv_deblock_plane_dev(const rv_plane *p, int pli, int width, int height, const uint8_t *d_lg,
+                         const uint8_t *d_skip, int mi_stride, const uint8_t levels[4],
+                         int bit_depth, hipStream_t s) {
+  if (pli == 0 ? (levels[0] == 0 && levels[1] == 0) : levels[pli + 1] == 0) return RV_OK;
+  DbArgs a;
+  a.p = *p;
+  a.lg = d_lg;
+  a.skip = d_skip;
+  a.mi_stride = mi_stride;
+  a.xdec = p->xdec;
+  a.ydec = p->ydec;
+  a.cols = ((((width + 3) >> 2) + ((1 << a.xdec) >> 1)) >> a.xdec) << a.xdec;
+  a.rows = ((((height + 3) >> 2) + ((1 << a.ydec) >> 1)) >> a.ydec) << a.ydec;
+  a.pli = pli;
+  a.bd = bit_depth;
+  for (int pass = 0; pass < 2; pass++) {
+    a.vert = pass == 0;
+    a.level = pli == 0 ? levels[a.vert ? 0 : 1] : levels[pli + 1];
+    if (a.level == 0) continue;
+    const int sx = a.vert ? (a.cols >> a.xdec) - 1 : (a.cols >> a.xdec);
+    const int sy = a.vert ? (a.rows >> a.ydec) : (a.rows >> a.ydec) - 1;
+    const int64_t n = (int64_t)(sx > 0 ? sx : 0) * (sy > 0 ? sy : 0) * 4;
+    if (n == 0) continue;
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    if (p->hbd)
+      deblock_kernel<uint16_t><<<grid, 256, 0, s>>>(a);
+    else
+      deblock_kernel<uint8_t><<<grid, 256, 0, s>>>(a);
+  }
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+extern "C" int rv_deblock_plane(const rv_plane *plane, int pli, int width, int height,
+                                const uint8_t *d_lg, const uint8_t *d_skip, int mi_stride,
+                                const uint8_t *levels, int bit_depth, void *stream) {
+  if (!plane || !levels || pli < 0 || pli > 2 || width <= 0 || height <= 0 || !d_lg || !d_skip ||
+      mi_stride < (width + 3) / 4 || (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
+      (plane->hbd != (bit_depth > 8)))
+    return rv_set_error(RV_EINVAL, "rv_deblock_plane: bad arguments");
+  return rv_deblock_plane_dev(plane, pli, width, height, d_lg, d_skip, mi_stride, levels,
+                              bit_depth, rv_resolve_stream(stream));
+}
+
+// deblock_filter_optimize's fast path (src/deblock.rs:1477-1517, speed >=
+// 8): the level of every plane and direction from the frame's ac quantizer
+extern "C" int rv_deblock_fast_level(int ac_q, int bit_depth, int is_key) {
+  int v;
+  if (bit_depth == 8)
+    v = is_key ? (ac_q * 17563 - 421574 + (1 << 17)) >> 18 : (ac_q * 6017 + 650707 + (1 << 17)) >> 18;
+  else if (bit_depth == 10)
+    v = ((ac_q * 20723 + 4060632 + (1 << 19)) >> 20) - (is_key ? 4 : 0);
+  else
+    v = ((ac_q * 20723 + 16242526 + (1 << 21)) >> 22) - (is_key ? 4 : 0);
+  return v < 0 ? 0 : v > 63 ? 63 : v;
+}

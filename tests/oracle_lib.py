@@ -60,6 +60,9 @@ def lib():
                                                 vp]
         L.orc_estimate_rate.argtypes = [i32, i32, C.c_uint64]
         L.orc_get_log_tx_scale.restype = i32
+        L.orc_deblock_plane.argtypes = [vp, sz, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32,
+                                        vp]
+        L.orc_deblock_fast_level.argtypes = [i32, i32, i32]
         _lib = L
     return _lib
 
@@ -101,6 +104,22 @@ def predict_intra(mode, variant, w, h, edge, bd=8):
     dst = np.zeros((h, w), dtype=edge.dtype)
     lib().orc_predict_intra(mode, variant, ptr(dst), w, w, h, bd, 1 if bd > 8 else 0, ptr(edge))
     return dst
+
+
+def deblock_plane(full, yo, xo, width, height, xdec, ydec, pli, lg, skip, levels, bd=8):
+    """orc_deblock_plane on a full (padded) plane array, visible origin (xo,
+    yo), in place."""
+    lg = np.ascontiguousarray(lg, dtype=np.uint8)
+    skip = np.ascontiguousarray(skip, dtype=np.uint8)
+    lv = np.ascontiguousarray(np.asarray(levels, dtype=np.uint8))
+    lib().orc_deblock_plane(ptr(full, yo * full.shape[1] + xo), full.shape[1], hbd_of(full), bd,
+                            width, height, xdec, ydec, pli, ptr(lg), ptr(skip), lg.shape[1],
+                            ptr(lv))
+    return full
+
+
+def deblock_fast_level(ac_q, bd, is_key=False):
+    return int(lib().orc_deblock_fast_level(int(ac_q), bd, 1 if is_key else 0))
 
 
 def prep_8tap(src, sy, sx, w, h, col_frac, row_frac, mode_x=0, mode_y=0, bd=8):

@@ -1,0 +1,87 @@
+"""Deblocking filter (deblock_plane, src/deblock.rs:1174-1335): the HIP
+kernel (rv_deblock_plane) against the oracle's restatement
+(oracle/orc_deblock.c) on random block layouts, and the oracle's own
+behaviour (a step edge inside the filter's reach is smoothed, level 0 is a
+no-op, the fast levels of deblock_filter_optimize)."""
+import numpy as np
+import pytest
+
+from tests import oracle_lib as O
+
+
+def _layout(rng, mi_w, mi_h, min_lg=1):
+    """A random quad-tree of square blocks 64x64 .. 8x8 over the 4x4 grid:
+    lg (log2 width in 4x4 units) and skip per 4x4 block."""
+    lg = np.zeros((mi_h, mi_w), np.uint8)
+    skip = np.zeros((mi_h, mi_w), np.uint8)
+
+    def place(x, y, l):
+        if x >= mi_w or y >= mi_h:
+            return
+        if l > min_lg and rng.random() < 0.6:
+            h = 1 << (l - 1)
+            for dy in (0, h):
+                for dx in (0, h):
+                    place(x + dx, y + dy, l - 1)
+            return
+        n = 1 << l
+        lg[y:y + n, x:x + n] = l
+        skip[y:y + n, x:x + n] = rng.random() < 0.5
+    for y in range(0, mi_h, 16):
+        for x in range(0, mi_w, 16):
+            place(x, y, 4)
+    return lg, skip
+
+
+def _blocky(rng, h, w, bd):
+    """8x8-blocky content plus noise: every edge has something to filter."""
+    base = rng.integers(0, 1 << bd, ((h + 7) // 8, (w + 7) // 8))
+    img = np.kron(base, np.ones((8, 8), np.int64))[:h, :w]
+    img = img // 4 + (1 << bd) * 3 // 8 + rng.integers(-2, 3, (h, w))
+    return np.clip(img, 0, (1 << bd) - 1).astype(np.uint16 if bd > 8 else np.uint8)
+
+
+def test_oracle_smooths_a_step_and_level_zero_is_identity():
+    w, h = 64, 32
+    img = np.zeros((h + 32, w + 32), np.uint8)
+    img[:, : 16 + 32] = 100
+    img[:, 16 + 32:] = 106
+    lg = np.full((h // 4, w // 4), 2, np.uint8)  # 16x16 blocks: an edge at x = 32
+    skip = np.zeros_like(lg)
+    a = O.deblock_plane(img.copy(), 16, 16, w, h, 0, 0, 0, lg, skip, [0, 0, 0, 0])
+    assert (a == img).all()
+    b = O.deblock_plane(img.copy(), 16, 16, w, h, 0, 0, 0, lg, skip, [20, 20, 0, 0])
+    row = b[20, 16 + 24:16 + 40].astype(int)
+    assert (np.diff(row) >= 0).all() and np.abs(np.diff(row)).max() < 6
+    # the fast levels (speed >= 8): 8-bit inter frame at ac_q 128
+    assert O.deblock_fast_level(128, 8) == (128 * 6017 + 650707 + (1 << 17)) >> 18
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bd,xdec,ydec,w,h", [(8, 1, 1, 200, 136), (10, 1, 1, 136, 72),
+                                              (12, 0, 0, 128, 96), (8, 0, 0, 256, 64)])
+def test_deblock_plane_vs_oracle(bd, xdec, ydec, w, h):
+    import rav1e_amd as R
+    R.require_device(0)
+    rng = np.random.default_rng(2000 + bd + 7 * w + xdec)
+    mi_w, mi_h = (w + 3) // 4, (h + 3) // 4
+    for trial in range(3):
+        lg, skip = _layout(rng, mi_w, mi_h)
+        levels = [int(v) for v in rng.integers(0, 64, 4)]
+        if trial == 0:
+            levels = [63, 63, 63, 63]
+        for pli in range(3):
+            pw = w if pli == 0 else (w + xdec) >> xdec
+            ph = h if pli == 0 else (h + ydec) >> ydec
+            xd, yd = (0, 0) if pli == 0 else (xdec, ydec)
+            img = _blocky(rng, ph, pw, bd)
+            dp = R.DevicePlane.from_array(img, xpad=88 >> xd, ypad=88 >> yd, xdec=xd, ydec=yd)
+            full = dp.download_full()
+            xo, yo = dp.desc.xorigin, dp.desc.yorigin
+            R.deblock_plane(dp, pli, w, h, lg, skip, levels, bd)
+            want = O.deblock_plane(full.copy(), yo, xo, w, h, xd, yd, pli, lg, skip, levels, bd)
+            got = dp.download_full()
+            bad = np.argwhere(got != want)
+            assert bad.size == 0, (trial, pli, levels, bad[:5])
+            if trial == 0:
+                assert (got != full).any()  # something was filtered
