@@ -464,6 +464,10 @@ typedef struct rv_replay_cfg {
  * superblock (bit 0: 64x64 split, 1 + q: 32x32 quadrant q split, 5 + 4 *
  * row + col: 16x16 split), then the 5 tail words. */
 #define RV_REPLAY_SPEED6 8
+/* flags: deblock every coded frame before it becomes a reference
+ * (deblock_filter_optimize's fast levels + deblock_filter_frame,
+ * src/encoder.rs:2789-2793); one tile group only. */
+#define RV_REPLAY_DEBLOCK 16
 typedef struct rv_replay_frame_info {
   int32_t display;            /* display index of the coded frame */
   int32_t me_range_scale;     /* 4 >> pyramid level (src/encoder.rs:838) */

@@ -90,6 +90,9 @@ typedef struct orc_replay {
   orc_qctx qs[3][4][3];
   uint8_t *leaf0;
   size_t nwords, wpart;
+  /* RV_REPLAY_DEBLOCK (orc_replay_set_deblock): the block map, fast levels */
+  int deblock, mi_cols, mi_rows;
+  uint8_t *mi_lg, *mi_skip;
   pthread_mutex_t mu;
   int next_sb, pass, sb_limit;
 } orc_replay;
@@ -353,6 +356,8 @@ void orc_replay_destroy(orc_replay *r) {
     free(P->leaf);
   }
   free(r->leaf0);
+  free(r->mi_lg);
+  free(r->mi_skip);
   pthread_mutex_destroy(&r->mu);
   free(r);
 }
@@ -398,6 +403,59 @@ int orc_replay_set_speed(orc_replay *r, int speed) {
   free(r->words);
   r->words = calloc(r->nwords, 8);
   return r->words && r->leaf0 ? 0 : -1;
+}
+
+/* Deblock every coded frame before it becomes a reference (one tile group:
+ * the replay's RV_REPLAY_DEBLOCK). */
+int orc_replay_set_deblock(orc_replay *r, int on) {
+  r->deblock = on != 0;
+  if (!r->deblock) return 0;
+  if (r->tx0 || r->ty0 || r->tw * SB < r->W || r->th * SB < r->H) return -1;
+  r->mi_cols = (r->W + 3) / 4;
+  r->mi_rows = (r->H + 3) / 4;
+  free(r->mi_lg);
+  free(r->mi_skip);
+  r->mi_lg = calloc((size_t)r->mi_cols * r->mi_rows, 1);
+  r->mi_skip = calloc((size_t)r->mi_cols * r->mi_rows, 1);
+  return r->mi_lg && r->mi_skip ? 0 : -1;
+}
+
+/* the block map of block (bx, by) of the level-l grid */
+static void map_block(orc_replay *r, int l, int gx, int gy, int skip) {
+  const int n4 = 16 >> l;
+  for (int y = gy * n4; y < (gy + 1) * n4 && y < r->mi_rows; y++)
+    for (int x = gx * n4; x < (gx + 1) * n4 && x < r->mi_cols; x++) {
+      r->mi_lg[(size_t)y * r->mi_cols + x] = (uint8_t)(4 - l);
+      r->mi_skip[(size_t)y * r->mi_cols + x] = (uint8_t)skip;
+    }
+}
+
+/* deblock_filter_optimize's fast levels + deblock_filter_frame
+ * (src/encoder.rs:2789-2793) of the frame just coded */
+static void deblock_frame(orc_replay *r) {
+  const int R = r->R;
+  for (int sb = 0; sb < r->nsb; sb++) {
+    const int sx = sb % r->tw, sy = sb / r->tw;
+    if (!r->s6 || r->leaf0[sb])
+      map_block(r, 0, r->tx0 + sx, r->ty0 + sy,
+                (int)r->words[(size_t)sb * (WPR * R + 4) + WPR * R + 1]);
+  }
+  for (int l = 1; r->s6 && l < 4; l++) {
+    const struct olevel *P = &r->pl[l];
+    for (int b = 0; b < P->n; b++)
+      if (P->leaf[b])
+        map_block(r, l, P->tx0 + b % P->gw, P->ty0 + b / P->gw,
+                  (int)r->words[P->woff + (size_t)b * (4 * R + 4) + 4 * R + 1]);
+  }
+  const int qidx = r->lv[r->fi.level].qidx;
+  const uint8_t lv = (uint8_t)orc_deblock_fast_level(orc_ac_q(qidx, 0, r->bd), r->bd, 0);
+  if (!lv) return;
+  const uint8_t lv4[4] = {lv, lv, lv, lv};
+  oslot *S = &r->slots[r->fi.display % NSLOT];
+  oplane *pl[3] = {&S->y, &S->u, &S->v};
+  for (int p = 0; p < 3; p++)
+    orc_deblock_plane(org_of(pl[p], r->hbd), pl[p]->stride, r->hbd, r->bd, r->W, r->H,
+                      p ? r->xdec : 0, p ? r->ydec : 0, p, r->mi_lg, r->mi_skip, r->mi_cols, lv4);
 }
 
 static void pad(const orc_replay *r, oplane *p) {
@@ -1232,6 +1290,7 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
   memset(r->tail, 0, sizeof(r->tail));
   r->sb_limit = sb_limit;
   for (int pass = 0; pass < 4; pass++) run_pass(r, pass);
+  if (r->deblock) deblock_frame(r);
   r->tail[3] = (uint64_t)(r->vis_w / 8) * (r->vis_h / 8);
   if (pad_recon) {
     pad(r, &S->y);

@@ -56,6 +56,12 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             int subpixel, int use_satd, int allow_hp, int bit_depth,
                             rv_fs_result *d_out, uint32_t *d_evals, const rv::ChainNext *next,
                             void *stream);
+// rv_deblock.hip
+int rv_deblock_plane_dev(const rv_plane *p, int pli, int width, int height, const uint8_t *d_lg,
+                         const uint8_t *d_skip, int mi_stride, const uint8_t levels[4],
+                         int bit_depth, hipStream_t s);
+extern "C" int rv_deblock_fast_level(int ac_q, int bit_depth, int is_key);
+extern "C" int rv_q_lookup(int ac, int qindex, int bit_depth);
 // rv_frame.hip
 int rv_plane_pyramid(const rv_plane *y, const rv_plane *h, const rv_plane *q, void *stream);
 int rv_synth_frame(const rv_plane *y, const rv_plane *u, const rv_plane *v, int t, int bit_depth,
@@ -493,6 +499,28 @@ __global__ __launch_bounds__(64) void partition_kernel(Geo g, PartArgs p) {
   if (live) p.words[sb] = mask;
 }
 
+// The deblocking filter's block map: every 4x4 of a committed block gets
+// the block's log2 size (4x4 units) and skip flag.  One thread per 4x4 row
+// of a block: block i = list ? list[i] : i of the level grid (gw wide,
+// origin (x0, y0) in blocks), lg = 4 - level.
+__global__ void block_map_kernel(const int32_t *list, const int32_t *count, int n, int gw, int x0,
+                                 int y0, int level, const RdoWinner *win, uint8_t *lg,
+                                 uint8_t *skip, int mi_stride, int mi_cols, int mi_rows) {
+  const int n4 = 16 >> level;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int nb = count ? *count : n;
+  if (i >= nb * n4) return;
+  const int j = i / n4, r = i - j * n4;
+  const int b = list ? list[j] : j;
+  const int mx = (x0 + b % gw) * n4, my = (y0 + b / gw) * n4 + r;
+  if (my >= mi_rows) return;
+  const uint8_t sk = (uint8_t)win[b].skip;
+  for (int c = 0; c < n4 && mx + c < mi_cols; c++) {
+    lg[(int64_t)my * mi_stride + mx + c] = (uint8_t)(4 - level);
+    skip[(int64_t)my * mi_stride + mx + c] = sk;
+  }
+}
+
 // Levels checksum over the committed blocks of a list: sum of q *
 // (position in its transform block + 1), wrapping u64.
 __global__ void coeff_checksum_list(const int32_t *packed, const int32_t *list,
@@ -552,6 +580,10 @@ struct rv_replay {
     size_t woff = 0;  // result words offset
   } pl[kLevels];
   bool s6 = false;
+  bool deblock = false;           // RV_REPLAY_DEBLOCK
+  uint8_t *mi_lg = nullptr, *mi_skip = nullptr;  // the deblocking block map
+  int mi_stride = 0, mi_cols = 0, mi_rows = 0;
+  uint8_t db_level[3] = {0, 0, 0};  // fast level per pyramid level
   int32_t *leaf_count = nullptr;  // [kLevels]
   size_t nwords = 0, wpart = 0;   // result words; offset of the partition masks
   bool jobs_built = false;
@@ -1082,6 +1114,18 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
     }
   }
   r->words = (uint64_t *)dalloc(r, r->nwords * 8);
+  if (cfg->flags & RV_REPLAY_DEBLOCK) {
+    r->deblock = true;
+    r->mi_cols = (g.W + 3) / 4;
+    r->mi_rows = (g.H + 3) / 4;
+    r->mi_stride = (r->mi_cols + 15) / 16 * 16;
+    const size_t mb = (size_t)r->mi_stride * (r->mi_rows + 16);
+    r->mi_lg = (uint8_t *)dalloc(r, mb);
+    r->mi_skip = (uint8_t *)dalloc(r, mb);
+    ok = ok && r->mi_lg && r->mi_skip;
+    if (r->mi_lg) (void)hipMemsetAsync(r->mi_lg, 4, mb, r->stream);
+    if (r->mi_skip) (void)hipMemsetAsync(r->mi_skip, 0, mb, r->stream);
+  }
   r->imp_bx = g.vis_w / 8;
   r->imp_by = g.vis_h / 8;
   r->n_imp = r->imp_bx * r->imp_by;
@@ -1142,6 +1186,9 @@ int rv_replay_set_level_params(rv_replay *r, int level, const rv_replay_level_pa
                         &L.qs[l][c]));
   }
   L.qidx = p->base_q_idx;
+  // deblock_filter_optimize's fast levels (inter frames; speed 6 would search
+  // them by SSE, sse_optimize -- not built, the fast levels stand in)
+  r->db_level[level] = (uint8_t)rv_deblock_fast_level(rv_q_lookup(1, p->base_q_idx, bd), bd, 0);
   L.lambda = p->lambda;
   L.me_lambda = p->me_lambda;
   for (int i = 0; i < 3; i++) L.ds[i] = p->dist_scale[i];
@@ -1238,6 +1285,8 @@ int rv_replay_set_groups(rv_replay *r, int n_groups, const int32_t *rects, int m
   if (rects[4 * my_group] != g.tx0 || rects[4 * my_group + 1] != g.ty0 ||
       rects[4 * my_group + 2] != g.tw || rects[4 * my_group + 3] != g.th)
     return rv_set_error(RV_EINVAL, "rv_replay_set_groups: my group != the configured tile group");
+  if (r->deblock && n_groups > 1)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_groups: deblocking needs one tile group");
   memcpy(r->grects, rects, (size_t)n_groups * 4 * sizeof(int32_t));
   r->n_groups = n_groups;
   r->my_group = my_group;
@@ -1601,6 +1650,30 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                                      r->imp_by, r->tail + 2);
   }
   RV_EV(11);
+  // F7 deblock_filter_frame (src/encoder.rs:2789-2793) when enabled: the
+  // block map of the committed blocks, then Y, U, V in place
+  if (r->deblock) {
+    if (!r->s6) {
+      block_map_kernel<<<(g.nsb * 16 + 255) / 256, 256, 0, st>>>(
+          nullptr, nullptr, g.nsb, g.tw, g.tx0, g.ty0, 0, r->win, r->mi_lg, r->mi_skip,
+          r->mi_stride, r->mi_cols, r->mi_rows);
+    } else {
+      for (int l = 0; l < kLevels; l++) {
+        const rv_replay::PLevel &P = r->pl[l];
+        const int n4 = 16 >> l;
+        block_map_kernel<<<(P.n * n4 + 255) / 256, 256, 0, st>>>(
+            P.leaf, r->leaf_count + l, P.n, P.gw, l ? P.cg.tx0 : g.tx0, l ? P.cg.ty0 : g.ty0, l,
+            l ? P.win : r->win, r->mi_lg, r->mi_skip, r->mi_stride, r->mi_cols, r->mi_rows);
+      }
+    }
+    const uint8_t lv4[4] = {r->db_level[lv], r->db_level[lv], r->db_level[lv], r->db_level[lv]};
+    if (lv4[0]) {  // deblock_filter_frame runs when a luma level is non-zero
+      const rv_plane pls[3] = {S.y, S.u, S.v};
+      for (int p = 0; p < 3; p++)
+        RV_R(rv_deblock_plane_dev(&pls[p], p, g.W, g.H, r->mi_lg, r->mi_skip, r->mi_stride, lv4,
+                                  g.bd, st));
+    }
+  }
   // F7 the reconstruction becomes a reference
   r->coded++;
   r->last = fi;

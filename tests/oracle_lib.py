@@ -434,7 +434,8 @@ class CpuReplay:
     baseline_lib()[0])."""
 
     def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, group=None,
-                 tile_size=(0, 0), n_inputs=8, threads=1, L=None, quantizer=100, speed=10):
+                 tile_size=(0, 0), n_inputs=8, threads=1, L=None, quantizer=100, speed=10,
+                 deblock=False):
         from rav1e_amd import rate as RT
         L = L or lib()
         self.L = L
@@ -460,6 +461,8 @@ class CpuReplay:
         from rav1e_amd.replay import result_words
         L.orc_replay_set_speed.argtypes = [C.c_void_p, C.c_int]
         assert L.orc_replay_set_speed(self.h, speed) == 0, "orc_replay_set_speed"
+        L.orc_replay_set_deblock.argtypes = [C.c_void_p, C.c_int]
+        assert L.orc_replay_set_deblock(self.h, 1 if deblock else 0) == 0, "orc_replay_set_deblock"
         self.speed = speed
         self.n_words = result_words(width, height, n_refs, tw, th, tx0, ty0, speed)
         self.geom = (width, height, xdec, ydec, bit_depth)

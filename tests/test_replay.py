@@ -170,6 +170,26 @@ def test_cpu_tile_groups_equal_the_whole_frame():
             assert wg[-1] == ws[-1]  # every rank holds the whole reconstruction
 
 
+def test_cpu_replay_deblock_changes_the_reference():
+    """RV_REPLAY_DEBLOCK: the coded frame is deblocked before it becomes a
+    reference (the fast levels are non-zero at quantizer 100), so its
+    reconstruction -- and every later frame's words -- differ from the
+    undeblocked run; the searches of the first inter frame do not."""
+    w, h = 256, 128
+    fr = _frames(w, h, 1, 1, 8, 8)
+    outs, recs = [], []
+    for db in (False, True):
+        r = O.CpuReplay(w, h, 1, 1, 8, 2, n_inputs=8, threads=2, deblock=db)
+        for i, f in enumerate(fr):
+            r.set_input(i, f)
+        r.frame()
+        r.frame()
+        outs.append(_sb_words(r.results(), 8, 2))
+        recs.append(r.get_recon(4))
+    np.testing.assert_array_equal(outs[0][:, :2 * PER_REF], outs[1][:, :2 * PER_REF])
+    assert (recs[0] != recs[1]).any()
+
+
 def test_cpu_speed6_partition_and_levels():
     """Speed 6 (config D): thread-invariant words; the 64x64 words keep the
     speed-10 layout; every superblock's partition mask is a valid tree
@@ -228,7 +248,8 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
     g.synth_inputs(0)
     c = O.CpuReplay(w, h, xdec, ydec, bd, refs, tile_size=ts, n_inputs=nin,
                     threads=O.cpu_share(), quantizer=quantizer,
-                    speed=6 if flags & RP.RV_REPLAY_SPEED6 else 10)
+                    speed=6 if flags & RP.RV_REPLAY_SPEED6 else 10,
+                    deblock=bool(flags & RP.RV_REPLAY_DEBLOCK))
     for i in range(nin):
         c.set_input(i, g.get_input(i))
     if imp is not None:
@@ -257,6 +278,11 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
     (256, 200, 1, 1, 8, 2, None, RP.RV_REPLAY_SPEED6),      # speed 6: partition RDO
     (256, 136, 1, 1, 10, 2, None, RP.RV_REPLAY_SPEED6),
     (192, 128, 0, 0, 8, 2, {"tile_cols": 2}, RP.RV_REPLAY_SPEED6),
+    # deblocking before the reference write-back
+    (256, 200, 1, 1, 8, 2, None, RP.RV_REPLAY_DEBLOCK),
+    (192, 136, 0, 0, 10, 2, None, RP.RV_REPLAY_DEBLOCK),
+    (256, 200, 1, 1, 8, 2, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_SPEED6),
+    (192, 128, 0, 0, 12, 1, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_SPEED6),
 ])
 def test_gpu_replay_matches_cpu_replay(w, h, xdec, ydec, bd, refs, tiling, flags):
     _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, 10, tiling, flags)
