@@ -144,7 +144,7 @@ def timed_run(engine, group, steps, warmup, sync=None):
 
 
 def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling, n_inputs,
-                            speed=10):
+                            speed=10, flags=0):
     """The CPU baseline and the full-size parity check, from one CPU run.
 
     The CPU replay (oracle/orc_replay.c: the same schedule over the oracle's
@@ -162,8 +162,9 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     threads = O.cpu_share()
     ts = (tiling["tile_width_sb"], tiling["tile_height_sb"])
     nin = len(hip_inputs)
+    db = bool(flags & RP.RV_REPLAY_DEBLOCK)
     c = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=threads, L=L,
-                    speed=speed)
+                    speed=speed, deblock=db)
     for i in range(nin):
         c.set_input(i, hip_inputs[i])
     c.frame()  # the key frame (a copy), untimed
@@ -179,7 +180,7 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     nsb = ((W + 63) // 64) * ((H + 63) // 64)
     lim = max(1, nsb // 8)
     c1 = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=1, L=L,
-                     speed=speed)
+                     speed=speed, deblock=db)
     for i in range(nin):
         c1.set_input(i, hip_inputs[i])
     c1.frame()
@@ -200,7 +201,7 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
                                     f"scaled to whole frames"}}
     # the GPU replay over the same frames, word for word
     g = RP.HipReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=n_inputs,
-                     flags=RP.RV_REPLAY_SPEED6 if speed == 6 else 0)
+                     flags=flags & (RP.RV_REPLAY_SPEED6 | RP.RV_REPLAY_DEBLOCK))
     g.synth_inputs(0)
     g.frame()
     bad = []
@@ -230,6 +231,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--speed", type=int, choices=(6, 10), default=None,
                     help="schedule (default: the config's BASELINE speed)")
+    ap.add_argument("--deblock", action="store_true",
+                    help="deblock every coded frame before it becomes a reference (1 GPU)")
     ap.add_argument("--exhaustive-fs", action="store_true",
                     help="F1 coarse search without successive elimination (same results)")
     args = ap.parse_args()
@@ -251,7 +254,9 @@ def main():
     rects = RP.tile_groups(tiling, world)
     n_inputs = args.warmup + args.steps + 8  # every display the run codes
     flags = (RP.RV_REPLAY_EXHAUSTIVE_FS if args.exhaustive_fs else 0) | \
-        (RP.RV_REPLAY_SPEED6 if speed == 6 else 0)
+        (RP.RV_REPLAY_SPEED6 if speed == 6 else 0) | (RP.RV_REPLAY_DEBLOCK if args.deblock else 0)
+    if args.deblock and world > 1:
+        raise SystemExit("--deblock: one tile group (one GPU) only")
     hip = RP.HipReplay(W, H, xdec, ydec, bd, nref, group=rects[rank], tile_size=ts,
                        n_inputs=n_inputs, flags=flags)
     hip.synth_inputs(0)  # the stream's frames, resident in HBM before the timing
@@ -349,7 +354,7 @@ def main():
         inputs = [hip.get_input(i) for i in range(min(22, n_inputs))]
         hip.close()  # the parity pass below builds a fresh GPU replay
         cpu, parity = cpu_baseline_and_parity(args, inputs, W, H, xdec, ydec, bd, nref,
-                                              tiling, n_inputs, speed)
+                                              tiling, n_inputs, speed, flags)
 
     if rank == 0:
         line = {
@@ -364,6 +369,7 @@ def main():
                                    f"{tiling['cols']}x{tiling['rows']} tiles over {world} GPU(s), "
                                    f"{nref} refs, reorder-pyramid coding order",
                        "width": W, "height": H, "refs": nref, "speed": speed,
+                       "deblock": bool(args.deblock),
                        "tiles": [tiling["cols"], tiling["rows"]],
                        "parallelism": f"tile-groups{world}",
                        "candidates_per_sb": f"{4 * nref} inter modes x (skip, non-skip)",
