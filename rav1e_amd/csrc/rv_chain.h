@@ -204,4 +204,29 @@ __host__ __device__ inline bool cand_mv(const CandGeo &g, const rv_fs_result *su
   }
 }
 
+// A candidate whose reference and MV (compound: MV pair) repeat an earlier
+// pushed one of the same block predicts, distorts and costs exactly the
+// same, so it can never win the strict-`<` argmin after that one (skip or
+// non-skip): it is evaluated once, as the first.  cand_live / comp_live:
+// pushed and not such a repeat.
+__host__ __device__ inline bool cand_live(const CandGeo &g, const rv_fs_result *sub, int sb, int c,
+                                          rv_mv *mv) {
+  if (!cand_mv(g, sub, sb, c, mv)) return false;
+  for (int c2 = (c / g.M) * g.M; c2 < c; c2++) {
+    rv_mv m2;
+    if (cand_mv(g, sub, sb, c2, &m2) && mv_eq(m2, *mv)) return false;
+  }
+  return true;
+}
+__host__ __device__ inline bool comp_live(const CandGeo &g, const rv_fs_result *sub, int sb, int m) {
+  rv_mv a0, a1;
+  comp_mvs(g, sub, sb, m, &a0, &a1);
+  for (int m2 = 0; m2 < m; m2++) {
+    rv_mv b0, b1;
+    comp_mvs(g, sub, sb, m2, &b0, &b1);
+    if (mv_eq(a0, b0) && mv_eq(a1, b1)) return false;
+  }
+  return true;
+}
+
 }  // namespace rv

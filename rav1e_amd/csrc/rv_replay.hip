@@ -165,7 +165,7 @@ __device__ inline RdoWinner block_argmin(const CandGeo &cg, double lambda, doubl
   const int ns = cg.R * cg.M;  // single-reference candidates; compound ones follow
   for (int c = 0; c < ns + cg.comp; c++) {
     rv_mv mv;
-    if (c < ns && !cand_mv(cg, sub, sb, c, &mv)) continue;
+    if (c < ns ? !cand_live(cg, sub, sb, c, &mv) : !comp_live(cg, sub, sb, c - ns)) continue;
     const int64_t o = (int64_t)c * cg.nsb + sb;
     uint64_t su = 0, sv = 0, nu = 0, nv = 0;
     uint32_t rate = (uint32_t)lout[o * 3 + 2];
@@ -204,10 +204,10 @@ __global__ __launch_bounds__(64) void score_candidates(
     const rv_fs_result *look, uint64_t *words, int32_t *cand_count,
     unsigned long long *imp_sum, uint32_t *evals, int32_t *leaf_count) {
   const int sb = blockIdx.x * 64 + threadIdx.x;
-  if (sb == 0) {  // F4's list is consumed: ready for the next frame; F5 sums next
-    evals[0] = (uint32_t)*cand_count;  // single-reference candidates evaluated
-    evals[1] = (uint32_t)(cg.comp * g.nsb);  // compound ones
-    *cand_count = 0;
+  if (sb == 0) {  // F4's lists are consumed: ready for the next frame; F5 sums next
+    evals[0] = (uint32_t)cand_count[0];  // single-reference candidates evaluated
+    evals[1] = (uint32_t)cand_count[1];  // compound ones
+    cand_count[0] = cand_count[1] = 0;
     *imp_sum = 0;
     if (leaf_count)  // speed 6: the partition decision appends next
       for (int l = 0; l < 4; l++) leaf_count[l] = 0;
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void cand_list_kernel(CandGeo cg, const rv_fs_
   if (i < n) {
     rv_mv mv;
     const int c = i / cg.nsb, sb = i - c * cg.nsb;
-    v = cand_mv(cg, sub, sb, c, &mv);
+    v = cand_live(cg, sub, sb, c, &mv);
   }
   const uint64_t m = __ballot(v);
   const int lane = threadIdx.x & 63;
@@ -277,6 +277,23 @@ __global__ __launch_bounds__(256) void cand_list_kernel(CandGeo cg, const rv_fs_
   if (lane == 0 && m) base = atomicAdd(count, (int)__popcll(m));
   base = __shfl(base, 0, 64);
   if (v) list[base + __popcll(m & ((1ull << lane) - 1))] = i;
+}
+// The compound candidates (all pushed on SELECT frames) without repeated
+// MV pairs: entries are absolute candidate indices nsingle + m * nsb + sb.
+__global__ __launch_bounds__(256) void comp_list_kernel(CandGeo cg, const rv_fs_result *sub,
+                                                         int nsingle, int32_t *list, int32_t *count) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  bool v = false;
+  if (i < cg.comp * cg.nsb) {
+    const int mm = i / cg.nsb, sb = i - mm * cg.nsb;
+    v = comp_live(cg, sub, sb, mm);
+  }
+  const uint64_t m = __ballot(v);
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == 0 && m) base = atomicAdd(count, (int)__popcll(m));
+  base = __shfl(base, 0, 64);
+  if (v) list[base + __popcll(m & ((1ull << lane) - 1))] = nsingle + i;
 }
 
 // F5: get_satd of every 8x8 luma block of the group inside the frame
@@ -387,9 +404,9 @@ __global__ __launch_bounds__(64) void score_level(CandGeo cg, double lambda, dou
                                                   int32_t *cand_count, uint32_t *evals) {
   const int b = blockIdx.x * 64 + threadIdx.x;
   if (b == 0) {
-    evals[0] = (uint32_t)*cand_count;
-    evals[1] = (uint32_t)(cg.comp * cg.nsb);
-    *cand_count = 0;
+    evals[0] = (uint32_t)cand_count[0];
+    evals[1] = (uint32_t)cand_count[1];
+    cand_count[0] = cand_count[1] = 0;
   }
   if (b >= cg.nsb) return;
   const RdoWinner w = block_argmin(cg, lambda, ds_u, ds_v, sub, lout, uout, vout, 1, b);
@@ -1050,11 +1067,11 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   r->c_out = (uint64_t *)dalloc(r, (size_t)nc * r->ntx_c * 3 * 8 * 2);
   r->win = (RdoWinner *)dalloc(r, (size_t)g.nsb * sizeof(RdoWinner));
   r->cand_list = (int32_t *)dalloc(r, (size_t)nc * 4);
-  r->cand_count = (int32_t *)dalloc(r, 4);
+  r->cand_count = (int32_t *)dalloc(r, 8);  // [single, compound]
   r->cand_evals = (uint32_t *)dalloc(r, rv_replay::kRing * 2 * kLevels * 4);
   if (r->cand_evals)
     (void)hipMemsetAsync(r->cand_evals, 0, rv_replay::kRing * 2 * kLevels * 4, r->stream);
-  if (r->cand_count) (void)hipMemsetAsync(r->cand_count, 0, 4, r->stream);
+  if (r->cand_count) (void)hipMemsetAsync(r->cand_count, 0, 8, r->stream);
   r->l_lev = (int32_t *)dalloc(r, (size_t)g.nsb * 1024 * 4);
   r->c_lev = (int32_t *)dalloc(r, (size_t)g.nsb * r->ntx_c * 1024 * 4 * 2);
   r->nwords = (size_t)g.nsb * (kWordsPerRef * g.R + 4);
@@ -1090,12 +1107,12 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
       P.c_out = (uint64_t *)dalloc(r, (size_t)nc * 3 * 8 * 2);
       P.win = (RdoWinner *)dalloc(r, (size_t)P.n * sizeof(RdoWinner));
       P.cand_list = (int32_t *)dalloc(r, (size_t)nc * 4);
-      P.cand_count = (int32_t *)dalloc(r, 4);
+      P.cand_count = (int32_t *)dalloc(r, 8);
       P.l_lev = (int32_t *)dalloc(r, (size_t)P.n * P.B * P.B * 4);
       P.c_lev = (int32_t *)dalloc(r, (size_t)P.n * P.bc * P.bch * 4 * 2);
       ok = ok && P.full && P.sub && P.l_out && P.c_out && P.win && P.cand_list && P.cand_count &&
            P.l_lev && P.c_lev;
-      if (P.cand_count) (void)hipMemsetAsync(P.cand_count, 0, 4, r->stream);
+      if (P.cand_count) (void)hipMemsetAsync(P.cand_count, 0, 8, r->stream);
       if (P.l_lev) (void)hipMemsetAsync(P.l_lev, 0, (size_t)P.n * P.B * P.B * 4, r->stream);
       if (P.c_lev) (void)hipMemsetAsync(P.c_lev, 0, (size_t)P.n * P.bc * P.bch * 8, r->stream);
       P.woff = r->nwords;
@@ -1468,6 +1485,18 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     const int ns = P.n * g.R * g.M;
     cand_list_kernel<<<(ns + 255) / 256, 256, 0, st>>>(P.cg, P.sub, ns, P.cand_list, P.cand_count);
   }
+  if (cg.comp) {  // the compound lists (after the single ones in the same arrays)
+    comp_list_kernel<<<(g.nsb * cg.comp + 255) / 256, 256, 0, st>>>(
+        cg, r->sub, nsingle, r->cand_list + nsingle, r->cand_count + 1);
+    for (int l = 1; r->s6 && l < kLevels; l++) {
+      rv_replay::PLevel &P = r->pl[l];
+      CandGeo cgl = P.cg;
+      cgl.comp = cg.comp;
+      const int ns = P.n * g.R * g.M;
+      comp_list_kernel<<<(P.n * cg.comp + 255) / 256, 256, 0, st>>>(
+          cgl, P.sub, ns, P.cand_list + ns, P.cand_count + 1);
+    }
+  }
   RV_EV(6);
   // F4 every valid candidate, luma + both chroma planes in one fused launch
   RdoArgs la, ca;
@@ -1567,11 +1596,11 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, st, 0));
     RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, st, 0));
   }
-  if (cg.comp) {  // the compound candidates: every one is pushed, no list
+  if (cg.comp) {  // the compound candidates (all pushed), distinct MV pairs from the list
     RdoArgs lc = la, cc = ca;
-    lc.list = cc.list = nullptr;
-    lc.count = cc.count = nullptr;
-    lc.cand_base = cc.cand_base = nsingle;
+    lc.list = cc.list = r->cand_list + nsingle;
+    lc.count = cc.count = r->cand_count + 1;
+    lc.cand_base = cc.cand_base = 0;
     lc.n_tx = g.nsb * cg.comp;
     cc.n_tx = g.nsb * cg.comp * ntx_c;
     RV_EV(7);
@@ -1579,9 +1608,9 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     for (int l = 1; r->s6 && l < kLevels; l++) {
       const rv_replay::PLevel &P = r->pl[l];
       RdoArgs a = ll[l], c = lc6[l];
-      a.list = c.list = nullptr;
-      a.count = c.count = nullptr;
-      a.cand_base = c.cand_base = P.n * g.R * g.M;
+      a.list = c.list = P.cand_list + P.n * g.R * g.M;
+      a.count = c.count = P.cand_count + 1;
+      a.cand_base = c.cand_base = 0;
       a.n_tx = c.n_tx = P.n * cg.comp;
       RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, st, 1));
       RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, st, 1));
