@@ -232,7 +232,7 @@ def main():
     ap.add_argument("--speed", type=int, choices=(6, 10), default=None,
                     help="schedule (default: the config's BASELINE speed)")
     ap.add_argument("--deblock", action="store_true",
-                    help="deblock every coded frame before it becomes a reference (1 GPU)")
+                    help="deblock every coded frame before it becomes a reference")
     ap.add_argument("--exhaustive-fs", action="store_true",
                     help="F1 coarse search without successive elimination (same results)")
     args = ap.parse_args()
@@ -255,8 +255,6 @@ def main():
     n_inputs = args.warmup + args.steps + 8  # every display the run codes
     flags = (RP.RV_REPLAY_EXHAUSTIVE_FS if args.exhaustive_fs else 0) | \
         (RP.RV_REPLAY_SPEED6 if speed == 6 else 0) | (RP.RV_REPLAY_DEBLOCK if args.deblock else 0)
-    if args.deblock and world > 1:
-        raise SystemExit("--deblock: one tile group (one GPU) only")
     hip = RP.HipReplay(W, H, xdec, ydec, bd, nref, group=rects[rank], tile_size=ts,
                        n_inputs=n_inputs, flags=flags)
     hip.synth_inputs(0)  # the stream's frames, resident in HBM before the timing

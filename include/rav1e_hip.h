@@ -466,7 +466,9 @@ typedef struct rv_replay_cfg {
 #define RV_REPLAY_SPEED6 8
 /* flags: deblock every coded frame before it becomes a reference
  * (deblock_filter_optimize's fast levels + deblock_filter_frame,
- * src/encoder.rs:2789-2793); one tile group only. */
+ * src/encoder.rs:2789-2793).  With several tile groups the exchange
+ * also carries each group's block map (log2 block size and skip per luma
+ * 4x4) and every group deblocks the whole frame after the import. */
 #define RV_REPLAY_DEBLOCK 16
 typedef struct rv_replay_frame_info {
   int32_t display;            /* display index of the coded frame */

@@ -410,7 +410,6 @@ int orc_replay_set_speed(orc_replay *r, int speed) {
 int orc_replay_set_deblock(orc_replay *r, int on) {
   r->deblock = on != 0;
   if (!r->deblock) return 0;
-  if (r->tx0 || r->ty0 || r->tw * SB < r->W || r->th * SB < r->H) return -1;
   r->mi_cols = (r->W + 3) / 4;
   r->mi_rows = (r->H + 3) / 4;
   free(r->mi_lg);
@@ -430,9 +429,8 @@ static void map_block(orc_replay *r, int l, int gx, int gy, int skip) {
     }
 }
 
-/* deblock_filter_optimize's fast levels + deblock_filter_frame
- * (src/encoder.rs:2789-2793) of the frame just coded */
-static void deblock_frame(orc_replay *r) {
+/* the block map of this group's committed blocks */
+static void map_own(orc_replay *r) {
   const int R = r->R;
   for (int sb = 0; sb < r->nsb; sb++) {
     const int sx = sb % r->tw, sy = sb / r->tw;
@@ -447,6 +445,12 @@ static void deblock_frame(orc_replay *r) {
         map_block(r, l, P->tx0 + b % P->gw, P->ty0 + b / P->gw,
                   (int)r->words[P->woff + (size_t)b * (4 * R + 4) + 4 * R + 1]);
   }
+}
+
+/* deblock_filter_optimize's fast levels + deblock_filter_frame
+ * (src/encoder.rs:2789-2793) of the frame just coded (the whole frame: its
+ * block map must be complete) */
+static void deblock_planes(orc_replay *r) {
   const int qidx = r->lv[r->fi.level].qidx;
   const uint8_t lv = (uint8_t)orc_deblock_fast_level(orc_ac_q(qidx, 0, r->bd), r->bd, 0);
   if (!lv) return;
@@ -1290,7 +1294,10 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
   memset(r->tail, 0, sizeof(r->tail));
   r->sb_limit = sb_limit;
   for (int pass = 0; pass < 4; pass++) run_pass(r, pass);
-  if (r->deblock) deblock_frame(r);
+  if (r->deblock) {
+    map_own(r);
+    if (pad_recon) deblock_planes(r);  /* tile groups: after the imports */
+  }
   r->tail[3] = (uint64_t)(r->vis_w / 8) * (r->vis_h / 8);
   if (pad_recon) {
     pad(r, &S->y);
@@ -1335,12 +1342,30 @@ int64_t orc_replay_xcopy(orc_replay *r, const int32_t *gr, void *buf, int to_buf
       off += (int64_t)rc[2] * px;
     }
   }
+  if (r->deblock) { /* the group's rows of the block map: log2 sizes, skip flags */
+    const int x0 = gr[0] * 16, y0 = gr[1] * 16;
+    const int x1 = (gr[0] + gr[2]) * 16 < r->mi_cols ? (gr[0] + gr[2]) * 16 : r->mi_cols;
+    const int y1 = (gr[1] + gr[3]) * 16 < r->mi_rows ? (gr[1] + gr[3]) * 16 : r->mi_rows;
+    uint8_t *maps[2] = {r->mi_lg, r->mi_skip};
+    for (int m = 0; m < 2; m++)
+      for (int y = y0; y < y1; y++) {
+        uint8_t *q = maps[m] + (size_t)y * r->mi_cols + x0;
+        if (b) {
+          if (to_buf)
+            memcpy(b + off, q, (size_t)(x1 - x0));
+          else
+            memcpy(q, b + off, (size_t)(x1 - x0));
+        }
+        off += x1 - x0;
+      }
+  }
   return off;
 }
 
 /* Pad the last coded frame (after every group's region is in). */
 void orc_replay_pad_recon(orc_replay *r) {
   oslot *s = &r->slots[r->fi.display % NSLOT];
+  if (r->deblock && !r->fi.is_key) deblock_planes(r);
   pad(r, &s->y);
   pad(r, &s->u);
   pad(r, &s->v);

@@ -352,7 +352,7 @@ struct XRect {
 };
 struct XArgs {
   rv_plane pl[3];
-  XRect rect[3 * kMaxGroups];
+  XRect rect[3 * kMaxGroups];  // pixel rectangles (or block-map ones, bytewise)
   int n;
   int to_plane;  // 1: buffer -> planes (unpack), 0: planes -> buffer (pack)
   uint8_t *buf;
@@ -883,9 +883,11 @@ int build_static_jobs(rv_replay *r) {
   return RV_OK;
 }
 
-// Packed rectangles of group k (its visible Y, U, V region), bytes into the
-// group's slice of the exchange buffer.
-int group_rects(const rv_replay *r, int k, XRect out[3]) {
+// Packed rectangles of group k (its visible Y, U, V region; with
+// deblocking also its rows of the block map, planes 3 = log2 size, 4 =
+// skip), bytes into the group's slice of the exchange buffer.  Returns the
+// bytes; *n = the rectangles.
+int group_rects(const rv_replay *r, int k, XRect out[5], int *n) {
   const Geo &g = r->g;
   const int32_t *gr = r->grects + 4 * k;
   const int px = g.hbd ? 2 : 1;
@@ -901,16 +903,28 @@ int group_rects(const rv_replay *r, int k, XRect out[3]) {
     out[p] = XRect{off, p, x0, y0, x1 - x0, y1 - y0};
     off += (int64_t)(x1 - x0) * (y1 - y0) * px;
   }
+  *n = 3;
+  if (r->deblock) {
+    const int x0 = gr[0] * 16, y0 = gr[1] * 16;
+    int x1 = (gr[0] + gr[2]) * 16, y1 = (gr[1] + gr[3]) * 16;
+    x1 = x1 < r->mi_cols ? x1 : r->mi_cols;
+    y1 = y1 < r->mi_rows ? y1 : r->mi_rows;
+    for (int m = 0; m < 2; m++) {
+      out[3 + m] = XRect{off, 3 + m, x0, y0, x1 - x0, y1 - y0};
+      off += (int64_t)(x1 - x0) * (y1 - y0);
+    }
+    *n = 5;
+  }
   return (int)off;
 }
 
-int xcopy(rv_replay *r, const RvSlot &s, const XRect *rects, int n, int to_plane, uint8_t *buf) {
-  if (n == 0) return RV_OK;
+template <typename Px>
+static void xcopy_launch(hipStream_t st, const rv_plane *pl, const XRect *rects, int n,
+                         int to_plane, uint8_t *buf) {
+  if (n == 0) return;
   XArgs a;
   memset(&a, 0, sizeof(a));
-  a.pl[0] = s.y;
-  a.pl[1] = s.u;
-  a.pl[2] = s.v;
+  for (int p = 0; p < 3; p++) a.pl[p] = pl[p];
   int64_t most = 0;
   for (int i = 0; i < n; i++) {
     a.rect[i] = rects[i];
@@ -922,11 +936,39 @@ int xcopy(rv_replay *r, const RvSlot &s, const XRect *rects, int n, int to_plane
   a.buf = buf;
   int64_t gx = (most + 255) / 256;
   gx = gx > 4096 ? 4096 : gx < 1 ? 1 : gx;
-  dim3 grid((unsigned)gx, (unsigned)n);
+  xcopy_kernel<Px><<<dim3((unsigned)gx, (unsigned)n), 256, 0, st>>>(a);
+}
+
+// Copy rectangles between the slot's planes / the block map and a packed
+// buffer (pixel rectangles at the pixel width, map rectangles bytewise).
+int xcopy(rv_replay *r, const RvSlot &s, const XRect *rects, int n, int to_plane, uint8_t *buf) {
+  XRect px[3 * kMaxGroups], mp[2 * kMaxGroups];
+  int npx = 0, nmp = 0;
+  for (int i = 0; i < n; i++) {
+    if (rects[i].plane < 3) {
+      px[npx++] = rects[i];
+    } else {
+      mp[nmp] = rects[i];
+      mp[nmp++].plane -= 3;
+    }
+  }
+  const rv_plane pl[3] = {s.y, s.u, s.v};
   if (r->g.hbd)
-    xcopy_kernel<uint16_t><<<grid, 256, 0, r->stream>>>(a);
+    xcopy_launch<uint16_t>(r->stream, pl, px, npx, to_plane, buf);
   else
-    xcopy_kernel<uint8_t><<<grid, 256, 0, r->stream>>>(a);
+    xcopy_launch<uint8_t>(r->stream, pl, px, npx, to_plane, buf);
+  if (nmp) {
+    rv_plane m[3];
+    memset(m, 0, sizeof(m));
+    m[0].data = r->mi_lg;
+    m[1].data = r->mi_skip;
+    for (int i = 0; i < 2; i++) {
+      m[i].stride = r->mi_stride;
+      m[i].width = r->mi_cols;
+      m[i].height = r->mi_rows;
+    }
+    xcopy_launch<uint8_t>(r->stream, m, mp, nmp, to_plane, buf);
+  }
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }
@@ -936,6 +978,21 @@ int pad_slot(rv_replay *r, const RvSlot &s) {
   if ((e = rv_plane_pad(&s.y, r->stream)) || (e = rv_plane_pad(&s.u, r->stream)) ||
       (e = rv_plane_pad(&s.v, r->stream)))
     return e;
+  return RV_OK;
+}
+
+// deblock_filter_frame of a slot with pyramid level lv's fast levels; it
+// runs when a luma level is non-zero (src/encoder.rs:2790-2793)
+int deblock_slot(rv_replay *r, const RvSlot &s, int lv) {
+  const uint8_t l = r->db_level[lv];
+  if (!l) return RV_OK;
+  const uint8_t lv4[4] = {l, l, l, l};
+  const rv_plane pls[3] = {s.y, s.u, s.v};
+  for (int p = 0; p < 3; p++) {
+    const int e = rv_deblock_plane_dev(&pls[p], p, r->g.W, r->g.H, r->mi_lg, r->mi_skip,
+                                       r->mi_stride, lv4, r->g.bd, r->stream);
+    if (e != RV_OK) return e;
+  }
   return RV_OK;
 }
 
@@ -1302,15 +1359,14 @@ int rv_replay_set_groups(rv_replay *r, int n_groups, const int32_t *rects, int m
   if (rects[4 * my_group] != g.tx0 || rects[4 * my_group + 1] != g.ty0 ||
       rects[4 * my_group + 2] != g.tw || rects[4 * my_group + 3] != g.th)
     return rv_set_error(RV_EINVAL, "rv_replay_set_groups: my group != the configured tile group");
-  if (r->deblock && n_groups > 1)
-    return rv_set_error(RV_EINVAL, "rv_replay_set_groups: deblocking needs one tile group");
   memcpy(r->grects, rects, (size_t)n_groups * 4 * sizeof(int32_t));
   r->n_groups = n_groups;
   r->my_group = my_group;
   size_t most = 0;
   for (int k = 0; k < n_groups; k++) {
-    XRect xr[3];
-    const size_t b = (size_t)group_rects(r, k, xr);
+    XRect xr[5];
+    int nx;
+    const size_t b = (size_t)group_rects(r, k, xr, &nx);
     most = b > most ? b : most;
   }
   r->xbytes = (most + 255) / 256 * 256;
@@ -1340,18 +1396,22 @@ int rv_replay_import(rv_replay *r) {
   // one group, or the key frame (every rank copied its own input): nothing to move
   if (r->n_groups < 2 || r->last.is_key) return RV_OK;
   const RvSlot &s = r->slots[r->last.display % kSlots];
-  XRect rects[3 * kMaxGroups];
+  XRect rects[5 * kMaxGroups];
   int n = 0;
   for (int k = 0; k < r->n_groups; k++) {
     if (k == r->my_group) continue;
-    XRect xr[3];
-    group_rects(r, k, xr);
-    for (int p = 0; p < 3; p++) {
+    XRect xr[5];
+    int nx;
+    group_rects(r, k, xr, &nx);
+    for (int p = 0; p < nx; p++) {
       xr[p].off += (int64_t)k * (int64_t)r->xbytes;
       rects[n++] = xr[p];
     }
   }
   RV_R(xcopy(r, s, rects, n, 1, r->xrecv));
+  // the whole frame and its block map are in: deblock it (every rank the
+  // same way), then pad
+  if (r->deblock) RV_R(deblock_slot(r, s, r->last.level));
   return pad_slot(r, s);
 }
 
@@ -1680,7 +1740,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   }
   RV_EV(11);
   // F7 deblock_filter_frame (src/encoder.rs:2789-2793) when enabled: the
-  // block map of the committed blocks, then Y, U, V in place
+  // block map of the committed blocks, then (once every group's pixels and
+  // map are in) Y, U, V in place; the reconstruction becomes a reference
   if (r->deblock) {
     if (!r->s6) {
       block_map_kernel<<<(g.nsb * 16 + 255) / 256, 256, 0, st>>>(
@@ -1695,23 +1756,17 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
             l ? P.win : r->win, r->mi_lg, r->mi_skip, r->mi_stride, r->mi_cols, r->mi_rows);
       }
     }
-    const uint8_t lv4[4] = {r->db_level[lv], r->db_level[lv], r->db_level[lv], r->db_level[lv]};
-    if (lv4[0]) {  // deblock_filter_frame runs when a luma level is non-zero
-      const rv_plane pls[3] = {S.y, S.u, S.v};
-      for (int p = 0; p < 3; p++)
-        RV_R(rv_deblock_plane_dev(&pls[p], p, g.W, g.H, r->mi_lg, r->mi_skip, r->mi_stride, lv4,
-                                  g.bd, st));
-    }
   }
-  // F7 the reconstruction becomes a reference
   r->coded++;
   r->last = fi;
   if (r->n_groups < 2) {
+    if (r->deblock) RV_R(deblock_slot(r, S, lv));
     RV_R(pad_slot(r, S));
   } else {
-    XRect xr[3];
-    group_rects(r, r->my_group, xr);
-    RV_R(xcopy(r, S, xr, 3, 0, r->xsend));
+    XRect xr[5];
+    int nx;
+    group_rects(r, r->my_group, xr, &nx);
+    RV_R(xcopy(r, S, xr, nx, 0, r->xsend));
     if (r->comm) {
 #if RV_HAVE_RCCL
       if (ncclAllGather(r->xsend, r->xrecv, r->xbytes, ncclUint8, (ncclComm_t)r->comm, st) !=

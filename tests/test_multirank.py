@@ -9,6 +9,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 from rav1e_amd import replay as RP
@@ -30,11 +31,12 @@ def _tiling():
     return t, (t["tile_width_sb"], t["tile_height_sb"])
 
 
-def _single_words(frames):
+def _single_words(frames, deblock=False):
     from rav1e_amd import replay as RP
     from tests import oracle_lib as O
     _, ts = _tiling()
-    c = O.CpuReplay(W, H, 1, 1, 8, REFS, tile_size=ts, n_inputs=NIN, threads=2)
+    c = O.CpuReplay(W, H, 1, 1, 8, REFS, tile_size=ts, n_inputs=NIN, threads=2,
+                    deblock=deblock)
     for i in range(NIN):
         c.set_input(i, RP.synth_frame(W, H, i))
     for _ in range(frames):
@@ -44,7 +46,7 @@ def _single_words(frames):
     return w
 
 
-def _rank_main(rank, world, port, q):
+def _rank_main(rank, world, port, q, deblock):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import bench
@@ -56,7 +58,7 @@ def _rank_main(rank, world, port, q):
     t, ts = _tiling()
     rects = RP.tile_groups(t, world)
     c = O.CpuReplay(W, H, 1, 1, 8, REFS, group=rects[rank], tile_size=ts, n_inputs=NIN,
-                    threads=2)
+                    threads=2, deblock=deblock)
     for i in range(NIN):
         c.set_input(i, RP.synth_frame(W, H, i))
     if rank == 1:  # make rank 1 the slow one: the reported time must be its
@@ -74,11 +76,14 @@ def _rank_main(rank, world, port, q):
     g.close()
 
 
-def test_two_rank_gloo_tile_parallel_stream():
+@pytest.mark.parametrize("deblock", [False, True])
+def test_two_rank_gloo_tile_parallel_stream(deblock):
+    """With deblock the exchange also carries the block maps and each rank
+    deblocks the whole frame."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q, deblock)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -90,7 +95,7 @@ def test_two_rank_gloo_tile_parallel_stream():
         assert p.exitcode == 0
     # max over ranks: both report the slow rank's time (>= 4 sleeps)
     assert abs(res[0][0] - res[1][0]) < 1e-9 and res[0][0] >= 0.2
-    single = _single_words(6)
+    single = _single_words(6, deblock)
     per = RP.sb_words_per(REFS)
     sbc = (W + 63) // 64
     sw = single[: len(single) - 5].reshape(-1, per)

@@ -133,9 +133,11 @@ def test_cpu_replay_importance_bias():
     assert (cost[1] >= cost[0]).all() and (cost[1] > cost[0]).any()
 
 
-def test_cpu_tile_groups_equal_the_whole_frame():
+@pytest.mark.parametrize("deblock,speed", [(False, 10), (True, 10), (True, 6)])
+def test_cpu_tile_groups_equal_the_whole_frame(deblock, speed):
     """Two tile groups coded separately and exchanging their
-    reconstructions reproduce the single-instance run of the same tiling,
+    reconstructions (with deblocking: and their block maps, each deblocking
+    the whole frame) reproduce the single-instance run of the same tiling,
     superblock for superblock (tiles are independent, src/encoder.rs:
     2772-2781)."""
     w, h = 384, 192
@@ -143,8 +145,9 @@ def test_cpu_tile_groups_equal_the_whole_frame():
     t = RP.tiling_for(w, h, tile_cols=2)
     ts = (t["tile_width_sb"], t["tile_height_sb"])
     rects = RP.tile_groups(t, 2)
-    single = O.CpuReplay(w, h, n_inputs=10, threads=2, tile_size=ts)
-    gs = [O.CpuReplay(w, h, n_inputs=10, threads=2, group=r, tile_size=ts) for r in rects]
+    kw = dict(n_inputs=10, threads=2, tile_size=ts, deblock=deblock, speed=speed)
+    single = O.CpuReplay(w, h, **kw)
+    gs = [O.CpuReplay(w, h, group=r, **kw) for r in rects]
     for e in [single] + gs:
         for i, f in enumerate(fr):
             e.set_input(i, f)
@@ -160,7 +163,8 @@ def test_cpu_tile_groups_equal_the_whole_frame():
                     g.import_(r, bufs[j])
             g.pad_recon()
         ws = single.results()
-        sw = _sb_words(ws, len(ws) // RP.sb_words_per(2), 2)
+        nsb = ((w + 63) // 64) * ((h + 63) // 64)
+        sw = _sb_words(ws, nsb, 2)
         for g, (x0, y0, gw_, gh_) in zip(gs, rects):
             wg = g.results()
             gsb = _sb_words(wg, gw_ * gh_, 2)
@@ -298,10 +302,12 @@ def test_gpu_replay_importance_bias_and_quantizer(flags):
 
 
 @pytest.mark.gpu
-def test_gpu_tile_groups_exchange():
-    """Two GPU tile groups in one process, exchanging reconstructions
-    through their device exchange buffers (the RCCL all-gather's layout),
-    reproduce the CPU replay of the whole frame."""
+@pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_DEBLOCK,
+                                   RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_SPEED6])
+def test_gpu_tile_groups_exchange(flags):
+    """Two GPU tile groups in one process, exchanging reconstructions (with
+    deblocking: and block maps) through their device exchange buffers (the
+    RCCL all-gather's layout), reproduce the CPU replay of the whole frame."""
     import ctypes as C
 
     import rav1e_amd as R
@@ -310,11 +316,13 @@ def test_gpu_tile_groups_exchange():
     t = RP.tiling_for(w, h, tile_cols=2)
     ts = (t["tile_width_sb"], t["tile_height_sb"])
     rects = RP.tile_groups(t, 2)
-    gs = [RP.HipReplay(w, h, group=r, tile_size=ts, n_inputs=14) for r in rects]
+    gs = [RP.HipReplay(w, h, group=r, tile_size=ts, n_inputs=14, flags=flags) for r in rects]
     for k, g in enumerate(gs):
         g.synth_inputs(0)
         g.set_groups(rects, k, None)
-    c = O.CpuReplay(w, h, tile_size=ts, n_inputs=14, threads=4)
+    c = O.CpuReplay(w, h, tile_size=ts, n_inputs=14, threads=4,
+                    deblock=bool(flags & RP.RV_REPLAY_DEBLOCK),
+                    speed=6 if flags & RP.RV_REPLAY_SPEED6 else 10)
     for i in range(14):
         c.set_input(i, RP.synth_frame(w, h, i))
     L = R.lib()
@@ -334,7 +342,7 @@ def test_gpu_tile_groups_exchange():
         for g in gs:
             g.import_()
         cw = c.results()
-        sw = _sb_words(cw, len(cw) // RP.sb_words_per(2), 2)
+        sw = _sb_words(cw, ((w + 63) // 64) * ((h + 63) // 64), 2)
         for g, (x0, y0, gw_, gh_) in zip(gs, rects):
             wg = g.results()
             gsb = _sb_words(wg, gw_ * gh_, 2)
