@@ -1033,6 +1033,16 @@ __global__ __launch_bounds__(64) void ds_wave_kernel(DsArgs a) {
 // the rounds' load latency better than one job per wavefront (FL, F2:
 // 0.24 -> 0.13 ms at 2160p).  (Sub-pel tried the same, and a window staged
 // in LDS per round: both slower, the sub-pel search is VALU-bound.)
+typedef short rv_s16x2 __attribute__((ext_vector_type(2)));
+// a.lo * b.lo + a.hi * b.hi + c over packed i16 halves (v_dot2_i32_i16)
+__device__ __forceinline__ int32_t sdot2(uint32_t a, uint32_t b, int32_t c) {
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(rv_s16x2, a), __builtin_bit_cast(rv_s16x2, b),
+                                c, false);
+}
+__device__ __forceinline__ uint32_t pk16(int lo, int hi) {
+  return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16);
+}
+
 template <int N, bool SADONLY>
 struct GrpGeo {
   static constexpr int C = N == 8 || (SADONLY && N == 16) ? 4 : 16;  // lanes per candidate
@@ -1044,7 +1054,7 @@ struct GrpGeo {
 };
 
 template <typename Px, int N, bool SUB, bool SATD>
-__global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
+__device__ __forceinline__ void ds_grp_body(const DsArgs &a) {
   using G = GrpGeo<N, !SUB && !SATD>;
   static_assert(G::CPL >= 1 && G::C % G::LPC == 0, "lane layout");
   const int lane = threadIdx.x & 63;
@@ -1061,7 +1071,7 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
   const int lic = c % G::LPC;  // lane in chunk
 
   // distortion of candidate mv for this subgroup (all lanes of the
-  // subgroup return it); ok = false: zero work, the value is unused
+  // subgroup return it); ok = false: the value is unused (zero work except in the branch-free sub-pel path)
   auto dist = [&](rv_mv mv, bool ok) -> uint32_t {
     int cf = 0, rf = 0, sx = 0, sy = 0;
     if (SUB) {
@@ -1075,16 +1085,97 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
       sx = jb.po_x + (ok ? mv.col / 8 : 0);
       sy = jb.po_y + (ok ? mv.row / 8 : 0);
     }
-    const int8_t *xf = kReg[0][cf];
-    const int8_t *yf = kReg[0][rf];
+    // sub-pel: the candidates of one wavefront differ in fraction, so the
+    // filter runs branch-free for all of them: a zero fraction takes the
+    // identity taps (128 at tap 3), whose 7-bit round trips are exact, so
+    // copy / horizontal-only / vertical-only / both equal put_8tap's four
+    // cases bit for bit (src/mc.rs:213-274).  Horizontal taps as i16 pairs
+    // for v_dot2: odd outputs (1,2) (3,4) (5,6), even outputs (0,1) (2,3)
+    // (4,5) (6,7); REGULAR taps 0 and 7 are zero for every fraction
+    // (src/mc.rs:71-88), so odd outputs need only 3 pairs.
+    uint32_t xp[7];
+    int32_t fy[8];
+    if (SUB) {
+      int32_t fx[8];
+      const int8_t *xf = kReg[0][cf];
+      const int8_t *yf = kReg[0][rf];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        fx[u] = cf ? (int32_t)xf[u] : (u == 3 ? 128 : 0);
+        fy[u] = rf ? (int32_t)yf[u] : (u == 3 ? 128 : 0);
+      }
+      xp[0] = pk16(fx[1], fx[2]);
+      xp[1] = pk16(fx[3], fx[4]);
+      xp[2] = pk16(fx[5], fx[6]);
+      xp[3] = pk16(fx[0], fx[1]);
+      xp[4] = pk16(fx[2], fx[3]);
+      xp[5] = pk16(fx[4], fx[5]);
+      xp[6] = pk16(fx[6], fx[7]);
+    }
+    const int32_t hround = (1 << (7 - ib)) >> 1, vround = (1 << (7 + ib)) >> 1;
     uint32_t acc = 0;
 #pragma unroll 1
     for (int j = 0; j < G::CPL; j++) {
       const int q = c / G::LPC + j * (G::C / G::LPC);
       const int x0 = (q % G::NC) * 8, y0 = (q / G::NC) * 8 + lic * G::RPL;
       int32_t d[G::RPL][8];
-      if (ok) {
-        if (!SUB && !SATD) {  // 8-pixel row chunks: unaligned vector loads + v_sad
+      if (SUB) {
+        // output rows y0 .. y0 + RPL - 1 take window rows y0 + 1 .. y0 + RPL + 5
+        // (taps 1..6); the window reads stay inside the clamped origin's
+        // reach whether or not the candidate is valid (ok only gates use)
+        int32_t v[G::RPL][8];
+#pragma unroll
+        for (int i = 0; i < G::RPL; i++)
+#pragma unroll
+          for (int t = 0; t < 8; t++) v[i][t] = vround;
+#pragma unroll
+        for (int m = 1; m < G::RPL + 6; m++) {
+          const Px *w = plane_ptr<Px>(ref, sx + x0, sy + y0 + m);
+          // pixel pairs (2j, 2j + 1) as packed i16, j < 7 (pixels 0..13)
+          uint32_t pp[7];
+          if constexpr (sizeof(Px) == 1) {  // 16 bytes, one unaligned load
+            const uint4 lv = ld16(w);
+            const uint32_t wd[4] = {lv.x, lv.y, lv.z, lv.w};
+#pragma unroll
+            for (int jj = 0; jj < 7; jj++)
+              pp[jj] = __builtin_amdgcn_perm(0u, wd[jj >> 1], jj & 1 ? 0x0c030c02u : 0x0c010c00u);
+          } else {  // 32 bytes, two: the dwords already are the pairs
+            const uint4 v0 = ld16(w), v1 = ld16(w + 8);
+            const uint32_t wd[7] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z};
+#pragma unroll
+            for (int jj = 0; jj < 7; jj++) pp[jj] = wd[jj];
+          }
+          int32_t mid[8];
+#pragma unroll
+          for (int t = 0; t < 8; t++) {
+            int32_t hs = hround;
+            if (t & 1) {
+#pragma unroll
+              for (int u = 0; u < 3; u++) hs = sdot2(pp[(t + 1) / 2 + u], xp[u], hs);
+            } else {
+#pragma unroll
+              for (int u = 0; u < 4; u++) hs = sdot2(pp[t / 2 + u], xp[3 + u], hs);
+            }
+            mid[t] = hs >> (7 - ib);
+          }
+#pragma unroll
+          for (int i = 0; i < G::RPL; i++) {
+            const int kk = m - i;
+            if (kk >= 1 && kk < 7) {  // taps 1..6
+#pragma unroll
+              for (int t = 0; t < 8; t++) v[i][t] += __mul24(fy[kk], mid[t]);
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < G::RPL; i++) {
+          const Px *o = plane_ptr<Px>(a.org, jb.po_x + x0, jb.po_y + y0 + i);
+#pragma unroll
+          for (int t = 0; t < 8; t++)
+            d[i][t] = (int32_t)o[t] - clampi(v[i][t] >> (7 + ib), 0, maxv);
+        }
+      } else if (ok) {
+        if (!SATD) {  // 8-pixel row chunks: unaligned vector loads + v_sad
 #pragma unroll
           for (int i = 0; i < G::RPL; i++) {
             const Px *o = plane_ptr<Px>(a.org, jb.po_x + x0, jb.po_y + y0 + i);
@@ -1101,77 +1192,13 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
 #pragma unroll
             for (int t = 0; t < 8; t++) d[i][t] = 0;
           }
-        } else if (!SUB) {
+        } else {
 #pragma unroll
           for (int i = 0; i < G::RPL; i++) {
             const Px *o = plane_ptr<Px>(a.org, jb.po_x + x0, jb.po_y + y0 + i);
             const Px *r = plane_ptr<Px>(ref, sx + x0, sy + y0 + i);
 #pragma unroll
             for (int t = 0; t < 8; t++) d[i][t] = (int32_t)o[t] - (int32_t)r[t];
-          }
-        } else {
-          // output rows y0 .. y0 + RPL - 1 need window rows y0 .. y0 + RPL + 6
-          int32_t v[G::RPL][8];
-#pragma unroll
-          for (int i = 0; i < G::RPL; i++)
-#pragma unroll
-            for (int t = 0; t < 8; t++) v[i][t] = 0;
-#pragma unroll
-          for (int m = 0; m < G::RPL + 7; m++) {
-            if (!rf && (m < 3 || m >= G::RPL + 3)) continue;  // only rows i + 3 are used
-            if (rf && (m == 0 || m == G::RPL + 6)) continue;    // only by the zero taps 0 / 7
-            const Px *w = plane_ptr<Px>(ref, sx + x0, sy + y0 + m);
-            int32_t mid[8];
-            if (cf) {
-              int32_t px[15];
-              if constexpr (sizeof(Px) == 1) {  // 16 bytes, one unaligned load
-                const uint4 v = ld16(w);
-                const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int t = 0; t < 15; t++) px[t] = (wd[t >> 2] >> (8 * (t & 3))) & 0xff;
-              } else {  // 32 bytes, two
-                const uint4 v0 = ld16(w), v1 = ld16(w + 8);
-                const uint32_t wd[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-                for (int t = 0; t < 15; t++) px[t] = (wd[t >> 1] >> (16 * (t & 1))) & 0xffff;
-              }
-              // REGULAR taps 0 and 7 are zero for every fraction (src/mc.rs:71-88)
-#pragma unroll
-              for (int t = 0; t < 8; t++) {
-                int32_t s = 0;
-#pragma unroll
-                for (int u = 1; u < 7; u++) s += __mul24((int32_t)xf[u], px[t + u]);
-                mid[t] = round_shift(s, 7 - ib);
-              }
-            } else {
-#pragma unroll
-              for (int t = 0; t < 8; t++) mid[t] = w[t + 3];
-            }
-            if (rf) {
-#pragma unroll
-              for (int i = 0; i < G::RPL; i++) {
-                const int kk = m - i;
-                if (kk >= 1 && kk < 7) {  // taps 1..6
-                  const int32_t f = yf[kk];
-#pragma unroll
-                  for (int t = 0; t < 8; t++) v[i][t] += __mul24(f, mid[t]);
-                }
-              }
-            } else {
-#pragma unroll
-              for (int t = 0; t < 8; t++) v[m - 3][t] = cf ? round_shift(mid[t], ib) : mid[t];
-            }
-          }
-#pragma unroll
-          for (int i = 0; i < G::RPL; i++) {
-            const Px *o = plane_ptr<Px>(a.org, jb.po_x + x0, jb.po_y + y0 + i);
-#pragma unroll
-            for (int t = 0; t < 8; t++) {
-              int32_t p = v[i][t];
-              if (rf) p = round_shift(p, cf ? 7 + ib : 7);
-              p = clampi(p, 0, maxv);
-              d[i][t] = (int32_t)o[t] - p;
-            }
           }
         }
       } else {
@@ -1305,6 +1332,10 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
   }
 }
 
+template <typename Px, int N, bool SUB, bool SATD>
+__global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
+  ds_grp_body<Px, N, SUB, SATD>(a);
+}
 template <typename Px>
 bool try_grp(const DsArgs &a, hipStream_t s) {
   if (a.tele || a.w != a.h) return false;
