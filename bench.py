@@ -50,15 +50,19 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
 # at full occupancy (tools/ubench/valu_rates.hip, profiles/valu_rates.txt)
 VALU_PEAK_GUIDE = 256 * 4 * 2.4 / 2
 VALU_PEAK_INT = 256 * 1 * 2.4
-STAGES = ["F0_pyramid", "F1_full_search", "F2_half_res_quadrants", "FL_lookahead_16x16",
+# FL runs on a second stream by default: "FL_on_main_stream" is then the
+# fork alone, and "FL_lookahead_span" the lookahead's own span, overlapped
+# with F3/F4 (RAV1E_HIP_REPLAY_SERIAL=1: both on one stream)
+STAGES = ["F0_pyramid", "F1_full_search", "F2_half_res_quadrants", "FL_on_main_stream",
           "F3_diamond_fullpel", "F3_diamond_subpel", "F4_rdo_single_ref", "F4_rdo_compound",
-          "F4_rd_cost_argmin", "F6_commit", "F5_importance_satd", "F7_pad_exchange"]
+          "F4_rd_cost_argmin", "F6_commit", "F5_importance_satd", "F7_pad_exchange",
+          "FL_lookahead_span"]
 # speed 6: the 32x32 / 16x16 / 8x8 searches run inside the sub-pel stage,
 # their candidates inside F4, the partition decision with the argmin
-STAGES6 = ["F0_pyramid", "F1_full_search", "F2_half_res_quadrants", "FL_lookahead_16x16",
+STAGES6 = ["F0_pyramid", "F1_full_search", "F2_half_res_quadrants", "FL_on_main_stream",
            "F3_diamond_fullpel", "F3_subpel_and_level_me", "F4_rdo_single_ref_all_levels",
            "F4_rdo_compound_all_levels", "F4_argmin_partition", "F6_commit_leaves",
-           "F5_importance_satd", "F7_pad_exchange"]
+           "F5_importance_satd", "F7_pad_exchange", "FL_lookahead_span"]
 
 
 def coarse_windows(W, H, R, scale, tiling, group):

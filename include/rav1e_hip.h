@@ -548,15 +548,18 @@ int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
  * instrument a sample: block = the GOP length keeps every me_range_scale
  * equally represented. */
 int rv_replay_set_timing(rv_replay *r, int stride, int block);
-/* Kernel-time breakdown of the last instrumented frame (HIP events on the
- * replay stream), ms: [0] F0 pyramid + box sums, [1] F1 full search, [2] F2
- * half-res diamond, [3] F3 full-pel diamond, [4] F3 sub-pel diamond + the
- * candidate list, [5] F4 fused single-reference candidate launch (luma: MC
- * + skip distortion + diff + fwd TX_64X64 + quantize + estimate_rate +
+/* Kernel-time breakdown of the last instrumented frame (HIP events), ms:
+ * [0] F0 pyramid + box sums, [1] F1 full search, [2] F2 half-res diamond,
+ * [3] FL on the main stream (the fork to the side stream; the whole
+ * lookahead with RAV1E_HIP_REPLAY_SERIAL=1), [4] F3 full-pel diamond, [5]
+ * F3 sub-pel diamond + the candidate lists (speed 6: + every level's
+ * searches), [6] F4 fused single-reference candidate launch (luma: MC +
+ * skip distortion + diff + fwd TX_64X64 + quantize + estimate_rate +
  * inverse + add + non-skip distortion; chroma U and V: the same with
- * TX_32X32 and SSE), [6] F4 compound candidates, [7] F4 rd cost + argmin,
- * [8] F6 commit, [9] F5 importance, [10] F7 pad / exchange.  Returns the
- * count written (<= 11). */
+ * TX_32X32 and SSE), [7] F4 compound candidates, [8] F4 rd cost + argmin
+ * (+ the join with the lookahead), [9] F6 commit, [10] F5 importance, [11]
+ * F7 deblock / pad / exchange, [12] the lookahead's own span (FL, on the
+ * side stream, overlapping [4]..[7]).  Returns the count written (<= 13). */
 int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
 /* Same breakdown summed over the last `last_frames` instrumented frames
  * (<= 64). */

@@ -571,6 +571,12 @@ struct rv_replay {
   Geo g;
   CandGeo cg;
   hipStream_t stream;
+  // FL runs on a second stream, overlapping F3/F4 (it only needs F1/F2's
+  // MVs; score_candidates and F5 join it).  RAV1E_HIP_REPLAY_SERIAL=1: one
+  // stream (A/B).
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  bool overlap = false;
   bool own_stream;
   bool sea;  // successive-elimination coarse search (bit depth <= 10)
   // per pyramid level: the frame's quantizers (QuantizationContext of
@@ -634,7 +640,10 @@ struct rv_replay {
   // frame.  Every `timing_stride`-th block of frames is instrumented (each
   // record costs ~4.4 us of idle GPU between kernels on MI355X).
   static constexpr int kRing = 64;
-  static constexpr int kEv = 13;
+  // e[0..12]: the stage boundaries on the main stream; e[13], e[14]: the
+  // lookahead's start and end (on the side stream when it overlaps)
+  static constexpr int kEv = 15;
+  static constexpr int kStageEv = 13;
   hipEvent_t evs[kRing][kEv];
   int timing_stride = 1, timing_block = 1;
   long timed = 0;
@@ -1042,6 +1051,10 @@ void rv_replay_destroy(rv_replay *r) {
   for (int f = 0; f < rv_replay::kRing; f++)
     for (int i = 0; i < rv_replay::kEv; i++)
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
+  if (r->side) (void)hipStreamSynchronize(r->side);
+  if (r->ev_fork) (void)hipEventDestroy(r->ev_fork);
+  if (r->ev_join) (void)hipEventDestroy(r->ev_join);
+  if (r->side) (void)hipStreamDestroy(r->side);
   if (r->own_stream && r->stream) (void)hipStreamDestroy(r->stream);
   delete r;
 }
@@ -1217,6 +1230,14 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
   for (int f = 0; f < rv_replay::kRing; f++)
     for (int i = 0; i < rv_replay::kEv; i++)
       ok = ok && hipEventCreateWithFlags(&r->evs[f][i], hipEventDisableSystemFence) == hipSuccess;
+  {
+    const char *e = getenv("RAV1E_HIP_REPLAY_SERIAL");
+    r->overlap = !(e && e[0] == '1');
+  }
+  if (r->overlap)
+    ok = ok && hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&r->ev_join, hipEventDisableTiming) == hipSuccess;
   const size_t ev_bytes = (size_t)rv_replay::kRing * 2 * nr * 4;
   r->ds_evals = (uint32_t *)dalloc(r, ev_bytes);
   ok = ok && r->ds_evals && hipMemsetAsync(r->ds_evals, 0, ev_bytes, r->stream) == hipSuccess;
@@ -1504,12 +1525,21 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // references' original frames; its coarse and half-res stages are F1 / F2
   // (the same inputs).  F5 reads its MVs.
   {
+    hipStream_t ls = st;
+    if (r->overlap) {
+      RV_H(hipEventRecord(r->ev_fork, st));
+      RV_H(hipStreamWaitEvent(r->side, r->ev_fork, 0));
+      ls = r->side;
+    }
+    if (tm) RV_H(hipEventRecord(e[13], ls));
     const int nl = nr * g.R * 16;
-    fill_preds_kernel<<<(nl + 255) / 256, 256, 0, st>>>(r->jobs_look[lv], r->src_look, nl,
+    fill_preds_kernel<<<(nl + 255) / 256, 256, 0, ls>>>(r->jobs_look[lv], r->src_look, nl,
                                                         r->coarse, r->half, 0);
+    RV_R(rv_diamond_search_multi(&cur.y, refs_o, g.R, r->jobs_look[lv], nr * 16, 16, 16, 0, 0,
+                                 0, g.bd, r->look, nullptr, nullptr, ls));
+    if (tm) RV_H(hipEventRecord(e[14], ls));
+    if (r->overlap) RV_H(hipEventRecord(r->ev_join, ls));
   }
-  RV_R(rv_diamond_search_multi(&cur.y, refs_o, g.R, r->jobs_look[lv], nr * 16, 16, 16, 0, 0, 0,
-                               g.bd, r->look, nullptr, nullptr, st));
   RV_EV(4);
   // F3 full-res full-pel diamond -> sub-pel predictor; sub-pel diamond
   // (speed 10: SAD, no hp) -> NEWMV of every superblock and reference
@@ -1679,6 +1709,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     RV_EV(7);
   }
   RV_EV(8);
+  if (r->overlap) RV_H(hipStreamWaitEvent(st, r->ev_join, 0));  // the lookahead's MVs
   score_candidates<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, cg, L.lambda, L.ds[1], L.ds[2], r->sub,
                                                      r->l_out,
                                                      r->c_out, r->c_out + nct * 3, ntx_c, r->win,
@@ -1847,15 +1878,22 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
   if (last < 1) last = 1;
   if (last > rv_replay::kRing) last = rv_replay::kRing;
   if (last > r->timed) last = (int)r->timed;
-  for (int i = 0; i < cap && i < rv_replay::kEv - 1; i++) ms_out[i] = 0.f;
+  constexpr int kS = rv_replay::kStageEv;
+  for (int i = 0; i < cap && i < kS; i++) ms_out[i] = 0.f;
   int n = 0;
   for (int f = 0; f < last; f++) {
     hipEvent_t *e = r->evs[(r->timed - 1 - f) % rv_replay::kRing];
-    RV_H(hipEventSynchronize(e[rv_replay::kEv - 1]));
+    RV_H(hipEventSynchronize(e[kS - 1]));
+    RV_H(hipEventSynchronize(e[14]));
     n = 0;
-    for (int i = 0; i < rv_replay::kEv - 1 && n < cap; i++) {
+    for (int i = 0; i < kS - 1 && n < cap; i++) {
       float ms = 0.f;
       RV_H(hipEventElapsedTime(&ms, e[i], e[i + 1]));
+      ms_out[n++] += ms;
+    }
+    if (n < cap) {  // the lookahead's own span (overlapped with F3/F4 by default)
+      float ms = 0.f;
+      RV_H(hipEventElapsedTime(&ms, e[13], e[14]));
       ms_out[n++] += ms;
     }
   }

@@ -24,7 +24,7 @@ RV_REPLAY_SPEED6 = 8  # the speed-6 schedule: partition RDO 64x64 .. 8x8 (config
 RV_REPLAY_DEBLOCK = 16  # deblock every coded frame before it becomes a reference (1 group)
 # HIP-event stages of a frame: F0, F1, F2, FL (lookahead), F3 full-pel, F3
 # sub-pel, F4 single, F4 compound, F4 argmin, F6 commit, F5, F7
-N_STAGES = 12
+N_STAGES = 13
 
 # GOP of the reference's reorder pyramid (src/api/internal.rs:61-95):
 # group_input_len 4, levels 0,1,2,2 -> me_range_scale = 4 >> level
