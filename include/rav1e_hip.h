@@ -318,6 +318,29 @@ int rv_deblock_plane(const rv_plane *plane, int pli, int width, int height, cons
  * the level from the frame's ac quantizer (ac_q(base_q_idx, 0, bd)). */
 int rv_deblock_fast_level(int ac_q, int bit_depth, int is_key);
 
+/* ---- CDEF (src/cdef.rs) ------------------------------------------------
+ * cdef_filter_frame (src/cdef.rs:542-641) as two steps on device planes.
+ * rv_cdef_find_dirs: cdef_analyze_superblock (:278-317) over the frame --
+ * cdef_find_dir (:68-126) of every 8x8 luma block that is not skip (skip =
+ * all four of its 4x4 blocks skip), dir 0 / var 0 otherwise; d_dir / d_var
+ * per 8x8 block, pitch ceil(width / 8).  d_skip per luma 4x4 block, pitch
+ * mi_stride >= 2 * ceil(width / 8), rows 2 * ceil(height / 8).
+ * rv_cdef_filter_plane: cdef_filter_superblock (:411-534) over every
+ * superblock of plane pli, src -> dst (distinct planes): cdef_filter_block
+ * (:152-228) on non-skip blocks with the strengths of the block's 64x64
+ * cdef_index (d_cdef_index, pitch ceil(width / 64)), a copy on skip ones.
+ * y_strengths / uv_strengths / damping: FrameInvariants::cdef_{y,uv}_
+ * strengths (host, 8 entries <= 63) and cdef_damping.  Taps outside the
+ * visible plane read what the reference's padded copy holds there
+ * (CDEF_VERY_LARGE in the 2-pixel ring, 128 beyond). */
+int rv_cdef_find_dirs(const rv_plane *luma, int width, int height, const uint8_t *d_skip,
+                      int mi_stride, uint8_t *d_dir, int32_t *d_var, int bit_depth, void *stream);
+int rv_cdef_filter_plane(const rv_plane *src, const rv_plane *dst, int pli, int width, int height,
+                         const uint8_t *d_skip, int mi_stride, const uint8_t *d_dir,
+                         const int32_t *d_var, const uint8_t *d_cdef_index,
+                         const uint8_t *y_strengths, const uint8_t *uv_strengths, int damping,
+                         int bit_depth, void *stream);
+
 /* dc_q / ac_q lookups (src/quantize.rs:42-62) on the host: ac = 0 for
  * dc_qlookup*_Q3, 1 for ac_qlookup*_Q3; -1 on bad arguments. */
 int rv_q_lookup(int ac, int qindex, int bit_depth);

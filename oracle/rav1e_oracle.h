@@ -81,6 +81,22 @@ void orc_deblock_plane(void *origin, ptrdiff_t stride, int hbd, int bd, int widt
                        int xdec, int ydec, int pli, const uint8_t *lg, const uint8_t *skip,
                        int mi_stride, const uint8_t levels[4]);
 int orc_deblock_fast_level(int ac_q, int bd, int is_key);
+/* CDEF (src/cdef.rs): cdef_find_dir (:68-126) of the 8x8 block at img
+ * (the padded u16 copy), cdef_filter_block (:152-228), adjust_strength
+ * (:232-239), and cdef_filter_frame (:542-641) out of place: planes at
+ * their visible origins, skip per luma 4x4 (pitch mi_stride), cdef_index
+ * per 64x64 superblock (pitch ceil(width / 64)); dirs / vars (optional,
+ * pitch ceil(width / 8)) receive the per-8x8 directions and variances. */
+int orc_cdef_find_dir(const uint16_t *img, ptrdiff_t stride, int32_t *var, int coeff_shift);
+void orc_cdef_filter_block(void *dst, ptrdiff_t dstride, int hbd, const uint16_t *in,
+                           ptrdiff_t istride, int pri, int sec, int dir, int damping, int bd,
+                           int xdec, int ydec);
+int orc_cdef_adjust_strength(int strength, int32_t var);
+void orc_cdef_filter_frame(const void *const in[3], const ptrdiff_t istride[3], void *const out[3],
+                           const ptrdiff_t ostride[3], int hbd, int bd, int width, int height,
+                           int xdec, int ydec, const uint8_t *skip, int mi_stride,
+                           const uint8_t *cdef_index, const uint8_t y_str[8],
+                           const uint8_t uv_str[8], int damping, uint8_t *dirs, int32_t *vars);
 /* SUBPEL_FILTERS + get_filter (src/mc.rs:70-179, 201-210) */
 const int32_t *orc_get_filter(int mode, int frac, int length);
 

@@ -249,6 +249,9 @@ def _declare(L):
         "rv_predict_intra_batch": (i32, [P, vp, vp, i32, i32, i32, vp]),
         "rv_deblock_plane": (i32, [P, i32, i32, i32, vp, vp, i32, vp, i32, vp]),
         "rv_deblock_fast_level": (i32, [i32, i32, i32]),
+        "rv_cdef_find_dirs": (i32, [P, i32, i32, vp, i32, vp, vp, i32, vp]),
+        "rv_cdef_filter_plane": (i32, [P, P, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32,
+                                       vp]),
         "rv_prep_8tap_batch": (i32, [vp, P, vp, i32, i32, i32, i32, i32, i32, vp]),
         "rv_mc_avg_batch": (i32, [P, vp, vp, vp, i32, i32, i32, i32, vp]),
         "rv_mc_dist_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
@@ -579,6 +582,40 @@ def deblock_plane(plane: DevicePlane, pli, width, height, lg: np.ndarray, skip: 
 
 def deblock_fast_level(ac_q, bit_depth, is_key=False):
     return int(lib().rv_deblock_fast_level(int(ac_q), bit_depth, 1 if is_key else 0))
+
+
+def cdef_filter_frame(src, dst, width, height, skip: np.ndarray, cdef_index: np.ndarray,
+                      y_strengths, uv_strengths, damping=3, bit_depth=8, stream=None):
+    """cdef_filter_frame (src/cdef.rs:542-641) of a frame: src / dst = three
+    DevicePlanes each (Y, U, V; distinct), skip per luma 4x4 block (rows,
+    cols >= 2 * ceil(width / 8)), cdef_index per 64x64 superblock, the
+    FrameInvariants strength tables and damping.  Returns (dir, var) per
+    8x8 luma block (cdef_analyze_superblock)."""
+    cols8, rows8 = (width + 7) // 8, (height + 7) // 8
+    skip = np.ascontiguousarray(skip, dtype=np.uint8)
+    cdef_index = np.ascontiguousarray(cdef_index, dtype=np.uint8)
+    if skip.shape[1] < 2 * cols8 or skip.shape[0] < 2 * rows8:
+        raise Rav1eHipError("cdef_filter_frame: skip must cover the frame's 8x8 grid")
+    if cdef_index.shape[0] < (height + 63) // 64 or cdef_index.shape[1] != (width + 63) // 64:
+        raise Rav1eHipError("cdef_filter_frame: cdef_index is per 64x64 superblock")
+    if cdef_index.max(initial=0) > 7:
+        raise Rav1eHipError("cdef_filter_frame: cdef_index above 7")
+    ds, di = DeviceBuffer.from_array(skip), DeviceBuffer.from_array(cdef_index)
+    dd, dv = DeviceBuffer(cols8 * rows8), DeviceBuffer(4 * cols8 * rows8)
+    ys = np.ascontiguousarray(np.asarray(y_strengths, dtype=np.uint8))
+    us = np.ascontiguousarray(np.asarray(uv_strengths, dtype=np.uint8))
+    if ys.shape != (8,) or us.shape != (8,):
+        raise Rav1eHipError("cdef_filter_frame: 8 strengths per table")
+    _check(lib().rv_cdef_find_dirs(C.byref(src[0].desc), width, height, ds.ptr, skip.shape[1],
+                                   dd.ptr, dv.ptr, bit_depth, stream), "rv_cdef_find_dirs")
+    for pli in range(3):
+        _check(lib().rv_cdef_filter_plane(C.byref(src[pli].desc), C.byref(dst[pli].desc), pli,
+                                          width, height, ds.ptr, skip.shape[1], dd.ptr, dv.ptr,
+                                          di.ptr, ys.ctypes.data, us.ctypes.data, damping,
+                                          bit_depth, stream), "rv_cdef_filter_plane")
+    _sync(stream)
+    return (dd.download(np.uint8).reshape(rows8, cols8),
+            dv.download(np.int32).reshape(rows8, cols8))
 
 
 def prep_8tap_batch(src: DevicePlane, jobs, w, h, mode_x=0, mode_y=0, bit_depth=8):

@@ -63,6 +63,13 @@ def lib():
         L.orc_deblock_plane.argtypes = [vp, sz, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32,
                                         vp]
         L.orc_deblock_fast_level.argtypes = [i32, i32, i32]
+        L.orc_cdef_find_dir.restype = i32
+        L.orc_cdef_find_dir.argtypes = [vp, sz, vp, i32]
+        L.orc_cdef_filter_block.argtypes = [vp, sz, i32, vp, sz] + [i32] * 7
+        L.orc_cdef_adjust_strength.restype = i32
+        L.orc_cdef_adjust_strength.argtypes = [i32, i32]
+        L.orc_cdef_filter_frame.argtypes = [vp, vp, vp, vp] + [i32] * 6 + [vp, i32, vp, vp, vp,
+                                                                          i32, vp, vp]
         _lib = L
     return _lib
 
@@ -120,6 +127,42 @@ def deblock_plane(full, yo, xo, width, height, xdec, ydec, pli, lg, skip, levels
 
 def deblock_fast_level(ac_q, bd, is_key=False):
     return int(lib().orc_deblock_fast_level(int(ac_q), bd, 1 if is_key else 0))
+
+
+def cdef_find_dir(img, coeff_shift=0):
+    """orc_cdef_find_dir of an 8x8 u16 block (the padded copy's samples):
+    (dir, var)."""
+    img = np.ascontiguousarray(img, dtype=np.uint16)
+    var = np.zeros(1, np.int32)
+    d = lib().orc_cdef_find_dir(ptr(img), img.shape[1], ptr(var), coeff_shift)
+    return int(d), int(var[0])
+
+
+def cdef_adjust_strength(strength, var):
+    return int(lib().orc_cdef_adjust_strength(int(strength), int(var)))
+
+
+def cdef_filter_frame(planes, width, height, xdec, ydec, skip, cdef_index, y_str, uv_str,
+                      damping=3, bd=8):
+    """orc_cdef_filter_frame on three visible planes (numpy); returns the
+    filtered planes and the per-8x8 (dir, var)."""
+    ins = [np.ascontiguousarray(p) for p in planes]
+    outs = [np.zeros_like(p) for p in ins]
+    skip = np.ascontiguousarray(skip, dtype=np.uint8)
+    cdef_index = np.ascontiguousarray(cdef_index, dtype=np.uint8)
+    ys = np.ascontiguousarray(np.asarray(y_str, dtype=np.uint8))
+    us = np.ascontiguousarray(np.asarray(uv_str, dtype=np.uint8))
+    cols8, rows8 = (width + 7) // 8, (height + 7) // 8
+    dirs = np.zeros((rows8, cols8), np.uint8)
+    vars_ = np.zeros((rows8, cols8), np.int32)
+    ip = (C.c_void_p * 3)(*[p.ctypes.data for p in ins])
+    op = (C.c_void_p * 3)(*[p.ctypes.data for p in outs])
+    ist = (C.c_ssize_t * 3)(*[p.shape[1] for p in ins])
+    ost = (C.c_ssize_t * 3)(*[p.shape[1] for p in outs])
+    lib().orc_cdef_filter_frame(ip, ist, op, ost, hbd_of(ins[0]), bd, width, height, xdec, ydec,
+                                ptr(skip), skip.shape[1], ptr(cdef_index), ptr(ys), ptr(us),
+                                damping, ptr(dirs), ptr(vars_))
+    return outs, dirs, vars_
 
 
 def prep_8tap(src, sy, sx, w, h, col_frac, row_frac, mode_x=0, mode_y=0, bd=8):

@@ -23,6 +23,9 @@ types over Python lists.  Only the resulting numbers are written
   quant src/quantize.rs:34-160, 205-333  QuantizationContext::update /
                                quantize, dequantize, divu_gen/divu_pair,
                                dc_q/ac_q, get_log_tx_scale (+ av1_scan_orders)
+  cdef  src/cdef.rs:54-239      cdef_find_dir (+ first_max_element),
+                               native::cdef_filter_block (+ constrain),
+                               adjust_strength (+ msb, src/util/mod.rs)
   tx    src/transform/forward.rs:1771-1900 FwdTxfm2D::fht and
         src/transform/inverse.rs:1939-2114 inv_txfm2d_add / inv_txfm2d, over
         the reference's 1-D kernels (rs2py.py); round_shift_array,
@@ -708,8 +711,94 @@ def gen_tx(I, rng, out):
     out["tx_inv_out"] = np.array(iout, np.uint16)
 
 
+# ---------------------------------------------------------------- cdef
+def _cdef_content(rng, h, w, bd):
+    """Directional ramps + an edge + small noise: taps land inside
+    constrain's active range at every strength."""
+    yy, xx = np.mgrid[0:h, 0:w]
+    a = rng.uniform(0, np.pi)
+    base = (np.cos(a) * xx + np.sin(a) * yy) * rng.uniform(2, 12)
+    img = base + rng.integers(-6, 7, (h, w)) + (xx > w // 2) * rng.integers(0, 40)
+    img = img * (1 << (bd - 8)) + (1 << bd) // 3
+    return np.clip(img, 0, (1 << bd) - 1).astype(np.int64)
+
+
+def gen_cdef(I, rng, out):
+    I.sources.append(RI.Source(REF + "cdef.rs"))
+    # release semantics: cdef_find_dir's debug_assert!(p >> coeff_shift <= 255)
+    # is compiled out, and a partial edge block of the padded copy sums
+    # CDEF_VERY_LARGE with i32 wrap-around (typed ints wrap in the interpreter)
+    I.release = True
+    I.globals.vars["CDEF_VERY_LARGE"] = RI.TInt(0x8000, "u16")
+    fd = F(I, "cdef_find_dir", "cdef.rs")
+    fb = F(I, "cdef_filter_block", "cdef.rs")
+    adj = F(I, "adjust_strength", "cdef.rs")
+
+    def u(v):
+        return RI.TInt(int(v), "usize")
+
+    def i32(v):
+        return RI.TInt(int(v), "i32")
+
+    imgs, shifts, dirs, vars_ = [], [], [], []
+    for n in range(96):
+        bd = (8, 10, 12)[n % 3]
+        img = _cdef_content(rng, 8, 8, bd)
+        if n % 8 == 5:  # a partial edge block of the padded copy
+            img[:, 8 - 1 - (n // 8) % 4:] = 0x8000
+        if n % 8 == 6:
+            img[5:, :] = 128
+            img[3:5, :] = 0x8000
+        plane = H.Plane.from_full(img, 0, 0, 8, 8)
+        v = [RI.TInt(0, "i32")]
+        d = fd(plane.slice(RI.Struct("PlaneOffset", {"x": 0, "y": 0})),
+               RI.Ref(lambda: v[0], lambda x: v.__setitem__(0, x)), u(bd - 8),
+               generics={"T": RI.PrimType("u16")})
+        imgs.append(img.astype(np.uint16))
+        shifts.append(bd - 8)
+        dirs.append(int(d))
+        vars_.append(int(v[0]))
+    out["dir_img"] = np.array(imgs, np.uint16)
+    out["dir_shift"] = np.array(shifts, np.int32)
+    out["dir_dir"] = np.array(dirs, np.int32)
+    out["dir_var"] = np.array(vars_, np.int32)
+    cases, srcs, dsts = [], [], []
+    for n in range(120):
+        bd = (8, 10, 12)[n % 3]
+        xdec, ydec = ((0, 0), (1, 1), (1, 0))[(n // 3) % 3]
+        cs = bd - 8
+        src = _cdef_content(rng, 12, 12, bd)
+        if n % 5 == 1:
+            src[:2, :] = 0x8000
+        if n % 5 == 2:
+            src[:, -3:] = 0x8000
+            src[-2:, :] = 128
+        pri = int(rng.integers(0, 16)) << cs
+        if n % 4 == 0:
+            pri = int(rng.integers(0, 16 << cs))  # adjust_strength output: any value
+        sec = (0, 1, 2, 4)[int(rng.integers(0, 4))] << cs
+        damping = 3 + cs - (1 if (xdec or ydec) else 0) + int(rng.integers(0, 4))
+        dr = int(rng.integers(0, 8))
+        flat = [RI.TInt(int(x), "u16") for x in src.ravel()]
+        dst = H.Plane.from_full(np.zeros((8, 8), np.int64), 0, 0, 8, 8)
+        fb(region_at(dst, 0, 0), RI.Ptr(flat, 2 * 12 + 2), RI.TInt(12, "isize"), i32(pri),
+           i32(sec), u(dr), i32(damping), u(bd), u(xdec), u(ydec), 0,
+           generics={"T": prim(bd)})
+        cases.append((bd, xdec, ydec, pri, sec, dr, damping))
+        srcs.append(src.astype(np.uint16))
+        dsts.append(np.array(dst.data, np.int64).reshape(8, 8).astype(np.uint16))
+    out["filt_cases"] = np.array(cases, np.int32)
+    out["filt_src"] = np.array(srcs, np.uint16)
+    out["filt_dst"] = np.array(dsts, np.uint16)
+    adj_cases = [(s, v) for s in (0, 1, 5, 15, 60) for v in
+                 (0, 1, 63, 64, 100, 1 << 12, 1 << 18, (1 << 30) + 5, 977)]
+    out["adj_cases"] = np.array(adj_cases, np.int32)
+    out["adj_out"] = np.array([int(adj(i32(s), i32(v))) for s, v in adj_cases], np.int32)
+    print("cdef: %d find_dir, %d filter_block, %d adjust" % (len(imgs), len(cases),
+                                                             len(adj_cases)))
+
 SECTIONS = {"mc": gen_mc, "dist": gen_dist, "rdo": gen_rdo, "me": gen_me, "quant": gen_quant,
-            "tx": gen_tx, "ds": gen_ds}
+            "tx": gen_tx, "ds": gen_ds, "cdef": gen_cdef}
 
 
 def main(argv):
@@ -717,7 +806,9 @@ def main(argv):
     os.makedirs(OUT, exist_ok=True)
     for n in names:
         I = make_interp()
-        rng = np.random.default_rng(0x5EED + sorted(SECTIONS).index(n))
+        # the sections that predate cdef keep the seeds they were generated with
+        old = sorted(set(SECTIONS) - {"cdef"})
+        rng = np.random.default_rng(0x5EED + (old.index(n) if n in old else 100))
         random.seed(1)
         out = {}
         t = time.time()

@@ -1589,6 +1589,8 @@ class Interp:
             return False
         if name in ("assert", "debug_assert", "assert_eq", "debug_assert_eq", "assert_ne",
                     "debug_assert_ne"):
+            if name.startswith("debug_") and getattr(self, "release", False):
+                return None  # a release build compiles debug_assert! out
             args = self._macro_args(toks)
             if name.endswith("_eq"):
                 a, b = (deref(self.ev(x, env)) for x in args[:2])
@@ -1994,6 +1996,8 @@ def call_method(r, name, args, gty, raw):
         return _option_method(r, name, args)
     if isinstance(r, (list, Slice)):
         return _slice_method(r, name, args, gty, raw)
+    if isinstance(r, tuple) and name in ("unwrap", "expect"):  # Some((a, b)) of max_by_key
+        return r
     if isinstance(r, (It, RangeV, tuple)):
         if isinstance(r, RangeV) and name == "contains":
             x = deref(args[0])
