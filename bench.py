@@ -167,8 +167,9 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     ts = (tiling["tile_width_sb"], tiling["tile_height_sb"])
     nin = len(hip_inputs)
     db = bool(flags & RP.RV_REPLAY_DEBLOCK)
+    cd = bool(flags & RP.RV_REPLAY_CDEF)
     c = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=threads, L=L,
-                    speed=speed, deblock=db)
+                    speed=speed, deblock=db, cdef=cd)
     for i in range(nin):
         c.set_input(i, hip_inputs[i])
     c.frame()  # the key frame (a copy), untimed
@@ -184,7 +185,7 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     nsb = ((W + 63) // 64) * ((H + 63) // 64)
     lim = max(1, nsb // 8)
     c1 = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=1, L=L,
-                     speed=speed, deblock=db)
+                     speed=speed, deblock=db, cdef=cd)
     for i in range(nin):
         c1.set_input(i, hip_inputs[i])
     c1.frame()
@@ -205,7 +206,8 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
                                     f"scaled to whole frames"}}
     # the GPU replay over the same frames, word for word
     g = RP.HipReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=n_inputs,
-                     flags=flags & (RP.RV_REPLAY_SPEED6 | RP.RV_REPLAY_DEBLOCK))
+                     flags=flags & (RP.RV_REPLAY_SPEED6 | RP.RV_REPLAY_DEBLOCK |
+                                    RP.RV_REPLAY_CDEF))
     g.synth_inputs(0)
     g.frame()
     bad = []
@@ -237,6 +239,8 @@ def main():
                     help="schedule (default: the config's BASELINE speed)")
     ap.add_argument("--deblock", action="store_true",
                     help="deblock every coded frame before it becomes a reference")
+    ap.add_argument("--cdef", action="store_true",
+                    help="deblock and CDEF every coded frame before it becomes a reference")
     ap.add_argument("--exhaustive-fs", action="store_true",
                     help="F1 coarse search without successive elimination (same results)")
     args = ap.parse_args()
@@ -258,7 +262,8 @@ def main():
     rects = RP.tile_groups(tiling, world)
     n_inputs = args.warmup + args.steps + 8  # every display the run codes
     flags = (RP.RV_REPLAY_EXHAUSTIVE_FS if args.exhaustive_fs else 0) | \
-        (RP.RV_REPLAY_SPEED6 if speed == 6 else 0) | (RP.RV_REPLAY_DEBLOCK if args.deblock else 0)
+        (RP.RV_REPLAY_SPEED6 if speed == 6 else 0) | (RP.RV_REPLAY_DEBLOCK if args.deblock or args.cdef else 0) | \
+        (RP.RV_REPLAY_CDEF if args.cdef else 0)
     hip = RP.HipReplay(W, H, xdec, ydec, bd, nref, group=rects[rank], tile_size=ts,
                        n_inputs=n_inputs, flags=flags)
     hip.synth_inputs(0)  # the stream's frames, resident in HBM before the timing
@@ -371,7 +376,7 @@ def main():
                                    f"{tiling['cols']}x{tiling['rows']} tiles over {world} GPU(s), "
                                    f"{nref} refs, reorder-pyramid coding order",
                        "width": W, "height": H, "refs": nref, "speed": speed,
-                       "deblock": bool(args.deblock),
+                       "deblock": bool(args.deblock or args.cdef), "cdef": bool(args.cdef),
                        "tiles": [tiling["cols"], tiling["rows"]],
                        "parallelism": f"tile-groups{world}",
                        "candidates_per_sb": f"{4 * nref} inter modes x (skip, non-skip)",

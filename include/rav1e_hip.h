@@ -493,6 +493,14 @@ typedef struct rv_replay_cfg {
  * also carries each group's block map (log2 block size and skip per luma
  * 4x4) and every group deblocks the whole frame after the import. */
 #define RV_REPLAY_DEBLOCK 16
+/* flags (with RV_REPLAY_DEBLOCK, as rav1e always deblocks before CDEF):
+ * CDEF every coded frame after deblocking (cdef_filter_frame,
+ * src/encoder.rs:2795-2802; enable_cdef at every speed, src/api/config.rs:
+ * 421-423) with cdef_bits 0, i.e. every superblock at cdef_index 0 and the
+ * level's strengths of FrameInvariants::set_quantizers (src/encoder.rs:
+ * 882-941, rv_replay_level_params.cdef_strengths).  Width and height must
+ * be multiples of 8. */
+#define RV_REPLAY_CDEF 32
 typedef struct rv_replay_frame_info {
   int32_t display;            /* display index of the coded frame */
   int32_t me_range_scale;     /* 4 >> pyramid level (src/encoder.rs:838) */
@@ -511,7 +519,8 @@ typedef struct rv_replay_level_params {
   int32_t base_q_idx;
   int32_t dc_delta_q[3];
   int32_t ac_delta_q[3];
-  int32_t reserved;
+  int32_t cdef_strengths;     /* cdef_y_strengths[0] | cdef_uv_strengths[0] << 8
+                               * (set_quantizers, src/encoder.rs:882-941) */
   double lambda, me_lambda;
   double dist_scale[3];
 } rv_replay_level_params;

@@ -93,6 +93,9 @@ typedef struct orc_replay {
   /* RV_REPLAY_DEBLOCK (orc_replay_set_deblock): the block map, fast levels */
   int deblock, mi_cols, mi_rows;
   uint8_t *mi_lg, *mi_skip;
+  /* RV_REPLAY_CDEF (orc_replay_set_cdef): (y, uv) strengths per level */
+  int cdef;
+  uint8_t cdef_str[3][2];
   pthread_mutex_t mu;
   int next_sb, pass, sb_limit;
 } orc_replay;
@@ -419,6 +422,19 @@ int orc_replay_set_deblock(orc_replay *r, int on) {
   return r->mi_lg && r->mi_skip ? 0 : -1;
 }
 
+/* CDEF every coded frame after deblocking (the replay's RV_REPLAY_CDEF):
+ * cdef_filter_frame with cdef_bits 0 and level l's strengths (y, uv) at
+ * cdef_index 0.  Needs the deblocking block map (orc_replay_set_deblock). */
+int orc_replay_set_cdef(orc_replay *r, int level, int y_strength, int uv_strength) {
+  if (!r->deblock || level < 0 || level > 2 || y_strength < 0 || y_strength > 63 ||
+      uv_strength < 0 || uv_strength > 63 || (r->W & 7) || (r->H & 7))
+    return -1;
+  r->cdef = 1;
+  r->cdef_str[level][0] = (uint8_t)y_strength;
+  r->cdef_str[level][1] = (uint8_t)uv_strength;
+  return 0;
+}
+
 /* the block map of block (bx, by) of the level-l grid */
 static void map_block(orc_replay *r, int l, int gx, int gy, int skip) {
   const int n4 = 16 >> l;
@@ -460,6 +476,41 @@ static void deblock_planes(orc_replay *r) {
   for (int p = 0; p < 3; p++)
     orc_deblock_plane(org_of(pl[p], r->hbd), pl[p]->stride, r->hbd, r->bd, r->W, r->H,
                       p ? r->xdec : 0, p ? r->ydec : 0, p, r->mi_lg, r->mi_skip, r->mi_cols, lv4);
+}
+
+/* cdef_filter_frame (src/encoder.rs:2795-2802) of the frame just coded,
+ * from a copy of its deblocked planes back into them */
+static void cdef_planes(orc_replay *r) {
+  oslot *S = &r->slots[r->fi.display % NSLOT];
+  oplane *pl[3] = {&S->y, &S->u, &S->v};
+  const void *in[3];
+  void *out[3];
+  ptrdiff_t ist[3], ost[3];
+  for (int p = 0; p < 3; p++) {
+    const size_t rowb = (size_t)pl[p]->w * px_of(r);
+    uint8_t *c = malloc(rowb * pl[p]->h);
+    const uint8_t *o = org_of(pl[p], r->hbd);
+    for (int y = 0; y < pl[p]->h; y++)
+      memcpy(c + y * rowb, o + (size_t)y * pl[p]->stride * px_of(r), rowb);
+    in[p] = c;
+    ist[p] = pl[p]->w;
+    out[p] = org_of(pl[p], r->hbd);
+    ost[p] = pl[p]->stride;
+  }
+  uint8_t ys[8] = {0}, us[8] = {0};
+  ys[0] = r->cdef_str[r->fi.level][0];
+  us[0] = r->cdef_str[r->fi.level][1];
+  uint8_t *idx = calloc((size_t)((r->W + 63) / 64) * ((r->H + 63) / 64), 1);
+  orc_cdef_filter_frame(in, ist, out, ost, r->hbd, r->bd, r->W, r->H, r->xdec, r->ydec,
+                        r->mi_skip, r->mi_cols, idx, ys, us, 3, NULL, NULL);
+  free(idx);
+  for (int p = 0; p < 3; p++) free((void *)in[p]);
+}
+
+/* the loop filters in rav1e's order (src/encoder.rs:2789-2802) */
+static void loop_filter_planes(orc_replay *r) {
+  deblock_planes(r);
+  if (r->cdef) cdef_planes(r);
 }
 
 static void pad(const orc_replay *r, oplane *p) {
@@ -1296,7 +1347,7 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
   for (int pass = 0; pass < 4; pass++) run_pass(r, pass);
   if (r->deblock) {
     map_own(r);
-    if (pad_recon) deblock_planes(r);  /* tile groups: after the imports */
+    if (pad_recon) loop_filter_planes(r);  /* tile groups: after the imports */
   }
   r->tail[3] = (uint64_t)(r->vis_w / 8) * (r->vis_h / 8);
   if (pad_recon) {
@@ -1365,7 +1416,7 @@ int64_t orc_replay_xcopy(orc_replay *r, const int32_t *gr, void *buf, int to_buf
 /* Pad the last coded frame (after every group's region is in). */
 void orc_replay_pad_recon(orc_replay *r) {
   oslot *s = &r->slots[r->fi.display % NSLOT];
-  if (r->deblock && !r->fi.is_key) deblock_planes(r);
+  if (r->deblock && !r->fi.is_key) loop_filter_planes(r);
   pad(r, &s->y);
   pad(r, &s->u);
   pad(r, &s->v);

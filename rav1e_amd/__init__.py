@@ -74,7 +74,7 @@ class RvReplayCfg(C.Structure):
 
 class RvReplayLevelParams(C.Structure):
     _fields_ = [("base_q_idx", C.c_int32), ("dc_delta_q", C.c_int32 * 3),
-                ("ac_delta_q", C.c_int32 * 3), ("reserved", C.c_int32), ("lambda_", C.c_double),
+                ("ac_delta_q", C.c_int32 * 3), ("cdef_strengths", C.c_int32), ("lambda_", C.c_double),
                 ("me_lambda", C.c_double), ("dist_scale", C.c_double * 3)]
 
     @classmethod
@@ -85,6 +85,7 @@ class RvReplayLevelParams(C.Structure):
             p.dc_delta_q[i], p.ac_delta_q[i] = d["dc_delta_q"][i], d["ac_delta_q"][i]
             p.dist_scale[i] = d["dist_scale"][i]
         p.lambda_, p.me_lambda = d["lambda"], d["me_lambda"]
+        p.cdef_strengths = d.get("cdef_y", 0) | d.get("cdef_uv", 0) << 8
         return p
 
 

@@ -607,6 +607,11 @@ struct rv_replay {
   uint8_t *mi_lg = nullptr, *mi_skip = nullptr;  // the deblocking block map
   int mi_stride = 0, mi_cols = 0, mi_rows = 0;
   uint8_t db_level[3] = {0, 0, 0};  // fast level per pyramid level
+  bool cdef = false;                // RV_REPLAY_CDEF
+  RvInput cdef_pre;                 // the deblocked, pre-CDEF frame (the padded copy's source)
+  uint8_t *cdef_dir = nullptr, *cdef_idx = nullptr;  // per 8x8 block; per 64x64 (all 0)
+  int32_t *cdef_var = nullptr;
+  uint8_t cdef_str[3][2] = {};      // [level] = (y, uv) strengths at cdef_index 0
   int32_t *leaf_count = nullptr;  // [kLevels]
   size_t nwords = 0, wpart = 0;   // result words; offset of the partition masks
   bool jobs_built = false;
@@ -1005,6 +1010,28 @@ int deblock_slot(rv_replay *r, const RvSlot &s, int lv) {
   return RV_OK;
 }
 
+// cdef_filter_frame of a deblocked slot (src/encoder.rs:2795-2802): the
+// slot is copied to the pre-CDEF frame, the directions come from its luma,
+// and every plane is filtered back into the slot.  cdef_bits 0: every
+// superblock uses entry 0 of the tables, the level's strengths.
+int cdef_slot(rv_replay *r, const RvSlot &s, int lv) {
+  const rv_plane dst[3] = {s.y, s.u, s.v};
+  const rv_plane pre[3] = {r->cdef_pre.y, r->cdef_pre.u, r->cdef_pre.v};
+  for (int p = 0; p < 3; p++)
+    if (hipMemcpyAsync(pre[p].data, dst[p].data, plane_bytes(dst[p]), hipMemcpyDeviceToDevice,
+                       r->stream) != hipSuccess)
+      return rv_set_error(RV_EHIP, "cdef_slot: hipMemcpyAsync");
+  uint8_t ys[8] = {}, us[8] = {};
+  ys[0] = r->cdef_str[lv][0];
+  us[0] = r->cdef_str[lv][1];
+  int e = rv_cdef_find_dirs(&pre[0], r->g.W, r->g.H, r->mi_skip, r->mi_stride, r->cdef_dir,
+                            r->cdef_var, r->g.bd, r->stream);
+  for (int p = 0; p < 3 && e == RV_OK; p++)  // cdef_damping = 3 (src/encoder.rs:665)
+    e = rv_cdef_filter_plane(&pre[p], &dst[p], p, r->g.W, r->g.H, r->mi_skip, r->mi_stride,
+                             r->cdef_dir, r->cdef_var, r->cdef_idx, ys, us, 3, r->g.bd, r->stream);
+  return e;
+}
+
 // Coding order of the reorder pyramid: coded frame n >= 1 (n = 0 is the
 // key frame, display 0).
 void frame_info(long n, int R, rv_replay_frame_info *f) {
@@ -1201,6 +1228,21 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
     }
   }
   r->words = (uint64_t *)dalloc(r, r->nwords * 8);
+  if (cfg->flags & RV_REPLAY_CDEF) {
+    if (!(cfg->flags & RV_REPLAY_DEBLOCK) || (g.W & 7) || (g.H & 7)) {
+      rv_set_error(RV_EINVAL, "rv_replay_create: RV_REPLAY_CDEF needs RV_REPLAY_DEBLOCK and a "
+                              "frame size that is a multiple of 8");
+      rv_replay_destroy(r);
+      return nullptr;
+    }
+    r->cdef = true;
+    const size_t n8 = (size_t)(g.W / 8) * (g.H / 8), n64 = (size_t)((g.W + 63) / 64) * ((g.H + 63) / 64);
+    r->cdef_dir = (uint8_t *)dalloc(r, n8);
+    r->cdef_var = (int32_t *)dalloc(r, n8 * 4);
+    r->cdef_idx = (uint8_t *)dalloc(r, n64);
+    ok = ok && r->cdef_dir && r->cdef_var && r->cdef_idx && alloc_input(r, r->cdef_pre);
+    if (r->cdef_idx) (void)hipMemsetAsync(r->cdef_idx, 0, n64, r->stream);
+  }
   if (cfg->flags & RV_REPLAY_DEBLOCK) {
     r->deblock = true;
     r->mi_cols = (g.W + 3) / 4;
@@ -1284,6 +1326,10 @@ int rv_replay_set_level_params(rv_replay *r, int level, const rv_replay_level_pa
   // deblock_filter_optimize's fast levels (inter frames; speed 6 would search
   // them by SSE, sse_optimize -- not built, the fast levels stand in)
   r->db_level[level] = (uint8_t)rv_deblock_fast_level(rv_q_lookup(1, p->base_q_idx, bd), bd, 0);
+  r->cdef_str[level][0] = (uint8_t)(p->cdef_strengths & 0xff);
+  r->cdef_str[level][1] = (uint8_t)((p->cdef_strengths >> 8) & 0xff);
+  if (r->cdef_str[level][0] > 63 || r->cdef_str[level][1] > 63)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_level_params: cdef strength above 63");
   L.lambda = p->lambda;
   L.me_lambda = p->me_lambda;
   for (int i = 0; i < 3; i++) L.ds[i] = p->dist_scale[i];
@@ -1433,6 +1479,7 @@ int rv_replay_import(rv_replay *r) {
   // the whole frame and its block map are in: deblock it (every rank the
   // same way), then pad
   if (r->deblock) RV_R(deblock_slot(r, s, r->last.level));
+  if (r->cdef) RV_R(cdef_slot(r, s, r->last.level));
   return pad_slot(r, s);
 }
 
@@ -1792,6 +1839,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   r->last = fi;
   if (r->n_groups < 2) {
     if (r->deblock) RV_R(deblock_slot(r, S, lv));
+    if (r->cdef) RV_R(cdef_slot(r, S, lv));
     RV_R(pad_slot(r, S));
   } else {
     XRect xr[5];

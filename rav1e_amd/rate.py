@@ -9,6 +9,8 @@ from __future__ import annotations
 import bisect
 import math
 
+import numpy as np
+
 from . import lib
 
 MASK64 = (1 << 64) - 1
@@ -171,10 +173,37 @@ def frame_params(quantizer: int, bit_depth: int, fti: int) -> dict:
     # FrameInvariants::set_quantizers: lambda scaled by 1 << 2 (bd - 8),
     # me_lambda = sqrt(lambda) (src/encoder.rs:865-880)
     lam = lambdas[0] * float(1 << (2 * (bit_depth - 8)))
-    return {"base_q_idx": base,
+    cdef_y, cdef_uv = cdef_strengths(log_q)
+    return {"base_q_idx": base, "cdef_y": cdef_y, "cdef_uv": cdef_uv,
             "dc_delta_q": [d - base for d in dc_qis], "ac_delta_q": [a - base for a in ac_qis],
             "lambda": lam, "me_lambda": math.sqrt(lam),
             "dist_scale": [1.0, lambdas[0] / lambdas[1], lambdas[0] / lambdas[2]]}
+
+
+def _f32_poly(q, a, b, c, neg_sq):
+    """clamp-free ((+/-)q*q*a + q*b + c).round() in f32 arithmetic, left to
+    right like the reference's expression (no fused multiply-add)."""
+    f = np.float32
+    sq = (f(-q) if neg_sq else q) * q * f(a)
+    v = f(f(sq) + f(q * f(b))) + f(c)
+    v = float(f(v))
+    return int(math.floor(abs(v) + 0.5)) * (1 if v >= 0 else -1)  # f32::round: half away
+
+
+def cdef_strengths(log_target_q: int):
+    """FrameInvariants::set_quantizers' CDEF strengths of an inter frame
+    (src/encoder.rs:882-912, the !intra_only branch): q = bexp64(
+    log_target_q + q57(QSCALE)) as f32, libaom-trained polynomials,
+    cdef_y_strengths[0] / cdef_uv_strengths[0] = f1 * CDEF_SEC_STRENGTHS + f2."""
+    q = np.float32(bexp64(log_target_q + q57(QSCALE)))
+
+    def cl(v, hi):
+        return min(max(v, 0), hi)
+    y1 = cl(_f32_poly(q, 0.0000023593946, 0.0068615186, 0.02709886, True), 15)
+    y2 = cl(_f32_poly(q, 0.00000057629734, 0.0013993345, 0.03831067, True), 3)
+    u1 = cl(_f32_poly(q, 0.0000007095069, 0.0034628846, 0.00887099, True), 15)
+    u2 = cl(_f32_poly(q, 0.00000023874085, 0.00028223585, 0.05576307, False), 3)
+    return y1 * 4 + y2, u1 * 4 + u2
 
 
 def level_params(quantizer: int, bit_depth: int, levels: int = 3) -> list:

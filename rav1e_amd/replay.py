@@ -22,6 +22,7 @@ DEFAULT_QUANTIZER = 100  # rav1e's default --quantizer (src/api/config.rs)
 RV_REPLAY_EXHAUSTIVE_FS = 4  # F1 without successive elimination (same results)
 RV_REPLAY_SPEED6 = 8  # the speed-6 schedule: partition RDO 64x64 .. 8x8 (config D)
 RV_REPLAY_DEBLOCK = 16  # deblock every coded frame before it becomes a reference (1 group)
+RV_REPLAY_CDEF = 32  # CDEF after deblocking (needs RV_REPLAY_DEBLOCK), cdef_bits 0
 # HIP-event stages of a frame: F0, F1, F2, FL (lookahead), F3 full-pel, F3
 # sub-pel, F4 single, F4 compound, F4 argmin, F6 commit, F5, F7
 N_STAGES = 13

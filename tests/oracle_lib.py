@@ -478,7 +478,7 @@ class CpuReplay:
 
     def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, group=None,
                  tile_size=(0, 0), n_inputs=8, threads=1, L=None, quantizer=100, speed=10,
-                 deblock=False):
+                 deblock=False, cdef=False):
         from rav1e_amd import rate as RT
         L = L or lib()
         self.L = L
@@ -510,7 +510,10 @@ class CpuReplay:
         self.n_words = result_words(width, height, n_refs, tw, th, tx0, ty0, speed)
         self.geom = (width, height, xdec, ydec, bit_depth)
         self.levels = RT.level_params(quantizer, bit_depth)
+        L.orc_replay_set_cdef.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
         for lv, d in enumerate(self.levels):
+            if cdef:
+                assert L.orc_replay_set_cdef(self.h, lv, d["cdef_y"], d["cdef_uv"]) == 0
             assert L.orc_replay_set_level_params(
                 self.h, lv, d["base_q_idx"], I3(*d["dc_delta_q"]), I3(*d["ac_delta_q"]),
                 d["lambda"], d["me_lambda"], D3(*d["dist_scale"])) == 0

@@ -194,6 +194,40 @@ def test_cpu_replay_deblock_changes_the_reference():
     assert (recs[0] != recs[1]).any()
 
 
+def test_cpu_replay_cdef_changes_the_reference():
+    """RV_REPLAY_CDEF: after deblocking, the coded frame is CDEF-filtered
+    (set_quantizers' inter strengths are non-zero at quantizer 100) before
+    it becomes a reference."""
+    from rav1e_amd import rate as RT
+    lv = RT.level_params(100, 8)
+    assert all(d["cdef_y"] > 0 and d["cdef_uv"] >= 0 for d in lv)
+    w, h = 256, 128
+    fr = _frames(w, h, 1, 1, 8, 8)
+    recs = []
+    for cd in (False, True):
+        r = O.CpuReplay(w, h, 1, 1, 8, 2, n_inputs=8, threads=2, deblock=True, cdef=cd)
+        for i, f in enumerate(fr):
+            r.set_input(i, f)
+        r.frame()
+        r.frame()
+        recs.append(r.get_recon(4))
+    assert (recs[0] != recs[1]).any()
+
+
+def test_cdef_strengths_of_set_quantizers():
+    """set_quantizers' inter CDEF polynomials (src/encoder.rs:882-912) at
+    a few quantizers: in range, monotone in q for luma's primary."""
+    from rav1e_amd import rate as RT
+    prev = -1
+    for qz in (20, 60, 100, 160, 255):
+        for bd in (8, 10, 12):
+            d = RT.level_params(qz, bd)[0]
+            assert 0 <= d["cdef_y"] <= 63 and 0 <= d["cdef_uv"] <= 63
+        y = RT.level_params(qz, 8)[0]["cdef_y"] >> 2
+        assert y >= prev
+        prev = y
+
+
 def test_cpu_speed6_partition_and_levels():
     """Speed 6 (config D): thread-invariant words; the 64x64 words keep the
     speed-10 layout; every superblock's partition mask is a valid tree
@@ -253,7 +287,8 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
     c = O.CpuReplay(w, h, xdec, ydec, bd, refs, tile_size=ts, n_inputs=nin,
                     threads=O.cpu_share(), quantizer=quantizer,
                     speed=6 if flags & RP.RV_REPLAY_SPEED6 else 10,
-                    deblock=bool(flags & RP.RV_REPLAY_DEBLOCK))
+                    deblock=bool(flags & RP.RV_REPLAY_DEBLOCK),
+                    cdef=bool(flags & RP.RV_REPLAY_CDEF))
     for i in range(nin):
         c.set_input(i, g.get_input(i))
     if imp is not None:
@@ -287,6 +322,12 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
     (192, 136, 0, 0, 10, 2, None, RP.RV_REPLAY_DEBLOCK),
     (256, 200, 1, 1, 8, 2, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_SPEED6),
     (192, 128, 0, 0, 12, 1, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_SPEED6),
+    # CDEF after deblocking (cdef_filter_frame, cdef_bits 0)
+    (256, 200, 1, 1, 8, 2, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF),
+    (192, 136, 0, 0, 10, 2, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF),
+    (256, 136, 1, 0, 8, 2, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF),
+    (256, 200, 1, 1, 8, 2, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF | RP.RV_REPLAY_SPEED6),
+    (192, 128, 0, 0, 12, 1, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF | RP.RV_REPLAY_SPEED6),
 ])
 def test_gpu_replay_matches_cpu_replay(w, h, xdec, ydec, bd, refs, tiling, flags):
     _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, 10, tiling, flags)
@@ -303,7 +344,8 @@ def test_gpu_replay_importance_bias_and_quantizer(flags):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_DEBLOCK,
-                                   RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_SPEED6])
+                                   RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_SPEED6,
+                                   RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF])
 def test_gpu_tile_groups_exchange(flags):
     """Two GPU tile groups in one process, exchanging reconstructions (with
     deblocking: and block maps) through their device exchange buffers (the
@@ -322,6 +364,7 @@ def test_gpu_tile_groups_exchange(flags):
         g.set_groups(rects, k, None)
     c = O.CpuReplay(w, h, tile_size=ts, n_inputs=14, threads=4,
                     deblock=bool(flags & RP.RV_REPLAY_DEBLOCK),
+                    cdef=bool(flags & RP.RV_REPLAY_CDEF),
                     speed=6 if flags & RP.RV_REPLAY_SPEED6 else 10)
     for i in range(14):
         c.set_input(i, RP.synth_frame(w, h, i))
