@@ -63,8 +63,8 @@ static uint64_t mv_rd_cost(const orc_ds_ctx *c, orc_mv mv) {
     /* predict_inter / get_params, src/predict.rs:267-283 (luma: dec 0) */
     int ys = 3 + c->ref_ydec, xs = 3 + c->ref_xdec;
     int roff = (int)mv.row >> ys, coff = (int)mv.col >> xs;
-    int rf = ((int)mv.row - (roff << ys)) << (4 - ys);
-    int cf = ((int)mv.col - (coff << xs)) << (4 - xs);
+    int rf = ((int)mv.row - roff * (1 << ys)) << (4 - ys);
+    int cf = ((int)mv.col - coff * (1 << xs)) << (4 - xs);
     /* PlaneSlice::clamp, src/frame/plane.rs:521-533 */
     int qx = c->po_x + coff - 3, qy = c->po_y + roff - 3;
     if (qx > c->ref_width) qx = c->ref_width;

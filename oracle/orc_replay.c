@@ -588,8 +588,8 @@ static void predict(const orc_replay *r, const oplane *ref, int po_x, int po_y, 
                     int h, void *dst, int dst_stride) {
   int ys = 3 + ref->ydec, xs = 3 + ref->xdec;
   int roff = (int)mv.row >> ys, coff = (int)mv.col >> xs;
-  int rf = ((int)mv.row - (roff << ys)) << (4 - ys);
-  int cf = ((int)mv.col - (coff << xs)) << (4 - xs);
+  int rf = ((int)mv.row - roff * (1 << ys)) << (4 - ys);
+  int cf = ((int)mv.col - coff * (1 << xs)) << (4 - xs);
   int qx = clamp_i32(po_x + coff - 3, -ref->xo, ref->w) + 3;
   int qy = clamp_i32(po_y + roff - 3, -ref->yo, ref->h) + 3;
   orc_put_8tap(dst, dst_stride, at(ref, r->hbd, qx, qy), ref->stride, w, h, cf, rf, 0, 0, r->bd,
@@ -608,8 +608,8 @@ static void predict_comp(const orc_replay *r, const oplane *ref0, const oplane *
     const oplane *ref = rf[i];
     int ys = 3 + ref->ydec, xs = 3 + ref->xdec;
     int roff = (int)mv[i].row >> ys, coff = (int)mv[i].col >> xs;
-    int rfr = ((int)mv[i].row - (roff << ys)) << (4 - ys);
-    int cfr = ((int)mv[i].col - (coff << xs)) << (4 - xs);
+    int rfr = ((int)mv[i].row - roff * (1 << ys)) << (4 - ys);
+    int cfr = ((int)mv[i].col - coff * (1 << xs)) << (4 - xs);
     int qx = clamp_i32(po_x + coff - 3, -ref->xo, ref->w) + 3;
     int qy = clamp_i32(po_y + roff - 3, -ref->yo, ref->h) + 3;
     orc_prep_8tap(tmp[i], at(ref, r->hbd, qx, qy), ref->stride, w, h, cfr, rfr, 0, 0, r->bd,

@@ -204,13 +204,16 @@ static bool cdef_bd_ok(const rv_plane *p, int bd) {
 
 // cdef_analyze_superblock over the frame (src/cdef.rs:278-317, called per
 // superblock by cdef_filter_frame :622-628): dir / var per 8x8 luma block,
-// pitch ceil(width / 8); skip blocks get dir 0, var 0.
+// pitch ceil(width / 8); skip blocks get dir 0, var 0.  The frame size
+// must be a multiple of 8: rav1e's reconstruction always is (Frame::new
+// aligns it, src/frame/mod.rs:58-59), so a ragged plane has no reference
+// counterpart.
 extern "C" int rv_cdef_find_dirs(const rv_plane *luma, int width, int height,
                                  const uint8_t *d_skip, int mi_stride, uint8_t *d_dir,
                                  int32_t *d_var, int bit_depth, void *stream) {
   const int cols8 = (width + 7) / 8, rows8 = (height + 7) / 8;
-  if (!luma || !d_skip || !d_dir || !d_var || width <= 0 || height <= 0 ||
-      mi_stride < 2 * cols8 || !cdef_bd_ok(luma, bit_depth) || luma->width < width ||
+  if (!luma || !d_skip || !d_dir || !d_var || width <= 0 || height <= 0 || (width & 7) ||
+      (height & 7) || mi_stride < 2 * cols8 || !cdef_bd_ok(luma, bit_depth) || luma->width < width ||
       luma->height < height)
     return rv_set_error(RV_EINVAL, "rv_cdef_find_dirs: bad arguments");
   CdefArgs a = {};
@@ -243,7 +246,8 @@ extern "C" int rv_cdef_filter_plane(const rv_plane *src, const rv_plane *dst, in
                                     const uint8_t *uv_strengths, int damping, int bit_depth,
                                     void *stream) {
   if (!src || !dst || !d_skip || !d_dir || !d_var || !d_cdef_index || !y_strengths ||
-      !uv_strengths || pli < 0 || pli > 2 || width <= 0 || height <= 0 || damping < 0 ||
+      !uv_strengths || pli < 0 || pli > 2 || width <= 0 || height <= 0 || (width & 7) ||
+      (height & 7) || damping < 0 ||
       mi_stride < 2 * ((width + 7) / 8) || !cdef_bd_ok(src, bit_depth) || dst->hbd != src->hbd ||
       src->data == dst->data)
     return rv_set_error(RV_EINVAL, "rv_cdef_filter_plane: bad arguments");

@@ -1073,12 +1073,15 @@ extern "C" {
 
 void rv_replay_destroy(rv_replay *r) {
   if (!r) return;
+  // both streams drain before anything they may still read is freed (an
+  // error return between the lookahead's fork and its join leaves the side
+  // stream running)
   if (r->stream) (void)hipStreamSynchronize(r->stream);
+  if (r->side) (void)hipStreamSynchronize(r->side);
   for (void *p : r->allocs) (void)hipFree(p);
   for (int f = 0; f < rv_replay::kRing; f++)
     for (int i = 0; i < rv_replay::kEv; i++)
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
-  if (r->side) (void)hipStreamSynchronize(r->side);
   if (r->ev_fork) (void)hipEventDestroy(r->ev_fork);
   if (r->ev_join) (void)hipEventDestroy(r->ev_join);
   if (r->side) (void)hipStreamDestroy(r->side);
@@ -1588,6 +1591,16 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     if (r->overlap) RV_H(hipEventRecord(r->ev_join, ls));
   }
   RV_EV(4);
+  // An error return from here on must not leave the lookahead running on
+  // the side stream: the next frame's F1 / F2 rewrite the MVs it reads, and
+  // rv_replay_destroy frees them.  Disarmed once the main stream has joined.
+  struct SideJoin {
+    rv_replay *r;
+    bool armed;
+    ~SideJoin() {
+      if (armed && r->side) (void)hipStreamSynchronize(r->side);
+    }
+  } side_join{r, r->overlap};
   // F3 full-res full-pel diamond -> sub-pel predictor; sub-pel diamond
   // (speed 10: SAD, no hp) -> NEWMV of every superblock and reference
   RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
@@ -1757,6 +1770,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   }
   RV_EV(8);
   if (r->overlap) RV_H(hipStreamWaitEvent(st, r->ev_join, 0));  // the lookahead's MVs
+  side_join.armed = false;
   score_candidates<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, cg, L.lambda, L.ds[1], L.ds[2], r->sub,
                                                      r->l_out,
                                                      r->c_out, r->c_out + nct * 3, ntx_c, r->win,

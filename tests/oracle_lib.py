@@ -9,7 +9,10 @@ import subprocess
 import numpy as np
 
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
-_LIB = os.path.join(ROOT, "oracle", "build", "librav1e_oracle.so")
+# RAV1E_ORACLE_LIB: another build of the same sources (tools/sanitize_oracle.sh
+# points it at the ASan + UBSan one)
+_LIB = os.environ.get("RAV1E_ORACLE_LIB") or os.path.join(ROOT, "oracle", "build",
+                                                           "librav1e_oracle.so")
 _lib = None
 
 

@@ -397,7 +397,8 @@ def test_gpu_tile_groups_exchange(flags):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("config,speed", [("1080p", 10), ("2160p", 10), ("2160p10", 10),
+@pytest.mark.parametrize("config,speed", [("360p", 10), ("1080p", 10), ("2160p", 10),
+                                          ("2160p10", 10),
                                           ("2160p10", 6), ("2160p444", 10)])
 def test_gpu_replay_full_size_gop(config, speed):
     """The key frame and one GOP (me_range_scale 4, 2, 1, 1) at the BASELINE

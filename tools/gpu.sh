@@ -1,0 +1,49 @@
+#!/bin/bash
+# The one GPU-box driver (run it through gpurun from the repo root):
+#
+#   tools/gpu.sh suite TAG            -m gpu suite in one process, smoke(), default bench
+#   tools/gpu.sh tests TAG 'EXPR'     pytest -m gpu -k EXPR
+#   tools/gpu.sh bench TAG CFG... [-- ARGS]   one bench line per config (ARGS to each)
+#   tools/gpu.sh prof TAG CFG [ARGS]  kernel trace + FETCH / WRITE / SQ PMC passes of a
+#                                     short bench run of CFG (one rocprofv3 pass each, the
+#                                     MI355X guide's rule: FETCH_SIZE and WRITE_SIZE do not
+#                                     share a pass)
+#   tools/gpu.sh ubench TAG           tools/ubench binaries (VALU issue rates, PMC calibration)
+#
+# Every step has its own time limit (tools/gpu_step.sh); a crash, abort or
+# timeout stops the call.  Logs and profiles land in gpurun_out/TAG/.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+MODE=$1; TAG=${2:-dev}; shift 2
+export TMPDIR=/tmp
+P="$R/gpurun_out/$TAG"
+mkdir -p "$P"
+PYT="python -u -m pytest $R/tests -x -q -m gpu --timeout 280 --timeout-method thread"
+case "$MODE" in
+  suite)
+    exec bash "$R/tools/gpu_step.sh" \
+      "900 $TAG/pytest_gpu.log $PYT" \
+      "300 $TAG/smoke.log python -c 'import __graft_entry__ as g; g.smoke()'" \
+      "400 $TAG/bench_default.log python $R/bench.py" ;;
+  tests)
+    exec bash "$R/tools/gpu_step.sh" "900 $TAG/pytest_k.log $PYT -v -k '$1'" ;;
+  bench)
+    cfgs=(); while [ $# -gt 0 ] && [ "$1" != "--" ]; do cfgs+=("$1"); shift; done
+    [ "$1" = "--" ] && shift
+    steps=()
+    for c in "${cfgs[@]}"; do steps+=("400 $TAG/bench_$c.log python $R/bench.py --config $c $*"); done
+    exec bash "$R/tools/gpu_step.sh" "${steps[@]}" ;;
+  prof)
+    CFG=${1:-2160p}; shift
+    B="python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 16 --warmup 5 $*"
+    SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
+    exec bash "$R/tools/gpu_step.sh" \
+      "200 $TAG/trace.log cd /tmp && rocprofv3 --kernel-trace --stats -d $P/trace -o run -- $B" \
+      "200 $TAG/fetch.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o run -- $B" \
+      "200 $TAG/write.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $P/write -o run -- $B" \
+      "200 $TAG/sq.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $SQ -d $P/sq -o run -- $B" ;;
+  ubench)
+    exec bash "$R/tools/gpu_step.sh" \
+      "120 $TAG/valu_rates.txt $R/tools/ubench/valu_rates" ;;
+  *)
+    echo "usage: tools/gpu.sh suite|tests|bench|prof|ubench TAG ..." >&2; exit 2 ;;
+esac
