@@ -572,8 +572,8 @@ def deblock_plane(plane: DevicePlane, pli, width, height, lg: np.ndarray, skip: 
     skip = np.ascontiguousarray(skip, dtype=np.uint8)
     if lg.shape != skip.shape or lg.shape[1] < (width + 3) // 4 or lg.shape[0] < (height + 3) // 4:
         raise Rav1eHipError("deblock_plane: lg / skip must cover the frame's 4x4 grid")
-    if not ((lg >= 1) & (lg <= 4)).all():
-        raise Rav1eHipError("deblock_plane: block sizes 8x8 .. 64x64 (lg 1 .. 4)")
+    if not (lg <= 4).all():
+        raise Rav1eHipError("deblock_plane: block sizes 4x4 .. 64x64 (lg 0 .. 4)")
     dl, ds = DeviceBuffer.from_array(lg), DeviceBuffer.from_array(skip)
     lv = np.ascontiguousarray(np.asarray(levels, dtype=np.uint8))
     _check(lib().rv_deblock_plane(C.byref(plane.desc), pli, width, height, dl.ptr, ds.ptr,

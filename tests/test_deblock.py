@@ -1,12 +1,55 @@
-"""Deblocking filter (deblock_plane, src/deblock.rs:1174-1335): the HIP
-kernel (rv_deblock_plane) against the oracle's restatement
-(oracle/orc_deblock.c) on random block layouts, and the oracle's own
-behaviour (a step edge inside the filter's reach is smoothed, level 0 is a
-no-op, the fast levels of deblock_filter_optimize)."""
+"""Deblocking filter (deblock_plane, src/deblock.rs:1174-1335): the oracle's
+restatement (oracle/orc_deblock.c) and the HIP kernel (rv_deblock_plane)
+against vectors made by evaluating the reference's own deblock_plane text
+(tests/golden/ref_deblock.npz, tools/refeval/gen_golden_ref.py deblock: every
+filter size 4/6/8/14, 8/10/12-bit, 4:2:0 / 4:2:2 / 4:4:4, 4x4 .. 64x64
+blocks, skip blocks, per-plane levels incl. 0); the HIP kernel against the
+oracle on larger random layouts; the oracle's own behaviour (a step edge
+inside the filter's reach is smoothed, level 0 is a no-op, the fast levels
+of deblock_filter_optimize)."""
+import os
+
 import numpy as np
 import pytest
 
 from tests import oracle_lib as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "ref_deblock.npz")
+
+
+def _ref_cases():
+    g = np.load(GOLD)
+    off = 0
+    for c in g["cases"]:
+        W, H, xdec, ydec, bd, pli = (int(v) for v in c[:6])
+        levels = [int(v) for v in c[6:10]]
+        m = int(c[10])
+        xd, yd = (xdec, ydec) if pli else (0, 0)
+        pw, ph = (W + xd) >> xd, (H + yd) >> yd
+        n = pw * ph
+        cols, rows = (W + 3) // 4, (H + 3) // 4
+        mo = g["map_off"]
+        lg = g["lg"][mo[m]:mo[m + 1]].reshape(rows, cols)
+        sk = g["skip"][mo[m]:mo[m + 1]].reshape(rows, cols)
+        px = np.uint16 if bd > 8 else np.uint8
+        img = g["px_in"][off:off + n].reshape(ph, pw).astype(px)
+        want = g["px_out"][off:off + n].reshape(ph, pw).astype(px)
+        off += n
+        yield (W, H, xd, yd, bd, pli, levels, lg, sk, img, want)
+
+
+def test_oracle_deblock_vs_reference():
+    n = changed = 0
+    for W, H, xd, yd, bd, pli, levels, lg, sk, img, want in _ref_cases():
+        pad = 16
+        full = np.pad(img, pad, mode="edge")
+        got = O.deblock_plane(full.copy(), pad, pad, W, H, xd, yd, pli, lg, sk, levels, bd)
+        got = got[pad:pad + img.shape[0], pad:pad + img.shape[1]]
+        bad = np.argwhere(got != want)
+        assert bad.size == 0, (W, H, bd, xd, yd, pli, levels, bad[:5])
+        n += 1
+        changed += int((want != img).any())
+    assert n == 24 and changed >= 18
 
 
 def _layout(rng, mi_w, mi_h, min_lg=1):
@@ -85,3 +128,15 @@ def test_deblock_plane_vs_oracle(bd, xdec, ydec, w, h):
             assert bad.size == 0, (trial, pli, levels, bad[:5])
             if trial == 0:
                 assert (got != full).any()  # something was filtered
+
+
+@pytest.mark.gpu
+def test_deblock_plane_vs_reference():
+    import rav1e_amd as R
+    R.require_device(0)
+    for W, H, xd, yd, bd, pli, levels, lg, sk, img, want in _ref_cases():
+        dp = R.DevicePlane.from_array(img, xpad=88 >> xd, ypad=88 >> yd, xdec=xd, ydec=yd)
+        R.deblock_plane(dp, pli, W, H, lg, sk, levels, bd)
+        got = dp.download_visible()
+        bad = np.argwhere(got != want)
+        assert bad.size == 0, (W, H, bd, xd, yd, pli, levels, bad[:5])

@@ -12,6 +12,7 @@ reference itself is not read at test time: the fixtures are data.
 Unmarked tests pin the CPU oracle (oracle/) to those vectors; the `gpu`
 tests pin the HIP path (through the C ABI) to the same vectors.
 """
+import json
 import os
 
 import numpy as np
@@ -364,3 +365,49 @@ def test_hip_diamond_subpel_vs_reference(R, bd):
             got = R.telescopic_subpel_batch(po, pr, jobs, st, w, h, bool(satd), bool(hp), bd)[0]
         want = (g[k + "mv"][n][0], g[k + "mv"][n][1], g[k + "cost"][n])
         assert (got["mv_row"], got["mv_col"], got["cost"]) == want, (n, got, want)
+
+
+# ---- rav1e_amd/rate.py (the host side of the fixed-quantizer frame
+# parameters) against the reference's own rate.rs / set_quantizers
+def test_rate_helpers_vs_reference():
+    from rav1e_amd import rate
+    g = np.load(os.path.join(GOLD, "ref_rate.npz"))
+    for v, want in g["bexp"]:
+        assert rate.bexp64(int(v)) == int(want), v
+    for v, want in g["blog"]:
+        assert rate.blog64(int(v)) == int(want), v
+    for v, want in g["q57"]:
+        assert rate.q57(int(v)) == int(want), v
+
+
+def test_cdef_strengths_vs_reference_set_quantizers():
+    """set_quantizers' f32 polynomials (src/encoder.rs:881-911), evaluated
+    by the reference's text, equal rate.cdef_strengths at every
+    log_target_q of the grid (8/10/12-bit)."""
+    from rav1e_amd import rate
+    g = np.load(os.path.join(GOLD, "ref_rate.npz"))
+    seen = set()
+    for bd, lq, y, uv in g["cdef_strengths"]:
+        assert rate.cdef_strengths(int(lq)) == (int(y), int(uv)), (bd, lq)
+        seen.add((int(y), int(uv)))
+    assert len(seen) > 8  # the grid spans many strength pairs
+
+
+# ---- the evaluator itself, on the reference's own unit tests
+def test_interpreter_reproduced_the_reference_kats():
+    """tools/refeval/gen_kat.py ran the reference's own test functions
+    through rsinterp (the evaluator behind every ref_*.npz): the 88 SAD /
+    SATD known answers of src/dist.rs:379-460 (u8 and u16), test_divu_pair
+    / test_tx_log_scale / log_tx_ratios, the transform round-trip tolerances
+    and the intra predictor tests.  Its record must hold the same SAD/SATD
+    table as the reference text (tests/golden/dist_kat.json)."""
+    rec = np.load(os.path.join(GOLD, "ref_kat.npz"))
+    with open(os.path.join(GOLD, "dist_kat.json")) as f:
+        kat = json.load(f)
+    for t in ("u8", "u16"):
+        assert list(rec["dist_sad_" + t]) == kat["sad"]
+        assert list(rec["dist_satd_" + t]) == kat["satd"]
+    assert rec["quant_tests"].tolist() == [1, 1, 1]
+    assert rec["intra_tests"].tolist() == [1, 1]
+    rt = rec["roundtrip"]
+    assert len(rt) >= 2 * 37 * 2 and (rt[:, 3] <= rt[:, 4]).all()

@@ -634,6 +634,64 @@ class _NS:
         self.__dict__.update(kw)
 
 
+def tx_fns(I):
+    """(fwd, inv): the reference's FwdTxfm2D::fht and inv_txfm2d_add bound to
+    one (TxSize, TxType), as gen_tx evaluates them.
+      fwd(ts, tt, residual (list, W*H), bd) -> W-stride raster of W*H ints
+      inv(ts, tt, coeffs (min(W,32)*min(H,32)), dst (H x W array), bd, "u8"|"u16")
+        -> the reconstruction (H x W array)"""
+    f1, i1, ish = tx_tables(I)
+    fwd_src = src_of(I, "transform/forward.rs")
+    inv_src = src_of(I, "transform/inverse.rs")
+    fht = fwd_src.fn("fht", "impl<P, S, T> FwdTxfm2D<P> for (S, T)")
+    itx2 = inv_src.fn("inv_txfm2d", "type ColTxfm = ")
+    itx_add = inv_src.fn("inv_txfm2d_add", "type ColTxfm = ")
+    I.globals.vars["AlignedArray"] = AlignedArray
+    I.globals.vars["round_shift_array"] = I.make_fn(
+        src_of(I, "transform/mod.rs").fn("round_shift_array"), I.globals)
+    I.globals.vars["PixelType"] = _NS(U8=0, U16=1)
+    nocall = [[None] * 4 for _ in range(4)]
+    I.globals.vars["kernels"] = _NS(U8_INV_TX_ADD_KERNELS=[[nocall] * 22],
+                                    U16_INV_TX_ADD_KERNELS=[[nocall] * 22])
+
+    def size_of(ts):
+        w, h = 1 << TX_W_LOG2[ts], 1 << TX_H_LOG2[ts]
+        return w, h, _NS(W=RI.TInt(w, "usize"), H=RI.TInt(h, "usize"), WIDTH=RI.TInt(w, "usize"),
+                         HEIGHT=RI.TInt(h, "usize"), AREA=RI.TInt(w * h, "usize"),
+                         ColSimd=Lane1, RowSimd=Lane1, IColSimd=Lane1,
+                         INTERMEDIATE_SHIFT=RI.TInt(ish[(w, h)], "u16"))
+
+    def fwd(ts, tt, res, bd):
+        w, h, size = size_of(ts)
+        ck, rk = TX_COL[tt], TX_ROW[tt]
+        shift = fwd_src.load_static(I, "FWD_SHIFT_%dX%d" % (w, h))
+        ctx = _NS(Size=size, SHIFT=shift, Col=_NS(FLIPPED=ck == 3), Row=_NS(FLIPPED=rk == 3),
+                  ColTx=_NS(forward=lambda i, o, f=f1[(ck, h)]: f(i, o)),
+                  RowTx=_NS(forward=lambda i, o, f=f1[(rk, w)]: f(i, o)))
+        co = [RI.TInt(0, "i32")] * (w * h)
+        I.make_fn(fht, I.globals)(RI.Slice([RI.TInt(int(v), "i16") for v in res]), RI.Slice(co),
+                                  RI.TInt(bd, "usize"), bind={"Self": ctx, "S": size})
+        return [int(v) for v in co]
+
+    def inv(ts, tt, co, dst, bd, px):
+        w, h, size = size_of(ts)
+        ck, rk = TX_COL[tt], TX_ROW[tt]
+        pd = H.Plane.from_full(np.asarray(dst, np.int64).copy(), 0, 0, w, h)
+        ictx = _NS(Size=size, RowTxfm=_NS(inverse=lambda i, o, r, f=i1[(rk, w)]: f(i, o, r)),
+                   ColTxfm=_NS(inverse=lambda i, o, r, f=i1[(ck, h)]: f(i, o, r)))
+        tt_ns = _NS(Row=_NS(TBL_IDX=0), Col=_NS(TBL_IDX=0), TX_TYPE=tt)
+        inner = I.make_fn(itx2, I.globals)
+        ictx.inv_txfm2d = (lambda *a, _f=inner, _c=ictx, _s=size: _f(*a, bind={"Self": _c, "S": _s}))
+        pt = RI.PrimType(px)
+        pt.type_enum = lambda: 0 if px == "u8" else 1
+        I.make_fn(itx_add, I.globals)(
+            RI.Slice([RI.TInt(int(v), "i32") for v in co] + [RI.TInt(0, "i32")] * 32),
+            region_at(pd, 0, 0), RI.TInt(bd, "usize"), H.base_env()["CpuFeatureLevel"],
+            bind={"Self": ictx, "S": size, "T": tt_ns, "P": pt})
+        return np.array(pd.data, np.int64).reshape(h, w)
+    return fwd, inv
+
+
 def gen_tx(I, rng, out):
     f1, i1, ish = tx_tables(I)
     fwd = src_of(I, "transform/forward.rs")
@@ -797,8 +855,400 @@ def gen_cdef(I, rng, out):
     print("cdef: %d find_dir, %d filter_block, %d adjust" % (len(imgs), len(cases),
                                                              len(adj_cases)))
 
+# ---------------------------------------------------------------- deblocking
+class _RefV(int):
+    def to_index(self):
+        return RI.TInt(int(self) - 1, "usize")
+
+
+class FrameBlocksV:
+    """FrameBlocks (src/context.rs): the Block of every luma 4x4, indexed by
+    PlaneBlockOffset; the fields deblock.rs reads (bsize, txsize, n4_w,
+    n4_h, skip, ref_frames, mode, deblock_deltas)."""
+
+    def __init__(self, cols, rows):
+        self.cols, self.rows = cols, rows
+        self.b = [[None] * cols for _ in range(rows)]
+
+    def place(self, x4, y4, w4, h4, skip, intra):
+        bs = H.BlockSize.from_width_and_height(w4 * 4, h4 * 4)
+        blk = RI.Struct("Block", {
+            "bsize": bs, "txsize": H.TxDims(min(w4 * 4, 64), min(h4 * 4, 64)),
+            "n4_w": RI.TInt(w4, "usize"), "n4_h": RI.TInt(h4, "usize"), "skip": bool(skip),
+            "ref_frames": [_RefV(0 if intra else 1), _RefV(8)],
+            "mode": RI.TInt(0 if intra else 19, "usize"),  # DC_PRED / NEWMV
+            "deblock_deltas": [RI.TInt(0, "i8")] * 4})
+        for y in range(y4, min(y4 + h4, self.rows)):
+            for x in range(x4, min(x4 + w4, self.cols)):
+                self.b[y][x] = blk
+
+    def index_any(self, bo):
+        o = bo._f["0"]
+        return self.b[int(o.y)][int(o.x)]
+
+
+def _deblock_map(rng, cols, rows, min_lg):
+    """A random quadtree of square blocks (64x64 down to 4 << min_lg px):
+    per 4x4, lg = log2(width in 4x4 units) and skip."""
+    lg = np.zeros((rows, cols), np.uint8)
+    sk = np.zeros((rows, cols), np.uint8)
+    intra = np.zeros((rows, cols), np.uint8)
+
+    def split(x, y, l):
+        n = 1 << l
+        if x >= cols or y >= rows:
+            return
+        if l > min_lg and (rng.random() < 0.55 or x + n > cols or y + n > rows):
+            h = n // 2
+            for dy in (0, h):
+                for dx in (0, h):
+                    split(x + dx, y + dy, l - 1)
+            return
+        lg[y:y + n, x:x + n] = l
+        sk[y:y + n, x:x + n] = rng.random() < 0.35
+    for y in range(0, rows, 16):
+        for x in range(0, cols, 16):
+            split(x, y, 4)
+    return lg, sk, intra
+
+
+def _deblock_content(rng, h, w, bd, lg):
+    """Smooth ramps with small steps on the 4x4 grid (inside the filters'
+    masks at moderate levels) + noise."""
+    yy, xx = np.mgrid[0:h, 0:w]
+    base = (xx * rng.uniform(0.2, 2) + yy * rng.uniform(0.2, 2)) + 60
+    step = np.kron(rng.integers(-6, 7, ((h + 3) // 4, (w + 3) // 4)), np.ones((4, 4)))[:h, :w]
+    img = base + step + rng.integers(-2, 3, (h, w))
+    img[:, w // 3: w // 3 + 2] += rng.integers(10, 40)  # a real edge
+    img = img * (1 << (bd - 8))
+    return np.clip(img, 0, (1 << bd) - 1).astype(np.int64)
+
+
+def gen_deblock(I, rng, out):
+    dsrc = RI.Source(REF + "deblock.rs")
+    ctx = RI.Source(REF + "context.rs")
+    I.sources.append(dsrc)
+    I.release = True
+    for n in ("BlockOffset", "PlaneBlockOffset"):
+        I.globals.vars[n] = RI.StructType(n)
+        I.define_impl(n, ctx.impl(n))
+    I.globals.vars.update({
+        "MI_SIZE_LOG2": RI.TInt(2, "usize"), "MI_SIZE": RI.TInt(4, "usize"),
+        "BLOCK_TO_PLANE_SHIFT": RI.TInt(2, "usize"), "SUPERBLOCK_TO_BLOCK_SHIFT": RI.TInt(4, "usize"),
+        "MAX_LOOP_FILTER": RI.TInt(63, "usize"),
+        "INTRA_FRAME": _RefV(0), "NEARESTMV": RI.TInt(14, "usize"),
+        "GLOBALMV": RI.TInt(18, "usize"), "GLOBAL_GLOBALMV": RI.TInt(26, "usize")})
+    dp = F(I, "deblock_plane", "deblock.rs")
+    cases, planes_in, planes_out, lgs, sks = [], [], [], [], []
+    shapes = [(80, 56, 1, 1, 8), (72, 48, 0, 0, 10), (64, 40, 1, 0, 12), (96, 64, 1, 1, 10),
+              (56, 72, 0, 0, 8), (88, 48, 1, 1, 12), (64, 64, 1, 1, 8), (48, 40, 0, 0, 12)]
+    for n, (W_, H_, xdec, ydec, bd) in enumerate(shapes):
+        cols, rows = (W_ + 3) // 4, (H_ + 3) // 4
+        min_lg = 0 if n % 2 else 1
+        lg, sk, _ = _deblock_map(rng, cols, rows, min_lg)
+        fb = FrameBlocksV(cols, rows)
+        for y in range(rows):
+            for x in range(cols):
+                n4 = 1 << int(lg[y, x])
+                if x % n4 == 0 and y % n4 == 0:
+                    fb.place(x, y, n4, n4, sk[y, x], False)
+        levels = [int(v) for v in rng.integers(0, 64, 4)]
+        if n % 3 == 0:
+            levels[int(rng.integers(0, 4))] = 0
+        deb = RI.Struct("DeblockState", {
+            "levels": [RI.TInt(v, "u8") for v in levels], "sharpness": RI.TInt(0, "u8"),
+            "deltas_enabled": False, "delta_updates_enabled": False,
+            "ref_deltas": [RI.TInt(v, "i8") for v in (1, 0, 0, 0, 0, -1, -1, -1)],
+            "mode_deltas": [RI.TInt(0, "i8")] * 2, "block_deltas_enabled": False,
+            "block_delta_shift": RI.TInt(0, "u8"), "block_delta_multi": False})
+        fi = RI.Struct("FrameInvariants", {
+            "width": RI.TInt(W_, "usize"), "height": RI.TInt(H_, "usize"),
+            "sequence": RI.Struct("Sequence", {"bit_depth": RI.TInt(bd, "usize")})})
+        for pli in range(3):
+            xd, yd = (xdec, ydec) if pli else (0, 0)
+            pw, ph = (W_ + xd) >> xd, (H_ + yd) >> yd
+            img = _deblock_content(rng, ph, pw, bd, lg)
+            pad = 8
+            full = np.pad(img, pad, mode="edge")
+            pl = H.Plane.from_full(full, pad, pad, pw, ph, xd, yd)
+            ty = "u8" if bd == 8 else "u16"
+            pl.data = [RI.TInt(v, ty) for v in pl.data]
+            # the callees' `T: Pixel` (inferred by rustc) resolve to the frame's pixel
+            I.globals.vars["T"] = prim(bd)
+            dp(fi, deb, pl, RI.TInt(pli, "usize"), fb, generics={"T": prim(bd)})
+            res = np.array([int(v) for v in pl.data], np.int64).reshape(full.shape)
+            res = res[pad:pad + ph, pad:pad + pw]
+            cases.append((W_, H_, xdec, ydec, bd, pli, *levels, len(lgs)))
+            planes_in.append(img.astype(np.uint16).reshape(-1))
+            planes_out.append(res.astype(np.uint16).reshape(-1))
+            print("  deblock %dx%d %d-bit dec %d%d plane %d levels %s: %d px changed" % (
+                W_, H_, bd, xdec, ydec, pli, levels, int((res != img).sum())))
+        lgs.append(lg.reshape(-1))
+        sks.append(sk.reshape(-1))
+    out["cases"] = np.array(cases, np.int32)
+    out["px_in"] = np.concatenate(planes_in)
+    out["px_out"] = np.concatenate(planes_out)
+    out["lg"] = np.concatenate(lgs)
+    out["skip"] = np.concatenate(sks)
+    out["map_off"] = np.cumsum([0] + [len(v) for v in lgs]).astype(np.int64)
+
+
+# ---------------------------------------------------------------- intra prediction
+INTRA_MODE_NAMES = ["DC_PRED", "V_PRED", "H_PRED", "D45_PRED", "D135_PRED", "D117_PRED",
+                    "D153_PRED", "D207_PRED", "D63_PRED", "SMOOTH_PRED", "SMOOTH_V_PRED",
+                    "SMOOTH_H_PRED", "PAETH_PRED", "UV_CFL_PRED", "NEARESTMV", "NEAR0MV",
+                    "NEAR1MV", "NEAR2MV", "GLOBALMV", "NEWMV"]
+
+
+class PModeV(int):
+    """A PredictionMode value (src/predict.rs:135-165 order); predict_intra
+    runs the reference's method text (bound by intra_env)."""
+    predict_fn = None
+    pixel = None
+
+    def is_intra(self):
+        return int(self) < 14
+
+    def predict_intra(self, *a):
+        return PModeV.predict_fn(self, *a, generics={"T": PModeV.pixel})
+
+
+class _PVariant:
+    """PredictionVariant (src/predict.rs:168-184)."""
+    NONE, LEFT, TOP, BOTH = 0, 1, 2, 3
+
+    @staticmethod
+    def new(x, y):
+        x, y = int(x), int(y)
+        return 0 if (x, y) == (0, 0) else 1 if y == 0 else 2 if x == 0 else 3
+
+
+def intra_env(I):
+    """Bind the reference's intra predictors: PredictionMode::predict_intra
+    (src/predict.rs:202-241), native::predict_intra_inner (:538-597) and the
+    Intra trait's default methods (:599-1034) per block size, and
+    get_intra_edges (src/partition.rs:500-693)."""
+    if getattr(I, "_intra", False):
+        return
+    I._intra = True
+    pr = RI.Source(REF + "predict.rs")
+    part = RI.Source(REF + "partition.rs")
+    I.sources += [pr, part]
+    ns = type("PredictionModeNS", (), {n: PModeV(i) for i, n in enumerate(INTRA_MODE_NAMES)})
+    I.globals.vars["PredictionMode"] = ns
+    I.globals.vars["PredictionVariant"] = _PVariant
+    I.globals.vars["MAX_TX_SIZE"] = RI.TInt(64, "usize")  # src/context.rs:49
+    I.globals.vars["MI_SIZE_LOG2"] = RI.TInt(2, "usize")
+    I.globals.vars["size_of"] = lambda *a, **k: RI.TInt(1, "usize")
+    I.globals.vars["AlignedArray"] = AlignedArray
+    I.globals.vars["TileRect"] = RI.StructType("TileRect")
+    for n in ("BlockOffset", "TileBlockOffset", "PlaneOffset"):
+        I.globals.vars.setdefault(n, RI.StructType(n))
+    trait = "pub trait Intra<T>: Dim"
+    meths = ["pred_dc", "pred_dc_128", "pred_dc_left", "pred_dc_top", "pred_h", "pred_v",
+             "pred_paeth", "pred_smooth", "pred_smooth_h", "pred_smooth_v", "pred_directional"]
+    tfn = {m: I.make_fn(pr.fn(m, trait), I.globals) for m in meths}
+    cache = {}
+
+    def block_ns(w, h):
+        if (w, h) not in cache:
+            size = _NS(W=RI.TInt(w, "usize"), H=RI.TInt(h, "usize"))
+            b = _NS(W=size.W, H=size.H)
+            for m, f in tfn.items():
+                setattr(b, m, lambda *a, _f=f, _s=size: _f(*a, bind={"Self": _s, "T": PModeV.pixel}))
+            cache[(w, h)] = b
+        return cache[(w, h)]
+    inner = I.make_fn(pr.fn("predict_intra_inner", "pub(crate) mod native"), I.globals)
+
+    def dispatch(mode, variant, dst, tx_size, bit_depth, ac, angle, edge_buf, cpu):
+        # impl_intra!'s table (src/predict.rs:506-535): TX_WxH -> Block WxH
+        b = block_ns(int(tx_size.width()), int(tx_size.height()))
+        return inner(mode, variant, dst, bit_depth, ac, angle, edge_buf,
+                     generics={"T": PModeV.pixel}, bind={"B": b})
+    I.globals.vars["dispatch_predict_intra"] = dispatch
+    for n in H.BLOCK_NAMES:  # `use BlockSize::*` in partition.rs
+        I.globals.vars["BLOCK_" + n] = getattr(H.BlockSize, "BLOCK_" + n)
+    I.globals.vars["TxSize"] = type("TxSizeNS", (), {
+        "TX_%dX%d" % (1 << TX_W_LOG2[i], 1 << TX_H_LOG2[i]): TxSizeV(i) for i in range(19)})
+    PModeV.predict_fn = I.make_fn(pr.fn("predict_intra", "impl PredictionMode"), I.globals)
+    I.globals.vars["get_intra_edges"] = (lambda *a, _f=I.make_fn(part.fn("get_intra_edges"),
+                                                                 I.globals):
+                                         _f(*a, generics={"T": PModeV.pixel}))
+
+
+# ---------------------------------------------------------------- lookahead
+class _MapV:
+    """BTreeMap<u64, V> as ContextInner uses it (get_mut / remove / insert /
+    index)."""
+
+    def __init__(self, d):
+        self.d = d
+
+    def get_mut(self, k):
+        return self.d.get(int(RI.deref(k)))
+
+    def remove(self, k):
+        return self.d.pop(int(RI.deref(k)), None)
+
+    def insert(self, k, v):
+        self.d[int(RI.deref(k))] = v
+
+    def index_any(self, k):
+        return self.d[int(RI.deref(k))]
+
+
+class _FrameTypeNS:
+    KEY, INTER = 0, 1
+
+
+def gen_lookahead(I, rng, out):
+    """compute_lookahead_intra_costs (src/api/internal.rs:678-765) and
+    compute_block_importances (:823-1077) as methods of a host ContextInner:
+    three frames of a moving synthetic clip, output 0 = the current frame
+    (KEY, referenced by 1 and 2), 1 references 0, 2 references 0 and 1 (two
+    unique references: the propagation splits in half).  Recorded: every
+    frame's intra costs, frame 1's block importances after frame 2
+    propagated into it (pure f32 propagation) and frame 0's final values
+    (after its log2)."""
+    intra_env(I)
+    api = RI.Source(REF + "api/internal.rs")
+    I.sources.append(api)
+    I.globals.vars["FrameType"] = _FrameTypeNS
+    I.globals.vars["ArrayVec"] = type("ArrayVecNS", (), {"new": staticmethod(lambda: [])})
+    I.globals.vars["IMPORTANCE_BLOCK_SIZE"] = RI.TInt(8, "usize")
+    satd_ref = F(I, "get_satd_ref")
+    intra_m = I.make_fn(api.fn("compute_lookahead_intra_costs"), I.globals)
+    imp_m = I.make_fn(api.fn("compute_block_importances"), I.globals)
+    for bd, W_, H_ in ((8, 64, 48), (10, 56, 40)):
+        PModeV.pixel = prim(bd)
+        I.globals.vars["T"] = prim(bd)
+        I.globals.vars["get_satd"] = lambda *a, _g={"T": prim(bd)}: satd_ref(*a, generics=_g)
+        w_imp, h_imp = W_ // 8, H_ // 8
+        pad = 48
+        planes, frames = [], []
+        base = rng.integers(0, 1 << bd, (H_ + 2 * pad + 16, W_ + 2 * pad + 16))
+        base = (np.cumsum(np.cumsum(base, 0), 1) // 97) % (1 << bd)  # smooth-ish texture
+        for t in range(3):
+            img = base[8 + t: 8 + t + H_, 8 + 2 * t: 8 + 2 * t + W_].copy()
+            img = np.clip(img + rng.integers(-3, 4, img.shape), 0, (1 << bd) - 1)
+            if t == 2:
+                img[8:24, 16:40] = (1 << bd) - 1 - img[8:24, 16:40]  # an occlusion
+            full = np.pad(img, pad, mode="edge")
+            pl = H.Plane.from_full(full, pad, pad, W_, H_)
+            ty = "u8" if bd == 8 else "u16"
+            pl.data = [RI.TInt(int(v), ty) for v in pl.data]
+            pl.clone = (lambda _p=pl: H.Plane(_p.cfg, list(_p.data)))
+            planes.append(img)
+            frames.append(RI.Struct("Frame", {"planes": [pl]}))
+        fis = {}
+        for t in range(3):
+            mvs = rng.integers(-20, 21, (h_imp * 2, w_imp * 2, 2))
+            mvs[..., 0] += -8 * t  # rows
+            mvs[..., 1] += -16 * t
+            lmv = [[[H.motion_vector(int(m[0]), int(m[1])) for m in row] for row in mvs],
+                   [[H.motion_vector(int(m[0]) // 2, int(m[1]) // 2) for m in row] for row in mvs]]
+            refs = {0: [0] * 7, 1: [0] * 7, 2: [0, 1, 0, 1, 0, 0, 0]}[t]
+            rec = {0: RI.Struct("Ref", {"frame": frames[0], "output_frameno": RI.TInt(0, "u64")}),
+                   1: RI.Struct("Ref", {"frame": frames[1], "output_frameno": RI.TInt(1, "u64")})}
+            fis[t] = RI.Struct("FrameInvariants", {
+                "invalid": False, "show_existing_frame": False,
+                "input_frameno": RI.TInt(t, "u64"),
+                "frame_type": _FrameTypeNS.KEY if t == 0 else _FrameTypeNS.INTER,
+                "w_in_imp_b": RI.TInt(w_imp, "usize"), "h_in_imp_b": RI.TInt(h_imp, "usize"),
+                "sequence": RI.Struct("Sequence", {"bit_depth": RI.TInt(bd, "usize")}),
+                "cpu_feature_level": 0,
+                "lookahead_intra_costs": [RI.TInt(0, "u32")] * (w_imp * h_imp),
+                "block_importances": [np.float32(0)] * (w_imp * h_imp),
+                "lookahead_mvs": lmv,
+                "ref_frames": [RI.TInt(v, "u8") for v in refs],
+                "rec_buffer": RI.Struct("RFS", {"frames": [rec.get(v) for v in range(8)]})})
+        fq = _MapV({t: frames[t] for t in range(3)})
+        ctx = RI.Struct("ContextInner", {
+            "frame_invariants": _MapV(fis), "frame_q": fq,
+            "config": RI.Struct("EncoderConfig", {"bit_depth": RI.TInt(bd, "usize")}),
+            "output_frameno": RI.TInt(0, "u64")})
+        ctx._f["get_rdo_lookahead_frames"] = lambda: RI.It(
+            iter([(RI.TInt(t, "u64"), fis[t]) for t in range(3)]))
+        for t in range(3):
+            intra_m(ctx, RI.TInt(t, "u64"))
+        f1_imp = []
+
+        # capture frame 1's importances once frame 2 has propagated into it:
+        # the loop visits 2 then 1; frame 1 is removed from the map when its
+        # own turn comes, so snapshot at that moment
+        orig_remove = ctx._f["frame_invariants"].remove
+
+        def remove(k, _o=orig_remove):
+            if int(RI.deref(k)) == 1:
+                f1_imp.append([float(v) for v in fis[1]._f["block_importances"]])
+            return _o(k)
+        ctx._f["frame_invariants"].remove = remove
+        imp_m(ctx)
+        k = "la_bd%d_" % bd
+        out[k + "frames"] = np.array(planes, np.uint16)
+        out[k + "mvs"] = np.array([[[[int(m.row), int(m.col)] for m in row] for row in l]
+                                   for l in fis[2]._f["lookahead_mvs"]], np.int16)
+        out[k + "mvs1"] = np.array([[[int(m.row), int(m.col)] for m in row]
+                                    for row in fis[1]._f["lookahead_mvs"][0]], np.int16)
+        out[k + "intra"] = np.array([[int(v) for v in fis[t]._f["lookahead_intra_costs"]]
+                                     for t in range(3)], np.uint32)
+        out[k + "imp1"] = np.array(f1_imp[0], np.float32)
+        out[k + "imp0"] = np.array([float(v) for v in fis[0]._f["block_importances"]], np.float32)
+        print("lookahead bd%d: intra costs %s..., imp1 sum %.3f, imp0 max %.3f" % (
+            bd, out[k + "intra"][0][:4], out[k + "imp1"].sum(), out[k + "imp0"].max()))
+
+
+# ---------------------------------------------------------------- rate / set_quantizers
+def gen_rate(I, rng, out):
+    """bexp64 / blog64 / q57 (src/rate.rs) over a grid, and
+    FrameInvariants::set_quantizers (src/encoder.rs:865-935) on a host
+    FrameInvariants: the CDEF strengths of inter frames (f32 polynomials)
+    and lambda / me_lambda, for log_target_q values around rav1e's range."""
+    rate = RI.Source(REF + "rate.rs")
+    enc = RI.Source(REF + "encoder.rs")
+    I.sources += [rate]
+    I.globals.vars["CDEF_SEC_STRENGTHS"] = RI.TInt(4, "u8")
+    bexp, blog = F(I, "bexp64", "rate.rs"), F(I, "blog64", "rate.rs")
+    q57 = F(I, "q57", "rate.rs")
+    logs = [0, 1, 7, 100, 1 << 20, (1 << 57) - 1, 3 << 56, -(1 << 57), 123456789012345678,
+            -987654321098765]
+    logs += [int(v) for v in rng.integers(-(1 << 59), 1 << 59, 40)]
+    out["bexp"] = np.array([(v, int(bexp(RI.TInt(v, "i64")))) for v in logs], np.int64)
+    ws = [1, 2, 3, 36, 55, 129, 1000, 65535, 1 << 40] + [int(v) for v in
+                                                         rng.integers(1, 1 << 62, 30)]
+    out["blog"] = np.array([(v, int(blog(RI.TInt(v, "i64")))) for v in ws], np.int64)
+    out["q57"] = np.array([(v, int(q57(RI.TInt(v, "i32")))) for v in range(-8, 30)], np.int64)
+    sq = I.make_fn(enc.fn("set_quantizers", "impl<T: Pixel> FrameInvariants<T>"), I.globals)
+    I.globals.vars["clamp"] = I.make_fn(RI.Source(REF + "util/mod.rs").fn("clamp"), I.globals)
+    rows = []
+    for bd in (8, 10, 12):
+        qlo = int(blog(RI.TInt(4, "i64")))
+        qhi = int(blog(RI.TInt(30000, "i64")))
+        for lq in list(np.linspace(qlo, qhi, 24).astype(np.int64)) + \
+                [int(v) for v in rng.integers(qlo, qhi, 16)]:
+            lq = int(lq) - int(q57(RI.TInt(3, "i32")))  # log_target_q = blog64(q) - q57(QSCALE)
+            fi = RI.Struct("FrameInvariants", {
+                "base_q_idx": RI.TInt(0, "u8"), "dc_delta_q": [RI.TInt(0, "i8")] * 3,
+                "ac_delta_q": [RI.TInt(0, "i8")] * 3, "lambda": 0.0, "me_lambda": 0.0,
+                "dist_scale": [0.0] * 3, "intra_only": False,
+                "cdef_y_strengths": [RI.TInt(0, "u8")] * 8,
+                "cdef_uv_strengths": [RI.TInt(0, "u8")] * 8,
+                "sequence": RI.Struct("Sequence", {"bit_depth": RI.TInt(bd, "usize")})})
+            lam = float(rng.uniform(1, 4000))
+            qps = RI.Struct("QuantizerParameters", {
+                "log_base_q": RI.TInt(lq, "i64"), "log_target_q": RI.TInt(lq, "i64"),
+                "dc_qi": [RI.TInt(100, "u8")] * 3, "ac_qi": [RI.TInt(100, "u8")] * 3,
+                "lambda": lam, "dist_scale": [1.0, 1.0, 1.0]})
+            sq(fi, qps)
+            rows.append((bd, lq, int(fi._f["cdef_y_strengths"][0]),
+                         int(fi._f["cdef_uv_strengths"][0])))
+    out["cdef_strengths"] = np.array(rows, np.int64)
+    print("rate: %d bexp, %d blog, %d set_quantizers" % (len(logs), len(ws), len(rows)))
+
+
 SECTIONS = {"mc": gen_mc, "dist": gen_dist, "rdo": gen_rdo, "me": gen_me, "quant": gen_quant,
-            "tx": gen_tx, "ds": gen_ds, "cdef": gen_cdef}
+            "tx": gen_tx, "ds": gen_ds, "cdef": gen_cdef, "deblock": gen_deblock,
+            "lookahead": gen_lookahead, "rate": gen_rate}
 
 
 def main(argv):
@@ -807,8 +1257,9 @@ def main(argv):
     for n in names:
         I = make_interp()
         # the sections that predate cdef keep the seeds they were generated with
-        old = sorted(set(SECTIONS) - {"cdef"})
-        rng = np.random.default_rng(0x5EED + (old.index(n) if n in old else 100))
+        old = sorted(set(SECTIONS) - {"cdef", "deblock", "lookahead", "rate"})
+        rng = np.random.default_rng(0x5EED + (old.index(n) if n in old else
+                                              100 + sorted(set(SECTIONS) - set(old)).index(n)))
         random.seed(1)
         out = {}
         t = time.time()

@@ -39,6 +39,32 @@ class BlockSizeV(int):
     def area(self):
         return TInt(self.w * self.h, "usize")
 
+    def width_mi(self):
+        return TInt(self.w >> 2, "usize")
+
+    def height_mi(self):
+        return TInt(self.h >> 2, "usize")
+
+    def largest_chroma_tx_size(self, xdec, ydec):
+        """src/partition.rs:288-297: subsampled_size -> max_txsize_rect_lookup
+        -> av1_get_coded_tx_size (a 64-point dimension codes as 32)."""
+        w = max(4, self.w >> int(xdec))
+        h = max(4, self.h >> int(ydec))
+        return TxDims(min(w, 32), min(h, 32))
+
+
+class TxDims:
+    """A TxSize by its dimensions (width_mi / height_mi, src/transform/mod.rs)."""
+
+    def __init__(self, w, h):
+        self.w, self.h = w, h
+
+    def width_mi(self):
+        return TInt(self.w >> 2, "usize")
+
+    def height_mi(self):
+        return TInt(self.h >> 2, "usize")
+
 
 class _BlockSizeNS:
     def __init__(self):
@@ -89,9 +115,11 @@ class Plane:
         cfg.xpad, cfg.ypad = xorigin, yorigin
         return cls(cfg, [int(v) for v in full.reshape(-1)])
 
-    # src/frame/plane.rs:316-318
+    # src/frame/plane.rs:316-322
     def slice(self, po):
         return PlaneSlice(self, int(po.x), int(po.y))
+
+    mut_slice = slice
 
     # src/frame/plane.rs:178-187
     def region(self, area):

@@ -20,6 +20,8 @@ method chains, `as` casts, turbofish, macros `assert!`/`debug_assert!`
 (checked) and `cfg!` (false).
 """
 import math
+
+import numpy as np
 import re
 
 # ---------------------------------------------------------------- integers
@@ -49,7 +51,7 @@ def wrap(v, ty):
     if ty == "bool":
         return bool(v)
     bits = INT_BITS[ty]
-    if isinstance(v, float):  # float -> int `as` saturates, NaN -> 0
+    if isinstance(v, (float, np.floating)):  # float -> int `as` saturates, NaN -> 0
         if v != v:
             v = 0
         else:
@@ -82,7 +84,7 @@ _TOK = re.compile(r"""
  (?P<lifetime>'[A-Za-z_]\w*(?!'))|
  (?P<char>'(?:\\.|[^\\'])')|
  (?P<str>"(?:\\.|[^"\\])*")|
- (?P<num>(?:0x[0-9a-fA-F_]+|0b[01_]+|\d[\d_]*(?:\.\d[\d_]*)?(?:[eE][+-]?\d+)?)
+ (?P<num>(?:0x[0-9a-fA-F_]+|0b[01_]+|\d[\d_]*(?:\.\d[\d_]*|\.(?![.\w]))?(?:[eE][+-]?\d+)?)
         (?:_?(?:i8|i16|i32|i64|i128|isize|u8|u16|u32|u64|u128|usize|f32|f64))?)|
  (?P<id>[A-Za-z_]\w*)|
  (?P<punct>\.\.=|\.\.\.|<<=|>>=|::|->|=>|==|!=|<=|>=|&&|\|\||\+=|-=|\*=|/=|%=|\^=|&=|\|=|<<|>>|\.\.|
@@ -126,7 +128,7 @@ def parse_num(text):
     elif body.startswith("0b"):
         v = int(body, 2)
     elif "." in body or "e" in body or "E" in body or suf in FLOATS:
-        return float(body)
+        return np.float32(body) if suf == "f32" else float(body)
     else:
         v = int(body)
     return wrap(v, suf) if suf else v
@@ -381,6 +383,9 @@ class Parser:
     no_or_pat = False
 
     def parse_pattern1(self):
+        if self.eat("&&"):  # `&&pat`: two reference levels
+            self.eat("mut")
+            return ("deref", ("deref", self.parse_pattern1()))
         if self.eat("&"):
             self.eat("mut")
             return ("deref", self.parse_pattern1())
@@ -461,7 +466,18 @@ class Parser:
         self.expect("{")
         stmts, tail = [], None
         while not self.at("}"):
-            self.skip_attrs()
+            # `#[cfg(feature = "...")]` on a statement: the feature is off
+            # (rav1e's default build); a braced statement is skipped unparsed
+            cfg_off = False
+            while self.at("#"):
+                j = self.i
+                self.skip_attrs()
+                if any(x.text == "cfg" for x in self.t[j:self.i]) and \
+                        any(x.text == "feature" for x in self.t[j:self.i]):
+                    cfg_off = True
+            if cfg_off and self.at("{"):
+                self.skip_balanced("{", "}")
+                continue
             if self.at("}"):
                 break
             if self.eat(";"):
@@ -751,7 +767,8 @@ class Parser:
             return ("path", segs)
         if tok.kind == "id":
             return self.parse_path_expr()
-        raise SyntaxError("unexpected token %r" % t)
+        raise SyntaxError("unexpected token %r near: %s" % (
+            t, " ".join(x.text for x in self.t[max(0, self.i - 8):self.i + 8])))
 
     def parse_if(self):
         self.expect("if")
@@ -1301,7 +1318,7 @@ class Interp:
     def ev_un(self, e, env):
         v = deref(self.ev(e[2], env))
         if e[1] == "-":
-            if isinstance(v, float):
+            if isinstance(v, (float, np.floating)):
                 return -v
             return wrap(-int(v), ty_of(v)) if ty_of(v) else -v
         if isinstance(v, bool):
@@ -1322,7 +1339,7 @@ class Interp:
                 name = inner[1][0]
                 scope = env.lookup(name)
                 v = scope.vars[name]
-                if isinstance(v, (int, float, Struct)) or v is None:
+                if isinstance(v, (int, float, np.floating, Struct)) or v is None:
                     return Ref(lambda: scope.vars[name], lambda x: scope.vars.__setitem__(name, x))
                 return v
             if inner[0] == "index":
@@ -1330,7 +1347,7 @@ class Interp:
                 idx = self.ev(inner[2], env)
                 if not isinstance(idx, RangeV):
                     v = index_get(base, idx)
-                    if isinstance(v, (int, float)):
+                    if isinstance(v, (int, float, np.floating)):
                         return index_ref(base, idx)
                     return v
         return self.ev(inner, env)
@@ -1341,9 +1358,11 @@ class Interp:
         if tn in INT_BITS:
             if isinstance(v, bool):
                 v = int(v)
-            if not isinstance(v, (int, float)):
+            if not isinstance(v, (int, float, np.floating)):
                 v = int(v)
             return wrap(v, tn)
+        if tn == "f32":  # IEEE single: every later f32 operation rounds (numpy float32)
+            return np.float32(v)
         if tn in FLOATS:
             return float(v)
         return v
@@ -1373,7 +1392,7 @@ class Interp:
                 return {"==": a is b, "!=": a is not b}[op]
             return {"==": a == b, "!=": a != b, "<": a < b, ">": a > b,
                     "<=": a <= b, ">=": a >= b}[op]
-        if isinstance(a, float) or isinstance(b, float):
+        if isinstance(a, (float, np.floating)) or isinstance(b, (float, np.floating)):
             return {"+": lambda: a + b, "-": lambda: a - b, "*": lambda: a * b,
                     "/": lambda: a / b, "%": lambda: math.fmod(a, b)}[op]()
         if isinstance(a, bool) and isinstance(b, bool) and op in ("&", "|", "^"):
@@ -1518,7 +1537,13 @@ class Interp:
 
     def ev_for(self, e, env):
         _, pat, ite, body, label = e
-        it = to_iter(self.ev(ite, env))
+        v = self.ev(ite, env)
+        if ite[0] == "ref" and ite[1] and isinstance(deref(v), (Slice, list)):
+            # `for x in &mut slice`: IntoIterator for &mut [T] yields &mut T
+            s = as_slice(deref(v))
+            it = iter([elem_ref(s.base, s.start + i) for i in range(len(s))])
+        else:
+            it = to_iter(v)
 
         def step(x):
             lenv = Env(env)
@@ -1593,7 +1618,7 @@ class Interp:
                 return None  # a release build compiles debug_assert! out
             args = self._macro_args(toks)
             if name.endswith("_eq"):
-                a, b = (deref(self.ev(x, env)) for x in args[:2])
+                a, b = (_eq_norm(deref(self.ev(x, env))) for x in args[:2])
                 if a != b:
                     raise AssertionError("%s: %r != %r" % (name, a, b))
             elif name.endswith("_ne"):
@@ -1718,6 +1743,16 @@ class StructType:
         self.__dict__.update(consts)
 
 
+def _eq_norm(v):
+    """assert_eq! operands: slices, arrays and vectors compare element-wise
+    (PartialEq of [T] against [T; N] / Vec<T>)."""
+    if isinstance(v, Slice):
+        v = v.tolist()
+    if isinstance(v, (list, tuple)):
+        return [_eq_norm(deref(x)) for x in v]
+    return v
+
+
 def to_iter(v):
     v = deref(v)
     if isinstance(v, It):
@@ -1731,6 +1766,8 @@ def to_iter(v):
 
 def index_get(base, idx):
     base = deref(base)
+    if hasattr(base, "index_any"):  # host containers indexed by a struct (FrameBlocks[bo])
+        return base.index_any(idx)
     if isinstance(idx, RangeV):
         if hasattr(base, "index_range"):
             return base.index_range(idx)
@@ -1825,10 +1862,15 @@ def _float_method(v, name, args, gty):
         return math.sqrt(v)
     if name == "abs":
         return abs(v)
-    if name == "min":
-        return min(v, args[0])
-    if name == "max":
-        return max(v, args[0])
+    if name in ("min", "max"):  # f32::min / max: a NaN operand yields the other one
+        a = args[0]
+        if math.isnan(v):
+            return a
+        if math.isnan(a):
+            return v
+        return (min if name == "min" else max)(v, a)
+    if name == "log2":
+        return np.log2(v) if isinstance(v, np.float32) else math.log2(v)
     if name == "is_finite":
         return math.isfinite(v)
     if name in ("floor", "ceil", "round"):
@@ -1976,6 +2018,8 @@ def _some_method(v, name, args):
 
 
 def call_method(r, name, args, gty, raw):
+    if name in ("is_none", "is_some") and not isinstance(r, (It, RangeV)):  # Option<tuple> too
+        return (r is None) == (name == "is_none")
     if name in _OPT and r is not None and not isinstance(r, (It, RangeV, tuple, list, Slice)) \
             and not (name == "unwrap" and not isinstance(r, (int, float, Struct))):
         if not (isinstance(r, int) and type(r) not in (int, TInt, bool) and hasattr(type(r), name)):
@@ -1990,7 +2034,7 @@ def call_method(r, name, args, gty, raw):
         if type(r) not in (int, TInt) and hasattr(type(r), name):  # host enums
             return getattr(r, name)(*args)
         return _int_method(r, name, args, gty)
-    if isinstance(r, float):
+    if isinstance(r, (float, np.floating)):
         return _float_method(r, name, args, gty)
     if r is None or isinstance(r, tuple) and len(r) == 2 and r[0] in ("Ok", "Err"):
         return _option_method(r, name, args)
@@ -2008,6 +2052,10 @@ def call_method(r, name, args, gty, raw):
     if isinstance(r, Struct):
         if name in ("clone", "to_owned"):
             return r.copy()
+        if name in ("as_ref", "as_mut", "unwrap", "expect"):  # Some(x) / Arc<x> is x here
+            return r
+        if name in r._f and callable(r._f[name]):  # host-supplied method
+            return r._f[name](*args)
         raise NotImplementedError("%s has no method %s" % (r._name, name))
     m = getattr(r, name, None)
     if m is None and hasattr(r, "as_slice"):  # Deref to a slice
@@ -2066,6 +2114,9 @@ def _slice_method(r, name, args, gty, raw):
         n = int(args[0])
         stop = len(s) - (len(s) % n if "exact" in name else 0)
         return It(s.sub(i, min(i + n, len(s))) for i in range(0, stop, n))
+    if name in ("split_at", "split_at_mut"):
+        n = int(args[0])
+        return (s.sub(0, n), s.sub(n, len(s)))
     if name == "copy_from_slice" or name == "clone_from_slice":
         src = as_slice(deref(args[0]))
         if len(src) != len(s):
