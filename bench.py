@@ -45,24 +45,43 @@ TIMING_STRIDE = 4  # in GOPs
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
 # VALU issue peaks, G wave64 instructions/s over 256 CUs at 2.4 GHz: the
 # guide's 2 cycles per wave instruction per SIMD (MI355X_MICROARCH.md "Wave
-# scheduling"), and the rate measured for the integer SAD / dot / alignbyte
-# instructions these kernels are built from: ~0.9 wave-instr per CU-cycle
-# at full occupancy (tools/ubench/valu_rates.hip, profiles/valu_rates.txt)
+# scheduling"), and the rate measured on MI355X for the integer SAD / dot /
+# mul24 instructions these kernels are built from (tools/ubench/valu_rates.hip,
+# its output committed as profiles/valu_rates.txt; read at run time)
 VALU_PEAK_GUIDE = 256 * 4 * 2.4 / 2
-VALU_PEAK_INT = 256 * 1 * 2.4
+VALU_RATES = os.path.join(ROOT, "profiles", "valu_rates.txt")
+INT_OPS = ("v_sad_u8", "v_dot4_i32_i8", "v_dot2_i32_i16", "v_mad_i32_i24")
+
+
+def valu_peak_int():
+    """Mean measured issue rate of INT_OPS (wave-instr / cycle / CU) x 256
+    CUs x 2.4 GHz, and the file it came from; None if the file is absent."""
+    if not os.path.exists(VALU_RATES):
+        return None
+    rates = {}
+    with open(VALU_RATES) as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) > 4 and parts[0] in INT_OPS and parts[4] == "wave-instr/cycle/CU":
+                rates[parts[0]] = float(parts[3])
+    if len(rates) != len(INT_OPS):
+        return None
+    per_cu = sum(rates.values()) / len(rates)
+    return {"G_per_s": round(per_cu * 256 * 2.4, 1), "wave_instr_per_cycle_per_cu": round(per_cu, 4),
+            "ops": rates, "source": "profiles/valu_rates.txt"}
 # FL runs on a second stream by default: "FL_on_main_stream" is then the
 # fork alone, and "FL_lookahead_span" the lookahead's own span, overlapped
 # with F3/F4 (RAV1E_HIP_REPLAY_SERIAL=1: both on one stream)
 STAGES = ["F0_pyramid", "F1_full_search", "F2_half_res_quadrants", "FL_on_main_stream",
           "F3_diamond_fullpel", "F3_diamond_subpel", "F4_rdo_single_ref", "F4_rdo_compound",
-          "F4_rd_cost_argmin", "F6_commit", "F5_importance_satd", "F7_pad_exchange",
-          "FL_lookahead_span"]
+          "F4_rd_cost_argmin", "F6_commit", "F6b_intra_screen_rdo", "F5_importance_satd",
+          "F7_pad_exchange", "FL_lookahead_span"]
 # speed 6: the 32x32 / 16x16 / 8x8 searches run inside the sub-pel stage,
 # their candidates inside F4, the partition decision with the argmin
 STAGES6 = ["F0_pyramid", "F1_full_search", "F2_half_res_quadrants", "FL_on_main_stream",
            "F3_diamond_fullpel", "F3_subpel_and_level_me", "F4_rdo_single_ref_all_levels",
            "F4_rdo_compound_all_levels", "F4_argmin_partition", "F6_commit_leaves",
-           "F5_importance_satd", "F7_pad_exchange", "FL_lookahead_span"]
+           "F6b_intra_screen_rdo", "F5_importance_satd", "F7_pad_exchange", "FL_lookahead_span"]
 
 
 def coarse_windows(W, H, R, scale, tiling, group):
@@ -336,23 +355,42 @@ def main():
     launch_s = kd["ms"] / 1e3
     ach = kd["bytes"] / launch_s / 1e9
     tr = _profile_entry(args, dom, bd, "traffic")
+    # `bound` names the roofline `frac` is priced against (the contract's HBM
+    # roofline for this integer path); `limiter` names what actually binds,
+    # with the committed counter evidence (SQ pass: profiles/valu_<config>.json)
     roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
             "traffic": ({"bytes_per_launch": round(tr[0]["hbm_bytes"]), "source": tr[1]["source"],
-                         "git": tr[1]["git"]} if tr else None),
+                         "git": tr[1]["git"],
+                         "over_algorithmic": round(tr[0]["hbm_bytes"] / kd["bytes"], 3)}
+                        if tr else None),
             "avg_launch_ms": round(kd["ms"], 5),
             "algorithmic_bytes_per_launch": round(kd["bytes"])}
     vp = _profile_entry(args, dom, bd, "valu")
+    pk = valu_peak_int()
     if vp:
         # instructions per launch from the committed SQ pass; time from this run
-        insts = vp[0]["SQ_INSTS_VALU"]
+        c = vp[0]
+        insts = c["SQ_INSTS_VALU"]
         achv = insts / launch_s / 1e9
+        wc = max(1.0, c.get("SQ_WAVE_CYCLES", 0.0))
+        wait, act = c.get("SQ_WAIT_ANY", 0.0) / wc, c.get("SQ_ACTIVE_INST_ANY", 0.0) / wc
         roof["valu"] = {"achieved": round(achv, 1), "unit": "G wave64 VALU instr/s",
                         "peak_guide": VALU_PEAK_GUIDE, "frac_guide": round(achv / VALU_PEAK_GUIDE, 4),
-                        "peak_int_measured": VALU_PEAK_INT,
-                        "frac_int_measured": round(achv / VALU_PEAK_INT, 4),
                         "insts_per_launch": round(insts), "source": vp[1]["source"],
                         "git": vp[1]["git"]}
+        if pk:
+            roof["valu"].update(peak_int_measured=pk["G_per_s"],
+                                frac_int_measured=round(achv / pk["G_per_s"], 4),
+                                peak_int_source=pk["source"])
+        roof["limiter"] = {
+            "resource": ("latency: waves parked on s_waitcnt / barriers" if wait > 0.3 else
+                         "VALU issue" if achv / VALU_PEAK_GUIDE > 0.6 else "mixed issue / latency"),
+            "SQ_WAIT_ANY_over_WAVE_CYCLES": round(wait, 4),
+            "SQ_ACTIVE_INST_ANY_over_WAVE_CYCLES": round(act, 4),
+            "valu_frac_guide": round(achv / VALU_PEAK_GUIDE, 4),
+            "hbm_frac": round(ach / HBM_PEAK_GBS, 5),
+            "source": vp[1]["source"]}
     fps = args.steps / dt  # frames of the one stream
 
     cpu = parity = None
@@ -395,6 +433,11 @@ def main():
             "rdo_candidates_per_frame": {"single_ref": round(ns, 1), "compound": round(nc, 1),
                                          "variants": "skip + non-skip each",
                                          **({"levels": level_cands} if level_cands else {})},
+            "intra_per_frame": {"screened_superblocks": round(cnt[11] / ev_frames, 2),
+                                "intra_winners": round(cnt[12] / ev_frames, 2),
+                                "rounds": round(cnt[13] / ev_frames, 2),
+                                "modes_per_screen": "13 predicted + SATD, 3 RDO x (chroma "
+                                                    "mode, DC)"},
             "checksum": int(words[-5]) & 0xFFFFFFFF,
         }
         print(json.dumps(line), flush=True)

@@ -501,6 +501,17 @@ typedef struct rv_replay_cfg {
  * 882-941, rv_replay_level_params.cdef_strengths).  Width and height must
  * be multiples of 8. */
 #define RV_REPLAY_CDEF 32
+/* flags: no intra-mode screening.  By default (speed 10, 4:2:0) every
+ * superblock whose inter winner is not skip and that lies inside the frame
+ * runs rdo_mode_decision's intra screening and intra RDO (src/rdo.rs:
+ * 1008-1152): get_intra_edges of the current reconstruction, the 13
+ * RAV1E_INTRA_MODES at TX_64X64 + get_satd, the three modes to try, each
+ * with chroma modes [mode, DC_PRED]; an intra winner's result words are
+ * [1000 + 16 * luma mode + chroma mode, 0, cost bits, distortion] and its
+ * reconstruction and levels replace the inter winner's.  rav1e's tile
+ * raster order is reproduced by re-evaluating, round after round, the
+ * superblocks whose left / top / top-right / top-left neighbour changed. */
+#define RV_REPLAY_NO_INTRA 64
 typedef struct rv_replay_frame_info {
   int32_t display;            /* display index of the coded frame */
   int32_t me_range_scale;     /* 4 >> pyramid level (src/encoder.rs:838) */
@@ -600,7 +611,10 @@ int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,
 /* Candidate evaluations summed over the last min(frames, 64) coded frames:
  * out[0] F3 full-pel 64x64 diamond, out[1] F3 sub-pel 64x64 diamond, out[2]
  * = the number of frames summed (cap >= 3); with cap >= 5, out[3] / out[4]
- * the F4 single-reference / compound RDO candidates.  Returns the count. */
+ * the F4 single-reference / compound RDO candidates; with cap >= 11, out[5
+ * .. 10] those of the 32x32, 16x16 and 8x8 blocks (speed 6); with cap >=
+ * 14, out[11] superblocks intra-screened, out[12] intra winners, out[13]
+ * intra rounds.  Returns the count. */
 int rv_replay_counters(rv_replay *r, uint64_t *out, int cap);
 
 /* ---------------------------------------------------------------------

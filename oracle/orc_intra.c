@@ -164,3 +164,60 @@ void orc_predict_intra(int mode, int variant, void *dst, ptrdiff_t stride, int w
 #undef LEFTB
 #undef ABOVE
 }
+
+/* get_intra_edges (src/partition.rs:500-693) with opt_mode None (every
+ * edge: left, top-left, top, top-right, bottom-left) for the first (only)
+ * transform block of a superblock-level partition: an n x n block at
+ * tile-relative pixel (x, y) of a plane region of tw x th pixels whose pixel
+ * (0, 0) is `tile` (stride in elements).  The partition is the 64x64
+ * superblock, so has_top_right (src/recon_intra.rs:174-241) holds iff the
+ * top row and the right neighbour exist (the block sits in the top row of
+ * its superblock) and has_bottom_left (:376-470) never does (the bottom-left
+ * superblock is coded later).  have_top / have_left: partition_bo.y / .x >
+ * 0 (> 1 for a decimated plane), i.e. not the tile's first superblock row /
+ * column.  Entries no branch writes stay zero (rav1e leaves them
+ * uninitialized; no predictor reads them).  edge: 4 * 64 + 1 pixels. */
+void orc_intra_edges_sb(const void *tile, ptrdiff_t stride, int hbd, int bd, int tw, int th,
+                        int x, int y, int n, int have_top, int have_left, void *edge) {
+  (void)th;
+  (void)have_left;
+  const int base = 128 << (bd - 8);
+#define D(r, c) orc_px(tile, hbd, (ptrdiff_t)(r) * stride + (c))
+#define S(i, v) orc_px_store(edge, hbd, (i), (v))
+#define G(i) orc_px(edge, hbd, (i))
+  for (int i = 0; i < 4 * MAXTX + 1; i++) S(i, 0);
+  const int L = 2 * MAXTX, A = 2 * MAXTX + 1;
+  /* left, bottom to top, right-aligned */
+  if (x != 0) {
+    for (int i = 0; i < n; i++) S(L - n + i, D(y + n - 1 - i, x - 1));
+  } else {
+    const int32_t v = y != 0 ? D(y - 1, 0) : base + 1;
+    for (int i = L - n; i < L; i++) S(i, v);
+  }
+  /* top-left */
+  S(L, x == 0 && y == 0 ? base : y == 0 ? D(0, x - 1) : x == 0 ? D(y - 1, 0) : D(y - 1, x - 1));
+  /* top */
+  if (y != 0) {
+    for (int i = 0; i < n; i++) S(A + i, D(y - 1, x + i));
+  } else {
+    const int32_t v = x != 0 ? D(0, x - 1) : base - 1;
+    for (int i = 0; i < n; i++) S(A + i, v);
+  }
+  /* top-right */
+  const int right_available = x + n < tw;
+  int na = 0;
+  if (y != 0 && have_top && right_available) na = n < tw - x - n ? n : tw - x - n;
+  for (int i = 0; i < na; i++) S(A + n + i, D(y - 1, x + n + i));
+  if (na < n) {
+    const int32_t v = G(A + n + na - 1);
+    for (int i = n + na; i < 2 * n; i++) S(A + i, v);
+  }
+  /* bottom-left: none available; replicate the bottom-most left pixel */
+  {
+    const int32_t v = G(L - n);
+    for (int i = L - 2 * n; i < L - n; i++) S(i, v);
+  }
+#undef D
+#undef S
+#undef G
+}

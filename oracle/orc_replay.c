@@ -60,6 +60,7 @@ typedef struct orc_replay {
   struct {
     int set, qidx, dc[3], ac[3];
     orc_qctx q[3];
+    orc_qctx qi[3]; /* the intra blocks' (is_intra: other rounding offsets) */
     double lambda, me_lambda, ds[3];
   } lv[3];
   oslot slots[NSLOT];
@@ -96,6 +97,11 @@ typedef struct orc_replay {
   /* RV_REPLAY_CDEF (orc_replay_set_cdef): (y, uv) strengths per level */
   int cdef;
   uint8_t cdef_str[3][2];
+  /* intra-mode screening + intra RDO of the non-skip superblocks
+   * (orc_replay_set_intra; speed 10, 4:2:0): screened / intra winners this
+   * frame */
+  int intra;
+  uint64_t istat[2];
   pthread_mutex_t mu;
   int next_sb, pass, sb_limit;
 } orc_replay;
@@ -547,6 +553,7 @@ int orc_replay_set_level_params(orc_replay *r, int level, int base_q_idx, const 
     r->lv[level].ac[p] = ac[p];
     r->lv[level].ds[p] = ds[p];
     orc_qctx_update(&r->lv[level].q[p], base_q_idx, p ? 3 : 4, 0, r->bd, dc[p], ac[p]);
+    orc_qctx_update(&r->lv[level].qi[p], base_q_idx, p ? 3 : 4, 1, r->bd, dc[p], ac[p]);
     for (int l = 1; r->s6 && l < 4; l++)
       orc_qctx_update(&r->qs[level][l][p], base_q_idx, p ? r->pl[l].txc : r->pl[l].txl, 0, r->bd,
                       dc[p], ac[p]);
@@ -1265,10 +1272,156 @@ static void run_rdo(orc_replay *r, int sb, uint64_t tail[3]) {
     }
 }
 
+/* ---- intra-mode screening and intra RDO (rdo_mode_decision,
+ * src/rdo.rs:1008-1152), speed 10, 4:2:0 ------------------------------------
+ * After every superblock's inter decision and commit: the superblocks of
+ * each tile in raster order.  A non-skip winner (`!best.skip`) fully inside
+ * the frame gets get_intra_edges (None) of the current reconstruction, the 13
+ * RAV1E_INTRA_MODES predicted at TX_64X64 and their get_satd, a stable sort,
+ * the modes to try = [the most probable mode under the intra y-mode CDF:
+ * DC_PRED in default_if_y_mode_cdf (src/entropymode.rs:166-184), which is
+ * not adapted here] + the three lowest SATDs not already in, take 3; each
+ * runs luma_chroma_mode_rdo with chroma modes [mode, DC_PRED] (DC_PRED only
+ * once): intra prediction, encode_tx_block with the intra quantizer, no
+ * skip variant; strict `<` against the inter winner's cost.  A winner's
+ * reconstruction and levels replace the inter winner's. */
+#define INTRA_C 1000 /* result word of an intra winner: 1000 + 16 * luma + chroma mode */
+
+/* get_intra_edges of plane p (0 luma) for superblock (ppx, ppy) of tile
+ * geometry g; n = the transform size in that plane */
+static void sb_edges(const orc_replay *r, const oplane *pl, const sbgeo *g, int ppx, int ppy,
+                     int dec_x, int dec_y, int n, void *edge) {
+  const int tx = (g->t0x * SB) >> dec_x, ty = (g->t0y * SB) >> dec_y;
+  const int tw = (g->mi_w * 4) >> dec_x, th = (g->mi_h * 4) >> dec_y;
+  const int x = (ppx >> dec_x) - tx, y = (ppy >> dec_y) - ty;
+  orc_intra_edges_sb(at(pl, r->hbd, tx, ty), pl->stride, r->hbd, r->bd, tw, th, x, y, n,
+                     g->tsy > 0, g->tsx > 0, edge);
+}
+static int variant_of(int x, int y) { return x == 0 && y == 0 ? 0 : y == 0 ? 1 : x == 0 ? 2 : 3; }
+
+static void intra_sb(orc_replay *r, int sb) {
+  const int R = r->R, hbd = r->hbd;
+  const size_t px = px_of(r);
+  uint64_t *w = r->words + (size_t)sb * (WPR * R + 4) + WPR * R;
+  if (w[1]) return; /* the inter winner is skip: no screening */
+  if (r->sb_limit > 0 && sb >= r->sb_limit) return; /* a bounded timing sample */
+  const int sx = sb % r->tw, sy = sb / r->tw;
+  const int ppx = (sx + r->tx0) * SB, ppy = (sy + r->ty0) * SB;
+  if (ppx + SB > r->W || ppy + SB > r->H) return; /* rav1e splits it (must_split) */
+  const sbgeo g = sb_geo_of(r, sb);
+  const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
+  oslot *S = &r->slots[r->fi.display % NSLOT];
+  const int lvl = r->fi.level;
+  const double lambda = r->lv[lvl].lambda;
+  const int cpx = ppx >> r->xdec, cpy = ppy >> r->ydec, cn = SB >> r->xdec;
+  uint16_t ey[4 * 64 + 1], eu[4 * 64 + 1], ev[4 * 64 + 1];
+  sb_edges(r, &S->y, &g, ppx, ppy, 0, 0, SB, ey);
+  sb_edges(r, &S->u, &g, ppx, ppy, r->xdec, r->ydec, cn, eu);
+  sb_edges(r, &S->v, &g, ppx, ppy, r->xdec, r->ydec, cn, ev);
+  const int lx = ppx - g.t0x * SB, ly_ = ppy - g.t0y * SB;
+  const int var = variant_of(lx, ly_), cvar = variant_of(lx >> r->xdec, ly_ >> r->ydec);
+  /* screening: RAV1E_INTRA_MODES order (src/predict.rs:32-46) */
+  static const int kModes[13] = {0, 2, 1, 9, 11, 10, 12, 3, 4, 5, 6, 7, 8};
+  uint32_t satd[13];
+  uint16_t pb[SB * SB];
+  for (int k = 0; k < 13; k++) {
+    orc_predict_intra(kModes[k], var, pb, SB, SB, SB, r->bd, hbd, ey);
+    satd[k] = orc_get_satd(at(&cur->y, hbd, ppx, ppy), cur->y.stride, pb, SB, SB, SB, hbd, 0);
+  }
+  int order[13];
+  for (int k = 0; k < 13; k++) order[k] = k;
+  for (int i = 1; i < 13; i++) /* stable insertion sort by satd (sort_by_key) */
+    for (int j = i; j > 0 && satd[order[j]] < satd[order[j - 1]]; j--) {
+      int t = order[j];
+      order[j] = order[j - 1];
+      order[j - 1] = t;
+    }
+  int modes[4], nm = 0;
+  modes[nm++] = 0; /* DC_PRED: the most probable mode */
+  for (int i = 0; i < 3; i++) {
+    int m = kModes[order[i]], seen = 0;
+    for (int j = 0; j < nm; j++) seen |= modes[j] == m;
+    if (!seen) modes[nm++] = m;
+  }
+  if (nm > 3) nm = 3;
+  /* RDO of each (luma mode, chroma mode) */
+  uint64_t cb = w[2];
+  double best;
+  memcpy(&best, &cb, 8);
+  int won = 0, bl = 0, bc = 0;
+  uint64_t bd_ = 0;
+  uint16_t by_[SB * SB], bu_[SB * SB], bv_[SB * SB];
+  int32_t blev[1024 + 2 * 1024];
+  uint16_t ly[SB * SB], lu[SB * SB], lv[SB * SB];
+  int32_t lev[1024 + 2 * 1024];
+  const orc_qctx *qi = r->lv[lvl].qi;
+  for (int i = 0; i < nm; i++) {
+    const int m = modes[i];
+    orc_predict_intra(m, var, ly, SB, SB, SB, r->bd, hbd, ey);
+    const uint32_t lrate = (uint32_t)tx_block_q(r, &cur->y, ppx, ppy, ly, SB, 4, 0, lev, &qi[0]);
+    const int cm[2] = {m, 0};
+    for (int j = 0; j < (m ? 2 : 1); j++) {
+      orc_predict_intra(cm[j], cvar, lu, cn, cn, cn, r->bd, hbd, eu);
+      orc_predict_intra(cm[j], cvar, lv, cn, cn, cn, r->bd, hbd, ev);
+      uint32_t rate = lrate;
+      rate += (uint32_t)tx_block_q(r, &cur->u, cpx, cpy, lu, cn, 3, 1, lev + 1024, &qi[1]);
+      rate += (uint32_t)tx_block_q(r, &cur->v, cpx, cpy, lv, cn, 3, 2, lev + 2048, &qi[2]);
+      const uint64_t d = sb_distortion(r, cur, ppx, ppy, ly, lu, lv);
+      const double rd = (double)d + lambda * ((double)rate / 8.0);
+      if (rd < best) {
+        best = rd;
+        won = 1;
+        bl = m;
+        bc = cm[j];
+        bd_ = d;
+        memcpy(by_, ly, SB * SB * px);
+        memcpy(bu_, lu, (size_t)cn * cn * px);
+        memcpy(bv_, lv, (size_t)cn * cn * px);
+        memcpy(blev, lev, sizeof(blev));
+      }
+    }
+  }
+  __atomic_fetch_add(&r->istat[0], 1, __ATOMIC_RELAXED);
+  if (!won) return;
+  __atomic_fetch_add(&r->istat[1], 1, __ATOMIC_RELAXED);
+  for (int y = 0; y < SB; y++)
+    memcpy(at(&S->y, hbd, ppx, ppy + y), (uint8_t *)by_ + y * SB * px, SB * px);
+  for (int y = 0; y < cn; y++) {
+    memcpy(at(&S->u, hbd, cpx, cpy + y), (uint8_t *)bu_ + (size_t)y * cn * px, cn * px);
+    memcpy(at(&S->v, hbd, cpx, cpy + y), (uint8_t *)bv_ + (size_t)y * cn * px, cn * px);
+  }
+  memcpy(r->lev + (size_t)sb * (1024 + 2 * r->ntx_c * 1024), blev, sizeof(blev));
+  memcpy(&cb, &best, 8);
+  w[0] = INTRA_C + 16 * bl + bc;
+  w[1] = 0;
+  w[2] = cb;
+  w[3] = bd_;
+}
+
+/* The intra pass over one tile (index t of the group's tiles), raster order. */
+static void intra_tile(orc_replay *r, int t) {
+  const int gtx = (r->tw + r->tws - 1) / r->tws;  /* tiles across the group */
+  const int tx0 = (t % gtx) * r->tws, ty0 = (t / gtx) * r->ths;
+  for (int y = ty0; y < ty0 + r->ths && y < r->th; y++)
+    for (int x = tx0; x < tx0 + r->tws && x < r->tw; x++) intra_sb(r, y * r->tw + x);
+}
+
+void orc_replay_intra_stats(const orc_replay *r, uint64_t out[2]) {
+  out[0] = r->istat[0];
+  out[1] = r->istat[1];
+}
+
+int orc_replay_set_intra(orc_replay *r, int on) {
+  r->intra = on != 0 && !r->s6 && r->xdec == 1 && r->ydec == 1;
+  return r->intra == (on != 0) ? 0 : -1;
+}
+
 static void *worker(void *arg) {
   orc_replay *r = arg;
   uint64_t tail[3] = {0, 0, 0};
   int lim = r->sb_limit > 0 && r->sb_limit < r->nsb ? r->sb_limit : r->nsb;
+  if (r->pass == 4) /* the group's tiles */
+    lim = ((r->tw + r->tws - 1) / r->tws) * ((r->th + r->ths - 1) / r->ths);
   for (;;) {
     pthread_mutex_lock(&r->mu);
     int sb = r->next_sb++;
@@ -1280,8 +1433,10 @@ static void *worker(void *arg) {
       run_half(r, sb);
     else if (r->pass == 2)
       run_me(r, sb);
-    else
+    else if (r->pass == 3)
       run_rdo(r, sb, tail);
+    else
+      intra_tile(r, sb); /* pass 4: `sb` counts tiles */
   }
   pthread_mutex_lock(&r->mu);
   for (int i = 0; i < 3; i++) r->tail[i] += tail[i];
@@ -1345,6 +1500,8 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
   memset(r->tail, 0, sizeof(r->tail));
   r->sb_limit = sb_limit;
   for (int pass = 0; pass < 4; pass++) run_pass(r, pass);
+  r->istat[0] = r->istat[1] = 0;
+  if (r->intra) run_pass(r, 4);
   if (r->deblock) {
     map_own(r);
     if (pad_recon) loop_filter_planes(r);  /* tile groups: after the imports */

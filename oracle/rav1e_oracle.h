@@ -73,6 +73,11 @@ void orc_mc_avg(void *dst, ptrdiff_t dst_stride, const int16_t *tmp1,
  * edge = rav1e's 257-pixel edge_buf. */
 void orc_predict_intra(int mode, int variant, void *dst, ptrdiff_t stride, int w, int h,
                        int bit_depth, int hbd, const void *edge);
+/* get_intra_edges (src/partition.rs:500-693), opt_mode None, for the
+ * transform block of a superblock-level partition at tile-relative pixel
+ * (x, y) of a tw x th tile region (pixel (0, 0) at `tile`); edge = 257 px. */
+void orc_intra_edges_sb(const void *tile, ptrdiff_t stride, int hbd, int bd, int tw, int th,
+                        int x, int y, int n, int have_top, int have_left, void *edge);
 /* deblock_plane (src/deblock.rs:1174-1335) of plane pli at origin (visible
  * (0, 0)); lg / skip per luma 4x4 block (row pitch mi_stride): log2 of the
  * square block's width in 4x4 units, skip flag; levels = [Y vertical, Y

@@ -46,6 +46,14 @@ struct RdoArgs {
   int xdec, ydec;      // this plane type's subsampling
   int q_tx_index;      // tx_size * 16 + tx_type: av1_scan_orders entry
   int tx_size, qindex; // estimate_rate
+  // intra chains (MODE 3, rv_rdo_intra): per superblock the get_intra_edges
+  // of Y, U, V (3 x kIntraEdge pixels), the modes to try [n, m0, m1, m2]
+  // (score; luma task = slot * 3 + k, chroma task = slot * 6 + 2 k + (0:
+  // chroma mode m_k, 1: DC_PRED)) and the winner's [luma, chroma] mode
+  // (commit; task = list entry)
+  const void *iedges;
+  const uint8_t *imodes;
+  const uint8_t *iwin;
 };
 
 }  // namespace rv
@@ -65,3 +73,9 @@ int rv_rdo_candidates(const rv::RdoArgs &luma, const rv::RdoArgs &chroma, int hb
 // 1 compound (score), 2 commit.
 int rv_rdo_blocks(const rv::RdoArgs &a, bool luma, int nplanes, int n_tx_size, int hbd,
                   hipStream_t s, int mode);
+
+// Intra chains of the 64x64 superblocks listed in luma.list (count): luma
+// TX_64X64 + chroma TX_32X32 (4:2:0), intra prediction from the edges in
+// RdoArgs::iedges, the intra quantizers; score (3 luma modes, 6 chroma
+// chains per plane) or commit (the winner's modes).
+int rv_rdo_intra(const rv::RdoArgs &luma, const rv::RdoArgs &chroma, int hbd, hipStream_t s);

@@ -38,6 +38,7 @@
 
 #include <type_traits>
 
+#include "rv_intra.h"
 #include "rv_rdo.h"
 #include "rv_tx.h"
 
@@ -102,7 +103,64 @@ struct RdoJob {
   int src2_x, src2_y, cf2, rf2;  // compound: reference 1's source and fracs
   bool zero;         // commit of a skip winner: every level is zero
   int oi;            // output slot: candidate (or superblock) * ntx_per_cand + block
+  int imode, ivar;   // intra (MODE 3): PredictionMode, PredictionVariant
+  const void *iedge; // intra: this plane's get_intra_edges (kIntraEdge pixels)
 };
+
+// An intra task (MODE 3, RdoArgs::iedges): the superblock of list entry
+// `slot`, its mode for this plane, the output slot (score: per superblock 3
+// luma / 6 chroma chains; commit: the superblock).  plane: 0 Y, 1 U, 2 V.
+template <typename Px, int N>
+__device__ __forceinline__ RdoJob rdo_job_intra(const RdoArgs &a, int plane, int t) {
+  RdoJob j;
+  int sb, mode;
+  if (a.commit) {
+    sb = a.list[t];
+    mode = a.iwin[sb * 2 + (plane ? 1 : 0)];
+    j.oi = sb;
+  } else if (plane == 0) {
+    const int slot = t / 3, k = t - 3 * slot;
+    sb = a.list[slot];
+    mode = a.imodes[sb * 4 + 1 + k];
+    j.oi = sb * 3 + k;
+  } else {
+    const int slot = t / 6, kc = t - 6 * slot;
+    sb = a.list[slot];
+    mode = (kc & 1) ? 0 : a.imodes[sb * 4 + 1 + (kc >> 1)];  // [m_k, DC_PRED]
+    j.oi = sb * 6 + kc;
+  }
+  const int sx = sb % a.g.tw, sy = sb / a.g.tw;
+  const int fx = a.g.tx0 + sx, fy = a.g.ty0 + sy;
+  const int tsx = fx % a.g.tws, tsy = fy % a.g.ths;  // the superblock in its tile
+  j.ivar = tsx == 0 && tsy == 0 ? 0 : tsy == 0 ? 1 : tsx == 0 ? 2 : 3;  // PredictionVariant::new
+  j.imode = mode;
+  j.iedge = (const uint8_t *)a.iedges + ((size_t)sb * 3 + plane) * kIntraEdge * sizeof(Px);
+  j.bx = (fx * a.bsize) >> a.xdec;
+  j.by = (fy * a.bsize) >> a.ydec;
+  j.ox = j.oy = 0;
+  j.src_x = j.src_y = j.cf = j.rf = j.ref = 0;
+  j.src2_x = j.src2_y = j.cf2 = j.rf2 = 0;
+  j.comp = false;
+  j.zero = false;
+  return j;
+}
+
+// The intra prediction of a job into pred (N x N, row-major) by the G lanes
+// of a group: edges staged in e (i32, kIntraEdge), then pred_* per pixel.
+template <typename Px, int N, int G>
+__device__ __forceinline__ void intra_fill(const RdoJob &jb, int32_t *e, Px *pred, int bd, int lane) {
+  const Px *eg = (const Px *)jb.iedge;
+  for (int i = lane; i < kIntraEdge; i += G) e[i] = eg[i];
+  wave_sync();
+  IntraSetup st = intra_setup(jb.imode, jb.ivar);
+  if (st.mode == 0) st.dcv = intra_dc<G>(e, jb.ivar, N, N, bd, lane);
+  const int maxv = (1 << bd) - 1;
+  for (int i = lane; i < N * N; i += G) {
+    const int r = i / N, c = i - r * N;
+    pred[i] = (Px)intra_px(st, e, N, N, r, c, maxv);
+  }
+  wave_sync();
+}
 
 // Transform blocks of this launch: n_tx, or count * ntx_per_cand for a
 // compacted candidate list.
@@ -455,7 +513,11 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   constexpr int C32 = N < 32 ? N : 32;           // coded coefficient extent
   static_assert(!LUMA || N >= 8, "cdef distortion runs on 8x8 blocks");
   const int lane = threadIdx.x & (LPB - 1);
-  const RdoJob jb = rdo_job<N>(a, pl, t);
+  RdoJob jb;
+  if constexpr (MODE == 3)
+    jb = rdo_job_intra<Px, N>(a, &pl == &a.p[1] ? 2 : 1, t);
+  else
+    jb = rdo_job<N>(a, pl, t);
   const rv_plane &ref = pl.ref[jb.ref];
   const int ox = jb.ox, oy = jb.oy;  // in the MC block
   const int bd = a.bd, ib = bd == 12 ? 2 : 4, maxv = (1 << bd) - 1;
@@ -466,8 +528,11 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
-  // ---- A. put_8tap into LDS (compound: prep_8tap x 2 + mc_avg) -------------
-  if (MODE == 1 || (MODE == 2 && jb.comp)) {
+  // ---- A. put_8tap into LDS (compound: prep_8tap x 2 + mc_avg; intra:
+  // predict_intra from the block's edges) -----------------------------------
+  if constexpr (MODE == 3) {
+    intra_fill<Px, N, LPB>(jb, buf, pred, a.bd, lane);
+  } else if (MODE == 1 || (MODE == 2 && jb.comp)) {
     static_assert(2 * (16 + 7) * (sizeof(Px) == 1 ? 48 : 80) <= N * (N + 1) * 4 || N != 32,
                   "compound windows must fit the coefficient slab");
     mc_compound<Px, N, (N < 16 ? N : 16)>(a, pl, jb, reinterpret_cast<uint32_t *>(buf), pred);
@@ -762,8 +827,10 @@ __device__ __forceinline__ void luma_front(const RdoArgs &a, const RdoPlane &pl,
   const int bd = a.bd, ib = bd == 12 ? 2 : 4, maxv = (1 << bd) - 1;
 
   // ---- A. put_8tap (src/mc.rs:213-307) into pred, NPART bands; compound:
-  // prep_8tap x 2 + mc_avg in bands of kCompRows
-  if (MODE == 1 || (MODE == 2 && jb.comp)) {
+  // prep_8tap x 2 + mc_avg in bands of kCompRows; intra: predict_intra
+  if constexpr (MODE == 3) {
+    intra_fill<Px, 64, 64>(jb, reinterpret_cast<int32_t *>(scr), pred, bd, lane);
+  } else if (MODE == 1 || (MODE == 2 && jb.comp)) {
     mc_compound<Px, 64, LumaLds<Px, int16_t, NPART>::kCompRows>(
         a, pl, jb, reinterpret_cast<uint32_t *>(scr), pred);
   } else
@@ -1005,7 +1072,11 @@ template <typename Px, typename Mid, int NPART, int MODE>
 __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &pl, int t,
                                               uint8_t *scr, Px *pred, const uint16_t *scan) {
   const int lane = threadIdx.x & 63;
-  const RdoJob jb = rdo_job<64>(a, pl, t);
+  RdoJob jb;
+  if constexpr (MODE == 3)
+    jb = rdo_job_intra<Px, 64>(a, 0, t);
+  else
+    jb = rdo_job<64>(a, pl, t);
   luma_front<Px, NPART, MODE>(a, pl, t, jb, true, scr, pred);
   wave_sync();
   int32_t *fmid = reinterpret_cast<int32_t *>(scr);
@@ -1121,7 +1192,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
   const int n = rdo_ntx(luma);
   if (t0 >= n) return;  // past the compacted list (uniform over the workgroup)
   const bool valid = t < n;
-  const RdoJob jb = rdo_job<64>(luma, luma.p[0], valid ? t : n - 1);
+  RdoJob jb;
+  if constexpr (MODE == 3)
+    jb = rdo_job_intra<Px, 64>(luma, 0, valid ? t : n - 1);
+  else
+    jb = rdo_job<64>(luma, luma.p[0], valid ? t : n - 1);
   if (valid) luma_front<Px, NPART, MODE>(luma, luma.p[0], t, jb, true, slot(wave), pred(wave));
   __syncthreads();
   if (wave == 0) {  // row DCT: lane = 16 * candidate + raster row
@@ -1224,6 +1299,13 @@ int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipSt
     rdo_launch<1>(luma, chroma, hbd, s, single, cpairs);
   else
     rdo_launch<0>(luma, chroma, hbd, s, single, cpairs);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+int rv_rdo_intra(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s) {
+  const unsigned cpairs = (unsigned)(2 * ((chroma.n_tx + 1) / 2));
+  rdo_launch<3>(luma, chroma, hbd, s, false, cpairs);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

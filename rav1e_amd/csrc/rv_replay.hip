@@ -36,6 +36,8 @@
 
 #include "rv_chain.h"
 #include "rv_device.h"
+#include "rv_intra.h"
+#include "rv_intra_pass.h"
 #include "rv_rdo.h"
 
 #if __has_include(<rccl/rccl.h>)
@@ -585,6 +587,7 @@ struct rv_replay {
     bool set = false;
     int qidx;
     QCtx ql, qu, qv;
+    QCtx qil, qiu, qiv;   // the same transforms, intra (is_intra rounding)
     QCtx qs[kLevels][3];  // speed 6: luma / U / V of the 32x32 .. 8x8 blocks
     double lambda, me_lambda, ds[3];
   } lv[3];
@@ -613,6 +616,16 @@ struct rv_replay {
   int32_t *cdef_var = nullptr;
   uint8_t cdef_str[3][2] = {};      // [level] = (y, uv) strengths at cdef_index 0
   int32_t *leaf_count = nullptr;  // [kLevels]
+  // intra-mode screening (rv_intra_pass.hip; speed 10, 4:2:0)
+  bool intra = false;
+  uint8_t *i_elig = nullptr, *i_was = nullptr, *i_win = nullptr, *i_modes = nullptr;
+  int32_t *i_mark = nullptr, *i_list[2] = {nullptr, nullptr}, *i_commit = nullptr,
+          *i_revert = nullptr;
+  int32_t *i_cnt = nullptr;    // [list 0, list 1, commit, revert]
+  int32_t *h_cnt = nullptr;    // pinned host copy of one count
+  void *i_edges = nullptr;
+  uint64_t *i_lout = nullptr, *i_cout = nullptr;
+  uint32_t *i_stats = nullptr; // [kRing][3]: screened, intra winners, rounds
   size_t nwords = 0, wpart = 0;   // result words; offset of the partition masks
   bool jobs_built = false;
   std::vector<RvSlot> slots;
@@ -645,10 +658,10 @@ struct rv_replay {
   // frame.  Every `timing_stride`-th block of frames is instrumented (each
   // record costs ~4.4 us of idle GPU between kernels on MI355X).
   static constexpr int kRing = 64;
-  // e[0..12]: the stage boundaries on the main stream; e[13], e[14]: the
+  // e[0..13]: the stage boundaries on the main stream; e[14], e[15]: the
   // lookahead's start and end (on the side stream when it overlaps)
-  static constexpr int kEv = 15;
-  static constexpr int kStageEv = 13;
+  static constexpr int kEv = 16;
+  static constexpr int kStageEv = 14;
   hipEvent_t evs[kRing][kEv];
   int timing_stride = 1, timing_block = 1;
   long timed = 0;
@@ -1069,6 +1082,111 @@ void frame_info(long n, int R, rv_replay_frame_info *f) {
     if (e_ != hipSuccess) return rv_set_hip_error(e_, #expr); \
   } while (0)
 
+// F6b: rdo_mode_decision's intra-mode screening and intra RDO of every
+// superblock whose inter winner is not skip (rv_intra_pass.hip), round by
+// round until no decision changes.  la / ca: the F6 commit arguments.
+static int intra_pass(rv_replay *r, const RdoArgs &la, const RdoArgs &ca, const RvInput &cur,
+                      const RvSlot &S, const rv_replay::Level &L, int slot) {
+  const Geo &g = r->g;
+  hipStream_t st = r->stream;
+  const IntraGeo ig{g.W, g.H, g.bd, g.nsb, g.tw, g.tx0, g.ty0, g.tws, g.ths};
+  uint32_t *stats = r->i_stats + (size_t)slot * 3;
+  RV_H(hipMemsetAsync(r->i_cnt, 0, 4 * sizeof(int32_t), st));
+  RV_R(rv_intra_elig(ig, r->win, r->i_elig, r->i_was, r->i_mark, r->i_list[0], r->i_cnt, st));
+  RV_H(hipMemcpyAsync(r->h_cnt, r->i_cnt, 4, hipMemcpyDeviceToHost, st));
+  RV_H(hipStreamSynchronize(st));
+  int n = *r->h_cnt, round = 0;
+  // the rounds are bounded by the longest dependency chain of a tile (its
+  // anti-diagonals: right, below-left)
+  const int max_rounds = g.tws + 2 * g.ths + 4;
+  while (n > 0) {
+    if (round >= max_rounds)
+      return rv_set_error(RV_EHIP, "rv_replay_frame: the intra rounds did not converge");
+    const int ci = round & 1;
+    int32_t *list = r->i_list[ci], *cnt = r->i_cnt + ci;
+    RV_H(hipMemsetAsync(r->i_cnt + (ci ^ 1), 0, sizeof(int32_t), st));
+    RV_H(hipMemsetAsync(r->i_cnt + 2, 0, 2 * sizeof(int32_t), st));
+    // screening: edges + the modes to try
+    IntraScreenArgs sa;
+    sa.g = ig;
+    sa.rec[0] = S.y;
+    sa.rec[1] = S.u;
+    sa.rec[2] = S.v;
+    sa.org = cur.y;
+    sa.list = list;
+    sa.count = cnt;
+    sa.edges = r->i_edges;
+    sa.modes = r->i_modes;
+    RV_R(rv_intra_screen(sa, g.hbd, st));
+    // the intra chains: 3 luma modes, 6 chroma chains per plane
+    RdoArgs li = la, cl = ca;
+    li.commit = cl.commit = 0;
+    li.list = cl.list = list;
+    li.count = cl.count = cnt;
+    li.ntx_per_cand = 3;
+    li.n_tx = g.nsb * 3;
+    cl.ntx_per_cand = 6;
+    cl.n_tx = g.nsb * 6;
+    li.iedges = cl.iedges = r->i_edges;
+    li.imodes = cl.imodes = r->i_modes;
+    li.iwin = cl.iwin = r->i_win;
+    li.p[0].q = L.qil;
+    li.p[0].out = r->i_lout;
+    cl.p[0].q = L.qiu;
+    cl.p[1].q = L.qiv;
+    cl.p[0].out = r->i_cout;
+    cl.p[1].out = r->i_cout + (size_t)g.nsb * 6 * 3;
+    RV_R(rv_rdo_intra(li, cl, g.hbd, st));
+    // the decisions, the commit / revert lists, the next round
+    IntraDecideArgs da;
+    da.g = ig;
+    da.win = r->win;
+    da.modes = r->i_modes;
+    da.lout = r->i_lout;
+    da.uout = r->i_cout;
+    da.vout = r->i_cout + (size_t)g.nsb * 6 * 3;
+    da.lambda = L.lambda;
+    da.ds_u = L.ds[1];
+    da.ds_v = L.ds[2];
+    da.list = list;
+    da.count = cnt;
+    da.iwin = r->i_win;
+    da.iwas = r->i_was;
+    da.elig = r->i_elig;
+    da.mark = r->i_mark;
+    da.round = round;
+    da.words = r->words;
+    da.words_per_sb = kWordsPerRef * g.R + 4;
+    da.win_off = kWordsPerRef * g.R;
+    da.commit_list = r->i_commit;
+    da.commit_count = r->i_cnt + 2;
+    da.revert_list = r->i_revert;
+    da.revert_count = r->i_cnt + 3;
+    da.next_list = r->i_list[ci ^ 1];
+    da.next_count = r->i_cnt + (ci ^ 1);
+    RV_R(rv_intra_decide(da, st));
+    // intra winners into the frame; superblocks back to inter: the F6 chain
+    li.commit = cl.commit = 1;
+    li.list = cl.list = r->i_commit;
+    li.count = cl.count = r->i_cnt + 2;
+    li.ntx_per_cand = cl.ntx_per_cand = 1;
+    li.n_tx = cl.n_tx = g.nsb;
+    li.p[0].out = cl.p[0].out = cl.p[1].out = nullptr;
+    RV_R(rv_rdo_intra(li, cl, g.hbd, st));
+    RdoArgs lr = la, cr = ca;
+    lr.list = cr.list = r->i_revert;
+    lr.count = cr.count = r->i_cnt + 3;
+    RV_R(rv_rdo_candidates(lr, cr, g.hbd, st));
+    RV_H(hipMemcpyAsync(r->h_cnt, r->i_cnt + (ci ^ 1), 4, hipMemcpyDeviceToHost, st));
+    RV_H(hipStreamSynchronize(st));
+    n = *r->h_cnt;
+    round++;
+  }
+  RV_R(rv_intra_stats(g.nsb, r->i_elig, r->i_was, stats, st));
+  RV_H(hipMemcpyAsync(stats + 2, &round, 4, hipMemcpyHostToDevice, st));
+  return RV_OK;
+}
+
 extern "C" {
 
 void rv_replay_destroy(rv_replay *r) {
@@ -1079,6 +1197,7 @@ void rv_replay_destroy(rv_replay *r) {
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->side) (void)hipStreamSynchronize(r->side);
   for (void *p : r->allocs) (void)hipFree(p);
+  if (r->h_cnt) (void)hipHostFree(r->h_cnt);
   for (int f = 0; f < rv_replay::kRing; f++)
     for (int i = 0; i < rv_replay::kEv; i++)
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
@@ -1231,6 +1350,32 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
     }
   }
   r->words = (uint64_t *)dalloc(r, r->nwords * 8);
+  // intra-mode screening: speed 10 4:2:0 unless RV_REPLAY_NO_INTRA
+  r->intra = !r->s6 && !(cfg->flags & RV_REPLAY_NO_INTRA) && g.xdec == 1 && g.ydec == 1;
+  r->i_stats = (uint32_t *)dalloc(r, (size_t)rv_replay::kRing * 3 * 4);
+  ok = ok && r->i_stats && hipMemsetAsync(r->i_stats, 0, (size_t)rv_replay::kRing * 3 * 4,
+                                          r->stream) == hipSuccess;
+  if (r->intra) {
+    const size_t n = (size_t)g.nsb;
+    r->i_elig = (uint8_t *)dalloc(r, n);
+    r->i_was = (uint8_t *)dalloc(r, n);
+    r->i_win = (uint8_t *)dalloc(r, 2 * n);
+    r->i_modes = (uint8_t *)dalloc(r, 4 * n);
+    r->i_mark = (int32_t *)dalloc(r, 4 * n);
+    r->i_list[0] = (int32_t *)dalloc(r, 4 * n);
+    r->i_list[1] = (int32_t *)dalloc(r, 4 * n);
+    r->i_commit = (int32_t *)dalloc(r, 4 * n);
+    r->i_revert = (int32_t *)dalloc(r, 4 * n);
+    r->i_cnt = (int32_t *)dalloc(r, 4 * sizeof(int32_t));
+    r->i_edges = dalloc(r, n * 3 * kIntraEdge * (g.hbd ? 2 : 1));
+    r->i_lout = (uint64_t *)dalloc(r, n * 3 * 3 * 8);
+    r->i_cout = (uint64_t *)dalloc(r, n * 6 * 3 * 8 * 2);
+    ok = ok && r->i_elig && r->i_was && r->i_win && r->i_modes && r->i_mark && r->i_list[0] &&
+         r->i_list[1] && r->i_commit && r->i_revert && r->i_cnt && r->i_edges && r->i_lout &&
+         r->i_cout && hipHostMalloc((void **)&r->h_cnt, 16, hipHostMallocDefault) == hipSuccess;
+    if (r->i_was) (void)hipMemsetAsync(r->i_was, 0, n, r->stream);
+    if (r->i_win) (void)hipMemsetAsync(r->i_win, 0, 2 * n, r->stream);
+  }
   if (cfg->flags & RV_REPLAY_CDEF) {
     if (!(cfg->flags & RV_REPLAY_DEBLOCK) || (g.W & 7) || (g.H & 7)) {
       rv_set_error(RV_EINVAL, "rv_replay_create: RV_REPLAY_CDEF needs RV_REPLAY_DEBLOCK and a "
@@ -1318,6 +1463,9 @@ int rv_replay_set_level_params(rv_replay *r, int level, const rv_replay_level_pa
   RV_R(rv_quant_ctx(p->base_q_idx, 64 * 64, 0, bd, p->dc_delta_q[0], p->ac_delta_q[0], &L.ql));
   RV_R(rv_quant_ctx(p->base_q_idx, 32 * 32, 0, bd, p->dc_delta_q[1], p->ac_delta_q[1], &L.qu));
   RV_R(rv_quant_ctx(p->base_q_idx, 32 * 32, 0, bd, p->dc_delta_q[2], p->ac_delta_q[2], &L.qv));
+  RV_R(rv_quant_ctx(p->base_q_idx, 64 * 64, 1, bd, p->dc_delta_q[0], p->ac_delta_q[0], &L.qil));
+  RV_R(rv_quant_ctx(p->base_q_idx, 32 * 32, 1, bd, p->dc_delta_q[1], p->ac_delta_q[1], &L.qiu));
+  RV_R(rv_quant_ctx(p->base_q_idx, 32 * 32, 1, bd, p->dc_delta_q[2], p->ac_delta_q[2], &L.qiv));
   for (int l = 1; r->s6 && l < kLevels; l++) {  // speed 6: the smaller transforms
     const rv_replay::PLevel &P = r->pl[l];
     RV_R(rv_quant_ctx(p->base_q_idx, P.B * P.B, 0, bd, p->dc_delta_q[0], p->ac_delta_q[0], &L.qs[l][0]));
@@ -1486,9 +1634,10 @@ int rv_replay_import(rv_replay *r) {
   return pad_slot(r, s);
 }
 
-// Event layout per instrumented frame: e[0] start, e[1..12] after F0, F1,
+// Event layout per instrumented frame: e[0] start, e[1..13] after F0, F1,
 // F2, FL (lookahead), F3 full-pel, F3 sub-pel, F4 single-reference
-// candidates, F4 compound candidates, F4 argmin, F6 commit, F5, F7.
+// candidates, F4 compound candidates, F4 argmin, F6 commit, F6b intra, F5,
+// F7.
 int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   if (!r) return rv_set_error(RV_EINVAL, "rv_replay_frame: null");
   const Geo &g = r->g;
@@ -1581,13 +1730,13 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       RV_H(hipStreamWaitEvent(r->side, r->ev_fork, 0));
       ls = r->side;
     }
-    if (tm) RV_H(hipEventRecord(e[13], ls));
+    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv], ls));
     const int nl = nr * g.R * 16;
     fill_preds_kernel<<<(nl + 255) / 256, 256, 0, ls>>>(r->jobs_look[lv], r->src_look, nl,
                                                         r->coarse, r->half, 0);
     RV_R(rv_diamond_search_multi(&cur.y, refs_o, g.R, r->jobs_look[lv], nr * 16, 16, 16, 0, 0,
                                  0, g.bd, r->look, nullptr, nullptr, ls));
-    if (tm) RV_H(hipEventRecord(e[14], ls));
+    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 1], ls));
     if (r->overlap) RV_H(hipEventRecord(r->ev_join, ls));
   }
   RV_EV(4);
@@ -1820,6 +1969,9 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, st, 2));
   }
   RV_EV(10);
+  // F6b intra-mode screening + intra RDO of the non-skip superblocks
+  if (r->intra) RV_R(intra_pass(r, la, ca, cur, S, L, slot));
+  RV_EV(11);
   // F5 importance SATD against reference 0 (the sum was zeroed by the argmin)
   {
     const unsigned nb = (unsigned)((r->n_imp + 255) / 256);
@@ -1830,7 +1982,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       importance_kernel<uint8_t><<<nb, 256, 0, st>>>(g, cur.y, refs_o[0], r->look, r->imp_bx,
                                                      r->imp_by, r->tail + 2);
   }
-  RV_EV(11);
+  RV_EV(12);
   // F7 deblock_filter_frame (src/encoder.rs:2789-2793) when enabled: the
   // block map of the committed blocks, then (once every group's pixels and
   // map are in) Y, U, V in place; the reconstruction becomes a reference
@@ -1871,7 +2023,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
 #endif
     }
   }
-  RV_EV(12);
+  RV_EV(13);
 #undef RV_EV
   if (info) *info = fi;
   RV_H(hipGetLastError());
@@ -1946,7 +2098,7 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
   for (int f = 0; f < last; f++) {
     hipEvent_t *e = r->evs[(r->timed - 1 - f) % rv_replay::kRing];
     RV_H(hipEventSynchronize(e[kS - 1]));
-    RV_H(hipEventSynchronize(e[14]));
+    RV_H(hipEventSynchronize(e[kS + 1]));
     n = 0;
     for (int i = 0; i < kS - 1 && n < cap; i++) {
       float ms = 0.f;
@@ -1955,7 +2107,7 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
     }
     if (n < cap) {  // the lookahead's own span (overlapped with F3/F4 by default)
       float ms = 0.f;
-      RV_H(hipEventElapsedTime(&ms, e[13], e[14]));
+      RV_H(hipEventElapsedTime(&ms, e[kS], e[kS + 1]));
       ms_out[n++] += ms;
     }
   }
@@ -2007,7 +2159,13 @@ int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
       b += ce[(size_t)(f * kLevels + l) * 2 + 1];
     }
   }
-  return nl == 1 ? 5 : 11;
+  if (cap < 14) return nl == 1 ? 5 : 11;
+  std::vector<uint32_t> is((size_t)nf * 3);
+  if (nf) RV_H(hipMemcpy(is.data(), r->i_stats, is.size() * 4, hipMemcpyDeviceToHost));
+  out[11] = out[12] = out[13] = 0;
+  for (int f = 0; f < nf; f++)
+    for (int k = 0; k < 3; k++) out[11 + k] += is[(size_t)f * 3 + k];
+  return 14;
 }
 
 // ---- RCCL communicator for the tile-group exchange ---------------------------

@@ -23,9 +23,12 @@ RV_REPLAY_EXHAUSTIVE_FS = 4  # F1 without successive elimination (same results)
 RV_REPLAY_SPEED6 = 8  # the speed-6 schedule: partition RDO 64x64 .. 8x8 (config D)
 RV_REPLAY_DEBLOCK = 16  # deblock every coded frame before it becomes a reference (1 group)
 RV_REPLAY_CDEF = 32  # CDEF after deblocking (needs RV_REPLAY_DEBLOCK), cdef_bits 0
+RV_REPLAY_NO_INTRA = 64  # no intra-mode screening of non-skip superblocks (default: on
+#                          at speed 10 in 4:2:0)
 # HIP-event stages of a frame: F0, F1, F2, FL (lookahead), F3 full-pel, F3
-# sub-pel, F4 single, F4 compound, F4 argmin, F6 commit, F5, F7
-N_STAGES = 13
+# sub-pel, F4 single, F4 compound, F4 argmin, F6 commit, F6b intra, F5, F7,
+# then the lookahead's own span
+N_STAGES = 14
 
 # GOP of the reference's reorder pyramid (src/api/internal.rs:61-95):
 # group_input_len 4, levels 0,1,2,2 -> me_range_scale = 4 >> level
@@ -340,10 +343,11 @@ class HipReplay:
     def counters(self) -> np.ndarray:
         """[F3 full-pel evals, F3 sub-pel evals, frames, F4 single-reference
         candidates, F4 compound candidates of the 64x64 blocks, then (speed
-        6) single / compound of the 32x32, 16x16 and 8x8 blocks] over the
-        last <= 64 frames."""
-        out = np.zeros(11, dtype=np.uint64)
-        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 11) - 11, "rv_replay_counters")
+        6) single / compound of the 32x32, 16x16 and 8x8 blocks, superblocks
+        intra-screened, intra winners, intra rounds] over the last <= 64
+        frames."""
+        out = np.zeros(14, dtype=np.uint64)
+        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 14) - 14, "rv_replay_counters")
         return out
 
     def close(self):

@@ -481,7 +481,7 @@ class CpuReplay:
 
     def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, group=None,
                  tile_size=(0, 0), n_inputs=8, threads=1, L=None, quantizer=100, speed=10,
-                 deblock=False, cdef=False):
+                 deblock=False, cdef=False, intra=True):
         from rav1e_amd import rate as RT
         L = L or lib()
         self.L = L
@@ -510,6 +510,12 @@ class CpuReplay:
         L.orc_replay_set_deblock.argtypes = [C.c_void_p, C.c_int]
         assert L.orc_replay_set_deblock(self.h, 1 if deblock else 0) == 0, "orc_replay_set_deblock"
         self.speed = speed
+        # intra-mode screening of non-skip superblocks: speed 10, 4:2:0 (the
+        # replay's default; RV_REPLAY_NO_INTRA turns it off on the GPU)
+        self.intra = bool(intra and speed == 10 and xdec == 1 and ydec == 1)
+        L.orc_replay_set_intra.argtypes = [C.c_void_p, C.c_int]
+        assert L.orc_replay_set_intra(self.h, 1 if self.intra else 0) == 0
+        L.orc_replay_intra_stats.argtypes = [C.c_void_p, C.c_void_p]
         self.n_words = result_words(width, height, n_refs, tw, th, tx0, ty0, speed)
         self.geom = (width, height, xdec, ydec, bit_depth)
         self.levels = RT.level_params(quantizer, bit_depth)
@@ -524,6 +530,12 @@ class CpuReplay:
     def set_input(self, idx, yuv):
         yuv = np.ascontiguousarray(yuv)
         assert self.L.orc_replay_set_input(self.h, idx, yuv.ctypes.data) == 0
+
+    def intra_stats(self):
+        """(superblocks screened, intra winners) of the last coded frame."""
+        out = np.zeros(2, np.uint64)
+        self.L.orc_replay_intra_stats(self.h, out.ctypes.data)
+        return int(out[0]), int(out[1])
 
     def set_importances(self, imp):
         if imp is None:

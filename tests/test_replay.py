@@ -263,6 +263,50 @@ def test_cpu_speed6_partition_and_levels():
     assert tail[0] != 0  # some committed block codes coefficients at quantizer 60
 
 
+def test_cpu_replay_intra_screening():
+    """New smooth content the references do not hold: non-skip superblocks
+    get the intra screening, some choose an intra mode (result word 1000 +
+    16 luma + chroma), their reconstruction follows the new content; with
+    RV_REPLAY_NO_INTRA the same frames stay inter."""
+    w, h = 320, 256
+    fr = intra_frames(w, h, 1, 1, 8, 10)
+    res = {}
+    for intra in (True, False):
+        r = O.CpuReplay(w, h, 1, 1, 8, 2, n_inputs=10, threads=4, intra=intra)
+        for i, f in enumerate(fr):
+            r.set_input(i, f)
+        r.frame()
+        wins, words, recs = 0, [], []
+        for _ in range(5):
+            fi = r.frame()
+            wins += r.intra_stats()[1]
+            words.append(_sb_words(r.results(), 20, 2)[:, 2 * PER_REF].copy())
+            recs.append((fi["display"], r.get_recon(fi["display"])))
+        res[intra] = (wins, words, recs)
+        r.close()
+    wins, words, recs = res[True]
+    assert wins > 0 and any((wd >= 1000).any() for wd in words)
+    assert res[False][0] == 0 and all((wd < 1000).all() for wd in res[False][1])
+    for wd in words:
+        for v in wd[wd >= 1000]:
+            assert (v - 1000) // 16 < 13 and (v - 1000) % 16 < 13
+    # intra improves the new content's reconstruction
+    e = [np.abs(a[1].astype(int) - fr[a[0]].astype(int)).sum() for a in recs]
+    e0 = [np.abs(a[1].astype(int) - fr[a[0]].astype(int)).sum() for a in res[False][2]]
+    assert sum(e) < sum(e0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,bd,tiling", [(320, 256, 8, None), (384, 256, 10, {"tile_cols": 2}),
+                                           (256, 192, 12, None)])
+def test_gpu_replay_intra_matches_cpu(w, h, bd, tiling):
+    """The intra pass (screening, intra RDO, the round-by-round fixed point)
+    on content where intra wins: words and reconstructions equal the CPU
+    replay's tile raster order."""
+    _gpu_vs_cpu(w, h, 1, 1, bd, 2, 9, tiling, inputs=intra_frames(w, h, 1, 1, bd, 17),
+                want_intra=True)
+
+
 @pytest.mark.gpu
 def test_gpu_synth_equals_numpy_twin():
     import rav1e_amd as R
@@ -275,7 +319,35 @@ def test_gpu_synth_equals_numpy_twin():
         g.close()
 
 
-def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=None, quantizer=100):
+def intra_frames(w, h, xdec, ydec, bd, n, seed=7):
+    """The synthetic clip with new smooth content appearing on odd frames
+    (ramps, a flat patch, a diagonal edge) that the references do not hold:
+    inter prediction fails there and intra candidates win."""
+    rng = np.random.default_rng(seed)
+    out = []
+    mx = (1 << bd) - 1
+    for t in range(n):
+        f = RP.synth_frame(w, h, t, xdec, ydec, bd).copy()
+        if t % 2 == 1:
+            Y = f[: w * h].reshape(h, w)
+            for k in range(max(1, (w * h) // (160 * 160))):
+                bw, bh = int(rng.integers(64, 200)), int(rng.integers(64, 160))
+                x0, y0 = int(rng.integers(0, max(1, w - bw))), int(rng.integers(0, max(1, h - bh)))
+                yy, xx = np.mgrid[0:min(bh, h - y0), 0:min(bw, w - x0)]
+                kind = (t + k) % 3
+                if kind == 0:
+                    v = 30 + xx * rng.uniform(0.3, 1.2) + yy * rng.uniform(0, 0.5)
+                elif kind == 1:
+                    v = np.full(xx.shape, rng.uniform(20, 230))
+                else:
+                    v = np.where(xx > yy, 60.0, 190.0) + (xx + yy) * 0.1
+                Y[y0:y0 + yy.shape[0], x0:x0 + xx.shape[1]] = np.clip(v * (1 << (bd - 8)), 0, mx)
+        out.append(f)
+    return out
+
+
+def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=None, quantizer=100,
+                inputs=None, want_intra=False):
     import rav1e_amd as R
     R.require_device(0)
     t = RP.tiling_for(w, h, **(tiling or {}))
@@ -284,23 +356,32 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
     g = RP.HipReplay(w, h, xdec, ydec, bd, refs, tile_size=ts, n_inputs=nin, flags=flags,
                      quantizer=quantizer)
     g.synth_inputs(0)
+    if inputs is not None:
+        for i in range(nin):
+            g.set_input(i, inputs[i])
     c = O.CpuReplay(w, h, xdec, ydec, bd, refs, tile_size=ts, n_inputs=nin,
                     threads=O.cpu_share(), quantizer=quantizer,
                     speed=6 if flags & RP.RV_REPLAY_SPEED6 else 10,
                     deblock=bool(flags & RP.RV_REPLAY_DEBLOCK),
-                    cdef=bool(flags & RP.RV_REPLAY_CDEF))
+                    cdef=bool(flags & RP.RV_REPLAY_CDEF),
+                    intra=not flags & RP.RV_REPLAY_NO_INTRA)
     for i in range(nin):
         c.set_input(i, g.get_input(i))
     if imp is not None:
         g.set_importances(imp)
         c.set_importances(imp)
+    won = 0
     for n in range(frames):
         gi, ci = g.frame(), c.frame()
         assert gi == ci
         gw, cw = g.results(), c.results()
         bad = np.nonzero(gw != cw)[0]
         assert bad.size == 0, (n, gi, bad[:10], gw[bad[:10]], cw[bad[:10]])
+        won += c.intra_stats()[1] if c.intra else 0
     np.testing.assert_array_equal(g.get_recon(gi["display"]), c.get_recon(ci["display"]))
+    if want_intra:
+        cnt = g.counters()
+        assert won > 0 and cnt[12] == won, (won, cnt[11:14])
     g.close()
     c.close()
 
