@@ -317,6 +317,24 @@ int rv_deblock_plane(const rv_plane *plane, int pli, int width, int height, cons
 /* deblock_filter_optimize's fast path (src/deblock.rs:1477-1517, speed >= 8):
  * the level from the frame's ac quantizer (ac_q(base_q_idx, 0, bd)). */
 int rv_deblock_fast_level(int ac_q, int bit_depth, int is_key);
+/* sse_optimize (src/deblock.rs:1418-1475, deblock_filter_optimize below
+ * speed 8; replaces sse_plane :1337-1407 and its sse_v_edge / sse_h_edge /
+ * sse_size{4,6,8,14}): rec[3] / src[3] = the frame's unfiltered
+ * reconstruction and its source (Y U V, the chroma planes' width / height =
+ * the luma's rounded up >> xdec / ydec); reads outside a plane's width are
+ * 128, the fill of a fresh plane.  d_tally (device, 3 x 130 int64) receives
+ * each plane's vertical then horizontal level tallies (65 each, not prefix
+ * summed), d_levels (device, 4 bytes) the chosen DeblockState.levels [Y
+ * vertical, Y horizontal, U, V].  Block map as rv_deblock_plane. */
+int rv_deblock_sse(const rv_plane *rec, const rv_plane *src, int width, int height,
+                   const uint8_t *d_lg, const uint8_t *d_skip, int mi_stride, int64_t *d_tally,
+                   uint8_t *d_levels, int bit_depth, void *stream);
+/* deblock_filter_frame (src/deblock.rs:1410-1416) of planes[3] with the
+ * levels in device memory (d_levels, e.g. from rv_deblock_sse); nothing is
+ * filtered when both luma levels are 0 (src/encoder.rs:2790-2793). */
+int rv_deblock_frame(const rv_plane *planes, int width, int height, const uint8_t *d_lg,
+                     const uint8_t *d_skip, int mi_stride, const uint8_t *d_levels, int bit_depth,
+                     void *stream);
 
 /* ---- CDEF (src/cdef.rs) ------------------------------------------------
  * cdef_filter_frame (src/cdef.rs:542-641) as two steps on device planes.

@@ -188,6 +188,162 @@ void orc_deblock_plane(void *origin, ptrdiff_t stride, int hbd, int bd, int widt
   }
 }
 
+/* ---- sse_optimize (src/deblock.rs:1418-1475): the level search of
+ * deblock_filter_optimize below speed 8.  Every edge segment row is measured
+ * unfiltered against the source: the tally at index L gains the SSE change
+ * of the filter a level-L pass would apply, so the prefix sum at L is the
+ * plane's SSE at level L (each edge filtered from the unfiltered
+ * reconstruction, the directions separable). */
+
+/* the mask / flat / nhev decisions of sse_size{4,6,8,14} (:425-999) on the
+ * n taps of one row: mask clamped to [1, 64], nhev to [mask, 64]; flat: 0 =
+ * narrow, 1 = wide (6 / 8), 2 = wide14 */
+static void sse_decide(const int32_t *t, int n, int s, int *mask, int *nhev, int *flat) {
+  const int fl = 1 << s;
+  int m, f = 0;
+  const int32_t *c; /* p1 p0 q0 q1 */
+  if (n == 4) {
+    c = t;
+    m = imax(limit_to_level(imax(iabs(t[0] - t[1]), iabs(t[3] - t[2])), s), blim(t, s));
+  } else if (n == 6) {
+    c = t + 1;
+    m = imax(limit_to_level(imax(iabs(t[0] - t[1]), imax(iabs(t[1] - t[2]),
+                            imax(iabs(t[5] - t[4]), iabs(t[4] - t[3])))), s), blim(c, s));
+    f = imax(iabs(t[1] - t[2]), imax(iabs(t[4] - t[3]), imax(iabs(t[0] - t[2]), iabs(t[5] - t[3])))) <= fl;
+  } else {
+    const int32_t *in = n == 8 ? t : t + 3;
+    c = in + 2;
+    m = imax(limit_to_level(imax(iabs(in[0] - in[1]), imax(iabs(in[1] - in[2]),
+             imax(iabs(in[2] - in[3]), imax(iabs(in[7] - in[6]),
+             imax(iabs(in[6] - in[5]), iabs(in[5] - in[4])))))), s), blim(c, s));
+    f = imax(iabs(in[2] - in[3]), imax(iabs(in[5] - in[4]), imax(iabs(in[1] - in[3]),
+        imax(iabs(in[6] - in[4]), imax(iabs(in[0] - in[3]), iabs(in[7] - in[4])))))) <= fl;
+    if (f && n == 14 &&
+        imax(iabs(t[2] - t[6]), imax(iabs(t[11] - t[7]), imax(iabs(t[1] - t[6]),
+        imax(iabs(t[12] - t[7]), imax(iabs(t[0] - t[6]), iabs(t[13] - t[7])))))) <= fl)
+      f = 2;
+  }
+  *mask = m < 1 ? 1 : m > 64 ? 64 : m;
+  const int h = nhev4(c, s);
+  *nhev = h < *mask ? *mask : h > 64 ? 64 : h;
+  *flat = f;
+}
+
+/* one variant of the row: the taps after filter `kind` (0 none, 1 narrow2,
+ * 2 narrow4, 3 wide), then the SSE of the compared outputs (taps [o, n-o),
+ * o = 0 for 4 taps else 1) against the source (stride_sse, :337-344) */
+static int64_t sse_variant(const int32_t *taps, const int32_t *a, int n, int kind, int flat, int s) {
+  int32_t t[14];
+  for (int i = 0; i < n; i++) t[i] = taps[i];
+  int32_t *c = t + (n == 4 ? 0 : n == 6 ? 1 : n == 8 ? 2 : 5);
+  if (kind == 1) narrow2(c, s);
+  if (kind == 2) narrow4(c, s);
+  if (kind == 3) {
+    /* the wide filters of filter_taps: level 63 passes every mask and the
+     * flatness decides (the caller only asks for wide when flat) */
+    filter_taps(t, n, 63, s + 8);
+    (void)flat;
+  }
+  const int o = n == 4 ? 0 : 1;
+  int64_t acc = 0;
+  for (int i = o; i < n - o; i++) acc += (int64_t)(a[i] - t[i]) * (a[i] - t[i]);
+  return acc;
+}
+
+/* the tally updates of one row (sse_size4 .. sse_size14's accumulation) */
+static void sse_row(const int32_t *t, const int32_t *a, int n, int bd, int64_t *tally) {
+  const int s = bd - 8;
+  int mask, nhev, flat;
+  sse_decide(t, n, s, &mask, &nhev, &flat);
+  const int64_t none = sse_variant(t, a, n, 0, 0, s);
+  tally[0] += none;
+  tally[mask] -= none;
+  if (flat) {
+    tally[mask] += mask <= 63 ? sse_variant(t, a, n, 3, flat, s) : none;
+  } else {
+    const int64_t n2 = nhev != mask ? sse_variant(t, a, n, 1, 0, s) : none;
+    const int64_t n4 = nhev <= 63 ? sse_variant(t, a, n, 2, 0, s) : none;
+    tally[mask] += n2;
+    tally[nhev] -= n2;
+    tally[nhev] += n4;
+  }
+}
+
+/* pixel x of row y, 128 outside [0, pw): the fill of a fresh plane
+ * (src/frame/plane.rs:130-134); neither the reconstruction nor the input
+ * frame is padded before the loop filters (src/encoder.rs:2789-2793) */
+static int32_t px_or_128(const void *o, ptrdiff_t stride, int hbd, int pw, int x, int y) {
+  return x < 0 || x >= pw ? 128 : orc_px(o, hbd, (ptrdiff_t)y * stride + x);
+}
+
+void orc_deblock_sse_plane(const void *rec, ptrdiff_t rstride, const void *src, ptrdiff_t sstride,
+                           int hbd, int bd, int width, int height, int xdec, int ydec, int pli,
+                           const uint8_t *lg, const uint8_t *skip, int mi_stride,
+                           int64_t v_tally[65], int64_t h_tally[65]) {
+  const int cols = (width + 3) >> 2, rows = (height + 3) >> 2;
+  const int pw = (width + xdec) >> xdec;
+  const int cap = pli == 0 ? 14 : 6;
+  for (int k = 0; k < 65; k++) v_tally[k] = h_tally[k] = 0;
+  /* sse_plane's edge walk (:1351-1406): vertical edges x >= 1 << xdec on
+   * every row, horizontal edges y >= 1 << ydec on every column */
+  for (int pass = 0; pass < 2; pass++) {
+    const int vert = pass == 0;
+    const int dec = vert ? xdec : ydec;
+    int64_t *tally = vert ? v_tally : h_tally;
+    for (int y = vert ? 0 : 1 << ydec; y < rows; y += 1 << ydec)
+      for (int x = vert ? 1 << xdec : 0; x < cols; x += 1 << xdec) {
+        const int b = y * mi_stride + x;
+        const int pos = vert ? x : y;
+        if (((pos >> dec) & (tx_mi(lg[b], pli, dec) - 1)) != 0) continue;
+        const int px_ = (x | xdec) - (vert ? 1 << xdec : 0);
+        const int py_ = (y | ydec) - (vert ? 0 : 1 << ydec);
+        const int pb = py_ * mi_stride + px_;
+        if (!((pos & ((1 << lg[b]) - 1)) == 0 || !skip[b] || !skip[pb])) continue;
+        /* sse_h_edge (:1129-1171) sizes the filter with deblock_size(...,
+         * vertical = true, ...) and measures the rows across the column
+         * po.x - size / 2 (pitch 1), as sse_v_edge does: both directions
+         * tally horizontal taps */
+        const int size = imin(cap, imin(tx_mi(lg[b], pli, xdec), tx_mi(lg[pb], pli, xdec)) << 2);
+        const int ox = (x * 4) >> xdec, oy = (y * 4) >> ydec;
+        for (int k = 0; k < 4; k++) {
+          int32_t t[14], a[14];
+          for (int i = 0; i < size; i++) {
+            t[i] = px_or_128(rec, rstride, hbd, pw, ox - size / 2 + i, oy + k);
+            a[i] = px_or_128(src, sstride, hbd, pw, ox - size / 2 + i, oy + k);
+          }
+          sse_row(t, a, size, bd, tally);
+        }
+      }
+  }
+}
+
+/* sse_optimize's choice (:1441-1473): prefix sums to MAX_LOOP_FILTER, the
+ * first minimum; luma per direction, chroma over both directions */
+void orc_deblock_sse_levels(const int64_t v_tally[3][65], const int64_t h_tally[3][65],
+                            uint8_t levels[4]) {
+  for (int p = 0; p < 3; p++) {
+    int64_t v[64], h[64];
+    v[0] = v_tally[p][0];
+    h[0] = h_tally[p][0];
+    for (int i = 1; i < 64; i++) {
+      v[i] = v[i - 1] + v_tally[p][i];
+      h[i] = h[i - 1] + h_tally[p][i];
+    }
+    int bv = 0, bh = 0, bc = 0;
+    for (int i = 1; i < 64; i++) {
+      if (v[bv] > v[i]) bv = i;
+      if (h[bh] > h[i]) bh = i;
+      if (v[bc] + h[bc] > v[i] + h[i]) bc = i;
+    }
+    if (p == 0) {
+      levels[0] = (uint8_t)bv;
+      levels[1] = (uint8_t)bh;
+    } else {
+      levels[p + 1] = (uint8_t)bc;
+    }
+  }
+}
+
 /* deblock_filter_optimize's fast path (src/deblock.rs:1477-1517,
  * speed >= 8): one level for every plane and direction from the frame's
  * ac quantizer. */

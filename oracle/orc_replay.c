@@ -93,6 +93,7 @@ typedef struct orc_replay {
   size_t nwords, wpart;
   /* RV_REPLAY_DEBLOCK (orc_replay_set_deblock): the block map, fast levels */
   int deblock, mi_cols, mi_rows;
+  uint8_t db_levels[4]; /* the last deblocked frame's levels */
   uint8_t *mi_lg, *mi_skip;
   /* RV_REPLAY_CDEF (orc_replay_set_cdef): (y, uv) strengths per level */
   int cdef;
@@ -469,19 +470,39 @@ static void map_own(orc_replay *r) {
   }
 }
 
-/* deblock_filter_optimize's fast levels + deblock_filter_frame
- * (src/encoder.rs:2789-2793) of the frame just coded (the whole frame: its
- * block map must be complete) */
+/* deblock_filter_optimize + deblock_filter_frame (src/encoder.rs:2789-2793)
+ * of the frame just coded (the whole frame: its block map must be
+ * complete): speed 6 searches the levels (sse_optimize, src/deblock.rs:
+ * 1418-1475, against the frame's source), speed 10 takes the fast ones;
+ * nothing is filtered unless a luma level is non-zero. */
 static void deblock_planes(orc_replay *r) {
-  const int qidx = r->lv[r->fi.level].qidx;
-  const uint8_t lv = (uint8_t)orc_deblock_fast_level(orc_ac_q(qidx, 0, r->bd), r->bd, 0);
-  if (!lv) return;
-  const uint8_t lv4[4] = {lv, lv, lv, lv};
   oslot *S = &r->slots[r->fi.display % NSLOT];
   oplane *pl[3] = {&S->y, &S->u, &S->v};
+  uint8_t lv4[4];
+  if (r->s6) {
+    const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
+    const oplane *src[3] = {&cur->y, &cur->u, &cur->v};
+    int64_t v[3][65], h[3][65];
+    for (int p = 0; p < 3; p++)
+      orc_deblock_sse_plane(org_of(pl[p], r->hbd), pl[p]->stride, org_of(src[p], r->hbd),
+                            src[p]->stride, r->hbd, r->bd, r->W, r->H, p ? r->xdec : 0,
+                            p ? r->ydec : 0, p, r->mi_lg, r->mi_skip, r->mi_cols, v[p], h[p]);
+    orc_deblock_sse_levels((const int64_t(*)[65])v, (const int64_t(*)[65])h, lv4);
+  } else {
+    const int qidx = r->lv[r->fi.level].qidx;
+    const uint8_t lv = (uint8_t)orc_deblock_fast_level(orc_ac_q(qidx, 0, r->bd), r->bd, 0);
+    for (int k = 0; k < 4; k++) lv4[k] = lv;
+  }
+  memcpy(r->db_levels, lv4, 4);
+  if (!lv4[0] && !lv4[1]) return;
   for (int p = 0; p < 3; p++)
     orc_deblock_plane(org_of(pl[p], r->hbd), pl[p]->stride, r->hbd, r->bd, r->W, r->H,
                       p ? r->xdec : 0, p ? r->ydec : 0, p, r->mi_lg, r->mi_skip, r->mi_cols, lv4);
+}
+
+/* the levels deblock_filter_optimize chose for the last deblocked frame */
+void orc_replay_deblock_levels(const orc_replay *r, uint8_t out[4]) {
+  memcpy(out, r->db_levels, 4);
 }
 
 /* cdef_filter_frame (src/encoder.rs:2795-2802) of the frame just coded,

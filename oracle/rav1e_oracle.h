@@ -86,6 +86,18 @@ void orc_deblock_plane(void *origin, ptrdiff_t stride, int hbd, int bd, int widt
                        int xdec, int ydec, int pli, const uint8_t *lg, const uint8_t *skip,
                        int mi_stride, const uint8_t levels[4]);
 int orc_deblock_fast_level(int ac_q, int bd, int is_key);
+/* sse_plane (src/deblock.rs:1337-1407) of plane pli: the vertical and
+ * horizontal level tallies (65 entries) of the unfiltered reconstruction
+ * `rec` against the source `src` (visible origins; reads outside the
+ * plane's width are 128, the fill of a fresh plane) */
+void orc_deblock_sse_plane(const void *rec, ptrdiff_t rstride, const void *src, ptrdiff_t sstride,
+                           int hbd, int bd, int width, int height, int xdec, int ydec, int pli,
+                           const uint8_t *lg, const uint8_t *skip, int mi_stride,
+                           int64_t v_tally[65], int64_t h_tally[65]);
+/* sse_optimize's level choice (src/deblock.rs:1441-1473) from the three
+ * planes' tallies */
+void orc_deblock_sse_levels(const int64_t v_tally[3][65], const int64_t h_tally[3][65],
+                            uint8_t levels[4]);
 /* CDEF (src/cdef.rs): cdef_find_dir (:68-126) of the 8x8 block at img
  * (the padded u16 copy), cdef_filter_block (:152-228), adjust_strength
  * (:232-239), and cdef_filter_frame (:542-641) out of place: planes at

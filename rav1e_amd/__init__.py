@@ -250,6 +250,8 @@ def _declare(L):
         "rv_predict_intra_batch": (i32, [P, vp, vp, i32, i32, i32, vp]),
         "rv_deblock_plane": (i32, [P, i32, i32, i32, vp, vp, i32, vp, i32, vp]),
         "rv_deblock_fast_level": (i32, [i32, i32, i32]),
+        "rv_deblock_sse": (i32, [P, P, i32, i32, vp, vp, i32, vp, vp, i32, vp]),
+        "rv_deblock_frame": (i32, [P, i32, i32, vp, vp, i32, vp, i32, vp]),
         "rv_cdef_find_dirs": (i32, [P, i32, i32, vp, i32, vp, vp, i32, vp]),
         "rv_cdef_filter_plane": (i32, [P, P, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32,
                                        vp]),
@@ -578,6 +580,43 @@ def deblock_plane(plane: DevicePlane, pli, width, height, lg: np.ndarray, skip: 
     lv = np.ascontiguousarray(np.asarray(levels, dtype=np.uint8))
     _check(lib().rv_deblock_plane(C.byref(plane.desc), pli, width, height, dl.ptr, ds.ptr,
                                   lg.shape[1], lv.ctypes.data, bit_depth, None), "rv_deblock_plane")
+    _sync()
+
+
+def _map_buffers(width, height, lg, skip, who):
+    lg = np.ascontiguousarray(lg, dtype=np.uint8)
+    skip = np.ascontiguousarray(skip, dtype=np.uint8)
+    if lg.shape != skip.shape or lg.shape[1] < (width + 3) // 4 or lg.shape[0] < (height + 3) // 4:
+        raise Rav1eHipError(who + ": lg / skip must cover the frame's 4x4 grid")
+    if not (lg <= 4).all():
+        raise Rav1eHipError(who + ": block sizes 4x4 .. 64x64 (lg 0 .. 4)")
+    return lg, DeviceBuffer.from_array(lg), DeviceBuffer.from_array(skip)
+
+
+def deblock_sse(rec, src, width, height, lg: np.ndarray, skip: np.ndarray, bit_depth=8):
+    """sse_optimize (src/deblock.rs:1418-1475) of a frame: rec / src = three
+    DevicePlanes each (Y U V).  Returns (tallies (3, 2, 65) int64: vertical,
+    horizontal per plane; levels [Y vertical, Y horizontal, U, V])."""
+    lg, dl, ds = _map_buffers(width, height, lg, skip, "deblock_sse")
+    rp = (RvPlane * 3)(*(p.desc for p in rec))
+    sp = (RvPlane * 3)(*(p.desc for p in src))
+    dt = DeviceBuffer(3 * 130 * 8)
+    dv = DeviceBuffer(4)
+    _check(lib().rv_deblock_sse(rp, sp, width, height, dl.ptr, ds.ptr, lg.shape[1], dt.ptr, dv.ptr,
+                                bit_depth, None), "rv_deblock_sse")
+    _sync()
+    return (dt.download(np.int64, 390).reshape(3, 2, 65),
+            [int(v) for v in dv.download(np.uint8, 4)])
+
+
+def deblock_frame(planes, width, height, lg: np.ndarray, skip: np.ndarray, levels, bit_depth=8):
+    """deblock_filter_frame (src/deblock.rs:1410-1416) of three DevicePlanes
+    with the levels passed through device memory (rv_deblock_frame)."""
+    lg, dl, ds = _map_buffers(width, height, lg, skip, "deblock_frame")
+    pp = (RvPlane * 3)(*(p.desc for p in planes))
+    dv = DeviceBuffer.from_array(np.ascontiguousarray(np.asarray(levels, dtype=np.uint8)))
+    _check(lib().rv_deblock_frame(pp, width, height, dl.ptr, ds.ptr, lg.shape[1], dv.ptr,
+                                  bit_depth, None), "rv_deblock_frame")
     _sync()
 
 

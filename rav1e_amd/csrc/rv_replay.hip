@@ -63,6 +63,12 @@ int rv_deblock_plane_dev(const rv_plane *p, int pli, int width, int height, cons
                          const uint8_t *d_skip, int mi_stride, const uint8_t levels[4],
                          int bit_depth, hipStream_t s);
 extern "C" int rv_deblock_fast_level(int ac_q, int bit_depth, int is_key);
+int rv_deblock_sse_dev(const rv_plane rec[3], const rv_plane src[3], int width, int height,
+                       const uint8_t *d_lg, const uint8_t *d_skip, int mi_stride,
+                       int64_t *d_tally, uint8_t *d_levels, int bit_depth, hipStream_t s);
+int rv_deblock_frame_dev(const rv_plane planes[3], int width, int height, const uint8_t *d_lg,
+                         const uint8_t *d_skip, int mi_stride, const uint8_t *d_levels,
+                         int bit_depth, hipStream_t s);
 extern "C" int rv_q_lookup(int ac, int qindex, int bit_depth);
 // rv_frame.hip
 int rv_plane_pyramid(const rv_plane *y, const rv_plane *h, const rv_plane *q, void *stream);
@@ -610,6 +616,9 @@ struct rv_replay {
   uint8_t *mi_lg = nullptr, *mi_skip = nullptr;  // the deblocking block map
   int mi_stride = 0, mi_cols = 0, mi_rows = 0;
   uint8_t db_level[3] = {0, 0, 0};  // fast level per pyramid level
+  // speed 6: sse_optimize's level search (rv_deblock_sse): tallies, levels
+  int64_t *db_tally = nullptr;
+  uint8_t *db_dlev = nullptr;
   bool cdef = false;                // RV_REPLAY_CDEF
   RvInput cdef_pre;                 // the deblocked, pre-CDEF frame (the padded copy's source)
   uint8_t *cdef_dir = nullptr, *cdef_idx = nullptr;  // per 8x8 block; per 64x64 (all 0)
@@ -1008,9 +1017,21 @@ int pad_slot(rv_replay *r, const RvSlot &s) {
   return RV_OK;
 }
 
-// deblock_filter_frame of a slot with pyramid level lv's fast levels; it
-// runs when a luma level is non-zero (src/encoder.rs:2790-2793)
-int deblock_slot(rv_replay *r, const RvSlot &s, int lv) {
+// deblock_filter_optimize + deblock_filter_frame of a slot coded from input
+// `in` (src/encoder.rs:2789-2793): speed 6 searches the levels on the
+// device (sse_optimize) and the filter reads them there; speed 10 takes
+// pyramid level lv's fast levels.  Nothing is filtered unless a luma level
+// is non-zero.
+int deblock_slot(rv_replay *r, const RvSlot &s, const RvInput &in, int lv) {
+  const rv_plane pl3[3] = {s.y, s.u, s.v};
+  if (r->s6) {
+    const rv_plane src[3] = {in.y, in.u, in.v};
+    const int e = rv_deblock_sse_dev(pl3, src, r->g.W, r->g.H, r->mi_lg, r->mi_skip,
+                                     r->mi_stride, r->db_tally, r->db_dlev, r->g.bd, r->stream);
+    if (e != RV_OK) return e;
+    return rv_deblock_frame_dev(pl3, r->g.W, r->g.H, r->mi_lg, r->mi_skip, r->mi_stride,
+                                r->db_dlev, r->g.bd, r->stream);
+  }
   const uint8_t l = r->db_level[lv];
   if (!l) return RV_OK;
   const uint8_t lv4[4] = {l, l, l, l};
@@ -1402,6 +1423,11 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
     ok = ok && r->mi_lg && r->mi_skip;
     if (r->mi_lg) (void)hipMemsetAsync(r->mi_lg, 4, mb, r->stream);
     if (r->mi_skip) (void)hipMemsetAsync(r->mi_skip, 0, mb, r->stream);
+    if (r->s6) {
+      r->db_tally = (int64_t *)dalloc(r, 3 * 130 * 8);
+      r->db_dlev = (uint8_t *)dalloc(r, 4);
+      ok = ok && r->db_tally && r->db_dlev;
+    }
   }
   r->imp_bx = g.vis_w / 8;
   r->imp_by = g.vis_h / 8;
@@ -1629,7 +1655,8 @@ int rv_replay_import(rv_replay *r) {
   RV_R(xcopy(r, s, rects, n, 1, r->xrecv));
   // the whole frame and its block map are in: deblock it (every rank the
   // same way), then pad
-  if (r->deblock) RV_R(deblock_slot(r, s, r->last.level));
+  if (r->deblock)
+    RV_R(deblock_slot(r, s, r->inputs[r->last.display % r->inputs.size()], r->last.level));
   if (r->cdef) RV_R(cdef_slot(r, s, r->last.level));
   return pad_slot(r, s);
 }
@@ -2004,7 +2031,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   r->coded++;
   r->last = fi;
   if (r->n_groups < 2) {
-    if (r->deblock) RV_R(deblock_slot(r, S, lv));
+    if (r->deblock) RV_R(deblock_slot(r, S, cur, lv));
     if (r->cdef) RV_R(cdef_slot(r, S, lv));
     RV_R(pad_slot(r, S));
   } else {

@@ -66,6 +66,8 @@ def lib():
         L.orc_deblock_plane.argtypes = [vp, sz, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32,
                                         vp]
         L.orc_deblock_fast_level.argtypes = [i32, i32, i32]
+        L.orc_deblock_sse_plane.argtypes = [vp, sz, vp, sz] + [i32] * 7 + [vp, vp, i32, vp, vp]
+        L.orc_deblock_sse_levels.argtypes = [vp, vp, vp]
         L.orc_cdef_find_dir.restype = i32
         L.orc_cdef_find_dir.argtypes = [vp, sz, vp, i32]
         L.orc_cdef_filter_block.argtypes = [vp, sz, i32, vp, sz] + [i32] * 7
@@ -126,6 +128,31 @@ def deblock_plane(full, yo, xo, width, height, xdec, ydec, pli, lg, skip, levels
                             width, height, xdec, ydec, pli, ptr(lg), ptr(skip), lg.shape[1],
                             ptr(lv))
     return full
+
+
+def deblock_sse_plane(rec, src, width, height, xdec, ydec, pli, lg, skip, bd=8):
+    """orc_deblock_sse_plane on visible planes rec / src (same shape): the
+    (vertical, horizontal) tallies, 65 int64 each."""
+    lg = np.ascontiguousarray(lg, dtype=np.uint8)
+    skip = np.ascontiguousarray(skip, dtype=np.uint8)
+    rec = np.ascontiguousarray(rec)
+    src = np.ascontiguousarray(src, dtype=rec.dtype)
+    v = np.zeros(65, np.int64)
+    h = np.zeros(65, np.int64)
+    lib().orc_deblock_sse_plane(ptr(rec), rec.shape[1], ptr(src), src.shape[1], hbd_of(rec), bd,
+                                width, height, xdec, ydec, pli, ptr(lg), ptr(skip), lg.shape[1],
+                                ptr(v), ptr(h))
+    return v, h
+
+
+def deblock_sse_levels(v, h):
+    """orc_deblock_sse_levels: levels [Y vertical, Y horizontal, U, V] from
+    the three planes' tallies (3 x 65 each)."""
+    v = np.ascontiguousarray(v, dtype=np.int64)
+    h = np.ascontiguousarray(h, dtype=np.int64)
+    lv = np.zeros(4, np.uint8)
+    lib().orc_deblock_sse_levels(ptr(v), ptr(h), ptr(lv))
+    return [int(x) for x in lv]
 
 
 def deblock_fast_level(ac_q, bd, is_key=False):
@@ -530,6 +557,13 @@ class CpuReplay:
     def set_input(self, idx, yuv):
         yuv = np.ascontiguousarray(yuv)
         assert self.L.orc_replay_set_input(self.h, idx, yuv.ctypes.data) == 0
+
+    def deblock_levels(self):
+        """deblock_filter_optimize's levels of the last deblocked frame."""
+        out = np.zeros(4, np.uint8)
+        self.L.orc_replay_deblock_levels.argtypes = [C.c_void_p, C.c_void_p]
+        self.L.orc_replay_deblock_levels(self.h, out.ctypes.data)
+        return [int(v) for v in out]
 
     def intra_stats(self):
         """(superblocks screened, intra winners) of the last coded frame."""

@@ -194,6 +194,27 @@ def test_cpu_replay_deblock_changes_the_reference():
     assert (recs[0] != recs[1]).any()
 
 
+def test_cpu_replay_speed6_searches_the_deblocking_levels():
+    """Below speed 8 deblock_filter_optimize searches the levels
+    (sse_optimize, src/deblock.rs:1418-1475): per direction and plane, from
+    the frame's source, instead of one fast level from the quantizer."""
+    w, h = 256, 200
+    fr = _frames(w, h, 1, 1, 8, 8)
+    got = {}
+    for sp in (6, 10):
+        r = O.CpuReplay(w, h, 1, 1, 8, 2, n_inputs=8, threads=2, deblock=True, speed=sp)
+        for i, f in enumerate(fr):
+            r.set_input(i, f)
+        got[sp] = []
+        for _ in range(3):
+            r.frame()
+            got[sp].append(r.deblock_levels())
+        r.close()
+    assert all(len(set(lv)) == 1 for lv in got[10])           # the fast level everywhere
+    assert any(len(set(lv)) > 1 for lv in got[6]) and got[6] != got[10]
+    assert all(0 <= v <= 63 for lv in got[6] for v in lv)
+
+
 def test_cpu_replay_cdef_changes_the_reference():
     """RV_REPLAY_CDEF: after deblocking, the coded frame is CDEF-filtered
     (set_quantizers' inter strengths are non-zero at quantizer 100) before

@@ -1246,9 +1246,95 @@ def gen_rate(I, rng, out):
     print("rate: %d bexp, %d blog, %d set_quantizers" % (len(logs), len(ws), len(rows)))
 
 
+# ---------------------------------------------------------------- sse_optimize
+def gen_sse(I, rng, out):
+    """sse_plane (src/deblock.rs:1337-1407) per plane and sse_optimize
+    (:1418-1475) on frames with a padded (128-filled, Plane::new)
+    reconstruction and source: the tallies and the chosen levels."""
+    dsrc = RI.Source(REF + "deblock.rs")
+    ctx = RI.Source(REF + "context.rs")
+    I.sources.append(dsrc)
+    I.release = True
+    for n in ("BlockOffset", "PlaneBlockOffset"):
+        I.globals.vars[n] = RI.StructType(n)
+        I.define_impl(n, ctx.impl(n))
+    I.globals.vars.update({
+        "MI_SIZE_LOG2": RI.TInt(2, "usize"), "MI_SIZE": RI.TInt(4, "usize"),
+        "BLOCK_TO_PLANE_SHIFT": RI.TInt(2, "usize"), "SUPERBLOCK_TO_BLOCK_SHIFT": RI.TInt(4, "usize"),
+        "MAX_LOOP_FILTER": RI.TInt(63, "usize"), "PLANES": RI.TInt(3, "usize"),
+        "INTRA_FRAME": _RefV(0), "NEARESTMV": RI.TInt(14, "usize"),
+        "GLOBALMV": RI.TInt(18, "usize"), "GLOBAL_GLOBALMV": RI.TInt(26, "usize")})
+    sp = F(I, "sse_plane", "deblock.rs")
+    so = F(I, "sse_optimize", "deblock.rs")
+    cases, recs, srcs, lgs, sks, tallies, levels_out = [], [], [], [], [], [], []
+    shapes = [(64, 48, 1, 1, 8, 2), (72, 40, 0, 0, 10, 3), (56, 64, 1, 0, 12, 1),
+              (80, 56, 1, 1, 10, 4), (48, 48, 1, 1, 8, 0), (64, 32, 0, 0, 8, 6),
+              (96, 64, 1, 1, 12, 2), (40, 56, 1, 1, 10, 8)]
+    for n, (W_, H_, xdec, ydec, bd, amp) in enumerate(shapes):
+        cols, rows = (W_ + 3) // 4, (H_ + 3) // 4
+        lg, sk, _ = _deblock_map(rng, cols, rows, 0 if n % 2 else 1)
+        fb = FrameBlocksV(cols, rows)
+        for y in range(rows):
+            for x in range(cols):
+                n4 = 1 << int(lg[y, x])
+                if x % n4 == 0 and y % n4 == 0:
+                    fb.place(x, y, n4, n4, sk[y, x], False)
+        pad = 8
+        ty = "u8" if bd == 8 else "u16"
+        planes = {"rec": [], "src": []}
+        for pli in range(3):
+            xd, yd = (xdec, ydec) if pli else (0, 0)
+            pw, ph = (W_ + xd) >> xd, (H_ + yd) >> yd
+            yy, xx = np.mgrid[0:ph, 0:pw]
+            src = xx * rng.uniform(0.3, 2) + yy * rng.uniform(0.3, 2) + 50 + rng.integers(-3, 4, (ph, pw))
+            # the reconstruction: the source + a step per 4x4 + noise (amp 0: exact)
+            step = np.kron(rng.integers(-amp, amp + 1, ((ph + 3) // 4, (pw + 3) // 4)),
+                           np.ones((4, 4)))[:ph, :pw]
+            rec = src + step + (rng.integers(-1, 2, (ph, pw)) if amp else 0)
+            for name, img in (("src", src), ("rec", rec)):
+                img = np.clip(img * (1 << (bd - 8)), 0, (1 << bd) - 1).astype(np.int64)
+                full = np.full((ph + 2 * pad, pw + 2 * pad), 128, np.int64)
+                full[pad:pad + ph, pad:pad + pw] = img
+                pl = H.Plane.from_full(full, pad, pad, pw, ph, xd, yd)
+                pl.data = [RI.TInt(v, ty) for v in pl.data]
+                planes[name].append(pl)
+                (recs if name == "rec" else srcs).append(img.astype(np.uint16).reshape(-1))
+        fi = RI.Struct("FrameInvariants", {
+            "width": RI.TInt(W_, "usize"), "height": RI.TInt(H_, "usize"),
+            "sequence": RI.Struct("Sequence", {"bit_depth": RI.TInt(bd, "usize")})})
+        I.globals.vars["T"] = prim(bd)
+        tl = []
+        for pli in range(3):
+            v = [RI.TInt(0, "i64") for _ in range(65)]
+            h = [RI.TInt(0, "i64") for _ in range(65)]
+            sp(fi, planes["rec"][pli], planes["src"][pli], v, h, RI.TInt(pli, "usize"), fb,
+               generics={"T": prim(bd)})
+            tl.append([int(x) for x in v] + [int(x) for x in h])
+        deb = RI.Struct("DeblockState", {"levels": [RI.TInt(0, "u8")] * 4})
+        fs = RI.Struct("FrameState", {
+            "rec": RI.Struct("Frame", {"planes": planes["rec"]}),
+            "input": RI.Struct("Frame", {"planes": planes["src"]}), "deblock": deb})
+        so(fi, fs, fb, generics={"T": prim(bd)})
+        lv = [int(x) for x in fs._f["deblock"]._f["levels"]]
+        cases.append((W_, H_, xdec, ydec, bd, len(lgs)))
+        lgs.append(lg.reshape(-1))
+        sks.append(sk.reshape(-1))
+        tallies.append(tl)
+        levels_out.append(lv)
+        print("  sse %dx%d %d-bit dec %d%d amp %d: levels %s" % (W_, H_, bd, xdec, ydec, amp, lv))
+    out["cases"] = np.array(cases, np.int32)
+    out["rec"] = np.concatenate(recs)
+    out["src"] = np.concatenate(srcs)
+    out["lg"] = np.concatenate(lgs)
+    out["skip"] = np.concatenate(sks)
+    out["map_off"] = np.cumsum([0] + [len(v) for v in lgs]).astype(np.int64)
+    out["tally"] = np.array(tallies, np.int64)  # [case][plane][v 65 | h 65]
+    out["levels"] = np.array(levels_out, np.int32)
+
+
 SECTIONS = {"mc": gen_mc, "dist": gen_dist, "rdo": gen_rdo, "me": gen_me, "quant": gen_quant,
             "tx": gen_tx, "ds": gen_ds, "cdef": gen_cdef, "deblock": gen_deblock,
-            "lookahead": gen_lookahead, "rate": gen_rate}
+            "lookahead": gen_lookahead, "rate": gen_rate, "sse": gen_sse}
 
 
 def main(argv):
@@ -1257,7 +1343,7 @@ def main(argv):
     for n in names:
         I = make_interp()
         # the sections that predate cdef keep the seeds they were generated with
-        old = sorted(set(SECTIONS) - {"cdef", "deblock", "lookahead", "rate"})
+        old = sorted(set(SECTIONS) - {"cdef", "deblock", "lookahead", "rate", "sse"})
         rng = np.random.default_rng(0x5EED + (old.index(n) if n in old else
                                               100 + sorted(set(SECTIONS) - set(old)).index(n)))
         random.seed(1)
