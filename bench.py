@@ -245,6 +245,73 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     return cpu, parity
 
 
+def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2):
+    """The N-rank tile-group split on ONE GPU: config's n tile groups as n
+    HipReplay instances (the ranks), each frame coded group by group with
+    the GPU to itself, the all-gather emulated by device copies into every
+    group's receive buffer (RCCL's layout), then every group's import
+    (unpack, loop filters, pad).  Per group: the HIP-event span of its frame
+    (stages F0 .. F7 on its stream); the projected N-rank step = the slowest
+    group + the slowest import + the all-gather at an assumed xGMI rate."""
+    import ctypes as C
+
+    import rav1e_amd as R
+    from rav1e_amd import replay as RP
+    L = R.lib()
+    ts = (tiling["tile_width_sb"], tiling["tile_height_sb"])
+    rects = RP.tile_groups(tiling, n)
+    gop = len(RP.GOP_SCALES)
+    frames = 1 + gops * gop
+    gs = [RP.HipReplay(W, H, xdec, ydec, bd, nref, group=r, tile_size=ts, n_inputs=frames + 8,
+                       flags=flags) for r in rects]
+    sync = lambda: R._check(L.rv_device_sync(), "rv_device_sync")  # noqa: E731
+    for k, g in enumerate(gs):
+        g.synth_inputs(0)
+        g.set_groups(rects, k, None)
+        g.set_timing(1, 1)
+    bufs = [g.exchange_buffers() for g in gs]
+    nb = bufs[0][2]
+    span = [[] for _ in gs]
+    imp = [[] for _ in gs]
+    for f in range(frames):
+        timed = f > gop  # the second GOP on: every me_range_scale once per GOP
+        for k, g in enumerate(gs):
+            g.frame()
+            sync()
+            if timed:
+                span[k].append(float(g.stage_ms()[:13].sum()))
+        if f == 0:
+            continue  # the key frame: every group copied its own input
+        for k in range(n):
+            for j in range(n):
+                R._check(L.rv_memcpy_d2d(C.c_void_p(bufs[k][1] + j * nb), C.c_void_p(bufs[j][0]),
+                                         nb, None), "rv_memcpy_d2d")
+        sync()
+        for k, g in enumerate(gs):
+            t0 = time.perf_counter()
+            g.import_()
+            sync()
+            if timed:
+                imp[k].append((time.perf_counter() - t0) * 1e3)
+    for g in gs:
+        g.close()
+    per = [sum(s) / len(s) for s in span]
+    imp_ms = max(sum(s) / len(s) for s in imp)
+    xgmi_gbs = 64.0  # assumed all-gather algorithm bandwidth per rank (RCCL over xGMI)
+    ag_ms = (n - 1) * nb / (xgmi_gbs * 1e9) * 1e3
+    proj = max(per) + imp_ms + ag_ms
+    return {"ranks": n, "groups_sb": [list(r) for r in rects],
+            "group_frame_ms": [round(v, 4) for v in per], "max_group_ms": round(max(per), 4),
+            "import_ms_max": round(imp_ms, 4), "exchange_bytes_per_group": int(nb),
+            "allgather_ms_model": round(ag_ms, 4),
+            "allgather_model": f"(n-1) x bytes_per_group at an assumed {xgmi_gbs:g} GB/s",
+            "projected_ms_per_step": round(proj, 4),
+            "projected_frames_per_s": round(1e3 / proj, 2),
+            "frames_averaged": len(span[0]),
+            "method": "one GPU, groups run one after another (HIP-event spans; import wall "
+                      "clock incl. launch), device-copy all-gather"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -260,6 +327,9 @@ def main():
                     help="deblock every coded frame before it becomes a reference")
     ap.add_argument("--cdef", action="store_true",
                     help="deblock and CDEF every coded frame before it becomes a reference")
+    ap.add_argument("--emulate-ranks", type=int, default=8,
+                    help="N > 1 (single-GPU runs): also code the N-rank tile-group split as N "
+                         "replays on this GPU and report the projected N-rank step (0: off)")
     ap.add_argument("--exhaustive-fs", action="store_true",
                     help="F1 coarse search without successive elimination (same results)")
     args = ap.parse_args()
@@ -393,6 +463,10 @@ def main():
             "source": vp[1]["source"]}
     fps = args.steps / dt  # frames of the one stream
 
+    emu = None
+    if rank == 0 and world == 1 and args.emulate_ranks > 1:
+        emu = emulate_ranks(args.emulate_ranks, W, H, xdec, ydec, bd, nref, tiling, flags)
+
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the CPU codes the same frames: the GPU's inputs, downloaded
@@ -439,6 +513,7 @@ def main():
                                 "modes_per_screen": "13 predicted + SATD, 3 RDO x (chroma "
                                                     "mode, DC)"},
             "checksum": int(words[-5]) & 0xFFFFFFFF,
+            **({"emulated_ranks": emu} if emu else {}),
         }
         print(json.dumps(line), flush=True)
     hip.close()

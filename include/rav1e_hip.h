@@ -618,9 +618,11 @@ int rv_replay_set_timing(rv_replay *r, int stride, int block);
  * skip distortion + diff + fwd TX_64X64 + quantize + estimate_rate +
  * inverse + add + non-skip distortion; chroma U and V: the same with
  * TX_32X32 and SSE), [7] F4 compound candidates, [8] F4 rd cost + argmin
- * (+ the join with the lookahead), [9] F6 commit, [10] F5 importance, [11]
- * F7 deblock / pad / exchange, [12] the lookahead's own span (FL, on the
- * side stream, overlapping [4]..[7]).  Returns the count written (<= 13). */
+ * (+ the join with the lookahead), [9] F6 commit, [10] F6b intra-mode
+ * screening + intra RDO rounds, [11] F5 importance, [12] F7 loop filters /
+ * pad / exchange, [13] the lookahead's own span (FL, on the side stream,
+ * overlapping [4]..[7]).  [0] .. [12] tile the frame's span on the replay
+ * stream.  Returns the count written (<= 14). */
 int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
 /* Same breakdown summed over the last `last_frames` instrumented frames
  * (<= 64). */

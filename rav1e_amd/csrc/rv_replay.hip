@@ -1614,7 +1614,7 @@ int rv_replay_set_groups(rv_replay *r, int n_groups, const int32_t *rects, int m
     most = b > most ? b : most;
   }
   r->xbytes = (most + 255) / 256 * 256;
-  if (n_groups > 1) {
+  if (n_groups > 1 || comm) {  // one group + a communicator: a 1-rank all-gather
     r->xsend = (uint8_t *)dalloc(r, r->xbytes);
     r->xrecv = (uint8_t *)dalloc(r, r->xbytes * n_groups);
     if (!r->xsend || !r->xrecv) return rv_set_error(RV_EHIP, "rv_replay_set_groups: alloc");
@@ -1637,8 +1637,9 @@ int rv_replay_exchange_buffers(rv_replay *r, void **send, void **recv, size_t *b
 // then a complete reference on this rank (src/encoder.rs:3411-3429).
 int rv_replay_import(rv_replay *r) {
   if (!r) return rv_set_error(RV_EINVAL, "rv_replay_import: null");
-  // one group, or the key frame (every rank copied its own input): nothing to move
-  if (r->n_groups < 2 || r->last.is_key) return RV_OK;
+  // one group without a communicator, or the key frame (every rank copied
+  // its own input): nothing to move
+  if ((r->n_groups < 2 && !r->comm) || r->last.is_key) return RV_OK;
   const RvSlot &s = r->slots[r->last.display % kSlots];
   XRect rects[5 * kMaxGroups];
   int n = 0;
@@ -2030,7 +2031,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   }
   r->coded++;
   r->last = fi;
-  if (r->n_groups < 2) {
+  if (r->n_groups < 2 && !r->comm) {
     if (r->deblock) RV_R(deblock_slot(r, S, cur, lv));
     if (r->cdef) RV_R(cdef_slot(r, S, lv));
     RV_R(pad_slot(r, S));

@@ -499,6 +499,44 @@ def test_gpu_tile_groups_exchange(flags):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF | RP.RV_REPLAY_SPEED6])
+def test_gpu_replay_one_rank_rccl_exchange(flags):
+    """The RCCL branch of the tile-group exchange (rv_replay.hip: pack,
+    ncclAllGather on the replay stream, import, loop filters, pad) with a
+    1-rank communicator (rv_comm_unique_id / rv_comm_create): the words and
+    every reconstruction equal the run without a communicator."""
+    import os
+
+    import rav1e_amd as R
+    R.require_device(0)
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")  # bootstrap over loopback (no network)
+    L = R.lib()
+    idb = np.zeros(256, np.uint8)
+    assert L.rv_comm_unique_id(idb.ctypes.data, idb.size) > 0, L.rv_last_error()
+    comm = L.rv_comm_create(idb.ctypes.data, 1, 0)
+    assert comm, L.rv_last_error()
+    w, h = 384, 192
+    t = RP.tiling_for(w, h, tile_cols=2)
+    ts = (t["tile_width_sb"], t["tile_height_sb"])
+    rects = RP.tile_groups(t, 1)
+    a, b = (RP.HipReplay(w, h, group=rects[0], tile_size=ts, n_inputs=14, flags=flags)
+            for _ in range(2))
+    a.synth_inputs(0)
+    b.synth_inputs(0)
+    a.set_groups(rects, 0, comm)
+    try:
+        for n in range(7):
+            ia, ib = a.frame(), b.frame()
+            assert ia == ib
+            np.testing.assert_array_equal(a.results(), b.results())
+            np.testing.assert_array_equal(a.get_recon(ia["display"]), b.get_recon(ib["display"]))
+    finally:
+        a.close()
+        b.close()
+        L.rv_comm_destroy(comm)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("config,speed", [("360p", 10), ("1080p", 10), ("2160p", 10),
                                           ("2160p10", 10),
                                           ("2160p10", 6), ("2160p444", 10)])
