@@ -77,8 +77,11 @@ typedef struct orc_replay {
   uint64_t *words;
   int32_t *lev; /* committed levels: per SB luma 1024 + 2 * ntx_c * 1024 */
   uint64_t tail[5];
-  /* speed 6 (orc_replay_set_speed): the 32x32, 16x16 and 8x8 levels */
-  int s6;
+  /* the 32x32, 16x16 and 8x8 levels: speed 6 (orc_replay_set_speed) over
+   * the whole group; speed 10 over the bounding rectangle of the group's
+   * frame-edge superblocks (must_split), in group superblocks (ex0, ey0) +
+   * (ew, eh) */
+  int s6, lvl, ex0, ey0, ew, eh;
   struct olevel {
     int B, n, gw, gh, bc, bch, txl, txc, tx0, ty0, tws, ths;
     orc_mv *full, *sub; /* [R][n] */
@@ -158,6 +161,18 @@ static void adjust_bo(int mi_w, int mi_h, int *bx, int *by, int bw, int bh) {
   *bx = x > 0 ? x : 0;
   *by = y > 0 ? y : 0;
 }
+/* a superblock of the group past the frame's right or bottom edge */
+static int edge_sb(const orc_replay *r, int sb) {
+  return (r->tx0 + sb % r->tw + 1) * SB > r->W || (r->ty0 + sb / r->tw + 1) * SB > r->H;
+}
+/* superblock sb inside the level rectangle: its (x, y) there, else 0 */
+static int in_rect(const orc_replay *r, int sb, int *x, int *y) {
+  const int sx = sb % r->tw - r->ex0, sy = sb / r->tw - r->ey0;
+  if (!r->lvl || sx < 0 || sy < 0 || sx >= r->ew || sy >= r->eh) return 0;
+  *x = sx;
+  *y = sy;
+  return 1;
+}
 static uint64_t pack_mv(orc_mv m) { return ((uint64_t)(uint16_t)m.row << 16) | (uint16_t)m.col; }
 static orc_mv qfull(orc_mv m) {
   orc_mv q = {(int16_t)((m.row / 8) * 8), (int16_t)((m.col / 8) * 8)};
@@ -181,8 +196,8 @@ static int cand_mv_g(const cgeo *g, int sb, int c, orc_mv *mv) {
   const orc_mv *s = g->sub + (size_t)k * g->nsb;
   orc_mv st[2], zero = {0, 0};
   int n = 0;
-  if (fy % g->ths) st[n++] = s[sb - g->tw];
-  if (fx % g->tws) {
+  if (sy > 0 && fy % g->ths) st[n++] = s[sb - g->tw];
+  if (sx > 0 && fx % g->tws) {
     orc_mv v = s[sb - 1];
     if (n == 0 || !mv_eq(v, st[0])) st[n++] = v;
   }
@@ -214,12 +229,12 @@ static void comp_mvs_g(const cgeo *g, int sb, int m, orc_mv *mv0, orc_mv *mv1) {
   const orc_mv *s0 = g->sub, *s1 = g->sub + g->nsb;
   orc_mv zero = {0, 0}, e[2][2] = {{zero, zero}, {zero, zero}};
   int n = 0;
-  if (fy % g->ths) {
+  if (sy > 0 && fy % g->ths) {
     e[0][0] = s0[sb - g->tw];
     e[0][1] = s1[sb - g->tw];
     n = 1;
   }
-  if (fx % g->tws) {
+  if (sx > 0 && fx % g->tws) {
     orc_mv l0 = s0[sb - 1], l1 = s1[sb - 1];
     if (n == 0 || !mv_eq(l0, e[0][0]) || !mv_eq(l1, e[0][1])) {
       e[n][0] = l0;
@@ -258,6 +273,8 @@ static void comp_mvs(const orc_replay *r, int sb, int m, orc_mv *mv0, orc_mv *mv
   cgeo g = sb_geo(r);
   comp_mvs_g(&g, sb, m, mv0, mv1);
 }
+
+static int edge_levels(orc_replay *r);
 
 orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile_x0, int tile_y0,
                               int tile_w, int tile_h, int tile_w_sb, int tile_h_sb, int n_refs,
@@ -323,8 +340,11 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile
   r->words = calloc(r->nwords, 8);
   r->lev = calloc((size_t)r->nsb * (1024 + 2 * r->ntx_c * 1024), 4);
   pthread_mutex_init(&r->mu, NULL);
+  if (edge_levels(r)) return NULL;
   return r;
 }
+
+static void free_levels(orc_replay *r);
 
 void orc_replay_destroy(orc_replay *r) {
   if (!r) return;
@@ -355,6 +375,14 @@ void orc_replay_destroy(orc_replay *r) {
   free(r->sc);
   free(r->words);
   free(r->lev);
+  free_levels(r);
+  free(r->mi_lg);
+  free(r->mi_skip);
+  pthread_mutex_destroy(&r->mu);
+  free(r);
+}
+
+static void free_levels(orc_replay *r) {
   for (int l = 1; l < 4; l++) {
     struct olevel *P = &r->pl[l];
     free(P->full);
@@ -364,35 +392,37 @@ void orc_replay_destroy(orc_replay *r) {
     free(P->cost);
     free(P->lev);
     free(P->leaf);
+    memset(P, 0, sizeof(*P));
   }
   free(r->leaf0);
-  free(r->mi_lg);
-  free(r->mi_skip);
-  pthread_mutex_destroy(&r->mu);
-  free(r);
+  r->leaf0 = NULL;
+  r->lvl = 0;
 }
 
-/* The speed-6 schedule (RV_REPLAY_SPEED6); call before the level params.
- * speed 10 is the default. */
-int orc_replay_set_speed(orc_replay *r, int speed) {
-  if (speed != 6 && speed != 10) return -1;
-  if (speed == 10 || r->s6) return 0;
-  if (r->xdec != r->ydec) return -1;
-  r->s6 = 1;
+/* The level grids over group superblocks (x0, y0) + (w, h) and the result
+ * words: per superblock, then per level block, then one partition mask per
+ * superblock. */
+static int alloc_levels(orc_replay *r, int x0, int y0, int w, int h) {
+  free_levels(r);
+  r->lvl = 1;
+  r->ex0 = x0;
+  r->ey0 = y0;
+  r->ew = w;
+  r->eh = h;
   r->nwords = (size_t)r->nsb * (WPR * r->R + 4);
   for (int l = 1; l < 4; l++) {
     struct olevel *P = &r->pl[l];
     int k = 1 << l;
     P->B = SB >> l;
-    P->gw = r->tw * k;
-    P->gh = r->th * k;
+    P->gw = w * k;
+    P->gh = h * k;
     P->n = P->gw * P->gh;
     P->bc = P->B >> r->xdec;
     P->bch = P->B >> r->ydec;
     P->txl = 4 - l;
     P->txc = P->bc == 32 ? 3 : P->bc == 16 ? 2 : P->bc == 8 ? 1 : 0;
-    P->tx0 = r->tx0 * k;
-    P->ty0 = r->ty0 * k;
+    P->tx0 = (r->tx0 + x0) * k;
+    P->ty0 = (r->ty0 + y0) * k;
     P->tws = r->tws * k;
     P->ths = r->ths * k;
     size_t nr = (size_t)r->R * P->n;
@@ -413,6 +443,33 @@ int orc_replay_set_speed(orc_replay *r, int speed) {
   free(r->words);
   r->words = calloc(r->nwords, 8);
   return r->words && r->leaf0 ? 0 : -1;
+}
+
+/* Speed 10: encode_partition_topdown's must_split (src/encoder.rs:2407-
+ * 2445) at the frame edges: the levels over the bounding rectangle of the
+ * group's superblocks past the right / bottom edge (4:2:0 and 4:4:4). */
+static int edge_levels(orc_replay *r) {
+  int x0 = r->tw, y0 = r->th, x1 = -1, y1 = -1;
+  for (int sb = 0; sb < r->nsb; sb++) {
+    if (!edge_sb(r, sb)) continue;
+    const int x = sb % r->tw, y = sb / r->tw;
+    x0 = x < x0 ? x : x0;
+    y0 = y < y0 ? y : y0;
+    x1 = x > x1 ? x : x1;
+    y1 = y > y1 ? y : y1;
+  }
+  if (x1 < 0 || r->xdec != r->ydec) return 0;
+  return alloc_levels(r, x0, y0, x1 - x0 + 1, y1 - y0 + 1);
+}
+
+/* The speed-6 schedule (RV_REPLAY_SPEED6); call before the level params.
+ * speed 10 is the default. */
+int orc_replay_set_speed(orc_replay *r, int speed) {
+  if (speed != 6 && speed != 10) return -1;
+  if (speed == 10 || r->s6) return 0;
+  if (r->xdec != r->ydec) return -1;
+  r->s6 = 1;
+  return alloc_levels(r, 0, 0, r->tw, r->th);
 }
 
 /* Deblock every coded frame before it becomes a reference (one tile group:
@@ -457,11 +514,11 @@ static void map_own(orc_replay *r) {
   const int R = r->R;
   for (int sb = 0; sb < r->nsb; sb++) {
     const int sx = sb % r->tw, sy = sb / r->tw;
-    if (!r->s6 || r->leaf0[sb])
+    if (!r->lvl || r->leaf0[sb])
       map_block(r, 0, r->tx0 + sx, r->ty0 + sy,
                 (int)r->words[(size_t)sb * (WPR * R + 4) + WPR * R + 1]);
   }
-  for (int l = 1; r->s6 && l < 4; l++) {
+  for (int l = 1; r->lvl && l < 4; l++) {
     const struct olevel *P = &r->pl[l];
     for (int b = 0; b < P->n; b++)
       if (P->leaf[b])
@@ -575,7 +632,7 @@ int orc_replay_set_level_params(orc_replay *r, int level, int base_q_idx, const 
     r->lv[level].ds[p] = ds[p];
     orc_qctx_update(&r->lv[level].q[p], base_q_idx, p ? 3 : 4, 0, r->bd, dc[p], ac[p]);
     orc_qctx_update(&r->lv[level].qi[p], base_q_idx, p ? 3 : 4, 1, r->bd, dc[p], ac[p]);
-    for (int l = 1; r->s6 && l < 4; l++)
+    for (int l = 1; r->lvl && l < 4; l++)
       orc_qctx_update(&r->qs[level][l][p], base_q_idx, p ? r->pl[l].txc : r->pl[l].txl, 0, r->bd,
                       dc[p], ac[p]);
   }
@@ -863,12 +920,11 @@ static void run_half(orc_replay *r, int sb) {
 
 /* Pass A3: the lookahead's build_full_res_pmvs (src/encoder.rs:3021-3166,
  * 16x16 full-pel vs the references' original frames), F3 motion_estimation
- * of the 64x64 (src/me.rs:193-278: zero + the coarse MV, then sub-pel) and,
- * at speed 6, of every 32x32, 16x16 and 8x8 block of the superblock. */
+ * of the 64x64 (src/me.rs:193-278: zero + the coarse MV, then sub-pel) and
+ * of the levels' blocks. */
 static void run_me(orc_replay *r, int sb) {
   const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
   const int R = r->R;
-  const int sx = sb % r->tw, sy = sb / r->tw;
   uint64_t cost;
   const sbgeo g = sb_geo_of(r, sb);
   const double me_lambda = r->lv[r->fi.level].me_lambda;
@@ -931,18 +987,20 @@ static void run_me(orc_replay *r, int sb) {
     r->sub[k * r->nsb + sb] = smv;
     r->sc[k * r->nsb + sb] = cost;
   }
-  if (!r->s6) return;
-  /* speed 6: motion_estimation of every 32x32, then 16x16 and 8x8 block of
-   * the superblock at its own position (src/me.rs:193-278), seeded with the
-   * pmvs entry: a 32x32 its half-res quadrant search, a 16x16 / 8x8 its
-   * 32x32's sub-pel winner */
+  /* the levels (speed 6: every superblock; speed 10: the frame-edge
+   * rectangle): motion_estimation of every 32x32, then 16x16 and 8x8 block
+   * of the superblock at its own position (src/me.rs:193-278), seeded with
+   * the pmvs entry: a 32x32 its half-res quadrant search, a 16x16 / 8x8 its
+   * 32x32's sub-pel winner; sub-pel by SATD at speed 6, SAD at speed 10 */
+  int ex, ey;
+  if (!in_rect(r, sb, &ex, &ey)) return;
   for (int l = 1; l < 4; l++) {
     struct olevel *P = &r->pl[l];
     const int k2 = 1 << l, B = P->B;
     const struct olevel *U = &r->pl[1];
     for (int j = 0; j < k2; j++)
       for (int i = 0; i < k2; i++) {
-        const int bx = sx * k2 + i, by = sy * k2 + j, b = by * P->gw + bx;
+        const int bx = ex * k2 + i, by = ey * k2 + j, b = by * P->gw + bx;
         const int X = (P->tx0 + bx) * B, Y = (P->ty0 + by) * B;
         int mb[4];
         mv_range(r, X >> 2, Y >> 2, B, B, mb);
@@ -957,7 +1015,7 @@ static void run_me(orc_replay *r, int sb) {
           P->full[(size_t)k * P->n + b] = fmv;
           P->fc[(size_t)k * P->n + b] = cost;
           c.subpel = 1;
-          c.satd = 1;
+          c.satd = r->s6;
           orc_diamond_search(&c, &fmv, 1, &smv, &cost);
           P->sub[(size_t)k * P->n + b] = smv;
           P->sc[(size_t)k * P->n + b] = cost;
@@ -1073,7 +1131,7 @@ static double level_cost(const orc_replay *r, double c0, int l, int x, int y) {
 static int split_at(const orc_replay *r, double c0, int l, int x, int y) {
   const int B = SB >> l;
   if (x + B > r->W || y + B > r->H) return 1;
-  if (l == 3) return 0;
+  if (l == 3 || !r->s6) return 0; /* speed 10: the minimum block is 64x64 */
   const int h = B / 2;
   double s = 0.0;
   s += level_cost(r, c0, l + 1, x, y);
@@ -1110,9 +1168,11 @@ static void partition_sb(orc_replay *r, int sb, double c0, oslot *S, uint16_t (*
   uint64_t mask = 0;
   /* clear this superblock's leaf flags */
   r->leaf0[sb] = 0;
+  int ex = 0, ey = 0;
+  (void)in_rect(r, sb, &ex, &ey); /* the caller's superblock is in the rectangle */
   for (int l = 1; l < 4; l++) {
     struct olevel *P = &r->pl[l];
-    const int k2 = 1 << l, bx0 = (sb % r->tw) * k2, by0 = (sb / r->tw) * k2;
+    const int k2 = 1 << l, bx0 = ex * k2, by0 = ey * k2;
     for (int j = 0; j < k2; j++) memset(P->leaf + (size_t)(by0 + j) * P->gw + bx0, 0, k2);
   }
   if (!split_at(r, c0, 0, X, Y)) {
@@ -1247,17 +1307,22 @@ static void run_rdo(orc_replay *r, int sb, uint64_t tail[3]) {
   w[WPR * R + 1] = (uint64_t)best_skip;
   w[WPR * R + 2] = cb;
   w[WPR * R + 3] = best_d;
-  if (!r->s6) {
-    /* F6: the winner into the frame (whole superblock; past the frame edge
-     * it lands in the padding, which F7 rewrites) */
+  int ex, ey;
+  const int lv_sb = in_rect(r, sb, &ex, &ey);
+  if (!lv_sb) {
+    /* F6: the winner into the frame (whole superblock) */
+    if (r->lvl) {
+      r->leaf0[sb] = 1;
+      r->words[r->wpart + sb] = 0;
+    }
     for (int y = 0; y < SB; y++) memcpy(at(&S->y, hbd, ppx, ppy + y), (uint8_t *)by_ + y * SB * px, SB * px);
     for (int y = 0; y < chei; y++) {
       memcpy(at(&S->u, hbd, cpx, cpy + y), (uint8_t *)bu_ + (size_t)y * cwid * px, cwid * px);
       memcpy(at(&S->v, hbd, cpx, cpy + y), (uint8_t *)bv_ + (size_t)y * cwid * px, cwid * px);
     }
   } else {
-    /* speed 6: every 32x32, 16x16 and 8x8 block of the superblock, the
-     * partition decision, the leaves into the frame */
+    /* every 32x32, 16x16 and 8x8 block of the superblock, the partition
+     * decision (speed 10: must_split only), the leaves into the frame */
     static _Thread_local uint16_t ry[4][SB * SB], ru[4][SB * SB], rv[4][SB * SB];
     memcpy(ry[0], by_, SB * SB * px);
     memcpy(ru[0], bu_, (size_t)cwid * chei * px);
@@ -1267,7 +1332,7 @@ static void run_rdo(orc_replay *r, int sb, uint64_t tail[3]) {
       const int k2 = 1 << l;
       for (int j = 0; j < k2; j++)
         for (int i = 0; i < k2; i++) {
-          const int b = (sy * k2 + j) * P->gw + sx * k2 + i;
+          const int b = (ey * k2 + j) * P->gw + ex * k2 + i;
           rdo_level_block(r, l, b, cur, ref, (uint8_t *)ry[l] + ((size_t)j * P->B * SB + i * P->B) * px,
                           (uint8_t *)ru[l] + ((size_t)j * P->bch * cwid + i * P->bc) * px,
                           (uint8_t *)rv[l] + ((size_t)j * P->bch * cwid + i * P->bc) * px);
@@ -1609,11 +1674,11 @@ int orc_replay_results(orc_replay *r, uint64_t *out, int cap) {
   uint64_t lc = 0;
   size_t per = 1024 + 2 * (size_t)r->ntx_c * 1024;
   for (int sb = 0; sb < r->nsb; sb++) {
-    if (r->s6 && !r->leaf0[sb]) continue;
+    if (r->lvl && !r->leaf0[sb]) continue;
     for (size_t i = 0; i < per; i++)
       lc += (uint64_t)(int64_t)r->lev[sb * per + i] * (uint64_t)(i % 1024 + 1);
   }
-  for (int l = 1; r->s6 && l < 4; l++) {
+  for (int l = 1; r->lvl && l < 4; l++) {
     const struct olevel *P = &r->pl[l];
     const size_t pl_ = (size_t)P->B * P->B, pc = (size_t)P->bc * P->bch, pb = pl_ + 2 * pc;
     for (int b = 0; b < P->n; b++) {

@@ -97,7 +97,9 @@ __host__ __device__ inline int cand_stack(const CandGeo &g, const rv_fs_result *
                                           int k, rv_mv &s0, rv_mv &s1) {
   const int sx = sb % g.tw, sy = sb / g.tw;
   const int fx = g.tx0 + sx, fy = g.ty0 + sy;
-  const bool up = fy % g.ths != 0, left = fx % g.tws != 0;
+  // neighbours inside the grid and the tile (a level grid over the frame-edge
+  // rectangle starts below / right of blocks it does not hold)
+  const bool up = sy > 0 && fy % g.ths != 0, left = sx > 0 && fx % g.tws != 0;
   const rv_mv zero{0, 0};
   const rv_mv a = up ? sub[k * g.nsb + sb - g.tw].best_mv : zero;
   const rv_mv l = left ? sub[k * g.nsb + sb - 1].best_mv : zero;
@@ -119,7 +121,9 @@ __host__ __device__ inline int comp_stack(const CandGeo &g, const rv_fs_result *
                                           rv_mv &e00, rv_mv &e01, rv_mv &e10, rv_mv &e11) {
   const int sx = sb % g.tw, sy = sb / g.tw;
   const int fx = g.tx0 + sx, fy = g.ty0 + sy;
-  const bool up = fy % g.ths != 0, left = fx % g.tws != 0;
+  // neighbours inside the grid and the tile (a level grid over the frame-edge
+  // rectangle starts below / right of blocks it does not hold)
+  const bool up = sy > 0 && fy % g.ths != 0, left = sx > 0 && fx % g.tws != 0;
   const rv_mv zero{0, 0};
   const rv_mv a0 = up ? sub[sb - g.tw].best_mv : zero, a1 = up ? sub[g.nsb + sb - g.tw].best_mv : zero;
   const rv_mv l0 = left ? sub[sb - 1].best_mv : zero, l1 = left ? sub[g.nsb + sb - 1].best_mv : zero;

@@ -389,12 +389,15 @@ constexpr int kLevels = 4;  // 64x64, 32x32, 16x16, 8x8
 // a 16x16 / 8x8 block the sub-pel winner of its 32x32 (rdo_mode_decision
 // stores b_me into pmvs for 32x32 and 64x64 blocks, src/rdo.rs:866-876).
 __global__ void seed_level_kernel(rv_ds_job *jobs, int n, int gw, int R,
-                                  const rv_fs_result *parent, int pn, int pgw, int f) {
+                                  const rv_fs_result *parent, int pn, int pgw, int f, int ex0,
+                                  int ey0, int tw) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n * R) return;
   const int k = i / n, b = i - k * n, bx = b % gw, by = b / gw;
   if (pgw == 0) {  // 32x32: the half-res search of its quadrant (pmvs[1..4], MV * 2)
-    const int sb = (by >> 1) * (gw >> 1) + (bx >> 1), q = (by & 1) * 2 + (bx & 1);
+    // the group superblock of the level grid's block (the grid starts at
+    // group superblock (ex0, ey0))
+    const int sb = (ey0 + (by >> 1)) * tw + ex0 + (bx >> 1), q = (by & 1) * 2 + (bx & 1);
     const rv_mv m = parent[((int64_t)k * pn + sb) * 4 + q].best_mv;
     jobs[i].pred[1] = qfull(rv_mv{(int16_t)(m.row * 2), (int16_t)(m.col * 2)});
     return;
@@ -438,6 +441,9 @@ __global__ __launch_bounds__(64) void score_level(CandGeo cg, double lambda, dou
 struct PartArgs {
   const RdoWinner *win[kLevels];
   int gw[kLevels];          // level grid width (blocks)
+  int x0[kLevels], y0[kLevels];  // level grid origin (frame pixels)
+  int ex0, ey0, ew, eh;     // the group superblocks the level grids cover
+  int forced;               // speed 10: must_split only (the minimum block is 64x64)
   int32_t *leaf[kLevels];   // the committed blocks of each level
   int32_t *leaf_count;      // [kLevels], zeroed by score_candidates
   uint64_t *words;          // one partition mask per superblock
@@ -454,17 +460,20 @@ struct PartArgs {
 __global__ __launch_bounds__(64) void partition_kernel(Geo g, PartArgs p) {
   const int sb = blockIdx.x * 64 + threadIdx.x;
   const bool live = sb < g.nsb;
-  const int gx0 = g.tx0 * kSb, gy0 = g.ty0 * kSb;
+  const int gx0 = g.tx0 * kSb, gy0 = g.ty0 * kSb;  // the group (level 0 grid)
   const int X = gx0 + (live ? sb % g.tw : 0) * kSb, Y = gy0 + (live ? sb / g.tw : 0) * kSb;
+  const int sx = live ? sb % g.tw - p.ex0 : -1, sy = live ? sb / g.tw - p.ey0 : -1;
+  const bool in_rect = sx >= 0 && sy >= 0 && sx < p.ew && sy < p.eh;
   auto idx = [&](int l, int x, int y) {
     const int B = kSb >> l;
-    return ((y - gy0) / B) * p.gw[l] + (x - gx0) / B;
+    return ((y - p.y0[l]) / B) * p.gw[l] + (x - p.x0[l]) / B;
   };
   auto cost = [&](int l, int x, int y) { return p.win[l][idx(l, x, y)].cost; };
   auto split = [&](int l, int x, int y) -> bool {
     const int B = kSb >> l;
+    if (!in_rect) return false;  // no level grid here: the superblock is a leaf
     if (x + B > g.W || y + B > g.H) return true;  // must_split
-    if (l == kLevels - 1) return false;
+    if (l == kLevels - 1 || p.forced) return false;
     const int h = B / 2;
     double s = 0.0;
     s += cost(l + 1, x, y);
@@ -612,6 +621,11 @@ struct rv_replay {
     size_t woff = 0;  // result words offset
   } pl[kLevels];
   bool s6 = false;
+  // the 32x32 .. 8x8 level grids: speed 6 over the group, speed 10 over the
+  // bounding rectangle (group superblocks ex0, ey0 + ew x eh) of the
+  // superblocks past the frame's right / bottom edge (must_split)
+  bool lvl = false;
+  int ex0 = 0, ey0 = 0, ew = 0, eh = 0;
   bool deblock = false;           // RV_REPLAY_DEBLOCK
   uint8_t *mi_lg = nullptr, *mi_skip = nullptr;  // the deblocking block map
   int mi_stride = 0, mi_cols = 0, mi_rows = 0;
@@ -890,7 +904,7 @@ int build_static_jobs(rv_replay *r) {
     // speed 6: motion_estimation of every 32x32 / 16x16 / 8x8 block at its
     // own position (no adjust_bo, src/me.rs:193-278): zero + the seeded
     // coarse predictor, then the sub-pel search from the full-pel winner
-    for (int l = 1; r->s6 && l < kLevels; l++) {
+    for (int l = 1; r->lvl && l < kLevels; l++) {
       rv_replay::PLevel &P = r->pl[l];
       std::vector<rv_ds_job> f6((size_t)P.n * g.R), s6((size_t)P.n * g.R);
       for (int k = 0; k < g.R; k++)
@@ -1322,6 +1336,31 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
       return nullptr;
     }
     r->s6 = true;
+    r->lvl = true;
+    r->ew = g.tw;
+    r->eh = g.th;
+  } else if (g.xdec == g.ydec) {
+    // speed 10: encode_partition_topdown's must_split (src/encoder.rs:2407-
+    // 2445) at the frame edges, over the bounding rectangle of the group's
+    // superblocks past the right / bottom edge
+    int x0 = g.tw, y0 = g.th, x1 = -1, y1 = -1;
+    for (int sb = 0; sb < g.nsb; sb++) {
+      const int x = sb % g.tw, y = sb / g.tw;
+      if ((g.tx0 + x + 1) * kSb <= g.W && (g.ty0 + y + 1) * kSb <= g.H) continue;
+      x0 = x < x0 ? x : x0;
+      y0 = y < y0 ? y : y0;
+      x1 = x > x1 ? x : x1;
+      y1 = y > y1 ? y : y1;
+    }
+    if (x1 >= 0) {
+      r->lvl = true;
+      r->ex0 = x0;
+      r->ey0 = y0;
+      r->ew = x1 - x0 + 1;
+      r->eh = y1 - y0 + 1;
+    }
+  }
+  if (r->lvl) {
     rv_replay::PLevel &P0 = r->pl[0];
     P0.B = kSb;
     P0.n = g.nsb;
@@ -1332,14 +1371,15 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
       rv_replay::PLevel &P = r->pl[l];
       const int k = 1 << l;
       P.B = kSb >> l;
-      P.gw = g.tw * k;
-      P.gh = g.th * k;
+      P.gw = r->ew * k;
+      P.gh = r->eh * k;
       P.n = P.gw * P.gh;
       P.bc = P.B >> g.xdec;
       P.bch = P.B >> g.ydec;
       P.txl = 4 - l;                                              // TX_32X32 .. TX_8X8
       P.txc = P.bc == 32 ? 3 : P.bc == 16 ? 2 : P.bc == 8 ? 1 : 0;  // .. TX_4X4
-      P.cg = CandGeo{P.n, P.gw, P.gh, g.tx0 * k, g.ty0 * k, g.tws * k, g.ths * k, g.R, g.M, 0};
+      P.cg = CandGeo{P.n, P.gw, P.gh, (g.tx0 + r->ex0) * k, (g.ty0 + r->ey0) * k, g.tws * k,
+                     g.ths * k, g.R, g.M, 0};
       const int64_t nc = (int64_t)P.n * g.C;
       P.full = (rv_fs_result *)dalloc(r, (size_t)P.n * g.R * sizeof(rv_fs_result));
       P.sub = (rv_fs_result *)dalloc(r, (size_t)P.n * g.R * sizeof(rv_fs_result));
@@ -1492,7 +1532,7 @@ int rv_replay_set_level_params(rv_replay *r, int level, const rv_replay_level_pa
   RV_R(rv_quant_ctx(p->base_q_idx, 64 * 64, 1, bd, p->dc_delta_q[0], p->ac_delta_q[0], &L.qil));
   RV_R(rv_quant_ctx(p->base_q_idx, 32 * 32, 1, bd, p->dc_delta_q[1], p->ac_delta_q[1], &L.qiu));
   RV_R(rv_quant_ctx(p->base_q_idx, 32 * 32, 1, bd, p->dc_delta_q[2], p->ac_delta_q[2], &L.qiv));
-  for (int l = 1; r->s6 && l < kLevels; l++) {  // speed 6: the smaller transforms
+  for (int l = 1; r->lvl && l < kLevels; l++) {  // the levels' smaller transforms
     const rv_replay::PLevel &P = r->pl[l];
     RV_R(rv_quant_ctx(p->base_q_idx, P.B * P.B, 0, bd, p->dc_delta_q[0], p->ac_delta_q[0], &L.qs[l][0]));
     for (int c = 1; c < 3; c++)
@@ -1785,29 +1825,31 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   RV_EV(5);
   RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, r->s6 ? 1 : 0,
                                0, g.bd, r->sub, ev_sub, nullptr, st));
-  // speed 6: the same search for every 32x32, 16x16 and 8x8 block (SATD
-  // sub-pel, use_satd_subpel, src/api/config.rs:429-431)
-  for (int l = 1; r->s6 && l < kLevels; l++) {
+  // the levels: the same search for every 32x32, 16x16 and 8x8 block of the
+  // level grids (sub-pel by SATD at speed 6, use_satd_subpel,
+  // src/api/config.rs:429-431; SAD at speed 10)
+  for (int l = 1; r->lvl && l < kLevels; l++) {
     rv_replay::PLevel &P = r->pl[l];
     // 32x32: the half-res quadrant searches; 16x16 / 8x8: the 32x32's sub-pel
     if (l == 1)
-      seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, st>>>(P.jobs_full[lv], P.n, P.gw, g.R,
-                                                                  r->half, g.nsb, 0, 0);
+      seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, st>>>(
+          P.jobs_full[lv], P.n, P.gw, g.R, r->half, g.nsb, 0, 0, r->ex0, r->ey0, g.tw);
     else
       seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, st>>>(
-          P.jobs_full[lv], P.n, P.gw, g.R, r->pl[1].sub, r->pl[1].n, r->pl[1].gw, 1 << (l - 1));
+          P.jobs_full[lv], P.n, P.gw, g.R, r->pl[1].sub, r->pl[1].n, r->pl[1].gw, 1 << (l - 1), 0, 0,
+          0);
     ChainNext to_s{kChainFullToSub, P.jobs_sub[lv]};
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, P.jobs_full[lv], P.n, P.B, P.B, 0, 0, 0,
                                  g.bd, P.full, nullptr, &to_s, st));
-    RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, P.jobs_sub[lv], P.n, P.B, P.B, 1, 1, 0,
-                                 g.bd, P.sub, nullptr, nullptr, st));
+    RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, P.jobs_sub[lv], P.n, P.B, P.B, 1,
+                                 r->s6 ? 1 : 0, 0, g.bd, P.sub, nullptr, nullptr, st));
   }
   // the valid candidates (a few microseconds; bracketed with F3 sub-pel;
   // the count was zeroed by the previous frame's argmin or at creation)
   const int nsingle = g.nsb * g.R * g.M;
   cand_list_kernel<<<(nsingle + 255) / 256, 256, 0, st>>>(cg, r->sub, nsingle, r->cand_list,
                                                           r->cand_count);
-  for (int l = 1; r->s6 && l < kLevels; l++) {
+  for (int l = 1; r->lvl && l < kLevels; l++) {
     rv_replay::PLevel &P = r->pl[l];
     const int ns = P.n * g.R * g.M;
     cand_list_kernel<<<(ns + 255) / 256, 256, 0, st>>>(P.cg, P.sub, ns, P.cand_list, P.cand_count);
@@ -1815,7 +1857,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   if (cg.comp) {  // the compound lists (after the single ones in the same arrays)
     comp_list_kernel<<<(g.nsb * cg.comp + 255) / 256, 256, 0, st>>>(
         cg, r->sub, nsingle, r->cand_list + nsingle, r->cand_count + 1);
-    for (int l = 1; r->s6 && l < kLevels; l++) {
+    for (int l = 1; r->lvl && l < kLevels; l++) {
       rv_replay::PLevel &P = r->pl[l];
       CandGeo cgl = P.cg;
       cgl.comp = cg.comp;
@@ -1878,7 +1920,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // speed 6: the candidates of every 32x32 .. 8x8 block, luma (cdef
   // distortion) and chroma launches per level
   RdoArgs ll[kLevels], lc6[kLevels];
-  for (int l = 1; r->s6 && l < kLevels; l++) {
+  for (int l = 1; r->lvl && l < kLevels; l++) {
     rv_replay::PLevel &P = r->pl[l];
     CandGeo cgl = P.cg;
     cgl.comp = cg.comp;
@@ -1932,7 +1974,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     cc.n_tx = g.nsb * cg.comp * ntx_c;
     RV_EV(7);
     RV_R(rv_rdo_candidates(lc, cc, g.hbd, st, true));
-    for (int l = 1; r->s6 && l < kLevels; l++) {
+    for (int l = 1; r->lvl && l < kLevels; l++) {
       const rv_replay::PLevel &P = r->pl[l];
       RdoArgs a = ll[l], c = lc6[l];
       a.list = c.list = P.cand_list + P.n * g.R * g.M;
@@ -1956,7 +1998,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                                      r->cand_count, r->tail + 2,
                                                      r->cand_evals + 2 * slot * kLevels,
                                                      r->leaf_count);
-  if (r->s6) {
+  if (r->lvl) {
     PartArgs pa;
     memset(&pa, 0, sizeof(pa));
     for (int l = 0; l < kLevels; l++) {
@@ -1971,8 +2013,15 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       }
       pa.win[l] = l ? P.win : r->win;
       pa.gw[l] = P.gw;
+      pa.x0[l] = (g.tx0 + (l ? r->ex0 : 0)) * kSb;
+      pa.y0[l] = (g.ty0 + (l ? r->ey0 : 0)) * kSb;
       pa.leaf[l] = P.leaf;
     }
+    pa.ex0 = r->ex0;
+    pa.ey0 = r->ey0;
+    pa.ew = r->ew;
+    pa.eh = r->eh;
+    pa.forced = !r->s6;
     pa.leaf_count = r->leaf_count;
     pa.words = r->words + r->wpart;
     partition_kernel<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, pa);
@@ -1980,13 +2029,13 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   RV_EV(9);
   // F6 commit the winners into the frame
   la.commit = ca.commit = 1;
-  la.list = ca.list = r->s6 ? r->pl[0].leaf : nullptr;  // speed 6: the unsplit superblocks
-  la.count = ca.count = r->s6 ? r->leaf_count : nullptr;
+  la.list = ca.list = r->lvl ? r->pl[0].leaf : nullptr;  // with levels: the unsplit superblocks
+  la.count = ca.count = r->lvl ? r->leaf_count : nullptr;
   la.n_tx = g.nsb;
   ca.n_tx = g.nsb * ntx_c;
   la.ntx_per_cand = 1;
   RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
-  for (int l = 1; r->s6 && l < kLevels; l++) {  // and the leaves of every level
+  for (int l = 1; r->lvl && l < kLevels; l++) {  // and the leaves of every level
     const rv_replay::PLevel &P = r->pl[l];
     RdoArgs a = ll[l], c = lc6[l];
     a.commit = c.commit = 1;
@@ -2015,7 +2064,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // block map of the committed blocks, then (once every group's pixels and
   // map are in) Y, U, V in place; the reconstruction becomes a reference
   if (r->deblock) {
-    if (!r->s6) {
+    if (!r->lvl) {
       block_map_kernel<<<(g.nsb * 16 + 255) / 256, 256, 0, st>>>(
           nullptr, nullptr, g.nsb, g.tw, g.tx0, g.ty0, 0, r->win, r->mi_lg, r->mi_skip,
           r->mi_stride, r->mi_cols, r->mi_rows);
@@ -2069,7 +2118,7 @@ int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap) {
   const int64_t nl = (int64_t)g.nsb * 1024, nc = (int64_t)g.nsb * r->ntx_c * 1024;
   RV_H(hipMemsetAsync(r->tail, 0, 2 * 8, st));
   RV_H(hipMemsetAsync(r->tail + 3, 0, 2 * 8, st));
-  if (!r->s6) {
+  if (!r->lvl) {
     coeff_checksum<<<1024, 256, 0, st>>>(r->l_lev, nl, 1024, r->tail);
     coeff_checksum<<<1024, 256, 0, st>>>(r->c_lev, 2 * nc, 1024, r->tail);
   } else {  // the committed blocks (leaves) of every level

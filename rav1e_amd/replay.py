@@ -199,33 +199,58 @@ def sb_words_per(n_refs):
     return WORDS_PER_REF * n_refs + 4
 
 
+def level_rect(width, height, tile_w_sb=0, tile_h_sb=0, tile_x0=0, tile_y0=0, speed=10, xdec=1,
+               ydec=1):
+    """The group superblocks (x0, y0, w, h) the 32x32 .. 8x8 levels cover:
+    speed 6 every one; speed 10 (4:2:0 / 4:4:4) the bounding rectangle of
+    those past the frame's right or bottom edge (encode_partition_topdown's
+    must_split, src/encoder.rs:2407-2445); None without levels."""
+    sbc, sbr = (width + 63) // 64, (height + 63) // 64
+    tw = tile_w_sb or (sbc - tile_x0)
+    th = tile_h_sb or (sbr - tile_y0)
+    if speed == 6:
+        return (0, 0, tw, th)
+    if xdec != ydec:
+        return None
+    edge = [(x, y) for y in range(th) for x in range(tw)
+            if (tile_x0 + x + 1) * 64 > width or (tile_y0 + y + 1) * 64 > height]
+    if not edge:
+        return None
+    xs, ys = [e[0] for e in edge], [e[1] for e in edge]
+    return (min(xs), min(ys), max(xs) - min(xs) + 1, max(ys) - min(ys) + 1)
+
+
 def result_words(width, height, n_refs, tile_w_sb=0, tile_h_sb=0, tile_x0=0, tile_y0=0,
-                 speed=10):
+                 speed=10, xdec=1, ydec=1):
     """Result words of a group (rv_replay_results): per superblock
-    WORDS_PER_REF * R + 4;
-    speed 6 adds 4 * R + 4 per 32x32, 16x16 and 8x8 block and one partition
-    mask per superblock; then 5 tail words."""
+    WORDS_PER_REF * R + 4; with levels (level_rect) 4 * R + 4 per 32x32,
+    16x16 and 8x8 block of the rectangle and one partition mask per
+    superblock; then 5 tail words."""
     sbc, sbr = (width + 63) // 64, (height + 63) // 64
     tw = tile_w_sb or (sbc - tile_x0)
     th = tile_h_sb or (sbr - tile_y0)
     n = tw * th * sb_words_per(n_refs)
-    if speed == 6:
-        n += sum(tw * th * 4 ** l * (4 * n_refs + 4) for l in (1, 2, 3)) + tw * th
+    rect = level_rect(width, height, tile_w_sb, tile_h_sb, tile_x0, tile_y0, speed, xdec, ydec)
+    if rect:
+        n += sum(rect[2] * rect[3] * 4 ** l * (4 * n_refs + 4) for l in (1, 2, 3)) + tw * th
     return n + 5
 
 
-def level_words(width, height, n_refs, words, tile_w_sb=0, tile_h_sb=0, tile_x0=0, tile_y0=0):
-    """Split speed-6 result words: (superblock words [nsb, 46R+4], [level 1..3
-    words [n_l, 4R+4]], partition masks [nsb], tail [5])."""
+def level_words(width, height, n_refs, words, tile_w_sb=0, tile_h_sb=0, tile_x0=0, tile_y0=0,
+                speed=6, xdec=1, ydec=1):
+    """Split result words with levels: (superblock words [nsb, 46R+4], [level
+    1..3 words [n_l, 4R+4]] over level_rect, partition masks [nsb], tail
+    [5])."""
     sbc, sbr = (width + 63) // 64, (height + 63) // 64
     tw = tile_w_sb or (sbc - tile_x0)
     th = tile_h_sb or (sbr - tile_y0)
     nsb = tw * th
+    rect = level_rect(width, height, tile_w_sb, tile_h_sb, tile_x0, tile_y0, speed, xdec, ydec)
     o = nsb * sb_words_per(n_refs)
     sbw = words[:o].reshape(nsb, sb_words_per(n_refs))
     lv = []
     for l in (1, 2, 3):
-        n = nsb * 4 ** l
+        n = rect[2] * rect[3] * 4 ** l
         lv.append(words[o:o + n * (4 * n_refs + 4)].reshape(n, 4 * n_refs + 4))
         o += n * (4 * n_refs + 4)
     return sbw, lv, words[o:o + nsb], words[o + nsb:]
@@ -254,7 +279,7 @@ class HipReplay:
             raise RuntimeError(f"rv_replay_create: {lib().rv_last_error().decode()}")
         self.speed = 6 if flags & RV_REPLAY_SPEED6 else 10
         self.n_words = result_words(width, height, n_refs, cfg.tile_w, cfg.tile_h,
-                                    cfg.tile_x0, cfg.tile_y0, self.speed)
+                                    cfg.tile_x0, cfg.tile_y0, self.speed, xdec, ydec)
         self.levels = _rate.level_params(quantizer, bit_depth)
         for lv, d in enumerate(self.levels):
             p = RvReplayLevelParams.from_dict(d)

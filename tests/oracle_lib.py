@@ -543,7 +543,7 @@ class CpuReplay:
         L.orc_replay_set_intra.argtypes = [C.c_void_p, C.c_int]
         assert L.orc_replay_set_intra(self.h, 1 if self.intra else 0) == 0
         L.orc_replay_intra_stats.argtypes = [C.c_void_p, C.c_void_p]
-        self.n_words = result_words(width, height, n_refs, tw, th, tx0, ty0, speed)
+        self.n_words = result_words(width, height, n_refs, tw, th, tx0, ty0, speed, xdec, ydec)
         self.geom = (width, height, xdec, ydec, bit_depth)
         self.levels = RT.level_params(quantizer, bit_depth)
         L.orc_replay_set_cdef.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]

@@ -194,6 +194,34 @@ def test_cpu_replay_deblock_changes_the_reference():
     assert (recs[0] != recs[1]).any()
 
 
+def test_cpu_replay_speed10_edge_superblocks_must_split():
+    """Speed 10 (minimum block 64x64): a superblock past the bottom edge is
+    split as encode_partition_topdown's must_split does (src/encoder.rs:
+    2407-2445) down to the largest blocks inside the frame; 232 = 3 x 64 +
+    40: the upper 32x32s stay whole, the lower ones split to 16x16, those to
+    8x8 (the rows 32..39 inside).  The other superblocks are single 64x64
+    blocks; the level words cover only the bottom superblock row."""
+    w, h = 256, 232
+    fr = _frames(w, h, 1, 1, 8, 8)
+    r = O.CpuReplay(w, h, 1, 1, 8, 2, n_inputs=8, threads=2)
+    for i, f in enumerate(fr):
+        r.set_input(i, f)
+    r.frame()
+    r.frame()
+    wd = r.results()
+    assert RP.level_rect(w, h) == (0, 3, 4, 1)
+    sbw, lv, part, tail = RP.level_words(w, h, 2, wd, speed=10)
+    want = 1 | (2 << 2) | (2 << 3) | sum(1 << (5 + 2 * 4 + i) for i in range(4))
+    np.testing.assert_array_equal(part, [0] * 12 + [want] * 4)
+    R = 2
+    # the leaves' rd costs: the upper 32x32s, the 8x8s of rows 32..39
+    l1 = lv[0].reshape(2, 8, 4 * R + 4)
+    assert (l1[0, :, 4 * R + 2] != 0).all()
+    l3 = lv[2].reshape(8, 32, 4 * R + 4)
+    assert (l3[4, :, 4 * R + 2] != 0).all()
+    r.close()
+
+
 def test_cpu_replay_speed6_searches_the_deblocking_levels():
     """Below speed 8 deblock_filter_optimize searches the levels
     (sse_optimize, src/deblock.rs:1418-1475): per direction and plane, from
@@ -416,6 +444,10 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
     (384, 192, 1, 1, 8, 2, {"tile_cols": 2}, 0),
     (384, 256, 0, 0, 8, 2, {"tiles": 4}, 0),
     (256, 192, 1, 1, 8, 2, None, RP.RV_REPLAY_EXHAUSTIVE_FS),
+    # speed 10 must_split at the frame edges (bottom; right + bottom; 4:4:4)
+    (256, 232, 1, 1, 8, 2, None, 0),
+    (200, 136, 1, 1, 10, 2, None, 0),
+    (320, 168, 0, 0, 8, 2, {"tile_cols": 2}, 0),
     (256, 200, 1, 1, 8, 2, None, RP.RV_REPLAY_SPEED6),      # speed 6: partition RDO
     (256, 136, 1, 1, 10, 2, None, RP.RV_REPLAY_SPEED6),
     (192, 128, 0, 0, 8, 2, {"tile_cols": 2}, RP.RV_REPLAY_SPEED6),
