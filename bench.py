@@ -147,6 +147,7 @@ def timed_run(engine, group, steps, warmup, sync=None):
     (max-over-ranks seconds, result words of the last frame).  `engine` is a
     HipReplay / TileParallel (the product) or, in the multi-rank CPU tests,
     the oracle's CpuReplay behind a TileParallel."""
+    drain = getattr(engine, "drain", None)  # PairedReplay: frames issued from a second thread
     for _ in range(warmup):
         engine.frame()
     if warmup:
@@ -157,6 +158,8 @@ def timed_run(engine, group, steps, warmup, sync=None):
     t0 = time.perf_counter()
     for _ in range(steps):
         engine.frame()
+    if drain:
+        drain()
     if sync:
         sync()  # device-wide: every frame on every stream has finished
     t1 = time.perf_counter()
@@ -330,6 +333,9 @@ def main():
     ap.add_argument("--emulate-ranks", type=int, default=8,
                     help="N > 1 (single-GPU runs): also code the N-rank tile-group split as N "
                          "replays on this GPU and report the projected N-rank step (0: off)")
+    ap.add_argument("--serial-levels", action="store_true",
+                    help="one instance codes every frame (default on one GPU: the level-2 "
+                         "frames run on a twin instance concurrently with levels 0 / 1)")
     ap.add_argument("--exhaustive-fs", action="store_true",
                     help="F1 coarse search without successive elimination (same results)")
     args = ap.parse_args()
@@ -358,10 +364,13 @@ def main():
     hip.synth_inputs(0)  # the stream's frames, resident in HBM before the timing
     comm = RP.RcclComm(group) if world > 1 else None
     eng = TileParallel(hip, rects, rank, group, comm)
+    paired = world == 1 and not args.serial_levels
+    if paired:
+        eng = RP.PairedReplay(hip)
     sea = bd <= 10 and not args.exhaustive_fs  # the replay's F1 path
     # HIP events on a sample of frames: every TIMING_STRIDE-th GOP
     gop = len(RP.GOP_SCALES)
-    hip.set_timing(TIMING_STRIDE, gop)
+    (eng if paired else hip).set_timing(TIMING_STRIDE, gop)
     dt, words = timed_run(eng, group, args.steps, args.warmup,
                           sync=lambda: R._check(R.lib().rv_device_sync(), "rv_device_sync"))
 
@@ -369,8 +378,15 @@ def main():
     nonkey = range(args.warmup - 1, args.warmup - 1 + args.steps)
     k = min(sum(1 for f in nonkey if (f // gop) % TIMING_STRIDE == 0), 64)
     k = max(k, 1)
-    ms = hip.stage_ms_sum(k) / k  # per frame
-    cnt = [int(v) for v in hip.counters()]
+    if paired:  # the instrumented frames of each instance in the timed region
+        inst = [f for f in nonkey if (f // gop) % TIMING_STRIDE == 0]
+        kp = min(sum(1 for f in inst if f % 4 < 2), 64)
+        kt = min(sum(1 for f in inst if f % 4 >= 2), 64)
+        ms = eng.stage_ms_sum(kp, kt) / max(1, kp + kt)
+        cnt = [int(v) for v in eng.counters()]
+    else:
+        ms = hip.stage_ms_sum(k) / k  # per frame
+        cnt = [int(v) for v in hip.counters()]
     ev_full, ev_sub, ev_frames, n_single, n_comp = cnt[:5]
     ev_frames = max(1, ev_frames)
     gx0, gy0, gw, gh = rects[rank]
@@ -471,6 +487,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the CPU codes the same frames: the GPU's inputs, downloaded
         inputs = [hip.get_input(i) for i in range(min(22, n_inputs))]
+        if paired:
+            eng.close()
         hip.close()  # the parity pass below builds a fresh GPU replay
         cpu, parity = cpu_baseline_and_parity(args, inputs, W, H, xdec, ydec, bd, nref,
                                               tiling, n_inputs, speed, flags)
@@ -491,6 +509,8 @@ def main():
                        "deblock": bool(args.deblock or args.cdef), "cdef": bool(args.cdef),
                        "tiles": [tiling["cols"], tiling["rows"]],
                        "parallelism": f"tile-groups{world}",
+                       "frame_concurrency": ("levels 0/1 + level-2 frames on a twin instance "
+                                             "(2 streams)" if paired else "serial"),
                        "candidates_per_sb": f"{4 * nref} inter modes x (skip, non-skip)",
                        **({"partition": "64x64 .. 8x8 top-down NONE vs SPLIT, every level "
                                         "searched and scored"} if speed == 6 else {})},
@@ -516,6 +536,8 @@ def main():
             **({"emulated_ranks": emu} if emu else {}),
         }
         print(json.dumps(line), flush=True)
+    if paired:
+        eng.close()
     hip.close()
     if comm:
         comm.close()

@@ -91,6 +91,9 @@ void *rv_event_create(void);
 int rv_event_destroy(void *ev);
 int rv_event_record(void *ev, void *stream);
 int rv_event_sync(void *ev);
+/* work submitted to `stream` after this call waits for `ev`'s last record
+ * (hipStreamWaitEvent) */
+int rv_stream_wait_event(void *stream, void *ev);
 /* milliseconds between two recorded events (hipEventElapsedTime) */
 float rv_event_elapsed_ms(void *start, void *stop);
 
@@ -559,6 +562,23 @@ typedef struct rv_replay rv_replay;
  * failure (rv_last_error). */
 rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream);
 void rv_replay_destroy(rv_replay *r);
+/* A second instance of `primary`'s tile group that shares its DPB and input
+ * frames (device memory owned by `primary`, which must outlive it) and has
+ * its own per-frame state, stream (`stream`, NULL = its own) and timing: it
+ * codes the pyramid's level-2 frames (display 4g+1, 4g+3), which no later
+ * frame references, concurrently with `primary`'s levels 0 / 1.  Level
+ * parameters, importances and the loop-filter settings are copied from
+ * `primary` at creation.  The caller orders the two streams
+ * (rv_replay_stream, rv_stream_wait_event): a level-2 frame of group g
+ * after `primary`'s level-1 frame of group g, and `primary`'s level-0 frame
+ * of group g + 2 (whose DPB slot is display 4g's) after both level-2 frames
+ * of group g. */
+rv_replay *rv_replay_create_twin(rv_replay *primary, void *stream);
+/* The next rv_replay_frame codes coding-order frame n (>= 1; n = 0 is the key
+ * frame): display 4g + {4, 2, 1, 3}[j] for n = 1 + 4g + j. */
+int rv_replay_seek(rv_replay *r, long n);
+/* The instance's replay stream (a hipStream_t). */
+void *rv_replay_stream(rv_replay *r);
 /* Set the parameters of pyramid level 0..2 (all three before the first
  * inter frame). */
 int rv_replay_set_level_params(rv_replay *r, int level, const rv_replay_level_params *p);

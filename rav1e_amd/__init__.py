@@ -235,6 +235,7 @@ def _declare(L):
         "rv_event_destroy": (i32, [vp]),
         "rv_event_record": (i32, [vp, vp]),
         "rv_event_sync": (i32, [vp]),
+        "rv_stream_wait_event": (i32, [vp, vp]),
         "rv_event_elapsed_ms": (C.c_float, [vp, vp]),
         "rv_plane_geometry": (sz, [P, i32, i32, i32, i32, i32, i32, i32]),
         "rv_plane_pad": (i32, [P, vp]),
@@ -269,6 +270,9 @@ def _declare(L):
         "rv_full_search_sea_batch": (i32, [P, P, vp, vp, i32, i32, vp, vp]),
         "rv_plane_box_sums": (i32, [P, vp, vp]),
         "rv_replay_create": (vp, [C.POINTER(RvReplayCfg), vp]),
+        "rv_replay_create_twin": (vp, [vp, vp]),
+        "rv_replay_seek": (i32, [vp, C.c_long]),
+        "rv_replay_stream": (vp, [vp]),
         "rv_replay_destroy": (None, [vp]),
         "rv_q_lookup": (i32, [i32, i32, i32]),
         "rv_replay_synth_inputs": (i32, [vp, i32]),

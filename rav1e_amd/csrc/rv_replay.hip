@@ -220,28 +220,43 @@ __global__ __launch_bounds__(64) void score_candidates(
     if (leaf_count)  // speed 6: the partition decision appends next
       for (int l = 0; l < 4; l++) leaf_count[l] = 0;
   }
-  if (sb >= g.nsb) return;
-  const RdoWinner w = block_argmin(cg, lambda, ds_u, ds_v, sub, lout, uout, vout, ntx_c, sb);
-  win[sb] = w;
-  uint64_t *wd = words + (int64_t)sb * (kWordsPerRef * g.R + 4);
-  auto put = [&](int i, const rv_fs_result &v) {
-    wd[2 * i] = pack_mv(v.best_mv);
-    wd[2 * i + 1] = v.cost;
-  };
-  for (int r = 0; r < g.R; r++, wd += kWordsPerRef) {
-    const int64_t o = (int64_t)r * g.nsb + sb;
-    put(0, coarse[o]);
-    for (int q = 0; q < 4; q++) put(1 + q, half[o * 4 + q]);
-    put(5, full[o]);
-    put(6, sub[o]);
-    for (int q = 0; q < 16; q++) put(7 + q, look[o * 16 + q]);
+  __shared__ RdoWinner ws[64];
+  if (sb < g.nsb) {
+    const RdoWinner w = block_argmin(cg, lambda, ds_u, ds_v, sub, lout, uout, vout, ntx_c, sb);
+    win[sb] = w;
+    ws[threadIdx.x] = w;
   }
-  uint64_t cb;
-  __builtin_memcpy(&cb, &w.cost, 8);
-  wd[0] = (uint64_t)w.c;
-  wd[1] = (uint64_t)w.skip;
-  wd[2] = cb;
-  wd[3] = w.dist;
+  __syncthreads();
+  // the result words of the workgroup's superblocks (one contiguous run):
+  // lane i stores word i, i + 64, ... so every store coalesces
+  const int sb0 = blockIdx.x * 64, nb = g.nsb - sb0 < 64 ? g.nsb - sb0 : 64;
+  const int per = kWordsPerRef * g.R + 4;
+  uint64_t *base = words + (int64_t)sb0 * per;
+  for (int i = threadIdx.x; i < nb * per; i += 64) {
+    const int s = i / per, wi = i - s * per, b = sb0 + s;
+    uint64_t v;
+    if (wi < kWordsPerRef * g.R) {
+      const int r = wi / kWordsPerRef, k = wi - r * kWordsPerRef, e = k >> 1;
+      const int64_t o = (int64_t)r * g.nsb + b;
+      // [coarse, 4 half-res quadrants, full-pel, sub-pel, 16 lookahead]
+      const rv_fs_result &f = e == 0 ? coarse[o] : e < 5 ? half[o * 4 + e - 1] : e == 5 ? full[o]
+                              : e == 6 ? sub[o] : look[o * 16 + e - 7];
+      v = (k & 1) ? f.cost : pack_mv(f.best_mv);
+    } else {
+      const RdoWinner &w = ws[s];
+      const int j = wi - kWordsPerRef * g.R;
+      if (j == 0) {
+        v = (uint64_t)w.c;
+      } else if (j == 1) {
+        v = (uint64_t)w.skip;
+      } else if (j == 2) {
+        __builtin_memcpy(&v, &w.cost, 8);
+      } else {
+        v = w.dist;
+      }
+    }
+    base[i] = v;
+  }
 }
 
 // The searches' predictor lists (get_subset_predictors, src/me.rs:82-96:
@@ -1243,7 +1258,9 @@ void rv_replay_destroy(rv_replay *r) {
   delete r;
 }
 
-rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
+// share: a primary instance whose DPB and inputs this one borrows
+// (rv_replay_create_twin)
+static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_replay *share) {
   if (!cfg || cfg->width <= 0 || cfg->height <= 0 || (cfg->width & 7) || (cfg->height & 7) ||
       (cfg->bit_depth != 8 && cfg->bit_depth != 10 && cfg->bit_depth != 12) || cfg->xdec < 0 ||
       cfg->xdec > 1 || cfg->ydec < 0 || cfg->ydec > 1 || cfg->n_refs < 1 || cfg->n_refs > 2 ||
@@ -1305,10 +1322,15 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
     }
   }
   bool ok = true;
-  r->slots.resize(kSlots);
-  for (auto &s : r->slots) ok = ok && alloc_slot(r, s);
-  r->inputs.resize(cfg->n_inputs);
-  for (auto &in : r->inputs) ok = ok && alloc_input(r, in);
+  if (share) {
+    r->slots = share->slots;
+    r->inputs = share->inputs;
+  } else {
+    r->slots.resize(kSlots);
+    for (auto &s : r->slots) ok = ok && alloc_slot(r, s);
+    r->inputs.resize(cfg->n_inputs);
+    for (auto &in : r->inputs) ok = ok && alloc_input(r, in);
+  }
   r->ntx_c = (g.cw / 32) * (g.ch / 32);
   const int nr = g.nsb * g.R;
   const int64_t nc = (int64_t)g.nsb * g.C;
@@ -1519,6 +1541,36 @@ rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
 // (FrameInvariants::set_quantizers, src/encoder.rs:865-880, from
 // QuantizerParameters; the host computes them, rav1e_amd/rate.py).  Every
 // level must be set before the first inter frame.
+rv_replay *rv_replay_create(const rv_replay_cfg *cfg, void *stream) {
+  return create_impl(cfg, stream, nullptr);
+}
+
+rv_replay *rv_replay_create_twin(rv_replay *primary, void *stream) {
+  if (!primary || primary->n_groups > 1) {
+    rv_set_error(RV_EINVAL, "rv_replay_create_twin: needs a one-group primary");
+    return nullptr;
+  }
+  rv_replay *r = create_impl(&primary->cfg, stream, primary);
+  if (!r) return nullptr;
+  for (int l = 0; l < 3; l++) {
+    r->lv[l] = primary->lv[l];
+    r->db_level[l] = primary->db_level[l];
+    r->cdef_str[l][0] = primary->cdef_str[l][0];
+    r->cdef_str[l][1] = primary->cdef_str[l][1];
+  }
+  r->imp = primary->imp;  // owned by the primary
+  r->coded = primary->coded;
+  return r;
+}
+
+int rv_replay_seek(rv_replay *r, long n) {
+  if (!r || n < 1) return rv_set_error(RV_EINVAL, "rv_replay_seek: n >= 1");
+  r->coded = n;
+  return RV_OK;
+}
+
+void *rv_replay_stream(rv_replay *r) { return r ? (void *)r->stream : nullptr; }
+
 int rv_replay_set_level_params(rv_replay *r, int level, const rv_replay_level_params *p) {
   if (!r || !p || level < 0 || level > 2 || p->base_q_idx < 1 || p->base_q_idx > 255)
     return rv_set_error(RV_EINVAL, "rv_replay_set_level_params: bad arguments");
@@ -1540,8 +1592,8 @@ int rv_replay_set_level_params(rv_replay *r, int level, const rv_replay_level_pa
                         &L.qs[l][c]));
   }
   L.qidx = p->base_q_idx;
-  // deblock_filter_optimize's fast levels (inter frames; speed 6 would search
-  // them by SSE, sse_optimize -- not built, the fast levels stand in)
+  // deblock_filter_optimize's fast levels (inter frames at speed 10; speed 6
+  // searches them on the device, deblock_slot)
   r->db_level[level] = (uint8_t)rv_deblock_fast_level(rv_q_lookup(1, p->base_q_idx, bd), bd, 0);
   r->cdef_str[level][0] = (uint8_t)(p->cdef_strengths & 0xff);
   r->cdef_str[level][1] = (uint8_t)((p->cdef_strengths >> 8) & 0xff);

@@ -157,6 +157,10 @@ int rv_event_record(void *ev, void *stream) {
                         rv_resolve_stream(stream)));
   return RV_OK;
 }
+int rv_stream_wait_event(void *stream, void *ev) {
+  RV_TRY(hipStreamWaitEvent(rv_resolve_stream(stream), reinterpret_cast<hipEvent_t>(ev), 0));
+  return RV_OK;
+}
 int rv_event_sync(void *ev) {
   RV_TRY(hipEventSynchronize(reinterpret_cast<hipEvent_t>(ev)));
   return RV_OK;

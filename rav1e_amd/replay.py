@@ -286,6 +286,27 @@ class HipReplay:
             _check(lib().rv_replay_set_level_params(self.h, lv, C.byref(p)),
                    "rv_replay_set_level_params")
 
+    def twin(self):
+        """A second instance sharing this one's DPB and inputs
+        (rv_replay_create_twin): it codes the level-2 frames concurrently
+        with this instance's levels 0 / 1 (PairedReplay)."""
+        t = HipReplay.__new__(HipReplay)
+        t.cfg, t.geom, t.speed, t.n_words, t.levels = self.cfg, self.geom, self.speed, \
+            self.n_words, self.levels
+        t.h = lib().rv_replay_create_twin(self.h, None)
+        if not t.h:
+            raise RuntimeError(f"rv_replay_create_twin: {lib().rv_last_error().decode()}")
+        t.primary = self  # the DPB's owner outlives the twin
+        return t
+
+    def seek(self, n: int):
+        """The next frame() codes coding-order frame n (rv_replay_seek)."""
+        _check(lib().rv_replay_seek(self.h, int(n)), "rv_replay_seek")
+
+    @property
+    def stream(self):
+        return lib().rv_replay_stream(self.h)
+
     def _frame_array(self):
         w, h, xd, yd, bd = self.geom
         n = frame_bytes(w, h, xd, yd, bd) // (2 if bd > 8 else 1)
@@ -385,6 +406,148 @@ class HipReplay:
             self.close()
         except Exception:
             pass
+
+
+def frame_info(n: int, n_refs: int = 2) -> dict:
+    """Coding-order frame n of the reorder pyramid (rv_replay.hip
+    frame_info): display, me_range_scale, pyramid level, key flag,
+    reference displays, compound."""
+    if n == 0:
+        return {"display": 0, "me_range_scale": 0, "level": 0, "is_key": 1,
+                "ref_display": [0, 0], "compound": 0}
+    g, j = (n - 1) // 4, (n - 1) % 4
+    rf = ((0, -4), (0, 4), (0, 2), (2, 4))[j]
+    refs = [max(0, 4 * g + rf[k]) for k in range(n_refs)] + [0] * (2 - n_refs)
+    return {"display": 4 * g + (4, 2, 1, 3)[j], "me_range_scale": (4, 2, 1, 1)[j],
+            "level": (0, 1, 2, 2)[j], "is_key": 0, "ref_display": refs,
+            "compound": int(n_refs == 2 and j in (1, 3))}
+
+
+class PairedReplay:
+    """One stream coded by two instances of the same tile group: `primary`
+    codes the key frame and the pyramid's levels 0 / 1 (display 4g+4,
+    4g+2), its twin (rv_replay_create_twin: shared DPB and inputs) the
+    level-2 frames 4g+1 and 4g+3, which no frame references, on its own
+    stream and host thread.  Device events order the two: a level-2 frame of
+    group g after the primary's level-1 frame of g, the primary's level-0
+    frame of g + 2 (its DPB slot is display 4g's) after the twin's group g.
+    frame() / drain() / results() / counters() / close() follow HipReplay's
+    interface for bench.timed_run.  The frames' results are the sequential
+    ones (the orders only interleave independent frames)."""
+
+    def __init__(self, primary: "HipReplay"):
+        import queue
+        import threading
+        self.p = primary
+        self.t = primary.twin()
+        self.n = 0
+        self.q = queue.Queue()
+        self.err = None
+        self._thr = threading
+        self.ev_p = [lib().rv_event_create() for _ in range(8)]
+        self.ev_t = [lib().rv_event_create() for _ in range(8)]
+        self.ready_p, self.ready_t = {}, {}
+        self.worker = threading.Thread(target=self._run, daemon=True)
+        self.worker.start()
+
+    def _flag(self, d, g):
+        if g not in d:
+            d[g] = self._thr.Event()
+        return d[g]
+
+    def frame(self) -> dict:
+        n = self.n
+        self.n += 1
+        if n == 0:
+            return self.p.frame()
+        g, j = (n - 1) // 4, (n - 1) % 4
+        if j >= 2:
+            self.q.put(n)
+            return frame_info(n, self.p.cfg.n_refs)
+        if j == 0 and g >= 2:
+            self._flag(self.ready_t, g - 2).wait()
+            self._raise()
+            _check(lib().rv_stream_wait_event(self.p.stream, self.ev_t[(g - 2) % 8]),
+                   "rv_stream_wait_event")
+        info = self.p.frame()
+        if j == 1:
+            _check(lib().rv_event_record(self.ev_p[g % 8], self.p.stream), "rv_event_record")
+            self._flag(self.ready_p, g).set()
+        return info
+
+    def _run(self):
+        while True:
+            n = self.q.get()
+            if n is None:
+                self.q.task_done()
+                return
+            g, j = (n - 1) // 4, (n - 1) % 4
+            try:
+                if self.err is None:
+                    self._flag(self.ready_p, g).wait()
+                    _check(lib().rv_stream_wait_event(self.t.stream, self.ev_p[g % 8]),
+                           "rv_stream_wait_event")
+                    self.t.seek(n)
+                    self.t.frame()
+                    if j == 3:
+                        _check(lib().rv_event_record(self.ev_t[g % 8], self.t.stream),
+                               "rv_event_record")
+            except Exception as e:  # handed to the main thread by drain()
+                self.err = e
+            finally:
+                if j == 3:
+                    self._flag(self.ready_t, g).set()
+                self.q.task_done()
+
+    def _raise(self):
+        if self.err is not None:
+            e, self.err = self.err, None
+            raise e
+
+    def drain(self):
+        """Every frame issued so far has been submitted to its stream."""
+        self.q.join()
+        self._raise()
+
+    def results(self) -> np.ndarray:
+        self.drain()
+        return self.p.results()
+
+    def set_timing(self, stride: int, block: int = 1):
+        self.p.set_timing(stride, block)
+        self.t.set_timing(stride, block)
+
+    def counters(self) -> np.ndarray:
+        """HipReplay.counters summed over both instances (their frames do not
+        overlap); [2] = the frames of the window."""
+        self.drain()
+        a, b = self.p.counters(), self.t.counters()
+        out = a + b
+        out[2] = max(a[2], b[2])
+        return out
+
+    def stage_ms_sum(self, kp: int, kt: int) -> np.ndarray:
+        """Stage times summed over the primary's last kp and the twin's last kt
+        instrumented frames."""
+        self.drain()
+        s = np.zeros(N_STAGES, np.float32)
+        if kp:
+            s = s + self.p.stage_ms_sum(kp)
+        if kt:
+            s = s + self.t.stage_ms_sum(kt)
+        return s
+
+    def close(self):
+        if self.t is not None:
+            self.q.put(None)
+            self.worker.join()
+            self.t.close()  # before the primary: it borrows the DPB
+            self.t = None
+            for e in self.ev_p + self.ev_t:
+                lib().rv_event_destroy(e)
+
+    def __getattr__(self, name):  # get_input, get_recon, ... of the primary
+        return getattr(self.p, name)
 
 
 class RcclComm:

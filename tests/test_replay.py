@@ -531,6 +531,45 @@ def test_gpu_tile_groups_exchange(flags):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF,
+                                   RP.RV_REPLAY_SPEED6])
+def test_gpu_paired_replay_matches_cpu(flags):
+    """PairedReplay: the level-2 frames on a twin instance (shared DPB, own
+    stream and host thread) give every frame's words and reconstruction of
+    the sequential CPU replay -- checked frame by frame, then over a run
+    with no host synchronisation between frames."""
+    import rav1e_amd as R
+    R.require_device(0)
+    w, h, nin = 256, 200, 24
+    speed = 6 if flags & RP.RV_REPLAY_SPEED6 else 10
+    g = RP.HipReplay(w, h, n_inputs=nin, flags=flags)
+    g.synth_inputs(0)
+    c = O.CpuReplay(w, h, n_inputs=nin, threads=O.cpu_share(), speed=speed,
+                    deblock=bool(flags & RP.RV_REPLAY_DEBLOCK), cdef=bool(flags & RP.RV_REPLAY_CDEF))
+    for i in range(nin):
+        c.set_input(i, g.get_input(i))
+    eng = RP.PairedReplay(g)
+    try:
+        for n in range(11):  # frame by frame
+            gi, ci = eng.frame(), c.frame()
+            assert gi == ci, (n, gi, ci)
+            eng.drain()
+            inst = eng.t if n and (n - 1) % 4 >= 2 else eng.p
+            np.testing.assert_array_equal(inst.results(), c.results())
+        for n in range(11, 21):  # free-running: the streams overlap
+            eng.frame()
+            c.frame()
+        eng.drain()
+        R._check(R.lib().rv_device_sync(), "sync")
+        for d in range(9, 21):  # displays coded in the second part
+            np.testing.assert_array_equal(g.get_recon(d), c.get_recon(d))
+    finally:
+        eng.close()
+        g.close()
+        c.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF | RP.RV_REPLAY_SPEED6])
 def test_gpu_replay_one_rank_rccl_exchange(flags):
     """The RCCL branch of the tile-group exchange (rv_replay.hip: pack,
