@@ -34,7 +34,7 @@ case "$MODE" in
     exec bash "$R/tools/gpu_step.sh" "${steps[@]}" ;;
   prof)
     CFG=${1:-2160p}; shift
-    B="python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 16 --warmup 5 $*"
+    B="python3 $R/bench.py --config $CFG --no-cpu-baseline --emulate-ranks 0 --steps 16 --warmup 5 $*"
     SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
     exec bash "$R/tools/gpu_step.sh" \
       "200 $TAG/trace.log cd /tmp && rocprofv3 --kernel-trace --stats -d $P/trace -o run -- $B" \
