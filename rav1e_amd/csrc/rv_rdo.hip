@@ -816,7 +816,8 @@ __device__ __forceinline__ uint64_t luma_dist(const RdoArgs &a, const RdoJob &j,
 
 template <typename Px, int NPART, int MODE>
 __device__ __forceinline__ void luma_front(const RdoArgs &a, const RdoPlane &pl, int t,
-                                           const RdoJob &jb, bool valid, uint8_t *scr, Px *pred) {
+                                           const RdoJob &jb, bool valid, uint8_t *scr, Px *pred,
+                                           bool skip_dist = true) {
   constexpr int N = 64, B = (int)sizeof(Px);
   constexpr int P = LumaLds<Px, int16_t, NPART>::kWinP;
   constexpr int RP = N / NPART;  // output rows per band
@@ -931,8 +932,9 @@ __device__ __forceinline__ void luma_front(const RdoArgs &a, const RdoPlane &pl,
   }
 
   const Px *o = plane_ptr<Px>(pl.org, jb.bx, jb.by);
-  // ---- skip variant: compute_distortion of the prediction -------------------
-  if (!a.commit) {
+  // ---- skip variant: compute_distortion of the prediction (or later, in a
+  // narrow phase of the quad kernel: skip_dist = false) ----------------------
+  if (!a.commit && skip_dist) {
     const uint64_t d = luma_dist<Px>(a, jb, o, pl.org.stride, pred);
     if (valid && lane == 0) pl.out[(int64_t)jb.oi * 3 + 0] = d;
   }
@@ -1160,9 +1162,13 @@ struct QuadLds {
   static constexpr int kBytes = cmax(4 * L::kSlot, 3 * kChromaPair(sizeof(Px)));
 };
 
+// var (RAV1E_HIP_RDO_VARIANT, A/B): bit 0 moves the skip distortion of the
+// scoring launches into the narrow phases (waves 1..3 during the row DCT,
+// wave 2 for wave 0's candidate during the inverse rows); bit 1 raises the
+// priority of the waves running a narrow phase (s_setprio).
 template <typename Px, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_quad_kernel(
-    RdoArgs luma, RdoArgs chroma, int nquads) {
+    RdoArgs luma, RdoArgs chroma, int nquads, int var) {
   using L = typename QuadLds<Px>::L;
   constexpr int NPART = sizeof(Px) == 1 ? 2 : 4;
   __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
@@ -1197,16 +1203,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     jb = rdo_job_intra<Px, 64>(luma, 0, valid ? t : n - 1);
   else
     jb = rdo_job<64>(luma, luma.p[0], valid ? t : n - 1);
-  if (valid) luma_front<Px, NPART, MODE>(luma, luma.p[0], t, jb, true, slot(wave), pred(wave));
+  const bool late_dist = (var & 1) && !luma.commit;
+  const bool prio = (var & 2) != 0;
+  if (valid)
+    luma_front<Px, NPART, MODE>(luma, luma.p[0], t, jb, true, slot(wave), pred(wave), !late_dist);
   __syncthreads();
   if (wave == 0) {  // row DCT: lane = 16 * candidate + raster row
+    if (prio) __builtin_amdgcn_s_setprio(2);
     const int q = lane >> 4;
     if (t0 + q < n) luma_fwd_row(fmid(q) + (lane & 15) * 65, luma.bd);
+    if (prio) __builtin_amdgcn_s_setprio(0);
+  } else if (late_dist && valid) {  // the skip variant's distortion of this wave's candidate
+    const uint64_t d = luma_dist<Px>(luma, jb, plane_ptr<Px>(luma.p[0].org, jb.bx, jb.by),
+                                     luma.p[0].org.stride, pred(wave));
+    if (lane == 0) luma.p[0].out[(int64_t)jb.oi * 3 + 0] = d;
   }
   __syncthreads();
   if (valid) luma_quantize(luma, luma.p[0], t, jb, true, fmid(wave), scan);
   __syncthreads();
   if (wave < 2) {  // inverse rows: lane = 32 * (candidate & 1) + coded row
+    if (prio) __builtin_amdgcn_s_setprio(2);
     const int q = 2 * wave + (lane >> 5), rr = lane & 31;
     const bool vq = t0 + q < n;
     const int range = luma.bd + 8, crange = luma.bd + 6 > 16 ? luma.bd + 6 : 16;
@@ -1214,6 +1230,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     if (vq) luma_inv_row_load(fmid(q), rr, v, range, nullptr);
     wave_sync();  // the wavefront's fmid reads precede its imid writes (same bytes)
     if (vq) luma_inv_row_tx(v, imid(q) + rr * 66, range, crange);
+    if (prio) __builtin_amdgcn_s_setprio(0);
+  } else if (wave == 2 && late_dist) {  // wave 0's candidate (its prediction is intact)
+    RdoJob j0;
+    if constexpr (MODE == 3)
+      j0 = rdo_job_intra<Px, 64>(luma, 0, t0);
+    else
+      j0 = rdo_job<64>(luma, luma.p[0], t0);
+    const uint64_t d = luma_dist<Px>(luma, j0, plane_ptr<Px>(luma.p[0].org, j0.bx, j0.by),
+                                     luma.p[0].org.stride, pred(0));
+    if (lane == 0) luma.p[0].out[(int64_t)j0.oi * 3 + 0] = d;
   }
   __syncthreads();
   if (valid) luma_back<Px, int16_t>(luma, luma.p[0], t, jb, true, imid(wave), pred(wave));
@@ -1264,6 +1290,10 @@ static void rdo_small_launch(const RdoArgs &a, int nplanes, int hbd, hipStream_t
 template <int MODE>
 static void rdo_launch(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s,
                        bool single, unsigned cpairs) {
+  static const int var = [] {
+    const char *e = getenv("RAV1E_HIP_RDO_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
   if (luma.bd == 12 || single) {  // 12-bit: i32 row-pass intermediate
     const unsigned grid = (unsigned)luma.n_tx + cpairs;
     if (grid == 0) return;
@@ -1277,9 +1307,9 @@ static void rdo_launch(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipS
   const unsigned grid = (unsigned)nquads + (cpairs + 2) / 3;
   if (grid == 0) return;
   if (hbd)
-    rdo_quad_kernel<uint16_t, MODE><<<grid, 256, 0, s>>>(luma, chroma, nquads);
+    rdo_quad_kernel<uint16_t, MODE><<<grid, 256, 0, s>>>(luma, chroma, nquads, var);
   else
-    rdo_quad_kernel<uint8_t, MODE><<<grid, 256, 0, s>>>(luma, chroma, nquads);
+    rdo_quad_kernel<uint8_t, MODE><<<grid, 256, 0, s>>>(luma, chroma, nquads, var);
 }
 
 // Replay-internal entry (rv_replay.hip): luma (N = 64, cdef distortion)

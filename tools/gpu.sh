@@ -8,6 +8,7 @@
 #                                     short bench run of CFG (one rocprofv3 pass each, the
 #                                     MI355X guide's rule: FETCH_SIZE and WRITE_SIZE do not
 #                                     share a pass)
+#   tools/gpu.sh envbench TAG CFG "ENV=.." ... [-- ARGS]  one bench line per environment (A/B)
 #   tools/gpu.sh ubench TAG           tools/ubench binaries (VALU issue rates, PMC calibration)
 #
 # Every step has its own time limit (tools/gpu_step.sh); a crash, abort or
@@ -41,6 +42,17 @@ case "$MODE" in
       "200 $TAG/fetch.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o run -- $B" \
       "200 $TAG/write.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $P/write -o run -- $B" \
       "200 $TAG/sq.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $SQ -d $P/sq -o run -- $B" ;;
+  envbench)
+    # one bench line per environment setting: envbench TAG CFG "A=1" "A=2 B=1" ... [-- ARGS]
+    CFG=$1; shift
+    envs=(); while [ $# -gt 0 ] && [ "$1" != "--" ]; do envs+=("$1"); shift; done
+    [ "$1" = "--" ] && shift
+    steps=(); i=0
+    for e in "${envs[@]}"; do
+      steps+=("400 $TAG/envbench_$i.log env $e python $R/bench.py --config $CFG --no-cpu-baseline --emulate-ranks 0 $*")
+      i=$((i + 1))
+    done
+    exec bash "$R/tools/gpu_step.sh" "${steps[@]}" ;;
   ubench)
     exec bash "$R/tools/gpu_step.sh" \
       "120 $TAG/valu_rates.txt $R/tools/ubench/valu_rates" ;;
