@@ -47,6 +47,6 @@ struct IntraDecideArgs {
 
 int rv_intra_elig(const rv::IntraGeo &g, const rv::RdoWinner *win, uint8_t *elig, uint8_t *iwas,
                   int32_t *mark, int32_t *list, int32_t *count, hipStream_t s);
-int rv_intra_screen(const rv::IntraScreenArgs &a, int hbd, hipStream_t s);
+int rv_intra_screen(const rv::IntraScreenArgs &a, int n, int hbd, hipStream_t s);
 int rv_intra_decide(const rv::IntraDecideArgs &a, hipStream_t s);
 int rv_intra_stats(int nsb, const uint8_t *elig, const uint8_t *iwas, uint32_t *out, hipStream_t s);

@@ -267,11 +267,15 @@ int rv_intra_elig(const IntraGeo &g, const RdoWinner *win, uint8_t *elig, uint8_
   return RV_OK;
 }
 
-int rv_intra_screen(const IntraScreenArgs &a, int hbd, hipStream_t s) {
+int rv_intra_screen(const IntraScreenArgs &a, int n, int hbd, hipStream_t s) {
+  // one workgroup per listed superblock (n = the list's count, read by the
+  // host; the kernel re-reads it from the device)
+  const unsigned grid = (unsigned)(n < a.g.nsb ? n : a.g.nsb);
+  if (grid == 0) return RV_OK;
   if (hbd)
-    intra_screen_kernel<uint16_t><<<a.g.nsb, 256, 0, s>>>(a);
+    intra_screen_kernel<uint16_t><<<grid, 256, 0, s>>>(a);
   else
-    intra_screen_kernel<uint8_t><<<a.g.nsb, 256, 0, s>>>(a);
+    intra_screen_kernel<uint8_t><<<grid, 256, 0, s>>>(a);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

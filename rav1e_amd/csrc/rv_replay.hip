@@ -1167,16 +1167,18 @@ static int intra_pass(rv_replay *r, const RdoArgs &la, const RdoArgs &ca, const 
     sa.count = cnt;
     sa.edges = r->i_edges;
     sa.modes = r->i_modes;
-    RV_R(rv_intra_screen(sa, g.hbd, st));
+    RV_R(rv_intra_screen(sa, n, g.hbd, st));
     // the intra chains: 3 luma modes, 6 chroma chains per plane
     RdoArgs li = la, cl = ca;
     li.commit = cl.commit = 0;
     li.list = cl.list = list;
     li.count = cl.count = cnt;
+    // grids sized by the round's count (the host read it): the lists hold
+    // n superblocks, the commit / revert lists at most n
     li.ntx_per_cand = 3;
-    li.n_tx = g.nsb * 3;
+    li.n_tx = n * 3;
     cl.ntx_per_cand = 6;
-    cl.n_tx = g.nsb * 6;
+    cl.n_tx = n * 6;
     li.iedges = cl.iedges = r->i_edges;
     li.imodes = cl.imodes = r->i_modes;
     li.iwin = cl.iwin = r->i_win;
@@ -1220,12 +1222,14 @@ static int intra_pass(rv_replay *r, const RdoArgs &la, const RdoArgs &ca, const 
     li.list = cl.list = r->i_commit;
     li.count = cl.count = r->i_cnt + 2;
     li.ntx_per_cand = cl.ntx_per_cand = 1;
-    li.n_tx = cl.n_tx = g.nsb;
+    li.n_tx = cl.n_tx = n;
     li.p[0].out = cl.p[0].out = cl.p[1].out = nullptr;
     RV_R(rv_rdo_intra(li, cl, g.hbd, st));
     RdoArgs lr = la, cr = ca;
     lr.list = cr.list = r->i_revert;
     lr.count = cr.count = r->i_cnt + 3;
+    lr.n_tx = n;
+    cr.n_tx = n * cr.ntx_per_cand;
     RV_R(rv_rdo_candidates(lr, cr, g.hbd, st));
     RV_H(hipMemcpyAsync(r->h_cnt, r->i_cnt + (ci ^ 1), 4, hipMemcpyDeviceToHost, st));
     RV_H(hipStreamSynchronize(st));
