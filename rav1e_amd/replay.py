@@ -469,6 +469,7 @@ class PairedReplay:
             self._raise()
             _check(lib().rv_stream_wait_event(self.p.stream, self.ev_t[(g - 2) % 8]),
                    "rv_stream_wait_event")
+        self.p.seek(n)  # its own counter has not seen the twin's frames
         info = self.p.frame()
         if j == 1:
             _check(lib().rv_event_record(self.ev_p[g % 8], self.p.stream), "rv_event_record")
