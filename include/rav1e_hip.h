@@ -641,8 +641,10 @@ int rv_replay_set_timing(rv_replay *r, int stride, int block);
  * (+ the join with the lookahead), [9] F6 commit, [10] F6b intra-mode
  * screening + intra RDO rounds, [11] F5 importance, [12] F7 loop filters /
  * pad / exchange, [13] the lookahead's own span (FL, on the side stream,
- * overlapping [4]..[7]).  [0] .. [12] tile the frame's span on the replay
- * stream.  Returns the count written (<= 14). */
+ * overlapping [4]..[7]), [14] the speed-10 frame-edge levels' own span (their
+ * searches, candidates and scores on the edge stream, beside [4]..[8]; 0
+ * without edge superblocks).  [0] .. [12] tile the frame's span on the replay
+ * stream.  Returns the count written (<= 15). */
 int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
 /* Same breakdown summed over the last `last_frames` instrumented frames
  * (<= 64). */

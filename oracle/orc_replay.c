@@ -82,6 +82,9 @@ typedef struct orc_replay {
    * frame-edge superblocks (must_split), in group superblocks (ex0, ey0) +
    * (ew, eh) */
   int s6, lvl, ex0, ey0, ew, eh;
+  /* per level: leaves exist (mode decision, commit) / the motion search runs
+   * (16x16 and 8x8 seed from the 32x32 searches) */
+  int lv_used[4], lv_me[4];
   struct olevel {
     int B, n, gw, gh, bc, bch, txl, txc, tx0, ty0, tws, ths;
     orc_mv *full, *sub; /* [R][n] */
@@ -440,6 +443,25 @@ static int alloc_levels(orc_replay *r, int x0, int y0, int w, int h) {
   r->wpart = r->nwords;
   r->nwords += (size_t)r->nsb;
   r->leaf0 = calloc(r->nsb, 1);
+  /* the levels holding leaves: every one at speed 6; at speed 10 those of the
+   * must_split walk of the edge superblocks (inside, parent not inside) */
+  for (int l = 1; l < 4; l++) r->lv_used[l] = r->s6;
+  for (int sb = 0; !r->s6 && sb < r->nsb; sb++) {
+    if (!edge_sb(r, sb)) continue;
+    const int X = (r->tx0 + sb % r->tw) * SB, Y = (r->ty0 + sb / r->tw) * SB;
+    for (int l = 1; l < 4; l++) {
+      const int B = SB >> l;
+      for (int y = Y; y < Y + SB; y += B)
+        for (int x = X; x < X + SB; x += B) {
+          const int in = x + B <= r->W && y + B <= r->H;
+          const int pin = (x & ~(2 * B - 1)) + 2 * B <= r->W && (y & ~(2 * B - 1)) + 2 * B <= r->H;
+          if (in && !pin) r->lv_used[l] = 1;
+        }
+    }
+  }
+  r->lv_me[1] = r->lv_used[1] || r->lv_used[2] || r->lv_used[3];
+  r->lv_me[2] = r->lv_used[2];
+  r->lv_me[3] = r->lv_used[3];
   free(r->words);
   r->words = calloc(r->nwords, 8);
   return r->words && r->leaf0 ? 0 : -1;
@@ -995,6 +1017,7 @@ static void run_me(orc_replay *r, int sb) {
   int ex, ey;
   if (!in_rect(r, sb, &ex, &ey)) return;
   for (int l = 1; l < 4; l++) {
+    if (!r->lv_me[l]) continue;
     struct olevel *P = &r->pl[l];
     const int k2 = 1 << l, B = P->B;
     const struct olevel *U = &r->pl[1];
@@ -1328,6 +1351,7 @@ static void run_rdo(orc_replay *r, int sb, uint64_t tail[3]) {
     memcpy(ru[0], bu_, (size_t)cwid * chei * px);
     memcpy(rv[0], bv_, (size_t)cwid * chei * px);
     for (int l = 1; l < 4; l++) {
+      if (!r->lv_used[l]) continue;
       const struct olevel *P = &r->pl[l];
       const int k2 = 1 << l;
       for (int j = 0; j < k2; j++)

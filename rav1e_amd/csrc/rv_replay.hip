@@ -641,6 +641,13 @@ struct rv_replay {
   // superblocks past the frame's right / bottom edge (must_split)
   bool lvl = false;
   int ex0 = 0, ey0 = 0, ew = 0, eh = 0;
+  // per level: leaves exist (RDO, score, commit) / the motion search runs
+  // (a 16x16 / 8x8 level seeds from the 32x32 searches)
+  bool lv_used[kLevels] = {false, false, false, false};
+  bool lv_me[kLevels] = {false, false, false, false};
+  // speed 10: the edge levels run on their own stream beside the 64x64 stages
+  hipStream_t edge = nullptr;
+  hipEvent_t ev_efork = nullptr, ev_ejoin = nullptr, ev_epart = nullptr, ev_ecommit = nullptr;
   bool deblock = false;           // RV_REPLAY_DEBLOCK
   uint8_t *mi_lg = nullptr, *mi_skip = nullptr;  // the deblocking block map
   int mi_stride = 0, mi_cols = 0, mi_rows = 0;
@@ -698,7 +705,7 @@ struct rv_replay {
   static constexpr int kRing = 64;
   // e[0..13]: the stage boundaries on the main stream; e[14], e[15]: the
   // lookahead's start and end (on the side stream when it overlaps)
-  static constexpr int kEv = 16;
+  static constexpr int kEv = 18;
   static constexpr int kStageEv = 14;
   hipEvent_t evs[kRing][kEv];
   int timing_stride = 1, timing_block = 1;
@@ -1250,6 +1257,7 @@ void rv_replay_destroy(rv_replay *r) {
   // stream running)
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->side) (void)hipStreamSynchronize(r->side);
+  if (r->edge) (void)hipStreamSynchronize(r->edge);
   for (void *p : r->allocs) (void)hipFree(p);
   if (r->h_cnt) (void)hipHostFree(r->h_cnt);
   for (int f = 0; f < rv_replay::kRing; f++)
@@ -1258,6 +1266,9 @@ void rv_replay_destroy(rv_replay *r) {
   if (r->ev_fork) (void)hipEventDestroy(r->ev_fork);
   if (r->ev_join) (void)hipEventDestroy(r->ev_join);
   if (r->side) (void)hipStreamDestroy(r->side);
+  for (hipEvent_t ev : {r->ev_efork, r->ev_ejoin, r->ev_epart, r->ev_ecommit})
+    if (ev) (void)hipEventDestroy(ev);
+  if (r->edge) (void)hipStreamDestroy(r->edge);
   if (r->own_stream && r->stream) (void)hipStreamDestroy(r->stream);
   delete r;
 }
@@ -1387,6 +1398,27 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     }
   }
   if (r->lvl) {
+    // the levels holding leaves: every one at speed 6; at speed 10 those of
+    // the must_split walk of the edge superblocks (largest blocks inside)
+    for (int l = 1; l < kLevels; l++) r->lv_used[l] = r->s6;
+    if (!r->s6) {
+      for (int sb = 0; sb < g.nsb; sb++) {
+        const int X = (g.tx0 + sb % g.tw) * kSb, Y = (g.ty0 + sb / g.tw) * kSb;
+        if (X + kSb <= g.W && Y + kSb <= g.H) continue;
+        for (int l = 1; l < kLevels; l++) {
+          const int B = kSb >> l;
+          for (int y = Y; y < Y + kSb; y += B)
+            for (int x = X; x < X + kSb; x += B) {
+              const int inside = x + B <= g.W && y + B <= g.H;
+              const int pin = (x & ~(2 * B - 1)) + 2 * B <= g.W && (y & ~(2 * B - 1)) + 2 * B <= g.H;
+              if (inside && !pin) r->lv_used[l] = true;  // a leaf: inside, its parent is not
+            }
+        }
+      }
+    }
+    r->lv_me[1] = r->lv_used[1] || r->lv_used[2] || r->lv_used[3];
+    r->lv_me[2] = r->lv_used[2];
+    r->lv_me[3] = r->lv_used[3];
     rv_replay::PLevel &P0 = r->pl[0];
     P0.B = kSb;
     P0.n = g.nsb;
@@ -1520,6 +1552,12 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     ok = ok && hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking) == hipSuccess &&
          hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&r->ev_join, hipEventDisableTiming) == hipSuccess;
+  if (r->overlap && r->lvl && !r->s6)
+    ok = ok && hipStreamCreateWithFlags(&r->edge, hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&r->ev_efork, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&r->ev_ejoin, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&r->ev_epart, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&r->ev_ecommit, hipEventDisableTiming) == hipSuccess;
   const size_t ev_bytes = (size_t)rv_replay::kRing * 2 * nr * 4;
   r->ds_evals = (uint32_t *)dalloc(r, ev_bytes);
   ok = ok && r->ds_evals && hipMemsetAsync(r->ds_evals, 0, ev_bytes, r->stream) == hipSuccess;
@@ -1864,66 +1902,21 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     if (r->overlap) RV_H(hipEventRecord(r->ev_join, ls));
   }
   RV_EV(4);
-  // An error return from here on must not leave the lookahead running on
-  // the side stream: the next frame's F1 / F2 rewrite the MVs it reads, and
-  // rv_replay_destroy frees them.  Disarmed once the main stream has joined.
+  // An error return from here on must not leave the lookahead (side stream)
+  // or the frame-edge levels (edge stream) running: the next frame's F1 / F2
+  // rewrite the MVs they read, and rv_replay_destroy frees them.  Disarmed
+  // once the main stream has joined them.
   struct SideJoin {
     rv_replay *r;
     bool armed;
     ~SideJoin() {
       if (armed && r->side) (void)hipStreamSynchronize(r->side);
+      if (armed && r->edge) (void)hipStreamSynchronize(r->edge);
     }
-  } side_join{r, r->overlap};
-  // F3 full-res full-pel diamond -> sub-pel predictor; sub-pel diamond
-  // (speed 10: SAD, no hp) -> NEWMV of every superblock and reference
-  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
-                               r->full, ev_full, &to_sub, st));
-  RV_EV(5);
-  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, r->s6 ? 1 : 0,
-                               0, g.bd, r->sub, ev_sub, nullptr, st));
-  // the levels: the same search for every 32x32, 16x16 and 8x8 block of the
-  // level grids (sub-pel by SATD at speed 6, use_satd_subpel,
-  // src/api/config.rs:429-431; SAD at speed 10)
-  for (int l = 1; r->lvl && l < kLevels; l++) {
-    rv_replay::PLevel &P = r->pl[l];
-    // 32x32: the half-res quadrant searches; 16x16 / 8x8: the 32x32's sub-pel
-    if (l == 1)
-      seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, st>>>(
-          P.jobs_full[lv], P.n, P.gw, g.R, r->half, g.nsb, 0, 0, r->ex0, r->ey0, g.tw);
-    else
-      seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, st>>>(
-          P.jobs_full[lv], P.n, P.gw, g.R, r->pl[1].sub, r->pl[1].n, r->pl[1].gw, 1 << (l - 1), 0, 0,
-          0);
-    ChainNext to_s{kChainFullToSub, P.jobs_sub[lv]};
-    RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, P.jobs_full[lv], P.n, P.B, P.B, 0, 0, 0,
-                                 g.bd, P.full, nullptr, &to_s, st));
-    RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, P.jobs_sub[lv], P.n, P.B, P.B, 1,
-                                 r->s6 ? 1 : 0, 0, g.bd, P.sub, nullptr, nullptr, st));
-  }
-  // the valid candidates (a few microseconds; bracketed with F3 sub-pel;
-  // the count was zeroed by the previous frame's argmin or at creation)
+  } side_join{r, r->overlap || r->edge};
+  // the candidates' RDO arguments: luma (N = 64, cdef distortion) and both
+  // chroma planes (N = 32, SSE) of every candidate
   const int nsingle = g.nsb * g.R * g.M;
-  cand_list_kernel<<<(nsingle + 255) / 256, 256, 0, st>>>(cg, r->sub, nsingle, r->cand_list,
-                                                          r->cand_count);
-  for (int l = 1; r->lvl && l < kLevels; l++) {
-    rv_replay::PLevel &P = r->pl[l];
-    const int ns = P.n * g.R * g.M;
-    cand_list_kernel<<<(ns + 255) / 256, 256, 0, st>>>(P.cg, P.sub, ns, P.cand_list, P.cand_count);
-  }
-  if (cg.comp) {  // the compound lists (after the single ones in the same arrays)
-    comp_list_kernel<<<(g.nsb * cg.comp + 255) / 256, 256, 0, st>>>(
-        cg, r->sub, nsingle, r->cand_list + nsingle, r->cand_count + 1);
-    for (int l = 1; r->lvl && l < kLevels; l++) {
-      rv_replay::PLevel &P = r->pl[l];
-      CandGeo cgl = P.cg;
-      cgl.comp = cg.comp;
-      const int ns = P.n * g.R * g.M;
-      comp_list_kernel<<<(P.n * cg.comp + 255) / 256, 256, 0, st>>>(
-          cgl, P.sub, ns, P.cand_list + ns, P.cand_count + 1);
-    }
-  }
-  RV_EV(6);
-  // F4 every valid candidate, luma + both chroma planes in one fused launch
   RdoArgs la, ca;
   memset(&la, 0, sizeof(la));
   la.p[0].org = cur.y;
@@ -1972,55 +1965,188 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   ca.sub_h = (g.ch < 8 ? g.ch : 8) >> g.ydec;
   ca.q_tx_index = 3 * 16 + 0;  // TX_32X32, DCT_DCT
   ca.tx_size = 3;
-  RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
-  // speed 6: the candidates of every 32x32 .. 8x8 block, luma (cdef
-  // distortion) and chroma launches per level
+
+  // ---- the 32x32 .. 8x8 levels (speed 6: every block; speed 10: the frame-
+  // edge rectangle), in pieces the schedule places: speed 6 interleaves them
+  // with the 64x64 stages on the main stream, speed 10 runs them all on the
+  // edge stream beside the 64x64 stages (levels with no leaf are skipped)
   RdoArgs ll[kLevels], lc6[kLevels];
-  for (int l = 1; r->lvl && l < kLevels; l++) {
-    rv_replay::PLevel &P = r->pl[l];
-    CandGeo cgl = P.cg;
-    cgl.comp = cg.comp;
-    const int ns = P.n * g.R * g.M;
-    RdoArgs a = la;
-    a.p[0].levels = P.l_lev;
-    a.p[0].out = P.l_out;
-    a.p[0].q = L.qs[l][0];
-    a.g = cgl;
-    a.sub = P.sub;
-    a.win = P.win;
-    a.n_tx = ns;
-    a.list = P.cand_list;
-    a.count = P.cand_count;
-    a.ntx_per_cand = 1;
-    a.bsize = P.B;
-    a.mb_w = a.mb_h = P.B;
-    a.q_tx_index = P.txl * 16;  // DCT_DCT
-    a.tx_size = P.txl;
-    RdoArgs c = ca;
-    for (int q = 0; q < 2; q++) {
-      c.p[q].levels = P.c_lev + (size_t)q * P.n * P.bc * P.bch;
-      c.p[q].out = P.c_out + (size_t)q * P.n * g.C * 3;
-      c.p[q].q = L.qs[l][1 + q];
+  // motion_estimation of every block (sub-pel by SATD at speed 6,
+  // use_satd_subpel, src/api/config.rs:429-431; SAD at speed 10), seeded with
+  // the pmvs entry: a 32x32 its half-res quadrant search, a 16x16 / 8x8 its
+  // 32x32's sub-pel winner
+  auto lv_me = [&](hipStream_t es) -> int {
+    for (int l = 1; l < kLevels; l++) {
+      if (!r->lv_me[l]) continue;
+      rv_replay::PLevel &P = r->pl[l];
+      if (l == 1)
+        seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, es>>>(
+            P.jobs_full[lv], P.n, P.gw, g.R, r->half, g.nsb, 0, 0, r->ex0, r->ey0, g.tw);
+      else
+        seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, es>>>(
+            P.jobs_full[lv], P.n, P.gw, g.R, r->pl[1].sub, r->pl[1].n, r->pl[1].gw, 1 << (l - 1),
+            0, 0, 0);
+      ChainNext to_s{kChainFullToSub, P.jobs_sub[lv]};
+      RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, P.jobs_full[lv], P.n, P.B, P.B, 0, 0, 0,
+                                   g.bd, P.full, nullptr, &to_s, es));
+      RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, P.jobs_sub[lv], P.n, P.B, P.B, 1,
+                                   r->s6 ? 1 : 0, 0, g.bd, P.sub, nullptr, nullptr, es));
     }
-    c.g = cgl;
-    c.sub = P.sub;
-    c.win = P.win;
-    c.n_tx = ns;
-    c.list = P.cand_list;
-    c.count = P.cand_count;
-    c.ntx_per_cand = 1;
-    c.bsize = P.B;
-    c.mb_w = P.bc;
-    c.mb_h = P.bch;
-    c.sub_w = (P.bc < 8 ? P.bc : 8) >> g.xdec;   // sse_wxh's importance blocks
-    c.sub_h = (P.bch < 8 ? P.bch : 8) >> g.ydec;
-    c.q_tx_index = P.txc * 16;
-    c.tx_size = P.txc;
-    ll[l] = a;
-    lc6[l] = c;
-    RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, st, 0));
-    RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, st, 0));
+    return RV_OK;
+  };
+  // the candidate lists of every used level (single, then compound)
+  auto lv_lists = [&](hipStream_t es, bool comp) {
+    for (int l = 1; l < kLevels; l++) {
+      if (!r->lv_used[l]) continue;
+      rv_replay::PLevel &P = r->pl[l];
+      const int ns = P.n * g.R * g.M;
+      if (!comp) {
+        cand_list_kernel<<<(ns + 255) / 256, 256, 0, es>>>(P.cg, P.sub, ns, P.cand_list,
+                                                            P.cand_count);
+      } else {
+        CandGeo cgl = P.cg;
+        cgl.comp = cg.comp;
+        comp_list_kernel<<<(P.n * cg.comp + 255) / 256, 256, 0, es>>>(
+            cgl, P.sub, ns, P.cand_list + ns, P.cand_count + 1);
+      }
+    }
+  };
+  // the single-reference candidates of every used level: luma (cdef
+  // distortion) and chroma launches
+  auto lv_rdo = [&](hipStream_t es) -> int {
+    for (int l = 1; l < kLevels; l++) {
+      if (!r->lv_used[l]) continue;
+      rv_replay::PLevel &P = r->pl[l];
+      CandGeo cgl = P.cg;
+      cgl.comp = cg.comp;
+      const int ns = P.n * g.R * g.M;
+      RdoArgs a = la;
+      a.p[0].levels = P.l_lev;
+      a.p[0].out = P.l_out;
+      a.p[0].q = L.qs[l][0];
+      a.g = cgl;
+      a.sub = P.sub;
+      a.win = P.win;
+      a.n_tx = ns;
+      a.list = P.cand_list;
+      a.count = P.cand_count;
+      a.ntx_per_cand = 1;
+      a.bsize = P.B;
+      a.mb_w = a.mb_h = P.B;
+      a.q_tx_index = P.txl * 16;  // DCT_DCT
+      a.tx_size = P.txl;
+      RdoArgs c = ca;
+      for (int q = 0; q < 2; q++) {
+        c.p[q].levels = P.c_lev + (size_t)q * P.n * P.bc * P.bch;
+        c.p[q].out = P.c_out + (size_t)q * P.n * g.C * 3;
+        c.p[q].q = L.qs[l][1 + q];
+      }
+      c.g = cgl;
+      c.sub = P.sub;
+      c.win = P.win;
+      c.n_tx = ns;
+      c.list = P.cand_list;
+      c.count = P.cand_count;
+      c.ntx_per_cand = 1;
+      c.bsize = P.B;
+      c.mb_w = P.bc;
+      c.mb_h = P.bch;
+      c.sub_w = (P.bc < 8 ? P.bc : 8) >> g.xdec;   // sse_wxh's importance blocks
+      c.sub_h = (P.bch < 8 ? P.bch : 8) >> g.ydec;
+      c.q_tx_index = P.txc * 16;
+      c.tx_size = P.txc;
+      ll[l] = a;
+      lc6[l] = c;
+      RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, es, 0));
+      RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, es, 0));
+    }
+    return RV_OK;
+  };
+  // the compound candidates of every used level (all pushed)
+  auto lv_rdo_comp = [&](hipStream_t es) -> int {
+    for (int l = 1; l < kLevels; l++) {
+      if (!r->lv_used[l]) continue;
+      const rv_replay::PLevel &P = r->pl[l];
+      RdoArgs a = ll[l], c = lc6[l];
+      a.list = c.list = P.cand_list + P.n * g.R * g.M;
+      a.count = c.count = P.cand_count + 1;
+      a.cand_base = c.cand_base = 0;
+      a.n_tx = c.n_tx = P.n * cg.comp;
+      RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, es, 1));
+      RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, es, 1));
+    }
+    return RV_OK;
+  };
+  // every used level's winners and result words
+  auto lv_score = [&](hipStream_t es) {
+    for (int l = 1; l < kLevels; l++) {
+      if (!r->lv_used[l]) continue;
+      rv_replay::PLevel &P = r->pl[l];
+      CandGeo cgl = P.cg;
+      cgl.comp = cg.comp;
+      score_level<<<(P.n + 63) / 64, 64, 0, es>>>(cgl, L.lambda, L.ds[1], L.ds[2], P.full, P.sub,
+                                                  P.l_out, P.c_out, P.c_out + (size_t)P.n * g.C * 3,
+                                                  P.win, r->words + P.woff, P.cand_count,
+                                                  r->cand_evals + 2 * (slot * kLevels + l));
+    }
+  };
+  // the leaves of every used level into the frame
+  auto lv_commit = [&](hipStream_t es) -> int {
+    for (int l = 1; l < kLevels; l++) {
+      if (!r->lv_used[l]) continue;
+      const rv_replay::PLevel &P = r->pl[l];
+      RdoArgs a = ll[l], c = lc6[l];
+      a.commit = c.commit = 1;
+      a.list = c.list = P.leaf;
+      a.count = c.count = r->leaf_count + l;
+      a.n_tx = c.n_tx = P.n;
+      RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, es, 2));
+      RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, es, 2));
+    }
+    return RV_OK;
+  };
+  // speed 10: the edge levels on their own stream, forked after F2
+  const bool edge = r->lvl && !r->s6 && r->edge;
+  if (edge) {
+    RV_H(hipEventRecord(r->ev_efork, st));
+    RV_H(hipStreamWaitEvent(r->edge, r->ev_efork, 0));
+    hipStream_t es = r->edge;
+    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 2], es));
+    RV_R(lv_me(es));
+    lv_lists(es, false);
+    if (cg.comp) lv_lists(es, true);
+    RV_R(lv_rdo(es));
+    if (cg.comp) RV_R(lv_rdo_comp(es));
+    lv_score(es);
+    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 3], es));
+    RV_H(hipEventRecord(r->ev_ejoin, es));
+  } else if (tm) {  // no edge stream: an empty span
+    RV_H(hipEventRecord(e[rv_replay::kStageEv + 2], st));
+    RV_H(hipEventRecord(e[rv_replay::kStageEv + 3], st));
   }
+
+  // F3 full-res full-pel diamond -> sub-pel predictor; sub-pel diamond
+  // (speed 10: SAD, no hp) -> NEWMV of every superblock and reference
+  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
+                               r->full, ev_full, &to_sub, st));
+  RV_EV(5);
+  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, r->s6 ? 1 : 0,
+                               0, g.bd, r->sub, ev_sub, nullptr, st));
+  if (r->lvl && !edge) RV_R(lv_me(st));
+  // the valid candidates (a few microseconds; bracketed with F3 sub-pel;
+  // the count was zeroed by the previous frame's argmin or at creation)
+  cand_list_kernel<<<(nsingle + 255) / 256, 256, 0, st>>>(cg, r->sub, nsingle, r->cand_list,
+                                                          r->cand_count);
+  if (r->lvl && !edge) lv_lists(st, false);
+  if (cg.comp) {  // the compound lists (after the single ones in the same arrays)
+    comp_list_kernel<<<(g.nsb * cg.comp + 255) / 256, 256, 0, st>>>(
+        cg, r->sub, nsingle, r->cand_list + nsingle, r->cand_count + 1);
+    if (r->lvl && !edge) lv_lists(st, true);
+  }
+  RV_EV(6);
+  // F4 every valid candidate, luma + both chroma planes in one fused launch
+  RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
+  if (r->lvl && !edge) RV_R(lv_rdo(st));
   if (cg.comp) {  // the compound candidates (all pushed), distinct MV pairs from the list
     RdoArgs lc = la, cc = ca;
     lc.list = cc.list = r->cand_list + nsingle;
@@ -2030,22 +2156,12 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     cc.n_tx = g.nsb * cg.comp * ntx_c;
     RV_EV(7);
     RV_R(rv_rdo_candidates(lc, cc, g.hbd, st, true));
-    for (int l = 1; r->lvl && l < kLevels; l++) {
-      const rv_replay::PLevel &P = r->pl[l];
-      RdoArgs a = ll[l], c = lc6[l];
-      a.list = c.list = P.cand_list + P.n * g.R * g.M;
-      a.count = c.count = P.cand_count + 1;
-      a.cand_base = c.cand_base = 0;
-      a.n_tx = c.n_tx = P.n * cg.comp;
-      RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, st, 1));
-      RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, st, 1));
-    }
+    if (r->lvl && !edge) RV_R(lv_rdo_comp(st));
   } else {
     RV_EV(7);
   }
   RV_EV(8);
   if (r->overlap) RV_H(hipStreamWaitEvent(st, r->ev_join, 0));  // the lookahead's MVs
-  side_join.armed = false;
   score_candidates<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, cg, L.lambda, L.ds[1], L.ds[2], r->sub,
                                                      r->l_out,
                                                      r->c_out, r->c_out + nct * 3, ntx_c, r->win,
@@ -2055,18 +2171,14 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                                      r->cand_evals + 2 * slot * kLevels,
                                                      r->leaf_count);
   if (r->lvl) {
+    if (edge)
+      RV_H(hipStreamWaitEvent(st, r->ev_ejoin, 0));  // the levels' winners
+    else
+      lv_score(st);
     PartArgs pa;
     memset(&pa, 0, sizeof(pa));
     for (int l = 0; l < kLevels; l++) {
       rv_replay::PLevel &P = r->pl[l];
-      if (l > 0) {
-        CandGeo cgl = P.cg;
-        cgl.comp = cg.comp;
-        score_level<<<(P.n + 63) / 64, 64, 0, st>>>(cgl, L.lambda, L.ds[1], L.ds[2], P.full, P.sub,
-                                                    P.l_out, P.c_out, P.c_out + (size_t)P.n * g.C * 3,
-                                                    P.win, r->words + P.woff, P.cand_count,
-                                                    r->cand_evals + 2 * (slot * kLevels + l));
-      }
       pa.win[l] = l ? P.win : r->win;
       pa.gw[l] = P.gw;
       pa.x0[l] = (g.tx0 + (l ? r->ex0 : 0)) * kSb;
@@ -2083,7 +2195,14 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     partition_kernel<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, pa);
   }
   RV_EV(9);
-  // F6 commit the winners into the frame
+  // F6 commit the winners into the frame: the levels' leaves (speed 10: on
+  // the edge stream, beside the superblocks' commit)
+  if (edge) {
+    RV_H(hipEventRecord(r->ev_epart, st));
+    RV_H(hipStreamWaitEvent(r->edge, r->ev_epart, 0));
+    RV_R(lv_commit(r->edge));
+    RV_H(hipEventRecord(r->ev_ecommit, r->edge));
+  }
   la.commit = ca.commit = 1;
   la.list = ca.list = r->lvl ? r->pl[0].leaf : nullptr;  // with levels: the unsplit superblocks
   la.count = ca.count = r->lvl ? r->leaf_count : nullptr;
@@ -2091,16 +2210,9 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   ca.n_tx = g.nsb * ntx_c;
   la.ntx_per_cand = 1;
   RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
-  for (int l = 1; r->lvl && l < kLevels; l++) {  // and the leaves of every level
-    const rv_replay::PLevel &P = r->pl[l];
-    RdoArgs a = ll[l], c = lc6[l];
-    a.commit = c.commit = 1;
-    a.list = c.list = P.leaf;
-    a.count = c.count = r->leaf_count + l;
-    a.n_tx = c.n_tx = P.n;
-    RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, st, 2));
-    RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, st, 2));
-  }
+  if (r->lvl && !edge) RV_R(lv_commit(st));
+  if (edge) RV_H(hipStreamWaitEvent(st, r->ev_ecommit, 0));
+  side_join.armed = false;  // both side streams have joined the main one
   RV_EV(10);
   // F6b intra-mode screening + intra RDO of the non-skip superblocks
   if (r->intra) RV_R(intra_pass(r, la, ca, cur, S, L, slot));
@@ -2241,6 +2353,12 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
     if (n < cap) {  // the lookahead's own span (overlapped with F3/F4 by default)
       float ms = 0.f;
       RV_H(hipEventElapsedTime(&ms, e[kS], e[kS + 1]));
+      ms_out[n++] += ms;
+    }
+    if (n < cap) {  // the edge levels' own span (speed 10, beside F3..F4)
+      float ms = 0.f;
+      RV_H(hipEventSynchronize(e[kS + 3]));
+      RV_H(hipEventElapsedTime(&ms, e[kS + 2], e[kS + 3]));
       ms_out[n++] += ms;
     }
   }

@@ -27,8 +27,8 @@ RV_REPLAY_NO_INTRA = 64  # no intra-mode screening of non-skip superblocks (defa
 #                          at speed 10 in 4:2:0)
 # HIP-event stages of a frame: F0, F1, F2, FL (lookahead), F3 full-pel, F3
 # sub-pel, F4 single, F4 compound, F4 argmin, F6 commit, F6b intra, F5, F7,
-# then the lookahead's own span
-N_STAGES = 14
+# then the lookahead's own span and the speed-10 edge levels' own span
+N_STAGES = 15
 
 # GOP of the reference's reorder pyramid (src/api/internal.rs:61-95):
 # group_input_len 4, levels 0,1,2,2 -> me_range_scale = 4 >> level
