@@ -1290,9 +1290,10 @@ static void rdo_small_launch(const RdoArgs &a, int nplanes, int hbd, hipStream_t
 template <int MODE>
 static void rdo_launch(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_t s,
                        bool single, unsigned cpairs) {
+  // default 3: both (measured at 2160p: 880 vs 850 frames/s, r03g)
   static const int var = [] {
     const char *e = getenv("RAV1E_HIP_RDO_VARIANT");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 3;
   }();
   if (luma.bd == 12 || single) {  // 12-bit: i32 row-pass intermediate
     const unsigned grid = (unsigned)luma.n_tx + cpairs;
