@@ -646,8 +646,10 @@ struct rv_replay {
   bool lv_used[kLevels] = {false, false, false, false};
   bool lv_me[kLevels] = {false, false, false, false};
   // speed 10: the edge levels run on their own stream beside the 64x64 stages
-  hipStream_t edge = nullptr;
-  hipEvent_t ev_efork = nullptr, ev_ejoin = nullptr, ev_epart = nullptr, ev_ecommit = nullptr;
+  hipStream_t edge[kLevels] = {nullptr, nullptr, nullptr, nullptr};  // [1..3]: one per level
+  hipEvent_t ev_efork = nullptr, ev_l1me = nullptr, ev_epart = nullptr;
+  hipEvent_t ev_ejoin[kLevels] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_ecommit[kLevels] = {nullptr, nullptr, nullptr, nullptr};
   bool deblock = false;           // RV_REPLAY_DEBLOCK
   uint8_t *mi_lg = nullptr, *mi_skip = nullptr;  // the deblocking block map
   int mi_stride = 0, mi_cols = 0, mi_rows = 0;
@@ -1257,7 +1259,8 @@ void rv_replay_destroy(rv_replay *r) {
   // stream running)
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->side) (void)hipStreamSynchronize(r->side);
-  if (r->edge) (void)hipStreamSynchronize(r->edge);
+  for (hipStream_t es : r->edge)
+    if (es) (void)hipStreamSynchronize(es);
   for (void *p : r->allocs) (void)hipFree(p);
   if (r->h_cnt) (void)hipHostFree(r->h_cnt);
   for (int f = 0; f < rv_replay::kRing; f++)
@@ -1266,9 +1269,13 @@ void rv_replay_destroy(rv_replay *r) {
   if (r->ev_fork) (void)hipEventDestroy(r->ev_fork);
   if (r->ev_join) (void)hipEventDestroy(r->ev_join);
   if (r->side) (void)hipStreamDestroy(r->side);
-  for (hipEvent_t ev : {r->ev_efork, r->ev_ejoin, r->ev_epart, r->ev_ecommit})
+  for (hipEvent_t ev : {r->ev_efork, r->ev_l1me, r->ev_epart})
     if (ev) (void)hipEventDestroy(ev);
-  if (r->edge) (void)hipStreamDestroy(r->edge);
+  for (int l = 0; l < kLevels; l++) {
+    if (r->ev_ejoin[l]) (void)hipEventDestroy(r->ev_ejoin[l]);
+    if (r->ev_ecommit[l]) (void)hipEventDestroy(r->ev_ecommit[l]);
+    if (r->edge[l]) (void)hipStreamDestroy(r->edge[l]);
+  }
   if (r->own_stream && r->stream) (void)hipStreamDestroy(r->stream);
   delete r;
 }
@@ -1552,12 +1559,15 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     ok = ok && hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking) == hipSuccess &&
          hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&r->ev_join, hipEventDisableTiming) == hipSuccess;
-  if (r->overlap && r->lvl && !r->s6)
-    ok = ok && hipStreamCreateWithFlags(&r->edge, hipStreamNonBlocking) == hipSuccess &&
-         hipEventCreateWithFlags(&r->ev_efork, hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&r->ev_ejoin, hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&r->ev_epart, hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&r->ev_ecommit, hipEventDisableTiming) == hipSuccess;
+  if (r->overlap && r->lvl && !r->s6) {
+    ok = ok && hipEventCreateWithFlags(&r->ev_efork, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&r->ev_l1me, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&r->ev_epart, hipEventDisableTiming) == hipSuccess;
+    for (int l = 1; l < kLevels; l++)
+      ok = ok && hipStreamCreateWithFlags(&r->edge[l], hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev_ejoin[l], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev_ecommit[l], hipEventDisableTiming) == hipSuccess;
+  }
   const size_t ev_bytes = (size_t)rv_replay::kRing * 2 * nr * 4;
   r->ds_evals = (uint32_t *)dalloc(r, ev_bytes);
   ok = ok && r->ds_evals && hipMemsetAsync(r->ds_evals, 0, ev_bytes, r->stream) == hipSuccess;
@@ -1911,9 +1921,10 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     bool armed;
     ~SideJoin() {
       if (armed && r->side) (void)hipStreamSynchronize(r->side);
-      if (armed && r->edge) (void)hipStreamSynchronize(r->edge);
+      for (int l = 1; l < kLevels; l++)
+        if (armed && r->edge[l]) (void)hipStreamSynchronize(r->edge[l]);
     }
-  } side_join{r, r->overlap || r->edge};
+  } side_join{r, r->overlap || r->edge[1]};
   // the candidates' RDO arguments: luma (N = 64, cdef distortion) and both
   // chroma planes (N = 32, SSE) of every candidate
   const int nsingle = g.nsb * g.R * g.M;
@@ -1975,8 +1986,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // use_satd_subpel, src/api/config.rs:429-431; SAD at speed 10), seeded with
   // the pmvs entry: a 32x32 its half-res quadrant search, a 16x16 / 8x8 its
   // 32x32's sub-pel winner
-  auto lv_me = [&](hipStream_t es) -> int {
-    for (int l = 1; l < kLevels; l++) {
+  auto lv_me = [&](hipStream_t es, int only = 0) -> int {
+    for (int l = only ? only : 1; l < (only ? only + 1 : kLevels); l++) {
       if (!r->lv_me[l]) continue;
       rv_replay::PLevel &P = r->pl[l];
       if (l == 1)
@@ -1995,8 +2006,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     return RV_OK;
   };
   // the candidate lists of every used level (single, then compound)
-  auto lv_lists = [&](hipStream_t es, bool comp) {
-    for (int l = 1; l < kLevels; l++) {
+  auto lv_lists = [&](hipStream_t es, bool comp, int only = 0) {
+    for (int l = only ? only : 1; l < (only ? only + 1 : kLevels); l++) {
       if (!r->lv_used[l]) continue;
       rv_replay::PLevel &P = r->pl[l];
       const int ns = P.n * g.R * g.M;
@@ -2013,8 +2024,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   };
   // the single-reference candidates of every used level: luma (cdef
   // distortion) and chroma launches
-  auto lv_rdo = [&](hipStream_t es) -> int {
-    for (int l = 1; l < kLevels; l++) {
+  auto lv_rdo = [&](hipStream_t es, int only = 0) -> int {
+    for (int l = only ? only : 1; l < (only ? only + 1 : kLevels); l++) {
       if (!r->lv_used[l]) continue;
       rv_replay::PLevel &P = r->pl[l];
       CandGeo cgl = P.cg;
@@ -2063,8 +2074,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     return RV_OK;
   };
   // the compound candidates of every used level (all pushed)
-  auto lv_rdo_comp = [&](hipStream_t es) -> int {
-    for (int l = 1; l < kLevels; l++) {
+  auto lv_rdo_comp = [&](hipStream_t es, int only = 0) -> int {
+    for (int l = only ? only : 1; l < (only ? only + 1 : kLevels); l++) {
       if (!r->lv_used[l]) continue;
       const rv_replay::PLevel &P = r->pl[l];
       RdoArgs a = ll[l], c = lc6[l];
@@ -2078,8 +2089,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     return RV_OK;
   };
   // every used level's winners and result words
-  auto lv_score = [&](hipStream_t es) {
-    for (int l = 1; l < kLevels; l++) {
+  auto lv_score = [&](hipStream_t es, int only = 0) {
+    for (int l = only ? only : 1; l < (only ? only + 1 : kLevels); l++) {
       if (!r->lv_used[l]) continue;
       rv_replay::PLevel &P = r->pl[l];
       CandGeo cgl = P.cg;
@@ -2091,8 +2102,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     }
   };
   // the leaves of every used level into the frame
-  auto lv_commit = [&](hipStream_t es) -> int {
-    for (int l = 1; l < kLevels; l++) {
+  auto lv_commit = [&](hipStream_t es, int only = 0) -> int {
+    for (int l = only ? only : 1; l < (only ? only + 1 : kLevels); l++) {
       if (!r->lv_used[l]) continue;
       const rv_replay::PLevel &P = r->pl[l];
       RdoArgs a = ll[l], c = lc6[l];
@@ -2106,20 +2117,32 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     return RV_OK;
   };
   // speed 10: the edge levels on their own stream, forked after F2
-  const bool edge = r->lvl && !r->s6 && r->edge;
+  // one stream per level: the 32x32 searches first (the smaller levels seed
+  // from them), then each level's candidates and scores beside the others'
+  const bool edge = r->lvl && !r->s6 && r->edge[1];
   if (edge) {
     RV_H(hipEventRecord(r->ev_efork, st));
-    RV_H(hipStreamWaitEvent(r->edge, r->ev_efork, 0));
-    hipStream_t es = r->edge;
-    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 2], es));
-    RV_R(lv_me(es));
-    lv_lists(es, false);
-    if (cg.comp) lv_lists(es, true);
-    RV_R(lv_rdo(es));
-    if (cg.comp) RV_R(lv_rdo_comp(es));
-    lv_score(es);
-    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 3], es));
-    RV_H(hipEventRecord(r->ev_ejoin, es));
+    for (int l = 1; l < kLevels; l++) RV_H(hipStreamWaitEvent(r->edge[l], r->ev_efork, 0));
+    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 2], r->edge[1]));
+    RV_R(lv_me(r->edge[1], 1));
+    RV_H(hipEventRecord(r->ev_l1me, r->edge[1]));
+    for (int l = 1; l < kLevels; l++) {
+      hipStream_t es = r->edge[l];
+      if (l > 1 && r->lv_me[l]) {
+        RV_H(hipStreamWaitEvent(es, r->ev_l1me, 0));
+        RV_R(lv_me(es, l));
+      }
+      if (!r->lv_used[l]) continue;
+      lv_lists(es, false, l);
+      if (cg.comp) lv_lists(es, true, l);
+      RV_R(lv_rdo(es, l));
+      if (cg.comp) RV_R(lv_rdo_comp(es, l));
+      lv_score(es, l);
+      RV_H(hipEventRecord(r->ev_ejoin[l], es));
+    }
+    for (int l = 2; l < kLevels; l++)
+      if (r->lv_used[l]) RV_H(hipStreamWaitEvent(r->edge[1], r->ev_ejoin[l], 0));
+    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 3], r->edge[1]));
   } else if (tm) {  // no edge stream: an empty span
     RV_H(hipEventRecord(e[rv_replay::kStageEv + 2], st));
     RV_H(hipEventRecord(e[rv_replay::kStageEv + 3], st));
@@ -2171,9 +2194,10 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                                      r->cand_evals + 2 * slot * kLevels,
                                                      r->leaf_count);
   if (r->lvl) {
-    if (edge)
-      RV_H(hipStreamWaitEvent(st, r->ev_ejoin, 0));  // the levels' winners
-    else
+    if (edge) {  // the levels' winners
+      for (int l = 1; l < kLevels; l++)
+        if (r->lv_used[l]) RV_H(hipStreamWaitEvent(st, r->ev_ejoin[l], 0));
+    } else
       lv_score(st);
     PartArgs pa;
     memset(&pa, 0, sizeof(pa));
@@ -2199,9 +2223,12 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // the edge stream, beside the superblocks' commit)
   if (edge) {
     RV_H(hipEventRecord(r->ev_epart, st));
-    RV_H(hipStreamWaitEvent(r->edge, r->ev_epart, 0));
-    RV_R(lv_commit(r->edge));
-    RV_H(hipEventRecord(r->ev_ecommit, r->edge));
+    for (int l = 1; l < kLevels; l++) {
+      if (!r->lv_used[l]) continue;
+      RV_H(hipStreamWaitEvent(r->edge[l], r->ev_epart, 0));
+      RV_R(lv_commit(r->edge[l], l));
+      RV_H(hipEventRecord(r->ev_ecommit[l], r->edge[l]));
+    }
   }
   la.commit = ca.commit = 1;
   la.list = ca.list = r->lvl ? r->pl[0].leaf : nullptr;  // with levels: the unsplit superblocks
@@ -2211,7 +2238,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   la.ntx_per_cand = 1;
   RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
   if (r->lvl && !edge) RV_R(lv_commit(st));
-  if (edge) RV_H(hipStreamWaitEvent(st, r->ev_ecommit, 0));
+  for (int l = 1; edge && l < kLevels; l++)
+    if (r->lv_used[l]) RV_H(hipStreamWaitEvent(st, r->ev_ecommit[l], 0));
   side_join.armed = false;  // both side streams have joined the main one
   RV_EV(10);
   // F6b intra-mode screening + intra RDO of the non-skip superblocks
