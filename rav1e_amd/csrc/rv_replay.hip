@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64) void score_candidates(
     evals[0] = (uint32_t)cand_count[0];  // single-reference candidates evaluated
     evals[1] = (uint32_t)cand_count[1];  // compound ones
     cand_count[0] = cand_count[1] = 0;
-    *imp_sum = 0;
+    if (imp_sum) *imp_sum = 0;  // null: F5 ran on the side stream (it zeroed its sum)
     if (leaf_count)  // speed 6: the partition decision appends next
       for (int l = 0; l < 4; l++) leaf_count[l] = 0;
   }
@@ -1891,6 +1891,19 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   RV_R(rv_diamond_search_multi(&S.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
                                g.bd, r->half, nullptr, nullptr, st));
   RV_EV(3);
+  // F5: the 8x8 importance SATD against reference 0's original frame at the
+  // lookahead MVs (only FL's output: on the side stream after FL when it
+  // overlaps, zeroing its own sum)
+  auto f5_importance = [&](hipStream_t fs) -> int {
+    const unsigned nb = (unsigned)((r->n_imp + 255) / 256);
+    if (g.hbd)
+      importance_kernel<uint16_t><<<nb, 256, 0, fs>>>(g, cur.y, refs_o[0], r->look, r->imp_bx,
+                                                      r->imp_by, r->tail + 2);
+    else
+      importance_kernel<uint8_t><<<nb, 256, 0, fs>>>(g, cur.y, refs_o[0], r->look, r->imp_bx,
+                                                     r->imp_by, r->tail + 2);
+    return RV_OK;
+  };
   // FL the lookahead's build_full_res_pmvs (compute_lookahead_motion_vectors,
   // src/api/internal.rs:514-622): 16x16 full-pel searches against the
   // references' original frames; its coarse and half-res stages are F1 / F2
@@ -1908,6 +1921,10 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                                         r->coarse, r->half, 0);
     RV_R(rv_diamond_search_multi(&cur.y, refs_o, g.R, r->jobs_look[lv], nr * 16, 16, 16, 0, 0,
                                  0, g.bd, r->look, nullptr, nullptr, ls));
+    if (r->overlap) {
+      RV_H(hipMemsetAsync(r->tail + 2, 0, 8, ls));
+      RV_R(f5_importance(ls));
+    }
     if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 1], ls));
     if (r->overlap) RV_H(hipEventRecord(r->ev_join, ls));
   }
@@ -2190,7 +2207,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                                      r->c_out, r->c_out + nct * 3, ntx_c, r->win,
                                                      r->coarse, r->half, r->full, r->look,
                                                      r->words,
-                                                     r->cand_count, r->tail + 2,
+                                                     r->cand_count,
+                                                     r->overlap ? nullptr : r->tail + 2,
                                                      r->cand_evals + 2 * slot * kLevels,
                                                      r->leaf_count);
   if (r->lvl) {
@@ -2245,16 +2263,9 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // F6b intra-mode screening + intra RDO of the non-skip superblocks
   if (r->intra) RV_R(intra_pass(r, la, ca, cur, S, L, slot));
   RV_EV(11);
-  // F5 importance SATD against reference 0 (the sum was zeroed by the argmin)
-  {
-    const unsigned nb = (unsigned)((r->n_imp + 255) / 256);
-    if (g.hbd)
-      importance_kernel<uint16_t><<<nb, 256, 0, st>>>(g, cur.y, refs_o[0], r->look, r->imp_bx,
-                                                      r->imp_by, r->tail + 2);
-    else
-      importance_kernel<uint8_t><<<nb, 256, 0, st>>>(g, cur.y, refs_o[0], r->look, r->imp_bx,
-                                                     r->imp_by, r->tail + 2);
-  }
+  // F5 importance SATD against reference 0 (the sum was zeroed by the argmin;
+  // with the side stream F5 ran there, after the lookahead)
+  if (!r->overlap) RV_R(f5_importance(st));
   RV_EV(12);
   // F7 deblock_filter_frame (src/encoder.rs:2789-2793) when enabled: the
   // block map of the committed blocks, then (once every group's pixels and
