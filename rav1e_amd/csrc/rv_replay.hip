@@ -608,6 +608,7 @@ struct rv_replay {
   // stream (A/B).
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_ielig = nullptr;  // intra_begin's count is on the host
   bool overlap = false;
   bool own_stream;
   bool sea;  // successive-elimination coarse search (bit depth <= 10)
@@ -1144,16 +1145,27 @@ void frame_info(long n, int R, rv_replay_frame_info *f) {
 // F6b: rdo_mode_decision's intra-mode screening and intra RDO of every
 // superblock whose inter winner is not skip (rv_intra_pass.hip), round by
 // round until no decision changes.  la / ca: the F6 commit arguments.
+// The eligible superblocks (they need only the inter winners): queued right
+// after the argmin, so the host's read of their count completes while the
+// commit (F6) runs instead of draining the stream.
+static int intra_begin(rv_replay *r) {
+  const Geo &g = r->g;
+  hipStream_t st = r->stream;
+  const IntraGeo ig{g.W, g.H, g.bd, g.nsb, g.tw, g.tx0, g.ty0, g.tws, g.ths};
+  RV_H(hipMemsetAsync(r->i_cnt, 0, 4 * sizeof(int32_t), st));
+  RV_R(rv_intra_elig(ig, r->win, r->i_elig, r->i_was, r->i_mark, r->i_list[0], r->i_cnt, st));
+  RV_H(hipMemcpyAsync(r->h_cnt, r->i_cnt, 4, hipMemcpyDeviceToHost, st));
+  RV_H(hipEventRecord(r->ev_ielig, st));
+  return RV_OK;
+}
+
 static int intra_pass(rv_replay *r, const RdoArgs &la, const RdoArgs &ca, const RvInput &cur,
                       const RvSlot &S, const rv_replay::Level &L, int slot) {
   const Geo &g = r->g;
   hipStream_t st = r->stream;
   const IntraGeo ig{g.W, g.H, g.bd, g.nsb, g.tw, g.tx0, g.ty0, g.tws, g.ths};
   uint32_t *stats = r->i_stats + (size_t)slot * 3;
-  RV_H(hipMemsetAsync(r->i_cnt, 0, 4 * sizeof(int32_t), st));
-  RV_R(rv_intra_elig(ig, r->win, r->i_elig, r->i_was, r->i_mark, r->i_list[0], r->i_cnt, st));
-  RV_H(hipMemcpyAsync(r->h_cnt, r->i_cnt, 4, hipMemcpyDeviceToHost, st));
-  RV_H(hipStreamSynchronize(st));
+  RV_H(hipEventSynchronize(r->ev_ielig));  // intra_begin's count
   int n = *r->h_cnt, round = 0;
   // the rounds are bounded by the longest dependency chain of a tile (its
   // anti-diagonals: right, below-left)
@@ -1268,6 +1280,7 @@ void rv_replay_destroy(rv_replay *r) {
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
   if (r->ev_fork) (void)hipEventDestroy(r->ev_fork);
   if (r->ev_join) (void)hipEventDestroy(r->ev_join);
+  if (r->ev_ielig) (void)hipEventDestroy(r->ev_ielig);
   if (r->side) (void)hipStreamDestroy(r->side);
   for (hipEvent_t ev : {r->ev_efork, r->ev_l1me, r->ev_epart})
     if (ev) (void)hipEventDestroy(ev);
@@ -1498,7 +1511,8 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     r->i_cout = (uint64_t *)dalloc(r, n * 6 * 3 * 8 * 2);
     ok = ok && r->i_elig && r->i_was && r->i_win && r->i_modes && r->i_mark && r->i_list[0] &&
          r->i_list[1] && r->i_commit && r->i_revert && r->i_cnt && r->i_edges && r->i_lout &&
-         r->i_cout && hipHostMalloc((void **)&r->h_cnt, 16, hipHostMallocDefault) == hipSuccess;
+         r->i_cout && hipHostMalloc((void **)&r->h_cnt, 16, hipHostMallocDefault) == hipSuccess &&
+         hipEventCreateWithFlags(&r->ev_ielig, hipEventDisableTiming) == hipSuccess;
     if (r->i_was) (void)hipMemsetAsync(r->i_was, 0, n, r->stream);
     if (r->i_win) (void)hipMemsetAsync(r->i_win, 0, 2 * n, r->stream);
   }
@@ -2236,6 +2250,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     pa.words = r->words + r->wpart;
     partition_kernel<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, pa);
   }
+  if (r->intra) RV_R(intra_begin(r));
   RV_EV(9);
   // F6 commit the winners into the frame: the levels' leaves (speed 10: on
   // the edge stream, beside the superblocks' commit)
