@@ -31,6 +31,10 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# Hardware queues per process (HIP's default 4): one GPU's replay runs up to
+# six streams (two instances x main / lookahead / frame-edge levels); more
+# streams than queues get multiplexed onto them.  Set before HIP initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 sys.path.insert(0, ROOT)
 
 # name: (width, height, xdec, ydec, bit_depth, tiling kwargs, BASELINE config, speed)

@@ -1287,7 +1287,7 @@ void rv_replay_destroy(rv_replay *r) {
   for (int l = 0; l < kLevels; l++) {
     if (r->ev_ejoin[l]) (void)hipEventDestroy(r->ev_ejoin[l]);
     if (r->ev_ecommit[l]) (void)hipEventDestroy(r->ev_ecommit[l]);
-    if (r->edge[l]) (void)hipStreamDestroy(r->edge[l]);
+    if (r->edge[l] && (l <= 1 || r->edge[l] != r->edge[1])) (void)hipStreamDestroy(r->edge[l]);
   }
   if (r->own_stream && r->stream) (void)hipStreamDestroy(r->stream);
   delete r;
@@ -1577,10 +1577,19 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     ok = ok && hipEventCreateWithFlags(&r->ev_efork, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&r->ev_l1me, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&r->ev_epart, hipEventDisableTiming) == hipSuccess;
-    for (int l = 1; l < kLevels; l++)
-      ok = ok && hipStreamCreateWithFlags(&r->edge[l], hipStreamNonBlocking) == hipSuccess &&
-           hipEventCreateWithFlags(&r->ev_ejoin[l], hipEventDisableTiming) == hipSuccess &&
+    // RAV1E_HIP_EDGE_STREAMS=3: one stream per level; default one stream for
+    // all levels (in order) -- every stream beyond the hardware queues
+    // (GPU_MAX_HW_QUEUES) is multiplexed onto them
+    const char *es = getenv("RAV1E_HIP_EDGE_STREAMS");
+    const bool per_level = es && es[0] == '3';
+    for (int l = 1; l < kLevels; l++) {
+      if (l == 1 || per_level)
+        ok = ok && hipStreamCreateWithFlags(&r->edge[l], hipStreamNonBlocking) == hipSuccess;
+      else
+        r->edge[l] = r->edge[1];  // an alias (destroyed once)
+      ok = ok && hipEventCreateWithFlags(&r->ev_ejoin[l], hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&r->ev_ecommit[l], hipEventDisableTiming) == hipSuccess;
+    }
   }
   const size_t ev_bytes = (size_t)rv_replay::kRing * 2 * nr * 4;
   r->ds_evals = (uint32_t *)dalloc(r, ev_bytes);
