@@ -223,6 +223,70 @@ void orc_plane_pad(void *data, int stride, int alloc_height, int xorigin,
 void orc_downsample(void *dst, ptrdiff_t dst_stride, int dst_w, int dst_h,
                     const void *src, ptrdiff_t src_stride, int hbd);
 
+
+/* ---- entropy coding (src/ec.rs, src/context.rs) --------------------- */
+/* WriterBase<WriterEncoder> (src/ec.rs:100-600) */
+typedef struct {
+  uint16_t rng;
+  int16_t cnt;
+  uint32_t low;        /* ec_window */
+  uint16_t *pre;       /* precarry */
+  size_t n, cap;
+} orc_ecw;
+/* the Reader of src/ec.rs's test module (:914-1010) */
+typedef struct {
+  const uint8_t *buf;
+  size_t len, bptr;
+  uint32_t dif;
+  uint16_t rng;
+  int16_t cnt;
+} orc_ecr;
+/* the coefficient CDFs of CDFContext (flat, orc_ec_tables.h layout) and
+ * BlockContext's above / left coefficient contexts */
+#define ORC_EC_CDF_TOTAL 4317
+typedef struct {
+  uint16_t cdf[ORC_EC_CDF_TOTAL];
+  uint8_t above[3][1024];  /* COEFF_CONTEXT_MAX_WIDTH */
+  uint8_t left[3][16];     /* MIB_SIZE */
+} orc_ec_ctx;
+/* one step of a tile's coefficient coding (orc_ec_code_jobs) */
+typedef struct {
+  int32_t kind;       /* 0 tx block, 1 skip leaf, 2 superblock row, 3 new tile */
+  int32_t plane;
+  int32_t bx, by;     /* TileBlockOffset (luma 4x4 units) */
+  int32_t tx_size;    /* TX_4X4 .. TX_64X64 (square) */
+  int32_t tx_type;
+  int32_t is_inter;
+  int32_t bw_lg, bh_lg;  /* tx job: plane block log2 w / h; skip job: the leaf's (luma) */
+  int32_t coeff_off;
+} orc_ec_job;
+void orc_ecw_init(orc_ecw *w);
+void orc_ecw_free(orc_ecw *w);
+void orc_ecw_symbol(orc_ecw *w, uint32_t s, const uint16_t *cdf, int n);
+void orc_update_cdf(uint16_t *cdf, int len, uint32_t val);
+void orc_ecw_symbol_update(orc_ecw *w, uint32_t s, uint16_t *cdf, int len);
+void orc_ecw_bool(orc_ecw *w, int val, uint16_t f);
+void orc_ecw_bit(orc_ecw *w, int bit);
+void orc_ecw_literal(orc_ecw *w, int bits, uint32_t s);
+void orc_ecw_golomb(orc_ecw *w, uint16_t level);
+size_t orc_ecw_finish(orc_ecw *w);
+void orc_ecw_bytes(const orc_ecw *w, uint8_t *out);
+size_t orc_ecw_done(orc_ecw *w, uint8_t *out, size_t cap);
+void orc_ecr_init(orc_ecr *r, const uint8_t *buf, size_t len);
+int orc_ecr_bool(orc_ecr *r, uint32_t f);
+int orc_ecr_symbol(orc_ecr *r, const uint16_t *icdf, int n_entries);
+void orc_ec_ctx_init(orc_ec_ctx *c, int qctx);
+void orc_ec_reset_counts(uint16_t *cdf);
+void orc_ec_reset_skip(orc_ec_ctx *c, int bx, int by, int bw_lg, int bh_lg, int xdec, int ydec);
+void orc_ec_reset_left(orc_ec_ctx *c);
+int orc_ec_write_coeffs(orc_ecw *w, orc_ec_ctx *cx, int plane, int bx, int by,
+                        const int32_t *coeffs_in, int is_inter, int tx, int tx_type,
+                        int plane_lg, int xdec, int ydec, int reduced, uint8_t *cul_out);
+long orc_ec_code_jobs(const orc_ec_job *jobs, int n, const int32_t *coeffs, const uint16_t *cdf_init,
+                      int xdec, int ydec, uint8_t *out, long cap, int32_t *tile_bytes,
+                      uint16_t *ret, uint16_t *cdf_out);
+const uint16_t *orc_ec_default_cdf(int qctx);
+
 #ifdef __cplusplus
 }
 #endif

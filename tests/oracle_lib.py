@@ -625,3 +625,115 @@ class CpuReplay:
 
     def __del__(self):
         self.close()
+
+
+# ---------------------------------------------------------------- entropy coder
+EC_CDF_TOTAL = 4317  # oracle/orc_ec_tables.h ORC_EC_TOTAL
+EC_JOB = np.dtype([(n, np.int32) for n in ("kind", "plane", "bx", "by", "tx_size", "tx_type",
+                                            "is_inter", "bw_lg", "bh_lg", "coeff_off")])
+
+
+def ec_lib():
+    """The oracle's range coder / coefficient coder (oracle/orc_ec.c)."""
+    L = lib()
+    if not getattr(L, "_ec_ready", False):
+        vp, i32 = C.c_void_p, C.c_int
+        for n, a in (("orc_ecw_init", [vp]), ("orc_ecw_free", [vp]),
+                     ("orc_ecw_symbol_update", [vp, C.c_uint32, vp, i32]),
+                     ("orc_ecw_bool", [vp, i32, C.c_uint16]), ("orc_ecw_bit", [vp, i32]),
+                     ("orc_ecw_literal", [vp, i32, C.c_uint32]),
+                     ("orc_ecw_golomb", [vp, C.c_uint16]), ("orc_ecw_bytes", [vp, vp]),
+                     ("orc_ecr_init", [vp, vp, C.c_size_t]),
+                     ("orc_ec_reset_counts", [vp])):
+            getattr(L, n).argtypes = a
+            getattr(L, n).restype = None
+        L.orc_ecw_finish.argtypes = [vp]
+        L.orc_ecw_finish.restype = C.c_size_t
+        L.orc_ecr_bool.argtypes = [vp, C.c_uint32]
+        L.orc_ecr_bool.restype = i32
+        L.orc_ecr_symbol.argtypes = [vp, vp, i32]
+        L.orc_ecr_symbol.restype = i32
+        L.orc_ec_default_cdf.argtypes = [i32]
+        L.orc_ec_default_cdf.restype = C.POINTER(C.c_uint16)
+        L.orc_ec_code_jobs.argtypes = [vp, i32, vp, vp, i32, i32, vp, C.c_long, vp, vp, vp]
+        L.orc_ec_code_jobs.restype = C.c_long
+        L._ec_ready = True
+    return L
+
+
+def ec_default_cdf(qctx):
+    L = ec_lib()
+    p = L.orc_ec_default_cdf(qctx)
+    return np.ctypeslib.as_array(p, (EC_CDF_TOTAL,)).copy()
+
+
+class EcWriter:
+    """orc_ecw (WriterBase<WriterEncoder>) behind ctypes."""
+
+    def __init__(self):
+        self.L = ec_lib()
+        self.buf = C.create_string_buffer(64)
+        self.L.orc_ecw_init(self.buf)
+
+    def symbol_update(self, s, cdf, off, n):
+        arr = cdf[off:off + n]  # a view: update_cdf writes through
+        self.L.orc_ecw_symbol_update(self.buf, s, arr.ctypes.data, n)
+
+    def bool(self, v, f):
+        self.L.orc_ecw_bool(self.buf, int(v), int(f))
+
+    def bit(self, b):
+        self.L.orc_ecw_bit(self.buf, int(b))
+
+    def literal(self, nb, v):
+        self.L.orc_ecw_literal(self.buf, int(nb), int(v))
+
+    def golomb(self, v):
+        self.L.orc_ecw_golomb(self.buf, int(v))
+
+    def done(self):
+        n = self.L.orc_ecw_finish(self.buf)
+        out = np.zeros(n, np.uint8)
+        self.L.orc_ecw_bytes(self.buf, out.ctypes.data)
+        self.L.orc_ecw_free(self.buf)
+        return out
+
+
+def ec_replay_ops(ops):
+    """Replay a gen_ec_ref op stream ((kind, a, b, c, d) rows) through the
+    oracle's writer; returns the bytes."""
+    w = EcWriter()
+    state = {}
+    for k, a, b, c, d in ops:
+        if k == 0:
+            if a not in state:
+                state[a] = ec_default_cdf(int(a))
+            w.symbol_update(int(d), state[a], int(b), int(c))
+        elif k == 1:
+            w.bool(b, a)
+        elif k == 2:
+            w.bit(a)
+        elif k == 3:
+            w.literal(a, b)
+        else:
+            w.golomb(a)
+    return w.done()
+
+
+def ec_code_jobs(jobs, coeffs, cdf_init, xdec, ydec, cap=1 << 24):
+    """orc_ec_code_jobs: (bytes, tile byte counts, per-job returns, final CDFs)."""
+    L = ec_lib()
+    jobs = np.ascontiguousarray(jobs, np.int32)
+    n = jobs.shape[0]
+    coeffs = np.ascontiguousarray(coeffs, np.int32)
+    cdf_init = np.ascontiguousarray(cdf_init, np.uint16)
+    out = np.zeros(cap, np.uint8)
+    ntiles = int((jobs[:, 0] == 3).sum()) + 1
+    tb = np.zeros(ntiles, np.int32)
+    ret = np.zeros(n, np.uint16)
+    fin = np.zeros(EC_CDF_TOTAL, np.uint16)
+    total = L.orc_ec_code_jobs(jobs.ctypes.data, n, coeffs.ctypes.data, cdf_init.ctypes.data,
+                               xdec, ydec, out.ctypes.data, cap, tb.ctypes.data, ret.ctypes.data,
+                               fin.ctypes.data)
+    assert total >= 0, total
+    return out[:total].copy(), tb, ret, fin

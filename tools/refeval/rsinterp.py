@@ -1104,6 +1104,10 @@ class Interp:
             if len(args) != len(params):
                 raise TypeError("%s takes %d args, got %d" % (name, len(params), len(args)))
             for (pat, ty), a in zip(params, args):
+                if ty is not None and ty[0] == "ref" and pat[0] == "bind" and \
+                        isinstance(deref(a), Struct):
+                    fenv.vars[pat[1]] = deref(a)  # `&` / `&mut` parameter: the caller's value
+                    continue
                 tn = type_name(ty)
                 a = deref(a) if (tn in INT_BITS or tn in FLOATS) else a
                 if tn in INT_BITS and isinstance(a, int) and not isinstance(a, bool):
@@ -1632,6 +1636,9 @@ class Interp:
             raise RuntimeError("reference %s!() reached" % name)
         if name in ("eprintln", "println", "format"):
             return ""
+        host = getattr(self, "macros", {}).get(name)
+        if host is not None:  # a macro the generator supplies (its expansion restated)
+            return host(self, self._macro_args(toks), env)
         raise NotImplementedError("macro %s!" % name)
 
     def _macro_args(self, toks):
