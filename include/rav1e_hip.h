@@ -362,6 +362,52 @@ int rv_cdef_filter_plane(const rv_plane *src, const rv_plane *dst, int pli, int 
                          const uint8_t *y_strengths, const uint8_t *uv_strengths, int damping,
                          int bit_depth, void *stream);
 
+/* ---- entropy coding (src/ec.rs, src/context.rs) -------------------------
+ * Coefficient coding = ContextWriter::write_coeffs_lv_map (src/context.rs:
+ * 3965-4220) for square transforms (TX_4X4 .. TX_64X64, the sizes the
+ * replay codes), split into a device tokenizer and the host range coder.
+ *
+ * rv_ec_job: one step of a tile's coding, in coding order (the shape of
+ * encode_tile's superblock loop, src/encoder.rs:3160-3340, down to
+ * write_tx_tree / write_tx_blocks, :1757-2030):
+ *   kind 0 a transform block: write_coeffs_lv_map(plane, bo = (bx, by),
+ *          coeffs, is_inter ? NEARESTMV : DC_PRED, tx_size, tx_type,
+ *          plane_bsize = (1 << bw_lg) x (1 << bh_lg), xdec, ydec,
+ *          reduced tx set); coeffs = the quantised coefficients, raster of the
+ *          coded size (min(w, 32) square), device pointer;
+ *   kind 1 a skip leaf of (1 << bw_lg) x (1 << bh_lg) luma pixels at (bx, by):
+ *          reset_skip_context (:1651-1679);
+ *   kind 2 a superblock row starts: reset_left_contexts;
+ *   kind 3 a tile starts (a fresh BlockContext; its own range coder).
+ * (bx, by) are TileBlockOffsets: luma 4x4 units relative to the tile.
+ * `tile` indexes the tile's context map (jobs of a tile share it). */
+typedef struct rv_ec_job {
+  int32_t kind, plane, bx, by, tx_size, tx_type, is_inter, bw_lg, bh_lg, tile;
+  const int32_t *coeffs;
+} rv_ec_job;
+/* rv_ec_tokenize: the symbols of every kind-0 job.  Device buffers: d_map
+ * n_tiles * 3 * map_w4 * map_h4 bytes (cleared here; map_w4 / map_h4 >= the
+ * largest tile in luma 4x4 units), d_scratch rv_ec_scratch_bytes(n) bytes,
+ * d_offsets n + 1 u32 (job j's tokens start at d_offsets[j]; [n] = total),
+ * d_tokens token_cap u32, d_status 2 u32 ([0] total tokens, [1] 1 if the
+ * total exceeded token_cap: tokens past it were dropped).  Token format in
+ * rav1e_amd/csrc/rv_ec.hip.  Returns 0 or an error (n <= 2^20). */
+size_t rv_ec_scratch_bytes(int n_jobs);
+int rv_ec_tokenize(const rv_ec_job *d_jobs, int n, int xdec, int ydec, int n_tiles, int map_w4,
+                   int map_h4, uint8_t *d_map, void *d_scratch, uint32_t *d_offsets,
+                   uint32_t *d_tokens, uint32_t token_cap, uint32_t *d_status, void *stream);
+/* rv_ec_code_tokens (host): one tile's tokens through WriterBase<
+ * WriterEncoder> (symbol_with_update on cdf, which adapts; Writer::bit),
+ * then done(): returns the byte count, the bytes go to out if they fit in
+ * cap.  cdf: the tile's CDFs (rv_ec_cdf_total() u16, updated in place). */
+long rv_ec_code_tokens(const uint32_t *tokens, size_t n, uint16_t *cdf, uint8_t *out, size_t cap);
+/* CDFContext::new(quantizer) coefficient CDFs for q context qctx 0..3
+ * (src/context.rs:793-850: base_q_idx <= 20, <= 60, <= 120, else 3) and
+ * CDFContext::reset_counts (:851-) over them. */
+int rv_ec_cdf_total(void);
+int rv_ec_default_cdf(int qctx, uint16_t *out);
+void rv_ec_reset_counts(uint16_t *cdf);
+
 /* dc_q / ac_q lookups (src/quantize.rs:42-62) on the host: ac = 0 for
  * dc_qlookup*_Q3, 1 for ac_qlookup*_Q3; -1 on bad arguments. */
 int rv_q_lookup(int ac, int qindex, int bit_depth);

@@ -299,6 +299,13 @@ def _declare(L):
         "rv_tx_dist_batch": (i32, [vp, i32, vp, i32, i32, vp, vp]),
         "rav1e_fwd_txfm_hip": (i32, [vp, vp, i32, i32, i32]),
         "rav1e_inv_txfm_add_hip": (i32, [vp, vp, C.c_ssize_t, i32, i32, i32]),
+        "rv_ec_scratch_bytes": (C.c_size_t, [i32]),
+        "rv_ec_tokenize": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, C.c_uint32, vp,
+                                 vp]),
+        "rv_ec_code_tokens": (C.c_long, [vp, C.c_size_t, vp, vp, C.c_size_t]),
+        "rv_ec_cdf_total": (i32, []),
+        "rv_ec_default_cdf": (i32, [i32, vp]),
+        "rv_ec_reset_counts": (None, [vp]),
         "rv_sad_fn": (vp, [i32, i32, i32]),
         "rv_satd_fn": (vp, [i32, i32, i32]),
         "rv_put_fn_get": (vp, [i32, i32, i32]),
@@ -660,6 +667,88 @@ def cdef_filter_frame(src, dst, width, height, skip: np.ndarray, cdef_index: np.
     _sync(stream)
     return (dd.download(np.uint8).reshape(rows8, cols8),
             dv.download(np.int32).reshape(rows8, cols8))
+
+
+# ---- entropy coding (src/ec.rs, src/context.rs write_coeffs_lv_map) --------
+EC_JOB = np.dtype({"names": ["kind", "plane", "bx", "by", "tx_size", "tx_type", "is_inter",
+                             "bw_lg", "bh_lg", "tile", "coeffs"],
+                   "formats": [np.int32] * 10 + [np.uint64],
+                   "offsets": [4 * i for i in range(10)] + [40], "itemsize": 48})
+
+
+def ec_default_cdf(qctx):
+    """CDFContext::new's coefficient CDFs for q context qctx (flat u16)."""
+    out = np.zeros(lib().rv_ec_cdf_total(), np.uint16)
+    _check(lib().rv_ec_default_cdf(qctx, out.ctypes.data), "rv_ec_default_cdf")
+    return out
+
+
+def ec_code_tokens(tokens, cdf):
+    """One tile's tokens through the host range coder; cdf adapts in place."""
+    tokens = np.ascontiguousarray(tokens, np.uint32)
+    out = np.zeros(tokens.size // 2 + 4096, np.uint8)  # > 2 bytes per token never happens
+    c2 = cdf.copy()
+    n = lib().rv_ec_code_tokens(tokens.ctypes.data, tokens.size, c2.ctypes.data, out.ctypes.data,
+                                out.size)
+    if n < 0:
+        _check(int(n), "rv_ec_code_tokens")
+    if n > out.size:
+        out = np.zeros(n, np.uint8)
+        c2 = cdf.copy()
+        lib().rv_ec_code_tokens(tokens.ctypes.data, tokens.size, c2.ctypes.data, out.ctypes.data,
+                                out.size)
+    cdf[:] = c2
+    return out[:n]
+
+
+def code_coefficients(jobs, coeffs, cdf_init, xdec, ydec):
+    """A coding-order job sequence (rows kind, plane, bx, by, tx_size, tx_type,
+    is_inter, bw_lg, bh_lg, coeff_off; kind 3 starts a tile) through the
+    device tokenizer and the host range coder: write_coeffs_lv_map of every
+    transform block, reset_skip_context / reset_left_contexts between them.
+    Returns (bytes of all tiles, bytes per tile, the last tile's final CDFs,
+    tokens)."""
+    jobs = np.asarray(jobs, np.int64)
+    n = len(jobs)
+    co = DeviceBuffer.from_array(np.ascontiguousarray(coeffs, np.int32))
+    ej = np.zeros(n, EC_JOB)
+    for k, f in enumerate(["kind", "plane", "bx", "by", "tx_size", "tx_type", "is_inter",
+                           "bw_lg", "bh_lg"]):
+        ej[f] = jobs[:, k]
+    starts = np.nonzero(jobs[:, 0] == 3)[0]
+    if len(starts) == 0 or starts[0] != 0:
+        starts = np.concatenate([[0], starts])
+    tile = np.cumsum(jobs[:, 0] == 3) - 1
+    ej["tile"] = np.maximum(tile, 0)
+    ej["coeffs"] = co.ptr + 4 * jobs[:, 9].astype(np.uint64)
+    ntiles = len(starts)
+    ext = np.where(jobs[:, 0] == 0, 1 << jobs[:, 4], np.where(jobs[:, 0] == 1, 1 << np.maximum(jobs[:, 7] - 2, 0), 0))
+    mw = int(max(1, (jobs[:, 2] + ext).max()))
+    mh = int(max(1, (jobs[:, 3] + ext).max()))
+    dj = DeviceBuffer.from_array(ej)
+    dmap = DeviceBuffer(ntiles * 3 * mw * mh)
+    scr = DeviceBuffer(lib().rv_ec_scratch_bytes(n))
+    doff = DeviceBuffer(4 * (n + 1))
+    cap = int(64 * n + 8 * int(np.asarray(coeffs).size) + 1024)
+    dtok = DeviceBuffer(4 * cap)
+    dst = DeviceBuffer(8)
+    _check(lib().rv_ec_tokenize(dj.ptr, n, xdec, ydec, ntiles, mw, mh, dmap.ptr, scr.ptr, doff.ptr,
+                                dtok.ptr, cap, dst.ptr, None), "rv_ec_tokenize")
+    _sync(None)
+    status = dst.download(np.uint32)
+    if status[1]:
+        raise Rav1eHipError("code_coefficients: token buffer overflow")
+    off = doff.download(np.uint32)[:n + 1]
+    tok = dtok.download(np.uint32)[:int(status[0])]
+    out, tb, cdf = [], [], None
+    for t in range(ntiles):
+        a = int(off[starts[t]])
+        b = int(off[starts[t + 1]]) if t + 1 < ntiles else int(off[n])
+        cdf = np.array(cdf_init, np.uint16)
+        by = ec_code_tokens(tok[a:b], cdf)
+        out.append(by)
+        tb.append(len(by))
+    return np.concatenate(out), np.array(tb, np.int32), cdf, tok
 
 
 def prep_8tap_batch(src: DevicePlane, jobs, w, h, mode_x=0, mode_y=0, bit_depth=8):

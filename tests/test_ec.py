@@ -117,3 +117,109 @@ def test_coefficient_coding_matches_reference(ref):
         np.testing.assert_array_equal(fin, fin_ref[t0 + ntiles - 1])
         b0 += nb
         t0 += ntiles
+
+
+# ------------------------------------------------------------- the product
+def _rand_jobs(rng, xdec, ydec, sbw, sbh, ntiles, vis_w4=None, vis_h4=None, scale=6.0):
+    """A coding-order job list like gen_ec_ref's (quadtree leaves 64..8 in
+    z-order, skip leaves, superblock rows, tiles) with random coefficients."""
+    from tests.test_ec_util import leaves, rand_coeffs
+    vis_w4 = vis_w4 or sbw * 16
+    vis_h4 = vis_h4 or sbh * 16
+    jobs, co = [], []
+    for _ in range(ntiles):
+        jobs.append((3, 0, 0, 0, 0, 0, 0, 0, 0, 0))
+        for sby in range(sbh):
+            jobs.append((2, 0, 0, 0, 0, 0, 0, 0, 0, 0))
+            for sbx in range(sbw):
+                lv = []
+                leaves(rng, sbx * 16, sby * 16, 6, 3, vis_w4, vis_h4, lv)
+                for x4, y4, lg in lv:
+                    if rng.random() < 0.3:
+                        jobs.append((1, 0, x4, y4, 0, 0, 0, lg, lg, 0))
+                        continue
+                    intra = lg == 6 and rng.random() < 0.25
+                    for p in range(3):
+                        xd = xdec if p else 0
+                        plg = lg - xd
+                        tx = min(plg - 2, 4)
+                        n_tx = 1
+                        if p and xdec == 0 and lg == 6:
+                            tx, n_tx = 3, 4
+                        cw = min(4 << tx, 32)
+                        for t in range(n_tx):
+                            bx = x4 + (t % 2) * 8 if n_tx == 4 else x4
+                            by = y4 + (t // 2) * 8 if n_tx == 4 else y4
+                            c = rand_coeffs(rng, cw, scale if p == 0 else scale / 2)
+                            jobs.append((0, p, bx, by, tx, 0, 0 if intra else 1, plg, plg,
+                                         sum(len(x) for x in co)))
+                            co.append(c)
+    return np.array(jobs, np.int64), np.concatenate(co).astype(np.int32)
+
+
+def test_host_range_coder_matches_oracle_writer():
+    """rv_ec_code_tokens (the product's host coder, plain C++ in the HIP
+    library) against the oracle's writer on random symbol / bit streams."""
+    import rav1e_amd as R
+    rng = np.random.default_rng(11)
+    for q in range(4):
+        tok, cdf_o = [], O.ec_default_cdf(q)
+        w = O.EcWriter()
+        fams = [(0, 3, 65), (877, 5, 420), (2977, 5, 210), (399, 12, 4), (195, 6, 4), (4045, 17, 16)]
+        for _ in range(4000):
+            if rng.random() < 0.2:
+                b = int(rng.integers(0, 2))
+                tok.append(0x80000000 | b)
+                w.bit(b)
+                continue
+            off, e, cnt = fams[int(rng.integers(0, len(fams)))]
+            if e == 17:
+                e = 3  # inter_tx_cdf[..][..][..=2]
+            o = off + int(rng.integers(0, cnt)) * (17 if off == 4045 else e)
+            s = int(min(e - 2, rng.geometric(0.4) - 1))
+            tok.append(o | (e << 13) | (s << 18))
+            w.symbol_update(s, cdf_o, o, e)
+        want = w.done()
+        cdf_p = R.ec_default_cdf(q)
+        got = R.ec_code_tokens(np.array(tok, np.uint32), cdf_p)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(cdf_p, cdf_o)
+
+
+@pytest.mark.gpu
+def test_gpu_coefficient_coding_matches_reference(ref):
+    import rav1e_amd as R
+    R.require_device()
+    jobs, co = ref["lv_jobs"], ref["lv_coeffs"]
+    by, tb_ref, fin_ref, init = ref["lv_bytes"], ref["lv_tile_bytes"], ref["lv_final_cdf"], \
+        ref["lv_init_cdf"]
+    b0 = t0 = 0
+    for ci, (cid, j0, nj, xdec, ydec, q, ntiles) in enumerate(ref["lv_cases"]):
+        got, tb, fin, _ = R.code_coefficients(jobs[j0:j0 + nj], co, init[ci], int(xdec), int(ydec))
+        np.testing.assert_array_equal(tb, tb_ref[t0:t0 + ntiles])
+        nb = int(tb_ref[t0:t0 + ntiles].sum())
+        np.testing.assert_array_equal(got, by[b0:b0 + nb])
+        np.testing.assert_array_equal(fin, fin_ref[t0 + ntiles - 1])
+        b0 += nb
+        t0 += ntiles
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("xdec,ydec,sbw,sbh,ntiles,scale", [
+    (1, 1, 6, 4, 3, 6.0), (0, 0, 4, 3, 2, 4.0), (1, 1, 3, 2, 1, 400.0), (1, 1, 8, 2, 2, 0.3)])
+def test_gpu_coefficient_coding_matches_oracle(xdec, ydec, sbw, sbh, ntiles, scale):
+    """Larger tiles (more superblocks, ragged edges, golomb-range and
+    near-empty blocks) through the device tokenizer + host coder against the
+    oracle's sequential write_coeffs_lv_map."""
+    import rav1e_amd as R
+    R.require_device()
+    rng = np.random.default_rng(sbw * 7 + ntiles)
+    jobs, co = _rand_jobs(rng, xdec, ydec, sbw, sbh, ntiles, vis_w4=sbw * 16 - 2,
+                          vis_h4=sbh * 16 - 6, scale=scale)
+    for q in (0, 3):
+        init = O.ec_default_cdf(q)
+        want, tbw, _, finw = O.ec_code_jobs(jobs, co, init, xdec, ydec, cap=1 << 26)
+        got, tb, fin, _ = R.code_coefficients(jobs, co, init, xdec, ydec)
+        np.testing.assert_array_equal(tb, tbw[:ntiles])
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(fin, finw)
