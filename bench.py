@@ -79,14 +79,14 @@ def valu_peak_int():
 STAGES = ["F0_pyramid", "F1_full_search", "F2_half_res_quadrants", "FL_on_main_stream",
           "F3_diamond_fullpel", "F3_diamond_subpel", "F4_rdo_single_ref", "F4_rdo_compound",
           "F4_rd_cost_argmin", "F6_commit", "F6b_intra_screen_rdo", "F5_importance_satd",
-          "F7_pad_exchange", "FL_lookahead_span", "EDGE_levels_span"]
+          "F7_pad_exchange", "FL_lookahead_span", "EDGE_levels_span", "F8_entropy_tokens"]
 # speed 6: the 32x32 / 16x16 / 8x8 searches run inside the sub-pel stage,
 # their candidates inside F4, the partition decision with the argmin
 STAGES6 = ["F0_pyramid", "F1_full_search", "F2_half_res_quadrants", "FL_on_main_stream",
            "F3_diamond_fullpel", "F3_subpel_and_level_me", "F4_rdo_single_ref_all_levels",
            "F4_rdo_compound_all_levels", "F4_argmin_partition", "F6_commit_leaves",
            "F6b_intra_screen_rdo", "F5_importance_satd", "F7_pad_exchange", "FL_lookahead_span",
-           "EDGE_levels_span"]
+           "EDGE_levels_span", "F8_entropy_tokens"]
 
 
 def coarse_windows(W, H, R, scale, tiling, group):

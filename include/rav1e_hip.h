@@ -579,6 +579,15 @@ typedef struct rv_replay_cfg {
  * raster order is reproduced by re-evaluating, round after round, the
  * superblocks whose left / top / top-right / top-left neighbour changed. */
 #define RV_REPLAY_NO_INTRA 64
+/* flags: code the coefficients of every coded frame (stage F8): the
+ * committed transform blocks of each tile in coding order through
+ * write_coeffs_lv_map (src/context.rs:3965) -- tokenized on the device,
+ * range-coded on a host thread beside the next frames (rv_ec_*) -- with the
+ * frame's CDFs from the previous frame of its pyramid level (primary
+ * reference LAST3, src/encoder.rs:776-830, 2750-2761) and the biggest
+ * tile's CDFs kept (:2824-2833).  One tile group (the whole frame), xdec ==
+ * ydec.  rv_replay_entropy_stats reads the result. */
+#define RV_REPLAY_ENTROPY 128
 typedef struct rv_replay_frame_info {
   int32_t display;            /* display index of the coded frame */
   int32_t me_range_scale;     /* 4 >> pyramid level (src/encoder.rs:838) */
@@ -669,6 +678,13 @@ void rv_comm_destroy(void *comm);
  * importance blocks, frame reconstruction sum].
  * Returns the number of u64 written (<= cap). */
 int rv_replay_results(rv_replay *r, uint64_t *host_out, int cap);
+/* RV_REPLAY_ENTROPY: waits for the host coder to finish every frame coded
+ * so far, then out[0..3] = the last frame's coefficient bytes, tiles,
+ * FNV-1a 64 of its tiles' bytes in tile order, frames coded; out[4] =
+ * coefficient bytes summed over every coded frame (cap >= 5).  Returns the
+ * count written, RV_EINVAL without the flag or when a frame's tokens
+ * overflowed the buffer. */
+int rv_replay_entropy_stats(rv_replay *r, uint64_t *out, int cap);
 /* Record the timing events only on frames f with (f / block) % stride == 0
  * (stride 1 = every frame, the default; 0 = never).  Each event record
  * leaves the GPU idle for a few microseconds between kernels, so timed runs

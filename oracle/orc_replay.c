@@ -109,6 +109,12 @@ typedef struct orc_replay {
    * frame */
   int intra;
   uint64_t istat[2];
+  /* coefficient entropy coding of every coded frame (orc_replay_set_entropy):
+   * the CDFs each pyramid level's next frame starts from (NULL: the key
+   * frame's, stood in for by CDFContext::new), the last frame's stats */
+  int entropy;
+  uint16_t *ec_chain[3];
+  uint64_t ec_stat[4];
   pthread_mutex_t mu;
   int next_sb, pass, sb_limit;
 } orc_replay;
@@ -381,6 +387,7 @@ void orc_replay_destroy(orc_replay *r) {
   free_levels(r);
   free(r->mi_lg);
   free(r->mi_skip);
+  for (int l = 0; l < 3; l++) free(r->ec_chain[l]);
   pthread_mutex_destroy(&r->mu);
   free(r);
 }
@@ -1526,6 +1533,169 @@ int orc_replay_set_intra(orc_replay *r, int on) {
   return r->intra == (on != 0) ? 0 : -1;
 }
 
+/* ---- coefficient entropy coding of the committed frame ------------------
+ * encode_tile's superblock loop (src/encoder.rs:3160-3340) down to the
+ * transform blocks (write_tx_tree for inter leaves, :1907-2030;
+ * write_tx_blocks for the intra superblocks, :1757-1906), coefficient
+ * syntax only: per tile, a fresh BlockContext and range coder from the
+ * frame's initial CDFs; reset_left_contexts at every superblock row; per
+ * superblock the committed partition's leaves in z-order
+ * (encode_partition_topdown, :2392-2470); a skip leaf resets its coefficient
+ * contexts (encode_block_post_cdef, :1499-1501), a coded leaf writes its
+ * luma block, then U, then V (write_coeffs_lv_map, src/context.rs:3965).
+ * The frame's CDFs: get_initial_cdfcontext (:2750-2761) -- the primary
+ * reference LAST3 is the previous frame of the same pyramid level
+ * (:776-830) -- and the biggest tile's CDFs with reset_counts
+ * (:2824-2833; Iterator::max_by_key keeps the last maximum). */
+typedef struct {
+  orc_ec_job *j;
+  int32_t *c;
+  size_t nj, cj, nc, cc;
+} ec_list;
+
+static void ec_push(ec_list *L, orc_ec_job jb, const int32_t *co, int n) {
+  if (L->nj == L->cj) {
+    L->cj = L->cj ? 2 * L->cj : 1024;
+    L->j = realloc(L->j, L->cj * sizeof(orc_ec_job));
+  }
+  if (co) {
+    if (L->nc + (size_t)n > L->cc) {
+      while (L->nc + (size_t)n > L->cc) L->cc = L->cc ? 2 * L->cc : 65536;
+      L->c = realloc(L->c, L->cc * 4);
+    }
+    jb.coeff_off = (int32_t)L->nc;
+    memcpy(L->c + L->nc, co, (size_t)n * 4);
+    L->nc += (size_t)n;
+  }
+  L->j[L->nj++] = jb;
+}
+
+/* the committed levels of a leaf of log2 size lg at luma 4x4 (x4, y4) of the
+ * frame: plane p's coefficients of chroma transform t */
+static const int32_t *ec_coeffs(const orc_replay *r, int lg, int x4, int y4, int p, int t) {
+  const int l = 6 - lg;
+  if (l == 0) {
+    const int sb = (y4 / 16 - r->ty0) * r->tw + (x4 / 16 - r->tx0);
+    const int32_t *b = r->lev + (size_t)sb * (1024 + 2 * r->ntx_c * 1024);
+    return p == 0 ? b : b + 1024 + ((size_t)(p - 1) * r->ntx_c + t) * 1024;
+  }
+  const struct olevel *P = &r->pl[l];
+  const int n4 = 16 >> l;
+  const int bi = (y4 / n4 - P->ty0) * P->gw + (x4 / n4 - P->tx0);
+  const size_t per = (size_t)P->B * P->B + 2 * (size_t)P->bc * P->bch;
+  const int32_t *b = P->lev + (size_t)bi * per;
+  return p == 0 ? b : b + (size_t)P->B * P->B + (size_t)(p - 1) * P->bc * P->bch;
+}
+
+static void ec_walk(const orc_replay *r, ec_list *L, int x4, int y4, int lg, int t0x4, int t0y4) {
+  if (x4 >= r->mi_cols || y4 >= r->mi_rows) return;
+  const int code = r->mi_lg[(size_t)y4 * r->mi_cols + x4];
+  if (code != lg - 2) {
+    const int h = 1 << (lg - 3);
+    ec_walk(r, L, x4, y4, lg - 1, t0x4, t0y4);
+    ec_walk(r, L, x4 + h, y4, lg - 1, t0x4, t0y4);
+    ec_walk(r, L, x4, y4 + h, lg - 1, t0x4, t0y4);
+    ec_walk(r, L, x4 + h, y4 + h, lg - 1, t0x4, t0y4);
+    return;
+  }
+  const int bx = x4 - t0x4, by = y4 - t0y4;
+  if (r->mi_skip[(size_t)y4 * r->mi_cols + x4]) {
+    orc_ec_job jb = {1, 0, bx, by, 0, 0, 0, lg, lg, 0};
+    ec_push(L, jb, NULL, 0);
+    return;
+  }
+  int inter = 1;
+  if (lg == 6) {
+    const int sb = (y4 / 16 - r->ty0) * r->tw + (x4 / 16 - r->tx0);
+    inter = r->words[(size_t)sb * (WPR * r->R + 4) + WPR * r->R] < INTRA_C;
+  }
+  const int ltx = lg - 2 < 4 ? lg - 2 : 4, lcw = ltx == 4 ? 32 : 4 << ltx;
+  orc_ec_job jl = {0, 0, bx, by, ltx, 0, inter, lg, lg, 0};
+  ec_push(L, jl, ec_coeffs(r, lg, x4, y4, 0, 0), lcw * lcw);
+  const int plg = lg - r->xdec;  /* xdec == ydec */
+  const int n_tx = plg == 6 ? 4 : 1;
+  const int ctx_ = plg == 6 ? 3 : plg - 2, ccw = ctx_ == 4 ? 32 : 4 << ctx_;
+  for (int p = 1; p < 3; p++)
+    for (int t = 0; t < n_tx; t++) {
+      orc_ec_job jc = {0, p, bx + (n_tx == 4 ? (t % 2) * 8 : 0), by + (n_tx == 4 ? (t / 2) * 8 : 0),
+                       ctx_, 0, inter, plg, plg, 0};
+      ec_push(L, jc, ec_coeffs(r, lg, x4, y4, p, t), ccw * ccw);
+    }
+}
+
+static int ec_qctx(int q) { return q <= 20 ? 0 : q <= 60 ? 1 : q <= 120 ? 2 : 3; }
+
+static void entropy_frame(orc_replay *r) {
+  const int lv = r->fi.level;
+  uint16_t init[ORC_EC_CDF_TOTAL];
+  if (r->ec_chain[lv])
+    memcpy(init, r->ec_chain[lv], sizeof(init));
+  else
+    memcpy(init, orc_ec_default_cdf(ec_qctx(r->lv[lv].qidx)), sizeof(init));
+  const int ntx = (r->tw + r->tws - 1) / r->tws, nty = (r->th + r->ths - 1) / r->ths;
+  uint64_t total = 0, h = 1469598103934665603ull;
+  long best = -1;
+  uint16_t *best_cdf = malloc(sizeof(init)), *cdf = malloc(sizeof(init));
+  for (int ty = 0; ty < nty; ty++)
+    for (int tx = 0; tx < ntx; tx++) {
+      ec_list L = {0};
+      const int sx0 = r->tx0 + tx * r->tws, sy0 = r->ty0 + ty * r->ths;
+      const int sx1 = sx0 + r->tws < r->tx0 + r->tw ? sx0 + r->tws : r->tx0 + r->tw;
+      const int sy1 = sy0 + r->ths < r->ty0 + r->th ? sy0 + r->ths : r->ty0 + r->th;
+      orc_ec_job j3 = {3, 0, 0, 0, 0, 0, 0, 0, 0, 0}, j2 = {2, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      ec_push(&L, j3, NULL, 0);
+      for (int sy = sy0; sy < sy1; sy++) {
+        ec_push(&L, j2, NULL, 0);
+        for (int sx = sx0; sx < sx1; sx++) ec_walk(r, &L, sx * 16, sy * 16, 6, sx0 * 16, sy0 * 16);
+      }
+      const long cap = (long)(L.nc * 4 + L.nj * 16 + 4096);
+      uint8_t *out = malloc((size_t)cap);
+      int32_t tb[2] = {0, 0};
+      const long nb = orc_ec_code_jobs(L.j, (int)L.nj, L.c, init, r->xdec, r->ydec, out, cap, tb,
+                                       NULL, cdf);
+      for (long i = 0; i < nb; i++) h = (h ^ out[i]) * 1099511628211ull;
+      total += (uint64_t)(nb > 0 ? nb : 0);
+      if (nb >= best) {
+        best = nb;
+        memcpy(best_cdf, cdf, sizeof(init));
+      }
+      free(out);
+      free(L.j);
+      free(L.c);
+    }
+  orc_ec_reset_counts(best_cdf);
+  free(r->ec_chain[lv]);
+  r->ec_chain[lv] = best_cdf;
+  free(cdf);
+  r->ec_stat[0] = total;
+  r->ec_stat[1] = (uint64_t)(ntx * nty);
+  r->ec_stat[2] = h;
+  r->ec_stat[3]++;
+}
+
+/* Coefficient entropy coding of every coded frame; needs one tile group
+ * (the biggest-tile CDF choice spans the frame's tiles) and xdec == ydec. */
+int orc_replay_set_entropy(orc_replay *r, int on) {
+  if (on && (r->xdec != r->ydec || r->tx0 || r->ty0 ||
+             r->tw != (r->W + 63) / 64 || r->th != (r->H + 63) / 64))
+    return -1;
+  r->entropy = on != 0;
+  if (r->entropy && !r->mi_lg) {
+    r->mi_cols = (r->W + 3) / 4;
+    r->mi_rows = (r->H + 3) / 4;
+    r->mi_lg = calloc((size_t)r->mi_cols * r->mi_rows, 1);
+    r->mi_skip = calloc((size_t)r->mi_cols * r->mi_rows, 1);
+    if (!r->mi_lg || !r->mi_skip) return -1;
+  }
+  return 0;
+}
+
+/* [bytes, tiles, FNV-1a 64 of the tiles' bytes in order, frames coded] of
+ * the last frame */
+void orc_replay_entropy_stats(const orc_replay *r, uint64_t out[4]) {
+  memcpy(out, r->ec_stat, sizeof(r->ec_stat));
+}
+
 static void *worker(void *arg) {
   orc_replay *r = arg;
   uint64_t tail[3] = {0, 0, 0};
@@ -1612,10 +1782,9 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
   for (int pass = 0; pass < 4; pass++) run_pass(r, pass);
   r->istat[0] = r->istat[1] = 0;
   if (r->intra) run_pass(r, 4);
-  if (r->deblock) {
-    map_own(r);
-    if (pad_recon) loop_filter_planes(r);  /* tile groups: after the imports */
-  }
+  if (r->deblock || r->entropy) map_own(r);
+  if (r->entropy) entropy_frame(r);
+  if (r->deblock && pad_recon) loop_filter_planes(r);  /* tile groups: after the imports */
   r->tail[3] = (uint64_t)(r->vis_w / 8) * (r->vis_h / 8);
   if (pad_recon) {
     pad(r, &S->y);

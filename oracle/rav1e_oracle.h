@@ -286,6 +286,9 @@ long orc_ec_code_jobs(const orc_ec_job *jobs, int n, const int32_t *coeffs, cons
                       int xdec, int ydec, uint8_t *out, long cap, int32_t *tile_bytes,
                       uint16_t *ret, uint16_t *cdf_out);
 const uint16_t *orc_ec_default_cdf(int qctx);
+struct orc_replay;
+int orc_replay_set_entropy(struct orc_replay *r, int on);
+void orc_replay_entropy_stats(const struct orc_replay *r, uint64_t out[4]);
 
 #ifdef __cplusplus
 }

@@ -290,6 +290,7 @@ def _declare(L):
         "rv_comm_create": (vp, [vp, i32, i32]),
         "rv_comm_destroy": (None, [vp]),
         "rv_replay_results": (i32, [vp, vp, i32]),
+        "rv_replay_entropy_stats": (i32, [vp, vp, i32]),
         "rv_replay_stage_times": (i32, [vp, vp, i32]),
         "rv_replay_stage_times_sum": (i32, [vp, i32, vp, i32]),
         "rv_replay_counters": (i32, [vp, vp, i32]),

@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "rv_device.h"
+#include "rv_ec.h"
 #include "rv_ec_tables.h"
 #include "rv_quant_tables.h"
 
@@ -94,6 +95,7 @@ __device__ inline int wave_incl_scan(int v, int lane) {
 struct EcArgs {
   const rv_ec_job *jobs;
   int n, xdec, ydec, map_w4, map_h4;
+  const uint32_t *dn;  // non-null: the job count is *dn (<= n, device-generated jobs)
   uint8_t *map;
   uint32_t *count;  // [n] token counts, then exclusive offsets [n + 1]
   int32_t *eob;     // [n]
@@ -109,10 +111,13 @@ __device__ inline uint8_t *ec_map(const EcArgs &a, int tile, int p) {
 // Pass 1, one wavefront per job: eob, the stored context value (cul_level
 // with the dc sign, src/context.rs:4209-4217; 0 for eob == 0 and for a skip
 // leaf's planes) into the map, and the job's token count.
+__device__ void ec_prep_job(const EcArgs &a, int j, int lane);
 __global__ __launch_bounds__(256) void ec_prep_kernel(EcArgs a) {
   const int lane = threadIdx.x & 63;
-  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (j >= a.n) return;
+  const int n = a.dn ? (int)*a.dn : a.n;
+  for (int j = blockIdx.x * 4 + (threadIdx.x >> 6); j < n; j += gridDim.x * 4) ec_prep_job(a, j, lane);
+}
+__device__ void ec_prep_job(const EcArgs &a, int j, int lane) {
   const rv_ec_job jb = a.jobs[j];
   if (jb.kind == 1) {
     for (int p = 0; p < 3; p++) {
@@ -175,26 +180,16 @@ __global__ __launch_bounds__(256) void ec_prep_kernel(EcArgs a) {
   }
 }
 
-// Exclusive scan of the counts in place (n <= 1024 * 1024): per-1024
-// block scans, a scan of the block sums, the block offsets added.
-__global__ __launch_bounds__(1024) void ec_scan_blocks(uint32_t *v, int n, uint32_t *bsum) {
+// Exclusive scan of the counts in place (n <= 1024 * 1024; dn non-null:
+// the count is *dn <= n): per-1024 block scans, a scan of the block sums,
+// the block offsets added.  v[count] = the total, status[0] too.
+__device__ inline int scan_n(int n, const uint32_t *dn) { return dn ? (int)*dn : n; }
+__global__ __launch_bounds__(1024) void ec_scan_blocks(uint32_t *v, int n, const uint32_t *dn,
+                                                       uint32_t *bsum) {
   __shared__ uint32_t s[1024];
+  n = scan_n(n, dn);
   const int i = blockIdx.x * 1024 + threadIdx.x;
-  s[threadIdx.x] = i < n ? v[i] : 0;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const uint32_t t = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
-    __syncthreads();
-    s[threadIdx.x] += t;
-    __syncthreads();
-  }
-  if (i < n) v[i] = s[threadIdx.x] - (i < n ? v[i] : 0);
-  if (threadIdx.x == 1023) bsum[blockIdx.x] = s[1023];
-}
-__global__ __launch_bounds__(1024) void ec_scan_top(uint32_t *bsum, int nb, uint32_t *v, int n,
-                                                    uint32_t *status) {
-  __shared__ uint32_t s[1024];
-  const uint32_t x = threadIdx.x < nb ? bsum[threadIdx.x] : 0;
+  const uint32_t x = i < n ? v[i] : 0;
   s[threadIdx.x] = x;
   __syncthreads();
   for (int o = 1; o < 1024; o <<= 1) {
@@ -203,16 +198,45 @@ __global__ __launch_bounds__(1024) void ec_scan_top(uint32_t *bsum, int nb, uint
     s[threadIdx.x] += t;
     __syncthreads();
   }
-  if (threadIdx.x < nb) bsum[threadIdx.x] = s[threadIdx.x] - x;
+  if (i < n) v[i] = s[threadIdx.x] - x;
+  if (threadIdx.x == 1023) bsum[blockIdx.x] = s[1023];
+}
+__global__ __launch_bounds__(1024) void ec_scan_top(uint32_t *bsum, int n, const uint32_t *dn,
+                                                    uint32_t *v, uint32_t *status) {
+  __shared__ uint32_t s[1024];
+  n = scan_n(n, dn);
+  const int nb = (n + 1023) / 1024;
+  const uint32_t x = (int)threadIdx.x < nb ? bsum[threadIdx.x] : 0;
+  s[threadIdx.x] = x;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const uint32_t t = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+    __syncthreads();
+    s[threadIdx.x] += t;
+    __syncthreads();
+  }
+  if ((int)threadIdx.x < nb) bsum[threadIdx.x] = s[threadIdx.x] - x;
   if (threadIdx.x == 0) {
     v[n] = s[1023];
-    status[0] = s[1023];
-    status[1] = 0;
+    if (status) {
+      status[0] = s[1023];
+      status[1] = 0;
+    }
   }
 }
-__global__ __launch_bounds__(1024) void ec_scan_add(uint32_t *v, int n, const uint32_t *bsum) {
+__global__ __launch_bounds__(1024) void ec_scan_add(uint32_t *v, int n, const uint32_t *dn,
+                                                    const uint32_t *bsum) {
+  n = scan_n(n, dn);
   const int i = blockIdx.x * 1024 + threadIdx.x;
   if (i < n) v[i] += bsum[blockIdx.x];
+}
+
+void ec_scan(uint32_t *v, int n, const uint32_t *dn, uint32_t *bsum, uint32_t *status,
+             hipStream_t st) {
+  const int nb = (n + 1023) / 1024;
+  ec_scan_blocks<<<nb, 1024, 0, st>>>(v, n, dn, bsum);
+  ec_scan_top<<<1, 1024, 0, st>>>(bsum, n, dn, v, status);
+  if (nb > 1) ec_scan_add<<<nb, 1024, 0, st>>>(v, n, dn, bsum);
 }
 
 struct TokW {
@@ -259,11 +283,17 @@ __device__ inline int br_ctx(const uint8_t *lv, int c, int bwl) {
 
 // Pass 2, one wavefront per transform-block job: its symbols, in
 // write_coeffs_lv_map's order, from its token offset.
+__device__ void ec_token_job(const EcArgs &a, int j, int lane, uint8_t *lv);
 __global__ __launch_bounds__(256) void ec_token_kernel(EcArgs a) {
   __shared__ uint8_t lds[4][kEcLds];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int j = blockIdx.x * 4 + wv;
-  if (j >= a.n) return;
+  const int n = a.dn ? (int)*a.dn : a.n;
+  for (int j = blockIdx.x * 4 + wv; j < n; j += gridDim.x * 4) {
+    ec_token_job(a, j, lane, lds[wv]);
+    wave_sync();
+  }
+}
+__device__ void ec_token_job(const EcArgs &a, int j, int lane, uint8_t *lv) {
   const rv_ec_job jb = a.jobs[j];
   if (jb.kind != 0) return;
   const TokW w{a.tokens, a.cap, a.status};
@@ -302,7 +332,6 @@ __global__ __launch_bounds__(256) void ec_token_kernel(EcArgs a) {
   o++;
   if (eob == 0) return;
   // txb_init_levels into LDS (pad columns / rows zero)
-  uint8_t *lv = lds[wv];
   const int st = cw + kEcPadHor;
   for (int i = lane; i < st * (cw + 4); i += 64) lv[i] = 0;
   wave_sync();
@@ -397,6 +426,173 @@ __global__ __launch_bounds__(256) void ec_token_kernel(EcArgs a) {
       for (int k = len - 1; k >= 0; k--) w.put(ob++, ec_raw((int)(x >> k)));
     }
   }
+}
+
+
+// ---- the replay's job list -------------------------------------------------
+// One thread per superblock of the group in coding order (tiles in raster
+// order, superblocks in raster order inside a tile; encode_tile_group /
+// encode_tile, src/encoder.rs:2766-2781, 3160-3340): its jobs are [tile
+// start] [superblock-row start] then its leaves in z-order
+// (encode_partition_topdown, :2392-2470): the Morton walk of the
+// superblock's 256 luma 4x4 positions meets each leaf's top-left first.
+// pass 0 counts, pass 1 writes at the scanned offsets.
+__device__ inline void ec_sb_of(const EcFrameArgs &a, int i, int &sx, int &sy, int &t, int &first,
+                                int &rowstart, int &t0x, int &t0y) {
+  const int ntx = (a.tw + a.tws - 1) / a.tws;
+  int base = 0;
+  for (t = 0;; t++) {
+    const int tx = t % ntx, ty = t / ntx;
+    const int w = min(a.tws, a.tw - tx * a.tws), h = min(a.ths, a.th - ty * a.ths);
+    if (i < base + w * h) {
+      const int k = i - base;
+      t0x = a.tx0 + tx * a.tws;
+      t0y = a.ty0 + ty * a.ths;
+      sx = t0x + k % w;
+      sy = t0y + k / w;
+      first = k == 0;
+      rowstart = k % w == 0;
+      return;
+    }
+    base += w * h;
+  }
+}
+
+__global__ __launch_bounds__(64) void ec_gen_kernel(EcFrameArgs a, EcFrameBufs b, int pass) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= a.nsb) return;
+  int sx, sy, t, first, rowstart, t0x, t0y;
+  ec_sb_of(a, i, sx, sy, t, first, rowstart, t0x, t0y);
+  uint32_t o = pass ? b.sb_off[i] : 0;
+  int n = 0;
+  auto put = [&](const rv_ec_job &jb) {
+    if (pass && o + n < (uint32_t)b.max_jobs) b.jobs[o + n] = jb;
+    n++;
+  };
+  rv_ec_job z{};
+  z.tile = t;
+  if (first) {
+    rv_ec_job j3 = z;
+    j3.kind = 3;
+    put(j3);
+  }
+  if (rowstart) {
+    rv_ec_job j2 = z;
+    j2.kind = 2;
+    put(j2);
+  }
+  const int sb = (sy - a.ty0) * a.tw + (sx - a.tx0);
+  for (int m = 0; m < 256; m++) {
+    int dx = 0, dy = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      dx |= ((m >> (2 * k)) & 1) << k;
+      dy |= ((m >> (2 * k + 1)) & 1) << k;
+    }
+    const int x4 = sx * 16 + dx, y4 = sy * 16 + dy;
+    if (x4 >= a.mi_cols || y4 >= a.mi_rows) continue;
+    const int code = a.mi_lg[(size_t)y4 * a.mi_stride + x4];
+    const int n4 = 1 << code, lg = code + 2;
+    if ((dx & (n4 - 1)) || (dy & (n4 - 1))) continue;  // not the leaf's top-left
+    rv_ec_job jb = z;
+    jb.bx = x4 - t0x * 16;
+    jb.by = y4 - t0y * 16;
+    if (a.mi_skip[(size_t)y4 * a.mi_stride + x4]) {
+      jb.kind = 1;
+      jb.bw_lg = jb.bh_lg = lg;
+      put(jb);
+      continue;
+    }
+    const int l = 6 - lg;
+    const EcGenLevel &L = a.lv[l];
+    int bi, inter = 1;
+    if (l == 0) {
+      bi = sb;
+      inter = a.words[(size_t)sb * a.words_per_sb + a.win_off] < 1000;
+    } else {
+      bi = (y4 / n4 - L.y0) * L.gw + (x4 / n4 - L.x0);
+    }
+    const int ltx = min(lg - 2, 4);
+    jb.kind = 0;
+    jb.is_inter = inter;
+    jb.plane = 0;
+    jb.tx_size = ltx;
+    jb.bw_lg = jb.bh_lg = lg;
+    jb.coeffs = L.l_lev + (size_t)bi * (l == 0 ? 1024 : L.B * L.B);
+    put(jb);
+    const int plg = lg - a.xdec;
+    const int ntc = plg == 6 ? 4 : 1;
+    const int ctx_ = plg == 6 ? 3 : plg - 2;
+    const int carea = plg == 6 ? 1024 : L.bc * L.bc;
+    for (int p = 1; p < 3; p++)
+      for (int c = 0; c < ntc; c++) {
+        rv_ec_job jc = jb;
+        jc.plane = p;
+        jc.tx_size = ctx_;
+        jc.bw_lg = jc.bh_lg = plg;
+        jc.bx = jb.bx + (ntc == 4 ? (c % 2) * 8 : 0);
+        jc.by = jb.by + (ntc == 4 ? (c / 2) * 8 : 0);
+        if (l == 0)
+          jc.coeffs = L.c_lev + (size_t)(p - 1) * a.nsb * a.ntx_c * 1024 +
+                      ((size_t)bi * a.ntx_c + c) * 1024;
+        else
+          jc.coeffs = L.c_lev + (size_t)(p - 1) * L.n * carea + (size_t)bi * carea;
+        put(jc);
+      }
+  }
+  if (!pass) b.sb_off[i] = (uint32_t)n;
+}
+
+// the jobs count, every tile's first token, the total (host-mapped stat)
+__global__ void ec_ranges_kernel(EcFrameBufs b, int nsb, const EcFrameArgs a) {
+  const int t = threadIdx.x;
+  const uint32_t nj = b.sb_off[nsb];
+  if (t == 0) {
+    b.stat[0] = b.dstat[0];
+    b.stat[1] = b.dstat[1] || nj > (uint32_t)b.max_jobs;
+    b.stat[2] = nj;
+    b.stat[3 + b.ntiles] = b.dstat[0];
+  }
+  if (t < b.ntiles) {
+    // the first superblock of tile t: the tiles before it hold their sizes
+    const int ntx = (a.tw + a.tws - 1) / a.tws;
+    int base = 0;
+    for (int k = 0; k < t; k++) {
+      const int tx = k % ntx, ty = k / ntx;
+      base += min(a.tws, a.tw - tx * a.tws) * min(a.ths, a.th - ty * a.ths);
+    }
+    b.stat[3 + t] = b.offsets[b.sb_off[base]];
+  }
+}
+
+int ec_frame_tokens(const EcFrameArgs &a, const EcFrameBufs &b, hipStream_t st) {
+  ec_gen_kernel<<<(a.nsb + 63) / 64, 64, 0, st>>>(a, b, 0);
+  uint32_t *bsum = (uint32_t *)((char *)b.scratch + (size_t)b.max_jobs * 4);
+  ec_scan(b.sb_off, a.nsb, nullptr, bsum, nullptr, st);
+  ec_gen_kernel<<<(a.nsb + 63) / 64, 64, 0, st>>>(a, b, 1);
+  EcArgs e;
+  e.jobs = b.jobs;
+  e.n = b.max_jobs;
+  e.dn = b.sb_off + a.nsb;
+  e.xdec = a.xdec;
+  e.ydec = a.ydec;
+  e.map_w4 = b.map_w4;
+  e.map_h4 = b.map_h4;
+  e.map = b.map;
+  e.count = b.offsets;
+  e.eob = (int32_t *)b.scratch;
+  e.tokens = b.tokens;
+  e.cap = b.cap;
+  e.status = b.dstat;
+  if (hipMemsetAsync(b.map, 0, (size_t)b.ntiles * 3 * b.map_w4 * b.map_h4, st) != hipSuccess)
+    return rv_set_error(RV_EHIP, "ec_frame_tokens: map clear");
+  // grid-stride over the device-side job count: 2048 workgroups of 4 waves
+  ec_prep_kernel<<<2048, 256, 0, st>>>(e);
+  ec_scan(b.offsets, b.max_jobs, e.dn, bsum, b.dstat, st);
+  ec_token_kernel<<<2048, 256, 0, st>>>(e);
+  ec_ranges_kernel<<<1, 256, 0, st>>>(b, a.nsb, a);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
 }
 
 }  // namespace rv
@@ -572,12 +768,11 @@ int rv_ec_tokenize(const rv_ec_job *d_jobs, int n, int xdec, int ydec, int n_til
   a.tokens = d_tokens;
   a.cap = token_cap;
   a.status = d_status;
-  const int nb = (n + 1023) / 1024;
-  ec_prep_kernel<<<(n + 3) / 4, 256, 0, st>>>(a);
-  ec_scan_blocks<<<nb, 1024, 0, st>>>(d_offsets, n, bsum);
-  ec_scan_top<<<1, 1024, 0, st>>>(bsum, nb, d_offsets, n, d_status);
-  if (nb > 1) ec_scan_add<<<nb, 1024, 0, st>>>(d_offsets, n, bsum);
-  ec_token_kernel<<<(n + 3) / 4, 256, 0, st>>>(a);
+  a.dn = nullptr;
+  const int grid = (n + 3) / 4 < 4096 ? (n + 3) / 4 : 4096;
+  ec_prep_kernel<<<grid, 256, 0, st>>>(a);
+  ec_scan(d_offsets, n, nullptr, bsum, d_status, st);
+  ec_token_kernel<<<grid, 256, 0, st>>>(a);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

@@ -32,10 +32,15 @@
 // produce the same result words.
 #include <string.h>
 
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "rv_chain.h"
 #include "rv_device.h"
+#include "rv_ec.h"
 #include "rv_intra.h"
 #include "rv_intra_pass.h"
 #include "rv_rdo.h"
@@ -598,6 +603,92 @@ struct RvInput {
   rv_plane y, u, v;
 };
 
+// The host side of stage F8 (RV_REPLAY_ENTROPY): a thread that range-codes
+// each frame's tile token streams once the device has written them into
+// host-mapped memory (two ring slots), keeping the CDF chain per pyramid
+// level (get_initial_cdfcontext / the biggest tile, src/encoder.rs:
+// 2750-2761, 2824-2833).
+struct EcHost {
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  struct Item {
+    int slot, level, qctx;
+  };
+  std::deque<Item> q;
+  bool stop = false;
+  long queued = 0, done = 0;
+  int ntiles = 1;
+  uint32_t *tok_h[2] = {nullptr, nullptr}, *stat_h[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  bool busy[2] = {false, false};
+  std::vector<uint16_t> chain[3];
+  uint64_t stat[5] = {0, 0, 0, 0, 0};
+  int err = 0;
+
+  void code(const Item &it) {
+    const uint32_t *st = stat_h[it.slot];
+    if (st[1]) {  // tokens past the buffer were dropped
+      err = RV_EINVAL;
+      return;
+    }
+    const int total = rv_ec_cdf_total();
+    std::vector<uint16_t> init(total), cdf(total), best_cdf(total);
+    if (chain[it.level].empty())
+      rv_ec_default_cdf(it.qctx, init.data());
+    else
+      init = chain[it.level];
+    uint64_t h = 1469598103934665603ull, bytes = 0;
+    long best = -1;
+    std::vector<uint8_t> out;
+    for (int t = 0; t < ntiles; t++) {
+      const uint32_t a = st[3 + t], b = st[3 + t + 1];
+      cdf = init;
+      out.resize(2 * (size_t)(b - a) + 64);
+      const long nb = rv_ec_code_tokens(tok_h[it.slot] + a, b - a, cdf.data(), out.data(), out.size());
+      if (nb < 0 || (size_t)nb > out.size()) {
+        err = RV_EINVAL;
+        return;
+      }
+      for (long i = 0; i < nb; i++) h = (h ^ out[i]) * 1099511628211ull;
+      bytes += (uint64_t)nb;
+      if (nb >= best) {  // Iterator::max_by_key keeps the last maximum
+        best = nb;
+        best_cdf = cdf;
+      }
+    }
+    rv_ec_reset_counts(best_cdf.data());
+    chain[it.level] = best_cdf;
+    stat[0] = bytes;
+    stat[1] = (uint64_t)ntiles;
+    stat[2] = h;
+    stat[3]++;
+    stat[4] += bytes;
+  }
+  void run() {
+    for (;;) {
+      Item it;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return stop || !q.empty(); });
+        if (q.empty()) return;
+        it = q.front();
+        q.pop_front();
+      }
+      (void)hipEventSynchronize(ev[it.slot]);
+      code(it);
+      std::lock_guard<std::mutex> lk(mu);
+      busy[it.slot] = false;
+      done++;
+      cv.notify_all();
+    }
+  }
+  void drain() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return done == queued; });
+  }
+};
+
 struct rv_replay {
   rv_replay_cfg cfg;
   Geo g;
@@ -664,6 +755,11 @@ struct rv_replay {
   int32_t *cdef_var = nullptr;
   uint8_t cdef_str[3][2] = {};      // [level] = (y, uv) strengths at cdef_index 0
   int32_t *leaf_count = nullptr;  // [kLevels]
+  // RV_REPLAY_ENTROPY: the coefficient-coding stage (F8)
+  bool entropy = false;
+  EcFrameBufs ecb{};
+  EcHost *ech = nullptr;
+  long ec_frames = 0;
   // intra-mode screening (rv_intra_pass.hip; speed 10, 4:2:0)
   bool intra = false;
   uint8_t *i_elig = nullptr, *i_was = nullptr, *i_win = nullptr, *i_modes = nullptr;
@@ -707,8 +803,9 @@ struct rv_replay {
   // record costs ~4.4 us of idle GPU between kernels on MI355X).
   static constexpr int kRing = 64;
   // e[0..13]: the stage boundaries on the main stream; e[14], e[15]: the
-  // lookahead's start and end (on the side stream when it overlaps)
-  static constexpr int kEv = 18;
+  // lookahead's start and end (on the side stream when it overlaps); e[16],
+  // e[17]: the edge levels' span; e[18], e[19]: F8's (coefficient tokens)
+  static constexpr int kEv = 20;
   static constexpr int kStageEv = 14;
   hipEvent_t evs[kRing][kEv];
   int timing_stride = 1, timing_block = 1;
@@ -1271,6 +1368,21 @@ void rv_replay_destroy(rv_replay *r) {
   // stream running)
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->side) (void)hipStreamSynchronize(r->side);
+  if (r->ech) {  // the host coder finishes the frames it holds, then stops
+    {
+      std::lock_guard<std::mutex> lk(r->ech->mu);
+      r->ech->stop = true;
+    }
+    r->ech->cv.notify_all();
+    if (r->ech->th.joinable()) r->ech->th.join();
+    for (int k = 0; k < 2; k++) {
+      if (r->ech->tok_h[k]) (void)hipHostFree(r->ech->tok_h[k]);
+      if (r->ech->stat_h[k]) (void)hipHostFree(r->ech->stat_h[k]);
+      if (r->ech->ev[k]) (void)hipEventDestroy(r->ech->ev[k]);
+    }
+    delete r->ech;
+    r->ech = nullptr;
+  }
   for (hipStream_t es : r->edge)
     if (es) (void)hipStreamSynchronize(es);
   for (void *p : r->allocs) (void)hipFree(p);
@@ -1531,8 +1643,14 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     ok = ok && r->cdef_dir && r->cdef_var && r->cdef_idx && alloc_input(r, r->cdef_pre);
     if (r->cdef_idx) (void)hipMemsetAsync(r->cdef_idx, 0, n64, r->stream);
   }
-  if (cfg->flags & RV_REPLAY_DEBLOCK) {
-    r->deblock = true;
+  r->entropy = (cfg->flags & RV_REPLAY_ENTROPY) != 0;
+  if (r->entropy && (g.xdec != g.ydec || g.tx0 || g.ty0 || g.tw != sbc || g.th != sbr)) {
+    rv_set_error(RV_EINVAL, "rv_replay_create: RV_REPLAY_ENTROPY needs the whole frame, xdec == ydec");
+    rv_replay_destroy(r);
+    return nullptr;
+  }
+  if (cfg->flags & (RV_REPLAY_DEBLOCK | RV_REPLAY_ENTROPY)) {
+    r->deblock = (cfg->flags & RV_REPLAY_DEBLOCK) != 0;
     r->mi_cols = (g.W + 3) / 4;
     r->mi_rows = (g.H + 3) / 4;
     r->mi_stride = (r->mi_cols + 15) / 16 * 16;
@@ -1542,11 +1660,39 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     ok = ok && r->mi_lg && r->mi_skip;
     if (r->mi_lg) (void)hipMemsetAsync(r->mi_lg, 4, mb, r->stream);
     if (r->mi_skip) (void)hipMemsetAsync(r->mi_skip, 0, mb, r->stream);
-    if (r->s6) {
+    if (r->s6 && r->deblock) {
       r->db_tally = (int64_t *)dalloc(r, 3 * 130 * 8);
       r->db_dlev = (uint8_t *)dalloc(r, 4);
       ok = ok && r->db_tally && r->db_dlev;
     }
+  }
+  if (r->entropy) {  // F8 buffers, the host-mapped token rings and the coder thread
+    EcFrameBufs &b = r->ecb;
+    b.ntiles = ((g.tw + g.tws - 1) / g.tws) * ((g.th + g.ths - 1) / g.ths);
+    b.max_jobs = ec_max_jobs(g.nsb, b.ntiles);
+    b.map_w4 = g.tws * 16;
+    b.map_h4 = g.ths * 16;
+    b.jobs = (rv_ec_job *)dalloc(r, (size_t)b.max_jobs * sizeof(rv_ec_job));
+    b.sb_off = (uint32_t *)dalloc(r, ((size_t)g.nsb + 1) * 4);
+    b.map = (uint8_t *)dalloc(r, (size_t)b.ntiles * 3 * b.map_w4 * b.map_h4);
+    b.scratch = dalloc(r, rv_ec_scratch_bytes(b.max_jobs));
+    b.offsets = (uint32_t *)dalloc(r, ((size_t)b.max_jobs + 1) * 4);
+    b.dstat = (uint32_t *)dalloc(r, 16);
+    // one token per coded coefficient plus 4 per job covers every block
+    // whose levels stay below 3; more sets the overflow flag (an error)
+    b.cap = (uint32_t)((size_t)g.nsb * (1024 + 2 * r->ntx_c * 1024) + (size_t)b.max_jobs * 4);
+    ok = ok && b.jobs && b.sb_off && b.map && b.scratch && b.offsets && b.dstat;
+    EcHost *eh = new EcHost();
+    r->ech = eh;
+    eh->ntiles = b.ntiles;
+    for (int k = 0; k < 2 && ok; k++) {
+      ok = hipHostMalloc((void **)&eh->tok_h[k], (size_t)b.cap * 4,
+                         hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+           hipHostMalloc((void **)&eh->stat_h[k], ((size_t)b.ntiles + 8) * 4,
+                         hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+           hipEventCreate(&eh->ev[k]) == hipSuccess;
+    }
+    if (ok) eh->th = std::thread([eh] { eh->run(); });
   }
   r->imp_bx = g.vis_w / 8;
   r->imp_by = g.vis_h / 8;
@@ -1770,6 +1916,8 @@ int rv_replay_set_groups(rv_replay *r, int n_groups, const int32_t *rects, int m
   if (rects[4 * my_group] != g.tx0 || rects[4 * my_group + 1] != g.ty0 ||
       rects[4 * my_group + 2] != g.tw || rects[4 * my_group + 3] != g.th)
     return rv_set_error(RV_EINVAL, "rv_replay_set_groups: my group != the configured tile group");
+  if (r->entropy && n_groups > 1)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_groups: RV_REPLAY_ENTROPY codes one group");
   memcpy(r->grects, rects, (size_t)n_groups * 4 * sizeof(int32_t));
   r->n_groups = n_groups;
   r->my_group = my_group;
@@ -2294,7 +2442,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // F7 deblock_filter_frame (src/encoder.rs:2789-2793) when enabled: the
   // block map of the committed blocks, then (once every group's pixels and
   // map are in) Y, U, V in place; the reconstruction becomes a reference
-  if (r->deblock) {
+  if (r->deblock || r->entropy) {
     if (!r->lvl) {
       block_map_kernel<<<(g.nsb * 16 + 255) / 256, 256, 0, st>>>(
           nullptr, nullptr, g.nsb, g.tw, g.tx0, g.ty0, 0, r->win, r->mi_lg, r->mi_skip,
@@ -2308,6 +2456,69 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
             l ? P.win : r->win, r->mi_lg, r->mi_skip, r->mi_stride, r->mi_cols, r->mi_rows);
       }
     }
+  }
+  // F8 (RV_REPLAY_ENTROPY): the committed transform blocks' symbols, in
+  // coding order, into a host-mapped ring slot; the host thread range-codes
+  // them beside the next frames
+  if (r->entropy) {
+    EcHost *eh = r->ech;
+    const int slot = (int)(r->ec_frames & 1);
+    {
+      std::unique_lock<std::mutex> lk(eh->mu);
+      eh->cv.wait(lk, [&] { return !eh->busy[slot]; });
+      eh->busy[slot] = true;
+    }
+    EcFrameArgs ea;
+    ea.tx0 = g.tx0;
+    ea.ty0 = g.ty0;
+    ea.tw = g.tw;
+    ea.th = g.th;
+    ea.tws = g.tws;
+    ea.ths = g.ths;
+    ea.xdec = g.xdec;
+    ea.ydec = g.ydec;
+    ea.ntx_c = r->ntx_c;
+    ea.nsb = g.nsb;
+    ea.mi_lg = r->mi_lg;
+    ea.mi_skip = r->mi_skip;
+    ea.mi_stride = r->mi_stride;
+    ea.mi_cols = r->mi_cols;
+    ea.mi_rows = r->mi_rows;
+    ea.lv[0].l_lev = r->l_lev;
+    ea.lv[0].c_lev = r->c_lev;
+    ea.lv[0].n = g.nsb;
+    ea.lv[0].gw = g.tw;
+    ea.lv[0].x0 = g.tx0;
+    ea.lv[0].y0 = g.ty0;
+    for (int l = 1; r->lvl && l < kLevels; l++) {
+      const rv_replay::PLevel &P = r->pl[l];
+      ea.lv[l].l_lev = P.l_lev;
+      ea.lv[l].c_lev = P.c_lev;
+      ea.lv[l].n = P.n;
+      ea.lv[l].gw = P.gw;
+      ea.lv[l].x0 = P.cg.tx0;
+      ea.lv[l].y0 = P.cg.ty0;
+      ea.lv[l].B = P.B;
+      ea.lv[l].bc = P.bc;
+    }
+    ea.words = r->words;
+    ea.words_per_sb = kWordsPerRef * g.R + 4;
+    ea.win_off = kWordsPerRef * g.R;
+    EcFrameBufs b = r->ecb;
+    RV_H(hipHostGetDevicePointer((void **)&b.tokens, eh->tok_h[slot], 0));
+    RV_H(hipHostGetDevicePointer((void **)&b.stat, eh->stat_h[slot], 0));
+    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 4], st));
+    RV_R(ec_frame_tokens(ea, b, st));
+    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 5], st));
+    RV_H(hipEventRecord(eh->ev[slot], st));
+    const int q = r->lv[lv].qidx;
+    {
+      std::lock_guard<std::mutex> lk(eh->mu);
+      eh->q.push_back({slot, lv, q <= 20 ? 0 : q <= 60 ? 1 : q <= 120 ? 2 : 3});
+      eh->queued++;
+    }
+    eh->cv.notify_all();
+    r->ec_frames++;
   }
   r->coded++;
   r->last = fi;
@@ -2424,7 +2635,23 @@ static int stage_times(rv_replay *r, float *ms_out, int cap, int last) {
       RV_H(hipEventElapsedTime(&ms, e[kS + 2], e[kS + 3]));
       ms_out[n++] += ms;
     }
+    if (n < cap && r->entropy) {  // F8: the coefficient tokens
+      float ms = 0.f;
+      RV_H(hipEventSynchronize(e[kS + 5]));
+      RV_H(hipEventElapsedTime(&ms, e[kS + 4], e[kS + 5]));
+      ms_out[n++] += ms;
+    }
   }
+  return n;
+}
+
+int rv_replay_entropy_stats(rv_replay *r, uint64_t *out, int cap) {
+  if (!r || !out || cap < 4) return rv_set_error(RV_EINVAL, "rv_replay_entropy_stats: null / cap");
+  if (!r->ech) return rv_set_error(RV_EINVAL, "rv_replay_entropy_stats: RV_REPLAY_ENTROPY off");
+  r->ech->drain();
+  if (r->ech->err) return rv_set_error(r->ech->err, "rv_replay_entropy_stats: token buffer overflow");
+  const int n = cap < 5 ? cap : 5;
+  for (int i = 0; i < n; i++) out[i] = r->ech->stat[i];
   return n;
 }
 

@@ -25,10 +25,12 @@ RV_REPLAY_DEBLOCK = 16  # deblock every coded frame before it becomes a referenc
 RV_REPLAY_CDEF = 32  # CDEF after deblocking (needs RV_REPLAY_DEBLOCK), cdef_bits 0
 RV_REPLAY_NO_INTRA = 64  # no intra-mode screening of non-skip superblocks (default: on
 #                          at speed 10 in 4:2:0)
+RV_REPLAY_ENTROPY = 128  # F8: code every frame's coefficients (device tokens, host range coder)
 # HIP-event stages of a frame: F0, F1, F2, FL (lookahead), F3 full-pel, F3
 # sub-pel, F4 single, F4 compound, F4 argmin, F6 commit, F6b intra, F5, F7,
-# then the lookahead's own span and the speed-10 edge levels' own span
-N_STAGES = 15
+# then the lookahead's own span, the speed-10 edge levels' own span and
+# (RV_REPLAY_ENTROPY) F8's coefficient tokens
+N_STAGES = 16
 
 # GOP of the reference's reorder pyramid (src/api/internal.rs:61-95):
 # group_input_len 4, levels 0,1,2,2 -> me_range_scale = 4 >> level
@@ -367,6 +369,16 @@ class HipReplay:
             _check(n, "rv_replay_results")
         return out[:n]
 
+    def entropy_stats(self):
+        """RV_REPLAY_ENTROPY: [last frame's coefficient bytes, tiles, FNV-1a
+        of its tiles' bytes, frames coded, bytes over every frame] (waits
+        for the host coder)."""
+        out = np.zeros(5, np.uint64)
+        n = lib().rv_replay_entropy_stats(self.h, out.ctypes.data, 5)
+        if n < 0:
+            _check(n, "rv_replay_entropy_stats")
+        return [int(v) for v in out]
+
     def set_timing(self, stride: int, block: int = 1):
         """Record the timing events on coded frames f with (f // block) %
         stride == 0 (rv_replay_set_timing)."""
@@ -384,7 +396,7 @@ class HipReplay:
         n = lib().rv_replay_stage_times_sum(self.h, last_frames, out.ctypes.data, N_STAGES)
         if n < 0:
             _check(n, "rv_replay_stage_times_sum")
-        return out[:n]
+        return out  # stages past n (F8 without RV_REPLAY_ENTROPY) stay 0
 
     def counters(self) -> np.ndarray:
         """[F3 full-pel evals, F3 sub-pel evals, frames, F4 single-reference
@@ -517,6 +529,14 @@ class PairedReplay:
     def set_timing(self, stride: int, block: int = 1):
         self.p.set_timing(stride, block)
         self.t.set_timing(stride, block)
+
+    def entropy_stats(self):
+        """Both instances' coefficient coding: [bytes of the primary's last
+        frame, tiles, its hash, frames coded by both, bytes over every
+        frame of both]."""
+        self.drain()
+        a, b = self.p.entropy_stats(), self.t.entropy_stats()
+        return [a[0], a[1], a[2], a[3] + b[3], a[4] + b[4]]
 
     def counters(self) -> np.ndarray:
         """HipReplay.counters summed over both instances (their frames do not

@@ -508,7 +508,7 @@ class CpuReplay:
 
     def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, group=None,
                  tile_size=(0, 0), n_inputs=8, threads=1, L=None, quantizer=100, speed=10,
-                 deblock=False, cdef=False, intra=True):
+                 deblock=False, cdef=False, intra=True, entropy=False):
         from rav1e_amd import rate as RT
         L = L or lib()
         self.L = L
@@ -543,6 +543,10 @@ class CpuReplay:
         L.orc_replay_set_intra.argtypes = [C.c_void_p, C.c_int]
         assert L.orc_replay_set_intra(self.h, 1 if self.intra else 0) == 0
         L.orc_replay_intra_stats.argtypes = [C.c_void_p, C.c_void_p]
+        L.orc_replay_set_entropy.argtypes = [C.c_void_p, C.c_int]
+        L.orc_replay_entropy_stats.argtypes = [C.c_void_p, C.c_void_p]
+        self.entropy = bool(entropy)
+        assert L.orc_replay_set_entropy(self.h, 1 if entropy else 0) == 0, "orc_replay_set_entropy"
         self.n_words = result_words(width, height, n_refs, tw, th, tx0, ty0, speed, xdec, ydec)
         self.geom = (width, height, xdec, ydec, bit_depth)
         self.levels = RT.level_params(quantizer, bit_depth)
@@ -570,6 +574,13 @@ class CpuReplay:
         out = np.zeros(2, np.uint64)
         self.L.orc_replay_intra_stats(self.h, out.ctypes.data)
         return int(out[0]), int(out[1])
+
+    def entropy_stats(self):
+        """[bytes, tiles, FNV-1a of the tiles' bytes, frames coded] of the
+        last frame's coefficient coding."""
+        out = np.zeros(4, np.uint64)
+        self.L.orc_replay_entropy_stats(self.h, out.ctypes.data)
+        return [int(v) for v in out]
 
     def set_importances(self, imp):
         if imp is None:

@@ -223,3 +223,42 @@ def test_gpu_coefficient_coding_matches_oracle(xdec, ydec, sbw, sbh, ntiles, sca
         np.testing.assert_array_equal(tb, tbw[:ntiles])
         np.testing.assert_array_equal(got, want)
         np.testing.assert_array_equal(fin, finw)
+
+
+# --------------------------------------------------------------- the replay
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H,xdec,tiles,speed,q", [
+    (640, 360, 1, (0, 0), 10, 100), (640, 360, 1, (0, 0), 10, 40), (640, 360, 1, (0, 0), 6, 60),
+    (1920, 1080, 1, (8, 17), 10, 60), (512, 384, 0, (4, 3), 10, 50)])
+def test_gpu_replay_entropy_matches_cpu(W, H, xdec, tiles, speed, q):
+    """RV_REPLAY_ENTROPY (F8: device tokens + host range coder + the CDF chain
+    per pyramid level) against the CPU replay's sequential
+    write_coeffs_lv_map over the same committed frames, frame by frame:
+    bytes, tiles and the hash of every tile's bytes, plus the result words."""
+    import rav1e_amd as R
+    from rav1e_amd import replay as RP
+    R.require_device()
+    n = 10
+    flags = RP.RV_REPLAY_ENTROPY | (RP.RV_REPLAY_SPEED6 if speed == 6 else 0)
+    g = RP.HipReplay(W, H, xdec, xdec, 8, 2, tile_size=tiles, n_inputs=n + 2, flags=flags,
+                     quantizer=q)
+    g.synth_inputs(0)
+    c = O.CpuReplay(W, H, xdec, xdec, 8, 2, tile_size=tiles, n_inputs=n + 2, threads=8,
+                    speed=speed, entropy=True, quantizer=q)
+    for i in range(n + 2):
+        c.set_input(i, g.get_input(i))
+    g.frame()
+    c.frame()
+    nonzero = 0
+    try:
+        for f in range(n):
+            g.frame()
+            c.frame()
+            np.testing.assert_array_equal(g.results(), c.results(), err_msg=f"frame {f}")
+            gs, cs = g.entropy_stats(), c.entropy_stats()
+            assert gs[:3] == cs[:3], (f, gs, cs)
+            nonzero += gs[0] > 8
+    finally:
+        g.close()
+        c.close()
+    assert nonzero >= 2  # coefficients were coded, not only empty tiles
