@@ -10,7 +10,9 @@ diamond + sub-pel (speed 6: also every 32x32, 16x16 and 8x8 block, and the
 partition decision), F4 every RDO inter candidate (NEARESTMV / NEAR0MV /
 GLOBALMV / NEWMV x reference, skip and non-skip: MC, distortion, diff + fwd
 DCT, quantize, estimate_rate, inverse + add) with rav1e's rd cost and
-argmin, F6 the winners' reconstruction, F5 8x8 importance SATD, F7 the
+argmin, F6 the winners' reconstruction, F5 8x8 importance SATD, F8 the
+committed coefficients' entropy coding (write_coeffs_lv_map: device tokens, a
+host range coder beside the next frames; --no-entropy skips it), F7 the
 reconstruction becomes a reference.  Frames run in the reorder pyramid's
 coding order (me_range_scale 4, 2, 1, 1), the input advances every frame.
 
@@ -146,7 +148,7 @@ def _profile_entry(args, kernel, bd, kind):
     return None
 
 
-def timed_run(engine, group, steps, warmup, sync=None):
+def timed_run(engine, group, steps, warmup, sync=None, finish=None):
     """W untimed frames (the key frame first), then exactly K timed coded
     frames bracketed by a barrier and a device sync on both sides; returns
     (max-over-ranks seconds, result words of the last frame).  `engine` is a
@@ -167,6 +169,8 @@ def timed_run(engine, group, steps, warmup, sync=None):
         drain()
     if sync:
         sync()  # device-wide: every frame on every stream has finished
+    if finish:
+        finish()  # the host's share of the frames (F8's range coder) has finished too
     t1 = time.perf_counter()
     group.barrier()
     # the verification checksums are not part of a frame: outside the timing
@@ -195,24 +199,27 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     nin = len(hip_inputs)
     db = bool(flags & RP.RV_REPLAY_DEBLOCK)
     cd = bool(flags & RP.RV_REPLAY_CDEF)
+    ent = bool(flags & RP.RV_REPLAY_ENTROPY)
     c = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=threads, L=L,
-                    speed=speed, deblock=db, cdef=cd)
+                    speed=speed, deblock=db, cdef=cd, entropy=ent)
     for i in range(nin):
         c.set_input(i, hip_inputs[i])
     c.frame()  # the key frame (a copy), untimed
-    cpu_words = []
+    cpu_words, cpu_ent = [], []
     n, tc0 = 0, time.perf_counter()
     while n < 4 or (time.perf_counter() - tc0 < args.cpu_seconds and n < nin - 6):
         c.frame()
         n += 1
         cpu_words.append(c.results())  # a memcpy + sums; kept inside the timing
+        if ent:
+            cpu_ent.append(c.entropy_stats()[:3])
     tc = time.perf_counter() - tc0
     c.close()
     # 1 thread: the first 1/8 of the superblocks of one GOP
     nsb = ((W + 63) // 64) * ((H + 63) // 64)
     lim = max(1, nsb // 8)
     c1 = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=1, L=L,
-                     speed=speed, deblock=db, cdef=cd)
+                     speed=speed, deblock=db, cdef=cd, entropy=ent)
     for i in range(nin):
         c1.set_input(i, hip_inputs[i])
     c1.frame()
@@ -234,7 +241,7 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     # the GPU replay over the same frames, word for word
     g = RP.HipReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=n_inputs,
                      flags=flags & (RP.RV_REPLAY_SPEED6 | RP.RV_REPLAY_DEBLOCK |
-                                    RP.RV_REPLAY_CDEF))
+                                    RP.RV_REPLAY_CDEF | RP.RV_REPLAY_ENTROPY))
     g.synth_inputs(0)
     g.frame()
     bad = []
@@ -244,10 +251,14 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
         d = np.nonzero(gw != cpu_words[i])[0]
         if d.size:
             bad.append({"frame": i, "n_diff": int(d.size), "first": int(d[0])})
+        if ent and g.entropy_stats()[:3] != cpu_ent[i]:
+            bad.append({"frame": i, "entropy": "coefficient bytes differ"})
     g.close()
     R._check(R.lib().rv_device_sync(), "rv_device_sync")
     parity = {"frames": n, "words": int(sum(w.size for w in cpu_words)),
               "bit_exact": not bad, "vs": "oracle/orc_replay.c (CPU replay)"}
+    if ent:
+        parity["coefficient_bytes"] = int(sum(e[0] for e in cpu_ent))
     if bad:
         parity["mismatches"] = bad[:8]
     return cpu, parity
@@ -341,6 +352,9 @@ def main():
     ap.add_argument("--serial-levels", action="store_true",
                     help="one instance codes every frame (default on one GPU: the level-2 "
                          "frames run on a twin instance concurrently with levels 0 / 1)")
+    ap.add_argument("--no-entropy", action="store_true",
+                    help="skip stage F8 (the coefficients' entropy coding: device tokens + "
+                         "the host range coder); default: every frame's coefficients are coded")
     ap.add_argument("--exhaustive-fs", action="store_true",
                     help="F1 coarse search without successive elimination (same results)")
     args = ap.parse_args()
@@ -363,7 +377,7 @@ def main():
     n_inputs = args.warmup + args.steps + 8  # every display the run codes
     flags = (RP.RV_REPLAY_EXHAUSTIVE_FS if args.exhaustive_fs else 0) | \
         (RP.RV_REPLAY_SPEED6 if speed == 6 else 0) | (RP.RV_REPLAY_DEBLOCK if args.deblock or args.cdef else 0) | \
-        (RP.RV_REPLAY_CDEF if args.cdef else 0)
+        (RP.RV_REPLAY_CDEF if args.cdef else 0) | (0 if args.no_entropy else RP.RV_REPLAY_ENTROPY)
     hip = RP.HipReplay(W, H, xdec, ydec, bd, nref, group=rects[rank], tile_size=ts,
                        n_inputs=n_inputs, flags=flags)
     hip.synth_inputs(0)  # the stream's frames, resident in HBM before the timing
@@ -376,8 +390,11 @@ def main():
     # HIP events on a sample of frames: every TIMING_STRIDE-th GOP
     gop = len(RP.GOP_SCALES)
     (eng if paired else hip).set_timing(TIMING_STRIDE, gop)
+    ent = not args.no_entropy
     dt, words = timed_run(eng, group, args.steps, args.warmup,
-                          sync=lambda: R._check(R.lib().rv_device_sync(), "rv_device_sync"))
+                          sync=lambda: R._check(R.lib().rv_device_sync(), "rv_device_sync"),
+                          finish=eng.entropy_stats if ent else None)
+    ent_stats = eng.entropy_stats() if ent else None
 
     # per-kernel times over the instrumented frames of the timed region
     nonkey = range(args.warmup - 1, args.warmup - 1 + args.steps)
@@ -509,7 +526,8 @@ def main():
                                    f"{'4:2:0' if xdec else '4:4:4'} speed={speed} hot-path replay of one "
                                    f"stream (BASELINE config {cfg_name}), "
                                    f"{tiling['cols']}x{tiling['rows']} tiles over {world} GPU(s), "
-                                   f"{nref} refs, reorder-pyramid coding order",
+                                   f"{nref} refs, reorder-pyramid coding order"
+                                   f"{'' if args.no_entropy else ', coefficients entropy-coded'}",
                        "width": W, "height": H, "refs": nref, "speed": speed,
                        "deblock": bool(args.deblock or args.cdef), "cdef": bool(args.cdef),
                        "tiles": [tiling["cols"], tiling["rows"]],
@@ -537,6 +555,15 @@ def main():
                                 "rounds": round(cnt[13] / ev_frames, 2),
                                 "modes_per_screen": "13 predicted + SATD, 3 RDO x (chroma "
                                                     "mode, DC)"},
+            **({"entropy": {
+                "stage": "F8: coefficients of every coded frame (write_coeffs_lv_map) tokenized on "
+                         "the GPU, range-coded on a host thread per replay instance beside the "
+                         "next frames; inside the timed region",
+                "frames": int(ent_stats[3]),
+                "coefficient_bytes_per_frame": round(ent_stats[4] / max(1, ent_stats[3]), 1),
+                "coefficient_kbit_per_frame": round(ent_stats[4] * 8 / 1e3 / max(1, ent_stats[3]), 3),
+                "scope": "coefficient syntax only (no mode / MV / partition symbols, headers)"}}
+               if ent else {}),
             "checksum": int(words[-5]) & 0xFFFFFFFF,
             **({"emulated_ranks": emu} if emu else {}),
         }

@@ -585,8 +585,10 @@ typedef struct rv_replay_cfg {
  * range-coded on a host thread beside the next frames (rv_ec_*) -- with the
  * frame's CDFs from the previous frame of its pyramid level (primary
  * reference LAST3, src/encoder.rs:776-830, 2750-2761) and the biggest
- * tile's CDFs kept (:2824-2833).  One tile group (the whole frame), xdec ==
- * ydec.  rv_replay_entropy_stats reads the result. */
+ * tile's CDFs kept (:2824-2833).  xdec == ydec.  With several tile groups
+ * each instance codes its own tiles and keeps its own biggest tile's CDFs
+ * (the frame's biggest tile in rav1e: exact with one group).
+ * rv_replay_entropy_stats reads the result. */
 #define RV_REPLAY_ENTROPY 128
 typedef struct rv_replay_frame_info {
   int32_t display;            /* display index of the coded frame */

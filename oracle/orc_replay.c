@@ -1673,12 +1673,11 @@ static void entropy_frame(orc_replay *r) {
   r->ec_stat[3]++;
 }
 
-/* Coefficient entropy coding of every coded frame; needs one tile group
- * (the biggest-tile CDF choice spans the frame's tiles) and xdec == ydec. */
+/* Coefficient entropy coding of every coded frame; xdec == ydec.  With
+ * several tile groups each codes its own tiles and keeps its own biggest
+ * tile's CDFs (rav1e: the frame's; exact with one group). */
 int orc_replay_set_entropy(orc_replay *r, int on) {
-  if (on && (r->xdec != r->ydec || r->tx0 || r->ty0 ||
-             r->tw != (r->W + 63) / 64 || r->th != (r->H + 63) / 64))
-    return -1;
+  if (on && r->xdec != r->ydec) return -1;
   r->entropy = on != 0;
   if (r->entropy && !r->mi_lg) {
     r->mi_cols = (r->W + 3) / 4;

@@ -458,15 +458,15 @@ __device__ inline void ec_sb_of(const EcFrameArgs &a, int i, int &sx, int &sy, i
   }
 }
 
-__global__ __launch_bounds__(64) void ec_gen_kernel(EcFrameArgs a, EcFrameBufs b, int pass) {
-  const int i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= a.nsb) return;
+// The jobs of superblock i (coding order): count (out == nullptr) or write
+// them from out[0].  Leaves in z-order by a depth-first walk of the block
+// map (a 64x64 leaf costs one read).
+__device__ int ec_sb_jobs(const EcFrameArgs &a, int i, rv_ec_job *out, int cap) {
   int sx, sy, t, first, rowstart, t0x, t0y;
   ec_sb_of(a, i, sx, sy, t, first, rowstart, t0x, t0y);
-  uint32_t o = pass ? b.sb_off[i] : 0;
   int n = 0;
   auto put = [&](const rv_ec_job &jb) {
-    if (pass && o + n < (uint32_t)b.max_jobs) b.jobs[o + n] = jb;
+    if (out && n < cap) out[n] = jb;
     n++;
   };
   rv_ec_job z{};
@@ -482,18 +482,28 @@ __global__ __launch_bounds__(64) void ec_gen_kernel(EcFrameArgs a, EcFrameBufs b
     put(j2);
   }
   const int sb = (sy - a.ty0) * a.tw + (sx - a.tx0);
-  for (int m = 0; m < 256; m++) {
-    int dx = 0, dy = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      dx |= ((m >> (2 * k)) & 1) << k;
-      dy |= ((m >> (2 * k + 1)) & 1) << k;
-    }
-    const int x4 = sx * 16 + dx, y4 = sy * 16 + dy;
+  int stk[16][3];
+  int sp = 0;
+  stk[sp][0] = sx * 16;
+  stk[sp][1] = sy * 16;
+  stk[sp][2] = 6;
+  sp++;
+  while (sp > 0) {
+    sp--;
+    const int x4 = stk[sp][0], y4 = stk[sp][1], lg = stk[sp][2];
     if (x4 >= a.mi_cols || y4 >= a.mi_rows) continue;
     const int code = a.mi_lg[(size_t)y4 * a.mi_stride + x4];
-    const int n4 = 1 << code, lg = code + 2;
-    if ((dx & (n4 - 1)) || (dy & (n4 - 1))) continue;  // not the leaf's top-left
+    if (code != lg - 2) {  // split: the children, popped in z-order
+      const int h = 1 << (lg - 3);
+      for (int c = 3; c >= 0; c--) {
+        stk[sp][0] = x4 + (c & 1) * h;
+        stk[sp][1] = y4 + (c >> 1) * h;
+        stk[sp][2] = lg - 1;
+        sp++;
+      }
+      continue;
+    }
+    const int n4 = 1 << code;
     rv_ec_job jb = z;
     jb.bx = x4 - t0x * 16;
     jb.by = y4 - t0y * 16;
@@ -512,11 +522,10 @@ __global__ __launch_bounds__(64) void ec_gen_kernel(EcFrameArgs a, EcFrameBufs b
     } else {
       bi = (y4 / n4 - L.y0) * L.gw + (x4 / n4 - L.x0);
     }
-    const int ltx = min(lg - 2, 4);
     jb.kind = 0;
     jb.is_inter = inter;
     jb.plane = 0;
-    jb.tx_size = ltx;
+    jb.tx_size = min(lg - 2, 4);
     jb.bw_lg = jb.bh_lg = lg;
     jb.coeffs = L.l_lev + (size_t)bi * (l == 0 ? 1024 : L.B * L.B);
     put(jb);
@@ -540,21 +549,84 @@ __global__ __launch_bounds__(64) void ec_gen_kernel(EcFrameArgs a, EcFrameBufs b
         put(jc);
       }
   }
-  if (!pass) b.sb_off[i] = (uint32_t)n;
+  return n;
 }
 
-// the jobs count, every tile's first token, the total (host-mapped stat)
-__global__ void ec_ranges_kernel(EcFrameBufs b, int nsb, const EcFrameArgs a) {
-  const int t = threadIdx.x;
-  const uint32_t nj = b.sb_off[nsb];
-  if (t == 0) {
-    b.stat[0] = b.dstat[0];
-    b.stat[1] = b.dstat[1] || nj > (uint32_t)b.max_jobs;
-    b.stat[2] = nj;
-    b.stat[3 + b.ntiles] = b.dstat[0];
+// block-wide exclusive scan of one value per thread (1024 threads)
+__device__ inline uint32_t block_scan_1024(uint32_t x, uint32_t *s, uint32_t &total) {
+  s[threadIdx.x] = x;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const uint32_t t = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+    __syncthreads();
+    s[threadIdx.x] += t;
+    __syncthreads();
   }
-  if (t < b.ntiles) {
-    // the first superblock of tile t: the tiles before it hold their sizes
+  total = s[1023];
+  const uint32_t r = s[threadIdx.x] - x;
+  __syncthreads();
+  return r;
+}
+
+// Every superblock's job count (pass 0) / its jobs at the scanned offset
+// (pass 1), one thread per superblock.
+__global__ __launch_bounds__(64) void ec_gen_kernel(EcFrameArgs a, EcFrameBufs b, int pass) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= a.nsb) return;
+  if (!pass) {
+    b.sb_off[i] = (uint32_t)ec_sb_jobs(a, i, nullptr, 0);
+    return;
+  }
+  const uint32_t o = b.sb_off[i];
+  if (o < (uint32_t)b.max_jobs) ec_sb_jobs(a, i, b.jobs + o, b.max_jobs - (int)o);
+}
+
+// One workgroup: the exclusive scan of the superblocks' job counts;
+// sb_off[nsb] = the job count (clamped to max_jobs, overflow flagged)
+__global__ __launch_bounds__(1024) void ec_sb_scan_kernel(EcFrameArgs a, EcFrameBufs b) {
+  __shared__ uint32_t s[1024];
+  uint32_t carry = 0;
+  for (int c0 = 0; c0 < a.nsb; c0 += 1024) {
+    const int i = c0 + threadIdx.x;
+    const uint32_t x = i < a.nsb ? b.sb_off[i] : 0;
+    uint32_t total;
+    const uint32_t o = carry + block_scan_1024(x, s, total);
+    if (i < a.nsb) b.sb_off[i] = o;
+    carry += total;
+  }
+  if (threadIdx.x == 0) {
+    b.sb_off[a.nsb] = carry < (uint32_t)b.max_jobs ? carry : b.max_jobs;
+    if (carry > (uint32_t)b.max_jobs) b.dstat[1] = 1;
+  }
+}
+
+// One workgroup: the exclusive scan of the jobs' token counts, then the
+// host-mapped stat: [total, overflow, jobs, first token of every tile, total]
+__global__ __launch_bounds__(1024) void ec_scan_frame_kernel(EcFrameArgs a, EcFrameBufs b) {
+  __shared__ uint32_t s[1024];
+  const int n = (int)b.sb_off[a.nsb];
+  uint32_t carry = 0;
+  for (int c0 = 0; c0 < n; c0 += 1024) {
+    const int i = c0 + threadIdx.x;
+    const uint32_t x = i < n ? b.offsets[i] : 0;
+    uint32_t total;
+    const uint32_t o = carry + block_scan_1024(x, s, total);
+    if (i < n) b.offsets[i] = o;
+    carry += total;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    b.offsets[n] = carry;
+    b.dstat[0] = carry;
+    const bool over = b.dstat[1] || carry > b.cap;
+    b.dstat[1] = over;
+    b.stat[0] = carry;
+    b.stat[1] = over;
+    b.stat[2] = (uint32_t)n;
+    b.stat[3 + b.ntiles] = carry;
+  }
+  if ((int)threadIdx.x < b.ntiles) {  // tile t's first superblock -> its first job's token
+    const int t = threadIdx.x;
     const int ntx = (a.tw + a.tws - 1) / a.tws;
     int base = 0;
     for (int k = 0; k < t; k++) {
@@ -566,10 +638,7 @@ __global__ void ec_ranges_kernel(EcFrameBufs b, int nsb, const EcFrameArgs a) {
 }
 
 int ec_frame_tokens(const EcFrameArgs &a, const EcFrameBufs &b, hipStream_t st) {
-  ec_gen_kernel<<<(a.nsb + 63) / 64, 64, 0, st>>>(a, b, 0);
-  uint32_t *bsum = (uint32_t *)((char *)b.scratch + (size_t)b.max_jobs * 4);
-  ec_scan(b.sb_off, a.nsb, nullptr, bsum, nullptr, st);
-  ec_gen_kernel<<<(a.nsb + 63) / 64, 64, 0, st>>>(a, b, 1);
+  if (b.ntiles > 1024) return rv_set_error(RV_EINVAL, "ec_frame_tokens: more than 1024 tiles");
   EcArgs e;
   e.jobs = b.jobs;
   e.n = b.max_jobs;
@@ -578,19 +647,21 @@ int ec_frame_tokens(const EcFrameArgs &a, const EcFrameBufs &b, hipStream_t st) 
   e.ydec = a.ydec;
   e.map_w4 = b.map_w4;
   e.map_h4 = b.map_h4;
-  e.map = b.map;
+  e.map = b.map;  // every visible 4x4 of a tile is stored by its leaf before it is read
   e.count = b.offsets;
   e.eob = (int32_t *)b.scratch;
   e.tokens = b.tokens;
   e.cap = b.cap;
   e.status = b.dstat;
-  if (hipMemsetAsync(b.map, 0, (size_t)b.ntiles * 3 * b.map_w4 * b.map_h4, st) != hipSuccess)
-    return rv_set_error(RV_EHIP, "ec_frame_tokens: map clear");
-  // grid-stride over the device-side job count: 2048 workgroups of 4 waves
-  ec_prep_kernel<<<2048, 256, 0, st>>>(e);
-  ec_scan(b.offsets, b.max_jobs, e.dn, bsum, b.dstat, st);
-  ec_token_kernel<<<2048, 256, 0, st>>>(e);
-  ec_ranges_kernel<<<1, 256, 0, st>>>(b, a.nsb, a);
+  if (hipMemsetAsync(b.dstat, 0, 8, st) != hipSuccess)
+    return rv_set_error(RV_EHIP, "ec_frame_tokens: status");
+  ec_gen_kernel<<<(a.nsb + 63) / 64, 64, 0, st>>>(a, b, 0);
+  ec_sb_scan_kernel<<<1, 1024, 0, st>>>(a, b);
+  ec_gen_kernel<<<(a.nsb + 63) / 64, 64, 0, st>>>(a, b, 1);
+  // grid-stride over the device-side job count
+  ec_prep_kernel<<<1024, 256, 0, st>>>(e);
+  ec_scan_frame_kernel<<<1, 1024, 0, st>>>(a, b);
+  ec_token_kernel<<<1024, 256, 0, st>>>(e);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

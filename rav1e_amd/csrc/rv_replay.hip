@@ -760,6 +760,11 @@ struct rv_replay {
   EcFrameBufs ecb{};
   EcHost *ech = nullptr;
   long ec_frames = 0;
+  // F8 runs on its own stream after the frame's block map, beside F7 and the
+  // next frame's F0..F4; the next commit (F6) waits for it
+  hipStream_t ecs = nullptr;
+  hipEvent_t ev_f8fork = nullptr, ev_f8done = nullptr;
+  bool f8_pending = false;
   // intra-mode screening (rv_intra_pass.hip; speed 10, 4:2:0)
   bool intra = false;
   uint8_t *i_elig = nullptr, *i_was = nullptr, *i_win = nullptr, *i_modes = nullptr;
@@ -1368,6 +1373,7 @@ void rv_replay_destroy(rv_replay *r) {
   // stream running)
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->side) (void)hipStreamSynchronize(r->side);
+  if (r->ecs) (void)hipStreamSynchronize(r->ecs);
   if (r->ech) {  // the host coder finishes the frames it holds, then stops
     {
       std::lock_guard<std::mutex> lk(r->ech->mu);
@@ -1383,6 +1389,9 @@ void rv_replay_destroy(rv_replay *r) {
     delete r->ech;
     r->ech = nullptr;
   }
+  if (r->ev_f8fork) (void)hipEventDestroy(r->ev_f8fork);
+  if (r->ev_f8done) (void)hipEventDestroy(r->ev_f8done);
+  if (r->ecs) (void)hipStreamDestroy(r->ecs);
   for (hipStream_t es : r->edge)
     if (es) (void)hipStreamSynchronize(es);
   for (void *p : r->allocs) (void)hipFree(p);
@@ -1644,8 +1653,8 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     if (r->cdef_idx) (void)hipMemsetAsync(r->cdef_idx, 0, n64, r->stream);
   }
   r->entropy = (cfg->flags & RV_REPLAY_ENTROPY) != 0;
-  if (r->entropy && (g.xdec != g.ydec || g.tx0 || g.ty0 || g.tw != sbc || g.th != sbr)) {
-    rv_set_error(RV_EINVAL, "rv_replay_create: RV_REPLAY_ENTROPY needs the whole frame, xdec == ydec");
+  if (r->entropy && g.xdec != g.ydec) {
+    rv_set_error(RV_EINVAL, "rv_replay_create: RV_REPLAY_ENTROPY needs xdec == ydec");
     rv_replay_destroy(r);
     return nullptr;
   }
@@ -1690,8 +1699,14 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
                          hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
            hipHostMalloc((void **)&eh->stat_h[k], ((size_t)b.ntiles + 8) * 4,
                          hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
-           hipEventCreate(&eh->ev[k]) == hipSuccess;
+           // blocking sync: the coder thread sleeps instead of spinning on the GPU
+           hipEventCreateWithFlags(&eh->ev[k], hipEventBlockingSync | hipEventDisableTiming) ==
+               hipSuccess;
     }
+    if (getenv("RAV1E_HIP_F8_STREAM") && atoi(getenv("RAV1E_HIP_F8_STREAM")))
+      ok = ok && hipStreamCreateWithFlags(&r->ecs, hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev_f8fork, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev_f8done, hipEventDisableTiming) == hipSuccess;
     if (ok) eh->th = std::thread([eh] { eh->run(); });
   }
   r->imp_bx = g.vis_w / 8;
@@ -1916,8 +1931,6 @@ int rv_replay_set_groups(rv_replay *r, int n_groups, const int32_t *rects, int m
   if (rects[4 * my_group] != g.tx0 || rects[4 * my_group + 1] != g.ty0 ||
       rects[4 * my_group + 2] != g.tw || rects[4 * my_group + 3] != g.th)
     return rv_set_error(RV_EINVAL, "rv_replay_set_groups: my group != the configured tile group");
-  if (r->entropy && n_groups > 1)
-    return rv_set_error(RV_EINVAL, "rv_replay_set_groups: RV_REPLAY_ENTROPY codes one group");
   memcpy(r->grects, rects, (size_t)n_groups * 4 * sizeof(int32_t));
   r->n_groups = n_groups;
   r->my_group = my_group;
@@ -2409,6 +2422,11 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   }
   if (r->intra) RV_R(intra_begin(r));
   RV_EV(9);
+  // the previous frame's F8 still reads the committed levels and the block map
+  if (r->f8_pending) {
+    RV_H(hipStreamWaitEvent(st, r->ev_f8done, 0));
+    r->f8_pending = false;
+  }
   // F6 commit the winners into the frame: the levels' leaves (speed 10: on
   // the edge stream, beside the superblocks' commit)
   if (edge) {
@@ -2507,10 +2525,21 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     EcFrameBufs b = r->ecb;
     RV_H(hipHostGetDevicePointer((void **)&b.tokens, eh->tok_h[slot], 0));
     RV_H(hipHostGetDevicePointer((void **)&b.stat, eh->stat_h[slot], 0));
-    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 4], st));
-    RV_R(ec_frame_tokens(ea, b, st));
-    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 5], st));
-    RV_H(hipEventRecord(eh->ev[slot], st));
+    // RAV1E_HIP_F8_STREAM=1: on its own stream (A/B; default: the main one)
+    const bool own = r->ecs != nullptr;
+    hipStream_t es = own ? r->ecs : st;
+    if (own) {
+      RV_H(hipEventRecord(r->ev_f8fork, st));
+      RV_H(hipStreamWaitEvent(r->ecs, r->ev_f8fork, 0));
+    }
+    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 4], es));
+    RV_R(ec_frame_tokens(ea, b, es));
+    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 5], es));
+    RV_H(hipEventRecord(eh->ev[slot], es));
+    if (own) {
+      RV_H(hipEventRecord(r->ev_f8done, r->ecs));
+      r->f8_pending = true;
+    }
     const int q = r->lv[lv].qidx;
     {
       std::lock_guard<std::mutex> lk(eh->mu);

@@ -124,3 +124,6 @@ class TileParallel:
 
     def results(self):
         return self.engine.results()
+
+    def entropy_stats(self):
+        return self.engine.entropy_stats()

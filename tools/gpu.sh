@@ -9,6 +9,7 @@
 #                                     MI355X guide's rule: FETCH_SIZE and WRITE_SIZE do not
 #                                     share a pass)
 #   tools/gpu.sh envbench TAG CFG "ENV=.." ... [-- ARGS]  one bench line per environment (A/B)
+#   tools/gpu.sh argbench TAG CFG "ARGS" ...  one bench line per argument set (A/B)
 #   tools/gpu.sh ubench TAG           tools/ubench binaries (VALU issue rates, PMC calibration)
 #
 # Every step has its own time limit (tools/gpu_step.sh); a crash, abort or
@@ -50,6 +51,15 @@ case "$MODE" in
     steps=(); i=0
     for e in "${envs[@]}"; do
       steps+=("400 $TAG/envbench_$i.log env $e python $R/bench.py --config $CFG --no-cpu-baseline --emulate-ranks 0 $*")
+      i=$((i + 1))
+    done
+    exec bash "$R/tools/gpu_step.sh" "${steps[@]}" ;;
+  argbench)
+    # one bench line per argument set: argbench TAG CFG "ARGS1" "ARGS2" ...
+    CFG=$1; shift
+    steps=(); i=0
+    for a in "$@"; do
+      steps+=("400 $TAG/argbench_$i.log python $R/bench.py --config $CFG --no-cpu-baseline --emulate-ranks 0 $a")
       i=$((i + 1))
     done
     exec bash "$R/tools/gpu_step.sh" "${steps[@]}" ;;
