@@ -510,8 +510,9 @@ int orc_replay_set_deblock(orc_replay *r, int on) {
   r->mi_rows = (r->H + 3) / 4;
   free(r->mi_lg);
   free(r->mi_skip);
-  r->mi_lg = calloc((size_t)r->mi_cols * r->mi_rows, 1);
+  r->mi_lg = malloc((size_t)r->mi_cols * r->mi_rows);
   r->mi_skip = calloc((size_t)r->mi_cols * r->mi_rows, 1);
+  if (r->mi_lg) memset(r->mi_lg, 4, (size_t)r->mi_cols * r->mi_rows);  /* as the device's */
   return r->mi_lg && r->mi_skip ? 0 : -1;
 }
 
@@ -1590,7 +1591,7 @@ static const int32_t *ec_coeffs(const orc_replay *r, int lg, int x4, int y4, int
 static void ec_walk(const orc_replay *r, ec_list *L, int x4, int y4, int lg, int t0x4, int t0y4) {
   if (x4 >= r->mi_cols || y4 >= r->mi_rows) return;
   const int code = r->mi_lg[(size_t)y4 * r->mi_cols + x4];
-  if (code != lg - 2) {
+  if (code != lg - 2 && lg > 3) {  /* 8x8 is the smallest partition */
     const int h = 1 << (lg - 3);
     ec_walk(r, L, x4, y4, lg - 1, t0x4, t0y4);
     ec_walk(r, L, x4 + h, y4, lg - 1, t0x4, t0y4);
@@ -1682,9 +1683,10 @@ int orc_replay_set_entropy(orc_replay *r, int on) {
   if (r->entropy && !r->mi_lg) {
     r->mi_cols = (r->W + 3) / 4;
     r->mi_rows = (r->H + 3) / 4;
-    r->mi_lg = calloc((size_t)r->mi_cols * r->mi_rows, 1);
+    r->mi_lg = malloc((size_t)r->mi_cols * r->mi_rows);
     r->mi_skip = calloc((size_t)r->mi_cols * r->mi_rows, 1);
     if (!r->mi_lg || !r->mi_skip) return -1;
+    memset(r->mi_lg, 4, (size_t)r->mi_cols * r->mi_rows);  /* 64x64 until written */
   }
   return 0;
 }
