@@ -502,8 +502,9 @@ def main():
     fps = args.steps / dt  # frames of the one stream
 
     emu = None
-    if rank == 0 and world == 1 and args.emulate_ranks > 1:
-        emu = emulate_ranks(args.emulate_ranks, W, H, xdec, ydec, bd, nref, tiling, flags)
+    n_emu = min(args.emulate_ranks, tiling["cols"] * tiling["rows"])  # one tile group per rank
+    if rank == 0 and world == 1 and n_emu > 1:
+        emu = emulate_ranks(n_emu, W, H, xdec, ydec, bd, nref, tiling, flags)
 
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
