@@ -71,6 +71,9 @@ int rv_rdo_candidates(const rv::RdoArgs &luma, const rv::RdoArgs &chroma, int hb
 // Blocks below 64x64 (speed 6): one launch over the tasks of a (luma or
 // the two chroma planes) for transform size n_tx_size; mode 0 single,
 // 1 compound (score), 2 commit.
+// a level's luma blocks (nl) and both chroma planes' (nc) in one launch
+int rv_rdo_blocks2(const rv::RdoArgs &l, const rv::RdoArgs &c, int nl, int nc, int hbd,
+                   hipStream_t s, int mode);
 int rv_rdo_blocks(const rv::RdoArgs &a, bool luma, int nplanes, int n_tx_size, int hbd,
                   hipStream_t s, int mode);
 

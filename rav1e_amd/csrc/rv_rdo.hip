@@ -1273,6 +1273,61 @@ __global__ __launch_bounds__(256) void rdo_small_kernel(RdoArgs a, int nplanes) 
                                        reinterpret_cast<Px *>(mine + SLAB), scan);
 }
 
+// One launch for a level's luma blocks (NL, plane p[0]) and both chroma
+// planes' blocks (NC): workgroups below lgrid run the luma tasks, the rest
+// the chroma ones (the partition levels' chain is launch-latency bound).
+template <typename Px, int N, int MODE, bool LUMA>
+__device__ __forceinline__ void rdo_small_part(const RdoArgs &a, int nplanes, int blk,
+                                               uint8_t *lds, uint16_t *scan) {
+  constexpr int TPW = 64 / N;
+  constexpr int SLAB = rdo_slab_bytes<Px, N>();
+  constexpr int PER = (SLAB + N * N * (int)sizeof(Px) + 15) / 16 * 16;
+  stage_scan(scan, a.q_tx_index);
+  const int wave = threadIdx.x >> 6, g = (threadIdx.x & 63) / N;
+  const int n = rdo_ntx(a), total = n * nplanes;
+  const int w0 = (blk * 4 + wave) * TPW;
+  if (w0 >= total) return;
+  const int i = w0 + g;
+  const bool valid = i < total;
+  const int ii = valid ? i : total - 1;
+  const int plane = ii / n, t = ii - plane * n;
+  uint8_t *mine = lds + (wave * TPW + g) * PER;
+  rdo_cand_body<Px, N, N, MODE, LUMA>(a, a.p[plane], t, valid, reinterpret_cast<int32_t *>(mine),
+                                       reinterpret_cast<Px *>(mine + SLAB), scan);
+}
+
+template <typename Px, int N>
+constexpr int rdo_small_lds() {
+  return 4 * (64 / N) * ((rdo_slab_bytes<Px, N>() + N * N * (int)sizeof(Px) + 15) / 16 * 16);
+}
+
+template <typename Px, int NL, int NC, int MODE>
+__global__ __launch_bounds__(256) void rdo_small2_kernel(RdoArgs l, RdoArgs c, int lgrid) {
+  constexpr int BL = rdo_small_lds<Px, NL>(), BC = rdo_small_lds<Px, NC>();
+  __shared__ __align__(16) uint8_t lds[BL > BC ? BL : BC];
+  __shared__ uint16_t scan[1024];
+  if ((int)blockIdx.x < lgrid)
+    rdo_small_part<Px, NL, MODE, true>(l, 1, blockIdx.x, lds, scan);
+  else
+    rdo_small_part<Px, NC, MODE, false>(c, 2, blockIdx.x - lgrid, lds, scan);
+}
+
+template <int NL, int NC>
+static void rdo_small2_launch(const RdoArgs &l, const RdoArgs &c, int hbd, hipStream_t s,
+                              int mode) {
+  const int lg = (l.n_tx + 4 * (64 / NL) - 1) / (4 * (64 / NL));
+  const int cg = (c.n_tx * 2 + 4 * (64 / NC) - 1) / (4 * (64 / NC));
+  const unsigned grid = (unsigned)(lg + cg);
+  if (grid == 0) return;
+#define RV_SMALL2(PX, M) rdo_small2_kernel<PX, NL, NC, M><<<grid, 256, 0, s>>>(l, c, lg)
+  if (hbd) {
+    if (mode == 0) RV_SMALL2(uint16_t, 0); else if (mode == 1) RV_SMALL2(uint16_t, 1); else RV_SMALL2(uint16_t, 2);
+  } else {
+    if (mode == 0) RV_SMALL2(uint8_t, 0); else if (mode == 1) RV_SMALL2(uint8_t, 1); else RV_SMALL2(uint8_t, 2);
+  }
+#undef RV_SMALL2
+}
+
 template <int N, bool LUMA>
 static void rdo_small_launch(const RdoArgs &a, int nplanes, int hbd, hipStream_t s, int mode) {
   constexpr int TPW = 64 / N;
@@ -1343,6 +1398,19 @@ int rv_rdo_intra(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipStream_
 
 // The speed-6 levels: luma N x N (N = 32, 16, 8; cdef distortion) or the
 // chroma planes' transform blocks (N = 16, 8, 4 in 4:2:0; SSE) of every task.
+int rv_rdo_blocks2(const RdoArgs &l, const RdoArgs &c, int nl, int nc, int hbd, hipStream_t s,
+                   int mode) {
+  if (nl == 32 && nc == 16) rdo_small2_launch<32, 16>(l, c, hbd, s, mode);
+  else if (nl == 16 && nc == 8) rdo_small2_launch<16, 8>(l, c, hbd, s, mode);
+  else if (nl == 8 && nc == 4) rdo_small2_launch<8, 4>(l, c, hbd, s, mode);
+  else if (nl == 32 && nc == 32) rdo_small2_launch<32, 32>(l, c, hbd, s, mode);
+  else if (nl == 16 && nc == 16) rdo_small2_launch<16, 16>(l, c, hbd, s, mode);
+  else if (nl == 8 && nc == 8) rdo_small2_launch<8, 8>(l, c, hbd, s, mode);
+  else return rv_set_error(RV_EINVAL, "rv_rdo_blocks2: sizes");
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
 int rv_rdo_blocks(const RdoArgs &a, bool luma, int nplanes, int n_tx_size, int hbd,
                   hipStream_t s, int mode) {
   if (luma) {

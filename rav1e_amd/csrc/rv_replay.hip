@@ -2269,8 +2269,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       c.tx_size = P.txc;
       ll[l] = a;
       lc6[l] = c;
-      RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, es, 0));
-      RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, es, 0));
+      RV_R(rv_rdo_blocks2(a, c, P.B, P.bc, g.hbd, es, 0));
     }
     return RV_OK;
   };
@@ -2284,8 +2283,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       a.count = c.count = P.cand_count + 1;
       a.cand_base = c.cand_base = 0;
       a.n_tx = c.n_tx = P.n * cg.comp;
-      RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, es, 1));
-      RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, es, 1));
+      RV_R(rv_rdo_blocks2(a, c, P.B, P.bc, g.hbd, es, 1));
     }
     return RV_OK;
   };
@@ -2312,8 +2310,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       a.list = c.list = P.leaf;
       a.count = c.count = r->leaf_count + l;
       a.n_tx = c.n_tx = P.n;
-      RV_R(rv_rdo_blocks(a, true, 1, P.B, g.hbd, es, 2));
-      RV_R(rv_rdo_blocks(c, false, 2, P.bc, g.hbd, es, 2));
+      RV_R(rv_rdo_blocks2(a, c, P.B, P.bc, g.hbd, es, 2));
     }
     return RV_OK;
   };
