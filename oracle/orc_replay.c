@@ -97,6 +97,17 @@ typedef struct orc_replay {
   orc_qctx qs[3][4][3];
   uint8_t *leaf0;
   size_t nwords, wpart;
+  /* speed 10: the superblocks' MV stacks are rav1e's (find_mvrefs over the
+   * tile's coded blocks, orc_mvref.c); the block grid of the group (4x4
+   * units, pitch tw * 16) and each superblock's stacks (first two entries;
+   * n = min(len, 2); the compound stack always holds two) */
+  int exact;
+  orc_blk *bgrid;
+  struct ostk {
+    int n[2];
+    orc_mv s[2][2];
+    orc_mv c[2][2];
+  } *stk;
   /* RV_REPLAY_DEBLOCK (orc_replay_set_deblock): the block map, fast levels */
   int deblock, mi_cols, mi_rows;
   uint8_t db_levels[4]; /* the last deblocked frame's levels */
@@ -274,13 +285,57 @@ static cgeo level_geo(const orc_replay *r, int l) {
   cgeo g = {P->n, P->gw, P->tx0, P->ty0, P->tws, P->ths, P->sub};
   return g;
 }
+/* The superblocks' candidates: speed 10 from rav1e's stacks (r->stk), speed
+ * 6 from the neighbour-NEWMV stand-in above.  rdo_mode_decision
+ * (src/rdo.rs:880-905, 949-986): NEARESTMV = stack[0] (zero if empty),
+ * NEAR0MV = stack[1] if len > 1, pushed if the stack is non-empty, GLOBALMV
+ * (zero) if len >= 2, NEWMV if the search MV is non-zero and not among the
+ * first two entries. */
 static int cand_mv(const orc_replay *r, int sb, int c, orc_mv *mv) {
-  cgeo g = sb_geo(r);
-  return cand_mv_g(&g, sb, c, mv);
+  if (!r->exact) {
+    cgeo g = sb_geo(r);
+    return cand_mv_g(&g, sb, c, mv);
+  }
+  const int k = c / NMODE, m = c % NMODE;
+  const struct ostk *s = &r->stk[sb];
+  const int n = s->n[k];
+  const orc_mv zero = {0, 0};
+  switch (m) {
+    case 0:
+      *mv = n >= 1 ? s->s[k][0] : zero;
+      return 1;
+    case 1:
+      *mv = n >= 2 ? s->s[k][1] : zero;
+      return n >= 1;
+    case 2:
+      *mv = zero;
+      return n >= 2;
+    default: {
+      const orc_mv me = r->sub[(size_t)k * r->nsb + sb];
+      *mv = me;
+      return !(n >= 1 && mv_eq(s->s[k][0], me)) && !(n >= 2 && mv_eq(s->s[k][1], me)) &&
+             (me.row != 0 || me.col != 0);
+    }
+  }
 }
+/* RAV1E_INTER_COMPOUND_MODES over the (ref 0, ref 1) stack, which the extra
+ * search always fills to two entries (src/context.rs:2858-2906) */
 static void comp_mvs(const orc_replay *r, int sb, int m, orc_mv *mv0, orc_mv *mv1) {
-  cgeo g = sb_geo(r);
-  comp_mvs_g(&g, sb, m, mv0, mv1);
+  if (!r->exact) {
+    cgeo g = sb_geo(r);
+    comp_mvs_g(&g, sb, m, mv0, mv1);
+    return;
+  }
+  const struct ostk *s = &r->stk[sb];
+  const orc_mv zero = {0, 0}, me0 = r->sub[sb], me1 = r->sub[r->nsb + sb];
+  switch (m) {
+    case 0: *mv0 = zero; *mv1 = zero; break;               /* GLOBAL_GLOBALMV */
+    case 1: *mv0 = s->c[0][0]; *mv1 = s->c[0][1]; break;   /* NEAREST_NEARESTMV */
+    case 2: *mv0 = me0; *mv1 = me1; break;                 /* NEW_NEWMV */
+    case 3: *mv0 = s->c[0][0]; *mv1 = me1; break;          /* NEAREST_NEWMV */
+    case 4: *mv0 = me0; *mv1 = s->c[0][1]; break;          /* NEW_NEARESTMV */
+    default: *mv0 = s->c[1][0]; *mv1 = s->c[1][1]; break;  /* NEAR_NEARMV */
+  }
 }
 
 static int edge_levels(orc_replay *r);
@@ -348,6 +403,10 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile
   r->nwords = (size_t)r->nsb * (WPR * r->R + 4);
   r->words = calloc(r->nwords, 8);
   r->lev = calloc((size_t)r->nsb * (1024 + 2 * r->ntx_c * 1024), 4);
+  r->exact = 1;
+  r->bgrid = malloc((size_t)r->tw * 16 * r->th * 16 * sizeof(orc_blk));
+  r->stk = calloc(r->nsb, sizeof(*r->stk));
+  if (!r->bgrid || !r->stk) return NULL;
   pthread_mutex_init(&r->mu, NULL);
   if (edge_levels(r)) return NULL;
   return r;
@@ -384,6 +443,8 @@ void orc_replay_destroy(orc_replay *r) {
   free(r->sc);
   free(r->words);
   free(r->lev);
+  free(r->bgrid);
+  free(r->stk);
   free_levels(r);
   free(r->mi_lg);
   free(r->mi_skip);
@@ -498,6 +559,7 @@ int orc_replay_set_speed(orc_replay *r, int speed) {
   if (speed == 10 || r->s6) return 0;
   if (r->xdec != r->ydec) return -1;
   r->s6 = 1;
+  r->exact = 0; /* speed 6: the neighbour-NEWMV stand-in */
   return alloc_levels(r, 0, 0, r->tw, r->th);
 }
 
@@ -948,6 +1010,39 @@ static void run_half(orc_replay *r, int sb) {
   }
 }
 
+/* F3 motion_estimation of the 64x64 (src/me.rs:193-278): the full-pel
+ * diamond from zero and the coarse MV, then sub-pel; the rate predictors
+ * pmv are the first two entries of the reference's MV stack
+ * (rdo_mode_decision, src/rdo.rs:858-870; zero without the exact stacks). */
+static void me64_sb(orc_replay *r, int sb) {
+  const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
+  const sbgeo g = sb_geo_of(r, sb);
+  const double me_lambda = r->lv[r->fi.level].me_lambda;
+  uint32_t lambda1 = (uint32_t)(me_lambda * 256.0 * 0.5);
+  const orc_mv zero = {0, 0};
+  for (int k = 0; k < r->R; k++) {
+    const oslot *ref = &r->slots[r->fi.ref_display[k] % NSLOT];
+    orc_ds_ctx c;
+    orc_mv fmv, smv;
+    uint64_t cost;
+    orc_mv fp[2] = {zero, coarse_fp(r, k, sb)};
+    ds_at(r, &c, &g, &cur->y, &ref->y, g.tsx * 16, g.tsy * 16, 64, 0, 0, lambda1);
+    if (r->exact) {
+      const struct ostk *s = &r->stk[sb];
+      c.pmv[0] = s->n[k] >= 1 ? s->s[k][0] : zero;
+      c.pmv[1] = s->n[k] >= 2 ? s->s[k][1] : zero;
+    }
+    orc_diamond_search(&c, fp, 2, &fmv, &cost);
+    r->full[k * r->nsb + sb] = fmv;
+    r->fc[k * r->nsb + sb] = cost;
+    c.subpel = 1;
+    c.satd = r->s6; /* use_satd_subpel (speed <= 9) */
+    orc_diamond_search(&c, &fmv, 1, &smv, &cost);
+    r->sub[k * r->nsb + sb] = smv;
+    r->sc[k * r->nsb + sb] = cost;
+  }
+}
+
 /* Pass A3: the lookahead's build_full_res_pmvs (src/encoder.rs:3021-3166,
  * 16x16 full-pel vs the references' original frames), F3 motion_estimation
  * of the 64x64 (src/me.rs:193-278: zero + the coarse MV, then sub-pel) and
@@ -1003,20 +1098,9 @@ static void run_me(orc_replay *r, int sb) {
       }
 #undef PM
   }
-  for (int k = 0; k < R; k++) {
-    orc_ds_ctx c;
-    orc_mv fmv, smv;
-    orc_mv fp[2] = {zero, coarse_fp(r, k, sb)};
-    ds_at(r, &c, &g, &cur->y, &ref[k]->y, g.tsx * 16, g.tsy * 16, 64, 0, 0, lambda1);
-    orc_diamond_search(&c, fp, 2, &fmv, &cost);
-    r->full[k * r->nsb + sb] = fmv;
-    r->fc[k * r->nsb + sb] = cost;
-    c.subpel = 1;
-    c.satd = r->s6; /* use_satd_subpel (speed <= 9) */
-    orc_diamond_search(&c, &fmv, 1, &smv, &cost);
-    r->sub[k * r->nsb + sb] = smv;
-    r->sc[k * r->nsb + sb] = cost;
-  }
+  /* speed 10: the 64x64 search needs the superblock's MV stack (its pmv),
+   * so it runs in coding order (chain_tile) */
+  if (!r->exact) me64_sb(r, sb);
   /* the levels (speed 6: every superblock; speed 10: the frame-edge
    * rectangle): motion_estimation of every 32x32, then 16x16 and 8x8 block
    * of the superblock at its own position (src/me.rs:193-278), seeded with
@@ -1524,6 +1608,134 @@ static void intra_tile(orc_replay *r, int t) {
     for (int x = tx0; x < tx0 + r->tws && x < r->tw; x++) intra_sb(r, y * r->tw + x);
 }
 
+/* ---- speed 10 in coding order: rav1e's MV stacks -------------------------
+ * encode_tile codes a tile's superblocks in raster order
+ * (src/encoder.rs:3190-3235); rdo_mode_decision's find_mvrefs reads the
+ * blocks coded before (above, left, top-right, top-left), and the 64x64
+ * search's rate predictors are that stack's first two entries.  So per
+ * superblock: the stacks, F3, the inter candidates (run_rdo), the intra
+ * screening, and its blocks into the grid for the ones after it. */
+
+/* the Block fields of the group grid (FrameBlocks::new: Block::default,
+ * src/context.rs:1425-1442: intra, 64x64) */
+static void grid_reset(orc_replay *r) {
+  const size_t n = (size_t)r->tw * 16 * r->th * 16;
+  const orc_blk d = {{ORC_INTRA_FRAME, ORC_INTRA_FRAME}, 16, 16, 0, {0, 0, 0}, {{0, 0}, {0, 0}}};
+  for (size_t i = 0; i < n; i++) r->bgrid[i] = d;
+}
+/* a coded block (group 4x4 units x, y, size w4 x h4) into the grid:
+ * candidate c (single: reference c / NMODE; compound: c >= C), intra if
+ * c >= INTRA_C */
+static void grid_set(orc_replay *r, int x, int y, int w4, int h4, int c, orc_mv m0, orc_mv m1) {
+  orc_blk b;
+  memset(&b, 0, sizeof(b));
+  b.n4_w = (uint8_t)w4;
+  b.n4_h = (uint8_t)h4;
+  if (c >= INTRA_C) {
+    b.ref[0] = ORC_INTRA_FRAME;
+    b.ref[1] = ORC_NONE_FRAME;
+  } else if (c < r->C) {
+    b.ref[0] = (int8_t)(1 + c / NMODE);
+    b.ref[1] = ORC_NONE_FRAME;
+    b.mv[0] = m0;
+    b.newmv = c % NMODE == 3; /* NEWMV (pushed only for a non-zero MV) */
+  } else {
+    const int m = c - r->C;
+    b.ref[0] = 1;
+    b.ref[1] = 2;
+    b.mv[0] = m0;
+    b.mv[1] = m1;
+    b.newmv = m >= 2 && m <= 4; /* NEW_NEWMV, NEAREST_NEWMV, NEW_NEARESTMV */
+  }
+  const int gs = r->tw * 16, gh = r->th * 16;
+  for (int j = y; j < y + h4 && j < gh; j++)
+    for (int i = x; i < x + w4 && i < gs; i++) r->bgrid[(size_t)j * gs + i] = b;
+}
+/* the coded blocks of superblock sb: its 64x64 winner, or the leaves the
+ * partition committed (their candidates come from the levels' stand-in) */
+static void record_sb(orc_replay *r, int sb) {
+  const int sx = sb % r->tw, sy = sb / r->tw;
+  const uint64_t *w = r->words + (size_t)sb * (WPR * r->R + 4) + WPR * r->R;
+  if (!r->lvl || r->leaf0[sb]) {
+    const int c = (int)w[0];
+    orc_mv m0 = {0, 0}, m1 = {0, 0};
+    if (c < r->C)
+      (void)cand_mv(r, sb, c, &m0);
+    else if (c < INTRA_C)
+      comp_mvs(r, sb, c - r->C, &m0, &m1);
+    grid_set(r, sx * 16, sy * 16, 16, 16, c, m0, m1);
+    return;
+  }
+  int ex, ey;
+  if (!in_rect(r, sb, &ex, &ey)) return;
+  for (int l = 1; l < 4; l++) {
+    const struct olevel *P = &r->pl[l];
+    const int k2 = 1 << l, n4 = 16 >> l;
+    const cgeo g = level_geo(r, l);
+    for (int j = 0; j < k2; j++)
+      for (int i = 0; i < k2; i++) {
+        const int b = (ey * k2 + j) * P->gw + ex * k2 + i;
+        if (!P->leaf[b]) continue;
+        const int c = (int)r->words[P->woff + (size_t)b * (4 * r->R + 4) + 4 * r->R];
+        orc_mv m0 = {0, 0}, m1 = {0, 0};
+        if (c < r->C)
+          (void)cand_mv_g(&g, b, c, &m0);
+        else
+          comp_mvs_g(&g, b, c - r->C, &m0, &m1);
+        grid_set(r, sx * 16 + i * n4, sy * 16 + j * n4, n4, n4, c, m0, m1);
+      }
+  }
+}
+/* find_mvrefs of the 64x64 of superblock sb for every reference and, on
+ * compound frames, the (ref 0, ref 1) pair (src/rdo.rs:847-943);
+ * ref_frame_sign_bias: the backward references (src/encoder.rs:842-855) */
+static void stacks_sb(orc_replay *r, int sb) {
+  const sbgeo g = sb_geo_of(r, sb);
+  const int gs = r->tw * 16;
+  const orc_blk *tile = r->bgrid + (size_t)(g.t0y - r->ty0) * 16 * gs + (size_t)(g.t0x - r->tx0) * 16;
+  uint8_t sbias[2] = {0, 0};
+  for (int k = 0; k < r->R; k++) sbias[k] = r->fi.ref_display[k] > r->fi.display;
+  struct ostk *s = &r->stk[sb];
+  memset(s, 0, sizeof(*s));
+  /* a superblock past the frame edge is split (must_split): its 64x64 is
+   * evaluated but never coded, with empty stacks */
+  if (r->lvl && edge_sb(r, sb)) return;
+  orc_mv_cand st[9];
+  int n;
+  for (int k = 0; k < r->R; k++) {
+    const int rf[2] = {1 + k, ORC_NONE_FRAME};
+    orc_find_mvrefs(tile, gs, g.mi_w, g.mi_h, g.t0x * 16, g.t0y * 16, r->w_in_b, r->h_in_b,
+                    g.tsx * 16, g.tsy * 16, 16, 16, rf, sbias, st, &n);
+    s->n[k] = n < 2 ? n : 2;
+    if (n >= 1) s->s[k][0] = st[0].this_mv;
+    if (n >= 2) s->s[k][1] = st[1].this_mv;
+  }
+  if (r->fi.compound) {
+    const int rf[2] = {1, 2};
+    orc_find_mvrefs(tile, gs, g.mi_w, g.mi_h, g.t0x * 16, g.t0y * 16, r->w_in_b, r->h_in_b,
+                    g.tsx * 16, g.tsy * 16, 16, 16, rf, sbias, st, &n);
+    for (int i = 0; i < 2; i++) {
+      s->c[i][0] = st[i].this_mv;
+      s->c[i][1] = st[i].comp_mv;
+    }
+  }
+}
+/* one tile (index t of the group's tiles) in raster order */
+static void chain_tile(orc_replay *r, int t, uint64_t tail[3]) {
+  const int gtx = (r->tw + r->tws - 1) / r->tws;
+  const int tx0 = (t % gtx) * r->tws, ty0 = (t / gtx) * r->ths;
+  for (int y = ty0; y < ty0 + r->ths && y < r->th; y++)
+    for (int x = tx0; x < tx0 + r->tws && x < r->tw; x++) {
+      const int sb = y * r->tw + x;
+      if (r->sb_limit > 0 && sb >= r->sb_limit) continue; /* a bounded timing sample */
+      stacks_sb(r, sb);
+      me64_sb(r, sb);
+      run_rdo(r, sb, tail);
+      if (r->intra) intra_sb(r, sb);
+      record_sb(r, sb);
+    }
+}
+
 void orc_replay_intra_stats(const orc_replay *r, uint64_t out[2]) {
   out[0] = r->istat[0];
   out[1] = r->istat[1];
@@ -1701,7 +1913,7 @@ static void *worker(void *arg) {
   orc_replay *r = arg;
   uint64_t tail[3] = {0, 0, 0};
   int lim = r->sb_limit > 0 && r->sb_limit < r->nsb ? r->sb_limit : r->nsb;
-  if (r->pass == 4) /* the group's tiles */
+  if (r->pass >= 4) /* the group's tiles */
     lim = ((r->tw + r->tws - 1) / r->tws) * ((r->th + r->ths - 1) / r->ths);
   for (;;) {
     pthread_mutex_lock(&r->mu);
@@ -1716,8 +1928,10 @@ static void *worker(void *arg) {
       run_me(r, sb);
     else if (r->pass == 3)
       run_rdo(r, sb, tail);
+    else if (r->pass == 4)
+      intra_tile(r, sb); /* passes 4, 5: `sb` counts tiles */
     else
-      intra_tile(r, sb); /* pass 4: `sb` counts tiles */
+      chain_tile(r, sb, tail);
   }
   pthread_mutex_lock(&r->mu);
   for (int i = 0; i < 3; i++) r->tail[i] += tail[i];
@@ -1780,9 +1994,17 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
   downsample(r, &S->qres, &S->hres);
   memset(r->tail, 0, sizeof(r->tail));
   r->sb_limit = sb_limit;
-  for (int pass = 0; pass < 4; pass++) run_pass(r, pass);
   r->istat[0] = r->istat[1] = 0;
-  if (r->intra) run_pass(r, 4);
+  if (r->exact) {
+    /* speed 10: F1, F2, the lookahead and the levels' searches, then each
+     * tile in coding order (F3, F4, F6, F6b per superblock) */
+    for (int pass = 0; pass < 3; pass++) run_pass(r, pass);
+    grid_reset(r);
+    run_pass(r, 5);
+  } else {
+    for (int pass = 0; pass < 4; pass++) run_pass(r, pass);
+    if (r->intra) run_pass(r, 4);
+  }
   if (r->deblock || r->entropy) map_own(r);
   if (r->entropy) entropy_frame(r);
   if (r->deblock && pad_recon) loop_filter_planes(r);  /* tile groups: after the imports */

@@ -206,6 +206,32 @@ void orc_diamond_search(const orc_ds_ctx *c, const orc_mv *pred, int n_pred,
 /* telescopic_subpel_search (src/me.rs:858-941): best_mv / lowest_cost are
  * the search's start (in) and result (out). */
 void orc_telescopic_subpel(const orc_ds_ctx *c, orc_mv *best_mv, uint64_t *lowest_cost);
+/* ---- MV reference stack (src/context.rs:2308-2965), orc_mvref.c -------- */
+/* RefType codes: INTRA_FRAME 0, reference k of the replay 1 + k, NONE 8 */
+#define ORC_INTRA_FRAME 0
+#define ORC_NONE_FRAME 8
+/* the fields of Block (src/context.rs:1395-1440) the scans read; newmv: the
+ * mode counts as a NEWMV one in add_ref_mv_candidate */
+typedef struct {
+  int8_t ref[2];
+  uint8_t n4_w, n4_h, newmv, pad_[3];
+  orc_mv mv[2];
+} orc_blk;
+typedef struct {
+  orc_mv this_mv, comp_mv;
+  uint32_t weight;
+} orc_mv_cand; /* CandidateMV */
+/* find_mvrefs of the block at tile 4x4 offset (bx, by), bw4 x bh4, over a
+ * tile grid (pitch stride, tile size cols x rows in 4x4 units, origin
+ * tile_mi_x / y in the frame, frame size frame_cols x frame_rows);
+ * ref_frames[1] = ORC_NONE_FRAME for a single reference; sign_bias[k] of
+ * reference k.  Writes the stack (<= 9 entries) and its length; returns
+ * the mode context. */
+int orc_find_mvrefs(const orc_blk *grid, int stride, int cols, int rows, int tile_mi_x,
+                    int tile_mi_y, int frame_cols, int frame_rows, int bx, int by, int bw4,
+                    int bh4, const int ref_frames[2], const uint8_t *sign_bias,
+                    orc_mv_cand stack[9], int *n_out);
+
 /* tx-domain distortion (src/encoder.rs:1210-1224). */
 uint64_t orc_tx_dist(const int32_t *coeffs, const int32_t *rcoeffs, int coded_area,
                      int tx_w, int tx_h);

@@ -62,11 +62,25 @@ __device__ inline void chain_emit(const ChainNext &c, int job, int n_per_ref, in
 // Superblock grid of a replay instance: a rectangle of whole AV1 tiles
 // (uniform tile size tws x ths superblocks, TilingInfo, src/tiling/tiler.rs:
 // 49-126) at superblock (tx0, ty0) of the frame, tw x th superblocks.
+// rav1e's MV stacks of a superblock (find_mvrefs, src/context.rs:2650-2965,
+// built by mvref_kernel in coding-order rounds, rv_mvref.hip): per
+// reference k the first two entries and n = min(len, 2); the compound
+// (ref 0, ref 1) stack's first two (this, comp) pairs -- its extra search
+// always leaves two (:2858-2906).
+struct MvStack {
+  int32_t n[2];
+  rv_mv s[2][2];
+  rv_mv c[2][2];
+};
+
 struct CandGeo {
   int nsb, tw, th, tx0, ty0, tws, ths;
   int R;     // references searched
   int M;     // inter modes per reference (kCandModes)
   int comp;  // compound candidates after the R * M single ones (0 or kCompModes)
+  // rav1e's stacks (speed 10 superblocks); null: the neighbour-NEWMV
+  // stand-in below (the speed-6 / frame-edge levels)
+  const MvStack *stk;
 };
 
 // Per reference, rav1e pushes (src/rdo.rs:880-905, speed 10: no near MVs
@@ -95,6 +109,12 @@ __host__ __device__ inline bool mv_eq(rv_mv a, rv_mv b) { return a.row == b.row 
 // count (0..2); s0 / s1 the entries (scalars: no scratch on the device).
 __host__ __device__ inline int cand_stack(const CandGeo &g, const rv_fs_result *sub, int sb,
                                           int k, rv_mv &s0, rv_mv &s1) {
+  if (g.stk) {
+    const MvStack &m = g.stk[sb];
+    s0 = m.s[k][0];
+    s1 = m.s[k][1];
+    return m.n[k];
+  }
   const int sx = sb % g.tw, sy = sb / g.tw;
   const int fx = g.tx0 + sx, fy = g.ty0 + sy;
   // neighbours inside the grid and the tile (a level grid over the frame-edge
@@ -119,6 +139,14 @@ __host__ __device__ inline int cand_stack(const CandGeo &g, const rv_fs_result *
 // scratch on the device); returns the count.
 __host__ __device__ inline int comp_stack(const CandGeo &g, const rv_fs_result *sub, int sb,
                                           rv_mv &e00, rv_mv &e01, rv_mv &e10, rv_mv &e11) {
+  if (g.stk) {
+    const MvStack &m = g.stk[sb];
+    e00 = m.c[0][0];
+    e01 = m.c[0][1];
+    e10 = m.c[1][0];
+    e11 = m.c[1][1];
+    return 2;
+  }
   const int sx = sb % g.tw, sy = sb / g.tw;
   const int fx = g.tx0 + sx, fy = g.ty0 + sy;
   // neighbours inside the grid and the tile (a level grid over the frame-edge

@@ -95,6 +95,8 @@ struct DsArgs {
   ChainNext next;   // replay: feed the winner into the next stage's jobs
   int tele;         // 1: telescopic_subpel_search instead of the diamond
   const rv_fs_result *start;  // tele: the search's start (best_mv, lowest_cost)
+  // replay rounds: only jobs j with active[j % n_per_ref] set run (null: all)
+  const uint8_t *active;
 };
 
 __device__ __forceinline__ void ds_write(const DsArgs &a, int job, rv_mv center,
@@ -302,6 +304,7 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a) {
 
   const int job = xcd_job(a.n);
   if (job >= a.n) return;  // whole workgroup, uniformly
+  if (a.active && !a.active[job % a.n_per_ref]) return;  // settled this round
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const rv_ds_job *jp = a.jobs + job;  // pred[] read through the pointer
@@ -746,6 +749,7 @@ __global__ __launch_bounds__(kDsThreads) void diamond_kernel(DsArgs a) {
   __shared__ uint64_t red[kDsWaves];
   const int job = blockIdx.x;
   if (job >= a.n) return;
+  if (a.active && !a.active[job % a.n_per_ref]) return;
   const rv_ds_job jb = a.jobs[job];
   const rv_plane &ref = a.ref[job / a.n_per_ref];
   const int w = a.w, h = a.h;
@@ -897,6 +901,7 @@ __global__ __launch_bounds__(64) void ds_wave_kernel(DsArgs a) {
   constexpr int B = (int)sizeof(Px);
   const int job = xcd_job(a.n);
   if (job >= a.n) return;
+  if (a.active && !a.active[job % a.n_per_ref]) return;
   const int lane = threadIdx.x;
   const rv_ds_job *jp = a.jobs + job;
   const rv_ds_job jb = *jp;
@@ -1338,7 +1343,7 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
 }
 template <typename Px>
 bool try_grp(const DsArgs &a, hipStream_t s) {
-  if (a.tele || a.w != a.h) return false;
+  if (a.tele || a.w != a.h || a.active) return false;
   const int n = a.w;
   const bool small = n == 8 || n == 16;
   if (!(small || (a.satd && (n == 32 || n == 64)))) return false;
@@ -1425,7 +1430,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             const rv_ds_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
                             int subpixel, int use_satd, int allow_hp, int bit_depth,
                             rv_fs_result *d_out, uint32_t *d_evals, const ChainNext *next,
-                            void *stream) {
+                            void *stream, const uint8_t *active) {
   auto p2 = [](int v) { return v >= 4 && v <= 128 && (v & (v - 1)) == 0; };
   if (!org || !refs || n_refs < 1 || n_refs > RV_DS_MAX_PRED || n_per_ref < 0 || !p2(blk_w) ||
       !p2(blk_h) || (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
@@ -1451,6 +1456,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
   a.hp = allow_hp ? 1 : 0;
   a.bd = bit_depth;
   a.evals = d_evals;
+  a.active = active;
   if (next) a.next = *next;
   return ds_dispatch(a, stream);
 }
@@ -1489,7 +1495,7 @@ extern "C" int rv_diamond_search_batch(const rv_plane *org, const rv_plane *ref,
                                        rv_fs_result *d_out, void *stream) {
   if (!ref) return rv_set_error(RV_EINVAL, "rv_diamond_search_batch: null ref");
   return rv_diamond_search_multi(org, ref, 1, d_jobs, n, blk_w, blk_h, subpixel, use_satd,
-                                 allow_hp, bit_depth, d_out, nullptr, nullptr, stream);
+                                 allow_hp, bit_depth, d_out, nullptr, nullptr, stream, nullptr);
 }
 
 // telescopic_subpel_search (src/me.rs:858-941) for every job in one launch:

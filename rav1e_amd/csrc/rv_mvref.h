@@ -1,0 +1,70 @@
+// rv_mvref.h -- rav1e's MV reference stacks of the replay's 64x64
+// superblocks (rv_mvref.hip), driven by rv_replay_frame's coding-order
+// rounds (DESIGN.md §3 "MV stacks in coding order").
+#pragma once
+
+#include "rv_chain.h"
+#include "rv_rdo.h"
+
+namespace rv {
+
+// RefType codes of a coded block (src/partition.rs RefType): INTRA_FRAME 0,
+// the replay's reference k is 1 + k, NONE_FRAME 8
+constexpr int kIntraFrame = 0, kNoneFrame = 8;
+
+// The fields of a coded block (Block, src/context.rs:1395-1440) that
+// find_mvrefs reads: ref_frames and mv.
+struct BlkDec {
+  int8_t ref[2];
+  int8_t newmv, pad;
+  rv_mv mv[2];
+};
+
+struct MvrefArgs {
+  // the group's superblock grid, its tiles and the frame (4x4 units)
+  int nsb, tw, th, tx0, ty0, tws, ths, W, H, w_in_b, h_in_b;
+  int R, comp;             // references; compound stack on this frame
+  uint8_t sign_bias[2];    // ref_frame_sign_bias of reference k
+  const BlkDec *dec;       // the superblocks' coded blocks
+  const uint8_t *iwas;     // null, or 1: the superblock is an intra winner
+  MvStack *stk;            // in / out: the stacks the superblocks were evaluated with
+  uint8_t *active;         // out: 1 = (re-)evaluate this round
+  int32_t *count;          // out: += superblocks marked
+  rv_ds_job *jf, *js;      // the F3 jobs [R][nsb]: pmv = the stack's first two
+  int init;                // 1: mark every superblock (the frame's first round)
+  // speed 10 frame-edge leaves (a top-right neighbour past the right edge):
+  // lvl = the edge superblocks are split; per level 1..3 (those holding
+  // leaves) the winners, sub-pel MVs and candidate geometry
+  int lvl;
+  const RdoWinner *lwin[4];
+  const rv_fs_result *lsub[4];
+  CandGeo lcg[4];
+};
+
+// The decision record of superblock sb's winner (candidate c of the
+// superblock grid cg, or an intra word)
+__device__ inline BlkDec blk_dec_of(const CandGeo &cg, const rv_fs_result *sub, int sb, int c) {
+  BlkDec d;
+  d.ref[1] = kNoneFrame;
+  d.newmv = 0;
+  d.pad = 0;
+  d.mv[0] = d.mv[1] = rv_mv{0, 0};
+  const int ns = cg.R * cg.M;
+  if (c >= 1000 || c < 0 || c >= ns + kCompModes) {  // kIntraWord (the range guards the reads)
+    d.ref[0] = kIntraFrame;
+  } else if (c < ns) {
+    d.ref[0] = (int8_t)(1 + c / cg.M);
+    (void)cand_mv(cg, sub, sb, c, &d.mv[0]);
+    d.newmv = (c % cg.M) == kNewMv;
+  } else {
+    d.ref[0] = 1;
+    d.ref[1] = 2;
+    comp_mvs(cg, sub, sb, c - ns, &d.mv[0], &d.mv[1]);
+    d.newmv = (c - ns) >= kNewNew && (c - ns) <= kNewNearest;
+  }
+  return d;
+}
+
+}  // namespace rv
+
+int rv_mvref_round(const rv::MvrefArgs &a, hipStream_t s);

@@ -33,6 +33,7 @@
 #include <string.h>
 
 #include <condition_variable>
+#include <algorithm>
 #include <deque>
 #include <mutex>
 #include <thread>
@@ -43,6 +44,7 @@
 #include "rv_ec.h"
 #include "rv_intra.h"
 #include "rv_intra_pass.h"
+#include "rv_mvref.h"
 #include "rv_rdo.h"
 
 #if __has_include(<rccl/rccl.h>)
@@ -62,7 +64,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             const rv_ds_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
                             int subpixel, int use_satd, int allow_hp, int bit_depth,
                             rv_fs_result *d_out, uint32_t *d_evals, const rv::ChainNext *next,
-                            void *stream);
+                            void *stream, const uint8_t *active = nullptr);
 // rv_deblock.hip
 int rv_deblock_plane_dev(const rv_plane *p, int pli, int width, int height, const uint8_t *d_lg,
                          const uint8_t *d_skip, int mi_stride, const uint8_t levels[4],
@@ -215,11 +217,14 @@ __global__ __launch_bounds__(64) void score_candidates(
     const uint64_t *uout, const uint64_t *vout, int ntx_c, RdoWinner *win,
     const rv_fs_result *coarse, const rv_fs_result *half, const rv_fs_result *full,
     const rv_fs_result *look, uint64_t *words, int32_t *cand_count,
-    unsigned long long *imp_sum, uint32_t *evals, int32_t *leaf_count) {
+    unsigned long long *imp_sum, uint32_t *evals, int32_t *leaf_count, const uint8_t *active,
+    BlkDec *dec, int round) {
   const int sb = blockIdx.x * 64 + threadIdx.x;
   if (sb == 0) {  // F4's lists are consumed: ready for the next frame; F5 sums next
-    evals[0] = (uint32_t)cand_count[0];  // single-reference candidates evaluated
-    evals[1] = (uint32_t)cand_count[1];  // compound ones
+    // single-reference and compound candidates evaluated (summed over the
+    // MV-stack rounds)
+    evals[0] = (round ? evals[0] : 0u) + (uint32_t)cand_count[0];
+    evals[1] = (round ? evals[1] : 0u) + (uint32_t)cand_count[1];
     cand_count[0] = cand_count[1] = 0;
     if (imp_sum) *imp_sum = 0;  // null: F5 ran on the side stream (it zeroed its sum)
     if (leaf_count)  // speed 6: the partition decision appends next
@@ -227,8 +232,14 @@ __global__ __launch_bounds__(64) void score_candidates(
   }
   __shared__ RdoWinner ws[64];
   if (sb < g.nsb) {
-    const RdoWinner w = block_argmin(cg, lambda, ds_u, ds_v, sub, lout, uout, vout, ntx_c, sb);
-    win[sb] = w;
+    RdoWinner w;
+    if (!active || active[sb]) {  // a superblock evaluated this round
+      w = block_argmin(cg, lambda, ds_u, ds_v, sub, lout, uout, vout, ntx_c, sb);
+      win[sb] = w;
+      if (dec) dec[sb] = blk_dec_of(cg, sub, sb, w.c);
+    } else {
+      w = win[sb];
+    }
     ws[threadIdx.x] = w;
   }
   __syncthreads();
@@ -291,13 +302,14 @@ __global__ void fill_preds_kernel(rv_ds_job *jobs, const int32_t *src, int n,
 // (the order of the list does not matter: every output is indexed by the
 // candidate).
 __global__ __launch_bounds__(256) void cand_list_kernel(CandGeo cg, const rv_fs_result *sub,
-                                                         int n, int32_t *list, int32_t *count) {
+                                                         int n, int32_t *list, int32_t *count,
+                                                         const uint8_t *active = nullptr) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   bool v = false;
   if (i < n) {
     rv_mv mv;
     const int c = i / cg.nsb, sb = i - c * cg.nsb;
-    v = cand_live(cg, sub, sb, c, &mv);
+    v = (!active || active[sb]) && cand_live(cg, sub, sb, c, &mv);
   }
   const uint64_t m = __ballot(v);
   const int lane = threadIdx.x & 63;
@@ -309,12 +321,13 @@ __global__ __launch_bounds__(256) void cand_list_kernel(CandGeo cg, const rv_fs_
 // The compound candidates (all pushed on SELECT frames) without repeated
 // MV pairs: entries are absolute candidate indices nsingle + m * nsb + sb.
 __global__ __launch_bounds__(256) void comp_list_kernel(CandGeo cg, const rv_fs_result *sub,
-                                                         int nsingle, int32_t *list, int32_t *count) {
+                                                         int nsingle, int32_t *list, int32_t *count,
+                                                         const uint8_t *active = nullptr) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   bool v = false;
   if (i < cg.comp * cg.nsb) {
     const int mm = i / cg.nsb, sb = i - mm * cg.nsb;
-    v = comp_live(cg, sub, sb, mm);
+    v = (!active || active[sb]) && comp_live(cg, sub, sb, mm);
   }
   const uint64_t m = __ballot(v);
   const int lane = threadIdx.x & 63;
@@ -775,6 +788,14 @@ struct rv_replay {
   void *i_edges = nullptr;
   uint64_t *i_lout = nullptr, *i_cout = nullptr;
   uint32_t *i_stats = nullptr; // [kRing][3]: screened, intra winners, rounds
+  // speed 10: rav1e's MV stacks (rv_mvref.hip) in coding-order rounds
+  bool exact = false;
+  MvStack *stk = nullptr;              // the stacks each superblock was evaluated with
+  BlkDec *dec_lv[3] = {nullptr, nullptr, nullptr};  // decisions, per pyramid level
+  uint8_t *mv_active = nullptr;        // re-evaluate this round
+  int32_t *mv_cnt = nullptr, *h_mv = nullptr;  // marked count (device, pinned host)
+  bool edge_tr = false;                // a stack reads a frame-edge leaf (top-right)
+  long mv_round_sum = 0, mv_reeval = 0;  // rounds per frame and re-evaluations, summed
   size_t nwords = 0, wpart = 0;   // result words; offset of the partition masks
   bool jobs_built = false;
   std::vector<RvSlot> slots;
@@ -1396,6 +1417,7 @@ void rv_replay_destroy(rv_replay *r) {
     if (es) (void)hipStreamSynchronize(es);
   for (void *p : r->allocs) (void)hipFree(p);
   if (r->h_cnt) (void)hipHostFree(r->h_cnt);
+  if (r->h_mv) (void)hipHostFree(r->h_mv);
   for (int f = 0; f < rv_replay::kRing; f++)
     for (int i = 0; i < rv_replay::kEv; i++)
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
@@ -1636,6 +1658,31 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
          hipEventCreateWithFlags(&r->ev_ielig, hipEventDisableTiming) == hipSuccess;
     if (r->i_was) (void)hipMemsetAsync(r->i_was, 0, n, r->stream);
     if (r->i_win) (void)hipMemsetAsync(r->i_win, 0, 2 * n, r->stream);
+  }
+  // speed 10: rav1e's MV stacks in coding-order rounds
+  r->exact = !r->s6;
+  if (r->exact) {
+    const size_t n = (size_t)g.nsb;
+    r->stk = (MvStack *)dalloc(r, n * sizeof(MvStack));
+    for (int l = 0; l < 3; l++) {
+      r->dec_lv[l] = (BlkDec *)dalloc(r, n * sizeof(BlkDec));
+      if (r->dec_lv[l]) (void)hipMemsetAsync(r->dec_lv[l], 0, n * sizeof(BlkDec), r->stream);
+      ok = ok && r->dec_lv[l];
+    }
+    r->mv_active = (uint8_t *)dalloc(r, n);
+    r->mv_cnt = (int32_t *)dalloc(r, 4);
+    ok = ok && r->stk && r->mv_active && r->mv_cnt &&
+         hipHostMalloc((void **)&r->h_mv, 16, hipHostMallocDefault) == hipSuccess;
+    // does a superblock's top-right neighbour (same tile) lie past the right
+    // frame edge, i.e. is it a must_split leaf?
+    for (int sb = 0; sb < g.nsb && r->lvl; sb++) {
+      const int fsx = g.tx0 + sb % g.tw, fsy = g.ty0 + sb / g.tw;
+      const int t0x = fsx - fsx % g.tws;
+      const int cols = std::min(g.tws * 16, g.w_in_b - t0x * 16);
+      if ((fsx + 1) * 64 <= g.W && (fsy + 1) * 64 <= g.H && fsy % g.ths != 0 &&
+          (fsx - t0x) * 16 + 16 < cols && (fsx + 2) * 64 > g.W)
+        r->edge_tr = true;
+    }
   }
   if (cfg->flags & RV_REPLAY_CDEF) {
     if (!(cfg->flags & RV_REPLAY_DEBLOCK) || (g.W & 7) || (g.H & 7)) {
@@ -2023,6 +2070,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   const int lv = fi.level;
   CandGeo cg = r->cg;
   cg.comp = fi.compound ? kCompModes : 0;
+  cg.stk = r->exact ? r->stk : nullptr;  // speed 10: rav1e's stacks (rv_mvref.hip)
   const RvInput &cur = r->inputs[fi.display % r->inputs.size()];
   const RvSlot &S = r->slots[fi.display % kSlots];
   const RvSlot *ref[2];
@@ -2346,58 +2394,147 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     RV_H(hipEventRecord(e[rv_replay::kStageEv + 3], st));
   }
 
+  // speed 10: the levels' work (edge rectangle) does not depend on the
+  // superblocks' and, without edge streams, runs first: the stack rounds may
+  // read their leaves (a top-right neighbour past the right frame edge)
+  const bool lv_early = r->exact && r->lvl && !edge;
+  if (lv_early) {
+    RV_R(lv_me(st));
+    lv_lists(st, false);
+    if (cg.comp) lv_lists(st, true);
+    RV_R(lv_rdo(st));
+    if (cg.comp) RV_R(lv_rdo_comp(st));
+    lv_score(st);
+  }
+  // speed 10: rav1e's MV stacks in coding-order rounds (rv_mvref.hip): round
+  // 0 evaluates every superblock with the stacks of this level's previous
+  // frame's decisions (a guess), each later round re-evaluates the
+  // superblocks whose stacks changed, until none does
+  MvrefArgs ma;
+  memset(&ma, 0, sizeof(ma));
+  if (r->exact) {
+    ma.nsb = g.nsb;
+    ma.tw = g.tw;
+    ma.th = g.th;
+    ma.tx0 = g.tx0;
+    ma.ty0 = g.ty0;
+    ma.tws = g.tws;
+    ma.ths = g.ths;
+    ma.W = g.W;
+    ma.H = g.H;
+    ma.w_in_b = g.w_in_b;
+    ma.h_in_b = g.h_in_b;
+    ma.R = g.R;
+    ma.comp = cg.comp ? 1 : 0;
+    for (int k = 0; k < g.R; k++) ma.sign_bias[k] = fi.ref_display[k] > fi.display;
+    ma.dec = r->dec_lv[lv];
+    ma.stk = r->stk;
+    ma.active = r->mv_active;
+    ma.count = r->mv_cnt;
+    ma.jf = r->jobs_full[lv];
+    ma.js = r->jobs_sub[lv];
+    ma.init = 1;
+    ma.lvl = r->lvl ? 1 : 0;
+    if (r->lvl)
+      for (int l = 1; l < kLevels; l++)
+        if (r->lv_used[l]) {
+          ma.lwin[l] = r->pl[l].win;
+          ma.lsub[l] = r->pl[l].sub;
+          ma.lcg[l] = r->pl[l].cg;
+        }
+    if (edge && r->edge_tr)  // the leaves the stacks read
+      for (int l = 1; l < kLevels; l++)
+        if (r->lv_used[l]) RV_H(hipStreamWaitEvent(st, r->ev_ejoin[l], 0));
+    RV_H(hipMemsetAsync(r->mv_cnt, 0, sizeof(int32_t), st));
+    RV_R(rv_mvref_round(ma, st));
+  }
+  const uint8_t *act = r->exact ? r->mv_active : nullptr;
+  // F4's arguments (la / ca become F6's commit arguments below; the rounds
+  // after the intra pass evaluate candidates again)
+  const RdoArgs la4 = la, ca4 = ca;
   // F3 full-res full-pel diamond -> sub-pel predictor; sub-pel diamond
-  // (speed 10: SAD, no hp) -> NEWMV of every superblock and reference
-  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
-                               r->full, ev_full, &to_sub, st));
-  RV_EV(5);
-  RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, r->s6 ? 1 : 0,
-                               0, g.bd, r->sub, ev_sub, nullptr, st));
-  if (r->lvl && !edge) RV_R(lv_me(st));
-  // the valid candidates (a few microseconds; bracketed with F3 sub-pel;
-  // the count was zeroed by the previous frame's argmin or at creation)
-  cand_list_kernel<<<(nsingle + 255) / 256, 256, 0, st>>>(cg, r->sub, nsingle, r->cand_list,
-                                                          r->cand_count);
-  if (r->lvl && !edge) lv_lists(st, false);
-  if (cg.comp) {  // the compound lists (after the single ones in the same arrays)
-    comp_list_kernel<<<(g.nsb * cg.comp + 255) / 256, 256, 0, st>>>(
-        cg, r->sub, nsingle, r->cand_list + nsingle, r->cand_count + 1);
-    if (r->lvl && !edge) lv_lists(st, true);
-  }
-  RV_EV(6);
-  // F4 every valid candidate, luma + both chroma planes in one fused launch
-  RV_R(rv_rdo_candidates(la, ca, g.hbd, st));
-  if (r->lvl && !edge) RV_R(lv_rdo(st));
-  if (cg.comp) {  // the compound candidates (all pushed), distinct MV pairs from the list
-    RdoArgs lc = la, cc = ca;
-    lc.list = cc.list = r->cand_list + nsingle;
-    lc.count = cc.count = r->cand_count + 1;
-    lc.cand_base = cc.cand_base = 0;
-    lc.n_tx = g.nsb * cg.comp;
-    cc.n_tx = g.nsb * cg.comp * ntx_c;
-    RV_EV(7);
-    RV_R(rv_rdo_candidates(lc, cc, g.hbd, st, true));
-    if (r->lvl && !edge) RV_R(lv_rdo_comp(st));
-  } else {
-    RV_EV(7);
-  }
-  RV_EV(8);
-  if (r->overlap) RV_H(hipStreamWaitEvent(st, r->ev_join, 0));  // the lookahead's MVs
-  score_candidates<<<(g.nsb + 63) / 64, 64, 0, st>>>(g, cg, L.lambda, L.ds[1], L.ds[2], r->sub,
-                                                     r->l_out,
-                                                     r->c_out, r->c_out + nct * 3, ntx_c, r->win,
-                                                     r->coarse, r->half, r->full, r->look,
-                                                     r->words,
-                                                     r->cand_count,
-                                                     r->overlap ? nullptr : r->tail + 2,
-                                                     r->cand_evals + 2 * slot * kLevels,
-                                                     r->leaf_count);
+  // (speed 10: SAD, no hp) -> NEWMV of every superblock and reference;
+  // the candidates; F4; the argmin (round `round` of the stacks)
+  auto f3_f4 = [&](int round) -> int {
+    RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
+                                 r->full, ev_full, &to_sub, st, act));
+    if (!round) RV_EV(5);
+    RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1,
+                                 r->s6 ? 1 : 0, 0, g.bd, r->sub, ev_sub, nullptr, st, act));
+    if (r->lvl && !edge && !lv_early) RV_R(lv_me(st));
+    // the valid candidates (a few microseconds; bracketed with F3 sub-pel;
+    // the count was zeroed by the previous argmin or at creation)
+    cand_list_kernel<<<(nsingle + 255) / 256, 256, 0, st>>>(cg, r->sub, nsingle, r->cand_list,
+                                                            r->cand_count, act);
+    if (r->lvl && !edge && !lv_early) lv_lists(st, false);
+    if (cg.comp) {  // the compound lists (after the single ones in the same arrays)
+      comp_list_kernel<<<(g.nsb * cg.comp + 255) / 256, 256, 0, st>>>(
+          cg, r->sub, nsingle, r->cand_list + nsingle, r->cand_count + 1, act);
+      if (r->lvl && !edge && !lv_early) lv_lists(st, true);
+    }
+    if (!round) RV_EV(6);
+    // F4 every valid candidate, luma + both chroma planes in one fused launch
+    RV_R(rv_rdo_candidates(la4, ca4, g.hbd, st));
+    if (r->lvl && !edge && !lv_early) RV_R(lv_rdo(st));
+    if (cg.comp) {  // the compound candidates (all pushed), distinct MV pairs from the list
+      RdoArgs lc = la4, cc = ca4;
+      lc.list = cc.list = r->cand_list + nsingle;
+      lc.count = cc.count = r->cand_count + 1;
+      lc.cand_base = cc.cand_base = 0;
+      lc.n_tx = g.nsb * cg.comp;
+      cc.n_tx = g.nsb * cg.comp * ntx_c;
+      if (!round) RV_EV(7);
+      RV_R(rv_rdo_candidates(lc, cc, g.hbd, st, true));
+      if (r->lvl && !edge && !lv_early) RV_R(lv_rdo_comp(st));
+    } else if (!round) {
+      RV_EV(7);
+    }
+    if (!round) {
+      RV_EV(8);
+      if (r->overlap) RV_H(hipStreamWaitEvent(st, r->ev_join, 0));  // the lookahead's MVs
+    }
+    score_candidates<<<(g.nsb + 63) / 64, 64, 0, st>>>(
+        g, cg, L.lambda, L.ds[1], L.ds[2], r->sub, r->l_out, r->c_out, r->c_out + nct * 3, ntx_c,
+        r->win, r->coarse, r->half, r->full, r->look, r->words, r->cand_count,
+        r->overlap ? nullptr : r->tail + 2, r->cand_evals + 2 * slot * kLevels, r->leaf_count, act,
+        r->exact ? r->dec_lv[lv] : nullptr, round);
+    return RV_OK;
+  };
+  RV_R(f3_f4(0));
+  int mv_rounds = 1;
+  // the stacks from the decisions so far; true when some superblock changed
+  auto mv_check = [&](const uint8_t *iwas) -> int {
+    ma.init = 0;
+    ma.iwas = iwas;
+    RV_H(hipMemsetAsync(r->mv_cnt, 0, sizeof(int32_t), st));
+    RV_R(rv_mvref_round(ma, st));
+    RV_H(hipMemcpyAsync(r->h_mv, r->mv_cnt, 4, hipMemcpyDeviceToHost, st));
+    RV_H(hipStreamSynchronize(st));
+    r->mv_reeval += *r->h_mv;
+    return RV_OK;
+  };
+  // the rounds after a check found *h_mv superblocks to re-evaluate; bounded
+  // by the tiles' dependency depth (every round settles the next superblock
+  // of each raster chain)
+  const int max_rounds = g.tws * g.ths + 2;
+  auto mv_rounds_run = [&](const uint8_t *iwas) -> int {
+    for (;;) {
+      RV_R(mv_check(iwas));
+      if (*r->h_mv == 0) return RV_OK;
+      if (mv_rounds >= max_rounds)
+        return rv_set_error(RV_EHIP, "rv_replay_frame: the MV-stack rounds did not converge");
+      RV_R(f3_f4(mv_rounds));
+      mv_rounds++;
+    }
+  };
+  if (r->exact) RV_R(mv_rounds_run(nullptr));
   if (r->lvl) {
     if (edge) {  // the levels' winners
       for (int l = 1; l < kLevels; l++)
         if (r->lv_used[l]) RV_H(hipStreamWaitEvent(st, r->ev_ejoin[l], 0));
-    } else
+    } else if (!lv_early) {
       lv_score(st);
+    }
     PartArgs pa;
     memset(&pa, 0, sizeof(pa));
     for (int l = 0; l < kLevels; l++) {
@@ -2449,6 +2586,23 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   RV_EV(10);
   // F6b intra-mode screening + intra RDO of the non-skip superblocks
   if (r->intra) RV_R(intra_pass(r, la, ca, cur, S, L, slot));
+  // an intra winner is no MV source (add_ref_mv_candidate skips intra
+  // blocks): the superblocks whose stacks it changes are re-decided, the
+  // frame re-committed and the intra pass re-run, until the stacks hold
+  // (the joint fixed point of the tile's coding order)
+  while (r->exact && r->intra) {
+    RV_R(mv_check(r->i_was));
+    if (*r->h_mv == 0) break;
+    if (mv_rounds >= max_rounds)
+      return rv_set_error(RV_EHIP, "rv_replay_frame: the MV-stack rounds did not converge");
+    RV_R(f3_f4(mv_rounds));
+    mv_rounds++;
+    RV_R(mv_rounds_run(r->i_was));
+    RV_R(rv_rdo_candidates(la, ca, g.hbd, st));  // F6 again: every inter winner
+    RV_R(intra_begin(r));
+    RV_R(intra_pass(r, la, ca, cur, S, L, slot));
+  }
+  if (r->exact) r->mv_round_sum += mv_rounds;
   RV_EV(11);
   // F5 importance SATD against reference 0 (the sum was zeroed by the argmin;
   // with the side stream F5 ran there, after the lookahead)

@@ -748,3 +748,27 @@ def ec_code_jobs(jobs, coeffs, cdf_init, xdec, ydec, cap=1 << 24):
                                fin.ctypes.data)
     assert total >= 0, total
     return out[:total].copy(), tb, ret, fin
+
+
+BLK = np.dtype([("ref", np.int8, 2), ("n4_w", np.uint8), ("n4_h", np.uint8), ("newmv", np.uint8),
+                ("pad", np.uint8, 3), ("mv", np.int16, (2, 2))])
+CAND = np.dtype([("this_mv", np.int16, 2), ("comp_mv", np.int16, 2), ("weight", np.uint32)])
+
+
+def find_mvrefs(grid, cols, rows, tile_x, tile_y, frame_cols, frame_rows, bx, by, bw4, bh4,
+                ref_frames, sign_bias):
+    """orc_find_mvrefs (src/context.rs:2650-2965) over grid, a (rows, pitch)
+    array of BLK: (mode_context, the stack's CAND entries)."""
+    L = lib()
+    if not getattr(L, "_mvref_bound", False):
+        L.orc_find_mvrefs.argtypes = [C.c_void_p] + [C.c_int] * 11 + [C.c_void_p] * 4
+        L.orc_find_mvrefs.restype = C.c_int
+        L._mvref_bound = True
+    g = np.ascontiguousarray(grid, dtype=BLK)
+    rf = np.array(ref_frames, np.int32)
+    sb = np.array(sign_bias, np.uint8)
+    st = np.zeros(9, CAND)
+    n = C.c_int(0)
+    ctx = L.orc_find_mvrefs(ptr(g), g.shape[1], cols, rows, tile_x, tile_y, frame_cols, frame_rows,
+                            bx, by, bw4, bh4, ptr(rf), ptr(sb), ptr(st), C.addressof(n))
+    return ctx, st[:n.value]

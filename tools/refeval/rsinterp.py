@@ -1546,6 +1546,14 @@ class Interp:
             # `for x in &mut slice`: IntoIterator for &mut [T] yields &mut T
             s = as_slice(deref(v))
             it = iter([elem_ref(s.base, s.start + i) for i in range(len(s))])
+        elif ite[0] == "path" and isinstance(deref(v), list) and \
+                any(isinstance(x, Struct) for x in deref(v)):
+            # `for x in v` over a variable: an owned collection is moved (a
+            # mutation of x is never observed) and a `&mut` one yields &mut
+            # T (`for mut c in mv_stack { c.weight += .. }`), so the elements
+            # bind by reference instead of as copies
+            lst = deref(v)
+            it = iter([elem_ref(lst, i) for i in range(len(lst))])
         else:
             it = to_iter(v)
 
@@ -1806,6 +1814,9 @@ def _int_method(v, name, args, gty):
     bits = INT_BITS.get(t, 32)
     if name == "abs":
         return wrap(abs(int(v)), ty_of(v)) if ty_of(v) else abs(v)
+    if name == "cmp":  # Ord::cmp -> Ordering as -1 / 0 / 1
+        o = int(deref(args[0]))
+        return (int(v) > o) - (int(v) < o)
     if name == "min":
         return v if v <= args[0] else args[0]
     if name == "max":
@@ -2163,6 +2174,13 @@ def _slice_method(r, name, args, gty, raw):
         return ("Err", TInt(lo, "usize"))
     if name in ("to_vec", "to_owned", "clone"):
         return s.tolist()
+    if name == "sort_by":  # stable, like slice::sort_by; the closure returns an Ordering
+        import functools
+        vals = s.tolist()
+        vals.sort(key=functools.cmp_to_key(lambda a, b: int(args[0](a, b))))
+        for i, x in enumerate(vals):
+            s.base[s.start + i] = x
+        return None
     if name == "first":
         return s[0] if len(s) else None
     if name == "last":
