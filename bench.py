@@ -80,7 +80,7 @@ def valu_peak_int():
 # with F3/F4 (RAV1E_HIP_REPLAY_SERIAL=1: both on one stream)
 STAGES = ["F0_pyramid", "F1_full_search", "F2_half_res_quadrants", "FL_on_main_stream",
           "F3_diamond_fullpel", "F3_diamond_subpel", "F4_rdo_single_ref", "F4_rdo_compound",
-          "F4_rd_cost_argmin", "F6_commit", "F6b_intra_screen_rdo", "F5_importance_satd",
+          "F4_argmin_and_mv_stack_rounds", "F6_commit", "F6b_intra_screen_rdo", "F5_importance_satd",
           "F7_pad_exchange", "FL_lookahead_span", "EDGE_levels_span", "F8_entropy_tokens"]
 # speed 6: the 32x32 / 16x16 / 8x8 searches run inside the sub-pel stage,
 # their candidates inside F4, the partition decision with the argmin
@@ -200,8 +200,9 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     db = bool(flags & RP.RV_REPLAY_DEBLOCK)
     cd = bool(flags & RP.RV_REPLAY_CDEF)
     ent = bool(flags & RP.RV_REPLAY_ENTROPY)
+    sti = bool(flags & RP.RV_REPLAY_MVREF_STANDIN)
     c = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=threads, L=L,
-                    speed=speed, deblock=db, cdef=cd, entropy=ent)
+                    speed=speed, deblock=db, cdef=cd, entropy=ent, mvref_standin=sti)
     for i in range(nin):
         c.set_input(i, hip_inputs[i])
     c.frame()  # the key frame (a copy), untimed
@@ -219,7 +220,7 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     nsb = ((W + 63) // 64) * ((H + 63) // 64)
     lim = max(1, nsb // 8)
     c1 = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=1, L=L,
-                     speed=speed, deblock=db, cdef=cd, entropy=ent)
+                     speed=speed, deblock=db, cdef=cd, entropy=ent, mvref_standin=sti)
     for i in range(nin):
         c1.set_input(i, hip_inputs[i])
     c1.frame()
@@ -241,7 +242,8 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     # the GPU replay over the same frames, word for word
     g = RP.HipReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=n_inputs,
                      flags=flags & (RP.RV_REPLAY_SPEED6 | RP.RV_REPLAY_DEBLOCK |
-                                    RP.RV_REPLAY_CDEF | RP.RV_REPLAY_ENTROPY))
+                                    RP.RV_REPLAY_CDEF | RP.RV_REPLAY_ENTROPY |
+                                    RP.RV_REPLAY_MVREF_STANDIN))
     g.synth_inputs(0)
     g.frame()
     bad = []
@@ -352,6 +354,9 @@ def main():
     ap.add_argument("--serial-levels", action="store_true",
                     help="one instance codes every frame (default on one GPU: the level-2 "
                          "frames run on a twin instance concurrently with levels 0 / 1)")
+    ap.add_argument("--mv-stack", choices=("exact", "standin"), default="exact",
+                    help="speed 10: rav1e's find_mvrefs stacks in coding-order rounds (default), or "
+                         "the neighbour-NEWMV stand-in (A/B of the rounds' cost)")
     ap.add_argument("--no-entropy", action="store_true",
                     help="skip stage F8 (the coefficients' entropy coding: device tokens + "
                          "the host range coder); default: every frame's coefficients are coded")
@@ -377,7 +382,8 @@ def main():
     n_inputs = args.warmup + args.steps + 8  # every display the run codes
     flags = (RP.RV_REPLAY_EXHAUSTIVE_FS if args.exhaustive_fs else 0) | \
         (RP.RV_REPLAY_SPEED6 if speed == 6 else 0) | (RP.RV_REPLAY_DEBLOCK if args.deblock or args.cdef else 0) | \
-        (RP.RV_REPLAY_CDEF if args.cdef else 0) | (0 if args.no_entropy else RP.RV_REPLAY_ENTROPY)
+        (RP.RV_REPLAY_CDEF if args.cdef else 0) | (0 if args.no_entropy else RP.RV_REPLAY_ENTROPY) | \
+        (RP.RV_REPLAY_MVREF_STANDIN if args.mv_stack == "standin" else 0)
     hip = RP.HipReplay(W, H, xdec, ydec, bd, nref, group=rects[rank], tile_size=ts,
                        n_inputs=n_inputs, flags=flags)
     hip.synth_inputs(0)  # the stream's frames, resident in HBM before the timing
@@ -536,6 +542,10 @@ def main():
                        "frame_concurrency": ("levels 0/1 + level-2 frames on a twin instance "
                                              "(2 streams)" if paired else "serial"),
                        "candidates_per_sb": f"{4 * nref} inter modes x (skip, non-skip)",
+                       **({"mv_stack": ("rav1e's find_mvrefs over the coded blocks, coding-order "
+                                        "rounds" if args.mv_stack == "exact" else
+                                        "stand-in: the neighbours' search MVs (A/B)")}
+                          if speed == 10 else {}),
                        **({"partition": "64x64 .. 8x8 top-down NONE vs SPLIT, every level "
                                         "searched and scored"} if speed == 6 else {})},
             "mpix_per_s": round(fps * W * H / 1e6, 3),
@@ -551,6 +561,13 @@ def main():
             "rdo_candidates_per_frame": {"single_ref": round(ns, 1), "compound": round(nc, 1),
                                          "variants": "skip + non-skip each",
                                          **({"levels": level_cands} if level_cands else {})},
+            **({"mv_stacks": {
+                "what": "speed 10: rav1e's find_mvrefs stacks (NEAREST / NEAR / GLOBAL candidates, "
+                        "the search's rate predictors) in coding-order rounds: round 0 evaluates "
+                        "every superblock, a later round the ones whose stacks changed",
+                "rounds_per_frame": round(cnt[14] / max(1, cnt[16]), 3),
+                "reevaluated_sb_per_frame": round(cnt[15] / max(1, cnt[16]), 2)}}
+               if speed == 10 and len(cnt) > 16 else {}),
             "intra_per_frame": {"screened_superblocks": round(cnt[11] / ev_frames, 2),
                                 "intra_winners": round(cnt[12] / ev_frames, 2),
                                 "rounds": round(cnt[13] / ev_frames, 2),

@@ -590,6 +590,14 @@ typedef struct rv_replay_cfg {
  * (the frame's biggest tile in rav1e: exact with one group).
  * rv_replay_entropy_stats reads the result. */
 #define RV_REPLAY_ENTROPY 128
+/* flags: speed 10 takes the MV stacks of the superblocks' candidates and
+ * of their 64x64 search's rate predictors from rav1e's find_mvrefs over the
+ * blocks coded before them (src/context.rs:2650-2965) by default, in
+ * coding-order rounds (a round re-evaluates the superblocks whose stacks
+ * changed, until none does).  This flag substitutes the neighbours'
+ * motion-search MVs (every superblock independent, one pass; zero rate
+ * predictors): an A/B of the rounds' cost, not rav1e's decisions. */
+#define RV_REPLAY_MVREF_STANDIN 256
 typedef struct rv_replay_frame_info {
   int32_t display;            /* display index of the coded frame */
   int32_t me_range_scale;     /* 4 >> pyramid level (src/encoder.rs:838) */

@@ -563,6 +563,14 @@ int orc_replay_set_speed(orc_replay *r, int speed) {
   return alloc_levels(r, 0, 0, r->tw, r->th);
 }
 
+/* Speed 10: the neighbour-NEWMV stand-in stacks instead of rav1e's (the
+ * replay's RV_REPLAY_MVREF_STANDIN A/B). */
+int orc_replay_set_mvref_standin(orc_replay *r, int on) {
+  if (r->s6) return 0; /* speed 6 always takes the stand-in */
+  r->exact = !on;
+  return 0;
+}
+
 /* Deblock every coded frame before it becomes a reference (one tile group:
  * the replay's RV_REPLAY_DEBLOCK). */
 int orc_replay_set_deblock(orc_replay *r, int on) {

@@ -221,13 +221,19 @@ __global__ __launch_bounds__(64) void score_candidates(
     BlkDec *dec, int round) {
   const int sb = blockIdx.x * 64 + threadIdx.x;
   if (sb == 0) {  // F4's lists are consumed: ready for the next frame; F5 sums next
-    // single-reference and compound candidates evaluated (summed over the
-    // MV-stack rounds)
-    evals[0] = (round ? evals[0] : 0u) + (uint32_t)cand_count[0];
-    evals[1] = (round ? evals[1] : 0u) + (uint32_t)cand_count[1];
+    // single-reference and compound candidates of the frame's first F4
+    // launch (the one the roofline times; later MV-stack rounds re-evaluate
+    // a few superblocks, counted by rv_replay_counters' [15])
+    if (!round) {
+      evals[0] = (uint32_t)cand_count[0];
+      evals[1] = (uint32_t)cand_count[1];
+    }
     cand_count[0] = cand_count[1] = 0;
-    if (imp_sum) *imp_sum = 0;  // null: F5 ran on the side stream (it zeroed its sum)
-    if (leaf_count)  // speed 6: the partition decision appends next
+    // once per frame: the MV-stack rounds after the first may run after the
+    // partition decision filled the leaf lists (the rounds the intra pass
+    // triggers)
+    if (imp_sum && !round) *imp_sum = 0;  // null: F5 ran on the side stream (it zeroed its sum)
+    if (leaf_count && !round)  // the partition decision appends next
       for (int l = 0; l < 4; l++) leaf_count[l] = 0;
   }
   __shared__ RdoWinner ws[64];
@@ -250,6 +256,9 @@ __global__ __launch_bounds__(64) void score_candidates(
   uint64_t *base = words + (int64_t)sb0 * per;
   for (int i = threadIdx.x; i < nb * per; i += 64) {
     const int s = i / per, wi = i - s * per, b = sb0 + s;
+    // a superblock not evaluated this round keeps its words (an intra
+    // winner's among them)
+    if (active && !active[b]) continue;
     uint64_t v;
     if (wi < kWordsPerRef * g.R) {
       const int r = wi / kWordsPerRef, k = wi - r * kWordsPerRef, e = k >> 1;
@@ -1660,7 +1669,7 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     if (r->i_win) (void)hipMemsetAsync(r->i_win, 0, 2 * n, r->stream);
   }
   // speed 10: rav1e's MV stacks in coding-order rounds
-  r->exact = !r->s6;
+  r->exact = !r->s6 && !(cfg->flags & RV_REPLAY_MVREF_STANDIN);
   if (r->exact) {
     const size_t n = (size_t)g.nsb;
     r->stk = (MvStack *)dalloc(r, n * sizeof(MvStack));
@@ -1670,9 +1679,10 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
       ok = ok && r->dec_lv[l];
     }
     r->mv_active = (uint8_t *)dalloc(r, n);
-    r->mv_cnt = (int32_t *)dalloc(r, 4);
+    const size_t nr = (size_t)g.tws * g.ths + 16;  // per-round counts (rv_replay_frame)
+    r->mv_cnt = (int32_t *)dalloc(r, nr * 4);
     ok = ok && r->stk && r->mv_active && r->mv_cnt &&
-         hipHostMalloc((void **)&r->h_mv, 16, hipHostMallocDefault) == hipSuccess;
+         hipHostMalloc((void **)&r->h_mv, nr * 4, hipHostMallocDefault) == hipSuccess;
     // does a superblock's top-right neighbour (same tile) lie past the right
     // frame edge, i.e. is it a must_split leaf?
     for (int sb = 0; sb < g.nsb && r->lvl; sb++) {
@@ -2445,6 +2455,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     if (edge && r->edge_tr)  // the leaves the stacks read
       for (int l = 1; l < kLevels; l++)
         if (r->lv_used[l]) RV_H(hipStreamWaitEvent(st, r->ev_ejoin[l], 0));
+    ma.count = r->mv_cnt;  // slot 0: the first round marks every superblock
     RV_H(hipMemsetAsync(r->mv_cnt, 0, sizeof(int32_t), st));
     RV_R(rv_mvref_round(ma, st));
   }
@@ -2502,32 +2513,48 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   };
   RV_R(f3_f4(0));
   int mv_rounds = 1;
-  // the stacks from the decisions so far; true when some superblock changed
-  auto mv_check = [&](const uint8_t *iwas) -> int {
-    ma.init = 0;
-    ma.iwas = iwas;
-    RV_H(hipMemsetAsync(r->mv_cnt, 0, sizeof(int32_t), st));
-    RV_R(rv_mvref_round(ma, st));
-    RV_H(hipMemcpyAsync(r->h_mv, r->mv_cnt, 4, hipMemcpyDeviceToHost, st));
-    RV_H(hipStreamSynchronize(st));
-    r->mv_reeval += *r->h_mv;
-    return RV_OK;
-  };
-  // the rounds after a check found *h_mv superblocks to re-evaluate; bounded
+  // The rounds after the first: a check (the stacks from the decisions so
+  // far, counts[i] = the superblocks marked before evaluation round i), then
+  // the evaluation of the marked ones -- a no-op once a check marks none.
+  // They are queued in batches of 1, 2, 4, 8 between host reads of the
+  // counts, so a long dependency chain costs few host round trips; bounded
   // by the tiles' dependency depth (every round settles the next superblock
-  // of each raster chain)
+  // of each raster chain).  Returns with *changed = some round evaluated.
   const int max_rounds = g.tws * g.ths + 2;
-  auto mv_rounds_run = [&](const uint8_t *iwas) -> int {
-    for (;;) {
-      RV_R(mv_check(iwas));
-      if (*r->h_mv == 0) return RV_OK;
-      if (mv_rounds >= max_rounds)
+  static const bool mv_trace = getenv("RAV1E_HIP_MV_TRACE") != nullptr;
+  auto mv_rounds_run = [&](const uint8_t *iwas, bool *changed) -> int {
+    if (changed) *changed = false;
+    for (int k = 1;; k = k < 8 ? 2 * k : 8) {
+      const int first = mv_rounds;
+      if (first + k > max_rounds) k = max_rounds - first;
+      if (k <= 0)
         return rv_set_error(RV_EHIP, "rv_replay_frame: the MV-stack rounds did not converge");
-      RV_R(f3_f4(mv_rounds));
-      mv_rounds++;
+      RV_H(hipMemsetAsync(r->mv_cnt + first, 0, (size_t)k * sizeof(int32_t), st));
+      for (int j = 0; j < k; j++) {
+        ma.init = 0;
+        ma.iwas = iwas;
+        ma.count = r->mv_cnt + first + j;
+        RV_R(rv_mvref_round(ma, st));
+        RV_R(f3_f4(first + j));
+      }
+      RV_H(hipMemcpyAsync(r->h_mv, r->mv_cnt + first, (size_t)k * sizeof(int32_t),
+                          hipMemcpyDeviceToHost, st));
+      RV_H(hipStreamSynchronize(st));
+      for (int j = 0; j < k; j++) {
+        if (mv_trace)
+          fprintf(stderr, "mvref frame %ld level %d round %d: %d\n", ncoded, lv, first + j,
+                  r->h_mv[j]);
+        if (r->h_mv[j] == 0) {  // converged: the rounds queued after it did nothing
+          mv_rounds = first + j;
+          return RV_OK;
+        }
+        r->mv_reeval += r->h_mv[j];
+        if (changed) *changed = true;
+      }
+      mv_rounds = first + k;
     }
   };
-  if (r->exact) RV_R(mv_rounds_run(nullptr));
+  if (r->exact) RV_R(mv_rounds_run(nullptr, nullptr));
   if (r->lvl) {
     if (edge) {  // the levels' winners
       for (int l = 1; l < kLevels; l++)
@@ -2591,13 +2618,9 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // frame re-committed and the intra pass re-run, until the stacks hold
   // (the joint fixed point of the tile's coding order)
   while (r->exact && r->intra) {
-    RV_R(mv_check(r->i_was));
-    if (*r->h_mv == 0) break;
-    if (mv_rounds >= max_rounds)
-      return rv_set_error(RV_EHIP, "rv_replay_frame: the MV-stack rounds did not converge");
-    RV_R(f3_f4(mv_rounds));
-    mv_rounds++;
-    RV_R(mv_rounds_run(r->i_was));
+    bool changed = false;
+    RV_R(mv_rounds_run(r->i_was, &changed));
+    if (!changed) break;
     RV_R(rv_rdo_candidates(la, ca, g.hbd, st));  // F6 again: every inter winner
     RV_R(intra_begin(r));
     RV_R(intra_pass(r, la, ca, cur, S, L, slot));
@@ -2886,7 +2909,13 @@ int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
   out[11] = out[12] = out[13] = 0;
   for (int f = 0; f < nf; f++)
     for (int k = 0; k < 3; k++) out[11 + k] += is[(size_t)f * 3 + k];
-  return 14;
+  if (cap < 17) return 14;
+  // speed 10 MV-stack rounds since creation: rounds (F3 + F4 launches),
+  // superblock re-evaluations after the first round, frames
+  out[14] = (uint64_t)r->mv_round_sum;
+  out[15] = (uint64_t)r->mv_reeval;
+  out[16] = r->exact ? (uint64_t)nonkey : 0;
+  return 17;
 }
 
 // ---- RCCL communicator for the tile-group exchange ---------------------------

@@ -26,6 +26,7 @@ RV_REPLAY_CDEF = 32  # CDEF after deblocking (needs RV_REPLAY_DEBLOCK), cdef_bit
 RV_REPLAY_NO_INTRA = 64  # no intra-mode screening of non-skip superblocks (default: on
 #                          at speed 10 in 4:2:0)
 RV_REPLAY_ENTROPY = 128  # F8: code every frame's coefficients (device tokens, host range coder)
+RV_REPLAY_MVREF_STANDIN = 256  # speed 10: neighbour-NEWMV stacks instead of rav1e's (A/B only)
 # HIP-event stages of a frame: F0, F1, F2, FL (lookahead), F3 full-pel, F3
 # sub-pel, F4 single, F4 compound, F4 argmin, F6 commit, F6b intra, F5, F7,
 # then the lookahead's own span, the speed-10 edge levels' own span and
@@ -403,9 +404,10 @@ class HipReplay:
         candidates, F4 compound candidates of the 64x64 blocks, then (speed
         6) single / compound of the 32x32, 16x16 and 8x8 blocks, superblocks
         intra-screened, intra winners, intra rounds] over the last <= 64
-        frames."""
-        out = np.zeros(14, dtype=np.uint64)
-        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 14) - 14, "rv_replay_counters")
+        frames, then (speed 10, since creation) the MV-stack rounds, the
+        superblocks they re-evaluated, and the frames."""
+        out = np.zeros(17, dtype=np.uint64)
+        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 17) - 17, "rv_replay_counters")
         return out
 
     def close(self):

@@ -508,7 +508,7 @@ class CpuReplay:
 
     def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, group=None,
                  tile_size=(0, 0), n_inputs=8, threads=1, L=None, quantizer=100, speed=10,
-                 deblock=False, cdef=False, intra=True, entropy=False):
+                 deblock=False, cdef=False, intra=True, entropy=False, mvref_standin=False):
         from rav1e_amd import rate as RT
         L = L or lib()
         self.L = L
@@ -537,6 +537,8 @@ class CpuReplay:
         L.orc_replay_set_deblock.argtypes = [C.c_void_p, C.c_int]
         assert L.orc_replay_set_deblock(self.h, 1 if deblock else 0) == 0, "orc_replay_set_deblock"
         self.speed = speed
+        L.orc_replay_set_mvref_standin.argtypes = [C.c_void_p, C.c_int]
+        assert L.orc_replay_set_mvref_standin(self.h, 1 if mvref_standin else 0) == 0
         # intra-mode screening of non-skip superblocks: speed 10, 4:2:0 (the
         # replay's default; RV_REPLAY_NO_INTRA turns it off on the GPU)
         self.intra = bool(intra and speed == 10 and xdec == 1 and ydec == 1)
