@@ -16,7 +16,8 @@ constexpr int kIntraFrame = 0, kNoneFrame = 8;
 // find_mvrefs reads: ref_frames and mv.
 struct BlkDec {
   int8_t ref[2];
-  int8_t newmv, pad;
+  int8_t newmv;
+  uint8_t cand;  // the replay's candidate index of the winner (255: intra / none)
   rv_mv mv[2];
 };
 
@@ -47,16 +48,18 @@ __device__ inline BlkDec blk_dec_of(const CandGeo &cg, const rv_fs_result *sub, 
   BlkDec d;
   d.ref[1] = kNoneFrame;
   d.newmv = 0;
-  d.pad = 0;
+  d.cand = 255;
   d.mv[0] = d.mv[1] = rv_mv{0, 0};
   const int ns = cg.R * cg.M;
   if (c >= 1000 || c < 0 || c >= ns + kCompModes) {  // kIntraWord (the range guards the reads)
     d.ref[0] = kIntraFrame;
   } else if (c < ns) {
+    d.cand = (uint8_t)c;
     d.ref[0] = (int8_t)(1 + c / cg.M);
     (void)cand_mv(cg, sub, sb, c, &d.mv[0]);
     d.newmv = (c % cg.M) == kNewMv;
   } else {
+    d.cand = (uint8_t)c;
     d.ref[0] = 1;
     d.ref[1] = 2;
     comp_mvs(cg, sub, sb, c - ns, &d.mv[0], &d.mv[1]);
@@ -67,4 +70,6 @@ __device__ inline BlkDec blk_dec_of(const CandGeo &cg, const rv_fs_result *sub, 
 
 }  // namespace rv
 
-int rv_mvref_round(const rv::MvrefArgs &a, hipStream_t s);
+// One round over the group's superblocks (the first marks every one); scan:
+// the tail rounds' predictive per-tile wavefront scan.
+int rv_mvref_round(const rv::MvrefArgs &a, hipStream_t s, bool scan = false);

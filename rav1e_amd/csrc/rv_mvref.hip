@@ -33,30 +33,45 @@ struct Cand {
 
 __device__ inline bool inter_of(const BlkDec &b) { return b.ref[0] != kIntraFrame; }
 
-// add_ref_mv_candidate (src/context.rs:2366-2435), MAX_REF_MV_STACK_SIZE 8
-__device__ inline void add_ref(Cand *st, int &n, const BlkDec &b, uint32_t w, int rf0, int rf1,
-                               bool compound) {
+// The stack in registers: at most kSlots entries reach it for a 64x64
+// block (one per neighbour from the scans -- a single-reference stack takes
+// one MV of a block, a compound one one pair -- and at most two from the
+// extra search), so MAX_REF_MV_STACK_SIZE (8) never binds.  Every access
+// uses a compile-time slot index (unrolled loops), so nothing goes to
+// scratch memory.
+constexpr int kSlots = 6;
+struct Stk {
+  Cand e[kSlots];
+  int n;
+};
+
+// find_matching_mv(_and_update_weight) / push
+__device__ __forceinline__ void push_or_add(Stk &k, rv_mv t, rv_mv c, uint32_t w, bool comp,
+                                            bool add_weight) {
+  bool found = false;
+#pragma unroll
+  for (int i = 0; i < kSlots; i++)
+    if (i < k.n && !found && mv_eq(k.e[i].t, t) && (!comp || mv_eq(k.e[i].c, c))) {
+      if (add_weight) k.e[i].w += w;
+      found = true;
+    }
+  if (found) return;
+#pragma unroll
+  for (int i = 0; i < kSlots; i++)
+    if (i == k.n) k.e[i] = Cand{t, c, w};
+  k.n++;
+}
+
+// add_ref_mv_candidate (src/context.rs:2366-2435)
+__device__ __forceinline__ void add_ref(Stk &k, const BlkDec &b, uint32_t w, int rf0, int rf1,
+                                        bool compound) {
   if (!inter_of(b)) return;
   if (compound) {
-    if (b.ref[0] != rf0 || b.ref[1] != rf1) return;
-    for (int i = 0; i < n; i++)
-      if (mv_eq(st[i].t, b.mv[0]) && mv_eq(st[i].c, b.mv[1])) {
-        st[i].w += w;
-        return;
-      }
-    if (n < 8) st[n++] = Cand{b.mv[0], b.mv[1], w};
+    if (b.ref[0] == rf0 && b.ref[1] == rf1) push_or_add(k, b.mv[0], b.mv[1], w, true, true);
     return;
   }
-  for (int i = 0; i < 2; i++) {
-    if (b.ref[i] != rf0) continue;
-    bool found = false;
-    for (int j = 0; j < n && !found; j++)
-      if (mv_eq(st[j].t, b.mv[i])) {
-        st[j].w += w;
-        found = true;
-      }
-    if (!found && n < 8) st[n++] = Cand{b.mv[i], rv_mv{0, 0}, w};
-  }
+  if (b.ref[0] == rf0) push_or_add(k, b.mv[0], rv_mv{0, 0}, w, false, true);
+  if (b.ref[1] == rf0) push_or_add(k, b.mv[1], rv_mv{0, 0}, w, false, true);
 }
 
 __device__ inline rv_mv neg(rv_mv m) { return rv_mv{(int16_t)-m.row, (int16_t)-m.col}; }
@@ -67,75 +82,113 @@ struct Nb {
 };
 
 // setup_mvref_list of a 64x64 block for ref_frames (rf0, rf1; rf1 = NONE:
-// single); n out, entries into st (clamped)
+// single): the first two entries (clamped) into s0 / s1, the length returned
 __device__ inline int stack64(const Nb &nb, int rf0, int rf1, const uint8_t *sbias, int fx, int fy,
-                              int fcols, int frows, Cand *st) {
+                              int fcols, int frows, Cand &s0, Cand &s1) {
   const bool compound = rf1 != kNoneFrame;
-  int n = 0;
-  if (nb.up) add_ref(st, n, nb.a, 16 * 6, rf0, rf1, compound);
-  if (nb.left) add_ref(st, n, nb.l, 16 * 6, rf0, rf1, compound);
-  if (nb.tr) add_ref(st, n, nb.r, 4, rf0, rf1, compound);
-  for (int i = 0; i < n; i++) st[i].w += 640;  // add_offset, REF_CAT_LEVEL
-  if (nb.tl) add_ref(st, n, nb.d, 4, rf0, rf1, compound);
-  // 7.10.2.11: stable sort, descending weight
-  for (int i = 1; i < n; i++)
-    for (int j = i; j > 0 && st[j].w > st[j - 1].w; j--) {
-      const Cand t = st[j];
-      st[j] = st[j - 1];
-      st[j - 1] = t;
-    }
-  if (n < 2) {
+  Stk k;
+  k.n = 0;
+#pragma unroll
+  for (int i = 0; i < kSlots; i++) k.e[i] = Cand{rv_mv{0, 0}, rv_mv{0, 0}, 0};
+  if (nb.up) add_ref(k, nb.a, 16 * 6, rf0, rf1, compound);
+  if (nb.left) add_ref(k, nb.l, 16 * 6, rf0, rf1, compound);
+  if (nb.tr) add_ref(k, nb.r, 4, rf0, rf1, compound);
+#pragma unroll
+  for (int i = 0; i < kSlots; i++)
+    if (i < k.n) k.e[i].w += 640;  // add_offset, REF_CAT_LEVEL
+  if (nb.tl) add_ref(k, nb.d, 4, rf0, rf1, compound);
+  // 7.10.2.11: stable sort, descending weight (an insertion sort over the
+  // slots; empty slots carry weight 0 and stay behind)
+#pragma unroll
+  for (int i = 1; i < kSlots; i++)
+#pragma unroll
+    for (int j = i; j > 0; j--)
+      if (j < k.n && k.e[j].w > k.e[j - 1].w) {
+        const Cand t = k.e[j];
+        k.e[j] = k.e[j - 1];
+        k.e[j - 1] = t;
+      }
+  if (k.n < 2) {
     // 7.10.2.12: the above block (pass 0), then the left one (pass 1); each
     // 64x64 pass reads one block (idx += n4_w = 16)
-    int idc[2] = {0, 0}, dfc[2] = {0, 0};
-    rv_mv idm[2][2], dfm[2][2];
-    for (int p = nb.up ? 0 : 1; p < (nb.left ? 2 : 1); p++) {
-      if (n >= 2) break;
+    int idc0 = 0, idc1 = 0, dfc0 = 0, dfc1 = 0;
+    rv_mv id0[2] = {rv_mv{0, 0}, rv_mv{0, 0}}, id1[2] = {rv_mv{0, 0}, rv_mv{0, 0}};
+    rv_mv df0[2] = {rv_mv{0, 0}, rv_mv{0, 0}}, df1[2] = {rv_mv{0, 0}, rv_mv{0, 0}};
+#pragma unroll
+    for (int p = 0; p < 2; p++) {
+      if (p == 0 ? !nb.up : !nb.left) continue;
+      if (k.n >= 2) break;
       const BlkDec &b = p == 0 ? nb.a : nb.l;
+#pragma unroll
       for (int cl = 0; cl < 2; cl++) {
         const int cr = b.ref[cl];
         if (cr == kIntraFrame || cr == kNoneFrame) continue;
+        const rv_mv m = b.mv[cl];
         if (compound) {
-          for (int list = 0; list < 2; list++) {
-            const int rl = list ? rf1 : rf0;
-            if (cr == rl && idc[list] < 2) {
-              idm[list][idc[list]++] = b.mv[cl];
-            } else if (dfc[list] < 2) {
-              dfm[list][dfc[list]++] = sbias[cr - 1] != sbias[rl - 1] ? neg(b.mv[cl]) : b.mv[cl];
-            }
+          // list 0 (rf0), then list 1 (rf1)
+          if (cr == rf0 && idc0 < 2) {
+            if (idc0 == 0) id0[0] = m; else id0[1] = m;
+            idc0++;
+          } else if (dfc0 < 2) {
+            const rv_mv v = sbias[cr - 1] != sbias[rf0 - 1] ? neg(m) : m;
+            if (dfc0 == 0) df0[0] = v; else df0[1] = v;
+            dfc0++;
+          }
+          if (cr == rf1 && idc1 < 2) {
+            if (idc1 == 0) id1[0] = m; else id1[1] = m;
+            idc1++;
+          } else if (dfc1 < 2) {
+            const rv_mv v = sbias[cr - 1] != sbias[rf1 - 1] ? neg(m) : m;
+            if (dfc1 == 0) df1[0] = v; else df1[1] = v;
+            dfc1++;
           }
         } else {
-          const rv_mv m = sbias[cr - 1] != sbias[rf0 - 1] ? neg(b.mv[cl]) : b.mv[cl];
-          bool found = false;
-          for (int j = 0; j < n; j++) found |= mv_eq(st[j].t, m);
-          if (!found) st[n++] = Cand{m, rv_mv{0, 0}, 2};
+          const rv_mv v = sbias[cr - 1] != sbias[rf0 - 1] ? neg(m) : m;
+          push_or_add(k, v, rv_mv{0, 0}, 2, false, false);
         }
       }
     }
     if (compound) {
-      rv_mv cm[2][2] = {{rv_mv{0, 0}, rv_mv{0, 0}}, {rv_mv{0, 0}, rv_mv{0, 0}}};
-      for (int list = 0; list < 2; list++) {
+      // combined_mvs[i][list]: the same-reference MVs, then the others
+      rv_mv c00 = rv_mv{0, 0}, c10 = rv_mv{0, 0}, c01 = rv_mv{0, 0}, c11 = rv_mv{0, 0};
+      {
         int cc = 0;
-        for (int i = 0; i < idc[list]; i++) cm[cc++][list] = idm[list][i];
-        for (int i = 0; i < dfc[list] && cc < 2; i++) cm[cc++][list] = dfm[list][i];
+        if (idc0 > 0) { c00 = id0[0]; cc++; }
+        if (idc0 > 1) { c10 = id0[1]; cc++; }
+        for (int i = 0; i < dfc0 && cc < 2; i++) {
+          if (cc == 0) c00 = df0[i]; else c10 = df0[i];
+          cc++;
+        }
       }
-      if (n == 1) {
-        const int pick = mv_eq(cm[0][0], st[0].t) && mv_eq(cm[0][1], st[0].c) ? 1 : 0;
-        st[n++] = Cand{cm[pick][0], cm[pick][1], 2};
+      {
+        int cc = 0;
+        if (idc1 > 0) { c01 = id1[0]; cc++; }
+        if (idc1 > 1) { c11 = id1[1]; cc++; }
+        for (int i = 0; i < dfc1 && cc < 2; i++) {
+          if (cc == 0) c01 = df1[i]; else c11 = df1[i];
+          cc++;
+        }
+      }
+      if (k.n == 1) {
+        const bool same = mv_eq(c00, k.e[0].t) && mv_eq(c01, k.e[0].c);
+        k.e[1] = same ? Cand{c10, c11, 2} : Cand{c00, c01, 2};
+        k.n = 2;
       } else {
-        st[n++] = Cand{cm[0][0], cm[0][1], 2};
-        st[n++] = Cand{cm[1][0], cm[1][1], 2};
+        k.e[0] = Cand{c00, c01, 2};
+        k.e[1] = Cand{c10, c11, 2};
+        k.n = 2;
       }
     }
   }
   // clamp (src/context.rs:2911-2941), 64x64: border 128 + 512
   const int xmin = -fx * 32 - 640, xmax = (fcols - fx - 16) * 32 + 640;
   const int ymin = -fy * 32 - 640, ymax = (frows - fy - 16) * 32 + 640;
-  for (int i = 0; i < n && i < 2; i++) {
-    st[i].t = rv_mv{(int16_t)clampi(st[i].t.row, ymin, ymax), (int16_t)clampi(st[i].t.col, xmin, xmax)};
-    st[i].c = rv_mv{(int16_t)clampi(st[i].c.row, ymin, ymax), (int16_t)clampi(st[i].c.col, xmin, xmax)};
-  }
-  return n;
+  auto cl = [&](rv_mv m) {
+    return rv_mv{(int16_t)clampi(m.row, ymin, ymax), (int16_t)clampi(m.col, xmin, xmax)};
+  };
+  s0 = Cand{cl(k.e[0].t), cl(k.e[0].c), k.e[0].w};
+  s1 = Cand{cl(k.e[1].t), cl(k.e[1].c), k.e[1].w};
+  return k.n;
 }
 
 // The coded block at frame pixel (X, Y) inside superblock nsb: its 64x64
@@ -157,6 +210,54 @@ __device__ inline BlkDec coded_at(const MvrefArgs &a, int nsb, int X, int Y) {
   const CandGeo &g = a.lcg[l];
   const int b = (Y / B - g.ty0) * g.tw + (X / B - g.tx0);
   return blk_dec_of(g, a.lsub[l], b, a.lwin[l][b].c);
+}
+
+// The superblock's stacks: every reference's and, on compound frames, the
+// (ref 0, ref 1) pair's (empty for a must_split superblock)
+__device__ inline MvStack stacks_of(const MvrefArgs &a, const Nb &nb, bool split, int fsx,
+                                    int fsy) {
+  MvStack s;
+  for (int k = 0; k < 2; k++) {
+    s.n[k] = 0;
+    s.s[k][0] = s.s[k][1] = rv_mv{0, 0};
+  }
+  Cand e0, e1;
+  for (int k = 0; k < a.R && !split; k++) {
+    const int n = stack64(nb, 1 + k, kNoneFrame, a.sign_bias, fsx * 16, fsy * 16, a.w_in_b,
+                          a.h_in_b, e0, e1);
+    s.n[k] = n < 2 ? n : 2;
+    if (n >= 1) s.s[k][0] = e0.t;
+    if (n >= 2) s.s[k][1] = e1.t;
+  }
+  s.c[0][0] = s.c[0][1] = s.c[1][0] = s.c[1][1] = rv_mv{0, 0};
+  if (a.comp && !split) {
+    (void)stack64(nb, 1, 2, a.sign_bias, fsx * 16, fsy * 16, a.w_in_b, a.h_in_b, e0, e1);
+    s.c[0][0] = e0.t;
+    s.c[0][1] = e0.c;
+    s.c[1][0] = e1.t;
+    s.c[1][1] = e1.c;
+  }
+  return s;
+}
+// the stacks a superblock was evaluated with still hold (never on the first round)
+__device__ inline bool same_stacks(const MvrefArgs &a, const MvStack &o, const MvStack &s) {
+  bool same = !a.init;
+  for (int k = 0; k < a.R && same; k++)
+    same = o.n[k] == s.n[k] && mv_eq(o.s[k][0], s.s[k][0]) && mv_eq(o.s[k][1], s.s[k][1]);
+  if (a.comp && same)
+    same = mv_eq(o.c[0][0], s.c[0][0]) && mv_eq(o.c[0][1], s.c[0][1]) &&
+           mv_eq(o.c[1][0], s.c[1][0]) && mv_eq(o.c[1][1], s.c[1][1]);
+  return same;
+}
+// a marked superblock's new stacks and motion_estimation's rate predictors
+// (src/rdo.rs:858-870)
+__device__ inline void set_stacks(const MvrefArgs &a, int sb, const MvStack &s) {
+  a.stk[sb] = s;
+  for (int k = 0; k < a.R; k++) {
+    const int j = k * a.nsb + sb;
+    a.jf[j].pmv[0] = a.js[j].pmv[0] = s.s[k][0];
+    a.jf[j].pmv[1] = a.js[j].pmv[1] = s.s[k][1];
+  }
 }
 
 __global__ __launch_bounds__(256) void mvref_kernel(MvrefArgs a) {
@@ -184,55 +285,112 @@ __global__ __launch_bounds__(256) void mvref_kernel(MvrefArgs a) {
     if (nb.left) nb.l = coded_at(a, sb - 1, X - 4, Y);
     if (nb.tr) nb.r = coded_at(a, sb - a.tw + 1, X + 64, Y - 4);
     if (nb.tl) nb.d = coded_at(a, sb - a.tw - 1, X - 4, Y - 4);
-    MvStack s;
-    Cand st[10];
-    for (int k = 0; k < 2; k++) {
-      s.n[k] = 0;
-      s.s[k][0] = s.s[k][1] = rv_mv{0, 0};
-    }
-    for (int k = 0; k < a.R && !split; k++) {
-      const int n = stack64(nb, 1 + k, kNoneFrame, a.sign_bias, fsx * 16, fsy * 16, a.w_in_b,
-                            a.h_in_b, st);
-      s.n[k] = n < 2 ? n : 2;
-      if (n >= 1) s.s[k][0] = st[0].t;
-      if (n >= 2) s.s[k][1] = st[1].t;
-    }
-    s.c[0][0] = s.c[0][1] = s.c[1][0] = s.c[1][1] = rv_mv{0, 0};
-    if (a.comp && !split) {
-      (void)stack64(nb, 1, 2, a.sign_bias, fsx * 16, fsy * 16, a.w_in_b, a.h_in_b, st);
-      s.c[0][0] = st[0].t;
-      s.c[0][1] = st[0].c;
-      s.c[1][0] = st[1].t;
-      s.c[1][1] = st[1].c;
-    }
-    const MvStack &o = a.stk[sb];
-    bool same = !a.init;
-    for (int k = 0; k < a.R && same; k++)
-      same = o.n[k] == s.n[k] && mv_eq(o.s[k][0], s.s[k][0]) && mv_eq(o.s[k][1], s.s[k][1]);
-    if (a.comp && same)
-      same = mv_eq(o.c[0][0], s.c[0][0]) && mv_eq(o.c[0][1], s.c[0][1]) &&
-             mv_eq(o.c[1][0], s.c[1][0]) && mv_eq(o.c[1][1], s.c[1][1]);
-    mark = !same;
+    const MvStack s = stacks_of(a, nb, split, fsx, fsy);
+    mark = !same_stacks(a, a.stk[sb], s);
     a.active[sb] = mark;
-    if (mark) {
-      a.stk[sb] = s;
-      // motion_estimation's rate predictors (src/rdo.rs:858-870)
-      for (int k = 0; k < a.R; k++) {
-        const int j = k * a.nsb + sb;
-        a.jf[j].pmv[0] = a.js[j].pmv[0] = s.s[k][0];
-        a.jf[j].pmv[1] = a.js[j].pmv[1] = s.s[k][1];
-      }
-    }
+    if (mark) set_stacks(a, sb, s);
   }
   const uint64_t m = __ballot(mark);
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(a.count, (int)__popcll(m));
 }
 
+
+// A decision predicted under a new stack: the same candidate, its MVs taken
+// from the new stack (NEWMV keeps the last search's MV).  Only a guess that
+// lets a change run down a dependency chain in one round; the fixed point
+// does not depend on it.
+__device__ inline BlkDec predict(BlkDec d, const MvStack &s, int M, int R) {
+  if (d.cand == 255 || d.ref[0] == kIntraFrame) return d;
+  const int c = d.cand, ns = R * M;
+  if (c < ns) {
+    const int k = c / M, m = c - k * M;
+    if (m == kNearestMv) d.mv[0] = s.n[k] >= 1 ? s.s[k][0] : rv_mv{0, 0};
+    if (m == kNear0Mv && s.n[k] >= 1) d.mv[0] = s.n[k] >= 2 ? s.s[k][1] : rv_mv{0, 0};
+    return d;
+  }
+  switch (c - ns) {
+    case kNearestNearest: d.mv[0] = s.c[0][0]; d.mv[1] = s.c[0][1]; break;
+    case kNearNear: d.mv[0] = s.c[1][0]; d.mv[1] = s.c[1][1]; break;
+    case kNearestNew: d.mv[0] = s.c[0][0]; break;
+    case kNewNearest: d.mv[1] = s.c[0][1]; break;
+    default: break;
+  }
+  return d;
+}
+
+// The tail rounds (few superblocks still changing, mostly along dependency
+// chains): one workgroup per tile scans its superblocks in anti-diagonal
+// wavefronts (x + 2 y = d: the left, above, top-right and top-left
+// neighbours lie on earlier ones).  A superblock whose stack held keeps its
+// evaluated decision; one whose stack changed is marked and, for the
+// superblocks after it, predicted (the same candidate under the new stack),
+// so a chain of changes is evaluated in one round when the predictions
+// hold.  The tile's decisions live in LDS.
+__global__ __launch_bounds__(64) void mvref_scan_kernel(MvrefArgs a) {
+  extern __shared__ BlkDec pd[];
+  __shared__ int nmark;
+  const int gtx = (a.tw + a.tws - 1) / a.tws;
+  const int lx0 = (int)(blockIdx.x % gtx) * a.tws, ly0 = (int)(blockIdx.x / gtx) * a.ths;
+  const int twd = min(a.tws, a.tw - lx0), tht = min(a.ths, a.th - ly0);
+  const int ndiag = (twd - 1) + 2 * (tht - 1) + 1;
+  if (threadIdx.x == 0) nmark = 0;
+  const int t0x = a.tx0 + lx0, t0y = a.ty0 + ly0;
+  const int cols = min(a.tws * 16, a.w_in_b - t0x * 16);
+  __syncthreads();
+  int mine = 0;
+  for (int d = 0; d < ndiag; d++) {
+    const int ylo = max(0, (d - twd + 2) / 2), yhi = min(tht - 1, d / 2);
+    for (int y = ylo + (int)threadIdx.x; y <= yhi; y += (int)blockDim.x) {
+      const int x = d - 2 * y;
+      const int sb = (ly0 + y) * a.tw + lx0 + x;
+      const int fsx = t0x + x, fsy = t0y + y;
+      const int X = fsx * 64, Y = fsy * 64, bx = x * 16, by = y * 16;
+      const bool split = a.lvl && (X + 64 > a.W || Y + 64 > a.H);
+      // a neighbour: LDS (this tile), or a must_split leaf
+      auto nbr = [&](int nx, int ny, int PX, int PY) -> BlkDec {
+        if (a.lvl && ((t0x + nx + 1) * 64 > a.W || (t0y + ny + 1) * 64 > a.H))
+          return coded_at(a, 0, PX, PY);
+        BlkDec v = pd[ny * twd + nx];
+        if (a.iwas && a.iwas[(ly0 + ny) * a.tw + lx0 + nx]) v.ref[0] = kIntraFrame, v.ref[1] = kNoneFrame;
+        return v;
+      };
+      Nb nb;
+      nb.up = !split && by > 0;
+      nb.left = !split && bx > 0;
+      nb.tr = !split && by > 0 && bx + 16 < cols;
+      nb.tl = !split && bx > 0 && by > 0;
+      if (nb.up) nb.a = nbr(x, y - 1, X, Y - 4);
+      if (nb.left) nb.l = nbr(x - 1, y, X - 4, Y);
+      if (nb.tr) nb.r = nbr(x + 1, y - 1, X + 64, Y - 4);
+      if (nb.tl) nb.d = nbr(x - 1, y - 1, X - 4, Y - 4);
+      const MvStack s = stacks_of(a, nb, split, fsx, fsy);
+      const bool mark = !same_stacks(a, a.stk[sb], s);
+      a.active[sb] = mark;
+      const BlkDec cur = a.dec[sb];
+      if (!mark) {
+        pd[y * twd + x] = cur;  // evaluated under this very stack
+      } else {
+        mine++;
+        set_stacks(a, sb, s);
+        pd[y * twd + x] = predict(cur, s, kCandModes, a.R);
+      }
+    }
+    __syncthreads();  // the wavefront's decisions before the next one reads them
+  }
+  if (mine) atomicAdd(&nmark, mine);
+  __syncthreads();
+  if (threadIdx.x == 0 && nmark) atomicAdd(a.count, nmark);
+}
 }  // namespace
 
-int rv_mvref_round(const MvrefArgs &a, hipStream_t s) {
+int rv_mvref_round(const MvrefArgs &a, hipStream_t s, bool scan) {
   if (a.nsb <= 0) return RV_OK;
-  mvref_kernel<<<(a.nsb + 255) / 256, 256, 0, s>>>(a);
+  if (scan && !a.init) {
+    const int ntiles = ((a.tw + a.tws - 1) / a.tws) * ((a.th + a.ths - 1) / a.ths);
+    mvref_scan_kernel<<<ntiles, 64, (size_t)a.tws * a.ths * sizeof(BlkDec), s>>>(a);
+  } else {
+    mvref_kernel<<<(a.nsb + 255) / 256, 256, 0, s>>>(a);
+  }
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }
