@@ -237,9 +237,15 @@ __global__ __launch_bounds__(64) void score_candidates(
       for (int l = 0; l < 4; l++) leaf_count[l] = 0;
   }
   __shared__ RdoWinner ws[64];
+  __shared__ uint8_t act[64];
+  // the MV-stack rounds after the first evaluate a few superblocks: a
+  // workgroup holding none of them has nothing to do
+  const bool mine = sb < g.nsb && (!active || active[sb]);
+  act[threadIdx.x] = mine;
+  if (!__syncthreads_or(mine)) return;
   if (sb < g.nsb) {
     RdoWinner w;
-    if (!active || active[sb]) {  // a superblock evaluated this round
+    if (mine) {  // a superblock evaluated this round
       w = block_argmin(cg, lambda, ds_u, ds_v, sub, lout, uout, vout, ntx_c, sb);
       win[sb] = w;
       if (dec) dec[sb] = blk_dec_of(cg, sub, sb, w.c);
@@ -258,7 +264,7 @@ __global__ __launch_bounds__(64) void score_candidates(
     const int s = i / per, wi = i - s * per, b = sb0 + s;
     // a superblock not evaluated this round keeps its words (an intra
     // winner's among them)
-    if (active && !active[b]) continue;
+    if (!act[s]) continue;
     uint64_t v;
     if (wi < kWordsPerRef * g.R) {
       const int r = wi / kWordsPerRef, k = wi - r * kWordsPerRef, e = k >> 1;
@@ -804,6 +810,9 @@ struct rv_replay {
   uint8_t *mv_active = nullptr;        // re-evaluate this round
   int32_t *mv_cnt = nullptr, *h_mv = nullptr;  // marked count (device, pinned host)
   bool edge_tr = false;                // a stack reads a frame-edge leaf (top-right)
+  // RAV1E_HIP_MV_HP=1: the rounds after the first on a high-priority stream
+  hipStream_t hp = nullptr;
+  hipEvent_t ev_hp0 = nullptr, ev_hp1 = nullptr;
   long mv_round_sum = 0, mv_reeval = 0;  // rounds per frame and re-evaluations, summed
   size_t nwords = 0, wpart = 0;   // result words; offset of the partition masks
   bool jobs_built = false;
@@ -1434,6 +1443,9 @@ void rv_replay_destroy(rv_replay *r) {
   if (r->ev_join) (void)hipEventDestroy(r->ev_join);
   if (r->ev_ielig) (void)hipEventDestroy(r->ev_ielig);
   if (r->side) (void)hipStreamDestroy(r->side);
+  if (r->hp) (void)hipStreamSynchronize(r->hp), (void)hipStreamDestroy(r->hp);
+  if (r->ev_hp0) (void)hipEventDestroy(r->ev_hp0);
+  if (r->ev_hp1) (void)hipEventDestroy(r->ev_hp1);
   for (hipEvent_t ev : {r->ev_efork, r->ev_l1me, r->ev_epart})
     if (ev) (void)hipEventDestroy(ev);
   for (int l = 0; l < kLevels; l++) {
@@ -1683,6 +1695,17 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     r->mv_cnt = (int32_t *)dalloc(r, nr * 4);
     ok = ok && r->stk && r->mv_active && r->mv_cnt &&
          hipHostMalloc((void **)&r->h_mv, nr * 4, hipHostMallocDefault) == hipSuccess;
+    // RAV1E_HIP_MV_HP=1: the rounds after the first on a high-priority
+    // stream (2160p A/B: 140 vs 177 fps -- the other instance's work loses
+    // more than the rounds gain; off)
+    const char *hpe = getenv("RAV1E_HIP_MV_HP");
+    if (hpe && hpe[0] == '1') {
+      int least = 0, greatest = 0;
+      ok = ok && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+           hipStreamCreateWithPriority(&r->hp, hipStreamNonBlocking, greatest) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev_hp0, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev_hp1, hipEventDisableTiming) == hipSuccess;
+    }
     // does a superblock's top-right neighbour (same tile) lie past the right
     // frame edge, i.e. is it a must_split leaf?
     for (int sb = 0; sb < g.nsb && r->lvl; sb++) {
@@ -2467,25 +2490,29 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // (speed 10: SAD, no hp) -> NEWMV of every superblock and reference;
   // the candidates; F4; the argmin (round `round` of the stacks)
   auto f3_f4 = [&](int round) -> int {
+    // rounds after the first: the high-priority stream (their few
+    // superblocks' kernels get the next free CUs ahead of the other
+    // instance's bulk launches)
+    hipStream_t xs = round ? (r->hp ? r->hp : st) : st;
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
-                                 r->full, ev_full, &to_sub, st, act));
+                                 r->full, ev_full, &to_sub, xs, act));
     if (!round) RV_EV(5);
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1,
-                                 r->s6 ? 1 : 0, 0, g.bd, r->sub, ev_sub, nullptr, st, act));
+                                 r->s6 ? 1 : 0, 0, g.bd, r->sub, ev_sub, nullptr, xs, act));
     if (r->lvl && !edge && !lv_early) RV_R(lv_me(st));
     // the valid candidates (a few microseconds; bracketed with F3 sub-pel;
     // the count was zeroed by the previous argmin or at creation)
-    cand_list_kernel<<<(nsingle + 255) / 256, 256, 0, st>>>(cg, r->sub, nsingle, r->cand_list,
+    cand_list_kernel<<<(nsingle + 255) / 256, 256, 0, xs>>>(cg, r->sub, nsingle, r->cand_list,
                                                             r->cand_count, act);
     if (r->lvl && !edge && !lv_early) lv_lists(st, false);
     if (cg.comp) {  // the compound lists (after the single ones in the same arrays)
-      comp_list_kernel<<<(g.nsb * cg.comp + 255) / 256, 256, 0, st>>>(
+      comp_list_kernel<<<(g.nsb * cg.comp + 255) / 256, 256, 0, xs>>>(
           cg, r->sub, nsingle, r->cand_list + nsingle, r->cand_count + 1, act);
       if (r->lvl && !edge && !lv_early) lv_lists(st, true);
     }
     if (!round) RV_EV(6);
     // F4 every valid candidate, luma + both chroma planes in one fused launch
-    RV_R(rv_rdo_candidates(la4, ca4, g.hbd, st));
+    RV_R(rv_rdo_candidates(la4, ca4, g.hbd, xs));
     if (r->lvl && !edge && !lv_early) RV_R(lv_rdo(st));
     if (cg.comp) {  // the compound candidates (all pushed), distinct MV pairs from the list
       RdoArgs lc = la4, cc = ca4;
@@ -2495,7 +2522,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       lc.n_tx = g.nsb * cg.comp;
       cc.n_tx = g.nsb * cg.comp * ntx_c;
       if (!round) RV_EV(7);
-      RV_R(rv_rdo_candidates(lc, cc, g.hbd, st, true));
+      RV_R(rv_rdo_candidates(lc, cc, g.hbd, xs, true));
       if (r->lvl && !edge && !lv_early) RV_R(lv_rdo_comp(st));
     } else if (!round) {
       RV_EV(7);
@@ -2504,7 +2531,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       RV_EV(8);
       if (r->overlap) RV_H(hipStreamWaitEvent(st, r->ev_join, 0));  // the lookahead's MVs
     }
-    score_candidates<<<(g.nsb + 63) / 64, 64, 0, st>>>(
+    score_candidates<<<(g.nsb + 63) / 64, 64, 0, xs>>>(
         g, cg, L.lambda, L.ds[1], L.ds[2], r->sub, r->l_out, r->c_out, r->c_out + nct * 3, ntx_c,
         r->win, r->coarse, r->half, r->full, r->look, r->words, r->cand_count,
         r->overlap ? nullptr : r->tail + 2, r->cand_evals + 2 * slot * kLevels, r->leaf_count, act,
@@ -2533,23 +2560,48 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     if (changed) *changed = false;
     // the tail (the last check marked few superblocks): the predictive scan
     bool tail = false;
-    for (int k = 1;; k = k < 8 ? 2 * k : 8) {
-      const int first = mv_rounds;
-      if (first + k > max_rounds) k = max_rounds - first;
-      if (k <= 0)
-        return rv_set_error(RV_EHIP, "rv_replay_frame: the MV-stack rounds did not converge");
-      RV_H(hipMemsetAsync(r->mv_cnt + first, 0, (size_t)k * sizeof(int32_t), st));
-      for (int j = 0; j < k; j++) {
-        ma.init = 0;
-        ma.iwas = iwas;
-        ma.count = r->mv_cnt + first + j;
-        RV_R(rv_mvref_round(ma, st, tail));
-        RV_R(f3_f4(first + j));
+    hipStream_t xs = r->hp ? r->hp : st;
+    auto check = [&](int slot) -> int {
+      ma.init = 0;
+      ma.iwas = iwas;
+      ma.count = r->mv_cnt + slot;
+      return rv_mvref_round(ma, xs, tail);
+    };
+    // the rounds follow the main stream's work and it waits for them (their
+    // host reads synchronise xs only)
+    struct Join {
+      rv_replay *r;
+      hipStream_t st;
+      ~Join() {
+        if (r->hp && hipEventRecord(r->ev_hp1, r->hp) == hipSuccess)
+          (void)hipStreamWaitEvent(st, r->ev_hp1, 0);
       }
-      RV_H(hipMemcpyAsync(r->h_mv, r->mv_cnt + first, (size_t)k * sizeof(int32_t),
-                          hipMemcpyDeviceToHost, st));
-      RV_H(hipStreamSynchronize(st));
-      for (int j = 0; j < k; j++) {
+    } join{r, st};
+    if (r->hp) {
+      RV_H(hipEventRecord(r->ev_hp0, st));
+      RV_H(hipStreamWaitEvent(r->hp, r->ev_hp0, 0));
+    }
+    // a check alone first (most frames end there), then batches of
+    // (evaluation round, check) x k; counts[slot] = the superblocks the
+    // check marked for evaluation round `slot`
+    RV_H(hipMemsetAsync(r->mv_cnt + mv_rounds, 0, sizeof(int32_t), xs));
+    RV_R(check(mv_rounds));
+    for (int k = 0;; k = k ? (k < 8 ? 2 * k : 8) : 1) {
+      const int first = mv_rounds;  // the check of slot `first` is queued
+      if (k) {
+        if (first + k > max_rounds) k = max_rounds - first;
+        if (k <= 0)
+          return rv_set_error(RV_EHIP, "rv_replay_frame: the MV-stack rounds did not converge");
+        RV_H(hipMemsetAsync(r->mv_cnt + first + 1, 0, (size_t)k * sizeof(int32_t), xs));
+        for (int j = 0; j < k; j++) {
+          RV_R(f3_f4(first + j));  // a no-op once a check marked nothing
+          RV_R(check(first + j + 1));
+        }
+      }
+      RV_H(hipMemcpyAsync(r->h_mv, r->mv_cnt + first, (size_t)(k + 1) * sizeof(int32_t),
+                          hipMemcpyDeviceToHost, xs));
+      RV_H(hipStreamSynchronize(xs));
+      for (int j = 0; j <= k; j++) {
         if (mv_trace)
           fprintf(stderr, "mvref frame %ld level %d round %d: %d\n", ncoded, lv, first + j,
                   r->h_mv[j]);
@@ -2557,11 +2609,13 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
           mv_rounds = first + j;
           return RV_OK;
         }
-        r->mv_reeval += r->h_mv[j];
-        if (changed) *changed = true;
+        if (j < k) {  // round first + j evaluated them
+          r->mv_reeval += r->h_mv[j];
+          if (changed) *changed = true;
+        }
         tail = scan_on && r->h_mv[j] * 16 < g.nsb;
       }
-      mv_rounds = first + k;
+      mv_rounds = first + k;  // the check of slot first + k is not yet acted on
     }
   };
   if (r->exact) RV_R(mv_rounds_run(nullptr, nullptr));
