@@ -414,7 +414,8 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
                     speed=6 if flags & RP.RV_REPLAY_SPEED6 else 10,
                     deblock=bool(flags & RP.RV_REPLAY_DEBLOCK),
                     cdef=bool(flags & RP.RV_REPLAY_CDEF),
-                    intra=not flags & RP.RV_REPLAY_NO_INTRA)
+                    intra=not flags & RP.RV_REPLAY_NO_INTRA,
+                    mvref_standin=bool(flags & RP.RV_REPLAY_MVREF_STANDIN))
     for i in range(nin):
         c.set_input(i, g.get_input(i))
     if imp is not None:
@@ -445,6 +446,7 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
     (384, 192, 1, 1, 8, 2, {"tile_cols": 2}, 0),
     (384, 256, 0, 0, 8, 2, {"tiles": 4}, 0),
     (256, 192, 1, 1, 8, 2, None, RP.RV_REPLAY_EXHAUSTIVE_FS),
+    (320, 200, 1, 1, 8, 2, {"tile_cols": 2}, RP.RV_REPLAY_MVREF_STANDIN),  # the A/B stand-in stacks
     # speed 10 must_split at the frame edges (bottom; right + bottom; 4:4:4)
     (256, 232, 1, 1, 8, 2, None, 0),
     (200, 136, 1, 1, 10, 2, None, 0),
