@@ -1691,7 +1691,7 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
       ok = ok && r->dec_lv[l];
     }
     r->mv_active = (uint8_t *)dalloc(r, n);
-    const size_t nr = (size_t)g.tws * g.ths + 16;  // per-round counts (rv_replay_frame)
+    const size_t nr = (size_t)2 * g.tws * g.ths + 24;  // per-round counts (rv_replay_frame)
     r->mv_cnt = (int32_t *)dalloc(r, nr * 4);
     ok = ok && r->stk && r->mv_active && r->mv_cnt &&
          hipHostMalloc((void **)&r->h_mv, nr * 4, hipHostMallocDefault) == hipSuccess;
@@ -2547,7 +2547,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // counts, so a long dependency chain costs few host round trips; bounded
   // by the tiles' dependency depth (every round settles the next superblock
   // of each raster chain).  Returns with *changed = some round evaluated.
-  const int max_rounds = g.tws * g.ths + 2;
+  // (the intra pass's re-runs add rounds of their own: twice the bound)
+  const int max_rounds = 2 * g.tws * g.ths + 8;
   static const bool mv_trace = getenv("RAV1E_HIP_MV_TRACE") != nullptr;
   // RAV1E_HIP_MV_SCAN=1: the predictive per-tile scan in the tail rounds
   // (fewer rounds -- 2160p: 5.1 vs 12.9 per frame -- but each scan walks
