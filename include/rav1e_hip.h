@@ -488,14 +488,19 @@ int rv_full_search_sea_batch(const rv_plane *org, const rv_plane *ref,
  * src/predict.rs:255-338, PlaneSlice::clamp included) into on-chip memory.
  * Distortion: SAD (use_satd = 0) or SATD; cost = 256 * dist + rate *
  * lambda; candidates outside [mv*_min, mv*_max] cost u64::MAX. */
-#define RV_DS_MAX_PRED 8
+/* ArrayVec<[MotionVector; 17]>: get_subset_predictors' capacity
+ * (src/me.rs:82-88: zero, <= 7 coarse MVs, 3 + 1 of subsets A / B, 5 of
+ * subset C) */
+#define RV_DS_MAX_PRED 17
+/* references of one multi-reference launch (job i: ref[i / n_per_ref]) */
+#define RV_MAX_REFS 8
 typedef struct rv_ds_job {
   int32_t po_x, po_y;                 /* block origin (plane coords) */
   int32_t mvx_min, mvx_max;           /* get_mv_range, 1/8 pel */
   int32_t mvy_min, mvy_max;
   rv_mv pmv[2];                       /* rate predictors */
   uint32_t lambda;
-  int32_t n_pred;                     /* predictors used (<= 8) */
+  int32_t n_pred;                     /* predictors used (<= 17) */
   rv_mv pred[RV_DS_MAX_PRED];         /* search start candidates */
 } rv_ds_job;
 int rv_diamond_search_batch(const rv_plane *org, const rv_plane *ref,
@@ -728,7 +733,10 @@ int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,
  * the F4 single-reference / compound RDO candidates; with cap >= 11, out[5
  * .. 10] those of the 32x32, 16x16 and 8x8 blocks (speed 6); with cap >=
  * 14, out[11] superblocks intra-screened, out[12] intra winners, out[13]
- * intra rounds.  Returns the count. */
+ * intra rounds; with cap >= 17 (speed 10, since creation) out[14] the
+ * MV-stack evaluation rounds, out[15] the superblocks they re-evaluated,
+ * out[16] the frames; with cap >= 18, out[17] the round runs (1 + the MV /
+ * intra passes of each frame).  Returns the count. */
 int rv_replay_counters(rv_replay *r, uint64_t *out, int cap);
 
 /* ---------------------------------------------------------------------

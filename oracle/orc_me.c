@@ -166,3 +166,64 @@ uint64_t orc_tx_dist(const int32_t *coeffs, const int32_t *rcoeffs, int coded_ar
   const int bits = 2 * (3 - log_scale);
   return (d + (1ull << (bits - 1))) >> bits;
 }
+
+/* get_subset_predictors, src/me.rs:82-174: zero; the coarse MVs
+ * quantize_to_fullpel'd; subsets A and B from the tile's motion field
+ * (left, top, top-right, each pushed when non-zero, then their mean
+ * quantize_to_fullpel'd when non-zero); subset C from the reference frame's
+ * field (left, top, right, bottom, co-located, each when non-zero).
+ * tile: the tile's field (4x4 units, row pitch tp, tc columns), the block
+ * at (bx, by) in it; prev: the frame-size field of the reference frame
+ * (pitch pp, fc x fr 4x4 units; NULL: none), the block at frame (fx, fy).
+ * Returns the count (<= ORC_MAX_PRED). */
+int orc_subset_predictors(int bx, int by, const orc_mv *cmvs, int ncmv, const orc_mv *tile,
+                          int tp, int tc, const orc_mv *prev, int pp, int fc, int fr, int fx,
+                          int fy, orc_mv *out) {
+  int n = 0;
+  out[n++] = (orc_mv){0, 0};
+  for (int i = 0; i < ncmv; i++)
+    out[n++] = (orc_mv){(int16_t)((cmvs[i].row / 8) * 8), (int16_t)((cmvs[i].col / 8) * 8)};
+  orc_mv med[3];
+  int nm = 0;
+  if (bx > 0) {
+    const orc_mv l = tile[(size_t)by * tp + bx - 1];
+    med[nm++] = l;
+    if (l.row || l.col) out[n++] = l;
+  }
+  if (by > 0) {
+    const orc_mv t = tile[(size_t)(by - 1) * tp + bx];
+    med[nm++] = t;
+    if (t.row || t.col) out[n++] = t;
+    if (bx < tc - 1) {
+      const orc_mv tr = tile[(size_t)(by - 1) * tp + bx + 1];
+      med[nm++] = tr;
+      if (tr.row || tr.col) out[n++] = tr;
+    }
+  }
+  if (nm) {
+    /* MotionVector Add / Div<i16>: i16 arithmetic, truncating division */
+    int16_t sr = 0, sc = 0;
+    for (int i = 0; i < nm; i++) {
+      sr = (int16_t)(sr + med[i].row);
+      sc = (int16_t)(sc + med[i].col);
+    }
+    sr = (int16_t)(sr / nm);
+    sc = (int16_t)(sc / nm);
+    const orc_mv q = {(int16_t)((sr / 8) * 8), (int16_t)((sc / 8) * 8)};
+    if (q.row || q.col) out[n++] = q;
+  }
+  if (prev) {
+#define ORC_PREV(x, y)                                  \
+  do {                                                  \
+    const orc_mv v_ = prev[(size_t)(y) * pp + (x)];     \
+    if (v_.row || v_.col) out[n++] = v_;                \
+  } while (0)
+    if (fx > 0) ORC_PREV(fx - 1, fy);
+    if (fy > 0) ORC_PREV(fx, fy - 1);
+    if (fx < fc - 1) ORC_PREV(fx + 1, fy);
+    if (fy < fr - 1) ORC_PREV(fx, fy + 1);
+    ORC_PREV(fx, fy);
+#undef ORC_PREV
+  }
+  return n;
+}

@@ -32,8 +32,9 @@
 #define NSLOT 12
 #define NMODE 4
 /* result words per superblock and reference: coarse (mv, cost), the four
- * half-res quadrants, full-pel, sub-pel, the 16 lookahead 16x16 blocks */
-#define WPR (2 + 8 + 2 + 2 + 32)
+ * half-res quadrants (the encode's build_half_res_pmvs), full-pel, sub-pel,
+ * the 16 lookahead 16x16 blocks, the lookahead's four half-res quadrants */
+#define WPR (2 + 8 + 2 + 2 + 32 + 8)
 
 typedef struct {
   uint8_t *mem; /* allocation, element 0 */
@@ -42,6 +43,9 @@ typedef struct {
 
 typedef struct {
   oplane y, u, v, hres, qres;
+  /* the coded frame's motion field (FrameState::frame_mvs, saved with the
+   * reference, src/encoder.rs:3411-3429): [R][h_in_b][w_in_b] 4x4 units */
+  orc_mv *fmv;
 } oslot;
 
 typedef struct {
@@ -73,7 +77,11 @@ typedef struct orc_replay {
   /* per frame */
   orc_mv *coarse, *half, *full, *sub; /* [R][nsb] (half: [R][nsb][4]) */
   orc_mv *look;                        /* lookahead: [R][nsb][16] */
-  uint64_t *cc, *hc, *fc, *sc, *lc;
+  orc_mv *half_l;                      /* the lookahead's half-res quadrants [R][nsb][4] */
+  uint64_t *cc, *hc, *fc, *sc, *lc, *hlc;
+  /* the tile motion fields (TileMotionVectors, ts.mvs) of the encode and of
+   * the lookahead: [R][th * 16][tw * 16] over the group, 4x4 units */
+  orc_mv *tmv_e, *tmv_l;
   uint64_t *words;
   int32_t *lev; /* committed levels: per SB luma 1024 + 2 * ntx_c * 1024 */
   uint64_t tail[5];
@@ -380,6 +388,8 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile
         plane_init(&o->hres, W / 2, H / 2, 0, 0, 44, r->hbd) ||
         plane_init(&o->qres, W / 4, H / 4, 0, 0, 22, r->hbd))
       return NULL;
+    o->fmv = calloc((size_t)n_refs * r->w_in_b * r->h_in_b, sizeof(orc_mv));
+    if (!o->fmv) return NULL;
   }
   r->n_inputs = n_inputs;
   r->inputs = calloc(n_inputs, sizeof(oinput));
@@ -392,6 +402,10 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile
   size_t nr = (size_t)r->R * r->nsb;
   r->coarse = calloc(nr, sizeof(orc_mv));
   r->half = calloc(nr * 4, sizeof(orc_mv));
+  r->half_l = calloc(nr * 4, sizeof(orc_mv));
+  r->hlc = calloc(nr * 4, 8);
+  r->tmv_e = calloc((size_t)r->R * r->tw * 16 * r->th * 16, sizeof(orc_mv));
+  r->tmv_l = calloc((size_t)r->R * r->tw * 16 * r->th * 16, sizeof(orc_mv));
   r->look = calloc(nr * 16, sizeof(orc_mv));
   r->lc = calloc(nr * 16, 8);
   r->full = calloc(nr, sizeof(orc_mv));
@@ -423,6 +437,7 @@ void orc_replay_destroy(orc_replay *r) {
     free(o->v.mem);
     free(o->hres.mem);
     free(o->qres.mem);
+    free(o->fmv);
   }
   for (int i = 0; i < r->n_inputs; i++) {
     free(r->inputs[i].y.mem);
@@ -433,6 +448,10 @@ void orc_replay_destroy(orc_replay *r) {
   free(r->imp);
   free(r->coarse);
   free(r->half);
+  free(r->half_l);
+  free(r->hlc);
+  free(r->tmv_e);
+  free(r->tmv_l);
   free(r->look);
   free(r->lc);
   free(r->full);
@@ -948,7 +967,7 @@ static orc_mv coarse_fp(const orc_replay *r, int k, int sb) {
   return qfull((orc_mv){(int16_t)(c.row * 4), (int16_t)(c.col * 4)});
 }
 static orc_mv half_fp(const orc_replay *r, int k, int sb, int q) {
-  orc_mv h = r->half[((size_t)k * r->nsb + sb) * 4 + q];
+  orc_mv h = r->half_l[((size_t)k * r->nsb + sb) * 4 + q];
   return qfull((orc_mv){(int16_t)(h.row * 2), (int16_t)(h.col * 2)});
 }
 
@@ -983,37 +1002,87 @@ static void run_coarse(orc_replay *r, int sb) {
   }
 }
 
-/* Pass A2: F2 build_half_res_pmvs (src/encoder.rs:2864-3019): the four
- * 32x32 quadrants at half resolution (me_ss2, src/me.rs:465-519) from
- * [zero, the coarse MVs of the superblock, its horizontal and vertical
- * neighbour in the tile], each halved. */
-static void run_half(orc_replay *r, int sb) {
+/* ---- EPZS: the tile motion fields ------------------------------------------
+ * get_subset_predictors (src/me.rs:82-174) reads the tile's field ts.mvs
+ * (save_block_motion, src/encoder.rs:1432-1444): FrameState starts it at
+ * zero for every frame; build_half_res_pmvs saves the four quadrant MVs of
+ * each superblock, the lookahead's build_full_res_pmvs its 16x16 MVs, and
+ * the encode every coded inter block's MV (its first reference's index,
+ * src/encoder.rs:2607-2613).  The encode's field becomes the frame's
+ * frame_mvs, which later frames read through their LAST reference (subset
+ * C); the lookahead's reference frames carry none. */
+
+/* reference k's field of a group grid, at the tile of g (pitch tw * 16) */
+static orc_mv *tile_field(const orc_replay *r, orc_mv *grid, int k, const sbgeo *g) {
+  const size_t gp = (size_t)r->tw * 16;
+  return grid + (size_t)k * gp * r->th * 16 + (size_t)(g->t0y - r->ty0) * 16 * gp +
+         (size_t)(g->t0x - r->tx0) * 16;
+}
+/* save_block_motion: mv over the w4 x h4 block at tile offset (bx, by),
+ * clipped to the tile */
+static void save_motion(const orc_replay *r, orc_mv *tile, const sbgeo *g, int bx, int by, int w4,
+                        int h4, orc_mv mv) {
+  const size_t gp = (size_t)r->tw * 16;
+  const int xe = bx + w4 < g->mi_w ? bx + w4 : g->mi_w, ye = by + h4 < g->mi_h ? by + h4 : g->mi_h;
+  for (int y = by; y < ye; y++)
+    for (int x = bx; x < xe; x++) tile[(size_t)y * gp + x] = mv;
+}
+/* estimate_motion_ss4's result (the coarse MV * 4) */
+static orc_mv coarse4(const orc_replay *r, int k, int sb) {
+  const orc_mv c = r->coarse[(size_t)k * r->nsb + sb];
+  return (orc_mv){(int16_t)(c.row * 4), (int16_t)(c.col * 4)};
+}
+
+/* estimate_motion_ss2 (src/me.rs:280-327) of quadrant q of superblock sb
+ * against reference k: me_ss2 (:465-519) from get_subset_predictors at the
+ * adjust_bo'd 32x32 -- cmvs: the coarse MVs of the superblock and of its
+ * horizontal and vertical neighbour in the tile (build_half_res_pmvs,
+ * src/encoder.rs:2864-3019) -- over the tile field of `grid` and the
+ * reference frame's field `prev` (NULL: none), every predictor halved. */
+static void half_quadrant(orc_replay *r, int sb, int k, int q, orc_mv *grid, const orc_mv *prev,
+                          orc_mv *mv, uint64_t *cost) {
   const oslot *S = &r->slots[r->fi.display % NSLOT];
+  const oslot *ref = &r->slots[r->fi.ref_display[k] % NSLOT];
   const sbgeo g = sb_geo_of(r, sb);
   const double me_lambda = r->lv[r->fi.level].me_lambda;
-  uint32_t lambda2 = (uint32_t)(me_lambda * 256.0 / 4.0 * 0.125);
+  const uint32_t lambda2 = (uint32_t)(me_lambda * 256.0 / 4.0 * 0.125);
   const int hw = g.tsx > 0, he = g.tsx < g.tsw - 1, hn = g.tsy > 0, hs = g.tsy < g.tsh - 1;
+  orc_mv cm[3];
+  int nc = 0;
+  cm[nc++] = coarse4(r, k, sb);
+  if ((q & 1) ? he : hw) cm[nc++] = coarse4(r, k, (q & 1) ? sb + 1 : sb - 1);
+  if ((q >> 1) ? hs : hn) cm[nc++] = coarse4(r, k, (q >> 1) ? sb + r->tw : sb - r->tw);
+  int bx = g.tsx * 16 + (q & 1) * 8, by = g.tsy * 16 + (q >> 1) * 8;
+  adjust_bo(g.mi_w, g.mi_h, &bx, &by, 32, 32);
+  orc_mv p[ORC_MAX_PRED];
+  const int n = orc_subset_predictors(bx, by, cm, nc, tile_field(r, grid, k, &g), r->tw * 16,
+                                      g.mi_w, prev, r->w_in_b, r->w_in_b, r->h_in_b,
+                                      g.t0x * 16 + bx, g.t0y * 16 + by, p);
+  for (int i = 0; i < n; i++) {
+    p[i].row = (int16_t)(p[i].row >> 1);
+    p[i].col = (int16_t)(p[i].col >> 1);
+  }
+  orc_ds_ctx c;
+  ds_at(r, &c, &g, &S->hres, &ref->hres, bx, by, 32, 1, 1, lambda2);
+  orc_diamond_search(&c, p, n, mv, cost);
+}
+/* build_half_res_pmvs of superblock sb over `grid`: the four quadrants per
+ * reference, then their MVs (estimate_motion_ss2 returns the half-res MV *
+ * 2) saved into the field at the quadrants' own offsets (no adjust_bo). */
+static void half_sb(orc_replay *r, int sb, orc_mv *grid, orc_mv *mvs, uint64_t *costs, int encode) {
+  const sbgeo g = sb_geo_of(r, sb);
   for (int k = 0; k < r->R; k++) {
-    const oslot *ref = &r->slots[r->fi.ref_display[k] % NSLOT];
+    /* subset C: the LAST reference's frame_mvs (fi.rec_buffer.frames[
+     * fi.ref_frames[0]], src/me.rs:399-402, 479-481) */
+    const orc_mv *prev = encode ? r->slots[r->fi.ref_display[0] % NSLOT].fmv +
+                                      (size_t)k * r->w_in_b * r->h_in_b
+                                : NULL;
+    const size_t o = ((size_t)k * r->nsb + sb) * 4;
+    for (int q = 0; q < 4; q++) half_quadrant(r, sb, k, q, grid, prev, &mvs[o + q], &costs[o + q]);
+    orc_mv *tile = tile_field(r, grid, k, &g);
     for (int q = 0; q < 4; q++) {
-      orc_mv p[4];
-      int n = 0;
-      p[n++] = (orc_mv){0, 0};
-      p[n++] = coarse_fp(r, k, sb);
-      if ((q & 1) ? he : hw) p[n++] = coarse_fp(r, k, (q & 1) ? sb + 1 : sb - 1);
-      if ((q >> 1) ? hs : hn) p[n++] = coarse_fp(r, k, (q >> 1) ? sb + r->tw : sb - r->tw);
-      for (int i = 0; i < n; i++) {
-        p[i].row = (int16_t)(p[i].row >> 1);
-        p[i].col = (int16_t)(p[i].col >> 1);
-      }
-      orc_ds_ctx c;
-      ds_at(r, &c, &g, &S->hres, &ref->hres, g.tsx * 16 + (q & 1) * 8, g.tsy * 16 + (q >> 1) * 8,
-            32, 1, 1, lambda2);
-      orc_mv mv;
-      uint64_t cost;
-      orc_diamond_search(&c, p, n, &mv, &cost);
-      r->half[((size_t)k * r->nsb + sb) * 4 + q] = mv;
-      r->hc[((size_t)k * r->nsb + sb) * 4 + q] = cost;
+      const orc_mv m = {(int16_t)(mvs[o + q].row * 2), (int16_t)(mvs[o + q].col * 2)};
+      save_motion(r, tile, &g, g.tsx * 16 + (q & 1) * 8, g.tsy * 16 + (q >> 1) * 8, 8, 8, m);
     }
   }
 }
@@ -1033,14 +1102,25 @@ static void me64_sb(orc_replay *r, int sb) {
     orc_ds_ctx c;
     orc_mv fmv, smv;
     uint64_t cost;
-    orc_mv fp[2] = {zero, coarse_fp(r, k, sb)};
+    orc_mv fp[ORC_MAX_PRED] = {zero, coarse_fp(r, k, sb)};
+    int np = 2;
     ds_at(r, &c, &g, &cur->y, &ref->y, g.tsx * 16, g.tsy * 16, 64, 0, 0, lambda1);
     if (r->exact) {
       const struct ostk *s = &r->stk[sb];
       c.pmv[0] = s->n[k] >= 1 ? s->s[k][0] : zero;
       c.pmv[1] = s->n[k] >= 2 ? s->s[k][1] : zero;
+      /* full_pixel_me (src/me.rs:390-431): get_subset_predictors at the
+       * block, cmvs = [pmvs[0], the coarse MV], the encode's tile field,
+       * the LAST reference's frame field */
+      const orc_mv cm = coarse4(r, k, sb);
+      np = orc_subset_predictors(g.tsx * 16, g.tsy * 16, &cm, 1, tile_field(r, r->tmv_e, k, &g),
+                                 r->tw * 16, g.mi_w,
+                                 r->slots[r->fi.ref_display[0] % NSLOT].fmv +
+                                     (size_t)k * r->w_in_b * r->h_in_b,
+                                 r->w_in_b, r->w_in_b, r->h_in_b, g.t0x * 16 + g.tsx * 16,
+                                 g.t0y * 16 + g.tsy * 16, fp);
     }
-    orc_diamond_search(&c, fp, 2, &fmv, &cost);
+    orc_diamond_search(&c, fp, np, &fmv, &cost);
     r->full[k * r->nsb + sb] = fmv;
     r->fc[k * r->nsb + sb] = cost;
     c.subpel = 1;
@@ -1051,25 +1131,25 @@ static void me64_sb(orc_replay *r, int sb) {
   }
 }
 
-/* Pass A3: the lookahead's build_full_res_pmvs (src/encoder.rs:3021-3166,
- * 16x16 full-pel vs the references' original frames), F3 motion_estimation
- * of the 64x64 (src/me.rs:193-278: zero + the coarse MV, then sub-pel) and
- * of the levels' blocks. */
-static void run_me(orc_replay *r, int sb) {
+/* The lookahead's build_full_res_pmvs of superblock sb (src/encoder.rs:
+ * 3021-3166; compute_lookahead_motion_vectors, src/api/internal.rs:514-622):
+ * per reference the 16 16x16 blocks in raster order, each estimate_motion
+ * (src/me.rs:337-390: full-pel, adjust_bo'd) against the reference's
+ * original frame from get_subset_predictors over the lookahead's field --
+ * cmvs: the coarse MV, the covering quadrant, two vertical and two
+ * horizontal candidates of this and the adjacent superblocks -- its MV
+ * saved at the block (the reference frames carry no field: no subset C). */
+static void full_res_sb(orc_replay *r, int sb) {
   const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
-  const int R = r->R;
-  uint64_t cost;
   const sbgeo g = sb_geo_of(r, sb);
   const double me_lambda = r->lv[r->fi.level].me_lambda;
   uint32_t lambda1 = (uint32_t)(me_lambda * 256.0 * 0.5);
-  orc_mv zero = {0, 0};
-  const oslot *ref[2];
-  for (int k = 0; k < R; k++) ref[k] = &r->slots[r->fi.ref_display[k] % NSLOT];
   const int hw = g.tsx > 0, he = g.tsx < g.tsw - 1, hn = g.tsy > 0, hs = g.tsy < g.tsh - 1;
-  for (int k = 0; k < R; k++) {
+  for (int k = 0; k < r->R; k++) {
     const oplane *orig = &r->inputs[r->fi.ref_display[k] % r->n_inputs].y;
+    orc_mv *tile = tile_field(r, r->tmv_l, k, &g);
     /* pmvs_X[e] of superblock sb + (dx, dy): e = 0 coarse, 1..4 quadrants */
-#define PM(dx, dy, e, out)                                                         \
+#define PM(dx, dy, e)                                                              \
   do {                                                                             \
     const int ok_ = (dx) < 0 ? hw : (dx) > 0 ? he : (dy) < 0 ? hn : (dy) > 0 ? hs : 1; \
     if (ok_) {                                                                     \
@@ -1079,33 +1159,70 @@ static void run_me(orc_replay *r, int sb) {
   } while (0)
     for (int y = 0; y < 4; y++)
       for (int x = 0; x < 4; x++) {
-        orc_mv cand[8];
+        orc_mv cand[6];
         int nc = 0;
-        cand[nc++] = zero;
         const int L = x <= 1, T = y <= 1;
-        PM(0, 0, 0, _);
-        PM(0, 0, T ? (L ? 1 : 2) : (L ? 3 : 4), _);
+        PM(0, 0, 0);
+        PM(0, 0, T ? (L ? 1 : 2) : (L ? 3 : 4));
         switch (y) {
-          case 0: PM(0, -1, 0, _); PM(0, -1, L ? 3 : 4, _); break;
-          case 1: PM(0, -1, L ? 3 : 4, _); PM(0, 0, L ? 3 : 4, _); break;
-          case 2: PM(0, 1, L ? 1 : 2, _); PM(0, 0, L ? 1 : 2, _); break;
-          default: PM(0, 1, 0, _); PM(0, 1, L ? 1 : 2, _); break;
+          case 0: PM(0, -1, 0); PM(0, -1, L ? 3 : 4); break;
+          case 1: PM(0, -1, L ? 3 : 4); PM(0, 0, L ? 3 : 4); break;
+          case 2: PM(0, 1, L ? 1 : 2); PM(0, 0, L ? 1 : 2); break;
+          default: PM(0, 1, 0); PM(0, 1, L ? 1 : 2); break;
         }
         switch (x) {
-          case 0: PM(-1, 0, 0, _); PM(-1, 0, T ? 2 : 4, _); break;
-          case 1: PM(-1, 0, T ? 2 : 4, _); PM(0, 0, T ? 2 : 4, _); break;
-          case 2: PM(1, 0, T ? 1 : 3, _); PM(0, 0, T ? 1 : 3, _); break;
-          default: PM(1, 0, 0, _); PM(1, 0, T ? 2 : 4, _); break;
+          case 0: PM(-1, 0, 0); PM(-1, 0, T ? 2 : 4); break;
+          case 1: PM(-1, 0, T ? 2 : 4); PM(0, 0, T ? 2 : 4); break;
+          case 2: PM(1, 0, T ? 1 : 3); PM(0, 0, T ? 1 : 3); break;
+          default: PM(1, 0, 0); PM(1, 0, T ? 2 : 4); break;
         }
+        int bx = g.tsx * 16 + x * 4, by = g.tsy * 16 + y * 4;
+        adjust_bo(g.mi_w, g.mi_h, &bx, &by, 16, 16);
+        orc_mv p[ORC_MAX_PRED];
+        const int np = orc_subset_predictors(bx, by, cand, nc, tile, r->tw * 16, g.mi_w, NULL, 0,
+                                             0, 0, 0, 0, p);
         orc_ds_ctx c;
-        ds_at(r, &c, &g, &cur->y, orig, g.tsx * 16 + x * 4, g.tsy * 16 + y * 4, 16, 1, 0, lambda1);
+        ds_at(r, &c, &g, &cur->y, orig, bx, by, 16, 1, 0, lambda1);
         orc_mv mv;
-        orc_diamond_search(&c, cand, nc, &mv, &cost);
+        uint64_t cost;
+        orc_diamond_search(&c, p, np, &mv, &cost);
         r->look[((size_t)k * r->nsb + sb) * 16 + y * 4 + x] = mv;
         r->lc[((size_t)k * r->nsb + sb) * 16 + y * 4 + x] = cost;
+        save_motion(r, tile, &g, g.tsx * 16 + x * 4, g.tsy * 16 + y * 4, 4, 4, mv);
       }
 #undef PM
   }
+}
+
+/* The lookahead of one tile (index t of the group's tiles) in rav1e's
+ * order: build_half_res_pmvs of every superblock, then build_full_res_pmvs
+ * of every superblock, raster order (src/api/internal.rs:604-620). */
+static void lookahead_tile(orc_replay *r, int t) {
+  const int gtx = (r->tw + r->tws - 1) / r->tws;
+  const int tx0 = (t % gtx) * r->tws, ty0 = (t / gtx) * r->ths;
+  for (int pass = 0; pass < 2; pass++)
+    for (int y = ty0; y < ty0 + r->ths && y < r->th; y++)
+      for (int x = tx0; x < tx0 + r->tws && x < r->tw; x++) {
+        const int sb = y * r->tw + x;
+        if (r->sb_limit > 0 && sb >= r->sb_limit) continue; /* a bounded timing sample */
+        if (pass == 0)
+          half_sb(r, sb, r->tmv_l, r->half_l, r->hlc, 0);
+        else
+          full_res_sb(r, sb);
+      }
+}
+
+/* Pass A3: F3 motion_estimation of the 64x64 (src/me.rs:193-278: zero + the
+ * coarse MV, then sub-pel) outside coding order, and the levels' blocks. */
+static void run_me(orc_replay *r, int sb) {
+  const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
+  const int R = r->R;
+  uint64_t cost;
+  const double me_lambda = r->lv[r->fi.level].me_lambda;
+  uint32_t lambda1 = (uint32_t)(me_lambda * 256.0 * 0.5);
+  orc_mv zero = {0, 0};
+  const oslot *ref[2];
+  for (int k = 0; k < R; k++) ref[k] = &r->slots[r->fi.ref_display[k] % NSLOT];
   /* speed 10: the 64x64 search needs the superblock's MV stack (its pmv),
    * so it runs in coding order (chain_tile) */
   if (!r->exact) me64_sb(r, sb);
@@ -1354,6 +1471,10 @@ static void run_rdo(orc_replay *r, int sb, uint64_t tail[3]) {
     for (int q = 0; q < 16; q++) {
       wk[14 + 2 * q] = pack_mv(r->look[o * 16 + q]);
       wk[15 + 2 * q] = r->lc[o * 16 + q];
+    }
+    for (int q = 0; q < 4; q++) {
+      wk[46 + 2 * q] = pack_mv(r->half_l[o * 4 + q]);
+      wk[47 + 2 * q] = r->hlc[o * 4 + q];
     }
   }
   const int ppx = (sx + r->tx0) * SB, ppy = (sy + r->ty0) * SB;
@@ -1661,8 +1782,17 @@ static void grid_set(orc_replay *r, int x, int y, int w4, int h4, int c, orc_mv 
 }
 /* the coded blocks of superblock sb: its 64x64 winner, or the leaves the
  * partition committed (their candidates come from the levels' stand-in) */
+/* an inter block's first MV into the encode's field, under its first
+ * reference (save_block_motion after the partition decision,
+ * src/encoder.rs:2607-2613) */
+static void save_decision(orc_replay *r, const sbgeo *g, int bx, int by, int n4, int c, orc_mv m0) {
+  if (c >= INTRA_C) return;
+  const int k = c < r->C ? c / NMODE : 0;
+  save_motion(r, tile_field(r, r->tmv_e, k, g), g, bx, by, n4, n4, m0);
+}
 static void record_sb(orc_replay *r, int sb) {
   const int sx = sb % r->tw, sy = sb / r->tw;
+  const sbgeo g = sb_geo_of(r, sb);
   const uint64_t *w = r->words + (size_t)sb * (WPR * r->R + 4) + WPR * r->R;
   if (!r->lvl || r->leaf0[sb]) {
     const int c = (int)w[0];
@@ -1672,10 +1802,12 @@ static void record_sb(orc_replay *r, int sb) {
     else if (c < INTRA_C)
       comp_mvs(r, sb, c - r->C, &m0, &m1);
     grid_set(r, sx * 16, sy * 16, 16, 16, c, m0, m1);
+    save_decision(r, &g, g.tsx * 16, g.tsy * 16, 16, c, m0);
     return;
   }
   int ex, ey;
   if (!in_rect(r, sb, &ex, &ey)) return;
+  const sbgeo sg = g;
   for (int l = 1; l < 4; l++) {
     const struct olevel *P = &r->pl[l];
     const int k2 = 1 << l, n4 = 16 >> l;
@@ -1691,6 +1823,7 @@ static void record_sb(orc_replay *r, int sb) {
         else
           comp_mvs_g(&g, b, c - r->C, &m0, &m1);
         grid_set(r, sx * 16 + i * n4, sy * 16 + j * n4, n4, n4, c, m0, m1);
+        save_decision(r, &sg, sg.tsx * 16 + i * n4, sg.tsy * 16 + j * n4, n4, c, m0);
       }
   }
 }
@@ -1736,6 +1869,7 @@ static void chain_tile(orc_replay *r, int t, uint64_t tail[3]) {
     for (int x = tx0; x < tx0 + r->tws && x < r->tw; x++) {
       const int sb = y * r->tw + x;
       if (r->sb_limit > 0 && sb >= r->sb_limit) continue; /* a bounded timing sample */
+      half_sb(r, sb, r->tmv_e, r->half, r->hc, 1);  /* build_half_res_pmvs (encode) */
       stacks_sb(r, sb);
       me64_sb(r, sb);
       run_rdo(r, sb, tail);
@@ -1921,7 +2055,7 @@ static void *worker(void *arg) {
   orc_replay *r = arg;
   uint64_t tail[3] = {0, 0, 0};
   int lim = r->sb_limit > 0 && r->sb_limit < r->nsb ? r->sb_limit : r->nsb;
-  if (r->pass >= 4) /* the group's tiles */
+  if (r->pass >= 4) /* the group's tiles (passes 4, 5, 6) */
     lim = ((r->tw + r->tws - 1) / r->tws) * ((r->th + r->ths - 1) / r->ths);
   for (;;) {
     pthread_mutex_lock(&r->mu);
@@ -1930,16 +2064,16 @@ static void *worker(void *arg) {
     if (sb >= lim) break;
     if (r->pass == 0)
       run_coarse(r, sb);
-    else if (r->pass == 1)
-      run_half(r, sb);
     else if (r->pass == 2)
       run_me(r, sb);
     else if (r->pass == 3)
       run_rdo(r, sb, tail);
     else if (r->pass == 4)
-      intra_tile(r, sb); /* passes 4, 5: `sb` counts tiles */
-    else
+      intra_tile(r, sb); /* passes 4, 5, 6: `sb` counts tiles */
+    else if (r->pass == 5)
       chain_tile(r, sb, tail);
+    else
+      lookahead_tile(r, sb);
   }
   pthread_mutex_lock(&r->mu);
   for (int i = 0; i < 3; i++) r->tail[i] += tail[i];
@@ -1992,6 +2126,8 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
     memcpy(s->v.mem, in->v.mem, plane_size(&in->v, r->hbd));
     downsample(r, &s->hres, &in->y);
     downsample(r, &s->qres, &s->hres);
+    /* an intra frame saves no motion: its field stays zero */
+    memset(s->fmv, 0, (size_t)r->R * r->w_in_b * r->h_in_b * sizeof(orc_mv));
     r->coded++;
     return 0;
   }
@@ -2003,14 +2139,31 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
   memset(r->tail, 0, sizeof(r->tail));
   r->sb_limit = sb_limit;
   r->istat[0] = r->istat[1] = 0;
+  /* the tile fields start at zero (FrameState::new_with_frame) */
+  const size_t nf = (size_t)r->R * r->tw * 16 * r->th * 16;
+  memset(r->tmv_e, 0, nf * sizeof(orc_mv));
+  memset(r->tmv_l, 0, nf * sizeof(orc_mv));
+  /* F1; the lookahead (its F2 and 16x16 searches, tile by tile) */
+  run_pass(r, 0);
+  run_pass(r, 6);
   if (r->exact) {
-    /* speed 10: F1, F2, the lookahead and the levels' searches, then each
-     * tile in coding order (F3, F4, F6, F6b per superblock) */
-    for (int pass = 0; pass < 3; pass++) run_pass(r, pass);
+    /* speed 10: the levels' searches, then each tile in coding order (F2,
+     * F3, F4, F6, F6b per superblock) */
+    run_pass(r, 2);
     grid_reset(r);
     run_pass(r, 5);
+    /* the encode's field becomes the frame's frame_mvs (the group's part) */
+    for (int k = 0; k < r->R; k++)
+      for (int y = 0; y < r->th * 16 && r->ty0 * 16 + y < r->h_in_b; y++)
+        for (int x = 0; x < r->tw * 16 && r->tx0 * 16 + x < r->w_in_b; x++)
+          S->fmv[((size_t)k * r->h_in_b + r->ty0 * 16 + y) * r->w_in_b + r->tx0 * 16 + x] =
+              r->tmv_e[((size_t)k * r->th * 16 + y) * r->tw * 16 + x];
   } else {
-    for (int pass = 0; pass < 4; pass++) run_pass(r, pass);
+    /* speed 6 / the MV-stack stand-in: the encode's half-res quadrants are
+     * the lookahead's (no coding-order field) */
+    memcpy(r->half, r->half_l, (size_t)r->R * r->nsb * 4 * sizeof(orc_mv));
+    memcpy(r->hc, r->hlc, (size_t)r->R * r->nsb * 4 * 8);
+    for (int pass = 2; pass < 4; pass++) run_pass(r, pass);
     if (r->intra) run_pass(r, 4);
   }
   if (r->deblock || r->entropy) map_own(r);
@@ -2059,6 +2212,23 @@ int64_t orc_replay_xcopy(orc_replay *r, const int32_t *gr, void *buf, int to_buf
       }
       off += (int64_t)rc[2] * px;
     }
+  }
+  if (r->exact) { /* the group's part of the frame's motion field, per reference */
+    const int x0 = gr[0] * 16, y0 = gr[1] * 16;
+    const int x1 = (gr[0] + gr[2]) * 16 < r->w_in_b ? (gr[0] + gr[2]) * 16 : r->w_in_b;
+    const int y1 = (gr[1] + gr[3]) * 16 < r->h_in_b ? (gr[1] + gr[3]) * 16 : r->h_in_b;
+    for (int k = 0; k < r->R; k++)
+      for (int y = y0; y < y1; y++) {
+        orc_mv *q = s->fmv + ((size_t)k * r->h_in_b + y) * r->w_in_b + x0;
+        const size_t nb = (size_t)(x1 - x0) * sizeof(orc_mv);
+        if (b) {
+          if (to_buf)
+            memcpy(b + off, q, nb);
+          else
+            memcpy(q, b + off, nb);
+        }
+        off += (int64_t)nb;
+      }
   }
   if (r->deblock) { /* the group's rows of the block map: log2 sizes, skip flags */
     const int x0 = gr[0] * 16, y0 = gr[1] * 16;

@@ -203,6 +203,11 @@ typedef struct {
 } orc_ds_ctx;
 void orc_diamond_search(const orc_ds_ctx *c, const orc_mv *pred, int n_pred,
                         orc_mv *best_mv, uint64_t *best_cost);
+/* get_subset_predictors (src/me.rs:82-174, ArrayVec capacity 17) */
+#define ORC_MAX_PRED 17
+int orc_subset_predictors(int bx, int by, const orc_mv *cmvs, int ncmv, const orc_mv *tile,
+                          int tp, int tc, const orc_mv *prev, int pp, int fc, int fr, int fx,
+                          int fy, orc_mv *out);
 /* telescopic_subpel_search (src/me.rs:858-941): best_mv / lowest_cost are
  * the search's start (in) and result (out). */
 void orc_telescopic_subpel(const orc_ds_ctx *c, orc_mv *best_mv, uint64_t *lowest_cost);

@@ -61,7 +61,7 @@ FS_JOB = np.dtype([("po_x", "<i4"), ("po_y", "<i4"), ("x_lo", "<i4"), ("x_hi", "
 DS_JOB = np.dtype([("po_x", "<i4"), ("po_y", "<i4"), ("mvx_min", "<i4"), ("mvx_max", "<i4"),
                    ("mvy_min", "<i4"), ("mvy_max", "<i4"), ("pmv0_row", "<i2"),
                    ("pmv0_col", "<i2"), ("pmv1_row", "<i2"), ("pmv1_col", "<i2"),
-                   ("lambda_", "<u4"), ("n_pred", "<i4"), ("pred", "<i2", (8, 2))])
+                   ("lambda_", "<u4"), ("n_pred", "<i4"), ("pred", "<i2", (17, 2))])
 FS_RESULT = np.dtype([("mv_row", "<i2"), ("mv_col", "<i2"), ("reserved", "<u4"),
                       ("cost", "<u8")])
 REPLAY_CFG_FIELDS = ["width", "height", "xdec", "ydec", "bit_depth", "tile_x0", "tile_y0",

@@ -633,7 +633,10 @@ __global__ __launch_bounds__(1024) void ec_scan_frame_kernel(EcFrameArgs a, EcFr
       const int tx = k % ntx, ty = k / ntx;
       base += min(a.tws, a.tw - tx * a.tws) * min(a.ths, a.th - ty * a.ths);
     }
-    b.stat[3 + t] = b.offsets[b.sb_off[base]];
+    // sb_off holds unclamped prefix sums: past an overflow (dstat[1]) the
+    // index is clamped to the job count (the host drops the frame anyway)
+    const uint32_t j = b.sb_off[base];
+    b.stat[3 + t] = b.offsets[j < (uint32_t)n ? j : (uint32_t)n];
   }
 }
 

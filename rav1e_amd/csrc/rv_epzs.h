@@ -1,0 +1,152 @@
+// rv_epzs.h -- rav1e's EPZS predictor sets (get_subset_predictors,
+// src/me.rs:82-174) for the replay's searches, device side.
+//
+// Every full-pel search of rav1e starts from zero, its coarse MVs
+// (quantize_to_fullpel) and the MVs around the block: subsets A and B from
+// the tile's motion field ts.mvs (the left, top and top-right 4x4 units, and
+// their mean), subset C from the LAST reference frame's saved field
+// (left, top, right, bottom, co-located).  The tile field fills in coding
+// order (save_block_motion, src/encoder.rs:1432-1444), so a search depends
+// on the searches and decisions before it in the tile; the replay reaches
+// that order by the rounds of rv_replay_frame: every check
+// recomputes each job's set from the current state and re-runs the jobs
+// whose set changed.
+#pragma once
+
+#include "rv_chain.h"
+
+namespace rv {
+
+// The group's superblock grid and the frame (4x4 units: w_in_b x h_in_b)
+struct EpzsGeo {
+  int tx0, ty0, tw, th, tws, ths, W, H, w_in_b, h_in_b;
+};
+
+// The tile of frame superblock (fx, fy): its origin (superblocks) and
+// visible size in 4x4 units (TileStateMut mi_width / mi_height)
+__device__ inline void epzs_tile(const EpzsGeo &g, int fx, int fy, int &t0x, int &t0y, int &mi_w,
+                                 int &mi_h) {
+  t0x = fx - fx % g.tws;
+  t0y = fy - fy % g.ths;
+  const int vw = g.W - t0x * 64 < g.tws * 64 ? g.W - t0x * 64 : g.tws * 64;
+  const int vh = g.H - t0y * 64 < g.ths * 64 ? g.H - t0y * 64 : g.ths * 64;
+  mi_w = vw >> 2;
+  mi_h = vh >> 2;
+}
+
+// adjust_bo (src/me.rs:993-1004) on tile-relative 4x4 offsets
+__device__ inline void epzs_adjust_bo(int mi_w, int mi_h, int &bx, int &by, int bw, int bh) {
+  const int x = bx < mi_w - bw / 4 ? bx : mi_w - bw / 4;
+  const int y = by < mi_h - bh / 4 ? by : mi_h - bh / 4;
+  bx = x > 0 ? x : 0;
+  by = y > 0 ? y : 0;
+}
+
+__device__ inline rv_mv epzs_qfull(rv_mv m) {
+  return rv_mv{(int16_t)((m.row / 8) * 8), (int16_t)((m.col / 8) * 8)};
+}
+__device__ inline bool epzs_zero(rv_mv m) { return m.row == 0 && m.col == 0; }
+
+// get_subset_predictors of the block at tile offset (bx, by) of the tile at
+// frame 4x4 (tx4, ty4), mi_w columns: zero, the ncm coarse MVs cm, subsets
+// A / B through rd(X4, Y4) (the tile field at frame 4x4 (X4, Y4)), subset C
+// from prev (the reference frame's field at 8x8 granularity -- every value
+// of rav1e's field is constant over 8x8 cells at speed 10 -- cell (x, y)
+// at prev[((y * w_in_b / 2) + x) * pr]; null: none).  Returns the count
+// (<= RV_DS_MAX_PRED).
+template <typename Rd, typename Emit>
+__device__ inline int epzs_list(const EpzsGeo &g, int tx4, int ty4, int mi_w, int bx, int by,
+                                const rv_mv *cm, int ncm, Rd rd, const rv_mv *prev, int pr,
+                                Emit emit) {
+  int n = 0;
+  emit(n++, rv_mv{0, 0});
+  for (int i = 0; i < ncm; i++) emit(n++, epzs_qfull(cm[i]));
+  int16_t sr = 0, sc = 0;
+  int nm = 0;
+  if (bx > 0) {
+    const rv_mv l = rd(tx4 + bx - 1, ty4 + by);
+    sr = (int16_t)(sr + l.row);
+    sc = (int16_t)(sc + l.col);
+    nm++;
+    if (!epzs_zero(l)) emit(n++, l);
+  }
+  if (by > 0) {
+    const rv_mv t = rd(tx4 + bx, ty4 + by - 1);
+    sr = (int16_t)(sr + t.row);
+    sc = (int16_t)(sc + t.col);
+    nm++;
+    if (!epzs_zero(t)) emit(n++, t);
+    if (bx < mi_w - 1) {
+      const rv_mv tr = rd(tx4 + bx + 1, ty4 + by - 1);
+      sr = (int16_t)(sr + tr.row);
+      sc = (int16_t)(sc + tr.col);
+      nm++;
+      if (!epzs_zero(tr)) emit(n++, tr);
+    }
+  }
+  if (nm) {  // MotionVector / i16: truncating division
+    const rv_mv q = epzs_qfull(rv_mv{(int16_t)(sr / nm), (int16_t)(sc / nm)});
+    if (!epzs_zero(q)) emit(n++, q);
+  }
+  if (prev) {
+    const int fx = tx4 + bx, fy = ty4 + by, w8 = g.w_in_b >> 1;
+    auto pv = [&](int x, int y) {
+      const rv_mv v = prev[((y >> 1) * w8 + (x >> 1)) * pr];
+      if (!epzs_zero(v)) emit(n++, v);
+    };
+    if (fx > 0) pv(fx - 1, fy);
+    if (fy > 0) pv(fx, fy - 1);
+    if (fx < g.w_in_b - 1) pv(fx + 1, fy);
+    if (fy < g.h_in_b - 1) pv(fx, fy + 1);
+    pv(fx, fy);
+  }
+  return n;
+}
+
+// The set of a job into its record (shr: every predictor >> 1, me_ss2),
+// unless it already holds it; returns whether it changed.  Two passes over
+// the generator keep the set out of private arrays.
+template <typename Gen>
+__device__ inline bool epzs_update(rv_ds_job *j, int shr, Gen gen) {
+  auto tf = [&](rv_mv m) {
+    return shr ? rv_mv{(int16_t)(m.row >> 1), (int16_t)(m.col >> 1)} : m;
+  };
+  const int n0 = j->n_pred;
+  bool diff = false;
+  const int n = gen([&](int i, rv_mv m) {
+    if (i >= n0 || !mv_eq(j->pred[i], tf(m))) diff = true;
+  });
+  if (!diff && n == n0) return false;
+  gen([&](int i, rv_mv m) { j->pred[i] = tf(m); });
+  j->n_pred = n;
+  return true;
+}
+
+// The round checks' counts: check q counts into cnt[0..1] (slot q of the
+// ring), the last workgroup to finish reads them, zeroes the next check's
+// slot and the ticket, and stores (seq << 32 | cnt[0] + cnt[1]) into
+// host-mapped memory (the host spins on it, no stream synchronisation).
+// Every workgroup's counted appends returned before its ticket.
+struct RoundPub {
+  int32_t *cnt, *next;
+  uint32_t *ticket;
+  unsigned long long *host;  // null: nothing published
+  uint32_t seq;
+};
+__device__ inline void round_publish(const RoundPub &p) {
+  if (!p.host) return;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  __threadfence();
+  const uint32_t t = atomicAdd(p.ticket, 1u);
+  if (t != gridDim.x - 1) return;
+  __threadfence();
+  const int c = atomicAdd(p.cnt, 0) + atomicAdd(p.cnt + 1, 0);
+  p.next[0] = p.next[1] = 0;
+  *p.ticket = 0;
+  __threadfence();
+  __hip_atomic_store(p.host, ((unsigned long long)p.seq << 32) | (uint32_t)c, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+}  // namespace rv

@@ -106,12 +106,12 @@ __device__ __forceinline__ rv_fs_result write_result(const rv_fs_job &jb, Best b
 
 struct FsArgs {
   rv_plane org;
-  rv_plane ref[RV_DS_MAX_PRED];  // job i searches ref[i / n_per_ref]
+  rv_plane ref[RV_MAX_REFS];  // job i searches ref[i / n_per_ref]
   const rv_fs_job *jobs;
   rv_fs_result *out;
   int n, n_per_ref, hp, bw, bh, step;
   ChainNext next;  // replay: feed the winner into the next stage's jobs
-  const uint32_t *box[RV_DS_MAX_PRED];  // rv_plane_box_sums of each ref (SEA path)
+  const uint32_t *box[RV_MAX_REFS];  // rv_plane_box_sums of each ref (SEA path)
 };
 
 // blockIdx -> job with consecutive jobs on one XCD (blocks are dealt
@@ -797,7 +797,7 @@ int rv_full_search_multi(const rv_plane *org, const rv_plane *refs, int n_refs,
                          const rv_fs_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
                          int step, int allow_hp, rv_fs_result *d_out, const ChainNext *next,
                          const uint32_t *const *box, void *stream) {
-  if (!org || !refs || n_refs < 1 || n_refs > RV_DS_MAX_PRED || n_per_ref < 0 || blk_w < 4 ||
+  if (!org || !refs || n_refs < 1 || n_refs > RV_MAX_REFS || n_per_ref < 0 || blk_w < 4 ||
       blk_h < 4 || blk_w > 128 || blk_h > 128 || (blk_w & 3) || step < 1)
     return rv_set_error(RV_EINVAL, "rv_full_search_batch: bad arguments");
   for (int k = 0; k < n_refs; k++)

@@ -22,6 +22,7 @@
 //    prediction never leaves the wavefront.
 // SATD and square blocks of 8 and 16: ds_grp_kernel (lane groups per job).
 // Anything else takes the generic workgroup-per-candidate kernel.
+#include <algorithm>
 #include <stdlib.h>
 #include <string.h>
 
@@ -87,7 +88,7 @@ __device__ __forceinline__ int xcd_job(int n) {
 
 struct DsArgs {
   rv_plane org;
-  rv_plane ref[RV_DS_MAX_PRED];  // reference of job i = ref[i / n_per_ref]
+  rv_plane ref[RV_MAX_REFS];  // reference of job i = ref[i / n_per_ref]
   const rv_ds_job *jobs;
   rv_fs_result *out;
   int n, n_per_ref, w, h, subpel, satd, hp, bd;
@@ -97,7 +98,32 @@ struct DsArgs {
   const rv_fs_result *start;  // tele: the search's start (best_mv, lowest_cost)
   // replay rounds: only jobs j with active[j % n_per_ref] set run (null: all)
   const uint8_t *active;
+  // replay rounds after the first: the jobs a round's check listed; the
+  // grid is a fixed pool of workgroups that loops over them.  lper > 0:
+  // alist[0 .. *acount) are superblocks, each with lper consecutive jobs
+  // per reference (job = r * n_per_ref + sb * lper + e); lper = 0: alist
+  // holds job indices
+  const int32_t *alist;
+  const int32_t *acount;
+  int lper;
 };
+
+// The ordinal-th job of a list-driven launch (its size: ds_list_total)
+__device__ __forceinline__ int ds_list_total(const DsArgs &a) {
+  const int cnt = __builtin_amdgcn_readfirstlane(*a.acount);
+  return a.lper ? cnt * a.lper * (a.n / a.n_per_ref) : cnt;
+}
+__device__ __forceinline__ int ds_list_job(const DsArgs &a, int ord) {
+  if (!a.lper) return a.alist[ord];
+  const int cnt = *a.acount, per = cnt * a.lper;
+  const int r = ord / per, rem = ord - r * per, i = rem / a.lper;
+  return r * a.n_per_ref + a.alist[i] * a.lper + (rem - i * a.lper);
+}
+
+// Workgroups of a list-driven launch: enough to cover a typical round's
+// superblocks at once, few enough that a near-empty round costs ~1 us of
+// dispatch (a full 4080-workgroup grid of early exits costs ~10 us).
+constexpr int kDsListGrid = 512;
 
 __device__ __forceinline__ void ds_write(const DsArgs &a, int job, rv_mv center,
                                          uint64_t cost) {
@@ -292,7 +318,7 @@ struct DsFast {
 };
 
 template <typename Px, int W, int H, bool SUB>
-__device__ __forceinline__ void ds_fast_body(const DsArgs &a) {
+__device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
   using F = FullGeo<Px, W, H>;
   using S = SubGeo<Px, W, H>;
   constexpr int B = (int)sizeof(Px);
@@ -302,9 +328,6 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a) {
   __shared__ uint32_t win_all[SUB ? S::kUnionDwords : 1];
   __shared__ Px org_lds[SUB ? W * H : 1];  // sub-pel: the source block, shared by all waves
 
-  const int job = xcd_job(a.n);
-  if (job >= a.n) return;  // whole workgroup, uniformly
-  if (a.active && !a.active[job % a.n_per_ref]) return;  // settled this round
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const rv_ds_job *jp = a.jobs + job;  // pred[] read through the pointer
@@ -648,14 +671,33 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a) {
 // The 4-wavefront search at 5 waves per SIMD (<= 96 VGPRs: the u8 sub-pel
 // search fits without spilling), and at the compiler's choice
 // (RAV1E_HIP_DS_OCC4=1, A/B).
+// The workgroup's jobs: one (xcd_job) on a full grid, or, list-driven, the
+// listed superblocks' jobs (every reference's) from blockIdx.x in steps of
+// the grid.  Every bound is uniform over the workgroup.
+template <typename Px, int W, int H, bool SUB>
+__device__ __forceinline__ void ds_fast_jobs(const DsArgs &a) {
+  if (!a.alist) {
+    const int job = xcd_job(a.n);
+    if (job >= a.n) return;                                // whole workgroup, uniformly
+    if (a.active && !a.active[job % a.n_per_ref]) return;  // settled this round
+    ds_fast_body<Px, W, H, SUB>(a, job);
+    return;
+  }
+  const int total = ds_list_total(a);
+  for (int i = blockIdx.x; i < total; i += gridDim.x) {
+    ds_fast_body<Px, W, H, SUB>(a, __builtin_amdgcn_readfirstlane(ds_list_job(a, i)));
+    __syncthreads();  // the job's LDS reads end before the next job's writes
+  }
+}
+
 template <typename Px, int W, int H, bool SUB>
 __global__ __launch_bounds__(kDsThreads) __attribute__((amdgpu_waves_per_eu(5))) void
 ds_fast_kernel(DsArgs a) {
-  ds_fast_body<Px, W, H, SUB>(a);
+  ds_fast_jobs<Px, W, H, SUB>(a);
 }
 template <typename Px, int W, int H, bool SUB>
 __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel_occ4(DsArgs a) {
-  ds_fast_body<Px, W, H, SUB>(a);
+  ds_fast_jobs<Px, W, H, SUB>(a);
 }
 
 // ============================ generic path =================================
@@ -1058,17 +1100,19 @@ struct GrpGeo {
   static constexpr int CPL = NC * NC * LPC / C;        // chunks per lane
 };
 
+// ord: this lane group's ordinal among nord jobs (the wavefront's first
+// ordinal is < nord); the job is ord itself or, list-driven, its list entry
 template <typename Px, int N, bool SUB, bool SATD>
-__device__ __forceinline__ void ds_grp_body(const DsArgs &a) {
+__device__ __forceinline__ void ds_grp_body(const DsArgs &a, const int ord, const int nord) {
   using G = GrpGeo<N, !SUB && !SATD>;
   static_assert(G::CPL >= 1 && G::C % G::LPC == 0, "lane layout");
   const int lane = threadIdx.x & 63;
   const int gl = lane % G::L, k = gl / G::C, c = gl % G::C;
   const int gbase = lane - gl;  // the group's first lane
-  const int job = ((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * (64 / G::L) + lane / G::L;
-  if (job - (lane / G::L) >= a.n) return;  // the whole wavefront is past the jobs
-  const bool live = job < a.n;
-  const int jid = live ? job : a.n - 1;
+  const bool live = ord < nord;
+  const int oid = live ? ord : nord - 1;
+  const int job = a.alist ? ds_list_job(a, oid) : oid;
+  const int jid = job;
   const rv_ds_job *jp = a.jobs + jid;
   const rv_ds_job jb = *jp;
   const rv_plane &ref = a.ref[jid / a.n_per_ref];
@@ -1339,7 +1383,16 @@ __device__ __forceinline__ void ds_grp_body(const DsArgs &a) {
 
 template <typename Px, int N, bool SUB, bool SATD>
 __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
-  ds_grp_body<Px, N, SUB, SATD>(a);
+  using G = GrpGeo<N, !SUB && !SATD>;
+  constexpr int JPW = 64 / G::L;  // jobs per wavefront
+  const int lane = threadIdx.x & 63;
+  const int w0 = ((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * JPW;  // the wavefront's first
+  const int nord = a.alist ? ds_list_total(a) : a.n;
+  const int step = (int)gridDim.x * 4 * JPW;  // list-driven: a fixed pool loops
+  for (int o = w0; o < nord; o += step) {
+    ds_grp_body<Px, N, SUB, SATD>(a, o + lane / G::L, nord);
+    if (!a.alist) break;
+  }
 }
 template <typename Px>
 bool try_grp(const DsArgs &a, hipStream_t s) {
@@ -1348,7 +1401,8 @@ bool try_grp(const DsArgs &a, hipStream_t s) {
   const bool small = n == 8 || n == 16;
   if (!(small || (a.satd && (n == 32 || n == 64)))) return false;
   const int jpw = 64 / (n == 8 || (n == 16 && !a.subpel && !a.satd) ? 16 : 64);
-  const unsigned grid = (unsigned)((a.n + 4 * jpw - 1) / (4 * jpw));
+  unsigned grid = (unsigned)((a.n + 4 * jpw - 1) / (4 * jpw));
+  if (a.alist && grid > (unsigned)kDsListGrid) grid = kDsListGrid;
 #define RV_GRP(N)                                                                     \
   if (n == N) {                                                                       \
     if (a.subpel) {                                                                   \
@@ -1383,12 +1437,12 @@ static bool ds_full_wave() {
 
 template <typename Px, int W, int H, bool SUB>
 void launch_fast(const DsArgs &a, hipStream_t s) {
-  const unsigned grid = (unsigned)((a.n + 7) / 8 * 8);
+  const unsigned grid = a.alist ? (unsigned)std::min(a.n, kDsListGrid) : (unsigned)((a.n + 7) / 8 * 8);
   static const bool occ4 = [] {
     const char *e = getenv("RAV1E_HIP_DS_OCC4");
     return e && e[0] == '1';
   }();
-  if (!SUB && !a.tele && W * H <= 32 * 32 && ds_full_wave())
+  if (!SUB && !a.tele && W * H <= 32 * 32 && ds_full_wave() && !a.alist)
     ds_wave_kernel<Px, W, H><<<grid, 64, 0, s>>>(a);
   else if (occ4)
     ds_fast_kernel_occ4<Px, W, H, SUB><<<grid, kDsThreads, 0, s>>>(a);
@@ -1430,9 +1484,10 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             const rv_ds_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
                             int subpixel, int use_satd, int allow_hp, int bit_depth,
                             rv_fs_result *d_out, uint32_t *d_evals, const ChainNext *next,
-                            void *stream, const uint8_t *active) {
+                            void *stream, const uint8_t *active, const int32_t *alist,
+                            const int32_t *acount, int lper) {
   auto p2 = [](int v) { return v >= 4 && v <= 128 && (v & (v - 1)) == 0; };
-  if (!org || !refs || n_refs < 1 || n_refs > RV_DS_MAX_PRED || n_per_ref < 0 || !p2(blk_w) ||
+  if (!org || !refs || n_refs < 1 || n_refs > RV_MAX_REFS || n_per_ref < 0 || !p2(blk_w) ||
       !p2(blk_h) || (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
       (!org->hbd && bit_depth != 8))
     return rv_set_error(RV_EINVAL, "rv_diamond_search_batch: bad arguments");
@@ -1457,6 +1512,13 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
   a.bd = bit_depth;
   a.evals = d_evals;
   a.active = active;
+  a.alist = alist;
+  a.acount = acount;
+  a.lper = lper;
+  if (alist && (!acount || lper < 0 || use_satd ||
+                !((blk_w == 64 && blk_h == 64) || (blk_w == 16 && blk_h == 16 && !subpixel))))
+    return rv_set_error(RV_EINVAL,
+                        "rv_diamond_search_multi: list-driven launches: 64x64, or 16x16 full-pel SAD");
   if (next) a.next = *next;
   return ds_dispatch(a, stream);
 }
@@ -1495,7 +1557,8 @@ extern "C" int rv_diamond_search_batch(const rv_plane *org, const rv_plane *ref,
                                        rv_fs_result *d_out, void *stream) {
   if (!ref) return rv_set_error(RV_EINVAL, "rv_diamond_search_batch: null ref");
   return rv_diamond_search_multi(org, ref, 1, d_jobs, n, blk_w, blk_h, subpixel, use_satd,
-                                 allow_hp, bit_depth, d_out, nullptr, nullptr, stream, nullptr);
+                                 allow_hp, bit_depth, d_out, nullptr, nullptr, stream, nullptr,
+                                 nullptr, nullptr, 0);
 }
 
 // telescopic_subpel_search (src/me.rs:858-941) for every job in one launch:

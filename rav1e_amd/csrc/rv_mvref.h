@@ -4,6 +4,7 @@
 #pragma once
 
 #include "rv_chain.h"
+#include "rv_epzs.h"
 #include "rv_rdo.h"
 
 namespace rv {
@@ -30,7 +31,9 @@ struct MvrefArgs {
   const uint8_t *iwas;     // null, or 1: the superblock is an intra winner
   MvStack *stk;            // in / out: the stacks the superblocks were evaluated with
   uint8_t *active;         // out: 1 = (re-)evaluate this round
-  int32_t *count;          // out: += superblocks marked
+  int32_t *count;          // out: += superblocks marked (= pub.cnt)
+  int32_t *list;           // out: the marked superblocks (any order), count of them
+  RoundPub pub;            // the count's publication (pub.host null: none)
   rv_ds_job *jf, *js;      // the F3 jobs [R][nsb]: pmv = the stack's first two
   int init;                // 1: mark every superblock (the frame's first round)
   // speed 10 frame-edge leaves (a top-right neighbour past the right edge):
@@ -40,6 +43,20 @@ struct MvrefArgs {
   const RdoWinner *lwin[4];
   const rv_fs_result *lsub[4];
   CandGeo lcg[4];
+  // EPZS (get_subset_predictors, src/me.rs:82-174): a superblock is also
+  // marked when the predictor set of one of its F2 (build_half_res_pmvs
+  // quadrant) or F3 (64x64 full-pel) searches changed, the new set stored
+  // into the job.  The encode's tile field at a 4x4 unit: the coded block's
+  // first MV under its first reference, else the superblock's F2 quadrant
+  // MV (hq; the first check: the lookahead's, a guess), zero inside the
+  // superblock searching.
+  int epzs;
+  EpzsGeo eg;
+  rv_ds_job *jh;                // F2 jobs [R][nsb][4]
+  const rv_fs_result *coarse;   // F1 [R][nsb]
+  const rv_fs_result *hq;       // quadrant MVs (half-res) [R][nsb][4]
+  const rv_mv *prev;            // the LAST reference's field, [h_in_b/2][w_in_b/2][R]; null: none
+  int edge_ok;                  // the frame-edge leaves are final (lwin / lsub readable)
 };
 
 // The decision record of superblock sb's winner (candidate c of the
@@ -71,5 +88,11 @@ __device__ inline BlkDec blk_dec_of(const CandGeo &cg, const rv_fs_result *sub, 
 }  // namespace rv
 
 // One round over the group's superblocks (the first marks every one); scan:
-// the tail rounds' predictive per-tile wavefront scan.
+// the tail rounds' predictive per-tile wavefront scan (its tile must fit
+// the 64 KiB of LDS a workgroup may take: RV_EINVAL otherwise).
 int rv_mvref_round(const rv::MvrefArgs &a, hipStream_t s, bool scan = false);
+// The coded frame's field (the frame_mvs subset C of later frames reads) of
+// the group's part, into field ([h_in_b/2][w_in_b/2][R] rv_mv).
+int rv_mvref_field(const rv::MvrefArgs &a, rv_mv *field, hipStream_t s);
+// The largest tile (superblocks) the scan takes.
+constexpr int kMvrefScanMaxSb = 65536 / (int)sizeof(rv::BlkDec);

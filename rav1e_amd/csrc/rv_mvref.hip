@@ -20,6 +20,8 @@
 // re-evaluates exactly those whose stacks changed, until none does -- the
 // fixed point of the raster-order dependency chain, which is the
 // sequential result.
+#include <algorithm>
+
 #include "rv_mvref.h"
 
 using namespace rv;
@@ -260,6 +262,79 @@ __device__ inline void set_stacks(const MvrefArgs &a, int sb, const MvStack &s) 
   }
 }
 
+// The encode's tile field of reference k at frame 4x4 (X4, Y4), as the
+// superblock at frame (fsx, fsy) would read it in coding order
+__device__ inline rv_mv enc_field(const MvrefArgs &a, int k, int X4, int Y4, int fsx, int fsy) {
+  const int SX = X4 >> 4, SY = Y4 >> 4;
+  if (SX == fsx && SY == fsy) return rv_mv{0, 0};  // its own quadrants are saved after its F2
+  const int gsb = (SY - a.ty0) * a.tw + (SX - a.tx0);
+  const bool edge = a.lvl && ((SX + 1) * 64 > a.W || (SY + 1) * 64 > a.H);
+  BlkDec d;
+  d.ref[0] = kIntraFrame;
+  if (!edge || a.edge_ok) d = coded_at(a, gsb, X4 * 4, Y4 * 4);
+  if (d.ref[0] != kIntraFrame && d.ref[0] - 1 == k) return d.mv[0];
+  const rv_mv h = a.hq[((size_t)k * a.nsb + gsb) * 4 + ((Y4 >> 3) & 1) * 2 + ((X4 >> 3) & 1)].best_mv;
+  return rv_mv{(int16_t)(h.row * 2), (int16_t)(h.col * 2)};
+}
+
+// estimate_motion_ss4's result: the coarse MV * 4
+__device__ inline rv_mv coarse4(const MvrefArgs &a, int k, int sb) {
+  const rv_mv c = a.coarse[(size_t)k * a.nsb + sb].best_mv;
+  return rv_mv{(int16_t)(c.row * 4), (int16_t)(c.col * 4)};
+}
+
+// The superblock's F2 and F3 predictor sets from the current state into its
+// jobs; returns whether one changed.
+__device__ inline bool epzs_sb(const MvrefArgs &a, int sb, int fsx, int fsy) {
+  int t0x, t0y, mi_w, mi_h;
+  epzs_tile(a.eg, fsx, fsy, t0x, t0y, mi_w, mi_h);
+  const int tsx = fsx - t0x, tsy = fsy - t0y;
+  const int tsw = (mi_w + 15) / 16, tsh = (mi_h + 15) / 16;
+  const bool hw = tsx > 0, he = tsx < tsw - 1, hn = tsy > 0, hs = tsy < tsh - 1;
+  bool changed = false;
+  for (int k = 0; k < a.R; k++) {
+    auto rd = [&](int X4, int Y4) { return enc_field(a, k, X4, Y4, fsx, fsy); };
+    const rv_mv *prev = a.prev ? a.prev + k : nullptr;
+    // F3: full_pixel_me of the 64x64 (src/me.rs:390-431), cmvs = [pmvs[0]]
+    {
+      const rv_mv cm = coarse4(a, k, sb);
+      changed |= epzs_update(a.jf + (size_t)k * a.nsb + sb, 0, [&](auto emit) {
+        return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, tsx * 16, tsy * 16, &cm, 1, rd, prev,
+                         a.R, emit);
+      });
+    }
+    // F2: me_ss2 of the four quadrants (src/me.rs:465-519), adjust_bo'd,
+    // cmvs = the coarse MVs of the superblock and its neighbour on each side
+    for (int q = 0; q < 4; q++) {
+      rv_mv cm[3];
+      int nc = 0;
+      cm[nc++] = coarse4(a, k, sb);
+      if ((q & 1) ? he : hw) cm[nc++] = coarse4(a, k, (q & 1) ? sb + 1 : sb - 1);
+      if ((q >> 1) ? hs : hn) cm[nc++] = coarse4(a, k, (q >> 1) ? sb + a.tw : sb - a.tw);
+      int bx = tsx * 16 + (q & 1) * 8, by = tsy * 16 + (q >> 1) * 8;
+      epzs_adjust_bo(mi_w, mi_h, bx, by, 32, 32);
+      changed |= epzs_update(a.jh + ((size_t)k * a.nsb + sb) * 4 + q, 1, [&](auto emit) {
+        return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, prev, a.R, emit);
+      });
+    }
+  }
+  return changed;
+}
+
+// The coded frame's field: one thread per 8x8 cell of the group (inside the
+// frame), every reference
+__global__ __launch_bounds__(256) void mvref_field_kernel(MvrefArgs a, rv_mv *field) {
+  const int w8 = a.w_in_b >> 1, h8 = a.h_in_b >> 1;
+  const int x0 = a.tx0 * 8, y0 = a.ty0 * 8;
+  const int x1 = min((a.tx0 + a.tw) * 8, w8), y1 = min((a.ty0 + a.th) * 8, h8);
+  const int gw = x1 - x0;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= gw * (y1 - y0)) return;
+  const int x8 = x0 + i % gw, y8 = y0 + i / gw;
+  for (int k = 0; k < a.R; k++)
+    field[((size_t)y8 * w8 + x8) * a.R + k] = enc_field(a, k, 2 * x8, 2 * y8, -1, -1);
+}
+
 __global__ __launch_bounds__(256) void mvref_kernel(MvrefArgs a) {
   const int sb = blockIdx.x * 256 + threadIdx.x;
   bool mark = false;
@@ -287,11 +362,19 @@ __global__ __launch_bounds__(256) void mvref_kernel(MvrefArgs a) {
     if (nb.tl) nb.d = coded_at(a, sb - a.tw - 1, X - 4, Y - 4);
     const MvStack s = stacks_of(a, nb, split, fsx, fsy);
     mark = !same_stacks(a, a.stk[sb], s);
+    if (a.epzs) mark |= epzs_sb(a, sb, fsx, fsy);  // (always evaluated: it stores the sets)
     a.active[sb] = mark;
     if (mark) set_stacks(a, sb, s);
   }
+  // wave-aggregated append to the list (the returned base orders the
+  // workgroup's adds before its ticket below)
   const uint64_t m = __ballot(mark);
-  if ((threadIdx.x & 63) == 0 && m) atomicAdd(a.count, (int)__popcll(m));
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == 0 && m) base = atomicAdd(a.count, (int)__popcll(m));
+  base = __shfl(base, 0, 64);
+  if (mark) a.list[base + __popcll(m & ((1ull << lane) - 1))] = sb;
+  round_publish(a.pub);
 }
 
 
@@ -328,16 +411,13 @@ __device__ inline BlkDec predict(BlkDec d, const MvStack &s, int M, int R) {
 // hold.  The tile's decisions live in LDS.
 __global__ __launch_bounds__(64) void mvref_scan_kernel(MvrefArgs a) {
   extern __shared__ BlkDec pd[];
-  __shared__ int nmark;
   const int gtx = (a.tw + a.tws - 1) / a.tws;
   const int lx0 = (int)(blockIdx.x % gtx) * a.tws, ly0 = (int)(blockIdx.x / gtx) * a.ths;
   const int twd = min(a.tws, a.tw - lx0), tht = min(a.ths, a.th - ly0);
   const int ndiag = (twd - 1) + 2 * (tht - 1) + 1;
-  if (threadIdx.x == 0) nmark = 0;
   const int t0x = a.tx0 + lx0, t0y = a.ty0 + ly0;
   const int cols = min(a.tws * 16, a.w_in_b - t0x * 16);
   __syncthreads();
-  int mine = 0;
   for (int d = 0; d < ndiag; d++) {
     const int ylo = max(0, (d - twd + 2) / 2), yhi = min(tht - 1, d / 2);
     for (int y = ylo + (int)threadIdx.x; y <= yhi; y += (int)blockDim.x) {
@@ -370,27 +450,38 @@ __global__ __launch_bounds__(64) void mvref_scan_kernel(MvrefArgs a) {
       if (!mark) {
         pd[y * twd + x] = cur;  // evaluated under this very stack
       } else {
-        mine++;
         set_stacks(a, sb, s);
         pd[y * twd + x] = predict(cur, s, kCandModes, a.R);
+        a.list[atomicAdd(a.count, 1)] = sb;  // the returned index orders it before the ticket
       }
     }
     __syncthreads();  // the wavefront's decisions before the next one reads them
   }
-  if (mine) atomicAdd(&nmark, mine);
-  __syncthreads();
-  if (threadIdx.x == 0 && nmark) atomicAdd(a.count, nmark);
+  round_publish(a.pub);
 }
 }  // namespace
 
 int rv_mvref_round(const MvrefArgs &a, hipStream_t s, bool scan) {
   if (a.nsb <= 0) return RV_OK;
   if (scan && !a.init) {
+    if (a.epzs) return rv_set_error(RV_EINVAL, "rv_mvref_round: the scan does not track EPZS sets");
+    if (a.tws * a.ths > kMvrefScanMaxSb)
+      return rv_set_error(RV_EINVAL, "rv_mvref_round: the tile exceeds the scan's LDS");
     const int ntiles = ((a.tw + a.tws - 1) / a.tws) * ((a.th + a.ths - 1) / a.ths);
     mvref_scan_kernel<<<ntiles, 64, (size_t)a.tws * a.ths * sizeof(BlkDec), s>>>(a);
   } else {
     mvref_kernel<<<(a.nsb + 255) / 256, 256, 0, s>>>(a);
   }
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+int rv_mvref_field(const MvrefArgs &a, rv_mv *field, hipStream_t s) {
+  const int w8 = a.w_in_b >> 1, h8 = a.h_in_b >> 1;
+  const int gw = std::min((a.tx0 + a.tw) * 8, w8) - a.tx0 * 8;
+  const int gh = std::min((a.ty0 + a.th) * 8, h8) - a.ty0 * 8;
+  if (gw <= 0 || gh <= 0) return RV_OK;
+  mvref_field_kernel<<<(gw * gh + 255) / 256, 256, 0, s>>>(a, field);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

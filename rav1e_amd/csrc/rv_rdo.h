@@ -11,7 +11,7 @@ namespace rv {
 
 struct RdoPlane {
   rv_plane org;                  // source plane
-  rv_plane ref[RV_DS_MAX_PRED];  // reference planes of this plane type
+  rv_plane ref[2];               // reference planes of this plane type (the replay's R <= 2)
   rv_plane dst;                  // commit: the reconstruction plane (frame slot)
   int32_t *levels;               // commit: CA i32 levels per transform block
   uint64_t *out;                 // score: [dist skip, dist non-skip, rate] per transform block
@@ -67,6 +67,12 @@ int rv_quant_ctx(int qindex, int tx_area, int is_intra, int bit_depth, int dc_de
 // transform blocks of planes U and V (32x32, SSE) in one launch.
 int rv_rdo_candidates(const rv::RdoArgs &luma, const rv::RdoArgs &chroma, int hbd,
                       hipStream_t s, bool compound = false);
+
+// The MV-stack rounds after the first: the listed single-reference (ls,
+// cs) and, when lc / cc are given, compound candidates in one launch of
+// `grid` workgroups that loop over the device counts (8 / 10-bit).
+int rv_rdo_round(const rv::RdoArgs &ls, const rv::RdoArgs &cs, const rv::RdoArgs *lc,
+                 const rv::RdoArgs *cc, int hbd, hipStream_t s, int grid);
 
 // Blocks below 64x64 (speed 6): one launch over the tasks of a (luma or
 // the two chroma planes) for transform size n_tx_size; mode 0 single,

@@ -1100,10 +1100,12 @@ __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &
 
 // Chroma transform blocks, two per wavefront (one per half), plane U then
 // V: pair b of the launch.
+// pairs: per plane (default: the grid's size, from n_tx; list-driven
+// launches pass the count's).
 template <typename Px, int MODE>
 __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, int32_t *buf,
-                                                Px *pred, const uint16_t *scan) {
-  const int pairs = (chroma.n_tx + 1) / 2;  // per plane, for the grid's size
+                                                Px *pred, const uint16_t *scan, int pairs = -1) {
+  if (pairs < 0) pairs = (chroma.n_tx + 1) / 2;
   const int plane = b / pairs;
   const int half = (threadIdx.x & 63) >> 5;
   const int n = rdo_ntx(chroma);
@@ -1166,24 +1168,13 @@ struct QuadLds {
 // scoring launches into the narrow phases (waves 1..3 during the row DCT,
 // wave 2 for wave 0's candidate during the inverse rows); bit 1 raises the
 // priority of the waves running a narrow phase (s_setprio).
+// The workgroup's four luma candidates t0 = 4 b .. 4 b + 3 (n: the tasks)
 template <typename Px, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_quad_kernel(
-    RdoArgs luma, RdoArgs chroma, int nquads, int var) {
+__device__ __forceinline__ void rdo_quad_luma(const RdoArgs &luma, int b, int n, int var,
+                                              uint8_t *lds, const uint16_t *scan) {
   using L = typename QuadLds<Px>::L;
   constexpr int NPART = sizeof(Px) == 1 ? 2 : 4;
-  __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
-  __shared__ uint16_t scan[1024];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int b = blockIdx.x;
-  stage_scan(scan, b >= nquads ? chroma.q_tx_index : luma.q_tx_index);
-  if (b >= nquads) {  // chroma pairs: wave-local, no workgroup barriers
-    const int pair = 3 * (b - nquads) + wave;
-    if (wave == 3 || pair >= 2 * ((chroma.n_tx + 1) / 2)) return;
-    uint8_t *w = lds + wave * kChromaPair(sizeof(Px));
-    rdo_chroma_pair<Px, MODE>(chroma, pair, reinterpret_cast<int32_t *>(w),
-                        reinterpret_cast<Px *>(w + 2 * 32 * 33 * 4), scan);
-    return;
-  }
   auto slot = [&](int q) __attribute__((always_inline)) { return lds + q * L::kSlot; };
   auto fmid = [&](int q) __attribute__((always_inline)) {
     return reinterpret_cast<int32_t *>(slot(q));
@@ -1195,7 +1186,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     return reinterpret_cast<Px *>(slot(q) + L::kScr);
   };
   const int t0 = 4 * b, t = t0 + wave;
-  const int n = rdo_ntx(luma);
   if (t0 >= n) return;  // past the compacted list (uniform over the workgroup)
   const bool valid = t < n;
   RdoJob jb;
@@ -1243,6 +1233,61 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
   }
   __syncthreads();
   if (valid) luma_back<Px, int16_t>(luma, luma.p[0], t, jb, true, imid(wave), pred(wave));
+}
+
+// Chroma pairs 3 c .. 3 c + 2 of the launch, one per wavefront (wave 3
+// idles): wave-local, no workgroup barriers.  pairs: per plane.
+template <typename Px, int MODE>
+__device__ __forceinline__ void rdo_quad_chroma(const RdoArgs &chroma, int c, int pairs,
+                                                uint8_t *lds, const uint16_t *scan) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int pair = 3 * c + wave;
+  if (wave == 3 || pair >= 2 * pairs) return;
+  uint8_t *w = lds + wave * kChromaPair(sizeof(Px));
+  rdo_chroma_pair<Px, MODE>(chroma, pair, reinterpret_cast<int32_t *>(w),
+                            reinterpret_cast<Px *>(w + 2 * 32 * 33 * 4), scan, pairs);
+}
+
+template <typename Px, int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_quad_kernel(
+    RdoArgs luma, RdoArgs chroma, int nquads, int var) {
+  __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
+  __shared__ uint16_t scan[1024];
+  const int b = blockIdx.x;
+  stage_scan(scan, b >= nquads ? chroma.q_tx_index : luma.q_tx_index);
+  if (b >= nquads)  // chroma pairs
+    rdo_quad_chroma<Px, MODE>(chroma, b - nquads, (chroma.n_tx + 1) / 2, lds, scan);
+  else
+    rdo_quad_luma<Px, MODE>(luma, b, rdo_ntx(luma), var, lds, scan);
+}
+
+// The MV-stack rounds after the first (rv_replay_frame): the candidates of
+// the superblocks the round's check listed, single-reference (ls / cs,
+// MODE 0) and compound (lc / cc, MODE 1; null list: none) in one launch.
+// A fixed pool of workgroups walks the tasks the device counts give: the
+// single luma quads, the single chroma triples, then the compound ones.
+template <typename Px>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_round_kernel(
+    RdoArgs ls, RdoArgs cs, RdoArgs lc, RdoArgs cc, int var) {
+  __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
+  __shared__ uint16_t scan_l[1024], scan_c[1024];
+  stage_scan(scan_l, ls.q_tx_index);
+  stage_scan(scan_c, cs.q_tx_index);
+  const int ns = rdo_ntx(ls), ps = (rdo_ntx(cs) + 1) / 2;
+  const int nc = lc.list ? rdo_ntx(lc) : 0, pc = lc.list ? (rdo_ntx(cc) + 1) / 2 : 0;
+  const int q0 = (ns + 3) / 4, c0 = q0 + (2 * ps + 2) / 3;
+  const int q1 = c0 + (nc + 3) / 4, total = q1 + (2 * pc + 2) / 3;
+  for (int b = blockIdx.x; b < total; b += gridDim.x) {
+    if (b < q0)
+      rdo_quad_luma<Px, 0>(ls, b, ns, var, lds, scan_l);
+    else if (b < c0)
+      rdo_quad_chroma<Px, 0>(cs, b - q0, ps, lds, scan_c);
+    else if (b < q1)
+      rdo_quad_luma<Px, 1>(lc, b - c0, nc, var, lds, scan_l);
+    else
+      rdo_quad_chroma<Px, 1>(cc, b - q1, pc, lds, scan_c);
+    __syncthreads();  // the task's LDS reads end before the next task's writes
+  }
 }
 
 }  // namespace rv
@@ -1385,6 +1430,31 @@ int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipSt
     rdo_launch<1>(luma, chroma, hbd, s, single, cpairs);
   else
     rdo_launch<0>(luma, chroma, hbd, s, single, cpairs);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+int rv_rdo_round(const RdoArgs &ls, const RdoArgs &cs, const RdoArgs *lc, const RdoArgs *cc,
+                 int hbd, hipStream_t s, int grid) {
+  if (!ls.list || !ls.count || !cs.list || !cs.count || (lc && (!lc->list || !cc || !cc->list)) ||
+      ls.bd == 12 || grid <= 0)
+    return rv_set_error(RV_EINVAL, "rv_rdo_round: list-driven 8 / 10-bit launches only");
+  static const int var = [] {
+    const char *e = getenv("RAV1E_HIP_RDO_VARIANT");
+    return e ? atoi(e) : 3;
+  }();
+  RdoArgs l1, c1;
+  if (lc) {
+    l1 = *lc;
+    c1 = *cc;
+  } else {
+    memset(&l1, 0, sizeof(l1));
+    memset(&c1, 0, sizeof(c1));
+  }
+  if (hbd)
+    rdo_round_kernel<uint16_t><<<grid, 256, 0, s>>>(ls, cs, l1, c1, var);
+  else
+    rdo_round_kernel<uint8_t><<<grid, 256, 0, s>>>(ls, cs, l1, c1, var);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

@@ -32,6 +32,7 @@
 // produce the same result words.
 #include <string.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <algorithm>
 #include <deque>
@@ -64,7 +65,9 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             const rv_ds_job *d_jobs, int n_per_ref, int blk_w, int blk_h,
                             int subpixel, int use_satd, int allow_hp, int bit_depth,
                             rv_fs_result *d_out, uint32_t *d_evals, const rv::ChainNext *next,
-                            void *stream, const uint8_t *active = nullptr);
+                            void *stream, const uint8_t *active = nullptr,
+                            const int32_t *alist = nullptr, const int32_t *acount = nullptr,
+                            int lper = 1);
 // rv_deblock.hip
 int rv_deblock_plane_dev(const rv_plane *p, int pli, int width, int height, const uint8_t *d_lg,
                          const uint8_t *d_skip, int mi_stride, const uint8_t levels[4],
@@ -88,7 +91,10 @@ constexpr int kSb = 64;
 constexpr int kSlots = 12;  // DPB slots, keyed by display index % 12
 // result words per superblock and reference: coarse (mv, cost), the four
 // half-res quadrants, full-pel, sub-pel, the 16 lookahead 16x16 blocks
-constexpr int kWordsPerRef = 2 + 8 + 2 + 2 + 32;
+constexpr int kWordsPerRef = 2 + 8 + 2 + 2 + 32 + 8;
+// Workgroups of the list-driven launches of the MV-stack rounds after the
+// first (a fixed pool that loops over the device counts)
+constexpr int kRoundGrid = 256;
 constexpr int kMaxGroups = 8;
 
 struct Geo {
@@ -171,122 +177,151 @@ __global__ void coeff_checksum(const int32_t *packed, int64_t total, int per_blo
 // entropy coder's mode and MV bits are out of scope); rd = dist as f64 +
 // lambda * rate / 8 (src/rdo.rs:563-569).  One thread per superblock, which
 // also writes the superblock's result words.
+// One candidate's rd costs: skip (rs, distortion ds) and non-skip (rn, dn);
+// live = rav1e pushes it and it repeats no earlier candidate's MVs.
+struct CandCost {
+  double rs, rn;
+  uint64_t ds, dn;
+  int live;
+};
+__device__ inline CandCost cand_cost(const CandGeo &cg, double lambda, double ds_u, double ds_v,
+                                     const rv_fs_result *sub, const uint64_t *lout,
+                                     const uint64_t *uout, const uint64_t *vout, int ntx_c, int sb,
+                                     int c) {
+  CandCost k{0.0, 0.0, 0, 0, 0};
+  const int ns = cg.R * cg.M;  // single-reference candidates; compound ones follow
+  rv_mv mv;
+  if (c < ns ? !cand_live(cg, sub, sb, c, &mv) : !comp_live(cg, sub, sb, c - ns)) return k;
+  k.live = 1;
+  const int64_t o = (int64_t)c * cg.nsb + sb;
+  uint64_t su = 0, sv = 0, nu = 0, nv = 0;
+  uint32_t rate = (uint32_t)lout[o * 3 + 2];
+  for (int j = 0; j < ntx_c; j++) {
+    const int64_t t = (o * ntx_c + j) * 3;
+    su += uout[t];
+    sv += vout[t];
+    nu += uout[t + 1];
+    nv += vout[t + 1];
+    rate += (uint32_t)uout[t + 2] + (uint32_t)vout[t + 2];
+  }
+  // Distortion * dist_scale[p] -> ScaledDistortion, summed over planes
+  k.ds = (uint64_t)((double)lout[o * 3 + 0] * 1.0) + (uint64_t)((double)su * ds_u) +
+         (uint64_t)((double)sv * ds_v);
+  k.dn = (uint64_t)((double)lout[o * 3 + 1] * 1.0) + (uint64_t)((double)nu * ds_u) +
+         (uint64_t)((double)nv * ds_v);
+  k.rs = (double)k.ds + lambda * (0.0 / 8.0);
+  k.rn = (double)k.dn + lambda * ((double)rate / 8.0);
+  return k;
+}
+// The argmin step of candidate k after the ones before it (strict <; skip
+// first, non-skip unless the skip variant became the best at zero distortion)
+__device__ inline void argmin_step(RdoWinner &w, const CandCost &k, int c) {
+  if (!k.live) return;
+  bool zero_dist = false;
+  if (k.rs < w.cost) {
+    w = RdoWinner{c, 1, k.rs, k.ds};
+    zero_dist = k.ds == 0;
+  }
+  if (!zero_dist && k.rn < w.cost) w = RdoWinner{c, 0, k.rn, k.dn};
+}
+
+// compute_rd_cost + the per-superblock argmin (rdo_mode_decision): the
+// candidates in rav1e's order (reference-major: NEARESTMV, NEAR0MV,
+// GLOBALMV, NEWMV, then the compound modes), each skip first, then non-skip
+// unless the skip variant became the best with zero distortion
+// (luma_chroma_mode_rdo, src/rdo.rs:690-700); strict `<`.  ScaledDistortion
+// = luma + U + V (dist_scale 1.0); rate = the estimate_rate bits of every
+// transform block (the rate model of RDOType::TxDistEstRate,
+// src/encoder.rs:1226-1231; the entropy coder's mode and MV bits are out of
+// scope); rd = dist as f64 + lambda * rate / 8 (src/rdo.rs:563-569).
 __device__ inline RdoWinner block_argmin(const CandGeo &cg, double lambda, double ds_u,
                                          double ds_v, const rv_fs_result *sub,
                                          const uint64_t *lout, const uint64_t *uout,
                                          const uint64_t *vout, int ntx_c, int sb) {
-  double best = 1.7976931348623157e308;  // f64::MAX
-  RdoWinner w{0, 0, best, 0};
-  const int ns = cg.R * cg.M;  // single-reference candidates; compound ones follow
-  for (int c = 0; c < ns + cg.comp; c++) {
-    rv_mv mv;
-    if (c < ns ? !cand_live(cg, sub, sb, c, &mv) : !comp_live(cg, sub, sb, c - ns)) continue;
-    const int64_t o = (int64_t)c * cg.nsb + sb;
-    uint64_t su = 0, sv = 0, nu = 0, nv = 0;
-    uint32_t rate = (uint32_t)lout[o * 3 + 2];
-    for (int j = 0; j < ntx_c; j++) {
-      const int64_t t = (o * ntx_c + j) * 3;
-      su += uout[t];
-      sv += vout[t];
-      nu += uout[t + 1];
-      nv += vout[t + 1];
-      rate += (uint32_t)uout[t + 2] + (uint32_t)vout[t + 2];
-    }
-    // Distortion * dist_scale[p] -> ScaledDistortion, summed over planes
-    const uint64_t ds = (uint64_t)((double)lout[o * 3 + 0] * 1.0) + (uint64_t)((double)su * ds_u) +
-                        (uint64_t)((double)sv * ds_v);
-    const uint64_t dn = (uint64_t)((double)lout[o * 3 + 1] * 1.0) + (uint64_t)((double)nu * ds_u) +
-                        (uint64_t)((double)nv * ds_v);
-    bool zero_dist = false;
-    const double rs = (double)ds + lambda * (0.0 / 8.0);
-    if (rs < w.cost) {
-      w = RdoWinner{c, 1, rs, ds};
-      zero_dist = ds == 0;
-    }
-    if (!zero_dist) {
-      const double rn = (double)dn + lambda * ((double)rate / 8.0);
-      if (rn < w.cost) w = RdoWinner{c, 0, rn, dn};
-    }
-  }
+  RdoWinner w{0, 0, 1.7976931348623157e308, 0};  // f64::MAX
+  for (int c = 0; c < cg.R * cg.M + cg.comp; c++)
+    argmin_step(w, cand_cost(cg, lambda, ds_u, ds_v, sub, lout, uout, vout, ntx_c, sb, c), c);
   return w;
 }
 
-__global__ __launch_bounds__(64) void score_candidates(
+// The scoring of the superblocks a round evaluated, one wavefront per
+// superblock: lane c costs candidate c (the loads of every candidate in
+// flight at once), lane 0 walks the argmin in rav1e's order over the
+// wavefront's LDS copy, then the wavefront writes the superblock's winner,
+// decision record and result words.  The superblocks: every one (alist
+// null, round 0) or the list the round's check wrote (alist[0 .. *acount)).
+// A fixed pool of workgroups loops over them.  Block 0 also resets the
+// candidate lists' counts (consumed) and, on round 0, the frame's counters.
+constexpr int kScoreMaxCands = 2 * kCandModes + kCompModes;
+__global__ __launch_bounds__(256) void score_wave_kernel(
     Geo g, CandGeo cg, double lambda, double ds_u, double ds_v, const rv_fs_result *sub,
-    const uint64_t *lout,
-    const uint64_t *uout, const uint64_t *vout, int ntx_c, RdoWinner *win,
+    const uint64_t *lout, const uint64_t *uout, const uint64_t *vout, int ntx_c, RdoWinner *win,
     const rv_fs_result *coarse, const rv_fs_result *half, const rv_fs_result *full,
-    const rv_fs_result *look, uint64_t *words, int32_t *cand_count,
-    unsigned long long *imp_sum, uint32_t *evals, int32_t *leaf_count, const uint8_t *active,
-    BlkDec *dec, int round) {
-  const int sb = blockIdx.x * 64 + threadIdx.x;
-  if (sb == 0) {  // F4's lists are consumed: ready for the next frame; F5 sums next
-    // single-reference and compound candidates of the frame's first F4
-    // launch (the one the roofline times; later MV-stack rounds re-evaluate
-    // a few superblocks, counted by rv_replay_counters' [15])
+    const rv_fs_result *look, const rv_fs_result *half_l, uint64_t *words, int32_t *cand_count,
+    unsigned long long *imp_sum, uint32_t *evals, int32_t *leaf_count, const int32_t *alist,
+    const int32_t *acount, BlkDec *dec, int round) {
+  __shared__ CandCost kc[4][kScoreMaxCands];
+  __shared__ RdoWinner ws[4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = alist ? __builtin_amdgcn_readfirstlane(*acount) : g.nsb;
+  const int nc = cg.R * cg.M + cg.comp;
+  const int per = kWordsPerRef * g.R + 4;
+  for (int i = blockIdx.x * 4 + wave; i < n; i += gridDim.x * 4) {
+    const int sb = alist ? __builtin_amdgcn_readfirstlane(alist[i]) : i;
+    if (lane < nc)
+      kc[wave][lane] = cand_cost(cg, lambda, ds_u, ds_v, sub, lout, uout, vout, ntx_c, sb, lane);
+    wave_sync();
+    if (lane == 0) {
+      RdoWinner w{0, 0, 1.7976931348623157e308, 0};  // f64::MAX
+      for (int c = 0; c < nc; c++) argmin_step(w, kc[wave][c], c);
+      ws[wave] = w;
+      win[sb] = w;
+      if (dec) dec[sb] = blk_dec_of(cg, sub, sb, w.c);
+    }
+    wave_sync();
+    const RdoWinner w = ws[wave];
+    uint64_t *base = words + (int64_t)sb * per;
+    for (int wi = lane; wi < per; wi += 64) {
+      uint64_t v;
+      if (wi < kWordsPerRef * g.R) {
+        const int r = wi / kWordsPerRef, k = wi - r * kWordsPerRef, e = k >> 1;
+        const int64_t o = (int64_t)r * g.nsb + sb;
+        // [coarse, 4 half-res quadrants, full-pel, sub-pel, 16 lookahead, the
+        // lookahead's 4 half-res quadrants]
+        const rv_fs_result &f = e == 0 ? coarse[o] : e < 5 ? half[o * 4 + e - 1] : e == 5 ? full[o]
+                                : e == 6 ? sub[o] : e < 23 ? look[o * 16 + e - 7]
+                                : half_l[o * 4 + e - 23];
+        v = (k & 1) ? f.cost : pack_mv(f.best_mv);
+      } else {
+        const int j = wi - kWordsPerRef * g.R;
+        if (j == 0) {
+          v = (uint64_t)w.c;
+        } else if (j == 1) {
+          v = (uint64_t)w.skip;
+        } else if (j == 2) {
+          __builtin_memcpy(&v, &w.cost, 8);
+        } else {
+          v = w.dist;
+        }
+      }
+      base[wi] = v;
+    }
+    wave_sync();  // kc / ws of this superblock are read before the next one's writes
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // F4's lists are consumed: ready for the next round / frame.  Round 0:
+    // the single-reference and compound candidates of the frame's first F4
+    // launch (the one the roofline times; later rounds are counted by
+    // rv_replay_counters' [15]); F5 sums next; the partition decision
+    // appends next (the rounds the intra pass triggers may run after it)
     if (!round) {
       evals[0] = (uint32_t)cand_count[0];
       evals[1] = (uint32_t)cand_count[1];
+      if (imp_sum) *imp_sum = 0;  // null: F5 ran on the side stream (it zeroed its sum)
+      if (leaf_count)
+        for (int l = 0; l < 4; l++) leaf_count[l] = 0;
     }
     cand_count[0] = cand_count[1] = 0;
-    // once per frame: the MV-stack rounds after the first may run after the
-    // partition decision filled the leaf lists (the rounds the intra pass
-    // triggers)
-    if (imp_sum && !round) *imp_sum = 0;  // null: F5 ran on the side stream (it zeroed its sum)
-    if (leaf_count && !round)  // the partition decision appends next
-      for (int l = 0; l < 4; l++) leaf_count[l] = 0;
-  }
-  __shared__ RdoWinner ws[64];
-  __shared__ uint8_t act[64];
-  // the MV-stack rounds after the first evaluate a few superblocks: a
-  // workgroup holding none of them has nothing to do
-  const bool mine = sb < g.nsb && (!active || active[sb]);
-  act[threadIdx.x] = mine;
-  if (!__syncthreads_or(mine)) return;
-  if (sb < g.nsb) {
-    RdoWinner w;
-    if (mine) {  // a superblock evaluated this round
-      w = block_argmin(cg, lambda, ds_u, ds_v, sub, lout, uout, vout, ntx_c, sb);
-      win[sb] = w;
-      if (dec) dec[sb] = blk_dec_of(cg, sub, sb, w.c);
-    } else {
-      w = win[sb];
-    }
-    ws[threadIdx.x] = w;
-  }
-  __syncthreads();
-  // the result words of the workgroup's superblocks (one contiguous run):
-  // lane i stores word i, i + 64, ... so every store coalesces
-  const int sb0 = blockIdx.x * 64, nb = g.nsb - sb0 < 64 ? g.nsb - sb0 : 64;
-  const int per = kWordsPerRef * g.R + 4;
-  uint64_t *base = words + (int64_t)sb0 * per;
-  for (int i = threadIdx.x; i < nb * per; i += 64) {
-    const int s = i / per, wi = i - s * per, b = sb0 + s;
-    // a superblock not evaluated this round keeps its words (an intra
-    // winner's among them)
-    if (!act[s]) continue;
-    uint64_t v;
-    if (wi < kWordsPerRef * g.R) {
-      const int r = wi / kWordsPerRef, k = wi - r * kWordsPerRef, e = k >> 1;
-      const int64_t o = (int64_t)r * g.nsb + b;
-      // [coarse, 4 half-res quadrants, full-pel, sub-pel, 16 lookahead]
-      const rv_fs_result &f = e == 0 ? coarse[o] : e < 5 ? half[o * 4 + e - 1] : e == 5 ? full[o]
-                              : e == 6 ? sub[o] : look[o * 16 + e - 7];
-      v = (k & 1) ? f.cost : pack_mv(f.best_mv);
-    } else {
-      const RdoWinner &w = ws[s];
-      const int j = wi - kWordsPerRef * g.R;
-      if (j == 0) {
-        v = (uint64_t)w.c;
-      } else if (j == 1) {
-        v = (uint64_t)w.skip;
-      } else if (j == 2) {
-        __builtin_memcpy(&v, &w.cost, 8);
-      } else {
-        v = w.dist;
-      }
-    }
-    base[i] = v;
   }
 }
 
@@ -299,7 +334,7 @@ __global__ void fill_preds_kernel(rv_ds_job *jobs, const int32_t *src, int n,
                                   const rv_fs_result *coarse, const rv_fs_result *half, int shr) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  for (int p = 1; p < RV_DS_MAX_PRED; p++) {
+  for (int p = 1; p < 8; p++) {  // src: 8 entries per job, [0] unused
     const int v = src[8 * i + p];
     if (v < 0) break;
     const rv_mv m = (v & 1) ? half[v >> 1].best_mv : coarse[v >> 1].best_mv;
@@ -308,6 +343,112 @@ __global__ void fill_preds_kernel(rv_ds_job *jobs, const int32_t *src, int n,
     if (shr) q = rv_mv{(int16_t)(q.row >> 1), (int16_t)(q.col >> 1)};
     jobs[i].pred[p] = q;
   }
+}
+
+// ---- the lookahead's EPZS rounds ---------------------------------------------
+// compute_lookahead_motion_vectors (src/api/internal.rs:514-622) searches a
+// tile's superblocks in raster order, first every build_half_res_pmvs
+// (F2L: four 32x32 quadrants at half resolution), then every
+// build_full_res_pmvs (FL: sixteen 16x16 blocks), each from
+// get_subset_predictors over the lookahead's own tile field, which starts
+// at zero and takes the quadrants' and then the 16x16 blocks' MVs as they
+// are found (save_block_motion); its references carry no field (no subset
+// C).  A check recomputes every job's set from the current results and
+// lists the jobs whose set changed; a round re-runs them.
+struct LaArgs {
+  Geo g;
+  EpzsGeo eg;
+  rv_ds_job *jh, *jl;            // F2L jobs [R][nsb][4], FL jobs [R][nsb][16]
+  const int32_t *sl;             // FL's cmv sources (8 per job, fill_preds_kernel's code)
+  const rv_fs_result *coarse, *half_l, *look;
+  int32_t *list_h, *list_l;      // out: the marked F2L / FL jobs
+  int init;                      // 1: store the sets, mark nothing
+  int what;                      // bit 0: the F2L jobs, bit 1: the FL jobs
+  RoundPub pub;                  // pub.cnt: [F2L marked, FL marked]
+};
+
+__device__ inline rv_mv la_coarse4(const LaArgs &a, int k, int sb) {
+  const rv_mv c = a.coarse[(size_t)k * a.g.nsb + sb].best_mv;
+  return rv_mv{(int16_t)(c.row * 4), (int16_t)(c.col * 4)};
+}
+
+__global__ __launch_bounds__(256) void la_check_kernel(LaArgs a) {
+  const Geo &g = a.g;
+  const int nh = (a.what & 1) ? g.R * g.nsb * 4 : 0, nl = (a.what & 2) ? g.R * g.nsb * 16 : 0;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  bool mh = false, ml = false;
+  int job = 0;
+  if (i < nh) {  // F2L: me_ss2 of quadrant q (src/me.rs:465-519)
+    job = i;
+    const int k = i / (g.nsb * 4), sb = (i / 4) % g.nsb, q = i % 4;
+    const int sx = sb % g.tw, sy = sb / g.tw;
+    int t0x, t0y, mi_w, mi_h;
+    sb_tile(g, sx, sy, t0x, t0y, mi_w, mi_h);
+    const int fsx = g.tx0 + sx, fsy = g.ty0 + sy, tsx = fsx - t0x, tsy = fsy - t0y;
+    const int tsw = (mi_w + 15) / 16, tsh = (mi_h + 15) / 16;
+    rv_mv cm[3];
+    int nc = 0;
+    cm[nc++] = la_coarse4(a, k, sb);
+    if ((q & 1) ? tsx < tsw - 1 : tsx > 0) cm[nc++] = la_coarse4(a, k, (q & 1) ? sb + 1 : sb - 1);
+    if ((q >> 1) ? tsy < tsh - 1 : tsy > 0) cm[nc++] = la_coarse4(a, k, (q >> 1) ? sb + g.tw : sb - g.tw);
+    int bx = tsx * 16 + (q & 1) * 8, by = tsy * 16 + (q >> 1) * 8;
+    adjust_bo(mi_w, mi_h, bx, by, 32, 32);
+    // the field: an earlier superblock's quadrant MV (estimate_motion_ss2's *
+    // 2), zero inside this one (its quadrants are saved after all four)
+    auto rd = [&](int X4, int Y4) {
+      const int SX = X4 >> 4, SY = Y4 >> 4;
+      if (SX == fsx && SY == fsy) return rv_mv{0, 0};
+      const int gsb = (SY - g.ty0) * g.tw + (SX - g.tx0);
+      const rv_mv h =
+          a.half_l[((size_t)k * g.nsb + gsb) * 4 + ((Y4 >> 3) & 1) * 2 + ((X4 >> 3) & 1)].best_mv;
+      return rv_mv{(int16_t)(h.row * 2), (int16_t)(h.col * 2)};
+    };
+    mh = epzs_update(a.jh + i, 1, [&](auto emit) {
+      return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, nullptr, 1, emit);
+    }) && !a.init;
+  } else if (i - nh < nl) {  // FL: estimate_motion of 16x16 block b (src/me.rs:337-390)
+    const int j = i - nh;
+    job = j;
+    const int k = j / (g.nsb * 16), sb = (j / 16) % g.nsb, b = j % 16;
+    const int sx = sb % g.tw, sy = sb / g.tw;
+    int t0x, t0y, mi_w, mi_h;
+    sb_tile(g, sx, sy, t0x, t0y, mi_w, mi_h);
+    const int tsx = g.tx0 + sx - t0x, tsy = g.ty0 + sy - t0y;
+    rv_mv cm[6];
+    int nc = 0;
+    for (int p = 1; p < 7; p++) {  // the coarse MV, the covering quadrant, 4 neighbours'
+      const int v = a.sl[8 * j + p];
+      if (v < 0) break;
+      const rv_mv m = (v & 1) ? a.half_l[v >> 1].best_mv : a.coarse[v >> 1].best_mv;
+      const int sc = (v & 1) ? 2 : 4;
+      cm[nc++] = rv_mv{(int16_t)(m.row * sc), (int16_t)(m.col * sc)};
+    }
+    int bx = tsx * 16 + (b % 4) * 4, by = tsy * 16 + (b / 4) * 4;
+    adjust_bo(mi_w, mi_h, bx, by, 16, 16);
+    // the field: the 16x16 block holding the unit (every block read comes
+    // before this one in raster order, so it holds its FL MV)
+    auto rd = [&](int X4, int Y4) {
+      const int gsb = ((Y4 >> 4) - g.ty0) * g.tw + ((X4 >> 4) - g.tx0);
+      return a.look[((size_t)k * g.nsb + gsb) * 16 + ((Y4 & 15) >> 2) * 4 + ((X4 & 15) >> 2)]
+          .best_mv;
+    };
+    ml = epzs_update(a.jl + j, 0, [&](auto emit) {
+      return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, nullptr, 1, emit);
+    }) && !a.init;
+  }
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1;
+  const uint64_t bh = __ballot(mh), bl = __ballot(ml);
+  int b0 = 0, b1 = 0;
+  if (lane == 0) {
+    if (bh) b0 = atomicAdd(a.pub.cnt, (int)__popcll(bh));
+    if (bl) b1 = atomicAdd(a.pub.cnt + 1, (int)__popcll(bl));
+  }
+  b0 = __shfl(b0, 0, 64);
+  b1 = __shfl(b1, 0, 64);
+  if (mh) a.list_h[b0 + __popcll(bh & below)] = job;
+  if (ml) a.list_l[b1 + __popcll(bl & below)] = job;
+  round_publish(a.pub);
 }
 
 // The valid candidates (cand_mv true) of every superblock, compacted for
@@ -350,6 +491,41 @@ __global__ __launch_bounds__(256) void comp_list_kernel(CandGeo cg, const rv_fs_
   if (lane == 0 && m) base = atomicAdd(count, (int)__popcll(m));
   base = __shfl(base, 0, 64);
   if (v) list[base + __popcll(m & ((1ull << lane) - 1))] = nsingle + i;
+}
+
+// The rounds after the first: both candidate lists (single-reference, then
+// compound from nsingle on) of the superblocks the round's check listed,
+// over a fixed pool of workgroups; wave-aggregated appends as above.
+__global__ __launch_bounds__(256) void round_lists_kernel(CandGeo cg, const rv_fs_result *sub,
+                                                          int nsingle, int32_t *list,
+                                                          int32_t *count, const int32_t *alist,
+                                                          const int32_t *acount) {
+  const int cnt = __builtin_amdgcn_readfirstlane(*acount);
+  const int ns = cg.R * cg.M, total = cnt * (ns + cg.comp);
+  const int lane = threadIdx.x & 63;
+  for (int b0 = blockIdx.x * 256; b0 < total; b0 += gridDim.x * 256) {
+    const int i = b0 + (int)threadIdx.x;
+    bool v = false;
+    int c = 0, sb = 0;
+    if (i < total) {
+      c = i / cnt;
+      sb = alist[i - c * cnt];
+      rv_mv mv;
+      v = c < ns ? cand_live(cg, sub, sb, c, &mv) : comp_live(cg, sub, sb, c - ns);
+    }
+    const bool comp = c >= ns;  // uniform per wavefront only where the split falls between them
+    const uint64_t ms = __ballot(v && !comp), mc = __ballot(v && comp);
+    int bs = 0, bc = 0;
+    if (lane == 0) {
+      if (ms) bs = atomicAdd(count, (int)__popcll(ms));
+      if (mc) bc = atomicAdd(count + 1, (int)__popcll(mc));
+    }
+    bs = __shfl(bs, 0, 64);
+    bc = __shfl(bc, 0, 64);
+    const uint64_t below = (1ull << lane) - 1;
+    if (v && !comp) list[bs + __popcll(ms & below)] = c * cg.nsb + sb;
+    if (v && comp) list[nsingle + bc + __popcll(mc & below)] = nsingle + (c - ns) * cg.nsb + sb;
+  }
 }
 
 // F5: get_satd of every 8x8 luma block of the group inside the frame
@@ -626,6 +802,9 @@ using namespace rv;
 struct RvSlot {  // one frame of the DPB: reconstruction + input pyramid
   rv_plane y, u, v, hres, qres;
   uint32_t *qres_box = nullptr;  // rv_plane_box_sums of qres (the SEA coarse search)
+  // the frame's motion field (frame_mvs: the encode's tile field when the
+  // frame was coded; zero for the key frame), 8x8 cells [h_in_b/2][w_in_b/2][R]
+  rv_mv *fmv = nullptr;
 };
 struct RvInput {
   rv_plane y, u, v;
@@ -808,12 +987,21 @@ struct rv_replay {
   MvStack *stk = nullptr;              // the stacks each superblock was evaluated with
   BlkDec *dec_lv[3] = {nullptr, nullptr, nullptr};  // decisions, per pyramid level
   uint8_t *mv_active = nullptr;        // re-evaluate this round
-  int32_t *mv_cnt = nullptr, *h_mv = nullptr;  // marked count (device, pinned host)
+  // the checks' counts: device ring (slot q % kCntRing for check q) and
+  // the host-mapped publication ring (seq << 32 | count, slot q % kPubRing)
+  static constexpr int kCntRing = 64, kPubRing = 64;
+  static constexpr int kRoundsAhead = 2;  // rounds queued beyond the last count read
+  int32_t *mv_cnt = nullptr, *mv_list = nullptr;
+  uint32_t *mv_ticket = nullptr;
+  unsigned long long *h_pub = nullptr, *d_pub = nullptr;
+  uint32_t mv_seq = 0;
   bool edge_tr = false;                // a stack reads a frame-edge leaf (top-right)
   // RAV1E_HIP_MV_HP=1: the rounds after the first on a high-priority stream
   hipStream_t hp = nullptr;
   hipEvent_t ev_hp0 = nullptr, ev_hp1 = nullptr;
-  long mv_round_sum = 0, mv_reeval = 0;  // rounds per frame and re-evaluations, summed
+  // evaluation rounds (round 0 included), re-evaluated superblocks and
+  // round runs (1 + the MV / intra passes) per frame, summed
+  long mv_round_sum = 0, mv_reeval = 0, mv_run_sum = 0;
   size_t nwords = 0, wpart = 0;   // result words; offset of the partition masks
   bool jobs_built = false;
   std::vector<RvSlot> slots;
@@ -822,7 +1010,11 @@ struct rv_replay {
   rv_fs_job *fs_jobs[3] = {nullptr, nullptr, nullptr};  // per level (scale 4, 2, 1)
   rv_fs_result *coarse, *half, *full, *sub;  // half: 4 quadrants per superblock
   rv_fs_result *look;                         // lookahead: 16 16x16 blocks per superblock
+  rv_fs_result *half_l = nullptr;             // the lookahead's 4 quadrants per superblock
   rv_ds_job *jobs_half[3], *jobs_full[3], *jobs_sub[3], *jobs_look[3];  // per level
+  rv_ds_job *jobs_half_l[3] = {nullptr, nullptr, nullptr};  // the lookahead's F2 (per level)
+  int32_t *la_list = nullptr;  // the lookahead rounds' marked jobs: F2 [R nsb 4], then FL [R nsb 16]
+  long la_round_sum = 0, la_reeval = 0;  // the lookahead rounds (round 0 included), re-evaluated jobs
   int32_t *src_half = nullptr, *src_full = nullptr, *src_look = nullptr;  // predictor sources
   uint64_t *l_out, *c_out;  // F4: [skip dist, non-skip dist, rate] per transform block
   RdoWinner *win;
@@ -903,7 +1095,8 @@ bool alloc_slot(rv_replay *r, RvSlot &s) {
   const size_t by = plane_bytes(s.y), bu = plane_bytes(s.u), bh = plane_bytes(s.hres),
                bq = plane_bytes(s.qres);
   const size_t bs8 = (size_t)s.qres.stride * s.qres.alloc_height * 8;
-  const size_t total = up(by) + 2 * up(bu) + up(bh) + up(bq) + up(bs8);
+  const size_t bf = (size_t)(g.w_in_b / 2) * (g.h_in_b / 2) * g.R * sizeof(rv_mv);
+  const size_t total = up(by) + 2 * up(bu) + up(bh) + up(bq) + up(bs8) + up(bf);
   uint8_t *m = (uint8_t *)dalloc(r, total);
   if (!m) return false;
   s.y.data = m;
@@ -917,6 +1110,8 @@ bool alloc_slot(rv_replay *r, RvSlot &s) {
   s.qres.data = m;
   m += up(bq);
   s.qres_box = (uint32_t *)m;
+  m += up(bs8);
+  s.fmv = (rv_mv *)m;
   return hipMemsetAsync(s.y.data, 0, total, r->stream) == hipSuccess;
 }
 
@@ -1061,8 +1256,9 @@ int build_static_jobs(rv_replay *r) {
             jl[(size_t)i * 16 + y * 4 + x] = j;
           }
       }
-    if ((e = upload(jh, r->jobs_half[lv])) || (e = upload(jf, r->jobs_full[lv])) ||
-        (e = upload(js, r->jobs_sub[lv])) || (e = upload(jl, r->jobs_look[lv])))
+    if ((e = upload(jh, r->jobs_half[lv])) || (e = upload(jh, r->jobs_half_l[lv])) ||
+        (e = upload(jf, r->jobs_full[lv])) || (e = upload(js, r->jobs_sub[lv])) ||
+        (e = upload(jl, r->jobs_look[lv])))
       return e;
     if (lv == 0 && ((e = upload(sh, r->src_half)) || (e = upload(sf, r->src_full)) ||
                     (e = upload(sl, r->src_look))))
@@ -1103,7 +1299,7 @@ int build_static_jobs(rv_replay *r) {
 // deblocking also its rows of the block map, planes 3 = log2 size, 4 =
 // skip), bytes into the group's slice of the exchange buffer.  Returns the
 // bytes; *n = the rectangles.
-int group_rects(const rv_replay *r, int k, XRect out[5], int *n) {
+int group_rects(const rv_replay *r, int k, XRect out[6], int *n) {
   const Geo &g = r->g;
   const int32_t *gr = r->grects + 4 * k;
   const int px = g.hbd ? 2 : 1;
@@ -1130,6 +1326,16 @@ int group_rects(const rv_replay *r, int k, XRect out[5], int *n) {
       off += (int64_t)(x1 - x0) * (y1 - y0);
     }
     *n = 5;
+  }
+  if (r->exact) {  // the group's 8x8 cells of the frame's motion field (bytes)
+    const int w8 = g.w_in_b / 2, h8 = g.h_in_b / 2, cb = g.R * (int)sizeof(rv_mv);
+    const int x0 = gr[0] * 8, y0 = gr[1] * 8;
+    int x1 = (gr[0] + gr[2]) * 8, y1 = (gr[1] + gr[3]) * 8;
+    x1 = x1 < w8 ? x1 : w8;
+    y1 = y1 < h8 ? y1 : h8;
+    out[*n] = XRect{off, 5, x0 * cb, y0, (x1 - x0) * cb, y1 - y0};
+    off += (int64_t)(x1 - x0) * cb * (y1 - y0);
+    (*n)++;
   }
   return (int)off;
 }
@@ -1158,7 +1364,7 @@ static void xcopy_launch(hipStream_t st, const rv_plane *pl, const XRect *rects,
 // Copy rectangles between the slot's planes / the block map and a packed
 // buffer (pixel rectangles at the pixel width, map rectangles bytewise).
 int xcopy(rv_replay *r, const RvSlot &s, const XRect *rects, int n, int to_plane, uint8_t *buf) {
-  XRect px[3 * kMaxGroups], mp[2 * kMaxGroups];
+  XRect px[3 * kMaxGroups], mp[3 * kMaxGroups];
   int npx = 0, nmp = 0;
   for (int i = 0; i < n; i++) {
     if (rects[i].plane < 3) {
@@ -1183,6 +1389,12 @@ int xcopy(rv_replay *r, const RvSlot &s, const XRect *rects, int n, int to_plane
       m[i].width = r->mi_cols;
       m[i].height = r->mi_rows;
     }
+    // plane 5: the slot's motion field as bytes ([h8][w8][R] rv_mv)
+    const int fb = r->g.w_in_b / 2 * r->g.R * (int)sizeof(rv_mv);
+    m[2].data = s.fmv;
+    m[2].stride = fb;
+    m[2].width = fb;
+    m[2].height = r->g.h_in_b / 2;
     xcopy_launch<uint8_t>(r->stream, m, mp, nmp, to_plane, buf);
   }
   RV_HIP_CHECK_LAUNCH();
@@ -1435,7 +1647,7 @@ void rv_replay_destroy(rv_replay *r) {
     if (es) (void)hipStreamSynchronize(es);
   for (void *p : r->allocs) (void)hipFree(p);
   if (r->h_cnt) (void)hipHostFree(r->h_cnt);
-  if (r->h_mv) (void)hipHostFree(r->h_mv);
+  if (r->h_pub) (void)hipHostFree(r->h_pub);
   for (int f = 0; f < rv_replay::kRing; f++)
     for (int i = 0; i < rv_replay::kEv; i++)
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
@@ -1536,6 +1748,10 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
   r->coarse = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
   r->half = (rv_fs_result *)dalloc(r, nr * 4 * sizeof(rv_fs_result));
   r->look = (rv_fs_result *)dalloc(r, nr * 16 * sizeof(rv_fs_result));
+  r->half_l = (rv_fs_result *)dalloc(r, nr * 4 * sizeof(rv_fs_result));
+  r->la_list = (int32_t *)dalloc(r, (size_t)nr * 20 * 4);
+  if (r->half_l) (void)hipMemsetAsync(r->half_l, 0, nr * 4 * sizeof(rv_fs_result), r->stream);
+  if (r->look) (void)hipMemsetAsync(r->look, 0, nr * 16 * sizeof(rv_fs_result), r->stream);
   r->full = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
   r->sub = (rv_fs_result *)dalloc(r, nr * sizeof(rv_fs_result));
   r->l_out = (uint64_t *)dalloc(r, (size_t)nc * 3 * 8);
@@ -1680,6 +1896,18 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     if (r->i_was) (void)hipMemsetAsync(r->i_was, 0, n, r->stream);
     if (r->i_win) (void)hipMemsetAsync(r->i_win, 0, 2 * n, r->stream);
   }
+  // the rounds' counts (the lookahead's EPZS rounds at every speed, the MV-
+  // stack rounds at speed 10): a device ring of count pairs + the ticket, the
+  // host-mapped publication ring
+  r->mv_cnt = (int32_t *)dalloc(r, rv_replay::kCntRing * 8 + 4);
+  r->mv_ticket = r->mv_cnt ? (uint32_t *)(r->mv_cnt + 2 * rv_replay::kCntRing) : nullptr;
+  if (r->mv_cnt) (void)hipMemsetAsync(r->mv_cnt, 0, rv_replay::kCntRing * 8 + 4, r->stream);
+  ok = ok && r->mv_cnt &&
+       hipHostMalloc((void **)&r->h_pub, rv_replay::kPubRing * 8,
+                     hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+       hipHostGetDevicePointer((void **)&r->d_pub, r->h_pub, 0) == hipSuccess;
+  if (r->h_pub)
+    for (int i = 0; i < rv_replay::kPubRing; i++) r->h_pub[i] = ~0ull;
   // speed 10: rav1e's MV stacks in coding-order rounds
   r->exact = !r->s6 && !(cfg->flags & RV_REPLAY_MVREF_STANDIN);
   if (r->exact) {
@@ -1691,10 +1919,8 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
       ok = ok && r->dec_lv[l];
     }
     r->mv_active = (uint8_t *)dalloc(r, n);
-    const size_t nr = (size_t)2 * g.tws * g.ths + 24;  // per-round counts (rv_replay_frame)
-    r->mv_cnt = (int32_t *)dalloc(r, nr * 4);
-    ok = ok && r->stk && r->mv_active && r->mv_cnt &&
-         hipHostMalloc((void **)&r->h_mv, nr * 4, hipHostMallocDefault) == hipSuccess;
+    r->mv_list = (int32_t *)dalloc(r, n * 4);
+    ok = ok && r->stk && r->mv_active && r->mv_list;
     // RAV1E_HIP_MV_HP=1: the rounds after the first on a high-priority
     // stream (2160p A/B: 140 vs 177 fps -- the other instance's work loses
     // more than the rounds gain; off)
@@ -1793,7 +2019,8 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
   r->imp_by = g.vis_h / 8;
   r->n_imp = r->imp_bx * r->imp_by;
   r->tail = (unsigned long long *)dalloc(r, 5 * 8);
-  ok = ok && r->coarse && r->half && r->look && r->full && r->sub && r->l_out && r->c_out && r->win &&
+  ok = ok && r->coarse && r->half && r->look && r->half_l && r->la_list && r->full && r->sub &&
+       r->l_out && r->c_out && r->win &&
        r->cand_list && r->cand_count && r->cand_evals &&
        r->l_lev && r->c_lev && r->words && r->tail;
   if (ok) {
@@ -1810,10 +2037,6 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     const char *e = getenv("RAV1E_HIP_REPLAY_SERIAL");
     r->overlap = !(e && e[0] == '1');
   }
-  if (r->overlap)
-    ok = ok && hipStreamCreateWithFlags(&r->side, hipStreamNonBlocking) == hipSuccess &&
-         hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&r->ev_join, hipEventDisableTiming) == hipSuccess;
   if (r->overlap && r->lvl && !r->s6) {
     ok = ok && hipEventCreateWithFlags(&r->ev_efork, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&r->ev_l1me, hipEventDisableTiming) == hipSuccess &&
@@ -2016,7 +2239,7 @@ int rv_replay_set_groups(rv_replay *r, int n_groups, const int32_t *rects, int m
   r->my_group = my_group;
   size_t most = 0;
   for (int k = 0; k < n_groups; k++) {
-    XRect xr[5];
+    XRect xr[6];
     int nx;
     const size_t b = (size_t)group_rects(r, k, xr, &nx);
     most = b > most ? b : most;
@@ -2049,11 +2272,11 @@ int rv_replay_import(rv_replay *r) {
   // its own input): nothing to move
   if ((r->n_groups < 2 && !r->comm) || r->last.is_key) return RV_OK;
   const RvSlot &s = r->slots[r->last.display % kSlots];
-  XRect rects[5 * kMaxGroups];
+  XRect rects[6 * kMaxGroups];
   int n = 0;
   for (int k = 0; k < r->n_groups; k++) {
     if (k == r->my_group) continue;
-    XRect xr[5];
+    XRect xr[6];
     int nx;
     group_rects(r, k, xr, &nx);
     for (int p = 0; p < nx; p++) {
@@ -2090,6 +2313,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     RV_H(hipMemcpyAsync(s.v.data, in.v.data, plane_bytes(in.v), hipMemcpyDeviceToDevice, st));
     RV_R(rv_plane_pyramid(&in.y, &s.hres, &s.qres, st));
     if (r->sea) RV_R(rv_plane_box_sums(&s.qres, s.qres_box, st));
+    // an intra frame saves no motion: its frame_mvs stay zero
+    RV_H(hipMemsetAsync(s.fmv, 0, (size_t)(g.w_in_b / 2) * (g.h_in_b / 2) * g.R * sizeof(rv_mv), st));
     r->coded++;
     r->last = fi;
     if (info) *info = fi;
@@ -2107,8 +2332,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   const RvInput &cur = r->inputs[fi.display % r->inputs.size()];
   const RvSlot &S = r->slots[fi.display % kSlots];
   const RvSlot *ref[2];
-  rv_plane refs_y[RV_DS_MAX_PRED], refs_h[RV_DS_MAX_PRED], refs_q[RV_DS_MAX_PRED];
-  const uint32_t *box[RV_DS_MAX_PRED];
+  rv_plane refs_y[RV_MAX_REFS], refs_h[RV_MAX_REFS], refs_q[RV_MAX_REFS];
+  const uint32_t *box[RV_MAX_REFS];
   for (int k = 0; k < g.R; k++) {
     ref[k] = &r->slots[fi.ref_display[k] % kSlots];
     refs_y[k] = ref[k]->y;
@@ -2123,7 +2348,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   uint32_t *ev_sub = ev_full + (size_t)nr * g.R;
   ChainNext to_sub{kChainFullToSub, r->jobs_sub[lv]};
   // the lookahead searches the references' original frames
-  rv_plane refs_o[RV_DS_MAX_PRED];
+  rv_plane refs_o[RV_MAX_REFS];
   for (int k = 0; k < g.R; k++) refs_o[k] = r->inputs[fi.ref_display[k] % r->inputs.size()].y;
 
   const bool tm = r->timing_stride > 0 && (ncoded / r->timing_block) % r->timing_stride == 0;
@@ -2143,22 +2368,119 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   RV_R(rv_full_search_multi(&S.qres, refs_q, g.R, r->fs_jobs[lv], nr, 16, 16, 1, 0, r->coarse,
                             nullptr, r->sea ? box : nullptr, st));
   RV_EV(2);
-  // F2 build_half_res_pmvs: the four 32x32 quadrants of every superblock at
-  // half resolution, predictors from the coarse MVs; the 64x64 full-pel
-  // predictors (pmvs[0]) too
+  // The host side of a round loop (the lookahead's EPZS rounds and the MV-
+  // stack rounds): check(q) queues check q, which lists the jobs to re-run
+  // and publishes their count into the host-mapped ring; eval(q) queues the
+  // round that re-runs check q's list.  The host keeps kRoundsAhead rounds
+  // queued beyond the last count it has read (it spins on the published
+  // counts, no stream synchronisation), so the GPU never waits on the host;
+  // the loop ends at the first check that lists nothing (the rounds queued
+  // after it find empty lists).  budget: the chain's depth bound (see the
+  // callers); a check still listing jobs after it is an internal error.
+  static const bool mv_trace = getenv("RAV1E_HIP_MV_TRACE") != nullptr;
+  auto rounds = [&](hipStream_t xs, int budget, auto &&check, auto &&eval, long *nrounds,
+                    long *nre, bool *changed, const char *what) -> int {
+    if (changed) *changed = false;
+    const uint32_t first = r->mv_seq++;
+    RV_R(check(first));
+    int queued = 0;  // evaluation rounds queued (round j evaluates check j - 1's list)
+    for (int seen = 0;; seen++) {
+      while (queued < budget && queued < seen + rv_replay::kRoundsAhead) {
+        RV_R(eval(first + (uint32_t)queued));
+        RV_R(check(r->mv_seq++));
+        queued++;
+      }
+      const uint32_t q = first + (uint32_t)seen;
+      volatile unsigned long long *pub = r->h_pub + q % rv_replay::kPubRing;
+      const auto t0 = std::chrono::steady_clock::now();
+      unsigned long long v;
+      for (long spin = 0;; spin++) {
+        v = *pub;
+        if ((uint32_t)(v >> 32) == q) break;
+        if ((spin & 1023) == 1023) {
+          const hipError_t he = hipStreamQuery(xs);
+          if (he != hipSuccess && he != hipErrorNotReady)
+            return rv_set_error(RV_EHIP, "rv_replay_frame: a round failed");
+          if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
+            return rv_set_error(RV_EHIP, "rv_replay_frame: a round's count never arrived");
+          std::this_thread::yield();
+        }
+      }
+      const int c = (int)(uint32_t)v;
+      if (mv_trace)
+        fprintf(stderr, "%s frame %ld level %d check %d: %d\n", what, ncoded, lv, seen, c);
+      if (c == 0) return RV_OK;
+      if (seen >= budget)
+        return rv_set_error(RV_EHIP, "rv_replay_frame: rounds beyond the chain's dependency "
+                                     "depth (internal error)");
+      *nre += c;
+      (*nrounds)++;
+      if (changed) *changed = true;
+    }
+  };
+  auto slot_cnt = [&](uint32_t q) { return r->mv_cnt + 2 * (q % rv_replay::kCntRing); };
+  const EpzsGeo eg{g.tx0, g.ty0, g.tw, g.th, g.tws, g.ths, g.W, g.H, g.w_in_b, g.h_in_b};
+
+  // F2L + FL: the lookahead's build_half_res_pmvs and build_full_res_pmvs
+  // (compute_lookahead_motion_vectors, src/api/internal.rs:514-622) with
+  // their EPZS sets (la_check_kernel): round 0 stores every F2L set (the
+  // field guessed from the previous frame's results) and runs every F2L
+  // search, then the same for FL; then the rounds.  Budget: a quadrant
+  // search reads the quadrants of the superblocks left of and above it, so
+  // it settles by round tws + ths - 1; a 16x16 search reads its coarse /
+  // quadrant predictors (settled by then) and the 16x16 blocks left of and
+  // above it, so it settles 4 tws + 4 ths - 2 rounds later.
   {
-    const int nh = nr * g.R * 4, nf = nr * g.R;
-    fill_preds_kernel<<<(nh + 255) / 256, 256, 0, st>>>(r->jobs_half[lv], r->src_half, nh,
-                                                        r->coarse, r->half, 1);
-    fill_preds_kernel<<<(nf + 255) / 256, 256, 0, st>>>(r->jobs_full[lv], r->src_full, nf,
-                                                        r->coarse, r->half, 0);
+    LaArgs la_a;
+    memset(&la_a, 0, sizeof(la_a));
+    la_a.g = g;
+    la_a.eg = eg;
+    la_a.jh = r->jobs_half_l[lv];
+    la_a.jl = r->jobs_look[lv];
+    la_a.sl = r->src_look;
+    la_a.coarse = r->coarse;
+    la_a.half_l = r->half_l;
+    la_a.look = r->look;
+    const int nh = nr * g.R * 4, nl = nr * g.R * 16;
+    la_a.list_h = r->la_list;
+    la_a.list_l = r->la_list + nh;
+    auto la_launch = [&](int what, uint32_t q, bool init) -> int {
+      la_a.what = what;
+      la_a.init = init ? 1 : 0;
+      la_a.pub = RoundPub{slot_cnt(q), slot_cnt(q + 1), r->mv_ticket, init ? nullptr : r->d_pub, q};
+      const int n = ((what & 1) ? nh : 0) + ((what & 2) ? nl : 0);
+      la_check_kernel<<<(n + 255) / 256, 256, 0, st>>>(la_a);
+      RV_H(hipGetLastError());
+      return RV_OK;
+    };
+    auto f2l = [&](const int32_t *list, const int32_t *cnt) {
+      return rv_diamond_search_multi(&S.hres, refs_h, g.R, r->jobs_half_l[lv], nr * 4, 16, 16, 0,
+                                     0, 0, g.bd, r->half_l, nullptr, nullptr, st, nullptr, list,
+                                     cnt, 0);
+    };
+    auto fl = [&](const int32_t *list, const int32_t *cnt) {
+      return rv_diamond_search_multi(&cur.y, refs_o, g.R, r->jobs_look[lv], nr * 16, 16, 16, 0, 0,
+                                     0, g.bd, r->look, nullptr, nullptr, st, nullptr, list, cnt, 0);
+    };
+    RV_R(la_launch(1, 0, true));
+    RV_R(f2l(nullptr, nullptr));
+    RV_EV(3);
+    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv], st));
+    RV_R(la_launch(2, 0, true));
+    RV_R(fl(nullptr, nullptr));
+    r->la_round_sum++;
+    RV_R(rounds(
+        st, 5 * (g.tws + g.ths),
+        [&](uint32_t q) { return la_launch(3, q, false); },
+        [&](uint32_t q) -> int {
+          RV_R(f2l(r->la_list, slot_cnt(q)));
+          return fl(r->la_list + nh, slot_cnt(q) + 1);
+        },
+        &r->la_round_sum, &r->la_reeval, nullptr, "lookahead"));
+    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 1], st));
   }
-  RV_R(rv_diamond_search_multi(&S.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
-                               g.bd, r->half, nullptr, nullptr, st));
-  RV_EV(3);
   // F5: the 8x8 importance SATD against reference 0's original frame at the
-  // lookahead MVs (only FL's output: on the side stream after FL when it
-  // overlaps, zeroing its own sum)
+  // lookahead MVs (FL's output; after the frame's decisions)
   auto f5_importance = [&](hipStream_t fs) -> int {
     const unsigned nb = (unsigned)((r->n_imp + 255) / 256);
     if (g.hbd)
@@ -2169,44 +2491,19 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                                      r->imp_by, r->tail + 2);
     return RV_OK;
   };
-  // FL the lookahead's build_full_res_pmvs (compute_lookahead_motion_vectors,
-  // src/api/internal.rs:514-622): 16x16 full-pel searches against the
-  // references' original frames; its coarse and half-res stages are F1 / F2
-  // (the same inputs).  F5 reads its MVs.
-  {
-    hipStream_t ls = st;
-    if (r->overlap) {
-      RV_H(hipEventRecord(r->ev_fork, st));
-      RV_H(hipStreamWaitEvent(r->side, r->ev_fork, 0));
-      ls = r->side;
-    }
-    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv], ls));
-    const int nl = nr * g.R * 16;
-    fill_preds_kernel<<<(nl + 255) / 256, 256, 0, ls>>>(r->jobs_look[lv], r->src_look, nl,
-                                                        r->coarse, r->half, 0);
-    RV_R(rv_diamond_search_multi(&cur.y, refs_o, g.R, r->jobs_look[lv], nr * 16, 16, 16, 0, 0,
-                                 0, g.bd, r->look, nullptr, nullptr, ls));
-    if (r->overlap) {
-      RV_H(hipMemsetAsync(r->tail + 2, 0, 8, ls));
-      RV_R(f5_importance(ls));
-    }
-    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 1], ls));
-    if (r->overlap) RV_H(hipEventRecord(r->ev_join, ls));
-  }
   RV_EV(4);
-  // An error return from here on must not leave the lookahead (side stream)
-  // or the frame-edge levels (edge stream) running: the next frame's F1 / F2
-  // rewrite the MVs they read, and rv_replay_destroy frees them.  Disarmed
-  // once the main stream has joined them.
+  // An error return from here on must not leave the frame-edge levels (edge
+  // streams) running: the next frame rewrites the MVs they read, and
+  // rv_replay_destroy frees them.  Disarmed once the main stream has joined
+  // them.
   struct SideJoin {
     rv_replay *r;
     bool armed;
     ~SideJoin() {
-      if (armed && r->side) (void)hipStreamSynchronize(r->side);
       for (int l = 1; l < kLevels; l++)
         if (armed && r->edge[l]) (void)hipStreamSynchronize(r->edge[l]);
     }
-  } side_join{r, r->overlap || r->edge[1]};
+  } side_join{r, r->edge[1] != nullptr};
   // the candidates' RDO arguments: luma (N = 64, cdef distortion) and both
   // chroma planes (N = 32, SSE) of every candidate
   const int nsingle = g.nsb * g.R * g.M;
@@ -2274,7 +2571,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       rv_replay::PLevel &P = r->pl[l];
       if (l == 1)
         seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, es>>>(
-            P.jobs_full[lv], P.n, P.gw, g.R, r->half, g.nsb, 0, 0, r->ex0, r->ey0, g.tw);
+            P.jobs_full[lv], P.n, P.gw, g.R, r->half_l, g.nsb, 0, 0, r->ex0, r->ey0, g.tw);
       else
         seed_level_kernel<<<(P.n * g.R + 255) / 256, 256, 0, es>>>(
             P.jobs_full[lv], P.n, P.gw, g.R, r->pl[1].sub, r->pl[1].n, r->pl[1].gw, 1 << (l - 1),
@@ -2478,9 +2775,35 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     if (edge && r->edge_tr)  // the leaves the stacks read
       for (int l = 1; l < kLevels; l++)
         if (r->lv_used[l]) RV_H(hipStreamWaitEvent(st, r->ev_ejoin[l], 0));
-    ma.count = r->mv_cnt;  // slot 0: the first round marks every superblock
-    RV_H(hipMemsetAsync(r->mv_cnt, 0, sizeof(int32_t), st));
+    ma.list = r->mv_list;
+    // EPZS: the F2 / F3 sets from the coding-order field; the first check
+    // guesses it from the previous decisions of this level and the
+    // lookahead's quadrants, and never reads the frame-edge leaves (they may
+    // be in flight)
+    ma.epzs = 1;
+    ma.eg = eg;
+    ma.jh = r->jobs_half[lv];
+    ma.coarse = r->coarse;
+    ma.hq = r->half_l;
+    ma.prev = r->slots[fi.ref_display[0] % kSlots].fmv;  // the LAST reference's frame_mvs
+    ma.edge_ok = 0;
+    // the first check marks every superblock (its count is not read)
+    const uint32_t q = r->mv_seq++;
+    ma.count = slot_cnt(q);
+    ma.pub = RoundPub{slot_cnt(q), slot_cnt(q + 1), r->mv_ticket, r->d_pub, q};
     RV_R(rv_mvref_round(ma, st));
+  }
+  // F2: build_half_res_pmvs of the encode (speed 10: the sets the check
+  // stored; otherwise the lookahead's quadrants stand in) and the F3
+  // full-pel predictors (otherwise zero + the coarse MV)
+  if (r->exact) {
+    RV_R(rv_diamond_search_multi(&S.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
+                                 g.bd, r->half, nullptr, nullptr, st));
+  } else {
+    RV_H(hipMemcpyAsync(r->half, r->half_l, (size_t)nr * g.R * 4 * sizeof(rv_fs_result),
+                        hipMemcpyDeviceToDevice, st));
+    fill_preds_kernel<<<(nr * g.R + 255) / 256, 256, 0, st>>>(r->jobs_full[lv], r->src_full,
+                                                              nr * g.R, r->coarse, r->half, 0);
   }
   const uint8_t *act = r->exact ? r->mv_active : nullptr;
   // F4's arguments (la / ca become F6's commit arguments below; the rounds
@@ -2488,31 +2811,27 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   const RdoArgs la4 = la, ca4 = ca;
   // F3 full-res full-pel diamond -> sub-pel predictor; sub-pel diamond
   // (speed 10: SAD, no hp) -> NEWMV of every superblock and reference;
-  // the candidates; F4; the argmin (round `round` of the stacks)
-  auto f3_f4 = [&](int round) -> int {
-    // rounds after the first: the high-priority stream (their few
-    // superblocks' kernels get the next free CUs ahead of the other
-    // instance's bulk launches)
-    hipStream_t xs = round ? (r->hp ? r->hp : st) : st;
+  // the candidates; F4; the argmin.  Round 0: every superblock, full grids.
+  auto f3_f4 = [&]() -> int {
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
-                                 r->full, ev_full, &to_sub, xs, act));
-    if (!round) RV_EV(5);
+                                 r->full, ev_full, &to_sub, st, act));
+    RV_EV(5);
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1,
-                                 r->s6 ? 1 : 0, 0, g.bd, r->sub, ev_sub, nullptr, xs, act));
+                                 r->s6 ? 1 : 0, 0, g.bd, r->sub, ev_sub, nullptr, st, act));
     if (r->lvl && !edge && !lv_early) RV_R(lv_me(st));
     // the valid candidates (a few microseconds; bracketed with F3 sub-pel;
     // the count was zeroed by the previous argmin or at creation)
-    cand_list_kernel<<<(nsingle + 255) / 256, 256, 0, xs>>>(cg, r->sub, nsingle, r->cand_list,
+    cand_list_kernel<<<(nsingle + 255) / 256, 256, 0, st>>>(cg, r->sub, nsingle, r->cand_list,
                                                             r->cand_count, act);
     if (r->lvl && !edge && !lv_early) lv_lists(st, false);
     if (cg.comp) {  // the compound lists (after the single ones in the same arrays)
-      comp_list_kernel<<<(g.nsb * cg.comp + 255) / 256, 256, 0, xs>>>(
+      comp_list_kernel<<<(g.nsb * cg.comp + 255) / 256, 256, 0, st>>>(
           cg, r->sub, nsingle, r->cand_list + nsingle, r->cand_count + 1, act);
       if (r->lvl && !edge && !lv_early) lv_lists(st, true);
     }
-    if (!round) RV_EV(6);
+    RV_EV(6);
     // F4 every valid candidate, luma + both chroma planes in one fused launch
-    RV_R(rv_rdo_candidates(la4, ca4, g.hbd, xs));
+    RV_R(rv_rdo_candidates(la4, ca4, g.hbd, st));
     if (r->lvl && !edge && !lv_early) RV_R(lv_rdo(st));
     if (cg.comp) {  // the compound candidates (all pushed), distinct MV pairs from the list
       RdoArgs lc = la4, cc = ca4;
@@ -2521,55 +2840,69 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       lc.cand_base = cc.cand_base = 0;
       lc.n_tx = g.nsb * cg.comp;
       cc.n_tx = g.nsb * cg.comp * ntx_c;
-      if (!round) RV_EV(7);
-      RV_R(rv_rdo_candidates(lc, cc, g.hbd, xs, true));
+      RV_EV(7);
+      RV_R(rv_rdo_candidates(lc, cc, g.hbd, st, true));
       if (r->lvl && !edge && !lv_early) RV_R(lv_rdo_comp(st));
-    } else if (!round) {
+    } else {
       RV_EV(7);
     }
-    if (!round) {
-      RV_EV(8);
-      if (r->overlap) RV_H(hipStreamWaitEvent(st, r->ev_join, 0));  // the lookahead's MVs
-    }
-    score_candidates<<<(g.nsb + 63) / 64, 64, 0, xs>>>(
+    RV_EV(8);
+    score_wave_kernel<<<(g.nsb + 3) / 4, 256, 0, st>>>(
         g, cg, L.lambda, L.ds[1], L.ds[2], r->sub, r->l_out, r->c_out, r->c_out + nct * 3, ntx_c,
-        r->win, r->coarse, r->half, r->full, r->look, r->words, r->cand_count,
-        r->overlap ? nullptr : r->tail + 2, r->cand_evals + 2 * slot * kLevels, r->leaf_count, act,
-        r->exact ? r->dec_lv[lv] : nullptr, round);
+        r->win, r->coarse, r->half, r->full, r->look, r->half_l, r->words, r->cand_count,
+        r->tail + 2, r->cand_evals + 2 * slot * kLevels, r->leaf_count, nullptr, nullptr,
+        r->exact ? r->dec_lv[lv] : nullptr, 0);
     return RV_OK;
   };
-  RV_R(f3_f4(0));
-  int mv_rounds = 1;
-  // The rounds after the first: a check (the stacks from the decisions so
-  // far, counts[i] = the superblocks marked before evaluation round i), then
-  // the evaluation of the marked ones -- a no-op once a check marks none.
-  // They are queued in batches of 1, 2, 4, 8 between host reads of the
-  // counts, so a long dependency chain costs few host round trips; bounded
-  // by the tiles' dependency depth (every round settles the next superblock
-  // of each raster chain).  Returns with *changed = some round evaluated.
-  // (the intra pass's re-runs add rounds of their own: twice the bound)
-  const int max_rounds = 2 * g.tws * g.ths + 8;
-  static const bool mv_trace = getenv("RAV1E_HIP_MV_TRACE") != nullptr;
-  // RAV1E_HIP_MV_SCAN=1: the predictive per-tile scan in the tail rounds
-  // (fewer rounds -- 2160p: 5.1 vs 12.9 per frame -- but each scan walks
-  // the tile's anti-diagonals one after another: 147 vs 176 fps, off)
-  static const bool scan_on = [] {
-    const char *e = getenv("RAV1E_HIP_MV_SCAN");
-    return e && e[0] == '1';
-  }();
+  // A later round: the same stages over the superblocks check q listed
+  // (r->mv_list, its count in the ring), each launch a fixed pool of
+  // workgroups that loops over the device count -- a round of a few dozen
+  // superblocks costs their latency, not a full grid of early exits.
+  auto f3_f4_list = [&](hipStream_t xs, uint32_t q) -> int {
+    const int32_t *acnt = slot_cnt(q);
+    // F2 of the listed superblocks (their 4 quadrants per reference)
+    RV_R(rv_diamond_search_multi(&S.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
+                                 g.bd, r->half, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 4));
+    RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
+                                 r->full, nullptr, &to_sub, xs, nullptr, r->mv_list, acnt));
+    RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
+                                 r->sub, nullptr, nullptr, xs, nullptr, r->mv_list, acnt));
+    round_lists_kernel<<<kRoundGrid, 256, 0, xs>>>(cg, r->sub, nsingle, r->cand_list,
+                                                   r->cand_count, r->mv_list, acnt);
+    RdoArgs lc = la4, cc = ca4;
+    lc.list = cc.list = r->cand_list + nsingle;
+    lc.count = cc.count = r->cand_count + 1;
+    lc.cand_base = cc.cand_base = 0;
+    RV_R(rv_rdo_round(la4, ca4, cg.comp ? &lc : nullptr, cg.comp ? &cc : nullptr, g.hbd, xs,
+                      kRoundGrid));
+    score_wave_kernel<<<kRoundGrid, 256, 0, xs>>>(
+        g, cg, L.lambda, L.ds[1], L.ds[2], r->sub, r->l_out, r->c_out, r->c_out + nct * 3, ntx_c,
+        r->win, r->coarse, r->half, r->full, r->look, r->half_l, r->words, r->cand_count, nullptr,
+        nullptr, nullptr, r->mv_list, acnt, r->dec_lv[lv], 1);
+    return RV_OK;
+  };
+  RV_R(f3_f4());
+  // The MV-stack rounds after the first (`rounds` above): a check
+  // recomputes every superblock's stacks and F2 / F3 EPZS sets from the
+  // decisions and results so far and lists the superblocks where one
+  // changed; the round re-runs their F2, F3, candidates, F4 and argmin.
+  //
+  // Termination: within a tile a superblock's stacks read its
+  // left, top-left, top and top-right neighbours, and its EPZS sets read
+  // fields of its left and top neighbours, so its dependency depth is at
+  // most x + 2 y <= (tws - 1) + 2 (ths - 1).  A superblock of depth d is
+  // settled (evaluated with its final inputs) after evaluation round d + 1:
+  // its predecessors are settled after round d, so check d + 1 gives its
+  // final inputs.  Hence every run ends by evaluation round tws + 2 ths - 2
+  // and the check after it lists nothing; that is the budget, per run.
+  //
+  // Returns with *changed = some round evaluated.
+  const int budget = g.tws + 2 * g.ths - 2;
+  int mv_runs = 0;
   auto mv_rounds_run = [&](const uint8_t *iwas, bool *changed) -> int {
-    if (changed) *changed = false;
-    // the tail (the last check marked few superblocks): the predictive scan
-    bool tail = false;
+    mv_runs++;
     hipStream_t xs = r->hp ? r->hp : st;
-    auto check = [&](int slot) -> int {
-      ma.init = 0;
-      ma.iwas = iwas;
-      ma.count = r->mv_cnt + slot;
-      return rv_mvref_round(ma, xs, tail);
-    };
-    // the rounds follow the main stream's work and it waits for them (their
-    // host reads synchronise xs only)
+    // the rounds follow the main stream's work and it waits for them
     struct Join {
       rv_replay *r;
       hipStream_t st;
@@ -2582,44 +2915,28 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       RV_H(hipEventRecord(r->ev_hp0, st));
       RV_H(hipStreamWaitEvent(r->hp, r->ev_hp0, 0));
     }
-    // a check alone first (most frames end there), then batches of
-    // (evaluation round, check) x k; counts[slot] = the superblocks the
-    // check marked for evaluation round `slot`
-    RV_H(hipMemsetAsync(r->mv_cnt + mv_rounds, 0, sizeof(int32_t), xs));
-    RV_R(check(mv_rounds));
-    for (int k = 0;; k = k ? (k < 8 ? 2 * k : 8) : 1) {
-      const int first = mv_rounds;  // the check of slot `first` is queued
-      if (k) {
-        if (first + k > max_rounds) k = max_rounds - first;
-        if (k <= 0)
-          return rv_set_error(RV_EHIP, "rv_replay_frame: the MV-stack rounds did not converge");
-        RV_H(hipMemsetAsync(r->mv_cnt + first + 1, 0, (size_t)k * sizeof(int32_t), xs));
-        for (int j = 0; j < k; j++) {
-          RV_R(f3_f4(first + j));  // a no-op once a check marked nothing
-          RV_R(check(first + j + 1));
-        }
-      }
-      RV_H(hipMemcpyAsync(r->h_mv, r->mv_cnt + first, (size_t)(k + 1) * sizeof(int32_t),
-                          hipMemcpyDeviceToHost, xs));
-      RV_H(hipStreamSynchronize(xs));
-      for (int j = 0; j <= k; j++) {
-        if (mv_trace)
-          fprintf(stderr, "mvref frame %ld level %d round %d: %d\n", ncoded, lv, first + j,
-                  r->h_mv[j]);
-        if (r->h_mv[j] == 0) {  // converged: the rounds queued after it did nothing
-          mv_rounds = first + j;
-          return RV_OK;
-        }
-        if (j < k) {  // round first + j evaluated them
-          r->mv_reeval += r->h_mv[j];
-          if (changed) *changed = true;
-        }
-        tail = scan_on && r->h_mv[j] * 16 < g.nsb;
-      }
-      mv_rounds = first + k;  // the check of slot first + k is not yet acted on
-    }
+    return rounds(
+        xs, budget,
+        [&](uint32_t q) {
+          ma.init = 0;
+          ma.iwas = iwas;
+          ma.count = slot_cnt(q);
+          ma.pub = RoundPub{slot_cnt(q), slot_cnt(q + 1), r->mv_ticket, r->d_pub, q};
+          return rv_mvref_round(ma, xs);
+        },
+        [&](uint32_t q) { return f3_f4_list(xs, q); }, &r->mv_round_sum, &r->mv_reeval, changed,
+        "mvref");
   };
-  if (r->exact) RV_R(mv_rounds_run(nullptr, nullptr));
+  if (r->exact) {
+    // from here on the checks read the frame-edge leaves (the EPZS field of
+    // the edge superblocks) and the encode's own F2 results
+    if (edge)
+      for (int l = 1; l < kLevels; l++)
+        if (r->lv_used[l]) RV_H(hipStreamWaitEvent(st, r->ev_ejoin[l], 0));
+    ma.hq = r->half;
+    ma.edge_ok = 1;
+    RV_R(mv_rounds_run(nullptr, nullptr));
+  }
   if (r->lvl) {
     if (edge) {  // the levels' winners
       for (int l = 1; l < kLevels; l++)
@@ -2682,7 +2999,14 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // blocks): the superblocks whose stacks it changes are re-decided, the
   // frame re-committed and the intra pass re-run, until the stacks hold
   // (the joint fixed point of the tile's coding order)
-  while (r->exact && r->intra) {
+  // Bound: each pass settles at least the next superblock of every tile's
+  // raster order (its predecessors' decisions, intra flags and
+  // reconstruction are final, so its stacks, inter winner and intra
+  // decision are too), so tws * ths passes always suffice.
+  for (int pass = 0; r->exact && r->intra; pass++) {
+    if (pass > g.tws * g.ths)
+      return rv_set_error(RV_EHIP, "rv_replay_frame: the MV / intra passes did not settle "
+                                   "(internal error)");
     bool changed = false;
     RV_R(mv_rounds_run(r->i_was, &changed));
     if (!changed) break;
@@ -2690,11 +3014,18 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     RV_R(intra_begin(r));
     RV_R(intra_pass(r, la, ca, cur, S, L, slot));
   }
-  if (r->exact) r->mv_round_sum += mv_rounds;
+  if (r->exact) {
+    r->mv_round_sum++;  // round 0
+    r->mv_run_sum += mv_runs;
+    // the encode's field becomes the frame's frame_mvs (the group's part;
+    // the other groups' arrive with the exchange)
+    ma.iwas = r->intra ? r->i_was : nullptr;
+    RV_R(rv_mvref_field(ma, S.fmv, st));
+  }
   RV_EV(11);
   // F5 importance SATD against reference 0 (the sum was zeroed by the argmin;
   // with the side stream F5 ran there, after the lookahead)
-  if (!r->overlap) RV_R(f5_importance(st));
+  RV_R(f5_importance(st));
   RV_EV(12);
   // F7 deblock_filter_frame (src/encoder.rs:2789-2793) when enabled: the
   // block map of the committed blocks, then (once every group's pixels and
@@ -2795,7 +3126,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     if (r->cdef) RV_R(cdef_slot(r, S, lv));
     RV_R(pad_slot(r, S));
   } else {
-    XRect xr[5];
+    XRect xr[6];
     int nx;
     group_rects(r, r->my_group, xr, &nx);
     RV_R(xcopy(r, S, xr, nx, 0, r->xsend));
@@ -2980,7 +3311,11 @@ int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
   out[14] = (uint64_t)r->mv_round_sum;
   out[15] = (uint64_t)r->mv_reeval;
   out[16] = r->exact ? (uint64_t)nonkey : 0;
-  return 17;
+  if (cap < 18) return 17;
+  // round runs: 1 + the MV / intra passes (the joint fixed point's outer
+  // iterations), summed over frames
+  out[17] = (uint64_t)r->mv_run_sum;
+  return 18;
 }
 
 // ---- RCCL communicator for the tile-group exchange ---------------------------

@@ -192,10 +192,11 @@ def tile_groups(tiling: dict, world: int) -> list:
 
 
 # result words per superblock and reference (rv_replay_results): coarse
-# (mv, cost), the four half-res quadrants, full-pel, sub-pel, the 16
-# lookahead 16x16 blocks; then per superblock winner, skip, cost, distortion
-WORDS_PER_REF = 2 + 8 + 2 + 2 + 32
-W_COARSE, W_HALF, W_FULL, W_SUB, W_LOOK = 0, 2, 10, 12, 14
+# (mv, cost), the four half-res quadrants (the encode's build_half_res_pmvs),
+# full-pel, sub-pel, the 16 lookahead 16x16 blocks, the lookahead's four
+# half-res quadrants; then per superblock winner, skip, cost, distortion
+WORDS_PER_REF = 2 + 8 + 2 + 2 + 32 + 8
+W_COARSE, W_HALF, W_FULL, W_SUB, W_LOOK, W_HALF_LA = 0, 2, 10, 12, 14, 46
 
 
 def sb_words_per(n_refs):
@@ -405,9 +406,10 @@ class HipReplay:
         6) single / compound of the 32x32, 16x16 and 8x8 blocks, superblocks
         intra-screened, intra winners, intra rounds] over the last <= 64
         frames, then (speed 10, since creation) the MV-stack rounds, the
-        superblocks they re-evaluated, and the frames."""
-        out = np.zeros(17, dtype=np.uint64)
-        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 17) - 17, "rv_replay_counters")
+        superblocks they re-evaluated, the frames, and the round runs (1 +
+        the MV / intra passes of each frame)."""
+        out = np.zeros(18, dtype=np.uint64)
+        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 18) - 18, "rv_replay_counters")
         return out
 
     def close(self):

@@ -323,7 +323,7 @@ def ds_case(c):
     j["mvx_min"], j["mvx_max"], j["mvy_min"], j["mvy_max"] = c[8:12]
     j["pmv0_row"], j["pmv0_col"], j["pmv1_row"], j["pmv1_col"] = c[12:16]
     j["lambda_"], j["n_pred"] = c[16], c[17]
-    j["pred"][:] = np.array(c[18:34]).reshape(8, 2)
+    j["pred"][:8] = np.array(c[18:34]).reshape(8, 2)  # the vectors' 8 predictor slots
     start = (c[34], c[35])
     start_cost = c[36] | (c[37] << 32)
     return w, h, sub, satd, hp, kind, j, start, start_cost
