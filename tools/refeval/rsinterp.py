@@ -2119,6 +2119,9 @@ def _slice_method(r, name, args, gty, raw):
     if isinstance(r, list) and name == "push":
         r.append(args[0])
         return None
+    if isinstance(r, list) and name == "extend":  # Vec / ArrayVec::extend
+        r.extend(list(to_iter(deref(args[0]))))
+        return None
     s = as_slice(r)
     if name == "len":
         return TInt(len(s), "usize")
