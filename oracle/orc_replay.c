@@ -42,7 +42,7 @@ typedef struct {
 } oplane;
 
 typedef struct {
-  oplane y, u, v, hres, qres;
+  oplane y, u, v;
   /* the coded frame's motion field (FrameState::frame_mvs, saved with the
    * reference, src/encoder.rs:3411-3429): [R][h_in_b][w_in_b] 4x4 units */
   orc_mv *fmv;
@@ -50,11 +50,31 @@ typedef struct {
 
 typedef struct {
   oplane y, u, v;
+  /* input_hres / input_qres of the input (FrameState, src/encoder.rs:362-
+   * 377; downsample_from + pad): the searches' half / quarter resolution
+   * planes of this frame and of every frame that references it */
+  oplane hres, qres;
+  int pyr; /* the pyramid is current */
 } oinput;
+
 
 typedef struct {
   int display, me_range_scale, level, is_key, ref_display[2], compound;
 } orc_frame_info; /* = rv_replay_frame_info */
+
+/* The lookahead of one coded frame (compute_lookahead_motion_vectors +
+ * compute_lookahead_intra_costs, src/api/internal.rs:514-765): its F1 /
+ * F2L / FL results, and what compute_block_importances reads of it. */
+typedef struct {
+  long coded; /* -1: empty */
+  orc_frame_info fi;
+  orc_mv *coarse, *half_l, *look; /* [R][nsb] (x4, x16) */
+  uint64_t *cc, *hlc, *lc;
+  uint32_t *intra; /* lookahead_intra_costs [h_imp][w_imp] */
+  orc_mv *mv8;     /* [R][h_imp][w_imp]: lookahead_mvs[k][2y][2x] */
+  float *frac;     /* [R][h_imp][w_imp]: max(1 - inter / intra, 0); NaN: no reference block */
+  float *imp;      /* block_importances, per output frame */
+} ola;
 
 typedef struct orc_replay {
   int W, H, xdec, ydec, bd, hbd, R, C;
@@ -70,6 +90,14 @@ typedef struct orc_replay {
   oslot slots[NSLOT];
   oinput *inputs;
   int n_inputs;
+  /* rdo_lookahead_frames (orc_replay_set_imp_window; 0: the importances are
+   * an input, orc_replay_set_importances): the lookahead runs that many
+   * coded frames ahead (ring la[W + 1]) and every frame's block importances
+   * come from compute_block_importances over the window */
+  int imp_window, h_imp;
+  ola *la;
+  long la_next; /* the next coded frame whose lookahead runs */
+  float *imp_own; /* the propagated importances of the frame being coded */
   float *imp; /* block_importances, NULL = zero */
   int threads;
   long coded;
@@ -384,9 +412,7 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile
   for (int s = 0; s < NSLOT; s++) {
     oslot *o = &r->slots[s];
     if (plane_init(&o->y, W, H, 0, 0, 88, r->hbd) || plane_init(&o->u, cw, ch, xdec, ydec, 88, r->hbd) ||
-        plane_init(&o->v, cw, ch, xdec, ydec, 88, r->hbd) ||
-        plane_init(&o->hres, W / 2, H / 2, 0, 0, 44, r->hbd) ||
-        plane_init(&o->qres, W / 4, H / 4, 0, 0, 22, r->hbd))
+        plane_init(&o->v, cw, ch, xdec, ydec, 88, r->hbd))
       return NULL;
     o->fmv = calloc((size_t)n_refs * r->w_in_b * r->h_in_b, sizeof(orc_mv));
     if (!o->fmv) return NULL;
@@ -396,9 +422,13 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile
   for (int i = 0; i < n_inputs; i++) {
     oinput *o = &r->inputs[i];
     if (plane_init(&o->y, W, H, 0, 0, 88, r->hbd) || plane_init(&o->u, cw, ch, xdec, ydec, 88, r->hbd) ||
-        plane_init(&o->v, cw, ch, xdec, ydec, 88, r->hbd))
+        plane_init(&o->v, cw, ch, xdec, ydec, 88, r->hbd) ||
+        plane_init(&o->hres, W / 2, H / 2, 0, 0, 44, r->hbd) ||
+        plane_init(&o->qres, W / 4, H / 4, 0, 0, 22, r->hbd))
       return NULL;
   }
+  r->h_imp = r->h_in_b / 2;
+  r->la_next = 1;
   size_t nr = (size_t)r->R * r->nsb;
   r->coarse = calloc(nr, sizeof(orc_mv));
   r->half = calloc(nr * 4, sizeof(orc_mv));
@@ -427,6 +457,7 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile
 }
 
 static void free_levels(orc_replay *r);
+static void free_la(orc_replay *r);
 
 void orc_replay_destroy(orc_replay *r) {
   if (!r) return;
@@ -435,14 +466,16 @@ void orc_replay_destroy(orc_replay *r) {
     free(o->y.mem);
     free(o->u.mem);
     free(o->v.mem);
-    free(o->hres.mem);
-    free(o->qres.mem);
     free(o->fmv);
   }
+  free_la(r);
+  free(r->imp_own);
   for (int i = 0; i < r->n_inputs; i++) {
     free(r->inputs[i].y.mem);
     free(r->inputs[i].u.mem);
     free(r->inputs[i].v.mem);
+    free(r->inputs[i].hres.mem);
+    free(r->inputs[i].qres.mem);
   }
   free(r->inputs);
   free(r->imp);
@@ -766,7 +799,19 @@ int orc_replay_set_input(orc_replay *r, int idx, const void *yuv) {
   oinput *o = &r->inputs[idx];
   oplane *pl[3] = {&o->y, &o->u, &o->v};
   copy_planes(r, pl, (void *)yuv, 1);
+  o->pyr = 0;
   return 0;
+}
+
+/* the input of display d with its pyramid */
+static oinput *input_pyr(orc_replay *r, int d) {
+  oinput *o = &r->inputs[d % r->n_inputs];
+  if (!o->pyr) {
+    downsample(r, &o->hres, &o->y);
+    downsample(r, &o->qres, &o->hres);
+    o->pyr = 1;
+  }
+  return o;
 }
 
 int orc_replay_get_recon(orc_replay *r, int display, void *yuv) {
@@ -973,7 +1018,7 @@ static orc_mv half_fp(const orc_replay *r, int k, int sb, int q) {
 
 /* Pass A1: F1 estimate_motion_ss4 (build_coarse_pmvs) of one superblock. */
 static void run_coarse(orc_replay *r, int sb) {
-  const oslot *S = &r->slots[r->fi.display % NSLOT];
+  const oinput *S = &r->inputs[r->fi.display % r->n_inputs];
   const int hbd = r->hbd;
   const sbgeo g = sb_geo_of(r, sb);
   int bx = g.tsx * 16, by = g.tsy * 16;
@@ -991,7 +1036,7 @@ static void run_coarse(orc_replay *r, int sb) {
   int y_hi = fby + ((m[3] / 8 < ry ? m[3] / 8 : ry) >> 2);
   orc_mv zero = {0, 0};
   for (int k = 0; k < r->R; k++) {
-    const oslot *ref = &r->slots[r->fi.ref_display[k] % NSLOT];
+    const oinput *ref = &r->inputs[r->fi.ref_display[k] % r->n_inputs];
     orc_mv best = {0, 0};
     uint64_t cost = UINT64_MAX;
     orc_full_search(org_of(&S->qres, hbd), S->qres.stride, org_of(&ref->qres, hbd),
@@ -1041,8 +1086,8 @@ static orc_mv coarse4(const orc_replay *r, int k, int sb) {
  * reference frame's field `prev` (NULL: none), every predictor halved. */
 static void half_quadrant(orc_replay *r, int sb, int k, int q, orc_mv *grid, const orc_mv *prev,
                           orc_mv *mv, uint64_t *cost) {
-  const oslot *S = &r->slots[r->fi.display % NSLOT];
-  const oslot *ref = &r->slots[r->fi.ref_display[k] % NSLOT];
+  const oinput *S = &r->inputs[r->fi.display % r->n_inputs];
+  const oinput *ref = &r->inputs[r->fi.ref_display[k] % r->n_inputs];
   const sbgeo g = sb_geo_of(r, sb);
   const double me_lambda = r->lv[r->fi.level].me_lambda;
   const uint32_t lambda2 = (uint32_t)(me_lambda * 256.0 / 4.0 * 0.125);
@@ -2081,6 +2126,25 @@ static void *worker(void *arg) {
   return NULL;
 }
 
+static void free_la(orc_replay *r) {
+  if (!r->la) return;
+  for (int i = 0; i <= r->imp_window; i++) {
+    ola *e = &r->la[i];
+    free(e->coarse);
+    free(e->half_l);
+    free(e->look);
+    free(e->cc);
+    free(e->hlc);
+    free(e->lc);
+    free(e->intra);
+    free(e->mv8);
+    free(e->frac);
+    free(e->imp);
+  }
+  free(r->la);
+  r->la = NULL;
+}
+
 static void run_pass(orc_replay *r, int pass) {
   r->pass = pass;
   r->next_sb = 0;
@@ -2124,18 +2188,15 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
     memcpy(s->y.mem, in->y.mem, plane_size(&in->y, r->hbd));
     memcpy(s->u.mem, in->u.mem, plane_size(&in->u, r->hbd));
     memcpy(s->v.mem, in->v.mem, plane_size(&in->v, r->hbd));
-    downsample(r, &s->hres, &in->y);
-    downsample(r, &s->qres, &s->hres);
     /* an intra frame saves no motion: its field stays zero */
     memset(s->fmv, 0, (size_t)r->R * r->w_in_b * r->h_in_b * sizeof(orc_mv));
     r->coded++;
     return 0;
   }
   if (!r->lv[0].set || !r->lv[1].set || !r->lv[2].set) return -1;
-  oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
   oslot *S = &r->slots[r->fi.display % NSLOT];
-  downsample(r, &S->hres, &cur->y);
-  downsample(r, &S->qres, &S->hres);
+  input_pyr(r, r->fi.display);
+  for (int k = 0; k < r->R; k++) input_pyr(r, r->fi.ref_display[k]);
   memset(r->tail, 0, sizeof(r->tail));
   r->sb_limit = sb_limit;
   r->istat[0] = r->istat[1] = 0;

@@ -51,75 +51,67 @@ __device__ inline bool epzs_zero(rv_mv m) { return m.row == 0 && m.col == 0; }
 // frame 4x4 (tx4, ty4), mi_w columns: zero, the ncm coarse MVs cm, subsets
 // A / B through rd(X4, Y4) (the tile field at frame 4x4 (X4, Y4)), subset C
 // from prev (the reference frame's field at 8x8 granularity -- every value
-// of rav1e's field is constant over 8x8 cells at speed 10 -- cell (x, y)
-// at prev[((y * w_in_b / 2) + x) * pr]; null: none).  Returns the count
-// (<= RV_DS_MAX_PRED).
-template <typename Rd, typename Emit>
+// of rav1e's field is constant over 8x8 cells at speed 10; null: none)
+// (cell (x, y) of prev at prev[((y * w_in_b / 2) + x) * pr]).  Writes the
+// set into out (<= RV_DS_MAX_PRED entries) and returns its size.  Every
+// field value is read once.
+template <typename Rd>
 __device__ inline int epzs_list(const EpzsGeo &g, int tx4, int ty4, int mi_w, int bx, int by,
                                 const rv_mv *cm, int ncm, Rd rd, const rv_mv *prev, int pr,
-                                Emit emit) {
+                                rv_mv *out) {
+  const bool hl = bx > 0, ht = by > 0, htr = ht && bx < mi_w - 1;
+  const rv_mv z{0, 0};
+  const rv_mv l = hl ? rd(tx4 + bx - 1, ty4 + by) : z;
+  const rv_mv t = ht ? rd(tx4 + bx, ty4 + by - 1) : z;
+  const rv_mv tr = htr ? rd(tx4 + bx + 1, ty4 + by - 1) : z;
   int n = 0;
-  emit(n++, rv_mv{0, 0});
-  for (int i = 0; i < ncm; i++) emit(n++, epzs_qfull(cm[i]));
-  int16_t sr = 0, sc = 0;
-  int nm = 0;
-  if (bx > 0) {
-    const rv_mv l = rd(tx4 + bx - 1, ty4 + by);
-    sr = (int16_t)(sr + l.row);
-    sc = (int16_t)(sc + l.col);
-    nm++;
-    if (!epzs_zero(l)) emit(n++, l);
-  }
-  if (by > 0) {
-    const rv_mv t = rd(tx4 + bx, ty4 + by - 1);
-    sr = (int16_t)(sr + t.row);
-    sc = (int16_t)(sc + t.col);
-    nm++;
-    if (!epzs_zero(t)) emit(n++, t);
-    if (bx < mi_w - 1) {
-      const rv_mv tr = rd(tx4 + bx + 1, ty4 + by - 1);
-      sr = (int16_t)(sr + tr.row);
-      sc = (int16_t)(sc + tr.col);
-      nm++;
-      if (!epzs_zero(tr)) emit(n++, tr);
-    }
-  }
-  if (nm) {  // MotionVector / i16: truncating division
+  out[n++] = z;
+  for (int i = 0; i < ncm; i++) out[n++] = epzs_qfull(cm[i]);
+  if (hl && !epzs_zero(l)) out[n++] = l;
+  if (ht && !epzs_zero(t)) out[n++] = t;
+  if (htr && !epzs_zero(tr)) out[n++] = tr;
+  const int nm = (int)hl + (int)ht + (int)htr;
+  if (nm) {  // the mean: MotionVector Add / Div<i16> (truncating)
+    const int16_t sr = (int16_t)((int16_t)(l.row + t.row) + tr.row);
+    const int16_t sc = (int16_t)((int16_t)(l.col + t.col) + tr.col);
     const rv_mv q = epzs_qfull(rv_mv{(int16_t)(sr / nm), (int16_t)(sc / nm)});
-    if (!epzs_zero(q)) emit(n++, q);
+    if (!epzs_zero(q)) out[n++] = q;
   }
   if (prev) {
     const int fx = tx4 + bx, fy = ty4 + by, w8 = g.w_in_b >> 1;
-    auto pv = [&](int x, int y) {
-      const rv_mv v = prev[((y >> 1) * w8 + (x >> 1)) * pr];
-      if (!epzs_zero(v)) emit(n++, v);
-    };
-    if (fx > 0) pv(fx - 1, fy);
-    if (fy > 0) pv(fx, fy - 1);
-    if (fx < g.w_in_b - 1) pv(fx + 1, fy);
-    if (fy < g.h_in_b - 1) pv(fx, fy + 1);
-    pv(fx, fy);
+    auto pv = [&](int x, int y) { return prev[((y >> 1) * w8 + (x >> 1)) * pr]; };
+    const rv_mv p0 = fx > 0 ? pv(fx - 1, fy) : z, p1 = fy > 0 ? pv(fx, fy - 1) : z;
+    const rv_mv p2 = fx < g.w_in_b - 1 ? pv(fx + 1, fy) : z;
+    const rv_mv p3 = fy < g.h_in_b - 1 ? pv(fx, fy + 1) : z, p4 = pv(fx, fy);
+    if (!epzs_zero(p0)) out[n++] = p0;
+    if (!epzs_zero(p1)) out[n++] = p1;
+    if (!epzs_zero(p2)) out[n++] = p2;
+    if (!epzs_zero(p3)) out[n++] = p3;
+    if (!epzs_zero(p4)) out[n++] = p4;
   }
   return n;
 }
 
-// The set of a job into its record (shr: every predictor >> 1, me_ss2),
-// unless it already holds it; returns whether it changed.  Two passes over
-// the generator keep the set out of private arrays.
-template <typename Gen>
-__device__ inline bool epzs_update(rv_ds_job *j, int shr, Gen gen) {
+// Set p (n entries; shr: every predictor >> 1, me_ss2) into job j unless it
+// already holds it; returns whether it changed.
+__device__ inline bool epzs_store(rv_ds_job *j, const rv_mv *p, int n, int shr) {
   auto tf = [&](rv_mv m) {
     return shr ? rv_mv{(int16_t)(m.row >> 1), (int16_t)(m.col >> 1)} : m;
   };
-  const int n0 = j->n_pred;
-  bool diff = false;
-  const int n = gen([&](int i, rv_mv m) {
-    if (i >= n0 || !mv_eq(j->pred[i], tf(m))) diff = true;
-  });
-  if (!diff && n == n0) return false;
-  gen([&](int i, rv_mv m) { j->pred[i] = tf(m); });
+  bool same = j->n_pred == n;
+  for (int i = 0; i < n && same; i++) same = mv_eq(j->pred[i], tf(p[i]));
+  if (same) return false;
+  for (int i = 0; i < n; i++) j->pred[i] = tf(p[i]);
   j->n_pred = n;
   return true;
+}
+
+// The set gen(out) builds into job j (see epzs_store)
+template <typename Gen>
+__device__ inline bool epzs_set(rv_ds_job *j, int shr, Gen gen) {
+  rv_mv p[RV_DS_MAX_PRED];
+  const int n = gen(p);
+  return epzs_store(j, p, n, shr);
 }
 
 // The round checks' counts: check q counts into cnt[0..1] (slot q of the

@@ -26,7 +26,8 @@ struct MvrefArgs {
   // the group's superblock grid, its tiles and the frame (4x4 units)
   int nsb, tw, th, tx0, ty0, tws, ths, W, H, w_in_b, h_in_b;
   int R, comp;             // references; compound stack on this frame
-  uint8_t sign_bias[2];    // ref_frame_sign_bias of reference k
+  uint32_t sign_bias;      // bit k: ref_frame_sign_bias of reference k (a bit mask: no
+                           // runtime index into the arguments)
   const BlkDec *dec;       // the superblocks' coded blocks
   const uint8_t *iwas;     // null, or 1: the superblock is an intra winner
   MvStack *stk;            // in / out: the stacks the superblocks were evaluated with

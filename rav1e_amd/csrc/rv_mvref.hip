@@ -85,7 +85,7 @@ struct Nb {
 
 // setup_mvref_list of a 64x64 block for ref_frames (rf0, rf1; rf1 = NONE:
 // single): the first two entries (clamped) into s0 / s1, the length returned
-__device__ inline int stack64(const Nb &nb, int rf0, int rf1, const uint8_t *sbias, int fx, int fy,
+__device__ inline int stack64(const Nb &nb, int rf0, int rf1, uint32_t sbias, int fx, int fy,
                               int fcols, int frows, Cand &s0, Cand &s1) {
   const bool compound = rf1 != kNoneFrame;
   Stk k;
@@ -132,7 +132,7 @@ __device__ inline int stack64(const Nb &nb, int rf0, int rf1, const uint8_t *sbi
             if (idc0 == 0) id0[0] = m; else id0[1] = m;
             idc0++;
           } else if (dfc0 < 2) {
-            const rv_mv v = sbias[cr - 1] != sbias[rf0 - 1] ? neg(m) : m;
+            const rv_mv v = ((sbias >> (cr - 1)) & 1) != ((sbias >> (rf0 - 1)) & 1) ? neg(m) : m;
             if (dfc0 == 0) df0[0] = v; else df0[1] = v;
             dfc0++;
           }
@@ -140,12 +140,12 @@ __device__ inline int stack64(const Nb &nb, int rf0, int rf1, const uint8_t *sbi
             if (idc1 == 0) id1[0] = m; else id1[1] = m;
             idc1++;
           } else if (dfc1 < 2) {
-            const rv_mv v = sbias[cr - 1] != sbias[rf1 - 1] ? neg(m) : m;
+            const rv_mv v = ((sbias >> (cr - 1)) & 1) != ((sbias >> (rf1 - 1)) & 1) ? neg(m) : m;
             if (dfc1 == 0) df1[0] = v; else df1[1] = v;
             dfc1++;
           }
         } else {
-          const rv_mv v = sbias[cr - 1] != sbias[rf0 - 1] ? neg(m) : m;
+          const rv_mv v = ((sbias >> (cr - 1)) & 1) != ((sbias >> (rf0 - 1)) & 1) ? neg(m) : m;
           push_or_add(k, v, rv_mv{0, 0}, 2, false, false);
         }
       }
@@ -208,10 +208,15 @@ __device__ inline BlkDec coded_at(const MvrefArgs &a, int nsb, int X, int Y) {
     const int B = 64 >> l, bx = X & ~(B - 1), by = Y & ~(B - 1);
     if (bx + B <= a.W && by + B <= a.H) break;
   }
-  const int B = 64 >> l;
-  const CandGeo &g = a.lcg[l];
-  const int b = (Y / B - g.ty0) * g.tw + (X / B - g.tx0);
-  return blk_dec_of(g, a.lsub[l], b, a.lwin[l][b].c);
+  // constant indices into the argument arrays (a runtime index would copy
+  // the arguments into scratch memory)
+  auto leaf = [&](const CandGeo &g, const rv_fs_result *sub, const RdoWinner *win, int B) {
+    const int b = (Y / B - g.ty0) * g.tw + (X / B - g.tx0);
+    return blk_dec_of(g, sub, b, win[b].c);
+  };
+  if (l == 1) return leaf(a.lcg[1], a.lsub[1], a.lwin[1], 32);
+  if (l == 2) return leaf(a.lcg[2], a.lsub[2], a.lwin[2], 16);
+  return leaf(a.lcg[3], a.lsub[3], a.lwin[3], 8);
 }
 
 // The superblock's stacks: every reference's and, on compound frames, the
@@ -283,42 +288,37 @@ __device__ inline rv_mv coarse4(const MvrefArgs &a, int k, int sb) {
   return rv_mv{(int16_t)(c.row * 4), (int16_t)(c.col * 4)};
 }
 
-// The superblock's F2 and F3 predictor sets from the current state into its
-// jobs; returns whether one changed.
-__device__ inline bool epzs_sb(const MvrefArgs &a, int sb, int fsx, int fsy) {
+// EPZS job j of the superblock (j < R: F3 of reference j; then F2 quadrant
+// q of reference k at j = R + 4 k + q): its predictor set from the current
+// state into the job; returns whether it changed.
+__device__ inline bool epzs_job(const MvrefArgs &a, int sb, int fsx, int fsy, int j) {
   int t0x, t0y, mi_w, mi_h;
   epzs_tile(a.eg, fsx, fsy, t0x, t0y, mi_w, mi_h);
   const int tsx = fsx - t0x, tsy = fsy - t0y;
-  const int tsw = (mi_w + 15) / 16, tsh = (mi_h + 15) / 16;
-  const bool hw = tsx > 0, he = tsx < tsw - 1, hn = tsy > 0, hs = tsy < tsh - 1;
-  bool changed = false;
-  for (int k = 0; k < a.R; k++) {
-    auto rd = [&](int X4, int Y4) { return enc_field(a, k, X4, Y4, fsx, fsy); };
-    const rv_mv *prev = a.prev ? a.prev + k : nullptr;
-    // F3: full_pixel_me of the 64x64 (src/me.rs:390-431), cmvs = [pmvs[0]]
-    {
-      const rv_mv cm = coarse4(a, k, sb);
-      changed |= epzs_update(a.jf + (size_t)k * a.nsb + sb, 0, [&](auto emit) {
-        return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, tsx * 16, tsy * 16, &cm, 1, rd, prev,
-                         a.R, emit);
-      });
-    }
-    // F2: me_ss2 of the four quadrants (src/me.rs:465-519), adjust_bo'd,
-    // cmvs = the coarse MVs of the superblock and its neighbour on each side
-    for (int q = 0; q < 4; q++) {
-      rv_mv cm[3];
-      int nc = 0;
-      cm[nc++] = coarse4(a, k, sb);
-      if ((q & 1) ? he : hw) cm[nc++] = coarse4(a, k, (q & 1) ? sb + 1 : sb - 1);
-      if ((q >> 1) ? hs : hn) cm[nc++] = coarse4(a, k, (q >> 1) ? sb + a.tw : sb - a.tw);
-      int bx = tsx * 16 + (q & 1) * 8, by = tsy * 16 + (q >> 1) * 8;
-      epzs_adjust_bo(mi_w, mi_h, bx, by, 32, 32);
-      changed |= epzs_update(a.jh + ((size_t)k * a.nsb + sb) * 4 + q, 1, [&](auto emit) {
-        return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, prev, a.R, emit);
-      });
-    }
+  const int k = j < a.R ? j : (j - a.R) >> 2;
+  auto rd = [&](int X4, int Y4) { return enc_field(a, k, X4, Y4, fsx, fsy); };
+  const rv_mv *prev = a.prev ? a.prev + k : nullptr;
+  if (j < a.R) {  // F3: full_pixel_me of the 64x64 (src/me.rs:390-431), cmvs = [pmvs[0]]
+    const rv_mv cm = coarse4(a, k, sb);
+    return epzs_set(a.jf + (size_t)k * a.nsb + sb, 0, [&](rv_mv *o) {
+      return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, tsx * 16, tsy * 16, &cm, 1, rd, prev, a.R,
+                       o);
+    });
   }
-  return changed;
+  // F2: me_ss2 of quadrant q (src/me.rs:465-519), adjust_bo'd, cmvs = the
+  // coarse MVs of the superblock and its neighbour on each side
+  const int q = (j - a.R) & 3;
+  const int tsw = (mi_w + 15) / 16, tsh = (mi_h + 15) / 16;
+  rv_mv cm[3];
+  int nc = 0;
+  cm[nc++] = coarse4(a, k, sb);
+  if ((q & 1) ? tsx < tsw - 1 : tsx > 0) cm[nc++] = coarse4(a, k, (q & 1) ? sb + 1 : sb - 1);
+  if ((q >> 1) ? tsy < tsh - 1 : tsy > 0) cm[nc++] = coarse4(a, k, (q >> 1) ? sb + a.tw : sb - a.tw);
+  int bx = tsx * 16 + (q & 1) * 8, by = tsy * 16 + (q >> 1) * 8;
+  epzs_adjust_bo(mi_w, mi_h, bx, by, 32, 32);
+  return epzs_set(a.jh + ((size_t)k * a.nsb + sb) * 4 + q, 1, [&](rv_mv *o) {
+    return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, prev, a.R, o);
+  });
 }
 
 // The coded frame's field: one thread per 8x8 cell of the group (inside the
@@ -335,45 +335,59 @@ __global__ __launch_bounds__(256) void mvref_field_kernel(MvrefArgs a, rv_mv *fi
     field[((size_t)y8 * w8 + x8) * a.R + k] = enc_field(a, k, 2 * x8, 2 * y8, -1, -1);
 }
 
+// One check: 16 lanes per superblock -- lane 0 its stacks, lanes 1 .. 5 R
+// its EPZS jobs (F3 per reference, F2 per quadrant and reference) -- so a
+// superblock's eleven sets are built side by side.
+constexpr int kCheckLanes = 16;
 __global__ __launch_bounds__(256) void mvref_kernel(MvrefArgs a) {
-  const int sb = blockIdx.x * 256 + threadIdx.x;
-  bool mark = false;
-  if (sb < a.nsb) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int sb = t / kCheckLanes, j = t % kCheckLanes;
+  const int lane = threadIdx.x & 63;
+  bool changed = false;
+  const bool live = sb < a.nsb;
+  if (live) {
     const int sx = sb % a.tw, sy = sb / a.tw;
     const int fsx = a.tx0 + sx, fsy = a.ty0 + sy;  // frame superblock
-    // the tile: its origin in superblocks and its size in 4x4 units
-    // (TileBlocks cols / rows, src/tiling/tiler.rs:194-202)
-    const int t0x = fsx - fsx % a.tws, t0y = fsy - fsy % a.ths;
-    const int cols = min(a.tws * 16, a.w_in_b - t0x * 16);
-    const int bx = (fsx - t0x) * 16, by = (fsy - t0y) * 16;  // tile-relative 4x4 offset
-    const int X = fsx * 64, Y = fsy * 64;
-    // a superblock past the frame edge is split (must_split): its 64x64 is
-    // evaluated but never coded, with empty stacks (and it reads no
-    // neighbour: the edge levels' winners may still be in flight)
-    const bool split = a.lvl && (X + 64 > a.W || Y + 64 > a.H);
-    Nb nb;
-    nb.up = !split && by > 0;
-    nb.left = !split && bx > 0;
-    nb.tr = !split && by > 0 && bx + 16 < cols;  // has_tr(64x64) && scan_blk_mbmi's bound
-    nb.tl = !split && bx > 0 && by > 0;
-    if (nb.up) nb.a = coded_at(a, sb - a.tw, X, Y - 4);
-    if (nb.left) nb.l = coded_at(a, sb - 1, X - 4, Y);
-    if (nb.tr) nb.r = coded_at(a, sb - a.tw + 1, X + 64, Y - 4);
-    if (nb.tl) nb.d = coded_at(a, sb - a.tw - 1, X - 4, Y - 4);
-    const MvStack s = stacks_of(a, nb, split, fsx, fsy);
-    mark = !same_stacks(a, a.stk[sb], s);
-    if (a.epzs) mark |= epzs_sb(a, sb, fsx, fsy);  // (always evaluated: it stores the sets)
-    a.active[sb] = mark;
-    if (mark) set_stacks(a, sb, s);
+    if (j == 0) {
+      // the tile: its origin in superblocks and its size in 4x4 units
+      // (TileBlocks cols / rows, src/tiling/tiler.rs:194-202)
+      const int t0x = fsx - fsx % a.tws, t0y = fsy - fsy % a.ths;
+      const int cols = min(a.tws * 16, a.w_in_b - t0x * 16);
+      const int bx = (fsx - t0x) * 16, by = (fsy - t0y) * 16;  // tile-relative 4x4 offset
+      const int X = fsx * 64, Y = fsy * 64;
+      // a superblock past the frame edge is split (must_split): its 64x64 is
+      // evaluated but never coded, with empty stacks (and it reads no
+      // neighbour: the edge levels' winners may still be in flight)
+      const bool split = a.lvl && (X + 64 > a.W || Y + 64 > a.H);
+      Nb nb;
+      nb.up = !split && by > 0;
+      nb.left = !split && bx > 0;
+      nb.tr = !split && by > 0 && bx + 16 < cols;  // has_tr(64x64) && scan_blk_mbmi's bound
+      nb.tl = !split && bx > 0 && by > 0;
+      if (nb.up) nb.a = coded_at(a, sb - a.tw, X, Y - 4);
+      if (nb.left) nb.l = coded_at(a, sb - 1, X - 4, Y);
+      if (nb.tr) nb.r = coded_at(a, sb - a.tw + 1, X + 64, Y - 4);
+      if (nb.tl) nb.d = coded_at(a, sb - a.tw - 1, X - 4, Y - 4);
+      const MvStack s = stacks_of(a, nb, split, fsx, fsy);
+      changed = !same_stacks(a, a.stk[sb], s);
+      if (changed) set_stacks(a, sb, s);  // (its pmv: the F3 jobs' rate predictors)
+    } else if (a.epzs && j <= 5 * a.R) {
+      changed = epzs_job(a, sb, fsx, fsy, j - 1);
+    }
   }
+  // the superblock's lanes: any change marks it (lane 0 records and lists it)
+  const uint64_t cm = __ballot(changed);
+  const int g0 = lane & ~(kCheckLanes - 1);
+  const bool mark = live && ((cm >> g0) & ((1ull << kCheckLanes) - 1)) != 0;
+  const bool lead = live && j == 0;
+  if (lead) a.active[sb] = mark;
   // wave-aggregated append to the list (the returned base orders the
   // workgroup's adds before its ticket below)
-  const uint64_t m = __ballot(mark);
-  const int lane = threadIdx.x & 63;
+  const uint64_t m = __ballot(lead && mark);
   int base = 0;
   if (lane == 0 && m) base = atomicAdd(a.count, (int)__popcll(m));
   base = __shfl(base, 0, 64);
-  if (mark) a.list[base + __popcll(m & ((1ull << lane) - 1))] = sb;
+  if (lead && mark) a.list[base + __popcll(m & ((1ull << lane) - 1))] = sb;
   round_publish(a.pub);
 }
 
@@ -470,7 +484,7 @@ int rv_mvref_round(const MvrefArgs &a, hipStream_t s, bool scan) {
     const int ntiles = ((a.tw + a.tws - 1) / a.tws) * ((a.th + a.ths - 1) / a.ths);
     mvref_scan_kernel<<<ntiles, 64, (size_t)a.tws * a.ths * sizeof(BlkDec), s>>>(a);
   } else {
-    mvref_kernel<<<(a.nsb + 255) / 256, 256, 0, s>>>(a);
+    mvref_kernel<<<(a.nsb * kCheckLanes + 255) / 256, 256, 0, s>>>(a);
   }
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;

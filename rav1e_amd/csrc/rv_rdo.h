@@ -68,12 +68,6 @@ int rv_quant_ctx(int qindex, int tx_area, int is_intra, int bit_depth, int dc_de
 int rv_rdo_candidates(const rv::RdoArgs &luma, const rv::RdoArgs &chroma, int hbd,
                       hipStream_t s, bool compound = false);
 
-// The MV-stack rounds after the first: the listed single-reference (ls,
-// cs) and, when lc / cc are given, compound candidates in one launch of
-// `grid` workgroups that loop over the device counts (8 / 10-bit).
-int rv_rdo_round(const rv::RdoArgs &ls, const rv::RdoArgs &cs, const rv::RdoArgs *lc,
-                 const rv::RdoArgs *cc, int hbd, hipStream_t s, int grid);
-
 // Blocks below 64x64 (speed 6): one launch over the tasks of a (luma or
 // the two chroma planes) for transform size n_tx_size; mode 0 single,
 // 1 compound (score), 2 commit.

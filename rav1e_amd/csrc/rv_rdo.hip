@@ -1254,40 +1254,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
   __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
   __shared__ uint16_t scan[1024];
   const int b = blockIdx.x;
+  // a workgroup past the compacted lists leaves before staging the scan:
+  // the MV-stack rounds launch the full grid for a few dozen superblocks'
+  // candidates (the device holds the count), so most workgroups exit here
+  if (b >= nquads) {
+    const int pairs = (chroma.n_tx + 1) / 2, nc = rdo_ntx(chroma);
+    bool any = false;
+    for (int w = 0; w < 3; w++) {
+      const int p = 3 * (b - nquads) + w;
+      if (p < 2 * pairs) any |= 2 * (p - (p / pairs) * pairs) < nc;
+    }
+    if (!any) return;
+  } else if (4 * b >= rdo_ntx(luma)) {
+    return;
+  }
   stage_scan(scan, b >= nquads ? chroma.q_tx_index : luma.q_tx_index);
   if (b >= nquads)  // chroma pairs
     rdo_quad_chroma<Px, MODE>(chroma, b - nquads, (chroma.n_tx + 1) / 2, lds, scan);
   else
     rdo_quad_luma<Px, MODE>(luma, b, rdo_ntx(luma), var, lds, scan);
-}
-
-// The MV-stack rounds after the first (rv_replay_frame): the candidates of
-// the superblocks the round's check listed, single-reference (ls / cs,
-// MODE 0) and compound (lc / cc, MODE 1; null list: none) in one launch.
-// A fixed pool of workgroups walks the tasks the device counts give: the
-// single luma quads, the single chroma triples, then the compound ones.
-template <typename Px>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_round_kernel(
-    RdoArgs ls, RdoArgs cs, RdoArgs lc, RdoArgs cc, int var) {
-  __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
-  __shared__ uint16_t scan_l[1024], scan_c[1024];
-  stage_scan(scan_l, ls.q_tx_index);
-  stage_scan(scan_c, cs.q_tx_index);
-  const int ns = rdo_ntx(ls), ps = (rdo_ntx(cs) + 1) / 2;
-  const int nc = lc.list ? rdo_ntx(lc) : 0, pc = lc.list ? (rdo_ntx(cc) + 1) / 2 : 0;
-  const int q0 = (ns + 3) / 4, c0 = q0 + (2 * ps + 2) / 3;
-  const int q1 = c0 + (nc + 3) / 4, total = q1 + (2 * pc + 2) / 3;
-  for (int b = blockIdx.x; b < total; b += gridDim.x) {
-    if (b < q0)
-      rdo_quad_luma<Px, 0>(ls, b, ns, var, lds, scan_l);
-    else if (b < c0)
-      rdo_quad_chroma<Px, 0>(cs, b - q0, ps, lds, scan_c);
-    else if (b < q1)
-      rdo_quad_luma<Px, 1>(lc, b - c0, nc, var, lds, scan_l);
-    else
-      rdo_quad_chroma<Px, 1>(cc, b - q1, pc, lds, scan_c);
-    __syncthreads();  // the task's LDS reads end before the next task's writes
-  }
 }
 
 }  // namespace rv
@@ -1430,31 +1415,6 @@ int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipSt
     rdo_launch<1>(luma, chroma, hbd, s, single, cpairs);
   else
     rdo_launch<0>(luma, chroma, hbd, s, single, cpairs);
-  RV_HIP_CHECK_LAUNCH();
-  return RV_OK;
-}
-
-int rv_rdo_round(const RdoArgs &ls, const RdoArgs &cs, const RdoArgs *lc, const RdoArgs *cc,
-                 int hbd, hipStream_t s, int grid) {
-  if (!ls.list || !ls.count || !cs.list || !cs.count || (lc && (!lc->list || !cc || !cc->list)) ||
-      ls.bd == 12 || grid <= 0)
-    return rv_set_error(RV_EINVAL, "rv_rdo_round: list-driven 8 / 10-bit launches only");
-  static const int var = [] {
-    const char *e = getenv("RAV1E_HIP_RDO_VARIANT");
-    return e ? atoi(e) : 3;
-  }();
-  RdoArgs l1, c1;
-  if (lc) {
-    l1 = *lc;
-    c1 = *cc;
-  } else {
-    memset(&l1, 0, sizeof(l1));
-    memset(&c1, 0, sizeof(c1));
-  }
-  if (hbd)
-    rdo_round_kernel<uint16_t><<<grid, 256, 0, s>>>(ls, cs, l1, c1, var);
-  else
-    rdo_round_kernel<uint8_t><<<grid, 256, 0, s>>>(ls, cs, l1, c1, var);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

@@ -403,8 +403,8 @@ __global__ __launch_bounds__(256) void la_check_kernel(LaArgs a) {
           a.half_l[((size_t)k * g.nsb + gsb) * 4 + ((Y4 >> 3) & 1) * 2 + ((X4 >> 3) & 1)].best_mv;
       return rv_mv{(int16_t)(h.row * 2), (int16_t)(h.col * 2)};
     };
-    mh = epzs_update(a.jh + i, 1, [&](auto emit) {
-      return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, nullptr, 1, emit);
+    mh = epzs_set(a.jh + i, 1, [&](rv_mv *o) {
+      return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, nullptr, 1, o);
     }) && !a.init;
   } else if (i - nh < nl) {  // FL: estimate_motion of 16x16 block b (src/me.rs:337-390)
     const int j = i - nh;
@@ -432,8 +432,8 @@ __global__ __launch_bounds__(256) void la_check_kernel(LaArgs a) {
       return a.look[((size_t)k * g.nsb + gsb) * 16 + ((Y4 & 15) >> 2) * 4 + ((X4 & 15) >> 2)]
           .best_mv;
     };
-    ml = epzs_update(a.jl + j, 0, [&](auto emit) {
-      return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, nullptr, 1, emit);
+    ml = epzs_set(a.jl + j, 0, [&](rv_mv *o) {
+      return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, nullptr, 1, o);
     }) && !a.init;
   }
   const int lane = threadIdx.x & 63;
@@ -2419,6 +2419,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     }
   };
   auto slot_cnt = [&](uint32_t q) { return r->mv_cnt + 2 * (q % rv_replay::kCntRing); };
+  // check q's slot of the host-mapped ring (read at h_pub + q % kPubRing)
+  auto pub_of = [&](uint32_t q) { return r->d_pub + q % rv_replay::kPubRing; };
   const EpzsGeo eg{g.tx0, g.ty0, g.tw, g.th, g.tws, g.ths, g.W, g.H, g.w_in_b, g.h_in_b};
 
   // F2L + FL: the lookahead's build_half_res_pmvs and build_full_res_pmvs
@@ -2447,7 +2449,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     auto la_launch = [&](int what, uint32_t q, bool init) -> int {
       la_a.what = what;
       la_a.init = init ? 1 : 0;
-      la_a.pub = RoundPub{slot_cnt(q), slot_cnt(q + 1), r->mv_ticket, init ? nullptr : r->d_pub, q};
+      la_a.pub = RoundPub{slot_cnt(q), slot_cnt(q + 1), r->mv_ticket, init ? nullptr : pub_of(q), q};
       const int n = ((what & 1) ? nh : 0) + ((what & 2) ? nl : 0);
       la_check_kernel<<<(n + 255) / 256, 256, 0, st>>>(la_a);
       RV_H(hipGetLastError());
@@ -2756,7 +2758,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     ma.h_in_b = g.h_in_b;
     ma.R = g.R;
     ma.comp = cg.comp ? 1 : 0;
-    for (int k = 0; k < g.R; k++) ma.sign_bias[k] = fi.ref_display[k] > fi.display;
+    for (int k = 0; k < g.R; k++) ma.sign_bias |= (uint32_t)(fi.ref_display[k] > fi.display) << k;
     ma.dec = r->dec_lv[lv];
     ma.stk = r->stk;
     ma.active = r->mv_active;
@@ -2790,7 +2792,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     // the first check marks every superblock (its count is not read)
     const uint32_t q = r->mv_seq++;
     ma.count = slot_cnt(q);
-    ma.pub = RoundPub{slot_cnt(q), slot_cnt(q + 1), r->mv_ticket, r->d_pub, q};
+    ma.pub = RoundPub{slot_cnt(q), slot_cnt(q + 1), r->mv_ticket, pub_of(q), q};
     RV_R(rv_mvref_round(ma, st));
   }
   // F2: build_half_res_pmvs of the encode (speed 10: the sets the check
@@ -2869,12 +2871,17 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                  r->sub, nullptr, nullptr, xs, nullptr, r->mv_list, acnt));
     round_lists_kernel<<<kRoundGrid, 256, 0, xs>>>(cg, r->sub, nsingle, r->cand_list,
                                                    r->cand_count, r->mv_list, acnt);
-    RdoArgs lc = la4, cc = ca4;
-    lc.list = cc.list = r->cand_list + nsingle;
-    lc.count = cc.count = r->cand_count + 1;
-    lc.cand_base = cc.cand_base = 0;
-    RV_R(rv_rdo_round(la4, ca4, cg.comp ? &lc : nullptr, cg.comp ? &cc : nullptr, g.hbd, xs,
-                      kRoundGrid));
+    // F4 (full grids: a workgroup past the device counts exits at once)
+    RV_R(rv_rdo_candidates(la4, ca4, g.hbd, xs));
+    if (cg.comp) {
+      RdoArgs lc = la4, cc = ca4;
+      lc.list = cc.list = r->cand_list + nsingle;
+      lc.count = cc.count = r->cand_count + 1;
+      lc.cand_base = cc.cand_base = 0;
+      lc.n_tx = g.nsb * cg.comp;
+      cc.n_tx = g.nsb * cg.comp * ntx_c;
+      RV_R(rv_rdo_candidates(lc, cc, g.hbd, xs, true));
+    }
     score_wave_kernel<<<kRoundGrid, 256, 0, xs>>>(
         g, cg, L.lambda, L.ds[1], L.ds[2], r->sub, r->l_out, r->c_out, r->c_out + nct * 3, ntx_c,
         r->win, r->coarse, r->half, r->full, r->look, r->half_l, r->words, r->cand_count, nullptr,
@@ -2921,7 +2928,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
           ma.init = 0;
           ma.iwas = iwas;
           ma.count = slot_cnt(q);
-          ma.pub = RoundPub{slot_cnt(q), slot_cnt(q + 1), r->mv_ticket, r->d_pub, q};
+          ma.pub = RoundPub{slot_cnt(q), slot_cnt(q + 1), r->mv_ticket, pub_of(q), q};
           return rv_mvref_round(ma, xs);
         },
         [&](uint32_t q) { return f3_f4_list(xs, q); }, &r->mv_round_sum, &r->mv_reeval, changed,
