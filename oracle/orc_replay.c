@@ -72,7 +72,7 @@ typedef struct {
   uint64_t *cc, *hlc, *lc;
   uint32_t *intra; /* lookahead_intra_costs [h_imp][w_imp] */
   orc_mv *mv8;     /* [R][h_imp][w_imp]: lookahead_mvs[k][2y][2x] */
-  float *frac;     /* [R][h_imp][w_imp]: max(1 - inter / intra, 0); NaN: no reference block */
+  uint32_t *inter; /* [R][h_imp][w_imp]: get_satd against the reference block at mv8 */
   float *imp;      /* block_importances, per output frame */
 } ola;
 
@@ -96,7 +96,8 @@ typedef struct orc_replay {
    * come from compute_block_importances over the window */
   int imp_window, h_imp;
   ola *la;
-  long la_next; /* the next coded frame whose lookahead runs */
+  long la_next;  /* the next coded frame whose lookahead runs */
+  long la_limit; /* coded frames in the stream (0: unbounded) */
   float *imp_own; /* the propagated importances of the frame being coded */
   float *imp; /* block_importances, NULL = zero */
   int threads;
@@ -898,12 +899,13 @@ static void ds_ctx(const orc_replay *r, orc_ds_ctx *c, const oplane *org, const 
  * m x m 4x4 blocks (BLOCK_8X8: m = 2; BLOCK_4X4 for chroma planes narrower
  * than 8: m = 1) at 4x4 block (mi_x, mi_y) */
 static double dist_bias(const orc_replay *r, int mi_x, int mi_y, int m) {
-  if (!r->imp) return 0.65;
+  const float *imp = r->imp_window ? r->imp_own : r->imp;
+  if (!imp) return 0.65;
   int x2 = mi_x + m < r->w_in_b ? mi_x + m : r->w_in_b;
   int y2 = mi_y + m < r->h_in_b ? mi_y + m : r->h_in_b;
   float tot = 0.f;
   for (int y = mi_y; y < y2; y++)
-    for (int x = mi_x; x < x2; x++) tot += r->imp[(y >> 1) * r->w_imp + (x >> 1)];
+    for (int x = mi_x; x < x2; x++) tot += imp[(y >> 1) * r->w_imp + (x >> 1)];
   float mean = tot / (float)(m * m);
   return (double)(mean / 3.0f) + 0.65;
 }
@@ -2138,7 +2140,7 @@ static void free_la(orc_replay *r) {
     free(e->lc);
     free(e->intra);
     free(e->mv8);
-    free(e->frac);
+    free(e->inter);
     free(e->imp);
   }
   free(r->la);
@@ -2176,6 +2178,173 @@ static void frame_info(long n, int R, orc_frame_info *f) {
   f->compound = R == 2 && (j == 1 || j == 3);
 }
 
+/* ---- block importances over the lookahead window (rdo_lookahead_frames) --
+ * compute_lookahead_data (src/api/internal.rs:767-820) runs the lookahead of
+ * every frame as it arrives, far ahead of its encode; compute_block_importances
+ * (:823-1081) then propagates over the window [n, n + W] of coded frames.
+ * Here frame m's lookahead (F1, F2L, FL -- it reads only the inputs) runs
+ * once, W frames before m is coded, into ring entry m % (W + 1), with what
+ * the propagation reads of it: lookahead_intra_costs, the 8x8 blocks'
+ * lookahead MVs ([2y][2x] of the field: the FL MV of the 16x16 holding the
+ * block) and their get_satd against each reference's original frame. */
+
+/* the coded index of display d (inverse of frame_info) */
+static long coded_of_display(long d) {
+  if (d == 0) return 0;
+  static const int jof[4] = {0, 2, 1, 3}, off[4] = {4, 2, 1, 3};
+  const int j = jof[d % 4];
+  return 4 * ((d - off[j]) / 4) + j + 1;
+}
+
+static ola *la_of(orc_replay *r, long m) { return &r->la[m % (r->imp_window + 1)]; }
+
+static void la_compute(orc_replay *r, long m) {
+  const orc_frame_info save = r->fi;
+  const int save_lim = r->sb_limit;
+  frame_info(m, r->R, &r->fi);
+  r->sb_limit = 0;
+  const size_t nr = (size_t)r->R * r->nsb;
+  input_pyr(r, r->fi.display);
+  for (int k = 0; k < r->R; k++) input_pyr(r, r->fi.ref_display[k]);
+  memset(r->tmv_l, 0, (size_t)r->R * r->tw * 16 * r->th * 16 * sizeof(orc_mv));
+  run_pass(r, 0);
+  run_pass(r, 6);
+  ola *e = la_of(r, m);
+  e->coded = m;
+  e->fi = r->fi;
+  memcpy(e->coarse, r->coarse, nr * sizeof(orc_mv));
+  memcpy(e->cc, r->cc, nr * 8);
+  memcpy(e->half_l, r->half_l, nr * 4 * sizeof(orc_mv));
+  memcpy(e->hlc, r->hlc, nr * 4 * 8);
+  memcpy(e->look, r->look, nr * 16 * sizeof(orc_mv));
+  memcpy(e->lc, r->lc, nr * 16 * 8);
+  const int w = r->w_imp, h = r->h_imp, hbd = r->hbd;
+  const size_t ni = (size_t)w * h;
+  const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      orc_lookahead_intra_costs(at(&cur->y, hbd, x * 8, y * 8), cur->y.stride, 8, 8, hbd, r->bd,
+                                &e->intra[(size_t)y * w + x]);
+      const int sb = (y / 8) * r->tw + x / 8, b = ((y % 8) / 2) * 4 + (x % 8) / 2;
+      for (int k = 0; k < r->R; k++)
+        e->mv8[k * ni + (size_t)y * w + x] = r->look[((size_t)k * r->nsb + sb) * 16 + b];
+    }
+  for (int k = 0; k < r->R; k++) {
+    const oplane *ref = &r->inputs[r->fi.ref_display[k] % r->n_inputs].y;
+    orc_importance_inter_costs(at(&cur->y, hbd, 0, 0), cur->y.stride, at(ref, hbd, 0, 0),
+                               ref->stride, w, h, hbd, e->mv8 + k * ni, e->inter + k * ni);
+  }
+  r->fi = save;
+  r->sb_limit = save_lim;
+}
+
+/* the lookahead of every frame up to n + W (n: the frame being coded) */
+static void la_fill(orc_replay *r) {
+  long last = r->coded + r->imp_window;
+  if (r->la_limit > 0 && last > r->la_limit - 1) last = r->la_limit - 1;
+  for (; r->la_next <= last; r->la_next++) la_compute(r, r->la_next);
+}
+
+/* compute_block_importances for frame n = r->coded: zero the window's
+ * importances, propagate from its last frame down to n + 1 (each frame's
+ * distinct references in order, the split by their count; references
+ * before n are outside the window and gone, :944-948), then log2(1 +
+ * importance / intra cost) for frame n (:1052-1070). */
+static void importance_frame(orc_replay *r) {
+  const long n = r->coded, last = r->la_next - 1;
+  const int w = r->w_imp, h = r->h_imp;
+  const size_t ni = (size_t)w * h;
+  for (long m = n; m <= last; m++) memset(la_of(r, m)->imp, 0, ni * sizeof(float));
+  for (long m = last; m > n; m--) {
+    const ola *e = la_of(r, m);
+    if (e->fi.is_key) continue;
+    int uk[2], nu = 0;
+    for (int k = 0; k < r->R; k++) {
+      int dup = 0;
+      for (int j = 0; j < nu; j++) dup |= e->fi.ref_display[uk[j]] == e->fi.ref_display[k];
+      if (!dup) uk[nu++] = k;
+    }
+    for (int j = 0; j < nu; j++) {
+      const int k = uk[j];
+      const long mref = coded_of_display(e->fi.ref_display[k]);
+      if (mref < n) continue;
+      orc_propagate_importances_costs(w, h, e->mv8 + k * ni, e->inter + k * ni, e->intra, e->imp,
+                                      nu, la_of(r, mref)->imp);
+    }
+  }
+  const ola *c = la_of(r, n);
+  for (size_t i = 0; i < ni; i++) {
+    const float intra = (float)c->intra[i];
+    r->imp_own[i] = intra > 0.f ? orc_log2f(1.f + c->imp[i] / intra) : 0.f;
+  }
+}
+
+/* The window W (rdo_lookahead_frames; 0: the importances are an input,
+ * orc_replay_set_importances) and the stream's length in coded frames
+ * (limit; 0: unbounded -- the inputs of frame n + W must be set before
+ * frame n is coded).  Only before the first frame, and only for a replay of
+ * the whole frame (a group's importances would need the other groups'). */
+int orc_replay_set_imp_window(orc_replay *r, int window, long limit) {
+  if (window < 0 || r->coded > 0) return -1;
+  if (window > 0 && (r->tx0 || r->ty0 || r->vis_w != r->W || r->vis_h != r->H)) return -1;
+  free_la(r);
+  free(r->imp_own);
+  r->imp_own = NULL;
+  r->imp_window = 0;
+  r->la_limit = limit;
+  r->la_next = 1;
+  if (!window) return 0;
+  const size_t nr = (size_t)r->R * r->nsb, ni = (size_t)r->w_imp * r->h_imp;
+  r->la = calloc((size_t)window + 1, sizeof(ola));
+  r->imp_own = calloc(ni, sizeof(float));
+  if (!r->la || !r->imp_own) return -1;
+  r->imp_window = window;
+  for (int i = 0; i <= window; i++) {
+    ola *e = &r->la[i];
+    e->coded = -1;
+    e->coarse = calloc(nr, sizeof(orc_mv));
+    e->cc = calloc(nr, 8);
+    e->half_l = calloc(nr * 4, sizeof(orc_mv));
+    e->hlc = calloc(nr * 4, 8);
+    e->look = calloc(nr * 16, sizeof(orc_mv));
+    e->lc = calloc(nr * 16, 8);
+    e->intra = calloc(ni, 4);
+    e->mv8 = calloc(ni * r->R, sizeof(orc_mv));
+    e->inter = calloc(ni * r->R, 4);
+    e->imp = calloc(ni, 4);
+    if (!e->coarse || !e->cc || !e->half_l || !e->hlc || !e->look || !e->lc || !e->intra ||
+        !e->mv8 || !e->inter || !e->imp)
+      return -1;
+  }
+  return 0;
+}
+
+/* ring entry of coded frame m (tests): its intra costs [h_imp][w_imp], 8x8
+ * lookahead MVs and inter costs [R][h_imp][w_imp], references; -1: absent */
+int orc_replay_la_data(orc_replay *r, long m, uint32_t *intra, orc_mv *mv8, uint32_t *inter,
+                       int32_t *ref_display) {
+  if (!r->imp_window || m < 1) return -1;
+  const ola *e = la_of(r, m);
+  if (e->coded != m) return -1;
+  const size_t ni = (size_t)r->w_imp * r->h_imp;
+  memcpy(intra, e->intra, ni * 4);
+  memcpy(mv8, e->mv8, ni * r->R * sizeof(orc_mv));
+  memcpy(inter, e->inter, ni * r->R * 4);
+  for (int k = 0; k < r->R; k++) ref_display[k] = e->fi.ref_display[k];
+  return 0;
+}
+
+/* frame n's importances (the window's, or the input's) for a caller */
+int orc_replay_get_importances(orc_replay *r, float *out, int n) {
+  if (n != r->w_imp * r->h_imp) return -1;
+  const float *imp = r->imp_window ? r->imp_own : r->imp;
+  if (imp)
+    memcpy(out, imp, (size_t)n * 4);
+  else
+    memset(out, 0, (size_t)n * 4);
+  return 0;
+}
+
 /* Code the next frame.  sb_limit > 0 runs only the first sb_limit
  * superblocks of both passes (a bounded sample for timing).  pad_recon = 0
  * leaves the padding to orc_replay_import (tile groups). */
@@ -2204,9 +2373,24 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
   const size_t nf = (size_t)r->R * r->tw * 16 * r->th * 16;
   memset(r->tmv_e, 0, nf * sizeof(orc_mv));
   memset(r->tmv_l, 0, nf * sizeof(orc_mv));
-  /* F1; the lookahead (its F2 and 16x16 searches, tile by tile) */
-  run_pass(r, 0);
-  run_pass(r, 6);
+  /* F1; the lookahead (its F2 and 16x16 searches, tile by tile) -- with
+   * an importance window, run W frames ahead and kept in the ring */
+  if (r->imp_window) {
+    la_fill(r);
+    const ola *e = la_of(r, r->coded);
+    if (e->coded != r->coded) return -1; /* the stream ended before this frame */
+    const size_t nr = (size_t)r->R * r->nsb;
+    memcpy(r->coarse, e->coarse, nr * sizeof(orc_mv));
+    memcpy(r->cc, e->cc, nr * 8);
+    memcpy(r->half_l, e->half_l, nr * 4 * sizeof(orc_mv));
+    memcpy(r->hlc, e->hlc, nr * 4 * 8);
+    memcpy(r->look, e->look, nr * 16 * sizeof(orc_mv));
+    memcpy(r->lc, e->lc, nr * 16 * 8);
+    importance_frame(r);
+  } else {
+    run_pass(r, 0);
+    run_pass(r, 6);
+  }
   if (r->exact) {
     /* speed 10: the levels' searches, then each tile in coding order (F2,
      * F3, F4, F6, F6b per superblock) */

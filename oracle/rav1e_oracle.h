@@ -175,6 +175,15 @@ void orc_propagate_importances(const void *org, ptrdiff_t org_stride, const void
                                const orc_mv *mvs, const uint32_t *intra_costs,
                                const float *importances, int n_unique,
                                float *ref_importances);
+void orc_propagate_importances_costs(int w_imp, int h_imp, const orc_mv *mvs,
+                                     const uint32_t *inter_costs, const uint32_t *intra_costs,
+                                     const float *importances, int n_unique,
+                                     float *ref_importances);
+void orc_importance_inter_costs(const void *org, ptrdiff_t org_stride, const void *ref,
+                                ptrdiff_t ref_stride, int w_imp, int h_imp, int hbd,
+                                const orc_mv *mvs, uint32_t *inter_costs);
+/* glibc's log2f restated (f32::log2 on x86-64 Linux), see orc_lookahead.c */
+float orc_log2f(float x);
 uint32_t orc_get_mv_rate(orc_mv a, orc_mv b, int allow_hp);
 /* full_search (src/me.rs:943-990). org/ref point at plane (0,0) (the data
  * origin); x/y in pixels relative to it; may be negative (padding). */

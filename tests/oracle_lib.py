@@ -508,7 +508,8 @@ class CpuReplay:
 
     def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, group=None,
                  tile_size=(0, 0), n_inputs=8, threads=1, L=None, quantizer=100, speed=10,
-                 deblock=False, cdef=False, intra=True, entropy=False, mvref_standin=False):
+                 deblock=False, cdef=False, intra=True, entropy=False, mvref_standin=False,
+                 imp_window=0, imp_limit=0):
         from rav1e_amd import rate as RT
         L = L or lib()
         self.L = L
@@ -559,6 +560,19 @@ class CpuReplay:
             assert L.orc_replay_set_level_params(
                 self.h, lv, d["base_q_idx"], I3(*d["dc_delta_q"]), I3(*d["ac_delta_q"]),
                 d["lambda"], d["me_lambda"], D3(*d["dist_scale"])) == 0
+        L.orc_replay_set_imp_window.argtypes = [C.c_void_p, C.c_int, C.c_long]
+        assert L.orc_replay_set_imp_window(self.h, imp_window, imp_limit) == 0, \
+            "orc_replay_set_imp_window"
+        self.imp_window = imp_window
+        self.imp_shape = ((height + 7) // 8, (width + 7) // 8)
+
+    def importances(self):
+        """The block importances the last coded frame's RDO used
+        ([h_imp][w_imp] f32; the window's, or the input's)."""
+        out = np.zeros(self.imp_shape, np.float32)
+        self.L.orc_replay_get_importances.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        assert self.L.orc_replay_get_importances(self.h, out.ctypes.data, out.size) == 0
+        return out
 
     def set_input(self, idx, yuv):
         yuv = np.ascontiguousarray(yuv)

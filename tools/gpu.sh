@@ -36,13 +36,14 @@ case "$MODE" in
     exec bash "$R/tools/gpu_step.sh" "${steps[@]}" ;;
   prof)
     CFG=${1:-2160p}; shift
-    B="python3 $R/bench.py --config $CFG --no-cpu-baseline --emulate-ranks 0 --steps 16 --warmup 5 $*"
+    B="python3 $R/bench.py --config $CFG --no-cpu-baseline --emulate-ranks 0 --steps 8 --warmup 3 $*"
     SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
     exec bash "$R/tools/gpu_step.sh" \
       "200 $TAG/trace.log cd /tmp && rocprofv3 --kernel-trace --stats -d $P/trace -o run -- $B" \
       "200 $TAG/fetch.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o run -- $B" \
       "200 $TAG/write.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $P/write -o run -- $B" \
-      "200 $TAG/sq.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $SQ -d $P/sq -o run -- $B" ;;
+      "200 $TAG/sq.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $SQ -d $P/sq -o run -- $B" \
+      "120 $TAG/gzip.log find $P -name '*.csv' -size +256k -exec gzip -9 {} +" ;;
   envbench)
     # one bench line per environment setting: envbench TAG CFG "A=1" "A=2 B=1" ... [-- ARGS]
     CFG=$1; shift
