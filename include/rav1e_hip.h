@@ -666,6 +666,23 @@ int rv_replay_get_recon(rv_replay *r, int display, void *host_yuv);
  * the RDO distortion (compute_distortion_bias, src/rdo.rs:476-508); NULL =
  * all zero (the default). */
 int rv_replay_set_importances(rv_replay *r, const float *host, int n);
+/* The importance window (rdo_lookahead_frames, src/api/config.rs:158;
+ * compute_block_importances, src/api/internal.rs:823-1081): window > 0 runs
+ * every frame's lookahead `window` coded frames ahead on a lookahead engine
+ * (its own host thread and stream) and biases each frame's RDO with the
+ * importances propagated over [n, n + window] (replaces
+ * rv_replay_set_importances); limit = the stream's length in coded frames
+ * (the window shrinks at its end; 0: unbounded).  The inputs of frame n +
+ * window must be in place when frame n is coded.  Before the first frame,
+ * on a primary instance replaying the whole frame as one group; a twin
+ * (rv_replay_create_twin) created afterwards shares the engine.  0 removes
+ * the window.  Replaces the reference's lookahead bookkeeping in
+ * ContextInner::compute_lookahead_data / receive_packet
+ * (src/api/internal.rs:767-823, 1116). */
+int rv_replay_set_imp_window(rv_replay *r, int window, long limit);
+/* The block importances (f32 [h_imp][w_imp]) the last coded frame's RDO
+ * used (zero without a window or input). */
+int rv_replay_get_importances(rv_replay *r, float *host, int n);
 /* Code the next frame of the stream (asynchronous on the replay's stream):
  * the key frame first, then the pyramid's coding order.  info may be NULL. */
 int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info);
@@ -736,7 +753,10 @@ int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,
  * intra rounds; with cap >= 17 (speed 10, since creation) out[14] the
  * MV-stack evaluation rounds, out[15] the superblocks they re-evaluated,
  * out[16] the frames; with cap >= 18, out[17] the round runs (1 + the MV /
- * intra passes of each frame).  Returns the count. */
+ * intra passes of each frame); with cap >= 20, out[18] the lookahead's
+ * EPZS rounds (round 0 included) and out[19] the jobs they re-ran (the
+ * engine's, on the primary, with an importance window).  Returns the
+ * count. */
 int rv_replay_counters(rv_replay *r, uint64_t *out, int cap);
 
 /* ---------------------------------------------------------------------

@@ -1,0 +1,53 @@
+// rv_impwin.h -- block importances over the lookahead window
+// (compute_block_importances, src/api/internal.rs:823-1081) for the replay's
+// lookahead engine (rv_replay.hip, RvLaEngine).
+//
+// The reference propagates, for every frame of the window from the last one
+// down to the second, each 8x8 block's share of (intra cost + its own
+// importance) into the four blocks of each reference its MV-displaced area
+// overlaps, with f32 `+=` in source raster order.  Where a source's
+// contributions land depends only on its lookahead MV, so the device
+// computes that once per frame (impwin_frame_data): a stable sort by target
+// turns the frame's 4 x n_imp (target, source) pairs into per-target lists
+// in source order (CSR).  A window pass (impwin_pass) is then one thread
+// per target that adds its list's contributions onto its current value in
+// that order -- the reference's sum, rounding for rounding, with no atomics.
+#pragma once
+
+#include "rv_device.h"
+
+namespace rv {
+
+// The importance data of one coded frame (a lookahead ring entry); every
+// array over the frame's 8x8 blocks [h_imp][w_imp] (n = w_imp * h_imp).
+struct ImpFrame {
+  uint32_t *intra = nullptr;  // lookahead_intra_costs [n]
+  rv_mv *mv8 = nullptr;       // [R][n]: lookahead_mvs[k][2y][2x] (the FL MV of the 16x16)
+  float *frac = nullptr;      // [R][n]: max(1 - inter / intra, 0) (inter: get_satd at mv8)
+  int32_t *off = nullptr;     // [R][n + 1]: target t's sources at src[off[t] .. off[t + 1])
+  int32_t *src = nullptr;     // [R][4 n]: 4 * source + corner, by target, in source order
+  float *imp = nullptr;       // [n]: block_importances while a window propagates
+  float *fin = nullptr;       // [n]: the frame's final importances (log2(1 + imp / intra))
+};
+
+size_t impwin_frame_bytes(int n, int R);        // one ImpFrame's arrays
+void impwin_frame_carve(ImpFrame &f, void *base, int n, int R);
+size_t impwin_scratch_bytes(int n);             // impwin_frame_data's sort scratch
+
+// Frame data of the coded frame whose luma input is `cur`: intra costs, the
+// 8x8 blocks' lookahead MVs from `look` ([R][nsb][16] of a whole-frame
+// superblock grid tw wide), their fractions against each reference's
+// original frame refs[k], and per reference the target lists.
+int impwin_frame_data(const rv_plane &cur, const rv_plane *refs, int R, int bit_depth,
+                      const rv_fs_result *look, int tw, int nsb, int w_imp, int h_imp,
+                      const ImpFrame &f, void *scratch, size_t scratch_bytes, hipStream_t st);
+
+// One (frame, reference k) pass: the source frame's contributions (split
+// over nu distinct references) added onto ref_imp.
+int impwin_pass(const ImpFrame &src, int k, int nu, int w_imp, int h_imp, float *ref_imp,
+                hipStream_t st);
+
+// The frame's final importances from its propagated ones.
+int impwin_final(const ImpFrame &f, int w_imp, int h_imp, hipStream_t st);
+
+}  // namespace rv

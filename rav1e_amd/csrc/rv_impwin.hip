@@ -1,0 +1,301 @@
+// rv_impwin.hip -- the lookahead window's block importances
+// (compute_block_importances, src/api/internal.rs:823-1081); see
+// rv_impwin.h for the decomposition.  f32 arithmetic in the reference's
+// operation order: products and sums round separately (-ffp-contract=off),
+// divisions are correctly rounded (__fdiv_rn), as in Rust.
+#include <hipcub/hipcub.hpp>
+
+#include "rv_impwin.h"
+
+namespace rv {
+
+namespace {
+
+constexpr int kImpB = 8, kMvUnits = 8, kBMv = kImpB * kMvUnits, kAreaMv = kBMv * kBMv;
+
+size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+int key_bits(uint32_t n) {  // keys are 0..n
+  int b = 1;
+  while (b < 32 && (n >> b) != 0) b++;
+  return b;
+}
+
+struct SortScratch {
+  size_t keys_in, vals_in, keys_out, temp, temp_bytes, total;
+};
+
+SortScratch sort_scratch(int n) {
+  SortScratch s;
+  const size_t m = 4 * (size_t)n;
+  s.keys_in = 0;
+  s.vals_in = al256(4 * m);
+  s.keys_out = al256(s.vals_in + 4 * m);
+  s.temp = al256(s.keys_out + 4 * m);
+  s.temp_bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, s.temp_bytes, (const uint32_t *)nullptr,
+                                           (uint32_t *)nullptr, (const int32_t *)nullptr,
+                                           (int32_t *)nullptr, (int)m, 0, key_bits((uint32_t)n));
+  s.total = al256(s.temp + s.temp_bytes);
+  return s;
+}
+
+// The four targets of a source block at (x, y) with lookahead MV mv (MV
+// units): target block index (n: off the frame) and area fraction, in the
+// order top-left, top-right, bottom-left, bottom-right (:967-1043).
+__device__ inline void corners(int x, int y, rv_mv mv, int w, int h, int tgt[4], float f[4]) {
+  const int64_t rx = (int64_t)x * kBMv + mv.col, ry = (int64_t)y * kBMv + mv.row;
+  // (reference_x - (BLOCK - 1 if negative)) / BLOCK * BLOCK: i64 `/` truncates
+  const int64_t tlx = (rx - (rx < 0 ? kBMv - 1 : 0)) / kBMv * kBMv;
+  const int64_t tly = (ry - (ry < 0 ? kBMv - 1 : 0)) / kBMv * kBMv;
+  const int64_t trx = tlx + kBMv, bly = tly + kBMv;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const int64_t tx = (c & 1) ? trx : tlx, ty = (c & 2) ? bly : tly;
+    const int64_t fx = (c & 1) ? rx + kBMv - trx : trx - rx;
+    const int64_t fy = (c & 2) ? ry + kBMv - bly : bly - ry;
+    f[c] = __fdiv_rn((float)(fx * fy), (float)kAreaMv);
+    const int64_t bx = tx / kBMv, by = ty / kBMv;
+    tgt[c] = bx >= 0 && by >= 0 && bx < w && by < h ? (int)(by * w + bx) : w * h;
+  }
+}
+
+template <typename Px>
+__device__ inline uint32_t satd8(const Px *o, int64_t os, const Px *r, int64_t rs, int base) {
+  int32_t d[64];
+#pragma unroll
+  for (int rr = 0; rr < 8; rr++)
+#pragma unroll
+    for (int cc = 0; cc < 8; cc++)
+      d[rr * 8 + cc] = (int32_t)o[rr * os + cc] - (r ? (int32_t)r[rr * rs + cc] : base);
+  return (uint32_t)((satd_chunk<8>(d) + 4) >> 3);  // get_satd 8x8: ln = msb(8)
+}
+
+// One thread per 8x8 block: lookahead_intra_costs (pred_dc_128, :680-765),
+// the lookahead MV of the 16x16 holding it, per reference get_satd against
+// the original reference block at that MV (:911-931) and the propagate
+// fraction (:939), and the (target, 4 * block + corner) sort pairs.
+struct DataArgs {
+  rv_plane cur, ref;
+  int k, base, w, h, tw, nsb;  // k: the reference (k = 0 also writes the intra costs)
+  const rv_fs_result *look;
+  ImpFrame f;
+  uint32_t *keys;  // [4 n]
+  int32_t *vals;   // [4 n]
+};
+
+template <typename Px>
+__global__ __launch_bounds__(256) void data_kernel(DataArgs a) {
+  const int n = a.w * a.h;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int x = i % a.w, y = i / a.w;
+  const Px *o = plane_ptr<Px>(a.cur, x * kImpB, y * kImpB);
+  const uint32_t intra = satd8<Px>(o, a.cur.stride, (const Px *)nullptr, 0, a.base);
+  if (a.k == 0) a.f.intra[i] = intra;
+  const int sb = (y / 8) * a.tw + x / 8, b = ((y % 8) / 2) * 4 + (x % 8) / 2;
+  {
+    const int k = a.k;
+    const rv_plane &ref = a.ref;
+    const rv_mv mv = a.look[((size_t)k * a.nsb + sb) * 16 + b].best_mv;
+    a.f.mv8[(size_t)k * n + i] = mv;
+    const int64_t px_x = ((int64_t)x * kBMv + mv.col) / kMvUnits;  // isize `/`
+    const int64_t px_y = ((int64_t)y * kBMv + mv.row) / kMvUnits;
+    // the reference block must lie inside the allocation (the reference's
+    // region would panic): the search windows keep it there
+    const bool inside = px_x >= -ref.xorigin && px_y >= -ref.yorigin &&
+                        px_x + kImpB <= ref.stride - ref.xorigin &&
+                        px_y + kImpB <= ref.alloc_height - ref.yorigin;
+    float frac = 0.f;
+    if (inside) {
+      const float inter = (float)satd8<Px>(o, a.cur.stride, plane_ptr<Px>(ref, (int)px_x, (int)px_y),
+                                           ref.stride, 0);
+      // f32::max(NaN, 0) = 0, as fmaxf
+      frac = fmaxf(1.0f - __fdiv_rn(inter, (float)intra), 0.0f);
+    }
+    a.f.frac[(size_t)k * n + i] = frac;
+    int tgt[4];
+    float fr[4];
+    corners(x, y, mv, a.w, a.h, tgt, fr);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const size_t j = 4 * (size_t)i + c;
+      a.keys[j] = inside ? (uint32_t)tgt[c] : (uint32_t)n;
+      a.vals[j] = 4 * i + c;
+    }
+  }
+}
+
+// off[t] = the first sorted position whose key is >= t (t = 0 .. n)
+__global__ __launch_bounds__(256) void offsets_kernel(const uint32_t *keys, int m, int n,
+                                                      int32_t *off) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t > n) return;
+  int lo = 0, hi = m;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (keys[mid] < (uint32_t)t)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  off[t] = lo;
+}
+
+// One window pass: target t of the reference frame adds its sources'
+// contributions in source order (:936-963).
+__global__ __launch_bounds__(256) void pass_kernel(const uint32_t *intra, const rv_mv *mv8,
+                                                   const float *frac, const float *imp,
+                                                   const int32_t *off, const int32_t *src, int nu,
+                                                   int w, int h, float *ref_imp) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= w * h) return;
+  const int j0 = off[t], j1 = off[t + 1];
+  if (j0 == j1) return;
+  float acc = ref_imp[t];
+  for (int j = j0; j < j1; j++) {
+    const int e = src[j], s = e >> 2, c = e & 3;
+    const float ic = (float)intra[s];
+    const float amount = __fdiv_rn((ic + imp[s]) * frac[s], (float)nu);
+    int tgt[4];
+    float fr[4];
+    corners(s % w, s / w, mv8[s], w, h, tgt, fr);
+    acc = acc + amount * fr[c];
+  }
+  ref_imp[t] = acc;
+}
+
+// f32::log2 as the reference gets it on x86-64 Linux: glibc's log2f
+// (sysdeps/ieee754/flt-32/e_log2f.c, its published algorithm, the FMA
+// build), restated in oracle/orc_lookahead.c orc_log2f and pinned there
+// against the host's log2f over every float in [1, 2) and a stride of the
+// rest.  x >= 1 here (1 + importance / intra cost); +inf passes through.
+__constant__ double kLog2fT[16][2] = {
+    {0x1.661ec79f8f3bep+0, -0x1.efec65b963019p-2}, {0x1.571ed4aaf883dp+0, -0x1.b0b6832d4fca4p-2},
+    {0x1.49539f0f010b0p+0, -0x1.7418b0a1fb77bp-2}, {0x1.3c995b0b80385p+0, -0x1.39de91a6dcf7bp-2},
+    {0x1.30d190c8864a5p+0, -0x1.01d9bf3f2b631p-2}, {0x1.25e227b0b8ea0p+0, -0x1.97c1d1b3b7af0p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.2f9e393af3c9fp-3}, {0x1.12358f08ae5bap+0, -0x1.960cbbf788d5cp-4},
+    {0x1.0953f419900a7p+0, -0x1.a6f9db6475fcep-5}, {0x1.0000000000000p+0, 0x0.0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.338ca9f24f53dp-4}, {0x1.ca4b31f026aa0p-1, 0x1.476a9543891bap-3},
+    {0x1.b2036576afce6p-1, 0x1.e840b4ac4e4d2p-3}, {0x1.9c2d163a1aa2dp-1, 0x1.40645f0c6651cp-2},
+    {0x1.886e6037841edp-1, 0x1.88e9c2c1b9ff8p-2}, {0x1.767dcf5534862p-1, 0x1.ce0a44eb17bccp-2}};
+__constant__ double kLog2fA[4] = {-0x1.712b6f70a7e4dp-2, 0x1.ecabf496832e0p-2,
+                                  -0x1.715479ffae3dep-1, 0x1.715475f35c8b8p+0};
+
+__device__ inline float log2f_ref(float x) {
+  const uint32_t ix = __float_as_uint(x);
+  if (ix == 0x3f800000u) return 0.0f;
+  if (ix >= 0x7f800000u) return x;  // +inf / NaN
+  const uint32_t tmp = ix - 0x3f330000u;
+  const int i = (int)((tmp >> 19) % 16);
+  const uint32_t iz = ix - (tmp & 0xff800000u);
+  const int k = (int32_t)tmp >> 23;
+  const double z = (double)__uint_as_float(iz), invc = kLog2fT[i][0], logc = kLog2fT[i][1];
+  const double r = fma(z, invc, -1.0);
+  const double y0 = logc + (double)k, r2 = r * r;
+  double y = fma(kLog2fA[1], r, kLog2fA[2]);
+  y = fma(kLog2fA[0], r2, y);
+  const double p = fma(kLog2fA[3], r, y0);
+  return (float)fma(y, r2, p);
+}
+
+// :1052-1070: log2(1 + importance / intra cost), 0 where the intra cost is 0
+__global__ __launch_bounds__(256) void final_kernel(const uint32_t *intra, const float *imp, int n,
+                                                    float *fin) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  const float ic = (float)intra[t];
+  fin[t] = ic > 0.f ? log2f_ref(1.0f + __fdiv_rn(imp[t], ic)) : 0.f;
+}
+
+}  // namespace
+
+size_t impwin_frame_bytes(int n, int R) {
+  return al256((size_t)n * 4) + al256((size_t)R * n * sizeof(rv_mv)) + al256((size_t)R * n * 4) +
+         al256((size_t)R * (n + 1) * 4) + al256((size_t)R * 4 * n * 4) + 2 * al256((size_t)n * 4);
+}
+
+void impwin_frame_carve(ImpFrame &f, void *base, int n, int R) {
+  uint8_t *m = (uint8_t *)base;
+  f.intra = (uint32_t *)m;
+  m += al256((size_t)n * 4);
+  f.mv8 = (rv_mv *)m;
+  m += al256((size_t)R * n * sizeof(rv_mv));
+  f.frac = (float *)m;
+  m += al256((size_t)R * n * 4);
+  f.off = (int32_t *)m;
+  m += al256((size_t)R * (n + 1) * 4);
+  f.src = (int32_t *)m;
+  m += al256((size_t)R * 4 * n * 4);
+  f.imp = (float *)m;
+  m += al256((size_t)n * 4);
+  f.fin = (float *)m;
+}
+
+size_t impwin_scratch_bytes(int n) { return sort_scratch(n).total; }
+
+int impwin_frame_data(const rv_plane &cur, const rv_plane *refs, int R, int bit_depth,
+                      const rv_fs_result *look, int tw, int nsb, int w_imp, int h_imp,
+                      const ImpFrame &f, void *scratch, size_t scratch_bytes, hipStream_t st) {
+  const int n = w_imp * h_imp;
+  if (R < 1 || R > 2 || n <= 0 || cur.xorigin + w_imp * 8 > cur.stride ||
+      cur.yorigin + h_imp * 8 > cur.alloc_height)
+    return rv_set_error(RV_EINVAL, "impwin_frame_data: bad geometry");
+  const SortScratch s = sort_scratch(n);
+  if (!scratch || scratch_bytes < s.total)
+    return rv_set_error(RV_EINVAL, "impwin_frame_data: scratch");
+  uint8_t *base = (uint8_t *)scratch;
+  DataArgs a;
+  a.cur = cur;
+  a.base = 128 << (bit_depth - 8);
+  a.w = w_imp;
+  a.h = h_imp;
+  a.tw = tw;
+  a.nsb = nsb;
+  a.look = look;
+  a.f = f;
+  a.keys = (uint32_t *)(base + s.keys_in);
+  a.vals = (int32_t *)(base + s.vals_in);
+  uint32_t *keys_out = (uint32_t *)(base + s.keys_out);
+  const int m = 4 * n;
+  const unsigned nb = (unsigned)((n + 255) / 256);
+  for (int k = 0; k < R; k++) {
+    a.k = k;
+    a.ref = refs[k];
+    if (cur.hbd)
+      data_kernel<uint16_t><<<nb, 256, 0, st>>>(a);
+    else
+      data_kernel<uint8_t><<<nb, 256, 0, st>>>(a);
+    RV_HIP_CHECK_LAUNCH();
+    // stable: a target's sources stay in raster order (the reference's order)
+    size_t tb = s.temp_bytes;
+    if (hipcub::DeviceRadixSort::SortPairs(base + s.temp, tb, a.keys, keys_out, a.vals,
+                                           f.src + (size_t)k * m, m, 0,
+                                           key_bits((uint32_t)n), st) != hipSuccess)
+      return rv_set_error(RV_EHIP, "impwin_frame_data: sort");
+    offsets_kernel<<<(unsigned)((n + 1 + 255) / 256), 256, 0, st>>>(keys_out, m, n,
+                                                                    f.off + (size_t)k * (n + 1));
+    RV_HIP_CHECK_LAUNCH();
+  }
+  return RV_OK;
+}
+
+int impwin_pass(const ImpFrame &src, int k, int nu, int w_imp, int h_imp, float *ref_imp,
+                hipStream_t st) {
+  const int n = w_imp * h_imp;
+  if (nu < 1 || nu > 3 || n <= 0) return rv_set_error(RV_EINVAL, "impwin_pass: bad arguments");
+  pass_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
+      src.intra, src.mv8 + (size_t)k * n, src.frac + (size_t)k * n, src.imp,
+      src.off + (size_t)k * (n + 1), src.src + (size_t)k * 4 * n, nu, w_imp, h_imp, ref_imp);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+int impwin_final(const ImpFrame &f, int w_imp, int h_imp, hipStream_t st) {
+  const int n = w_imp * h_imp;
+  final_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(f.intra, f.imp, n, f.fin);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+}  // namespace rv

@@ -46,7 +46,9 @@
 #include "rv_intra.h"
 #include "rv_intra_pass.h"
 #include "rv_mvref.h"
+#include "rv_impwin.h"
 #include "rv_rdo.h"
+#include <string>
 
 #if __has_include(<rccl/rccl.h>)
 #include <rccl/rccl.h>
@@ -799,15 +801,20 @@ __global__ void coeff_checksum_list(const int32_t *packed, const int32_t *list,
 
 using namespace rv;
 
-struct RvSlot {  // one frame of the DPB: reconstruction + input pyramid
-  rv_plane y, u, v, hres, qres;
-  uint32_t *qres_box = nullptr;  // rv_plane_box_sums of qres (the SEA coarse search)
+struct RvSlot {  // one frame of the DPB: the reconstruction and its motion field
+  rv_plane y, u, v;
   // the frame's motion field (frame_mvs: the encode's tile field when the
   // frame was coded; zero for the key frame), 8x8 cells [h_in_b/2][w_in_b/2][R]
   rv_mv *fmv = nullptr;
 };
 struct RvInput {
   rv_plane y, u, v;
+  // input_hres / input_qres (FrameState, src/encoder.rs:362-377: downsample
+  // + pad): the half / quarter resolution planes the searches of this frame
+  // and of every frame referencing it read; F0 of the frame (or the
+  // lookahead running ahead) writes them
+  rv_plane hres, qres;
+  uint32_t *qres_box = nullptr;  // rv_plane_box_sums of qres (the SEA coarse search)
 };
 
 // The host side of stage F8 (RV_REPLAY_ENTROPY): a thread that range-codes
@@ -894,6 +901,77 @@ struct EcHost {
     std::unique_lock<std::mutex> lk(mu);
     cv.wait(lk, [&] { return done == queued; });
   }
+};
+
+// The counts of one chain of round checks (the lookahead's EPZS rounds, the
+// MV-stack rounds): check q counts into the device slot q % kCnt and
+// publishes (q << 32 | count) into the host-mapped ring at q % kPub
+// (round_publish), where the host reads it without a stream sync.  One
+// ring per host thread that runs round loops.
+struct RoundRing {
+  static constexpr int kCnt = 64, kPub = 64;
+  int32_t *cnt = nullptr;  // [kCnt][2], then the ticket
+  uint32_t *ticket = nullptr;
+  unsigned long long *h_pub = nullptr, *d_pub = nullptr;
+  uint32_t seq = 0;
+  int32_t *slot(uint32_t q) const { return cnt + 2 * (q % kCnt); }
+  // check q's publication (publish = false: counted, not published)
+  RoundPub pub(uint32_t q, bool publish = true) const {
+    return RoundPub{slot(q), slot(q + 1), ticket, publish ? d_pub + q % kPub : nullptr, q};
+  }
+};
+
+// Where a frame's lookahead writes (compute_lookahead_motion_vectors):
+// F1 [R][nsb], F2L [R][nsb][4], FL [R][nsb][16]
+struct LaOut {
+  rv_fs_result *coarse = nullptr, *half_l = nullptr, *look = nullptr;
+};
+
+// The lookahead engine of an importance window W (rdo_lookahead_frames,
+// src/api/config.rs:158; rv_replay_set_imp_window).  rav1e computes every
+// frame's lookahead as the frame arrives, far ahead of its encode
+// (compute_lookahead_data, src/api/internal.rs:767-820), and before coding
+// output frame n propagates block importances over the window [n, n + W]
+// (compute_block_importances, :823-1081).  Here a host thread of its own
+// runs, on its own stream and round ring, the lookahead of coded frame m
+// (F0 pyramids, F1, F2L, FL with their EPZS rounds, then the importance
+// data of rv_impwin.h) into ring entry m % RW, and as soon as frame n + W is
+// in, the window propagation for frame n.  The encode of frame n waits for
+// that (a host flag, then a stream event), takes its lookahead results and
+// final importances from the entry, and marks the entry used when the frame
+// is done; the engine reuses entry m % RW for frame m + RW only after that.
+// RW = W + 1 + kLaSlack: the slack covers the frames a twin instance still
+// has in flight behind the primary.
+struct RvLaEngine {
+  static constexpr int kLaSlack = 12;
+  int W = 0, RW = 0, dev = 0;
+  long limit = 0;  // coded frames in the stream (0: unbounded)
+  hipStream_t las = nullptr;
+  RoundRing rr;
+  int32_t *la_list = nullptr;
+  void *scratch = nullptr;
+  size_t scratch_bytes = 0;
+  struct Entry {
+    LaOut o;
+    ImpFrame f;
+    long m = -1;       // the coded frame the entry holds
+    long used_by = -1; // host: the frame whose encode recorded ev_used
+    rv_replay_frame_info fi{};
+    hipEvent_t ev_imp = nullptr, ev_used = nullptr;
+  };
+  std::vector<Entry> ring;
+  std::vector<long> pyr_display;  // per input: the display whose pyramid it holds
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  long requested = 0;  // the highest frame an encode has asked for (0: none yet)
+  long imp_ready = 0;  // the importances of frames <= imp_ready are recorded
+  long imp_next = 1;
+  bool stop = false;
+  int err = 0;
+  std::string msg;
+  long la_round_sum = 0, la_reeval = 0;
+  Entry &at(long m) { return ring[(size_t)(m % RW)]; }
 };
 
 struct rv_replay {
@@ -987,14 +1065,10 @@ struct rv_replay {
   MvStack *stk = nullptr;              // the stacks each superblock was evaluated with
   BlkDec *dec_lv[3] = {nullptr, nullptr, nullptr};  // decisions, per pyramid level
   uint8_t *mv_active = nullptr;        // re-evaluate this round
-  // the checks' counts: device ring (slot q % kCntRing for check q) and
-  // the host-mapped publication ring (seq << 32 | count, slot q % kPubRing)
-  static constexpr int kCntRing = 64, kPubRing = 64;
+  // the round checks' counts (this instance's host thread)
   static constexpr int kRoundsAhead = 2;  // rounds queued beyond the last count read
-  int32_t *mv_cnt = nullptr, *mv_list = nullptr;
-  uint32_t *mv_ticket = nullptr;
-  unsigned long long *h_pub = nullptr, *d_pub = nullptr;
-  uint32_t mv_seq = 0;
+  RoundRing rr;
+  int32_t *mv_list = nullptr;
   bool edge_tr = false;                // a stack reads a frame-edge leaf (top-right)
   // RAV1E_HIP_MV_HP=1: the rounds after the first on a high-priority stream
   hipStream_t hp = nullptr;
@@ -1015,6 +1089,9 @@ struct rv_replay {
   rv_ds_job *jobs_half_l[3] = {nullptr, nullptr, nullptr};  // the lookahead's F2 (per level)
   int32_t *la_list = nullptr;  // the lookahead rounds' marked jobs: F2 [R nsb 4], then FL [R nsb 16]
   long la_round_sum = 0, la_reeval = 0;  // the lookahead rounds (round 0 included), re-evaluated jobs
+  RvLaEngine *eng = nullptr;  // the importance window's lookahead engine (null: W = 0)
+  bool eng_owned = false;     // the primary owns it; a twin borrows it
+  const float *imp_last = nullptr;  // the importances the last coded frame used
   int32_t *src_half = nullptr, *src_full = nullptr, *src_look = nullptr;  // predictor sources
   uint64_t *l_out, *c_out;  // F4: [skip dist, non-skip dist, rate] per transform block
   RdoWinner *win;
@@ -1071,32 +1148,46 @@ size_t frame_planes(const Geo &g, rv_plane &y, rv_plane &u, rv_plane &v) {
 }
 size_t plane_bytes(const rv_plane &p) { return (size_t)p.stride * p.alloc_height * (p.hbd ? 2 : 1); }
 
-bool alloc_input(rv_replay *r, RvInput &in) {
-  frame_planes(r->g, in.y, in.u, in.v);
+bool alloc_input(rv_replay *r, RvInput &in, bool pyramid) {
+  const Geo &g = r->g;
+  frame_planes(g, in.y, in.u, in.v);
+  const int pad = 88;
+  rv_plane_geometry(&in.hres, g.W / 2, g.H / 2, 1, 1, pad / 2, pad / 2, g.hbd);
+  rv_plane_geometry(&in.qres, g.W / 4, g.H / 4, 2, 2, pad / 4, pad / 4, g.hbd);
+  in.hres.bit_depth = in.qres.bit_depth = g.bd;
+  const size_t al = 256;
+  auto up = [&](size_t v) { return (v + al - 1) / al * al; };
   const size_t by = plane_bytes(in.y), bu = plane_bytes(in.u);
-  uint8_t *m = (uint8_t *)dalloc(r, by + 2 * bu);
+  const size_t bh = pyramid ? plane_bytes(in.hres) : 0, bq = pyramid ? plane_bytes(in.qres) : 0;
+  const size_t bs8 = pyramid ? (size_t)in.qres.stride * in.qres.alloc_height * 8 : 0;
+  const size_t total = up(by) + 2 * up(bu) + up(bh) + up(bq) + up(bs8);
+  uint8_t *m = (uint8_t *)dalloc(r, total);
   if (!m) return false;
+  uint8_t *m0 = m;
   in.y.data = m;
-  in.u.data = m + by;
-  in.v.data = m + by + bu;
-  return hipMemsetAsync(m, 0, by + 2 * bu, r->stream) == hipSuccess;
+  m += up(by);
+  in.u.data = m;
+  m += up(bu);
+  in.v.data = m;
+  m += up(bu);
+  if (pyramid) {
+    in.hres.data = m;
+    m += up(bh);
+    in.qres.data = m;
+    m += up(bq);
+    in.qres_box = (uint32_t *)m;
+  }
+  return hipMemsetAsync(m0, 0, total, r->stream) == hipSuccess;
 }
 
 bool alloc_slot(rv_replay *r, RvSlot &s) {
   const Geo &g = r->g;
   frame_planes(g, s.y, s.u, s.v);
-  const int pad = 88;
-  // input_hres / input_qres (src/encoder.rs:362-377)
-  rv_plane_geometry(&s.hres, g.W / 2, g.H / 2, 1, 1, pad / 2, pad / 2, g.hbd);
-  rv_plane_geometry(&s.qres, g.W / 4, g.H / 4, 2, 2, pad / 4, pad / 4, g.hbd);
-  s.hres.bit_depth = s.qres.bit_depth = g.bd;
   const size_t al = 256;
   auto up = [&](size_t v) { return (v + al - 1) / al * al; };
-  const size_t by = plane_bytes(s.y), bu = plane_bytes(s.u), bh = plane_bytes(s.hres),
-               bq = plane_bytes(s.qres);
-  const size_t bs8 = (size_t)s.qres.stride * s.qres.alloc_height * 8;
+  const size_t by = plane_bytes(s.y), bu = plane_bytes(s.u);
   const size_t bf = (size_t)(g.w_in_b / 2) * (g.h_in_b / 2) * g.R * sizeof(rv_mv);
-  const size_t total = up(by) + 2 * up(bu) + up(bh) + up(bq) + up(bs8) + up(bf);
+  const size_t total = up(by) + 2 * up(bu) + up(bf);
   uint8_t *m = (uint8_t *)dalloc(r, total);
   if (!m) return false;
   s.y.data = m;
@@ -1105,14 +1196,21 @@ bool alloc_slot(rv_replay *r, RvSlot &s) {
   m += up(bu);
   s.v.data = m;
   m += up(bu);
-  s.hres.data = m;
-  m += up(bh);
-  s.qres.data = m;
-  m += up(bq);
-  s.qres_box = (uint32_t *)m;
-  m += up(bs8);
   s.fmv = (rv_mv *)m;
   return hipMemsetAsync(s.y.data, 0, total, r->stream) == hipSuccess;
+}
+
+bool round_ring_alloc(rv_replay *r, RoundRing &q, hipStream_t st) {
+  const size_t b = RoundRing::kCnt * 8 + 4;
+  q.cnt = (int32_t *)dalloc(r, b);
+  if (!q.cnt || hipMemsetAsync(q.cnt, 0, b, st) != hipSuccess) return false;
+  q.ticket = (uint32_t *)(q.cnt + 2 * RoundRing::kCnt);
+  if (hipHostMalloc((void **)&q.h_pub, RoundRing::kPub * 8,
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&q.d_pub, q.h_pub, 0) != hipSuccess)
+    return false;
+  for (int i = 0; i < RoundRing::kPub; i++) q.h_pub[i] = ~0ull;
+  return true;
 }
 
 int build_static_jobs(rv_replay *r) {
@@ -1617,8 +1715,11 @@ static int intra_pass(rv_replay *r, const RdoArgs &la, const RdoArgs &ca, const 
 
 extern "C" {
 
+static void la_engine_destroy(rv_replay *r);
+
 void rv_replay_destroy(rv_replay *r) {
   if (!r) return;
+  la_engine_destroy(r);  // its thread first: it launches on the replay's arrays
   // both streams drain before anything they may still read is freed (an
   // error return between the lookahead's fork and its join leaves the side
   // stream running)
@@ -1647,7 +1748,7 @@ void rv_replay_destroy(rv_replay *r) {
     if (es) (void)hipStreamSynchronize(es);
   for (void *p : r->allocs) (void)hipFree(p);
   if (r->h_cnt) (void)hipHostFree(r->h_cnt);
-  if (r->h_pub) (void)hipHostFree(r->h_pub);
+  if (r->rr.h_pub) (void)hipHostFree(r->rr.h_pub);
   for (int f = 0; f < rv_replay::kRing; f++)
     for (int i = 0; i < rv_replay::kEv; i++)
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
@@ -1740,7 +1841,7 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     r->slots.resize(kSlots);
     for (auto &s : r->slots) ok = ok && alloc_slot(r, s);
     r->inputs.resize(cfg->n_inputs);
-    for (auto &in : r->inputs) ok = ok && alloc_input(r, in);
+    for (auto &in : r->inputs) ok = ok && alloc_input(r, in, true);
   }
   r->ntx_c = (g.cw / 32) * (g.ch / 32);
   const int nr = g.nsb * g.R;
@@ -1899,15 +2000,7 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
   // the rounds' counts (the lookahead's EPZS rounds at every speed, the MV-
   // stack rounds at speed 10): a device ring of count pairs + the ticket, the
   // host-mapped publication ring
-  r->mv_cnt = (int32_t *)dalloc(r, rv_replay::kCntRing * 8 + 4);
-  r->mv_ticket = r->mv_cnt ? (uint32_t *)(r->mv_cnt + 2 * rv_replay::kCntRing) : nullptr;
-  if (r->mv_cnt) (void)hipMemsetAsync(r->mv_cnt, 0, rv_replay::kCntRing * 8 + 4, r->stream);
-  ok = ok && r->mv_cnt &&
-       hipHostMalloc((void **)&r->h_pub, rv_replay::kPubRing * 8,
-                     hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
-       hipHostGetDevicePointer((void **)&r->d_pub, r->h_pub, 0) == hipSuccess;
-  if (r->h_pub)
-    for (int i = 0; i < rv_replay::kPubRing; i++) r->h_pub[i] = ~0ull;
+  ok = ok && round_ring_alloc(r, r->rr, r->stream);
   // speed 10: rav1e's MV stacks in coding-order rounds
   r->exact = !r->s6 && !(cfg->flags & RV_REPLAY_MVREF_STANDIN);
   if (r->exact) {
@@ -1955,7 +2048,7 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     r->cdef_dir = (uint8_t *)dalloc(r, n8);
     r->cdef_var = (int32_t *)dalloc(r, n8 * 4);
     r->cdef_idx = (uint8_t *)dalloc(r, n64);
-    ok = ok && r->cdef_dir && r->cdef_var && r->cdef_idx && alloc_input(r, r->cdef_pre);
+    ok = ok && r->cdef_dir && r->cdef_var && r->cdef_idx && alloc_input(r, r->cdef_pre, false);
     if (r->cdef_idx) (void)hipMemsetAsync(r->cdef_idx, 0, n64, r->stream);
   }
   r->entropy = (cfg->flags & RV_REPLAY_ENTROPY) != 0;
@@ -2098,6 +2191,7 @@ rv_replay *rv_replay_create_twin(rv_replay *primary, void *stream) {
     r->cdef_str[l][1] = primary->cdef_str[l][1];
   }
   r->imp = primary->imp;  // owned by the primary
+  r->eng = primary->eng;  // so is the importance window's engine
   r->coded = primary->coded;
   return r;
 }
@@ -2293,6 +2387,377 @@ int rv_replay_import(rv_replay *r) {
   return pad_slot(r, s);
 }
 
+// The host side of a round loop: check(q) queues check q, which lists the
+// jobs to re-run and publishes their count into the ring; eval(q) queues the
+// round that re-runs check q's list.  The host keeps kRoundsAhead rounds
+// queued beyond the last count it has read (it spins on the published
+// counts, no stream synchronisation), so the GPU never waits on the host;
+// the loop ends at the first check that lists nothing (the rounds queued
+// after it find empty lists).  budget: the chain's depth bound (see the
+// callers); a check still listing jobs after it is an internal error.
+}  // extern "C"
+
+template <typename Check, typename Eval>
+static int run_rounds(RoundRing &rr, hipStream_t xs, int budget, Check &&check, Eval &&eval,
+               long *nrounds, long *nre, bool *changed, const char *what, long frame, int level) {
+  static const bool mv_trace = getenv("RAV1E_HIP_MV_TRACE") != nullptr;
+  if (changed) *changed = false;
+  const uint32_t first = rr.seq++;
+  RV_R(check(first));
+  int queued = 0;  // evaluation rounds queued (round j evaluates check j - 1's list)
+  for (int seen = 0;; seen++) {
+    while (queued < budget && queued < seen + rv_replay::kRoundsAhead) {
+      RV_R(eval(first + (uint32_t)queued));
+      RV_R(check(rr.seq++));
+      queued++;
+    }
+    const uint32_t q = first + (uint32_t)seen;
+    volatile unsigned long long *pub = rr.h_pub + q % RoundRing::kPub;
+    const auto t0 = std::chrono::steady_clock::now();
+    unsigned long long v;
+    for (long spin = 0;; spin++) {
+      v = *pub;
+      if ((uint32_t)(v >> 32) == q) break;
+      if ((spin & 1023) == 1023) {
+        const hipError_t he = hipStreamQuery(xs);
+        if (he != hipSuccess && he != hipErrorNotReady)
+          return rv_set_error(RV_EHIP, "rv_replay_frame: a round failed");
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
+          return rv_set_error(RV_EHIP, "rv_replay_frame: a round's count never arrived");
+        std::this_thread::yield();
+      }
+    }
+    const int c = (int)(uint32_t)v;
+    if (mv_trace) fprintf(stderr, "%s frame %ld level %d check %d: %d\n", what, frame, level, seen, c);
+    if (c == 0) return RV_OK;
+    if (seen >= budget)
+      return rv_set_error(RV_EHIP, "rv_replay_frame: rounds beyond the chain's dependency "
+                                   "depth (internal error)");
+    *nre += c;
+    (*nrounds)++;
+    if (changed) *changed = true;
+  }
+}
+
+extern "C" {
+
+// The lookahead of coded frame fi (compute_lookahead_motion_vectors,
+// src/api/internal.rs:514-622) on stream xs: F0 the input's hres / qres
+// (pyramid: false when they are already current), F1 build_coarse_pmvs,
+// then F2L + FL (build_half_res_pmvs / build_full_res_pmvs) with their EPZS
+// sets (la_check_kernel): round 0 stores every F2L set (the field guessed
+// from o's previous contents) and runs every F2L search, then the same for
+// FL; then the rounds.  Budget: a quadrant search reads the quadrants of
+// the superblocks left of and above it, so it settles by round tws + ths - 1;
+// a 16x16 search reads its coarse / quadrant predictors (settled by then)
+// and the 16x16 blocks left of and above it, so it settles 4 tws + 4 ths - 2
+// rounds later.  e: the frame's timing events (null: untimed).
+static int lookahead_frame(rv_replay *r, RoundRing &rr, hipStream_t xs,
+                           const rv_replay_frame_info &fi, long frame, const LaOut &o,
+                           int32_t *la_list, bool pyramid, long *nrounds, long *nre, hipEvent_t *e) {
+  const Geo &g = r->g;
+  const int lv = fi.level, nr = g.nsb;
+  const RvInput &cur = r->inputs[fi.display % r->inputs.size()];
+  rv_plane refs_h[RV_MAX_REFS], refs_q[RV_MAX_REFS], refs_o[RV_MAX_REFS];
+  const uint32_t *box[RV_MAX_REFS];
+  for (int k = 0; k < g.R; k++) {
+    const RvInput &ri = r->inputs[fi.ref_display[k] % r->inputs.size()];
+    refs_h[k] = ri.hres;
+    refs_q[k] = ri.qres;
+    refs_o[k] = ri.y;  // the lookahead searches the references' original frames
+    box[k] = ri.qres_box;
+  }
+  auto ev = [&](int i) -> int {
+    if (e) RV_H(hipEventRecord(e[i], xs));
+    return RV_OK;
+  };
+  if (pyramid) {  // F0 (encode_frame, src/encoder.rs:3382-3385)
+    RV_R(rv_plane_pyramid(&cur.y, &cur.hres, &cur.qres, xs));
+    if (r->sea) RV_R(rv_plane_box_sums(&cur.qres, cur.qres_box, xs));
+  }
+  RV_R(ev(1));
+  // F1 coarse full search (build_coarse_pmvs), every reference in one launch
+  RV_R(rv_full_search_multi(&cur.qres, refs_q, g.R, r->fs_jobs[lv], nr, 16, 16, 1, 0, o.coarse,
+                            nullptr, r->sea ? box : nullptr, xs));
+  RV_R(ev(2));
+  LaArgs la_a;
+  memset(&la_a, 0, sizeof(la_a));
+  la_a.g = g;
+  la_a.eg = EpzsGeo{g.tx0, g.ty0, g.tw, g.th, g.tws, g.ths, g.W, g.H, g.w_in_b, g.h_in_b};
+  la_a.jh = r->jobs_half_l[lv];
+  la_a.jl = r->jobs_look[lv];
+  la_a.sl = r->src_look;
+  la_a.coarse = o.coarse;
+  la_a.half_l = o.half_l;
+  la_a.look = o.look;
+  const int nh = nr * g.R * 4, nl = nr * g.R * 16;
+  la_a.list_h = la_list;
+  la_a.list_l = la_list + nh;
+  auto la_launch = [&](int what, uint32_t q, bool init) -> int {
+    la_a.what = what;
+    la_a.init = init ? 1 : 0;
+    la_a.pub = rr.pub(q, !init);
+    const int n = ((what & 1) ? nh : 0) + ((what & 2) ? nl : 0);
+    la_check_kernel<<<(n + 255) / 256, 256, 0, xs>>>(la_a);
+    RV_H(hipGetLastError());
+    return RV_OK;
+  };
+  auto f2l = [&](const int32_t *list, const int32_t *cnt) {
+    return rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half_l[lv], nr * 4, 16, 16, 0,
+                                   0, 0, g.bd, o.half_l, nullptr, nullptr, xs, nullptr, list, cnt,
+                                   0);
+  };
+  auto fl = [&](const int32_t *list, const int32_t *cnt) {
+    return rv_diamond_search_multi(&cur.y, refs_o, g.R, r->jobs_look[lv], nr * 16, 16, 16, 0, 0, 0,
+                                   g.bd, o.look, nullptr, nullptr, xs, nullptr, list, cnt, 0);
+  };
+  RV_R(la_launch(1, 0, true));
+  RV_R(f2l(nullptr, nullptr));
+  RV_R(ev(3));
+  RV_R(ev(rv_replay::kStageEv));
+  RV_R(la_launch(2, 0, true));
+  RV_R(fl(nullptr, nullptr));
+  (*nrounds)++;
+  RV_R(run_rounds(
+      rr, xs, 5 * (g.tws + g.ths), [&](uint32_t q) { return la_launch(3, q, false); },
+      [&](uint32_t q) -> int {
+        RV_R(f2l(la_list, rr.slot(q)));
+        return fl(la_list + nh, rr.slot(q) + 1);
+      },
+      nrounds, nre, nullptr, "lookahead", frame, lv));
+  RV_R(ev(rv_replay::kStageEv + 1));
+  return RV_OK;
+}
+
+// the coded index of display d (frame_info's inverse)
+static long coded_of_display(long d) {
+  if (d == 0) return 0;
+  static const int jof[4] = {0, 2, 1, 3}, off[4] = {4, 2, 1, 3};
+  const int j = jof[d % 4];
+  return 4 * ((d - off[j]) / 4) + j + 1;
+}
+
+// One step of the engine: coded frame m's lookahead and importance data
+// into its entry, then the window propagation of every frame whose window
+// is now complete (n + W = m, or the stream's last frame).
+static int la_step(rv_replay *r, long m) {
+  RvLaEngine &E = *r->eng;
+  const Geo &g = r->g;
+  hipStream_t xs = E.las;
+  RvLaEngine::Entry &e = E.at(m);
+  if (m - E.RW >= 1) RV_H(hipStreamWaitEvent(xs, e.ev_used, 0));  // frame m - RW is done with it
+  rv_replay_frame_info fi;
+  frame_info(m, g.R, &fi);
+  // the pyramids of the frame's and its references' inputs
+  long ds[1 + RV_MAX_REFS];
+  int nd = 0;
+  ds[nd++] = fi.display;
+  for (int k = 0; k < g.R; k++) ds[nd++] = fi.ref_display[k];
+  for (int i = 0; i < nd; i++) {
+    const size_t idx = (size_t)(ds[i] % (long)r->inputs.size());
+    if (E.pyr_display[idx] == ds[i]) continue;
+    const RvInput &in = r->inputs[idx];
+    RV_R(rv_plane_pyramid(&in.y, &in.hres, &in.qres, xs));
+    if (r->sea) RV_R(rv_plane_box_sums(&in.qres, in.qres_box, xs));
+    E.pyr_display[idx] = ds[i];
+  }
+  const size_t nr = (size_t)g.nsb * g.R;
+  if (m > 1) {  // the field's first guess: the previous frame's lookahead
+    const RvLaEngine::Entry &p = E.at(m - 1);
+    RV_H(hipMemcpyAsync(e.o.half_l, p.o.half_l, nr * 4 * sizeof(rv_fs_result),
+                        hipMemcpyDeviceToDevice, xs));
+    RV_H(hipMemcpyAsync(e.o.look, p.o.look, nr * 16 * sizeof(rv_fs_result),
+                        hipMemcpyDeviceToDevice, xs));
+  }
+  RV_R(lookahead_frame(r, E.rr, xs, fi, m - 1, e.o, E.la_list, false, &E.la_round_sum,
+                       &E.la_reeval, nullptr));
+  rv_plane refs_o[RV_MAX_REFS];
+  for (int k = 0; k < g.R; k++) refs_o[k] = r->inputs[fi.ref_display[k] % r->inputs.size()].y;
+  RV_R(impwin_frame_data(r->inputs[fi.display % r->inputs.size()].y, refs_o, g.R, g.bd, e.o.look,
+                         g.tw, g.nsb, g.w_imp, g.h_imp, e.f, E.scratch, E.scratch_bytes, xs));
+  e.m = m;
+  e.fi = fi;
+  const long last_frame = E.limit > 0 ? E.limit - 1 : -1;
+  const size_t ni = (size_t)g.w_imp * g.h_imp;
+  while (E.imp_next <= m && (E.imp_next + E.W <= m || m == last_frame)) {
+    const long n = E.imp_next, last = n + E.W < m ? n + E.W : m;
+    for (long t = n; t <= last; t++) RV_H(hipMemsetAsync(E.at(t).f.imp, 0, ni * 4, xs));
+    for (long s2 = last; s2 > n; s2--) {
+      const RvLaEngine::Entry &es = E.at(s2);
+      int uk[RV_MAX_REFS], nu = 0;
+      for (int k = 0; k < g.R; k++) {
+        bool dup = false;
+        for (int j = 0; j < nu; j++) dup |= es.fi.ref_display[uk[j]] == es.fi.ref_display[k];
+        if (!dup) uk[nu++] = k;
+      }
+      for (int j = 0; j < nu; j++) {
+        const long t = coded_of_display(es.fi.ref_display[uk[j]]);
+        if (t < n) continue;  // before the window: gone (:944-948)
+        RV_R(impwin_pass(es.f, uk[j], nu, g.w_imp, g.h_imp, E.at(t).f.imp, xs));
+      }
+    }
+    RV_R(impwin_final(E.at(n).f, g.w_imp, g.h_imp, xs));
+    RV_H(hipEventRecord(E.at(n).ev_imp, xs));
+    std::lock_guard<std::mutex> lk(E.mu);
+    E.imp_ready = n;
+    E.imp_next = n + 1;
+    E.cv.notify_all();
+  }
+  return RV_OK;
+}
+
+static void la_thread_main(rv_replay *r) {
+  RvLaEngine &E = *r->eng;
+  (void)hipSetDevice(E.dev);
+  for (long m = 1;; m++) {
+    {
+      std::unique_lock<std::mutex> lk(E.mu);
+      E.cv.wait(lk, [&] {
+        if (E.stop) return true;
+        if (E.requested < 1 || m > E.requested + E.W) return false;
+        if (E.limit > 0 && m >= E.limit) return false;
+        return m - E.RW < 1 || E.at(m).used_by == m - E.RW;
+      });
+      if (E.stop) return;
+    }
+    const int rc = la_step(r, m);
+    if (rc != RV_OK) {
+      std::lock_guard<std::mutex> lk(E.mu);
+      E.err = rc;
+      E.msg = rv_last_error();
+      E.cv.notify_all();
+      return;
+    }
+  }
+}
+
+static void la_engine_destroy(rv_replay *r) {
+  RvLaEngine *E = r->eng;
+  r->eng = nullptr;
+  if (!E || !r->eng_owned) return;
+  {
+    std::lock_guard<std::mutex> lk(E->mu);
+    E->stop = true;
+    E->cv.notify_all();
+  }
+  if (E->th.joinable()) E->th.join();
+  if (E->las) (void)hipStreamSynchronize(E->las);
+  for (auto &en : E->ring) {
+    if (en.ev_imp) (void)hipEventDestroy(en.ev_imp);
+    if (en.ev_used) (void)hipEventDestroy(en.ev_used);
+  }
+  if (E->rr.h_pub) (void)hipHostFree(E->rr.h_pub);
+  if (E->las) (void)hipStreamDestroy(E->las);
+  delete E;  // its device arrays are the replay's allocations (freed with it)
+}
+
+// The encode side: wait for frame n's importances, take its lookahead.
+static int la_engine_take(rv_replay *r, long n, hipStream_t st, const float **imp) {
+  RvLaEngine &E = *r->eng;
+  {
+    std::unique_lock<std::mutex> lk(E.mu);
+    if (n > E.requested) E.requested = n;
+    E.cv.notify_all();
+    E.cv.wait(lk, [&] { return E.err != 0 || E.imp_ready >= n; });
+    if (E.err) return rv_set_error(E.err, E.msg.c_str());
+  }
+  const RvLaEngine::Entry &e = E.at(n);
+  if (e.m != n) return rv_set_error(RV_EINVAL, "rv_replay_frame: the lookahead ring lost a frame");
+  RV_H(hipStreamWaitEvent(st, e.ev_imp, 0));
+  const size_t nr = (size_t)r->g.nsb * r->g.R;
+  RV_H(hipMemcpyAsync(r->coarse, e.o.coarse, nr * sizeof(rv_fs_result), hipMemcpyDeviceToDevice, st));
+  RV_H(hipMemcpyAsync(r->half_l, e.o.half_l, nr * 4 * sizeof(rv_fs_result),
+                      hipMemcpyDeviceToDevice, st));
+  RV_H(hipMemcpyAsync(r->look, e.o.look, nr * 16 * sizeof(rv_fs_result), hipMemcpyDeviceToDevice,
+                      st));
+  *imp = e.f.fin;
+  return RV_OK;
+}
+
+// ... and when the frame's last reader of the entry is queued
+static int la_engine_release(rv_replay *r, long n, hipStream_t st) {
+  RvLaEngine &E = *r->eng;
+  RvLaEngine::Entry &e = E.at(n);
+  RV_H(hipEventRecord(e.ev_used, st));
+  std::lock_guard<std::mutex> lk(E.mu);
+  e.used_by = n;
+  E.cv.notify_all();
+  return RV_OK;
+}
+
+}  // extern "C" (closed for the C++ helpers above)
+extern "C" {
+
+// The importance window W (rdo_lookahead_frames) and the stream's length in
+// coded frames (limit; 0: unbounded).  W = 0: the importances are an input
+// (rv_replay_set_importances).  Only before the first frame, on a primary
+// instance replaying the whole frame as one group.
+int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
+  if (!r || window < 0 || window > 1024 || limit < 0)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_imp_window: bad arguments");
+  if (r->coded > 0) return rv_set_error(RV_EINVAL, "rv_replay_set_imp_window: after the first frame");
+  const Geo &g = r->g;
+  if (window > 0 && (g.tx0 || g.ty0 || g.vis_w != g.W || g.vis_h != g.H || r->n_groups > 1))
+    return rv_set_error(RV_EINVAL, "rv_replay_set_imp_window: a window needs the whole frame "
+                                   "(one group)");
+  if (r->eng && !r->eng_owned)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_imp_window: on the primary instance");
+  la_engine_destroy(r);
+  if (!window) return RV_OK;
+  RvLaEngine *E = new RvLaEngine();
+  E->W = window;
+  E->RW = window + 1 + RvLaEngine::kLaSlack;
+  E->limit = limit;
+  bool ok = hipGetDevice(&E->dev) == hipSuccess &&
+            hipStreamCreateWithFlags(&E->las, hipStreamNonBlocking) == hipSuccess &&
+            round_ring_alloc(r, E->rr, E->las);
+  const int ni = g.w_imp * g.h_imp, nr = g.nsb * g.R;
+  E->la_list = ok ? (int32_t *)dalloc(r, (size_t)nr * 20 * 4) : nullptr;
+  E->scratch_bytes = impwin_scratch_bytes(ni);
+  E->scratch = ok ? dalloc(r, E->scratch_bytes) : nullptr;
+  ok = ok && E->la_list && E->scratch;
+  E->ring.resize((size_t)E->RW);
+  const size_t ob = ((size_t)nr * 21 * sizeof(rv_fs_result) + 255) / 256 * 256;
+  for (auto &en : E->ring) {
+    if (!ok) break;
+    uint8_t *m = (uint8_t *)dalloc(r, ob + impwin_frame_bytes(ni, g.R));
+    ok = m && hipMemsetAsync(m, 0, ob, E->las) == hipSuccess &&
+         hipEventCreateWithFlags(&en.ev_imp, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&en.ev_used, hipEventDisableTiming) == hipSuccess;
+    if (!ok) break;
+    en.o.coarse = (rv_fs_result *)m;
+    en.o.half_l = en.o.coarse + nr;
+    en.o.look = en.o.half_l + (size_t)nr * 4;
+    impwin_frame_carve(en.f, m + ob, ni, g.R);
+  }
+  E->pyr_display.assign(r->inputs.size(), -1);
+  r->eng = E;
+  r->eng_owned = true;
+  if (!ok || hipStreamSynchronize(E->las) != hipSuccess) {
+    la_engine_destroy(r);
+    return rv_set_error(RV_EHIP, "rv_replay_set_imp_window: allocation failed");
+  }
+  E->th = std::thread(la_thread_main, r);
+  return RV_OK;
+}
+
+// The importances ([h_imp][w_imp] f32) the last coded frame's RDO used.
+int rv_replay_get_importances(rv_replay *r, float *host, int n) {
+  if (!r || !host || n != r->g.w_imp * r->g.h_imp)
+    return rv_set_error(RV_EINVAL, "rv_replay_get_importances: bad arguments");
+  RV_H(hipStreamSynchronize(r->stream));
+  if (!r->imp_last) {
+    memset(host, 0, (size_t)n * 4);
+    return RV_OK;
+  }
+  RV_H(hipMemcpy(host, r->imp_last, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return RV_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
 // Event layout per instrumented frame: e[0] start, e[1..13] after F0, F1,
 // F2, FL (lookahead), F3 full-pel, F3 sub-pel, F4 single-reference
 // candidates, F4 compound candidates, F4 argmin, F6 commit, F6b intra, F5,
@@ -2311,8 +2776,10 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     RV_H(hipMemcpyAsync(s.y.data, in.y.data, plane_bytes(in.y), hipMemcpyDeviceToDevice, st));
     RV_H(hipMemcpyAsync(s.u.data, in.u.data, plane_bytes(in.u), hipMemcpyDeviceToDevice, st));
     RV_H(hipMemcpyAsync(s.v.data, in.v.data, plane_bytes(in.v), hipMemcpyDeviceToDevice, st));
-    RV_R(rv_plane_pyramid(&in.y, &s.hres, &s.qres, st));
-    if (r->sea) RV_R(rv_plane_box_sums(&s.qres, s.qres_box, st));
+    if (!r->eng) {  // (the lookahead engine computes every pyramid itself)
+      RV_R(rv_plane_pyramid(&in.y, &in.hres, &in.qres, st));
+      if (r->sea) RV_R(rv_plane_box_sums(&in.qres, in.qres_box, st));
+    }
     // an intra frame saves no motion: its frame_mvs stay zero
     RV_H(hipMemsetAsync(s.fmv, 0, (size_t)(g.w_in_b / 2) * (g.h_in_b / 2) * g.R * sizeof(rv_mv), st));
     r->coded++;
@@ -2337,9 +2804,10 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   for (int k = 0; k < g.R; k++) {
     ref[k] = &r->slots[fi.ref_display[k] % kSlots];
     refs_y[k] = ref[k]->y;
-    refs_h[k] = ref[k]->hres;
-    refs_q[k] = ref[k]->qres;
-    box[k] = ref[k]->qres_box;
+    const RvInput &ri = r->inputs[fi.ref_display[k] % r->inputs.size()];
+    refs_h[k] = ri.hres;
+    refs_q[k] = ri.qres;
+    box[k] = ri.qres_box;
   }
   const int nr = g.nsb;  // jobs per reference
   const long ncoded = r->coded - 1;  // non-key frames before this one
@@ -2359,128 +2827,25 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     if (tm) RV_H(hipEventRecord(e[i], st));        \
   } while (0)
   RV_EV(0);
-  // F0 hres + qres of the input (encode_frame, src/encoder.rs:3382-3385)
-  // into this frame's DPB slot, and the box sums its later searches need
-  RV_R(rv_plane_pyramid(&cur.y, &S.hres, &S.qres, st));
-  if (r->sea) RV_R(rv_plane_box_sums(&S.qres, S.qres_box, st));
-  RV_EV(1);
-  // F1 coarse full search (build_coarse_pmvs), every reference in one launch
-  RV_R(rv_full_search_multi(&S.qres, refs_q, g.R, r->fs_jobs[lv], nr, 16, 16, 1, 0, r->coarse,
-                            nullptr, r->sea ? box : nullptr, st));
-  RV_EV(2);
-  // The host side of a round loop (the lookahead's EPZS rounds and the MV-
-  // stack rounds): check(q) queues check q, which lists the jobs to re-run
-  // and publishes their count into the host-mapped ring; eval(q) queues the
-  // round that re-runs check q's list.  The host keeps kRoundsAhead rounds
-  // queued beyond the last count it has read (it spins on the published
-  // counts, no stream synchronisation), so the GPU never waits on the host;
-  // the loop ends at the first check that lists nothing (the rounds queued
-  // after it find empty lists).  budget: the chain's depth bound (see the
-  // callers); a check still listing jobs after it is an internal error.
-  static const bool mv_trace = getenv("RAV1E_HIP_MV_TRACE") != nullptr;
+  // F0 .. FL: the frame's lookahead (lookahead_frame), or with an importance
+  // window the engine's, run W frames ahead, and the window's importances
+  const float *imp = r->imp;
+  if (r->eng) {
+    RV_R(la_engine_take(r, r->coded, st, &imp));
+    if (tm)  // F0 .. FL ran on the engine: empty stages here
+      for (int i : {1, 2, 3, rv_replay::kStageEv, rv_replay::kStageEv + 1})
+        RV_H(hipEventRecord(e[i], st));
+  } else {
+    RV_R(lookahead_frame(r, r->rr, st, fi, ncoded, LaOut{r->coarse, r->half_l, r->look}, r->la_list,
+                         true, &r->la_round_sum, &r->la_reeval, tm ? e : nullptr));
+  }
+  r->imp_last = imp;
   auto rounds = [&](hipStream_t xs, int budget, auto &&check, auto &&eval, long *nrounds,
                     long *nre, bool *changed, const char *what) -> int {
-    if (changed) *changed = false;
-    const uint32_t first = r->mv_seq++;
-    RV_R(check(first));
-    int queued = 0;  // evaluation rounds queued (round j evaluates check j - 1's list)
-    for (int seen = 0;; seen++) {
-      while (queued < budget && queued < seen + rv_replay::kRoundsAhead) {
-        RV_R(eval(first + (uint32_t)queued));
-        RV_R(check(r->mv_seq++));
-        queued++;
-      }
-      const uint32_t q = first + (uint32_t)seen;
-      volatile unsigned long long *pub = r->h_pub + q % rv_replay::kPubRing;
-      const auto t0 = std::chrono::steady_clock::now();
-      unsigned long long v;
-      for (long spin = 0;; spin++) {
-        v = *pub;
-        if ((uint32_t)(v >> 32) == q) break;
-        if ((spin & 1023) == 1023) {
-          const hipError_t he = hipStreamQuery(xs);
-          if (he != hipSuccess && he != hipErrorNotReady)
-            return rv_set_error(RV_EHIP, "rv_replay_frame: a round failed");
-          if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
-            return rv_set_error(RV_EHIP, "rv_replay_frame: a round's count never arrived");
-          std::this_thread::yield();
-        }
-      }
-      const int c = (int)(uint32_t)v;
-      if (mv_trace)
-        fprintf(stderr, "%s frame %ld level %d check %d: %d\n", what, ncoded, lv, seen, c);
-      if (c == 0) return RV_OK;
-      if (seen >= budget)
-        return rv_set_error(RV_EHIP, "rv_replay_frame: rounds beyond the chain's dependency "
-                                     "depth (internal error)");
-      *nre += c;
-      (*nrounds)++;
-      if (changed) *changed = true;
-    }
+    return run_rounds(r->rr, xs, budget, check, eval, nrounds, nre, changed, what, ncoded, lv);
   };
-  auto slot_cnt = [&](uint32_t q) { return r->mv_cnt + 2 * (q % rv_replay::kCntRing); };
-  // check q's slot of the host-mapped ring (read at h_pub + q % kPubRing)
-  auto pub_of = [&](uint32_t q) { return r->d_pub + q % rv_replay::kPubRing; };
+  auto slot_cnt = [&](uint32_t q) { return r->rr.slot(q); };
   const EpzsGeo eg{g.tx0, g.ty0, g.tw, g.th, g.tws, g.ths, g.W, g.H, g.w_in_b, g.h_in_b};
-
-  // F2L + FL: the lookahead's build_half_res_pmvs and build_full_res_pmvs
-  // (compute_lookahead_motion_vectors, src/api/internal.rs:514-622) with
-  // their EPZS sets (la_check_kernel): round 0 stores every F2L set (the
-  // field guessed from the previous frame's results) and runs every F2L
-  // search, then the same for FL; then the rounds.  Budget: a quadrant
-  // search reads the quadrants of the superblocks left of and above it, so
-  // it settles by round tws + ths - 1; a 16x16 search reads its coarse /
-  // quadrant predictors (settled by then) and the 16x16 blocks left of and
-  // above it, so it settles 4 tws + 4 ths - 2 rounds later.
-  {
-    LaArgs la_a;
-    memset(&la_a, 0, sizeof(la_a));
-    la_a.g = g;
-    la_a.eg = eg;
-    la_a.jh = r->jobs_half_l[lv];
-    la_a.jl = r->jobs_look[lv];
-    la_a.sl = r->src_look;
-    la_a.coarse = r->coarse;
-    la_a.half_l = r->half_l;
-    la_a.look = r->look;
-    const int nh = nr * g.R * 4, nl = nr * g.R * 16;
-    la_a.list_h = r->la_list;
-    la_a.list_l = r->la_list + nh;
-    auto la_launch = [&](int what, uint32_t q, bool init) -> int {
-      la_a.what = what;
-      la_a.init = init ? 1 : 0;
-      la_a.pub = RoundPub{slot_cnt(q), slot_cnt(q + 1), r->mv_ticket, init ? nullptr : pub_of(q), q};
-      const int n = ((what & 1) ? nh : 0) + ((what & 2) ? nl : 0);
-      la_check_kernel<<<(n + 255) / 256, 256, 0, st>>>(la_a);
-      RV_H(hipGetLastError());
-      return RV_OK;
-    };
-    auto f2l = [&](const int32_t *list, const int32_t *cnt) {
-      return rv_diamond_search_multi(&S.hres, refs_h, g.R, r->jobs_half_l[lv], nr * 4, 16, 16, 0,
-                                     0, 0, g.bd, r->half_l, nullptr, nullptr, st, nullptr, list,
-                                     cnt, 0);
-    };
-    auto fl = [&](const int32_t *list, const int32_t *cnt) {
-      return rv_diamond_search_multi(&cur.y, refs_o, g.R, r->jobs_look[lv], nr * 16, 16, 16, 0, 0,
-                                     0, g.bd, r->look, nullptr, nullptr, st, nullptr, list, cnt, 0);
-    };
-    RV_R(la_launch(1, 0, true));
-    RV_R(f2l(nullptr, nullptr));
-    RV_EV(3);
-    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv], st));
-    RV_R(la_launch(2, 0, true));
-    RV_R(fl(nullptr, nullptr));
-    r->la_round_sum++;
-    RV_R(rounds(
-        st, 5 * (g.tws + g.ths),
-        [&](uint32_t q) { return la_launch(3, q, false); },
-        [&](uint32_t q) -> int {
-          RV_R(f2l(r->la_list, slot_cnt(q)));
-          return fl(r->la_list + nh, slot_cnt(q) + 1);
-        },
-        &r->la_round_sum, &r->la_reeval, nullptr, "lookahead"));
-    if (tm) RV_H(hipEventRecord(e[rv_replay::kStageEv + 1], st));
-  }
   // F5: the 8x8 importance SATD against reference 0's original frame at the
   // lookahead MVs (FL's output; after the frame's decisions)
   auto f5_importance = [&](hipStream_t fs) -> int {
@@ -2519,7 +2884,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   la.g = cg;
   la.sub = r->sub;
   la.win = r->win;
-  la.imp = r->imp;
+  la.imp = imp;
   la.w_in_b = g.w_in_b;
   la.h_in_b = g.h_in_b;
   la.w_imp = g.w_imp;
@@ -2762,7 +3127,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     ma.dec = r->dec_lv[lv];
     ma.stk = r->stk;
     ma.active = r->mv_active;
-    ma.count = r->mv_cnt;
+    ma.count = r->rr.cnt;
     ma.jf = r->jobs_full[lv];
     ma.js = r->jobs_sub[lv];
     ma.init = 1;
@@ -2790,16 +3155,16 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     ma.prev = r->slots[fi.ref_display[0] % kSlots].fmv;  // the LAST reference's frame_mvs
     ma.edge_ok = 0;
     // the first check marks every superblock (its count is not read)
-    const uint32_t q = r->mv_seq++;
+    const uint32_t q = r->rr.seq++;
     ma.count = slot_cnt(q);
-    ma.pub = RoundPub{slot_cnt(q), slot_cnt(q + 1), r->mv_ticket, pub_of(q), q};
+    ma.pub = r->rr.pub(q);
     RV_R(rv_mvref_round(ma, st));
   }
   // F2: build_half_res_pmvs of the encode (speed 10: the sets the check
   // stored; otherwise the lookahead's quadrants stand in) and the F3
   // full-pel predictors (otherwise zero + the coarse MV)
   if (r->exact) {
-    RV_R(rv_diamond_search_multi(&S.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
+    RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
                                  g.bd, r->half, nullptr, nullptr, st));
   } else {
     RV_H(hipMemcpyAsync(r->half, r->half_l, (size_t)nr * g.R * 4 * sizeof(rv_fs_result),
@@ -2863,7 +3228,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   auto f3_f4_list = [&](hipStream_t xs, uint32_t q) -> int {
     const int32_t *acnt = slot_cnt(q);
     // F2 of the listed superblocks (their 4 quadrants per reference)
-    RV_R(rv_diamond_search_multi(&S.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
+    RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
                                  g.bd, r->half, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 4));
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
                                  r->full, nullptr, &to_sub, xs, nullptr, r->mv_list, acnt));
@@ -2928,7 +3293,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
           ma.init = 0;
           ma.iwas = iwas;
           ma.count = slot_cnt(q);
-          ma.pub = RoundPub{slot_cnt(q), slot_cnt(q + 1), r->mv_ticket, pub_of(q), q};
+          ma.pub = r->rr.pub(q);
           return rv_mvref_round(ma, xs);
         },
         [&](uint32_t q) { return f3_f4_list(xs, q); }, &r->mv_round_sum, &r->mv_reeval, changed,
@@ -3150,6 +3515,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   }
   RV_EV(13);
 #undef RV_EV
+  if (r->eng) RV_R(la_engine_release(r, r->coded - 1, st));  // its lookahead entry is free
   if (info) *info = fi;
   RV_H(hipGetLastError());
   return RV_OK;
@@ -3322,7 +3688,12 @@ int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
   // round runs: 1 + the MV / intra passes (the joint fixed point's outer
   // iterations), summed over frames
   out[17] = (uint64_t)r->mv_run_sum;
-  return 18;
+  if (cap < 20) return 18;
+  // the lookahead's EPZS rounds and re-run jobs (the engine's on its owner)
+  const bool own_eng = r->eng && r->eng_owned;
+  out[18] = (uint64_t)(r->la_round_sum + (own_eng ? r->eng->la_round_sum : 0));
+  out[19] = (uint64_t)(r->la_reeval + (own_eng ? r->eng->la_reeval : 0));
+  return 20;
 }
 
 // ---- RCCL communicator for the tile-group exchange ---------------------------

@@ -269,7 +269,7 @@ class HipReplay:
 
     def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, group=None,
                  tile_size=(0, 0), n_inputs=8, stream=None, flags=0,
-                 quantizer=DEFAULT_QUANTIZER):
+                 quantizer=DEFAULT_QUANTIZER, imp_window=0, imp_limit=0):
         cfg = RvReplayCfg()
         cfg.width, cfg.height, cfg.xdec, cfg.ydec = width, height, xdec, ydec
         cfg.bit_depth, cfg.n_refs, cfg.n_inputs, cfg.flags = bit_depth, n_refs, n_inputs, flags
@@ -289,6 +289,11 @@ class HipReplay:
             p = RvReplayLevelParams.from_dict(d)
             _check(lib().rv_replay_set_level_params(self.h, lv, C.byref(p)),
                    "rv_replay_set_level_params")
+        self.imp_window = imp_window
+        if imp_window:
+            _check(lib().rv_replay_set_imp_window(self.h, int(imp_window), int(imp_limit)),
+                   "rv_replay_set_imp_window")
+        self.imp_shape = ((height + 7) // 8, (width + 7) // 8)
 
     def twin(self):
         """A second instance sharing this one's DPB and inputs
@@ -297,6 +302,7 @@ class HipReplay:
         t = HipReplay.__new__(HipReplay)
         t.cfg, t.geom, t.speed, t.n_words, t.levels = self.cfg, self.geom, self.speed, \
             self.n_words, self.levels
+        t.imp_window, t.imp_shape = self.imp_window, self.imp_shape
         t.h = lib().rv_replay_create_twin(self.h, None)
         if not t.h:
             raise RuntimeError(f"rv_replay_create_twin: {lib().rv_last_error().decode()}")
@@ -340,6 +346,13 @@ class HipReplay:
         imp = np.ascontiguousarray(imp, dtype=np.float32)
         _check(lib().rv_replay_set_importances(self.h, imp.ctypes.data, imp.size),
                "rv_replay_set_importances")
+
+    def importances(self) -> np.ndarray:
+        """The block importances the last coded frame's RDO used."""
+        out = np.zeros(self.imp_shape, np.float32)
+        _check(lib().rv_replay_get_importances(self.h, out.ctypes.data, out.size),
+               "rv_replay_get_importances")
+        return out
 
     def frame(self) -> dict:
         fi = RvReplayFrameInfo()
@@ -408,8 +421,8 @@ class HipReplay:
         frames, then (speed 10, since creation) the MV-stack rounds, the
         superblocks they re-evaluated, the frames, and the round runs (1 +
         the MV / intra passes of each frame)."""
-        out = np.zeros(18, dtype=np.uint64)
-        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 18) - 18, "rv_replay_counters")
+        out = np.zeros(20, dtype=np.uint64)
+        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 20) - 20, "rv_replay_counters")
         return out
 
     def close(self):

@@ -397,14 +397,14 @@ def intra_frames(w, h, xdec, ydec, bd, n, seed=7):
 
 
 def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=None, quantizer=100,
-                inputs=None, want_intra=False):
+                inputs=None, want_intra=False, imp_window=0):
     import rav1e_amd as R
     R.require_device(0)
     t = RP.tiling_for(w, h, **(tiling or {}))
     ts = (t["tile_width_sb"], t["tile_height_sb"])
     nin = frames + 8
     g = RP.HipReplay(w, h, xdec, ydec, bd, refs, tile_size=ts, n_inputs=nin, flags=flags,
-                     quantizer=quantizer)
+                     quantizer=quantizer, imp_window=imp_window, imp_limit=frames)
     g.synth_inputs(0)
     if inputs is not None:
         for i in range(nin):
@@ -415,24 +415,32 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
                     deblock=bool(flags & RP.RV_REPLAY_DEBLOCK),
                     cdef=bool(flags & RP.RV_REPLAY_CDEF),
                     intra=not flags & RP.RV_REPLAY_NO_INTRA,
-                    mvref_standin=bool(flags & RP.RV_REPLAY_MVREF_STANDIN))
+                    mvref_standin=bool(flags & RP.RV_REPLAY_MVREF_STANDIN),
+                    imp_window=imp_window, imp_limit=frames)
     for i in range(nin):
         c.set_input(i, g.get_input(i))
     if imp is not None:
         g.set_importances(imp)
         c.set_importances(imp)
-    won = 0
+    won = nz = 0
     for n in range(frames):
         gi, ci = g.frame(), c.frame()
         assert gi == ci
         gw, cw = g.results(), c.results()
         bad = np.nonzero(gw != cw)[0]
         assert bad.size == 0, (n, gi, bad[:10], gw[bad[:10]], cw[bad[:10]])
+        if imp_window:
+            gimp, cimp = g.importances(), c.importances()
+            np.testing.assert_array_equal(gimp.view(np.uint32), cimp.view(np.uint32),
+                                          err_msg="importances of frame %d" % n)
+            nz += bool((cimp > 0).any())
         won += c.intra_stats()[1] if c.intra else 0
     np.testing.assert_array_equal(g.get_recon(gi["display"]), c.get_recon(ci["display"]))
     if want_intra:
         cnt = g.counters()
         assert won > 0 and cnt[12] == won, (won, cnt[11:14])
+    if imp_window:
+        assert nz >= 2, nz  # the referenced frames carry importances
     g.close()
     c.close()
 
@@ -477,6 +485,21 @@ def test_gpu_replay_importance_bias_and_quantizer(flags):
     rng = np.random.default_rng(3)
     imp = rng.random((h // 8) * (w // 8)).astype(np.float32) * 7
     _gpu_vs_cpu(w, h, 1, 1, 8, 2, 6, imp=imp, quantizer=60, flags=flags)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,bd,refs,tiling,flags,window", [
+    (256, 192, 8, 2, None, 0, 4),
+    (320, 136, 10, 2, {"tile_cols": 2}, 0, 6),
+    (256, 200, 8, 1, None, 0, 3),
+    (256, 200, 8, 2, None, RP.RV_REPLAY_SPEED6, 4),
+    (192, 128, 12, 2, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF, 2),
+])
+def test_gpu_replay_importance_window(w, h, bd, refs, tiling, flags, window):
+    """compute_block_importances over the lookahead window on the GPU's
+    lookahead engine (its own thread, stream and round ring, W frames
+    ahead): every frame's importances and words equal the CPU replay's."""
+    _gpu_vs_cpu(w, h, 1, 1, bd, refs, 11, tiling, flags, quantizer=60, imp_window=window)
 
 
 @pytest.mark.gpu
@@ -534,9 +557,9 @@ def test_gpu_tile_groups_exchange(flags):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF,
-                                   RP.RV_REPLAY_SPEED6])
-def test_gpu_paired_replay_matches_cpu(flags):
+@pytest.mark.parametrize("flags,window", [(0, 0), (RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF, 0),
+                                          (RP.RV_REPLAY_SPEED6, 0), (0, 5)])
+def test_gpu_paired_replay_matches_cpu(flags, window):
     """PairedReplay: the level-2 frames on a twin instance (shared DPB, own
     stream and host thread) give every frame's words and reconstruction of
     the sequential CPU replay -- checked frame by frame, then over a run
@@ -545,10 +568,11 @@ def test_gpu_paired_replay_matches_cpu(flags):
     R.require_device(0)
     w, h, nin = 256, 200, 24
     speed = 6 if flags & RP.RV_REPLAY_SPEED6 else 10
-    g = RP.HipReplay(w, h, n_inputs=nin, flags=flags)
+    g = RP.HipReplay(w, h, n_inputs=nin, flags=flags, imp_window=window, imp_limit=21)
     g.synth_inputs(0)
     c = O.CpuReplay(w, h, n_inputs=nin, threads=O.cpu_share(), speed=speed,
-                    deblock=bool(flags & RP.RV_REPLAY_DEBLOCK), cdef=bool(flags & RP.RV_REPLAY_CDEF))
+                    deblock=bool(flags & RP.RV_REPLAY_DEBLOCK), cdef=bool(flags & RP.RV_REPLAY_CDEF),
+                    imp_window=window, imp_limit=21)
     for i in range(nin):
         c.set_input(i, g.get_input(i))
     eng = RP.PairedReplay(g)
