@@ -48,6 +48,8 @@ CONFIGS = {
     "2160p444": (3840, 2160, 0, 0, 8, {"tiles": 4}, "E", 10),
 }
 TIMING_STRIDE = 4  # in GOPs
+IMP_WINDOW = 40  # rdo_lookahead_frames default (src/api/config.rs:158)
+CPU_FRAMES = 8  # coded frames of the CPU baseline / parity stream with a window
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
 # VALU issue peaks, G wave64 instructions/s over 256 CUs at 2.4 GHz: the
 # guide's 2 cycles per wave instruction per SIMD (MI355X_MICROARCH.md "Wave
@@ -179,7 +181,7 @@ def timed_run(engine, group, steps, warmup, sync=None, finish=None):
 
 
 def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling, n_inputs,
-                            speed=10, flags=0):
+                            speed=10, flags=0, imp_window=0):
     """The CPU baseline and the full-size parity check, from one CPU run.
 
     The CPU replay (oracle/orc_replay.c: the same schedule over the oracle's
@@ -189,7 +191,9 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     replay then codes the same frames and its words must equal the CPU's,
     frame by frame: the bench's own full-size bit-exactness check.  A
     bounded 1-thread sample (the first superblocks of one GOP) is timed
-    beside it."""
+    beside it.  With an importance window both code a stream of CPU_FRAMES
+    coded frames (the window shrinks at its end, as rav1e's does at the end
+    of a stream)."""
     import rav1e_amd as R
     from rav1e_amd import replay as RP
     from tests import oracle_lib as O  # the checker / CPU baseline only
@@ -201,14 +205,17 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     cd = bool(flags & RP.RV_REPLAY_CDEF)
     ent = bool(flags & RP.RV_REPLAY_ENTROPY)
     sti = bool(flags & RP.RV_REPLAY_MVREF_STANDIN)
+    limit = CPU_FRAMES + 1 if imp_window else 0
     c = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=threads, L=L,
-                    speed=speed, deblock=db, cdef=cd, entropy=ent, mvref_standin=sti)
+                    speed=speed, deblock=db, cdef=cd, entropy=ent, mvref_standin=sti,
+                    imp_window=imp_window, imp_limit=limit)
     for i in range(nin):
         c.set_input(i, hip_inputs[i])
     c.frame()  # the key frame (a copy), untimed
     cpu_words, cpu_ent = [], []
     n, tc0 = 0, time.perf_counter()
-    while n < 4 or (time.perf_counter() - tc0 < args.cpu_seconds and n < nin - 6):
+    while n < 4 or (time.perf_counter() - tc0 < args.cpu_seconds and n < nin - 6 and
+                    (not limit or n < CPU_FRAMES)):
         c.frame()
         n += 1
         cpu_words.append(c.results())  # a memcpy + sums; kept inside the timing
@@ -220,7 +227,8 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     nsb = ((W + 63) // 64) * ((H + 63) // 64)
     lim = max(1, nsb // 8)
     c1 = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=1, L=L,
-                     speed=speed, deblock=db, cdef=cd, entropy=ent, mvref_standin=sti)
+                     speed=speed, deblock=db, cdef=cd, entropy=ent, mvref_standin=sti,
+                     imp_window=imp_window, imp_limit=5 if imp_window else 0)
     for i in range(nin):
         c1.set_input(i, hip_inputs[i])
     c1.frame()
@@ -243,7 +251,8 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     g = RP.HipReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=n_inputs,
                      flags=flags & (RP.RV_REPLAY_SPEED6 | RP.RV_REPLAY_DEBLOCK |
                                     RP.RV_REPLAY_CDEF | RP.RV_REPLAY_ENTROPY |
-                                    RP.RV_REPLAY_MVREF_STANDIN))
+                                    RP.RV_REPLAY_MVREF_STANDIN),
+                     imp_window=imp_window, imp_limit=limit)
     g.synth_inputs(0)
     g.frame()
     bad = []
@@ -258,7 +267,8 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     g.close()
     R._check(R.lib().rv_device_sync(), "rv_device_sync")
     parity = {"frames": n, "words": int(sum(w.size for w in cpu_words)),
-              "bit_exact": not bad, "vs": "oracle/orc_replay.c (CPU replay)"}
+              "bit_exact": not bad, "vs": "oracle/orc_replay.c (CPU replay)",
+              **({"importance_window": imp_window, "stream_frames": limit} if imp_window else {})}
     if ent:
         parity["coefficient_bytes"] = int(sum(e[0] for e in cpu_ent))
     if bad:
@@ -362,6 +372,10 @@ def main():
                          "the host range coder); default: every frame's coefficients are coded")
     ap.add_argument("--exhaustive-fs", action="store_true",
                     help="F1 coarse search without successive elimination (same results)")
+    ap.add_argument("--imp-window", type=int, default=IMP_WINDOW,
+                    help="rdo_lookahead_frames: block importances propagated over that many "
+                         "coded frames ahead (rav1e's default 40; 0: importance 0, bias 0.65); "
+                         "one GPU only (a window needs the whole frame's lookahead)")
     args = ap.parse_args()
 
     import rav1e_amd as R  # load the HIP library before anything else
@@ -379,13 +393,16 @@ def main():
     tiling = RP.tiling_for(W, H, **tkw)
     ts = (tiling["tile_width_sb"], tiling["tile_height_sb"])
     rects = RP.tile_groups(tiling, world)
-    n_inputs = args.warmup + args.steps + 8  # every display the run codes
+    imp_window = args.imp_window if world == 1 else 0
+    # every display the run codes, and the lookahead's W frames beyond
+    n_inputs = args.warmup + args.steps + 8 + imp_window
     flags = (RP.RV_REPLAY_EXHAUSTIVE_FS if args.exhaustive_fs else 0) | \
         (RP.RV_REPLAY_SPEED6 if speed == 6 else 0) | (RP.RV_REPLAY_DEBLOCK if args.deblock or args.cdef else 0) | \
         (RP.RV_REPLAY_CDEF if args.cdef else 0) | (0 if args.no_entropy else RP.RV_REPLAY_ENTROPY) | \
         (RP.RV_REPLAY_MVREF_STANDIN if args.mv_stack == "standin" else 0)
     hip = RP.HipReplay(W, H, xdec, ydec, bd, nref, group=rects[rank], tile_size=ts,
-                       n_inputs=n_inputs, flags=flags)
+                       n_inputs=n_inputs, flags=flags, imp_window=imp_window,
+                       imp_limit=args.warmup + args.steps)
     hip.synth_inputs(0)  # the stream's frames, resident in HBM before the timing
     comm = RP.RcclComm(group) if world > 1 else None
     eng = TileParallel(hip, rects, rank, group, comm)
@@ -515,12 +532,12 @@ def main():
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the CPU codes the same frames: the GPU's inputs, downloaded
-        inputs = [hip.get_input(i) for i in range(min(22, n_inputs))]
+        inputs = [hip.get_input(i) for i in range(min(22 + imp_window, n_inputs))]
         if paired:
             eng.close()
         hip.close()  # the parity pass below builds a fresh GPU replay
         cpu, parity = cpu_baseline_and_parity(args, inputs, W, H, xdec, ydec, bd, nref,
-                                              tiling, n_inputs, speed, flags)
+                                              tiling, n_inputs, speed, flags, imp_window)
 
     if rank == 0:
         line = {
@@ -568,6 +585,18 @@ def main():
                 "rounds_per_frame": round(cnt[14] / max(1, cnt[16]), 3),
                 "reevaluated_sb_per_frame": round(cnt[15] / max(1, cnt[16]), 2)}}
                if speed == 10 and len(cnt) > 16 else {}),
+            "importances": ({
+                "window": imp_window,
+                "what": "compute_block_importances over rdo_lookahead_frames coded frames: every "
+                        "frame's lookahead (F0 pyramids, F1, F2L / FL with their EPZS rounds) runs "
+                        "that many frames ahead on a lookahead engine (own host thread, stream and "
+                        "round ring), then the window's propagation (per-frame target lists, one "
+                        "pass per frame and reference) and log2; the frame's RDO bias reads them",
+                "stream_frames": args.warmup + args.steps,
+                "lookahead_rounds_per_frame": round(cnt[18] / max(1, args.warmup + args.steps), 3)
+                if len(cnt) > 18 else None} if imp_window else
+                {"window": 0, "what": "importance 0 (bias 0.65)" +
+                 ("; a window needs the whole frame's lookahead: one GPU only" if world > 1 else "")}),
             "intra_per_frame": {"screened_superblocks": round(cnt[11] / ev_frames, 2),
                                 "intra_winners": round(cnt[12] / ev_frames, 2),
                                 "rounds": round(cnt[13] / ev_frames, 2),
