@@ -134,6 +134,18 @@ ROCPROF_NAMES = {
 }
 
 
+def _prof_json(args):
+    """The newest committed kernel profile of this config
+    (profiles/rNN_prof_<config>.json, tools/prof_json.py over a
+    `tools/gpu.sh prof` run of this bench)."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_prof_{args.config}.json")))
+    if args.refs != 2 or not fs:
+        return None
+    with open(fs[-1]) as f:
+        return json.load(f)
+
+
 def _profile_entry(args, kernel, bd, kind):
     """A kernel's entry in the committed rocprofv3 PMC summaries
     (profiles/<kind>_<config>.json), for the workload it was measured on."""
@@ -148,6 +160,27 @@ def _profile_entry(args, kernel, bd, kind):
         if want in name:
             return v, tj
     return None
+
+
+def _kernels_trace(pj):
+    """Every kernel of the committed trace of this bench, per coded frame
+    (all launches: round 0, the MV-stack rounds, the lookahead engine, the
+    twin), up to 95 % of the busy time; busy time is summed over streams,
+    which overlap, so it may exceed the step."""
+    ks = list(pj["kernels"].items())
+    busy = pj["busy_ms_per_frame"]
+    out, acc = {}, 0.0
+    for k, v in ks:
+        if acc >= 0.95 * busy:
+            break
+        out[k] = {"ms_per_frame": v["ms_per_frame"], "launches_per_frame": v["launches_per_frame"]}
+        acc += v["ms_per_frame"]
+    bl = pj.get("bench_line") or {}
+    return {"source": pj["source"], "git": pj["git"], "busy_ms_per_frame": busy,
+            "listed_ms_per_frame": round(acc, 4),
+            "traced_run_ms_per_step": bl.get("ms_per_step"),
+            "busy_over_step": round(busy / bl["ms_per_step"], 3) if bl.get("ms_per_step") else None,
+            "kernels": out}
 
 
 def timed_run(engine, group, steps, warmup, sync=None, finish=None):
@@ -486,6 +519,10 @@ def main():
     launch_s = kd["ms"] / 1e3
     ach = kd["bytes"] / launch_s / 1e9
     tr = _profile_entry(args, dom, bd, "traffic")
+    pj = _prof_json(args)
+    pk_name = ROCPROF_NAMES.get(dom, "?").format(px="unsigned short" if bd > 8 else "unsigned char",
+                                                 pxs="u16" if bd > 8 else "u8")
+    pke = next((v for k, v in pj["kernels"].items() if pk_name in k), None) if pj else None
     # `bound` names the roofline `frac` is priced against (the contract's HBM
     # roofline for this integer path); `limiter` names what actually binds,
     # with the committed counter evidence (SQ pass: profiles/valu_<config>.json)
@@ -496,7 +533,25 @@ def main():
                          "over_algorithmic": round(tr[0]["hbm_bytes"] / kd["bytes"], 3)}
                         if tr else None),
             "avg_launch_ms": round(kd["ms"], 5),
-            "algorithmic_bytes_per_launch": round(kd["bytes"])}
+            "algorithmic_bytes_per_launch": round(kd["bytes"]),
+            "launch": "the frame's full evaluation (round 0: every superblock's candidates, the "
+                      "ones counted in rdo_candidates_per_frame), HIP events on its stream"}
+    if pke and pke.get("round0"):
+        # the same launch in the committed trace of this bench (tools/prof_json.py): its mean
+        # duration and PMC traffic; frac re-priced from it for the reproducibility check
+        r0 = pke["round0"]
+        roof["trace"] = {
+            "source": pj["source"], "git": pj["git"], "round0_avg_us": r0["avg_us"],
+            "round0_hbm_bytes_per_launch": r0.get("hbm_bytes_per_launch"),
+            "frac_from_trace": round(kd["bytes"] / (r0["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
+            "live_over_trace_duration": round(kd["ms"] * 1e3 / r0["avg_us"], 3),
+            "all_launches": {"ms_per_frame": pke["ms_per_frame"],
+                             "launches_per_frame": pke["launches_per_frame"],
+                             "rounds_ms_per_frame": pke.get("rounds", {}).get("ms_per_frame")}}
+        if r0.get("hbm_bytes_per_launch"):
+            roof["traffic"] = {"bytes_per_launch": r0["hbm_bytes_per_launch"],
+                               "source": pj["source"], "git": pj["git"],
+                               "over_algorithmic": round(r0["hbm_bytes_per_launch"] / kd["bytes"], 3)}
     vp = _profile_entry(args, dom, bd, "valu")
     pk = valu_peak_int()
     if vp:
@@ -572,6 +627,7 @@ def main():
             "gpu_vs_cpu": round(fps / cpu["value"], 2) if cpu else None,
             "stage_ms": {n: round(float(v), 4) for n, v in zip(STAGES6 if speed == 6 else STAGES, ms)},
             "kernels_ms": {n: round(v["ms"], 4) for n, v in kernels.items()},
+            **({"kernels_trace": _kernels_trace(pj)} if pj else {}),
             "full_search_path": "successive elimination" if sea else "exhaustive",
             "diamond_evals_per_frame": [round(ev_full / ev_frames, 1),
                                         round(ev_sub / ev_frames, 1)],

@@ -43,7 +43,7 @@ case "$MODE" in
       "200 $TAG/fetch.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o run -- $B" \
       "200 $TAG/write.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $P/write -o run -- $B" \
       "200 $TAG/sq.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $SQ -d $P/sq -o run -- $B" \
-      "120 $TAG/gzip.log find $P -name '*.csv' -size +256k -exec gzip -9 {} +" ;;
+      "120 $TAG/gzip.log find $P -type f -size +256k ! -name '*.gz' -exec gzip -9 {} +" ;;
   envbench)
     # one bench line per environment setting: envbench TAG CFG "A=1" "A=2 B=1" ... [-- ARGS]
     CFG=$1; shift

@@ -15,9 +15,17 @@ import sqlite3
 
 
 def load(d):
-    dbs = glob.glob(os.path.join(d, "*.db"))
+    dbs = glob.glob(os.path.join(d, "*.db")) + glob.glob(os.path.join(d, "*.db.gz"))
     if dbs:
-        c = sqlite3.connect(dbs[0])
+        path = dbs[0]
+        if path.endswith(".gz"):  # tools/gpu.sh prof compresses the results
+            import tempfile
+            tmp = tempfile.NamedTemporaryFile(suffix=".db", delete=False)
+            with gzip.open(path, "rb") as f:
+                tmp.write(f.read())
+            tmp.close()
+            path = tmp.name
+        c = sqlite3.connect(path)
         return [(n, int(s), int(e), int(sc)) for n, s, e, sc in
                 c.execute("select name, start, end, scratch_size from kernels")]
     f = glob.glob(os.path.join(d, "*kernel_trace.csv*"))[0]
