@@ -453,6 +453,34 @@ __global__ __launch_bounds__(256) void la_check_kernel(LaArgs a) {
   round_publish(a.pub);
 }
 
+// What a candidate slot's F4 outputs (l_out / c_out) were computed for: an
+// F4 evaluation (rdo_quad: prediction, transform, quantisation, distortion,
+// coefficient rate) is a function of the block, its reference(s) and
+// MV(s) alone -- the stacks only enter the mode / MV rates, which the argmin
+// adds (cand_cost) -- so a later round of the same frame whose candidate has
+// the MV the slot was last evaluated with keeps the slot's outputs instead of
+// re-running it.  tag: the frame (rv_replay::coded + 1; 0 = never).
+struct CandKey {
+  uint32_t tag, mv0, mv1;
+};
+struct CandKeys {
+  CandKey *key;  // [nsingle + nsb * kCompModes]
+  uint32_t tag;
+  int reuse;     // 0: record only (round 0); 1: skip a slot whose key matches
+};
+__device__ inline uint32_t mv_bits(rv_mv m) {
+  return (uint32_t)(uint16_t)m.row | ((uint32_t)(uint16_t)m.col << 16);
+}
+// v: the candidate is live; returns whether F4 must evaluate it
+__device__ inline bool cand_key_step(const CandKeys &k, int slot, bool v, rv_mv m0, rv_mv m1) {
+  if (!v || !k.key) return v;
+  const CandKey n{k.tag, mv_bits(m0), mv_bits(m1)};
+  const CandKey o = k.key[slot];
+  if (k.reuse && o.tag == n.tag && o.mv0 == n.mv0 && o.mv1 == n.mv1) return false;
+  k.key[slot] = n;
+  return true;
+}
+
 // The valid candidates (cand_mv true) of every superblock, compacted for
 // the F4 launch: rav1e evaluates only the modes it pushes (about half of
 // the 4 per reference on smooth motion: NEWMV often repeats a neighbour's
@@ -461,13 +489,15 @@ __global__ __launch_bounds__(256) void la_check_kernel(LaArgs a) {
 // candidate).
 __global__ __launch_bounds__(256) void cand_list_kernel(CandGeo cg, const rv_fs_result *sub,
                                                          int n, int32_t *list, int32_t *count,
-                                                         const uint8_t *active = nullptr) {
+                                                         const uint8_t *active = nullptr,
+                                                         CandKeys keys = CandKeys{nullptr, 0, 0}) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   bool v = false;
   if (i < n) {
     rv_mv mv;
     const int c = i / cg.nsb, sb = i - c * cg.nsb;
     v = (!active || active[sb]) && cand_live(cg, sub, sb, c, &mv);
+    v = cand_key_step(keys, i, v, mv, rv_mv{0, 0});
   }
   const uint64_t m = __ballot(v);
   const int lane = threadIdx.x & 63;
@@ -480,12 +510,18 @@ __global__ __launch_bounds__(256) void cand_list_kernel(CandGeo cg, const rv_fs_
 // MV pairs: entries are absolute candidate indices nsingle + m * nsb + sb.
 __global__ __launch_bounds__(256) void comp_list_kernel(CandGeo cg, const rv_fs_result *sub,
                                                          int nsingle, int32_t *list, int32_t *count,
-                                                         const uint8_t *active = nullptr) {
+                                                         const uint8_t *active = nullptr,
+                                                         CandKeys keys = CandKeys{nullptr, 0, 0}) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   bool v = false;
   if (i < cg.comp * cg.nsb) {
     const int mm = i / cg.nsb, sb = i - mm * cg.nsb;
     v = (!active || active[sb]) && comp_live(cg, sub, sb, mm);
+    if (v && keys.key) {
+      rv_mv a0, a1;
+      comp_mvs(cg, sub, sb, mm, &a0, &a1);
+      v = cand_key_step(keys, nsingle + i, v, a0, a1);
+    }
   }
   const uint64_t m = __ballot(v);
   const int lane = threadIdx.x & 63;
@@ -501,7 +537,7 @@ __global__ __launch_bounds__(256) void comp_list_kernel(CandGeo cg, const rv_fs_
 __global__ __launch_bounds__(256) void round_lists_kernel(CandGeo cg, const rv_fs_result *sub,
                                                           int nsingle, int32_t *list,
                                                           int32_t *count, const int32_t *alist,
-                                                          const int32_t *acount) {
+                                                          const int32_t *acount, CandKeys keys) {
   const int cnt = __builtin_amdgcn_readfirstlane(*acount);
   const int ns = cg.R * cg.M, total = cnt * (ns + cg.comp);
   const int lane = threadIdx.x & 63;
@@ -512,8 +548,15 @@ __global__ __launch_bounds__(256) void round_lists_kernel(CandGeo cg, const rv_f
     if (i < total) {
       c = i / cnt;
       sb = alist[i - c * cnt];
-      rv_mv mv;
-      v = c < ns ? cand_live(cg, sub, sb, c, &mv) : comp_live(cg, sub, sb, c - ns);
+      rv_mv mv, m1{0, 0};
+      if (c < ns) {
+        v = cand_live(cg, sub, sb, c, &mv);
+      } else {
+        v = comp_live(cg, sub, sb, c - ns);
+        if (v) comp_mvs(cg, sub, sb, c - ns, &mv, &m1);
+      }
+      const int slot = c < ns ? c * cg.nsb + sb : nsingle + (c - ns) * cg.nsb + sb;
+      v = cand_key_step(keys, slot, v, mv, m1);
     }
     const bool comp = c >= ns;  // uniform per wavefront only where the split falls between them
     const uint64_t ms = __ballot(v && !comp), mc = __ballot(v && comp);
@@ -1096,6 +1139,8 @@ struct rv_replay {
   uint64_t *l_out, *c_out;  // F4: [skip dist, non-skip dist, rate] per transform block
   RdoWinner *win;
   int32_t *cand_list, *cand_count;  // F4: the valid candidates
+  CandKey *cand_key = nullptr;       // F4: what each candidate slot was last evaluated with
+  bool cand_reuse = true;            // a round keeps the F4 outputs of an unchanged candidate
   uint32_t *cand_evals;  // [kRing][2 * kLevels]: F4 candidates per frame and level (single, compound)
   int32_t *l_lev, *c_lev;   // F6: committed levels
   uint64_t *words;
@@ -1859,6 +1904,13 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
   r->c_out = (uint64_t *)dalloc(r, (size_t)nc * r->ntx_c * 3 * 8 * 2);
   r->win = (RdoWinner *)dalloc(r, (size_t)g.nsb * sizeof(RdoWinner));
   r->cand_list = (int32_t *)dalloc(r, (size_t)nc * 4);
+  {  // zeroed: tag 0 matches no frame
+    const size_t kb = ((size_t)g.nsb * (g.R * g.M + kCompModes)) * sizeof(CandKey);
+    r->cand_key = (CandKey *)dalloc(r, kb);
+    ok = ok && r->cand_key && hipMemsetAsync(r->cand_key, 0, kb, r->stream) == hipSuccess;
+    const char *e = getenv("RAV1E_HIP_F4_REUSE");  // =0: every round re-runs its F4 (A/B)
+    r->cand_reuse = !(e && e[0] == '0');
+  }
   r->cand_count = (int32_t *)dalloc(r, 8);  // [single, compound]
   r->cand_evals = (uint32_t *)dalloc(r, rv_replay::kRing * 2 * kLevels * 4);
   if (r->cand_evals)
@@ -3188,12 +3240,13 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     if (r->lvl && !edge && !lv_early) RV_R(lv_me(st));
     // the valid candidates (a few microseconds; bracketed with F3 sub-pel;
     // the count was zeroed by the previous argmin or at creation)
+    const CandKeys keys0{r->cand_key, (uint32_t)(r->coded + 1), 0};
     cand_list_kernel<<<(nsingle + 255) / 256, 256, 0, st>>>(cg, r->sub, nsingle, r->cand_list,
-                                                            r->cand_count, act);
+                                                            r->cand_count, act, keys0);
     if (r->lvl && !edge && !lv_early) lv_lists(st, false);
     if (cg.comp) {  // the compound lists (after the single ones in the same arrays)
       comp_list_kernel<<<(g.nsb * cg.comp + 255) / 256, 256, 0, st>>>(
-          cg, r->sub, nsingle, r->cand_list + nsingle, r->cand_count + 1, act);
+          cg, r->sub, nsingle, r->cand_list + nsingle, r->cand_count + 1, act, keys0);
       if (r->lvl && !edge && !lv_early) lv_lists(st, true);
     }
     RV_EV(6);
@@ -3234,8 +3287,9 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                  r->full, nullptr, &to_sub, xs, nullptr, r->mv_list, acnt));
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
                                  r->sub, nullptr, nullptr, xs, nullptr, r->mv_list, acnt));
-    round_lists_kernel<<<kRoundGrid, 256, 0, xs>>>(cg, r->sub, nsingle, r->cand_list,
-                                                   r->cand_count, r->mv_list, acnt);
+    round_lists_kernel<<<kRoundGrid, 256, 0, xs>>>(
+        cg, r->sub, nsingle, r->cand_list, r->cand_count, r->mv_list, acnt,
+        CandKeys{r->cand_key, (uint32_t)(r->coded + 1), r->cand_reuse ? 1 : 0});
     // F4 (full grids: a workgroup past the device counts exits at once)
     RV_R(rv_rdo_candidates(la4, ca4, g.hbd, xs));
     if (cg.comp) {
