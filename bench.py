@@ -639,7 +639,10 @@ def main():
                         "the search's rate predictors) in coding-order rounds: round 0 evaluates "
                         "every superblock, a later round the ones whose stacks changed",
                 "rounds_per_frame": round(cnt[14] / max(1, cnt[16]), 3),
-                "reevaluated_sb_per_frame": round(cnt[15] / max(1, cnt[16]), 2)}}
+                "reevaluated_sb_per_frame": round(cnt[15] / max(1, cnt[16]), 2),
+                "outer_passes_per_frame": round(cnt[17] / max(1, cnt[16]), 3) if len(cnt) > 17
+                else None,
+                "round_bound": "tws + 2 ths - 2 evaluation rounds per run (DESIGN.md §3)"}}
                if speed == 10 and len(cnt) > 16 else {}),
             "importances": ({
                 "window": imp_window,

@@ -106,6 +106,9 @@ struct DsArgs {
   const int32_t *alist;
   const int32_t *acount;
   int lper;
+  // list-driven rounds: a listed job with dirty[job] == 0 keeps its result
+  // (its inputs did not change; null: every listed job runs)
+  const uint8_t *dirty;
 };
 
 // The ordinal-th job of a list-driven launch (its size: ds_list_total)
@@ -685,7 +688,9 @@ __device__ __forceinline__ void ds_fast_jobs(const DsArgs &a) {
   }
   const int total = ds_list_total(a);
   for (int i = blockIdx.x; i < total; i += gridDim.x) {
-    ds_fast_body<Px, W, H, SUB>(a, __builtin_amdgcn_readfirstlane(ds_list_job(a, i)));
+    const int job = __builtin_amdgcn_readfirstlane(ds_list_job(a, i));
+    if (a.dirty && !a.dirty[job]) continue;  // uniform: its inputs are unchanged
+    ds_fast_body<Px, W, H, SUB>(a, job);
     __syncthreads();  // the job's LDS reads end before the next job's writes
   }
 }
@@ -1485,7 +1490,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             int subpixel, int use_satd, int allow_hp, int bit_depth,
                             rv_fs_result *d_out, uint32_t *d_evals, const ChainNext *next,
                             void *stream, const uint8_t *active, const int32_t *alist,
-                            const int32_t *acount, int lper) {
+                            const int32_t *acount, int lper, const uint8_t *dirty) {
   auto p2 = [](int v) { return v >= 4 && v <= 128 && (v & (v - 1)) == 0; };
   if (!org || !refs || n_refs < 1 || n_refs > RV_MAX_REFS || n_per_ref < 0 || !p2(blk_w) ||
       !p2(blk_h) || (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
@@ -1515,6 +1520,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
   a.alist = alist;
   a.acount = acount;
   a.lper = lper;
+  a.dirty = alist ? dirty : nullptr;
   if (alist && (!acount || lper < 0 || use_satd ||
                 !((blk_w == 64 && blk_h == 64) || (blk_w == 16 && blk_h == 16 && !subpixel))))
     return rv_set_error(RV_EINVAL,
@@ -1558,7 +1564,7 @@ extern "C" int rv_diamond_search_batch(const rv_plane *org, const rv_plane *ref,
   if (!ref) return rv_set_error(RV_EINVAL, "rv_diamond_search_batch: null ref");
   return rv_diamond_search_multi(org, ref, 1, d_jobs, n, blk_w, blk_h, subpixel, use_satd,
                                  allow_hp, bit_depth, d_out, nullptr, nullptr, stream, nullptr,
-                                 nullptr, nullptr, 0);
+                                 nullptr, nullptr, 0, nullptr);
 }
 
 // telescopic_subpel_search (src/me.rs:858-941) for every job in one launch:

@@ -58,6 +58,10 @@ struct MvrefArgs {
   const rv_fs_result *hq;       // quadrant MVs (half-res) [R][nsb][4]
   const rv_mv *prev;            // the LAST reference's field, [h_in_b/2][w_in_b/2][R]; null: none
   int edge_ok;                  // the frame-edge leaves are final (lwin / lsub readable)
+  // out (null: none): per F3 job [R][nsb], 1 = its predictor set or rate
+  // predictors (pmv) changed, so its full-pel and sub-pel searches must
+  // re-run; a listed superblock's other jobs keep their results
+  uint8_t *f3dirty;
 };
 
 // The decision record of superblock sb's winner (candidate c of the

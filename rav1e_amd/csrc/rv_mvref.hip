@@ -344,6 +344,7 @@ __global__ __launch_bounds__(256) void mvref_kernel(MvrefArgs a) {
   const int sb = t / kCheckLanes, j = t % kCheckLanes;
   const int lane = threadIdx.x & 63;
   bool changed = false;
+  uint32_t pmask = 0;  // lane 0: the references whose rate predictors changed
   const bool live = sb < a.nsb;
   if (live) {
     const int sx = sb % a.tw, sy = sb / a.tw;
@@ -370,6 +371,9 @@ __global__ __launch_bounds__(256) void mvref_kernel(MvrefArgs a) {
       if (nb.tl) nb.d = coded_at(a, sb - a.tw - 1, X - 4, Y - 4);
       const MvStack s = stacks_of(a, nb, split, fsx, fsy);
       changed = !same_stacks(a, a.stk[sb], s);
+      for (int k = 0; k < a.R; k++)
+        if (a.init || !mv_eq(a.stk[sb].s[k][0], s.s[k][0]) || !mv_eq(a.stk[sb].s[k][1], s.s[k][1]))
+          pmask |= 1u << k;
       if (changed) set_stacks(a, sb, s);  // (its pmv: the F3 jobs' rate predictors)
     } else if (a.epzs && j <= 5 * a.R) {
       changed = epzs_job(a, sb, fsx, fsy, j - 1);
@@ -378,6 +382,9 @@ __global__ __launch_bounds__(256) void mvref_kernel(MvrefArgs a) {
   // the superblock's lanes: any change marks it (lane 0 records and lists it)
   const uint64_t cm = __ballot(changed);
   const int g0 = lane & ~(kCheckLanes - 1);
+  const uint32_t pm = (uint32_t)__shfl((int)pmask, g0, 64);
+  if (a.f3dirty && live && j >= 1 && j <= a.R)  // F3 job j - 1: its set or its pmv
+    a.f3dirty[(size_t)(j - 1) * a.nsb + sb] = (changed || ((pm >> (j - 1)) & 1)) ? 1 : 0;
   const bool mark = live && ((cm >> g0) & ((1ull << kCheckLanes) - 1)) != 0;
   const bool lead = live && j == 0;
   if (lead) a.active[sb] = mark;

@@ -69,7 +69,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             rv_fs_result *d_out, uint32_t *d_evals, const rv::ChainNext *next,
                             void *stream, const uint8_t *active = nullptr,
                             const int32_t *alist = nullptr, const int32_t *acount = nullptr,
-                            int lper = 1);
+                            int lper = 1, const uint8_t *dirty = nullptr);
 // rv_deblock.hip
 int rv_deblock_plane_dev(const rv_plane *p, int pli, int width, int height, const uint8_t *d_lg,
                          const uint8_t *d_skip, int mi_stride, const uint8_t levels[4],
@@ -1140,6 +1140,7 @@ struct rv_replay {
   RdoWinner *win;
   int32_t *cand_list, *cand_count;  // F4: the valid candidates
   CandKey *cand_key = nullptr;       // F4: what each candidate slot was last evaluated with
+  uint8_t *f3dirty = nullptr;        // rounds: the F3 jobs whose set / pmv changed [R][nsb]
   bool cand_reuse = true;            // a round keeps the F4 outputs of an unchanged candidate
   uint32_t *cand_evals;  // [kRing][2 * kLevels]: F4 candidates per frame and level (single, compound)
   int32_t *l_lev, *c_lev;   // F6: committed levels
@@ -1910,6 +1911,8 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     ok = ok && r->cand_key && hipMemsetAsync(r->cand_key, 0, kb, r->stream) == hipSuccess;
     const char *e = getenv("RAV1E_HIP_F4_REUSE");  // =0: every round re-runs its F4 (A/B)
     r->cand_reuse = !(e && e[0] == '0');
+    r->f3dirty = (uint8_t *)dalloc(r, (size_t)g.nsb * g.R);
+    ok = ok && r->f3dirty;
   }
   r->cand_count = (int32_t *)dalloc(r, 8);  // [single, compound]
   r->cand_evals = (uint32_t *)dalloc(r, rv_replay::kRing * 2 * kLevels * 4);
@@ -3206,6 +3209,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     ma.hq = r->half_l;
     ma.prev = r->slots[fi.ref_display[0] % kSlots].fmv;  // the LAST reference's frame_mvs
     ma.edge_ok = 0;
+    ma.f3dirty = r->cand_reuse ? r->f3dirty : nullptr;
     // the first check marks every superblock (its count is not read)
     const uint32_t q = r->rr.seq++;
     ma.count = slot_cnt(q);
@@ -3283,10 +3287,13 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     // F2 of the listed superblocks (their 4 quadrants per reference)
     RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
                                  g.bd, r->half, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 4));
+    // F3 of the listed superblocks: only the jobs whose set or pmv changed
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
-                                 r->full, nullptr, &to_sub, xs, nullptr, r->mv_list, acnt));
+                                 r->full, nullptr, &to_sub, xs, nullptr, r->mv_list, acnt, 1,
+                                 ma.f3dirty));
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
-                                 r->sub, nullptr, nullptr, xs, nullptr, r->mv_list, acnt));
+                                 r->sub, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 1,
+                                 ma.f3dirty));
     round_lists_kernel<<<kRoundGrid, 256, 0, xs>>>(
         cg, r->sub, nsingle, r->cand_list, r->cand_count, r->mv_list, acnt,
         CandKeys{r->cand_key, (uint32_t)(r->coded + 1), r->cand_reuse ? 1 : 0});
