@@ -1114,9 +1114,12 @@ __device__ __forceinline__ void ds_grp_body(const DsArgs &a, const int ord, cons
   const int lane = threadIdx.x & 63;
   const int gl = lane % G::L, k = gl / G::C, c = gl % G::C;
   const int gbase = lane - gl;  // the group's first lane
-  const bool live = ord < nord;
-  const int oid = live ? ord : nord - 1;
+  const int oid = ord < nord ? ord : nord - 1;
   const int job = a.alist ? ds_list_job(a, oid) : oid;
+  // a listed job whose inputs did not change keeps its result; a wavefront
+  // whose jobs all do leaves (no workgroup barrier below)
+  const bool live = ord < nord && !(a.dirty && !a.dirty[job]);
+  if (__ballot(live) == 0) return;
   const int jid = job;
   const rv_ds_job *jp = a.jobs + jid;
   const rv_ds_job jb = *jp;

@@ -62,6 +62,7 @@ struct MvrefArgs {
   // predictors (pmv) changed, so its full-pel and sub-pel searches must
   // re-run; a listed superblock's other jobs keep their results
   uint8_t *f3dirty;
+  uint8_t *f2dirty;  // out (null: none): per F2 job [R][nsb][4], 1 = its set changed
 };
 
 // The decision record of superblock sb's winner (candidate c of the

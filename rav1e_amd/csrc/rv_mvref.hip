@@ -385,6 +385,10 @@ __global__ __launch_bounds__(256) void mvref_kernel(MvrefArgs a) {
   const uint32_t pm = (uint32_t)__shfl((int)pmask, g0, 64);
   if (a.f3dirty && live && j >= 1 && j <= a.R)  // F3 job j - 1: its set or its pmv
     a.f3dirty[(size_t)(j - 1) * a.nsb + sb] = (changed || ((pm >> (j - 1)) & 1)) ? 1 : 0;
+  if (a.f2dirty && live && j > a.R && j <= 5 * a.R) {  // F2 quadrant job (me_ss2's rate
+    const int e = j - 1 - a.R, k = e >> 2;             // predictor is the global MV: its set
+    a.f2dirty[((size_t)k * a.nsb + sb) * 4 + (e & 3)] = (changed || a.init) ? 1 : 0;  // alone)
+  }
   const bool mark = live && ((cm >> g0) & ((1ull << kCheckLanes) - 1)) != 0;
   const bool lead = live && j == 0;
   if (lead) a.active[sb] = mark;

@@ -1141,6 +1141,7 @@ struct rv_replay {
   int32_t *cand_list, *cand_count;  // F4: the valid candidates
   CandKey *cand_key = nullptr;       // F4: what each candidate slot was last evaluated with
   uint8_t *f3dirty = nullptr;        // rounds: the F3 jobs whose set / pmv changed [R][nsb]
+  uint8_t *f2dirty = nullptr;        // rounds: the F2 jobs whose set changed [R][nsb][4]
   bool cand_reuse = true;            // a round keeps the F4 outputs of an unchanged candidate
   uint32_t *cand_evals;  // [kRing][2 * kLevels]: F4 candidates per frame and level (single, compound)
   int32_t *l_lev, *c_lev;   // F6: committed levels
@@ -1912,7 +1913,8 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     const char *e = getenv("RAV1E_HIP_F4_REUSE");  // =0: every round re-runs its F4 (A/B)
     r->cand_reuse = !(e && e[0] == '0');
     r->f3dirty = (uint8_t *)dalloc(r, (size_t)g.nsb * g.R);
-    ok = ok && r->f3dirty;
+    r->f2dirty = (uint8_t *)dalloc(r, (size_t)g.nsb * g.R * 4);
+    ok = ok && r->f3dirty && r->f2dirty;
   }
   r->cand_count = (int32_t *)dalloc(r, 8);  // [single, compound]
   r->cand_evals = (uint32_t *)dalloc(r, rv_replay::kRing * 2 * kLevels * 4);
@@ -3210,6 +3212,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     ma.prev = r->slots[fi.ref_display[0] % kSlots].fmv;  // the LAST reference's frame_mvs
     ma.edge_ok = 0;
     ma.f3dirty = r->cand_reuse ? r->f3dirty : nullptr;
+    static const bool f2d = !(getenv("RAV1E_HIP_F2_DIRTY") && getenv("RAV1E_HIP_F2_DIRTY")[0] == '0');
+    ma.f2dirty = r->cand_reuse && f2d ? r->f2dirty : nullptr;
     // the first check marks every superblock (its count is not read)
     const uint32_t q = r->rr.seq++;
     ma.count = slot_cnt(q);
@@ -3286,7 +3290,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     const int32_t *acnt = slot_cnt(q);
     // F2 of the listed superblocks (their 4 quadrants per reference)
     RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
-                                 g.bd, r->half, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 4));
+                                 g.bd, r->half, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 4,
+                                 ma.f2dirty));
     // F3 of the listed superblocks: only the jobs whose set or pmv changed
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
                                  r->full, nullptr, &to_sub, xs, nullptr, r->mv_list, acnt, 1,
