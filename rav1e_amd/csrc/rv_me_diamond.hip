@@ -109,6 +109,9 @@ struct DsArgs {
   // list-driven rounds: a listed job with dirty[job] == 0 keeps its result
   // (its inputs did not change; null: every listed job runs)
   const uint8_t *dirty;
+  // list-driven: the workgroup pool (0: kDsListGrid; a round expected to
+  // list most jobs, e.g. the first after round 0, asks for a full grid)
+  int list_grid;
 };
 
 // The ordinal-th job of a list-driven launch (its size: ds_list_total)
@@ -1410,7 +1413,8 @@ bool try_grp(const DsArgs &a, hipStream_t s) {
   if (!(small || (a.satd && (n == 32 || n == 64)))) return false;
   const int jpw = 64 / (n == 8 || (n == 16 && !a.subpel && !a.satd) ? 16 : 64);
   unsigned grid = (unsigned)((a.n + 4 * jpw - 1) / (4 * jpw));
-  if (a.alist && grid > (unsigned)kDsListGrid) grid = kDsListGrid;
+  if (a.alist && grid > (unsigned)(a.list_grid ? a.list_grid : kDsListGrid))
+    grid = (unsigned)(a.list_grid ? a.list_grid : kDsListGrid);
 #define RV_GRP(N)                                                                     \
   if (n == N) {                                                                       \
     if (a.subpel) {                                                                   \
@@ -1445,7 +1449,8 @@ static bool ds_full_wave() {
 
 template <typename Px, int W, int H, bool SUB>
 void launch_fast(const DsArgs &a, hipStream_t s) {
-  const unsigned grid = a.alist ? (unsigned)std::min(a.n, kDsListGrid) : (unsigned)((a.n + 7) / 8 * 8);
+  const unsigned grid = a.alist ? (unsigned)std::min(a.n, a.list_grid ? a.list_grid : kDsListGrid)
+                                 : (unsigned)((a.n + 7) / 8 * 8);
   static const bool occ4 = [] {
     const char *e = getenv("RAV1E_HIP_DS_OCC4");
     return e && e[0] == '1';
@@ -1493,7 +1498,8 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             int subpixel, int use_satd, int allow_hp, int bit_depth,
                             rv_fs_result *d_out, uint32_t *d_evals, const ChainNext *next,
                             void *stream, const uint8_t *active, const int32_t *alist,
-                            const int32_t *acount, int lper, const uint8_t *dirty) {
+                            const int32_t *acount, int lper, const uint8_t *dirty,
+                            int list_grid) {
   auto p2 = [](int v) { return v >= 4 && v <= 128 && (v & (v - 1)) == 0; };
   if (!org || !refs || n_refs < 1 || n_refs > RV_MAX_REFS || n_per_ref < 0 || !p2(blk_w) ||
       !p2(blk_h) || (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
@@ -1524,6 +1530,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
   a.acount = acount;
   a.lper = lper;
   a.dirty = alist ? dirty : nullptr;
+  a.list_grid = list_grid;
   if (alist && (!acount || lper < 0 || use_satd ||
                 !((blk_w == 64 && blk_h == 64) || (blk_w == 16 && blk_h == 16 && !subpixel))))
     return rv_set_error(RV_EINVAL,
@@ -1567,7 +1574,7 @@ extern "C" int rv_diamond_search_batch(const rv_plane *org, const rv_plane *ref,
   if (!ref) return rv_set_error(RV_EINVAL, "rv_diamond_search_batch: null ref");
   return rv_diamond_search_multi(org, ref, 1, d_jobs, n, blk_w, blk_h, subpixel, use_satd,
                                  allow_hp, bit_depth, d_out, nullptr, nullptr, stream, nullptr,
-                                 nullptr, nullptr, 0, nullptr);
+                                 nullptr, nullptr, 0, nullptr, 0);
 }
 
 // telescopic_subpel_search (src/me.rs:858-941) for every job in one launch:

@@ -69,7 +69,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             rv_fs_result *d_out, uint32_t *d_evals, const rv::ChainNext *next,
                             void *stream, const uint8_t *active = nullptr,
                             const int32_t *alist = nullptr, const int32_t *acount = nullptr,
-                            int lper = 1, const uint8_t *dirty = nullptr);
+                            int lper = 1, const uint8_t *dirty = nullptr, int list_grid = 0);
 // rv_deblock.hip
 int rv_deblock_plane_dev(const rv_plane *p, int pli, int width, int height, const uint8_t *d_lg,
                          const uint8_t *d_skip, int mi_stride, const uint8_t levels[4],
@@ -3286,19 +3286,23 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // (r->mv_list, its count in the ring), each launch a fixed pool of
   // workgroups that loops over the device count -- a round of a few dozen
   // superblocks costs their latency, not a full grid of early exits.
+  // the first round of a run lists most superblocks (check 1 after round 0:
+  // 70-80 % at 2160p): its searches take full grids, later ones the pool
+  uint32_t q_first = 0;
   auto f3_f4_list = [&](hipStream_t xs, uint32_t q) -> int {
     const int32_t *acnt = slot_cnt(q);
+    const int lg = q == q_first ? nr * g.R : 0;
     // F2 of the listed superblocks (their 4 quadrants per reference)
     RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
                                  g.bd, r->half, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 4,
-                                 ma.f2dirty));
+                                 ma.f2dirty, lg));
     // F3 of the listed superblocks: only the jobs whose set or pmv changed
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
                                  r->full, nullptr, &to_sub, xs, nullptr, r->mv_list, acnt, 1,
-                                 ma.f3dirty));
+                                 ma.f3dirty, lg));
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
                                  r->sub, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 1,
-                                 ma.f3dirty));
+                                 ma.f3dirty, lg));
     round_lists_kernel<<<kRoundGrid, 256, 0, xs>>>(
         cg, r->sub, nsingle, r->cand_list, r->cand_count, r->mv_list, acnt,
         CandKeys{r->cand_key, (uint32_t)(r->coded + 1), r->cand_reuse ? 1 : 0});
@@ -3353,6 +3357,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       RV_H(hipEventRecord(r->ev_hp0, st));
       RV_H(hipStreamWaitEvent(r->hp, r->ev_hp0, 0));
     }
+    q_first = r->rr.seq;  // run_rounds' first check (its list: the first round)
     return rounds(
         xs, budget,
         [&](uint32_t q) {
