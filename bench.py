@@ -339,7 +339,9 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2):
     imp = [[] for _ in gs]
     for f in range(frames):
         timed = f > gop  # the second GOP on: every me_range_scale once per GOP
-        for k, g in enumerate(gs):
+        order = range(n - 1, -1, -1) if os.environ.get("RAV1E_BENCH_EMU_REVERSE") else range(n)
+        for k in order:  # (reversed: A/B of the first group's position)
+            g = gs[k]
             g.frame()
             sync()
             if timed:
@@ -357,6 +359,7 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2):
             sync()
             if timed:
                 imp[k].append((time.perf_counter() - t0) * 1e3)
+    cnts = [[int(v) for v in g.counters()] for g in gs]
     for g in gs:
         g.close()
     per = [sum(s) / len(s) for s in span]
@@ -372,6 +375,12 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2):
             "projected_ms_per_step": round(proj, 4),
             "projected_frames_per_s": round(1e3 / proj, 2),
             "frames_averaged": len(span[0]),
+            # per group, over all its frames: MV-stack rounds and re-evaluated
+            # superblocks per frame, outer passes, lookahead rounds
+            "group_rounds_per_frame": [round(c[14] / max(1, c[16]), 2) for c in cnts],
+            "group_reevaluated_sb_per_frame": [round(c[15] / max(1, c[16]), 1) for c in cnts],
+            "group_lookahead_rounds_per_frame": [round(c[18] / max(1, c[16]), 2) for c in cnts],
+            "group_order": "groups code each frame in index order (group 0 first)",
             "method": "one GPU, groups run one after another (HIP-event spans; import wall "
                       "clock incl. launch), device-copy all-gather"}
 

@@ -1116,6 +1116,13 @@ struct rv_replay {
   // RAV1E_HIP_MV_HP=1: the rounds after the first on a high-priority stream
   hipStream_t hp = nullptr;
   hipEvent_t ev_hp0 = nullptr, ev_hp1 = nullptr;
+  // RAV1E_HIP_ROUND_FORK=1: a round's independent launches on a second
+  // stream (F2 beside F3, the compound F4 beside the single-reference one).
+  // Off: 2160p A/B 144-148 vs 164-165 fps (r04q) -- with the twin and the
+  // lookahead engine the process already has more streams than hardware
+  // queues, and the fork's events cost more than the overlap gains
+  hipStream_t rs2 = nullptr;
+  hipEvent_t ev_rfork = nullptr, ev_rlists = nullptr, ev_rjoin = nullptr;
   // evaluation rounds (round 0 included), re-evaluated superblocks and
   // round runs (1 + the MV / intra passes) per frame, summed
   long mv_round_sum = 0, mv_reeval = 0, mv_run_sum = 0;
@@ -1772,6 +1779,7 @@ void rv_replay_destroy(rv_replay *r) {
   // stream running)
   if (r->stream) (void)hipStreamSynchronize(r->stream);
   if (r->side) (void)hipStreamSynchronize(r->side);
+  if (r->rs2) (void)hipStreamSynchronize(r->rs2);
   if (r->ecs) (void)hipStreamSynchronize(r->ecs);
   if (r->ech) {  // the host coder finishes the frames it holds, then stops
     {
@@ -1803,6 +1811,9 @@ void rv_replay_destroy(rv_replay *r) {
   if (r->ev_join) (void)hipEventDestroy(r->ev_join);
   if (r->ev_ielig) (void)hipEventDestroy(r->ev_ielig);
   if (r->side) (void)hipStreamDestroy(r->side);
+  if (r->rs2) (void)hipStreamDestroy(r->rs2);
+  for (hipEvent_t ev : {r->ev_rfork, r->ev_rlists, r->ev_rjoin})
+    if (ev) (void)hipEventDestroy(ev);
   if (r->hp) (void)hipStreamSynchronize(r->hp), (void)hipStreamDestroy(r->hp);
   if (r->ev_hp0) (void)hipEventDestroy(r->ev_hp0);
   if (r->ev_hp1) (void)hipEventDestroy(r->ev_hp1);
@@ -2082,6 +2093,12 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
            hipEventCreateWithFlags(&r->ev_hp0, hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&r->ev_hp1, hipEventDisableTiming) == hipSuccess;
     }
+    const char *rfe = getenv("RAV1E_HIP_ROUND_FORK");
+    if (rfe && rfe[0] == '1')
+      ok = ok && hipStreamCreateWithFlags(&r->rs2, hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev_rfork, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev_rlists, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev_rjoin, hipEventDisableTiming) == hipSuccess;
     // does a superblock's top-right neighbour (same tile) lie past the right
     // frame edge, i.e. is it a must_split leaf?
     for (int sb = 0; sb < g.nsb && r->lvl; sb++) {
@@ -3292,9 +3309,17 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   auto f3_f4_list = [&](hipStream_t xs, uint32_t q) -> int {
     const int32_t *acnt = slot_cnt(q);
     const int lg = q == q_first ? nr * g.R : 0;
+    // the check's F2 / F3 sets came from the state before this round, so F2
+    // and F3 are independent (F2's results feed the next check): F2 on the
+    // second stream
+    hipStream_t x2 = r->rs2 ? r->rs2 : xs;
+    if (r->rs2) {
+      RV_H(hipEventRecord(r->ev_rfork, xs));
+      RV_H(hipStreamWaitEvent(x2, r->ev_rfork, 0));
+    }
     // F2 of the listed superblocks (their 4 quadrants per reference)
     RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
-                                 g.bd, r->half, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 4,
+                                 g.bd, r->half, nullptr, nullptr, x2, nullptr, r->mv_list, acnt, 4,
                                  ma.f2dirty, lg));
     // F3 of the listed superblocks: only the jobs whose set or pmv changed
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
@@ -3306,6 +3331,10 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     round_lists_kernel<<<kRoundGrid, 256, 0, xs>>>(
         cg, r->sub, nsingle, r->cand_list, r->cand_count, r->mv_list, acnt,
         CandKeys{r->cand_key, (uint32_t)(r->coded + 1), r->cand_reuse ? 1 : 0});
+    if (r->rs2) {  // the lists are out: the compound F4 runs beside the single one
+      RV_H(hipEventRecord(r->ev_rlists, xs));
+      RV_H(hipStreamWaitEvent(x2, r->ev_rlists, 0));
+    }
     // F4 (full grids: a workgroup past the device counts exits at once)
     RV_R(rv_rdo_candidates(la4, ca4, g.hbd, xs));
     if (cg.comp) {
@@ -3315,7 +3344,11 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       lc.cand_base = cc.cand_base = 0;
       lc.n_tx = g.nsb * cg.comp;
       cc.n_tx = g.nsb * cg.comp * ntx_c;
-      RV_R(rv_rdo_candidates(lc, cc, g.hbd, xs, true));
+      RV_R(rv_rdo_candidates(lc, cc, g.hbd, x2, true));
+    }
+    if (r->rs2) {  // F2 and the compound F4 join before the argmin
+      RV_H(hipEventRecord(r->ev_rjoin, x2));
+      RV_H(hipStreamWaitEvent(xs, r->ev_rjoin, 0));
     }
     score_wave_kernel<<<kRoundGrid, 256, 0, xs>>>(
         g, cg, L.lambda, L.ds[1], L.ds[2], r->sub, r->l_out, r->c_out, r->c_out + nct * 3, ntx_c,

@@ -358,6 +358,21 @@ def test_gpu_replay_intra_matches_cpu(w, h, bd, tiling, seed):
 
 
 @pytest.mark.gpu
+def test_gpu_replay_intra_reruns_1080p():
+    """1080p with content that makes intra win: intra winners change their
+    neighbours' MV stacks, so frames need MV <-> intra outer passes (runs
+    beyond one per frame, rv_replay_counters [17]); every one stays within its
+    round budget (tws + 2 ths - 2) and the words equal the CPU
+    replay's raster-order coding."""
+    w, h, frames = 1920, 1080, 6
+    cnt = _gpu_vs_cpu(w, h, 1, 1, 8, 2, frames, {"tile_cols": 2},
+                      inputs=intra_frames(w, h, 1, 1, 8, frames + 8, seed=11), want_intra=True,
+                      quantizer=60)
+    runs, nonkey = int(cnt[17]), frames - 1
+    assert runs > nonkey, (runs, nonkey)  # some frame re-ran its MV rounds after the intra pass
+
+
+@pytest.mark.gpu
 def test_gpu_synth_equals_numpy_twin():
     import rav1e_amd as R
     R.require_device(0)
@@ -441,8 +456,10 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
         assert won > 0 and cnt[12] == won, (won, cnt[11:14])
     if imp_window:
         assert nz >= 2, nz  # the referenced frames carry importances
+    cnt = g.counters()
     g.close()
     c.close()
+    return cnt
 
 
 @pytest.mark.gpu

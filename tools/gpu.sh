@@ -4,8 +4,8 @@
 #   tools/gpu.sh suite TAG            -m gpu suite in one process, smoke(), default bench
 #   tools/gpu.sh tests TAG 'EXPR'     pytest -m gpu -k EXPR
 #   tools/gpu.sh bench TAG CFG... [-- ARGS]   one bench line per config (ARGS to each)
-#   tools/gpu.sh prof TAG CFG [ARGS]  kernel trace + FETCH / WRITE / SQ PMC passes of a
-#                                     short bench run of CFG (one rocprofv3 pass each, the
+#   tools/gpu.sh prof TAG CFG [ARGS]  kernel trace + FETCH / WRITE / SQ PMC passes of the
+#                                     bench run of CFG (default steps; one rocprofv3 pass each, the
 #                                     MI355X guide's rule: FETCH_SIZE and WRITE_SIZE do not
 #                                     share a pass)
 #   tools/gpu.sh envbench TAG CFG "ENV=.." ... [-- ARGS]  one bench line per environment (A/B)
@@ -36,7 +36,7 @@ case "$MODE" in
     exec bash "$R/tools/gpu_step.sh" "${steps[@]}" ;;
   prof)
     CFG=${1:-2160p}; shift
-    B="python3 $R/bench.py --config $CFG --no-cpu-baseline --emulate-ranks 0 --steps 8 --warmup 3 $*"
+    B="python3 $R/bench.py --config $CFG --no-cpu-baseline --emulate-ranks 0 $*"
     SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
     exec bash "$R/tools/gpu_step.sh" \
       "200 $TAG/trace.log cd /tmp && rocprofv3 --kernel-trace --stats -d $P/trace -o run -- $B" \

@@ -11,7 +11,7 @@ LOG="$R/profiles/${TAG}_oracle_sanitize.log"
 {
   echo "# oracle/build/librav1e_oracle_san.so: gcc $(gcc -dumpversion) -fsanitize=address,undefined -fno-sanitize-recover=all"
   echo "# git $(git -C "$R" rev-parse --short HEAD)$(git -C "$R" diff --quiet || echo +dirty), $(date -u +%FT%TZ)"
-  LD_PRELOAD="$(gcc -print-file-name=libasan.so)" \
+  LD_PRELOAD="$(gcc -print-file-name=libasan.so)${LD_PRELOAD:+:$LD_PRELOAD}" \
   ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 \
   UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \
   RAV1E_ORACLE_LIB="$R/oracle/build/librav1e_oracle_san.so" \
