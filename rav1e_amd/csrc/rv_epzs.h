@@ -48,70 +48,82 @@ __device__ inline rv_mv epzs_qfull(rv_mv m) {
 __device__ inline bool epzs_zero(rv_mv m) { return m.row == 0 && m.col == 0; }
 
 // get_subset_predictors of the block at tile offset (bx, by) of the tile at
-// frame 4x4 (tx4, ty4), mi_w columns: zero, the ncm coarse MVs cm, subsets
-// A / B through rd(X4, Y4) (the tile field at frame 4x4 (X4, Y4)), subset C
-// from prev (the reference frame's field at 8x8 granularity -- every value
-// of rav1e's field is constant over 8x8 cells at speed 10; null: none)
-// (cell (x, y) of prev at prev[((y * w_in_b / 2) + x) * pr]).  Writes the
-// set into out (<= RV_DS_MAX_PRED entries) and returns its size.  Every
-// field value is read once.
-template <typename Rd>
-__device__ inline int epzs_list(const EpzsGeo &g, int tx4, int ty4, int mi_w, int bx, int by,
-                                const rv_mv *cm, int ncm, Rd rd, const rv_mv *prev, int pr,
-                                rv_mv *out) {
+// frame 4x4 (tx4, ty4), mi_w columns: zero, the ncm (<= NCM) coarse MVs cm,
+// subsets A / B through rd(X4, Y4) (the tile field at frame 4x4 (X4, Y4)),
+// subset C from prev (the reference frame's field at 8x8 granularity --
+// every value of rav1e's field is constant over 8x8 cells at speed 10;
+// null: none) (cell (x, y) of prev at prev[((y * w_in_b / 2) + x) * pr]),
+// stored into job j (shr: every predictor >> 1, me_ss2) unless it already
+// holds that set; returns whether it changed.  The set's entries sit in 17
+// fixed slots (zero, 7 coarse, left, top, top-right, the mean, 5 of subset
+// C), each with a validity bit, so no local array is indexed at run time
+// (no scratch); the job's list is their compaction.  Every field value is
+// read once.
+template <int NCM, typename Rd>
+__device__ inline bool epzs_update(rv_ds_job *j, int shr, const EpzsGeo &g, int tx4, int ty4,
+                                   int mi_w, int bx, int by, const rv_mv (&cm)[NCM], int ncm,
+                                   Rd rd, const rv_mv *prev, int pr) {
+  static_assert(NCM >= 1 && 1 + NCM + 4 + 5 <= RV_DS_MAX_PRED, "slots");
+  constexpr int NS = 1 + NCM + 4 + 5;
   const bool hl = bx > 0, ht = by > 0, htr = ht && bx < mi_w - 1;
   const rv_mv z{0, 0};
   const rv_mv l = hl ? rd(tx4 + bx - 1, ty4 + by) : z;
   const rv_mv t = ht ? rd(tx4 + bx, ty4 + by - 1) : z;
   const rv_mv tr = htr ? rd(tx4 + bx + 1, ty4 + by - 1) : z;
-  int n = 0;
-  out[n++] = z;
-  for (int i = 0; i < ncm; i++) out[n++] = epzs_qfull(cm[i]);
-  if (hl && !epzs_zero(l)) out[n++] = l;
-  if (ht && !epzs_zero(t)) out[n++] = t;
-  if (htr && !epzs_zero(tr)) out[n++] = tr;
+  rv_mv c[NS];
+  uint32_t valid = 1;
+  c[0] = z;
+#pragma unroll
+  for (int i = 0; i < NCM; i++) {
+    c[1 + i] = epzs_qfull(cm[i]);
+    valid |= (uint32_t)(i < ncm) << (1 + i);
+  }
+  c[NCM + 1] = l;
+  c[NCM + 2] = t;
+  c[NCM + 3] = tr;
+  valid |= (uint32_t)(hl && !epzs_zero(l)) << (NCM + 1);
+  valid |= (uint32_t)(ht && !epzs_zero(t)) << (NCM + 2);
+  valid |= (uint32_t)(htr && !epzs_zero(tr)) << (NCM + 3);
   const int nm = (int)hl + (int)ht + (int)htr;
-  if (nm) {  // the mean: MotionVector Add / Div<i16> (truncating)
+  {  // the mean: MotionVector Add / Div<i16> (truncating)
     const int16_t sr = (int16_t)((int16_t)(l.row + t.row) + tr.row);
     const int16_t sc = (int16_t)((int16_t)(l.col + t.col) + tr.col);
-    const rv_mv q = epzs_qfull(rv_mv{(int16_t)(sr / nm), (int16_t)(sc / nm)});
-    if (!epzs_zero(q)) out[n++] = q;
+    const int d = nm ? nm : 1;
+    c[NCM + 4] = epzs_qfull(rv_mv{(int16_t)(sr / d), (int16_t)(sc / d)});
+    valid |= (uint32_t)(nm && !epzs_zero(c[NCM + 4])) << (NCM + 4);
   }
   if (prev) {
     const int fx = tx4 + bx, fy = ty4 + by, w8 = g.w_in_b >> 1;
     auto pv = [&](int x, int y) { return prev[((y >> 1) * w8 + (x >> 1)) * pr]; };
-    const rv_mv p0 = fx > 0 ? pv(fx - 1, fy) : z, p1 = fy > 0 ? pv(fx, fy - 1) : z;
-    const rv_mv p2 = fx < g.w_in_b - 1 ? pv(fx + 1, fy) : z;
-    const rv_mv p3 = fy < g.h_in_b - 1 ? pv(fx, fy + 1) : z, p4 = pv(fx, fy);
-    if (!epzs_zero(p0)) out[n++] = p0;
-    if (!epzs_zero(p1)) out[n++] = p1;
-    if (!epzs_zero(p2)) out[n++] = p2;
-    if (!epzs_zero(p3)) out[n++] = p3;
-    if (!epzs_zero(p4)) out[n++] = p4;
+    c[NCM + 5] = fx > 0 ? pv(fx - 1, fy) : z;
+    c[NCM + 6] = fy > 0 ? pv(fx, fy - 1) : z;
+    c[NCM + 7] = fx < g.w_in_b - 1 ? pv(fx + 1, fy) : z;
+    c[NCM + 8] = fy < g.h_in_b - 1 ? pv(fx, fy + 1) : z;
+    c[NCM + 9] = pv(fx, fy);
+#pragma unroll
+    for (int i = NCM + 5; i < NS; i++) valid |= (uint32_t)!epzs_zero(c[i]) << i;
+  } else {
+#pragma unroll
+    for (int i = NCM + 5; i < NS; i++) c[i] = z;
   }
-  return n;
-}
-
-// Set p (n entries; shr: every predictor >> 1, me_ss2) into job j unless it
-// already holds it; returns whether it changed.
-__device__ inline bool epzs_store(rv_ds_job *j, const rv_mv *p, int n, int shr) {
-  auto tf = [&](rv_mv m) {
-    return shr ? rv_mv{(int16_t)(m.row >> 1), (int16_t)(m.col >> 1)} : m;
-  };
-  bool same = j->n_pred == n;
-  for (int i = 0; i < n && same; i++) same = mv_eq(j->pred[i], tf(p[i]));
-  if (same) return false;
-  for (int i = 0; i < n; i++) j->pred[i] = tf(p[i]);
+  auto tf = [&](rv_mv m) { return shr ? rv_mv{(int16_t)(m.row >> 1), (int16_t)(m.col >> 1)} : m; };
+  // compare with the job's list (global reads at the running count), then store
+  const int old_n = j->n_pred;
+  int n = 0;
+  bool same = true;
+#pragma unroll
+  for (int i = 0; i < NS; i++)
+    if ((valid >> i) & 1) {
+      same = same && n < old_n && mv_eq(j->pred[n], tf(c[i]));
+      n++;
+    }
+  if (same && n == old_n) return false;
+  n = 0;
+#pragma unroll
+  for (int i = 0; i < NS; i++)
+    if ((valid >> i) & 1) j->pred[n++] = tf(c[i]);
   j->n_pred = n;
   return true;
-}
-
-// The set gen(out) builds into job j (see epzs_store)
-template <typename Gen>
-__device__ inline bool epzs_set(rv_ds_job *j, int shr, Gen gen) {
-  rv_mv p[RV_DS_MAX_PRED];
-  const int n = gen(p);
-  return epzs_store(j, p, n, shr);
 }
 
 // The round checks' counts: check q counts into cnt[0..1] (slot q of the

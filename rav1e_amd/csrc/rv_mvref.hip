@@ -299,26 +299,24 @@ __device__ inline bool epzs_job(const MvrefArgs &a, int sb, int fsx, int fsy, in
   auto rd = [&](int X4, int Y4) { return enc_field(a, k, X4, Y4, fsx, fsy); };
   const rv_mv *prev = a.prev ? a.prev + k : nullptr;
   if (j < a.R) {  // F3: full_pixel_me of the 64x64 (src/me.rs:390-431), cmvs = [pmvs[0]]
-    const rv_mv cm = coarse4(a, k, sb);
-    return epzs_set(a.jf + (size_t)k * a.nsb + sb, 0, [&](rv_mv *o) {
-      return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, tsx * 16, tsy * 16, &cm, 1, rd, prev, a.R,
-                       o);
-    });
+    const rv_mv cm[1] = {coarse4(a, k, sb)};
+    return epzs_update(a.jf + (size_t)k * a.nsb + sb, 0, a.eg, t0x * 16, t0y * 16, mi_w, tsx * 16,
+                       tsy * 16, cm, 1, rd, prev, a.R);
   }
   // F2: me_ss2 of quadrant q (src/me.rs:465-519), adjust_bo'd, cmvs = the
   // coarse MVs of the superblock and its neighbour on each side
   const int q = (j - a.R) & 3;
   const int tsw = (mi_w + 15) / 16, tsh = (mi_h + 15) / 16;
-  rv_mv cm[3];
-  int nc = 0;
-  cm[nc++] = coarse4(a, k, sb);
-  if ((q & 1) ? tsx < tsw - 1 : tsx > 0) cm[nc++] = coarse4(a, k, (q & 1) ? sb + 1 : sb - 1);
-  if ((q >> 1) ? tsy < tsh - 1 : tsy > 0) cm[nc++] = coarse4(a, k, (q >> 1) ? sb + a.tw : sb - a.tw);
+  // [own, horizontal neighbour if any, vertical neighbour if any] in static slots
+  const bool hh = (q & 1) ? tsx < tsw - 1 : tsx > 0, hv = (q >> 1) ? tsy < tsh - 1 : tsy > 0;
+  const rv_mv ch = hh ? coarse4(a, k, (q & 1) ? sb + 1 : sb - 1) : rv_mv{0, 0};
+  const rv_mv cv = hv ? coarse4(a, k, (q >> 1) ? sb + a.tw : sb - a.tw) : rv_mv{0, 0};
+  const rv_mv cm[3] = {coarse4(a, k, sb), hh ? ch : cv, cv};
+  const int nc = 1 + (int)hh + (int)hv;
   int bx = tsx * 16 + (q & 1) * 8, by = tsy * 16 + (q >> 1) * 8;
   epzs_adjust_bo(mi_w, mi_h, bx, by, 32, 32);
-  return epzs_set(a.jh + ((size_t)k * a.nsb + sb) * 4 + q, 1, [&](rv_mv *o) {
-    return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, prev, a.R, o);
-  });
+  return epzs_update(a.jh + ((size_t)k * a.nsb + sb) * 4 + q, 1, a.eg, t0x * 16, t0y * 16, mi_w, bx,
+                     by, cm, nc, rd, prev, a.R);
 }
 
 // The coded frame's field: one thread per 8x8 cell of the group (inside the

@@ -388,11 +388,11 @@ __global__ __launch_bounds__(256) void la_check_kernel(LaArgs a) {
     sb_tile(g, sx, sy, t0x, t0y, mi_w, mi_h);
     const int fsx = g.tx0 + sx, fsy = g.ty0 + sy, tsx = fsx - t0x, tsy = fsy - t0y;
     const int tsw = (mi_w + 15) / 16, tsh = (mi_h + 15) / 16;
-    rv_mv cm[3];
-    int nc = 0;
-    cm[nc++] = la_coarse4(a, k, sb);
-    if ((q & 1) ? tsx < tsw - 1 : tsx > 0) cm[nc++] = la_coarse4(a, k, (q & 1) ? sb + 1 : sb - 1);
-    if ((q >> 1) ? tsy < tsh - 1 : tsy > 0) cm[nc++] = la_coarse4(a, k, (q >> 1) ? sb + g.tw : sb - g.tw);
+    const bool hh = (q & 1) ? tsx < tsw - 1 : tsx > 0, hv = (q >> 1) ? tsy < tsh - 1 : tsy > 0;
+    const rv_mv ch = hh ? la_coarse4(a, k, (q & 1) ? sb + 1 : sb - 1) : rv_mv{0, 0};
+    const rv_mv cv = hv ? la_coarse4(a, k, (q >> 1) ? sb + g.tw : sb - g.tw) : rv_mv{0, 0};
+    const rv_mv cm[3] = {la_coarse4(a, k, sb), hh ? ch : cv, cv};  // static slots
+    const int nc = 1 + (int)hh + (int)hv;
     int bx = tsx * 16 + (q & 1) * 8, by = tsy * 16 + (q >> 1) * 8;
     adjust_bo(mi_w, mi_h, bx, by, 32, 32);
     // the field: an earlier superblock's quadrant MV (estimate_motion_ss2's *
@@ -405,9 +405,8 @@ __global__ __launch_bounds__(256) void la_check_kernel(LaArgs a) {
           a.half_l[((size_t)k * g.nsb + gsb) * 4 + ((Y4 >> 3) & 1) * 2 + ((X4 >> 3) & 1)].best_mv;
       return rv_mv{(int16_t)(h.row * 2), (int16_t)(h.col * 2)};
     };
-    mh = epzs_set(a.jh + i, 1, [&](rv_mv *o) {
-      return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, nullptr, 1, o);
-    }) && !a.init;
+    mh = epzs_update(a.jh + i, 1, a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, nullptr, 1) &&
+         !a.init;
   } else if (i - nh < nl) {  // FL: estimate_motion of 16x16 block b (src/me.rs:337-390)
     const int j = i - nh;
     job = j;
@@ -418,12 +417,16 @@ __global__ __launch_bounds__(256) void la_check_kernel(LaArgs a) {
     const int tsx = g.tx0 + sx - t0x, tsy = g.ty0 + sy - t0y;
     rv_mv cm[6];
     int nc = 0;
-    for (int p = 1; p < 7; p++) {  // the coarse MV, the covering quadrant, 4 neighbours'
-      const int v = a.sl[8 * j + p];
-      if (v < 0) break;
-      const rv_mv m = (v & 1) ? a.half_l[v >> 1].best_mv : a.coarse[v >> 1].best_mv;
+    bool more = true;
+#pragma unroll
+    for (int p = 1; p < 7; p++) {  // the coarse MV, the covering quadrant, 4 neighbours' (a prefix)
+      const int v = more ? a.sl[8 * j + p] : -1;
+      more = more && v >= 0;
+      const rv_mv m = !more ? rv_mv{0, 0}
+                            : (v & 1) ? a.half_l[v >> 1].best_mv : a.coarse[v >> 1].best_mv;
       const int sc = (v & 1) ? 2 : 4;
-      cm[nc++] = rv_mv{(int16_t)(m.row * sc), (int16_t)(m.col * sc)};
+      cm[p - 1] = rv_mv{(int16_t)(m.row * sc), (int16_t)(m.col * sc)};
+      nc += more ? 1 : 0;
     }
     int bx = tsx * 16 + (b % 4) * 4, by = tsy * 16 + (b / 4) * 4;
     adjust_bo(mi_w, mi_h, bx, by, 16, 16);
@@ -434,9 +437,8 @@ __global__ __launch_bounds__(256) void la_check_kernel(LaArgs a) {
       return a.look[((size_t)k * g.nsb + gsb) * 16 + ((Y4 & 15) >> 2) * 4 + ((X4 & 15) >> 2)]
           .best_mv;
     };
-    ml = epzs_set(a.jl + j, 0, [&](rv_mv *o) {
-      return epzs_list(a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, nullptr, 1, o);
-    }) && !a.init;
+    ml = epzs_update(a.jl + j, 0, a.eg, t0x * 16, t0y * 16, mi_w, bx, by, cm, nc, rd, nullptr, 1) &&
+         !a.init;
   }
   const int lane = threadIdx.x & 63;
   const uint64_t below = (1ull << lane) - 1;

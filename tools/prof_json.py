@@ -45,6 +45,7 @@ def open_db(d):
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")  # rv_mvref.hip's kernels
     return name.split("(")[0].replace("void ", "").strip() or "(unnamed)"
 
 

@@ -43,7 +43,7 @@ def main():
     rows = load(a.dir)
     agg = collections.defaultdict(lambda: [0, 0.0, 0])
     for n, s, e, sc in rows:
-        k = n.split("(")[0][:70]
+        k = n.replace("(anonymous namespace)::", "").split("(")[0][:70]
         agg[k][0] += 1
         agg[k][1] += (e - s) / 1e6
         agg[k][2] = max(agg[k][2], sc)
