@@ -63,6 +63,7 @@ struct MvrefArgs {
   // re-run; a listed superblock's other jobs keep their results
   uint8_t *f3dirty;
   uint8_t *f2dirty;  // out (null: none): per F2 job [R][nsb][4], 1 = its set changed
+  int field_guess_la;  // the first check: the EPZS field from the quadrants alone (A/B)
 };
 
 // The decision record of superblock sb's winner (candidate c of the

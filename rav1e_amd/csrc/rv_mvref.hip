@@ -276,7 +276,7 @@ __device__ inline rv_mv enc_field(const MvrefArgs &a, int k, int X4, int Y4, int
   const bool edge = a.lvl && ((SX + 1) * 64 > a.W || (SY + 1) * 64 > a.H);
   BlkDec d;
   d.ref[0] = kIntraFrame;
-  if (!edge || a.edge_ok) d = coded_at(a, gsb, X4 * 4, Y4 * 4);
+  if ((!edge || a.edge_ok) && !(a.init && a.field_guess_la)) d = coded_at(a, gsb, X4 * 4, Y4 * 4);
   if (d.ref[0] != kIntraFrame && d.ref[0] - 1 == k) return d.mv[0];
   const rv_mv h = a.hq[((size_t)k * a.nsb + gsb) * 4 + ((Y4 >> 3) & 1) * 2 + ((X4 >> 3) & 1)].best_mv;
   return rv_mv{(int16_t)(h.row * 2), (int16_t)(h.col * 2)};

@@ -2477,12 +2477,15 @@ template <typename Check, typename Eval>
 static int run_rounds(RoundRing &rr, hipStream_t xs, int budget, Check &&check, Eval &&eval,
                long *nrounds, long *nre, bool *changed, const char *what, long frame, int level) {
   static const bool mv_trace = getenv("RAV1E_HIP_MV_TRACE") != nullptr;
+  // RAV1E_HIP_ROUNDS_AHEAD=n: rounds queued beyond the last count read (A/B)
+  static const int ahead = getenv("RAV1E_HIP_ROUNDS_AHEAD") ? atoi(getenv("RAV1E_HIP_ROUNDS_AHEAD"))
+                                                            : rv_replay::kRoundsAhead;
   if (changed) *changed = false;
   const uint32_t first = rr.seq++;
   RV_R(check(first));
   int queued = 0;  // evaluation rounds queued (round j evaluates check j - 1's list)
   for (int seen = 0;; seen++) {
-    while (queued < budget && queued < seen + rv_replay::kRoundsAhead) {
+    while (queued < budget && queued < seen + (ahead > 0 ? ahead : 1)) {
       RV_R(eval(first + (uint32_t)queued));
       RV_R(check(rr.seq++));
       queued++;
@@ -3231,6 +3234,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     ma.prev = r->slots[fi.ref_display[0] % kSlots].fmv;  // the LAST reference's frame_mvs
     ma.edge_ok = 0;
     ma.f3dirty = r->cand_reuse ? r->f3dirty : nullptr;
+    static const bool gla = getenv("RAV1E_HIP_GUESS_LA") && getenv("RAV1E_HIP_GUESS_LA")[0] == '1';
+    ma.field_guess_la = gla ? 1 : 0;
     static const bool f2d = !(getenv("RAV1E_HIP_F2_DIRTY") && getenv("RAV1E_HIP_F2_DIRTY")[0] == '0');
     ma.f2dirty = r->cand_reuse && f2d ? r->f2dirty : nullptr;
     // the first check marks every superblock (its count is not read)
