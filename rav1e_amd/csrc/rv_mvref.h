@@ -102,4 +102,4 @@ int rv_mvref_round(const rv::MvrefArgs &a, hipStream_t s, bool scan = false);
 // the group's part, into field ([h_in_b/2][w_in_b/2][R] rv_mv).
 int rv_mvref_field(const rv::MvrefArgs &a, rv_mv *field, hipStream_t s);
 // The largest tile (superblocks) the scan takes.
-constexpr int kMvrefScanMaxSb = 65536 / (int)sizeof(rv::BlkDec);
+constexpr int kMvrefScanMaxSb = (65536 - 1024) / (int)sizeof(rv::BlkDec);  // + the scan's static LDS

@@ -291,12 +291,13 @@ __device__ inline rv_mv coarse4(const MvrefArgs &a, int k, int sb) {
 // EPZS job j of the superblock (j < R: F3 of reference j; then F2 quadrant
 // q of reference k at j = R + 4 k + q): its predictor set from the current
 // state into the job; returns whether it changed.
-__device__ inline bool epzs_job(const MvrefArgs &a, int sb, int fsx, int fsy, int j) {
+template <typename Fld>
+__device__ inline bool epzs_job_f(const MvrefArgs &a, int sb, int fsx, int fsy, int j, Fld fld) {
   int t0x, t0y, mi_w, mi_h;
   epzs_tile(a.eg, fsx, fsy, t0x, t0y, mi_w, mi_h);
   const int tsx = fsx - t0x, tsy = fsy - t0y;
   const int k = j < a.R ? j : (j - a.R) >> 2;
-  auto rd = [&](int X4, int Y4) { return enc_field(a, k, X4, Y4, fsx, fsy); };
+  auto rd = [&](int X4, int Y4) { return fld(k, X4, Y4); };
   const rv_mv *prev = a.prev ? a.prev + k : nullptr;
   if (j < a.R) {  // F3: full_pixel_me of the 64x64 (src/me.rs:390-431), cmvs = [pmvs[0]]
     const rv_mv cm[1] = {coarse4(a, k, sb)};
@@ -317,6 +318,11 @@ __device__ inline bool epzs_job(const MvrefArgs &a, int sb, int fsx, int fsy, in
   epzs_adjust_bo(mi_w, mi_h, bx, by, 32, 32);
   return epzs_update(a.jh + ((size_t)k * a.nsb + sb) * 4 + q, 1, a.eg, t0x * 16, t0y * 16, mi_w, bx,
                      by, cm, nc, rd, prev, a.R);
+}
+
+__device__ inline bool epzs_job(const MvrefArgs &a, int sb, int fsx, int fsy, int j) {
+  return epzs_job_f(a, sb, fsx, fsy, j,
+                    [&](int k, int X4, int Y4) { return enc_field(a, k, X4, Y4, fsx, fsy); });
 }
 
 // The coded frame's field: one thread per 8x8 cell of the group (inside the
@@ -427,32 +433,41 @@ __device__ inline BlkDec predict(BlkDec d, const MvStack &s, int M, int R) {
 // The tail rounds (few superblocks still changing, mostly along dependency
 // chains): one workgroup per tile scans its superblocks in anti-diagonal
 // wavefronts (x + 2 y = d: the left, above, top-right and top-left
-// neighbours lie on earlier ones).  A superblock whose stack held keeps its
-// evaluated decision; one whose stack changed is marked and, for the
-// superblocks after it, predicted (the same candidate under the new stack),
-// so a chain of changes is evaluated in one round when the predictions
-// hold.  The tile's decisions live in LDS.
-__global__ __launch_bounds__(64) void mvref_scan_kernel(MvrefArgs a) {
+// neighbours lie on earlier ones).  A superblock whose stack and EPZS sets
+// held keeps its evaluated decision; one whose stack changed is marked and,
+// for the superblocks after it, predicted (the same candidate under the new
+// stack), so a chain of changes is evaluated in one round when the
+// predictions hold.  The EPZS sets read the field of those (predicted)
+// decisions, or the quadrant results.  The tile's decisions live in LDS.
+// Per wavefront: (A) one thread per superblock, its stacks; (B) one thread
+// per (superblock, EPZS job); (C) one thread per superblock, the mark.
+constexpr int kScanThreads = 256, kScanMaxDiag = 64;
+__global__ __launch_bounds__(kScanThreads) void mvref_scan_kernel(MvrefArgs a) {
   extern __shared__ BlkDec pd[];
+  __shared__ uint8_t smark[kScanMaxDiag], sch[kScanMaxDiag];
+  __shared__ uint32_t spm[kScanMaxDiag];
   const int gtx = (a.tw + a.tws - 1) / a.tws;
   const int lx0 = (int)(blockIdx.x % gtx) * a.tws, ly0 = (int)(blockIdx.x / gtx) * a.ths;
   const int twd = min(a.tws, a.tw - lx0), tht = min(a.ths, a.th - ly0);
   const int ndiag = (twd - 1) + 2 * (tht - 1) + 1;
   const int t0x = a.tx0 + lx0, t0y = a.ty0 + ly0;
   const int cols = min(a.tws * 16, a.w_in_b - t0x * 16);
+  const int nj = a.epzs ? 5 * a.R : 0;  // EPZS jobs per superblock
+  auto is_split = [&](int SX, int SY) { return a.lvl && ((SX + 1) * 64 > a.W || (SY + 1) * 64 > a.H); };
   __syncthreads();
   for (int d = 0; d < ndiag; d++) {
     const int ylo = max(0, (d - twd + 2) / 2), yhi = min(tht - 1, d / 2);
-    for (int y = ylo + (int)threadIdx.x; y <= yhi; y += (int)blockDim.x) {
-      const int x = d - 2 * y;
+    const int nd = yhi - ylo + 1;  // superblocks on this wavefront (<= kScanMaxDiag)
+    // (A) stacks
+    for (int i = (int)threadIdx.x; i < nd; i += kScanThreads) {
+      const int y = ylo + i, x = d - 2 * y;
       const int sb = (ly0 + y) * a.tw + lx0 + x;
       const int fsx = t0x + x, fsy = t0y + y;
       const int X = fsx * 64, Y = fsy * 64, bx = x * 16, by = y * 16;
-      const bool split = a.lvl && (X + 64 > a.W || Y + 64 > a.H);
+      const bool split = is_split(fsx, fsy);
       // a neighbour: LDS (this tile), or a must_split leaf
       auto nbr = [&](int nx, int ny, int PX, int PY) -> BlkDec {
-        if (a.lvl && ((t0x + nx + 1) * 64 > a.W || (t0y + ny + 1) * 64 > a.H))
-          return coded_at(a, 0, PX, PY);
+        if (is_split(t0x + nx, t0y + ny)) return coded_at(a, 0, PX, PY);
         BlkDec v = pd[ny * twd + nx];
         if (a.iwas && a.iwas[(ly0 + ny) * a.tw + lx0 + nx]) v.ref[0] = kIntraFrame, v.ref[1] = kNoneFrame;
         return v;
@@ -466,17 +481,64 @@ __global__ __launch_bounds__(64) void mvref_scan_kernel(MvrefArgs a) {
       if (nb.left) nb.l = nbr(x - 1, y, X - 4, Y);
       if (nb.tr) nb.r = nbr(x + 1, y - 1, X + 64, Y - 4);
       if (nb.tl) nb.d = nbr(x - 1, y - 1, X - 4, Y - 4);
-      const MvStack s = stacks_of(a, nb, split, fsx, fsy);
-      const bool mark = !same_stacks(a, a.stk[sb], s);
-      a.active[sb] = mark;
+      const MvStack st = stacks_of(a, nb, split, fsx, fsy);
+      const bool mark = !same_stacks(a, a.stk[sb], st);
+      uint32_t pm = 0;
+      for (int k = 0; k < a.R; k++)
+        if (!mv_eq(a.stk[sb].s[k][0], st.s[k][0]) || !mv_eq(a.stk[sb].s[k][1], st.s[k][1]))
+          pm |= 1u << k;
       const BlkDec cur = a.dec[sb];
-      if (!mark) {
-        pd[y * twd + x] = cur;  // evaluated under this very stack
-      } else {
-        set_stacks(a, sb, s);
-        pd[y * twd + x] = predict(cur, s, kCandModes, a.R);
-        a.list[atomicAdd(a.count, 1)] = sb;  // the returned index orders it before the ticket
+      if (mark) set_stacks(a, sb, st);
+      pd[y * twd + x] = mark ? predict(cur, st, kCandModes, a.R) : cur;
+      smark[i] = mark;
+      sch[i] = 0;
+      spm[i] = pm;
+    }
+    __syncthreads();
+    // (B) the EPZS sets, the field from the tile's (predicted) decisions
+    for (int t = (int)threadIdx.x; t < nd * nj; t += kScanThreads) {
+      const int i = t / nj, j = t - i * nj;
+      const int y = ylo + i, x = d - 2 * y;
+      const int sb = (ly0 + y) * a.tw + lx0 + x;
+      const int fsx = t0x + x, fsy = t0y + y;
+      auto fld = [&](int k, int X4, int Y4) -> rv_mv {
+        const int SX = X4 >> 4, SY = Y4 >> 4;
+        if (SX == fsx && SY == fsy) return rv_mv{0, 0};  // its own quadrants: after its F2
+        const int gsb = (SY - a.ty0) * a.tw + (SX - a.tx0);
+        const int lx = SX - t0x, ly = SY - t0y;
+        BlkDec dd;
+        dd.ref[0] = kIntraFrame;
+        if (is_split(SX, SY)) {
+          if (a.edge_ok) dd = coded_at(a, gsb, X4 * 4, Y4 * 4);
+        } else if (lx >= 0 && lx < twd && ly >= 0 && ly < tht) {
+          dd = pd[ly * twd + lx];
+          if (a.iwas && a.iwas[gsb]) dd.ref[0] = kIntraFrame;
+        } else {
+          dd = coded_at(a, gsb, X4 * 4, Y4 * 4);
+        }
+        if (dd.ref[0] != kIntraFrame && dd.ref[0] - 1 == k) return dd.mv[0];
+        const rv_mv h = a.hq[((size_t)k * a.nsb + gsb) * 4 + ((Y4 >> 3) & 1) * 2 + ((X4 >> 3) & 1)].best_mv;
+        return rv_mv{(int16_t)(h.row * 2), (int16_t)(h.col * 2)};
+      };
+      const bool ch = epzs_job_f(a, sb, fsx, fsy, j, fld);
+      if (ch) sch[i] = 1;  // (any writer)
+      if (j < a.R) {
+        if (a.f3dirty) a.f3dirty[(size_t)j * a.nsb + sb] = (ch || ((spm[i] >> j) & 1)) ? 1 : 0;
+      } else if (a.f2dirty) {
+        const int e = j - a.R;
+        a.f2dirty[((size_t)(e >> 2) * a.nsb + sb) * 4 + (e & 3)] = ch ? 1 : 0;
       }
+    }
+    __syncthreads();
+    // (C) the mark (a superblock marked by its sets alone keeps its decision)
+    for (int i = (int)threadIdx.x; i < nd; i += kScanThreads) {
+      const int y = ylo + i, x = d - 2 * y;
+      const int sb = (ly0 + y) * a.tw + lx0 + x;
+      const bool mark = smark[i] || sch[i];
+      a.active[sb] = mark;
+      if (!a.epzs && a.f3dirty)
+        for (int k = 0; k < a.R; k++) a.f3dirty[(size_t)k * a.nsb + sb] = (spm[i] >> k) & 1;
+      if (mark) a.list[atomicAdd(a.count, 1)] = sb;  // the returned index orders it before the ticket
     }
     __syncthreads();  // the wavefront's decisions before the next one reads them
   }
@@ -486,12 +548,12 @@ __global__ __launch_bounds__(64) void mvref_scan_kernel(MvrefArgs a) {
 
 int rv_mvref_round(const MvrefArgs &a, hipStream_t s, bool scan) {
   if (a.nsb <= 0) return RV_OK;
-  if (scan && !a.init) {
-    if (a.epzs) return rv_set_error(RV_EINVAL, "rv_mvref_round: the scan does not track EPZS sets");
-    if (a.tws * a.ths > kMvrefScanMaxSb)
-      return rv_set_error(RV_EINVAL, "rv_mvref_round: the tile exceeds the scan's LDS");
+  // the scan: a tile's decisions in LDS, at most kScanMaxDiag superblocks
+  // per wavefront; otherwise the Jacobi check
+  const bool scan_ok = a.tws * a.ths <= kMvrefScanMaxSb && (a.ths < a.tws ? a.ths : a.tws) <= kScanMaxDiag;
+  if (scan && !a.init && scan_ok) {
     const int ntiles = ((a.tw + a.tws - 1) / a.tws) * ((a.th + a.ths - 1) / a.ths);
-    mvref_scan_kernel<<<ntiles, 64, (size_t)a.tws * a.ths * sizeof(BlkDec), s>>>(a);
+    mvref_scan_kernel<<<ntiles, kScanThreads, (size_t)a.tws * a.ths * sizeof(BlkDec), s>>>(a);
   } else {
     mvref_kernel<<<(a.nsb * kCheckLanes + 255) / 256, 256, 0, s>>>(a);
   }

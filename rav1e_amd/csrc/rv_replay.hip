@@ -3398,14 +3398,26 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       RV_H(hipStreamWaitEvent(r->hp, r->ev_hp0, 0));
     }
     q_first = r->rr.seq;  // run_rounds' first check (its list: the first round)
+    // Long chains (a change running down a tile's columns, one superblock
+    // row per Jacobi round: compound frames reach ~70 rounds at 2160p): from
+    // check kScanAfter on, up to kScanMax checks are the predictive scan
+    // (mvref_scan_kernel), which lets a chain run down in one round when the
+    // predicted decisions hold.  The Jacobi bound still holds after them, so
+    // the run's budget grows by kScanMax.
+    static const int scan_after = getenv("RAV1E_HIP_MV_SCAN_AFTER")
+                                      ? atoi(getenv("RAV1E_HIP_MV_SCAN_AFTER")) : 0;
+    constexpr int kScanMax = 8;
+    const bool scans = scan_after > 0;
     return rounds(
-        xs, budget,
+        xs, budget + (scans ? kScanMax : 0),
         [&](uint32_t q) {
           ma.init = 0;
           ma.iwas = iwas;
           ma.count = slot_cnt(q);
           ma.pub = r->rr.pub(q);
-          return rv_mvref_round(ma, xs);
+          const uint32_t c = q - q_first;
+          return rv_mvref_round(ma, xs, scans && c >= (uint32_t)scan_after &&
+                                            c < (uint32_t)(scan_after + kScanMax));
         },
         [&](uint32_t q) { return f3_f4_list(xs, q); }, &r->mv_round_sum, &r->mv_reeval, changed,
         "mvref");
