@@ -680,6 +680,15 @@ int rv_replay_set_importances(rv_replay *r, const float *host, int n);
  * ContextInner::compute_lookahead_data / receive_packet
  * (src/api/internal.rs:767-823, 1116). */
 int rv_replay_set_imp_window(rv_replay *r, int window, long limit);
+/* The inputs of displays 0 .. displays - 1 are in place (rv_replay_input /
+ * set) and stay until their frames are coded: the lookahead engine may run
+ * every frame they cover as far ahead as its ring allows (W + 13 frames
+ * past the oldest frame still being coded), instead of starting frame
+ * n + window only when frame n is asked for.  rav1e computes a frame's
+ * lookahead data as soon as the frame arrives (compute_lookahead_data,
+ * src/api/internal.rs:767-820).  At most the instance's n_inputs; no
+ * effect without a window.  Results are unchanged. */
+int rv_replay_set_inputs_ready(rv_replay *r, long displays);
 /* The block importances (f32 [h_imp][w_imp]) the last coded frame's RDO
  * used (zero without a window or input). */
 int rv_replay_get_importances(rv_replay *r, float *host, int n);
@@ -755,8 +764,9 @@ int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,
  * out[16] the frames; with cap >= 18, out[17] the round runs (1 + the MV /
  * intra passes of each frame); with cap >= 20, out[18] the lookahead's
  * EPZS rounds (round 0 included) and out[19] the jobs they re-ran (the
- * engine's, on the primary, with an importance window).  Returns the
- * count. */
+ * engine's, on the primary, with an importance window); with cap >= 21,
+ * out[20] the frames whose lookahead those rounds ran (the engine runs up to
+ * W frames ahead of the encode).  Returns the count. */
 int rv_replay_counters(rv_replay *r, uint64_t *out, int cap);
 
 /* ---------------------------------------------------------------------

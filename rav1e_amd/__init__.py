@@ -282,6 +282,7 @@ def _declare(L):
         "rv_replay_get_recon": (i32, [vp, i32, vp]),
         "rv_replay_set_importances": (i32, [vp, vp, i32]),
         "rv_replay_set_imp_window": (i32, [vp, i32, C.c_long]),
+        "rv_replay_set_inputs_ready": (i32, [vp, C.c_long]),
         "rv_replay_get_importances": (i32, [vp, vp, i32]),
         "rv_replay_frame": (i32, [vp, C.POINTER(RvReplayFrameInfo)]),
         "rv_replay_set_groups": (i32, [vp, i32, vp, i32, vp]),

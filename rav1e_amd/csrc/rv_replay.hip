@@ -1010,12 +1010,13 @@ struct RvLaEngine {
   std::mutex mu;
   std::condition_variable cv;
   long requested = 0;  // the highest frame an encode has asked for (0: none yet)
+  long inputs_ready = 0;  // the inputs of displays < this are in place (rv_replay_set_inputs_ready)
   long imp_ready = 0;  // the importances of frames <= imp_ready are recorded
   long imp_next = 1;
   bool stop = false;
   int err = 0;
   std::string msg;
-  long la_round_sum = 0, la_reeval = 0;
+  long la_round_sum = 0, la_reeval = 0, la_frames = 0;  // under mu
   Entry &at(long m) { return ring[(size_t)(m % RW)]; }
 };
 
@@ -1141,6 +1142,7 @@ struct rv_replay {
   rv_ds_job *jobs_half_l[3] = {nullptr, nullptr, nullptr};  // the lookahead's F2 (per level)
   int32_t *la_list = nullptr;  // the lookahead rounds' marked jobs: F2 [R nsb 4], then FL [R nsb 16]
   long la_round_sum = 0, la_reeval = 0;  // the lookahead rounds (round 0 included), re-evaluated jobs
+  long la_frames = 0;                    // ... and their frames
   RvLaEngine *eng = nullptr;  // the importance window's lookahead engine (null: W = 0)
   bool eng_owned = false;     // the primary owns it; a twin borrows it
   const float *imp_last = nullptr;  // the importances the last coded frame used
@@ -2648,8 +2650,15 @@ static int la_step(rv_replay *r, long m) {
     RV_H(hipMemcpyAsync(e.o.look, p.o.look, nr * 16 * sizeof(rv_fs_result),
                         hipMemcpyDeviceToDevice, xs));
   }
-  RV_R(lookahead_frame(r, E.rr, xs, fi, m - 1, e.o, E.la_list, false, &E.la_round_sum,
-                       &E.la_reeval, nullptr));
+  long la_rounds = 0, la_reeval = 0;
+  RV_R(lookahead_frame(r, E.rr, xs, fi, m - 1, e.o, E.la_list, false, &la_rounds, &la_reeval,
+                       nullptr));
+  {
+    std::lock_guard<std::mutex> lk(E.mu);
+    E.la_round_sum += la_rounds;
+    E.la_reeval += la_reeval;
+    E.la_frames++;
+  }
   rv_plane refs_o[RV_MAX_REFS];
   for (int k = 0; k < g.R; k++) refs_o[k] = r->inputs[fi.ref_display[k] % r->inputs.size()].y;
   RV_R(impwin_frame_data(r->inputs[fi.display % r->inputs.size()].y, refs_o, g.R, g.bd, e.o.look,
@@ -2693,7 +2702,11 @@ static void la_thread_main(rv_replay *r) {
       std::unique_lock<std::mutex> lk(E.mu);
       E.cv.wait(lk, [&] {
         if (E.stop) return true;
-        if (E.requested < 1 || m > E.requested + E.W) return false;
+        // frame m reads the inputs of displays <= 4 ((m - 1) / 4) + 4
+        // (frame_info): with them in place it may run before frame m - W
+        // is asked for, as rav1e computes a frame's lookahead on arrival
+        if (E.requested < 1) return false;
+        if (m > E.requested + E.W && 4 * ((m - 1) / 4) + 4 >= E.inputs_ready) return false;
         if (E.limit > 0 && m >= E.limit) return false;
         return m - E.RW < 1 || E.at(m).used_by == m - E.RW;
       });
@@ -2731,6 +2744,7 @@ static void la_engine_destroy(rv_replay *r) {
 }
 
 // The encode side: wait for frame n's importances, take its lookahead.
+// (rv_replay_set_inputs_ready below lets the engine run further ahead.)
 static int la_engine_take(rv_replay *r, long n, hipStream_t st, const float **imp) {
   RvLaEngine &E = *r->eng;
   {
@@ -2766,6 +2780,21 @@ static int la_engine_release(rv_replay *r, long n, hipStream_t st) {
 
 }  // extern "C" (closed for the C++ helpers above)
 extern "C" {
+
+// The inputs of displays < `displays` are in place and stay until coded:
+// the engine may run the lookahead of every frame they cover (up to its
+// ring), not only up to W frames past the last frame asked for.
+int rv_replay_set_inputs_ready(rv_replay *r, long displays) {
+  if (!r || displays < 0) return rv_set_error(RV_EINVAL, "rv_replay_set_inputs_ready: bad arguments");
+  if (displays > (long)r->inputs.size())
+    return rv_set_error(RV_EINVAL, "rv_replay_set_inputs_ready: more displays than input slots");
+  if (r->eng) {
+    std::lock_guard<std::mutex> lk(r->eng->mu);
+    r->eng->inputs_ready = displays;
+    r->eng->cv.notify_all();
+  }
+  return RV_OK;
+}
 
 // The importance window W (rdo_lookahead_frames) and the stream's length in
 // coded frames (limit; 0: unbounded).  W = 0: the importances are an input
@@ -2917,6 +2946,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   } else {
     RV_R(lookahead_frame(r, r->rr, st, fi, ncoded, LaOut{r->coarse, r->half_l, r->look}, r->la_list,
                          true, &r->la_round_sum, &r->la_reeval, tm ? e : nullptr));
+    r->la_frames++;
   }
   r->imp_last = imp;
   auto rounds = [&](hipStream_t xs, int budget, auto &&check, auto &&eval, long *nrounds,
@@ -3814,9 +3844,20 @@ int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
   if (cap < 20) return 18;
   // the lookahead's EPZS rounds and re-run jobs (the engine's on its owner)
   const bool own_eng = r->eng && r->eng_owned;
-  out[18] = (uint64_t)(r->la_round_sum + (own_eng ? r->eng->la_round_sum : 0));
-  out[19] = (uint64_t)(r->la_reeval + (own_eng ? r->eng->la_reeval : 0));
-  return 20;
+  long er = 0, ere = 0, ef = 0;
+  if (own_eng) {
+    std::lock_guard<std::mutex> lk(r->eng->mu);
+    er = r->eng->la_round_sum;
+    ere = r->eng->la_reeval;
+    ef = r->eng->la_frames;
+  }
+  out[18] = (uint64_t)(r->la_round_sum + er);
+  out[19] = (uint64_t)(r->la_reeval + ere);
+  if (cap < 21) return 20;
+  // the frames those lookahead rounds belong to (the engine runs ahead of
+  // the encode: up to W frames past the last coded one)
+  out[20] = (uint64_t)(r->la_frames + ef);
+  return 21;
 }
 
 // ---- RCCL communicator for the tile-group exchange ---------------------------

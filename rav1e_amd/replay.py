@@ -339,6 +339,13 @@ class HipReplay:
         _check(lib().rv_replay_get_recon(self.h, display, out.ctypes.data), "rv_replay_get_recon")
         return out
 
+    def set_inputs_ready(self, displays: int):
+        """The inputs of displays < `displays` are in place: the lookahead
+        engine may run ahead as far as its ring allows
+        (rv_replay_set_inputs_ready)."""
+        _check(lib().rv_replay_set_inputs_ready(self.h, int(displays)),
+               "rv_replay_set_inputs_ready")
+
     def set_importances(self, imp):
         if imp is None:
             _check(lib().rv_replay_set_importances(self.h, None, 0), "rv_replay_set_importances")
@@ -420,9 +427,10 @@ class HipReplay:
         intra-screened, intra winners, intra rounds] over the last <= 64
         frames, then (speed 10, since creation) the MV-stack rounds, the
         superblocks they re-evaluated, the frames, and the round runs (1 +
-        the MV / intra passes of each frame)."""
-        out = np.zeros(20, dtype=np.uint64)
-        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 20) - 20, "rv_replay_counters")
+        the MV / intra passes of each frame), the lookahead's EPZS rounds,
+        the jobs they re-ran and the frames they belong to."""
+        out = np.zeros(21, dtype=np.uint64)
+        _check(lib().rv_replay_counters(self.h, out.ctypes.data, 21) - 21, "rv_replay_counters")
         return out
 
     def close(self):

@@ -412,7 +412,7 @@ def intra_frames(w, h, xdec, ydec, bd, n, seed=7):
 
 
 def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=None, quantizer=100,
-                inputs=None, want_intra=False, imp_window=0):
+                inputs=None, want_intra=False, imp_window=0, ready=False):
     import rav1e_amd as R
     R.require_device(0)
     t = RP.tiling_for(w, h, **(tiling or {}))
@@ -424,6 +424,8 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
     if inputs is not None:
         for i in range(nin):
             g.set_input(i, inputs[i])
+    if ready:  # the engine may run ahead of the window (results unchanged)
+        g.set_inputs_ready(nin)
     c = O.CpuReplay(w, h, xdec, ydec, bd, refs, tile_size=ts, n_inputs=nin,
                     threads=O.cpu_share(), quantizer=quantizer,
                     speed=6 if flags & RP.RV_REPLAY_SPEED6 else 10,
@@ -505,18 +507,21 @@ def test_gpu_replay_importance_bias_and_quantizer(flags):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,h,bd,refs,tiling,flags,window", [
-    (256, 192, 8, 2, None, 0, 4),
-    (320, 136, 10, 2, {"tile_cols": 2}, 0, 6),
-    (256, 200, 8, 1, None, 0, 3),
-    (256, 200, 8, 2, None, RP.RV_REPLAY_SPEED6, 4),
-    (192, 128, 12, 2, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF, 2),
+@pytest.mark.parametrize("w,h,bd,refs,tiling,flags,window,ready", [
+    (256, 192, 8, 2, None, 0, 4, False),
+    (256, 192, 8, 2, None, 0, 4, True),
+    (320, 136, 10, 2, {"tile_cols": 2}, 0, 6, False),
+    (256, 200, 8, 1, None, 0, 3, True),
+    (256, 200, 8, 2, None, RP.RV_REPLAY_SPEED6, 4, False),
+    (192, 128, 12, 2, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF, 2, False),
 ])
-def test_gpu_replay_importance_window(w, h, bd, refs, tiling, flags, window):
+def test_gpu_replay_importance_window(w, h, bd, refs, tiling, flags, window, ready):
     """compute_block_importances over the lookahead window on the GPU's
     lookahead engine (its own thread, stream and round ring, W frames
-    ahead): every frame's importances and words equal the CPU replay's."""
-    _gpu_vs_cpu(w, h, 1, 1, bd, refs, 11, tiling, flags, quantizer=60, imp_window=window)
+    ahead; with every input ready, as far ahead as its ring allows): every
+    frame's importances and words equal the CPU replay's."""
+    _gpu_vs_cpu(w, h, 1, 1, bd, refs, 11, tiling, flags, quantizer=60, imp_window=window,
+                ready=ready)
 
 
 @pytest.mark.gpu
@@ -574,9 +579,11 @@ def test_gpu_tile_groups_exchange(flags):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("flags,window", [(0, 0), (RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF, 0),
-                                          (RP.RV_REPLAY_SPEED6, 0), (0, 5)])
-def test_gpu_paired_replay_matches_cpu(flags, window):
+@pytest.mark.parametrize("flags,window,ready", [(0, 0, False),
+                                                (RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF, 0, False),
+                                                (RP.RV_REPLAY_SPEED6, 0, False), (0, 5, False),
+                                                (0, 5, True)])
+def test_gpu_paired_replay_matches_cpu(flags, window, ready):
     """PairedReplay: the level-2 frames on a twin instance (shared DPB, own
     stream and host thread) give every frame's words and reconstruction of
     the sequential CPU replay -- checked frame by frame, then over a run
@@ -587,6 +594,8 @@ def test_gpu_paired_replay_matches_cpu(flags, window):
     speed = 6 if flags & RP.RV_REPLAY_SPEED6 else 10
     g = RP.HipReplay(w, h, n_inputs=nin, flags=flags, imp_window=window, imp_limit=21)
     g.synth_inputs(0)
+    if ready:
+        g.set_inputs_ready(nin)
     c = O.CpuReplay(w, h, n_inputs=nin, threads=O.cpu_share(), speed=speed,
                     deblock=bool(flags & RP.RV_REPLAY_DEBLOCK), cdef=bool(flags & RP.RV_REPLAY_CDEF),
                     imp_window=window, imp_limit=21)
