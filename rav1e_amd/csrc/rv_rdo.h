@@ -67,6 +67,10 @@ int rv_quant_ctx(int qindex, int tx_area, int is_intra, int bit_depth, int dc_de
 // transform blocks of planes U and V (32x32, SSE) in one launch.
 int rv_rdo_candidates(const rv::RdoArgs &luma, const rv::RdoArgs &chroma, int hbd,
                       hipStream_t s, bool compound = false);
+// The single-reference (l0, c0) and the compound (l1, c1) candidates in one
+// launch.
+int rv_rdo_candidates_pair(const rv::RdoArgs &l0, const rv::RdoArgs &c0, const rv::RdoArgs &l1,
+                           const rv::RdoArgs &c1, int hbd, hipStream_t s);
 
 // Blocks below 64x64 (speed 6): one launch over the tasks of a (luma or
 // the two chroma planes) for transform size n_tx_size; mode 0 single,

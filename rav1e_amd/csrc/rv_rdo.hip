@@ -1248,12 +1248,13 @@ __device__ __forceinline__ void rdo_quad_chroma(const RdoArgs &chroma, int c, in
                             reinterpret_cast<Px *>(w + 2 * 32 * 33 * 4), scan, pairs);
 }
 
+// One workgroup b of the quad launch: four luma candidates, or three
+// chroma pairs past nquads.  The arguments come by value: bound by
+// reference to the kernel's arguments they were copied to scratch memory
+// (1.5 KB per lane; by value the kernels keep the 16-20 B they had)
 template <typename Px, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_quad_kernel(
-    RdoArgs luma, RdoArgs chroma, int nquads, int var) {
-  __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
-  __shared__ uint16_t scan[1024];
-  const int b = blockIdx.x;
+__device__ __forceinline__ void rdo_quad_wg(RdoArgs luma, RdoArgs chroma, int nquads,
+                                            int var, int b, uint8_t *lds, uint16_t *scan) {
   // a workgroup past the compacted lists leaves before staging the scan:
   // the MV-stack rounds launch the full grid for a few dozen superblocks'
   // candidates (the device holds the count), so most workgroups exit here
@@ -1273,6 +1274,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     rdo_quad_chroma<Px, MODE>(chroma, b - nquads, (chroma.n_tx + 1) / 2, lds, scan);
   else
     rdo_quad_luma<Px, MODE>(luma, b, rdo_ntx(luma), var, lds, scan);
+}
+
+template <typename Px, int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_quad_kernel(
+    RdoArgs luma, RdoArgs chroma, int nquads, int var) {
+  __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
+  __shared__ uint16_t scan[1024];
+  rdo_quad_wg<Px, MODE>(luma, chroma, nquads, var, blockIdx.x, lds, scan);
+}
+
+// The single-reference (MODE 0) and the compound (MODE 1) candidates of a
+// frame in one launch: workgroups below g0 run the single ones, the rest the
+// compound ones.  They are independent, and in the MV-stack rounds each
+// launch holds a few dozen superblocks' candidates, so two launches in a row
+// cost two candidate latencies where one costs one.
+template <typename Px>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_quad_pair_kernel(
+    RdoArgs l0, RdoArgs c0, int nq0, int g0, RdoArgs l1, RdoArgs c1, int nq1, int var) {
+  __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
+  __shared__ uint16_t scan[1024];
+  if ((int)blockIdx.x < g0)
+    rdo_quad_wg<Px, 0>(l0, c0, nq0, var, blockIdx.x, lds, scan);
+  else
+    rdo_quad_wg<Px, 1>(l1, c1, nq1, var, blockIdx.x - g0, lds, scan);
 }
 
 }  // namespace rv
@@ -1415,6 +1440,35 @@ int rv_rdo_candidates(const RdoArgs &luma, const RdoArgs &chroma, int hbd, hipSt
     rdo_launch<1>(luma, chroma, hbd, s, single, cpairs);
   else
     rdo_launch<0>(luma, chroma, hbd, s, single, cpairs);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+// The single-reference and the compound candidates in one launch
+// (rdo_quad_pair_kernel); the 12-bit and RAV1E_HIP_RDO_SINGLE paths launch
+// them one after the other.
+int rv_rdo_candidates_pair(const RdoArgs &l0, const RdoArgs &c0, const RdoArgs &l1,
+                           const RdoArgs &c1, int hbd, hipStream_t s) {
+  static const bool single = [] {
+    const char *e = getenv("RAV1E_HIP_RDO_SINGLE");
+    return e && e[0] == '1';
+  }();
+  if (l0.bd == 12 || single || l0.commit) {
+    const int rc = rv_rdo_candidates(l0, c0, hbd, s, false);
+    return rc != RV_OK ? rc : rv_rdo_candidates(l1, c1, hbd, s, true);
+  }
+  static const int var = [] {
+    const char *e = getenv("RAV1E_HIP_RDO_VARIANT");
+    return e ? atoi(e) : 3;
+  }();
+  const unsigned cp0 = (unsigned)(2 * ((c0.n_tx + 1) / 2)), cp1 = (unsigned)(2 * ((c1.n_tx + 1) / 2));
+  const int nq0 = (l0.n_tx + 3) / 4, nq1 = (l1.n_tx + 3) / 4;
+  const unsigned g0 = (unsigned)nq0 + (cp0 + 2) / 3, g1 = (unsigned)nq1 + (cp1 + 2) / 3;
+  if (g0 + g1 == 0) return RV_OK;
+  if (hbd)
+    rdo_quad_pair_kernel<uint16_t><<<g0 + g1, 256, 0, s>>>(l0, c0, nq0, (int)g0, l1, c1, nq1, var);
+  else
+    rdo_quad_pair_kernel<uint8_t><<<g0 + g1, 256, 0, s>>>(l0, c0, nq0, (int)g0, l1, c1, nq1, var);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

@@ -2816,8 +2816,18 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
   E->W = window;
   E->RW = window + 1 + RvLaEngine::kLaSlack;
   E->limit = limit;
+  // The engine's stream takes the lowest priority: HIP keeps a queue pool per
+  // priority, so it gets a hardware queue of its own instead of sharing one
+  // (GPU_MAX_HW_QUEUES, 4 by default) with an encode instance's stream, whose
+  // round kernels would wait behind the lookahead's in the queue's order.
+  // RAV1E_HIP_LA_PRIORITY=0: a normal-priority stream (A/B).
+  const char *lpe = getenv("RAV1E_HIP_LA_PRIORITY");
+  const bool low = !(lpe && lpe[0] == '0');
+  int least = 0, greatest = 0;
   bool ok = hipGetDevice(&E->dev) == hipSuccess &&
-            hipStreamCreateWithFlags(&E->las, hipStreamNonBlocking) == hipSuccess &&
+            hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+            (low ? hipStreamCreateWithPriority(&E->las, hipStreamNonBlocking, least)
+                 : hipStreamCreateWithFlags(&E->las, hipStreamNonBlocking)) == hipSuccess &&
             round_ring_alloc(r, E->rr, E->las);
   const int ni = g.w_imp * g.h_imp, nr = g.nsb * g.R;
   E->la_list = ok ? (int32_t *)dalloc(r, (size_t)nr * 20 * 4) : nullptr;
@@ -3343,6 +3353,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // the first round of a run lists most superblocks (check 1 after round 0:
   // 70-80 % at 2160p): its searches take full grids, later ones the pool
   uint32_t q_first = 0;
+  // RAV1E_HIP_F4_PAIR=0: the rounds' single and compound F4 in two launches (A/B)
+  static const bool f4_pair = !(getenv("RAV1E_HIP_F4_PAIR") && getenv("RAV1E_HIP_F4_PAIR")[0] == '0');
   auto f3_f4_list = [&](hipStream_t xs, uint32_t q) -> int {
     const int32_t *acnt = slot_cnt(q);
     const int lg = q == q_first ? nr * g.R : 0;
@@ -3372,8 +3384,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       RV_H(hipEventRecord(r->ev_rlists, xs));
       RV_H(hipStreamWaitEvent(x2, r->ev_rlists, 0));
     }
-    // F4 (full grids: a workgroup past the device counts exits at once)
-    RV_R(rv_rdo_candidates(la4, ca4, g.hbd, xs));
+    // F4 (full grids: a workgroup past the device counts exits at once);
+    // on a compound frame the single and compound candidates in one launch
     if (cg.comp) {
       RdoArgs lc = la4, cc = ca4;
       lc.list = cc.list = r->cand_list + nsingle;
@@ -3381,7 +3393,14 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       lc.cand_base = cc.cand_base = 0;
       lc.n_tx = g.nsb * cg.comp;
       cc.n_tx = g.nsb * cg.comp * ntx_c;
-      RV_R(rv_rdo_candidates(lc, cc, g.hbd, x2, true));
+      if (f4_pair && !r->rs2) {
+        RV_R(rv_rdo_candidates_pair(la4, ca4, lc, cc, g.hbd, xs));
+      } else {
+        RV_R(rv_rdo_candidates(la4, ca4, g.hbd, xs));
+        RV_R(rv_rdo_candidates(lc, cc, g.hbd, x2, true));
+      }
+    } else {
+      RV_R(rv_rdo_candidates(la4, ca4, g.hbd, xs));
     }
     if (r->rs2) {  // F2 and the compound F4 join before the argmin
       RV_H(hipEventRecord(r->ev_rjoin, x2));

@@ -8,6 +8,7 @@
 #                                     bench run of CFG (default steps; one rocprofv3 pass each, the
 #                                     MI355X guide's rule: FETCH_SIZE and WRITE_SIZE do not
 #                                     share a pass)
+#   tools/gpu.sh trace TAG CFG [ARGS] the kernel trace pass alone
 #   tools/gpu.sh envbench TAG CFG "ENV=.." ... [-- ARGS]  one bench line per environment (A/B)
 #   tools/gpu.sh argbench TAG CFG "ARGS" ...  one bench line per argument set (A/B)
 #   tools/gpu.sh ubench TAG           tools/ubench binaries (VALU issue rates, PMC calibration)
@@ -43,6 +44,13 @@ case "$MODE" in
       "200 $TAG/fetch.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o run -- $B" \
       "200 $TAG/write.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $P/write -o run -- $B" \
       "200 $TAG/sq.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $SQ -d $P/sq -o run -- $B" \
+      "120 $TAG/gzip.log find $P -type f -size +256k ! -name '*.gz' -exec gzip -9 {} +" ;;
+  trace)
+    # kernel trace only: trace TAG CFG [ARGS]
+    CFG=${1:-2160p}; shift
+    B="python3 $R/bench.py --config $CFG --no-cpu-baseline --emulate-ranks 0 $*"
+    exec bash "$R/tools/gpu_step.sh" \
+      "200 $TAG/trace.log cd /tmp && rocprofv3 --kernel-trace --stats -d $P/trace -o run -- $B" \
       "120 $TAG/gzip.log find $P -type f -size +256k ! -name '*.gz' -exec gzip -9 {} +" ;;
   envbench)
     # one bench line per environment setting: envbench TAG CFG "A=1" "A=2 B=1" ... [-- ARGS]
