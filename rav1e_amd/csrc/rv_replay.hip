@@ -2816,13 +2816,14 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
   E->W = window;
   E->RW = window + 1 + RvLaEngine::kLaSlack;
   E->limit = limit;
-  // The engine's stream takes the lowest priority: HIP keeps a queue pool per
-  // priority, so it gets a hardware queue of its own instead of sharing one
-  // (GPU_MAX_HW_QUEUES, 4 by default) with an encode instance's stream, whose
-  // round kernels would wait behind the lookahead's in the queue's order.
-  // RAV1E_HIP_LA_PRIORITY=0: a normal-priority stream (A/B).
+  // RAV1E_HIP_LA_PRIORITY=1: the engine's stream at the lowest priority.
+  // HIP keeps a queue pool per priority, so it then gets a hardware queue of
+  // its own instead of sharing one (GPU_MAX_HW_QUEUES: 4) with the twin's
+  // stream.  Measured at 2160p (r04p1): 101-103 vs 118 fps -- the lookahead's
+  // kernels then run beside the rounds' and slow them more than the shared
+  // queue's ordering does; off.
   const char *lpe = getenv("RAV1E_HIP_LA_PRIORITY");
-  const bool low = !(lpe && lpe[0] == '0');
+  const bool low = lpe && lpe[0] == '1';
   int least = 0, greatest = 0;
   bool ok = hipGetDevice(&E->dev) == hipSuccess &&
             hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
