@@ -1405,6 +1405,39 @@ __global__ __launch_bounds__(256) void ds_grp_kernel(DsArgs a) {
     if (!a.alist) break;
   }
 }
+// A round's F2 (16x16 full-pel quadrants at half resolution, ds_grp) and
+// F3 full-pel (64x64, ds_fast) in one launch: they are independent, so the
+// round pays one search latency for both.  Workgroups below g2 run the F2
+// pool, the rest the F3 pool (both list-driven).  The arguments come by
+// value (bound by reference to kernel arguments they can land in scratch).
+template <typename Px>
+__device__ __forceinline__ void ds_grp16_pool(DsArgs a, int b, int gsz) {
+  using G = GrpGeo<16, true>;
+  constexpr int JPW = 64 / G::L;
+  const int lane = threadIdx.x & 63;
+  const int nord = ds_list_total(a);
+  for (int o = (b * 4 + (int)(threadIdx.x >> 6)) * JPW; o < nord; o += gsz * 4 * JPW)
+    ds_grp_body<Px, 16, false, false>(a, o + lane / G::L, nord);
+}
+template <typename Px>
+__device__ __forceinline__ void ds_fast64_pool(DsArgs a, int b, int gsz) {
+  const int total = ds_list_total(a);
+  for (int i = b; i < total; i += gsz) {
+    const int job = __builtin_amdgcn_readfirstlane(ds_list_job(a, i));
+    if (a.dirty && !a.dirty[job]) continue;
+    ds_fast_body<Px, 64, 64, false>(a, job);
+    __syncthreads();
+  }
+}
+template <typename Px>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void ds_f2_f3_kernel(
+    DsArgs f2, DsArgs f3, int g2) {
+  if ((int)blockIdx.x < g2)
+    ds_grp16_pool<Px>(f2, blockIdx.x, g2);
+  else
+    ds_fast64_pool<Px>(f3, (int)blockIdx.x - g2, (int)gridDim.x - g2);
+}
+
 template <typename Px>
 bool try_grp(const DsArgs &a, hipStream_t s) {
   if (a.tele || a.w != a.h || a.active) return false;
@@ -1537,6 +1570,53 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                         "rv_diamond_search_multi: list-driven launches: 64x64, or 16x16 full-pel SAD");
   if (next) a.next = *next;
   return ds_dispatch(a, stream);
+}
+
+static void ds_fill(DsArgs &a, const rv_plane *org, const rv_plane *refs, int n_refs,
+                    const rv_ds_job *d_jobs, int n_per_ref, int blk, rv_fs_result *d_out,
+                    int bit_depth, const int32_t *alist, const int32_t *acount, int lper,
+                    const uint8_t *dirty) {
+  memset(&a, 0, sizeof(a));
+  a.org = *org;
+  for (int k = 0; k < n_refs; k++) a.ref[k] = refs[k];
+  a.jobs = d_jobs;
+  a.out = d_out;
+  a.n = n_refs * n_per_ref;
+  a.n_per_ref = n_per_ref;
+  a.w = a.h = blk;
+  a.bd = bit_depth;
+  a.alist = alist;
+  a.acount = acount;
+  a.lper = lper;
+  a.dirty = dirty;
+}
+
+// A round's list-driven F2 (16x16 full-pel SAD on the half-resolution
+// planes) and F3 full-pel (64x64 SAD) in one launch (ds_f2_f3_kernel);
+// pools of list_grid workgroups each (0: kDsListGrid).
+int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_job *jobs_h,
+                     rv_fs_result *out_h, const uint8_t *dirty_h, const rv_plane *org,
+                     const rv_plane *refs, const rv_ds_job *jobs, rv_fs_result *out,
+                     const uint8_t *dirty, const ChainNext *next, int n_refs, int n_per_ref,
+                     int bit_depth, const int32_t *alist, const int32_t *acount, int list_grid,
+                     void *stream) {
+  if (!org_h || !refs_h || !org || !refs || n_refs < 1 || n_refs > RV_MAX_REFS || n_per_ref <= 0 ||
+      !alist || !acount || org->hbd != org_h->hbd)
+    return rv_set_error(RV_EINVAL, "rv_diamond_f2_f3: bad arguments");
+  DsArgs f2, f3;
+  ds_fill(f2, org_h, refs_h, n_refs, jobs_h, n_per_ref * 4, 16, out_h, bit_depth, alist, acount, 4,
+          dirty_h);
+  ds_fill(f3, org, refs, n_refs, jobs, n_per_ref, 64, out, bit_depth, alist, acount, 1, dirty);
+  if (next) f3.next = *next;
+  const int pool = list_grid ? list_grid : kDsListGrid;
+  const int g2 = std::min(pool, (f2.n + 15) / 16), g3 = std::min(f3.n, pool);
+  hipStream_t s = rv_resolve_stream(stream);
+  if (org->hbd)
+    ds_f2_f3_kernel<uint16_t><<<g2 + g3, 256, 0, s>>>(f2, f3, g2);
+  else
+    ds_f2_f3_kernel<uint8_t><<<g2 + g3, 256, 0, s>>>(f2, f3, g2);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
 }
 
 // Launch a filled DsArgs: the wavefront-per-candidate fast path where it

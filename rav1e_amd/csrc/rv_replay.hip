@@ -70,6 +70,12 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             void *stream, const uint8_t *active = nullptr,
                             const int32_t *alist = nullptr, const int32_t *acount = nullptr,
                             int lper = 1, const uint8_t *dirty = nullptr, int list_grid = 0);
+int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_job *jobs_h,
+                     rv_fs_result *out_h, const uint8_t *dirty_h, const rv_plane *org,
+                     const rv_plane *refs, const rv_ds_job *jobs, rv_fs_result *out,
+                     const uint8_t *dirty, const rv::ChainNext *next, int n_refs, int n_per_ref,
+                     int bit_depth, const int32_t *alist, const int32_t *acount, int list_grid,
+                     void *stream);
 // rv_deblock.hip
 int rv_deblock_plane_dev(const rv_plane *p, int pli, int width, int height, const uint8_t *d_lg,
                          const uint8_t *d_skip, int mi_stride, const uint8_t levels[4],
@@ -3356,6 +3362,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   uint32_t q_first = 0;
   // RAV1E_HIP_F4_PAIR=0: the rounds' single and compound F4 in two launches (A/B)
   static const bool f4_pair = !(getenv("RAV1E_HIP_F4_PAIR") && getenv("RAV1E_HIP_F4_PAIR")[0] == '0');
+  // RAV1E_HIP_F2_F3=0: the rounds' F2 and F3 full-pel searches in two launches (A/B)
+  static const bool f2_f3 = !(getenv("RAV1E_HIP_F2_F3") && getenv("RAV1E_HIP_F2_F3")[0] == '0');
   auto f3_f4_list = [&](hipStream_t xs, uint32_t q) -> int {
     const int32_t *acnt = slot_cnt(q);
     const int lg = q == q_first ? nr * g.R : 0;
@@ -3367,14 +3375,20 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       RV_H(hipEventRecord(r->ev_rfork, xs));
       RV_H(hipStreamWaitEvent(x2, r->ev_rfork, 0));
     }
-    // F2 of the listed superblocks (their 4 quadrants per reference)
-    RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0, 0,
-                                 g.bd, r->half, nullptr, nullptr, x2, nullptr, r->mv_list, acnt, 4,
-                                 ma.f2dirty, lg));
-    // F3 of the listed superblocks: only the jobs whose set or pmv changed
-    RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
-                                 r->full, nullptr, &to_sub, xs, nullptr, r->mv_list, acnt, 1,
-                                 ma.f3dirty, lg));
+    if (f2_f3 && !r->rs2) {  // F2 and F3 full-pel in one launch
+      RV_R(rv_diamond_f2_f3(&cur.hres, refs_h, r->jobs_half[lv], r->half, ma.f2dirty, &cur.y,
+                            refs_y, r->jobs_full[lv], r->full, ma.f3dirty, &to_sub, g.R, nr, g.bd,
+                            r->mv_list, acnt, lg, xs));
+    } else {
+      // F2 of the listed superblocks (their 4 quadrants per reference)
+      RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0,
+                                   0, g.bd, r->half, nullptr, nullptr, x2, nullptr, r->mv_list,
+                                   acnt, 4, ma.f2dirty, lg));
+      // F3 of the listed superblocks: only the jobs whose set or pmv changed
+      RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0,
+                                   g.bd, r->full, nullptr, &to_sub, xs, nullptr, r->mv_list, acnt,
+                                   1, ma.f3dirty, lg));
+    }
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
                                  r->sub, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 1,
                                  ma.f3dirty, lg));
