@@ -19,7 +19,8 @@ import os
 import numpy as np
 
 _ROOT = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_ROOT, "lib", "librav1e_hip.so")
+# RAV1E_HIP_LIB: another in-tree build of the same library (A/B benchmarks)
+LIB_PATH = os.environ.get("RAV1E_HIP_LIB") or os.path.join(_ROOT, "lib", "librav1e_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_ROOT), "include", "rav1e_hip.h")
 
 RV_OK, RV_EINVAL, RV_EHIP, RV_ENOTSUP = 0, -1, -2, -3

@@ -107,21 +107,36 @@ __device__ inline bool epzs_update(rv_ds_job *j, int shr, const EpzsGeo &g, int 
     for (int i = NCM + 5; i < NS; i++) c[i] = z;
   }
   auto tf = [&](rv_mv m) { return shr ? rv_mv{(int16_t)(m.row >> 1), (int16_t)(m.col >> 1)} : m; };
-  // compare with the job's list (global reads at the running count), then store
+  // the set by list position: slot i goes to position popcount(valid below
+  // i) -- a selection over static indices (a list indexed by a running
+  // count would live in scratch memory)
+  rv_mv nw[NS];
+#pragma unroll
+  for (int p = 0; p < NS; p++) nw[p] = z;
+#pragma unroll
+  for (int i = 0; i < NS; i++) {
+    const bool v = (valid >> i) & 1;
+    const int pos = __popc(valid & ((1u << i) - 1));
+    const rv_mv ti = tf(c[i]);
+#pragma unroll
+    for (int p = 0; p <= i; p++)
+      if (v && pos == p) nw[p] = ti;
+  }
+  const int n = __popc(valid);
+  // compare with the job's list: every entry read unconditionally, so the
+  // loads are in flight together (a compare that stops at the first
+  // difference issues them one after another)
+  rv_mv old[NS];
+#pragma unroll
+  for (int p = 0; p < NS; p++) old[p] = j->pred[p];
   const int old_n = j->n_pred;
-  int n = 0;
-  bool same = true;
+  bool same = old_n == n;
 #pragma unroll
-  for (int i = 0; i < NS; i++)
-    if ((valid >> i) & 1) {
-      same = same && n < old_n && mv_eq(j->pred[n], tf(c[i]));
-      n++;
-    }
-  if (same && n == old_n) return false;
-  n = 0;
+  for (int p = 0; p < NS; p++) same &= (p >= n) | mv_eq(old[p], nw[p]);
+  if (same) return false;
 #pragma unroll
-  for (int i = 0; i < NS; i++)
-    if ((valid >> i) & 1) j->pred[n++] = tf(c[i]);
+  for (int p = 0; p < NS; p++)
+    if (p < n) j->pred[p] = nw[p];
   j->n_pred = n;
   return true;
 }

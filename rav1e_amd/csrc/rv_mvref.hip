@@ -274,11 +274,13 @@ __device__ inline rv_mv enc_field(const MvrefArgs &a, int k, int X4, int Y4, int
   if (SX == fsx && SY == fsy) return rv_mv{0, 0};  // its own quadrants are saved after its F2
   const int gsb = (SY - a.ty0) * a.tw + (SX - a.tx0);
   const bool edge = a.lvl && ((SX + 1) * 64 > a.W || (SY + 1) * 64 > a.H);
+  // the quadrant's MV is read before the decision, not after it: the two
+  // loads are then in flight together
+  const rv_mv h = a.hq[((size_t)k * a.nsb + gsb) * 4 + ((Y4 >> 3) & 1) * 2 + ((X4 >> 3) & 1)].best_mv;
   BlkDec d;
   d.ref[0] = kIntraFrame;
   if ((!edge || a.edge_ok) && !(a.init && a.field_guess_la)) d = coded_at(a, gsb, X4 * 4, Y4 * 4);
   if (d.ref[0] != kIntraFrame && d.ref[0] - 1 == k) return d.mv[0];
-  const rv_mv h = a.hq[((size_t)k * a.nsb + gsb) * 4 + ((Y4 >> 3) & 1) * 2 + ((X4 >> 3) & 1)].best_mv;
   return rv_mv{(int16_t)(h.row * 2), (int16_t)(h.col * 2)};
 }
 
