@@ -2700,6 +2700,21 @@ static int la_step(rv_replay *r, long m) {
   return RV_OK;
 }
 
+// the engine's stream (RAV1E_HIP_LA_PRIORITY=1: the lowest priority, which
+// HIP serves from a queue pool of its own)
+static int la_stream_create(RvLaEngine *E) {
+  const char *lpe = getenv("RAV1E_HIP_LA_PRIORITY");
+  const bool low = lpe && lpe[0] == '1';
+  int least = 0, greatest = 0;
+  if (low) {
+    RV_H(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    RV_H(hipStreamCreateWithPriority(&E->las, hipStreamNonBlocking, least));
+  } else {
+    RV_H(hipStreamCreateWithFlags(&E->las, hipStreamNonBlocking));
+  }
+  return RV_OK;
+}
+
 static void la_thread_main(rv_replay *r) {
   RvLaEngine &E = *r->eng;
   (void)hipSetDevice(E.dev);
@@ -2718,7 +2733,8 @@ static void la_thread_main(rv_replay *r) {
       });
       if (E.stop) return;
     }
-    const int rc = la_step(r, m);
+    int rc = E.las ? RV_OK : la_stream_create(&E);
+    if (rc == RV_OK) rc = la_step(r, m);
     if (rc != RV_OK) {
       std::lock_guard<std::mutex> lk(E.mu);
       E.err = rc;
@@ -2828,14 +2844,17 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
   // stream.  Measured at 2160p (r04p1): 101-103 vs 118 fps -- the lookahead's
   // kernels then run beside the rounds' and slow them more than the shared
   // queue's ordering does; off.
-  const char *lpe = getenv("RAV1E_HIP_LA_PRIORITY");
-  const bool low = lpe && lpe[0] == '1';
-  int least = 0, greatest = 0;
+  //
+  // The stream is created on the engine's thread when the first frame is
+  // asked for, after the twin instance's streams: HIP gives a new stream the
+  // least-used hardware queue, so the engine's then shares one with a
+  // frame-edge or entropy stream instead of with the twin's round kernels
+  // (which the trace showed waiting 6-7 us behind the lookahead's).
+  // RAV1E_HIP_LA_LAZY=0: created here (A/B).
+  const char *lze = getenv("RAV1E_HIP_LA_LAZY");
+  const bool lazy = !(lze && lze[0] == '0');
   bool ok = hipGetDevice(&E->dev) == hipSuccess &&
-            hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
-            (low ? hipStreamCreateWithPriority(&E->las, hipStreamNonBlocking, least)
-                 : hipStreamCreateWithFlags(&E->las, hipStreamNonBlocking)) == hipSuccess &&
-            round_ring_alloc(r, E->rr, E->las);
+            (lazy || la_stream_create(E) == RV_OK) && round_ring_alloc(r, E->rr, r->stream);
   const int ni = g.w_imp * g.h_imp, nr = g.nsb * g.R;
   E->la_list = ok ? (int32_t *)dalloc(r, (size_t)nr * 20 * 4) : nullptr;
   E->scratch_bytes = impwin_scratch_bytes(ni);
@@ -2846,7 +2865,7 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
   for (auto &en : E->ring) {
     if (!ok) break;
     uint8_t *m = (uint8_t *)dalloc(r, ob + impwin_frame_bytes(ni, g.R));
-    ok = m && hipMemsetAsync(m, 0, ob, E->las) == hipSuccess &&
+    ok = m && hipMemsetAsync(m, 0, ob, r->stream) == hipSuccess &&
          hipEventCreateWithFlags(&en.ev_imp, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&en.ev_used, hipEventDisableTiming) == hipSuccess;
     if (!ok) break;
@@ -2858,7 +2877,7 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
   E->pyr_display.assign(r->inputs.size(), -1);
   r->eng = E;
   r->eng_owned = true;
-  if (!ok || hipStreamSynchronize(E->las) != hipSuccess) {
+  if (!ok || hipStreamSynchronize(r->stream) != hipSuccess) {
     la_engine_destroy(r);
     return rv_set_error(RV_EHIP, "rv_replay_set_imp_window: allocation failed");
   }
