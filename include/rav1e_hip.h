@@ -761,7 +761,8 @@ int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,
  * 14, out[11] superblocks intra-screened, out[12] intra winners, out[13]
  * intra rounds; with cap >= 17 (speed 10, since creation) out[14] the
  * MV-stack evaluation rounds, out[15] the superblocks they re-evaluated,
- * out[16] the frames; with cap >= 18, out[17] the round runs (1 + the MV /
+ * out[16] the frames this instance coded (a twin codes some of the
+ * stream's); with cap >= 18, out[17] the round runs (1 + the MV /
  * intra passes of each frame); with cap >= 20, out[18] the lookahead's
  * EPZS rounds (round 0 included) and out[19] the jobs they re-ran (the
  * engine's, on the primary, with an importance window); with cap >= 21,

@@ -1135,6 +1135,7 @@ struct rv_replay {
   // evaluation rounds (round 0 included), re-evaluated superblocks and
   // round runs (1 + the MV / intra passes) per frame, summed
   long mv_round_sum = 0, mv_reeval = 0, mv_run_sum = 0;
+  long mv_frames = 0;  // the frames this instance coded with the rounds (a twin codes some)
   size_t nwords = 0, wpart = 0;   // result words; offset of the partition masks
   bool jobs_built = false;
   std::vector<RvSlot> slots;
@@ -3595,6 +3596,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   if (r->exact) {
     r->mv_round_sum++;  // round 0
     r->mv_run_sum += mv_runs;
+    r->mv_frames++;
     // the encode's field becomes the frame's frame_mvs (the group's part;
     // the other groups' arrive with the exchange)
     ma.iwas = r->intra ? r->i_was : nullptr;
@@ -3889,7 +3891,7 @@ int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
   // superblock re-evaluations after the first round, frames
   out[14] = (uint64_t)r->mv_round_sum;
   out[15] = (uint64_t)r->mv_reeval;
-  out[16] = r->exact ? (uint64_t)nonkey : 0;
+  out[16] = (uint64_t)r->mv_frames;
   if (cap < 18) return 17;
   // round runs: 1 + the MV / intra passes (the joint fixed point's outer
   // iterations), summed over frames

@@ -12,6 +12,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import os
+
 import numpy as np
 
 from . import RvReplayCfg, RvReplayFrameInfo, RvReplayLevelParams, _check, lib
@@ -462,19 +464,28 @@ def frame_info(n: int, n_refs: int = 2) -> dict:
 
 class PairedReplay:
     """One stream coded by two instances of the same tile group: `primary`
-    codes the key frame and the pyramid's levels 0 / 1 (display 4g+4,
-    4g+2), its twin (rv_replay_create_twin: shared DPB and inputs) the
-    level-2 frames 4g+1 and 4g+3, which no frame references, on its own
-    stream and host thread.  Device events order the two: a level-2 frame of
+    codes the key frame, the pyramid's levels 0 / 1 (display 4g+4, 4g+2)
+    and (twin_levels "l2b", the default) the level-2 frame 4g+1; its twin
+    (rv_replay_create_twin: shared DPB and inputs) the level-2 frame 4g+3
+    ("l2": both level-2 frames), which no frame references, on its own
+    stream and host thread.  Device events order the two: a twin frame of
     group g after the primary's level-1 frame of g, the primary's level-0
     frame of g + 2 (its DPB slot is display 4g's) after the twin's group g.
     frame() / drain() / results() / counters() / close() follow HipReplay's
     interface for bench.timed_run.  The frames' results are the sequential
     ones (the orders only interleave independent frames)."""
 
-    def __init__(self, primary: "HipReplay"):
+    def __init__(self, primary: "HipReplay", twin_levels: str = None):
         import queue
         import threading
+        # which frames of a group the twin codes: "l2" both level-2 frames
+        # (4g+1, 4g+3), "l2b" only 4g+3 (the primary codes 4g+1 after 4g+2)
+        # (2160p: "l2b" 187 vs 163-166 fps for "l2", r04j2 -- the compound
+        # frames 4g+2 and 4g+3 carry the most MV-stack rounds, so "l2" left
+        # the twin with the heavier half)
+        self.twin_levels = twin_levels or os.environ.get("RAV1E_PAIRED_TWIN", "l2b")
+        if self.twin_levels not in ("l2", "l2b"):
+            raise ValueError(f"PairedReplay: twin_levels {self.twin_levels!r}")
         self.p = primary
         self.t = primary.twin()
         self.n = 0
@@ -487,6 +498,10 @@ class PairedReplay:
         self.worker = threading.Thread(target=self._run, daemon=True)
         self.worker.start()
 
+    def on_primary(self, j: int) -> bool:
+        """Frame j (0..3) of a group runs on the primary."""
+        return j < 2 or (j == 2 and self.twin_levels == "l2b")
+
     def _flag(self, d, g):
         if g not in d:
             d[g] = self._thr.Event()
@@ -498,7 +513,7 @@ class PairedReplay:
         if n == 0:
             return self.p.frame()
         g, j = (n - 1) // 4, (n - 1) % 4
-        if j >= 2:
+        if not self.on_primary(j):
             self.q.put(n)
             return frame_info(n, self.p.cfg.n_refs)
         if j == 0 and g >= 2:

@@ -579,11 +579,11 @@ def test_gpu_tile_groups_exchange(flags):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("flags,window,ready", [(0, 0, False),
-                                                (RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF, 0, False),
-                                                (RP.RV_REPLAY_SPEED6, 0, False), (0, 5, False),
-                                                (0, 5, True)])
-def test_gpu_paired_replay_matches_cpu(flags, window, ready):
+@pytest.mark.parametrize("flags,window,ready,twin", [
+    (0, 0, False, "l2"), (RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF, 0, False, "l2"),
+    (RP.RV_REPLAY_SPEED6, 0, False, "l2"), (0, 5, False, "l2"), (0, 5, True, "l2"),
+    (0, 5, True, "l2b"), (RP.RV_REPLAY_DEBLOCK, 0, False, "l2b")])
+def test_gpu_paired_replay_matches_cpu(flags, window, ready, twin):
     """PairedReplay: the level-2 frames on a twin instance (shared DPB, own
     stream and host thread) give every frame's words and reconstruction of
     the sequential CPU replay -- checked frame by frame, then over a run
@@ -601,13 +601,13 @@ def test_gpu_paired_replay_matches_cpu(flags, window, ready):
                     imp_window=window, imp_limit=21)
     for i in range(nin):
         c.set_input(i, g.get_input(i))
-    eng = RP.PairedReplay(g)
+    eng = RP.PairedReplay(g, twin_levels=twin)
     try:
         for n in range(11):  # frame by frame
             gi, ci = eng.frame(), c.frame()
             assert gi == ci, (n, gi, ci)
             eng.drain()
-            inst = eng.t if n and (n - 1) % 4 >= 2 else eng.p
+            inst = eng.p if not n or eng.on_primary((n - 1) % 4) else eng.t
             np.testing.assert_array_equal(inst.results(), c.results())
         for n in range(11, 21):  # free-running: the streams overlap
             eng.frame()
