@@ -484,7 +484,7 @@ class PairedReplay:
         # frames 4g+2 and 4g+3 carry the most MV-stack rounds, so "l2" left
         # the twin with the heavier half)
         self.twin_levels = twin_levels or os.environ.get("RAV1E_PAIRED_TWIN", "l2b")
-        if self.twin_levels not in ("l2", "l2b"):
+        if self.twin_levels not in ("l2", "l2b", "alt"):
             raise ValueError(f"PairedReplay: twin_levels {self.twin_levels!r}")
         self.p = primary
         self.t = primary.twin()
@@ -498,9 +498,16 @@ class PairedReplay:
         self.worker = threading.Thread(target=self._run, daemon=True)
         self.worker.start()
 
-    def on_primary(self, j: int) -> bool:
-        """Frame j (0..3) of a group runs on the primary."""
-        return j < 2 or (j == 2 and self.twin_levels == "l2b")
+    def on_primary(self, f: int) -> bool:
+        """Inter frame f (coded frame f + 1: group f // 4, frame j = f % 4
+        of it) runs on the primary.  "alt": the twin codes 4g+3, and 4g+1
+        of the odd groups."""
+        g, j = f // 4, f % 4
+        if j < 2:
+            return True
+        if j == 3:
+            return False
+        return self.twin_levels == "l2b" or (self.twin_levels == "alt" and g % 2 == 0)
 
     def _flag(self, d, g):
         if g not in d:
@@ -513,7 +520,7 @@ class PairedReplay:
         if n == 0:
             return self.p.frame()
         g, j = (n - 1) // 4, (n - 1) % 4
-        if not self.on_primary(j):
+        if not self.on_primary(n - 1):
             self.q.put(n)
             return frame_info(n, self.p.cfg.n_refs)
         if j == 0 and g >= 2:

@@ -582,7 +582,7 @@ def test_gpu_tile_groups_exchange(flags):
 @pytest.mark.parametrize("flags,window,ready,twin", [
     (0, 0, False, "l2"), (RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF, 0, False, "l2"),
     (RP.RV_REPLAY_SPEED6, 0, False, "l2"), (0, 5, False, "l2"), (0, 5, True, "l2"),
-    (0, 5, True, "l2b"), (RP.RV_REPLAY_DEBLOCK, 0, False, "l2b")])
+    (0, 5, True, "l2b"), (RP.RV_REPLAY_DEBLOCK, 0, False, "l2b"), (0, 5, True, "alt")])
 def test_gpu_paired_replay_matches_cpu(flags, window, ready, twin):
     """PairedReplay: the level-2 frames on a twin instance (shared DPB, own
     stream and host thread) give every frame's words and reconstruction of
@@ -607,7 +607,7 @@ def test_gpu_paired_replay_matches_cpu(flags, window, ready, twin):
             gi, ci = eng.frame(), c.frame()
             assert gi == ci, (n, gi, ci)
             eng.drain()
-            inst = eng.p if not n or eng.on_primary((n - 1) % 4) else eng.t
+            inst = eng.p if not n or eng.on_primary(n - 1) else eng.t
             np.testing.assert_array_equal(inst.results(), c.results())
         for n in range(11, 21):  # free-running: the streams overlap
             eng.frame()
