@@ -408,6 +408,72 @@ __global__ __launch_bounds__(256) void mvref_kernel(MvrefArgs a) {
   round_publish(a.pub);
 }
 
+// The same check with one role per wavefront: a workgroup holds 64
+// superblocks, wavefront 0 their stacks and wavefront r (1 .. 5 R) their
+// EPZS job r - 1, so no wavefront runs two roles' code one after the other
+// (the 16-lane layout above executes the stack path and the EPZS path of
+// its lanes in turn, with their loads' latencies in series).  A
+// superblock's roles meet in LDS.
+constexpr int kSplitSb = 64;
+__global__ __launch_bounds__(1024) void mvref_split_kernel(MvrefArgs a) {
+  __shared__ uint32_t chg[kSplitSb];  // per superblock: bit r = role r changed
+  __shared__ uint32_t pmk[kSplitSb];  // role 0: the references whose rate predictors changed
+  const int role = (int)(threadIdx.x >> 6), sbl = (int)(threadIdx.x & 63);
+  const int sb = (int)blockIdx.x * kSplitSb + sbl;
+  const bool live = sb < a.nsb;
+  if (threadIdx.x < kSplitSb) chg[threadIdx.x] = pmk[threadIdx.x] = 0;
+  __syncthreads();
+  if (live) {
+    const int sx = sb % a.tw, sy = sb / a.tw;
+    const int fsx = a.tx0 + sx, fsy = a.ty0 + sy;
+    bool changed = false;
+    if (role == 0) {  // the stacks (as in mvref_kernel's lane 0)
+      const int t0x = fsx - fsx % a.tws, t0y = fsy - fsy % a.ths;
+      const int cols = min(a.tws * 16, a.w_in_b - t0x * 16);
+      const int bx = (fsx - t0x) * 16, by = (fsy - t0y) * 16;
+      const int X = fsx * 64, Y = fsy * 64;
+      const bool split = a.lvl && (X + 64 > a.W || Y + 64 > a.H);
+      Nb nb;
+      nb.up = !split && by > 0;
+      nb.left = !split && bx > 0;
+      nb.tr = !split && by > 0 && bx + 16 < cols;
+      nb.tl = !split && bx > 0 && by > 0;
+      if (nb.up) nb.a = coded_at(a, sb - a.tw, X, Y - 4);
+      if (nb.left) nb.l = coded_at(a, sb - 1, X - 4, Y);
+      if (nb.tr) nb.r = coded_at(a, sb - a.tw + 1, X + 64, Y - 4);
+      if (nb.tl) nb.d = coded_at(a, sb - a.tw - 1, X - 4, Y - 4);
+      const MvStack st = stacks_of(a, nb, split, fsx, fsy);
+      changed = !same_stacks(a, a.stk[sb], st);
+      uint32_t pmask = 0;
+      for (int k = 0; k < a.R; k++)
+        if (a.init || !mv_eq(a.stk[sb].s[k][0], st.s[k][0]) || !mv_eq(a.stk[sb].s[k][1], st.s[k][1]))
+          pmask |= 1u << k;
+      pmk[sbl] = pmask;
+      if (changed) set_stacks(a, sb, st);
+    } else {
+      changed = epzs_job(a, sb, fsx, fsy, role - 1);
+    }
+    if (changed) atomicOr(&chg[sbl], 1u << role);
+  }
+  __syncthreads();
+  const uint32_t cm = chg[sbl], pm = pmk[sbl];
+  if (a.f3dirty && live && role >= 1 && role <= a.R)  // F3 job role - 1: its set or its pmv
+    a.f3dirty[(size_t)(role - 1) * a.nsb + sb] = (((cm >> role) & 1) || ((pm >> (role - 1)) & 1)) ? 1 : 0;
+  if (a.f2dirty && live && role > a.R) {  // F2 quadrant job: its set alone
+    const int e = role - 1 - a.R, k = e >> 2;
+    a.f2dirty[((size_t)k * a.nsb + sb) * 4 + (e & 3)] = (((cm >> role) & 1) || a.init) ? 1 : 0;
+  }
+  if (role == 0) {
+    const bool mark = live && cm != 0;
+    if (live) a.active[sb] = mark;
+    const uint64_t m = __ballot(mark);
+    int base = 0;
+    if (sbl == 0 && m) base = atomicAdd(a.count, (int)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (mark) a.list[base + __popcll(m & ((1ull << sbl) - 1))] = sb;
+  }
+  round_publish(a.pub);
+}
 
 // A decision predicted under a new stack: the same candidate, its MVs taken
 // from the new stack (NEWMV keeps the last search's MV).  Only a guess that
@@ -550,12 +616,17 @@ __global__ __launch_bounds__(kScanThreads) void mvref_scan_kernel(MvrefArgs a) {
 
 int rv_mvref_round(const MvrefArgs &a, hipStream_t s, bool scan) {
   if (a.nsb <= 0) return RV_OK;
+  // RAV1E_HIP_CHECK_SPLIT=0: the 16-lane check (A/B)
+  static const bool check_split = !(getenv("RAV1E_HIP_CHECK_SPLIT") && getenv("RAV1E_HIP_CHECK_SPLIT")[0] == '0');
   // the scan: a tile's decisions in LDS, at most kScanMaxDiag superblocks
   // per wavefront; otherwise the Jacobi check
   const bool scan_ok = a.tws * a.ths <= kMvrefScanMaxSb && (a.ths < a.tws ? a.ths : a.tws) <= kScanMaxDiag;
   if (scan && !a.init && scan_ok) {
     const int ntiles = ((a.tw + a.tws - 1) / a.tws) * ((a.th + a.ths - 1) / a.ths);
     mvref_scan_kernel<<<ntiles, kScanThreads, (size_t)a.tws * a.ths * sizeof(BlkDec), s>>>(a);
+  } else if (check_split) {
+    const int nr = 1 + (a.epzs ? 5 * a.R : 0);
+    mvref_split_kernel<<<(a.nsb + kSplitSb - 1) / kSplitSb, kSplitSb * nr, 0, s>>>(a);
   } else {
     mvref_kernel<<<(a.nsb * kCheckLanes + 255) / 256, 256, 0, s>>>(a);
   }
