@@ -42,10 +42,14 @@ int impwin_frame_data(const rv_plane &cur, const rv_plane *refs, int R, int bit_
                       const rv_fs_result *look, int tw, int nsb, int w_imp, int h_imp,
                       const ImpFrame &f, void *scratch, size_t scratch_bytes, hipStream_t st);
 
-// One (frame, reference k) pass: the source frame's contributions (split
-// over nu distinct references) added onto ref_imp.
-int impwin_pass(const ImpFrame &src, int k, int nu, int w_imp, int h_imp, float *ref_imp,
-                hipStream_t st);
+// The (frame, reference ks[i]) passes, i < np <= 2, in one launch: the
+// source frame's contributions (split over nu distinct references) added
+// onto ref_imp[i] (distinct frames).
+int impwin_pass(const ImpFrame &src, const int *ks, float *const *ref_imp, int np, int nu,
+                int w_imp, int h_imp, hipStream_t st);
+
+// imp[0 .. count) (n floats each) to zero.
+int impwin_zero(float *const *imp, int count, int n, hipStream_t st);
 
 // The frame's final importances from its propagated ones.
 int impwin_final(const ImpFrame &f, int w_imp, int h_imp, hipStream_t st);

@@ -143,26 +143,48 @@ __global__ __launch_bounds__(256) void offsets_kernel(const uint32_t *keys, int 
 }
 
 // One window pass: target t of the reference frame adds its sources'
-// contributions in source order (:936-963).
-__global__ __launch_bounds__(256) void pass_kernel(const uint32_t *intra, const rv_mv *mv8,
-                                                   const float *frac, const float *imp,
-                                                   const int32_t *off, const int32_t *src, int nu,
-                                                   int w, int h, float *ref_imp) {
+// contributions in source order (:936-963).  blockIdx.y picks one of the
+// launch's passes: a source frame's passes into its distinct references
+// write different frames and read only the source, so they share a launch.
+struct PassSet {
+  const uint32_t *intra;
+  const float *imp;
+  const rv_mv *mv8[2];
+  const float *frac[2];
+  const int32_t *off[2], *src[2];
+  float *ref_imp[2];
+  int nu;
+};
+__global__ __launch_bounds__(256) void pass_kernel(PassSet p, int w, int h) {
   const int t = blockIdx.x * 256 + threadIdx.x;
   if (t >= w * h) return;
+  const int y = blockIdx.y;
+  const int32_t *off = p.off[y], *src = p.src[y];
+  const rv_mv *mv8 = p.mv8[y];
+  const float *frac = p.frac[y];
   const int j0 = off[t], j1 = off[t + 1];
   if (j0 == j1) return;
+  float *ref_imp = p.ref_imp[y];
   float acc = ref_imp[t];
   for (int j = j0; j < j1; j++) {
     const int e = src[j], s = e >> 2, c = e & 3;
-    const float ic = (float)intra[s];
-    const float amount = __fdiv_rn((ic + imp[s]) * frac[s], (float)nu);
+    const float ic = (float)p.intra[s];
+    const float amount = __fdiv_rn((ic + p.imp[s]) * frac[s], (float)p.nu);
     int tgt[4];
     float fr[4];
     corners(s % w, s / w, mv8[s], w, h, tgt, fr);
     acc = acc + amount * fr[c];
   }
   ref_imp[t] = acc;
+}
+
+// The window's frames' propagated importances to zero, up to 64 frames a launch
+struct ZeroSet {
+  float *p[64];
+};
+__global__ __launch_bounds__(256) void zero_kernel(ZeroSet z, int n) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t < n) z.p[blockIdx.y][t] = 0.f;
 }
 
 // f32::log2 as the reference gets it on x86-64 Linux: glibc's log2f
@@ -280,14 +302,36 @@ int impwin_frame_data(const rv_plane &cur, const rv_plane *refs, int R, int bit_
   return RV_OK;
 }
 
-int impwin_pass(const ImpFrame &src, int k, int nu, int w_imp, int h_imp, float *ref_imp,
-                hipStream_t st) {
+int impwin_pass(const ImpFrame &src, const int *ks, float *const *ref_imp, int np, int nu,
+                int w_imp, int h_imp, hipStream_t st) {
   const int n = w_imp * h_imp;
-  if (nu < 1 || nu > 3 || n <= 0) return rv_set_error(RV_EINVAL, "impwin_pass: bad arguments");
-  pass_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(
-      src.intra, src.mv8 + (size_t)k * n, src.frac + (size_t)k * n, src.imp,
-      src.off + (size_t)k * (n + 1), src.src + (size_t)k * 4 * n, nu, w_imp, h_imp, ref_imp);
+  if (nu < 1 || nu > 3 || n <= 0 || np < 1 || np > 2)
+    return rv_set_error(RV_EINVAL, "impwin_pass: bad arguments");
+  PassSet p;
+  p.intra = src.intra;
+  p.imp = src.imp;
+  p.nu = nu;
+  for (int i = 0; i < np; i++) {
+    const int k = ks[i];
+    p.mv8[i] = src.mv8 + (size_t)k * n;
+    p.frac[i] = src.frac + (size_t)k * n;
+    p.off[i] = src.off + (size_t)k * (n + 1);
+    p.src[i] = src.src + (size_t)k * 4 * n;
+    p.ref_imp[i] = ref_imp[i];
+  }
+  pass_kernel<<<dim3((unsigned)((n + 255) / 256), (unsigned)np), 256, 0, st>>>(p, w_imp, h_imp);
   RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+int impwin_zero(float *const *imp, int count, int n, hipStream_t st) {
+  for (int i0 = 0; i0 < count; i0 += 64) {
+    ZeroSet z;
+    const int c = count - i0 < 64 ? count - i0 : 64;
+    for (int i = 0; i < c; i++) z.p[i] = imp[i0 + i];
+    zero_kernel<<<dim3((unsigned)((n + 255) / 256), (unsigned)c), 256, 0, st>>>(z, n);
+    RV_HIP_CHECK_LAUNCH();
+  }
   return RV_OK;
 }
 

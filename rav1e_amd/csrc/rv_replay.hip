@@ -2676,7 +2676,11 @@ static int la_step(rv_replay *r, long m) {
   const size_t ni = (size_t)g.w_imp * g.h_imp;
   while (E.imp_next <= m && (E.imp_next + E.W <= m || m == last_frame)) {
     const long n = E.imp_next, last = n + E.W < m ? n + E.W : m;
-    for (long t = n; t <= last; t++) RV_H(hipMemsetAsync(E.at(t).f.imp, 0, ni * 4, xs));
+    {
+      std::vector<float *> zs;
+      for (long t = n; t <= last; t++) zs.push_back(E.at(t).f.imp);
+      RV_R(impwin_zero(zs.data(), (int)zs.size(), (int)ni, xs));
+    }
     for (long s2 = last; s2 > n; s2--) {
       const RvLaEngine::Entry &es = E.at(s2);
       int uk[RV_MAX_REFS], nu = 0;
@@ -2685,11 +2689,17 @@ static int la_step(rv_replay *r, long m) {
         for (int j = 0; j < nu; j++) dup |= es.fi.ref_display[uk[j]] == es.fi.ref_display[k];
         if (!dup) uk[nu++] = k;
       }
+      // the frame's passes into its distinct references in the window: one launch
+      int ks[RV_MAX_REFS], np = 0;
+      float *dst[RV_MAX_REFS];
       for (int j = 0; j < nu; j++) {
         const long t = coded_of_display(es.fi.ref_display[uk[j]]);
         if (t < n) continue;  // before the window: gone (:944-948)
-        RV_R(impwin_pass(es.f, uk[j], nu, g.w_imp, g.h_imp, E.at(t).f.imp, xs));
+        ks[np] = uk[j];
+        dst[np++] = E.at(t).f.imp;
       }
+      for (int i = 0; i < np; i += 2)
+        RV_R(impwin_pass(es.f, ks + i, dst + i, np - i < 2 ? np - i : 2, nu, g.w_imp, g.h_imp, xs));
     }
     RV_R(impwin_final(E.at(n).f, g.w_imp, g.h_imp, xs));
     RV_H(hipEventRecord(E.at(n).ev_imp, xs));
