@@ -140,6 +140,14 @@ def _prof_json(args):
     `tools/gpu.sh prof` run of this bench)."""
     import glob
     fs = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_prof_{args.config}.json")))
+    # profiles/prof_current.json names the current one per config (tags do
+    # not sort by time)
+    cur = os.path.join(ROOT, "profiles", "prof_current.json")
+    if os.path.exists(cur):
+        with open(cur) as f:
+            name = json.load(f).get(args.config)
+        if name and os.path.exists(os.path.join(ROOT, "profiles", name)):
+            fs = [os.path.join(ROOT, "profiles", name)]
     if args.refs != 2 or not fs:
         return None
     with open(fs[-1]) as f:
