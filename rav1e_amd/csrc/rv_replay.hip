@@ -1676,7 +1676,7 @@ static int intra_begin(rv_replay *r) {
 }
 
 static int intra_pass(rv_replay *r, const RdoArgs &la, const RdoArgs &ca, const RvInput &cur,
-                      const RvSlot &S, const rv_replay::Level &L, int slot) {
+                      const RvSlot &S, const rv_replay::Level &L, int slot, int *nrounds) {
   const Geo &g = r->g;
   hipStream_t st = r->stream;
   const IntraGeo ig{g.W, g.H, g.bd, g.nsb, g.tw, g.tx0, g.ty0, g.tws, g.ths};
@@ -1775,6 +1775,7 @@ static int intra_pass(rv_replay *r, const RdoArgs &la, const RdoArgs &ca, const 
   }
   RV_R(rv_intra_stats(g.nsb, r->i_elig, r->i_was, stats, st));
   RV_H(hipMemcpyAsync(stats + 2, &round, 4, hipMemcpyHostToDevice, st));
+  if (nrounds) *nrounds = round;
   return RV_OK;
 }
 
@@ -3583,7 +3584,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   side_join.armed = false;  // both side streams have joined the main one
   RV_EV(10);
   // F6b intra-mode screening + intra RDO of the non-skip superblocks
-  if (r->intra) RV_R(intra_pass(r, la, ca, cur, S, L, slot));
+  int irounds = 0;
+  if (r->intra) RV_R(intra_pass(r, la, ca, cur, S, L, slot, &irounds));
   // an intra winner is no MV source (add_ref_mv_candidate skips intra
   // blocks): the superblocks whose stacks it changes are re-decided, the
   // frame re-committed and the intra pass re-run, until the stacks hold
@@ -3596,12 +3598,17 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     if (pass > g.tws * g.ths)
       return rv_set_error(RV_EHIP, "rv_replay_frame: the MV / intra passes did not settle "
                                    "(internal error)");
+    // no screened superblock (no intra round): no superblock is intra, the
+    // stacks are the ones the MV rounds settled -- the check would list
+    // nothing (only after the first pass: later ones follow a run whose
+    // stacks saw intra blocks)
+    if (pass == 0 && irounds == 0) break;
     bool changed = false;
     RV_R(mv_rounds_run(r->i_was, &changed));
     if (!changed) break;
     RV_R(rv_rdo_candidates(la, ca, g.hbd, st));  // F6 again: every inter winner
     RV_R(intra_begin(r));
-    RV_R(intra_pass(r, la, ca, cur, S, L, slot));
+    RV_R(intra_pass(r, la, ca, cur, S, L, slot, &irounds));
   }
   if (r->exact) {
     r->mv_round_sum++;  // round 0
