@@ -2946,6 +2946,14 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   }
   if (!r->lv[0].set || !r->lv[1].set || !r->lv[2].set)
     return rv_set_error(RV_EINVAL, "rv_replay_frame: level params not set");
+  // RAV1E_HIP_HOST_TRACE=1: the host's time per frame phase (stderr)
+  static const bool host_trace = getenv("RAV1E_HIP_HOST_TRACE") != nullptr;
+  using hclock = std::chrono::steady_clock;
+  const auto h0 = hclock::now();
+  auto h_take = h0, h_r0 = h0, h_mv = h0, h_intra = h0;
+  auto us = [&](hclock::time_point a, hclock::time_point b) {
+    return (long)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
+  };
   if (!r->jobs_built) RV_R(build_static_jobs(r));
   const rv_replay::Level &L = r->lv[fi.level];
   const int lv = fi.level;
@@ -2997,6 +3005,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     r->la_frames++;
   }
   r->imp_last = imp;
+  h_take = hclock::now();
   auto rounds = [&](hipStream_t xs, int budget, auto &&check, auto &&eval, long *nrounds,
                     long *nre, bool *changed, const char *what) -> int {
     return run_rounds(r->rr, xs, budget, check, eval, nrounds, nre, changed, what, ncoded, lv);
@@ -3525,7 +3534,9 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
         if (r->lv_used[l]) RV_H(hipStreamWaitEvent(st, r->ev_ejoin[l], 0));
     ma.hq = r->half;
     ma.edge_ok = 1;
+    h_r0 = hclock::now();
     RV_R(mv_rounds_run(nullptr, nullptr));
+    h_mv = hclock::now();
   }
   if (r->lvl) {
     if (edge) {  // the levels' winners
@@ -3586,6 +3597,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // F6b intra-mode screening + intra RDO of the non-skip superblocks
   int irounds = 0;
   if (r->intra) RV_R(intra_pass(r, la, ca, cur, S, L, slot, &irounds));
+  h_intra = hclock::now();
   // an intra winner is no MV source (add_ref_mv_candidate skips intra
   // blocks): the superblocks whose stacks it changes are re-decided, the
   // frame re-committed and the intra pass re-run, until the stacks hold
@@ -3715,6 +3727,14 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     }
     eh->cv.notify_all();
     r->ec_frames++;
+  }
+  if (host_trace) {
+    static thread_local hclock::time_point prev_end = h0;
+    const auto h1 = hclock::now();
+    fprintf(stderr, "host frame %ld level %d: since-last-exit %ld take %ld r0 %ld mv %ld intra %ld tail %ld us\n",
+            r->coded, lv, us(prev_end, h0), us(h0, h_take), us(h_take, h_r0), us(h_r0, h_mv),
+            us(h_mv, h_intra), us(h_intra, h1));
+    prev_end = h1;
   }
   r->coded++;
   r->last = fi;
