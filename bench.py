@@ -465,7 +465,10 @@ def main():
     eng = TileParallel(hip, rects, rank, group, comm)
     paired = world == 1 and not args.serial_levels
     if paired:
-        eng = RP.PairedReplay(hip)
+        # three instances (PipelinedReplay: 2160p 205-206 vs 189-193 fps for
+        # two, r04p4); RAV1E_BENCH_INSTANCES=2: PairedReplay (A/B)
+        eng = (RP.PairedReplay(hip) if os.environ.get("RAV1E_BENCH_INSTANCES") == "2"
+               else RP.PipelinedReplay(hip))
     sea = bd <= 10 and not args.exhaustive_fs  # the replay's F1 path
     # HIP events on a sample of frames: every TIMING_STRIDE-th GOP
     gop = len(RP.GOP_SCALES)
@@ -635,8 +638,12 @@ def main():
                        "deblock": bool(args.deblock or args.cdef), "cdef": bool(args.cdef),
                        "tiles": [tiling["cols"], tiling["rows"]],
                        "parallelism": f"tile-groups{world}",
-                       "frame_concurrency": ("levels 0/1 + level-2 frames on a twin instance "
-                                             "(2 streams)" if paired else "serial"),
+                       "frame_concurrency": (("levels 0/1 + 4g+1 on the primary, 4g+3 on a "
+                                              "twin (2 instances)")
+                                             if paired and isinstance(eng, RP.PairedReplay) else
+                                             ("level 0 + 4g+1, level 1, 4g+3 on three instances "
+                                              "(own streams and host threads, device events)")
+                                             if paired else "serial"),
                        "candidates_per_sb": f"{4 * nref} inter modes x (skip, non-skip)",
                        **({"mv_stack": ("rav1e's find_mvrefs over the coded blocks, coding-order "
                                         "rounds" if args.mv_stack == "exact" else

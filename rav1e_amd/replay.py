@@ -618,6 +618,180 @@ class PairedReplay:
         return getattr(self.p, name)
 
 
+def _refs_of(n: int, n_refs: int) -> list:
+    fi = frame_info(n, n_refs)
+    return sorted(set(fi["ref_display"][:n_refs]))
+
+
+def _coded_of_display(d: int) -> int:
+    """frame_info's inverse (rv_replay.hip coded_of_display)."""
+    if d == 0:
+        return 0
+    j = {0: 0, 2: 1, 1: 2, 3: 3}[d % 4]
+    off = (4, 2, 1, 3)[j]
+    return 4 * ((d - off) // 4) + j + 1
+
+
+class PipelinedReplay:
+    """One stream coded by three instances of the same tile group (shared
+    DPB and inputs, rv_replay_create_twin), each on its own stream and host
+    thread: `primary` the key frame, the level-0 frames (display 4g+4) and
+    the level-2 frames 4g+1 (each after the next group's level-0 frame), a
+    twin the level-1 frames (4g+2), a second twin the level-2 frames 4g+3.
+    Every frame waits, through device events, for the frames on the other
+    instances it depends on: the producers of its references, and the
+    previous occupant of its DPB slot (display d - 12) with every frame that
+    reads it.  The frames' results are the sequential ones."""
+
+    def __init__(self, primary: "HipReplay"):
+        import queue
+        import threading
+        self.p = primary
+        self.inst = [primary, primary.twin(), primary.twin()]
+        self.R = primary.cfg.n_refs
+        self.n = 0
+        self.err = None
+        self.ev = [lib().rv_event_create() for _ in range(64)]
+        self.done = {}  # coded frame -> threading.Event (its event is recorded)
+        self.lock = threading.Lock()
+        self.held = None  # a 4g+1 frame waiting for the next level-0 frame
+        self.qs = [queue.Queue() for _ in self.inst]
+        self.workers = [threading.Thread(target=self._run, args=(i,), daemon=True)
+                        for i in range(3)]
+        for w in self.workers:
+            w.start()
+
+    @staticmethod
+    def instance_of(n: int) -> int:
+        if n == 0:
+            return 0
+        return (0, 1, 0, 2)[(n - 1) % 4]
+
+    def on_primary(self, f: int) -> bool:
+        return self.instance_of(f + 1) == 0
+
+    def _flag(self, n):
+        with self.lock:
+            if n not in self.done:
+                self.done[n] = __import__("threading").Event()
+            return self.done[n]
+
+    def _deps(self, n: int) -> list:
+        """Coded frames on other instances that frame n waits for."""
+        if n == 0:
+            return []
+        d = frame_info(n, self.R)["display"]
+        deps = {_coded_of_display(r) for r in _refs_of(n, self.R)}
+        prev = d - 12  # the DPB slot's previous occupant and its readers
+        if prev >= 0:
+            c = _coded_of_display(prev)
+            deps.add(c)
+            for k in range(c + 1, c + 17):
+                if k < n and prev in _refs_of(k, self.R):
+                    deps.add(k)
+        me = self.instance_of(n)
+        return sorted(k for k in deps if k < n and self.instance_of(k) != me)
+
+    def frame(self) -> dict:
+        n = self.n
+        self.n += 1
+        i = self.instance_of(n)
+        j = (n - 1) % 4 if n else -1
+        if n and j == 2:  # 4g+1: after the next group's level-0 frame
+            self.held = n
+        else:
+            self.qs[i].put(n)
+            if n and j == 0 and self.held is not None:
+                self.qs[0].put(self.held)
+                self.held = None
+        self._raise()
+        return frame_info(n, self.R)
+
+    def _run(self, i):
+        inst = self.inst[i]
+        while True:
+            n = self.qs[i].get()
+            if n is None:
+                self.qs[i].task_done()
+                return
+            try:
+                if self.err is None:
+                    for k in self._deps(n):
+                        self._flag(k).wait()
+                        _check(lib().rv_stream_wait_event(inst.stream, self.ev[k % 64]),
+                               "rv_stream_wait_event")
+                    if n:
+                        inst.seek(n)
+                    inst.frame()
+                    _check(lib().rv_event_record(self.ev[n % 64], inst.stream), "rv_event_record")
+            except Exception as e:  # handed to the main thread by drain()
+                self.err = e
+            finally:
+                self._flag(n).set()
+                self.qs[i].task_done()
+
+    def _raise(self):
+        if self.err is not None:
+            e, self.err = self.err, None
+            raise e
+
+    def drain(self):
+        if self.held is not None:  # the stream ends: the held frame goes now
+            self.qs[0].put(self.held)
+            self.held = None
+        for q in self.qs:
+            q.join()
+        self._raise()
+
+    def results(self) -> np.ndarray:
+        self.drain()
+        return self.p.results()
+
+    def set_timing(self, stride: int, block: int = 1):
+        for t in self.inst:
+            t.set_timing(stride, block)
+
+    def entropy_stats(self):
+        self.drain()
+        st = [t.entropy_stats() for t in self.inst]
+        a = st[0]
+        return [a[0], a[1], a[2], sum(x[3] for x in st), sum(x[4] for x in st)]
+
+    def counters(self) -> np.ndarray:
+        self.drain()
+        cs = [t.counters() for t in self.inst]
+        out = cs[0] + cs[1] + cs[2]
+        out[2] = max(c[2] for c in cs)
+        return out
+
+    def stage_ms_sum(self, kp: int, kt: int) -> np.ndarray:
+        """Stage times over the primary's last kp instrumented frames and kt of
+        the twins' (split evenly)."""
+        self.drain()
+        s = np.zeros(N_STAGES, np.float32)
+        if kp:
+            s = s + self.p.stage_ms_sum(kp)
+        for t, k in ((self.inst[1], (kt + 1) // 2), (self.inst[2], kt // 2)):
+            if k:
+                s = s + t.stage_ms_sum(k)
+        return s
+
+    def close(self):
+        if self.workers:
+            for q in self.qs:
+                q.put(None)
+            for w in self.workers:
+                w.join()
+            self.workers = []
+            for t in self.inst[1:]:
+                t.close()  # before the primary: they borrow the DPB
+            for e in self.ev:
+                lib().rv_event_destroy(e)
+
+    def __getattr__(self, name):
+        return getattr(self.p, name)
+
+
 class RcclComm:
     """An RCCL communicator over all ranks (rv_comm_*), bootstrapped through
     torch.distributed (gloo): rank 0's unique id is broadcast as bytes."""

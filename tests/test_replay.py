@@ -579,6 +579,38 @@ def test_gpu_tile_groups_exchange(flags):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("window", [0, 5])
+def test_gpu_pipelined_replay_matches_cpu(window):
+    """PipelinedReplay: three instances (levels 0 + 4g+1, level 1, 4g+3) on
+    their own streams and host threads, ordered by device events only; the
+    reconstructions of a free-running stretch equal the sequential CPU
+    replay's."""
+    import rav1e_amd as R
+    R.require_device(0)
+    w, h, nin = 256, 200, 24
+    g = RP.HipReplay(w, h, n_inputs=nin, imp_window=window, imp_limit=21)
+    g.synth_inputs(0)
+    if window:
+        g.set_inputs_ready(nin)
+    c = O.CpuReplay(w, h, n_inputs=nin, threads=O.cpu_share(), imp_window=window, imp_limit=21)
+    for i in range(nin):
+        c.set_input(i, g.get_input(i))
+    eng = RP.PipelinedReplay(g)
+    try:
+        for n in range(21):
+            gi, ci = eng.frame(), c.frame()
+            assert gi == ci, (n, gi, ci)
+        eng.drain()
+        R._check(R.lib().rv_device_sync(), "sync")
+        for d in range(9, 21):
+            np.testing.assert_array_equal(g.get_recon(d), c.get_recon(d), err_msg=f"display {d}")
+    finally:
+        eng.close()
+        g.close()
+        c.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("flags,window,ready,twin", [
     (0, 0, False, "l2"), (RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF, 0, False, "l2"),
     (RP.RV_REPLAY_SPEED6, 0, False, "l2"), (0, 5, False, "l2"), (0, 5, True, "l2"),
