@@ -485,9 +485,13 @@ def main():
     k = max(k, 1)
     if paired:  # the instrumented frames of each instance in the timed region
         inst = [f for f in nonkey if (f // gop) % TIMING_STRIDE == 0]
-        kp = min(sum(1 for f in inst if eng.on_primary(f)), 64)
-        kt = min(sum(1 for f in inst if not eng.on_primary(f)), 64)
-        ms = eng.stage_ms_sum(kp, kt) / max(1, kp + kt)
+        if hasattr(eng, "stage_ms_sum_frames"):
+            ssum, kn = eng.stage_ms_sum_frames(inst)
+            ms = ssum / max(1, kn)
+        else:
+            kp = min(sum(1 for f in inst if eng.on_primary(f)), 64)
+            kt = min(sum(1 for f in inst if not eng.on_primary(f)), 64)
+            ms = eng.stage_ms_sum(kp, kt) / max(1, kp + kt)
         cnt = [int(v) for v in eng.counters()]
     else:
         ms = hip.stage_ms_sum(k) / k  # per frame

@@ -994,7 +994,7 @@ struct LaOut {
 // RW = W + 1 + kLaSlack: the slack covers the frames a twin instance still
 // has in flight behind the primary.
 struct RvLaEngine {
-  static constexpr int kLaSlack = 20;
+  static constexpr int kLaSlack = 28;
   int W = 0, RW = 0, dev = 0;
   long limit = 0;  // coded frames in the stream (0: unbounded)
   hipStream_t las = nullptr;

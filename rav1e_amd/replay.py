@@ -643,11 +643,16 @@ class PipelinedReplay:
     previous occupant of its DPB slot (display d - 12) with every frame that
     reads it.  The frames' results are the sequential ones."""
 
-    def __init__(self, primary: "HipReplay"):
+    def __init__(self, primary: "HipReplay", instances: int = None):
         import queue
         import threading
+        # 3: level 0 + 4g+1 | level 1 | 4g+3; 5: the level-1 and the 4g+3
+        # frames alternate between two instances each (even / odd groups)
+        self.k = instances or int(os.environ.get("RAV1E_PIPE_INSTANCES", "3"))
+        if self.k not in (3, 5):
+            raise ValueError(f"PipelinedReplay: {self.k} instances (3 or 5)")
         self.p = primary
-        self.inst = [primary, primary.twin(), primary.twin()]
+        self.inst = [primary] + [primary.twin() for _ in range(self.k - 1)]
         self.R = primary.cfg.n_refs
         self.n = 0
         self.err = None
@@ -657,15 +662,17 @@ class PipelinedReplay:
         self.held = None  # a 4g+1 frame waiting for the next level-0 frame
         self.qs = [queue.Queue() for _ in self.inst]
         self.workers = [threading.Thread(target=self._run, args=(i,), daemon=True)
-                        for i in range(3)]
+                        for i in range(self.k)]
         for w in self.workers:
             w.start()
 
-    @staticmethod
-    def instance_of(n: int) -> int:
+    def instance_of(self, n: int) -> int:
         if n == 0:
             return 0
-        return (0, 1, 0, 2)[(n - 1) % 4]
+        g, j = (n - 1) // 4, (n - 1) % 4
+        if self.k == 3:
+            return (0, 1, 0, 2)[j]
+        return (0, 1 + g % 2, 0, 3 + g % 2)[j]
 
     def on_primary(self, f: int) -> bool:
         return self.instance_of(f + 1) == 0
@@ -760,21 +767,23 @@ class PipelinedReplay:
     def counters(self) -> np.ndarray:
         self.drain()
         cs = [t.counters() for t in self.inst]
-        out = cs[0] + cs[1] + cs[2]
+        out = sum(cs[1:], cs[0].copy())
         out[2] = max(c[2] for c in cs)
         return out
 
-    def stage_ms_sum(self, kp: int, kt: int) -> np.ndarray:
-        """Stage times over the primary's last kp instrumented frames and kt of
-        the twins' (split evenly)."""
+    def stage_ms_sum_frames(self, frames) -> tuple:
+        """Stage times summed over the instrumented inter frames `frames`
+        (f: coded frame f + 1), each instance its own last ones; returns
+        (sum, frames counted)."""
         self.drain()
         s = np.zeros(N_STAGES, np.float32)
-        if kp:
-            s = s + self.p.stage_ms_sum(kp)
-        for t, k in ((self.inst[1], (kt + 1) // 2), (self.inst[2], kt // 2)):
+        cnt = [0] * self.k
+        for f in frames:
+            cnt[self.instance_of(f + 1)] += 1
+        for t, k in zip(self.inst, cnt):
             if k:
-                s = s + t.stage_ms_sum(k)
-        return s
+                s = s + t.stage_ms_sum(min(k, 64))
+        return s, sum(min(k, 64) for k in cnt)
 
     def close(self):
         if self.workers:

@@ -579,8 +579,8 @@ def test_gpu_tile_groups_exchange(flags):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("window", [0, 5])
-def test_gpu_pipelined_replay_matches_cpu(window):
+@pytest.mark.parametrize("window,k", [(0, 3), (5, 3), (5, 5)])
+def test_gpu_pipelined_replay_matches_cpu(window, k):
     """PipelinedReplay: three instances (levels 0 + 4g+1, level 1, 4g+3) on
     their own streams and host threads, ordered by device events only; the
     reconstructions of a free-running stretch equal the sequential CPU
@@ -595,7 +595,7 @@ def test_gpu_pipelined_replay_matches_cpu(window):
     c = O.CpuReplay(w, h, n_inputs=nin, threads=O.cpu_share(), imp_window=window, imp_limit=21)
     for i in range(nin):
         c.set_input(i, g.get_input(i))
-    eng = RP.PipelinedReplay(g)
+    eng = RP.PipelinedReplay(g, instances=k)
     try:
         for n in range(21):
             gi, ci = eng.frame(), c.frame()
