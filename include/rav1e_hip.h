@@ -84,6 +84,9 @@ int rv_memcpy_d2h(void *dst, const void *src, size_t bytes, void *stream);
 int rv_memcpy_d2d(void *dst, const void *src, size_t bytes, void *stream);
 int rv_memset(void *dst, int value, size_t bytes, void *stream);
 void *rv_stream_create(void);
+/* A stream at a priority: < 0 the highest, > 0 the lowest, 0 the default
+ * (HIP serves each priority from a hardware-queue pool of its own). */
+void *rv_stream_create_priority(int priority);
 int rv_stream_destroy(void *stream);
 int rv_stream_sync(void *stream);
 int rv_device_sync(void);

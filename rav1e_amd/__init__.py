@@ -229,6 +229,7 @@ def _declare(L):
         "rv_memcpy_d2d": (i32, [vp, vp, sz, vp]),
         "rv_memset": (i32, [vp, i32, sz, vp]),
         "rv_stream_create": (vp, []),
+        "rv_stream_create_priority": (vp, [i32]),
         "rv_stream_destroy": (i32, [vp]),
         "rv_stream_sync": (i32, [vp]),
         "rv_device_sync": (i32, []),

@@ -127,6 +127,22 @@ void *rv_stream_create(void) {
   }
   return s;
 }
+void *rv_stream_create_priority(int priority) {
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) {
+    rv_set_hip_error(e, "hipDeviceGetStreamPriorityRange");
+    return nullptr;
+  }
+  hipStream_t s = nullptr;
+  e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking,
+                                  priority < 0 ? greatest : priority > 0 ? least : 0);
+  if (e != hipSuccess) {
+    rv_set_hip_error(e, "hipStreamCreateWithPriority");
+    return nullptr;
+  }
+  return s;
+}
 int rv_stream_destroy(void *stream) {
   if (stream) RV_TRY(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)));
   return RV_OK;

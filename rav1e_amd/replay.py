@@ -297,15 +297,17 @@ class HipReplay:
                    "rv_replay_set_imp_window")
         self.imp_shape = ((height + 7) // 8, (width + 7) // 8)
 
-    def twin(self):
+    def twin(self, stream=None):
         """A second instance sharing this one's DPB and inputs
         (rv_replay_create_twin): it codes the level-2 frames concurrently
-        with this instance's levels 0 / 1 (PairedReplay)."""
+        with this instance's levels 0 / 1 (PairedReplay).  stream: its
+        stream (the caller's, kept alive until the twin closes); None: its
+        own."""
         t = HipReplay.__new__(HipReplay)
         t.cfg, t.geom, t.speed, t.n_words, t.levels = self.cfg, self.geom, self.speed, \
             self.n_words, self.levels
         t.imp_window, t.imp_shape = self.imp_window, self.imp_shape
-        t.h = lib().rv_replay_create_twin(self.h, None)
+        t.h = lib().rv_replay_create_twin(self.h, stream)
         if not t.h:
             raise RuntimeError(f"rv_replay_create_twin: {lib().rv_last_error().decode()}")
         t.primary = self  # the DPB's owner outlives the twin
@@ -652,7 +654,17 @@ class PipelinedReplay:
         if self.k not in (3, 5):
             raise ValueError(f"PipelinedReplay: {self.k} instances (3 or 5)")
         self.p = primary
-        self.inst = [primary] + [primary.twin() for _ in range(self.k - 1)]
+        # RAV1E_PIPE_HP=1: the twins (the compound frames' instances) on
+        # high-priority streams (A/B)
+        self.hp_streams = []
+        if os.environ.get("RAV1E_PIPE_HP") == "1":
+            for _ in range(self.k - 1):
+                st = lib().rv_stream_create_priority(-1)
+                if not st:
+                    raise RuntimeError(f"rv_stream_create_priority: {lib().rv_last_error().decode()}")
+                self.hp_streams.append(st)
+        self.inst = [primary] + [primary.twin(self.hp_streams[i] if self.hp_streams else None)
+                                 for i in range(self.k - 1)]
         self.R = primary.cfg.n_refs
         self.n = 0
         self.err = None
@@ -794,6 +806,9 @@ class PipelinedReplay:
             self.workers = []
             for t in self.inst[1:]:
                 t.close()  # before the primary: they borrow the DPB
+            for st in self.hp_streams:
+                lib().rv_stream_destroy(st)
+            self.hp_streams = []
             for e in self.ev:
                 lib().rv_event_destroy(e)
 
