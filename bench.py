@@ -33,10 +33,13 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-# Hardware queues per process (HIP's default 4): one GPU's replay runs up to
-# six streams (two instances x main / lookahead / frame-edge levels); more
-# streams than queues get multiplexed onto them.  Set before HIP initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# Hardware queues per process: HIP's default 4, set explicitly before HIP
+# initialises.  The three replay instances, their frame-edge / entropy
+# streams and the lookahead engine share them; more queues measured slower
+# (2160p, 96 frames: 205 fps at 4, 188 at 6, 161 at 8, r04hq -- the more
+# streams run side by side, the more the rounds' latency-bound kernels
+# lose to the others' work).  RAV1E_BENCH_HW_QUEUES: another count (A/B).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RAV1E_BENCH_HW_QUEUES", "4")
 sys.path.insert(0, ROOT)
 
 # name: (width, height, xdec, ydec, bit_depth, tiling kwargs, BASELINE config, speed)
