@@ -157,22 +157,6 @@ def _prof_json(args):
         return json.load(f)
 
 
-def _profile_entry(args, kernel, bd, kind):
-    """A kernel's entry in the committed rocprofv3 PMC summaries
-    (profiles/<kind>_<config>.json), for the workload it was measured on."""
-    path = os.path.join(ROOT, "profiles", f"{kind}_{args.config}.json")
-    if args.refs != 2 or not os.path.exists(path):
-        return None
-    with open(path) as f:
-        tj = json.load(f)
-    want = ROCPROF_NAMES.get(kernel, "?").format(px="unsigned short" if bd > 8 else "unsigned char",
-                                                 pxs="u16" if bd > 8 else "u8")
-    for name, v in tj["kernels"].items():
-        if want in name:
-            return v, tj
-    return None
-
-
 def _kernels_trace(pj):
     """Every kernel of the committed trace of this bench, per coded frame
     (all launches: round 0, the MV-stack rounds, the lookahead engine, the
@@ -194,21 +178,27 @@ def _kernels_trace(pj):
             "kernels": out}
 
 
-def timed_run(engine, group, steps, warmup, sync=None, finish=None):
+def timed_run(engine, group, steps, warmup, sync=None, finish=None, before=None, start=None):
     """W untimed frames (the key frame first), then exactly K timed coded
     frames bracketed by a barrier and a device sync on both sides; returns
     (max-over-ranks seconds, result words of the last frame).  `engine` is a
     HipReplay / TileParallel (the product) or, in the multi-rank CPU tests,
-    the oracle's CpuReplay behind a TileParallel."""
+    the oracle's CpuReplay behind a TileParallel.  before(): after the
+    warmup, outside the timing (probes reset); start(): the first thing
+    inside the timing (the lookahead engine released)."""
     drain = getattr(engine, "drain", None)  # PairedReplay: frames issued from a second thread
     for _ in range(warmup):
         engine.frame()
     if warmup:
         engine.results()  # drains the stream
+    if before:
+        before()
     group.barrier()
     if sync:
         sync()
     t0 = time.perf_counter()
+    if start:
+        start()
     for _ in range(steps):
         engine.frame()
     if drain:
@@ -284,6 +274,9 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     fps1 = 4 * (lim / nsb) / t1
     cpu = {"value": round(n / tc, 4), "unit": "frames/s", "cores": threads, "kind": "port",
            "isa": isa,
+           "cores_note": "the GPU box's per-GPU CPU share (16 threads; the harness sizes worker "
+                         "pools to it), not every physical core of the host as SURVEY.md §8d "
+                         "asks; a scalar C restatement of the schedule, not rav1e's SIMD path",
            "sample": f"the first {n} coded {args.config} frames of the same stream and schedule "
                      f"(after the key frame), oracle/orc_replay.c -O3 -march={isa} on "
                      f"{threads} host threads",
@@ -399,7 +392,9 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=32)
+    # 96 frames: a steady-state sample (24 GOPs; the lookahead engine's lead
+    # is capped at the window at the start of the timing, see below)
+    ap.add_argument("--steps", type=int, default=96)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="2160p", choices=sorted(CONFIGS))
     ap.add_argument("--refs", type=int, default=2)
@@ -407,10 +402,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--speed", type=int, choices=(6, 10), default=None,
                     help="schedule (default: the config's BASELINE speed)")
-    ap.add_argument("--deblock", action="store_true",
-                    help="deblock every coded frame before it becomes a reference")
-    ap.add_argument("--cdef", action="store_true",
-                    help="deblock and CDEF every coded frame before it becomes a reference")
+    ap.add_argument("--loop-filters", choices=("all", "deblock", "none"), default="all",
+                    help="the in-loop filters every coded frame runs before it becomes a "
+                         "reference: rav1e's deblocking (fast levels at speed >= 8, "
+                         "sse_optimize below) and CDEF (cdef_preset is always true, "
+                         "src/api/config.rs:421-423; src/encoder.rs:2789-2803) -- the default; "
+                         "'deblock' / 'none' for A/B")
     ap.add_argument("--emulate-ranks", type=int, default=8,
                     help="N > 1 (single-GPU runs): also code the N-rank tile-group split as N "
                          "replays on this GPU and report the projected N-rank step (0: off)")
@@ -447,23 +444,33 @@ def main():
     ts = (tiling["tile_width_sb"], tiling["tile_height_sb"])
     rects = RP.tile_groups(tiling, world)
     imp_window = args.imp_window if world == 1 else 0
-    # every display the run codes, and the lookahead's W frames beyond.  The
-    # stream is unbounded (imp_limit 0): every frame's window reaches W frames
-    # ahead, so the engine's lookahead of frames past the run is inside the
-    # timed region as it is in a streaming encode (a stream bounded at the
-    # run's end would have its whole lookahead done before the first frame)
-    n_inputs = args.warmup + args.steps + 8 + imp_window
+    # every display the run codes, the lookahead's W frames beyond, and the
+    # engine's ring slack (RW = W + 29: it may run that far past the oldest
+    # frame in flight).  The stream is unbounded (imp_limit 0): every frame's
+    # window reaches W frames ahead, so the engine's lookahead of frames past
+    # the run is inside the timed region, as in a streaming encode, and it
+    # never runs out of inputs before the last timed frame
+    n_inputs = args.warmup + args.steps + 8 + (imp_window + 29 + 8 if imp_window else 0)
+    deblock = args.loop_filters in ("all", "deblock")
+    cdef = args.loop_filters == "all"
     flags = (RP.RV_REPLAY_EXHAUSTIVE_FS if args.exhaustive_fs else 0) | \
-        (RP.RV_REPLAY_SPEED6 if speed == 6 else 0) | (RP.RV_REPLAY_DEBLOCK if args.deblock or args.cdef else 0) | \
-        (RP.RV_REPLAY_CDEF if args.cdef else 0) | (0 if args.no_entropy else RP.RV_REPLAY_ENTROPY) | \
+        (RP.RV_REPLAY_SPEED6 if speed == 6 else 0) | (RP.RV_REPLAY_DEBLOCK if deblock else 0) | \
+        (RP.RV_REPLAY_CDEF if cdef else 0) | (0 if args.no_entropy else RP.RV_REPLAY_ENTROPY) | \
         (RP.RV_REPLAY_MVREF_STANDIN if args.mv_stack == "standin" else 0)
     hip = RP.HipReplay(W, H, xdec, ydec, bd, nref, group=rects[rank], tile_size=ts,
                        n_inputs=n_inputs, flags=flags, imp_window=imp_window,
                        imp_limit=0)
     hip.synth_inputs(0)  # the stream's frames, resident in HBM before the timing
-    if imp_window and os.environ.get("RAV1E_BENCH_NO_READY") != "1":
-        # all of them have arrived: the lookahead runs ahead as rav1e's does
-        hip.set_inputs_ready(n_inputs)
+    # The lookahead engine's lead: during the warmup it runs only the W
+    # frames each coded frame's window needs (no inputs declared ready), so
+    # at the start of the timing it is exactly W frames ahead of the encode.
+    # The first thing inside the timing declares every input in place, and
+    # from then on it runs as far ahead as its ring allows, as rav1e computes
+    # a frame's lookahead when the frame arrives.  So every timed frame's own
+    # lookahead (frame n + W's, for n's window) is computed inside the timing:
+    # the line reports that count (>= steps), and no lookahead done before
+    # the timing flatters it.
+    ready = bool(imp_window) and os.environ.get("RAV1E_BENCH_NO_READY") != "1"
     comm = RP.RcclComm(group) if world > 1 else None
     eng = TileParallel(hip, rects, rank, group, comm)
     paired = world == 1 and not args.serial_levels
@@ -477,9 +484,25 @@ def main():
     gop = len(RP.GOP_SCALES)
     (eng if paired else hip).set_timing(TIMING_STRIDE, gop)
     ent = not args.no_entropy
+    probe = world == 1 and speed == 10 and hasattr(eng, "set_kernel_probe")
+    la_cnt = {}
+
+    def before():
+        if probe:  # the F3 sub-pel kernel probe over the timed frames
+            eng.set_kernel_probe(True)
+        if imp_window:
+            la_cnt["t0"] = int(eng.counters()[20])
+
+    def start():
+        if ready:
+            hip.set_inputs_ready(n_inputs)
+
     dt, words = timed_run(eng, group, args.steps, args.warmup,
                           sync=lambda: R._check(R.lib().rv_device_sync(), "rv_device_sync"),
-                          finish=eng.entropy_stats if ent else None)
+                          finish=eng.entropy_stats if ent else None, before=before, start=start)
+    if imp_window:
+        la_cnt["t1"] = int(eng.counters()[20])
+    kp = eng.kernel_probe() if probe else None
     ent_stats = eng.entropy_stats() if ent else None
 
     # per-kernel times over the instrumented frames of the timed region
@@ -548,75 +571,103 @@ def main():
         "rdo_compound": dict(ms=float(ms[7]), bytes=comp_bytes),
         "rdo_commit": dict(ms=float(ms[9]), bytes=commit_bytes),
     }
-    # the roofline prices the frame's full F4 evaluation (round 0): the kernel
-    # class with the most work per frame, whose committed trace and PMC passes
-    # the line cross-checks.  (Picking the largest HIP-event span instead
-    # follows the instances' overlap: with three instances on the GPU a short
-    # stage's span holds the other instances' kernels too.)
-    dom = "rdo_candidates" if kernels["rdo_candidates"]["bytes"] > 0 else \
-        max(kernels, key=lambda n: kernels[n]["ms"])
-    kd = kernels[dom]
-    launch_s = kd["ms"] / 1e3
-    ach = kd["bytes"] / launch_s / 1e9
-    tr = _profile_entry(args, dom, bd, "traffic")
     pj = _prof_json(args)
-    pk_name = ROCPROF_NAMES.get(dom, "?").format(px="unsigned short" if bd > 8 else "unsigned char",
-                                                 pxs="u16" if bd > 8 else "u8")
-    pke = next((v for k, v in pj["kernels"].items() if pk_name in k), None) if pj else None
-    # `bound` names the roofline `frac` is priced against (the contract's HBM
-    # roofline for this integer path); `limiter` names what actually binds,
-    # with the committed counter evidence (SQ pass: profiles/valu_<config>.json)
-    roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
-            "traffic": ({"bytes_per_launch": round(tr[0]["hbm_bytes"]), "source": tr[1]["source"],
-                         "git": tr[1]["git"],
-                         "over_algorithmic": round(tr[0]["hbm_bytes"] / kd["bytes"], 3)}
-                        if tr else None),
-            "avg_launch_ms": round(kd["ms"], 5),
-            "algorithmic_bytes_per_launch": round(kd["bytes"]),
-            "launch": "the frame's full evaluation (round 0: every superblock's candidates, the "
-                      "ones counted in rdo_candidates_per_frame), HIP events on its stream"}
-    if pke and pke.get("round0"):
-        # the same launch in the committed trace of this bench (tools/prof_json.py): its mean
-        # duration and PMC traffic; frac re-priced from it for the reproducibility check
-        r0 = pke["round0"]
-        roof["trace"] = {
-            "source": pj["source"], "git": pj["git"], "round0_avg_us": r0["avg_us"],
-            "round0_hbm_bytes_per_launch": r0.get("hbm_bytes_per_launch"),
-            "frac_from_trace": round(kd["bytes"] / (r0["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
-            "live_over_trace_duration": round(kd["ms"] * 1e3 / r0["avg_us"], 3),
-            "all_launches": {"ms_per_frame": pke["ms_per_frame"],
-                             "launches_per_frame": pke["launches_per_frame"],
-                             "rounds_ms_per_frame": pke.get("rounds", {}).get("ms_per_frame")}}
-        if r0.get("hbm_bytes_per_launch"):
-            roof["traffic"] = {"bytes_per_launch": r0["hbm_bytes_per_launch"],
-                               "source": pj["source"], "git": pj["git"],
-                               "over_algorithmic": round(r0["hbm_bytes_per_launch"] / kd["bytes"], 3)}
-    vp = _profile_entry(args, dom, bd, "valu")
     pk = valu_peak_int()
-    if vp:
-        # instructions per launch from the committed SQ pass; time from this run
-        c = vp[0]
-        insts = c["SQ_INSTS_VALU"]
-        achv = insts / launch_s / 1e9
-        wc = max(1.0, c.get("SQ_WAVE_CYCLES", 0.0))
-        wait, act = c.get("SQ_WAIT_ANY", 0.0) / wc, c.get("SQ_ACTIVE_INST_ANY", 0.0) / wc
-        roof["valu"] = {"achieved": round(achv, 1), "unit": "G wave64 VALU instr/s",
-                        "peak_guide": VALU_PEAK_GUIDE, "frac_guide": round(achv / VALU_PEAK_GUIDE, 4),
-                        "insts_per_launch": round(insts), "source": vp[1]["source"],
-                        "git": vp[1]["git"]}
+    pxn = "unsigned short" if bd > 8 else "unsigned char"
+
+    def trace_entry(kernel):
+        """the kernel's entry in the committed trace + PMC summary of this bench"""
+        nm = ROCPROF_NAMES.get(kernel, "?").format(px=pxn, pxs="u16" if bd > 8 else "u8")
+        return next((v for k, v in pj["kernels"].items() if nm in k), None) if pj else None
+
+    def valu_of(te, avg_s, hbm_frac):
+        """VALU rate of a kernel: its SQ_INSTS_VALU per launch (the committed SQ
+        pass of the same bench) over the live launch duration"""
+        sq = te.get("sq") if te else None
+        if not sq:
+            return None, None
+        achv = sq["valu_insts_per_launch"] / avg_s / 1e9
+        v = {"achieved": round(achv, 1), "unit": "G wave64 VALU instr/s",
+             "peak_guide": VALU_PEAK_GUIDE, "frac_guide": round(achv / VALU_PEAK_GUIDE, 4),
+             "insts_per_launch": sq["valu_insts_per_launch"],
+             "waves_per_launch": sq.get("waves_per_launch"), "source": pj["source"], "git": pj["git"]}
         if pk:
-            roof["valu"].update(peak_int_measured=pk["G_per_s"],
-                                frac_int_measured=round(achv / pk["G_per_s"], 4),
-                                peak_int_source=pk["source"])
-        roof["limiter"] = {
-            "resource": ("latency: waves parked on s_waitcnt / barriers" if wait > 0.3 else
-                         "VALU issue" if achv / VALU_PEAK_GUIDE > 0.6 else "mixed issue / latency"),
-            "SQ_WAIT_ANY_over_WAVE_CYCLES": round(wait, 4),
-            "SQ_ACTIVE_INST_ANY_over_WAVE_CYCLES": round(act, 4),
-            "valu_frac_guide": round(achv / VALU_PEAK_GUIDE, 4),
-            "hbm_frac": round(ach / HBM_PEAK_GBS, 5),
-            "source": vp[1]["source"]}
+            v.update(peak_int_measured=pk["G_per_s"], frac_int_measured=round(achv / pk["G_per_s"], 4),
+                     peak_int_source=pk["source"])
+        wait = sq["wait_any_over_wave_cycles"]
+        lim = {"resource": ("latency: waves parked on s_waitcnt / barriers" if wait > 0.3 else
+                            "VALU issue" if achv / VALU_PEAK_GUIDE > 0.6 else "mixed issue / latency"),
+               "SQ_WAIT_ANY_over_WAVE_CYCLES": wait,
+               "SQ_ACTIVE_INST_ANY_over_WAVE_CYCLES": sq["active_inst_over_wave_cycles"],
+               "valu_frac_guide": round(achv / VALU_PEAK_GUIDE, 4), "hbm_frac": hbm_frac,
+               "source": pj["source"]}
+        return v, lim
+
+    if kp is not None and kp[0] > 0:
+        # The dominant kernel of the committed trace (ms per frame over all its
+        # launches): ds_fast_kernel<64, 64, sub-pel>, F3's sub-pel search -- the
+        # batched MC + distortion kernel north_star names (every candidate a
+        # 6-tap put_8tap of its 71 x 71 window, then SAD against the source).
+        # Live: every launch of the instrumented timed frames (round 0 and the
+        # MV-stack rounds) bracketed by HIP events on the stream it runs on;
+        # its units: the candidate evaluations those launches counted.
+        dom = "diamond_subpel_64"
+        nl = float(kp[0])
+        avg_s = kp[1] / nl / 1e3
+        cand_b = (71 * 71 + 64 * 64) * px + 4  # SURVEY §8(d): fused MC + dist candidate
+        bytes_l = kp[2] / nl * cand_b
+        ach = bytes_l / avg_s / 1e9
+        roof = {"kernel": dom, "name": f"ds_fast_kernel<{pxn}, 64, 64, true>", "bound": "hbm",
+                "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                "avg_launch_ms": round(avg_s * 1e3, 5),
+                "algorithmic_bytes_per_launch": round(bytes_l),
+                "per_unit": {"unit": "candidate (MC + SAD of one sub-pel MV)", "bytes": cand_b,
+                             "rule": "(64+7)^2 b window + 64^2 b source + 4 (SURVEY.md §8d)"},
+                "units_per_launch": round(kp[2] / nl, 1), "jobs_per_launch": round(kp[3] / nl, 1),
+                "launches_probed": int(nl),
+                "launch": "every F3 sub-pel launch (round 0 and the MV-stack rounds) of the "
+                          "instrumented timed frames, HIP event pairs on its stream"}
+        te = trace_entry(dom)
+        if te:
+            roof["trace"] = {"source": pj["source"], "git": pj["git"], "avg_us": te["avg_us"],
+                             "launches_per_frame": te["launches_per_frame"],
+                             "ms_per_frame": te["ms_per_frame"],
+                             "frac_from_trace": round(bytes_l / (te["avg_us"] * 1e-6) / 1e9 /
+                                                      HBM_PEAK_GBS, 5),
+                             "live_over_trace_duration": round(avg_s * 1e6 / te["avg_us"], 3)}
+            if te.get("hbm_bytes_per_launch"):
+                roof["traffic"] = {"bytes_per_launch": te["hbm_bytes_per_launch"],
+                                   "source": pj["source"], "git": pj["git"],
+                                   "over_algorithmic": round(te["hbm_bytes_per_launch"] / bytes_l, 3),
+                                   "rule": pj.get("hbm_bytes_rule")}
+            v, lim = valu_of(te, avg_s, round(ach / HBM_PEAK_GBS, 5))
+            if v:
+                roof["valu"], roof["limiter"] = v, lim
+    else:
+        # no probe (speed 6, several ranks): the frame's full F4 evaluation
+        # (round 0), from its HIP-event stage span
+        dom = "rdo_candidates" if kernels["rdo_candidates"]["bytes"] > 0 else \
+            max(kernels, key=lambda n: kernels[n]["ms"])
+        kd = kernels[dom]
+        avg_s = kd["ms"] / 1e3
+        ach = kd["bytes"] / avg_s / 1e9
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                "avg_launch_ms": round(kd["ms"], 5),
+                "algorithmic_bytes_per_launch": round(kd["bytes"]),
+                "launch": "the frame's full evaluation (round 0), HIP events on its stream"}
+        te = trace_entry(dom)
+        if te and te.get("round0"):
+            r0 = te["round0"]
+            roof["trace"] = {"source": pj["source"], "git": pj["git"], "round0_avg_us": r0["avg_us"],
+                             "frac_from_trace": round(kd["bytes"] / (r0["avg_us"] * 1e-6) / 1e9 /
+                                                      HBM_PEAK_GBS, 5),
+                             "live_over_trace_duration": round(kd["ms"] * 1e3 / r0["avg_us"], 3)}
+            if r0.get("hbm_bytes_per_launch"):
+                roof["traffic"] = {"bytes_per_launch": r0["hbm_bytes_per_launch"],
+                                   "source": pj["source"], "git": pj["git"],
+                                   "over_algorithmic": round(r0["hbm_bytes_per_launch"] / kd["bytes"], 3)}
     fps = args.steps / dt  # frames of the one stream
 
     emu = None
@@ -648,7 +699,7 @@ def main():
                                    f"{nref} refs, reorder-pyramid coding order"
                                    f"{'' if args.no_entropy else ', coefficients entropy-coded'}",
                        "width": W, "height": H, "refs": nref, "speed": speed,
-                       "deblock": bool(args.deblock or args.cdef), "cdef": bool(args.cdef),
+                       "deblock": deblock, "cdef": cdef,
                        "tiles": [tiling["cols"], tiling["rows"]],
                        "parallelism": f"tile-groups{world}",
                        "frame_concurrency": (("levels 0/1 + 4g+1 on the primary, 4g+3 on a "
@@ -698,6 +749,10 @@ def main():
                 "stream": "unbounded: each frame's window reaches W frames past it, so the "
                           "engine's lookahead runs W frames ahead of the timed frames",
                 "lookahead_frames": cnt[20] if len(cnt) > 20 else None,
+                "lookahead_frames_in_timed_region": (la_cnt["t1"] - la_cnt["t0"]
+                                                     if "t1" in la_cnt else None),
+                "engine_lead_at_start": ("the window (W frames): no input declared ready before "
+                                         "the timing" if ready else "not capped"),
                 "lookahead_rounds_per_frame": round(cnt[18] / max(1, cnt[20]), 3)
                 if len(cnt) > 20 else None} if imp_window else
                 {"window": 0, "what": "importance 0 (bias 0.65)" +
@@ -716,7 +771,6 @@ def main():
                 "coefficient_kbit_per_frame": round(ent_stats[4] * 8 / 1e3 / max(1, ent_stats[3]), 3),
                 "scope": "coefficient syntax only (no mode / MV / partition symbols, headers)"}}
                if ent else {}),
-            "checksum": int(words[-5]) & 0xFFFFFFFF,
             **({"emulated_ranks": emu} if emu else {}),
         }
         print(json.dumps(line), flush=True)

@@ -685,8 +685,8 @@ int rv_replay_set_importances(rv_replay *r, const float *host, int n);
 int rv_replay_set_imp_window(rv_replay *r, int window, long limit);
 /* The inputs of displays 0 .. displays - 1 are in place (rv_replay_input /
  * set) and stay until their frames are coded: the lookahead engine may run
- * every frame they cover as far ahead as its ring allows (W + 13 frames
- * past the oldest frame still being coded), instead of starting frame
+ * every frame they cover as far ahead as its ring allows (W + 1 +
+ * kLaSlack = W + 29 frames past the oldest frame still being coded), instead of starting frame
  * n + window only when frame n is asked for.  rav1e computes a frame's
  * lookahead data as soon as the frame arrives (compute_lookahead_data,
  * src/api/internal.rs:767-820).  At most the instance's n_inputs; no
@@ -756,6 +756,28 @@ int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
  * (<= 64). */
 int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,
                               int cap);
+/* Kernel probe for the bench's roofline: with on != 0, every F3 sub-pel
+ * launch (ds_fast_kernel, 64x64, speed 10: round 0 and the MV-stack rounds)
+ * of an instrumented frame (rv_replay_set_timing) is bracketed by a HIP
+ * event pair on the stream it runs on and adds its candidate evaluations
+ * and jobs to a device counter.  (Re)starting drops the sums so far.
+ * rv_replay_kernel_probe: out[0] launches, out[1] their summed ms, out[2]
+ * candidate evaluations, out[3] jobs since the last start (cap >= 4;
+ * returns 4; waits for the launches). */
+int rv_replay_set_kernel_probe(rv_replay *r, int on);
+/* Host-only test hook (no device call): the slots the round ring gives
+ * round check q -- out[0] its device count slot, out[1] the slot it zeroes
+ * for check q + 1, out[2] its host publication slot -- then out[3] the
+ * rounds queued ahead of the host's reads, out[4] / out[5] the ring sizes.
+ * Returns 6. */
+int rv_round_ring_slots(uint32_t q, int32_t *out, int cap);
+/* Host-only test hook: the importance window's reference slots of coded
+ * frame m >= 1 (rav1e's distinct DPB slots of fi.ref_frames,
+ * src/api/internal.rs:875-882; with 2 references a frame above pyramid
+ * level 0 adds LAST3): out[0] = their count, out[1..3] their displays,
+ * out[4..6] the propagation order.  Returns 0. */
+int rv_replay_la_refs(long m, int R, int32_t *out);
+int rv_replay_kernel_probe(rv_replay *r, double *out, int cap);
 /* Candidate evaluations summed over the last min(frames, 64) coded frames:
  * out[0] F3 full-pel 64x64 diamond, out[1] F3 sub-pel 64x64 diamond, out[2]
  * = the number of frames summed (cap >= 3); with cap >= 5, out[3] / out[4]

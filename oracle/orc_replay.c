@@ -65,19 +65,40 @@ typedef struct {
 /* The lookahead of one coded frame (compute_lookahead_motion_vectors +
  * compute_lookahead_intra_costs, src/api/internal.rs:514-765): its F1 /
  * F2L / FL results, and what compute_block_importances reads of it. */
+/* The lookahead's references of a coded frame: rav1e's distinct DPB slots
+ * of fi.ref_frames (compute_block_importances' unique_indices,
+ * src/api/internal.rs:875-882), one search each in
+ * compute_lookahead_motion_vectors (build_coarse_pmvs / build_half_res_pmvs /
+ * build_full_res_pmvs loop over ALL_INTER_REFS and search each slot once,
+ * src/encoder.rs:2732-2738, 3037-3040).  k < R are the encode's references
+ * (k = 0 LAST / the backward reference, k = 1 LAST2 on level 0, ALTREF (the
+ * forward reference) above); with R = 2 a level > 0 frame adds k = 2,
+ * LAST3 = its own slot, i.e. the previous frame of its level (or the key
+ * frame, which fills every slot), src/encoder.rs:772-828.  order: the
+ * propagation's reference order (mv index order: LAST, LAST2 / LAST3,
+ * ALTREF). */
+typedef struct {
+  int n, disp[3], order[3];
+} orc_la_refs;
+
 typedef struct {
   long coded; /* -1: empty */
   orc_frame_info fi;
-  orc_mv *coarse, *half_l, *look; /* [R][nsb] (x4, x16) */
+  orc_la_refs lr;
+  orc_mv *coarse, *half_l, *look; /* [RA][nsb] (x4, x16) */
   uint64_t *cc, *hlc, *lc;
   uint32_t *intra; /* lookahead_intra_costs [h_imp][w_imp] */
-  orc_mv *mv8;     /* [R][h_imp][w_imp]: lookahead_mvs[k][2y][2x] */
-  uint32_t *inter; /* [R][h_imp][w_imp]: get_satd against the reference block at mv8 */
+  orc_mv *mv8;     /* [RA][h_imp][w_imp]: lookahead_mvs[k][2y][2x] */
+  uint32_t *inter; /* [RA][h_imp][w_imp]: get_satd against the reference block at mv8 */
   float *imp;      /* block_importances, per output frame */
 } ola;
 
 typedef struct orc_replay {
   int W, H, xdec, ydec, bd, hbd, R, C;
+  /* RA: the lookahead arrays' references (R = 2: 3, orc_la_refs); la_mode:
+   * the lookahead is running (its references are lar.disp[0 .. lar.n)) */
+  int RA, la_mode;
+  orc_la_refs lar;
   int w_in_b, h_in_b, w_imp, tx0, ty0, tw, th, tws, ths, nsb, cw, ch, vis_w, vis_h, ntx_c;
   /* per pyramid level: quantizers (TX_64X64 luma, TX_32X32 chroma, inter)
    * and lambdas (rv_replay_set_level_params) */
@@ -391,6 +412,7 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile
   r->bd = bd;
   r->hbd = bd > 8;
   r->R = n_refs;
+  r->RA = n_refs == 2 ? 3 : n_refs;
   r->C = NMODE * n_refs;
   r->w_in_b = 2 * ((W + 7) >> 3);
   r->h_in_b = 2 * ((H + 7) >> 3);
@@ -430,18 +452,18 @@ orc_replay *orc_replay_create(int W, int H, int xdec, int ydec, int bd, int tile
   }
   r->h_imp = r->h_in_b / 2;
   r->la_next = 1;
-  size_t nr = (size_t)r->R * r->nsb;
-  r->coarse = calloc(nr, sizeof(orc_mv));
+  size_t nr = (size_t)r->R * r->nsb, na = (size_t)r->RA * r->nsb;
+  r->coarse = calloc(na, sizeof(orc_mv));
   r->half = calloc(nr * 4, sizeof(orc_mv));
-  r->half_l = calloc(nr * 4, sizeof(orc_mv));
-  r->hlc = calloc(nr * 4, 8);
+  r->half_l = calloc(na * 4, sizeof(orc_mv));
+  r->hlc = calloc(na * 4, 8);
   r->tmv_e = calloc((size_t)r->R * r->tw * 16 * r->th * 16, sizeof(orc_mv));
-  r->tmv_l = calloc((size_t)r->R * r->tw * 16 * r->th * 16, sizeof(orc_mv));
-  r->look = calloc(nr * 16, sizeof(orc_mv));
-  r->lc = calloc(nr * 16, 8);
+  r->tmv_l = calloc((size_t)r->RA * r->tw * 16 * r->th * 16, sizeof(orc_mv));
+  r->look = calloc(na * 16, sizeof(orc_mv));
+  r->lc = calloc(na * 16, 8);
   r->full = calloc(nr, sizeof(orc_mv));
   r->sub = calloc(nr, sizeof(orc_mv));
-  r->cc = calloc(nr, 8);
+  r->cc = calloc(na, 8);
   r->hc = calloc(nr * 4, 8);
   r->fc = calloc(nr, 8);
   r->sc = calloc(nr, 8);
@@ -1018,6 +1040,13 @@ static orc_mv half_fp(const orc_replay *r, int k, int sb, int q) {
   return qfull((orc_mv){(int16_t)(h.row * 2), (int16_t)(h.col * 2)});
 }
 
+/* the references the current search pass runs over: the lookahead's (la_mode)
+ * or the encode's */
+static int nrefs(const orc_replay *r) { return r->la_mode ? r->lar.n : r->R; }
+static int rdisp(const orc_replay *r, int k) {
+  return r->la_mode ? r->lar.disp[k] : r->fi.ref_display[k];
+}
+
 /* Pass A1: F1 estimate_motion_ss4 (build_coarse_pmvs) of one superblock. */
 static void run_coarse(orc_replay *r, int sb) {
   const oinput *S = &r->inputs[r->fi.display % r->n_inputs];
@@ -1037,8 +1066,8 @@ static void run_coarse(orc_replay *r, int sb) {
   int y_lo = fby + ((m[2] / 8 > -ry ? m[2] / 8 : -ry) >> 2);
   int y_hi = fby + ((m[3] / 8 < ry ? m[3] / 8 : ry) >> 2);
   orc_mv zero = {0, 0};
-  for (int k = 0; k < r->R; k++) {
-    const oinput *ref = &r->inputs[r->fi.ref_display[k] % r->n_inputs];
+  for (int k = 0; k < nrefs(r); k++) {
+    const oinput *ref = &r->inputs[rdisp(r, k) % r->n_inputs];
     orc_mv best = {0, 0};
     uint64_t cost = UINT64_MAX;
     orc_full_search(org_of(&S->qres, hbd), S->qres.stride, org_of(&ref->qres, hbd),
@@ -1089,7 +1118,7 @@ static orc_mv coarse4(const orc_replay *r, int k, int sb) {
 static void half_quadrant(orc_replay *r, int sb, int k, int q, orc_mv *grid, const orc_mv *prev,
                           orc_mv *mv, uint64_t *cost) {
   const oinput *S = &r->inputs[r->fi.display % r->n_inputs];
-  const oinput *ref = &r->inputs[r->fi.ref_display[k] % r->n_inputs];
+  const oinput *ref = &r->inputs[rdisp(r, k) % r->n_inputs];
   const sbgeo g = sb_geo_of(r, sb);
   const double me_lambda = r->lv[r->fi.level].me_lambda;
   const uint32_t lambda2 = (uint32_t)(me_lambda * 256.0 / 4.0 * 0.125);
@@ -1118,7 +1147,7 @@ static void half_quadrant(orc_replay *r, int sb, int k, int q, orc_mv *grid, con
  * 2) saved into the field at the quadrants' own offsets (no adjust_bo). */
 static void half_sb(orc_replay *r, int sb, orc_mv *grid, orc_mv *mvs, uint64_t *costs, int encode) {
   const sbgeo g = sb_geo_of(r, sb);
-  for (int k = 0; k < r->R; k++) {
+  for (int k = 0; k < nrefs(r); k++) {
     /* subset C: the LAST reference's frame_mvs (fi.rec_buffer.frames[
      * fi.ref_frames[0]], src/me.rs:399-402, 479-481) */
     const orc_mv *prev = encode ? r->slots[r->fi.ref_display[0] % NSLOT].fmv +
@@ -1192,8 +1221,8 @@ static void full_res_sb(orc_replay *r, int sb) {
   const double me_lambda = r->lv[r->fi.level].me_lambda;
   uint32_t lambda1 = (uint32_t)(me_lambda * 256.0 * 0.5);
   const int hw = g.tsx > 0, he = g.tsx < g.tsw - 1, hn = g.tsy > 0, hs = g.tsy < g.tsh - 1;
-  for (int k = 0; k < r->R; k++) {
-    const oplane *orig = &r->inputs[r->fi.ref_display[k] % r->n_inputs].y;
+  for (int k = 0; k < nrefs(r); k++) {
+    const oplane *orig = &r->inputs[rdisp(r, k) % r->n_inputs].y;
     orc_mv *tile = tile_field(r, r->tmv_l, k, &g);
     /* pmvs_X[e] of superblock sb + (dx, dy): e = 0 coarse, 1..4 quadrants */
 #define PM(dx, dy, e)                                                              \
@@ -2198,20 +2227,50 @@ static long coded_of_display(long d) {
 
 static ola *la_of(orc_replay *r, long m) { return &r->la[m % (r->imp_window + 1)]; }
 
+/* orc_la_refs of coded frame m >= 1 (frame_info's group g, position j) */
+static orc_la_refs la_refs_of(long m, int R) {
+  orc_la_refs l;
+  memset(&l, 0, sizeof(l));
+  orc_frame_info f;
+  frame_info(m, R, &f);
+  for (int k = 0; k < R; k++) {
+    l.disp[k] = f.ref_display[k];
+    l.order[k] = k;
+  }
+  l.n = R;
+  const long g = (m - 1) / 4, j = (m - 1) % 4;
+  if (R == 2 && j > 0) {
+    /* LAST3: the previous frame of this level (4g+2: 4g-2; 4g+1: 4g-1, the
+     * last level-2 frame of group g-1; 4g+3: 4g+1), the key frame before */
+    const long d3 = j == 1 ? 4 * g - 2 : j == 2 ? 4 * g - 1 : 4 * g + 1;
+    l.disp[2] = (int)(d3 < 0 ? 0 : d3);
+    l.n = 3;
+    l.order[0] = 0;  /* LAST (the backward reference) */
+    l.order[1] = 2;  /* LAST3 */
+    l.order[2] = 1;  /* ALTREF (the forward reference) */
+  }
+  return l;
+}
+
 static void la_compute(orc_replay *r, long m) {
   const orc_frame_info save = r->fi;
   const int save_lim = r->sb_limit;
   frame_info(m, r->R, &r->fi);
   r->sb_limit = 0;
-  const size_t nr = (size_t)r->R * r->nsb;
+  r->lar = la_refs_of(m, r->R);
+  r->la_mode = 1;
+  const int RL = r->lar.n;
+  const size_t nr = (size_t)RL * r->nsb;
   input_pyr(r, r->fi.display);
-  for (int k = 0; k < r->R; k++) input_pyr(r, r->fi.ref_display[k]);
-  memset(r->tmv_l, 0, (size_t)r->R * r->tw * 16 * r->th * 16 * sizeof(orc_mv));
+  for (int k = 0; k < RL; k++) input_pyr(r, r->lar.disp[k]);
+  memset(r->tmv_l, 0, (size_t)RL * r->tw * 16 * r->th * 16 * sizeof(orc_mv));
   run_pass(r, 0);
   run_pass(r, 6);
+  r->la_mode = 0;
   ola *e = la_of(r, m);
   e->coded = m;
   e->fi = r->fi;
+  e->lr = r->lar;
   memcpy(e->coarse, r->coarse, nr * sizeof(orc_mv));
   memcpy(e->cc, r->cc, nr * 8);
   memcpy(e->half_l, r->half_l, nr * 4 * sizeof(orc_mv));
@@ -2226,11 +2285,11 @@ static void la_compute(orc_replay *r, long m) {
       orc_lookahead_intra_costs(at(&cur->y, hbd, x * 8, y * 8), cur->y.stride, 8, 8, hbd, r->bd,
                                 &e->intra[(size_t)y * w + x]);
       const int sb = (y / 8) * r->tw + x / 8, b = ((y % 8) / 2) * 4 + (x % 8) / 2;
-      for (int k = 0; k < r->R; k++)
+      for (int k = 0; k < RL; k++)
         e->mv8[k * ni + (size_t)y * w + x] = r->look[((size_t)k * r->nsb + sb) * 16 + b];
     }
-  for (int k = 0; k < r->R; k++) {
-    const oplane *ref = &r->inputs[r->fi.ref_display[k] % r->n_inputs].y;
+  for (int k = 0; k < RL; k++) {
+    const oplane *ref = &r->inputs[r->lar.disp[k] % r->n_inputs].y;
     orc_importance_inter_costs(at(&cur->y, hbd, 0, 0), cur->y.stride, at(ref, hbd, 0, 0),
                                ref->stride, w, h, hbd, e->mv8 + k * ni, e->inter + k * ni);
   }
@@ -2247,7 +2306,8 @@ static void la_fill(orc_replay *r) {
 
 /* compute_block_importances for frame n = r->coded: zero the window's
  * importances, propagate from its last frame down to n + 1 (each frame's
- * distinct references in order, the split by their count; references
+ * distinct reference slots in mv index order, orc_la_refs, the split by
+ * their count -- two slots may hold one frame, e.g. the key frame; targets
  * before n are outside the window and gone, :944-948), then log2(1 +
  * importance / intra cost) for frame n (:1052-1070). */
 static void importance_frame(orc_replay *r) {
@@ -2258,15 +2318,10 @@ static void importance_frame(orc_replay *r) {
   for (long m = last; m > n; m--) {
     const ola *e = la_of(r, m);
     if (e->fi.is_key) continue;
-    int uk[2], nu = 0;
-    for (int k = 0; k < r->R; k++) {
-      int dup = 0;
-      for (int j = 0; j < nu; j++) dup |= e->fi.ref_display[uk[j]] == e->fi.ref_display[k];
-      if (!dup) uk[nu++] = k;
-    }
+    const int nu = e->lr.n;
     for (int j = 0; j < nu; j++) {
-      const int k = uk[j];
-      const long mref = coded_of_display(e->fi.ref_display[k]);
+      const int k = e->lr.order[j];
+      const long mref = coded_of_display(e->lr.disp[k]);
       if (mref < n) continue;
       orc_propagate_importances_costs(w, h, e->mv8 + k * ni, e->inter + k * ni, e->intra, e->imp,
                                       nu, la_of(r, mref)->imp);
@@ -2294,7 +2349,7 @@ int orc_replay_set_imp_window(orc_replay *r, int window, long limit) {
   r->la_limit = limit;
   r->la_next = 1;
   if (!window) return 0;
-  const size_t nr = (size_t)r->R * r->nsb, ni = (size_t)r->w_imp * r->h_imp;
+  const size_t nr = (size_t)r->RA * r->nsb, ni = (size_t)r->w_imp * r->h_imp;
   r->la = calloc((size_t)window + 1, sizeof(ola));
   r->imp_own = calloc(ni, sizeof(float));
   if (!r->la || !r->imp_own) return -1;
@@ -2309,8 +2364,8 @@ int orc_replay_set_imp_window(orc_replay *r, int window, long limit) {
     e->look = calloc(nr * 16, sizeof(orc_mv));
     e->lc = calloc(nr * 16, 8);
     e->intra = calloc(ni, 4);
-    e->mv8 = calloc(ni * r->R, sizeof(orc_mv));
-    e->inter = calloc(ni * r->R, 4);
+    e->mv8 = calloc(ni * r->RA, sizeof(orc_mv));
+    e->inter = calloc(ni * r->RA, 4);
     e->imp = calloc(ni, 4);
     if (!e->coarse || !e->cc || !e->half_l || !e->hlc || !e->look || !e->lc || !e->intra ||
         !e->mv8 || !e->inter || !e->imp)
@@ -2320,17 +2375,36 @@ int orc_replay_set_imp_window(orc_replay *r, int window, long limit) {
 }
 
 /* ring entry of coded frame m (tests): its intra costs [h_imp][w_imp], 8x8
- * lookahead MVs and inter costs [R][h_imp][w_imp], references; -1: absent */
+ * lookahead MVs and inter costs [n][h_imp][w_imp] of its lookahead
+ * references, and refs[0] = n, refs[1..3] their displays (k order),
+ * refs[4..6] the propagation order; -1: absent */
 int orc_replay_la_data(orc_replay *r, long m, uint32_t *intra, orc_mv *mv8, uint32_t *inter,
-                       int32_t *ref_display) {
+                       int32_t *refs) {
   if (!r->imp_window || m < 1) return -1;
   const ola *e = la_of(r, m);
   if (e->coded != m) return -1;
   const size_t ni = (size_t)r->w_imp * r->h_imp;
   memcpy(intra, e->intra, ni * 4);
-  memcpy(mv8, e->mv8, ni * r->R * sizeof(orc_mv));
-  memcpy(inter, e->inter, ni * r->R * 4);
-  for (int k = 0; k < r->R; k++) ref_display[k] = e->fi.ref_display[k];
+  memcpy(mv8, e->mv8, ni * e->lr.n * sizeof(orc_mv));
+  memcpy(inter, e->inter, ni * e->lr.n * 4);
+  refs[0] = e->lr.n;
+  for (int k = 0; k < 3; k++) {
+    refs[1 + k] = k < e->lr.n ? e->lr.disp[k] : -1;
+    refs[4 + k] = k < e->lr.n ? e->lr.order[k] : -1;
+  }
+  return 0;
+}
+
+/* the orc_la_refs of coded frame m >= 1 (tests): out[0] = n, out[1..3] the
+ * displays in k order, out[4..6] the propagation order (-1: unused) */
+int orc_replay_la_refs(long m, int R, int32_t *out) {
+  if (m < 1 || R < 1 || R > 2) return -1;
+  const orc_la_refs l = la_refs_of(m, R);
+  out[0] = l.n;
+  for (int k = 0; k < 3; k++) {
+    out[1 + k] = k < l.n ? l.disp[k] : -1;
+    out[4 + k] = k < l.n ? l.order[k] : -1;
+  }
   return 0;
 }
 

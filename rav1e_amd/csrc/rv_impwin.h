@@ -9,7 +9,7 @@
 // contributions land depends only on its lookahead MV, so the device
 // computes that once per frame (impwin_frame_data): a stable sort by target
 // turns the frame's 4 x n_imp (target, source) pairs into per-target lists
-// in source order (CSR).  A window pass (impwin_pass) is then one thread
+// in source order (CSR, a counting sort: rv_csr.h).  A window pass (impwin_pass) is then one thread
 // per target that adds its list's contributions onto its current value in
 // that order -- the reference's sum, rounding for rounding, with no atomics.
 #pragma once
@@ -17,6 +17,10 @@
 #include "rv_device.h"
 
 namespace rv {
+
+// references whose lookahead a frame's importances propagate into: rav1e's
+// distinct DPB slots of fi.ref_frames, at most 3 (src/api/internal.rs:875-882)
+constexpr int kImpMaxRefs = 3;
 
 // The importance data of one coded frame (a lookahead ring entry); every
 // array over the frame's 8x8 blocks [h_imp][w_imp] (n = w_imp * h_imp).
@@ -42,9 +46,9 @@ int impwin_frame_data(const rv_plane &cur, const rv_plane *refs, int R, int bit_
                       const rv_fs_result *look, int tw, int nsb, int w_imp, int h_imp,
                       const ImpFrame &f, void *scratch, size_t scratch_bytes, hipStream_t st);
 
-// The (frame, reference ks[i]) passes, i < np <= 2, in one launch: the
-// source frame's contributions (split over nu distinct references) added
-// onto ref_imp[i] (distinct frames).
+// The (frame, reference ks[i]) passes, i < np <= kImpMaxRefs, in one
+// launch: the source frame's contributions (split over its nu reference
+// slots) added onto ref_imp[i] (distinct frames).
 int impwin_pass(const ImpFrame &src, const int *ks, float *const *ref_imp, int np, int nu,
                 int w_imp, int h_imp, hipStream_t st);
 

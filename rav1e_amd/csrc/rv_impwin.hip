@@ -3,8 +3,9 @@
 // rv_impwin.h for the decomposition.  f32 arithmetic in the reference's
 // operation order: products and sums round separately (-ffp-contract=off),
 // divisions are correctly rounded (__fdiv_rn), as in Rust.
-#include <hipcub/hipcub.hpp>
+#include <string.h>
 
+#include "rv_csr.h"
 #include "rv_impwin.h"
 
 namespace rv {
@@ -15,28 +16,19 @@ constexpr int kImpB = 8, kMvUnits = 8, kBMv = kImpB * kMvUnits, kAreaMv = kBMv *
 
 size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
-int key_bits(uint32_t n) {  // keys are 0..n
-  int b = 1;
-  while (b < 32 && (n >> b) != 0) b++;
-  return b;
-}
-
-struct SortScratch {
-  size_t keys_in, vals_in, keys_out, temp, temp_bytes, total;
+// impwin_frame_data's scratch: the entries' keys [R][4 n], the per-target
+// counts and cursors [R][n] (rv_csr.h)
+struct CsrScratch {
+  size_t keys, cnt, cur, total;
 };
 
-SortScratch sort_scratch(int n) {
-  SortScratch s;
+CsrScratch csr_scratch(int n) {
+  CsrScratch s;
   const size_t m = 4 * (size_t)n;
-  s.keys_in = 0;
-  s.vals_in = al256(4 * m);
-  s.keys_out = al256(s.vals_in + 4 * m);
-  s.temp = al256(s.keys_out + 4 * m);
-  s.temp_bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, s.temp_bytes, (const uint32_t *)nullptr,
-                                           (uint32_t *)nullptr, (const int32_t *)nullptr,
-                                           (int32_t *)nullptr, (int)m, 0, key_bits((uint32_t)n));
-  s.total = al256(s.temp + s.temp_bytes);
+  s.keys = 0;
+  s.cnt = al256(s.keys + 4 * m * kImpMaxRefs);
+  s.cur = al256(s.cnt + 4 * (size_t)n * kImpMaxRefs);
+  s.total = al256(s.cur + 4 * (size_t)n * kImpMaxRefs);
   return s;
 }
 
@@ -71,75 +63,58 @@ __device__ inline uint32_t satd8(const Px *o, int64_t os, const Px *r, int64_t r
   return (uint32_t)((satd_chunk<8>(d) + 4) >> 3);  // get_satd 8x8: ln = msb(8)
 }
 
-// One thread per 8x8 block: lookahead_intra_costs (pred_dc_128, :680-765),
-// the lookahead MV of the 16x16 holding it, per reference get_satd against
-// the original reference block at that MV (:911-931) and the propagate
-// fraction (:939), and the (target, 4 * block + corner) sort pairs.
+// One thread per 8x8 block and reference (blockIdx.y): lookahead_intra_costs
+// (pred_dc_128, :680-765; reference 0 stores them), the lookahead MV of the
+// 16x16 holding the block, get_satd against the reference's original block
+// at that MV (:911-931) and the propagate fraction (:939), and the block's
+// four (target, 4 * block + corner) entries, counted per target.
 struct DataArgs {
-  rv_plane cur, ref;
-  int k, base, w, h, tw, nsb;  // k: the reference (k = 0 also writes the intra costs)
+  rv_plane cur, ref[kImpMaxRefs];
+  int base, w, h, tw, nsb;
   const rv_fs_result *look;
   ImpFrame f;
-  uint32_t *keys;  // [4 n]
-  int32_t *vals;   // [4 n]
+  uint32_t *keys;  // [R][4 n]
+  int32_t *cnt;    // [R][n], zero on entry
 };
 
 template <typename Px>
 __global__ __launch_bounds__(256) void data_kernel(DataArgs a) {
   const int n = a.w * a.h;
   const int i = blockIdx.x * 256 + threadIdx.x;
+  const int k = blockIdx.y;
   if (i >= n) return;
   const int x = i % a.w, y = i / a.w;
   const Px *o = plane_ptr<Px>(a.cur, x * kImpB, y * kImpB);
   const uint32_t intra = satd8<Px>(o, a.cur.stride, (const Px *)nullptr, 0, a.base);
-  if (a.k == 0) a.f.intra[i] = intra;
+  if (k == 0) a.f.intra[i] = intra;
   const int sb = (y / 8) * a.tw + x / 8, b = ((y % 8) / 2) * 4 + (x % 8) / 2;
-  {
-    const int k = a.k;
-    const rv_plane &ref = a.ref;
-    const rv_mv mv = a.look[((size_t)k * a.nsb + sb) * 16 + b].best_mv;
-    a.f.mv8[(size_t)k * n + i] = mv;
-    const int64_t px_x = ((int64_t)x * kBMv + mv.col) / kMvUnits;  // isize `/`
-    const int64_t px_y = ((int64_t)y * kBMv + mv.row) / kMvUnits;
-    // the reference block must lie inside the allocation (the reference's
-    // region would panic): the search windows keep it there
-    const bool inside = px_x >= -ref.xorigin && px_y >= -ref.yorigin &&
-                        px_x + kImpB <= ref.stride - ref.xorigin &&
-                        px_y + kImpB <= ref.alloc_height - ref.yorigin;
-    float frac = 0.f;
-    if (inside) {
-      const float inter = (float)satd8<Px>(o, a.cur.stride, plane_ptr<Px>(ref, (int)px_x, (int)px_y),
-                                           ref.stride, 0);
-      // f32::max(NaN, 0) = 0, as fmaxf
-      frac = fmaxf(1.0f - __fdiv_rn(inter, (float)intra), 0.0f);
-    }
-    a.f.frac[(size_t)k * n + i] = frac;
-    int tgt[4];
-    float fr[4];
-    corners(x, y, mv, a.w, a.h, tgt, fr);
+  const rv_plane &ref = a.ref[k];
+  const rv_mv mv = a.look[((size_t)k * a.nsb + sb) * 16 + b].best_mv;
+  a.f.mv8[(size_t)k * n + i] = mv;
+  const int64_t px_x = ((int64_t)x * kBMv + mv.col) / kMvUnits;  // isize `/`
+  const int64_t px_y = ((int64_t)y * kBMv + mv.row) / kMvUnits;
+  // the reference block must lie inside the allocation (the reference's
+  // region would panic): the search windows keep it there
+  const bool inside = px_x >= -ref.xorigin && px_y >= -ref.yorigin &&
+                      px_x + kImpB <= ref.stride - ref.xorigin &&
+                      px_y + kImpB <= ref.alloc_height - ref.yorigin;
+  float frac = 0.f;
+  if (inside) {
+    const float inter = (float)satd8<Px>(o, a.cur.stride, plane_ptr<Px>(ref, (int)px_x, (int)px_y),
+                                         ref.stride, 0);
+    // f32::max(NaN, 0) = 0, as fmaxf
+    frac = fmaxf(1.0f - __fdiv_rn(inter, (float)intra), 0.0f);
+  }
+  a.f.frac[(size_t)k * n + i] = frac;
+  int tgt[4];
+  float fr[4];
+  corners(x, y, mv, a.w, a.h, tgt, fr);
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const size_t j = 4 * (size_t)i + c;
-      a.keys[j] = inside ? (uint32_t)tgt[c] : (uint32_t)n;
-      a.vals[j] = 4 * i + c;
-    }
+  for (int c = 0; c < 4; c++) {
+    const uint32_t key = inside ? (uint32_t)tgt[c] : (uint32_t)n;
+    a.keys[(size_t)k * 4 * n + 4 * (size_t)i + c] = key;
+    if (key < (uint32_t)n) atomicAdd(a.cnt + (size_t)k * n + key, 1);
   }
-}
-
-// off[t] = the first sorted position whose key is >= t (t = 0 .. n)
-__global__ __launch_bounds__(256) void offsets_kernel(const uint32_t *keys, int m, int n,
-                                                      int32_t *off) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t > n) return;
-  int lo = 0, hi = m;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (keys[mid] < (uint32_t)t)
-      lo = mid + 1;
-    else
-      hi = mid;
-  }
-  off[t] = lo;
 }
 
 // One window pass: target t of the reference frame adds its sources'
@@ -149,10 +124,10 @@ __global__ __launch_bounds__(256) void offsets_kernel(const uint32_t *keys, int 
 struct PassSet {
   const uint32_t *intra;
   const float *imp;
-  const rv_mv *mv8[2];
-  const float *frac[2];
-  const int32_t *off[2], *src[2];
-  float *ref_imp[2];
+  const rv_mv *mv8[kImpMaxRefs];
+  const float *frac[kImpMaxRefs];
+  const int32_t *off[kImpMaxRefs], *src[kImpMaxRefs];
+  float *ref_imp[kImpMaxRefs];
   int nu;
 };
 __global__ __launch_bounds__(256) void pass_kernel(PassSet p, int w, int h) {
@@ -254,21 +229,23 @@ void impwin_frame_carve(ImpFrame &f, void *base, int n, int R) {
   f.fin = (float *)m;
 }
 
-size_t impwin_scratch_bytes(int n) { return sort_scratch(n).total; }
+size_t impwin_scratch_bytes(int n) { return csr_scratch(n).total; }
 
 int impwin_frame_data(const rv_plane &cur, const rv_plane *refs, int R, int bit_depth,
                       const rv_fs_result *look, int tw, int nsb, int w_imp, int h_imp,
                       const ImpFrame &f, void *scratch, size_t scratch_bytes, hipStream_t st) {
   const int n = w_imp * h_imp;
-  if (R < 1 || R > 2 || n <= 0 || cur.xorigin + w_imp * 8 > cur.stride ||
+  if (R < 1 || R > kImpMaxRefs || n <= 0 || cur.xorigin + w_imp * 8 > cur.stride ||
       cur.yorigin + h_imp * 8 > cur.alloc_height)
     return rv_set_error(RV_EINVAL, "impwin_frame_data: bad geometry");
-  const SortScratch s = sort_scratch(n);
+  const CsrScratch s = csr_scratch(n);
   if (!scratch || scratch_bytes < s.total)
     return rv_set_error(RV_EINVAL, "impwin_frame_data: scratch");
   uint8_t *base = (uint8_t *)scratch;
   DataArgs a;
+  memset(&a, 0, sizeof(a));
   a.cur = cur;
+  for (int k = 0; k < R; k++) a.ref[k] = refs[k];
   a.base = 128 << (bit_depth - 8);
   a.w = w_imp;
   a.h = h_imp;
@@ -276,36 +253,27 @@ int impwin_frame_data(const rv_plane &cur, const rv_plane *refs, int R, int bit_
   a.nsb = nsb;
   a.look = look;
   a.f = f;
-  a.keys = (uint32_t *)(base + s.keys_in);
-  a.vals = (int32_t *)(base + s.vals_in);
-  uint32_t *keys_out = (uint32_t *)(base + s.keys_out);
-  const int m = 4 * n;
-  const unsigned nb = (unsigned)((n + 255) / 256);
-  for (int k = 0; k < R; k++) {
-    a.k = k;
-    a.ref = refs[k];
-    if (cur.hbd)
-      data_kernel<uint16_t><<<nb, 256, 0, st>>>(a);
-    else
-      data_kernel<uint8_t><<<nb, 256, 0, st>>>(a);
-    RV_HIP_CHECK_LAUNCH();
-    // stable: a target's sources stay in raster order (the reference's order)
-    size_t tb = s.temp_bytes;
-    if (hipcub::DeviceRadixSort::SortPairs(base + s.temp, tb, a.keys, keys_out, a.vals,
-                                           f.src + (size_t)k * m, m, 0,
-                                           key_bits((uint32_t)n), st) != hipSuccess)
-      return rv_set_error(RV_EHIP, "impwin_frame_data: sort");
-    offsets_kernel<<<(unsigned)((n + 1 + 255) / 256), 256, 0, st>>>(keys_out, m, n,
-                                                                    f.off + (size_t)k * (n + 1));
-    RV_HIP_CHECK_LAUNCH();
+  a.keys = (uint32_t *)(base + s.keys);
+  a.cnt = (int32_t *)(base + s.cnt);
+  int32_t *cursor = (int32_t *)(base + s.cur);
+  {
+    const hipError_t e = hipMemsetAsync(a.cnt, 0, (size_t)R * n * 4, st);
+    if (e != hipSuccess) return rv_set_hip_error(e, "impwin_frame_data");
   }
-  return RV_OK;
+  const dim3 grid((unsigned)((n + 255) / 256), (unsigned)R);
+  if (cur.hbd)
+    data_kernel<uint16_t><<<grid, 256, 0, st>>>(a);
+  else
+    data_kernel<uint8_t><<<grid, 256, 0, st>>>(a);
+  RV_HIP_CHECK_LAUNCH();
+  // every reference's target lists, in source order within a target
+  return csr_build(a.keys, 4 * n, n, R, a.cnt, cursor, f.off, f.src, st);
 }
 
 int impwin_pass(const ImpFrame &src, const int *ks, float *const *ref_imp, int np, int nu,
                 int w_imp, int h_imp, hipStream_t st) {
   const int n = w_imp * h_imp;
-  if (nu < 1 || nu > 3 || n <= 0 || np < 1 || np > 2)
+  if (nu < 1 || nu > kImpMaxRefs || n <= 0 || np < 1 || np > kImpMaxRefs)
     return rv_set_error(RV_EINVAL, "impwin_pass: bad arguments");
   PassSet p;
   p.intra = src.intra;

@@ -10,14 +10,13 @@
 // depends on its order, so the device does not scatter with atomics:
 //   1. one thread per source block writes its four (target, amount *
 //      fraction) contributions at [4 * source + k] -- the reference's order;
-//   2. a stable radix sort by target (hipcub) groups them, keeping that
-//      order within a target;
+//   2. a counting sort by target (rv_csr.h: the keys are bounded block
+//      indices) groups them, keeping that order within a target;
 //   3. one thread per target adds its contributions in order onto the
 //      target's current value, as the reference's `+=` sequence does.
 // Products and sums are separate roundings (-ffp-contract=off) and the
 // divisions are correctly rounded (__fdiv_rn), as in Rust.
-#include <hipcub/hipcub.hpp>
-
+#include "rv_csr.h"
 #include "rv_device.h"
 
 namespace rv {
@@ -27,7 +26,7 @@ constexpr int kImpB = 8, kMvUnits = 8, kBMv = kImpB * kMvUnits, kAreaMv = kBMv *
 template <typename Px>
 __global__ __launch_bounds__(256) void importance_contrib_kernel(
     rv_plane org, rv_plane ref, int nbx, int nby, const rv_mv *mvs, const uint32_t *intra,
-    const float *imp, int n_unique, uint32_t *keys, float *vals) {
+    const float *imp, int n_unique, uint32_t *keys, float *vals, int32_t *cnt) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int n = nbx * nby;
   if (i >= n) return;
@@ -44,6 +43,7 @@ __global__ __launch_bounds__(256) void importance_contrib_kernel(
   float val[4] = {0.f, 0.f, 0.f, 0.f};
   if (inside) {
     const Px *o = plane_ptr<Px>(org, x * kImpB, y * kImpB);
+
     const Px *r = plane_ptr<Px>(ref, (int)px_x, (int)px_y);
     int32_t d[64];
 #pragma unroll
@@ -77,50 +77,42 @@ __global__ __launch_bounds__(256) void importance_contrib_kernel(
   for (int k = 0; k < 4; k++) {
     keys[4 * (int64_t)i + k] = key[k];
     vals[4 * (int64_t)i + k] = val[k];
+    if (key[k] < (uint32_t)n) atomicAdd(cnt + key[k], 1);
   }
 }
 
-// One thread per run of equal keys (the sorted contributions of a target):
-// the target's value plus its contributions, one rounding per addition, in
-// the reference's order.
-__global__ __launch_bounds__(256) void importance_accumulate_kernel(const uint32_t *keys,
-                                                                    const float *vals,
-                                                                    int64_t m, uint32_t n,
+// One thread per target: its value plus its contributions (src: entry
+// indices in source order), one rounding per addition, in the reference's
+// order.
+__global__ __launch_bounds__(256) void importance_accumulate_kernel(const int32_t *off,
+                                                                    const int32_t *src,
+                                                                    const float *vals, int n,
                                                                     float *ref_imp) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= m) return;
-  const uint32_t k = keys[i];
-  if (k >= n || (i > 0 && keys[i - 1] == k)) return;
-  float acc = ref_imp[k];
-  for (int64_t j = i; j < m && keys[j] == k; j++) acc = acc + vals[j];
-  ref_imp[k] = acc;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  const int a = off[t], b = off[t + 1];
+  if (a == b) return;
+  float acc = ref_imp[t];
+  for (int j = a; j < b; j++) acc = acc + vals[src[j]];
+  ref_imp[t] = acc;
 }
 
 struct ImpScratch {
-  size_t keys_in, vals_in, keys_out, vals_out, temp, temp_bytes, total;
+  size_t keys, vals, cnt, cur, off, src, total;
 };
 
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
-static int key_bits(uint32_t n) {  // keys are 0..n
-  int b = 1;
-  while (b < 32 && (n >> b) != 0) b++;
-  return b;
-}
-
 static ImpScratch imp_scratch(int n) {
   ImpScratch s;
   const size_t m = 4 * (size_t)n;
-  s.keys_in = 0;
-  s.vals_in = align256(s.keys_in + 4 * m);
-  s.keys_out = align256(s.vals_in + 4 * m);
-  s.vals_out = align256(s.keys_out + 4 * m);
-  s.temp = align256(s.vals_out + 4 * m);
-  s.temp_bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, s.temp_bytes, (const uint32_t *)nullptr,
-                                           (uint32_t *)nullptr, (const float *)nullptr,
-                                           (float *)nullptr, (int)m, 0, key_bits((uint32_t)n));
-  s.total = align256(s.temp + s.temp_bytes);
+  s.keys = 0;
+  s.vals = align256(s.keys + 4 * m);
+  s.cnt = align256(s.vals + 4 * m);
+  s.cur = align256(s.cnt + 4 * (size_t)n);
+  s.off = align256(s.cur + 4 * (size_t)n);
+  s.src = align256(s.off + 4 * ((size_t)n + 1));
+  s.total = align256(s.src + 4 * m);
   return s;
 }
 
@@ -151,27 +143,30 @@ extern "C" int rv_propagate_importances(const rv_plane *org, const rv_plane *ref
     return rv_set_error(RV_EINVAL, "rv_propagate_importances: scratch below "
                                    "rv_propagate_importances_scratch()");
   uint8_t *base = (uint8_t *)d_scratch;
-  uint32_t *keys_in = (uint32_t *)(base + s.keys_in), *keys_out = (uint32_t *)(base + s.keys_out);
-  float *vals_in = (float *)(base + s.vals_in), *vals_out = (float *)(base + s.vals_out);
+  uint32_t *keys = (uint32_t *)(base + s.keys);
+  float *vals = (float *)(base + s.vals);
+  int32_t *cnt = (int32_t *)(base + s.cnt), *cur = (int32_t *)(base + s.cur);
+  int32_t *off = (int32_t *)(base + s.off), *src = (int32_t *)(base + s.src);
   hipStream_t st = rv_resolve_stream(stream);
+  {
+    const hipError_t e = hipMemsetAsync(cnt, 0, (size_t)n * 4, st);
+    if (e != hipSuccess) return rv_set_hip_error(e, "rv_propagate_importances");
+  }
   const unsigned g1 = (unsigned)((n + 255) / 256);
   if (org->hbd)
     importance_contrib_kernel<uint16_t><<<g1, 256, 0, st>>>(*org, *ref, nbx, nby, d_mvs,
                                                             d_intra_costs, d_importances,
-                                                            n_unique, keys_in, vals_in);
+                                                            n_unique, keys, vals, cnt);
   else
     importance_contrib_kernel<uint8_t><<<g1, 256, 0, st>>>(*org, *ref, nbx, nby, d_mvs,
                                                            d_intra_costs, d_importances,
-                                                           n_unique, keys_in, vals_in);
+                                                           n_unique, keys, vals, cnt);
   RV_HIP_CHECK_LAUNCH();
-  const int m = 4 * n;
-  size_t temp_bytes = s.temp_bytes;
-  if (hipcub::DeviceRadixSort::SortPairs(base + s.temp, temp_bytes, keys_in, keys_out, vals_in,
-                                         vals_out, m, 0, key_bits((uint32_t)n), st) !=
-      hipSuccess)
-    return rv_set_error(RV_EHIP, "rv_propagate_importances: sort");
-  importance_accumulate_kernel<<<(unsigned)((m + 255) / 256), 256, 0, st>>>(
-      keys_out, vals_out, m, (uint32_t)n, d_ref_importances);
+  {
+    const int e = csr_build(keys, 4 * n, n, 1, cnt, cur, off, src, st);
+    if (e != RV_OK) return e;
+  }
+  importance_accumulate_kernel<<<g1, 256, 0, st>>>(off, src, vals, n, d_ref_importances);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

@@ -93,6 +93,9 @@ struct DsArgs {
   rv_fs_result *out;
   int n, n_per_ref, w, h, subpel, satd, hp, bd;
   uint32_t *evals;  // optional: in-range candidate evaluations per job
+  // optional (ds_fast_kernel): [0] += the launch's candidate evaluations,
+  // [1] += its jobs -- the bench's kernel probe (algorithmic bytes per launch)
+  uint32_t *eval_acc;
   ChainNext next;   // replay: feed the winner into the next stage's jobs
   int tele;         // 1: telescopic_subpel_search instead of the diamond
   const rv_fs_result *start;  // tele: the search's start (best_mv, lowest_cost)
@@ -663,10 +666,17 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
       }
     }
   }
-  if (a.evals) {
+  if (a.evals || a.eval_acc) {
     if (lane == 0) wevals[wave] = evals;
     __syncthreads();
-    if (threadIdx.x == 0) a.evals[job] = wevals[0] + wevals[1] + wevals[2] + wevals[3];
+    if (threadIdx.x == 0) {
+      const uint32_t ev = wevals[0] + wevals[1] + wevals[2] + wevals[3];
+      if (a.evals) a.evals[job] = ev;
+      if (a.eval_acc) {
+        atomicAdd(a.eval_acc, ev);
+        atomicAdd(a.eval_acc + 1, 1u);
+      }
+    }
   }
   if (threadIdx.x == 0) {
     ds_write(a, job, center, center_cost);
@@ -1532,7 +1542,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             rv_fs_result *d_out, uint32_t *d_evals, const ChainNext *next,
                             void *stream, const uint8_t *active, const int32_t *alist,
                             const int32_t *acount, int lper, const uint8_t *dirty,
-                            int list_grid) {
+                            int list_grid, uint32_t *eval_acc) {
   auto p2 = [](int v) { return v >= 4 && v <= 128 && (v & (v - 1)) == 0; };
   if (!org || !refs || n_refs < 1 || n_refs > RV_MAX_REFS || n_per_ref < 0 || !p2(blk_w) ||
       !p2(blk_h) || (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
@@ -1564,6 +1574,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
   a.lper = lper;
   a.dirty = alist ? dirty : nullptr;
   a.list_grid = list_grid;
+  a.eval_acc = eval_acc;
   if (alist && (!acount || lper < 0 || use_satd ||
                 !((blk_w == 64 && blk_h == 64) || (blk_w == 16 && blk_h == 16 && !subpixel))))
     return rv_set_error(RV_EINVAL,
@@ -1654,7 +1665,7 @@ extern "C" int rv_diamond_search_batch(const rv_plane *org, const rv_plane *ref,
   if (!ref) return rv_set_error(RV_EINVAL, "rv_diamond_search_batch: null ref");
   return rv_diamond_search_multi(org, ref, 1, d_jobs, n, blk_w, blk_h, subpixel, use_satd,
                                  allow_hp, bit_depth, d_out, nullptr, nullptr, stream, nullptr,
-                                 nullptr, nullptr, 0, nullptr, 0);
+                                 nullptr, nullptr, 0, nullptr, 0, nullptr);
 }
 
 // telescopic_subpel_search (src/me.rs:858-941) for every job in one launch:

@@ -69,7 +69,8 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             rv_fs_result *d_out, uint32_t *d_evals, const rv::ChainNext *next,
                             void *stream, const uint8_t *active = nullptr,
                             const int32_t *alist = nullptr, const int32_t *acount = nullptr,
-                            int lper = 1, const uint8_t *dirty = nullptr, int list_grid = 0);
+                            int lper = 1, const uint8_t *dirty = nullptr, int list_grid = 0,
+                            uint32_t *eval_acc = nullptr);
 int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_job *jobs_h,
                      rv_fs_result *out_h, const uint8_t *dirty_h, const rv_plane *org,
                      const rv_plane *refs, const rv_ds_job *jobs, rv_fs_result *out,
@@ -372,6 +373,7 @@ struct LaArgs {
   int32_t *list_h, *list_l;      // out: the marked F2L / FL jobs
   int init;                      // 1: store the sets, mark nothing
   int what;                      // bit 0: the F2L jobs, bit 1: the FL jobs
+  int nref;                      // the lookahead's references (LaRefs::n)
   RoundPub pub;                  // pub.cnt: [F2L marked, FL marked]
 };
 
@@ -382,7 +384,7 @@ __device__ inline rv_mv la_coarse4(const LaArgs &a, int k, int sb) {
 
 __global__ __launch_bounds__(256) void la_check_kernel(LaArgs a) {
   const Geo &g = a.g;
-  const int nh = (a.what & 1) ? g.R * g.nsb * 4 : 0, nl = (a.what & 2) ? g.R * g.nsb * 16 : 0;
+  const int nh = (a.what & 1) ? a.nref * g.nsb * 4 : 0, nl = (a.what & 2) ? a.nref * g.nsb * 16 : 0;
   const int i = blockIdx.x * 256 + threadIdx.x;
   bool mh = false, ml = false;
   int job = 0;
@@ -972,6 +974,12 @@ struct RoundRing {
   }
 };
 
+// A frame's lookahead references (la_refs_of below): the displays in k order
+// and the propagation order
+struct LaRefs {
+  int n, disp[kImpMaxRefs], order[kImpMaxRefs];
+};
+
 // Where a frame's lookahead writes (compute_lookahead_motion_vectors):
 // F1 [R][nsb], F2L [R][nsb][4], FL [R][nsb][16]
 struct LaOut {
@@ -993,6 +1001,7 @@ struct LaOut {
 // is done; the engine reuses entry m % RW for frame m + RW only after that.
 // RW = W + 1 + kLaSlack: the slack covers the frames a twin instance still
 // has in flight behind the primary.
+constexpr int kEngineWaitS = 60;  // la_engine_take's bound on one frame's wait
 struct RvLaEngine {
   static constexpr int kLaSlack = 28;
   int W = 0, RW = 0, dev = 0;
@@ -1008,6 +1017,7 @@ struct RvLaEngine {
     long m = -1;       // the coded frame the entry holds
     long used_by = -1; // host: the frame whose encode recorded ev_used
     rv_replay_frame_info fi{};
+    LaRefs lr{};
     hipEvent_t ev_imp = nullptr, ev_used = nullptr;
   };
   std::vector<Entry> ring;
@@ -1029,6 +1039,7 @@ struct RvLaEngine {
 struct rv_replay {
   rv_replay_cfg cfg;
   Geo g;
+  int RA = 1;  // the lookahead's references (LaRefs; R = 2: 3, LAST3 added)
   CandGeo cg;
   hipStream_t stream;
   // FL runs on a second stream, overlapping F3/F4 (it only needs F1/F2's
@@ -1190,6 +1201,17 @@ struct rv_replay {
   long timed = 0;
   // diamond candidate evaluations per job, per ring slot: [kRing][2][nsb*R]
   uint32_t *ds_evals;
+  // Kernel probe (rv_replay_set_kernel_probe): on instrumented frames every
+  // F3 sub-pel launch (ds_fast_kernel<W = H = 64, sub-pel>: round 0 and the
+  // MV-stack rounds) is bracketed by an event pair on its stream, and the
+  // launches add their candidate evaluations and jobs into kp_cnt.  Pair i
+  // uses kp_ev[2 (i % kKp)], harvested (elapsed time summed) before reuse.
+  bool kprobe = false;
+  static constexpr int kKp = 512;
+  std::vector<hipEvent_t> kp_ev;
+  long kp_n = 0, kp_done = 0, kp_base = 0;  // pairs recorded / harvested / at the last start
+  double kp_ms = 0.0;
+  uint32_t *kp_cnt = nullptr;  // device [2]: evaluations, jobs
 };
 
 namespace {
@@ -1199,6 +1221,19 @@ void *dalloc(rv_replay *r, size_t bytes) {
   if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return nullptr;
   r->allocs.push_back(p);
   return p;
+}
+
+// the kernel probe's pairs [kp_done, upto): their elapsed times summed
+hipError_t kp_harvest(rv_replay *r, long upto) {
+  for (; r->kp_done < upto; r->kp_done++) {
+    const size_t i = 2 * (size_t)(r->kp_done % rv_replay::kKp);
+    hipError_t e = hipEventSynchronize(r->kp_ev[i + 1]);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, r->kp_ev[i], r->kp_ev[i + 1]);
+    if (e != hipSuccess) return e;
+    r->kp_ms += ms;
+  }
+  return hipSuccess;
 }
 
 // Frame::new (src/frame/mod.rs:55-90): luma pad 64 + 24, chroma >> dec
@@ -1295,7 +1330,9 @@ int build_static_jobs(rv_replay *r) {
     // F1 coarse jobs (estimate_motion_ss4) at this level's me_range_scale
     const int s = 4 >> lv;
     const uint32_t lambda4 = (uint32_t)(me_lambda * 256.0 / 16.0 * 0.125);
-    std::vector<rv_fs_job> jobs(g.nsb * g.R);
+    // every job array holds the lookahead's references (RA >= R: the
+    // encode's first, then LAST3, la_refs_of); the encode launches R
+    std::vector<rv_fs_job> jobs(g.nsb * r->RA);
     for (int sb = 0; sb < g.nsb; sb++) {
       const int sx = sb % g.tw, sy = sb / g.tw;
       int t0x, t0y, mi_w, mi_h;
@@ -1315,7 +1352,7 @@ int build_static_jobs(rv_replay *r) {
       j.y_lo = fby + (mx(-range_y, div_trunc8(mr[2])) >> 2);
       j.y_hi = fby + (mn(range_y, div_trunc8(mr[3])) >> 2);
       j.lambda = lambda4;
-      for (int k = 0; k < g.R; k++) jobs[k * g.nsb + sb] = j;  // ref-major
+      for (int k = 0; k < r->RA; k++) jobs[k * g.nsb + sb] = j;  // ref-major
     }
     int e;
     if ((e = upload(jobs, r->fs_jobs[lv]))) return e;
@@ -1325,10 +1362,10 @@ int build_static_jobs(rv_replay *r) {
     const uint32_t lambda2 = (uint32_t)(me_lambda * 256.0 / 4.0 * 0.125);
     const uint32_t lambda1 = (uint32_t)(me_lambda * 256.0 * 0.5);
     const int nsb = g.nsb;
-    std::vector<rv_ds_job> jh((size_t)nsb * g.R * 4), jf(nsb * g.R), js(nsb * g.R),
-        jl((size_t)nsb * g.R * 16);
+    std::vector<rv_ds_job> jh((size_t)nsb * r->RA * 4), jf(nsb * r->RA), js(nsb * r->RA),
+        jl((size_t)nsb * r->RA * 16);
     std::vector<int32_t> sh(jh.size() * 8, -1), sf(jf.size() * 8, -1), sl(jl.size() * 8, -1);
-    for (int k = 0; k < g.R; k++)
+    for (int k = 0; k < r->RA; k++)
       for (int sb = 0; sb < nsb; sb++) {
         const int i = k * nsb + sb;
         const int sx = sb % g.tw, sy = sb / g.tw;
@@ -1645,6 +1682,40 @@ void frame_info(long n, int R, rv_replay_frame_info *f) {
   f->compound = R == 2 && (j == 1 || j == 3);
 }
 
+// The lookahead's references of coded frame m >= 1: rav1e's distinct DPB
+// slots of fi.ref_frames (compute_block_importances' unique_indices,
+// src/api/internal.rs:875-882); compute_lookahead_motion_vectors searches
+// each slot once (build_coarse_pmvs / build_full_res_pmvs loop over
+// ALL_INTER_REFS, src/encoder.rs:2732-2738, 3037-3040).  k < R are the
+// encode's references (k = 0: LAST, the backward reference; k = 1: LAST2 at
+// level 0, ALTREF -- the forward reference -- above); with R = 2 a frame
+// above level 0 adds k = 2, LAST3: its own slot, which holds the previous
+// frame of its level, or the key frame, which fills every slot
+// (src/encoder.rs:658, 772-828).  order: the propagation's reference order
+// (mv index order: LAST, LAST2 / LAST3, ALTREF).  oracle/orc_replay.c
+// la_refs_of is the same table; tests/test_importance_window.py derives it
+// from rav1e's slot logic.
+LaRefs la_refs_of(long m, int R) {
+  LaRefs l;
+  memset(&l, 0, sizeof(l));
+  rv_replay_frame_info f;
+  frame_info(m, R, &f);
+  for (int k = 0; k < R; k++) {
+    l.disp[k] = f.ref_display[k];
+    l.order[k] = k;
+  }
+  l.n = R;
+  const long g = (m - 1) / 4, j = (m - 1) % 4;
+  if (R == 2 && j > 0) {
+    const long d3 = j == 1 ? 4 * g - 2 : j == 2 ? 4 * g - 1 : 4 * g + 1;
+    l.disp[2] = (int)(d3 < 0 ? 0 : d3);
+    l.n = 3;
+    l.order[1] = 2;
+    l.order[2] = 1;
+  }
+  return l;
+}
+
 }  // namespace
 
 #define RV_R(expr)                  \
@@ -1819,6 +1890,8 @@ void rv_replay_destroy(rv_replay *r) {
   for (int f = 0; f < rv_replay::kRing; f++)
     for (int i = 0; i < rv_replay::kEv; i++)
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
+  for (hipEvent_t ev : r->kp_ev)
+    if (ev) (void)hipEventDestroy(ev);
   if (r->ev_fork) (void)hipEventDestroy(r->ev_fork);
   if (r->ev_join) (void)hipEventDestroy(r->ev_join);
   if (r->ev_ielig) (void)hipEventDestroy(r->ev_ielig);
@@ -1882,6 +1955,7 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
   g.vis_h = (g.H - g.ty0 * kSb) < g.th * kSb ? g.H - g.ty0 * kSb : g.th * kSb;
   g.nsb = g.tw * g.th;
   g.R = cfg->n_refs;
+  r->RA = g.R == 2 ? kImpMaxRefs : g.R;
   g.M = kCandModes;
   g.C = g.R * g.M + (g.R == 2 ? kCompModes : 0);  // the most a frame evaluates
   g.cw = kSb >> g.xdec;
@@ -2542,15 +2616,16 @@ extern "C" {
 // and the 16x16 blocks left of and above it, so it settles 4 tws + 4 ths - 2
 // rounds later.  e: the frame's timing events (null: untimed).
 static int lookahead_frame(rv_replay *r, RoundRing &rr, hipStream_t xs,
-                           const rv_replay_frame_info &fi, long frame, const LaOut &o,
-                           int32_t *la_list, bool pyramid, long *nrounds, long *nre, hipEvent_t *e) {
+                           const rv_replay_frame_info &fi, const LaRefs &lr, long frame,
+                           const LaOut &o, int32_t *la_list, bool pyramid, long *nrounds,
+                           long *nre, hipEvent_t *e) {
   const Geo &g = r->g;
-  const int lv = fi.level, nr = g.nsb;
+  const int lv = fi.level, nr = g.nsb, RL = lr.n;
   const RvInput &cur = r->inputs[fi.display % r->inputs.size()];
-  rv_plane refs_h[RV_MAX_REFS], refs_q[RV_MAX_REFS], refs_o[RV_MAX_REFS];
-  const uint32_t *box[RV_MAX_REFS];
-  for (int k = 0; k < g.R; k++) {
-    const RvInput &ri = r->inputs[fi.ref_display[k] % r->inputs.size()];
+  rv_plane refs_h[kImpMaxRefs], refs_q[kImpMaxRefs], refs_o[kImpMaxRefs];
+  const uint32_t *box[kImpMaxRefs];
+  for (int k = 0; k < RL; k++) {
+    const RvInput &ri = r->inputs[lr.disp[k] % r->inputs.size()];
     refs_h[k] = ri.hres;
     refs_q[k] = ri.qres;
     refs_o[k] = ri.y;  // the lookahead searches the references' original frames
@@ -2566,7 +2641,7 @@ static int lookahead_frame(rv_replay *r, RoundRing &rr, hipStream_t xs,
   }
   RV_R(ev(1));
   // F1 coarse full search (build_coarse_pmvs), every reference in one launch
-  RV_R(rv_full_search_multi(&cur.qres, refs_q, g.R, r->fs_jobs[lv], nr, 16, 16, 1, 0, o.coarse,
+  RV_R(rv_full_search_multi(&cur.qres, refs_q, RL, r->fs_jobs[lv], nr, 16, 16, 1, 0, o.coarse,
                             nullptr, r->sea ? box : nullptr, xs));
   RV_R(ev(2));
   LaArgs la_a;
@@ -2579,7 +2654,8 @@ static int lookahead_frame(rv_replay *r, RoundRing &rr, hipStream_t xs,
   la_a.coarse = o.coarse;
   la_a.half_l = o.half_l;
   la_a.look = o.look;
-  const int nh = nr * g.R * 4, nl = nr * g.R * 16;
+  const int nh = nr * RL * 4, nl = nr * RL * 16;
+  la_a.nref = RL;
   la_a.list_h = la_list;
   la_a.list_l = la_list + nh;
   auto la_launch = [&](int what, uint32_t q, bool init) -> int {
@@ -2592,12 +2668,12 @@ static int lookahead_frame(rv_replay *r, RoundRing &rr, hipStream_t xs,
     return RV_OK;
   };
   auto f2l = [&](const int32_t *list, const int32_t *cnt) {
-    return rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half_l[lv], nr * 4, 16, 16, 0,
+    return rv_diamond_search_multi(&cur.hres, refs_h, RL, r->jobs_half_l[lv], nr * 4, 16, 16, 0,
                                    0, 0, g.bd, o.half_l, nullptr, nullptr, xs, nullptr, list, cnt,
                                    0);
   };
   auto fl = [&](const int32_t *list, const int32_t *cnt) {
-    return rv_diamond_search_multi(&cur.y, refs_o, g.R, r->jobs_look[lv], nr * 16, 16, 16, 0, 0, 0,
+    return rv_diamond_search_multi(&cur.y, refs_o, RL, r->jobs_look[lv], nr * 16, 16, 16, 0, 0, 0,
                                    g.bd, o.look, nullptr, nullptr, xs, nullptr, list, cnt, 0);
   };
   RV_R(la_launch(1, 0, true));
@@ -2637,11 +2713,12 @@ static int la_step(rv_replay *r, long m) {
   if (m - E.RW >= 1) RV_H(hipStreamWaitEvent(xs, e.ev_used, 0));  // frame m - RW is done with it
   rv_replay_frame_info fi;
   frame_info(m, g.R, &fi);
-  // the pyramids of the frame's and its references' inputs
-  long ds[1 + RV_MAX_REFS];
+  const LaRefs lr = la_refs_of(m, g.R);
+  // the pyramids of the frame's and its lookahead references' inputs
+  long ds[1 + kImpMaxRefs];
   int nd = 0;
   ds[nd++] = fi.display;
-  for (int k = 0; k < g.R; k++) ds[nd++] = fi.ref_display[k];
+  for (int k = 0; k < lr.n; k++) ds[nd++] = lr.disp[k];
   for (int i = 0; i < nd; i++) {
     const size_t idx = (size_t)(ds[i] % (long)r->inputs.size());
     if (E.pyr_display[idx] == ds[i]) continue;
@@ -2650,7 +2727,7 @@ static int la_step(rv_replay *r, long m) {
     if (r->sea) RV_R(rv_plane_box_sums(&in.qres, in.qres_box, xs));
     E.pyr_display[idx] = ds[i];
   }
-  const size_t nr = (size_t)g.nsb * g.R;
+  const size_t nr = (size_t)g.nsb * lr.n;
   if (m > 1) {  // the field's first guess: the previous frame's lookahead
     const RvLaEngine::Entry &p = E.at(m - 1);
     RV_H(hipMemcpyAsync(e.o.half_l, p.o.half_l, nr * 4 * sizeof(rv_fs_result),
@@ -2659,7 +2736,7 @@ static int la_step(rv_replay *r, long m) {
                         hipMemcpyDeviceToDevice, xs));
   }
   long la_rounds = 0, la_reeval = 0;
-  RV_R(lookahead_frame(r, E.rr, xs, fi, m - 1, e.o, E.la_list, false, &la_rounds, &la_reeval,
+  RV_R(lookahead_frame(r, E.rr, xs, fi, lr, m - 1, e.o, E.la_list, false, &la_rounds, &la_reeval,
                        nullptr));
   {
     std::lock_guard<std::mutex> lk(E.mu);
@@ -2667,12 +2744,13 @@ static int la_step(rv_replay *r, long m) {
     E.la_reeval += la_reeval;
     E.la_frames++;
   }
-  rv_plane refs_o[RV_MAX_REFS];
-  for (int k = 0; k < g.R; k++) refs_o[k] = r->inputs[fi.ref_display[k] % r->inputs.size()].y;
-  RV_R(impwin_frame_data(r->inputs[fi.display % r->inputs.size()].y, refs_o, g.R, g.bd, e.o.look,
+  rv_plane refs_o[kImpMaxRefs];
+  for (int k = 0; k < lr.n; k++) refs_o[k] = r->inputs[lr.disp[k] % r->inputs.size()].y;
+  RV_R(impwin_frame_data(r->inputs[fi.display % r->inputs.size()].y, refs_o, lr.n, g.bd, e.o.look,
                          g.tw, g.nsb, g.w_imp, g.h_imp, e.f, E.scratch, E.scratch_bytes, xs));
   e.m = m;
   e.fi = fi;
+  e.lr = lr;
   const long last_frame = E.limit > 0 ? E.limit - 1 : -1;
   const size_t ni = (size_t)g.w_imp * g.h_imp;
   while (E.imp_next <= m && (E.imp_next + E.W <= m || m == last_frame)) {
@@ -2684,23 +2762,24 @@ static int la_step(rv_replay *r, long m) {
     }
     for (long s2 = last; s2 > n; s2--) {
       const RvLaEngine::Entry &es = E.at(s2);
-      int uk[RV_MAX_REFS], nu = 0;
-      for (int k = 0; k < g.R; k++) {
-        bool dup = false;
-        for (int j = 0; j < nu; j++) dup |= es.fi.ref_display[uk[j]] == es.fi.ref_display[k];
-        if (!dup) uk[nu++] = k;
-      }
-      // the frame's passes into its distinct references in the window: one launch
-      int ks[RV_MAX_REFS], np = 0;
-      float *dst[RV_MAX_REFS];
+      // the frame's passes into its reference slots in the window (mv index
+      // order; the split is over every slot, :886-942), one launch: within
+      // the window they land on distinct frames (only the key frame, before
+      // every window, can fill two slots)
+      const int nu = es.lr.n;
+      int ks[kImpMaxRefs], np = 0;
+      float *dst[kImpMaxRefs];
       for (int j = 0; j < nu; j++) {
-        const long t = coded_of_display(es.fi.ref_display[uk[j]]);
+        const int k = es.lr.order[j];
+        const long t = coded_of_display(es.lr.disp[k]);
         if (t < n) continue;  // before the window: gone (:944-948)
-        ks[np] = uk[j];
+        for (int i = 0; i < np; i++)
+          if (dst[i] == E.at(t).f.imp)
+            return rv_set_error(RV_EINVAL, "la_step: two passes into one frame");
+        ks[np] = k;
         dst[np++] = E.at(t).f.imp;
       }
-      for (int i = 0; i < np; i += 2)
-        RV_R(impwin_pass(es.f, ks + i, dst + i, np - i < 2 ? np - i : 2, nu, g.w_imp, g.h_imp, xs));
+      if (np) RV_R(impwin_pass(es.f, ks, dst, np, nu, g.w_imp, g.h_imp, xs));
     }
     RV_R(impwin_final(E.at(n).f, g.w_imp, g.h_imp, xs));
     RV_H(hipEventRecord(E.at(n).ev_imp, xs));
@@ -2781,11 +2860,21 @@ static void la_engine_destroy(rv_replay *r) {
 // (rv_replay_set_inputs_ready below lets the engine run further ahead.)
 static int la_engine_take(rv_replay *r, long n, hipStream_t st, const float **imp) {
   RvLaEngine &E = *r->eng;
+  // the engine never computes a frame at or past the stream's limit
+  if (E.limit > 0 && n >= E.limit)
+    return rv_set_error(RV_EINVAL, "rv_replay_frame: past the stream's limit "
+                                   "(rv_replay_set_imp_window)");
   {
     std::unique_lock<std::mutex> lk(E.mu);
     if (n > E.requested) E.requested = n;
     E.cv.notify_all();
-    E.cv.wait(lk, [&] { return E.err != 0 || E.imp_ready >= n; });
+    // Bounded: an engine frame takes milliseconds.  It never arrives when a
+    // frame RW or more back was skipped (rv_replay_seek) and never coded:
+    // the engine then waits for that frame's entry to be released.
+    if (!E.cv.wait_for(lk, std::chrono::seconds(kEngineWaitS),
+                       [&] { return E.err != 0 || E.imp_ready >= n; }))
+      return rv_set_error(RV_EHIP, "rv_replay_frame: the lookahead engine did not deliver the "
+                                   "frame's importances (a frame skipped and never coded?)");
     if (E.err) return rv_set_error(E.err, E.msg.c_str());
   }
   const RvLaEngine::Entry &e = E.at(n);
@@ -2867,7 +2956,7 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
   const bool lazy = !(lze && lze[0] == '0');
   bool ok = hipGetDevice(&E->dev) == hipSuccess &&
             (lazy || la_stream_create(E) == RV_OK) && round_ring_alloc(r, E->rr, r->stream);
-  const int ni = g.w_imp * g.h_imp, nr = g.nsb * g.R;
+  const int ni = g.w_imp * g.h_imp, nr = g.nsb * r->RA;  // the lookahead's references
   E->la_list = ok ? (int32_t *)dalloc(r, (size_t)nr * 20 * 4) : nullptr;
   E->scratch_bytes = impwin_scratch_bytes(ni);
   E->scratch = ok ? dalloc(r, E->scratch_bytes) : nullptr;
@@ -2876,7 +2965,7 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
   const size_t ob = ((size_t)nr * 21 * sizeof(rv_fs_result) + 255) / 256 * 256;
   for (auto &en : E->ring) {
     if (!ok) break;
-    uint8_t *m = (uint8_t *)dalloc(r, ob + impwin_frame_bytes(ni, g.R));
+    uint8_t *m = (uint8_t *)dalloc(r, ob + impwin_frame_bytes(ni, r->RA));
     ok = m && hipMemsetAsync(m, 0, ob, r->stream) == hipSuccess &&
          hipEventCreateWithFlags(&en.ev_imp, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&en.ev_used, hipEventDisableTiming) == hipSuccess;
@@ -2884,7 +2973,7 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
     en.o.coarse = (rv_fs_result *)m;
     en.o.half_l = en.o.coarse + nr;
     en.o.look = en.o.half_l + (size_t)nr * 4;
-    impwin_frame_carve(en.f, m + ob, ni, g.R);
+    impwin_frame_carve(en.f, m + ob, ni, r->RA);
   }
   E->pyr_display.assign(r->inputs.size(), -1);
   r->eng = E;
@@ -2991,6 +3080,21 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     if (tm) RV_H(hipEventRecord(e[i], st));        \
   } while (0)
   RV_EV(0);
+  // the kernel probe's brackets around the F3 sub-pel launches (speed 10)
+  const bool kp = tm && r->kprobe && !r->s6;
+  uint32_t *kp_acc = kp ? r->kp_cnt : nullptr;
+  auto kp_open = [&](hipStream_t xs) -> int {
+    if (!kp) return RV_OK;
+    if (r->kp_n - r->kp_done >= rv_replay::kKp) RV_H(kp_harvest(r, r->kp_n - rv_replay::kKp + 1));
+    RV_H(hipEventRecord(r->kp_ev[2 * (size_t)(r->kp_n % rv_replay::kKp)], xs));
+    return RV_OK;
+  };
+  auto kp_close = [&](hipStream_t xs) -> int {
+    if (!kp) return RV_OK;
+    RV_H(hipEventRecord(r->kp_ev[2 * (size_t)(r->kp_n % rv_replay::kKp) + 1], xs));
+    r->kp_n++;
+    return RV_OK;
+  };
   // F0 .. FL: the frame's lookahead (lookahead_frame), or with an importance
   // window the engine's, run W frames ahead, and the window's importances
   const float *imp = r->imp;
@@ -3000,7 +3104,11 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       for (int i : {1, 2, 3, rv_replay::kStageEv, rv_replay::kStageEv + 1})
         RV_H(hipEventRecord(e[i], st));
   } else {
-    RV_R(lookahead_frame(r, r->rr, st, fi, ncoded, LaOut{r->coarse, r->half_l, r->look}, r->la_list,
+    LaRefs er;  // without a window: the encode's references only
+    memset(&er, 0, sizeof(er));
+    er.n = g.R;
+    for (int k = 0; k < g.R; k++) er.disp[k] = fi.ref_display[k], er.order[k] = k;
+    RV_R(lookahead_frame(r, r->rr, st, fi, er, ncoded, LaOut{r->coarse, r->half_l, r->look}, r->la_list,
                          true, &r->la_round_sum, &r->la_reeval, tm ? e : nullptr));
     r->la_frames++;
   }
@@ -3354,8 +3462,11 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0, g.bd,
                                  r->full, ev_full, &to_sub, st, act));
     RV_EV(5);
+    RV_R(kp_open(st));
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1,
-                                 r->s6 ? 1 : 0, 0, g.bd, r->sub, ev_sub, nullptr, st, act));
+                                 r->s6 ? 1 : 0, 0, g.bd, r->sub, ev_sub, nullptr, st, act, nullptr,
+                                 nullptr, 1, nullptr, 0, kp_acc));
+    RV_R(kp_close(st));
     if (r->lvl && !edge && !lv_early) RV_R(lv_me(st));
     // the valid candidates (a few microseconds; bracketed with F3 sub-pel;
     // the count was zeroed by the previous argmin or at creation)
@@ -3429,9 +3540,11 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                    g.bd, r->full, nullptr, &to_sub, xs, nullptr, r->mv_list, acnt,
                                    1, ma.f3dirty, lg));
     }
+    RV_R(kp_open(xs));
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
                                  r->sub, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 1,
-                                 ma.f3dirty, lg));
+                                 ma.f3dirty, lg, kp_acc));
+    RV_R(kp_close(xs));
     round_lists_kernel<<<kRoundGrid, 256, 0, xs>>>(
         cg, r->sub, nsingle, r->cand_list, r->cand_count, r->mv_list, acnt,
         CandKeys{r->cand_key, (uint32_t)(r->coded + 1), r->cand_reuse ? 1 : 0});
@@ -3886,6 +3999,45 @@ int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap) {
 int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out, int cap) {
   return stage_times(r, ms_out, cap, last_frames);
 }
+
+// The kernel probe: on (re)start, the sums so far are dropped (the pairs in
+// flight are waited for); off stops recording.
+int rv_replay_set_kernel_probe(rv_replay *r, int on) {
+  if (!r) return rv_set_error(RV_EINVAL, "rv_replay_set_kernel_probe: null");
+  if (on && r->kp_ev.empty()) {
+    r->kp_ev.assign(2 * rv_replay::kKp, nullptr);
+    for (auto &ev : r->kp_ev) RV_H(hipEventCreate(&ev));
+    r->kp_cnt = (uint32_t *)dalloc(r, 2 * sizeof(uint32_t));
+    if (!r->kp_cnt) return rv_set_error(RV_EHIP, "rv_replay_set_kernel_probe: allocation failed");
+  }
+  if (!r->kp_ev.empty()) {
+    RV_H(kp_harvest(r, r->kp_n));
+    RV_H(hipDeviceSynchronize());
+    RV_H(hipMemset(r->kp_cnt, 0, 2 * sizeof(uint32_t)));
+    RV_H(hipDeviceSynchronize());
+  }
+  r->kp_ms = 0.0;
+  r->kp_base = r->kp_n;
+  r->kprobe = on != 0;
+  return RV_OK;
+}
+
+// out[0] launches, [1] their summed milliseconds (event pairs on their
+// streams), [2] candidate evaluations, [3] jobs, since the probe started
+int rv_replay_kernel_probe(rv_replay *r, double *out, int cap) {
+  if (!r || !out || cap < 4) return rv_set_error(RV_EINVAL, "rv_replay_kernel_probe: null / cap");
+  for (int i = 0; i < 4; i++) out[i] = 0.0;
+  if (r->kp_ev.empty()) return 4;
+  RV_H(kp_harvest(r, r->kp_n));
+  uint32_t c[2] = {0, 0};
+  RV_H(hipDeviceSynchronize());
+  RV_H(hipMemcpy(c, r->kp_cnt, sizeof(c), hipMemcpyDeviceToHost));
+  out[0] = (double)(r->kp_n - r->kp_base);
+  out[1] = r->kp_ms;
+  out[2] = (double)c[0];
+  out[3] = (double)c[1];
+  return 4;
+}
 // Candidate evaluations summed over the last min(frames, 64) coded frames:
 // out[0] F3 full-pel diamond, out[1] F3 sub-pel diamond (64x64 jobs), out[2]
 // frames summed, (cap >= 5) out[3] / out[4] the F4 single-reference /
@@ -3950,6 +4102,41 @@ int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
   // the encode: up to W frames past the last coded one)
   out[20] = (uint64_t)(r->la_frames + ef);
   return 21;
+}
+
+// Host-only test hook: the slots RoundRing gives check q -- out[0] the
+// device count slot it counts into, out[1] the slot it zeroes for check
+// q + 1, out[2] its host publication slot -- and out[3] kRoundsAhead,
+// out[4] kCnt, out[5] kPub (cap >= 6).  Returns 6.
+int rv_round_ring_slots(uint32_t q, int32_t *out, int cap) {
+  if (!out || cap < 6) return rv_set_error(RV_EINVAL, "rv_round_ring_slots: cap");
+  static int32_t cnt[2 * RoundRing::kCnt + 1];
+  static unsigned long long pub[RoundRing::kPub];
+  RoundRing rr;
+  rr.cnt = cnt;
+  rr.d_pub = pub;
+  const RoundPub p = rr.pub(q);
+  out[0] = (int32_t)((p.cnt - cnt) / 2);
+  out[1] = (int32_t)((p.next - cnt) / 2);
+  out[2] = (int32_t)(p.host - pub);
+  out[3] = rv_replay::kRoundsAhead;
+  out[4] = RoundRing::kCnt;
+  out[5] = RoundRing::kPub;
+  return 6;
+}
+
+// Host-only test hook: the lookahead references of coded frame m >= 1
+// (la_refs_of): out[0] = n, out[1..3] their displays in k order, out[4..6]
+// the propagation order (-1: unused).  Returns 0.
+int rv_replay_la_refs(long m, int R, int32_t *out) {
+  if (!out || m < 1 || R < 1 || R > 2) return rv_set_error(RV_EINVAL, "rv_replay_la_refs");
+  const LaRefs l = la_refs_of(m, R);
+  out[0] = l.n;
+  for (int k = 0; k < 3; k++) {
+    out[1 + k] = k < l.n ? l.disp[k] : -1;
+    out[4 + k] = k < l.n ? l.order[k] : -1;
+  }
+  return RV_OK;
 }
 
 // ---- RCCL communicator for the tile-group exchange ---------------------------

@@ -424,6 +424,19 @@ class HipReplay:
             _check(n, "rv_replay_stage_times_sum")
         return out  # stages past n (F8 without RV_REPLAY_ENTROPY) stay 0
 
+    def set_kernel_probe(self, on: bool = True):
+        """(Re)start the F3 sub-pel kernel probe (rv_replay_set_kernel_probe)."""
+        _check(lib().rv_replay_set_kernel_probe(self.h, 1 if on else 0),
+               "rv_replay_set_kernel_probe")
+
+    def kernel_probe(self) -> np.ndarray:
+        """[launches, summed ms, candidate evaluations, jobs] of the probed
+        F3 sub-pel launches since the probe started."""
+        out = np.zeros(4, np.float64)
+        _check(lib().rv_replay_kernel_probe(self.h, out.ctypes.data, 4) - 4,
+               "rv_replay_kernel_probe")
+        return out
+
     def counters(self) -> np.ndarray:
         """[F3 full-pel evals, F3 sub-pel evals, frames, F4 single-reference
         candidates, F4 compound candidates of the 64x64 blocks, then (speed
@@ -668,8 +681,9 @@ class PipelinedReplay:
         self.R = primary.cfg.n_refs
         self.n = 0
         self.err = None
-        self.ev = [lib().rv_event_create() for _ in range(64)]
+        self.ev = [lib().rv_event_create() for _ in range(self.EV_RING)]
         self.done = {}  # coded frame -> threading.Event (its event is recorded)
+        self.issued = {}  # coded frame -> threading.Event (its stream waits are queued)
         self.lock = threading.Lock()
         self.held = None  # a 4g+1 frame waiting for the next level-0 frame
         self.qs = [queue.Queue() for _ in self.inst]
@@ -677,6 +691,11 @@ class PipelinedReplay:
                         for i in range(self.k)]
         for w in self.workers:
             w.start()
+
+    # device events, one per coded frame in flight: frame n records
+    # ev[n % EV_RING]; a frame waits for frames at most DEP_SPAN back
+    EV_RING = 64
+    DEP_SPAN = 20
 
     def instance_of(self, n: int) -> int:
         if n == 0:
@@ -689,11 +708,29 @@ class PipelinedReplay:
     def on_primary(self, f: int) -> bool:
         return self.instance_of(f + 1) == 0
 
-    def _flag(self, n):
+    def _flag(self, n, d=None):
+        d = self.done if d is None else d
         with self.lock:
-            if n not in self.done:
-                self.done[n] = __import__("threading").Event()
-            return self.done[n]
+            if n not in d:
+                d[n] = __import__("threading").Event()
+            return d[n]
+
+    def _before_record(self, n):
+        """Frame n is about to re-record ev[n % EV_RING], the event of frame
+        n - EV_RING: every frame that waits on that one must have queued its
+        stream wait first (they are all within DEP_SPAN of it, far behind n,
+        so this never blocks in practice; it enforces the ring's bound).
+        Then flags of frames no later frame can wait on are dropped."""
+        old = n - self.EV_RING
+        if old < 0:
+            return
+        for k in range(old + 1, min(n, old + self.DEP_SPAN + 1)):
+            if old in self._deps(k):
+                self._flag(k, self.issued).wait()
+        with self.lock:
+            for d in (self.done, self.issued):
+                for k in [k for k in d if k <= old and d[k].is_set()]:
+                    del d[k]
 
     def _deps(self, n: int) -> list:
         """Coded frames on other instances that frame n waits for."""
@@ -735,17 +772,23 @@ class PipelinedReplay:
                 return
             try:
                 if self.err is None:
-                    for k in self._deps(n):
+                    deps = self._deps(n)
+                    assert all(n - k <= self.DEP_SPAN for k in deps), (n, deps)
+                    for k in deps:
                         self._flag(k).wait()
-                        _check(lib().rv_stream_wait_event(inst.stream, self.ev[k % 64]),
+                        _check(lib().rv_stream_wait_event(inst.stream, self.ev[k % self.EV_RING]),
                                "rv_stream_wait_event")
+                    self._flag(n, self.issued).set()
                     if n:
                         inst.seek(n)
                     inst.frame()
-                    _check(lib().rv_event_record(self.ev[n % 64], inst.stream), "rv_event_record")
+                    self._before_record(n)
+                    _check(lib().rv_event_record(self.ev[n % self.EV_RING], inst.stream),
+                           "rv_event_record")
             except Exception as e:  # handed to the main thread by drain()
                 self.err = e
             finally:
+                self._flag(n, self.issued).set()
                 self._flag(n).set()
                 self.qs[i].task_done()
 
@@ -782,6 +825,15 @@ class PipelinedReplay:
         out = sum(cs[1:], cs[0].copy())
         out[2] = max(c[2] for c in cs)
         return out
+
+    def set_kernel_probe(self, on: bool = True):
+        self.drain()
+        for t in self.inst:
+            t.set_kernel_probe(on)
+
+    def kernel_probe(self) -> np.ndarray:
+        self.drain()
+        return sum((t.kernel_probe() for t in self.inst), np.zeros(4))
 
     def stage_ms_sum_frames(self, frames) -> tuple:
         """Stage times summed over the instrumented inter frames `frames`

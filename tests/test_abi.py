@@ -97,3 +97,32 @@ def test_no_device_here_fails_loudly():
         pytest.skip("a device is visible")
     with pytest.raises(R.Rav1eHipError):
         R.require_device(0)
+
+
+def test_round_ring_slots_keep_live_checks_apart():
+    """The MV-stack / lookahead round loop (rv_replay.hip run_rounds) keeps
+    kRoundsAhead rounds queued beyond the last published count it read, so
+    up to kRoundsAhead + 2 checks are in flight at once.  Their device count
+    slots, the slot each zeroes for its successor and their host
+    publication slots must stay apart (round 4 published every check into
+    one host slot and a count could be read for the wrong check; the slot
+    layout is RoundRing's own code, through rv_round_ring_slots)."""
+    L = R.lib()
+    out = (C.c_int32 * 6)()
+    slots = []
+    for q in range(0, 3 * 256):
+        assert L.rv_round_ring_slots(q, out, 6) == 6
+        slots.append(tuple(out[:3]))
+    ahead, kcnt, kpub = out[3], out[4], out[5]
+    live = ahead + 2
+    assert live < min(kcnt, kpub)
+    for q in range(len(slots) - live):
+        cnt, nxt, pub = slots[q]
+        assert nxt == slots[q + 1][0]  # check q zeroes check q + 1's slot
+        assert nxt != cnt
+        for k in range(1, live):
+            assert slots[q + k][0] != cnt, (q, k)  # no later live check counts into q's slot
+            assert slots[q + k][1] != cnt, (q, k)  # ... or zeroes it
+            assert slots[q + k][2] != pub, (q, k)  # ... or publishes over q's count
+    # the ring wraps (the sequence number is u32): q and q + kPub share a slot
+    assert slots[0][2] == slots[kpub][2]

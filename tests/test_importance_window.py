@@ -66,6 +66,78 @@ def test_log2f_restatement_matches_host():
     assert L.orc_log2f_mismatches(1, 0x7F800000, 251) == 0
 
 
+def _pos_to_lvl(pos, depth=2):
+    """src/encoder.rs:555-564"""
+    v = pos | (1 << depth)
+    return depth - ((v & -v).bit_length() - 1)
+
+
+def rav1e_propagation_refs(n_coded):
+    """Per coded frame m >= 1: the displays compute_block_importances
+    propagates frame m's importance into, in its order -- unique_indices:
+    fi.ref_frames de-duplicated by DPB slot, in mv index order
+    (src/api/internal.rs:875-882) -- derived from rav1e's own tables, not
+    the replay's: InterConfig with reorder, multiref, pyramid_depth 2,
+    group_input_len 4 (:40-95), a group's output order idx_in_group_output
+    0..5 with get_level / get_show_existing_frame / get_order_hint /
+    get_slot_idx (:104-166), FrameInvariants::new_inter_frame's ref_frames
+    (src/encoder.rs:761-828: level 0 LAST = the previous P slot, LAST2 the
+    one before; level > 0 all = the backward slot, ALTREF the forward one,
+    LAST3 its own slot), and the key frame filling every slot
+    (refresh_frame_flags ALL_REF_FRAMES_MASK, :658).  Slot contents follow
+    refresh_frame_flags in coding order (SEF frames refresh nothing)."""
+    depth, gil = 2, 4
+    slots = [0] * 8  # the display each DPB slot holds after the key frame
+    out, m, g = {}, 0, 0
+    while m < n_coded - 1:
+        for idx in range(6):
+            if idx >= depth and bin(idx - depth + 1).count("1") == 1 and idx != depth:
+                continue  # show_existing_frame
+            level = idx if idx < depth else _pos_to_lvl(idx - depth + 1, depth)
+            offset = gil >> idx if idx < depth else idx - depth + 1
+            oh = gil * g + offset
+
+            def slot_of(o):
+                lv = _pos_to_lvl(o, depth)
+                return (o >> depth) % 4 if lv == 0 else 3 + lv
+            slot_idx = (oh >> depth) & 3 if level == 0 else 3 + level
+            if level == 0:
+                rf = [(slot_idx + 4 - 1) % 4] * 7
+                rf[1] = (slot_idx + 4 - 2) % 4  # LAST2: second_ref_frame at idx 0
+            else:
+                rf = [slot_of(oh - (gil >> level))] * 7
+                rf[6] = slot_of(oh + (gil >> level))  # ALTREF
+                rf[2] = slot_idx  # LAST3: ref_in_previous_group
+            uniq = []
+            for sl in rf:
+                if sl not in uniq:
+                    uniq.append(sl)
+            m += 1
+            out[m] = (oh, [slots[sl] for sl in uniq])
+            slots[slot_idx] = oh
+        g += 1
+    return out
+
+
+def test_lookahead_references_follow_rav1e_slots():
+    """The oracle's and the GPU library's lookahead references (the slots the
+    propagation splits over) equal rav1e's, frame by frame over 10 GOPs."""
+    import rav1e_amd as R
+    L = O.lib()
+    L.orc_replay_la_refs.argtypes = [C.c_long, C.c_int, C.c_void_p]
+    want = rav1e_propagation_refs(41)
+    for m, (disp, refs) in want.items():
+        assert RP.frame_info(m)["display"] == disp
+        for name, fn in (("oracle", L.orc_replay_la_refs), ("hip", R.lib().rv_replay_la_refs)):
+            out = np.zeros(7, np.int32)
+            assert fn(m, 2, out.ctypes.data) == 0
+            n = int(out[0])
+            got = [int(out[1 + int(out[4 + i])]) for i in range(n)]
+            assert got == refs, (name, m, disp, got, refs)
+    # the first GOP: two slots holding the key frame count twice
+    assert want[1][1] == [0, 0] and want[2][1] == [0, 0, 4] and want[3][1] == [0, 0, 2]
+
+
 def test_oracle_importance_window_vs_numpy():
     w, h, n, W = 256, 192, 9, 4
     refs = 2
@@ -77,6 +149,7 @@ def test_oracle_importance_window_vs_numpy():
     L = c.L
     L.orc_replay_la_data.argtypes = [C.c_void_p, C.c_long] + [C.c_void_p] * 4
     hi, wi = c.imp_shape
+    rv_refs = rav1e_propagation_refs(n)
     c.frame()  # the key frame
     checked = nonzero = 0
     for coded in range(1, n):
@@ -86,24 +159,24 @@ def test_oracle_importance_window_vs_numpy():
         data = {}
         for m in range(coded, last + 1):
             intra = np.zeros((hi, wi), np.uint32)
-            mv8 = np.zeros((refs, hi, wi, 2), np.int16)
-            inter = np.zeros((refs, hi, wi), np.uint32)
-            rd = np.zeros(2, np.int32)
+            mv8 = np.zeros((3, hi, wi, 2), np.int16)
+            inter = np.zeros((3, hi, wi), np.uint32)
+            rd = np.zeros(7, np.int32)
             assert L.orc_replay_la_data(c.h, m, intra.ctypes.data, mv8.ctypes.data,
                                         inter.ctypes.data, rd.ctypes.data) == 0, (coded, m)
-            data[m] = (intra, mv8, inter, list(rd[:refs]))
+            nr = int(rd[0])
+            order = [int(rd[4 + i]) for i in range(nr)]
+            # the oracle's lookahead references, in propagation order, are rav1e's
+            assert [int(rd[1 + k]) for k in order] == rv_refs[m][1], (m, rd)
+            data[m] = (intra, mv8, inter, [int(rd[1 + k]) for k in range(nr)], order)
         imp = {m: np.zeros((hi, wi), np.float32) for m in data}
         for m in range(last, coded, -1):
-            intra, mv8, inter, rd = data[m]
-            uniq = []
-            for k, d in enumerate(rd):
-                if d not in [rd[j] for j in uniq]:
-                    uniq.append(k)
-            for k in uniq:
+            intra, mv8, inter, rd, order = data[m]
+            for k in order:
                 t = coded_of_display(rd[k])
                 if t < coded:
                     continue
-                _propagate(mv8[k], inter[k], intra, imp[m], len(uniq), imp[t])
+                _propagate(mv8[k], inter[k], intra, imp[m], len(order), imp[t])
         ic = data[coded][0].astype(np.float32)
         want = np.zeros((hi, wi), np.float32)
         nz = ic > 0
@@ -113,9 +186,11 @@ def test_oracle_importance_window_vs_numpy():
         want[nz] = [L.orc_log2f(float(a)) for a in arg]
         np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32),
                                       err_msg="coded frame %d" % coded)
-        nonzero += bool((got > 0).any())  # level-2 frames are not referenced: zero
+        nonzero += bool((got > 0).any())
         checked += 1
-    assert checked == n - 1 and nonzero >= (n - 1) // 2
+    # level-2 frames are LAST3 of the next level-2 frame: only the window's
+    # last frames (nothing after them yet) stay zero
+    assert checked == n - 1 and nonzero >= n - 3
 
 
 def test_importance_window_changes_the_decision_inputs_only():
