@@ -52,6 +52,12 @@ CONFIGS = {
 }
 TIMING_STRIDE = 4  # in GOPs
 IMP_WINDOW = 40  # rdo_lookahead_frames default (src/api/config.rs:158)
+_T0 = time.time()
+
+
+def progress(msg):
+    """one line per bench phase on stderr (a long silent run looks hung)"""
+    print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 CPU_FRAMES = 8  # coded frames of the CPU baseline / parity stream with a window
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8.0 TB/s spec
 # VALU issue peaks, G wave64 instructions/s over 256 CUs at 2.4 GHz: the
@@ -187,10 +193,12 @@ def timed_run(engine, group, steps, warmup, sync=None, finish=None, before=None,
     warmup, outside the timing (probes reset); start(): the first thing
     inside the timing (the lookahead engine released)."""
     drain = getattr(engine, "drain", None)  # PairedReplay: frames issued from a second thread
-    for _ in range(warmup):
+    for i in range(warmup):
         engine.frame()
+        progress(f"warmup frame {i} issued")
     if warmup:
         engine.results()  # drains the stream
+    progress(f"warmup: {warmup} frames")
     if before:
         before()
     group.barrier()
@@ -208,6 +216,7 @@ def timed_run(engine, group, steps, warmup, sync=None, finish=None, before=None,
     if finish:
         finish()  # the host's share of the frames (F8's range coder) has finished too
     t1 = time.perf_counter()
+    progress(f"timed: {steps} frames in {t1 - t0:.3f} s")
     group.barrier()
     # the verification checksums are not part of a frame: outside the timing
     words = engine.results()
@@ -246,6 +255,7 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     for i in range(nin):
         c.set_input(i, hip_inputs[i])
     c.frame()  # the key frame (a copy), untimed
+    progress("CPU replay: started")
     cpu_words, cpu_ent = [], []
     n, tc0 = 0, time.perf_counter()
     while n < 4 or (time.perf_counter() - tc0 < args.cpu_seconds and n < nin - 6 and
@@ -256,6 +266,7 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
         if ent:
             cpu_ent.append(c.entropy_stats()[:3])
     tc = time.perf_counter() - tc0
+    progress(f"CPU replay: {n} frames in {tc:.1f} s")
     c.close()
     # 1 thread: the first 1/8 of the superblocks of one GOP
     nsb = ((W + 63) // 64) * ((H + 63) // 64)
@@ -272,6 +283,7 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     t1 = time.perf_counter() - t1
     c1.close()
     fps1 = 4 * (lim / nsb) / t1
+    progress("CPU one-thread sample done")
     cpu = {"value": round(n / tc, 4), "unit": "frames/s", "cores": threads, "kind": "port",
            "isa": isa,
            "cores_note": "the GPU box's per-GPU CPU share (16 threads; the harness sizes worker "
@@ -303,6 +315,7 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
             bad.append({"frame": i, "entropy": "coefficient bytes differ"})
     g.close()
     R._check(R.lib().rv_device_sync(), "rv_device_sync")
+    progress(f"GPU parity pass: {n} frames, {len(bad)} mismatches")
     parity = {"frames": n, "words": int(sum(w.size for w in cpu_words)),
               "bit_exact": not bad, "vs": "oracle/orc_replay.c (CPU replay)",
               **({"importance_window": imp_window, "stream_frames": limit} if imp_window else {})}
@@ -341,6 +354,7 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2):
     nb = bufs[0][2]
     span = [[] for _ in gs]
     imp = [[] for _ in gs]
+    progress(f"emulated ranks: {n} groups")
     for f in range(frames):
         timed = f > gop  # the second GOP on: every me_range_scale once per GOP
         order = range(n - 1, -1, -1) if os.environ.get("RAV1E_BENCH_EMU_REVERSE") else range(n)
@@ -363,6 +377,7 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2):
             sync()
             if timed:
                 imp[k].append((time.perf_counter() - t0) * 1e3)
+    progress("emulated ranks: done")
     cnts = [[int(v) for v in g.counters()] for g in gs]
     for g in gs:
         g.close()
@@ -427,6 +442,9 @@ def main():
                          "coded frames ahead (rav1e's default 40; 0: importance 0, bias 0.65); "
                          "one GPU only (a window needs the whole frame's lookahead)")
     args = ap.parse_args()
+    # a stalled run names where it stalled (every thread's stack on stderr)
+    import faulthandler
+    faulthandler.dump_traceback_later(120, repeat=True, file=sys.stderr)
 
     import rav1e_amd as R  # load the HIP library before anything else
     from rav1e_amd import replay as RP

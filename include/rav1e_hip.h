@@ -692,6 +692,18 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit);
  * src/api/internal.rs:767-820).  At most the instance's n_inputs; no
  * effect without a window.  Results are unchanged. */
 int rv_replay_set_inputs_ready(rv_replay *r, long displays);
+/* Tile groups with an importance window: the propagation reads the whole
+ * frame, so every group's engine computes its own blocks' lookahead part of
+ * each coded frame (intra costs, lookahead MVs, fractions: 28 bytes per 8x8
+ * block) and the parts are all-gathered before the frame's target lists are
+ * built -- over RCCL (comm from rv_comm_create: one rank per group) or, for
+ * several groups in one process, through an in-process hub.  After
+ * rv_replay_set_groups and rv_replay_set_imp_window, before the first frame,
+ * on every group's primary instance (exactly one of comm / hub). */
+typedef struct rv_la_hub rv_la_hub;
+rv_la_hub *rv_la_hub_create(int n_groups);
+void rv_la_hub_destroy(rv_la_hub *hub);
+int rv_replay_set_la_exchange(rv_replay *r, void *comm, rv_la_hub *hub);
 /* The block importances (f32 [h_imp][w_imp]) the last coded frame's RDO
  * used (zero without a window or input). */
 int rv_replay_get_importances(rv_replay *r, float *host, int n);

@@ -116,6 +116,11 @@ typedef struct orc_replay {
    * coded frames ahead (ring la[W + 1]) and every frame's block importances
    * come from compute_block_importances over the window */
   int imp_window, h_imp;
+  /* la_ext: a tile group's window -- the importances need the whole frame's
+   * lookahead, so each group computes its own blocks' part
+   * (orc_replay_la_group) and the caller exchanges the parts
+   * (orc_replay_la_import) before coding; frame() does not run it */
+  int la_ext;
   ola *la;
   long la_next;  /* the next coded frame whose lookahead runs */
   long la_limit; /* coded frames in the stream (0: unbounded) */
@@ -2227,6 +2232,14 @@ static long coded_of_display(long d) {
 
 static ola *la_of(orc_replay *r, long m) { return &r->la[m % (r->imp_window + 1)]; }
 
+/* this group's 8x8 importance blocks [x0, x1) x [y0, y1) */
+static void group_blocks(const orc_replay *r, int *x0, int *y0, int *x1, int *y1) {
+  *x0 = r->tx0 * 8;
+  *y0 = r->ty0 * 8;
+  *x1 = (r->tx0 + r->tw) * 8 < r->w_imp ? (r->tx0 + r->tw) * 8 : r->w_imp;
+  *y1 = (r->ty0 + r->th) * 8 < r->h_imp ? (r->ty0 + r->th) * 8 : r->h_imp;
+}
+
 /* orc_la_refs of coded frame m >= 1 (frame_info's group g, position j) */
 static orc_la_refs la_refs_of(long m, int R) {
   orc_la_refs l;
@@ -2280,28 +2293,123 @@ static void la_compute(orc_replay *r, long m) {
   const int w = r->w_imp, h = r->h_imp, hbd = r->hbd;
   const size_t ni = (size_t)w * h;
   const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
-  for (int y = 0; y < h; y++)
-    for (int x = 0; x < w; x++) {
+  /* the group's 8x8 blocks (the whole frame with one group) */
+  int bx0, by0, bx1, by1;
+  group_blocks(r, &bx0, &by0, &bx1, &by1);
+  for (int y = by0; y < by1; y++)
+    for (int x = bx0; x < bx1; x++) {
       orc_lookahead_intra_costs(at(&cur->y, hbd, x * 8, y * 8), cur->y.stride, 8, 8, hbd, r->bd,
                                 &e->intra[(size_t)y * w + x]);
-      const int sb = (y / 8) * r->tw + x / 8, b = ((y % 8) / 2) * 4 + (x % 8) / 2;
-      for (int k = 0; k < RL; k++)
-        e->mv8[k * ni + (size_t)y * w + x] = r->look[((size_t)k * r->nsb + sb) * 16 + b];
+      const int sb = (y / 8 - r->ty0) * r->tw + x / 8 - r->tx0, b = ((y % 8) / 2) * 4 + (x % 8) / 2;
+      for (int k = 0; k < RL; k++) {
+        const orc_mv mv = r->look[((size_t)k * r->nsb + sb) * 16 + b];
+        e->mv8[k * ni + (size_t)y * w + x] = mv;
+        /* get_satd against the reference block at the MV (:902-931; the
+         * region at (x * 64 + mv.col) / 8, isize `/`), as
+         * orc_importance_inter_costs does for a whole frame */
+        const oplane *ref = &r->inputs[r->lar.disp[k] % r->n_inputs].y;
+        const int64_t px_x = ((int64_t)x * 64 + mv.col) / 8, px_y = ((int64_t)y * 64 + mv.row) / 8;
+        e->inter[k * ni + (size_t)y * w + x] =
+            orc_get_satd(at(&cur->y, hbd, x * 8, y * 8), cur->y.stride,
+                         at(ref, hbd, (int)px_x, (int)px_y), ref->stride, 8, 8, hbd, 0);
+      }
     }
-  for (int k = 0; k < RL; k++) {
-    const oplane *ref = &r->inputs[r->lar.disp[k] % r->n_inputs].y;
-    orc_importance_inter_costs(at(&cur->y, hbd, 0, 0), cur->y.stride, at(ref, hbd, 0, 0),
-                               ref->stride, w, h, hbd, e->mv8 + k * ni, e->inter + k * ni);
-  }
   r->fi = save;
   r->sb_limit = save_lim;
 }
 
-/* the lookahead of every frame up to n + W (n: the frame being coded) */
-static void la_fill(orc_replay *r) {
+/* the last coded frame whose lookahead frame n = r->coded needs: n + W,
+ * or the stream's last frame */
+static long la_last(const orc_replay *r) {
   long last = r->coded + r->imp_window;
   if (r->la_limit > 0 && last > r->la_limit - 1) last = r->la_limit - 1;
+  return last;
+}
+
+/* the lookahead of every frame up to n + W (n: the frame being coded) */
+static void la_fill(orc_replay *r) {
+  const long last = la_last(r);
   for (; r->la_next <= last; r->la_next++) la_compute(r, r->la_next);
+}
+
+/* ---- a tile group's window (la_ext) ------------------------------------------
+ * Each group computes the lookahead of its own superblocks (the searches
+ * are tile-local) and the importance data of its own 8x8 blocks; the
+ * caller all-gathers the groups' parts (the importance propagation reads
+ * the whole frame) and imports them; then frame() propagates over the
+ * whole frame, exactly as a one-group replay does.  A part: per block of
+ * the group's rectangle in raster order, the intra cost, then per
+ * reference slot k < 3 the lookahead MV and the inter cost (28 bytes). */
+#define LA_PART_B 28
+static size_t la_part_bytes(int bw, int bh) { return (size_t)bw * bh * LA_PART_B; }
+
+/* the 8x8 importance blocks [x0, x1) x [y0, y1) of a superblock rectangle */
+static void sb_rect_blocks(const orc_replay *r, int tx0, int ty0, int tw, int th, int *x0, int *y0,
+                           int *x1, int *y1) {
+  *x0 = tx0 * 8;
+  *y0 = ty0 * 8;
+  *x1 = (tx0 + tw) * 8 < r->w_imp ? (tx0 + tw) * 8 : r->w_imp;
+  *y1 = (ty0 + th) * 8 < r->h_imp ? (ty0 + th) * 8 : r->h_imp;
+}
+
+/* (next, last): the next coded frame whose group part is due and the last
+ * one frame() of the next frame needs; out[2] = the part's bytes */
+int orc_replay_la_due(orc_replay *r, long *out) {
+  if (!r->imp_window || !r->la_ext) return -1;
+  int x0, y0, x1, y1;
+  sb_rect_blocks(r, r->tx0, r->ty0, r->tw, r->th, &x0, &y0, &x1, &y1);
+  out[0] = r->la_next;
+  out[1] = la_last(r);
+  out[2] = (long)la_part_bytes(x1 - x0, y1 - y0);
+  return 0;
+}
+
+static void la_pack(const orc_replay *r, const ola *e, int x0, int y0, int x1, int y1,
+                    uint8_t *buf, int unpack, ola *dst) {
+  const size_t ni = (size_t)r->w_imp * r->h_imp;
+  for (int y = y0; y < y1; y++)
+    for (int x = x0; x < x1; x++) {
+      uint8_t *p = buf + ((size_t)(y - y0) * (x1 - x0) + (x - x0)) * LA_PART_B;
+      const size_t i = (size_t)y * r->w_imp + x;
+      if (!unpack) {
+        memset(p, 0, LA_PART_B);
+        memcpy(p, &e->intra[i], 4);
+        for (int k = 0; k < e->lr.n; k++) {
+          memcpy(p + 4 + 8 * k, &e->mv8[k * ni + i], 4);
+          memcpy(p + 8 + 8 * k, &e->inter[k * ni + i], 4);
+        }
+      } else {
+        memcpy(&dst->intra[i], p, 4);
+        for (int k = 0; k < dst->lr.n; k++) {
+          memcpy(&dst->mv8[k * ni + i], p + 4 + 8 * k, 4);
+          memcpy(&dst->inter[k * ni + i], p + 8 + 8 * k, 4);
+        }
+      }
+    }
+}
+
+/* coded frame m's group part (m = the next due): its lookahead, then the
+ * part of this group's blocks into buf (la_due's bytes) */
+int orc_replay_la_group(orc_replay *r, long m, uint8_t *buf) {
+  if (!r->imp_window || !r->la_ext || m != r->la_next) return -1;
+  la_compute(r, m);
+  r->la_next++;
+  int x0, y0, x1, y1;
+  sb_rect_blocks(r, r->tx0, r->ty0, r->tw, r->th, &x0, &y0, &x1, &y1);
+  la_pack(r, la_of(r, m), x0, y0, x1, y1, buf, 0, NULL);
+  return 0;
+}
+
+/* another group's part of coded frame m (its superblock rectangle) */
+int orc_replay_la_import(orc_replay *r, long m, int tx0, int ty0, int tw, int th,
+                         const uint8_t *buf) {
+  if (!r->imp_window || !r->la_ext || m >= r->la_next) return -1;
+  ola *e = la_of(r, m);
+  if (e->coded != m) return -1;
+  int x0, y0, x1, y1;
+  sb_rect_blocks(r, tx0, ty0, tw, th, &x0, &y0, &x1, &y1);
+  la_pack(r, e, x0, y0, x1, y1, (uint8_t *)buf, 1, e);
+  return 0;
 }
 
 /* compute_block_importances for frame n = r->coded: zero the window's
@@ -2341,7 +2449,8 @@ static void importance_frame(orc_replay *r) {
  * the whole frame (a group's importances would need the other groups'). */
 int orc_replay_set_imp_window(orc_replay *r, int window, long limit) {
   if (window < 0 || r->coded > 0) return -1;
-  if (window > 0 && (r->tx0 || r->ty0 || r->vis_w != r->W || r->vis_h != r->H)) return -1;
+  /* a tile group's window needs the other groups' parts (la_ext) */
+  r->la_ext = r->tx0 || r->ty0 || r->vis_w != r->W || r->vis_h != r->H;
   free_la(r);
   free(r->imp_own);
   r->imp_own = NULL;
@@ -2450,7 +2559,10 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
   /* F1; the lookahead (its F2 and 16x16 searches, tile by tile) -- with
    * an importance window, run W frames ahead and kept in the ring */
   if (r->imp_window) {
-    la_fill(r);
+    if (!r->la_ext)
+      la_fill(r);
+    else if (r->la_next <= la_last(r))
+      return -1; /* a group's parts are due first (orc_replay_la_due) */
     const ola *e = la_of(r, r->coded);
     if (e->coded != r->coded) return -1; /* the stream ended before this frame */
     const size_t nr = (size_t)r->R * r->nsb;

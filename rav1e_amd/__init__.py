@@ -303,6 +303,9 @@ def _declare(L):
         "rv_replay_kernel_probe": (i32, [vp, vp, i32]),
         "rv_round_ring_slots": (i32, [C.c_uint32, vp, i32]),
         "rv_replay_la_refs": (i32, [C.c_long, i32, vp]),
+        "rv_la_hub_create": (vp, [i32]),
+        "rv_la_hub_destroy": (None, [vp]),
+        "rv_replay_set_la_exchange": (i32, [vp, vp, vp]),
         "rv_replay_set_timing": (i32, [vp, i32, i32]),
         "rv_diamond_search_batch": (i32, [P, P, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
         "rv_telescopic_subpel_batch": (i32, [P, P, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp]),

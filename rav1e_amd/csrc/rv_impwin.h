@@ -36,15 +36,36 @@ struct ImpFrame {
 
 size_t impwin_frame_bytes(int n, int R);        // one ImpFrame's arrays
 void impwin_frame_carve(ImpFrame &f, void *base, int n, int R);
-size_t impwin_scratch_bytes(int n);             // impwin_frame_data's sort scratch
+size_t impwin_scratch_bytes(int n);             // impwin_lists' scratch
 
-// Frame data of the coded frame whose luma input is `cur`: intra costs, the
-// 8x8 blocks' lookahead MVs from `look` ([R][nsb][16] of a whole-frame
-// superblock grid tw wide), their fractions against each reference's
-// original frame refs[k], and per reference the target lists.
-int impwin_frame_data(const rv_plane &cur, const rv_plane *refs, int R, int bit_depth,
-                      const rv_fs_result *look, int tw, int nsb, int w_imp, int h_imp,
-                      const ImpFrame &f, void *scratch, size_t scratch_bytes, hipStream_t st);
+// A tile group's (tx0, ty0, tw, th superblocks) 8x8 importance blocks:
+// [bx0, bx0 + bw) x [by0, by0 + bh) of the frame's w_imp x h_imp
+inline void impwin_group_blocks(int tx0, int ty0, int tw, int th, int w_imp, int h_imp, int &bx0,
+                                int &by0, int &bw, int &bh) {
+  bx0 = tx0 * 8;
+  by0 = ty0 * 8;
+  bw = ((tx0 + tw) * 8 < w_imp ? (tx0 + tw) * 8 : w_imp) - bx0;
+  bh = ((ty0 + th) * 8 < h_imp ? (ty0 + th) * 8 : h_imp) - by0;
+}
+
+// Frame data of the group's blocks of the coded frame whose luma input is
+// `cur`: intra costs, the 8x8 blocks' lookahead MVs from `look` ([R][nsb][16]
+// over the group's tw x th superblocks), their fractions against each
+// reference's original frame refs[k].
+int impwin_group_data(const rv_plane &cur, const rv_plane *refs, int R, int bit_depth,
+                      const rv_fs_result *look, int tx0, int ty0, int tw, int th, int w_imp,
+                      int h_imp, const ImpFrame &f, hipStream_t st);
+
+// A group's part for the exchange (kImpPartBytes per block of its
+// rectangle) out of the frame data, or (unpack) back into it.
+constexpr int kImpPartBytes = 4 + 8 * kImpMaxRefs;
+int impwin_part(const ImpFrame &f, int R, int tx0, int ty0, int tw, int th, int w_imp, int h_imp,
+                void *buf, bool unpack, hipStream_t st);
+
+// Once every block's data is in: per reference the target lists of the
+// whole frame.
+int impwin_lists(const ImpFrame &f, int R, int w_imp, int h_imp, void *scratch,
+                 size_t scratch_bytes, hipStream_t st);
 
 // The (frame, reference ks[i]) passes, i < np <= kImpMaxRefs, in one
 // launch: the source frame's contributions (split over its nu reference

@@ -16,7 +16,7 @@ constexpr int kImpB = 8, kMvUnits = 8, kBMv = kImpB * kMvUnits, kAreaMv = kBMv *
 
 size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
-// impwin_frame_data's scratch: the entries' keys [R][4 n], the per-target
+// impwin_lists' scratch: the entries' keys [R][4 n], the per-target
 // counts and cursors [R][n] (rv_csr.h)
 struct CsrScratch {
   size_t keys, cnt, cur, total;
@@ -63,38 +63,38 @@ __device__ inline uint32_t satd8(const Px *o, int64_t os, const Px *r, int64_t r
   return (uint32_t)((satd_chunk<8>(d) + 4) >> 3);  // get_satd 8x8: ln = msb(8)
 }
 
-// One thread per 8x8 block and reference (blockIdx.y): lookahead_intra_costs
-// (pred_dc_128, :680-765; reference 0 stores them), the lookahead MV of the
-// 16x16 holding the block, get_satd against the reference's original block
-// at that MV (:911-931) and the propagate fraction (:939), and the block's
-// four (target, 4 * block + corner) entries, counted per target.
+// One thread per 8x8 block of the group's rectangle and reference
+// (blockIdx.y): lookahead_intra_costs (pred_dc_128, :680-765; reference 0
+// stores them), the lookahead MV of the 16x16 holding the block, get_satd
+// against the reference's original block at that MV (:911-931) and the
+// propagate fraction (:939).  A block whose reference region would leave
+// the allocation (the reference would panic; the search windows prevent
+// it) gets fraction 0.
 struct DataArgs {
   rv_plane cur, ref[kImpMaxRefs];
-  int base, w, h, tw, nsb;
+  int base, w, h;       // the frame's 8x8 blocks
+  int bx0, by0, bw, bh; // the group's blocks
+  int tx0, ty0, tw, nsb;  // the group's superblocks (look is [R][nsb][16] over them)
   const rv_fs_result *look;
   ImpFrame f;
-  uint32_t *keys;  // [R][4 n]
-  int32_t *cnt;    // [R][n], zero on entry
 };
 
 template <typename Px>
 __global__ __launch_bounds__(256) void data_kernel(DataArgs a) {
-  const int n = a.w * a.h;
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int j = blockIdx.x * 256 + threadIdx.x;
   const int k = blockIdx.y;
-  if (i >= n) return;
-  const int x = i % a.w, y = i / a.w;
+  if (j >= a.bw * a.bh) return;
+  const int n = a.w * a.h;
+  const int x = a.bx0 + j % a.bw, y = a.by0 + j / a.bw, i = y * a.w + x;
   const Px *o = plane_ptr<Px>(a.cur, x * kImpB, y * kImpB);
   const uint32_t intra = satd8<Px>(o, a.cur.stride, (const Px *)nullptr, 0, a.base);
   if (k == 0) a.f.intra[i] = intra;
-  const int sb = (y / 8) * a.tw + x / 8, b = ((y % 8) / 2) * 4 + (x % 8) / 2;
+  const int sb = (y / 8 - a.ty0) * a.tw + x / 8 - a.tx0, b = ((y % 8) / 2) * 4 + (x % 8) / 2;
   const rv_plane &ref = a.ref[k];
   const rv_mv mv = a.look[((size_t)k * a.nsb + sb) * 16 + b].best_mv;
   a.f.mv8[(size_t)k * n + i] = mv;
   const int64_t px_x = ((int64_t)x * kBMv + mv.col) / kMvUnits;  // isize `/`
   const int64_t px_y = ((int64_t)y * kBMv + mv.row) / kMvUnits;
-  // the reference block must lie inside the allocation (the reference's
-  // region would panic): the search windows keep it there
   const bool inside = px_x >= -ref.xorigin && px_y >= -ref.yorigin &&
                       px_x + kImpB <= ref.stride - ref.xorigin &&
                       px_y + kImpB <= ref.alloc_height - ref.yorigin;
@@ -106,14 +106,62 @@ __global__ __launch_bounds__(256) void data_kernel(DataArgs a) {
     frac = fmaxf(1.0f - __fdiv_rn(inter, (float)intra), 0.0f);
   }
   a.f.frac[(size_t)k * n + i] = frac;
+}
+
+// One thread per 8x8 block of the frame and reference (blockIdx.y): its four
+// (target, 4 * block + corner) entries, counted per target.  A block with
+// fraction 0 adds exactly +0.0f to each target (its amount is +0 and every
+// importance is >= +0), which leaves the target unchanged, so it is not
+// listed: the lists hold the blocks that change something.
+__global__ __launch_bounds__(256) void keys_kernel(ImpFrame f, int w, int h, uint32_t *keys,
+                                                   int32_t *cnt) {
+  const int n = w * h;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int k = blockIdx.y;
+  if (i >= n) return;
+  const bool live = f.frac[(size_t)k * n + i] > 0.f;
   int tgt[4];
   float fr[4];
-  corners(x, y, mv, a.w, a.h, tgt, fr);
+  corners(i % w, i / w, f.mv8[(size_t)k * n + i], w, h, tgt, fr);
 #pragma unroll
   for (int c = 0; c < 4; c++) {
-    const uint32_t key = inside ? (uint32_t)tgt[c] : (uint32_t)n;
-    a.keys[(size_t)k * 4 * n + 4 * (size_t)i + c] = key;
-    if (key < (uint32_t)n) atomicAdd(a.cnt + (size_t)k * n + key, 1);
+    const uint32_t key = live ? (uint32_t)tgt[c] : (uint32_t)n;
+    keys[(size_t)k * 4 * n + 4 * (size_t)i + c] = key;
+    if (key < (uint32_t)n) atomicAdd(cnt + (size_t)k * n + key, 1);
+  }
+}
+
+// A group's part of the frame data for the exchange (multi-group runs): per
+// block of the rectangle in raster order the intra cost, then per reference
+// slot k < 3 the MV and the fraction (kImpPartBytes).  unpack: the reverse.
+__global__ __launch_bounds__(256) void part_kernel(ImpFrame f, int w, int h, int R, int bx0,
+                                                   int by0, int bw, int bh, uint32_t *buf,
+                                                   int unpack) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= bw * bh) return;
+  const int n = w * h;
+  const size_t i = (size_t)(by0 + j / bw) * w + bx0 + j % bw;
+  uint32_t *p = buf + (size_t)j * (kImpPartBytes / 4);
+  if (!unpack) {
+    p[0] = f.intra[i];
+#pragma unroll
+    for (int k = 0; k < kImpMaxRefs; k++) {
+      const bool on = k < R;
+      rv_mv mv = on ? f.mv8[(size_t)k * n + i] : rv_mv{0, 0};
+      uint32_t mw;
+      __builtin_memcpy(&mw, &mv, 4);
+      p[1 + 2 * k] = mw;
+      p[2 + 2 * k] = on ? __float_as_uint(f.frac[(size_t)k * n + i]) : 0u;
+    }
+  } else {
+    f.intra[i] = p[0];
+    for (int k = 0; k < R; k++) {
+      rv_mv mv;
+      const uint32_t mw = p[1 + 2 * k];
+      __builtin_memcpy(&mv, &mw, 4);
+      f.mv8[(size_t)k * n + i] = mv;
+      f.frac[(size_t)k * n + i] = __uint_as_float(p[2 + 2 * k]);
+    }
   }
 }
 
@@ -231,17 +279,15 @@ void impwin_frame_carve(ImpFrame &f, void *base, int n, int R) {
 
 size_t impwin_scratch_bytes(int n) { return csr_scratch(n).total; }
 
-int impwin_frame_data(const rv_plane &cur, const rv_plane *refs, int R, int bit_depth,
-                      const rv_fs_result *look, int tw, int nsb, int w_imp, int h_imp,
-                      const ImpFrame &f, void *scratch, size_t scratch_bytes, hipStream_t st) {
+int impwin_group_data(const rv_plane &cur, const rv_plane *refs, int R, int bit_depth,
+                      const rv_fs_result *look, int tx0, int ty0, int tw, int th, int w_imp,
+                      int h_imp, const ImpFrame &f, hipStream_t st) {
   const int n = w_imp * h_imp;
-  if (R < 1 || R > kImpMaxRefs || n <= 0 || cur.xorigin + w_imp * 8 > cur.stride ||
-      cur.yorigin + h_imp * 8 > cur.alloc_height)
-    return rv_set_error(RV_EINVAL, "impwin_frame_data: bad geometry");
-  const CsrScratch s = csr_scratch(n);
-  if (!scratch || scratch_bytes < s.total)
-    return rv_set_error(RV_EINVAL, "impwin_frame_data: scratch");
-  uint8_t *base = (uint8_t *)scratch;
+  int bx0, by0, bw, bh;
+  impwin_group_blocks(tx0, ty0, tw, th, w_imp, h_imp, bx0, by0, bw, bh);
+  if (R < 1 || R > kImpMaxRefs || n <= 0 || bw <= 0 || bh <= 0 ||
+      cur.xorigin + w_imp * 8 > cur.stride || cur.yorigin + h_imp * 8 > cur.alloc_height)
+    return rv_set_error(RV_EINVAL, "impwin_group_data: bad geometry");
   DataArgs a;
   memset(&a, 0, sizeof(a));
   a.cur = cur;
@@ -249,25 +295,55 @@ int impwin_frame_data(const rv_plane &cur, const rv_plane *refs, int R, int bit_
   a.base = 128 << (bit_depth - 8);
   a.w = w_imp;
   a.h = h_imp;
+  a.bx0 = bx0;
+  a.by0 = by0;
+  a.bw = bw;
+  a.bh = bh;
+  a.tx0 = tx0;
+  a.ty0 = ty0;
   a.tw = tw;
-  a.nsb = nsb;
+  a.nsb = tw * th;
   a.look = look;
   a.f = f;
-  a.keys = (uint32_t *)(base + s.keys);
-  a.cnt = (int32_t *)(base + s.cnt);
-  int32_t *cursor = (int32_t *)(base + s.cur);
-  {
-    const hipError_t e = hipMemsetAsync(a.cnt, 0, (size_t)R * n * 4, st);
-    if (e != hipSuccess) return rv_set_hip_error(e, "impwin_frame_data");
-  }
-  const dim3 grid((unsigned)((n + 255) / 256), (unsigned)R);
+  const dim3 grid((unsigned)((bw * bh + 255) / 256), (unsigned)R);
   if (cur.hbd)
     data_kernel<uint16_t><<<grid, 256, 0, st>>>(a);
   else
     data_kernel<uint8_t><<<grid, 256, 0, st>>>(a);
   RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+int impwin_lists(const ImpFrame &f, int R, int w_imp, int h_imp, void *scratch,
+                 size_t scratch_bytes, hipStream_t st) {
+  const int n = w_imp * h_imp;
+  if (R < 1 || R > kImpMaxRefs || n <= 0) return rv_set_error(RV_EINVAL, "impwin_lists: bad arguments");
+  const CsrScratch s = csr_scratch(n);
+  if (!scratch || scratch_bytes < s.total) return rv_set_error(RV_EINVAL, "impwin_lists: scratch");
+  uint8_t *base = (uint8_t *)scratch;
+  uint32_t *keys = (uint32_t *)(base + s.keys);
+  int32_t *cnt = (int32_t *)(base + s.cnt), *cursor = (int32_t *)(base + s.cur);
+  {
+    const hipError_t e = hipMemsetAsync(cnt, 0, (size_t)R * n * 4, st);
+    if (e != hipSuccess) return rv_set_hip_error(e, "impwin_lists");
+  }
+  keys_kernel<<<dim3((unsigned)((n + 255) / 256), (unsigned)R), 256, 0, st>>>(f, w_imp, h_imp, keys,
+                                                                            cnt);
+  RV_HIP_CHECK_LAUNCH();
   // every reference's target lists, in source order within a target
-  return csr_build(a.keys, 4 * n, n, R, a.cnt, cursor, f.off, f.src, st);
+  return csr_build(keys, 4 * n, n, R, cnt, cursor, f.off, f.src, st);
+}
+
+int impwin_part(const ImpFrame &f, int R, int tx0, int ty0, int tw, int th, int w_imp, int h_imp,
+                void *buf, bool unpack, hipStream_t st) {
+  int bx0, by0, bw, bh;
+  impwin_group_blocks(tx0, ty0, tw, th, w_imp, h_imp, bx0, by0, bw, bh);
+  if (R < 1 || R > kImpMaxRefs || bw <= 0 || bh <= 0 || !buf)
+    return rv_set_error(RV_EINVAL, "impwin_part: bad arguments");
+  part_kernel<<<(unsigned)((bw * bh + 255) / 256), 256, 0, st>>>(f, w_imp, h_imp, R, bx0, by0, bw,
+                                                                 bh, (uint32_t *)buf, unpack ? 1 : 0);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
 }
 
 int impwin_pass(const ImpFrame &src, const int *ks, float *const *ref_imp, int np, int nu,

@@ -1002,6 +1002,25 @@ struct LaOut {
 // RW = W + 1 + kLaSlack: the slack covers the frames a twin instance still
 // has in flight behind the primary.
 constexpr int kEngineWaitS = 60;  // la_engine_take's bound on one frame's wait
+
+// An in-process exchange of the lookahead engines' frame parts between the
+// tile groups of one process (rv_la_hub_create: the GPU tests and the
+// bench's rank emulation; real ranks all-gather over RCCL).  Group k's
+// engine packs coded frame m's part into its buffer m % kRing, records an
+// event and posts m; once every group has posted m it waits on the others'
+// events and unpacks their parts.  A buffer is rewritten kRing frames later,
+// after every group's unpack of it (each group posts frame m + 1 only after
+// issuing its unpack of m).
+struct rv_la_hub {
+  static constexpr int kRing = 4;
+  int n = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<long> posted;
+  std::vector<uint8_t *> buf[kRing];
+  std::vector<hipEvent_t> ev[kRing];
+};
+
 struct RvLaEngine {
   static constexpr int kLaSlack = 28;
   int W = 0, RW = 0, dev = 0;
@@ -1033,6 +1052,15 @@ struct RvLaEngine {
   int err = 0;
   std::string msg;
   long la_round_sum = 0, la_reeval = 0, la_frames = 0;  // under mu
+  // several tile groups (rv_replay_set_la_exchange): every group's part of
+  // each frame's importance data reaches every group, over RCCL (comm, the
+  // part buffers psend / precv, pbytes per group) or an in-process hub
+  void *comm = nullptr;
+  uint8_t *psend = nullptr, *precv = nullptr;
+  size_t pbytes = 0;
+  rv_la_hub *hub = nullptr;
+  int hub_k = -1;
+  std::vector<hipEvent_t> hub_ev;  // this member's hub events (destroyed with the engine)
   Entry &at(long m) { return ring[(size_t)(m % RW)]; }
 };
 
@@ -2702,6 +2730,63 @@ static long coded_of_display(long d) {
   return 4 * ((d - off[j]) / 4) + j + 1;
 }
 
+// Several tile groups: every group's part of frame m's importance data into
+// every group's entry (the propagation reads the whole frame).  One group
+// covering the frame: nothing to do.
+static int la_exchange(rv_replay *r, long m, RvLaEngine::Entry &e, int R, hipStream_t xs) {
+  RvLaEngine &E = *r->eng;
+  const Geo &g = r->g;
+  const int ng = r->n_groups;
+  if (ng <= 1 && !E.comm) {
+    if (g.tx0 || g.ty0 || g.vis_w != g.W || g.vis_h != g.H)
+      return rv_set_error(RV_EINVAL, "rv_replay_frame: a tile group's window needs the other groups "
+                                     "(rv_replay_set_groups + rv_replay_set_la_exchange)");
+    return RV_OK;
+  }
+  auto rect = [&](int j) { return r->grects + 4 * j; };
+  if (E.comm) {
+#if RV_HAVE_RCCL
+    const int32_t *me = rect(r->my_group);
+    RV_R(impwin_part(e.f, R, me[0], me[1], me[2], me[3], g.w_imp, g.h_imp, E.psend, false, xs));
+    if (ncclAllGather(E.psend, E.precv, E.pbytes, ncclUint8, (ncclComm_t)E.comm, xs) != ncclSuccess)
+      return rv_set_error(RV_EHIP, "la_exchange: ncclAllGather");
+    for (int j = 0; j < ng; j++)
+      if (j != r->my_group)
+        RV_R(impwin_part(e.f, R, rect(j)[0], rect(j)[1], rect(j)[2], rect(j)[3], g.w_imp, g.h_imp,
+                         E.precv + (size_t)j * E.pbytes, true, xs));
+    return RV_OK;
+#else
+    return rv_set_error(RV_EINVAL, "la_exchange: built without RCCL");
+#endif
+  }
+  rv_la_hub *h = E.hub;
+  if (!h || h->n != ng)
+    return rv_set_error(RV_EINVAL, "rv_replay_frame: a tile group's window needs an exchange "
+                                   "(rv_replay_set_la_exchange)");
+  const int k = E.hub_k, slot = (int)(m % rv_la_hub::kRing);
+  const int32_t *me = rect(k);
+  RV_R(impwin_part(e.f, R, me[0], me[1], me[2], me[3], g.w_imp, g.h_imp, h->buf[slot][k], false, xs));
+  RV_H(hipEventRecord(h->ev[slot][k], xs));
+  {
+    std::unique_lock<std::mutex> lk(h->mu);
+    h->posted[k] = m;
+    h->cv.notify_all();
+    if (!h->cv.wait_for(lk, std::chrono::seconds(kEngineWaitS), [&] {
+          for (int j = 0; j < ng; j++)
+            if (h->posted[j] < m) return false;
+          return true;
+        }))
+      return rv_set_error(RV_EHIP, "la_exchange: a group's part never arrived");
+  }
+  for (int j = 0; j < ng; j++) {
+    if (j == k) continue;
+    RV_H(hipStreamWaitEvent(xs, h->ev[slot][j], 0));
+    RV_R(impwin_part(e.f, R, rect(j)[0], rect(j)[1], rect(j)[2], rect(j)[3], g.w_imp, g.h_imp,
+                     h->buf[slot][j], true, xs));
+  }
+  return RV_OK;
+}
+
 // One step of the engine: coded frame m's lookahead and importance data
 // into its entry, then the window propagation of every frame whose window
 // is now complete (n + W = m, or the stream's last frame).
@@ -2746,8 +2831,10 @@ static int la_step(rv_replay *r, long m) {
   }
   rv_plane refs_o[kImpMaxRefs];
   for (int k = 0; k < lr.n; k++) refs_o[k] = r->inputs[lr.disp[k] % r->inputs.size()].y;
-  RV_R(impwin_frame_data(r->inputs[fi.display % r->inputs.size()].y, refs_o, lr.n, g.bd, e.o.look,
-                         g.tw, g.nsb, g.w_imp, g.h_imp, e.f, E.scratch, E.scratch_bytes, xs));
+  RV_R(impwin_group_data(r->inputs[fi.display % r->inputs.size()].y, refs_o, lr.n, g.bd, e.o.look,
+                         g.tx0, g.ty0, g.tw, g.th, g.w_imp, g.h_imp, e.f, xs));
+  RV_R(la_exchange(r, m, e, lr.n, xs));
+  RV_R(impwin_lists(e.f, lr.n, g.w_imp, g.h_imp, E.scratch, E.scratch_bytes, xs));
   e.m = m;
   e.fi = fi;
   e.lr = lr;
@@ -2851,6 +2938,8 @@ static void la_engine_destroy(rv_replay *r) {
     if (en.ev_imp) (void)hipEventDestroy(en.ev_imp);
     if (en.ev_used) (void)hipEventDestroy(en.ev_used);
   }
+  for (hipEvent_t ev : E->hub_ev)
+    if (ev) (void)hipEventDestroy(ev);
   if (E->rr.h_pub) (void)hipHostFree(E->rr.h_pub);
   if (E->las) (void)hipStreamDestroy(E->las);
   delete E;  // its device arrays are the replay's allocations (freed with it)
@@ -2928,9 +3017,7 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
     return rv_set_error(RV_EINVAL, "rv_replay_set_imp_window: bad arguments");
   if (r->coded > 0) return rv_set_error(RV_EINVAL, "rv_replay_set_imp_window: after the first frame");
   const Geo &g = r->g;
-  if (window > 0 && (g.tx0 || g.ty0 || g.vis_w != g.W || g.vis_h != g.H || r->n_groups > 1))
-    return rv_set_error(RV_EINVAL, "rv_replay_set_imp_window: a window needs the whole frame "
-                                   "(one group)");
+  (void)g;  // a tile group's window exchanges parts (rv_replay_set_la_exchange)
   if (r->eng && !r->eng_owned)
     return rv_set_error(RV_EINVAL, "rv_replay_set_imp_window: on the primary instance");
   la_engine_destroy(r);
@@ -2983,6 +3070,67 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
     return rv_set_error(RV_EHIP, "rv_replay_set_imp_window: allocation failed");
   }
   E->th = std::thread(la_thread_main, r);
+  return RV_OK;
+}
+
+// Tile groups with an importance window: how each frame's importance data
+// of the other groups arrives (la_exchange).
+rv_la_hub *rv_la_hub_create(int n_groups) {
+  if (n_groups < 2 || n_groups > kMaxGroups) {
+    rv_set_error(RV_EINVAL, "rv_la_hub_create: 2 .. kMaxGroups groups");
+    return nullptr;
+  }
+  rv_la_hub *h = new rv_la_hub();
+  h->n = n_groups;
+  h->posted.assign((size_t)n_groups, 0);
+  for (int s = 0; s < rv_la_hub::kRing; s++) {
+    h->buf[s].assign((size_t)n_groups, nullptr);
+    h->ev[s].assign((size_t)n_groups, nullptr);
+  }
+  return h;
+}
+void rv_la_hub_destroy(rv_la_hub *h) { delete h; }  // the members own the buffers / events
+
+int rv_replay_set_la_exchange(rv_replay *r, void *comm, rv_la_hub *hub) {
+  if (!r || (!comm == !hub)) return rv_set_error(RV_EINVAL, "rv_replay_set_la_exchange: comm xor hub");
+  if (!r->eng || !r->eng_owned || r->coded > 0)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_la_exchange: a primary instance with a window, "
+                                   "before the first frame");
+  if (r->n_groups < 2 && !comm)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_la_exchange: rv_replay_set_groups first");
+  RvLaEngine &E = *r->eng;
+  const Geo &g = r->g;
+  size_t most = 0;
+  for (int j = 0; j < r->n_groups; j++) {
+    int bx0, by0, bw, bh;
+    impwin_group_blocks(r->grects[4 * j], r->grects[4 * j + 1], r->grects[4 * j + 2],
+                        r->grects[4 * j + 3], g.w_imp, g.h_imp, bx0, by0, bw, bh);
+    const size_t b = (size_t)bw * bh * kImpPartBytes;
+    most = b > most ? b : most;
+  }
+  E.pbytes = (most + 255) / 256 * 256;
+  if (comm) {
+    E.psend = (uint8_t *)dalloc(r, E.pbytes);
+    E.precv = (uint8_t *)dalloc(r, E.pbytes * (size_t)r->n_groups);
+    if (!E.psend || !E.precv) return rv_set_error(RV_EHIP, "rv_replay_set_la_exchange: alloc");
+    E.comm = comm;
+    return RV_OK;
+  }
+  if (hub->n != r->n_groups)
+    return rv_set_error(RV_EINVAL, "rv_replay_set_la_exchange: the hub's group count");
+  const int k = r->my_group;
+  std::lock_guard<std::mutex> lk(hub->mu);
+  for (int s = 0; s < rv_la_hub::kRing; s++) {
+    if (hub->buf[s][k]) return rv_set_error(RV_EINVAL, "rv_replay_set_la_exchange: group joined twice");
+    hub->buf[s][k] = (uint8_t *)dalloc(r, E.pbytes);
+    hipEvent_t ev = nullptr;
+    RV_H(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    E.hub_ev.push_back(ev);
+    hub->ev[s][k] = ev;
+    if (!hub->buf[s][k]) return rv_set_error(RV_EHIP, "rv_replay_set_la_exchange: alloc");
+  }
+  E.hub = hub;
+  E.hub_k = k;
   return RV_OK;
 }
 

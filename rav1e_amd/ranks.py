@@ -108,11 +108,29 @@ class TileParallel:
         if self.host:
             self.size = max(engine.region_bytes(r) for r in self.rects)
 
+    def _lookahead_parts(self):
+        """A group's importance window (CpuReplay): every lookahead frame the
+        next frame needs, each group's part all-gathered and imported (the
+        propagation reads the whole frame)."""
+        due = self.engine.la_due() if hasattr(self.engine, "la_due") else None
+        if due is None:
+            return
+        nxt, last, _ = due
+        size = max(self.engine.la_part_bytes(r) for r in self.rects)
+        mine_b = self.engine.la_part_bytes(self.rects[self.my])
+        for m in range(nxt, last + 1):
+            mine = self.engine.la_group(m, mine_b)
+            bufs = self.group.all_gather_bytes(mine, size)
+            for k, (rect, b) in enumerate(zip(self.rects, bufs)):
+                if k != self.my:
+                    self.engine.la_import(m, rect, b[: self.engine.la_part_bytes(rect)])
+
     def frame(self):
         if self.world == 1:
             return self.engine.frame()
         if not self.host:
             return self.engine.frame()
+        self._lookahead_parts()
         info = self.engine.frame(pad=False)
         mine = self.engine.export(self.rects[self.my])
         bufs = self.group.all_gather_bytes(mine, self.size)

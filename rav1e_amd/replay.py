@@ -372,6 +372,13 @@ class HipReplay:
                 "is_key": fi.is_key, "ref_display": list(fi.ref_display),
                 "compound": fi.compound}
 
+    def set_la_exchange(self, comm=None, hub=None):
+        """A tile group's importance window: how the other groups' lookahead
+        parts arrive (rv_replay_set_la_exchange) -- an RCCL communicator
+        (handle) or an in-process LaHub."""
+        _check(lib().rv_replay_set_la_exchange(self.h, comm, hub.h if hub else None),
+               "rv_replay_set_la_exchange")
+
     def set_groups(self, rects, my_group, comm=None):
         arr = np.ascontiguousarray(np.asarray(rects, dtype=np.int32).ravel())
         _check(lib().rv_replay_set_groups(self.h, len(rects), arr.ctypes.data, my_group, comm),
@@ -683,8 +690,9 @@ class PipelinedReplay:
         self.err = None
         self.ev = [lib().rv_event_create() for _ in range(self.EV_RING)]
         self.done = {}  # coded frame -> threading.Event (its event is recorded)
-        self.issued = {}  # coded frame -> threading.Event (its stream waits are queued)
         self.lock = threading.Lock()
+        self.cv = threading.Condition(self.lock)
+        self.issued_set, self.issued_upto, self.pruned = set(), -1, -1
         self.held = None  # a 4g+1 frame waiting for the next level-0 frame
         self.qs = [queue.Queue() for _ in self.inst]
         self.workers = [threading.Thread(target=self._run, args=(i,), daemon=True)
@@ -708,29 +716,41 @@ class PipelinedReplay:
     def on_primary(self, f: int) -> bool:
         return self.instance_of(f + 1) == 0
 
-    def _flag(self, n, d=None):
-        d = self.done if d is None else d
+    def _flag(self, n):
         with self.lock:
-            if n not in d:
-                d[n] = __import__("threading").Event()
-            return d[n]
+            if n not in self.done:
+                assert n > self.pruned, (n, self.pruned)
+                self.done[n] = __import__("threading").Event()
+            return self.done[n]
+
+    def _mark_issued(self, n):
+        """Frame n's stream waits are queued: advance issued_upto (every
+        frame <= it has queued its waits) and drop the flags no frame can
+        wait on any more (a frame waits on frames at most DEP_SPAN back, and
+        every frame still to queue its waits is after issued_upto)."""
+        with self.lock:
+            self.issued_set.add(n)
+            while self.issued_upto + 1 in self.issued_set:
+                self.issued_upto += 1
+                self.issued_set.discard(self.issued_upto)
+            cut = self.issued_upto - self.DEP_SPAN
+            if cut > self.pruned:
+                for k in range(self.pruned + 1, cut):
+                    self.done.pop(k, None)
+                self.pruned = cut - 1
+            self.cv.notify_all()
 
     def _before_record(self, n):
         """Frame n is about to re-record ev[n % EV_RING], the event of frame
-        n - EV_RING: every frame that waits on that one must have queued its
-        stream wait first (they are all within DEP_SPAN of it, far behind n,
-        so this never blocks in practice; it enforces the ring's bound).
-        Then flags of frames no later frame can wait on are dropped."""
-        old = n - self.EV_RING
-        if old < 0:
-            return
-        for k in range(old + 1, min(n, old + self.DEP_SPAN + 1)):
-            if old in self._deps(k):
-                self._flag(k, self.issued).wait()
+        n - EV_RING: every frame that can wait on that one (within DEP_SPAN
+        after it) must have queued its stream wait first.  Those frames
+        precede n and wait only on frames before them, none queued behind n
+        on this instance, so this never deadlocks (and in practice never
+        blocks: the instances stay within a few frames of each other)."""
+        need = n - self.EV_RING + self.DEP_SPAN
         with self.lock:
-            for d in (self.done, self.issued):
-                for k in [k for k in d if k <= old and d[k].is_set()]:
-                    del d[k]
+            while self.issued_upto < need:
+                self.cv.wait()
 
     def _deps(self, n: int) -> list:
         """Coded frames on other instances that frame n waits for."""
@@ -778,7 +798,7 @@ class PipelinedReplay:
                         self._flag(k).wait()
                         _check(lib().rv_stream_wait_event(inst.stream, self.ev[k % self.EV_RING]),
                                "rv_stream_wait_event")
-                    self._flag(n, self.issued).set()
+                    self._mark_issued(n)
                     if n:
                         inst.seek(n)
                     inst.frame()
@@ -788,7 +808,8 @@ class PipelinedReplay:
             except Exception as e:  # handed to the main thread by drain()
                 self.err = e
             finally:
-                self._flag(n, self.issued).set()
+                if n not in self.issued_set and n > self.issued_upto:
+                    self._mark_issued(n)
                 self._flag(n).set()
                 self.qs[i].task_done()
 
@@ -866,6 +887,22 @@ class PipelinedReplay:
 
     def __getattr__(self, name):
         return getattr(self.p, name)
+
+
+class LaHub:
+    """The in-process exchange of the lookahead engines' frame parts between
+    the tile groups of one process (rv_la_hub_create): GPU tests and the
+    bench's rank emulation."""
+
+    def __init__(self, n_groups: int):
+        self.h = lib().rv_la_hub_create(int(n_groups))
+        if not self.h:
+            raise RuntimeError(f"rv_la_hub_create: {lib().rv_last_error().decode()}")
+
+    def close(self):
+        if self.h:
+            lib().rv_la_hub_destroy(self.h)
+            self.h = None
 
 
 class RcclComm:

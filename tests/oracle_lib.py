@@ -605,6 +605,38 @@ class CpuReplay:
         imp = np.ascontiguousarray(imp, dtype=np.float32)
         assert self.L.orc_replay_set_importances(self.h, imp.ctypes.data, imp.size) == 0
 
+    # ---- a tile group's importance window (orc_replay_la_due / _group /
+    # _import): each group computes its own blocks' lookahead part, the
+    # caller exchanges the parts before frame()
+    def la_due(self):
+        """(next coded frame whose part is due, the last one the next frame
+        needs, the part's bytes); None without a group window"""
+        out = (C.c_long * 3)()
+        self.L.orc_replay_la_due.argtypes = [C.c_void_p, C.c_void_p]
+        if self.L.orc_replay_la_due(self.h, out) != 0:
+            return None
+        return int(out[0]), int(out[1]), int(out[2])
+
+    def la_group(self, m, nbytes) -> np.ndarray:
+        out = np.zeros(nbytes, np.uint8)
+        self.L.orc_replay_la_group.argtypes = [C.c_void_p, C.c_long, C.c_void_p]
+        assert self.L.orc_replay_la_group(self.h, m, out.ctypes.data) == 0, "orc_replay_la_group"
+        return out
+
+    def la_import(self, m, rect, buf):
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        self.L.orc_replay_la_import.argtypes = [C.c_void_p, C.c_long] + [C.c_int] * 4 + [C.c_void_p]
+        assert self.L.orc_replay_la_import(self.h, m, *[int(v) for v in rect],
+                                           buf.ctypes.data) == 0, "orc_replay_la_import"
+
+    def la_part_bytes(self, rect) -> int:
+        """bytes of a group's lookahead part (28 per 8x8 block of its rect)"""
+        tx0, ty0, tw, th = rect
+        hi, wi = self.imp_shape
+        bw = min((tx0 + tw) * 8, wi) - tx0 * 8
+        bh = min((ty0 + th) * 8, hi) - ty0 * 8
+        return 28 * bw * bh
+
     def frame(self, sb_limit=0, pad=True) -> dict:
         fi = OrcFrameInfo()
         assert self.L.orc_replay_frame(self.h, C.byref(fi), sb_limit, 1 if pad else 0) == 0

@@ -209,5 +209,11 @@ def test_importance_window_changes_the_decision_inputs_only():
         assert (a.importances() == 0).all()
         assert (b.importances() >= 0).all()
     assert (b.importances() > 0).any()
+    # a tile group's window needs the other groups' lookahead parts first
+    g = O.CpuReplay(w, h, group=(1, 0, 2, 2), n_inputs=len(fr), imp_window=2)
+    for i, f in enumerate(fr):
+        g.set_input(i, f)
+    g.frame()  # the key frame
     with pytest.raises(AssertionError):
-        O.CpuReplay(w, h, group=(1, 0, 2, 2), n_inputs=4, imp_window=2)
+        g.frame()
+    assert g.la_due()[:2] == (1, 3)

@@ -14,7 +14,7 @@ import torch.multiprocessing as mp
 
 from rav1e_amd import replay as RP
 
-W, H, REFS, NIN = 384, 192, 2, 12
+W, H, REFS, NIN = 384, 192, 2, 16
 
 
 def _free_port():
@@ -31,22 +31,22 @@ def _tiling():
     return t, (t["tile_width_sb"], t["tile_height_sb"])
 
 
-def _single_words(frames, deblock=False):
+def _single_words(frames, deblock=False, window=0):
     from rav1e_amd import replay as RP
     from tests import oracle_lib as O
     _, ts = _tiling()
     c = O.CpuReplay(W, H, 1, 1, 8, REFS, tile_size=ts, n_inputs=NIN, threads=2,
-                    deblock=deblock)
+                    deblock=deblock, imp_window=window)
     for i in range(NIN):
         c.set_input(i, RP.synth_frame(W, H, i))
     for _ in range(frames):
         c.frame()
-    w = c.results()
+    w, imp = c.results(), c.importances()
     c.close()
-    return w
+    return w, imp
 
 
-def _rank_main(rank, world, port, q, deblock):
+def _rank_main(rank, world, port, q, deblock, window):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import bench
@@ -58,7 +58,7 @@ def _rank_main(rank, world, port, q, deblock):
     t, ts = _tiling()
     rects = RP.tile_groups(t, world)
     c = O.CpuReplay(W, H, 1, 1, 8, REFS, group=rects[rank], tile_size=ts, n_inputs=NIN,
-                    threads=2, deblock=deblock)
+                    threads=2, deblock=deblock, imp_window=window)
     for i in range(NIN):
         c.set_input(i, RP.synth_frame(W, H, i))
     if rank == 1:  # make rank 1 the slow one: the reported time must be its
@@ -71,31 +71,34 @@ def _rank_main(rank, world, port, q, deblock):
         c.frame = slow
     eng = TileParallel(c, rects, rank, g)
     dt, words = bench.timed_run(eng, g, steps=4, warmup=2)
-    q.put((rank, dt, words.tolist(), rects[rank]))
+    q.put((rank, dt, words.tolist(), rects[rank], c.importances().tolist()))
     c.close()
     g.close()
 
 
-@pytest.mark.parametrize("deblock", [False, True])
-def test_two_rank_gloo_tile_parallel_stream(deblock):
+@pytest.mark.parametrize("deblock,window", [(False, 0), (True, 0), (True, 3)])
+def test_two_rank_gloo_tile_parallel_stream(deblock, window):
     """With deblock the exchange also carries the block maps and each rank
-    deblocks the whole frame."""
+    deblocks the whole frame.  With an importance window each rank computes
+    its group's lookahead part and the parts are all-gathered before every
+    frame: the ranks code the one-process stream, importances included."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q, deblock)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q, deblock, window))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = {}
     for _ in range(2):
-        rank, dt, words, rect = q.get(timeout=240)
-        res[rank] = (dt, np.array(words, dtype=np.uint64), rect)
+        rank, dt, words, rect, imp = q.get(timeout=240)
+        res[rank] = (dt, np.array(words, dtype=np.uint64), rect, np.array(imp, np.float32))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     # max over ranks: both report the slow rank's time (>= 4 sleeps)
     assert abs(res[0][0] - res[1][0]) < 1e-9 and res[0][0] >= 0.2
-    single = _single_words(6, deblock)
+    single, simp = _single_words(6, deblock, window)
     per = RP.sb_words_per(REFS)
     sbc = (W + 63) // 64
     sw = single[: len(single) - 5].reshape(-1, per)
@@ -105,4 +108,7 @@ def test_two_rank_gloo_tile_parallel_stream(deblock):
         for sb in range(gw * gh):
             np.testing.assert_array_equal(gsb[sb], sw[(y0 + sb // gw) * sbc + x0 + sb % gw])
         assert words[-1] == single[-1]  # the whole reconstruction on every rank
+        np.testing.assert_array_equal(res[r][3].view(np.uint32), simp.view(np.uint32))
+    if window:
+        assert (simp > 0).any()
     assert res[0][2] != res[1][2]

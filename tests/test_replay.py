@@ -579,6 +579,105 @@ def test_gpu_tile_groups_exchange(flags):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF])
+def test_gpu_tile_groups_importance_window(flags):
+    """Two GPU tile groups with an importance window: each group's engine
+    computes its own blocks' lookahead part, the parts meet in an in-process
+    hub (the RCCL all-gather's role), every group propagates over the whole
+    frame -- words, reconstructions and importances equal the CPU replay of
+    the whole frame with the same window."""
+    import ctypes as C
+
+    import rav1e_amd as R
+    R.require_device(0)
+    w, h, nin, W = 384, 192, 20, 3
+    t = RP.tiling_for(w, h, tile_cols=2)
+    ts = (t["tile_width_sb"], t["tile_height_sb"])
+    rects = RP.tile_groups(t, 2)
+    hub = RP.LaHub(2)
+    gs = [RP.HipReplay(w, h, group=r, tile_size=ts, n_inputs=nin, flags=flags, imp_window=W)
+          for r in rects]
+    for k, g in enumerate(gs):
+        g.synth_inputs(0)
+        g.set_groups(rects, k, None)
+        g.set_la_exchange(hub=hub)
+        g.set_inputs_ready(nin)  # the groups code one after another here
+    c = O.CpuReplay(w, h, tile_size=ts, n_inputs=nin, threads=4, imp_window=W,
+                    deblock=bool(flags & RP.RV_REPLAY_DEBLOCK), cdef=bool(flags & RP.RV_REPLAY_CDEF))
+    for i in range(nin):
+        c.set_input(i, RP.synth_frame(w, h, i))
+    L = R.lib()
+    bufs = [g.exchange_buffers() for g in gs]
+    nb = bufs[0][2]
+    sbc = (w + 63) // 64
+    try:
+        for n in range(9):
+            for g in gs:
+                g.frame()
+            c.frame()
+            R._check(L.rv_device_sync(), "sync")
+            for k in range(2):
+                for j in range(2):
+                    R._check(L.rv_memcpy_d2d(C.c_void_p(bufs[k][1] + j * nb),
+                                             C.c_void_p(bufs[j][0]), nb, None), "rv_memcpy_d2d")
+            R._check(L.rv_device_sync(), "sync")
+            for g in gs:
+                g.import_()
+            cw = c.results()
+            sw = _sb_words(cw, sbc * ((h + 63) // 64), 2)
+            ci = c.importances()
+            for g, (x0, y0, gw_, gh_) in zip(gs, rects):
+                wg = g.results()
+                gsb = _sb_words(wg, gw_ * gh_, 2)
+                for sb in range(gw_ * gh_):
+                    np.testing.assert_array_equal(gsb[sb],
+                                                  sw[(y0 + sb // gw_) * sbc + x0 + sb % gw_],
+                                                  err_msg=f"frame {n}")
+                assert wg[-1] == cw[-1]
+                np.testing.assert_array_equal(g.importances().view(np.uint32),
+                                              ci.view(np.uint32), err_msg=f"frame {n}")
+        assert (ci > 0).any()
+    finally:
+        for g in gs:
+            g.close()
+        hub.close()
+
+
+@pytest.mark.gpu
+def test_gpu_replay_one_rank_rccl_la_exchange():
+    """The RCCL branch of the engine's part exchange (pack, ncclAllGather on
+    the engine stream) with a 1-rank communicator: the same importances and
+    words as the run without one."""
+    import os
+
+    import rav1e_amd as R
+    R.require_device(0)
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    L = R.lib()
+    idb = np.zeros(256, np.uint8)
+    assert L.rv_comm_unique_id(idb.ctypes.data, idb.size) > 0, L.rv_last_error()
+    comm = L.rv_comm_create(idb.ctypes.data, 1, 0)
+    assert comm, L.rv_last_error()
+    w, h, nin = 256, 192, 20
+    a, b = (RP.HipReplay(w, h, n_inputs=nin, imp_window=4, imp_limit=12) for _ in range(2))
+    a.synth_inputs(0)
+    b.synth_inputs(0)
+    a.set_groups([(0, 0, 4, 3)], 0, None)
+    a.set_la_exchange(comm=comm)
+    try:
+        for n in range(12):
+            ia, ib = a.frame(), b.frame()
+            assert ia == ib
+            np.testing.assert_array_equal(a.results(), b.results())
+            np.testing.assert_array_equal(a.importances().view(np.uint32),
+                                          b.importances().view(np.uint32))
+    finally:
+        a.close()
+        b.close()
+        L.rv_comm_destroy(comm)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("window,k", [(0, 3), (5, 3), (5, 5)])
 def test_gpu_pipelined_replay_matches_cpu(window, k):
     """PipelinedReplay: three instances (levels 0 + 4g+1, level 1, 4g+3) on
