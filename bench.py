@@ -326,7 +326,7 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     return cpu, parity
 
 
-def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2):
+def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2, imp_window=0):
     """The N-rank tile-group split on ONE GPU: config's n tile groups as n
     HipReplay instances (the ranks), each frame coded group by group with
     the GPU to itself, the all-gather emulated by device copies into every
@@ -343,12 +343,19 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2):
     rects = RP.tile_groups(tiling, n)
     gop = len(RP.GOP_SCALES)
     frames = 1 + gops * gop
-    gs = [RP.HipReplay(W, H, xdec, ydec, bd, nref, group=r, tile_size=ts, n_inputs=frames + 8,
-                       flags=flags) for r in rects]
+    nin = frames + 8 + (imp_window + 37 if imp_window else 0)
+    gs = [RP.HipReplay(W, H, xdec, ydec, bd, nref, group=r, tile_size=ts, n_inputs=nin,
+                       flags=flags, imp_window=imp_window) for r in rects]
+    # the importance window: each group's engine computes its blocks' part,
+    # the parts meet in an in-process hub (the ranks' RCCL all-gather)
+    hub = RP.LaHub(n) if imp_window else None
     sync = lambda: R._check(L.rv_device_sync(), "rv_device_sync")  # noqa: E731
     for k, g in enumerate(gs):
         g.synth_inputs(0)
         g.set_groups(rects, k, None)
+        if hub:
+            g.set_la_exchange(hub=hub)
+            g.set_inputs_ready(nin)  # the groups code one after another here
         g.set_timing(1, 1)
     bufs = [g.exchange_buffers() for g in gs]
     nb = bufs[0][2]
@@ -381,6 +388,8 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2):
     cnts = [[int(v) for v in g.counters()] for g in gs]
     for g in gs:
         g.close()
+    if hub:
+        hub.close()
     per = [sum(s) / len(s) for s in span]
     imp_ms = max(sum(s) / len(s) for s in imp)
     xgmi_gbs = 64.0  # assumed all-gather algorithm bandwidth per rank (RCCL over xGMI)
@@ -400,6 +409,7 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2):
             "group_reevaluated_sb_per_frame": [round(c[15] / max(1, c[16]), 1) for c in cnts],
             "group_lookahead_rounds_per_frame": [round(c[18] / max(1, c[16]), 2) for c in cnts],
             "group_order": "groups code each frame in index order (group 0 first)",
+            "importance_window": imp_window,
             "method": "one GPU, groups run one after another (HIP-event spans; import wall "
                       "clock incl. launch), device-copy all-gather"}
 
@@ -440,7 +450,8 @@ def main():
     ap.add_argument("--imp-window", type=int, default=IMP_WINDOW,
                     help="rdo_lookahead_frames: block importances propagated over that many "
                          "coded frames ahead (rav1e's default 40; 0: importance 0, bias 0.65); "
-                         "one GPU only (a window needs the whole frame's lookahead)")
+                         "with several GPUs each rank computes its tile group's lookahead part "
+                         "and the parts are all-gathered (the propagation reads the whole frame)")
     args = ap.parse_args()
     # a stalled run names where it stalled (every thread's stack on stderr)
     import faulthandler
@@ -461,7 +472,7 @@ def main():
     tiling = RP.tiling_for(W, H, **tkw)
     ts = (tiling["tile_width_sb"], tiling["tile_height_sb"])
     rects = RP.tile_groups(tiling, world)
-    imp_window = args.imp_window if world == 1 else 0
+    imp_window = args.imp_window
     # every display the run codes, the lookahead's W frames beyond, and the
     # engine's ring slack (RW = W + 29: it may run that far past the oldest
     # frame in flight).  The stream is unbounded (imp_limit 0): every frame's
@@ -509,7 +520,7 @@ def main():
         if probe:  # the F3 sub-pel kernel probe over the timed frames
             eng.set_kernel_probe(True)
         if imp_window:
-            la_cnt["t0"] = int(eng.counters()[20])
+            la_cnt["t0"] = int((eng if paired else hip).counters()[20])
 
     def start():
         if ready:
@@ -519,7 +530,7 @@ def main():
                           sync=lambda: R._check(R.lib().rv_device_sync(), "rv_device_sync"),
                           finish=eng.entropy_stats if ent else None, before=before, start=start)
     if imp_window:
-        la_cnt["t1"] = int(eng.counters()[20])
+        la_cnt["t1"] = int((eng if paired else hip).counters()[20])
     kp = eng.kernel_probe() if probe else None
     ent_stats = eng.entropy_stats() if ent else None
 
@@ -631,7 +642,12 @@ def main():
         # its units: the candidate evaluations those launches counted.
         dom = "diamond_subpel_64"
         nl = float(kp[0])
-        avg_s = kp[1] / nl / 1e3
+        # the launch's duration: its span on the device clock (the first
+        # workgroup's start to the last one's end, what rocprofv3 times);
+        # the HIP event pairs around it also hold the dispatch and the
+        # records (reported beside it)
+        ev_s = kp[1] / nl / 1e3
+        avg_s = kp[4] / nl / 1e3 if len(kp) > 4 and kp[4] > 0 else ev_s
         cand_b = (71 * 71 + 64 * 64) * px + 4  # fused MC + dist candidate
         bytes_l = kp[2] / nl * cand_b
         ach = bytes_l / avg_s / 1e9
@@ -639,6 +655,10 @@ def main():
                 "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
                 "avg_launch_ms": round(avg_s * 1e3, 5),
+                "avg_launch_ms_hip_events": round(ev_s * 1e3, 5),
+                "duration": "device clock (wall_clock64) span of every probed launch: first "
+                            "workgroup start to last workgroup end; HIP event pairs on the "
+                            "launch's stream beside it",
                 "algorithmic_bytes_per_launch": round(bytes_l),
                 "per_unit": {"unit": "candidate (MC + SAD of one sub-pel MV)", "bytes": cand_b,
                              "rule": "(64+7)^2 b window + 64^2 b source + 4 (SURVEY.md §8d)"},
@@ -691,7 +711,8 @@ def main():
     emu = None
     n_emu = min(args.emulate_ranks, tiling["cols"] * tiling["rows"])  # one tile group per rank
     if rank == 0 and world == 1 and n_emu > 1:
-        emu = emulate_ranks(n_emu, W, H, xdec, ydec, bd, nref, tiling, flags)
+        emu = emulate_ranks(n_emu, W, H, xdec, ydec, bd, nref, tiling, flags,
+                            imp_window=imp_window)
 
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -772,9 +793,12 @@ def main():
                 "engine_lead_at_start": ("the window (W frames): no input declared ready before "
                                          "the timing" if ready else "not capped"),
                 "lookahead_rounds_per_frame": round(cnt[18] / max(1, cnt[20]), 3)
-                if len(cnt) > 20 else None} if imp_window else
-                {"window": 0, "what": "importance 0 (bias 0.65)" +
-                 ("; a window needs the whole frame's lookahead: one GPU only" if world > 1 else "")}),
+                if len(cnt) > 20 else None,
+                **({"ranks": "each rank's engine computes its tile group's lookahead part; the "
+                             "parts are all-gathered over RCCL on the encode stream before the "
+                             "frames whose window needs them, so every rank propagates over the "
+                             "whole frame"} if world > 1 else {})} if imp_window else
+                {"window": 0, "what": "importance 0 (bias 0.65)"}),
             "intra_per_frame": {"screened_superblocks": round(cnt[11] / ev_frames, 2),
                                 "intra_winners": round(cnt[12] / ev_frames, 2),
                                 "rounds": round(cnt[13] / ev_frames, 2),

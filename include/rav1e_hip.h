@@ -773,9 +773,11 @@ int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,
  * of an instrumented frame (rv_replay_set_timing) is bracketed by a HIP
  * event pair on the stream it runs on and adds its candidate evaluations
  * and jobs to a device counter.  (Re)starting drops the sums so far.
- * rv_replay_kernel_probe: out[0] launches, out[1] their summed ms, out[2]
- * candidate evaluations, out[3] jobs since the last start (cap >= 4;
- * returns 4; waits for the launches). */
+ * rv_replay_kernel_probe: out[0] launches, out[1] their summed ms (event
+ * pairs), out[2] candidate evaluations, out[3] jobs since the last start,
+ * (cap >= 5) out[4] the launches' summed ms on the device clock (first
+ * workgroup's start to last workgroup's end, wall_clock64); returns the
+ * count written; waits for the launches. */
 int rv_replay_set_kernel_probe(rv_replay *r, int on);
 /* Host-only test hook (no device call): the slots the round ring gives
  * round check q -- out[0] its device count slot, out[1] the slot it zeroes

@@ -96,6 +96,10 @@ struct DsArgs {
   // optional (ds_fast_kernel): [0] += the launch's candidate evaluations,
   // [1] += its jobs -- the bench's kernel probe (algorithmic bytes per launch)
   uint32_t *eval_acc;
+  // optional (ds_fast_kernel, the kernel probe): the launch's span on the
+  // device clock -- every workgroup's first instruction min'd into t0, its
+  // last max'd into t1 (wall_clock64 ticks)
+  unsigned long long *t0, *t1;
   ChainNext next;   // replay: feed the winner into the next stage's jobs
   int tele;         // 1: telescopic_subpel_search instead of the diamond
   const rv_fs_result *start;  // tele: the search's start (best_mv, lowest_cost)
@@ -711,7 +715,12 @@ __device__ __forceinline__ void ds_fast_jobs(const DsArgs &a) {
 template <typename Px, int W, int H, bool SUB>
 __global__ __launch_bounds__(kDsThreads) __attribute__((amdgpu_waves_per_eu(5))) void
 ds_fast_kernel(DsArgs a) {
+  if (a.t0 && threadIdx.x == 0) atomicMin(a.t0, (unsigned long long)wall_clock64());
   ds_fast_jobs<Px, W, H, SUB>(a);
+  if (a.t1) {
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(a.t1, (unsigned long long)wall_clock64());
+  }
 }
 template <typename Px, int W, int H, bool SUB>
 __global__ __launch_bounds__(kDsThreads) void ds_fast_kernel_occ4(DsArgs a) {
@@ -1542,7 +1551,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             rv_fs_result *d_out, uint32_t *d_evals, const ChainNext *next,
                             void *stream, const uint8_t *active, const int32_t *alist,
                             const int32_t *acount, int lper, const uint8_t *dirty,
-                            int list_grid, uint32_t *eval_acc) {
+                            int list_grid, uint32_t *eval_acc, unsigned long long *t01) {
   auto p2 = [](int v) { return v >= 4 && v <= 128 && (v & (v - 1)) == 0; };
   if (!org || !refs || n_refs < 1 || n_refs > RV_MAX_REFS || n_per_ref < 0 || !p2(blk_w) ||
       !p2(blk_h) || (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) ||
@@ -1575,6 +1584,10 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
   a.dirty = alist ? dirty : nullptr;
   a.list_grid = list_grid;
   a.eval_acc = eval_acc;
+  if (t01) {
+    a.t0 = t01;
+    a.t1 = t01 + 1;
+  }
   if (alist && (!acount || lper < 0 || use_satd ||
                 !((blk_w == 64 && blk_h == 64) || (blk_w == 16 && blk_h == 16 && !subpixel))))
     return rv_set_error(RV_EINVAL,
@@ -1665,7 +1678,7 @@ extern "C" int rv_diamond_search_batch(const rv_plane *org, const rv_plane *ref,
   if (!ref) return rv_set_error(RV_EINVAL, "rv_diamond_search_batch: null ref");
   return rv_diamond_search_multi(org, ref, 1, d_jobs, n, blk_w, blk_h, subpixel, use_satd,
                                  allow_hp, bit_depth, d_out, nullptr, nullptr, stream, nullptr,
-                                 nullptr, nullptr, 0, nullptr, 0, nullptr);
+                                 nullptr, nullptr, 0, nullptr, 0, nullptr, nullptr);
 }
 
 // telescopic_subpel_search (src/me.rs:858-941) for every job in one launch:

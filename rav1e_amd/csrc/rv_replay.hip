@@ -70,7 +70,7 @@ int rv_diamond_search_multi(const rv_plane *org, const rv_plane *refs, int n_ref
                             void *stream, const uint8_t *active = nullptr,
                             const int32_t *alist = nullptr, const int32_t *acount = nullptr,
                             int lper = 1, const uint8_t *dirty = nullptr, int list_grid = 0,
-                            uint32_t *eval_acc = nullptr);
+                            uint32_t *eval_acc = nullptr, unsigned long long *t01 = nullptr);
 int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_job *jobs_h,
                      rv_fs_result *out_h, const uint8_t *dirty_h, const rv_plane *org,
                      const rv_plane *refs, const rv_ds_job *jobs, rv_fs_result *out,
@@ -1038,6 +1038,7 @@ struct RvLaEngine {
     rv_replay_frame_info fi{};
     LaRefs lr{};
     hipEvent_t ev_imp = nullptr, ev_used = nullptr;
+    hipEvent_t ev_data = nullptr, ev_xchg = nullptr;  // RCCL parts: data in / exchanged
   };
   std::vector<Entry> ring;
   std::vector<long> pyr_display;  // per input: the display whose pyramid it holds
@@ -1054,10 +1055,17 @@ struct RvLaEngine {
   long la_round_sum = 0, la_reeval = 0, la_frames = 0;  // under mu
   // several tile groups (rv_replay_set_la_exchange): every group's part of
   // each frame's importance data reaches every group, over RCCL (comm, the
-  // part buffers psend / precv, pbytes per group) or an in-process hub
+  // part buffers psend / precv, pbytes per group) or an in-process hub.
+  // RCCL: the all-gathers run on the encode's stream with the reconstruction
+  // all-gathers, one communicator and one stream per rank, so every rank
+  // issues its collectives in the same order on one queue (la_encode_
+  // exchange; two communicators on streams sharing hardware queues can
+  // deadlock across ranks).  The engine posts a frame's data (data_ready,
+  // ev_data) and waits for its exchange (xchg_done, ev_xchg).
   void *comm = nullptr;
   uint8_t *psend = nullptr, *precv = nullptr;
   size_t pbytes = 0;
+  long data_ready = 0, xchg_done = 0, xchg_next = 1;
   rv_la_hub *hub = nullptr;
   int hub_k = -1;
   std::vector<hipEvent_t> hub_ev;  // this member's hub events (destroyed with the engine)
@@ -1238,8 +1246,12 @@ struct rv_replay {
   static constexpr int kKp = 512;
   std::vector<hipEvent_t> kp_ev;
   long kp_n = 0, kp_done = 0, kp_base = 0;  // pairs recorded / harvested / at the last start
-  double kp_ms = 0.0;
+  double kp_ms = 0.0, kp_dev_ms = 0.0;
   uint32_t *kp_cnt = nullptr;  // device [2]: evaluations, jobs
+  // ... and each launch's span on the device clock: [kKp][2] (first
+  // workgroup's start, last one's end), harvested with the events
+  unsigned long long *kp_ts = nullptr;
+  double kp_tick_ms = 0.0;  // ms per wall_clock64 tick
 };
 
 namespace {
@@ -1258,8 +1270,11 @@ hipError_t kp_harvest(rv_replay *r, long upto) {
     hipError_t e = hipEventSynchronize(r->kp_ev[i + 1]);
     float ms = 0.f;
     if (e == hipSuccess) e = hipEventElapsedTime(&ms, r->kp_ev[i], r->kp_ev[i + 1]);
+    unsigned long long t[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpy(t, r->kp_ts + i, sizeof(t), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return e;
     r->kp_ms += ms;
+    if (t[1] > t[0]) r->kp_dev_ms += (double)(t[1] - t[0]) * r->kp_tick_ms;
   }
   return hipSuccess;
 }
@@ -2744,20 +2759,19 @@ static int la_exchange(rv_replay *r, long m, RvLaEngine::Entry &e, int R, hipStr
     return RV_OK;
   }
   auto rect = [&](int j) { return r->grects + 4 * j; };
-  if (E.comm) {
-#if RV_HAVE_RCCL
-    const int32_t *me = rect(r->my_group);
-    RV_R(impwin_part(e.f, R, me[0], me[1], me[2], me[3], g.w_imp, g.h_imp, E.psend, false, xs));
-    if (ncclAllGather(E.psend, E.precv, E.pbytes, ncclUint8, (ncclComm_t)E.comm, xs) != ncclSuccess)
-      return rv_set_error(RV_EHIP, "la_exchange: ncclAllGather");
-    for (int j = 0; j < ng; j++)
-      if (j != r->my_group)
-        RV_R(impwin_part(e.f, R, rect(j)[0], rect(j)[1], rect(j)[2], rect(j)[3], g.w_imp, g.h_imp,
-                         E.precv + (size_t)j * E.pbytes, true, xs));
+  (void)R;
+  if (E.comm) {  // the encode thread all-gathers (la_encode_exchange)
+    RV_H(hipEventRecord(e.ev_data, xs));
+    std::unique_lock<std::mutex> lk(E.mu);
+    E.data_ready = m;
+    E.cv.notify_all();
+    if (!E.cv.wait_for(lk, std::chrono::seconds(kEngineWaitS),
+                       [&] { return E.stop || E.xchg_done >= m; }))
+      return rv_set_error(RV_EHIP, "la_exchange: the frame's parts were never all-gathered");
+    if (E.stop) return rv_set_error(RV_EINVAL, "la_exchange: stopped");
+    lk.unlock();
+    RV_H(hipStreamWaitEvent(xs, e.ev_xchg, 0));
     return RV_OK;
-#else
-    return rv_set_error(RV_EINVAL, "la_exchange: built without RCCL");
-#endif
   }
   rv_la_hub *h = E.hub;
   if (!h || h->n != ng)
@@ -2904,7 +2918,10 @@ static void la_thread_main(rv_replay *r) {
         // frame m reads the inputs of displays <= 4 ((m - 1) / 4) + 4
         // (frame_info): with them in place it may run before frame m - W
         // is asked for, as rav1e computes a frame's lookahead on arrival
-        if (E.requested < 1) return false;
+        // not before the first frame is asked for -- or the inputs are declared
+        // in place (tile groups coded one after another in one process need
+        // every group's engine running: their parts meet in the hub)
+        if (E.requested < 1 && E.inputs_ready == 0) return false;
         if (m > E.requested + E.W && 4 * ((m - 1) / 4) + 4 >= E.inputs_ready) return false;
         if (E.limit > 0 && m >= E.limit) return false;
         return m - E.RW < 1 || E.at(m).used_by == m - E.RW;
@@ -2934,15 +2951,70 @@ static void la_engine_destroy(rv_replay *r) {
   }
   if (E->th.joinable()) E->th.join();
   if (E->las) (void)hipStreamSynchronize(E->las);
-  for (auto &en : E->ring) {
-    if (en.ev_imp) (void)hipEventDestroy(en.ev_imp);
-    if (en.ev_used) (void)hipEventDestroy(en.ev_used);
-  }
+  for (auto &en : E->ring)
+    for (hipEvent_t ev : {en.ev_imp, en.ev_used, en.ev_data, en.ev_xchg})
+      if (ev) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : E->hub_ev)
     if (ev) (void)hipEventDestroy(ev);
   if (E->rr.h_pub) (void)hipHostFree(E->rr.h_pub);
   if (E->las) (void)hipStreamDestroy(E->las);
   delete E;  // its device arrays are the replay's allocations (freed with it)
+}
+
+// Tile groups over RCCL: before frame n takes its importances, the encode
+// thread all-gathers the lookahead parts of every frame up to n + W (the
+// window's end) on its own stream, with the same communicator as the
+// reconstruction all-gathers -- each rank issues the same collectives in
+// the same order on one stream: [parts 1 .. W + 1], frame 1, recon 1,
+// [part W + 2], frame 2, ...
+static int la_encode_exchange(rv_replay *r, long n, hipStream_t st) {
+  RvLaEngine &E = *r->eng;
+  if (!E.comm) return RV_OK;
+  if (!r->eng_owned)
+    return rv_set_error(RV_EINVAL, "rv_replay_frame: RCCL lookahead parts on the primary only");
+#if RV_HAVE_RCCL
+  const Geo &g = r->g;
+  long last = n + E.W;
+  if (E.limit > 0 && last > E.limit - 1) last = E.limit - 1;
+  {
+    std::lock_guard<std::mutex> lk(E.mu);
+    if (n > E.requested) E.requested = n;  // the engine runs up to n + W
+    E.cv.notify_all();
+  }
+  for (long m = E.xchg_next; m <= last; m++) {
+    {
+      std::unique_lock<std::mutex> lk(E.mu);
+      if (!E.cv.wait_for(lk, std::chrono::seconds(kEngineWaitS),
+                         [&] { return E.err != 0 || E.data_ready >= m; }))
+        return rv_set_error(RV_EHIP, "rv_replay_frame: the lookahead engine's part never came");
+      if (E.err) return rv_set_error(E.err, E.msg.c_str());
+    }
+    RvLaEngine::Entry &e = E.at(m);
+    if (e.m != m) return rv_set_error(RV_EINVAL, "rv_replay_frame: the lookahead ring lost a frame");
+    const int R = e.lr.n;
+    const int32_t *me = r->grects + 4 * r->my_group;
+    RV_H(hipStreamWaitEvent(st, e.ev_data, 0));
+    RV_R(impwin_part(e.f, R, me[0], me[1], me[2], me[3], g.w_imp, g.h_imp, E.psend, false, st));
+    if (ncclAllGather(E.psend, E.precv, E.pbytes, ncclUint8, (ncclComm_t)E.comm, st) != ncclSuccess)
+      return rv_set_error(RV_EHIP, "rv_replay_frame: ncclAllGather (lookahead parts)");
+    for (int j = 0; j < r->n_groups; j++) {
+      if (j == r->my_group) continue;
+      const int32_t *q = r->grects + 4 * j;
+      RV_R(impwin_part(e.f, R, q[0], q[1], q[2], q[3], g.w_imp, g.h_imp,
+                       E.precv + (size_t)j * E.pbytes, true, st));
+    }
+    RV_H(hipEventRecord(e.ev_xchg, st));
+    std::lock_guard<std::mutex> lk(E.mu);
+    E.xchg_done = m;
+    E.xchg_next = m + 1;
+    E.cv.notify_all();
+  }
+  return RV_OK;
+#else
+  (void)n;
+  (void)st;
+  return rv_set_error(RV_EINVAL, "rv_replay_frame: built without RCCL");
+#endif
 }
 
 // The encode side: wait for frame n's importances, take its lookahead.
@@ -3055,7 +3127,9 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
     uint8_t *m = (uint8_t *)dalloc(r, ob + impwin_frame_bytes(ni, r->RA));
     ok = m && hipMemsetAsync(m, 0, ob, r->stream) == hipSuccess &&
          hipEventCreateWithFlags(&en.ev_imp, hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&en.ev_used, hipEventDisableTiming) == hipSuccess;
+         hipEventCreateWithFlags(&en.ev_used, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&en.ev_data, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&en.ev_xchg, hipEventDisableTiming) == hipSuccess;
     if (!ok) break;
     en.o.coarse = (rv_fs_result *)m;
     en.o.half_l = en.o.coarse + nr;
@@ -3234,8 +3308,15 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   auto kp_open = [&](hipStream_t xs) -> int {
     if (!kp) return RV_OK;
     if (r->kp_n - r->kp_done >= rv_replay::kKp) RV_H(kp_harvest(r, r->kp_n - rv_replay::kKp + 1));
+    // the launch's device-clock span slot: start = max, end = 0
+    static const unsigned long long init[2] = {~0ull, 0ull};
+    RV_H(hipMemcpyAsync(r->kp_ts + 2 * (size_t)(r->kp_n % rv_replay::kKp), init, sizeof(init),
+                        hipMemcpyHostToDevice, xs));
     RV_H(hipEventRecord(r->kp_ev[2 * (size_t)(r->kp_n % rv_replay::kKp)], xs));
     return RV_OK;
+  };
+  auto kp_ts = [&]() -> unsigned long long * {
+    return kp ? r->kp_ts + 2 * (size_t)(r->kp_n % rv_replay::kKp) : nullptr;
   };
   auto kp_close = [&](hipStream_t xs) -> int {
     if (!kp) return RV_OK;
@@ -3247,6 +3328,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // window the engine's, run W frames ahead, and the window's importances
   const float *imp = r->imp;
   if (r->eng) {
+    RV_R(la_encode_exchange(r, r->coded, st));
     RV_R(la_engine_take(r, r->coded, st, &imp));
     if (tm)  // F0 .. FL ran on the engine: empty stages here
       for (int i : {1, 2, 3, rv_replay::kStageEv, rv_replay::kStageEv + 1})
@@ -3613,7 +3695,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     RV_R(kp_open(st));
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1,
                                  r->s6 ? 1 : 0, 0, g.bd, r->sub, ev_sub, nullptr, st, act, nullptr,
-                                 nullptr, 1, nullptr, 0, kp_acc));
+                                 nullptr, 1, nullptr, 0, kp_acc, kp_ts()));
     RV_R(kp_close(st));
     if (r->lvl && !edge && !lv_early) RV_R(lv_me(st));
     // the valid candidates (a few microseconds; bracketed with F3 sub-pel;
@@ -3691,7 +3773,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     RV_R(kp_open(xs));
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
                                  r->sub, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 1,
-                                 ma.f3dirty, lg, kp_acc));
+                                 ma.f3dirty, lg, kp_acc, kp_ts()));
     RV_R(kp_close(xs));
     round_lists_kernel<<<kRoundGrid, 256, 0, xs>>>(
         cg, r->sub, nsingle, r->cand_list, r->cand_count, r->mv_list, acnt,
@@ -4156,7 +4238,13 @@ int rv_replay_set_kernel_probe(rv_replay *r, int on) {
     r->kp_ev.assign(2 * rv_replay::kKp, nullptr);
     for (auto &ev : r->kp_ev) RV_H(hipEventCreate(&ev));
     r->kp_cnt = (uint32_t *)dalloc(r, 2 * sizeof(uint32_t));
-    if (!r->kp_cnt) return rv_set_error(RV_EHIP, "rv_replay_set_kernel_probe: allocation failed");
+    r->kp_ts = (unsigned long long *)dalloc(r, 2 * sizeof(unsigned long long) * rv_replay::kKp);
+    if (!r->kp_cnt || !r->kp_ts)
+      return rv_set_error(RV_EHIP, "rv_replay_set_kernel_probe: allocation failed");
+    int dev = 0, khz = 0;
+    RV_H(hipGetDevice(&dev));
+    RV_H(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    r->kp_tick_ms = khz > 0 ? 1.0 / (double)khz : 0.0;
   }
   if (!r->kp_ev.empty()) {
     RV_H(kp_harvest(r, r->kp_n));
@@ -4165,6 +4253,7 @@ int rv_replay_set_kernel_probe(rv_replay *r, int on) {
     RV_H(hipDeviceSynchronize());
   }
   r->kp_ms = 0.0;
+  r->kp_dev_ms = 0.0;
   r->kp_base = r->kp_n;
   r->kprobe = on != 0;
   return RV_OK;
@@ -4174,8 +4263,9 @@ int rv_replay_set_kernel_probe(rv_replay *r, int on) {
 // streams), [2] candidate evaluations, [3] jobs, since the probe started
 int rv_replay_kernel_probe(rv_replay *r, double *out, int cap) {
   if (!r || !out || cap < 4) return rv_set_error(RV_EINVAL, "rv_replay_kernel_probe: null / cap");
-  for (int i = 0; i < 4; i++) out[i] = 0.0;
-  if (r->kp_ev.empty()) return 4;
+  const int nout = cap < 5 ? 4 : 5;
+  for (int i = 0; i < nout; i++) out[i] = 0.0;
+  if (r->kp_ev.empty()) return nout;
   RV_H(kp_harvest(r, r->kp_n));
   uint32_t c[2] = {0, 0};
   RV_H(hipDeviceSynchronize());
@@ -4184,7 +4274,8 @@ int rv_replay_kernel_probe(rv_replay *r, double *out, int cap) {
   out[1] = r->kp_ms;
   out[2] = (double)c[0];
   out[3] = (double)c[1];
-  return 4;
+  if (nout > 4) out[4] = r->kp_dev_ms;
+  return nout;
 }
 // Candidate evaluations summed over the last min(frames, 64) coded frames:
 // out[0] F3 full-pel diamond, out[1] F3 sub-pel diamond (64x64 jobs), out[2]

@@ -102,9 +102,14 @@ class TileParallel:
         self.world = len(self.rects)
         self.host = not hasattr(engine, "set_groups")
         if self.world > 1 and not self.host:
-            engine.set_groups(self.rects, my, comm.h if comm else None)
             if comm is None:
                 raise ValueError("a GPU engine in a multi-rank run needs an RCCL communicator")
+            engine.set_groups(self.rects, my, comm.h)
+            if getattr(engine, "imp_window", 0):
+                # the importance window: every group's lookahead part is
+                # all-gathered with the same communicator, on the encode's
+                # stream, before the frames whose window needs it
+                engine.set_la_exchange(comm=comm.h)
         if self.host:
             self.size = max(engine.region_bytes(r) for r in self.rects)
 

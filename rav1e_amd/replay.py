@@ -437,10 +437,11 @@ class HipReplay:
                "rv_replay_set_kernel_probe")
 
     def kernel_probe(self) -> np.ndarray:
-        """[launches, summed ms, candidate evaluations, jobs] of the probed
-        F3 sub-pel launches since the probe started."""
-        out = np.zeros(4, np.float64)
-        _check(lib().rv_replay_kernel_probe(self.h, out.ctypes.data, 4) - 4,
+        """[launches, summed ms (HIP event pairs), candidate evaluations,
+        jobs, summed ms (device clock spans)] of the probed F3 sub-pel
+        launches since the probe started."""
+        out = np.zeros(5, np.float64)
+        _check(lib().rv_replay_kernel_probe(self.h, out.ctypes.data, 5) - 5,
                "rv_replay_kernel_probe")
         return out
 
@@ -854,7 +855,7 @@ class PipelinedReplay:
 
     def kernel_probe(self) -> np.ndarray:
         self.drain()
-        return sum((t.kernel_probe() for t in self.inst), np.zeros(4))
+        return sum((t.kernel_probe() for t in self.inst), np.zeros(5))
 
     def stage_ms_sum_frames(self, frames) -> tuple:
         """Stage times summed over the instrumented inter frames `frames`
