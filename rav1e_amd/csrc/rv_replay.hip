@@ -1185,6 +1185,7 @@ struct rv_replay {
   long mv_frames = 0;  // the frames this instance coded with the rounds (a twin codes some)
   size_t nwords = 0, wpart = 0;   // result words; offset of the partition masks
   bool jobs_built = false;
+  std::mutex jobs_mu;  // ensure_jobs: the encode and the lookahead engine may both need them
   std::vector<RvSlot> slots;
   std::vector<RvInput> inputs;
   std::vector<void *> allocs;
@@ -1536,6 +1537,16 @@ int build_static_jobs(rv_replay *r) {
   }
   r->jobs_built = true;
   return RV_OK;
+}
+
+// The static job records, built once: the first coded frame, or the
+// lookahead engine when it starts before any frame (inputs declared ready).
+int ensure_jobs(rv_replay *r) {
+  std::lock_guard<std::mutex> lk(r->jobs_mu);
+  if (r->jobs_built) return RV_OK;
+  if (!r->lv[0].set || !r->lv[1].set || !r->lv[2].set)
+    return rv_set_error(RV_EINVAL, "rv_replay: level params not set");
+  return build_static_jobs(r);
 }
 
 // Packed rectangles of group k (its visible Y, U, V region; with
@@ -2929,6 +2940,7 @@ static void la_thread_main(rv_replay *r) {
       if (E.stop) return;
     }
     int rc = E.las ? RV_OK : la_stream_create(&E);
+    if (rc == RV_OK) rc = ensure_jobs(r);  // (the engine may start before the first frame)
     if (rc == RV_OK) rc = la_step(r, m);
     if (rc != RV_OK) {
       std::lock_guard<std::mutex> lk(E.mu);
@@ -3073,6 +3085,8 @@ int rv_replay_set_inputs_ready(rv_replay *r, long displays) {
   if (displays > (long)r->inputs.size())
     return rv_set_error(RV_EINVAL, "rv_replay_set_inputs_ready: more displays than input slots");
   if (r->eng) {
+    // the engine may start now, before any frame: its job records first
+    RV_R(ensure_jobs(r));
     std::lock_guard<std::mutex> lk(r->eng->mu);
     r->eng->inputs_ready = displays;
     r->eng->cv.notify_all();
@@ -3265,7 +3279,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   auto us = [&](hclock::time_point a, hclock::time_point b) {
     return (long)std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
   };
-  if (!r->jobs_built) RV_R(build_static_jobs(r));
+  RV_R(ensure_jobs(r));
   const rv_replay::Level &L = r->lv[fi.level];
   const int lv = fi.level;
   CandGeo cg = r->cg;

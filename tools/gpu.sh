@@ -44,7 +44,8 @@ case "$MODE" in
       "200 $TAG/fetch.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o run -- $B" \
       "200 $TAG/write.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $P/write -o run -- $B" \
       "200 $TAG/sq.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $SQ -d $P/sq -o run -- $B" \
-      "120 $TAG/gzip.log find $P -type f -size +256k ! -name '*.gz' -exec gzip -9 {} +" ;;
+      "120 $TAG/summary.log python3 $R/tools/prof_json.py $P $P/prof_$CFG.json --frames ${FRAMES:-101} --bench $P/trace.log --md $P/prof_$CFG.md" \
+      "60 $TAG/slim.log $R/tools/slim_prof.sh $P" ;;
   trace)
     # kernel trace only: trace TAG CFG [ARGS]
     CFG=${1:-2160p}; shift
