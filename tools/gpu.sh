@@ -3,6 +3,7 @@
 #
 #   tools/gpu.sh suite TAG            -m gpu suite in one process, smoke(), default bench
 #   tools/gpu.sh tests TAG 'EXPR'     pytest -m gpu -k EXPR
+#   tools/gpu.sh testbench TAG 'EXPR' CFG...  those tests, then a bench line per config
 #   tools/gpu.sh bench TAG CFG... [-- ARGS]   one bench line per config (ARGS to each)
 #   tools/gpu.sh prof TAG CFG [ARGS]  kernel trace + FETCH / WRITE / SQ PMC passes of the
 #                                     bench run of CFG (default steps; one rocprofv3 pass each, the
@@ -29,6 +30,13 @@ case "$MODE" in
       "400 $TAG/bench_default.log python $R/bench.py" ;;
   tests)
     exec bash "$R/tools/gpu_step.sh" "900 $TAG/pytest_k.log $PYT -v -k '$1'" ;;
+  testbench)
+    # testbench TAG 'EXPR' CFG...: the selected tests, then one bench line per
+    # config, in one step chain (a crash stops it; a test failure does not)
+    expr=$1; shift
+    steps=("900 $TAG/pytest_k.log $PYT -v -k '$expr'")
+    for c in "$@"; do steps+=("400 $TAG/bench_$c.log python $R/bench.py --config $c"); done
+    exec bash "$R/tools/gpu_step.sh" "${steps[@]}" ;;
   bench)
     cfgs=(); while [ $# -gt 0 ] && [ "$1" != "--" ]; do cfgs+=("$1"); shift; done
     [ "$1" = "--" ] && shift
