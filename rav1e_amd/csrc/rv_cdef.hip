@@ -29,6 +29,13 @@ struct CdefArgs {
   int pw, ph, xdec, ydec, pli, cols8, rows8, mi_stride, fb_w, damping, bd;
   uint8_t ystr[8], uvstr[8];
 };
+// the filter of up to three planes in one launch: plane p owns the 64x4
+// tiles [blk[p], blk[p + 1]), tx[p] of them per row
+struct CdefPlanes {
+  CdefArgs pl[3];
+  unsigned blk[4];
+  int tx[3];
+};
 
 template <typename T>
 __device__ __forceinline__ int cdef_px(const rv_plane &p, int pw, int ph, int x, int y) {
@@ -143,9 +150,12 @@ __constant__ int8_t kCdefDirs[8][2][2] = {
     {{1, 1}, {2, 2}},   {{1, 0}, {2, 1}},  {{1, 0}, {2, 0}},  {{1, 0}, {2, -1}}};
 
 template <typename T>
-__global__ __launch_bounds__(256) void cdef_filter_kernel(CdefArgs a) {
-  const int x = blockIdx.x * 64 + threadIdx.x;
-  const int y = blockIdx.y * 4 + threadIdx.y;
+__global__ __launch_bounds__(256) void cdef_filter_kernel(CdefPlanes P) {
+  const int pi = blockIdx.x >= P.blk[1] ? (blockIdx.x >= P.blk[2] ? 2 : 1) : 0;
+  const CdefArgs &a = P.pl[pi];
+  const int t = (int)(blockIdx.x - P.blk[pi]), ty = t / P.tx[pi];
+  const int x = (t - ty * P.tx[pi]) * 64 + threadIdx.x;
+  const int y = ty * 4 + threadIdx.y;
   if (x >= a.pw || y >= a.ph) return;
   const int bx = (x << a.xdec) >> 3, by = (y << a.ydec) >> 3;
   const int px = cdef_px<T>(a.src, a.pw, a.ph, x, y);
@@ -237,21 +247,19 @@ extern "C" int rv_cdef_find_dirs(const rv_plane *luma, int width, int height,
   return RV_OK;
 }
 
-// cdef_filter_superblock over every superblock of plane pli (src/cdef.rs:
-// 411-534 via cdef_filter_frame :614-640), src -> dst (distinct planes).
-extern "C" int rv_cdef_filter_plane(const rv_plane *src, const rv_plane *dst, int pli, int width,
-                                    int height, const uint8_t *d_skip, int mi_stride,
-                                    const uint8_t *d_dir, const int32_t *d_var,
-                                    const uint8_t *d_cdef_index, const uint8_t *y_strengths,
-                                    const uint8_t *uv_strengths, int damping, int bit_depth,
-                                    void *stream) {
+// The arguments of cdef_filter_superblock over plane pli (cdef_bits <= 3).
+static int cdef_plane_args(CdefArgs &a, const rv_plane *src, const rv_plane *dst, int pli,
+                           int width, int height, const uint8_t *d_skip, int mi_stride,
+                           const uint8_t *d_dir, const int32_t *d_var, const uint8_t *d_cdef_index,
+                           const uint8_t *y_strengths, const uint8_t *uv_strengths, int damping,
+                           int bit_depth) {
   if (!src || !dst || !d_skip || !d_dir || !d_var || !d_cdef_index || !y_strengths ||
       !uv_strengths || pli < 0 || pli > 2 || width <= 0 || height <= 0 || (width & 7) ||
       (height & 7) || damping < 0 ||
       mi_stride < 2 * ((width + 7) / 8) || !cdef_bd_ok(src, bit_depth) || dst->hbd != src->hbd ||
       src->data == dst->data)
     return rv_set_error(RV_EINVAL, "rv_cdef_filter_plane: bad arguments");
-  CdefArgs a = {};
+  a = CdefArgs{};
   a.src = *src;
   a.dst = *dst;
   a.xdec = pli ? src->xdec : 0;
@@ -280,12 +288,56 @@ extern "C" int rv_cdef_filter_plane(const rv_plane *src, const rv_plane *dst, in
     a.ystr[k] = y_strengths[k];
     a.uvstr[k] = uv_strengths[k];
   }
-  const dim3 grid((unsigned)((a.pw + 63) / 64), (unsigned)((a.ph + 3) / 4)), block(64, 4);
-  hipStream_t s = rv_resolve_stream(stream);
-  if (src->hbd)
-    cdef_filter_kernel<uint16_t><<<grid, block, 0, s>>>(a);
+  return RV_OK;
+}
+
+static void cdef_filter_launch(CdefPlanes &P, int np, hipStream_t s) {
+  unsigned blocks = 0;
+  for (int p = 0; p < np; p++) {
+    P.tx[p] = (P.pl[p].pw + 63) / 64;
+    P.blk[p] = blocks;
+    blocks += (unsigned)(P.tx[p] * ((P.pl[p].ph + 3) / 4));
+  }
+  for (int p = np; p < 4; p++) P.blk[p] = blocks;
+  const dim3 block(64, 4);
+  if (P.pl[0].src.hbd)
+    cdef_filter_kernel<uint16_t><<<blocks, block, 0, s>>>(P);
   else
-    cdef_filter_kernel<uint8_t><<<grid, block, 0, s>>>(a);
+    cdef_filter_kernel<uint8_t><<<blocks, block, 0, s>>>(P);
+}
+
+// cdef_filter_superblock over every superblock of plane pli (src/cdef.rs:
+// 411-534 via cdef_filter_frame :614-640), src -> dst (distinct planes).
+extern "C" int rv_cdef_filter_plane(const rv_plane *src, const rv_plane *dst, int pli, int width,
+                                    int height, const uint8_t *d_skip, int mi_stride,
+                                    const uint8_t *d_dir, const int32_t *d_var,
+                                    const uint8_t *d_cdef_index, const uint8_t *y_strengths,
+                                    const uint8_t *uv_strengths, int damping, int bit_depth,
+                                    void *stream) {
+  CdefPlanes P = {};
+  const int e = cdef_plane_args(P.pl[0], src, dst, pli, width, height, d_skip, mi_stride, d_dir,
+                                d_var, d_cdef_index, y_strengths, uv_strengths, damping, bit_depth);
+  if (e != RV_OK) return e;
+  cdef_filter_launch(P, 1, rv_resolve_stream(stream));
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+// cdef_filter_frame's filter pass over the three planes (src/cdef.rs:
+// 614-640) in one launch, src[p] -> dst[p].
+int rv_cdef_filter_frame_dev(const rv_plane src[3], const rv_plane dst[3], int width, int height,
+                             const uint8_t *d_skip, int mi_stride, const uint8_t *d_dir,
+                             const int32_t *d_var, const uint8_t *d_cdef_index,
+                             const uint8_t *y_strengths, const uint8_t *uv_strengths, int damping,
+                             int bit_depth, hipStream_t s) {
+  CdefPlanes P = {};
+  for (int p = 0; p < 3; p++) {
+    const int e = cdef_plane_args(P.pl[p], &src[p], &dst[p], p, width, height, d_skip, mi_stride,
+                                  d_dir, d_var, d_cdef_index, y_strengths, uv_strengths, damping,
+                                  bit_depth);
+    if (e != RV_OK) return e;
+  }
+  cdef_filter_launch(P, 3, s);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

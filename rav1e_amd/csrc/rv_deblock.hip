@@ -19,6 +19,12 @@ struct DbArgs {
   const uint8_t *dlev;  // null: `level`; else the device levels [Y v, Y h, U, V]
   int mi_stride, cols, rows, xdec, ydec, pli, level, bd, vert;
 };
+// one pass (vertical or horizontal edges) over up to three planes in one
+// launch: plane p owns workgroups [blk[p], blk[p + 1])
+struct DbPlanes {
+  DbArgs pl[3];
+  unsigned blk[4];
+};
 
 __device__ __forceinline__ int db_abs(int v) { return v < 0 ? -v : v; }
 __device__ __forceinline__ int db_max(int a, int b) { return a > b ? a : b; }
@@ -145,8 +151,10 @@ __device__ __forceinline__ void db_apply(const DbArgs &a, int ox, int oy, int k,
 
 // thread = (edge segment, pixel row / column k of its 4)
 template <typename Px>
-__global__ __launch_bounds__(256) void deblock_kernel(DbArgs a) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(256) void deblock_kernel(DbPlanes P) {
+  const int pi = blockIdx.x >= P.blk[1] ? (blockIdx.x >= P.blk[2] ? 2 : 1) : 0;
+  const DbArgs &a = P.pl[pi];
+  const int i = (blockIdx.x - P.blk[pi]) * 256 + threadIdx.x;
   const int k = i & 3, seg = i >> 2;
   const int sx = a.vert ? (a.cols >> a.xdec) - 1 : (a.cols >> a.xdec);  // segments per row
   const int sy = a.vert ? (a.rows >> a.ydec) : (a.rows >> a.ydec) - 1;
@@ -418,41 +426,65 @@ int rv_deblock_sse_dev(const rv_plane rec[3], const rv_plane src[3], int width, 
   return RV_OK;
 }
 
-// deblock_filter_frame with the levels in device memory (the frame is
-// filtered only when a luma level is non-zero, src/encoder.rs:2790-2793):
-// every plane's two passes are launched, each lane reads its level
-int rv_deblock_frame_dev(const rv_plane planes[3], int width, int height, const uint8_t *d_lg,
-                         const uint8_t *d_skip, int mi_stride, const uint8_t *d_levels,
-                         int bit_depth, hipStream_t s) {
-  for (int pli = 0; pli < 3; pli++) {
-    const rv_plane *p = &planes[pli];
-    DbArgs a;
+// One pass of the deblocking over planes pl[0 .. np) in one launch (the
+// passes of different planes touch different memory).  levels: the host
+// levels [Y v, Y h, U, V] (a plane whose level is 0 is left out), or null
+// with d_levels the device ones (every lane reads its level).
+static int deblock_pass(const rv_plane *planes, const int *pli, int np, int width, int height,
+                        const uint8_t *d_lg, const uint8_t *d_skip, int mi_stride,
+                        const uint8_t *levels, const uint8_t *d_levels, int bit_depth, bool vert,
+                        hipStream_t s) {
+  DbPlanes P = {};
+  unsigned blocks = 0;
+  int k = 0;
+  for (int j = 0; j < np; j++) {
+    const rv_plane *p = &planes[j];
+    DbArgs &a = P.pl[k];
     a.p = *p;
     a.lg = d_lg;
     a.skip = d_skip;
-    a.dlev = d_levels;
+    a.dlev = levels ? nullptr : d_levels;
     a.mi_stride = mi_stride;
     a.xdec = p->xdec;
     a.ydec = p->ydec;
     a.cols = ((((width + 3) >> 2) + ((1 << a.xdec) >> 1)) >> a.xdec) << a.xdec;
     a.rows = ((((height + 3) >> 2) + ((1 << a.ydec) >> 1)) >> a.ydec) << a.ydec;
-    a.pli = pli;
+    a.pli = pli[j];
     a.bd = bit_depth;
-    a.level = 0;
-    for (int pass = 0; pass < 2; pass++) {
-      a.vert = pass == 0;
-      const int sx = a.vert ? (a.cols >> a.xdec) - 1 : (a.cols >> a.xdec);
-      const int sy = a.vert ? (a.rows >> a.ydec) : (a.rows >> a.ydec) - 1;
-      const int64_t n = (int64_t)(sx > 0 ? sx : 0) * (sy > 0 ? sy : 0) * 4;
-      if (n == 0) continue;
-      const unsigned grid = (unsigned)((n + 255) / 256);
-      if (p->hbd)
-        deblock_kernel<uint16_t><<<grid, 256, 0, s>>>(a);
-      else
-        deblock_kernel<uint8_t><<<grid, 256, 0, s>>>(a);
-    }
+    a.vert = vert;
+    a.level = levels ? (a.pli == 0 ? levels[vert ? 0 : 1] : levels[a.pli + 1]) : 0;
+    if (levels && a.level == 0) continue;
+    const int sx = vert ? (a.cols >> a.xdec) - 1 : (a.cols >> a.xdec);
+    const int sy = vert ? (a.rows >> a.ydec) : (a.rows >> a.ydec) - 1;
+    const int64_t n = (int64_t)(sx > 0 ? sx : 0) * (sy > 0 ? sy : 0) * 4;
+    if (n == 0) continue;
+    P.blk[k] = blocks;
+    blocks += (unsigned)((n + 255) / 256);
+    k++;
   }
+  for (int j = k; j < 4; j++) P.blk[j] = blocks;
+  if (!blocks) return RV_OK;
+  if (planes[0].hbd)
+    deblock_kernel<uint16_t><<<blocks, 256, 0, s>>>(P);
+  else
+    deblock_kernel<uint8_t><<<blocks, 256, 0, s>>>(P);
   RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+// deblock_filter_frame (src/deblock.rs:1337-1345 via src/encoder.rs:
+// 2789-2793) of a frame's three planes: all vertical edges, then all
+// horizontal ones, each pass one launch over the planes.  d_levels: the
+// device levels (sse_optimize's; nothing is filtered unless a luma level is
+// non-zero, every lane reads its level) or, with levels, the host ones.
+int rv_deblock_frame_dev(const rv_plane planes[3], int width, int height, const uint8_t *d_lg,
+                         const uint8_t *d_skip, int mi_stride, const uint8_t *d_levels,
+                         int bit_depth, hipStream_t s, const uint8_t *levels) {
+  static const int pli[3] = {0, 1, 2};
+  for (int pass = 0; pass < 2; pass++)
+    if (const int e = deblock_pass(planes, pli, 3, width, height, d_lg, d_skip, mi_stride, levels,
+                                   d_levels, bit_depth, pass == 0, s))
+      return e;
   return RV_OK;
 }
 
@@ -463,34 +495,10 @@ int rv_deblock_frame_dev(const rv_plane planes[3], int width, int height, const 
 int rv_deblock_plane_dev(const rv_plane *p, int pli, int width, int height, const uint8_t *d_lg,
                          const uint8_t *d_skip, int mi_stride, const uint8_t levels[4],
                          int bit_depth, hipStream_t s) {
-  if (pli == 0 ? (levels[0] == 0 && levels[1] == 0) : levels[pli + 1] == 0) return RV_OK;
-  DbArgs a;
-  a.p = *p;
-  a.lg = d_lg;
-  a.skip = d_skip;
-  a.mi_stride = mi_stride;
-  a.xdec = p->xdec;
-  a.ydec = p->ydec;
-  a.cols = ((((width + 3) >> 2) + ((1 << a.xdec) >> 1)) >> a.xdec) << a.xdec;
-  a.rows = ((((height + 3) >> 2) + ((1 << a.ydec) >> 1)) >> a.ydec) << a.ydec;
-  a.pli = pli;
-  a.bd = bit_depth;
-  a.dlev = nullptr;
-  for (int pass = 0; pass < 2; pass++) {
-    a.vert = pass == 0;
-    a.level = pli == 0 ? levels[a.vert ? 0 : 1] : levels[pli + 1];
-    if (a.level == 0) continue;
-    const int sx = a.vert ? (a.cols >> a.xdec) - 1 : (a.cols >> a.xdec);
-    const int sy = a.vert ? (a.rows >> a.ydec) : (a.rows >> a.ydec) - 1;
-    const int64_t n = (int64_t)(sx > 0 ? sx : 0) * (sy > 0 ? sy : 0) * 4;
-    if (n == 0) continue;
-    const unsigned grid = (unsigned)((n + 255) / 256);
-    if (p->hbd)
-      deblock_kernel<uint16_t><<<grid, 256, 0, s>>>(a);
-    else
-      deblock_kernel<uint8_t><<<grid, 256, 0, s>>>(a);
-  }
-  RV_HIP_CHECK_LAUNCH();
+  for (int pass = 0; pass < 2; pass++)
+    if (const int e = deblock_pass(p, &pli, 1, width, height, d_lg, d_skip, mi_stride, levels,
+                                   nullptr, bit_depth, pass == 0, s))
+      return e;
   return RV_OK;
 }
 
@@ -530,7 +538,7 @@ extern "C" int rv_deblock_frame(const rv_plane *planes, int width, int height, c
   for (int p = 0; ok && p < 3; p++) ok = planes[p].hbd == (bit_depth > 8);
   if (!ok) return rv_set_error(RV_EINVAL, "rv_deblock_frame: bad arguments");
   return rv_deblock_frame_dev(planes, width, height, d_lg, d_skip, mi_stride, d_levels, bit_depth,
-                              rv_resolve_stream(stream));
+                              rv_resolve_stream(stream), nullptr);
 }
 
 // deblock_filter_optimize's fast path (src/deblock.rs:1477-1517, speed >=

@@ -23,6 +23,51 @@ __global__ __launch_bounds__(256) void pad_kernel(rv_plane p) {
   d[i] = d[(int64_t)sy * p.stride + sx];
 }
 
+// The three planes of a frame in one launch (plane p owns workgroups
+// [blk[p], blk[p + 1])).  Without src: Plane::pad of dst, one lane per
+// padding pixel only (the top rows, the visible rows' left and right
+// margins, the bottom rows).  With src (same geometry): every allocation
+// pixel of dst = src's visible pixel at the clamped coordinate -- copying a
+// frame and padding it in one pass.
+struct PadPlanes {
+  rv_plane dst[3], src[3];
+  unsigned blk[4];
+  int copy;
+};
+template <typename Px>
+__global__ __launch_bounds__(256) void pad3_kernel(PadPlanes P) {
+  const int pi = blockIdx.x >= P.blk[1] ? (blockIdx.x >= P.blk[2] ? 2 : 1) : 0;
+  const rv_plane &d = P.dst[pi];
+  int64_t i = (int64_t)(blockIdx.x - P.blk[pi]) * 256 + threadIdx.x;
+  const int x0 = d.xorigin, y0 = d.yorigin, w = d.width, h = d.height;
+  const int64_t st = d.stride;
+  int x, y;
+  if (P.copy) {
+    if (i >= st * d.alloc_height) return;
+    y = (int)(i / st);
+    x = (int)(i - y * st);
+  } else {
+    const int64_t top = (int64_t)y0 * st, side = (int64_t)h * (st - w);
+    if (i < top) {
+      y = (int)(i / st);
+      x = (int)(i - y * st);
+    } else if ((i -= top) < side) {
+      const int r = (int)(i / (st - w)), c = (int)(i - r * (st - w));
+      y = y0 + r;
+      x = c < x0 ? c : c + w;
+    } else {
+      i -= side;
+      if (i >= (int64_t)(d.alloc_height - y0 - h) * st) return;
+      const int r = (int)(i / st);
+      y = y0 + h + r;
+      x = (int)(i - r * st);
+    }
+  }
+  const int sx = clampi(x, x0, x0 + w - 1), sy = clampi(y, y0, y0 + h - 1);
+  const Px *sp = reinterpret_cast<const Px *>(P.copy ? P.src[pi].data : d.data);
+  reinterpret_cast<Px *>(d.data)[(int64_t)y * st + x] = sp[(int64_t)sy * st + sx];
+}
+
 // downsample_from: (sum of the 2x2 source pixels + 2) >> 2
 template <typename Px>
 __global__ __launch_bounds__(256) void downsample_kernel(rv_plane dst,
@@ -130,6 +175,35 @@ int rv_synth_frame(const rv_plane *y, const rv_plane *u, const rv_plane *v, int 
     const int e = rv_plane_pad(pl[k], stream);
     if (e != RV_OK) return e;
   }
+  return RV_OK;
+}
+
+// Plane::pad of a frame's three planes, or (src) src copied into dst and
+// padded, in one launch (pad3_kernel).  src's planes have dst's geometry.
+int rv_frame_pad_dev(const rv_plane dst[3], const rv_plane *src, hipStream_t s) {
+  PadPlanes P = {};
+  P.copy = src != nullptr;
+  unsigned blocks = 0;
+  for (int p = 0; p < 3; p++) {
+    const rv_plane &d = dst[p];
+    if (!d.data || d.width <= 0 || d.height <= 0 || d.hbd != dst[0].hbd ||
+        (src && (src[p].stride != d.stride || src[p].xorigin != d.xorigin ||
+                 src[p].yorigin != d.yorigin || src[p].width != d.width ||
+                 src[p].height != d.height || src[p].hbd != d.hbd)))
+      return rv_set_error(RV_EINVAL, "rv_frame_pad: bad planes");
+    P.dst[p] = d;
+    if (src) P.src[p] = src[p];
+    const int64_t n = src ? (int64_t)d.stride * d.alloc_height
+                          : (int64_t)d.stride * d.alloc_height - (int64_t)d.width * d.height;
+    P.blk[p] = blocks;
+    blocks += (unsigned)((n + 255) / 256);
+  }
+  P.blk[3] = blocks;
+  if (dst[0].hbd)
+    pad3_kernel<uint16_t><<<blocks, 256, 0, s>>>(P);
+  else
+    pad3_kernel<uint8_t><<<blocks, 256, 0, s>>>(P);
+  RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }
 

@@ -87,9 +87,27 @@ int rv_deblock_sse_dev(const rv_plane rec[3], const rv_plane src[3], int width, 
                        int64_t *d_tally, uint8_t *d_levels, int bit_depth, hipStream_t s);
 int rv_deblock_frame_dev(const rv_plane planes[3], int width, int height, const uint8_t *d_lg,
                          const uint8_t *d_skip, int mi_stride, const uint8_t *d_levels,
-                         int bit_depth, hipStream_t s);
+                         int bit_depth, hipStream_t s, const uint8_t *levels);
 extern "C" int rv_q_lookup(int ac, int qindex, int bit_depth);
+#define RV_R(expr)                  \
+  do {                              \
+    int e_ = (expr);                \
+    if (e_ != RV_OK) return e_;     \
+  } while (0)
+#define RV_H(expr)                                            \
+  do {                                                        \
+    hipError_t e_ = (expr);                                   \
+    if (e_ != hipSuccess) return rv_set_hip_error(e_, #expr); \
+  } while (0)
+
 // rv_frame.hip
+int rv_frame_pad_dev(const rv_plane dst[3], const rv_plane *src, hipStream_t s);
+// rv_cdef.hip
+int rv_cdef_filter_frame_dev(const rv_plane src[3], const rv_plane dst[3], int width, int height,
+                             const uint8_t *d_skip, int mi_stride, const uint8_t *d_dir,
+                             const int32_t *d_var, const uint8_t *d_cdef_index,
+                             const uint8_t *y_strengths, const uint8_t *uv_strengths, int damping,
+                             int bit_depth, hipStream_t s);
 int rv_plane_pyramid(const rv_plane *y, const rv_plane *h, const rv_plane *q, void *stream);
 int rv_synth_frame(const rv_plane *y, const rv_plane *u, const rv_plane *v, int t, int bit_depth,
                    void *stream);
@@ -1026,6 +1044,11 @@ struct RvLaEngine {
   int W = 0, RW = 0, dev = 0;
   long limit = 0;  // coded frames in the stream (0: unbounded)
   hipStream_t las = nullptr;
+  // the window passes' stream (split): frame m's searches on las overlap
+  // window m - W's propagation (they share only the entries' lists, handed
+  // over with ev_lists); null: everything on las (RAV1E_HIP_LA_SPLIT=0)
+  hipStream_t lap = nullptr;
+  bool split = true;
   RoundRing rr;
   int32_t *la_list = nullptr;
   void *scratch = nullptr;
@@ -1039,6 +1062,7 @@ struct RvLaEngine {
     LaRefs lr{};
     hipEvent_t ev_imp = nullptr, ev_used = nullptr;
     hipEvent_t ev_data = nullptr, ev_xchg = nullptr;  // RCCL parts: data in / exchanged
+    hipEvent_t ev_lists = nullptr;  // split: the frame's lists are built (las -> lap)
   };
   std::vector<Entry> ring;
   std::vector<long> pyr_display;  // per input: the display whose pyramid it holds
@@ -1656,11 +1680,8 @@ int xcopy(rv_replay *r, const RvSlot &s, const XRect *rects, int n, int to_plane
 }
 
 int pad_slot(rv_replay *r, const RvSlot &s) {
-  int e;
-  if ((e = rv_plane_pad(&s.y, r->stream)) || (e = rv_plane_pad(&s.u, r->stream)) ||
-      (e = rv_plane_pad(&s.v, r->stream)))
-    return e;
-  return RV_OK;
+  const rv_plane pl3[3] = {s.y, s.u, s.v};
+  return rv_frame_pad_dev(pl3, nullptr, r->stream);
 }
 
 // deblock_filter_optimize + deblock_filter_frame of a slot coded from input
@@ -1676,40 +1697,40 @@ int deblock_slot(rv_replay *r, const RvSlot &s, const RvInput &in, int lv) {
                                      r->mi_stride, r->db_tally, r->db_dlev, r->g.bd, r->stream);
     if (e != RV_OK) return e;
     return rv_deblock_frame_dev(pl3, r->g.W, r->g.H, r->mi_lg, r->mi_skip, r->mi_stride,
-                                r->db_dlev, r->g.bd, r->stream);
+                                r->db_dlev, r->g.bd, r->stream, nullptr);
   }
   const uint8_t l = r->db_level[lv];
   if (!l) return RV_OK;
   const uint8_t lv4[4] = {l, l, l, l};
-  const rv_plane pls[3] = {s.y, s.u, s.v};
-  for (int p = 0; p < 3; p++) {
-    const int e = rv_deblock_plane_dev(&pls[p], p, r->g.W, r->g.H, r->mi_lg, r->mi_skip,
-                                       r->mi_stride, lv4, r->g.bd, r->stream);
-    if (e != RV_OK) return e;
-  }
-  return RV_OK;
+  return rv_deblock_frame_dev(pl3, r->g.W, r->g.H, r->mi_lg, r->mi_skip, r->mi_stride, nullptr,
+                              r->g.bd, r->stream, lv4);
 }
 
-// cdef_filter_frame of a deblocked slot (src/encoder.rs:2795-2802): the
-// slot is copied to the pre-CDEF frame, the directions come from its luma,
-// and every plane is filtered back into the slot.  cdef_bits 0: every
-// superblock uses entry 0 of the tables, the level's strengths.
-int cdef_slot(rv_replay *r, const RvSlot &s, int lv) {
-  const rv_plane dst[3] = {s.y, s.u, s.v};
-  const rv_plane pre[3] = {r->cdef_pre.y, r->cdef_pre.u, r->cdef_pre.v};
-  for (int p = 0; p < 3; p++)
-    if (hipMemcpyAsync(pre[p].data, dst[p].data, plane_bytes(dst[p]), hipMemcpyDeviceToDevice,
-                       r->stream) != hipSuccess)
-      return rv_set_error(RV_EHIP, "cdef_slot: hipMemcpyAsync");
+// cdef_filter_frame of a deblocked slot (src/encoder.rs:2795-2802), then
+// the slot's padding: the directions come from the slot's luma, every plane
+// is filtered out of the slot into the scratch frame (one launch), and the
+// scratch frame is copied back and padded in one pass (rv_frame_pad_dev) --
+// three launches.  cdef_bits 0: every superblock uses entry 0 of the
+// tables, the level's strengths.
+int cdef_pad_slot(rv_replay *r, const RvSlot &s, int lv) {
+  const rv_plane rec[3] = {s.y, s.u, s.v};
+  const rv_plane out[3] = {r->cdef_pre.y, r->cdef_pre.u, r->cdef_pre.v};
   uint8_t ys[8] = {}, us[8] = {};
   ys[0] = r->cdef_str[lv][0];
   us[0] = r->cdef_str[lv][1];
-  int e = rv_cdef_find_dirs(&pre[0], r->g.W, r->g.H, r->mi_skip, r->mi_stride, r->cdef_dir,
-                            r->cdef_var, r->g.bd, r->stream);
-  for (int p = 0; p < 3 && e == RV_OK; p++)  // cdef_damping = 3 (src/encoder.rs:665)
-    e = rv_cdef_filter_plane(&pre[p], &dst[p], p, r->g.W, r->g.H, r->mi_skip, r->mi_stride,
-                             r->cdef_dir, r->cdef_var, r->cdef_idx, ys, us, 3, r->g.bd, r->stream);
-  return e;
+  RV_R(rv_cdef_find_dirs(&rec[0], r->g.W, r->g.H, r->mi_skip, r->mi_stride, r->cdef_dir,
+                         r->cdef_var, r->g.bd, r->stream));
+  // cdef_damping = 3 (src/encoder.rs:665)
+  RV_R(rv_cdef_filter_frame_dev(rec, out, r->g.W, r->g.H, r->mi_skip, r->mi_stride, r->cdef_dir,
+                                r->cdef_var, r->cdef_idx, ys, us, 3, r->g.bd, r->stream));
+  return rv_frame_pad_dev(rec, out, r->stream);
+}
+
+// The loop filters of a coded slot and its padding: the frame is then a
+// reference (src/encoder.rs:2789-2802, 3411-3429).
+int filter_slot(rv_replay *r, const RvSlot &s, const RvInput &in, int lv) {
+  if (r->deblock) RV_R(deblock_slot(r, s, in, lv));
+  return r->cdef ? cdef_pad_slot(r, s, lv) : pad_slot(r, s);
 }
 
 // Coding order of the reorder pyramid: coded frame n >= 1 (n = 0 is the
@@ -1771,17 +1792,6 @@ LaRefs la_refs_of(long m, int R) {
 }
 
 }  // namespace
-
-#define RV_R(expr)                  \
-  do {                              \
-    int e_ = (expr);                \
-    if (e_ != RV_OK) return e_;     \
-  } while (0)
-#define RV_H(expr)                                            \
-  do {                                                        \
-    hipError_t e_ = (expr);                                   \
-    if (e_ != hipSuccess) return rv_set_hip_error(e_, #expr); \
-  } while (0)
 
 // F6b: rdo_mode_decision's intra-mode screening and intra RDO of every
 // superblock whose inter winner is not skip (rv_intra_pass.hip), round by
@@ -2595,10 +2605,7 @@ int rv_replay_import(rv_replay *r) {
   RV_R(xcopy(r, s, rects, n, 1, r->xrecv));
   // the whole frame and its block map are in: deblock it (every rank the
   // same way), then pad
-  if (r->deblock)
-    RV_R(deblock_slot(r, s, r->inputs[r->last.display % r->inputs.size()], r->last.level));
-  if (r->cdef) RV_R(cdef_slot(r, s, r->last.level));
-  return pad_slot(r, s);
+  return filter_slot(r, s, r->inputs[r->last.display % r->inputs.size()], r->last.level);
 }
 
 // The host side of a round loop: check(q) queues check q, which lists the
@@ -2866,6 +2873,15 @@ static int la_step(rv_replay *r, long m) {
   RV_R(impwin_lists(e.f, lr.n, g.w_imp, g.h_imp, E.scratch, E.scratch_bytes, xs));
   const long last_frame = E.limit > 0 ? E.limit - 1 : -1;
   const size_t ni = (size_t)g.w_imp * g.h_imp;
+  // split: the passes run on lap once frame m's lists are in.  Entry reuse
+  // stays ordered: las waits ev_used of frame m - RW, recorded after that
+  // frame's encode waited its ev_imp on lap -- behind every earlier
+  // window's passes, the only other readers of the entry's lists.
+  if (E.split && E.imp_next <= m && (E.imp_next + E.W <= m || m == last_frame)) {
+    RV_H(hipEventRecord(e.ev_lists, xs));
+    RV_H(hipStreamWaitEvent(E.lap, e.ev_lists, 0));
+    xs = E.lap;
+  }
   while (E.imp_next <= m && (E.imp_next + E.W <= m || m == last_frame)) {
     const long n = E.imp_next, last = n + E.W < m ? n + E.W : m;
     {
@@ -2913,8 +2929,10 @@ static int la_stream_create(RvLaEngine *E) {
   if (low) {
     RV_H(hipDeviceGetStreamPriorityRange(&least, &greatest));
     RV_H(hipStreamCreateWithPriority(&E->las, hipStreamNonBlocking, least));
+    if (E->split) RV_H(hipStreamCreateWithPriority(&E->lap, hipStreamNonBlocking, least));
   } else {
     RV_H(hipStreamCreateWithFlags(&E->las, hipStreamNonBlocking));
+    if (E->split) RV_H(hipStreamCreateWithFlags(&E->lap, hipStreamNonBlocking));
   }
   return RV_OK;
 }
@@ -2964,13 +2982,15 @@ static void la_engine_destroy(rv_replay *r) {
   }
   if (E->th.joinable()) E->th.join();
   if (E->las) (void)hipStreamSynchronize(E->las);
+  if (E->lap) (void)hipStreamSynchronize(E->lap);
   for (auto &en : E->ring)
-    for (hipEvent_t ev : {en.ev_imp, en.ev_used, en.ev_data, en.ev_xchg})
+    for (hipEvent_t ev : {en.ev_imp, en.ev_used, en.ev_data, en.ev_xchg, en.ev_lists})
       if (ev) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : E->hub_ev)
     if (ev) (void)hipEventDestroy(ev);
   if (E->rr.h_pub) (void)hipHostFree(E->rr.h_pub);
   if (E->las) (void)hipStreamDestroy(E->las);
+  if (E->lap) (void)hipStreamDestroy(E->lap);
   delete E;  // its device arrays are the replay's allocations (freed with it)
 }
 
@@ -3126,6 +3146,8 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
   // frame-edge or entropy stream instead of with the twin's round kernels
   // (which the trace showed waiting 6-7 us behind the lookahead's).
   // RAV1E_HIP_LA_LAZY=0: created here (A/B).
+  const char *spe = getenv("RAV1E_HIP_LA_SPLIT");
+  E->split = !(spe && spe[0] == '0');
   const char *lze = getenv("RAV1E_HIP_LA_LAZY");
   const bool lazy = !(lze && lze[0] == '0');
   bool ok = hipGetDevice(&E->dev) == hipSuccess &&
@@ -3144,7 +3166,8 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
          hipEventCreateWithFlags(&en.ev_imp, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&en.ev_used, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&en.ev_data, hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&en.ev_xchg, hipEventDisableTiming) == hipSuccess;
+         hipEventCreateWithFlags(&en.ev_xchg, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&en.ev_lists, hipEventDisableTiming) == hipSuccess;
     if (!ok) break;
     en.o.coarse = (rv_fs_result *)m;
     en.o.half_l = en.o.coarse + nr;
@@ -4097,9 +4120,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   r->coded++;
   r->last = fi;
   if (r->n_groups < 2 && !r->comm) {
-    if (r->deblock) RV_R(deblock_slot(r, S, cur, lv));
-    if (r->cdef) RV_R(cdef_slot(r, S, lv));
-    RV_R(pad_slot(r, S));
+    RV_R(filter_slot(r, S, cur, lv));
   } else {
     XRect xr[6];
     int nx;
