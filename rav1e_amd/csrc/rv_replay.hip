@@ -1046,9 +1046,9 @@ struct RvLaEngine {
   hipStream_t las = nullptr;
   // the window passes' stream (split): frame m's searches on las overlap
   // window m - W's propagation (they share only the entries' lists, handed
-  // over with ev_lists); null: everything on las (RAV1E_HIP_LA_SPLIT=0)
+  // over with ev_lists); null: everything on las (the default; RAV1E_HIP_LA_SPLIT=1)
   hipStream_t lap = nullptr;
-  bool split = true;
+  bool split = false;
   RoundRing rr;
   int32_t *la_list = nullptr;
   void *scratch = nullptr;
@@ -3146,8 +3146,11 @@ int rv_replay_set_imp_window(rv_replay *r, int window, long limit) {
   // frame-edge or entropy stream instead of with the twin's round kernels
   // (which the trace showed waiting 6-7 us behind the lookahead's).
   // RAV1E_HIP_LA_LAZY=0: created here (A/B).
+  // RAV1E_HIP_LA_SPLIT=1: the window passes on a stream of their own.  Off:
+  // the extra stream shares the 4 hardware queues with the encode's and
+  // measured 4-10 % slower (profiles/r05i_*).
   const char *spe = getenv("RAV1E_HIP_LA_SPLIT");
-  E->split = !(spe && spe[0] == '0');
+  E->split = spe && spe[0] == '1';
   const char *lze = getenv("RAV1E_HIP_LA_LAZY");
   const bool lazy = !(lze && lze[0] == '0');
   bool ok = hipGetDevice(&E->dev) == hipSuccess &&

@@ -10,6 +10,7 @@
 #                                     MI355X guide's rule: FETCH_SIZE and WRITE_SIZE do not
 #                                     share a pass)
 #   tools/gpu.sh trace TAG CFG [ARGS] the kernel trace pass alone
+#   tools/gpu.sh tracesum TAG CFG [ARGS]  the kernel trace pass, summarised on the box
 #   tools/gpu.sh envbench TAG CFG "ENV=.." ... [-- ARGS]  one bench line per environment (A/B)
 #   tools/gpu.sh argbench TAG CFG "ARGS" ...  one bench line per argument set (A/B)
 #   tools/gpu.sh ubench TAG           tools/ubench binaries (VALU issue rates, PMC calibration)
@@ -53,6 +54,15 @@ case "$MODE" in
       "200 $TAG/write.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $P/write -o run -- $B" \
       "200 $TAG/sq.log cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $SQ -d $P/sq -o run -- $B" \
       "120 $TAG/summary.log python3 $R/tools/prof_json.py $P $P/prof_$CFG.json --frames ${FRAMES:-101} --bench $P/trace.log --md $P/prof_$CFG.md" \
+      "60 $TAG/slim.log $R/tools/slim_prof.sh $P" ;;
+  tracesum)
+    # kernel trace + its summary on the box (occupancy, gaps; no PMC passes):
+    # tracesum TAG CFG [ARGS]
+    CFG=${1:-2160p}; shift
+    B="python3 $R/bench.py --config $CFG --no-cpu-baseline --emulate-ranks 0 $*"
+    exec bash "$R/tools/gpu_step.sh" \
+      "200 $TAG/trace.log cd /tmp && rocprofv3 --kernel-trace --stats -d $P/trace -o run -- $B" \
+      "120 $TAG/summary.log python3 $R/tools/prof_json.py $P $P/trace_$CFG.json --frames ${FRAMES:-101} --bench $P/trace.log --md $P/trace_$CFG.md" \
       "60 $TAG/slim.log $R/tools/slim_prof.sh $P" ;;
   trace)
     # kernel trace only: trace TAG CFG [ARGS]

@@ -83,6 +83,76 @@ def pmc(c, counters):
     return list(disp.values())
 
 
+def _union(iv):
+    """Total length of the union of [start, end) intervals (sorted by start)."""
+    tot, cur_s, cur_e = 0, None, None
+    for s, e in iv:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        tot += cur_e - cur_s
+    return tot
+
+
+def occupancy(tr):
+    """How busy the device and each stream were over the trace: the fraction
+    of the span some kernel ran (any stream), each stream's own fraction
+    (a stream near 1.0 is a serial chain of kernels: its latency, not the
+    chip, bounds it), and the mean number of kernels in flight."""
+    iv = sorted((s, s + du) for _, _, _, _, s, du in tr)
+    t0, t1 = iv[0][0], max(e for _, e in iv)
+    span = t1 - t0
+    per = collections.defaultdict(list)
+    for _, _, q, _, s, du in tr:
+        per[q].append((s, s + du))
+    streams = {}
+    names = collections.defaultdict(lambda: collections.Counter())
+    for _, n, q, _, s, du in tr:
+        names[q][short(n)] += du
+    for q, v in per.items():
+        v.sort()
+        streams[str(q)] = {"busy_frac": round(_union(v) / span, 4), "launches": len(v),
+                           "top": [k for k, _ in names[q].most_common(3)]}
+    # each stream's idle gaps between its kernels, by length (fraction of
+    # the span): short ones are dispatch, long ones waits (events, host)
+    edges = [5e3, 20e3, 100e3, 1e6]  # ns
+    for q, v in per.items():
+        hist = [0] * (len(edges) + 1)
+        end = v[0][1]
+        for s, e in v[1:]:
+            if s > end:
+                gap = s - end
+                hist[sum(gap >= x for x in edges)] += gap
+            end = max(end, e)
+        streams[str(q)]["gaps_frac"] = dict(zip(["<5us", "5-20us", "20-100us", "0.1-1ms", ">1ms"],
+                                                [round(h / span, 4) for h in hist]))
+    # device-idle stretches (no kernel anywhere), charged to the stream whose
+    # kernel ends them: the chain the device waited on
+    idle = collections.defaultdict(int)
+    owner = sorted((s, s + du, q) for _, _, q, _, s, du in tr)
+    end = owner[0][1]
+    for s, e, q in owner[1:]:
+        if s > end:
+            idle[str(q)] += s - end
+        end = max(end, e)
+    return {"any_kernel_frac": round(_union(iv) / span, 4),
+            "mean_kernels_in_flight": round(sum(e - s for s, e in iv) / span, 3),
+            "idle_ended_by": {q: round(v / span, 4) for q, v in
+                              sorted(idle.items(), key=lambda x: -x[1])},
+            "streams": dict(sorted(streams.items(), key=lambda x: -x[1]["busy_frac"]))}
+
+
+def quantiles(v):
+    v = sorted(v)
+    q = lambda f: round(v[min(len(v) - 1, int(f * len(v)))], 2)
+    return {"p10": q(0.1), "p50": q(0.5), "p90": q(0.9), "max": round(v[-1], 2),
+            "top10pct_time_frac": round(sum(v[int(0.9 * len(v)):]) / sum(v), 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tagdir")
@@ -97,13 +167,15 @@ def main():
     ker = collections.OrderedDict()
     for d, n, q, g, s, du in tr:
         k = ker.setdefault(short(n), {"launches": 0, "us": 0.0, "round0": [0, 0.0],
-                                      "rounds": [0, 0.0]})
+                                      "rounds": [0, 0.0], "durs": []})
         k["launches"] += 1
+        k["durs"].append(du / 1e3)
         k["us"] += du / 1e3
         if d in cls:
             k[cls[d]][0] += 1
             k[cls[d]][1] += du / 1e3
     span = (max(s + du for _, _, _, _, s, du in tr) - min(s for _, _, _, _, s, _ in tr)) / 1e6
+    occ = occupancy(tr)
     # PMC passes: bytes per launch (all launches, and round 0 of the F4 kernels)
     traffic = collections.defaultdict(lambda: {"fetch": [0, 0.0], "write": [0, 0.0],
                                                "fetch0": [0, 0.0], "write0": [0, 0.0]})
@@ -133,6 +205,7 @@ def main():
                ["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip(),
            "frames": a.frames, "span_ms": round(span, 3),
            "busy_ms_per_frame": round(sum(k["us"] for k in ker.values()) / 1e3 / a.frames, 4),
+           "occupancy": occ,
            "hbm_bytes_rule": "2 x FETCH_SIZE + WRITE_SIZE (KB x 1024; MI355X_MICROARCH.md, "
                              "tools/ubench/pmc_cal.hip)",
            "kernels": {}}
@@ -146,6 +219,8 @@ def main():
         e = {"launches_per_frame": round(k["launches"] / a.frames, 3),
              "ms_per_frame": round(k["us"] / 1e3 / a.frames, 4),
              "avg_us": round(k["us"] / k["launches"], 3)}
+        if k["us"] / 1e3 / a.frames >= 0.1:  # the heavy kernels: launch duration spread (us)
+            e["dur_us"] = quantiles(k["durs"])
         if k["round0"][0]:
             e["round0"] = {"launches": k["round0"][0],
                            "avg_us": round(k["round0"][1] / k["round0"][0], 3)}
@@ -173,7 +248,12 @@ def main():
         lines = [f"# Kernel profile `{out['tagdir']}` (git {out['git']})", "",
                  f"`bench.py` traced by `tools/gpu.sh prof`: {a.frames:g} coded frames, trace span "
                  f"{span:.1f} ms, kernel busy time {out['busy_ms_per_frame']:.3f} ms per frame "
-                 "(summed over streams: the twin instance and the lookahead engine overlap).", ""]
+                 "(summed over streams: the twin instance and the lookahead engine overlap).", "",
+                 f"Occupancy: some kernel in flight {occ['any_kernel_frac']:.1%} of the span, "
+                 f"{occ['mean_kernels_in_flight']:.2f} kernels in flight on average; busiest "
+                 "streams (fraction of the span with a kernel of theirs running): " +
+                 ", ".join(f"{q}: {v['busy_frac']:.1%}" for q, v in
+                           list(occ["streams"].items())[:6]), ""]
         if "bench_line" in out:
             lines += [f"Bench line of the traced run: `{json.dumps(out['bench_line'])}`", ""]
         lines += ["| kernel | ms/frame | launches/frame | avg us | HBM B/launch | round 0 avg us | "
