@@ -184,14 +184,17 @@ def _kernels_trace(pj):
             "kernels": out}
 
 
-def timed_run(engine, group, steps, warmup, sync=None, finish=None, before=None, start=None):
+def timed_run(engine, group, steps, warmup, sync=None, finish=None, before=None, start=None,
+              mark=None):
     """W untimed frames (the key frame first), then exactly K timed coded
     frames bracketed by a barrier and a device sync on both sides; returns
     (max-over-ranks seconds, result words of the last frame).  `engine` is a
     HipReplay / TileParallel (the product) or, in the multi-rank CPU tests,
     the oracle's CpuReplay behind a TileParallel.  before(): after the
     warmup, outside the timing (probes reset); start(): the first thing
-    inside the timing (the lookahead engine released)."""
+    inside the timing (the lookahead engine released); mark(): an empty
+    marker kernel right before t0 and after t1 (a kernel trace's timed
+    region, tools/prof_json.py)."""
     drain = getattr(engine, "drain", None)  # PairedReplay: frames issued from a second thread
     for i in range(warmup):
         engine.frame()
@@ -204,6 +207,8 @@ def timed_run(engine, group, steps, warmup, sync=None, finish=None, before=None,
     group.barrier()
     if sync:
         sync()
+    if mark:
+        mark()
     t0 = time.perf_counter()
     if start:
         start()
@@ -216,6 +221,8 @@ def timed_run(engine, group, steps, warmup, sync=None, finish=None, before=None,
     if finish:
         finish()  # the host's share of the frames (F8's range coder) has finished too
     t1 = time.perf_counter()
+    if mark:
+        mark()
     progress(f"timed: {steps} frames in {t1 - t0:.3f} s")
     group.barrier()
     # the verification checksums are not part of a frame: outside the timing
@@ -528,7 +535,8 @@ def main():
 
     dt, words = timed_run(eng, group, args.steps, args.warmup,
                           sync=lambda: R._check(R.lib().rv_device_sync(), "rv_device_sync"),
-                          finish=eng.entropy_stats if ent else None, before=before, start=start)
+                          finish=eng.entropy_stats if ent else None, before=before, start=start,
+                          mark=lambda: R._check(R.lib().rv_trace_marker(None), "rv_trace_marker"))
     if imp_window:
         la_cnt["t1"] = int((eng if paired else hip).counters()[20])
     kp = eng.kernel_probe() if probe else None

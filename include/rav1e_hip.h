@@ -90,6 +90,11 @@ void *rv_stream_create_priority(int priority);
 int rv_stream_destroy(void *stream);
 int rv_stream_sync(void *stream);
 int rv_device_sync(void);
+/* An empty kernel on `stream` (null: the default stream), for finding a
+ * region in a kernel trace: bench.py launches one right before and one right
+ * after its timed region (tools/prof_json.py restricts the occupancy figures
+ * to what lies between). */
+int rv_trace_marker(void *stream);
 void *rv_event_create(void);
 int rv_event_destroy(void *ev);
 int rv_event_record(void *ev, void *stream);

@@ -233,6 +233,7 @@ def _declare(L):
         "rv_stream_destroy": (i32, [vp]),
         "rv_stream_sync": (i32, [vp]),
         "rv_device_sync": (i32, []),
+        "rv_trace_marker": (i32, [vp]),
         "rv_event_create": (vp, []),
         "rv_event_destroy": (i32, [vp]),
         "rv_event_record": (i32, [vp, vp]),

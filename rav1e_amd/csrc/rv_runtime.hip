@@ -151,6 +151,14 @@ int rv_stream_sync(void *stream) {
   RV_TRY(hipStreamSynchronize(rv_resolve_stream(stream)));
   return RV_OK;
 }
+// an empty kernel a kernel trace can find (bench.py brackets its timed
+// region with two; tools/prof_json.py)
+__global__ void rv_trace_marker_kernel() {}
+int rv_trace_marker(void *stream) {
+  rv_trace_marker_kernel<<<1, 64, 0, rv_resolve_stream(stream)>>>();
+  RV_TRY(hipGetLastError());
+  return RV_OK;
+}
 int rv_device_sync(void) {
   RV_TRY(hipDeviceSynchronize());
   return RV_OK;

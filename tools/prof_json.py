@@ -98,6 +98,15 @@ def _union(iv):
     return tot
 
 
+def timed_window(tr):
+    """The trace between bench.py's two rv_trace_marker_kernel launches (its
+    timed region), or the whole trace without them."""
+    ms = sorted(s for _, n, _, _, s, _ in tr if "rv_trace_marker_kernel" in n)
+    if len(ms) < 2:
+        return tr, False
+    return [t for t in tr if ms[0] < t[4] < ms[-1] and "rv_trace_marker_kernel" not in t[1]], True
+
+
 def occupancy(tr):
     """How busy the device and each stream were over the trace: the fraction
     of the span some kernel ran (any stream), each stream's own fraction
@@ -175,7 +184,9 @@ def main():
             k[cls[d]][0] += 1
             k[cls[d]][1] += du / 1e3
     span = (max(s + du for _, _, _, _, s, du in tr) - min(s for _, _, _, _, s, _ in tr)) / 1e6
-    occ = occupancy(tr)
+    win, marked = timed_window(tr)
+    occ = occupancy(win)
+    occ["window"] = "bench.py's timed region (marker kernels)" if marked else "the whole trace"
     # PMC passes: bytes per launch (all launches, and round 0 of the F4 kernels)
     traffic = collections.defaultdict(lambda: {"fetch": [0, 0.0], "write": [0, 0.0],
                                                "fetch0": [0, 0.0], "write0": [0, 0.0]})
@@ -249,7 +260,7 @@ def main():
                  f"`bench.py` traced by `tools/gpu.sh prof`: {a.frames:g} coded frames, trace span "
                  f"{span:.1f} ms, kernel busy time {out['busy_ms_per_frame']:.3f} ms per frame "
                  "(summed over streams: the twin instance and the lookahead engine overlap).", "",
-                 f"Occupancy: some kernel in flight {occ['any_kernel_frac']:.1%} of the span, "
+                 f"Occupancy ({occ['window']}): some kernel in flight {occ['any_kernel_frac']:.1%} of the span, "
                  f"{occ['mean_kernels_in_flight']:.2f} kernels in flight on average; busiest "
                  "streams (fraction of the span with a kernel of theirs running): " +
                  ", ".join(f"{q}: {v['busy_frac']:.1%}" for q, v in
