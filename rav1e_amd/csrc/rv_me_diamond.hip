@@ -330,28 +330,18 @@ struct DsFast {
   static constexpr int kOrgRegs = SUB ? 1 : 4 * F::I;
 };
 
-// RS > 1 (sub-pel, 64-wide blocks): RS wavefronts per candidate, each
-// filtering H / RS output rows (plus the 7-row filter halo) -- RS x 4
-// wavefronts per workgroup, a diamond step's latency about RS x shorter for
-// (H / RS + 7) / (H + 7) x RS more filter rows; the partial SADs meet in LDS.
-template <typename Px, int W, int H, bool SUB, int RS = 1>
+template <typename Px, int W, int H, bool SUB>
 __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
   using F = FullGeo<Px, W, H>;
   using S = SubGeo<Px, W, H>;
   constexpr int B = (int)sizeof(Px);
-  constexpr int kT = kDsThreads * RS;  // the workgroup
-  constexpr int RGp = SUB ? S::RG / RS : 1;  // output rows per wavefront
-  static_assert(RS == 1 || (SUB && W == 64), "row split: 64-wide sub-pel blocks");
-  static_assert(!SUB || RGp % 8 == 0, "sub-pel row groups are unrolled by 8");
+  static_assert(!SUB || S::RG % 8 == 0, "sub-pel row groups are unrolled by 8");
   __shared__ uint64_t scost[2][kDsWaves];
   __shared__ uint32_t wevals[kDsWaves];
-  __shared__ uint32_t spart[RS][kDsWaves];  // RS > 1: the candidates' partial SADs
   __shared__ uint32_t win_all[SUB ? S::kUnionDwords : 1];
   __shared__ Px org_lds[SUB ? W * H : 1];  // sub-pel: the source block, shared by all waves
 
-  const int wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wave = wave_id % kDsWaves;  // the candidate this wavefront evaluates
-  const int part = wave_id / kDsWaves;  // RS > 1: its rows [part * RGp, +RGp)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const rv_ds_job *jp = a.jobs + job;  // pred[] read through the pointer
   const rv_ds_job jb = *jp;
@@ -366,7 +356,7 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
   if constexpr (SUB) {
     org[0] = 0;
     const Px *o = plane_ptr<Px>(a.org, jb.po_x, jb.po_y);
-    for (int i = threadIdx.x; i < W * H; i += kT)
+    for (int i = threadIdx.x; i < W * H; i += kDsThreads)
       org_lds[i] = o[(int64_t)(i / W) * a.org.stride + (i % W)];
     __syncthreads();
   } else {
@@ -432,11 +422,11 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
     const uint8_t *sp = (const uint8_t *)plane_ptr<Px>(ref, bx, by);
     const int64_t rs = (int64_t)ref.stride * B;
     const int rdw = (cols * B + 3) >> 2, tot = rows * rdw;
-    for (int i0 = threadIdx.x; i0 < tot; i0 += 4 * kT) {
+    for (int i0 = threadIdx.x; i0 < tot; i0 += 4 * kDsThreads) {
       uint32_t v[4];
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        const int i = i0 + u * kT;
+        const int i = i0 + u * kDsThreads;
         v[u] = 0;
         if (i < tot) {
           const int r = i / rdw, d = i - r * rdw;
@@ -445,7 +435,7 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
       }
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        const int i = i0 + u * kT;
+        const int i = i0 + u * kDsThreads;
         if (i < tot) {
           const int r = i / rdw, d = i - r * rdw;
           // u8: stored as i8 = pixel - 128 (the horizontal v_dot4_i32_i8)
@@ -457,21 +447,20 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
   // SAD of this wavefront's candidate from the staged window, the window
   // pixel (dx, dy) being the candidate's (-3, -3) origin; the filter case
   // (horizontal / vertical / both / copy) is resolved once per candidate
-  // (RS > 1: this wavefront's rows of it)
   auto sub_sad = [&](int cf, int rf, int dx, int dy) __attribute__((always_inline)) -> uint32_t {
-    const uint32_t *w0 = win_all + (dy + part * RGp) * (S::UP / 4);
-    const Px *ocol = org_lds + grp * S::RG * W + part * RGp * W + col;
+    const uint32_t *w0 = win_all + dy * (S::UP / 4);
+    const Px *ocol = org_lds + grp * S::RG * W + col;
     const int8_t *xf = kReg[W <= 4][cf];
     const int8_t *yf = kReg[H <= 4][rf];
     uint32_t acc;
     if (cf && rf)
-      acc = sub_sad_rows<Px, W, RGp, S::UP, true, true>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
+      acc = sub_sad_rows<Px, W, S::RG, S::UP, true, true>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
     else if (cf)
-      acc = sub_sad_rows<Px, W, RGp, S::UP, true, false>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
+      acc = sub_sad_rows<Px, W, S::RG, S::UP, true, false>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
     else if (rf)
-      acc = sub_sad_rows<Px, W, RGp, S::UP, false, true>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
+      acc = sub_sad_rows<Px, W, S::RG, S::UP, false, true>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
     else
-      acc = sub_sad_rows<Px, W, RGp, S::UP, false, false>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
+      acc = sub_sad_rows<Px, W, S::RG, S::UP, false, false>(w0, ocol, col + dx, grp, xf, yf, ib, maxv);
     return wave_sum(acc);
   };
   // Called by every thread.  Wave w evaluates cands[w] (w < n, w != skip);
@@ -497,10 +486,7 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
       }
     }
     uint64_t mine = ~0ull;
-    if (!any) return mine;  // (uniform over the workgroup)
-    uint32_t psad = 0;  // this wavefront's (partial) SAD of candidate `wave`
-    bool mok = false;
-    rv_mv mmv = cands[0];
+    if (!any) return mine;
     SubPos me = q[0];
     rv_mv me_mv = cands[0];
 #pragma unroll
@@ -525,10 +511,8 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
         wvalid = true;
       }
       if (me.ok) {
-        evals += part == 0;
-        mok = true;
-        mmv = me_mv;
-        psad = sub_sad(me.cf, me.rf, me.qx - wx, me.qy - wy);
+        evals++;
+        mine = ds_cost(sub_sad(me.cf, me.rf, me.qx - wx, me.qy - wy), me_mv, jb, a.hp);
       }
     } else {  // far-apart predictors: one window at a time
       wvalid = false;
@@ -544,26 +528,10 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
         if (qk.ok) load_box(qk.qx, qk.qy, H + 7, W + 7);
         __syncthreads();
         if (qk.ok && wave == k) {
-          evals += part == 0;
-          mok = true;
-          mmv = ck;
-          psad = sub_sad(qk.cf, qk.rf, 0, 0);
+          evals++;
+          mine = ds_cost(sub_sad(qk.cf, qk.rf, 0, 0), ck, jb, a.hp);
         }
       }
-    }
-    if constexpr (RS > 1) {
-      // the partial SADs meet (spart is next written after the caller's
-      // cost-exchange barrier, which follows these reads)
-      if (lane == 0) spart[part][wave] = psad;
-      __syncthreads();
-      if (mok) {
-        uint32_t sum = 0;
-#pragma unroll
-        for (int p = 0; p < RS; p++) sum += spart[p][wave];
-        mine = ds_cost(sum, mmv, jb, a.hp);
-      }
-    } else if (mok) {
-      mine = ds_cost(psad, mmv, jb, a.hp);
     }
     return mine;
   };
@@ -603,7 +571,7 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
             if (wave == k) mine = c4[k];
           c = eval_full(mine);
         }
-        if (lane == 0 && part == 0) scost[round & 1][wave] = c;
+        if (lane == 0) scost[round & 1][wave] = c;
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < kDsWaves; k++) {
@@ -667,7 +635,7 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
           if (wave == k) mine = c4[k];
         c = wave < n && wave != skip ? eval_full(mine) : ~0ull;
       }
-      if (lane == 0 && part == 0) scost[iter & 1][wave] = c;
+      if (lane == 0) scost[iter & 1][wave] = c;
       __syncthreads();
       uint64_t best = ~0ull;
       int bp = 0;
@@ -703,7 +671,7 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
     }
   }
   if (a.evals || a.eval_acc) {
-    if (lane == 0 && part == 0) wevals[wave] = evals;
+    if (lane == 0) wevals[wave] = evals;
     __syncthreads();
     if (threadIdx.x == 0) {
       const uint32_t ev = wevals[0] + wevals[1] + wevals[2] + wevals[3];
@@ -726,20 +694,20 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
 // The workgroup's jobs: one (xcd_job) on a full grid, or, list-driven, the
 // listed superblocks' jobs (every reference's) from blockIdx.x in steps of
 // the grid.  Every bound is uniform over the workgroup.
-template <typename Px, int W, int H, bool SUB, int RS = 1>
+template <typename Px, int W, int H, bool SUB>
 __device__ __forceinline__ void ds_fast_jobs(const DsArgs &a) {
   if (!a.alist) {
     const int job = xcd_job(a.n);
     if (job >= a.n) return;                                // whole workgroup, uniformly
     if (a.active && !a.active[job % a.n_per_ref]) return;  // settled this round
-    ds_fast_body<Px, W, H, SUB, RS>(a, job);
+    ds_fast_body<Px, W, H, SUB>(a, job);
     return;
   }
   const int total = ds_list_total(a);
   for (int i = blockIdx.x; i < total; i += gridDim.x) {
     const int job = __builtin_amdgcn_readfirstlane(ds_list_job(a, i));
     if (a.dirty && !a.dirty[job]) continue;  // uniform: its inputs are unchanged
-    ds_fast_body<Px, W, H, SUB, RS>(a, job);
+    ds_fast_body<Px, W, H, SUB>(a, job);
     __syncthreads();  // the job's LDS reads end before the next job's writes
   }
 }
@@ -749,16 +717,6 @@ __global__ __launch_bounds__(kDsThreads) __attribute__((amdgpu_waves_per_eu(5)))
 ds_fast_kernel(DsArgs a) {
   if (a.t0 && threadIdx.x == 0) atomicMin(a.t0, (unsigned long long)wall_clock64());
   ds_fast_jobs<Px, W, H, SUB>(a);
-  if (a.t1) {
-    __syncthreads();
-    if (threadIdx.x == 0) atomicMax(a.t1, (unsigned long long)wall_clock64());
-  }
-}
-// the row-split sub-pel search (ds_fast_body RS = 4): 16 wavefronts
-template <typename Px, int W, int H>
-__global__ __launch_bounds__(4 * kDsThreads) void ds_fast_split_kernel(DsArgs a) {
-  if (a.t0 && threadIdx.x == 0) atomicMin(a.t0, (unsigned long long)wall_clock64());
-  ds_fast_jobs<Px, W, H, true, 4>(a);
   if (a.t1) {
     __syncthreads();
     if (threadIdx.x == 0) atomicMax(a.t1, (unsigned long long)wall_clock64());
@@ -1549,19 +1507,6 @@ void launch_fast(const DsArgs &a, hipStream_t s) {
     const char *e = getenv("RAV1E_HIP_DS_OCC4");
     return e && e[0] == '1';
   }();
-  // RAV1E_HIP_DS_SPLIT: the 64x64 sub-pel searches row-split over 16
-  // wavefronts (ds_fast_split_kernel) -- 0 never, 1 the list-driven rounds
-  // (a few dozen jobs: latency), 2 every launch
-  static const int split = [] {
-    const char *e = getenv("RAV1E_HIP_DS_SPLIT");
-    return e ? e[0] - '0' : 1;
-  }();
-  if constexpr (SUB && W == 64 && H == 64) {
-    if (split >= 2 || (split == 1 && a.alist)) {
-      ds_fast_split_kernel<Px, W, H><<<grid, 4 * kDsThreads, 0, s>>>(a);
-      return;
-    }
-  }
   if (!SUB && !a.tele && W * H <= 32 * 32 && ds_full_wave() && !a.alist)
     ds_wave_kernel<Px, W, H><<<grid, 64, 0, s>>>(a);
   else if (occ4)
