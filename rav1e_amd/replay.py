@@ -675,17 +675,20 @@ class PipelinedReplay:
         if self.k not in (3, 5):
             raise ValueError(f"PipelinedReplay: {self.k} instances (3 or 5)")
         self.p = primary
-        # RAV1E_PIPE_HP=1: the twins (the compound frames' instances) on
-        # high-priority streams (A/B)
+        # RAV1E_PIPE_HP (A/B): "1" the twins (the compound frames' instances)
+        # on high-priority streams; "L1" the level-1 twin alone (the frames
+        # every level-2 frame waits for)
         self.hp_streams = []
-        if os.environ.get("RAV1E_PIPE_HP") == "1":
-            for _ in range(self.k - 1):
+        hp = os.environ.get("RAV1E_PIPE_HP")
+        self.inst = [primary]
+        for i in range(self.k - 1):
+            st = None
+            if hp == "1" or (hp == "L1" and i == 0):
                 st = lib().rv_stream_create_priority(-1)
                 if not st:
                     raise RuntimeError(f"rv_stream_create_priority: {lib().rv_last_error().decode()}")
                 self.hp_streams.append(st)
-        self.inst = [primary] + [primary.twin(self.hp_streams[i] if self.hp_streams else None)
-                                 for i in range(self.k - 1)]
+            self.inst.append(primary.twin(st))
         self.R = primary.cfg.n_refs
         self.n = 0
         self.err = None
