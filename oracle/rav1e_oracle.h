@@ -330,6 +330,39 @@ struct orc_replay;
 int orc_replay_set_entropy(struct orc_replay *r, int on);
 void orc_replay_entropy_stats(const struct orc_replay *r, uint64_t out[4]);
 
+/* ---- loop restoration, self-guided filter (orc_lrf.c) ---- */
+typedef struct {
+  int unit_size, sb_h_shift, sb_v_shift, stripe_h, cols, rows;
+} orc_lrf_plane_cfg;
+typedef struct {
+  int8_t set;     /* -1: RestorationFilter::None, else the Sgrproj set */
+  int8_t xqd[2];
+} orc_lrf_unit;
+extern const uint32_t ORC_SGRPROJ_PARAMS_S[16][2];
+void orc_lrf_config(int width, int height, int xdec, int ydec, int base_q_idx, int tiled,
+                    int tile_w_sb, int tile_h_sb, orc_lrf_plane_cfg out[3]);
+void orc_lrf_integral(const void *cdeffed, ptrdiff_t cs, const void *deblocked, ptrdiff_t ds,
+                      int hbd, int x0, int y0, int crop_w, int crop_h, int stripe_w, int stripe_h,
+                      uint32_t *ii, uint32_t *sq, int iis);
+void orc_sgr_stripe_filter(int set, const int8_t xqd[2], int bd, const uint32_t *ii,
+                           const uint32_t *sq, int iis, int w, int h, const void *cd, ptrdiff_t cs,
+                           void *out, ptrdiff_t os, int hbd);
+void orc_sgr_solve(int set, int bd, const uint32_t *ii, const uint32_t *sq, int iis,
+                   const void *in, ptrdiff_t is, const void *cd, ptrdiff_t cs, int hbd, int w, int h,
+                   int8_t xqd[2]);
+void orc_sgr_solve_finish(int set, int w, int h, int64_t H00, int64_t H01, int64_t H11, int64_t C0,
+                          int64_t C1, int8_t xqd[2]);
+void orc_lrf_filter_frame(void *const out[3], const void *const pre[3], const ptrdiff_t stride[3],
+                          int hbd, int bd, int width, int height, int xdec, int ydec,
+                          const orc_lrf_plane_cfg cfg[3], const orc_lrf_unit *const units[3],
+                          int enable_cdef);
+uint32_t orc_symbol_bits(uint32_t s, const uint16_t *cdf, int nsym);
+uint32_t orc_lrf_rate(const uint16_t cdf[4], const int8_t ref[2], int set, const int8_t xqd[2]);
+void orc_lrf_commit(uint16_t cdf[4], int8_t ref[2], int set, const int8_t xqd[2]);
+void orc_lrf_tile_init(uint16_t cdf[4], int8_t ref[3][2]);
+int orc_replay_set_lrf(struct orc_replay *r, int on);
+void orc_replay_lrf_units(const struct orc_replay *r, int plane, int8_t *out, int cap);
+
 #ifdef __cplusplus
 }
 #endif

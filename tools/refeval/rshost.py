@@ -134,12 +134,20 @@ class Plane:
 
     as_region_mut = as_region
 
-    def row_range(self, x, y):  # src/frame/plane.rs:335-343
-        base_y = self.cfg.yorigin + y
-        base_x = self.cfg.xorigin + x
+    def _row_range(self, x, y):  # src/frame/plane.rs:335-343
+        base_y = self.cfg.yorigin + int(y)
+        base_x = self.cfg.xorigin + int(x)
         assert base_y >= 0 and base_x >= 0
         base = base_y * self.cfg.stride + base_x
         return base, base + self.cfg.stride - base_x
+
+    def row_range(self, x, y):  # as the reference's callers see it: a Range<usize>
+        from rsinterp import RangeV
+        a, b = self._row_range(x, y)
+        return RangeV(TInt(a, "usize"), TInt(b, "usize"), False)
+
+    def p(self, x, y):  # src/frame/plane.rs PlaneSlice::p via the plane
+        return self.data[self._row_range(x, y)[0]]
 
 
 class PlaneSlice:
@@ -149,7 +157,7 @@ class PlaneSlice:
         self.plane, self.x, self.y = plane, x, y
 
     def index_row(self, r):
-        a, b = self.plane.row_range(self.x, self.y + r)
+        a, b = self.plane._row_range(self.x, self.y + r)
         return Slice(self.plane.data, a, b)
 
     def clamp(self):
@@ -169,9 +177,12 @@ class PlaneSlice:
     def go_left(self, i):
         return PlaneSlice(self.plane, self.x - int(i), self.y)
 
+    def p(self, x, y):  # src/frame/plane.rs:548-553
+        return self.plane.p(self.x + int(x), self.y + int(y))
+
     def as_ptr(self):
         from rsinterp import Ptr
-        return Ptr(self.plane.data, self.plane.row_range(self.x, self.y)[0])
+        return Ptr(self.plane.data, self.plane._row_range(self.x, self.y)[0])
 
 
 def to_rect(area, xdec, ydec, parent_w, parent_h):

@@ -1689,6 +1689,19 @@ class Interp:
         r = deref(recv) if not isinstance(recv, Ptr) else recv
         if isinstance(r, Struct) and name in self.impls.get(r._name, {}):
             return self.make_method(r._name, name, r, env)(*args)
+        if isinstance(r, Struct) and "next" in self.impls.get(r._name, {}) and \
+                name not in ("unwrap", "expect", "unwrap_or", "is_some", "is_none", "clone"):
+            # a struct with its own `impl Iterator` (src/lrf.rs VertPaddedIter):
+            # the std adaptors run over its next() (Some(x) = x, None = None)
+            nxt = self.make_method(r._name, "next", r, env)
+
+            def items(nxt=nxt):
+                while True:
+                    o = deref(nxt())
+                    if o is None:
+                        return
+                    yield o
+            r = It(items())
         gty = type_name(gens[0]) if gens else None
         return call_method(r, name, args, gty, recv)
 
