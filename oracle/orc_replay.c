@@ -178,6 +178,12 @@ typedef struct orc_replay {
   /* RV_REPLAY_CDEF (orc_replay_set_cdef): (y, uv) strengths per level */
   int cdef;
   uint8_t cdef_str[3][2];
+  /* RV_REPLAY_LRF (orc_replay_set_lrf): loop restoration, the frame's unit
+   * geometry and each unit's filter (set -1: None) */
+  int lrf;
+  orc_lrf_plane_cfg lrf_cfg[3];
+  orc_lrf_unit *lrf_units[3];
+  int lrf_n[3];
   /* intra-mode screening + intra RDO of the non-skip superblocks
    * (orc_replay_set_intra; speed 10, 4:2:0): screened / intra winners this
    * frame */
@@ -528,6 +534,7 @@ void orc_replay_destroy(orc_replay *r) {
   free_levels(r);
   free(r->mi_lg);
   free(r->mi_skip);
+  for (int p = 0; p < 3; p++) free(r->lrf_units[p]);
   for (int l = 0; l < 3; l++) free(r->ec_chain[l]);
   pthread_mutex_destroy(&r->mu);
   free(r);
@@ -737,6 +744,25 @@ static void deblock_planes(orc_replay *r) {
                       p ? r->xdec : 0, p ? r->ydec : 0, p, r->mi_lg, r->mi_skip, r->mi_cols, lv4);
 }
 
+/* Loop restoration of every coded frame (the replay's RV_REPLAY_LRF):
+ * rdo_loop_decision's restoration choice per unit while the frame is coded
+ * (src/encoder.rs:3236-3320, src/rdo.rs:1726-2120), lrf_filter_frame after
+ * CDEF (src/encoder.rs:2803-2806).  Needs the deblocking block map; one
+ * tile group. */
+int orc_replay_set_lrf(orc_replay *r, int on) {
+  if (on && !r->deblock) return -1;
+  r->lrf = on != 0;
+  return 0;
+}
+/* the last frame's unit filters of plane p: (set, xqd0, xqd1) per unit */
+void orc_replay_lrf_units(const orc_replay *r, int plane, int8_t *out, int cap) {
+  for (int i = 0; i < r->lrf_n[plane] && 3 * i + 2 < cap; i++) {
+    out[3 * i] = r->lrf_units[plane][i].set;
+    out[3 * i + 1] = r->lrf_units[plane][i].xqd[0];
+    out[3 * i + 2] = r->lrf_units[plane][i].xqd[1];
+  }
+}
+
 /* the levels deblock_filter_optimize chose for the last deblocked frame */
 void orc_replay_deblock_levels(const orc_replay *r, uint8_t out[4]) {
   memcpy(out, r->db_levels, 4);
@@ -771,10 +797,253 @@ static void cdef_planes(orc_replay *r) {
   for (int p = 0; p < 3; p++) free((void *)in[p]);
 }
 
-/* the loop filters in rav1e's order (src/encoder.rs:2789-2802) */
+static double dist_bias(const orc_replay *r, int mi_x, int mi_y, int m);
+static uint64_t biased(uint64_t v, double bias);
+/* rdo_loop_plane_error (src/rdo.rs:1675-1720) of the superblock at tile
+ * superblock (sx, sy) of the tile at superblock (t0x, t0y), plane p: test
+ * holds the superblock's plane-p block at pitch tp; luma cdef_dist_wxh_8x8,
+ * chroma sse_wxh of the 8x8's (8 >> xdec) x (8 >> ydec) part, each biased
+ * with its 8x8's compute_distortion_bias, the sum scaled by dist_scale[p] */
+static uint64_t lrf_plane_error(const orc_replay *r, const oplane *src, int p, int t0x, int t0y,
+                                int sx, int sy, int mi_cols, int mi_rows, const void *test, int tp) {
+  const int xd = p ? r->xdec : 0, yd = p ? r->ydec : 0, hbd = r->hbd;
+  uint64_t err = 0;
+  for (int by = 0; by < 8; by++)
+    for (int bx = 0; bx < 8; bx++) {
+      const int bo_x = sx * 16 + 2 * bx, bo_y = sy * 16 + 2 * by;  /* tile 4x4 units */
+      if (bo_x >= mi_cols || bo_y >= mi_rows) continue;
+      const int fx = t0x * 16 + bo_x, fy = t0y * 16 + bo_y;      /* frame 4x4 units */
+      const double bias = dist_bias(r, fx, fy, 2);
+      const int px = (fx * 4) >> xd, py = (fy * 4) >> yd;
+      const int qx = (bx * 8) >> xd, qy = (by * 8) >> yd;
+      const uint8_t *t = (const uint8_t *)test + ((size_t)qy * tp + qx) * px_of(r);
+      if (p == 0) {
+        int64_t mo[5];
+        orc_cdef_moments_8x8(at(src, hbd, px, py), src->stride, t, tp, hbd, mo);
+        err += biased(orc_cdef_dist_from_moments(mo, r->bd), bias);
+      } else {
+        uint64_t parts[4];
+        const int n = orc_sse_wxh(at(src, hbd, px, py), src->stride, t, tp, 8 >> xd, 8 >> yd, xd, yd,
+                                  hbd, parts);
+        for (int k = 0; k < n; k++) err += biased(parts[k], bias);
+      }
+    }
+  return (uint64_t)((double)err * r->lv[r->fi.level].ds[p]);
+}
+
+/* Loop restoration's choice of every unit of the frame just coded, as
+ * rdo_loop_decision makes it while the tile is coded (src/encoder.rs:
+ * 3236-3320: a unit's decision follows its last superblock; src/rdo.rs:
+ * 1726-2120): units of one superblock in every plane (RestorationState::new
+ * at base_q_idx <= 160, the replay's levels).  Per superblock in tile raster
+ * order: the padded CDEF input of cdef_sb_padded_frame_copy (src/cdef.rs:
+ * 345-406) -- the tile's reconstruction so far, 128 where a superblock is
+ * not coded yet (Plane::new's fill), CDEF_VERY_LARGE outside the tile --
+ * filtered with cdef index 0 into the unit's input; then per plane None and
+ * the 16 sets (sgrproj_solve + sgrproj_stripe_filter), each priced with
+ * count_lrf_switchable and compute_rd_cost (src/rdo.rs:563-568); the
+ * cheapest (first minimum) is the unit's filter; write_lrf then updates
+ * the tile's restoration CDF and the plane's sgrproj_ref.  Two quirks kept:
+ * sgrproj_solve's source and the unit size read the whole frame at the
+ * unit's tile-relative offset (ts.input with loop_tile_po, :2028-2033). */
+static int lrf_decide(orc_replay *r) {
+  const int lvl = r->fi.level, hbd = r->hbd, B = (int)px_of(r), cs = r->bd - 8;
+  const int sbc = (r->W + SB - 1) / SB, sbr = (r->H + SB - 1) / SB;
+  const int tiled = (sbc + r->tws - 1) / r->tws > 1 || (sbr + r->ths - 1) / r->ths > 1;
+  orc_lrf_config(r->W, r->H, r->xdec, r->ydec, r->lv[lvl].qidx, tiled, r->tws, r->ths, r->lrf_cfg);
+  for (int p = 0; p < 3; p++) {
+    if (r->lrf_cfg[p].sb_h_shift || r->lrf_cfg[p].sb_v_shift) return -1;
+    const int n = r->lrf_cfg[p].cols * r->lrf_cfg[p].rows;
+    if (n != r->lrf_n[p]) {
+      free(r->lrf_units[p]);
+      r->lrf_units[p] = malloc(sizeof(orc_lrf_unit) * (size_t)n);
+      if (!r->lrf_units[p]) return -1;
+      r->lrf_n[p] = n;
+    }
+    for (int i = 0; i < n; i++) r->lrf_units[p][i] = (orc_lrf_unit){-1, {0, 0}};
+  }
+  const oinput *cur = &r->inputs[r->fi.display % r->n_inputs];
+  const oslot *S = &r->slots[r->fi.display % NSLOT];
+  const oplane *rec[3] = {&S->y, &S->u, &S->v}, *src[3] = {&cur->y, &cur->u, &cur->v};
+  const double lambda = r->lv[lvl].lambda;
+  enum { IIS = 264 };
+  uint16_t *pad16[3];
+  uint8_t *lin[3], *lout[3];
+  uint32_t *ii = malloc(sizeof(uint32_t) * IIS * 72), *sq = malloc(sizeof(uint32_t) * IIS * 72);
+  for (int p = 0; p < 3; p++) {
+    pad16[p] = malloc(sizeof(uint16_t) * 68 * 68);
+    lin[p] = malloc((size_t)64 * 64 * B);
+    lout[p] = malloc((size_t)64 * 64 * B);
+  }
+  const uint8_t ys = r->cdef_str[lvl][0], us = r->cdef_str[lvl][1];
+  const int pri_y = ys / 4, pri_uv = us / 4;
+  int sec_y = ys % 4, sec_uv = us % 4;
+  if (sec_y == 3) sec_y++;
+  if (sec_uv == 3) sec_uv++;
+  for (int t0y = 0; t0y < sbr; t0y += r->ths)
+    for (int t0x = 0; t0x < sbc; t0x += r->tws) {
+      const int tw_px = r->W - t0x * SB < r->tws * SB ? r->W - t0x * SB : r->tws * SB;
+      const int th_px = r->H - t0y * SB < r->ths * SB ? r->H - t0y * SB : r->ths * SB;
+      const int tsw = (tw_px + SB - 1) / SB, tsh = (th_px + SB - 1) / SB;
+      const int mi_cols = tw_px >> 2, mi_rows = th_px >> 2;
+      uint16_t cdf[4];
+      int8_t ref[3][2];
+      orc_lrf_tile_init(cdf, ref);
+      int ucols[3], urows[3];
+      for (int p = 0; p < 3; p++) {  /* TileRestorationState's unit view */
+        const int c = r->lrf_cfg[p].cols, rw = r->lrf_cfg[p].rows;
+        ucols[p] = t0x >= c ? 0 : (tsw < c - t0x ? tsw : c - t0x);
+        urows[p] = t0y >= rw ? 0 : (tsh < rw - t0y ? tsh : rw - t0y);
+      }
+      for (int sy = 0; sy < tsh; sy++)
+        for (int sx = 0; sx < tsw; sx++) {
+          /* the unit's input: the superblock's reconstruction, CDEF'd */
+          for (int p = 0; p < 3; p++) {
+            const int xd = p ? r->xdec : 0, yd = p ? r->ydec : 0;
+            const int bw = SB >> xd, bh = SB >> yd, pw_t = (tw_px + xd) >> xd, ph_t = (th_px + yd) >> yd;
+            const int ox = (sx * SB) >> xd, oy = (sy * SB) >> yd;
+            const int fx0 = (t0x * SB) >> xd, fy0 = (t0y * SB) >> yd;
+            for (int y = -2; y < bh + 2; y++)
+              for (int x = -2; x < bw + 2; x++) {
+                const int tx = ox + x, ty = oy + y;
+                uint16_t v = 0x8000;  /* CDEF_VERY_LARGE */
+                if (tx >= 0 && tx < pw_t && ty >= 0 && ty < ph_t) {
+                  const int csx = (tx << xd) / SB, csy = (ty << yd) / SB;
+                  v = (csy < sy || (csy == sy && csx <= sx))
+                          ? (uint16_t)orc_px(org_of(rec[p], hbd), hbd,
+                                             (ptrdiff_t)(fy0 + ty) * rec[p]->stride + fx0 + tx)
+                          : 128;
+                }
+                pad16[p][(y + 2) * (bw + 4) + x + 2] = v;
+              }
+            const int w = bw < pw_t - ox ? bw : pw_t - ox, h = bh < ph_t - oy ? bh : ph_t - oy;
+            for (int y = 0; y < bh; y++)  /* copy + Plane::pad (replicate) */
+              for (int x = 0; x < bw; x++) {
+                const int cx = x < w ? x : w - 1, cy = y < h ? y : h - 1;
+                orc_px_store(lin[p], hbd, y * bw + x,
+                             orc_px(org_of(rec[p], hbd), hbd,
+                                    (ptrdiff_t)(fy0 + oy + cy) * rec[p]->stride + fx0 + ox + cx));
+              }
+          }
+          if (r->cdef)
+            for (int by = 0; by < 8; by++)
+              for (int bx = 0; bx < 8; bx++) {
+                const int gx = sx * 16 + 2 * bx, gy = sy * 16 + 2 * by;
+                if (gx >= mi_cols || gy >= mi_rows) continue;
+                const int fx = t0x * 16 + gx, fy = t0y * 16 + gy;
+                const uint8_t *sk = r->mi_skip + (size_t)fy * r->mi_cols + fx;
+                const int skip = sk[0] & sk[1] & sk[r->mi_cols] & sk[r->mi_cols + 1];
+                int dir = 0;
+                int32_t var = 0;
+                if (!skip) dir = orc_cdef_find_dir(pad16[0] + (8 * by + 2) * 68 + 8 * bx + 2, 68, &var, cs);
+                for (int p = 0; p < 3; p++) {
+                  const int xd = p ? r->xdec : 0, yd = p ? r->ydec : 0, bw = SB >> xd;
+                  const int xs = 8 >> xd, ysz = 8 >> yd, x0 = (8 * bx) >> xd, y0 = (8 * by) >> yd;
+                  const uint16_t *in = pad16[p] + (y0 + 2) * (bw + 4) + x0 + 2;
+                  uint8_t *o = lin[p] + ((size_t)y0 * bw + x0) * B;
+                  if (!skip) {
+                    int pri, sec, dmp = 3 + cs, d;
+                    if (p == 0) {
+                      pri = orc_cdef_adjust_strength(pri_y << cs, var);
+                      sec = sec_y << cs;
+                      d = pri_y ? dir : 0;
+                    } else {
+                      pri = pri_uv << cs;
+                      sec = sec_uv << cs;
+                      dmp -= 1;
+                      d = pri_uv ? dir : 0;
+                    }
+                    orc_cdef_filter_block(o, bw, hbd, in, bw + 4, pri, sec, d, dmp, r->bd, xd, yd);
+                  } else {
+                    for (int i = 0; i < ysz; i++)
+                      for (int j = 0; j < xs; j++) orc_px_store(o, hbd, i * bw + j, in[i * (bw + 4) + j]);
+                  }
+                }
+              }
+          /* rdo_loop_decision's restoration pass (src/rdo.rs:2003-2116) */
+          orc_lrf_unit pick[3];
+          int has[3];
+          for (int p = 0; p < 3; p++) {
+            has[p] = sx < ucols[p] && sy < urows[p];
+            if (!has[p]) continue;
+            const int xd = p ? r->xdec : 0, yd = p ? r->ydec : 0, bw = SB >> xd;
+            const int pw = p ? (r->W + xd) >> xd : r->W, ph = p ? (r->H + yd) >> yd : r->H;
+            const int rx = (sx * SB) >> xd, ry = (sy * SB) >> yd;  /* tile-relative (quirk) */
+            const int us_ = r->lrf_cfg[p].unit_size;
+            const int uw = us_ < pw - rx ? us_ : pw - rx, uh = us_ < ph - ry ? us_ : ph - ry;
+            orc_lrf_unit best = {-1, {0, 0}};
+            const int8_t z[2] = {0, 0};
+            uint64_t err = lrf_plane_error(r, src[p], p, t0x, t0y, sx, sy, mi_cols, mi_rows, lin[p], bw);
+            double best_cost = (double)err + lambda * ((double)orc_lrf_rate(cdf, ref[p], -1, z) / 8.0);
+            orc_lrf_integral(lin[p], bw, lin[p], bw, hbd, 0, 0, uw, uh, uw, uh, ii, sq, IIS);
+            for (int k = 0; k < 64 * 64; k++) orc_px_store(lout[p], hbd, k, 128);
+            for (int set = 0; set < 16; set++) {
+              int8_t xqd[2];
+              orc_sgr_solve(set, r->bd, ii, sq, IIS, at(src[p], hbd, rx, ry), src[p]->stride, lin[p], bw,
+                            hbd, uw, uh, xqd);
+              orc_sgr_stripe_filter(set, xqd, r->bd, ii, sq, IIS, uw, uh, lin[p], bw, lout[p], bw, hbd);
+              err = lrf_plane_error(r, src[p], p, t0x, t0y, sx, sy, mi_cols, mi_rows, lout[p], bw);
+              const double cost =
+                  (double)err + lambda * ((double)orc_lrf_rate(cdf, ref[p], set, xqd) / 8.0);
+              if (cost < best_cost) {
+                best_cost = cost;
+                best = (orc_lrf_unit){(int8_t)set, {xqd[0], xqd[1]}};
+              }
+            }
+            pick[p] = best;
+            r->lrf_units[p][(t0y + sy) * r->lrf_cfg[p].cols + t0x + sx] = best;
+          }
+          for (int p = 0; p < 3; p++)  /* write_lrf, planes in order */
+            if (has[p]) orc_lrf_commit(cdf, ref[p], pick[p].set, pick[p].xqd);
+        }
+    }
+  for (int p = 0; p < 3; p++) {
+    free(pad16[p]);
+    free(lin[p]);
+    free(lout[p]);
+  }
+  free(ii);
+  free(sq);
+  return 0;
+}
+
+/* the loop filters in rav1e's order (src/encoder.rs:2789-2806) */
 static void loop_filter_planes(orc_replay *r) {
   deblock_planes(r);
+  if (!r->lrf) {
+    if (r->cdef) cdef_planes(r);
+    return;
+  }
+  /* pre_cdef_frame (:2795): the deblocked planes, for the stripes' edges */
+  oslot *S = &r->slots[r->fi.display % NSLOT];
+  oplane *pl[3] = {&S->y, &S->u, &S->v};
+  void *pre[3], *out[3];
+  ptrdiff_t st[3];
+  for (int p = 0; p < 3; p++) {
+    const size_t rowb = (size_t)pl[p]->w * px_of(r);
+    uint8_t *c = malloc(rowb * pl[p]->h);
+    for (int y = 0; y < pl[p]->h; y++)
+      memcpy(c + y * rowb, (const uint8_t *)org_of(pl[p], r->hbd) + (size_t)y * pl[p]->stride * px_of(r),
+             rowb);
+    pre[p] = c;
+    out[p] = org_of(pl[p], r->hbd);
+    st[p] = pl[p]->stride;
+  }
   if (r->cdef) cdef_planes(r);
+  /* the deblocked copy's pitch is the plane width, the output's the stride:
+   * lrf_filter_frame takes one stride, so the copy goes back to it */
+  for (int p = 0; p < 3; p++) {
+    const size_t rowb = (size_t)pl[p]->w * px_of(r);
+    uint8_t *w = malloc((size_t)st[p] * pl[p]->h * px_of(r));
+    for (int y = 0; y < pl[p]->h; y++)
+      memcpy(w + (size_t)y * st[p] * px_of(r), (const uint8_t *)pre[p] + y * rowb, rowb);
+    free(pre[p]);
+    pre[p] = w;
+  }
+  const orc_lrf_unit *u[3] = {r->lrf_units[0], r->lrf_units[1], r->lrf_units[2]};
+  orc_lrf_filter_frame(out, (const void *const *)pre, st, r->hbd, r->bd, r->W, r->H, r->xdec, r->ydec,
+                       r->lrf_cfg, u, r->cdef);
+  for (int p = 0; p < 3; p++) free(pre[p]);
 }
 
 static void pad(const orc_replay *r, oplane *p) {
@@ -2598,6 +2867,7 @@ int orc_replay_frame(orc_replay *r, orc_frame_info *info, int sb_limit, int pad_
     if (r->intra) run_pass(r, 4);
   }
   if (r->deblock || r->entropy) map_own(r);
+  if (r->lrf && lrf_decide(r) != 0) return -1;
   if (r->entropy) entropy_frame(r);
   if (r->deblock && pad_recon) loop_filter_planes(r);  /* tile groups: after the imports */
   r->tail[3] = (uint64_t)(r->vis_w / 8) * (r->vis_h / 8);

@@ -509,7 +509,7 @@ class CpuReplay:
     def __init__(self, width, height, xdec=1, ydec=1, bit_depth=8, n_refs=2, group=None,
                  tile_size=(0, 0), n_inputs=8, threads=1, L=None, quantizer=100, speed=10,
                  deblock=False, cdef=False, intra=True, entropy=False, mvref_standin=False,
-                 imp_window=0, imp_limit=0):
+                 imp_window=0, imp_limit=0, lrf=False):
         from rav1e_amd import rate as RT
         L = L or lib()
         self.L = L
@@ -563,8 +563,18 @@ class CpuReplay:
         L.orc_replay_set_imp_window.argtypes = [C.c_void_p, C.c_int, C.c_long]
         assert L.orc_replay_set_imp_window(self.h, imp_window, imp_limit) == 0, \
             "orc_replay_set_imp_window"
+        L.orc_replay_set_lrf.argtypes = [C.c_void_p, C.c_int]
+        assert L.orc_replay_set_lrf(self.h, 1 if lrf else 0) == 0, "orc_replay_set_lrf"
         self.imp_window = imp_window
         self.imp_shape = ((height + 7) // 8, (width + 7) // 8)
+
+    def lrf_units(self, plane, n):
+        """The last frame's loop-restoration units of plane p: (set, xqd0,
+        xqd1) per unit, set -1 = None."""
+        out = np.zeros(3 * n, np.int8)
+        self.L.orc_replay_lrf_units.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int]
+        self.L.orc_replay_lrf_units(self.h, plane, out.ctypes.data, out.size)
+        return out.reshape(n, 3)
 
     def importances(self):
         """The block importances the last coded frame's RDO used

@@ -194,6 +194,36 @@ def test_cpu_replay_deblock_changes_the_reference():
     assert (recs[0] != recs[1]).any()
 
 
+def test_cpu_replay_loop_restoration():
+    """RV_REPLAY_LRF: every unit of the coded frame (one 64x64 superblock in
+    luma, 32x32 in 4:2:0 chroma at the levels' quantizers) gets rav1e's
+    rdo_loop_decision choice -- None or a self-guided set whose xqd lie in
+    SGRPROJ_XQD_MIN .. MAX -- and lrf_filter_frame changes the reference
+    after CDEF; the first frame's searches do not change."""
+    w, h = 256, 192
+    fr = _frames(w, h, 1, 1, 8, 8)
+    outs, recs, units = [], [], []
+    for lrf in (False, True):
+        r = O.CpuReplay(w, h, 1, 1, 8, 2, n_inputs=8, threads=2, deblock=True, cdef=True, lrf=lrf,
+                        tile_size=(2, 2))
+        for i, f in enumerate(fr):
+            r.set_input(i, f)
+        r.frame()
+        r.frame()
+        outs.append(_sb_words(r.results(), 8, 2))
+        recs.append(r.get_recon(4))
+        if lrf:
+            units = [r.lrf_units(p, n) for p, n in ((0, 4 * 3), (1, 4 * 3), (2, 4 * 3))]
+    np.testing.assert_array_equal(outs[0][:, :2 * PER_REF], outs[1][:, :2 * PER_REF])
+    y = units[0]
+    assert (y[:, 0] >= -1).all() and (y[:, 0] < 16).all()
+    on = y[y[:, 0] >= 0]
+    assert len(on) > 0, "no unit chose a filter"
+    assert (on[:, 1] >= -96).all() and (on[:, 1] <= 31).all()
+    assert (on[:, 2] >= -32).all() and (on[:, 2] <= 95).all()
+    assert (recs[0] != recs[1]).any()
+
+
 def test_cpu_replay_speed10_edge_superblocks_must_split():
     """Speed 10 (minimum block 64x64): a superblock past the bottom edge is
     split as encode_partition_topdown's must_split does (src/encoder.rs:
