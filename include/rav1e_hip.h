@@ -611,6 +611,17 @@ typedef struct rv_replay_cfg {
  * motion-search MVs (every superblock independent, one pass; zero rate
  * predictors): an A/B of the rounds' cost, not rav1e's decisions. */
 #define RV_REPLAY_MVREF_STANDIN 256
+/* flags (with RV_REPLAY_CDEF): loop restoration of every coded frame, the
+ * self-guided filter (rav1e evaluates no Wiener filter): each unit's choice
+ * as rdo_loop_decision makes it while the tile is coded (src/rdo.rs:
+ * 1726-2120; the unit's input is the reconstruction so far with CDEF index
+ * 0, None and the 16 parameter sets solved, filtered and priced with
+ * count_lrf_switchable), then lrf_filter_frame after CDEF (src/lrf.rs:
+ * 1345-1444, src/encoder.rs:2803-2806).  Units of one superblock in every
+ * plane (RestorationState::new at base_q_idx <= 160, every level of the
+ * default quantizer); one tile group.  The symbol prices assume a range
+ * coder in its initial state (the replay codes no other symbols). */
+#define RV_REPLAY_LRF 512
 typedef struct rv_replay_frame_info {
   int32_t display;            /* display index of the coded frame */
   int32_t me_range_scale;     /* 4 >> pyramid level (src/encoder.rs:838) */
@@ -795,6 +806,10 @@ int rv_round_ring_slots(uint32_t q, int32_t *out, int cap);
  * src/api/internal.rs:875-882; with 2 references a frame above pyramid
  * level 0 adds LAST3): out[0] = their count, out[1..3] their displays,
  * out[4..6] the propagation order.  Returns 0. */
+/* RV_REPLAY_LRF: the last coded frame's loop-restoration units of plane p,
+ * (set, xqd0, xqd1) int8 triples in raster order of the superblocks (set -1:
+ * RestorationFilter::None); cap >= 3 x superblocks.  Synchronous. */
+int rv_replay_lrf_units(rv_replay *r, int plane, int8_t *out, int cap);
 int rv_replay_la_refs(long m, int R, int32_t *out);
 int rv_replay_kernel_probe(rv_replay *r, double *out, int cap);
 /* Candidate evaluations summed over the last min(frames, 64) coded frames:

@@ -303,6 +303,7 @@ def _declare(L):
         "rv_replay_set_kernel_probe": (i32, [vp, i32]),
         "rv_replay_kernel_probe": (i32, [vp, vp, i32]),
         "rv_round_ring_slots": (i32, [C.c_uint32, vp, i32]),
+        "rv_replay_lrf_units": (i32, [vp, i32, vp, i32]),
         "rv_replay_la_refs": (i32, [C.c_long, i32, vp]),
         "rv_la_hub_create": (vp, [i32]),
         "rv_la_hub_destroy": (None, [vp]),

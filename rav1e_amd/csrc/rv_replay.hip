@@ -47,6 +47,7 @@
 #include "rv_intra_pass.h"
 #include "rv_mvref.h"
 #include "rv_impwin.h"
+#include "rv_lrf.h"
 #include "rv_rdo.h"
 #include <string>
 
@@ -1158,6 +1159,12 @@ struct rv_replay {
   int64_t *db_tally = nullptr;
   uint8_t *db_dlev = nullptr;
   bool cdef = false;                // RV_REPLAY_CDEF
+  // RV_REPLAY_LRF: the units' distortions / solved xqd per (plane,
+  // superblock), the units' filters, the restored frame before its padding
+  bool lrf = false;
+  uint64_t *lrf_err = nullptr;
+  int8_t *lrf_xqd = nullptr, *lrf_units = nullptr;
+  RvInput lrf_out;
   RvInput cdef_pre;                 // the deblocked, pre-CDEF frame (the padded copy's source)
   uint8_t *cdef_dir = nullptr, *cdef_idx = nullptr;  // per 8x8 block; per 64x64 (all 0)
   int32_t *cdef_var = nullptr;
@@ -1712,7 +1719,7 @@ int deblock_slot(rv_replay *r, const RvSlot &s, const RvInput &in, int lv) {
 // scratch frame is copied back and padded in one pass (rv_frame_pad_dev) --
 // three launches.  cdef_bits 0: every superblock uses entry 0 of the
 // tables, the level's strengths.
-int cdef_pad_slot(rv_replay *r, const RvSlot &s, int lv) {
+int cdef_pad_slot(rv_replay *r, const RvSlot &s, int lv, const LrfGeo *lg) {
   const rv_plane rec[3] = {s.y, s.u, s.v};
   const rv_plane out[3] = {r->cdef_pre.y, r->cdef_pre.u, r->cdef_pre.v};
   uint8_t ys[8] = {}, us[8] = {};
@@ -1723,14 +1730,30 @@ int cdef_pad_slot(rv_replay *r, const RvSlot &s, int lv) {
   // cdef_damping = 3 (src/encoder.rs:665)
   RV_R(rv_cdef_filter_frame_dev(rec, out, r->g.W, r->g.H, r->mi_skip, r->mi_stride, r->cdef_dir,
                                 r->cdef_var, r->cdef_idx, ys, us, 3, r->g.bd, r->stream));
-  return rv_frame_pad_dev(rec, out, r->stream);
+  if (!lg) return rv_frame_pad_dev(rec, out, r->stream);
+  // lrf_filter_frame: the CDEF output restored, the deblocked slot for the
+  // stripes' edges (pre_cdef_frame, src/encoder.rs:2795-2806)
+  const rv_plane lo[3] = {r->lrf_out.y, r->lrf_out.u, r->lrf_out.v};
+  RV_R(lrf_filter_launch(out, rec, lo, *lg, r->lrf_units, 1, r->stream));
+  return rv_frame_pad_dev(rec, lo, r->stream);
 }
 
 // The loop filters of a coded slot and its padding: the frame is then a
 // reference (src/encoder.rs:2789-2802, 3411-3429).
 int filter_slot(rv_replay *r, const RvSlot &s, const RvInput &in, int lv) {
+  LrfGeo lg;
+  if (r->lrf) {
+    // rdo_loop_decision's restoration choices, from the reconstruction as
+    // the tile's coding leaves it (before the deblocking)
+    const Geo &g = r->g;
+    RV_R(lrf_geometry(g.W, g.H, g.xdec, g.ydec, g.bd, r->lv[lv].qidx, g.tws, g.ths, &lg));
+    const rv_plane rec[3] = {s.y, s.u, s.v}, src[3] = {in.y, in.u, in.v};
+    RV_R(lrf_rdo_launch(rec, src, r->mi_skip, r->mi_stride, r->imp_last, g.w_imp, g.w_in_b, g.h_in_b, lg,
+                        r->cdef, r->cdef_str[lv], r->lv[lv].ds, r->lrf_err, r->lrf_xqd, r->lv[lv].lambda,
+                        r->lrf_units, r->stream));
+  }
   if (r->deblock) RV_R(deblock_slot(r, s, in, lv));
-  return r->cdef ? cdef_pad_slot(r, s, lv) : pad_slot(r, s);
+  return r->cdef ? cdef_pad_slot(r, s, lv, r->lrf ? &lg : nullptr) : pad_slot(r, s);
 }
 
 // Coding order of the reorder pyramid: coded frame n >= 1 (n = 0 is the
@@ -2274,6 +2297,21 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     r->cdef_idx = (uint8_t *)dalloc(r, n64);
     ok = ok && r->cdef_dir && r->cdef_var && r->cdef_idx && alloc_input(r, r->cdef_pre, false);
     if (r->cdef_idx) (void)hipMemsetAsync(r->cdef_idx, 0, n64, r->stream);
+  }
+  if (cfg->flags & RV_REPLAY_LRF) {
+    LrfGeo lg;
+    if (!r->cdef || lrf_geometry(g.W, g.H, g.xdec, g.ydec, g.bd, 100, g.tws, g.ths, &lg) != RV_OK ||
+        g.tx0 || g.ty0 || g.tw * kSb < g.W || g.th * kSb < g.H) {
+      rv_set_error(RV_EINVAL, "rv_replay_create: RV_REPLAY_LRF needs RV_REPLAY_CDEF, one tile group "
+                              "and units of one superblock");
+      rv_replay_destroy(r);
+      return nullptr;
+    }
+    r->lrf = true;
+    r->lrf_err = (uint64_t *)dalloc(r, (size_t)3 * lg.nsb * 17 * 8);
+    r->lrf_xqd = (int8_t *)dalloc(r, (size_t)3 * lg.nsb * 32);
+    r->lrf_units = (int8_t *)dalloc(r, (size_t)3 * lg.nsb * 3);
+    ok = ok && r->lrf_err && r->lrf_xqd && r->lrf_units && alloc_input(r, r->lrf_out, false);
   }
   r->entropy = (cfg->flags & RV_REPLAY_ENTROPY) != 0;
   if (r->entropy && g.xdec != g.ydec) {
@@ -4406,6 +4444,19 @@ int rv_round_ring_slots(uint32_t q, int32_t *out, int cap) {
 // Host-only test hook: the lookahead references of coded frame m >= 1
 // (la_refs_of): out[0] = n, out[1..3] their displays in k order, out[4..6]
 // the propagation order (-1: unused).  Returns 0.
+// RV_REPLAY_LRF: the last coded frame's loop-restoration units of plane p,
+// (set, xqd0, xqd1) per unit in raster order (set -1: None); synchronous
+int rv_replay_lrf_units(rv_replay *r, int plane, int8_t *out, int cap) {
+  if (!r || !out || plane < 0 || plane > 2) return rv_set_error(RV_EINVAL, "rv_replay_lrf_units: bad arguments");
+  if (!r->lrf) return rv_set_error(RV_EINVAL, "rv_replay_lrf_units: RV_REPLAY_LRF is off");
+  const Geo &g = r->g;
+  const int nsb = ((g.W + 63) / 64) * ((g.H + 63) / 64);
+  if (cap < 3 * nsb) return rv_set_error(RV_EINVAL, "rv_replay_lrf_units: cap < 3 * superblocks");
+  RV_H(hipStreamSynchronize(r->stream));
+  RV_H(hipMemcpy(out, r->lrf_units + (size_t)plane * nsb * 3, (size_t)nsb * 3, hipMemcpyDeviceToHost));
+  return RV_OK;
+}
+
 int rv_replay_la_refs(long m, int R, int32_t *out) {
   if (!out || m < 1 || R < 1 || R > 2) return rv_set_error(RV_EINVAL, "rv_replay_la_refs");
   const LaRefs l = la_refs_of(m, R);

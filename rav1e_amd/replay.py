@@ -25,6 +25,7 @@ RV_REPLAY_EXHAUSTIVE_FS = 4  # F1 without successive elimination (same results)
 RV_REPLAY_SPEED6 = 8  # the speed-6 schedule: partition RDO 64x64 .. 8x8 (config D)
 RV_REPLAY_DEBLOCK = 16  # deblock every coded frame before it becomes a reference (1 group)
 RV_REPLAY_CDEF = 32  # CDEF after deblocking (needs RV_REPLAY_DEBLOCK), cdef_bits 0
+RV_REPLAY_LRF = 512  # loop restoration (self-guided) after CDEF (needs RV_REPLAY_CDEF, one group)
 RV_REPLAY_NO_INTRA = 64  # no intra-mode screening of non-skip superblocks (default: on
 #                          at speed 10 in 4:2:0)
 RV_REPLAY_ENTROPY = 128  # F8: code every frame's coefficients (device tokens, host range coder)
@@ -337,6 +338,14 @@ class HipReplay:
         out = self._frame_array()
         _check(lib().rv_replay_get_input(self.h, idx, out.ctypes.data), "rv_replay_get_input")
         return out
+
+    def lrf_units(self, plane: int) -> np.ndarray:
+        """RV_REPLAY_LRF: the last frame's units of plane p, (set, xqd0,
+        xqd1) per superblock (set -1: None)."""
+        n = ((self.cfg.width + 63) // 64) * ((self.cfg.height + 63) // 64)
+        out = np.zeros(3 * n, np.int8)
+        _check(lib().rv_replay_lrf_units(self.h, plane, out.ctypes.data, out.size), "rv_replay_lrf_units")
+        return out.reshape(n, 3)
 
     def get_recon(self, display: int) -> np.ndarray:
         out = self._frame_array()

@@ -441,6 +441,9 @@ def intra_frames(w, h, xdec, ydec, bd, n, seed=7):
     return out
 
 
+_LRF = RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF | RP.RV_REPLAY_LRF
+
+
 def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=None, quantizer=100,
                 inputs=None, want_intra=False, imp_window=0, ready=False):
     import rav1e_amd as R
@@ -463,9 +466,10 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
                     cdef=bool(flags & RP.RV_REPLAY_CDEF),
                     intra=not flags & RP.RV_REPLAY_NO_INTRA,
                     mvref_standin=bool(flags & RP.RV_REPLAY_MVREF_STANDIN),
-                    imp_window=imp_window, imp_limit=frames)
+                    imp_window=imp_window, imp_limit=frames, lrf=bool(flags & RP.RV_REPLAY_LRF))
     for i in range(nin):
         c.set_input(i, g.get_input(i))
+    nsb = ((w + 63) // 64) * ((h + 63) // 64)
     if imp is not None:
         g.set_importances(imp)
         c.set_importances(imp)
@@ -476,6 +480,10 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
         gw, cw = g.results(), c.results()
         bad = np.nonzero(gw != cw)[0]
         assert bad.size == 0, (n, gi, bad[:10], gw[bad[:10]], cw[bad[:10]])
+        if flags & RP.RV_REPLAY_LRF and not gi["is_key"]:
+            for p in range(3):  # every unit's choice (set, xqd)
+                np.testing.assert_array_equal(g.lrf_units(p), c.lrf_units(p, nsb),
+                                              err_msg="frame %d plane %d units" % (n, p))
         if imp_window:
             gimp, cimp = g.importances(), c.importances()
             np.testing.assert_array_equal(gimp.view(np.uint32), cimp.view(np.uint32),
@@ -522,6 +530,12 @@ def _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, frames, tiling=None, flags=0, imp=No
     (256, 136, 1, 0, 8, 2, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF),
     (256, 200, 1, 1, 8, 2, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF | RP.RV_REPLAY_SPEED6),
     (192, 128, 0, 0, 12, 1, None, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF | RP.RV_REPLAY_SPEED6),
+    # loop restoration after CDEF: the units' choices and the restored frame
+    (256, 200, 1, 1, 8, 2, None, _LRF),
+    (192, 136, 0, 0, 10, 2, None, _LRF),
+    (384, 192, 1, 1, 8, 2, {"tile_cols": 2}, _LRF),
+    (192, 128, 1, 1, 12, 1, None, _LRF),
+    (256, 200, 1, 1, 8, 2, None, _LRF | RP.RV_REPLAY_SPEED6),
 ])
 def test_gpu_replay_matches_cpu_replay(w, h, xdec, ydec, bd, refs, tiling, flags):
     _gpu_vs_cpu(w, h, xdec, ydec, bd, refs, 10, tiling, flags)
