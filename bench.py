@@ -255,10 +255,11 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     cd = bool(flags & RP.RV_REPLAY_CDEF)
     ent = bool(flags & RP.RV_REPLAY_ENTROPY)
     sti = bool(flags & RP.RV_REPLAY_MVREF_STANDIN)
+    lrf = bool(flags & RP.RV_REPLAY_LRF)
     limit = CPU_FRAMES + 1 if imp_window else 0
     c = O.CpuReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=nin, threads=threads, L=L,
                     speed=speed, deblock=db, cdef=cd, entropy=ent, mvref_standin=sti,
-                    imp_window=imp_window, imp_limit=limit)
+                    imp_window=imp_window, imp_limit=limit, lrf=lrf)
     for i in range(nin):
         c.set_input(i, hip_inputs[i])
     c.frame()  # the key frame (a copy), untimed
@@ -307,7 +308,7 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     g = RP.HipReplay(W, H, xdec, ydec, bd, nref, tile_size=ts, n_inputs=n_inputs,
                      flags=flags & (RP.RV_REPLAY_SPEED6 | RP.RV_REPLAY_DEBLOCK |
                                     RP.RV_REPLAY_CDEF | RP.RV_REPLAY_ENTROPY |
-                                    RP.RV_REPLAY_MVREF_STANDIN),
+                                    RP.RV_REPLAY_MVREF_STANDIN | RP.RV_REPLAY_LRF),
                      imp_window=imp_window, imp_limit=limit)
     g.synth_inputs(0)
     g.frame()
@@ -352,7 +353,7 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2, imp_wind
     frames = 1 + gops * gop
     nin = frames + 8 + (imp_window + 37 if imp_window else 0)
     gs = [RP.HipReplay(W, H, xdec, ydec, bd, nref, group=r, tile_size=ts, n_inputs=nin,
-                       flags=flags, imp_window=imp_window) for r in rects]
+                       flags=flags & ~RP.RV_REPLAY_LRF, imp_window=imp_window) for r in rects]
     # the importance window: each group's engine computes its blocks' part,
     # the parts meet in an in-process hub (the ranks' RCCL all-gather)
     hub = RP.LaHub(n) if imp_window else None
@@ -434,12 +435,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--speed", type=int, choices=(6, 10), default=None,
                     help="schedule (default: the config's BASELINE speed)")
-    ap.add_argument("--loop-filters", choices=("all", "deblock", "none"), default="all",
+    ap.add_argument("--loop-filters", choices=("all", "cdef", "deblock", "none"), default="all",
                     help="the in-loop filters every coded frame runs before it becomes a "
                          "reference: rav1e's deblocking (fast levels at speed >= 8, "
-                         "sse_optimize below) and CDEF (cdef_preset is always true, "
-                         "src/api/config.rs:421-423; src/encoder.rs:2789-2803) -- the default; "
-                         "'deblock' / 'none' for A/B")
+                         "sse_optimize below), CDEF (cdef_preset is always true, "
+                         "src/api/config.rs:421-423) and loop restoration (enable_restoration "
+                         "on 4:2:0 / 4:4:4, src/encoder.rs:229-230, 2789-2806; one tile group: "
+                         "off with several ranks) -- the default; 'cdef' / 'deblock' / 'none' "
+                         "for A/B")
     ap.add_argument("--emulate-ranks", type=int, default=8,
                     help="N > 1 (single-GPU runs): also code the N-rank tile-group split as N "
                          "replays on this GPU and report the projected N-rank step (0: off)")
@@ -487,12 +490,16 @@ def main():
     # the run is inside the timed region, as in a streaming encode, and it
     # never runs out of inputs before the last timed frame
     n_inputs = args.warmup + args.steps + 8 + (imp_window + 29 + 8 if imp_window else 0)
-    deblock = args.loop_filters in ("all", "deblock")
-    cdef = args.loop_filters == "all"
+    deblock = args.loop_filters in ("all", "cdef", "deblock")
+    cdef = args.loop_filters in ("all", "cdef")
+    # loop restoration: one tile group (rv_replay_create); 4:2:2 has none
+    # (enable_restoration, src/encoder.rs:229-230)
+    lrf = args.loop_filters == "all" and world == 1 and not (xdec == 1 and ydec == 0)
     flags = (RP.RV_REPLAY_EXHAUSTIVE_FS if args.exhaustive_fs else 0) | \
         (RP.RV_REPLAY_SPEED6 if speed == 6 else 0) | (RP.RV_REPLAY_DEBLOCK if deblock else 0) | \
         (RP.RV_REPLAY_CDEF if cdef else 0) | (0 if args.no_entropy else RP.RV_REPLAY_ENTROPY) | \
-        (RP.RV_REPLAY_MVREF_STANDIN if args.mv_stack == "standin" else 0)
+        (RP.RV_REPLAY_MVREF_STANDIN if args.mv_stack == "standin" else 0) | \
+        (RP.RV_REPLAY_LRF if lrf else 0)
     hip = RP.HipReplay(W, H, xdec, ydec, bd, nref, group=rects[rank], tile_size=ts,
                        n_inputs=n_inputs, flags=flags, imp_window=imp_window,
                        imp_limit=0)
@@ -746,7 +753,7 @@ def main():
                                    f"{nref} refs, reorder-pyramid coding order"
                                    f"{'' if args.no_entropy else ', coefficients entropy-coded'}",
                        "width": W, "height": H, "refs": nref, "speed": speed,
-                       "deblock": deblock, "cdef": cdef,
+                       "deblock": deblock, "cdef": cdef, "loop_restoration": lrf,
                        "tiles": [tiling["cols"], tiling["rows"]],
                        "parallelism": f"tile-groups{world}",
                        "frame_concurrency": (("levels 0/1 + 4g+1 on the primary, 4g+3 on a "

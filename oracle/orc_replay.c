@@ -754,13 +754,22 @@ int orc_replay_set_lrf(orc_replay *r, int on) {
   r->lrf = on != 0;
   return 0;
 }
-/* the last frame's unit filters of plane p: (set, xqd0, xqd1) per unit */
+/* the last frame's unit filters of plane p: (set, xqd0, xqd1) per
+ * superblock in raster order (a superblock without a unit of its own --
+ * stretched into its neighbour's -- reads None) */
 void orc_replay_lrf_units(const orc_replay *r, int plane, int8_t *out, int cap) {
-  for (int i = 0; i < r->lrf_n[plane] && 3 * i + 2 < cap; i++) {
-    out[3 * i] = r->lrf_units[plane][i].set;
-    out[3 * i + 1] = r->lrf_units[plane][i].xqd[0];
-    out[3 * i + 2] = r->lrf_units[plane][i].xqd[1];
-  }
+  const int sbc = (r->W + SB - 1) / SB, sbr = (r->H + SB - 1) / SB;
+  const orc_lrf_plane_cfg *c = &r->lrf_cfg[plane];
+  for (int y = 0; y < sbr; y++)
+    for (int x = 0; x < sbc; x++) {
+      const int i = y * sbc + x;
+      if (3 * i + 2 >= cap) return;
+      orc_lrf_unit u = {-1, {0, 0}};
+      if (x < c->cols && y < c->rows && r->lrf_units[plane]) u = r->lrf_units[plane][y * c->cols + x];
+      out[3 * i] = u.set;
+      out[3 * i + 1] = u.xqd[0];
+      out[3 * i + 2] = u.xqd[1];
+    }
 }
 
 /* the levels deblock_filter_optimize chose for the last deblocked frame */

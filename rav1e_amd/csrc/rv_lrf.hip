@@ -549,7 +549,12 @@ __global__ void lrf_decide_kernel(LrfDecideArgs a) {
       bool has[3];
       for (int p = 0; p < 3; p++) {
         has[p] = fsx < g.cols[p] && fsy < g.rows[p];
-        if (!has[p]) continue;
+        if (!has[p]) {  // stretched into its neighbour's unit: none of its own
+          int8_t *u = a.units + (((size_t)p * g.urows_max + fsy) * g.ucols_max + fsx) * 3;
+          u[0] = -1;
+          u[1] = u[2] = 0;
+          continue;
+        }
         const uint64_t *e = a.err + ((size_t)p * g.nsb + sb) * 17;
         const int8_t *xq = a.xqd + ((size_t)p * g.nsb + sb) * 32;
         int best = -1;
@@ -666,9 +671,10 @@ int lrf_geometry(int width, int height, int xdec, int ydec, int bit_depth, int b
   LrfPlaneCfg c[3];
   lrf_config(width, height, xdec, ydec, base_q_idx, tiled, g->tws, g->ths, c);
   for (int p = 0; p < 3; p++) {
-    // one superblock per unit (and no stretched unit: the last one covers
-    // at most its superblock), the shape every BASELINE config has
-    if (c[p].sb_h_shift || c[p].sb_v_shift || c[p].cols != g->sbc || c[p].rows != g->sbr)
+    // one superblock per unit, the shape of every BASELINE config (a last
+    // superblock row / column narrower than half a unit is stretched into
+    // the unit before it: it has no unit of its own)
+    if (c[p].sb_h_shift || c[p].sb_v_shift || c[p].cols > g->sbc || c[p].rows > g->sbr)
       return rv_set_error(RV_EINVAL, "loop restoration: units of one superblock only");
     g->unit[p] = c[p].unit_size;
     g->cols[p] = c[p].cols;
