@@ -91,8 +91,7 @@ __host__ __device__ inline uint32_t lrf_symbol_bits(uint32_t s, const uint16_t *
     r = full - ((rng * fh) >> 1) - ((uint32_t)nsym - s - 1) * 4;
   }
   const uint32_t pre = lrf_frac_compute((uint32_t)(cnt + 9), full);
-  int lg = 0;
-  for (uint32_t t = r; t; t >>= 1) lg++;
+  const int lg = 32 - __builtin_clz(r);  // r >= 4
   const int d = 16 - lg;
   int c = cnt, bits = 0, sh = c + d;
   if (sh >= 0) {
@@ -159,14 +158,18 @@ __host__ __device__ inline void lrf_tile_init(LrfTileState &s) {
   }
 }
 __host__ __device__ inline bool lrf_set_has(int set, int i);
-// count_lrf_switchable; set < 0: None
-__host__ __device__ inline uint32_t lrf_rate(const LrfTileState &s, int p, int set, const int8_t *xqd) {
-  if (set < 0) return lrf_symbol_bits(0, s.cdf, 3);
-  uint32_t bits = lrf_symbol_bits(2, s.cdf, 3) + (4u << 3);  // + SGRPROJ_PARAMS_BITS
-  const int lo[2] = {-96, -32}, hi[2] = {31, 95};
-  for (int i = 0; i < 2; i++)
-    if (lrf_set_has(set, i)) bits += lrf_subexp_ref(xqd[i], lo[i], hi[i] + 1, 4, s.ref[p][i]);
+// count_lrf_switchable at restoration CDF cdf and the plane's sgrproj_ref
+// (r0, r1); set < 0: None
+__host__ __device__ inline uint32_t lrf_rate_at(const uint16_t *cdf, int r0, int r1, int set, int x0, int x1) {
+  if (set < 0) return lrf_symbol_bits(0, cdf, 3);
+  uint32_t bits = lrf_symbol_bits(2, cdf, 3) + (4u << 3);  // + SGRPROJ_PARAMS_BITS
+  if (lrf_set_has(set, 0)) bits += lrf_subexp_ref(x0, -96, 32, 4, r0);
+  if (lrf_set_has(set, 1)) bits += lrf_subexp_ref(x1, -32, 96, 4, r1);
   return bits;
+}
+__host__ __device__ inline uint32_t lrf_rate(const LrfTileState &s, int p, int set, const int8_t *xqd) {
+  return set < 0 ? lrf_rate_at(s.cdf, 0, 0, -1, 0, 0)
+                 : lrf_rate_at(s.cdf, s.ref[p][0], s.ref[p][1], set, xqd[0], xqd[1]);
 }
 // write_lrf's updates (src/context.rs:3596-3659): symbol_with_update's
 // update_cdf (src/ec.rs:891-905) and the plane's sgrproj_ref
@@ -226,7 +229,7 @@ int lrf_geometry(int width, int height, int xdec, int ydec, int bit_depth, int b
                  int tile_h_sb, LrfGeo *g);
 int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *skip, int mi_stride,
                    const float *imp, int w_imp, int w_in_b, int h_in_b, const LrfGeo &g, int cdef,
-                   const uint8_t cdef_str[2], const double ds[3], uint64_t *err, int8_t *xqd,
-                   double lambda, int8_t *units, hipStream_t s);
+                   const uint8_t *dir, const int32_t *var, const uint8_t cdef_str[2], const double ds[3],
+                   uint64_t *err, int8_t *xqd, double lambda, int8_t *units, hipStream_t s);
 int lrf_filter_launch(const rv_plane cd[3], const rv_plane db[3], const rv_plane out[3], const LrfGeo &g,
                       const int8_t *units, int enable_cdef, hipStream_t s);

@@ -22,6 +22,8 @@
 //    above and below the stripe), the unit's set, the restored pixels.
 // All of it is integer work but sgrproj_solve's tail, whose f64 operations
 // run in the reference's order (IEEE division, no contraction).
+#include <stddef.h>
+#include <type_traits>
 #include <string.h>
 
 #include "rv_device.h"
@@ -59,18 +61,25 @@ __device__ __forceinline__ int cdef_adjust(int strength, int32_t var) {  // :232
   const int i = (var >> 6) ? min(msb32(var >> 6), 12) : 0;
   return var ? (strength * (4 + i) + 8) >> 4 : 0;
 }
-// in: the padded u16 input at the pixel, pitch s
-__device__ inline int cdef_px(const uint16_t *in, int s, int pri, int sec, int dir, int damping,
-                              int cs) {
+// the taps' offsets in a buffer of pitch s: [dir][k][primary, the two
+// secondaries], from cdef_directions (one lane per entry)
+__device__ __forceinline__ void cdef_offsets(int16_t *offs, int s) {
+  const int t = threadIdx.x;
+  if (t < 48) {
+    const int dir = t / 6, k = (t / 3) & 1, j = t % 3;
+    const int d = j == 0 ? dir : j == 1 ? (dir + 2) & 7 : (dir + 6) & 7;
+    offs[t] = (int16_t)(kLrfCdefDirs[d][k][0] * s + kLrfCdefDirs[d][k][1]);
+  }
+}
+// in: the padded u16 input at the pixel; off: cdef_offsets of its direction
+__device__ inline int cdef_px(const uint16_t *in, const int16_t *off, int pri, int sec, int damping, int cs) {
   const int x = in[0];
   const int odd = (pri >> cs) & 1;
   int sum = 0, mx = x, mn = x;
 #pragma unroll
   for (int k = 0; k < 2; k++) {
     const int pt = odd ? 3 : (k ? 2 : 4), st = k ? 1 : 2;
-    const int d0 = kLrfCdefDirs[dir][k][0] * s + kLrfCdefDirs[dir][k][1];
-    const int d1 = kLrfCdefDirs[(dir + 2) & 7][k][0] * s + kLrfCdefDirs[(dir + 2) & 7][k][1];
-    const int d2 = kLrfCdefDirs[(dir + 6) & 7][k][0] * s + kLrfCdefDirs[(dir + 6) & 7][k][1];
+    const int d0 = off[3 * k], d1 = off[3 * k + 1], d2 = off[3 * k + 2];
     const int p0 = in[d0], p1 = in[-d0];
     sum += pt * (cdef_constrain(p0 - x, pri, damping) + cdef_constrain(p1 - x, pri, damping));
     if (p0 != kVeryLarge) mx = max(p0, mx);
@@ -86,74 +95,6 @@ __device__ inline int cdef_px(const uint16_t *in, int s, int pri, int sec, int d
   }
   return iclamp(x + ((8 + sum - (sum < 0)) >> 4), mn, mx);
 }
-// cdef_find_dir (src/cdef.rs:68-126) of the 8x8 luma block at p (pitch s);
-// u32 wrapping like the reference's release build
-template <typename Px>
-__device__ inline int cdef_dir(const Px *p, int64_t s, int cs, int32_t *var) {
-  int32_t partial[8][15];
-#pragma unroll
-  for (int d = 0; d < 8; d++)
-#pragma unroll
-    for (int k = 0; k < 15; k++) partial[d][k] = 0;
-#pragma unroll
-  for (int r = 0; r < 8; r++)
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-      const int32_t x = ((int)p[r * s + c] >> cs) - 128;
-      partial[0][r + c] += x;
-      partial[1][r + c / 2] += x;
-      partial[2][r] += x;
-      partial[3][3 + r - c / 2] += x;
-      partial[4][7 + r - c] += x;
-      partial[5][3 - r / 2 + c] += x;
-      partial[6][c] += x;
-      partial[7][r / 2 + c] += x;
-    }
-  constexpr uint32_t div[9] = {0, 840, 420, 280, 210, 168, 140, 120, 105};
-  uint32_t cost[8];
-#define SQ(v) ((uint32_t)(v) * (uint32_t)(v))
-  cost[2] = cost[6] = 0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    cost[2] += SQ(partial[2][k]);
-    cost[6] += SQ(partial[6][k]);
-  }
-  cost[2] *= div[8];
-  cost[6] *= div[8];
-  cost[0] = SQ(partial[0][7]) * div[8];
-  cost[4] = SQ(partial[4][7]) * div[8];
-#pragma unroll
-  for (int k = 0; k < 7; k++) {
-    cost[0] += (SQ(partial[0][k]) + SQ(partial[0][14 - k])) * div[k + 1];
-    cost[4] += (SQ(partial[4][k]) + SQ(partial[4][14 - k])) * div[k + 1];
-  }
-#pragma unroll
-  for (int d = 1; d < 8; d += 2) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < 5; k++) c += SQ(partial[d][3 + k]);
-    c *= div[8];
-#pragma unroll
-    for (int k = 0; k < 3; k++) c += (SQ(partial[d][k]) + SQ(partial[d][10 - k])) * div[2 * k + 2];
-    cost[d] = c;
-  }
-#undef SQ
-  int best = 0;
-  int32_t best_cost = (int32_t)cost[0];
-#pragma unroll
-  for (int d = 1; d < 8; d++)
-    if ((int32_t)cost[d] > best_cost) {
-      best = d;
-      best_cost = (int32_t)cost[d];
-    }
-  uint32_t orth = cost[0];
-#pragma unroll
-  for (int d = 1; d < 8; d++)
-    if (d == ((best + 4) & 7)) orth = cost[d];
-  *var = (int32_t)((uint32_t)best_cost - orth) >> 10;
-  return best;
-}
-
 // ---- distortion (src/rdo.rs) -------------------------------------------------
 // compute_distortion_bias of an 8x8 at 4x4 block (mi_x, mi_y) (src/rdo.rs:
 // 476-508): f32 mean of its importance cells / 3 + 0.65
@@ -182,78 +123,136 @@ __device__ inline uint64_t cdef_dist(int32_t ss, int32_t sd, uint32_t ss2, uint3
 }
 
 // ---- the self-guided filter (src/lrf.rs:156-334) ------------------------------
-// sgrproj_sum_finish (:305-323), u32 wrapping
-__device__ __forceinline__ void sum_finish(uint32_t ssq, uint32_t sum, uint32_t n, uint32_t one_over_n,
-                                           uint32_t s, int bdm8, uint32_t &a, uint32_t &b) {
-  const uint32_t sssq = (ssq + ((1u << (2 * bdm8)) >> 1)) >> (2 * bdm8);
-  const uint32_t ssum = (sum + ((1u << bdm8) >> 1)) >> bdm8;
-  const int32_t pd = (int32_t)(sssq * n - ssum * ssum);  // (i32) - (i32), wrapping
-  const uint32_t p = (uint32_t)(pd > 0 ? pd : 0);
-  const uint32_t z = (p * s + ((1u << kMtableBits) >> 1)) >> kMtableBits;
-  a = z >= 255 ? 256 : z == 0 ? 1 : ((z << kSgrBits) + z / 2) / (z + 1);
-  const uint32_t bb = ((1u << kSgrBits) - a) * sum * one_over_n;
-  b = (bb + ((1u << kRecipBits) >> 1)) >> kRecipBits;
-}
-// get_integral_square (:326-334): rows (y, y + d], columns (x, x + d]
-__device__ __forceinline__ uint32_t isq(const uint32_t *ii, int s, int x, int y, int d) {
-  return ii[y * s + x] + ii[(y + d) * s + x + d] - ii[(y + d) * s + x] - ii[y * s + x + d];
-}
-
-// The LDS tables of one region (w x h pixels, w <= W): the integral images
-// ((h + 7) x (w + 7)), the r = 1 (a, b) rows 0 .. h + 1 and the r = 2 rows
-// 0, 2, .. h (+1), each w + 2 wide.
+// The LDS of one region (w x h pixels, w <= W): the integral images
+// ((h + 7) x (w + 7), ii then sq), the r = 1 (a, b) rows 0 .. h + 1 and the
+// r = 2 rows 0, 2, .. h (+1), each w + 2 wide, (a, b) side by side (one
+// 8-byte read), and x_by_xplus1 of z.
 template <int W, int HMAX>
 struct SgrLds {
   static constexpr int IS = W + 7, IR = HMAX + 8;  // image pitch / rows
   static constexpr int AS = W + 2, A1R = HMAX + 2, A2R = HMAX / 2 + 2;
+  static constexpr int TAB = (A1R + A2R) * AS;
   uint32_t ii[IR * IS], sq[IR * IS];
-  uint32_t a1[A1R * AS], b1[A1R * AS];
-  uint32_t a2[A2R * AS], b2[A2R * AS];
+  uint2 tab[TAB];  // r = 1 rows then r = 2 rows
+  uint16_t xz[256];
 };
+using SgrL64 = SgrLds<64, 64>;
+using SgrL32 = SgrLds<32, 64>;
+// the loops below walk ii and sq as one array by integer offsets (a select
+// of two LDS constants trips the compiler here)
+static_assert(offsetof(SgrL32, sq) == sizeof(uint32_t) * SgrL32::IR * SgrL32::IS, "");
 
-// the (a, b) tables of set s over the region's image (every lane)
-template <int W, int HMAX>
-__device__ inline void sgr_tables(SgrLds<W, HMAX> &L, int set, int w, int h, int bdm8) {
-  using S = SgrLds<W, HMAX>;
-  const uint32_t s2 = kSgrS[set][0], s1 = kSgrS[set][1];
-  const int n1 = s1 ? (h + 2) * (w + 2) : 0;
-  const int r2rows = s2 ? (h + 1) / 2 + 1 + ((h + 1) & 1 ? 0 : 0) : 0;  // rows 0, 2, .., <= h + 1
-  const int n2 = r2rows * (w + 2);
-  for (int i = threadIdx.x; i < n1 + n2; i += blockDim.x) {
-    if (i < n1) {  // box_ab r1: the image from (1, 1) (:626-650, 877-889)
-      const int y = i / (w + 2), x = i - y * (w + 2);
-      uint32_t a, b;
-      sum_finish(isq(L.sq + S::IS + 1, S::IS, x, y, 3), isq(L.ii + S::IS + 1, S::IS, x, y, 3), 9, 455,
-                 s1, bdm8, a, b);
-      L.a1[y * S::AS + x] = a;
-      L.b1[y * S::AS + x] = b;
-    } else {  // box_ab r2 at even rows (:611-624, 843-856)
-      const int j = i - n1, yr = j / (w + 2), x = j - yr * (w + 2);
-      uint32_t a, b;
-      sum_finish(isq(L.sq, S::IS, x, 2 * yr, 5), isq(L.ii, S::IS, x, 2 * yr, 5), 25, 164, s2, bdm8, a, b);
-      L.a2[yr * S::AS + x] = a;
-      L.b2[yr * S::AS + x] = b;
-    }
+// x_by_xplus1 (the a of sgrproj_sum_finish for z < 255); every lane, a
+// barrier before the first use
+__device__ __forceinline__ void sgr_init_xz(uint16_t *xz) {
+  for (int z = threadIdx.x; z < 256; z += blockDim.x)
+    xz[z] = (uint16_t)(z == 255 ? 256 : z == 0 ? 1 : ((z << kSgrBits) + z / 2) / (z + 1));
+}
+// sgrproj_sum_finish (:305-323), u32 wrapping, in its two halves: the box's
+// p (the set-independent variance term) with its sum, then a and b of
+// strength s
+__device__ __forceinline__ uint2 sgr_box(uint32_t ssq, uint32_t sum, uint32_t n, int bdm8) {
+  const uint32_t sssq = (ssq + ((1u << (2 * bdm8)) >> 1)) >> (2 * bdm8);
+  const uint32_t ssum = (sum + ((1u << bdm8) >> 1)) >> bdm8;
+  const int32_t pd = (int32_t)(sssq * n - ssum * ssum);  // (i32) - (i32), wrapping
+  return make_uint2((uint32_t)(pd > 0 ? pd : 0), sum);
+}
+__device__ __forceinline__ uint2 sgr_ab(uint2 ps, uint32_t s, uint32_t one_over_n, const uint16_t *xz) {
+  const uint32_t z = (ps.x * s + ((1u << kMtableBits) >> 1)) >> kMtableBits;
+  const uint32_t a = xz[z < 255 ? z : 255];
+  const uint32_t bb = ((1u << kSgrBits) - a) * ps.y * one_over_n;
+  return make_uint2(a, (bb + ((1u << kRecipBits) >> 1)) >> kRecipBits);
+}
+// get_integral_square (:326-334): rows (y, y + d], columns (x, x + d] of
+// the image at ii + o (o = y * s + x)
+__device__ __forceinline__ uint32_t isq(const uint32_t *ii, int s, int o, int d) {
+  return ii[o] + ii[o + d * s + d] - ii[o + d * s] - ii[o + d];
+}
+
+// A lane's fixed place in a region's (w + 2)-wide tables: column tx, first
+// row ty, row step tstep (lanes past tstep full rows idle).
+struct SgrLane {
+  int tx, ty, tstep;
+};
+__device__ __forceinline__ SgrLane sgr_lane(int w, int t, int nt) {  // lane t of nt
+  const int cw = w + 2, step = nt / cw;
+  return {t % cw, t >= 0 && t < step * cw ? t / cw : 1 << 20, step};
+}
+__device__ __forceinline__ SgrLane sgr_lane(int w) { return sgr_lane(w, (int)threadIdx.x, (int)blockDim.x); }
+// where table row r of a set with r1rows rows of r = 1 lives, and its box
+// in the image: r = 1 boxes from (1, 1) (:626-650, 877-889), r = 2 at even
+// rows (:611-624, 843-856)
+template <int IS, int AS, int A1R>
+__device__ __forceinline__ void sgr_row(int r, int r1rows, int tx, int &to, int &o, int &d) {
+  if (r < r1rows) {
+    to = r * AS + tx;
+    o = (r + 1) * IS + tx + 1;
+    d = 3;
+  } else {
+    const int yr = r - r1rows;
+    to = (A1R + yr) * AS + tx;
+    o = 2 * yr * IS + tx;
+    d = 5;
   }
 }
 
+// the (a, b) tables of set s straight from the integral images (every lane)
+template <int IS, int IR, int AS, int A1R>
+__device__ __forceinline__ void sgr_tables(const uint32_t *img, uint2 *tab, const uint16_t *xz,
+                                           const SgrLane &ln, int set, int h, int bdm8) {
+  const uint32_t s2 = kSgrS[set][0], s1 = kSgrS[set][1];
+  const int r1rows = s1 ? h + 2 : 0, r2rows = s2 ? (h + 1) / 2 + 1 : 0;  // r = 2: rows 0, 2, .., <= h + 1
+  for (int r = ln.ty; r < r1rows + r2rows; r += ln.tstep) {
+    int to, o, d;
+    sgr_row<IS, AS, A1R>(r, r1rows, ln.tx, to, o, d);
+    const bool one = r < r1rows;
+    tab[to] = sgr_ab(sgr_box(isq(img, IS, IR * IS + o, d), isq(img, IS, o, d), one ? 9 : 25, bdm8),
+                     one ? s1 : s2, one ? 455 : 164, xz);
+  }
+}
+// the boxes' (p, sum) of both radii, once per region (every lane) ...
+template <int IS, int IR, int AS, int A1R>
+__device__ __forceinline__ void sgr_boxes(const uint32_t *img, uint2 *ps, const SgrLane &ln, int h, int bdm8) {
+  const int r1rows = h + 2, r2rows = (h + 1) / 2 + 1;
+  for (int r = ln.ty; r < r1rows + r2rows; r += ln.tstep) {
+    int to, o, d;
+    sgr_row<IS, AS, A1R>(r, r1rows, ln.tx, to, o, d);
+    ps[to] = sgr_box(isq(img, IS, IR * IS + o, d), isq(img, IS, o, d), r < r1rows ? 9 : 25, bdm8);
+  }
+}
+// ... and each set's tables from them (the same places)
+template <int AS, int A1R>
+__device__ __forceinline__ void sgr_tables_ps(const uint2 *ps, uint2 *tab, const uint16_t *xz,
+                                              const SgrLane &ln, int set, int h) {
+  const uint32_t s2 = kSgrS[set][0], s1 = kSgrS[set][1];
+  const int r1rows = s1 ? h + 2 : 0, r2rows = s2 ? (h + 1) / 2 + 1 : 0;
+  for (int r = ln.ty; r < r1rows + r2rows; r += ln.tstep) {
+    const bool one = r < r1rows;
+    const int to = (one ? r : A1R + r - r1rows) * AS + ln.tx;
+    tab[to] = sgr_ab(ps[to], one ? s1 : s2, one ? 455 : 164, xz);
+  }
+}
+
+// 5 * (t[x] + t[x + 2]) + 6 * t[x + 1], a and b
+__device__ __forceinline__ void sgr_row3(const uint2 *t, int x, uint32_t &a, uint32_t &b) {
+  const uint2 v0 = t[x], v1 = t[x + 1], v2 = t[x + 2];
+  a = 5 * (v0.x + v2.x) + 6 * v1.x;
+  b = 5 * (v0.y + v2.y) + 6 * v1.y;
+}
 // f_r2 and f_r1 of pixel (x, y) with value px (src/lrf.rs:244-301 via the
 // row loop :656-733); px0: the pixel of row y & ~1 (box_f_r0 shares it)
-template <int W, int HMAX>
-__device__ __forceinline__ void sgr_f(const SgrLds<W, HMAX> &L, int set, int x, int y, uint32_t px,
-                                      uint32_t px0, uint32_t &f2, uint32_t &f1) {
-  using S = SgrLds<W, HMAX>;
+template <int AS, int A1R>
+__device__ __forceinline__ void sgr_f(const uint2 *tab, int set, int x, int y, uint32_t px, uint32_t px0,
+                                      uint32_t &f2, uint32_t &f1) {
   const uint32_t s2 = kSgrS[set][0], s1 = kSgrS[set][1];
   constexpr int sh = 5 + kSgrBits - kRstBits, sho = 4 + kSgrBits - kRstBits;
   if (s2) {
     const int yr = y >> 1;
-    const uint32_t *an = L.a2 + (yr + 1) * S::AS, *bn = L.b2 + (yr + 1) * S::AS;
-    const uint32_t ao = 5 * (an[x] + an[x + 2]) + 6 * an[x + 1];
-    const uint32_t bo = 5 * (bn[x] + bn[x + 2]) + 6 * bn[x + 1];
+    uint32_t ao, bo;
+    sgr_row3(tab + (A1R + yr + 1) * AS, x, ao, bo);
     if (!(y & 1)) {
-      const uint32_t *ap = L.a2 + yr * S::AS, *bp = L.b2 + yr * S::AS;
-      const uint32_t a = 5 * (ap[x] + ap[x + 2]) + 6 * ap[x + 1];
-      const uint32_t b = 5 * (bp[x] + bp[x + 2]) + 6 * bp[x + 1];
+      uint32_t a, b;
+      sgr_row3(tab + (A1R + yr) * AS, x, a, b);
       f2 = ((a + ao) * px + b + bo + ((1u << sh) >> 1)) >> sh;
     } else {
       f2 = (ao * px + bo + ((1u << sho) >> 1)) >> sho;
@@ -262,15 +261,57 @@ __device__ __forceinline__ void sgr_f(const SgrLds<W, HMAX> &L, int set, int x, 
     f2 = px0 << kRstBits;
   }
   if (s1) {
-    const uint32_t *A0 = L.a1 + y * S::AS, *A1 = A0 + S::AS, *A2 = A1 + S::AS;
-    const uint32_t *B0 = L.b1 + y * S::AS, *B1 = B0 + S::AS, *B2 = B1 + S::AS;
-    const uint32_t a = 3 * (A0[x] + A2[x] + A0[x + 2] + A2[x + 2]) +
-                       4 * (A1[x] + A0[x + 1] + A1[x + 1] + A2[x + 1] + A1[x + 2]);
-    const uint32_t b = 3 * (B0[x] + B2[x] + B0[x + 2] + B2[x + 2]) +
-                       4 * (B1[x] + B0[x + 1] + B1[x + 1] + B2[x + 1] + B1[x + 2]);
+    const uint2 *T0 = tab + y * AS + x, *T1 = T0 + AS, *T2 = T1 + AS;
+    const uint2 c0 = T0[0], c1 = T0[1], c2 = T0[2], c3 = T1[0], c4 = T1[1], c5 = T1[2], c6 = T2[0],
+                c7 = T2[1], c8 = T2[2];
+    // corners weigh 3, the cross 4
+    const uint32_t a = 3 * (c0.x + c6.x + c2.x + c8.x) + 4 * (c3.x + c1.x + c4.x + c7.x + c5.x);
+    const uint32_t b = 3 * (c0.y + c6.y + c2.y + c8.y) + 4 * (c3.y + c1.y + c4.y + c7.y + c5.y);
     f1 = (a * px + b + ((1u << sh) >> 1)) >> sh;
   } else {
     f1 = px << kRstBits;
+  }
+}
+// sgr_f of the four pixels (x, y0 .. y0 + 3) of a column strip (y0 a
+// multiple of 4): the table rows they share are read once
+template <int AS, int A1R>
+__device__ __forceinline__ void sgr_f4(const uint2 *tab, int set, int x, int y0, const uint32_t px[4],
+                                       uint32_t f2[4], uint32_t f1[4]) {
+  const uint32_t s2 = kSgrS[set][0], s1 = kSgrS[set][1];
+  constexpr int sh = 5 + kSgrBits - kRstBits, sho = 4 + kSgrBits - kRstBits;
+  constexpr uint32_t rnd = (1u << sh) >> 1, rndo = (1u << sho) >> 1;
+  if (s2) {  // r = 2 rows y0 / 2 .. y0 / 2 + 2: even pixels use two, odd ones the second
+    uint32_t wa[3], wb[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++) sgr_row3(tab + (A1R + (y0 >> 1) + j) * AS, x, wa[j], wb[j]);
+    f2[0] = ((wa[0] + wa[1]) * px[0] + wb[0] + wb[1] + rnd) >> sh;
+    f2[1] = (wa[1] * px[1] + wb[1] + rndo) >> sho;
+    f2[2] = ((wa[1] + wa[2]) * px[2] + wb[1] + wb[2] + rnd) >> sh;
+    f2[3] = (wa[2] * px[3] + wb[2] + rndo) >> sho;
+  } else {  // box_f_r0: the pixel of the even row
+    f2[0] = f2[1] = px[0] << kRstBits;
+    f2[2] = f2[3] = px[2] << kRstBits;
+  }
+  if (s1) {  // r = 1 rows y0 .. y0 + 5: each row's corner pair and middle
+    uint32_t ca[6], cb[6], ma[6], mb[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      const uint2 *T = tab + (y0 + j) * AS + x;
+      const uint2 v0 = T[0], v1 = T[1], v2 = T[2];
+      ca[j] = v0.x + v2.x;
+      cb[j] = v0.y + v2.y;
+      ma[j] = v1.x;
+      mb[j] = v1.y;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // corners weigh 3, the cross 4
+      const uint32_t a = 3 * (ca[k] + ca[k + 2]) + 4 * (ma[k] + ca[k + 1] + ma[k + 1] + ma[k + 2]);
+      const uint32_t b = 3 * (cb[k] + cb[k + 2]) + 4 * (mb[k] + cb[k + 1] + mb[k + 1] + mb[k + 2]);
+      f1[k] = (a * px[k] + b + rnd) >> sh;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) f1[k] = px[k] << kRstBits;
   }
 }
 // the restored pixel (:734-746)
@@ -281,34 +322,105 @@ __device__ __forceinline__ int sgr_out(uint32_t f2, uint32_t f1, uint32_t px, in
   return iclamp((v + ((1 << sh) >> 1)) >> sh, 0, mx);
 }
 
+// inclusive u32 prefix sums (wrapping) of the image's lines -- rows of ii
+// and sq, or their columns -- 8 lanes per line, each a chunk of up to 9
+// consecutive elements in registers, the chunk totals scanned by shuffles
+// within the 8 (lines up to 72 long)
+template <int IS, int IR>
+__device__ __forceinline__ void img_prefix(uint32_t *img, int rows, int cols, bool along_rows) {
+  const int nline = along_rows ? 2 * rows : 2 * cols, len = along_rows ? cols : rows;
+  const int chunk = (len + 7) >> 3, g = threadIdx.x & 7;
+  for (int line = threadIdx.x >> 3; line < nline; line += blockDim.x >> 3) {
+    uint32_t *p;
+    int st;
+    if (along_rows) {
+      p = img + (line < rows ? line : IR + line - rows) * IS;
+      st = 1;
+    } else {
+      p = img + (line < cols ? line : IR * IS + line - cols);
+      st = IS;
+    }
+    uint32_t v[9], acc = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      const int idx = g * chunk + k;
+      v[k] = (k < chunk && idx < len) ? p[idx * st] : 0;
+      acc += v[k];
+      v[k] = acc;
+    }
+    uint32_t t = acc;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      const uint32_t u = __shfl_up(t, o, 8);
+      if (g >= o) t += u;
+    }
+    const uint32_t off = t - acc;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      const int idx = g * chunk + k;
+      if (k < chunk && idx < len) p[idx * st] = v[k] + off;
+    }
+  }
+}
 // the integral images of a region (w x h, rows / columns of the image from
-// pix(r, c)): row prefix sums, then column prefix sums, u32 wrapping
-template <int W, int HMAX, typename Pix>
-__device__ inline void sgr_integral(SgrLds<W, HMAX> &L, int w, int h, Pix pix) {
-  using S = SgrLds<W, HMAX>;
+// pix(r, c)) at img (ii) and img + IR * IS (sq): the values, then row and
+// column prefix sums
+template <int IS, int IR, typename Pix>
+__device__ __forceinline__ void sgr_integral(uint32_t *img, int w, int h, Pix pix) {
   const int rows = 4 + h + (h & 1) + 2, cols = w + 7;
   for (int i = threadIdx.x; i < rows * cols; i += blockDim.x) {
     const int r = i / cols, c = i - r * cols;
     const uint32_t v = pix(r, c);
-    L.ii[r * S::IS + c] = v;
-    L.sq[r * S::IS + c] = v * v;
+    img[r * IS + c] = v;
+    img[IR * IS + r * IS + c] = v * v;
   }
   __syncthreads();
-  for (int r = threadIdx.x; r < 2 * rows; r += blockDim.x) {
-    uint32_t *p = (r < rows ? L.ii : L.sq) + (r % rows) * S::IS, acc = 0;
-    for (int c = 0; c < cols; c++) p[c] = acc += p[c];
-  }
+  img_prefix<IS, IR>(img, rows, cols, true);
   __syncthreads();
-  for (int c = threadIdx.x; c < 2 * cols; c += blockDim.x) {
-    uint32_t *p = (c < cols ? L.ii : L.sq) + c % cols, acc = 0;
-    for (int r = 0; r < rows; r++) p[r * S::IS] = acc += p[r * S::IS];
-  }
+  img_prefix<IS, IR>(img, rows, cols, false);
   __syncthreads();
 }
 
-// sum of a u64 over the workgroup (LDS slots red[0 .. 8)), result to all lanes
-__device__ inline uint64_t wg_sum_u64(uint64_t v, uint64_t *red) {
-  v = group_sum<64>(v);
+// ---- wave sums on the DPP lane network (VALU, no LDS traffic) --------------
+// lanes' values moved by DPP control CTRL; rows outside ROWS read 0
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  return (uint64_t)dpp32<CTRL, ROWS>((uint32_t)(v >> 32)) << 32 | dpp32<CTRL, ROWS>((uint32_t)v);
+}
+template <typename T, int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ T dpp_t(T v) {
+  if constexpr (sizeof(T) == 8)
+    return (T)dpp64<CTRL, ROWS>((uint64_t)v);
+  else
+    return (T)dpp32<CTRL, ROWS>((uint32_t)v);
+}
+// the sum over each aligned 8 lanes, to all of them: quad_perm [1,0,3,2],
+// [2,3,0,1], row_half_mirror (wrapping)
+template <typename T>
+__device__ __forceinline__ T dpp_sum8(T v) {
+  v += dpp_t<T, 0xB1>(v);
+  v += dpp_t<T, 0x4E>(v);
+  v += dpp_t<T, 0x141>(v);
+  return v;
+}
+// the sum over the wave, to all lanes: the rows of 16 (row_mirror), then
+// row_bcast:15 / :31 carry them up to lane 63
+__device__ __forceinline__ uint64_t dpp_sum64(uint64_t v) {
+  v = dpp_sum8(v);
+  v += dpp64<0x140>(v);
+  v += dpp64<0x142, 0xa>(v);
+  v += dpp64<0x143, 0xc>(v);
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32 |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+}
+
+// sum of a u64 over the workgroup (LDS slots red[0 .. 16)), result to all lanes
+__device__ __forceinline__ uint64_t wg_sum_u64(uint64_t v, uint64_t *red) {
+  v = dpp_sum64(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   uint64_t t = 0;
@@ -316,7 +428,6 @@ __device__ inline uint64_t wg_sum_u64(uint64_t v, uint64_t *red) {
   __syncthreads();
   return t;
 }
-__device__ inline int64_t wg_sum_i64(int64_t v, uint64_t *red) { return (int64_t)wg_sum_u64((uint64_t)v, red); }
 
 // ---- the unit decision's distortions (rdo_loop_decision) -----------------------
 struct LrfRdoArgs {
@@ -327,30 +438,66 @@ struct LrfRdoArgs {
   int w_imp, w_in_b, h_in_b;
   LrfGeo g;
   int cdef;                  // CDEF on (strengths at index 0)
+  const uint8_t *dir;        // cdef_analyze_superblock of the unit's input: per 8x8 luma block,
+  const int32_t *var;        // pitch dstride (rv_cdef_find_dirs)
+  int dstride;
   int pri_y, sec_y, pri_uv, sec_uv, damping;
   double ds[3];
   uint64_t *err;             // [3][nsb][17]
   int8_t *xqd;               // [3][nsb][16][2]
 };
 
-constexpr int kRdoThreads = 256;
+// 1024 lanes (16 waves, ~130 KB of LDS: one workgroup per CU). The boxes'
+// (p, sum) are set-independent: computed once, each set's (a, b) tables are
+// a multiply and a table lookup per entry. Pixel phases: a lane owns a
+// column strip of 4 pixels (one table read serves all four) and keeps its f
+// values in registers from the solve sums to the filtered pixels.
+// Distortion phase: lanes 0 .. 511, 8 per 8x8 block, one row each, the
+// block's moments summed over the 8 lanes by shuffles.
+constexpr int kRdoThreads = 1024;
+
+#ifdef LRF_PHASES  // tools/ubench/lrf_bench.hip: one workgroup's phase clocks
+__device__ unsigned long long lrf_phase_t[96];
+#define PHASE(k) \
+  if (tid == 0 && blockIdx.x == LRF_PHASES && blockIdx.y == 0) lrf_phase_t[k] = wall_clock64()
+#else
+#define PHASE(k)
+#endif
+
+struct RdoLds {
+  union {
+    uint32_t img[2 * SgrL64::IR * SgrL64::IS];  // ii, sq
+    uint2 tab[SgrL64::TAB];                     // then each set's (a, b)
+  } a;
+  union {
+    uint16_t lin[64 * 64];  // the unit's input (lrf_input)
+    uint2 ps[SgrL64::TAB];  // then the boxes' (p, sum)
+  } b;
+  uint16_t xz[256];
+  int16_t coffs[48];      // cdef_offsets at the pad's pitch
+  uint16_t pad[68 * 68];  // the padded CDEF input, then each option's output
+  uint16_t ssolve[64 * 64], esrc[64 * 64];  // the source at the solve's / the distortion's place
+  uint8_t bdir[64], bskip[64];
+  int32_t bvar[64];
+  uint64_t red[kRdoThreads / 64];
+  int64_t red5[5][kRdoThreads / 64];
+  uint3 hm[16 * 8];            // luma: each half block's (sd, sd2, ssd), [strip][block column]
+  int32_t bss[64];             // luma: each block's source sum and sum of squares
+  uint32_t bss2[64];
+  int8_t sxqd[2];
+};
 
 template <typename Px>
 __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
-  using L64 = SgrLds<64, 64>;
-  __shared__ L64 L;
-  __shared__ uint16_t pad[68 * 68];  // the padded CDEF input (cdef_sb_padded_frame_copy)
-  __shared__ uint16_t lin[64 * 64];  // the unit's input (lrf_input)
-  __shared__ uint8_t bdir[64], bskip[64];
-  __shared__ int32_t bvar[64];
-  __shared__ uint64_t red[kRdoThreads / 64];
-  __shared__ int8_t sxqd[2];
+  __shared__ RdoLds S;
+  constexpr int AS = SgrL64::AS, A1R = SgrL64::A1R;
   const LrfGeo &g = a.g;
-  const int p = blockIdx.y, sb = blockIdx.x;
+  const int p = blockIdx.y, sb = blockIdx.x, tid = threadIdx.x;
   const int sbc = g.sbc, fsx = sb % sbc, fsy = sb / sbc;
   if (fsx >= g.cols[p] || fsy >= g.rows[p]) return;  // no unit (uniform)
   const int t0x = fsx - fsx % g.tws, t0y = fsy - fsy % g.ths, sx = fsx - t0x, sy = fsy - t0y;
-  const int xd = p ? g.xdec : 0, yd = p ? g.ydec : 0, bw = 64 >> xd, bh = 64 >> yd;
+  const int xd = p ? g.xdec : 0, yd = p ? g.ydec : 0, bw = 64 >> xd, bh = 64 >> yd, npx = bw * bh;
+  const int lbw = 6 - xd;  // log2 bw
   const int tw_px = min(g.tws * 64, g.W - t0x * 64), th_px = min(g.ths * 64, g.H - t0y * 64);
   const int pw_t = (tw_px + xd) >> xd, ph_t = (th_px + yd) >> yd;
   const int mi_cols = tw_px >> 2, mi_rows = th_px >> 2;
@@ -360,167 +507,283 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
   auto recpx = [&](int x, int y) -> int {  // frame plane coordinates
     return (int)((const Px *)rec.data)[(int64_t)(rec.yorigin + y) * rec.stride + rec.xorigin + x];
   };
+  PHASE(0);
+  sgr_init_xz(S.xz);
+  cdef_offsets(S.coffs, bw + 4);
   // 1. the padded copy and the unit's input
-  for (int i = threadIdx.x; i < (bh + 4) * (bw + 4); i += blockDim.x) {
+  for (int i = tid; i < (bh + 4) * (bw + 4); i += blockDim.x) {
     const int y = i / (bw + 4) - 2, x = i % (bw + 4) - 2, tx = ox + x, ty = oy + y;
     int v = kVeryLarge;
     if (tx >= 0 && tx < pw_t && ty >= 0 && ty < ph_t) {
       const int csx = (tx << xd) >> 6, csy = (ty << yd) >> 6;
       v = (csy < sy || (csy == sy && csx <= sx)) ? recpx(fx0 + tx, fy0 + ty) : 128;
     }
-    pad[i] = (uint16_t)v;
+    S.pad[i] = (uint16_t)v;
   }
   const int vw = min(bw, pw_t - ox), vh = min(bh, ph_t - oy);
-  for (int i = threadIdx.x; i < bw * bh; i += blockDim.x) {
-    const int y = i / bw, x = i - y * bw;
-    lin[i] = (uint16_t)recpx(fx0 + ox + min(x, vw - 1), fy0 + oy + min(y, vh - 1));
+  for (int i = tid; i < npx; i += blockDim.x) {
+    const int y = i >> lbw, x = i & (bw - 1);
+    S.b.lin[i] = (uint16_t)recpx(fx0 + ox + min(x, vw - 1), fy0 + oy + min(y, vh - 1));
   }
   // 2. CDEF index 0 on the 8x8 blocks inside the tile (cdef_filter_superblock)
+  PHASE(1);
   if (a.cdef) {
-    if (threadIdx.x < 64) {
-      const int bx = threadIdx.x & 7, by = threadIdx.x >> 3, gx = sx * 16 + 2 * bx, gy = sy * 16 + 2 * by;
+    if (tid < 64) {
+      const int bx = tid & 7, by = tid >> 3, gx = sx * 16 + 2 * bx, gy = sy * 16 + 2 * by;
       uint8_t sk = 2, dir = 0;
       int32_t var = 0;
       if (gx < mi_cols && gy < mi_rows) {
         const uint8_t *k = a.skip + (int64_t)(t0y * 16 + gy) * a.mi_stride + t0x * 16 + gx;
         sk = k[0] & k[1] & k[a.mi_stride] & k[a.mi_stride + 1];
         if (!sk) {
-          const rv_plane &yl = a.rec[0];
-          const Px *bp = (const Px *)yl.data + (int64_t)(yl.yorigin + t0y * 64 + sy * 64 + 8 * by) * yl.stride +
-                         yl.xorigin + t0x * 64 + sx * 64 + 8 * bx;
-          dir = (uint8_t)cdef_dir<Px>(bp, yl.stride, cs, &var);
+          const int64_t o = (int64_t)(fsy * 8 + by) * a.dstride + fsx * 8 + bx;
+          dir = a.dir[o];
+          var = a.var[o];
         }
       }
-      bskip[threadIdx.x] = sk;
-      bdir[threadIdx.x] = dir;
-      bvar[threadIdx.x] = var;
+      S.bskip[tid] = sk;
+      S.bdir[tid] = dir;
+      S.bvar[tid] = var;
     }
     __syncthreads();
     const int bxs = 8 >> xd, bys = 8 >> yd;
-    for (int i = threadIdx.x; i < bw * bh; i += blockDim.x) {
-      const int y = i / bw, x = i - y * bw, blk = (y / bys) * 8 + x / bxs;
-      if (bskip[blk]) continue;  // skip: the copy (equal to lin); 2: outside the tile
+    for (int i = tid; i < npx; i += blockDim.x) {
+      const int y = i >> lbw, x = i & (bw - 1), blk = (y / bys) * 8 + x / bxs;
+      if (S.bskip[blk]) continue;  // skip: the copy (equal to lin); 2: outside the tile
       int pri, sec, dmp = a.damping + cs, d;
       if (p == 0) {
-        pri = cdef_adjust(a.pri_y << cs, bvar[blk]);
+        pri = cdef_adjust(a.pri_y << cs, S.bvar[blk]);
         sec = a.sec_y << cs;
-        d = a.pri_y ? bdir[blk] : 0;
+        d = a.pri_y ? S.bdir[blk] : 0;
       } else {
         pri = a.pri_uv << cs;
         sec = a.sec_uv << cs;
         dmp -= 1;
-        d = a.pri_uv ? bdir[blk] : 0;
+        d = a.pri_uv ? S.bdir[blk] : 0;
       }
-      lin[i] = (uint16_t)cdef_px(pad + (y + 2) * (bw + 4) + x + 2, bw + 4, pri, sec, d, dmp, cs);
+      S.b.lin[i] = (uint16_t)cdef_px(S.pad + (y + 2) * (bw + 4) + x + 2, S.coffs + 6 * d, pri, sec, dmp, cs);
     }
   }
   __syncthreads();
   // 3. the unit (unit size clipped at the tile-relative offset, the
   // reference's quirk) and its integral image: lrf_input alone, replicated
+  PHASE(2);
   const int pw = p ? (g.W + xd) >> xd : g.W, ph = p ? (g.H + yd) >> yd : g.H;
   const int uw = min(bw, pw - ox), uh = min(bh, ph - oy);
-  sgr_integral<64, 64>(L, uw, uh, [&](int r, int c) -> uint32_t {
-    return lin[iclamp(r - 4, 0, uh - 1) * bw + iclamp(c - 4, 0, uw - 1)];
+  sgr_integral<SgrL64::IS, SgrL64::IR>(S.a.img, uw, uh, [&](int r, int c) -> uint32_t {
+    return S.b.lin[iclamp(r - 4, 0, uh - 1) * bw + iclamp(c - 4, 0, uw - 1)];
   });
-  // 4. the distortions: rdo_loop_plane_error over the superblock's 8x8s in
-  // the tile; lane = 8x8 block (64), the option's pixels from `val`
+  // the lane's pixels (px | px of row y & ~1 << 16), the option None's
+  // pixels (the input as it is) and the two source tiles: sgrproj_solve's,
+  // read at the unit's tile-relative offset of the whole frame (ts.input
+  // with loop_tile_po, src/rdo.rs:2028-2033), and the distortion's, over the
+  // 8x8 blocks inside the tile (a block reaches at most 7 past the frame,
+  // into the plane's padding)
+  PHASE(3);
   const int64_t ss_ = src.stride;
-  const Px *sbase = (const Px *)src.data + (int64_t)(src.yorigin + fy0 + oy) * ss_ + src.xorigin + fx0 + ox;
-  auto plane_err = [&](auto val) -> uint64_t {
+  const Px *const sp = (const Px *)src.data;
+  const int elx = (min(8, max(0, (mi_cols - sx * 16 + 1) / 2)) * 8) >> xd;
+  const int ely = (min(8, max(0, (mi_rows - sy * 16 + 1) / 2)) * 8) >> yd;
+  const Px *const ssolve = sp + (int64_t)(src.yorigin + oy) * ss_ + src.xorigin + ox;
+  const Px *const sdist = sp + (int64_t)(src.yorigin + fy0 + oy) * ss_ + src.xorigin + fx0 + ox;
+  // the lane's column strip: pixels (qx, qy0 .. qy0 + 3), on the unit's
+  // raster (lanes past its height idle in the pixel phases)
+  const int qx = tid & (bw - 1), qy0 = (tid >> lbw) * 4;
+  const bool qlane = qy0 < bh;
+  uint32_t pxr[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int y = qy0 + k, i = y * bw + qx;
+    pxr[k] = 0;
+    if (qlane) {
+      const bool in = qx < uw && y < uh;
+      if (in) pxr[k] = S.b.lin[i];
+      S.pad[i] = S.b.lin[i];
+      S.ssolve[i] = in ? (uint16_t)ssolve[(int64_t)y * ss_ + qx] : 0;
+      S.esrc[i] = (qx < elx && y < ely) ? (uint16_t)sdist[(int64_t)y * ss_ + qx] : 0;
+    }
+  }
+  __syncthreads();  // lin is read: the boxes take its place
+  PHASE(4);
+  const SgrLane ln = sgr_lane(uw);
+  sgr_boxes<SgrL64::IS, SgrL64::IR, AS, A1R>(S.a.img, S.b.ps, ln, uh, cs);
+  // 4. the distortion lanes: rdo_loop_plane_error over the superblock's 8x8s
+  // in the tile; lane = (block, row)
+  const int eb = tid >> 3, ej = tid & 7, ebx = eb & 7, eby = eb >> 3;
+  const int egx = sx * 16 + 2 * ebx, egy = sy * 16 + 2 * eby;
+  const bool eblk = eb < 64 && egx < mi_cols && egy < mi_rows;
+  const int w8 = 8 >> xd, h8 = 8 >> yd, pbw = min(8, w8) >> xd, pbh = min(8, h8) >> yd;
+  const int eqx = (8 * ebx) >> xd, eqy = ((8 * eby) >> yd) + ej;
+  const bool erow = eblk && ej < h8;
+  const double ebias =
+      eblk ? lrf_bias(a.imp, a.w_imp, a.w_in_b, a.h_in_b, t0x * 16 + egx, t0y * 16 + egy) : 0.0;
+  // the luma finish: lane b < 64 prices block b
+  const int fgx = sx * 16 + 2 * (tid & 7), fgy = sy * 16 + 2 * ((tid >> 3) & 7);
+  const bool eblk8 = tid < 64 && fgx < mi_cols && fgy < mi_rows;
+  const double bbias8 =
+      eblk8 ? lrf_bias(a.imp, a.w_imp, a.w_in_b, a.h_in_b, t0x * 16 + fgx, t0y * 16 + fgy) : 0.0;
+  auto plane_err = [&]() -> uint64_t {  // the option's pixels in pad
     uint64_t e = 0;
-    if (threadIdx.x < 64) {
-      const int bx = threadIdx.x & 7, by = threadIdx.x >> 3, gx = sx * 16 + 2 * bx, gy = sy * 16 + 2 * by;
-      if (gx < mi_cols && gy < mi_rows) {
-        const double bias = lrf_bias(a.imp, a.w_imp, a.w_in_b, a.h_in_b, t0x * 16 + gx, t0y * 16 + gy);
-        const int qx = (8 * bx) >> xd, qy = (8 * by) >> yd;
-        if (p == 0) {
-          int32_t ss = 0, sd = 0;
-          uint32_t ss2 = 0, sd2 = 0, ssd = 0;
-          for (int j = 0; j < 8; j++)
-            for (int i = 0; i < 8; i++) {
-              const int32_t s = sbase[(int64_t)(qy + j) * ss_ + qx + i], d = val(qx + i, qy + j);
-              ss += s;
-              sd += d;
-              ss2 += (uint32_t)(s * s);
-              sd2 += (uint32_t)(d * d);
-              ssd += (uint32_t)(s * d);
-            }
-          e = biased(cdef_dist(ss, sd, ss2, sd2, ssd, bd), bias);
-        } else {  // sse_wxh of (8 >> xdec) x (8 >> ydec) in parts of the importance block
-          const int w8 = 8 >> xd, h8 = 8 >> yd, pbw = min(8, w8) >> xd, pbh = min(8, h8) >> yd;
-          for (int py = 0; py < h8 / pbh; py++)
-            for (int px_ = 0; px_ < w8 / pbw; px_++) {
-              uint64_t v = 0;
-              for (int j = 0; j < pbh; j++) {
-                uint32_t row = 0;
-                for (int i = 0; i < pbw; i++) {
-                  const int c = (int)(int16_t)sbase[(int64_t)(qy + py * pbh + j) * ss_ + qx + px_ * pbw + i] -
-                                (int)(int16_t)val(qx + px_ * pbw + i, qy + py * pbh + j);
-                  row += (uint32_t)(c * c);
-                }
-                v += row;
-              }
-              e += biased(v, bias);
-            }
+    const int eo = eqy * bw + eqx;
+    if (p == 0) {
+      int32_t ss = 0, sd = 0;
+      uint32_t ss2 = 0, sd2 = 0, ssd = 0;
+      if (erow) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const int32_t s = S.esrc[eo + i], d = S.pad[eo + i];
+          ss += s;
+          sd += d;
+          ss2 += (uint32_t)(s * s);
+          sd2 += (uint32_t)(d * d);
+          ssd += (uint32_t)(s * d);
         }
       }
+      ss = dpp_sum8(ss);
+      sd = dpp_sum8(sd);
+      ss2 = dpp_sum8(ss2);
+      sd2 = dpp_sum8(sd2);
+      ssd = dpp_sum8(ssd);
+      if (eblk && ej == 0) e = biased(cdef_dist(ss, sd, ss2, sd2, ssd, bd), ebias);
+    } else {  // sse_wxh of (8 >> xdec) x (8 >> ydec) in parts of the importance block
+      uint32_t v0 = 0, v1 = 0;  // the row's part columns (w8 / pbw <= 2)
+      if (erow) {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+          if (i < w8) {
+            const int c = (int)(int16_t)S.esrc[eo + i] - (int)(int16_t)S.pad[eo + i];
+            if (i < pbw)
+              v0 += (uint32_t)(c * c);
+            else
+              v1 += (uint32_t)(c * c);
+          }
+      }
+      for (int o = 1; o < pbh; o <<= 1) {  // the part's rows (aligned lane groups)
+        v0 += __shfl_xor(v0, o, RV_WAVE);
+        v1 += __shfl_xor(v1, o, RV_WAVE);
+      }
+      if (erow && ej % pbh == 0) e = biased(v0, ebias) + (w8 > pbw ? biased(v1, ebias) : 0);
     }
-    const uint64_t t = wg_sum_u64(e, red);
-    return (uint64_t)((double)t * a.ds[p]);
+    return (uint64_t)((double)wg_sum_u64(e, S.red) * a.ds[p]);
   };
+  if (p == 0 && tid < 64) {  // the source moments of the luma blocks (every set reuses them)
+    int32_t ss = 0;
+    uint32_t ss2 = 0;
+    for (int j = 0; j < 8; j++)
+      for (int i = 0; i < 8; i++) {
+        const int32_t v = S.esrc[(8 * (tid >> 3) + j) * 64 + 8 * (tid & 7) + i];
+        ss += v;
+        ss2 += (uint32_t)(v * v);
+      }
+    S.bss[tid] = ss;
+    S.bss2[tid] = ss2;
+  }
   uint64_t *eo = a.err + ((size_t)p * g.nsb + sb) * 17;
   int8_t *xo = a.xqd + ((size_t)p * g.nsb + sb) * 32;
   {
-    const uint64_t e = plane_err([&](int x, int y) { return (int32_t)lin[y * bw + x]; });
-    if (threadIdx.x == 0) eo[0] = e;
+    const uint64_t e = plane_err();  // (its barriers also publish the boxes)
+    if (tid == 0) eo[0] = e;
   }
-  // 5. the 16 sets: tables, solve sums, xqd, the filtered unit's distortion
+  PHASE(5);
+  // 5. the 16 sets: tables, solve sums, xqd, the filtered unit's
+  // distortion; wave 0 solves set s while the other waves build set s + 1's
+  // tables (the f values of s are in registers by then)
+  using Acc = typename std::conditional<sizeof(Px) == 1, int32_t, int64_t>::type;  // 8-bit: 4 products fit
+  const SgrLane ln_rest = sgr_lane(uw, tid - 64, kRdoThreads - 64);
+  sgr_tables_ps<AS, A1R>(S.b.ps, S.a.tab, S.xz, ln, 0, uh);
   for (int set = 0; set < 16; set++) {
-    sgr_tables<64, 64>(L, set, uw, uh, cs);
     __syncthreads();
-    int64_t H00 = 0, H11 = 0, H01 = 0, C0 = 0, C1 = 0;
-    for (int i = threadIdx.x; i < uw * uh; i += blockDim.x) {
-      const int y = i / uw, x = i - y * uw;
-      const uint32_t px = lin[y * bw + x], px0 = lin[(y & ~1) * bw + x];
-      uint32_t f2, f1;
-      sgr_f<64, 64>(L, set, x, y, px, px0, f2, f1);
-      // sgrproj_solve reads the source at the unit's tile-relative offset
-      // of the whole frame (ts.input with loop_tile_po, src/rdo.rs:2028-2033)
-      const int64_t u = (int64_t)px << kRstBits;
-      const int64_t s = ((int64_t)((const Px *)src.data)[(int64_t)(src.yorigin + oy + y) * ss_ + src.xorigin +
-                                                         ox + x]
-                         << kRstBits) - u;
-      const int64_t e2 = (int64_t)(int32_t)f2 - u, e1 = (int64_t)(int32_t)f1 - u;
-      H00 += e2 * e2;
-      H11 += e1 * e1;
-      H01 += e1 * e2;
-      C0 += e2 * s;
-      C1 += e1 * s;
+    PHASE(6 + 5 * set);
+    uint32_t f2r[4] = {0, 0, 0, 0}, f1r[4] = {0, 0, 0, 0};
+    Acc H00 = 0, H11 = 0, H01 = 0, C0 = 0, C1 = 0;
+    if (qlane && qx < uw) {
+      sgr_f4<AS, A1R>(S.a.tab, set, qx, qy0, pxr, f2r, f1r);
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (qy0 + k < uh) {
+          const Acc u = (Acc)pxr[k] << kRstBits;
+          const Acc sv = ((Acc)S.ssolve[(qy0 + k) * bw + qx] << kRstBits) - u;
+          const Acc e2 = (Acc)(int32_t)f2r[k] - u, e1 = (Acc)(int32_t)f1r[k] - u;
+          H00 += e2 * e2;
+          H11 += e1 * e1;
+          H01 += e1 * e2;
+          C0 += e2 * sv;
+          C1 += e1 * sv;
+        }
     }
-    H00 = wg_sum_i64(H00, red);
-    H11 = wg_sum_i64(H11, red);
-    H01 = wg_sum_i64(H01, red);
-    C0 = wg_sum_i64(C0, red);
-    C1 = wg_sum_i64(C1, red);
-    if (threadIdx.x == 0) {
-      int8_t q[2];
-      lrf_solve_finish(set, uw, uh, H00, H01, H11, C0, C1, q);
-      sxqd[0] = q[0];
-      sxqd[1] = q[1];
-      xo[2 * set] = q[0];
-      xo[2 * set + 1] = q[1];
+    {
+      const int64_t v[5] = {H00, H11, H01, C0, C1};
+#pragma unroll
+      for (int q = 0; q < 5; q++) {
+        const int64_t t = (int64_t)dpp_sum64((uint64_t)v[q]);
+        if ((tid & 63) == 0) S.red5[q][tid >> 6] = t;
+      }
     }
     __syncthreads();
-    const int w0 = sxqd[0], w1 = sxqd[1];
-    const uint64_t e = plane_err([&](int x, int y) -> int32_t {
-      if (x >= uw || y >= uh) return 128;  // lrf_output's fill (never inside the frame)
-      const uint32_t px = lin[y * bw + x], px0 = lin[(y & ~1) * bw + x];
-      uint32_t f2, f1;
-      sgr_f<64, 64>(L, set, x, y, px, px0, f2, f1);
-      return sgr_out(f2, f1, px, w0, w1, mx);
-    });
-    if (threadIdx.x == 0) eo[1 + set] = e;
-    __syncthreads();  // the tables are rewritten by the next set
+    PHASE(7 + 5 * set);
+    if (tid < 64) {  // wave 0: the solve (lanes 0 .. 4 add up one sum each)
+      int64_t t = 0;
+      if (tid < 5)
+        for (int w = 0; w < kRdoThreads / 64; w++) t += S.red5[tid][w];
+      const int64_t h00 = __shfl(t, 0, 64), h11 = __shfl(t, 1, 64), h01 = __shfl(t, 2, 64),
+                    c0 = __shfl(t, 3, 64), c1 = __shfl(t, 4, 64);
+      if (tid == 0) {
+        int8_t q[2];
+        lrf_solve_finish(set, uw, uh, h00, h01, h11, c0, c1, q);
+        S.sxqd[0] = q[0];
+        S.sxqd[1] = q[1];
+        xo[2 * set] = q[0];
+        xo[2 * set + 1] = q[1];
+      }
+    } else if (set < 15) {
+      sgr_tables_ps<AS, A1R>(S.b.ps, S.a.tab, S.xz, ln_rest, set + 1, uh);
+    }
+    __syncthreads();
+    PHASE(8 + 5 * set);
+    const int w0 = S.sxqd[0], w1 = S.sxqd[1];
+    if (p == 0) {
+      // luma: the filtered pixels' moments straight from registers -- a
+      // strip is half a block column: 8 lanes make a half block, wave 0 puts
+      // the halves together and prices the 64 blocks
+      int32_t sd = 0;
+      uint32_t sd2 = 0, ssd = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {  // 128 outside the unit: lrf_output's fill (never inside the frame)
+        const int y = qy0 + k;
+        const int32_t d = (qx < uw && y < uh) ? sgr_out(f2r[k], f1r[k], pxr[k], w0, w1, mx) : 128;
+        const int32_t sv = S.esrc[y * 64 + qx];
+        sd += d;
+        sd2 += (uint32_t)(d * d);
+        ssd += (uint32_t)(sv * d);
+      }
+      sd = dpp_sum8(sd);
+      sd2 = dpp_sum8(sd2);
+      ssd = dpp_sum8(ssd);
+      if ((qx & 7) == 0) S.hm[(qy0 >> 2) * 8 + (qx >> 3)] = make_uint3((uint32_t)sd, sd2, ssd);
+      __syncthreads();
+      PHASE(9 + 5 * set);
+      if (tid < 64) {
+        uint64_t e = 0;
+        if (eblk8) {
+          const uint3 u0 = S.hm[(2 * (tid >> 3)) * 8 + (tid & 7)], u1 = S.hm[(2 * (tid >> 3) + 1) * 8 + (tid & 7)];
+          e = biased(cdef_dist(S.bss[tid], (int32_t)(u0.x + u1.x), S.bss2[tid], u0.y + u1.y, u0.z + u1.z, bd), bbias8);
+        }
+        e = dpp_sum64(e);
+        if (tid == 0) eo[1 + set] = (uint64_t)((double)e * a.ds[p]);
+      }
+    } else {
+      if (qlane) {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+          S.pad[(qy0 + k) * bw + qx] =
+              (qx < uw && qy0 + k < uh) ? (uint16_t)sgr_out(f2r[k], f1r[k], pxr[k], w0, w1, mx) : 128;
+      }
+      __syncthreads();
+      PHASE(9 + 5 * set);
+      const uint64_t e = plane_err();
+      if (tid == 0) eo[1 + set] = e;
+    }
+    PHASE(10 + 5 * set);
   }
 }
 
@@ -533,50 +796,93 @@ struct LrfDecideArgs {
   int8_t *units;  // [3][rows][cols][3]: set (-1 None), xqd0, xqd1
 };
 
-__global__ void lrf_decide_kernel(LrfDecideArgs a) {
+// One wave per tile: lane 16 p + s prices set s of plane p, lane 48 + p
+// plane p's None, at the tile's current state; a (cost, set) minimum over
+// each 16-lane group by shuffles, then None (first in the reference's order:
+// it wins ties) picks the first cheapest, and every lane applies the same
+// write_lrf updates (the state stays uniform). No LDS and no barrier: the
+// next superblock's distortions load while this one is decided.
+__global__ __launch_bounds__(64) void lrf_decide_kernel(LrfDecideArgs a) {
   const LrfGeo &g = a.g;
-  const int ntx = (g.sbc + g.tws - 1) / g.tws, nty = (g.sbr + g.ths - 1) / g.ths;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntx * nty) return;
+  const int ntx = (g.sbc + g.tws - 1) / g.tws;
+  const int t = blockIdx.x, lane = threadIdx.x;
   const int t0x = (t % ntx) * g.tws, t0y = (t / ntx) * g.ths;
-  const int tsw = min(g.tws, g.sbc - t0x), tsh = min(g.ths, g.sbr - t0y);
+  const int tsw = min(g.tws, g.sbc - t0x), tsh = min(g.ths, g.sbr - t0y), n = tsw * tsh;
+  const bool none = lane >= 48, live = lane < 51;
+  const int lp = none ? lane - 48 : lane >> 4, ls = none ? -1 : lane & 15;  // plane, set (-1: None)
   LrfTileState st;
   lrf_tile_init(st);
-  for (int sy = 0; sy < tsh; sy++)
-    for (int sx = 0; sx < tsw; sx++) {
-      const int fsx = t0x + sx, fsy = t0y + sy, sb = fsy * g.sbc + fsx;
-      int8_t pick[3][3];
-      bool has[3];
-      for (int p = 0; p < 3; p++) {
-        has[p] = fsx < g.cols[p] && fsy < g.rows[p];
-        if (!has[p]) {  // stretched into its neighbour's unit: none of its own
-          int8_t *u = a.units + (((size_t)p * g.urows_max + fsy) * g.ucols_max + fsx) * 3;
-          u[0] = -1;
-          u[1] = u[2] = 0;
-          continue;
-        }
-        const uint64_t *e = a.err + ((size_t)p * g.nsb + sb) * 17;
-        const int8_t *xq = a.xqd + ((size_t)p * g.nsb + sb) * 32;
-        int best = -1;
-        double best_cost = (double)e[0] + a.lambda * ((double)lrf_rate(st, p, -1, nullptr) / 8.0);
-        for (int s = 0; s < 16; s++) {
-          const double c = (double)e[1 + s] + a.lambda * ((double)lrf_rate(st, p, s, xq + 2 * s) / 8.0);
-          if (c < best_cost) {
-            best_cost = c;
-            best = s;
-          }
-        }
-        pick[p][0] = (int8_t)best;
-        pick[p][1] = best < 0 ? 0 : xq[2 * best];
-        pick[p][2] = best < 0 ? 0 : xq[2 * best + 1];
-        int8_t *u = a.units + (((size_t)p * g.urows_max + fsy) * g.ucols_max + fsx) * 3;
-        u[0] = pick[p][0];
-        u[1] = pick[p][1];
-        u[2] = pick[p][2];
+  auto load = [&](int k, uint64_t &e, int &x0, int &x1) {
+    e = 0;
+    x0 = x1 = 0;
+    if (live && k < n) {
+      const size_t u = (size_t)lp * g.nsb + (t0y + k / tsw) * g.sbc + t0x + k % tsw;
+      e = a.err[u * 17 + 1 + ls];
+      if (!none) {
+        x0 = a.xqd[u * 32 + 2 * ls];
+        x1 = a.xqd[u * 32 + 2 * ls + 1];
       }
-      for (int p = 0; p < 3; p++)
-        if (has[p]) lrf_commit(st, p, pick[p][0], pick[p] + 1);
     }
+  };
+  uint64_t e;
+  int x0, x1;
+  load(0, e, x0, x1);
+  for (int k = 0; k < n; k++) {
+    const int fsx = t0x + k % tsw, fsy = t0y + k / tsw;
+    uint64_t en;
+    int n0, n1;
+    load(k + 1, en, n0, n1);
+    const int r0 = lp == 0 ? st.ref[0][0] : lp == 1 ? st.ref[1][0] : st.ref[2][0];
+    const int r1 = lp == 0 ? st.ref[0][1] : lp == 1 ? st.ref[1][1] : st.ref[2][1];
+    const uint32_t bits = lrf_rate_at(st.cdf, r0, r1, ls, x0, x1);
+    const double c = (double)e + a.lambda * ((double)bits / 8.0);
+    // costs are >= 0: their bit patterns order like the values
+    const uint64_t key = live ? (uint64_t)__double_as_longlong(c) : ~0ull;
+    uint64_t bk = key;
+    int bs = ls;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {  // the first cheapest set of each 16
+      const uint64_t ok = __shfl_xor(bk, o, 64);
+      const int os = __shfl_xor(bs, o, 64);
+      if (ok < bk || (ok == bk && os < bs)) {
+        bk = ok;
+        bs = os;
+      }
+    }
+    int pick[3][3];
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+      const uint64_t sk = __shfl(bk, 16 * p, 64), nk = __shfl(key, 48 + p, 64);
+      const int s = __shfl(bs, 16 * p, 64);
+      const int best = nk <= sk ? -1 : s;
+      const int src = 16 * p + (best < 0 ? 0 : best);
+      const int q0 = __shfl(x0, src, 64), q1 = __shfl(x1, src, 64);
+      // a stretched superblock has no unit of its own
+      const bool has = fsx < g.cols[p] && fsy < g.rows[p];
+      pick[p][0] = has ? best : -2;
+      pick[p][1] = has && best >= 0 ? q0 : 0;
+      pick[p][2] = has && best >= 0 ? q1 : 0;
+    }
+    if (lane < 3) {
+      const int p = lane;
+      const int b0 = p == 0 ? pick[0][0] : p == 1 ? pick[1][0] : pick[2][0];
+      const int b1 = p == 0 ? pick[0][1] : p == 1 ? pick[1][1] : pick[2][1];
+      const int b2 = p == 0 ? pick[0][2] : p == 1 ? pick[1][2] : pick[2][2];
+      int8_t *u = a.units + (((size_t)p * g.urows_max + fsy) * g.ucols_max + fsx) * 3;
+      u[0] = (int8_t)(b0 < 0 ? -1 : b0);
+      u[1] = (int8_t)b1;
+      u[2] = (int8_t)b2;
+    }
+#pragma unroll
+    for (int p = 0; p < 3; p++)
+      if (pick[p][0] > -2) {
+        const int8_t q[2] = {(int8_t)pick[p][1], (int8_t)pick[p][2]};
+        lrf_commit(st, p, pick[p][0], q);
+      }
+    e = en;
+    x0 = n0;
+    x1 = n1;
+  }
 }
 
 // ---- lrf_filter_frame (src/lrf.rs:1345-1444) ------------------------------------
@@ -627,7 +933,8 @@ __global__ __launch_bounds__(256) void lrf_filter_kernel(LrfFilterArgs a) {
   // clamp to the frame (the unit's own right limit reaches 3 past it),
   // rows to the frame and the stripe's +-2 extension, deblocked outside
   const int sh = sz + (sz & 1), crop = crop_h;
-  sgr_integral<32, 64>(L, w, sz, [&](int r, int c) -> uint32_t {
+  sgr_init_xz(L.xz);
+  sgr_integral<L32::IS, L32::IR>(L.ii, w, sz, [&](int r, int c) -> uint32_t {
     const int cy = iclamp(y0 - 4 + r, 0, crop - 1), ly = iclamp(cy, y0 - 2, y0 + sh + 1);
     const int xx = iclamp(x - 4 + c, 0, crop_w - 1);
     return (uint32_t)((ly >= y0 && ly < y0 + sh) ? at(cd, xx, ly) : at(db, xx, ly));
@@ -637,14 +944,14 @@ __global__ __launch_bounds__(256) void lrf_filter_kernel(LrfFilterArgs a) {
     blk[yy * 32 + xx] = (uint16_t)at(cd, x + xx, y0 + yy);
   }
   const int set = u[0];
-  sgr_tables<32, 64>(L, set, w, sz, g.bd - 8);
+  sgr_tables<L32::IS, L32::IR, L32::AS, L32::A1R>(L.ii, L.tab, L.xz, sgr_lane(w), set, sz, g.bd - 8);
   __syncthreads();
   const int mx = (1 << g.bd) - 1;
   for (int i = threadIdx.x; i < w * sz; i += blockDim.x) {
     const int yy = i / w, xx = i - yy * w;
     const uint32_t px = blk[yy * 32 + xx], px0 = blk[(yy & ~1) * 32 + xx];
     uint32_t f2, f1;
-    sgr_f<32, 64>(L, set, xx, yy, px, px0, f2, f1);
+    sgr_f<L32::AS, L32::A1R>(L.tab, set, xx, yy, px, px0, f2, f1);
     op[(int64_t)yy * out.stride + xx] = (Px)sgr_out(f2, f1, px, u[1], u[2], mx);
   }
 }
@@ -688,8 +995,8 @@ int lrf_geometry(int width, int height, int xdec, int ydec, int bit_depth, int b
 
 int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *skip, int mi_stride,
                    const float *imp, int w_imp, int w_in_b, int h_in_b, const LrfGeo &g, int cdef,
-                   const uint8_t cdef_str[2], const double ds[3], uint64_t *err, int8_t *xqd,
-                   double lambda, int8_t *units, hipStream_t s) {
+                   const uint8_t *dir, const int32_t *var, const uint8_t cdef_str[2], const double ds[3],
+                   uint64_t *err, int8_t *xqd, double lambda, int8_t *units, hipStream_t s) {
   LrfRdoArgs a;
   memset(&a, 0, sizeof(a));
   for (int p = 0; p < 3; p++) {
@@ -705,6 +1012,9 @@ int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *
   a.h_in_b = h_in_b;
   a.g = g;
   a.cdef = cdef;
+  a.dir = dir;
+  a.var = var;
+  a.dstride = (g.W + 7) / 8;
   a.pri_y = cdef_str[0] / 4;
   a.sec_y = cdef_str[0] % 4 == 3 ? 4 : cdef_str[0] % 4;
   a.pri_uv = cdef_str[1] / 4;
@@ -725,7 +1035,7 @@ int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *
   d.lambda = lambda;
   d.units = units;
   const int nt = ((g.sbc + g.tws - 1) / g.tws) * ((g.sbr + g.ths - 1) / g.ths);
-  lrf_decide_kernel<<<(nt + 63) / 64, 64, 0, s>>>(d);
+  lrf_decide_kernel<<<nt, 64, 0, s>>>(d);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

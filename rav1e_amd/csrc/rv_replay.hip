@@ -1748,9 +1748,14 @@ int filter_slot(rv_replay *r, const RvSlot &s, const RvInput &in, int lv) {
     const Geo &g = r->g;
     RV_R(lrf_geometry(g.W, g.H, g.xdec, g.ydec, g.bd, r->lv[lv].qidx, g.tws, g.ths, &lg));
     const rv_plane rec[3] = {s.y, s.u, s.v}, src[3] = {in.y, in.u, in.v};
+    // its CDEF's directions (cdef_pad_slot finds the deblocked frame's
+    // afterwards, in the same buffers)
+    if (r->cdef)
+      RV_R(rv_cdef_find_dirs(&rec[0], g.W, g.H, r->mi_skip, r->mi_stride, r->cdef_dir, r->cdef_var, g.bd,
+                             r->stream));
     RV_R(lrf_rdo_launch(rec, src, r->mi_skip, r->mi_stride, r->imp_last, g.w_imp, g.w_in_b, g.h_in_b, lg,
-                        r->cdef, r->cdef_str[lv], r->lv[lv].ds, r->lrf_err, r->lrf_xqd, r->lv[lv].lambda,
-                        r->lrf_units, r->stream));
+                        r->cdef, r->cdef_dir, r->cdef_var, r->cdef_str[lv], r->lv[lv].ds, r->lrf_err,
+                        r->lrf_xqd, r->lv[lv].lambda, r->lrf_units, r->stream));
   }
   if (r->deblock) RV_R(deblock_slot(r, s, in, lv));
   return r->cdef ? cdef_pad_slot(r, s, lv, r->lrf ? &lg : nullptr) : pad_slot(r, s);

@@ -1,0 +1,137 @@
+// lrf_bench.hip -- loop restoration's decision kernels alone on a 2160p
+// 4:2:0 8-bit frame of synthetic content: the per-unit distortion kernel's
+// duration (full grid, HIP events) and one workgroup's phase clocks.
+// Build (tools/ubench/Makefile):  hipcc -DLRF_PHASES=... includes the
+// kernel source so the harness launches it directly.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+#include "../../rav1e_amd/csrc/rv_lrf.hip"
+
+extern "C" int rv_cdef_find_dirs(const rv_plane *luma, int width, int height, const uint8_t *d_skip,
+                                 int mi_stride, uint8_t *d_dir, int32_t *d_var, int bit_depth, void *stream);
+
+#define CK(x)                                                               \
+  do {                                                                      \
+    hipError_t e_ = (x);                                                    \
+    if (e_ != hipSuccess) {                                                 \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                              \
+    }                                                                       \
+  } while (0)
+
+static rv_plane plane(int w, int h, int xdec, int ydec, unsigned seed) {
+  rv_plane p{};
+  const int pad = 80;
+  p.stride = w + 2 * pad;
+  p.alloc_height = h + 2 * pad;
+  p.width = w;
+  p.height = h;
+  p.xorigin = pad;
+  p.yorigin = pad;
+  p.xdec = xdec;
+  p.ydec = ydec;
+  p.hbd = 0;
+  p.bit_depth = 8;
+  std::vector<uint8_t> v((size_t)p.stride * p.alloc_height);
+  srand(seed);
+  for (int y = 0; y < p.alloc_height; y++)
+    for (int x = 0; x < p.stride; x++) {
+      int t = 96 + ((x * 3 + y * 2) >> 4) % 64 + (rand() % 17) - 8 + (((x >> 5) ^ (y >> 5)) & 1) * 30;
+      v[(size_t)y * p.stride + x] = (uint8_t)(t < 0 ? 0 : t > 255 ? 255 : t);
+    }
+  CK(hipMalloc(&p.data, v.size()));
+  CK(hipMemcpy(p.data, v.data(), v.size(), hipMemcpyHostToDevice));
+  return p;
+}
+
+int main(int argc, char **argv) {
+  const int W = 3840, H = 2160, reps = argc > 1 ? atoi(argv[1]) : 5;
+  rv_plane rec[3], src[3];
+  for (int p = 0; p < 3; p++) {
+    const int d = p ? 1 : 0;
+    rec[p] = plane(W >> d, H >> d, d, d, 1 + p);
+    src[p] = plane(W >> d, H >> d, d, d, 11 + p);
+  }
+  LrfGeo g;
+  if (lrf_geometry(W, H, 1, 1, 8, 100, 8, 34, &g) != RV_OK) return 1;
+  const int mi_stride = W / 4 + 8;
+  uint8_t *skip;
+  CK(hipMalloc(&skip, (size_t)mi_stride * (H / 4 + 8)));
+  CK(hipMemset(skip, 0, (size_t)mi_stride * (H / 4 + 8)));
+  uint64_t *err;
+  int8_t *xqd, *units;
+  CK(hipMalloc(&err, sizeof(uint64_t) * 3 * g.nsb * 17));
+  CK(hipMalloc(&xqd, 3 * g.nsb * 32));
+  CK(hipMalloc(&units, 3 * g.urows_max * g.ucols_max * 3));
+  uint8_t *dir;
+  int32_t *var;
+  const int n8 = (W / 8) * (H / 8);
+  CK(hipMalloc(&dir, n8));
+  CK(hipMalloc(&var, n8 * 4));
+  if (rv_cdef_find_dirs(&rec[0], W, H, skip, mi_stride, dir, var, 8, nullptr) != RV_OK) return 1;
+  LrfRdoArgs a;
+  memset(&a, 0, sizeof(a));
+  for (int p = 0; p < 3; p++) {
+    a.rec[p] = rec[p];
+    a.src[p] = src[p];
+    a.ds[p] = 1.0;
+  }
+  a.skip = skip;
+  a.mi_stride = mi_stride;
+  a.g = g;
+  a.cdef = 1;
+  a.dir = dir;
+  a.var = var;
+  a.dstride = W / 8;
+  a.pri_y = 2;
+  a.sec_y = 1;
+  a.pri_uv = 1;
+  a.sec_uv = 1;
+  a.damping = 3;
+  a.err = err;
+  a.xqd = xqd;
+  LrfDecideArgs d;
+  d.g = g;
+  d.err = err;
+  d.xqd = xqd;
+  d.lambda = 300.0;
+  d.units = units;
+  const int nt = ((g.sbc + g.tws - 1) / g.tws) * ((g.sbr + g.ths - 1) / g.ths);
+  hipEvent_t e0, e1, e2;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventCreate(&e2));
+  const dim3 grid((unsigned)g.nsb, 3);
+  for (int r = 0; r < reps; r++) {
+    CK(hipEventRecord(e0, 0));
+    lrf_rdo_kernel<uint8_t><<<grid, kRdoThreads>>>(a);
+    CK(hipEventRecord(e1, 0));
+    lrf_decide_kernel<<<nt, 64>>>(d);
+    CK(hipEventRecord(e2, 0));
+    CK(hipEventSynchronize(e2));
+    float t1, t2;
+    CK(hipEventElapsedTime(&t1, e0, e1));
+    CK(hipEventElapsedTime(&t2, e1, e2));
+    printf("rep %d: rdo %.3f ms (%d x 3 workgroups), decide %.3f ms (%d tiles)\n", r, t1, g.nsb, t2, nt);
+  }
+#ifdef LRF_PHASES
+  // one workgroup alone: its phases in wall_clock64 ticks (100 MHz)
+  lrf_rdo_kernel<uint8_t><<<dim3(LRF_PHASES + 1, 1), kRdoThreads>>>(a);
+  CK(hipDeviceSynchronize());
+  unsigned long long t[96];
+  CK(hipMemcpyFromSymbol(t, HIP_SYMBOL(lrf_phase_t), sizeof(t)));
+  printf("one workgroup (unit %d, luma), us:\n", LRF_PHASES);
+  const char *names[6] = {"start", "pad+lin", "cdef", "integral", "tiles", "boxes+none"};  // (stamps before barriers)
+  for (int k = 1; k < 6; k++) printf("  %-12s %8.2f\n", names[k], (t[k] - t[k - 1]) / 100.0);
+  for (int s = 0; s < 16; s++) {
+    const unsigned long long *q = t + 6 + 5 * s, prev = s ? q[-1] : t[5];
+    printf("  set %2d: tables %6.2f f+sums %6.2f solve %6.2f out %6.2f err %6.2f\n", s, (q[0] - prev) / 100.0,
+           (q[1] - q[0]) / 100.0, (q[2] - q[1]) / 100.0, (q[3] - q[2]) / 100.0, (q[4] - q[3]) / 100.0);
+  }
+  printf("  total %8.2f\n", (t[6 + 5 * 15 + 4] - t[0]) / 100.0);
+#endif
+  return 0;
+}
