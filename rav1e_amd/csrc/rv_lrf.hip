@@ -23,6 +23,7 @@
 // All of it is integer work but sgrproj_solve's tail, whose f64 operations
 // run in the reference's order (IEEE division, no contraction).
 #include <stddef.h>
+#include <mutex>
 #include <type_traits>
 #include <string.h>
 
@@ -226,6 +227,7 @@ __device__ __forceinline__ void sgr_tables_ps(const uint2 *ps, uint2 *tab, const
                                               const SgrLane &ln, int set, int h) {
   const uint32_t s2 = kSgrS[set][0], s1 = kSgrS[set][1];
   const int r1rows = s1 ? h + 2 : 0, r2rows = s2 ? (h + 1) / 2 + 1 : 0;
+#pragma unroll 2
   for (int r = ln.ty; r < r1rows + r2rows; r += ln.tstep) {
     const bool one = r < r1rows;
     const int to = (one ? r : A1R + r - r1rows) * AS + ln.tx;
@@ -418,6 +420,50 @@ __device__ __forceinline__ uint64_t dpp_sum64(uint64_t v) {
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
 }
 
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32 |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  return __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(v), l));
+}
+// lrf_solve_finish on a whole wave: the independent divisions on separate
+// lanes (each IEEE-rounded as on one), the same operations in the same order
+__device__ __forceinline__ void lrf_solve_finish_wave(int set, int w, int h, int64_t H00, int64_t H01,
+                                                      int64_t H11, int64_t C0, int64_t C1, int8_t xqd[2]) {
+  const int lane = threadIdx.x & 63;
+  const bool r2 = lrf_set_has(set, 0), r1 = lrf_set_has(set, 1);
+  const double n = (double)w * (double)h;
+  const double num = lane == 0 ? (double)H00 : lane == 1 ? (double)H01 : lane == 2 ? (double)H11 : 128.0;
+  const double q = num / n;
+  const double h00 = readlane_f64(q, 0), h01 = readlane_f64(q, 1), h11 = readlane_f64(q, 2);
+  const double sc = readlane_f64(q, 3);
+  const double h10 = h01;
+  const double c0 = (double)C0 * sc, c1 = (double)C1 * sc;
+  int xq0, xq1;
+  if (!r2) {
+    xq0 = 0;
+    xq1 = h11 == 0. ? 0 : (int)round(c1 / h11);
+  } else if (!r1) {
+    xq0 = h00 == 0. ? 0 : (int)round(c0 / h00);
+    xq1 = 0;
+  } else {
+    const double det = h00 * h11 - h01 * h10;
+    if (det == 0.) {
+      xq0 = xq1 = 0;
+    } else {
+      const double d1 = h11 * c0 - h01 * c1, d2 = h00 * c1 - h10 * c0;
+      const double r = (lane == 0 ? d1 : d2) / det;
+      xq0 = (int)round(readlane_f64(r, 0));
+      xq1 = (int)round(readlane_f64(r, 1));
+    }
+  }
+  const int x0 = xq0 < -96 ? -96 : xq0 > 31 ? 31 : xq0;
+  const int t = 128 - x0 - xq1, x1 = t < -32 ? -32 : t > 95 ? 95 : t;
+  xqd[0] = (int8_t)x0;
+  xqd[1] = (int8_t)x1;
+}
+
 // sum of a u64 over the workgroup (LDS slots red[0 .. 16)), result to all lanes
 __device__ __forceinline__ uint64_t wg_sum_u64(uint64_t v, uint64_t *red) {
   v = dpp_sum64(v);
@@ -525,6 +571,27 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
     const int y = i >> lbw, x = i & (bw - 1);
     S.b.lin[i] = (uint16_t)recpx(fx0 + ox + min(x, vw - 1), fy0 + oy + min(y, vh - 1));
   }
+  // the unit (unit size clipped at the tile-relative offset, the
+  // reference's quirk) and the two source tiles: sgrproj_solve's, read at
+  // the unit's tile-relative offset of the whole frame (ts.input with
+  // loop_tile_po, src/rdo.rs:2028-2033), and the distortion's, over the 8x8
+  // blocks inside the tile (a block reaches at most 7 past the frame, into
+  // the plane's padding)
+  const int pw = p ? (g.W + xd) >> xd : g.W, ph = p ? (g.H + yd) >> yd : g.H;
+  const int uw = min(bw, pw - ox), uh = min(bh, ph - oy);
+  const int64_t ss_ = src.stride;
+  const Px *const sp = (const Px *)src.data;
+  const int elx = (min(8, max(0, (mi_cols - sx * 16 + 1) / 2)) * 8) >> xd;
+  const int ely = (min(8, max(0, (mi_rows - sy * 16 + 1) / 2)) * 8) >> yd;
+  {
+    const Px *const ssolve = sp + (int64_t)(src.yorigin + oy) * ss_ + src.xorigin + ox;
+    const Px *const sdist = sp + (int64_t)(src.yorigin + fy0 + oy) * ss_ + src.xorigin + fx0 + ox;
+    for (int i = tid; i < npx; i += blockDim.x) {
+      const int y = i >> lbw, x = i & (bw - 1);
+      S.ssolve[i] = (x < uw && y < uh) ? (uint16_t)ssolve[(int64_t)y * ss_ + x] : 0;
+      S.esrc[i] = (x < elx && y < ely) ? (uint16_t)sdist[(int64_t)y * ss_ + x] : 0;
+    }
+  }
   // 2. CDEF index 0 on the 8x8 blocks inside the tile (cdef_filter_superblock)
   PHASE(1);
   if (a.cdef) {
@@ -565,27 +632,13 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
     }
   }
   __syncthreads();
-  // 3. the unit (unit size clipped at the tile-relative offset, the
-  // reference's quirk) and its integral image: lrf_input alone, replicated
+  // 3. the unit's integral image: lrf_input alone, replicated
   PHASE(2);
-  const int pw = p ? (g.W + xd) >> xd : g.W, ph = p ? (g.H + yd) >> yd : g.H;
-  const int uw = min(bw, pw - ox), uh = min(bh, ph - oy);
   sgr_integral<SgrL64::IS, SgrL64::IR>(S.a.img, uw, uh, [&](int r, int c) -> uint32_t {
     return S.b.lin[iclamp(r - 4, 0, uh - 1) * bw + iclamp(c - 4, 0, uw - 1)];
   });
-  // the lane's pixels (px | px of row y & ~1 << 16), the option None's
-  // pixels (the input as it is) and the two source tiles: sgrproj_solve's,
-  // read at the unit's tile-relative offset of the whole frame (ts.input
-  // with loop_tile_po, src/rdo.rs:2028-2033), and the distortion's, over the
-  // 8x8 blocks inside the tile (a block reaches at most 7 past the frame,
-  // into the plane's padding)
+  // the lane's pixels and the option None's pixels (the input as it is)
   PHASE(3);
-  const int64_t ss_ = src.stride;
-  const Px *const sp = (const Px *)src.data;
-  const int elx = (min(8, max(0, (mi_cols - sx * 16 + 1) / 2)) * 8) >> xd;
-  const int ely = (min(8, max(0, (mi_rows - sy * 16 + 1) / 2)) * 8) >> yd;
-  const Px *const ssolve = sp + (int64_t)(src.yorigin + oy) * ss_ + src.xorigin + ox;
-  const Px *const sdist = sp + (int64_t)(src.yorigin + fy0 + oy) * ss_ + src.xorigin + fx0 + ox;
   // the lane's column strip: pixels (qx, qy0 .. qy0 + 3), on the unit's
   // raster (lanes past its height idle in the pixel phases)
   const int qx = tid & (bw - 1), qy0 = (tid >> lbw) * 4;
@@ -599,8 +652,6 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
       const bool in = qx < uw && y < uh;
       if (in) pxr[k] = S.b.lin[i];
       S.pad[i] = S.b.lin[i];
-      S.ssolve[i] = in ? (uint16_t)ssolve[(int64_t)y * ss_ + qx] : 0;
-      S.esrc[i] = (qx < elx && y < ely) ? (uint16_t)sdist[(int64_t)y * ss_ + qx] : 0;
     }
   }
   __syncthreads();  // lin is read: the boxes take its place
@@ -617,9 +668,11 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
   const bool erow = eblk && ej < h8;
   const double ebias =
       eblk ? lrf_bias(a.imp, a.w_imp, a.w_in_b, a.h_in_b, t0x * 16 + egx, t0y * 16 + egy) : 0.0;
-  // the luma finish: lane b < 64 prices block b
+  // the luma finish: lane b of the last wave prices block b
+  constexpr int kFinWave = kRdoThreads / 64 - 1;
+  const bool fin = (tid >> 6) == kFinWave;
   const int fgx = sx * 16 + 2 * (tid & 7), fgy = sy * 16 + 2 * ((tid >> 3) & 7);
-  const bool eblk8 = tid < 64 && fgx < mi_cols && fgy < mi_rows;
+  const bool eblk8 = fin && fgx < mi_cols && fgy < mi_rows;
   const double bbias8 =
       eblk8 ? lrf_bias(a.imp, a.w_imp, a.w_in_b, a.h_in_b, t0x * 16 + fgx, t0y * 16 + fgy) : 0.0;
   auto plane_err = [&]() -> uint64_t {  // the option's pixels in pad
@@ -691,9 +744,22 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
   using Acc = typename std::conditional<sizeof(Px) == 1, int32_t, int64_t>::type;  // 8-bit: 4 products fit
   const SgrLane ln_rest = sgr_lane(uw, tid - 64, kRdoThreads - 64);
   sgr_tables_ps<AS, A1R>(S.b.ps, S.a.tab, S.xz, ln, 0, uh);
+  // set s's luma distortion from its half blocks: the last wave, after the
+  // next barrier (hm is rewritten two barriers later)
+  auto luma_finish = [&](int set) {
+    const int b = tid & 63;
+    uint64_t e = 0;
+    if (eblk8) {
+      const uint3 u0 = S.hm[(2 * (b >> 3)) * 8 + (b & 7)], u1 = S.hm[(2 * (b >> 3) + 1) * 8 + (b & 7)];
+      e = biased(cdef_dist(S.bss[b], (int32_t)(u0.x + u1.x), S.bss2[b], u0.y + u1.y, u0.z + u1.z, bd), bbias8);
+    }
+    e = dpp_sum64(e);
+    if (b == 0) eo[1 + set] = (uint64_t)((double)e * a.ds[p]);
+  };
   for (int set = 0; set < 16; set++) {
     __syncthreads();
     PHASE(6 + 5 * set);
+    if (p == 0 && set > 0 && fin) luma_finish(set - 1);
     uint32_t f2r[4] = {0, 0, 0, 0}, f1r[4] = {0, 0, 0, 0};
     Acc H00 = 0, H11 = 0, H01 = 0, C0 = 0, C1 = 0;
     if (qlane && qx < uw) {
@@ -725,11 +791,12 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
       int64_t t = 0;
       if (tid < 5)
         for (int w = 0; w < kRdoThreads / 64; w++) t += S.red5[tid][w];
-      const int64_t h00 = __shfl(t, 0, 64), h11 = __shfl(t, 1, 64), h01 = __shfl(t, 2, 64),
-                    c0 = __shfl(t, 3, 64), c1 = __shfl(t, 4, 64);
+      const int64_t h00 = readlane64((uint64_t)t, 0), h11 = readlane64((uint64_t)t, 1),
+                    h01 = readlane64((uint64_t)t, 2), c0 = readlane64((uint64_t)t, 3),
+                    c1 = readlane64((uint64_t)t, 4);
+      int8_t q[2];
+      lrf_solve_finish_wave(set, uw, uh, h00, h01, h11, c0, c1, q);
       if (tid == 0) {
-        int8_t q[2];
-        lrf_solve_finish(set, uw, uh, h00, h01, h11, c0, c1, q);
         S.sxqd[0] = q[0];
         S.sxqd[1] = q[1];
         xo[2 * set] = q[0];
@@ -760,17 +827,7 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
       sd2 = dpp_sum8(sd2);
       ssd = dpp_sum8(ssd);
       if ((qx & 7) == 0) S.hm[(qy0 >> 2) * 8 + (qx >> 3)] = make_uint3((uint32_t)sd, sd2, ssd);
-      __syncthreads();
       PHASE(9 + 5 * set);
-      if (tid < 64) {
-        uint64_t e = 0;
-        if (eblk8) {
-          const uint3 u0 = S.hm[(2 * (tid >> 3)) * 8 + (tid & 7)], u1 = S.hm[(2 * (tid >> 3) + 1) * 8 + (tid & 7)];
-          e = biased(cdef_dist(S.bss[tid], (int32_t)(u0.x + u1.x), S.bss2[tid], u0.y + u1.y, u0.z + u1.z, bd), bbias8);
-        }
-        e = dpp_sum64(e);
-        if (tid == 0) eo[1 + set] = (uint64_t)((double)e * a.ds[p]);
-      }
     } else {
       if (qlane) {
 #pragma unroll
@@ -785,6 +842,10 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
     }
     PHASE(10 + 5 * set);
   }
+  if (p == 0) {
+    __syncthreads();
+    if (fin) luma_finish(15);
+  }
 }
 
 // ---- the sequential decisions (count_lrf_switchable, write_lrf) -----------------
@@ -796,13 +857,36 @@ struct LrfDecideArgs {
   int8_t *units;  // [3][rows][cols][3]: set (-1 None), xqd0, xqd1
 };
 
+// (key, set) lexicographic minimum with the lane DPP control CTRL reads
+template <int CTRL>
+__device__ __forceinline__ void dpp_min_step(uint64_t &bk, int &bs) {
+  const uint64_t ok = dpp64<CTRL>(bk);
+  const int os = (int)dpp32<CTRL>((uint32_t)bs);
+  if (ok < bk || (ok == bk && os < bs)) {
+    bk = ok;
+    bs = os;
+  }
+}
+
 // One wave per tile: lane 16 p + s prices set s of plane p, lane 48 + p
 // plane p's None, at the tile's current state; a (cost, set) minimum over
-// each 16-lane group by shuffles, then None (first in the reference's order:
+// each 16-lane group on the DPP network, then None (first in the reference's order:
 // it wins ties) picks the first cheapest, and every lane applies the same
 // write_lrf updates (the state stays uniform). No LDS and no barrier: the
 // next superblock's distortions load while this one is decided.
+#ifdef LRF_PHASES
+__device__ unsigned long long lrf_dphase[5];
+#endif
+// count_signed_subexp_with_ref of each (xqd, ref) pair, per radius (bits *
+// 8; uploaded once by lrf_lut_upload)
+__device__ uint8_t g_lrf_subexp[2][128][128];
+constexpr int kDecideAhead = 4;        // superblocks of distortions in flight
+constexpr int kDecideBuf = 4096;        // superblocks whose picks wait in LDS
+
 __global__ __launch_bounds__(64) void lrf_decide_kernel(LrfDecideArgs a) {
+  __shared__ int8_t ubuf[kDecideBuf][3][3];
+  __shared__ uint8_t slut[2][128][128];  // g_lrf_subexp
+  __shared__ uint16_t sbl[2][520];       // symbol_bits of None / Sgrproj by cdf[0] / cdf[1] >> 6
   const LrfGeo &g = a.g;
   const int ntx = (g.sbc + g.tws - 1) / g.tws;
   const int t = blockIdx.x, lane = threadIdx.x;
@@ -810,13 +894,36 @@ __global__ __launch_bounds__(64) void lrf_decide_kernel(LrfDecideArgs a) {
   const int tsw = min(g.tws, g.sbc - t0x), tsh = min(g.ths, g.sbr - t0y), n = tsw * tsh;
   const bool none = lane >= 48, live = lane < 51;
   const int lp = none ? lane - 48 : lane >> 4, ls = none ? -1 : lane & 15;  // plane, set (-1: None)
+  const bool buffered = n <= kDecideBuf;
+  {
+    const uint4 *gl = (const uint4 *)&g_lrf_subexp[0][0][0];
+    uint4 *sl = (uint4 *)&slut[0][0][0];
+    for (int i = lane; i < 2 * 128 * 128 / 16; i += 64) sl[i] = gl[i];
+    for (int f = lane; f < 520; f += 64) {
+      const uint16_t c0[4] = {(uint16_t)(f << 6), 0, 0, 0}, c1[4] = {0, (uint16_t)(f << 6), 0, 0};
+      sbl[0][f] = (uint16_t)lrf_symbol_bits(0, c0, 3);
+      sbl[1][f] = (uint16_t)lrf_symbol_bits(2, c1, 3);
+    }
+    __syncthreads();
+  }
   LrfTileState st;
   lrf_tile_init(st);
-  auto load = [&](int k, uint64_t &e, int &x0, int &x1) {
+#ifdef LRF_PHASES  // cycles per part of a step, summed over the tile (s_memtime)
+  unsigned long long dacc[5] = {0, 0, 0, 0, 0}, dlast = clock64();
+#define DPHASE(i)                             \
+  {                                           \
+    const unsigned long long now = clock64(); \
+    dacc[i] += now - dlast;                   \
+    dlast = now;                              \
+  }
+#else
+#define DPHASE(i)
+#endif
+  auto load = [&](int k, int kx, int ky, uint64_t &e, int &x0, int &x1) {  // superblock k = (kx, ky)
     e = 0;
     x0 = x1 = 0;
     if (live && k < n) {
-      const size_t u = (size_t)lp * g.nsb + (t0y + k / tsw) * g.sbc + t0x + k % tsw;
+      const size_t u = (size_t)lp * g.nsb + (t0y + ky) * g.sbc + t0x + kx;
       e = a.err[u * 17 + 1 + ls];
       if (!none) {
         x0 = a.xqd[u * 32 + 2 * ls];
@@ -824,64 +931,99 @@ __global__ __launch_bounds__(64) void lrf_decide_kernel(LrfDecideArgs a) {
       }
     }
   };
-  uint64_t e;
-  int x0, x1;
-  load(0, e, x0, x1);
-  for (int k = 0; k < n; k++) {
-    const int fsx = t0x + k % tsw, fsy = t0y + k / tsw;
-    uint64_t en;
-    int n0, n1;
-    load(k + 1, en, n0, n1);
-    const int r0 = lp == 0 ? st.ref[0][0] : lp == 1 ? st.ref[1][0] : st.ref[2][0];
-    const int r1 = lp == 0 ? st.ref[0][1] : lp == 1 ? st.ref[1][1] : st.ref[2][1];
-    const uint32_t bits = lrf_rate_at(st.cdf, r0, r1, ls, x0, x1);
-    const double c = (double)e + a.lambda * ((double)bits / 8.0);
-    // costs are >= 0: their bit patterns order like the values
-    const uint64_t key = live ? (uint64_t)__double_as_longlong(c) : ~0ull;
-    uint64_t bk = key;
-    int bs = ls;
+  uint64_t ev[kDecideAhead];
+  int xv0[kDecideAhead], xv1[kDecideAhead];
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {  // the first cheapest set of each 16
-      const uint64_t ok = __shfl_xor(bk, o, 64);
-      const int os = __shfl_xor(bs, o, 64);
-      if (ok < bk || (ok == bk && os < bs)) {
-        bk = ok;
-        bs = os;
+  for (int d = 0; d < kDecideAhead; d++) load(d, d % tsw, d / tsw, ev[d], xv0[d], xv1[d]);
+  int sx = 0, sy = 0;                                            // the superblock in the tile
+  int lx = kDecideAhead % tsw, ly = kDecideAhead / tsw;          // the next one to load
+  for (int k0 = 0; k0 < n; k0 += kDecideAhead) {
+#pragma unroll
+    for (int d = 0; d < kDecideAhead; d++) {
+      const int k = k0 + d;
+      if (k >= n) break;
+      const int fsx = t0x + sx, fsy = t0y + sy;
+      DPHASE(0);
+      const int x0 = xv0[d], x1 = xv1[d];
+      const int r0 = lp == 0 ? st.ref[0][0] : lp == 1 ? st.ref[1][0] : st.ref[2][0];
+      const int r1 = lp == 0 ? st.ref[0][1] : lp == 1 ? st.ref[1][1] : st.ref[2][1];
+      // count_lrf_switchable (lrf_rate_at) from the tables
+      uint32_t bits;
+      if (none) {
+        bits = sbl[0][st.cdf[0] >> 6];
+      } else {
+        bits = sbl[1][st.cdf[1] >> 6] + (4u << 3);
+        if (lrf_set_has(ls, 0)) bits += slut[0][x0 + 96][r0 + 96];
+        if (lrf_set_has(ls, 1)) bits += slut[1][x1 + 32][r1 + 32];
+      }
+      const double c = (double)ev[d] + a.lambda * ((double)bits / 8.0);
+      // costs are >= 0: their bit patterns order like the values
+      const uint64_t key = live ? (uint64_t)__double_as_longlong(c) : ~0ull;
+      DPHASE(1);
+      uint64_t bk = key;
+      int bs = ls;
+      // the first cheapest set of each 16 lanes: quad pairs, quads, halves
+      // (any pairing reaches all 16 for a minimum)
+      dpp_min_step<0xB1>(bk, bs);
+      dpp_min_step<0x4E>(bk, bs);
+      dpp_min_step<0x141>(bk, bs);
+      dpp_min_step<0x140>(bk, bs);
+      int pick[3][3];
+#pragma unroll
+      for (int p = 0; p < 3; p++) {  // uniform from here: lane reads
+        const uint64_t sk = readlane64(bk, 16 * p), nk = readlane64(key, 48 + p);
+        const int s = __builtin_amdgcn_readlane(bs, 16 * p);
+        const int best = nk <= sk ? -1 : s;
+        const int src = 16 * p + (best < 0 ? 0 : best);
+        const int q0 = __builtin_amdgcn_readlane(x0, src), q1 = __builtin_amdgcn_readlane(x1, src);
+        // a stretched superblock has no unit of its own
+        const bool has = fsx < g.cols[p] && fsy < g.rows[p];
+        pick[p][0] = has ? best : -2;
+        pick[p][1] = has && best >= 0 ? q0 : 0;
+        pick[p][2] = has && best >= 0 ? q1 : 0;
+      }
+      DPHASE(2);
+      load(k + kDecideAhead, lx, ly, ev[d], xv0[d], xv1[d]);  // this slot's next superblock
+      if (++lx == tsw) {
+        lx = 0;
+        ly++;
+      }
+      if (lane < 9) {  // the picks wait in LDS (a store would hold up the loads' counter)
+        const int p = lane / 3, j = lane % 3;
+        const int v = p == 0 ? (j == 0 ? pick[0][0] : j == 1 ? pick[0][1] : pick[0][2])
+                    : p == 1 ? (j == 0 ? pick[1][0] : j == 1 ? pick[1][1] : pick[1][2])
+                             : (j == 0 ? pick[2][0] : j == 1 ? pick[2][1] : pick[2][2]);
+        const int8_t b = (int8_t)(j == 0 && v < 0 ? -1 : v);
+        if (buffered)
+          ubuf[k][p][j] = b;
+        else
+          a.units[(((size_t)p * g.urows_max + fsy) * g.ucols_max + fsx) * 3 + j] = b;
+      }
+      DPHASE(3);
+#pragma unroll
+      for (int p = 0; p < 3; p++)
+        if (pick[p][0] > -2) {
+          const int8_t q[2] = {(int8_t)pick[p][1], (int8_t)pick[p][2]};
+          lrf_commit(st, p, pick[p][0], q);
+        }
+      DPHASE(4);
+      if (++sx == tsw) {
+        sx = 0;
+        sy++;
       }
     }
-    int pick[3][3];
-#pragma unroll
-    for (int p = 0; p < 3; p++) {
-      const uint64_t sk = __shfl(bk, 16 * p, 64), nk = __shfl(key, 48 + p, 64);
-      const int s = __shfl(bs, 16 * p, 64);
-      const int best = nk <= sk ? -1 : s;
-      const int src = 16 * p + (best < 0 ? 0 : best);
-      const int q0 = __shfl(x0, src, 64), q1 = __shfl(x1, src, 64);
-      // a stretched superblock has no unit of its own
-      const bool has = fsx < g.cols[p] && fsy < g.rows[p];
-      pick[p][0] = has ? best : -2;
-      pick[p][1] = has && best >= 0 ? q0 : 0;
-      pick[p][2] = has && best >= 0 ? q1 : 0;
+  }
+#ifdef LRF_PHASES
+  if (lane == 0 && t == 0)
+    for (int i = 0; i < 5; i++) lrf_dphase[i] = dacc[i];
+#endif
+  if (buffered) {
+    __syncthreads();
+    for (int i = lane; i < n * 9; i += 64) {
+      const int k = i / 9, p = (i / 3) % 3, j = i % 3;
+      const int fsx = t0x + k % tsw, fsy = t0y + k / tsw;
+      a.units[(((size_t)p * g.urows_max + fsy) * g.ucols_max + fsx) * 3 + j] = ubuf[k][p][j];
     }
-    if (lane < 3) {
-      const int p = lane;
-      const int b0 = p == 0 ? pick[0][0] : p == 1 ? pick[1][0] : pick[2][0];
-      const int b1 = p == 0 ? pick[0][1] : p == 1 ? pick[1][1] : pick[2][1];
-      const int b2 = p == 0 ? pick[0][2] : p == 1 ? pick[1][2] : pick[2][2];
-      int8_t *u = a.units + (((size_t)p * g.urows_max + fsy) * g.ucols_max + fsx) * 3;
-      u[0] = (int8_t)(b0 < 0 ? -1 : b0);
-      u[1] = (int8_t)b1;
-      u[2] = (int8_t)b2;
-    }
-#pragma unroll
-    for (int p = 0; p < 3; p++)
-      if (pick[p][0] > -2) {
-        const int8_t q[2] = {(int8_t)pick[p][1], (int8_t)pick[p][2]};
-        lrf_commit(st, p, pick[p][0], q);
-      }
-    e = en;
-    x0 = n0;
-    x1 = n1;
   }
 }
 
@@ -993,10 +1135,30 @@ int lrf_geometry(int width, int height, int xdec, int ydec, int bit_depth, int b
   return RV_OK;
 }
 
+// g_lrf_subexp, once per process (the table is a constant of the codec)
+static int lrf_lut_upload() {
+  static std::once_flag once;
+  static int rc = RV_OK;
+  std::call_once(once, [] {
+    static uint8_t t[2][128][128];
+    for (int i = 0; i < 2; i++)
+      for (int x = 0; x < 128; x++)
+        for (int r = 0; r < 128; r++) {
+          const int lo = i ? -32 : -96;
+          const uint32_t b = lrf_subexp_ref(x + lo, lo, lo + 128, 4, r + lo);
+          if (b > 255) rc = RV_EINVAL;
+          t[i][x][r] = (uint8_t)b;
+        }
+    if (rc == RV_OK && hipMemcpyToSymbol(HIP_SYMBOL(g_lrf_subexp), t, sizeof(t)) != hipSuccess) rc = RV_EHIP;
+  });
+  return rc == RV_OK ? RV_OK : rv_set_error(rc, "loop restoration: subexp table upload failed");
+}
+
 int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *skip, int mi_stride,
                    const float *imp, int w_imp, int w_in_b, int h_in_b, const LrfGeo &g, int cdef,
                    const uint8_t *dir, const int32_t *var, const uint8_t cdef_str[2], const double ds[3],
                    uint64_t *err, int8_t *xqd, double lambda, int8_t *units, hipStream_t s) {
+  if (lrf_lut_upload() != RV_OK) return RV_EHIP;
   LrfRdoArgs a;
   memset(&a, 0, sizeof(a));
   for (int p = 0; p < 3; p++) {

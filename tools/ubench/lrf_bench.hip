@@ -104,6 +104,7 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventCreate(&e2));
+  if (lrf_lut_upload() != RV_OK) return 1;
   const dim3 grid((unsigned)g.nsb, 3);
   for (int r = 0; r < reps; r++) {
     CK(hipEventRecord(e0, 0));
@@ -132,6 +133,10 @@ int main(int argc, char **argv) {
            (q[1] - q[0]) / 100.0, (q[2] - q[1]) / 100.0, (q[3] - q[2]) / 100.0, (q[4] - q[3]) / 100.0);
   }
   printf("  total %8.2f\n", (t[6 + 5 * 15 + 4] - t[0]) / 100.0);
+  unsigned long long dp[5];
+  CK(hipMemcpyFromSymbol(dp, HIP_SYMBOL(lrf_dphase), sizeof(dp)));
+  printf("decide, tile 0, shader clocks per step: wait+loads %.0f rate %.0f min+picks %.0f stores %.0f commit %.0f\n",
+         dp[0] / 272.0, dp[1] / 272.0, dp[2] / 272.0, dp[3] / 272.0, dp[4] / 272.0);
 #endif
   return 0;
 }
