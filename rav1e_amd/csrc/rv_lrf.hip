@@ -483,6 +483,7 @@ struct LrfRdoArgs {
   const float *imp;
   int w_imp, w_in_b, h_in_b;
   LrfGeo g;
+  int p0;                    // the launch's first plane (blockIdx.y + p0)
   int cdef;                  // CDEF on (strengths at index 0)
   const uint8_t *dir;        // cdef_analyze_superblock of the unit's input: per 8x8 luma block,
   const int32_t *var;        // pitch dstride (rv_cdef_find_dirs)
@@ -493,57 +494,65 @@ struct LrfRdoArgs {
   int8_t *xqd;               // [3][nsb][16][2]
 };
 
-// 1024 lanes (16 waves, ~130 KB of LDS: one workgroup per CU). The boxes'
-// (p, sum) are set-independent: computed once, each set's (a, b) tables are
-// a multiply and a table lookup per entry. Pixel phases: a lane owns a
-// column strip of 4 pixels (one table read serves all four) and keeps its f
-// values in registers from the solve sums to the filtered pixels.
-// Distortion phase: lanes 0 .. 511, 8 per 8x8 block, one row each, the
-// block's moments summed over the 8 lanes by shuffles.
-constexpr int kRdoThreads = 1024;
-
+// One workgroup per unit, BW * BH / 4 lanes: a lane owns a column strip of
+// 4 pixels (x, y0 .. y0 + 3) -- one table read serves all four -- and keeps
+// its f values in registers from the solve sums to the filtered pixels.
+// 64 x 64 units (luma, 4:4:4 chroma): 1024 lanes, ~135 KB of LDS, one per
+// CU; 32 x 32 (4:2:0 chroma): 256 lanes, ~36 KB, several per CU. The
+// boxes' (p, sum) are set-independent: computed once, each set's (a, b)
+// tables are a multiply and a table lookup per entry. The distortion of an
+// option comes from the lanes' registers: 64-wide units sum half blocks
+// over 8 lanes and the last wave joins the halves; 4:2:0 chroma sums 2x2
+// parts over lane pairs.
 #ifdef LRF_PHASES  // tools/ubench/lrf_bench.hip: one workgroup's phase clocks
 __device__ unsigned long long lrf_phase_t[96];
 #define PHASE(k) \
-  if (tid == 0 && blockIdx.x == LRF_PHASES && blockIdx.y == 0) lrf_phase_t[k] = wall_clock64()
+  if (tid == 0 && blockIdx.x == LRF_PHASES && p == 0) lrf_phase_t[k] = wall_clock64()
 #else
 #define PHASE(k)
 #endif
 
+template <int BW, int BH>
 struct RdoLds {
+  using L = SgrLds<BW, BH>;
+  static constexpr int NT = BW * BH / 4, NW = NT / 64;
   union {
-    uint32_t img[2 * SgrL64::IR * SgrL64::IS];  // ii, sq
-    uint2 tab[SgrL64::TAB];                     // then each set's (a, b)
+    uint32_t img[2 * L::IR * L::IS];  // ii, sq
+    uint2 tab[L::TAB];                // then each set's (a, b)
   } a;
   union {
-    uint16_t lin[64 * 64];  // the unit's input (lrf_input)
-    uint2 ps[SgrL64::TAB];  // then the boxes' (p, sum)
+    uint16_t lin[BW * BH];  // the unit's input (lrf_input)
+    uint2 ps[L::TAB];       // then the boxes' (p, sum)
   } b;
   uint16_t xz[256];
-  int16_t coffs[48];      // cdef_offsets at the pad's pitch
-  uint16_t pad[68 * 68];  // the padded CDEF input, then each option's output
-  uint16_t ssolve[64 * 64], esrc[64 * 64];  // the source at the solve's / the distortion's place
+  int16_t coffs[48];                     // cdef_offsets at the pad's pitch
+  uint16_t pad[(BW + 4) * (BH + 4)];     // the padded CDEF input
+  uint16_t ssolve[BW * BH], esrc[BW * BH];  // the source at the solve's / the distortion's place
   uint8_t bdir[64], bskip[64];
   int32_t bvar[64];
-  uint64_t red[kRdoThreads / 64];
-  int64_t red5[5][kRdoThreads / 64];
-  uint3 hm[16 * 8];            // luma: each half block's (sd, sd2, ssd), [strip][block column]
-  int32_t bss[64];             // luma: each block's source sum and sum of squares
+  int64_t red5[5][NW];
+  uint3 hm[(BH / 4) * 8];  // 64-wide: each half block's (sd, sd2, ssd) / (sse), [strip][block column]
+  uint64_t wsum[NW];       // 4:2:0 chroma: each wave's biased part errors
+  int32_t bss[64];         // luma: each block's source sum and sum of squares
   uint32_t bss2[64];
   int8_t sxqd[2];
 };
 
-template <typename Px>
-__global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
-  __shared__ RdoLds S;
-  constexpr int AS = SgrL64::AS, A1R = SgrL64::A1R;
+template <typename Px, int BW, int BH>
+__global__ __launch_bounds__(BW * BH / 4) void lrf_rdo_kernel(LrfRdoArgs a) {
+  using Lds = RdoLds<BW, BH>;
+  using SL = SgrLds<BW, BH>;
+  constexpr int NT = Lds::NT, NW = Lds::NW, AS = SL::AS, A1R = SL::A1R;
+  constexpr int LBW = BW == 64 ? 6 : 5;
+  constexpr bool WIDE = BW == 64;  // luma / 4:4:4 chroma; else 4:2:0 chroma
+  __shared__ Lds S;
   const LrfGeo &g = a.g;
-  const int p = blockIdx.y, sb = blockIdx.x, tid = threadIdx.x;
+  const int p = a.p0 + blockIdx.y, sb = blockIdx.x, tid = threadIdx.x;
   const int sbc = g.sbc, fsx = sb % sbc, fsy = sb / sbc;
   if (fsx >= g.cols[p] || fsy >= g.rows[p]) return;  // no unit (uniform)
   const int t0x = fsx - fsx % g.tws, t0y = fsy - fsy % g.ths, sx = fsx - t0x, sy = fsy - t0y;
-  const int xd = p ? g.xdec : 0, yd = p ? g.ydec : 0, bw = 64 >> xd, bh = 64 >> yd, npx = bw * bh;
-  const int lbw = 6 - xd;  // log2 bw
+  const int xd = p ? g.xdec : 0, yd = p ? g.ydec : 0;
+  constexpr int npx = BW * BH;
   const int tw_px = min(g.tws * 64, g.W - t0x * 64), th_px = min(g.ths * 64, g.H - t0y * 64);
   const int pw_t = (tw_px + xd) >> xd, ph_t = (th_px + yd) >> yd;
   const int mi_cols = tw_px >> 2, mi_rows = th_px >> 2;
@@ -555,10 +564,10 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
   };
   PHASE(0);
   sgr_init_xz(S.xz);
-  cdef_offsets(S.coffs, bw + 4);
+  cdef_offsets(S.coffs, BW + 4);
   // 1. the padded copy and the unit's input
-  for (int i = tid; i < (bh + 4) * (bw + 4); i += blockDim.x) {
-    const int y = i / (bw + 4) - 2, x = i % (bw + 4) - 2, tx = ox + x, ty = oy + y;
+  for (int i = tid; i < (BH + 4) * (BW + 4); i += NT) {
+    const int y = i / (BW + 4) - 2, x = i % (BW + 4) - 2, tx = ox + x, ty = oy + y;
     int v = kVeryLarge;
     if (tx >= 0 && tx < pw_t && ty >= 0 && ty < ph_t) {
       const int csx = (tx << xd) >> 6, csy = (ty << yd) >> 6;
@@ -566,9 +575,9 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
     }
     S.pad[i] = (uint16_t)v;
   }
-  const int vw = min(bw, pw_t - ox), vh = min(bh, ph_t - oy);
-  for (int i = tid; i < npx; i += blockDim.x) {
-    const int y = i >> lbw, x = i & (bw - 1);
+  const int vw = min(BW, pw_t - ox), vh = min(BH, ph_t - oy);
+  for (int i = tid; i < npx; i += NT) {
+    const int y = i >> LBW, x = i & (BW - 1);
     S.b.lin[i] = (uint16_t)recpx(fx0 + ox + min(x, vw - 1), fy0 + oy + min(y, vh - 1));
   }
   // the unit (unit size clipped at the tile-relative offset, the
@@ -578,7 +587,7 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
   // blocks inside the tile (a block reaches at most 7 past the frame, into
   // the plane's padding)
   const int pw = p ? (g.W + xd) >> xd : g.W, ph = p ? (g.H + yd) >> yd : g.H;
-  const int uw = min(bw, pw - ox), uh = min(bh, ph - oy);
+  const int uw = min(BW, pw - ox), uh = min(BH, ph - oy);
   const int64_t ss_ = src.stride;
   const Px *const sp = (const Px *)src.data;
   const int elx = (min(8, max(0, (mi_cols - sx * 16 + 1) / 2)) * 8) >> xd;
@@ -586,8 +595,8 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
   {
     const Px *const ssolve = sp + (int64_t)(src.yorigin + oy) * ss_ + src.xorigin + ox;
     const Px *const sdist = sp + (int64_t)(src.yorigin + fy0 + oy) * ss_ + src.xorigin + fx0 + ox;
-    for (int i = tid; i < npx; i += blockDim.x) {
-      const int y = i >> lbw, x = i & (bw - 1);
+    for (int i = tid; i < npx; i += NT) {
+      const int y = i >> LBW, x = i & (BW - 1);
       S.ssolve[i] = (x < uw && y < uh) ? (uint16_t)ssolve[(int64_t)y * ss_ + x] : 0;
       S.esrc[i] = (x < elx && y < ely) ? (uint16_t)sdist[(int64_t)y * ss_ + x] : 0;
     }
@@ -614,8 +623,8 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
     }
     __syncthreads();
     const int bxs = 8 >> xd, bys = 8 >> yd;
-    for (int i = tid; i < npx; i += blockDim.x) {
-      const int y = i >> lbw, x = i & (bw - 1), blk = (y / bys) * 8 + x / bxs;
+    for (int i = tid; i < npx; i += NT) {
+      const int y = i >> LBW, x = i & (BW - 1), blk = (y / bys) * 8 + x / bxs;
       if (S.bskip[blk]) continue;  // skip: the copy (equal to lin); 2: outside the tile
       int pri, sec, dmp = a.damping + cs, d;
       if (p == 0) {
@@ -628,147 +637,145 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
         dmp -= 1;
         d = a.pri_uv ? S.bdir[blk] : 0;
       }
-      S.b.lin[i] = (uint16_t)cdef_px(S.pad + (y + 2) * (bw + 4) + x + 2, S.coffs + 6 * d, pri, sec, dmp, cs);
+      S.b.lin[i] = (uint16_t)cdef_px(S.pad + (y + 2) * (BW + 4) + x + 2, S.coffs + 6 * d, pri, sec, dmp, cs);
     }
   }
   __syncthreads();
   // 3. the unit's integral image: lrf_input alone, replicated
   PHASE(2);
-  sgr_integral<SgrL64::IS, SgrL64::IR>(S.a.img, uw, uh, [&](int r, int c) -> uint32_t {
-    return S.b.lin[iclamp(r - 4, 0, uh - 1) * bw + iclamp(c - 4, 0, uw - 1)];
+  sgr_integral<SL::IS, SL::IR>(S.a.img, uw, uh, [&](int r, int c) -> uint32_t {
+    return S.b.lin[iclamp(r - 4, 0, uh - 1) * BW + iclamp(c - 4, 0, uw - 1)];
   });
-  // the lane's pixels and the option None's pixels (the input as it is)
+  // the lane's column strip (qx, qy0 .. qy0 + 3): its input pixels
   PHASE(3);
-  // the lane's column strip: pixels (qx, qy0 .. qy0 + 3), on the unit's
-  // raster (lanes past its height idle in the pixel phases)
-  const int qx = tid & (bw - 1), qy0 = (tid >> lbw) * 4;
-  const bool qlane = qy0 < bh;
-  uint32_t pxr[4];
+  const int qx = tid & (BW - 1), qy0 = (tid >> LBW) * 4;
+  uint32_t pxr[4], lnr[4];  // the unit's pixels (0 outside it), lrf_input's
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const int y = qy0 + k, i = y * bw + qx;
-    pxr[k] = 0;
-    if (qlane) {
-      const bool in = qx < uw && y < uh;
-      if (in) pxr[k] = S.b.lin[i];
-      S.pad[i] = S.b.lin[i];
-    }
+    const int y = qy0 + k, i = y * BW + qx;
+    lnr[k] = S.b.lin[i];
+    pxr[k] = (qx < uw && y < uh) ? lnr[k] : 0;
   }
   __syncthreads();  // lin is read: the boxes take its place
   PHASE(4);
-  const SgrLane ln = sgr_lane(uw);
-  sgr_boxes<SgrL64::IS, SgrL64::IR, AS, A1R>(S.a.img, S.b.ps, ln, uh, cs);
-  // 4. the distortion lanes: rdo_loop_plane_error over the superblock's 8x8s
-  // in the tile; lane = (block, row)
-  const int eb = tid >> 3, ej = tid & 7, ebx = eb & 7, eby = eb >> 3;
-  const int egx = sx * 16 + 2 * ebx, egy = sy * 16 + 2 * eby;
-  const bool eblk = eb < 64 && egx < mi_cols && egy < mi_rows;
-  const int w8 = 8 >> xd, h8 = 8 >> yd, pbw = min(8, w8) >> xd, pbh = min(8, h8) >> yd;
-  const int eqx = (8 * ebx) >> xd, eqy = ((8 * eby) >> yd) + ej;
-  const bool erow = eblk && ej < h8;
-  const double ebias =
-      eblk ? lrf_bias(a.imp, a.w_imp, a.w_in_b, a.h_in_b, t0x * 16 + egx, t0y * 16 + egy) : 0.0;
-  // the luma finish: lane b of the last wave prices block b
-  constexpr int kFinWave = kRdoThreads / 64 - 1;
-  const bool fin = (tid >> 6) == kFinWave;
-  const int fgx = sx * 16 + 2 * (tid & 7), fgy = sy * 16 + 2 * ((tid >> 3) & 7);
-  const bool eblk8 = fin && fgx < mi_cols && fgy < mi_rows;
-  const double bbias8 =
-      eblk8 ? lrf_bias(a.imp, a.w_imp, a.w_in_b, a.h_in_b, t0x * 16 + fgx, t0y * 16 + fgy) : 0.0;
-  auto plane_err = [&]() -> uint64_t {  // the option's pixels in pad
-    uint64_t e = 0;
-    const int eo = eqy * bw + eqx;
-    if (p == 0) {
-      int32_t ss = 0, sd = 0;
-      uint32_t ss2 = 0, sd2 = 0, ssd = 0;
-      if (erow) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          const int32_t s = S.esrc[eo + i], d = S.pad[eo + i];
-          ss += s;
-          sd += d;
-          ss2 += (uint32_t)(s * s);
-          sd2 += (uint32_t)(d * d);
-          ssd += (uint32_t)(s * d);
-        }
-      }
-      ss = dpp_sum8(ss);
-      sd = dpp_sum8(sd);
-      ss2 = dpp_sum8(ss2);
-      sd2 = dpp_sum8(sd2);
-      ssd = dpp_sum8(ssd);
-      if (eblk && ej == 0) e = biased(cdef_dist(ss, sd, ss2, sd2, ssd, bd), ebias);
-    } else {  // sse_wxh of (8 >> xdec) x (8 >> ydec) in parts of the importance block
-      uint32_t v0 = 0, v1 = 0;  // the row's part columns (w8 / pbw <= 2)
-      if (erow) {
-#pragma unroll
-        for (int i = 0; i < 8; i++)
-          if (i < w8) {
-            const int c = (int)(int16_t)S.esrc[eo + i] - (int)(int16_t)S.pad[eo + i];
-            if (i < pbw)
-              v0 += (uint32_t)(c * c);
-            else
-              v1 += (uint32_t)(c * c);
-          }
-      }
-      for (int o = 1; o < pbh; o <<= 1) {  // the part's rows (aligned lane groups)
-        v0 += __shfl_xor(v0, o, RV_WAVE);
-        v1 += __shfl_xor(v1, o, RV_WAVE);
-      }
-      if (erow && ej % pbh == 0) e = biased(v0, ebias) + (w8 > pbw ? biased(v1, ebias) : 0);
-    }
-    return (uint64_t)((double)wg_sum_u64(e, S.red) * a.ds[p]);
-  };
-  if (p == 0 && tid < 64) {  // the source moments of the luma blocks (every set reuses them)
+  const SgrLane ln = sgr_lane(uw, tid, NT);
+  sgr_boxes<SL::IS, SL::IR, AS, A1R>(S.a.img, S.b.ps, ln, uh, cs);
+  // 4. the distortion: rdo_loop_plane_error over the superblock's 8x8s in
+  // the tile (cdef_dist_wxh_8x8 for luma, sse_wxh in the importance
+  // block's parts for chroma), each weighted by its distortion bias
+  const int wave = tid >> 6;
+  const bool fin = wave == NW - 1;  // the last wave joins the parts
+  const int fb = tid & 63, fgx = sx * 16 + 2 * (fb & 7), fgy = sy * 16 + 2 * (fb >> 3);
+  const bool fblk = fin && fgx < mi_cols && fgy < mi_rows;  // lane fb of the last wave: block fb
+  const double fbias = fblk ? lrf_bias(a.imp, a.w_imp, a.w_in_b, a.h_in_b, t0x * 16 + fgx, t0y * 16 + fgy) : 0.0;
+  // 4:2:0 chroma: lane (qx, strip by) covers column qx of the 4x4 block
+  // (qx / 4, by); the even lane of a pair adds up its two 2x2 parts
+  const int cgx = sx * 16 + 2 * (qx >> 2), cgy = sy * 16 + 2 * (qy0 >> 2);
+  const bool cblk = !WIDE && !(qx & 1) && cgx < mi_cols && cgy < mi_rows;
+  const double cbias = cblk ? lrf_bias(a.imp, a.w_imp, a.w_in_b, a.h_in_b, t0x * 16 + cgx, t0y * 16 + cgy) : 0.0;
+  if (WIDE && p == 0 && tid < 64) {  // luma blocks' source moments (every option reuses them)
     int32_t ss = 0;
     uint32_t ss2 = 0;
     for (int j = 0; j < 8; j++)
       for (int i = 0; i < 8; i++) {
-        const int32_t v = S.esrc[(8 * (tid >> 3) + j) * 64 + 8 * (tid & 7) + i];
+        const int32_t v = S.esrc[(8 * (tid >> 3) + j) * BW + 8 * (tid & 7) + i];
         ss += v;
         ss2 += (uint32_t)(v * v);
       }
     S.bss[tid] = ss;
     S.bss2[tid] = ss2;
   }
+  // an option's pixels d[4] (the lane's strip) -> its partial sums in LDS
+  auto err_part = [&](const int32_t d[4]) {
+    if (WIDE) {
+      if (p == 0) {
+        int32_t sd = 0;
+        uint32_t sd2 = 0, ssd = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int32_t sv = S.esrc[(qy0 + k) * BW + qx];
+          sd += d[k];
+          sd2 += (uint32_t)(d[k] * d[k]);
+          ssd += (uint32_t)(sv * d[k]);
+        }
+        sd = dpp_sum8(sd);
+        sd2 = dpp_sum8(sd2);
+        ssd = dpp_sum8(ssd);
+        if ((qx & 7) == 0) S.hm[(qy0 >> 2) * 8 + (qx >> 3)] = make_uint3((uint32_t)sd, sd2, ssd);
+      } else {  // 4:4:4 chroma: one 8x8 part per block
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int c = (int)(int16_t)S.esrc[(qy0 + k) * BW + qx] - (int)(int16_t)d[k];
+          v += (uint32_t)(c * c);
+        }
+        v = dpp_sum8(v);
+        if ((qx & 7) == 0) S.hm[(qy0 >> 2) * 8 + (qx >> 3)] = make_uint3(v, 0, 0);
+      }
+    } else {
+      uint32_t top = 0, bot = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int c = (int)(int16_t)S.esrc[(qy0 + k) * BW + qx] - (int)(int16_t)d[k];
+        if (k < 2)
+          top += (uint32_t)(c * c);
+        else
+          bot += (uint32_t)(c * c);
+      }
+      top += dpp32<0xB1>(top);  // the lane pair (quad_perm [1,0,3,2])
+      bot += dpp32<0xB1>(bot);
+      uint64_t e = cblk ? biased(top, cbias) + biased(bot, cbias) : 0;
+      e = dpp_sum64(e);
+      if ((tid & 63) == 0) S.wsum[wave] = e;
+    }
+  };
   uint64_t *eo = a.err + ((size_t)p * g.nsb + sb) * 17;
   int8_t *xo = a.xqd + ((size_t)p * g.nsb + sb) * 32;
+  // option o's distortion from the parts: the last wave, after the next
+  // barrier (the parts are rewritten two barriers later)
+  auto err_finish = [&](int o) {
+    uint64_t e = 0;
+    if (WIDE) {
+      if (fblk) {
+        const uint3 u0 = S.hm[(2 * (fb >> 3)) * 8 + (fb & 7)], u1 = S.hm[(2 * (fb >> 3) + 1) * 8 + (fb & 7)];
+        e = p == 0 ? biased(cdef_dist(S.bss[fb], (int32_t)(u0.x + u1.x), S.bss2[fb], u0.y + u1.y, u0.z + u1.z, bd),
+                            fbias)
+                   : biased((uint64_t)u0.x + u1.x, fbias);
+      }
+      e = dpp_sum64(e);
+    } else {
+      for (int w = 0; w < NW; w++) e += S.wsum[w];
+    }
+    if (fb == 0) eo[o] = (uint64_t)((double)e * a.ds[p]);
+  };
   {
-    const uint64_t e = plane_err();  // (its barriers also publish the boxes)
-    if (tid == 0) eo[0] = e;
+    int32_t d[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) d[k] = (int32_t)lnr[k];  // None: the input as it is
+    err_part(d);
   }
-  PHASE(5);
   // 5. the 16 sets: tables, solve sums, xqd, the filtered unit's
   // distortion; wave 0 solves set s while the other waves build set s + 1's
   // tables (the f values of s are in registers by then)
   using Acc = typename std::conditional<sizeof(Px) == 1, int32_t, int64_t>::type;  // 8-bit: 4 products fit
-  const SgrLane ln_rest = sgr_lane(uw, tid - 64, kRdoThreads - 64);
+  const SgrLane ln_rest = sgr_lane(uw, tid - 64, NT - 64);
+  __syncthreads();  // the boxes and the None parts
+  if (fin) err_finish(0);
   sgr_tables_ps<AS, A1R>(S.b.ps, S.a.tab, S.xz, ln, 0, uh);
-  // set s's luma distortion from its half blocks: the last wave, after the
-  // next barrier (hm is rewritten two barriers later)
-  auto luma_finish = [&](int set) {
-    const int b = tid & 63;
-    uint64_t e = 0;
-    if (eblk8) {
-      const uint3 u0 = S.hm[(2 * (b >> 3)) * 8 + (b & 7)], u1 = S.hm[(2 * (b >> 3) + 1) * 8 + (b & 7)];
-      e = biased(cdef_dist(S.bss[b], (int32_t)(u0.x + u1.x), S.bss2[b], u0.y + u1.y, u0.z + u1.z, bd), bbias8);
-    }
-    e = dpp_sum64(e);
-    if (b == 0) eo[1 + set] = (uint64_t)((double)e * a.ds[p]);
-  };
+  PHASE(5);
   for (int set = 0; set < 16; set++) {
     __syncthreads();
     PHASE(6 + 5 * set);
-    if (p == 0 && set > 0 && fin) luma_finish(set - 1);
+    if (set > 0 && fin) err_finish(set);  // set - 1's, at eo[set]
     uint32_t f2r[4] = {0, 0, 0, 0}, f1r[4] = {0, 0, 0, 0};
     Acc H00 = 0, H11 = 0, H01 = 0, C0 = 0, C1 = 0;
-    if (qlane && qx < uw) {
+    if (qx < uw) {
       sgr_f4<AS, A1R>(S.a.tab, set, qx, qy0, pxr, f2r, f1r);
 #pragma unroll
       for (int k = 0; k < 4; k++)
         if (qy0 + k < uh) {
           const Acc u = (Acc)pxr[k] << kRstBits;
-          const Acc sv = ((Acc)S.ssolve[(qy0 + k) * bw + qx] << kRstBits) - u;
+          const Acc sv = ((Acc)S.ssolve[(qy0 + k) * BW + qx] << kRstBits) - u;
           const Acc e2 = (Acc)(int32_t)f2r[k] - u, e1 = (Acc)(int32_t)f1r[k] - u;
           H00 += e2 * e2;
           H11 += e1 * e1;
@@ -782,15 +789,15 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
 #pragma unroll
       for (int q = 0; q < 5; q++) {
         const int64_t t = (int64_t)dpp_sum64((uint64_t)v[q]);
-        if ((tid & 63) == 0) S.red5[q][tid >> 6] = t;
+        if ((tid & 63) == 0) S.red5[q][wave] = t;
       }
     }
     __syncthreads();
     PHASE(7 + 5 * set);
-    if (tid < 64) {  // wave 0: the solve (lanes 0 .. 4 add up one sum each)
+    if (wave == 0) {  // the solve (lanes 0 .. 4 add up one sum each)
       int64_t t = 0;
       if (tid < 5)
-        for (int w = 0; w < kRdoThreads / 64; w++) t += S.red5[tid][w];
+        for (int w = 0; w < NW; w++) t += S.red5[tid][w];
       const int64_t h00 = readlane64((uint64_t)t, 0), h11 = readlane64((uint64_t)t, 1),
                     h01 = readlane64((uint64_t)t, 2), c0 = readlane64((uint64_t)t, 3),
                     c1 = readlane64((uint64_t)t, 4);
@@ -808,44 +815,16 @@ __global__ __launch_bounds__(kRdoThreads) void lrf_rdo_kernel(LrfRdoArgs a) {
     __syncthreads();
     PHASE(8 + 5 * set);
     const int w0 = S.sxqd[0], w1 = S.sxqd[1];
-    if (p == 0) {
-      // luma: the filtered pixels' moments straight from registers -- a
-      // strip is half a block column: 8 lanes make a half block, wave 0 puts
-      // the halves together and prices the 64 blocks
-      int32_t sd = 0;
-      uint32_t sd2 = 0, ssd = 0;
+    int32_t d[4];
 #pragma unroll
-      for (int k = 0; k < 4; k++) {  // 128 outside the unit: lrf_output's fill (never inside the frame)
-        const int y = qy0 + k;
-        const int32_t d = (qx < uw && y < uh) ? sgr_out(f2r[k], f1r[k], pxr[k], w0, w1, mx) : 128;
-        const int32_t sv = S.esrc[y * 64 + qx];
-        sd += d;
-        sd2 += (uint32_t)(d * d);
-        ssd += (uint32_t)(sv * d);
-      }
-      sd = dpp_sum8(sd);
-      sd2 = dpp_sum8(sd2);
-      ssd = dpp_sum8(ssd);
-      if ((qx & 7) == 0) S.hm[(qy0 >> 2) * 8 + (qx >> 3)] = make_uint3((uint32_t)sd, sd2, ssd);
-      PHASE(9 + 5 * set);
-    } else {
-      if (qlane) {
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-          S.pad[(qy0 + k) * bw + qx] =
-              (qx < uw && qy0 + k < uh) ? (uint16_t)sgr_out(f2r[k], f1r[k], pxr[k], w0, w1, mx) : 128;
-      }
-      __syncthreads();
-      PHASE(9 + 5 * set);
-      const uint64_t e = plane_err();
-      if (tid == 0) eo[1 + set] = e;
-    }
+    for (int k = 0; k < 4; k++)  // 128 outside the unit: lrf_output's fill (never inside the frame)
+      d[k] = (qx < uw && qy0 + k < uh) ? sgr_out(f2r[k], f1r[k], pxr[k], w0, w1, mx) : 128;
+    err_part(d);
+    PHASE(9 + 5 * set);
     PHASE(10 + 5 * set);
   }
-  if (p == 0) {
-    __syncthreads();
-    if (fin) luma_finish(15);
-  }
+  __syncthreads();
+  if (fin) err_finish(16);
 }
 
 // ---- the sequential decisions (count_lrf_switchable, write_lrf) -----------------
@@ -1158,6 +1137,7 @@ int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *
                    const float *imp, int w_imp, int w_in_b, int h_in_b, const LrfGeo &g, int cdef,
                    const uint8_t *dir, const int32_t *var, const uint8_t cdef_str[2], const double ds[3],
                    uint64_t *err, int8_t *xqd, double lambda, int8_t *units, hipStream_t s) {
+  if (g.xdec != g.ydec) return rv_set_error(RV_EINVAL, "loop restoration: 4:2:0, 4:4:4 (4:2:2 has none)");
   if (lrf_lut_upload() != RV_OK) return RV_EHIP;
   LrfRdoArgs a;
   memset(&a, 0, sizeof(a));
@@ -1184,12 +1164,23 @@ int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *
   a.damping = 3;  // cdef_damping (src/encoder.rs:665)
   a.err = err;
   a.xqd = xqd;
-  const dim3 grid((unsigned)g.nsb, 3);
+  // 64 x 64 units: luma (and 4:4:4 chroma); 32 x 32: 4:2:0 chroma
+  const bool c420 = g.xdec && g.ydec;
+  a.p0 = 0;
+  const dim3 grid64((unsigned)g.nsb, c420 ? 1 : 3), grid32((unsigned)g.nsb, 2);
   if (rec[0].hbd)
-    lrf_rdo_kernel<uint16_t><<<grid, kRdoThreads, 0, s>>>(a);
+    lrf_rdo_kernel<uint16_t, 64, 64><<<grid64, 1024, 0, s>>>(a);
   else
-    lrf_rdo_kernel<uint8_t><<<grid, kRdoThreads, 0, s>>>(a);
+    lrf_rdo_kernel<uint8_t, 64, 64><<<grid64, 1024, 0, s>>>(a);
   RV_HIP_CHECK_LAUNCH();
+  if (c420) {
+    a.p0 = 1;
+    if (rec[0].hbd)
+      lrf_rdo_kernel<uint16_t, 32, 32><<<grid32, 256, 0, s>>>(a);
+    else
+      lrf_rdo_kernel<uint8_t, 32, 32><<<grid32, 256, 0, s>>>(a);
+    RV_HIP_CHECK_LAUNCH();
+  }
   LrfDecideArgs d;
   d.g = g;
   d.err = err;

@@ -105,10 +105,12 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e1));
   CK(hipEventCreate(&e2));
   if (lrf_lut_upload() != RV_OK) return 1;
-  const dim3 grid((unsigned)g.nsb, 3);
   for (int r = 0; r < reps; r++) {
     CK(hipEventRecord(e0, 0));
-    lrf_rdo_kernel<uint8_t><<<grid, kRdoThreads>>>(a);
+    a.p0 = 0;
+    lrf_rdo_kernel<uint8_t, 64, 64><<<dim3(g.nsb, 1), 1024>>>(a);
+    a.p0 = 1;
+    lrf_rdo_kernel<uint8_t, 32, 32><<<dim3(g.nsb, 2), 256>>>(a);
     CK(hipEventRecord(e1, 0));
     lrf_decide_kernel<<<nt, 64>>>(d);
     CK(hipEventRecord(e2, 0));
@@ -120,7 +122,8 @@ int main(int argc, char **argv) {
   }
 #ifdef LRF_PHASES
   // one workgroup alone: its phases in wall_clock64 ticks (100 MHz)
-  lrf_rdo_kernel<uint8_t><<<dim3(LRF_PHASES + 1, 1), kRdoThreads>>>(a);
+  a.p0 = 0;
+  lrf_rdo_kernel<uint8_t, 64, 64><<<dim3(LRF_PHASES + 1, 1), 1024>>>(a);
   CK(hipDeviceSynchronize());
   unsigned long long t[96];
   CK(hipMemcpyFromSymbol(t, HIP_SYMBOL(lrf_phase_t), sizeof(t)));
