@@ -353,7 +353,7 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2, imp_wind
     frames = 1 + gops * gop
     nin = frames + 8 + (imp_window + 37 if imp_window else 0)
     gs = [RP.HipReplay(W, H, xdec, ydec, bd, nref, group=r, tile_size=ts, n_inputs=nin,
-                       flags=flags & ~RP.RV_REPLAY_LRF, imp_window=imp_window) for r in rects]
+                       flags=flags, imp_window=imp_window) for r in rects]
     # the importance window: each group's engine computes its blocks' part,
     # the parts meet in an in-process hub (the ranks' RCCL all-gather)
     hub = RP.LaHub(n) if imp_window else None
@@ -492,9 +492,10 @@ def main():
     n_inputs = args.warmup + args.steps + 8 + (imp_window + 29 + 8 if imp_window else 0)
     deblock = args.loop_filters in ("all", "cdef", "deblock")
     cdef = args.loop_filters in ("all", "cdef")
-    # loop restoration: one tile group (rv_replay_create); 4:2:2 has none
-    # (enable_restoration, src/encoder.rs:229-230)
-    lrf = args.loop_filters == "all" and world == 1 and not (xdec == 1 and ydec == 0)
+    # loop restoration: 4:2:2 has none (enable_restoration,
+    # src/encoder.rs:229-230); with tile groups each rank decides its own
+    # units and they travel with its reconstruction
+    lrf = args.loop_filters == "all" and not (xdec == 1 and ydec == 0)
     flags = (RP.RV_REPLAY_EXHAUSTIVE_FS if args.exhaustive_fs else 0) | \
         (RP.RV_REPLAY_SPEED6 if speed == 6 else 0) | (RP.RV_REPLAY_DEBLOCK if deblock else 0) | \
         (RP.RV_REPLAY_CDEF if cdef else 0) | (0 if args.no_entropy else RP.RV_REPLAY_ENTROPY) | \

@@ -619,8 +619,10 @@ typedef struct rv_replay_cfg {
  * count_lrf_switchable), then lrf_filter_frame after CDEF (src/lrf.rs:
  * 1345-1444, src/encoder.rs:2803-2806).  Units of one superblock in every
  * plane (RestorationState::new at base_q_idx <= 160, every level of the
- * default quantizer); one tile group.  The symbol prices assume a range
- * coder in its initial state (the replay codes no other symbols). */
+ * default quantizer).  With tile groups each group decides its own units
+ * before the exchange and they travel with its reconstruction (the choices
+ * are tile-local).  The symbol prices assume a range coder in its initial
+ * state (the replay codes no other symbols). */
 #define RV_REPLAY_LRF 512
 typedef struct rv_replay_frame_info {
   int32_t display;            /* display index of the coded frame */

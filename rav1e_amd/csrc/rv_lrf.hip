@@ -484,6 +484,7 @@ struct LrfRdoArgs {
   int w_imp, w_in_b, h_in_b;
   LrfGeo g;
   int p0;                    // the launch's first plane (blockIdx.y + p0)
+  int gx0, gy0, gx1, gy1;    // the superblocks decided here (a tile group's)
   int cdef;                  // CDEF on (strengths at index 0)
   const uint8_t *dir;        // cdef_analyze_superblock of the unit's input: per 8x8 luma block,
   const int32_t *var;        // pitch dstride (rv_cdef_find_dirs)
@@ -550,6 +551,7 @@ __global__ __launch_bounds__(BW * BH / 4) void lrf_rdo_kernel(LrfRdoArgs a) {
   const int p = a.p0 + blockIdx.y, sb = blockIdx.x, tid = threadIdx.x;
   const int sbc = g.sbc, fsx = sb % sbc, fsy = sb / sbc;
   if (fsx >= g.cols[p] || fsy >= g.rows[p]) return;  // no unit (uniform)
+  if (fsx < a.gx0 || fsx >= a.gx1 || fsy < a.gy0 || fsy >= a.gy1) return;  // another group's
   const int t0x = fsx - fsx % g.tws, t0y = fsy - fsy % g.ths, sx = fsx - t0x, sy = fsy - t0y;
   const int xd = p ? g.xdec : 0, yd = p ? g.ydec : 0;
   constexpr int npx = BW * BH;
@@ -830,6 +832,7 @@ __global__ __launch_bounds__(BW * BH / 4) void lrf_rdo_kernel(LrfRdoArgs a) {
 // ---- the sequential decisions (count_lrf_switchable, write_lrf) -----------------
 struct LrfDecideArgs {
   LrfGeo g;
+  int gx0, gy0, gx1, gy1;  // the superblocks decided here (whole tiles)
   const uint64_t *err;
   const int8_t *xqd;
   double lambda;
@@ -870,6 +873,7 @@ __global__ __launch_bounds__(64) void lrf_decide_kernel(LrfDecideArgs a) {
   const int ntx = (g.sbc + g.tws - 1) / g.tws;
   const int t = blockIdx.x, lane = threadIdx.x;
   const int t0x = (t % ntx) * g.tws, t0y = (t / ntx) * g.ths;
+  if (t0x < a.gx0 || t0x >= a.gx1 || t0y < a.gy0 || t0y >= a.gy1) return;  // another group's tile
   const int tsw = min(g.tws, g.sbc - t0x), tsh = min(g.ths, g.sbr - t0y), n = tsw * tsh;
   const bool none = lane >= 48, live = lane < 51;
   const int lp = none ? lane - 48 : lane >> 4, ls = none ? -1 : lane & 15;  // plane, set (-1: None)
@@ -1136,7 +1140,8 @@ static int lrf_lut_upload() {
 int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *skip, int mi_stride,
                    const float *imp, int w_imp, int w_in_b, int h_in_b, const LrfGeo &g, int cdef,
                    const uint8_t *dir, const int32_t *var, const uint8_t cdef_str[2], const double ds[3],
-                   uint64_t *err, int8_t *xqd, double lambda, int8_t *units, hipStream_t s) {
+                   uint64_t *err, int8_t *xqd, double lambda, int8_t *units, const int32_t *rect,
+                   hipStream_t s) {
   if (g.xdec != g.ydec) return rv_set_error(RV_EINVAL, "loop restoration: 4:2:0, 4:4:4 (4:2:2 has none)");
   if (lrf_lut_upload() != RV_OK) return RV_EHIP;
   LrfRdoArgs a;
@@ -1164,6 +1169,10 @@ int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *
   a.damping = 3;  // cdef_damping (src/encoder.rs:665)
   a.err = err;
   a.xqd = xqd;
+  a.gx0 = rect ? rect[0] : 0;
+  a.gy0 = rect ? rect[1] : 0;
+  a.gx1 = rect ? rect[0] + rect[2] : g.sbc;
+  a.gy1 = rect ? rect[1] + rect[3] : g.sbr;
   // 64 x 64 units: luma (and 4:4:4 chroma); 32 x 32: 4:2:0 chroma
   const bool c420 = g.xdec && g.ydec;
   a.p0 = 0;
@@ -1187,6 +1196,10 @@ int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *
   d.xqd = xqd;
   d.lambda = lambda;
   d.units = units;
+  d.gx0 = a.gx0;
+  d.gy0 = a.gy0;
+  d.gx1 = a.gx1;
+  d.gy1 = a.gy1;
   const int nt = ((g.sbc + g.tws - 1) / g.tws) * ((g.sbr + g.ths - 1) / g.ths);
   lrf_decide_kernel<<<nt, 64, 0, s>>>(d);
   RV_HIP_CHECK_LAUNCH();

@@ -1584,7 +1584,7 @@ int ensure_jobs(rv_replay *r) {
 // deblocking also its rows of the block map, planes 3 = log2 size, 4 =
 // skip), bytes into the group's slice of the exchange buffer.  Returns the
 // bytes; *n = the rectangles.
-int group_rects(const rv_replay *r, int k, XRect out[6], int *n) {
+int group_rects(const rv_replay *r, int k, XRect out[9], int *n) {
   const Geo &g = r->g;
   const int32_t *gr = r->grects + 4 * k;
   const int px = g.hbd ? 2 : 1;
@@ -1622,6 +1622,18 @@ int group_rects(const rv_replay *r, int k, XRect out[6], int *n) {
     off += (int64_t)(x1 - x0) * cb * (y1 - y0);
     (*n)++;
   }
+  if (r->lrf) {  // the group's loop-restoration units ((set, xqd0, xqd1) per superblock)
+    const int sbc = (g.W + kSb - 1) / kSb, sbr = (g.H + kSb - 1) / kSb;
+    const int x0 = gr[0], y0 = gr[1];
+    int x1 = gr[0] + gr[2], y1 = gr[1] + gr[3];
+    x1 = x1 < sbc ? x1 : sbc;
+    y1 = y1 < sbr ? y1 : sbr;
+    for (int p = 0; p < 3; p++) {
+      out[*n] = XRect{off, 6 + p, 3 * x0, y0, 3 * (x1 - x0), y1 - y0};
+      off += (int64_t)3 * (x1 - x0) * (y1 - y0);
+      (*n)++;
+    }
+  }
   return (int)off;
 }
 
@@ -1649,14 +1661,17 @@ static void xcopy_launch(hipStream_t st, const rv_plane *pl, const XRect *rects,
 // Copy rectangles between the slot's planes / the block map and a packed
 // buffer (pixel rectangles at the pixel width, map rectangles bytewise).
 int xcopy(rv_replay *r, const RvSlot &s, const XRect *rects, int n, int to_plane, uint8_t *buf) {
-  XRect px[3 * kMaxGroups], mp[3 * kMaxGroups];
-  int npx = 0, nmp = 0;
+  XRect px[3 * kMaxGroups], mp[3 * kMaxGroups], un[3 * kMaxGroups];
+  int npx = 0, nmp = 0, nun = 0;
   for (int i = 0; i < n; i++) {
     if (rects[i].plane < 3) {
       px[npx++] = rects[i];
-    } else {
+    } else if (rects[i].plane < 6) {
       mp[nmp] = rects[i];
       mp[nmp++].plane -= 3;
+    } else {
+      un[nun] = rects[i];
+      un[nun++].plane -= 6;
     }
   }
   const rv_plane pl[3] = {s.y, s.u, s.v};
@@ -1681,6 +1696,18 @@ int xcopy(rv_replay *r, const RvSlot &s, const XRect *rects, int n, int to_plane
     m[2].width = fb;
     m[2].height = r->g.h_in_b / 2;
     xcopy_launch<uint8_t>(r->stream, m, mp, nmp, to_plane, buf);
+  }
+  if (nun) {  // planes 6-8: the loop-restoration units of Y, U, V ([sbr][sbc][3] bytes each)
+    const int sbc = (r->g.W + kSb - 1) / kSb, sbr = (r->g.H + kSb - 1) / kSb;
+    rv_plane u[3];
+    memset(u, 0, sizeof(u));
+    for (int p = 0; p < 3; p++) {
+      u[p].data = r->lrf_units + (size_t)p * sbr * sbc * 3;
+      u[p].stride = 3 * sbc;
+      u[p].width = 3 * sbc;
+      u[p].height = sbr;
+    }
+    xcopy_launch<uint8_t>(r->stream, u, un, nun, to_plane, buf);
   }
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
@@ -1738,24 +1765,35 @@ int cdef_pad_slot(rv_replay *r, const RvSlot &s, int lv, const LrfGeo *lg) {
   return rv_frame_pad_dev(rec, lo, r->stream);
 }
 
+// rdo_loop_decision's restoration choices for the superblocks of group
+// rect (in superblocks; null: the frame), from the reconstruction as the
+// tile's coding leaves it (before the deblocking), into r->lrf_units.
+static int lrf_decide_slot(rv_replay *r, const RvSlot &s, const RvInput &in, int lv, const LrfGeo &lg,
+                           const int32_t *rect) {
+  const Geo &g = r->g;
+  const rv_plane rec[3] = {s.y, s.u, s.v}, src[3] = {in.y, in.u, in.v};
+  // its CDEF's directions (cdef_pad_slot finds the deblocked frame's
+  // afterwards, in the same buffers)
+  if (r->cdef)
+    RV_R(rv_cdef_find_dirs(&rec[0], g.W, g.H, r->mi_skip, r->mi_stride, r->cdef_dir, r->cdef_var, g.bd,
+                           r->stream));
+  return lrf_rdo_launch(rec, src, r->mi_skip, r->mi_stride, r->imp_last, g.w_imp, g.w_in_b, g.h_in_b, lg,
+                        r->cdef, r->cdef_dir, r->cdef_var, r->cdef_str[lv], r->lv[lv].ds, r->lrf_err,
+                        r->lrf_xqd, r->lv[lv].lambda, r->lrf_units, rect, r->stream);
+}
+
+// several tile groups (or a one-rank all-gather): each rank decides its own
+// units before the exchange and imports the others'
+static bool groups_active(const rv_replay *r) { return r->n_groups >= 2 || r->comm; }
+
 // The loop filters of a coded slot and its padding: the frame is then a
 // reference (src/encoder.rs:2789-2802, 3411-3429).
 int filter_slot(rv_replay *r, const RvSlot &s, const RvInput &in, int lv) {
   LrfGeo lg;
   if (r->lrf) {
-    // rdo_loop_decision's restoration choices, from the reconstruction as
-    // the tile's coding leaves it (before the deblocking)
     const Geo &g = r->g;
     RV_R(lrf_geometry(g.W, g.H, g.xdec, g.ydec, g.bd, r->lv[lv].qidx, g.tws, g.ths, &lg));
-    const rv_plane rec[3] = {s.y, s.u, s.v}, src[3] = {in.y, in.u, in.v};
-    // its CDEF's directions (cdef_pad_slot finds the deblocked frame's
-    // afterwards, in the same buffers)
-    if (r->cdef)
-      RV_R(rv_cdef_find_dirs(&rec[0], g.W, g.H, r->mi_skip, r->mi_stride, r->cdef_dir, r->cdef_var, g.bd,
-                             r->stream));
-    RV_R(lrf_rdo_launch(rec, src, r->mi_skip, r->mi_stride, r->imp_last, g.w_imp, g.w_in_b, g.h_in_b, lg,
-                        r->cdef, r->cdef_dir, r->cdef_var, r->cdef_str[lv], r->lv[lv].ds, r->lrf_err,
-                        r->lrf_xqd, r->lv[lv].lambda, r->lrf_units, r->stream));
+    if (!groups_active(r)) RV_R(lrf_decide_slot(r, s, in, lv, lg, nullptr));
   }
   if (r->deblock) RV_R(deblock_slot(r, s, in, lv));
   return r->cdef ? cdef_pad_slot(r, s, lv, r->lrf ? &lg : nullptr) : pad_slot(r, s);
@@ -2305,10 +2343,9 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
   }
   if (cfg->flags & RV_REPLAY_LRF) {
     LrfGeo lg;
-    if (!r->cdef || lrf_geometry(g.W, g.H, g.xdec, g.ydec, g.bd, 100, g.tws, g.ths, &lg) != RV_OK ||
-        g.tx0 || g.ty0 || g.tw * kSb < g.W || g.th * kSb < g.H) {
-      rv_set_error(RV_EINVAL, "rv_replay_create: RV_REPLAY_LRF needs RV_REPLAY_CDEF, one tile group "
-                              "and units of one superblock");
+    if (!r->cdef || lrf_geometry(g.W, g.H, g.xdec, g.ydec, g.bd, 100, g.tws, g.ths, &lg) != RV_OK) {
+      rv_set_error(RV_EINVAL, "rv_replay_create: RV_REPLAY_LRF needs RV_REPLAY_CDEF and units of one "
+                              "superblock");
       rv_replay_destroy(r);
       return nullptr;
     }
@@ -2600,7 +2637,7 @@ int rv_replay_set_groups(rv_replay *r, int n_groups, const int32_t *rects, int m
   r->my_group = my_group;
   size_t most = 0;
   for (int k = 0; k < n_groups; k++) {
-    XRect xr[6];
+    XRect xr[9];
     int nx;
     const size_t b = (size_t)group_rects(r, k, xr, &nx);
     most = b > most ? b : most;
@@ -2633,11 +2670,11 @@ int rv_replay_import(rv_replay *r) {
   // its own input): nothing to move
   if ((r->n_groups < 2 && !r->comm) || r->last.is_key) return RV_OK;
   const RvSlot &s = r->slots[r->last.display % kSlots];
-  XRect rects[6 * kMaxGroups];
+  XRect rects[9 * kMaxGroups];
   int n = 0;
   for (int k = 0; k < r->n_groups; k++) {
     if (k == r->my_group) continue;
-    XRect xr[6];
+    XRect xr[9];
     int nx;
     group_rects(r, k, xr, &nx);
     for (int p = 0; p < nx; p++) {
@@ -4168,8 +4205,13 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   if (r->n_groups < 2 && !r->comm) {
     RV_R(filter_slot(r, S, cur, lv));
   } else {
-    XRect xr[6];
+    XRect xr[9];
     int nx;
+    if (r->lrf) {  // this group's units travel with its reconstruction
+      LrfGeo lg;
+      RV_R(lrf_geometry(g.W, g.H, g.xdec, g.ydec, g.bd, r->lv[lv].qidx, g.tws, g.ths, &lg));
+      RV_R(lrf_decide_slot(r, S, cur, lv, lg, r->grects + 4 * r->my_group));
+    }
     group_rects(r, r->my_group, xr, &nx);
     RV_R(xcopy(r, S, xr, nx, 0, r->xsend));
     if (r->comm) {

@@ -573,11 +573,12 @@ def test_gpu_replay_importance_window(w, h, bd, refs, tiling, flags, window, rea
 @pytest.mark.gpu
 @pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_DEBLOCK,
                                    RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_SPEED6,
-                                   RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF])
+                                   RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF, _LRF])
 def test_gpu_tile_groups_exchange(flags):
     """Two GPU tile groups in one process, exchanging reconstructions (with
-    deblocking: and block maps) through their device exchange buffers (the
-    RCCL all-gather's layout), reproduce the CPU replay of the whole frame."""
+    deblocking: and block maps; with loop restoration: each group's units)
+    through their device exchange buffers (the RCCL all-gather's layout),
+    reproduce the CPU replay of the whole frame."""
     import ctypes as C
 
     import rav1e_amd as R
@@ -592,7 +593,7 @@ def test_gpu_tile_groups_exchange(flags):
         g.set_groups(rects, k, None)
     c = O.CpuReplay(w, h, tile_size=ts, n_inputs=14, threads=4,
                     deblock=bool(flags & RP.RV_REPLAY_DEBLOCK),
-                    cdef=bool(flags & RP.RV_REPLAY_CDEF),
+                    cdef=bool(flags & RP.RV_REPLAY_CDEF), lrf=bool(flags & RP.RV_REPLAY_LRF),
                     speed=6 if flags & RP.RV_REPLAY_SPEED6 else 10)
     for i in range(14):
         c.set_input(i, RP.synth_frame(w, h, i))
@@ -620,6 +621,10 @@ def test_gpu_tile_groups_exchange(flags):
             for sb in range(gw_ * gh_):
                 np.testing.assert_array_equal(gsb[sb], sw[(y0 + sb // gw_) * sbc + x0 + sb % gw_])
             assert wg[-1] == cw[-1]
+            if flags & RP.RV_REPLAY_LRF and n:  # every group holds every unit after the import
+                nsb = sbc * ((h + 63) // 64)
+                for p in range(3):
+                    np.testing.assert_array_equal(g.lrf_units(p), c.lrf_units(p, nsb), err_msg=f"frame {n} plane {p}")
     for g in gs:
         g.close()
 

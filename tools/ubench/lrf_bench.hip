@@ -83,6 +83,8 @@ int main(int argc, char **argv) {
   a.mi_stride = mi_stride;
   a.g = g;
   a.cdef = 1;
+  a.gx1 = g.sbc;
+  a.gy1 = g.sbr;
   a.dir = dir;
   a.var = var;
   a.dstride = W / 8;
@@ -99,6 +101,9 @@ int main(int argc, char **argv) {
   d.xqd = xqd;
   d.lambda = 300.0;
   d.units = units;
+  d.gx0 = d.gy0 = 0;
+  d.gx1 = g.sbc;
+  d.gy1 = g.sbr;
   const int nt = ((g.sbc + g.tws - 1) / g.tws) * ((g.sbr + g.ths - 1) / g.ths);
   hipEvent_t e0, e1, e2;
   CK(hipEventCreate(&e0));
