@@ -862,7 +862,7 @@ __device__ unsigned long long lrf_dphase[5];
 // count_signed_subexp_with_ref of each (xqd, ref) pair, per radius (bits *
 // 8; uploaded once by lrf_lut_upload)
 __device__ uint8_t g_lrf_subexp[2][128][128];
-constexpr int kDecideAhead = 4;        // superblocks of distortions in flight
+constexpr int kDecideAhead = 8;        // superblocks of distortions in flight
 constexpr int kDecideBuf = 4096;        // superblocks whose picks wait in LDS
 
 __global__ __launch_bounds__(64) void lrf_decide_kernel(LrfDecideArgs a) {
@@ -902,22 +902,20 @@ __global__ __launch_bounds__(64) void lrf_decide_kernel(LrfDecideArgs a) {
 #else
 #define DPHASE(i)
 #endif
-  auto load = [&](int k, int kx, int ky, uint64_t &e, int &x0, int &x1) {  // superblock k = (kx, ky)
-    e = 0;
-    x0 = x1 = 0;
-    if (live && k < n) {
-      const size_t u = (size_t)lp * g.nsb + (t0y + ky) * g.sbc + t0x + kx;
-      e = a.err[u * 17 + 1 + ls];
-      if (!none) {
-        x0 = a.xqd[u * 32 + 2 * ls];
-        x1 = a.xqd[u * 32 + 2 * ls + 1];
-      }
-    }
+  // superblock k = (kx, ky): unconditional loads (indices clamped; the
+  // dead lanes' and None's xqd are never used) kept raw until their step,
+  // so the wait for them is the only one
+  const int lpc = lp < 3 ? lp : 2, lsc = ls > 0 ? ls : 0;
+  auto load = [&](int k, int kx, int ky, uint64_t &e, uint32_t &xq) {
+    if (k >= n) kx = ky = 0;
+    const size_t u = (size_t)lpc * g.nsb + (t0y + ky) * g.sbc + t0x + kx;
+    e = a.err[u * 17 + 1 + ls];
+    xq = *(const uint32_t *)(a.xqd + u * 32 + 4 * (lsc >> 1));  // an aligned word: two pairs
   };
   uint64_t ev[kDecideAhead];
-  int xv0[kDecideAhead], xv1[kDecideAhead];
+  uint32_t xv[kDecideAhead];
 #pragma unroll
-  for (int d = 0; d < kDecideAhead; d++) load(d, d % tsw, d / tsw, ev[d], xv0[d], xv1[d]);
+  for (int d = 0; d < kDecideAhead; d++) load(d, d % tsw, d / tsw, ev[d], xv[d]);
   int sx = 0, sy = 0;                                            // the superblock in the tile
   int lx = kDecideAhead % tsw, ly = kDecideAhead / tsw;          // the next one to load
   for (int k0 = 0; k0 < n; k0 += kDecideAhead) {
@@ -927,7 +925,8 @@ __global__ __launch_bounds__(64) void lrf_decide_kernel(LrfDecideArgs a) {
       if (k >= n) break;
       const int fsx = t0x + sx, fsy = t0y + sy;
       DPHASE(0);
-      const int x0 = xv0[d], x1 = xv1[d];
+      const uint32_t xw = (lsc & 1) ? xv[d] >> 16 : xv[d];
+      const int x0 = none ? 0 : (int)(int8_t)(xw & 0xff), x1 = none ? 0 : (int)(int8_t)((xw >> 8) & 0xff);
       const int r0 = lp == 0 ? st.ref[0][0] : lp == 1 ? st.ref[1][0] : st.ref[2][0];
       const int r1 = lp == 0 ? st.ref[0][1] : lp == 1 ? st.ref[1][1] : st.ref[2][1];
       // count_lrf_switchable (lrf_rate_at) from the tables
@@ -966,7 +965,7 @@ __global__ __launch_bounds__(64) void lrf_decide_kernel(LrfDecideArgs a) {
         pick[p][2] = has && best >= 0 ? q1 : 0;
       }
       DPHASE(2);
-      load(k + kDecideAhead, lx, ly, ev[d], xv0[d], xv1[d]);  // this slot's next superblock
+      load(k + kDecideAhead, lx, ly, ev[d], xv[d]);  // this slot's next superblock
       if (++lx == tsw) {
         lx = 0;
         ly++;
