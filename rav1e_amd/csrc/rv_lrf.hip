@@ -23,6 +23,7 @@
 // All of it is integer work but sgrproj_solve's tail, whose f64 operations
 // run in the reference's order (IEEE division, no contraction).
 #include <stddef.h>
+#include <stdlib.h>
 #include <mutex>
 #include <type_traits>
 #include <string.h>
@@ -197,9 +198,17 @@ __device__ __forceinline__ void sgr_row(int r, int r1rows, int tx, int &to, int 
   }
 }
 
+// A table entry: (a, b) side by side, or packed in one word ((a << 20) | b:
+// a <= 256, b < 2^20 since it is a u32 >> 12) where LDS is short.
+constexpr uint32_t kBMask = (1u << 20) - 1;
+__device__ __forceinline__ uint2 tab_get(uint2 v) { return v; }
+__device__ __forceinline__ uint2 tab_get(uint32_t v) { return make_uint2(v >> 20, v & kBMask); }
+__device__ __forceinline__ void tab_put(uint2 &d, uint2 v) { d = v; }
+__device__ __forceinline__ void tab_put(uint32_t &d, uint2 v) { d = (v.x << 20) | v.y; }
+
 // the (a, b) tables of set s straight from the integral images (every lane)
-template <int IS, int IR, int AS, int A1R>
-__device__ __forceinline__ void sgr_tables(const uint32_t *img, uint2 *tab, const uint16_t *xz,
+template <int IS, int IR, int AS, int A1R, typename T>
+__device__ __forceinline__ void sgr_tables(const uint32_t *img, T *tab, const uint16_t *xz,
                                            const SgrLane &ln, int set, int h, int bdm8) {
   const uint32_t s2 = kSgrS[set][0], s1 = kSgrS[set][1];
   const int r1rows = s1 ? h + 2 : 0, r2rows = s2 ? (h + 1) / 2 + 1 : 0;  // r = 2: rows 0, 2, .., <= h + 1
@@ -207,8 +216,8 @@ __device__ __forceinline__ void sgr_tables(const uint32_t *img, uint2 *tab, cons
     int to, o, d;
     sgr_row<IS, AS, A1R>(r, r1rows, ln.tx, to, o, d);
     const bool one = r < r1rows;
-    tab[to] = sgr_ab(sgr_box(isq(img, IS, IR * IS + o, d), isq(img, IS, o, d), one ? 9 : 25, bdm8),
-                     one ? s1 : s2, one ? 455 : 164, xz);
+    tab_put(tab[to], sgr_ab(sgr_box(isq(img, IS, IR * IS + o, d), isq(img, IS, o, d), one ? 9 : 25, bdm8),
+                            one ? s1 : s2, one ? 455 : 164, xz));
   }
 }
 // the boxes' (p, sum) of both radii, once per region (every lane) ...
@@ -236,8 +245,9 @@ __device__ __forceinline__ void sgr_tables_ps(const uint2 *ps, uint2 *tab, const
 }
 
 // 5 * (t[x] + t[x + 2]) + 6 * t[x + 1], a and b
-__device__ __forceinline__ void sgr_row3(const uint2 *t, int x, uint32_t &a, uint32_t &b) {
-  const uint2 v0 = t[x], v1 = t[x + 1], v2 = t[x + 2];
+template <typename T>
+__device__ __forceinline__ void sgr_row3(const T *t, int x, uint32_t &a, uint32_t &b) {
+  const uint2 v0 = tab_get(t[x]), v1 = tab_get(t[x + 1]), v2 = tab_get(t[x + 2]);
   a = 5 * (v0.x + v2.x) + 6 * v1.x;
   b = 5 * (v0.y + v2.y) + 6 * v1.y;
 }
@@ -276,8 +286,8 @@ __device__ __forceinline__ void sgr_f(const uint2 *tab, int set, int x, int y, u
 }
 // sgr_f of the four pixels (x, y0 .. y0 + 3) of a column strip (y0 a
 // multiple of 4): the table rows they share are read once
-template <int AS, int A1R>
-__device__ __forceinline__ void sgr_f4(const uint2 *tab, int set, int x, int y0, const uint32_t px[4],
+template <int AS, int A1R, typename T>
+__device__ __forceinline__ void sgr_f4(const T *tab, int set, int x, int y0, const uint32_t px[4],
                                        uint32_t f2[4], uint32_t f1[4]) {
   const uint32_t s2 = kSgrS[set][0], s1 = kSgrS[set][1];
   constexpr int sh = 5 + kSgrBits - kRstBits, sho = 4 + kSgrBits - kRstBits;
@@ -298,8 +308,8 @@ __device__ __forceinline__ void sgr_f4(const uint2 *tab, int set, int x, int y0,
     uint32_t ca[6], cb[6], ma[6], mb[6];
 #pragma unroll
     for (int j = 0; j < 6; j++) {
-      const uint2 *T = tab + (y0 + j) * AS + x;
-      const uint2 v0 = T[0], v1 = T[1], v2 = T[2];
+      const T *t = tab + (y0 + j) * AS + x;
+      const uint2 v0 = tab_get(t[0]), v1 = tab_get(t[1]), v2 = tab_get(t[2]);
       ca[j] = v0.x + v2.x;
       cb[j] = v0.y + v2.y;
       ma[j] = v1.x;
@@ -829,6 +839,295 @@ __global__ __launch_bounds__(BW * BH / 4) void lrf_rdo_kernel(LrfRdoArgs a) {
   if (fin) err_finish(16);
 }
 
+// 64 x 64 units (luma, 4:4:4 chroma) in 512-lane workgroups with ~71 KB of
+// LDS, two per CU: a lane owns two column strips (rows y0 .. y0 + 3 and
+// y0 + 32 .. y0 + 35), the source pixels it needs sit in its registers, and
+// each set's (a, b) tables are built from the integral images (which stay)
+// into packed words. Otherwise as lrf_rdo_kernel.
+struct RdoWideLds {
+  using L = SgrL64;
+  uint32_t img[2 * L::IR * L::IS];  // ii, sq
+  union {
+    uint32_t tab[L::TAB];  // each set's (a, b), packed
+    struct {
+      uint16_t lin[64 * 64];  // the unit's input (lrf_input)
+      uint16_t pad[68 * 68];  // the padded CDEF input
+    } in;
+  } u;
+  uint16_t xz[256];
+  int16_t coffs[48];
+  uint8_t bdir[64], bskip[64];
+  int32_t bvar[64];
+  int64_t red5[5][8];
+  uint3 hm[16 * 8];  // each half block's (sd, sd2, ssd) / (sse), [strip][block column]
+  int2 bsh[16 * 8];  // luma: each half block's source (sum, sum of squares)
+  int8_t sxqd[2];
+};
+
+template <typename Px>
+__global__ __launch_bounds__(512, 4) void lrf_rdo_wide_kernel(LrfRdoArgs a) {
+  using SL = SgrL64;
+  constexpr int BW = 64, BH = 64, NT = 512, NW = 8, AS = SL::AS, A1R = SL::A1R;
+  __shared__ RdoWideLds S;
+  const LrfGeo &g = a.g;
+  const int p = a.p0 + blockIdx.y, sb = blockIdx.x, tid = threadIdx.x;
+  const int sbc = g.sbc, fsx = sb % sbc, fsy = sb / sbc;
+  if (fsx >= g.cols[p] || fsy >= g.rows[p]) return;  // no unit (uniform)
+  if (fsx < a.gx0 || fsx >= a.gx1 || fsy < a.gy0 || fsy >= a.gy1) return;  // another group's
+  const int t0x = fsx - fsx % g.tws, t0y = fsy - fsy % g.ths, sx = fsx - t0x, sy = fsy - t0y;
+  const int xd = p ? g.xdec : 0, yd = p ? g.ydec : 0;
+  const int tw_px = min(g.tws * 64, g.W - t0x * 64), th_px = min(g.ths * 64, g.H - t0y * 64);
+  const int pw_t = (tw_px + xd) >> xd, ph_t = (th_px + yd) >> yd;
+  const int mi_cols = tw_px >> 2, mi_rows = th_px >> 2;
+  const int ox = (sx * 64) >> xd, oy = (sy * 64) >> yd, fx0 = (t0x * 64) >> xd, fy0 = (t0y * 64) >> yd;
+  const int bd = g.bd, cs = bd - 8, mx = (1 << bd) - 1;
+  const rv_plane &rec = a.rec[p], &src = a.src[p];
+  auto recpx = [&](int x, int y) __attribute__((always_inline)) -> int {  // frame plane coordinates
+    return (int)((const Px *)rec.data)[(int64_t)(rec.yorigin + y) * rec.stride + rec.xorigin + x];
+  };
+  sgr_init_xz(S.xz);
+  cdef_offsets(S.coffs, BW + 4);
+  // 1. the padded copy and the unit's input
+  for (int i = tid; i < (BH + 4) * (BW + 4); i += NT) {
+    const int y = i / (BW + 4) - 2, x = i % (BW + 4) - 2, tx = ox + x, ty = oy + y;
+    int v = kVeryLarge;
+    if (tx >= 0 && tx < pw_t && ty >= 0 && ty < ph_t) {
+      const int csx = (tx << xd) >> 6, csy = (ty << yd) >> 6;
+      v = (csy < sy || (csy == sy && csx <= sx)) ? recpx(fx0 + tx, fy0 + ty) : 128;
+    }
+    S.u.in.pad[i] = (uint16_t)v;
+  }
+  const int vw = min(BW, pw_t - ox), vh = min(BH, ph_t - oy);
+  for (int i = tid; i < BW * BH; i += NT) {
+    const int y = i >> 6, x = i & 63;
+    S.u.in.lin[i] = (uint16_t)recpx(fx0 + ox + min(x, vw - 1), fy0 + oy + min(y, vh - 1));
+  }
+  // the unit (size clipped at the tile-relative offset, the reference's
+  // quirk) and the lane's source pixels: sgrproj_solve's at the unit's
+  // tile-relative offset of the whole frame (src/rdo.rs:2028-2033), the
+  // distortion's over the 8x8 blocks inside the tile (two u16 per word)
+  const int pw = p ? (g.W + xd) >> xd : g.W, ph = p ? (g.H + yd) >> yd : g.H;
+  const int uw = min(BW, pw - ox), uh = min(BH, ph - oy);
+  const int elx = (min(8, max(0, (mi_cols - sx * 16 + 1) / 2)) * 8) >> xd;
+  const int ely = (min(8, max(0, (mi_rows - sy * 16 + 1) / 2)) * 8) >> yd;
+  const int qx = tid & 63, qy0 = (tid >> 6) * 4;  // strips (qx, qy0 + 32 j + k)
+  uint32_t ssw[4], esw[4];
+  {
+    const int64_t ss_ = src.stride;
+    const Px *const sp = (const Px *)src.data;
+    const Px *const ssolve = sp + (int64_t)(src.yorigin + oy) * ss_ + src.xorigin + ox;
+    const Px *const sdist = sp + (int64_t)(src.yorigin + fy0 + oy) * ss_ + src.xorigin + fx0 + ox;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      uint32_t sv[2], ev[2];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int y = qy0 + 32 * ((j + h) >> 2) + ((j + h) & 3);
+        sv[h] = (qx < uw && y < uh) ? (uint32_t)ssolve[(int64_t)y * ss_ + qx] : 0;
+        ev[h] = (qx < elx && y < ely) ? (uint32_t)sdist[(int64_t)y * ss_ + qx] : 0;
+      }
+      ssw[j >> 1] = sv[0] | sv[1] << 16;
+      esw[j >> 1] = ev[0] | ev[1] << 16;
+    }
+  }
+  auto srcv = [&](const uint32_t *w, int i) __attribute__((always_inline)) -> int32_t {  // pixel i (0 .. 7) of the lane's strips
+    return (int32_t)((w[i >> 1] >> (16 * (i & 1))) & 0xffff);
+  };
+  // 2. CDEF index 0 on the 8x8 blocks inside the tile (cdef_filter_superblock)
+  if (a.cdef) {
+    if (tid < 64) {
+      const int bx = tid & 7, by = tid >> 3, gx = sx * 16 + 2 * bx, gy = sy * 16 + 2 * by;
+      uint8_t sk = 2, dir = 0;
+      int32_t var = 0;
+      if (gx < mi_cols && gy < mi_rows) {
+        const uint8_t *k = a.skip + (int64_t)(t0y * 16 + gy) * a.mi_stride + t0x * 16 + gx;
+        sk = k[0] & k[1] & k[a.mi_stride] & k[a.mi_stride + 1];
+        if (!sk) {
+          const int64_t o = (int64_t)(fsy * 8 + by) * a.dstride + fsx * 8 + bx;
+          dir = a.dir[o];
+          var = a.var[o];
+        }
+      }
+      S.bskip[tid] = sk;
+      S.bdir[tid] = dir;
+      S.bvar[tid] = var;
+    }
+    __syncthreads();
+    const int bxs = 8 >> xd, bys = 8 >> yd;
+    for (int i = tid; i < BW * BH; i += NT) {
+      const int y = i >> 6, x = i & 63, blk = (y / bys) * 8 + x / bxs;
+      if (S.bskip[blk]) continue;  // skip: the copy (equal to lin); 2: outside the tile
+      int pri, sec, dmp = a.damping + cs, d;
+      if (p == 0) {
+        pri = cdef_adjust(a.pri_y << cs, S.bvar[blk]);
+        sec = a.sec_y << cs;
+        d = a.pri_y ? S.bdir[blk] : 0;
+      } else {
+        pri = a.pri_uv << cs;
+        sec = a.sec_uv << cs;
+        dmp -= 1;
+        d = a.pri_uv ? S.bdir[blk] : 0;
+      }
+      S.u.in.lin[i] = (uint16_t)cdef_px(S.u.in.pad + (y + 2) * (BW + 4) + x + 2, S.coffs + 6 * d, pri, sec, dmp, cs);
+    }
+  }
+  __syncthreads();
+  // 3. the unit's integral image: lrf_input alone, replicated
+  sgr_integral<SL::IS, SL::IR>(S.img, uw, uh, [&](int r, int c) -> uint32_t {
+    return S.u.in.lin[iclamp(r - 4, 0, uh - 1) * BW + iclamp(c - 4, 0, uw - 1)];
+  });
+  uint32_t pxr[8], lnr[8];  // the unit's pixels (0 outside it), lrf_input's
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int y = qy0 + 32 * (i >> 2) + (i & 3);
+    lnr[i] = S.u.in.lin[y * BW + qx];
+    pxr[i] = (qx < uw && y < uh) ? lnr[i] : 0;
+  }
+  // 4. the distortion (as lrf_rdo_kernel): half blocks over 8 lanes, the
+  // last wave joins them
+  const int wave = tid >> 6;
+  const bool fin = wave == NW - 1;
+  const int fb = tid & 63, fgx = sx * 16 + 2 * (fb & 7), fgy = sy * 16 + 2 * (fb >> 3);
+  const bool fblk = fin && fgx < mi_cols && fgy < mi_rows;
+  const double fbias = fblk ? lrf_bias(a.imp, a.w_imp, a.w_in_b, a.h_in_b, t0x * 16 + fgx, t0y * 16 + fgy) : 0.0;
+  if (p == 0) {  // the luma half blocks' source moments (every option reuses them)
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      int32_t ss = 0;
+      uint32_t ss2 = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int32_t v = srcv(esw, 4 * j + k);
+        ss += v;
+        ss2 += (uint32_t)(v * v);
+      }
+      ss = dpp_sum8(ss);
+      ss2 = dpp_sum8(ss2);
+      if ((qx & 7) == 0) S.bsh[((qy0 >> 2) + 8 * j) * 8 + (qx >> 3)] = make_int2(ss, (int32_t)ss2);
+    }
+  }
+  auto err_part = [&](const int32_t d[8]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const int slot = ((qy0 >> 2) + 8 * j) * 8 + (qx >> 3);
+      if (p == 0) {
+        int32_t sd = 0;
+        uint32_t sd2 = 0, ssd = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int32_t dv = d[4 * j + k], sv = srcv(esw, 4 * j + k);
+          sd += dv;
+          sd2 += (uint32_t)(dv * dv);
+          ssd += (uint32_t)(sv * dv);
+        }
+        sd = dpp_sum8(sd);
+        sd2 = dpp_sum8(sd2);
+        ssd = dpp_sum8(ssd);
+        if ((qx & 7) == 0) S.hm[slot] = make_uint3((uint32_t)sd, sd2, ssd);
+      } else {  // 4:4:4 chroma: one 8x8 part per block
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int c = (int)(int16_t)srcv(esw, 4 * j + k) - (int)(int16_t)d[4 * j + k];
+          v += (uint32_t)(c * c);
+        }
+        v = dpp_sum8(v);
+        if ((qx & 7) == 0) S.hm[slot] = make_uint3(v, 0, 0);
+      }
+    }
+  };
+  uint64_t *eo = a.err + ((size_t)p * g.nsb + sb) * 17;
+  int8_t *xo = a.xqd + ((size_t)p * g.nsb + sb) * 32;
+  auto err_finish = [&](int o) __attribute__((always_inline)) {
+    uint64_t e = 0;
+    if (fblk) {
+      const int h0 = (2 * (fb >> 3)) * 8 + (fb & 7), h1 = h0 + 8;
+      const uint3 u0 = S.hm[h0], u1 = S.hm[h1];
+      if (p == 0) {
+        const int2 s0 = S.bsh[h0], s1 = S.bsh[h1];
+        e = biased(cdef_dist(s0.x + s1.x, (int32_t)(u0.x + u1.x), (uint32_t)s0.y + (uint32_t)s1.y, u0.y + u1.y,
+                             u0.z + u1.z, bd),
+                   fbias);
+      } else {
+        e = biased((uint64_t)u0.x + u1.x, fbias);
+      }
+    }
+    e = dpp_sum64(e);
+    if (fb == 0) eo[o] = (uint64_t)((double)e * a.ds[p]);
+  };
+  {
+    int32_t d[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) d[i] = (int32_t)lnr[i];  // None: the input as it is
+    err_part(d);
+  }
+  // 5. the 16 sets (wave 0 solves set s while the others build s + 1's tables)
+  using Acc = typename std::conditional<sizeof(Px) == 1, int32_t, int64_t>::type;  // 8-bit: 8 products fit
+  const SgrLane ln = sgr_lane(uw, tid, NT), ln_rest = sgr_lane(uw, tid - 64, NT - 64);
+  __syncthreads();  // lin is read (the tables take its place); the None parts
+  if (fin) err_finish(0);
+  sgr_tables<SL::IS, SL::IR, AS, A1R>(S.img, S.u.tab, S.xz, ln, 0, uh, cs);
+  for (int set = 0; set < 16; set++) {
+    __syncthreads();
+    if (set > 0 && fin) err_finish(set);  // set - 1's, at eo[set]
+    uint32_t f2r[8], f1r[8];
+    Acc H00 = 0, H11 = 0, H01 = 0, C0 = 0, C1 = 0;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      sgr_f4<AS, A1R>(S.u.tab, set, qx, qy0 + 32 * j, pxr + 4 * j, f2r + 4 * j, f1r + 4 * j);
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (qx < uw && qy0 + 32 * j + k < uh) {
+          const int i = 4 * j + k;
+          const Acc u = (Acc)pxr[i] << kRstBits;
+          const Acc sv = ((Acc)srcv(ssw, i) << kRstBits) - u;
+          const Acc e2 = (Acc)(int32_t)f2r[i] - u, e1 = (Acc)(int32_t)f1r[i] - u;
+          H00 += e2 * e2;
+          H11 += e1 * e1;
+          H01 += e1 * e2;
+          C0 += e2 * sv;
+          C1 += e1 * sv;
+        }
+    }
+    {
+      const int64_t v[5] = {H00, H11, H01, C0, C1};
+#pragma unroll
+      for (int q = 0; q < 5; q++) {
+        const int64_t t = (int64_t)dpp_sum64((uint64_t)v[q]);
+        if ((tid & 63) == 0) S.red5[q][wave] = t;
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {
+      int64_t t = 0;
+      if (tid < 5)
+        for (int w = 0; w < NW; w++) t += S.red5[tid][w];
+      const int64_t h00 = readlane64((uint64_t)t, 0), h11 = readlane64((uint64_t)t, 1),
+                    h01 = readlane64((uint64_t)t, 2), c0 = readlane64((uint64_t)t, 3),
+                    c1 = readlane64((uint64_t)t, 4);
+      int8_t q[2];
+      lrf_solve_finish_wave(set, uw, uh, h00, h01, h11, c0, c1, q);
+      if (tid == 0) {
+        S.sxqd[0] = q[0];
+        S.sxqd[1] = q[1];
+        xo[2 * set] = q[0];
+        xo[2 * set + 1] = q[1];
+      }
+    } else if (set < 15) {
+      sgr_tables<SL::IS, SL::IR, AS, A1R>(S.img, S.u.tab, S.xz, ln_rest, set + 1, uh, cs);
+    }
+    __syncthreads();
+    const int w0 = S.sxqd[0], w1 = S.sxqd[1];
+    int32_t d[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++)  // 128 outside the unit: lrf_output's fill (never inside the frame)
+      d[i] = (qx < uw && qy0 + 32 * (i >> 2) + (i & 3) < uh) ? sgr_out(f2r[i], f1r[i], pxr[i], w0, w1, mx) : 128;
+    err_part(d);
+  }
+  __syncthreads();
+  if (fin) err_finish(16);
+}
+
 // ---- the sequential decisions (count_lrf_switchable, write_lrf) -----------------
 struct LrfDecideArgs {
   LrfGeo g;
@@ -1176,10 +1475,22 @@ int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *
   const bool c420 = g.xdec && g.ydec;
   a.p0 = 0;
   const dim3 grid64((unsigned)g.nsb, c420 ? 1 : 3), grid32((unsigned)g.nsb, 2);
-  if (rec[0].hbd)
-    lrf_rdo_kernel<uint16_t, 64, 64><<<grid64, 1024, 0, s>>>(a);
-  else
-    lrf_rdo_kernel<uint8_t, 64, 64><<<grid64, 1024, 0, s>>>(a);
+  // RAV1E_LRF_WIDE=0 (A/B): the 1024-lane, 135 KB workgroup for 64 x 64 units
+  static const bool wide = [] {
+    const char *e = getenv("RAV1E_LRF_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  if (wide) {
+    if (rec[0].hbd)
+      lrf_rdo_wide_kernel<uint16_t><<<grid64, 512, 0, s>>>(a);
+    else
+      lrf_rdo_wide_kernel<uint8_t><<<grid64, 512, 0, s>>>(a);
+  } else {
+    if (rec[0].hbd)
+      lrf_rdo_kernel<uint16_t, 64, 64><<<grid64, 1024, 0, s>>>(a);
+    else
+      lrf_rdo_kernel<uint8_t, 64, 64><<<grid64, 1024, 0, s>>>(a);
+  }
   RV_HIP_CHECK_LAUNCH();
   if (c420) {
     a.p0 = 1;

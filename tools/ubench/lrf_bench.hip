@@ -113,7 +113,10 @@ int main(int argc, char **argv) {
   for (int r = 0; r < reps; r++) {
     CK(hipEventRecord(e0, 0));
     a.p0 = 0;
-    lrf_rdo_kernel<uint8_t, 64, 64><<<dim3(g.nsb, 1), 1024>>>(a);
+    if (r & 1)  // odd reps: the 1024-lane luma kernel (RAV1E_LRF_WIDE=0)
+      lrf_rdo_kernel<uint8_t, 64, 64><<<dim3(g.nsb, 1), 1024>>>(a);
+    else
+      lrf_rdo_wide_kernel<uint8_t><<<dim3(g.nsb, 1), 512>>>(a);
     a.p0 = 1;
     lrf_rdo_kernel<uint8_t, 32, 32><<<dim3(g.nsb, 2), 256>>>(a);
     CK(hipEventRecord(e1, 0));
@@ -123,7 +126,8 @@ int main(int argc, char **argv) {
     float t1, t2;
     CK(hipEventElapsedTime(&t1, e0, e1));
     CK(hipEventElapsedTime(&t2, e1, e2));
-    printf("rep %d: rdo %.3f ms (%d x 3 workgroups), decide %.3f ms (%d tiles)\n", r, t1, g.nsb, t2, nt);
+    printf("rep %d (%s luma): rdo %.3f ms (%d x 3 workgroups), decide %.3f ms (%d tiles)\n", r,
+           r & 1 ? "1024-lane" : "512-lane", t1, g.nsb, t2, nt);
   }
 #ifdef LRF_PHASES
   // one workgroup alone: its phases in wall_clock64 ticks (100 MHz)
