@@ -230,7 +230,8 @@ int lrf_geometry(int width, int height, int xdec, int ydec, int bit_depth, int b
 int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *skip, int mi_stride,
                    const float *imp, int w_imp, int w_in_b, int h_in_b, const LrfGeo &g, int cdef,
                    const uint8_t *dir, const int32_t *var, const uint8_t cdef_str[2], const double ds[3],
-                   uint64_t *err, int8_t *xqd, double lambda, int8_t *units, const int32_t *rect,
-                   hipStream_t s);
+                   uint64_t *err, int8_t *xqd, const int32_t *rect, hipStream_t s);
+int lrf_decide_launch(const LrfGeo &g, const uint64_t *err, const int8_t *xqd, double lambda, int8_t *units,
+                      const int32_t *rect, hipStream_t s);
 int lrf_filter_launch(const rv_plane cd[3], const rv_plane db[3], const rv_plane out[3], const LrfGeo &g,
                       const int8_t *units, int enable_cdef, hipStream_t s);

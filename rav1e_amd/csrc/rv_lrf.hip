@@ -1438,8 +1438,7 @@ static int lrf_lut_upload() {
 int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *skip, int mi_stride,
                    const float *imp, int w_imp, int w_in_b, int h_in_b, const LrfGeo &g, int cdef,
                    const uint8_t *dir, const int32_t *var, const uint8_t cdef_str[2], const double ds[3],
-                   uint64_t *err, int8_t *xqd, double lambda, int8_t *units, const int32_t *rect,
-                   hipStream_t s) {
+                   uint64_t *err, int8_t *xqd, const int32_t *rect, hipStream_t s) {
   if (g.xdec != g.ydec) return rv_set_error(RV_EINVAL, "loop restoration: 4:2:0, 4:4:4 (4:2:2 has none)");
   if (lrf_lut_upload() != RV_OK) return RV_EHIP;
   LrfRdoArgs a;
@@ -1500,16 +1499,23 @@ int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *
       lrf_rdo_kernel<uint8_t, 32, 32><<<grid32, 256, 0, s>>>(a);
     RV_HIP_CHECK_LAUNCH();
   }
+  return RV_OK;
+}
+
+// the sequential decisions over the units lrf_rdo_launch priced (rect: the
+// same superblocks)
+int lrf_decide_launch(const LrfGeo &g, const uint64_t *err, const int8_t *xqd, double lambda, int8_t *units,
+                      const int32_t *rect, hipStream_t s) {
   LrfDecideArgs d;
   d.g = g;
   d.err = err;
   d.xqd = xqd;
   d.lambda = lambda;
   d.units = units;
-  d.gx0 = a.gx0;
-  d.gy0 = a.gy0;
-  d.gx1 = a.gx1;
-  d.gy1 = a.gy1;
+  d.gx0 = rect ? rect[0] : 0;
+  d.gy0 = rect ? rect[1] : 0;
+  d.gx1 = rect ? rect[0] + rect[2] : g.sbc;
+  d.gy1 = rect ? rect[1] + rect[3] : g.sbr;
   const int nt = ((g.sbc + g.tws - 1) / g.tws) * ((g.sbr + g.ths - 1) / g.ths);
   lrf_decide_kernel<<<nt, 64, 0, s>>>(d);
   RV_HIP_CHECK_LAUNCH();

@@ -1164,6 +1164,10 @@ struct rv_replay {
   bool lrf = false;
   uint64_t *lrf_err = nullptr;
   int8_t *lrf_xqd = nullptr, *lrf_units = nullptr;
+  // the decision's side stream (RAV1E_LRF_SIDE=1; default: the replay stream)
+  hipStream_t lrf_side = nullptr;
+  hipEvent_t ev_lrf0 = nullptr, ev_lrf1 = nullptr;
+  bool lrf_pending = false;
   RvInput lrf_out;
   RvInput cdef_pre;                 // the deblocked, pre-CDEF frame (the padded copy's source)
   uint8_t *cdef_dir = nullptr, *cdef_idx = nullptr;  // per 8x8 block; per 64x64 (all 0)
@@ -1761,6 +1765,10 @@ int cdef_pad_slot(rv_replay *r, const RvSlot &s, int lv, const LrfGeo *lg) {
   // lrf_filter_frame: the CDEF output restored, the deblocked slot for the
   // stripes' edges (pre_cdef_frame, src/encoder.rs:2795-2806)
   const rv_plane lo[3] = {r->lrf_out.y, r->lrf_out.u, r->lrf_out.v};
+  if (r->lrf_pending) {  // the units of the side stream's decision
+    RV_H(hipStreamWaitEvent(r->stream, r->ev_lrf1, 0));
+    r->lrf_pending = false;
+  }
   RV_R(lrf_filter_launch(out, rec, lo, *lg, r->lrf_units, 1, r->stream));
   return rv_frame_pad_dev(rec, lo, r->stream);
 }
@@ -1777,9 +1785,19 @@ static int lrf_decide_slot(rv_replay *r, const RvSlot &s, const RvInput &in, int
   if (r->cdef)
     RV_R(rv_cdef_find_dirs(&rec[0], g.W, g.H, r->mi_skip, r->mi_stride, r->cdef_dir, r->cdef_var, g.bd,
                            r->stream));
-  return lrf_rdo_launch(rec, src, r->mi_skip, r->mi_stride, r->imp_last, g.w_imp, g.w_in_b, g.h_in_b, lg,
-                        r->cdef, r->cdef_dir, r->cdef_var, r->cdef_str[lv], r->lv[lv].ds, r->lrf_err,
-                        r->lrf_xqd, r->lv[lv].lambda, r->lrf_units, rect, r->stream);
+  RV_R(lrf_rdo_launch(rec, src, r->mi_skip, r->mi_stride, r->imp_last, g.w_imp, g.w_in_b, g.h_in_b, lg,
+                      r->cdef, r->cdef_dir, r->cdef_var, r->cdef_str[lv], r->lv[lv].ds, r->lrf_err,
+                      r->lrf_xqd, rect, r->stream));
+  if (rect || !r->lrf_side)  // a group's units are packed right after: no overlap
+    return lrf_decide_launch(lg, r->lrf_err, r->lrf_xqd, r->lv[lv].lambda, r->lrf_units, rect, r->stream);
+  // the sequential decision (a few waves, latency only) on the side stream,
+  // beside the deblocking and CDEF; lrf_filter_launch waits for it
+  RV_H(hipEventRecord(r->ev_lrf0, r->stream));
+  RV_H(hipStreamWaitEvent(r->lrf_side, r->ev_lrf0, 0));
+  RV_R(lrf_decide_launch(lg, r->lrf_err, r->lrf_xqd, r->lv[lv].lambda, r->lrf_units, rect, r->lrf_side));
+  RV_H(hipEventRecord(r->ev_lrf1, r->lrf_side));
+  r->lrf_pending = true;
+  return RV_OK;
 }
 
 // several tile groups (or a one-rank all-gather): each rank decides its own
@@ -2030,6 +2048,9 @@ void rv_replay_destroy(rv_replay *r) {
   for (hipEvent_t ev : {r->ev_rfork, r->ev_rlists, r->ev_rjoin})
     if (ev) (void)hipEventDestroy(ev);
   if (r->hp) (void)hipStreamSynchronize(r->hp), (void)hipStreamDestroy(r->hp);
+  if (r->lrf_side) (void)hipStreamSynchronize(r->lrf_side), (void)hipStreamDestroy(r->lrf_side);
+  for (hipEvent_t ev : {r->ev_lrf0, r->ev_lrf1})
+    if (ev) (void)hipEventDestroy(ev);
   if (r->ev_hp0) (void)hipEventDestroy(r->ev_hp0);
   if (r->ev_hp1) (void)hipEventDestroy(r->ev_hp1);
   for (hipEvent_t ev : {r->ev_efork, r->ev_l1me, r->ev_epart})
@@ -2354,6 +2375,14 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     r->lrf_xqd = (int8_t *)dalloc(r, (size_t)3 * lg.nsb * 32);
     r->lrf_units = (int8_t *)dalloc(r, (size_t)3 * lg.nsb * 3);
     ok = ok && r->lrf_err && r->lrf_xqd && r->lrf_units && alloc_input(r, r->lrf_out, false);
+    // RAV1E_LRF_SIDE=1: the decision on a side stream (2160p A/B, r05an:
+    // 136-142 vs 152-154 fps without -- one more stream per instance than
+    // the hardware queues serve well; off)
+    const char *se = getenv("RAV1E_LRF_SIDE");
+    if (se && se[0] == '1')
+      ok = ok && hipStreamCreateWithFlags(&r->lrf_side, hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev_lrf0, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&r->ev_lrf1, hipEventDisableTiming) == hipSuccess;
   }
   r->entropy = (cfg->flags & RV_REPLAY_ENTROPY) != 0;
   if (r->entropy && g.xdec != g.ydec) {
