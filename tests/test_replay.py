@@ -846,7 +846,7 @@ def test_gpu_paired_replay_matches_cpu(flags, window, ready, twin):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF | RP.RV_REPLAY_SPEED6])
+@pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_DEBLOCK | RP.RV_REPLAY_CDEF | RP.RV_REPLAY_SPEED6, _LRF])
 def test_gpu_replay_one_rank_rccl_exchange(flags):
     """The RCCL branch of the tile-group exchange (rv_replay.hip: pack,
     ncclAllGather on the replay stream, import, loop filters, pad) with a
@@ -877,6 +877,9 @@ def test_gpu_replay_one_rank_rccl_exchange(flags):
             assert ia == ib
             np.testing.assert_array_equal(a.results(), b.results())
             np.testing.assert_array_equal(a.get_recon(ia["display"]), b.get_recon(ib["display"]))
+            if flags & RP.RV_REPLAY_LRF and n:  # the units came through the all-gather
+                for p in range(3):
+                    np.testing.assert_array_equal(a.lrf_units(p), b.lrf_units(p))
     finally:
         a.close()
         b.close()
