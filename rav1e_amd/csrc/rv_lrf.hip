@@ -1249,19 +1249,33 @@ __global__ __launch_bounds__(64) void lrf_decide_kernel(LrfDecideArgs a) {
       dpp_min_step<0x4E>(bk, bs);
       dpp_min_step<0x141>(bk, bs);
       dpp_min_step<0x140>(bk, bs);
+      // lanes 0 .. 2, plane p = lane: its best set (lane 16 p) against its
+      // None (lane 48 + p), its xqd, packed; then uniform by lane reads
+      int packed;
+      {
+        const int pl = lane < 3 ? lane : 0;
+        auto shfl64 = [](uint64_t v, int l) {
+          return (uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64) << 32 |
+                 (uint32_t)__shfl((int)(uint32_t)v, l, 64);
+        };
+        const uint64_t sk = shfl64(bk, 16 * pl), nk = shfl64(key, 48 + pl);
+        const int sbest = __shfl(bs, 16 * pl, 64);
+        const int best = nk <= sk ? -1 : sbest;
+        const int src = 16 * pl + (best < 0 ? 0 : best);
+        const int q0 = __shfl(x0, src, 64), q1 = __shfl(x1, src, 64);
+        // a stretched superblock has no unit of its own
+        const int cols = pl == 0 ? g.cols[0] : pl == 1 ? g.cols[1] : g.cols[2];
+        const int rows = pl == 0 ? g.rows[0] : pl == 1 ? g.rows[1] : g.rows[2];
+        const bool has = fsx < cols && fsy < rows;
+        packed = has ? (best & 0xff) | (best >= 0 ? (q0 & 0xff) << 8 | (q1 & 0xff) << 16 : 0) : 0xfe;
+      }
       int pick[3][3];
 #pragma unroll
-      for (int p = 0; p < 3; p++) {  // uniform from here: lane reads
-        const uint64_t sk = readlane64(bk, 16 * p), nk = readlane64(key, 48 + p);
-        const int s = __builtin_amdgcn_readlane(bs, 16 * p);
-        const int best = nk <= sk ? -1 : s;
-        const int src = 16 * p + (best < 0 ? 0 : best);
-        const int q0 = __builtin_amdgcn_readlane(x0, src), q1 = __builtin_amdgcn_readlane(x1, src);
-        // a stretched superblock has no unit of its own
-        const bool has = fsx < g.cols[p] && fsy < g.rows[p];
-        pick[p][0] = has ? best : -2;
-        pick[p][1] = has && best >= 0 ? q0 : 0;
-        pick[p][2] = has && best >= 0 ? q1 : 0;
+      for (int p = 0; p < 3; p++) {
+        const int v = __builtin_amdgcn_readlane(packed, p);
+        pick[p][0] = (int8_t)(v & 0xff);
+        pick[p][1] = (int8_t)((v >> 8) & 0xff);
+        pick[p][2] = (int8_t)((v >> 16) & 0xff);
       }
       DPHASE(2);
       load(k + kDecideAhead, lx, ly, ev[d], xv[d]);  // this slot's next superblock
