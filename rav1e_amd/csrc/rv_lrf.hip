@@ -844,16 +844,24 @@ __global__ __launch_bounds__(BW * BH / 4) void lrf_rdo_kernel(LrfRdoArgs a) {
 // y0 + 32 .. y0 + 35), the source pixels it needs sit in its registers, and
 // each set's (a, b) tables are built from the integral images (which stay)
 // into packed words. Otherwise as lrf_rdo_kernel.
-struct RdoWideLds {
+// Region `raw` by phase (word offsets): the integral images at 0 and the
+// unit's input + padded copy after them; then, 8-bit, the packed tables at
+// 0 and the boxes' p (u32) and sum (u16) after them, over the images (the
+// boxes go through registers); 10/12-bit (a box sum can exceed 16 bits), the
+// images stay and the tables sit after them, over the input.
+template <bool PS>
+struct RdoWideMap {
   using L = SgrL64;
-  uint32_t img[2 * L::IR * L::IS];  // ii, sq
-  union {
-    uint32_t tab[L::TAB];  // each set's (a, b), packed
-    struct {
-      uint16_t lin[64 * 64];  // the unit's input (lrf_input)
-      uint16_t pad[68 * 68];  // the padded CDEF input
-    } in;
-  } u;
+  static constexpr int IMG = 0, IMGW = 2 * L::IR * L::IS;
+  static constexpr int LIN = IMGW, PAD = LIN + 64 * 64 / 2;  // u16 pairs
+  static constexpr int INW = PAD + 68 * 68 / 2;
+  static constexpr int TAB = PS ? 0 : IMGW, PP = L::TAB, P16 = 2 * L::TAB;
+  static constexpr int TABW = PS ? 2 * L::TAB + (L::TAB + 1) / 2 : IMGW + L::TAB;
+  static constexpr int WORDS = TABW > INW ? TABW : INW;
+};
+template <bool PS>
+struct RdoWideLds {
+  uint32_t raw[RdoWideMap<PS>::WORDS];
   uint16_t xz[256];
   int16_t coffs[48];
   uint8_t bdir[64], bskip[64];
@@ -864,11 +872,29 @@ struct RdoWideLds {
   int8_t sxqd[2];
 };
 
+// each set's tables from the boxes' p and sum (the same places)
+template <int AS, int A1R>
+__device__ __forceinline__ void sgr_tables_pp(const uint32_t *pp, const uint16_t *p16, uint32_t *tab,
+                                              const uint16_t *xz, const SgrLane &ln, int set, int h) {
+  const uint32_t s2 = kSgrS[set][0], s1 = kSgrS[set][1];
+  const int r1rows = s1 ? h + 2 : 0, r2rows = s2 ? (h + 1) / 2 + 1 : 0;
+#pragma unroll 2
+  for (int r = ln.ty; r < r1rows + r2rows; r += ln.tstep) {
+    const bool one = r < r1rows;
+    const int to = (one ? r : A1R + r - r1rows) * AS + ln.tx;
+    tab_put(tab[to], sgr_ab(make_uint2(pp[to], p16[to]), one ? s1 : s2, one ? 455 : 164, xz));
+  }
+}
+
 template <typename Px>
 __global__ __launch_bounds__(512, 4) void lrf_rdo_wide_kernel(LrfRdoArgs a) {
   using SL = SgrL64;
   constexpr int BW = 64, BH = 64, NT = 512, NW = 8, AS = SL::AS, A1R = SL::A1R;
-  __shared__ RdoWideLds S;
+  constexpr bool PS = sizeof(Px) == 1;  // 8-bit: the boxes' p and sum kept (see RdoWideMap)
+  using M = RdoWideMap<PS>;
+  __shared__ RdoWideLds<PS> S;
+  uint32_t *const img = S.raw + M::IMG, *const tab = S.raw + M::TAB;
+  uint16_t *const lin = (uint16_t *)(S.raw + M::LIN), *const pad = (uint16_t *)(S.raw + M::PAD);
   const LrfGeo &g = a.g;
   const int p = a.p0 + blockIdx.y, sb = blockIdx.x, tid = threadIdx.x;
   const int sbc = g.sbc, fsx = sb % sbc, fsy = sb / sbc;
@@ -885,6 +911,7 @@ __global__ __launch_bounds__(512, 4) void lrf_rdo_wide_kernel(LrfRdoArgs a) {
   auto recpx = [&](int x, int y) __attribute__((always_inline)) -> int {  // frame plane coordinates
     return (int)((const Px *)rec.data)[(int64_t)(rec.yorigin + y) * rec.stride + rec.xorigin + x];
   };
+  PHASE(0);
   sgr_init_xz(S.xz);
   cdef_offsets(S.coffs, BW + 4);
   // 1. the padded copy and the unit's input
@@ -895,12 +922,12 @@ __global__ __launch_bounds__(512, 4) void lrf_rdo_wide_kernel(LrfRdoArgs a) {
       const int csx = (tx << xd) >> 6, csy = (ty << yd) >> 6;
       v = (csy < sy || (csy == sy && csx <= sx)) ? recpx(fx0 + tx, fy0 + ty) : 128;
     }
-    S.u.in.pad[i] = (uint16_t)v;
+    pad[i] = (uint16_t)v;
   }
   const int vw = min(BW, pw_t - ox), vh = min(BH, ph_t - oy);
   for (int i = tid; i < BW * BH; i += NT) {
     const int y = i >> 6, x = i & 63;
-    S.u.in.lin[i] = (uint16_t)recpx(fx0 + ox + min(x, vw - 1), fy0 + oy + min(y, vh - 1));
+    lin[i] = (uint16_t)recpx(fx0 + ox + min(x, vw - 1), fy0 + oy + min(y, vh - 1));
   }
   // the unit (size clipped at the tile-relative offset, the reference's
   // quirk) and the lane's source pixels: sgrproj_solve's at the unit's
@@ -934,6 +961,7 @@ __global__ __launch_bounds__(512, 4) void lrf_rdo_wide_kernel(LrfRdoArgs a) {
     return (int32_t)((w[i >> 1] >> (16 * (i & 1))) & 0xffff);
   };
   // 2. CDEF index 0 on the 8x8 blocks inside the tile (cdef_filter_superblock)
+  PHASE(1);
   if (a.cdef) {
     if (tid < 64) {
       const int bx = tid & 7, by = tid >> 3, gx = sx * 16 + 2 * bx, gy = sy * 16 + 2 * by;
@@ -968,19 +996,21 @@ __global__ __launch_bounds__(512, 4) void lrf_rdo_wide_kernel(LrfRdoArgs a) {
         dmp -= 1;
         d = a.pri_uv ? S.bdir[blk] : 0;
       }
-      S.u.in.lin[i] = (uint16_t)cdef_px(S.u.in.pad + (y + 2) * (BW + 4) + x + 2, S.coffs + 6 * d, pri, sec, dmp, cs);
+      lin[i] = (uint16_t)cdef_px(pad + (y + 2) * (BW + 4) + x + 2, S.coffs + 6 * d, pri, sec, dmp, cs);
     }
   }
   __syncthreads();
   // 3. the unit's integral image: lrf_input alone, replicated
-  sgr_integral<SL::IS, SL::IR>(S.img, uw, uh, [&](int r, int c) -> uint32_t {
-    return S.u.in.lin[iclamp(r - 4, 0, uh - 1) * BW + iclamp(c - 4, 0, uw - 1)];
+  PHASE(2);
+  sgr_integral<SL::IS, SL::IR>(img, uw, uh, [&](int r, int c) -> uint32_t {
+    return lin[iclamp(r - 4, 0, uh - 1) * BW + iclamp(c - 4, 0, uw - 1)];
   });
+  PHASE(3);
   uint32_t pxr[8], lnr[8];  // the unit's pixels (0 outside it), lrf_input's
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const int y = qy0 + 32 * (i >> 2) + (i & 3);
-    lnr[i] = S.u.in.lin[y * BW + qx];
+    lnr[i] = lin[y * BW + qx];
     pxr[i] = (qx < uw && y < uh) ? lnr[i] : 0;
   }
   // 4. the distortion (as lrf_rdo_kernel): half blocks over 8 lanes, the
@@ -1064,17 +1094,53 @@ __global__ __launch_bounds__(512, 4) void lrf_rdo_wide_kernel(LrfRdoArgs a) {
   // 5. the 16 sets (wave 0 solves set s while the others build s + 1's tables)
   using Acc = typename std::conditional<sizeof(Px) == 1, int32_t, int64_t>::type;  // 8-bit: 8 products fit
   const SgrLane ln = sgr_lane(uw, tid, NT), ln_rest = sgr_lane(uw, tid - 64, NT - 64);
-  __syncthreads();  // lin is read (the tables take its place); the None parts
+  uint32_t *const pp = S.raw + M::PP;
+  uint16_t *const p16 = (uint16_t *)(S.raw + M::P16);
+  if (PS) {  // the boxes' p and sum, through registers (they land on the images)
+    constexpr int KMAX = (SL::A1R + SL::A2R + NT / SL::AS - 1) / (NT / SL::AS) + 1;
+    uint32_t bp[KMAX], bs[KMAX];
+    const int r1rows = uh + 2, r2rows = (uh + 1) / 2 + 1;
+#pragma unroll
+    for (int k = 0; k < KMAX; k++) {
+      const int r = ln.ty + k * ln.tstep;
+      bp[k] = bs[k] = 0;
+      if (r < r1rows + r2rows) {
+        int to, o, dd;
+        sgr_row<SL::IS, AS, A1R>(r, r1rows, ln.tx, to, o, dd);
+        const uint2 v = sgr_box(isq(img, SL::IS, SL::IR * SL::IS + o, dd), isq(img, SL::IS, o, dd),
+                                r < r1rows ? 9 : 25, cs);
+        bp[k] = v.x;
+        bs[k] = v.y;
+      }
+    }
+    __syncthreads();  // the images and lin are read
+#pragma unroll
+    for (int k = 0; k < KMAX; k++) {
+      const int r = ln.ty + k * ln.tstep;
+      if (r < r1rows + r2rows) {
+        const int to = (r < r1rows ? r : A1R + r - r1rows) * AS + ln.tx;
+        pp[to] = bp[k];
+        p16[to] = (uint16_t)bs[k];  // <= 25 x 255
+      }
+    }
+  }
+  __syncthreads();  // lin is read (the tables take its place); the None parts; the boxes
+  PHASE(4);
   if (fin) err_finish(0);
-  sgr_tables<SL::IS, SL::IR, AS, A1R>(S.img, S.u.tab, S.xz, ln, 0, uh, cs);
+  if (PS)
+    sgr_tables_pp<AS, A1R>(pp, p16, tab, S.xz, ln, 0, uh);
+  else
+    sgr_tables<SL::IS, SL::IR, AS, A1R>(img, tab, S.xz, ln, 0, uh, cs);
+  PHASE(5);
   for (int set = 0; set < 16; set++) {
     __syncthreads();
+    PHASE(6 + 5 * set);
     if (set > 0 && fin) err_finish(set);  // set - 1's, at eo[set]
     uint32_t f2r[8], f1r[8];
     Acc H00 = 0, H11 = 0, H01 = 0, C0 = 0, C1 = 0;
 #pragma unroll
     for (int j = 0; j < 2; j++) {
-      sgr_f4<AS, A1R>(S.u.tab, set, qx, qy0 + 32 * j, pxr + 4 * j, f2r + 4 * j, f1r + 4 * j);
+      sgr_f4<AS, A1R>(tab, set, qx, qy0 + 32 * j, pxr + 4 * j, f2r + 4 * j, f1r + 4 * j);
 #pragma unroll
       for (int k = 0; k < 4; k++)
         if (qx < uw && qy0 + 32 * j + k < uh) {
@@ -1098,6 +1164,7 @@ __global__ __launch_bounds__(512, 4) void lrf_rdo_wide_kernel(LrfRdoArgs a) {
       }
     }
     __syncthreads();
+    PHASE(7 + 5 * set);
     if (wave == 0) {
       int64_t t = 0;
       if (tid < 5)
@@ -1114,15 +1181,21 @@ __global__ __launch_bounds__(512, 4) void lrf_rdo_wide_kernel(LrfRdoArgs a) {
         xo[2 * set + 1] = q[1];
       }
     } else if (set < 15) {
-      sgr_tables<SL::IS, SL::IR, AS, A1R>(S.img, S.u.tab, S.xz, ln_rest, set + 1, uh, cs);
+      if (PS)
+        sgr_tables_pp<AS, A1R>(pp, p16, tab, S.xz, ln_rest, set + 1, uh);
+      else
+        sgr_tables<SL::IS, SL::IR, AS, A1R>(img, tab, S.xz, ln_rest, set + 1, uh, cs);
     }
     __syncthreads();
+    PHASE(8 + 5 * set);
     const int w0 = S.sxqd[0], w1 = S.sxqd[1];
     int32_t d[8];
 #pragma unroll
     for (int i = 0; i < 8; i++)  // 128 outside the unit: lrf_output's fill (never inside the frame)
       d[i] = (qx < uw && qy0 + 32 * (i >> 2) + (i & 3) < uh) ? sgr_out(f2r[i], f1r[i], pxr[i], w0, w1, mx) : 128;
     err_part(d);
+    PHASE(9 + 5 * set);
+    PHASE(10 + 5 * set);
   }
   __syncthreads();
   if (fin) err_finish(16);

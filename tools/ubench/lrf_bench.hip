@@ -132,12 +132,15 @@ int main(int argc, char **argv) {
 #ifdef LRF_PHASES
   // one workgroup alone: its phases in wall_clock64 ticks (100 MHz)
   a.p0 = 0;
-  lrf_rdo_kernel<uint8_t, 64, 64><<<dim3(LRF_PHASES + 1, 1), 1024>>>(a);
+  if (getenv("LRF_BENCH_OLD"))
+    lrf_rdo_kernel<uint8_t, 64, 64><<<dim3(LRF_PHASES + 1, 1), 1024>>>(a);
+  else
+    lrf_rdo_wide_kernel<uint8_t><<<dim3(LRF_PHASES + 1, 1), 512>>>(a);
   CK(hipDeviceSynchronize());
   unsigned long long t[96];
   CK(hipMemcpyFromSymbol(t, HIP_SYMBOL(lrf_phase_t), sizeof(t)));
   printf("one workgroup (unit %d, luma), us:\n", LRF_PHASES);
-  const char *names[6] = {"start", "pad+lin", "cdef", "integral", "tiles", "boxes+none"};  // (stamps before barriers)
+  const char *names[6] = {"start", "pad+lin", "cdef", "integral", "pixels", "boxes/tables0+none"};  // (stamps before barriers)
   for (int k = 1; k < 6; k++) printf("  %-12s %8.2f\n", names[k], (t[k] - t[k - 1]) / 100.0);
   for (int s = 0; s < 16; s++) {
     const unsigned long long *q = t + 6 + 5 * s, prev = s ? q[-1] : t[5];
