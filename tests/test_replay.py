@@ -887,13 +887,15 @@ def test_gpu_replay_one_rank_rccl_exchange(flags):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("config,speed", [("360p", 10), ("1080p", 10), ("2160p", 10),
-                                          ("2160p10", 10),
-                                          ("2160p10", 6), ("2160p444", 10)])
-def test_gpu_replay_full_size_gop(config, speed):
+@pytest.mark.parametrize("config,speed,filters", [("360p", 10, 0), ("1080p", 10, 0), ("2160p", 10, 0),
+                                                  ("2160p10", 10, 0),
+                                                  ("2160p10", 6, 0), ("2160p444", 10, 0),
+                                                  ("1080p", 10, _LRF), ("2160p444", 10, _LRF)])
+def test_gpu_replay_full_size_gop(config, speed, filters):
     """The key frame and one GOP (me_range_scale 4, 2, 1, 1) at the BASELINE
-    shapes and tilings (config D also at its speed-6 schedule), GPU words
-    equal to the CPU replay's frame by frame."""
+    shapes and tilings (config D also at its speed-6 schedule; two shapes
+    with every loop filter, loop restoration's units compared per frame),
+    GPU words equal to the CPU replay's frame by frame."""
     import bench
     w, h, xdec, ydec, bd, tk = bench.CONFIGS[config][:6]
-    _gpu_vs_cpu(w, h, xdec, ydec, bd, 2, 5, tk, flags=RP.RV_REPLAY_SPEED6 if speed == 6 else 0)
+    _gpu_vs_cpu(w, h, xdec, ydec, bd, 2, 5, tk, flags=(RP.RV_REPLAY_SPEED6 if speed == 6 else 0) | filters)
