@@ -1395,6 +1395,298 @@ __global__ __launch_bounds__(64) void lrf_decide_kernel(LrfDecideArgs a) {
   }
 }
 
+// The same decisions by a fixed point (tiles of at most kFixMax superblocks):
+// the tile's restoration state before each superblock -- the CDF and each
+// plane's sgrproj_ref -- is a cheap serial function of the decisions before
+// it, and each decision a parallel function of its state. Guess every state
+// (the initial one), decide every (superblock, plane) in parallel, run the
+// states from the first decision that changed, repeat. Decisions before the
+// first change are final (their states are), so an iteration settles at
+// least one more superblock, and the fixed point is the sequential result;
+// after kFixIter iterations the rest is decided in order.
+constexpr int kFixMax = 1024, kFixIter = 12, kFixThreads = 1024;
+#ifdef LRF_PHASES
+__device__ int lrf_fix_stats[8], lrf_fix_iters[8], lrf_fix_trace[8][kFixIter];
+__device__ unsigned long long lrf_fix_clk[40];
+#define FIXCLK(i) \
+  if (tid == 0 && t == 0) lrf_fix_clk[i] = wall_clock64()
+#else
+#define FIXCLK(i)
+#endif
+struct FixState {
+  uint16_t c0, c1, c3;  // lrf_switchable_cdf[0], [1] and its counter
+  int8_t ref[3][2];
+};
+__device__ __forceinline__ void fix_load(LrfTileState &st, const FixState &f) {
+  st.cdf[0] = f.c0;
+  st.cdf[1] = f.c1;
+  st.cdf[2] = 0;
+  st.cdf[3] = f.c3;
+  for (int p = 0; p < 3; p++)
+    for (int i = 0; i < 2; i++) st.ref[p][i] = f.ref[p][i];
+}
+__device__ __forceinline__ void fix_store(FixState &f, const LrfTileState &st) {
+  f.c0 = st.cdf[0];
+  f.c1 = st.cdf[1];
+  f.c3 = st.cdf[3];
+  for (int p = 0; p < 3; p++)
+    for (int i = 0; i < 2; i++) f.ref[p][i] = st.ref[p][i];
+}
+// one unit's choice at a state: None, then the 16 sets, the first cheapest
+// (the costs of lrf_decide_kernel's lanes, in the reference's order);
+// packed as set | xqd0 << 8 | xqd1 << 16 (set -1: None)
+// (the unit's 17 distortions and 16 xqd pairs in registers: ev, xw)
+struct FixUnit {
+  uint64_t ev[17];
+  uint32_t xw[8];
+};
+__device__ __forceinline__ void fix_load_unit(FixUnit &fu, const uint64_t *e, const int8_t *xq) {
+#pragma unroll
+  for (int s = 0; s < 17; s++) fu.ev[s] = e[s];
+#pragma unroll
+  for (int w = 0; w < 8; w++) fu.xw[w] = ((const uint32_t *)xq)[w];
+}
+__device__ __forceinline__ int fix_decide(const FixUnit &fu, const FixState &f, int p, double lambda,
+                                          const uint8_t (*slut)[128][128], const uint16_t (*sbl)[520]) {
+  int best = -1, bx0 = 0, bx1 = 0;
+  double bc = (double)fu.ev[0] + lambda * ((double)sbl[0][f.c0 >> 6] / 8.0);
+  const uint32_t base = sbl[1][f.c1 >> 6] + (4u << 3);
+  const int r0 = f.ref[p][0], r1 = f.ref[p][1];
+#pragma unroll
+  for (int s = 0; s < 16; s++) {
+    const uint32_t pr = (fu.xw[s >> 1] >> (16 * (s & 1))) & 0xffff;
+    const int x0 = (int)(int8_t)(pr & 0xff), x1 = (int)(int8_t)(pr >> 8);
+    uint32_t bits = base;
+    if (lrf_set_has(s, 0)) bits += slut[0][x0 + 96][r0 + 96];
+    if (lrf_set_has(s, 1)) bits += slut[1][x1 + 32][r1 + 32];
+    const double c = (double)fu.ev[1 + s] + lambda * ((double)bits / 8.0);
+    if (c < bc) {
+      bc = c;
+      best = s;
+      bx0 = x0;
+      bx1 = x1;
+    }
+  }
+  return best < 0 ? 0xff : (best & 0xff) | (bx0 & 0xff) << 8 | (bx1 & 0xff) << 16;
+}
+// the same from memory, one option at a time (no registers held)
+__device__ __noinline__ int fix_decide_mem(const uint64_t *e, const int8_t *xq, const FixState &f, int p,
+                                           double lambda, const uint8_t (*slut)[128][128],
+                                           const uint16_t (*sbl)[520]) {
+  int best = -1, bx0 = 0, bx1 = 0;
+  double bc = (double)e[0] + lambda * ((double)sbl[0][f.c0 >> 6] / 8.0);
+  const uint32_t base = sbl[1][f.c1 >> 6] + (4u << 3);
+  const int r0 = f.ref[p][0], r1 = f.ref[p][1];
+  for (int s = 0; s < 16; s++) {
+    const int x0 = xq[2 * s], x1 = xq[2 * s + 1];
+    uint32_t bits = base;
+    if (lrf_set_has(s, 0)) bits += slut[0][x0 + 96][r0 + 96];
+    if (lrf_set_has(s, 1)) bits += slut[1][x1 + 32][r1 + 32];
+    const double c = (double)e[1 + s] + lambda * ((double)bits / 8.0);
+    if (c < bc) {
+      bc = c;
+      best = s;
+      bx0 = x0;
+      bx1 = x1;
+    }
+  }
+  return best < 0 ? 0xff : (best & 0xff) | (bx0 & 0xff) << 8 | (bx1 & 0xff) << 16;
+}
+constexpr int kFixNoUnit = 0xfe;  // a stretched superblock (no unit of its own)
+
+__global__ __launch_bounds__(kFixThreads) void lrf_decide_fix_kernel(LrfDecideArgs a) {
+  __shared__ uint8_t slut[2][128][128];
+  __shared__ uint16_t sbl[2][520];
+  __shared__ FixState fs[kFixMax];
+  __shared__ int dec[kFixMax][3];
+  __shared__ int first;
+  const LrfGeo &g = a.g;
+  const int ntx = (g.sbc + g.tws - 1) / g.tws;
+  const int t = blockIdx.x, tid = threadIdx.x;
+  FIXCLK(0);
+  const int t0x = (t % ntx) * g.tws, t0y = (t / ntx) * g.ths;
+  if (t0x < a.gx0 || t0x >= a.gx1 || t0y < a.gy0 || t0y >= a.gy1) return;  // another group's tile
+  const int tsw = min(g.tws, g.sbc - t0x), tsh = min(g.ths, g.sbr - t0y), n = tsw * tsh;
+  {
+    const uint4 *gl = (const uint4 *)&g_lrf_subexp[0][0][0];
+    uint4 *sl = (uint4 *)&slut[0][0][0];
+    for (int i = tid; i < 2 * 128 * 128 / 16; i += kFixThreads) sl[i] = gl[i];
+    for (int f = tid; f < 520; f += kFixThreads) {
+      const uint16_t c0[4] = {(uint16_t)(f << 6), 0, 0, 0}, c1[4] = {0, (uint16_t)(f << 6), 0, 0};
+      sbl[0][f] = (uint16_t)lrf_symbol_bits(0, c0, 3);
+      sbl[1][f] = (uint16_t)lrf_symbol_bits(2, c1, 3);
+    }
+    LrfTileState st;
+    lrf_tile_init(st);
+    for (int k = tid; k < n; k += kFixThreads) {
+      fix_store(fs[k], st);  // the guess: every state the initial one
+      dec[k][0] = dec[k][1] = dec[k][2] = -1;
+    }
+  }
+  auto unit_of = [&](int i, int &k, int &p, bool &has, size_t &u) {
+    k = i / 3;
+    p = i - 3 * k;
+    const int fsx = t0x + k % tsw, fsy = t0y + k / tsw;
+    has = fsx < (p == 0 ? g.cols[0] : p == 1 ? g.cols[1] : g.cols[2]) &&
+          fsy < (p == 0 ? g.rows[0] : p == 1 ? g.rows[1] : g.rows[2]);
+    u = (size_t)p * g.nsb + (size_t)fsy * g.sbc + fsx;
+  };
+  // serial: the states from superblock k0 on (k0's own is final), wave 0.
+  // Batches of 64 superblocks: lane j holds superblock k + j's decisions
+  // (read in one LDS access) and receives the state before it (a lane
+  // select), so the chain itself is scalar: lane reads and the updates.
+  auto run_states = [&](int k0) {
+    auto uni = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
+    // the state in three scalar words, updated without branches: cc =
+    // lrf_switchable_cdf[0] | [1] << 16 (both entries move the same way, and
+    // each half stays within 0..32768, so one subtract serves both), c3 its
+    // counter, rp the planes' sgrproj_ref as bytes (ref0 | ref1 << 8 each)
+    uint32_t cc = (uint32_t)uni(fs[k0].c0) | (uint32_t)uni(fs[k0].c1) << 16;
+    int c3 = uni(fs[k0].c3);
+    uint32_t rp[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++)
+      rp[q] = ((uint32_t)uni(fs[k0].ref[q][0]) & 0xff) | ((uint32_t)uni(fs[k0].ref[q][1]) & 0xff) << 8;
+    for (int kb = k0; kb < n; kb += 64) {
+      const int kk = kb + tid, m = min(64, n - kb);
+      const int d0 = kk < n ? dec[kk][0] : kFixNoUnit, d1 = kk < n ? dec[kk][1] : kFixNoUnit,
+                d2 = kk < n ? dec[kk][2] : kFixNoUnit;
+      uint32_t w0 = 0, w1 = 0, w2 = 0;  // the state before superblock kk
+      for (int j = 0; j < m; j++) {
+        const bool me = tid == j;
+        w0 = me ? cc : w0;
+        w1 = me ? (uint32_t)c3 | rp[2] << 16 : w1;
+        w2 = me ? rp[0] | rp[1] << 16 : w2;
+        const int dd[3] = {__builtin_amdgcn_readlane(d0, j), __builtin_amdgcn_readlane(d1, j),
+                           __builtin_amdgcn_readlane(d2, j)};
+#pragma unroll
+        for (int p = 0; p < 3; p++) {
+          // lrf_commit: update_cdf (src/ec.rs:891-905) with symbol 0 (None:
+          // the entries fall) or 2 (a set: they rise towards 32768), and the
+          // set's sgrproj_ref
+          const uint32_t d = (uint32_t)dd[p], set = d & 0xff;
+          const bool valid = set != kFixNoUnit, rise = valid && set < 16;
+          const uint32_t sh = 4 + ((uint32_t)c3 >> 4), msk = (0xffffu >> sh) * 0x10001u;
+          uint32_t x = rise ? 0x80008000u - cc : cc;
+          x -= (x >> sh) & msk;
+          x = rise ? 0x80008000u - x : x;
+          cc = valid ? x : cc;
+          c3 = valid ? min(c3 + 1, 32) : c3;
+          // (masks, not selects: the compiler would branch on them)
+          const uint32_t h0 = 0u - (uint32_t)(set - 10u > 3u), h1 = 0u - (uint32_t)(set < 14u),
+                         rm = 0u - (uint32_t)rise;
+          const uint32_t nr = ((d >> 8) & 0xffu & h0) | ((d >> 8) & 0xff00u & h1) | (95u << 8 & ~h1);
+          rp[p] = (nr & rm) | (rp[p] & ~rm);
+        }
+      }
+      if (kk > k0 && kk < n) {
+        FixState &f = fs[kk];
+        f.c0 = (uint16_t)(w0 & 0xffff);
+        f.c1 = (uint16_t)(w0 >> 16);
+        f.c3 = (uint16_t)(w1 & 0xffff);
+        f.ref[0][0] = (int8_t)(w2 & 0xff);
+        f.ref[0][1] = (int8_t)((w2 >> 8) & 0xff);
+        f.ref[1][0] = (int8_t)((w2 >> 16) & 0xff);
+        f.ref[1][1] = (int8_t)(w2 >> 24);
+        f.ref[2][0] = (int8_t)((w1 >> 16) & 0xff);
+        f.ref[2][1] = (int8_t)(w1 >> 24);
+      }
+    }
+  };
+  __syncthreads();
+  bool settled = false;
+  int from = 0;
+  // the lane's first item stays in registers across the passes
+  FixUnit mine;
+  int mk = 0, mp = 0;
+  bool mhas = false;
+  if (tid < 3 * n) {
+    size_t u;
+    unit_of(tid, mk, mp, mhas, u);
+    if (mhas) fix_load_unit(mine, a.err + u * 17, a.xqd + u * 32);
+  }
+  FIXCLK(1);
+  for (int it = 0; it < kFixIter; it++) {
+    if (tid == 0) first = n;
+    __syncthreads();
+    FIXCLK(2 + 3 * it);
+    for (int i = tid; i < 3 * n; i += kFixThreads) {
+      int k, p, d;
+      if (i == tid) {
+        k = mk;
+        p = mp;
+        if (k < from) continue;
+        d = mhas ? fix_decide(mine, fs[k], p, a.lambda, slut, sbl) : kFixNoUnit;
+      } else {  // tiles past 341 superblocks: the other items straight from memory
+        bool has;
+        size_t u;
+        unit_of(i, k, p, has, u);
+        if (k < from) continue;
+        d = has ? fix_decide_mem(a.err + u * 17, a.xqd + u * 32, fs[k], p, a.lambda, slut, sbl) : kFixNoUnit;
+      }
+      if (d != dec[k][p]) {
+        dec[k][p] = d;
+        atomicMin(&first, k);
+      }
+    }
+    __syncthreads();
+    FIXCLK(3 + 3 * it);
+    from = first;
+#ifdef LRF_PHASES
+    if (tid == 0 && t < 8) lrf_fix_trace[t][it] = from;
+#endif
+    if (from == n) {
+      settled = true;
+      break;
+    }
+    if (tid < 64) run_states(from);
+    __syncthreads();
+    FIXCLK(4 + 3 * it);
+  }
+#ifdef LRF_PHASES
+  if (tid == 0 && t < 8) lrf_fix_iters[t] = settled ? 0 : -1;
+#endif
+  if (!settled && tid == 0) {  // the rest in order (from: its state is final)
+    LrfTileState st;
+    fix_load(st, fs[from]);
+    for (int k = from; k < n; k++) {
+      FixState f;
+      fix_store(f, st);
+#pragma unroll
+      for (int p = 0; p < 3; p++) {
+        int kk, pp;
+        bool has;
+        size_t u;
+        unit_of(3 * k + p, kk, pp, has, u);
+        dec[k][p] = has ? fix_decide_mem(a.err + u * 17, a.xqd + u * 32, f, p, a.lambda, slut, sbl) : kFixNoUnit;
+      }
+#pragma unroll
+      for (int p = 0; p < 3; p++) {
+        const int d = dec[k][p];
+        if (d != kFixNoUnit) {
+          const int8_t q[2] = {(int8_t)((d >> 8) & 0xff), (int8_t)((d >> 16) & 0xff)};
+          lrf_commit(st, p, (int8_t)(d & 0xff), q);
+        }
+      }
+    }
+  }
+#ifdef LRF_PHASES
+  if (tid == 0 && t < 8) lrf_fix_stats[t] = (settled ? 0 : 1000) + from;  // where it settled / fell back
+#endif
+  FIXCLK(39);
+  __syncthreads();
+  for (int i = tid; i < 9 * n; i += kFixThreads) {
+    const int k = i / 9, p = (i / 3) % 3, j = i % 3;
+    const int fsx = t0x + k % tsw, fsy = t0y + k / tsw, d = dec[k][p];
+    int8_t b;
+    if (d == kFixNoUnit)
+      b = j == 0 ? -1 : 0;
+    else
+      b = (int8_t)((d >> (8 * j)) & 0xff);
+    a.units[(((size_t)p * g.urows_max + fsy) * g.ucols_max + fsx) * 3 + j] = b;
+  }
+}
+
 // ---- lrf_filter_frame (src/lrf.rs:1345-1444) ------------------------------------
 struct LrfFilterArgs {
   rv_plane cd[3], db[3], out[3];  // the CDEF output, the deblocked frame, the restored frame
@@ -1604,7 +1896,15 @@ int lrf_decide_launch(const LrfGeo &g, const uint64_t *err, const int8_t *xqd, d
   d.gx1 = rect ? rect[0] + rect[2] : g.sbc;
   d.gy1 = rect ? rect[1] + rect[3] : g.sbr;
   const int nt = ((g.sbc + g.tws - 1) / g.tws) * ((g.sbr + g.ths - 1) / g.ths);
-  lrf_decide_kernel<<<nt, 64, 0, s>>>(d);
+  // RAV1E_LRF_FIX=0 (A/B): the one-wave serial decision
+  static const bool fix = [] {
+    const char *e = getenv("RAV1E_LRF_FIX");
+    return !(e && e[0] == '0');
+  }();
+  if (fix && g.tws * g.ths <= kFixMax)
+    lrf_decide_fix_kernel<<<nt, kFixThreads, 0, s>>>(d);
+  else
+    lrf_decide_kernel<<<nt, 64, 0, s>>>(d);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

@@ -120,16 +120,49 @@ int main(int argc, char **argv) {
     a.p0 = 1;
     lrf_rdo_kernel<uint8_t, 32, 32><<<dim3(g.nsb, 2), 256>>>(a);
     CK(hipEventRecord(e1, 0));
-    lrf_decide_kernel<<<nt, 64>>>(d);
+    if (r & 1)
+      lrf_decide_kernel<<<nt, 64>>>(d);
+    else
+      lrf_decide_fix_kernel<<<nt, kFixThreads>>>(d);
     CK(hipEventRecord(e2, 0));
     CK(hipEventSynchronize(e2));
     float t1, t2;
     CK(hipEventElapsedTime(&t1, e0, e1));
     CK(hipEventElapsedTime(&t2, e1, e2));
-    printf("rep %d (%s luma): rdo %.3f ms (%d x 3 workgroups), decide %.3f ms (%d tiles)\n", r,
-           r & 1 ? "1024-lane" : "512-lane", t1, g.nsb, t2, nt);
+    printf("rep %d (%s luma, %s decision): rdo %.3f ms (%d x 3 workgroups), decide %.3f ms (%d tiles)\n", r,
+           r & 1 ? "1024-lane" : "512-lane", r & 1 ? "serial" : "fixed-point", t1, g.nsb, t2, nt);
+    // the two decisions agree unit for unit
+    static std::vector<int8_t> prev;
+    std::vector<int8_t> cur((size_t)3 * g.urows_max * g.ucols_max * 3);
+    CK(hipMemcpy(cur.data(), units, cur.size(), hipMemcpyDeviceToHost));
+    if (!prev.empty()) {
+      size_t bad = 0;
+      for (size_t i = 0; i < cur.size(); i++) bad += cur[i] != prev[i];
+      printf("  units vs the previous rep's decision: %zu of %zu bytes differ\n", bad, cur.size());
+    }
+    prev = cur;
   }
 #ifdef LRF_PHASES
+  {  // the fixed point's passes (the last rep with it)
+    lrf_decide_fix_kernel<<<nt, kFixThreads>>>(d);
+    CK(hipDeviceSynchronize());
+    int st[8], tr[8][kFixIter];
+    CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(lrf_fix_stats), sizeof(st)));
+    CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(lrf_fix_trace), sizeof(tr)));
+    unsigned long long ck[40];
+    CK(hipMemcpyFromSymbol(ck, HIP_SYMBOL(lrf_fix_clk), sizeof(ck)));
+    printf("  tile 0 clocks (us): setup %.2f", (ck[1] - ck[0]) / 100.0);
+    for (int j = 0; j < 3; j++)
+      printf(" | pass %d: decide %.2f states %.2f", j, (ck[3 + 3 * j] - ck[2 + 3 * j]) / 100.0,
+             (ck[4 + 3 * j] - ck[3 + 3 * j]) / 100.0);
+    printf(" | total %.2f\n", (ck[39] - ck[0]) / 100.0);
+    for (int i = 0; i < 8 && i < nt; i++) {
+      printf("  tile %d: %s at %d; first change per pass:", i, st[i] >= 1000 ? "fell back" : "settled",
+             st[i] % 1000);
+      for (int j = 0; j < kFixIter; j++) printf(" %d", tr[i][j]);
+      printf("\n");
+    }
+  }
   // one workgroup alone: its phases in wall_clock64 ticks (100 MHz)
   a.p0 = 0;
   if (getenv("LRF_BENCH_OLD"))
