@@ -105,7 +105,8 @@ int main(int argc, char **argv) {
   d.gx1 = g.sbc;
   d.gy1 = g.sbr;
   const int nt = ((g.sbc + g.tws - 1) / g.tws) * ((g.sbr + g.ths - 1) / g.ths);
-  hipEvent_t e0, e1, e2;
+  hipEvent_t e0, e1, e2, em;
+  CK(hipEventCreate(&em));
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventCreate(&e2));
@@ -117,6 +118,7 @@ int main(int argc, char **argv) {
       lrf_rdo_kernel<uint8_t, 64, 64><<<dim3(g.nsb, 1), 1024>>>(a);
     else
       lrf_rdo_wide_kernel<uint8_t><<<dim3(g.nsb, 1), 512>>>(a);
+    CK(hipEventRecord(em, 0));
     a.p0 = 1;
     lrf_rdo_kernel<uint8_t, 32, 32><<<dim3(g.nsb, 2), 256>>>(a);
     CK(hipEventRecord(e1, 0));
@@ -129,8 +131,20 @@ int main(int argc, char **argv) {
     float t1, t2;
     CK(hipEventElapsedTime(&t1, e0, e1));
     CK(hipEventElapsedTime(&t2, e1, e2));
-    printf("rep %d (%s luma, %s decision): rdo %.3f ms (%d x 3 workgroups), decide %.3f ms (%d tiles)\n", r,
-           r & 1 ? "1024-lane" : "512-lane", r & 1 ? "serial" : "fixed-point", t1, g.nsb, t2, nt);
+    float tl;
+    CK(hipEventElapsedTime(&tl, e0, em));
+    printf("rep %d (%s luma, %s decision): rdo %.3f ms (luma %.3f; %d x 3 workgroups), decide %.3f ms (%d tiles)\n",
+           r, r & 1 ? "1024-lane" : "512-lane", r & 1 ? "serial" : "fixed-point", t1, tl, g.nsb, t2, nt);
+    {  // the distortions and solutions, hashed (compare builds)
+      std::vector<uint64_t> he((size_t)3 * g.nsb * 17);
+      std::vector<int8_t> hx((size_t)3 * g.nsb * 32);
+      CK(hipMemcpy(he.data(), err, he.size() * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hx.data(), xqd, hx.size(), hipMemcpyDeviceToHost));
+      uint64_t h = 1469598103934665603ull;
+      for (uint64_t v : he) h = (h ^ v) * 1099511628211ull;
+      for (int8_t v : hx) h = (h ^ (uint8_t)v) * 1099511628211ull;
+      printf("  err/xqd hash %016llx\n", (unsigned long long)h);
+    }
     // the two decisions agree unit for unit
     static std::vector<int8_t> prev;
     std::vector<int8_t> cur((size_t)3 * g.urows_max * g.ucols_max * 3);
