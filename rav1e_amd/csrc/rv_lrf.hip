@@ -24,6 +24,7 @@
 // run in the reference's order (IEEE division, no contraction).
 #include <stddef.h>
 #include <stdlib.h>
+#include <algorithm>
 #include <mutex>
 #include <type_traits>
 #include <string.h>
@@ -1209,6 +1210,7 @@ struct LrfDecideArgs {
   const int8_t *xqd;
   double lambda;
   int8_t *units;  // [3][rows][cols][3]: set (-1 None), xqd0, xqd1
+  int fix_passes;  // lrf_decide_fix_kernel: parallel passes before the serial rest
 };
 
 // (key, set) lexicographic minimum with the lane DPP control CTRL reads
@@ -1606,7 +1608,7 @@ __global__ __launch_bounds__(kFixThreads) void lrf_decide_fix_kernel(LrfDecideAr
     if (mhas) fix_load_unit(mine, a.err + u * 17, a.xqd + u * 32);
   }
   FIXCLK(1);
-  for (int it = 0; it < kFixIter; it++) {
+  for (int it = 0; it < a.fix_passes; it++) {
     if (tid == 0) first = n;
     __syncthreads();
     FIXCLK(2 + 3 * it);
@@ -1896,11 +1898,13 @@ int lrf_decide_launch(const LrfGeo &g, const uint64_t *err, const int8_t *xqd, d
   d.gx1 = rect ? rect[0] + rect[2] : g.sbc;
   d.gy1 = rect ? rect[1] + rect[3] : g.sbr;
   const int nt = ((g.sbc + g.tws - 1) / g.tws) * ((g.sbr + g.ths - 1) / g.ths);
-  // RAV1E_LRF_FIX=0 (A/B): the one-wave serial decision
-  static const bool fix = [] {
-    const char *e = getenv("RAV1E_LRF_FIX");
-    return !(e && e[0] == '0');
-  }();
+  // RAV1E_LRF_FIX=0 (A/B): the one-wave serial decision; RAV1E_LRF_FIX_PASSES
+  // = 1 .. kFixIter caps the fixed point's parallel passes (tests: the serial
+  // rest after the cap). Read per frame, so a test can switch them.
+  const char *e = getenv("RAV1E_LRF_FIX");
+  const bool fix = !(e && e[0] == '0');
+  const char *ep = getenv("RAV1E_LRF_FIX_PASSES");
+  d.fix_passes = ep ? std::min(std::max(atoi(ep), 1), kFixIter) : kFixIter;
   if (fix && g.tws * g.ths <= kFixMax)
     lrf_decide_fix_kernel<<<nt, kFixThreads, 0, s>>>(d);
   else

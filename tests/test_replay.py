@@ -544,6 +544,23 @@ def test_gpu_replay_matches_cpu_replay(w, h, xdec, ydec, bd, refs, tiling, flags
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fix,passes", [("0", None), ("1", "1"), ("1", "2"), ("1", None)])
+def test_gpu_lrf_decision_paths(monkeypatch, fix, passes):
+    """rdo_loop_decision's units by each decision kernel: the one-wave
+    serial lrf_decide_kernel (RAV1E_LRF_FIX=0) and the fixed point, whole
+    (default) or capped after one or two parallel passes so that its serial
+    rest decides the tile from the first unsettled superblock on
+    (RAV1E_LRF_FIX_PASSES); 70 superblocks in one tile cross the state
+    chain's 64-superblock batches. Every unit equals the CPU replay's."""
+    monkeypatch.setenv("RAV1E_LRF_FIX", fix)
+    if passes is None:
+        monkeypatch.delenv("RAV1E_LRF_FIX_PASSES", raising=False)
+    else:
+        monkeypatch.setenv("RAV1E_LRF_FIX_PASSES", passes)
+    _gpu_vs_cpu(640, 448, 1, 1, 8, 2, 4, None, _LRF)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("flags", [0, RP.RV_REPLAY_SPEED6])
 def test_gpu_replay_importance_bias_and_quantizer(flags):
     w, h = 256, 192

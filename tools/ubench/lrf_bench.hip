@@ -101,6 +101,7 @@ int main(int argc, char **argv) {
   d.xqd = xqd;
   d.lambda = 300.0;
   d.units = units;
+  d.fix_passes = kFixIter;
   d.gx0 = d.gy0 = 0;
   d.gx1 = g.sbc;
   d.gy1 = g.sbr;
