@@ -293,20 +293,23 @@ __device__ __forceinline__ void sgr_f4(const T *tab, int set, int x, int y0, con
   const uint32_t s2 = kSgrS[set][0], s1 = kSgrS[set][1];
   constexpr int sh = 5 + kSgrBits - kRstBits, sho = 4 + kSgrBits - kRstBits;
   constexpr uint32_t rnd = (1u << sh) >> 1, rndo = (1u << sho) >> 1;
+  // (the results go to scalars in both branches and to the arrays after
+  // them: array stores inside the branches sent the arrays to scratch)
+  uint32_t g0, g1, g2, g3, h0, h1, h2, h3;
   if (s2) {  // r = 2 rows y0 / 2 .. y0 / 2 + 2: even pixels use two, odd ones the second
     uint32_t wa[3], wb[3];
 #pragma unroll
     for (int j = 0; j < 3; j++) sgr_row3(tab + (A1R + (y0 >> 1) + j) * AS, x, wa[j], wb[j]);
-    f2[0] = ((wa[0] + wa[1]) * px[0] + wb[0] + wb[1] + rnd) >> sh;
-    f2[1] = (wa[1] * px[1] + wb[1] + rndo) >> sho;
-    f2[2] = ((wa[1] + wa[2]) * px[2] + wb[1] + wb[2] + rnd) >> sh;
-    f2[3] = (wa[2] * px[3] + wb[2] + rndo) >> sho;
+    g0 = ((wa[0] + wa[1]) * px[0] + wb[0] + wb[1] + rnd) >> sh;
+    g1 = (wa[1] * px[1] + wb[1] + rndo) >> sho;
+    g2 = ((wa[1] + wa[2]) * px[2] + wb[1] + wb[2] + rnd) >> sh;
+    g3 = (wa[2] * px[3] + wb[2] + rndo) >> sho;
   } else {  // box_f_r0: the pixel of the even row
-    f2[0] = f2[1] = px[0] << kRstBits;
-    f2[2] = f2[3] = px[2] << kRstBits;
+    g0 = g1 = px[0] << kRstBits;
+    g2 = g3 = px[2] << kRstBits;
   }
   if (s1) {  // r = 1 rows y0 .. y0 + 5: each row's corner pair and middle
-    uint32_t ca[6], cb[6], ma[6], mb[6];
+    uint32_t ca[6], cb[6], ma[6], mb[6], o[4];
 #pragma unroll
     for (int j = 0; j < 6; j++) {
       const T *t = tab + (y0 + j) * AS + x;
@@ -320,12 +323,26 @@ __device__ __forceinline__ void sgr_f4(const T *tab, int set, int x, int y0, con
     for (int k = 0; k < 4; k++) {  // corners weigh 3, the cross 4
       const uint32_t a = 3 * (ca[k] + ca[k + 2]) + 4 * (ma[k] + ca[k + 1] + ma[k + 1] + ma[k + 2]);
       const uint32_t b = 3 * (cb[k] + cb[k + 2]) + 4 * (mb[k] + cb[k + 1] + mb[k + 1] + mb[k + 2]);
-      f1[k] = (a * px[k] + b + rnd) >> sh;
+      o[k] = (a * px[k] + b + rnd) >> sh;
     }
+    h0 = o[0];
+    h1 = o[1];
+    h2 = o[2];
+    h3 = o[3];
   } else {
-#pragma unroll
-    for (int k = 0; k < 4; k++) f1[k] = px[k] << kRstBits;
+    h0 = px[0] << kRstBits;
+    h1 = px[1] << kRstBits;
+    h2 = px[2] << kRstBits;
+    h3 = px[3] << kRstBits;
   }
+  f2[0] = g0;
+  f2[1] = g1;
+  f2[2] = g2;
+  f2[3] = g3;
+  f1[0] = h0;
+  f1[1] = h1;
+  f1[2] = h2;
+  f1[3] = h3;
 }
 // the restored pixel (:734-746)
 __device__ __forceinline__ int sgr_out(uint32_t f2, uint32_t f1, uint32_t px, int w0, int w1, int mx) {
