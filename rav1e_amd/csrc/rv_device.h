@@ -14,6 +14,16 @@
 
 namespace rv {
 
+// The work-item id, opaque to loop-invariant code motion: a workgroup that
+// loops over work items (rdo_quad_list_kernel) would otherwise compute every
+// lane-dependent LDS / pixel offset of the inlined bodies once before the
+// loop and keep them all live -- spilled to scratch (~0.5 KB per lane).
+__device__ __forceinline__ unsigned rv_tid() {
+  unsigned t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 __device__ __forceinline__ int32_t wadd(int32_t a, int32_t b) {
   return (int32_t)((uint32_t)a + (uint32_t)b);
 }

@@ -232,6 +232,6 @@ int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *
                    const uint8_t *dir, const int32_t *var, const uint8_t cdef_str[2], const double ds[3],
                    uint64_t *err, int8_t *xqd, const int32_t *rect, hipStream_t s);
 int lrf_decide_launch(const LrfGeo &g, const uint64_t *err, const int8_t *xqd, double lambda, int8_t *units,
-                      const int32_t *rect, hipStream_t s);
+                      const int32_t *rect, int fix_passes, hipStream_t s);
 int lrf_filter_launch(const rv_plane cd[3], const rv_plane db[3], const rv_plane out[3], const LrfGeo &g,
                       const int8_t *units, int enable_cdef, hipStream_t s);

@@ -1903,7 +1903,7 @@ int lrf_rdo_launch(const rv_plane rec[3], const rv_plane src[3], const uint8_t *
 // the sequential decisions over the units lrf_rdo_launch priced (rect: the
 // same superblocks)
 int lrf_decide_launch(const LrfGeo &g, const uint64_t *err, const int8_t *xqd, double lambda, int8_t *units,
-                      const int32_t *rect, hipStream_t s) {
+                      const int32_t *rect, int fix_passes, hipStream_t s) {
   LrfDecideArgs d;
   d.g = g;
   d.err = err;
@@ -1915,14 +1915,10 @@ int lrf_decide_launch(const LrfGeo &g, const uint64_t *err, const int8_t *xqd, d
   d.gx1 = rect ? rect[0] + rect[2] : g.sbc;
   d.gy1 = rect ? rect[1] + rect[3] : g.sbr;
   const int nt = ((g.sbc + g.tws - 1) / g.tws) * ((g.sbr + g.ths - 1) / g.ths);
-  // RAV1E_LRF_FIX=0 (A/B): the one-wave serial decision; RAV1E_LRF_FIX_PASSES
-  // = 1 .. kFixIter caps the fixed point's parallel passes (tests: the serial
-  // rest after the cap). Read per frame, so a test can switch them.
-  const char *e = getenv("RAV1E_LRF_FIX");
-  const bool fix = !(e && e[0] == '0');
-  const char *ep = getenv("RAV1E_LRF_FIX_PASSES");
-  d.fix_passes = ep ? std::min(std::max(atoi(ep), 1), kFixIter) : kFixIter;
-  if (fix && g.tws * g.ths <= kFixMax)
+  // fix_passes: 0 the one-wave serial decision, else the fixed point with at
+  // most that many parallel passes (capped at kFixIter) before its serial rest
+  d.fix_passes = std::min(std::max(fix_passes, 1), kFixIter);
+  if (fix_passes > 0 && g.tws * g.ths <= kFixMax)
     lrf_decide_fix_kernel<<<nt, kFixThreads, 0, s>>>(d);
   else
     lrf_decide_kernel<<<nt, 64, 0, s>>>(d);

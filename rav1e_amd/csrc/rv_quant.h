@@ -109,7 +109,7 @@ template <int N, int LPB, typename Co, typename Put>
 __device__ __forceinline__ int quantize_block(const QCtx &c, const uint16_t *scan, Co co,
                                               Put put) {
   constexpr int K = N >= LPB ? N / LPB : 1;  // scan indices per lane
-  const int lane = threadIdx.x & (LPB - 1);
+  const int lane = rv_tid() & (LPB - 1);
   const int i0 = lane * K;
   const bool live = i0 < N;
   const int s = c.log_tx_scale;
@@ -136,7 +136,7 @@ __device__ __forceinline__ int quantize_block(const QCtx &c, const uint16_t *sca
     if (i0 + k >= 1 && (v < 0 ? -v : v) >= c.deadzone) last = i0 + k;
   }
   // lanes of this group in the wavefront's 64-bit masks
-  const int wl = threadIdx.x & 63;
+  const int wl = rv_tid() & 63;
   const uint64_t gmask = LPB == 64 ? ~0ull : (((1ull << LPB) - 1) << (wl & ~(LPB - 1)));
   const uint64_t sig = __ballot(last >= 1) & gmask;
   // chunks ascend with the lane, so the highest lane holding a significant

@@ -304,7 +304,7 @@ __device__ __forceinline__ void mc_compound(const RdoArgs &a, const RdoPlane &pl
   constexpr int kRowDw = ((N + 7) * B + 3) / 4, kTot = (RB + 7) * kRowDw;
   static_assert((RB % 8 == 0 || RB < 8) && N % RB == 0, "bands of whole 8-row groups");
   constexpr int U = RB < 8 ? RB : 8;
-  const int col = threadIdx.x & (N - 1);
+  const int col = rv_tid() & (N - 1);
   const int ib = a.bd == 12 ? 2 : 4, maxv = (1 << a.bd) - 1;
   const McF f0 = mc_setup<Px>(jb.cf, jb.rf, a.mb_w, a.mb_h);
   const McF f1 = mc_setup<Px>(jb.cf2, jb.rf2, a.mb_w, a.mb_h);
@@ -413,7 +413,7 @@ template <typename Px, int N, int LPB>
 __device__ __forceinline__ uint64_t rdo_sse_biased(const RdoArgs &a, const RdoJob &j, const Px *o,
                                                    int64_t os, const Px *d) {
   const int bw = a.sub_w, bh = a.sub_h, nbx = N / bw, nby = N / bh;
-  const int lane = threadIdx.x & (LPB - 1);
+  const int lane = rv_tid() & (LPB - 1);
   uint64_t acc = 0;
   for (int k = lane; k < nbx * nby; k += LPB) {
     const int by = k / nbx, bx = k - by * nbx;
@@ -443,7 +443,7 @@ __device__ __forceinline__ uint64_t rdo_dist_biased(const RdoArgs &a, const RdoJ
     // block's 8 lanes (aligned groups of 8), the f64 tail on its first lane
     constexpr int NB = N / 8, ROWS = NB * NB * 8;
     static_assert(LPB % 8 == 0 && ROWS % LPB == 0, "rows of 8x8 blocks over the lanes");
-    const int lane = threadIdx.x & (LPB - 1);
+    const int lane = rv_tid() & (LPB - 1);
     uint64_t acc = 0;
 #pragma unroll
     for (int k0 = 0; k0 < ROWS; k0 += LPB) {
@@ -512,7 +512,7 @@ __device__ __forceinline__ void rdo_cand_body(const RdoArgs &a, const RdoPlane &
   constexpr int P = B == 1 ? ((N + 8 + 15) / 16) * 16 : ((2 * (N + 8) + 15) / 16) * 16;
   constexpr int C32 = N < 32 ? N : 32;           // coded coefficient extent
   static_assert(!LUMA || N >= 8, "cdef distortion runs on 8x8 blocks");
-  const int lane = threadIdx.x & (LPB - 1);
+  const int lane = rv_tid() & (LPB - 1);
   RdoJob jb;
   if constexpr (MODE == 3)
     jb = rdo_job_intra<Px, N>(a, &pl == &a.p[1] ? 2 : 1, t);
@@ -807,7 +807,7 @@ struct LumaLds {
 template <typename Px>
 __device__ __forceinline__ uint64_t luma_dist(const RdoArgs &a, const RdoJob &j, const Px *o,
                                               int64_t os, const Px *pred) {
-  const int lane = threadIdx.x & 63, by = lane >> 3, bx = lane & 7;
+  const int lane = rv_tid() & 63, by = lane >> 3, bx = lane & 7;
   const uint64_t v =
       rdo_cdef_8x8<Px>(o + (int64_t)(by * 8) * os + bx * 8, os, pred + by * 8 * 64 + bx * 8, 64, a.bd);
   const int px = j.bx + bx * 8, py = j.by + by * 8;
@@ -822,7 +822,7 @@ __device__ __forceinline__ void luma_front(const RdoArgs &a, const RdoPlane &pl,
   constexpr int P = LumaLds<Px, int16_t, NPART>::kWinP;
   constexpr int RP = N / NPART;  // output rows per band
   static_assert(RP % 8 == 0, "MC rows run in groups of 8");
-  const int lane = threadIdx.x & 63;
+  const int lane = rv_tid() & 63;
   const rv_plane &ref = pl.ref[jb.ref];
   const int ox = 0, oy = 0;
   const int bd = a.bd, ib = bd == 12 ? 2 : 4, maxv = (1 << bd) - 1;
@@ -986,7 +986,7 @@ __device__ __forceinline__ void luma_quantize(const RdoArgs &a, const RdoPlane &
         txd += (uint64_t)(int64_t)wmul(dd, dd);
         *e = jb.zero ? 0 : q;
       });
-  const int lane = threadIdx.x & 63;
+  const int lane = rv_tid() & 63;
   if (!a.commit) {
     txd = group_sum<64>(txd);
     const int bits = 2 * (3 - pl.q.log_tx_scale);
@@ -1035,7 +1035,7 @@ __device__ __forceinline__ void luma_back(const RdoArgs &a, const RdoPlane &pl, 
                                           const RdoJob &jb, bool valid, const Mid *imid,
                                           Px *pred) {
   constexpr int N = 64, B = (int)sizeof(Px);
-  const int lane = threadIdx.x & 63;
+  const int lane = rv_tid() & 63;
   const int bd = a.bd, maxv = (1 << bd) - 1;
   const int crange = bd + 6 > 16 ? bd + 6 : 16;
   // ---- D'. inverse columns + add into pred ---------------------------------
@@ -1073,7 +1073,7 @@ __device__ __forceinline__ void luma_back(const RdoArgs &a, const RdoPlane &pl, 
 template <typename Px, typename Mid, int NPART, int MODE>
 __device__ __forceinline__ void rdo_luma_body(const RdoArgs &a, const RdoPlane &pl, int t,
                                               uint8_t *scr, Px *pred, const uint16_t *scan) {
-  const int lane = threadIdx.x & 63;
+  const int lane = rv_tid() & 63;
   RdoJob jb;
   if constexpr (MODE == 3)
     jb = rdo_job_intra<Px, 64>(a, 0, t);
@@ -1107,7 +1107,7 @@ __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, in
                                                 Px *pred, const uint16_t *scan, int pairs = -1) {
   if (pairs < 0) pairs = (chroma.n_tx + 1) / 2;
   const int plane = b / pairs;
-  const int half = (threadIdx.x & 63) >> 5;
+  const int half = (rv_tid() & 63) >> 5;
   const int n = rdo_ntx(chroma);
   int i = 2 * (b - plane * pairs) + half;
   if (i - half >= n) return;  // past the compacted list: the whole pair
@@ -1121,7 +1121,7 @@ __device__ __forceinline__ void rdo_chroma_pair(const RdoArgs &chroma, int b, in
 // workgroup; ends with a barrier.
 __device__ __forceinline__ void stage_scan(uint16_t *dst, int tx_index) {
   const uint16_t *src = RV_SCANS + RV_SCAN_OFF[tx_index];
-  for (int i = threadIdx.x; i < 1024; i += blockDim.x) dst[i] = src[i];
+  for (int i = rv_tid(); i < 1024; i += blockDim.x) dst[i] = src[i];
   __syncthreads();
 }
 
@@ -1174,7 +1174,7 @@ __device__ __forceinline__ void rdo_quad_luma(const RdoArgs &luma, int b, int n,
                                               uint8_t *lds, const uint16_t *scan) {
   using L = typename QuadLds<Px>::L;
   constexpr int NPART = sizeof(Px) == 1 ? 2 : 4;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(rv_tid() >> 6), lane = rv_tid() & 63;
   auto slot = [&](int q) __attribute__((always_inline)) { return lds + q * L::kSlot; };
   auto fmid = [&](int q) __attribute__((always_inline)) {
     return reinterpret_cast<int32_t *>(slot(q));
@@ -1240,7 +1240,7 @@ __device__ __forceinline__ void rdo_quad_luma(const RdoArgs &luma, int b, int n,
 template <typename Px, int MODE>
 __device__ __forceinline__ void rdo_quad_chroma(const RdoArgs &chroma, int c, int pairs,
                                                 uint8_t *lds, const uint16_t *scan) {
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane(rv_tid() >> 6);
   const int pair = 3 * c + wave;
   if (wave == 3 || pair >= 2 * pairs) return;
   uint8_t *w = lds + wave * kChromaPair(sizeof(Px));
@@ -1300,6 +1300,77 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     rdo_quad_wg<Px, 1>(l1, c1, nq1, var, blockIdx.x - g0, lds, scan);
 }
 
+// List-driven score launches (the compacted candidate lists of round 0 and of
+// every MV-stack round): a pool of workgroups walks the live work only.  The
+// device counts give the live luma quads and chroma triples of set A (MODE
+// MA) and, when nsets == 2, of set B (MODE MB), laid out back to back:
+//   [A luma quads | A chroma triples | B luma quads | B chroma triples]
+// so a round of a few dozen superblocks launches a pool, not the frame's full
+// grid of early exits (66 k waves per launch at 2160p: the ~60 us dispatch
+// floor of the round-5 trace).  Chroma pairs are indexed by the live count
+// (pairs per plane = ceil(count / 2)), which keeps them contiguous.
+//
+// The arguments [la, ca, lb, cb] come from device memory (rdo_args_store_kernel,
+// once per frame): by value or bound to the kernel's parameters, a loop over
+// the inlined bodies copies them to scratch.  The bodies read the work-item
+// id through rv_tid(), so the loop does not hoist (and spill) their lane
+// addresses either: 52 B of scratch per lane instead of ~2 KB.
+template <typename Px, int MA, int MB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_quad_list_kernel(
+    const RdoArgs *__restrict__ A, int nsets, int var) {
+  __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
+  __shared__ uint16_t scan[1024];
+  const RdoArgs &la = A[0], &ca = A[1], &lb = A[2], &cb = A[3];
+  const int na = rdo_ntx(la), ma = rdo_ntx(ca);
+  const int nb = nsets > 1 ? rdo_ntx(lb) : 0, mb = nsets > 1 ? rdo_ntx(cb) : 0;
+  const int pa = (ma + 1) / 2, pb = (mb + 1) / 2;
+  const int e0 = (na + 3) / 4, e1 = e0 + (2 * pa + 2) / 3;
+  const int e2 = e1 + (nb + 3) / 4, e3 = e2 + (2 * pb + 2) / 3;
+  for (int b = blockIdx.x; b < e3; b += gridDim.x) {
+    if (b < e0) {
+      stage_scan(scan, la.q_tx_index);
+      rdo_quad_luma<Px, MA>(la, b, na, var, lds, scan);
+    } else if (b < e1) {
+      stage_scan(scan, ca.q_tx_index);
+      rdo_quad_chroma<Px, MA>(ca, b - e0, pa, lds, scan);
+    } else if (b < e2) {
+      stage_scan(scan, lb.q_tx_index);
+      rdo_quad_luma<Px, MB>(lb, b - e1, nb, var, lds, scan);
+    } else {
+      stage_scan(scan, cb.q_tx_index);
+      rdo_quad_chroma<Px, MB>(cb, b - e2, pb, lds, scan);
+    }
+    __syncthreads();  // the slots and the scan are reused by the next item
+  }
+}
+
+// Kernel arguments -> device memory (they are captured at launch, so the
+// host's copies need not outlive the call).
+__global__ __launch_bounds__(256) void rdo_args_store_kernel(RdoArgs a0, RdoArgs a1, RdoArgs a2,
+                                                              RdoArgs a3, int n, RdoArgs *out) {
+  static_assert(sizeof(RdoArgs) % 4 == 0, "word copy");
+  constexpr int W = (int)(sizeof(RdoArgs) / 4);
+  for (int i = threadIdx.x; i < n * W; i += blockDim.x) {
+    const int k = i / W, w = i - k * W;
+    const RdoArgs *s = k == 0 ? &a0 : k == 1 ? &a1 : k == 2 ? &a2 : &a3;
+    uint32_t v;
+    __builtin_memcpy(&v, reinterpret_cast<const uint8_t *>(s) + 4 * w, 4);
+    __builtin_memcpy(reinterpret_cast<uint8_t *>(out + k) + 4 * w, &v, 4);
+  }
+}
+
+// The pool of a list-driven launch: RAV1E_HIP_F4_POOL workgroups (default
+// 1024, four per CU: the LDS of QuadLds allows four), never more than the
+// full grid.
+static int rdo_f4_pool() {
+  static const int pool = [] {
+    const char *e = getenv("RAV1E_HIP_F4_POOL");
+    const int v = e ? atoi(e) : 1024;
+    return v > 0 ? v : 1024;
+  }();
+  return pool;
+}
+
 }  // namespace rv
 
 using namespace rv;
@@ -1315,7 +1386,7 @@ __global__ __launch_bounds__(256) void rdo_small_kernel(RdoArgs a, int nplanes) 
   __shared__ __align__(16) uint8_t lds[4 * TPW * PER];
   __shared__ uint16_t scan[1024];
   stage_scan(scan, a.q_tx_index);
-  const int wave = threadIdx.x >> 6, g = (threadIdx.x & 63) / N;
+  const int wave = rv_tid() >> 6, g = (rv_tid() & 63) / N;
   const int n = rdo_ntx(a), total = n * nplanes;
   const int w0 = (blockIdx.x * 4 + wave) * TPW;
   if (w0 >= total) return;  // the whole wavefront is past the tasks
@@ -1338,7 +1409,7 @@ __device__ __forceinline__ void rdo_small_part(const RdoArgs &a, int nplanes, in
   constexpr int SLAB = rdo_slab_bytes<Px, N>();
   constexpr int PER = (SLAB + N * N * (int)sizeof(Px) + 15) / 16 * 16;
   stage_scan(scan, a.q_tx_index);
-  const int wave = threadIdx.x >> 6, g = (threadIdx.x & 63) / N;
+  const int wave = rv_tid() >> 6, g = (rv_tid() & 63) / N;
   const int n = rdo_ntx(a), total = n * nplanes;
   const int w0 = (blk * 4 + wave) * TPW;
   if (w0 >= total) return;
@@ -1469,6 +1540,44 @@ int rv_rdo_candidates_pair(const RdoArgs &l0, const RdoArgs &c0, const RdoArgs &
     rdo_quad_pair_kernel<uint16_t><<<g0 + g1, 256, 0, s>>>(l0, c0, nq0, (int)g0, l1, c1, nq1, var);
   else
     rdo_quad_pair_kernel<uint8_t><<<g0 + g1, 256, 0, s>>>(l0, c0, nq0, (int)g0, l1, c1, nq1, var);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+int rv_rdo_args_put(const RdoArgs *h, int n, RdoArgs *dev, hipStream_t s) {
+  if (!h || !dev || n < 1 || n > 4) return rv_set_error(RV_EINVAL, "rv_rdo_args_put: bad arguments");
+  rdo_args_store_kernel<<<1, 256, 0, s>>>(h[0], h[n > 1 ? 1 : 0], h[n > 2 ? 2 : 0], h[n > 3 ? 3 : 0],
+                                          n, dev);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+int rv_rdo_candidates_list(const RdoArgs *h, const RdoArgs *dev, int nsets, int mode_a, int hbd,
+                           hipStream_t s) {
+  if (!h || !dev || nsets < 1 || nsets > 2 || mode_a < 0 || mode_a > 1 || (nsets == 2 && mode_a) ||
+      h[0].commit || h[0].bd == 12)
+    return rv_set_error(RV_EINVAL, "rv_rdo_candidates_list: bad arguments");
+  for (int k = 0; k < 2 * nsets; k++)
+    if (!h[k].list || !h[k].count)
+      return rv_set_error(RV_EINVAL, "rv_rdo_candidates_list: the sets must be list-driven");
+  static const int var = [] {
+    const char *e = getenv("RAV1E_HIP_RDO_VARIANT");
+    return e ? atoi(e) : 3;
+  }();
+  // the full grid (every listed slot live) bounds the pool
+  unsigned full = 0;
+  for (int k = 0; k < nsets; k++)
+    full += (unsigned)((h[2 * k].n_tx + 3) / 4) +
+            (unsigned)(2 * ((h[2 * k + 1].n_tx + 1) / 2) + 2) / 3;
+  const unsigned grid = std::min(full, (unsigned)rdo_f4_pool());
+  if (grid == 0) return RV_OK;
+#define RV_LIST(PX, MA, MB) rdo_quad_list_kernel<PX, MA, MB><<<grid, 256, 0, s>>>(dev, nsets, var)
+  if (hbd) {
+    if (nsets == 2) RV_LIST(uint16_t, 0, 1); else if (mode_a) RV_LIST(uint16_t, 1, 1); else RV_LIST(uint16_t, 0, 0);
+  } else {
+    if (nsets == 2) RV_LIST(uint8_t, 0, 1); else if (mode_a) RV_LIST(uint8_t, 1, 1); else RV_LIST(uint8_t, 0, 0);
+  }
+#undef RV_LIST
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

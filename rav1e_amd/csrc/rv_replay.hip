@@ -1168,6 +1168,7 @@ struct rv_replay {
   hipStream_t lrf_side = nullptr;
   hipEvent_t ev_lrf0 = nullptr, ev_lrf1 = nullptr;
   bool lrf_pending = false;
+  int lrf_fix_passes = 1 << 30;  // the decision kernel (create: RAV1E_LRF_FIX[_PASSES])
   RvInput lrf_out;
   RvInput cdef_pre;                 // the deblocked, pre-CDEF frame (the padded copy's source)
   uint8_t *cdef_dir = nullptr, *cdef_idx = nullptr;  // per 8x8 block; per 64x64 (all 0)
@@ -1240,6 +1241,7 @@ struct rv_replay {
   uint64_t *l_out, *c_out;  // F4: [skip dist, non-skip dist, rate] per transform block
   RdoWinner *win;
   int32_t *cand_list, *cand_count;  // F4: the valid candidates
+  RdoArgs *f4_args = nullptr;        // F4: the frame's list-launch arguments [la, ca, lc, cc]
   CandKey *cand_key = nullptr;       // F4: what each candidate slot was last evaluated with
   uint8_t *f3dirty = nullptr;        // rounds: the F3 jobs whose set / pmv changed [R][nsb]
   uint8_t *f2dirty = nullptr;        // rounds: the F2 jobs whose set changed [R][nsb][4]
@@ -1789,12 +1791,12 @@ static int lrf_decide_slot(rv_replay *r, const RvSlot &s, const RvInput &in, int
                       r->cdef, r->cdef_dir, r->cdef_var, r->cdef_str[lv], r->lv[lv].ds, r->lrf_err,
                       r->lrf_xqd, rect, r->stream));
   if (rect || !r->lrf_side)  // a group's units are packed right after: no overlap
-    return lrf_decide_launch(lg, r->lrf_err, r->lrf_xqd, r->lv[lv].lambda, r->lrf_units, rect, r->stream);
+    return lrf_decide_launch(lg, r->lrf_err, r->lrf_xqd, r->lv[lv].lambda, r->lrf_units, rect, r->lrf_fix_passes, r->stream);
   // the sequential decision (a few waves, latency only) on the side stream,
   // beside the deblocking and CDEF; lrf_filter_launch waits for it
   RV_H(hipEventRecord(r->ev_lrf0, r->stream));
   RV_H(hipStreamWaitEvent(r->lrf_side, r->ev_lrf0, 0));
-  RV_R(lrf_decide_launch(lg, r->lrf_err, r->lrf_xqd, r->lv[lv].lambda, r->lrf_units, rect, r->lrf_side));
+  RV_R(lrf_decide_launch(lg, r->lrf_err, r->lrf_xqd, r->lv[lv].lambda, r->lrf_units, rect, r->lrf_fix_passes, r->lrf_side));
   RV_H(hipEventRecord(r->ev_lrf1, r->lrf_side));
   r->lrf_pending = true;
   return RV_OK;
@@ -2165,6 +2167,7 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     ok = ok && r->f3dirty && r->f2dirty;
   }
   r->cand_count = (int32_t *)dalloc(r, 8);  // [single, compound]
+  r->f4_args = (RdoArgs *)dalloc(r, 4 * sizeof(RdoArgs));
   r->cand_evals = (uint32_t *)dalloc(r, rv_replay::kRing * 2 * kLevels * 4);
   if (r->cand_evals)
     (void)hipMemsetAsync(r->cand_evals, 0, rv_replay::kRing * 2 * kLevels * 4, r->stream);
@@ -2364,9 +2367,12 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
   }
   if (cfg->flags & RV_REPLAY_LRF) {
     LrfGeo lg;
-    if (!r->cdef || lrf_geometry(g.W, g.H, g.xdec, g.ydec, g.bd, 100, g.tws, g.ths, &lg) != RV_OK) {
-      rv_set_error(RV_EINVAL, "rv_replay_create: RV_REPLAY_LRF needs RV_REPLAY_CDEF and units of one "
-                              "superblock");
+    // (the unit size depends on the quantizer: rv_replay_set_level_params
+    // checks every level's; 100 here is the replay's default level 0)
+    if (!r->cdef || g.xdec != g.ydec ||
+        lrf_geometry(g.W, g.H, g.xdec, g.ydec, g.bd, 100, g.tws, g.ths, &lg) != RV_OK) {
+      rv_set_error(RV_EINVAL, "rv_replay_create: RV_REPLAY_LRF needs RV_REPLAY_CDEF, 4:2:0 or 4:4:4 "
+                              "(rav1e's enable_restoration is off in 4:2:2) and units of one superblock");
       rv_replay_destroy(r);
       return nullptr;
     }
@@ -2378,6 +2384,14 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
     // RAV1E_LRF_SIDE=1: the decision on a side stream (2160p A/B, r05an:
     // 136-142 vs 152-154 fps without -- one more stream per instance than
     // the hardware queues serve well; off)
+    // RAV1E_LRF_FIX=0 (A/B): the one-wave serial decision; RAV1E_LRF_FIX_PASSES
+    // = 1 .. caps the fixed point's parallel passes (tests: the serial rest
+    // after the cap).  Read here, once: the worker threads of a pipelined
+    // replay must not call getenv per frame while the caller may setenv.
+    {
+      const char *fe = getenv("RAV1E_LRF_FIX"), *fp = getenv("RAV1E_LRF_FIX_PASSES");
+      r->lrf_fix_passes = (fe && fe[0] == '0') ? 0 : fp ? std::max(atoi(fp), 1) : 1 << 30;
+    }
     const char *se = getenv("RAV1E_LRF_SIDE");
     if (se && se[0] == '1')
       ok = ok && hipStreamCreateWithFlags(&r->lrf_side, hipStreamNonBlocking) == hipSuccess &&
@@ -2447,7 +2461,7 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
   r->tail = (unsigned long long *)dalloc(r, 5 * 8);
   ok = ok && r->coarse && r->half && r->look && r->half_l && r->la_list && r->full && r->sub &&
        r->l_out && r->c_out && r->win &&
-       r->cand_list && r->cand_count && r->cand_evals &&
+       r->cand_list && r->cand_count && r->f4_args && r->cand_evals &&
        r->l_lev && r->c_lev && r->words && r->tail;
   if (ok) {
     ok = hipMemsetAsync(r->words, 0, r->nwords * 8, r->stream) == hipSuccess &&
@@ -2556,6 +2570,10 @@ int rv_replay_set_level_params(rv_replay *r, int level, const rv_replay_level_pa
     for (int c = 1; c < 3; c++)
       RV_R(rv_quant_ctx(p->base_q_idx, P.bc * P.bch, 0, bd, p->dc_delta_q[c], p->ac_delta_q[c],
                         &L.qs[l][c]));
+  }
+  if (r->lrf) {  // the level's restoration units must be one superblock (checked before any frame)
+    LrfGeo lg;
+    RV_R(lrf_geometry(r->g.W, r->g.H, r->g.xdec, r->g.ydec, bd, p->base_q_idx, r->g.tws, r->g.ths, &lg));
   }
   L.qidx = p->base_q_idx;
   // deblock_filter_optimize's fast levels (inter frames at speed 10; speed 6
@@ -3835,6 +3853,19 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   // F4's arguments (la / ca become F6's commit arguments below; the rounds
   // after the intra pass evaluate candidates again)
   const RdoArgs la4 = la, ca4 = ca;
+  // the compound sets (all pushed; distinct MV pairs from the list) and the
+  // list launches' arguments in device memory: [la4, ca4, lc4, cc4]
+  RdoArgs lc4 = la4, cc4 = ca4;
+  lc4.list = cc4.list = r->cand_list + nsingle;
+  lc4.count = cc4.count = r->cand_count + 1;
+  lc4.cand_base = cc4.cand_base = 0;
+  lc4.n_tx = g.nsb * cg.comp;
+  cc4.n_tx = g.nsb * cg.comp * ntx_c;
+  const RdoArgs f4h[4] = {la4, ca4, lc4, cc4};
+  // RAV1E_HIP_F4_LIST=0: the full-grid launches (A/B); 12-bit keeps them
+  static const bool f4_list_env = !(getenv("RAV1E_HIP_F4_LIST") && getenv("RAV1E_HIP_F4_LIST")[0] == '0');
+  const bool f4_list = f4_list_env && g.bd != 12;
+  if (f4_list) RV_R(rv_rdo_args_put(f4h, cg.comp ? 4 : 2, r->f4_args, st));
   // F3 full-res full-pel diamond -> sub-pel predictor; sub-pel diamond
   // (speed 10: SAD, no hp) -> NEWMV of every superblock and reference;
   // the candidates; F4; the argmin.  Round 0: every superblock, full grids.
@@ -3861,17 +3892,17 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     }
     RV_EV(6);
     // F4 every valid candidate, luma + both chroma planes in one fused launch
-    RV_R(rv_rdo_candidates(la4, ca4, g.hbd, st));
+    if (f4_list)
+      RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 1, 0, g.hbd, st));
+    else
+      RV_R(rv_rdo_candidates(la4, ca4, g.hbd, st));
     if (r->lvl && !edge && !lv_early) RV_R(lv_rdo(st));
     if (cg.comp) {  // the compound candidates (all pushed), distinct MV pairs from the list
-      RdoArgs lc = la4, cc = ca4;
-      lc.list = cc.list = r->cand_list + nsingle;
-      lc.count = cc.count = r->cand_count + 1;
-      lc.cand_base = cc.cand_base = 0;
-      lc.n_tx = g.nsb * cg.comp;
-      cc.n_tx = g.nsb * cg.comp * ntx_c;
       RV_EV(7);
-      RV_R(rv_rdo_candidates(lc, cc, g.hbd, st, true));
+      if (f4_list)
+        RV_R(rv_rdo_candidates_list(f4h + 2, r->f4_args + 2, 1, 1, g.hbd, st));
+      else
+        RV_R(rv_rdo_candidates(lc4, cc4, g.hbd, st, true));
       if (r->lvl && !edge && !lv_early) RV_R(lv_rdo_comp(st));
     } else {
       RV_EV(7);
@@ -3932,21 +3963,21 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       RV_H(hipEventRecord(r->ev_rlists, xs));
       RV_H(hipStreamWaitEvent(x2, r->ev_rlists, 0));
     }
-    // F4 (full grids: a workgroup past the device counts exits at once);
-    // on a compound frame the single and compound candidates in one launch
+    // F4: a pool of workgroups over the live list entries (rdo_quad_list_kernel;
+    // RAV1E_HIP_F4_LIST=0: full grids whose workgroups past the device counts
+    // exit at once); on a compound frame the single and compound candidates
+    // in one launch
     if (cg.comp) {
-      RdoArgs lc = la4, cc = ca4;
-      lc.list = cc.list = r->cand_list + nsingle;
-      lc.count = cc.count = r->cand_count + 1;
-      lc.cand_base = cc.cand_base = 0;
-      lc.n_tx = g.nsb * cg.comp;
-      cc.n_tx = g.nsb * cg.comp * ntx_c;
-      if (f4_pair && !r->rs2) {
-        RV_R(rv_rdo_candidates_pair(la4, ca4, lc, cc, g.hbd, xs));
+      if (f4_list && f4_pair && !r->rs2) {  // the pool over both lists
+        RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 2, 0, g.hbd, xs));
+      } else if (f4_pair && !r->rs2) {
+        RV_R(rv_rdo_candidates_pair(la4, ca4, lc4, cc4, g.hbd, xs));
       } else {
         RV_R(rv_rdo_candidates(la4, ca4, g.hbd, xs));
-        RV_R(rv_rdo_candidates(lc, cc, g.hbd, x2, true));
+        RV_R(rv_rdo_candidates(lc4, cc4, g.hbd, x2, true));
       }
+    } else if (f4_list) {
+      RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 1, 0, g.hbd, xs));
     } else {
       RV_R(rv_rdo_candidates(la4, ca4, g.hbd, xs));
     }
