@@ -370,6 +370,41 @@ int rv_cdef_filter_plane(const rv_plane *src, const rv_plane *dst, int pli, int 
                          const uint8_t *y_strengths, const uint8_t *uv_strengths, int damping,
                          int bit_depth, void *stream);
 
+/* ---- loop restoration (src/lrf.rs) --------------------------------------
+ * The frame's restoration runs inside the replay (RV_REPLAY_LRF).  This
+ * entry runs one stripe through the same device code as lrf_filter_frame's
+ * kernel: setup_integral_image's view of the stripe at (x0, y0), sw x sh
+ * pixels (sh <= 64) of a cw x ch crop (cd inside the stripe, db outside its
+ * rows, clamped), then sgrproj_stripe_filter (src/lrf.rs:677-760) with set
+ * `set` and xqd (xqd0, xqd1), into d_out (u8 / u16, row pitch sw). */
+int rv_lrf_stripe_filter(const rv_plane *cd, const rv_plane *db, int x0, int y0, int sw, int sh,
+                         int cw, int ch, int set, int xqd0, int xqd1, int bit_depth, void *d_out,
+                         void *stream);
+
+/* ---- stream containers ---------------------------------
+ * The y4m input rav1e reads (src/bin/decoder/y4m.rs through the y4m crate)
+ * and the IVF file it writes (ivf/src/lib.rs:6-30).  Host code.
+ * rv_y4m_read_frame reads the next frame's planar samples (Y, then U, V;
+ * 16-bit little endian above 8 bits: the packed layout rv_replay_set_input
+ * takes, rv_y4m_frame_bytes of them) and returns RV_OK, or 1 at the end of
+ * the stream. */
+typedef struct rv_y4m_info {
+  int width, height, bit_depth, xdec, ydec, fps_num, fps_den;
+} rv_y4m_info;
+typedef struct rv_y4m rv_y4m;
+typedef struct rv_ivf rv_ivf;
+int rv_y4m_parse_header(const char *line, rv_y4m_info *out);
+rv_y4m *rv_y4m_open(const char *path);
+int rv_y4m_get_info(const rv_y4m *y, rv_y4m_info *out);
+size_t rv_y4m_frame_bytes(const rv_y4m *y);
+int rv_y4m_read_frame(rv_y4m *y, void *host_yuv);
+void rv_y4m_close(rv_y4m *y);
+/* write_ivf_header (version 0, header size 32, "AV01", width, height,
+ * framerate num / den), then write_ivf_frame per frame (length, pts, bytes). */
+rv_ivf *rv_ivf_create(const char *path, int width, int height, int fps_num, int fps_den);
+int rv_ivf_write_frame(rv_ivf *v, uint64_t pts, const uint8_t *data, size_t len);
+int rv_ivf_close(rv_ivf *v);
+
 /* ---- entropy coding (src/ec.rs, src/context.rs) -------------------------
  * Coefficient coding = ContextWriter::write_coeffs_lv_map (src/context.rs:
  * 3965-4220) for square transforms (TX_4X4 .. TX_64X64, the sizes the
@@ -830,6 +865,13 @@ int rv_replay_kernel_probe(rv_replay *r, double *out, int cap);
  * out[20] the frames whose lookahead those rounds ran (the engine runs up to
  * W frames ahead of the encode).  Returns the count. */
 int rv_replay_counters(rv_replay *r, uint64_t *out, int cap);
+
+/* The replay's DPB: reconstructions (and their saved motion fields) live in
+ * slot display % rv_replay_dpb_slots().  A frame that reuses a slot must
+ * follow every frame that reads the slot's previous occupant (display -
+ * slots); instances coding frames concurrently (PipelinedReplay) order
+ * themselves by it. */
+int rv_replay_dpb_slots(void);
 
 /* ---------------------------------------------------------------------
  * Layer 1: drop-in asm-shaped entry points.  Signatures = the reference's

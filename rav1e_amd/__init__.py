@@ -257,6 +257,16 @@ def _declare(L):
         "rv_deblock_sse": (i32, [P, P, i32, i32, vp, vp, i32, vp, vp, i32, vp]),
         "rv_deblock_frame": (i32, [P, i32, i32, vp, vp, i32, vp, i32, vp]),
         "rv_cdef_find_dirs": (i32, [P, i32, i32, vp, i32, vp, vp, i32, vp]),
+        "rv_lrf_stripe_filter": (i32, [P, P] + [i32] * 10 + [vp, vp]),
+        "rv_y4m_parse_header": (i32, [C.c_char_p, vp]),
+        "rv_y4m_open": (vp, [C.c_char_p]),
+        "rv_y4m_get_info": (i32, [vp, vp]),
+        "rv_y4m_frame_bytes": (sz, [vp]),
+        "rv_y4m_read_frame": (i32, [vp, vp]),
+        "rv_y4m_close": (None, [vp]),
+        "rv_ivf_create": (vp, [C.c_char_p, i32, i32, i32, i32]),
+        "rv_ivf_write_frame": (i32, [vp, C.c_uint64, vp, sz]),
+        "rv_ivf_close": (i32, [vp]),
         "rv_cdef_filter_plane": (i32, [P, P, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, i32, i32,
                                        vp]),
         "rv_prep_8tap_batch": (i32, [vp, P, vp, i32, i32, i32, i32, i32, i32, vp]),
@@ -300,6 +310,7 @@ def _declare(L):
         "rv_replay_stage_times": (i32, [vp, vp, i32]),
         "rv_replay_stage_times_sum": (i32, [vp, i32, vp, i32]),
         "rv_replay_counters": (i32, [vp, vp, i32]),
+        "rv_replay_dpb_slots": (i32, []),
         "rv_replay_set_kernel_probe": (i32, [vp, i32]),
         "rv_replay_kernel_probe": (i32, [vp, vp, i32]),
         "rv_round_ring_slots": (i32, [C.c_uint32, vp, i32]),
@@ -682,6 +693,88 @@ def cdef_filter_frame(src, dst, width, height, skip: np.ndarray, cdef_index: np.
     _sync(stream)
     return (dd.download(np.uint8).reshape(rows8, cols8),
             dv.download(np.int32).reshape(rows8, cols8))
+
+
+def lrf_stripe_filter(cd, db, x0, y0, sw, sh, cw, ch, set_, xqd, bit_depth=8, stream=None):
+    """One stripe through the device's loop-restoration filter code
+    (lrf_filter_frame's chunk body): setup_integral_image's view of the
+    sw x sh stripe at (x0, y0) of a cw x ch crop of DevicePlanes cd (the
+    CDEF output) / db (the deblocked frame, outside the stripe's rows), then
+    sgrproj_stripe_filter (src/lrf.rs:677-760) with set `set_` and xqd.
+    Returns the restored stripe (sh x sw)."""
+    hbd = cd.desc.hbd
+    out = DeviceBuffer(sw * sh * (2 if hbd else 1))
+    _check(lib().rv_lrf_stripe_filter(C.byref(cd.desc), C.byref(db.desc), x0, y0, sw, sh, cw, ch,
+                                      set_, int(xqd[0]), int(xqd[1]), bit_depth, out.ptr, stream),
+           "rv_lrf_stripe_filter")
+    _sync(stream)
+    return out.download(np.uint16 if hbd else np.uint8).reshape(sh, sw)
+
+
+# ---- stream containers: y4m input, IVF output (rv_container.hip) -----------
+class Y4mInfo(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ("width", "height", "bit_depth", "xdec", "ydec", "fps_num",
+                                       "fps_den")]
+
+
+class Y4mReader:
+    """A y4m stream (the input rav1e's CLI reads, src/bin/decoder/y4m.rs):
+    `info` (width, height, bit depth, chroma decimation, frame rate) and
+    read_frame() -> the frame's packed planar samples (Y, U, V; the layout
+    HipReplay.set_input takes), or None at the end of the stream."""
+
+    def __init__(self, path):
+        self.h = lib().rv_y4m_open(os.fsencode(path))
+        if not self.h:
+            raise Rav1eHipError(f"rv_y4m_open failed: {lib().rv_last_error().decode()}")
+        self.info = Y4mInfo()
+        _check(lib().rv_y4m_get_info(self.h, C.byref(self.info)), "rv_y4m_get_info")
+        self.nbytes = int(lib().rv_y4m_frame_bytes(self.h))
+
+    def read_frame(self):
+        hbd = self.info.bit_depth > 8
+        out = np.empty(self.nbytes // (2 if hbd else 1), np.uint16 if hbd else np.uint8)
+        rc = lib().rv_y4m_read_frame(self.h, out.ctypes.data)
+        if rc == 1:
+            return None
+        _check(rc, "rv_y4m_read_frame")
+        return out
+
+    def close(self):
+        if self.h:
+            lib().rv_y4m_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class IvfWriter:
+    """An IVF file (ivf/src/lib.rs write_ivf_header / write_ivf_frame)."""
+
+    def __init__(self, path, width, height, fps_num=30, fps_den=1):
+        self.h = lib().rv_ivf_create(os.fsencode(path), width, height, fps_num, fps_den)
+        if not self.h:
+            raise Rav1eHipError(f"rv_ivf_create failed: {lib().rv_last_error().decode()}")
+
+    def write_frame(self, pts, data: bytes):
+        buf = np.frombuffer(bytes(data), np.uint8)
+        _check(lib().rv_ivf_write_frame(self.h, int(pts), buf.ctypes.data if len(buf) else None,
+                                        len(buf)), "rv_ivf_write_frame")
+
+    def close(self):
+        if self.h:
+            _check(lib().rv_ivf_close(self.h), "rv_ivf_close")
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 # ---- entropy coding (src/ec.rs, src/context.rs write_coeffs_lv_map) --------

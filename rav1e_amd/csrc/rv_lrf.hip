@@ -1715,6 +1715,45 @@ struct LrfFilterArgs {
   int nchunk[3], nstripe;  // 32-column chunks per plane row, stripes
 };
 
+// The restored chunk: columns x .. x + w - 1 (w <= 32) of the stripe at rows
+// y0 .. y0 + sz - 1 (sz <= 64) of a crop_w x crop_h plane, set `set`,
+// weights (w0, w1) = xqd, into op (row pitch ostride) -- lrf_filter_kernel's
+// body, shared with the golden-stripe test kernel.
+template <typename Px>
+__device__ __forceinline__ void lrf_filter_chunk(SgrLds<32, 64> &L, uint16_t *blk, const rv_plane &cd,
+                                                 const rv_plane &db, int x, int w, int y0, int sz,
+                                                 int crop_w, int crop_h, int set, int w0, int w1, int bd,
+                                                 Px *op, int64_t ostride) {
+  using L32 = SgrLds<32, 64>;
+  auto at = [](const rv_plane &pl, int xx, int yy) -> int {
+    return (int)((const Px *)pl.data)[(int64_t)(pl.yorigin + yy) * pl.stride + pl.xorigin + xx];
+  };
+  // setup_integral_image's view (VertPaddedIter / HorzPaddedIter): columns
+  // clamp to the frame (the unit's own right limit reaches 3 past it),
+  // rows to the frame and the stripe's +-2 extension, deblocked outside
+  const int sh = sz + (sz & 1), crop = crop_h;
+  sgr_init_xz(L.xz);
+  sgr_integral<L32::IS, L32::IR>(L.ii, w, sz, [&](int r, int c) -> uint32_t {
+    const int cy = iclamp(y0 - 4 + r, 0, crop - 1), ly = iclamp(cy, y0 - 2, y0 + sh + 1);
+    const int xx = iclamp(x - 4 + c, 0, crop_w - 1);
+    return (uint32_t)((ly >= y0 && ly < y0 + sh) ? at(cd, xx, ly) : at(db, xx, ly));
+  });
+  for (int i = threadIdx.x; i < w * sz; i += blockDim.x) {
+    const int yy = i / w, xx = i - yy * w;
+    blk[yy * 32 + xx] = (uint16_t)at(cd, x + xx, y0 + yy);
+  }
+  sgr_tables<L32::IS, L32::IR, L32::AS, L32::A1R>(L.ii, L.tab, L.xz, sgr_lane(w), set, sz, bd - 8);
+  __syncthreads();
+  const int mx = (1 << bd) - 1;
+  for (int i = threadIdx.x; i < w * sz; i += blockDim.x) {
+    const int yy = i / w, xx = i - yy * w;
+    const uint32_t px = blk[yy * 32 + xx], px0 = blk[(yy & ~1) * 32 + xx];
+    uint32_t f2, f1;
+    sgr_f<L32::AS, L32::A1R>(L.tab, set, xx, yy, px, px0, f2, f1);
+    op[(int64_t)yy * ostride + xx] = (Px)sgr_out(f2, f1, px, w0, w1, mx);
+  }
+}
+
 template <typename Px>
 __global__ __launch_bounds__(256) void lrf_filter_kernel(LrfFilterArgs a) {
   using L32 = SgrLds<32, 64>;
@@ -1750,31 +1789,25 @@ __global__ __launch_bounds__(256) void lrf_filter_kernel(LrfFilterArgs a) {
     }
     return;
   }
-  // setup_integral_image's view (VertPaddedIter / HorzPaddedIter): columns
-  // clamp to the frame (the unit's own right limit reaches 3 past it),
-  // rows to the frame and the stripe's +-2 extension, deblocked outside
-  const int sh = sz + (sz & 1), crop = crop_h;
-  sgr_init_xz(L.xz);
-  sgr_integral<L32::IS, L32::IR>(L.ii, w, sz, [&](int r, int c) -> uint32_t {
-    const int cy = iclamp(y0 - 4 + r, 0, crop - 1), ly = iclamp(cy, y0 - 2, y0 + sh + 1);
-    const int xx = iclamp(x - 4 + c, 0, crop_w - 1);
-    return (uint32_t)((ly >= y0 && ly < y0 + sh) ? at(cd, xx, ly) : at(db, xx, ly));
-  });
-  for (int i = threadIdx.x; i < w * sz; i += blockDim.x) {
-    const int yy = i / w, xx = i - yy * w;
-    blk[yy * 32 + xx] = (uint16_t)at(cd, x + xx, y0 + yy);
-  }
-  const int set = u[0];
-  sgr_tables<L32::IS, L32::IR, L32::AS, L32::A1R>(L.ii, L.tab, L.xz, sgr_lane(w), set, sz, g.bd - 8);
-  __syncthreads();
-  const int mx = (1 << g.bd) - 1;
-  for (int i = threadIdx.x; i < w * sz; i += blockDim.x) {
-    const int yy = i / w, xx = i - yy * w;
-    const uint32_t px = blk[yy * 32 + xx], px0 = blk[(yy & ~1) * 32 + xx];
-    uint32_t f2, f1;
-    sgr_f<L32::AS, L32::A1R>(L.tab, set, xx, yy, px, px0, f2, f1);
-    op[(int64_t)yy * out.stride + xx] = (Px)sgr_out(f2, f1, px, u[1], u[2], mx);
-  }
+  lrf_filter_chunk<Px>(L, blk, cd, db, x, w, y0, sz, crop_w, crop_h, u[0], u[1], u[2], g.bd, op,
+                       out.stride);
+}
+
+// One golden stripe (tests/golden/ref_lrf.npz, rv_lrf_stripe_filter): the
+// stripe at (x0, y0) of sw x sz pixels inside a cw x ch crop, restored with
+// set `set` and weights (w0, w1) by the product's chunk code, 32 columns per
+// workgroup, into out (row pitch sw).
+template <typename Px>
+__global__ __launch_bounds__(256) void lrf_stripe_case_kernel(rv_plane cd, rv_plane db, int x0, int y0,
+                                                               int sw, int sz, int cw, int ch, int set,
+                                                               int w0, int w1, int bd, Px *out) {
+  using L32 = SgrLds<32, 64>;
+  __shared__ L32 L;
+  __shared__ uint16_t blk[64 * 32];
+  const int c = (int)blockIdx.x * 32;
+  if (c >= sw) return;
+  lrf_filter_chunk<Px>(L, blk, cd, db, x0 + c, min(32, sw - c), y0, sz, cw, ch, set, w0, w1, bd,
+                       out + c, sw);
 }
 
 }  // namespace
@@ -1949,6 +1982,28 @@ int lrf_filter_launch(const rv_plane cd[3], const rv_plane db[3], const rv_plane
     lrf_filter_kernel<uint16_t><<<grid, 256, 0, s>>>(a);
   else
     lrf_filter_kernel<uint8_t><<<grid, 256, 0, s>>>(a);
+  RV_HIP_CHECK_LAUNCH();
+  return RV_OK;
+}
+
+// One stripe of the golden loop-restoration vectors through the device's
+// filter code (lrf_filter_kernel's chunk body): tests/test_lrf.py -m gpu.
+extern "C" int rv_lrf_stripe_filter(const rv_plane *cd, const rv_plane *db, int x0, int y0, int sw,
+                                    int sh, int cw, int ch, int set, int xqd0, int xqd1, int bit_depth,
+                                    void *d_out, void *stream) {
+  if (!cd || !db || !d_out || cd->hbd != db->hbd || sw < 1 || sw > 256 || sh < 1 || sh > 64 ||
+      set < 0 || set > 15 || x0 < 0 || y0 < 0 || x0 + sw > cw || y0 + sh > ch || cw > cd->width ||
+      ch > cd->height || cw > db->width || ch > db->height ||
+      (bit_depth != 8 && bit_depth != 10 && bit_depth != 12) || (!cd->hbd && bit_depth != 8))
+    return rv_set_error(RV_EINVAL, "rv_lrf_stripe_filter: bad arguments");
+  hipStream_t s = rv_resolve_stream(stream);
+  const unsigned grid = (unsigned)((sw + 31) / 32);
+  if (cd->hbd)
+    lrf_stripe_case_kernel<uint16_t><<<grid, 256, 0, s>>>(*cd, *db, x0, y0, sw, sh, cw, ch, set, xqd0, xqd1,
+                                                          bit_depth, (uint16_t *)d_out);
+  else
+    lrf_stripe_case_kernel<uint8_t><<<grid, 256, 0, s>>>(*cd, *db, x0, y0, sw, sh, cw, ch, set, xqd0, xqd1,
+                                                         bit_depth, (uint8_t *)d_out);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

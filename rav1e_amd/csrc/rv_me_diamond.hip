@@ -116,7 +116,7 @@ struct DsArgs {
   // list-driven rounds: a listed job with dirty[job] == 0 keeps its result
   // (its inputs did not change; null: every listed job runs)
   const uint8_t *dirty;
-  // list-driven: the workgroup pool (0: kDsListGrid; a round expected to
+  // list-driven: the workgroup pool (0: ds_list_grid(); a round expected to
   // list most jobs, e.g. the first after round 0, asks for a full grid)
   int list_grid;
 };
@@ -136,7 +136,16 @@ __device__ __forceinline__ int ds_list_job(const DsArgs &a, int ord) {
 // Workgroups of a list-driven launch: enough to cover a typical round's
 // superblocks at once, few enough that a near-empty round costs ~1 us of
 // dispatch (a full 4080-workgroup grid of early exits costs ~10 us).
-constexpr int kDsListGrid = 512;
+constexpr int kDsListGridDefault = 512;
+// RAV1E_HIP_DS_POOL (A/B): the list-driven launches' workgroup pool
+static int ds_list_grid() {
+  static const int g = [] {
+    const char *e = getenv("RAV1E_HIP_DS_POOL");
+    const int v = e ? atoi(e) : kDsListGridDefault;
+    return v > 0 ? v : kDsListGridDefault;
+  }();
+  return g;
+}
 
 __device__ __forceinline__ void ds_write(const DsArgs &a, int job, rv_mv center,
                                          uint64_t cost) {
@@ -1465,8 +1474,8 @@ bool try_grp(const DsArgs &a, hipStream_t s) {
   if (!(small || (a.satd && (n == 32 || n == 64)))) return false;
   const int jpw = 64 / (n == 8 || (n == 16 && !a.subpel && !a.satd) ? 16 : 64);
   unsigned grid = (unsigned)((a.n + 4 * jpw - 1) / (4 * jpw));
-  if (a.alist && grid > (unsigned)(a.list_grid ? a.list_grid : kDsListGrid))
-    grid = (unsigned)(a.list_grid ? a.list_grid : kDsListGrid);
+  if (a.alist && grid > (unsigned)(a.list_grid ? a.list_grid : ds_list_grid()))
+    grid = (unsigned)(a.list_grid ? a.list_grid : ds_list_grid());
 #define RV_GRP(N)                                                                     \
   if (n == N) {                                                                       \
     if (a.subpel) {                                                                   \
@@ -1501,7 +1510,7 @@ static bool ds_full_wave() {
 
 template <typename Px, int W, int H, bool SUB>
 void launch_fast(const DsArgs &a, hipStream_t s) {
-  const unsigned grid = a.alist ? (unsigned)std::min(a.n, a.list_grid ? a.list_grid : kDsListGrid)
+  const unsigned grid = a.alist ? (unsigned)std::min(a.n, a.list_grid ? a.list_grid : ds_list_grid())
                                  : (unsigned)((a.n + 7) / 8 * 8);
   static const bool occ4 = [] {
     const char *e = getenv("RAV1E_HIP_DS_OCC4");
@@ -1617,7 +1626,7 @@ static void ds_fill(DsArgs &a, const rv_plane *org, const rv_plane *refs, int n_
 
 // A round's list-driven F2 (16x16 full-pel SAD on the half-resolution
 // planes) and F3 full-pel (64x64 SAD) in one launch (ds_f2_f3_kernel);
-// pools of list_grid workgroups each (0: kDsListGrid).
+// pools of list_grid workgroups each (0: ds_list_grid()).
 int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_job *jobs_h,
                      rv_fs_result *out_h, const uint8_t *dirty_h, const rv_plane *org,
                      const rv_plane *refs, const rv_ds_job *jobs, rv_fs_result *out,
@@ -1632,7 +1641,7 @@ int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_
           dirty_h);
   ds_fill(f3, org, refs, n_refs, jobs, n_per_ref, 64, out, bit_depth, alist, acount, 1, dirty);
   if (next) f3.next = *next;
-  const int pool = list_grid ? list_grid : kDsListGrid;
+  const int pool = list_grid ? list_grid : ds_list_grid();
   const int g2 = std::min(pool, (f2.n + 15) / 16), g3 = std::min(f3.n, pool);
   hipStream_t s = rv_resolve_stream(stream);
   if (org->hbd)

@@ -84,10 +84,11 @@ int rv_rdo_blocks(const rv::RdoArgs &a, bool luma, int nplanes, int n_tx_size, i
 // The list-driven score launches on a pool of workgroups (rdo_quad_list_kernel):
 // the sets' arguments in device memory (rv_rdo_args_put, up to four: [luma,
 // chroma] of set A, then set B), nsets 1 (set A, MODE mode_a) or 2 (A single-
-// reference, B compound); h: the same arguments on the host (grid bound).
+// reference, B compound); h: the same arguments on the host (grid bound);
+// max_grid > 0 caps the pool (a round's expected work).
 int rv_rdo_args_put(const rv::RdoArgs *h, int n, rv::RdoArgs *dev, hipStream_t s);
 int rv_rdo_candidates_list(const rv::RdoArgs *h, const rv::RdoArgs *dev, int nsets, int mode_a,
-                           int hbd, hipStream_t s);
+                           int hbd, hipStream_t s, int max_grid = 0);
 
 // Intra chains of the 64x64 superblocks listed in luma.list (count): luma
 // TX_64X64 + chroma TX_32X32 (4:2:0), intra prediction from the edges in

@@ -1553,7 +1553,7 @@ int rv_rdo_args_put(const RdoArgs *h, int n, RdoArgs *dev, hipStream_t s) {
 }
 
 int rv_rdo_candidates_list(const RdoArgs *h, const RdoArgs *dev, int nsets, int mode_a, int hbd,
-                           hipStream_t s) {
+                           hipStream_t s, int max_grid) {
   if (!h || !dev || nsets < 1 || nsets > 2 || mode_a < 0 || mode_a > 1 || (nsets == 2 && mode_a) ||
       h[0].commit || h[0].bd == 12)
     return rv_set_error(RV_EINVAL, "rv_rdo_candidates_list: bad arguments");
@@ -1569,7 +1569,8 @@ int rv_rdo_candidates_list(const RdoArgs *h, const RdoArgs *dev, int nsets, int 
   for (int k = 0; k < nsets; k++)
     full += (unsigned)((h[2 * k].n_tx + 3) / 4) +
             (unsigned)(2 * ((h[2 * k + 1].n_tx + 1) / 2) + 2) / 3;
-  const unsigned grid = std::min(full, (unsigned)rdo_f4_pool());
+  unsigned grid = std::min(full, (unsigned)rdo_f4_pool());
+  if (max_grid > 0) grid = std::min(grid, (unsigned)max_grid);
   if (grid == 0) return RV_OK;
 #define RV_LIST(PX, MA, MB) rdo_quad_list_kernel<PX, MA, MB><<<grid, 256, 0, s>>>(dev, nsets, var)
   if (hbd) {

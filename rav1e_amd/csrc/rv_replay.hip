@@ -116,7 +116,12 @@ int rv_synth_frame(const rv_plane *y, const rv_plane *u, const rv_plane *v, int 
 namespace rv {
 
 constexpr int kSb = 64;
-constexpr int kSlots = 12;  // DPB slots, keyed by display index % 12
+// DPB slots, keyed by display index % kSlots.  24 (round 6; 12 before): the
+// reuse of a slot orders a level-0 frame after the level-2 frames that read
+// the slot's previous occupant, and with 12 slots that closed a cycle of
+// two groups (level 0 of g -> level 1 -> level 2 -> level 0 of g + 2) that
+// bounded the three pipelined instances; with 24 it spans five groups.
+constexpr int kSlots = 24;
 // result words per superblock and reference: coarse (mv, cost), the four
 // half-res quadrants, full-pel, sub-pel, the 16 lookahead 16x16 blocks
 constexpr int kWordsPerRef = 2 + 8 + 2 + 2 + 32 + 8;
@@ -986,6 +991,7 @@ struct RoundRing {
   uint32_t *ticket = nullptr;
   unsigned long long *h_pub = nullptr, *d_pub = nullptr;
   uint32_t seq = 0;
+  int last_count = -1;  // the run's last count the host read (-1: none yet)
   int32_t *slot(uint32_t q) const { return cnt + 2 * (q % kCnt); }
   // check q's publication (publish = false: counted, not published)
   RoundPub pub(uint32_t q, bool publish = true) const {
@@ -2753,6 +2759,7 @@ static int run_rounds(RoundRing &rr, hipStream_t xs, int budget, Check &&check, 
   static const int ahead = getenv("RAV1E_HIP_ROUNDS_AHEAD") ? atoi(getenv("RAV1E_HIP_ROUNDS_AHEAD"))
                                                             : rv_replay::kRoundsAhead;
   if (changed) *changed = false;
+  rr.last_count = -1;
   const uint32_t first = rr.seq++;
   RV_R(check(first));
   int queued = 0;  // evaluation rounds queued (round j evaluates check j - 1's list)
@@ -2779,6 +2786,7 @@ static int run_rounds(RoundRing &rr, hipStream_t xs, int budget, Check &&check, 
       }
     }
     const int c = (int)(uint32_t)v;
+    rr.last_count = c;
     if (mv_trace) fprintf(stderr, "%s frame %ld level %d check %d: %d\n", what, frame, level, seen, c);
     if (c == 0) return RV_OK;
     if (seen >= budget)
@@ -3928,7 +3936,21 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   static const bool f2_f3 = !(getenv("RAV1E_HIP_F2_F3") && getenv("RAV1E_HIP_F2_F3")[0] == '0');
   auto f3_f4_list = [&](hipStream_t xs, uint32_t q) -> int {
     const int32_t *acnt = slot_cnt(q);
-    const int lg = q == q_first ? nr * g.R : 0;
+    int lg = q == q_first ? nr * g.R : 0;
+    // A later round's grids from the last count the host read (a check one
+    // or two rounds back): twice that many superblocks, so the launches
+    // carry the live work and few empty workgroups (a round's fixed pools
+    // put ~12 k waves through the dispatcher for a few dozen superblocks).
+    // A list longer than the hint loops over the grid, so the hint only
+    // sizes, never decides.  RAV1E_HIP_ROUND_HINT=0: the fixed pools (A/B).
+    static const bool round_hint = !(getenv("RAV1E_HIP_ROUND_HINT") && getenv("RAV1E_HIP_ROUND_HINT")[0] == '0');
+    const int hint = q == q_first || !round_hint ? -1 : r->rr.last_count;
+    const int hsb = hint >= 0 ? std::max(2 * hint, 16) : 0;
+    int f4_grid = 0;
+    if (hsb) {
+      lg = std::min(hsb * g.R, 512);
+      f4_grid = std::min(6 * hsb, 1024);
+    }
     // the check's F2 / F3 sets came from the state before this round, so F2
     // and F3 are independent (F2's results feed the next check): F2 on the
     // second stream
@@ -3956,7 +3978,14 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                  r->sub, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 1,
                                  ma.f3dirty, lg, kp_acc, kp_ts()));
     RV_R(kp_close(xs));
-    round_lists_kernel<<<kRoundGrid, 256, 0, xs>>>(
+    // the pools of the small per-round kernels: kRoundGrid for a run's first
+    // round (most superblocks listed), RAV1E_HIP_ROUND_POOL (A/B) after it
+    static const int round_pool = getenv("RAV1E_HIP_ROUND_POOL") ? std::max(1, atoi(getenv("RAV1E_HIP_ROUND_POOL")))
+                                                                 : kRoundGrid;
+    const int rg = q == q_first ? kRoundGrid
+                   : hsb ? std::min(kRoundGrid, std::max((14 * hsb + 255) / 256, (hsb + 3) / 4))
+                         : round_pool;
+    round_lists_kernel<<<rg, 256, 0, xs>>>(
         cg, r->sub, nsingle, r->cand_list, r->cand_count, r->mv_list, acnt,
         CandKeys{r->cand_key, (uint32_t)(r->coded + 1), r->cand_reuse ? 1 : 0});
     if (r->rs2) {  // the lists are out: the compound F4 runs beside the single one
@@ -3969,7 +3998,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     // in one launch
     if (cg.comp) {
       if (f4_list && f4_pair && !r->rs2) {  // the pool over both lists
-        RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 2, 0, g.hbd, xs));
+        RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 2, 0, g.hbd, xs, f4_grid));
       } else if (f4_pair && !r->rs2) {
         RV_R(rv_rdo_candidates_pair(la4, ca4, lc4, cc4, g.hbd, xs));
       } else {
@@ -3977,7 +4006,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
         RV_R(rv_rdo_candidates(lc4, cc4, g.hbd, x2, true));
       }
     } else if (f4_list) {
-      RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 1, 0, g.hbd, xs));
+      RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 1, 0, g.hbd, xs, f4_grid));
     } else {
       RV_R(rv_rdo_candidates(la4, ca4, g.hbd, xs));
     }
@@ -3985,7 +4014,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       RV_H(hipEventRecord(r->ev_rjoin, x2));
       RV_H(hipStreamWaitEvent(xs, r->ev_rjoin, 0));
     }
-    score_wave_kernel<<<kRoundGrid, 256, 0, xs>>>(
+    score_wave_kernel<<<rg, 256, 0, xs>>>(
         g, cg, L.lambda, L.ds[1], L.ds[2], r->sub, r->l_out, r->c_out, r->c_out + nct * 3, ntx_c,
         r->win, r->coarse, r->half, r->full, r->look, r->half_l, r->words, r->cand_count, nullptr,
         nullptr, nullptr, r->mv_list, acnt, r->dec_lv[lv], 1);
@@ -4466,6 +4495,8 @@ int rv_replay_kernel_probe(rv_replay *r, double *out, int cap) {
 // frames summed, (cap >= 5) out[3] / out[4] the F4 single-reference /
 // compound RDO candidates of the 64x64 blocks, (cap >= 11, speed 6) out[5 +
 // 2 (l - 1)] / out[6 + 2 (l - 1)] those of the 32x32, 16x16, 8x8 blocks.
+int rv_replay_dpb_slots(void) { return kSlots; }
+
 int rv_replay_counters(rv_replay *r, uint64_t *out, int cap) {
   if (!r || !out || cap < 3) return rv_set_error(RV_EINVAL, "rv_replay_counters");
   const Geo &g = r->g;

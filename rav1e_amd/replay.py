@@ -672,7 +672,8 @@ class PipelinedReplay:
     twin the level-1 frames (4g+2), a second twin the level-2 frames 4g+3.
     Every frame waits, through device events, for the frames on the other
     instances it depends on: the producers of its references, and the
-    previous occupant of its DPB slot (display d - 12) with every frame that
+    previous occupant of its DPB slot (display d - rv_replay_dpb_slots())
+    with every frame that
     reads it.  The frames' results are the sequential ones."""
 
     def __init__(self, primary: "HipReplay", instances: int = None):
@@ -699,6 +700,9 @@ class PipelinedReplay:
                 self.hp_streams.append(st)
             self.inst.append(primary.twin(st))
         self.R = primary.cfg.n_refs
+        self.slots = int(lib().rv_replay_dpb_slots())
+        self.DEP_SPAN = self.slots + 8
+        assert self.EV_RING >= 2 * self.DEP_SPAN, (self.EV_RING, self.DEP_SPAN)
         self.n = 0
         self.err = None
         self.ev = [lib().rv_event_create() for _ in range(self.EV_RING)]
@@ -714,9 +718,9 @@ class PipelinedReplay:
             w.start()
 
     # device events, one per coded frame in flight: frame n records
-    # ev[n % EV_RING]; a frame waits for frames at most DEP_SPAN back
-    EV_RING = 64
-    DEP_SPAN = 20
+    # ev[n % EV_RING]; a frame waits for frames at most DEP_SPAN back (its
+    # references, and its DPB slot's previous occupant: slots + 8 covers it)
+    EV_RING = 128
 
     def instance_of(self, n: int) -> int:
         if n == 0:
@@ -771,7 +775,7 @@ class PipelinedReplay:
             return []
         d = frame_info(n, self.R)["display"]
         deps = {_coded_of_display(r) for r in _refs_of(n, self.R)}
-        prev = d - 12  # the DPB slot's previous occupant and its readers
+        prev = d - self.slots  # the DPB slot's previous occupant and its readers
         if prev >= 0:
             c = _coded_of_display(prev)
             deps.add(c)

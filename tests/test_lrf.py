@@ -126,3 +126,29 @@ def test_lrf_rate_helpers():
     # a set with both radii: the symbol, 4 bits of set, two subexp codes
     r = L.orc_lrf_rate(O.ptr(cdf), O.ptr(ref), 0, O.ptr(np.array([-32, 31], np.int8)))
     assert r > bits[2] + 4 * 8
+
+
+@pytest.mark.gpu
+def test_gpu_lrf_stripe_filter_vs_reference():
+    """The device's loop-restoration filter code (lrf_filter_kernel's chunk
+    body, through rv_lrf_stripe_filter) on every stripe of the
+    reference-evaluated vectors: setup_integral_image's view and
+    sgrproj_stripe_filter at 8/10/12 bits, edge crops, odd heights, all 16
+    sets -- bit-exact against tests/golden/ref_lrf.npz, not through the
+    oracle."""
+    import rav1e_amd as R
+    R.require_device(0)
+    checked = 0
+    for g, n, k, pad in _cases():
+        bd, x0, y0, sw, sh, cw, ch, s, xq0, xq1 = (int(v) for v in g["cases"][k])
+        cd, db = (_px(g[a][n], bd) for a in ("cd", "db"))
+        # (cw, ch): what is left from (x0, y0) to the crop's edge; the
+        # device entry takes the crop itself
+        fw, fh = x0 + cw, y0 + ch
+        pc = R.DevicePlane.from_full(cd, pad, pad, fw, fh, bit_depth=bd)
+        pdb = R.DevicePlane.from_full(db, pad, pad, fw, fh, bit_depth=bd)
+        out = R.lrf_stripe_filter(pc, pdb, x0, y0, sw, sh, fw, fh, s, (xq0, xq1), bd)
+        np.testing.assert_array_equal(out.ravel().astype(np.uint16), g["filt"][k][:sw * sh],
+                                      err_msg=str(g["cases"][k]))
+        checked += 1
+    assert checked >= 21

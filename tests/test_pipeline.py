@@ -16,7 +16,8 @@ from rav1e_amd import replay as RP
 
 
 class _FakeLib:
-    def __init__(self):
+    def __init__(self, slots=24):
+        self.slots = slots  # rv_replay_dpb_slots
         self.lock = threading.Lock()
         self.events = {}   # handle -> the coded frame last recorded into it
         self.errors = []
@@ -31,6 +32,9 @@ class _FakeLib:
 
     def rv_event_destroy(self, h):
         return 0
+
+    def rv_replay_dpb_slots(self):
+        return self.slots
 
     def rv_event_record(self, ev, stream):
         with self.lock:
@@ -81,9 +85,9 @@ class _FakeInst:
         pass
 
 
-@pytest.mark.parametrize("seed", [1, 2])
-def test_pipelined_schedule_long_stream(monkeypatch, seed):
-    fake = _FakeLib()
+@pytest.mark.parametrize("seed,slots", [(1, 24), (2, 24), (3, 12)])
+def test_pipelined_schedule_long_stream(monkeypatch, seed, slots):
+    fake = _FakeLib(slots)
     monkeypatch.setattr(RP, "lib", lambda: fake)
     monkeypatch.setattr(RP, "_check", lambda rc, what: None)
     rnd = random.Random(seed)
