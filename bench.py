@@ -137,8 +137,8 @@ ROCPROF_NAMES = {
     "full_search": "fs16_sea_kernel_{pxs}",
     "diamond_fullpel_64": "ds_fast_kernel<{px}, 64, 64, false>",
     "diamond_subpel_64": "ds_fast_kernel<{px}, 64, 64, true>",
-    "rdo_candidates": "rdo_quad_kernel<{px}, 0>",
-    "rdo_compound": "rdo_quad_kernel<{px}, 1>",
+    "rdo_candidates": "rdo_quad_list_kernel<{px}, 0, 0>",
+    "rdo_compound": "rdo_quad_list_kernel<{px}, 1, 1>",
     "rdo_commit": "rdo_quad_kernel<{px}, 2>",
 }
 
@@ -648,15 +648,58 @@ def main():
                "source": pj["source"]}
         return v, lim
 
+    def family_entry(sub):
+        """Every instance of a kernel in the committed trace (template
+        instances are traced as separate names) aggregated per coded frame:
+        ms, launches, mean launch, and HBM bytes / SQ ratios weighted by
+        launches."""
+        if not pj:
+            return None
+        es = [v for k, v in pj["kernels"].items() if sub in k]
+        if not es:
+            return None
+        lpf = sum(e["launches_per_frame"] for e in es)
+        mpf = sum(e["ms_per_frame"] for e in es)
+        out = {"ms_per_frame": round(mpf, 4), "launches_per_frame": round(lpf, 3),
+               "avg_us": round(mpf * 1e3 / lpf, 3), "instances": len(es)}
+        if all(e.get("hbm_bytes_per_launch") for e in es):
+            out["hbm_bytes_per_launch"] = round(sum(e["hbm_bytes_per_launch"] * e["launches_per_frame"]
+                                                    for e in es) / lpf)
+        if all(e.get("sq") for e in es):
+            w = [e["launches_per_frame"] / lpf for e in es]
+            out["sq"] = {k: round(sum(wi * e["sq"][k] for wi, e in zip(w, es)), 4)
+                         for k in ("wait_any_over_wave_cycles", "active_inst_over_wave_cycles",
+                                   "valu_insts_per_launch", "waves_per_launch")}
+        return out
+
+    def attach_trace(roof, te, bytes_l, avg_s, ach):
+        if not te:
+            return
+        roof["trace"] = {"source": pj["source"], "git": pj["git"], "avg_us": te["avg_us"],
+                         "launches_per_frame": te["launches_per_frame"],
+                         "ms_per_frame": te["ms_per_frame"],
+                         "frac_from_trace": round(bytes_l / (te["avg_us"] * 1e-6) / 1e9 /
+                                                  HBM_PEAK_GBS, 5),
+                         "live_over_trace_duration": round(avg_s * 1e6 / te["avg_us"], 3)}
+        if te.get("instances"):
+            roof["trace"]["instances_aggregated"] = te["instances"]
+        if te.get("hbm_bytes_per_launch"):
+            roof["traffic"] = {"bytes_per_launch": te["hbm_bytes_per_launch"],
+                               "source": pj["source"], "git": pj["git"],
+                               "over_algorithmic": round(te["hbm_bytes_per_launch"] / bytes_l, 3),
+                               "rule": pj.get("hbm_bytes_rule")}
+        v, lim = valu_of(te, avg_s, round(ach / HBM_PEAK_GBS, 5))
+        if v:
+            roof["valu"], roof["limiter"] = v, lim
+
+    roofs = {}
     if kp is not None and kp[0] > 0:
-        # The dominant kernel of the committed trace (ms per frame over all its
-        # launches): ds_fast_kernel<64, 64, sub-pel>, F3's sub-pel search -- the
-        # batched MC + distortion kernel north_star names (every candidate a
-        # 6-tap put_8tap of its 71 x 71 window, then SAD against the source).
+        # F3's sub-pel search, ds_fast_kernel<64, 64, sub-pel>: the batched MC +
+        # distortion kernel north_star names (every candidate a 6-tap
+        # put_8tap of its 71 x 71 window, then SAD against the source).
         # Live: every launch of the instrumented timed frames (round 0 and the
         # MV-stack rounds) bracketed by HIP events on the stream it runs on;
         # its units: the candidate evaluations those launches counted.
-        dom = "diamond_subpel_64"
         nl = float(kp[0])
         # the launch's duration: its span on the device clock (the first
         # workgroup's start to the last one's end, what rocprofv3 times);
@@ -667,8 +710,8 @@ def main():
         cand_b = (71 * 71 + 64 * 64) * px + 4  # fused MC + dist candidate
         bytes_l = kp[2] / nl * cand_b
         ach = bytes_l / avg_s / 1e9
-        roof = {"kernel": dom, "name": f"ds_fast_kernel<{pxn}, 64, 64, true>", "bound": "hbm",
-                "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        roof = {"kernel": "diamond_subpel_64", "name": f"ds_fast_kernel<{pxn}, 64, 64, true>",
+                "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
                 "avg_launch_ms": round(avg_s * 1e3, 5),
                 "avg_launch_ms_hip_events": round(ev_s * 1e3, 5),
@@ -682,23 +725,60 @@ def main():
                 "launches_probed": int(nl),
                 "launch": "every F3 sub-pel launch (round 0 and the MV-stack rounds) of the "
                           "instrumented timed frames, HIP event pairs on its stream"}
-        te = trace_entry(dom)
-        if te:
-            roof["trace"] = {"source": pj["source"], "git": pj["git"], "avg_us": te["avg_us"],
-                             "launches_per_frame": te["launches_per_frame"],
-                             "ms_per_frame": te["ms_per_frame"],
-                             "frac_from_trace": round(bytes_l / (te["avg_us"] * 1e-6) / 1e9 /
-                                                      HBM_PEAK_GBS, 5),
-                             "live_over_trace_duration": round(avg_s * 1e6 / te["avg_us"], 3)}
-            if te.get("hbm_bytes_per_launch"):
-                roof["traffic"] = {"bytes_per_launch": te["hbm_bytes_per_launch"],
-                                   "source": pj["source"], "git": pj["git"],
-                                   "over_algorithmic": round(te["hbm_bytes_per_launch"] / bytes_l, 3),
-                                   "rule": pj.get("hbm_bytes_rule")}
-            v, lim = valu_of(te, avg_s, round(ach / HBM_PEAK_GBS, 5))
-            if v:
-                roof["valu"], roof["limiter"] = v, lim
-    else:
+        attach_trace(roof, family_entry(f"ds_fast_kernel<{pxn}, 64, 64, true>"), bytes_l, avg_s, ach)
+        roofs["diamond_subpel_64"] = roof
+    if kp is not None and len(kp) >= 12 and kp[5] > 0:
+        # F4, rdo_quad_list_kernel: every inter candidate's fused chain (MC,
+        # distortion, fht, quantise, rate, inverse, distortion) over the
+        # compacted lists, round 0's single-reference and compound launches
+        # and each MV-stack round's pair.  Units: the candidates and chroma
+        # transform blocks the launches counted (device-side, per launch).
+        nl = float(kp[5])
+        ev_s = kp[6] / nl / 1e3
+        avg_s = kp[7] / nl / 1e3 if kp[7] > 0 else ev_s
+        per = {"luma_single": (71 * 71 + 64 * 64) * px + 24,
+               "luma_compound": (2 * 71 * 71 + 64 * 64) * px + 24,
+               "chroma_single": (39 * 39 + 32 * 32) * px + 24,
+               "chroma_compound": (2 * 39 * 39 + 32 * 32) * px + 24}
+        # (the chroma counts are per plane: U and V each)
+        units = dict(zip(per, (kp[8], kp[9], 2 * kp[10], 2 * kp[11])))
+        bytes_l = sum(units[k] * per[k] for k in per) / nl
+        ach = bytes_l / avg_s / 1e9
+        roof = {"kernel": "rdo_candidates_list", "name": f"rdo_quad_list_kernel<{pxn}, *, *>",
+                "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                "avg_launch_ms": round(avg_s * 1e3, 5),
+                "avg_launch_ms_hip_events": round(ev_s * 1e3, 5),
+                "duration": "device clock (wall_clock64) span of every probed launch: first "
+                            "workgroup start to last workgroup end; HIP event pairs on the "
+                            "launch's stream beside it",
+                "algorithmic_bytes_per_launch": round(bytes_l),
+                "per_unit": {"unit": "candidate transform block (its MC window(s) + source + 3 "
+                                     "result words)", "bytes": per,
+                             "rule": "luma (64+7)^2 b window (two for compound) + 64^2 b source "
+                                     "+ 24; chroma per 32x32 block the same at 32 (SURVEY.md §8d: "
+                                     "fused MC + distortion candidate)"},
+                "units_per_launch": {k: round(v / nl, 1) for k, v in units.items()},
+                "launches_probed": int(nl),
+                "launch": "every F4 list launch (round 0's single and compound, each MV-stack "
+                          "round's pair) of the instrumented timed frames"}
+        attach_trace(roof, family_entry(f"rdo_quad_list_kernel<{pxn}"), bytes_l, avg_s, ach)
+        roofs["rdo_candidates_list"] = roof
+    if roofs:
+        # the line prices the kernel with the most milliseconds per frame in
+        # the committed trace (every template instance of a kernel summed:
+        # rocprofv3 names them apart), or live when there is no trace
+        def weight(r):
+            t = r.get("trace")
+            return t["ms_per_frame"] if t else r["avg_launch_ms"] * r["launches_probed"]
+        order = sorted(roofs.values(), key=weight, reverse=True)
+        roof = dict(order[0])
+        roof["chosen_by"] = ("the most ms per coded frame in the committed trace (all template "
+                             "instances of the kernel)" if "trace" in roof else
+                             "the most probed ms (no committed trace)")
+        if len(order) > 1:
+            roof["other"] = order[1]
+    if not roofs:
         # no probe (speed 6, several ranks): the frame's full F4 evaluation
         # (round 0), from its HIP-event stage span
         dom = "rdo_candidates" if kernels["rdo_candidates"]["bytes"] > 0 else \
@@ -771,6 +851,15 @@ def main():
                        **({"partition": "64x64 .. 8x8 top-down NONE vs SPLIT, every level "
                                         "searched and scored"} if speed == 6 else {})},
             "mpix_per_s": round(fps * W * H / 1e6, 3),
+            "inputs": {"residency": "every input frame is generated in HBM (rv_replay_synth_inputs) "
+                                    "before the timed region; the timed region moves no pixels "
+                                    "over PCIe",
+                       "upload_bytes_per_frame": int(W * H * px + 2 * ((W + xdec) >> xdec) *
+                                                     ((H + ydec) >> ydec) * px),
+                       "note": "a streaming encoder would upload that many bytes per frame "
+                               "(rv_replay_set_input; ~0.3 ms at 2160p 8-bit over a ~40 GB/s "
+                               "host link), overlappable with the lookahead engine's W-frame "
+                               "lead; not measured here"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,

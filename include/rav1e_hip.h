@@ -821,16 +821,21 @@ int rv_replay_stage_times(rv_replay *r, float *ms_out, int cap);
  * (<= 64). */
 int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out,
                               int cap);
-/* Kernel probe for the bench's roofline: with on != 0, every F3 sub-pel
+/* Kernel probes for the bench's roofline: with on != 0, every F3 sub-pel
  * launch (ds_fast_kernel, 64x64, speed 10: round 0 and the MV-stack rounds)
- * of an instrumented frame (rv_replay_set_timing) is bracketed by a HIP
- * event pair on the stream it runs on and adds its candidate evaluations
- * and jobs to a device counter.  (Re)starting drops the sums so far.
- * rv_replay_kernel_probe: out[0] launches, out[1] their summed ms (event
- * pairs), out[2] candidate evaluations, out[3] jobs since the last start,
- * (cap >= 5) out[4] the launches' summed ms on the device clock (first
- * workgroup's start to last workgroup's end, wall_clock64); returns the
- * count written; waits for the launches. */
+ * and every F4 candidate-list launch (rdo_quad_list_kernel: round 0's single
+ * and compound launches, each round's pair) of an instrumented frame
+ * (rv_replay_set_timing) is bracketed by a HIP event pair on the stream it
+ * runs on and adds its units to device counters.  (Re)starting drops the
+ * sums so far.  rv_replay_kernel_probe: out[0] F3 sub-pel launches, out[1]
+ * their summed ms (event pairs), out[2] candidate evaluations, out[3] jobs
+ * since the last start, (cap >= 5) out[4] the launches' summed ms on the
+ * device clock (first workgroup's start to last workgroup's end,
+ * wall_clock64); (cap >= 12) out[5] F4 list launches, out[6] their event
+ * ms, out[7] their device-clock ms, out[8] / out[9] single-reference /
+ * compound luma candidates, out[10] / out[11] single-reference / compound
+ * chroma transform blocks.  Returns the count written; waits for the
+ * launches. */
 int rv_replay_set_kernel_probe(rv_replay *r, int on);
 /* Host-only test hook (no device call): the slots the round ring gives
  * round check q -- out[0] its device count slot, out[1] the slot it zeroes

@@ -459,8 +459,12 @@ __device__ inline void ec_sb_of(const EcFrameArgs &a, int i, int &sx, int &sy, i
 }
 
 // The jobs of superblock i (coding order): count (out == nullptr) or write
-// them from out[0].  Leaves in z-order by a depth-first walk of the block
-// map (a 64x64 leaf costs one read).
+// them from out[0].  Leaves in z-order: a walk over the superblock's 8x8
+// cells in z-order (the depth-first order of the partition tree) that reads
+// the block map's leaf size at a cell and, at a leaf's top-left cell, emits
+// the leaf and steps over its cells (a 64x64 leaf costs one read).  No
+// stack: the explicit depth-first stack it replaces was indexed at run time
+// and lived in scratch memory (208 B per lane).
 __device__ int ec_sb_jobs(const EcFrameArgs &a, int i, rv_ec_job *out, int cap) {
   int sx, sy, t, first, rowstart, t0x, t0y;
   ec_sb_of(a, i, sx, sy, t, first, rowstart, t0x, t0y);
@@ -482,28 +486,22 @@ __device__ int ec_sb_jobs(const EcFrameArgs &a, int i, rv_ec_job *out, int cap) 
     put(j2);
   }
   const int sb = (sy - a.ty0) * a.tw + (sx - a.tx0);
-  int stk[16][3];
-  int sp = 0;
-  stk[sp][0] = sx * 16;
-  stk[sp][1] = sy * 16;
-  stk[sp][2] = 6;
-  sp++;
-  while (sp > 0) {
-    sp--;
-    const int x4 = stk[sp][0], y4 = stk[sp][1], lg = stk[sp][2];
-    if (x4 >= a.mi_cols || y4 >= a.mi_rows) continue;
-    const int code = a.mi_lg[(size_t)y4 * a.mi_stride + x4];
-    if (code != lg - 2) {  // split: the children, popped in z-order
-      const int h = 1 << (lg - 3);
-      for (int c = 3; c >= 0; c--) {
-        stk[sp][0] = x4 + (c & 1) * h;
-        stk[sp][1] = y4 + (c >> 1) * h;
-        stk[sp][2] = lg - 1;
-        sp++;
-      }
+  for (int zc = 0; zc < 64;) {
+    // cell zc of the superblock in z-order: de-interleave its bits
+    const int cx = (zc & 1) | ((zc >> 1) & 2) | ((zc >> 2) & 4);
+    const int cy = ((zc >> 1) & 1) | ((zc >> 2) & 2) | ((zc >> 3) & 4);
+    const int x4 = sx * 16 + 2 * cx, y4 = sy * 16 + 2 * cy;
+    if (x4 >= a.mi_cols || y4 >= a.mi_rows) {  // outside the frame: no block starts here
+      zc++;
       continue;
     }
-    const int n4 = 1 << code;
+    const int code = a.mi_lg[(size_t)y4 * a.mi_stride + x4];  // log2 of the leaf's 4x4 units
+    const int n4 = 1 << code, lg = code + 2;
+    if (((x4 | y4) & (n4 - 1)) != 0) {  // not the leaf's first cell (never for a consistent map)
+      zc++;
+      continue;
+    }
+    zc += (n4 >> 1) * (n4 >> 1);  // the leaf's cells
     rv_ec_job jb = z;
     jb.bx = x4 - t0x * 16;
     jb.by = y4 - t0y * 16;

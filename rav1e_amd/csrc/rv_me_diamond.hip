@@ -484,7 +484,7 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
     int ux = 1 << 30, uy = 1 << 30, ux2 = -(1 << 30), uy2 = -(1 << 30), any = 0;
 #pragma unroll
     for (int k = 0; k < kDsWaves; k++) {
-      q[k] = sub_pos(cands[k < n ? k : 0]);
+      q[k] = sub_pos(cands[k]);  // (every slot is set; ok masks k >= n)
       q[k].ok = q[k].ok && k < n && k != skip;
       if (q[k].ok) {
         any = 1;
@@ -502,7 +502,7 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
     for (int k = 1; k < kDsWaves; k++)
       if (wave == k) {
         me = q[k];
-        me_mv = cands[k < n ? k : 0];
+        me_mv = cands[k];
       }
     if (ux2 - ux <= S::D && uy2 - uy <= S::D) {
       // Re-stage only when a candidate leaves the staged window.  The last
@@ -927,24 +927,27 @@ __global__ __launch_bounds__(kDsThreads) void diamond_kernel(DsArgs a) {
         }
     }
   } else {
-    // get_best_predictor
+    // get_best_predictor (the predictors read through the job's pointer: a
+    // runtime index into the local copy kept it in scratch memory)
+    const rv_ds_job *jp = a.jobs + job;
     const int np = jb.n_pred < RV_DS_MAX_PRED ? jb.n_pred : RV_DS_MAX_PRED;
     for (int p = 0; p < np; p++) {
-      const uint64_t c = rd_cost(jb.pred[p]);
+      const rv_mv pm = jp->pred[p];
+      const uint64_t c = rd_cost(pm);
       if (c < center_cost) {
-        center = jb.pred[p];
+        center = pm;
         center_cost = c;
       }
     }
     int16_t radius = a.subpel ? 4 : 16;
     const int16_t radius_end = a.subpel ? (a.hp ? 1 : 2) : 8;
-    const int16_t pat[4][2] = {{1, 0}, {0, 1}, {-1, 0}, {0, -1}};
     for (int iter = 0; iter < 4096; iter++) {
       uint64_t best = ~0ull;
       rv_mv best_mv{0, 0};
       for (int p = 0; p < 4; p++) {
-        const rv_mv cand{(int16_t)(center.row + radius * pat[p][0]),
-                         (int16_t)(center.col + radius * pat[p][1])};
+        // diamond_pattern {(1, 0), (0, 1), (-1, 0), (0, -1)} without a table
+        const int dr = (p == 0) - (p == 2), dc = (p == 1) - (p == 3);
+        const rv_mv cand{(int16_t)(center.row + radius * dr), (int16_t)(center.col + radius * dc)};
         const uint64_t c = rd_cost(cand);
         if (c < best) {
           best = c;

@@ -157,19 +157,23 @@ __device__ inline int stack64(const Nb &nb, int rf0, int rf1, uint32_t sbias, in
         int cc = 0;
         if (idc0 > 0) { c00 = id0[0]; cc++; }
         if (idc0 > 1) { c10 = id0[1]; cc++; }
-        for (int i = 0; i < dfc0 && cc < 2; i++) {
-          if (cc == 0) c00 = df0[i]; else c10 = df0[i];
-          cc++;
-        }
+#pragma unroll
+        for (int i = 0; i < 2; i++)  // (static indices: no scratch)
+          if (i < dfc0 && cc < 2) {
+            if (cc == 0) c00 = df0[i]; else c10 = df0[i];
+            cc++;
+          }
       }
       {
         int cc = 0;
         if (idc1 > 0) { c01 = id1[0]; cc++; }
         if (idc1 > 1) { c11 = id1[1]; cc++; }
-        for (int i = 0; i < dfc1 && cc < 2; i++) {
-          if (cc == 0) c01 = df1[i]; else c11 = df1[i];
-          cc++;
-        }
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+          if (i < dfc1 && cc < 2) {
+            if (cc == 0) c01 = df1[i]; else c11 = df1[i];
+            cc++;
+          }
       }
       if (k.n == 1) {
         const bool same = mv_eq(c00, k.e[0].t) && mv_eq(c01, k.e[0].c);
@@ -229,7 +233,11 @@ __device__ inline MvStack stacks_of(const MvrefArgs &a, const Nb &nb, bool split
     s.s[k][0] = s.s[k][1] = rv_mv{0, 0};
   }
   Cand e0, e1;
-  for (int k = 0; k < a.R && !split; k++) {
+  // (every loop over the references runs to the stack's two slots with a
+  // compile-time index: a runtime one kept the MvStack in scratch memory)
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if (k >= a.R || split) continue;
     const int n = stack64(nb, 1 + k, kNoneFrame, a.sign_bias, fsx * 16, fsy * 16, a.w_in_b,
                           a.h_in_b, e0, e1);
     s.n[k] = n < 2 ? n : 2;
@@ -249,8 +257,10 @@ __device__ inline MvStack stacks_of(const MvrefArgs &a, const Nb &nb, bool split
 // the stacks a superblock was evaluated with still hold (never on the first round)
 __device__ inline bool same_stacks(const MvrefArgs &a, const MvStack &o, const MvStack &s) {
   bool same = !a.init;
-  for (int k = 0; k < a.R && same; k++)
-    same = o.n[k] == s.n[k] && mv_eq(o.s[k][0], s.s[k][0]) && mv_eq(o.s[k][1], s.s[k][1]);
+#pragma unroll
+  for (int k = 0; k < 2; k++)
+    if (k < a.R)
+      same = same && o.n[k] == s.n[k] && mv_eq(o.s[k][0], s.s[k][0]) && mv_eq(o.s[k][1], s.s[k][1]);
   if (a.comp && same)
     same = mv_eq(o.c[0][0], s.c[0][0]) && mv_eq(o.c[0][1], s.c[0][1]) &&
            mv_eq(o.c[1][0], s.c[1][0]) && mv_eq(o.c[1][1], s.c[1][1]);
@@ -260,7 +270,9 @@ __device__ inline bool same_stacks(const MvrefArgs &a, const MvStack &o, const M
 // (src/rdo.rs:858-870)
 __device__ inline void set_stacks(const MvrefArgs &a, int sb, const MvStack &s) {
   a.stk[sb] = s;
-  for (int k = 0; k < a.R; k++) {
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if (k >= a.R) continue;
     const int j = k * a.nsb + sb;
     a.jf[j].pmv[0] = a.js[j].pmv[0] = s.s[k][0];
     a.jf[j].pmv[1] = a.js[j].pmv[1] = s.s[k][1];
@@ -312,8 +324,13 @@ __device__ inline bool epzs_job_f(const MvrefArgs &a, int sb, int fsx, int fsy, 
   const int tsw = (mi_w + 15) / 16, tsh = (mi_h + 15) / 16;
   // [own, horizontal neighbour if any, vertical neighbour if any] in static slots
   const bool hh = (q & 1) ? tsx < tsw - 1 : tsx > 0, hv = (q >> 1) ? tsy < tsh - 1 : tsy > 0;
-  const rv_mv ch = hh ? coarse4(a, k, (q & 1) ? sb + 1 : sb - 1) : rv_mv{0, 0};
-  const rv_mv cv = hv ? coarse4(a, k, (q >> 1) ? sb + a.tw : sb - a.tw) : rv_mv{0, 0};
+  // the neighbours' loads from a valid index either way, then a select of
+  // the values (a select of the loads became a flat load through a pointer
+  // to a zero in scratch memory)
+  const rv_mv ch0 = coarse4(a, k, hh ? ((q & 1) ? sb + 1 : sb - 1) : sb);
+  const rv_mv cv0 = coarse4(a, k, hv ? ((q >> 1) ? sb + a.tw : sb - a.tw) : sb);
+  const rv_mv ch = hh ? ch0 : rv_mv{0, 0};
+  const rv_mv cv = hv ? cv0 : rv_mv{0, 0};
   const rv_mv cm[3] = {coarse4(a, k, sb), hh ? ch : cv, cv};
   const int nc = 1 + (int)hh + (int)hv;
   int bx = tsx * 16 + (q & 1) * 8, by = tsy * 16 + (q >> 1) * 8;
@@ -377,8 +394,10 @@ __global__ __launch_bounds__(256) void mvref_kernel(MvrefArgs a) {
       if (nb.tl) nb.d = coded_at(a, sb - a.tw - 1, X - 4, Y - 4);
       const MvStack s = stacks_of(a, nb, split, fsx, fsy);
       changed = !same_stacks(a, a.stk[sb], s);
-      for (int k = 0; k < a.R; k++)
-        if (a.init || !mv_eq(a.stk[sb].s[k][0], s.s[k][0]) || !mv_eq(a.stk[sb].s[k][1], s.s[k][1]))
+#pragma unroll
+      for (int k = 0; k < 2; k++)
+        if (k < a.R && (a.init || !mv_eq(a.stk[sb].s[k][0], s.s[k][0]) ||
+                        !mv_eq(a.stk[sb].s[k][1], s.s[k][1])))
           pmask |= 1u << k;
       if (changed) set_stacks(a, sb, s);  // (its pmv: the F3 jobs' rate predictors)
     } else if (a.epzs && j <= 5 * a.R) {
@@ -445,8 +464,10 @@ __global__ __launch_bounds__(1024) void mvref_split_kernel(MvrefArgs a) {
       const MvStack st = stacks_of(a, nb, split, fsx, fsy);
       changed = !same_stacks(a, a.stk[sb], st);
       uint32_t pmask = 0;
-      for (int k = 0; k < a.R; k++)
-        if (a.init || !mv_eq(a.stk[sb].s[k][0], st.s[k][0]) || !mv_eq(a.stk[sb].s[k][1], st.s[k][1]))
+#pragma unroll
+      for (int k = 0; k < 2; k++)
+        if (k < a.R && (a.init || !mv_eq(a.stk[sb].s[k][0], st.s[k][0]) ||
+                        !mv_eq(a.stk[sb].s[k][1], st.s[k][1])))
           pmask |= 1u << k;
       pmk[sbl] = pmask;
       if (changed) set_stacks(a, sb, st);
@@ -552,8 +573,10 @@ __global__ __launch_bounds__(kScanThreads) void mvref_scan_kernel(MvrefArgs a) {
       const MvStack st = stacks_of(a, nb, split, fsx, fsy);
       const bool mark = !same_stacks(a, a.stk[sb], st);
       uint32_t pm = 0;
-      for (int k = 0; k < a.R; k++)
-        if (!mv_eq(a.stk[sb].s[k][0], st.s[k][0]) || !mv_eq(a.stk[sb].s[k][1], st.s[k][1]))
+#pragma unroll
+      for (int k = 0; k < 2; k++)
+        if (k < a.R && (!mv_eq(a.stk[sb].s[k][0], st.s[k][0]) ||
+                        !mv_eq(a.stk[sb].s[k][1], st.s[k][1])))
           pm |= 1u << k;
       const BlkDec cur = a.dec[sb];
       if (mark) set_stacks(a, sb, st);

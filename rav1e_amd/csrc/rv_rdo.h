@@ -87,8 +87,13 @@ int rv_rdo_blocks(const rv::RdoArgs &a, bool luma, int nplanes, int n_tx_size, i
 // reference, B compound); h: the same arguments on the host (grid bound);
 // max_grid > 0 caps the pool (a round's expected work).
 int rv_rdo_args_put(const rv::RdoArgs *h, int n, rv::RdoArgs *dev, hipStream_t s);
+// kp_cnt / kp_t (the replay's kernel probe, may be null): the launch adds
+// its single / compound luma candidates and single / compound chroma
+// transform blocks into kp_cnt[0..3], and min / max's its workgroups'
+// device-clock start / end into kp_t[0] / kp_t[1].
 int rv_rdo_candidates_list(const rv::RdoArgs *h, const rv::RdoArgs *dev, int nsets, int mode_a,
-                           int hbd, hipStream_t s, int max_grid = 0);
+                           int hbd, hipStream_t s, int max_grid = 0, uint32_t *kp_cnt = nullptr,
+                           unsigned long long *kp_t = nullptr);
 
 // Intra chains of the 64x64 superblocks listed in luma.list (count): luma
 // TX_64X64 + chroma TX_32X32 (4:2:0), intra prediction from the edges in

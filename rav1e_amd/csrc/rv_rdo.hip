@@ -1317,12 +1317,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
 // addresses either: 52 B of scratch per lane instead of ~2 KB.
 template <typename Px, int MA, int MB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void rdo_quad_list_kernel(
-    const RdoArgs *__restrict__ A, int nsets, int var) {
+    const RdoArgs *__restrict__ A, int nsets, int var, uint32_t *kp_cnt, unsigned long long *kp_t) {
   __shared__ __align__(16) uint8_t lds[QuadLds<Px>::kBytes];
   __shared__ uint16_t scan[1024];
+  if (kp_t && threadIdx.x == 0) atomicMin(kp_t, (unsigned long long)wall_clock64());
   const RdoArgs &la = A[0], &ca = A[1], &lb = A[2], &cb = A[3];
   const int na = rdo_ntx(la), ma = rdo_ntx(ca);
   const int nb = nsets > 1 ? rdo_ntx(lb) : 0, mb = nsets > 1 ? rdo_ntx(cb) : 0;
+  if (kp_cnt && blockIdx.x == 0 && threadIdx.x == 0) {  // the launch's units, once
+    atomicAdd(kp_cnt + (MA ? 1 : 0), (uint32_t)na);
+    atomicAdd(kp_cnt + (MA ? 3 : 2), (uint32_t)ma);
+    if (nsets > 1) {
+      atomicAdd(kp_cnt + (MB ? 1 : 0), (uint32_t)nb);
+      atomicAdd(kp_cnt + (MB ? 3 : 2), (uint32_t)mb);
+    }
+  }
   const int pa = (ma + 1) / 2, pb = (mb + 1) / 2;
   const int e0 = (na + 3) / 4, e1 = e0 + (2 * pa + 2) / 3;
   const int e2 = e1 + (nb + 3) / 4, e3 = e2 + (2 * pb + 2) / 3;
@@ -1342,6 +1351,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     }
     __syncthreads();  // the slots and the scan are reused by the next item
   }
+  if (kp_t && threadIdx.x == 0) atomicMax(kp_t + 1, (unsigned long long)wall_clock64());
 }
 
 // Kernel arguments -> device memory (they are captured at launch, so the
@@ -1553,7 +1563,7 @@ int rv_rdo_args_put(const RdoArgs *h, int n, RdoArgs *dev, hipStream_t s) {
 }
 
 int rv_rdo_candidates_list(const RdoArgs *h, const RdoArgs *dev, int nsets, int mode_a, int hbd,
-                           hipStream_t s, int max_grid) {
+                           hipStream_t s, int max_grid, uint32_t *kp_cnt, unsigned long long *kp_t) {
   if (!h || !dev || nsets < 1 || nsets > 2 || mode_a < 0 || mode_a > 1 || (nsets == 2 && mode_a) ||
       h[0].commit || h[0].bd == 12)
     return rv_set_error(RV_EINVAL, "rv_rdo_candidates_list: bad arguments");
@@ -1572,7 +1582,8 @@ int rv_rdo_candidates_list(const RdoArgs *h, const RdoArgs *dev, int nsets, int 
   unsigned grid = std::min(full, (unsigned)rdo_f4_pool());
   if (max_grid > 0) grid = std::min(grid, (unsigned)max_grid);
   if (grid == 0) return RV_OK;
-#define RV_LIST(PX, MA, MB) rdo_quad_list_kernel<PX, MA, MB><<<grid, 256, 0, s>>>(dev, nsets, var)
+#define RV_LIST(PX, MA, MB) \
+  rdo_quad_list_kernel<PX, MA, MB><<<grid, 256, 0, s>>>(dev, nsets, var, kp_cnt, kp_t)
   if (hbd) {
     if (nsets == 2) RV_LIST(uint16_t, 0, 1); else if (mode_a) RV_LIST(uint16_t, 1, 1); else RV_LIST(uint16_t, 0, 0);
   } else {

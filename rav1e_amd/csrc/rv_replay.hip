@@ -1281,20 +1281,25 @@ struct rv_replay {
   long timed = 0;
   // diamond candidate evaluations per job, per ring slot: [kRing][2][nsb*R]
   uint32_t *ds_evals;
-  // Kernel probe (rv_replay_set_kernel_probe): on instrumented frames every
-  // F3 sub-pel launch (ds_fast_kernel<W = H = 64, sub-pel>: round 0 and the
-  // MV-stack rounds) is bracketed by an event pair on its stream, and the
-  // launches add their candidate evaluations and jobs into kp_cnt.  Pair i
-  // uses kp_ev[2 (i % kKp)], harvested (elapsed time summed) before reuse.
+  // Kernel probes (rv_replay_set_kernel_probe): on instrumented frames
+  // every launch of a probed kernel -- probe 0: F3 sub-pel
+  // (ds_fast_kernel<W = H = 64, sub-pel>), probe 1: the F4 candidate lists
+  // (rdo_quad_list_kernel); round 0 and the MV-stack rounds -- is bracketed
+  // by an event pair on its stream, and the launches add their units into
+  // kp_cnt[p] (probe 0: candidate evaluations, jobs; probe 1: single /
+  // compound luma candidates, single / compound chroma transform blocks).
+  // Pair i of probe p uses kp_ev[p][2 (i % kKp)], harvested (elapsed time
+  // summed) before reuse.
+  static constexpr int kProbes = 2, kKpCnt = 4;
   bool kprobe = false;
   static constexpr int kKp = 512;
-  std::vector<hipEvent_t> kp_ev;
-  long kp_n = 0, kp_done = 0, kp_base = 0;  // pairs recorded / harvested / at the last start
-  double kp_ms = 0.0, kp_dev_ms = 0.0;
-  uint32_t *kp_cnt = nullptr;  // device [2]: evaluations, jobs
+  std::vector<hipEvent_t> kp_ev[kProbes];
+  long kp_n[kProbes] = {0, 0}, kp_done[kProbes] = {0, 0}, kp_base[kProbes] = {0, 0};
+  double kp_ms[kProbes] = {0.0, 0.0}, kp_dev_ms[kProbes] = {0.0, 0.0};
+  uint32_t *kp_cnt[kProbes] = {nullptr, nullptr};  // device [kKpCnt] each
   // ... and each launch's span on the device clock: [kKp][2] (first
   // workgroup's start, last one's end), harvested with the events
-  unsigned long long *kp_ts = nullptr;
+  unsigned long long *kp_ts[kProbes] = {nullptr, nullptr};
   double kp_tick_ms = 0.0;  // ms per wall_clock64 tick
 };
 
@@ -1307,18 +1312,18 @@ void *dalloc(rv_replay *r, size_t bytes) {
   return p;
 }
 
-// the kernel probe's pairs [kp_done, upto): their elapsed times summed
-hipError_t kp_harvest(rv_replay *r, long upto) {
-  for (; r->kp_done < upto; r->kp_done++) {
-    const size_t i = 2 * (size_t)(r->kp_done % rv_replay::kKp);
-    hipError_t e = hipEventSynchronize(r->kp_ev[i + 1]);
+// kernel probe p's pairs [kp_done, upto): their elapsed times summed
+hipError_t kp_harvest(rv_replay *r, int p, long upto) {
+  for (; r->kp_done[p] < upto; r->kp_done[p]++) {
+    const size_t i = 2 * (size_t)(r->kp_done[p] % rv_replay::kKp);
+    hipError_t e = hipEventSynchronize(r->kp_ev[p][i + 1]);
     float ms = 0.f;
-    if (e == hipSuccess) e = hipEventElapsedTime(&ms, r->kp_ev[i], r->kp_ev[i + 1]);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, r->kp_ev[p][i], r->kp_ev[p][i + 1]);
     unsigned long long t[2] = {0, 0};
-    if (e == hipSuccess) e = hipMemcpy(t, r->kp_ts + i, sizeof(t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(t, r->kp_ts[p] + i, sizeof(t), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return e;
-    r->kp_ms += ms;
-    if (t[1] > t[0]) r->kp_dev_ms += (double)(t[1] - t[0]) * r->kp_tick_ms;
+    r->kp_ms[p] += ms;
+    if (t[1] > t[0]) r->kp_dev_ms[p] += (double)(t[1] - t[0]) * r->kp_tick_ms;
   }
   return hipSuccess;
 }
@@ -2046,7 +2051,8 @@ void rv_replay_destroy(rv_replay *r) {
   for (int f = 0; f < rv_replay::kRing; f++)
     for (int i = 0; i < rv_replay::kEv; i++)
       if (r->evs[f][i]) (void)hipEventDestroy(r->evs[f][i]);
-  for (hipEvent_t ev : r->kp_ev)
+  for (const auto &evs : r->kp_ev)
+    for (hipEvent_t ev : evs)
     if (ev) (void)hipEventDestroy(ev);
   if (r->ev_fork) (void)hipEventDestroy(r->ev_fork);
   if (r->ev_join) (void)hipEventDestroy(r->ev_join);
@@ -3480,24 +3486,26 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   RV_EV(0);
   // the kernel probe's brackets around the F3 sub-pel launches (speed 10)
   const bool kp = tm && r->kprobe && !r->s6;
-  uint32_t *kp_acc = kp ? r->kp_cnt : nullptr;
-  auto kp_open = [&](hipStream_t xs) -> int {
+  uint32_t *kp_acc = kp ? r->kp_cnt[0] : nullptr;
+  uint32_t *kp_f4 = kp ? r->kp_cnt[1] : nullptr;
+  auto kp_open = [&](hipStream_t xs, int p = 0) -> int {
     if (!kp) return RV_OK;
-    if (r->kp_n - r->kp_done >= rv_replay::kKp) RV_H(kp_harvest(r, r->kp_n - rv_replay::kKp + 1));
+    if (r->kp_n[p] - r->kp_done[p] >= rv_replay::kKp)
+      RV_H(kp_harvest(r, p, r->kp_n[p] - rv_replay::kKp + 1));
     // the launch's device-clock span slot: start = max, end = 0
     static const unsigned long long init[2] = {~0ull, 0ull};
-    RV_H(hipMemcpyAsync(r->kp_ts + 2 * (size_t)(r->kp_n % rv_replay::kKp), init, sizeof(init),
+    RV_H(hipMemcpyAsync(r->kp_ts[p] + 2 * (size_t)(r->kp_n[p] % rv_replay::kKp), init, sizeof(init),
                         hipMemcpyHostToDevice, xs));
-    RV_H(hipEventRecord(r->kp_ev[2 * (size_t)(r->kp_n % rv_replay::kKp)], xs));
+    RV_H(hipEventRecord(r->kp_ev[p][2 * (size_t)(r->kp_n[p] % rv_replay::kKp)], xs));
     return RV_OK;
   };
-  auto kp_ts = [&]() -> unsigned long long * {
-    return kp ? r->kp_ts + 2 * (size_t)(r->kp_n % rv_replay::kKp) : nullptr;
+  auto kp_ts = [&](int p = 0) -> unsigned long long * {
+    return kp ? r->kp_ts[p] + 2 * (size_t)(r->kp_n[p] % rv_replay::kKp) : nullptr;
   };
-  auto kp_close = [&](hipStream_t xs) -> int {
+  auto kp_close = [&](hipStream_t xs, int p = 0) -> int {
     if (!kp) return RV_OK;
-    RV_H(hipEventRecord(r->kp_ev[2 * (size_t)(r->kp_n % rv_replay::kKp) + 1], xs));
-    r->kp_n++;
+    RV_H(hipEventRecord(r->kp_ev[p][2 * (size_t)(r->kp_n[p] % rv_replay::kKp) + 1], xs));
+    r->kp_n[p]++;
     return RV_OK;
   };
   // F0 .. FL: the frame's lookahead (lookahead_frame), or with an importance
@@ -3900,16 +3908,20 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     }
     RV_EV(6);
     // F4 every valid candidate, luma + both chroma planes in one fused launch
-    if (f4_list)
-      RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 1, 0, g.hbd, st));
-    else
+    if (f4_list) {
+      RV_R(kp_open(st, 1));
+      RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 1, 0, g.hbd, st, 0, kp_f4, kp_ts(1)));
+      RV_R(kp_close(st, 1));
+    } else
       RV_R(rv_rdo_candidates(la4, ca4, g.hbd, st));
     if (r->lvl && !edge && !lv_early) RV_R(lv_rdo(st));
     if (cg.comp) {  // the compound candidates (all pushed), distinct MV pairs from the list
       RV_EV(7);
-      if (f4_list)
-        RV_R(rv_rdo_candidates_list(f4h + 2, r->f4_args + 2, 1, 1, g.hbd, st));
-      else
+      if (f4_list) {
+        RV_R(kp_open(st, 1));
+        RV_R(rv_rdo_candidates_list(f4h + 2, r->f4_args + 2, 1, 1, g.hbd, st, 0, kp_f4, kp_ts(1)));
+        RV_R(kp_close(st, 1));
+      } else
         RV_R(rv_rdo_candidates(lc4, cc4, g.hbd, st, true));
       if (r->lvl && !edge && !lv_early) RV_R(lv_rdo_comp(st));
     } else {
@@ -3998,7 +4010,9 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     // in one launch
     if (cg.comp) {
       if (f4_list && f4_pair && !r->rs2) {  // the pool over both lists
-        RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 2, 0, g.hbd, xs, f4_grid));
+        RV_R(kp_open(xs, 1));
+        RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 2, 0, g.hbd, xs, f4_grid, kp_f4, kp_ts(1)));
+        RV_R(kp_close(xs, 1));
       } else if (f4_pair && !r->rs2) {
         RV_R(rv_rdo_candidates_pair(la4, ca4, lc4, cc4, g.hbd, xs));
       } else {
@@ -4006,7 +4020,9 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
         RV_R(rv_rdo_candidates(lc4, cc4, g.hbd, x2, true));
       }
     } else if (f4_list) {
-      RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 1, 0, g.hbd, xs, f4_grid));
+      RV_R(kp_open(xs, 1));
+      RV_R(rv_rdo_candidates_list(f4h, r->f4_args, 1, 0, g.hbd, xs, f4_grid, kp_f4, kp_ts(1)));
+      RV_R(kp_close(xs, 1));
     } else {
       RV_R(rv_rdo_candidates(la4, ca4, g.hbd, xs));
     }
@@ -4447,47 +4463,62 @@ int rv_replay_stage_times_sum(rv_replay *r, int last_frames, float *ms_out, int 
 // flight are waited for); off stops recording.
 int rv_replay_set_kernel_probe(rv_replay *r, int on) {
   if (!r) return rv_set_error(RV_EINVAL, "rv_replay_set_kernel_probe: null");
-  if (on && r->kp_ev.empty()) {
-    r->kp_ev.assign(2 * rv_replay::kKp, nullptr);
-    for (auto &ev : r->kp_ev) RV_H(hipEventCreate(&ev));
-    r->kp_cnt = (uint32_t *)dalloc(r, 2 * sizeof(uint32_t));
-    r->kp_ts = (unsigned long long *)dalloc(r, 2 * sizeof(unsigned long long) * rv_replay::kKp);
-    if (!r->kp_cnt || !r->kp_ts)
-      return rv_set_error(RV_EHIP, "rv_replay_set_kernel_probe: allocation failed");
+  constexpr int P = rv_replay::kProbes, C = rv_replay::kKpCnt;
+  if (on && r->kp_ev[0].empty()) {
+    for (int p = 0; p < P; p++) {
+      r->kp_ev[p].assign(2 * rv_replay::kKp, nullptr);
+      for (auto &ev : r->kp_ev[p]) RV_H(hipEventCreate(&ev));
+      r->kp_cnt[p] = (uint32_t *)dalloc(r, C * sizeof(uint32_t));
+      r->kp_ts[p] = (unsigned long long *)dalloc(r, 2 * sizeof(unsigned long long) * rv_replay::kKp);
+      if (!r->kp_cnt[p] || !r->kp_ts[p])
+        return rv_set_error(RV_EHIP, "rv_replay_set_kernel_probe: allocation failed");
+    }
     int dev = 0, khz = 0;
     RV_H(hipGetDevice(&dev));
     RV_H(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
     r->kp_tick_ms = khz > 0 ? 1.0 / (double)khz : 0.0;
   }
-  if (!r->kp_ev.empty()) {
-    RV_H(kp_harvest(r, r->kp_n));
+  if (!r->kp_ev[0].empty()) {
+    for (int p = 0; p < P; p++) RV_H(kp_harvest(r, p, r->kp_n[p]));
     RV_H(hipDeviceSynchronize());
-    RV_H(hipMemset(r->kp_cnt, 0, 2 * sizeof(uint32_t)));
+    for (int p = 0; p < P; p++) RV_H(hipMemset(r->kp_cnt[p], 0, C * sizeof(uint32_t)));
     RV_H(hipDeviceSynchronize());
   }
-  r->kp_ms = 0.0;
-  r->kp_dev_ms = 0.0;
-  r->kp_base = r->kp_n;
+  for (int p = 0; p < P; p++) {
+    r->kp_ms[p] = 0.0;
+    r->kp_dev_ms[p] = 0.0;
+    r->kp_base[p] = r->kp_n[p];
+  }
   r->kprobe = on != 0;
   return RV_OK;
 }
 
-// out[0] launches, [1] their summed milliseconds (event pairs on their
-// streams), [2] candidate evaluations, [3] jobs, since the probe started
+// probe 0: out[0] launches, [1] their summed milliseconds (event pairs on
+// their streams), [2] candidate evaluations, [3] jobs, [4] device-clock ms;
+// probe 1 (cap >= 11): out[5] launches, [6] event ms, [7] device-clock ms,
+// [8] single / [9] compound luma candidates, [10] single chroma transform
+// blocks, [11] compound ones (cap >= 12)
 int rv_replay_kernel_probe(rv_replay *r, double *out, int cap) {
   if (!r || !out || cap < 4) return rv_set_error(RV_EINVAL, "rv_replay_kernel_probe: null / cap");
-  const int nout = cap < 5 ? 4 : 5;
+  const int nout = cap >= 12 ? 12 : cap < 5 ? 4 : 5;
   for (int i = 0; i < nout; i++) out[i] = 0.0;
-  if (r->kp_ev.empty()) return nout;
-  RV_H(kp_harvest(r, r->kp_n));
-  uint32_t c[2] = {0, 0};
+  if (r->kp_ev[0].empty()) return nout;
+  for (int p = 0; p < rv_replay::kProbes; p++) RV_H(kp_harvest(r, p, r->kp_n[p]));
+  uint32_t c[2][rv_replay::kKpCnt] = {{0}};
   RV_H(hipDeviceSynchronize());
-  RV_H(hipMemcpy(c, r->kp_cnt, sizeof(c), hipMemcpyDeviceToHost));
-  out[0] = (double)(r->kp_n - r->kp_base);
-  out[1] = r->kp_ms;
-  out[2] = (double)c[0];
-  out[3] = (double)c[1];
-  if (nout > 4) out[4] = r->kp_dev_ms;
+  for (int p = 0; p < rv_replay::kProbes; p++)
+    RV_H(hipMemcpy(c[p], r->kp_cnt[p], sizeof(c[p]), hipMemcpyDeviceToHost));
+  out[0] = (double)(r->kp_n[0] - r->kp_base[0]);
+  out[1] = r->kp_ms[0];
+  out[2] = (double)c[0][0];
+  out[3] = (double)c[0][1];
+  if (nout > 4) out[4] = r->kp_dev_ms[0];
+  if (nout >= 12) {
+    out[5] = (double)(r->kp_n[1] - r->kp_base[1]);
+    out[6] = r->kp_ms[1];
+    out[7] = r->kp_dev_ms[1];
+    for (int i = 0; i < 4; i++) out[8 + i] = (double)c[1][i];
+  }
   return nout;
 }
 // Candidate evaluations summed over the last min(frames, 64) coded frames:

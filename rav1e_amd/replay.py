@@ -448,9 +448,11 @@ class HipReplay:
     def kernel_probe(self) -> np.ndarray:
         """[launches, summed ms (HIP event pairs), candidate evaluations,
         jobs, summed ms (device clock spans)] of the probed F3 sub-pel
-        launches since the probe started."""
-        out = np.zeros(5, np.float64)
-        _check(lib().rv_replay_kernel_probe(self.h, out.ctypes.data, 5) - 5,
+        launches since the probe started, then [launches, event ms,
+        device-clock ms, single / compound luma candidates, single / compound
+        chroma transform blocks] of the F4 candidate-list launches."""
+        out = np.zeros(12, np.float64)
+        _check(lib().rv_replay_kernel_probe(self.h, out.ctypes.data, 12) - 12,
                "rv_replay_kernel_probe")
         return out
 
@@ -871,7 +873,7 @@ class PipelinedReplay:
 
     def kernel_probe(self) -> np.ndarray:
         self.drain()
-        return sum((t.kernel_probe() for t in self.inst), np.zeros(5))
+        return sum((t.kernel_probe() for t in self.inst), np.zeros(12))
 
     def stage_ms_sum_frames(self, frames) -> tuple:
         """Stage times summed over the instrumented inter frames `frames`

@@ -27,7 +27,9 @@ import sqlite3
 import tempfile
 
 ROUND0_OF = ("rdo_quad_kernel<unsigned char, 0>", "rdo_quad_kernel<unsigned char, 1>",
-             "rdo_quad_kernel<unsigned short, 0>", "rdo_quad_kernel<unsigned short, 1>")
+             "rdo_quad_kernel<unsigned short, 0>", "rdo_quad_kernel<unsigned short, 1>",
+             "rdo_quad_list_kernel<unsigned char, 0, 0>", "rdo_quad_list_kernel<unsigned char, 1, 1>",
+             "rdo_quad_list_kernel<unsigned short, 0, 0>", "rdo_quad_list_kernel<unsigned short, 1, 1>")
 
 
 def open_db(d):
