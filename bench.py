@@ -334,14 +334,33 @@ def cpu_baseline_and_parity(args, hip_inputs, W, H, xdec, ydec, bd, nref, tiling
     return cpu, parity
 
 
-def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2, imp_window=0):
+# The lookahead engine's kernels (rocprofv3 names) and how a rank's share of
+# them scales at N ranks: the searches and the 8x8 importance data run on the
+# rank's own tile group (1 / N), the window's target lists and propagation
+# over the whole frame on every rank
+LA_KERNELS_PER_GROUP = ("ds_grp_kernel<{px}, 16, false, false>", "la_check_kernel",
+                        "fs16_sea_kernel_{pxs}", "pyramid_kernel<{px}>", "box_sums_kernel<{px}>",
+                        "data_kernel<{px}>")
+LA_KERNELS_WHOLE_FRAME = ("pass_kernel", "csr_scan_kernel", "csr_scatter_kernel", "csr_order_kernel",
+                          "keys_kernel", "zero_kernel", "final_kernel")
+
+
+def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=6, imp_window=0, pj=None):
     """The N-rank tile-group split on ONE GPU: config's n tile groups as n
     HipReplay instances (the ranks), each frame coded group by group with
     the GPU to itself, the all-gather emulated by device copies into every
     group's receive buffer (RCCL's layout), then every group's import
-    (unpack, loop filters, pad).  Per group: the HIP-event span of its frame
-    (stages F0 .. F7 on its stream); the projected N-rank step = the slowest
-    group + the slowest import + the all-gather at an assumed xGMI rate."""
+    (unpack, loop filters, pad).  Per group: the wall time of its frame
+    (frame() to a device sync: every stream of the group -- F0 .. F8, the
+    frame-edge levels, the side streams); averaged over the frames past GOP 4.
+    The groups' lookahead engines run ahead (inputs declared in place: the
+    window's part exchange needs every group's engine), so their per-frame
+    work is not in that span; it is added from the committed kernel trace of
+    the one-GPU bench: the rank's share of the search kernels (1 / N) and
+    all of the whole-frame importance propagation.  The projected N-rank step
+    = the slowest group + that lookahead share + the slowest import + the
+    all-gather at an assumed xGMI rate.  At N > 1 every rank codes its frames
+    one after another (PipelinedReplay is one-GPU only), which this models."""
     import ctypes as C
 
     import rav1e_amd as R
@@ -370,15 +389,18 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2, imp_wind
     span = [[] for _ in gs]
     imp = [[] for _ in gs]
     progress(f"emulated ranks: {n} groups")
+    stage = [[] for _ in gs]
     for f in range(frames):
-        timed = f > gop  # the second GOP on: every me_range_scale once per GOP
+        timed = f > 4 * gop  # past GOP 4: every me_range_scale once per GOP
         order = range(n - 1, -1, -1) if os.environ.get("RAV1E_BENCH_EMU_REVERSE") else range(n)
         for k in order:  # (reversed: A/B of the first group's position)
             g = gs[k]
+            t0 = time.perf_counter()
             g.frame()
             sync()
             if timed:
-                span[k].append(float(g.stage_ms()[:13].sum()))
+                span[k].append((time.perf_counter() - t0) * 1e3)
+                stage[k].append(float(g.stage_ms()[:13].sum()))
         if f == 0:
             continue  # the key frame: every group copied its own input
         for k in range(n):
@@ -399,12 +421,27 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2, imp_wind
     if hub:
         hub.close()
     per = [sum(s) / len(s) for s in span]
+    per_stage = [sum(s) / len(s) for s in stage]
     imp_ms = max(sum(s) / len(s) for s in imp)
     xgmi_gbs = 64.0  # assumed all-gather algorithm bandwidth per rank (RCCL over xGMI)
     ag_ms = (n - 1) * nb / (xgmi_gbs * 1e9) * 1e3
-    proj = max(per) + imp_ms + ag_ms
+    la_ms, la_src = 0.0, None
+    if imp_window and pj:
+        pxn = "unsigned short" if bd > 8 else "unsigned char"
+        fmt = dict(px=pxn, pxs="u16" if bd > 8 else "u8")
+        grp = sum(v["ms_per_frame"] for k, v in pj["kernels"].items()
+                  if any(nm.format(**fmt) in k for nm in LA_KERNELS_PER_GROUP))
+        whole = sum(v["ms_per_frame"] for k, v in pj["kernels"].items()
+                    if any(nm in k for nm in LA_KERNELS_WHOLE_FRAME))
+        la_ms = grp / n + whole
+        la_src = {"source": pj["source"], "git": pj["git"], "search_ms_per_frame": round(grp, 4),
+                  "whole_frame_ms_per_frame": round(whole, 4),
+                  "rule": "searches / N + the whole-frame propagation, from the one-GPU trace"}
+    proj = max(per) + la_ms + imp_ms + ag_ms
     return {"ranks": n, "groups_sb": [list(r) for r in rects],
             "group_frame_ms": [round(v, 4) for v in per], "max_group_ms": round(max(per), 4),
+            "group_stage_sum_ms": [round(v, 4) for v in per_stage],
+            "lookahead_ms_per_rank": round(la_ms, 4), "lookahead_model": la_src,
             "import_ms_max": round(imp_ms, 4), "exchange_bytes_per_group": int(nb),
             "allgather_ms_model": round(ag_ms, 4),
             "allgather_model": f"(n-1) x bytes_per_group at an assumed {xgmi_gbs:g} GB/s",
@@ -418,8 +455,9 @@ def emulate_ranks(n, W, H, xdec, ydec, bd, nref, tiling, flags, gops=2, imp_wind
             "group_lookahead_rounds_per_frame": [round(c[18] / max(1, c[16]), 2) for c in cnts],
             "group_order": "groups code each frame in index order (group 0 first)",
             "importance_window": imp_window,
-            "method": "one GPU, groups run one after another (HIP-event spans; import wall "
-                      "clock incl. launch), device-copy all-gather"}
+            "method": "one GPU, groups run one after another (wall clock of each group's "
+                      "frame to a device sync, frames past GOP 4; import wall clock incl. "
+                      "launch), device-copy all-gather; each rank codes its frames serially"}
 
 
 def main():
@@ -808,7 +846,7 @@ def main():
     n_emu = min(args.emulate_ranks, tiling["cols"] * tiling["rows"])  # one tile group per rank
     if rank == 0 and world == 1 and n_emu > 1:
         emu = emulate_ranks(n_emu, W, H, xdec, ydec, bd, nref, tiling, flags,
-                            imp_window=imp_window)
+                            imp_window=imp_window, pj=pj)
 
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

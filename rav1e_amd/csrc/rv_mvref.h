@@ -64,6 +64,18 @@ struct MvrefArgs {
   uint8_t *f3dirty;
   uint8_t *f2dirty;  // out (null: none): per F2 job [R][nsb][4], 1 = its set changed
   int field_guess_la;  // the first check: the EPZS field from the quadrants alone (A/B)
+  // An incremental check (plist non-null): only the superblocks whose inputs
+  // the previous round can have changed -- the right, below-left, below and
+  // below-right neighbours of every superblock the previous check listed
+  // (its list plist, *pcount entries): a superblock's stacks and EPZS sets
+  // read only its left, top-left, top and top-right neighbours (DESIGN.md
+  // §3).  epoch[sb] holds the tag of the last check that claimed sb (each
+  // candidate is checked once per check); tag > every earlier check's.
+  const int32_t *plist;
+  const int32_t *pcount;
+  uint32_t *epoch;
+  uint32_t tag;
+  int inc_grid;  // workgroups of the incremental check (0: the full check's)
 };
 
 // The decision record of superblock sb's winner (candidate c of the

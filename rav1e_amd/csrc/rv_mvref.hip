@@ -434,50 +434,47 @@ __global__ __launch_bounds__(256) void mvref_kernel(MvrefArgs a) {
 // its lanes in turn, with their loads' latencies in series).  A
 // superblock's roles meet in LDS.
 constexpr int kSplitSb = 64;
-__global__ __launch_bounds__(1024) void mvref_split_kernel(MvrefArgs a) {
-  __shared__ uint32_t chg[kSplitSb];  // per superblock: bit r = role r changed
-  __shared__ uint32_t pmk[kSplitSb];  // role 0: the references whose rate predictors changed
-  const int role = (int)(threadIdx.x >> 6), sbl = (int)(threadIdx.x & 63);
-  const int sb = (int)blockIdx.x * kSplitSb + sbl;
-  const bool live = sb < a.nsb;
-  if (threadIdx.x < kSplitSb) chg[threadIdx.x] = pmk[threadIdx.x] = 0;
-  __syncthreads();
-  if (live) {
-    const int sx = sb % a.tw, sy = sb / a.tw;
-    const int fsx = a.tx0 + sx, fsy = a.ty0 + sy;
-    bool changed = false;
-    if (role == 0) {  // the stacks (as in mvref_kernel's lane 0)
-      const int t0x = fsx - fsx % a.tws, t0y = fsy - fsy % a.ths;
-      const int cols = min(a.tws * 16, a.w_in_b - t0x * 16);
-      const int bx = (fsx - t0x) * 16, by = (fsy - t0y) * 16;
-      const int X = fsx * 64, Y = fsy * 64;
-      const bool split = a.lvl && (X + 64 > a.W || Y + 64 > a.H);
-      Nb nb;
-      nb.up = !split && by > 0;
-      nb.left = !split && bx > 0;
-      nb.tr = !split && by > 0 && bx + 16 < cols;
-      nb.tl = !split && bx > 0 && by > 0;
-      if (nb.up) nb.a = coded_at(a, sb - a.tw, X, Y - 4);
-      if (nb.left) nb.l = coded_at(a, sb - 1, X - 4, Y);
-      if (nb.tr) nb.r = coded_at(a, sb - a.tw + 1, X + 64, Y - 4);
-      if (nb.tl) nb.d = coded_at(a, sb - a.tw - 1, X - 4, Y - 4);
-      const MvStack st = stacks_of(a, nb, split, fsx, fsy);
-      changed = !same_stacks(a, a.stk[sb], st);
-      uint32_t pmask = 0;
+// One role of superblock sb's check: role 0 its stacks (pmask: the
+// references whose rate predictors changed), role r its EPZS job r - 1.
+// Returns whether what the role checked changed.
+__device__ __forceinline__ bool check_role(const MvrefArgs &a, int sb, int role, uint32_t *pmask) {
+  const int sx = sb % a.tw, sy = sb / a.tw;
+  const int fsx = a.tx0 + sx, fsy = a.ty0 + sy;
+  if (role == 0) {  // the stacks (as in mvref_kernel's lane 0)
+    const int t0x = fsx - fsx % a.tws, t0y = fsy - fsy % a.ths;
+    const int cols = min(a.tws * 16, a.w_in_b - t0x * 16);
+    const int bx = (fsx - t0x) * 16, by = (fsy - t0y) * 16;
+    const int X = fsx * 64, Y = fsy * 64;
+    const bool split = a.lvl && (X + 64 > a.W || Y + 64 > a.H);
+    Nb nb;
+    nb.up = !split && by > 0;
+    nb.left = !split && bx > 0;
+    nb.tr = !split && by > 0 && bx + 16 < cols;
+    nb.tl = !split && bx > 0 && by > 0;
+    if (nb.up) nb.a = coded_at(a, sb - a.tw, X, Y - 4);
+    if (nb.left) nb.l = coded_at(a, sb - 1, X - 4, Y);
+    if (nb.tr) nb.r = coded_at(a, sb - a.tw + 1, X + 64, Y - 4);
+    if (nb.tl) nb.d = coded_at(a, sb - a.tw - 1, X - 4, Y - 4);
+    const MvStack st = stacks_of(a, nb, split, fsx, fsy);
+    const bool changed = !same_stacks(a, a.stk[sb], st);
+    uint32_t pm = 0;
 #pragma unroll
-      for (int k = 0; k < 2; k++)
-        if (k < a.R && (a.init || !mv_eq(a.stk[sb].s[k][0], st.s[k][0]) ||
-                        !mv_eq(a.stk[sb].s[k][1], st.s[k][1])))
-          pmask |= 1u << k;
-      pmk[sbl] = pmask;
-      if (changed) set_stacks(a, sb, st);
-    } else {
-      changed = epzs_job(a, sb, fsx, fsy, role - 1);
-    }
-    if (changed) atomicOr(&chg[sbl], 1u << role);
+    for (int k = 0; k < 2; k++)
+      if (k < a.R && (a.init || !mv_eq(a.stk[sb].s[k][0], st.s[k][0]) ||
+                      !mv_eq(a.stk[sb].s[k][1], st.s[k][1])))
+        pm |= 1u << k;
+    *pmask = pm;
+    if (changed) set_stacks(a, sb, st);
+    return changed;
   }
-  __syncthreads();
-  const uint32_t cm = chg[sbl], pm = pmk[sbl];
+  return epzs_job(a, sb, fsx, fsy, role - 1);
+}
+
+// The end of a check of superblock sb (role's thread): its F3 / F2 dirty
+// flags from the roles' changes cm (bit r: role r) and the rate predictors'
+// pm; role 0 marks it and appends it, wave-aggregated (sbl = its lane).
+__device__ __forceinline__ void check_finish(const MvrefArgs &a, int sb, int role, int sbl, bool live,
+                                    uint32_t cm, uint32_t pm) {
   if (a.f3dirty && live && role >= 1 && role <= a.R)  // F3 job role - 1: its set or its pmv
     a.f3dirty[(size_t)(role - 1) * a.nsb + sb] = (((cm >> role) & 1) || ((pm >> (role - 1)) & 1)) ? 1 : 0;
   if (a.f2dirty && live && role > a.R) {  // F2 quadrant job: its set alone
@@ -492,6 +489,64 @@ __global__ __launch_bounds__(1024) void mvref_split_kernel(MvrefArgs a) {
     if (sbl == 0 && m) base = atomicAdd(a.count, (int)__popcll(m));
     base = __shfl(base, 0, 64);
     if (mark) a.list[base + __popcll(m & ((1ull << sbl) - 1))] = sb;
+  }
+}
+
+__global__ __launch_bounds__(1024) void mvref_split_kernel(MvrefArgs a) {
+  __shared__ uint32_t chg[kSplitSb];  // per superblock: bit r = role r changed
+  __shared__ uint32_t pmk[kSplitSb];  // role 0: the references whose rate predictors changed
+  const int role = (int)(threadIdx.x >> 6), sbl = (int)(threadIdx.x & 63);
+  const int sb = (int)blockIdx.x * kSplitSb + sbl;
+  const bool live = sb < a.nsb;
+  if (threadIdx.x < kSplitSb) chg[threadIdx.x] = pmk[threadIdx.x] = 0;
+  __syncthreads();
+  if (live) {
+    uint32_t pm = 0;
+    const bool changed = check_role(a, sb, role, &pm);
+    if (role == 0) pmk[sbl] = pm;
+    if (changed) atomicOr(&chg[sbl], 1u << role);
+  }
+  __syncthreads();
+  check_finish(a, sb, role, sbl, live, chg[sbl], pmk[sbl]);
+  round_publish(a.pub);
+}
+
+// The incremental check (a.plist): the same roles over the dependents of
+// the previous check's list, 64 candidates per workgroup pass; a candidate
+// is claimed once per check through epoch (the first claimant checks it).
+__global__ __launch_bounds__(1024) void mvref_inc_kernel(MvrefArgs a) {
+  __shared__ int32_t sbs[kSplitSb];
+  __shared__ uint32_t chg[kSplitSb];
+  __shared__ uint32_t pmk[kSplitSb];
+  const int role = (int)(rv_tid() >> 6), sbl = (int)(rv_tid() & 63);
+  const int items = 4 * __builtin_amdgcn_readfirstlane(*a.pcount);
+  for (int base = (int)blockIdx.x * kSplitSb; base < items; base += (int)gridDim.x * kSplitSb) {
+    if (role == 0) {
+      int s = -1;
+      const int it = base + sbl;
+      if (it < items) {
+        const int e = a.plist[it >> 2], d = it & 3;  // right, below-left, below, below-right
+        const int nx = e % a.tw + (d == 0 ? 1 : d - 2), ny = e / a.tw + (d == 0 ? 0 : 1);
+        if (nx >= 0 && nx < a.tw && ny < a.th) {
+          const int c = ny * a.tw + nx;
+          if (atomicMax(&a.epoch[c], a.tag) < a.tag) s = c;
+        }
+      }
+      sbs[sbl] = s;
+      chg[sbl] = pmk[sbl] = 0;
+    }
+    __syncthreads();
+    const int sb = sbs[sbl];
+    const bool live = sb >= 0;
+    if (live) {
+      uint32_t pm = 0;
+      const bool changed = check_role(a, sb, role, &pm);
+      if (role == 0) pmk[sbl] = pm;
+      if (changed) atomicOr(&chg[sbl], 1u << role);
+    }
+    __syncthreads();
+    check_finish(a, live ? sb : 0, role, sbl, live, chg[sbl], pmk[sbl]);
+    __syncthreads();  // the slot tables are rewritten by the next pass
   }
   round_publish(a.pub);
 }
@@ -647,6 +702,11 @@ int rv_mvref_round(const MvrefArgs &a, hipStream_t s, bool scan) {
   if (scan && !a.init && scan_ok) {
     const int ntiles = ((a.tw + a.tws - 1) / a.tws) * ((a.th + a.ths - 1) / a.ths);
     mvref_scan_kernel<<<ntiles, kScanThreads, (size_t)a.tws * a.ths * sizeof(BlkDec), s>>>(a);
+  } else if (check_split && a.plist && a.epoch) {
+    const int nr = 1 + (a.epzs ? 5 * a.R : 0);
+    const int full = (a.nsb + kSplitSb - 1) / kSplitSb;
+    const int grid = a.inc_grid > 0 ? std::min(a.inc_grid, full) : full;
+    mvref_inc_kernel<<<grid, kSplitSb * nr, 0, s>>>(a);
   } else if (check_split) {
     const int nr = 1 + (a.epzs ? 5 * a.R : 0);
     mvref_split_kernel<<<(a.nsb + kSplitSb - 1) / kSplitSb, kSplitSb * nr, 0, s>>>(a);

@@ -1209,7 +1209,8 @@ struct rv_replay {
   // the round checks' counts (this instance's host thread)
   static constexpr int kRoundsAhead = 2;  // rounds queued beyond the last count read
   RoundRing rr;
-  int32_t *mv_list = nullptr;
+  int32_t *mv_list = nullptr;          // [2][nsb]: check q lists into half q & 1
+  uint32_t *mv_epoch = nullptr;        // [nsb]: the incremental checks' claims (MvrefArgs::epoch)
   bool edge_tr = false;                // a stack reads a frame-edge leaf (top-right)
   // RAV1E_HIP_MV_HP=1: the rounds after the first on a high-priority stream
   hipStream_t hp = nullptr;
@@ -2332,8 +2333,10 @@ static rv_replay *create_impl(const rv_replay_cfg *cfg, void *stream, const rv_r
       ok = ok && r->dec_lv[l];
     }
     r->mv_active = (uint8_t *)dalloc(r, n);
-    r->mv_list = (int32_t *)dalloc(r, n * 4);
-    ok = ok && r->stk && r->mv_active && r->mv_list;
+    r->mv_list = (int32_t *)dalloc(r, 2 * n * 4);
+    r->mv_epoch = (uint32_t *)dalloc(r, n * 4);
+    ok = ok && r->stk && r->mv_active && r->mv_list && r->mv_epoch &&
+         hipMemsetAsync(r->mv_epoch, 0, n * 4, r->stream) == hipSuccess;
     // RAV1E_HIP_MV_HP=1: the rounds after the first on a high-priority
     // stream (2160p A/B: 140 vs 177 fps -- the other instance's work loses
     // more than the rounds gain; off)
@@ -3533,6 +3536,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     return run_rounds(r->rr, xs, budget, check, eval, nrounds, nre, changed, what, ncoded, lv);
   };
   auto slot_cnt = [&](uint32_t q) { return r->rr.slot(q); };
+  // check q's list (two halves: an incremental check reads the previous one)
+  auto mvl = [&](uint32_t q) { return r->mv_list + (size_t)(q & 1) * g.nsb; };
   const EpzsGeo eg{g.tx0, g.ty0, g.tw, g.th, g.tws, g.ths, g.W, g.H, g.w_in_b, g.h_in_b};
   // F5: the 8x8 importance SATD against reference 0's original frame at the
   // lookahead MVs (FL's output; after the frame's decisions)
@@ -3830,7 +3835,6 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     if (edge && r->edge_tr)  // the leaves the stacks read
       for (int l = 1; l < kLevels; l++)
         if (r->lv_used[l]) RV_H(hipStreamWaitEvent(st, r->ev_ejoin[l], 0));
-    ma.list = r->mv_list;
     // EPZS: the F2 / F3 sets from the coding-order field; the first check
     // guesses it from the previous decisions of this level and the
     // lookahead's quadrants, and never reads the frame-edge leaves (they may
@@ -3851,6 +3855,8 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     const uint32_t q = r->rr.seq++;
     ma.count = slot_cnt(q);
     ma.pub = r->rr.pub(q);
+    ma.list = mvl(q);
+    ma.plist = nullptr;
     RV_R(rv_mvref_round(ma, st));
   }
   // F2: build_half_res_pmvs of the encode (speed 10: the sets the check
@@ -3974,20 +3980,20 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     if (f2_f3 && !r->rs2) {  // F2 and F3 full-pel in one launch
       RV_R(rv_diamond_f2_f3(&cur.hres, refs_h, r->jobs_half[lv], r->half, ma.f2dirty, &cur.y,
                             refs_y, r->jobs_full[lv], r->full, ma.f3dirty, &to_sub, g.R, nr, g.bd,
-                            r->mv_list, acnt, lg, xs));
+                            mvl(q), acnt, lg, xs));
     } else {
       // F2 of the listed superblocks (their 4 quadrants per reference)
       RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0,
-                                   0, g.bd, r->half, nullptr, nullptr, x2, nullptr, r->mv_list,
+                                   0, g.bd, r->half, nullptr, nullptr, x2, nullptr, mvl(q),
                                    acnt, 4, ma.f2dirty, lg));
       // F3 of the listed superblocks: only the jobs whose set or pmv changed
       RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_full[lv], nr, 64, 64, 0, 0, 0,
-                                   g.bd, r->full, nullptr, &to_sub, xs, nullptr, r->mv_list, acnt,
+                                   g.bd, r->full, nullptr, &to_sub, xs, nullptr, mvl(q), acnt,
                                    1, ma.f3dirty, lg));
     }
     RV_R(kp_open(xs));
     RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
-                                 r->sub, nullptr, nullptr, xs, nullptr, r->mv_list, acnt, 1,
+                                 r->sub, nullptr, nullptr, xs, nullptr, mvl(q), acnt, 1,
                                  ma.f3dirty, lg, kp_acc, kp_ts()));
     RV_R(kp_close(xs));
     // the pools of the small per-round kernels: kRoundGrid for a run's first
@@ -3998,7 +4004,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                    : hsb ? std::min(kRoundGrid, std::max((14 * hsb + 255) / 256, (hsb + 3) / 4))
                          : round_pool;
     round_lists_kernel<<<rg, 256, 0, xs>>>(
-        cg, r->sub, nsingle, r->cand_list, r->cand_count, r->mv_list, acnt,
+        cg, r->sub, nsingle, r->cand_list, r->cand_count, mvl(q), acnt,
         CandKeys{r->cand_key, (uint32_t)(r->coded + 1), r->cand_reuse ? 1 : 0});
     if (r->rs2) {  // the lists are out: the compound F4 runs beside the single one
       RV_H(hipEventRecord(r->ev_rlists, xs));
@@ -4033,7 +4039,7 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     score_wave_kernel<<<rg, 256, 0, xs>>>(
         g, cg, L.lambda, L.ds[1], L.ds[2], r->sub, r->l_out, r->c_out, r->c_out + nct * 3, ntx_c,
         r->win, r->coarse, r->half, r->full, r->look, r->half_l, r->words, r->cand_count, nullptr,
-        nullptr, nullptr, r->mv_list, acnt, r->dec_lv[lv], 1);
+        nullptr, nullptr, mvl(q), acnt, r->dec_lv[lv], 1);
     return RV_OK;
   };
   RV_R(f3_f4());
@@ -4088,6 +4094,21 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
           ma.iwas = iwas;
           ma.count = slot_cnt(q);
           ma.pub = r->rr.pub(q);
+          ma.list = mvl(q);
+          // after the run's first (full) check, each check covers only the
+          // dependents of the previous check's list (RAV1E_HIP_CHECK_INC=0:
+          // every check full, A/B); its grid from the last count read
+          static const bool inc = !(getenv("RAV1E_HIP_CHECK_INC") && getenv("RAV1E_HIP_CHECK_INC")[0] == '0');
+          if (inc && q != q_first) {
+            ma.plist = mvl(q - 1);
+            ma.pcount = slot_cnt(q - 1);
+            ma.epoch = r->mv_epoch;
+            ma.tag = q + 1;
+            const int h = r->rr.last_count;
+            ma.inc_grid = h >= 0 ? std::max(1, (8 * h + 63) / 64) : 0;
+          } else {
+            ma.plist = nullptr;
+          }
           const uint32_t c = q - q_first;
           return rv_mvref_round(ma, xs, scans && c >= (uint32_t)scan_after &&
                                             c < (uint32_t)(scan_after + kScanMax));
