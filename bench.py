@@ -586,6 +586,8 @@ def main():
     if imp_window:
         la_cnt["t1"] = int((eng if paired else hip).counters()[20])
     kp = eng.kernel_probe() if probe else None
+    if os.environ.get("RAV1E_HIP_DS_PHASES") == "1":  # diagnostic: the rounds' sub-pel phases
+        R._check(R.lib().rv_ds_phase_dump(), "rv_ds_phase_dump")
     ent_stats = eng.entropy_stats() if ent else None
 
     # per-kernel times over the instrumented frames of the timed region

@@ -854,6 +854,11 @@ int rv_round_ring_slots(uint32_t q, int32_t *out, int cap);
 int rv_replay_lrf_units(rv_replay *r, int plane, int8_t *out, int cap);
 int rv_replay_la_refs(long m, int R, int32_t *out);
 int rv_replay_kernel_probe(rv_replay *r, double *out, int cap);
+/* Diagnostic (RAV1E_HIP_DS_PHASES=1 in the environment): the MV-stack
+ * rounds' 64x64 sub-pel searches add their phase times (setup, window +
+ * filter + SAD, cost exchange, whole job; iterations, window stagings) on
+ * the device clock; this prints the per-job means to stderr and clears them. */
+int rv_ds_phase_dump(void);
 /* Candidate evaluations summed over the last min(frames, 64) coded frames:
  * out[0] F3 full-pel 64x64 diamond, out[1] F3 sub-pel 64x64 diamond, out[2]
  * = the number of frames summed (cap >= 3); with cap >= 5, out[3] / out[4]

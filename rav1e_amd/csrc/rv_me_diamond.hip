@@ -23,6 +23,7 @@
 // SATD and square blocks of 8 and 16: ds_grp_kernel (lane groups per job).
 // Anything else takes the generic workgroup-per-candidate kernel.
 #include <algorithm>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -119,7 +120,15 @@ struct DsArgs {
   // list-driven: the workgroup pool (0: ds_list_grid(); a round expected to
   // list most jobs, e.g. the first after round 0, asks for a full grid)
   int list_grid;
+  // RAV1E_HIP_DS_PHASES=1 (diagnostic): list-driven sub-pel jobs add their
+  // phase times (wall_clock64 ticks on thread 0) into g_ds_ph
+  int ph;
 };
+
+// [0] setup (job record, source block to LDS), [1] window staging + filter
+// + SAD, [2] the cost exchange, [3] whole job, [4] diamond iterations,
+// [5] jobs, [6] window re-stagings, [7] workgroup spans, [8] workgroups
+__device__ unsigned long long g_ds_ph[16];
 
 // The ordinal-th job of a list-driven launch (its size: ds_list_total)
 __device__ __forceinline__ int ds_list_total(const DsArgs &a) {
@@ -339,8 +348,12 @@ struct DsFast {
   static constexpr int kOrgRegs = SUB ? 1 : 4 * F::I;
 };
 
+// Returns the search's result MV (uniform).  pred0 (optional): the job's
+// first predictor, in place of jobs[job].pred[0] (the fused F3 path hands
+// its full-pel winner over without a round trip through memory).
 template <typename Px, int W, int H, bool SUB>
-__device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
+__device__ __forceinline__ rv_mv ds_fast_body(const DsArgs &a, const int job, bool has_pred0 = false,
+                                              rv_mv pred0 = rv_mv{0, 0}) {
   using F = FullGeo<Px, W, H>;
   using S = SubGeo<Px, W, H>;
   constexpr int B = (int)sizeof(Px);
@@ -350,6 +363,8 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
   __shared__ uint32_t win_all[SUB ? S::kUnionDwords : 1];
   __shared__ Px org_lds[SUB ? W * H : 1];  // sub-pel: the source block, shared by all waves
 
+  const bool ph = SUB && a.ph && threadIdx.x == 0;
+  const unsigned long long ph_t0 = ph ? wall_clock64() : 0;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const rv_ds_job *jp = a.jobs + job;  // pred[] read through the pointer
@@ -383,6 +398,8 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
     }
   }
   uint32_t evals = 0;
+  unsigned long long ph_t1 = 0, ph_sub = 0, ph_ex = 0, ph_it = 0, ph_stage = 0;
+  if (ph) ph_t1 = wall_clock64();
 
   // ---- full-pel: one candidate, evaluated by this wavefront -------------
   auto eval_full = [&](rv_mv mv) __attribute__((always_inline)) -> uint64_t {
@@ -518,6 +535,7 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
         load_box(wx, wy, S::D + H + 7, S::D + W + 7);
         __syncthreads();
         wvalid = true;
+        ph_stage++;
       }
       if (me.ok) {
         evals++;
@@ -625,7 +643,10 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
       if (pred_phase) {
         n = np - p0 < kDsWaves ? np - p0 : kDsWaves;
   #pragma unroll
-        for (int k = 0; k < kDsWaves; k++) c4[k] = jp->pred[p0 + (k < n ? k : 0)];
+        for (int k = 0; k < kDsWaves; k++) {
+          const int pi = p0 + (k < n ? k : 0);
+          c4[k] = has_pred0 && pi == 0 ? pred0 : jp->pred[pi];
+        }
       } else {
         n = kDsWaves;
         c4[0] = rv_mv{(int16_t)(center.row + radius), center.col};  // diamond_pattern
@@ -636,7 +657,12 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
       const int skip = pred_phase ? -1 : back;
       uint64_t c;
       if constexpr (SUB) {
+        const unsigned long long ta = ph ? wall_clock64() : 0;
         c = sub_round(c4, n, skip);
+        if (ph) {
+          ph_sub += wall_clock64() - ta;
+          ph_it++;
+        }
       } else {
         rv_mv mine = c4[0];
   #pragma unroll
@@ -644,8 +670,10 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
           if (wave == k) mine = c4[k];
         c = wave < n && wave != skip ? eval_full(mine) : ~0ull;
       }
+      const unsigned long long tb = ph ? wall_clock64() : 0;
       if (lane == 0) scost[iter & 1][wave] = c;
       __syncthreads();
+      if (ph) ph_ex += wall_clock64() - tb;
       uint64_t best = ~0ull;
       int bp = 0;
   #pragma unroll
@@ -695,6 +723,16 @@ __device__ __forceinline__ void ds_fast_body(const DsArgs &a, const int job) {
     ds_write(a, job, center, center_cost);
     chain_emit(a.next, job, a.n_per_ref, a.n / a.n_per_ref, center);
   }
+  if (ph) {
+    atomicAdd(&g_ds_ph[0], ph_t1 - ph_t0);
+    atomicAdd(&g_ds_ph[1], ph_sub);
+    atomicAdd(&g_ds_ph[2], ph_ex);
+    atomicAdd(&g_ds_ph[3], wall_clock64() - ph_t0);
+    atomicAdd(&g_ds_ph[4], ph_it);
+    atomicAdd(&g_ds_ph[5], 1ull);
+    atomicAdd(&g_ds_ph[6], ph_stage);
+  }
+  return center;
 }
 
 // The 4-wavefront search at 5 waves per SIMD (<= 96 VGPRs: the u8 sub-pel
@@ -725,7 +763,12 @@ template <typename Px, int W, int H, bool SUB>
 __global__ __launch_bounds__(kDsThreads) __attribute__((amdgpu_waves_per_eu(5))) void
 ds_fast_kernel(DsArgs a) {
   if (a.t0 && threadIdx.x == 0) atomicMin(a.t0, (unsigned long long)wall_clock64());
+  const unsigned long long ph_k = SUB && a.ph && a.alist && threadIdx.x == 0 ? wall_clock64() : 0;
   ds_fast_jobs<Px, W, H, SUB>(a);
+  if (ph_k) {
+    atomicAdd(&g_ds_ph[7], wall_clock64() - ph_k);
+    atomicAdd(&g_ds_ph[8], 1ull);
+  }
   if (a.t1) {
     __syncthreads();
     if (threadIdx.x == 0) atomicMax(a.t1, (unsigned long long)wall_clock64());
@@ -1450,23 +1493,31 @@ __device__ __forceinline__ void ds_grp16_pool(DsArgs a, int b, int gsz) {
   for (int o = (b * 4 + (int)(threadIdx.x >> 6)) * JPW; o < nord; o += gsz * 4 * JPW)
     ds_grp_body<Px, 16, false, false>(a, o + lane / G::L, nord);
 }
+// fuse: each F3 job's sub-pel search (f3s, the same job index and dirty
+// flag) right after its full-pel search in the same workgroup, from the
+// full-pel winner -- the round's separate sub-pel launch and its dependent
+// dispatch go away.
 template <typename Px>
-__device__ __forceinline__ void ds_fast64_pool(DsArgs a, int b, int gsz) {
+__device__ __forceinline__ void ds_fast64_pool(DsArgs a, DsArgs sa, bool fuse, int b, int gsz) {
   const int total = ds_list_total(a);
   for (int i = b; i < total; i += gsz) {
     const int job = __builtin_amdgcn_readfirstlane(ds_list_job(a, i));
     if (a.dirty && !a.dirty[job]) continue;
-    ds_fast_body<Px, 64, 64, false>(a, job);
+    const rv_mv best = ds_fast_body<Px, 64, 64, false>(a, job);
     __syncthreads();
+    if (fuse) {
+      ds_fast_body<Px, 64, 64, true>(sa, job, true, best);
+      __syncthreads();
+    }
   }
 }
 template <typename Px>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void ds_f2_f3_kernel(
-    DsArgs f2, DsArgs f3, int g2) {
+__global__ __launch_bounds__(256) void ds_f2_f3_kernel(
+    DsArgs f2, DsArgs f3, DsArgs f3s, int g2, int fuse) {
   if ((int)blockIdx.x < g2)
     ds_grp16_pool<Px>(f2, blockIdx.x, g2);
   else
-    ds_fast64_pool<Px>(f3, (int)blockIdx.x - g2, (int)gridDim.x - g2);
+    ds_fast64_pool<Px>(f3, f3s, fuse != 0, (int)blockIdx.x - g2, (int)gridDim.x - g2);
 }
 
 template <typename Px>
@@ -1512,7 +1563,9 @@ static bool ds_full_wave() {
 }
 
 template <typename Px, int W, int H, bool SUB>
-void launch_fast(const DsArgs &a, hipStream_t s) {
+void launch_fast(DsArgs a, hipStream_t s) {
+  static const bool phases = getenv("RAV1E_HIP_DS_PHASES") && getenv("RAV1E_HIP_DS_PHASES")[0] == '1';
+  a.ph = phases && SUB && a.alist ? 1 : 0;
   const unsigned grid = a.alist ? (unsigned)std::min(a.n, a.list_grid ? a.list_grid : ds_list_grid())
                                  : (unsigned)((a.n + 7) / 8 * 8);
   static const bool occ4 = [] {
@@ -1551,6 +1604,23 @@ bool try_fast(const DsArgs &a, hipStream_t s) {
 }  // namespace rv
 
 using namespace rv;
+
+// RAV1E_HIP_DS_PHASES=1: print the list-driven sub-pel searches' phase
+// times (g_ds_ph, microseconds per job / per workgroup) to stderr and clear them
+extern "C" int rv_ds_phase_dump(void) {
+  unsigned long long h[16];
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(h, HIP_SYMBOL(g_ds_ph), sizeof(h)) != hipSuccess)
+    return rv_set_error(RV_EHIP, "rv_ds_phase_dump");
+  const double us = 0.01;  // wall_clock64: 100 MHz
+  const double j = h[5] ? (double)h[5] : 1.0, w = h[8] ? (double)h[8] : 1.0;
+  fprintf(stderr,
+          "[ds phases] jobs %llu: setup %.2f us, stage+filter+SAD %.2f us, exchange %.2f us, "
+          "job %.2f us per job; %.2f iterations, %.2f stagings per job; workgroups %llu: %.2f us each\n",
+          h[5], h[0] * us / j, h[1] * us / j, h[2] * us / j, h[3] * us / j, h[4] / j, h[6] / j, h[8],
+          h[7] * us / w);
+  memset(h, 0, sizeof(h));
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_ds_ph), h, sizeof(h)) == hipSuccess ? RV_OK : rv_set_error(RV_EHIP, "rv_ds_phase_dump");
+}
 
 // Multi-reference form used by the replay driver: jobs [n_refs][n_per_ref],
 // job i searches refs[i / n_per_ref]; evals (optional) receives the
@@ -1635,7 +1705,7 @@ int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_
                      const rv_plane *refs, const rv_ds_job *jobs, rv_fs_result *out,
                      const uint8_t *dirty, const ChainNext *next, int n_refs, int n_per_ref,
                      int bit_depth, const int32_t *alist, const int32_t *acount, int list_grid,
-                     void *stream) {
+                     void *stream, const rv_ds_job *jobs_sub, rv_fs_result *out_sub) {
   if (!org_h || !refs_h || !org || !refs || n_refs < 1 || n_refs > RV_MAX_REFS || n_per_ref <= 0 ||
       !alist || !acount || org->hbd != org_h->hbd)
     return rv_set_error(RV_EINVAL, "rv_diamond_f2_f3: bad arguments");
@@ -1644,13 +1714,22 @@ int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_
           dirty_h);
   ds_fill(f3, org, refs, n_refs, jobs, n_per_ref, 64, out, bit_depth, alist, acount, 1, dirty);
   if (next) f3.next = *next;
+  // jobs_sub / out_sub (optional): F3's sub-pel searches fused behind the
+  // full-pel ones (SAD, no half-pel: the rounds' 64x64 diamond)
+  DsArgs f3s;
+  ds_fill(f3s, org, refs, n_refs, jobs_sub ? jobs_sub : jobs, n_per_ref, 64, out_sub ? out_sub : out,
+          bit_depth, alist, acount, 1, dirty);
+  f3s.subpel = 1;
+  static const bool phases = getenv("RAV1E_HIP_DS_PHASES") && getenv("RAV1E_HIP_DS_PHASES")[0] == '1';
+  f3s.ph = phases ? 1 : 0;
+  const int fuse = jobs_sub && out_sub ? 1 : 0;
   const int pool = list_grid ? list_grid : ds_list_grid();
   const int g2 = std::min(pool, (f2.n + 15) / 16), g3 = std::min(f3.n, pool);
   hipStream_t s = rv_resolve_stream(stream);
   if (org->hbd)
-    ds_f2_f3_kernel<uint16_t><<<g2 + g3, 256, 0, s>>>(f2, f3, g2);
+    ds_f2_f3_kernel<uint16_t><<<g2 + g3, 256, 0, s>>>(f2, f3, f3s, g2, fuse);
   else
-    ds_f2_f3_kernel<uint8_t><<<g2 + g3, 256, 0, s>>>(f2, f3, g2);
+    ds_f2_f3_kernel<uint8_t><<<g2 + g3, 256, 0, s>>>(f2, f3, f3s, g2, fuse);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }

@@ -77,7 +77,8 @@ int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_
                      const rv_plane *refs, const rv_ds_job *jobs, rv_fs_result *out,
                      const uint8_t *dirty, const rv::ChainNext *next, int n_refs, int n_per_ref,
                      int bit_depth, const int32_t *alist, const int32_t *acount, int list_grid,
-                     void *stream);
+                     void *stream, const rv_ds_job *jobs_sub = nullptr,
+                     rv_fs_result *out_sub = nullptr);
 // rv_deblock.hip
 int rv_deblock_plane_dev(const rv_plane *p, int pli, int width, int height, const uint8_t *d_lg,
                          const uint8_t *d_skip, int mi_stride, const uint8_t levels[4],
@@ -3952,6 +3953,10 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   static const bool f4_pair = !(getenv("RAV1E_HIP_F4_PAIR") && getenv("RAV1E_HIP_F4_PAIR")[0] == '0');
   // RAV1E_HIP_F2_F3=0: the rounds' F2 and F3 full-pel searches in two launches (A/B)
   static const bool f2_f3 = !(getenv("RAV1E_HIP_F2_F3") && getenv("RAV1E_HIP_F2_F3")[0] == '0');
+  // RAV1E_HIP_F3_FUSE=0: the rounds' F3 sub-pel searches in a launch of their
+  // own after F2 || F3 full-pel (A/B); fused, each F3 workgroup runs its
+  // job's sub-pel search right after the full-pel one
+  static const bool f3_fuse = !(getenv("RAV1E_HIP_F3_FUSE") && getenv("RAV1E_HIP_F3_FUSE")[0] == '0');
   auto f3_f4_list = [&](hipStream_t xs, uint32_t q) -> int {
     const int32_t *acnt = slot_cnt(q);
     int lg = q == q_first ? nr * g.R : 0;
@@ -3977,10 +3982,12 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
       RV_H(hipEventRecord(r->ev_rfork, xs));
       RV_H(hipStreamWaitEvent(x2, r->ev_rfork, 0));
     }
-    if (f2_f3 && !r->rs2) {  // F2 and F3 full-pel in one launch
+    const bool fused = f2_f3 && f3_fuse && !r->rs2 && !r->s6;
+    if (f2_f3 && !r->rs2) {  // F2 and F3 full-pel (+ F3 sub-pel when fused) in one launch
       RV_R(rv_diamond_f2_f3(&cur.hres, refs_h, r->jobs_half[lv], r->half, ma.f2dirty, &cur.y,
                             refs_y, r->jobs_full[lv], r->full, ma.f3dirty, &to_sub, g.R, nr, g.bd,
-                            mvl(q), acnt, lg, xs));
+                            mvl(q), acnt, lg, xs, fused ? r->jobs_sub[lv] : nullptr,
+                            fused ? r->sub : nullptr));
     } else {
       // F2 of the listed superblocks (their 4 quadrants per reference)
       RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0,
@@ -3991,11 +3998,13 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
                                    g.bd, r->full, nullptr, &to_sub, xs, nullptr, mvl(q), acnt,
                                    1, ma.f3dirty, lg));
     }
-    RV_R(kp_open(xs));
-    RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
-                                 r->sub, nullptr, nullptr, xs, nullptr, mvl(q), acnt, 1,
-                                 ma.f3dirty, lg, kp_acc, kp_ts()));
-    RV_R(kp_close(xs));
+    if (!fused) {
+      RV_R(kp_open(xs));
+      RV_R(rv_diamond_search_multi(&cur.y, refs_y, g.R, r->jobs_sub[lv], nr, 64, 64, 1, 0, 0, g.bd,
+                                   r->sub, nullptr, nullptr, xs, nullptr, mvl(q), acnt, 1,
+                                   ma.f3dirty, lg, kp_acc, kp_ts()));
+      RV_R(kp_close(xs));
+    }
     // the pools of the small per-round kernels: kRoundGrid for a run's first
     // round (most superblocks listed), RAV1E_HIP_ROUND_POOL (A/B) after it
     static const int round_pool = getenv("RAV1E_HIP_ROUND_POOL") ? std::max(1, atoi(getenv("RAV1E_HIP_ROUND_POOL")))
@@ -4095,17 +4104,21 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
           ma.count = slot_cnt(q);
           ma.pub = r->rr.pub(q);
           ma.list = mvl(q);
-          // after the run's first (full) check, each check covers only the
-          // dependents of the previous check's list (RAV1E_HIP_CHECK_INC=0:
-          // every check full, A/B); its grid from the last count read
-          static const bool inc = !(getenv("RAV1E_HIP_CHECK_INC") && getenv("RAV1E_HIP_CHECK_INC")[0] == '0');
-          if (inc && q != q_first) {
+          // RAV1E_HIP_CHECK_INC=1 (A/B, off: DESIGN.md §8): from the run's
+          // third check on, each check covers only the dependents of the
+          // previous check's list.  The second check follows the run's
+          // first round, which lists most superblocks: it stays full (their
+          // dependents, 4 per listed superblock, would take the incremental
+          // kernel several passes).  The incremental grid is the full
+          // check's: a short list leaves most workgroups empty, which exit
+          // at once, and a long one never loops.
+          static const bool inc = getenv("RAV1E_HIP_CHECK_INC") && getenv("RAV1E_HIP_CHECK_INC")[0] == '1';
+          if (inc && q > q_first + 1) {
             ma.plist = mvl(q - 1);
             ma.pcount = slot_cnt(q - 1);
             ma.epoch = r->mv_epoch;
             ma.tag = q + 1;
-            const int h = r->rr.last_count;
-            ma.inc_grid = h >= 0 ? std::max(1, (8 * h + 63) / 64) : 0;
+            ma.inc_grid = 0;
           } else {
             ma.plist = nullptr;
           }
