@@ -588,6 +588,8 @@ def main():
     kp = eng.kernel_probe() if probe else None
     if os.environ.get("RAV1E_HIP_DS_PHASES") == "1":  # diagnostic: the rounds' sub-pel phases
         R._check(R.lib().rv_ds_phase_dump(), "rv_ds_phase_dump")
+    if os.environ.get("RAV1E_HIP_RDO_PHASES") == "1":  # diagnostic: the rounds' F4 phases
+        R._check(R.lib().rv_rdo_phase_dump(), "rv_rdo_phase_dump")
     ent_stats = eng.entropy_stats() if ent else None
 
     # per-kernel times over the instrumented frames of the timed region

@@ -859,6 +859,10 @@ int rv_replay_kernel_probe(rv_replay *r, double *out, int cap);
  * filter + SAD, cost exchange, whole job; iterations, window stagings) on
  * the device clock; this prints the per-job means to stderr and clears them. */
 int rv_ds_phase_dump(void);
+/* Diagnostic (RAV1E_HIP_RDO_PHASES=1): the MV-stack rounds' F4 items
+ * (luma quads per set, chroma triples) add their phase spans; this prints
+ * the per-item means to stderr and clears them. */
+int rv_rdo_phase_dump(void);
 /* Candidate evaluations summed over the last min(frames, 64) coded frames:
  * out[0] F3 full-pel 64x64 diamond, out[1] F3 sub-pel 64x64 diamond, out[2]
  * = the number of frames summed (cap >= 3); with cap >= 5, out[3] / out[4]

@@ -33,6 +33,7 @@
 // rv_inv_txfm_add_batch, rv_cdef_moments_batch, rv_sse_batch) compute the
 // same values one stage per launch; the replay parity test pins the fused
 // kernel to the CPU replay, which chains the oracle's restatements of them.
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1164,6 +1165,22 @@ struct QuadLds {
   static constexpr int kBytes = cmax(4 * L::kSlot, 3 * kChromaPair(sizeof(Px)));
 };
 
+// RAV1E_HIP_RDO_PHASES=1 (diagnostic, var bit 4 on the list launches with a
+// pool hint, i.e. the MV-stack rounds): thread 0 of each workgroup adds its
+// item's phase spans (wall_clock64 ticks) into g_rdo_ph[set][k]: luma quads
+// k = 0 front (scan staging, MC, skip distortion, column DCT), 1 row DCT,
+// 2 quantize, 3 inverse rows, 4 inverse columns + reconstruction +
+// distortion, 5 items; chroma triples (set 2) k = 0 whole item, 5 items
+// Compiled in with -DRV_RDO_PHASES=1 only (a diagnostic build: the
+// timestamps cost scratch in the product kernels).
+#ifndef RV_RDO_PHASES
+#define RV_RDO_PHASES 0
+#endif
+__device__ unsigned long long g_rdo_ph[3][8];
+struct QuadPh {
+  unsigned long long t[5];
+};
+
 // var (RAV1E_HIP_RDO_VARIANT, A/B): bit 0 moves the skip distortion of the
 // scoring launches into the narrow phases (waves 1..3 during the row DCT,
 // wave 2 for wave 0's candidate during the inverse rows); bit 1 raises the
@@ -1171,7 +1188,8 @@ struct QuadLds {
 // The workgroup's four luma candidates t0 = 4 b .. 4 b + 3 (n: the tasks)
 template <typename Px, int MODE>
 __device__ __forceinline__ void rdo_quad_luma(const RdoArgs &luma, int b, int n, int var,
-                                              uint8_t *lds, const uint16_t *scan) {
+                                              uint8_t *lds, const uint16_t *scan,
+                                              QuadPh *ph = nullptr) {
   using L = typename QuadLds<Px>::L;
   constexpr int NPART = sizeof(Px) == 1 ? 2 : 4;
   const int wave = __builtin_amdgcn_readfirstlane(rv_tid() >> 6), lane = rv_tid() & 63;
@@ -1198,6 +1216,7 @@ __device__ __forceinline__ void rdo_quad_luma(const RdoArgs &luma, int b, int n,
   if (valid)
     luma_front<Px, NPART, MODE>(luma, luma.p[0], t, jb, true, slot(wave), pred(wave), !late_dist);
   __syncthreads();
+  if (RV_RDO_PHASES && ph) ph->t[1] = wall_clock64();
   if (wave == 0) {  // row DCT: lane = 16 * candidate + raster row
     if (prio) __builtin_amdgcn_s_setprio(2);
     const int q = lane >> 4;
@@ -1209,8 +1228,10 @@ __device__ __forceinline__ void rdo_quad_luma(const RdoArgs &luma, int b, int n,
     if (lane == 0) luma.p[0].out[(int64_t)jb.oi * 3 + 0] = d;
   }
   __syncthreads();
+  if (RV_RDO_PHASES && ph) ph->t[2] = wall_clock64();
   if (valid) luma_quantize(luma, luma.p[0], t, jb, true, fmid(wave), scan);
   __syncthreads();
+  if (RV_RDO_PHASES && ph) ph->t[3] = wall_clock64();
   if (wave < 2) {  // inverse rows: lane = 32 * (candidate & 1) + coded row
     if (prio) __builtin_amdgcn_s_setprio(2);
     const int q = 2 * wave + (lane >> 5), rr = lane & 31;
@@ -1232,6 +1253,7 @@ __device__ __forceinline__ void rdo_quad_luma(const RdoArgs &luma, int b, int n,
     if (lane == 0) luma.p[0].out[(int64_t)j0.oi * 3 + 0] = d;
   }
   __syncthreads();
+  if (RV_RDO_PHASES && ph) ph->t[4] = wall_clock64();
   if (valid) luma_back<Px, int16_t>(luma, luma.p[0], t, jb, true, imid(wave), pred(wave));
 }
 
@@ -1335,21 +1357,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
   const int pa = (ma + 1) / 2, pb = (mb + 1) / 2;
   const int e0 = (na + 3) / 4, e1 = e0 + (2 * pa + 2) / 3;
   const int e2 = e1 + (nb + 3) / 4, e3 = e2 + (2 * pb + 2) / 3;
+  const bool phd = RV_RDO_PHASES && (var & 16) && rv_tid() == 0;
   for (int b = blockIdx.x; b < e3; b += gridDim.x) {
+    QuadPh ph;
+    ph.t[0] = phd ? wall_clock64() : 0;
+    QuadPh *pp = phd ? &ph : nullptr;
+    int set = 2;
     if (b < e0) {
       stage_scan(scan, la.q_tx_index);
-      rdo_quad_luma<Px, MA>(la, b, na, var, lds, scan);
+      rdo_quad_luma<Px, MA>(la, b, na, var, lds, scan, pp);
+      set = MA;
     } else if (b < e1) {
       stage_scan(scan, ca.q_tx_index);
       rdo_quad_chroma<Px, MA>(ca, b - e0, pa, lds, scan);
     } else if (b < e2) {
       stage_scan(scan, lb.q_tx_index);
-      rdo_quad_luma<Px, MB>(lb, b - e1, nb, var, lds, scan);
+      rdo_quad_luma<Px, MB>(lb, b - e1, nb, var, lds, scan, pp);
+      set = MB;
     } else {
       stage_scan(scan, cb.q_tx_index);
       rdo_quad_chroma<Px, MB>(cb, b - e2, pb, lds, scan);
     }
     __syncthreads();  // the slots and the scan are reused by the next item
+    if (phd) {
+      const unsigned long long te = wall_clock64();
+      if (set < 2) {
+        for (int k = 0; k < 4; k++) atomicAdd(&g_rdo_ph[set][k], ph.t[k + 1] - ph.t[k]);
+        atomicAdd(&g_rdo_ph[set][4], te - ph.t[4]);
+      } else {
+        atomicAdd(&g_rdo_ph[2][0], te - ph.t[0]);
+      }
+      atomicAdd(&g_rdo_ph[set][5], 1ull);
+    }
   }
   if (kp_t && threadIdx.x == 0) atomicMax(kp_t + 1, (unsigned long long)wall_clock64());
 }
@@ -1570,10 +1609,12 @@ int rv_rdo_candidates_list(const RdoArgs *h, const RdoArgs *dev, int nsets, int 
   for (int k = 0; k < 2 * nsets; k++)
     if (!h[k].list || !h[k].count)
       return rv_set_error(RV_EINVAL, "rv_rdo_candidates_list: the sets must be list-driven");
-  static const int var = [] {
+  static const int var0 = [] {
     const char *e = getenv("RAV1E_HIP_RDO_VARIANT");
     return e ? atoi(e) : 3;
   }();
+  static const bool phases = getenv("RAV1E_HIP_RDO_PHASES") && getenv("RAV1E_HIP_RDO_PHASES")[0] == '1';
+  const int var = var0 | (phases && max_grid > 0 ? 16 : 0);
   // the full grid (every listed slot live) bounds the pool
   unsigned full = 0;
   for (int k = 0; k < nsets; k++)
@@ -1632,4 +1673,27 @@ int rv_rdo_blocks(const RdoArgs &a, bool luma, int nplanes, int n_tx_size, int h
   }
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
+}
+
+// RAV1E_HIP_RDO_PHASES=1: print the MV-stack rounds' F4 item phases
+// (g_rdo_ph, microseconds per item) to stderr and clear them
+extern "C" int rv_rdo_phase_dump(void) {
+  unsigned long long h[3][8];
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(h, HIP_SYMBOL(g_rdo_ph), sizeof(h)) != hipSuccess)
+    return rv_set_error(RV_EHIP, "rv_rdo_phase_dump");
+  const double us = 0.01;  // wall_clock64: 100 MHz
+  static const char *kName[2] = {"single", "compound"};
+  for (int m = 0; m < 2; m++) {
+    const double n = h[m][5] ? (double)h[m][5] : 1.0;
+    fprintf(stderr,
+            "[f4 phases] %s luma quads %llu: front %.2f, row DCT %.2f, quantize %.2f, inverse rows %.2f, "
+            "back %.2f us per quad\n",
+            kName[m], h[m][5], h[m][0] * us / n, h[m][1] * us / n, h[m][2] * us / n, h[m][3] * us / n,
+            h[m][4] * us / n);
+  }
+  fprintf(stderr, "[f4 phases] chroma triples %llu: %.2f us each\n", h[2][5],
+          h[2][0] * us / (h[2][5] ? (double)h[2][5] : 1.0));
+  memset(h, 0, sizeof(h));
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_rdo_ph), h, sizeof(h)) == hipSuccess ? RV_OK
+                                                                           : rv_set_error(RV_EHIP, "rv_rdo_phase_dump");
 }
