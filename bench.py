@@ -136,7 +136,7 @@ def coarse_windows(W, H, R, scale, tiling, group):
 ROCPROF_NAMES = {
     "full_search": "fs16_sea_kernel_{pxs}",
     "diamond_fullpel_64": "ds_fast_kernel<{px}, 64, 64, false>",
-    "diamond_subpel_64": "ds_fast_kernel<{px}, 64, 64, true>",
+    "diamond_subpel_64": "ds_fast_kernel<{px}, 64, 64, true>",  # (+ ds_f2_f3_kernel: fused rounds)
     "rdo_candidates": "rdo_quad_list_kernel<{px}, 0, 0>",
     "rdo_compound": "rdo_quad_list_kernel<{px}, 1, 1>",
     "rdo_commit": "rdo_quad_kernel<{px}, 2>",
@@ -692,12 +692,13 @@ def main():
 
     def family_entry(sub):
         """Every instance of a kernel in the committed trace (template
-        instances are traced as separate names) aggregated per coded frame:
-        ms, launches, mean launch, and HBM bytes / SQ ratios weighted by
-        launches."""
+        instances are traced as separate names; `sub`: a name substring or a
+        tuple of them) aggregated per coded frame: ms, launches, mean launch,
+        and HBM bytes / SQ ratios weighted by launches."""
         if not pj:
             return None
-        es = [v for k, v in pj["kernels"].items() if sub in k]
+        subs = sub if isinstance(sub, tuple) else (sub,)
+        es = [v for k, v in pj["kernels"].items() if any(x in k for x in subs)]
         if not es:
             return None
         lpf = sum(e["launches_per_frame"] for e in es)
@@ -736,12 +737,14 @@ def main():
 
     roofs = {}
     if kp is not None and kp[0] > 0:
-        # F3's sub-pel search, ds_fast_kernel<64, 64, sub-pel>: the batched MC +
-        # distortion kernel north_star names (every candidate a 6-tap
-        # put_8tap of its 71 x 71 window, then SAD against the source).
-        # Live: every launch of the instrumented timed frames (round 0 and the
-        # MV-stack rounds) bracketed by HIP events on the stream it runs on;
-        # its units: the candidate evaluations those launches counted.
+        # F3's sub-pel search: the batched MC + distortion kernel north_star
+        # names (every candidate a 6-tap put_8tap of its 71 x 71 window, then
+        # SAD against the source) -- ds_fast_kernel<64, 64, sub-pel> for round
+        # 0 and a run's first round, and inside ds_f2_f3_kernel (fused behind
+        # F2 || F3 full-pel) for the later MV-stack rounds.  Live: every such
+        # launch of the instrumented timed frames; its units: the sub-pel
+        # candidate evaluations those launches counted.  The fused launches'
+        # F2 and full-pel searches are not counted: achieved is a lower bound.
         nl = float(kp[0])
         # the launch's duration: its span on the device clock (the first
         # workgroup's start to the last one's end, what rocprofv3 times);
@@ -752,7 +755,8 @@ def main():
         cand_b = (71 * 71 + 64 * 64) * px + 4  # fused MC + dist candidate
         bytes_l = kp[2] / nl * cand_b
         ach = bytes_l / avg_s / 1e9
-        roof = {"kernel": "diamond_subpel_64", "name": f"ds_fast_kernel<{pxn}, 64, 64, true>",
+        roof = {"kernel": "diamond_subpel_64",
+                "name": f"ds_fast_kernel<{pxn}, 64, 64, true> + ds_f2_f3_kernel<{pxn}> (fused rounds)",
                 "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
                 "avg_launch_ms": round(avg_s * 1e3, 5),
@@ -765,9 +769,12 @@ def main():
                              "rule": "(64+7)^2 b window + 64^2 b source + 4 (SURVEY.md §8d)"},
                 "units_per_launch": round(kp[2] / nl, 1), "jobs_per_launch": round(kp[3] / nl, 1),
                 "launches_probed": int(nl),
-                "launch": "every F3 sub-pel launch (round 0 and the MV-stack rounds) of the "
-                          "instrumented timed frames, HIP event pairs on its stream"}
-        attach_trace(roof, family_entry(f"ds_fast_kernel<{pxn}, 64, 64, true>"), bytes_l, avg_s, ach)
+                "launch": "every launch holding F3 sub-pel searches (round 0, each run's first "
+                          "round, the fused F2 || F3 launches of the later MV-stack rounds) of "
+                          "the instrumented timed frames; the fused launches' F2 and full-pel "
+                          "searches are not counted (achieved is a lower bound)"}
+        attach_trace(roof, family_entry((f"ds_fast_kernel<{pxn}, 64, 64, true>",
+                                         f"ds_f2_f3_kernel<{pxn}>")), bytes_l, avg_s, ach)
         roofs["diamond_subpel_64"] = roof
     if kp is not None and len(kp) >= 12 and kp[5] > 0:
         # F4, rdo_quad_list_kernel: every inter candidate's fused chain (MC,

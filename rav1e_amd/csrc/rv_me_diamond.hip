@@ -1514,10 +1514,17 @@ __device__ __forceinline__ void ds_fast64_pool(DsArgs a, DsArgs sa, bool fuse, i
 template <typename Px>
 __global__ __launch_bounds__(256) void ds_f2_f3_kernel(
     DsArgs f2, DsArgs f3, DsArgs f3s, int g2, int fuse) {
+  // the kernel probe (fused launches): the launch's device-clock span; the
+  // sub-pel bodies count their candidates into f3s.eval_acc
+  if (f3s.t0 && threadIdx.x == 0) atomicMin(f3s.t0, (unsigned long long)wall_clock64());
   if ((int)blockIdx.x < g2)
     ds_grp16_pool<Px>(f2, blockIdx.x, g2);
   else
     ds_fast64_pool<Px>(f3, f3s, fuse != 0, (int)blockIdx.x - g2, (int)gridDim.x - g2);
+  if (f3s.t1) {
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(f3s.t1, (unsigned long long)wall_clock64());
+  }
 }
 
 template <typename Px>
@@ -1705,7 +1712,8 @@ int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_
                      const rv_plane *refs, const rv_ds_job *jobs, rv_fs_result *out,
                      const uint8_t *dirty, const ChainNext *next, int n_refs, int n_per_ref,
                      int bit_depth, const int32_t *alist, const int32_t *acount, int list_grid,
-                     void *stream, const rv_ds_job *jobs_sub, rv_fs_result *out_sub) {
+                     void *stream, const rv_ds_job *jobs_sub, rv_fs_result *out_sub,
+                     uint32_t *eval_acc, unsigned long long *t01) {
   if (!org_h || !refs_h || !org || !refs || n_refs < 1 || n_refs > RV_MAX_REFS || n_per_ref <= 0 ||
       !alist || !acount || org->hbd != org_h->hbd)
     return rv_set_error(RV_EINVAL, "rv_diamond_f2_f3: bad arguments");
@@ -1723,6 +1731,13 @@ int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_
   static const bool phases = getenv("RAV1E_HIP_DS_PHASES") && getenv("RAV1E_HIP_DS_PHASES")[0] == '1';
   f3s.ph = phases ? 1 : 0;
   const int fuse = jobs_sub && out_sub ? 1 : 0;
+  if (fuse) {  // the kernel probe (null: off)
+    f3s.eval_acc = eval_acc;
+    if (t01) {
+      f3s.t0 = t01;
+      f3s.t1 = t01 + 1;
+    }
+  }
   const int pool = list_grid ? list_grid : ds_list_grid();
   const int g2 = std::min(pool, (f2.n + 15) / 16), g3 = std::min(f3.n, pool);
   hipStream_t s = rv_resolve_stream(stream);

@@ -1270,6 +1270,26 @@ __device__ __forceinline__ void rdo_quad_chroma(const RdoArgs &chroma, int c, in
                             reinterpret_cast<Px *>(w + 2 * 32 * 33 * 4), scan, pairs);
 }
 
+// The MV-stack rounds' chroma (var bit 5): blocks 4 c .. 4 c + 3 of the
+// launch (plane U's n, then V's), one per wavefront on all 64 lanes (two
+// lanes per column in MC, twice the lanes in the residual, quantizer and
+// distortion loops).  A round launch costs its slowest item, and a
+// wavefront holding two blocks (one per half) was it: 61 us per triple
+// against 55 us per single-reference luma quad (profiles/r06_phases.txt).
+template <typename Px, int MODE>
+__device__ __forceinline__ void rdo_quad_chroma4(const RdoArgs &chroma, int c, int n, uint8_t *lds,
+                                                 const uint16_t *scan) {
+  constexpr int kSlab = rdo_slab_bytes<Px, 32>();
+  static_assert(4 * (kSlab + 32 * 32 * (int)sizeof(Px)) <= QuadLds<Px>::kBytes, "4 chroma slabs");
+  const int wave = __builtin_amdgcn_readfirstlane(rv_tid() >> 6);
+  const int k = 4 * c + wave;
+  if (k >= 2 * n) return;
+  const int plane = k >= n ? 1 : 0, i = k - plane * n;
+  uint8_t *w = lds + wave * (kSlab + 32 * 32 * (int)sizeof(Px));
+  rdo_cand_body<Px, 32, 64, MODE>(chroma, chroma.p[plane], i, true, reinterpret_cast<int32_t *>(w),
+                                  reinterpret_cast<Px *>(w + kSlab), scan);
+}
+
 // One workgroup b of the quad launch: four luma candidates, or three
 // chroma pairs past nquads.  The arguments come by value: bound by
 // reference to the kernel's arguments they were copied to scratch memory
@@ -1355,8 +1375,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
     }
   }
   const int pa = (ma + 1) / 2, pb = (mb + 1) / 2;
-  const int e0 = (na + 3) / 4, e1 = e0 + (2 * pa + 2) / 3;
-  const int e2 = e1 + (nb + 3) / 4, e3 = e2 + (2 * pb + 2) / 3;
+  const bool c4 = (var & 32) != 0;  // chroma: a block per wavefront (rounds)
+  const int e0 = (na + 3) / 4, e1 = e0 + (c4 ? (2 * ma + 3) / 4 : (2 * pa + 2) / 3);
+  const int e2 = e1 + (nb + 3) / 4, e3 = e2 + (c4 ? (2 * mb + 3) / 4 : (2 * pb + 2) / 3);
   const bool phd = RV_RDO_PHASES && (var & 16) && rv_tid() == 0;
   for (int b = blockIdx.x; b < e3; b += gridDim.x) {
     QuadPh ph;
@@ -1369,14 +1390,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void r
       set = MA;
     } else if (b < e1) {
       stage_scan(scan, ca.q_tx_index);
-      rdo_quad_chroma<Px, MA>(ca, b - e0, pa, lds, scan);
+      if (c4)
+        rdo_quad_chroma4<Px, MA>(ca, b - e0, ma, lds, scan);
+      else
+        rdo_quad_chroma<Px, MA>(ca, b - e0, pa, lds, scan);
     } else if (b < e2) {
       stage_scan(scan, lb.q_tx_index);
       rdo_quad_luma<Px, MB>(lb, b - e1, nb, var, lds, scan, pp);
       set = MB;
     } else {
       stage_scan(scan, cb.q_tx_index);
-      rdo_quad_chroma<Px, MB>(cb, b - e2, pb, lds, scan);
+      if (c4)
+        rdo_quad_chroma4<Px, MB>(cb, b - e2, mb, lds, scan);
+      else
+        rdo_quad_chroma<Px, MB>(cb, b - e2, pb, lds, scan);
     }
     __syncthreads();  // the slots and the scan are reused by the next item
     if (phd) {
@@ -1614,12 +1641,15 @@ int rv_rdo_candidates_list(const RdoArgs *h, const RdoArgs *dev, int nsets, int 
     return e ? atoi(e) : 3;
   }();
   static const bool phases = getenv("RAV1E_HIP_RDO_PHASES") && getenv("RAV1E_HIP_RDO_PHASES")[0] == '1';
-  const int var = var0 | (phases && max_grid > 0 ? 16 : 0);
+  // RAV1E_HIP_F4_CHROMA4=0: the rounds' chroma two blocks per wavefront (A/B)
+  static const bool chroma4 = !(getenv("RAV1E_HIP_F4_CHROMA4") && getenv("RAV1E_HIP_F4_CHROMA4")[0] == '0');
+  const int var = var0 | (phases && max_grid > 0 ? 16 : 0) | (chroma4 && max_grid > 0 ? 32 : 0);
   // the full grid (every listed slot live) bounds the pool
   unsigned full = 0;
   for (int k = 0; k < nsets; k++)
     full += (unsigned)((h[2 * k].n_tx + 3) / 4) +
-            (unsigned)(2 * ((h[2 * k + 1].n_tx + 1) / 2) + 2) / 3;
+            ((var & 32) ? (unsigned)(2 * h[2 * k + 1].n_tx + 3) / 4
+                        : (unsigned)(2 * ((h[2 * k + 1].n_tx + 1) / 2) + 2) / 3);
   unsigned grid = std::min(full, (unsigned)rdo_f4_pool());
   if (max_grid > 0) grid = std::min(grid, (unsigned)max_grid);
   if (grid == 0) return RV_OK;

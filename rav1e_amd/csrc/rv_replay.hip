@@ -78,7 +78,8 @@ int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_
                      const uint8_t *dirty, const rv::ChainNext *next, int n_refs, int n_per_ref,
                      int bit_depth, const int32_t *alist, const int32_t *acount, int list_grid,
                      void *stream, const rv_ds_job *jobs_sub = nullptr,
-                     rv_fs_result *out_sub = nullptr);
+                     rv_fs_result *out_sub = nullptr, uint32_t *eval_acc = nullptr,
+                     unsigned long long *t01 = nullptr);
 // rv_deblock.hip
 int rv_deblock_plane_dev(const rv_plane *p, int pli, int width, int height, const uint8_t *d_lg,
                          const uint8_t *d_skip, int mi_stride, const uint8_t levels[4],
@@ -3984,10 +3985,14 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
     }
     const bool fused = f2_f3 && f3_fuse && !r->rs2 && !r->s6;
     if (f2_f3 && !r->rs2) {  // F2 and F3 full-pel (+ F3 sub-pel when fused) in one launch
+      // fused: the probe brackets the launch (its sub-pel candidates, its span)
+      if (fused) RV_R(kp_open(xs));
       RV_R(rv_diamond_f2_f3(&cur.hres, refs_h, r->jobs_half[lv], r->half, ma.f2dirty, &cur.y,
                             refs_y, r->jobs_full[lv], r->full, ma.f3dirty, &to_sub, g.R, nr, g.bd,
                             mvl(q), acnt, lg, xs, fused ? r->jobs_sub[lv] : nullptr,
-                            fused ? r->sub : nullptr));
+                            fused ? r->sub : nullptr, fused ? kp_acc : nullptr,
+                            fused ? kp_ts() : nullptr));
+      if (fused) RV_R(kp_close(xs));
     } else {
       // F2 of the listed superblocks (their 4 quadrants per reference)
       RV_R(rv_diamond_search_multi(&cur.hres, refs_h, g.R, r->jobs_half[lv], nr * 4, 16, 16, 0, 0,
