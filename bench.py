@@ -566,7 +566,9 @@ def main():
     gop = len(RP.GOP_SCALES)
     (eng if paired else hip).set_timing(TIMING_STRIDE, gop)
     ent = not args.no_entropy
-    probe = world == 1 and speed == 10 and hasattr(eng, "set_kernel_probe")
+    # RAV1E_BENCH_NO_PROBE=1: no kernel probe (A/B of the probe's own cost)
+    probe = (world == 1 and speed == 10 and hasattr(eng, "set_kernel_probe")
+             and os.environ.get("RAV1E_BENCH_NO_PROBE") != "1")
     la_cnt = {}
 
     def before():

@@ -1513,17 +1513,19 @@ __device__ __forceinline__ void ds_fast64_pool(DsArgs a, DsArgs sa, bool fuse, i
 }
 template <typename Px>
 __global__ __launch_bounds__(256) void ds_f2_f3_kernel(
-    DsArgs f2, DsArgs f3, DsArgs f3s, int g2, int fuse) {
-  // the kernel probe (fused launches): the launch's device-clock span; the
-  // sub-pel bodies count their candidates into f3s.eval_acc
-  if (f3s.t0 && threadIdx.x == 0) atomicMin(f3s.t0, (unsigned long long)wall_clock64());
+    DsArgs f2, DsArgs f3, DsArgs f3s, int g2, int fuse, unsigned long long *t01) {
+  // the kernel probe (fused launches, t01 non-null): the launch's
+  // device-clock span; the sub-pel bodies count their candidates into
+  // f3s.eval_acc.  (t01 is a parameter of its own: reading it out of an
+  // argument struct made the compiler copy the struct to scratch, 704 B.)
+  if (t01 && threadIdx.x == 0) atomicMin(t01, (unsigned long long)wall_clock64());
   if ((int)blockIdx.x < g2)
     ds_grp16_pool<Px>(f2, blockIdx.x, g2);
   else
     ds_fast64_pool<Px>(f3, f3s, fuse != 0, (int)blockIdx.x - g2, (int)gridDim.x - g2);
-  if (f3s.t1) {
+  if (t01) {
     __syncthreads();
-    if (threadIdx.x == 0) atomicMax(f3s.t1, (unsigned long long)wall_clock64());
+    if (threadIdx.x == 0) atomicMax(t01 + 1, (unsigned long long)wall_clock64());
   }
 }
 
@@ -1731,20 +1733,15 @@ int rv_diamond_f2_f3(const rv_plane *org_h, const rv_plane *refs_h, const rv_ds_
   static const bool phases = getenv("RAV1E_HIP_DS_PHASES") && getenv("RAV1E_HIP_DS_PHASES")[0] == '1';
   f3s.ph = phases ? 1 : 0;
   const int fuse = jobs_sub && out_sub ? 1 : 0;
-  if (fuse) {  // the kernel probe (null: off)
-    f3s.eval_acc = eval_acc;
-    if (t01) {
-      f3s.t0 = t01;
-      f3s.t1 = t01 + 1;
-    }
-  }
+  if (fuse) f3s.eval_acc = eval_acc;  // the kernel probe (null: off)
+  unsigned long long *ts = fuse ? t01 : nullptr;
   const int pool = list_grid ? list_grid : ds_list_grid();
   const int g2 = std::min(pool, (f2.n + 15) / 16), g3 = std::min(f3.n, pool);
   hipStream_t s = rv_resolve_stream(stream);
   if (org->hbd)
-    ds_f2_f3_kernel<uint16_t><<<g2 + g3, 256, 0, s>>>(f2, f3, f3s, g2, fuse);
+    ds_f2_f3_kernel<uint16_t><<<g2 + g3, 256, 0, s>>>(f2, f3, f3s, g2, fuse, ts);
   else
-    ds_f2_f3_kernel<uint8_t><<<g2 + g3, 256, 0, s>>>(f2, f3, f3s, g2, fuse);
+    ds_f2_f3_kernel<uint8_t><<<g2 + g3, 256, 0, s>>>(f2, f3, f3s, g2, fuse, ts);
   RV_HIP_CHECK_LAUNCH();
   return RV_OK;
 }
