@@ -1298,6 +1298,11 @@ struct rv_replay {
   static constexpr int kKp = 512;
   std::vector<hipEvent_t> kp_ev[kProbes];
   long kp_n[kProbes] = {0, 0}, kp_done[kProbes] = {0, 0}, kp_base[kProbes] = {0, 0};
+  // span slots [kp_n, kp_init) are initialised (start = max, end = 0): one
+  // copy per kKpInit launches instead of one per launch (each a dependent
+  // blit on the round's stream: the probe cost 2.5 % of the line, r06np)
+  long kp_init[kProbes] = {0, 0};
+  static constexpr int kKpInit = 256;
   double kp_ms[kProbes] = {0.0, 0.0}, kp_dev_ms[kProbes] = {0.0, 0.0};
   uint32_t *kp_cnt[kProbes] = {nullptr, nullptr};  // device [kKpCnt] each
   // ... and each launch's span on the device clock: [kKp][2] (first
@@ -1315,19 +1320,31 @@ void *dalloc(rv_replay *r, size_t bytes) {
   return p;
 }
 
-// kernel probe p's pairs [kp_done, upto): their elapsed times summed
+// kernel probe p's pairs [kp_done, upto): their elapsed times and device
+// spans summed (the spans in at most two copies)
 hipError_t kp_harvest(rv_replay *r, int p, long upto) {
-  for (; r->kp_done[p] < upto; r->kp_done[p]++) {
-    const size_t i = 2 * (size_t)(r->kp_done[p] % rv_replay::kKp);
+  const long d0 = r->kp_done[p], n = upto - d0;
+  if (n <= 0) return hipSuccess;
+  constexpr long K = rv_replay::kKp;
+  for (long k = d0; k < upto; k++) {
+    const size_t i = 2 * (size_t)(k % K);
     hipError_t e = hipEventSynchronize(r->kp_ev[p][i + 1]);
     float ms = 0.f;
     if (e == hipSuccess) e = hipEventElapsedTime(&ms, r->kp_ev[p][i], r->kp_ev[p][i + 1]);
-    unsigned long long t[2] = {0, 0};
-    if (e == hipSuccess) e = hipMemcpy(t, r->kp_ts[p] + i, sizeof(t), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return e;
     r->kp_ms[p] += ms;
-    if (t[1] > t[0]) r->kp_dev_ms[p] += (double)(t[1] - t[0]) * r->kp_tick_ms;
   }
+  std::vector<unsigned long long> t(2 * (size_t)n);
+  const long s0 = d0 % K, first = std::min(n, K - s0);
+  hipError_t e = hipMemcpy(t.data(), r->kp_ts[p] + 2 * s0, 2 * sizeof(unsigned long long) * first,
+                           hipMemcpyDeviceToHost);
+  if (e == hipSuccess && n > first)
+    e = hipMemcpy(t.data() + 2 * first, r->kp_ts[p], 2 * sizeof(unsigned long long) * (n - first),
+                  hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  for (long k = 0; k < n; k++)
+    if (t[2 * k + 1] > t[2 * k]) r->kp_dev_ms[p] += (double)(t[2 * k + 1] - t[2 * k]) * r->kp_tick_ms;
+  r->kp_done[p] = upto;
   return hipSuccess;
 }
 
@@ -3495,12 +3512,26 @@ int rv_replay_frame(rv_replay *r, rv_replay_frame_info *info) {
   uint32_t *kp_f4 = kp ? r->kp_cnt[1] : nullptr;
   auto kp_open = [&](hipStream_t xs, int p = 0) -> int {
     if (!kp) return RV_OK;
-    if (r->kp_n[p] - r->kp_done[p] >= rv_replay::kKp)
-      RV_H(kp_harvest(r, p, r->kp_n[p] - rv_replay::kKp + 1));
-    // the launch's device-clock span slot: start = max, end = 0
-    static const unsigned long long init[2] = {~0ull, 0ull};
-    RV_H(hipMemcpyAsync(r->kp_ts[p] + 2 * (size_t)(r->kp_n[p] % rv_replay::kKp), init, sizeof(init),
-                        hipMemcpyHostToDevice, xs));
+    if (r->kp_n[p] >= r->kp_init[p]) {
+      // the next kKpInit launches' device-clock span slots: start = max,
+      // end = 0, in one or two copies; their previous pairs harvested first
+      constexpr long K = rv_replay::kKp, C = rv_replay::kKpInit;
+      static_assert(C <= K, "the initialised slots fit the ring");
+      const long need = r->kp_n[p] + C - K;
+      if (r->kp_done[p] < need) RV_H(kp_harvest(r, p, need));
+      static const std::vector<unsigned long long> init = [] {
+        std::vector<unsigned long long> v(2 * (size_t)C, 0ull);
+        for (long i = 0; i < C; i++) v[2 * (size_t)i] = ~0ull;
+        return v;
+      }();
+      const long s0 = r->kp_n[p] % K, first = std::min(C, K - s0);
+      RV_H(hipMemcpyAsync(r->kp_ts[p] + 2 * s0, init.data(), 2 * sizeof(unsigned long long) * first,
+                          hipMemcpyHostToDevice, xs));
+      if (C > first)
+        RV_H(hipMemcpyAsync(r->kp_ts[p], init.data(), 2 * sizeof(unsigned long long) * (C - first),
+                            hipMemcpyHostToDevice, xs));
+      r->kp_init[p] = r->kp_n[p] + C;
+    }
     RV_H(hipEventRecord(r->kp_ev[p][2 * (size_t)(r->kp_n[p] % rv_replay::kKp)], xs));
     return RV_OK;
   };
